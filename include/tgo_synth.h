@@ -1,0 +1,30 @@
+/*
+ * tgo_synth.h — synthetic inputs for the bench and the parity tests (not part of the
+ * reference boundary; the reference reads real edgestore rows).
+ *
+ * RMAT / Graph500 Kronecker generator (A,B,C,D = 0.57,0.19,0.19,0.05), counter-based
+ * splitmix64 so any edge range can be generated independently and in parallel, followed
+ * by a seeded vertex relabel.  Duplicates and self-loops are kept (a Titan MULTI label
+ * stores them).  Weights: w = 1 + (splitmix64(seed ^ edge_index) mod 255).
+ */
+#ifndef TGO_SYNTH_H
+#define TGO_SYNTH_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Fill src/dst (m entries each, m = edge_factor << scale) and optionally weight.
+ * Edges [edge_begin, edge_begin + count) of the stream are produced. */
+int tgo_rmat_edges(int32_t scale, int32_t edge_factor, uint64_t seed, int64_t edge_begin,
+                   int64_t count, int32_t* src, int32_t* dst, int32_t* weight, int32_t threads);
+
+/* Undirected degree (out + in) histogram helper and seeded root selection among vertices
+ * of degree > 0 (Graph500 style): writes `nroots` distinct dense ids. */
+int tgo_pick_roots(int64_t n, int64_t m, const int32_t* src, const int32_t* dst, uint64_t seed,
+                   int32_t nroots, int64_t* roots_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,247 @@
+/*
+ * titan_gpu_olap.h — C-ABI of the MI355X-native OLAP traversal engine for Titan.
+ *
+ * This is the drop-in boundary for Titan's in-JVM OLAP executor ("Fulgora"):
+ *
+ *   graph.compute()                          TitanBlueprintsGraph.java:133-146
+ *     .program(VertexProgram)                FulgoraGraphComputer.java:103-107
+ *     .workers(n)                            FulgoraGraphComputer.java:96-100
+ *     .submit().get()                        FulgoraGraphComputer.java:117-311
+ *
+ * The Java side keeps TitanGraphComputer (titan-core/.../core/TitanGraphComputer.java:8-43)
+ * and the edgestore scan (Backend.buildEdgeScanJob(), Backend.java:336-355 →
+ * StandardScanner.Builder, StandardScanner.java:100-209).  A CSR-collecting
+ * VertexScanJob hands every scanned row to tgo_load_rows() in the reference's own
+ * StaticArrayEntryList layout (StaticArrayEntryList.java:15-50); the superstep loop
+ * of FulgoraGraphComputer.submit (:151-189) and the per-vertex gather of
+ * VertexMemoryHandler.receiveMessages (VertexMemoryHandler.java:77-103) are replaced
+ * by one call per vertex program (tgo_bfs / tgo_sssp / tgo_pagerank / tgo_walkcount)
+ * executed by hand-written HIP kernels for gfx950 over a device-resident adjacency.
+ *
+ * ABI conventions
+ *  - Plain C types only; no C++ exceptions cross this boundary.
+ *  - Every call returns a tgo_status (0 = ok, < 0 = error class);
+ *    tgo_last_error() returns a message for the last failing call on that ctx.
+ *    This mirrors the reference's error behaviour: TitanException /
+ *    IllegalArgumentException thrown from submit().get() (OLAPTest.java:222-239,
+ *    FulgoraGraphComputer.java:165-174).
+ *  - The caller owns every host buffer; buffers are read during the call and never
+ *    retained.  Output buffers are caller-allocated (n = tgo_num_vertices()).
+ *  - Device memory is owned by the ctx and freed by tgo_destroy().
+ *  - A ctx is used by one host thread at a time; several ctxs may coexist.
+ *  - The library owns one HIP stream per ctx unless tgo_options.stream is given.
+ *  - There is NO CPU fallback: when no gfx950 device is usable, tgo_create() fails
+ *    with TGO_E_HIP.
+ */
+#ifndef TITAN_GPU_OLAP_H
+#define TITAN_GPU_OLAP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TGO_ABI_VERSION 1
+
+typedef struct tgo_ctx tgo_ctx;
+
+typedef enum {
+    TGO_OK = 0,
+    TGO_E_INVALID = -1,     /* bad argument (Preconditions.checkArgument)               */
+    TGO_E_HIP = -2,         /* HIP runtime error / no usable device                      */
+    TGO_E_OOM = -3,         /* device or host allocation failed                          */
+    TGO_E_CODEC = -4,       /* malformed edgestore entry (EdgeSerializer.parseRelation)  */
+    TGO_E_STATE = -5,       /* call order violated (e.g. program before load)            */
+    TGO_E_PROGRAM = -6,     /* vertex program failure: the reference throws in execute() */
+    TGO_E_UNSUPPORTED = -7, /* feature outside the implemented scope (e.g. vertex cuts)  */
+    TGO_E_COMM = -8         /* multi-GPU exchange failure                                */
+} tgo_status;
+
+/* Incident direction of a MessageScope.Local(__::outE / __::inE / __::bothE).
+ * Messages flow AGAINST the declared direction: a receiver gathers over the
+ * reversed incident step (FulgoraUtil.java:49-62, reversal at :57). */
+typedef enum { TGO_SCOPE_OUT_E = 0, TGO_SCOPE_IN_E = 1, TGO_SCOPE_BOTH_E = 2 } tgo_scope;
+
+/* Multiplicity of an edge label (core/Multiplicity.java:21-75). Decides where the
+ * other vertex id sits inside an edge entry (EdgeSerializer.java:90-110). */
+typedef enum {
+    TGO_MULTI = 0, TGO_SIMPLE = 1, TGO_MANY2ONE = 2, TGO_ONE2MANY = 3, TGO_ONE2ONE = 4
+} tgo_multiplicity;
+
+/* Datatypes of inline edge properties the decoder can read or skip
+ * (graphdb/database/serialize/attribute/ IntegerSerializer.java, LongSerializer.java, ...). */
+typedef enum {
+    TGO_DT_BYTE = 1, TGO_DT_SHORT = 2, TGO_DT_INTEGER = 3, TGO_DT_LONG = 4,
+    TGO_DT_FLOAT = 5, TGO_DT_DOUBLE = 6, TGO_DT_BOOLEAN = 7
+} tgo_datatype;
+
+typedef struct {
+    int32_t abi_version;       /* must be TGO_ABI_VERSION                                  */
+    int32_t device;            /* HIP device ordinal                                       */
+    int32_t partition_bits;    /* log2(cluster.max-partitions); reference default 5
+                                  (GraphDatabaseConfiguration.java:665; VertexIDAssigner.java:73-74) */
+    int32_t host_threads;      /* CSR-assembly threads (0 = hardware concurrency)          */
+    int64_t hard_query_limit;  /* QueryContainer.DEFAULT_HARD_QUERY_LIMIT = 100000 (QueryContainer.java:28) */
+    void*   stream;            /* optional external hipStream_t; NULL = ctx-owned stream   */
+} tgo_options;
+
+/* ---- Edgestore input (tgo_load_rows) ------------------------------------------------
+ * Rows are passed exactly as the scan hands them to VertexJobConverter.process
+ * (VertexJobConverter.java:109-129): per row, the 8-byte key and the row's entry list
+ * in StaticArrayEntryList form (StaticArrayEntryList.java:15-50), concatenated over rows:
+ *   row_keys[r]                 key as StaticBuffer.getLong(0) (big-endian long)
+ *   row_entry_begin[r..r+1)     entry index range of row r                (nrows+1)
+ *   row_byte_begin[r]           byte offset of row r's data in entry_bytes (nrows+1)
+ *   entry_limit_valpos[e]       (limit << 32) | valuePos, limit = end offset of entry e
+ *                               relative to row_byte_begin[r] (StaticArrayEntryList:46-56)
+ * Entries of a row are in column byte order, as every backend returns them. */
+typedef struct {
+    int64_t nrows;
+    const int64_t* row_keys;
+    const int64_t* row_entry_begin;
+    const int64_t* row_byte_begin;
+    const uint8_t* entry_bytes;
+    const int64_t* entry_limit_valpos;
+} tgo_rows;
+
+typedef struct {
+    int64_t type_id;              /* UserEdgeLabel schema id (IDManager.getSchemaId)          */
+    int32_t multiplicity;         /* tgo_multiplicity                                        */
+    int32_t n_sort_key;           /* sort-key property keys (only for MULTI; KEY inline)       */
+    const int64_t* sort_key_ids;
+    int32_t n_signature;          /* signature property keys, in definition order             */
+    const int64_t* signature_ids;
+} tgo_edge_type;
+
+typedef struct {
+    int64_t key_id;               /* PropertyKey schema id                                    */
+    int32_t datatype;             /* tgo_datatype                                             */
+} tgo_property_key;
+
+typedef struct {
+    int32_t n_edge_types;  const tgo_edge_type* edge_types;
+    int32_t n_property_keys; const tgo_property_key* property_keys;
+} tgo_schema;
+
+typedef struct {
+    int32_t scope;                /* tgo_scope the programs will use; decides the per-row
+                                     preload cap: untyped single-direction scopes are cut at
+                                     hard_query_limit entries of slice [0x60,0x80), BOTH is
+                                     fitted and uncapped (BasicVertexCentricQueryBuilder.java:418-431,
+                                     QueryContainer.java:110-134)                              */
+    int32_t apply_cap;            /* 1 = reproduce the reference's cap (parity mode), 0 = not   */
+    int32_t n_labels;             /* 0 = untyped scope (all user edge labels)                  */
+    const int64_t* label_ids;     /* typed scope: __.inE("label")... — fitted, no cap          */
+    int64_t weight_key;           /* Integer edge property read as weight; 0 = none            */
+} tgo_load_opts;
+
+/* Decoded adjacency given directly (bench / already-decoded callers).  Dense vertex ids
+ * 0..n-1 in row order; titan_ids may be NULL (ids are then synthesised monotonically).
+ * Each directed edge u->v yields an OUT entry at u and an IN entry at v, as the
+ * reference's commit path writes two entries per edge (StandardTitanGraph.java:564-591). */
+typedef struct {
+    int64_t n;                    /* vertices                                                 */
+    int64_t m;                    /* directed edges                                           */
+    const int32_t* src;           /* m                                                        */
+    const int32_t* dst;           /* m                                                        */
+    const int32_t* weight;        /* m or NULL                                                */
+    const int64_t* titan_ids;     /* n or NULL                                                */
+} tgo_edges;
+
+/* ---- Programs ----------------------------------------------------------------------- */
+
+/* ShortestDistanceVertexProgram (titan-test/.../olap/ShortestDistanceVertexProgram.java:49-130)
+ * with the edge function (m,e) -> m + 1 (BFS / k-hop) or m + e.value(weight) (SSSP).
+ * Iterations 0..max_depth are executed; a vertex's distance is the minimum over walks of
+ * at most max_depth hops (Jacobi Bellman-Ford, :96-130).  dist_out[v] = TGO_DIST_ABSENT
+ * when no distance property was set (ShortestDistanceMapReduce emits nothing, :45-50). */
+typedef struct {
+    int64_t seed;                 /* Titan vertex id (ShortestDistanceVertexProgram.seed)     */
+    int32_t seed_is_dense;        /* 1: seed is a dense index instead of a Titan id            */
+    int32_t max_depth;            /* terminate when iteration >= max_depth (:128-130)          */
+    int32_t scope;                /* tgo_scope; must match the loaded scope                    */
+    int32_t flags;                /* TGO_FLAG_STATS: fill tgo_stats.reached / reached_entries  */
+} tgo_bfs_args;
+
+#define TGO_FLAG_STATS 1
+/* Distance value for "no DISTANCE property" (the vertex was not reached). */
+#define TGO_DIST_ABSENT INT64_MIN
+
+typedef enum { TGO_SSSP_HOP_BOUNDED = 0, TGO_SSSP_DELTA = 1 } tgo_sssp_mode;
+
+typedef struct {
+    int64_t seed;
+    int32_t seed_is_dense;
+    int32_t max_depth;
+    int32_t scope;
+    int32_t mode;                 /* tgo_sssp_mode: HOP_BOUNDED = exact reference semantics;
+                                     DELTA = converged distances (== reference iff every
+                                     shortest path has <= max_depth hops)                     */
+    int64_t delta;                /* bucket width for DELTA (0 = auto)                         */
+    int32_t flags;                /* TGO_FLAG_STATS                                            */
+    int32_t reserved;
+} tgo_sssp_args;
+
+/* PageRankVertexProgram (titan-test/.../olap/PageRankVertexProgram.java:45-100):
+ * it0 send 1 on inE; it1 edgeCount = sum, PR = 1/N; it>=2 PR = a*sum + (1-a)/N;
+ * terminate when iteration >= max_iterations, i.e. max_iterations-1 rank updates. */
+typedef struct {
+    double  alpha;                /* dampingFactor, default 0.85 (:52)                         */
+    int64_t vertex_count;         /* N = configured vertexCount (:54)                          */
+    int32_t max_iterations;       /* iterations(k), default 10 (:53)                           */
+    int32_t reserved;
+} tgo_pr_args;
+
+typedef struct {
+    int64_t num_vertices;         /* executed (non-ghost, visible) vertices                   */
+    int64_t num_entries;          /* adjacency entries kept (both directions)                  */
+    int64_t ghost_vertices;       /* VertexJobConverter GHOST_VERTEX_COUNT ("ghost-vertices")  */
+    int64_t truncated_results;    /* VertexJobConverter TRUNCATED_ENTRY_LISTS ("truncated-results") */
+    int64_t skipped_rows;         /* rows rejected by the key filter (Invisible ids)           */
+    int32_t iterations;           /* memory.getIteration() of the last program (FulgoraMemory.java:73-76) */
+    int32_t levels;               /* BFS/SSSP frontier levels executed on device               */
+    int64_t reached;              /* vertices with a distance after the last BFS/SSSP          */
+    int64_t reached_entries;      /* adjacency entries of reached vertices (m_R)               */
+    double  load_ms;              /* CSR assembly + upload                                     */
+    double  last_kernel_ms;       /* device time of the last program (HIP events)              */
+    int64_t device_bytes;         /* device memory held by the ctx                             */
+} tgo_stats;
+
+/* ---- Entry points ------------------------------------------------------------------- */
+
+void tgo_default_options(tgo_options* opts);
+int  tgo_create(const tgo_options* opts, tgo_ctx** out);
+void tgo_destroy(tgo_ctx* ctx);
+const char* tgo_last_error(const tgo_ctx* ctx);
+
+/* Append one batch of scanned rows (the scan delivers rows in work blocks:
+ * StandardScannerExecutor.java:235-288); tgo_finish_load() decodes, assembles and
+ * uploads the adjacency.  Replaces the per-superstep rescan + decode. */
+int  tgo_load_rows(tgo_ctx* ctx, const tgo_rows* rows, const tgo_schema* schema,
+                   const tgo_load_opts* opts);
+int  tgo_finish_load(tgo_ctx* ctx);
+/* Load an already-decoded edge list (finishes the load). */
+int  tgo_load_edges(tgo_ctx* ctx, const tgo_edges* edges, const tgo_load_opts* opts);
+
+int64_t tgo_num_vertices(const tgo_ctx* ctx);
+/* Titan vertex id of every dense index, in row order (n entries). */
+int  tgo_vertex_ids(tgo_ctx* ctx, int64_t* titan_ids_out);
+
+/* BFS / k-hop: ShortestDistance with unit edge function.  dist_out may be NULL: the
+ * result then stays on the device (tgo_copy_distances fetches it). */
+int  tgo_bfs(tgo_ctx* ctx, const tgo_bfs_args* args, int64_t* dist_out);
+int  tgo_sssp(tgo_ctx* ctx, const tgo_sssp_args* args, int64_t* dist_out);
+int  tgo_copy_distances(tgo_ctx* ctx, int64_t* dist_out);
+int  tgo_pagerank(tgo_ctx* ctx, const tgo_pr_args* args, double* pr_out);
+/* OLAPTest.DegreeCounter(k) (OLAPTest.java:334-416): k-walk counts, Java int wrap. */
+int  tgo_walkcount(tgo_ctx* ctx, int32_t k, int32_t* out);
+
+int  tgo_stats_get(tgo_ctx* ctx, tgo_stats* out);
+/* Block until all work queued on the ctx stream has finished. */
+int  tgo_sync(tgo_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TITAN_GPU_OLAP_H */

@@ -1,0 +1,724 @@
+/*
+ * fulgora_ref.c — CPU ORACLE for the Titan OLAP path (test infrastructure; see header).
+ *
+ * Every function cites the reference file:line it restates.  Paths are relative to
+ * /root/reference/titan-core/src/main/java/com/thinkaurelius/titan/ unless noted;
+ * "tmain/" = titan-test/src/main/java/com/thinkaurelius/titan/.
+ */
+#define _GNU_SOURCE
+#include "fulgora_ref.h"
+#include <stdlib.h>
+#include <string.h>
+#include <math.h>
+#include <pthread.h>
+
+/* ===================================================================== buffers */
+static void buf_put(fr_buf* b, uint8_t x) {
+    if (b->len == b->cap) {
+        b->cap = b->cap ? 2 * b->cap : 64;
+        b->p = (uint8_t*)realloc(b->p, b->cap);
+    }
+    b->p[b->len++] = x;
+}
+void fr_buf_free(fr_buf* b) { free(b->p); b->p = NULL; b->len = b->cap = 0; }
+
+/* ===================================================================== VariableLong */
+/* graphdb/database/idhandling/VariableLong.java */
+static int bit_length(uint64_t v) {            /* unsignedBitLength :71-73 */
+    return v == 0 ? 1 : 64 - __builtin_clzll(v);
+}
+static int num_blocks(int bits) { return (bits - 1) / 7 + 1; }   /* :66-69 */
+
+static void write_unsigned_n(fr_buf* b, int offset, uint64_t value) {   /* :46-57 */
+    while (offset > 0) {
+        offset -= 7;
+        uint8_t x = (uint8_t)((value >> offset) & 0x7F);
+        if (offset == 0) x |= 0x80;             /* STOP_MASK on the last byte */
+        buf_put(b, x);
+    }
+}
+static uint64_t read_unsigned(const uint8_t* d, size_t* pos) {          /* :30-38 */
+    uint64_t value = 0;
+    int8_t x;
+    do {
+        x = (int8_t)d[(*pos)++];
+        value = (value << 7) | (uint64_t)(x & 0x7F);
+    } while (x >= 0);
+    return value;
+}
+int fr_vl_positive_length(int64_t v) { return num_blocks(bit_length((uint64_t)v)); }
+void fr_vl_write_positive(fr_buf* b, int64_t v) {                       /* :84-87 */
+    write_unsigned_n(b, num_blocks(bit_length((uint64_t)v)) * 7, (uint64_t)v);
+}
+int64_t fr_vl_read_positive(const uint8_t* d, size_t* pos) { return (int64_t)read_unsigned(d, pos); }
+
+static uint64_t to_unsigned(int64_t v) {                                 /* convert2Unsigned :112-115 */
+    uint64_t a = v < 0 ? (uint64_t)(-(v)) : (uint64_t)v;
+    return (a << 1) | (v < 0 ? 1u : 0u);
+}
+static int64_t from_unsigned(uint64_t u) {                               /* :117-119 */
+    return (u & 1) ? -(int64_t)(u >> 1) : (int64_t)(u >> 1);
+}
+void fr_vl_write(fr_buf* b, int64_t v) {                                 /* :125-127 */
+    uint64_t u = to_unsigned(v);
+    write_unsigned_n(b, num_blocks(bit_length(u)) * 7, u);
+}
+int64_t fr_vl_read(const uint8_t* d, size_t* pos) { return from_unsigned(read_unsigned(d, pos)); }
+
+void fr_vl_write_positive_with_prefix(fr_buf* b, int64_t value, int64_t prefix, int prefix_len) {
+    /* :139-164 */
+    int delta_len = 8 - prefix_len;
+    uint8_t first = (uint8_t)(prefix << delta_len);
+    uint64_t v = (uint64_t)value;
+    int value_len = bit_length(v);
+    int mod = value_len % 7;
+    if (mod <= delta_len - 1) {
+        int offset = value_len - mod;
+        first |= (uint8_t)(v >> offset);
+        v = offset >= 64 ? v : (v & ((1ULL << offset) - 1));
+        value_len -= mod;
+    } else {
+        value_len += 7 - mod;
+    }
+    if (value_len > 0) first |= (uint8_t)(1 << (delta_len - 1));   /* continue mask */
+    buf_put(b, first);
+    if (value_len > 0) write_unsigned_n(b, value_len, v);
+}
+void fr_vl_read_positive_with_prefix(const uint8_t* d, size_t* pos, int prefix_len,
+                                     int64_t* value, int64_t* prefix) {  /* :171-186 */
+    int first = d[(*pos)++];
+    int delta_len = 8 - prefix_len;
+    *prefix = first >> delta_len;
+    uint64_t v = (uint64_t)(first & ((1 << (delta_len - 1)) - 1));
+    if ((first >> (delta_len - 1)) & 1) {
+        size_t p0 = *pos;
+        uint64_t rem = read_unsigned(d, pos);
+        size_t dp = *pos - p0;
+        v = (v << (dp * 7)) + rem;
+    }
+    *value = (int64_t)v;
+}
+int fr_vl_backward_length(int64_t value) {                               /* :247-252 */
+    int bl = bit_length((uint64_t)value);
+    int nb = 1 + (bl <= 4 ? 0 : (1 + (bl - 5) / 7));
+    return nb < 3 ? 3 : nb;
+}
+void fr_vl_write_positive_backward(fr_buf* b, int64_t value) {          /* :234-245 */
+    int nbytes = fr_vl_backward_length(value);
+    int prefix_len = nbytes - 3;
+    uint8_t x = (uint8_t)((prefix_len << 4) | 0x80);
+    for (int i = nbytes - 1; i >= 0; i--) {
+        x |= (uint8_t)(0x7F & ((uint64_t)value >> (i * 7)));
+        buf_put(b, x);
+        x = 0;
+    }
+}
+int64_t fr_vl_read_positive_backward(const uint8_t* d, size_t* pos) {   /* :254-272 */
+    size_t position = *pos;
+    int nbytes = 0;
+    uint64_t value = 0;
+    for (;;) {
+        position--;
+        int8_t x = (int8_t)d[position];
+        if (x < 0) {
+            value |= (uint64_t)(x & 0x0F) << (7 * nbytes);
+            break;
+        }
+        value |= (uint64_t)x << (7 * nbytes);
+        nbytes++;
+    }
+    *pos = position;
+    return (int64_t)value;
+}
+
+/* ===================================================================== IDManager */
+/* graphdb/idmanagement/IDManager.java: VertexIDType offsets/suffixes :45-345 */
+int64_t fr_schema_id(int type, int64_t count) {                          /* getSchemaId :620-623 */
+    static const int64_t suffix[4] = {5, 37, 21, 53};  /* User/System PropertyKey, User/System EdgeLabel */
+    return (count << 6) | suffix[type];
+}
+int64_t fr_vertex_id(int64_t count, int64_t partition, int pb) {         /* constructId :428-437 */
+    int64_t id = (count << pb) + partition;
+    return (id << 3) | 0;                                                /* NormalVertex 000b */
+}
+int64_t fr_key_of(int64_t vid, int pb) {                                 /* getKey :461-473 */
+    if ((vid & 3) == 1) return vid;                                      /* Schema 01b */
+    int64_t partition = (int64_t)(((uint64_t)vid >> 3) & ((1ULL << pb) - 1));
+    int64_t count = (int64_t)((uint64_t)vid >> (pb + 3));
+    int64_t suffix = vid & 7;
+    uint64_t high = pb == 0 ? 0 : ((uint64_t)partition << (64 - pb));
+    return (int64_t)(high | ((uint64_t)count << 3) | (uint64_t)suffix);
+}
+int64_t fr_key_id(int64_t key, int pb) {                                 /* getKeyID :476-486 */
+    if ((key & 3) == 1) return key;                                      /* Schema */
+    int64_t suffix = key & 7;
+    int poff = 64 - pb;
+    int64_t partition = poff < 64 ? (int64_t)((uint64_t)key >> poff) : 0;
+    int64_t count = (int64_t)(((uint64_t)key >> 3) & ((1ULL << (poff - 3)) - 1));
+    int64_t id = (count << pb) + partition;
+    return (id << 3) | suffix;
+}
+int fr_is_invisible(int64_t vid) { return (vid & 1) == 1; }              /* VertexIDType.Invisible 1b */
+
+/* ===================================================================== IDHandler */
+/* graphdb/database/idhandling/IDHandler.java */
+void fr_write_relation_type(fr_buf* b, int64_t type_id, int is_edge, int dir, int invisible) {
+    /* writeRelationType :88-94; getPrefix :61-64 */
+    int system = ((type_id & 63) == 37) || ((type_id & 63) == 53);
+    int64_t stripped = ((int64_t)((uint64_t)type_id >> 6) << 1) + dir;
+    int64_t prefix = ((system ? 0 : invisible ? 2 : 1) << 1) + (is_edge ? 1 : 0);
+    fr_vl_write_positive_with_prefix(b, stripped, prefix, 3);
+}
+int fr_read_relation_type(const uint8_t* d, size_t* pos, int64_t* type_id, int* is_edge, int* dir) {
+    /* readRelationType :116-127 */
+    int64_t value, prefix;
+    fr_vl_read_positive_with_prefix(d, pos, 3, &value, &prefix);
+    int rel = (int)(prefix & 1), dr = (int)(value & 1);
+    if (rel == 0 && dr == 1) return FR_E_CODEC;                          /* DirectionID.forId(1) */
+    int system = (prefix >> 1) == 0;
+    int64_t cnt = (int64_t)((uint64_t)value >> 1);
+    if (cnt <= 0) return FR_E_CODEC;
+    *type_id = fr_schema_id(rel ? (system ? 3 : 2) : (system ? 1 : 0), cnt);
+    *is_edge = rel;
+    *dir = dr;
+    return FR_OK;
+}
+
+/* ===================================================================== Serializer */
+static const fr_edge_type* find_type(const fr_schema* s, int64_t id) {
+    for (int i = 0; i < s->n_edge_types; i++) if (s->edge_types[i].type_id == id) return &s->edge_types[i];
+    return NULL;
+}
+static int key_datatype(const fr_schema* s, int64_t id) {
+    for (int i = 0; i < s->n_property_keys; i++) if (s->property_keys[i].key_id == id) return s->property_keys[i].datatype;
+    return 0;
+}
+static int is_unique(int mult, int dir) {                                /* Multiplicity.isUnique :59-70 */
+    if (dir == 1) return mult == FR_ONE2MANY || mult == FR_ONE2ONE;
+    return mult == FR_MANY2ONE || mult == FR_ONE2ONE;
+}
+static void put_be(fr_buf* b, uint64_t v, int n) { for (int i = n - 1; i >= 0; i--) buf_put(b, (uint8_t)(v >> (8 * i))); }
+static uint64_t get_be(const uint8_t* d, size_t* pos, int n) {
+    uint64_t v = 0; for (int i = 0; i < n; i++) v = (v << 8) | d[(*pos)++]; return v;
+}
+/* StandardSerializer.writeObjectInternal :286-301 (null flag) + attribute serializers. */
+static int write_object(fr_buf* b, int dt, int present, int64_t value, int byte_order) {
+    if (!present) { buf_put(b, 0xFF); return FR_OK; }
+    buf_put(b, 0x00);
+    switch (dt) {
+    case FR_DT_BYTE: buf_put(b, (uint8_t)((int8_t)value - (-128))); break;          /* ByteSerializer :17-19 */
+    case FR_DT_SHORT: put_be(b, (uint16_t)((int16_t)value - (-32768)), 2); break;    /* ShortSerializer */
+    case FR_DT_INTEGER:
+        if (byte_order) put_be(b, (uint32_t)((int32_t)value - INT32_MIN), 4);        /* IntegerSerializer :27-34 */
+        else fr_vl_write(b, (int32_t)value);                                         /* :20-23 */
+        break;
+    case FR_DT_LONG: put_be(b, (uint64_t)value - (uint64_t)INT64_MIN, 8); break;     /* LongSerializer :20-22 */
+    case FR_DT_BOOLEAN: buf_put(b, value ? 1 : 0); break;
+    default: return FR_E_UNSUPPORTED;
+    }
+    return FR_OK;
+}
+/* StandardSerializer.readObjectInternal :220-233.  Returns size-consumed; *present=0 on null. */
+static int read_object(const uint8_t* d, size_t len, size_t* pos, int dt, int byte_order,
+                       int* present, int64_t* ival) {
+    if (*pos >= len) return FR_E_CODEC;
+    int8_t flag = (int8_t)d[(*pos)++];
+    if (flag == -1) { *present = 0; return FR_OK; }
+    if (flag != 0) return FR_E_CODEC;
+    *present = 1;
+    switch (dt) {
+    case FR_DT_BYTE: *ival = (int8_t)(d[(*pos)++] + (-128)); break;
+    case FR_DT_SHORT: *ival = (int16_t)(get_be(d, pos, 2) + (-32768)); break;
+    case FR_DT_INTEGER:
+        if (byte_order) *ival = (int32_t)(get_be(d, pos, 4) + (uint32_t)INT32_MIN);
+        else { int64_t l = fr_vl_read(d, pos); if (l < INT32_MIN || l > INT32_MAX) return FR_E_CODEC; *ival = l; }
+        break;
+    case FR_DT_LONG: *ival = (int64_t)(get_be(d, pos, 8) + (uint64_t)INT64_MIN); break;
+    case FR_DT_FLOAT: *pos += 4; *ival = 0; break;
+    case FR_DT_DOUBLE: *pos += 8; *ival = 0; break;
+    case FR_DT_BOOLEAN: *ival = d[(*pos)++]; break;
+    default: return FR_E_UNSUPPORTED;
+    }
+    return *pos <= len ? FR_OK : FR_E_CODEC;
+}
+
+int fr_encode_vertex_exists(fr_buf* out, int32_t* value_pos, int64_t relation_id) {
+    /* BaseKey.VertexExists (BaseKey.java:27-28): system property key count 1, SINGLE
+     * cardinality => constrained & unique: valuePos before value (EdgeSerializer.java:277-281). */
+    fr_write_relation_type(out, fr_schema_id(1, 1), 0, 0, 1);
+    *value_pos = (int32_t)out->len;
+    write_object(out, FR_DT_BOOLEAN, 1, 1, 0);
+    fr_vl_write_positive(out, relation_id);
+    return FR_OK;
+}
+
+int fr_encode_property(fr_buf* out, int32_t* value_pos, int64_t key_id, int datatype,
+                       int64_t value, int64_t relation_id) {
+    /* user property of SINGLE cardinality: constrained & unique OUT => valuePos before
+     * the value, then the relation id (EdgeSerializer.java:270-281). */
+    fr_write_relation_type(out, key_id, 0, 0, 0);
+    *value_pos = (int32_t)out->len;
+    int rc = write_object(out, datatype, 1, value, 0);
+    if (rc) return rc;
+    fr_vl_write_positive(out, relation_id);
+    return FR_OK;
+}
+
+int fr_encode_edge(fr_buf* out, int32_t* value_pos, const fr_schema* schema, int64_t type_id,
+                   int dir, int64_t other, int64_t relation_id, const fr_prop* props, int nprops) {
+    /* EdgeSerializer.writeRelation :222-315 (edge branch :255-266) */
+    const fr_edge_type* t = find_type(schema, type_id);
+    if (!t) return FR_E_INVALID;
+    fr_write_relation_type(out, type_id, 1, dir, 0);
+    int mult = t->multiplicity;
+    if (mult == FR_MULTI) {
+        for (int k = 0; k < t->n_sort_key; k++) {                        /* writeInlineTypes KEY */
+            int present = 0; int64_t v = 0;
+            for (int j = 0; j < nprops; j++) if (props[j].key_id == t->sort_key_ids[k]) { present = 1; v = props[j].value; }
+            int rc = write_object(out, key_datatype(schema, t->sort_key_ids[k]), present, v, 1);
+            if (rc) return rc;
+        }
+        fr_vl_write_positive_backward(out, other);
+        fr_vl_write_positive_backward(out, relation_id);
+        *value_pos = (int32_t)out->len;
+    } else if (is_unique(mult, dir)) {
+        *value_pos = (int32_t)out->len;
+        fr_vl_write_positive(out, other);
+        fr_vl_write_positive(out, relation_id);
+    } else {
+        fr_vl_write_positive_backward(out, other);
+        *value_pos = (int32_t)out->len;
+        fr_vl_write_positive(out, relation_id);
+    }
+    for (int k = 0; k < t->n_signature; k++) {                           /* signature :285 */
+        int present = 0; int64_t v = 0;
+        for (int j = 0; j < nprops; j++) if (props[j].key_id == t->signature_ids[k]) { present = 1; v = props[j].value; }
+        int rc = write_object(out, key_datatype(schema, t->signature_ids[k]), present, v, 0);
+        if (rc) return rc;
+    }
+    /* remaining properties, sorted by key id (:287-308) */
+    int64_t rem[64]; int nrem = 0;
+    for (int j = 0; j < nprops && nrem < 64; j++) {
+        int64_t id = props[j].key_id, skip = 0;
+        if (mult == FR_MULTI) for (int k = 0; k < t->n_sort_key; k++) skip |= t->sort_key_ids[k] == id;
+        for (int k = 0; k < t->n_signature; k++) skip |= t->signature_ids[k] == id;
+        if (!skip) rem[nrem++] = id;
+    }
+    for (int a = 1; a < nrem; a++) for (int c = a; c > 0 && rem[c - 1] > rem[c]; c--) { int64_t x = rem[c]; rem[c] = rem[c - 1]; rem[c - 1] = x; }
+    for (int a = 0; a < nrem; a++) {
+        int64_t v = 0;
+        for (int j = 0; j < nprops; j++) if (props[j].key_id == rem[a]) v = props[j].value;
+        fr_vl_write_positive(out, (int64_t)((uint64_t)rem[a] >> 4));    /* writeInlineRelationType, IDHandler :135-138 */
+        int rc = write_object(out, key_datatype(schema, rem[a]), 1, v, 0);
+        if (rc) return rc;
+    }
+    return FR_OK;
+}
+
+int fr_decode_edge(const uint8_t* d, size_t len, size_t value_pos, const fr_schema* schema,
+                   int64_t weight_key, int64_t* type_id, int* dir, int64_t* other_id,
+                   int64_t* relation_id, int* has_weight, int64_t* weight) {
+    /* EdgeSerializer.parseRelation :73-166 (edge branch :90-110, properties :138-158) */
+    size_t pos = 0;
+    int is_edge;
+    if (len == 0 || value_pos > len) return FR_E_CODEC;
+    int rc = fr_read_relation_type(d, &pos, type_id, &is_edge, dir);
+    if (rc) return rc;
+    if (!is_edge) return FR_E_CODEC;
+    const fr_edge_type* t = find_type(schema, *type_id);
+    if (!t) return FR_E_CODEC;                                           /* tx.getExistingRelationType */
+    int mult = t->multiplicity;
+    size_t props_pos;
+    if (mult != FR_MULTI) {
+        if (is_unique(mult, *dir)) {
+            *other_id = fr_vl_read_positive(d, &pos);
+        } else {
+            size_t p = value_pos;
+            *other_id = fr_vl_read_positive_backward(d, &p);
+            pos = value_pos;
+        }
+        *relation_id = fr_vl_read_positive(d, &pos);
+        props_pos = pos;
+    } else {
+        size_t p = value_pos;
+        *relation_id = fr_vl_read_positive_backward(d, &p);
+        *other_id = fr_vl_read_positive_backward(d, &p);
+        props_pos = value_pos;
+    }
+    *has_weight = 0;
+    if (weight_key == 0) return FR_OK;
+    if (mult == FR_MULTI) for (int k = 0; k < t->n_sort_key; k++)
+        if (t->sort_key_ids[k] == weight_key) return FR_E_UNSUPPORTED;
+    pos = props_pos;
+    for (int k = 0; k < t->n_signature; k++) {                           /* readInlineTypes SIGNATURE */
+        int present; int64_t v = 0;
+        rc = read_object(d, len, &pos, key_datatype(schema, t->signature_ids[k]), 0, &present, &v);
+        if (rc) return rc;
+        if (t->signature_ids[k] == weight_key) { *has_weight = present; *weight = v; return FR_OK; }
+    }
+    while (pos < len) {                                                  /* remaining :147-152 */
+        int64_t kid = (fr_vl_read_positive(d, &pos) << 4) | 5;           /* readInlineRelationType */
+        int present; int64_t v = 0;
+        rc = read_object(d, len, &pos, key_datatype(schema, kid), 0, &present, &v);
+        if (rc) return rc;
+        if (kid == weight_key) { *has_weight = present; *weight = v; return FR_OK; }
+    }
+    return FR_OK;
+}
+
+/* ===================================================================== graph */
+struct fr_graph {
+    int64_t n;
+    int64_t* titan_id;        /* n, row order                                   */
+    int64_t* eoff;            /* n+1: kept user-edge entries of each row          */
+    int64_t* other;           /* E: other vertex Titan id                         */
+    uint8_t* edir;            /* E: 0 OUT, 1 IN                                   */
+    uint8_t* has_w;           /* E                                                */
+    int32_t* w;               /* E                                                */
+    /* FulgoraVertexMemory's NonBlockingHashMapLong<VertexState>: Titan id -> index */
+    int64_t* hkeys; int64_t* hvals; uint64_t hmask;
+};
+
+static uint64_t mix64(uint64_t x) {
+    x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL; x ^= x >> 33; return x;
+}
+static void build_hash(fr_graph* g) {
+    uint64_t cap = 16; while (cap < (uint64_t)g->n * 2) cap <<= 1;
+    g->hmask = cap - 1;
+    g->hkeys = (int64_t*)malloc(cap * sizeof(int64_t));
+    g->hvals = (int64_t*)malloc(cap * sizeof(int64_t));
+    for (uint64_t i = 0; i < cap; i++) g->hkeys[i] = INT64_MIN;
+    for (int64_t v = 0; v < g->n; v++) {
+        uint64_t h = mix64((uint64_t)g->titan_id[v]) & g->hmask;
+        while (g->hkeys[h] != INT64_MIN && g->hkeys[h] != g->titan_id[v]) h = (h + 1) & g->hmask;
+        g->hkeys[h] = g->titan_id[v]; g->hvals[h] = v;
+    }
+}
+static inline int64_t lookup(const fr_graph* g, int64_t id) {            /* vertexStates.get :49-58 */
+    uint64_t h = mix64((uint64_t)id) & g->hmask;
+    for (;;) {
+        int64_t k = g->hkeys[h];
+        if (k == id) return g->hvals[h];
+        if (k == INT64_MIN) return -1;                                   /* EMPTY_STATE */
+        h = (h + 1) & g->hmask;
+    }
+}
+
+void fr_free(fr_graph* g) {
+    if (!g) return;
+    free(g->titan_id); free(g->eoff); free(g->other); free(g->edir); free(g->has_w); free(g->w);
+    free(g->hkeys); free(g->hvals); free(g);
+}
+int64_t fr_num_vertices(const fr_graph* g) { return g->n; }
+void fr_vertex_ids(const fr_graph* g, int64_t* out) { memcpy(out, g->titan_id, g->n * sizeof(int64_t)); }
+int64_t fr_num_entries(const fr_graph* g) { return g->eoff[g->n]; }
+
+int fr_load_rows(const fr_rows* rows, const fr_schema* schema, const fr_load_opts* opts,
+                 fr_graph** out, fr_load_stats* stats) {
+    /* VertexJobConverter.process/getKeyFilter/isGhostVertex (VertexJobConverter.java:109-171)
+     * + slice [0x60,0x80) with the QueryContainer limit (QueryContainer.java:110-134). */
+    fr_load_stats st = {0, 0, 0, 0};
+    int pb = opts->partition_bits;
+    fr_graph* g = (fr_graph*)calloc(1, sizeof(fr_graph));
+    int64_t total = rows->row_entry_begin[rows->nrows];
+    g->titan_id = (int64_t*)malloc((rows->nrows + 1) * sizeof(int64_t));
+    g->eoff = (int64_t*)malloc((rows->nrows + 1) * sizeof(int64_t));
+    g->other = (int64_t*)malloc((total + 1) * sizeof(int64_t));
+    g->edir = (uint8_t*)malloc(total + 1);
+    g->has_w = (uint8_t*)malloc(total + 1);
+    g->w = (int32_t*)malloc((total + 1) * sizeof(int32_t));
+    int typed = opts->n_labels > 0;
+    int64_t limit = (opts->apply_cap && !typed && opts->scope != FR_SCOPE_BOTH_E) ? opts->hard_query_limit : INT64_MAX;
+    int64_t n = 0, e = 0;
+    g->eoff[0] = 0;
+    for (int64_t r = 0; r < rows->nrows; r++) {
+        int64_t vid = fr_key_id(rows->row_keys[r], pb);
+        if (fr_is_invisible(vid)) { st.skipped_rows++; continue; }       /* getKeyFilter :156-162 */
+        int64_t sfx = vid & 7;
+        if (sfx == 2) { fr_free(g); return FR_E_UNSUPPORTED; }           /* partitioned (vertex cut) */
+        if (sfx != 0 && sfx != 4) { fr_free(g); return FR_E_CODEC; }     /* getUserVertexIDType */
+        const uint8_t* base = rows->entry_bytes + rows->row_byte_begin[r];
+        int64_t e0 = rows->row_entry_begin[r], e1 = rows->row_entry_begin[r + 1];
+        if (e1 <= e0) { fr_free(g); return FR_E_CODEC; }
+        {   /* ghost check: first entry must be VertexExists (:131-137) */
+            size_t pos = 0; int64_t tid; int ie, dr;
+            if (fr_read_relation_type(base, &pos, &tid, &ie, &dr)) { fr_free(g); return FR_E_CODEC; }
+            if (ie || tid != fr_schema_id(1, 1)) { st.ghost_vertices++; continue; }
+        }
+        /* user-edge slice: column first byte in [0x60, 0x80) (IDHandler.getBounds :158-179) */
+        int64_t cnt = 0, first = -1;
+        for (int64_t k = e0; k < e1; k++) {
+            int64_t start = k == e0 ? 0 : (int64_t)((uint64_t)rows->entry_limit_valpos[k - 1] >> 32);
+            uint8_t c0 = base[start];
+            if (c0 >= 0x60 && c0 < 0x80) { if (first < 0) first = k; cnt++; }
+        }
+        if (limit != INT64_MAX && cnt >= limit) st.truncated_results++;  /* :125 */
+        int64_t keep = cnt < limit ? cnt : limit;
+        for (int64_t k = first; k >= 0 && k < first + keep; k++) {
+            int64_t start = k == e0 ? 0 : (int64_t)((uint64_t)rows->entry_limit_valpos[k - 1] >> 32);
+            int64_t end = (int64_t)((uint64_t)rows->entry_limit_valpos[k] >> 32);
+            int64_t vpos = rows->entry_limit_valpos[k] & 0x7FFFFFFF;
+            int64_t tid, oid, rid, wv = 0; int dr, hw;
+            int rc = fr_decode_edge(base + start, (size_t)(end - start), (size_t)vpos, schema,
+                                    opts->weight_key, &tid, &dr, &oid, &rid, &hw, &wv);
+            if (rc) { fr_free(g); return rc; }
+            if (typed) {
+                int ok = 0; for (int j = 0; j < opts->n_labels; j++) ok |= opts->label_ids[j] == tid;
+                if (!ok) continue;
+            }
+            g->other[e] = oid; g->edir[e] = (uint8_t)dr; g->has_w[e] = (uint8_t)hw; g->w[e] = (int32_t)wv;
+            e++;
+        }
+        g->titan_id[n] = vid;
+        n++;
+        g->eoff[n] = e;
+    }
+    g->n = n;
+    st.num_entries = e;
+    build_hash(g);
+    *out = g;
+    if (stats) *stats = st;
+    return FR_OK;
+}
+
+int fr_load_adjacency(int64_t n, const int64_t* titan_ids, const int64_t* off, const int64_t* mid,
+                      const int32_t* adj, const int32_t* w, fr_graph** out) {
+    fr_graph* g = (fr_graph*)calloc(1, sizeof(fr_graph));
+    int64_t E = off[n];
+    g->n = n;
+    g->titan_id = (int64_t*)malloc((n + 1) * sizeof(int64_t));
+    g->eoff = (int64_t*)malloc((n + 1) * sizeof(int64_t));
+    g->other = (int64_t*)malloc((E + 1) * sizeof(int64_t));
+    g->edir = (uint8_t*)malloc(E + 1);
+    g->has_w = (uint8_t*)malloc(E + 1);
+    g->w = (int32_t*)malloc((E + 1) * sizeof(int32_t));
+    memcpy(g->titan_id, titan_ids, n * sizeof(int64_t));
+    memcpy(g->eoff, off, (n + 1) * sizeof(int64_t));
+    for (int64_t v = 0; v < n; v++)
+        for (int64_t k = off[v]; k < off[v + 1]; k++) {
+            g->other[k] = titan_ids[adj[k]];
+            g->edir[k] = k >= mid[v];
+            g->has_w[k] = w != NULL;
+            g->w[k] = w ? w[k] : 0;
+        }
+    build_hash(g);
+    *out = g;
+    return FR_OK;
+}
+
+int64_t fr_export(const fr_graph* g, int64_t* off, int64_t* mid, int32_t* adj, int32_t* w) {
+    /* dense form with OUT entries first within each row (stable); entries whose other
+     * endpoint is not an executed vertex are dropped: they can never carry a message
+     * (absent VertexState => EMPTY_STATE => null, FulgoraVertexMemory.java:49-58). */
+    int64_t e = 0;
+    off[0] = 0;
+    for (int64_t v = 0; v < g->n; v++) {
+        for (int pass = 0; pass < 2; pass++) {
+            if (pass == 1) mid[v] = e;
+            for (int64_t k = g->eoff[v]; k < g->eoff[v + 1]; k++) {
+                if (g->edir[k] != pass) continue;
+                int64_t o = lookup(g, g->other[k]);
+                if (o < 0) continue;
+                adj[e] = (int32_t)o;
+                if (w) w[e] = g->has_w[k] ? g->w[k] : INT32_MIN;
+                e++;
+            }
+        }
+        off[v + 1] = e;
+    }
+    return e;
+}
+
+/* ===================================================================== executor */
+/* One superstep = every vertex executes (VertexProgramScanJob.process :71-97), fanned
+ * out over `threads` workers (StandardScannerExecutor processors :235-288). */
+typedef struct {
+    const fr_graph* g; int64_t lo, hi; void* prog; void (*fn)(void*, const fr_graph*, int64_t, int64_t);
+} task_t;
+static void* run_task(void* a) { task_t* t = (task_t*)a; t->fn(t->prog, t->g, t->lo, t->hi); return NULL; }
+static void superstep(const fr_graph* g, int threads, void* prog, void (*fn)(void*, const fr_graph*, int64_t, int64_t)) {
+    if (threads < 1) threads = 1;
+    if (threads == 1 || g->n < 1024) { fn(prog, g, 0, g->n); return; }
+    pthread_t th[256]; task_t tk[256];
+    if (threads > 256) threads = 256;
+    for (int i = 0; i < threads; i++) {
+        tk[i].g = g; tk[i].prog = prog; tk[i].fn = fn;
+        tk[i].lo = g->n * i / threads; tk[i].hi = g->n * (i + 1) / threads;
+        pthread_create(&th[i], NULL, run_task, &tk[i]);
+    }
+    for (int i = 0; i < threads; i++) pthread_join(th[i], NULL);
+}
+
+/* Reversed scope selection (FulgoraUtil.getReverseTraversal :49-62, reverseDirection :57):
+ * scope inE -> receiver walks its OUT entries; outE -> IN entries; bothE -> all. */
+static inline int take(int scope, uint8_t edir) {
+    if (scope == FR_SCOPE_BOTH_E) return 1;
+    return scope == FR_SCOPE_IN_E ? edir == 0 : edir == 1;
+}
+
+/* ---- ShortestDistanceVertexProgram (tmain/olap/ShortestDistanceVertexProgram.java:96-130) ---- */
+typedef struct {
+    int scope, weighted, iteration;
+    int64_t seed;
+    int64_t* dist;               /* property DISTANCE (immediate, VertexState.setProperty)      */
+    int64_t* prev; int64_t* cur; /* double-buffered Local messages (VertexState :55-89)        */
+    volatile int failed;
+} sd_t;
+static void sd_exec(void* p, const fr_graph* g, int64_t lo, int64_t hi) {
+    sd_t* s = (sd_t*)p;
+    for (int64_t v = lo; v < hi; v++) {
+        if (s->iteration == 0) {                                         /* :97-104 */
+            if (g->titan_id[v] == s->seed) { s->dist[v] = 0; s->cur[v] = 0; }
+            continue;
+        }
+        int64_t best = FR_ABSENT;                                        /* reduce(min).orElse(null) :109-110 */
+        for (int64_t k = g->eoff[v]; k < g->eoff[v + 1]; k++) {
+            if (!take(s->scope, g->edir[k])) continue;
+            int64_t o = lookup(g, g->other[k]);
+            if (o < 0) continue;
+            int64_t m = s->prev[o];
+            if (m == FR_ABSENT) continue;                                /* filter(m != null) */
+            int64_t wt = 1;
+            if (s->weighted) {
+                if (!g->has_w[k]) { s->failed = 1; continue; }           /* edge.value(weight) throws */
+                wt = g->w[k];
+            }
+            int64_t c = (int64_t)((uint64_t)m + (uint64_t)wt);           /* Long + Integer, Java wrap */
+            if (best == FR_ABSENT || c < best) best = c;
+        }
+        if (best == FR_ABSENT) continue;                                 /* :112-113 */
+        if (s->dist[v] == FR_ABSENT || s->dist[v] > best) {             /* :117-122 */
+            s->dist[v] = best; s->cur[v] = best;
+        }
+    }
+}
+int fr_shortest_distance(const fr_graph* g, int64_t seed, int max_depth, int scope, int weighted,
+                         int threads, int64_t* dist_out, int* iterations_out) {
+    sd_t s; memset(&s, 0, sizeof s);
+    s.scope = scope; s.weighted = weighted; s.seed = seed;
+    s.dist = dist_out;
+    s.prev = (int64_t*)malloc((g->n + 1) * sizeof(int64_t));
+    s.cur = (int64_t*)malloc((g->n + 1) * sizeof(int64_t));
+    for (int64_t v = 0; v < g->n; v++) s.dist[v] = s.prev[v] = s.cur[v] = FR_ABSENT;
+    int it;
+    for (it = 0;; it++) {                                                /* FulgoraGraphComputer :151-189 */
+        s.iteration = it;
+        superstep(g, threads, &s, sd_exec);
+        if (s.failed) { free(s.prev); free(s.cur); return FR_E_PROGRAM; }
+        int64_t* t = s.prev; s.prev = s.cur; s.cur = t;                  /* completeIteration: prev=cur, cur=null */
+        for (int64_t v = 0; v < g->n; v++) s.cur[v] = FR_ABSENT;
+        if (it >= max_depth) break;                                      /* terminate :128-130 */
+    }
+    if (iterations_out) *iterations_out = it;                            /* FulgoraMemory.complete :73-76 */
+    free(s.prev); free(s.cur);
+    return FR_OK;
+}
+
+/* ---- PageRankVertexProgram (tmain/olap/PageRankVertexProgram.java:75-100) ---- */
+typedef struct {
+    int iteration; double alpha; int64_t N;
+    double* pr; double* edge_count;
+    /* two scopes (outE, inE): VertexState keeps Object[2]; NaN = null message */
+    double* prev_out; double* prev_in; double* cur_out; double* cur_in;
+} pr_t;
+static void pr_exec(void* p, const fr_graph* g, int64_t lo, int64_t hi) {
+    pr_t* s = (pr_t*)p;
+    for (int64_t v = lo; v < hi; v++) {
+        if (s->iteration == 0) { s->cur_in[v] = 1.0; continue; }         /* :76-77 sendMessage(inE, 1) */
+        /* receiveMessages(): concat(inE stream, outE stream) (VertexMemoryHandler :95-102);
+         * reduce(0D, a+b) sequentially in that order. */
+        double sum = 0.0;
+        for (int64_t k = g->eoff[v]; k < g->eoff[v + 1]; k++) {          /* inE scope: walk OUT entries */
+            if (g->edir[k] != 0) continue;
+            int64_t o = lookup(g, g->other[k]);
+            if (o < 0) continue;
+            double m = s->prev_in[o];
+            if (isnan(m)) continue;
+            sum = sum + m;
+        }
+        for (int64_t k = g->eoff[v]; k < g->eoff[v + 1]; k++) {          /* outE scope: walk IN entries */
+            if (g->edir[k] != 1) continue;
+            int64_t o = lookup(g, g->other[k]);
+            if (o < 0) continue;
+            double m = s->prev_out[o];
+            if (isnan(m)) continue;
+            sum = sum + m;
+        }
+        if (s->iteration == 1) {                                         /* :78-83 */
+            double init = 1.0 / (double)s->N;
+            s->pr[v] = init; s->edge_count[v] = sum;
+            s->cur_out[v] = init / sum;
+        } else {                                                         /* :84-89 */
+            double npr = (s->alpha * sum) + ((1.0 - s->alpha) / (double)s->N);
+            s->pr[v] = npr;
+            s->cur_out[v] = npr / s->edge_count[v];
+        }
+    }
+}
+int fr_pagerank(const fr_graph* g, double alpha, int64_t vertex_count, int max_iterations,
+                int threads, double* pr_out, int* iterations_out) {
+    pr_t s; memset(&s, 0, sizeof s);
+    s.alpha = alpha; s.N = vertex_count; s.pr = pr_out;
+    size_t nb = (g->n + 1) * sizeof(double);
+    s.edge_count = (double*)malloc(nb);
+    s.prev_out = (double*)malloc(nb); s.prev_in = (double*)malloc(nb);
+    s.cur_out = (double*)malloc(nb); s.cur_in = (double*)malloc(nb);
+    for (int64_t v = 0; v < g->n; v++) {
+        pr_out[v] = NAN; s.edge_count[v] = NAN;
+        s.prev_out[v] = s.prev_in[v] = s.cur_out[v] = s.cur_in[v] = NAN;
+    }
+    int it;
+    for (it = 0;; it++) {
+        s.iteration = it;
+        superstep(g, threads, &s, pr_exec);
+        double* t;
+        t = s.prev_out; s.prev_out = s.cur_out; s.cur_out = t;
+        t = s.prev_in; s.prev_in = s.cur_in; s.cur_in = t;
+        for (int64_t v = 0; v < g->n; v++) s.cur_out[v] = s.cur_in[v] = NAN;
+        if (it >= max_iterations) break;                                 /* terminate :93-95 */
+    }
+    if (iterations_out) *iterations_out = it;
+    free(s.edge_count); free(s.prev_out); free(s.prev_in); free(s.cur_out); free(s.cur_in);
+    return FR_OK;
+}
+
+/* ---- OLAPTest.DegreeCounter (tmain/olap/OLAPTest.java:334-416) ---- */
+typedef struct {
+    int iteration, length;
+    int32_t* deg; int32_t* prev; int32_t* cur; uint8_t* prev_ok; uint8_t* cur_ok;
+} dc_t;
+static void dc_exec(void* p, const fr_graph* g, int64_t lo, int64_t hi) {
+    dc_t* s = (dc_t*)p;
+    for (int64_t v = lo; v < hi; v++) {
+        if (s->iteration == 0) { s->cur[v] = 1; s->cur_ok[v] = 1; continue; }   /* :358-359 */
+        uint32_t sum = 0;                                                /* Java int, wraps (:361) */
+        for (int64_t k = g->eoff[v]; k < g->eoff[v + 1]; k++) {          /* DEG_MSG = inE: walk OUT */
+            if (g->edir[k] != 0) continue;
+            int64_t o = lookup(g, g->other[k]);
+            if (o < 0 || !s->prev_ok[o]) continue;
+            sum += (uint32_t)s->prev[o];
+        }
+        s->deg[v] = (int32_t)sum;                                        /* :362 */
+        if (s->iteration < s->length) { s->cur[v] = (int32_t)sum; s->cur_ok[v] = 1; }   /* :363 */
+    }
+}
+int fr_degree_counter(const fr_graph* g, int length, int threads, int32_t* out, int* iterations_out) {
+    if (length <= 0) return FR_E_INVALID;                                /* :347 checkArgument */
+    dc_t s; memset(&s, 0, sizeof s);
+    s.length = length; s.deg = out;
+    s.prev = (int32_t*)calloc(g->n + 1, 4); s.cur = (int32_t*)calloc(g->n + 1, 4);
+    s.prev_ok = (uint8_t*)calloc(g->n + 1, 1); s.cur_ok = (uint8_t*)calloc(g->n + 1, 1);
+    for (int64_t v = 0; v < g->n; v++) out[v] = 0;
+    int it;
+    for (it = 0;; it++) {
+        s.iteration = it;
+        superstep(g, threads, &s, dc_exec);
+        int32_t* t = s.prev; s.prev = s.cur; s.cur = t;
+        uint8_t* u = s.prev_ok; s.prev_ok = s.cur_ok; s.cur_ok = u;
+        memset(s.cur_ok, 0, g->n + 1);
+        if (it >= length) break;                                         /* terminate :368-370 */
+    }
+    if (iterations_out) *iterations_out = it;
+    free(s.prev); free(s.cur); free(s.prev_ok); free(s.cur_ok);
+    return FR_OK;
+}

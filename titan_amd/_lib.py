@@ -1,0 +1,157 @@
+"""ctypes binding of the C-ABI in include/titan_gpu_olap.h (libtitan_gpu_olap.so).
+
+The library is built in-tree (titan_amd/libtitan_gpu_olap.so, see titan_amd/csrc/Makefile)
+and is the only compute path: there is no CPU fallback.  Loading fails loudly when the
+shared object is missing.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libtitan_gpu_olap.so")
+
+# status codes (tgo_status)
+TGO_OK = 0
+TGO_E_INVALID = -1
+TGO_E_HIP = -2
+TGO_E_OOM = -3
+TGO_E_CODEC = -4
+TGO_E_STATE = -5
+TGO_E_PROGRAM = -6
+TGO_E_UNSUPPORTED = -7
+TGO_E_COMM = -8
+
+SCOPE_OUT_E, SCOPE_IN_E, SCOPE_BOTH_E = 0, 1, 2
+MULTI, SIMPLE, MANY2ONE, ONE2MANY, ONE2ONE = 0, 1, 2, 3, 4
+DT_BYTE, DT_SHORT, DT_INTEGER, DT_LONG, DT_FLOAT, DT_DOUBLE, DT_BOOLEAN = 1, 2, 3, 4, 5, 6, 7
+SSSP_HOP_BOUNDED, SSSP_DELTA = 0, 1
+FLAG_STATS = 1
+DIST_ABSENT = -(1 << 63)
+ABI_VERSION = 1
+
+_i64p = C.POINTER(C.c_int64)
+_i32p = C.POINTER(C.c_int32)
+_u8p = C.POINTER(C.c_uint8)
+
+
+class Options(C.Structure):
+    _fields_ = [("abi_version", C.c_int32), ("device", C.c_int32), ("partition_bits", C.c_int32),
+                ("host_threads", C.c_int32), ("hard_query_limit", C.c_int64), ("stream", C.c_void_p)]
+
+
+class Rows(C.Structure):
+    _fields_ = [("nrows", C.c_int64), ("row_keys", _i64p), ("row_entry_begin", _i64p),
+                ("row_byte_begin", _i64p), ("entry_bytes", _u8p), ("entry_limit_valpos", _i64p)]
+
+
+class EdgeType(C.Structure):
+    _fields_ = [("type_id", C.c_int64), ("multiplicity", C.c_int32), ("n_sort_key", C.c_int32),
+                ("sort_key_ids", _i64p), ("n_signature", C.c_int32), ("signature_ids", _i64p)]
+
+
+class PropertyKey(C.Structure):
+    _fields_ = [("key_id", C.c_int64), ("datatype", C.c_int32)]
+
+
+class Schema(C.Structure):
+    _fields_ = [("n_edge_types", C.c_int32), ("edge_types", C.POINTER(EdgeType)),
+                ("n_property_keys", C.c_int32), ("property_keys", C.POINTER(PropertyKey))]
+
+
+class LoadOpts(C.Structure):
+    _fields_ = [("scope", C.c_int32), ("apply_cap", C.c_int32), ("n_labels", C.c_int32),
+                ("label_ids", _i64p), ("weight_key", C.c_int64)]
+
+
+class Edges(C.Structure):
+    _fields_ = [("n", C.c_int64), ("m", C.c_int64), ("src", _i32p), ("dst", _i32p),
+                ("weight", _i32p), ("titan_ids", _i64p)]
+
+
+class BfsArgs(C.Structure):
+    _fields_ = [("seed", C.c_int64), ("seed_is_dense", C.c_int32), ("max_depth", C.c_int32),
+                ("scope", C.c_int32), ("flags", C.c_int32)]
+
+
+class SsspArgs(C.Structure):
+    _fields_ = [("seed", C.c_int64), ("seed_is_dense", C.c_int32), ("max_depth", C.c_int32),
+                ("scope", C.c_int32), ("mode", C.c_int32), ("delta", C.c_int64),
+                ("flags", C.c_int32), ("reserved", C.c_int32)]
+
+
+class PrArgs(C.Structure):
+    _fields_ = [("alpha", C.c_double), ("vertex_count", C.c_int64), ("max_iterations", C.c_int32),
+                ("reserved", C.c_int32)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("num_vertices", C.c_int64), ("num_entries", C.c_int64), ("ghost_vertices", C.c_int64),
+                ("truncated_results", C.c_int64), ("skipped_rows", C.c_int64), ("iterations", C.c_int32),
+                ("levels", C.c_int32), ("reached", C.c_int64), ("reached_entries", C.c_int64),
+                ("load_ms", C.c_double), ("last_kernel_ms", C.c_double), ("device_bytes", C.c_int64)]
+
+
+# Every symbol include/*.h declares (checked by tests/test_abi.py).
+EXPORTS = [
+    "tgo_default_options", "tgo_create", "tgo_destroy", "tgo_last_error", "tgo_load_rows",
+    "tgo_finish_load", "tgo_load_edges", "tgo_num_vertices", "tgo_vertex_ids", "tgo_bfs",
+    "tgo_sssp", "tgo_copy_distances", "tgo_pagerank", "tgo_walkcount", "tgo_stats_get", "tgo_sync",
+    "tgo_rmat_edges", "tgo_pick_roots",
+]
+
+_lib = None
+
+
+def load() -> C.CDLL:
+    """Load libtitan_gpu_olap.so (raises when it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} is missing: build it with `make -C titan_amd/csrc` "
+                           "(or __graft_entry__.build()); there is no CPU fallback")
+    # If torch is present in this process its HIP runtime must be the one we bind to:
+    # import it first so the loader resolves libamdhip64.so.7 to the same copy.
+    try:
+        import torch  # noqa: F401
+    except Exception:  # pragma: no cover - torch is optional for the library itself
+        pass
+    lib = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+    P = C.POINTER
+    vp = C.c_void_p
+    sig = {
+        "tgo_default_options": (None, [P(Options)]),
+        "tgo_create": (C.c_int, [P(Options), P(vp)]),
+        "tgo_destroy": (None, [vp]),
+        "tgo_last_error": (C.c_char_p, [vp]),
+        "tgo_load_rows": (C.c_int, [vp, P(Rows), P(Schema), P(LoadOpts)]),
+        "tgo_finish_load": (C.c_int, [vp]),
+        "tgo_load_edges": (C.c_int, [vp, P(Edges), P(LoadOpts)]),
+        "tgo_num_vertices": (C.c_int64, [vp]),
+        "tgo_vertex_ids": (C.c_int, [vp, _i64p]),
+        "tgo_bfs": (C.c_int, [vp, P(BfsArgs), _i64p]),
+        "tgo_sssp": (C.c_int, [vp, P(SsspArgs), _i64p]),
+        "tgo_copy_distances": (C.c_int, [vp, _i64p]),
+        "tgo_pagerank": (C.c_int, [vp, P(PrArgs), C.POINTER(C.c_double)]),
+        "tgo_walkcount": (C.c_int, [vp, C.c_int32, _i32p]),
+        "tgo_stats_get": (C.c_int, [vp, P(Stats)]),
+        "tgo_sync": (C.c_int, [vp]),
+        "tgo_rmat_edges": (C.c_int, [C.c_int32, C.c_int32, C.c_uint64, C.c_int64, C.c_int64,
+                                     _i32p, _i32p, _i32p, C.c_int32]),
+        "tgo_pick_roots": (C.c_int, [C.c_int64, C.c_int64, _i32p, _i32p, C.c_uint64, C.c_int32, _i64p]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = lib
+    return lib
+
+
+def ptr(arr, ctype):
+    """ctypes pointer to a contiguous numpy array (None -> NULL)."""
+    if arr is None:
+        return None
+    return arr.ctypes.data_as(C.POINTER(ctype))

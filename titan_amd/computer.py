@@ -1,0 +1,412 @@
+"""Host-side mirror of Titan's GraphComputer API for the OLAP path.
+
+Same names, argument meaning and error behaviour as the reference, so the parity tests
+read like OLAPTest:
+
+    computer = graph.compute()                          # TitanBlueprintsGraph.java:133-146
+    computer.resultMode(TitanGraphComputer.ResultMode.NONE)
+    computer.workers(4)                                 # FulgoraGraphComputer.java:96-100
+    computer.program(PageRankVertexProgram.build().iterations(10).vertexCount(n)
+                     .dampingFactor(0.85).create(graph))
+    computer.mapReduce(PageRankMapReduce.build().create())
+    result = computer.submit().get()                    # FulgoraGraphComputer.java:117-311
+    ranks = result.memory().get(PageRankMapReduce.DEFAULT_MEMORY_KEY)
+
+What runs underneath is the HIP engine (titan_amd/engine.py -> libtitan_gpu_olap.so):
+the graph's edgestore rows are decoded once per message-scope (the reference preloads the
+reversed-scope slice every superstep, VertexProgramScanJob.getQueries :99-120) and each
+program is one tgo_* call.  Failures surface as ExecutionException from get(), wrapping a
+TitanException (OLAPTest.vertexProgramExceptionPropagatesToCaller, :222-239).
+"""
+from __future__ import annotations
+
+import enum
+import threading
+from concurrent.futures import Future, ThreadPoolExecutor
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib as L
+from .engine import Engine, Schema, TitanException
+
+SCOPE_NAMES = {"outE": L.SCOPE_OUT_E, "inE": L.SCOPE_IN_E, "bothE": L.SCOPE_BOTH_E}
+
+
+class ExecutionException(Exception):
+    """java.util.concurrent.ExecutionException: raised by Future.get() on failure."""
+
+
+class ComputerFuture:
+    def __init__(self, fut: Future):
+        self._f = fut
+
+    def get(self, timeout=None):
+        try:
+            return self._f.result(timeout)
+        except ExecutionException:
+            raise
+        except Exception as e:  # noqa: BLE001 - mirror CompletableFuture semantics
+            raise ExecutionException(e) from e
+
+    def done(self):
+        return self._f.done()
+
+
+@dataclass(frozen=True)
+class KeyValue:
+    key: int
+    value: object
+
+    def getKey(self):  # noqa: N802 - reference naming
+        return self.key
+
+    def getValue(self):  # noqa: N802
+        return self.value
+
+
+class Memory:
+    """FulgoraMemory after complete(): iteration reports T (FulgoraMemory.java:73-76)."""
+
+    def __init__(self, iteration, runtime_ms, values):
+        self._it = iteration
+        self._rt = runtime_ms
+        self._values = values
+
+    def getIteration(self):  # noqa: N802
+        return self._it
+
+    def getRuntime(self):  # noqa: N802
+        return self._rt
+
+    def exists(self, key):
+        return key in self._values
+
+    def get(self, key):
+        if key not in self._values:
+            raise KeyError(f"The memory does not have a value for provided key: {key}")
+        v = self._values[key]
+        return iter(v) if isinstance(v, list) else v
+
+    def keys(self):
+        return set(self._values)
+
+
+class ComputerResult:
+    def __init__(self, graph, memory: Memory, vertex_properties):
+        self._graph = graph
+        self._memory = memory
+        self.vertex_properties = vertex_properties   # compute key -> (titan_ids, values)
+
+    def memory(self):
+        return self._memory
+
+    def graph(self):
+        return self._graph
+
+
+# ----------------------------------------------------------------------------- programs
+class VertexProgram:
+    scope_name = "bothE"
+    compute_keys: tuple = ()
+
+
+class ShortestDistanceVertexProgram(VertexProgram):
+    """tmain/olap/ShortestDistanceVertexProgram.java: Local(inE, m + e.value(weight))."""
+    DISTANCE = "titan.shortestDistanceVertexProgram.distance"
+    compute_keys = (DISTANCE,)
+
+    def __init__(self, seed, max_depth, weight_property="distance", scope="inE", weighted=True, mode=L.SSSP_HOP_BOUNDED):
+        self.seed = seed
+        self.max_depth = max_depth
+        self.weight_property = weight_property
+        self.scope_name = scope
+        self.weighted = weighted
+        self.mode = mode
+
+    class Builder:
+        def __init__(self):
+            self._seed = None
+            self._max_depth = None
+            self._weight = "distance"
+            self._scope = "inE"
+            self._weighted = True
+            self._mode = L.SSSP_HOP_BOUNDED
+
+        def seed(self, s):
+            self._seed = int(s)
+            return self
+
+        def maxDepth(self, d):  # noqa: N802
+            self._max_depth = int(d)
+            return self
+
+        def weightProperty(self, name):  # noqa: N802
+            self._weight = name
+            return self
+
+        def scope(self, name):
+            self._scope = name
+            return self
+
+        def unitWeight(self):  # noqa: N802 - BFS / k-hop: edge function m -> m + 1
+            self._weighted = False
+            return self
+
+        def deltaStepping(self):  # noqa: N802
+            self._mode = L.SSSP_DELTA
+            return self
+
+        def create(self, graph=None):
+            if self._seed is None or self._max_depth is None:
+                raise ValueError("seed and maxDepth are required (configuration.getInt(MAX_DEPTH))")
+            return ShortestDistanceVertexProgram(self._seed, self._max_depth, self._weight, self._scope,
+                                                 self._weighted, self._mode)
+
+    @staticmethod
+    def build():
+        return ShortestDistanceVertexProgram.Builder()
+
+
+class PageRankVertexProgram(VertexProgram):
+    """tmain/olap/PageRankVertexProgram.java:45-100 (scopes outE + inE)."""
+    PAGE_RANK = "titan.pageRank.pageRank"
+    OUTGOING_EDGE_COUNT = "titan.pageRank.edgeCount"
+    compute_keys = (PAGE_RANK, OUTGOING_EDGE_COUNT)
+    scope_name = "inE"
+
+    def __init__(self, alpha=0.85, max_iterations=10, vertex_count=1):
+        self.alpha = alpha
+        self.max_iterations = max_iterations
+        self.vertex_count = vertex_count
+
+    class Builder:
+        def __init__(self):
+            self._a, self._it, self._n = 0.85, 10, 1          # loadState defaults (:52-54)
+
+        def vertexCount(self, n):  # noqa: N802
+            self._n = int(n)
+            return self
+
+        def dampingFactor(self, a):  # noqa: N802
+            self._a = float(a)
+            return self
+
+        def iterations(self, k):
+            self._it = int(k)
+            return self
+
+        def create(self, graph=None):
+            return PageRankVertexProgram(self._a, self._it, self._n)
+
+    @staticmethod
+    def build():
+        return PageRankVertexProgram.Builder()
+
+
+class DegreeCounter(VertexProgram):
+    """tmain/olap/OLAPTest.java:334-416 — k-walk counts over inE, Java int wrap."""
+    DEGREE = "degree"
+    compute_keys = (DEGREE,)
+    scope_name = "inE"
+
+    def __init__(self, length=1):
+        if length <= 0:
+            raise ValueError("length must be > 0")      # Preconditions.checkArgument(length>0)
+        self.length = length
+
+
+# ----------------------------------------------------------------------------- map-reduces
+class MapReduce:
+    memory_key = ""
+
+
+class PageRankMapReduce(MapReduce):
+    DEFAULT_MEMORY_KEY = "pageRank"     # PageRankMapReduce.java:19
+
+    def __init__(self, key=DEFAULT_MEMORY_KEY):
+        self.memory_key = key
+
+    class Builder:
+        def __init__(self):
+            self._k = PageRankMapReduce.DEFAULT_MEMORY_KEY
+
+        def memoryKey(self, k):  # noqa: N802
+            self._k = k
+            return self
+
+        def create(self):
+            return PageRankMapReduce(self._k)
+
+    @staticmethod
+    def build():
+        return PageRankMapReduce.Builder()
+
+    def emit(self, ids, props):
+        pr = props.get(PageRankVertexProgram.PAGE_RANK)
+        if pr is None:
+            return []
+        # map() emits only vertices where the property is present (:45-50)
+        return [KeyValue(int(i), float(v)) for i, v in zip(ids, pr) if not np.isnan(v)]
+
+
+class ShortestDistanceMapReduce(MapReduce):
+    DEFAULT_MEMORY_KEY = "shortestDistance"   # ShortestDistanceMapReduce.java:16
+
+    def __init__(self, key=DEFAULT_MEMORY_KEY):
+        self.memory_key = key
+
+    class Builder:
+        def __init__(self):
+            self._k = ShortestDistanceMapReduce.DEFAULT_MEMORY_KEY
+
+        def memoryKey(self, k):  # noqa: N802
+            self._k = k
+            return self
+
+        def create(self):
+            return ShortestDistanceMapReduce(self._k)
+
+    @staticmethod
+    def build():
+        return ShortestDistanceMapReduce.Builder()
+
+    def emit(self, ids, props):
+        d = props.get(ShortestDistanceVertexProgram.DISTANCE)
+        if d is None:
+            return []
+        return [KeyValue(int(i), int(v)) for i, v in zip(ids, d) if v != L.DIST_ABSENT]
+
+
+class DegreeMapper(MapReduce):
+    DEGREE_RESULT = "degrees"                 # OLAPTest.java:420
+    memory_key = DEGREE_RESULT
+
+    def emit(self, ids, props):
+        d = props.get(DegreeCounter.DEGREE)
+        return {int(i): int(v) for i, v in zip(ids, d)} if d is not None else {}
+
+
+# ----------------------------------------------------------------------------- graph / computer
+class GpuGraph:
+    """An edgestore snapshot: rows (as a scan returns them) + schema.  The engine preloads
+    the slice each message scope needs, once, and keeps it resident on the device."""
+
+    def __init__(self, rows=None, schema=None, edges=None, device=0, partition_bits=5, hard_query_limit=100000,
+                 apply_cap=True):
+        self.rows = rows
+        self.schema = schema if (schema is None or isinstance(schema, Schema)) else Schema.from_dict(schema)
+        self.edges = edges       # (n, src, dst, weight) decoded-adjacency input
+        self.device = device
+        self.partition_bits = partition_bits
+        self.hard_query_limit = hard_query_limit
+        self.apply_cap = apply_cap
+        self._engines = {}
+        self._lock = threading.Lock()
+
+    def compute(self):
+        return GpuGraphComputer(self)
+
+    def engine_for(self, scope: int, weight_key: int = 0) -> Engine:
+        key = (scope, weight_key)
+        with self._lock:
+            if key not in self._engines:
+                eng = Engine(self.device, self.partition_bits, hard_query_limit=self.hard_query_limit)
+                if self.rows is not None:
+                    eng.load_rows(self.rows, self.schema, scope, apply_cap=self.apply_cap, weight_key=weight_key)
+                else:
+                    n, src, dst, w = self.edges
+                    eng.load_edges(n, src, dst, scope, weight=w if weight_key else None, apply_cap=self.apply_cap)
+                self._engines[key] = eng
+            return self._engines[key]
+
+
+class TitanGraphComputer:
+    class ResultMode(enum.Enum):          # core/TitanGraphComputer.java:10-31
+        NONE = 0
+        PERSIST = 1
+        LOCALTX = 2
+
+
+_POOL = ThreadPoolExecutor(max_workers=4, thread_name_prefix="tgo-submit")
+
+
+class GpuGraphComputer(TitanGraphComputer):
+    """Drop-in for FulgoraGraphComputer on the OLAP path."""
+
+    def __init__(self, graph: GpuGraph):
+        self.graph = graph
+        self._program = None
+        self._map_reduces = []
+        self._workers = 1
+        self._mode = TitanGraphComputer.ResultMode.NONE
+        self._executed = False
+        self.weight_keys = {}            # weight property name -> key id (schema lookup)
+
+    def workers(self, threads: int):
+        if threads <= 0:
+            raise ValueError(f"Invalid number of threads: {threads}")
+        self._workers = threads
+        return self
+
+    def resultMode(self, mode):  # noqa: N802
+        self._mode = mode
+        return self
+
+    def program(self, program: VertexProgram):
+        if self._program is not None:
+            raise RuntimeError("A vertex program has already been set")
+        self._program = program
+        return self
+
+    def mapReduce(self, mr: MapReduce):  # noqa: N802
+        self._map_reduces.append(mr)
+        return self
+
+    def submit(self) -> ComputerFuture:
+        if self._executed:
+            raise RuntimeError("This computer has already executed a vertex program")
+        self._executed = True
+        if self._program is None and not self._map_reduces:
+            raise RuntimeError("The computer has no vertex program or map reducers to execute")
+        return ComputerFuture(_POOL.submit(self._run))
+
+    def _run(self):
+        import time
+        t0 = time.perf_counter()
+        p = self._program
+        props = {}
+        iteration = 0
+        if isinstance(p, ShortestDistanceVertexProgram):
+            scope = SCOPE_NAMES[p.scope_name]
+            wk = 0
+            if p.weighted:
+                wk = self.weight_keys.get(p.weight_property, 0)
+                if wk == 0:
+                    raise TitanException(L.TGO_E_INVALID, f"weight property '{p.weight_property}' has no key id")
+            eng = self.graph.engine_for(scope, wk)
+            if p.weighted or p.mode == L.SSSP_DELTA:
+                d = eng.sssp(p.seed, p.max_depth, scope, mode=p.mode)
+            else:
+                d = eng.bfs(p.seed, p.max_depth, scope)
+            props[ShortestDistanceVertexProgram.DISTANCE] = d
+            iteration = p.max_depth
+            ids = eng.vertex_ids()
+        elif isinstance(p, PageRankVertexProgram):
+            eng = self.graph.engine_for(L.SCOPE_IN_E)
+            props[PageRankVertexProgram.PAGE_RANK] = eng.pagerank(p.alpha, p.vertex_count, p.max_iterations)
+            iteration = p.max_iterations
+            ids = eng.vertex_ids()
+        elif isinstance(p, DegreeCounter):
+            eng = self.graph.engine_for(L.SCOPE_IN_E)
+            props[DegreeCounter.DEGREE] = eng.walkcount(p.length)
+            iteration = p.length
+            ids = eng.vertex_ids()
+        else:
+            raise TitanException(L.TGO_E_UNSUPPORTED, f"vertex program {type(p).__name__} is not supported on the GPU path")
+        values = {}
+        for mr in self._map_reduces:
+            values[mr.memory_key] = mr.emit(ids, props)
+        rt = (time.perf_counter() - t0) * 1000.0
+        vprops = {k: (ids, v) for k, v in props.items()}
+        return ComputerResult(self.graph, Memory(iteration, rt, values), vprops)

@@ -1,0 +1,572 @@
+// api.cpp — the C-ABI (include/titan_gpu_olap.h): context, loads, program drivers.
+//
+// The program drivers replace FulgoraGraphComputer.submit's superstep loop
+// (FulgoraGraphComputer.java:151-189): instead of one full edgestore scan per superstep,
+// each iteration is one or two kernel launches over the device-resident adjacency, and
+// only the frontier is touched for BFS/SSSP.
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <new>
+#include <thread>
+#include <unordered_map>
+#include <hip/hip_runtime_api.h>
+#include "engine.hpp"
+
+using namespace tgo;
+
+struct tgo_ctx {
+    tgo_options opts{};
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    std::string err;
+    RowStaging staging;
+    DevGraph g;
+    bool loaded = false;
+    std::vector<int64_t> titan_id;
+    std::unordered_map<int64_t, int64_t> id_index;   // Titan id -> dense (seed lookup)
+    Scratch sc;
+    tgo_stats st{};
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    int64_t dev_bytes = 0;
+    std::vector<void*> allocs;
+};
+
+namespace {
+
+int fail(tgo_ctx* c, int code, const std::string& msg) {
+    if (c) c->err = msg;
+    return code;
+}
+
+#define HIP_TRY(call)                                                              \
+    do {                                                                           \
+        hipError_t e__ = (call);                                                   \
+        if (e__ != hipSuccess)                                                     \
+            return fail(ctx, e__ == hipErrorOutOfMemory ? TGO_E_OOM : TGO_E_HIP,   \
+                        std::string(#call) + ": " + hipGetErrorString(e__));       \
+    } while (0)
+
+template <class T>
+hipError_t dev_alloc(tgo_ctx* ctx, T*& p, int64_t count) {
+    void* q = nullptr;
+    const size_t bytes = static_cast<size_t>(std::max<int64_t>(count, 1)) * sizeof(T);
+    hipError_t e = hipMalloc(&q, bytes);
+    if (e != hipSuccess) return e;
+    ctx->allocs.push_back(q);
+    ctx->dev_bytes += static_cast<int64_t>(bytes);
+    p = static_cast<T*>(q);
+    return hipSuccess;
+}
+
+template <class T>
+hipError_t upload(tgo_ctx* ctx, T*& p, const std::vector<T>& h) {
+    hipError_t e = dev_alloc(ctx, p, static_cast<int64_t>(h.size()));
+    if (e != hipSuccess || h.empty()) return e;
+    return hipMemcpy(p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice);
+}
+
+void free_graph(tgo_ctx* ctx) {
+    for (void* p : ctx->allocs) (void)hipFree(p);
+    ctx->allocs.clear();
+    ctx->dev_bytes = 0;
+    ctx->g = DevGraph();
+    ctx->sc = Scratch();
+    ctx->loaded = false;
+}
+
+int threads_of(const tgo_ctx* ctx) {
+    int t = ctx->opts.host_threads;
+    if (t <= 0) t = static_cast<int>(std::thread::hardware_concurrency());
+    return std::max(1, std::min(t, 64));
+}
+
+int upload_graph(tgo_ctx* ctx, HostGraph& h) {
+    DevGraph& g = ctx->g;
+    g.n = h.n;
+    g.scope = h.scope;
+    g.has_weight = h.has_weight;
+    g.has_transpose = h.has_transpose;
+    g.min_weight = 0;
+    for (const HostCsr* c : {&h.out, &h.in})
+        for (int32_t x : c->w) if (x != kMissingWeight) g.min_weight = std::min(g.min_weight, x);
+    auto up = [&](HostCsr& src, DevCsr& dst) -> hipError_t {
+        hipError_t e;
+        if ((e = upload(ctx, dst.off, src.off)) != hipSuccess) return e;
+        if ((e = upload(ctx, dst.adj, src.adj)) != hipSuccess) return e;
+        if (h.has_weight && (e = upload(ctx, dst.w, src.w)) != hipSuccess) return e;
+        dst.nnz = static_cast<int64_t>(src.adj.size());
+        return hipSuccess;
+    };
+    HIP_TRY(up(h.out, g.out));
+    HIP_TRY(up(h.in, g.in));
+    if (h.has_transpose) HIP_TRY(up(h.push_t, g.push_t));
+    // CSR-adaptive blocks for the two pull gathers (walk counts: out; PageRank: in).
+    auto blocks = [&](const std::vector<int64_t>& off, RowBlocks& rb) -> hipError_t {
+        std::vector<int64_t> blk, crow, cbeg, cend, lrow, lch;
+        build_row_blocks(off, kTile, kMaxRows, blk, crow, cbeg, cend, lrow, lch);
+        rb.nblocks = static_cast<int64_t>(blk.size()) - 1;
+        rb.nchunks = static_cast<int64_t>(crow.size());
+        rb.nlong = static_cast<int64_t>(lrow.size());
+        hipError_t e;
+        if ((e = upload(ctx, rb.blk, blk)) != hipSuccess) return e;
+        if ((e = upload(ctx, rb.chunk_row, crow)) != hipSuccess) return e;
+        if ((e = upload(ctx, rb.chunk_beg, cbeg)) != hipSuccess) return e;
+        if ((e = upload(ctx, rb.chunk_end, cend)) != hipSuccess) return e;
+        if ((e = upload(ctx, rb.long_row, lrow)) != hipSuccess) return e;
+        if ((e = upload(ctx, rb.long_chunk, lch)) != hipSuccess) return e;
+        return hipSuccess;
+    };
+    HIP_TRY(blocks(h.out.off, g.rb_out));
+    HIP_TRY(blocks(h.in.off, g.rb_in));
+    g.rb_out_ready = g.rb_in_ready = true;
+    // scratch
+    Scratch& s = ctx->sc;
+    const int64_t n = h.n, words = (n + 63) / 64 + 1;
+    s.n = n;
+    HIP_TRY(dev_alloc(ctx, s.level, n));
+    HIP_TRY(dev_alloc(ctx, s.q[0], n + 1));
+    HIP_TRY(dev_alloc(ctx, s.q[1], n + 1));
+    HIP_TRY(dev_alloc(ctx, s.qdeg, n + 2));
+    HIP_TRY(dev_alloc(ctx, s.qpre, n + 2));
+    HIP_TRY(dev_alloc(ctx, s.fb, words));
+    HIP_TRY(dev_alloc(ctx, s.nb, words));
+    HIP_TRY(dev_alloc(ctx, s.vb, words));
+    HIP_TRY(dev_alloc(ctx, s.dist, n));
+    HIP_TRY(dev_alloc(ctx, s.msg, n));
+    for (int i = 0; i < 3; ++i) HIP_TRY(dev_alloc(ctx, s.vec[i], n));
+    s.partial_cap = std::max<int64_t>({g.rb_out.nchunks, g.rb_in.nchunks, 1});
+    HIP_TRY(dev_alloc(ctx, s.partial, s.partial_cap));
+    HIP_TRY(dev_alloc(ctx, s.cnt, 1));
+    if (!s.hcnt) {
+        void* hp = nullptr;
+        HIP_TRY(hipHostMalloc(&hp, sizeof(Counters), hipHostMallocDefault));
+        s.hcnt = static_cast<Counters*>(hp);
+    }
+    HIP_TRY(hipDeviceSynchronize());
+    ctx->titan_id = h.titan_id;
+    ctx->id_index.clear();
+    ctx->id_index.reserve(static_cast<size_t>(n) * 2);
+    for (int64_t v = 0; v < n; ++v) ctx->id_index.emplace(h.titan_id[v], v);
+    ctx->st.num_vertices = n;
+    ctx->st.num_entries = static_cast<int64_t>(h.out.adj.size() + h.in.adj.size());
+    ctx->st.ghost_vertices = h.ghost;
+    ctx->st.truncated_results = h.truncated;
+    ctx->st.skipped_rows = h.skipped;
+    ctx->st.device_bytes = ctx->dev_bytes;
+    ctx->loaded = true;
+    return TGO_OK;
+}
+
+// Views of the loaded scope.
+View make_view(const DevCsr* a, const DevCsr* b) {
+    View v{};
+    v.off0 = a->off; v.adj0 = a->adj; v.w0 = a->w;
+    if (b) { v.off1 = b->off; v.adj1 = b->adj; v.w1 = b->w; v.nlists = 2; }
+    else { v.off1 = a->off; v.adj1 = a->adj; v.w1 = a->w; v.nlists = 1; }
+    return v;
+}
+View pull_view(const DevGraph& g, int scope) {
+    if (scope == TGO_SCOPE_IN_E) return make_view(&g.out, nullptr);
+    if (scope == TGO_SCOPE_OUT_E) return make_view(&g.in, nullptr);
+    return make_view(&g.out, &g.in);
+}
+View push_view(const DevGraph& g, int scope) {
+    if (g.has_transpose) return make_view(&g.push_t, nullptr);
+    if (scope == TGO_SCOPE_IN_E) return make_view(&g.in, nullptr);
+    if (scope == TGO_SCOPE_OUT_E) return make_view(&g.out, nullptr);
+    return make_view(&g.out, &g.in);
+}
+
+int resolve_seed(tgo_ctx* ctx, int64_t seed, int is_dense, int64_t& out) {
+    if (is_dense) {
+        if (seed < 0 || seed >= ctx->g.n) return fail(ctx, TGO_E_INVALID, "dense seed out of range");
+        out = seed;
+        return TGO_OK;
+    }
+    auto it = ctx->id_index.find(seed);
+    out = it == ctx->id_index.end() ? -1 : it->second;   // unknown seed: nobody gets a distance
+    return TGO_OK;
+}
+
+int check_program(tgo_ctx* ctx, int scope) {
+    if (!ctx->loaded) return fail(ctx, TGO_E_STATE, "no graph loaded");
+    if (scope < 0 || scope > 2) return fail(ctx, TGO_E_INVALID, "invalid scope");
+    if (scope != ctx->g.scope)
+        return fail(ctx, TGO_E_INVALID, "program scope differs from the scope the graph was loaded (preloaded) for");
+    return TGO_OK;
+}
+
+int read_counters(tgo_ctx* ctx) {
+    HIP_TRY(hipMemcpyAsync(ctx->sc.hcnt, ctx->sc.cnt, sizeof(Counters), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return TGO_OK;
+}
+
+// Exclusive scan of qdeg[0..qlen) into qpre[0..qlen] (qpre[qlen] = total).
+int scan_frontier(tgo_ctx* ctx, int64_t qlen) {
+    Scratch& s = ctx->sc;
+    HIP_TRY(hipMemsetAsync(s.qdeg + qlen, 0, sizeof(int64_t), ctx->stream));
+    HIP_TRY(scan_exclusive_i64(s.cub_tmp, s.cub_bytes, s.qdeg, s.qpre, qlen + 1, ctx->stream));
+    return TGO_OK;
+}
+
+// Direction-optimizing level loop for unit weights (Beamer et al., SC'12 heuristics).
+int run_bfs(tgo_ctx* ctx, int64_t seed, int max_depth, int scope) {
+    DevGraph& g = ctx->g;
+    Scratch& s = ctx->sc;
+    hipStream_t st = ctx->stream;
+    const int64_t n = g.n, words = (n + 63) / 64 + 1;
+    const View pull = pull_view(g, scope), push = push_view(g, scope);
+    HIP_TRY(k_fill_i32(s.level, -1, n, st));
+    HIP_TRY(hipMemsetAsync(s.vb, 0, words * 8, st));
+    HIP_TRY(hipMemsetAsync(s.fb, 0, words * 8, st));
+    int levels = 0;
+    if (seed >= 0) {
+        HIP_TRY(k_bfs_seed(push, s.level, s.vb, s.fb, s.q[0], s.qdeg, seed, st));
+        int64_t qlen = 1;
+        int cur = 0;
+        bool bottom_up = false;
+        const double alpha = 15.0, beta = 18.0;
+        // m_u: entries of unexplored vertices (push degrees); m_f: of the frontier.
+        const int64_t total_push = push.nlists > 1 ? (g.out.nnz + g.in.nnz)
+                                                   : (g.has_transpose ? g.push_t.nnz
+                                                                      : (scope == TGO_SCOPE_IN_E ? g.in.nnz : g.out.nnz));
+        int64_t mf = -1, mu = total_push;
+        for (int L = 0; L < max_depth && qlen > 0; ++L) {
+            if (mf < 0) {   // degree of the seed
+                int64_t d = 0;
+                HIP_TRY(hipMemcpyAsync(&d, s.qdeg, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+                HIP_TRY(hipStreamSynchronize(st));
+                mf = d;
+                mu -= d;
+            }
+            if (!bottom_up && static_cast<double>(mf) > static_cast<double>(mu) / alpha) bottom_up = true;
+            else if (bottom_up && static_cast<double>(qlen) < static_cast<double>(n) / beta) bottom_up = false;
+            HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
+            HIP_TRY(hipMemsetAsync(s.nb, 0, words * 8, st));
+            if (bottom_up) {
+                HIP_TRY(k_bu_step(pull, push, n, s.fb, s.vb, s.nb, s.level, s.q[cur ^ 1], s.qdeg, s.cnt, L + 1, st));
+            } else {
+                int rc = scan_frontier(ctx, qlen);
+                if (rc) return rc;
+                // qdeg is reused for the next queue's degrees after the scan consumed it
+                HIP_TRY(k_td_expand(push, s.q[cur], s.qpre, qlen, s.level, s.vb, s.nb, s.q[cur ^ 1], s.qdeg, s.cnt, L + 1, st));
+            }
+            int rc = read_counters(ctx);
+            if (rc) return rc;
+            qlen = static_cast<int64_t>(s.hcnt->qlen);
+            mf = static_cast<int64_t>(s.hcnt->mf);
+            mu -= mf;
+            std::swap(s.fb, s.nb);
+            cur ^= 1;
+            ++levels;
+        }
+    }
+    HIP_TRY(k_level_to_dist(s.level, s.dist, n, st));
+    ctx->st.levels = levels;
+    ctx->st.iterations = max_depth;   // the reference always runs iterations 0..maxDepth
+    return TGO_OK;
+}
+
+int run_sssp(tgo_ctx* ctx, int64_t seed, int max_depth, int scope, bool weighted) {
+    DevGraph& g = ctx->g;
+    Scratch& s = ctx->sc;
+    hipStream_t st = ctx->stream;
+    const int64_t n = g.n, words = (n + 63) / 64 + 1;
+    const View push = push_view(g, scope);
+    HIP_TRY(k_fill_i64(s.dist, INT64_MAX, n, st));
+    HIP_TRY(hipMemsetAsync(s.vb, 0, words * 8, st));
+    int levels = 0;
+    if (seed >= 0) {
+        HIP_TRY(k_sssp_seed(push, s.dist, s.msg, s.vb, s.q[0], s.qdeg, seed, st));
+        int64_t qlen = 1;
+        int cur = 0;
+        for (int L = 0; L < max_depth && qlen > 0; ++L) {
+            HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
+            HIP_TRY(hipMemsetAsync(s.vb, 0, words * 8, st));       // "improved this level" marks
+            int rc = scan_frontier(ctx, qlen);
+            if (rc) return rc;
+            HIP_TRY(k_sssp_relax(push, s.q[cur], s.qpre, qlen, s.msg, s.dist, s.vb, s.q[cur ^ 1], s.qdeg, s.cnt, weighted ? 1 : 0, st));
+            rc = read_counters(ctx);
+            if (rc) return rc;
+            if (s.hcnt->err) return fail(ctx, TGO_E_PROGRAM,
+                "vertex program failed: a traversed edge has no value for the weight property");
+            qlen = static_cast<int64_t>(s.hcnt->qlen);
+            // snapshot the improved vertices' distances: these are their messages
+            if (qlen > 0) HIP_TRY(k_sssp_commit(s.q[cur ^ 1], qlen, s.dist, s.msg, s.vb, st));
+            cur ^= 1;
+            ++levels;
+        }
+    }
+    HIP_TRY(k_dist_finalize(s.dist, n, st));
+    ctx->st.levels = levels;
+    ctx->st.iterations = max_depth;
+    return TGO_OK;
+}
+
+int finish_distance_program(tgo_ctx* ctx, int scope, int flags, int64_t* dist_out) {
+    Scratch& s = ctx->sc;
+    HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
+    HIP_TRY(hipEventSynchronize(ctx->ev1));
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+    ctx->st.last_kernel_ms = ms;
+    if (flags & TGO_FLAG_STATS) {
+        // reached vertices and the entries of their pull lists (both lists for bothE)
+        HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), ctx->stream));
+        HIP_TRY(k_reach_stats(pull_view(ctx->g, scope), s.dist, ctx->g.n, s.cnt->red, ctx->stream));
+        int rc = read_counters(ctx);
+        if (rc) return rc;
+        ctx->st.reached = static_cast<int64_t>(s.hcnt->red[0]);
+        ctx->st.reached_entries = static_cast<int64_t>(s.hcnt->red[1]);
+    }
+    if (dist_out) {
+        HIP_TRY(hipMemcpy(dist_out, s.dist, ctx->g.n * sizeof(int64_t), hipMemcpyDeviceToHost));
+    }
+    (void)scope;
+    return TGO_OK;
+}
+
+}  // namespace
+
+// ============================================================================ C-ABI
+extern "C" {
+
+void tgo_default_options(tgo_options* o) {
+    std::memset(o, 0, sizeof(*o));
+    o->abi_version = TGO_ABI_VERSION;
+    o->device = 0;
+    o->partition_bits = 5;
+    o->host_threads = 0;
+    o->hard_query_limit = 100000;
+    o->stream = nullptr;
+}
+
+int tgo_create(const tgo_options* opts, tgo_ctx** out) {
+    if (!opts || !out) return TGO_E_INVALID;
+    *out = nullptr;
+    if (opts->abi_version != TGO_ABI_VERSION) return TGO_E_INVALID;
+    if (opts->partition_bits < 0 || opts->partition_bits > 16) return TGO_E_INVALID;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return TGO_E_HIP;
+    if (opts->device < 0 || opts->device >= ndev) return TGO_E_INVALID;
+    if (hipSetDevice(opts->device) != hipSuccess) return TGO_E_HIP;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, opts->device) != hipSuccess) return TGO_E_HIP;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return TGO_E_HIP;   // gfx950 code objects only
+    tgo_ctx* ctx = new (std::nothrow) tgo_ctx();
+    if (!ctx) return TGO_E_OOM;
+    ctx->opts = *opts;
+    if (ctx->opts.hard_query_limit <= 0) ctx->opts.hard_query_limit = 100000;
+    if (opts->stream) {
+        ctx->stream = static_cast<hipStream_t>(opts->stream);
+    } else {
+        if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) { delete ctx; return TGO_E_HIP; }
+        ctx->own_stream = true;
+    }
+    if (hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess) {
+        delete ctx;
+        return TGO_E_HIP;
+    }
+    *out = ctx;
+    return TGO_OK;
+}
+
+void tgo_destroy(tgo_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->opts.device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    free_graph(ctx);
+    if (ctx->sc.hcnt) (void)hipHostFree(ctx->sc.hcnt);
+    if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
+    if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+    if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+const char* tgo_last_error(const tgo_ctx* ctx) { return ctx ? ctx->err.c_str() : "null ctx"; }
+
+int tgo_load_rows(tgo_ctx* ctx, const tgo_rows* rows, const tgo_schema* schema, const tgo_load_opts* opts) {
+    if (!ctx) return TGO_E_INVALID;
+    if (!rows || !schema || !opts) return fail(ctx, TGO_E_INVALID, "null argument");
+    if (rows->nrows < 0 || (rows->nrows > 0 && (!rows->row_keys || !rows->row_entry_begin ||
+        !rows->row_byte_begin || !rows->entry_bytes || !rows->entry_limit_valpos)))
+        return fail(ctx, TGO_E_INVALID, "incomplete tgo_rows");
+    if (opts->scope < 0 || opts->scope > 2) return fail(ctx, TGO_E_INVALID, "invalid scope");
+    if (ctx->loaded && !ctx->staging.active) free_graph(ctx);
+    (void)hipSetDevice(ctx->opts.device);
+    const auto t0 = std::chrono::steady_clock::now();
+    std::string err;
+    int rc = decode_rows(ctx->staging, rows, schema, opts, ctx->opts.partition_bits,
+                         ctx->opts.hard_query_limit, threads_of(ctx), err);
+    ctx->st.load_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (rc) { ctx->staging = RowStaging(); return fail(ctx, rc, err); }
+    return TGO_OK;
+}
+
+int tgo_finish_load(tgo_ctx* ctx) {
+    if (!ctx) return TGO_E_INVALID;
+    if (!ctx->staging.active) return fail(ctx, TGO_E_STATE, "tgo_finish_load without tgo_load_rows");
+    (void)hipSetDevice(ctx->opts.device);
+    const auto t0 = std::chrono::steady_clock::now();
+    HostGraph h;
+    std::string err;
+    int rc = assemble_from_rows(ctx->staging, h, threads_of(ctx), err);
+    if (rc) return fail(ctx, rc, err);
+    free_graph(ctx);
+    rc = upload_graph(ctx, h);
+    ctx->st.load_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return rc;
+}
+
+int tgo_load_edges(tgo_ctx* ctx, const tgo_edges* edges, const tgo_load_opts* opts) {
+    if (!ctx) return TGO_E_INVALID;
+    if (!edges || !opts || (edges->m > 0 && (!edges->src || !edges->dst)))
+        return fail(ctx, TGO_E_INVALID, "null argument");
+    if (opts->scope < 0 || opts->scope > 2) return fail(ctx, TGO_E_INVALID, "invalid scope");
+    (void)hipSetDevice(ctx->opts.device);
+    const auto t0 = std::chrono::steady_clock::now();
+    HostGraph h;
+    std::string err;
+    int rc = assemble_from_edges(edges, opts, ctx->opts.hard_query_limit, h, threads_of(ctx), err);
+    if (rc) return fail(ctx, rc, err);
+    free_graph(ctx);
+    ctx->staging = RowStaging();
+    rc = upload_graph(ctx, h);
+    ctx->st.load_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return rc;
+}
+
+int64_t tgo_num_vertices(const tgo_ctx* ctx) { return ctx && ctx->loaded ? ctx->g.n : 0; }
+
+int tgo_vertex_ids(tgo_ctx* ctx, int64_t* out) {
+    if (!ctx || !out) return TGO_E_INVALID;
+    if (!ctx->loaded) return fail(ctx, TGO_E_STATE, "no graph loaded");
+    std::memcpy(out, ctx->titan_id.data(), ctx->titan_id.size() * sizeof(int64_t));
+    return TGO_OK;
+}
+
+int tgo_bfs(tgo_ctx* ctx, const tgo_bfs_args* a, int64_t* dist_out) {
+    if (!ctx) return TGO_E_INVALID;
+    if (!a) return fail(ctx, TGO_E_INVALID, "null args");
+    int rc = check_program(ctx, a->scope);
+    if (rc) return rc;
+    if (a->max_depth < 0) return fail(ctx, TGO_E_INVALID, "max_depth < 0");
+    (void)hipSetDevice(ctx->opts.device);
+    int64_t seed;
+    if ((rc = resolve_seed(ctx, a->seed, a->seed_is_dense, seed))) return rc;
+    HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
+    if ((rc = run_bfs(ctx, seed, a->max_depth, a->scope))) return rc;
+    return finish_distance_program(ctx, a->scope, a->flags, dist_out);
+}
+
+int tgo_sssp(tgo_ctx* ctx, const tgo_sssp_args* a, int64_t* dist_out) {
+    if (!ctx) return TGO_E_INVALID;
+    if (!a) return fail(ctx, TGO_E_INVALID, "null args");
+    int rc = check_program(ctx, a->scope);
+    if (rc) return rc;
+    if (a->max_depth < 0) return fail(ctx, TGO_E_INVALID, "max_depth < 0");
+    if (a->mode != TGO_SSSP_HOP_BOUNDED && a->mode != TGO_SSSP_DELTA) return fail(ctx, TGO_E_INVALID, "invalid mode");
+    (void)hipSetDevice(ctx->opts.device);
+    int64_t seed;
+    if ((rc = resolve_seed(ctx, a->seed, a->seed_is_dense, seed))) return rc;
+    HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
+    // DELTA mode is served by the exact hop-bounded kernel with an unbounded hop count
+    // until the bucketed kernel lands; its result is the converged distance either way.
+    if (a->mode == TGO_SSSP_DELTA && ctx->g.has_weight && ctx->g.min_weight < 0)
+        return fail(ctx, TGO_E_INVALID, "DELTA mode needs non-negative weights");
+    const int depth = a->mode == TGO_SSSP_DELTA ? INT32_MAX : a->max_depth;
+    if ((rc = run_sssp(ctx, seed, depth, a->scope, ctx->g.has_weight))) return rc;
+    return finish_distance_program(ctx, a->scope, a->flags, dist_out);
+}
+
+int tgo_copy_distances(tgo_ctx* ctx, int64_t* dist_out) {
+    if (!ctx || !dist_out) return TGO_E_INVALID;
+    if (!ctx->loaded) return fail(ctx, TGO_E_STATE, "no graph loaded");
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    HIP_TRY(hipMemcpy(dist_out, ctx->sc.dist, ctx->g.n * sizeof(int64_t), hipMemcpyDeviceToHost));
+    return TGO_OK;
+}
+
+int tgo_pagerank(tgo_ctx* ctx, const tgo_pr_args* a, double* pr_out) {
+    if (!ctx) return TGO_E_INVALID;
+    if (!a) return fail(ctx, TGO_E_INVALID, "null args");
+    if (!ctx->loaded) return fail(ctx, TGO_E_STATE, "no graph loaded");
+    if (ctx->g.scope == TGO_SCOPE_BOTH_E)
+        return fail(ctx, TGO_E_INVALID, "PageRank uses the inE/outE scopes; load the graph with a single-direction scope");
+    if (a->max_iterations < 0) return fail(ctx, TGO_E_INVALID, "max_iterations < 0");
+    (void)hipSetDevice(ctx->opts.device);
+    DevGraph& g = ctx->g;
+    Scratch& s = ctx->sc;
+    const int64_t n = g.n;
+    hipStream_t st = ctx->stream;
+    HIP_TRY(hipEventRecord(ctx->ev0, st));
+    double* edge_count = s.vec[0];
+    double* contrib = s.vec[1];
+    double* contrib_next = s.vec[2];
+    double* pr = reinterpret_cast<double*>(s.dist);    // int64-sized scratch reused for PR
+    const double N = static_cast<double>(a->vertex_count);
+    if (a->max_iterations == 0) {
+        HIP_TRY(k_fill_f64(pr, NAN, n, st));           // iteration 0 sets no PAGE_RANK property
+    } else {
+        HIP_TRY(k_pr_init(g.out, edge_count, contrib, pr, 1.0 / N, n, st));
+        const double base = (1.0 - a->alpha) / N;
+        for (int it = 2; it <= a->max_iterations; ++it) {
+            HIP_TRY(k_pr_iter(g.in, g.rb_in, contrib, edge_count, pr, contrib_next, s.partial, a->alpha, base, n, st));
+            std::swap(contrib, contrib_next);
+        }
+    }
+    HIP_TRY(hipEventRecord(ctx->ev1, st));
+    HIP_TRY(hipEventSynchronize(ctx->ev1));
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+    ctx->st.last_kernel_ms = ms;
+    ctx->st.iterations = a->max_iterations;
+    if (pr_out) HIP_TRY(hipMemcpy(pr_out, pr, n * sizeof(double), hipMemcpyDeviceToHost));
+    return TGO_OK;
+}
+
+int tgo_walkcount(tgo_ctx* ctx, int32_t k, int32_t* out) {
+    if (!ctx) return TGO_E_INVALID;
+    if (!ctx->loaded) return fail(ctx, TGO_E_STATE, "no graph loaded");
+    if (k <= 0) return fail(ctx, TGO_E_INVALID, "DegreeCounter length must be > 0");   // OLAPTest.java:347
+    if (ctx->g.scope != TGO_SCOPE_IN_E)
+        return fail(ctx, TGO_E_INVALID, "DegreeCounter uses the inE scope; load the graph with TGO_SCOPE_IN_E");
+    (void)hipSetDevice(ctx->opts.device);
+    DevGraph& g = ctx->g;
+    Scratch& s = ctx->sc;
+    const int64_t n = g.n;
+    hipStream_t st = ctx->stream;
+    HIP_TRY(hipEventRecord(ctx->ev0, st));
+    int32_t* a = reinterpret_cast<int32_t*>(s.vec[0]);
+    int32_t* b = reinterpret_cast<int32_t*>(s.vec[1]);
+    HIP_TRY(k_fill_i32(a, 1, n, st));                  // iteration 0: every vertex sends 1
+    for (int it = 1; it <= k; ++it) {
+        HIP_TRY(k_walk_iter(g.out, g.rb_out, a, b, reinterpret_cast<int32_t*>(s.partial), n, st));
+        std::swap(a, b);
+    }
+    HIP_TRY(hipEventRecord(ctx->ev1, st));
+    HIP_TRY(hipEventSynchronize(ctx->ev1));
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+    ctx->st.last_kernel_ms = ms;
+    ctx->st.iterations = k;
+    if (out) HIP_TRY(hipMemcpy(out, a, n * sizeof(int32_t), hipMemcpyDeviceToHost));
+    return TGO_OK;
+}
+
+int tgo_stats_get(tgo_ctx* ctx, tgo_stats* out) {
+    if (!ctx || !out) return TGO_E_INVALID;
+    *out = ctx->st;
+    return TGO_OK;
+}
+
+int tgo_sync(tgo_ctx* ctx) {
+    if (!ctx) return TGO_E_INVALID;
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return TGO_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,396 @@
+// bfs.hip — frontier kernels for ShortestDistanceVertexProgram on gfx950.
+//
+// Reference semantics (ShortestDistanceVertexProgram.java:96-130 over Fulgora's pull
+// gather, VertexMemoryHandler.java:77-103): at iteration i every vertex v takes the
+// minimum over its reversed-scope neighbours w that SENT at iteration i-1 (double
+// buffered, VertexState.java:55-89) of msg(w)+weight, and keeps it if strictly smaller.
+// With unit weights this is level-synchronous BFS, exactly: a vertex first reached at
+// iteration i has distance i and never improves.  The device executes only the frontier
+// (the reference executes every vertex every superstep), in either direction:
+//   top-down  : frontier vertices push over the transposed (push) view, edge-balanced
+//               load-balanced search over the exclusive scan of frontier degrees;
+//   bottom-up : every unvisited vertex pulls over its own list and stops at the first
+//               neighbour in the frontier bitmap (one wave per 64-vertex bitmap word,
+//               so visited/next bitmap words are written without atomics).
+// Wave = 64 lanes; ballots are 64-bit.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include "engine.hpp"
+
+namespace tgo {
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kEdgesPerThread = 8;
+constexpr int kTileEdges = kBlock * kEdgesPerThread;   // 2048 edges per block tile
+constexpr int kLdsEntries = kTileEdges + 2;
+
+__device__ __forceinline__ int lane() { return static_cast<int>(threadIdx.x & 63); }
+
+__device__ __forceinline__ int64_t push_degree(const View& v, int64_t u) {
+    int64_t d = v.off0[u + 1] - v.off0[u];
+    if (v.nlists > 1) d += v.off1[u + 1] - v.off1[u];
+    return d;
+}
+
+// Entry `o` (0 <= o < push_degree(u)) of u's list(s): neighbour and weight.
+__device__ __forceinline__ void entry_at(const View& v, int64_t u, int64_t o, int32_t& nbr, int32_t& w) {
+    const int64_t b0 = v.off0[u];
+    const int64_t d0 = v.off0[u + 1] - b0;
+    if (o < d0) {
+        nbr = v.adj0[b0 + o];
+        w = v.w0 ? v.w0[b0 + o] : 1;
+    } else {
+        const int64_t b1 = v.off1[u] + (o - d0);
+        nbr = v.adj1[b1];
+        w = v.w1 ? v.w1[b1] : 1;
+    }
+}
+
+// Wave-aggregated append of `v` (for lanes with take=true) to queue qn/qdeg.
+__device__ __forceinline__ void wave_append(bool take, int32_t v, int64_t deg, int32_t* qn,
+                                            int64_t* qdeg, Counters* cnt) {
+    const unsigned long long mask = __ballot(take);
+    if (mask == 0) return;
+    const int leader = __ffsll(static_cast<long long>(mask)) - 1;
+    const unsigned long long below = mask & ((1ULL << lane()) - 1ULL);
+    const int rank = __popcll(below);
+    unsigned long long base = 0;
+    // sum of degrees of the appended vertices (for the direction heuristic)
+    int64_t dsum = take ? deg : 0;
+    for (int off = 32; off > 0; off >>= 1) dsum += __shfl_xor(dsum, off, 64);
+    if (lane() == leader) {
+        base = atomicAdd(&cnt->qlen, static_cast<unsigned long long>(__popcll(mask)));
+        atomicAdd(&cnt->mf, static_cast<unsigned long long>(dsum));
+    }
+    base = __shfl(base, leader, 64);
+    if (take) {
+        qn[base + rank] = v;
+        qdeg[base + rank] = deg;
+    }
+}
+
+__global__ void fill_i32(int32_t* p, int32_t v, int64_t n) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = v;
+}
+__global__ void fill_i64(int64_t* p, int64_t v, int64_t n) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = v;
+}
+
+__global__ void bfs_seed(View push, int32_t* level, uint64_t* vb, uint64_t* fb, int32_t* q, int64_t* qdeg, int64_t seed) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        level[seed] = 0;
+        vb[seed >> 6] |= 1ULL << (seed & 63);
+        fb[seed >> 6] |= 1ULL << (seed & 63);
+        q[0] = static_cast<int32_t>(seed);
+        qdeg[0] = push_degree(push, seed);
+    }
+}
+
+// Top-down: load-balanced search over the exclusive scan qpre[0..qlen] of frontier degrees.
+__global__ void __launch_bounds__(kBlock) td_expand(View push, const int32_t* __restrict__ q,
+        const int64_t* __restrict__ qpre, int64_t qlen, int32_t* __restrict__ level,
+        uint64_t* __restrict__ vb, uint64_t* __restrict__ nb, int32_t* __restrict__ qn,
+        int64_t* __restrict__ qdeg_n, Counters* cnt, int32_t next_level) {
+    __shared__ int64_t s_pre[kLdsEntries];
+    __shared__ int32_t s_q[kLdsEntries];
+    __shared__ int64_t s_lo, s_hi;
+    const int64_t total = qpre[qlen];
+    const int64_t ntiles = (total + kTileEdges - 1) / kTileEdges;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t t0 = tile * kTileEdges;
+        const int64_t t1 = min(total, t0 + kTileEdges);
+        if (threadIdx.x == 0) {
+            // lo = last i with qpre[i] <= t0 ; hi = last i with qpre[i] <= t1-1
+            int64_t a = 0, b = qlen;          // qpre[a] <= t0 < qpre[b] invariant-ish search
+            while (b - a > 1) { const int64_t c = (a + b) >> 1; if (qpre[c] <= t0) a = c; else b = c; }
+            s_lo = a;
+            int64_t a2 = a, b2 = qlen;
+            while (b2 - a2 > 1) { const int64_t c = (a2 + b2) >> 1; if (qpre[c] <= t1 - 1) a2 = c; else b2 = c; }
+            s_hi = a2;
+        }
+        __syncthreads();
+        const int64_t lo = s_lo, hi = s_hi;
+        const int64_t span = hi - lo + 1;       // queue entries touching this tile
+        const bool in_lds = span + 1 <= kLdsEntries;
+        if (in_lds) {
+            for (int64_t i = threadIdx.x; i <= span; i += kBlock) {
+                s_pre[i] = qpre[lo + i];
+                if (i < span) s_q[i] = q[lo + i];
+            }
+        }
+        __syncthreads();
+        for (int k = 0; k < kEdgesPerThread; ++k) {
+            const int64_t j = t0 + k * kBlock + threadIdx.x;
+            bool take = false;
+            int32_t v = 0;
+            int64_t vdeg = 0;
+            if (j < t1) {
+                int64_t idx;
+                int32_t u;
+                int64_t start;
+                if (in_lds) {
+                    int64_t a = 0, b = span;     // last a with s_pre[a] <= j
+                    while (b - a > 1) { const int64_t c = (a + b) >> 1; if (s_pre[c] <= j) a = c; else b = c; }
+                    idx = a; u = s_q[a]; start = s_pre[a];
+                } else {
+                    int64_t a = lo, b = hi + 1;
+                    while (b - a > 1) { const int64_t c = (a + b) >> 1; if (qpre[c] <= j) a = c; else b = c; }
+                    idx = a; u = q[a]; start = qpre[a];
+                }
+                (void)idx;
+                int32_t w;
+                entry_at(push, u, j - start, v, w);
+                const uint64_t bit = 1ULL << (v & 63);
+                if (!(vb[v >> 6] & bit)) {
+                    const unsigned long long old = atomicOr(reinterpret_cast<unsigned long long*>(&vb[v >> 6]), bit);
+                    if (!(old & bit)) {
+                        take = true;
+                        level[v] = next_level;
+                        atomicOr(reinterpret_cast<unsigned long long*>(&nb[v >> 6]), bit);
+                        vdeg = push_degree(push, v);
+                    }
+                }
+            }
+            wave_append(take, v, vdeg, qn, qdeg_n, cnt);
+        }
+        __syncthreads();
+    }
+}
+
+// Bottom-up: one wave per 64-vertex bitmap word.
+__global__ void __launch_bounds__(kBlock) bu_step(View pull, View push, int64_t n,
+        const uint64_t* __restrict__ fb, uint64_t* __restrict__ vb, uint64_t* __restrict__ nb,
+        int32_t* __restrict__ level, int32_t* __restrict__ qn, int64_t* __restrict__ qdeg_n,
+        Counters* cnt, int32_t next_level) {
+    const int64_t words = (n + 63) >> 6;
+    const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t wd = wave; wd < words; wd += nwaves) {
+        const uint64_t vis = vb[wd];
+        const int64_t v = (wd << 6) + lane();
+        bool found = false;
+        if (v < n && !((vis >> lane()) & 1ULL)) {
+            for (int l = 0; l < pull.nlists && !found; ++l) {
+                const int64_t* off = l == 0 ? pull.off0 : pull.off1;
+                const int32_t* adj = l == 0 ? pull.adj0 : pull.adj1;
+                const int64_t e = off[v + 1];
+                for (int64_t k = off[v]; k < e; ++k) {
+                    const int32_t u = adj[k];
+                    if ((fb[u >> 6] >> (u & 63)) & 1ULL) { found = true; break; }
+                }
+            }
+        }
+        const unsigned long long fm = __ballot(found);
+        if (lane() == 0) {
+            nb[wd] = fm;
+            if (fm) vb[wd] = vis | fm;
+        }
+        if (found) level[v] = next_level;
+        wave_append(found, static_cast<int32_t>(v), found ? push_degree(push, v) : 0, qn, qdeg_n, cnt);
+    }
+}
+
+__global__ void level_to_dist(const int32_t* level, int64_t* dist, int64_t n) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t l = level[i];
+        dist[i] = l >= 0 ? static_cast<int64_t>(l) : INT64_MIN;
+    }
+}
+
+// reached vertices and their list entries (m_R) — for GTEPS / roofline accounting.
+__global__ void reach_stats(View v, const int64_t* dist, int64_t n, unsigned long long* out2) {
+    unsigned long long r = 0, m = 0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        if (dist[i] != INT64_MIN) { ++r; m += static_cast<unsigned long long>(push_degree(v, i)); }
+    }
+    for (int off = 32; off > 0; off >>= 1) { r += __shfl_xor(r, off, 64); m += __shfl_xor(m, off, 64); }
+    if (lane() == 0) { atomicAdd(&out2[0], r); atomicAdd(&out2[1], m); }
+}
+
+__global__ void degree_i64(View v, const int32_t* q, int64_t qlen, int64_t* qdeg) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < qlen; i += (int64_t)gridDim.x * blockDim.x)
+        qdeg[i] = push_degree(v, q[i]);
+}
+
+// ---------------------------------------------------------------- SSSP (hop-bounded Jacobi)
+__global__ void sssp_seed(View push, int64_t* dist, int64_t* msg, uint64_t* vb, int32_t* q, int64_t* qdeg, int64_t seed) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        dist[seed] = 0;
+        msg[seed] = 0;
+        q[0] = static_cast<int32_t>(seed);
+        qdeg[0] = push_degree(push, seed);
+    }
+}
+
+// Relax every push edge of the frontier with the frontier's iteration-(i-1) message
+// (msg is a snapshot, so the update is Jacobi exactly like the reference's double buffer).
+__global__ void __launch_bounds__(kBlock) sssp_relax(View push, const int32_t* __restrict__ q,
+        const int64_t* __restrict__ qpre, int64_t qlen, const int64_t* __restrict__ msg,
+        int64_t* __restrict__ dist, uint64_t* __restrict__ mark, int32_t* __restrict__ qn,
+        int64_t* __restrict__ qdeg_n, Counters* cnt, int weighted) {
+    __shared__ int64_t s_pre[kLdsEntries];
+    __shared__ int32_t s_q[kLdsEntries];
+    __shared__ int64_t s_lo, s_hi;
+    const int64_t total = qpre[qlen];
+    const int64_t ntiles = (total + kTileEdges - 1) / kTileEdges;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t t0 = tile * kTileEdges;
+        const int64_t t1 = min(total, t0 + kTileEdges);
+        if (threadIdx.x == 0) {
+            int64_t a = 0, b = qlen;
+            while (b - a > 1) { const int64_t c = (a + b) >> 1; if (qpre[c] <= t0) a = c; else b = c; }
+            s_lo = a;
+            int64_t a2 = a, b2 = qlen;
+            while (b2 - a2 > 1) { const int64_t c = (a2 + b2) >> 1; if (qpre[c] <= t1 - 1) a2 = c; else b2 = c; }
+            s_hi = a2;
+        }
+        __syncthreads();
+        const int64_t lo = s_lo, hi = s_hi;
+        const int64_t span = hi - lo + 1;
+        const bool in_lds = span + 1 <= kLdsEntries;
+        if (in_lds) {
+            for (int64_t i = threadIdx.x; i <= span; i += kBlock) {
+                s_pre[i] = qpre[lo + i];
+                if (i < span) s_q[i] = q[lo + i];
+            }
+        }
+        __syncthreads();
+        for (int k = 0; k < kEdgesPerThread; ++k) {
+            const int64_t j = t0 + k * kBlock + threadIdx.x;
+            bool take = false;
+            int32_t v = 0;
+            int64_t vdeg = 0;
+            if (j < t1) {
+                int32_t u; int64_t start;
+                if (in_lds) {
+                    int64_t a = 0, b = span;
+                    while (b - a > 1) { const int64_t c = (a + b) >> 1; if (s_pre[c] <= j) a = c; else b = c; }
+                    u = s_q[a]; start = s_pre[a];
+                } else {
+                    int64_t a = lo, b = hi + 1;
+                    while (b - a > 1) { const int64_t c = (a + b) >> 1; if (qpre[c] <= j) a = c; else b = c; }
+                    u = q[a]; start = qpre[a];
+                }
+                int32_t w;
+                entry_at(push, u, j - start, v, w);
+                if (!weighted) w = 1;
+                if (w == kMissingWeight) {
+                    atomicOr(&cnt->err, 1ULL);          // edge.value(weight) on a missing key
+                } else {
+                    const int64_t cand = static_cast<int64_t>(static_cast<uint64_t>(msg[u]) + static_cast<uint64_t>(static_cast<int64_t>(w)));
+                    if (cand < dist[v]) {
+                        const long long old = atomicMin(reinterpret_cast<long long*>(&dist[v]), static_cast<long long>(cand));
+                        if (cand < old) {
+                            const uint64_t bit = 1ULL << (v & 63);
+                            const unsigned long long ob = atomicOr(reinterpret_cast<unsigned long long*>(&mark[v >> 6]), bit);
+                            if (!(ob & bit)) { take = true; vdeg = push_degree(push, v); }
+                        }
+                    }
+                }
+            }
+            wave_append(take, v, vdeg, qn, qdeg_n, cnt);
+        }
+        __syncthreads();
+    }
+}
+
+__global__ void sssp_commit(const int32_t* q, int64_t qlen, const int64_t* dist, int64_t* msg) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < qlen; i += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t v = q[i];
+        msg[v] = dist[v];
+    }
+}
+
+__global__ void dist_finalize(int64_t* dist, int64_t n) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        if (dist[i] == INT64_MAX) dist[i] = INT64_MIN;
+}
+
+inline int grid_for(int64_t work, int block = kBlock, int cap = 256 * 8) {
+    int64_t g = (work + block - 1) / block;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return static_cast<int>(g);
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- launchers
+hipError_t k_fill_i32(int32_t* p, int32_t v, int64_t n, hipStream_t s) {
+    fill_i32<<<grid_for(n), kBlock, 0, s>>>(p, v, n);
+    return hipGetLastError();
+}
+hipError_t k_fill_i64(int64_t* p, int64_t v, int64_t n, hipStream_t s) {
+    fill_i64<<<grid_for(n), kBlock, 0, s>>>(p, v, n);
+    return hipGetLastError();
+}
+hipError_t k_bfs_seed(const View& push, int32_t* level, uint64_t* vb, uint64_t* fb, int32_t* q,
+                      int64_t* qdeg, int64_t seed, hipStream_t s) {
+    bfs_seed<<<1, 64, 0, s>>>(push, level, vb, fb, q, qdeg, seed);
+    return hipGetLastError();
+}
+hipError_t k_td_expand(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen,
+                       int32_t* level, uint64_t* vb, uint64_t* nb, int32_t* qn, int64_t* qdeg_n,
+                       Counters* cnt, int32_t next_level, hipStream_t s) {
+    td_expand<<<256 * 8, kBlock, 0, s>>>(push, q, qpre, qlen, level, vb, nb, qn, qdeg_n, cnt, next_level);
+    return hipGetLastError();
+}
+hipError_t k_bu_step(const View& pull, const View& push, int64_t n, const uint64_t* fb, uint64_t* vb,
+                     uint64_t* nb, int32_t* level, int32_t* qn, int64_t* qdeg_n, Counters* cnt,
+                     int32_t next_level, hipStream_t s) {
+    const int64_t words = (n + 63) / 64;
+    bu_step<<<grid_for(words * 64, kBlock, 256 * 16), kBlock, 0, s>>>(pull, push, n, fb, vb, nb, level, qn, qdeg_n, cnt, next_level);
+    return hipGetLastError();
+}
+hipError_t k_level_to_dist(const int32_t* level, int64_t* dist, int64_t n, hipStream_t s) {
+    level_to_dist<<<grid_for(n), kBlock, 0, s>>>(level, dist, n);
+    return hipGetLastError();
+}
+hipError_t k_reach_stats(const View& v, const int64_t* dist, int64_t n, unsigned long long* out2, hipStream_t s) {
+    reach_stats<<<grid_for(n), kBlock, 0, s>>>(v, dist, n, out2);
+    return hipGetLastError();
+}
+hipError_t k_degree_i64(const View& v, const int32_t* q, int64_t qlen, int64_t* qdeg, hipStream_t s) {
+    degree_i64<<<grid_for(qlen), kBlock, 0, s>>>(v, q, qlen, qdeg);
+    return hipGetLastError();
+}
+hipError_t k_sssp_seed(const View& push, int64_t* dist, int64_t* msg, uint64_t* vb, int32_t* q,
+                       int64_t* qdeg, int64_t seed, hipStream_t s) {
+    sssp_seed<<<1, 64, 0, s>>>(push, dist, msg, vb, q, qdeg, seed);
+    return hipGetLastError();
+}
+hipError_t k_sssp_relax(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen,
+                        const int64_t* msg, int64_t* dist, uint64_t* mark, int32_t* qn,
+                        int64_t* qdeg_n, Counters* cnt, int weighted, hipStream_t s) {
+    sssp_relax<<<256 * 8, kBlock, 0, s>>>(push, q, qpre, qlen, msg, dist, mark, qn, qdeg_n, cnt, weighted);
+    return hipGetLastError();
+}
+hipError_t k_sssp_commit(const int32_t* q, int64_t qlen, const int64_t* dist, int64_t* msg,
+                         uint64_t* mark, hipStream_t s) {
+    (void)mark;
+    sssp_commit<<<grid_for(qlen), kBlock, 0, s>>>(q, qlen, dist, msg);
+    return hipGetLastError();
+}
+hipError_t k_dist_finalize(int64_t* dist, int64_t n, hipStream_t s) {
+    dist_finalize<<<grid_for(n), kBlock, 0, s>>>(dist, n);
+    return hipGetLastError();
+}
+
+hipError_t scan_exclusive_i64(void*& tmp, size_t& tmp_bytes, const int64_t* in, int64_t* out,
+                              int64_t n, hipStream_t s) {
+    size_t need = 0;
+    hipError_t e = hipcub::DeviceScan::ExclusiveSum(nullptr, need, in, out, static_cast<int>(n), s);
+    if (e != hipSuccess) return e;
+    if (need > tmp_bytes) {
+        if (tmp) (void)hipFree(tmp);
+        tmp = nullptr;
+        e = hipMalloc(&tmp, need);
+        if (e != hipSuccess) { tmp_bytes = 0; return e; }
+        tmp_bytes = need;
+    }
+    return hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, in, out, static_cast<int>(n), s);
+}
+
+}  // namespace tgo

@@ -1,0 +1,185 @@
+// engine.hpp — internal interfaces of the MI355X OLAP engine (not part of the C-ABI).
+//
+// Data layout in HBM (see DESIGN.md "Data layout"):
+//   out-CSR : off_o[n+1] (int64), adj_o[E_o] (int32 dense ids), w_o[E_o] (int32, optional)
+//             row v = the OUT entries of Titan row v, in column order
+//   in-CSR  : off_i[n+1], adj_i[E_i], w_i[E_i]  — the IN entries of row v
+// A message scope's reversed incident traversal (FulgoraUtil.java:57) is a "view":
+//   scope inE  -> receiver pulls over out-CSR, sender pushes over in-CSR
+//   scope outE -> receiver pulls over in-CSR,  sender pushes over out-CSR
+//   scope bothE-> both lists (pull == push)
+// When the per-row preload cap truncated a row (QueryContainer.java:28,122) the pull lists
+// are no longer transposes of each other, and the push list is an explicit transpose
+// of the pull list (t-CSR).
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+#include <hip/hip_runtime_api.h>
+#include "../../include/titan_gpu_olap.h"
+
+namespace tgo {
+
+// ---------------------------------------------------------------- host graph
+struct HostCsr {
+    std::vector<int64_t> off;   // n+1
+    std::vector<int32_t> adj;
+    std::vector<int32_t> w;     // empty when unweighted
+};
+
+struct HostGraph {
+    int64_t n = 0;
+    std::vector<int64_t> titan_id;
+    HostCsr out, in;
+    HostCsr push_t;             // explicit transpose of the pull view (cap / asymmetric rows)
+    bool has_transpose = false;
+    bool has_weight = false;
+    int32_t scope = TGO_SCOPE_BOTH_E;
+    int64_t ghost = 0, truncated = 0, skipped = 0;
+};
+
+// Staging of decoded rows between tgo_load_rows batches (decoded on arrival).
+struct RowStaging {
+    std::vector<int64_t> vid;        // live vertices in row order
+    std::vector<int64_t> row_begin;  // per live row, index into entries (size = vid+1)
+    std::vector<int64_t> other;      // other vertex Titan id per kept entry
+    std::vector<uint8_t> dir;        // 0 OUT, 1 IN
+    std::vector<int32_t> w;          // weight (INT32_MIN = property missing)
+    int64_t ghost = 0, truncated = 0, skipped = 0;
+    bool active = false;
+    tgo_load_opts opts{};
+    std::vector<int64_t> labels;
+};
+
+// Weight value marking an edge whose weight property is absent: traversing it makes the
+// reference throw inside execute() (edge.value() on a missing key), i.e. TGO_E_PROGRAM.
+constexpr int32_t kMissingWeight = INT32_MIN;
+
+int decode_rows(RowStaging& st, const tgo_rows* rows, const tgo_schema* schema,
+                const tgo_load_opts* opts, int pb, int64_t hard_limit, int threads,
+                std::string& err);
+int assemble_from_rows(RowStaging& st, HostGraph& g, int threads, std::string& err);
+int assemble_from_edges(const tgo_edges* e, const tgo_load_opts* opts, int64_t hard_limit,
+                        HostGraph& g, int threads, std::string& err);
+
+// ---------------------------------------------------------------- device graph
+struct DevCsr {
+    int64_t* off = nullptr;
+    int32_t* adj = nullptr;
+    int32_t* w = nullptr;
+    int64_t nnz = 0;
+};
+
+// A list view handed to kernels: up to two CSRs walked back to back per vertex.
+struct View {
+    const int64_t* off0; const int32_t* adj0; const int32_t* w0;
+    const int64_t* off1; const int32_t* adj1; const int32_t* w1;
+    int nlists;
+};
+
+// Row blocks for the CSR-adaptive gather (PageRank / walk counts), built on the host.
+struct RowBlocks {
+    int64_t nblocks = 0;        // short-row blocks
+    int64_t* blk = nullptr;     // nblocks+1 row boundaries (device)
+    int64_t nchunks = 0;        // chunks of long rows
+    int64_t* chunk_row = nullptr;   // per chunk: row
+    int64_t* chunk_beg = nullptr;   // per chunk: first entry
+    int64_t* chunk_end = nullptr;
+    int64_t nlong = 0;          // long rows
+    int64_t* long_row = nullptr;    // per long row: row id
+    int64_t* long_chunk = nullptr;  // nlong+1: chunk index range
+    std::vector<int64_t> h_blk;
+};
+
+struct DevGraph {
+    int64_t n = 0;
+    DevCsr out, in, push_t;
+    bool has_transpose = false;
+    bool has_weight = false;
+    int32_t min_weight = 0;
+    int32_t scope = TGO_SCOPE_BOTH_E;
+    RowBlocks rb_out, rb_in;    // CSR-adaptive blocks per pull list
+    bool rb_out_ready = false, rb_in_ready = false;
+};
+
+// Device scratch reused across programs (allocated on first use, sized for n).
+struct Counters {               // device-side level counters (one cache line each)
+    unsigned long long qlen;    // next-queue length
+    unsigned long long pad0[7];
+    unsigned long long mf;      // sum of push degrees of the next frontier
+    unsigned long long pad1[7];
+    unsigned long long err;     // program failure flag
+    unsigned long long pad2[7];
+    unsigned long long red[2];  // reductions (reached vertices, reached entries)
+    unsigned long long pad3[6];
+};
+
+struct Scratch {
+    int64_t n = 0;
+    int32_t* level = nullptr;       // n
+    int32_t* q[2] = {nullptr, nullptr};   // frontier queues
+    int64_t* qdeg = nullptr;        // push degree of each queue entry
+    int64_t* qpre = nullptr;        // exclusive scan of qdeg (+1)
+    uint64_t* fb = nullptr;         // frontier bitmap
+    uint64_t* nb = nullptr;         // next-frontier bitmap
+    uint64_t* vb = nullptr;         // visited bitmap
+    int64_t* dist = nullptr;        // n: int64 distances / messages
+    int64_t* msg = nullptr;         // n: SSSP message snapshot
+    double* vec[3] = {nullptr, nullptr, nullptr};  // PageRank vectors
+    double* partial = nullptr;      // long-row partial sums
+    int64_t partial_cap = 0;
+    void* cub_tmp = nullptr;
+    size_t cub_bytes = 0;
+    Counters* cnt = nullptr;        // device
+    Counters* hcnt = nullptr;       // pinned host mirror
+};
+
+// ---------------------------------------------------------------- kernel launchers (HIP)
+hipError_t k_fill_i32(int32_t* p, int32_t v, int64_t n, hipStream_t s);
+hipError_t k_fill_i64(int64_t* p, int64_t v, int64_t n, hipStream_t s);
+hipError_t k_bfs_seed(const View& push, int32_t* level, uint64_t* vb, uint64_t* fb, int32_t* q,
+                      int64_t* qdeg, int64_t seed, hipStream_t s);
+hipError_t k_td_expand(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen,
+                       int32_t* level, uint64_t* vb, uint64_t* nb, int32_t* qn, int64_t* qdeg_n,
+                       Counters* cnt, int32_t next_level, hipStream_t s);
+hipError_t k_bu_step(const View& pull, const View& push, int64_t n, const uint64_t* fb, uint64_t* vb,
+                     uint64_t* nb, int32_t* level, int32_t* qn, int64_t* qdeg_n, Counters* cnt,
+                     int32_t next_level, hipStream_t s);
+hipError_t k_level_to_dist(const int32_t* level, int64_t* dist, int64_t n, hipStream_t s);
+hipError_t k_reach_stats(const View& both_or_pull, const int64_t* dist, int64_t n,
+                         unsigned long long* out2, hipStream_t s);
+hipError_t k_degree_i64(const View& v, const int32_t* q, int64_t qlen, int64_t* qdeg, hipStream_t s);
+
+// SSSP (hop-bounded Jacobi, exact reference semantics)
+hipError_t k_sssp_seed(const View& push, int64_t* dist, int64_t* msg, uint64_t* vb, int32_t* q,
+                       int64_t* qdeg, int64_t seed, hipStream_t s);
+hipError_t k_sssp_relax(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen,
+                        const int64_t* msg, int64_t* dist, uint64_t* mark, int32_t* qn,
+                        int64_t* qdeg_n, Counters* cnt, int weighted, hipStream_t s);
+hipError_t k_sssp_commit(const int32_t* q, int64_t qlen, const int64_t* dist, int64_t* msg,
+                         uint64_t* mark, hipStream_t s);
+hipError_t k_dist_finalize(int64_t* dist, int64_t n, hipStream_t s);
+
+// CSR-adaptive gather
+hipError_t k_pr_init(const DevCsr& out, double* edge_count, double* contrib, double* pr,
+                     double inv_n, int64_t n, hipStream_t s);
+hipError_t k_pr_iter(const DevCsr& in, const RowBlocks& rb, const double* contrib,
+                     const double* edge_count, double* pr, double* contrib_next, double* partial,
+                     double alpha, double base, int64_t n, hipStream_t s);
+hipError_t k_fill_f64(double* p, double v, int64_t n, hipStream_t s);
+hipError_t k_walk_iter(const DevCsr& out, const RowBlocks& rb, const int32_t* prev, int32_t* next,
+                       int32_t* partial, int64_t n, hipStream_t s);
+
+hipError_t scan_exclusive_i64(void*& tmp, size_t& tmp_bytes, const int64_t* in, int64_t* out,
+                              int64_t n, hipStream_t s);
+
+// Row-block construction (host) for a CSR.
+void build_row_blocks(const std::vector<int64_t>& off, int64_t tile, int64_t max_rows,
+                      std::vector<int64_t>& blk, std::vector<int64_t>& chunk_row,
+                      std::vector<int64_t>& chunk_beg, std::vector<int64_t>& chunk_end,
+                      std::vector<int64_t>& long_row, std::vector<int64_t>& long_chunk);
+
+constexpr int64_t kTile = 2048;      // entries per CSR-adaptive block (16 KB of fp64 in LDS)
+constexpr int64_t kMaxRows = 1024;   // rows per CSR-adaptive block
+
+}  // namespace tgo

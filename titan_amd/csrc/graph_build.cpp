@@ -1,0 +1,433 @@
+// graph_build.cpp — one-time CSR assembly on the host (multi-threaded).
+//
+// Replaces the reference's per-superstep rescan + decode (FulgoraGraphComputer.java:155-164
+// runs a full edgestore scan every iteration; VertexJobConverter.process,
+// VertexJobConverter.java:109-129, rebuilds a PreloadedVertex per row per superstep).
+// Here the rows are decoded once into an out-CSR and an in-CSR of dense vertex ids.
+#include <algorithm>
+#include <atomic>
+#include <cstring>
+#include <thread>
+#include <unordered_map>
+#include "codec.hpp"
+#include "engine.hpp"
+
+namespace tgo {
+
+template <class F>
+static void parallel_for(int64_t n, int threads, F&& fn) {
+    if (threads <= 1 || n < 4096) { fn(int64_t(0), n, 0); return; }
+    std::vector<std::thread> th;
+    th.reserve(threads);
+    for (int t = 0; t < threads; ++t) {
+        const int64_t lo = n * t / threads, hi = n * (t + 1) / threads;
+        th.emplace_back([&, lo, hi, t] { fn(lo, hi, t); });
+    }
+    for (auto& x : th) x.join();
+}
+
+// Dynamic chunked loop for skewed per-item work (e.g. sorting hub rows).
+template <class F>
+static void parallel_dynamic(int64_t n, int threads, int64_t chunk, F&& fn) {
+    std::atomic<int64_t> next{0};
+    auto worker = [&] {
+        for (;;) {
+            const int64_t lo = next.fetch_add(chunk);
+            if (lo >= n) break;
+            fn(lo, std::min(n, lo + chunk));
+        }
+    };
+    if (threads <= 1) { worker(); return; }
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads; ++t) th.emplace_back(worker);
+    for (auto& x : th) x.join();
+}
+
+// ------------------------------------------------------------------ rows -> staging
+int decode_rows(RowStaging& st, const tgo_rows* rows, const tgo_schema* schema,
+                const tgo_load_opts* opts, int pb, int64_t hard_limit, int threads,
+                std::string& err) {
+    DecodePlan plan;
+    plan.weight_key = opts->weight_key;
+    for (int k = 0; k < schema->n_property_keys; ++k)
+        plan.key_types.emplace_back(schema->property_keys[k].key_id, schema->property_keys[k].datatype);
+    for (int t = 0; t < schema->n_edge_types; ++t) {
+        const tgo_edge_type& et = schema->edge_types[t];
+        LabelPlan lp;
+        lp.type_id = et.type_id;
+        lp.multiplicity = et.multiplicity;
+        if (opts->n_labels > 0) {
+            lp.selected = false;
+            for (int j = 0; j < opts->n_labels; ++j) lp.selected |= opts->label_ids[j] == et.type_id;
+        }
+        for (int k = 0; k < et.n_signature; ++k) {
+            lp.sig_types.push_back(plan.datatype(et.signature_ids[k]));
+            if (et.signature_ids[k] == opts->weight_key && lp.weight_sig_index < 0) lp.weight_sig_index = k;
+        }
+        if (et.multiplicity == TGO_MULTI)
+            for (int k = 0; k < et.n_sort_key; ++k) lp.weight_in_sortkey |= et.sort_key_ids[k] == opts->weight_key;
+        plan.labels.push_back(lp);
+    }
+    // Untyped single-direction scopes are not "fitted" and get the hard limit; BOTH and
+    // typed scopes keep NO_LIMIT (BasicVertexCentricQueryBuilder.java:418-431,469-474;
+    // QueryContainer.java:122).
+    const bool typed = opts->n_labels > 0;
+    const int64_t limit = (opts->apply_cap && !typed && opts->scope != TGO_SCOPE_BOTH_E)
+                              ? hard_limit : INT64_MAX;
+
+    struct Local {
+        std::vector<int64_t> vid, cnt, other;
+        std::vector<uint8_t> dir;
+        std::vector<int32_t> w;
+        int64_t ghost = 0, truncated = 0, skipped = 0;
+        int rc = TGO_OK;
+        std::string msg;
+    };
+    const int64_t nrows = rows->nrows;
+    const int nth = std::max(1, std::min<int>(threads, static_cast<int>((nrows + 1023) / 1024)));
+    std::vector<Local> loc(nth);
+    parallel_for(nrows, nth, [&](int64_t lo, int64_t hi, int t) {
+        Local& L = loc[t];
+        for (int64_t r = lo; r < hi && L.rc == TGO_OK; ++r) {
+            const int64_t vid = key_to_vertex_id(rows->row_keys[r], pb);
+            if (vid & 1) { ++L.skipped; continue; }           // key filter: Invisible (:156-162)
+            const int64_t sfx = vid & 7;
+            if (sfx == 2) { L.rc = TGO_E_UNSUPPORTED; L.msg = "partitioned (vertex-cut) vertex rows are not supported"; break; }
+            if (sfx != 0 && sfx != 4) { L.rc = TGO_E_CODEC; L.msg = "row key has an unrecognized vertex id type"; break; }
+            const uint8_t* base = rows->entry_bytes + rows->row_byte_begin[r];
+            const int64_t e0 = rows->row_entry_begin[r], e1 = rows->row_entry_begin[r + 1];
+            auto ent_start = [&](int64_t k) -> int64_t {
+                return k == e0 ? 0 : static_cast<int64_t>(static_cast<uint64_t>(rows->entry_limit_valpos[k - 1]) >> 32);
+            };
+            if (e1 <= e0) { L.rc = TGO_E_CODEC; L.msg = "row without entries"; break; }
+            {   // ghost check: the first column must be VertexExists (:131-137)
+                const int64_t end = static_cast<int64_t>(static_cast<uint64_t>(rows->entry_limit_valpos[e0]) >> 32);
+                Cursor c{base, static_cast<size_t>(end), 0};
+                RelType rt;
+                if (!read_relation_type(c, rt)) { L.rc = TGO_E_CODEC; L.msg = "malformed first column"; break; }
+                if (rt.is_edge || rt.type_id != kVertexExistsId) { ++L.ghost; continue; }
+            }
+            // user-edge slice [0x60,0x80): entries are column-sorted, so it is contiguous.
+            int64_t first = -1, cnt = 0;
+            for (int64_t k = e0; k < e1; ++k) {
+                const uint8_t c0 = base[ent_start(k)];
+                if (c0 >= 0x60 && c0 < 0x80) { if (first < 0) first = k; ++cnt; }
+                else if (first >= 0) break;
+            }
+            if (limit != INT64_MAX && cnt >= limit) ++L.truncated;     // TRUNCATED_ENTRY_LISTS
+            const int64_t keep = std::min(cnt, limit);
+            int64_t kept = 0;
+            for (int64_t k = first; k >= 0 && k < first + keep; ++k) {
+                const int64_t s = ent_start(k);
+                const int64_t e = static_cast<int64_t>(static_cast<uint64_t>(rows->entry_limit_valpos[k]) >> 32);
+                const int64_t vp = rows->entry_limit_valpos[k] & 0x7FFFFFFF;
+                DecodedEdge de;
+                const DecodeResult dr = decode_edge(base + s, static_cast<size_t>(e - s), static_cast<size_t>(vp), plan, de);
+                if (dr == DecodeResult::kSkip) continue;
+                if (dr != DecodeResult::kOk) {
+                    L.rc = dr == DecodeResult::kUnsupported ? TGO_E_UNSUPPORTED : TGO_E_CODEC;
+                    L.msg = dr == DecodeResult::kUnsupported ? "weight property datatype/placement not supported"
+                                                             : "malformed edge entry";
+                    break;
+                }
+                L.other.push_back(de.other);
+                L.dir.push_back(static_cast<uint8_t>(de.dir));
+                L.w.push_back(plan.weight_key == 0 ? 1 : (de.has_weight ? de.weight : kMissingWeight));
+                ++kept;
+            }
+            if (L.rc != TGO_OK) break;
+            L.vid.push_back(vid);
+            L.cnt.push_back(kept);
+        }
+    });
+    for (auto& L : loc) if (L.rc != TGO_OK) { err = L.msg; return L.rc; }
+    if (!st.active) {
+        st = RowStaging();
+        st.active = true;
+        st.opts = *opts;
+        st.labels.assign(opts->label_ids, opts->label_ids + opts->n_labels);
+        st.opts.label_ids = nullptr;
+        st.row_begin.push_back(0);
+    } else if (st.opts.scope != opts->scope || st.opts.weight_key != opts->weight_key ||
+               st.opts.apply_cap != opts->apply_cap) {
+        err = "tgo_load_opts differ between row batches";
+        return TGO_E_INVALID;
+    }
+    for (auto& L : loc) {
+        st.ghost += L.ghost; st.truncated += L.truncated; st.skipped += L.skipped;
+        for (size_t i = 0; i < L.vid.size(); ++i) {
+            st.vid.push_back(L.vid[i]);
+            st.row_begin.push_back(st.row_begin.back() + L.cnt[i]);
+        }
+        st.other.insert(st.other.end(), L.other.begin(), L.other.end());
+        st.dir.insert(st.dir.end(), L.dir.begin(), L.dir.end());
+        st.w.insert(st.w.end(), L.w.begin(), L.w.end());
+    }
+    return TGO_OK;
+}
+
+// ------------------------------------------------------------------ helpers
+// Open-addressing Titan id -> dense index map (the role of FulgoraVertexMemory's
+// NonBlockingHashMapLong keyed by Titan id, FulgoraVertexMemory.java:30,49-58).
+struct IdMap {
+    std::vector<int64_t> keys;
+    std::vector<int32_t> vals;
+    uint64_t mask = 0;
+    static uint64_t h(uint64_t x) { x ^= x >> 31; x *= 0x7fb5d329728ea185ULL; x ^= x >> 27; x *= 0x81dadef4bc2dd44dULL; return x ^ (x >> 33); }
+    void build(const std::vector<int64_t>& ids) {
+        uint64_t cap = 16;
+        while (cap < ids.size() * 2) cap <<= 1;
+        mask = cap - 1;
+        keys.assign(cap, INT64_MIN);
+        vals.assign(cap, -1);
+        for (size_t i = 0; i < ids.size(); ++i) {
+            uint64_t p = h(static_cast<uint64_t>(ids[i])) & mask;
+            while (keys[p] != INT64_MIN && keys[p] != ids[i]) p = (p + 1) & mask;
+            keys[p] = ids[i];
+            vals[p] = static_cast<int32_t>(i);
+        }
+    }
+    int32_t find(int64_t id) const {
+        uint64_t p = h(static_cast<uint64_t>(id)) & mask;
+        for (;;) {
+            if (keys[p] == id) return vals[p];
+            if (keys[p] == INT64_MIN) return -1;
+            p = (p + 1) & mask;
+        }
+    }
+};
+
+// Transpose of the union of `lists` (each an n-row CSR): t[w] gets v for every w in L(v).
+static void transpose_lists(int64_t n, const std::vector<const HostCsr*>& lists, bool weighted,
+                            HostCsr& t, int threads) {
+    std::vector<std::atomic<int64_t>> cnt(n + 1);
+    for (auto& c : cnt) c.store(0, std::memory_order_relaxed);
+    for (const HostCsr* L : lists)
+        parallel_for(static_cast<int64_t>(L->adj.size()), threads, [&](int64_t lo, int64_t hi, int) {
+            for (int64_t k = lo; k < hi; ++k) cnt[L->adj[k]].fetch_add(1, std::memory_order_relaxed);
+        });
+    t.off.assign(n + 1, 0);
+    for (int64_t v = 0; v < n; ++v) t.off[v + 1] = t.off[v] + cnt[v].load(std::memory_order_relaxed);
+    const int64_t E = t.off[n];
+    t.adj.assign(E, 0);
+    if (weighted) t.w.assign(E, 0);
+    // Sequential fill in source order keeps each transposed row sorted by source id.
+    std::vector<int64_t> pos(t.off.begin(), t.off.end() - 1);
+    for (int64_t v = 0; v < n; ++v)
+        for (const HostCsr* L : lists)
+            for (int64_t k = L->off[v]; k < L->off[v + 1]; ++k) {
+                const int64_t p = pos[L->adj[k]]++;
+                t.adj[p] = static_cast<int32_t>(v);
+                if (weighted) t.w[p] = L->w[k];
+            }
+}
+
+// Decide whether the push view equals the stored opposite list; if not, build it.
+static void finish_views(HostGraph& g, int threads) {
+    const int64_t n = g.n;
+    bool consistent = g.truncated == 0;
+    if (consistent) {   // every OUT entry u->v must have a matching IN entry at v (count check)
+        std::vector<std::atomic<int64_t>> indeg(n);
+        for (auto& c : indeg) c.store(0, std::memory_order_relaxed);
+        parallel_for(static_cast<int64_t>(g.out.adj.size()), threads, [&](int64_t lo, int64_t hi, int) {
+            for (int64_t k = lo; k < hi; ++k) indeg[g.out.adj[k]].fetch_add(1, std::memory_order_relaxed);
+        });
+        for (int64_t v = 0; v < n && consistent; ++v)
+            consistent = indeg[v].load(std::memory_order_relaxed) == g.in.off[v + 1] - g.in.off[v];
+    }
+    g.has_transpose = !consistent;
+    g.push_t = HostCsr();
+    if (!consistent) {
+        std::vector<const HostCsr*> pull;
+        if (g.scope == TGO_SCOPE_IN_E) pull = {&g.out};
+        else if (g.scope == TGO_SCOPE_OUT_E) pull = {&g.in};
+        else pull = {&g.out, &g.in};
+        transpose_lists(n, pull, g.has_weight, g.push_t, threads);
+    }
+}
+
+// ------------------------------------------------------------------ staging -> CSR
+int assemble_from_rows(RowStaging& st, HostGraph& g, int threads, std::string& err) {
+    g = HostGraph();
+    g.n = static_cast<int64_t>(st.vid.size());
+    if (g.n >= INT32_MAX) { err = "more than 2^31-1 vertices per device"; return TGO_E_UNSUPPORTED; }
+    g.titan_id = st.vid;
+    g.scope = st.opts.scope;
+    g.has_weight = st.opts.weight_key != 0;
+    g.ghost = st.ghost; g.truncated = st.truncated; g.skipped = st.skipped;
+    IdMap map;
+    map.build(st.vid);
+    const int64_t n = g.n;
+    // Map Titan ids to dense ids; entries to non-executed vertices can never carry a
+    // message (EMPTY_STATE => null, VertexState.java:103-137) and are dropped.
+    std::vector<int32_t> dense(st.other.size());
+    parallel_for(static_cast<int64_t>(st.other.size()), threads, [&](int64_t lo, int64_t hi, int) {
+        for (int64_t k = lo; k < hi; ++k) dense[k] = map.find(st.other[k]);
+    });
+    std::vector<int64_t> co(n + 1, 0), ci(n + 1, 0);
+    parallel_for(n, threads, [&](int64_t lo, int64_t hi, int) {
+        for (int64_t v = lo; v < hi; ++v) {
+            int64_t a = 0, b = 0;
+            for (int64_t k = st.row_begin[v]; k < st.row_begin[v + 1]; ++k) {
+                if (dense[k] < 0) continue;
+                if (st.dir[k] == 0) ++a; else ++b;
+            }
+            co[v + 1] = a; ci[v + 1] = b;
+        }
+    });
+    for (int64_t v = 0; v < n; ++v) { co[v + 1] += co[v]; ci[v + 1] += ci[v]; }
+    g.out.off = co; g.in.off = ci;
+    g.out.adj.resize(co[n]); g.in.adj.resize(ci[n]);
+    if (g.has_weight) { g.out.w.resize(co[n]); g.in.w.resize(ci[n]); }
+    parallel_for(n, threads, [&](int64_t lo, int64_t hi, int) {
+        for (int64_t v = lo; v < hi; ++v) {
+            int64_t a = co[v], b = ci[v];
+            for (int64_t k = st.row_begin[v]; k < st.row_begin[v + 1]; ++k) {
+                if (dense[k] < 0) continue;
+                if (st.dir[k] == 0) { g.out.adj[a] = dense[k]; if (g.has_weight) g.out.w[a] = st.w[k]; ++a; }
+                else { g.in.adj[b] = dense[k]; if (g.has_weight) g.in.w[b] = st.w[k]; ++b; }
+            }
+        }
+    });
+    finish_views(g, threads);
+    st = RowStaging();
+    return TGO_OK;
+}
+
+// ------------------------------------------------------------------ edges -> CSR
+// Each directed edge u->v contributes an OUT entry to row u and an IN entry to row v
+// (StandardTitanGraph.java:564-591; loops therefore give two entries on one row).
+// Within a row the column order is (direction, other Titan id, relation id)
+// (IDHandler.writeRelationType puts the direction bit in the type varint;
+// EdgeSerializer.java:255-259 writes the other id then the relation id backward-encoded,
+// which is byte-order preserving, VariableLong.java:223-233).  Relation ids follow the
+// edge index.  Titan ids, when not given, are assigned monotonically in dense order.
+int assemble_from_edges(const tgo_edges* e, const tgo_load_opts* opts, int64_t hard_limit,
+                        HostGraph& g, int threads, std::string& err) {
+    g = HostGraph();
+    const int64_t n = e->n, m = e->m;
+    if (n <= 0 || n >= INT32_MAX) { err = "vertex count out of range"; return TGO_E_INVALID; }
+    g.n = n;
+    g.scope = opts->scope;
+    g.has_weight = opts->weight_key != 0 && e->weight != nullptr;
+    g.titan_id.resize(n);
+    for (int64_t v = 0; v < n; ++v)
+        g.titan_id[v] = e->titan_ids ? e->titan_ids[v] : ((v + 1) << 3);  // NormalVertex, 0 partition bits
+    for (int64_t v = 1; e->titan_ids && v < n; ++v)
+        if (e->titan_ids[v] <= e->titan_ids[v - 1]) { err = "titan_ids must be strictly increasing"; return TGO_E_INVALID; }
+    // Range check (a bad id would scatter out of bounds).
+    std::atomic<bool> bad{false};
+    parallel_for(m, threads, [&](int64_t lo, int64_t hi, int) {
+        for (int64_t k = lo; k < hi; ++k)
+            if (e->src[k] < 0 || e->src[k] >= n || e->dst[k] < 0 || e->dst[k] >= n) { bad = true; return; }
+    });
+    if (bad) { err = "edge endpoint out of range"; return TGO_E_INVALID; }
+
+    const bool cap = opts->apply_cap && opts->n_labels == 0 && opts->scope != TGO_SCOPE_BOTH_E;
+    const int64_t limit = cap ? hard_limit : INT64_MAX;
+
+    // Full (uncapped) sorted rows for one direction: keys = neighbor << 32 | edge index.
+    auto build_dir = [&](bool out_dir, std::vector<int64_t>& off, std::vector<uint64_t>& keys) {
+        const int32_t* own = out_dir ? e->src : e->dst;
+        const int32_t* nbr = out_dir ? e->dst : e->src;
+        std::vector<std::atomic<int64_t>> cnt(n + 1);
+        for (auto& c : cnt) c.store(0, std::memory_order_relaxed);
+        parallel_for(m, threads, [&](int64_t lo, int64_t hi, int) {
+            for (int64_t k = lo; k < hi; ++k) cnt[own[k]].fetch_add(1, std::memory_order_relaxed);
+        });
+        off.assign(n + 1, 0);
+        for (int64_t v = 0; v < n; ++v) off[v + 1] = off[v] + cnt[v].load(std::memory_order_relaxed);
+        for (int64_t v = 0; v < n; ++v) cnt[v].store(off[v], std::memory_order_relaxed);
+        keys.resize(m);
+        parallel_for(m, threads, [&](int64_t lo, int64_t hi, int) {
+            for (int64_t k = lo; k < hi; ++k) {
+                const int64_t p = cnt[own[k]].fetch_add(1, std::memory_order_relaxed);
+                keys[p] = (static_cast<uint64_t>(static_cast<uint32_t>(nbr[k])) << 32) | static_cast<uint64_t>(k);
+            }
+        });
+        parallel_dynamic(n, threads, 4096, [&](int64_t lo, int64_t hi) {
+            for (int64_t v = lo; v < hi; ++v) std::sort(keys.begin() + off[v], keys.begin() + off[v + 1]);
+        });
+    };
+    if (m >= (int64_t(1) << 32)) { err = "more than 2^32 edges per load"; return TGO_E_UNSUPPORTED; }
+    std::vector<int64_t> off_o, off_i;
+    std::vector<uint64_t> keys_o, keys_i;
+    build_dir(true, off_o, keys_o);
+    build_dir(false, off_i, keys_i);
+    // Cap: keep the first `limit` entries of [OUT... | IN...] per row.
+    std::vector<int64_t> ko(n + 1, 0), ki(n + 1, 0);
+    int64_t truncated = 0;
+    for (int64_t v = 0; v < n; ++v) {
+        const int64_t a = off_o[v + 1] - off_o[v], b = off_i[v + 1] - off_i[v];
+        if (limit != INT64_MAX && a + b >= limit) ++truncated;
+        const int64_t ka = std::min(a, limit);
+        const int64_t kb = std::min(b, limit - ka);
+        ko[v + 1] = ko[v] + ka;
+        ki[v + 1] = ki[v] + kb;
+    }
+    g.truncated = truncated;
+    auto fill = [&](const std::vector<int64_t>& off, const std::vector<uint64_t>& keys,
+                    const std::vector<int64_t>& koff, HostCsr& c) {
+        c.off = koff;
+        c.adj.resize(koff[n]);
+        if (g.has_weight) c.w.resize(koff[n]);
+        parallel_for(n, threads, [&](int64_t lo, int64_t hi, int) {
+            for (int64_t v = lo; v < hi; ++v) {
+                const int64_t len = koff[v + 1] - koff[v];
+                for (int64_t j = 0; j < len; ++j) {
+                    const uint64_t key = keys[off[v] + j];
+                    c.adj[koff[v] + j] = static_cast<int32_t>(key >> 32);
+                    if (g.has_weight) c.w[koff[v] + j] = e->weight[key & 0xFFFFFFFFULL];
+                }
+            }
+        });
+    };
+    fill(off_o, keys_o, ko, g.out);
+    std::vector<uint64_t>().swap(keys_o);
+    fill(off_i, keys_i, ki, g.in);
+    finish_views(g, threads);
+    return TGO_OK;
+}
+
+// ------------------------------------------------------------------ CSR-adaptive blocks
+// Greedy partition of rows into blocks of <= tile entries and <= max_rows rows
+// (CSR-Adaptive, Greathouse & Daga SC'14); rows longer than `tile` become "long rows"
+// split into tile-sized chunks whose partial sums are added in chunk order.
+void build_row_blocks(const std::vector<int64_t>& off, int64_t tile, int64_t max_rows,
+                      std::vector<int64_t>& blk, std::vector<int64_t>& chunk_row,
+                      std::vector<int64_t>& chunk_beg, std::vector<int64_t>& chunk_end,
+                      std::vector<int64_t>& long_row, std::vector<int64_t>& long_chunk) {
+    const int64_t n = static_cast<int64_t>(off.size()) - 1;
+    blk.clear(); chunk_row.clear(); chunk_beg.clear(); chunk_end.clear();
+    long_row.clear(); long_chunk.clear();
+    blk.push_back(0);
+    long_chunk.push_back(0);
+    int64_t r = 0;
+    while (r < n) {
+        const int64_t d = off[r + 1] - off[r];
+        if (d > tile) {
+            // long row: an empty short block marks its position, chunks carry the work
+            long_row.push_back(r);
+            for (int64_t s = off[r]; s < off[r + 1]; s += tile) {
+                chunk_row.push_back(r);
+                chunk_beg.push_back(s);
+                chunk_end.push_back(std::min(off[r + 1], s + tile));
+            }
+            long_chunk.push_back(static_cast<int64_t>(chunk_row.size()));
+            ++r;
+            blk.push_back(r);   // block [r-1, r) is a long row: skipped by the short kernel
+            continue;
+        }
+        int64_t e = r, nnz = 0;
+        while (e < n && e - r < max_rows) {
+            const int64_t de = off[e + 1] - off[e];
+            if (de > tile || nnz + de > tile) break;
+            nnz += de;
+            ++e;
+        }
+        r = e;
+        blk.push_back(r);
+    }
+}
+
+}  // namespace tgo

@@ -1,0 +1,185 @@
+// spmv.hip — pull gathers for PageRankVertexProgram and OLAPTest.DegreeCounter on gfx950.
+//
+// Both programs gather, for every vertex, a sum over its reversed-scope list of the
+// neighbours' previous-superstep messages (VertexMemoryHandler.receiveMessages,
+// VertexMemoryHandler.java:77-103):
+//   PageRank  (PageRankVertexProgram.java:84-89): PR'(v) = a * sum_{u in IN(v)} c(u) + (1-a)/N,
+//             c'(v) = PR'(v) / edgeCount(v)  — fp64, bandwidth-bound SpMV over the in-CSR.
+//   DegreeCounter (OLAPTest.java:357-364): d'(v) = sum_{w in OUT(v)} d(w), Java int wrap.
+//
+// CSR-Adaptive (Greathouse & Daga, SC'14): rows are cut on the host into blocks of at
+// most kTile entries; a 256-thread workgroup stages its block's gathered messages in LDS
+// with coalesced index reads, then reduces rows from LDS — thread-per-row when the block
+// has many short rows, wave-per-row (fixed shuffle tree) when it has few.  Rows longer
+// than kTile are split into kTile chunks reduced by separate workgroups and summed in chunk
+// order by a finalize kernel.  Every sum has a fixed order: results are bitwise
+// reproducible run to run.
+#include <hip/hip_runtime.h>
+#include "engine.hpp"
+
+namespace tgo {
+namespace {
+
+constexpr int kBlock = 256;
+
+__device__ __forceinline__ int lane() { return static_cast<int>(threadIdx.x & 63); }
+
+struct PrOp {
+    using T = double;
+    const double* msg;
+    __device__ __forceinline__ double load(int32_t u) const { return msg[u]; }
+    __device__ __forceinline__ static double add(double a, double b) { return a + b; }
+    __device__ __forceinline__ static double zero() { return 0.0; }
+};
+struct WalkOp {
+    using T = uint32_t;                     // Java int arithmetic wraps: use unsigned adds
+    const int32_t* msg;
+    __device__ __forceinline__ uint32_t load(int32_t u) const { return static_cast<uint32_t>(msg[u]); }
+    __device__ __forceinline__ static uint32_t add(uint32_t a, uint32_t b) { return a + b; }
+    __device__ __forceinline__ static uint32_t zero() { return 0u; }
+};
+
+template <class T>
+__device__ __forceinline__ T wave_sum(T x) {
+    for (int off = 32; off > 0; off >>= 1) x = x + __shfl_xor(x, off, 64);
+    return x;
+}
+
+// Finalisers: what a vertex does with its gathered sum.
+struct PrFinal {
+    const double* edge_count; double* pr; double* contrib_next; double alpha; double base;
+    __device__ __forceinline__ void operator()(int64_t r, double sum) const {
+        const double p = (alpha * sum) + base;      // PageRankVertexProgram.java:86
+        pr[r] = p;
+        contrib_next[r] = p / edge_count[r];        // :88, edgeCount 0 => +inf (never read)
+    }
+};
+struct WalkFinal {
+    int32_t* next;
+    __device__ __forceinline__ void operator()(int64_t r, uint32_t sum) const { next[r] = static_cast<int32_t>(sum); }
+};
+
+template <class Op, class Fin>
+__global__ void __launch_bounds__(kBlock) gather_short(const int64_t* __restrict__ off,
+        const int32_t* __restrict__ adj, const int64_t* __restrict__ blk, Op op, Fin fin) {
+    using T = typename Op::T;
+    __shared__ T s_val[kTile];
+    const int64_t r0 = blk[blockIdx.x], r1 = blk[blockIdx.x + 1];
+    const int64_t s0 = off[r0], s1 = off[r1];
+    const int64_t nnz = s1 - s0;
+    if (nnz > kTile) return;                          // long row: handled by chunks
+    for (int64_t k = threadIdx.x; k < nnz; k += kBlock) s_val[k] = op.load(adj[s0 + k]);
+    __syncthreads();
+    const int64_t nrows = r1 - r0;
+    if (nrows > 64) {
+        for (int64_t r = r0 + threadIdx.x; r < r1; r += kBlock) {
+            T sum = Op::zero();
+            const int64_t e = off[r + 1] - s0;
+            for (int64_t k = off[r] - s0; k < e; ++k) sum = Op::add(sum, s_val[k]);
+            fin(r, sum);
+        }
+    } else {
+        const int wave = threadIdx.x >> 6;
+        for (int64_t r = r0 + wave; r < r1; r += kBlock / 64) {
+            T sum = Op::zero();
+            const int64_t e = off[r + 1] - s0;
+            for (int64_t k = off[r] - s0 + lane(); k < e; k += 64) sum = Op::add(sum, s_val[k]);
+            sum = wave_sum(sum);
+            if (lane() == 0) fin(r, sum);
+        }
+    }
+}
+
+template <class Op>
+__global__ void __launch_bounds__(kBlock) gather_chunks(const int32_t* __restrict__ adj,
+        const int64_t* __restrict__ cbeg, const int64_t* __restrict__ cend, Op op,
+        typename Op::T* __restrict__ partial) {
+    using T = typename Op::T;
+    __shared__ T s_w[kBlock / 64];
+    const int64_t b = cbeg[blockIdx.x], e = cend[blockIdx.x];
+    T sum = Op::zero();
+    for (int64_t k = b + threadIdx.x; k < e; k += kBlock) sum = Op::add(sum, op.load(adj[k]));
+    sum = wave_sum(sum);
+    if (lane() == 0) s_w[threadIdx.x >> 6] = sum;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        T t = Op::zero();
+        for (int i = 0; i < kBlock / 64; ++i) t = Op::add(t, s_w[i]);
+        partial[blockIdx.x] = t;
+    }
+}
+
+template <class Op, class Fin>
+__global__ void finalize_long(const int64_t* __restrict__ long_row, const int64_t* __restrict__ long_chunk,
+                              int64_t nlong, const typename Op::T* __restrict__ partial, Fin fin) {
+    using T = typename Op::T;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nlong; i += (int64_t)gridDim.x * blockDim.x) {
+        T s = Op::zero();
+        for (int64_t c = long_chunk[i]; c < long_chunk[i + 1]; ++c) s = Op::add(s, partial[c]);
+        fin(long_row[i], s);
+    }
+}
+
+__global__ void pr_init(const int64_t* __restrict__ out_off, double* edge_count, double* contrib,
+                        double* pr, double inv_n, int64_t n) {
+    for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x) {
+        // iteration 1 (PageRankVertexProgram.java:78-83): edgeCount = sum of the inE
+        // messages (1.0 from every out-neighbour), PR = 1/N, send PR/edgeCount on outE.
+        const double ec = static_cast<double>(out_off[v + 1] - out_off[v]);
+        edge_count[v] = ec;
+        pr[v] = inv_n;
+        contrib[v] = inv_n / ec;
+    }
+}
+__global__ void fill_f64(double* p, double v, int64_t n) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = v;
+}
+
+inline int grid_for(int64_t work) {
+    int64_t g = (work + kBlock - 1) / kBlock;
+    if (g < 1) g = 1;
+    if (g > 2048) g = 2048;
+    return static_cast<int>(g);
+}
+
+template <class Op, class Fin>
+hipError_t run_gather(const DevCsr& c, const RowBlocks& rb, Op op, Fin fin,
+                      typename Op::T* partial, hipStream_t s) {
+    if (rb.nblocks > 0) {
+        gather_short<Op, Fin><<<static_cast<unsigned>(rb.nblocks), kBlock, 0, s>>>(c.off, c.adj, rb.blk, op, fin);
+    }
+    if (rb.nchunks > 0) {
+        gather_chunks<Op><<<static_cast<unsigned>(rb.nchunks), kBlock, 0, s>>>(c.adj, rb.chunk_beg, rb.chunk_end, op, partial);
+        finalize_long<Op, Fin><<<grid_for(rb.nlong), kBlock, 0, s>>>(rb.long_row, rb.long_chunk, rb.nlong, partial, fin);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t k_pr_init(const DevCsr& out, double* edge_count, double* contrib, double* pr,
+                     double inv_n, int64_t n, hipStream_t s) {
+    pr_init<<<grid_for(n), kBlock, 0, s>>>(out.off, edge_count, contrib, pr, inv_n, n);
+    return hipGetLastError();
+}
+hipError_t k_fill_f64(double* p, double v, int64_t n, hipStream_t s) {
+    fill_f64<<<grid_for(n), kBlock, 0, s>>>(p, v, n);
+    return hipGetLastError();
+}
+hipError_t k_pr_iter(const DevCsr& in, const RowBlocks& rb, const double* contrib,
+                     const double* edge_count, double* pr, double* contrib_next, double* partial,
+                     double alpha, double base, int64_t n, hipStream_t s) {
+    (void)n;
+    PrOp op{contrib};
+    PrFinal fin{edge_count, pr, contrib_next, alpha, base};
+    return run_gather(in, rb, op, fin, partial, s);
+}
+hipError_t k_walk_iter(const DevCsr& out, const RowBlocks& rb, const int32_t* prev, int32_t* next,
+                       int32_t* partial, int64_t n, hipStream_t s) {
+    (void)n;
+    WalkOp op{prev};
+    WalkFinal fin{next};
+    return run_gather(out, rb, op, fin, reinterpret_cast<uint32_t*>(partial), s);
+}
+
+}  // namespace tgo

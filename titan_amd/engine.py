@@ -1,0 +1,180 @@
+"""Object wrapper over the C-ABI: one Engine = one tgo_ctx (one device)."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib as L
+
+
+class TitanException(RuntimeError):
+    """Mirrors com.thinkaurelius.titan.core.TitanException (status + message of the C-ABI)."""
+
+    def __init__(self, code: int, message: str):
+        super().__init__(f"[{code}] {message}")
+        self.code = code
+
+
+def _check(lib, ctx, rc):
+    if rc != L.TGO_OK:
+        msg = lib.tgo_last_error(ctx).decode(errors="replace") if ctx else "tgo_create failed"
+        raise TitanException(rc, msg)
+
+
+class Schema:
+    """Edge-label / property-key schema (what tx.getExistingRelationType resolves)."""
+
+    def __init__(self, edge_types, property_keys):
+        self._keep = []
+        et = (L.EdgeType * max(1, len(edge_types)))()
+        for i, t in enumerate(edge_types):
+            sk = np.ascontiguousarray(t.get("sort_key", []), dtype=np.int64)
+            sg = np.ascontiguousarray(t.get("signature", []), dtype=np.int64)
+            self._keep += [sk, sg]
+            et[i] = L.EdgeType(t["type_id"], t["multiplicity"], len(sk), L.ptr(sk, C.c_int64),
+                               len(sg), L.ptr(sg, C.c_int64))
+        pk = (L.PropertyKey * max(1, len(property_keys)))()
+        for i, (kid, dt) in enumerate(property_keys):
+            pk[i] = L.PropertyKey(kid, dt)
+        self._keep += [et, pk]
+        self.c = L.Schema(len(edge_types), et, len(property_keys), pk)
+
+    @classmethod
+    def from_dict(cls, d):
+        return cls(d["edge_types"], [tuple(x) for x in d["property_keys"]])
+
+
+class Engine:
+    def __init__(self, device: int = 0, partition_bits: int = 5, host_threads: int = 0,
+                 hard_query_limit: int = 100000):
+        self.lib = L.load()
+        o = L.Options()
+        self.lib.tgo_default_options(C.byref(o))
+        o.device = device
+        o.partition_bits = partition_bits
+        o.host_threads = host_threads
+        o.hard_query_limit = hard_query_limit
+        h = C.c_void_p()
+        rc = self.lib.tgo_create(C.byref(o), C.byref(h))
+        if rc != L.TGO_OK:
+            raise TitanException(rc, "tgo_create failed: no usable gfx950 device "
+                                     "(the engine has no CPU fallback)")
+        self.ctx = h
+        self.n = 0
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            self.lib.tgo_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ loads
+    @staticmethod
+    def _opts(scope, apply_cap, labels, weight_key):
+        lab = np.ascontiguousarray(labels, dtype=np.int64)
+        o = L.LoadOpts(scope, 1 if apply_cap else 0, len(lab), L.ptr(lab, C.c_int64) if len(lab) else None,
+                       weight_key)
+        return o, lab
+
+    def load_rows(self, rows, schema: Schema, scope, apply_cap=True, labels=(), weight_key=0, batch_rows=None):
+        """Feed scanned rows (optionally in work blocks) and finish the load."""
+        opts, keep = self._opts(scope, apply_cap, labels, weight_key)
+        nrows = rows.nrows
+        step = batch_rows or max(nrows, 1)
+        for r0 in range(0, max(nrows, 1), step):
+            r1 = min(nrows, r0 + step)
+            eb = rows.entry_begin[r0:r1 + 1]
+            bb = rows.byte_begin[r0:r1 + 1]
+            keys = np.ascontiguousarray(rows.keys[r0:r1])
+            eb0 = np.ascontiguousarray(eb - eb[0])
+            bb0 = np.ascontiguousarray(bb - bb[0])
+            data = np.ascontiguousarray(rows.data[bb[0]:max(bb[-1], bb[0] + 1)])
+            lv = np.ascontiguousarray(rows.limit_valpos[eb[0]:max(eb[-1], eb[0] + 1)])
+            cr = L.Rows(r1 - r0, L.ptr(keys, C.c_int64), L.ptr(eb0, C.c_int64), L.ptr(bb0, C.c_int64),
+                        L.ptr(data, C.c_uint8), L.ptr(lv, C.c_int64))
+            _check(self.lib, self.ctx, self.lib.tgo_load_rows(self.ctx, C.byref(cr), C.byref(schema.c), C.byref(opts)))
+        _check(self.lib, self.ctx, self.lib.tgo_finish_load(self.ctx))
+        self.n = self.lib.tgo_num_vertices(self.ctx)
+        return self
+
+    def load_edges(self, n, src, dst, scope, weight=None, titan_ids=None, apply_cap=True, weight_key=0):
+        src = np.ascontiguousarray(src, dtype=np.int32)
+        dst = np.ascontiguousarray(dst, dtype=np.int32)
+        w = None if weight is None else np.ascontiguousarray(weight, dtype=np.int32)
+        t = None if titan_ids is None else np.ascontiguousarray(titan_ids, dtype=np.int64)
+        e = L.Edges(n, len(src), L.ptr(src, C.c_int32), L.ptr(dst, C.c_int32), L.ptr(w, C.c_int32),
+                    L.ptr(t, C.c_int64))
+        opts, keep = self._opts(scope, apply_cap, (), weight_key)
+        if w is not None and weight_key == 0:
+            opts.weight_key = 1      # any non-zero key: the edge list carries the weights
+        _check(self.lib, self.ctx, self.lib.tgo_load_edges(self.ctx, C.byref(e), C.byref(opts)))
+        self.n = self.lib.tgo_num_vertices(self.ctx)
+        return self
+
+    def vertex_ids(self):
+        out = np.zeros(self.n, dtype=np.int64)
+        _check(self.lib, self.ctx, self.lib.tgo_vertex_ids(self.ctx, L.ptr(out, C.c_int64)))
+        return out
+
+    # ------------------------------------------------------------------ programs
+    def bfs(self, seed, max_depth, scope, seed_is_dense=False, stats=False, fetch=True):
+        a = L.BfsArgs(int(seed), 1 if seed_is_dense else 0, int(max_depth), scope, L.FLAG_STATS if stats else 0)
+        out = np.zeros(self.n, dtype=np.int64) if fetch else None
+        _check(self.lib, self.ctx, self.lib.tgo_bfs(self.ctx, C.byref(a), L.ptr(out, C.c_int64)))
+        return out
+
+    def sssp(self, seed, max_depth, scope, mode=L.SSSP_HOP_BOUNDED, seed_is_dense=False, stats=False, fetch=True):
+        a = L.SsspArgs(int(seed), 1 if seed_is_dense else 0, int(max_depth), scope, mode, 0,
+                       L.FLAG_STATS if stats else 0, 0)
+        out = np.zeros(self.n, dtype=np.int64) if fetch else None
+        _check(self.lib, self.ctx, self.lib.tgo_sssp(self.ctx, C.byref(a), L.ptr(out, C.c_int64)))
+        return out
+
+    def pagerank(self, alpha, vertex_count, max_iterations, fetch=True):
+        a = L.PrArgs(alpha, int(vertex_count), int(max_iterations), 0)
+        out = np.zeros(self.n, dtype=np.float64) if fetch else None
+        _check(self.lib, self.ctx, self.lib.tgo_pagerank(self.ctx, C.byref(a), L.ptr(out, C.c_double)))
+        return out
+
+    def walkcount(self, k, fetch=True):
+        out = np.zeros(self.n, dtype=np.int32) if fetch else None
+        _check(self.lib, self.ctx, self.lib.tgo_walkcount(self.ctx, int(k), L.ptr(out, C.c_int32)))
+        return out
+
+    def stats(self):
+        s = L.Stats()
+        _check(self.lib, self.ctx, self.lib.tgo_stats_get(self.ctx, C.byref(s)))
+        return {f: getattr(s, f) for f, _ in L.Stats._fields_}
+
+    def sync(self):
+        _check(self.lib, self.ctx, self.lib.tgo_sync(self.ctx))
+
+
+def rmat_edges(scale, edge_factor=16, seed=0x54495441, weights=False, threads=0):
+    """Synthetic RMAT edge list (include/tgo_synth.h)."""
+    lib = L.load()
+    m = edge_factor << scale
+    src = np.empty(m, dtype=np.int32)
+    dst = np.empty(m, dtype=np.int32)
+    w = np.empty(m, dtype=np.int32) if weights else None
+    rc = lib.tgo_rmat_edges(scale, edge_factor, seed, 0, m, L.ptr(src, C.c_int32), L.ptr(dst, C.c_int32),
+                            L.ptr(w, C.c_int32), threads)
+    if rc:
+        raise TitanException(rc, "tgo_rmat_edges failed")
+    return src, dst, w
+
+
+def pick_roots(n, src, dst, nroots=64, seed=7):
+    lib = L.load()
+    out = np.zeros(nroots, dtype=np.int64)
+    rc = lib.tgo_pick_roots(n, len(src), L.ptr(src, C.c_int32), L.ptr(dst, C.c_int32), seed, nroots,
+                            L.ptr(out, C.c_int64))
+    if rc:
+        raise TitanException(rc, "tgo_pick_roots failed")
+    return out
