@@ -195,7 +195,8 @@ typedef struct {
 
 typedef struct {
     int64_t num_vertices;         /* executed (non-ghost, visible) vertices                   */
-    int64_t num_entries;          /* adjacency entries kept (both directions)                  */
+    int64_t out_entries;          /* OUT-list entries kept (out-CSR)                           */
+    int64_t in_entries;           /* IN-list entries kept (in-CSR)                             */
     int64_t ghost_vertices;       /* VertexJobConverter GHOST_VERTEX_COUNT ("ghost-vertices")  */
     int64_t truncated_results;    /* VertexJobConverter TRUNCATED_ENTRY_LISTS ("truncated-results") */
     int64_t skipped_rows;         /* rows rejected by the key filter (Invisible ids)           */

@@ -101,6 +101,7 @@ def load() -> C.CDLL:
                                      P(C.c_int), _i64p, _i64p, P(C.c_int), _i64p]),
         "fr_load_rows": (C.c_int, [P(FrRows), P(FrSchema), P(FrLoadOpts), P(vp), P(FrLoadStats)]),
         "fr_load_adjacency": (C.c_int, [C.c_int64, _i64p, _i64p, _i64p, _i32p, _i32p, P(vp)]),
+        "fr_load_edges": (C.c_int, [C.c_int64, C.c_int64, _i32p, _i32p, _i32p, _i64p, P(vp)]),
         "fr_free": (None, [vp]),
         "fr_num_vertices": (C.c_int64, [vp]),
         "fr_vertex_ids": (None, [vp, _i64p]),
@@ -217,6 +218,20 @@ class OracleGraph:
                                    _p(adj, C.c_int32), _p(w, C.c_int32), C.byref(h))
         if rc:
             raise RuntimeError(f"fr_load_adjacency rc={rc}")
+        return cls(h)
+
+    @classmethod
+    def from_edges(cls, n, src, dst, w=None, titan_ids=None):
+        lib = load()
+        src = np.ascontiguousarray(src, np.int32)
+        dst = np.ascontiguousarray(dst, np.int32)
+        w = None if w is None else np.ascontiguousarray(w, np.int32)
+        ids = (np.arange(n, dtype=np.int64) + 1) << 3 if titan_ids is None else np.ascontiguousarray(titan_ids, np.int64)
+        h = C.c_void_p()
+        rc = lib.fr_load_edges(n, len(src), _p(src, C.c_int32), _p(dst, C.c_int32), _p(w, C.c_int32),
+                               _p(ids, C.c_int64), C.byref(h))
+        if rc:
+            raise RuntimeError(f"fr_load_edges rc={rc}")
         return cls(h)
 
     def __del__(self):

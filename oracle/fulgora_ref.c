@@ -506,6 +506,52 @@ int fr_load_adjacency(int64_t n, const int64_t* titan_ids, const int64_t* off, c
     return FR_OK;
 }
 
+int fr_load_edges(int64_t n, int64_t m, const int32_t* src, const int32_t* dst, const int32_t* w,
+                  const int64_t* titan_ids, fr_graph** out) {
+    /* Rows as the commit path writes them (StandardTitanGraph.java:564-591): every edge
+     * u->v gives an OUT entry on row u and an IN entry on row v; within a row OUT entries
+     * precede IN entries and each run is ordered by (other id, relation id = edge index). */
+    fr_graph* g = (fr_graph*)calloc(1, sizeof(fr_graph));
+    g->n = n;
+    g->titan_id = (int64_t*)malloc((n + 1) * sizeof(int64_t));
+    g->eoff = (int64_t*)calloc(n + 1, sizeof(int64_t));
+    int64_t E = 2 * m;
+    g->other = (int64_t*)malloc((E + 1) * sizeof(int64_t));
+    g->edir = (uint8_t*)malloc(E + 1);
+    g->has_w = (uint8_t*)malloc(E + 1);
+    g->w = (int32_t*)malloc((E + 1) * sizeof(int32_t));
+    for (int64_t v = 0; v < n; v++) g->titan_id[v] = titan_ids[v];
+    int64_t* outc = (int64_t*)calloc(n + 1, sizeof(int64_t));
+    for (int64_t k = 0; k < m; k++) { outc[src[k]]++; g->eoff[src[k] + 1]++; g->eoff[dst[k] + 1]++; }
+    for (int64_t v = 0; v < n; v++) g->eoff[v + 1] += g->eoff[v];
+    int64_t* po = (int64_t*)malloc((n + 1) * sizeof(int64_t));
+    int64_t* pi = (int64_t*)malloc((n + 1) * sizeof(int64_t));
+    for (int64_t v = 0; v < n; v++) { po[v] = g->eoff[v]; pi[v] = g->eoff[v] + outc[v]; }
+    /* counting sort by neighbour keeps edge-index order among equal neighbours */
+    int64_t* bucket = (int64_t*)calloc(n + 1, sizeof(int64_t));
+    int64_t* order = (int64_t*)malloc((m + 1) * sizeof(int64_t));
+    for (int pass = 0; pass < 2; pass++) {
+        const int32_t* key = pass == 0 ? dst : src;      /* neighbour of the OUT / IN entry */
+        const int32_t* own = pass == 0 ? src : dst;
+        memset(bucket, 0, (n + 1) * sizeof(int64_t));
+        for (int64_t k = 0; k < m; k++) bucket[key[k] + 1]++;
+        for (int64_t v = 0; v < n; v++) bucket[v + 1] += bucket[v];
+        for (int64_t k = 0; k < m; k++) order[bucket[key[k]]++] = k;
+        for (int64_t j = 0; j < m; j++) {
+            int64_t k = order[j];
+            int64_t p = pass == 0 ? po[own[k]]++ : pi[own[k]]++;
+            g->other[p] = titan_ids[key[k]];
+            g->edir[p] = (uint8_t)pass;
+            g->has_w[p] = w != NULL;
+            g->w[p] = w ? w[k] : 0;
+        }
+    }
+    free(outc); free(po); free(pi); free(bucket); free(order);
+    build_hash(g);
+    *out = g;
+    return FR_OK;
+}
+
 int64_t fr_export(const fr_graph* g, int64_t* off, int64_t* mid, int32_t* adj, int32_t* w) {
     /* dense form with OUT entries first within each row (stable); entries whose other
      * endpoint is not an executed vertex are dropped: they can never carry a message

@@ -114,6 +114,9 @@ int  fr_load_rows(const fr_rows* rows, const fr_schema* schema, const fr_load_op
  * copied into the oracle's Titan-id keyed form. w may be NULL. */
 int  fr_load_adjacency(int64_t n, const int64_t* titan_ids, const int64_t* off, const int64_t* mid,
                        const int32_t* adj, const int32_t* w, fr_graph** out);
+/* Rows from a directed edge list (both entries per edge, column order). w may be NULL. */
+int  fr_load_edges(int64_t n, int64_t m, const int32_t* src, const int32_t* dst, const int32_t* w,
+                   const int64_t* titan_ids, fr_graph** out);
 void fr_free(fr_graph* g);
 int64_t fr_num_vertices(const fr_graph* g);
 void fr_vertex_ids(const fr_graph* g, int64_t* out);

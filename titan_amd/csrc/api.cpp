@@ -150,7 +150,8 @@ int upload_graph(tgo_ctx* ctx, HostGraph& h) {
     ctx->id_index.reserve(static_cast<size_t>(n) * 2);
     for (int64_t v = 0; v < n; ++v) ctx->id_index.emplace(h.titan_id[v], v);
     ctx->st.num_vertices = n;
-    ctx->st.num_entries = static_cast<int64_t>(h.out.adj.size() + h.in.adj.size());
+    ctx->st.out_entries = static_cast<int64_t>(h.out.adj.size());
+    ctx->st.in_entries = static_cast<int64_t>(h.in.adj.size());
     ctx->st.ghost_vertices = h.ghost;
     ctx->st.truncated_results = h.truncated;
     ctx->st.skipped_rows = h.skipped;
