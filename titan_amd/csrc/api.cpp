@@ -25,6 +25,7 @@ struct tgo_ctx {
     DevGraph g;
     bool loaded = false;
     std::vector<int64_t> titan_id;
+    std::vector<int32_t> perm;                       // row-order dense -> internal
     std::unordered_map<int64_t, int64_t> id_index;   // Titan id -> dense (seed lookup)
     Scratch sc;
     tgo_stats st{};
@@ -146,6 +147,9 @@ int upload_graph(tgo_ctx* ctx, HostGraph& h) {
     }
     HIP_TRY(hipDeviceSynchronize());
     ctx->titan_id = h.titan_id;
+    ctx->perm = h.perm;
+    if (ctx->perm.empty()) { ctx->perm.resize(n); for (int64_t v = 0; v < n; ++v) ctx->perm[v] = static_cast<int32_t>(v); }
+    HIP_TRY(upload(ctx, g.perm, ctx->perm));
     ctx->id_index.clear();
     ctx->id_index.reserve(static_cast<size_t>(n) * 2);
     for (int64_t v = 0; v < n; ++v) ctx->id_index.emplace(h.titan_id[v], v);
@@ -183,11 +187,11 @@ View push_view(const DevGraph& g, int scope) {
 int resolve_seed(tgo_ctx* ctx, int64_t seed, int is_dense, int64_t& out) {
     if (is_dense) {
         if (seed < 0 || seed >= ctx->g.n) return fail(ctx, TGO_E_INVALID, "dense seed out of range");
-        out = seed;
+        out = ctx->perm[seed];
         return TGO_OK;
     }
     auto it = ctx->id_index.find(seed);
-    out = it == ctx->id_index.end() ? -1 : it->second;   // unknown seed: nobody gets a distance
+    out = it == ctx->id_index.end() ? -1 : ctx->perm[it->second];   // unknown seed: nobody gets a distance
     return TGO_OK;
 }
 
@@ -324,7 +328,9 @@ int finish_distance_program(tgo_ctx* ctx, int scope, int flags, int64_t* dist_ou
         ctx->st.reached_entries = static_cast<int64_t>(s.hcnt->red[1]);
     }
     if (dist_out) {
-        HIP_TRY(hipMemcpy(dist_out, s.dist, ctx->g.n * sizeof(int64_t), hipMemcpyDeviceToHost));
+        HIP_TRY(k_unpermute_i64(s.dist, ctx->g.perm, s.msg, ctx->g.n, ctx->stream));
+        HIP_TRY(hipMemcpyAsync(dist_out, s.msg, ctx->g.n * sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
     }
     (void)scope;
     return TGO_OK;
@@ -487,7 +493,9 @@ int tgo_copy_distances(tgo_ctx* ctx, int64_t* dist_out) {
     if (!ctx || !dist_out) return TGO_E_INVALID;
     if (!ctx->loaded) return fail(ctx, TGO_E_STATE, "no graph loaded");
     HIP_TRY(hipStreamSynchronize(ctx->stream));
-    HIP_TRY(hipMemcpy(dist_out, ctx->sc.dist, ctx->g.n * sizeof(int64_t), hipMemcpyDeviceToHost));
+    HIP_TRY(k_unpermute_i64(ctx->sc.dist, ctx->g.perm, ctx->sc.msg, ctx->g.n, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(dist_out, ctx->sc.msg, ctx->g.n * sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
     return TGO_OK;
 }
 
@@ -525,7 +533,11 @@ int tgo_pagerank(tgo_ctx* ctx, const tgo_pr_args* a, double* pr_out) {
     HIP_TRY(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
     ctx->st.last_kernel_ms = ms;
     ctx->st.iterations = a->max_iterations;
-    if (pr_out) HIP_TRY(hipMemcpy(pr_out, pr, n * sizeof(double), hipMemcpyDeviceToHost));
+    if (pr_out) {
+        HIP_TRY(k_unpermute_i64(reinterpret_cast<const int64_t*>(pr), g.perm, s.msg, n, st));
+        HIP_TRY(hipMemcpyAsync(pr_out, s.msg, n * sizeof(double), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+    }
     return TGO_OK;
 }
 
@@ -554,7 +566,11 @@ int tgo_walkcount(tgo_ctx* ctx, int32_t k, int32_t* out) {
     HIP_TRY(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
     ctx->st.last_kernel_ms = ms;
     ctx->st.iterations = k;
-    if (out) HIP_TRY(hipMemcpy(out, a, n * sizeof(int32_t), hipMemcpyDeviceToHost));
+    if (out) {
+        HIP_TRY(k_unpermute_i32(a, g.perm, s.level, n, st));
+        HIP_TRY(hipMemcpyAsync(out, s.level, n * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+    }
     return TGO_OK;
 }
 

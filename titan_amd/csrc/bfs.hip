@@ -25,6 +25,7 @@ constexpr int kBlock = 256;
 constexpr int kEdgesPerThread = 8;
 constexpr int kTileEdges = kBlock * kEdgesPerThread;   // 2048 edges per block tile
 constexpr int kLdsEntries = kTileEdges + 2;
+constexpr int64_t kSerialScan = 32;    // bottom-up: longer lists are scanned by the whole wave
 
 __device__ __forceinline__ int lane() { return static_cast<int>(threadIdx.x & 63); }
 
@@ -171,16 +172,44 @@ __global__ void __launch_bounds__(kBlock) bu_step(View pull, View push, int64_t 
         const uint64_t vis = vb[wd];
         const int64_t v = (wd << 6) + lane();
         bool found = false;
-        if (v < n && !((vis >> lane()) & 1ULL)) {
-            for (int l = 0; l < pull.nlists && !found; ++l) {
-                const int64_t* off = l == 0 ? pull.off0 : pull.off1;
+        const bool open = v < n && !((vis >> lane()) & 1ULL);
+        int64_t b0 = 0, e0 = 0, b1 = 0, e1 = 0;
+        if (open) {
+            b0 = pull.off0[v]; e0 = pull.off0[v + 1];
+            if (pull.nlists > 1) { b1 = pull.off1[v]; e1 = pull.off1[v + 1]; }
+        }
+        const int64_t deg = (e0 - b0) + (e1 - b1);
+        // short lists: the lane scans its own list and stops at the first frontier hit
+        if (open && deg <= kSerialScan) {
+            for (int64_t k = b0; k < e0 && !found; ++k) {
+                const int32_t u = pull.adj0[k];
+                found = (fb[u >> 6] >> (u & 63)) & 1ULL;
+            }
+            for (int64_t k = b1; k < e1 && !found; ++k) {
+                const int32_t u = pull.adj1[k];
+                found = (fb[u >> 6] >> (u & 63)) & 1ULL;
+            }
+        }
+        // long lists: the whole wave scans one list 64 entries at a time (ballot exit)
+        unsigned long long big = __ballot(open && deg > kSerialScan);
+        while (big) {
+            const int src = __ffsll(static_cast<long long>(big)) - 1;
+            big &= big - 1;
+            bool hit = false;
+            for (int l = 0; l < 2 && !hit; ++l) {
+                const int64_t bb = __shfl(l == 0 ? b0 : b1, src, 64);
+                const int64_t ee = __shfl(l == 0 ? e0 : e1, src, 64);
                 const int32_t* adj = l == 0 ? pull.adj0 : pull.adj1;
-                const int64_t e = off[v + 1];
-                for (int64_t k = off[v]; k < e; ++k) {
-                    const int32_t u = adj[k];
-                    if ((fb[u >> 6] >> (u & 63)) & 1ULL) { found = true; break; }
+                for (int64_t k = bb; k < ee; k += 64) {
+                    bool h = false;
+                    if (k + lane() < ee) {
+                        const int32_t u = adj[k + lane()];
+                        h = (fb[u >> 6] >> (u & 63)) & 1ULL;
+                    }
+                    if (__ballot(h)) { hit = true; break; }
                 }
             }
+            if (lane() == src) found = hit;
         }
         const unsigned long long fm = __ballot(found);
         if (lane() == 0) {
@@ -308,6 +337,13 @@ __global__ void dist_finalize(int64_t* dist, int64_t n) {
         if (dist[i] == INT64_MAX) dist[i] = INT64_MIN;
 }
 
+// out[v] = in[perm[v]]: internal (degree-grouped) order -> the API's row order.
+template <class T>
+__global__ void gather_perm(const T* __restrict__ in, const int32_t* __restrict__ perm, T* __restrict__ out, int64_t n) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = in[perm[i]];
+}
+
 inline int grid_for(int64_t work, int block = kBlock, int cap = 256 * 8) {
     int64_t g = (work + block - 1) / block;
     if (g < 1) g = 1;
@@ -371,6 +407,14 @@ hipError_t k_sssp_commit(const int32_t* q, int64_t qlen, const int64_t* dist, in
                          uint64_t* mark, hipStream_t s) {
     (void)mark;
     sssp_commit<<<grid_for(qlen), kBlock, 0, s>>>(q, qlen, dist, msg);
+    return hipGetLastError();
+}
+hipError_t k_unpermute_i64(const int64_t* in, const int32_t* perm, int64_t* out, int64_t n, hipStream_t s) {
+    gather_perm<int64_t><<<grid_for(n), kBlock, 0, s>>>(in, perm, out, n);
+    return hipGetLastError();
+}
+hipError_t k_unpermute_i32(const int32_t* in, const int32_t* perm, int32_t* out, int64_t n, hipStream_t s) {
+    gather_perm<int32_t><<<grid_for(n), kBlock, 0, s>>>(in, perm, out, n);
     return hipGetLastError();
 }
 hipError_t k_dist_finalize(int64_t* dist, int64_t n, hipStream_t s) {

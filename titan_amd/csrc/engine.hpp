@@ -29,7 +29,8 @@ struct HostCsr {
 
 struct HostGraph {
     int64_t n = 0;
-    std::vector<int64_t> titan_id;
+    std::vector<int64_t> titan_id;   // row order (the API's dense ids)
+    std::vector<int32_t> perm;       // row-order dense id -> internal id (degree-grouped)
     HostCsr out, in;
     HostCsr push_t;             // explicit transpose of the pull view (cap / asymmetric rows)
     bool has_transpose = false;
@@ -93,6 +94,7 @@ struct RowBlocks {
 
 struct DevGraph {
     int64_t n = 0;
+    int32_t* perm = nullptr;    // row-order dense id -> internal id (device)
     DevCsr out, in, push_t;
     bool has_transpose = false;
     bool has_weight = false;
@@ -159,6 +161,8 @@ hipError_t k_sssp_relax(const View& push, const int32_t* q, const int64_t* qpre,
 hipError_t k_sssp_commit(const int32_t* q, int64_t qlen, const int64_t* dist, int64_t* msg,
                          uint64_t* mark, hipStream_t s);
 hipError_t k_dist_finalize(int64_t* dist, int64_t n, hipStream_t s);
+hipError_t k_unpermute_i64(const int64_t* in, const int32_t* perm, int64_t* out, int64_t n, hipStream_t s);
+hipError_t k_unpermute_i32(const int32_t* in, const int32_t* perm, int32_t* out, int64_t n, hipStream_t s);
 
 // CSR-adaptive gather
 hipError_t k_pr_init(const DevCsr& out, double* edge_count, double* contrib, double* pr,
