@@ -1,14 +1,17 @@
 #!/usr/bin/env python3
-"""Bench: BFS GTEPS + PageRank s/iter on RMAT (BASELINE.json metric, configs[2]).
+"""Bench: BFS GTEPS + PageRank s/iter on RMAT (BASELINE.json metric).
 
 One step = one pass of the hot path over the synthetic graph resident in HBM:
-  64-root BFS sweep (ShortestDistanceVertexProgram with unit weights over bothE, full
+  a 64-root BFS sweep (ShortestDistanceVertexProgram with unit weights over bothE, full
   hop depth = Graph500-style undirected BFS) + one PageRankVertexProgram run with
   iterations(20) (19 rank updates, alpha 0.85, N = 2^scale, parity cap on).
 value = BFS GTEPS over the timed steps = sum of input edges with a reached endpoint
 (m_R / 2 for bothE) / BFS wall time.  PageRank is reported as pagerank_s_per_iter.
 
-Launch: python bench.py [--gpus 1 --steps K --warmup W]; N>1 via torch.distributed.run.
+N = 1: RMAT scale 24 on one MI355X (configs[2]).
+N > 1: weak scaling, RMAT scale 24 + log2(N) (N = 8 -> scale 27, configs[3]), 1-D vertex
+       partitioned, one process per GPU, RCCL exchanges (titan_amd/distributed.py).
+Launch: python bench.py [--steps K --warmup W]; N > 1 via torch.distributed.run.
 """
 from __future__ import annotations
 
@@ -25,6 +28,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8 TB/s peak (spec)
+METRIC = "BFS GTEPS + PageRank s/iter, RMAT scale-24 (1 GPU) and scale-27 (1/2/4/8 GPU)"
 
 
 def log(*a):
@@ -37,7 +41,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--scale", type=int, default=24)
+    p.add_argument("--scale", type=int, default=24, help="per-GPU scale; N GPUs run scale + log2(N)")
     p.add_argument("--edge-factor", type=int, default=16)
     p.add_argument("--roots", type=int, default=64)
     p.add_argument("--pr-iters", type=int, default=20)
@@ -46,38 +50,62 @@ def parse():
     return p.parse_args()
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+def roofline(kernel, achieved_gbs, unit_desc):
+    return {"kernel": kernel, "bound": "hbm", "achieved": round(achieved_gbs, 2), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": None,
+            "bytes_per_unit": unit_desc}
+
+
+def result_line(args, world, scale, n, m, roots, elapsed, teps, hmean, pr_s_iter, e_in, roof_bfs, roof_pr,
+                bfs_share, cpu, parallelism):
+    return {
+        "metric": METRIC,
+        "value": round(teps / 1e9, 4),
+        "unit": "GTEPS",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32 (BFS levels); f64 (PageRank)",
+        "data": "synthetic RMAT (Graph500 A/B/C=0.57/0.19/0.19, ef16, seeded), 64 seeded roots",
+        "config": {"workload": f"rmat{scale}-bfs{len(roots)}-bothE+pagerank{args.pr_iters}", "scale": scale,
+                   "edge_factor": args.edge_factor, "vertices": n, "edges": int(m), "roots": len(roots),
+                   "pr_iterations": args.pr_iters, "parallelism": parallelism},
+        "gteps_hmean": round(hmean / 1e9, 4) if hmean else None,
+        "pagerank_s_per_iter": round(pr_s_iter, 6),
+        "pagerank_edges_per_s": round(e_in / pr_s_iter, 1),
+        "bfs_share_of_step": round(bfs_share, 3),
+        "roofline": roof_bfs if bfs_share >= 0.5 else roof_pr,
+        "roofline_bfs": roof_bfs,
+        "roofline_pagerank": roof_pr,
+        "cpu_baseline": cpu,
+    }
+
+
+# ----------------------------------------------------------------------------- 1 GPU
+def run_single(args):
     import torch
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("gloo")
     from titan_amd import Engine, pick_roots, rmat_edges
     from titan_amd import _lib as L
-
-    # Weak scaling: every rank keeps a scale-`args.scale` share (replicas until the
-    # vertex-partitioned path lands; see DESIGN.md "Multi-GPU").
     scale = args.scale
     n = 1 << scale
     t0 = time.perf_counter()
-    src, dst, _ = rmat_edges(scale, args.edge_factor, seed=0x54495441 + (rank if world > 1 else 0))
+    src, dst, _ = rmat_edges(scale, args.edge_factor, seed=0x54495441)
     m = len(src)
     roots = pick_roots(n, src, dst, args.roots, seed=7)
     log(f"rmat scale {scale}: n={n} m={m} generated in {time.perf_counter() - t0:.1f}s")
-
     t0 = time.perf_counter()
-    bfs_eng = Engine(device=local_rank, host_threads=16).load_edges(n, src, dst, L.SCOPE_BOTH_E, apply_cap=False)
+    bfs_eng = Engine(device=0, host_threads=16).load_edges(n, src, dst, L.SCOPE_BOTH_E, apply_cap=False)
     log(f"bfs graph (bothE, uncapped) loaded in {time.perf_counter() - t0:.1f}s")
     t0 = time.perf_counter()
-    pr_eng = Engine(device=local_rank, host_threads=16).load_edges(n, src, dst, L.SCOPE_IN_E, apply_cap=True)
+    pr_eng = Engine(device=0, host_threads=16).load_edges(n, src, dst, L.SCOPE_IN_E, apply_cap=True)
     pst = pr_eng.stats()
-    log(f"pagerank graph (inE, capped: {pst['truncated_results']} truncated rows) loaded in {time.perf_counter() - t0:.1f}s")
-
-    # Per-root reached counts (untimed): m_R, n_R for GTEPS and algorithmic bytes.
+    log(f"pagerank graph (inE, capped: {pst['truncated_results']} truncated rows) loaded in "
+        f"{time.perf_counter() - t0:.1f}s")
+    # per-root reached counts (untimed): m_R, n_R for GTEPS and algorithmic bytes
     mR = np.zeros(len(roots), np.int64)
     nR = np.zeros(len(roots), np.int64)
     depth = np.zeros(len(roots), np.int64)
@@ -86,7 +114,7 @@ def main():
         st = bfs_eng.stats()
         mR[i], nR[i], depth[i] = st["reached_entries"], st["reached"], st["levels"]
 
-    def step(timed):
+    def step():
         bt = np.zeros(len(roots))
         bk = np.zeros(len(roots))
         for i, r in enumerate(roots):
@@ -96,92 +124,134 @@ def main():
             bk[i] = bfs_eng.stats()["last_kernel_ms"] / 1e3
         t = time.perf_counter()
         pr_eng.pagerank(0.85, n, args.pr_iters, fetch=False)
-        pt = time.perf_counter() - t
-        pk = pr_eng.stats()["last_kernel_ms"] / 1e3
-        return bt, bk, pt, pk
+        return bt, bk, time.perf_counter() - t, pr_eng.stats()["last_kernel_ms"] / 1e3
 
     for _ in range(args.warmup):
-        step(False)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize() if torch.cuda.is_available() else None
+        step()
+    torch.cuda.synchronize()
     T0 = time.perf_counter()
-    bts, bks, pts, pks = [], [], [], []
-    for _ in range(args.steps):
-        bt, bk, pt, pk = step(True)
-        bts.append(bt); bks.append(bk); pts.append(pt); pks.append(pk)
-    torch.cuda.synchronize() if torch.cuda.is_available() else None
-    if dist:
-        dist.barrier()
+    res = [step() for _ in range(args.steps)]
+    torch.cuda.synchronize()
     elapsed = time.perf_counter() - T0
-    bfs_wall = float(np.sum(bts))
-    if dist:
-        t = torch.tensor([elapsed, bfs_wall], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, bfs_wall = float(t[0]), float(t[1])
-
-    edges_in = mR / 2.0                              # Graph500 undirected count for bothE
-    teps_total = float(edges_in.sum()) * args.steps * world / bfs_wall
-    per_root_t = np.mean(np.stack(bts), axis=0)
-    hmean = len(roots) / float(np.sum(per_root_t / edges_in))
-    # roofline: SURVEY.md §8(d) algorithmic bytes, per BFS root (all its level launches)
+    bts = np.stack([r[0] for r in res])
+    bks = np.stack([r[1] for r in res])
+    pts = np.array([r[2] for r in res])
+    pks = np.array([r[3] for r in res])
+    edges_in = mR / 2.0                      # Graph500 undirected count for bothE
+    teps = float(edges_in.sum()) * args.steps / float(bts.sum())
+    hmean = len(roots) / float(np.sum(bts.mean(axis=0) / edges_in))
+    # roofline: BFS per root 4*m_R + 8*n_R + 4*n over the root's device time
     bfs_bytes = 4.0 * mR + 8.0 * nR + 4.0 * n
-    bfs_dev = np.mean(np.stack(bks), axis=0)
-    bfs_achieved = float(bfs_bytes.sum() / bfs_dev.sum()) / 1e9
+    roof_bfs = roofline("bfs_root (all level launches of one root)", float(bfs_bytes.sum() / bks.mean(axis=0).sum()) / 1e9,
+                        "4*m_R + 8*n_R + 4*n per root")
     upd = max(args.pr_iters - 1, 1)
-    pr_s_iter = float(np.mean(pts)) / upd
-    pr_dev_iter = float(np.mean(pks)) / upd
-    # PageRank per update: in-CSR index 4m + offsets 8(n+1) + contributions read 8n +
-    # rank write 8n + next contribution write 8n  
-    res = {}
+    e_in = int(pst["in_entries"])
+    pr_bytes = 4.0 * e_in + 8.0 * (n + 1) + 24.0 * n
+    roof_pr = roofline("pagerank_update (gather_short + long-row chunks)", pr_bytes / (pks.mean() / upd) / 1e9,
+                       "4*m + 8*(n+1) + 24*n per update")
+    bfs_share = float(bts.sum()) / (float(bts.sum()) + float(pts.sum()))
+    cpu = None
+    if args.cpu_baseline:
+        # levels counts the final empty level; the eccentricity is one less
+        cpu = cpu_baseline(n, src, dst, roots, mR, max(int(depth[0]) - 1, 1), args.cpu_threads)
+    print(json.dumps(result_line(args, 1, scale, n, m, roots, elapsed, teps, hmean, float(pts.mean()) / upd, e_in,
+                                 roof_bfs, roof_pr, bfs_share, cpu, "single")), flush=True)
+
+
+# ----------------------------------------------------------------------------- N GPUs
+def run_partitioned(args, world, rank, local_rank):
+    import ctypes as C
+    import torch
+    import torch.distributed as dist
+    from titan_amd import Engine
+    from titan_amd import _lib as L
+    from titan_amd.distributed import HipPartBackend, distributed_bfs, distributed_pagerank, partition_range
+    torch.cuda.set_device(local_rank)
+    dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    scale = args.scale + int(round(math.log2(world)))
+    n = 1 << scale
+    m = args.edge_factor << scale
+    lo, hi = partition_range(n, world, rank)
+    lib = L.load()
+    t0 = time.perf_counter()
+    cap = int(2.3 * m / world) + (1 << 22)
+    src = np.empty(cap, np.int32)
+    dst = np.empty(cap, np.int32)
+    cnt = C.c_int64()
+    rc = lib.tgo_rmat_partition(scale, args.edge_factor, 0x54495441, lo, hi, L.ptr(src, C.c_int32),
+                                L.ptr(dst, C.c_int32), None, cap, C.byref(cnt), 16)
+    if rc:
+        raise RuntimeError(f"tgo_rmat_partition rc={rc} count={cnt.value} cap={cap}")
+    src, dst = src[:cnt.value], dst[:cnt.value]
+    log(f"rmat scale {scale} partition [{lo},{hi}) of {world}: {cnt.value} edges in {time.perf_counter() - t0:.1f}s")
+    stream = torch.cuda.current_stream().cuda_stream
+    t0 = time.perf_counter()
+    bfs_be = HipPartBackend(Engine(device=local_rank, host_threads=16, stream=stream)
+                            .load_partition(n, lo, hi, src, dst, L.SCOPE_BOTH_E, apply_cap=False), n, lo, hi)
+    pr_eng = Engine(device=local_rank, host_threads=16, stream=stream).load_partition(n, lo, hi, src, dst,
+                                                                                    L.SCOPE_IN_E, apply_cap=True)
+    pr_be = HipPartBackend(pr_eng, n, lo, hi)
+    log(f"partition graphs loaded in {time.perf_counter() - t0:.1f}s")
+    # roots: seeded candidates, kept when their (global) degree is > 0
+    rng = np.random.default_rng(7)
+    cand = rng.integers(0, n, size=max(16 * args.roots, 1024))
+    own = (src >= lo) & (src < hi)
+    deg = np.bincount(src[own] - lo, minlength=hi - lo) + np.bincount(dst[(dst >= lo) & (dst < hi)] - lo, minlength=hi - lo)
+    ok = np.array([deg[c - lo] > 0 if lo <= c < hi else 0 for c in cand], np.int64)
+    okt = torch.from_numpy(ok).cuda()
+    dist.all_reduce(okt)
+    roots = [int(c) for c, k in zip(cand, okt.cpu().numpy()) if k > 0]
+    roots = list(dict.fromkeys(roots))[:args.roots]
+    mR = np.zeros(len(roots), np.int64)
+    for i, r in enumerate(roots):
+        _, reached, _ = distributed_bfs(bfs_be, r, n, fetch=False, stats=True)
+        mR[i] = reached[1]
+
+    def step():
+        bt = np.zeros(len(roots))
+        for i, r in enumerate(roots):
+            t = time.perf_counter()
+            distributed_bfs(bfs_be, r, n, fetch=False, stats=False)
+            bt[i] = time.perf_counter() - t
+        t = time.perf_counter()
+        distributed_pagerank(pr_be, 0.85, n, args.pr_iters, fetch=False)
+        torch.cuda.synchronize()
+        return bt, time.perf_counter() - t
+
+    for _ in range(args.warmup):
+        step()
+    dist.barrier()
+    torch.cuda.synchronize()
+    T0 = time.perf_counter()
+    res = [step() for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    dist.barrier()
+    elapsed = time.perf_counter() - T0
+    bts = np.stack([r[0] for r in res])
+    pts = np.array([r[1] for r in res])
+    t = torch.tensor([elapsed, float(bts.sum()), float(pts.mean())], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, bfs_wall, pr_wall = [float(x) for x in t.cpu()]
+    e_loc = torch.tensor([float(pr_eng.stats()["in_entries"])], dtype=torch.float64, device="cuda")
+    dist.all_reduce(e_loc)
+    e_in = int(e_loc.item())
     if rank == 0:
-        e_in = int(pst["in_entries"])
-        pr_bytes = 4.0 * e_in + 8.0 * (n + 1) + 24.0 * n
-        pr_achieved = pr_bytes / pr_dev_iter / 1e9
-        bfs_share = float(np.sum(bts)) / (float(np.sum(bts)) + float(np.sum(pts)))
-        roof_bfs = {"kernel": "bfs_root (all level launches of one root)", "bound": "hbm",
-                    "achieved": round(bfs_achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(bfs_achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                    "bytes_per_unit": "4*m_R + 8*n_R + 4*n per root"}
-        roof_pr = {"kernel": "pagerank_update (gather_short + long-row chunks)", "bound": "hbm",
-                   "achieved": round(pr_achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                   "frac": round(pr_achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                   "bytes_per_unit": "4*m + 8*(n+1) + 24*n per update"}
-        dominant = roof_bfs if bfs_share >= 0.5 else roof_pr
-        cpu = None
-        if args.cpu_baseline:
-            # levels counts the final empty level; the eccentricity is one less
-            cpu = cpu_baseline(n, src, dst, roots, mR, max(int(depth[0]) - 1, 1), args.cpu_threads)
-        res = {
-            "metric": "BFS GTEPS + PageRank s/iter, RMAT scale-24 (1 GPU) and scale-27 (1/2/4/8 GPU)",
-            "value": round(teps_total / 1e9, 4),
-            "unit": "GTEPS",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "int32 (BFS levels); f64 (PageRank)",
-            "data": "synthetic RMAT (Graph500 A/B/C=0.57/0.19/0.19, ef16, seeded), 64 seeded roots",
-            "config": {"workload": f"rmat{scale}-bfs{len(roots)}-bothE+pagerank{args.pr_iters}",
-                       "scale": scale, "edge_factor": args.edge_factor, "vertices": n, "edges": int(m),
-                       "roots": len(roots), "pr_iterations": args.pr_iters,
-                       "parallelism": "single" if world == 1 else f"replica{world}"},
-            "gteps_hmean": round(hmean / 1e9, 4),
-            "pagerank_s_per_iter": round(pr_s_iter, 6),
-            "pagerank_edges_per_s": round(e_in / pr_s_iter, 1),
-            "bfs_share_of_step": round(bfs_share, 3),
-            "roofline": dominant,
-            "roofline_bfs": roof_bfs,
-            "roofline_pagerank": roof_pr,
-            "cpu_baseline": cpu,
-        }
-        print(json.dumps(res), flush=True)
-    if dist:
-        dist.barrier()
-        dist.destroy_process_group()
+        edges_in = mR / 2.0
+        teps = float(edges_in.sum()) * args.steps / bfs_wall
+        hmean = len(roots) / float(np.sum(bts.mean(axis=0) / edges_in))
+        upd = max(args.pr_iters - 1, 1)
+        # per-GPU algorithmic bytes over wall time (the exchange is inside the time)
+        bfs_bytes = (4.0 * mR.sum() + 4.0 * n * len(roots)) / world
+        roof_bfs = roofline("bfs_root per GPU (local kernels + RCCL exchange)", bfs_bytes * args.steps / bfs_wall / 1e9,
+                            "(4*m_R + 4*n)/N per root per GPU")
+        pr_bytes = (4.0 * e_in + 32.0 * n) / world
+        roof_pr = roofline("pagerank_update per GPU (gather + all-gather)", pr_bytes / (pr_wall / upd) / 1e9,
+                           "(4*m + 32*n)/N per update per GPU")
+        bfs_share = bfs_wall / (bfs_wall + pr_wall * args.steps)
+        print(json.dumps(result_line(args, world, scale, n, m, roots, elapsed, teps, hmean, pr_wall / upd, e_in,
+                                     roof_bfs, roof_pr, bfs_share, None, f"vertex-partition{world}")), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
 
 
 def cpu_baseline(n, src, dst, roots, mR, depth, threads):
@@ -199,13 +269,21 @@ def cpu_baseline(n, src, dst, roots, mR, depth, threads):
         # this is the smallest maxDepth that yields the full BFS result.
         d, it = g.shortest_distance(int((int(roots[0]) + 1) << 3), int(depth), 2, weighted=False, threads=threads)
         t = time.perf_counter() - t0
-        reached_entries = float(mR[0])
         del g
-        return {"value": round(reached_entries / 2.0 / t / 1e9, 6), "unit": "GTEPS", "cores": threads,
-                "kind": "port", "sample": f"1 of {len(roots)} roots (root 0), same RMAT graph, bothE, full depth "
-                                           f"({it} supersteps, {t:.1f}s; row decode/preload {load_s:.1f}s excluded)"}
+        return {"value": round(float(mR[0]) / 2.0 / t / 1e9, 6), "unit": "GTEPS", "cores": threads, "kind": "port",
+                "sample": f"1 of {len(roots)} roots (root 0), same RMAT graph, bothE, maxDepth {depth} "
+                          f"({it + 1} supersteps, {t:.1f}s; row decode/preload {load_s:.1f}s excluded)"}
     except Exception as e:  # noqa: BLE001
         return {"value": None, "unit": "GTEPS", "cores": threads, "kind": "port", "sample": f"failed: {e}"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        run_partitioned(args, world, int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0")))
+    else:
+        run_single(args)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,59 @@
+/*
+ * titan_gpu_olap_part.h — multi-GPU (1-D vertex-partitioned) extension of the C-ABI.
+ *
+ * The reference has no multi-process OLAP executor (Fulgora is single-JVM,
+ * FulgoraGraphComputer.java:117-311; cross-machine OLAP exists only as Hadoop scans,
+ * hadoop/scan/HadoopScanRunner.java:63-137).  Graphs that outgrow one GPU are split over
+ * the node's GPUs, one process per GPU: rank r owns global vertices [lo, hi) and holds
+ * their Titan rows (OUT + IN entries, global neighbour ids).  Each superstep is a
+ * local kernel plus one exchange, run by the caller with RCCL (torch.distributed, backend
+ * "nccl") on the ctx stream — so the exchange buffers are caller-owned DEVICE pointers:
+ *
+ *   BFS bottom-up level : all-gather of the owned next-frontier bitmap slices
+ *                         (nb_local, n_local/64 words each) into fb_global (n_global/64)
+ *   BFS top-down level  : all-to-all of the "discovered" bitmap (disc, n_global/64 words,
+ *                         slice r to rank r) into recv (nranks x n_local/64), then claim
+ *   PageRank iteration  : all-gather of the owned contributions (n_local doubles)
+ *   every level         : all-reduce(SUM) of the two frontier counters
+ * RCCL has no bitwise-OR reduction, hence slice exchanges instead of an all-reduce.
+ *
+ * Preconditions: n_local = hi - lo is a multiple of 64 (bitmap slices are whole words),
+ * tgo_options.stream is the stream the caller's collectives run on.
+ */
+#ifndef TITAN_GPU_OLAP_PART_H
+#define TITAN_GPU_OLAP_PART_H
+#include "titan_gpu_olap.h"
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Load the rows of global vertices [lo, hi) from an edge list (global ids) holding at
+ * least every edge with an endpoint in [lo, hi). */
+int tgo_load_partition(tgo_ctx* ctx, int64_t n_global, int64_t lo, int64_t hi,
+                       const tgo_edges* edges, const tgo_load_opts* opts);
+
+/* counts[0] = vertices put in this rank's next frontier, counts[1] = their list entries */
+int tgo_part_bfs_begin(tgo_ctx* ctx, int64_t seed_global, uint64_t* nb_local, int64_t* counts);
+int tgo_part_bfs_td(tgo_ctx* ctx, int32_t level, uint64_t* disc_global);
+int tgo_part_bfs_claim(tgo_ctx* ctx, int32_t level, const uint64_t* recv, int32_t nslices,
+                       uint64_t* nb_local, int64_t* counts);
+int tgo_part_bfs_bu(tgo_ctx* ctx, int32_t level, const uint64_t* fb_global, uint64_t* nb_local,
+                    int64_t* counts);
+/* Local distances (TGO_DIST_ABSENT = unreached) and reached[2] = {vertices, list entries}. */
+int tgo_part_bfs_end(tgo_ctx* ctx, int64_t* dist_local, int64_t* reached);
+
+int tgo_part_pr_begin(tgo_ctx* ctx, const tgo_pr_args* args, double* contrib_local);
+int tgo_part_pr_step(tgo_ctx* ctx, const double* contrib_global, double* contrib_local);
+int tgo_part_pr_end(tgo_ctx* ctx, double* pr_local);
+
+/* Bench / test input: the edges of an RMAT stream (tgo_synth.h) with an endpoint in
+ * [lo, hi).  *count = edges written; if capacity is too small, nothing is written,
+ * *count = required capacity and TGO_E_INVALID is returned. */
+int tgo_rmat_partition(int32_t scale, int32_t edge_factor, uint64_t seed, int64_t lo, int64_t hi,
+                       int32_t* src, int32_t* dst, int32_t* weight, int64_t capacity,
+                       int64_t* count, int32_t threads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,191 @@
+"""CPU, world_size 2 and 4 over gloo: the multi-GPU exchange protocol of
+titan_amd/distributed.py (partitioning, bitmap all-to-all / all-gather, count
+all-reduce, direction switching, PageRank contribution all-gather) against the oracle.
+
+The per-rank local steps are a numpy test double with the exact contract of the HIP
+backend (include/titan_gpu_olap_part.h); the GPU backend itself is exercised by
+tests/test_gpu_distributed.py on the device.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ABSENT = -(1 << 63)
+
+
+class NumpyPartBackend:
+    """Reference implementation of the per-rank local steps (test double)."""
+
+    def __init__(self, n_global, lo, hi, src, dst):
+        self.n_global, self.lo, self.hi = n_global, lo, hi
+        self.n_local = hi - lo
+        self.device = torch.device("cpu")
+        own_o = (src >= lo) & (src < hi)
+        own_i = (dst >= lo) & (dst < hi)
+        self.out = [[] for _ in range(self.n_local)]
+        self.inn = [[] for _ in range(self.n_local)]
+        for s, d in zip(src[own_o], dst[own_o]):
+            self.out[s - lo].append(int(d))
+        for s, d in zip(src[own_i], dst[own_i]):
+            self.inn[d - lo].append(int(s))
+        self.total_entries = sum(map(len, self.out)) + sum(map(len, self.inn))
+
+    def tensor(self, n, dtype):
+        return torch.zeros(n, dtype=dtype)
+
+    @staticmethod
+    def _u(t):
+        return t.numpy().view(np.uint64)
+
+    def _deg(self, v):
+        return len(self.out[v]) + len(self.inn[v])
+
+    def bfs_begin(self, seed, nb_local):
+        self.level = np.full(self.n_local, -1, np.int64)
+        self.vis = np.zeros(self.n_local, bool)
+        nb = self._u(nb_local)
+        nb[:] = 0
+        self.queue = []
+        if self.lo <= seed < self.hi:
+            v = seed - self.lo
+            self.level[v] = 0
+            self.vis[v] = True
+            nb[v >> 6] |= np.uint64(1 << (v & 63))
+            self.queue = [v]
+            return np.array([1, self._deg(v)])
+        return np.array([0, 0])
+
+    def bfs_td(self, level, disc):
+        d = self._u(disc)
+        for u in self.queue:
+            for w in self.out[u] + self.inn[u]:
+                if self.lo <= w < self.hi and self.vis[w - self.lo]:
+                    continue
+                d[w >> 6] |= np.uint64(1 << (w & 63))
+
+    def _finish(self, level, fresh, nb_local):
+        nb = self._u(nb_local)
+        nb[:] = 0
+        self.queue = []
+        ent = 0
+        for v in fresh:
+            self.level[v] = level + 1
+            self.vis[v] = True
+            nb[v >> 6] |= np.uint64(1 << (v & 63))
+            self.queue.append(v)
+            ent += self._deg(v)
+        return np.array([len(fresh), ent])
+
+    def bfs_claim(self, level, recv, nslices, nb_local):
+        r = self._u(recv).reshape(nslices, -1)
+        bits = np.bitwise_or.reduce(r, axis=0)
+        fresh = [v for v in range(self.n_local) if (int(bits[v >> 6]) >> (v & 63)) & 1 and not self.vis[v]]
+        return self._finish(level, fresh, nb_local)
+
+    def bfs_bu(self, level, fb_global, nb_local):
+        fb = self._u(fb_global)
+        fresh = []
+        for v in range(self.n_local):
+            if self.vis[v]:
+                continue
+            if any((int(fb[w >> 6]) >> (w & 63)) & 1 for w in self.out[v] + self.inn[v]):
+                fresh.append(v)
+        return self._finish(level, fresh, nb_local)
+
+    def bfs_end(self, fetch=True, stats=True):
+        d = np.where(self.level >= 0, self.level, ABSENT)
+        reached = np.array([int((self.level >= 0).sum()), sum(self._deg(v) for v in range(self.n_local) if self.level[v] >= 0)])
+        return d, reached
+
+    def pr_begin(self, alpha, N, iters, contrib_local):
+        self.alpha, self.base = alpha, (1 - alpha) / N
+        self.ec = np.array([float(len(o)) for o in self.out])
+        self.pr = np.full(self.n_local, 1.0 / N)
+        with np.errstate(divide="ignore"):
+            contrib_local.numpy()[:] = (1.0 / N) / self.ec
+
+    def pr_step(self, contrib_global, contrib_local):
+        cg = contrib_global.numpy()
+        s = np.array([cg[self.inn[v]].sum() if self.inn[v] else 0.0 for v in range(self.n_local)])
+        self.pr = self.alpha * s + self.base
+        with np.errstate(divide="ignore"):
+            contrib_local.numpy()[:] = self.pr / self.ec
+
+    def pr_end(self, fetch=True):
+        return self.pr
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, scale, roots, out_q, alpha):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from titan_amd import rmat_edges
+    from titan_amd.distributed import distributed_bfs, distributed_pagerank, partition_range
+    n = 1 << scale
+    src, dst, _ = rmat_edges(scale, 8, seed=21)
+    lo, hi = partition_range(n, world, rank)
+    be = NumpyPartBackend(n, lo, hi, src, dst)
+    res = {"bfs": [], "reached": []}
+    for r in roots:
+        d, reached, levels = distributed_bfs(be, int(r), n, alpha=alpha)
+        full = [torch.zeros(be.n_local, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(full, torch.from_numpy(d.astype(np.int64)))
+        res["bfs"].append(torch.cat(full).numpy())
+        res["reached"].append(reached)
+    pr = distributed_pagerank(be, 0.85, n, 10)
+    full = [torch.zeros(be.n_local, dtype=torch.float64) for _ in range(world)]
+    dist.all_gather(full, torch.from_numpy(pr))
+    res["pr"] = torch.cat(full).numpy()
+    if rank == 0:
+        out_q.put(res)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,alpha", [(2, 15.0), (2, 1e9), (4, 15.0)])
+def test_distributed_bfs_and_pagerank_match_oracle(world, alpha):
+    import fulgora as fr
+    from titan_amd import rmat_edges
+    scale = 9
+    n = 1 << scale
+    src, dst, _ = rmat_edges(scale, 8, seed=21)
+    roots = [int(src[0]), int(dst[5]), int(src[77])]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, scale, roots, q, alpha)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    og = fr.OracleGraph.from_edges(n, src, dst)
+    ids = (np.arange(n, dtype=np.int64) + 1) << 3
+    for r, d, reached in zip(roots, res["bfs"], res["reached"]):
+        od, _ = og.shortest_distance(int(ids[r]), n, 2)
+        assert np.array_equal(d, od)
+        assert reached[0] == int((od != ABSENT).sum())
+    opr, _ = og.pagerank(0.85, n, 10)
+    fin = np.isfinite(opr)
+    assert np.array_equal(np.isfinite(res["pr"]), fin)
+    assert np.abs(res["pr"][fin] - opr[fin]).sum() <= 1e-6
+
+
+def test_partition_range_is_word_aligned():
+    from titan_amd.distributed import partition_range
+    assert partition_range(1 << 10, 4, 3) == (768, 1024)
+    with pytest.raises(ValueError):
+        partition_range(1000, 4, 0)

@@ -1,0 +1,106 @@
+"""GPU: the partitioned (multi-GPU) local steps of the HIP engine, driven by the same
+exchange driver as the real multi-GPU run.  The 1-GPU box has one device, so the ranks
+are simulated in ONE process: every "rank" is an Engine holding its partition, and a
+tiny in-process communicator performs the all-to-all / all-gather / all-reduce with
+torch ops on the device.  Results must equal the oracle bit-for-bit (BFS) / 1e-6 L1 (PR).
+"""
+import numpy as np
+import pytest
+import torch
+
+import fulgora as fr
+from titan_amd import Engine, rmat_edges
+from titan_amd import _lib as L
+from titan_amd.distributed import HipPartBackend, partition_range
+
+pytestmark = pytest.mark.gpu
+ABSENT = L.DIST_ABSENT
+
+
+def run_bfs(backends, seed, max_depth, alpha=15.0, beta=18.0):
+    """The distributed_bfs protocol with the collectives done in-process."""
+    world = len(backends)
+    n = backends[0].n_global
+    nwl = backends[0].n_local // 64
+    dev = backends[0].device
+    fb = [b.tensor(n // 64, torch.int64) for b in backends]
+    nb = [b.tensor(nwl, torch.int64) for b in backends]
+    disc = [b.tensor(n // 64, torch.int64) for b in backends]
+    recv = [b.tensor(n // 64, torch.int64) for b in backends]
+
+    def allgather():
+        g = torch.cat(nb)
+        for t in fb:
+            t.copy_(g)
+
+    total = sum(b.total_entries for b in backends)
+    c = sum(b.bfs_begin(seed, nb[i]) for i, b in enumerate(backends))
+    allgather()
+    nf, mf = c
+    mu = total - mf
+    bottom_up = False
+    for level in range(max_depth):
+        if nf == 0:
+            break
+        if not bottom_up and mf > mu / alpha:
+            bottom_up = True
+        elif bottom_up and nf < n / beta:
+            bottom_up = False
+        cs = []
+        if bottom_up:
+            for i, b in enumerate(backends):
+                cs.append(b.bfs_bu(level, fb[i], nb[i]))
+        else:
+            for i, b in enumerate(backends):
+                disc[i].zero_()
+                b.bfs_td(level, disc[i])
+            torch.cuda.synchronize()
+            for r in range(world):          # all_to_all_single: slice r of every sender -> rank r
+                recv[r].copy_(torch.cat([disc[s][r * nwl:(r + 1) * nwl] for s in range(world)]))
+            for i, b in enumerate(backends):
+                cs.append(b.bfs_claim(level, recv[i], world, nb[i]))
+        allgather()
+        nf, mf = sum(cs)
+        mu -= mf
+    outs = [b.bfs_end(True) for b in backends]
+    return np.concatenate([o[0] for o in outs]), sum(o[1] for o in outs)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_partitioned_bfs_and_pagerank(world):
+    scale = 12
+    n = 1 << scale
+    src, dst, _ = rmat_edges(scale, 16, seed=31)
+    backends = []
+    for r in range(world):
+        lo, hi = partition_range(n, world, r)
+        eng = Engine(stream=torch.cuda.current_stream().cuda_stream).load_partition(n, lo, hi, src, dst, L.SCOPE_BOTH_E,
+                                                                                    apply_cap=False)
+        backends.append(HipPartBackend(eng, n, lo, hi))
+    og = fr.OracleGraph.from_edges(n, src, dst)
+    ids = (np.arange(n, dtype=np.int64) + 1) << 3
+    for seed in (int(src[0]), int(dst[9]), int(src[100])):
+        for alpha in (15.0, 1e9):
+            d, reached = run_bfs(backends, seed, n, alpha=alpha)
+            od, _ = og.shortest_distance(int(ids[seed]), n, 2)
+            assert np.array_equal(d, od)
+            assert reached[0] == int((od != ABSENT).sum())
+    # PageRank: in-process all-gather of the contributions
+    iters = 10
+    cl = [b.tensor(b.n_local, torch.float64) for b in backends]
+    cg = [b.tensor(n, torch.float64) for b in backends]
+    for b, c in zip(backends, cl):
+        b.pr_begin(0.85, n, iters, c)
+    for _ in range(2, iters + 1):
+        torch.cuda.synchronize()
+        g = torch.cat(cl)
+        for t in cg:
+            t.copy_(g)
+        torch.cuda.synchronize()
+        for b, c, gg in zip(backends, cl, cg):
+            b.pr_step(gg, c)
+    pr = np.concatenate([b.pr_end(True) for b in backends])
+    opr, _ = og.pagerank(0.85, n, iters)
+    fin = np.isfinite(opr)
+    assert np.array_equal(np.isfinite(pr), fin)
+    assert np.abs(pr[fin] - opr[fin]).sum() <= 1e-6

@@ -99,6 +99,9 @@ EXPORTS = [
     "tgo_finish_load", "tgo_load_edges", "tgo_num_vertices", "tgo_vertex_ids", "tgo_bfs",
     "tgo_sssp", "tgo_copy_distances", "tgo_pagerank", "tgo_walkcount", "tgo_stats_get", "tgo_sync",
     "tgo_rmat_edges", "tgo_pick_roots",
+    # titan_gpu_olap_part.h (1-D vertex-partitioned multi-GPU)
+    "tgo_load_partition", "tgo_part_bfs_begin", "tgo_part_bfs_td", "tgo_part_bfs_claim", "tgo_part_bfs_bu",
+    "tgo_part_bfs_end", "tgo_part_pr_begin", "tgo_part_pr_step", "tgo_part_pr_end", "tgo_rmat_partition",
 ]
 
 _lib = None
@@ -141,6 +144,17 @@ def load() -> C.CDLL:
         "tgo_rmat_edges": (C.c_int, [C.c_int32, C.c_int32, C.c_uint64, C.c_int64, C.c_int64,
                                      _i32p, _i32p, _i32p, C.c_int32]),
         "tgo_pick_roots": (C.c_int, [C.c_int64, C.c_int64, _i32p, _i32p, C.c_uint64, C.c_int32, _i64p]),
+        "tgo_load_partition": (C.c_int, [vp, C.c_int64, C.c_int64, C.c_int64, P(Edges), P(LoadOpts)]),
+        "tgo_part_bfs_begin": (C.c_int, [vp, C.c_int64, vp, _i64p]),
+        "tgo_part_bfs_td": (C.c_int, [vp, C.c_int32, vp]),
+        "tgo_part_bfs_claim": (C.c_int, [vp, C.c_int32, vp, C.c_int32, vp, _i64p]),
+        "tgo_part_bfs_bu": (C.c_int, [vp, C.c_int32, vp, vp, _i64p]),
+        "tgo_part_bfs_end": (C.c_int, [vp, _i64p, _i64p]),
+        "tgo_part_pr_begin": (C.c_int, [vp, P(PrArgs), vp]),
+        "tgo_part_pr_step": (C.c_int, [vp, vp, vp]),
+        "tgo_part_pr_end": (C.c_int, [vp, C.POINTER(C.c_double)]),
+        "tgo_rmat_partition": (C.c_int, [C.c_int32, C.c_int32, C.c_uint64, C.c_int64, C.c_int64, _i32p, _i32p,
+                                         _i32p, C.c_int64, _i64p, C.c_int32]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

@@ -7,12 +7,15 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <thread>
 #include <unordered_map>
 #include <hip/hip_runtime_api.h>
 #include "engine.hpp"
+#include "../../include/titan_gpu_olap_part.h"
 
 using namespace tgo;
 
@@ -32,9 +35,18 @@ struct tgo_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     int64_t dev_bytes = 0;
     std::vector<void*> allocs;
+    int part_cur = 0;           // partitioned BFS: queue buffer holding the frontier
+    int64_t part_qlen = 0;      // its length
+    double part_alpha = 0.85, part_base = 0.0;
+    int32_t part_pr_iter = 0;
 };
 
 namespace {
+
+double env_double(const char* name, double dflt) {
+    const char* v = std::getenv(name);
+    return v ? std::atof(v) : dflt;
+}
 
 int fail(tgo_ctx* c, int code, const std::string& msg) {
     if (c) c->err = msg;
@@ -89,6 +101,9 @@ int upload_graph(tgo_ctx* ctx, HostGraph& h) {
     g.scope = h.scope;
     g.has_weight = h.has_weight;
     g.has_transpose = h.has_transpose;
+    g.n_active = 0;
+    for (int64_t v = h.n - 1; v >= 0; --v)
+        if (h.out.off[v + 1] > h.out.off[v] || h.in.off[v + 1] > h.in.off[v]) { g.n_active = v + 1; break; }
     g.min_weight = 0;
     for (const HostCsr* c : {&h.out, &h.in})
         for (int32_t x : c->w) if (x != kMissingWeight) g.min_weight = std::min(g.min_weight, x);
@@ -233,7 +248,10 @@ int run_bfs(tgo_ctx* ctx, int64_t seed, int max_depth, int scope) {
         int64_t qlen = 1;
         int cur = 0;
         bool bottom_up = false;
-        const double alpha = 15.0, beta = 18.0;
+        // Beamer's switch thresholds; TGO_BFS_ALPHA / TGO_BFS_BETA override for tuning.
+        static const double alpha = env_double("TGO_BFS_ALPHA", 15.0);
+        static const double beta = env_double("TGO_BFS_BETA", 18.0);
+        static const bool trace = env_double("TGO_TRACE", 0.0) != 0.0;
         // m_u: entries of unexplored vertices (push degrees); m_f: of the frontier.
         const int64_t total_push = push.nlists > 1 ? (g.out.nnz + g.in.nnz)
                                                    : (g.has_transpose ? g.push_t.nnz
@@ -252,7 +270,8 @@ int run_bfs(tgo_ctx* ctx, int64_t seed, int max_depth, int scope) {
             HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
             HIP_TRY(hipMemsetAsync(s.nb, 0, words * 8, st));
             if (bottom_up) {
-                HIP_TRY(k_bu_step(pull, push, n, s.fb, s.vb, s.nb, s.level, s.q[cur ^ 1], s.qdeg, s.cnt, L + 1, st));
+                // words past n_active hold only entry-less vertices: nothing to find there
+                HIP_TRY(k_bu_step(pull, push, g.n_active, s.fb, s.vb, s.nb, s.level, s.q[cur ^ 1], s.qdeg, s.cnt, L + 1, st));
             } else {
                 int rc = scan_frontier(ctx, qlen);
                 if (rc) return rc;
@@ -264,6 +283,8 @@ int run_bfs(tgo_ctx* ctx, int64_t seed, int max_depth, int scope) {
             qlen = static_cast<int64_t>(s.hcnt->qlen);
             mf = static_cast<int64_t>(s.hcnt->mf);
             mu -= mf;
+            if (trace) std::fprintf(stderr, "[tgo] level %d %s -> next frontier %lld vertices, %lld entries (unexplored %lld)\n",
+                                    L, bottom_up ? "BU" : "TD", (long long)qlen, (long long)mf, (long long)mu);
             std::swap(s.fb, s.nb);
             cur ^= 1;
             ++levels;
@@ -571,6 +592,187 @@ int tgo_walkcount(tgo_ctx* ctx, int32_t k, int32_t* out) {
         HIP_TRY(hipMemcpyAsync(out, s.level, n * sizeof(int32_t), hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
     }
+    return TGO_OK;
+}
+
+// ------------------------------------------------------------------ 1-D partitioned (multi-GPU)
+int tgo_load_partition(tgo_ctx* ctx, int64_t n_global, int64_t lo, int64_t hi, const tgo_edges* edges,
+                       const tgo_load_opts* opts) {
+    if (!ctx) return TGO_E_INVALID;
+    if (!edges || !opts || (edges->m > 0 && (!edges->src || !edges->dst))) return fail(ctx, TGO_E_INVALID, "null argument");
+    if ((hi - lo) % 64 != 0) return fail(ctx, TGO_E_INVALID, "partition size must be a multiple of 64");
+    (void)hipSetDevice(ctx->opts.device);
+    const auto t0 = std::chrono::steady_clock::now();
+    HostGraph h;
+    std::string err;
+    int rc = assemble_partition(edges, n_global, lo, hi, opts, ctx->opts.hard_query_limit, h, threads_of(ctx), err);
+    if (rc) return fail(ctx, rc, err);
+    free_graph(ctx);
+    ctx->staging = RowStaging();
+    rc = upload_graph(ctx, h);
+    if (rc) return rc;
+    ctx->g.partitioned = true;
+    ctx->g.lo = lo;
+    ctx->g.n_global = n_global;
+    ctx->st.load_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return TGO_OK;
+}
+
+static int part_check(tgo_ctx* ctx) {
+    if (!ctx) return TGO_E_INVALID;
+    if (!ctx->loaded || !ctx->g.partitioned) return fail(ctx, TGO_E_STATE, "no partitioned graph loaded");
+    (void)hipSetDevice(ctx->opts.device);
+    return TGO_OK;
+}
+
+static int part_counts(tgo_ctx* ctx, int64_t* counts) {
+    int rc = read_counters(ctx);
+    if (rc) return rc;
+    ctx->part_qlen = static_cast<int64_t>(ctx->sc.hcnt->qlen);
+    if (counts) {
+        counts[0] = ctx->part_qlen;
+        counts[1] = static_cast<int64_t>(ctx->sc.hcnt->mf);
+    }
+    return TGO_OK;
+}
+
+int tgo_part_bfs_begin(tgo_ctx* ctx, int64_t seed_global, uint64_t* nb_local, int64_t* counts) {
+    int rc = part_check(ctx);
+    if (rc) return rc;
+    if (ctx->g.scope != TGO_SCOPE_BOTH_E) return fail(ctx, TGO_E_UNSUPPORTED, "partitioned BFS runs over bothE");
+    DevGraph& g = ctx->g;
+    Scratch& s = ctx->sc;
+    hipStream_t st = ctx->stream;
+    const int64_t n = g.n, words = n / 64;
+    const View push = push_view(g, TGO_SCOPE_BOTH_E);
+    HIP_TRY(hipEventRecord(ctx->ev0, st));
+    HIP_TRY(k_fill_i32(s.level, -1, n, st));
+    HIP_TRY(hipMemsetAsync(s.vb, 0, (words + 1) * 8, st));
+    HIP_TRY(hipMemsetAsync(nb_local, 0, words * 8, st));
+    HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
+    ctx->part_cur = 0;
+    ctx->part_qlen = 0;
+    int64_t deg = 0;
+    const int64_t seed = seed_global - g.lo;
+    if (seed >= 0 && seed < n) {
+        // the owner seeds: level 0, visited, in the frontier bitmap slice and the queue
+        HIP_TRY(k_bfs_seed(push, s.level, s.vb, nb_local, s.q[0], s.qdeg, seed, st));
+        HIP_TRY(hipMemcpyAsync(&deg, s.qdeg, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+        ctx->part_qlen = 1;
+    }
+    HIP_TRY(hipStreamSynchronize(st));
+    if (counts) { counts[0] = ctx->part_qlen; counts[1] = deg; }
+    return TGO_OK;
+}
+
+int tgo_part_bfs_td(tgo_ctx* ctx, int32_t level, uint64_t* disc_global) {
+    int rc = part_check(ctx);
+    if (rc) return rc;
+    (void)level;
+    DevGraph& g = ctx->g;
+    Scratch& s = ctx->sc;
+    hipStream_t st = ctx->stream;
+    const View push = push_view(g, TGO_SCOPE_BOTH_E);
+    if (ctx->part_qlen > 0) {
+        if ((rc = scan_frontier(ctx, ctx->part_qlen))) return rc;
+        HIP_TRY(k_part_td_mark(push, s.q[ctx->part_cur], s.qpre, ctx->part_qlen, disc_global, s.vb, g.lo, g.n, st));
+    }
+    return TGO_OK;
+}
+
+int tgo_part_bfs_claim(tgo_ctx* ctx, int32_t level, const uint64_t* recv, int32_t nslices,
+                       uint64_t* nb_local, int64_t* counts) {
+    int rc = part_check(ctx);
+    if (rc) return rc;
+    DevGraph& g = ctx->g;
+    Scratch& s = ctx->sc;
+    hipStream_t st = ctx->stream;
+    const View push = push_view(g, TGO_SCOPE_BOTH_E);
+    HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
+    const int nxt = ctx->part_cur ^ 1;
+    HIP_TRY(k_part_claim(push, recv, nslices, g.n / 64, g.n, s.vb, nb_local, s.level, s.q[nxt], s.qdeg, s.cnt,
+                         level + 1, st));
+    ctx->part_cur = nxt;
+    return part_counts(ctx, counts);
+}
+
+int tgo_part_bfs_bu(tgo_ctx* ctx, int32_t level, const uint64_t* fb_global, uint64_t* nb_local, int64_t* counts) {
+    int rc = part_check(ctx);
+    if (rc) return rc;
+    DevGraph& g = ctx->g;
+    Scratch& s = ctx->sc;
+    hipStream_t st = ctx->stream;
+    const View pull = pull_view(g, TGO_SCOPE_BOTH_E), push = push_view(g, TGO_SCOPE_BOTH_E);
+    HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
+    HIP_TRY(hipMemsetAsync(nb_local, 0, (g.n / 64) * 8, st));
+    const int nxt = ctx->part_cur ^ 1;
+    HIP_TRY(k_bu_step(pull, push, g.n_active, fb_global, s.vb, nb_local, s.level, s.q[nxt], s.qdeg, s.cnt, level + 1, st));
+    ctx->part_cur = nxt;
+    return part_counts(ctx, counts);
+}
+
+int tgo_part_bfs_end(tgo_ctx* ctx, int64_t* dist_local, int64_t* reached) {
+    int rc = part_check(ctx);
+    if (rc) return rc;
+    DevGraph& g = ctx->g;
+    Scratch& s = ctx->sc;
+    hipStream_t st = ctx->stream;
+    HIP_TRY(k_level_to_dist(s.level, s.dist, g.n, st));
+    HIP_TRY(hipEventRecord(ctx->ev1, st));
+    if (reached) {
+        HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
+        HIP_TRY(k_reach_stats(pull_view(g, TGO_SCOPE_BOTH_E), s.dist, g.n, s.cnt->red, st));
+        if ((rc = read_counters(ctx))) return rc;
+        reached[0] = static_cast<int64_t>(s.hcnt->red[0]);
+        reached[1] = static_cast<int64_t>(s.hcnt->red[1]);
+    }
+    if (dist_local) {
+        HIP_TRY(hipMemcpyAsync(dist_local, s.dist, g.n * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    }
+    HIP_TRY(hipStreamSynchronize(st));
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+    ctx->st.last_kernel_ms = ms;
+    return TGO_OK;
+}
+
+int tgo_part_pr_begin(tgo_ctx* ctx, const tgo_pr_args* a, double* contrib_local) {
+    int rc = part_check(ctx);
+    if (rc) return rc;
+    if (!a || a->max_iterations < 1) return fail(ctx, TGO_E_INVALID, "partitioned PageRank needs max_iterations >= 1");
+    DevGraph& g = ctx->g;
+    Scratch& s = ctx->sc;
+    const double N = static_cast<double>(a->vertex_count);
+    ctx->part_alpha = a->alpha;
+    ctx->part_base = (1.0 - a->alpha) / N;
+    HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
+    // iteration 1 (PageRankVertexProgram.java:78-83) on the owned rows
+    HIP_TRY(k_pr_init(g.out, s.vec[0], contrib_local, reinterpret_cast<double*>(s.dist), 1.0 / N, g.n, ctx->stream));
+    return TGO_OK;
+}
+
+int tgo_part_pr_step(tgo_ctx* ctx, const double* contrib_global, double* contrib_local) {
+    int rc = part_check(ctx);
+    if (rc) return rc;
+    DevGraph& g = ctx->g;
+    Scratch& s = ctx->sc;
+    // owned rows gather over their IN lists (global source ids) from the gathered vector
+    HIP_TRY(k_pr_iter(g.in, g.rb_in, contrib_global, s.vec[0], reinterpret_cast<double*>(s.dist), contrib_local,
+                      s.partial, ctx->part_alpha, ctx->part_base, g.n, ctx->stream));
+    return TGO_OK;
+}
+
+int tgo_part_pr_end(tgo_ctx* ctx, double* pr_local) {
+    int rc = part_check(ctx);
+    if (rc) return rc;
+    DevGraph& g = ctx->g;
+    Scratch& s = ctx->sc;
+    HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
+    if (pr_local) HIP_TRY(hipMemcpyAsync(pr_local, s.dist, g.n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+    ctx->st.last_kernel_ms = ms;
     return TGO_OK;
 }
 

@@ -181,13 +181,20 @@ __global__ void __launch_bounds__(kBlock) bu_step(View pull, View push, int64_t 
         const int64_t deg = (e0 - b0) + (e1 - b1);
         // short lists: the lane scans its own list and stops at the first frontier hit
         if (open && deg <= kSerialScan) {
-            for (int64_t k = b0; k < e0 && !found; ++k) {
-                const int32_t u = pull.adj0[k];
-                found = (fb[u >> 6] >> (u & 63)) & 1ULL;
-            }
-            for (int64_t k = b1; k < e1 && !found; ++k) {
-                const int32_t u = pull.adj1[k];
-                found = (fb[u >> 6] >> (u & 63)) & 1ULL;
+            // 4 entries per step: their index loads and bitmap probes issue together, so a
+            // lane pays one dependent round trip per 4 entries instead of per entry.
+            for (int l = 0; l < 2 && !found; ++l) {
+                const int32_t* adj = l == 0 ? pull.adj0 : pull.adj1;
+                const int64_t e = l == 0 ? e0 : e1;
+                for (int64_t k = l == 0 ? b0 : b1; k < e && !found; k += 4) {
+                    int32_t u[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) u[j] = k + j < e ? adj[k + j] : -1;
+                    uint64_t f[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) f[j] = u[j] >= 0 ? fb[u[j] >> 6] >> (u[j] & 63) : 0;
+                    found = ((f[0] | f[1] | f[2] | f[3]) & 1ULL) != 0;
+                }
             }
         }
         // long lists: the whole wave scans one list 64 entries at a time (ballot exit)
@@ -337,6 +344,87 @@ __global__ void dist_finalize(int64_t* dist, int64_t n) {
         if (dist[i] == INT64_MAX) dist[i] = INT64_MIN;
 }
 
+// ---------------------------------------------------------------- 1-D partitioned BFS
+// Top-down on a partition: every entry of the local frontier marks its (global) neighbour
+// in a global "discovered" bitmap; the owners claim them after the all-to-all of slices.
+__global__ void __launch_bounds__(kBlock) part_td_mark(View push, const int32_t* __restrict__ q,
+        const int64_t* __restrict__ qpre, int64_t qlen, uint64_t* __restrict__ disc,
+        const uint64_t* __restrict__ vb_local, int64_t lo, int64_t n_local) {
+    __shared__ int64_t s_pre[kLdsEntries];
+    __shared__ int32_t s_q[kLdsEntries];
+    __shared__ int64_t s_lo, s_hi;
+    const int64_t total = qpre[qlen];
+    const int64_t ntiles = (total + kTileEdges - 1) / kTileEdges;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t t0 = tile * kTileEdges;
+        const int64_t t1 = min(total, t0 + kTileEdges);
+        if (threadIdx.x == 0) {
+            int64_t a = 0, b = qlen;
+            while (b - a > 1) { const int64_t c = (a + b) >> 1; if (qpre[c] <= t0) a = c; else b = c; }
+            s_lo = a;
+            int64_t a2 = a, b2 = qlen;
+            while (b2 - a2 > 1) { const int64_t c = (a2 + b2) >> 1; if (qpre[c] <= t1 - 1) a2 = c; else b2 = c; }
+            s_hi = a2;
+        }
+        __syncthreads();
+        const int64_t lo_q = s_lo, hi_q = s_hi;
+        const int64_t span = hi_q - lo_q + 1;
+        const bool in_lds = span + 1 <= kLdsEntries;
+        if (in_lds) {
+            for (int64_t i = threadIdx.x; i <= span; i += kBlock) {
+                s_pre[i] = qpre[lo_q + i];
+                if (i < span) s_q[i] = q[lo_q + i];
+            }
+        }
+        __syncthreads();
+        for (int k = 0; k < kEdgesPerThread; ++k) {
+            const int64_t j = t0 + k * kBlock + threadIdx.x;
+            if (j >= t1) break;
+            int32_t u; int64_t start;
+            if (in_lds) {
+                int64_t a = 0, b = span;
+                while (b - a > 1) { const int64_t c = (a + b) >> 1; if (s_pre[c] <= j) a = c; else b = c; }
+                u = s_q[a]; start = s_pre[a];
+            } else {
+                int64_t a = lo_q, b = hi_q + 1;
+                while (b - a > 1) { const int64_t c = (a + b) >> 1; if (qpre[c] <= j) a = c; else b = c; }
+                u = q[a]; start = qpre[a];
+            }
+            int32_t v, w;
+            entry_at(push, u, j - start, v, w);
+            const uint64_t bit = 1ULL << (v & 63);
+            const int64_t vl = static_cast<int64_t>(v) - lo;
+            if (vl >= 0 && vl < n_local && (vb_local[vl >> 6] & (1ULL << (vl & 63)))) continue;   // owned & visited
+            if (!(disc[v >> 6] & bit)) atomicOr(reinterpret_cast<unsigned long long*>(&disc[v >> 6]), bit);
+        }
+        __syncthreads();
+    }
+}
+
+// Owner side: OR the received slices, claim the unvisited bits (one wave per word).
+__global__ void __launch_bounds__(kBlock) part_claim(View push, const uint64_t* __restrict__ recv,
+        int nslices, int64_t words, int64_t n_local, uint64_t* __restrict__ vb, uint64_t* __restrict__ nb,
+        int32_t* __restrict__ level, int32_t* __restrict__ qn, int64_t* __restrict__ qdeg_n, Counters* cnt,
+        int32_t next_level) {
+    const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t wd = wave; wd < words; wd += nwaves) {
+        uint64_t bits = 0;
+        for (int s = 0; s < nslices; ++s) bits |= recv[static_cast<int64_t>(s) * words + wd];
+        const uint64_t vis = vb[wd];
+        const uint64_t fresh = bits & ~vis;
+        const int64_t v = (wd << 6) + lane();
+        const bool take = v < n_local && ((fresh >> lane()) & 1ULL);
+        const unsigned long long tm = __ballot(take);
+        if (lane() == 0) {
+            nb[wd] = tm;
+            if (tm) vb[wd] = vis | tm;
+        }
+        if (take) level[v] = next_level;
+        wave_append(take, static_cast<int32_t>(v), take ? push_degree(push, v) : 0, qn, qdeg_n, cnt);
+    }
+}
+
 // out[v] = in[perm[v]]: internal (degree-grouped) order -> the API's row order.
 template <class T>
 __global__ void gather_perm(const T* __restrict__ in, const int32_t* __restrict__ perm, T* __restrict__ out, int64_t n) {
@@ -376,8 +464,10 @@ hipError_t k_td_expand(const View& push, const int32_t* q, const int64_t* qpre, 
 hipError_t k_bu_step(const View& pull, const View& push, int64_t n, const uint64_t* fb, uint64_t* vb,
                      uint64_t* nb, int32_t* level, int32_t* qn, int64_t* qdeg_n, Counters* cnt,
                      int32_t next_level, hipStream_t s) {
+    // one wave per bitmap word, all launched at once: the dispatcher keeps every CU full
+    // and a wave's dependent probe chain overlaps with hundreds of others.
     const int64_t words = (n + 63) / 64;
-    bu_step<<<grid_for(words * 64, kBlock, 256 * 16), kBlock, 0, s>>>(pull, push, n, fb, vb, nb, level, qn, qdeg_n, cnt, next_level);
+    bu_step<<<grid_for(words * 64, kBlock, 1 << 20), kBlock, 0, s>>>(pull, push, n, fb, vb, nb, level, qn, qdeg_n, cnt, next_level);
     return hipGetLastError();
 }
 hipError_t k_level_to_dist(const int32_t* level, int64_t* dist, int64_t n, hipStream_t s) {
@@ -407,6 +497,18 @@ hipError_t k_sssp_commit(const int32_t* q, int64_t qlen, const int64_t* dist, in
                          uint64_t* mark, hipStream_t s) {
     (void)mark;
     sssp_commit<<<grid_for(qlen), kBlock, 0, s>>>(q, qlen, dist, msg);
+    return hipGetLastError();
+}
+hipError_t k_part_td_mark(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen,
+                          uint64_t* disc, const uint64_t* vb_local, int64_t lo, int64_t n_local, hipStream_t s) {
+    part_td_mark<<<256 * 8, kBlock, 0, s>>>(push, q, qpre, qlen, disc, vb_local, lo, n_local);
+    return hipGetLastError();
+}
+hipError_t k_part_claim(const View& push, const uint64_t* recv, int nslices, int64_t words, int64_t n_local,
+                        uint64_t* vb, uint64_t* nb, int32_t* level, int32_t* qn, int64_t* qdeg_n,
+                        Counters* cnt, int32_t next_level, hipStream_t s) {
+    part_claim<<<grid_for(words * 64, kBlock, 1 << 20), kBlock, 0, s>>>(push, recv, nslices, words, n_local, vb, nb,
+                                                                      level, qn, qdeg_n, cnt, next_level);
     return hipGetLastError();
 }
 hipError_t k_unpermute_i64(const int64_t* in, const int32_t* perm, int64_t* out, int64_t n, hipStream_t s) {

@@ -62,6 +62,9 @@ int decode_rows(RowStaging& st, const tgo_rows* rows, const tgo_schema* schema,
 int assemble_from_rows(RowStaging& st, HostGraph& g, int threads, std::string& err);
 int assemble_from_edges(const tgo_edges* e, const tgo_load_opts* opts, int64_t hard_limit,
                         HostGraph& g, int threads, std::string& err);
+int assemble_partition(const tgo_edges* e, int64_t n_global, int64_t lo, int64_t hi,
+                       const tgo_load_opts* opts, int64_t hard_limit, HostGraph& g, int threads,
+                       std::string& err);
 
 // ---------------------------------------------------------------- device graph
 struct DevCsr {
@@ -95,11 +98,14 @@ struct RowBlocks {
 struct DevGraph {
     int64_t n = 0;
     int32_t* perm = nullptr;    // row-order dense id -> internal id (device)
+    int64_t n_active = 0;       // internal ids >= n_active have no entries (never reachable)
     DevCsr out, in, push_t;
     bool has_transpose = false;
     bool has_weight = false;
     int32_t min_weight = 0;
     int32_t scope = TGO_SCOPE_BOTH_E;
+    bool partitioned = false;   // 1-D vertex partition: rows [lo, lo+n) of an n_global graph
+    int64_t lo = 0, n_global = 0;
     RowBlocks rb_out, rb_in;    // CSR-adaptive blocks per pull list
     bool rb_out_ready = false, rb_in_ready = false;
 };
@@ -162,6 +168,11 @@ hipError_t k_sssp_commit(const int32_t* q, int64_t qlen, const int64_t* dist, in
                          uint64_t* mark, hipStream_t s);
 hipError_t k_dist_finalize(int64_t* dist, int64_t n, hipStream_t s);
 hipError_t k_unpermute_i64(const int64_t* in, const int32_t* perm, int64_t* out, int64_t n, hipStream_t s);
+hipError_t k_part_td_mark(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen,
+                          uint64_t* disc, const uint64_t* vb_local, int64_t lo, int64_t n_local, hipStream_t s);
+hipError_t k_part_claim(const View& push, const uint64_t* recv, int nslices, int64_t words, int64_t n_local,
+                        uint64_t* vb, uint64_t* nb, int32_t* level, int32_t* qn, int64_t* qdeg_n,
+                        Counters* cnt, int32_t next_level, hipStream_t s);
 hipError_t k_unpermute_i32(const int32_t* in, const int32_t* perm, int32_t* out, int64_t n, hipStream_t s);
 
 // CSR-adaptive gather

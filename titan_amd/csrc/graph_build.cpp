@@ -442,6 +442,92 @@ int assemble_from_edges(const tgo_edges* e, const tgo_load_opts* opts, int64_t h
     return TGO_OK;
 }
 
+// ------------------------------------------------------------------ 1-D vertex partition
+// Multi-GPU: this device owns global vertices [lo, hi).  Its rows are the Titan rows of
+// those vertices (OUT entries of edges leaving them, IN entries of edges entering them),
+// with GLOBAL neighbour ids, so a gather reads remote messages from an all-gathered
+// global vector and bottom-up BFS probes an all-gathered global frontier bitmap.
+// No relabel (ids are global) and no push transposes (the partitioned path serves bothE
+// BFS, which is symmetric, and pull-only gathers).
+int assemble_partition(const tgo_edges* e, int64_t n_global, int64_t lo, int64_t hi,
+                       const tgo_load_opts* opts, int64_t hard_limit, HostGraph& g, int threads,
+                       std::string& err) {
+    g = HostGraph();
+    const int64_t n = hi - lo, m = e->m;
+    if (lo < 0 || hi > n_global || n <= 0 || n_global >= INT32_MAX) { err = "invalid partition range"; return TGO_E_INVALID; }
+    g.n = n;
+    g.scope = opts->scope;
+    g.has_weight = opts->weight_key != 0 && e->weight != nullptr;
+    g.titan_id.resize(n);
+    for (int64_t v = 0; v < n; ++v) g.titan_id[v] = (lo + v + 1) << 3;
+    std::atomic<bool> bad{false};
+    parallel_for(m, threads, [&](int64_t a, int64_t b, int) {
+        for (int64_t k = a; k < b; ++k)
+            if (e->src[k] < 0 || e->src[k] >= n_global || e->dst[k] < 0 || e->dst[k] >= n_global) { bad = true; return; }
+    });
+    if (bad) { err = "edge endpoint out of range"; return TGO_E_INVALID; }
+    const bool cap = opts->apply_cap && opts->n_labels == 0 && opts->scope != TGO_SCOPE_BOTH_E;
+    const int64_t limit = cap ? hard_limit : INT64_MAX;
+    auto build_dir = [&](bool out_dir, std::vector<int64_t>& off, std::vector<uint64_t>& keys) {
+        const int32_t* own = out_dir ? e->src : e->dst;
+        const int32_t* nbr = out_dir ? e->dst : e->src;
+        std::vector<std::atomic<int64_t>> cnt(n + 1);
+        for (auto& c : cnt) c.store(0, std::memory_order_relaxed);
+        parallel_for(m, threads, [&](int64_t a, int64_t b, int) {
+            for (int64_t k = a; k < b; ++k)
+                if (own[k] >= lo && own[k] < hi) cnt[own[k] - lo].fetch_add(1, std::memory_order_relaxed);
+        });
+        off.assign(n + 1, 0);
+        for (int64_t v = 0; v < n; ++v) off[v + 1] = off[v] + cnt[v].load(std::memory_order_relaxed);
+        for (int64_t v = 0; v < n; ++v) cnt[v].store(off[v], std::memory_order_relaxed);
+        keys.resize(off[n]);
+        parallel_for(m, threads, [&](int64_t a, int64_t b, int) {
+            for (int64_t k = a; k < b; ++k) {
+                if (own[k] < lo || own[k] >= hi) continue;
+                const int64_t p = cnt[own[k] - lo].fetch_add(1, std::memory_order_relaxed);
+                keys[p] = (static_cast<uint64_t>(static_cast<uint32_t>(nbr[k])) << 32) | static_cast<uint64_t>(k);
+            }
+        });
+        parallel_dynamic(n, threads, 4096, [&](int64_t a, int64_t b) {
+            for (int64_t v = a; v < b; ++v) std::sort(keys.begin() + off[v], keys.begin() + off[v + 1]);
+        });
+    };
+    if (m >= (int64_t(1) << 32)) { err = "more than 2^32 edges per load"; return TGO_E_UNSUPPORTED; }
+    std::vector<int64_t> off_o, off_i;
+    std::vector<uint64_t> keys_o, keys_i;
+    build_dir(true, off_o, keys_o);
+    build_dir(false, off_i, keys_i);
+    std::vector<int64_t> ko(n + 1, 0), ki(n + 1, 0);
+    int64_t truncated = 0;
+    for (int64_t v = 0; v < n; ++v) {
+        const int64_t a = off_o[v + 1] - off_o[v], b = off_i[v + 1] - off_i[v];
+        if (limit != INT64_MAX && a + b >= limit) ++truncated;
+        const int64_t ka = std::min(a, limit);
+        ko[v + 1] = ko[v] + ka;
+        ki[v + 1] = ki[v] + std::min(b, limit - ka);
+    }
+    g.truncated = truncated;
+    auto fill = [&](const std::vector<int64_t>& off, const std::vector<uint64_t>& keys,
+                    const std::vector<int64_t>& koff, HostCsr& c) {
+        c.off = koff;
+        c.adj.resize(koff[n]);
+        if (g.has_weight) c.w.resize(koff[n]);
+        parallel_for(n, threads, [&](int64_t a, int64_t b, int) {
+            for (int64_t v = a; v < b; ++v)
+                for (int64_t j = 0; j < koff[v + 1] - koff[v]; ++j) {
+                    const uint64_t key = keys[off[v] + j];
+                    c.adj[koff[v] + j] = static_cast<int32_t>(key >> 32);
+                    if (g.has_weight) c.w[koff[v] + j] = e->weight[key & 0xFFFFFFFFULL];
+                }
+        });
+    };
+    fill(off_o, keys_o, ko, g.out);
+    std::vector<uint64_t>().swap(keys_o);
+    fill(off_i, keys_i, ki, g.in);
+    g.has_transpose = false;
+    return TGO_OK;
+}
+
 // ------------------------------------------------------------------ CSR-adaptive blocks
 // Greedy partition of rows into blocks of <= tile entries and <= max_rows rows
 // (CSR-Adaptive, Greathouse & Daga SC'14); rows longer than `tile` become "long rows"

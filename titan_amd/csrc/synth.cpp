@@ -5,6 +5,7 @@
 #include <vector>
 #include "../../include/tgo_synth.h"
 #include "../../include/titan_gpu_olap.h"
+#include "../../include/titan_gpu_olap_part.h"
 
 namespace {
 
@@ -29,13 +30,9 @@ std::vector<int32_t> relabel(int64_t n, uint64_t seed) {
 
 }  // namespace
 
-extern "C" int tgo_rmat_edges(int32_t scale, int32_t edge_factor, uint64_t seed, int64_t edge_begin,
-                              int64_t count, int32_t* src, int32_t* dst, int32_t* weight, int32_t threads) {
-    if (scale < 1 || scale > 30 || edge_factor < 1 || count < 0 || !src || !dst) return TGO_E_INVALID;
-    const int64_t n = int64_t(1) << scale;
-    if (threads <= 0) threads = static_cast<int>(std::thread::hardware_concurrency());
-    threads = std::max(1, std::min(threads, 64));
-    const std::vector<int32_t> perm = relabel(n, seed ^ 0x5EED5EEDULL);
+static void rmat_range(int32_t scale, uint64_t seed, int64_t edge_begin, int64_t count,
+                       const std::vector<int32_t>& perm, int32_t* src, int32_t* dst, int32_t* weight,
+                       int threads) {
     // Quadrant thresholds in 16-bit fixed point: A=0.57, A+B=0.76, A+B+C=0.95.
     const uint32_t tA = static_cast<uint32_t>(0.57 * 65536.0);
     const uint32_t tB = static_cast<uint32_t>(0.76 * 65536.0);
@@ -65,8 +62,52 @@ extern "C" int tgo_rmat_edges(int32_t scale, int32_t edge_factor, uint64_t seed,
         th.emplace_back(work, lo, hi);
     }
     for (auto& x : th) x.join();
-    (void)edge_factor;
+}
+
+static int clamp_threads(int threads) {
+    if (threads <= 0) threads = static_cast<int>(std::thread::hardware_concurrency());
+    return std::max(1, std::min(threads, 64));
+}
+
+extern "C" int tgo_rmat_edges(int32_t scale, int32_t edge_factor, uint64_t seed, int64_t edge_begin,
+                              int64_t count, int32_t* src, int32_t* dst, int32_t* weight, int32_t threads) {
+    if (scale < 1 || scale > 30 || edge_factor < 1 || count < 0 || !src || !dst) return TGO_E_INVALID;
+    const std::vector<int32_t> perm = relabel(int64_t(1) << scale, seed ^ 0x5EED5EEDULL);
+    rmat_range(scale, seed, edge_begin, count, perm, src, dst, weight, clamp_threads(threads));
     return TGO_OK;
+}
+
+extern "C" int tgo_rmat_partition(int32_t scale, int32_t edge_factor, uint64_t seed, int64_t lo, int64_t hi,
+                                  int32_t* src, int32_t* dst, int32_t* weight, int64_t capacity,
+                                  int64_t* count, int32_t threads) {
+    if (scale < 1 || scale > 30 || edge_factor < 1 || !count || lo < 0 || hi <= lo) return TGO_E_INVALID;
+    threads = clamp_threads(threads);
+    const std::vector<int32_t> perm = relabel(int64_t(1) << scale, seed ^ 0x5EED5EEDULL);
+    const int64_t m = static_cast<int64_t>(edge_factor) << scale;
+    const int64_t chunk = int64_t(1) << 24;
+    std::vector<int32_t> s(chunk), d(chunk), w(weight ? chunk : 0);
+    int64_t got = 0;
+    bool overflow = false;
+    // Stream the full edge list in chunks (counter-based, so every rank sees the same
+    // stream) and keep the edges with an endpoint in [lo, hi).
+    for (int64_t e0 = 0; e0 < m; e0 += chunk) {
+        const int64_t c = std::min(chunk, m - e0);
+        rmat_range(scale, seed, e0, c, perm, s.data(), d.data(), weight ? w.data() : nullptr, threads);
+        for (int64_t k = 0; k < c; ++k) {
+            if ((s[k] >= lo && s[k] < hi) || (d[k] >= lo && d[k] < hi)) {
+                if (got < capacity && src && dst) {
+                    src[got] = s[k];
+                    dst[got] = d[k];
+                    if (weight) weight[got] = w[k];
+                } else {
+                    overflow = true;
+                }
+                ++got;
+            }
+        }
+    }
+    *count = got;
+    return overflow ? TGO_E_INVALID : TGO_OK;
 }
 
 extern "C" int tgo_pick_roots(int64_t n, int64_t m, const int32_t* src, const int32_t* dst, uint64_t seed,

@@ -1,0 +1,155 @@
+"""Multi-GPU driver: 1-D vertex-partitioned BFS and PageRank, one process per GPU.
+
+Rank r owns global vertices [r*n/N, (r+1)*n/N) and their Titan rows (include/
+titan_gpu_olap_part.h).  Every superstep is one local kernel on the rank's GPU plus one
+exchange through torch.distributed — backend "nccl", i.e. RCCL over xGMI on MI355X:
+
+  BFS top-down level   : local frontier marks neighbours in a global "discovered" bitmap
+                         -> all_to_all_single (slice r to rank r, n/8/N bytes each)
+                         -> owners OR the slices and claim unvisited vertices
+  BFS bottom-up level  : all_gather_into_tensor of owned next-frontier bitmap slices
+                         (n/8 bytes in total) -> unvisited owned vertices probe it
+  PageRank iteration   : all_gather_into_tensor of owned fp64 contributions (8n bytes)
+  every level          : all_reduce(SUM) of (frontier size, frontier entries)
+
+RCCL has no bitwise-OR reduction, hence slice exchanges (all-to-all / all-gather) instead
+of an all-reduce of bitmaps.  The direction switch is Beamer's, on global counts.
+
+The driver is written against a small "local step" backend so the exchange protocol is
+the same code on the GPU (HipPartBackend over the C-ABI, device tensors, RCCL) and in the
+CPU tests (a numpy backend with CPU tensors over gloo, tests/test_distributed.py).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import _lib as L
+
+
+def partition_range(n_global: int, world: int, rank: int):
+    """Contiguous owned range; every slice is a whole number of 64-bit bitmap words."""
+    if n_global % (64 * world):
+        raise ValueError("n_global must be a multiple of 64 * world_size")
+    per = n_global // world
+    return rank * per, (rank + 1) * per
+
+
+class HipPartBackend:
+    """Local steps on this rank's GPU through the C-ABI (titan_gpu_olap_part.h)."""
+
+    def __init__(self, engine, n_global, lo, hi):
+        self.e = engine
+        self.n_global, self.lo, self.hi = n_global, lo, hi
+        self.n_local = hi - lo
+        self.device = torch.device("cuda", torch.cuda.current_device())
+        self.total_entries = int(engine.stats()["out_entries"] + engine.stats()["in_entries"])
+
+    def tensor(self, n, dtype):
+        return torch.zeros(n, dtype=dtype, device=self.device)
+
+    @staticmethod
+    def _vp(t):
+        return C.c_void_p(t.data_ptr())
+
+    def _counts(self, fn, *args):
+        c = np.zeros(2, np.int64)
+        self.e.part_call(fn, *args, L.ptr(c, C.c_int64))
+        return c
+
+    def bfs_begin(self, seed, nb_local):
+        return self._counts("tgo_part_bfs_begin", C.c_int64(seed), self._vp(nb_local))
+
+    def bfs_td(self, level, disc):
+        self.e.part_call("tgo_part_bfs_td", level, self._vp(disc))
+
+    def bfs_claim(self, level, recv, nslices, nb_local):
+        return self._counts("tgo_part_bfs_claim", level, self._vp(recv), nslices, self._vp(nb_local))
+
+    def bfs_bu(self, level, fb_global, nb_local):
+        return self._counts("tgo_part_bfs_bu", level, self._vp(fb_global), self._vp(nb_local))
+
+    def bfs_end(self, fetch=True, stats=True):
+        out = np.zeros(self.n_local, np.int64) if fetch else None
+        reached = np.zeros(2, np.int64) if stats else None
+        self.e.part_call("tgo_part_bfs_end", L.ptr(out, C.c_int64), L.ptr(reached, C.c_int64))
+        return out, reached
+
+    def pr_begin(self, alpha, vertex_count, iters, contrib_local):
+        a = L.PrArgs(alpha, int(vertex_count), int(iters), 0)
+        self.e.part_call("tgo_part_pr_begin", C.byref(a), self._vp(contrib_local))
+
+    def pr_step(self, contrib_global, contrib_local):
+        self.e.part_call("tgo_part_pr_step", self._vp(contrib_global), self._vp(contrib_local))
+
+    def pr_end(self, fetch=True):
+        out = np.zeros(self.n_local, np.float64) if fetch else None
+        self.e.part_call("tgo_part_pr_end", L.ptr(out, C.c_double))
+        return out
+
+
+def _allreduce_counts(c, device):
+    t = torch.tensor(c, dtype=torch.int64, device=device)
+    dist.all_reduce(t)
+    return t.cpu().numpy()
+
+
+def distributed_bfs(backend, seed: int, max_depth: int, alpha: float = 15.0, beta: float = 18.0,
+                    fetch: bool = True, stats: bool = True, group=None):
+    """ShortestDistance with unit weights over bothE on a vertex-partitioned graph.
+    Returns (local distances or None, global reached [vertices, entries] or None, levels)."""
+    world = dist.get_world_size(group)
+    nwl = backend.n_local // 64
+    nwg = backend.n_global // 64
+    dev = backend.device
+    fb_global = backend.tensor(nwg, torch.int64)
+    nb_local = backend.tensor(nwl, torch.int64)
+    disc = backend.tensor(nwg, torch.int64)
+    recv = backend.tensor(nwg, torch.int64)
+    total = _allreduce_counts([backend.total_entries, 0], dev)[0]
+    c = backend.bfs_begin(seed, nb_local)
+    dist.all_gather_into_tensor(fb_global, nb_local, group=group)
+    nf, mf = _allreduce_counts(c, dev)
+    mu = total - mf
+    bottom_up = False
+    levels = 0
+    n = backend.n_global
+    for level in range(max_depth):
+        if nf == 0:
+            break
+        if not bottom_up and mf > mu / alpha:
+            bottom_up = True
+        elif bottom_up and nf < n / beta:
+            bottom_up = False
+        if bottom_up:
+            c = backend.bfs_bu(level, fb_global, nb_local)
+        else:
+            disc.zero_()
+            backend.bfs_td(level, disc)
+            dist.all_to_all_single(recv, disc, group=group)
+            c = backend.bfs_claim(level, recv, world, nb_local)
+        dist.all_gather_into_tensor(fb_global, nb_local, group=group)
+        nf, mf = _allreduce_counts(c, dev)
+        mu -= mf
+        levels += 1
+    out, reached = backend.bfs_end(fetch, stats)
+    if stats:
+        reached = _allreduce_counts(reached, dev)
+    return out, reached, levels
+
+
+def distributed_pagerank(backend, alpha: float, vertex_count: int, iterations: int, fetch: bool = True,
+                         group=None):
+    """PageRankVertexProgram on a vertex-partitioned graph; returns local ranks."""
+    if iterations == 0:
+        return np.full(backend.n_local, np.nan) if fetch else None
+    contrib_local = backend.tensor(backend.n_local, torch.float64)
+    contrib_global = backend.tensor(backend.n_global, torch.float64)
+    backend.pr_begin(alpha, vertex_count, iterations, contrib_local)
+    for _ in range(2, iterations + 1):
+        dist.all_gather_into_tensor(contrib_global, contrib_local, group=group)
+        backend.pr_step(contrib_global, contrib_local)
+    return backend.pr_end(fetch)

@@ -47,7 +47,7 @@ class Schema:
 
 class Engine:
     def __init__(self, device: int = 0, partition_bits: int = 5, host_threads: int = 0,
-                 hard_query_limit: int = 100000):
+                 hard_query_limit: int = 100000, stream: int = 0):
         self.lib = L.load()
         o = L.Options()
         self.lib.tgo_default_options(C.byref(o))
@@ -55,6 +55,7 @@ class Engine:
         o.partition_bits = partition_bits
         o.host_threads = host_threads
         o.hard_query_limit = hard_query_limit
+        o.stream = stream or None
         h = C.c_void_p()
         rc = self.lib.tgo_create(C.byref(o), C.byref(h))
         if rc != L.TGO_OK:
@@ -116,6 +117,20 @@ class Engine:
         _check(self.lib, self.ctx, self.lib.tgo_load_edges(self.ctx, C.byref(e), C.byref(opts)))
         self.n = self.lib.tgo_num_vertices(self.ctx)
         return self
+
+    # ------------------------------------------------------------------ 1-D partition (multi-GPU)
+    def load_partition(self, n_global, lo, hi, src, dst, scope, weight=None, apply_cap=True):
+        src = np.ascontiguousarray(src, dtype=np.int32)
+        dst = np.ascontiguousarray(dst, dtype=np.int32)
+        w = None if weight is None else np.ascontiguousarray(weight, dtype=np.int32)
+        e = L.Edges(n_global, len(src), L.ptr(src, C.c_int32), L.ptr(dst, C.c_int32), L.ptr(w, C.c_int32), None)
+        opts, keep = self._opts(scope, apply_cap, (), 1 if w is not None else 0)
+        _check(self.lib, self.ctx, self.lib.tgo_load_partition(self.ctx, n_global, lo, hi, C.byref(e), C.byref(opts)))
+        self.n = self.lib.tgo_num_vertices(self.ctx)
+        return self
+
+    def part_call(self, name, *args):
+        _check(self.lib, self.ctx, getattr(self.lib, name)(self.ctx, *args))
 
     def vertex_ids(self):
         out = np.zeros(self.n, dtype=np.int64)
