@@ -47,6 +47,8 @@ def parse():
     p.add_argument("--pr-iters", type=int, default=20)
     p.add_argument("--cpu-baseline", type=int, default=1, help="0 disables the oracle timing")
     p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--partitioned", action="store_true",
+                   help="use the vertex-partitioned multi-GPU path even at N=1 (for testing it on one GPU)")
     return p.parse_args()
 
 
@@ -280,7 +282,7 @@ def cpu_baseline(n, src, dst, roots, mR, depth, threads):
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world > 1:
+    if world > 1 or args.partitioned:
         run_partitioned(args, world, int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0")))
     else:
         run_single(args)
