@@ -1,0 +1,300 @@
+// msbfs.hip — multi-source BFS: up to 64 ShortestDistanceVertexProgram runs with unit
+// weights executed together (bit-parallel frontiers; Then et al., "The More the Merrier",
+// VLDB 2014).
+//
+// Per vertex v a 64-bit mask holds one bit per source: vis[v] (reached), fr[v] (reached at
+// the current level), nx[v] (reached at the next level).  A level of all sources is
+//   pull : nx[v] = (OR over v's reversed-scope neighbours u of fr[u]) & ~vis[v]
+//   push : for every frontier vertex u and push-neighbour v: atomicOr(nx[v], fr[u])
+// so one pass over the adjacency serves every source whose frontier touches it — the
+// adjacency is read once per level instead of once per level per source.  Each source's
+// result is identical to its own single-source run (Jacobi: fr is the previous level's
+// snapshot), stored as uint16 levels in a [vertex][source] layout (one 128-byte row per
+// vertex, so the discoveries of a vertex are written into one cache line).
+#include <hip/hip_runtime.h>
+#include "engine.hpp"
+
+namespace tgo {
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kEdgesPerThread = 8;
+constexpr int kTileEdges = kBlock * kEdgesPerThread;
+constexpr int kLdsEntries = kTileEdges + 2;
+constexpr int kMaxSources = 64;
+
+__device__ __forceinline__ int lane() { return static_cast<int>(threadIdx.x & 63); }
+
+__device__ __forceinline__ int64_t view_degree(const View& v, int64_t u) {
+    int64_t d = v.off0[u + 1] - v.off0[u];
+    if (v.nlists > 1) d += v.off1[u + 1] - v.off1[u];
+    return d;
+}
+
+__device__ __forceinline__ int32_t view_entry(const View& v, int64_t u, int64_t o) {
+    const int64_t b0 = v.off0[u];
+    const int64_t d0 = v.off0[u + 1] - b0;
+    return o < d0 ? v.adj0[b0 + o] : v.adj1[v.off1[u] + (o - d0)];
+}
+
+// Record the level of every newly reached source of v; append v to the next queue.
+__device__ __forceinline__ void discover(int64_t v, uint64_t fresh, int32_t level, uint16_t* __restrict__ lvl,
+                                         const View& push, int32_t* qn, int64_t* qdeg, Counters* cnt) {
+    const bool take = fresh != 0;
+    if (take) {
+        uint16_t* row = lvl + v * kMaxSources;
+        uint64_t b = fresh;
+        while (b) {
+            const int r = __ffsll(static_cast<long long>(b)) - 1;
+            b &= b - 1;
+            row[r] = static_cast<uint16_t>(level);
+        }
+    }
+    const unsigned long long mask = __ballot(take);
+    if (!mask) return;
+    const int leader = __ffsll(static_cast<long long>(mask)) - 1;
+    const int rank = __popcll(mask & ((1ULL << lane()) - 1ULL));
+    const int64_t deg = take ? view_degree(push, v) : 0;
+    int64_t dsum = deg;
+    unsigned long long bits = take ? static_cast<unsigned long long>(__popcll(fresh)) : 0ULL;
+    for (int off = 32; off > 0; off >>= 1) {
+        dsum += __shfl_xor(dsum, off, 64);
+        bits += __shfl_xor(bits, off, 64);
+    }
+    unsigned long long base = 0;
+    if (lane() == leader) {
+        base = atomicAdd(&cnt->qlen, static_cast<unsigned long long>(__popcll(mask)));
+        atomicAdd(&cnt->mf, static_cast<unsigned long long>(dsum));
+        atomicAdd(&cnt->red[0], bits);
+    }
+    base = __shfl(base, leader, 64);
+    if (take) {
+        qn[base + rank] = static_cast<int32_t>(v);
+        qdeg[base + rank] = deg;
+    }
+}
+
+__global__ void ms_seed(const int64_t* __restrict__ seeds, int nseeds, uint64_t* vis, uint64_t* fr,
+                        uint16_t* lvl) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        for (int r = 0; r < nseeds; ++r) {
+            const int64_t s = seeds[r];
+            vis[s] |= 1ULL << r;
+            fr[s] |= 1ULL << r;
+            lvl[s * kMaxSources + r] = 0;
+        }
+    }
+}
+
+// Pull level over the active vertices: OR the neighbours' frontier masks, stop as soon as
+// every still-unreached source of v is covered.  One vertex per lane; lists longer than
+// kCoop are OR-reduced by the whole wave.
+constexpr int64_t kCoop = 64;
+__global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t n_active, uint64_t full,
+        const uint64_t* __restrict__ fr, uint64_t* __restrict__ vis, uint64_t* __restrict__ nx,
+        uint16_t* __restrict__ lvl, int32_t* __restrict__ qn, int64_t* __restrict__ qdeg,
+        Counters* cnt, int32_t next_level) {
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    const int64_t words = (n_active + 63) >> 6;
+    for (int64_t wd = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; wd < words; wd += nwaves) {
+        const int64_t v = (wd << 6) + lane();
+        const uint64_t seen = v < n_active ? vis[v] : full;
+        const uint64_t open = full & ~seen;
+        int64_t b0 = 0, e0 = 0, b1 = 0, e1 = 0;
+        if (open) {
+            b0 = pull.off0[v]; e0 = pull.off0[v + 1];
+            if (pull.nlists > 1) { b1 = pull.off1[v]; e1 = pull.off1[v + 1]; }
+        }
+        const int64_t deg = (e0 - b0) + (e1 - b1);
+        uint64_t acc = 0;
+        if (open && deg <= kCoop) {
+            for (int l = 0; l < 2 && (acc & open) != open; ++l) {
+                const int32_t* adj = l == 0 ? pull.adj0 : pull.adj1;
+                const int64_t e = l == 0 ? e0 : e1;
+                for (int64_t k = l == 0 ? b0 : b1; k < e && (acc & open) != open; k += 4) {
+                    uint64_t m = 0;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        if (k + j < e) m |= fr[adj[k + j]];
+                    acc |= m;
+                }
+            }
+        }
+        unsigned long long big = __ballot(open != 0 && deg > kCoop);
+        while (big) {
+            const int src = __ffsll(static_cast<long long>(big)) - 1;
+            big &= big - 1;
+            const uint64_t want = __shfl(open, src, 64);
+            uint64_t a = 0;
+            for (int l = 0; l < 2; ++l) {
+                const int64_t bb = __shfl(l == 0 ? b0 : b1, src, 64);
+                const int64_t ee = __shfl(l == 0 ? e0 : e1, src, 64);
+                const int32_t* adj = l == 0 ? pull.adj0 : pull.adj1;
+                bool done = false;
+                for (int64_t k = bb; k < ee && !done; k += 64) {
+                    uint64_t m = k + lane() < ee ? fr[adj[k + lane()]] : 0;
+                    for (int off = 32; off > 0; off >>= 1) m |= __shfl_xor(m, off, 64);
+                    a |= m;
+                    done = (a & want) == want;
+                }
+                if ((a & want) == want) break;
+            }
+            if (lane() == src) acc = a;
+        }
+        const uint64_t fresh = acc & open;
+        if (v < n_active) {
+            nx[v] = fresh;
+            if (fresh) vis[v] = seen | fresh;
+        }
+        discover(v, fresh, next_level, lvl, push, qn, qdeg, cnt);
+    }
+}
+
+// Push level: edge-balanced over the frontier queue (exclusive scan of degrees in qpre).
+__global__ void __launch_bounds__(kBlock) ms_push(View push, const int32_t* __restrict__ q,
+        const int64_t* __restrict__ qpre, int64_t qlen, const uint64_t* __restrict__ fr,
+        const uint64_t* __restrict__ vis, uint64_t* __restrict__ nx) {
+    __shared__ int64_t s_pre[kLdsEntries];
+    __shared__ int32_t s_q[kLdsEntries];
+    __shared__ int64_t s_lo, s_hi;
+    const int64_t total = qpre[qlen];
+    const int64_t ntiles = (total + kTileEdges - 1) / kTileEdges;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t t0 = tile * kTileEdges;
+        const int64_t t1 = min(total, t0 + kTileEdges);
+        if (threadIdx.x == 0) {
+            int64_t a = 0, b = qlen;
+            while (b - a > 1) { const int64_t c = (a + b) >> 1; if (qpre[c] <= t0) a = c; else b = c; }
+            s_lo = a;
+            int64_t a2 = a, b2 = qlen;
+            while (b2 - a2 > 1) { const int64_t c = (a2 + b2) >> 1; if (qpre[c] <= t1 - 1) a2 = c; else b2 = c; }
+            s_hi = a2;
+        }
+        __syncthreads();
+        const int64_t lo = s_lo, hi = s_hi;
+        const int64_t span = hi - lo + 1;
+        const bool in_lds = span + 1 <= kLdsEntries;
+        if (in_lds) {
+            for (int64_t i = threadIdx.x; i <= span; i += kBlock) {
+                s_pre[i] = qpre[lo + i];
+                if (i < span) s_q[i] = q[lo + i];
+            }
+        }
+        __syncthreads();
+        for (int k = 0; k < kEdgesPerThread; ++k) {
+            const int64_t j = t0 + k * kBlock + threadIdx.x;
+            if (j >= t1) break;
+            int32_t u; int64_t start;
+            if (in_lds) {
+                int64_t a = 0, b = span;
+                while (b - a > 1) { const int64_t c = (a + b) >> 1; if (s_pre[c] <= j) a = c; else b = c; }
+                u = s_q[a]; start = s_pre[a];
+            } else {
+                int64_t a = lo, b = hi + 1;
+                while (b - a > 1) { const int64_t c = (a + b) >> 1; if (qpre[c] <= j) a = c; else b = c; }
+                u = q[a]; start = qpre[a];
+            }
+            const int32_t v = view_entry(push, u, j - start);
+            const uint64_t m = fr[u] & ~vis[v];
+            if (m && (nx[v] & m) != m) atomicOr(reinterpret_cast<unsigned long long*>(&nx[v]), m);
+        }
+        __syncthreads();
+    }
+}
+
+// After a push level: settle the candidates (nx & ~vis), record levels, build the queue.
+__global__ void __launch_bounds__(kBlock) ms_settle(View push, int64_t n_active, uint64_t* __restrict__ vis,
+        uint64_t* __restrict__ nx, uint16_t* __restrict__ lvl, int32_t* __restrict__ qn,
+        int64_t* __restrict__ qdeg, Counters* cnt, int32_t next_level) {
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    const int64_t words = (n_active + 63) >> 6;
+    for (int64_t wd = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; wd < words; wd += nwaves) {
+        const int64_t v = (wd << 6) + lane();
+        uint64_t fresh = 0;
+        if (v < n_active) {
+            const uint64_t c = nx[v];
+            if (c) {
+                const uint64_t seen = vis[v];
+                fresh = c & ~seen;
+                nx[v] = fresh;
+                if (fresh) vis[v] = seen | fresh;
+            }
+        }
+        discover(v, fresh, next_level, lvl, push, qn, qdeg, cnt);
+    }
+}
+
+// Per-source reached vertices / entries (stats, untimed): 64 counters per block in LDS.
+__global__ void __launch_bounds__(kBlock) ms_reach(View v, const uint64_t* __restrict__ vis, int64_t n_active,
+        int nsrc, unsigned long long* __restrict__ reached, unsigned long long* __restrict__ entries) {
+    __shared__ unsigned long long s_r[kMaxSources], s_e[kMaxSources];
+    if (threadIdx.x < kMaxSources) { s_r[threadIdx.x] = 0; s_e[threadIdx.x] = 0; }
+    __syncthreads();
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n_active; i += (int64_t)gridDim.x * blockDim.x) {
+        uint64_t b = vis[i];
+        if (!b) continue;
+        const unsigned long long d = static_cast<unsigned long long>(view_degree(v, i));
+        while (b) {
+            const int r = __ffsll(static_cast<long long>(b)) - 1;
+            b &= b - 1;
+            atomicAdd(&s_r[r], 1ULL);
+            atomicAdd(&s_e[r], d);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < nsrc) {
+        atomicAdd(&reached[threadIdx.x], s_r[threadIdx.x]);
+        atomicAdd(&entries[threadIdx.x], s_e[threadIdx.x]);
+    }
+}
+
+// Source r's distances in row order: dist[v] = level of (perm[v], r).
+__global__ void ms_extract(const uint16_t* __restrict__ lvl, const int32_t* __restrict__ perm, int r,
+                           int64_t* __restrict__ dist, int64_t n) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint16_t l = lvl[static_cast<int64_t>(perm[i]) * kMaxSources + r];
+        dist[i] = l == 0xFFFF ? INT64_MIN : static_cast<int64_t>(l);
+    }
+}
+
+inline int grid_for(int64_t work, int cap) {
+    int64_t g = (work + kBlock - 1) / kBlock;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return static_cast<int>(g);
+}
+
+}  // namespace
+
+hipError_t k_ms_seed(const int64_t* seeds, int nseeds, uint64_t* vis, uint64_t* fr, uint16_t* lvl, hipStream_t s) {
+    ms_seed<<<1, 64, 0, s>>>(seeds, nseeds, vis, fr, lvl);
+    return hipGetLastError();
+}
+hipError_t k_ms_pull(const View& pull, const View& push, int64_t n_active, uint64_t full, const uint64_t* fr,
+                     uint64_t* vis, uint64_t* nx, uint16_t* lvl, int32_t* qn, int64_t* qdeg, Counters* cnt,
+                     int32_t next_level, hipStream_t s) {
+    ms_pull<<<grid_for(n_active, 1 << 20), kBlock, 0, s>>>(pull, push, n_active, full, fr, vis, nx, lvl, qn, qdeg, cnt,
+                                                        next_level);
+    return hipGetLastError();
+}
+hipError_t k_ms_push(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen, const uint64_t* fr,
+                     const uint64_t* vis, uint64_t* nx, hipStream_t s) {
+    ms_push<<<256 * 8, kBlock, 0, s>>>(push, q, qpre, qlen, fr, vis, nx);
+    return hipGetLastError();
+}
+hipError_t k_ms_settle(const View& push, int64_t n_active, uint64_t* vis, uint64_t* nx, uint16_t* lvl, int32_t* qn,
+                       int64_t* qdeg, Counters* cnt, int32_t next_level, hipStream_t s) {
+    ms_settle<<<grid_for(n_active, 1 << 20), kBlock, 0, s>>>(push, n_active, vis, nx, lvl, qn, qdeg, cnt, next_level);
+    return hipGetLastError();
+}
+hipError_t k_ms_reach(const View& v, const uint64_t* vis, int64_t n_active, int nsrc, unsigned long long* reached,
+                      unsigned long long* entries, hipStream_t s) {
+    ms_reach<<<grid_for(n_active, 2048), kBlock, 0, s>>>(v, vis, n_active, nsrc, reached, entries);
+    return hipGetLastError();
+}
+hipError_t k_ms_extract(const uint16_t* lvl, const int32_t* perm, int r, int64_t* dist, int64_t n, hipStream_t s) {
+    ms_extract<<<grid_for(n, 4096), kBlock, 0, s>>>(lvl, perm, r, dist, n);
+    return hipGetLastError();
+}
+
+}  // namespace tgo
