@@ -73,10 +73,11 @@ def result_line(args, world, scale, n, m, roots, elapsed, teps, hmean, pr_s_iter
         "vs_baseline": None,
         "dtype": "int32 (BFS levels); f64 (PageRank)",
         "data": "synthetic RMAT (Graph500 A/B/C=0.57/0.19/0.19, ef16, seeded), 64 seeded roots",
-        "config": {"workload": f"rmat{scale}-bfs{len(roots)}-bothE+pagerank{args.pr_iters}", "scale": scale,
+        "config": {"workload": f"rmat{scale}-msbfs{len(roots)}-bothE+pagerank{args.pr_iters}", "scale": scale,
                    "edge_factor": args.edge_factor, "vertices": n, "edges": int(m), "roots": len(roots),
                    "pr_iterations": args.pr_iters, "parallelism": parallelism},
-        "gteps_hmean": round(hmean / 1e9, 4) if hmean else None,
+        "bfs_mode": "multi-source (64 ShortestDistance programs per sweep, bit-parallel frontiers)",
+        "single_source_gteps_hmean": round(hmean / 1e9, 4) if hmean else None,
         "pagerank_s_per_iter": round(pr_s_iter, 6),
         "pagerank_edges_per_s": round(e_in / pr_s_iter, 1),
         "bfs_share_of_step": round(bfs_share, 3),
@@ -108,22 +109,24 @@ def run_single(args):
     log(f"pagerank graph (inE, capped: {pst['truncated_results']} truncated rows) loaded in "
         f"{time.perf_counter() - t0:.1f}s")
     # per-root reached counts (untimed): m_R, n_R for GTEPS and algorithmic bytes
-    mR = np.zeros(len(roots), np.int64)
-    nR = np.zeros(len(roots), np.int64)
-    depth = np.zeros(len(roots), np.int64)
-    for i, r in enumerate(roots):
-        bfs_eng.bfs(int(r), n, L.SCOPE_BOTH_E, seed_is_dense=True, stats=True, fetch=False)
-        st = bfs_eng.stats()
-        mR[i], nR[i], depth[i] = st["reached_entries"], st["reached"], st["levels"]
+    bfs_eng.bfs_multi(roots, n, L.SCOPE_BOTH_E, seed_is_dense=True, stats=True, fetch=False)
+    nR, mR = bfs_eng.multi_stats(len(roots))
+    # single-source reference numbers (untimed side measurement, Graph500 style, 8 roots)
+    ss_t, depth0 = [], 1
+    for i, r in enumerate(roots[:8]):
+        bfs_eng.bfs(int(r), n, L.SCOPE_BOTH_E, seed_is_dense=True, fetch=False)
+        t = time.perf_counter()
+        bfs_eng.bfs(int(r), n, L.SCOPE_BOTH_E, seed_is_dense=True, fetch=False)
+        ss_t.append(time.perf_counter() - t)
+        if i == 0:
+            depth0 = bfs_eng.stats()["levels"]
+    ss_hmean = len(ss_t) / float(np.sum(np.array(ss_t) / (mR[:len(ss_t)] / 2.0)))
 
     def step():
-        bt = np.zeros(len(roots))
-        bk = np.zeros(len(roots))
-        for i, r in enumerate(roots):
-            t = time.perf_counter()
-            bfs_eng.bfs(int(r), n, L.SCOPE_BOTH_E, seed_is_dense=True, fetch=False)
-            bt[i] = time.perf_counter() - t
-            bk[i] = bfs_eng.stats()["last_kernel_ms"] / 1e3
+        t = time.perf_counter()
+        bfs_eng.bfs_multi(roots, n, L.SCOPE_BOTH_E, seed_is_dense=True, fetch=False)
+        bt = time.perf_counter() - t
+        bk = bfs_eng.stats()["last_kernel_ms"] / 1e3
         t = time.perf_counter()
         pr_eng.pagerank(0.85, n, args.pr_iters, fetch=False)
         return bt, bk, time.perf_counter() - t, pr_eng.stats()["last_kernel_ms"] / 1e3
@@ -135,17 +138,21 @@ def run_single(args):
     res = [step() for _ in range(args.steps)]
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - T0
-    bts = np.stack([r[0] for r in res])
-    bks = np.stack([r[1] for r in res])
+    bts = np.array([r[0] for r in res])
+    bks = np.array([r[1] for r in res])
     pts = np.array([r[2] for r in res])
     pks = np.array([r[3] for r in res])
     edges_in = mR / 2.0                      # Graph500 undirected count for bothE
     teps = float(edges_in.sum()) * args.steps / float(bts.sum())
-    hmean = len(roots) / float(np.sum(bts.mean(axis=0) / edges_in))
-    # roofline: BFS per root 4*m_R + 8*n_R + 4*n over the root's device time
-    bfs_bytes = 4.0 * mR + 8.0 * nR + 4.0 * n
-    roof_bfs = roofline("bfs_root (all level launches of one root)", float(bfs_bytes.sum() / bks.mean(axis=0).sum()) / 1e9,
-                        "4*m_R + 8*n_R + 4*n per root")
+    # roofline of the multi-source sweep: every reached vertex's entries and offsets read
+    # once (4*E_R + 16*n_R) + the uint16 level row of every vertex written (128*n)
+    nR_u = int(nR.max())
+    e_all = int(mR.max())
+    ms_bytes = 4.0 * e_all + 16.0 * nR_u + 128.0 * n
+    roof_bfs = roofline("msbfs sweep (64 sources, all level launches)", ms_bytes / bks.mean() / 1e9,
+                        "4*E + 16*n_R + 128*n per 64-source sweep")
+    hmean = ss_hmean
+    depth = np.array([depth0])
     upd = max(args.pr_iters - 1, 1)
     e_in = int(pst["in_entries"])
     pr_bytes = 4.0 * e_in + 8.0 * (n + 1) + 24.0 * n

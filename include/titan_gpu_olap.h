@@ -233,6 +233,17 @@ int  tgo_vertex_ids(tgo_ctx* ctx, int64_t* titan_ids_out);
  * result then stays on the device (tgo_copy_distances fetches it). */
 int  tgo_bfs(tgo_ctx* ctx, const tgo_bfs_args* args, int64_t* dist_out);
 int  tgo_sssp(tgo_ctx* ctx, const tgo_sssp_args* args, int64_t* dist_out);
+
+/* Multi-source BFS: up to TGO_MAX_SOURCES ShortestDistance programs with unit weights (one
+ * per seed; args->seed is ignored) run together with bit-parallel frontiers, one pass over
+ * the adjacency per level for all of them.  Each seed's distances equal its own tgo_bfs.
+ * dist_out: NULL (results stay on the device) or nseeds * n values, seed-major. */
+#define TGO_MAX_SOURCES 64
+int  tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_bfs_args* args,
+                   int64_t* dist_out);
+int  tgo_copy_multi_distances(tgo_ctx* ctx, int32_t source, int64_t* dist_out);
+/* After tgo_bfs_multi with TGO_FLAG_STATS: per seed, reached vertices and their entries. */
+int  tgo_multi_stats(tgo_ctx* ctx, int64_t* reached, int64_t* reached_entries);
 int  tgo_copy_distances(tgo_ctx* ctx, int64_t* dist_out);
 int  tgo_pagerank(tgo_ctx* ctx, const tgo_pr_args* args, double* pr_out);
 /* OLAPTest.DegreeCounter(k) (OLAPTest.java:334-416): k-walk counts, Java int wrap. */

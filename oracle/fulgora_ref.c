@@ -609,12 +609,13 @@ typedef struct {
     int64_t* dist;               /* property DISTANCE (immediate, VertexState.setProperty)      */
     int64_t* prev; int64_t* cur; /* double-buffered Local messages (VertexState :55-89)        */
     volatile int failed;
+    volatile int sent;           /* any message sent this superstep */
 } sd_t;
 static void sd_exec(void* p, const fr_graph* g, int64_t lo, int64_t hi) {
     sd_t* s = (sd_t*)p;
     for (int64_t v = lo; v < hi; v++) {
         if (s->iteration == 0) {                                         /* :97-104 */
-            if (g->titan_id[v] == s->seed) { s->dist[v] = 0; s->cur[v] = 0; }
+            if (g->titan_id[v] == s->seed) { s->dist[v] = 0; s->cur[v] = 0; s->sent = 1; }
             continue;
         }
         int64_t best = FR_ABSENT;                                        /* reduce(min).orElse(null) :109-110 */
@@ -634,7 +635,7 @@ static void sd_exec(void* p, const fr_graph* g, int64_t lo, int64_t hi) {
         }
         if (best == FR_ABSENT) continue;                                 /* :112-113 */
         if (s->dist[v] == FR_ABSENT || s->dist[v] > best) {             /* :117-122 */
-            s->dist[v] = best; s->cur[v] = best;
+            s->dist[v] = best; s->cur[v] = best; s->sent = 1;
         }
     }
 }
@@ -649,11 +650,15 @@ int fr_shortest_distance(const fr_graph* g, int64_t seed, int max_depth, int sco
     int it;
     for (it = 0;; it++) {                                                /* FulgoraGraphComputer :151-189 */
         s.iteration = it;
+        s.sent = 0;
         superstep(g, threads, &s, sd_exec);
         if (s.failed) { free(s.prev); free(s.cur); return FR_E_PROGRAM; }
         int64_t* t = s.prev; s.prev = s.cur; s.cur = t;                  /* completeIteration: prev=cur, cur=null */
         for (int64_t v = 0; v < g->n; v++) s.cur[v] = FR_ABSENT;
         if (it >= max_depth) break;                                      /* terminate :128-130 */
+        /* No message was sent: every later superstep receives nothing and changes nothing
+         * (:106-113), so skipping them is exact; the reported iteration stays maxDepth. */
+        if (!s.sent) { it = max_depth; break; }
     }
     if (iterations_out) *iterations_out = it;                            /* FulgoraMemory.complete :73-76 */
     free(s.prev); free(s.cur);

@@ -195,6 +195,35 @@ def test_rmat_bfs_bit_exact(rmat12, scope):
     assert np.array_equal(d, od)
 
 
+@pytest.mark.parametrize("scope", [BOTH, IN, OUT])
+@pytest.mark.parametrize("nseeds", [1, 5, 64])
+def test_rmat_multi_source_bfs_bit_exact(rmat12, scope, nseeds):
+    """64 ShortestDistance programs at once: every seed's result equals its own run."""
+    n, src, dst, w, ids, oracle, roots = rmat12
+    eng = Engine().load_edges(n, src, dst, scope)
+    seeds = pick_roots(n, src, dst, nseeds, seed=13)
+    d = eng.bfs_multi(seeds, n, scope, seed_is_dense=True, stats=True)
+    r, e = eng.multi_stats(nseeds)
+    for i, s in enumerate(seeds):
+        od, _ = oracle.shortest_distance(int(ids[s]), n, scope)
+        assert np.array_equal(d[i], od), i
+        assert r[i] == int((od != ABSENT).sum())
+    # hop bound applies to every source
+    d2 = eng.bfs_multi(seeds[:3], 2, scope, seed_is_dense=True)
+    for i, s in enumerate(seeds[:3]):
+        assert np.array_equal(d2[i], oracle.shortest_distance(int(ids[s]), 2, scope)[0])
+
+
+def test_multi_source_duplicate_and_gotg_seeds():
+    eng, rows, vids, sd, npz = engine_from_fixture("gotg", BOTH)
+    names = list(npz["names"])
+    seeds = [int(vids[names.index("jupiter")]), int(vids[names.index("saturn")]), int(vids[names.index("jupiter")])]
+    d = eng.bfs_multi(seeds, 12, BOTH)
+    single = eng.bfs(seeds[0], 12, BOTH)
+    assert np.array_equal(d[0], single) and np.array_equal(d[2], single)
+    assert np.array_equal(d[1], eng.bfs(seeds[1], 12, BOTH))
+
+
 def test_rmat_bfs_deterministic(rmat12):
     n, src, dst, w, ids, oracle, roots = rmat12
     eng = Engine().load_edges(n, src, dst, BOTH)

@@ -98,6 +98,7 @@ EXPORTS = [
     "tgo_default_options", "tgo_create", "tgo_destroy", "tgo_last_error", "tgo_load_rows",
     "tgo_finish_load", "tgo_load_edges", "tgo_num_vertices", "tgo_vertex_ids", "tgo_bfs",
     "tgo_sssp", "tgo_copy_distances", "tgo_pagerank", "tgo_walkcount", "tgo_stats_get", "tgo_sync",
+    "tgo_bfs_multi", "tgo_copy_multi_distances", "tgo_multi_stats",
     "tgo_rmat_edges", "tgo_pick_roots",
     # titan_gpu_olap_part.h (1-D vertex-partitioned multi-GPU)
     "tgo_load_partition", "tgo_part_bfs_begin", "tgo_part_bfs_td", "tgo_part_bfs_claim", "tgo_part_bfs_bu",
@@ -141,6 +142,9 @@ def load() -> C.CDLL:
         "tgo_walkcount": (C.c_int, [vp, C.c_int32, _i32p]),
         "tgo_stats_get": (C.c_int, [vp, P(Stats)]),
         "tgo_sync": (C.c_int, [vp]),
+        "tgo_bfs_multi": (C.c_int, [vp, _i64p, C.c_int32, P(BfsArgs), _i64p]),
+        "tgo_copy_multi_distances": (C.c_int, [vp, C.c_int32, _i64p]),
+        "tgo_multi_stats": (C.c_int, [vp, _i64p, _i64p]),
         "tgo_rmat_edges": (C.c_int, [C.c_int32, C.c_int32, C.c_uint64, C.c_int64, C.c_int64,
                                      _i32p, _i32p, _i32p, C.c_int32]),
         "tgo_pick_roots": (C.c_int, [C.c_int64, C.c_int64, _i32p, _i32p, C.c_uint64, C.c_int32, _i64p]),

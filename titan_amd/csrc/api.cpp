@@ -510,6 +510,138 @@ int tgo_sssp(tgo_ctx* ctx, const tgo_sssp_args* a, int64_t* dist_out) {
     return finish_distance_program(ctx, a->scope, a->flags, dist_out);
 }
 
+// ------------------------------------------------------------------ multi-source BFS
+static int ms_alloc(tgo_ctx* ctx) {
+    Scratch& s = ctx->sc;
+    if (s.ms_vis) return TGO_OK;
+    const int64_t n = ctx->g.n;
+    HIP_TRY(dev_alloc(ctx, s.ms_vis, n + 1));
+    HIP_TRY(dev_alloc(ctx, s.ms_fr, n + 1));
+    HIP_TRY(dev_alloc(ctx, s.ms_nx, n + 1));
+    HIP_TRY(dev_alloc(ctx, s.ms_lvl, (n + 1) * TGO_MAX_SOURCES));
+    HIP_TRY(dev_alloc(ctx, s.ms_seeds, TGO_MAX_SOURCES));
+    HIP_TRY(dev_alloc(ctx, s.ms_stat, 2 * TGO_MAX_SOURCES));
+    ctx->st.device_bytes = ctx->dev_bytes;
+    return TGO_OK;
+}
+
+int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_bfs_args* a, int64_t* dist_out) {
+    if (!ctx) return TGO_E_INVALID;
+    if (!a || !seeds) return fail(ctx, TGO_E_INVALID, "null args");
+    if (nseeds < 1 || nseeds > TGO_MAX_SOURCES) return fail(ctx, TGO_E_INVALID, "nseeds must be in [1, 64]");
+    int rc = check_program(ctx, a->scope);
+    if (rc) return rc;
+    if (a->max_depth < 0) return fail(ctx, TGO_E_INVALID, "max_depth < 0");
+    (void)hipSetDevice(ctx->opts.device);
+    if ((rc = ms_alloc(ctx))) return rc;
+    DevGraph& g = ctx->g;
+    Scratch& s = ctx->sc;
+    hipStream_t st = ctx->stream;
+    const int64_t n = g.n;
+    const View pull = pull_view(g, a->scope), push = push_view(g, a->scope);
+    std::vector<int64_t> in(nseeds);
+    std::vector<int32_t> uniq;
+    for (int r = 0; r < nseeds; ++r) {
+        if ((rc = resolve_seed(ctx, seeds[r], a->seed_is_dense, in[r]))) return rc;
+        if (in[r] < 0) return fail(ctx, TGO_E_INVALID, "multi-source BFS needs seeds that are executed vertices");
+        if (std::find(uniq.begin(), uniq.end(), static_cast<int32_t>(in[r])) == uniq.end())
+            uniq.push_back(static_cast<int32_t>(in[r]));
+    }
+    s.ms_nsrc = nseeds;
+    HIP_TRY(hipEventRecord(ctx->ev0, st));
+    HIP_TRY(hipMemcpyAsync(s.ms_seeds, in.data(), nseeds * sizeof(int64_t), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(s.q[0], uniq.data(), uniq.size() * sizeof(int32_t), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemsetAsync(s.ms_vis, 0, n * 8, st));
+    HIP_TRY(hipMemsetAsync(s.ms_fr, 0, n * 8, st));
+    HIP_TRY(hipMemsetAsync(s.ms_lvl, 0xFF, n * TGO_MAX_SOURCES * sizeof(uint16_t), st));
+    HIP_TRY(k_ms_seed(s.ms_seeds, nseeds, s.ms_vis, s.ms_fr, s.ms_lvl, st));
+    HIP_TRY(k_degree_i64(push, s.q[0], static_cast<int64_t>(uniq.size()), s.qdeg, st));
+    const uint64_t full = nseeds == 64 ? ~0ULL : ((1ULL << nseeds) - 1ULL);
+    const int64_t total = pull.nlists > 1 ? g.out.nnz + g.in.nnz : (a->scope == TGO_SCOPE_IN_E ? g.out.nnz : g.in.nnz);
+    static const double ms_alpha = env_double("TGO_MS_ALPHA", 12.0);
+    static const bool trace = env_double("TGO_TRACE", 0.0) != 0.0;
+    int64_t qlen = static_cast<int64_t>(uniq.size());
+    int64_t mf = 0;
+    {
+        std::vector<int64_t> d(qlen);
+        HIP_TRY(hipMemcpyAsync(d.data(), s.qdeg, qlen * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        for (int64_t x : d) mf += x;
+    }
+    const int depth = std::min(a->max_depth, 65534);
+    uint64_t* fr = s.ms_fr;
+    uint64_t* nx = s.ms_nx;
+    int cur = 0, levels = 0;
+    for (int L = 0; L < depth && qlen > 0; ++L) {
+        const bool use_pull = static_cast<double>(mf) * ms_alpha > static_cast<double>(total);
+        HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
+        if (use_pull) {
+            HIP_TRY(k_ms_pull(pull, push, g.n_active, full, fr, s.ms_vis, nx, s.ms_lvl, s.q[cur ^ 1], s.qdeg, s.cnt, L + 1, st));
+        } else {
+            HIP_TRY(hipMemsetAsync(nx, 0, n * 8, st));
+            if ((rc = scan_frontier(ctx, qlen))) return rc;
+            HIP_TRY(k_ms_push(push, s.q[cur], s.qpre, qlen, fr, s.ms_vis, nx, st));
+            HIP_TRY(k_ms_settle(push, g.n_active, s.ms_vis, nx, s.ms_lvl, s.q[cur ^ 1], s.qdeg, s.cnt, L + 1, st));
+        }
+        if ((rc = read_counters(ctx))) return rc;
+        qlen = static_cast<int64_t>(s.hcnt->qlen);
+        mf = static_cast<int64_t>(s.hcnt->mf);
+        if (trace) std::fprintf(stderr, "[tgo] ms level %d %s -> %lld vertices, %lld entries, %llu source-bits\n", L,
+                                use_pull ? "pull" : "push", (long long)qlen, (long long)mf, s.hcnt->red[0]);
+        std::swap(fr, nx);
+        cur ^= 1;
+        ++levels;
+    }
+    if (qlen > 0 && a->max_depth > depth)
+        return fail(ctx, TGO_E_UNSUPPORTED, "multi-source BFS stores levels as uint16: depth > 65534");
+    HIP_TRY(hipEventRecord(ctx->ev1, st));
+    HIP_TRY(hipEventSynchronize(ctx->ev1));
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+    ctx->st.last_kernel_ms = ms;
+    ctx->st.levels = levels;
+    ctx->st.iterations = a->max_depth;
+    if (a->flags & TGO_FLAG_STATS) {
+        HIP_TRY(hipMemsetAsync(s.ms_stat, 0, 2 * TGO_MAX_SOURCES * sizeof(unsigned long long), st));
+        HIP_TRY(k_ms_reach(pull, s.ms_vis, n, nseeds, s.ms_stat, s.ms_stat + TGO_MAX_SOURCES, st));
+        HIP_TRY(hipStreamSynchronize(st));
+    }
+    if (dist_out)
+        for (int r = 0; r < nseeds; ++r) {
+            HIP_TRY(k_ms_extract(s.ms_lvl, g.perm, r, s.msg, n, st));
+            HIP_TRY(hipMemcpyAsync(dist_out + static_cast<int64_t>(r) * n, s.msg, n * sizeof(int64_t),
+                                   hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+        }
+    return TGO_OK;
+}
+
+int tgo_copy_multi_distances(tgo_ctx* ctx, int32_t source, int64_t* dist_out) {
+    if (!ctx || !dist_out) return TGO_E_INVALID;
+    Scratch& s = ctx->sc;
+    if (!ctx->loaded || !s.ms_vis) return fail(ctx, TGO_E_STATE, "no multi-source BFS has run");
+    if (source < 0 || source >= s.ms_nsrc) return fail(ctx, TGO_E_INVALID, "source index out of range");
+    (void)hipSetDevice(ctx->opts.device);
+    HIP_TRY(k_ms_extract(s.ms_lvl, ctx->g.perm, source, s.msg, ctx->g.n, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(dist_out, s.msg, ctx->g.n * sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return TGO_OK;
+}
+
+int tgo_multi_stats(tgo_ctx* ctx, int64_t* reached, int64_t* reached_entries) {
+    if (!ctx) return TGO_E_INVALID;
+    Scratch& s = ctx->sc;
+    if (!ctx->loaded || !s.ms_vis) return fail(ctx, TGO_E_STATE, "no multi-source BFS has run");
+    (void)hipSetDevice(ctx->opts.device);
+    std::vector<unsigned long long> h(2 * TGO_MAX_SOURCES);
+    HIP_TRY(hipMemcpy(h.data(), s.ms_stat, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    for (int r = 0; r < s.ms_nsrc; ++r) {
+        if (reached) reached[r] = static_cast<int64_t>(h[r]);
+        if (reached_entries) reached_entries[r] = static_cast<int64_t>(h[TGO_MAX_SOURCES + r]);
+    }
+    return TGO_OK;
+}
+
 int tgo_copy_distances(tgo_ctx* ctx, int64_t* dist_out) {
     if (!ctx || !dist_out) return TGO_E_INVALID;
     if (!ctx->loaded) return fail(ctx, TGO_E_STATE, "no graph loaded");

@@ -140,6 +140,14 @@ struct Scratch {
     size_t cub_bytes = 0;
     Counters* cnt = nullptr;        // device
     Counters* hcnt = nullptr;       // pinned host mirror
+    // multi-source BFS (allocated on first use)
+    uint64_t* ms_vis = nullptr;     // n: reached-by mask
+    uint64_t* ms_fr = nullptr;      // n: frontier mask
+    uint64_t* ms_nx = nullptr;      // n: next-frontier mask
+    uint16_t* ms_lvl = nullptr;     // n * 64: level per (vertex, source), 0xFFFF = unreached
+    int64_t* ms_seeds = nullptr;    // 64
+    unsigned long long* ms_stat = nullptr;   // 128: reached[64], entries[64]
+    int32_t ms_nsrc = 0;
 };
 
 // ---------------------------------------------------------------- kernel launchers (HIP)
@@ -168,6 +176,17 @@ hipError_t k_sssp_commit(const int32_t* q, int64_t qlen, const int64_t* dist, in
                          uint64_t* mark, hipStream_t s);
 hipError_t k_dist_finalize(int64_t* dist, int64_t n, hipStream_t s);
 hipError_t k_unpermute_i64(const int64_t* in, const int32_t* perm, int64_t* out, int64_t n, hipStream_t s);
+hipError_t k_ms_seed(const int64_t* seeds, int nseeds, uint64_t* vis, uint64_t* fr, uint16_t* lvl, hipStream_t s);
+hipError_t k_ms_pull(const View& pull, const View& push, int64_t n_active, uint64_t full, const uint64_t* fr,
+                     uint64_t* vis, uint64_t* nx, uint16_t* lvl, int32_t* qn, int64_t* qdeg, Counters* cnt,
+                     int32_t next_level, hipStream_t s);
+hipError_t k_ms_push(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen, const uint64_t* fr,
+                     const uint64_t* vis, uint64_t* nx, hipStream_t s);
+hipError_t k_ms_settle(const View& push, int64_t n_active, uint64_t* vis, uint64_t* nx, uint16_t* lvl, int32_t* qn,
+                       int64_t* qdeg, Counters* cnt, int32_t next_level, hipStream_t s);
+hipError_t k_ms_reach(const View& v, const uint64_t* vis, int64_t n_active, int nsrc, unsigned long long* reached,
+                      unsigned long long* entries, hipStream_t s);
+hipError_t k_ms_extract(const uint16_t* lvl, const int32_t* perm, int r, int64_t* dist, int64_t n, hipStream_t s);
 hipError_t k_part_td_mark(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen,
                           uint64_t* disc, const uint64_t* vb_local, int64_t lo, int64_t n_local, hipStream_t s);
 hipError_t k_part_claim(const View& push, const uint64_t* recv, int nslices, int64_t words, int64_t n_local,

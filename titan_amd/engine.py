@@ -144,6 +144,21 @@ class Engine:
         _check(self.lib, self.ctx, self.lib.tgo_bfs(self.ctx, C.byref(a), L.ptr(out, C.c_int64)))
         return out
 
+    def bfs_multi(self, seeds, max_depth, scope, seed_is_dense=False, stats=False, fetch=True):
+        """Multi-source BFS (<= 64 seeds): returns a (nseeds, n) int64 array (or None)."""
+        sd = np.ascontiguousarray(seeds, dtype=np.int64)
+        a = L.BfsArgs(0, 1 if seed_is_dense else 0, int(max_depth), scope, L.FLAG_STATS if stats else 0)
+        out = np.zeros((len(sd), self.n), dtype=np.int64) if fetch else None
+        _check(self.lib, self.ctx, self.lib.tgo_bfs_multi(self.ctx, L.ptr(sd, C.c_int64), len(sd), C.byref(a),
+                                                          L.ptr(out, C.c_int64)))
+        return out
+
+    def multi_stats(self, nseeds):
+        r = np.zeros(nseeds, np.int64)
+        e = np.zeros(nseeds, np.int64)
+        _check(self.lib, self.ctx, self.lib.tgo_multi_stats(self.ctx, L.ptr(r, C.c_int64), L.ptr(e, C.c_int64)))
+        return r, e
+
     def sssp(self, seed, max_depth, scope, mode=L.SSSP_HOP_BOUNDED, seed_is_dense=False, stats=False, fetch=True):
         a = L.SsspArgs(int(seed), 1 if seed_is_dense else 0, int(max_depth), scope, mode, 0,
                        L.FLAG_STATS if stats else 0, 0)
