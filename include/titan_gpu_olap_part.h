@@ -42,6 +42,21 @@ int tgo_part_bfs_bu(tgo_ctx* ctx, int32_t level, const uint64_t* fb_global, uint
 /* Local distances (TGO_DIST_ABSENT = unreached) and reached[2] = {vertices, list entries}. */
 int tgo_part_bfs_end(tgo_ctx* ctx, int64_t* dist_local, int64_t* reached);
 
+/* Partitioned multi-source BFS (<= 64 seeds, global ids; bit r = seeds[r]).  Frontier
+ * masks are per owned vertex (fr_local / fr_next: n_local uint64 each).  Dense level:
+ * all-gather fr_local -> fr_global, then tgo_part_ms_pull.  Sparse level:
+ * tgo_part_ms_push marks candidate masks of global neighbours in cand_global (n_global),
+ * all-to-all of its slices into recv (nranks x n_local), then tgo_part_ms_settle. */
+int tgo_part_ms_begin(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, uint64_t* fr_local, int64_t* counts);
+int tgo_part_ms_pull(tgo_ctx* ctx, int32_t level, const uint64_t* fr_global, uint64_t* fr_next, int64_t* counts);
+int tgo_part_ms_push(tgo_ctx* ctx, int32_t level, const uint64_t* fr_local, uint64_t* cand_global);
+int tgo_part_ms_settle(tgo_ctx* ctx, int32_t level, const uint64_t* recv, int32_t nslices, uint64_t* fr_next,
+                       int64_t* counts);
+/* reached / entries: per seed, over this rank's vertices (NULL to skip). */
+int tgo_part_ms_end(tgo_ctx* ctx, int64_t* reached, int64_t* entries);
+/* Source `source`'s distances of the owned vertices (TGO_DIST_ABSENT = unreached). */
+int tgo_part_ms_levels(tgo_ctx* ctx, int32_t source, int64_t* dist_local);
+
 int tgo_part_pr_begin(tgo_ctx* ctx, const tgo_pr_args* args, double* contrib_local);
 int tgo_part_pr_step(tgo_ctx* ctx, const double* contrib_global, double* contrib_local);
 int tgo_part_pr_end(tgo_ctx* ctx, double* pr_local);

@@ -102,6 +102,72 @@ class NumpyPartBackend:
         reached = np.array([int((self.level >= 0).sum()), sum(self._deg(v) for v in range(self.n_local) if self.level[v] >= 0)])
         return d, reached
 
+    # ---- multi-source BFS local steps
+    def _ms_fresh(self, level, cand, fr_next):
+        fn = self._u(fr_next)
+        fn[:] = 0
+        self.msq = []
+        cnt = ent = 0
+        for v in range(self.n_local):
+            fresh = int(cand[v]) & ~int(self.msvis[v]) & self.full
+            if fresh:
+                self.msvis[v] = np.uint64(int(self.msvis[v]) | fresh)
+                fn[v] = np.uint64(fresh)
+                for r in range(self.nseeds):
+                    if (fresh >> r) & 1:
+                        self.mslvl[v, r] = level + 1
+                self.msq.append(v)
+                cnt += 1
+                ent += self._deg(v)
+        return np.array([cnt, ent])
+
+    def ms_begin(self, seeds, fr_local):
+        self.nseeds = len(seeds)
+        self.full = (1 << self.nseeds) - 1
+        self.msvis = np.zeros(self.n_local, np.uint64)
+        self.mslvl = np.full((self.n_local, self.nseeds), -1, np.int64)
+        fr = self._u(fr_local)
+        fr[:] = 0
+        self.msq = []
+        for r, s in enumerate(seeds):
+            if self.lo <= s < self.hi:
+                v = s - self.lo
+                self.msvis[v] = np.uint64(int(self.msvis[v]) | (1 << r))
+                fr[v] = np.uint64(int(fr[v]) | (1 << r))
+                self.mslvl[v, r] = 0
+                if v not in self.msq:
+                    self.msq.append(v)
+        return np.array([len(self.msq), sum(self._deg(v) for v in self.msq)])
+
+    def ms_pull(self, level, fr_global, fr_next):
+        fg = self._u(fr_global)
+        acc = np.zeros(self.n_local, np.uint64)
+        for v in range(self.n_local):
+            a = 0
+            for w in self.out[v] + self.inn[v]:
+                a |= int(fg[w])
+            acc[v] = np.uint64(a)
+        return self._ms_fresh(level, acc, fr_next)
+
+    def ms_push(self, level, fr_local, cand):
+        fr = self._u(fr_local)
+        c = self._u(cand)
+        for u in self.msq:
+            for w in self.out[u] + self.inn[u]:
+                c[w] = np.uint64(int(c[w]) | int(fr[u]))
+
+    def ms_settle(self, level, recv, nslices, fr_next):
+        r = self._u(recv).reshape(nslices, -1)
+        return self._ms_fresh(level, np.bitwise_or.reduce(r, axis=0), fr_next)
+
+    def ms_end(self, nseeds, stats=True):
+        if not stats:
+            return None, None
+        reached = np.array([int((self.mslvl[:, r] >= 0).sum()) for r in range(nseeds)])
+        entries = np.array([sum(self._deg(v) for v in range(self.n_local) if self.mslvl[v, r] >= 0)
+                            for r in range(nseeds)])
+        return reached, entries
+
     def pr_begin(self, alpha, N, iters, contrib_local):
         self.alpha, self.base = alpha, (1 - alpha) / N
         self.ec = np.array([float(len(o)) for o in self.out])
@@ -144,6 +210,16 @@ def _worker(rank, world, port, scale, roots, out_q, alpha):
         dist.all_gather(full, torch.from_numpy(d.astype(np.int64)))
         res["bfs"].append(torch.cat(full).numpy())
         res["reached"].append(reached)
+    from titan_amd.distributed import distributed_msbfs
+    for ms_alpha in (12.0, 1e9, 1e-9):         # mixed, always push, always pull
+        r, e, _ = distributed_msbfs(be, roots, n, ms_alpha=ms_alpha)
+        lv = []
+        for i in range(len(roots)):
+            loc = np.where(be.mslvl[:, i] >= 0, be.mslvl[:, i], ABSENT)
+            full = [torch.zeros(be.n_local, dtype=torch.int64) for _ in range(world)]
+            dist.all_gather(full, torch.from_numpy(loc.astype(np.int64)))
+            lv.append(torch.cat(full).numpy())
+        res.setdefault("ms", []).append((lv, r))
     pr = distributed_pagerank(be, 0.85, n, 10)
     full = [torch.zeros(be.n_local, dtype=torch.float64) for _ in range(world)]
     dist.all_gather(full, torch.from_numpy(pr))
@@ -178,6 +254,11 @@ def test_distributed_bfs_and_pagerank_match_oracle(world, alpha):
         od, _ = og.shortest_distance(int(ids[r]), n, 2)
         assert np.array_equal(d, od)
         assert reached[0] == int((od != ABSENT).sum())
+    for lv, reached in res["ms"]:
+        for i, r in enumerate(roots):
+            od, _ = og.shortest_distance(int(ids[r]), n, 2)
+            assert np.array_equal(lv[i], od)
+            assert reached[i] == int((od != ABSENT).sum())
     opr, _ = og.pagerank(0.85, n, 10)
     fin = np.isfinite(opr)
     assert np.array_equal(np.isfinite(res["pr"]), fin)

@@ -66,6 +66,71 @@ def run_bfs(backends, seed, max_depth, alpha=15.0, beta=18.0):
     return np.concatenate([o[0] for o in outs]), sum(o[1] for o in outs)
 
 
+def run_msbfs(backends, seeds, max_depth, ms_alpha=12.0):
+    """The distributed_msbfs protocol with the collectives done in-process."""
+    world = len(backends)
+    n = backends[0].n_global
+    nl = backends[0].n_local
+    fr_ = [b.tensor(nl, torch.int64) for b in backends]
+    frn = [b.tensor(nl, torch.int64) for b in backends]
+    fg = [b.tensor(n, torch.int64) for b in backends]
+    cand = [b.tensor(n, torch.int64) for b in backends]
+    recv = [b.tensor(n, torch.int64) for b in backends]
+    total = sum(b.total_entries for b in backends)
+    nf, mf = sum(b.ms_begin(seeds, fr_[i]) for i, b in enumerate(backends))
+    for level in range(max_depth):
+        if nf == 0:
+            break
+        cs = []
+        if mf * ms_alpha > total:
+            torch.cuda.synchronize()
+            g = torch.cat(fr_)
+            for t in fg:
+                t.copy_(g)
+            torch.cuda.synchronize()
+            for i, b in enumerate(backends):
+                cs.append(b.ms_pull(level, fg[i], frn[i]))
+        else:
+            for i, b in enumerate(backends):
+                cand[i].zero_()
+                b.ms_push(level, fr_[i], cand[i])
+            torch.cuda.synchronize()
+            for r in range(world):
+                recv[r].copy_(torch.cat([cand[s][r * nl:(r + 1) * nl] for s in range(world)]))
+            torch.cuda.synchronize()
+            for i, b in enumerate(backends):
+                cs.append(b.ms_settle(level, recv[i], world, frn[i]))
+        fr_, frn = frn, fr_
+        nf, mf = sum(cs)
+    ends = [b.ms_end(len(seeds)) for b in backends]
+    reached = sum(e[0] for e in ends)
+    levels = [np.concatenate([b.ms_levels(s) for b in backends]) for s in range(len(seeds))]
+    return levels, reached
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_partitioned_multi_source_bfs(world):
+    scale = 12
+    n = 1 << scale
+    src, dst, _ = rmat_edges(scale, 16, seed=33)
+    backends = []
+    for r in range(world):
+        lo, hi = partition_range(n, world, r)
+        eng = Engine(stream=torch.cuda.current_stream().cuda_stream).load_partition(n, lo, hi, src, dst, L.SCOPE_BOTH_E,
+                                                                                    apply_cap=False)
+        backends.append(HipPartBackend(eng, n, lo, hi))
+    og = fr.OracleGraph.from_edges(n, src, dst)
+    ids = (np.arange(n, dtype=np.int64) + 1) << 3
+    rng = np.random.default_rng(5)
+    seeds = [int(s) for s in rng.choice(n, 40, replace=False)] + [int(src[0])]
+    expect = [og.shortest_distance(int(ids[s]), n, 2)[0] for s in seeds]
+    for ms_alpha in (12.0, 1e9, 1e-9):
+        levels, reached = run_msbfs(backends, seeds, n, ms_alpha)
+        for i, od in enumerate(expect):
+            assert np.array_equal(levels[i], od), (ms_alpha, i)
+            assert reached[i] == int((od != ABSENT).sum())
+
+
 @pytest.mark.parametrize("world", [2, 4])
 def test_partitioned_bfs_and_pagerank(world):
     scale = 12

@@ -103,6 +103,8 @@ EXPORTS = [
     # titan_gpu_olap_part.h (1-D vertex-partitioned multi-GPU)
     "tgo_load_partition", "tgo_part_bfs_begin", "tgo_part_bfs_td", "tgo_part_bfs_claim", "tgo_part_bfs_bu",
     "tgo_part_bfs_end", "tgo_part_pr_begin", "tgo_part_pr_step", "tgo_part_pr_end", "tgo_rmat_partition",
+    "tgo_part_ms_begin", "tgo_part_ms_pull", "tgo_part_ms_push", "tgo_part_ms_settle", "tgo_part_ms_end",
+    "tgo_part_ms_levels",
 ]
 
 _lib = None
@@ -154,6 +156,12 @@ def load() -> C.CDLL:
         "tgo_part_bfs_claim": (C.c_int, [vp, C.c_int32, vp, C.c_int32, vp, _i64p]),
         "tgo_part_bfs_bu": (C.c_int, [vp, C.c_int32, vp, vp, _i64p]),
         "tgo_part_bfs_end": (C.c_int, [vp, _i64p, _i64p]),
+        "tgo_part_ms_begin": (C.c_int, [vp, _i64p, C.c_int32, vp, _i64p]),
+        "tgo_part_ms_pull": (C.c_int, [vp, C.c_int32, vp, vp, _i64p]),
+        "tgo_part_ms_push": (C.c_int, [vp, C.c_int32, vp, vp]),
+        "tgo_part_ms_settle": (C.c_int, [vp, C.c_int32, vp, C.c_int32, vp, _i64p]),
+        "tgo_part_ms_end": (C.c_int, [vp, _i64p, _i64p]),
+        "tgo_part_ms_levels": (C.c_int, [vp, C.c_int32, _i64p]),
         "tgo_part_pr_begin": (C.c_int, [vp, P(PrArgs), vp]),
         "tgo_part_pr_step": (C.c_int, [vp, vp, vp]),
         "tgo_part_pr_end": (C.c_int, [vp, C.POINTER(C.c_double)]),

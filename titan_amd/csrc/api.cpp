@@ -868,6 +868,135 @@ int tgo_part_bfs_end(tgo_ctx* ctx, int64_t* dist_local, int64_t* reached) {
     return TGO_OK;
 }
 
+// ---- partitioned multi-source BFS
+int tgo_part_ms_begin(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, uint64_t* fr_local, int64_t* counts) {
+    int rc = part_check(ctx);
+    if (rc) return rc;
+    if (!seeds || nseeds < 1 || nseeds > TGO_MAX_SOURCES) return fail(ctx, TGO_E_INVALID, "nseeds must be in [1, 64]");
+    if (ctx->g.scope != TGO_SCOPE_BOTH_E) return fail(ctx, TGO_E_UNSUPPORTED, "partitioned BFS runs over bothE");
+    if ((rc = ms_alloc(ctx))) return rc;
+    DevGraph& g = ctx->g;
+    Scratch& s = ctx->sc;
+    hipStream_t st = ctx->stream;
+    const int64_t n = g.n;
+    const View push = push_view(g, TGO_SCOPE_BOTH_E);
+    // owned seeds, as local ids; sources keep their global bit position r
+    std::vector<int64_t> local(nseeds, -1);
+    std::vector<int32_t> uniq;
+    for (int r = 0; r < nseeds; ++r) {
+        const int64_t l = seeds[r] - g.lo;
+        if (l >= 0 && l < n) {
+            local[r] = l;
+            if (std::find(uniq.begin(), uniq.end(), static_cast<int32_t>(l)) == uniq.end()) uniq.push_back(static_cast<int32_t>(l));
+        }
+    }
+    s.ms_nsrc = nseeds;
+    HIP_TRY(hipEventRecord(ctx->ev0, st));
+    HIP_TRY(hipMemsetAsync(s.ms_vis, 0, n * 8, st));
+    HIP_TRY(hipMemsetAsync(fr_local, 0, n * 8, st));
+    HIP_TRY(hipMemsetAsync(s.ms_lvl, 0xFF, n * TGO_MAX_SOURCES * sizeof(uint16_t), st));
+    // seeds owned elsewhere stay -1 (skipped by the seed kernel; their bit is set by the owner)
+    HIP_TRY(hipMemcpyAsync(s.ms_seeds, local.data(), nseeds * sizeof(int64_t), hipMemcpyHostToDevice, st));
+    HIP_TRY(k_ms_seed(s.ms_seeds, nseeds, s.ms_vis, fr_local, s.ms_lvl, st));
+    ctx->part_cur = 0;
+    ctx->part_qlen = static_cast<int64_t>(uniq.size());
+    int64_t mf = 0;
+    if (!uniq.empty()) {
+        HIP_TRY(hipMemcpyAsync(s.q[0], uniq.data(), uniq.size() * sizeof(int32_t), hipMemcpyHostToDevice, st));
+        HIP_TRY(k_degree_i64(push, s.q[0], static_cast<int64_t>(uniq.size()), s.qdeg, st));
+        std::vector<int64_t> d(uniq.size());
+        HIP_TRY(hipMemcpyAsync(d.data(), s.qdeg, d.size() * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        for (int64_t x : d) mf += x;
+    }
+    HIP_TRY(hipStreamSynchronize(st));
+    if (counts) { counts[0] = ctx->part_qlen; counts[1] = mf; }
+    return TGO_OK;
+}
+
+int tgo_part_ms_pull(tgo_ctx* ctx, int32_t level, const uint64_t* fr_global, uint64_t* fr_next, int64_t* counts) {
+    int rc = part_check(ctx);
+    if (rc) return rc;
+    DevGraph& g = ctx->g;
+    Scratch& s = ctx->sc;
+    hipStream_t st = ctx->stream;
+    const View pull = pull_view(g, TGO_SCOPE_BOTH_E), push = push_view(g, TGO_SCOPE_BOTH_E);
+    const uint64_t full = s.ms_nsrc == 64 ? ~0ULL : ((1ULL << s.ms_nsrc) - 1ULL);
+    HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
+    HIP_TRY(hipMemsetAsync(fr_next, 0, g.n * 8, st));
+    const int nxt = ctx->part_cur ^ 1;
+    HIP_TRY(k_ms_pull(pull, push, g.n_active, full, fr_global, s.ms_vis, fr_next, s.ms_lvl, s.q[nxt], s.qdeg, s.cnt,
+                      level + 1, st));
+    ctx->part_cur = nxt;
+    return part_counts(ctx, counts);
+}
+
+int tgo_part_ms_push(tgo_ctx* ctx, int32_t level, const uint64_t* fr_local, uint64_t* cand_global) {
+    int rc = part_check(ctx);
+    if (rc) return rc;
+    (void)level;
+    DevGraph& g = ctx->g;
+    Scratch& s = ctx->sc;
+    if (ctx->part_qlen > 0) {
+        if ((rc = scan_frontier(ctx, ctx->part_qlen))) return rc;
+        HIP_TRY(k_ms_push(push_view(g, TGO_SCOPE_BOTH_E), s.q[ctx->part_cur], s.qpre, ctx->part_qlen, fr_local,
+                          nullptr, cand_global, ctx->stream));
+    }
+    return TGO_OK;
+}
+
+int tgo_part_ms_settle(tgo_ctx* ctx, int32_t level, const uint64_t* recv, int32_t nslices, uint64_t* fr_next,
+                       int64_t* counts) {
+    int rc = part_check(ctx);
+    if (rc) return rc;
+    DevGraph& g = ctx->g;
+    Scratch& s = ctx->sc;
+    hipStream_t st = ctx->stream;
+    HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
+    HIP_TRY(k_or_slices(recv, nslices, g.n, fr_next, st));
+    const int nxt = ctx->part_cur ^ 1;
+    HIP_TRY(k_ms_settle(push_view(g, TGO_SCOPE_BOTH_E), g.n, s.ms_vis, fr_next, s.ms_lvl, s.q[nxt], s.qdeg, s.cnt,
+                        level + 1, st));
+    ctx->part_cur = nxt;
+    return part_counts(ctx, counts);
+}
+
+int tgo_part_ms_end(tgo_ctx* ctx, int64_t* reached, int64_t* entries) {
+    int rc = part_check(ctx);
+    if (rc) return rc;
+    Scratch& s = ctx->sc;
+    hipStream_t st = ctx->stream;
+    HIP_TRY(hipEventRecord(ctx->ev1, st));
+    if (reached || entries) {
+        HIP_TRY(hipMemsetAsync(s.ms_stat, 0, 2 * TGO_MAX_SOURCES * sizeof(unsigned long long), st));
+        HIP_TRY(k_ms_reach(pull_view(ctx->g, TGO_SCOPE_BOTH_E), s.ms_vis, ctx->g.n, s.ms_nsrc, s.ms_stat,
+                           s.ms_stat + TGO_MAX_SOURCES, st));
+        std::vector<unsigned long long> h(2 * TGO_MAX_SOURCES);
+        HIP_TRY(hipMemcpyAsync(h.data(), s.ms_stat, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        for (int r = 0; r < s.ms_nsrc; ++r) {
+            if (reached) reached[r] = static_cast<int64_t>(h[r]);
+            if (entries) entries[r] = static_cast<int64_t>(h[TGO_MAX_SOURCES + r]);
+        }
+    }
+    HIP_TRY(hipStreamSynchronize(st));
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+    ctx->st.last_kernel_ms = ms;
+    return TGO_OK;
+}
+
+int tgo_part_ms_levels(tgo_ctx* ctx, int32_t source, int64_t* dist_local) {
+    int rc = part_check(ctx);
+    if (rc) return rc;
+    Scratch& s = ctx->sc;
+    if (!s.ms_vis || source < 0 || source >= s.ms_nsrc || !dist_local) return fail(ctx, TGO_E_INVALID, "bad source");
+    HIP_TRY(k_ms_extract(s.ms_lvl, ctx->g.perm, source, s.msg, ctx->g.n, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(dist_local, s.msg, ctx->g.n * sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return TGO_OK;
+}
+
 int tgo_part_pr_begin(tgo_ctx* ctx, const tgo_pr_args* a, double* contrib_local) {
     int rc = part_check(ctx);
     if (rc) return rc;

@@ -187,6 +187,7 @@ hipError_t k_ms_settle(const View& push, int64_t n_active, uint64_t* vis, uint64
 hipError_t k_ms_reach(const View& v, const uint64_t* vis, int64_t n_active, int nsrc, unsigned long long* reached,
                       unsigned long long* entries, hipStream_t s);
 hipError_t k_ms_extract(const uint16_t* lvl, const int32_t* perm, int r, int64_t* dist, int64_t n, hipStream_t s);
+hipError_t k_or_slices(const uint64_t* recv, int nslices, int64_t n_local, uint64_t* out, hipStream_t s);
 hipError_t k_part_td_mark(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen,
                           uint64_t* disc, const uint64_t* vb_local, int64_t lo, int64_t n_local, hipStream_t s);
 hipError_t k_part_claim(const View& push, const uint64_t* recv, int nslices, int64_t words, int64_t n_local,

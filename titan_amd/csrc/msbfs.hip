@@ -79,6 +79,7 @@ __global__ void ms_seed(const int64_t* __restrict__ seeds, int nseeds, uint64_t*
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         for (int r = 0; r < nseeds; ++r) {
             const int64_t s = seeds[r];
+            if (s < 0) continue;                 // partitioned: seed owned by another rank
             vis[s] |= 1ULL << r;
             fr[s] |= 1ULL << r;
             lvl[s * kMaxSources + r] = 0;
@@ -195,7 +196,8 @@ __global__ void __launch_bounds__(kBlock) ms_push(View push, const int32_t* __re
                 u = q[a]; start = qpre[a];
             }
             const int32_t v = view_entry(push, u, j - start);
-            const uint64_t m = fr[u] & ~vis[v];
+            // partitioned graphs pass vis = nullptr: remote vertices' masks are not local
+            const uint64_t m = vis ? (fr[u] & ~vis[v]) : fr[u];
             if (m && (nx[v] & m) != m) atomicOr(reinterpret_cast<unsigned long long*>(&nx[v]), m);
         }
         __syncthreads();
@@ -221,6 +223,15 @@ __global__ void __launch_bounds__(kBlock) ms_settle(View push, int64_t n_active,
             }
         }
         discover(v, fresh, next_level, lvl, push, qn, qdeg, cnt);
+    }
+}
+
+// Partitioned push: OR the candidate-mask slices every rank sent for the owned vertices.
+__global__ void or_slices(const uint64_t* __restrict__ recv, int nslices, int64_t n_local, uint64_t* __restrict__ out) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n_local; i += (int64_t)gridDim.x * blockDim.x) {
+        uint64_t m = 0;
+        for (int s = 0; s < nslices; ++s) m |= recv[static_cast<int64_t>(s) * n_local + i];
+        out[i] = m;
     }
 }
 
@@ -290,6 +301,10 @@ hipError_t k_ms_settle(const View& push, int64_t n_active, uint64_t* vis, uint64
 hipError_t k_ms_reach(const View& v, const uint64_t* vis, int64_t n_active, int nsrc, unsigned long long* reached,
                       unsigned long long* entries, hipStream_t s) {
     ms_reach<<<grid_for(n_active, 2048), kBlock, 0, s>>>(v, vis, n_active, nsrc, reached, entries);
+    return hipGetLastError();
+}
+hipError_t k_or_slices(const uint64_t* recv, int nslices, int64_t n_local, uint64_t* out, hipStream_t s) {
+    or_slices<<<grid_for(n_local, 4096), kBlock, 0, s>>>(recv, nslices, n_local, out);
     return hipGetLastError();
 }
 hipError_t k_ms_extract(const uint16_t* lvl, const int32_t* perm, int r, int64_t* dist, int64_t n, hipStream_t s) {

@@ -78,6 +78,34 @@ class HipPartBackend:
         self.e.part_call("tgo_part_bfs_end", L.ptr(out, C.c_int64), L.ptr(reached, C.c_int64))
         return out, reached
 
+    # multi-source BFS local steps
+    def ms_begin(self, seeds, fr_local):
+        sd = np.ascontiguousarray(seeds, np.int64)
+        return self._counts("tgo_part_ms_begin", L.ptr(sd, C.c_int64), len(sd), self._vp(fr_local))
+
+    def ms_pull(self, level, fr_global, fr_next):
+        return self._counts("tgo_part_ms_pull", level, self._vp(fr_global), self._vp(fr_next))
+
+    def ms_push(self, level, fr_local, cand):
+        self.e.part_call("tgo_part_ms_push", level, self._vp(fr_local), self._vp(cand))
+
+    def ms_settle(self, level, recv, nslices, fr_next):
+        return self._counts("tgo_part_ms_settle", level, self._vp(recv), nslices, self._vp(fr_next))
+
+    def ms_end(self, nseeds, stats=True):
+        if not stats:
+            self.e.part_call("tgo_part_ms_end", None, None)
+            return None, None
+        r = np.zeros(nseeds, np.int64)
+        e = np.zeros(nseeds, np.int64)
+        self.e.part_call("tgo_part_ms_end", L.ptr(r, C.c_int64), L.ptr(e, C.c_int64))
+        return r, e
+
+    def ms_levels(self, source):
+        out = np.zeros(self.n_local, np.int64)
+        self.e.part_call("tgo_part_ms_levels", source, L.ptr(out, C.c_int64))
+        return out
+
     def pr_begin(self, alpha, vertex_count, iters, contrib_local):
         a = L.PrArgs(alpha, int(vertex_count), int(iters), 0)
         self.e.part_call("tgo_part_pr_begin", C.byref(a), self._vp(contrib_local))
@@ -139,6 +167,46 @@ def distributed_bfs(backend, seed: int, max_depth: int, alpha: float = 15.0, bet
     if stats:
         reached = _allreduce_counts(reached, dev)
     return out, reached, levels
+
+
+def distributed_msbfs(backend, seeds, max_depth: int, ms_alpha: float = 12.0, stats: bool = True, group=None):
+    """Up to 64 ShortestDistance programs with unit weights over bothE, run together with
+    bit-parallel frontier masks on a vertex-partitioned graph.
+      dense level : all_gather of owned frontier masks (8 bytes per vertex) -> local pull
+      sparse level: local push into global candidate masks -> all_to_all of slices -> settle
+    Returns (per-seed global reached vertices, per-seed reached entries, levels)."""
+    world = dist.get_world_size(group)
+    nseeds = len(seeds)
+    dev = backend.device
+    fr = backend.tensor(backend.n_local, torch.int64)
+    frn = backend.tensor(backend.n_local, torch.int64)
+    fr_global = backend.tensor(backend.n_global, torch.int64)
+    cand = backend.tensor(backend.n_global, torch.int64)
+    recv = backend.tensor(backend.n_global, torch.int64)
+    total = _allreduce_counts([backend.total_entries, 0], dev)[0]
+    nf, mf = _allreduce_counts(backend.ms_begin(seeds, fr), dev)
+    levels = 0
+    for level in range(max_depth):
+        if nf == 0:
+            break
+        if mf * ms_alpha > total:
+            dist.all_gather_into_tensor(fr_global, fr, group=group)
+            c = backend.ms_pull(level, fr_global, frn)
+        else:
+            cand.zero_()
+            backend.ms_push(level, fr, cand)
+            dist.all_to_all_single(recv, cand, group=group)
+            c = backend.ms_settle(level, recv, world, frn)
+        fr, frn = frn, fr
+        nf, mf = _allreduce_counts(c, dev)
+        levels += 1
+    r, e = backend.ms_end(nseeds, stats)
+    if stats:
+        t = torch.tensor(np.concatenate([r, e]), dtype=torch.int64, device=dev)
+        dist.all_reduce(t, group=group)
+        t = t.cpu().numpy()
+        r, e = t[:nseeds], t[nseeds:]
+    return r, e, levels
 
 
 def distributed_pagerank(backend, alpha: float, vertex_count: int, iterations: int, fetch: bool = True,
