@@ -47,15 +47,43 @@ def parse():
     p.add_argument("--pr-iters", type=int, default=20)
     p.add_argument("--cpu-baseline", type=int, default=1, help="0 disables the oracle timing")
     p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--sssp-roots", type=int, default=4, help="delta-stepping SSSP leg (configs[4]); 0 disables")
+    p.add_argument("--delta", type=int, default=0, help="delta-stepping bucket width (0 = engine default)")
     p.add_argument("--partitioned", action="store_true",
                    help="use the vertex-partitioned multi-GPU path even at N=1 (for testing it on one GPU)")
     return p.parse_args()
 
 
-def roofline(kernel, achieved_gbs, unit_desc):
-    return {"kernel": kernel, "bound": "hbm", "achieved": round(achieved_gbs, 2), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": None,
-            "bytes_per_unit": unit_desc}
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+
+
+def pmc_traffic(group):
+    """HBM bytes per unit (one rank update / one 64-source sweep) from the committed PMC
+    passes of this workload (scripts/gpu_pmc.sh -> scripts/pmc_traffic.py); None if absent.
+    PMC counters cannot be read from inside a timed run, so they come from separate
+    rocprofv3 --pmc runs of the same bench command."""
+    try:
+        with open(PMC_FILE) as f:
+            ent = json.load(f).get(group)
+    except (OSError, ValueError):
+        return None, None
+    if not ent:
+        return None, None
+    return ent["traffic_bytes"], ent
+
+
+def roofline(kernel, achieved_gbs, unit_desc, group=None, alg_bytes=None):
+    traffic, ent = pmc_traffic(group) if group else (None, None)
+    r = {"kernel": kernel, "bound": "hbm", "achieved": round(achieved_gbs, 2), "peak": HBM_PEAK_GBS,
+         "unit": "GB/s", "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
+         "traffic": round(traffic) if traffic else None, "bytes_per_unit": unit_desc}
+    if alg_bytes:
+        r["algorithmic_bytes"] = round(alg_bytes)
+    if ent:
+        r["traffic_detail"] = {"source": os.path.relpath(PMC_FILE, ROOT), "fetch_bytes_raw": round(ent["fetch_bytes_raw"]),
+                               "write_bytes": round(ent["write_bytes"]), "l2_hit_rate": ent.get("l2_hit_rate"),
+                               "correction": ent["correction"]}
+    return r
 
 
 def result_line(args, world, scale, n, m, roots, elapsed, teps, hmean, pr_s_iter, e_in, roof_bfs, roof_pr,
@@ -150,21 +178,58 @@ def run_single(args):
     e_all = int(mR.max())
     ms_bytes = 4.0 * e_all + 16.0 * nR_u + 128.0 * n
     roof_bfs = roofline("msbfs sweep (64 sources, all level launches)", ms_bytes / bks.mean() / 1e9,
-                        "4*E + 16*n_R + 128*n per 64-source sweep")
+                        "4*E + 16*n_R + 128*n per 64-source sweep", "msbfs_sweep", ms_bytes)
     hmean = ss_hmean
     depth = np.array([depth0])
     upd = max(args.pr_iters - 1, 1)
     e_in = int(pst["in_entries"])
     pr_bytes = 4.0 * e_in + 8.0 * (n + 1) + 24.0 * n
     roof_pr = roofline("pagerank_update (gather_short + long-row chunks)", pr_bytes / (pks.mean() / upd) / 1e9,
-                       "4*m + 8*(n+1) + 24*n per update")
+                       "4*m + 8*(n+1) + 24*n per update", "pagerank_update", pr_bytes)
     bfs_share = float(bts.sum()) / (float(bts.sum()) + float(pts.sum()))
+    del pr_eng
+    sssp = sssp_leg(args, n, src, dst, roots) if args.sssp_roots > 0 else None
     cpu = None
     if args.cpu_baseline:
         # levels counts the final empty level; the eccentricity is one less
         cpu = cpu_baseline(n, src, dst, roots, mR, max(int(depth[0]) - 1, 1), args.cpu_threads)
-    print(json.dumps(result_line(args, 1, scale, n, m, roots, elapsed, teps, hmean, float(pts.mean()) / upd, e_in,
-                                 roof_bfs, roof_pr, bfs_share, cpu, "single")), flush=True)
+    line = result_line(args, 1, scale, n, m, roots, elapsed, teps, hmean, float(pts.mean()) / upd, e_in,
+                       roof_bfs, roof_pr, bfs_share, cpu, "single")
+    line["sssp"] = sssp
+    print(json.dumps(line), flush=True)
+
+
+def sssp_leg(args, n, src, dst, roots):
+    """configs[4] on one GPU: delta-stepping SSSP (ShortestDistanceVertexProgram, inE scope,
+    int32 weights w = 1 + splitmix64 mod 255, parity cap on) from a few of the BFS roots on
+    the same RMAT graph; GTEPS = pull entries of reached vertices / device time."""
+    from titan_amd import Engine, rmat_edges
+    from titan_amd import _lib as L
+    _, _, w = rmat_edges(args.scale, args.edge_factor, seed=0x54495441, weights=True)
+    eng = Engine(device=0, host_threads=16).load_edges(n, src, dst, L.SCOPE_IN_E, weight=w, apply_cap=True)
+    del w
+    res = []
+    for r in roots:
+        if len(res) == args.sssp_roots:
+            break
+        eng.sssp(int(r), n, L.SCOPE_IN_E, mode=L.SSSP_DELTA, seed_is_dense=True, stats=True, fetch=False,
+                 delta=args.delta)
+        st = eng.stats()
+        if st["reached"] * 4 < n:        # directed scope: skip roots whose reach is not the giant component
+            continue
+        t = time.perf_counter()
+        eng.sssp(int(r), n, L.SCOPE_IN_E, mode=L.SSSP_DELTA, seed_is_dense=True, fetch=False, delta=args.delta)
+        wall = time.perf_counter() - t
+        res.append((st["reached_entries"], st["relaxed_entries"], eng.stats()["last_kernel_ms"] / 1e3, wall,
+                    st["levels"]))
+    mR = np.array([x[0] for x in res], np.float64)
+    dev = np.array([x[2] for x in res])
+    wall = np.array([x[3] for x in res])
+    return {"workload": f"rmat{args.scale}-weighted-inE-delta-sssp", "roots": len(res),
+            "gteps_hmean": round(len(res) / float(np.sum(wall / mR)) / 1e9, 4),
+            "ms_per_root": round(float(wall.mean()) * 1e3, 3), "device_ms_per_root": round(float(dev.mean()) * 1e3, 3),
+            "reached_entries": int(mR.mean()), "relaxed_entries": int(np.mean([x[1] for x in res])),
+            "phases": int(np.mean([x[4] for x in res]))}
 
 
 # ----------------------------------------------------------------------------- N GPUs

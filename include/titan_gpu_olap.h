@@ -207,6 +207,8 @@ typedef struct {
     double  load_ms;              /* CSR assembly + upload                                     */
     double  last_kernel_ms;       /* device time of the last program (HIP events)              */
     int64_t device_bytes;         /* device memory held by the ctx                             */
+    int64_t relaxed_entries;      /* push entries relaxed by the last SSSP (work done; equals
+                                     reached_entries when every vertex is relaxed once)         */
 } tgo_stats;
 
 /* ---- Entry points ------------------------------------------------------------------- */

@@ -242,12 +242,44 @@ def test_rmat_sssp_weighted_bit_exact(rmat12, depth):
         assert np.array_equal(d, od)
 
 
-def test_rmat_sssp_delta_equals_converged(rmat12):
+@pytest.mark.parametrize("scope", [OUT, IN, BOTH])
+@pytest.mark.parametrize("delta", [0, 1, 37, 1 << 40])
+def test_rmat_sssp_delta_equals_converged(rmat12, scope, delta):
+    """Delta-stepping (any bucket width, incl. one bucket = Bellman-Ford and width 1 =
+    Dijkstra-like) gives the converged distances of the reference program bit-exactly."""
     n, src, dst, w, ids, oracle, roots = rmat12
-    eng = Engine().load_edges(n, src, dst, OUT, weight=w)
-    d = eng.sssp(int(roots[0]), n, OUT, mode=L.SSSP_DELTA, seed_is_dense=True)
-    od, _ = oracle.shortest_distance(int(ids[roots[0]]), n, OUT, weighted=True)
-    assert np.array_equal(d, od)
+    eng = Engine().load_edges(n, src, dst, scope, weight=w)
+    for r in roots[:3]:
+        d = eng.sssp(int(r), n, scope, mode=L.SSSP_DELTA, seed_is_dense=True, stats=True, delta=delta)
+        od, _ = oracle.shortest_distance(int(ids[r]), n, scope, weighted=True)
+        assert np.array_equal(d, od)
+        st = eng.stats()
+        assert st["reached"] == int((od != ABSENT).sum())
+        assert (st["relaxed_entries"] > 0) == (st["reached"] > 1)   # a seed with no push entries reaches nobody
+
+
+def test_rmat_sssp_delta_zero_weights(rmat12):
+    """Zero-weight edges (ties inside a bucket, re-relaxation at equal distance)."""
+    n, src, dst, w, ids, _, roots = rmat12
+    w0 = (w % 3).astype(np.int32)
+    off, mid, adj, ww = numpy_adjacency(n, src, dst, w0)
+    oracle = fr.OracleGraph.from_adjacency(ids, off, mid, adj, ww)
+    eng = Engine().load_edges(n, src, dst, OUT, weight=w0)
+    for r in roots[:2]:
+        d = eng.sssp(int(r), n, OUT, mode=L.SSSP_DELTA, seed_is_dense=True, delta=2)
+        assert np.array_equal(d, oracle.shortest_distance(int(ids[r]), n, OUT, weighted=True)[0])
+
+
+def test_sssp_tree_delta():
+    rows, vids, sd, npz = load_fixture("sssp_tree")
+    wk = int(npz["weight_key"])
+    eng = Engine().load_rows(rows, Schema.from_dict(sd), IN, weight_key=wk)
+    seed = int(vids[int(npz["seed_index"])])
+    d = reorder(eng.vertex_ids(), eng.sssp(seed, 100, IN, mode=L.SSSP_DELTA), vids)
+    assert list(d) == list(npz["expected_dist"])
+    # unknown seed: nobody gets a distance
+    assert -1 not in set(int(v) for v in vids)
+    assert (eng.sssp(-1, 100, IN, mode=L.SSSP_DELTA) == ABSENT).all()
 
 
 @pytest.mark.parametrize("iters", [0, 1, 2, 5, 20])

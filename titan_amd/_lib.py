@@ -90,7 +90,8 @@ class Stats(C.Structure):
     _fields_ = [("num_vertices", C.c_int64), ("out_entries", C.c_int64), ("in_entries", C.c_int64), ("ghost_vertices", C.c_int64),
                 ("truncated_results", C.c_int64), ("skipped_rows", C.c_int64), ("iterations", C.c_int32),
                 ("levels", C.c_int32), ("reached", C.c_int64), ("reached_entries", C.c_int64),
-                ("load_ms", C.c_double), ("last_kernel_ms", C.c_double), ("device_bytes", C.c_int64)]
+                ("load_ms", C.c_double), ("last_kernel_ms", C.c_double), ("device_bytes", C.c_int64),
+                ("relaxed_entries", C.c_int64)]
 
 
 # Every symbol include/*.h declares (checked by tests/test_abi.py).

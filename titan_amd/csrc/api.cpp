@@ -105,8 +105,12 @@ int upload_graph(tgo_ctx* ctx, HostGraph& h) {
     for (int64_t v = h.n - 1; v >= 0; --v)
         if (h.out.off[v + 1] > h.out.off[v] || h.in.off[v + 1] > h.in.off[v]) { g.n_active = v + 1; break; }
     g.min_weight = 0;
+    double wsum = 0.0;
+    int64_t wcnt = 0;
     for (const HostCsr* c : {&h.out, &h.in})
-        for (int32_t x : c->w) if (x != kMissingWeight) g.min_weight = std::min(g.min_weight, x);
+        for (int32_t x : c->w)
+            if (x != kMissingWeight) { g.min_weight = std::min(g.min_weight, x); wsum += x; ++wcnt; }
+    g.mean_weight = wcnt ? wsum / static_cast<double>(wcnt) : 1.0;
     auto up = [&](HostCsr& src, DevCsr& dst) -> hipError_t {
         hipError_t e;
         if ((e = upload(ctx, dst.off, src.off)) != hipSuccess) return e;
@@ -332,6 +336,66 @@ int run_sssp(tgo_ctx* ctx, int64_t seed, int max_depth, int scope, bool weighted
     return TGO_OK;
 }
 
+// Delta-stepping (delta.hip): converged distances, near queue relaxed phase by phase,
+// bucket threshold advanced from the minimum pending distance when the queue runs dry.
+int run_delta(tgo_ctx* ctx, int64_t seed, int scope, bool weighted, int64_t delta) {
+    DevGraph& g = ctx->g;
+    Scratch& s = ctx->sc;
+    hipStream_t st = ctx->stream;
+    const int64_t n = g.n, words = (n + 63) / 64 + 1;
+    const View push = push_view(g, scope);
+    static const double delta_env = env_double("TGO_DELTA", 0.0);
+    static const bool trace = env_double("TGO_TRACE", 0.0) != 0.0;
+    if (delta <= 0) delta = delta_env > 0 ? static_cast<int64_t>(delta_env)
+                                          : std::max<int64_t>(1, static_cast<int64_t>(weighted ? 2.0 * g.mean_weight : 1.0));
+    HIP_TRY(k_fill_i64(s.dist, INT64_MAX, n, st));
+    HIP_TRY(hipMemsetAsync(s.vb, 0, words * 8, st));        // pending bitmap
+    int phases = 0, buckets = 0;
+    int64_t relaxed = 0;
+    if (seed >= 0) {
+        HIP_TRY(k_ds_seed(push, s.dist, s.q[0], s.qdeg, seed, st));
+        int64_t qlen = 1, thr = delta;
+        int cur = 0;
+        for (;;) {
+            if (qlen == 0) {
+                HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
+                HIP_TRY(hipMemsetAsync(&s.cnt->red[0], 0x7F, sizeof(unsigned long long), st));   // ~INT64_MAX
+                HIP_TRY(k_ds_pending_min(s.vb, words, s.dist, s.cnt, st));
+                if (int rc = read_counters(ctx)) return rc;
+                if (s.hcnt->red[1] == 0) break;                 // nothing pending: converged
+                const int64_t mn = static_cast<int64_t>(s.hcnt->red[0]);
+                if (mn >= thr) thr = (mn / delta + 1) * delta;
+                ++buckets;
+                HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
+                HIP_TRY(k_ds_extract(push, s.vb, n, s.dist, thr, s.q[cur], s.qdeg, s.cnt, st));
+                if (int rc = read_counters(ctx)) return rc;
+                qlen = static_cast<int64_t>(s.hcnt->qlen);
+                if (trace) std::fprintf(stderr, "[tgo] delta bucket thr %lld: min pending %lld, %llu pending, %lld queued\n",
+                                        (long long)thr, (long long)mn, s.hcnt->red[1], (long long)qlen);
+                if (qlen == 0) return fail(ctx, TGO_E_HIP, "delta-stepping: extraction found no vertex below the threshold");
+            }
+            HIP_TRY(k_ds_commit(s.q[cur], qlen, s.dist, s.msg, s.vb, st));
+            if (int rc = scan_frontier(ctx, qlen)) return rc;
+            HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
+            HIP_TRY(k_ds_relax(push, s.q[cur], s.qpre, qlen, s.msg, s.dist, s.vb, s.q[cur ^ 1], s.qdeg, s.cnt,
+                               weighted ? 1 : 0, thr, st));
+            if (int rc = read_counters(ctx)) return rc;
+            if (s.hcnt->err) return fail(ctx, TGO_E_PROGRAM,
+                "vertex program failed: a traversed edge has no value for the weight property");
+            relaxed += static_cast<int64_t>(s.hcnt->red[1]);      // qpre[qlen], set by ds_relax
+            qlen = static_cast<int64_t>(s.hcnt->qlen);
+            cur ^= 1;
+            ++phases;
+        }
+    }
+    HIP_TRY(k_dist_finalize(s.dist, n, st));
+    if (trace) std::fprintf(stderr, "[tgo] delta %lld: %d phases, %d buckets, %lld entries relaxed\n",
+                            (long long)delta, phases, buckets, (long long)relaxed);
+    ctx->st.levels = phases;
+    ctx->st.relaxed_entries = relaxed;
+    return TGO_OK;
+}
+
 int finish_distance_program(tgo_ctx* ctx, int scope, int flags, int64_t* dist_out) {
     Scratch& s = ctx->sc;
     HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
@@ -501,12 +565,17 @@ int tgo_sssp(tgo_ctx* ctx, const tgo_sssp_args* a, int64_t* dist_out) {
     int64_t seed;
     if ((rc = resolve_seed(ctx, a->seed, a->seed_is_dense, seed))) return rc;
     HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
-    // DELTA mode is served by the exact hop-bounded kernel with an unbounded hop count
-    // until the bucketed kernel lands; its result is the converged distance either way.
-    if (a->mode == TGO_SSSP_DELTA && ctx->g.has_weight && ctx->g.min_weight < 0)
-        return fail(ctx, TGO_E_INVALID, "DELTA mode needs non-negative weights");
-    const int depth = a->mode == TGO_SSSP_DELTA ? INT32_MAX : a->max_depth;
-    if ((rc = run_sssp(ctx, seed, depth, a->scope, ctx->g.has_weight))) return rc;
+    ctx->st.relaxed_entries = 0;
+    if (a->mode == TGO_SSSP_DELTA) {
+        // converged distances (== the reference's whenever maxDepth >= the hop count of
+        // every shortest path); max_depth only sets the reported iteration count
+        if (ctx->g.has_weight && ctx->g.min_weight < 0)
+            return fail(ctx, TGO_E_INVALID, "DELTA mode needs non-negative weights");
+        if ((rc = run_delta(ctx, seed, a->scope, ctx->g.has_weight, a->delta))) return rc;
+        ctx->st.iterations = a->max_depth;
+    } else {
+        if ((rc = run_sssp(ctx, seed, a->max_depth, a->scope, ctx->g.has_weight))) return rc;
+    }
     return finish_distance_program(ctx, a->scope, a->flags, dist_out);
 }
 

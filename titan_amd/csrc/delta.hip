@@ -1,0 +1,237 @@
+// delta.hip — delta-stepping SSSP (Meyer & Sanders, J. Algorithms 2003) on gfx950 for
+// ShortestDistanceVertexProgram's converged distances (TGO_SSSP_DELTA).
+//
+// The reference program (ShortestDistanceVertexProgram.java:96-130) is a Jacobi
+// Bellman-Ford: every superstep every reached vertex re-sends its distance, so a run of
+// maxDepth supersteps relaxes every edge of the reached set up to maxDepth times.  With
+// non-negative integer weights the converged result is unique, so any relaxation order
+// reaches the same bit-exact distances; delta-stepping orders the work by distance buckets
+// of width delta so that most vertices are relaxed once, with their final distance.
+//
+// Device state per run:
+//   dist[v]   int64, atomicMin'd (global atomics execute at the memory side: coherent
+//             across the 8 XCDs' L2s)
+//   pend      bitmap: v improved and not yet relaxed with its current distance
+//   msg[v]    snapshot of dist[v] taken when v enters a phase queue; the phase relaxes from
+//             the snapshot, so a concurrent improvement of v (which sets pend again) never
+//             leaks into the phase half-seen — it simply queues v once more.
+// A phase relaxes the near queue (pending vertices with dist < thr) edge-balanced; a
+// vertex improved below thr whose pend bit was clear joins the next near queue at once;
+// the rest stay pending.  When the near queue runs dry, the host reads the minimum pending
+// distance, moves thr to the end of that bucket and extracts the next near queue from the
+// pending bitmap (a 2 MB scan at RMAT scale 24).
+#include <hip/hip_runtime.h>
+#include "engine.hpp"
+
+namespace tgo {
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kEdgesPerThread = 8;
+constexpr int kTileEdges = kBlock * kEdgesPerThread;
+constexpr int kLdsEntries = kTileEdges + 2;
+
+__device__ __forceinline__ int lane() { return static_cast<int>(threadIdx.x & 63); }
+
+__device__ __forceinline__ int64_t push_degree(const View& v, int64_t u) {
+    int64_t d = v.off0[u + 1] - v.off0[u];
+    if (v.nlists > 1) d += v.off1[u + 1] - v.off1[u];
+    return d;
+}
+
+// Wave-aggregated append to (qn, qdeg) and of the appended degrees to cnt->mf.
+__device__ __forceinline__ void append(bool take, int32_t v, int64_t deg, int32_t* qn, int64_t* qdeg, Counters* cnt) {
+    const unsigned long long mask = __ballot(take);
+    if (!mask) return;
+    const int leader = __ffsll(static_cast<long long>(mask)) - 1;
+    const int rank = __popcll(mask & ((1ULL << lane()) - 1ULL));
+    int64_t dsum = take ? deg : 0;
+    for (int off = 32; off > 0; off >>= 1) dsum += __shfl_xor(dsum, off, 64);
+    unsigned long long base = 0;
+    if (lane() == leader) {
+        base = atomicAdd(&cnt->qlen, static_cast<unsigned long long>(__popcll(mask)));
+        atomicAdd(&cnt->mf, static_cast<unsigned long long>(dsum));
+    }
+    base = __shfl(base, leader, 64);
+    if (take) {
+        qn[base + rank] = v;
+        qdeg[base + rank] = deg;
+    }
+}
+
+__global__ void ds_seed(View push, int64_t* dist, int32_t* q, int64_t* qdeg, int64_t seed) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        dist[seed] = 0;
+        q[0] = static_cast<int32_t>(seed);
+        qdeg[0] = push_degree(push, seed);
+    }
+}
+
+// Phase prologue: snapshot the queue's distances, clear their pending bits.
+__global__ void ds_commit(const int32_t* __restrict__ q, int64_t qlen, const int64_t* __restrict__ dist,
+                          int64_t* __restrict__ msg, uint64_t* __restrict__ pend) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < qlen; i += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t v = q[i];
+        msg[v] = dist[v];
+        const uint64_t bit = 1ULL << (v & 63);
+        if (pend[v >> 6] & bit) atomicAnd(reinterpret_cast<unsigned long long*>(&pend[v >> 6]), ~bit);
+    }
+}
+
+// Relax every push entry of the near queue (load-balanced search over the exclusive scan
+// of the queue's degrees, 2048 entries per 256-thread tile, queue slice staged in LDS).
+__global__ void __launch_bounds__(kBlock) ds_relax(View push, const int32_t* __restrict__ q,
+        const int64_t* __restrict__ qpre, int64_t qlen, const int64_t* __restrict__ msg,
+        int64_t* __restrict__ dist, uint64_t* __restrict__ pend, int32_t* __restrict__ qn,
+        int64_t* __restrict__ qdeg_n, Counters* cnt, int weighted, int64_t thr) {
+    __shared__ int64_t s_pre[kLdsEntries];
+    __shared__ int32_t s_q[kLdsEntries];
+    __shared__ int64_t s_lo, s_hi;
+    const int64_t total = qpre[qlen];
+    if (blockIdx.x == 0 && threadIdx.x == 0) cnt->red[1] = static_cast<unsigned long long>(total);   // work done
+    const int64_t ntiles = (total + kTileEdges - 1) / kTileEdges;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t t0 = tile * kTileEdges;
+        const int64_t t1 = min(total, t0 + kTileEdges);
+        if (threadIdx.x == 0) {
+            int64_t a = 0, b = qlen;
+            while (b - a > 1) { const int64_t c = (a + b) >> 1; if (qpre[c] <= t0) a = c; else b = c; }
+            s_lo = a;
+            int64_t a2 = a, b2 = qlen;
+            while (b2 - a2 > 1) { const int64_t c = (a2 + b2) >> 1; if (qpre[c] <= t1 - 1) a2 = c; else b2 = c; }
+            s_hi = a2;
+        }
+        __syncthreads();
+        const int64_t lo = s_lo, hi = s_hi;
+        const int64_t span = hi - lo + 1;
+        const bool in_lds = span + 1 <= kLdsEntries;
+        if (in_lds) {
+            for (int64_t i = threadIdx.x; i <= span; i += kBlock) {
+                s_pre[i] = qpre[lo + i];
+                if (i < span) s_q[i] = q[lo + i];
+            }
+        }
+        __syncthreads();
+        for (int k = 0; k < kEdgesPerThread; ++k) {
+            const int64_t j = t0 + k * kBlock + threadIdx.x;
+            bool take = false;
+            int32_t v = 0;
+            int64_t vdeg = 0;
+            if (j < t1) {
+                int32_t u; int64_t start;
+                if (in_lds) {
+                    int64_t a = 0, b = span;
+                    while (b - a > 1) { const int64_t c = (a + b) >> 1; if (s_pre[c] <= j) a = c; else b = c; }
+                    u = s_q[a]; start = s_pre[a];
+                } else {
+                    int64_t a = lo, b = hi + 1;
+                    while (b - a > 1) { const int64_t c = (a + b) >> 1; if (qpre[c] <= j) a = c; else b = c; }
+                    u = q[a]; start = qpre[a];
+                }
+                const int64_t o = j - start;
+                const int64_t b0 = push.off0[u];
+                const int64_t d0 = push.off0[u + 1] - b0;
+                int32_t w;
+                if (o < d0) { v = push.adj0[b0 + o]; w = push.w0 && weighted ? push.w0[b0 + o] : 1; }
+                else {
+                    const int64_t b1 = push.off1[u] + (o - d0);
+                    v = push.adj1[b1]; w = push.w1 && weighted ? push.w1[b1] : 1;
+                }
+                if (w == kMissingWeight) {
+                    atomicOr(&cnt->err, 1ULL);          // edge.value(weight) on a missing key
+                } else {
+                    const int64_t cand = msg[u] + static_cast<int64_t>(w);
+                    if (cand < dist[v]) {               // a stale (larger) read only costs an atomic
+                        const long long old = atomicMin(reinterpret_cast<long long*>(&dist[v]), static_cast<long long>(cand));
+                        if (cand < old) {
+                            const uint64_t bit = 1ULL << (v & 63);
+                            const unsigned long long ob = atomicOr(reinterpret_cast<unsigned long long*>(&pend[v >> 6]), bit);
+                            if (!(ob & bit) && cand < thr) { take = true; vdeg = push_degree(push, v); }
+                        }
+                    }
+                }
+            }
+            append(take, v, vdeg, qn, qdeg_n, cnt);
+        }
+        __syncthreads();
+    }
+}
+
+// Minimum distance over the pending vertices (into cnt->red[0], pre-set to INT64_MAX) and
+// their number (cnt->red[1]).
+__global__ void __launch_bounds__(kBlock) ds_pending_min(const uint64_t* __restrict__ pend, int64_t words,
+                                                         const int64_t* __restrict__ dist, Counters* cnt) {
+    unsigned long long mn = ~0ULL >> 1, count = 0;
+    for (int64_t wd = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; wd < words; wd += (int64_t)gridDim.x * blockDim.x) {
+        uint64_t b = pend[wd];
+        count += __popcll(b);
+        while (b) {
+            const int r = __ffsll(static_cast<long long>(b)) - 1;
+            b &= b - 1;
+            const unsigned long long d = static_cast<unsigned long long>(dist[(wd << 6) + r]);
+            mn = d < mn ? d : mn;
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_xor(mn, off, 64);
+        mn = o < mn ? o : mn;
+        count += __shfl_xor(count, off, 64);
+    }
+    if (lane() == 0) {
+        atomicMin(&cnt->red[0], mn);
+        atomicAdd(&cnt->red[1], count);
+    }
+}
+
+// Next near queue: pending vertices with dist < thr (one wave per 64-vertex word).
+__global__ void __launch_bounds__(kBlock) ds_extract(View push, uint64_t* __restrict__ pend, int64_t n,
+        const int64_t* __restrict__ dist, int64_t thr, int32_t* __restrict__ qn, int64_t* __restrict__ qdeg,
+        Counters* cnt) {
+    const int64_t words = (n + 63) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t wd = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; wd < words; wd += nwaves) {
+        const uint64_t b = pend[wd];                     // uniform across the wave
+        if (!b) continue;
+        const int64_t v = (wd << 6) + lane();
+        const bool take = ((b >> lane()) & 1ULL) && dist[v] < thr;
+        const unsigned long long tm = __ballot(take);
+        if (lane() == 0 && tm) pend[wd] = b & ~tm;       // one writer per word
+        append(take, static_cast<int32_t>(v), take ? push_degree(push, v) : 0, qn, qdeg, cnt);
+    }
+}
+
+inline int grid_for(int64_t work, int cap) {
+    int64_t g = (work + kBlock - 1) / kBlock;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return static_cast<int>(g);
+}
+
+}  // namespace
+
+hipError_t k_ds_seed(const View& push, int64_t* dist, int32_t* q, int64_t* qdeg, int64_t seed, hipStream_t s) {
+    ds_seed<<<1, 64, 0, s>>>(push, dist, q, qdeg, seed);
+    return hipGetLastError();
+}
+hipError_t k_ds_commit(const int32_t* q, int64_t qlen, const int64_t* dist, int64_t* msg, uint64_t* pend, hipStream_t s) {
+    ds_commit<<<grid_for(qlen, 2048), kBlock, 0, s>>>(q, qlen, dist, msg, pend);
+    return hipGetLastError();
+}
+hipError_t k_ds_relax(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen, const int64_t* msg,
+                      int64_t* dist, uint64_t* pend, int32_t* qn, int64_t* qdeg_n, Counters* cnt, int weighted,
+                      int64_t thr, hipStream_t s) {
+    ds_relax<<<256 * 8, kBlock, 0, s>>>(push, q, qpre, qlen, msg, dist, pend, qn, qdeg_n, cnt, weighted, thr);
+    return hipGetLastError();
+}
+hipError_t k_ds_pending_min(const uint64_t* pend, int64_t words, const int64_t* dist, Counters* cnt, hipStream_t s) {
+    ds_pending_min<<<grid_for(words, 1024), kBlock, 0, s>>>(pend, words, dist, cnt);
+    return hipGetLastError();
+}
+hipError_t k_ds_extract(const View& push, uint64_t* pend, int64_t n, const int64_t* dist, int64_t thr, int32_t* qn,
+                        int64_t* qdeg, Counters* cnt, hipStream_t s) {
+    const int64_t words = (n + 63) / 64;
+    ds_extract<<<grid_for(words * 64, 1 << 20), kBlock, 0, s>>>(push, pend, n, dist, thr, qn, qdeg, cnt);
+    return hipGetLastError();
+}
+
+}  // namespace tgo

@@ -103,6 +103,7 @@ struct DevGraph {
     bool has_transpose = false;
     bool has_weight = false;
     int32_t min_weight = 0;
+    double mean_weight = 1.0;   // over present weights (delta-stepping's default bucket width)
     int32_t scope = TGO_SCOPE_BOTH_E;
     bool partitioned = false;   // 1-D vertex partition: rows [lo, lo+n) of an n_global graph
     int64_t lo = 0, n_global = 0;
@@ -175,6 +176,16 @@ hipError_t k_sssp_relax(const View& push, const int32_t* q, const int64_t* qpre,
 hipError_t k_sssp_commit(const int32_t* q, int64_t qlen, const int64_t* dist, int64_t* msg,
                          uint64_t* mark, hipStream_t s);
 hipError_t k_dist_finalize(int64_t* dist, int64_t n, hipStream_t s);
+
+// SSSP (delta-stepping, converged distances) — delta.hip
+hipError_t k_ds_seed(const View& push, int64_t* dist, int32_t* q, int64_t* qdeg, int64_t seed, hipStream_t s);
+hipError_t k_ds_commit(const int32_t* q, int64_t qlen, const int64_t* dist, int64_t* msg, uint64_t* pend, hipStream_t s);
+hipError_t k_ds_relax(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen, const int64_t* msg,
+                      int64_t* dist, uint64_t* pend, int32_t* qn, int64_t* qdeg_n, Counters* cnt, int weighted,
+                      int64_t thr, hipStream_t s);
+hipError_t k_ds_pending_min(const uint64_t* pend, int64_t words, const int64_t* dist, Counters* cnt, hipStream_t s);
+hipError_t k_ds_extract(const View& push, uint64_t* pend, int64_t n, const int64_t* dist, int64_t thr, int32_t* qn,
+                        int64_t* qdeg, Counters* cnt, hipStream_t s);
 hipError_t k_unpermute_i64(const int64_t* in, const int32_t* perm, int64_t* out, int64_t n, hipStream_t s);
 hipError_t k_ms_seed(const int64_t* seeds, int nseeds, uint64_t* vis, uint64_t* fr, uint16_t* lvl, hipStream_t s);
 hipError_t k_ms_pull(const View& pull, const View& push, int64_t n_active, uint64_t full, const uint64_t* fr,

@@ -91,6 +91,7 @@ __global__ void ms_seed(const int64_t* __restrict__ seeds, int nseeds, uint64_t*
 // every still-unreached source of v is covered.  One vertex per lane; lists longer than
 // kCoop are OR-reduced by the whole wave.
 constexpr int64_t kCoop = 64;
+constexpr int kStep = 8;
 __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t n_active, uint64_t full,
         const uint64_t* __restrict__ fr, uint64_t* __restrict__ vis, uint64_t* __restrict__ nx,
         uint16_t* __restrict__ lvl, int32_t* __restrict__ qn, int64_t* __restrict__ qdeg,
@@ -112,11 +113,16 @@ __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t 
             for (int l = 0; l < 2 && (acc & open) != open; ++l) {
                 const int32_t* adj = l == 0 ? pull.adj0 : pull.adj1;
                 const int64_t e = l == 0 ? e0 : e1;
-                for (int64_t k = l == 0 ? b0 : b1; k < e && (acc & open) != open; k += 4) {
+                // kStep entries per dependent round trip: their index loads issue together,
+                // then their mask gathers (lists rarely cover every open source early)
+                for (int64_t k = l == 0 ? b0 : b1; k < e && (acc & open) != open; k += kStep) {
+                    int32_t u[kStep];
+#pragma unroll
+                    for (int j = 0; j < kStep; ++j) u[j] = k + j < e ? __builtin_nontemporal_load(adj + k + j) : -1;
                     uint64_t m = 0;
 #pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        if (k + j < e) m |= fr[adj[k + j]];
+                    for (int j = 0; j < kStep; ++j)
+                        if (u[j] >= 0) m |= fr[u[j]];
                     acc |= m;
                 }
             }
@@ -132,8 +138,17 @@ __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t 
                 const int64_t ee = __shfl(l == 0 ? e0 : e1, src, 64);
                 const int32_t* adj = l == 0 ? pull.adj0 : pull.adj1;
                 bool done = false;
-                for (int64_t k = bb; k < ee && !done; k += 64) {
-                    uint64_t m = k + lane() < ee ? fr[adj[k + lane()]] : 0;
+                for (int64_t k = bb; k < ee && !done; k += 4 * 64) {
+                    int32_t u[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int64_t x = k + j * 64 + lane();
+                        u[j] = x < ee ? __builtin_nontemporal_load(adj + x) : -1;
+                    }
+                    uint64_t m = 0;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        if (u[j] >= 0) m |= fr[u[j]];
                     for (int off = 32; off > 0; off >>= 1) m |= __shfl_xor(m, off, 64);
                     a |= m;
                     done = (a & want) == want;

@@ -59,6 +59,29 @@ struct WalkFinal {
     __device__ __forceinline__ void operator()(int64_t r, uint32_t sum) const { next[r] = static_cast<int32_t>(sum); }
 };
 
+// The index stream is read exactly once per superstep: load it non-temporally so it does
+// not evict the message vector from L2 / the Infinity Cache, which every gather re-reads.
+__device__ __forceinline__ int32_t stream_idx(const int32_t* p) { return __builtin_nontemporal_load(p); }
+
+constexpr int kPer = static_cast<int>(kTile / kBlock);   // entries per thread per tile (8)
+
+// Gather up to kTile messages of the entries [s0, s0+nnz) into registers: all kPer index
+// loads are issued first, then all kPer message loads, so every thread keeps kPer
+// independent gathers in flight (a dependent load per loop trip leaves the wave waiting
+// one memory latency per entry).
+template <class Op>
+__device__ __forceinline__ void gather_tile(const int32_t* __restrict__ adj, int64_t s0, int64_t nnz, const Op& op,
+                                            typename Op::T (&val)[kPer]) {
+    int32_t idx[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+        const int64_t k = threadIdx.x + static_cast<int64_t>(j) * kBlock;
+        idx[j] = k < nnz ? stream_idx(adj + s0 + k) : -1;
+    }
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) val[j] = idx[j] >= 0 ? op.load(idx[j]) : Op::zero();
+}
+
 template <class Op, class Fin>
 __global__ void __launch_bounds__(kBlock) gather_short(const int64_t* __restrict__ off,
         const int32_t* __restrict__ adj, const int64_t* __restrict__ blk, Op op, Fin fin) {
@@ -68,7 +91,15 @@ __global__ void __launch_bounds__(kBlock) gather_short(const int64_t* __restrict
     const int64_t s0 = off[r0], s1 = off[r1];
     const int64_t nnz = s1 - s0;
     if (nnz > kTile) return;                          // long row: handled by chunks
-    for (int64_t k = threadIdx.x; k < nnz; k += kBlock) s_val[k] = op.load(adj[s0 + k]);
+    {
+        T val[kPer];
+        gather_tile(adj, s0, nnz, op, val);
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+            const int k = threadIdx.x + j * kBlock;
+            if (k < nnz) s_val[k] = val[j];
+        }
+    }
     __syncthreads();
     const int64_t nrows = r1 - r0;
     if (nrows > 64) {
@@ -98,7 +129,12 @@ __global__ void __launch_bounds__(kBlock) gather_chunks(const int32_t* __restric
     __shared__ T s_w[kBlock / 64];
     const int64_t b = cbeg[blockIdx.x], e = cend[blockIdx.x];
     T sum = Op::zero();
-    for (int64_t k = b + threadIdx.x; k < e; k += kBlock) sum = Op::add(sum, op.load(adj[k]));
+    for (int64_t t = b; t < e; t += kTile) {          // chunks are <= kTile: one trip
+        T val[kPer];
+        gather_tile(adj, t, min(e - t, kTile), op, val);
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) sum = Op::add(sum, val[j]);
+    }
     sum = wave_sum(sum);
     if (lane() == 0) s_w[threadIdx.x >> 6] = sum;
     __syncthreads();

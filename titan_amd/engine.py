@@ -159,8 +159,12 @@ class Engine:
         _check(self.lib, self.ctx, self.lib.tgo_multi_stats(self.ctx, L.ptr(r, C.c_int64), L.ptr(e, C.c_int64)))
         return r, e
 
-    def sssp(self, seed, max_depth, scope, mode=L.SSSP_HOP_BOUNDED, seed_is_dense=False, stats=False, fetch=True):
-        a = L.SsspArgs(int(seed), 1 if seed_is_dense else 0, int(max_depth), scope, mode, 0,
+    def sssp(self, seed, max_depth, scope, mode=L.SSSP_HOP_BOUNDED, seed_is_dense=False, stats=False, fetch=True,
+             delta=0):
+        """ShortestDistanceVertexProgram.  HOP_BOUNDED: the reference's Jacobi supersteps
+        0..max_depth exactly; DELTA: delta-stepping to the converged distances (bucket width
+        `delta`, 0 = 2 x the mean weight)."""
+        a = L.SsspArgs(int(seed), 1 if seed_is_dense else 0, int(max_depth), scope, mode, int(delta),
                        L.FLAG_STATS if stats else 0, 0)
         out = np.zeros(self.n, dtype=np.int64) if fetch else None
         _check(self.lib, self.ctx, self.lib.tgo_sssp(self.ctx, C.byref(a), L.ptr(out, C.c_int64)))
