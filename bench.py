@@ -173,12 +173,15 @@ def run_single(args):
     edges_in = mR / 2.0                      # Graph500 undirected count for bothE
     teps = float(edges_in.sum()) * args.steps / float(bts.sum())
     # roofline of the multi-source sweep: every reached vertex's entries and offsets read
-    # once (4*E_R + 16*n_R) + the uint16 level row of every vertex written (128*n)
+    # once (4*E_R + 16*n_R) + the 64 levels of every vertex written once as P bit planes
+    # (P = bits of the deepest level: 8*P bytes per vertex)
     nR_u = int(nR.max())
     e_all = int(mR.max())
-    ms_bytes = 4.0 * e_all + 16.0 * nR_u + 128.0 * n
+    planes = max(1, int(bfs_eng.stats()["levels"]).bit_length())
+    ms_bytes = 4.0 * e_all + 16.0 * nR_u + 8.0 * planes * n
     roof_bfs = roofline("msbfs sweep (64 sources, all level launches)", ms_bytes / bks.mean() / 1e9,
-                        "4*E + 16*n_R + 128*n per 64-source sweep", "msbfs_sweep", ms_bytes)
+                        f"4*E + 16*n_R + 8*P*n per 64-source sweep (P = {planes} level bit planes)", "msbfs_sweep",
+                        ms_bytes)
     hmean = ss_hmean
     depth = np.array([depth0])
     upd = max(args.pr_iters - 1, 1)

@@ -580,6 +580,21 @@ int tgo_sssp(tgo_ctx* ctx, const tgo_sssp_args* a, int64_t* dist_out) {
 }
 
 // ------------------------------------------------------------------ multi-source BFS
+static LevelPlanes ms_planes(tgo_ctx* ctx) { return LevelPlanes{ctx->sc.ms_lvl, ctx->g.n}; }
+
+// Zero the level planes a discovery at `level` writes (planes 0..floor(log2(level))) that
+// this sweep has not zeroed yet: vertices reached earlier have levels < 2^k, whose bit k
+// is 0, so a plane is valid from the moment it is zeroed.
+static int ms_planes_for(tgo_ctx* ctx, int32_t level) {
+    Scratch& s = ctx->sc;
+    while (s.ms_nplanes < kLevelPlanes && (level >> s.ms_nplanes) != 0) {
+        HIP_TRY(hipMemsetAsync(s.ms_lvl + static_cast<int64_t>(s.ms_nplanes) * ctx->g.n, 0,
+                               ctx->g.n * sizeof(uint64_t), ctx->stream));
+        ++s.ms_nplanes;
+    }
+    return TGO_OK;
+}
+
 static int ms_alloc(tgo_ctx* ctx) {
     Scratch& s = ctx->sc;
     if (s.ms_vis) return TGO_OK;
@@ -587,7 +602,7 @@ static int ms_alloc(tgo_ctx* ctx) {
     HIP_TRY(dev_alloc(ctx, s.ms_vis, n + 1));
     HIP_TRY(dev_alloc(ctx, s.ms_fr, n + 1));
     HIP_TRY(dev_alloc(ctx, s.ms_nx, n + 1));
-    HIP_TRY(dev_alloc(ctx, s.ms_lvl, (n + 1) * TGO_MAX_SOURCES));
+    HIP_TRY(dev_alloc(ctx, s.ms_lvl, n * kLevelPlanes + 1));
     HIP_TRY(dev_alloc(ctx, s.ms_seeds, TGO_MAX_SOURCES));
     HIP_TRY(dev_alloc(ctx, s.ms_stat, 2 * TGO_MAX_SOURCES));
     ctx->st.device_bytes = ctx->dev_bytes;
@@ -622,8 +637,8 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
     HIP_TRY(hipMemcpyAsync(s.q[0], uniq.data(), uniq.size() * sizeof(int32_t), hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemsetAsync(s.ms_vis, 0, n * 8, st));
     HIP_TRY(hipMemsetAsync(s.ms_fr, 0, n * 8, st));
-    HIP_TRY(hipMemsetAsync(s.ms_lvl, 0xFF, n * TGO_MAX_SOURCES * sizeof(uint16_t), st));
-    HIP_TRY(k_ms_seed(s.ms_seeds, nseeds, s.ms_vis, s.ms_fr, s.ms_lvl, st));
+    s.ms_nplanes = 0;
+    HIP_TRY(k_ms_seed(s.ms_seeds, nseeds, s.ms_vis, s.ms_fr, st));
     HIP_TRY(k_degree_i64(push, s.q[0], static_cast<int64_t>(uniq.size()), s.qdeg, st));
     const uint64_t full = nseeds == 64 ? ~0ULL : ((1ULL << nseeds) - 1ULL);
     const int64_t total = pull.nlists > 1 ? g.out.nnz + g.in.nnz : (a->scope == TGO_SCOPE_IN_E ? g.out.nnz : g.in.nnz);
@@ -643,14 +658,15 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
     int cur = 0, levels = 0;
     for (int L = 0; L < depth && qlen > 0; ++L) {
         const bool use_pull = static_cast<double>(mf) * ms_alpha > static_cast<double>(total);
+        if ((rc = ms_planes_for(ctx, L + 1))) return rc;
         HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
         if (use_pull) {
-            HIP_TRY(k_ms_pull(pull, push, g.n_active, full, fr, s.ms_vis, nx, s.ms_lvl, s.q[cur ^ 1], s.qdeg, s.cnt, L + 1, st));
+            HIP_TRY(k_ms_pull(pull, push, g.n_active, full, fr, s.ms_vis, nx, ms_planes(ctx), s.q[cur ^ 1], s.qdeg, s.cnt, L + 1, st));
         } else {
             HIP_TRY(hipMemsetAsync(nx, 0, n * 8, st));
             if ((rc = scan_frontier(ctx, qlen))) return rc;
             HIP_TRY(k_ms_push(push, s.q[cur], s.qpre, qlen, fr, s.ms_vis, nx, st));
-            HIP_TRY(k_ms_settle(push, g.n_active, s.ms_vis, nx, s.ms_lvl, s.q[cur ^ 1], s.qdeg, s.cnt, L + 1, st));
+            HIP_TRY(k_ms_settle(push, g.n_active, s.ms_vis, nx, ms_planes(ctx), s.q[cur ^ 1], s.qdeg, s.cnt, L + 1, st));
         }
         if ((rc = read_counters(ctx))) return rc;
         qlen = static_cast<int64_t>(s.hcnt->qlen);
@@ -677,7 +693,7 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
     }
     if (dist_out)
         for (int r = 0; r < nseeds; ++r) {
-            HIP_TRY(k_ms_extract(s.ms_lvl, g.perm, r, s.msg, n, st));
+            HIP_TRY(k_ms_extract(ms_planes(ctx), s.ms_nplanes, s.ms_vis, g.perm, r, s.msg, n, st));
             HIP_TRY(hipMemcpyAsync(dist_out + static_cast<int64_t>(r) * n, s.msg, n * sizeof(int64_t),
                                    hipMemcpyDeviceToHost, st));
             HIP_TRY(hipStreamSynchronize(st));
@@ -691,7 +707,7 @@ int tgo_copy_multi_distances(tgo_ctx* ctx, int32_t source, int64_t* dist_out) {
     if (!ctx->loaded || !s.ms_vis) return fail(ctx, TGO_E_STATE, "no multi-source BFS has run");
     if (source < 0 || source >= s.ms_nsrc) return fail(ctx, TGO_E_INVALID, "source index out of range");
     (void)hipSetDevice(ctx->opts.device);
-    HIP_TRY(k_ms_extract(s.ms_lvl, ctx->g.perm, source, s.msg, ctx->g.n, ctx->stream));
+    HIP_TRY(k_ms_extract(ms_planes(ctx), s.ms_nplanes, s.ms_vis, ctx->g.perm, source, s.msg, ctx->g.n, ctx->stream));
     HIP_TRY(hipMemcpyAsync(dist_out, s.msg, ctx->g.n * sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     return TGO_OK;
@@ -963,10 +979,10 @@ int tgo_part_ms_begin(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, uint64
     HIP_TRY(hipEventRecord(ctx->ev0, st));
     HIP_TRY(hipMemsetAsync(s.ms_vis, 0, n * 8, st));
     HIP_TRY(hipMemsetAsync(fr_local, 0, n * 8, st));
-    HIP_TRY(hipMemsetAsync(s.ms_lvl, 0xFF, n * TGO_MAX_SOURCES * sizeof(uint16_t), st));
+    s.ms_nplanes = 0;
     // seeds owned elsewhere stay -1 (skipped by the seed kernel; their bit is set by the owner)
     HIP_TRY(hipMemcpyAsync(s.ms_seeds, local.data(), nseeds * sizeof(int64_t), hipMemcpyHostToDevice, st));
-    HIP_TRY(k_ms_seed(s.ms_seeds, nseeds, s.ms_vis, fr_local, s.ms_lvl, st));
+    HIP_TRY(k_ms_seed(s.ms_seeds, nseeds, s.ms_vis, fr_local, st));
     ctx->part_cur = 0;
     ctx->part_qlen = static_cast<int64_t>(uniq.size());
     int64_t mf = 0;
@@ -991,10 +1007,12 @@ int tgo_part_ms_pull(tgo_ctx* ctx, int32_t level, const uint64_t* fr_global, uin
     hipStream_t st = ctx->stream;
     const View pull = pull_view(g, TGO_SCOPE_BOTH_E), push = push_view(g, TGO_SCOPE_BOTH_E);
     const uint64_t full = s.ms_nsrc == 64 ? ~0ULL : ((1ULL << s.ms_nsrc) - 1ULL);
+    if (level + 1 >= (1 << kLevelPlanes)) return fail(ctx, TGO_E_UNSUPPORTED, "multi-source BFS levels are < 65536");
+    if ((rc = ms_planes_for(ctx, level + 1))) return rc;
     HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
     HIP_TRY(hipMemsetAsync(fr_next, 0, g.n * 8, st));
     const int nxt = ctx->part_cur ^ 1;
-    HIP_TRY(k_ms_pull(pull, push, g.n_active, full, fr_global, s.ms_vis, fr_next, s.ms_lvl, s.q[nxt], s.qdeg, s.cnt,
+    HIP_TRY(k_ms_pull(pull, push, g.n_active, full, fr_global, s.ms_vis, fr_next, ms_planes(ctx), s.q[nxt], s.qdeg, s.cnt,
                       level + 1, st));
     ctx->part_cur = nxt;
     return part_counts(ctx, counts);
@@ -1021,10 +1039,12 @@ int tgo_part_ms_settle(tgo_ctx* ctx, int32_t level, const uint64_t* recv, int32_
     DevGraph& g = ctx->g;
     Scratch& s = ctx->sc;
     hipStream_t st = ctx->stream;
+    if (level + 1 >= (1 << kLevelPlanes)) return fail(ctx, TGO_E_UNSUPPORTED, "multi-source BFS levels are < 65536");
+    if ((rc = ms_planes_for(ctx, level + 1))) return rc;
     HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
     HIP_TRY(k_or_slices(recv, nslices, g.n, fr_next, st));
     const int nxt = ctx->part_cur ^ 1;
-    HIP_TRY(k_ms_settle(push_view(g, TGO_SCOPE_BOTH_E), g.n, s.ms_vis, fr_next, s.ms_lvl, s.q[nxt], s.qdeg, s.cnt,
+    HIP_TRY(k_ms_settle(push_view(g, TGO_SCOPE_BOTH_E), g.n, s.ms_vis, fr_next, ms_planes(ctx), s.q[nxt], s.qdeg, s.cnt,
                         level + 1, st));
     ctx->part_cur = nxt;
     return part_counts(ctx, counts);
@@ -1060,7 +1080,7 @@ int tgo_part_ms_levels(tgo_ctx* ctx, int32_t source, int64_t* dist_local) {
     if (rc) return rc;
     Scratch& s = ctx->sc;
     if (!s.ms_vis || source < 0 || source >= s.ms_nsrc || !dist_local) return fail(ctx, TGO_E_INVALID, "bad source");
-    HIP_TRY(k_ms_extract(s.ms_lvl, ctx->g.perm, source, s.msg, ctx->g.n, ctx->stream));
+    HIP_TRY(k_ms_extract(ms_planes(ctx), s.ms_nplanes, s.ms_vis, ctx->g.perm, source, s.msg, ctx->g.n, ctx->stream));
     HIP_TRY(hipMemcpyAsync(dist_local, s.msg, ctx->g.n * sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     return TGO_OK;

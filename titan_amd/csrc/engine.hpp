@@ -111,6 +111,14 @@ struct DevGraph {
     bool rb_out_ready = false, rb_in_ready = false;
 };
 
+// Multi-source BFS levels as bit planes: the level of (v, source r) is
+// sum_k ((p[k * stride + v] >> r) & 1) << k; levels < 2^kLevelPlanes (uint16 range).
+constexpr int kLevelPlanes = 16;
+struct LevelPlanes {
+    uint64_t* p;
+    int64_t stride;
+};
+
 // Device scratch reused across programs (allocated on first use, sized for n).
 struct Counters {               // device-side level counters (one cache line each)
     unsigned long long qlen;    // next-queue length
@@ -145,7 +153,8 @@ struct Scratch {
     uint64_t* ms_vis = nullptr;     // n: reached-by mask
     uint64_t* ms_fr = nullptr;      // n: frontier mask
     uint64_t* ms_nx = nullptr;      // n: next-frontier mask
-    uint16_t* ms_lvl = nullptr;     // n * 64: level per (vertex, source), 0xFFFF = unreached
+    uint64_t* ms_lvl = nullptr;     // kLevelPlanes x n: bit r of plane k = bit k of source r's level
+    int32_t ms_nplanes = 0;         // planes zeroed (and valid) in the current sweep
     int64_t* ms_seeds = nullptr;    // 64
     unsigned long long* ms_stat = nullptr;   // 128: reached[64], entries[64]
     int32_t ms_nsrc = 0;
@@ -187,17 +196,18 @@ hipError_t k_ds_pending_min(const uint64_t* pend, int64_t words, const int64_t* 
 hipError_t k_ds_extract(const View& push, uint64_t* pend, int64_t n, const int64_t* dist, int64_t thr, int32_t* qn,
                         int64_t* qdeg, Counters* cnt, hipStream_t s);
 hipError_t k_unpermute_i64(const int64_t* in, const int32_t* perm, int64_t* out, int64_t n, hipStream_t s);
-hipError_t k_ms_seed(const int64_t* seeds, int nseeds, uint64_t* vis, uint64_t* fr, uint16_t* lvl, hipStream_t s);
+hipError_t k_ms_seed(const int64_t* seeds, int nseeds, uint64_t* vis, uint64_t* fr, hipStream_t s);
 hipError_t k_ms_pull(const View& pull, const View& push, int64_t n_active, uint64_t full, const uint64_t* fr,
-                     uint64_t* vis, uint64_t* nx, uint16_t* lvl, int32_t* qn, int64_t* qdeg, Counters* cnt,
+                     uint64_t* vis, uint64_t* nx, LevelPlanes lvl, int32_t* qn, int64_t* qdeg, Counters* cnt,
                      int32_t next_level, hipStream_t s);
 hipError_t k_ms_push(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen, const uint64_t* fr,
                      const uint64_t* vis, uint64_t* nx, hipStream_t s);
-hipError_t k_ms_settle(const View& push, int64_t n_active, uint64_t* vis, uint64_t* nx, uint16_t* lvl, int32_t* qn,
+hipError_t k_ms_settle(const View& push, int64_t n_active, uint64_t* vis, uint64_t* nx, LevelPlanes lvl, int32_t* qn,
                        int64_t* qdeg, Counters* cnt, int32_t next_level, hipStream_t s);
 hipError_t k_ms_reach(const View& v, const uint64_t* vis, int64_t n_active, int nsrc, unsigned long long* reached,
                       unsigned long long* entries, hipStream_t s);
-hipError_t k_ms_extract(const uint16_t* lvl, const int32_t* perm, int r, int64_t* dist, int64_t n, hipStream_t s);
+hipError_t k_ms_extract(LevelPlanes lvl, int nplanes, const uint64_t* vis, const int32_t* perm, int r, int64_t* dist,
+                        int64_t n, hipStream_t s);
 hipError_t k_or_slices(const uint64_t* recv, int nslices, int64_t n_local, uint64_t* out, hipStream_t s);
 hipError_t k_part_td_mark(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen,
                           uint64_t* disc, const uint64_t* vb_local, int64_t lo, int64_t n_local, hipStream_t s);

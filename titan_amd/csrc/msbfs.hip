@@ -9,8 +9,10 @@
 // so one pass over the adjacency serves every source whose frontier touches it — the
 // adjacency is read once per level instead of once per level per source.  Each source's
 // result is identical to its own single-source run (Jacobi: fr is the previous level's
-// snapshot), stored as uint16 levels in a [vertex][source] layout (one 128-byte row per
-// vertex, so the discoveries of a vertex are written into one cache line).
+// snapshot).  Levels are stored as bit planes (engine.hpp LevelPlanes): discovering the
+// sources `fresh` of v at level L ORs `fresh` into plane k of v for every set bit k of L —
+// at most log2(L)+1 coalesced 8-byte writes per vertex and level, and planes are zeroed
+// only when the sweep first reaches level 2^k.
 #include <hip/hip_runtime.h>
 #include "engine.hpp"
 
@@ -37,18 +39,15 @@ __device__ __forceinline__ int32_t view_entry(const View& v, int64_t u, int64_t 
     return o < d0 ? v.adj0[b0 + o] : v.adj1[v.off1[u] + (o - d0)];
 }
 
-// Record the level of every newly reached source of v; append v to the next queue.
-__device__ __forceinline__ void discover(int64_t v, uint64_t fresh, int32_t level, uint16_t* __restrict__ lvl,
+// Record the level of every newly reached source of v (bit k of the level goes into
+// plane k: one coalesced 8-byte OR per set level bit, the lane owns v); append v to the
+// next queue.
+__device__ __forceinline__ void discover(int64_t v, uint64_t fresh, int32_t level, LevelPlanes pl,
                                          const View& push, int32_t* qn, int64_t* qdeg, Counters* cnt) {
     const bool take = fresh != 0;
     if (take) {
-        uint16_t* row = lvl + v * kMaxSources;
-        uint64_t b = fresh;
-        while (b) {
-            const int r = __ffsll(static_cast<long long>(b)) - 1;
-            b &= b - 1;
-            row[r] = static_cast<uint16_t>(level);
-        }
+        for (int k = 0; k < kLevelPlanes && (level >> k); ++k)
+            if ((level >> k) & 1) pl.p[k * pl.stride + v] |= fresh;
     }
     const unsigned long long mask = __ballot(take);
     if (!mask) return;
@@ -74,15 +73,14 @@ __device__ __forceinline__ void discover(int64_t v, uint64_t fresh, int32_t leve
     }
 }
 
-__global__ void ms_seed(const int64_t* __restrict__ seeds, int nseeds, uint64_t* vis, uint64_t* fr,
-                        uint16_t* lvl) {
+// Level 0 is all-zero level bits: seeding only marks vis/fr.
+__global__ void ms_seed(const int64_t* __restrict__ seeds, int nseeds, uint64_t* vis, uint64_t* fr) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         for (int r = 0; r < nseeds; ++r) {
             const int64_t s = seeds[r];
             if (s < 0) continue;                 // partitioned: seed owned by another rank
             vis[s] |= 1ULL << r;
             fr[s] |= 1ULL << r;
-            lvl[s * kMaxSources + r] = 0;
         }
     }
 }
@@ -94,7 +92,7 @@ constexpr int64_t kCoop = 64;
 constexpr int kStep = 8;
 __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t n_active, uint64_t full,
         const uint64_t* __restrict__ fr, uint64_t* __restrict__ vis, uint64_t* __restrict__ nx,
-        uint16_t* __restrict__ lvl, int32_t* __restrict__ qn, int64_t* __restrict__ qdeg,
+        LevelPlanes lvl, int32_t* __restrict__ qn, int64_t* __restrict__ qdeg,
         Counters* cnt, int32_t next_level) {
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
     const int64_t words = (n_active + 63) >> 6;
@@ -221,7 +219,7 @@ __global__ void __launch_bounds__(kBlock) ms_push(View push, const int32_t* __re
 
 // After a push level: settle the candidates (nx & ~vis), record levels, build the queue.
 __global__ void __launch_bounds__(kBlock) ms_settle(View push, int64_t n_active, uint64_t* __restrict__ vis,
-        uint64_t* __restrict__ nx, uint16_t* __restrict__ lvl, int32_t* __restrict__ qn,
+        uint64_t* __restrict__ nx, LevelPlanes lvl, int32_t* __restrict__ qn,
         int64_t* __restrict__ qdeg, Counters* cnt, int32_t next_level) {
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
     const int64_t words = (n_active + 63) >> 6;
@@ -274,12 +272,18 @@ __global__ void __launch_bounds__(kBlock) ms_reach(View v, const uint64_t* __res
     }
 }
 
-// Source r's distances in row order: dist[v] = level of (perm[v], r).
-__global__ void ms_extract(const uint16_t* __restrict__ lvl, const int32_t* __restrict__ perm, int r,
-                           int64_t* __restrict__ dist, int64_t n) {
+// Source r's distances in row order: the level of (perm[v], r) read back from the planes
+// (nplanes = planes written by this sweep); unreached = r's bit clear in vis.
+__global__ void ms_extract(LevelPlanes lvl, int nplanes, const uint64_t* __restrict__ vis,
+                           const int32_t* __restrict__ perm, int r, int64_t* __restrict__ dist, int64_t n) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const uint16_t l = lvl[static_cast<int64_t>(perm[i]) * kMaxSources + r];
-        dist[i] = l == 0xFFFF ? INT64_MIN : static_cast<int64_t>(l);
+        const int64_t v = perm[i];
+        int64_t l = INT64_MIN;
+        if ((vis[v] >> r) & 1ULL) {
+            l = 0;
+            for (int k = 0; k < nplanes; ++k) l |= static_cast<int64_t>((lvl.p[k * lvl.stride + v] >> r) & 1ULL) << k;
+        }
+        dist[i] = l;
     }
 }
 
@@ -292,12 +296,12 @@ inline int grid_for(int64_t work, int cap) {
 
 }  // namespace
 
-hipError_t k_ms_seed(const int64_t* seeds, int nseeds, uint64_t* vis, uint64_t* fr, uint16_t* lvl, hipStream_t s) {
-    ms_seed<<<1, 64, 0, s>>>(seeds, nseeds, vis, fr, lvl);
+hipError_t k_ms_seed(const int64_t* seeds, int nseeds, uint64_t* vis, uint64_t* fr, hipStream_t s) {
+    ms_seed<<<1, 64, 0, s>>>(seeds, nseeds, vis, fr);
     return hipGetLastError();
 }
 hipError_t k_ms_pull(const View& pull, const View& push, int64_t n_active, uint64_t full, const uint64_t* fr,
-                     uint64_t* vis, uint64_t* nx, uint16_t* lvl, int32_t* qn, int64_t* qdeg, Counters* cnt,
+                     uint64_t* vis, uint64_t* nx, LevelPlanes lvl, int32_t* qn, int64_t* qdeg, Counters* cnt,
                      int32_t next_level, hipStream_t s) {
     ms_pull<<<grid_for(n_active, 1 << 20), kBlock, 0, s>>>(pull, push, n_active, full, fr, vis, nx, lvl, qn, qdeg, cnt,
                                                         next_level);
@@ -308,7 +312,7 @@ hipError_t k_ms_push(const View& push, const int32_t* q, const int64_t* qpre, in
     ms_push<<<256 * 8, kBlock, 0, s>>>(push, q, qpre, qlen, fr, vis, nx);
     return hipGetLastError();
 }
-hipError_t k_ms_settle(const View& push, int64_t n_active, uint64_t* vis, uint64_t* nx, uint16_t* lvl, int32_t* qn,
+hipError_t k_ms_settle(const View& push, int64_t n_active, uint64_t* vis, uint64_t* nx, LevelPlanes lvl, int32_t* qn,
                        int64_t* qdeg, Counters* cnt, int32_t next_level, hipStream_t s) {
     ms_settle<<<grid_for(n_active, 1 << 20), kBlock, 0, s>>>(push, n_active, vis, nx, lvl, qn, qdeg, cnt, next_level);
     return hipGetLastError();
@@ -322,8 +326,9 @@ hipError_t k_or_slices(const uint64_t* recv, int nslices, int64_t n_local, uint6
     or_slices<<<grid_for(n_local, 4096), kBlock, 0, s>>>(recv, nslices, n_local, out);
     return hipGetLastError();
 }
-hipError_t k_ms_extract(const uint16_t* lvl, const int32_t* perm, int r, int64_t* dist, int64_t n, hipStream_t s) {
-    ms_extract<<<grid_for(n, 4096), kBlock, 0, s>>>(lvl, perm, r, dist, n);
+hipError_t k_ms_extract(LevelPlanes lvl, int nplanes, const uint64_t* vis, const int32_t* perm, int r, int64_t* dist,
+                        int64_t n, hipStream_t s) {
+    ms_extract<<<grid_for(n, 4096), kBlock, 0, s>>>(lvl, nplanes, vis, perm, r, dist, n);
     return hipGetLastError();
 }
 
