@@ -57,6 +57,27 @@ int tgo_part_ms_end(tgo_ctx* ctx, int64_t* reached, int64_t* entries);
 /* Source `source`'s distances of the owned vertices (TGO_DIST_ABSENT = unreached). */
 int tgo_part_ms_levels(tgo_ctx* ctx, int32_t source, int64_t* dist_local);
 
+/* Partitioned delta-stepping SSSP (ShortestDistance converged distances over the loaded
+ * scope; weights when the partition was loaded with them).  Per phase:
+ *   tgo_part_sssp_relax  relaxes this rank's near queue; owned targets are updated in
+ *                        place, remote ones are packed per owner into `send` (device,
+ *                        capacity 2 * n_global int64: pairs {owner-local id, distance},
+ *                        rank-major) with send_counts[r] pairs for rank r (host array);
+ *   caller               all-to-all of the counts, then of the pairs (2 int64 each);
+ *   tgo_part_sssp_apply  mins the received pairs in and builds the next near queue.
+ * When every rank's near queue is empty: all-reduce(MIN) of tgo_part_sssp_pending_min's
+ * out[0] (INT64_MAX = nothing pending = done), move thr to the end of that bucket, and
+ * tgo_part_sssp_extract.  begin: out[0] = owned queue length, out[1] = the bucket width
+ * (delta, or the default when delta <= 0; ranks should agree on the maximum).
+ * counts = {next near-queue length, its push entries}.  Seeds are global ids. */
+int tgo_part_sssp_begin(tgo_ctx* ctx, int64_t seed_global, int64_t delta, int64_t* out);
+int tgo_part_sssp_relax(tgo_ctx* ctx, int64_t thr, int32_t nranks, int64_t* send, int64_t* send_counts);
+int tgo_part_sssp_apply(tgo_ctx* ctx, int64_t thr, const int64_t* recv, int64_t npairs, int64_t* counts);
+int tgo_part_sssp_pending_min(tgo_ctx* ctx, int64_t* out);
+int tgo_part_sssp_extract(tgo_ctx* ctx, int64_t thr, int64_t* counts);
+/* Local distances (TGO_DIST_ABSENT = unreached) and reached[2] = {vertices, pull entries}. */
+int tgo_part_sssp_end(tgo_ctx* ctx, int64_t* dist_local, int64_t* reached);
+
 int tgo_part_pr_begin(tgo_ctx* ctx, const tgo_pr_args* args, double* contrib_local);
 int tgo_part_pr_step(tgo_ctx* ctx, const double* contrib_global, double* contrib_local);
 int tgo_part_pr_end(tgo_ctx* ctx, double* pr_local);

@@ -108,6 +108,64 @@ def run_msbfs(backends, seeds, max_depth, ms_alpha=12.0):
     return levels, reached
 
 
+INT64_MAX = (1 << 63) - 1
+
+
+def run_sssp(backends, seed, delta):
+    """The distributed_sssp protocol with the collectives done in-process."""
+    world = len(backends)
+    n = backends[0].n_global
+    send = [b.tensor(2 * n, torch.int64) for b in backends]
+    recv = [b.tensor(2 * n, torch.int64) for b in backends]
+    st = [b.sssp_begin(seed, delta) for b in backends]
+    if delta <= 0:
+        delta = max(int(s[1]) for s in st)
+    q = [int(s[0]) for s in st]
+    thr = delta
+    while True:
+        if sum(q) == 0:
+            mn = min(int(b.sssp_pending_min()[0]) for b in backends)
+            if mn == INT64_MAX:
+                break
+            if mn >= thr:
+                thr = (mn // delta + 1) * delta
+            q = [int(b.sssp_extract(thr)[0]) for b in backends]
+            continue
+        sc = [b.sssp_relax(thr, send[i], world) for i, b in enumerate(backends)]
+        torch.cuda.synchronize()
+        npairs = []
+        for r in range(world):            # all_to_all_single: rank s's block r -> rank r
+            parts = [send[s][2 * int(sc[s][:r].sum()): 2 * int(sc[s][:r + 1].sum())] for s in range(world)]
+            cat = torch.cat(parts)
+            recv[r][:cat.numel()].copy_(cat)
+            npairs.append(cat.numel() // 2)
+        torch.cuda.synchronize()
+        q = [int(b.sssp_apply(thr, recv[r], npairs[r])[0]) for r, b in enumerate(backends)]
+    outs = [b.sssp_end(True) for b in backends]
+    return np.concatenate([o[0] for o in outs]), sum(o[1] for o in outs)
+
+
+@pytest.mark.parametrize("world,scope", [(2, L.SCOPE_IN_E), (4, L.SCOPE_OUT_E), (4, L.SCOPE_BOTH_E)])
+def test_partitioned_delta_stepping(world, scope):
+    scale = 12
+    n = 1 << scale
+    src, dst, w = rmat_edges(scale, 16, seed=35, weights=True)
+    backends = []
+    for r in range(world):
+        lo, hi = partition_range(n, world, r)
+        eng = Engine(stream=torch.cuda.current_stream().cuda_stream).load_partition(n, lo, hi, src, dst, scope,
+                                                                                    weight=w, apply_cap=False)
+        backends.append(HipPartBackend(eng, n, lo, hi))
+    og = fr.OracleGraph.from_edges(n, src, dst, w)
+    ids = (np.arange(n, dtype=np.int64) + 1) << 3
+    for seed in (int(src[0]), int(dst[9])):
+        od, _ = og.shortest_distance(int(ids[seed]), n, scope, weighted=True)
+        for delta in (0, 1, 1 << 40):
+            d, reached = run_sssp(backends, seed, delta)
+            assert np.array_equal(d, od), (seed, delta)
+            assert reached[0] == int((od != ABSENT).sum())
+
+
 @pytest.mark.parametrize("world", [2, 4])
 def test_partitioned_multi_source_bfs(world):
     scale = 12

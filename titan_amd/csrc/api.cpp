@@ -39,6 +39,8 @@ struct tgo_ctx {
     int64_t part_qlen = 0;      // its length
     double part_alpha = 0.85, part_base = 0.0;
     int32_t part_pr_iter = 0;
+    int64_t part_relaxed = 0;   // partitioned SSSP: entries relaxed, phases
+    int32_t part_phases = 0;
 };
 
 namespace {
@@ -336,6 +338,13 @@ int run_sssp(tgo_ctx* ctx, int64_t seed, int max_depth, int scope, bool weighted
     return TGO_OK;
 }
 
+// Bucket width when the caller passes 0: TGO_DELTA, else 2 x the mean edge weight.
+int64_t default_delta(const DevGraph& g, bool weighted) {
+    const double env = env_double("TGO_DELTA", 0.0);
+    if (env > 0) return static_cast<int64_t>(env);
+    return std::max<int64_t>(1, static_cast<int64_t>(weighted ? 2.0 * g.mean_weight : 1.0));
+}
+
 // Delta-stepping (delta.hip): converged distances, near queue relaxed phase by phase,
 // bucket threshold advanced from the minimum pending distance when the queue runs dry.
 int run_delta(tgo_ctx* ctx, int64_t seed, int scope, bool weighted, int64_t delta) {
@@ -344,10 +353,8 @@ int run_delta(tgo_ctx* ctx, int64_t seed, int scope, bool weighted, int64_t delt
     hipStream_t st = ctx->stream;
     const int64_t n = g.n, words = (n + 63) / 64 + 1;
     const View push = push_view(g, scope);
-    static const double delta_env = env_double("TGO_DELTA", 0.0);
     static const bool trace = env_double("TGO_TRACE", 0.0) != 0.0;
-    if (delta <= 0) delta = delta_env > 0 ? static_cast<int64_t>(delta_env)
-                                          : std::max<int64_t>(1, static_cast<int64_t>(weighted ? 2.0 * g.mean_weight : 1.0));
+    if (delta <= 0) delta = default_delta(g, weighted);
     HIP_TRY(k_fill_i64(s.dist, INT64_MAX, n, st));
     HIP_TRY(hipMemsetAsync(s.vb, 0, words * 8, st));        // pending bitmap
     int phases = 0, buckets = 0;
@@ -1123,6 +1130,163 @@ int tgo_part_pr_end(tgo_ctx* ctx, double* pr_local) {
     float ms = 0;
     HIP_TRY(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
     ctx->st.last_kernel_ms = ms;
+    return TGO_OK;
+}
+
+// ---- partitioned delta-stepping SSSP (delta.hip; exchange protocol: titan_amd/distributed.py)
+static int ds_part_alloc(tgo_ctx* ctx) {
+    Scratch& s = ctx->sc;
+    if (s.ds_rbest) return TGO_OK;
+    HIP_TRY(dev_alloc(ctx, s.ds_rbest, ctx->g.n_global));
+    HIP_TRY(dev_alloc(ctx, s.ds_rmark, ctx->g.n_global / 64 + 1));
+    HIP_TRY(dev_alloc(ctx, s.ds_pack, 3 * kMaxRanks));
+    return TGO_OK;
+}
+
+int tgo_part_sssp_begin(tgo_ctx* ctx, int64_t seed_global, int64_t delta, int64_t* out) {
+    int rc = part_check(ctx);
+    if (rc) return rc;
+    DevGraph& g = ctx->g;
+    if (g.has_weight && g.min_weight < 0) return fail(ctx, TGO_E_INVALID, "delta-stepping needs non-negative weights");
+    if ((rc = ds_part_alloc(ctx))) return rc;
+    Scratch& s = ctx->sc;
+    hipStream_t st = ctx->stream;
+    const int64_t n = g.n;
+    const View push = push_view(g, g.scope);
+    HIP_TRY(hipEventRecord(ctx->ev0, st));
+    HIP_TRY(k_fill_i64(s.dist, INT64_MAX, n, st));
+    HIP_TRY(hipMemsetAsync(s.vb, 0, ((n + 63) / 64 + 1) * 8, st));
+    HIP_TRY(k_fill_i64(s.ds_rbest, INT64_MAX, g.n_global, st));
+    HIP_TRY(hipMemsetAsync(s.ds_rmark, 0, (g.n_global / 64 + 1) * 8, st));
+    ctx->part_cur = 0;
+    ctx->part_qlen = 0;
+    ctx->part_relaxed = 0;
+    ctx->part_phases = 0;
+    const int64_t seed = seed_global - g.lo;
+    if (seed >= 0 && seed < n) {
+        HIP_TRY(k_ds_seed(push, s.dist, s.q[0], s.qdeg, seed, st));
+        ctx->part_qlen = 1;
+    }
+    HIP_TRY(hipStreamSynchronize(st));
+    if (out) {
+        out[0] = ctx->part_qlen;
+        out[1] = delta > 0 ? delta : default_delta(g, g.has_weight);
+    }
+    return TGO_OK;
+}
+
+int tgo_part_sssp_relax(tgo_ctx* ctx, int64_t thr, int32_t nranks, int64_t* send, int64_t* send_counts) {
+    int rc = part_check(ctx);
+    if (rc) return rc;
+    DevGraph& g = ctx->g;
+    Scratch& s = ctx->sc;
+    if (!s.ds_rbest) return fail(ctx, TGO_E_STATE, "tgo_part_sssp_begin has not run");
+    if (nranks < 1 || nranks > kMaxRanks || g.n * nranks != g.n_global || !send || !send_counts)
+        return fail(ctx, TGO_E_INVALID, "nranks * n_local must equal n_global (equal partitions, <= 64 ranks)");
+    hipStream_t st = ctx->stream;
+    const View push = push_view(g, g.scope);
+    HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
+    const int cur = ctx->part_cur;
+    if (ctx->part_qlen > 0) {
+        HIP_TRY(k_ds_commit(s.q[cur], ctx->part_qlen, s.dist, s.msg, s.vb, st));
+        if ((rc = scan_frontier(ctx, ctx->part_qlen))) return rc;
+        HIP_TRY(k_ds_relax_part(push, s.q[cur], s.qpre, ctx->part_qlen, s.msg, s.dist, s.vb, s.q[cur ^ 1], s.qdeg,
+                                s.cnt, g.has_weight ? 1 : 0, thr, g.lo, g.n, s.ds_rbest, s.ds_rmark, st));
+    }
+    unsigned long long* counts = s.ds_pack;
+    unsigned long long* offs = counts + kMaxRanks;
+    unsigned long long* cursor = offs + kMaxRanks;
+    HIP_TRY(hipMemsetAsync(counts, 0, 3 * kMaxRanks * sizeof(unsigned long long), st));
+    const int64_t words = g.n_global / 64, wpr = g.n / 64;
+    HIP_TRY(k_ds_mark_count(s.ds_rmark, words, wpr, counts, st));
+    unsigned long long h[kMaxRanks], ho[kMaxRanks];
+    HIP_TRY(hipMemcpyAsync(h, counts, nranks * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    unsigned long long acc = 0;
+    for (int r = 0; r < nranks; ++r) {
+        ho[r] = acc;
+        acc += h[r];
+        send_counts[r] = static_cast<int64_t>(h[r]);
+    }
+    HIP_TRY(hipMemcpyAsync(offs, ho, nranks * sizeof(unsigned long long), hipMemcpyHostToDevice, st));
+    HIP_TRY(k_ds_mark_pack(s.ds_rmark, words, wpr, g.n, s.ds_rbest, offs, cursor, send, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return TGO_OK;
+}
+
+int tgo_part_sssp_apply(tgo_ctx* ctx, int64_t thr, const int64_t* recv, int64_t npairs, int64_t* counts) {
+    int rc = part_check(ctx);
+    if (rc) return rc;
+    DevGraph& g = ctx->g;
+    Scratch& s = ctx->sc;
+    if (!s.ds_rbest) return fail(ctx, TGO_E_STATE, "tgo_part_sssp_begin has not run");
+    if (npairs < 0 || (npairs > 0 && !recv)) return fail(ctx, TGO_E_INVALID, "bad received pairs");
+    hipStream_t st = ctx->stream;
+    if (npairs > 0)
+        HIP_TRY(k_ds_apply(push_view(g, g.scope), recv, npairs, s.dist, s.vb, s.q[ctx->part_cur ^ 1], s.qdeg, s.cnt,
+                           thr, st));
+    if ((rc = read_counters(ctx))) return rc;
+    if (s.hcnt->err) return fail(ctx, TGO_E_PROGRAM,
+        "vertex program failed: a traversed edge has no value for the weight property");
+    if (ctx->part_qlen > 0) ctx->part_relaxed += static_cast<int64_t>(s.hcnt->red[1]);
+    ctx->part_cur ^= 1;
+    ctx->part_qlen = static_cast<int64_t>(s.hcnt->qlen);
+    ++ctx->part_phases;
+    if (counts) {
+        counts[0] = ctx->part_qlen;
+        counts[1] = static_cast<int64_t>(s.hcnt->mf);
+    }
+    return TGO_OK;
+}
+
+int tgo_part_sssp_pending_min(tgo_ctx* ctx, int64_t* out) {
+    int rc = part_check(ctx);
+    if (rc) return rc;
+    Scratch& s = ctx->sc;
+    if (!out) return fail(ctx, TGO_E_INVALID, "null output");
+    hipStream_t st = ctx->stream;
+    HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
+    HIP_TRY(hipMemsetAsync(&s.cnt->red[0], 0x7F, sizeof(unsigned long long), st));
+    HIP_TRY(k_ds_pending_min(s.vb, (ctx->g.n + 63) / 64, s.dist, s.cnt, st));
+    if ((rc = read_counters(ctx))) return rc;
+    out[1] = static_cast<int64_t>(s.hcnt->red[1]);
+    out[0] = out[1] ? static_cast<int64_t>(s.hcnt->red[0]) : INT64_MAX;
+    return TGO_OK;
+}
+
+int tgo_part_sssp_extract(tgo_ctx* ctx, int64_t thr, int64_t* counts) {
+    int rc = part_check(ctx);
+    if (rc) return rc;
+    DevGraph& g = ctx->g;
+    Scratch& s = ctx->sc;
+    hipStream_t st = ctx->stream;
+    HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
+    HIP_TRY(k_ds_extract(push_view(g, g.scope), s.vb, g.n, s.dist, thr, s.q[ctx->part_cur], s.qdeg, s.cnt, st));
+    return part_counts(ctx, counts);
+}
+
+int tgo_part_sssp_end(tgo_ctx* ctx, int64_t* dist_local, int64_t* reached) {
+    int rc = part_check(ctx);
+    if (rc) return rc;
+    DevGraph& g = ctx->g;
+    Scratch& s = ctx->sc;
+    hipStream_t st = ctx->stream;
+    HIP_TRY(k_dist_finalize(s.dist, g.n, st));
+    HIP_TRY(hipEventRecord(ctx->ev1, st));
+    if (reached) {
+        HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
+        HIP_TRY(k_reach_stats(pull_view(g, g.scope), s.dist, g.n, s.cnt->red, st));
+        if ((rc = read_counters(ctx))) return rc;
+        reached[0] = static_cast<int64_t>(s.hcnt->red[0]);
+        reached[1] = static_cast<int64_t>(s.hcnt->red[1]);
+    }
+    if (dist_local) HIP_TRY(hipMemcpyAsync(dist_local, s.dist, g.n * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+    ctx->st.last_kernel_ms = ms;
+    ctx->st.relaxed_entries = ctx->part_relaxed;
+    ctx->st.levels = ctx->part_phases;
     return TGO_OK;
 }
 

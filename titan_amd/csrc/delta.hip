@@ -1,5 +1,6 @@
 // delta.hip — delta-stepping SSSP (Meyer & Sanders, J. Algorithms 2003) on gfx950 for
-// ShortestDistanceVertexProgram's converged distances (TGO_SSSP_DELTA).
+// ShortestDistanceVertexProgram's converged distances (TGO_SSSP_DELTA), on one GPU or on a
+// 1-D vertex partition of the graph over several.
 //
 // The reference program (ShortestDistanceVertexProgram.java:96-130) is a Jacobi
 // Bellman-Ford: every superstep every reached vertex re-sends its distance, so a run of
@@ -20,6 +21,14 @@
 // the rest stay pending.  When the near queue runs dry, the host reads the minimum pending
 // distance, moves thr to the end of that bucket and extracts the next near queue from the
 // pending bitmap (a 2 MB scan at RMAT scale 24).
+//
+// Partitioned (titan_gpu_olap_part.h): the ctx holds the rows of global vertices
+// [lo, lo + n_local).  A relaxation whose target is owned elsewhere is min-reduced per
+// global target into rbest (int64 per global vertex) and marked in rmark (one bit per
+// global vertex); after the phase the marks are packed per owner rank into (owner-local
+// id, distance) pairs, the caller's all-to-all moves them, and the owner mins them into its
+// dist with the same pending / near-queue rule (ds_apply).  rbest lives for the whole run:
+// a target is re-sent only when this rank improves on what it sent before.
 #include <hip/hip_runtime.h>
 #include "engine.hpp"
 
@@ -59,6 +68,16 @@ __device__ __forceinline__ void append(bool take, int32_t v, int64_t deg, int32_
     }
 }
 
+// min(cand) into dist[v] of an owned vertex; true when v has to join the near queue.
+__device__ __forceinline__ bool relax_owned(int64_t* dist, uint64_t* pend, int64_t v, int64_t cand, int64_t thr) {
+    if (cand >= dist[v]) return false;                  // a stale (larger) read only costs an atomic
+    const long long old = atomicMin(reinterpret_cast<long long*>(&dist[v]), static_cast<long long>(cand));
+    if (cand >= old) return false;
+    const uint64_t bit = 1ULL << (v & 63);
+    const unsigned long long ob = atomicOr(reinterpret_cast<unsigned long long*>(&pend[v >> 6]), bit);
+    return !(ob & bit) && cand < thr;
+}
+
 __global__ void ds_seed(View push, int64_t* dist, int32_t* q, int64_t* qdeg, int64_t seed) {
     if (threadIdx.x == 0 && blockIdx.x == 0) {
         dist[seed] = 0;
@@ -80,10 +99,13 @@ __global__ void ds_commit(const int32_t* __restrict__ q, int64_t qlen, const int
 
 // Relax every push entry of the near queue (load-balanced search over the exclusive scan
 // of the queue's degrees, 2048 entries per 256-thread tile, queue slice staged in LDS).
+// kPart: targets outside [lo, lo + n_local) go to rbest / rmark (see the header).
+template <bool kPart>
 __global__ void __launch_bounds__(kBlock) ds_relax(View push, const int32_t* __restrict__ q,
         const int64_t* __restrict__ qpre, int64_t qlen, const int64_t* __restrict__ msg,
         int64_t* __restrict__ dist, uint64_t* __restrict__ pend, int32_t* __restrict__ qn,
-        int64_t* __restrict__ qdeg_n, Counters* cnt, int weighted, int64_t thr) {
+        int64_t* __restrict__ qdeg_n, Counters* cnt, int weighted, int64_t thr, int64_t lo, int64_t n_local,
+        int64_t* __restrict__ rbest, uint64_t* __restrict__ rmark) {
     __shared__ int64_t s_pre[kLdsEntries];
     __shared__ int32_t s_q[kLdsEntries];
     __shared__ int64_t s_lo, s_hi;
@@ -102,13 +124,13 @@ __global__ void __launch_bounds__(kBlock) ds_relax(View push, const int32_t* __r
             s_hi = a2;
         }
         __syncthreads();
-        const int64_t lo = s_lo, hi = s_hi;
-        const int64_t span = hi - lo + 1;
+        const int64_t lo_q = s_lo, hi_q = s_hi;
+        const int64_t span = hi_q - lo_q + 1;
         const bool in_lds = span + 1 <= kLdsEntries;
         if (in_lds) {
             for (int64_t i = threadIdx.x; i <= span; i += kBlock) {
-                s_pre[i] = qpre[lo + i];
-                if (i < span) s_q[i] = q[lo + i];
+                s_pre[i] = qpre[lo_q + i];
+                if (i < span) s_q[i] = q[lo_q + i];
             }
         }
         __syncthreads();
@@ -124,29 +146,39 @@ __global__ void __launch_bounds__(kBlock) ds_relax(View push, const int32_t* __r
                     while (b - a > 1) { const int64_t c = (a + b) >> 1; if (s_pre[c] <= j) a = c; else b = c; }
                     u = s_q[a]; start = s_pre[a];
                 } else {
-                    int64_t a = lo, b = hi + 1;
+                    int64_t a = lo_q, b = hi_q + 1;
                     while (b - a > 1) { const int64_t c = (a + b) >> 1; if (qpre[c] <= j) a = c; else b = c; }
                     u = q[a]; start = qpre[a];
                 }
                 const int64_t o = j - start;
                 const int64_t b0 = push.off0[u];
                 const int64_t d0 = push.off0[u + 1] - b0;
-                int32_t w;
-                if (o < d0) { v = push.adj0[b0 + o]; w = push.w0 && weighted ? push.w0[b0 + o] : 1; }
+                int32_t t, w;
+                if (o < d0) { t = push.adj0[b0 + o]; w = push.w0 && weighted ? push.w0[b0 + o] : 1; }
                 else {
                     const int64_t b1 = push.off1[u] + (o - d0);
-                    v = push.adj1[b1]; w = push.w1 && weighted ? push.w1[b1] : 1;
+                    t = push.adj1[b1]; w = push.w1 && weighted ? push.w1[b1] : 1;
                 }
+                const int64_t mu = msg[u];
                 if (w == kMissingWeight) {
                     atomicOr(&cnt->err, 1ULL);          // edge.value(weight) on a missing key
+                } else if (dist[u] < mu) {
+                    // u improved during this phase: it is pending again and will relax every
+                    // entry with the better distance, so this relaxation is wasted work
                 } else {
-                    const int64_t cand = msg[u] + static_cast<int64_t>(w);
-                    if (cand < dist[v]) {               // a stale (larger) read only costs an atomic
-                        const long long old = atomicMin(reinterpret_cast<long long*>(&dist[v]), static_cast<long long>(cand));
+                    const int64_t cand = mu + static_cast<int64_t>(w);
+                    const int64_t tl = kPart ? static_cast<int64_t>(t) - lo : static_cast<int64_t>(t);
+                    if (!kPart || (tl >= 0 && tl < n_local)) {
+                        if (relax_owned(dist, pend, tl, cand, thr)) {
+                            take = true;
+                            v = static_cast<int32_t>(tl);
+                            vdeg = push_degree(push, tl);
+                        }
+                    } else if (cand < rbest[t]) {
+                        const long long old = atomicMin(reinterpret_cast<long long*>(&rbest[t]), static_cast<long long>(cand));
                         if (cand < old) {
-                            const uint64_t bit = 1ULL << (v & 63);
-                            const unsigned long long ob = atomicOr(reinterpret_cast<unsigned long long*>(&pend[v >> 6]), bit);
-                            if (!(ob & bit) && cand < thr) { take = true; vdeg = push_degree(push, v); }
+                            const uint64_t bit = 1ULL << (t & 63);
+                            if (!(rmark[t >> 6] & bit)) atomicOr(reinterpret_cast<unsigned long long*>(&rmark[t >> 6]), bit);
                         }
                     }
                 }
@@ -157,8 +189,8 @@ __global__ void __launch_bounds__(kBlock) ds_relax(View push, const int32_t* __r
     }
 }
 
-// Minimum distance over the pending vertices (into cnt->red[0], pre-set to INT64_MAX) and
-// their number (cnt->red[1]).
+// Minimum distance over the pending vertices (into cnt->red[0], pre-set to a large value)
+// and their number (cnt->red[1]).
 __global__ void __launch_bounds__(kBlock) ds_pending_min(const uint64_t* __restrict__ pend, int64_t words,
                                                          const int64_t* __restrict__ dist, Counters* cnt) {
     unsigned long long mn = ~0ULL >> 1, count = 0;
@@ -200,6 +232,59 @@ __global__ void __launch_bounds__(kBlock) ds_extract(View push, uint64_t* __rest
     }
 }
 
+// Partitioned: marked remote targets per owner rank (rank r owns words [r*wpr, (r+1)*wpr)).
+__global__ void ds_mark_count(const uint64_t* __restrict__ rmark, int64_t words, int64_t wpr,
+                              unsigned long long* __restrict__ counts) {
+    for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < words; w += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t b = rmark[w];
+        if (b) atomicAdd(&counts[w / wpr], static_cast<unsigned long long>(__popcll(b)));
+    }
+}
+
+// Pack (owner-local id, distance) pairs rank-major from offs[r]; clears the marks.
+__global__ void ds_mark_pack(uint64_t* __restrict__ rmark, int64_t words, int64_t wpr, int64_t n_local,
+                             const int64_t* __restrict__ rbest, const unsigned long long* __restrict__ offs,
+                             unsigned long long* __restrict__ cursor, int64_t* __restrict__ send) {
+    for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < words; w += (int64_t)gridDim.x * blockDim.x) {
+        uint64_t b = rmark[w];
+        if (!b) continue;
+        rmark[w] = 0;
+        const int64_t r = w / wpr;
+        unsigned long long pos = offs[r] + atomicAdd(&cursor[r], static_cast<unsigned long long>(__popcll(b)));
+        while (b) {
+            const int k = __ffsll(static_cast<long long>(b)) - 1;
+            b &= b - 1;
+            const int64_t v = (w << 6) + k;
+            send[2 * pos] = v - r * n_local;
+            send[2 * pos + 1] = rbest[v];
+            ++pos;
+        }
+    }
+}
+
+// Owner side of the exchange: min the received (local id, distance) pairs into dist with
+// the pending / near-queue rule of ds_relax.
+__global__ void __launch_bounds__(kBlock) ds_apply(View push, const int64_t* __restrict__ recv, int64_t npairs,
+        int64_t* __restrict__ dist, uint64_t* __restrict__ pend, int32_t* __restrict__ qn,
+        int64_t* __restrict__ qdeg_n, Counters* cnt, int64_t thr) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < npairs; base += stride) {   // block-uniform trips
+        const int64_t i = base + threadIdx.x;
+        bool take = false;
+        int32_t v = 0;
+        int64_t vdeg = 0;
+        if (i < npairs) {
+            const int64_t vl = recv[2 * i];
+            if (relax_owned(dist, pend, vl, recv[2 * i + 1], thr)) {
+                take = true;
+                v = static_cast<int32_t>(vl);
+                vdeg = push_degree(push, vl);
+            }
+        }
+        append(take, v, vdeg, qn, qdeg_n, cnt);
+    }
+}
+
 inline int grid_for(int64_t work, int cap) {
     int64_t g = (work + kBlock - 1) / kBlock;
     if (g < 1) g = 1;
@@ -220,7 +305,15 @@ hipError_t k_ds_commit(const int32_t* q, int64_t qlen, const int64_t* dist, int6
 hipError_t k_ds_relax(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen, const int64_t* msg,
                       int64_t* dist, uint64_t* pend, int32_t* qn, int64_t* qdeg_n, Counters* cnt, int weighted,
                       int64_t thr, hipStream_t s) {
-    ds_relax<<<256 * 8, kBlock, 0, s>>>(push, q, qpre, qlen, msg, dist, pend, qn, qdeg_n, cnt, weighted, thr);
+    ds_relax<false><<<256 * 8, kBlock, 0, s>>>(push, q, qpre, qlen, msg, dist, pend, qn, qdeg_n, cnt, weighted, thr,
+                                              0, 0, nullptr, nullptr);
+    return hipGetLastError();
+}
+hipError_t k_ds_relax_part(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen, const int64_t* msg,
+                           int64_t* dist, uint64_t* pend, int32_t* qn, int64_t* qdeg_n, Counters* cnt, int weighted,
+                           int64_t thr, int64_t lo, int64_t n_local, int64_t* rbest, uint64_t* rmark, hipStream_t s) {
+    ds_relax<true><<<256 * 8, kBlock, 0, s>>>(push, q, qpre, qlen, msg, dist, pend, qn, qdeg_n, cnt, weighted, thr,
+                                             lo, n_local, rbest, rmark);
     return hipGetLastError();
 }
 hipError_t k_ds_pending_min(const uint64_t* pend, int64_t words, const int64_t* dist, Counters* cnt, hipStream_t s) {
@@ -231,6 +324,20 @@ hipError_t k_ds_extract(const View& push, uint64_t* pend, int64_t n, const int64
                         int64_t* qdeg, Counters* cnt, hipStream_t s) {
     const int64_t words = (n + 63) / 64;
     ds_extract<<<grid_for(words * 64, 1 << 20), kBlock, 0, s>>>(push, pend, n, dist, thr, qn, qdeg, cnt);
+    return hipGetLastError();
+}
+hipError_t k_ds_mark_count(const uint64_t* rmark, int64_t words, int64_t wpr, unsigned long long* counts, hipStream_t s) {
+    ds_mark_count<<<grid_for(words, 4096), kBlock, 0, s>>>(rmark, words, wpr, counts);
+    return hipGetLastError();
+}
+hipError_t k_ds_mark_pack(uint64_t* rmark, int64_t words, int64_t wpr, int64_t n_local, const int64_t* rbest,
+                          const unsigned long long* offs, unsigned long long* cursor, int64_t* send, hipStream_t s) {
+    ds_mark_pack<<<grid_for(words, 4096), kBlock, 0, s>>>(rmark, words, wpr, n_local, rbest, offs, cursor, send);
+    return hipGetLastError();
+}
+hipError_t k_ds_apply(const View& push, const int64_t* recv, int64_t npairs, int64_t* dist, uint64_t* pend, int32_t* qn,
+                      int64_t* qdeg_n, Counters* cnt, int64_t thr, hipStream_t s) {
+    ds_apply<<<grid_for(npairs, 4096), kBlock, 0, s>>>(push, recv, npairs, dist, pend, qn, qdeg_n, cnt, thr);
     return hipGetLastError();
 }
 

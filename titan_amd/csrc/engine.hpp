@@ -158,7 +158,13 @@ struct Scratch {
     int64_t* ms_seeds = nullptr;    // 64
     unsigned long long* ms_stat = nullptr;   // 128: reached[64], entries[64]
     int32_t ms_nsrc = 0;
+    // partitioned delta-stepping (allocated on first use)
+    int64_t* ds_rbest = nullptr;    // n_global: best distance sent to each remote vertex
+    uint64_t* ds_rmark = nullptr;   // n_global bits: remote vertices improved this phase
+    unsigned long long* ds_pack = nullptr;   // 3 x kMaxRanks: counts, offsets, cursors
 };
+
+constexpr int kMaxRanks = 64;
 
 // ---------------------------------------------------------------- kernel launchers (HIP)
 hipError_t k_fill_i32(int32_t* p, int32_t v, int64_t n, hipStream_t s);
@@ -195,6 +201,14 @@ hipError_t k_ds_relax(const View& push, const int32_t* q, const int64_t* qpre, i
 hipError_t k_ds_pending_min(const uint64_t* pend, int64_t words, const int64_t* dist, Counters* cnt, hipStream_t s);
 hipError_t k_ds_extract(const View& push, uint64_t* pend, int64_t n, const int64_t* dist, int64_t thr, int32_t* qn,
                         int64_t* qdeg, Counters* cnt, hipStream_t s);
+hipError_t k_ds_relax_part(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen, const int64_t* msg,
+                           int64_t* dist, uint64_t* pend, int32_t* qn, int64_t* qdeg_n, Counters* cnt, int weighted,
+                           int64_t thr, int64_t lo, int64_t n_local, int64_t* rbest, uint64_t* rmark, hipStream_t s);
+hipError_t k_ds_mark_count(const uint64_t* rmark, int64_t words, int64_t wpr, unsigned long long* counts, hipStream_t s);
+hipError_t k_ds_mark_pack(uint64_t* rmark, int64_t words, int64_t wpr, int64_t n_local, const int64_t* rbest,
+                          const unsigned long long* offs, unsigned long long* cursor, int64_t* send, hipStream_t s);
+hipError_t k_ds_apply(const View& push, const int64_t* recv, int64_t npairs, int64_t* dist, uint64_t* pend, int32_t* qn,
+                      int64_t* qdeg_n, Counters* cnt, int64_t thr, hipStream_t s);
 hipError_t k_unpermute_i64(const int64_t* in, const int32_t* perm, int64_t* out, int64_t n, hipStream_t s);
 hipError_t k_ms_seed(const int64_t* seeds, int nseeds, uint64_t* vis, uint64_t* fr, hipStream_t s);
 hipError_t k_ms_pull(const View& pull, const View& push, int64_t n_active, uint64_t full, const uint64_t* fr,

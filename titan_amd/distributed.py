@@ -106,6 +106,34 @@ class HipPartBackend:
         self.e.part_call("tgo_part_ms_levels", source, L.ptr(out, C.c_int64))
         return out
 
+    # delta-stepping SSSP local steps
+    def sssp_begin(self, seed, delta):
+        c = np.zeros(2, np.int64)
+        self.e.part_call("tgo_part_sssp_begin", C.c_int64(seed), C.c_int64(delta), L.ptr(c, C.c_int64))
+        return c
+
+    def sssp_relax(self, thr, send, nranks):
+        sc = np.zeros(nranks, np.int64)
+        self.e.part_call("tgo_part_sssp_relax", C.c_int64(thr), nranks, self._vp(send), L.ptr(sc, C.c_int64))
+        return sc
+
+    def sssp_apply(self, thr, recv, npairs):
+        return self._counts("tgo_part_sssp_apply", C.c_int64(thr), self._vp(recv), C.c_int64(npairs))
+
+    def sssp_pending_min(self):
+        c = np.zeros(2, np.int64)
+        self.e.part_call("tgo_part_sssp_pending_min", L.ptr(c, C.c_int64))
+        return c
+
+    def sssp_extract(self, thr):
+        return self._counts("tgo_part_sssp_extract", C.c_int64(thr))
+
+    def sssp_end(self, fetch=True, stats=True):
+        out = np.zeros(self.n_local, np.int64) if fetch else None
+        reached = np.zeros(2, np.int64) if stats else None
+        self.e.part_call("tgo_part_sssp_end", L.ptr(out, C.c_int64), L.ptr(reached, C.c_int64))
+        return out, reached
+
     def pr_begin(self, alpha, vertex_count, iters, contrib_local):
         a = L.PrArgs(alpha, int(vertex_count), int(iters), 0)
         self.e.part_call("tgo_part_pr_begin", C.byref(a), self._vp(contrib_local))
@@ -207,6 +235,56 @@ def distributed_msbfs(backend, seeds, max_depth: int, ms_alpha: float = 12.0, st
         t = t.cpu().numpy()
         r, e = t[:nseeds], t[nseeds:]
     return r, e, levels
+
+
+INT64_MAX = (1 << 63) - 1
+
+
+def distributed_sssp(backend, seed: int, delta: int = 0, fetch: bool = True, stats: bool = True, group=None):
+    """Delta-stepping ShortestDistance (converged distances) on a vertex-partitioned graph.
+      phase  : local relax of the owned near queue; improvements of remote vertices are
+               packed per owner -> all_to_all of the pair counts, all_to_all_single of the
+               (owner-local id, distance) pairs -> owners min them in and queue the ones
+               below the bucket threshold
+      bucket : when every near queue is empty, all_reduce(MIN) of the pending distances
+               moves the threshold to the end of the next non-empty bucket
+    Returns (local distances or None, global [reached vertices, entries] or None, phases)."""
+    world = dist.get_world_size(group)
+    dev = backend.device
+    n = backend.n_global
+    send = backend.tensor(2 * n, torch.int64)
+    recv = backend.tensor(2 * n, torch.int64)
+    qlen, dflt = (int(x) for x in backend.sssp_begin(seed, delta))
+    if delta <= 0:      # ranks' default widths differ with their local mean weight: agree on one
+        t = torch.tensor([dflt], dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        delta = int(t.item())
+    thr, phases = delta, 0
+    while True:
+        if int(_allreduce_counts([qlen, 0], dev)[0]) == 0:
+            mn = torch.tensor([int(backend.sssp_pending_min()[0])], dtype=torch.int64, device=dev)
+            dist.all_reduce(mn, op=dist.ReduceOp.MIN, group=group)
+            mn = int(mn.item())
+            if mn == INT64_MAX:
+                break
+            if mn >= thr:
+                thr = (mn // delta + 1) * delta
+            qlen = int(backend.sssp_extract(thr)[0])
+            continue
+        sc = backend.sssp_relax(thr, send, world)
+        sct = torch.from_numpy(2 * sc).to(dev)
+        rct = torch.empty_like(sct)
+        dist.all_to_all_single(rct, sct, group=group)
+        ins = [int(x) for x in 2 * sc]
+        outs = [int(x) for x in rct.cpu()]
+        dist.all_to_all_single(recv[:sum(outs)], send[:sum(ins)], output_split_sizes=outs, input_split_sizes=ins,
+                               group=group)
+        qlen = int(backend.sssp_apply(thr, recv, sum(outs) // 2)[0])
+        phases += 1
+    out, reached = backend.sssp_end(fetch, stats)
+    if stats:
+        reached = _allreduce_counts(reached, dev)
+    return out, reached, phases
 
 
 def distributed_pagerank(backend, alpha: float, vertex_count: int, iterations: int, fetch: bool = True,
