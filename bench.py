@@ -255,12 +255,14 @@ def run_partitioned(args, world, rank, local_rank):
     cap = int(2.3 * m / world) + (1 << 22)
     src = np.empty(cap, np.int32)
     dst = np.empty(cap, np.int32)
+    wgt = np.empty(cap, np.int32) if args.sssp_roots > 0 else None
     cnt = C.c_int64()
     rc = lib.tgo_rmat_partition(scale, args.edge_factor, 0x54495441, lo, hi, L.ptr(src, C.c_int32),
-                                L.ptr(dst, C.c_int32), None, cap, C.byref(cnt), 16)
+                                L.ptr(dst, C.c_int32), L.ptr(wgt, C.c_int32), cap, C.byref(cnt), 16)
     if rc:
         raise RuntimeError(f"tgo_rmat_partition rc={rc} count={cnt.value} cap={cap}")
     src, dst = src[:cnt.value], dst[:cnt.value]
+    wgt = wgt[:cnt.value] if wgt is not None else None
     log(f"rmat scale {scale} partition [{lo},{hi}) of {world}: {cnt.value} edges in {time.perf_counter() - t0:.1f}s")
     stream = torch.cuda.current_stream().cuda_stream
     t0 = time.perf_counter()
@@ -281,7 +283,7 @@ def run_partitioned(args, world, rank, local_rank):
     roots = [int(c) for c, k in zip(cand, okt.cpu().numpy()) if k > 0]
     roots = list(dict.fromkeys(roots))[:args.roots]
     # per-root reached entries (untimed) for GTEPS
-    _, mR, _ = distributed_msbfs(bfs_be, roots, n, stats=True)
+    _, mR, depth_ms = distributed_msbfs(bfs_be, roots, n, stats=True)
     # single-source side measurement (untimed, 8 roots, Graph500 style)
     ss_t = []
     for r in roots[:8]:
@@ -320,22 +322,66 @@ def run_partitioned(args, world, rank, local_rank):
     e_loc = torch.tensor([float(pr_eng.stats()["in_entries"])], dtype=torch.float64, device="cuda")
     dist.all_reduce(e_loc)
     e_in = int(e_loc.item())
+    planes = max(1, int(depth_ms).bit_length())      # level bit planes the sweeps wrote
+    del pr_be, pr_eng
+    sssp = None
+    if wgt is not None:
+        sssp = sssp_leg_partitioned(args, world, rank, local_rank, n, lo, hi, src, dst, wgt, roots, stream)
     if rank == 0:
         edges_in = mR / 2.0
         teps = float(edges_in.sum()) * args.steps / bfs_wall
         upd = max(args.pr_iters - 1, 1)
         # per-GPU algorithmic bytes over wall time (the exchange is inside the time)
-        bfs_bytes = (4.0 * float(mR.max()) + 16.0 * n + 128.0 * n) / world
+        bfs_bytes = (4.0 * float(mR.max()) + 16.0 * n + 8.0 * planes * n) / world
         roof_bfs = roofline("msbfs sweep per GPU (local kernels + RCCL exchange)", bfs_bytes * args.steps / bfs_wall / 1e9,
-                            "(4*E + 16*n + 128*n)/N per 64-source sweep per GPU")
+                            f"(4*E + 16*n + 8*P*n)/N per 64-source sweep per GPU (P = {planes} level bit planes)")
         pr_bytes = (4.0 * e_in + 32.0 * n) / world
         roof_pr = roofline("pagerank_update per GPU (gather + all-gather)", pr_bytes / (pr_wall / upd) / 1e9,
                            "(4*m + 32*n)/N per update per GPU")
         bfs_share = bfs_wall / (bfs_wall + pr_wall * args.steps)
-        print(json.dumps(result_line(args, world, scale, n, m, roots, elapsed, teps, hmean, pr_wall / upd, e_in,
-                                     roof_bfs, roof_pr, bfs_share, None, f"vertex-partition{world}")), flush=True)
+        line = result_line(args, world, scale, n, m, roots, elapsed, teps, hmean, pr_wall / upd, e_in,
+                           roof_bfs, roof_pr, bfs_share, None, f"vertex-partition{world}")
+        line["sssp"] = sssp
+        print(json.dumps(line), flush=True)
     dist.barrier()
     dist.destroy_process_group()
+
+
+def sssp_leg_partitioned(args, world, rank, local_rank, n, lo, hi, src, dst, wgt, roots, stream):
+    """configs[4] over N GPUs: delta-stepping SSSP on the vertex-partitioned weighted graph
+    (inE scope, no preload cap), per-owner relaxation exchange over RCCL
+    (titan_amd/distributed.distributed_sssp); roots whose reach is the giant component."""
+    import torch
+    import torch.distributed as dist
+    from titan_amd import Engine
+    from titan_amd import _lib as L
+    from titan_amd.distributed import HipPartBackend, distributed_sssp
+    eng = Engine(device=local_rank, host_threads=16, stream=stream).load_partition(n, lo, hi, src, dst, L.SCOPE_IN_E,
+                                                                                 weight=wgt, apply_cap=False)
+    be = HipPartBackend(eng, n, lo, hi)
+    res = []
+    for r in roots:
+        if len(res) == args.sssp_roots:
+            break
+        _, reached, _ = distributed_sssp(be, int(r), args.delta, fetch=False, stats=True)
+        if reached[0] * 4 < n:
+            continue
+        torch.cuda.synchronize()
+        dist.barrier()
+        t = time.perf_counter()
+        _, _, phases = distributed_sssp(be, int(r), args.delta, fetch=False, stats=False)
+        torch.cuda.synchronize()
+        wall = torch.tensor([time.perf_counter() - t], dtype=torch.float64, device="cuda")
+        dist.all_reduce(wall, op=dist.ReduceOp.MAX)
+        res.append((int(reached[1]), float(wall.item()), phases))
+    if not res:
+        return None
+    mR = np.array([x[0] for x in res], np.float64)
+    wall = np.array([x[1] for x in res])
+    return {"workload": f"rmat{int(math.log2(n))}-weighted-inE-delta-sssp-partitioned", "roots": len(res),
+            "gteps_hmean": round(len(res) / float(np.sum(wall / mR)) / 1e9, 4),
+            "ms_per_root": round(float(wall.mean()) * 1e3, 3), "reached_entries": int(mR.mean()),
+            "phases": int(np.mean([x[2] for x in res]))}
 
 
 def cpu_baseline(n, src, dst, roots, mR, depth, threads):

@@ -338,11 +338,13 @@ int run_sssp(tgo_ctx* ctx, int64_t seed, int max_depth, int scope, bool weighted
     return TGO_OK;
 }
 
-// Bucket width when the caller passes 0: TGO_DELTA, else 2 x the mean edge weight.
+// Bucket width when the caller passes 0: TGO_DELTA, else a quarter of the mean edge weight
+// (RMAT scale 24, weights 1..255: 39 ms at width 32 against 49 ms at 256 and 43 ms at one
+// bucket per 2048 — profiles/r01_sssp_delta_sweep.log).
 int64_t default_delta(const DevGraph& g, bool weighted) {
     const double env = env_double("TGO_DELTA", 0.0);
     if (env > 0) return static_cast<int64_t>(env);
-    return std::max<int64_t>(1, static_cast<int64_t>(weighted ? 2.0 * g.mean_weight : 1.0));
+    return std::max<int64_t>(1, static_cast<int64_t>(weighted ? 0.25 * g.mean_weight : 1.0));
 }
 
 // Delta-stepping (delta.hip): converged distances, near queue relaxed phase by phase,

@@ -163,7 +163,7 @@ class Engine:
              delta=0):
         """ShortestDistanceVertexProgram.  HOP_BOUNDED: the reference's Jacobi supersteps
         0..max_depth exactly; DELTA: delta-stepping to the converged distances (bucket width
-        `delta`, 0 = 2 x the mean weight)."""
+        `delta`, 0 = a quarter of the mean weight)."""
         a = L.SsspArgs(int(seed), 1 if seed_is_dense else 0, int(max_depth), scope, mode, int(delta),
                        L.FLAG_STATS if stats else 0, 0)
         out = np.zeros(self.n, dtype=np.int64) if fetch else None
