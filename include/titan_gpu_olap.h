@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define TGO_ABI_VERSION 1
+#define TGO_ABI_VERSION 2
 
 typedef struct tgo_ctx tgo_ctx;
 
@@ -54,7 +54,7 @@ typedef enum {
     TGO_E_CODEC = -4,       /* malformed edgestore entry (EdgeSerializer.parseRelation)  */
     TGO_E_STATE = -5,       /* call order violated (e.g. program before load)            */
     TGO_E_PROGRAM = -6,     /* vertex program failure: the reference throws in execute() */
-    TGO_E_UNSUPPORTED = -7, /* feature outside the implemented scope (e.g. vertex cuts)  */
+    TGO_E_UNSUPPORTED = -7, /* feature outside the implemented scope (e.g. Float weights)  */
     TGO_E_COMM = -8         /* multi-GPU exchange failure                                */
 } tgo_status;
 
@@ -209,6 +209,11 @@ typedef struct {
     int64_t device_bytes;         /* device memory held by the ctx                             */
     int64_t relaxed_entries;      /* push entries relaxed by the last SSSP (work done; equals
                                      reached_entries when every vertex is relaxed once)         */
+    /* vertex cuts (IDManager PartitionedVertex ids; VertexProgramScanJob.java:76-92) */
+    int64_t partitioned_vertices; /* canonical partitioned vertices executed                  */
+    int64_t partition_rows;       /* non-canonical representative rows folded into them       */
+    int64_t ghost_partition_rows; /* representative rows whose canonical row is absent or a
+                                     ghost (PartitionedVertexProgramExecutor "partition-ghost") */
 } tgo_stats;
 
 /* ---- Entry points ------------------------------------------------------------------- */

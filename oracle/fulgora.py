@@ -55,7 +55,9 @@ class FrLoadOpts(C.Structure):
 
 class FrLoadStats(C.Structure):
     _fields_ = [("ghost_vertices", C.c_int64), ("truncated_results", C.c_int64),
-                ("skipped_rows", C.c_int64), ("num_entries", C.c_int64)]
+                ("skipped_rows", C.c_int64), ("num_entries", C.c_int64),
+                ("partitioned_vertices", C.c_int64), ("partition_rows", C.c_int64),
+                ("ghost_partition_rows", C.c_int64)]
 
 
 _lib = None
@@ -91,6 +93,9 @@ def load() -> C.CDLL:
         "fr_key_of": (C.c_int64, [C.c_int64, C.c_int]),
         "fr_key_id": (C.c_int64, [C.c_int64, C.c_int]),
         "fr_is_invisible": (C.c_int, [C.c_int64]),
+        "fr_partitioned_vertex_id": (C.c_int64, [C.c_int64, C.c_int64, C.c_int]),
+        "fr_is_partitioned": (C.c_int, [C.c_int64, C.c_int]),
+        "fr_canonical_vertex_id": (C.c_int64, [C.c_int64, C.c_int]),
         "fr_write_relation_type": (None, [P(FrBuf), C.c_int64, C.c_int, C.c_int, C.c_int]),
         "fr_read_relation_type": (C.c_int, [_u8p, P(C.c_size_t), _i64p, P(C.c_int), P(C.c_int)]),
         "fr_encode_edge": (C.c_int, [P(FrBuf), _i32p, P(FrSchema), C.c_int64, C.c_int, C.c_int64,

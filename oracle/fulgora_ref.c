@@ -159,6 +159,23 @@ int64_t fr_key_id(int64_t key, int pb) {                                 /* getK
     return (id << 3) | suffix;
 }
 int fr_is_invisible(int64_t vid) { return (vid & 1) == 1; }              /* VertexIDType.Invisible 1b */
+/* Vertex cuts ("partitioned" vertices, VertexIDType.PartitionedVertex suffix 010b :78-90). */
+static int64_t partition_hash(int64_t id, int pb) {                      /* getPartitionHashForId :512-523 */
+    uint64_t r = 0;
+    for (int off = 0; off < 64; off += pb) r ^= ((uint64_t)id >> off) & ((1ULL << pb) - 1);
+    return (int64_t)r;
+}
+int64_t fr_partitioned_vertex_id(int64_t count, int64_t partition, int pb) {   /* constructId :432-441 */
+    return (((count << pb) + partition) << 3) | 2;
+}
+int fr_is_partitioned(int64_t vid, int pb) {                             /* isPartitionedVertex :557-559 */
+    return (vid & 7) == 2 && ((uint64_t)vid >> (pb + 3)) > 0;            /* + isUserVertexId :454-457 */
+}
+int64_t fr_canonical_vertex_id(int64_t vid, int pb) {                    /* getCanonicalVertexId :530-534 */
+    if (pb <= 0) return vid;                     /* no partition bits: one representative only */
+    int64_t count = (int64_t)((uint64_t)vid >> (pb + 3));
+    return fr_partitioned_vertex_id(count, partition_hash(count, pb), pb);   /* :525-528 */
+}
 
 /* ===================================================================== IDHandler */
 /* graphdb/database/idhandling/IDHandler.java */
@@ -377,6 +394,11 @@ struct fr_graph {
     int32_t* w;               /* E                                                */
     /* FulgoraVertexMemory's NonBlockingHashMapLong<VertexState>: Titan id -> index */
     int64_t* hkeys; int64_t* hvals; uint64_t hmask;
+    /* Vertex cuts: pv[v] = 1 for a canonical partitioned vertex.  Its canonical row's
+     * entries are [eoff[v], eoff[v+1]); every other representative row r of it (in scan
+     * order) is xr_beg[j]..xr_end[j] for j in [xr_off[v], xr_off[v+1]). NULL if none. */
+    uint8_t* pv;
+    int64_t* xr_off; int64_t* xr_beg; int64_t* xr_end;
 };
 
 static uint64_t mix64(uint64_t x) {
@@ -407,75 +429,150 @@ static inline int64_t lookup(const fr_graph* g, int64_t id) {            /* vert
 void fr_free(fr_graph* g) {
     if (!g) return;
     free(g->titan_id); free(g->eoff); free(g->other); free(g->edir); free(g->has_w); free(g->w);
-    free(g->hkeys); free(g->hvals); free(g);
+    free(g->hkeys); free(g->hvals);
+    free(g->pv); free(g->xr_off); free(g->xr_beg); free(g->xr_end); free(g);
 }
 int64_t fr_num_vertices(const fr_graph* g) { return g->n; }
 void fr_vertex_ids(const fr_graph* g, int64_t* out) { memcpy(out, g->titan_id, g->n * sizeof(int64_t)); }
-int64_t fr_num_entries(const fr_graph* g) { return g->eoff[g->n]; }
+/* Rows of vertex v: 0 = its own (canonical) row, 1.. = its other representative rows. */
+static inline int64_t nrows_of(const fr_graph* g, int64_t v) {
+    return 1 + (g->xr_off ? g->xr_off[v + 1] - g->xr_off[v] : 0);
+}
+static inline void row_range(const fr_graph* g, int64_t v, int64_t i, int64_t* b, int64_t* e) {
+    if (i == 0) { *b = g->eoff[v]; *e = g->eoff[v + 1]; return; }
+    int64_t j = g->xr_off[v] + i - 1;
+    *b = g->xr_beg[j]; *e = g->xr_end[j];
+}
+int64_t fr_num_entries(const fr_graph* g) {
+    int64_t e = 0;
+    for (int64_t v = 0; v < g->n; v++)
+        for (int64_t i = 0; i < nrows_of(g, v); i++) { int64_t b, x; row_range(g, v, i, &b, &x); e += x - b; }
+    return e;
+}
+
+/* Decode the kept user-edge entries of one row into g->other/edir/has_w/w from index *e. */
+static int decode_row_entries(const fr_rows* rows, int64_t r, const fr_schema* schema, const fr_load_opts* opts,
+                              int64_t limit, fr_graph* g, int64_t* e, fr_load_stats* st) {
+    int pb = opts->partition_bits;
+    int typed = opts->n_labels > 0;
+    const uint8_t* base = rows->entry_bytes + rows->row_byte_begin[r];
+    int64_t e0 = rows->row_entry_begin[r], e1 = rows->row_entry_begin[r + 1];
+    /* user-edge slice: column first byte in [0x60, 0x80) (IDHandler.getBounds :158-179) */
+    int64_t cnt = 0, first = -1;
+    for (int64_t k = e0; k < e1; k++) {
+        int64_t start = k == e0 ? 0 : (int64_t)((uint64_t)rows->entry_limit_valpos[k - 1] >> 32);
+        uint8_t c0 = base[start];
+        if (c0 >= 0x60 && c0 < 0x80) { if (first < 0) first = k; cnt++; }
+    }
+    if (limit != INT64_MAX && cnt >= limit) st->truncated_results++;    /* VertexJobConverter :125 */
+    int64_t keep = cnt < limit ? cnt : limit;
+    for (int64_t k = first; k >= 0 && k < first + keep; k++) {
+        int64_t start = k == e0 ? 0 : (int64_t)((uint64_t)rows->entry_limit_valpos[k - 1] >> 32);
+        int64_t end = (int64_t)((uint64_t)rows->entry_limit_valpos[k] >> 32);
+        int64_t vpos = rows->entry_limit_valpos[k] & 0x7FFFFFFF;
+        int64_t tid, oid, rid, wv = 0; int dr, hw;
+        int rc = fr_decode_edge(base + start, (size_t)(end - start), (size_t)vpos, schema,
+                                opts->weight_key, &tid, &dr, &oid, &rid, &hw, &wv);
+        if (rc) return rc;
+        if (typed) {
+            int ok = 0; for (int j = 0; j < opts->n_labels; j++) ok |= opts->label_ids[j] == tid;
+            if (!ok) continue;
+        }
+        /* messages are looked up by canonical id (VertexMemoryHandler.java:89) */
+        if (fr_is_partitioned(oid, pb)) oid = fr_canonical_vertex_id(oid, pb);
+        g->other[*e] = oid; g->edir[*e] = (uint8_t)dr; g->has_w[*e] = (uint8_t)hw; g->w[*e] = (int32_t)wv;
+        (*e)++;
+    }
+    return FR_OK;
+}
 
 int fr_load_rows(const fr_rows* rows, const fr_schema* schema, const fr_load_opts* opts,
                  fr_graph** out, fr_load_stats* stats) {
     /* VertexJobConverter.process/getKeyFilter/isGhostVertex (VertexJobConverter.java:109-171)
-     * + slice [0x60,0x80) with the QueryContainer limit (QueryContainer.java:110-134). */
-    fr_load_stats st = {0, 0, 0, 0};
+     * + slice [0x60,0x80) with the QueryContainer limit (QueryContainer.java:110-134).
+     * Vertex cuts: a non-canonical representative row skips the ghost check (:132); its
+     * messages are folded into the canonical vertex's aggregate (VertexProgramScanJob.java
+     * :76-92), which only executes if the canonical row was processed (setLoadedProperties
+     * :78-81; otherwise GHOTST_PARTITION_VERTEX, PartitionedVertexProgramExecutor.java:53-56). */
+    fr_load_stats st; memset(&st, 0, sizeof st);
     int pb = opts->partition_bits;
+    int64_t nr = rows->nrows;
     fr_graph* g = (fr_graph*)calloc(1, sizeof(fr_graph));
-    int64_t total = rows->row_entry_begin[rows->nrows];
-    g->titan_id = (int64_t*)malloc((rows->nrows + 1) * sizeof(int64_t));
-    g->eoff = (int64_t*)malloc((rows->nrows + 1) * sizeof(int64_t));
+    int64_t total = rows->row_entry_begin[nr];
+    g->titan_id = (int64_t*)malloc((nr + 1) * sizeof(int64_t));
+    g->eoff = (int64_t*)malloc((nr + 1) * sizeof(int64_t));
+    g->pv = (uint8_t*)calloc(nr + 1, 1);
     g->other = (int64_t*)malloc((total + 1) * sizeof(int64_t));
     g->edir = (uint8_t*)malloc(total + 1);
     g->has_w = (uint8_t*)malloc(total + 1);
     g->w = (int32_t*)malloc((total + 1) * sizeof(int32_t));
     int typed = opts->n_labels > 0;
     int64_t limit = (opts->apply_cap && !typed && opts->scope != FR_SCOPE_BOTH_E) ? opts->hard_query_limit : INT64_MAX;
-    int64_t n = 0, e = 0;
-    g->eoff[0] = 0;
-    for (int64_t r = 0; r < rows->nrows; r++) {
+    /* pass 1: which rows execute (0 = filtered, 1 = vertex row, 2 = representative row) */
+    int8_t* kind = (int8_t*)calloc(nr + 1, 1);
+    int64_t* rid = (int64_t*)malloc((nr + 1) * sizeof(int64_t));
+    int64_t n = 0, nrep = 0;
+    for (int64_t r = 0; r < nr; r++) {
         int64_t vid = fr_key_id(rows->row_keys[r], pb);
         if (fr_is_invisible(vid)) { st.skipped_rows++; continue; }       /* getKeyFilter :156-162 */
         int64_t sfx = vid & 7;
-        if (sfx == 2) { fr_free(g); return FR_E_UNSUPPORTED; }           /* partitioned (vertex cut) */
-        if (sfx != 0 && sfx != 4) { fr_free(g); return FR_E_CODEC; }     /* getUserVertexIDType */
+        if (sfx != 0 && sfx != 2 && sfx != 4) { fr_free(g); free(kind); free(rid); return FR_E_CODEC; }  /* getUserVertexIDType */
         const uint8_t* base = rows->entry_bytes + rows->row_byte_begin[r];
-        int64_t e0 = rows->row_entry_begin[r], e1 = rows->row_entry_begin[r + 1];
-        if (e1 <= e0) { fr_free(g); return FR_E_CODEC; }
+        if (rows->row_entry_begin[r + 1] <= rows->row_entry_begin[r]) { fr_free(g); free(kind); free(rid); return FR_E_CODEC; }
+        if (sfx == 2 && vid != fr_canonical_vertex_id(vid, pb)) {        /* isGhostVertex :132 */
+            kind[r] = 2; rid[r] = fr_canonical_vertex_id(vid, pb); nrep++;
+            continue;
+        }
         {   /* ghost check: first entry must be VertexExists (:131-137) */
             size_t pos = 0; int64_t tid; int ie, dr;
-            if (fr_read_relation_type(base, &pos, &tid, &ie, &dr)) { fr_free(g); return FR_E_CODEC; }
+            if (fr_read_relation_type(base, &pos, &tid, &ie, &dr)) { fr_free(g); free(kind); free(rid); return FR_E_CODEC; }
             if (ie || tid != fr_schema_id(1, 1)) { st.ghost_vertices++; continue; }
         }
-        /* user-edge slice: column first byte in [0x60, 0x80) (IDHandler.getBounds :158-179) */
-        int64_t cnt = 0, first = -1;
-        for (int64_t k = e0; k < e1; k++) {
-            int64_t start = k == e0 ? 0 : (int64_t)((uint64_t)rows->entry_limit_valpos[k - 1] >> 32);
-            uint8_t c0 = base[start];
-            if (c0 >= 0x60 && c0 < 0x80) { if (first < 0) first = k; cnt++; }
-        }
-        if (limit != INT64_MAX && cnt >= limit) st.truncated_results++;  /* :125 */
-        int64_t keep = cnt < limit ? cnt : limit;
-        for (int64_t k = first; k >= 0 && k < first + keep; k++) {
-            int64_t start = k == e0 ? 0 : (int64_t)((uint64_t)rows->entry_limit_valpos[k - 1] >> 32);
-            int64_t end = (int64_t)((uint64_t)rows->entry_limit_valpos[k] >> 32);
-            int64_t vpos = rows->entry_limit_valpos[k] & 0x7FFFFFFF;
-            int64_t tid, oid, rid, wv = 0; int dr, hw;
-            int rc = fr_decode_edge(base + start, (size_t)(end - start), (size_t)vpos, schema,
-                                    opts->weight_key, &tid, &dr, &oid, &rid, &hw, &wv);
-            if (rc) { fr_free(g); return rc; }
-            if (typed) {
-                int ok = 0; for (int j = 0; j < opts->n_labels; j++) ok |= opts->label_ids[j] == tid;
-                if (!ok) continue;
-            }
-            g->other[e] = oid; g->edir[e] = (uint8_t)dr; g->has_w[e] = (uint8_t)hw; g->w[e] = (int32_t)wv;
-            e++;
-        }
+        kind[r] = 1; rid[r] = vid;
         g->titan_id[n] = vid;
+        g->pv[n] = sfx == 2;
+        st.partitioned_vertices += sfx == 2;
         n++;
-        g->eoff[n] = e;
     }
     g->n = n;
-    st.num_entries = e;
     build_hash(g);
+    /* pass 2: entries of vertex rows, in row order; then the representative rows */
+    int64_t e = 0, v = 0;
+    g->eoff[0] = 0;
+    for (int64_t r = 0; r < nr; r++) {
+        if (kind[r] != 1) continue;
+        int rc = decode_row_entries(rows, r, schema, opts, limit, g, &e, &st);
+        if (rc) { fr_free(g); free(kind); free(rid); return rc; }
+        g->eoff[++v] = e;
+    }
+    if (nrep) {
+        int64_t* xv = (int64_t*)malloc(nrep * sizeof(int64_t));
+        int64_t* xb = (int64_t*)malloc(nrep * sizeof(int64_t));
+        int64_t* xe = (int64_t*)malloc(nrep * sizeof(int64_t));
+        int64_t j = 0;
+        for (int64_t r = 0; r < nr; r++) {
+            if (kind[r] != 2) continue;
+            int64_t owner = lookup(g, rid[r]);
+            if (owner < 0) { st.ghost_partition_rows++; continue; }
+            xv[j] = owner; xb[j] = e;
+            int rc = decode_row_entries(rows, r, schema, opts, limit, g, &e, &st);
+            if (rc) { free(xv); free(xb); free(xe); fr_free(g); free(kind); free(rid); return rc; }
+            xe[j] = e; j++;
+        }
+        st.partition_rows = j;
+        /* per-vertex CSR of representative rows, scan order kept */
+        g->xr_off = (int64_t*)calloc(n + 1, sizeof(int64_t));
+        g->xr_beg = (int64_t*)malloc((j + 1) * sizeof(int64_t));
+        g->xr_end = (int64_t*)malloc((j + 1) * sizeof(int64_t));
+        for (int64_t i = 0; i < j; i++) g->xr_off[xv[i] + 1]++;
+        for (int64_t u = 0; u < n; u++) g->xr_off[u + 1] += g->xr_off[u];
+        int64_t* pos = (int64_t*)malloc((n + 1) * sizeof(int64_t));
+        memcpy(pos, g->xr_off, (n + 1) * sizeof(int64_t));
+        for (int64_t i = 0; i < j; i++) { int64_t p = pos[xv[i]]++; g->xr_beg[p] = xb[i]; g->xr_end[p] = xe[i]; }
+        free(pos); free(xv); free(xb); free(xe);
+    }
+    free(kind); free(rid);
+    st.num_entries = e;
     *out = g;
     if (stats) *stats = st;
     return FR_OK;
@@ -487,6 +584,7 @@ int fr_load_adjacency(int64_t n, const int64_t* titan_ids, const int64_t* off, c
     int64_t E = off[n];
     g->n = n;
     g->titan_id = (int64_t*)malloc((n + 1) * sizeof(int64_t));
+    g->pv = (uint8_t*)calloc(n + 1, 1);
     g->eoff = (int64_t*)malloc((n + 1) * sizeof(int64_t));
     g->other = (int64_t*)malloc((E + 1) * sizeof(int64_t));
     g->edir = (uint8_t*)malloc(E + 1);
@@ -514,6 +612,7 @@ int fr_load_edges(int64_t n, int64_t m, const int32_t* src, const int32_t* dst, 
     fr_graph* g = (fr_graph*)calloc(1, sizeof(fr_graph));
     g->n = n;
     g->titan_id = (int64_t*)malloc((n + 1) * sizeof(int64_t));
+    g->pv = (uint8_t*)calloc(n + 1, 1);
     g->eoff = (int64_t*)calloc(n + 1, sizeof(int64_t));
     int64_t E = 2 * m;
     g->other = (int64_t*)malloc((E + 1) * sizeof(int64_t));
@@ -555,19 +654,23 @@ int fr_load_edges(int64_t n, int64_t m, const int32_t* src, const int32_t* dst, 
 int64_t fr_export(const fr_graph* g, int64_t* off, int64_t* mid, int32_t* adj, int32_t* w) {
     /* dense form with OUT entries first within each row (stable); entries whose other
      * endpoint is not an executed vertex are dropped: they can never carry a message
-     * (absent VertexState => EMPTY_STATE => null, FulgoraVertexMemory.java:49-58). */
+     * (absent VertexState => EMPTY_STATE => null, FulgoraVertexMemory.java:49-58).
+     * A vertex cut exports the union of its representative rows (canonical row first). */
     int64_t e = 0;
     off[0] = 0;
     for (int64_t v = 0; v < g->n; v++) {
         for (int pass = 0; pass < 2; pass++) {
             if (pass == 1) mid[v] = e;
-            for (int64_t k = g->eoff[v]; k < g->eoff[v + 1]; k++) {
-                if (g->edir[k] != pass) continue;
-                int64_t o = lookup(g, g->other[k]);
-                if (o < 0) continue;
-                adj[e] = (int32_t)o;
-                if (w) w[e] = g->has_w[k] ? g->w[k] : INT32_MIN;
-                e++;
+            for (int64_t i = 0; i < nrows_of(g, v); i++) {
+                int64_t kb, ke; row_range(g, v, i, &kb, &ke);
+                for (int64_t k = kb; k < ke; k++) {
+                    if (g->edir[k] != pass) continue;
+                    int64_t o = lookup(g, g->other[k]);
+                    if (o < 0) continue;
+                    adj[e] = (int32_t)o;
+                    if (w) w[e] = g->has_w[k] ? g->w[k] : INT32_MIN;
+                    e++;
+                }
             }
         }
         off[v + 1] = e;
@@ -611,6 +714,27 @@ typedef struct {
     volatile int failed;
     volatile int sent;           /* any message sent this superstep */
 } sd_t;
+/* The messages one row receives on the scope, reduced with min: execute()'s reduce
+ * (:109-110) for a vertex row, ShortestDistanceMessageCombiner (min, :17) for a
+ * representative row of a vertex cut (VertexProgramScanJob.java:82-90). */
+static int64_t sd_row_min(sd_t* s, const fr_graph* g, int64_t kb, int64_t ke) {
+    int64_t best = FR_ABSENT;
+    for (int64_t k = kb; k < ke; k++) {
+        if (!take(s->scope, g->edir[k])) continue;
+        int64_t o = lookup(g, g->other[k]);
+        if (o < 0) continue;
+        int64_t m = s->prev[o];
+        if (m == FR_ABSENT) continue;                                    /* filter(m != null) */
+        int64_t wt = 1;
+        if (s->weighted) {
+            if (!g->has_w[k]) { s->failed = 1; continue; }               /* edge.value(weight) throws */
+            wt = g->w[k];
+        }
+        int64_t c = (int64_t)((uint64_t)m + (uint64_t)wt);               /* Long + Integer, Java wrap */
+        if (best == FR_ABSENT || c < best) best = c;
+    }
+    return best;
+}
 static void sd_exec(void* p, const fr_graph* g, int64_t lo, int64_t hi) {
     sd_t* s = (sd_t*)p;
     for (int64_t v = lo; v < hi; v++) {
@@ -618,20 +742,19 @@ static void sd_exec(void* p, const fr_graph* g, int64_t lo, int64_t hi) {
             if (g->titan_id[v] == s->seed) { s->dist[v] = 0; s->cur[v] = 0; s->sent = 1; }
             continue;
         }
-        int64_t best = FR_ABSENT;                                        /* reduce(min).orElse(null) :109-110 */
-        for (int64_t k = g->eoff[v]; k < g->eoff[v + 1]; k++) {
-            if (!take(s->scope, g->edir[k])) continue;
-            int64_t o = lookup(g, g->other[k]);
-            if (o < 0) continue;
-            int64_t m = s->prev[o];
-            if (m == FR_ABSENT) continue;                                /* filter(m != null) */
-            int64_t wt = 1;
-            if (s->weighted) {
-                if (!g->has_w[k]) { s->failed = 1; continue; }           /* edge.value(weight) throws */
-                wt = g->w[k];
+        int64_t best = FR_ABSENT;
+        if (!g->pv[v]) {
+            best = sd_row_min(s, g, g->eoff[v], g->eoff[v + 1]);         /* reduce(min).orElse(null) :109-110 */
+        } else {
+            /* vertex cut: every representative row's combined message is aggregated with the
+             * combiner (FulgoraVertexMemory.aggregateMessage :138-140); execute() then runs once
+             * after the scan and receives only the aggregate (PartitionedVertexProgramExecutor
+             * :88-95, VertexMemoryHandler.Partition :126-135). */
+            for (int64_t i = 0; i < nrows_of(g, v); i++) {
+                int64_t kb, ke; row_range(g, v, i, &kb, &ke);
+                int64_t m = sd_row_min(s, g, kb, ke);
+                if (m != FR_ABSENT && (best == FR_ABSENT || m < best)) best = m;
             }
-            int64_t c = (int64_t)((uint64_t)m + (uint64_t)wt);           /* Long + Integer, Java wrap */
-            if (best == FR_ABSENT || c < best) best = c;
         }
         if (best == FR_ABSENT) continue;                                 /* :112-113 */
         if (s->dist[v] == FR_ABSENT || s->dist[v] > best) {             /* :117-122 */
@@ -671,7 +794,23 @@ typedef struct {
     double* pr; double* edge_count;
     /* two scopes (outE, inE): VertexState keeps Object[2]; NaN = null message */
     double* prev_out; double* prev_in; double* cur_out; double* cur_in;
+    volatile int failed;
 } pr_t;
+/* One scope's non-null messages on entries [kb,ke) of a row: sum added to *sum in entry
+ * order, count returned.  sel = the entry direction the reversed scope walks. */
+static int64_t pr_row(const fr_graph* g, const double* prev, int sel, int64_t kb, int64_t ke, double* sum) {
+    int64_t cnt = 0;
+    for (int64_t k = kb; k < ke; k++) {
+        if (g->edir[k] != sel) continue;
+        int64_t o = lookup(g, g->other[k]);
+        if (o < 0) continue;
+        double m = prev[o];
+        if (isnan(m)) continue;
+        *sum = *sum + m;
+        cnt++;
+    }
+    return cnt;
+}
 static void pr_exec(void* p, const fr_graph* g, int64_t lo, int64_t hi) {
     pr_t* s = (pr_t*)p;
     for (int64_t v = lo; v < hi; v++) {
@@ -679,21 +818,24 @@ static void pr_exec(void* p, const fr_graph* g, int64_t lo, int64_t hi) {
         /* receiveMessages(): concat(inE stream, outE stream) (VertexMemoryHandler :95-102);
          * reduce(0D, a+b) sequentially in that order. */
         double sum = 0.0;
-        for (int64_t k = g->eoff[v]; k < g->eoff[v + 1]; k++) {          /* inE scope: walk OUT entries */
-            if (g->edir[k] != 0) continue;
-            int64_t o = lookup(g, g->other[k]);
-            if (o < 0) continue;
-            double m = s->prev_in[o];
-            if (isnan(m)) continue;
-            sum = sum + m;
-        }
-        for (int64_t k = g->eoff[v]; k < g->eoff[v + 1]; k++) {          /* outE scope: walk IN entries */
-            if (g->edir[k] != 1) continue;
-            int64_t o = lookup(g, g->other[k]);
-            if (o < 0) continue;
-            double m = s->prev_out[o];
-            if (isnan(m)) continue;
-            sum = sum + m;
+        if (!g->pv[v]) {
+            pr_row(g, s->prev_in, 0, g->eoff[v], g->eoff[v + 1], &sum);  /* inE scope: walk OUT entries */
+            pr_row(g, s->prev_out, 1, g->eoff[v], g->eoff[v + 1], &sum); /* outE scope: walk IN entries */
+        } else {
+            /* vertex cut: PageRankVertexProgram has no combiner, so FulgoraUtil's
+             * ThrowingCombiner (:80-91) throws as soon as two messages of one scope meet,
+             * in one row (VertexProgramScanJob.java:84-87) or across rows
+             * (VertexState.addMessage :63-78); the failed row aborts the job
+             * (FulgoraGraphComputer.java:165-168).  One message per scope passes through. */
+            for (int sc = 0; sc < 2; sc++) {
+                int64_t tot = 0; double agg = 0.0;
+                for (int64_t i = 0; i < nrows_of(g, v); i++) {
+                    int64_t kb, ke; row_range(g, v, i, &kb, &ke);
+                    tot += pr_row(g, sc == 0 ? s->prev_in : s->prev_out, sc == 0 ? 0 : 1, kb, ke, &agg);
+                }
+                if (tot > 1) { s->failed = 1; break; }
+                sum = sum + agg;
+            }
         }
         if (s->iteration == 1) {                                         /* :78-83 */
             double init = 1.0 / (double)s->N;
@@ -722,6 +864,10 @@ int fr_pagerank(const fr_graph* g, double alpha, int64_t vertex_count, int max_i
     for (it = 0;; it++) {
         s.iteration = it;
         superstep(g, threads, &s, pr_exec);
+        if (s.failed) {
+            free(s.edge_count); free(s.prev_out); free(s.prev_in); free(s.cur_out); free(s.cur_in);
+            return FR_E_PROGRAM;
+        }
         double* t;
         t = s.prev_out; s.prev_out = s.cur_out; s.cur_out = t;
         t = s.prev_in; s.prev_in = s.cur_in; s.cur_in = t;
@@ -738,16 +884,30 @@ typedef struct {
     int iteration, length;
     int32_t* deg; int32_t* prev; int32_t* cur; uint8_t* prev_ok; uint8_t* cur_ok;
 } dc_t;
+/* DEG_MSG = inE: a row walks its OUT entries; messages summed as Java ints (wrap).  For a
+ * representative row of a vertex cut this is the ADDITION combiner (:337). */
+static uint32_t dc_row(const dc_t* s, const fr_graph* g, int64_t kb, int64_t ke, int* any) {
+    uint32_t sum = 0;
+    for (int64_t k = kb; k < ke; k++) {
+        if (g->edir[k] != 0) continue;
+        int64_t o = lookup(g, g->other[k]);
+        if (o < 0 || !s->prev_ok[o]) continue;
+        sum += (uint32_t)s->prev[o];
+        *any = 1;
+    }
+    return sum;
+}
 static void dc_exec(void* p, const fr_graph* g, int64_t lo, int64_t hi) {
     dc_t* s = (dc_t*)p;
     for (int64_t v = lo; v < hi; v++) {
         if (s->iteration == 0) { s->cur[v] = 1; s->cur_ok[v] = 1; continue; }   /* :358-359 */
         uint32_t sum = 0;                                                /* Java int, wraps (:361) */
-        for (int64_t k = g->eoff[v]; k < g->eoff[v + 1]; k++) {          /* DEG_MSG = inE: walk OUT */
-            if (g->edir[k] != 0) continue;
-            int64_t o = lookup(g, g->other[k]);
-            if (o < 0 || !s->prev_ok[o]) continue;
-            sum += (uint32_t)s->prev[o];
+        int any = 0;
+        /* a vertex cut sums each row's combined message into its aggregate (same Integer
+         * sum, FulgoraVertexMemory.aggregateMessage :138-140) and executes once on it */
+        for (int64_t i = 0; i < nrows_of(g, v); i++) {
+            int64_t kb, ke; row_range(g, v, i, &kb, &ke);
+            sum += dc_row(s, g, kb, ke, &any);
         }
         s->deg[v] = (int32_t)sum;                                        /* :362 */
         if (s->iteration < s->length) { s->cur[v] = (int32_t)sum; s->cur_ok[v] = 1; }   /* :363 */

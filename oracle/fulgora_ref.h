@@ -58,6 +58,9 @@ int64_t fr_schema_id(int type /*0=UserPropertyKey,1=SystemPropertyKey,2=UserEdge
 int64_t fr_vertex_id(int64_t count, int64_t partition, int partition_bits);     /* IDManager.constructId, NormalVertex */
 int64_t fr_key_of(int64_t vertex_id, int partition_bits);                       /* IDManager.getKey :461-473 */
 int64_t fr_key_id(int64_t key, int partition_bits);                             /* IDManager.getKeyID :476-486 */
+int64_t fr_partitioned_vertex_id(int64_t count, int64_t partition, int partition_bits); /* constructId, PartitionedVertex */
+int     fr_is_partitioned(int64_t vid, int partition_bits);                     /* isPartitionedVertex :557-559 */
+int64_t fr_canonical_vertex_id(int64_t vid, int partition_bits);                /* getCanonicalVertexId :530-534 */
 int     fr_is_invisible(int64_t vertex_id);
 
 /* Relation-type column prefix (IDHandler.writeRelationType, :88-94). dir: 0 OUT/property, 1 IN. */
@@ -106,7 +109,13 @@ typedef struct {
     int32_t scope; int32_t apply_cap; int64_t hard_query_limit;
     int32_t n_labels; const int64_t* label_ids; int64_t weight_key; int32_t partition_bits;
 } fr_load_opts;
-typedef struct { int64_t ghost_vertices, truncated_results, skipped_rows, num_entries; } fr_load_stats;
+typedef struct {
+    int64_t ghost_vertices, truncated_results, skipped_rows, num_entries;
+    int64_t partitioned_vertices;      /* canonical vertex-cut vertices executed              */
+    int64_t partition_rows;            /* non-canonical representative rows folded into them  */
+    int64_t ghost_partition_rows;      /* representative rows whose canonical row is absent or a ghost
+                                          (PartitionedVertexProgramExecutor GHOTST_PARTITION_VERTEX) */
+} fr_load_stats;
 
 int  fr_load_rows(const fr_rows* rows, const fr_schema* schema, const fr_load_opts* opts,
                   fr_graph** out, fr_load_stats* stats);

@@ -73,24 +73,52 @@ class GraphSpec:
     ghost_rows: list = field(default_factory=list)      # extra rows without VertexExists: (vid, edges as (dir, other_vid, label))
     schema_rows: int = 0                                # rows keyed by schema vertex ids (filtered)
     vids: list = None
+    # vertex cuts (vertex labels made with partition(), TitanPartitionGraphTest.java:291-321):
+    # their edges are stored on the representative in the other endpoint's partition
+    partitioned: list = field(default_factory=list)
+    pv_ghost: list = field(default_factory=list)       # partitioned vertices whose canonical row is absent
+
+
+def partitioned_vertex_id(count, pb=PB):
+    """Canonical id of a vertex cut (IDManager.getVertexID -> getCanonicalVertexIdFromCount, :500-528)."""
+    lib = fr.load()
+    return lib.fr_canonical_vertex_id(lib.fr_partitioned_vertex_id(count, 0, pb), pb)
+
+
+def representative(pvid, partition, pb=PB):
+    """IDManager.getPartitionedVertexId(pvid, partition) (:540-545)."""
+    return fr.load().fr_partitioned_vertex_id(pvid >> (pb + 3), partition, pb)
+
+
+def partition_of(vid, pb=PB):
+    return (vid >> 3) & ((1 << pb) - 1)
 
 
 def build_rows(spec: GraphSpec, schema: fr.OracleSchema, pb=PB, prop_types=None) -> tuple[Rows, np.ndarray]:
     prop_types = prop_types or {}
     vids = spec.vids if spec.vids is not None else [vertex_id(i, pb) for i in range(spec.n)]
-    per_row = {v: [] for v in vids}
+    pset = set(spec.partitioned)
+    vids = [partitioned_vertex_id(1000 + i, pb) if i in pset else v for i, v in enumerate(vids)]
+    per_row = {v: [] for i, v in enumerate(vids) if i not in set(spec.pv_ghost)}
     rel = 1000
     for i, v in enumerate(vids):
+        if i in set(spec.pv_ghost):
+            continue
         rel += 1
         per_row[v].append(fr.encode_vertex_exists(rel))
         for key, val in spec.vprops.get(i, []):
             rel += 1
             per_row[v].append(fr.encode_property(key, prop_types.get(key, 3), val, rel))
+
+    def placed(i, other_i):
+        # a vertex cut keeps the edge on its representative in the other endpoint's partition
+        return representative(vids[i], partition_of(vids[other_i], pb), pb) if i in pset else vids[i]
+
     for (s, d, label, props) in spec.edges:
         rel += 1
-        vs, vd = vids[s], vids[d]
-        per_row[vs].append(fr.encode_edge(schema, label, 0, vd, rel, props))
-        per_row[vd].append(fr.encode_edge(schema, label, 1, vs, rel, props))
+        vs, vd = placed(s, d), placed(d, s)
+        per_row.setdefault(vs, []).append(fr.encode_edge(schema, label, 0, vd, rel, props))
+        per_row.setdefault(vd, []).append(fr.encode_edge(schema, label, 1, vs, rel, props))
     for (gvid, gedges) in spec.ghost_rows:
         ents = []
         for (dr, other, label) in gedges:

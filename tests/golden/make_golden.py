@@ -213,10 +213,48 @@ def make_degree_random(num_v, name, seed):
     save(name, rows, vids, sd, degree1=np.asarray(degree1, np.int64), degree2=np.asarray(degree2, np.int64))
 
 
+def make_partition_groups(group_degrees=(10, 20, 30), ghost_degree=5):
+    """TitanPartitionGraphTest.setupGroupClusters (:291-321): each group vertex has a
+    partition() label (a vertex cut); person k of group i has member person->group and
+    contain group->person.  testVertexPartitionOlap (:395-435): DegreeCounter gives the
+    group degree for the partitioned vertices and 1 for every person.  One more vertex cut
+    whose canonical row is absent (its other representative rows stay) is joined by
+    `ghost_degree` persons of group 0; it never executes, so nothing changes for them."""
+    member, contain = es.user_edge_label(1), es.user_edge_label(2)
+    sd = schema_dict([{"type_id": member, "multiplicity": MULTI}, {"type_id": contain, "multiplicity": MULTI}], [])
+    edges, groups, group_of = [], [], []
+    v = 0
+    for deg in group_degrees:
+        g = v
+        groups.append(g)
+        group_of.append(-1)
+        v += 1
+        for _ in range(deg):
+            edges.append((v, g, member, []))
+            edges.append((g, v, contain, []))
+            group_of.append(g)
+            v += 1
+    ghost = v
+    group_of.append(-2)
+    v += 1
+    for k in range(ghost_degree):
+        edges.append((groups[0] + 1 + k, ghost, member, []))
+    spec = es.GraphSpec(n=v, edges=edges, partitioned=groups + [ghost], pv_ghost=[ghost])
+    rows, vids = es.build_rows(spec, oracle_schema(sd))
+    live = [i for i in range(v) if i != ghost]
+    degree1 = [group_degrees[groups.index(i)] if i in groups else 1 for i in live]
+    # bothE BFS from group 0: the group, then its members
+    bfs_g0 = [0 if i == groups[0] else (1 if group_of[i] == groups[0] else -1) for i in live]
+    save("partition_groups", rows, vids[live], sd, degree1=np.asarray(degree1, np.int64),
+         bfs_both_group0=np.asarray(bfs_g0, np.int64), group_index=np.asarray([live.index(g) for g in groups]),
+         ghost_vid=np.int64(vids[ghost]))
+
+
 if __name__ == "__main__":
     make_gotg()
     make_pagerank_tree()
     make_sssp_tree()
     make_degree_random(200, "degree_random", seed=7)
     make_degree_random(100, "degree_random100", seed=11)
+    make_partition_groups()
     print("fixtures written to", HERE)

@@ -377,3 +377,65 @@ def test_errors_are_reported():
         eng.pagerank(0.85, 6, 3)            # PageRank needs a single-direction preload
     with pytest.raises(TitanException):
         eng.bfs(0, 3, IN)                   # scope differs from the preloaded one
+
+
+# ----------------------------------------------------------------------------- vertex cuts
+def test_partition_groups_degree_and_bfs():
+    """TitanPartitionGraphTest.testVertexPartitionOlap (:395-435) on the device: DegreeCounter
+    gives the group degree at each vertex cut and 1 for every person."""
+    eng, rows, vids, sd, npz = engine_from_fixture("partition_groups", IN)
+    o = oracle_from_fixture("partition_groups", IN)
+    st = eng.stats()
+    assert st["partitioned_vertices"] == o.stats.partitioned_vertices == 3
+    assert st["partition_rows"] == o.stats.partition_rows
+    assert st["ghost_partition_rows"] == o.stats.ghost_partition_rows > 0
+    assert sorted(eng.vertex_ids().tolist()) == sorted(int(v) for v in vids)
+    assert np.array_equal(reorder(eng.vertex_ids(), eng.walkcount(1), vids), npz["degree1"])
+    with pytest.raises(TitanException) as ei:            # no combiner: ThrowingCombiner (FulgoraUtil.java:80-91)
+        eng.pagerank(0.85, len(vids), 3)
+    assert ei.value.code == L.TGO_E_PROGRAM
+    eb, _, _, _, _ = engine_from_fixture("partition_groups", BOTH)
+    g0 = int(vids[int(npz["group_index"][0])])
+    d = reorder(eb.vertex_ids(), eb.bfs(g0, 10, BOTH), vids)
+    assert np.array_equal(np.where(d == ABSENT, -1, d), npz["bfs_both_group0"])
+
+
+def test_partitioned_hubs_match_oracle():
+    """Random weighted graph whose hubs are vertex cuts (edges spread over representative rows,
+    each row capped on its own): every program bit-exact against the oracle's Fulgora restatement."""
+    import random
+    import edgestore as es
+    rnd = random.Random(5)
+    knows = es.user_edge_label(1)
+    wkey = es.user_property_key(1)
+    sd = {"edge_types": [{"type_id": knows, "multiplicity": 0, "signature": [wkey]}], "property_keys": [[wkey, 3]]}
+    osch = fr.OracleSchema(sd["edge_types"], [tuple(x) for x in sd["property_keys"]])
+    n = 600
+    edges = [(rnd.randrange(n), rnd.randrange(n), knows, [(wkey, rnd.randint(1, 20))]) for _ in range(6000)]
+    for hub in (0, 1, 2):
+        edges += [(hub, rnd.randrange(n), knows, [(wkey, rnd.randint(1, 20))]) for _ in range(150)]
+        edges += [(rnd.randrange(n), hub, knows, [(wkey, rnd.randint(1, 20))]) for _ in range(150)]
+    rows, vids = es.build_rows(es.GraphSpec(n=n, edges=edges, partitioned=[0, 1, 2, 3, 9]), osch)
+    for scope in (IN, OUT, BOTH):
+        o = fr.OracleGraph.from_rows(rows, osch, scope, hard_limit=12, weight_key=wkey)
+        eng = Engine(hard_query_limit=12).load_rows(rows, Schema.from_dict(sd), scope, weight_key=wkey, batch_rows=64)
+        ids = eng.vertex_ids()
+        assert np.array_equal(ids, o.vertex_ids())
+        st = eng.stats()
+        assert (st["partitioned_vertices"], st["partition_rows"], st["truncated_results"]) == \
+            (o.stats.partitioned_vertices, o.stats.partition_rows, o.stats.truncated_results)
+        for r in (0, 3, 17):
+            seed = int(vids[r])
+            assert np.array_equal(eng.bfs(seed, n, scope), o.shortest_distance(seed, n, scope)[0])
+            for depth in (3, n):
+                assert np.array_equal(eng.sssp(seed, depth, scope),
+                                      o.shortest_distance(seed, depth, scope, weighted=True)[0])
+            conv = o.shortest_distance(seed, n, scope, weighted=True)[0]
+            assert np.array_equal(eng.sssp(seed, n, scope, mode=L.SSSP_DELTA), conv)
+        if scope == IN:
+            assert np.array_equal(eng.walkcount(3), o.degree_counter(3)[0])
+        if scope != BOTH:
+            with pytest.raises(TitanException):
+                eng.pagerank(0.85, n, 4)
+            with pytest.raises(RuntimeError):
+                o.pagerank(0.85, n, 4)

@@ -124,3 +124,63 @@ def test_cap_keeps_out_entries_first():
     outdeg_full = mf - of[:-1]
     outdeg_cap = mc - oc[:-1]
     assert np.array_equal(outdeg_cap, np.minimum(outdeg_full, 50))
+
+
+# ----------------------------------------------------------------------------- vertex cuts
+def test_partitioned_vertices_degree_counter():
+    # TitanPartitionGraphTest.testVertexPartitionOlap (:395-435): DegreeCounter over vertex
+    # cuts gives the group degree for the partitioned vertex and 1 for every person.
+    g, vids, npz = oracle_graph("partition_groups", SCOPE_IN)
+    assert g.stats.partitioned_vertices == 3
+    assert g.stats.partition_rows > 3            # the group edges spread over many representatives
+    assert g.stats.ghost_partition_rows > 0      # the cut whose canonical row is absent
+    assert sorted(int(v) for v in g.vertex_ids()) == sorted(int(v) for v in vids)
+    d, it = g.degree_counter(1)
+    assert it == 1
+    assert np.array_equal(by_vid(g, vids, d), npz["degree1"])
+
+
+def test_partitioned_vertices_bfs_and_canonical_ids():
+    g, vids, npz = oracle_graph("partition_groups", SCOPE_BOTH)
+    lib = fr.load()
+    group0 = int(vids[int(npz["group_index"][0])])
+    assert lib.fr_is_partitioned(group0, 5) and lib.fr_canonical_vertex_id(group0, 5) == group0
+    d, _ = g.shortest_distance(group0, 10, SCOPE_BOTH)
+    d = by_vid(g, vids, d)
+    assert np.array_equal(np.where(d == ABSENT, -1, d), npz["bfs_both_group0"])
+
+
+def test_partitioned_vertices_pagerank_needs_a_combiner():
+    # PageRankVertexProgram defines no combiner: two messages meeting at a vertex cut hit
+    # FulgoraUtil's ThrowingCombiner (:80-91) and the job fails.
+    g, _, _ = oracle_graph("partition_groups", SCOPE_IN)
+    with pytest.raises(RuntimeError, match="rc=-6"):
+        g.pagerank(0.85, g.n, 3)
+
+
+def test_partitioned_merge_equals_unpartitioned_graph():
+    # With an associative combiner (min / sum) a vertex cut behaves like one vertex holding the
+    # union of its representative rows: compare against the same graph without partition().
+    import random
+    import edgestore as es
+    rnd = random.Random(3)
+    knows = es.user_edge_label(1)
+    wkey = es.user_property_key(1)
+    sd = {"edge_types": [{"type_id": knows, "multiplicity": 0, "signature": [wkey]}], "property_keys": [[wkey, 3]]}
+    schema = fr.OracleSchema(sd["edge_types"], [tuple(x) for x in sd["property_keys"]])
+    n = 300
+    edges = [(rnd.randrange(n), rnd.randrange(n), knows, [(wkey, rnd.randint(1, 9))]) for _ in range(2500)]
+    edges += [(0, rnd.randrange(n), knows, [(wkey, rnd.randint(1, 9))]) for _ in range(200)]
+    hubs = [0, 1, 2, 7]
+    res = []
+    for part in (hubs, []):
+        rows, vids = es.build_rows(es.GraphSpec(n=n, edges=edges, partitioned=part), schema)
+        gi = fr.OracleGraph.from_rows(rows, schema, SCOPE_IN, weight_key=wkey)
+        pos = {int(v): i for i, v in enumerate(gi.vertex_ids())}
+        perm = np.array([pos[int(v)] for v in vids])
+        d, _ = gi.shortest_distance(int(vids[5]), 12, SCOPE_IN, weighted=True)
+        k, _ = gi.degree_counter(3)
+        res.append((d[perm], k[perm]))
+        assert gi.stats.partitioned_vertices == len(part)
+    assert np.array_equal(res[0][0], res[1][0])
+    assert np.array_equal(res[0][1], res[1][1])

@@ -29,7 +29,7 @@ DT_BYTE, DT_SHORT, DT_INTEGER, DT_LONG, DT_FLOAT, DT_DOUBLE, DT_BOOLEAN = 1, 2, 
 SSSP_HOP_BOUNDED, SSSP_DELTA = 0, 1
 FLAG_STATS = 1
 DIST_ABSENT = -(1 << 63)
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 _i64p = C.POINTER(C.c_int64)
 _i32p = C.POINTER(C.c_int32)
@@ -91,7 +91,8 @@ class Stats(C.Structure):
                 ("truncated_results", C.c_int64), ("skipped_rows", C.c_int64), ("iterations", C.c_int32),
                 ("levels", C.c_int32), ("reached", C.c_int64), ("reached_entries", C.c_int64),
                 ("load_ms", C.c_double), ("last_kernel_ms", C.c_double), ("device_bytes", C.c_int64),
-                ("relaxed_entries", C.c_int64)]
+                ("relaxed_entries", C.c_int64), ("partitioned_vertices", C.c_int64),
+                ("partition_rows", C.c_int64), ("ghost_partition_rows", C.c_int64)]
 
 
 # Every symbol include/*.h declares (checked by tests/test_abi.py).

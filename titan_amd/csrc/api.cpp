@@ -41,6 +41,7 @@ struct tgo_ctx {
     int32_t part_pr_iter = 0;
     int64_t part_relaxed = 0;   // partitioned SSSP: entries relaxed, phases
     int32_t part_phases = 0;
+    int64_t pv_max_out = 0, pv_max_in = 0;   // largest OUT / IN list of a vertex cut
 };
 
 namespace {
@@ -180,6 +181,11 @@ int upload_graph(tgo_ctx* ctx, HostGraph& h) {
     ctx->st.ghost_vertices = h.ghost;
     ctx->st.truncated_results = h.truncated;
     ctx->st.skipped_rows = h.skipped;
+    ctx->st.partitioned_vertices = h.partitioned;
+    ctx->st.partition_rows = h.partition_rows;
+    ctx->st.ghost_partition_rows = h.ghost_partition_rows;
+    ctx->pv_max_out = h.pv_max_out;
+    ctx->pv_max_in = h.pv_max_in;
     ctx->st.device_bytes = ctx->dev_bytes;
     ctx->loaded = true;
     return TGO_OK;
@@ -753,6 +759,12 @@ int tgo_pagerank(tgo_ctx* ctx, const tgo_pr_args* a, double* pr_out) {
     if (ctx->g.scope == TGO_SCOPE_BOTH_E)
         return fail(ctx, TGO_E_INVALID, "PageRank uses the inE/outE scopes; load the graph with a single-direction scope");
     if (a->max_iterations < 0) return fail(ctx, TGO_E_INVALID, "max_iterations < 0");
+    // PageRankVertexProgram has no combiner: two messages of one scope meeting at a vertex cut
+    // hit FulgoraUtil's ThrowingCombiner (:80-91) and the job fails.  Iteration 1 receives the
+    // inE messages over OUT entries, iterations >= 2 the outE messages over IN entries.
+    if ((a->max_iterations >= 1 && ctx->pv_max_out >= 2) || (a->max_iterations >= 2 && ctx->pv_max_in >= 2))
+        return fail(ctx, TGO_E_PROGRAM, "The VertexProgram needs to define a message combiner in order to "
+                                        "preserve memory and handle partitioned vertices");
     (void)hipSetDevice(ctx->opts.device);
     DevGraph& g = ctx->g;
     Scratch& s = ctx->sc;

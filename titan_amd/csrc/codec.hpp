@@ -114,6 +114,20 @@ inline int64_t key_to_vertex_id(int64_t key, int pb) {
     return static_cast<int64_t>((((count << pb) + partition) << 3) | (k & 7u));
 }
 
+// Vertex cuts (VertexIDType.PartitionedVertex, suffix 010b, IDManager.java:78-90).
+inline bool is_partitioned_vertex(int64_t vid, int pb) {            // isPartitionedVertex :557-559
+    return (vid & 7) == 2 && (static_cast<uint64_t>(vid) >> (pb + 3)) > 0;
+}
+// getCanonicalVertexId (:530-534): the representative in partition getPartitionHashForId(count)
+// (:512-523, XOR of the count's pb-bit chunks).
+inline int64_t canonical_vertex_id(int64_t vid, int pb) {
+    if (pb <= 0) return vid;
+    const uint64_t count = static_cast<uint64_t>(vid) >> (pb + 3);
+    uint64_t part = 0;
+    for (int off = 0; off < 64; off += pb) part ^= (count >> off) & ((1ULL << pb) - 1);
+    return static_cast<int64_t>((((count << pb) + part) << 3) | 2u);
+}
+
 // Per-edge-label decode plan derived from tgo_schema.
 struct LabelPlan {
     int64_t type_id = 0;

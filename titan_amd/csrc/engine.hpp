@@ -37,6 +37,11 @@ struct HostGraph {
     bool has_weight = false;
     int32_t scope = TGO_SCOPE_BOTH_E;
     int64_t ghost = 0, truncated = 0, skipped = 0;
+    int64_t partitioned = 0, partition_rows = 0, ghost_partition_rows = 0;
+    // largest OUT / IN list of a vertex cut (PageRank has no combiner: >= 2 messages at a
+    // cut make the reference throw, FulgoraUtil.java:80-91)
+    int64_t pv_max_out = 0, pv_max_in = 0;
+    std::vector<uint8_t> pv_flags;   // row-order dense id -> is a vertex cut (empty if none)
 };
 
 // Staging of decoded rows between tgo_load_rows batches (decoded on arrival).
@@ -46,7 +51,9 @@ struct RowStaging {
     std::vector<int64_t> other;      // other vertex Titan id per kept entry
     std::vector<uint8_t> dir;        // 0 OUT, 1 IN
     std::vector<int32_t> w;          // weight (INT32_MIN = property missing)
+    std::vector<uint8_t> rep;        // per row: 1 = non-canonical representative of a vertex cut
     int64_t ghost = 0, truncated = 0, skipped = 0;
+    int64_t n_rep = 0;               // representative rows staged
     bool active = false;
     tgo_load_opts opts{};
     std::vector<int64_t> labels;

@@ -78,7 +78,7 @@ int decode_rows(RowStaging& st, const tgo_rows* rows, const tgo_schema* schema,
 
     struct Local {
         std::vector<int64_t> vid, cnt, other;
-        std::vector<uint8_t> dir;
+        std::vector<uint8_t> dir, rep;
         std::vector<int32_t> w;
         int64_t ghost = 0, truncated = 0, skipped = 0;
         int rc = TGO_OK;
@@ -93,15 +93,17 @@ int decode_rows(RowStaging& st, const tgo_rows* rows, const tgo_schema* schema,
             const int64_t vid = key_to_vertex_id(rows->row_keys[r], pb);
             if (vid & 1) { ++L.skipped; continue; }           // key filter: Invisible (:156-162)
             const int64_t sfx = vid & 7;
-            if (sfx == 2) { L.rc = TGO_E_UNSUPPORTED; L.msg = "partitioned (vertex-cut) vertex rows are not supported"; break; }
-            if (sfx != 0 && sfx != 4) { L.rc = TGO_E_CODEC; L.msg = "row key has an unrecognized vertex id type"; break; }
+            if (sfx != 0 && sfx != 2 && sfx != 4) { L.rc = TGO_E_CODEC; L.msg = "row key has an unrecognized vertex id type"; break; }
+            // a non-canonical representative row of a vertex cut skips the ghost check
+            // (VertexJobConverter.java:132) and is folded into its canonical vertex at assembly
+            const bool is_rep = sfx == 2 && vid != canonical_vertex_id(vid, pb);
             const uint8_t* base = rows->entry_bytes + rows->row_byte_begin[r];
             const int64_t e0 = rows->row_entry_begin[r], e1 = rows->row_entry_begin[r + 1];
             auto ent_start = [&](int64_t k) -> int64_t {
                 return k == e0 ? 0 : static_cast<int64_t>(static_cast<uint64_t>(rows->entry_limit_valpos[k - 1]) >> 32);
             };
             if (e1 <= e0) { L.rc = TGO_E_CODEC; L.msg = "row without entries"; break; }
-            {   // ghost check: the first column must be VertexExists (:131-137)
+            if (!is_rep) {   // ghost check: the first column must be VertexExists (:131-137)
                 const int64_t end = static_cast<int64_t>(static_cast<uint64_t>(rows->entry_limit_valpos[e0]) >> 32);
                 Cursor c{base, static_cast<size_t>(end), 0};
                 RelType rt;
@@ -131,13 +133,15 @@ int decode_rows(RowStaging& st, const tgo_rows* rows, const tgo_schema* schema,
                                                              : "malformed edge entry";
                     break;
                 }
-                L.other.push_back(de.other);
+                // messages are looked up by canonical id (VertexMemoryHandler.java:89)
+                L.other.push_back(is_partitioned_vertex(de.other, pb) ? canonical_vertex_id(de.other, pb) : de.other);
                 L.dir.push_back(static_cast<uint8_t>(de.dir));
                 L.w.push_back(plan.weight_key == 0 ? 1 : (de.has_weight ? de.weight : kMissingWeight));
                 ++kept;
             }
             if (L.rc != TGO_OK) break;
-            L.vid.push_back(vid);
+            L.vid.push_back(is_rep ? canonical_vertex_id(vid, pb) : vid);
+            L.rep.push_back(is_rep ? 1 : 0);
             L.cnt.push_back(kept);
         }
     });
@@ -158,6 +162,8 @@ int decode_rows(RowStaging& st, const tgo_rows* rows, const tgo_schema* schema,
         st.ghost += L.ghost; st.truncated += L.truncated; st.skipped += L.skipped;
         for (size_t i = 0; i < L.vid.size(); ++i) {
             st.vid.push_back(L.vid[i]);
+            st.rep.push_back(L.rep[i]);
+            st.n_rep += L.rep[i];
             st.row_begin.push_back(st.row_begin.back() + L.cnt[i]);
         }
         st.other.insert(st.other.end(), L.other.begin(), L.other.end());
@@ -297,9 +303,65 @@ static void finish_views(HostGraph& g, int threads) {
     }
 }
 
+// ------------------------------------------------------------------ vertex cuts
+// Fold every non-canonical representative row into its canonical vertex: Fulgora combines
+// each representative row's messages with the program's combiner, aggregates them per
+// canonical id and executes the program once on the aggregate (VertexProgramScanJob.java
+// :76-92, FulgoraVertexMemory.java:121-147, PartitionedVertexProgramExecutor.java:47-103).
+// With an associative combiner (ShortestDistance min, DegreeCounter sum) that equals one
+// vertex holding the union of the rows, which is what the device sees.  Representative rows
+// whose canonical row was not processed never execute (GHOTST_PARTITION_VERTEX, :53-56).
+// Entry order per vertex: its own row, then the other representatives in scan order.
+static void fold_representatives(RowStaging& st, HostGraph& g) {
+    const int64_t rows = static_cast<int64_t>(st.vid.size());
+    std::vector<int64_t> live;
+    for (int64_t r = 0; r < rows; ++r)
+        if (!st.rep[r]) live.push_back(st.vid[r]);
+    IdMap map;
+    map.build(live);
+    const int64_t n = static_cast<int64_t>(live.size());
+    std::vector<int32_t> owner(rows);
+    std::vector<int64_t> cnt(n + 1, 0);
+    std::vector<uint8_t> pv(n, 0);
+    for (int64_t r = 0, v = 0; r < rows; ++r) {
+        owner[r] = st.rep[r] ? map.find(st.vid[r]) : static_cast<int32_t>(v++);
+        if (owner[r] < 0) { ++g.ghost_partition_rows; continue; }
+        if (st.rep[r]) { ++g.partition_rows; pv[owner[r]] = 1; }
+        cnt[owner[r] + 1] += st.row_begin[r + 1] - st.row_begin[r];
+    }
+    for (int64_t r = 0; r < rows; ++r)    // every canonical row of a cut (PartitionedVertex suffix)
+        if (!st.rep[r] && (st.vid[r] & 7) == 2) pv[owner[r]] = 1;
+    for (int64_t v = 0; v < n; ++v) cnt[v + 1] += cnt[v];
+    std::vector<int64_t> pos(cnt.begin(), cnt.end() - 1);
+    std::vector<int64_t> other(cnt[n]);
+    std::vector<uint8_t> dir(cnt[n]);
+    std::vector<int32_t> w(st.w.empty() ? 0 : cnt[n]);
+    for (int pass = 0; pass < 2; ++pass)
+        for (int64_t r = 0; r < rows; ++r) {
+            if (owner[r] < 0 || st.rep[r] != pass) continue;
+            for (int64_t k = st.row_begin[r]; k < st.row_begin[r + 1]; ++k) {
+                const int64_t p = pos[owner[r]]++;
+                other[p] = st.other[k];
+                dir[p] = st.dir[k];
+                if (!w.empty()) w[p] = st.w[k];
+            }
+        }
+    for (int64_t v = 0; v < n; ++v) g.partitioned += pv[v];
+    st.vid = std::move(live);
+    st.row_begin = std::move(cnt);
+    st.other = std::move(other);
+    st.dir = std::move(dir);
+    st.w = std::move(w);
+    st.rep.assign(n, 0);
+    st.n_rep = 0;
+    g.pv_flags = std::move(pv);
+}
+
 // ------------------------------------------------------------------ staging -> CSR
 int assemble_from_rows(RowStaging& st, HostGraph& g, int threads, std::string& err) {
     g = HostGraph();
+    if (st.n_rep > 0 || std::any_of(st.vid.begin(), st.vid.end(), [](int64_t v) { return (v & 7) == 2; }))
+        fold_representatives(st, g);
     g.n = static_cast<int64_t>(st.vid.size());
     if (g.n >= INT32_MAX) { err = "more than 2^31-1 vertices per device"; return TGO_E_UNSUPPORTED; }
     g.titan_id = st.vid;
@@ -326,6 +388,8 @@ int assemble_from_rows(RowStaging& st, HostGraph& g, int threads, std::string& e
             co[v + 1] = a; ci[v + 1] = b;
         }
     });
+    for (int64_t v = 0; v < static_cast<int64_t>(g.pv_flags.size()); ++v)
+        if (g.pv_flags[v]) { g.pv_max_out = std::max(g.pv_max_out, co[v + 1]); g.pv_max_in = std::max(g.pv_max_in, ci[v + 1]); }
     for (int64_t v = 0; v < n; ++v) { co[v + 1] += co[v]; ci[v + 1] += ci[v]; }
     g.out.off = co; g.in.off = ci;
     g.out.adj.resize(co[n]); g.in.adj.resize(ci[n]);
