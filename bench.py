@@ -27,6 +27,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+JSON_OUT = sys.stdout    # the one result line; the partitioned path moves fd 1 (see main)
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8 TB/s peak (spec)
 METRIC = "BFS GTEPS + PageRank s/iter, RMAT scale-24 (1 GPU) and scale-27 (1/2/4/8 GPU)"
 
@@ -49,6 +50,8 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--sssp-roots", type=int, default=4, help="delta-stepping SSSP leg (configs[4]); 0 disables")
     p.add_argument("--delta", type=int, default=0, help="delta-stepping bucket width (0 = engine default)")
+    p.add_argument("--layout", type=int, default=1,
+                   help="partitioned path: degree-grouped device layout (tgo_part_layout); 0 = global ids as given")
     p.add_argument("--partitioned", action="store_true",
                    help="use the vertex-partitioned multi-GPU path even at N=1 (for testing it on one GPU)")
     return p.parse_args()
@@ -242,8 +245,8 @@ def run_partitioned(args, world, rank, local_rank):
     import torch.distributed as dist
     from titan_amd import Engine
     from titan_amd import _lib as L
-    from titan_amd.distributed import (HipPartBackend, distributed_bfs, distributed_msbfs, distributed_pagerank,
-                                       partition_range)
+    from titan_amd.distributed import (HipPartBackend, all_gather_layout, distributed_bfs, distributed_msbfs,
+                                       distributed_pagerank, partition_range)
     torch.cuda.set_device(local_rank)
     dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     scale = args.scale + int(round(math.log2(world)))
@@ -266,10 +269,13 @@ def run_partitioned(args, world, rank, local_rank):
     log(f"rmat scale {scale} partition [{lo},{hi}) of {world}: {cnt.value} edges in {time.perf_counter() - t0:.1f}s")
     stream = torch.cuda.current_stream().cuda_stream
     t0 = time.perf_counter()
+    lay = all_gather_layout(src, dst, n, lo, hi, torch.device("cuda", local_rank)) if args.layout else None
     bfs_be = HipPartBackend(Engine(device=local_rank, host_threads=16, stream=stream)
-                            .load_partition(n, lo, hi, src, dst, L.SCOPE_BOTH_E, apply_cap=False), n, lo, hi)
+                            .load_partition(n, lo, hi, src, dst, L.SCOPE_BOTH_E, apply_cap=False, layout=lay),
+                            n, lo, hi)
     pr_eng = Engine(device=local_rank, host_threads=16, stream=stream).load_partition(n, lo, hi, src, dst,
-                                                                                    L.SCOPE_IN_E, apply_cap=True)
+                                                                                    L.SCOPE_IN_E, apply_cap=True,
+                                                                                    layout=lay)
     pr_be = HipPartBackend(pr_eng, n, lo, hi)
     log(f"partition graphs loaded in {time.perf_counter() - t0:.1f}s")
     # roots: seeded candidates, kept when their (global) degree is > 0
@@ -326,7 +332,7 @@ def run_partitioned(args, world, rank, local_rank):
     del pr_be, pr_eng
     sssp = None
     if wgt is not None:
-        sssp = sssp_leg_partitioned(args, world, rank, local_rank, n, lo, hi, src, dst, wgt, roots, stream)
+        sssp = sssp_leg_partitioned(args, world, rank, local_rank, n, lo, hi, src, dst, wgt, roots, stream, lay)
     if rank == 0:
         edges_in = mR / 2.0
         teps = float(edges_in.sum()) * args.steps / bfs_wall
@@ -341,13 +347,14 @@ def run_partitioned(args, world, rank, local_rank):
         bfs_share = bfs_wall / (bfs_wall + pr_wall * args.steps)
         line = result_line(args, world, scale, n, m, roots, elapsed, teps, hmean, pr_wall / upd, e_in,
                            roof_bfs, roof_pr, bfs_share, None, f"vertex-partition{world}")
+        line["config"]["device_layout"] = "degree-grouped per rank" if args.layout else "global ids"
         line["sssp"] = sssp
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=JSON_OUT, flush=True)
     dist.barrier()
     dist.destroy_process_group()
 
 
-def sssp_leg_partitioned(args, world, rank, local_rank, n, lo, hi, src, dst, wgt, roots, stream):
+def sssp_leg_partitioned(args, world, rank, local_rank, n, lo, hi, src, dst, wgt, roots, stream, lay):
     """configs[4] over N GPUs: delta-stepping SSSP on the vertex-partitioned weighted graph
     (inE scope, no preload cap), per-owner relaxation exchange over RCCL
     (titan_amd/distributed.distributed_sssp); roots whose reach is the giant component."""
@@ -357,7 +364,8 @@ def sssp_leg_partitioned(args, world, rank, local_rank, n, lo, hi, src, dst, wgt
     from titan_amd import _lib as L
     from titan_amd.distributed import HipPartBackend, distributed_sssp
     eng = Engine(device=local_rank, host_threads=16, stream=stream).load_partition(n, lo, hi, src, dst, L.SCOPE_IN_E,
-                                                                                 weight=wgt, apply_cap=False)
+                                                                                 weight=wgt, apply_cap=False,
+                                                                                 layout=lay)
     be = HipPartBackend(eng, n, lo, hi)
     res = []
     for r in roots:
@@ -411,6 +419,12 @@ def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1 or args.partitioned:
+        # RCCL prints its version banner on fd 1: route native stdout to stderr and keep the
+        # real stdout for the single JSON result line.
+        global JSON_OUT
+        sys.stdout.flush()
+        JSON_OUT = os.fdopen(os.dup(1), "w")
+        os.dup2(2, 1)
         run_partitioned(args, world, int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0")))
     else:
         run_single(args)

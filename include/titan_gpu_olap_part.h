@@ -32,6 +32,19 @@ extern "C" {
 int tgo_load_partition(tgo_ctx* ctx, int64_t n_global, int64_t lo, int64_t hi,
                        const tgo_edges* edges, const tgo_load_opts* opts);
 
+/* Device layout for the partitioned path (the multi-GPU form of the single-GPU
+ * degree-grouped relabel): tgo_part_layout writes, for each owned vertex lo+v, its internal
+ * global id layout_local[v] in [lo, hi) (owned vertices grouped by half-octave of degree,
+ * hottest first).  The caller all-gathers the ranks' slices into layout_global (n_global
+ * int32, host) and loads with tgo_load_partition_layout; every kernel then runs on internal
+ * ids (hot vertices share cache lines in the gathered global vectors) while seeds and
+ * outputs of the tgo_part_* calls stay in the caller's global ids / row order.  All ranks
+ * must load with the same layout_global. */
+int tgo_part_layout(const tgo_edges* edges, int64_t n_global, int64_t lo, int64_t hi, int32_t threads,
+                    int32_t* layout_local);
+int tgo_load_partition_layout(tgo_ctx* ctx, int64_t n_global, int64_t lo, int64_t hi,
+                              const tgo_edges* edges, const tgo_load_opts* opts, const int32_t* layout_global);
+
 /* counts[0] = vertices put in this rank's next frontier, counts[1] = their list entries */
 int tgo_part_bfs_begin(tgo_ctx* ctx, int64_t seed_global, uint64_t* nb_local, int64_t* counts);
 int tgo_part_bfs_td(tgo_ctx* ctx, int32_t level, uint64_t* disc_global);

@@ -399,3 +399,51 @@ def test_partition_range_is_word_aligned():
     assert partition_range(1 << 10, 4, 3) == (768, 1024)
     with pytest.raises(ValueError):
         partition_range(1000, 4, 0)
+
+
+def _layout_worker(rank, world, port, scale, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from titan_amd import rmat_edges
+    from titan_amd.distributed import all_gather_layout, partition_range
+    n = 1 << scale
+    src, dst, _ = rmat_edges(scale, 8, seed=23)
+    lo, hi = partition_range(n, world, rank)
+    lay = all_gather_layout(src, dst, n, lo, hi, torch.device("cpu"), threads=2)
+    out_q.put((rank, lay))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_all_gathered_layout_is_a_rangewise_degree_order():
+    """tgo_part_layout (host code of the C-ABI) + the all-gather every rank loads with: a
+    permutation keeping each owned range, hottest half-octave degree group first, stable."""
+    from titan_amd import rmat_edges
+    from titan_amd.distributed import partition_range
+    world, scale = 2, 10
+    n = 1 << scale
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_layout_worker, args=(r, world, port, scale, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert np.array_equal(got[0], got[1])
+    lay = got[0].astype(np.int64)
+    src, dst, _ = rmat_edges(scale, 8, seed=23)
+    deg = np.bincount(src, minlength=n) + np.bincount(dst, minlength=n)
+    bucket = np.where(deg == 0, 0, 1 + np.floor(2.0 * np.log2(np.maximum(deg, 1))).astype(np.int64))
+    for r in range(world):
+        lo, hi = partition_range(n, world, r)
+        part = lay[lo:hi]
+        assert np.array_equal(np.sort(part), np.arange(lo, hi))
+        inv = np.empty(hi - lo, np.int64)
+        inv[part - lo] = np.arange(lo, hi)
+        b = bucket[inv]
+        assert np.all(np.diff(b) <= 0)                       # hottest group first
+        for g in np.unique(b):                               # row order kept inside a group
+            assert np.all(np.diff(inv[b == g]) > 0)

@@ -11,7 +11,7 @@ import torch
 import fulgora as fr
 from titan_amd import Engine, rmat_edges
 from titan_amd import _lib as L
-from titan_amd.distributed import HipPartBackend, partition_range
+from titan_amd.distributed import HipPartBackend, local_layout, partition_range
 
 pytestmark = pytest.mark.gpu
 ABSENT = L.DIST_ABSENT
@@ -145,17 +145,29 @@ def run_sssp(backends, seed, delta):
     return np.concatenate([o[0] for o in outs]), sum(o[1] for o in outs)
 
 
-@pytest.mark.parametrize("world,scope", [(2, L.SCOPE_IN_E), (4, L.SCOPE_OUT_E), (4, L.SCOPE_BOTH_E)])
-def test_partitioned_delta_stepping(world, scope):
-    scale = 12
-    n = 1 << scale
-    src, dst, w = rmat_edges(scale, 16, seed=35, weights=True)
+def make_backends(world, n, src, dst, scope, weight=None, layout=False):
+    """One Engine per simulated rank; layout=True loads every rank with the all-gathered
+    degree-grouped layout (tgo_part_layout), as bench.py does."""
+    lay = None
+    if layout:
+        lay = np.concatenate([local_layout(src, dst, n, *partition_range(n, world, r)) for r in range(world)])
+        assert np.array_equal(np.sort(lay), np.arange(n))
     backends = []
     for r in range(world):
         lo, hi = partition_range(n, world, r)
-        eng = Engine(stream=torch.cuda.current_stream().cuda_stream).load_partition(n, lo, hi, src, dst, scope,
-                                                                                    weight=w, apply_cap=False)
+        eng = Engine(stream=torch.cuda.current_stream().cuda_stream).load_partition(
+            n, lo, hi, src, dst, scope, weight=weight, apply_cap=False, layout=lay)
         backends.append(HipPartBackend(eng, n, lo, hi))
+    return backends
+
+
+@pytest.mark.parametrize("layout", [False, True])
+@pytest.mark.parametrize("world,scope", [(2, L.SCOPE_IN_E), (4, L.SCOPE_OUT_E), (4, L.SCOPE_BOTH_E)])
+def test_partitioned_delta_stepping(world, scope, layout):
+    scale = 12
+    n = 1 << scale
+    src, dst, w = rmat_edges(scale, 16, seed=35, weights=True)
+    backends = make_backends(world, n, src, dst, scope, weight=w, layout=layout)
     og = fr.OracleGraph.from_edges(n, src, dst, w)
     ids = (np.arange(n, dtype=np.int64) + 1) << 3
     for seed in (int(src[0]), int(dst[9])):
@@ -166,17 +178,13 @@ def test_partitioned_delta_stepping(world, scope):
             assert reached[0] == int((od != ABSENT).sum())
 
 
+@pytest.mark.parametrize("layout", [False, True])
 @pytest.mark.parametrize("world", [2, 4])
-def test_partitioned_multi_source_bfs(world):
+def test_partitioned_multi_source_bfs(world, layout):
     scale = 12
     n = 1 << scale
     src, dst, _ = rmat_edges(scale, 16, seed=33)
-    backends = []
-    for r in range(world):
-        lo, hi = partition_range(n, world, r)
-        eng = Engine(stream=torch.cuda.current_stream().cuda_stream).load_partition(n, lo, hi, src, dst, L.SCOPE_BOTH_E,
-                                                                                    apply_cap=False)
-        backends.append(HipPartBackend(eng, n, lo, hi))
+    backends = make_backends(world, n, src, dst, L.SCOPE_BOTH_E, layout=layout)
     og = fr.OracleGraph.from_edges(n, src, dst)
     ids = (np.arange(n, dtype=np.int64) + 1) << 3
     rng = np.random.default_rng(5)
@@ -189,17 +197,13 @@ def test_partitioned_multi_source_bfs(world):
             assert reached[i] == int((od != ABSENT).sum())
 
 
+@pytest.mark.parametrize("layout", [False, True])
 @pytest.mark.parametrize("world", [2, 4])
-def test_partitioned_bfs_and_pagerank(world):
+def test_partitioned_bfs_and_pagerank(world, layout):
     scale = 12
     n = 1 << scale
     src, dst, _ = rmat_edges(scale, 16, seed=31)
-    backends = []
-    for r in range(world):
-        lo, hi = partition_range(n, world, r)
-        eng = Engine(stream=torch.cuda.current_stream().cuda_stream).load_partition(n, lo, hi, src, dst, L.SCOPE_BOTH_E,
-                                                                                    apply_cap=False)
-        backends.append(HipPartBackend(eng, n, lo, hi))
+    backends = make_backends(world, n, src, dst, L.SCOPE_BOTH_E, layout=layout)
     og = fr.OracleGraph.from_edges(n, src, dst)
     ids = (np.arange(n, dtype=np.int64) + 1) << 3
     for seed in (int(src[0]), int(dst[9]), int(src[100])):

@@ -103,7 +103,7 @@ EXPORTS = [
     "tgo_bfs_multi", "tgo_copy_multi_distances", "tgo_multi_stats",
     "tgo_rmat_edges", "tgo_pick_roots",
     # titan_gpu_olap_part.h (1-D vertex-partitioned multi-GPU)
-    "tgo_load_partition", "tgo_part_bfs_begin", "tgo_part_bfs_td", "tgo_part_bfs_claim", "tgo_part_bfs_bu",
+    "tgo_load_partition", "tgo_part_layout", "tgo_load_partition_layout", "tgo_part_bfs_begin", "tgo_part_bfs_td", "tgo_part_bfs_claim", "tgo_part_bfs_bu",
     "tgo_part_bfs_end", "tgo_part_pr_begin", "tgo_part_pr_step", "tgo_part_pr_end", "tgo_rmat_partition",
     "tgo_part_ms_begin", "tgo_part_ms_pull", "tgo_part_ms_push", "tgo_part_ms_settle", "tgo_part_ms_end",
     "tgo_part_ms_levels", "tgo_part_sssp_begin", "tgo_part_sssp_relax", "tgo_part_sssp_apply",
@@ -154,6 +154,8 @@ def load() -> C.CDLL:
                                      _i32p, _i32p, _i32p, C.c_int32]),
         "tgo_pick_roots": (C.c_int, [C.c_int64, C.c_int64, _i32p, _i32p, C.c_uint64, C.c_int32, _i64p]),
         "tgo_load_partition": (C.c_int, [vp, C.c_int64, C.c_int64, C.c_int64, P(Edges), P(LoadOpts)]),
+        "tgo_part_layout": (C.c_int, [P(Edges), C.c_int64, C.c_int64, C.c_int64, C.c_int32, _i32p]),
+        "tgo_load_partition_layout": (C.c_int, [vp, C.c_int64, C.c_int64, C.c_int64, P(Edges), P(LoadOpts), _i32p]),
         "tgo_part_bfs_begin": (C.c_int, [vp, C.c_int64, vp, _i64p]),
         "tgo_part_bfs_td": (C.c_int, [vp, C.c_int32, vp]),
         "tgo_part_bfs_claim": (C.c_int, [vp, C.c_int32, vp, C.c_int32, vp, _i64p]),

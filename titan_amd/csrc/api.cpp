@@ -834,8 +834,20 @@ int tgo_walkcount(tgo_ctx* ctx, int32_t k, int32_t* out) {
 }
 
 // ------------------------------------------------------------------ 1-D partitioned (multi-GPU)
+int tgo_part_layout(const tgo_edges* edges, int64_t n_global, int64_t lo, int64_t hi, int32_t threads,
+                    int32_t* layout_local) {
+    if (!edges || !layout_local || (edges->m > 0 && (!edges->src || !edges->dst))) return TGO_E_INVALID;
+    std::string err;
+    return partition_layout(edges, n_global, lo, hi, threads > 0 ? threads : 1, layout_local, err);
+}
+
 int tgo_load_partition(tgo_ctx* ctx, int64_t n_global, int64_t lo, int64_t hi, const tgo_edges* edges,
                        const tgo_load_opts* opts) {
+    return tgo_load_partition_layout(ctx, n_global, lo, hi, edges, opts, nullptr);
+}
+
+int tgo_load_partition_layout(tgo_ctx* ctx, int64_t n_global, int64_t lo, int64_t hi, const tgo_edges* edges,
+                              const tgo_load_opts* opts, const int32_t* layout_global) {
     if (!ctx) return TGO_E_INVALID;
     if (!edges || !opts || (edges->m > 0 && (!edges->src || !edges->dst))) return fail(ctx, TGO_E_INVALID, "null argument");
     if ((hi - lo) % 64 != 0) return fail(ctx, TGO_E_INVALID, "partition size must be a multiple of 64");
@@ -843,7 +855,8 @@ int tgo_load_partition(tgo_ctx* ctx, int64_t n_global, int64_t lo, int64_t hi, c
     const auto t0 = std::chrono::steady_clock::now();
     HostGraph h;
     std::string err;
-    int rc = assemble_partition(edges, n_global, lo, hi, opts, ctx->opts.hard_query_limit, h, threads_of(ctx), err);
+    int rc = assemble_partition(edges, n_global, lo, hi, opts, ctx->opts.hard_query_limit, layout_global, h,
+                                threads_of(ctx), err);
     if (rc) return fail(ctx, rc, err);
     free_graph(ctx);
     ctx->staging = RowStaging();
@@ -891,8 +904,9 @@ int tgo_part_bfs_begin(tgo_ctx* ctx, int64_t seed_global, uint64_t* nb_local, in
     ctx->part_cur = 0;
     ctx->part_qlen = 0;
     int64_t deg = 0;
-    const int64_t seed = seed_global - g.lo;
+    int64_t seed = seed_global - g.lo;
     if (seed >= 0 && seed < n) {
+        seed = ctx->perm[seed];
         // the owner seeds: level 0, visited, in the frontier bitmap slice and the queue
         HIP_TRY(k_bfs_seed(push, s.level, s.vb, nb_local, s.q[0], s.qdeg, seed, st));
         HIP_TRY(hipMemcpyAsync(&deg, s.qdeg, sizeof(int64_t), hipMemcpyDeviceToHost, st));
@@ -964,8 +978,9 @@ int tgo_part_bfs_end(tgo_ctx* ctx, int64_t* dist_local, int64_t* reached) {
         reached[0] = static_cast<int64_t>(s.hcnt->red[0]);
         reached[1] = static_cast<int64_t>(s.hcnt->red[1]);
     }
-    if (dist_local) {
-        HIP_TRY(hipMemcpyAsync(dist_local, s.dist, g.n * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    if (dist_local) {   // back to row order
+        HIP_TRY(k_unpermute_i64(s.dist, g.perm, s.msg, g.n, st));
+        HIP_TRY(hipMemcpyAsync(dist_local, s.msg, g.n * sizeof(int64_t), hipMemcpyDeviceToHost, st));
     }
     HIP_TRY(hipStreamSynchronize(st));
     float ms = 0;
@@ -990,8 +1005,9 @@ int tgo_part_ms_begin(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, uint64
     std::vector<int64_t> local(nseeds, -1);
     std::vector<int32_t> uniq;
     for (int r = 0; r < nseeds; ++r) {
-        const int64_t l = seeds[r] - g.lo;
+        int64_t l = seeds[r] - g.lo;
         if (l >= 0 && l < n) {
+            l = ctx->perm[l];
             local[r] = l;
             if (std::find(uniq.begin(), uniq.end(), static_cast<int32_t>(l)) == uniq.end()) uniq.push_back(static_cast<int32_t>(l));
         }
@@ -1139,7 +1155,10 @@ int tgo_part_pr_end(tgo_ctx* ctx, double* pr_local) {
     DevGraph& g = ctx->g;
     Scratch& s = ctx->sc;
     HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
-    if (pr_local) HIP_TRY(hipMemcpyAsync(pr_local, s.dist, g.n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    if (pr_local) {     // back to row order
+        HIP_TRY(k_unpermute_i64(s.dist, g.perm, s.msg, g.n, ctx->stream));
+        HIP_TRY(hipMemcpyAsync(pr_local, s.msg, g.n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    }
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     float ms = 0;
     HIP_TRY(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
@@ -1176,8 +1195,9 @@ int tgo_part_sssp_begin(tgo_ctx* ctx, int64_t seed_global, int64_t delta, int64_
     ctx->part_qlen = 0;
     ctx->part_relaxed = 0;
     ctx->part_phases = 0;
-    const int64_t seed = seed_global - g.lo;
+    int64_t seed = seed_global - g.lo;
     if (seed >= 0 && seed < n) {
+        seed = ctx->perm[seed];
         HIP_TRY(k_ds_seed(push, s.dist, s.q[0], s.qdeg, seed, st));
         ctx->part_qlen = 1;
     }
@@ -1294,7 +1314,10 @@ int tgo_part_sssp_end(tgo_ctx* ctx, int64_t* dist_local, int64_t* reached) {
         reached[0] = static_cast<int64_t>(s.hcnt->red[0]);
         reached[1] = static_cast<int64_t>(s.hcnt->red[1]);
     }
-    if (dist_local) HIP_TRY(hipMemcpyAsync(dist_local, s.dist, g.n * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    if (dist_local) {   // back to row order
+        HIP_TRY(k_unpermute_i64(s.dist, g.perm, s.msg, g.n, st));
+        HIP_TRY(hipMemcpyAsync(dist_local, s.msg, g.n * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    }
     HIP_TRY(hipStreamSynchronize(st));
     float ms = 0;
     HIP_TRY(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));

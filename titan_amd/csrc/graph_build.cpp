@@ -235,12 +235,14 @@ static void transpose_lists(int64_t n, const std::vector<const HostCsr*>& lists,
 // random message gathers of the pull kernels and the frontier-bitmap probes of bottom-up
 // BFS hit the XCD L2 / Infinity Cache instead of HBM.  Purely a device layout: the API
 // keeps row-order dense ids (perm maps them) and every result is mapped back.
-static void relabel_by_degree(HostGraph& g, int threads) {
-    const int64_t n = g.n;
+// order[v] = position of vertex v (0..n-1) when grouped by half-octave of its degree deg(v),
+// hottest group first, index order kept inside a group.
+template <class Deg>
+static void degree_group_order(int64_t n, Deg deg, std::vector<int32_t>& order) {
     std::vector<int> bucket(n);
     int maxb = 0;
     for (int64_t v = 0; v < n; ++v) {
-        const int64_t d = (g.out.off[v + 1] - g.out.off[v]) + (g.in.off[v + 1] - g.in.off[v]);
+        const int64_t d = deg(v);
         const int b = d == 0 ? 0 : 1 + static_cast<int>(2.0 * std::log2(static_cast<double>(d)));
         bucket[v] = b;
         maxb = std::max(maxb, b);
@@ -248,8 +250,15 @@ static void relabel_by_degree(HostGraph& g, int threads) {
     std::vector<int64_t> start(maxb + 2, 0);
     for (int64_t v = 0; v < n; ++v) ++start[maxb - bucket[v] + 1];          // descending buckets
     for (int b = 0; b <= maxb; ++b) start[b + 1] += start[b];
-    g.perm.assign(n, 0);
-    for (int64_t v = 0; v < n; ++v) g.perm[v] = static_cast<int32_t>(start[maxb - bucket[v]]++);
+    order.assign(n, 0);
+    for (int64_t v = 0; v < n; ++v) order[v] = static_cast<int32_t>(start[maxb - bucket[v]]++);
+}
+
+// Rows move to g.perm[v]; every neighbour id u becomes nbr(u); rows are re-sorted by the
+// new neighbour ids (stable).
+template <class Nbr>
+static void permute_graph(HostGraph& g, Nbr nbr, int threads) {
+    const int64_t n = g.n;
     std::vector<int32_t> inv(n);
     for (int64_t v = 0; v < n; ++v) inv[g.perm[v]] = static_cast<int32_t>(v);
     auto remap = [&](HostCsr& c) {
@@ -265,7 +274,7 @@ static void relabel_by_degree(HostGraph& g, int threads) {
                 const int64_t b = c.off[inv[u]], len = c.off[inv[u] + 1] - b;
                 key.resize(len);
                 for (int64_t j = 0; j < len; ++j)   // (new neighbour, original position)
-                    key[j] = (static_cast<uint64_t>(static_cast<uint32_t>(g.perm[c.adj[b + j]])) << 32) | static_cast<uint64_t>(j);
+                    key[j] = (static_cast<uint64_t>(static_cast<uint32_t>(nbr(c.adj[b + j]))) << 32) | static_cast<uint64_t>(j);
                 std::sort(key.begin(), key.end());
                 for (int64_t j = 0; j < len; ++j) {
                     r.adj[r.off[u] + j] = static_cast<int32_t>(key[j] >> 32);
@@ -277,6 +286,40 @@ static void relabel_by_degree(HostGraph& g, int threads) {
     };
     remap(g.out);
     remap(g.in);
+}
+
+// Degree-grouped relabel (DBG, Faldu et al., IISWC'19): vertices are grouped by
+// half-octave of their total degree, hottest group first, keeping row order inside a
+// group.  High-degree vertices then share cache lines in every per-vertex array, so the
+// random message gathers of the pull kernels and the frontier-bitmap probes of bottom-up
+// BFS hit the XCD L2 / Infinity Cache instead of HBM.  Purely a device layout: the API
+// keeps row-order dense ids (perm maps them) and every result is mapped back.
+static void relabel_by_degree(HostGraph& g, int threads) {
+    degree_group_order(g.n, [&](int64_t v) {
+        return (g.out.off[v + 1] - g.out.off[v]) + (g.in.off[v + 1] - g.in.off[v]);
+    }, g.perm);
+    const int32_t* p = g.perm.data();
+    permute_graph(g, [p](int32_t u) { return p[u]; }, threads);
+}
+
+// Multi-GPU layout (tgo_part_layout): the degree-grouped order of the owned range, as
+// global internal ids lo + order[v].  Degrees = entries of the owned rows.
+int partition_layout(const tgo_edges* e, int64_t n_global, int64_t lo, int64_t hi, int threads,
+                     int32_t* layout_local, std::string& err) {
+    const int64_t n = hi - lo;
+    if (lo < 0 || hi > n_global || n <= 0 || n_global >= INT32_MAX) { err = "invalid partition range"; return TGO_E_INVALID; }
+    std::vector<std::atomic<int64_t>> deg(n);
+    for (auto& d : deg) d.store(0, std::memory_order_relaxed);
+    parallel_for(e->m, threads, [&](int64_t a, int64_t b, int) {
+        for (int64_t k = a; k < b; ++k) {
+            if (e->src[k] >= lo && e->src[k] < hi) deg[e->src[k] - lo].fetch_add(1, std::memory_order_relaxed);
+            if (e->dst[k] >= lo && e->dst[k] < hi) deg[e->dst[k] - lo].fetch_add(1, std::memory_order_relaxed);
+        }
+    });
+    std::vector<int32_t> order;
+    degree_group_order(n, [&](int64_t v) { return deg[v].load(std::memory_order_relaxed); }, order);
+    for (int64_t v = 0; v < n; ++v) layout_local[v] = static_cast<int32_t>(lo + order[v]);
+    return TGO_OK;
 }
 
 // Decide whether the push view equals the stored opposite list; if not, build it.
@@ -514,8 +557,8 @@ int assemble_from_edges(const tgo_edges* e, const tgo_load_opts* opts, int64_t h
 // No relabel (ids are global) and no push transposes (the partitioned path serves bothE
 // BFS, which is symmetric, and pull-only gathers).
 int assemble_partition(const tgo_edges* e, int64_t n_global, int64_t lo, int64_t hi,
-                       const tgo_load_opts* opts, int64_t hard_limit, HostGraph& g, int threads,
-                       std::string& err) {
+                       const tgo_load_opts* opts, int64_t hard_limit, const int32_t* layout, HostGraph& g,
+                       int threads, std::string& err) {
     g = HostGraph();
     const int64_t n = hi - lo, m = e->m;
     if (lo < 0 || hi > n_global || n <= 0 || n_global >= INT32_MAX) { err = "invalid partition range"; return TGO_E_INVALID; }
@@ -589,6 +632,17 @@ int assemble_partition(const tgo_edges* e, int64_t n_global, int64_t lo, int64_t
     std::vector<uint64_t>().swap(keys_o);
     fill(off_i, keys_i, ki, g.in);
     g.has_transpose = false;
+    if (layout) {   // owned rows move inside [lo, hi); neighbours take their owners' layout
+        g.perm.resize(n);
+        std::vector<uint8_t> seen(n, 0);
+        for (int64_t v = 0; v < n; ++v) {
+            const int64_t p = static_cast<int64_t>(layout[lo + v]) - lo;
+            if (p < 0 || p >= n || seen[p]) { err = "layout is not a permutation of the owned range"; return TGO_E_INVALID; }
+            seen[p] = 1;
+            g.perm[v] = static_cast<int32_t>(p);
+        }
+        permute_graph(g, [layout](int32_t u) { return layout[u]; }, threads);
+    }
     return TGO_OK;
 }
 

@@ -38,6 +38,29 @@ def partition_range(n_global: int, world: int, rank: int):
     return rank * per, (rank + 1) * per
 
 
+def local_layout(src, dst, n_global: int, lo: int, hi: int, threads: int = 16):
+    """tgo_part_layout: internal global ids of the owned vertices [lo, hi) (degree-grouped,
+    hottest first, kept inside the owned range).  Host code only (no device needed)."""
+    lib = L.load()
+    src = np.ascontiguousarray(src, np.int32)
+    dst = np.ascontiguousarray(dst, np.int32)
+    e = L.Edges(n_global, len(src), L.ptr(src, C.c_int32), L.ptr(dst, C.c_int32), None, None)
+    out = np.empty(hi - lo, np.int32)
+    rc = lib.tgo_part_layout(C.byref(e), n_global, lo, hi, threads, L.ptr(out, C.c_int32))
+    if rc:
+        raise RuntimeError(f"tgo_part_layout rc={rc}")
+    return out
+
+
+def all_gather_layout(src, dst, n_global: int, lo: int, hi: int, device, group=None, threads: int = 16):
+    """Every rank's local_layout slice, all-gathered into the global layout (host int32,
+    n_global) that every rank passes to Engine.load_partition(layout=...)."""
+    loc = torch.from_numpy(local_layout(src, dst, n_global, lo, hi, threads)).to(device)
+    out = torch.empty(n_global, dtype=torch.int32, device=device)
+    dist.all_gather_into_tensor(out, loc, group=group)
+    return out.cpu().numpy()
+
+
 class HipPartBackend:
     """Local steps on this rank's GPU through the C-ABI (titan_gpu_olap_part.h)."""
 

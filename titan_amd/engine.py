@@ -119,13 +119,23 @@ class Engine:
         return self
 
     # ------------------------------------------------------------------ 1-D partition (multi-GPU)
-    def load_partition(self, n_global, lo, hi, src, dst, scope, weight=None, apply_cap=True):
+    def load_partition(self, n_global, lo, hi, src, dst, scope, weight=None, apply_cap=True, layout=None):
+        """Rows of global vertices [lo, hi) (titan_gpu_olap_part.h); `layout` = the
+        all-gathered tgo_part_layout slices (n_global int32) or None for identity ids."""
         src = np.ascontiguousarray(src, dtype=np.int32)
         dst = np.ascontiguousarray(dst, dtype=np.int32)
         w = None if weight is None else np.ascontiguousarray(weight, dtype=np.int32)
         e = L.Edges(n_global, len(src), L.ptr(src, C.c_int32), L.ptr(dst, C.c_int32), L.ptr(w, C.c_int32), None)
         opts, keep = self._opts(scope, apply_cap, (), 1 if w is not None else 0)
-        _check(self.lib, self.ctx, self.lib.tgo_load_partition(self.ctx, n_global, lo, hi, C.byref(e), C.byref(opts)))
+        if layout is None:
+            rc = self.lib.tgo_load_partition(self.ctx, n_global, lo, hi, C.byref(e), C.byref(opts))
+        else:
+            lay = np.ascontiguousarray(layout, dtype=np.int32)
+            if len(lay) != n_global:
+                raise ValueError("layout must hold n_global entries")
+            rc = self.lib.tgo_load_partition_layout(self.ctx, n_global, lo, hi, C.byref(e), C.byref(opts),
+                                                    L.ptr(lay, C.c_int32))
+        _check(self.lib, self.ctx, rc)
         self.n = self.lib.tgo_num_vertices(self.ctx)
         return self
 
