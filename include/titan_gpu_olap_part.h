@@ -65,6 +65,18 @@ int tgo_part_ms_pull(tgo_ctx* ctx, int32_t level, const uint64_t* fr_global, uin
 int tgo_part_ms_push(tgo_ctx* ctx, int32_t level, const uint64_t* fr_local, uint64_t* cand_global);
 int tgo_part_ms_settle(tgo_ctx* ctx, int32_t level, const uint64_t* recv, int32_t nslices, uint64_t* fr_next,
                        int64_t* counts);
+/* Sparse form of the sparse-level exchange (what bench.py / distributed.py use): after
+ * tgo_part_ms_push, tgo_part_ms_pack compacts the nonzero words of cand_global into
+ * (owner-local id, mask) int64 pairs in `send` (device, capacity 2 * n_global int64),
+ * rank-major and contiguous: send_counts[r] pairs for rank r (host), and zeroes the packed
+ * words (cand_global is all-zero again afterwards).  The caller all-to-alls the counts, then
+ * the pairs with split sizes (recv = the senders' pairs back to back, recv_counts[s] from
+ * sender s), and tgo_part_ms_settle_pairs ORs them in.  Requires nranks * n_local ==
+ * n_global.  Pair order within a rank's run is unspecified; results are not affected (the
+ * masks are OR-ed). */
+int tgo_part_ms_pack(tgo_ctx* ctx, uint64_t* cand_global, int32_t nranks, int64_t* send, int64_t* send_counts);
+int tgo_part_ms_settle_pairs(tgo_ctx* ctx, int32_t level, const int64_t* recv, const int64_t* recv_counts,
+                             int32_t nslices, uint64_t* fr_next, int64_t* counts);
 /* reached / entries: per seed, over this rank's vertices (NULL to skip). */
 int tgo_part_ms_end(tgo_ctx* ctx, int64_t* reached, int64_t* entries);
 /* Source `source`'s distances of the owned vertices (TGO_DIST_ABSENT = unreached). */

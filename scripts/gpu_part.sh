@@ -6,7 +6,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out/$TAG
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/$TAG/gpu_tests.log 2>&1
 rc=$?; tail -3 gpurun_out/$TAG/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
-for lay in 1 0; do
+for lay in ${LAYOUTS:-1 0}; do
   timeout -k 10 400 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
       --master-port 29511 bench.py --partitioned --steps 2 --warmup 1 --layout $lay "$@" \
       > gpurun_out/$TAG/bench_part_l$lay.json 2> gpurun_out/$TAG/bench_part_l$lay.err

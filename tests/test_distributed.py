@@ -236,6 +236,28 @@ class NumpyPartBackend:
         r = self._u(recv).reshape(nslices, -1)
         return self._ms_fresh(level, np.bitwise_or.reduce(r, axis=0), fr_next)
 
+    def ms_pack(self, cand, send, nranks):
+        c = self._u(cand)
+        s = send.numpy()
+        counts = np.zeros(nranks, np.int64)
+        p = 0
+        for r in range(nranks):
+            sl = c[r * self.n_local:(r + 1) * self.n_local]
+            nz = np.nonzero(sl)[0][::-1]            # any order: the receiver ORs the masks
+            s[2 * p:2 * (p + len(nz)):2] = nz
+            s[2 * p + 1:2 * (p + len(nz)):2] = sl[nz].view(np.int64)
+            sl[nz] = 0
+            counts[r] = len(nz)
+            p += len(nz)
+        return counts
+
+    def ms_settle_pairs(self, level, recv, recv_counts, fr_next):
+        r = recv.numpy()
+        k = int(np.sum(recv_counts))
+        acc = np.zeros(self.n_local, np.uint64)
+        np.bitwise_or.at(acc, r[0:2 * k:2], r[1:2 * k:2].view(np.uint64))
+        return self._ms_fresh(level, acc, fr_next)
+
     def ms_end(self, nseeds, stats=True):
         if not stats:
             return None, None
@@ -287,8 +309,9 @@ def _worker(rank, world, port, scale, roots, out_q, alpha):
         res["bfs"].append(torch.cat(full).numpy())
         res["reached"].append(reached)
     from titan_amd.distributed import distributed_msbfs
-    for ms_alpha in (12.0, 1e9, 1e-9):         # mixed, always push, always pull
-        r, e, _ = distributed_msbfs(be, roots, n, ms_alpha=ms_alpha)
+    # mixed, always push (packed pairs and dense slices), always pull
+    for ms_alpha, sparse in ((12.0, True), (1e9, True), (1e9, False), (1e-9, True)):
+        r, e, _ = distributed_msbfs(be, roots, n, ms_alpha=ms_alpha, sparse_exchange=sparse)
         lv = []
         for i in range(len(roots)):
             loc = np.where(be.mslvl[:, i] >= 0, be.mslvl[:, i], ABSENT)

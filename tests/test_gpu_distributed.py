@@ -66,8 +66,9 @@ def run_bfs(backends, seed, max_depth, alpha=15.0, beta=18.0):
     return np.concatenate([o[0] for o in outs]), sum(o[1] for o in outs)
 
 
-def run_msbfs(backends, seeds, max_depth, ms_alpha=12.0):
-    """The distributed_msbfs protocol with the collectives done in-process."""
+def run_msbfs(backends, seeds, max_depth, ms_alpha=12.0, sparse=False):
+    """The distributed_msbfs protocol with the collectives done in-process (sparse: the
+    packed-pair exchange of the sparse levels, tgo_part_ms_pack / ms_settle_pairs)."""
     world = len(backends)
     n = backends[0].n_global
     nl = backends[0].n_local
@@ -75,7 +76,8 @@ def run_msbfs(backends, seeds, max_depth, ms_alpha=12.0):
     frn = [b.tensor(nl, torch.int64) for b in backends]
     fg = [b.tensor(n, torch.int64) for b in backends]
     cand = [b.tensor(n, torch.int64) for b in backends]
-    recv = [b.tensor(n, torch.int64) for b in backends]
+    recv = [b.tensor(2 * n if sparse else n, torch.int64) for b in backends]
+    send = [b.tensor(2 * n, torch.int64) for b in backends] if sparse else None
     total = sum(b.total_entries for b in backends)
     nf, mf = sum(b.ms_begin(seeds, fr_[i]) for i, b in enumerate(backends))
     for level in range(max_depth):
@@ -90,6 +92,21 @@ def run_msbfs(backends, seeds, max_depth, ms_alpha=12.0):
             torch.cuda.synchronize()
             for i, b in enumerate(backends):
                 cs.append(b.ms_pull(level, fg[i], frn[i]))
+        elif sparse:
+            counts = []
+            for i, b in enumerate(backends):
+                b.ms_push(level, fr_[i], cand[i])
+                counts.append(b.ms_pack(cand[i], send[i], world))
+                assert int(torch.count_nonzero(cand[i])) == 0        # pack clears what it packs
+            torch.cuda.synchronize()
+            offs = [np.concatenate([[0], np.cumsum(c)]) for c in counts]
+            for r in range(world):      # all_to_all with split sizes: sender s's run for rank r
+                parts = [send[s][2 * offs[s][r]:2 * offs[s][r + 1]] for s in range(world)]
+                got = torch.cat(parts)
+                recv[r][:got.numel()].copy_(got)
+            torch.cuda.synchronize()
+            for i, b in enumerate(backends):
+                cs.append(b.ms_settle_pairs(level, recv[i], [counts[s][i] for s in range(world)], frn[i]))
         else:
             for i, b in enumerate(backends):
                 cand[i].zero_()
@@ -190,8 +207,8 @@ def test_partitioned_multi_source_bfs(world, layout):
     rng = np.random.default_rng(5)
     seeds = [int(s) for s in rng.choice(n, 40, replace=False)] + [int(src[0])]
     expect = [og.shortest_distance(int(ids[s]), n, 2)[0] for s in seeds]
-    for ms_alpha in (12.0, 1e9, 1e-9):
-        levels, reached = run_msbfs(backends, seeds, n, ms_alpha)
+    for ms_alpha, sparse in ((12.0, False), (12.0, True), (1e9, False), (1e9, True), (1e-9, False)):
+        levels, reached = run_msbfs(backends, seeds, n, ms_alpha, sparse)
         for i, od in enumerate(expect):
             assert np.array_equal(levels[i], od), (ms_alpha, i)
             assert reached[i] == int((od != ABSENT).sum())

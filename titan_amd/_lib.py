@@ -106,6 +106,7 @@ EXPORTS = [
     "tgo_load_partition", "tgo_part_layout", "tgo_load_partition_layout", "tgo_part_bfs_begin", "tgo_part_bfs_td", "tgo_part_bfs_claim", "tgo_part_bfs_bu",
     "tgo_part_bfs_end", "tgo_part_pr_begin", "tgo_part_pr_step", "tgo_part_pr_end", "tgo_rmat_partition",
     "tgo_part_ms_begin", "tgo_part_ms_pull", "tgo_part_ms_push", "tgo_part_ms_settle", "tgo_part_ms_end",
+    "tgo_part_ms_pack", "tgo_part_ms_settle_pairs",
     "tgo_part_ms_levels", "tgo_part_sssp_begin", "tgo_part_sssp_relax", "tgo_part_sssp_apply",
     "tgo_part_sssp_pending_min", "tgo_part_sssp_extract", "tgo_part_sssp_end",
 ]
@@ -165,6 +166,8 @@ def load() -> C.CDLL:
         "tgo_part_ms_pull": (C.c_int, [vp, C.c_int32, vp, vp, _i64p]),
         "tgo_part_ms_push": (C.c_int, [vp, C.c_int32, vp, vp]),
         "tgo_part_ms_settle": (C.c_int, [vp, C.c_int32, vp, C.c_int32, vp, _i64p]),
+        "tgo_part_ms_pack": (C.c_int, [vp, vp, C.c_int32, vp, _i64p]),
+        "tgo_part_ms_settle_pairs": (C.c_int, [vp, C.c_int32, vp, _i64p, C.c_int32, vp, _i64p]),
         "tgo_part_ms_end": (C.c_int, [vp, _i64p, _i64p]),
         "tgo_part_ms_levels": (C.c_int, [vp, C.c_int32, _i64p]),
         "tgo_part_sssp_begin": (C.c_int, [vp, C.c_int64, C.c_int64, _i64p]),

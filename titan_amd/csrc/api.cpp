@@ -1087,6 +1087,59 @@ int tgo_part_ms_settle(tgo_ctx* ctx, int32_t level, const uint64_t* recv, int32_
     return part_counts(ctx, counts);
 }
 
+int tgo_part_ms_pack(tgo_ctx* ctx, uint64_t* cand_global, int32_t nranks, int64_t* send, int64_t* send_counts) {
+    int rc = part_check(ctx);
+    if (rc) return rc;
+    DevGraph& g = ctx->g;
+    Scratch& s = ctx->sc;
+    if (!cand_global || !send || !send_counts || nranks < 1 || nranks > kMaxRanks ||
+        static_cast<int64_t>(nranks) * g.n != g.n_global)
+        return fail(ctx, TGO_E_INVALID, "ms_pack: bad arguments (nranks * n_local must equal n_global)");
+    hipStream_t st = ctx->stream;
+    const int64_t cps = (g.n + kPackChunk - 1) / kPackChunk;     // chunks per slice
+    const int64_t nchunks = cps * nranks;
+    if (!s.pk_cnt) {
+        HIP_TRY(dev_alloc(ctx, s.pk_cnt, g.n_global / kPackChunk + kMaxRanks + 1));
+        HIP_TRY(dev_alloc(ctx, s.pk_off, g.n_global / kPackChunk + kMaxRanks + 1));
+    }
+    HIP_TRY(hipMemsetAsync(s.pk_cnt + nchunks, 0, sizeof(int64_t), st));
+    HIP_TRY(k_ms_pack(false, cand_global, g.n, cps, nchunks, s.pk_cnt, s.pk_off, send, st));
+    HIP_TRY(scan_exclusive_i64(s.cub_tmp, s.cub_bytes, s.pk_cnt, s.pk_off, nchunks + 1, st));
+    std::vector<int64_t> off(nranks + 1);
+    for (int r = 0; r <= nranks; ++r)     // offsets at the slice boundaries (pk_cnt[nchunks] is 0)
+        HIP_TRY(hipMemcpyAsync(&off[r], s.pk_off + r * cps, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    for (int r = 0; r < nranks; ++r) send_counts[r] = off[r + 1] - off[r];
+    if (off[nranks] > 0) HIP_TRY(k_ms_pack(true, cand_global, g.n, cps, nchunks, s.pk_cnt, s.pk_off, send, st));
+    return TGO_OK;
+}
+
+int tgo_part_ms_settle_pairs(tgo_ctx* ctx, int32_t level, const int64_t* recv, const int64_t* recv_counts,
+                             int32_t nslices, uint64_t* fr_next, int64_t* counts) {
+    int rc = part_check(ctx);
+    if (rc) return rc;
+    DevGraph& g = ctx->g;
+    Scratch& s = ctx->sc;
+    hipStream_t st = ctx->stream;
+    if (!recv || !recv_counts || !fr_next || nslices < 1 || nslices > kMaxRanks)
+        return fail(ctx, TGO_E_INVALID, "ms_settle_pairs: bad arguments");
+    if (level + 1 >= (1 << kLevelPlanes)) return fail(ctx, TGO_E_UNSUPPORTED, "multi-source BFS levels are < 65536");
+    if ((rc = ms_planes_for(ctx, level + 1))) return rc;
+    HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
+    HIP_TRY(hipMemsetAsync(fr_next, 0, g.n * 8, st));
+    int64_t npairs = 0;
+    for (int r = 0; r < nslices; ++r) {
+        if (recv_counts[r] < 0 || recv_counts[r] > g.n) return fail(ctx, TGO_E_INVALID, "ms_settle_pairs: bad count");
+        npairs += recv_counts[r];
+    }
+    HIP_TRY(k_ms_or_pairs(recv, npairs, fr_next, st));
+    const int nxt = ctx->part_cur ^ 1;
+    HIP_TRY(k_ms_settle(push_view(g, TGO_SCOPE_BOTH_E), g.n, s.ms_vis, fr_next, ms_planes(ctx), s.q[nxt], s.qdeg, s.cnt,
+                        level + 1, st));
+    ctx->part_cur = nxt;
+    return part_counts(ctx, counts);
+}
+
 int tgo_part_ms_end(tgo_ctx* ctx, int64_t* reached, int64_t* entries) {
     int rc = part_check(ctx);
     if (rc) return rc;

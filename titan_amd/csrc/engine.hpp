@@ -167,6 +167,8 @@ struct Scratch {
     int64_t* ms_seeds = nullptr;    // 64
     unsigned long long* ms_stat = nullptr;   // 128: reached[64], entries[64]
     int32_t ms_nsrc = 0;
+    int64_t* pk_cnt = nullptr;      // partitioned sparse exchange: per-chunk pair counts
+    int64_t* pk_off = nullptr;      // and their exclusive scan (n_global / kPackChunk + 1 each)
     // partitioned delta-stepping (allocated on first use)
     int64_t* ds_rbest = nullptr;    // n_global: best distance sent to each remote vertex
     uint64_t* ds_rmark = nullptr;   // n_global bits: remote vertices improved this phase
@@ -232,6 +234,10 @@ hipError_t k_ms_reach(const View& v, const uint64_t* vis, int64_t n_active, int 
 hipError_t k_ms_extract(LevelPlanes lvl, int nplanes, const uint64_t* vis, const int32_t* perm, int r, int64_t* dist,
                         int64_t n, hipStream_t s);
 hipError_t k_or_slices(const uint64_t* recv, int nslices, int64_t n_local, uint64_t* out, hipStream_t s);
+constexpr int64_t kPackChunk = 2048;   // candidate words per wave in the sparse-exchange pack
+hipError_t k_ms_pack(bool write, uint64_t* cand, int64_t n_local, int64_t cps, int64_t nchunks, int64_t* cnt,
+                     const int64_t* offs, int64_t* send, hipStream_t s);
+hipError_t k_ms_or_pairs(const int64_t* pairs, int64_t npairs, uint64_t* nx, hipStream_t s);
 hipError_t k_part_td_mark(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen,
                           uint64_t* disc, const uint64_t* vb_local, int64_t lo, int64_t n_local, hipStream_t s);
 hipError_t k_part_claim(const View& push, const uint64_t* recv, int nslices, int64_t words, int64_t n_local,

@@ -248,6 +248,43 @@ __global__ void or_slices(const uint64_t* __restrict__ recv, int nslices, int64_
     }
 }
 
+// Partitioned sparse push exchange: the nonzero candidate words of every owner's slice
+// become (owner-local id, mask) pairs, rank-major and contiguous, so they go straight into
+// an all-to-all with split sizes.  Each slice is cut into chunks of kPackChunk words (a
+// multiple of 64, so a chunk never straddles slices); one wave owns one chunk.  Pass 0
+// counts the chunk's nonzero words (cnt[c]); an exclusive scan gives each chunk its first
+// pair; pass 1 writes the pairs in word order and clears the words (the candidate array is
+// zero again for the next level).  No atomics: the pair order is deterministic.
+template <bool kWrite>
+__global__ void __launch_bounds__(kBlock) ms_pack(uint64_t* __restrict__ cand, int64_t n_local, int64_t cps,
+        int64_t nchunks, int64_t* __restrict__ cnt, const int64_t* __restrict__ offs, int64_t* __restrict__ send) {
+    const int64_t c = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    if (c >= nchunks) return;
+    const int64_t r = c / cps, j = c - r * cps;
+    const int64_t w0 = r * n_local + j * kPackChunk;
+    const int64_t w1 = r * n_local + min(n_local, (j + 1) * kPackChunk);
+    int64_t base = kWrite ? offs[c] : 0;
+    for (int64_t g = w0; g < w1; g += 64) {
+        const int64_t i = g + lane();
+        const uint64_t m = cand[i];
+        const uint64_t bal = __ballot(m != 0);
+        if (kWrite && m) {
+            const int64_t p = base + __popcll(bal & ((1ULL << lane()) - 1ULL));
+            send[2 * p] = i - r * n_local;
+            send[2 * p + 1] = static_cast<int64_t>(m);
+            cand[i] = 0;
+        }
+        base += __popcll(bal);
+    }
+    if (!kWrite && lane() == 0) cnt[c] = base;
+}
+// Received pairs of one sender: OR the masks into the owned candidate words (several
+// senders may name one vertex).
+__global__ void ms_or_pairs(const int64_t* __restrict__ pairs, int64_t npairs, uint64_t* __restrict__ nx) {
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < npairs; k += (int64_t)gridDim.x * blockDim.x)
+        atomicOr(reinterpret_cast<unsigned long long*>(nx + pairs[2 * k]), static_cast<unsigned long long>(pairs[2 * k + 1]));
+}
+
 // Per-source reached vertices / entries (stats, untimed): 64 counters per block in LDS.
 __global__ void __launch_bounds__(kBlock) ms_reach(View v, const uint64_t* __restrict__ vis, int64_t n_active,
         int nsrc, unsigned long long* __restrict__ reached, unsigned long long* __restrict__ entries) {
@@ -320,6 +357,17 @@ hipError_t k_ms_settle(const View& push, int64_t n_active, uint64_t* vis, uint64
 hipError_t k_ms_reach(const View& v, const uint64_t* vis, int64_t n_active, int nsrc, unsigned long long* reached,
                       unsigned long long* entries, hipStream_t s) {
     ms_reach<<<grid_for(n_active, 2048), kBlock, 0, s>>>(v, vis, n_active, nsrc, reached, entries);
+    return hipGetLastError();
+}
+hipError_t k_ms_pack(bool write, uint64_t* cand, int64_t n_local, int64_t cps, int64_t nchunks, int64_t* cnt,
+                     const int64_t* offs, int64_t* send, hipStream_t s) {
+    const unsigned blocks = static_cast<unsigned>((nchunks * 64 + kBlock - 1) / kBlock);
+    if (write) ms_pack<true><<<blocks, kBlock, 0, s>>>(cand, n_local, cps, nchunks, cnt, offs, send);
+    else ms_pack<false><<<blocks, kBlock, 0, s>>>(cand, n_local, cps, nchunks, cnt, offs, send);
+    return hipGetLastError();
+}
+hipError_t k_ms_or_pairs(const int64_t* pairs, int64_t npairs, uint64_t* nx, hipStream_t s) {
+    if (npairs > 0) ms_or_pairs<<<grid_for(npairs, 4096), kBlock, 0, s>>>(pairs, npairs, nx);
     return hipGetLastError();
 }
 hipError_t k_or_slices(const uint64_t* recv, int nslices, int64_t n_local, uint64_t* out, hipStream_t s) {

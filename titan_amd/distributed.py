@@ -115,6 +115,16 @@ class HipPartBackend:
     def ms_settle(self, level, recv, nslices, fr_next):
         return self._counts("tgo_part_ms_settle", level, self._vp(recv), nslices, self._vp(fr_next))
 
+    def ms_pack(self, cand, send, nranks):
+        sc = np.zeros(nranks, np.int64)
+        self.e.part_call("tgo_part_ms_pack", self._vp(cand), nranks, self._vp(send), L.ptr(sc, C.c_int64))
+        return sc
+
+    def ms_settle_pairs(self, level, recv, recv_counts, fr_next):
+        rc = np.ascontiguousarray(recv_counts, np.int64)
+        return self._counts("tgo_part_ms_settle_pairs", level, self._vp(recv), L.ptr(rc, C.c_int64), len(rc),
+                            self._vp(fr_next))
+
     def ms_end(self, nseeds, stats=True):
         if not stats:
             self.e.part_call("tgo_part_ms_end", None, None)
@@ -220,11 +230,27 @@ def distributed_bfs(backend, seed: int, max_depth: int, alpha: float = 15.0, bet
     return out, reached, levels
 
 
-def distributed_msbfs(backend, seeds, max_depth: int, ms_alpha: float = 12.0, stats: bool = True, group=None):
+def _exchange_pairs(send, counts, recv, dev, group):
+    """all_to_all of the per-rank pair counts, then of the (id, value) int64 pairs with
+    split sizes; returns the received count per sender."""
+    sct = torch.from_numpy(2 * np.asarray(counts, np.int64)).to(dev)
+    rct = torch.empty_like(sct)
+    dist.all_to_all_single(rct, sct, group=group)
+    ins = [int(x) for x in sct.cpu()]
+    outs = [int(x) for x in rct.cpu()]
+    dist.all_to_all_single(recv[:sum(outs)], send[:sum(ins)], output_split_sizes=outs, input_split_sizes=ins,
+                           group=group)
+    return np.asarray(outs, np.int64) // 2
+
+
+def distributed_msbfs(backend, seeds, max_depth: int, ms_alpha: float = 12.0, stats: bool = True, group=None,
+                      sparse_exchange: bool = True):
     """Up to 64 ShortestDistance programs with unit weights over bothE, run together with
     bit-parallel frontier masks on a vertex-partitioned graph.
       dense level : all_gather of owned frontier masks (8 bytes per vertex) -> local pull
-      sparse level: local push into global candidate masks -> all_to_all of slices -> settle
+      sparse level: local push into global candidate masks -> pack the nonzero ones into
+                    (owner-local id, mask) pairs -> all_to_all with split sizes -> settle
+                    (sparse_exchange=False: all_to_all of the whole n_global-word slices)
     Returns (per-seed global reached vertices, per-seed reached entries, levels)."""
     world = dist.get_world_size(group)
     nseeds = len(seeds)
@@ -233,7 +259,7 @@ def distributed_msbfs(backend, seeds, max_depth: int, ms_alpha: float = 12.0, st
     frn = backend.tensor(backend.n_local, torch.int64)
     fr_global = backend.tensor(backend.n_global, torch.int64)
     cand = backend.tensor(backend.n_global, torch.int64)
-    recv = backend.tensor(backend.n_global, torch.int64)
+    send = recv = None
     total = _allreduce_counts([backend.total_entries, 0], dev)[0]
     nf, mf = _allreduce_counts(backend.ms_begin(seeds, fr), dev)
     levels = 0
@@ -243,7 +269,16 @@ def distributed_msbfs(backend, seeds, max_depth: int, ms_alpha: float = 12.0, st
         if mf * ms_alpha > total:
             dist.all_gather_into_tensor(fr_global, fr, group=group)
             c = backend.ms_pull(level, fr_global, frn)
+        elif sparse_exchange:
+            if send is None:
+                send = backend.tensor(2 * backend.n_global, torch.int64)
+                recv = backend.tensor(2 * backend.n_global, torch.int64)
+            backend.ms_push(level, fr, cand)           # cand is all-zero here: ms_pack clears it
+            rcounts = _exchange_pairs(send, backend.ms_pack(cand, send, world), recv, dev, group)
+            c = backend.ms_settle_pairs(level, recv, rcounts, frn)
         else:
+            if recv is None:
+                recv = backend.tensor(backend.n_global, torch.int64)
             cand.zero_()
             backend.ms_push(level, fr, cand)
             dist.all_to_all_single(recv, cand, group=group)
