@@ -245,7 +245,7 @@ def run_partitioned(args, world, rank, local_rank):
     import torch.distributed as dist
     from titan_amd import Engine
     from titan_amd import _lib as L
-    from titan_amd.distributed import (HipPartBackend, all_gather_layout, distributed_bfs, distributed_msbfs,
+    from titan_amd.distributed import (HipPartBackend, all_gather_layout, exchange_stream, distributed_bfs, distributed_msbfs,
                                        distributed_pagerank, partition_range)
     torch.cuda.set_device(local_rank)
     dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
@@ -267,7 +267,7 @@ def run_partitioned(args, world, rank, local_rank):
     src, dst = src[:cnt.value], dst[:cnt.value]
     wgt = wgt[:cnt.value] if wgt is not None else None
     log(f"rmat scale {scale} partition [{lo},{hi}) of {world}: {cnt.value} edges in {time.perf_counter() - t0:.1f}s")
-    stream = torch.cuda.current_stream().cuda_stream
+    stream = exchange_stream()     # kernels and RCCL collectives ordered on one (non-default) stream
     t0 = time.perf_counter()
     lay = all_gather_layout(src, dst, n, lo, hi, torch.device("cuda", local_rank)) if args.layout else None
     bfs_be = HipPartBackend(Engine(device=local_rank, host_threads=16, stream=stream)

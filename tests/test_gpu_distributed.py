@@ -11,7 +11,7 @@ import torch
 import fulgora as fr
 from titan_amd import Engine, rmat_edges
 from titan_amd import _lib as L
-from titan_amd.distributed import HipPartBackend, local_layout, partition_range
+from titan_amd.distributed import HipPartBackend, exchange_stream, local_layout, partition_range
 
 pytestmark = pytest.mark.gpu
 ABSENT = L.DIST_ABSENT
@@ -172,7 +172,7 @@ def make_backends(world, n, src, dst, scope, weight=None, layout=False):
     backends = []
     for r in range(world):
         lo, hi = partition_range(n, world, r)
-        eng = Engine(stream=torch.cuda.current_stream().cuda_stream).load_partition(
+        eng = Engine(stream=exchange_stream()).load_partition(
             n, lo, hi, src, dst, scope, weight=weight, apply_cap=False, layout=lay)
         backends.append(HipPartBackend(eng, n, lo, hi))
     return backends

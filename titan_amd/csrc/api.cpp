@@ -917,6 +917,14 @@ int tgo_part_bfs_begin(tgo_ctx* ctx, int64_t seed_global, uint64_t* nb_local, in
     return TGO_OK;
 }
 
+// Entry points that leave work queued: on a ctx-owned stream the caller cannot order its
+// collectives after that work, so finish it before returning; on the caller's stream the
+// work stays stream-ordered (the caller's collectives follow it on the same stream).
+static int part_done(tgo_ctx* ctx) {
+    if (ctx->own_stream) HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return TGO_OK;
+}
+
 int tgo_part_bfs_td(tgo_ctx* ctx, int32_t level, uint64_t* disc_global) {
     int rc = part_check(ctx);
     if (rc) return rc;
@@ -929,7 +937,7 @@ int tgo_part_bfs_td(tgo_ctx* ctx, int32_t level, uint64_t* disc_global) {
         if ((rc = scan_frontier(ctx, ctx->part_qlen))) return rc;
         HIP_TRY(k_part_td_mark(push, s.q[ctx->part_cur], s.qpre, ctx->part_qlen, disc_global, s.vb, g.lo, g.n, st));
     }
-    return TGO_OK;
+    return part_done(ctx);
 }
 
 int tgo_part_bfs_claim(tgo_ctx* ctx, int32_t level, const uint64_t* recv, int32_t nslices,
@@ -1066,7 +1074,7 @@ int tgo_part_ms_push(tgo_ctx* ctx, int32_t level, const uint64_t* fr_local, uint
         HIP_TRY(k_ms_push(push_view(g, TGO_SCOPE_BOTH_E), s.q[ctx->part_cur], s.qpre, ctx->part_qlen, fr_local,
                           nullptr, cand_global, ctx->stream));
     }
-    return TGO_OK;
+    return part_done(ctx);
 }
 
 int tgo_part_ms_settle(tgo_ctx* ctx, int32_t level, const uint64_t* recv, int32_t nslices, uint64_t* fr_next,
@@ -1111,7 +1119,7 @@ int tgo_part_ms_pack(tgo_ctx* ctx, uint64_t* cand_global, int32_t nranks, int64_
     HIP_TRY(hipStreamSynchronize(st));
     for (int r = 0; r < nranks; ++r) send_counts[r] = off[r + 1] - off[r];
     if (off[nranks] > 0) HIP_TRY(k_ms_pack(true, cand_global, g.n, cps, nchunks, s.pk_cnt, s.pk_off, send, st));
-    return TGO_OK;
+    return part_done(ctx);
 }
 
 int tgo_part_ms_settle_pairs(tgo_ctx* ctx, int32_t level, const int64_t* recv, const int64_t* recv_counts,
@@ -1188,7 +1196,7 @@ int tgo_part_pr_begin(tgo_ctx* ctx, const tgo_pr_args* a, double* contrib_local)
     HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
     // iteration 1 (PageRankVertexProgram.java:78-83) on the owned rows
     HIP_TRY(k_pr_init(g.out, s.vec[0], contrib_local, reinterpret_cast<double*>(s.dist), 1.0 / N, g.n, ctx->stream));
-    return TGO_OK;
+    return part_done(ctx);
 }
 
 int tgo_part_pr_step(tgo_ctx* ctx, const double* contrib_global, double* contrib_local) {
@@ -1199,7 +1207,7 @@ int tgo_part_pr_step(tgo_ctx* ctx, const double* contrib_global, double* contrib
     // owned rows gather over their IN lists (global source ids) from the gathered vector
     HIP_TRY(k_pr_iter(g.in, g.rb_in, contrib_global, s.vec[0], reinterpret_cast<double*>(s.dist), contrib_local,
                       s.partial, ctx->part_alpha, ctx->part_base, g.n, ctx->stream));
-    return TGO_OK;
+    return part_done(ctx);
 }
 
 int tgo_part_pr_end(tgo_ctx* ctx, double* pr_local) {

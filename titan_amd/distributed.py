@@ -61,10 +61,26 @@ def all_gather_layout(src, dst, n_global: int, lo: int, hi: int, device, group=N
     return out.cpu().numpy()
 
 
+def exchange_stream() -> int:
+    """The HIP stream handle the partitioned engine must share with torch's collectives.
+    torch's default stream has handle 0, which the C-ABI reads as "ctx-owned stream" (not
+    ordered with torch's work), so switch this thread to a dedicated side stream first."""
+    cur = torch.cuda.current_stream()
+    if cur.cuda_stream == 0:
+        cur = torch.cuda.Stream()
+        torch.cuda.set_stream(cur)
+    return cur.cuda_stream
+
+
 class HipPartBackend:
-    """Local steps on this rank's GPU through the C-ABI (titan_gpu_olap_part.h)."""
+    """Local steps on this rank's GPU through the C-ABI (titan_gpu_olap_part.h).  The
+    engine runs on torch's current (non-default) stream, so its kernels and the RCCL
+    collectives of the driver are ordered on one stream (see exchange_stream)."""
 
     def __init__(self, engine, n_global, lo, hi):
+        if engine.stream == 0 or engine.stream != torch.cuda.current_stream().cuda_stream:
+            raise ValueError("HipPartBackend: the Engine must run on torch's current non-default stream "
+                             "(Engine(stream=exchange_stream()))")
         self.e = engine
         self.n_global, self.lo, self.hi = n_global, lo, hi
         self.n_local = hi - lo

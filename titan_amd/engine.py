@@ -48,6 +48,9 @@ class Schema:
 class Engine:
     def __init__(self, device: int = 0, partition_bits: int = 5, host_threads: int = 0,
                  hard_query_limit: int = 100000, stream: int = 0):
+        """stream: a HIP stream handle the ctx runs on (stream-ordered with the caller's
+        work); 0 = a ctx-owned stream (the handle of torch's default stream is also 0, so a
+        caller that wants ordering with torch must run on a non-default stream)."""
         self.lib = L.load()
         o = L.Options()
         self.lib.tgo_default_options(C.byref(o))
@@ -56,6 +59,7 @@ class Engine:
         o.host_threads = host_threads
         o.hard_query_limit = hard_query_limit
         o.stream = stream or None
+        self.stream = int(stream or 0)
         h = C.c_void_p()
         rc = self.lib.tgo_create(C.byref(o), C.byref(h))
         if rc != L.TGO_OK:
