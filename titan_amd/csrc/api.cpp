@@ -98,7 +98,16 @@ int threads_of(const tgo_ctx* ctx) {
     return std::max(1, std::min(t, 64));
 }
 
-int upload_graph(tgo_ctx* ctx, HostGraph& h) {
+// TGO_PR_SEGMENTS=1 builds the XCD-segmented PageRank lists (SegGather); off by default:
+// measured on MI355X, RMAT-24, it is slower than the plain CSR-adaptive gather (2.41 vs
+// 1.84 ms/update, profiles/r01n_kernel_stats.csv) — the per-(row, segment) partial sums
+// cost ~0.4 ms and the gathers did not speed up enough to pay for them.
+bool want_segments(int64_t nnz) {
+    const char* e = std::getenv("TGO_PR_SEGMENTS");
+    return nnz > 0 && e && e[0] == '1';
+}
+
+int upload_graph(tgo_ctx* ctx, HostGraph& h, bool allow_segments = true) {
     DevGraph& g = ctx->g;
     g.n = h.n;
     g.scope = h.scope;
@@ -144,6 +153,26 @@ int upload_graph(tgo_ctx* ctx, HostGraph& h) {
     HIP_TRY(blocks(h.out.off, g.rb_out));
     HIP_TRY(blocks(h.in.off, g.rb_in));
     g.rb_out_ready = g.rb_in_ready = true;
+    g.seg_in = SegGather();
+    g.seg_in_ready = false;
+    if (allow_segments && h.scope != TGO_SCOPE_BOTH_E && want_segments(static_cast<int64_t>(h.in.adj.size())) &&
+        h.in.adj.size() < (size_t(1) << 31)) {
+        HostSegments hs;
+        build_segments(h.in.off, h.in.adj, kTile, kMaxRows, hs);
+        SegGather& sg = g.seg_in;
+        sg.npairs = static_cast<int64_t>(hs.pslot.size());
+        sg.nblocks = static_cast<int64_t>(hs.sb_beg.size());
+        sg.max_seg_blocks = hs.max_seg_blocks;
+        sg.base = hs.base;
+        HIP_TRY(upload(ctx, sg.poff, hs.poff));
+        HIP_TRY(upload(ctx, sg.adj, hs.adj));
+        HIP_TRY(upload(ctx, sg.pslot, hs.pslot));
+        HIP_TRY(upload(ctx, sg.row_ptr, hs.row_ptr));
+        HIP_TRY(upload(ctx, sg.sb_beg, hs.sb_beg));
+        HIP_TRY(upload(ctx, sg.sb_end, hs.sb_end));
+        HIP_TRY(dev_alloc(ctx, sg.partial, sg.npairs));
+        g.seg_in_ready = true;
+    }
     // scratch
     Scratch& s = ctx->sc;
     const int64_t n = h.n, words = (n + 63) / 64 + 1;
@@ -782,7 +811,11 @@ int tgo_pagerank(tgo_ctx* ctx, const tgo_pr_args* a, double* pr_out) {
         HIP_TRY(k_pr_init(g.out, edge_count, contrib, pr, 1.0 / N, n, st));
         const double base = (1.0 - a->alpha) / N;
         for (int it = 2; it <= a->max_iterations; ++it) {
-            HIP_TRY(k_pr_iter(g.in, g.rb_in, contrib, edge_count, pr, contrib_next, s.partial, a->alpha, base, n, st));
+            if (g.seg_in_ready)
+                HIP_TRY(k_pr_iter_seg(g.seg_in, contrib, edge_count, pr, contrib_next, a->alpha, base, n, st));
+            else
+                HIP_TRY(k_pr_iter(g.in, g.rb_in, contrib, edge_count, pr, contrib_next, s.partial, a->alpha, base, n,
+                                  st));
             std::swap(contrib, contrib_next);
         }
     }
@@ -860,7 +893,7 @@ int tgo_load_partition_layout(tgo_ctx* ctx, int64_t n_global, int64_t lo, int64_
     if (rc) return fail(ctx, rc, err);
     free_graph(ctx);
     ctx->staging = RowStaging();
-    rc = upload_graph(ctx, h);
+    rc = upload_graph(ctx, h, false);     // partitioned PageRank gathers global ids: plain CSR
     if (rc) return rc;
     ctx->g.partitioned = true;
     ctx->g.lo = lo;

@@ -104,6 +104,30 @@ struct RowBlocks {
     std::vector<int64_t> h_blk;
 };
 
+// Source-segmented in-lists for the one-GPU PageRank gather.  Source u belongs to segment
+// (u >> kSegShift) & (kSeg-1): 16 fp64 messages = one 128-byte line per granule, so the
+// segments split the message vector's lines 8 ways, interleaved (hot lines of the
+// degree-grouped order land in every segment).  Blocks of segment s are launched at
+// blockIdx % 8 == s, i.e. (with the observed round-robin dispatch) on one XCD, so each
+// XCD's 4 MB L2 only caches its eighth of the message vector.  Every (row, segment) run of
+// entries is a "pair" (split at kTile entries); a pair's sum goes to its slot, slots are
+// ordered (row, segment, chunk) and a finalize adds a row's slots in that order — a fixed
+// order, so results are bitwise reproducible.
+constexpr int kSeg = 8;
+constexpr int kSegShift = 4;
+struct SegBase { int64_t b[kSeg + 1]; };     // segment s owns blocks [b[s], b[s+1])
+struct SegGather {
+    int64_t npairs = 0, nblocks = 0, max_seg_blocks = 0;
+    int64_t* poff = nullptr;    // npairs+1 entry offsets into adj (segment-major)
+    int32_t* adj = nullptr;     // in-entries regrouped by segment
+    int32_t* pslot = nullptr;   // pair -> slot
+    int64_t* row_ptr = nullptr; // n+1: row r's slots
+    int64_t* sb_beg = nullptr;  // per block: first pair
+    int64_t* sb_end = nullptr;  // per block: end pair
+    double* partial = nullptr;  // per slot
+    SegBase base{};
+};
+
 struct DevGraph {
     int64_t n = 0;
     int32_t* perm = nullptr;    // row-order dense id -> internal id (device)
@@ -118,6 +142,8 @@ struct DevGraph {
     int64_t lo = 0, n_global = 0;
     RowBlocks rb_out, rb_in;    // CSR-adaptive blocks per pull list
     bool rb_out_ready = false, rb_in_ready = false;
+    SegGather seg_in;           // segmented in-lists (one-GPU PageRank); npairs 0 = not built
+    bool seg_in_ready = false;
 };
 
 // Multi-source BFS levels as bit planes: the level of (v, source r) is
@@ -252,6 +278,8 @@ hipError_t k_pr_iter(const DevCsr& in, const RowBlocks& rb, const double* contri
                      const double* edge_count, double* pr, double* contrib_next, double* partial,
                      double alpha, double base, int64_t n, hipStream_t s);
 hipError_t k_fill_f64(double* p, double v, int64_t n, hipStream_t s);
+hipError_t k_pr_iter_seg(const SegGather& sg, const double* contrib, const double* edge_count, double* pr,
+                         double* contrib_next, double alpha, double base, int64_t n, hipStream_t s);
 hipError_t k_walk_iter(const DevCsr& out, const RowBlocks& rb, const int32_t* prev, int32_t* next,
                        int32_t* partial, int64_t n, hipStream_t s);
 
@@ -263,6 +291,15 @@ void build_row_blocks(const std::vector<int64_t>& off, int64_t tile, int64_t max
                       std::vector<int64_t>& blk, std::vector<int64_t>& chunk_row,
                       std::vector<int64_t>& chunk_beg, std::vector<int64_t>& chunk_end,
                       std::vector<int64_t>& long_row, std::vector<int64_t>& long_chunk);
+// Host side of SegGather: regroup a CSR's entries by source segment (see SegGather).
+struct HostSegments {
+    std::vector<int64_t> poff, row_ptr, sb_beg, sb_end;
+    std::vector<int32_t> adj, pslot;
+    SegBase base{};
+    int64_t max_seg_blocks = 0;
+};
+void build_segments(const std::vector<int64_t>& off, const std::vector<int32_t>& adj, int64_t tile,
+                    int64_t max_pairs, HostSegments& hs);
 
 constexpr int64_t kTile = 2048;      // entries per CSR-adaptive block (16 KB of fp64 in LDS)
 constexpr int64_t kMaxRows = 1024;   // rows per CSR-adaptive block

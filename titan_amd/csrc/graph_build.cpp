@@ -687,4 +687,69 @@ void build_row_blocks(const std::vector<int64_t>& off, int64_t tile, int64_t max
     }
 }
 
+// ------------------------------------------------------------------ source segments
+// SegGather layout (engine.hpp): pass 1 counts every row's entries per segment to size
+// the pairs and slots; pass 2 lays the pairs of each segment out in row order and
+// scatters every row's entries into its segment runs, keeping list order inside a run.
+void build_segments(const std::vector<int64_t>& off, const std::vector<int32_t>& adj, int64_t tile,
+                    int64_t max_pairs, HostSegments& hs) {
+    const int64_t n = static_cast<int64_t>(off.size()) - 1;
+    auto seg = [](int32_t u) { return (static_cast<uint32_t>(u) >> kSegShift) & (kSeg - 1); };
+    hs.row_ptr.assign(n + 1, 0);
+    int64_t seg_pairs[kSeg] = {}, seg_entries[kSeg] = {};
+    for (int64_t r = 0; r < n; ++r) {
+        int64_t c[kSeg] = {};
+        for (int64_t k = off[r]; k < off[r + 1]; ++k) ++c[seg(adj[k])];
+        int64_t np = 0;
+        for (int s = 0; s < kSeg; ++s) {
+            const int64_t p = (c[s] + tile - 1) / tile;
+            np += p;
+            seg_pairs[s] += p;
+            seg_entries[s] += c[s];
+        }
+        hs.row_ptr[r + 1] = hs.row_ptr[r] + np;
+    }
+    const int64_t npairs = hs.row_ptr[n];
+    int64_t pcur[kSeg], ecur[kSeg];
+    pcur[0] = ecur[0] = 0;
+    for (int s = 1; s < kSeg; ++s) {
+        pcur[s] = pcur[s - 1] + seg_pairs[s - 1];
+        ecur[s] = ecur[s - 1] + seg_entries[s - 1];
+    }
+    int64_t pbase[kSeg + 1];
+    for (int s = 0; s < kSeg; ++s) pbase[s] = pcur[s];
+    pbase[kSeg] = npairs;
+    hs.poff.assign(npairs + 1, 0);
+    hs.pslot.assign(npairs, 0);
+    hs.adj.assign(adj.size(), 0);
+    for (int64_t r = 0; r < n; ++r) {
+        int64_t c[kSeg] = {};
+        for (int64_t k = off[r]; k < off[r + 1]; ++k) ++c[seg(adj[k])];
+        int64_t slot = hs.row_ptr[r];
+        for (int s = 0; s < kSeg; ++s)
+            for (int64_t k = 0; k < c[s]; k += tile) {
+                hs.poff[pcur[s]] = ecur[s] + k;
+                hs.pslot[pcur[s]++] = static_cast<int32_t>(slot++);
+            }
+        for (int64_t k = off[r]; k < off[r + 1]; ++k) hs.adj[ecur[seg(adj[k])]++] = adj[k];
+    }
+    hs.poff[npairs] = static_cast<int64_t>(adj.size());
+    // blocks: greedy per segment, <= tile entries and <= max_pairs pairs (every pair <= tile)
+    hs.sb_beg.clear(); hs.sb_end.clear();
+    hs.max_seg_blocks = 0;
+    for (int s = 0; s < kSeg; ++s) {
+        hs.base.b[s] = static_cast<int64_t>(hs.sb_beg.size());
+        int64_t p = pbase[s];
+        while (p < pbase[s + 1]) {
+            int64_t e = p;
+            while (e < pbase[s + 1] && e - p < max_pairs && hs.poff[e + 1] - hs.poff[p] <= tile) ++e;
+            hs.sb_beg.push_back(p);
+            hs.sb_end.push_back(e);
+            p = e;
+        }
+        hs.max_seg_blocks = std::max<int64_t>(hs.max_seg_blocks, static_cast<int64_t>(hs.sb_beg.size()) - hs.base.b[s]);
+    }
+    hs.base.b[kSeg] = static_cast<int64_t>(hs.sb_beg.size());
+}
+
 }  // namespace tgo

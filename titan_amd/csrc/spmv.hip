@@ -156,6 +156,60 @@ __global__ void finalize_long(const int64_t* __restrict__ long_row, const int64_
     }
 }
 
+// Segmented PageRank gather (SegGather, engine.hpp).  Block b serves segment b % 8 (its
+// XCD under round-robin dispatch): the block's pairs' messages are gathered into LDS, each
+// pair reduced from LDS (thread-per-pair for many short pairs, wave-per-pair otherwise)
+// and written to its slot.  Blocks past the segment's block count exit at once.
+__global__ void __launch_bounds__(kBlock) seg_gather(const int64_t* __restrict__ poff,
+        const int32_t* __restrict__ adj, const int64_t* __restrict__ sb_beg, const int64_t* __restrict__ sb_end,
+        SegBase bb, const int32_t* __restrict__ pslot, PrOp op, double* __restrict__ partial) {
+    __shared__ double s_val[kTile];
+    const int sg = static_cast<int>(blockIdx.x & (kSeg - 1));
+    const int64_t j = bb.b[sg] + (blockIdx.x >> 3);
+    if (j >= bb.b[sg + 1]) return;
+    const int64_t p0 = sb_beg[j], p1 = sb_end[j];
+    const int64_t s0 = poff[p0];
+    const int64_t nnz = poff[p1] - s0;                 // <= kTile by construction
+    {
+        double val[kPer];
+        gather_tile(adj, s0, nnz, op, val);
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const int x = threadIdx.x + k * kBlock;
+            if (x < nnz) s_val[x] = val[k];
+        }
+    }
+    __syncthreads();
+    if (p1 - p0 > 64) {
+        for (int64_t p = p0 + threadIdx.x; p < p1; p += kBlock) {
+            double sum = 0.0;
+            const int64_t e = poff[p + 1] - s0;
+            for (int64_t k = poff[p] - s0; k < e; ++k) sum += s_val[k];
+            partial[pslot[p]] = sum;
+        }
+    } else {
+        const int wave = threadIdx.x >> 6;
+        for (int64_t p = p0 + wave; p < p1; p += kBlock / 64) {
+            double sum = 0.0;
+            const int64_t e = poff[p + 1] - s0;
+            for (int64_t k = poff[p] - s0 + lane(); k < e; k += 64) sum += s_val[k];
+            sum = wave_sum(sum);
+            if (lane() == 0) partial[pslot[p]] = sum;
+        }
+    }
+}
+
+// A row's slots added in (segment, chunk) order, then the PageRank update of the row.
+__global__ void seg_finalize(const int64_t* __restrict__ row_ptr, const double* __restrict__ partial, int64_t n,
+                             PrFinal fin) {
+    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+        double sum = 0.0;
+        const int64_t e = row_ptr[r + 1];
+        for (int64_t k = row_ptr[r]; k < e; ++k) sum += partial[k];
+        fin(r, sum);
+    }
+}
+
 __global__ void pr_init(const int64_t* __restrict__ out_off, double* edge_count, double* contrib,
                         double* pr, double inv_n, int64_t n) {
     for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x) {
@@ -209,6 +263,17 @@ hipError_t k_pr_iter(const DevCsr& in, const RowBlocks& rb, const double* contri
     PrOp op{contrib};
     PrFinal fin{edge_count, pr, contrib_next, alpha, base};
     return run_gather(in, rb, op, fin, partial, s);
+}
+hipError_t k_pr_iter_seg(const SegGather& sg, const double* contrib, const double* edge_count, double* pr,
+                         double* contrib_next, double alpha, double base, int64_t n, hipStream_t s) {
+    if (sg.max_seg_blocks > 0)
+        seg_gather<<<static_cast<unsigned>(sg.max_seg_blocks * kSeg), kBlock, 0, s>>>(
+            sg.poff, sg.adj, sg.sb_beg, sg.sb_end, sg.base, sg.pslot, PrOp{contrib}, sg.partial);
+    int64_t g = (n + kBlock - 1) / kBlock;
+    g = g < 1 ? 1 : (g > 8192 ? 8192 : g);
+    seg_finalize<<<static_cast<unsigned>(g), kBlock, 0, s>>>(sg.row_ptr, sg.partial, n,
+                                                             PrFinal{edge_count, pr, contrib_next, alpha, base});
+    return hipGetLastError();
 }
 hipError_t k_walk_iter(const DevCsr& out, const RowBlocks& rb, const int32_t* prev, int32_t* next,
                        int32_t* partial, int64_t n, hipStream_t s) {
