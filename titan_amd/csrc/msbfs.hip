@@ -41,36 +41,64 @@ __device__ __forceinline__ int32_t view_entry(const View& v, int64_t u, int64_t 
 
 // Record the level of every newly reached source of v (bit k of the level goes into
 // plane k: one coalesced 8-byte OR per set level bit, the lane owns v); append v to the
-// next queue.
+// next queue.  Block-aggregated: every thread of the block calls it in the same trip (the
+// callers' loops are block-uniform), the block reserves its queue slots with ONE atomicAdd,
+// and the frontier-degree / source-bit sums stay in the wave-leader's registers (mf, bits)
+// until discover_flush.  One contended counter word takes ~88 atomics/us
+// (MI355X_MICROARCH.md, dequeue), so per-wave counter atomics cost ~1.6 ms per dense level
+// on RMAT-24 — more than the level's gathers.
+constexpr int kWaves = kBlock / 64;
+struct DiscoverLds { unsigned long long cnt[kWaves]; unsigned long long base; };
 __device__ __forceinline__ void discover(int64_t v, uint64_t fresh, int32_t level, LevelPlanes pl,
-                                         const View& push, int32_t* qn, int64_t* qdeg, Counters* cnt) {
+                                         const View& push, int32_t* qn, int64_t* qdeg, Counters* cnt,
+                                         DiscoverLds& sh, unsigned long long& mf, unsigned long long& bits) {
     const bool take = fresh != 0;
     if (take) {
         for (int k = 0; k < kLevelPlanes && (level >> k); ++k)
             if ((level >> k) & 1) pl.p[k * pl.stride + v] |= fresh;
     }
     const unsigned long long mask = __ballot(take);
-    if (!mask) return;
-    const int leader = __ffsll(static_cast<long long>(mask)) - 1;
+    const int wave = threadIdx.x >> 6;
     const int rank = __popcll(mask & ((1ULL << lane()) - 1ULL));
-    const int64_t deg = take ? view_degree(push, v) : 0;
-    int64_t dsum = deg;
-    unsigned long long bits = take ? static_cast<unsigned long long>(__popcll(fresh)) : 0ULL;
-    for (int off = 32; off > 0; off >>= 1) {
-        dsum += __shfl_xor(dsum, off, 64);
-        bits += __shfl_xor(bits, off, 64);
+    int64_t deg = 0;
+    if (mask) {
+        deg = take ? view_degree(push, v) : 0;
+        int64_t dsum = deg;
+        unsigned long long b = take ? static_cast<unsigned long long>(__popcll(fresh)) : 0ULL;
+        for (int off = 32; off > 0; off >>= 1) {
+            dsum += __shfl_xor(dsum, off, 64);
+            b += __shfl_xor(b, off, 64);
+        }
+        mf += static_cast<unsigned long long>(dsum);
+        bits += b;
     }
-    unsigned long long base = 0;
-    if (lane() == leader) {
-        base = atomicAdd(&cnt->qlen, static_cast<unsigned long long>(__popcll(mask)));
-        atomicAdd(&cnt->mf, static_cast<unsigned long long>(dsum));
-        atomicAdd(&cnt->red[0], bits);
+    if (lane() == 0) sh.cnt[wave] = static_cast<unsigned long long>(__popcll(mask));
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+        for (int w = 0; w < kWaves; ++w) { const unsigned long long c = sh.cnt[w]; sh.cnt[w] = t; t += c; }
+        sh.base = t ? atomicAdd(&cnt->qlen, t) : 0ULL;
     }
-    base = __shfl(base, leader, 64);
+    __syncthreads();
     if (take) {
-        qn[base + rank] = static_cast<int32_t>(v);
-        qdeg[base + rank] = deg;
+        const unsigned long long slot = sh.base + sh.cnt[wave] + static_cast<unsigned long long>(rank);
+        qn[slot] = static_cast<int32_t>(v);
+        qdeg[slot] = deg;
     }
+}
+// End of a discovering kernel (block-uniform): one atomicAdd per block for each sum.
+__device__ __forceinline__ void discover_flush(Counters* cnt, DiscoverLds& sh, unsigned long long mf,
+                                               unsigned long long bits) {
+    __shared__ unsigned long long s_mf[kWaves], s_bits[kWaves];
+    if (lane() == 0) { s_mf[threadIdx.x >> 6] = mf; s_bits[threadIdx.x >> 6] = bits; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long a = 0, c = 0;
+        for (int w = 0; w < kWaves; ++w) { a += s_mf[w]; c += s_bits[w]; }
+        if (a) atomicAdd(&cnt->mf, a);
+        if (c) atomicAdd(&cnt->red[0], c);
+    }
+    (void)sh;
 }
 
 // Level 0 is all-zero level bits: seeding only marks vis/fr.
@@ -94,9 +122,13 @@ __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t 
         const uint64_t* __restrict__ fr, uint64_t* __restrict__ vis, uint64_t* __restrict__ nx,
         LevelPlanes lvl, int32_t* __restrict__ qn, int64_t* __restrict__ qdeg,
         Counters* cnt, int32_t next_level) {
-    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    __shared__ DiscoverLds sh;
+    unsigned long long mf = 0, bits = 0;
     const int64_t words = (n_active + 63) >> 6;
-    for (int64_t wd = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; wd < words; wd += nwaves) {
+    // block-uniform trips (discover synchronises the block): wave w of the block takes word
+    // b + w; words past the end run as all-closed lanes
+    for (int64_t b = static_cast<int64_t>(blockIdx.x) * kWaves; b < words; b += static_cast<int64_t>(gridDim.x) * kWaves) {
+        const int64_t wd = b + (threadIdx.x >> 6);
         const int64_t v = (wd << 6) + lane();
         const uint64_t seen = v < n_active ? vis[v] : full;
         const uint64_t open = full & ~seen;
@@ -160,8 +192,9 @@ __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t 
             nx[v] = fresh;
             if (fresh) vis[v] = seen | fresh;
         }
-        discover(v, fresh, next_level, lvl, push, qn, qdeg, cnt);
+        discover(v, fresh, next_level, lvl, push, qn, qdeg, cnt, sh, mf, bits);
     }
+    discover_flush(cnt, sh, mf, bits);
 }
 
 // Push level: edge-balanced over the frontier queue (exclusive scan of degrees in qpre).
@@ -221,9 +254,11 @@ __global__ void __launch_bounds__(kBlock) ms_push(View push, const int32_t* __re
 __global__ void __launch_bounds__(kBlock) ms_settle(View push, int64_t n_active, uint64_t* __restrict__ vis,
         uint64_t* __restrict__ nx, LevelPlanes lvl, int32_t* __restrict__ qn,
         int64_t* __restrict__ qdeg, Counters* cnt, int32_t next_level) {
-    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    __shared__ DiscoverLds sh;
+    unsigned long long mf = 0, bits = 0;
     const int64_t words = (n_active + 63) >> 6;
-    for (int64_t wd = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; wd < words; wd += nwaves) {
+    for (int64_t b = static_cast<int64_t>(blockIdx.x) * kWaves; b < words; b += static_cast<int64_t>(gridDim.x) * kWaves) {
+        const int64_t wd = b + (threadIdx.x >> 6);
         const int64_t v = (wd << 6) + lane();
         uint64_t fresh = 0;
         if (v < n_active) {
@@ -235,8 +270,9 @@ __global__ void __launch_bounds__(kBlock) ms_settle(View push, int64_t n_active,
                 if (fresh) vis[v] = seen | fresh;
             }
         }
-        discover(v, fresh, next_level, lvl, push, qn, qdeg, cnt);
+        discover(v, fresh, next_level, lvl, push, qn, qdeg, cnt, sh, mf, bits);
     }
+    discover_flush(cnt, sh, mf, bits);
 }
 
 // Partitioned push: OR the candidate-mask slices every rank sent for the owned vertices.
@@ -340,7 +376,7 @@ hipError_t k_ms_seed(const int64_t* seeds, int nseeds, uint64_t* vis, uint64_t* 
 hipError_t k_ms_pull(const View& pull, const View& push, int64_t n_active, uint64_t full, const uint64_t* fr,
                      uint64_t* vis, uint64_t* nx, LevelPlanes lvl, int32_t* qn, int64_t* qdeg, Counters* cnt,
                      int32_t next_level, hipStream_t s) {
-    ms_pull<<<grid_for(n_active, 1 << 20), kBlock, 0, s>>>(pull, push, n_active, full, fr, vis, nx, lvl, qn, qdeg, cnt,
+    ms_pull<<<grid_for(n_active, 8192), kBlock, 0, s>>>(pull, push, n_active, full, fr, vis, nx, lvl, qn, qdeg, cnt,
                                                         next_level);
     return hipGetLastError();
 }
@@ -351,7 +387,7 @@ hipError_t k_ms_push(const View& push, const int32_t* q, const int64_t* qpre, in
 }
 hipError_t k_ms_settle(const View& push, int64_t n_active, uint64_t* vis, uint64_t* nx, LevelPlanes lvl, int32_t* qn,
                        int64_t* qdeg, Counters* cnt, int32_t next_level, hipStream_t s) {
-    ms_settle<<<grid_for(n_active, 1 << 20), kBlock, 0, s>>>(push, n_active, vis, nx, lvl, qn, qdeg, cnt, next_level);
+    ms_settle<<<grid_for(n_active, 8192), kBlock, 0, s>>>(push, n_active, vis, nx, lvl, qn, qdeg, cnt, next_level);
     return hipGetLastError();
 }
 hipError_t k_ms_reach(const View& v, const uint64_t* vis, int64_t n_active, int nsrc, unsigned long long* reached,
