@@ -72,6 +72,46 @@ __device__ __forceinline__ void wave_append(bool take, int32_t v, int64_t deg, i
     }
 }
 
+// Block-aggregated append (all threads of the block call it in the same trip): the block
+// reserves its queue slots with ONE atomicAdd on cnt->qlen; the appended degrees stay in
+// registers (mf) until block_flush.  A single contended counter word serves ~88 atomics/us
+// (MI355X_MICROARCH.md, dequeue), so per-wave counter atomics dominated the dense levels.
+constexpr int kWavesPerBlock = kBlock / 64;
+struct AppendLds { unsigned long long off[kWavesPerBlock]; unsigned long long base; unsigned long long mf[kWavesPerBlock]; };
+__device__ __forceinline__ void block_append(bool take, int32_t v, int64_t deg, int32_t* qn, int64_t* qdeg,
+                                             Counters* cnt, AppendLds& sh, unsigned long long& mf) {
+    const unsigned long long mask = __ballot(take);
+    const int wave = threadIdx.x >> 6;
+    if (mask) {
+        int64_t dsum = take ? deg : 0;
+        for (int off = 32; off > 0; off >>= 1) dsum += __shfl_xor(dsum, off, 64);
+        mf += static_cast<unsigned long long>(dsum);
+    }
+    if (lane() == 0) sh.off[wave] = static_cast<unsigned long long>(__popcll(mask));
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+        for (int w = 0; w < kWavesPerBlock; ++w) { const unsigned long long c = sh.off[w]; sh.off[w] = t; t += c; }
+        sh.base = t ? atomicAdd(&cnt->qlen, t) : 0ULL;
+    }
+    __syncthreads();
+    if (take) {
+        const unsigned long long slot = sh.base + sh.off[wave] + static_cast<unsigned long long>(__popcll(mask & ((1ULL << lane()) - 1ULL)));
+        qn[slot] = v;
+        qdeg[slot] = deg;
+    }
+}
+__device__ __forceinline__ void block_flush(Counters* cnt, AppendLds& sh, unsigned long long mf) {
+    __syncthreads();
+    if (lane() == 0) sh.mf[threadIdx.x >> 6] = mf;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long a = 0;
+        for (int w = 0; w < kWavesPerBlock; ++w) a += sh.mf[w];
+        if (a) atomicAdd(&cnt->mf, a);
+    }
+}
+
 __global__ void fill_i32(int32_t* p, int32_t v, int64_t n) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = v;
 }
@@ -97,6 +137,8 @@ __global__ void __launch_bounds__(kBlock) td_expand(View push, const int32_t* __
     __shared__ int64_t s_pre[kLdsEntries];
     __shared__ int32_t s_q[kLdsEntries];
     __shared__ int64_t s_lo, s_hi;
+    __shared__ AppendLds sh;
+    unsigned long long mf = 0;
     const int64_t total = qpre[qlen];
     const int64_t ntiles = (total + kTileEdges - 1) / kTileEdges;
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
@@ -154,10 +196,11 @@ __global__ void __launch_bounds__(kBlock) td_expand(View push, const int32_t* __
                     }
                 }
             }
-            wave_append(take, v, vdeg, qn, qdeg_n, cnt);
+            block_append(take, v, vdeg, qn, qdeg_n, cnt, sh, mf);
         }
         __syncthreads();
     }
+    block_flush(cnt, sh, mf);
 }
 
 // Bottom-up: one wave per 64-vertex bitmap word.
@@ -165,11 +208,14 @@ __global__ void __launch_bounds__(kBlock) bu_step(View pull, View push, int64_t 
         const uint64_t* __restrict__ fb, uint64_t* __restrict__ vb, uint64_t* __restrict__ nb,
         int32_t* __restrict__ level, int32_t* __restrict__ qn, int64_t* __restrict__ qdeg_n,
         Counters* cnt, int32_t next_level) {
+    __shared__ AppendLds sh;
+    unsigned long long mf = 0;
     const int64_t words = (n + 63) >> 6;
-    const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
-    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    for (int64_t wd = wave; wd < words; wd += nwaves) {
-        const uint64_t vis = vb[wd];
+    // block-uniform trips (block_append synchronises the block): wave w takes word b + w
+    for (int64_t b = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock; b < words;
+         b += static_cast<int64_t>(gridDim.x) * kWavesPerBlock) {
+        const int64_t wd = b + (threadIdx.x >> 6);
+        const uint64_t vis = wd < words ? vb[wd] : ~0ULL;
         const int64_t v = (wd << 6) + lane();
         bool found = false;
         const bool open = v < n && !((vis >> lane()) & 1ULL);
@@ -219,13 +265,14 @@ __global__ void __launch_bounds__(kBlock) bu_step(View pull, View push, int64_t 
             if (lane() == src) found = hit;
         }
         const unsigned long long fm = __ballot(found);
-        if (lane() == 0) {
+        if (lane() == 0 && wd < words) {
             nb[wd] = fm;
             if (fm) vb[wd] = vis | fm;
         }
         if (found) level[v] = next_level;
-        wave_append(found, static_cast<int32_t>(v), found ? push_degree(push, v) : 0, qn, qdeg_n, cnt);
+        block_append(found, static_cast<int32_t>(v), found ? push_degree(push, v) : 0, qn, qdeg_n, cnt, sh, mf);
     }
+    block_flush(cnt, sh, mf);
 }
 
 __global__ void level_to_dist(const int32_t* level, int64_t* dist, int64_t n) {
@@ -467,7 +514,7 @@ hipError_t k_bu_step(const View& pull, const View& push, int64_t n, const uint64
     // one wave per bitmap word, all launched at once: the dispatcher keeps every CU full
     // and a wave's dependent probe chain overlaps with hundreds of others.
     const int64_t words = (n + 63) / 64;
-    bu_step<<<grid_for(words * 64, kBlock, 1 << 20), kBlock, 0, s>>>(pull, push, n, fb, vb, nb, level, qn, qdeg_n, cnt, next_level);
+    bu_step<<<grid_for(words * 64, kBlock, 8192), kBlock, 0, s>>>(pull, push, n, fb, vb, nb, level, qn, qdeg_n, cnt, next_level);
     return hipGetLastError();
 }
 hipError_t k_level_to_dist(const int32_t* level, int64_t* dist, int64_t n, hipStream_t s) {

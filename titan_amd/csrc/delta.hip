@@ -68,6 +68,46 @@ __device__ __forceinline__ void append(bool take, int32_t v, int64_t deg, int32_
     }
 }
 
+// Block-aggregated append (all threads of the block call it in the same trip): the block
+// reserves its queue slots with ONE atomicAdd on cnt->qlen; the appended degrees stay in
+// registers (mf) until block_flush.  A single contended counter word serves ~88 atomics/us
+// (MI355X_MICROARCH.md, dequeue), so per-wave counter atomics dominated the dense levels.
+constexpr int kWavesPerBlock = kBlock / 64;
+struct AppendLds { unsigned long long off[kWavesPerBlock]; unsigned long long base; unsigned long long mf[kWavesPerBlock]; };
+__device__ __forceinline__ void block_append(bool take, int32_t v, int64_t deg, int32_t* qn, int64_t* qdeg,
+                                             Counters* cnt, AppendLds& sh, unsigned long long& mf) {
+    const unsigned long long mask = __ballot(take);
+    const int wave = threadIdx.x >> 6;
+    if (mask) {
+        int64_t dsum = take ? deg : 0;
+        for (int off = 32; off > 0; off >>= 1) dsum += __shfl_xor(dsum, off, 64);
+        mf += static_cast<unsigned long long>(dsum);
+    }
+    if (lane() == 0) sh.off[wave] = static_cast<unsigned long long>(__popcll(mask));
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+        for (int w = 0; w < kWavesPerBlock; ++w) { const unsigned long long c = sh.off[w]; sh.off[w] = t; t += c; }
+        sh.base = t ? atomicAdd(&cnt->qlen, t) : 0ULL;
+    }
+    __syncthreads();
+    if (take) {
+        const unsigned long long slot = sh.base + sh.off[wave] + static_cast<unsigned long long>(__popcll(mask & ((1ULL << lane()) - 1ULL)));
+        qn[slot] = v;
+        qdeg[slot] = deg;
+    }
+}
+__device__ __forceinline__ void block_flush(Counters* cnt, AppendLds& sh, unsigned long long mf) {
+    __syncthreads();
+    if (lane() == 0) sh.mf[threadIdx.x >> 6] = mf;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long a = 0;
+        for (int w = 0; w < kWavesPerBlock; ++w) a += sh.mf[w];
+        if (a) atomicAdd(&cnt->mf, a);
+    }
+}
+
 // min(cand) into dist[v] of an owned vertex; true when v has to join the near queue.
 __device__ __forceinline__ bool relax_owned(int64_t* dist, uint64_t* pend, int64_t v, int64_t cand, int64_t thr) {
     if (cand >= dist[v]) return false;                  // a stale (larger) read only costs an atomic
@@ -109,6 +149,8 @@ __global__ void __launch_bounds__(kBlock) ds_relax(View push, const int32_t* __r
     __shared__ int64_t s_pre[kLdsEntries];
     __shared__ int32_t s_q[kLdsEntries];
     __shared__ int64_t s_lo, s_hi;
+    __shared__ AppendLds sh;
+    unsigned long long mf = 0;
     const int64_t total = qpre[qlen];
     if (blockIdx.x == 0 && threadIdx.x == 0) cnt->red[1] = static_cast<unsigned long long>(total);   // work done
     const int64_t ntiles = (total + kTileEdges - 1) / kTileEdges;
@@ -183,10 +225,11 @@ __global__ void __launch_bounds__(kBlock) ds_relax(View push, const int32_t* __r
                     }
                 }
             }
-            append(take, v, vdeg, qn, qdeg_n, cnt);
+            block_append(take, v, vdeg, qn, qdeg_n, cnt, sh, mf);
         }
         __syncthreads();
     }
+    block_flush(cnt, sh, mf);
 }
 
 // Minimum distance over the pending vertices (into cnt->red[0], pre-set to a large value)
@@ -209,9 +252,15 @@ __global__ void __launch_bounds__(kBlock) ds_pending_min(const uint64_t* __restr
         mn = o < mn ? o : mn;
         count += __shfl_xor(count, off, 64);
     }
-    if (lane() == 0) {
-        atomicMin(&cnt->red[0], mn);
-        atomicAdd(&cnt->red[1], count);
+    __shared__ unsigned long long s_mn[kBlock / 64], s_ct[kBlock / 64];
+    if (lane() == 0) { s_mn[threadIdx.x >> 6] = mn; s_ct[threadIdx.x >> 6] = count; }
+    __syncthreads();
+    if (threadIdx.x == 0) {                              // one pair of atomics per block
+        for (int w = 1; w < kBlock / 64; ++w) { mn = s_mn[w] < mn ? s_mn[w] : mn; count += s_ct[w]; }
+        if (count) {
+            atomicMin(&cnt->red[0], mn);
+            atomicAdd(&cnt->red[1], count);
+        }
     }
 }
 
@@ -219,17 +268,20 @@ __global__ void __launch_bounds__(kBlock) ds_pending_min(const uint64_t* __restr
 __global__ void __launch_bounds__(kBlock) ds_extract(View push, uint64_t* __restrict__ pend, int64_t n,
         const int64_t* __restrict__ dist, int64_t thr, int32_t* __restrict__ qn, int64_t* __restrict__ qdeg,
         Counters* cnt) {
+    __shared__ AppendLds sh;
+    unsigned long long mf = 0;
     const int64_t words = (n + 63) >> 6;
-    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    for (int64_t wd = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; wd < words; wd += nwaves) {
-        const uint64_t b = pend[wd];                     // uniform across the wave
-        if (!b) continue;
+    for (int64_t bw = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock; bw < words;
+         bw += static_cast<int64_t>(gridDim.x) * kWavesPerBlock) {        // block-uniform trips
+        const int64_t wd = bw + (threadIdx.x >> 6);
+        const uint64_t b = wd < words ? pend[wd] : 0ULL;     // uniform across the wave
         const int64_t v = (wd << 6) + lane();
-        const bool take = ((b >> lane()) & 1ULL) && dist[v] < thr;
+        const bool take = b && ((b >> lane()) & 1ULL) && dist[v] < thr;
         const unsigned long long tm = __ballot(take);
         if (lane() == 0 && tm) pend[wd] = b & ~tm;       // one writer per word
-        append(take, static_cast<int32_t>(v), take ? push_degree(push, v) : 0, qn, qdeg, cnt);
+        block_append(take, static_cast<int32_t>(v), take ? push_degree(push, v) : 0, qn, qdeg, cnt, sh, mf);
     }
+    block_flush(cnt, sh, mf);
 }
 
 // Partitioned: marked remote targets per owner rank (rank r owns words [r*wpr, (r+1)*wpr)).
@@ -323,7 +375,7 @@ hipError_t k_ds_pending_min(const uint64_t* pend, int64_t words, const int64_t* 
 hipError_t k_ds_extract(const View& push, uint64_t* pend, int64_t n, const int64_t* dist, int64_t thr, int32_t* qn,
                         int64_t* qdeg, Counters* cnt, hipStream_t s) {
     const int64_t words = (n + 63) / 64;
-    ds_extract<<<grid_for(words * 64, 1 << 20), kBlock, 0, s>>>(push, pend, n, dist, thr, qn, qdeg, cnt);
+    ds_extract<<<grid_for(words * 64, 8192), kBlock, 0, s>>>(push, pend, n, dist, thr, qn, qdeg, cnt);
     return hipGetLastError();
 }
 hipError_t k_ds_mark_count(const uint64_t* rmark, int64_t words, int64_t wpr, unsigned long long* counts, hipStream_t s) {
