@@ -49,29 +49,6 @@ __device__ __forceinline__ void entry_at(const View& v, int64_t u, int64_t o, in
     }
 }
 
-// Wave-aggregated append of `v` (for lanes with take=true) to queue qn/qdeg.
-__device__ __forceinline__ void wave_append(bool take, int32_t v, int64_t deg, int32_t* qn,
-                                            int64_t* qdeg, Counters* cnt) {
-    const unsigned long long mask = __ballot(take);
-    if (mask == 0) return;
-    const int leader = __ffsll(static_cast<long long>(mask)) - 1;
-    const unsigned long long below = mask & ((1ULL << lane()) - 1ULL);
-    const int rank = __popcll(below);
-    unsigned long long base = 0;
-    // sum of degrees of the appended vertices (for the direction heuristic)
-    int64_t dsum = take ? deg : 0;
-    for (int off = 32; off > 0; off >>= 1) dsum += __shfl_xor(dsum, off, 64);
-    if (lane() == leader) {
-        base = atomicAdd(&cnt->qlen, static_cast<unsigned long long>(__popcll(mask)));
-        atomicAdd(&cnt->mf, static_cast<unsigned long long>(dsum));
-    }
-    base = __shfl(base, leader, 64);
-    if (take) {
-        qn[base + rank] = v;
-        qdeg[base + rank] = deg;
-    }
-}
-
 // Block-aggregated append (all threads of the block call it in the same trip): the block
 // reserves its queue slots with ONE atomicAdd on cnt->qlen; the appended degrees stay in
 // registers (mf) until block_flush.  A single contended counter word serves ~88 atomics/us
@@ -316,6 +293,8 @@ __global__ void __launch_bounds__(kBlock) sssp_relax(View push, const int32_t* _
     __shared__ int64_t s_pre[kLdsEntries];
     __shared__ int32_t s_q[kLdsEntries];
     __shared__ int64_t s_lo, s_hi;
+    __shared__ AppendLds sh;
+    unsigned long long mf = 0;
     const int64_t total = qpre[qlen];
     const int64_t ntiles = (total + kTileEdges - 1) / kTileEdges;
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
@@ -373,10 +352,11 @@ __global__ void __launch_bounds__(kBlock) sssp_relax(View push, const int32_t* _
                     }
                 }
             }
-            wave_append(take, v, vdeg, qn, qdeg_n, cnt);
+            block_append(take, v, vdeg, qn, qdeg_n, cnt, sh, mf);
         }
         __syncthreads();
     }
+    block_flush(cnt, sh, mf);
 }
 
 __global__ void sssp_commit(const int32_t* q, int64_t qlen, const int64_t* dist, int64_t* msg) {
@@ -453,23 +433,28 @@ __global__ void __launch_bounds__(kBlock) part_claim(View push, const uint64_t* 
         int nslices, int64_t words, int64_t n_local, uint64_t* __restrict__ vb, uint64_t* __restrict__ nb,
         int32_t* __restrict__ level, int32_t* __restrict__ qn, int64_t* __restrict__ qdeg_n, Counters* cnt,
         int32_t next_level) {
-    const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
-    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    for (int64_t wd = wave; wd < words; wd += nwaves) {
+    __shared__ AppendLds sh;
+    unsigned long long mf = 0;
+    for (int64_t b = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock; b < words;
+         b += static_cast<int64_t>(gridDim.x) * kWavesPerBlock) {        // block-uniform trips
+        const int64_t wd = b + (threadIdx.x >> 6);
+        const bool live = wd < words;
         uint64_t bits = 0;
-        for (int s = 0; s < nslices; ++s) bits |= recv[static_cast<int64_t>(s) * words + wd];
-        const uint64_t vis = vb[wd];
+        if (live)
+            for (int s = 0; s < nslices; ++s) bits |= recv[static_cast<int64_t>(s) * words + wd];
+        const uint64_t vis = live ? vb[wd] : ~0ULL;
         const uint64_t fresh = bits & ~vis;
         const int64_t v = (wd << 6) + lane();
         const bool take = v < n_local && ((fresh >> lane()) & 1ULL);
         const unsigned long long tm = __ballot(take);
-        if (lane() == 0) {
+        if (lane() == 0 && live) {
             nb[wd] = tm;
             if (tm) vb[wd] = vis | tm;
         }
         if (take) level[v] = next_level;
-        wave_append(take, static_cast<int32_t>(v), take ? push_degree(push, v) : 0, qn, qdeg_n, cnt);
+        block_append(take, static_cast<int32_t>(v), take ? push_degree(push, v) : 0, qn, qdeg_n, cnt, sh, mf);
     }
+    block_flush(cnt, sh, mf);
 }
 
 // out[v] = in[perm[v]]: internal (degree-grouped) order -> the API's row order.
@@ -554,7 +539,7 @@ hipError_t k_part_td_mark(const View& push, const int32_t* q, const int64_t* qpr
 hipError_t k_part_claim(const View& push, const uint64_t* recv, int nslices, int64_t words, int64_t n_local,
                         uint64_t* vb, uint64_t* nb, int32_t* level, int32_t* qn, int64_t* qdeg_n,
                         Counters* cnt, int32_t next_level, hipStream_t s) {
-    part_claim<<<grid_for(words * 64, kBlock, 1 << 20), kBlock, 0, s>>>(push, recv, nslices, words, n_local, vb, nb,
+    part_claim<<<grid_for(words * 64, kBlock, 8192), kBlock, 0, s>>>(push, recv, nslices, words, n_local, vb, nb,
                                                                       level, qn, qdeg_n, cnt, next_level);
     return hipGetLastError();
 }

@@ -48,26 +48,6 @@ __device__ __forceinline__ int64_t push_degree(const View& v, int64_t u) {
     return d;
 }
 
-// Wave-aggregated append to (qn, qdeg) and of the appended degrees to cnt->mf.
-__device__ __forceinline__ void append(bool take, int32_t v, int64_t deg, int32_t* qn, int64_t* qdeg, Counters* cnt) {
-    const unsigned long long mask = __ballot(take);
-    if (!mask) return;
-    const int leader = __ffsll(static_cast<long long>(mask)) - 1;
-    const int rank = __popcll(mask & ((1ULL << lane()) - 1ULL));
-    int64_t dsum = take ? deg : 0;
-    for (int off = 32; off > 0; off >>= 1) dsum += __shfl_xor(dsum, off, 64);
-    unsigned long long base = 0;
-    if (lane() == leader) {
-        base = atomicAdd(&cnt->qlen, static_cast<unsigned long long>(__popcll(mask)));
-        atomicAdd(&cnt->mf, static_cast<unsigned long long>(dsum));
-    }
-    base = __shfl(base, leader, 64);
-    if (take) {
-        qn[base + rank] = v;
-        qdeg[base + rank] = deg;
-    }
-}
-
 // Block-aggregated append (all threads of the block call it in the same trip): the block
 // reserves its queue slots with ONE atomicAdd on cnt->qlen; the appended degrees stay in
 // registers (mf) until block_flush.  A single contended counter word serves ~88 atomics/us
@@ -319,6 +299,8 @@ __global__ void ds_mark_pack(uint64_t* __restrict__ rmark, int64_t words, int64_
 __global__ void __launch_bounds__(kBlock) ds_apply(View push, const int64_t* __restrict__ recv, int64_t npairs,
         int64_t* __restrict__ dist, uint64_t* __restrict__ pend, int32_t* __restrict__ qn,
         int64_t* __restrict__ qdeg_n, Counters* cnt, int64_t thr) {
+    __shared__ AppendLds sh;
+    unsigned long long mf = 0;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < npairs; base += stride) {   // block-uniform trips
         const int64_t i = base + threadIdx.x;
@@ -333,8 +315,9 @@ __global__ void __launch_bounds__(kBlock) ds_apply(View push, const int64_t* __r
                 vdeg = push_degree(push, vl);
             }
         }
-        append(take, v, vdeg, qn, qdeg_n, cnt);
+        block_append(take, v, vdeg, qn, qdeg_n, cnt, sh, mf);
     }
+    block_flush(cnt, sh, mf);
 }
 
 inline int grid_for(int64_t work, int cap) {
