@@ -18,7 +18,12 @@
  * RCCL has no bitwise-OR reduction, hence slice exchanges instead of an all-reduce.
  *
  * Preconditions: n_local = hi - lo is a multiple of 64 (bitmap slices are whole words),
- * tgo_options.stream is the stream the caller's collectives run on.
+ * tgo_options.stream is the stream the caller's collectives run on.  A NULL stream makes
+ * the ctx create its own stream, which the caller's collectives are NOT ordered with; the
+ * entry points that leave kernels queued (bfs_td, ms_push, ms_pack, pr_begin, pr_step)
+ * then finish them before returning, but inputs the caller wrote on another stream must
+ * be complete before the call.  (torch's default stream has handle 0 = NULL: a torch
+ * caller switches to a side stream first — titan_amd/distributed.exchange_stream.)
  */
 #ifndef TITAN_GPU_OLAP_PART_H
 #define TITAN_GPU_OLAP_PART_H
