@@ -63,7 +63,7 @@ struct WalkFinal {
 // not evict the message vector from L2 / the Infinity Cache, which every gather re-reads.
 __device__ __forceinline__ int32_t stream_idx(const int32_t* p) { return __builtin_nontemporal_load(p); }
 
-constexpr int kPer = static_cast<int>(kTile / kBlock);   // entries per thread per tile (8)
+constexpr int kPer = static_cast<int>(kTile / kBlock);   // entries per thread per tile (16)
 
 // Gather up to kTile messages of the entries [s0, s0+nnz) into registers: all kPer index
 // loads are issued first, then all kPer message loads, so every thread keeps kPer
