@@ -24,6 +24,20 @@ int tgo_rmat_edges(int32_t scale, int32_t edge_factor, uint64_t seed, int64_t ed
 int tgo_pick_roots(int64_t n, int64_t m, const int32_t* src, const int32_t* dst, uint64_t seed,
                    int32_t nroots, int64_t* roots_out);
 
+/* Synthetic edgestore rows (the rows an ordered scan of Titan's `edgestore` returns to
+ * VertexJobConverter.process, VertexJobConverter.java:109-129) for the directed edge list
+ * (src, dst) of ONE MULTI edge label `label_id` (a UserEdgeLabel schema id), with the
+ * Integer weight as the label's only signature property when `weight` is non-NULL.
+ * Vertex i has id IDManager.constructId(i / 2^pb + 1, i % 2^pb) (round-robin partitions);
+ * every row starts with VertexExists; OUT then IN entries, each sorted by (other id,
+ * relation id); relation ids 1001 + i (VertexExists of i) and 1001 + n + k (edge k).
+ * Output in the tgo_rows layout (titan_gpu_olap.h).  sizes_out = {nrows, nentries,
+ * nbytes}; when any output array is NULL only the sizes are computed. */
+int tgo_synth_rows(int64_t n, int64_t m, const int32_t* src, const int32_t* dst, const int32_t* weight,
+                   int64_t label_id, int32_t partition_bits, int32_t threads, int64_t* sizes_out,
+                   int64_t* row_keys, int64_t* row_entry_begin, int64_t* row_byte_begin,
+                   uint8_t* entry_bytes, int64_t* entry_limit_valpos);
+
 #ifdef __cplusplus
 }
 #endif

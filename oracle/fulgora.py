@@ -107,6 +107,9 @@ def load() -> C.CDLL:
         "fr_load_rows": (C.c_int, [P(FrRows), P(FrSchema), P(FrLoadOpts), P(vp), P(FrLoadStats)]),
         "fr_load_adjacency": (C.c_int, [C.c_int64, _i64p, _i64p, _i64p, _i32p, _i32p, P(vp)]),
         "fr_load_edges": (C.c_int, [C.c_int64, C.c_int64, _i32p, _i32p, _i32p, _i64p, P(vp)]),
+        "fr_load_edges_capped": (C.c_int, [C.c_int64, C.c_int64, _i32p, _i32p, _i32p, _i64p, C.c_int64, _i64p,
+                                           P(vp)]),
+        "fr_resolve": (C.c_int, [vp, C.c_int]),
         "fr_free": (None, [vp]),
         "fr_num_vertices": (C.c_int64, [vp]),
         "fr_vertex_ids": (None, [vp, _i64p]),
@@ -226,18 +229,30 @@ class OracleGraph:
         return cls(h)
 
     @classmethod
-    def from_edges(cls, n, src, dst, w=None, titan_ids=None):
+    def from_edges(cls, n, src, dst, w=None, titan_ids=None, hard_limit=0):
+        """Rows of a directed edge list (one MULTI label).  hard_limit > 0 applies the preload
+        cap of an untyped inE/outE scope; stats.truncated_results counts the cut rows."""
         lib = load()
         src = np.ascontiguousarray(src, np.int32)
         dst = np.ascontiguousarray(dst, np.int32)
         w = None if w is None else np.ascontiguousarray(w, np.int32)
         ids = (np.arange(n, dtype=np.int64) + 1) << 3 if titan_ids is None else np.ascontiguousarray(titan_ids, np.int64)
         h = C.c_void_p()
-        rc = lib.fr_load_edges(n, len(src), _p(src, C.c_int32), _p(dst, C.c_int32), _p(w, C.c_int32),
-                               _p(ids, C.c_int64), C.byref(h))
+        cut = C.c_int64(0)
+        rc = lib.fr_load_edges_capped(n, len(src), _p(src, C.c_int32), _p(dst, C.c_int32), _p(w, C.c_int32),
+                                      _p(ids, C.c_int64), int(hard_limit), C.byref(cut), C.byref(h))
         if rc:
             raise RuntimeError(f"fr_load_edges rc={rc}")
-        return cls(h)
+        st = FrLoadStats()
+        st.truncated_results = cut.value
+        return cls(h, st)
+
+    def resolve(self, threads=16):
+        """Memoise the per-entry hash lookups (faster supersteps, identical results)."""
+        rc = load().fr_resolve(self.h, int(threads))
+        if rc:
+            raise RuntimeError(f"fr_resolve rc={rc}")
+        return self
 
     def __del__(self):
         if getattr(self, "h", None) and _lib is not None:

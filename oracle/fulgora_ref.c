@@ -399,6 +399,11 @@ struct fr_graph {
      * order) is xr_beg[j]..xr_end[j] for j in [xr_off[v], xr_off[v+1]). NULL if none. */
     uint8_t* pv;
     int64_t* xr_off; int64_t* xr_beg; int64_t* xr_end;
+    /* Optional memo of lookup(other[k]) per entry (fr_resolve): the hash probe is a pure
+     * function of the loaded graph, so caching it changes no result, only the oracle's speed
+     * on the full-size parity tests.  NULL = probe the hash map per entry, as the reference. */
+    int64_t* oidx;
+    int64_t nent;             /* entries stored in other/edir/has_w/w                */
 };
 
 static uint64_t mix64(uint64_t x) {
@@ -426,8 +431,14 @@ static inline int64_t lookup(const fr_graph* g, int64_t id) {            /* vert
     }
 }
 
+/* The executor's per-entry neighbour lookup (VertexMemoryHandler.java:89 -> getMessage). */
+static inline int64_t entry_vertex(const fr_graph* g, int64_t k) {
+    return g->oidx ? g->oidx[k] : lookup(g, g->other[k]);
+}
+
 void fr_free(fr_graph* g) {
     if (!g) return;
+    free(g->oidx);
     free(g->titan_id); free(g->eoff); free(g->other); free(g->edir); free(g->has_w); free(g->w);
     free(g->hkeys); free(g->hvals);
     free(g->pv); free(g->xr_off); free(g->xr_beg); free(g->xr_end); free(g);
@@ -573,6 +584,7 @@ int fr_load_rows(const fr_rows* rows, const fr_schema* schema, const fr_load_opt
     }
     free(kind); free(rid);
     st.num_entries = e;
+    g->nent = e;
     *out = g;
     if (stats) *stats = st;
     return FR_OK;
@@ -599,16 +611,21 @@ int fr_load_adjacency(int64_t n, const int64_t* titan_ids, const int64_t* off, c
             g->has_w[k] = w != NULL;
             g->w[k] = w ? w[k] : 0;
         }
+    g->nent = E;
     build_hash(g);
     *out = g;
     return FR_OK;
 }
 
-int fr_load_edges(int64_t n, int64_t m, const int32_t* src, const int32_t* dst, const int32_t* w,
-                  const int64_t* titan_ids, fr_graph** out) {
+int fr_load_edges_capped(int64_t n, int64_t m, const int32_t* src, const int32_t* dst, const int32_t* w,
+                         const int64_t* titan_ids, int64_t hard_limit, int64_t* truncated, fr_graph** out) {
     /* Rows as the commit path writes them (StandardTitanGraph.java:564-591): every edge
      * u->v gives an OUT entry on row u and an IN entry on row v; within a row OUT entries
-     * precede IN entries and each run is ordered by (other id, relation id = edge index). */
+     * precede IN entries and each run is ordered by (other id, relation id = edge index).
+     * hard_limit > 0 restates the preload cap of an untyped single-direction scope: the
+     * row's user-edge slice is returned in column order and cut at the limit
+     * (QueryContainer.java:28,122; ColumnValueStore.getSlice :59), and a row with at least
+     * `limit` entries counts as truncated (VertexJobConverter.java:125). */
     fr_graph* g = (fr_graph*)calloc(1, sizeof(fr_graph));
     g->n = n;
     g->titan_id = (int64_t*)malloc((n + 1) * sizeof(int64_t));
@@ -646,8 +663,51 @@ int fr_load_edges(int64_t n, int64_t m, const int32_t* src, const int32_t* dst, 
         }
     }
     free(outc); free(po); free(pi); free(bucket); free(order);
+    int64_t cut = 0;
+    if (hard_limit > 0) {                               /* compact rows to their first `limit` entries */
+        int64_t wpos = 0, beg = 0;
+        for (int64_t v = 0; v < n; v++) {
+            int64_t end = g->eoff[v + 1], cnt = end - beg;
+            if (cnt >= hard_limit) cut++;
+            int64_t keep = cnt < hard_limit ? cnt : hard_limit;
+            for (int64_t k = beg; k < beg + keep; k++, wpos++) {
+                g->other[wpos] = g->other[k]; g->edir[wpos] = g->edir[k];
+                g->has_w[wpos] = g->has_w[k]; g->w[wpos] = g->w[k];
+            }
+            beg = end;
+            g->eoff[v + 1] = wpos;
+        }
+    }
+    if (truncated) *truncated = cut;
+    g->nent = g->eoff[n];
     build_hash(g);
     *out = g;
+    return FR_OK;
+}
+
+int fr_load_edges(int64_t n, int64_t m, const int32_t* src, const int32_t* dst, const int32_t* w,
+                  const int64_t* titan_ids, fr_graph** out) {
+    return fr_load_edges_capped(n, m, src, dst, w, titan_ids, 0, NULL, out);
+}
+
+typedef struct { fr_graph* g; int64_t lo, hi; } resolve_t;
+static void* resolve_range(void* a) {
+    resolve_t* r = (resolve_t*)a;
+    for (int64_t k = r->lo; k < r->hi; k++) r->g->oidx[k] = lookup(r->g, r->g->other[k]);
+    return NULL;
+}
+int fr_resolve(fr_graph* g, int threads) {
+    if (g->oidx) return FR_OK;
+    g->oidx = (int64_t*)malloc((g->nent + 1) * sizeof(int64_t));
+    if (!g->oidx) return FR_E_INVALID;
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    pthread_t th[256]; resolve_t rt[256];
+    for (int i = 0; i < threads; i++) {
+        rt[i].g = g; rt[i].lo = g->nent * i / threads; rt[i].hi = g->nent * (i + 1) / threads;
+        pthread_create(&th[i], NULL, resolve_range, &rt[i]);
+    }
+    for (int i = 0; i < threads; i++) pthread_join(th[i], NULL);
     return FR_OK;
 }
 
@@ -665,7 +725,7 @@ int64_t fr_export(const fr_graph* g, int64_t* off, int64_t* mid, int32_t* adj, i
                 int64_t kb, ke; row_range(g, v, i, &kb, &ke);
                 for (int64_t k = kb; k < ke; k++) {
                     if (g->edir[k] != pass) continue;
-                    int64_t o = lookup(g, g->other[k]);
+                    int64_t o = entry_vertex(g, k);
                     if (o < 0) continue;
                     adj[e] = (int32_t)o;
                     if (w) w[e] = g->has_w[k] ? g->w[k] : INT32_MIN;
@@ -721,7 +781,7 @@ static int64_t sd_row_min(sd_t* s, const fr_graph* g, int64_t kb, int64_t ke) {
     int64_t best = FR_ABSENT;
     for (int64_t k = kb; k < ke; k++) {
         if (!take(s->scope, g->edir[k])) continue;
-        int64_t o = lookup(g, g->other[k]);
+        int64_t o = entry_vertex(g, k);
         if (o < 0) continue;
         int64_t m = s->prev[o];
         if (m == FR_ABSENT) continue;                                    /* filter(m != null) */
@@ -802,7 +862,7 @@ static int64_t pr_row(const fr_graph* g, const double* prev, int sel, int64_t kb
     int64_t cnt = 0;
     for (int64_t k = kb; k < ke; k++) {
         if (g->edir[k] != sel) continue;
-        int64_t o = lookup(g, g->other[k]);
+        int64_t o = entry_vertex(g, k);
         if (o < 0) continue;
         double m = prev[o];
         if (isnan(m)) continue;
@@ -890,7 +950,7 @@ static uint32_t dc_row(const dc_t* s, const fr_graph* g, int64_t kb, int64_t ke,
     uint32_t sum = 0;
     for (int64_t k = kb; k < ke; k++) {
         if (g->edir[k] != 0) continue;
-        int64_t o = lookup(g, g->other[k]);
+        int64_t o = entry_vertex(g, k);
         if (o < 0 || !s->prev_ok[o]) continue;
         sum += (uint32_t)s->prev[o];
         *any = 1;

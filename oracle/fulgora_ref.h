@@ -126,6 +126,12 @@ int  fr_load_adjacency(int64_t n, const int64_t* titan_ids, const int64_t* off, 
 /* Rows from a directed edge list (both entries per edge, column order). w may be NULL. */
 int  fr_load_edges(int64_t n, int64_t m, const int32_t* src, const int32_t* dst, const int32_t* w,
                    const int64_t* titan_ids, fr_graph** out);
+/* fr_load_edges with the preload cap of an untyped single-direction scope (hard_limit > 0;
+ * QueryContainer.java:28,122): *truncated = rows with >= hard_limit entries. */
+int  fr_load_edges_capped(int64_t n, int64_t m, const int32_t* src, const int32_t* dst, const int32_t* w,
+                          const int64_t* titan_ids, int64_t hard_limit, int64_t* truncated, fr_graph** out);
+/* Memoise every entry's hash-map lookup (speed only; results are unchanged). */
+int  fr_resolve(fr_graph* g, int threads);
 void fr_free(fr_graph* g);
 int64_t fr_num_vertices(const fr_graph* g);
 void fr_vertex_ids(const fr_graph* g, int64_t* out);

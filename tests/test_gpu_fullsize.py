@@ -1,0 +1,121 @@
+"""GPU parity at the benchmarked sizes (BASELINE.json configs[1] and configs[2]).
+
+Small graphs pin semantics (test_gpu_parity.py); these tests check the HIP engine against the
+CPU oracle on the very graphs bench.py measures:
+
+* configs[1] — RMAT scale 20 (ef 16), single-source BFS, through the edgestore path:
+  byte-exact rows (tgo_synth_rows) -> tgo_load_rows in work blocks of the reference's
+  readBatchSize (FulgoraGraphComputer.java:76-81) -> device decode + CSR -> tgo_bfs.
+  inE at the real 100 000-entry preload cap (QueryContainer.java:28,122; RMAT-20 hubs hold
+  up to ~138 K entries, so rows ARE cut) and bothE (fitted, uncapped).  Oracle: its own row
+  decoder (fr_load_rows) + Fulgora superstep restatement.
+* configs[2] — RMAT scale 24: the 64-source multi-source BFS sweep against 64 single-source
+  runs and against the oracle for two seeds; PageRank(20) on the capped inE graph within
+  1e-6 L1 of the oracle, with the same truncated-row count on both sides.
+
+Sized so each test finishes in well under two minutes on the GPU box (oracle threads = 16,
+the box's CPU share).
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import fulgora as fr
+from titan_amd import Engine, pick_roots, rmat_edges, synth_rows
+from titan_amd import _lib as L
+
+pytestmark = pytest.mark.gpu
+
+IN, BOTH = L.SCOPE_IN_E, L.SCOPE_BOTH_E
+THREADS = 16
+PR_L1_TOL = 1e-6
+READ_BATCH = 10 * 1024           # FulgoraGraphComputer readBatchSize = 10 x storage.buffer-size
+
+
+@pytest.fixture(scope="module")
+def rmat20_rows():
+    import edgestore as es
+    scale = 20
+    n = 1 << scale
+    src, dst, _ = rmat_edges(scale, 16, seed=0x54495441)
+    knows = es.user_edge_label(1)
+    rows = synth_rows(n, src, dst, None, label_id=knows, threads=THREADS)
+    sd = {"edge_types": [{"type_id": knows, "multiplicity": 0}], "property_keys": []}
+    roots = pick_roots(n, src, dst, 4, seed=7)
+    vid = np.array([es.vertex_id(int(r)) for r in roots], np.int64)
+    return n, rows, sd, vid
+
+
+@pytest.mark.parametrize("scope", [IN, BOTH])
+def test_config2_rmat20_rows_bfs_bit_exact(rmat20_rows, scope):
+    from titan_amd import Schema
+    n, rows, sd, seeds = rmat20_rows
+    osch = fr.OracleSchema(sd["edge_types"], [])
+    o = fr.OracleGraph.from_rows(rows, osch, scope, hard_limit=100000).resolve(THREADS)
+    eng = Engine(host_threads=THREADS).load_rows(rows, Schema.from_dict(sd), scope, batch_rows=READ_BATCH)
+    assert np.array_equal(eng.vertex_ids(), o.vertex_ids())
+    st = eng.stats()
+    assert st["num_vertices"] == n
+    assert st["truncated_results"] == o.stats.truncated_results
+    if scope == IN:
+        assert st["truncated_results"] > 0          # the real cap is exercised at this scale
+    else:
+        assert st["truncated_results"] == 0        # bothE is fitted: no limit
+    for s in seeds:
+        d = eng.bfs(int(s), n, scope, stats=True)
+        od, it = o.shortest_distance(int(s), n, scope, threads=THREADS)
+        assert it == n
+        assert np.array_equal(d, od)
+        assert eng.stats()["reached"] == int((od != L.DIST_ABSENT).sum())
+
+
+@pytest.fixture(scope="module")
+def rmat24():
+    scale = 24
+    n = 1 << scale
+    src, dst, _ = rmat_edges(scale, 16, seed=0x54495441)
+    roots = pick_roots(n, src, dst, 64, seed=7)
+    return n, src, dst, roots
+
+
+def test_config3_rmat24_msbfs_sweep(rmat24):
+    """All 64 seeds of the bench's sweep equal their single-source runs; two equal the oracle."""
+    n, src, dst, roots = rmat24
+    eng = Engine(host_threads=THREADS).load_edges(n, src, dst, BOTH, apply_cap=False)
+    eng.bfs_multi(roots, n, BOTH, seed_is_dense=True, stats=True, fetch=False)
+    reached, entries = eng.multi_stats(len(roots))
+    ms = np.empty(n, np.int64)
+    for i, r in enumerate(roots):
+        assert eng.lib.tgo_copy_multi_distances(eng.ctx, i, L.ptr(ms, C.c_int64)) == 0
+        single = eng.bfs(int(r), n, BOTH, seed_is_dense=True, stats=True)
+        assert np.array_equal(ms, single), i
+        assert reached[i] == eng.stats()["reached"]
+        assert entries[i] == eng.stats()["reached_entries"]
+    keep = {int(roots[0]): eng.bfs(int(roots[0]), n, BOTH, seed_is_dense=True),
+            int(roots[37]): eng.bfs(int(roots[37]), n, BOTH, seed_is_dense=True)}
+    del eng
+    o = fr.OracleGraph.from_edges(n, src, dst).resolve(THREADS)
+    for r, d in keep.items():
+        od, _ = o.shortest_distance(int((r + 1) << 3), n, BOTH, threads=THREADS)
+        assert np.array_equal(d, od), r
+
+
+def test_config3_rmat24_pagerank_capped(rmat24):
+    """PageRank(20) on the capped inE graph (25 rows cut at 100 000 entries)."""
+    n, src, dst, roots = rmat24
+    eng = Engine(host_threads=THREADS).load_edges(n, src, dst, IN, apply_cap=True)
+    pr = eng.pagerank(0.85, n, 20)
+    assert np.array_equal(pr, eng.pagerank(0.85, n, 20))             # fixed reduction order
+    st = eng.stats()
+    d_in = eng.bfs(int(roots[1]), n, IN, seed_is_dense=True)
+    del eng
+    o = fr.OracleGraph.from_edges(n, src, dst, hard_limit=100000).resolve(THREADS)
+    assert st["truncated_results"] == o.stats.truncated_results > 0
+    opr, it = o.pagerank(0.85, n, 20, threads=THREADS)
+    assert it == 20
+    fin = np.isfinite(opr)
+    assert np.array_equal(np.isfinite(pr), fin)
+    assert np.abs(pr[fin] - opr[fin]).sum() <= PR_L1_TOL
+    od, _ = o.shortest_distance(int((int(roots[1]) + 1) << 3), n, IN, threads=THREADS)
+    assert np.array_equal(d_in, od)

@@ -457,23 +457,47 @@ def test_rmat_pagerank_segmented(rmat12, iters, monkeypatch):
     assert np.abs(pr - plain).sum() <= 1e-12
 
 
-def test_pagerank_segmented_long_rows(monkeypatch):
-    """Rows whose per-segment runs exceed one 2048-entry tile are split into chunk pairs:
-    a hub receiving 40 000 edges (5 000 per segment) plus a random background."""
-    monkeypatch.setenv("TGO_PR_SEGMENTS", "1")
-    rng = np.random.default_rng(11)
+def hub_graph(n, hub, k_in, k_out, seed=11):
+    """A random background plus a hub receiving `k_in` and sending `k_out` edges."""
+    rng = np.random.default_rng(seed)
+    src = np.concatenate([rng.integers(0, n, k_in), np.full(k_out, hub), rng.integers(0, n, 200000)]).astype(np.int32)
+    dst = np.concatenate([np.full(k_in, hub), rng.integers(0, n, k_out), rng.integers(0, n, 200000)]).astype(np.int32)
+    return src, dst
+
+
+KTILE = 4096     # CSR-adaptive tile (engine.hpp kTile): rows longer than this are split in chunks
+
+
+@pytest.mark.parametrize("segments", ["0", "1"])
+def test_pagerank_long_rows(monkeypatch, segments):
+    """A hub whose in-list spans many tiles: 80 000 entries = ~20 chunks of kTile on the default
+    path (gather_chunks + finalize_long) and ~10 000 per source segment (> 2 kTile) on the
+    segmented path; both within 1e-6 L1 of the oracle and bitwise reproducible."""
+    monkeypatch.setenv("TGO_PR_SEGMENTS", segments)
     n = 1 << 15
-    hub_src = rng.integers(0, n, 40000).astype(np.int32)
-    bg_src = rng.integers(0, n, 200000).astype(np.int32)
-    bg_dst = rng.integers(0, n, 200000).astype(np.int32)
-    src = np.concatenate([hub_src, bg_src])
-    dst = np.concatenate([np.full(40000, 7, np.int32), bg_dst])
+    src, dst = hub_graph(n, 7, 80000, 0)
+    assert (dst == 7).sum() > 2 * 8 * KTILE
     ids = (np.arange(n, dtype=np.int64) + 1) << 3
     off, mid, adj, ww = numpy_adjacency(n, src, dst, None)
     oracle = fr.OracleGraph.from_adjacency(ids, off, mid, adj, ww)
-    eng = Engine().load_edges(n, src, dst, IN)
+    eng = Engine(hard_query_limit=1 << 30).load_edges(n, src, dst, IN)
     pr = eng.pagerank(0.85, n, 6)
     opr, _ = oracle.pagerank(0.85, n, 6)
     fin = np.isfinite(opr)
     assert np.array_equal(np.isfinite(pr), fin)
     assert np.abs(pr[fin] - opr[fin]).sum() <= PR_L1_TOL
+    assert np.array_equal(pr, eng.pagerank(0.85, n, 6))
+
+
+def test_walkcount_long_rows():
+    """DegreeCounter gathers over OUT lists: an out-hub of 50 000 entries (> 12 tiles) plus an
+    in-hub, exact (with Java int wrap) against the oracle."""
+    n = 1 << 14
+    src, dst = hub_graph(n, 3, 30000, 50000, seed=4)
+    ids = (np.arange(n, dtype=np.int64) + 1) << 3
+    off, mid, adj, ww = numpy_adjacency(n, src, dst, None)
+    oracle = fr.OracleGraph.from_adjacency(ids, off, mid, adj, ww)
+    eng = Engine(hard_query_limit=1 << 30).load_edges(n, src, dst, IN)
+    assert (src == 3).sum() > 12 * KTILE
+    for k in (1, 2, 4):
+        assert np.array_equal(eng.walkcount(k), oracle.degree_counter(k)[0])

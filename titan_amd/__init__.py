@@ -4,7 +4,7 @@ Compute runs in libtitan_gpu_olap.so (hand-written HIP for gfx950, C-ABI in
 include/titan_gpu_olap.h).  This package is the host-side mirror of the reference's
 TitanGraphComputer API plus a thin ctypes binding; it has no CPU fallback.
 """
-from .engine import Engine, Schema, TitanException, rmat_edges, pick_roots  # noqa: F401
+from .engine import Engine, Rows, Schema, TitanException, rmat_edges, pick_roots, synth_rows  # noqa: F401
 from .computer import (  # noqa: F401
     DegreeCounter, DegreeMapper, ExecutionException, GpuGraph, GpuGraphComputer, KeyValue,
     PageRankMapReduce, PageRankVertexProgram, ShortestDistanceMapReduce,
@@ -13,7 +13,7 @@ from .computer import (  # noqa: F401
 from . import _lib  # noqa: F401
 
 __all__ = [
-    "Engine", "Schema", "TitanException", "rmat_edges", "pick_roots", "DegreeCounter", "DegreeMapper",
+    "Engine", "Rows", "Schema", "synth_rows", "TitanException", "rmat_edges", "pick_roots", "DegreeCounter", "DegreeMapper",
     "ExecutionException", "GpuGraph", "GpuGraphComputer", "KeyValue", "PageRankMapReduce",
     "PageRankVertexProgram", "ShortestDistanceMapReduce", "ShortestDistanceVertexProgram",
     "TitanGraphComputer",

@@ -101,7 +101,7 @@ EXPORTS = [
     "tgo_finish_load", "tgo_load_edges", "tgo_num_vertices", "tgo_vertex_ids", "tgo_bfs",
     "tgo_sssp", "tgo_copy_distances", "tgo_pagerank", "tgo_walkcount", "tgo_stats_get", "tgo_sync",
     "tgo_bfs_multi", "tgo_copy_multi_distances", "tgo_multi_stats",
-    "tgo_rmat_edges", "tgo_pick_roots",
+    "tgo_rmat_edges", "tgo_pick_roots", "tgo_synth_rows",
     # titan_gpu_olap_part.h (1-D vertex-partitioned multi-GPU)
     "tgo_load_partition", "tgo_part_layout", "tgo_load_partition_layout", "tgo_part_bfs_begin", "tgo_part_bfs_td", "tgo_part_bfs_claim", "tgo_part_bfs_bu",
     "tgo_part_bfs_end", "tgo_part_pr_begin", "tgo_part_pr_step", "tgo_part_pr_end", "tgo_rmat_partition",
@@ -154,6 +154,8 @@ def load() -> C.CDLL:
         "tgo_rmat_edges": (C.c_int, [C.c_int32, C.c_int32, C.c_uint64, C.c_int64, C.c_int64,
                                      _i32p, _i32p, _i32p, C.c_int32]),
         "tgo_pick_roots": (C.c_int, [C.c_int64, C.c_int64, _i32p, _i32p, C.c_uint64, C.c_int32, _i64p]),
+        "tgo_synth_rows": (C.c_int, [C.c_int64, C.c_int64, _i32p, _i32p, _i32p, C.c_int64, C.c_int32, C.c_int32,
+                                     _i64p, _i64p, _i64p, _i64p, P(C.c_uint8), _i64p]),
         "tgo_load_partition": (C.c_int, [vp, C.c_int64, C.c_int64, C.c_int64, P(Edges), P(LoadOpts)]),
         "tgo_part_layout": (C.c_int, [P(Edges), C.c_int64, C.c_int64, C.c_int64, C.c_int32, _i32p]),
         "tgo_load_partition_layout": (C.c_int, [vp, C.c_int64, C.c_int64, C.c_int64, P(Edges), P(LoadOpts), _i32p]),

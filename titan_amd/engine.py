@@ -218,6 +218,46 @@ def rmat_edges(scale, edge_factor=16, seed=0x54495441, weights=False, threads=0)
     return src, dst, w
 
 
+class Rows:
+    """Scanned edgestore rows in the tgo_rows layout (StaticArrayEntryList per row)."""
+
+    def __init__(self, keys, entry_begin, byte_begin, data, limit_valpos):
+        self.keys, self.entry_begin, self.byte_begin = keys, entry_begin, byte_begin
+        self.data, self.limit_valpos = data, limit_valpos
+
+    @property
+    def nrows(self):
+        return len(self.keys)
+
+
+USER_EDGE_LABEL_1 = (1 << 6) | 21     # IDManager.getSchemaId(UserEdgeLabel, 1)
+
+
+def synth_rows(n, src, dst, weight=None, label_id=USER_EDGE_LABEL_1, partition_bits=5, threads=0):
+    """Byte-exact edgestore rows of a directed edge list (include/tgo_synth.h)."""
+    lib = L.load()
+    src = np.ascontiguousarray(src, dtype=np.int32)
+    dst = np.ascontiguousarray(dst, dtype=np.int32)
+    w = None if weight is None else np.ascontiguousarray(weight, dtype=np.int32)
+    sz = np.zeros(3, np.int64)
+    args = (n, len(src), L.ptr(src, C.c_int32), L.ptr(dst, C.c_int32), L.ptr(w, C.c_int32), label_id,
+            partition_bits, threads, L.ptr(sz, C.c_int64))
+    rc = lib.tgo_synth_rows(*args, None, None, None, None, None)
+    if rc:
+        raise TitanException(rc, "tgo_synth_rows failed")
+    nrows, nent, nbytes = (int(x) for x in sz)
+    keys = np.empty(nrows, np.int64)
+    eb = np.empty(nrows + 1, np.int64)
+    bb = np.empty(nrows + 1, np.int64)
+    data = np.empty(max(nbytes, 1), np.uint8)
+    lv = np.empty(max(nent, 1), np.int64)
+    rc = lib.tgo_synth_rows(*args, L.ptr(keys, C.c_int64), L.ptr(eb, C.c_int64), L.ptr(bb, C.c_int64),
+                            L.ptr(data, C.c_uint8), L.ptr(lv, C.c_int64))
+    if rc:
+        raise TitanException(rc, "tgo_synth_rows failed")
+    return Rows(keys, eb, bb, data[:nbytes], lv[:nent])
+
+
 def pick_roots(n, src, dst, nroots=64, seed=7):
     lib = L.load()
     out = np.zeros(nroots, dtype=np.int64)
