@@ -37,6 +37,20 @@ def log(*a):
         print("[bench]", *a, file=sys.stderr, flush=True)
 
 
+def host_cores():
+    """CPUs this process may run on: the affinity mask, capped by a cgroup CPU quota
+    (cpu.max) when one is set — on the GPU box os.cpu_count() shows the whole machine."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -47,7 +61,9 @@ def parse():
     p.add_argument("--roots", type=int, default=64)
     p.add_argument("--pr-iters", type=int, default=20)
     p.add_argument("--cpu-baseline", type=int, default=1, help="0 disables the oracle timing")
-    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--cpu-threads", type=int, default=0, help="oracle threads (0 = every CPU this process may use)")
+    p.add_argument("--rows-scale", type=int, default=20,
+                   help="configs[1]: single-source BFS over byte-exact edgestore rows of this RMAT scale (0 = off)")
     p.add_argument("--sssp-roots", type=int, default=4, help="delta-stepping SSSP leg (configs[4]); 0 disables")
     p.add_argument("--delta", type=int, default=0, help="delta-stepping bucket width (0 = engine default)")
     p.add_argument("--layout", type=int, default=1,
@@ -126,25 +142,38 @@ def run_single(args):
     from titan_amd import _lib as L
     scale = args.scale
     n = 1 << scale
+    cores = host_cores()
     t0 = time.perf_counter()
     src, dst, _ = rmat_edges(scale, args.edge_factor, seed=0x54495441)
     m = len(src)
     roots = pick_roots(n, src, dst, args.roots, seed=7)
-    log(f"rmat scale {scale}: n={n} m={m} generated in {time.perf_counter() - t0:.1f}s")
+    log(f"rmat scale {scale}: n={n} m={m} generated in {time.perf_counter() - t0:.1f}s ({cores} host cores)")
+    load = {}
     t0 = time.perf_counter()
-    bfs_eng = Engine(device=0, host_threads=16).load_edges(n, src, dst, L.SCOPE_BOTH_E, apply_cap=False)
+    bfs_eng = Engine(device=0, host_threads=cores).load_edges(n, src, dst, L.SCOPE_BOTH_E, apply_cap=False)
+    load["bfs_bothE_wall_ms"] = round((time.perf_counter() - t0) * 1e3, 1)
+    load["bfs_bothE_engine_ms"] = round(bfs_eng.stats()["load_ms"], 1)
     log(f"bfs graph (bothE, uncapped) loaded in {time.perf_counter() - t0:.1f}s")
     t0 = time.perf_counter()
-    pr_eng = Engine(device=0, host_threads=16).load_edges(n, src, dst, L.SCOPE_IN_E, apply_cap=True)
+    pr_eng = Engine(device=0, host_threads=cores).load_edges(n, src, dst, L.SCOPE_IN_E, apply_cap=True)
     pst = pr_eng.stats()
+    load["pagerank_inE_wall_ms"] = round((time.perf_counter() - t0) * 1e3, 1)
+    load["pagerank_inE_engine_ms"] = round(pst["load_ms"], 1)
     log(f"pagerank graph (inE, capped: {pst['truncated_results']} truncated rows) loaded in "
         f"{time.perf_counter() - t0:.1f}s")
     # per-root reached counts (untimed): m_R, n_R for GTEPS and algorithmic bytes
     bfs_eng.bfs_multi(roots, n, L.SCOPE_BOTH_E, seed_is_dense=True, stats=True, fetch=False)
     nR, mR = bfs_eng.multi_stats(len(roots))
-    # single-source reference numbers (untimed side measurement, Graph500 style, 8 roots)
+    # self-check (untimed): two of the sweep's sources against their single-source runs
+    import ctypes as C
+    ms = np.empty(n, np.int64)
+    checked = 0
+    for i in (0, len(roots) - 1):
+        bfs_eng.lib.tgo_copy_multi_distances(bfs_eng.ctx, i, L.ptr(ms, C.c_int64))
+        checked += int(np.array_equal(ms, bfs_eng.bfs(int(roots[i]), n, L.SCOPE_BOTH_E, seed_is_dense=True)))
+    # single-source side measurement (untimed, Graph500 style: every one of the 64 roots)
     ss_t, depth0 = [], 1
-    for i, r in enumerate(roots[:8]):
+    for i, r in enumerate(roots):
         bfs_eng.bfs(int(r), n, L.SCOPE_BOTH_E, seed_is_dense=True, fetch=False)
         t = time.perf_counter()
         bfs_eng.bfs(int(r), n, L.SCOPE_BOTH_E, seed_is_dense=True, fetch=False)
@@ -193,26 +222,74 @@ def run_single(args):
     roof_pr = roofline("pagerank_update (gather_short + long-row chunks)", pr_bytes / (pks.mean() / upd) / 1e9,
                        "4*m + 8*(n+1) + 24*n per update", "pagerank_update", pr_bytes)
     bfs_share = float(bts.sum()) / (float(bts.sum()) + float(pts.sum()))
-    del pr_eng
-    sssp = sssp_leg(args, n, src, dst, roots) if args.sssp_roots > 0 else None
+    del pr_eng, bfs_eng
+    sssp = sssp_leg(args, n, src, dst, roots, cores) if args.sssp_roots > 0 else None
+    rows_leg = config2_rows_leg(args, cores) if args.rows_scale > 0 else None
     cpu = None
     if args.cpu_baseline:
         # levels counts the final empty level; the eccentricity is one less
-        cpu = cpu_baseline(n, src, dst, roots, mR, max(int(depth[0]) - 1, 1), args.cpu_threads)
+        cpu = cpu_baseline(args, n, src, dst, roots, mR, max(int(depth[0]) - 1, 1),
+                           args.cpu_threads or cores, pr_s_iter_gpu=float(pks.mean()) / upd)
     line = result_line(args, 1, scale, n, m, roots, elapsed, teps, hmean, float(pts.mean()) / upd, e_in,
                        roof_bfs, roof_pr, bfs_share, cpu, "single")
+    line["load"] = load
+    line["validation"] = {"msbfs_vs_single_source": f"{checked}/2 sources bit-exact (untimed self-check); "
+                                                    "full-size oracle parity: tests/test_gpu_fullsize.py"}
     line["sssp"] = sssp
+    line["config2_rows"] = rows_leg
     print(json.dumps(line), flush=True)
 
 
-def sssp_leg(args, n, src, dst, roots):
+def config2_rows_leg(args, cores):
+    """configs[1]: RMAT scale 20 as byte-exact edgestore rows (what the scan hands to
+    VertexJobConverter), fed to tgo_load_rows in readBatchSize work blocks, then
+    single-source BFS (bothE, Graph500 style) from 64 seeded roots.  Reports the decode +
+    CSR assembly + upload time separately from the traversal."""
+    from titan_amd import Engine, Schema, pick_roots, rmat_edges, synth_rows
+    from titan_amd import _lib as L
+    scale = args.rows_scale
+    n = 1 << scale
+    src, dst, _ = rmat_edges(scale, args.edge_factor, seed=0x54495441)
+    roots = pick_roots(n, src, dst, args.roots, seed=7)
+    label = (1 << 6) | 21                      # IDManager.getSchemaId(UserEdgeLabel, 1)
+    t0 = time.perf_counter()
+    rows = synth_rows(n, src, dst, None, label_id=label, threads=cores)
+    encode_s = time.perf_counter() - t0
+    vid = ((roots >> 5) + 1) << 5
+    vid = (vid + (roots & 31)) << 3             # IDManager.constructId(i/32 + 1, i%32), pb = 5
+    schema = Schema([{"type_id": label, "multiplicity": 0}], [])
+    t0 = time.perf_counter()
+    eng = Engine(device=0, host_threads=cores).load_rows(rows, schema, L.SCOPE_BOTH_E, batch_rows=10 * 1024)
+    load_s = time.perf_counter() - t0
+    st = eng.stats()
+    nbytes, nent = int(rows.byte_begin[-1]), int(rows.entry_begin[-1])
+    del rows
+    t_all, mR = [], []
+    for r in vid:
+        eng.bfs(int(r), n, L.SCOPE_BOTH_E, stats=True, fetch=False)
+        mR.append(eng.stats()["reached_entries"])
+        t = time.perf_counter()
+        eng.bfs(int(r), n, L.SCOPE_BOTH_E, fetch=False)
+        t_all.append(time.perf_counter() - t)
+    mR = np.array(mR, np.float64) / 2.0
+    t_all = np.array(t_all)
+    return {"workload": f"rmat{scale}-edgestore-rows-bothE-single-source-bfs", "roots": len(vid),
+            "rows": int(st["num_vertices"]), "entries": nent, "row_bytes": nbytes,
+            "rows_encode_s": round(encode_s, 3),
+            "load_rows_ms": round(load_s * 1e3, 1), "engine_load_ms": round(st["load_ms"], 1),
+            "decode_entries_per_s": round(nent / load_s, 1),
+            "gteps_hmean": round(len(t_all) / float(np.sum(t_all / mR)) / 1e9, 4),
+            "ms_per_root": round(float(t_all.mean()) * 1e3, 3)}
+
+
+def sssp_leg(args, n, src, dst, roots, cores=16):
     """configs[4] on one GPU: delta-stepping SSSP (ShortestDistanceVertexProgram, inE scope,
     int32 weights w = 1 + splitmix64 mod 255, parity cap on) from a few of the BFS roots on
     the same RMAT graph; GTEPS = pull entries of reached vertices / device time."""
     from titan_amd import Engine, rmat_edges
     from titan_amd import _lib as L
     _, _, w = rmat_edges(args.scale, args.edge_factor, seed=0x54495441, weights=True)
-    eng = Engine(device=0, host_threads=16).load_edges(n, src, dst, L.SCOPE_IN_E, weight=w, apply_cap=True)
+    eng = Engine(device=0, host_threads=cores).load_edges(n, src, dst, L.SCOPE_IN_E, weight=w, apply_cap=True)
     del w
     res = []
     for r in roots:
@@ -392,13 +469,19 @@ def sssp_leg_partitioned(args, world, rank, local_rank, n, lo, hi, src, dst, wgt
             "phases": int(np.mean([x[2] for x in res]))}
 
 
-def cpu_baseline(n, src, dst, roots, mR, depth, threads):
-    """Oracle (C restatement of Fulgora: every vertex every superstep, hash-map message
-    lookup by Titan id) on ONE root of the same graph, timed on this host's cores."""
+def cpu_baseline(args, n, src, dst, roots, mR, depth, threads, pr_s_iter_gpu=None):
+    """The oracle (C restatement of Fulgora: every vertex executes every superstep and looks
+    up each neighbour's message in a hash map by Titan id, as FulgoraVertexMemory does) on
+    bounded samples of the same workload, on this host's cores:
+      bfs      : root 0 of the sweep, bothE, maxDepth = its eccentricity (complete result)
+      pagerank : iterations(3) on the capped inE graph -> seconds per superstep
+      sssp     : 4 hop-bounded supersteps of the weighted inE program -> seconds per superstep
+    Row decode / preload is timed apart (the reference pays it in EVERY superstep)."""
+    out = {"value": None, "unit": "GTEPS", "cores": threads, "kind": "port"}
     try:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import fulgora as fr
-        threads = max(1, min(threads, os.cpu_count() or 1))
+        from titan_amd import rmat_edges
         t0 = time.perf_counter()
         g = fr.OracleGraph.from_edges(n, src, dst)
         load_s = time.perf_counter() - t0
@@ -408,11 +491,32 @@ def cpu_baseline(n, src, dst, roots, mR, depth, threads):
         d, it = g.shortest_distance(int((int(roots[0]) + 1) << 3), int(depth), 2, weighted=False, threads=threads)
         t = time.perf_counter() - t0
         del g
-        return {"value": round(float(mR[0]) / 2.0 / t / 1e9, 6), "unit": "GTEPS", "cores": threads, "kind": "port",
-                "sample": f"1 of {len(roots)} roots (root 0), same RMAT graph, bothE, maxDepth {depth} "
-                          f"({it + 1} supersteps, {t:.1f}s; row decode/preload {load_s:.1f}s excluded)"}
+        out["value"] = round(float(mR[0]) / 2.0 / t / 1e9, 6)
+        out["sample"] = (f"BFS: 1 of {len(roots)} roots (root 0), same RMAT graph, bothE, maxDepth {depth} "
+                         f"({it + 1} supersteps, {t:.1f}s); PageRank: iterations(3) (4 supersteps) on the capped inE "
+                         f"graph; SSSP: maxDepth 3 (4 supersteps) weighted inE; edge-list preload timed apart")
+        out["bfs"] = {"gteps": out["value"], "seconds": round(t, 3), "supersteps": it + 1,
+                      "preload_s": round(load_s, 2)}
+        _, _, w = rmat_edges(args.scale, args.edge_factor, seed=0x54495441, weights=True)
+        t0 = time.perf_counter()
+        g = fr.OracleGraph.from_edges(n, src, dst, w, hard_limit=100000)
+        load_s = time.perf_counter() - t0
+        del w
+        t0 = time.perf_counter()
+        g.pagerank(0.85, n, 3, threads=threads)
+        t = time.perf_counter() - t0
+        pr = {"s_per_superstep": round(t / 4, 4), "supersteps": 4, "preload_s": round(load_s, 2)}
+        if pr_s_iter_gpu:
+            pr["gpu_speedup_per_update"] = round(t / 4 / pr_s_iter_gpu, 1)
+        out["pagerank_s_per_iter"] = pr
+        t0 = time.perf_counter()
+        g.shortest_distance(int((int(roots[0]) + 1) << 3), 3, 1, weighted=True, threads=threads)
+        t = time.perf_counter() - t0
+        out["sssp"] = {"s_per_superstep": round(t / 4, 4), "supersteps": 4}
+        del g
     except Exception as e:  # noqa: BLE001
-        return {"value": None, "unit": "GTEPS", "cores": threads, "kind": "port", "sample": f"failed: {e}"}
+        out["sample"] = f"failed: {e}"
+    return out
 
 
 def main():

@@ -470,3 +470,63 @@ def test_all_gathered_layout_is_a_rangewise_degree_order():
         assert np.all(np.diff(b) <= 0)                       # hottest group first
         for g in np.unique(b):                               # row order kept inside a group
             assert np.all(np.diff(inv[b == g]) > 0)
+
+
+def _subgroup_worker(rank, world, port, scale, roots, out_q):
+    """Ranks {0, 3} and {1, 2} run the drivers concurrently on two subgroups: every
+    collective (counts included) must stay inside its group or the run hangs / mixes sums."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from titan_amd import rmat_edges
+    from titan_amd.distributed import (distributed_bfs, distributed_msbfs, distributed_pagerank, distributed_sssp,
+                                       partition_range)
+    groups = {0: dist.new_group([0, 3]), 1: dist.new_group([1, 2])}
+    gid = 0 if rank in (0, 3) else 1
+    grp = groups[gid]
+    grank = dist.get_rank(grp)
+    n = 1 << scale
+    src, dst, w = rmat_edges(scale, 8, seed=31 + gid, weights=True)
+    lo, hi = partition_range(n, 2, grank)
+    res = {}
+    be = NumpyPartBackend(n, lo, hi, src, dst)
+    d, reached, _ = distributed_bfs(be, roots[gid], n, group=grp)
+    r, e, _ = distributed_msbfs(be, [roots[gid], roots[1 - gid]], n, group=grp)
+    pr = distributed_pagerank(be, 0.85, n, 6, group=grp)
+    bw = NumpyPartBackend(n, lo, hi, src, dst, w=w, scope=1)
+    sd, sreached, _ = distributed_sssp(bw, roots[gid], 40, group=grp)
+    res = {"gid": gid, "lo": lo, "bfs": d, "reached": reached, "ms_reached": r, "pr": pr, "sssp": sd}
+    out_q.put(res)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_distributed_drivers_on_subgroups():
+    import fulgora as fr
+    from titan_amd import rmat_edges
+    world, scale = 4, 8
+    n = 1 << scale
+    roots = [3, 77]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_subgroup_worker, args=(r, world, port, scale, roots, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ids = (np.arange(n, dtype=np.int64) + 1) << 3
+    for gid in (0, 1):
+        parts = sorted((g for g in got if g["gid"] == gid), key=lambda g: g["lo"])
+        assert len(parts) == 2
+        src, dst, w = rmat_edges(scale, 8, seed=31 + gid, weights=True)
+        og = fr.OracleGraph.from_edges(n, src, dst, w)
+        od, _ = og.shortest_distance(int(ids[roots[gid]]), n, 2)
+        assert np.array_equal(np.concatenate([p["bfs"] for p in parts]), od)
+        assert parts[0]["reached"][0] == int((od != ABSENT).sum())
+        assert parts[0]["ms_reached"][0] == int((od != ABSENT).sum())
+        opr, _ = og.pagerank(0.85, n, 6)
+        assert np.abs(np.concatenate([p["pr"] for p in parts]) - opr).sum() <= 1e-6
+        osd, _ = og.shortest_distance(int(ids[roots[gid]]), n, 1, weighted=True)
+        assert np.array_equal(np.concatenate([p["sssp"] for p in parts]), osd)

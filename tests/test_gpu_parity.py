@@ -442,17 +442,21 @@ def test_partitioned_hubs_match_oracle():
 
 
 @pytest.mark.parametrize("iters", [2, 20])
-def test_rmat_pagerank_segmented(rmat12, iters, monkeypatch):
-    """The XCD-segmented PageRank gather (SegGather) forced on a small graph: same oracle
-    bar, bitwise reproducible, and within rounding of the plain CSR-adaptive gather."""
+@pytest.mark.parametrize("hot,seg", [(64, 256), (1000, 100), (4096, 512)])
+def test_rmat_pagerank_cache_blocked(rmat12, iters, hot, seg, monkeypatch):
+    """The cache-blocked PageRank gather (hot CSR + XCD-pinned cold segments, engine.hpp
+    ColdBlocks) forced onto a small graph with tiny hot sets / segments (many segments, so
+    every XCD has several): oracle bar, bitwise reproducible, within rounding of the plain
+    CSR-adaptive gather.  hot >= n means nothing is cold (plain path)."""
     n, src, dst, w, ids, oracle, roots = rmat12
-    monkeypatch.setenv("TGO_PR_SEGMENTS", "1")
+    monkeypatch.setenv("TGO_PR_HOT", str(hot))
+    monkeypatch.setenv("TGO_PR_SEG", str(seg))
     eng = Engine().load_edges(n, src, dst, IN)
     pr = eng.pagerank(0.85, n, iters)
     opr, _ = oracle.pagerank(0.85, n, iters)
     assert np.abs(pr - opr).sum() <= PR_L1_TOL
     assert np.array_equal(pr, eng.pagerank(0.85, n, iters))
-    monkeypatch.setenv("TGO_PR_SEGMENTS", "0")
+    monkeypatch.setenv("TGO_PR_BLOCKED", "0")
     plain = Engine().load_edges(n, src, dst, IN).pagerank(0.85, n, iters)
     assert np.abs(pr - plain).sum() <= 1e-12
 
@@ -468,12 +472,15 @@ def hub_graph(n, hub, k_in, k_out, seed=11):
 KTILE = 4096     # CSR-adaptive tile (engine.hpp kTile): rows longer than this are split in chunks
 
 
-@pytest.mark.parametrize("segments", ["0", "1"])
-def test_pagerank_long_rows(monkeypatch, segments):
-    """A hub whose in-list spans many tiles: 80 000 entries = ~20 chunks of kTile on the default
-    path (gather_chunks + finalize_long) and ~10 000 per source segment (> 2 kTile) on the
-    segmented path; both within 1e-6 L1 of the oracle and bitwise reproducible."""
-    monkeypatch.setenv("TGO_PR_SEGMENTS", segments)
+@pytest.mark.parametrize("blocked", ["0", "1"])
+def test_pagerank_long_rows(monkeypatch, blocked):
+    """A hub whose in-list spans many tiles: 80 000 entries = ~20 chunks of kTile through
+    gather_chunks + finalize_long; cache-blocked with 1024 hot sources and 4096-source cold
+    segments, its cold run per segment (~10 000 entries) is cut into several kTile pieces.
+    Both within 1e-6 L1 of the oracle and bitwise reproducible."""
+    monkeypatch.setenv("TGO_PR_BLOCKED", blocked)
+    monkeypatch.setenv("TGO_PR_HOT", "1024")
+    monkeypatch.setenv("TGO_PR_SEG", "4096")
     n = 1 << 15
     src, dst = hub_graph(n, 7, 80000, 0)
     assert (dst == 7).sum() > 2 * 8 * KTILE

@@ -42,6 +42,7 @@ struct tgo_ctx {
     int64_t part_relaxed = 0;   // partitioned SSSP: entries relaxed, phases
     int32_t part_phases = 0;
     int64_t pv_max_out = 0, pv_max_in = 0;   // largest OUT / IN list of a vertex cut
+    int num_cus = 256;          // compute units of the device (persistent launches)
 };
 
 namespace {
@@ -98,13 +99,24 @@ int threads_of(const tgo_ctx* ctx) {
     return std::max(1, std::min(t, 64));
 }
 
-// TGO_PR_SEGMENTS=1 builds the XCD-segmented PageRank lists (SegGather); off by default:
-// measured on MI355X, RMAT-24, it is slower than the plain CSR-adaptive gather (2.41 vs
-// 1.84 ms/update, profiles/r01n_kernel_stats.csv) — the per-(row, segment) partial sums
-// cost ~0.4 ms and the gathers did not speed up enough to pay for them.
-bool want_segments(int64_t nnz) {
-    const char* e = std::getenv("TGO_PR_SEGMENTS");
-    return nnz > 0 && e && e[0] == '1';
+// Cache-blocked PageRank in-lists (ColdBlocks, engine.hpp) for one-GPU PageRank.
+// TGO_PR_BLOCKED=0 turns it off; TGO_PR_HOT / TGO_PR_SEG set the hot threshold and the cold
+// segment size in sources (defaults: 2 MB of fp64 messages each, half the XCD's L2).
+int64_t env_i64(const char* name, int64_t dflt) {
+    const char* v = std::getenv(name);
+    return v ? std::atoll(v) : dflt;
+}
+constexpr int64_t kPrHotDefault = 262144, kPrSegDefault = 262144;
+
+// PageRank diagnostics (engine.hpp PrTuning): TGO_PR_DIAG=lo:hi gathers only sources in
+// [lo, hi) — a timing attribution tool, its ranks are wrong (scripts/pr_probe.py).
+PrTuning pr_tuning() {
+    PrTuning t;
+    if (const char* d = std::getenv("TGO_PR_DIAG")) {
+        long lo = 0, hi = 0;
+        if (std::sscanf(d, "%ld:%ld", &lo, &hi) == 2) { t.diag_lo = static_cast<int32_t>(lo); t.diag_hi = static_cast<int32_t>(hi); }
+    }
+    return t;
 }
 
 int upload_graph(tgo_ctx* ctx, HostGraph& h, bool allow_segments = true) {
@@ -153,25 +165,33 @@ int upload_graph(tgo_ctx* ctx, HostGraph& h, bool allow_segments = true) {
     HIP_TRY(blocks(h.out.off, g.rb_out));
     HIP_TRY(blocks(h.in.off, g.rb_in));
     g.rb_out_ready = g.rb_in_ready = true;
-    g.seg_in = SegGather();
-    g.seg_in_ready = false;
-    if (allow_segments && h.scope != TGO_SCOPE_BOTH_E && want_segments(static_cast<int64_t>(h.in.adj.size())) &&
-        h.in.adj.size() < (size_t(1) << 31)) {
-        HostSegments hs;
-        build_segments(h.in.off, h.in.adj, kTile, kMaxRows, hs);
-        SegGather& sg = g.seg_in;
-        sg.npairs = static_cast<int64_t>(hs.pslot.size());
-        sg.nblocks = static_cast<int64_t>(hs.sb_beg.size());
-        sg.max_seg_blocks = hs.max_seg_blocks;
-        sg.base = hs.base;
-        HIP_TRY(upload(ctx, sg.poff, hs.poff));
-        HIP_TRY(upload(ctx, sg.adj, hs.adj));
-        HIP_TRY(upload(ctx, sg.pslot, hs.pslot));
-        HIP_TRY(upload(ctx, sg.row_ptr, hs.row_ptr));
-        HIP_TRY(upload(ctx, sg.sb_beg, hs.sb_beg));
-        HIP_TRY(upload(ctx, sg.sb_end, hs.sb_end));
-        HIP_TRY(dev_alloc(ctx, sg.partial, sg.npairs));
-        g.seg_in_ready = true;
+    g.cold_in = ColdBlocks();
+    g.cold_in_ready = false;
+    if (allow_segments && h.scope != TGO_SCOPE_BOTH_E && env_i64("TGO_PR_BLOCKED", 1) != 0) {
+        HostColdBlocks hc;
+        if (build_cold_blocks(h.in.off, h.in.adj, h.n, env_i64("TGO_PR_HOT", kPrHotDefault),
+                              env_i64("TGO_PR_SEG", kPrSegDefault), kTile, kMaxRows, threads_of(ctx), hc)) {
+            ColdBlocks& cb = g.cold_in;
+            cb.hot = hc.hot;
+            cb.seg = hc.seg;
+            cb.npieces = static_cast<int64_t>(hc.cpid.size());
+            cb.nblocks = static_cast<int64_t>(hc.bbeg.size());
+            cb.max_xcd_blocks = hc.max_xcd_blocks;
+            cb.xbase = hc.xbase;
+            HIP_TRY(upload(ctx, cb.hcsr.off, hc.hoff));
+            HIP_TRY(upload(ctx, cb.hcsr.adj, hc.hadj));
+            cb.hcsr.nnz = static_cast<int64_t>(hc.hadj.size());
+            HIP_TRY(upload(ctx, cb.poff, hc.poff));
+            HIP_TRY(upload(ctx, cb.cadj, hc.cadj));
+            HIP_TRY(upload(ctx, cb.cptr, hc.cptr));
+            HIP_TRY(upload(ctx, cb.cpid, hc.cpid));
+            HIP_TRY(upload(ctx, cb.bbeg, hc.bbeg));
+            HIP_TRY(upload(ctx, cb.bend, hc.bend));
+            HIP_TRY(upload(ctx, cb.xblk, hc.xblk));
+            HIP_TRY(dev_alloc(ctx, cb.partial, cb.npieces));
+            HIP_TRY(blocks(hc.hoff, cb.rb_hot));
+            g.cold_in_ready = true;
+        }
     }
     // scratch
     Scratch& s = ctx->sc;
@@ -188,7 +208,7 @@ int upload_graph(tgo_ctx* ctx, HostGraph& h, bool allow_segments = true) {
     HIP_TRY(dev_alloc(ctx, s.dist, n));
     HIP_TRY(dev_alloc(ctx, s.msg, n));
     for (int i = 0; i < 3; ++i) HIP_TRY(dev_alloc(ctx, s.vec[i], n));
-    s.partial_cap = std::max<int64_t>({g.rb_out.nchunks, g.rb_in.nchunks, 1});
+    s.partial_cap = std::max<int64_t>({g.rb_out.nchunks, g.rb_in.nchunks, g.cold_in.rb_hot.nchunks, 1});
     HIP_TRY(dev_alloc(ctx, s.partial, s.partial_cap));
     HIP_TRY(dev_alloc(ctx, s.cnt, 1));
     if (!s.hcnt) {
@@ -495,6 +515,7 @@ int tgo_create(const tgo_options* opts, tgo_ctx** out) {
     tgo_ctx* ctx = new (std::nothrow) tgo_ctx();
     if (!ctx) return TGO_E_OOM;
     ctx->opts = *opts;
+    ctx->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     if (ctx->opts.hard_query_limit <= 0) ctx->opts.hard_query_limit = 100000;
     if (opts->stream) {
         ctx->stream = static_cast<hipStream_t>(opts->stream);
@@ -810,12 +831,17 @@ int tgo_pagerank(tgo_ctx* ctx, const tgo_pr_args* a, double* pr_out) {
     } else {
         HIP_TRY(k_pr_init(g.out, edge_count, contrib, pr, 1.0 / N, n, st));
         const double base = (1.0 - a->alpha) / N;
+        const PrTuning tune = pr_tuning();
+        const bool blocked = g.cold_in_ready && tune.diag_hi <= tune.diag_lo;
         for (int it = 2; it <= a->max_iterations; ++it) {
-            if (g.seg_in_ready)
-                HIP_TRY(k_pr_iter_seg(g.seg_in, contrib, edge_count, pr, contrib_next, a->alpha, base, n, st));
+            // the PAGE_RANK property is only read after the last superstep: write it there
+            double* pr_it = it == a->max_iterations ? pr : nullptr;
+            if (blocked)
+                HIP_TRY(k_pr_iter_cold(g.cold_in, contrib, edge_count, pr_it, contrib_next, s.partial, a->alpha, base,
+                                       st));
             else
-                HIP_TRY(k_pr_iter(g.in, g.rb_in, contrib, edge_count, pr, contrib_next, s.partial, a->alpha, base, n,
-                                  st));
+                HIP_TRY(k_pr_iter(g.in, g.rb_in, contrib, edge_count, pr_it, contrib_next, s.partial, a->alpha, base,
+                                  n, tune, st));
             std::swap(contrib, contrib_next);
         }
     }
@@ -1239,7 +1265,7 @@ int tgo_part_pr_step(tgo_ctx* ctx, const double* contrib_global, double* contrib
     Scratch& s = ctx->sc;
     // owned rows gather over their IN lists (global source ids) from the gathered vector
     HIP_TRY(k_pr_iter(g.in, g.rb_in, contrib_global, s.vec[0], reinterpret_cast<double*>(s.dist), contrib_local,
-                      s.partial, ctx->part_alpha, ctx->part_base, g.n, ctx->stream));
+                      s.partial, ctx->part_alpha, ctx->part_base, g.n, PrTuning{}, ctx->stream));
     return part_done(ctx);
 }
 

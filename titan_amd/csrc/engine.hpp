@@ -104,29 +104,46 @@ struct RowBlocks {
     std::vector<int64_t> h_blk;
 };
 
-// Source-segmented in-lists for the one-GPU PageRank gather.  Source u belongs to segment
-// (u >> kSegShift) & (kSeg-1): 16 fp64 messages = one 128-byte line per granule, so the
-// segments split the message vector's lines 8 ways, interleaved (hot lines of the
-// degree-grouped order land in every segment).  Blocks of segment s are launched at
-// blockIdx % 8 == s, i.e. (with the observed round-robin dispatch) on one XCD, so each
-// XCD's 4 MB L2 only caches its eighth of the message vector.  Every (row, segment) run of
-// entries is a "pair" (split at kTile entries); a pair's sum goes to its slot, slots are
-// ordered (row, segment, chunk) and a finalize adds a row's slots in that order — a fixed
-// order, so results are bitwise reproducible.
-constexpr int kSeg = 8;
-constexpr int kSegShift = 4;
-struct SegBase { int64_t b[kSeg + 1]; };     // segment s owns blocks [b[s], b[s+1])
-struct SegGather {
-    int64_t npairs = 0, nblocks = 0, max_seg_blocks = 0;
-    int64_t* poff = nullptr;    // npairs+1 entry offsets into adj (segment-major)
-    int32_t* adj = nullptr;     // in-entries regrouped by segment
-    int32_t* pslot = nullptr;   // pair -> slot
-    int64_t* row_ptr = nullptr; // n+1: row r's slots
-    int64_t* sb_beg = nullptr;  // per block: first pair
-    int64_t* sb_end = nullptr;  // per block: end pair
-    double* partial = nullptr;  // per slot
-    SegBase base{};
+// Cache-blocked PageRank gather.  The update is bound by L2 misses: every
+// random 8-byte gather that misses the XCD's 4 MB L2 costs one 128-byte fabric request,
+// served at ~55 G requests/s chip-wide whether the line sits in the Infinity Cache or in HBM
+// (profiles/r02f_pmc_calibration.txt).  So the in-lists are split by source:
+//   hot  : sources < hot (the hottest after the degree-grouped relabel; their messages fit
+//          in L2) -> gathered row by row as before, in a compact hot CSR;
+//   cold : sources >= hot, cut into segments of `seg` sources (a 2 MB slice of the message
+//          vector).  Segment s belongs to XCD s % 8 and its workgroups are launched at
+//          blockIdx % 8 == s % 8 in segment order, so each XCD's L2 holds the slice it is
+//          working on and every cold gather hits L2.  Each (row, segment) run of entries is
+//          a "piece" (split at kTile entries) whose sum is written to partial[piece] in piece
+//          order (streaming writes); the hot pass then adds a row's pieces in segment order.
+// Every sum has a fixed order: results are bitwise reproducible run to run.
+struct XcdBase { int64_t b[9]; };           // XCD x owns cold blocks [b[x], b[x+1]) of xblk
+struct ColdBlocks {
+    int64_t hot = 0, seg = 0, npieces = 0, nblocks = 0, max_xcd_blocks = 0;
+    DevCsr hcsr;                // hot CSR (n+1 offsets, hot entries)
+    int64_t* poff = nullptr;    // npieces+1: piece -> entry range in cadj
+    int32_t* cadj = nullptr;    // cold entries, segment-major, row order inside a segment
+    uint32_t* cptr = nullptr;   // n+1: row -> its pieces in cpid
+    int32_t* cpid = nullptr;    // pieces of each row, segment order
+    int64_t* bbeg = nullptr;    // per cold block: first piece
+    int64_t* bend = nullptr;    // per cold block: end piece
+    int32_t* xblk = nullptr;    // cold blocks in XCD-major launch order
+    double* partial = nullptr;  // npieces
+    XcdBase xbase{};
+    RowBlocks rb_hot;           // CSR-adaptive blocks of the hot CSR
 };
+struct HostColdBlocks {
+    int64_t hot = 0, seg = 0;
+    std::vector<int64_t> hoff, poff, bbeg, bend;
+    std::vector<int32_t> hadj, cadj, cpid, xblk;
+    std::vector<uint32_t> cptr;
+    XcdBase xbase{};
+    int64_t max_xcd_blocks = 0;
+};
+// Builds the split of a CSR (entries = source ids) at hot / seg (see ColdBlocks); returns
+// false when nothing is cold (n <= hot) or the piece count overflows 32-bit indices.
+bool build_cold_blocks(const std::vector<int64_t>& off, const std::vector<int32_t>& adj, int64_t n_src,
+                       int64_t hot, int64_t seg, int64_t tile, int64_t max_pieces, int threads, HostColdBlocks& hc);
 
 struct DevGraph {
     int64_t n = 0;
@@ -142,8 +159,8 @@ struct DevGraph {
     int64_t lo = 0, n_global = 0;
     RowBlocks rb_out, rb_in;    // CSR-adaptive blocks per pull list
     bool rb_out_ready = false, rb_in_ready = false;
-    SegGather seg_in;           // segmented in-lists (one-GPU PageRank); npairs 0 = not built
-    bool seg_in_ready = false;
+    ColdBlocks cold_in;         // cache-blocked in-lists (one-GPU PageRank)
+    bool cold_in_ready = false;
 };
 
 // Multi-source BFS levels as bit planes: the level of (v, source r) is
@@ -271,15 +288,21 @@ hipError_t k_part_claim(const View& push, const uint64_t* recv, int nslices, int
                         Counters* cnt, int32_t next_level, hipStream_t s);
 hipError_t k_unpermute_i32(const int32_t* in, const int32_t* perm, int32_t* out, int64_t n, hipStream_t s);
 
+// PageRank gather diagnostics: [diag_lo, diag_hi) = only sources in this range are gathered
+// (the others read as 0; results invalid) — attributes the update's time to source ranges.
+struct PrTuning {
+    int32_t diag_lo = 0, diag_hi = 0;
+};
+
 // CSR-adaptive gather
 hipError_t k_pr_init(const DevCsr& out, double* edge_count, double* contrib, double* pr,
                      double inv_n, int64_t n, hipStream_t s);
 hipError_t k_pr_iter(const DevCsr& in, const RowBlocks& rb, const double* contrib,
                      const double* edge_count, double* pr, double* contrib_next, double* partial,
-                     double alpha, double base, int64_t n, hipStream_t s);
+                     double alpha, double base, int64_t n, const PrTuning& t, hipStream_t s);
 hipError_t k_fill_f64(double* p, double v, int64_t n, hipStream_t s);
-hipError_t k_pr_iter_seg(const SegGather& sg, const double* contrib, const double* edge_count, double* pr,
-                         double* contrib_next, double alpha, double base, int64_t n, hipStream_t s);
+hipError_t k_pr_iter_cold(const ColdBlocks& cb, const double* contrib, const double* edge_count, double* pr,
+                          double* contrib_next, double* partial_long, double alpha, double base, hipStream_t s);
 hipError_t k_walk_iter(const DevCsr& out, const RowBlocks& rb, const int32_t* prev, int32_t* next,
                        int32_t* partial, int64_t n, hipStream_t s);
 
@@ -291,16 +314,6 @@ void build_row_blocks(const std::vector<int64_t>& off, int64_t tile, int64_t max
                       std::vector<int64_t>& blk, std::vector<int64_t>& chunk_row,
                       std::vector<int64_t>& chunk_beg, std::vector<int64_t>& chunk_end,
                       std::vector<int64_t>& long_row, std::vector<int64_t>& long_chunk);
-// Host side of SegGather: regroup a CSR's entries by source segment (see SegGather).
-struct HostSegments {
-    std::vector<int64_t> poff, row_ptr, sb_beg, sb_end;
-    std::vector<int32_t> adj, pslot;
-    SegBase base{};
-    int64_t max_seg_blocks = 0;
-};
-void build_segments(const std::vector<int64_t>& off, const std::vector<int32_t>& adj, int64_t tile,
-                    int64_t max_pairs, HostSegments& hs);
-
 constexpr int64_t kTile = 4096;      // entries per CSR-adaptive block (32 KB of fp64 in LDS; 2048: 1.84, 8192: 1.87 ms/update)
 constexpr int64_t kMaxRows = 1024;   // rows per CSR-adaptive block
 

@@ -687,69 +687,151 @@ void build_row_blocks(const std::vector<int64_t>& off, int64_t tile, int64_t max
     }
 }
 
-// ------------------------------------------------------------------ source segments
-// SegGather layout (engine.hpp): pass 1 counts every row's entries per segment to size
-// the pairs and slots; pass 2 lays the pairs of each segment out in row order and
-// scatters every row's entries into its segment runs, keeping list order inside a run.
-void build_segments(const std::vector<int64_t>& off, const std::vector<int32_t>& adj, int64_t tile,
-                    int64_t max_pairs, HostSegments& hs) {
+// ------------------------------------------------------------------ cache-blocked gather
+// ColdBlocks layout (engine.hpp).  Rows are split over `threads` contiguous ranges; pass 1
+// counts every row's hot entries and cold pieces per segment (per-thread segment totals),
+// pass 2 writes the hot CSR and scatters the cold runs into their segment, rows in order
+// (a thread's rows follow the previous thread's rows in every segment).
+bool build_cold_blocks(const std::vector<int64_t>& off, const std::vector<int32_t>& adj, int64_t n_src,
+                       int64_t hot, int64_t seg, int64_t tile, int64_t max_pieces, int threads, HostColdBlocks& hc) {
     const int64_t n = static_cast<int64_t>(off.size()) - 1;
-    auto seg = [](int32_t u) { return (static_cast<uint32_t>(u) >> kSegShift) & (kSeg - 1); };
-    hs.row_ptr.assign(n + 1, 0);
-    int64_t seg_pairs[kSeg] = {}, seg_entries[kSeg] = {};
-    for (int64_t r = 0; r < n; ++r) {
-        int64_t c[kSeg] = {};
-        for (int64_t k = off[r]; k < off[r + 1]; ++k) ++c[seg(adj[k])];
-        int64_t np = 0;
-        for (int s = 0; s < kSeg; ++s) {
-            const int64_t p = (c[s] + tile - 1) / tile;
-            np += p;
-            seg_pairs[s] += p;
-            seg_entries[s] += c[s];
+    if (hot <= 0 || seg <= 0 || n_src <= hot || n <= 0) return false;
+    const int64_t nseg = (n_src - hot + seg - 1) / seg;
+    threads = std::max(1, std::min<int>(threads, static_cast<int>(std::max<int64_t>(1, n / 4096))));
+    hc.hot = hot;
+    hc.seg = seg;
+    std::vector<int64_t> hcount(n), npc(n);
+    std::vector<std::vector<int64_t>> tpieces(threads, std::vector<int64_t>(nseg, 0)),
+        tentries(threads, std::vector<int64_t>(nseg, 0));
+    // A row's cold entries grouped by segment (stable: list order inside a segment).  Lists
+    // are sorted by internal id after the relabel, so the runs are normally contiguous.
+    auto cold_runs = [&](int64_t r, std::vector<std::pair<int64_t, int32_t>>& buf) {
+        buf.clear();
+        bool sorted = true;
+        int64_t last = -1;
+        for (int64_t k = off[r]; k < off[r + 1]; ++k) {
+            const int32_t u = adj[k];
+            if (u < hot) continue;
+            const int64_t sg = (u - hot) / seg;
+            if (sg < last) sorted = false;
+            last = sg;
+            buf.emplace_back(sg, u);
         }
-        hs.row_ptr[r + 1] = hs.row_ptr[r] + np;
+        if (!sorted)
+            std::stable_sort(buf.begin(), buf.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+    };
+    auto range = [&](int t) { return std::make_pair(n * t / threads, n * (t + 1) / threads); };
+    {
+        std::vector<std::thread> th;
+        for (int t = 0; t < threads; ++t)
+            th.emplace_back([&, t] {
+                std::vector<std::pair<int64_t, int32_t>> buf;
+                const auto [lo, hi] = range(t);
+                for (int64_t r = lo; r < hi; ++r) {
+                    int64_t h = 0;
+                    for (int64_t k = off[r]; k < off[r + 1]; ++k) h += adj[k] < hot;
+                    hcount[r] = h;
+                    cold_runs(r, buf);
+                    int64_t pcs = 0;
+                    for (size_t i = 0; i < buf.size();) {
+                        size_t j = i;
+                        while (j < buf.size() && buf[j].first == buf[i].first) ++j;
+                        const int64_t c = static_cast<int64_t>(j - i);
+                        const int64_t p = (c + tile - 1) / tile;
+                        tpieces[t][buf[i].first] += p;
+                        tentries[t][buf[i].first] += c;
+                        pcs += p;
+                        i = j;
+                    }
+                    npc[r] = pcs;
+                }
+            });
+        for (auto& x : th) x.join();
     }
-    const int64_t npairs = hs.row_ptr[n];
-    int64_t pcur[kSeg], ecur[kSeg];
-    pcur[0] = ecur[0] = 0;
-    for (int s = 1; s < kSeg; ++s) {
-        pcur[s] = pcur[s - 1] + seg_pairs[s - 1];
-        ecur[s] = ecur[s - 1] + seg_entries[s - 1];
-    }
-    int64_t pbase[kSeg + 1];
-    for (int s = 0; s < kSeg; ++s) pbase[s] = pcur[s];
-    pbase[kSeg] = npairs;
-    hs.poff.assign(npairs + 1, 0);
-    hs.pslot.assign(npairs, 0);
-    hs.adj.assign(adj.size(), 0);
-    for (int64_t r = 0; r < n; ++r) {
-        int64_t c[kSeg] = {};
-        for (int64_t k = off[r]; k < off[r + 1]; ++k) ++c[seg(adj[k])];
-        int64_t slot = hs.row_ptr[r];
-        for (int s = 0; s < kSeg; ++s)
-            for (int64_t k = 0; k < c[s]; k += tile) {
-                hs.poff[pcur[s]] = ecur[s] + k;
-                hs.pslot[pcur[s]++] = static_cast<int32_t>(slot++);
+    hc.hoff.assign(n + 1, 0);
+    hc.cptr.assign(n + 1, 0);
+    int64_t acc = 0;
+    for (int64_t r = 0; r < n; ++r) { hc.hoff[r + 1] = hc.hoff[r] + hcount[r]; acc += npc[r]; }
+    if (acc >= (int64_t(1) << 31)) return false;
+    for (int64_t r = 0; r < n; ++r) hc.cptr[r + 1] = hc.cptr[r] + static_cast<uint32_t>(npc[r]);
+    const int64_t npieces = acc;
+    // bases: segment-major, then thread order inside a segment
+    std::vector<int64_t> seg_pbase(nseg + 1, 0), seg_ebase(nseg + 1, 0);
+    std::vector<std::vector<int64_t>> pbase(threads, std::vector<int64_t>(nseg)), ebase(threads, std::vector<int64_t>(nseg));
+    {
+        int64_t pp = 0, ee = 0;
+        for (int64_t sg = 0; sg < nseg; ++sg) {
+            seg_pbase[sg] = pp;
+            seg_ebase[sg] = ee;
+            for (int t = 0; t < threads; ++t) {
+                pbase[t][sg] = pp; ebase[t][sg] = ee;
+                pp += tpieces[t][sg]; ee += tentries[t][sg];
             }
-        for (int64_t k = off[r]; k < off[r + 1]; ++k) hs.adj[ecur[seg(adj[k])]++] = adj[k];
+        }
+        seg_pbase[nseg] = pp;
+        seg_ebase[nseg] = ee;
     }
-    hs.poff[npairs] = static_cast<int64_t>(adj.size());
-    // blocks: greedy per segment, <= tile entries and <= max_pairs pairs (every pair <= tile)
-    hs.sb_beg.clear(); hs.sb_end.clear();
-    hs.max_seg_blocks = 0;
-    for (int s = 0; s < kSeg; ++s) {
-        hs.base.b[s] = static_cast<int64_t>(hs.sb_beg.size());
-        int64_t p = pbase[s];
-        while (p < pbase[s + 1]) {
+    hc.hadj.assign(static_cast<size_t>(hc.hoff[n]), 0);
+    hc.cadj.assign(static_cast<size_t>(seg_ebase[nseg]), 0);
+    hc.poff.assign(npieces + 1, 0);
+    hc.cpid.assign(npieces, 0);
+    {
+        std::vector<std::thread> th;
+        for (int t = 0; t < threads; ++t)
+            th.emplace_back([&, t] {
+                std::vector<std::pair<int64_t, int32_t>> buf;
+                std::vector<int64_t> pc = pbase[t], ec = ebase[t];
+                const auto [lo, hi] = range(t);
+                for (int64_t r = lo; r < hi; ++r) {
+                    int64_t h = hc.hoff[r];
+                    for (int64_t k = off[r]; k < off[r + 1]; ++k)
+                        if (adj[k] < hot) hc.hadj[h++] = adj[k];
+                    cold_runs(r, buf);
+                    int64_t slot = hc.cptr[r];
+                    for (size_t i = 0; i < buf.size();) {
+                        const int64_t sg = buf[i].first;
+                        size_t j = i;
+                        while (j < buf.size() && buf[j].first == sg) ++j;
+                        for (size_t q = i; q < j; q += static_cast<size_t>(tile)) {
+                            const size_t qe = std::min(j, q + static_cast<size_t>(tile));
+                            hc.poff[pc[sg]] = ec[sg];
+                            hc.cpid[slot++] = static_cast<int32_t>(pc[sg]++);
+                            for (size_t z = q; z < qe; ++z) hc.cadj[ec[sg]++] = buf[z].second;
+                        }
+                        i = j;
+                    }
+                }
+            });
+        for (auto& x : th) x.join();
+    }
+    hc.poff[npieces] = seg_ebase[nseg];
+    // cold blocks: greedy per segment (<= tile entries, <= max_pieces pieces), then the
+    // XCD-major launch order: XCD x runs segments x, x+8, x+16, ... in that order
+    std::vector<std::pair<int64_t, int64_t>> seg_blocks(nseg);
+    hc.bbeg.clear();
+    hc.bend.clear();
+    for (int64_t sg = 0; sg < nseg; ++sg) {
+        const int64_t b0 = static_cast<int64_t>(hc.bbeg.size());
+        int64_t p = seg_pbase[sg];
+        while (p < seg_pbase[sg + 1]) {
             int64_t e = p;
-            while (e < pbase[s + 1] && e - p < max_pairs && hs.poff[e + 1] - hs.poff[p] <= tile) ++e;
-            hs.sb_beg.push_back(p);
-            hs.sb_end.push_back(e);
+            while (e < seg_pbase[sg + 1] && e - p < max_pieces && hc.poff[e + 1] - hc.poff[p] <= tile) ++e;
+            hc.bbeg.push_back(p);
+            hc.bend.push_back(e);
             p = e;
         }
-        hs.max_seg_blocks = std::max<int64_t>(hs.max_seg_blocks, static_cast<int64_t>(hs.sb_beg.size()) - hs.base.b[s]);
+        seg_blocks[sg] = {b0, static_cast<int64_t>(hc.bbeg.size())};
     }
-    hs.base.b[kSeg] = static_cast<int64_t>(hs.sb_beg.size());
+    hc.xblk.clear();
+    hc.max_xcd_blocks = 0;
+    for (int x = 0; x < 8; ++x) {
+        hc.xbase.b[x] = static_cast<int64_t>(hc.xblk.size());
+        for (int64_t sg = x; sg < nseg; sg += 8)
+            for (int64_t b = seg_blocks[sg].first; b < seg_blocks[sg].second; ++b) hc.xblk.push_back(static_cast<int32_t>(b));
+        hc.max_xcd_blocks = std::max<int64_t>(hc.max_xcd_blocks, static_cast<int64_t>(hc.xblk.size()) - hc.xbase.b[x]);
+    }
+    hc.xbase.b[8] = static_cast<int64_t>(hc.xblk.size());
+    return true;
 }
 
 }  // namespace tgo

@@ -4,7 +4,7 @@
 // neighbours' previous-superstep messages (VertexMemoryHandler.receiveMessages,
 // VertexMemoryHandler.java:77-103):
 //   PageRank  (PageRankVertexProgram.java:84-89): PR'(v) = a * sum_{u in IN(v)} c(u) + (1-a)/N,
-//             c'(v) = PR'(v) / edgeCount(v)  — fp64, bandwidth-bound SpMV over the in-CSR.
+//             c'(v) = PR'(v) / edgeCount(v)  — fp64 SpMV over the in-CSR.
 //   DegreeCounter (OLAPTest.java:357-364): d'(v) = sum_{w in OUT(v)} d(w), Java int wrap.
 //
 // CSR-Adaptive (Greathouse & Daga, SC'14): rows are cut on the host into blocks of at
@@ -12,8 +12,13 @@
 // with coalesced index reads, then reduces rows from LDS — thread-per-row when the block
 // has many short rows, wave-per-row (fixed shuffle tree) when it has few.  Rows longer
 // than kTile are split into kTile chunks reduced by separate workgroups and summed in chunk
-// order by a finalize kernel.  Every sum has a fixed order: results are bitwise
-// reproducible run to run.
+// order by a finalize kernel.
+//
+// PageRank on one GPU is cache-blocked (ColdBlocks, engine.hpp): cold sources are gathered
+// segment by segment by workgroups pinned to the XCD that caches the segment (cold_gather),
+// their per-(row, segment) sums land in partial[], and the hot pass adds them to each row.
+// Every sum has a fixed order: results are bitwise reproducible run to run.
+#include <algorithm>
 #include <hip/hip_runtime.h>
 #include "engine.hpp"
 
@@ -28,6 +33,15 @@ struct PrOp {
     using T = double;
     const double* msg;
     __device__ __forceinline__ double load(int32_t u) const { return msg[u]; }
+    __device__ __forceinline__ static double add(double a, double b) { return a + b; }
+    __device__ __forceinline__ static double zero() { return 0.0; }
+};
+// Diagnostic only (TGO_PR_DIAG=lo:hi): gathers of sources outside [lo, hi) are skipped (read
+// as 0), so the time attributable to a source range can be measured.  Results are wrong.
+struct PrDiagOp {
+    using T = double;
+    const double* msg; int32_t lo, hi;
+    __device__ __forceinline__ double load(int32_t u) const { return (u >= lo && u < hi) ? msg[u] : 0.0; }
     __device__ __forceinline__ static double add(double a, double b) { return a + b; }
     __device__ __forceinline__ static double zero() { return 0.0; }
 };
@@ -50,8 +64,17 @@ struct PrFinal {
     const double* edge_count; double* pr; double* contrib_next; double alpha; double base;
     __device__ __forceinline__ void operator()(int64_t r, double sum) const {
         const double p = (alpha * sum) + base;      // PageRankVertexProgram.java:86
-        pr[r] = p;
-        contrib_next[r] = p / edge_count[r];        // :88, edgeCount 0 => +inf (never read)
+        if (pr) pr[r] = p;                          // the PAGE_RANK property: read after the last update only
+        contrib_next[r] = p / __builtin_nontemporal_load(edge_count + r);   // :88, edgeCount 0 => +inf (never read)
+    }
+};
+// Cache-blocked form: the row's cold pieces (segment order) are added after its hot sum.
+struct PrColdFinal {
+    PrFinal f; const uint32_t* cptr; const int32_t* cpid; const double* partial;
+    __device__ __forceinline__ void operator()(int64_t r, double sum) const {
+        const uint32_t e = cptr[r + 1];
+        for (uint32_t k = cptr[r]; k < e; ++k) sum += partial[cpid[k]];
+        f(r, sum);
     }
 };
 struct WalkFinal {
@@ -82,43 +105,55 @@ __device__ __forceinline__ void gather_tile(const int32_t* __restrict__ adj, int
     for (int j = 0; j < kPer; ++j) val[j] = idx[j] >= 0 ? op.load(idx[j]) : Op::zero();
 }
 
-template <class Op, class Fin>
-__global__ void __launch_bounds__(kBlock) gather_short(const int64_t* __restrict__ off,
-        const int32_t* __restrict__ adj, const int64_t* __restrict__ blk, Op op, Fin fin) {
-    using T = typename Op::T;
-    __shared__ T s_val[kTile];
-    const int64_t r0 = blk[blockIdx.x], r1 = blk[blockIdx.x + 1];
-    const int64_t s0 = off[r0], s1 = off[r1];
-    const int64_t nnz = s1 - s0;
-    if (nnz > kTile) return;                          // long row: handled by chunks
-    {
-        T val[kPer];
-        gather_tile(adj, s0, nnz, op, val);
+// Stage a tile's gathered messages in LDS.
+template <class Op>
+__device__ __forceinline__ void stage_tile(const int32_t* __restrict__ adj, int64_t s0, int64_t nnz, const Op& op,
+                                           typename Op::T* s_val) {
+    typename Op::T val[kPer];
+    gather_tile(adj, s0, nnz, op, val);
 #pragma unroll
-        for (int j = 0; j < kPer; ++j) {
-            const int k = threadIdx.x + j * kBlock;
-            if (k < nnz) s_val[k] = val[j];
-        }
+    for (int j = 0; j < kPer; ++j) {
+        const int k = threadIdx.x + j * kBlock;
+        if (k < nnz) s_val[k] = val[j];
     }
     __syncthreads();
-    const int64_t nrows = r1 - r0;
-    if (nrows > 64) {
-        for (int64_t r = r0 + threadIdx.x; r < r1; r += kBlock) {
+}
+
+// Reduce the runs [off[i], off[i+1]) of items i in [i0, i1) from the staged tile (base s0):
+// thread-per-run for many runs, wave-per-run with a fixed shuffle tree for few.
+template <class Op, class Emit>
+__device__ __forceinline__ void reduce_runs(const int64_t* __restrict__ off, int64_t i0, int64_t i1, int64_t s0,
+                                            const typename Op::T* s_val, const Emit& emit) {
+    using T = typename Op::T;
+    if (i1 - i0 > 64) {
+        for (int64_t i = i0 + threadIdx.x; i < i1; i += kBlock) {
             T sum = Op::zero();
-            const int64_t e = off[r + 1] - s0;
-            for (int64_t k = off[r] - s0; k < e; ++k) sum = Op::add(sum, s_val[k]);
-            fin(r, sum);
+            const int64_t e = off[i + 1] - s0;
+            for (int64_t k = off[i] - s0; k < e; ++k) sum = Op::add(sum, s_val[k]);
+            emit(i, sum);
         }
     } else {
         const int wave = threadIdx.x >> 6;
-        for (int64_t r = r0 + wave; r < r1; r += kBlock / 64) {
+        for (int64_t i = i0 + wave; i < i1; i += kBlock / 64) {
             T sum = Op::zero();
-            const int64_t e = off[r + 1] - s0;
-            for (int64_t k = off[r] - s0 + lane(); k < e; k += 64) sum = Op::add(sum, s_val[k]);
+            const int64_t e = off[i + 1] - s0;
+            for (int64_t k = off[i] - s0 + lane(); k < e; k += 64) sum = Op::add(sum, s_val[k]);
             sum = wave_sum(sum);
-            if (lane() == 0) fin(r, sum);
+            if (lane() == 0) emit(i, sum);
         }
     }
+}
+
+template <class Op, class Fin>
+__global__ void __launch_bounds__(kBlock) gather_short(const int64_t* __restrict__ off,
+        const int32_t* __restrict__ adj, const int64_t* __restrict__ blk, Op op, Fin fin) {
+    __shared__ typename Op::T s_val[kTile];
+    const int64_t r0 = blk[blockIdx.x], r1 = blk[blockIdx.x + 1];
+    const int64_t s0 = off[r0];
+    const int64_t nnz = off[r1] - s0;
+    if (nnz > kTile) return;                          // long row: handled by chunks
+    stage_tile(adj, s0, nnz, op, s_val);
+    reduce_runs<Op>(off, r0, r1, s0, s_val, fin);
 }
 
 template <class Op>
@@ -156,58 +191,22 @@ __global__ void finalize_long(const int64_t* __restrict__ long_row, const int64_
     }
 }
 
-// Segmented PageRank gather (SegGather, engine.hpp).  Block b serves segment b % 8 (its
-// XCD under round-robin dispatch): the block's pairs' messages are gathered into LDS, each
-// pair reduced from LDS (thread-per-pair for many short pairs, wave-per-pair otherwise)
-// and written to its slot.  Blocks past the segment's block count exit at once.
-__global__ void __launch_bounds__(kBlock) seg_gather(const int64_t* __restrict__ poff,
-        const int32_t* __restrict__ adj, const int64_t* __restrict__ sb_beg, const int64_t* __restrict__ sb_end,
-        SegBase bb, const int32_t* __restrict__ pslot, PrOp op, double* __restrict__ partial) {
+// Cold pass of the cache-blocked PageRank gather.  Workgroup b runs on XCD b % 8 (the
+// dispatcher deals workgroups round-robin over the 8 XCDs) and takes that XCD's (b / 8)-th
+// cold block, so each XCD walks its own segments in order and its L2 holds the 2 MB slice of
+// messages the block gathers from.  Workgroups past the XCD's block count exit at once.
+__global__ void __launch_bounds__(kBlock) cold_gather(const int64_t* __restrict__ poff,
+        const int32_t* __restrict__ cadj, const int64_t* __restrict__ bbeg, const int64_t* __restrict__ bend,
+        const int32_t* __restrict__ xblk, XcdBase xb, PrOp op, double* __restrict__ partial) {
     __shared__ double s_val[kTile];
-    const int sg = static_cast<int>(blockIdx.x & (kSeg - 1));
-    const int64_t j = bb.b[sg] + (blockIdx.x >> 3);
-    if (j >= bb.b[sg + 1]) return;
-    const int64_t p0 = sb_beg[j], p1 = sb_end[j];
+    const int x = static_cast<int>(blockIdx.x & 7);
+    const int64_t j = xb.b[x] + (blockIdx.x >> 3);
+    if (j >= xb.b[x + 1]) return;
+    const int64_t blk = xblk[j];
+    const int64_t p0 = bbeg[blk], p1 = bend[blk];
     const int64_t s0 = poff[p0];
-    const int64_t nnz = poff[p1] - s0;                 // <= kTile by construction
-    {
-        double val[kPer];
-        gather_tile(adj, s0, nnz, op, val);
-#pragma unroll
-        for (int k = 0; k < kPer; ++k) {
-            const int x = threadIdx.x + k * kBlock;
-            if (x < nnz) s_val[x] = val[k];
-        }
-    }
-    __syncthreads();
-    if (p1 - p0 > 64) {
-        for (int64_t p = p0 + threadIdx.x; p < p1; p += kBlock) {
-            double sum = 0.0;
-            const int64_t e = poff[p + 1] - s0;
-            for (int64_t k = poff[p] - s0; k < e; ++k) sum += s_val[k];
-            partial[pslot[p]] = sum;
-        }
-    } else {
-        const int wave = threadIdx.x >> 6;
-        for (int64_t p = p0 + wave; p < p1; p += kBlock / 64) {
-            double sum = 0.0;
-            const int64_t e = poff[p + 1] - s0;
-            for (int64_t k = poff[p] - s0 + lane(); k < e; k += 64) sum += s_val[k];
-            sum = wave_sum(sum);
-            if (lane() == 0) partial[pslot[p]] = sum;
-        }
-    }
-}
-
-// A row's slots added in (segment, chunk) order, then the PageRank update of the row.
-__global__ void seg_finalize(const int64_t* __restrict__ row_ptr, const double* __restrict__ partial, int64_t n,
-                             PrFinal fin) {
-    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
-        double sum = 0.0;
-        const int64_t e = row_ptr[r + 1];
-        for (int64_t k = row_ptr[r]; k < e; ++k) sum += partial[k];
-        fin(r, sum);
-    }
+    stage_tile(cadj, s0, poff[p1] - s0, op, s_val);    // <= kTile by construction
+    reduce_runs<PrOp>(poff, p0, p1, s0, s_val, [&](int64_t p, double sum) { partial[p] = sum; });
 }
 
 __global__ void pr_init(const int64_t* __restrict__ out_off, double* edge_count, double* contrib,
@@ -258,22 +257,19 @@ hipError_t k_fill_f64(double* p, double v, int64_t n, hipStream_t s) {
 }
 hipError_t k_pr_iter(const DevCsr& in, const RowBlocks& rb, const double* contrib,
                      const double* edge_count, double* pr, double* contrib_next, double* partial,
-                     double alpha, double base, int64_t n, hipStream_t s) {
+                     double alpha, double base, int64_t n, const PrTuning& t, hipStream_t s) {
     (void)n;
-    PrOp op{contrib};
-    PrFinal fin{edge_count, pr, contrib_next, alpha, base};
-    return run_gather(in, rb, op, fin, partial, s);
+    const PrFinal fin{edge_count, pr, contrib_next, alpha, base};
+    if (t.diag_hi > t.diag_lo) return run_gather(in, rb, PrDiagOp{contrib, t.diag_lo, t.diag_hi}, fin, partial, s);
+    return run_gather(in, rb, PrOp{contrib}, fin, partial, s);
 }
-hipError_t k_pr_iter_seg(const SegGather& sg, const double* contrib, const double* edge_count, double* pr,
-                         double* contrib_next, double alpha, double base, int64_t n, hipStream_t s) {
-    if (sg.max_seg_blocks > 0)
-        seg_gather<<<static_cast<unsigned>(sg.max_seg_blocks * kSeg), kBlock, 0, s>>>(
-            sg.poff, sg.adj, sg.sb_beg, sg.sb_end, sg.base, sg.pslot, PrOp{contrib}, sg.partial);
-    int64_t g = (n + kBlock - 1) / kBlock;
-    g = g < 1 ? 1 : (g > 8192 ? 8192 : g);
-    seg_finalize<<<static_cast<unsigned>(g), kBlock, 0, s>>>(sg.row_ptr, sg.partial, n,
-                                                             PrFinal{edge_count, pr, contrib_next, alpha, base});
-    return hipGetLastError();
+hipError_t k_pr_iter_cold(const ColdBlocks& cb, const double* contrib, const double* edge_count, double* pr,
+                          double* contrib_next, double* partial_long, double alpha, double base, hipStream_t s) {
+    if (cb.max_xcd_blocks > 0)
+        cold_gather<<<static_cast<unsigned>(cb.max_xcd_blocks * 8), kBlock, 0, s>>>(
+            cb.poff, cb.cadj, cb.bbeg, cb.bend, cb.xblk, cb.xbase, PrOp{contrib}, cb.partial);
+    const PrColdFinal fin{PrFinal{edge_count, pr, contrib_next, alpha, base}, cb.cptr, cb.cpid, cb.partial};
+    return run_gather(cb.hcsr, cb.rb_hot, PrOp{contrib}, fin, partial_long, s);
 }
 hipError_t k_walk_iter(const DevCsr& out, const RowBlocks& rb, const int32_t* prev, int32_t* next,
                        int32_t* partial, int64_t n, hipStream_t s) {

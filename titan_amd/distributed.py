@@ -196,9 +196,10 @@ class HipPartBackend:
         return out
 
 
-def _allreduce_counts(c, device):
+def _allreduce_counts(c, device, group):
+    """Global sums of per-rank counters (frontier size / entries, reached, ...) over `group`."""
     t = torch.tensor(c, dtype=torch.int64, device=device)
-    dist.all_reduce(t)
+    dist.all_reduce(t, group=group)
     return t.cpu().numpy()
 
 
@@ -214,10 +215,10 @@ def distributed_bfs(backend, seed: int, max_depth: int, alpha: float = 15.0, bet
     nb_local = backend.tensor(nwl, torch.int64)
     disc = backend.tensor(nwg, torch.int64)
     recv = backend.tensor(nwg, torch.int64)
-    total = _allreduce_counts([backend.total_entries, 0], dev)[0]
+    total = _allreduce_counts([backend.total_entries, 0], dev, group)[0]
     c = backend.bfs_begin(seed, nb_local)
     dist.all_gather_into_tensor(fb_global, nb_local, group=group)
-    nf, mf = _allreduce_counts(c, dev)
+    nf, mf = _allreduce_counts(c, dev, group)
     mu = total - mf
     bottom_up = False
     levels = 0
@@ -237,12 +238,12 @@ def distributed_bfs(backend, seed: int, max_depth: int, alpha: float = 15.0, bet
             dist.all_to_all_single(recv, disc, group=group)
             c = backend.bfs_claim(level, recv, world, nb_local)
         dist.all_gather_into_tensor(fb_global, nb_local, group=group)
-        nf, mf = _allreduce_counts(c, dev)
+        nf, mf = _allreduce_counts(c, dev, group)
         mu -= mf
         levels += 1
     out, reached = backend.bfs_end(fetch, stats)
     if stats:
-        reached = _allreduce_counts(reached, dev)
+        reached = _allreduce_counts(reached, dev, group)
     return out, reached, levels
 
 
@@ -276,8 +277,8 @@ def distributed_msbfs(backend, seeds, max_depth: int, ms_alpha: float = 12.0, st
     fr_global = backend.tensor(backend.n_global, torch.int64)
     cand = backend.tensor(backend.n_global, torch.int64)
     send = recv = None
-    total = _allreduce_counts([backend.total_entries, 0], dev)[0]
-    nf, mf = _allreduce_counts(backend.ms_begin(seeds, fr), dev)
+    total = _allreduce_counts([backend.total_entries, 0], dev, group)[0]
+    nf, mf = _allreduce_counts(backend.ms_begin(seeds, fr), dev, group)
     levels = 0
     for level in range(max_depth):
         if nf == 0:
@@ -300,7 +301,7 @@ def distributed_msbfs(backend, seeds, max_depth: int, ms_alpha: float = 12.0, st
             dist.all_to_all_single(recv, cand, group=group)
             c = backend.ms_settle(level, recv, world, frn)
         fr, frn = frn, fr
-        nf, mf = _allreduce_counts(c, dev)
+        nf, mf = _allreduce_counts(c, dev, group)
         levels += 1
     r, e = backend.ms_end(nseeds, stats)
     if stats:
@@ -335,7 +336,7 @@ def distributed_sssp(backend, seed: int, delta: int = 0, fetch: bool = True, sta
         delta = int(t.item())
     thr, phases = delta, 0
     while True:
-        if int(_allreduce_counts([qlen, 0], dev)[0]) == 0:
+        if int(_allreduce_counts([qlen, 0], dev, group)[0]) == 0:
             mn = torch.tensor([int(backend.sssp_pending_min()[0])], dtype=torch.int64, device=dev)
             dist.all_reduce(mn, op=dist.ReduceOp.MIN, group=group)
             mn = int(mn.item())
@@ -357,7 +358,7 @@ def distributed_sssp(backend, seed: int, delta: int = 0, fetch: bool = True, sta
         phases += 1
     out, reached = backend.sssp_end(fetch, stats)
     if stats:
-        reached = _allreduce_counts(reached, dev)
+        reached = _allreduce_counts(reached, dev, group)
     return out, reached, phases
 
 
