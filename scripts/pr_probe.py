@@ -20,22 +20,18 @@ n = 1 << scale
 src, dst, _ = rmat_edges(scale, 16, seed=0x54495441)
 eng = None
 loaded_with = None
-KEYS = ("TGO_PR_BLOCKED", "TGO_PR_HOT", "TGO_PR_SEG", "TGO_PR_DIAG")
+KEYS = ("TGO_PR_BLOCKED", "TGO_PR_HOT", "TGO_PR_SEG", "TGO_PR_DIAG", "TGO_PR_PACK")
 variants = [
     {},
     {"TGO_PR_BLOCKED": "0"},
-    {"TGO_PR_HOT": "131072", "TGO_PR_SEG": "131072"},
-    {"TGO_PR_HOT": "131072", "TGO_PR_SEG": "262144"},
+    {"TGO_PR_PACK": "0"},
+    {"TGO_PR_HOT": "262144", "TGO_PR_SEG": "262144"},
     {"TGO_PR_HOT": "262144", "TGO_PR_SEG": "524288"},
-    {"TGO_PR_HOT": "524288", "TGO_PR_SEG": "262144"},
-    {"TGO_PR_HOT": "524288", "TGO_PR_SEG": "524288"},
-    {"TGO_PR_HOT": "1048576", "TGO_PR_SEG": "262144"},
+    {"TGO_PR_HOT": "524288", "TGO_PR_SEG": "1048576"},
     {"TGO_PR_DIAG": "-2:-1"},                 # no gathers at all: index stream + finalize
-    {"TGO_PR_DIAG": "0:524288"},              # hot sources only (4 MB of messages)
-    {"TGO_PR_DIAG": f"524288:{n}"},           # cold sources only
     {},
 ]
-RELOAD = ("TGO_PR_BLOCKED", "TGO_PR_HOT", "TGO_PR_SEG")   # read at load time
+RELOAD = ("TGO_PR_BLOCKED", "TGO_PR_HOT", "TGO_PR_SEG", "TGO_PR_PACK")   # read at load time
 if os.environ.get("PR_PROBE_DEFAULT_ONLY"):
     variants = [{}]
 base = None

@@ -101,12 +101,13 @@ int threads_of(const tgo_ctx* ctx) {
 
 // Cache-blocked PageRank in-lists (ColdBlocks, engine.hpp) for one-GPU PageRank.
 // TGO_PR_BLOCKED=0 turns it off; TGO_PR_HOT / TGO_PR_SEG set the hot threshold and the cold
-// segment size in sources (defaults: 2 MB of fp64 messages each, half the XCD's L2).
+// segment size in sources (defaults: 4 MB of fp64 messages each, one XCD's L2; swept on
+// RMAT-24 in profiles/r02m_pr_probe.log: 512K/512K fastest of 128K..1M).
 int64_t env_i64(const char* name, int64_t dflt) {
     const char* v = std::getenv(name);
     return v ? std::atoll(v) : dflt;
 }
-constexpr int64_t kPrHotDefault = 262144, kPrSegDefault = 262144;
+constexpr int64_t kPrHotDefault = 524288, kPrSegDefault = 524288;
 
 // PageRank diagnostics (engine.hpp PrTuning): TGO_PR_DIAG=lo:hi gathers only sources in
 // [lo, hi) — a timing attribution tool, its ranks are wrong (scripts/pr_probe.py).
@@ -147,9 +148,12 @@ int upload_graph(tgo_ctx* ctx, HostGraph& h, bool allow_segments = true) {
     HIP_TRY(up(h.in, g.in));
     if (h.has_transpose) HIP_TRY(up(h.push_t, g.push_t));
     // CSR-adaptive blocks for the two pull gathers (walk counts: out; PageRank: in).
-    auto blocks = [&](const std::vector<int64_t>& off, RowBlocks& rb) -> hipError_t {
+    // CSR-adaptive blocks; `pack` (optional) source-sorts and packs the CSR's tiles first
+    auto blocks = [&](const std::vector<int64_t>& off, RowBlocks& rb, std::vector<int32_t>* pack = nullptr,
+                      bool* packed = nullptr) -> hipError_t {
         std::vector<int64_t> blk, crow, cbeg, cend, lrow, lch;
         build_row_blocks(off, kTile, kMaxRows, blk, crow, cbeg, cend, lrow, lch);
+        if (pack) *packed = pack_tiles(off, *pack, blk, cbeg, cend, kTile, threads_of(ctx));
         rb.nblocks = static_cast<int64_t>(blk.size()) - 1;
         rb.nchunks = static_cast<int64_t>(crow.size());
         rb.nlong = static_cast<int64_t>(lrow.size());
@@ -178,6 +182,11 @@ int upload_graph(tgo_ctx* ctx, HostGraph& h, bool allow_segments = true) {
             cb.nblocks = static_cast<int64_t>(hc.bbeg.size());
             cb.max_xcd_blocks = hc.max_xcd_blocks;
             cb.xbase = hc.xbase;
+            // rows >= n_active have no entries at all: the hot pass skips them (their rank
+            // after any update is (1-a)/N, written once at the end of the program)
+            cb.n_rows = g.n_active;
+            const std::vector<int64_t> hoff_act(hc.hoff.begin(), hc.hoff.begin() + cb.n_rows + 1);
+            HIP_TRY(blocks(hoff_act, cb.rb_hot, env_i64("TGO_PR_PACK", 1) ? &hc.hadj : nullptr, &cb.packed));
             HIP_TRY(upload(ctx, cb.hcsr.off, hc.hoff));
             HIP_TRY(upload(ctx, cb.hcsr.adj, hc.hadj));
             cb.hcsr.nnz = static_cast<int64_t>(hc.hadj.size());
@@ -189,7 +198,10 @@ int upload_graph(tgo_ctx* ctx, HostGraph& h, bool allow_segments = true) {
             HIP_TRY(upload(ctx, cb.bend, hc.bend));
             HIP_TRY(upload(ctx, cb.xblk, hc.xblk));
             HIP_TRY(dev_alloc(ctx, cb.partial, cb.npieces));
-            HIP_TRY(blocks(hc.hoff, cb.rb_hot));
+            HIP_TRY(dev_alloc(ctx, cb.csum, std::max<int64_t>(cb.n_rows, 1)));
+            HIP_TRY(hipMemset(cb.csum, 0, std::max<int64_t>(cb.n_rows, 1) * sizeof(double)));
+            cb.n_crows = static_cast<int64_t>(hc.crow.size());
+            HIP_TRY(upload(ctx, cb.crow, hc.crow));
             g.cold_in_ready = true;
         }
     }
@@ -844,6 +856,8 @@ int tgo_pagerank(tgo_ctx* ctx, const tgo_pr_args* a, double* pr_out) {
                                   n, tune, st));
             std::swap(contrib, contrib_next);
         }
+        if (blocked && a->max_iterations >= 2 && g.cold_in.n_rows < n)   // entry-less rows: PR = (1-a)/N
+            HIP_TRY(k_fill_f64(pr + g.cold_in.n_rows, base, n - g.cold_in.n_rows, st));
     }
     HIP_TRY(hipEventRecord(ctx->ev1, st));
     HIP_TRY(hipEventSynchronize(ctx->ev1));

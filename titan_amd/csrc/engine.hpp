@@ -115,9 +115,12 @@ struct RowBlocks {
 //          blockIdx % 8 == s % 8 in segment order, so each XCD's L2 holds the slice it is
 //          working on and every cold gather hits L2.  Each (row, segment) run of entries is
 //          a "piece" (split at kTile entries) whose sum is written to partial[piece] in piece
-//          order (streaming writes); the hot pass then adds a row's pieces in segment order.
+//          order (streaming writes; row-major slots measured slower: the scattered 8-byte
+//          writes cost more than they save, profiles/r02n_pr_probe.log); cold_fold adds each
+//          row's pieces (segment order) into csum[row], which the hot pass adds to its sum.
 // Every sum has a fixed order: results are bitwise reproducible run to run.
-struct XcdBase { int64_t b[9]; };           // XCD x owns cold blocks [b[x], b[x+1]) of xblk
+struct XcdBase { int64_t b[9]; };
+constexpr int kPackShift = 12;              // packed tile entry = source << 12 | slot (kTile <= 4096)           // XCD x owns cold blocks [b[x], b[x+1]) of xblk
 struct ColdBlocks {
     int64_t hot = 0, seg = 0, npieces = 0, nblocks = 0, max_xcd_blocks = 0;
     DevCsr hcsr;                // hot CSR (n+1 offsets, hot entries)
@@ -128,14 +131,19 @@ struct ColdBlocks {
     int64_t* bbeg = nullptr;    // per cold block: first piece
     int64_t* bend = nullptr;    // per cold block: end piece
     int32_t* xblk = nullptr;    // cold blocks in XCD-major launch order
-    double* partial = nullptr;  // npieces
+    double* partial = nullptr;  // npieces, in piece order (streaming writes)
+    double* csum = nullptr;     // n_rows: per-row cold sums (cold_fold; 0 for rows without pieces)
+    int32_t* crow = nullptr;    // rows that own cold pieces (ascending)
+    int64_t n_crows = 0;
+    int64_t n_rows = 0;         // rows the hot pass updates: [0, n_active) — the rest have no entries
     XcdBase xbase{};
     RowBlocks rb_hot;           // CSR-adaptive blocks of the hot CSR
+    bool packed = false;        // hot CSR tiles source-sorted and packed (pack_tiles)
 };
 struct HostColdBlocks {
     int64_t hot = 0, seg = 0;
     std::vector<int64_t> hoff, poff, bbeg, bend;
-    std::vector<int32_t> hadj, cadj, cpid, xblk;
+    std::vector<int32_t> hadj, cadj, cpid, xblk, crow;
     std::vector<uint32_t> cptr;
     XcdBase xbase{};
     int64_t max_xcd_blocks = 0;
@@ -309,6 +317,9 @@ hipError_t k_walk_iter(const DevCsr& out, const RowBlocks& rb, const int32_t* pr
 hipError_t scan_exclusive_i64(void*& tmp, size_t& tmp_bytes, const int64_t* in, int64_t* out,
                               int64_t n, hipStream_t s);
 
+// Source-sorted, packed tiles of a CSR (see graph_build.cpp); false if sources need > 19 bits.
+bool pack_tiles(const std::vector<int64_t>& off, std::vector<int32_t>& adj, const std::vector<int64_t>& blk,
+                const std::vector<int64_t>& cbeg, const std::vector<int64_t>& cend, int64_t tile, int threads);
 // Row-block construction (host) for a CSR.
 void build_row_blocks(const std::vector<int64_t>& off, int64_t tile, int64_t max_rows,
                       std::vector<int64_t>& blk, std::vector<int64_t>& chunk_row,

@@ -687,6 +687,39 @@ void build_row_blocks(const std::vector<int64_t>& off, int64_t tile, int64_t max
     }
 }
 
+// Source-sorted tiles (engine.hpp kPackShift): every CSR-adaptive tile's (and long-row
+// chunk's) entries are re-ordered by source and packed as (source << 12 | slot), slot = the
+// entry's position in the tile.  Lanes of one wave instruction then read neighbouring
+// sources — shared 128-byte lines are fetched once — and the gathered values are written
+// back to their slot, so the row sums keep the tile's row order.
+bool pack_tiles(const std::vector<int64_t>& off, std::vector<int32_t>& adj, const std::vector<int64_t>& blk,
+                const std::vector<int64_t>& cbeg, const std::vector<int64_t>& cend, int64_t tile, int threads) {
+    if (tile > (int64_t(1) << kPackShift)) return false;
+    for (int32_t u : adj)
+        if (u < 0 || u >= (int32_t(1) << (31 - kPackShift))) return false;
+    const int64_t nblk = static_cast<int64_t>(blk.size()) - 1, nch = static_cast<int64_t>(cbeg.size());
+    auto pack_range = [&](int64_t b, int64_t e, std::vector<uint32_t>& tmp) {
+        tmp.resize(static_cast<size_t>(e - b));
+        for (int64_t k = b; k < e; ++k)
+            tmp[k - b] = (static_cast<uint32_t>(adj[k]) << kPackShift) | static_cast<uint32_t>(k - b);
+        std::sort(tmp.begin(), tmp.end());
+        for (int64_t k = b; k < e; ++k) adj[k] = static_cast<int32_t>(tmp[k - b]);
+    };
+    threads = std::max(1, threads);
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads; ++t)
+        th.emplace_back([&, t] {
+            std::vector<uint32_t> tmp;
+            for (int64_t b = t; b < nblk; b += threads) {
+                const int64_t s0 = off[blk[b]], s1 = off[blk[b + 1]];
+                if (s1 - s0 <= tile) pack_range(s0, s1, tmp);       // longer: a long row, packed per chunk
+            }
+            for (int64_t c = t; c < nch; c += threads) pack_range(cbeg[c], cend[c], tmp);
+        });
+    for (auto& x : th) x.join();
+    return true;
+}
+
 // ------------------------------------------------------------------ cache-blocked gather
 // ColdBlocks layout (engine.hpp).  Rows are split over `threads` contiguous ranges; pass 1
 // counts every row's hot entries and cold pieces per segment (per-thread segment totals),
@@ -753,7 +786,11 @@ bool build_cold_blocks(const std::vector<int64_t>& off, const std::vector<int32_
     int64_t acc = 0;
     for (int64_t r = 0; r < n; ++r) { hc.hoff[r + 1] = hc.hoff[r] + hcount[r]; acc += npc[r]; }
     if (acc >= (int64_t(1) << 31)) return false;
-    for (int64_t r = 0; r < n; ++r) hc.cptr[r + 1] = hc.cptr[r] + static_cast<uint32_t>(npc[r]);
+    hc.crow.clear();
+    for (int64_t r = 0; r < n; ++r) {
+        hc.cptr[r + 1] = hc.cptr[r] + static_cast<uint32_t>(npc[r]);
+        if (npc[r]) hc.crow.push_back(static_cast<int32_t>(r));
+    }
     const int64_t npieces = acc;
     // bases: segment-major, then thread order inside a segment
     std::vector<int64_t> seg_pbase(nseg + 1, 0), seg_ebase(nseg + 1, 0);
@@ -805,13 +842,13 @@ bool build_cold_blocks(const std::vector<int64_t>& off, const std::vector<int32_
         for (auto& x : th) x.join();
     }
     hc.poff[npieces] = seg_ebase[nseg];
-    // cold blocks: greedy per segment (<= tile entries, <= max_pieces pieces), then the
-    // XCD-major launch order: XCD x runs segments x, x+8, x+16, ... in that order
-    std::vector<std::pair<int64_t, int64_t>> seg_blocks(nseg);
+    // cold blocks: greedy per segment (<= tile entries, <= max_pieces pieces), segment-major.
+    // The block list is cut into 8 contiguous ranges of equal entry counts, range x for XCD
+    // x: every XCD walks consecutive segments in order (a dense segment may be shared by two
+    // neighbouring XCDs, each caching its slice) and the XCDs finish together.
     hc.bbeg.clear();
     hc.bend.clear();
     for (int64_t sg = 0; sg < nseg; ++sg) {
-        const int64_t b0 = static_cast<int64_t>(hc.bbeg.size());
         int64_t p = seg_pbase[sg];
         while (p < seg_pbase[sg + 1]) {
             int64_t e = p;
@@ -820,15 +857,18 @@ bool build_cold_blocks(const std::vector<int64_t>& off, const std::vector<int32_
             hc.bend.push_back(e);
             p = e;
         }
-        seg_blocks[sg] = {b0, static_cast<int64_t>(hc.bbeg.size())};
     }
-    hc.xblk.clear();
+    const int64_t nb = static_cast<int64_t>(hc.bbeg.size());
+    hc.xblk.resize(nb);
+    for (int64_t b = 0; b < nb; ++b) hc.xblk[b] = static_cast<int32_t>(b);
+    const int64_t total = hc.poff[npieces];
     hc.max_xcd_blocks = 0;
+    int64_t b = 0;
     for (int x = 0; x < 8; ++x) {
-        hc.xbase.b[x] = static_cast<int64_t>(hc.xblk.size());
-        for (int64_t sg = x; sg < nseg; sg += 8)
-            for (int64_t b = seg_blocks[sg].first; b < seg_blocks[sg].second; ++b) hc.xblk.push_back(static_cast<int32_t>(b));
-        hc.max_xcd_blocks = std::max<int64_t>(hc.max_xcd_blocks, static_cast<int64_t>(hc.xblk.size()) - hc.xbase.b[x]);
+        hc.xbase.b[x] = b;
+        const int64_t target = total * (x + 1) / 8;
+        while (b < nb && (x == 7 || hc.poff[hc.bend[b]] <= target)) ++b;
+        hc.max_xcd_blocks = std::max<int64_t>(hc.max_xcd_blocks, b - hc.xbase.b[x]);
     }
     hc.xbase.b[8] = static_cast<int64_t>(hc.xblk.size());
     return true;

@@ -68,14 +68,11 @@ struct PrFinal {
         contrib_next[r] = p / __builtin_nontemporal_load(edge_count + r);   // :88, edgeCount 0 => +inf (never read)
     }
 };
-// Cache-blocked form: the row's cold pieces (segment order) are added after its hot sum.
+// Cache-blocked form: the row's cold sum (its pieces in segment order, cold_fold) is added
+// after its hot sum — one coalesced load, no dependent chain in the reduce loop.
 struct PrColdFinal {
-    PrFinal f; const uint32_t* cptr; const int32_t* cpid; const double* partial;
-    __device__ __forceinline__ void operator()(int64_t r, double sum) const {
-        const uint32_t e = cptr[r + 1];
-        for (uint32_t k = cptr[r]; k < e; ++k) sum += partial[cpid[k]];
-        f(r, sum);
-    }
+    PrFinal f; const double* csum;
+    __device__ __forceinline__ void operator()(int64_t r, double sum) const { f(r, sum + csum[r]); }
 };
 struct WalkFinal {
     int32_t* next;
@@ -156,6 +153,42 @@ __global__ void __launch_bounds__(kBlock) gather_short(const int64_t* __restrict
     reduce_runs<Op>(off, r0, r1, s0, s_val, fin);
 }
 
+// Packed, source-sorted tiles (pack_tiles): entry = source << kPackShift | slot.  The
+// gathered message goes back to its slot, so the row reduce is unchanged.
+template <class Fin>
+__global__ void __launch_bounds__(kBlock) gather_short_packed(const int64_t* __restrict__ off,
+        const int32_t* __restrict__ padj, const int64_t* __restrict__ blk, const double* __restrict__ msg, Fin fin) {
+    __shared__ double s_val[kTile];
+    const int64_t r0 = blk[blockIdx.x], r1 = blk[blockIdx.x + 1];
+    const int64_t s0 = off[r0];
+    const int64_t nnz = off[r1] - s0;
+    if (nnz > kTile) return;                          // long row: handled by chunks
+    {
+        int32_t v[kPer];
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+            const int64_t k = threadIdx.x + static_cast<int64_t>(j) * kBlock;
+            v[j] = k < nnz ? stream_idx(padj + s0 + k) : -1;
+        }
+        double val[kPer];
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) val[j] = v[j] >= 0 ? msg[v[j] >> kPackShift] : 0.0;
+#pragma unroll
+        for (int j = 0; j < kPer; ++j)
+            if (v[j] >= 0) s_val[v[j] & ((1 << kPackShift) - 1)] = val[j];
+    }
+    __syncthreads();
+    reduce_runs<PrOp>(off, r0, r1, s0, s_val, fin);
+}
+// A long row's chunk of packed entries: the chunk sum (source order, fixed).
+struct PackedOp {
+    using T = double;
+    const double* msg;
+    __device__ __forceinline__ double load(int32_t v) const { return msg[v >> kPackShift]; }
+    __device__ __forceinline__ static double add(double a, double b) { return a + b; }
+    __device__ __forceinline__ static double zero() { return 0.0; }
+};
+
 template <class Op>
 __global__ void __launch_bounds__(kBlock) gather_chunks(const int32_t* __restrict__ adj,
         const int64_t* __restrict__ cbeg, const int64_t* __restrict__ cend, Op op,
@@ -207,6 +240,18 @@ __global__ void __launch_bounds__(kBlock) cold_gather(const int64_t* __restrict_
     const int64_t s0 = poff[p0];
     stage_tile(cadj, s0, poff[p1] - s0, op, s_val);    // <= kTile by construction
     reduce_runs<PrOp>(poff, p0, p1, s0, s_val, [&](int64_t p, double sum) { partial[p] = sum; });
+}
+
+// Per-row cold sums of the rows that own pieces: the pieces added in segment order.
+__global__ void cold_fold(const int32_t* __restrict__ crow, int64_t ncrows, const uint32_t* __restrict__ cptr,
+                          const int32_t* __restrict__ cpid, const double* __restrict__ partial, double* __restrict__ csum) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < ncrows; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = crow[i];
+        double s = 0.0;
+        const uint32_t e = cptr[r + 1];
+        for (uint32_t k = cptr[r]; k < e; ++k) s += partial[cpid[k]];
+        csum[r] = s;
+    }
 }
 
 __global__ void pr_init(const int64_t* __restrict__ out_off, double* edge_count, double* contrib,
@@ -268,8 +313,25 @@ hipError_t k_pr_iter_cold(const ColdBlocks& cb, const double* contrib, const dou
     if (cb.max_xcd_blocks > 0)
         cold_gather<<<static_cast<unsigned>(cb.max_xcd_blocks * 8), kBlock, 0, s>>>(
             cb.poff, cb.cadj, cb.bbeg, cb.bend, cb.xblk, cb.xbase, PrOp{contrib}, cb.partial);
-    const PrColdFinal fin{PrFinal{edge_count, pr, contrib_next, alpha, base}, cb.cptr, cb.cpid, cb.partial};
-    return run_gather(cb.hcsr, cb.rb_hot, PrOp{contrib}, fin, partial_long, s);
+    {
+        int64_t g = (cb.n_crows + kBlock - 1) / kBlock;
+        g = std::max<int64_t>(1, std::min<int64_t>(g, 65536));
+        cold_fold<<<static_cast<unsigned>(g), kBlock, 0, s>>>(cb.crow, cb.n_crows, cb.cptr, cb.cpid, cb.partial, cb.csum);
+    }
+    const PrColdFinal fin{PrFinal{edge_count, pr, contrib_next, alpha, base}, cb.csum};
+    if (!cb.packed) return run_gather(cb.hcsr, cb.rb_hot, PrOp{contrib}, fin, partial_long, s);
+    const RowBlocks& rb = cb.rb_hot;
+    if (rb.nblocks > 0)
+        gather_short_packed<PrColdFinal><<<static_cast<unsigned>(rb.nblocks), kBlock, 0, s>>>(cb.hcsr.off, cb.hcsr.adj,
+                                                                                             rb.blk, contrib, fin);
+    if (rb.nchunks > 0) {
+        gather_chunks<PackedOp><<<static_cast<unsigned>(rb.nchunks), kBlock, 0, s>>>(cb.hcsr.adj, rb.chunk_beg,
+                                                                                    rb.chunk_end, PackedOp{contrib},
+                                                                                    partial_long);
+        finalize_long<PackedOp, PrColdFinal><<<grid_for(rb.nlong), kBlock, 0, s>>>(rb.long_row, rb.long_chunk, rb.nlong,
+                                                                                   partial_long, fin);
+    }
+    return hipGetLastError();
 }
 hipError_t k_walk_iter(const DevCsr& out, const RowBlocks& rb, const int32_t* prev, int32_t* next,
                        int32_t* partial, int64_t n, hipStream_t s) {
