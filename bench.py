@@ -101,7 +101,7 @@ def roofline(kernel, achieved_gbs, unit_desc, group=None, alg_bytes=None):
     if ent:
         r["traffic_detail"] = {"source": os.path.relpath(PMC_FILE, ROOT), "fetch_bytes_raw": round(ent["fetch_bytes_raw"]),
                                "write_bytes": round(ent["write_bytes"]), "l2_hit_rate": ent.get("l2_hit_rate"),
-                               "correction": ent["correction"]}
+                               "ea_read_requests": ent.get("ea_read_requests"), "correction": ent["correction"]}
     return r
 
 
@@ -219,7 +219,8 @@ def run_single(args):
     upd = max(args.pr_iters - 1, 1)
     e_in = int(pst["in_entries"])
     pr_bytes = 4.0 * e_in + 8.0 * (n + 1) + 24.0 * n
-    roof_pr = roofline("pagerank_update (gather_short + long-row chunks)", pr_bytes / (pks.mean() / upd) / 1e9,
+    roof_pr = roofline("pagerank_update (cache-blocked: cold_gather + cold_fold + gather_short_packed + long-row chunks)",
+                       pr_bytes / (pks.mean() / upd) / 1e9,
                        "4*m + 8*(n+1) + 24*n per update", "pagerank_update", pr_bytes)
     bfs_share = float(bts.sum()) / (float(bts.sum()) + float(pts.sum()))
     del pr_eng, bfs_eng

@@ -1,0 +1,79 @@
+package com.thinkaurelius.titan.graphdb.olap.gpu;
+
+import com.thinkaurelius.titan.core.TitanException;
+
+import java.nio.ByteBuffer;
+
+/**
+ * JNI binding of the MI355X engine's C-ABI (include/titan_gpu_olap.h), implemented by
+ * java/jni/titan_gpu_olap_jni.c over libtitan_gpu_olap.so.  Every call maps one C entry point;
+ * a non-zero status becomes a TitanException carrying tgo_last_error(), which is how the
+ * reference reports executor failures (FulgoraGraphComputer.java:165-174; the future of
+ * submit() then fails with ExecutionException, OLAPTest.java:222-239).
+ *
+ * Handles are opaque tgo_ctx pointers.  A handle is used by one thread at a time (the ABI's
+ * rule); CsrCollectingScanJob serialises its work-block flushes on the handle.
+ */
+public final class TgoNative {
+
+    static {
+        System.loadLibrary("titan_gpu_olap_jni");
+    }
+
+    private TgoNative() {}
+
+    /* tgo_scope: MessageScope.Local(__::outE / __::inE / __::bothE) */
+    public static final int SCOPE_OUT_E = 0, SCOPE_IN_E = 1, SCOPE_BOTH_E = 2;
+    /* tgo_sssp_mode */
+    public static final int SSSP_HOP_BOUNDED = 0, SSSP_DELTA = 1;
+    /* tgo_multiplicity (core/Multiplicity.java:21-75) */
+    public static final int MULTI = 0, SIMPLE = 1, MANY2ONE = 2, ONE2MANY = 3, ONE2ONE = 4;
+    /* tgo_datatype */
+    public static final int DT_BYTE = 1, DT_SHORT = 2, DT_INTEGER = 3, DT_LONG = 4, DT_FLOAT = 5, DT_DOUBLE = 6,
+            DT_BOOLEAN = 7;
+    /** TGO_DIST_ABSENT: no DISTANCE property was set (the vertex was not reached). */
+    public static final long DIST_ABSENT = Long.MIN_VALUE;
+
+    /** tgo_default_options + tgo_create; returns 0 when no gfx950 device is usable (no CPU fallback). */
+    public static native long create(int device, int partitionBits, int hostThreads, long hardQueryLimit);
+
+    public static native void destroy(long ctx);
+
+    public static native String lastError(long ctx);
+
+    /**
+     * tgo_load_rows: one work block of scanned rows in StaticArrayEntryList form
+     * (StaticArrayEntryList.java:15-50).  {@code entryBytes} must be a direct buffer.
+     * The schema is flattened: per edge label {typeId, multiplicity, nSortKey, sortKeyIds...,
+     * nSignature, signatureIds...}; per property key {keyId, datatype}.
+     */
+    public static native int loadRows(long ctx, long[] rowKeys, long[] rowEntryBegin, long[] rowByteBegin,
+                                      ByteBuffer entryBytes, long[] entryLimitValuePos, long[] edgeTypes,
+                                      long[] propertyKeys, int scope, boolean applyCap, long[] labelIds,
+                                      long weightKey);
+
+    public static native int finishLoad(long ctx);
+
+    public static native long[] vertexIds(long ctx);
+
+    /** tgo_bfs with the unit edge function; null on failure (see lastError). */
+    public static native long[] bfs(long ctx, long seedId, int maxDepth, int scope);
+
+    public static native long[] sssp(long ctx, long seedId, int maxDepth, int scope, int mode, long delta);
+
+    public static native double[] pageRank(long ctx, double alpha, long vertexCount, int maxIterations);
+
+    public static native int[] walkCount(long ctx, int length);
+
+    /** tgo_stats_get: {ghostVertices, truncatedResults, skippedRows, iterations, loadMs, lastKernelMs}. */
+    public static native double[] stats(long ctx);
+
+    static void check(long ctx, int rc) {
+        if (rc != 0) throw new TitanException("[" + rc + "] " + lastError(ctx));
+    }
+
+    static <T> T checked(long ctx, T result) {
+        if (result == null) throw new TitanException(lastError(ctx));
+        return result;
+    }
+}

@@ -16,5 +16,6 @@ run_pass() {   # $1 = dir name, rest = counters
     return $rc
 }
 BENCH_ARGS="$*"
-run_pass fetch FETCH_SIZE && run_pass write WRITE_SIZE && run_pass hit TCC_HIT_sum TCC_MISS_sum || exit 1
-python3 scripts/pmc_traffic.py $OUT/pmc_traffic.json $OUT/fetch $OUT/write $OUT/hit
+run_pass fetch FETCH_SIZE && run_pass write WRITE_SIZE && run_pass hit TCC_HIT_sum TCC_MISS_sum && \
+    run_pass ea TCC_EA0_RDREQ_sum || exit 1
+python3 scripts/pmc_traffic.py $OUT/pmc_traffic.json $OUT/fetch $OUT/write $OUT/hit $OUT/ea

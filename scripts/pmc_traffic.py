@@ -10,10 +10,14 @@ grouped the way bench.py prices them:
   pagerank_update : gather_short + gather_chunks + finalize_long (one group = one rank update)
   msbfs_sweep     : ms_seed + ms_pull + ms_push + ms_settle (one group = one 64-source sweep)
 
-Corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950
-FETCH_SIZE reports half the bytes of a wide coalesced stream, so `traffic` doubles it
-(an upper bound for the narrower gather reads, whose tally is uncalibrated); the raw
-figure is kept beside it.
+Corrections (MI355X_MICROARCH.md §HBM, calibrated for these access shapes by
+scripts/pmc_calib.hip, profiles/r02f_pmc_calibration.txt): FETCH_SIZE and WRITE_SIZE are in
+KiB; FETCH_SIZE = TCC_EA0_RDREQ x 64 B while every request moves a 128-byte line — for 16-B
+and 4-B-per-lane streams AND for random 8-byte gathers alike — so `traffic` doubles it.
+WRITE_SIZE is exact for 8-byte-per-lane stores.  Infinity-Cache hits are counted like HBM
+reads (a warmed 128 MiB table gave the same requests per gather as a 2 GiB one), so
+`traffic` is L2->fabric line traffic, an upper bound on HBM bytes; TCC_EA0_RDREQ is kept
+beside it as the request count that bounds the gather (~55 G requests/s measured).
 """
 import csv
 import glob
@@ -23,11 +27,12 @@ import sys
 from collections import defaultdict
 
 GROUPS = {
-    "pagerank_update": ("gather_short<tgo::(anonymous namespace)::PrOp", "gather_chunks<tgo::(anonymous namespace)::PrOp",
-                        "finalize_long<tgo::(anonymous namespace)::PrOp"),
+    # one rank update of the cache-blocked gather (spmv.hip): cold pass, fold, hot pass, long rows
+    "pagerank_update": ("cold_gather<", "cold_fold(", "gather_short_packed<", "gather_chunks<tgo::(anonymous namespace)::PackedOp",
+                        "finalize_long<tgo::(anonymous namespace)::PackedOp"),
     "msbfs_sweep": ("ms_seed(", "ms_pull(", "ms_push(", "ms_settle("),
 }
-UNIT_KERNEL = {"pagerank_update": "gather_short<tgo::(anonymous namespace)::PrOp", "msbfs_sweep": "ms_seed("}
+UNIT_KERNEL = {"pagerank_update": "gather_short_packed<", "msbfs_sweep": "ms_seed("}
 
 
 def load(d):
@@ -68,6 +73,7 @@ def main():
     passes = [load(d) for d in dirs]
     fetch = per_unit(passes, "FETCH_SIZE")
     write = per_unit(passes, "WRITE_SIZE")
+    rdreq = per_unit(passes, "TCC_EA0_RDREQ_sum")
     hit = per_unit(passes, "TCC_HIT_sum")
     miss = per_unit(passes, "TCC_MISS_sum")
     res = {}
@@ -76,7 +82,11 @@ def main():
             continue
         f_b, w_b = fetch[g] * 1024.0, write[g] * 1024.0
         ent = {"fetch_bytes_raw": f_b, "write_bytes": w_b, "traffic_bytes": 2.0 * f_b + w_b,
-               "correction": "FETCH_SIZE x2 (gfx950 wide-read tally, MI355X_MICROARCH.md HBM), WRITE_SIZE x1; KiB->B"}
+               "correction": "FETCH_SIZE x2 (one 128-B line per TCC_EA0_RDREQ, tallied as 64 B; calibrated for streams "
+                             "and 8-B gathers, profiles/r02f_pmc_calibration.txt), WRITE_SIZE x1; KiB->B; Infinity-Cache "
+                             "hits included"}
+        if g in rdreq:
+            ent["ea_read_requests"] = rdreq[g]
         if g in hit and g in miss and hit[g] + miss[g] > 0:
             ent["l2_hit_rate"] = hit[g] / (hit[g] + miss[g])
         res[g] = ent

@@ -20,18 +20,18 @@ n = 1 << scale
 src, dst, _ = rmat_edges(scale, 16, seed=0x54495441)
 eng = None
 loaded_with = None
-KEYS = ("TGO_PR_BLOCKED", "TGO_PR_HOT", "TGO_PR_SEG", "TGO_PR_DIAG", "TGO_PR_PACK")
+KEYS = ("TGO_PR_BLOCKED", "TGO_PR_HOT", "TGO_PR_SEG", "TGO_PR_DIAG", "TGO_PR_PACK", "TGO_PR_CPACK")
 variants = [
     {},
     {"TGO_PR_BLOCKED": "0"},
-    {"TGO_PR_PACK": "0"},
+    {"TGO_PR_CPACK": "0"},
+    {"TGO_PR_PACK": "0", "TGO_PR_CPACK": "0"},
     {"TGO_PR_HOT": "262144", "TGO_PR_SEG": "262144"},
     {"TGO_PR_HOT": "262144", "TGO_PR_SEG": "524288"},
-    {"TGO_PR_HOT": "524288", "TGO_PR_SEG": "1048576"},
     {"TGO_PR_DIAG": "-2:-1"},                 # no gathers at all: index stream + finalize
     {},
 ]
-RELOAD = ("TGO_PR_BLOCKED", "TGO_PR_HOT", "TGO_PR_SEG", "TGO_PR_PACK")   # read at load time
+RELOAD = ("TGO_PR_BLOCKED", "TGO_PR_HOT", "TGO_PR_SEG", "TGO_PR_PACK", "TGO_PR_CPACK")   # read at load time
 if os.environ.get("PR_PROBE_DEFAULT_ONLY"):
     variants = [{}]
 base = None

@@ -174,7 +174,8 @@ int upload_graph(tgo_ctx* ctx, HostGraph& h, bool allow_segments = true) {
     if (allow_segments && h.scope != TGO_SCOPE_BOTH_E && env_i64("TGO_PR_BLOCKED", 1) != 0) {
         HostColdBlocks hc;
         if (build_cold_blocks(h.in.off, h.in.adj, h.n, env_i64("TGO_PR_HOT", kPrHotDefault),
-                              env_i64("TGO_PR_SEG", kPrSegDefault), kTile, kMaxRows, threads_of(ctx), hc)) {
+                              env_i64("TGO_PR_SEG", kPrSegDefault), kTile, kMaxRows, threads_of(ctx),
+                              env_i64("TGO_PR_CPACK", 1) != 0, hc)) {
             ColdBlocks& cb = g.cold_in;
             cb.hot = hc.hot;
             cb.seg = hc.seg;
@@ -197,6 +198,8 @@ int upload_graph(tgo_ctx* ctx, HostGraph& h, bool allow_segments = true) {
             HIP_TRY(upload(ctx, cb.bbeg, hc.bbeg));
             HIP_TRY(upload(ctx, cb.bend, hc.bend));
             HIP_TRY(upload(ctx, cb.xblk, hc.xblk));
+            HIP_TRY(upload(ctx, cb.bsrc, hc.bsrc));
+            cb.cpacked = hc.cpacked;
             HIP_TRY(dev_alloc(ctx, cb.partial, cb.npieces));
             HIP_TRY(dev_alloc(ctx, cb.csum, std::max<int64_t>(cb.n_rows, 1)));
             HIP_TRY(hipMemset(cb.csum, 0, std::max<int64_t>(cb.n_rows, 1) * sizeof(double)));

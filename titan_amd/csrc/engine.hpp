@@ -131,6 +131,8 @@ struct ColdBlocks {
     int64_t* bbeg = nullptr;    // per cold block: first piece
     int64_t* bend = nullptr;    // per cold block: end piece
     int32_t* xblk = nullptr;    // cold blocks in XCD-major launch order
+    int32_t* bsrc = nullptr;    // per cold block: first source of its segment (packed tiles)
+    bool cpacked = false;       // cold tiles source-sorted and packed relative to bsrc
     double* partial = nullptr;  // npieces, in piece order (streaming writes)
     double* csum = nullptr;     // n_rows: per-row cold sums (cold_fold; 0 for rows without pieces)
     int32_t* crow = nullptr;    // rows that own cold pieces (ascending)
@@ -143,7 +145,8 @@ struct ColdBlocks {
 struct HostColdBlocks {
     int64_t hot = 0, seg = 0;
     std::vector<int64_t> hoff, poff, bbeg, bend;
-    std::vector<int32_t> hadj, cadj, cpid, xblk, crow;
+    std::vector<int32_t> hadj, cadj, cpid, xblk, crow, bsrc;
+    bool cpacked = false;
     std::vector<uint32_t> cptr;
     XcdBase xbase{};
     int64_t max_xcd_blocks = 0;
@@ -151,7 +154,8 @@ struct HostColdBlocks {
 // Builds the split of a CSR (entries = source ids) at hot / seg (see ColdBlocks); returns
 // false when nothing is cold (n <= hot) or the piece count overflows 32-bit indices.
 bool build_cold_blocks(const std::vector<int64_t>& off, const std::vector<int32_t>& adj, int64_t n_src,
-                       int64_t hot, int64_t seg, int64_t tile, int64_t max_pieces, int threads, HostColdBlocks& hc);
+                       int64_t hot, int64_t seg, int64_t tile, int64_t max_pieces, int threads, bool pack,
+                       HostColdBlocks& hc);
 
 struct DevGraph {
     int64_t n = 0;

@@ -726,7 +726,8 @@ bool pack_tiles(const std::vector<int64_t>& off, std::vector<int32_t>& adj, cons
 // pass 2 writes the hot CSR and scatters the cold runs into their segment, rows in order
 // (a thread's rows follow the previous thread's rows in every segment).
 bool build_cold_blocks(const std::vector<int64_t>& off, const std::vector<int32_t>& adj, int64_t n_src,
-                       int64_t hot, int64_t seg, int64_t tile, int64_t max_pieces, int threads, HostColdBlocks& hc) {
+                       int64_t hot, int64_t seg, int64_t tile, int64_t max_pieces, int threads, bool pack,
+                       HostColdBlocks& hc) {
     const int64_t n = static_cast<int64_t>(off.size()) - 1;
     if (hot <= 0 || seg <= 0 || n_src <= hot || n <= 0) return false;
     const int64_t nseg = (n_src - hot + seg - 1) / seg;
@@ -848,6 +849,7 @@ bool build_cold_blocks(const std::vector<int64_t>& off, const std::vector<int32_
     // neighbouring XCDs, each caching its slice) and the XCDs finish together.
     hc.bbeg.clear();
     hc.bend.clear();
+    hc.bsrc.clear();
     for (int64_t sg = 0; sg < nseg; ++sg) {
         int64_t p = seg_pbase[sg];
         while (p < seg_pbase[sg + 1]) {
@@ -855,10 +857,30 @@ bool build_cold_blocks(const std::vector<int64_t>& off, const std::vector<int32_
             while (e < seg_pbase[sg + 1] && e - p < max_pieces && hc.poff[e + 1] - hc.poff[p] <= tile) ++e;
             hc.bbeg.push_back(p);
             hc.bend.push_back(e);
+            hc.bsrc.push_back(static_cast<int32_t>(hot + sg * seg));
             p = e;
         }
     }
     const int64_t nb = static_cast<int64_t>(hc.bbeg.size());
+    // Source-sorted, packed cold tiles: (source - segment base) << kPackShift | slot.
+    if (pack && seg <= (int64_t(1) << (31 - kPackShift)) && tile <= (int64_t(1) << kPackShift)) {
+        std::vector<std::thread> th;
+        for (int t = 0; t < threads; ++t)
+            th.emplace_back([&, t] {
+                std::vector<uint32_t> tmp;
+                for (int64_t b = t; b < nb; b += threads) {
+                    const int64_t s0 = hc.poff[hc.bbeg[b]], s1 = hc.poff[hc.bend[b]];
+                    tmp.resize(static_cast<size_t>(s1 - s0));
+                    for (int64_t k = s0; k < s1; ++k)
+                        tmp[k - s0] = (static_cast<uint32_t>(hc.cadj[k] - hc.bsrc[b]) << kPackShift) |
+                                      static_cast<uint32_t>(k - s0);
+                    std::sort(tmp.begin(), tmp.end());
+                    for (int64_t k = s0; k < s1; ++k) hc.cadj[k] = static_cast<int32_t>(tmp[k - s0]);
+                }
+            });
+        for (auto& x : th) x.join();
+        hc.cpacked = true;
+    }
     hc.xblk.resize(nb);
     for (int64_t b = 0; b < nb; ++b) hc.xblk[b] = static_cast<int32_t>(b);
     const int64_t total = hc.poff[npieces];

@@ -228,9 +228,11 @@ __global__ void finalize_long(const int64_t* __restrict__ long_row, const int64_
 // dispatcher deals workgroups round-robin over the 8 XCDs) and takes that XCD's (b / 8)-th
 // cold block, so each XCD walks its own segments in order and its L2 holds the 2 MB slice of
 // messages the block gathers from.  Workgroups past the XCD's block count exit at once.
+template <bool kPacked>
 __global__ void __launch_bounds__(kBlock) cold_gather(const int64_t* __restrict__ poff,
         const int32_t* __restrict__ cadj, const int64_t* __restrict__ bbeg, const int64_t* __restrict__ bend,
-        const int32_t* __restrict__ xblk, XcdBase xb, PrOp op, double* __restrict__ partial) {
+        const int32_t* __restrict__ xblk, const int32_t* __restrict__ bsrc, XcdBase xb, const double* __restrict__ msg,
+        double* __restrict__ partial) {
     __shared__ double s_val[kTile];
     const int x = static_cast<int>(blockIdx.x & 7);
     const int64_t j = xb.b[x] + (blockIdx.x >> 3);
@@ -238,7 +240,25 @@ __global__ void __launch_bounds__(kBlock) cold_gather(const int64_t* __restrict_
     const int64_t blk = xblk[j];
     const int64_t p0 = bbeg[blk], p1 = bend[blk];
     const int64_t s0 = poff[p0];
-    stage_tile(cadj, s0, poff[p1] - s0, op, s_val);    // <= kTile by construction
+    const int64_t nnz = poff[p1] - s0;                 // <= kTile by construction
+    if (kPacked) {                                     // source-sorted tile: values go back to their slot
+        const double* seg_msg = msg + bsrc[blk];
+        int32_t v[kPer];
+#pragma unroll
+        for (int q = 0; q < kPer; ++q) {
+            const int64_t k = threadIdx.x + static_cast<int64_t>(q) * kBlock;
+            v[q] = k < nnz ? stream_idx(cadj + s0 + k) : -1;
+        }
+        double val[kPer];
+#pragma unroll
+        for (int q = 0; q < kPer; ++q) val[q] = v[q] >= 0 ? seg_msg[v[q] >> kPackShift] : 0.0;
+#pragma unroll
+        for (int q = 0; q < kPer; ++q)
+            if (v[q] >= 0) s_val[v[q] & ((1 << kPackShift) - 1)] = val[q];
+        __syncthreads();
+    } else {
+        stage_tile(cadj, s0, nnz, PrOp{msg}, s_val);
+    }
     reduce_runs<PrOp>(poff, p0, p1, s0, s_val, [&](int64_t p, double sum) { partial[p] = sum; });
 }
 
@@ -310,9 +330,15 @@ hipError_t k_pr_iter(const DevCsr& in, const RowBlocks& rb, const double* contri
 }
 hipError_t k_pr_iter_cold(const ColdBlocks& cb, const double* contrib, const double* edge_count, double* pr,
                           double* contrib_next, double* partial_long, double alpha, double base, hipStream_t s) {
-    if (cb.max_xcd_blocks > 0)
-        cold_gather<<<static_cast<unsigned>(cb.max_xcd_blocks * 8), kBlock, 0, s>>>(
-            cb.poff, cb.cadj, cb.bbeg, cb.bend, cb.xblk, cb.xbase, PrOp{contrib}, cb.partial);
+    if (cb.max_xcd_blocks > 0) {
+        const unsigned g = static_cast<unsigned>(cb.max_xcd_blocks * 8);
+        if (cb.cpacked)
+            cold_gather<true><<<g, kBlock, 0, s>>>(cb.poff, cb.cadj, cb.bbeg, cb.bend, cb.xblk, cb.bsrc, cb.xbase, contrib,
+                                                   cb.partial);
+        else
+            cold_gather<false><<<g, kBlock, 0, s>>>(cb.poff, cb.cadj, cb.bbeg, cb.bend, cb.xblk, cb.bsrc, cb.xbase, contrib,
+                                                    cb.partial);
+    }
     {
         int64_t g = (cb.n_crows + kBlock - 1) / kBlock;
         g = std::max<int64_t>(1, std::min<int64_t>(g, 65536));
