@@ -256,6 +256,45 @@ int  tgo_pagerank(tgo_ctx* ctx, const tgo_pr_args* args, double* pr_out);
 /* OLAPTest.DegreeCounter(k) (OLAPTest.java:334-416): k-walk counts, Java int wrap. */
 int  tgo_walkcount(tgo_ctx* ctx, int32_t k, int32_t* out);
 
+/* ---- Generic vertex programs ----------------------------------------
+ * A vertex program the engine does not implement natively runs its execute() on the host
+ * over whole per-vertex vectors (titan_amd/computer.py GenericVertexProgram; the Java host
+ * would do the same) while the device combines its messages, superstep by superstep:
+ *   tgo_gather          MessageScope.Local(incident, edgeFct): for every vertex, the combiner
+ *                       over edgeFct(msg[u], e) for the entries of its reversed incident
+ *                       traversal whose sender u holds a message (VertexMemoryHandler.java:
+ *                       77-93, FulgoraUtil.java:57).  The scope must be the loaded scope, or
+ *                       any direction of a bothE load (whose lists are uncapped).
+ *   tgo_combine_global  MessageScope.Global: the messages sent to each target combined in the
+ *                       order they were sent (VertexState.addMessage, VertexState.java:63-78).
+ * Vectors are host arrays in the API's row order (n = tgo_num_vertices); has[] = 1 where a
+ * message is present (NULL in: every vertex holds one).  MIN/MAX and int64 SUM are exact;
+ * fp64 SUM folds in a fixed order (list order / message order): bitwise reproducible.
+ * int64 arithmetic wraps like Java long.  A weight edge function over an edge without the
+ * weight property fails with TGO_E_PROGRAM (edge.value() throws in the reference). */
+typedef enum { TGO_COMBINE_SUM = 0, TGO_COMBINE_MIN = 1, TGO_COMBINE_MAX = 2 } tgo_combiner;
+typedef enum { TGO_VAL_INT64 = 0, TGO_VAL_FP64 = 1 } tgo_value_type;
+typedef enum {
+    TGO_EDGE_IDENTITY = 0,    /* (m, e) -> m                    */
+    TGO_EDGE_ADD_ONE = 1,     /* (m, e) -> m + 1                */
+    TGO_EDGE_ADD_WEIGHT = 2,  /* (m, e) -> m + e.value(weight)  */
+    TGO_EDGE_MUL_WEIGHT = 3   /* (m, e) -> m * e.value(weight)  */
+} tgo_edge_fn;
+typedef struct {
+    int32_t scope;            /* tgo_scope of the Local message scope                     */
+    int32_t value_type;       /* tgo_value_type                                          */
+    int32_t combiner;         /* tgo_combiner (the program's MessageCombiner)            */
+    int32_t edge_fn;          /* tgo_edge_fn                                             */
+} tgo_gather_args;
+int  tgo_gather(tgo_ctx* ctx, const tgo_gather_args* args, const void* msg, const uint8_t* has,
+                void* out, uint8_t* out_has);
+/* targets: dense row ids (tgo_dense_ids); values: nmsgs int64 or fp64. */
+int  tgo_combine_global(tgo_ctx* ctx, int32_t value_type, int32_t combiner, int64_t nmsgs,
+                        const int64_t* targets, const void* values, void* out, uint8_t* out_has);
+/* Titan vertex ids -> dense row ids (canonical id of a vertex cut, VertexMemoryHandler.java:
+ * 111-115); -1 for an id that is not an executed vertex (its messages are never read). */
+int  tgo_dense_ids(tgo_ctx* ctx, const int64_t* titan_ids, int64_t count, int64_t* dense_out);
+
 int  tgo_stats_get(tgo_ctx* ctx, tgo_stats* out);
 /* Block until all work queued on the ctx stream has finished. */
 int  tgo_sync(tgo_ctx* ctx);

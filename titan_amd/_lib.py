@@ -30,6 +30,9 @@ SSSP_HOP_BOUNDED, SSSP_DELTA = 0, 1
 FLAG_STATS = 1
 DIST_ABSENT = -(1 << 63)
 ABI_VERSION = 2
+COMBINE_SUM, COMBINE_MIN, COMBINE_MAX = 0, 1, 2
+VAL_INT64, VAL_FP64 = 0, 1
+EDGE_IDENTITY, EDGE_ADD_ONE, EDGE_ADD_WEIGHT, EDGE_MUL_WEIGHT = 0, 1, 2, 3
 
 _i64p = C.POINTER(C.c_int64)
 _i32p = C.POINTER(C.c_int32)
@@ -86,6 +89,10 @@ class PrArgs(C.Structure):
                 ("reserved", C.c_int32)]
 
 
+class GatherArgs(C.Structure):
+    _fields_ = [("scope", C.c_int32), ("value_type", C.c_int32), ("combiner", C.c_int32), ("edge_fn", C.c_int32)]
+
+
 class Stats(C.Structure):
     _fields_ = [("num_vertices", C.c_int64), ("out_entries", C.c_int64), ("in_entries", C.c_int64), ("ghost_vertices", C.c_int64),
                 ("truncated_results", C.c_int64), ("skipped_rows", C.c_int64), ("iterations", C.c_int32),
@@ -101,6 +108,7 @@ EXPORTS = [
     "tgo_finish_load", "tgo_load_edges", "tgo_num_vertices", "tgo_vertex_ids", "tgo_bfs",
     "tgo_sssp", "tgo_copy_distances", "tgo_pagerank", "tgo_walkcount", "tgo_stats_get", "tgo_sync",
     "tgo_bfs_multi", "tgo_copy_multi_distances", "tgo_multi_stats",
+    "tgo_gather", "tgo_combine_global", "tgo_dense_ids",
     "tgo_rmat_edges", "tgo_pick_roots", "tgo_synth_rows",
     # titan_gpu_olap_part.h (1-D vertex-partitioned multi-GPU)
     "tgo_load_partition", "tgo_part_layout", "tgo_load_partition_layout", "tgo_part_bfs_begin", "tgo_part_bfs_td", "tgo_part_bfs_claim", "tgo_part_bfs_bu",
@@ -151,6 +159,9 @@ def load() -> C.CDLL:
         "tgo_bfs_multi": (C.c_int, [vp, _i64p, C.c_int32, P(BfsArgs), _i64p]),
         "tgo_copy_multi_distances": (C.c_int, [vp, C.c_int32, _i64p]),
         "tgo_multi_stats": (C.c_int, [vp, _i64p, _i64p]),
+        "tgo_gather": (C.c_int, [vp, P(GatherArgs), vp, P(C.c_uint8), vp, P(C.c_uint8)]),
+        "tgo_combine_global": (C.c_int, [vp, C.c_int32, C.c_int32, C.c_int64, _i64p, vp, vp, P(C.c_uint8)]),
+        "tgo_dense_ids": (C.c_int, [vp, _i64p, C.c_int64, _i64p]),
         "tgo_rmat_edges": (C.c_int, [C.c_int32, C.c_int32, C.c_uint64, C.c_int64, C.c_int64,
                                      _i32p, _i32p, _i32p, C.c_int32]),
         "tgo_pick_roots": (C.c_int, [C.c_int64, C.c_int64, _i32p, _i32p, C.c_uint64, C.c_int32, _i64p]),

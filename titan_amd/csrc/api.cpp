@@ -14,6 +14,7 @@
 #include <thread>
 #include <unordered_map>
 #include <hip/hip_runtime_api.h>
+#include "codec.hpp"
 #include "engine.hpp"
 #include "../../include/titan_gpu_olap_part.h"
 
@@ -85,6 +86,9 @@ hipError_t upload(tgo_ctx* ctx, T*& p, const std::vector<T>& h) {
 }
 
 void free_graph(tgo_ctx* ctx) {
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->sc.cub_tmp) (void)hipFree(ctx->sc.cub_tmp);       // grown by the scans, not in allocs
+    if (ctx->sc.sort_tmp) (void)hipFree(ctx->sc.sort_tmp);
     for (void* p : ctx->allocs) (void)hipFree(p);
     ctx->allocs.clear();
     ctx->dev_bytes = 0;
@@ -1461,6 +1465,107 @@ int tgo_part_sssp_end(tgo_ctx* ctx, int64_t* dist_local, int64_t* reached) {
     ctx->st.last_kernel_ms = ms;
     ctx->st.relaxed_entries = ctx->part_relaxed;
     ctx->st.levels = ctx->part_phases;
+    return TGO_OK;
+}
+
+// ------------------------------------------------------------------ generic vertex programs
+static int generic_alloc(tgo_ctx* ctx) {
+    Scratch& s = ctx->sc;
+    if (s.gv[0]) return TGO_OK;
+    for (int i = 0; i < 3; ++i) {
+        HIP_TRY(dev_alloc(ctx, s.gv[i], ctx->g.n + 1));
+        HIP_TRY(dev_alloc(ctx, s.gh[i], ctx->g.n + 1));
+    }
+    ctx->st.device_bytes = ctx->dev_bytes;
+    return TGO_OK;
+}
+
+int tgo_gather(tgo_ctx* ctx, const tgo_gather_args* a, const void* msg, const uint8_t* has, void* out,
+               uint8_t* out_has) {
+    if (!ctx) return TGO_E_INVALID;
+    if (!a || !msg || !out || !out_has) return fail(ctx, TGO_E_INVALID, "null argument");
+    if (!ctx->loaded) return fail(ctx, TGO_E_STATE, "no graph loaded");
+    if (ctx->g.partitioned) return fail(ctx, TGO_E_UNSUPPORTED, "generic gathers run on a one-GPU load");
+    if (a->scope < 0 || a->scope > 2) return fail(ctx, TGO_E_INVALID, "invalid scope");
+    if (a->scope != ctx->g.scope && ctx->g.scope != TGO_SCOPE_BOTH_E)
+        return fail(ctx, TGO_E_INVALID, "message scope differs from the scope the graph was loaded (preloaded) for");
+    if (a->value_type < 0 || a->value_type > 1 || a->combiner < 0 || a->combiner > 2 || a->edge_fn < 0 || a->edge_fn > 3)
+        return fail(ctx, TGO_E_INVALID, "invalid value type, combiner or edge function");
+    if ((a->edge_fn == TGO_EDGE_ADD_WEIGHT || a->edge_fn == TGO_EDGE_MUL_WEIGHT) && !ctx->g.has_weight)
+        return fail(ctx, TGO_E_INVALID, "weight edge function on a graph loaded without a weight property");
+    (void)hipSetDevice(ctx->opts.device);
+    int rc = generic_alloc(ctx);
+    if (rc) return rc;
+    Scratch& s = ctx->sc;
+    hipStream_t st = ctx->stream;
+    const int64_t n = ctx->g.n;
+    HIP_TRY(hipEventRecord(ctx->ev0, st));
+    HIP_TRY(hipMemcpyAsync(s.gv[0], msg, n * 8, hipMemcpyHostToDevice, st));
+    if (has) HIP_TRY(hipMemcpyAsync(s.gh[0], has, n, hipMemcpyHostToDevice, st));
+    else HIP_TRY(hipMemsetAsync(s.gh[0], 1, n, st));
+    HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
+    HIP_TRY(k_to_internal(s.gv[0], s.gh[0], ctx->g.perm, s.gv[1], s.gh[1], n, st));
+    HIP_TRY(k_local_gather(pull_view(ctx->g, a->scope), n, a->value_type, s.gv[1], s.gh[1], a->combiner, a->edge_fn,
+                           s.gv[2], s.gh[2], &s.cnt->err, st));
+    HIP_TRY(k_to_rows(s.gv[2], s.gh[2], ctx->g.perm, s.gv[0], s.gh[0], n, st));
+    HIP_TRY(hipEventRecord(ctx->ev1, st));
+    HIP_TRY(hipMemcpyAsync(out, s.gv[0], n * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(out_has, s.gh[0], n, hipMemcpyDeviceToHost, st));
+    if ((rc = read_counters(ctx))) return rc;
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+    ctx->st.last_kernel_ms = ms;
+    if (s.hcnt->err) return fail(ctx, TGO_E_PROGRAM, "vertex program failed: a traversed edge has no value for the weight property");
+    return TGO_OK;
+}
+
+int tgo_combine_global(tgo_ctx* ctx, int32_t value_type, int32_t combiner, int64_t nmsgs, const int64_t* targets,
+                       const void* values, void* out, uint8_t* out_has) {
+    if (!ctx) return TGO_E_INVALID;
+    if (nmsgs < 0 || (nmsgs > 0 && (!targets || !values)) || !out || !out_has) return fail(ctx, TGO_E_INVALID, "null argument");
+    if (!ctx->loaded) return fail(ctx, TGO_E_STATE, "no graph loaded");
+    if (value_type < 0 || value_type > 1 || combiner < 0 || combiner > 2)
+        return fail(ctx, TGO_E_INVALID, "invalid value type or combiner");
+    if (nmsgs >= (int64_t(1) << 31)) return fail(ctx, TGO_E_UNSUPPORTED, "more than 2^31 global messages in one superstep");
+    const int64_t n = ctx->g.n;
+    for (int64_t i = 0; i < nmsgs; ++i)
+        if (targets[i] < 0 || targets[i] >= n) return fail(ctx, TGO_E_INVALID, "global message target out of range");
+    (void)hipSetDevice(ctx->opts.device);
+    int rc = generic_alloc(ctx);
+    if (rc) return rc;
+    Scratch& s = ctx->sc;
+    hipStream_t st = ctx->stream;
+    HIP_TRY(hipMemsetAsync(s.gv[0], 0, n * 8, st));
+    HIP_TRY(hipMemsetAsync(s.gh[0], 0, n, st));
+    if (nmsgs > 0) {
+        int64_t* buf = nullptr;          // targets, values, sort scratch (3 m): freed below
+        HIP_TRY(hipMalloc(&buf, static_cast<size_t>(nmsgs) * 5 * sizeof(int64_t)));
+        hipError_t e = hipMemcpyAsync(buf, targets, nmsgs * 8, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess) e = hipMemcpyAsync(buf + nmsgs, values, nmsgs * 8, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess)
+            e = k_global_combine(s.sort_tmp, s.sort_bytes, buf, nmsgs, n, value_type, buf + nmsgs, combiner, buf + 2 * nmsgs,
+                                 s.gv[0], s.gh[0], st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        (void)hipFree(buf);
+        HIP_TRY(e);
+    }
+    HIP_TRY(hipMemcpyAsync(out, s.gv[0], n * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(out_has, s.gh[0], n, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return TGO_OK;
+}
+
+int tgo_dense_ids(tgo_ctx* ctx, const int64_t* titan_ids, int64_t count, int64_t* dense_out) {
+    if (!ctx) return TGO_E_INVALID;
+    if (count < 0 || (count > 0 && (!titan_ids || !dense_out))) return fail(ctx, TGO_E_INVALID, "null argument");
+    if (!ctx->loaded) return fail(ctx, TGO_E_STATE, "no graph loaded");
+    const int pb = ctx->opts.partition_bits;
+    for (int64_t i = 0; i < count; ++i) {
+        int64_t id = titan_ids[i];
+        if (is_partitioned_vertex(id, pb)) id = canonical_vertex_id(id, pb);    // getCanonicalId
+        auto it = ctx->id_index.find(id);
+        dense_out[i] = it == ctx->id_index.end() ? -1 : it->second;
+    }
     return TGO_OK;
 }
 

@@ -224,6 +224,11 @@ struct Scratch {
     int32_t ms_nsrc = 0;
     int64_t* pk_cnt = nullptr;      // partitioned sparse exchange: per-chunk pair counts
     int64_t* pk_off = nullptr;      // and their exclusive scan (n_global / kPackChunk + 1 each)
+    // generic vertex programs (allocated on first use): row-order staging + internal-order vectors
+    int64_t* gv[3] = {nullptr, nullptr, nullptr};
+    uint8_t* gh[3] = {nullptr, nullptr, nullptr};
+    void* sort_tmp = nullptr;
+    size_t sort_bytes = 0;
     // partitioned delta-stepping (allocated on first use)
     int64_t* ds_rbest = nullptr;    // n_global: best distance sent to each remote vertex
     uint64_t* ds_rmark = nullptr;   // n_global bits: remote vertices improved this phase
@@ -317,6 +322,17 @@ hipError_t k_pr_iter_cold(const ColdBlocks& cb, const double* contrib, const dou
                           double* contrib_next, double* partial_long, double alpha, double base, hipStream_t s);
 hipError_t k_walk_iter(const DevCsr& out, const RowBlocks& rb, const int32_t* prev, int32_t* next,
                        int32_t* partial, int64_t n, hipStream_t s);
+
+// Generic vertex programs (generic.hip)
+hipError_t k_local_gather(const View& pull, int64_t n, int value_type, const void* msg_int, const uint8_t* has_int,
+                          int comb, int fn, void* out_int, uint8_t* out_has_int, unsigned long long* err, hipStream_t s);
+hipError_t k_to_internal(const void* row8, const uint8_t* row1, const int32_t* perm, void* int8, uint8_t* int1,
+                         int64_t n, hipStream_t s);
+hipError_t k_to_rows(const void* int8, const uint8_t* int1, const int32_t* perm, void* row8, uint8_t* row1, int64_t n,
+                     hipStream_t s);
+hipError_t k_global_combine(void*& tmp, size_t& tmp_bytes, const int64_t* targets, int64_t m, int64_t n,
+                            int value_type, const void* values, int comb, int64_t* scratch3m, void* out,
+                            uint8_t* out_has, hipStream_t s);
 
 hipError_t scan_exclusive_i64(void*& tmp, size_t& tmp_bytes, const int64_t* in, int64_t* out,
                               int64_t n, hipStream_t s);

@@ -195,6 +195,41 @@ class Engine:
         _check(self.lib, self.ctx, self.lib.tgo_walkcount(self.ctx, int(k), L.ptr(out, C.c_int32)))
         return out
 
+    # ------------------------------------------------------------------ generic vertex programs
+    @staticmethod
+    def _vals(values, value_type):
+        return np.ascontiguousarray(values, dtype=np.int64 if value_type == L.VAL_INT64 else np.float64)
+
+    def gather(self, scope, value_type, combiner, edge_fn, msg, has=None):
+        """MessageScope.Local receive with a combiner (tgo_gather): returns (combined values,
+        has-message mask) per vertex in row order."""
+        m = self._vals(msg, value_type)
+        h = None if has is None else np.ascontiguousarray(has, dtype=np.uint8)
+        out = np.empty(self.n, dtype=m.dtype)
+        out_has = np.empty(self.n, dtype=np.uint8)
+        a = L.GatherArgs(scope, value_type, combiner, edge_fn)
+        _check(self.lib, self.ctx, self.lib.tgo_gather(self.ctx, C.byref(a), m.ctypes.data_as(C.c_void_p),
+                                                       L.ptr(h, C.c_uint8), out.ctypes.data_as(C.c_void_p),
+                                                       L.ptr(out_has, C.c_uint8)))
+        return out, out_has.astype(bool)
+
+    def combine_global(self, value_type, combiner, targets, values):
+        """MessageScope.Global: messages to dense row ids combined per target in send order."""
+        t = np.ascontiguousarray(targets, dtype=np.int64)
+        v = self._vals(values, value_type)
+        out = np.empty(self.n, dtype=v.dtype)
+        out_has = np.empty(self.n, dtype=np.uint8)
+        _check(self.lib, self.ctx, self.lib.tgo_combine_global(self.ctx, value_type, combiner, len(t), L.ptr(t, C.c_int64),
+                                                               v.ctypes.data_as(C.c_void_p),
+                                                               out.ctypes.data_as(C.c_void_p), L.ptr(out_has, C.c_uint8)))
+        return out, out_has.astype(bool)
+
+    def dense_ids(self, titan_ids):
+        ids = np.ascontiguousarray(titan_ids, dtype=np.int64)
+        out = np.empty(len(ids), dtype=np.int64)
+        _check(self.lib, self.ctx, self.lib.tgo_dense_ids(self.ctx, L.ptr(ids, C.c_int64), len(ids), L.ptr(out, C.c_int64)))
+        return out
+
     def stats(self):
         s = L.Stats()
         _check(self.lib, self.ctx, self.lib.tgo_stats_get(self.ctx, C.byref(s)))
