@@ -118,6 +118,8 @@ def load() -> C.CDLL:
         "fr_shortest_distance": (C.c_int, [vp, C.c_int64, C.c_int, C.c_int, C.c_int, C.c_int, _i64p, P(C.c_int)]),
         "fr_pagerank": (C.c_int, [vp, C.c_double, C.c_int64, C.c_int, C.c_int, C.POINTER(C.c_double), P(C.c_int)]),
         "fr_degree_counter": (C.c_int, [vp, C.c_int, C.c_int, _i32p, P(C.c_int)]),
+        "fr_gather": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, _u8p, vp, _u8p]),
+        "fr_combine_global": (C.c_int, [C.c_int64, C.c_int, C.c_int, C.c_int64, _i64p, vp, vp, _u8p]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -194,6 +196,18 @@ def encode_vertex_exists(relation_id):
     out = C.string_at(b.p, b.len)
     lib.fr_buf_free(C.byref(b))
     return out, vp.value
+
+
+def combine_global(n, value_type, combiner, targets, values):
+    """Global-scope messages folded per target in send order (fr_combine_global)."""
+    dt = np.int64 if value_type == 0 else np.float64
+    t = np.ascontiguousarray(targets, np.int64)
+    v = np.ascontiguousarray(values, dt)
+    out = np.zeros(n, dt)
+    oh = np.zeros(n, np.uint8)
+    load().fr_combine_global(n, value_type, combiner, len(t), _p(t, C.c_int64), v.ctypes.data_as(C.c_void_p),
+                             out.ctypes.data_as(C.c_void_p), _p(oh, C.c_uint8))
+    return out, oh.astype(bool)
 
 
 # ----------------------------------------------------------------------------- graph
@@ -296,6 +310,19 @@ class OracleGraph:
         if rc:
             raise RuntimeError(f"fr_pagerank rc={rc}")
         return out, it.value
+
+    def gather(self, scope, value_type, combiner, edge_fn, msg, has):
+        """Local-scope receive folded with the combiner (fr_gather); vectors in vertex order."""
+        dt = np.int64 if value_type == 0 else np.float64
+        m = np.ascontiguousarray(msg, dt)
+        h = np.ascontiguousarray(has, np.uint8)
+        out = np.zeros(self.n, dt)
+        oh = np.zeros(self.n, np.uint8)
+        rc = load().fr_gather(self.h, scope, value_type, combiner, edge_fn, m.ctypes.data_as(C.c_void_p), _p(h, C.c_uint8),
+                              out.ctypes.data_as(C.c_void_p), _p(oh, C.c_uint8))
+        if rc:
+            raise RuntimeError(f"fr_gather rc={rc}")
+        return out, oh.astype(bool)
 
     def degree_counter(self, length, threads=1):
         out = np.zeros(self.n, dtype=np.int32)

@@ -993,3 +993,75 @@ int fr_degree_counter(const fr_graph* g, int length, int threads, int32_t* out, 
     free(s.prev); free(s.cur); free(s.prev_ok); free(s.cur_ok);
     return FR_OK;
 }
+
+/* ---- Generic message passing (the primitives behind any VertexProgram) ----
+ * Local scope: VertexMemoryHandler.receiveMessages (VertexMemoryHandler.java:77-93) streams
+ * edgeFct(msg, e) over the reversed incident traversal (FulgoraUtil.java:57) for every
+ * neighbour holding a message (null filtered); the program reduces the stream with its
+ * combiner.  Here: the fold in entry order over all of the vertex's rows (a vertex cut's
+ * representative rows are combined with the same combiner, FulgoraVertexMemory.java:121-147).
+ * Global scope: VertexState.addMessage (VertexState.java:63-78) folds each message into the
+ * target's state as it arrives: combine(message, current), in send order. */
+static inline int64_t g_combine_i(int comb, int64_t acc, int64_t m) {
+    if (comb == 1) return m < acc ? m : acc;
+    if (comb == 2) return m > acc ? m : acc;
+    return (int64_t)((uint64_t)m + (uint64_t)acc);
+}
+static inline double g_combine_d(int comb, double acc, double m) {
+    if (comb == 1) return m < acc ? m : acc;
+    if (comb == 2) return m > acc ? m : acc;
+    return m + acc;
+}
+int fr_gather(const fr_graph* g, int scope, int value_type, int combiner, int edge_fn, const void* msg,
+              const uint8_t* has, void* out, uint8_t* out_has) {
+    const int64_t* mi = (const int64_t*)msg; const double* md = (const double*)msg;
+    int64_t* oi = (int64_t*)out; double* od = (double*)out;
+    int needs_w = edge_fn == 2 || edge_fn == 3;
+    for (int64_t v = 0; v < g->n; v++) {
+        int any = 0; int64_t ai = 0; double ad = 0.0;
+        for (int64_t i = 0; i < nrows_of(g, v); i++) {
+            int64_t kb, ke; row_range(g, v, i, &kb, &ke);
+            for (int64_t k = kb; k < ke; k++) {
+                if (!take(scope, g->edir[k])) continue;
+                int64_t o = entry_vertex(g, k);
+                if (o < 0 || !has[o]) continue;                                /* filter(m != null) */
+                int64_t w = 0;
+                if (needs_w) {
+                    if (!g->has_w[k]) return FR_E_PROGRAM;                     /* e.value(key) throws */
+                    w = g->w[k];
+                }
+                if (value_type == 0) {
+                    uint64_t m = (uint64_t)mi[o];
+                    if (edge_fn == 1) m += 1u;
+                    else if (edge_fn == 2) m += (uint64_t)w;
+                    else if (edge_fn == 3) m *= (uint64_t)w;
+                    ai = any ? g_combine_i(combiner, ai, (int64_t)m) : (int64_t)m;
+                } else {
+                    double m = md[o];
+                    if (edge_fn == 1) m += 1.0;
+                    else if (edge_fn == 2) m += (double)w;
+                    else if (edge_fn == 3) m *= (double)w;
+                    ad = any ? g_combine_d(combiner, ad, m) : m;
+                }
+                any = 1;
+            }
+        }
+        if (value_type == 0) oi[v] = ai; else od[v] = ad;
+        out_has[v] = (uint8_t)any;
+    }
+    return FR_OK;
+}
+int fr_combine_global(int64_t n, int value_type, int combiner, int64_t nmsgs, const int64_t* targets,
+                      const void* values, void* out, uint8_t* out_has) {
+    const int64_t* vi = (const int64_t*)values; const double* vd = (const double*)values;
+    int64_t* oi = (int64_t*)out; double* od = (double*)out;
+    for (int64_t v = 0; v < n; v++) { out_has[v] = 0; if (value_type == 0) oi[v] = 0; else od[v] = 0.0; }
+    for (int64_t i = 0; i < nmsgs; i++) {
+        int64_t t = targets[i];
+        if (t < 0 || t >= n) continue;                                          /* no executing vertex */
+        if (value_type == 0) oi[t] = out_has[t] ? g_combine_i(combiner, oi[t], vi[i]) : vi[i];
+        else od[t] = out_has[t] ? g_combine_d(combiner, od[t], vd[i]) : vd[i];
+        out_has[t] = 1;
+    }
+    return FR_OK;
+}

@@ -1,0 +1,195 @@
+"""GPU: generic vertex programs.  The device's message combining
+(tgo_gather, tgo_combine_global) against the oracle's restatement (fr_gather,
+fr_combine_global), and whole vectorised programs run through the computer mirror against
+the same programs driven through the oracle double.
+
+Bars: int64 results and MIN/MAX bit-exact; fp64 SUM of a Local scope within 1e-12 relative
+(the device folds each in-list in its own list order); Global fp64 SUM bit-exact (both fold
+in send order); programs: int64 exact, PageRank within 1e-6 L1 of the native oracle.
+"""
+import numpy as np
+import pytest
+
+import fulgora as fr
+from conftest import load_fixture
+from generic_programs import ConnectedComponents, GenericPageRank, GlobalDegreeSum, OracleEngine
+from titan_amd import (ComputeKeyMapReduce, Engine, ExecutionException, GpuGraph, Schema, TitanException,
+                       TitanGraphComputer, rmat_edges)
+from titan_amd import _lib as L
+
+pytestmark = pytest.mark.gpu
+
+OUT, IN, BOTH = L.SCOPE_OUT_E, L.SCOPE_IN_E, L.SCOPE_BOTH_E
+
+
+def reorder(ids_from, values, ids_to):
+    pos = {int(v): i for i, v in enumerate(ids_from)}
+    return np.array([values[pos[int(v)]] for v in ids_to])
+
+
+@pytest.fixture(scope="module")
+def weighted_rmat():
+    scale = 11
+    n = 1 << scale
+    src, dst, w = rmat_edges(scale, 8, seed=31, weights=True)
+    return n, src, dst, w
+
+
+@pytest.mark.parametrize("load_scope,scope", [(IN, IN), (OUT, OUT), (BOTH, BOTH), (BOTH, IN), (BOTH, OUT)])
+def test_local_gather_matches_oracle(weighted_rmat, load_scope, scope):
+    n, src, dst, w = weighted_rmat
+    eng = Engine().load_edges(n, src, dst, load_scope, weight=w, apply_cap=False)
+    o = fr.OracleGraph.from_edges(n, src, dst, w)
+    ids = eng.vertex_ids()
+    assert np.array_equal(ids, o.vertex_ids())
+    rng = np.random.default_rng(7)
+    for vt in (L.VAL_INT64, L.VAL_FP64):
+        msg = rng.integers(-(1 << 40), 1 << 40, n) if vt == L.VAL_INT64 else rng.standard_normal(n)
+        has = rng.random(n) < 0.6
+        for comb in (L.COMBINE_SUM, L.COMBINE_MIN, L.COMBINE_MAX):
+            for fn in (L.EDGE_IDENTITY, L.EDGE_ADD_ONE, L.EDGE_ADD_WEIGHT, L.EDGE_MUL_WEIGHT):
+                got, gh = eng.gather(scope, vt, comb, fn, msg, has)
+                exp, eh = o.gather(scope, vt, comb, fn, msg, has)
+                assert np.array_equal(gh, eh), (vt, comb, fn)
+                if vt == L.VAL_INT64 or comb != L.COMBINE_SUM:
+                    assert np.array_equal(got[gh], exp[eh]), (vt, comb, fn)
+                else:
+                    np.testing.assert_allclose(got[gh], exp[eh], rtol=1e-12, atol=1e-300)
+                    again, _ = eng.gather(scope, vt, comb, fn, msg, has)
+                    assert np.array_equal(got, again)            # fixed fold order
+
+
+def test_gather_all_present_and_scope_checks(weighted_rmat):
+    n, src, dst, w = weighted_rmat
+    eng = Engine().load_edges(n, src, dst, IN, weight=w)
+    o = fr.OracleGraph.from_edges(n, src, dst, w, hard_limit=100000)
+    msg = np.arange(n, dtype=np.int64)
+    got, gh = eng.gather(IN, L.VAL_INT64, L.COMBINE_MAX, L.EDGE_IDENTITY, msg)       # has = NULL: all present
+    exp, eh = o.gather(IN, 0, 2, 0, msg, np.ones(n, bool))
+    assert np.array_equal(gh, eh) and np.array_equal(got[gh], exp[eh])
+    with pytest.raises(TitanException) as e:
+        eng.gather(OUT, L.VAL_INT64, L.COMBINE_SUM, L.EDGE_IDENTITY, msg)            # not the preloaded slice
+    assert e.value.code == L.TGO_E_INVALID
+    plain = Engine().load_edges(n, src, dst, IN)
+    with pytest.raises(TitanException):
+        plain.gather(IN, L.VAL_INT64, L.COMBINE_SUM, L.EDGE_ADD_WEIGHT, msg)         # no weight property loaded
+
+
+def test_weight_function_over_an_edge_without_the_property_fails():
+    """GotG: `time` exists only on battled edges; reading it elsewhere throws in the
+    reference (edge.value()), here TGO_E_PROGRAM."""
+    rows, vids, sd, npz = load_fixture("gotg")
+    eng = Engine().load_rows(rows, Schema.from_dict(sd), BOTH, weight_key=sd["property_keys"][0][0])
+    n = eng.n
+    with pytest.raises(TitanException) as e:
+        eng.gather(BOTH, L.VAL_INT64, L.COMBINE_SUM, L.EDGE_ADD_WEIGHT, np.zeros(n, np.int64))
+    assert e.value.code == L.TGO_E_PROGRAM
+
+
+def test_global_combine_matches_oracle(weighted_rmat):
+    n, src, dst, w = weighted_rmat
+    eng = Engine().load_edges(n, src, dst, BOTH)
+    rng = np.random.default_rng(11)
+    m = 200000
+    targets = rng.integers(0, n, m)
+    targets[::7] = rng.integers(0, 16, len(targets[::7]))           # a few hot targets
+    for vt in (L.VAL_INT64, L.VAL_FP64):
+        vals = rng.integers(-(1 << 50), 1 << 50, m) if vt == L.VAL_INT64 else rng.standard_normal(m)
+        for comb in (L.COMBINE_SUM, L.COMBINE_MIN, L.COMBINE_MAX):
+            got, gh = eng.combine_global(vt, comb, targets, vals)
+            exp, eh = fr.combine_global(n, vt, comb, targets, vals)
+            assert np.array_equal(gh, eh)
+            assert np.array_equal(got[gh], exp[eh]), (vt, comb)       # same (send) order: bit-exact
+    got, gh = eng.combine_global(L.VAL_INT64, L.COMBINE_SUM, np.zeros(0, np.int64), np.zeros(0, np.int64))
+    assert not gh.any()
+    with pytest.raises(TitanException):
+        eng.combine_global(L.VAL_INT64, L.COMBINE_SUM, np.array([n]), np.array([1]))
+    ids = eng.vertex_ids()
+    assert np.array_equal(eng.dense_ids(ids[[3, 0, 9]]), [3, 0, 9])
+    assert eng.dense_ids(np.array([-5]))[0] == -1
+
+
+def run_both(graph_args, program_factory, oracle, weight_keys=None, mr_key=None):
+    graph = GpuGraph(**graph_args)
+    computer = graph.compute()
+    if weight_keys:
+        computer.weight_keys = weight_keys
+    computer.program(program_factory())
+    if mr_key:
+        computer.mapReduce(ComputeKeyMapReduce(*mr_key))
+    result = computer.submit().get()
+    from titan_amd import FulgoraMemory
+    from titan_amd.generic import run_generic
+    p = program_factory()
+    mem = FulgoraMemory(p.memory_compute_keys)
+    verts = run_generic(OracleEngine(oracle), p, mem)
+    mem.complete()
+    return result, verts, mem
+
+
+def test_connected_components_program(weighted_rmat):
+    n, src, dst, w = weighted_rmat
+    o = fr.OracleGraph.from_edges(n, src, dst)
+    result, verts, mem = run_both({"edges": (n, src, dst, None)}, ConnectedComponents, o, mr_key=("cc", "components"))
+    ids, (cc, present) = result.vertex_properties["cc"][0], result.vertex_properties["cc"][1]
+    assert present.all()
+    assert np.array_equal(reorder(ids, cc, verts.ids), verts.property("cc")[0])
+    assert result.memory().getIteration() == mem.getIteration()
+    assert result.memory().get("changes") == mem.get("changes")
+    kv = {x.getKey(): x.getValue() for x in result.memory().get("components")}
+    assert len(kv) == n and all(kv[int(i)] == int(c) for i, c in zip(ids, cc))
+
+
+def test_generic_pagerank_program(weighted_rmat):
+    n, src, dst, w = weighted_rmat
+    o = fr.OracleGraph.from_edges(n, src, dst)
+    result, verts, mem = run_both({"edges": (n, src, dst, None)}, lambda: GenericPageRank(0.85, n, 10), o)
+    ids, (pr, present) = result.vertex_properties["pr"]
+    opr, it = o.pagerank(0.85, n, 10)
+    assert present.all() and result.memory().getIteration() == it
+    assert np.abs(reorder(ids, pr, o.vertex_ids()) - opr).sum() <= 1e-6
+    np.testing.assert_allclose(reorder(ids, pr, verts.ids), verts.property("pr")[0], rtol=1e-12)
+
+
+def test_global_scope_program(weighted_rmat):
+    n, src, dst, w = weighted_rmat
+    o = fr.OracleGraph.from_edges(n, src, dst, w)
+    ids = o.vertex_ids()
+    hubs = ids[[1, 500, 1999]]
+    result, verts, mem = run_both({"edges": (n, src, dst, w)}, lambda: GlobalDegreeSum(hubs), o,
+                                  weight_keys={"w": 1})
+    gids, (inbox, has) = result.vertex_properties["inbox"]
+    assert np.array_equal(reorder(gids, has, verts.ids), verts.property("inbox")[1])
+    assert np.array_equal(reorder(gids, inbox, verts.ids)[verts.property("inbox")[1]],
+                          verts.property("inbox")[0][verts.property("inbox")[1]])
+    assert result.memory().get("total") == mem.get("total")
+    assert result.memory().get("best") == mem.get("best")
+
+
+def test_components_over_vertex_cuts():
+    """TitanPartitionGraphTest's vertex cuts (:380-435): canonical-id folding keeps the
+    generic program equal to the oracle's per-row combine."""
+    rows, vids, sd, npz = load_fixture("partition_groups")
+    o = fr.OracleGraph.from_rows(rows, fr.OracleSchema(sd["edge_types"], [tuple(x) for x in sd["property_keys"]]),
+                                 BOTH)
+    result, verts, mem = run_both({"rows": rows, "schema": sd}, ConnectedComponents, o)
+    ids, (cc, present) = result.vertex_properties["cc"]
+    assert np.array_equal(reorder(ids, cc, verts.ids), verts.property("cc")[0])
+
+
+def test_result_modes_other_than_none_are_rejected():
+    rows, vids, sd, npz = load_fixture("gotg")
+    computer = GpuGraph(rows, sd).compute()
+    with pytest.raises(TitanException):
+        computer.resultMode(TitanGraphComputer.ResultMode.PERSIST)
+    computer.resultMode(TitanGraphComputer.ResultMode.NONE)
+
+
+def test_generic_program_failure_surfaces_as_execution_exception():
+    rows, vids, sd, npz = load_fixture("gotg")
+    graph = GpuGraph(rows, sd)
+    computer = graph.compute()
+    computer.weight_keys = {"w": sd["property_keys"][0][0]}
+    computer.program(GlobalDegreeSum(np.array(vids[:2])))      # add_weight over edges without `time`
+    with pytest.raises(ExecutionException):
+        computer.submit().get()

@@ -10,11 +10,15 @@ from .computer import (  # noqa: F401
     PageRankMapReduce, PageRankVertexProgram, ShortestDistanceMapReduce,
     ShortestDistanceVertexProgram, TitanGraphComputer,
 )
+from .generic import (  # noqa: F401
+    ComputeKeyMapReduce, FulgoraMemory, GenericVertexProgram, MessageScope, Messenger, Vertices,
+)
 from . import _lib  # noqa: F401
 
 __all__ = [
     "Engine", "Rows", "Schema", "synth_rows", "TitanException", "rmat_edges", "pick_roots", "DegreeCounter", "DegreeMapper",
     "ExecutionException", "GpuGraph", "GpuGraphComputer", "KeyValue", "PageRankMapReduce",
     "PageRankVertexProgram", "ShortestDistanceMapReduce", "ShortestDistanceVertexProgram",
-    "TitanGraphComputer",
+    "TitanGraphComputer", "ComputeKeyMapReduce", "FulgoraMemory", "GenericVertexProgram", "MessageScope",
+    "Messenger", "Vertices",
 ]

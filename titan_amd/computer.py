@@ -29,6 +29,7 @@ import numpy as np
 
 from . import _lib as L
 from .engine import Engine, Schema, TitanException
+from .generic import FulgoraMemory, GenericVertexProgram, preload_scope, run_generic
 
 SCOPE_NAMES = {"outE": L.SCOPE_OUT_E, "inE": L.SCOPE_IN_E, "bothE": L.SCOPE_BOTH_E}
 
@@ -350,6 +351,12 @@ class GpuGraphComputer(TitanGraphComputer):
         return self
 
     def resultMode(self, mode):  # noqa: N802
+        """ResultMode NONE only: PERSIST / LOCALTX write compute keys back through batched
+        transactions in the reference (FulgoraGraphComputer.java:248-305), which this
+        path does not do — rejected instead of silently ignored."""
+        if mode != TitanGraphComputer.ResultMode.NONE:
+            raise TitanException(L.TGO_E_UNSUPPORTED, f"result mode {mode.name} (property write-back) is not supported; "
+                                                      "results are returned through memory and MapReduce")
         self._mode = mode
         return self
 
@@ -377,6 +384,8 @@ class GpuGraphComputer(TitanGraphComputer):
         p = self._program
         props = {}
         iteration = 0
+        if isinstance(p, GenericVertexProgram):
+            return self._run_generic(p, t0)
         if isinstance(p, ShortestDistanceVertexProgram):
             scope = SCOPE_NAMES[p.scope_name]
             wk = 0
@@ -410,3 +419,24 @@ class GpuGraphComputer(TitanGraphComputer):
         rt = (time.perf_counter() - t0) * 1000.0
         vprops = {k: (ids, v) for k, v in props.items()}
         return ComputerResult(self.graph, Memory(iteration, rt, values), vprops)
+
+    def _run_generic(self, p, t0):
+        """Vectorised program: Fulgora's superstep loop on the host, messages combined on the
+        device (titan_amd/generic.py)."""
+        import time
+        scope = preload_scope(p, probe_memory_iterations=3)
+        wk = 0
+        if p.weight_property is not None:
+            wk = self.weight_keys.get(p.weight_property, 0)
+            if wk == 0:
+                raise TitanException(L.TGO_E_INVALID, f"weight property '{p.weight_property}' has no key id")
+        eng = self.graph.engine_for(scope, wk)
+        memory = FulgoraMemory(tuple(p.memory_compute_keys) + tuple(mr.memory_key for mr in self._map_reduces))
+        verts = run_generic(eng, p, memory)
+        memory.setRuntime((time.perf_counter() - t0) * 1000.0)
+        memory.complete()
+        values = dict(memory.previous)
+        for mr in self._map_reduces:
+            values[mr.memory_key] = mr.emit_generic(verts)
+        vprops = {k: (verts.ids, v) for k, v in verts._props.items() if v is not None}
+        return ComputerResult(self.graph, Memory(memory.getIteration(), memory.getRuntime(), values), vprops)

@@ -1,0 +1,309 @@
+"""Generic vertex programs on the GPU path.
+
+A program the engine does not implement natively runs Fulgora's superstep loop
+(FulgoraGraphComputer.submit, FulgoraGraphComputer.java:140-189) here on the host, with its
+``execute`` written over whole per-vertex vectors instead of one vertex at a time, while the
+message traffic — what Fulgora spends its supersteps on — is combined on the device:
+
+* ``MessageScope.Local(incident, edge_fn)`` receives run ``tgo_gather``: every vertex folds
+  ``edge_fn(msg[u], e)`` over its reversed incident entries with the program's combiner
+  (VertexMemoryHandler.receiveMessages, VertexMemoryHandler.java:77-93; FulgoraUtil.java:57);
+* ``MessageScope.Global`` sends run ``tgo_combine_global``: messages to explicit targets fold
+  into the target in send order (VertexState.addMessage, VertexState.java:63-78);
+* ``FulgoraMemory`` restates the global memory: ``incr/and/or/set`` write the current map,
+  ``get`` reads the previous one, ``completeSubRound`` copies current -> previous and
+  ``complete`` steps the iteration back (FulgoraMemory.java:21-131).
+
+Messages are double-buffered exactly as VertexState does (sent in iteration i, read in i+1;
+VertexState.java:55-89), and the scopes a vertex may receive on are the ones the program
+declared for the previous iteration (FulgoraVertexMemory.nextIteration/completeIteration).
+A combiner is required: the vectorised receive returns the combined message (the reference's
+programs reduce the stream with theirs, and a vertex cut needs one anyway, FulgoraUtil.java:80-91).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _lib as L
+
+EDGE_FNS = {"identity": L.EDGE_IDENTITY, "add_one": L.EDGE_ADD_ONE, "add_weight": L.EDGE_ADD_WEIGHT,
+            "mul_weight": L.EDGE_MUL_WEIGHT}
+INCIDENT = {"outE": L.SCOPE_OUT_E, "inE": L.SCOPE_IN_E, "bothE": L.SCOPE_BOTH_E}
+
+
+class MessageScope:
+    class Local:
+        """MessageScope.Local.of(__::<incident>, edgeFunction)."""
+
+        def __init__(self, incident="inE", edge_fn="identity"):
+            if incident not in INCIDENT:
+                raise ValueError(f"incident traversal must be outE, inE or bothE: {incident}")
+            if edge_fn not in EDGE_FNS:
+                raise ValueError(f"unsupported edge function {edge_fn}")
+            self.incident, self.edge_fn = incident, edge_fn
+
+        def __eq__(self, o):
+            return isinstance(o, MessageScope.Local) and (o.incident, o.edge_fn) == (self.incident, self.edge_fn)
+
+        def __hash__(self):
+            return hash(("local", self.incident, self.edge_fn))
+
+        def __repr__(self):
+            return f"Local({self.incident}, {self.edge_fn})"
+
+    class Global:
+        """MessageScope.Global: every Global scope is one inbox (FulgoraVertexMemory.normalizeScope)."""
+
+        def __eq__(self, o):
+            return isinstance(o, MessageScope.Global)
+
+        def __hash__(self):
+            return hash("global")
+
+        def __repr__(self):
+            return "Global"
+
+
+class MemoryException(KeyError):
+    pass
+
+
+class FulgoraMemory:
+    """core/graphdb/olap/computer/FulgoraMemory.java:21-131."""
+
+    def __init__(self, memory_keys=()):
+        self.memory_keys = set(memory_keys)
+        self.previous, self.current = {}, {}
+        self._iteration = 0
+        self._runtime = 0
+
+    def keys(self):
+        return set(self.previous)
+
+    def incrIteration(self):  # noqa: N802
+        self._iteration += 1
+
+    def setIteration(self, it):  # noqa: N802
+        self._iteration = it
+
+    def getIteration(self):  # noqa: N802
+        return self._iteration
+
+    def setRuntime(self, rt):  # noqa: N802
+        self._runtime = rt
+
+    def getRuntime(self):  # noqa: N802
+        return self._runtime
+
+    def isInitialIteration(self):  # noqa: N802
+        return self._iteration == 0
+
+    def complete(self):                       # :73-76
+        self._iteration -= 1
+        self.previous = self.current
+
+    def completeSubRound(self):  # noqa: N802  :78-81
+        self.previous = dict(self.current)
+
+    def exists(self, key):
+        return key in self.previous
+
+    def get(self, key):
+        if key not in self.previous:
+            raise MemoryException(f"The memory does not have a value for provided key: {key}")
+        return self.previous[key]
+
+    def _check(self, key, value):
+        if key not in self.memory_keys:
+            raise ValueError(f"The provided key is not a memory compute key: {key}")
+        if value is None:
+            raise ValueError("Memory values can not be null")
+
+    def incr(self, key, delta):
+        self._check(key, delta)
+        v = self.current.get(key)
+        self.current[key] = int(delta) if v is None else int(delta) + v
+
+    def and_(self, key, b):
+        self._check(key, b)
+        v = self.current.get(key)
+        self.current[key] = bool(b) if v is None else (bool(b) and v)
+
+    def or_(self, key, b):
+        self._check(key, b)
+        v = self.current.get(key)
+        self.current[key] = bool(b) if v is None else (bool(b) or v)
+
+    def set(self, key, value):
+        self._check(key, value)
+        self.current[key] = value
+
+
+class Vertices:
+    """All executing vertices of one superstep: Titan ids (row order) and compute-key
+    properties as (values, present) vectors (VertexState properties, immediate writes)."""
+
+    def __init__(self, ids, compute_keys):
+        self.ids = ids
+        self.n = len(ids)
+        self._props = {k: None for k in compute_keys}
+
+    def property(self, key):
+        """(values, present) — present False where the property was never set."""
+        if key not in self._props:
+            raise KeyError(f"not an element compute key: {key}")
+        return self._props[key]
+
+    def set_property(self, key, values, present=None):
+        if key not in self._props:
+            raise KeyError(f"not an element compute key: {key}")
+        values = np.asarray(values)
+        present = np.ones(self.n, bool) if present is None else np.asarray(present, bool)
+        old = self._props[key]
+        if old is None:
+            self._props[key] = (values.copy(), present.copy())
+        else:                                 # only the vertices that set it change
+            ov, op = old
+            nv = ov.copy()
+            nv[present] = values[present]
+            self._props[key] = (nv, op | present)
+
+
+class Messenger:
+    """Messenger of one superstep: receive() combines the previous superstep's messages of a
+    scope on the device; send() records this superstep's messages."""
+
+    def __init__(self, engine, program, previous, current_scopes):
+        self._e = engine
+        self._p = program
+        self._prev = previous           # scope -> (values, has) as sent last superstep
+        self._scopes = set(current_scopes)
+        self.sent = {}                  # Local scope -> (values, has); Global -> [(targets, values)]
+
+    def receive(self, scope):
+        """(combined values, has-message mask) per vertex for `scope`."""
+        n = self._e.n
+        zero = np.zeros(n, np.int64 if self._p.value_type == L.VAL_INT64 else np.float64)
+        if scope not in self._prev:
+            return zero, np.zeros(n, bool)
+        vals, has = self._prev[scope]
+        if isinstance(scope, MessageScope.Global):
+            return vals, has
+        return self._e.gather(INCIDENT[scope.incident], self._p.value_type, self._p.combiner, EDGE_FNS[scope.edge_fn],
+                              vals, has)
+
+    def send(self, scope, values, has=None):
+        """Local scope: every vertex with has[v] sends values[v] (setMessage on the sender,
+        VertexMemoryHandler.java:106-108).  Global scope: use send_global."""
+        if scope not in self._scopes:
+            raise ValueError(f"Provided scope was not declared in the VertexProgram: {scope}")
+        if isinstance(scope, MessageScope.Global):
+            raise TypeError("Global messages name their targets: use send_global(scope, targets, values)")
+        n = self._e.n
+        has = np.ones(n, bool) if has is None else np.asarray(has, bool)
+        old = self.sent.get(scope)
+        if old is None:
+            self.sent[scope] = (np.array(values, copy=True), has.copy())
+        else:                           # a later send replaces the earlier message (setMessage)
+            ov, oh = old
+            nv = ov.copy()
+            nv[has] = np.asarray(values)[has]
+            self.sent[scope] = (nv, oh | has)
+
+    def send_global(self, scope, target_ids, values):
+        """Messages to explicit vertices (Titan ids; vertex cuts canonicalised, unknown ids
+        dropped), combined per target in send order."""
+        if scope not in self._scopes:
+            raise ValueError(f"Provided scope was not declared in the VertexProgram: {scope}")
+        self.sent.setdefault(MessageScope.Global(), []).append((np.asarray(target_ids, np.int64), np.asarray(values)))
+
+    def finish(self):
+        """completeIteration: this superstep's messages become the next one's previous."""
+        out = {}
+        for scope, v in self.sent.items():
+            if isinstance(scope, MessageScope.Global):
+                tid = np.concatenate([t for t, _ in v]) if v else np.zeros(0, np.int64)
+                val = np.concatenate([x for _, x in v]) if v else np.zeros(0)
+                dense = self._e.dense_ids(tid)
+                keep = dense >= 0
+                out[scope] = self._e.combine_global(self._p.value_type, self._p.combiner, dense[keep], val[keep])
+            else:
+                out[scope] = v
+        return out
+
+
+class GenericVertexProgram:
+    """Base of vectorised vertex programs (TinkerPop VertexProgram, one call per superstep
+    over all vertices).  Subclasses set value_type / combiner and override the hooks."""
+    value_type = L.VAL_INT64
+    combiner = L.COMBINE_SUM
+    compute_keys: tuple = ()
+    memory_compute_keys: tuple = ()
+    weight_property = None              # property read by add_weight / mul_weight edge functions
+
+    def setup(self, memory):
+        pass
+
+    def getMessageScopes(self, memory):  # noqa: N802
+        return []
+
+    def execute(self, vertices: Vertices, messenger: Messenger, memory: FulgoraMemory):
+        raise NotImplementedError("GenericVertexProgram.execute must be overridden")
+
+    def terminate(self, memory) -> bool:
+        return True
+
+
+def preload_scope(program, probe_memory_iterations=1):
+    """The single preload a program's Local scopes need: their common direction, or bothE when
+    they differ (VertexProgramScanJob.getQueries adds one slice per scope, :109-119)."""
+    dirs = set()
+    mem = FulgoraMemory(program.memory_compute_keys)
+    for it in range(probe_memory_iterations):
+        mem.setIteration(it)
+        for s in program.getMessageScopes(mem):
+            if isinstance(s, MessageScope.Local):
+                dirs.add(INCIDENT[s.incident])
+    if len(dirs) == 1:
+        return dirs.pop()
+    return L.SCOPE_BOTH_E
+
+
+def run_generic(engine, program: GenericVertexProgram, memory: FulgoraMemory):
+    """FulgoraGraphComputer.submit's superstep loop (:140-189) over one loaded engine.
+    Returns the final Vertices (compute-key properties)."""
+    ids = engine.vertex_ids()
+    verts = Vertices(ids, program.compute_keys)
+    program.setup(memory)
+    memory.completeSubRound()
+    previous = {}
+    while True:
+        scopes = list(program.getMessageScopes(memory))          # vertexMemory.nextIteration
+        messenger = Messenger(engine, program, previous, scopes)
+        program.execute(verts, messenger, memory)
+        previous = messenger.finish()                            # vertexMemory.completeIteration
+        memory.completeSubRound()
+        try:
+            if program.terminate(memory):
+                break
+        finally:
+            memory.incrIteration()
+            memory.completeSubRound()
+    return verts
+
+
+class ComputeKeyMapReduce:
+    """Emits (vertex id, value) of one compute key for every vertex where it is set — the
+    shape of PageRankMapReduce / ShortestDistanceMapReduce (map :45-50)."""
+
+    def __init__(self, compute_key, memory_key):
+        self.compute_key = compute_key
+        self.memory_key = memory_key
+
+    def emit_generic(self, verts: Vertices):
+        from .computer import KeyValue
+        p = verts.property(self.compute_key)
+        if p is None:
+            return []
+        vals, present = p
+        return [KeyValue(int(i), v.item()) for i, v, ok in zip(verts.ids, vals, present) if ok]
