@@ -508,3 +508,60 @@ def test_walkcount_long_rows():
     assert (src == 3).sum() > 12 * KTILE
     for k in (1, 2, 4):
         assert np.array_equal(eng.walkcount(k), oracle.degree_counter(k)[0])
+
+
+# ----------------------------------------------------------------------------- typed scopes
+def two_label_rows(n=400, seed=21):
+    """Rows of a graph with two MULTI labels: `knows` (weighted) and `likes`; a few hubs carry
+    more than the small hard limit used below."""
+    import random
+    import edgestore as es
+    rnd = random.Random(seed)
+    knows, likes = es.user_edge_label(1), es.user_edge_label(2)
+    wkey = es.user_property_key(1)
+    sd = {"edge_types": [{"type_id": knows, "multiplicity": 0, "signature": [wkey]},
+                         {"type_id": likes, "multiplicity": 0, "signature": [wkey]}],
+          "property_keys": [[wkey, 3]]}
+    osch = fr.OracleSchema(sd["edge_types"], [tuple(x) for x in sd["property_keys"]])
+    edges = []
+    for _ in range(4000):
+        a, b = rnd.randrange(n), rnd.randrange(n)
+        edges.append((a, b, knows if rnd.random() < 0.5 else likes, [(wkey, rnd.randint(1, 9))]))
+    for hub in (0, 1):
+        edges += [(rnd.randrange(n), hub, knows, [(wkey, rnd.randint(1, 9))]) for _ in range(60)]
+        edges += [(hub, rnd.randrange(n), likes, [(wkey, rnd.randint(1, 9))]) for _ in range(60)]
+    rows, vids = es.build_rows(es.GraphSpec(n=n, edges=edges), osch)
+    return rows, vids, sd, osch, knows, likes, wkey
+
+
+@pytest.mark.parametrize("scope", [IN, OUT, BOTH])
+def test_typed_scope_is_fitted_and_sees_only_its_label(scope):
+    """__.inE("knows") etc.: a typed scope sees only that label's entries and is never capped,
+    even past the hard limit (BasicVertexCentricQueryBuilder.java:469-474,710-711); the same
+    scope untyped is cut at the limit (QueryContainer.java:122)."""
+    rows, vids, sd, osch, knows, likes, wkey = two_label_rows()
+    limit = 12
+    n = len(vids)
+    o = fr.OracleGraph.from_rows(rows, osch, scope, hard_limit=limit, labels=[knows], weight_key=wkey)
+    eng = Engine(hard_query_limit=limit).load_rows(rows, Schema.from_dict(sd), scope, labels=[knows],
+                                                   weight_key=wkey, batch_rows=64)
+    assert eng.stats()["truncated_results"] == o.stats.truncated_results == 0
+    untyped = fr.OracleGraph.from_rows(rows, osch, scope, hard_limit=limit, weight_key=wkey)
+    if scope != BOTH:
+        assert untyped.stats.truncated_results > 0
+    # only `knows` entries: the typed entry count is that label's share
+    off, mid, adj, _ = o.export()
+    st = eng.stats()
+    assert st["out_entries"] + st["in_entries"] == len(adj)
+    for r in (0, 1, 5, 77):
+        seed = int(vids[r])
+        assert np.array_equal(eng.bfs(seed, n, scope), o.shortest_distance(seed, n, scope)[0])
+        assert np.array_equal(eng.sssp(seed, 4, scope), o.shortest_distance(seed, 4, scope, weighted=True)[0])
+    if scope == IN:
+        assert np.array_equal(eng.walkcount(3), o.degree_counter(3)[0])
+    if scope != BOTH:
+        pr = eng.pagerank(0.85, n, 8)
+        opr = o.pagerank(0.85, n, 8)[0]
+        fin = np.isfinite(opr)
+        assert np.array_equal(np.isfinite(pr), fin)
+        assert np.abs(pr[fin] - opr[fin]).sum() <= PR_L1_TOL

@@ -184,3 +184,29 @@ def test_partitioned_merge_equals_unpartitioned_graph():
         assert gi.stats.partitioned_vertices == len(part)
     assert np.array_equal(res[0][0], res[1][0])
     assert np.array_equal(res[0][1], res[1][1])
+
+
+def test_typed_scope_filters_labels_and_is_uncapped():
+    """Typed scope (labels given): only those labels' entries, no QueryContainer cap."""
+    import random
+    import edgestore as es
+    rnd = random.Random(3)
+    knows, likes = es.user_edge_label(1), es.user_edge_label(2)
+    sd = {"edge_types": [{"type_id": knows, "multiplicity": 0}, {"type_id": likes, "multiplicity": 0}],
+          "property_keys": []}
+    osch = fr.OracleSchema(sd["edge_types"], [])
+    n = 50
+    edges = [(rnd.randrange(n), rnd.randrange(n), knows if rnd.random() < 0.4 else likes, []) for _ in range(600)]
+    rows, vids = es.build_rows(es.GraphSpec(n=n, edges=edges), osch)
+    o = fr.OracleGraph.from_rows(rows, osch, 1, hard_limit=3, labels=[knows])
+    assert o.stats.truncated_results == 0
+    off, mid, adj, _ = o.export()
+    pos = {int(v): i for i, v in enumerate(o.vertex_ids())}
+    idx = {int(v): i for i, v in enumerate(vids)}
+    for v in range(n):
+        row = pos[int(vids[v])]
+        outs = sorted(pos[int(vids[b])] for a, b, lab, _ in edges if a == v and lab == knows)
+        ins = sorted(pos[int(vids[a])] for a, b, lab, _ in edges if b == v and lab == knows)
+        assert sorted(adj[off[row]:mid[row]].tolist()) == outs
+        assert sorted(adj[mid[row]:off[row + 1]].tolist()) == ins
+    assert idx

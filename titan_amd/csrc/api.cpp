@@ -173,6 +173,14 @@ int upload_graph(tgo_ctx* ctx, HostGraph& h, bool allow_segments = true) {
     HIP_TRY(blocks(h.out.off, g.rb_out));
     HIP_TRY(blocks(h.in.off, g.rb_in));
     g.rb_out_ready = g.rb_in_ready = true;
+    g.push_ws = DevCsr();
+    g.push_ws_ready = false;
+    if (allow_segments && h.has_weight && env_i64("TGO_DS_SPLIT", 1) != 0) {
+        HostCsr ws;                      // light/heavy delta-stepping: push entries sorted by weight
+        weight_sorted_push(h, ws, threads_of(ctx));
+        HIP_TRY(up(ws, g.push_ws));
+        g.push_ws_ready = true;
+    }
     g.cold_in = ColdBlocks();
     g.cold_in_ready = false;
     if (allow_segments && h.scope != TGO_SCOPE_BOTH_E && env_i64("TGO_PR_BLOCKED", 1) != 0) {
@@ -421,6 +429,81 @@ int64_t default_delta(const DevGraph& g, bool weighted) {
     return std::max<int64_t>(1, static_cast<int64_t>(weighted ? 0.25 * g.mean_weight : 1.0));
 }
 
+// Light/heavy delta-stepping (delta.hip, weighted one-GPU loads): a bucket's phases relax
+// light entries only; when its near queue runs dry the bucket's members relax their heavy
+// entries once; then the threshold moves to the next non-empty bucket.
+int run_delta_split(tgo_ctx* ctx, int64_t seed, int64_t delta) {
+    DevGraph& g = ctx->g;
+    Scratch& s = ctx->sc;
+    hipStream_t st = ctx->stream;
+    const int64_t n = g.n, words = (n + 63) / 64 + 1;
+    static const bool trace = env_double("TGO_TRACE", 0.0) != 0.0;
+    if (!s.ds_light) {
+        HIP_TRY(dev_alloc(ctx, s.ds_light, n + 1));
+        HIP_TRY(dev_alloc(ctx, s.ds_member, words));
+        ctx->st.device_bytes = ctx->dev_bytes;
+    }
+    if (s.ds_light_delta != delta) {
+        HIP_TRY(k_ds_light_end(g.push_ws, delta, n, s.ds_light, st));
+        s.ds_light_delta = delta;
+    }
+    HIP_TRY(k_fill_i64(s.dist, INT64_MAX, n, st));
+    HIP_TRY(hipMemsetAsync(s.vb, 0, words * 8, st));        // pending bitmap
+    HIP_TRY(hipMemsetAsync(s.ds_member, 0, words * 8, st));
+    int phases = 0, buckets = 0;
+    int64_t relaxed = 0;
+    if (seed >= 0) {
+        HIP_TRY(k_ds_seed_ws(g.push_ws, s.ds_light, s.dist, s.q[0], s.qdeg, seed, st));
+        int64_t qlen = 1, thr = delta;
+        int cur = 0;
+        for (;;) {
+            if (qlen == 0) {
+                // bucket settled: next near queue + the members' heavy entries, one extraction
+                HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
+                HIP_TRY(hipMemsetAsync(&s.cnt->red[0], 0x7F, sizeof(unsigned long long), st));   // ~INT64_MAX
+                HIP_TRY(k_ds_pending_min_ws(s.vb, s.ds_member, words, s.dist, s.cnt, st));
+                if (int rc = read_counters(ctx)) return rc;
+                const int64_t pending = static_cast<int64_t>(s.hcnt->red[1]);
+                const int64_t members = static_cast<int64_t>(s.hcnt->red2);
+                if (pending == 0 && members == 0) break;        // converged
+                if (pending > 0) {
+                    const int64_t mn = static_cast<int64_t>(s.hcnt->red[0]);
+                    if (mn >= thr) thr = (mn / delta + 1) * delta;
+                    ++buckets;
+                }
+                HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
+                HIP_TRY(k_ds_extract_ws(g.push_ws, s.ds_light, s.vb, s.ds_member, n, s.dist, thr, s.q[cur], s.qdeg, s.cnt,
+                                        st));
+                if (int rc = read_counters(ctx)) return rc;
+                qlen = static_cast<int64_t>(s.hcnt->qlen);
+                if (trace) std::fprintf(stderr, "[tgo] delta bucket thr %lld: %lld pending, %lld members, %lld queued\n",
+                                        (long long)thr, (long long)pending, (long long)members, (long long)qlen);
+                if (qlen == 0) {
+                    if (pending > 0) return fail(ctx, TGO_E_HIP, "delta-stepping: extraction found no vertex below the threshold");
+                    continue;                                   // members without heavy entries
+                }
+            }
+            HIP_TRY(k_ds_commit_ws(s.q[cur], qlen, s.dist, s.msg, s.vb, s.ds_member, s.qdeg, s.cnt, st));
+            HIP_TRY(scan_exclusive_i64(s.cub_tmp, s.cub_bytes, s.qdeg, s.qpre, qlen + 1, st));   // tail zeroed by commit
+            HIP_TRY(k_ds_relax_ws(g.push_ws, s.ds_light, s.q[cur], s.qpre, qlen, s.msg, s.dist, s.vb, s.q[cur ^ 1], s.qdeg,
+                                  s.cnt, thr, st));
+            if (int rc = read_counters(ctx)) return rc;
+            if (s.hcnt->err) return fail(ctx, TGO_E_PROGRAM,
+                "vertex program failed: a traversed edge has no value for the weight property");
+            relaxed += static_cast<int64_t>(s.hcnt->red[1]);
+            qlen = static_cast<int64_t>(s.hcnt->qlen);
+            cur ^= 1;
+            ++phases;
+        }
+    }
+    HIP_TRY(k_dist_finalize(s.dist, n, st));
+    if (trace) std::fprintf(stderr, "[tgo] delta %lld (light/heavy): %d phases, %d buckets, %lld entries relaxed\n",
+                            (long long)delta, phases, buckets, (long long)relaxed);
+    ctx->st.levels = phases;
+    ctx->st.relaxed_entries = relaxed;
+    return TGO_OK;
+}
+
 // Delta-stepping (delta.hip): converged distances, near queue relaxed phase by phase,
 // bucket threshold advanced from the minimum pending distance when the queue runs dry.
 int run_delta(tgo_ctx* ctx, int64_t seed, int scope, bool weighted, int64_t delta) {
@@ -431,6 +514,7 @@ int run_delta(tgo_ctx* ctx, int64_t seed, int scope, bool weighted, int64_t delt
     const View push = push_view(g, scope);
     static const bool trace = env_double("TGO_TRACE", 0.0) != 0.0;
     if (delta <= 0) delta = default_delta(g, weighted);
+    if (weighted && g.push_ws_ready && scope == g.scope) return run_delta_split(ctx, seed, delta);
     HIP_TRY(k_fill_i64(s.dist, INT64_MAX, n, st));
     HIP_TRY(hipMemsetAsync(s.vb, 0, words * 8, st));        // pending bitmap
     int phases = 0, buckets = 0;

@@ -88,6 +88,65 @@ __device__ __forceinline__ void block_flush(Counters* cnt, AppendLds& sh, unsign
     }
 }
 
+// Bitmap extraction into a queue, two passes over a contiguous chunk of 64-vertex words per
+// block (one wave per word): pass 1 counts what the chunk takes, one atomicAdd per block
+// reserves its slots, pass 2 re-reads (L2-warm) and writes.  No per-trip block barriers or
+// counter atomics, which dominated the one-pass version (~200 us per extraction at 16M
+// vertices).  probe(wd, takes, commit) fills up to kStreams (take, entry, degree) per lane and
+// returns whether the word needs a write; with commit it also clears what it took (one
+// writer per word) — pass 1 never writes, so both passes see the same bits.
+struct Take { bool take; int32_t entry; int64_t deg; };
+template <int kStreams, class Probe>
+__device__ __forceinline__ void chunk_extract(int64_t words, const Probe& probe, int32_t* __restrict__ qn,
+                                              int64_t* __restrict__ qdeg, Counters* cnt) {
+    __shared__ unsigned long long s_cnt[kWavesPerBlock], s_mf[kWavesPerBlock], s_base;
+    const int64_t per = ((words + gridDim.x - 1) / gridDim.x + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock;
+    const int64_t w0 = static_cast<int64_t>(blockIdx.x) * per;
+    const int64_t w1 = min(words, w0 + per);
+    const int wave = threadIdx.x >> 6;
+    const unsigned long long below = (1ULL << lane()) - 1ULL;
+    unsigned long long count = 0, dsum = 0;
+    bool touch = false;
+    for (int64_t wd = w0 + wave; wd < w1; wd += kWavesPerBlock) {
+        Take t[kStreams];
+        touch |= probe(wd, t, false);
+        for (int k = 0; k < kStreams; ++k) {
+            count += __popcll(__ballot(t[k].take));
+            if (t[k].take) dsum += static_cast<unsigned long long>(t[k].deg);
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) dsum += __shfl_xor(dsum, o, 64);
+    if (lane() == 0) { s_cnt[wave] = count; s_mf[wave] = dsum; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0, m = 0;
+        for (int w = 0; w < kWavesPerBlock; ++w) { const unsigned long long c = s_cnt[w]; s_cnt[w] = t; t += c; m += s_mf[w]; }
+        s_base = t ? atomicAdd(&cnt->qlen, t) : 0ULL;
+        if (m) atomicAdd(&cnt->mf, m);
+    }
+    __syncthreads();
+    if (!touch) return;                                      // wave-uniform
+    unsigned long long cursor = s_base + s_cnt[wave];
+    for (int64_t wd = w0 + wave; wd < w1; wd += kWavesPerBlock) {
+        Take t[kStreams];
+        probe(wd, t, true);
+        for (int k = 0; k < kStreams; ++k) {
+            const unsigned long long mask = __ballot(t[k].take);
+            if (t[k].take) {
+                const unsigned long long slot = cursor + __popcll(mask & below);
+                qn[slot] = t[k].entry;
+                qdeg[slot] = t[k].deg;
+            }
+            cursor += __popcll(mask);
+        }
+    }
+}
+
+inline int extract_grid(int64_t words) {
+    const int64_t g = (words + 63) / 64;                      // >= 64 words per block
+    return static_cast<int>(g < 1 ? 1 : (g > 2048 ? 2048 : g));
+}
+
 // min(cand) into dist[v] of an owned vertex; true when v has to join the near queue.
 __device__ __forceinline__ bool relax_owned(int64_t* dist, uint64_t* pend, int64_t v, int64_t cand, int64_t thr) {
     if (cand >= dist[v]) return false;                  // a stale (larger) read only costs an atomic
@@ -212,6 +271,200 @@ __global__ void __launch_bounds__(kBlock) ds_relax(View push, const int32_t* __r
     block_flush(cnt, sh, mf);
 }
 
+// ---- light/heavy split (one GPU, weighted): the push entries of every vertex sorted by
+// weight (DevGraph::push_ws), light[u] = end of u's entries lighter than delta.  A bucket's
+// phases relax LIGHT entries only; a vertex relaxed in the bucket is marked in `member`.  When
+// the bucket's near queue runs dry its members' distances are final, and their HEAVY entries
+// are relaxed once (Meyer & Sanders' light/heavy split) — in the same launches as the next
+// bucket's first light phase: the extraction queues the next near queue and the members'
+// heavy entries together (queue entry | kHeavyFlag), so the split costs no extra host round
+// trip.  A heavy relaxation lands at >= the settled bucket's threshold: in the new bucket it
+// simply joins the near queue, beyond it it stays pending (label-correcting: the converged
+// distances do not depend on the order).
+constexpr uint32_t kHeavyFlag = 0x80000000u;
+
+__device__ __forceinline__ int64_t light_degree(const int64_t* off, const int64_t* light, int64_t u) {
+    return light[u] - off[u];
+}
+
+__global__ void ds_light_end(const int64_t* __restrict__ off, const int32_t* __restrict__ w, int64_t delta,
+                             int64_t n, int64_t* __restrict__ light) {
+    for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x) {
+        int64_t a = off[v], b = off[v + 1];               // first entry with w >= delta
+        while (a < b) {
+            const int64_t c = (a + b) >> 1;
+            if (static_cast<int64_t>(w[c]) < delta) a = c + 1; else b = c;
+        }
+        light[v] = a;
+    }
+}
+
+__global__ void ds_seed_ws(const int64_t* off, const int64_t* light, int64_t* dist, int32_t* q, int64_t* qdeg,
+                           int64_t seed) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        dist[seed] = 0;
+        q[0] = static_cast<int32_t>(seed);
+        qdeg[0] = light_degree(off, light, seed);
+    }
+}
+
+// Light entries: snapshot, clear pending, mark the bucket member.  Heavy entries: the member's
+// distance is final and msg already holds it.  Also zeroes the counters and the scan's tail
+// degree for the phase (saves two memset launches per phase).
+__global__ void ds_commit_ws(const int32_t* __restrict__ q, int64_t qlen, const int64_t* __restrict__ dist,
+                             int64_t* __restrict__ msg, uint64_t* __restrict__ pend, uint64_t* __restrict__ member,
+                             int64_t* __restrict__ qdeg, Counters* cnt) {
+    if (blockIdx.x == 0) {
+        constexpr int kWords = sizeof(Counters) / sizeof(unsigned long long);
+        static_assert(kWords <= kBlock, "one thread per counter word");
+        if (threadIdx.x < kWords) reinterpret_cast<unsigned long long*>(cnt)[threadIdx.x] = 0ULL;
+        if (threadIdx.x == 0) qdeg[qlen] = 0;
+    }
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < qlen; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t e = static_cast<uint32_t>(q[i]);
+        if (e & kHeavyFlag) continue;
+        const int32_t v = static_cast<int32_t>(e);
+        msg[v] = dist[v];
+        const uint64_t bit = 1ULL << (v & 63);
+        if (pend[v >> 6] & bit) atomicAnd(reinterpret_cast<unsigned long long*>(&pend[v >> 6]), ~bit);
+        if (!(member[v >> 6] & bit)) atomicOr(reinterpret_cast<unsigned long long*>(&member[v >> 6]), bit);
+    }
+}
+
+// ds_relax over one weight-sorted list: queue entry u relaxes [off[u], light[u]) or, flagged
+// heavy, [light[u], off[u+1]); load-balanced as in ds_relax.
+__global__ void __launch_bounds__(kBlock) ds_relax_ws(const int64_t* __restrict__ off, const int32_t* __restrict__ adj,
+        const int32_t* __restrict__ wt, const int64_t* __restrict__ light, const int32_t* __restrict__ q,
+        const int64_t* __restrict__ qpre, int64_t qlen, const int64_t* __restrict__ msg, int64_t* __restrict__ dist,
+        uint64_t* __restrict__ pend, int32_t* __restrict__ qn, int64_t* __restrict__ qdeg_n, Counters* cnt, int64_t thr) {
+    __shared__ int64_t s_pre[kLdsEntries];
+    __shared__ int32_t s_q[kLdsEntries];
+    __shared__ int64_t s_lo, s_hi;
+    __shared__ AppendLds sh;
+    unsigned long long mf = 0;
+    const int64_t total = qpre[qlen];
+    if (blockIdx.x == 0 && threadIdx.x == 0) cnt->red[1] = static_cast<unsigned long long>(total);   // work done
+    const int64_t ntiles = (total + kTileEdges - 1) / kTileEdges;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t t0 = tile * kTileEdges;
+        const int64_t t1 = min(total, t0 + kTileEdges);
+        if (threadIdx.x == 0) {
+            int64_t a = 0, b = qlen;
+            while (b - a > 1) { const int64_t c = (a + b) >> 1; if (qpre[c] <= t0) a = c; else b = c; }
+            s_lo = a;
+            int64_t a2 = a, b2 = qlen;
+            while (b2 - a2 > 1) { const int64_t c = (a2 + b2) >> 1; if (qpre[c] <= t1 - 1) a2 = c; else b2 = c; }
+            s_hi = a2;
+        }
+        __syncthreads();
+        const int64_t lo_q = s_lo, hi_q = s_hi;
+        const int64_t span = hi_q - lo_q + 1;
+        const bool in_lds = span + 1 <= kLdsEntries;
+        if (in_lds) {
+            for (int64_t i = threadIdx.x; i <= span; i += kBlock) {
+                s_pre[i] = qpre[lo_q + i];
+                if (i < span) s_q[i] = q[lo_q + i];
+            }
+        }
+        __syncthreads();
+        for (int k = 0; k < kEdgesPerThread; ++k) {
+            const int64_t j = t0 + k * kBlock + threadIdx.x;
+            bool take = false;
+            int32_t v = 0;
+            int64_t vdeg = 0;
+            if (j < t1) {
+                uint32_t qe; int64_t start;
+                if (in_lds) {
+                    int64_t a = 0, b = span;
+                    while (b - a > 1) { const int64_t c = (a + b) >> 1; if (s_pre[c] <= j) a = c; else b = c; }
+                    qe = static_cast<uint32_t>(s_q[a]); start = s_pre[a];
+                } else {
+                    int64_t a = lo_q, b = hi_q + 1;
+                    while (b - a > 1) { const int64_t c = (a + b) >> 1; if (qpre[c] <= j) a = c; else b = c; }
+                    qe = static_cast<uint32_t>(q[a]); start = qpre[a];
+                }
+                const int64_t u = static_cast<int64_t>(qe & ~kHeavyFlag);
+                const int64_t e = ((qe & kHeavyFlag) ? light[u] : off[u]) + (j - start);
+                const int32_t t = adj[e], w = wt[e];
+                const int64_t mu = msg[u];
+                if (w == kMissingWeight) {
+                    atomicOr(&cnt->err, 1ULL);              // edge.value(weight) on a missing key
+                } else if (dist[u] < mu) {
+                    // improved during this phase: pending again, relaxes with the better distance
+                } else if (relax_owned(dist, pend, t, mu + static_cast<int64_t>(w), thr)) {
+                    take = true;
+                    v = t;
+                    vdeg = light_degree(off, light, t);
+                }
+            }
+            block_append(take, v, vdeg, qn, qdeg_n, cnt, sh, mf);
+        }
+        __syncthreads();
+    }
+    block_flush(cnt, sh, mf);
+}
+
+// Next queue from the bitmaps (one wave per 64-vertex word), clearing what it takes: pending
+// vertices with dist < thr (the new bucket's near queue, light degrees) and every member of
+// the settled bucket with heavy entries (flagged, heavy degrees).
+__global__ void __launch_bounds__(kBlock) ds_extract_ws(const int64_t* __restrict__ off,
+        const int64_t* __restrict__ light, uint64_t* __restrict__ pend, uint64_t* __restrict__ member, int64_t n,
+        const int64_t* __restrict__ dist, int64_t thr, int32_t* __restrict__ qn, int64_t* __restrict__ qdeg,
+        Counters* cnt) {
+    const int64_t words = (n + 63) >> 6;
+    auto probe = [&](int64_t wd, Take* t, bool commit) -> bool {
+        const uint64_t pb = pend[wd];                            // uniform across the wave
+        const uint64_t mb = member[wd];
+        const int64_t v = (wd << 6) + lane();
+        const bool lt = pb && ((pb >> lane()) & 1ULL) && dist[v] < thr;
+        const bool mine = mb && ((mb >> lane()) & 1ULL);
+        const int64_t hdeg = mine ? off[v + 1] - light[v] : 0;
+        const unsigned long long tm = __ballot(lt);
+        if (commit && lane() == 0) {
+            if (tm) pend[wd] = pb & ~tm;
+            if (mb) member[wd] = 0;
+        }
+        t[0] = {lt, static_cast<int32_t>(v), lt ? light_degree(off, light, v) : 0};
+        t[1] = {hdeg > 0, static_cast<int32_t>(static_cast<uint32_t>(v) | kHeavyFlag), hdeg};
+        return tm || mb;
+    };
+    chunk_extract<2>(words, probe, qn, qdeg, cnt);
+}
+
+// Pending minimum / count (red[0], red[1]) and the settled bucket's members left (red2).
+__global__ void __launch_bounds__(kBlock) ds_pending_min_ws(const uint64_t* __restrict__ pend,
+        const uint64_t* __restrict__ member, int64_t words, const int64_t* __restrict__ dist, Counters* cnt) {
+    unsigned long long mn = ~0ULL >> 1, count = 0, mem = 0;
+    for (int64_t wd = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; wd < words; wd += (int64_t)gridDim.x * blockDim.x) {
+        uint64_t b = pend[wd];
+        count += __popcll(b);
+        mem += __popcll(member[wd]);
+        while (b) {
+            const int r = __ffsll(static_cast<long long>(b)) - 1;
+            b &= b - 1;
+            const unsigned long long d = static_cast<unsigned long long>(dist[(wd << 6) + r]);
+            mn = d < mn ? d : mn;
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_xor(mn, off, 64);
+        mn = o < mn ? o : mn;
+        count += __shfl_xor(count, off, 64);
+        mem += __shfl_xor(mem, off, 64);
+    }
+    __shared__ unsigned long long s_mn[kBlock / 64], s_ct[kBlock / 64], s_mb[kBlock / 64];
+    if (lane() == 0) { s_mn[threadIdx.x >> 6] = mn; s_ct[threadIdx.x >> 6] = count; s_mb[threadIdx.x >> 6] = mem; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kBlock / 64; ++w) { mn = s_mn[w] < mn ? s_mn[w] : mn; count += s_ct[w]; mem += s_mb[w]; }
+        if (count) {
+            atomicMin(&cnt->red[0], mn);
+            atomicAdd(&cnt->red[1], count);
+        }
+        if (mem) atomicAdd(&cnt->red2, mem);
+    }
+}
+
 // Minimum distance over the pending vertices (into cnt->red[0], pre-set to a large value)
 // and their number (cnt->red[1]).
 __global__ void __launch_bounds__(kBlock) ds_pending_min(const uint64_t* __restrict__ pend, int64_t words,
@@ -248,20 +501,17 @@ __global__ void __launch_bounds__(kBlock) ds_pending_min(const uint64_t* __restr
 __global__ void __launch_bounds__(kBlock) ds_extract(View push, uint64_t* __restrict__ pend, int64_t n,
         const int64_t* __restrict__ dist, int64_t thr, int32_t* __restrict__ qn, int64_t* __restrict__ qdeg,
         Counters* cnt) {
-    __shared__ AppendLds sh;
-    unsigned long long mf = 0;
     const int64_t words = (n + 63) >> 6;
-    for (int64_t bw = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock; bw < words;
-         bw += static_cast<int64_t>(gridDim.x) * kWavesPerBlock) {        // block-uniform trips
-        const int64_t wd = bw + (threadIdx.x >> 6);
-        const uint64_t b = wd < words ? pend[wd] : 0ULL;     // uniform across the wave
+    auto probe = [&](int64_t wd, Take* t, bool commit) -> bool {
+        const uint64_t b = pend[wd];                             // uniform across the wave
         const int64_t v = (wd << 6) + lane();
         const bool take = b && ((b >> lane()) & 1ULL) && dist[v] < thr;
         const unsigned long long tm = __ballot(take);
-        if (lane() == 0 && tm) pend[wd] = b & ~tm;       // one writer per word
-        block_append(take, static_cast<int32_t>(v), take ? push_degree(push, v) : 0, qn, qdeg, cnt, sh, mf);
-    }
-    block_flush(cnt, sh, mf);
+        if (commit && lane() == 0 && tm) pend[wd] = b & ~tm;
+        t[0] = {take, static_cast<int32_t>(v), take ? push_degree(push, v) : 0};
+        return tm != 0;
+    };
+    chunk_extract<1>(words, probe, qn, qdeg, cnt);
 }
 
 // Partitioned: marked remote targets per owner rank (rank r owns words [r*wpr, (r+1)*wpr)).
@@ -351,6 +601,38 @@ hipError_t k_ds_relax_part(const View& push, const int32_t* q, const int64_t* qp
                                              lo, n_local, rbest, rmark);
     return hipGetLastError();
 }
+hipError_t k_ds_light_end(const DevCsr& ws, int64_t delta, int64_t n, int64_t* light, hipStream_t s) {
+    ds_light_end<<<grid_for(n, 8192), kBlock, 0, s>>>(ws.off, ws.w, delta, n, light);
+    return hipGetLastError();
+}
+hipError_t k_ds_seed_ws(const DevCsr& ws, const int64_t* light, int64_t* dist, int32_t* q, int64_t* qdeg, int64_t seed,
+                        hipStream_t s) {
+    ds_seed_ws<<<1, 64, 0, s>>>(ws.off, light, dist, q, qdeg, seed);
+    return hipGetLastError();
+}
+hipError_t k_ds_commit_ws(const int32_t* q, int64_t qlen, const int64_t* dist, int64_t* msg, uint64_t* pend,
+                          uint64_t* member, int64_t* qdeg, Counters* cnt, hipStream_t s) {
+    ds_commit_ws<<<grid_for(qlen, 2048), kBlock, 0, s>>>(q, qlen, dist, msg, pend, member, qdeg, cnt);
+    return hipGetLastError();
+}
+hipError_t k_ds_relax_ws(const DevCsr& ws, const int64_t* light, const int32_t* q, const int64_t* qpre, int64_t qlen,
+                         const int64_t* msg, int64_t* dist, uint64_t* pend, int32_t* qn, int64_t* qdeg_n, Counters* cnt,
+                         int64_t thr, hipStream_t s) {
+    ds_relax_ws<<<256 * 8, kBlock, 0, s>>>(ws.off, ws.adj, ws.w, light, q, qpre, qlen, msg, dist, pend, qn, qdeg_n, cnt,
+                                           thr);
+    return hipGetLastError();
+}
+hipError_t k_ds_extract_ws(const DevCsr& ws, const int64_t* light, uint64_t* pend, uint64_t* member, int64_t n,
+                           const int64_t* dist, int64_t thr, int32_t* qn, int64_t* qdeg, Counters* cnt, hipStream_t s) {
+    const int64_t words = (n + 63) / 64;
+    ds_extract_ws<<<extract_grid(words), kBlock, 0, s>>>(ws.off, light, pend, member, n, dist, thr, qn, qdeg, cnt);
+    return hipGetLastError();
+}
+hipError_t k_ds_pending_min_ws(const uint64_t* pend, const uint64_t* member, int64_t words, const int64_t* dist,
+                               Counters* cnt, hipStream_t s) {
+    ds_pending_min_ws<<<grid_for(words, 1024), kBlock, 0, s>>>(pend, member, words, dist, cnt);
+    return hipGetLastError();
+}
 hipError_t k_ds_pending_min(const uint64_t* pend, int64_t words, const int64_t* dist, Counters* cnt, hipStream_t s) {
     ds_pending_min<<<grid_for(words, 1024), kBlock, 0, s>>>(pend, words, dist, cnt);
     return hipGetLastError();
@@ -358,7 +640,7 @@ hipError_t k_ds_pending_min(const uint64_t* pend, int64_t words, const int64_t* 
 hipError_t k_ds_extract(const View& push, uint64_t* pend, int64_t n, const int64_t* dist, int64_t thr, int32_t* qn,
                         int64_t* qdeg, Counters* cnt, hipStream_t s) {
     const int64_t words = (n + 63) / 64;
-    ds_extract<<<grid_for(words * 64, 8192), kBlock, 0, s>>>(push, pend, n, dist, thr, qn, qdeg, cnt);
+    ds_extract<<<extract_grid(words), kBlock, 0, s>>>(push, pend, n, dist, thr, qn, qdeg, cnt);
     return hipGetLastError();
 }
 hipError_t k_ds_mark_count(const uint64_t* rmark, int64_t words, int64_t wpr, unsigned long long* counts, hipStream_t s) {

@@ -171,6 +171,8 @@ struct DevGraph {
     int64_t lo = 0, n_global = 0;
     RowBlocks rb_out, rb_in;    // CSR-adaptive blocks per pull list
     bool rb_out_ready = false, rb_in_ready = false;
+    DevCsr push_ws;             // weighted loads: push entries sorted by weight (light/heavy delta-stepping)
+    bool push_ws_ready = false;
     ColdBlocks cold_in;         // cache-blocked in-lists (one-GPU PageRank)
     bool cold_in_ready = false;
 };
@@ -192,7 +194,8 @@ struct Counters {               // device-side level counters (one cache line ea
     unsigned long long err;     // program failure flag
     unsigned long long pad2[7];
     unsigned long long red[2];  // reductions (reached vertices, reached entries)
-    unsigned long long pad3[6];
+    unsigned long long red2;    // third reduction (delta-stepping: bucket members left)
+    unsigned long long pad3[5];
 };
 
 struct Scratch {
@@ -224,6 +227,10 @@ struct Scratch {
     int32_t ms_nsrc = 0;
     int64_t* pk_cnt = nullptr;      // partitioned sparse exchange: per-chunk pair counts
     int64_t* pk_off = nullptr;      // and their exclusive scan (n_global / kPackChunk + 1 each)
+    // light/heavy delta-stepping (allocated on first use)
+    int64_t* ds_light = nullptr;    // n: end of each vertex's light entries in push_ws
+    int64_t ds_light_delta = -1;    // bucket width ds_light was computed for
+    uint64_t* ds_member = nullptr;  // words: vertices relaxed in the current bucket
     // generic vertex programs (allocated on first use): row-order staging + internal-order vectors
     int64_t* gv[3] = {nullptr, nullptr, nullptr};
     uint8_t* gh[3] = {nullptr, nullptr, nullptr};
@@ -269,6 +276,19 @@ hipError_t k_ds_commit(const int32_t* q, int64_t qlen, const int64_t* dist, int6
 hipError_t k_ds_relax(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen, const int64_t* msg,
                       int64_t* dist, uint64_t* pend, int32_t* qn, int64_t* qdeg_n, Counters* cnt, int weighted,
                       int64_t thr, hipStream_t s);
+// light/heavy delta-stepping over the weight-sorted push lists (delta.hip)
+hipError_t k_ds_light_end(const DevCsr& ws, int64_t delta, int64_t n, int64_t* light, hipStream_t s);
+hipError_t k_ds_seed_ws(const DevCsr& ws, const int64_t* light, int64_t* dist, int32_t* q, int64_t* qdeg, int64_t seed,
+                        hipStream_t s);
+hipError_t k_ds_commit_ws(const int32_t* q, int64_t qlen, const int64_t* dist, int64_t* msg, uint64_t* pend,
+                          uint64_t* member, int64_t* qdeg, Counters* cnt, hipStream_t s);
+hipError_t k_ds_relax_ws(const DevCsr& ws, const int64_t* light, const int32_t* q, const int64_t* qpre, int64_t qlen,
+                         const int64_t* msg, int64_t* dist, uint64_t* pend, int32_t* qn, int64_t* qdeg_n, Counters* cnt,
+                         int64_t thr, hipStream_t s);
+hipError_t k_ds_extract_ws(const DevCsr& ws, const int64_t* light, uint64_t* pend, uint64_t* member, int64_t n,
+                           const int64_t* dist, int64_t thr, int32_t* qn, int64_t* qdeg, Counters* cnt, hipStream_t s);
+hipError_t k_ds_pending_min_ws(const uint64_t* pend, const uint64_t* member, int64_t words, const int64_t* dist,
+                               Counters* cnt, hipStream_t s);
 hipError_t k_ds_pending_min(const uint64_t* pend, int64_t words, const int64_t* dist, Counters* cnt, hipStream_t s);
 hipError_t k_ds_extract(const View& push, uint64_t* pend, int64_t n, const int64_t* dist, int64_t thr, int32_t* qn,
                         int64_t* qdeg, Counters* cnt, hipStream_t s);
@@ -337,6 +357,8 @@ hipError_t k_global_combine(void*& tmp, size_t& tmp_bytes, const int64_t* target
 hipError_t scan_exclusive_i64(void*& tmp, size_t& tmp_bytes, const int64_t* in, int64_t* out,
                               int64_t n, hipStream_t s);
 
+// Push entries of the loaded scope in one list per vertex sorted by (weight, target).
+void weight_sorted_push(const HostGraph& g, HostCsr& ws, int threads);
 // Source-sorted, packed tiles of a CSR (see graph_build.cpp); false if sources need > 19 bits.
 bool pack_tiles(const std::vector<int64_t>& off, std::vector<int32_t>& adj, const std::vector<int64_t>& blk,
                 const std::vector<int64_t>& cbeg, const std::vector<int64_t>& cend, int64_t tile, int threads);

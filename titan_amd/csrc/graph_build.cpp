@@ -720,6 +720,44 @@ bool pack_tiles(const std::vector<int64_t>& off, std::vector<int32_t>& adj, cons
     return true;
 }
 
+// ------------------------------------------------------------------ weight-sorted push lists
+// Light/heavy delta-stepping (delta.hip): every vertex's push entries (the push view of the
+// loaded scope: the explicit transpose when the cap made lists asymmetric, both lists for
+// bothE) in one list sorted by (weight, target) — the light entries of any bucket width are a
+// prefix.  An entry without the weight property (kMissingWeight = INT32_MIN) sorts first,
+// so the first light relaxation reports it.  A min over the list does not depend on order.
+void weight_sorted_push(const HostGraph& g, HostCsr& ws, int threads) {
+    const int64_t n = g.n;
+    std::vector<const HostCsr*> lists;
+    if (g.has_transpose) lists = {&g.push_t};
+    else if (g.scope == TGO_SCOPE_IN_E) lists = {&g.in};
+    else if (g.scope == TGO_SCOPE_OUT_E) lists = {&g.out};
+    else lists = {&g.out, &g.in};
+    ws.off.assign(n + 1, 0);
+    for (int64_t v = 0; v < n; ++v) {
+        int64_t d = 0;
+        for (const HostCsr* c : lists) d += c->off[v + 1] - c->off[v];
+        ws.off[v + 1] = ws.off[v] + d;
+    }
+    ws.adj.assign(static_cast<size_t>(ws.off[n]), 0);
+    ws.w.assign(static_cast<size_t>(ws.off[n]), 0);
+    threads = std::max(1, threads);
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads; ++t)
+        th.emplace_back([&, t] {
+            std::vector<std::pair<int32_t, int32_t>> buf;
+            for (int64_t v = n * t / threads; v < n * (t + 1) / threads; ++v) {
+                buf.clear();
+                for (const HostCsr* c : lists)
+                    for (int64_t k = c->off[v]; k < c->off[v + 1]; ++k) buf.emplace_back(c->w[k], c->adj[k]);
+                std::sort(buf.begin(), buf.end());
+                int64_t o = ws.off[v];
+                for (const auto& e : buf) { ws.w[o] = e.first; ws.adj[o] = e.second; ++o; }
+            }
+        });
+    for (auto& x : th) x.join();
+}
+
 // ------------------------------------------------------------------ cache-blocked gather
 // ColdBlocks layout (engine.hpp).  Rows are split over `threads` contiguous ranges; pass 1
 // counts every row's hot entries and cold pieces per segment (per-thread segment totals),
