@@ -323,8 +323,9 @@ def run_partitioned(args, world, rank, local_rank):
     import torch.distributed as dist
     from titan_amd import Engine
     from titan_amd import _lib as L
-    from titan_amd.distributed import (HipPartBackend, all_gather_layout, exchange_stream, distributed_bfs, distributed_msbfs,
-                                       distributed_pagerank, partition_range)
+    from titan_amd.distributed import (HipPartBackend, all_gather_layout, distributed_bfs, distributed_msbfs,
+                                       distributed_pagerank, entry_imbalance, exchange_stream, pagerank_layout,
+                                       partition_range, pick_roots_partitioned)
     torch.cuda.set_device(local_rank)
     dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     scale = args.scale + int(round(math.log2(world)))
@@ -350,28 +351,25 @@ def run_partitioned(args, world, rank, local_rank):
     lay = all_gather_layout(src, dst, n, lo, hi, torch.device("cuda", local_rank)) if args.layout else None
     bfs_be = HipPartBackend(Engine(device=local_rank, host_threads=16, stream=stream)
                             .load_partition(n, lo, hi, src, dst, L.SCOPE_BOTH_E, apply_cap=False, layout=lay),
-                            n, lo, hi)
+                            n, lo, hi, device_counts=True)
     pr_eng = Engine(device=local_rank, host_threads=16, stream=stream).load_partition(n, lo, hi, src, dst,
                                                                                     L.SCOPE_IN_E, apply_cap=True,
                                                                                     layout=lay)
     pr_be = HipPartBackend(pr_eng, n, lo, hi)
+    pr_layout = pagerank_layout(pr_be)       # cache-blocked hot-first exchange (tgo_part_pr_blocked)
     log(f"partition graphs loaded in {time.perf_counter() - t0:.1f}s")
-    # roots: seeded candidates, kept when their (global) degree is > 0
-    rng = np.random.default_rng(7)
-    cand = rng.integers(0, n, size=max(16 * args.roots, 1024))
-    own = (src >= lo) & (src < hi)
-    deg = np.bincount(src[own] - lo, minlength=hi - lo) + np.bincount(dst[(dst >= lo) & (dst < hi)] - lo, minlength=hi - lo)
-    ok = np.array([deg[c - lo] > 0 if lo <= c < hi else 0 for c in cand], np.int64)
-    okt = torch.from_numpy(ok).cuda()
-    dist.all_reduce(okt)
-    roots = [int(c) for c, k in zip(cand, okt.cpu().numpy()) if k > 0]
-    roots = list(dict.fromkeys(roots))[:args.roots]
+    # the one-GPU bench's roots (tgo_pick_roots over the whole edge list), from partition edges
+    roots = pick_roots_partitioned(n, src, dst, lo, hi, args.roots, 7, torch.device("cuda", local_rank))
+    # per-rank owned entries of the bothE graph: the partition's load imbalance (max / mean)
+    ent = bfs_be.e.stats()
+    rank_entries, imbalance = entry_imbalance(int(ent["out_entries"] + ent["in_entries"]),
+                                              torch.device("cuda", local_rank))
     # per-root reached entries (untimed) for GTEPS
     _, mR, depth_ms = distributed_msbfs(bfs_be, roots, n, stats=True)
-    # single-source side measurement (untimed, 8 roots, Graph500 style)
+    # single-source side measurement (untimed, every root, Graph500 style harmonic mean)
     ss_t = []
-    for r in roots[:8]:
-        distributed_bfs(bfs_be, r, n, fetch=False, stats=False)
+    distributed_bfs(bfs_be, roots[0], n, fetch=False, stats=False)
+    for r in roots:
         torch.cuda.synchronize()
         t = time.perf_counter()
         distributed_bfs(bfs_be, r, n, fetch=False, stats=False)
@@ -385,7 +383,7 @@ def run_partitioned(args, world, rank, local_rank):
         torch.cuda.synchronize()
         bt = time.perf_counter() - t
         t = time.perf_counter()
-        distributed_pagerank(pr_be, 0.85, n, args.pr_iters, fetch=False)
+        distributed_pagerank(pr_be, 0.85, n, args.pr_iters, fetch=False, layout=pr_layout)
         torch.cuda.synchronize()
         return bt, time.perf_counter() - t
 
@@ -426,6 +424,10 @@ def run_partitioned(args, world, rank, local_rank):
         line = result_line(args, world, scale, n, m, roots, elapsed, teps, hmean, pr_wall / upd, e_in,
                            roof_bfs, roof_pr, bfs_share, None, f"vertex-partition{world}")
         line["config"]["device_layout"] = "degree-grouped per rank" if args.layout else "global ids"
+        line["pagerank_exchange"] = {"hot_rows_per_rank": pr_layout[0], "active_span": pr_layout[1],
+                                     "bytes_per_rank_per_update": 8 * pr_layout[1]}
+        line["partition"] = {"ranges": "equal 64-aligned vertex ranges of the seeded relabel",
+                             "rank_entries": rank_entries, "entry_imbalance_max_over_mean": round(imbalance, 4)}
         line["sssp"] = sssp
         print(json.dumps(line), file=JSON_OUT, flush=True)
     dist.barrier()

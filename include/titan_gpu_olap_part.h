@@ -13,7 +13,8 @@
  *                         (nb_local, n_local/64 words each) into fb_global (n_global/64)
  *   BFS top-down level  : all-to-all of the "discovered" bitmap (disc, n_global/64 words,
  *                         slice r to rank r) into recv (nranks x n_local/64), then claim
- *   PageRank iteration  : all-gather of the owned contributions (n_local doubles)
+ *   PageRank iteration  : all-gather of the owned contributions (n_local doubles), or
+ *                         with tgo_part_pr_blocked two all-gathers into a hot-first layout
  *   every level         : all-reduce(SUM) of the two frontier counters
  * RCCL has no bitwise-OR reduction, hence slice exchanges instead of an all-reduce.
  *
@@ -108,9 +109,39 @@ int tgo_part_sssp_extract(tgo_ctx* ctx, int64_t thr, int64_t* counts);
 /* Local distances (TGO_DIST_ABSENT = unreached) and reached[2] = {vertices, pull entries}. */
 int tgo_part_sssp_end(tgo_ctx* ctx, int64_t* dist_local, int64_t* reached);
 
+/* PageRankVertexProgram (PageRankVertexProgram.java:75-95) on the owned rows.
+ * begin runs iteration 1 (contrib_local = (1/N) / edgeCount); every step is one rank update
+ * (iterations 2..max_iterations) from the gathered contributions; end returns the owned ranks
+ * (TGO_E_STATE unless exactly max_iterations - 1 steps ran: the rank property is written by
+ * the last step only).  Plain layout: contrib_global = the rank-major all-gather of every
+ * rank's contrib_local (n_global doubles). */
 int tgo_part_pr_begin(tgo_ctx* ctx, const tgo_pr_args* args, double* contrib_local);
 int tgo_part_pr_step(tgo_ctx* ctx, const double* contrib_global, double* contrib_local);
 int tgo_part_pr_end(tgo_ctx* ctx, double* pr_local);
+
+/* Device-resident level counts for the BFS / multi-source BFS steps: with dev_counts (a
+ * device int64[2]) set, the steps that return counts {next queue length, its push entries}
+ * write them there stream-ordered instead of synchronising into the host `counts` (which
+ * may then be NULL); the caller all-reduces the device buffer and reads it once per level.
+ * NULL restores host counts.  The SSSP steps always return host counts. */
+int tgo_part_device_counts(tgo_ctx* ctx, int64_t* dev_counts);
+
+/* Rows of this rank holding any entry (the degree-grouped layout puts the others last). */
+int tgo_part_active_rows(tgo_ctx* ctx, int64_t* n_active);
+
+/* Cache-blocked partitioned PageRank (the one-GPU ColdBlocks over the job's sources).
+ * active_span A = the maximum of every rank's tgo_part_active_rows; world = n_global/n_local.
+ * *hot_per_rank = H > 0: the gathered vector is hot-first, W*A doubles —
+ *     [rank 0 contrib_local[0,H)] ... [rank W-1 contrib_local[0,H)]
+ *     [rank 0 contrib_local[H,A)] ... [rank W-1 contrib_local[H,A)]
+ * i.e. two rank-major all-gathers (hot slices, then cold slices); rows >= A are no one's
+ * source and are not exchanged.  A step may then be split so the hot all-gather overlaps
+ * the cold phase: step_cold reads only the cold region of `gathered`, step_hot both.
+ * *hot_per_rank = 0: blocking not applicable (bothE load, TGO_PR_BLOCKED=0, too small) —
+ * keep the plain layout.  Building is host work on the downloaded in-lists (load time). */
+int tgo_part_pr_blocked(tgo_ctx* ctx, int32_t world, int64_t active_span, int64_t* hot_per_rank);
+int tgo_part_pr_step_cold(tgo_ctx* ctx, const double* gathered);
+int tgo_part_pr_step_hot(tgo_ctx* ctx, const double* gathered, double* contrib_local);
 
 /* Bench / test input: the edges of an RMAT stream (tgo_synth.h) with an endpoint in
  * [lo, hi).  *count = edges written; if capacity is too small, nothing is written,

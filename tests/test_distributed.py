@@ -266,6 +266,34 @@ class NumpyPartBackend:
                             for r in range(nseeds)])
         return reached, entries
 
+    pr_hot = 0          # blocked gathered layout: hot rows per rank (0 = plain layout)
+
+    def active_rows(self):
+        act = [v for v in range(self.n_local) if self.out[v] or self.inn[v]]
+        return act[-1] + 1 if act else 0
+
+    def pr_layout(self, world, span):
+        """tgo_part_pr_blocked's contract: the hot-first gathered layout of world * span."""
+        self.world, self.span = world, span
+        self.hot = min(self.pr_hot, span)
+        return self.hot
+
+    def _split(self, v):
+        from titan_amd.distributed import gathered_index
+        idx = gathered_index(np.array(self.inn[v], np.int64), self.n_local, self.world, self.hot, self.span)
+        return idx[idx < self.world * self.hot], idx[idx >= self.world * self.hot]
+
+    def pr_step_cold(self, gathered):
+        g = gathered.numpy()        # only the cold region is complete here (hot gather in flight)
+        self.csum = np.array([g[self._split(v)[1]].sum() for v in range(self.n_local)])
+
+    def pr_step_hot(self, gathered, contrib_local):
+        g = gathered.numpy()
+        s = np.array([g[self._split(v)[0]].sum() for v in range(self.n_local)]) + self.csum
+        self.pr = self.alpha * s + self.base
+        with np.errstate(divide="ignore"):
+            contrib_local.numpy()[:] = self.pr / self.ec
+
     def pr_begin(self, alpha, N, iters, contrib_local):
         self.alpha, self.base = alpha, (1 - alpha) / N
         self.ec = np.array([float(len(o)) for o in self.out])
@@ -319,10 +347,12 @@ def _worker(rank, world, port, scale, roots, out_q, alpha):
             dist.all_gather(full, torch.from_numpy(loc.astype(np.int64)))
             lv.append(torch.cat(full).numpy())
         res.setdefault("ms", []).append((lv, r))
-    pr = distributed_pagerank(be, 0.85, n, 10)
-    full = [torch.zeros(be.n_local, dtype=torch.float64) for _ in range(world)]
-    dist.all_gather(full, torch.from_numpy(pr))
-    res["pr"] = torch.cat(full).numpy()
+    for hot in (0, 16):             # plain rank-major all-gather; blocked hot-first layout
+        be.pr_hot = hot
+        pr = distributed_pagerank(be, 0.85, n, 10)
+        full = [torch.zeros(be.n_local, dtype=torch.float64) for _ in range(world)]
+        dist.all_gather(full, torch.from_numpy(pr))
+        res.setdefault("pr", []).append(torch.cat(full).numpy())
     if rank == 0:
         out_q.put(res)
     dist.barrier()
@@ -360,8 +390,9 @@ def test_distributed_bfs_and_pagerank_match_oracle(world, alpha):
             assert reached[i] == int((od != ABSENT).sum())
     opr, _ = og.pagerank(0.85, n, 10)
     fin = np.isfinite(opr)
-    assert np.array_equal(np.isfinite(res["pr"]), fin)
-    assert np.abs(res["pr"][fin] - opr[fin]).sum() <= 1e-6
+    for pr in res["pr"]:
+        assert np.array_equal(np.isfinite(pr), fin)
+        assert np.abs(pr[fin] - opr[fin]).sum() <= 1e-6
 
 
 def _sssp_worker(rank, world, port, scale, seeds, scope, deltas, out_q):
@@ -428,12 +459,15 @@ def _layout_worker(rank, world, port, scale, out_q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from titan_amd import rmat_edges
-    from titan_amd.distributed import all_gather_layout, partition_range
+    from titan_amd.distributed import all_gather_layout, entry_imbalance, partition_range, pick_roots_partitioned
     n = 1 << scale
     src, dst, _ = rmat_edges(scale, 8, seed=23)
     lo, hi = partition_range(n, world, rank)
     lay = all_gather_layout(src, dst, n, lo, hi, torch.device("cpu"), threads=2)
-    out_q.put((rank, lay))
+    mine = ((src >= lo) & (src < hi)) | ((dst >= lo) & (dst < hi))      # the rank's partition edges
+    roots = pick_roots_partitioned(n, src[mine], dst[mine], lo, hi, 16, 7, torch.device("cpu"))
+    owned = int(((src >= lo) & (src < hi)).sum() + ((dst >= lo) & (dst < hi)).sum())
+    out_q.put((rank, (lay, roots, entry_imbalance(owned, torch.device("cpu")))))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -455,9 +489,15 @@ def test_all_gathered_layout_is_a_rangewise_degree_order():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert np.array_equal(got[0], got[1])
-    lay = got[0].astype(np.int64)
+    (lay0, roots0, imb0), (lay1, roots1, imb1) = got[0], got[1]
+    assert np.array_equal(lay0, lay1)
+    lay = lay0.astype(np.int64)
     src, dst, _ = rmat_edges(scale, 8, seed=23)
+    from titan_amd import pick_roots
+    assert roots0 == roots1 == [int(x) for x in pick_roots(n, src, dst, 16, seed=7)]   # the one-GPU bench's roots
+    ent = [int(((src >= lo) & (src < hi)).sum() + ((dst >= lo) & (dst < hi)).sum())
+           for lo, hi in (partition_range(n, world, r) for r in range(world))]
+    assert imb0 == imb1 and imb0[0] == ent and abs(imb0[1] - max(ent) / np.mean(ent)) < 1e-12
     deg = np.bincount(src, minlength=n) + np.bincount(dst, minlength=n)
     bucket = np.where(deg == 0, 0, 1 + np.floor(2.0 * np.log2(np.maximum(deg, 1))).astype(np.int64))
     for r in range(world):

@@ -248,3 +248,111 @@ def test_partitioned_bfs_and_pagerank(world, layout):
     fin = np.isfinite(opr)
     assert np.array_equal(np.isfinite(pr), fin)
     assert np.abs(pr[fin] - opr[fin]).sum() <= 1e-6
+
+
+def run_pagerank_blocked(backends, n, iters):
+    """distributed_pagerank's blocked protocol in-process: agree on the active span, build
+    the hot-first gathered layout, cold slices gathered before step_cold, hot slices before
+    step_hot."""
+    world = len(backends)
+    span = max(b.active_rows() for b in backends)
+    hots = {b.pr_layout(world, span) for b in backends}
+    assert len(hots) == 1
+    hot = hots.pop()
+    cl = [b.tensor(b.n_local, torch.float64) for b in backends]
+    cg = [b.tensor(world * span, torch.float64) for b in backends]
+    for b, c in zip(backends, cl):
+        b.pr_begin(0.85, n, iters, c)
+    for _ in range(2, iters + 1):
+        torch.cuda.synchronize()
+        cold = torch.cat([c[hot:span] for c in cl])
+        for t in cg:
+            t[world * hot:].copy_(cold)
+            t[:world * hot].fill_(float("nan"))          # the hot gather is still in flight
+        torch.cuda.synchronize()
+        for b, gg in zip(backends, cg):
+            b.pr_step_cold(gg)
+        torch.cuda.synchronize()
+        hotv = torch.cat([c[:hot] for c in cl])
+        for t in cg:
+            t[:world * hot].copy_(hotv)
+        torch.cuda.synchronize()
+        for b, c, gg in zip(backends, cl, cg):
+            b.pr_step_hot(gg, c)
+    return hot, span, np.concatenate([b.pr_end(True) for b in backends])
+
+
+@pytest.mark.parametrize("layout", [False, True])
+@pytest.mark.parametrize("world", [1, 2, 4])
+def test_partitioned_pagerank_cache_blocked(world, layout, monkeypatch):
+    """tgo_part_pr_blocked: the owned in-lists re-expressed in the hot-first gathered index
+    space and cache-blocked (small hot set / segments so every rank has hot rows, cold
+    pieces in several segments and entry-less rows past the span)."""
+    monkeypatch.setenv("TGO_PR_HOT", "512")
+    monkeypatch.setenv("TGO_PR_SEG", "256")
+    scale = 12
+    n = 1 << scale
+    src, dst, _ = rmat_edges(scale, 16, seed=37)
+    backends = make_backends(world, n, src, dst, L.SCOPE_IN_E, layout=layout)
+    og = fr.OracleGraph.from_edges(n, src, dst)
+    for iters in (2, 10):
+        hot, span, pr = run_pagerank_blocked(backends, n, iters)
+        assert hot == max(64, 512 // world // 64 * 64)
+        if layout:
+            assert span < n // world                    # entry-less rows are not exchanged
+        opr, _ = og.pagerank(0.85, n, iters)
+        fin = np.isfinite(opr)
+        assert np.array_equal(np.isfinite(pr), fin)
+        assert np.abs(pr[fin] - opr[fin]).sum() <= 1e-6
+    with pytest.raises(Exception):                      # rank property only after the last step
+        backends[0].pr_begin(0.85, n, 5, backends[0].tensor(backends[0].n_local, torch.float64))
+        backends[0].pr_end(True)
+
+
+def test_drivers_on_a_real_world1_group(monkeypatch):
+    """The real drivers (titan_amd.distributed) on a one-rank RCCL group: device-resident
+    level counts (tgo_part_device_counts) for BFS / multi-source BFS, and the cache-blocked
+    PageRank exchange with the hot all-gather overlapping the cold phase."""
+    import socket
+    import torch.distributed as dist
+    from titan_amd.distributed import (distributed_bfs, distributed_msbfs, distributed_pagerank, pagerank_layout)
+    monkeypatch.setenv("TGO_PR_HOT", "512")
+    monkeypatch.setenv("TGO_PR_SEG", "256")
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        scale = 12
+        n = 1 << scale
+        src, dst, _ = rmat_edges(scale, 16, seed=41)
+        lay = local_layout(src, dst, n, 0, n)
+        st = exchange_stream()
+        bfs_be = HipPartBackend(Engine(stream=st).load_partition(n, 0, n, src, dst, L.SCOPE_BOTH_E, apply_cap=False,
+                                                                  layout=lay), n, 0, n, device_counts=True)
+        og = fr.OracleGraph.from_edges(n, src, dst)
+        ids = (np.arange(n, dtype=np.int64) + 1) << 3
+        seeds = [int(src[0]), int(dst[7]), int(src[300])]
+        for seed in seeds:
+            od, _ = og.shortest_distance(int(ids[seed]), n, 2)
+            d, reached, _ = distributed_bfs(bfs_be, seed, n)
+            assert np.array_equal(d, od)
+            assert reached[0] == int((od != ABSENT).sum())
+        r, _, _ = distributed_msbfs(bfs_be, seeds, n)
+        for i, seed in enumerate(seeds):
+            od, _ = og.shortest_distance(int(ids[seed]), n, 2)
+            assert np.array_equal(bfs_be.ms_levels(i), od)
+            assert r[i] == int((od != ABSENT).sum())
+        pr_be = HipPartBackend(Engine(stream=st).load_partition(n, 0, n, src, dst, L.SCOPE_IN_E, apply_cap=False,
+                                                                 layout=lay), n, 0, n)
+        hot, span = pagerank_layout(pr_be)
+        assert hot == 512 and span < n
+        pr = distributed_pagerank(pr_be, 0.85, n, 10, layout=(hot, span))
+        opr, _ = og.pagerank(0.85, n, 10)
+        fin = np.isfinite(opr)
+        assert np.array_equal(np.isfinite(pr), fin)
+        assert np.abs(pr[fin] - opr[fin]).sum() <= 1e-6
+    finally:
+        dist.destroy_process_group()

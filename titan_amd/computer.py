@@ -155,6 +155,12 @@ class ShortestDistanceVertexProgram(VertexProgram):
             return self
 
         def deltaStepping(self):  # noqa: N802
+            """Converged shortest distances by delta-stepping (TGO_SSSP_DELTA) instead of
+            maxDepth Jacobi supersteps.  Equal to ShortestDistanceVertexProgram's result only
+            when every shortest path has at most maxDepth hops: the reference stops after
+            maxDepth supersteps (ShortestDistanceVertexProgram.java:128-130) and leaves longer
+            paths at their bounded distance; this mode does not check the hop count.  Use the
+            default (hop-bounded) mode for exact reference semantics at small maxDepth."""
             self._mode = L.SSSP_DELTA
             return self
 

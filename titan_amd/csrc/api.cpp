@@ -5,6 +5,7 @@
 // each iteration is one or two kernel launches over the device-resident adjacency, and
 // only the frontier is touched for BFS/SSSP.
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -38,8 +39,14 @@ struct tgo_ctx {
     std::vector<void*> allocs;
     int part_cur = 0;           // partitioned BFS: queue buffer holding the frontier
     int64_t part_qlen = 0;      // its length
+    int64_t* part_dcounts = nullptr;    // caller's device counts (tgo_part_device_counts)
+    int64_t* part_qlen_dev = nullptr;   // device copy of the queue length (lazy host read)
+    bool part_qlen_stale = false;       // part_qlen must be read from part_qlen_dev
     double part_alpha = 0.85, part_base = 0.0;
-    int32_t part_pr_iter = 0;
+    int32_t part_pr_iter = 0;   // partitioned PageRank: iteration reached / program length
+    int32_t part_pr_iters = 0;
+    int32_t part_pr_world = 0;  // blocked gathered layout (tgo_part_pr_blocked): world, H, A
+    int64_t part_pr_hot = 0, part_pr_span = 0;
     int64_t part_relaxed = 0;   // partitioned SSSP: entries relaxed, phases
     int32_t part_phases = 0;
     int64_t pv_max_out = 0, pv_max_in = 0;   // largest OUT / IN list of a vertex cut
@@ -124,6 +131,66 @@ PrTuning pr_tuning() {
     return t;
 }
 
+// CSR-adaptive row blocks of one CSR; `pack` (optional) source-sorts and packs the CSR's
+// tiles first (spmv.hip gather_short_packed).
+hipError_t upload_row_blocks(tgo_ctx* ctx, const std::vector<int64_t>& off, RowBlocks& rb,
+                             std::vector<int32_t>* pack = nullptr, bool* packed = nullptr) {
+    std::vector<int64_t> blk, crow, cbeg, cend, lrow, lch;
+    build_row_blocks(off, kTile, kMaxRows, blk, crow, cbeg, cend, lrow, lch);
+    if (pack) *packed = pack_tiles(off, *pack, blk, cbeg, cend, kTile, threads_of(ctx));
+    rb.nblocks = static_cast<int64_t>(blk.size()) - 1;
+    rb.nchunks = static_cast<int64_t>(crow.size());
+    rb.nlong = static_cast<int64_t>(lrow.size());
+    hipError_t e;
+    if ((e = upload(ctx, rb.blk, blk)) != hipSuccess) return e;
+    if ((e = upload(ctx, rb.chunk_row, crow)) != hipSuccess) return e;
+    if ((e = upload(ctx, rb.chunk_beg, cbeg)) != hipSuccess) return e;
+    if ((e = upload(ctx, rb.chunk_end, cend)) != hipSuccess) return e;
+    if ((e = upload(ctx, rb.long_row, lrow)) != hipSuccess) return e;
+    if ((e = upload(ctx, rb.long_chunk, lch)) != hipSuccess) return e;
+    return hipSuccess;
+}
+
+// Cache-blocked PageRank in-lists of the rows [0, n_rows) (rows past n_rows have no entries)
+// over sources [0, n_src): build on the host, upload into cb.
+int upload_cold_blocks(tgo_ctx* ctx, const std::vector<int64_t>& off, const std::vector<int32_t>& adj,
+                       int64_t n_src, int64_t hot, int64_t n_rows, ColdBlocks& cb, bool& ready) {
+    cb = ColdBlocks();
+    ready = false;
+    HostColdBlocks hc;
+    if (!build_cold_blocks(off, adj, n_src, hot, env_i64("TGO_PR_SEG", kPrSegDefault), kTile, kMaxRows,
+                           threads_of(ctx), env_i64("TGO_PR_CPACK", 1) != 0, hc))
+        return TGO_OK;                                    // too small to block: plain gather
+    cb.hot = hc.hot;
+    cb.seg = hc.seg;
+    cb.npieces = static_cast<int64_t>(hc.cpid.size());
+    cb.nblocks = static_cast<int64_t>(hc.bbeg.size());
+    cb.max_xcd_blocks = hc.max_xcd_blocks;
+    cb.xbase = hc.xbase;
+    cb.n_rows = n_rows;
+    const std::vector<int64_t> hoff_act(hc.hoff.begin(), hc.hoff.begin() + n_rows + 1);
+    HIP_TRY(upload_row_blocks(ctx, hoff_act, cb.rb_hot, env_i64("TGO_PR_PACK", 1) ? &hc.hadj : nullptr, &cb.packed));
+    HIP_TRY(upload(ctx, cb.hcsr.off, hc.hoff));
+    HIP_TRY(upload(ctx, cb.hcsr.adj, hc.hadj));
+    cb.hcsr.nnz = static_cast<int64_t>(hc.hadj.size());
+    HIP_TRY(upload(ctx, cb.poff, hc.poff));
+    HIP_TRY(upload(ctx, cb.cadj, hc.cadj));
+    HIP_TRY(upload(ctx, cb.cptr, hc.cptr));
+    HIP_TRY(upload(ctx, cb.cpid, hc.cpid));
+    HIP_TRY(upload(ctx, cb.bbeg, hc.bbeg));
+    HIP_TRY(upload(ctx, cb.bend, hc.bend));
+    HIP_TRY(upload(ctx, cb.xblk, hc.xblk));
+    HIP_TRY(upload(ctx, cb.bsrc, hc.bsrc));
+    cb.cpacked = hc.cpacked;
+    HIP_TRY(dev_alloc(ctx, cb.partial, cb.npieces));
+    HIP_TRY(dev_alloc(ctx, cb.csum, std::max<int64_t>(cb.n_rows, 1)));
+    HIP_TRY(hipMemset(cb.csum, 0, std::max<int64_t>(cb.n_rows, 1) * sizeof(double)));
+    cb.n_crows = static_cast<int64_t>(hc.crow.size());
+    HIP_TRY(upload(ctx, cb.crow, hc.crow));
+    ready = true;
+    return TGO_OK;
+}
+
 int upload_graph(tgo_ctx* ctx, HostGraph& h, bool allow_segments = true) {
     DevGraph& g = ctx->g;
     g.n = h.n;
@@ -152,26 +219,8 @@ int upload_graph(tgo_ctx* ctx, HostGraph& h, bool allow_segments = true) {
     HIP_TRY(up(h.in, g.in));
     if (h.has_transpose) HIP_TRY(up(h.push_t, g.push_t));
     // CSR-adaptive blocks for the two pull gathers (walk counts: out; PageRank: in).
-    // CSR-adaptive blocks; `pack` (optional) source-sorts and packs the CSR's tiles first
-    auto blocks = [&](const std::vector<int64_t>& off, RowBlocks& rb, std::vector<int32_t>* pack = nullptr,
-                      bool* packed = nullptr) -> hipError_t {
-        std::vector<int64_t> blk, crow, cbeg, cend, lrow, lch;
-        build_row_blocks(off, kTile, kMaxRows, blk, crow, cbeg, cend, lrow, lch);
-        if (pack) *packed = pack_tiles(off, *pack, blk, cbeg, cend, kTile, threads_of(ctx));
-        rb.nblocks = static_cast<int64_t>(blk.size()) - 1;
-        rb.nchunks = static_cast<int64_t>(crow.size());
-        rb.nlong = static_cast<int64_t>(lrow.size());
-        hipError_t e;
-        if ((e = upload(ctx, rb.blk, blk)) != hipSuccess) return e;
-        if ((e = upload(ctx, rb.chunk_row, crow)) != hipSuccess) return e;
-        if ((e = upload(ctx, rb.chunk_beg, cbeg)) != hipSuccess) return e;
-        if ((e = upload(ctx, rb.chunk_end, cend)) != hipSuccess) return e;
-        if ((e = upload(ctx, rb.long_row, lrow)) != hipSuccess) return e;
-        if ((e = upload(ctx, rb.long_chunk, lch)) != hipSuccess) return e;
-        return hipSuccess;
-    };
-    HIP_TRY(blocks(h.out.off, g.rb_out));
-    HIP_TRY(blocks(h.in.off, g.rb_in));
+    HIP_TRY(upload_row_blocks(ctx, h.out.off, g.rb_out));
+    HIP_TRY(upload_row_blocks(ctx, h.in.off, g.rb_in));
     g.rb_out_ready = g.rb_in_ready = true;
     g.push_ws = DevCsr();
     g.push_ws_ready = false;
@@ -184,41 +233,11 @@ int upload_graph(tgo_ctx* ctx, HostGraph& h, bool allow_segments = true) {
     g.cold_in = ColdBlocks();
     g.cold_in_ready = false;
     if (allow_segments && h.scope != TGO_SCOPE_BOTH_E && env_i64("TGO_PR_BLOCKED", 1) != 0) {
-        HostColdBlocks hc;
-        if (build_cold_blocks(h.in.off, h.in.adj, h.n, env_i64("TGO_PR_HOT", kPrHotDefault),
-                              env_i64("TGO_PR_SEG", kPrSegDefault), kTile, kMaxRows, threads_of(ctx),
-                              env_i64("TGO_PR_CPACK", 1) != 0, hc)) {
-            ColdBlocks& cb = g.cold_in;
-            cb.hot = hc.hot;
-            cb.seg = hc.seg;
-            cb.npieces = static_cast<int64_t>(hc.cpid.size());
-            cb.nblocks = static_cast<int64_t>(hc.bbeg.size());
-            cb.max_xcd_blocks = hc.max_xcd_blocks;
-            cb.xbase = hc.xbase;
-            // rows >= n_active have no entries at all: the hot pass skips them (their rank
-            // after any update is (1-a)/N, written once at the end of the program)
-            cb.n_rows = g.n_active;
-            const std::vector<int64_t> hoff_act(hc.hoff.begin(), hc.hoff.begin() + cb.n_rows + 1);
-            HIP_TRY(blocks(hoff_act, cb.rb_hot, env_i64("TGO_PR_PACK", 1) ? &hc.hadj : nullptr, &cb.packed));
-            HIP_TRY(upload(ctx, cb.hcsr.off, hc.hoff));
-            HIP_TRY(upload(ctx, cb.hcsr.adj, hc.hadj));
-            cb.hcsr.nnz = static_cast<int64_t>(hc.hadj.size());
-            HIP_TRY(upload(ctx, cb.poff, hc.poff));
-            HIP_TRY(upload(ctx, cb.cadj, hc.cadj));
-            HIP_TRY(upload(ctx, cb.cptr, hc.cptr));
-            HIP_TRY(upload(ctx, cb.cpid, hc.cpid));
-            HIP_TRY(upload(ctx, cb.bbeg, hc.bbeg));
-            HIP_TRY(upload(ctx, cb.bend, hc.bend));
-            HIP_TRY(upload(ctx, cb.xblk, hc.xblk));
-            HIP_TRY(upload(ctx, cb.bsrc, hc.bsrc));
-            cb.cpacked = hc.cpacked;
-            HIP_TRY(dev_alloc(ctx, cb.partial, cb.npieces));
-            HIP_TRY(dev_alloc(ctx, cb.csum, std::max<int64_t>(cb.n_rows, 1)));
-            HIP_TRY(hipMemset(cb.csum, 0, std::max<int64_t>(cb.n_rows, 1) * sizeof(double)));
-            cb.n_crows = static_cast<int64_t>(hc.crow.size());
-            HIP_TRY(upload(ctx, cb.crow, hc.crow));
-            g.cold_in_ready = true;
-        }
+        // rows >= n_active have no entries at all: the hot pass skips them (their rank
+        // after any update is (1-a)/N, written once at the end of the program)
+        if (int rc = upload_cold_blocks(ctx, h.in.off, h.in.adj, h.n, env_i64("TGO_PR_HOT", kPrHotDefault), g.n_active,
+                                        g.cold_in, g.cold_in_ready))
+            return rc;
     }
     // scratch
     Scratch& s = ctx->sc;
@@ -1027,6 +1046,9 @@ int tgo_load_partition_layout(tgo_ctx* ctx, int64_t n_global, int64_t lo, int64_
     rc = upload_graph(ctx, h, false);     // partitioned PageRank gathers global ids: plain CSR
     if (rc) return rc;
     ctx->g.partitioned = true;
+    ctx->part_pr_world = 0;
+    ctx->part_pr_hot = ctx->part_pr_span = 0;
+    ctx->part_pr_iter = ctx->part_pr_iters = 0;
     ctx->g.lo = lo;
     ctx->g.n_global = n_global;
     ctx->st.load_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -1040,14 +1062,54 @@ static int part_check(tgo_ctx* ctx) {
     return TGO_OK;
 }
 
-static int part_counts(tgo_ctx* ctx, int64_t* counts) {
+// Entry points that leave work queued: on a ctx-owned stream the caller cannot order its
+// collectives after that work, so finish it before returning; on the caller's stream the
+// work stays stream-ordered (the caller's collectives follow it on the same stream).
+static int part_done(tgo_ctx* ctx) {
+    if (ctx->own_stream) HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return TGO_OK;
+}
+
+// Level counters {next queue length, its push entries}.  Host mode: read (one stream sync)
+// into counts.  Device mode (tgo_part_device_counts): published to the caller's device
+// buffer without a sync — the caller all-reduces it and reads the global counts once; the
+// local queue length is fetched lazily by the next call that needs it (part_qlen_now).
+static int part_counts(tgo_ctx* ctx, int64_t* counts, bool device_ok = true) {
+    if (ctx->part_dcounts && device_ok) {
+        HIP_TRY(k_publish_counts(ctx->sc.cnt, ctx->part_dcounts, ctx->part_qlen_dev, ctx->stream));
+        ctx->part_qlen_stale = true;
+        return part_done(ctx);
+    }
     int rc = read_counters(ctx);
     if (rc) return rc;
     ctx->part_qlen = static_cast<int64_t>(ctx->sc.hcnt->qlen);
+    ctx->part_qlen_stale = false;
     if (counts) {
         counts[0] = ctx->part_qlen;
         counts[1] = static_cast<int64_t>(ctx->sc.hcnt->mf);
     }
+    return TGO_OK;
+}
+
+static int part_qlen_now(tgo_ctx* ctx, int64_t& q) {
+    if (ctx->part_qlen_stale) {
+        HIP_TRY(hipMemcpyAsync(&ctx->part_qlen, ctx->part_qlen_dev, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        ctx->part_qlen_stale = false;
+    }
+    q = ctx->part_qlen;
+    return TGO_OK;
+}
+
+int tgo_part_device_counts(tgo_ctx* ctx, int64_t* dev_counts) {
+    int rc = part_check(ctx);
+    if (rc) return rc;
+    if (dev_counts && !ctx->part_qlen_dev) HIP_TRY(dev_alloc(ctx, ctx->part_qlen_dev, 1));
+    if (!dev_counts && ctx->part_qlen_stale) {
+        int64_t q;
+        if ((rc = part_qlen_now(ctx, q))) return rc;
+    }
+    ctx->part_dcounts = dev_counts;
     return TGO_OK;
 }
 
@@ -1067,6 +1129,7 @@ int tgo_part_bfs_begin(tgo_ctx* ctx, int64_t seed_global, uint64_t* nb_local, in
     HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
     ctx->part_cur = 0;
     ctx->part_qlen = 0;
+    ctx->part_qlen_stale = false;
     int64_t deg = 0;
     int64_t seed = seed_global - g.lo;
     if (seed >= 0 && seed < n) {
@@ -1081,14 +1144,6 @@ int tgo_part_bfs_begin(tgo_ctx* ctx, int64_t seed_global, uint64_t* nb_local, in
     return TGO_OK;
 }
 
-// Entry points that leave work queued: on a ctx-owned stream the caller cannot order its
-// collectives after that work, so finish it before returning; on the caller's stream the
-// work stays stream-ordered (the caller's collectives follow it on the same stream).
-static int part_done(tgo_ctx* ctx) {
-    if (ctx->own_stream) HIP_TRY(hipStreamSynchronize(ctx->stream));
-    return TGO_OK;
-}
-
 int tgo_part_bfs_td(tgo_ctx* ctx, int32_t level, uint64_t* disc_global) {
     int rc = part_check(ctx);
     if (rc) return rc;
@@ -1097,7 +1152,9 @@ int tgo_part_bfs_td(tgo_ctx* ctx, int32_t level, uint64_t* disc_global) {
     Scratch& s = ctx->sc;
     hipStream_t st = ctx->stream;
     const View push = push_view(g, TGO_SCOPE_BOTH_E);
-    if (ctx->part_qlen > 0) {
+    int64_t qlen = 0;
+    if ((rc = part_qlen_now(ctx, qlen))) return rc;
+    if (qlen > 0) {
         if ((rc = scan_frontier(ctx, ctx->part_qlen))) return rc;
         HIP_TRY(k_part_td_mark(push, s.q[ctx->part_cur], s.qpre, ctx->part_qlen, disc_global, s.vb, g.lo, g.n, st));
     }
@@ -1194,6 +1251,7 @@ int tgo_part_ms_begin(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, uint64
     HIP_TRY(k_ms_seed(s.ms_seeds, nseeds, s.ms_vis, fr_local, st));
     ctx->part_cur = 0;
     ctx->part_qlen = static_cast<int64_t>(uniq.size());
+    ctx->part_qlen_stale = false;
     int64_t mf = 0;
     if (!uniq.empty()) {
         HIP_TRY(hipMemcpyAsync(s.q[0], uniq.data(), uniq.size() * sizeof(int32_t), hipMemcpyHostToDevice, st));
@@ -1233,7 +1291,9 @@ int tgo_part_ms_push(tgo_ctx* ctx, int32_t level, const uint64_t* fr_local, uint
     (void)level;
     DevGraph& g = ctx->g;
     Scratch& s = ctx->sc;
-    if (ctx->part_qlen > 0) {
+    int64_t qlen = 0;
+    if ((rc = part_qlen_now(ctx, qlen))) return rc;
+    if (qlen > 0) {
         if ((rc = scan_frontier(ctx, ctx->part_qlen))) return rc;
         HIP_TRY(k_ms_push(push_view(g, TGO_SCOPE_BOTH_E), s.q[ctx->part_cur], s.qpre, ctx->part_qlen, fr_local,
                           nullptr, cand_global, ctx->stream));
@@ -1348,6 +1408,75 @@ int tgo_part_ms_levels(tgo_ctx* ctx, int32_t source, int64_t* dist_local) {
     return TGO_OK;
 }
 
+int tgo_part_active_rows(tgo_ctx* ctx, int64_t* n_active) {
+    int rc = part_check(ctx);
+    if (rc) return rc;
+    if (!n_active) return fail(ctx, TGO_E_INVALID, "null argument");
+    *n_active = ctx->g.n_active;
+    return TGO_OK;
+}
+
+// Cache-blocked partitioned PageRank.  The gathered contribution vector is laid out hot-first
+// across ranks: [rank 0 rows 0..H) ... [rank W-1 rows 0..H) | [rank 0 rows H..A) ... — the
+// degree-grouped layout puts each rank's hottest rows first and its entry-less rows last, so
+// the first W*H sources are the job's hot set and rows >= A are never anyone's source.  The
+// owned in-lists are re-expressed in that index space and cache-blocked as on one GPU.
+int tgo_part_pr_blocked(tgo_ctx* ctx, int32_t world, int64_t active_span, int64_t* hot_per_rank) {
+    int rc = part_check(ctx);
+    if (rc) return rc;
+    DevGraph& g = ctx->g;
+    const int64_t nl = g.n;
+    if (!hot_per_rank || world < 1 || g.n_global != static_cast<int64_t>(world) * nl)
+        return fail(ctx, TGO_E_INVALID, "tgo_part_pr_blocked: world must equal n_global / n_local");
+    if (active_span < g.n_active || active_span > nl)
+        return fail(ctx, TGO_E_INVALID, "tgo_part_pr_blocked: active_span must cover every rank's active rows");
+    *hot_per_rank = 0;
+    if (g.scope == TGO_SCOPE_BOTH_E || env_i64("TGO_PR_BLOCKED", 1) == 0) {
+        ctx->part_pr_world = 0;
+        return TGO_OK;                                  // plain layout: one rank-major all-gather
+    }
+    int64_t H = env_i64("TGO_PR_HOT", kPrHotDefault) / world;
+    H = std::min(active_span, std::max<int64_t>(64, H / 64 * 64));
+    if (ctx->part_pr_world == world && ctx->part_pr_hot == H && ctx->part_pr_span == active_span) {
+        *hot_per_rank = H;
+        return TGO_OK;                                  // already built for this layout
+    }
+    const int64_t A = active_span, W = world;
+    std::vector<int64_t> off(nl + 1);
+    std::vector<int32_t> adj(static_cast<size_t>(g.in.nnz));
+    HIP_TRY(hipMemcpy(off.data(), g.in.off, (nl + 1) * sizeof(int64_t), hipMemcpyDeviceToHost));
+    if (g.in.nnz) HIP_TRY(hipMemcpy(adj.data(), g.in.adj, g.in.nnz * sizeof(int32_t), hipMemcpyDeviceToHost));
+    std::atomic<bool> bad{false};
+    const int threads = threads_of(ctx);
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads; ++t)
+        th.emplace_back([&, t] {
+            const size_t m = adj.size(), a = m * t / threads, b = m * (t + 1) / threads;
+            for (size_t k = a; k < b; ++k) {
+                const int64_t u = adj[k], r = u / nl, o = u % nl;
+                if (o >= A) { bad = true; continue; }
+                adj[k] = static_cast<int32_t>(o < H ? r * H + o : W * H + r * (A - H) + (o - H));
+            }
+        });
+    for (auto& x : th) x.join();
+    if (bad) return fail(ctx, TGO_E_INVALID, "tgo_part_pr_blocked: a source row lies beyond active_span");
+    bool ready = false;
+    if ((rc = upload_cold_blocks(ctx, off, adj, W * A, W * H, g.n_active, g.cold_in, ready))) return rc;
+    g.cold_in_ready = ready;
+    if (!ready) { ctx->part_pr_world = 0; return TGO_OK; }
+    Scratch& s = ctx->sc;
+    if (g.cold_in.rb_hot.nchunks > s.partial_cap) {
+        s.partial_cap = g.cold_in.rb_hot.nchunks;
+        HIP_TRY(dev_alloc(ctx, s.partial, s.partial_cap));
+    }
+    ctx->part_pr_world = world;
+    ctx->part_pr_hot = H;
+    ctx->part_pr_span = A;
+    ctx->st.device_bytes = ctx->dev_bytes;
+    *hot_per_rank = H;
+    return TGO_OK;
+}
+
 int tgo_part_pr_begin(tgo_ctx* ctx, const tgo_pr_args* a, double* contrib_local) {
     int rc = part_check(ctx);
     if (rc) return rc;
@@ -1357,28 +1486,69 @@ int tgo_part_pr_begin(tgo_ctx* ctx, const tgo_pr_args* a, double* contrib_local)
     const double N = static_cast<double>(a->vertex_count);
     ctx->part_alpha = a->alpha;
     ctx->part_base = (1.0 - a->alpha) / N;
+    ctx->part_pr_iter = 1;
+    ctx->part_pr_iters = a->max_iterations;
     HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
     // iteration 1 (PageRankVertexProgram.java:78-83) on the owned rows
     HIP_TRY(k_pr_init(g.out, s.vec[0], contrib_local, reinterpret_cast<double*>(s.dist), 1.0 / N, g.n, ctx->stream));
     return part_done(ctx);
 }
 
+static bool part_pr_blocked_ready(const tgo_ctx* ctx) { return ctx->part_pr_world > 0 && ctx->g.cold_in_ready; }
+
+// the PAGE_RANK property is only read after the last superstep: write it there
+static double* part_pr_out(tgo_ctx* ctx) {
+    return ctx->part_pr_iter + 1 == ctx->part_pr_iters ? reinterpret_cast<double*>(ctx->sc.dist) : nullptr;
+}
+
+int tgo_part_pr_step_cold(tgo_ctx* ctx, const double* gathered) {
+    int rc = part_check(ctx);
+    if (rc) return rc;
+    if (!part_pr_blocked_ready(ctx)) return fail(ctx, TGO_E_STATE, "tgo_part_pr_step_cold needs tgo_part_pr_blocked");
+    HIP_TRY(k_pr_cold_phase(ctx->g.cold_in, gathered, ctx->stream));
+    return part_done(ctx);
+}
+
+int tgo_part_pr_step_hot(tgo_ctx* ctx, const double* gathered, double* contrib_local) {
+    int rc = part_check(ctx);
+    if (rc) return rc;
+    if (!part_pr_blocked_ready(ctx)) return fail(ctx, TGO_E_STATE, "tgo_part_pr_step_hot needs tgo_part_pr_blocked");
+    if (ctx->part_pr_iter >= ctx->part_pr_iters) return fail(ctx, TGO_E_STATE, "PageRank program already complete");
+    Scratch& s = ctx->sc;
+    HIP_TRY(k_pr_hot_phase(ctx->g.cold_in, gathered, s.vec[0], part_pr_out(ctx), contrib_local, s.partial,
+                           ctx->part_alpha, ctx->part_base, ctx->stream));
+    ++ctx->part_pr_iter;
+    return part_done(ctx);
+}
+
 int tgo_part_pr_step(tgo_ctx* ctx, const double* contrib_global, double* contrib_local) {
     int rc = part_check(ctx);
     if (rc) return rc;
+    if (part_pr_blocked_ready(ctx)) {
+        if ((rc = tgo_part_pr_step_cold(ctx, contrib_global))) return rc;
+        return tgo_part_pr_step_hot(ctx, contrib_global, contrib_local);
+    }
+    if (ctx->part_pr_iter >= ctx->part_pr_iters) return fail(ctx, TGO_E_STATE, "PageRank program already complete");
     DevGraph& g = ctx->g;
     Scratch& s = ctx->sc;
     // owned rows gather over their IN lists (global source ids) from the gathered vector
-    HIP_TRY(k_pr_iter(g.in, g.rb_in, contrib_global, s.vec[0], reinterpret_cast<double*>(s.dist), contrib_local,
-                      s.partial, ctx->part_alpha, ctx->part_base, g.n, PrTuning{}, ctx->stream));
+    HIP_TRY(k_pr_iter(g.in, g.rb_in, contrib_global, s.vec[0], part_pr_out(ctx), contrib_local, s.partial,
+                      ctx->part_alpha, ctx->part_base, g.n, PrTuning{}, ctx->stream));
+    ++ctx->part_pr_iter;
     return part_done(ctx);
 }
 
 int tgo_part_pr_end(tgo_ctx* ctx, double* pr_local) {
     int rc = part_check(ctx);
     if (rc) return rc;
+    if (ctx->part_pr_iter != ctx->part_pr_iters)
+        return fail(ctx, TGO_E_STATE, "partitioned PageRank ended before its last iteration");
     DevGraph& g = ctx->g;
     Scratch& s = ctx->sc;
+    double* pr = reinterpret_cast<double*>(s.dist);
+    // blocked updates skip the entry-less rows: their rank after any update is (1-a)/N
+    if (part_pr_blocked_ready(ctx) && ctx->part_pr_iters >= 2 && g.cold_in.n_rows < g.n)
+        HIP_TRY(k_fill_f64(pr + g.cold_in.n_rows, ctx->part_base, g.n - g.cold_in.n_rows, ctx->stream));
     HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
     if (pr_local) {     // back to row order
         HIP_TRY(k_unpermute_i64(s.dist, g.perm, s.msg, g.n, ctx->stream));
@@ -1418,6 +1588,7 @@ int tgo_part_sssp_begin(tgo_ctx* ctx, int64_t seed_global, int64_t delta, int64_
     HIP_TRY(hipMemsetAsync(s.ds_rmark, 0, (g.n_global / 64 + 1) * 8, st));
     ctx->part_cur = 0;
     ctx->part_qlen = 0;
+    ctx->part_qlen_stale = false;
     ctx->part_relaxed = 0;
     ctx->part_phases = 0;
     int64_t seed = seed_global - g.lo;
@@ -1490,6 +1661,7 @@ int tgo_part_sssp_apply(tgo_ctx* ctx, int64_t thr, const int64_t* recv, int64_t 
     if (ctx->part_qlen > 0) ctx->part_relaxed += static_cast<int64_t>(s.hcnt->red[1]);
     ctx->part_cur ^= 1;
     ctx->part_qlen = static_cast<int64_t>(s.hcnt->qlen);
+    ctx->part_qlen_stale = false;
     ++ctx->part_phases;
     if (counts) {
         counts[0] = ctx->part_qlen;
@@ -1521,7 +1693,7 @@ int tgo_part_sssp_extract(tgo_ctx* ctx, int64_t thr, int64_t* counts) {
     hipStream_t st = ctx->stream;
     HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
     HIP_TRY(k_ds_extract(push_view(g, g.scope), s.vb, g.n, s.dist, thr, s.q[ctx->part_cur], s.qdeg, s.cnt, st));
-    return part_counts(ctx, counts);
+    return part_counts(ctx, counts, false);   // the SSSP driver reads counts on the host
 }
 
 int tgo_part_sssp_end(tgo_ctx* ctx, int64_t* dist_local, int64_t* reached) {

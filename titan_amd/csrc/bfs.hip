@@ -15,79 +15,13 @@
 // Wave = 64 lanes; ballots are 64-bit.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
-#include "engine.hpp"
+#include "frontier.hpp"
 
 namespace tgo {
 
 namespace {
 
-constexpr int kBlock = 256;
-constexpr int kEdgesPerThread = 8;
-constexpr int kTileEdges = kBlock * kEdgesPerThread;   // 2048 edges per block tile
-constexpr int kLdsEntries = kTileEdges + 2;
 constexpr int64_t kSerialScan = 32;    // bottom-up: longer lists are scanned by the whole wave
-
-__device__ __forceinline__ int lane() { return static_cast<int>(threadIdx.x & 63); }
-
-__device__ __forceinline__ int64_t push_degree(const View& v, int64_t u) {
-    int64_t d = v.off0[u + 1] - v.off0[u];
-    if (v.nlists > 1) d += v.off1[u + 1] - v.off1[u];
-    return d;
-}
-
-// Entry `o` (0 <= o < push_degree(u)) of u's list(s): neighbour and weight.
-__device__ __forceinline__ void entry_at(const View& v, int64_t u, int64_t o, int32_t& nbr, int32_t& w) {
-    const int64_t b0 = v.off0[u];
-    const int64_t d0 = v.off0[u + 1] - b0;
-    if (o < d0) {
-        nbr = v.adj0[b0 + o];
-        w = v.w0 ? v.w0[b0 + o] : 1;
-    } else {
-        const int64_t b1 = v.off1[u] + (o - d0);
-        nbr = v.adj1[b1];
-        w = v.w1 ? v.w1[b1] : 1;
-    }
-}
-
-// Block-aggregated append (all threads of the block call it in the same trip): the block
-// reserves its queue slots with ONE atomicAdd on cnt->qlen; the appended degrees stay in
-// registers (mf) until block_flush.  A single contended counter word serves ~88 atomics/us
-// (MI355X_MICROARCH.md, dequeue), so per-wave counter atomics dominated the dense levels.
-constexpr int kWavesPerBlock = kBlock / 64;
-struct AppendLds { unsigned long long off[kWavesPerBlock]; unsigned long long base; unsigned long long mf[kWavesPerBlock]; };
-__device__ __forceinline__ void block_append(bool take, int32_t v, int64_t deg, int32_t* qn, int64_t* qdeg,
-                                             Counters* cnt, AppendLds& sh, unsigned long long& mf) {
-    const unsigned long long mask = __ballot(take);
-    const int wave = threadIdx.x >> 6;
-    if (mask) {
-        int64_t dsum = take ? deg : 0;
-        for (int off = 32; off > 0; off >>= 1) dsum += __shfl_xor(dsum, off, 64);
-        mf += static_cast<unsigned long long>(dsum);
-    }
-    if (lane() == 0) sh.off[wave] = static_cast<unsigned long long>(__popcll(mask));
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long t = 0;
-        for (int w = 0; w < kWavesPerBlock; ++w) { const unsigned long long c = sh.off[w]; sh.off[w] = t; t += c; }
-        sh.base = t ? atomicAdd(&cnt->qlen, t) : 0ULL;
-    }
-    __syncthreads();
-    if (take) {
-        const unsigned long long slot = sh.base + sh.off[wave] + static_cast<unsigned long long>(__popcll(mask & ((1ULL << lane()) - 1ULL)));
-        qn[slot] = v;
-        qdeg[slot] = deg;
-    }
-}
-__device__ __forceinline__ void block_flush(Counters* cnt, AppendLds& sh, unsigned long long mf) {
-    __syncthreads();
-    if (lane() == 0) sh.mf[threadIdx.x >> 6] = mf;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long a = 0;
-        for (int w = 0; w < kWavesPerBlock; ++w) a += sh.mf[w];
-        if (a) atomicAdd(&cnt->mf, a);
-    }
-}
 
 __global__ void fill_i32(int32_t* p, int32_t v, int64_t n) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = v;
@@ -111,72 +45,28 @@ __global__ void __launch_bounds__(kBlock) td_expand(View push, const int32_t* __
         const int64_t* __restrict__ qpre, int64_t qlen, int32_t* __restrict__ level,
         uint64_t* __restrict__ vb, uint64_t* __restrict__ nb, int32_t* __restrict__ qn,
         int64_t* __restrict__ qdeg_n, Counters* cnt, int32_t next_level) {
-    __shared__ int64_t s_pre[kLdsEntries];
-    __shared__ int32_t s_q[kLdsEntries];
-    __shared__ int64_t s_lo, s_hi;
     __shared__ AppendLds sh;
     unsigned long long mf = 0;
-    const int64_t total = qpre[qlen];
-    const int64_t ntiles = (total + kTileEdges - 1) / kTileEdges;
-    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const int64_t t0 = tile * kTileEdges;
-        const int64_t t1 = min(total, t0 + kTileEdges);
-        if (threadIdx.x == 0) {
-            // lo = last i with qpre[i] <= t0 ; hi = last i with qpre[i] <= t1-1
-            int64_t a = 0, b = qlen;          // qpre[a] <= t0 < qpre[b] invariant-ish search
-            while (b - a > 1) { const int64_t c = (a + b) >> 1; if (qpre[c] <= t0) a = c; else b = c; }
-            s_lo = a;
-            int64_t a2 = a, b2 = qlen;
-            while (b2 - a2 > 1) { const int64_t c = (a2 + b2) >> 1; if (qpre[c] <= t1 - 1) a2 = c; else b2 = c; }
-            s_hi = a2;
-        }
-        __syncthreads();
-        const int64_t lo = s_lo, hi = s_hi;
-        const int64_t span = hi - lo + 1;       // queue entries touching this tile
-        const bool in_lds = span + 1 <= kLdsEntries;
-        if (in_lds) {
-            for (int64_t i = threadIdx.x; i <= span; i += kBlock) {
-                s_pre[i] = qpre[lo + i];
-                if (i < span) s_q[i] = q[lo + i];
-            }
-        }
-        __syncthreads();
-        for (int k = 0; k < kEdgesPerThread; ++k) {
-            const int64_t j = t0 + k * kBlock + threadIdx.x;
-            bool take = false;
-            int32_t v = 0;
-            int64_t vdeg = 0;
-            if (j < t1) {
-                int64_t idx;
-                int32_t u;
-                int64_t start;
-                if (in_lds) {
-                    int64_t a = 0, b = span;     // last a with s_pre[a] <= j
-                    while (b - a > 1) { const int64_t c = (a + b) >> 1; if (s_pre[c] <= j) a = c; else b = c; }
-                    idx = a; u = s_q[a]; start = s_pre[a];
-                } else {
-                    int64_t a = lo, b = hi + 1;
-                    while (b - a > 1) { const int64_t c = (a + b) >> 1; if (qpre[c] <= j) a = c; else b = c; }
-                    idx = a; u = q[a]; start = qpre[a];
-                }
-                (void)idx;
-                int32_t w;
-                entry_at(push, u, j - start, v, w);
-                const uint64_t bit = 1ULL << (v & 63);
-                if (!(vb[v >> 6] & bit)) {
-                    const unsigned long long old = atomicOr(reinterpret_cast<unsigned long long*>(&vb[v >> 6]), bit);
-                    if (!(old & bit)) {
-                        take = true;
-                        level[v] = next_level;
-                        atomicOr(reinterpret_cast<unsigned long long*>(&nb[v >> 6]), bit);
-                        vdeg = push_degree(push, v);
-                    }
+    for_each_queue_edge(q, qpre, qlen, [&](bool valid, int32_t u, int64_t o) {
+        bool take = false;
+        int32_t v = 0;
+        int64_t vdeg = 0;
+        if (valid) {
+            int32_t w;
+            entry_at(push, u, o, v, w);
+            const uint64_t bit = 1ULL << (v & 63);
+            if (!(vb[v >> 6] & bit)) {
+                const unsigned long long old = atomicOr(reinterpret_cast<unsigned long long*>(&vb[v >> 6]), bit);
+                if (!(old & bit)) {
+                    take = true;
+                    level[v] = next_level;
+                    atomicOr(reinterpret_cast<unsigned long long*>(&nb[v >> 6]), bit);
+                    vdeg = push_degree(push, v);
                 }
             }
-            block_append(take, v, vdeg, qn, qdeg_n, cnt, sh, mf);
         }
-        __syncthreads();
-    }
+        block_append(take, v, vdeg, qn, qdeg_n, cnt, sh, mf);
+    });
     block_flush(cnt, sh, mf);
 }
 
@@ -252,6 +142,16 @@ __global__ void __launch_bounds__(kBlock) bu_step(View pull, View push, int64_t 
     block_flush(cnt, sh, mf);
 }
 
+// Partitioned levels with device-resident counts: {qlen, push entries} for the caller's
+// all-reduce, and qlen for the ctx's own lazy read.
+__global__ void publish_counts(const Counters* __restrict__ c, int64_t* __restrict__ out, int64_t* __restrict__ slot) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        out[0] = static_cast<int64_t>(c->qlen);
+        out[1] = static_cast<int64_t>(c->mf);
+        slot[0] = static_cast<int64_t>(c->qlen);
+    }
+}
+
 __global__ void level_to_dist(const int32_t* level, int64_t* dist, int64_t n) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const int32_t l = level[i];
@@ -290,72 +190,32 @@ __global__ void __launch_bounds__(kBlock) sssp_relax(View push, const int32_t* _
         const int64_t* __restrict__ qpre, int64_t qlen, const int64_t* __restrict__ msg,
         int64_t* __restrict__ dist, uint64_t* __restrict__ mark, int32_t* __restrict__ qn,
         int64_t* __restrict__ qdeg_n, Counters* cnt, int weighted) {
-    __shared__ int64_t s_pre[kLdsEntries];
-    __shared__ int32_t s_q[kLdsEntries];
-    __shared__ int64_t s_lo, s_hi;
     __shared__ AppendLds sh;
     unsigned long long mf = 0;
-    const int64_t total = qpre[qlen];
-    const int64_t ntiles = (total + kTileEdges - 1) / kTileEdges;
-    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const int64_t t0 = tile * kTileEdges;
-        const int64_t t1 = min(total, t0 + kTileEdges);
-        if (threadIdx.x == 0) {
-            int64_t a = 0, b = qlen;
-            while (b - a > 1) { const int64_t c = (a + b) >> 1; if (qpre[c] <= t0) a = c; else b = c; }
-            s_lo = a;
-            int64_t a2 = a, b2 = qlen;
-            while (b2 - a2 > 1) { const int64_t c = (a2 + b2) >> 1; if (qpre[c] <= t1 - 1) a2 = c; else b2 = c; }
-            s_hi = a2;
-        }
-        __syncthreads();
-        const int64_t lo = s_lo, hi = s_hi;
-        const int64_t span = hi - lo + 1;
-        const bool in_lds = span + 1 <= kLdsEntries;
-        if (in_lds) {
-            for (int64_t i = threadIdx.x; i <= span; i += kBlock) {
-                s_pre[i] = qpre[lo + i];
-                if (i < span) s_q[i] = q[lo + i];
-            }
-        }
-        __syncthreads();
-        for (int k = 0; k < kEdgesPerThread; ++k) {
-            const int64_t j = t0 + k * kBlock + threadIdx.x;
-            bool take = false;
-            int32_t v = 0;
-            int64_t vdeg = 0;
-            if (j < t1) {
-                int32_t u; int64_t start;
-                if (in_lds) {
-                    int64_t a = 0, b = span;
-                    while (b - a > 1) { const int64_t c = (a + b) >> 1; if (s_pre[c] <= j) a = c; else b = c; }
-                    u = s_q[a]; start = s_pre[a];
-                } else {
-                    int64_t a = lo, b = hi + 1;
-                    while (b - a > 1) { const int64_t c = (a + b) >> 1; if (qpre[c] <= j) a = c; else b = c; }
-                    u = q[a]; start = qpre[a];
-                }
-                int32_t w;
-                entry_at(push, u, j - start, v, w);
-                if (!weighted) w = 1;
-                if (w == kMissingWeight) {
-                    atomicOr(&cnt->err, 1ULL);          // edge.value(weight) on a missing key
-                } else {
-                    const int64_t cand = static_cast<int64_t>(static_cast<uint64_t>(msg[u]) + static_cast<uint64_t>(static_cast<int64_t>(w)));
-                    if (cand < dist[v]) {
-                        const long long old = atomicMin(reinterpret_cast<long long*>(&dist[v]), static_cast<long long>(cand));
-                        if (cand < old) {
-                            const uint64_t bit = 1ULL << (v & 63);
-                            const unsigned long long ob = atomicOr(reinterpret_cast<unsigned long long*>(&mark[v >> 6]), bit);
-                            if (!(ob & bit)) { take = true; vdeg = push_degree(push, v); }
-                        }
+    for_each_queue_edge(q, qpre, qlen, [&](bool valid, int32_t u, int64_t o) {
+        bool take = false;
+        int32_t v = 0;
+        int64_t vdeg = 0;
+        if (valid) {
+            int32_t w;
+            entry_at(push, u, o, v, w);
+            if (!weighted) w = 1;
+            if (w == kMissingWeight) {
+                atomicOr(&cnt->err, 1ULL);          // edge.value(weight) on a missing key
+            } else {
+                const int64_t cand = static_cast<int64_t>(static_cast<uint64_t>(msg[u]) + static_cast<uint64_t>(static_cast<int64_t>(w)));
+                if (cand < dist[v]) {
+                    const long long old = atomicMin(reinterpret_cast<long long*>(&dist[v]), static_cast<long long>(cand));
+                    if (cand < old) {
+                        const uint64_t bit = 1ULL << (v & 63);
+                        const unsigned long long ob = atomicOr(reinterpret_cast<unsigned long long*>(&mark[v >> 6]), bit);
+                        if (!(ob & bit)) { take = true; vdeg = push_degree(push, v); }
                     }
                 }
             }
-            block_append(take, v, vdeg, qn, qdeg_n, cnt, sh, mf);
         }
-        __syncthreads();
-    }
+        block_append(take, v, vdeg, qn, qdeg_n, cnt, sh, mf);
+    });
     block_flush(cnt, sh, mf);
 }
 
@@ -377,84 +237,42 @@ __global__ void dist_finalize(int64_t* dist, int64_t n) {
 __global__ void __launch_bounds__(kBlock) part_td_mark(View push, const int32_t* __restrict__ q,
         const int64_t* __restrict__ qpre, int64_t qlen, uint64_t* __restrict__ disc,
         const uint64_t* __restrict__ vb_local, int64_t lo, int64_t n_local) {
-    __shared__ int64_t s_pre[kLdsEntries];
-    __shared__ int32_t s_q[kLdsEntries];
-    __shared__ int64_t s_lo, s_hi;
-    const int64_t total = qpre[qlen];
-    const int64_t ntiles = (total + kTileEdges - 1) / kTileEdges;
-    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const int64_t t0 = tile * kTileEdges;
-        const int64_t t1 = min(total, t0 + kTileEdges);
-        if (threadIdx.x == 0) {
-            int64_t a = 0, b = qlen;
-            while (b - a > 1) { const int64_t c = (a + b) >> 1; if (qpre[c] <= t0) a = c; else b = c; }
-            s_lo = a;
-            int64_t a2 = a, b2 = qlen;
-            while (b2 - a2 > 1) { const int64_t c = (a2 + b2) >> 1; if (qpre[c] <= t1 - 1) a2 = c; else b2 = c; }
-            s_hi = a2;
-        }
-        __syncthreads();
-        const int64_t lo_q = s_lo, hi_q = s_hi;
-        const int64_t span = hi_q - lo_q + 1;
-        const bool in_lds = span + 1 <= kLdsEntries;
-        if (in_lds) {
-            for (int64_t i = threadIdx.x; i <= span; i += kBlock) {
-                s_pre[i] = qpre[lo_q + i];
-                if (i < span) s_q[i] = q[lo_q + i];
-            }
-        }
-        __syncthreads();
-        for (int k = 0; k < kEdgesPerThread; ++k) {
-            const int64_t j = t0 + k * kBlock + threadIdx.x;
-            if (j >= t1) break;
-            int32_t u; int64_t start;
-            if (in_lds) {
-                int64_t a = 0, b = span;
-                while (b - a > 1) { const int64_t c = (a + b) >> 1; if (s_pre[c] <= j) a = c; else b = c; }
-                u = s_q[a]; start = s_pre[a];
-            } else {
-                int64_t a = lo_q, b = hi_q + 1;
-                while (b - a > 1) { const int64_t c = (a + b) >> 1; if (qpre[c] <= j) a = c; else b = c; }
-                u = q[a]; start = qpre[a];
-            }
-            int32_t v, w;
-            entry_at(push, u, j - start, v, w);
-            const uint64_t bit = 1ULL << (v & 63);
-            const int64_t vl = static_cast<int64_t>(v) - lo;
-            if (vl >= 0 && vl < n_local && (vb_local[vl >> 6] & (1ULL << (vl & 63)))) continue;   // owned & visited
-            if (!(disc[v >> 6] & bit)) atomicOr(reinterpret_cast<unsigned long long*>(&disc[v >> 6]), bit);
-        }
-        __syncthreads();
-    }
+    for_each_queue_edge(q, qpre, qlen, [&](bool valid, int32_t u, int64_t o) {
+        if (!valid) return;
+        int32_t v, w;
+        entry_at(push, u, o, v, w);
+        const uint64_t bit = 1ULL << (v & 63);
+        const int64_t vl = static_cast<int64_t>(v) - lo;
+        if (vl >= 0 && vl < n_local && (vb_local[vl >> 6] & (1ULL << (vl & 63)))) return;   // owned & visited
+        if (!(disc[v >> 6] & bit)) atomicOr(reinterpret_cast<unsigned long long*>(&disc[v >> 6]), bit);
+    });
 }
 
-// Owner side: OR the received slices, claim the unvisited bits (one wave per word).
+// Owner side: OR the received slices, claim the unvisited bits (one wave per word; two-pass
+// chunked extraction, frontier.hpp).
 __global__ void __launch_bounds__(kBlock) part_claim(View push, const uint64_t* __restrict__ recv,
         int nslices, int64_t words, int64_t n_local, uint64_t* __restrict__ vb, uint64_t* __restrict__ nb,
         int32_t* __restrict__ level, int32_t* __restrict__ qn, int64_t* __restrict__ qdeg_n, Counters* cnt,
         int32_t next_level) {
-    __shared__ AppendLds sh;
-    unsigned long long mf = 0;
-    for (int64_t b = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock; b < words;
-         b += static_cast<int64_t>(gridDim.x) * kWavesPerBlock) {        // block-uniform trips
-        const int64_t wd = b + (threadIdx.x >> 6);
-        const bool live = wd < words;
+    auto probe = [&](int64_t wd, Take* t, bool commit) -> bool {
         uint64_t bits = 0;
-        if (live)
-            for (int s = 0; s < nslices; ++s) bits |= recv[static_cast<int64_t>(s) * words + wd];
-        const uint64_t vis = live ? vb[wd] : ~0ULL;
+        for (int s = 0; s < nslices; ++s) bits |= recv[static_cast<int64_t>(s) * words + wd];
+        const uint64_t vis = vb[wd];
         const uint64_t fresh = bits & ~vis;
         const int64_t v = (wd << 6) + lane();
         const bool take = v < n_local && ((fresh >> lane()) & 1ULL);
         const unsigned long long tm = __ballot(take);
-        if (lane() == 0 && live) {
-            nb[wd] = tm;
-            if (tm) vb[wd] = vis | tm;
+        if (commit) {
+            if (lane() == 0) {
+                nb[wd] = tm;
+                if (tm) vb[wd] = vis | tm;
+            }
+            if (take) level[v] = next_level;
         }
-        if (take) level[v] = next_level;
-        block_append(take, static_cast<int32_t>(v), take ? push_degree(push, v) : 0, qn, qdeg_n, cnt, sh, mf);
-    }
-    block_flush(cnt, sh, mf);
+        t[0] = {take, static_cast<int32_t>(v), take ? push_degree(push, v) : 0};
+        return true;                            // nb[wd] is written for every word
+    };
+    chunk_extract<1>(words, probe, qn, qdeg_n, cnt);
 }
 
 // out[v] = in[perm[v]]: internal (degree-grouped) order -> the API's row order.
@@ -502,6 +320,10 @@ hipError_t k_bu_step(const View& pull, const View& push, int64_t n, const uint64
     bu_step<<<grid_for(words * 64, kBlock, 8192), kBlock, 0, s>>>(pull, push, n, fb, vb, nb, level, qn, qdeg_n, cnt, next_level);
     return hipGetLastError();
 }
+hipError_t k_publish_counts(const Counters* c, int64_t* out, int64_t* slot, hipStream_t s) {
+    publish_counts<<<1, 64, 0, s>>>(c, out, slot);
+    return hipGetLastError();
+}
 hipError_t k_level_to_dist(const int32_t* level, int64_t* dist, int64_t n, hipStream_t s) {
     level_to_dist<<<grid_for(n), kBlock, 0, s>>>(level, dist, n);
     return hipGetLastError();
@@ -539,8 +361,8 @@ hipError_t k_part_td_mark(const View& push, const int32_t* q, const int64_t* qpr
 hipError_t k_part_claim(const View& push, const uint64_t* recv, int nslices, int64_t words, int64_t n_local,
                         uint64_t* vb, uint64_t* nb, int32_t* level, int32_t* qn, int64_t* qdeg_n,
                         Counters* cnt, int32_t next_level, hipStream_t s) {
-    part_claim<<<grid_for(words * 64, kBlock, 8192), kBlock, 0, s>>>(push, recv, nslices, words, n_local, vb, nb,
-                                                                      level, qn, qdeg_n, cnt, next_level);
+    part_claim<<<extract_grid(words), kBlock, 0, s>>>(push, recv, nslices, words, n_local, vb, nb, level, qn, qdeg_n, cnt,
+                                                       next_level);
     return hipGetLastError();
 }
 hipError_t k_unpermute_i64(const int64_t* in, const int32_t* perm, int64_t* out, int64_t n, hipStream_t s) {

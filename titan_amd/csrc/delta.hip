@@ -30,122 +30,10 @@
 // dist with the same pending / near-queue rule (ds_apply).  rbest lives for the whole run:
 // a target is re-sent only when this rank improves on what it sent before.
 #include <hip/hip_runtime.h>
-#include "engine.hpp"
+#include "frontier.hpp"
 
 namespace tgo {
 namespace {
-
-constexpr int kBlock = 256;
-constexpr int kEdgesPerThread = 8;
-constexpr int kTileEdges = kBlock * kEdgesPerThread;
-constexpr int kLdsEntries = kTileEdges + 2;
-
-__device__ __forceinline__ int lane() { return static_cast<int>(threadIdx.x & 63); }
-
-__device__ __forceinline__ int64_t push_degree(const View& v, int64_t u) {
-    int64_t d = v.off0[u + 1] - v.off0[u];
-    if (v.nlists > 1) d += v.off1[u + 1] - v.off1[u];
-    return d;
-}
-
-// Block-aggregated append (all threads of the block call it in the same trip): the block
-// reserves its queue slots with ONE atomicAdd on cnt->qlen; the appended degrees stay in
-// registers (mf) until block_flush.  A single contended counter word serves ~88 atomics/us
-// (MI355X_MICROARCH.md, dequeue), so per-wave counter atomics dominated the dense levels.
-constexpr int kWavesPerBlock = kBlock / 64;
-struct AppendLds { unsigned long long off[kWavesPerBlock]; unsigned long long base; unsigned long long mf[kWavesPerBlock]; };
-__device__ __forceinline__ void block_append(bool take, int32_t v, int64_t deg, int32_t* qn, int64_t* qdeg,
-                                             Counters* cnt, AppendLds& sh, unsigned long long& mf) {
-    const unsigned long long mask = __ballot(take);
-    const int wave = threadIdx.x >> 6;
-    if (mask) {
-        int64_t dsum = take ? deg : 0;
-        for (int off = 32; off > 0; off >>= 1) dsum += __shfl_xor(dsum, off, 64);
-        mf += static_cast<unsigned long long>(dsum);
-    }
-    if (lane() == 0) sh.off[wave] = static_cast<unsigned long long>(__popcll(mask));
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long t = 0;
-        for (int w = 0; w < kWavesPerBlock; ++w) { const unsigned long long c = sh.off[w]; sh.off[w] = t; t += c; }
-        sh.base = t ? atomicAdd(&cnt->qlen, t) : 0ULL;
-    }
-    __syncthreads();
-    if (take) {
-        const unsigned long long slot = sh.base + sh.off[wave] + static_cast<unsigned long long>(__popcll(mask & ((1ULL << lane()) - 1ULL)));
-        qn[slot] = v;
-        qdeg[slot] = deg;
-    }
-}
-__device__ __forceinline__ void block_flush(Counters* cnt, AppendLds& sh, unsigned long long mf) {
-    __syncthreads();
-    if (lane() == 0) sh.mf[threadIdx.x >> 6] = mf;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long a = 0;
-        for (int w = 0; w < kWavesPerBlock; ++w) a += sh.mf[w];
-        if (a) atomicAdd(&cnt->mf, a);
-    }
-}
-
-// Bitmap extraction into a queue, two passes over a contiguous chunk of 64-vertex words per
-// block (one wave per word): pass 1 counts what the chunk takes, one atomicAdd per block
-// reserves its slots, pass 2 re-reads (L2-warm) and writes.  No per-trip block barriers or
-// counter atomics, which dominated the one-pass version (~200 us per extraction at 16M
-// vertices).  probe(wd, takes, commit) fills up to kStreams (take, entry, degree) per lane and
-// returns whether the word needs a write; with commit it also clears what it took (one
-// writer per word) — pass 1 never writes, so both passes see the same bits.
-struct Take { bool take; int32_t entry; int64_t deg; };
-template <int kStreams, class Probe>
-__device__ __forceinline__ void chunk_extract(int64_t words, const Probe& probe, int32_t* __restrict__ qn,
-                                              int64_t* __restrict__ qdeg, Counters* cnt) {
-    __shared__ unsigned long long s_cnt[kWavesPerBlock], s_mf[kWavesPerBlock], s_base;
-    const int64_t per = ((words + gridDim.x - 1) / gridDim.x + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock;
-    const int64_t w0 = static_cast<int64_t>(blockIdx.x) * per;
-    const int64_t w1 = min(words, w0 + per);
-    const int wave = threadIdx.x >> 6;
-    const unsigned long long below = (1ULL << lane()) - 1ULL;
-    unsigned long long count = 0, dsum = 0;
-    bool touch = false;
-    for (int64_t wd = w0 + wave; wd < w1; wd += kWavesPerBlock) {
-        Take t[kStreams];
-        touch |= probe(wd, t, false);
-        for (int k = 0; k < kStreams; ++k) {
-            count += __popcll(__ballot(t[k].take));
-            if (t[k].take) dsum += static_cast<unsigned long long>(t[k].deg);
-        }
-    }
-    for (int o = 32; o > 0; o >>= 1) dsum += __shfl_xor(dsum, o, 64);
-    if (lane() == 0) { s_cnt[wave] = count; s_mf[wave] = dsum; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long t = 0, m = 0;
-        for (int w = 0; w < kWavesPerBlock; ++w) { const unsigned long long c = s_cnt[w]; s_cnt[w] = t; t += c; m += s_mf[w]; }
-        s_base = t ? atomicAdd(&cnt->qlen, t) : 0ULL;
-        if (m) atomicAdd(&cnt->mf, m);
-    }
-    __syncthreads();
-    if (!touch) return;                                      // wave-uniform
-    unsigned long long cursor = s_base + s_cnt[wave];
-    for (int64_t wd = w0 + wave; wd < w1; wd += kWavesPerBlock) {
-        Take t[kStreams];
-        probe(wd, t, true);
-        for (int k = 0; k < kStreams; ++k) {
-            const unsigned long long mask = __ballot(t[k].take);
-            if (t[k].take) {
-                const unsigned long long slot = cursor + __popcll(mask & below);
-                qn[slot] = t[k].entry;
-                qdeg[slot] = t[k].deg;
-            }
-            cursor += __popcll(mask);
-        }
-    }
-}
-
-inline int extract_grid(int64_t words) {
-    const int64_t g = (words + 63) / 64;                      // >= 64 words per block
-    return static_cast<int>(g < 1 ? 1 : (g > 2048 ? 2048 : g));
-}
 
 // min(cand) into dist[v] of an owned vertex; true when v has to join the near queue.
 __device__ __forceinline__ bool relax_owned(int64_t* dist, uint64_t* pend, int64_t v, int64_t cand, int64_t thr) {
@@ -185,89 +73,43 @@ __global__ void __launch_bounds__(kBlock) ds_relax(View push, const int32_t* __r
         int64_t* __restrict__ dist, uint64_t* __restrict__ pend, int32_t* __restrict__ qn,
         int64_t* __restrict__ qdeg_n, Counters* cnt, int weighted, int64_t thr, int64_t lo, int64_t n_local,
         int64_t* __restrict__ rbest, uint64_t* __restrict__ rmark) {
-    __shared__ int64_t s_pre[kLdsEntries];
-    __shared__ int32_t s_q[kLdsEntries];
-    __shared__ int64_t s_lo, s_hi;
     __shared__ AppendLds sh;
     unsigned long long mf = 0;
-    const int64_t total = qpre[qlen];
-    if (blockIdx.x == 0 && threadIdx.x == 0) cnt->red[1] = static_cast<unsigned long long>(total);   // work done
-    const int64_t ntiles = (total + kTileEdges - 1) / kTileEdges;
-    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const int64_t t0 = tile * kTileEdges;
-        const int64_t t1 = min(total, t0 + kTileEdges);
-        if (threadIdx.x == 0) {
-            int64_t a = 0, b = qlen;
-            while (b - a > 1) { const int64_t c = (a + b) >> 1; if (qpre[c] <= t0) a = c; else b = c; }
-            s_lo = a;
-            int64_t a2 = a, b2 = qlen;
-            while (b2 - a2 > 1) { const int64_t c = (a2 + b2) >> 1; if (qpre[c] <= t1 - 1) a2 = c; else b2 = c; }
-            s_hi = a2;
-        }
-        __syncthreads();
-        const int64_t lo_q = s_lo, hi_q = s_hi;
-        const int64_t span = hi_q - lo_q + 1;
-        const bool in_lds = span + 1 <= kLdsEntries;
-        if (in_lds) {
-            for (int64_t i = threadIdx.x; i <= span; i += kBlock) {
-                s_pre[i] = qpre[lo_q + i];
-                if (i < span) s_q[i] = q[lo_q + i];
-            }
-        }
-        __syncthreads();
-        for (int k = 0; k < kEdgesPerThread; ++k) {
-            const int64_t j = t0 + k * kBlock + threadIdx.x;
-            bool take = false;
-            int32_t v = 0;
-            int64_t vdeg = 0;
-            if (j < t1) {
-                int32_t u; int64_t start;
-                if (in_lds) {
-                    int64_t a = 0, b = span;
-                    while (b - a > 1) { const int64_t c = (a + b) >> 1; if (s_pre[c] <= j) a = c; else b = c; }
-                    u = s_q[a]; start = s_pre[a];
-                } else {
-                    int64_t a = lo_q, b = hi_q + 1;
-                    while (b - a > 1) { const int64_t c = (a + b) >> 1; if (qpre[c] <= j) a = c; else b = c; }
-                    u = q[a]; start = qpre[a];
-                }
-                const int64_t o = j - start;
-                const int64_t b0 = push.off0[u];
-                const int64_t d0 = push.off0[u + 1] - b0;
-                int32_t t, w;
-                if (o < d0) { t = push.adj0[b0 + o]; w = push.w0 && weighted ? push.w0[b0 + o] : 1; }
-                else {
-                    const int64_t b1 = push.off1[u] + (o - d0);
-                    t = push.adj1[b1]; w = push.w1 && weighted ? push.w1[b1] : 1;
-                }
-                const int64_t mu = msg[u];
-                if (w == kMissingWeight) {
-                    atomicOr(&cnt->err, 1ULL);          // edge.value(weight) on a missing key
-                } else if (dist[u] < mu) {
-                    // u improved during this phase: it is pending again and will relax every
-                    // entry with the better distance, so this relaxation is wasted work
-                } else {
-                    const int64_t cand = mu + static_cast<int64_t>(w);
-                    const int64_t tl = kPart ? static_cast<int64_t>(t) - lo : static_cast<int64_t>(t);
-                    if (!kPart || (tl >= 0 && tl < n_local)) {
-                        if (relax_owned(dist, pend, tl, cand, thr)) {
-                            take = true;
-                            v = static_cast<int32_t>(tl);
-                            vdeg = push_degree(push, tl);
-                        }
-                    } else if (cand < rbest[t]) {
-                        const long long old = atomicMin(reinterpret_cast<long long*>(&rbest[t]), static_cast<long long>(cand));
-                        if (cand < old) {
-                            const uint64_t bit = 1ULL << (t & 63);
-                            if (!(rmark[t >> 6] & bit)) atomicOr(reinterpret_cast<unsigned long long*>(&rmark[t >> 6]), bit);
-                        }
+    if (blockIdx.x == 0 && threadIdx.x == 0) cnt->red[1] = static_cast<unsigned long long>(qpre[qlen]);   // work done
+    for_each_queue_edge(q, qpre, qlen, [&](bool valid, int32_t u, int64_t o) {
+        bool take = false;
+        int32_t v = 0;
+        int64_t vdeg = 0;
+        if (valid) {
+            int32_t t, w;
+            entry_at(push, u, o, t, w);
+            if (!weighted) w = 1;
+            const int64_t mu = msg[u];
+            if (w == kMissingWeight) {
+                atomicOr(&cnt->err, 1ULL);          // edge.value(weight) on a missing key
+            } else if (dist[u] < mu) {
+                // u improved during this phase: it is pending again and will relax every
+                // entry with the better distance, so this relaxation is wasted work
+            } else {
+                const int64_t cand = mu + static_cast<int64_t>(w);
+                const int64_t tl = kPart ? static_cast<int64_t>(t) - lo : static_cast<int64_t>(t);
+                if (!kPart || (tl >= 0 && tl < n_local)) {
+                    if (relax_owned(dist, pend, tl, cand, thr)) {
+                        take = true;
+                        v = static_cast<int32_t>(tl);
+                        vdeg = push_degree(push, tl);
+                    }
+                } else if (cand < rbest[t]) {
+                    const long long old = atomicMin(reinterpret_cast<long long*>(&rbest[t]), static_cast<long long>(cand));
+                    if (cand < old) {
+                        const uint64_t bit = 1ULL << (t & 63);
+                        if (!(rmark[t >> 6] & bit)) atomicOr(reinterpret_cast<unsigned long long*>(&rmark[t >> 6]), bit);
                     }
                 }
             }
-            block_append(take, v, vdeg, qn, qdeg_n, cnt, sh, mf);
         }
-        __syncthreads();
-    }
+        block_append(take, v, vdeg, qn, qdeg_n, cnt, sh, mf);
+    });
     block_flush(cnt, sh, mf);
 }
 
@@ -337,70 +179,31 @@ __global__ void __launch_bounds__(kBlock) ds_relax_ws(const int64_t* __restrict_
         const int32_t* __restrict__ wt, const int64_t* __restrict__ light, const int32_t* __restrict__ q,
         const int64_t* __restrict__ qpre, int64_t qlen, const int64_t* __restrict__ msg, int64_t* __restrict__ dist,
         uint64_t* __restrict__ pend, int32_t* __restrict__ qn, int64_t* __restrict__ qdeg_n, Counters* cnt, int64_t thr) {
-    __shared__ int64_t s_pre[kLdsEntries];
-    __shared__ int32_t s_q[kLdsEntries];
-    __shared__ int64_t s_lo, s_hi;
     __shared__ AppendLds sh;
     unsigned long long mf = 0;
-    const int64_t total = qpre[qlen];
-    if (blockIdx.x == 0 && threadIdx.x == 0) cnt->red[1] = static_cast<unsigned long long>(total);   // work done
-    const int64_t ntiles = (total + kTileEdges - 1) / kTileEdges;
-    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const int64_t t0 = tile * kTileEdges;
-        const int64_t t1 = min(total, t0 + kTileEdges);
-        if (threadIdx.x == 0) {
-            int64_t a = 0, b = qlen;
-            while (b - a > 1) { const int64_t c = (a + b) >> 1; if (qpre[c] <= t0) a = c; else b = c; }
-            s_lo = a;
-            int64_t a2 = a, b2 = qlen;
-            while (b2 - a2 > 1) { const int64_t c = (a2 + b2) >> 1; if (qpre[c] <= t1 - 1) a2 = c; else b2 = c; }
-            s_hi = a2;
-        }
-        __syncthreads();
-        const int64_t lo_q = s_lo, hi_q = s_hi;
-        const int64_t span = hi_q - lo_q + 1;
-        const bool in_lds = span + 1 <= kLdsEntries;
-        if (in_lds) {
-            for (int64_t i = threadIdx.x; i <= span; i += kBlock) {
-                s_pre[i] = qpre[lo_q + i];
-                if (i < span) s_q[i] = q[lo_q + i];
+    if (blockIdx.x == 0 && threadIdx.x == 0) cnt->red[1] = static_cast<unsigned long long>(qpre[qlen]);   // work done
+    for_each_queue_edge(q, qpre, qlen, [&](bool valid, int32_t qentry, int64_t o) {
+        bool take = false;
+        int32_t v = 0;
+        int64_t vdeg = 0;
+        if (valid) {
+            const uint32_t qe = static_cast<uint32_t>(qentry);
+            const int64_t u = static_cast<int64_t>(qe & ~kHeavyFlag);
+            const int64_t e = ((qe & kHeavyFlag) ? light[u] : off[u]) + o;
+            const int32_t t = adj[e], w = wt[e];
+            const int64_t mu = msg[u];
+            if (w == kMissingWeight) {
+                atomicOr(&cnt->err, 1ULL);              // edge.value(weight) on a missing key
+            } else if (dist[u] < mu) {
+                // improved during this phase: pending again, relaxes with the better distance
+            } else if (relax_owned(dist, pend, t, mu + static_cast<int64_t>(w), thr)) {
+                take = true;
+                v = t;
+                vdeg = light_degree(off, light, t);
             }
         }
-        __syncthreads();
-        for (int k = 0; k < kEdgesPerThread; ++k) {
-            const int64_t j = t0 + k * kBlock + threadIdx.x;
-            bool take = false;
-            int32_t v = 0;
-            int64_t vdeg = 0;
-            if (j < t1) {
-                uint32_t qe; int64_t start;
-                if (in_lds) {
-                    int64_t a = 0, b = span;
-                    while (b - a > 1) { const int64_t c = (a + b) >> 1; if (s_pre[c] <= j) a = c; else b = c; }
-                    qe = static_cast<uint32_t>(s_q[a]); start = s_pre[a];
-                } else {
-                    int64_t a = lo_q, b = hi_q + 1;
-                    while (b - a > 1) { const int64_t c = (a + b) >> 1; if (qpre[c] <= j) a = c; else b = c; }
-                    qe = static_cast<uint32_t>(q[a]); start = qpre[a];
-                }
-                const int64_t u = static_cast<int64_t>(qe & ~kHeavyFlag);
-                const int64_t e = ((qe & kHeavyFlag) ? light[u] : off[u]) + (j - start);
-                const int32_t t = adj[e], w = wt[e];
-                const int64_t mu = msg[u];
-                if (w == kMissingWeight) {
-                    atomicOr(&cnt->err, 1ULL);              // edge.value(weight) on a missing key
-                } else if (dist[u] < mu) {
-                    // improved during this phase: pending again, relaxes with the better distance
-                } else if (relax_owned(dist, pend, t, mu + static_cast<int64_t>(w), thr)) {
-                    take = true;
-                    v = t;
-                    vdeg = light_degree(off, light, t);
-                }
-            }
-            block_append(take, v, vdeg, qn, qdeg_n, cnt, sh, mf);
-        }
-        __syncthreads();
-    }
+        block_append(take, v, vdeg, qn, qdeg_n, cnt, sh, mf);
+    });
     block_flush(cnt, sh, mf);
 }
 

@@ -256,6 +256,7 @@ hipError_t k_bu_step(const View& pull, const View& push, int64_t n, const uint64
                      uint64_t* nb, int32_t* level, int32_t* qn, int64_t* qdeg_n, Counters* cnt,
                      int32_t next_level, hipStream_t s);
 hipError_t k_level_to_dist(const int32_t* level, int64_t* dist, int64_t n, hipStream_t s);
+hipError_t k_publish_counts(const Counters* c, int64_t* out, int64_t* slot, hipStream_t s);
 hipError_t k_reach_stats(const View& both_or_pull, const int64_t* dist, int64_t n,
                          unsigned long long* out2, hipStream_t s);
 hipError_t k_degree_i64(const View& v, const int32_t* q, int64_t qlen, int64_t* qdeg, hipStream_t s);
@@ -338,6 +339,9 @@ hipError_t k_pr_iter(const DevCsr& in, const RowBlocks& rb, const double* contri
                      const double* edge_count, double* pr, double* contrib_next, double* partial,
                      double alpha, double base, int64_t n, const PrTuning& t, hipStream_t s);
 hipError_t k_fill_f64(double* p, double v, int64_t n, hipStream_t s);
+hipError_t k_pr_cold_phase(const ColdBlocks& cb, const double* contrib, hipStream_t s);
+hipError_t k_pr_hot_phase(const ColdBlocks& cb, const double* contrib, const double* edge_count, double* pr,
+                          double* contrib_next, double* partial_long, double alpha, double base, hipStream_t s);
 hipError_t k_pr_iter_cold(const ColdBlocks& cb, const double* contrib, const double* edge_count, double* pr,
                           double* contrib_next, double* partial_long, double alpha, double base, hipStream_t s);
 hipError_t k_walk_iter(const DevCsr& out, const RowBlocks& rb, const int32_t* prev, int32_t* next,

@@ -1,0 +1,201 @@
+// frontier.hpp — device building blocks shared by the frontier kernels (bfs.hip, delta.hip,
+// msbfs.hip): edge-balanced load-balanced search over a vertex queue, block-aggregated
+// queue appends, and two-pass bitmap extraction.  Include from exactly those .hip files
+// (everything here is in an anonymous namespace, one copy per translation unit).
+#pragma once
+#include <hip/hip_runtime.h>
+#include "engine.hpp"
+
+namespace tgo {
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kWavesPerBlock = kBlock / 64;
+constexpr int kEdgesPerThread = 8;
+constexpr int kTileEdges = kBlock * kEdgesPerThread;   // 2048 queue entries' edges per block tile
+constexpr int kLdsEntries = kTileEdges + 2;
+
+__device__ __forceinline__ int lane() { return static_cast<int>(threadIdx.x & 63); }
+
+// Entries of u over the one or two lists of a view.
+__device__ __forceinline__ int64_t push_degree(const View& v, int64_t u) {
+    int64_t d = v.off0[u + 1] - v.off0[u];
+    if (v.nlists > 1) d += v.off1[u + 1] - v.off1[u];
+    return d;
+}
+
+// Entry `o` (0 <= o < push_degree(u)) of u's list(s): neighbour and weight (1 if unweighted).
+__device__ __forceinline__ void entry_at(const View& v, int64_t u, int64_t o, int32_t& nbr, int32_t& w) {
+    const int64_t b0 = v.off0[u];
+    const int64_t d0 = v.off0[u + 1] - b0;
+    if (o < d0) {
+        nbr = v.adj0[b0 + o];
+        w = v.w0 ? v.w0[b0 + o] : 1;
+    } else {
+        const int64_t b1 = v.off1[u] + (o - d0);
+        nbr = v.adj1[b1];
+        w = v.w1 ? v.w1[b1] : 1;
+    }
+}
+
+// Edge-balanced load-balanced search (Merrill et al., PPoPP'12) over a queue q[0..qlen) whose
+// entries' edge counts have the exclusive scan qpre[0..qlen] (qpre[qlen] = total).  The edge
+// space is cut into kTileEdges tiles; a block stages the scan entries its tile touches in
+// LDS (when they fit) and every thread binary-searches the queue entry of each of its
+// kEdgesPerThread edges.  body(valid, entry, offset) is called by EVERY thread of the block
+// for every k in the same trip (block-uniform, so it may synchronise the block, e.g. via
+// block_append); valid = the edge exists, entry = q[i] of the owning queue slot, offset = the
+// edge's position inside that entry's list.
+template <class Body>
+__device__ __forceinline__ void for_each_queue_edge(const int32_t* __restrict__ q, const int64_t* __restrict__ qpre,
+                                                    int64_t qlen, Body&& body) {
+    __shared__ int64_t s_pre[kLdsEntries];
+    __shared__ int32_t s_q[kLdsEntries];
+    __shared__ int64_t s_lo, s_hi;
+    const int64_t total = qpre[qlen];
+    const int64_t ntiles = (total + kTileEdges - 1) / kTileEdges;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t t0 = tile * kTileEdges;
+        const int64_t t1 = min(total, t0 + kTileEdges);
+        if (threadIdx.x == 0) {             // lo = last i with qpre[i] <= t0; hi = last i with qpre[i] <= t1-1
+            int64_t a = 0, b = qlen;
+            while (b - a > 1) { const int64_t c = (a + b) >> 1; if (qpre[c] <= t0) a = c; else b = c; }
+            s_lo = a;
+            int64_t a2 = a, b2 = qlen;
+            while (b2 - a2 > 1) { const int64_t c = (a2 + b2) >> 1; if (qpre[c] <= t1 - 1) a2 = c; else b2 = c; }
+            s_hi = a2;
+        }
+        __syncthreads();
+        const int64_t lo = s_lo, hi = s_hi;
+        const int64_t span = hi - lo + 1;   // queue entries touching this tile
+        const bool in_lds = span + 1 <= kLdsEntries;
+        if (in_lds) {
+            for (int64_t i = threadIdx.x; i <= span; i += kBlock) {
+                s_pre[i] = qpre[lo + i];
+                if (i < span) s_q[i] = q[lo + i];
+            }
+        }
+        __syncthreads();
+        for (int k = 0; k < kEdgesPerThread; ++k) {
+            const int64_t j = t0 + k * kBlock + threadIdx.x;
+            int32_t entry = 0;
+            int64_t start = j;
+            const bool valid = j < t1;
+            if (valid) {
+                if (in_lds) {
+                    int64_t a = 0, b = span;
+                    while (b - a > 1) { const int64_t c = (a + b) >> 1; if (s_pre[c] <= j) a = c; else b = c; }
+                    entry = s_q[a]; start = s_pre[a];
+                } else {
+                    int64_t a = lo, b = hi + 1;
+                    while (b - a > 1) { const int64_t c = (a + b) >> 1; if (qpre[c] <= j) a = c; else b = c; }
+                    entry = q[a]; start = qpre[a];
+                }
+            }
+            body(valid, entry, j - start);
+        }
+        __syncthreads();
+    }
+}
+
+// Block-aggregated append (all threads of the block call it in the same trip): the block
+// reserves its queue slots with ONE atomicAdd on cnt->qlen; the appended degrees stay in
+// registers (mf) until block_flush.  A single contended counter word serves ~88 atomics/us
+// (MI355X_MICROARCH.md, dequeue), so per-wave counter atomics dominated the dense levels.
+struct AppendLds { unsigned long long off[kWavesPerBlock]; unsigned long long base; unsigned long long mf[kWavesPerBlock]; };
+__device__ __forceinline__ void block_append(bool take, int32_t v, int64_t deg, int32_t* qn, int64_t* qdeg,
+                                             Counters* cnt, AppendLds& sh, unsigned long long& mf) {
+    const unsigned long long mask = __ballot(take);
+    const int wave = threadIdx.x >> 6;
+    if (mask) {
+        int64_t dsum = take ? deg : 0;
+        for (int off = 32; off > 0; off >>= 1) dsum += __shfl_xor(dsum, off, 64);
+        mf += static_cast<unsigned long long>(dsum);
+    }
+    if (lane() == 0) sh.off[wave] = static_cast<unsigned long long>(__popcll(mask));
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+        for (int w = 0; w < kWavesPerBlock; ++w) { const unsigned long long c = sh.off[w]; sh.off[w] = t; t += c; }
+        sh.base = t ? atomicAdd(&cnt->qlen, t) : 0ULL;
+    }
+    __syncthreads();
+    if (take) {
+        const unsigned long long slot = sh.base + sh.off[wave] + static_cast<unsigned long long>(__popcll(mask & ((1ULL << lane()) - 1ULL)));
+        qn[slot] = v;
+        qdeg[slot] = deg;
+    }
+}
+__device__ __forceinline__ void block_flush(Counters* cnt, AppendLds& sh, unsigned long long mf) {
+    __syncthreads();
+    if (lane() == 0) sh.mf[threadIdx.x >> 6] = mf;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long a = 0;
+        for (int w = 0; w < kWavesPerBlock; ++w) a += sh.mf[w];
+        if (a) atomicAdd(&cnt->mf, a);
+    }
+}
+
+// Bitmap extraction into a queue, two passes over a contiguous chunk of 64-vertex words per
+// block (one wave per word): pass 1 counts what the chunk takes, one atomicAdd per block
+// reserves its slots, pass 2 re-reads (L2-warm) and writes.  No per-trip block barriers or
+// counter atomics, which dominated the one-pass form (~200 us per extraction at 16M
+// vertices).  probe(wd, takes, commit) fills up to kStreams (take, entry, degree) per lane and
+// returns whether the word needs a write; with commit it also applies its writes (one writer
+// per word) — pass 1 never writes, so both passes see the same state.
+struct Take { bool take; int32_t entry; int64_t deg; };
+template <int kStreams, class Probe>
+__device__ __forceinline__ void chunk_extract(int64_t words, const Probe& probe, int32_t* __restrict__ qn,
+                                              int64_t* __restrict__ qdeg, Counters* cnt) {
+    __shared__ unsigned long long s_cnt[kWavesPerBlock], s_mf[kWavesPerBlock], s_base;
+    const int64_t per = ((words + gridDim.x - 1) / gridDim.x + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock;
+    const int64_t w0 = static_cast<int64_t>(blockIdx.x) * per;
+    const int64_t w1 = min(words, w0 + per);
+    const int wave = threadIdx.x >> 6;
+    const unsigned long long below = (1ULL << lane()) - 1ULL;
+    unsigned long long count = 0, dsum = 0;
+    bool touch = false;
+    for (int64_t wd = w0 + wave; wd < w1; wd += kWavesPerBlock) {
+        Take t[kStreams];
+        touch |= probe(wd, t, false);
+        for (int k = 0; k < kStreams; ++k) {
+            count += __popcll(__ballot(t[k].take));
+            if (t[k].take) dsum += static_cast<unsigned long long>(t[k].deg);
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) dsum += __shfl_xor(dsum, o, 64);
+    if (lane() == 0) { s_cnt[wave] = count; s_mf[wave] = dsum; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0, m = 0;
+        for (int w = 0; w < kWavesPerBlock; ++w) { const unsigned long long c = s_cnt[w]; s_cnt[w] = t; t += c; m += s_mf[w]; }
+        s_base = t ? atomicAdd(&cnt->qlen, t) : 0ULL;
+        if (m) atomicAdd(&cnt->mf, m);
+    }
+    __syncthreads();
+    if (!touch) return;                                      // wave-uniform
+    unsigned long long cursor = s_base + s_cnt[wave];
+    for (int64_t wd = w0 + wave; wd < w1; wd += kWavesPerBlock) {
+        Take t[kStreams];
+        probe(wd, t, true);
+        for (int k = 0; k < kStreams; ++k) {
+            const unsigned long long mask = __ballot(t[k].take);
+            if (t[k].take) {
+                const unsigned long long slot = cursor + __popcll(mask & below);
+                qn[slot] = t[k].entry;
+                qdeg[slot] = t[k].deg;
+            }
+            cursor += __popcll(mask);
+        }
+    }
+}
+
+// Grid for chunk_extract: >= 64 words per block, at most 2048 blocks.
+inline int extract_grid(int64_t words) {
+    const int64_t g = (words + 63) / 64;
+    return static_cast<int>(g < 1 ? 1 : (g > 2048 ? 2048 : g));
+}
+
+}  // namespace
+}  // namespace tgo

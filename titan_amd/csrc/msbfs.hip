@@ -14,24 +14,12 @@
 // at most log2(L)+1 coalesced 8-byte writes per vertex and level, and planes are zeroed
 // only when the sweep first reaches level 2^k.
 #include <hip/hip_runtime.h>
-#include "engine.hpp"
+#include "frontier.hpp"
 
 namespace tgo {
 namespace {
 
-constexpr int kBlock = 256;
-constexpr int kEdgesPerThread = 8;
-constexpr int kTileEdges = kBlock * kEdgesPerThread;
-constexpr int kLdsEntries = kTileEdges + 2;
 constexpr int kMaxSources = 64;
-
-__device__ __forceinline__ int lane() { return static_cast<int>(threadIdx.x & 63); }
-
-__device__ __forceinline__ int64_t view_degree(const View& v, int64_t u) {
-    int64_t d = v.off0[u + 1] - v.off0[u];
-    if (v.nlists > 1) d += v.off1[u + 1] - v.off1[u];
-    return d;
-}
 
 __device__ __forceinline__ int32_t view_entry(const View& v, int64_t u, int64_t o) {
     const int64_t b0 = v.off0[u];
@@ -47,7 +35,7 @@ __device__ __forceinline__ int32_t view_entry(const View& v, int64_t u, int64_t 
 // until discover_flush.  One contended counter word takes ~88 atomics/us
 // (MI355X_MICROARCH.md, dequeue), so per-wave counter atomics cost ~1.6 ms per dense level
 // on RMAT-24 — more than the level's gathers.
-constexpr int kWaves = kBlock / 64;
+constexpr int kWaves = kWavesPerBlock;
 struct DiscoverLds { unsigned long long cnt[kWaves]; unsigned long long base; };
 __device__ __forceinline__ void discover(int64_t v, uint64_t fresh, int32_t level, LevelPlanes pl,
                                          const View& push, int32_t* qn, int64_t* qdeg, Counters* cnt,
@@ -62,7 +50,7 @@ __device__ __forceinline__ void discover(int64_t v, uint64_t fresh, int32_t leve
     const int rank = __popcll(mask & ((1ULL << lane()) - 1ULL));
     int64_t deg = 0;
     if (mask) {
-        deg = take ? view_degree(push, v) : 0;
+        deg = take ? push_degree(push, v) : 0;
         int64_t dsum = deg;
         unsigned long long b = take ? static_cast<unsigned long long>(__popcll(fresh)) : 0ULL;
         for (int off = 32; off > 0; off >>= 1) {
@@ -201,53 +189,13 @@ __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t 
 __global__ void __launch_bounds__(kBlock) ms_push(View push, const int32_t* __restrict__ q,
         const int64_t* __restrict__ qpre, int64_t qlen, const uint64_t* __restrict__ fr,
         const uint64_t* __restrict__ vis, uint64_t* __restrict__ nx) {
-    __shared__ int64_t s_pre[kLdsEntries];
-    __shared__ int32_t s_q[kLdsEntries];
-    __shared__ int64_t s_lo, s_hi;
-    const int64_t total = qpre[qlen];
-    const int64_t ntiles = (total + kTileEdges - 1) / kTileEdges;
-    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const int64_t t0 = tile * kTileEdges;
-        const int64_t t1 = min(total, t0 + kTileEdges);
-        if (threadIdx.x == 0) {
-            int64_t a = 0, b = qlen;
-            while (b - a > 1) { const int64_t c = (a + b) >> 1; if (qpre[c] <= t0) a = c; else b = c; }
-            s_lo = a;
-            int64_t a2 = a, b2 = qlen;
-            while (b2 - a2 > 1) { const int64_t c = (a2 + b2) >> 1; if (qpre[c] <= t1 - 1) a2 = c; else b2 = c; }
-            s_hi = a2;
-        }
-        __syncthreads();
-        const int64_t lo = s_lo, hi = s_hi;
-        const int64_t span = hi - lo + 1;
-        const bool in_lds = span + 1 <= kLdsEntries;
-        if (in_lds) {
-            for (int64_t i = threadIdx.x; i <= span; i += kBlock) {
-                s_pre[i] = qpre[lo + i];
-                if (i < span) s_q[i] = q[lo + i];
-            }
-        }
-        __syncthreads();
-        for (int k = 0; k < kEdgesPerThread; ++k) {
-            const int64_t j = t0 + k * kBlock + threadIdx.x;
-            if (j >= t1) break;
-            int32_t u; int64_t start;
-            if (in_lds) {
-                int64_t a = 0, b = span;
-                while (b - a > 1) { const int64_t c = (a + b) >> 1; if (s_pre[c] <= j) a = c; else b = c; }
-                u = s_q[a]; start = s_pre[a];
-            } else {
-                int64_t a = lo, b = hi + 1;
-                while (b - a > 1) { const int64_t c = (a + b) >> 1; if (qpre[c] <= j) a = c; else b = c; }
-                u = q[a]; start = qpre[a];
-            }
-            const int32_t v = view_entry(push, u, j - start);
-            // partitioned graphs pass vis = nullptr: remote vertices' masks are not local
-            const uint64_t m = vis ? (fr[u] & ~vis[v]) : fr[u];
-            if (m && (nx[v] & m) != m) atomicOr(reinterpret_cast<unsigned long long*>(&nx[v]), m);
-        }
-        __syncthreads();
-    }
+    for_each_queue_edge(q, qpre, qlen, [&](bool valid, int32_t u, int64_t o) {
+        if (!valid) return;
+        const int32_t v = view_entry(push, u, o);
+        // partitioned graphs pass vis = nullptr: remote vertices' masks are not local
+        const uint64_t m = vis ? (fr[u] & ~vis[v]) : fr[u];
+        if (m && (nx[v] & m) != m) atomicOr(reinterpret_cast<unsigned long long*>(&nx[v]), m);
+    });
 }
 
 // After a push level: settle the candidates (nx & ~vis), record levels, build the queue.
@@ -330,7 +278,7 @@ __global__ void __launch_bounds__(kBlock) ms_reach(View v, const uint64_t* __res
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n_active; i += (int64_t)gridDim.x * blockDim.x) {
         uint64_t b = vis[i];
         if (!b) continue;
-        const unsigned long long d = static_cast<unsigned long long>(view_degree(v, i));
+        const unsigned long long d = static_cast<unsigned long long>(push_degree(v, i));
         while (b) {
             const int r = __ffsll(static_cast<long long>(b)) - 1;
             b &= b - 1;

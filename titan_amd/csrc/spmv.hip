@@ -328,8 +328,9 @@ hipError_t k_pr_iter(const DevCsr& in, const RowBlocks& rb, const double* contri
     if (t.diag_hi > t.diag_lo) return run_gather(in, rb, PrDiagOp{contrib, t.diag_lo, t.diag_hi}, fin, partial, s);
     return run_gather(in, rb, PrOp{contrib}, fin, partial, s);
 }
-hipError_t k_pr_iter_cold(const ColdBlocks& cb, const double* contrib, const double* edge_count, double* pr,
-                          double* contrib_next, double* partial_long, double alpha, double base, hipStream_t s) {
+// Cold phase: the cold segments' partial sums, folded per row into csum (reads only the cold
+// sources [hot, n_src) of `contrib`).
+hipError_t k_pr_cold_phase(const ColdBlocks& cb, const double* contrib, hipStream_t s) {
     if (cb.max_xcd_blocks > 0) {
         const unsigned g = static_cast<unsigned>(cb.max_xcd_blocks * 8);
         if (cb.cpacked)
@@ -339,11 +340,15 @@ hipError_t k_pr_iter_cold(const ColdBlocks& cb, const double* contrib, const dou
             cold_gather<false><<<g, kBlock, 0, s>>>(cb.poff, cb.cadj, cb.bbeg, cb.bend, cb.xblk, cb.bsrc, cb.xbase, contrib,
                                                     cb.partial);
     }
-    {
-        int64_t g = (cb.n_crows + kBlock - 1) / kBlock;
-        g = std::max<int64_t>(1, std::min<int64_t>(g, 65536));
-        cold_fold<<<static_cast<unsigned>(g), kBlock, 0, s>>>(cb.crow, cb.n_crows, cb.cptr, cb.cpid, cb.partial, cb.csum);
-    }
+    int64_t g = (cb.n_crows + kBlock - 1) / kBlock;
+    g = std::max<int64_t>(1, std::min<int64_t>(g, 65536));
+    cold_fold<<<static_cast<unsigned>(g), kBlock, 0, s>>>(cb.crow, cb.n_crows, cb.cptr, cb.cpid, cb.partial, cb.csum);
+    return hipGetLastError();
+}
+
+// Hot phase: every row's hot entries (sources [0, hot)) + its folded cold sum -> the update.
+hipError_t k_pr_hot_phase(const ColdBlocks& cb, const double* contrib, const double* edge_count, double* pr,
+                          double* contrib_next, double* partial_long, double alpha, double base, hipStream_t s) {
     const PrColdFinal fin{PrFinal{edge_count, pr, contrib_next, alpha, base}, cb.csum};
     if (!cb.packed) return run_gather(cb.hcsr, cb.rb_hot, PrOp{contrib}, fin, partial_long, s);
     const RowBlocks& rb = cb.rb_hot;
@@ -358,6 +363,13 @@ hipError_t k_pr_iter_cold(const ColdBlocks& cb, const double* contrib, const dou
                                                                                    partial_long, fin);
     }
     return hipGetLastError();
+}
+
+hipError_t k_pr_iter_cold(const ColdBlocks& cb, const double* contrib, const double* edge_count, double* pr,
+                          double* contrib_next, double* partial_long, double alpha, double base, hipStream_t s) {
+    hipError_t e = k_pr_cold_phase(cb, contrib, s);
+    if (e != hipSuccess) return e;
+    return k_pr_hot_phase(cb, contrib, edge_count, pr, contrib_next, partial_long, alpha, base, s);
 }
 hipError_t k_walk_iter(const DevCsr& out, const RowBlocks& rb, const int32_t* prev, int32_t* next,
                        int32_t* partial, int64_t n, hipStream_t s) {

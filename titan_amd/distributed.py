@@ -9,8 +9,11 @@ exchange through torch.distributed — backend "nccl", i.e. RCCL over xGMI on MI
                          -> owners OR the slices and claim unvisited vertices
   BFS bottom-up level  : all_gather_into_tensor of owned next-frontier bitmap slices
                          (n/8 bytes in total) -> unvisited owned vertices probe it
-  PageRank iteration   : all_gather_into_tensor of owned fp64 contributions (8n bytes)
-  every level          : all_reduce(SUM) of (frontier size, frontier entries)
+  PageRank iteration   : all_gather_into_tensor of owned fp64 contributions (8n bytes), or
+                         cache-blocked: cold slices, then hot slices overlapping the cold
+                         gather kernels (tgo_part_pr_blocked; entry-less rows not sent)
+  every level          : all_reduce(SUM) of (frontier size, frontier entries), reduced in
+                         place on the device and read once (tgo_part_device_counts)
 
 RCCL has no bitwise-OR reduction, hence slice exchanges (all-to-all / all-gather) instead
 of an all-reduce of bitmaps.  The direction switch is Beamer's, on global counts.
@@ -61,6 +64,53 @@ def all_gather_layout(src, dst, n_global: int, lo: int, hi: int, device, group=N
     return out.cpu().numpy()
 
 
+_MASK64 = (1 << 64) - 1
+
+
+def _splitmix64(x: int) -> int:
+    x = (x + 0x9E3779B97F4A7C15) & _MASK64
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & _MASK64
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & _MASK64
+    return x ^ (x >> 31)
+
+
+def pick_roots_partitioned(n_global: int, src, dst, lo: int, hi: int, nroots: int, seed: int, device, group=None):
+    """The roots tgo_pick_roots draws on the whole edge list (synth.cpp), from a rank's
+    partition edges: owned "has an entry" flags are all-gathered (n bytes), then every rank
+    walks the same splitmix64 candidate sequence — the partitioned bench runs the same
+    sources as the one-GPU bench."""
+    has = np.zeros(hi - lo, np.uint8)
+    for x in (src, dst):
+        x = np.asarray(x)
+        has[x[(x >= lo) & (x < hi)] - lo] = 1
+    loc = torch.from_numpy(has).to(device)
+    out = torch.empty(n_global, dtype=torch.uint8, device=device)
+    dist.all_gather_into_tensor(out, loc, group=group)
+    has = out.cpu().numpy()
+    if int(has.sum()) < nroots:
+        raise ValueError("fewer vertices with entries than roots")
+    roots, used, i = [], set(), 0
+    base = (seed * 0x9E3779B97F4A7C15) & _MASK64
+    while len(roots) < nroots:
+        v = _splitmix64((base + i) & _MASK64) % n_global
+        i += 1
+        if has[v] and v not in used:
+            used.add(v)
+            roots.append(v)
+    return roots
+
+
+def entry_imbalance(entries_local: int, device, group=None):
+    """Per-rank owned entries, all-gathered: (list, max / mean) — the load imbalance of the
+    1-D partition."""
+    t = torch.tensor([int(entries_local)], dtype=torch.int64, device=device)
+    out = torch.empty(dist.get_world_size(group), dtype=torch.int64, device=device)
+    dist.all_gather_into_tensor(out, t, group=group)
+    e = [int(x) for x in out.cpu()]
+    mean = sum(e) / len(e)
+    return e, (max(e) / mean if mean else 1.0)
+
+
 def exchange_stream() -> int:
     """The HIP stream handle the partitioned engine must share with torch's collectives.
     torch's default stream has handle 0, which the C-ABI reads as "ctx-owned stream" (not
@@ -77,7 +127,11 @@ class HipPartBackend:
     engine runs on torch's current (non-default) stream, so its kernels and the RCCL
     collectives of the driver are ordered on one stream (see exchange_stream)."""
 
-    def __init__(self, engine, n_global, lo, hi):
+    # steps whose level counts can stay on the device (tgo_part_device_counts)
+    DEVICE_COUNT_STEPS = frozenset({"tgo_part_bfs_claim", "tgo_part_bfs_bu", "tgo_part_ms_pull", "tgo_part_ms_settle",
+                                    "tgo_part_ms_settle_pairs"})
+
+    def __init__(self, engine, n_global, lo, hi, device_counts=False):
         if engine.stream == 0 or engine.stream != torch.cuda.current_stream().cuda_stream:
             raise ValueError("HipPartBackend: the Engine must run on torch's current non-default stream "
                              "(Engine(stream=exchange_stream()))")
@@ -86,6 +140,12 @@ class HipPartBackend:
         self.n_local = hi - lo
         self.device = torch.device("cuda", torch.cuda.current_device())
         self.total_entries = int(engine.stats()["out_entries"] + engine.stats()["in_entries"])
+        # device_counts: level counts are returned as this device tensor (all-reduced in
+        # place by the driver, read once per level) instead of a host array per call
+        self.dc = None
+        if device_counts:
+            self.dc = torch.zeros(2, dtype=torch.int64, device=self.device)
+            engine.part_call("tgo_part_device_counts", self._vp(self.dc))
 
     def tensor(self, n, dtype):
         return torch.zeros(n, dtype=dtype, device=self.device)
@@ -95,6 +155,9 @@ class HipPartBackend:
         return C.c_void_p(t.data_ptr())
 
     def _counts(self, fn, *args):
+        if self.dc is not None and fn in self.DEVICE_COUNT_STEPS:
+            self.e.part_call(fn, *args, None)
+            return self.dc
         c = np.zeros(2, np.int64)
         self.e.part_call(fn, *args, L.ptr(c, C.c_int64))
         return c
@@ -183,12 +246,29 @@ class HipPartBackend:
         self.e.part_call("tgo_part_sssp_end", L.ptr(out, C.c_int64), L.ptr(reached, C.c_int64))
         return out, reached
 
+    def active_rows(self):
+        a = C.c_int64()
+        self.e.part_call("tgo_part_active_rows", C.byref(a))
+        return a.value
+
+    def pr_layout(self, world, active_span):
+        """Hot rows per rank of the blocked gathered layout (tgo_part_pr_blocked); 0 = plain."""
+        h = C.c_int64()
+        self.e.part_call("tgo_part_pr_blocked", int(world), C.c_int64(active_span), C.byref(h))
+        return h.value
+
     def pr_begin(self, alpha, vertex_count, iters, contrib_local):
         a = L.PrArgs(alpha, int(vertex_count), int(iters), 0)
         self.e.part_call("tgo_part_pr_begin", C.byref(a), self._vp(contrib_local))
 
     def pr_step(self, contrib_global, contrib_local):
         self.e.part_call("tgo_part_pr_step", self._vp(contrib_global), self._vp(contrib_local))
+
+    def pr_step_cold(self, gathered):
+        self.e.part_call("tgo_part_pr_step_cold", self._vp(gathered))
+
+    def pr_step_hot(self, gathered, contrib_local):
+        self.e.part_call("tgo_part_pr_step_hot", self._vp(gathered), self._vp(contrib_local))
 
     def pr_end(self, fetch=True):
         out = np.zeros(self.n_local, np.float64) if fetch else None
@@ -197,8 +277,9 @@ class HipPartBackend:
 
 
 def _allreduce_counts(c, device, group):
-    """Global sums of per-rank counters (frontier size / entries, reached, ...) over `group`."""
-    t = torch.tensor(c, dtype=torch.int64, device=device)
+    """Global sums of per-rank counters (frontier size / entries, reached, ...) over `group`.
+    A device tensor (HipPartBackend device_counts) is reduced in place: one read per level."""
+    t = c if isinstance(c, torch.Tensor) else torch.tensor(c, dtype=torch.int64, device=device)
     dist.all_reduce(t, group=group)
     return t.cpu().numpy()
 
@@ -362,15 +443,54 @@ def distributed_sssp(backend, seed: int, delta: int = 0, fetch: bool = True, sta
     return out, reached, phases
 
 
+def gathered_index(u, n_local: int, world: int, hot: int, span: int):
+    """Position of global source u in the blocked gathered contribution vector
+    (tgo_part_pr_blocked): rank-major hot slices [0, hot) first, then the cold slices
+    [hot, span) — the layout the two all-gathers of distributed_pagerank produce."""
+    u = np.asarray(u, np.int64)
+    r, o = u // n_local, u % n_local
+    return np.where(o < hot, r * hot + o, world * hot + r * (span - hot) + (o - hot))
+
+
+def pagerank_layout(backend, group=None):
+    """(hot rows per rank H, active span A) agreed by every rank: A = max active rows
+    (all-reduce MAX), H from the backend (0 = plain rank-major layout, A = n_local)."""
+    world = dist.get_world_size(group)
+    t = torch.tensor([backend.active_rows()], dtype=torch.int64, device=backend.device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    span = int(t.item())
+    hot = backend.pr_layout(world, span)
+    return (hot, span) if hot > 0 else (0, backend.n_local)
+
+
 def distributed_pagerank(backend, alpha: float, vertex_count: int, iterations: int, fetch: bool = True,
-                         group=None):
-    """PageRankVertexProgram on a vertex-partitioned graph; returns local ranks."""
+                         group=None, layout=None, overlap: bool = True):
+    """PageRankVertexProgram on a vertex-partitioned graph; returns local ranks.
+      plain   : all_gather of the owned contributions (8 n_local B per rank) -> local update
+      blocked : (pagerank_layout) cold slices [H, A) all-gathered first; the hot slices
+                [0, H) all-gather asynchronously while the cold segments are gathered
+                (pr_step_cold); then the hot pass finishes the update (pr_step_hot).  Rows
+                past A hold no entries anywhere and are not exchanged."""
     if iterations == 0:
         return np.full(backend.n_local, np.nan) if fetch else None
+    world = dist.get_world_size(group)
+    hot, span = layout if layout is not None else pagerank_layout(backend, group)
     contrib_local = backend.tensor(backend.n_local, torch.float64)
-    contrib_global = backend.tensor(backend.n_global, torch.float64)
+    contrib_global = backend.tensor(world * span, torch.float64)
     backend.pr_begin(alpha, vertex_count, iterations, contrib_local)
     for _ in range(2, iterations + 1):
-        dist.all_gather_into_tensor(contrib_global, contrib_local, group=group)
-        backend.pr_step(contrib_global, contrib_local)
+        if hot == 0:
+            dist.all_gather_into_tensor(contrib_global, contrib_local, group=group)
+            backend.pr_step(contrib_global, contrib_local)
+            continue
+        dist.all_gather_into_tensor(contrib_global[world * hot:], contrib_local[hot:span], group=group)
+        if not overlap:
+            dist.all_gather_into_tensor(contrib_global[:world * hot], contrib_local[:hot], group=group)
+            backend.pr_step(contrib_global, contrib_local)
+            continue
+        work = dist.all_gather_into_tensor(contrib_global[:world * hot], contrib_local[:hot], group=group,
+                                           async_op=True)
+        backend.pr_step_cold(contrib_global)
+        work.wait()
+        backend.pr_step_hot(contrib_global, contrib_local)
     return backend.pr_end(fetch)
