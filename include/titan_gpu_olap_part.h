@@ -56,6 +56,8 @@ int tgo_part_bfs_begin(tgo_ctx* ctx, int64_t seed_global, uint64_t* nb_local, in
 int tgo_part_bfs_td(tgo_ctx* ctx, int32_t level, uint64_t* disc_global);
 int tgo_part_bfs_claim(tgo_ctx* ctx, int32_t level, const uint64_t* recv, int32_t nslices,
                        uint64_t* nb_local, int64_t* counts);
+/* bfs_bu only counts the next frontier (nb_local); a following bfs_td queues it from
+ * nb_local, which the caller must leave unchanged until then (the all-gather reads it). */
 int tgo_part_bfs_bu(tgo_ctx* ctx, int32_t level, const uint64_t* fb_global, uint64_t* nb_local,
                     int64_t* counts);
 /* Local distances (TGO_DIST_ABSENT = unreached) and reached[2] = {vertices, list entries}. */
@@ -81,6 +83,10 @@ int tgo_part_ms_settle(tgo_ctx* ctx, int32_t level, const uint64_t* recv, int32_
  * n_global.  Pair order within a rank's run is unspecified; results are not affected (the
  * masks are OR-ed). */
 int tgo_part_ms_pack(tgo_ctx* ctx, uint64_t* cand_global, int32_t nranks, int64_t* send, int64_t* send_counts);
+/* tgo_part_ms_pack without the host round trip: send_elems_dev (DEVICE int64[nranks])
+ * receives the int64 element count per destination (2 per pair), stream-ordered, for a
+ * device all-to-all of the split sizes. */
+int tgo_part_ms_pack_dev(tgo_ctx* ctx, uint64_t* cand_global, int32_t nranks, int64_t* send, int64_t* send_elems_dev);
 int tgo_part_ms_settle_pairs(tgo_ctx* ctx, int32_t level, const int64_t* recv, const int64_t* recv_counts,
                              int32_t nslices, uint64_t* fr_next, int64_t* counts);
 /* reached / entries: per seed, over this rank's vertices (NULL to skip). */

@@ -236,6 +236,10 @@ class NumpyPartBackend:
         r = self._u(recv).reshape(nslices, -1)
         return self._ms_fresh(level, np.bitwise_or.reduce(r, axis=0), fr_next)
 
+    def ms_pack_dev(self, cand, send, nranks, send_elems):
+        """tgo_part_ms_pack_dev: the split sizes (int64 elements) land in a tensor."""
+        send_elems.copy_(torch.from_numpy(2 * np.asarray(self.ms_pack(cand, send, nranks), np.int64)))
+
     def ms_pack(self, cand, send, nranks):
         c = self._u(cand)
         s = send.numpy()

@@ -39,6 +39,8 @@ struct tgo_ctx {
     std::vector<void*> allocs;
     int part_cur = 0;           // partitioned BFS: queue buffer holding the frontier
     int64_t part_qlen = 0;      // its length
+    bool part_queued = true;    // q[part_cur] holds the frontier (pull / bottom-up levels only count it)
+    const uint64_t* part_frontier = nullptr;   // after bottom-up: the caller's nb_local (queued lazily)
     int64_t* part_dcounts = nullptr;    // caller's device counts (tgo_part_device_counts)
     int64_t* part_qlen_dev = nullptr;   // device copy of the queue length (lazy host read)
     bool part_qlen_stale = false;       // part_qlen must be read from part_qlen_dev
@@ -364,6 +366,7 @@ int run_bfs(tgo_ctx* ctx, int64_t seed, int max_depth, int scope) {
                                                    : (g.has_transpose ? g.push_t.nnz
                                                                       : (scope == TGO_SCOPE_IN_E ? g.in.nnz : g.out.nnz));
         int64_t mf = -1, mu = total_push;
+        bool queued = true;         // q[cur] holds the frontier (bottom-up levels only count it)
         for (int L = 0; L < max_depth && qlen > 0; ++L) {
             if (mf < 0) {   // degree of the seed
                 int64_t d = 0;
@@ -374,11 +377,16 @@ int run_bfs(tgo_ctx* ctx, int64_t seed, int max_depth, int scope) {
             }
             if (!bottom_up && static_cast<double>(mf) > static_cast<double>(mu) / alpha) bottom_up = true;
             else if (bottom_up && static_cast<double>(qlen) < static_cast<double>(n) / beta) bottom_up = false;
+            if (!bottom_up && !queued) {    // after bottom-up levels: queue the frontier bitmap
+                HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
+                HIP_TRY(k_bfs_queue(push, g.n_active, s.fb, s.q[cur], s.qdeg, s.cnt, st));
+            }
+            queued = !bottom_up;
             HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
             HIP_TRY(hipMemsetAsync(s.nb, 0, words * 8, st));
             if (bottom_up) {
                 // words past n_active hold only entry-less vertices: nothing to find there
-                HIP_TRY(k_bu_step(pull, push, g.n_active, s.fb, s.vb, s.nb, s.level, s.q[cur ^ 1], s.qdeg, s.cnt, L + 1, st));
+                HIP_TRY(k_bu_step(pull, push, g.n_active, s.fb, s.vb, s.nb, s.level, s.cnt, L + 1, st));
             } else {
                 int rc = scan_frontier(ctx, qlen);
                 if (rc) return rc;
@@ -843,12 +851,18 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
     uint64_t* fr = s.ms_fr;
     uint64_t* nx = s.ms_nx;
     int cur = 0, levels = 0;
+    bool queued = true;         // q[cur] holds the frontier (pull levels only count it)
     for (int L = 0; L < depth && qlen > 0; ++L) {
         const bool use_pull = static_cast<double>(mf) * ms_alpha > static_cast<double>(total);
         if ((rc = ms_planes_for(ctx, L + 1))) return rc;
+        if (!use_pull && !queued) {     // the frontier's queue, for the push level's scan
+            HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
+            HIP_TRY(k_ms_queue(push, g.n_active, fr, s.q[cur], s.qdeg, s.cnt, st));
+        }
         HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
+        queued = !use_pull;
         if (use_pull) {
-            HIP_TRY(k_ms_pull(pull, push, g.n_active, full, fr, s.ms_vis, nx, ms_planes(ctx), s.q[cur ^ 1], s.qdeg, s.cnt, L + 1, st));
+            HIP_TRY(k_ms_pull(pull, push, g.n_active, full, fr, s.ms_vis, nx, ms_planes(ctx), s.cnt, L + 1, st));
         } else {
             HIP_TRY(hipMemsetAsync(nx, 0, n * 8, st));
             if ((rc = scan_frontier(ctx, qlen))) return rc;
@@ -1128,6 +1142,7 @@ int tgo_part_bfs_begin(tgo_ctx* ctx, int64_t seed_global, uint64_t* nb_local, in
     HIP_TRY(hipMemsetAsync(nb_local, 0, words * 8, st));
     HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
     ctx->part_cur = 0;
+    ctx->part_queued = true;
     ctx->part_qlen = 0;
     ctx->part_qlen_stale = false;
     int64_t deg = 0;
@@ -1154,6 +1169,11 @@ int tgo_part_bfs_td(tgo_ctx* ctx, int32_t level, uint64_t* disc_global) {
     const View push = push_view(g, TGO_SCOPE_BOTH_E);
     int64_t qlen = 0;
     if ((rc = part_qlen_now(ctx, qlen))) return rc;
+    if (qlen > 0 && !ctx->part_queued) {
+        HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
+        HIP_TRY(k_bfs_queue(push, g.n_active, ctx->part_frontier, s.q[ctx->part_cur], s.qdeg, s.cnt, st));
+        ctx->part_queued = true;
+    }
     if (qlen > 0) {
         if ((rc = scan_frontier(ctx, ctx->part_qlen))) return rc;
         HIP_TRY(k_part_td_mark(push, s.q[ctx->part_cur], s.qpre, ctx->part_qlen, disc_global, s.vb, g.lo, g.n, st));
@@ -1174,6 +1194,7 @@ int tgo_part_bfs_claim(tgo_ctx* ctx, int32_t level, const uint64_t* recv, int32_
     HIP_TRY(k_part_claim(push, recv, nslices, g.n / 64, g.n, s.vb, nb_local, s.level, s.q[nxt], s.qdeg, s.cnt,
                          level + 1, st));
     ctx->part_cur = nxt;
+    ctx->part_queued = true;
     return part_counts(ctx, counts);
 }
 
@@ -1187,8 +1208,10 @@ int tgo_part_bfs_bu(tgo_ctx* ctx, int32_t level, const uint64_t* fb_global, uint
     HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
     HIP_TRY(hipMemsetAsync(nb_local, 0, (g.n / 64) * 8, st));
     const int nxt = ctx->part_cur ^ 1;
-    HIP_TRY(k_bu_step(pull, push, g.n_active, fb_global, s.vb, nb_local, s.level, s.q[nxt], s.qdeg, s.cnt, level + 1, st));
+    HIP_TRY(k_bu_step(pull, push, g.n_active, fb_global, s.vb, nb_local, s.level, s.cnt, level + 1, st));
     ctx->part_cur = nxt;
+    ctx->part_queued = false;       // counted only: bfs_td queues nb_local if it runs next
+    ctx->part_frontier = nb_local;
     return part_counts(ctx, counts);
 }
 
@@ -1250,6 +1273,7 @@ int tgo_part_ms_begin(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, uint64
     HIP_TRY(hipMemcpyAsync(s.ms_seeds, local.data(), nseeds * sizeof(int64_t), hipMemcpyHostToDevice, st));
     HIP_TRY(k_ms_seed(s.ms_seeds, nseeds, s.ms_vis, fr_local, st));
     ctx->part_cur = 0;
+    ctx->part_queued = true;
     ctx->part_qlen = static_cast<int64_t>(uniq.size());
     ctx->part_qlen_stale = false;
     int64_t mf = 0;
@@ -1279,9 +1303,9 @@ int tgo_part_ms_pull(tgo_ctx* ctx, int32_t level, const uint64_t* fr_global, uin
     HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
     HIP_TRY(hipMemsetAsync(fr_next, 0, g.n * 8, st));
     const int nxt = ctx->part_cur ^ 1;
-    HIP_TRY(k_ms_pull(pull, push, g.n_active, full, fr_global, s.ms_vis, fr_next, ms_planes(ctx), s.q[nxt], s.qdeg, s.cnt,
-                      level + 1, st));
+    HIP_TRY(k_ms_pull(pull, push, g.n_active, full, fr_global, s.ms_vis, fr_next, ms_planes(ctx), s.cnt, level + 1, st));
     ctx->part_cur = nxt;
+    ctx->part_queued = false;       // counted only: ms_push builds the queue if it needs one
     return part_counts(ctx, counts);
 }
 
@@ -1293,6 +1317,11 @@ int tgo_part_ms_push(tgo_ctx* ctx, int32_t level, const uint64_t* fr_local, uint
     Scratch& s = ctx->sc;
     int64_t qlen = 0;
     if ((rc = part_qlen_now(ctx, qlen))) return rc;
+    if (qlen > 0 && !ctx->part_queued) {
+        HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), ctx->stream));
+        HIP_TRY(k_ms_queue(push_view(g, TGO_SCOPE_BOTH_E), g.n, fr_local, s.q[ctx->part_cur], s.qdeg, s.cnt, ctx->stream));
+        ctx->part_queued = true;
+    }
     if (qlen > 0) {
         if ((rc = scan_frontier(ctx, ctx->part_qlen))) return rc;
         HIP_TRY(k_ms_push(push_view(g, TGO_SCOPE_BOTH_E), s.q[ctx->part_cur], s.qpre, ctx->part_qlen, fr_local,
@@ -1316,6 +1345,7 @@ int tgo_part_ms_settle(tgo_ctx* ctx, int32_t level, const uint64_t* recv, int32_
     HIP_TRY(k_ms_settle(push_view(g, TGO_SCOPE_BOTH_E), g.n, s.ms_vis, fr_next, ms_planes(ctx), s.q[nxt], s.qdeg, s.cnt,
                         level + 1, st));
     ctx->part_cur = nxt;
+    ctx->part_queued = true;
     return part_counts(ctx, counts);
 }
 
@@ -1346,6 +1376,31 @@ int tgo_part_ms_pack(tgo_ctx* ctx, uint64_t* cand_global, int32_t nranks, int64_
     return part_done(ctx);
 }
 
+// Device form of tgo_part_ms_pack: no host synchronisation — the split sizes (int64
+// elements, 2 per pair) go to send_elems_dev for the caller's device all-to-all.
+int tgo_part_ms_pack_dev(tgo_ctx* ctx, uint64_t* cand_global, int32_t nranks, int64_t* send, int64_t* send_elems_dev) {
+    int rc = part_check(ctx);
+    if (rc) return rc;
+    DevGraph& g = ctx->g;
+    Scratch& s = ctx->sc;
+    if (!cand_global || !send || !send_elems_dev || nranks < 1 || nranks > kMaxRanks ||
+        static_cast<int64_t>(nranks) * g.n != g.n_global)
+        return fail(ctx, TGO_E_INVALID, "ms_pack_dev: bad arguments (nranks * n_local must equal n_global)");
+    hipStream_t st = ctx->stream;
+    const int64_t cps = (g.n + kPackChunk - 1) / kPackChunk;
+    const int64_t nchunks = cps * nranks;
+    if (!s.pk_cnt) {
+        HIP_TRY(dev_alloc(ctx, s.pk_cnt, g.n_global / kPackChunk + kMaxRanks + 1));
+        HIP_TRY(dev_alloc(ctx, s.pk_off, g.n_global / kPackChunk + kMaxRanks + 1));
+    }
+    HIP_TRY(hipMemsetAsync(s.pk_cnt + nchunks, 0, sizeof(int64_t), st));
+    HIP_TRY(k_ms_pack(false, cand_global, g.n, cps, nchunks, s.pk_cnt, s.pk_off, send, st));
+    HIP_TRY(scan_exclusive_i64(s.cub_tmp, s.cub_bytes, s.pk_cnt, s.pk_off, nchunks + 1, st));
+    HIP_TRY(k_slice_elems(s.pk_off, cps, nranks, send_elems_dev, st));
+    HIP_TRY(k_ms_pack(true, cand_global, g.n, cps, nchunks, s.pk_cnt, s.pk_off, send, st));
+    return part_done(ctx);
+}
+
 int tgo_part_ms_settle_pairs(tgo_ctx* ctx, int32_t level, const int64_t* recv, const int64_t* recv_counts,
                              int32_t nslices, uint64_t* fr_next, int64_t* counts) {
     int rc = part_check(ctx);
@@ -1369,6 +1424,7 @@ int tgo_part_ms_settle_pairs(tgo_ctx* ctx, int32_t level, const int64_t* recv, c
     HIP_TRY(k_ms_settle(push_view(g, TGO_SCOPE_BOTH_E), g.n, s.ms_vis, fr_next, ms_planes(ctx), s.q[nxt], s.qdeg, s.cnt,
                         level + 1, st));
     ctx->part_cur = nxt;
+    ctx->part_queued = true;
     return part_counts(ctx, counts);
 }
 

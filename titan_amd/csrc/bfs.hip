@@ -70,15 +70,14 @@ __global__ void __launch_bounds__(kBlock) td_expand(View push, const int32_t* __
     block_flush(cnt, sh, mf);
 }
 
-// Bottom-up: one wave per 64-vertex bitmap word.
+// Bottom-up: one wave per 64-vertex bitmap word.  The next frontier is counted (vertices,
+// push entries), not queued: bfs_queue builds the queue from nb when the next level is
+// top-down.  No block barrier inside, so waves with long lists do not hold up the block.
 __global__ void __launch_bounds__(kBlock) bu_step(View pull, View push, int64_t n,
         const uint64_t* __restrict__ fb, uint64_t* __restrict__ vb, uint64_t* __restrict__ nb,
-        int32_t* __restrict__ level, int32_t* __restrict__ qn, int64_t* __restrict__ qdeg_n,
-        Counters* cnt, int32_t next_level) {
-    __shared__ AppendLds sh;
-    unsigned long long mf = 0;
+        int32_t* __restrict__ level, Counters* cnt, int32_t next_level) {
+    unsigned long long nv = 0, mf = 0;
     const int64_t words = (n + 63) >> 6;
-    // block-uniform trips (block_append synchronises the block): wave w takes word b + w
     for (int64_t b = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock; b < words;
          b += static_cast<int64_t>(gridDim.x) * kWavesPerBlock) {
         const int64_t wd = b + (threadIdx.x >> 6);
@@ -136,10 +135,26 @@ __global__ void __launch_bounds__(kBlock) bu_step(View pull, View push, int64_t 
             nb[wd] = fm;
             if (fm) vb[wd] = vis | fm;
         }
-        if (found) level[v] = next_level;
-        block_append(found, static_cast<int32_t>(v), found ? push_degree(push, v) : 0, qn, qdeg_n, cnt, sh, mf);
+        if (found) {
+            level[v] = next_level;
+            ++nv;
+            mf += static_cast<unsigned long long>(push_degree(push, v));
+        }
     }
-    block_flush(cnt, sh, mf);
+    count_flush(cnt, nv, mf);
+}
+
+// Queue of the frontier bitmap fb (after a bottom-up level), push degrees for the scan.
+__global__ void __launch_bounds__(kBlock) bfs_queue(View push, int64_t n, const uint64_t* __restrict__ fb,
+        int32_t* __restrict__ qn, int64_t* __restrict__ qdeg, Counters* cnt) {
+    const int64_t words = (n + 63) >> 6;
+    auto probe = [&](int64_t wd, Take* t, bool) -> bool {
+        const int64_t v = (wd << 6) + lane();
+        const bool take = v < n && ((fb[wd] >> lane()) & 1ULL);
+        t[0] = {take, static_cast<int32_t>(v), take ? push_degree(push, v) : 0};
+        return true;
+    };
+    chunk_extract<1>(words, probe, qn, qdeg, cnt);
 }
 
 // Partitioned levels with device-resident counts: {qlen, push entries} for the caller's
@@ -311,13 +326,17 @@ hipError_t k_td_expand(const View& push, const int32_t* q, const int64_t* qpre, 
     td_expand<<<256 * 8, kBlock, 0, s>>>(push, q, qpre, qlen, level, vb, nb, qn, qdeg_n, cnt, next_level);
     return hipGetLastError();
 }
-hipError_t k_bu_step(const View& pull, const View& push, int64_t n, const uint64_t* fb, uint64_t* vb,
-                     uint64_t* nb, int32_t* level, int32_t* qn, int64_t* qdeg_n, Counters* cnt,
-                     int32_t next_level, hipStream_t s) {
+hipError_t k_bu_step(const View& pull, const View& push, int64_t n, const uint64_t* fb, uint64_t* vb, uint64_t* nb,
+                     int32_t* level, Counters* cnt, int32_t next_level, hipStream_t s) {
     // one wave per bitmap word, all launched at once: the dispatcher keeps every CU full
     // and a wave's dependent probe chain overlaps with hundreds of others.
     const int64_t words = (n + 63) / 64;
-    bu_step<<<grid_for(words * 64, kBlock, 8192), kBlock, 0, s>>>(pull, push, n, fb, vb, nb, level, qn, qdeg_n, cnt, next_level);
+    bu_step<<<grid_for(words * 64, kBlock, 8192), kBlock, 0, s>>>(pull, push, n, fb, vb, nb, level, cnt, next_level);
+    return hipGetLastError();
+}
+hipError_t k_bfs_queue(const View& push, int64_t n, const uint64_t* fb, int32_t* qn, int64_t* qdeg, Counters* cnt,
+                       hipStream_t s) {
+    bfs_queue<<<extract_grid((n + 63) / 64), kBlock, 0, s>>>(push, n, fb, qn, qdeg, cnt);
     return hipGetLastError();
 }
 hipError_t k_publish_counts(const Counters* c, int64_t* out, int64_t* slot, hipStream_t s) {

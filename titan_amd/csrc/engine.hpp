@@ -252,9 +252,11 @@ hipError_t k_bfs_seed(const View& push, int32_t* level, uint64_t* vb, uint64_t* 
 hipError_t k_td_expand(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen,
                        int32_t* level, uint64_t* vb, uint64_t* nb, int32_t* qn, int64_t* qdeg_n,
                        Counters* cnt, int32_t next_level, hipStream_t s);
-hipError_t k_bu_step(const View& pull, const View& push, int64_t n, const uint64_t* fb, uint64_t* vb,
-                     uint64_t* nb, int32_t* level, int32_t* qn, int64_t* qdeg_n, Counters* cnt,
-                     int32_t next_level, hipStream_t s);
+// bottom-up level: counts the next frontier (qlen, mf) without queueing it (k_bfs_queue)
+hipError_t k_bu_step(const View& pull, const View& push, int64_t n, const uint64_t* fb, uint64_t* vb, uint64_t* nb,
+                     int32_t* level, Counters* cnt, int32_t next_level, hipStream_t s);
+hipError_t k_bfs_queue(const View& push, int64_t n, const uint64_t* fb, int32_t* qn, int64_t* qdeg, Counters* cnt,
+                       hipStream_t s);
 hipError_t k_level_to_dist(const int32_t* level, int64_t* dist, int64_t n, hipStream_t s);
 hipError_t k_publish_counts(const Counters* c, int64_t* out, int64_t* slot, hipStream_t s);
 hipError_t k_reach_stats(const View& both_or_pull, const int64_t* dist, int64_t n,
@@ -304,8 +306,9 @@ hipError_t k_ds_apply(const View& push, const int64_t* recv, int64_t npairs, int
 hipError_t k_unpermute_i64(const int64_t* in, const int32_t* perm, int64_t* out, int64_t n, hipStream_t s);
 hipError_t k_ms_seed(const int64_t* seeds, int nseeds, uint64_t* vis, uint64_t* fr, hipStream_t s);
 hipError_t k_ms_pull(const View& pull, const View& push, int64_t n_active, uint64_t full, const uint64_t* fr,
-                     uint64_t* vis, uint64_t* nx, LevelPlanes lvl, int32_t* qn, int64_t* qdeg, Counters* cnt,
-                     int32_t next_level, hipStream_t s);
+                     uint64_t* vis, uint64_t* nx, LevelPlanes lvl, Counters* cnt, int32_t next_level, hipStream_t s);
+hipError_t k_ms_queue(const View& push, int64_t n_active, const uint64_t* fr, int32_t* qn, int64_t* qdeg, Counters* cnt,
+                      hipStream_t s);
 hipError_t k_ms_push(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen, const uint64_t* fr,
                      const uint64_t* vis, uint64_t* nx, hipStream_t s);
 hipError_t k_ms_settle(const View& push, int64_t n_active, uint64_t* vis, uint64_t* nx, LevelPlanes lvl, int32_t* qn,
@@ -318,6 +321,7 @@ hipError_t k_or_slices(const uint64_t* recv, int nslices, int64_t n_local, uint6
 constexpr int64_t kPackChunk = 2048;   // candidate words per wave in the sparse-exchange pack
 hipError_t k_ms_pack(bool write, uint64_t* cand, int64_t n_local, int64_t cps, int64_t nchunks, int64_t* cnt,
                      const int64_t* offs, int64_t* send, hipStream_t s);
+hipError_t k_slice_elems(const int64_t* off, int64_t cps, int nranks, int64_t* out, hipStream_t s);
 hipError_t k_ms_or_pairs(const int64_t* pairs, int64_t npairs, uint64_t* nx, hipStream_t s);
 hipError_t k_part_td_mark(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen,
                           uint64_t* disc, const uint64_t* vb_local, int64_t lo, int64_t n_local, hipStream_t s);

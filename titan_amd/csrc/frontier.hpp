@@ -137,6 +137,24 @@ __device__ __forceinline__ void block_flush(Counters* cnt, AppendLds& sh, unsign
     }
 }
 
+// End of a counting kernel: per-thread sums of the next frontier (vertices, push entries)
+// reduced over the block, one atomicAdd per block and counter (no per-trip barrier).
+__device__ __forceinline__ void count_flush(Counters* cnt, unsigned long long nv, unsigned long long mf) {
+    __shared__ unsigned long long s_nv[kWavesPerBlock], s_mf[kWavesPerBlock];
+    for (int off = 32; off > 0; off >>= 1) {
+        nv += __shfl_xor(nv, off, 64);
+        mf += __shfl_xor(mf, off, 64);
+    }
+    if (lane() == 0) { s_nv[threadIdx.x >> 6] = nv; s_mf[threadIdx.x >> 6] = mf; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long a = 0, m = 0;
+        for (int w = 0; w < kWavesPerBlock; ++w) { a += s_nv[w]; m += s_mf[w]; }
+        if (a) atomicAdd(&cnt->qlen, a);
+        if (m) atomicAdd(&cnt->mf, m);
+    }
+}
+
 // Bitmap extraction into a queue, two passes over a contiguous chunk of 64-vertex words per
 // block (one wave per word): pass 1 counts what the chunk takes, one atomicAdd per block
 // reserves its slots, pass 2 re-reads (L2-warm) and writes.  No per-trip block barriers or

@@ -27,69 +27,36 @@ __device__ __forceinline__ int32_t view_entry(const View& v, int64_t u, int64_t 
     return o < d0 ? v.adj0[b0 + o] : v.adj1[v.off1[u] + (o - d0)];
 }
 
-// Record the level of every newly reached source of v (bit k of the level goes into
-// plane k: one coalesced 8-byte OR per set level bit, the lane owns v); append v to the
-// next queue.  Block-aggregated: every thread of the block calls it in the same trip (the
-// callers' loops are block-uniform), the block reserves its queue slots with ONE atomicAdd,
-// and the frontier-degree / source-bit sums stay in the wave-leader's registers (mf, bits)
-// until discover_flush.  One contended counter word takes ~88 atomics/us
-// (MI355X_MICROARCH.md, dequeue), so per-wave counter atomics cost ~1.6 ms per dense level
-// on RMAT-24 — more than the level's gathers.
-constexpr int kWaves = kWavesPerBlock;
-struct DiscoverLds { unsigned long long cnt[kWaves]; unsigned long long base; };
-__device__ __forceinline__ void discover(int64_t v, uint64_t fresh, int32_t level, LevelPlanes pl,
-                                         const View& push, int32_t* qn, int64_t* qdeg, Counters* cnt,
-                                         DiscoverLds& sh, unsigned long long& mf, unsigned long long& bits) {
-    const bool take = fresh != 0;
-    if (take) {
-        for (int k = 0; k < kLevelPlanes && (level >> k); ++k)
-            if ((level >> k) & 1) pl.p[k * pl.stride + v] |= fresh;
-    }
-    const unsigned long long mask = __ballot(take);
-    const int wave = threadIdx.x >> 6;
-    const int rank = __popcll(mask & ((1ULL << lane()) - 1ULL));
-    int64_t deg = 0;
-    if (mask) {
-        deg = take ? push_degree(push, v) : 0;
-        int64_t dsum = deg;
-        unsigned long long b = take ? static_cast<unsigned long long>(__popcll(fresh)) : 0ULL;
-        for (int off = 32; off > 0; off >>= 1) {
-            dsum += __shfl_xor(dsum, off, 64);
-            b += __shfl_xor(b, off, 64);
-        }
-        mf += static_cast<unsigned long long>(dsum);
-        bits += b;
-    }
-    if (lane() == 0) sh.cnt[wave] = static_cast<unsigned long long>(__popcll(mask));
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long t = 0;
-        for (int w = 0; w < kWaves; ++w) { const unsigned long long c = sh.cnt[w]; sh.cnt[w] = t; t += c; }
-        sh.base = t ? atomicAdd(&cnt->qlen, t) : 0ULL;
-    }
-    __syncthreads();
-    if (take) {
-        const unsigned long long slot = sh.base + sh.cnt[wave] + static_cast<unsigned long long>(rank);
-        qn[slot] = static_cast<int32_t>(v);
-        qdeg[slot] = deg;
-    }
-}
-// End of a discovering kernel (block-uniform): one atomicAdd per block for each sum.
-__device__ __forceinline__ void discover_flush(Counters* cnt, DiscoverLds& sh, unsigned long long mf,
-                                               unsigned long long bits) {
-    __shared__ unsigned long long s_mf[kWaves], s_bits[kWaves];
-    if (lane() == 0) { s_mf[threadIdx.x >> 6] = mf; s_bits[threadIdx.x >> 6] = bits; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long a = 0, c = 0;
-        for (int w = 0; w < kWaves; ++w) { a += s_mf[w]; c += s_bits[w]; }
-        if (a) atomicAdd(&cnt->mf, a);
-        if (c) atomicAdd(&cnt->red[0], c);
-    }
-    (void)sh;
+// Record the level of every newly reached source of v: bit k of the level goes into plane k,
+// one coalesced 8-byte OR per set level bit (the lane owns v).
+__device__ __forceinline__ void record_level(int64_t v, uint64_t fresh, int32_t level, const LevelPlanes& pl) {
+    for (int k = 0; k < kLevelPlanes && (level >> k); ++k)
+        if ((level >> k) & 1) pl.p[k * pl.stride + v] |= fresh;
 }
 
-// Level 0 is all-zero level bits: seeding only marks vis/fr.
+// End of a counting kernel: per-thread sums of the next frontier (vertices, their push
+// entries, source bits) reduced over the block, one atomicAdd per block and counter.  No
+// per-word block barrier: a pull level's waves finish their words independently (lists are
+// skewed; a barrier per word made every wave wait for the block's longest list).
+__device__ __forceinline__ void count_flush(Counters* cnt, unsigned long long nv, unsigned long long mf,
+                                            unsigned long long bits) {
+    __shared__ unsigned long long s_nv[kWavesPerBlock], s_mf[kWavesPerBlock], s_bits[kWavesPerBlock];
+    for (int off = 32; off > 0; off >>= 1) {
+        nv += __shfl_xor(nv, off, 64);
+        mf += __shfl_xor(mf, off, 64);
+        bits += __shfl_xor(bits, off, 64);
+    }
+    if (lane() == 0) { s_nv[threadIdx.x >> 6] = nv; s_mf[threadIdx.x >> 6] = mf; s_bits[threadIdx.x >> 6] = bits; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long a = 0, m = 0, c = 0;
+        for (int w = 0; w < kWavesPerBlock; ++w) { a += s_nv[w]; m += s_mf[w]; c += s_bits[w]; }
+        if (a) atomicAdd(&cnt->qlen, a);
+        if (m) atomicAdd(&cnt->mf, m);
+        if (c) atomicAdd(&cnt->red[0], c);
+    }
+}
+
 __global__ void ms_seed(const int64_t* __restrict__ seeds, int nseeds, uint64_t* vis, uint64_t* fr) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         for (int r = 0; r < nseeds; ++r) {
@@ -108,14 +75,13 @@ constexpr int64_t kCoop = 64;
 constexpr int kStep = 8;
 __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t n_active, uint64_t full,
         const uint64_t* __restrict__ fr, uint64_t* __restrict__ vis, uint64_t* __restrict__ nx,
-        LevelPlanes lvl, int32_t* __restrict__ qn, int64_t* __restrict__ qdeg,
-        Counters* cnt, int32_t next_level) {
-    __shared__ DiscoverLds sh;
-    unsigned long long mf = 0, bits = 0;
+        LevelPlanes lvl, Counters* cnt, int32_t next_level) {
+    unsigned long long nv = 0, mf = 0, bits = 0;
     const int64_t words = (n_active + 63) >> 6;
-    // block-uniform trips (discover synchronises the block): wave w of the block takes word
-    // b + w; words past the end run as all-closed lanes
-    for (int64_t b = static_cast<int64_t>(blockIdx.x) * kWaves; b < words; b += static_cast<int64_t>(gridDim.x) * kWaves) {
+    // wave w of the block takes word b + w; words past the end run as all-closed lanes.  No
+    // block barrier inside: the next frontier is only counted here (ms_queue builds its queue
+    // if the next level pushes)
+    for (int64_t b = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock; b < words; b += static_cast<int64_t>(gridDim.x) * kWavesPerBlock) {
         const int64_t wd = b + (threadIdx.x >> 6);
         const int64_t v = (wd << 6) + lane();
         const uint64_t seen = v < n_active ? vis[v] : full;
@@ -180,9 +146,14 @@ __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t 
             nx[v] = fresh;
             if (fresh) vis[v] = seen | fresh;
         }
-        discover(v, fresh, next_level, lvl, push, qn, qdeg, cnt, sh, mf, bits);
+        if (fresh) {
+            record_level(v, fresh, next_level, lvl);
+            ++nv;
+            mf += static_cast<unsigned long long>(push_degree(push, v));
+            bits += static_cast<unsigned long long>(__popcll(fresh));
+        }
     }
-    discover_flush(cnt, sh, mf, bits);
+    count_flush(cnt, nv, mf, bits);
 }
 
 // Push level: edge-balanced over the frontier queue (exclusive scan of degrees in qpre).
@@ -198,15 +169,13 @@ __global__ void __launch_bounds__(kBlock) ms_push(View push, const int32_t* __re
     });
 }
 
-// After a push level: settle the candidates (nx & ~vis), record levels, build the queue.
+// After a push level: settle the candidates (nx & ~vis), record levels, build the queue
+// (two-pass chunked extraction, frontier.hpp).
 __global__ void __launch_bounds__(kBlock) ms_settle(View push, int64_t n_active, uint64_t* __restrict__ vis,
         uint64_t* __restrict__ nx, LevelPlanes lvl, int32_t* __restrict__ qn,
         int64_t* __restrict__ qdeg, Counters* cnt, int32_t next_level) {
-    __shared__ DiscoverLds sh;
-    unsigned long long mf = 0, bits = 0;
     const int64_t words = (n_active + 63) >> 6;
-    for (int64_t b = static_cast<int64_t>(blockIdx.x) * kWaves; b < words; b += static_cast<int64_t>(gridDim.x) * kWaves) {
-        const int64_t wd = b + (threadIdx.x >> 6);
+    auto probe = [&](int64_t wd, Take* t, bool commit) -> bool {
         const int64_t v = (wd << 6) + lane();
         uint64_t fresh = 0;
         if (v < n_active) {
@@ -214,13 +183,30 @@ __global__ void __launch_bounds__(kBlock) ms_settle(View push, int64_t n_active,
             if (c) {
                 const uint64_t seen = vis[v];
                 fresh = c & ~seen;
-                nx[v] = fresh;
-                if (fresh) vis[v] = seen | fresh;
+                if (commit) {
+                    nx[v] = fresh;
+                    if (fresh) { vis[v] = seen | fresh; record_level(v, fresh, next_level, lvl); }
+                }
             }
         }
-        discover(v, fresh, next_level, lvl, push, qn, qdeg, cnt, sh, mf, bits);
-    }
-    discover_flush(cnt, sh, mf, bits);
+        t[0] = {fresh != 0, static_cast<int32_t>(v), fresh ? push_degree(push, v) : 0};
+        return true;
+    };
+    chunk_extract<1>(words, probe, qn, qdeg, cnt);
+}
+
+// The queue of a frontier produced by a pull level (which only counts): every active v with
+// fr[v] != 0, push degrees for the scan.  Built only when the next level pushes.
+__global__ void __launch_bounds__(kBlock) ms_queue(View push, int64_t n_active, const uint64_t* __restrict__ fr,
+        int32_t* __restrict__ qn, int64_t* __restrict__ qdeg, Counters* cnt) {
+    const int64_t words = (n_active + 63) >> 6;
+    auto probe = [&](int64_t wd, Take* t, bool) -> bool {
+        const int64_t v = (wd << 6) + lane();
+        const bool take = v < n_active && fr[v] != 0;
+        t[0] = {take, static_cast<int32_t>(v), take ? push_degree(push, v) : 0};
+        return true;
+    };
+    chunk_extract<1>(words, probe, qn, qdeg, cnt);
 }
 
 // Partitioned push: OR the candidate-mask slices every rank sent for the owned vertices.
@@ -261,6 +247,12 @@ __global__ void __launch_bounds__(kBlock) ms_pack(uint64_t* __restrict__ cand, i
         base += __popcll(bal);
     }
     if (!kWrite && lane() == 0) cnt[c] = base;
+}
+// Per-destination element counts of the packed pairs (2 int64 per pair) from the chunk
+// offsets, for a device-side all-to-all of the split sizes.
+__global__ void slice_elems(const int64_t* __restrict__ off, int64_t cps, int nranks, int64_t* __restrict__ out) {
+    const int r = threadIdx.x;
+    if (blockIdx.x == 0 && r < nranks) out[r] = 2 * (off[(r + 1) * cps] - off[r * cps]);
 }
 // Received pairs of one sender: OR the masks into the owned candidate words (several
 // senders may name one vertex).
@@ -322,10 +314,13 @@ hipError_t k_ms_seed(const int64_t* seeds, int nseeds, uint64_t* vis, uint64_t* 
     return hipGetLastError();
 }
 hipError_t k_ms_pull(const View& pull, const View& push, int64_t n_active, uint64_t full, const uint64_t* fr,
-                     uint64_t* vis, uint64_t* nx, LevelPlanes lvl, int32_t* qn, int64_t* qdeg, Counters* cnt,
-                     int32_t next_level, hipStream_t s) {
-    ms_pull<<<grid_for(n_active, 8192), kBlock, 0, s>>>(pull, push, n_active, full, fr, vis, nx, lvl, qn, qdeg, cnt,
-                                                        next_level);
+                     uint64_t* vis, uint64_t* nx, LevelPlanes lvl, Counters* cnt, int32_t next_level, hipStream_t s) {
+    ms_pull<<<grid_for(n_active, 8192), kBlock, 0, s>>>(pull, push, n_active, full, fr, vis, nx, lvl, cnt, next_level);
+    return hipGetLastError();
+}
+hipError_t k_ms_queue(const View& push, int64_t n_active, const uint64_t* fr, int32_t* qn, int64_t* qdeg, Counters* cnt,
+                      hipStream_t s) {
+    ms_queue<<<extract_grid((n_active + 63) / 64), kBlock, 0, s>>>(push, n_active, fr, qn, qdeg, cnt);
     return hipGetLastError();
 }
 hipError_t k_ms_push(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen, const uint64_t* fr,
@@ -335,7 +330,8 @@ hipError_t k_ms_push(const View& push, const int32_t* q, const int64_t* qpre, in
 }
 hipError_t k_ms_settle(const View& push, int64_t n_active, uint64_t* vis, uint64_t* nx, LevelPlanes lvl, int32_t* qn,
                        int64_t* qdeg, Counters* cnt, int32_t next_level, hipStream_t s) {
-    ms_settle<<<grid_for(n_active, 8192), kBlock, 0, s>>>(push, n_active, vis, nx, lvl, qn, qdeg, cnt, next_level);
+    ms_settle<<<extract_grid((n_active + 63) / 64), kBlock, 0, s>>>(push, n_active, vis, nx, lvl, qn, qdeg, cnt,
+                                                                    next_level);
     return hipGetLastError();
 }
 hipError_t k_ms_reach(const View& v, const uint64_t* vis, int64_t n_active, int nsrc, unsigned long long* reached,
@@ -348,6 +344,10 @@ hipError_t k_ms_pack(bool write, uint64_t* cand, int64_t n_local, int64_t cps, i
     const unsigned blocks = static_cast<unsigned>((nchunks * 64 + kBlock - 1) / kBlock);
     if (write) ms_pack<true><<<blocks, kBlock, 0, s>>>(cand, n_local, cps, nchunks, cnt, offs, send);
     else ms_pack<false><<<blocks, kBlock, 0, s>>>(cand, n_local, cps, nchunks, cnt, offs, send);
+    return hipGetLastError();
+}
+hipError_t k_slice_elems(const int64_t* off, int64_t cps, int nranks, int64_t* out, hipStream_t s) {
+    slice_elems<<<1, kBlock, 0, s>>>(off, cps, nranks, out);
     return hipGetLastError();
 }
 hipError_t k_ms_or_pairs(const int64_t* pairs, int64_t npairs, uint64_t* nx, hipStream_t s) {

@@ -194,6 +194,9 @@ class HipPartBackend:
     def ms_settle(self, level, recv, nslices, fr_next):
         return self._counts("tgo_part_ms_settle", level, self._vp(recv), nslices, self._vp(fr_next))
 
+    def ms_pack_dev(self, cand, send, nranks, send_elems):
+        self.e.part_call("tgo_part_ms_pack_dev", self._vp(cand), nranks, self._vp(send), self._vp(send_elems))
+
     def ms_pack(self, cand, send, nranks):
         sc = np.zeros(nranks, np.int64)
         self.e.part_call("tgo_part_ms_pack", self._vp(cand), nranks, self._vp(send), L.ptr(sc, C.c_int64))
@@ -276,6 +279,17 @@ class HipPartBackend:
         return out
 
 
+def _scratch(backend, name, n, dtype):
+    """Exchange buffers live as long as the backend (allocated zero-filled once, reused by
+    every run: the drivers only rely on zeros where the local steps restore them)."""
+    bufs = backend.__dict__.setdefault("_scratch", {})
+    t = bufs.get(name)
+    if t is None or t.numel() < n or t.dtype != dtype:
+        t = backend.tensor(n, dtype)
+        bufs[name] = t
+    return t[:n]
+
+
 def _allreduce_counts(c, device, group):
     """Global sums of per-rank counters (frontier size / entries, reached, ...) over `group`.
     A device tensor (HipPartBackend device_counts) is reduced in place: one read per level."""
@@ -292,10 +306,10 @@ def distributed_bfs(backend, seed: int, max_depth: int, alpha: float = 15.0, bet
     nwl = backend.n_local // 64
     nwg = backend.n_global // 64
     dev = backend.device
-    fb_global = backend.tensor(nwg, torch.int64)
-    nb_local = backend.tensor(nwl, torch.int64)
-    disc = backend.tensor(nwg, torch.int64)
-    recv = backend.tensor(nwg, torch.int64)
+    fb_global = _scratch(backend, "bfs_fb", nwg, torch.int64)
+    nb_local = _scratch(backend, "bfs_nb", nwl, torch.int64)
+    disc = _scratch(backend, "bfs_disc", nwg, torch.int64)
+    recv = _scratch(backend, "bfs_recv", nwg, torch.int64)
     total = _allreduce_counts([backend.total_entries, 0], dev, group)[0]
     c = backend.bfs_begin(seed, nb_local)
     dist.all_gather_into_tensor(fb_global, nb_local, group=group)
@@ -341,6 +355,20 @@ def _exchange_pairs(send, counts, recv, dev, group):
     return np.asarray(outs, np.int64) // 2
 
 
+def _exchange_pairs_dev(send, sct, recv, group):
+    """As _exchange_pairs with the split sizes already on the device (sct, int64 elements per
+    destination): one all_to_all of the sizes, ONE host read of both size vectors."""
+    rct = torch.empty_like(sct)
+    dist.all_to_all_single(rct, sct, group=group)
+    both = torch.cat([sct, rct]).cpu().numpy()
+    w = len(sct)
+    ins = [int(x) for x in both[:w]]
+    outs = [int(x) for x in both[w:]]
+    dist.all_to_all_single(recv[:sum(outs)], send[:sum(ins)], output_split_sizes=outs, input_split_sizes=ins,
+                           group=group)
+    return np.asarray(outs, np.int64) // 2
+
+
 def distributed_msbfs(backend, seeds, max_depth: int, ms_alpha: float = 12.0, stats: bool = True, group=None,
                       sparse_exchange: bool = True):
     """Up to 64 ShortestDistance programs with unit weights over bothE, run together with
@@ -353,10 +381,11 @@ def distributed_msbfs(backend, seeds, max_depth: int, ms_alpha: float = 12.0, st
     world = dist.get_world_size(group)
     nseeds = len(seeds)
     dev = backend.device
-    fr = backend.tensor(backend.n_local, torch.int64)
-    frn = backend.tensor(backend.n_local, torch.int64)
-    fr_global = backend.tensor(backend.n_global, torch.int64)
-    cand = backend.tensor(backend.n_global, torch.int64)
+    fr = _scratch(backend, "ms_fr", backend.n_local, torch.int64)
+    frn = _scratch(backend, "ms_frn", backend.n_local, torch.int64)
+    frn.zero_()                  # rows without entries are never rewritten by the pull levels
+    fr_global = _scratch(backend, "ms_fr_global", backend.n_global, torch.int64)
+    cand = _scratch(backend, "ms_cand", backend.n_global, torch.int64)     # all-zero between sparse levels
     send = recv = None
     total = _allreduce_counts([backend.total_entries, 0], dev, group)[0]
     nf, mf = _allreduce_counts(backend.ms_begin(seeds, fr), dev, group)
@@ -368,18 +397,22 @@ def distributed_msbfs(backend, seeds, max_depth: int, ms_alpha: float = 12.0, st
             dist.all_gather_into_tensor(fr_global, fr, group=group)
             c = backend.ms_pull(level, fr_global, frn)
         elif sparse_exchange:
-            if send is None:
-                send = backend.tensor(2 * backend.n_global, torch.int64)
-                recv = backend.tensor(2 * backend.n_global, torch.int64)
-            backend.ms_push(level, fr, cand)           # cand is all-zero here: ms_pack clears it
-            rcounts = _exchange_pairs(send, backend.ms_pack(cand, send, world), recv, dev, group)
+            send = _scratch(backend, "pairs_send", 2 * backend.n_global, torch.int64)
+            recv = _scratch(backend, "pairs_recv", 2 * backend.n_global, torch.int64)
+            backend.ms_push(level, fr, cand)           # cand is all-zero here: the pack clears it
+            if hasattr(backend, "ms_pack_dev"):
+                sct = _scratch(backend, "pairs_sct", world, torch.int64)
+                backend.ms_pack_dev(cand, send, world, sct)
+                rcounts = _exchange_pairs_dev(send, sct, recv, group)
+            else:
+                rcounts = _exchange_pairs(send, backend.ms_pack(cand, send, world), recv, dev, group)
             c = backend.ms_settle_pairs(level, recv, rcounts, frn)
         else:
-            if recv is None:
-                recv = backend.tensor(backend.n_global, torch.int64)
+            recv = _scratch(backend, "slices_recv", backend.n_global, torch.int64)
             cand.zero_()
             backend.ms_push(level, fr, cand)
             dist.all_to_all_single(recv, cand, group=group)
+            cand.zero_()
             c = backend.ms_settle(level, recv, world, frn)
         fr, frn = frn, fr
         nf, mf = _allreduce_counts(c, dev, group)
@@ -408,8 +441,8 @@ def distributed_sssp(backend, seed: int, delta: int = 0, fetch: bool = True, sta
     world = dist.get_world_size(group)
     dev = backend.device
     n = backend.n_global
-    send = backend.tensor(2 * n, torch.int64)
-    recv = backend.tensor(2 * n, torch.int64)
+    send = _scratch(backend, "pairs_send", 2 * n, torch.int64)
+    recv = _scratch(backend, "pairs_recv", 2 * n, torch.int64)
     qlen, dflt = (int(x) for x in backend.sssp_begin(seed, delta))
     if delta <= 0:      # ranks' default widths differ with their local mean weight: agree on one
         t = torch.tensor([dflt], dtype=torch.int64, device=dev)
@@ -475,8 +508,8 @@ def distributed_pagerank(backend, alpha: float, vertex_count: int, iterations: i
         return np.full(backend.n_local, np.nan) if fetch else None
     world = dist.get_world_size(group)
     hot, span = layout if layout is not None else pagerank_layout(backend, group)
-    contrib_local = backend.tensor(backend.n_local, torch.float64)
-    contrib_global = backend.tensor(world * span, torch.float64)
+    contrib_local = _scratch(backend, "pr_local", backend.n_local, torch.float64)
+    contrib_global = _scratch(backend, "pr_global", world * span, torch.float64)
     backend.pr_begin(alpha, vertex_count, iterations, contrib_local)
     for _ in range(2, iterations + 1):
         if hot == 0:
