@@ -73,8 +73,14 @@ typedef enum {
  * (graphdb/database/serialize/attribute/ IntegerSerializer.java, LongSerializer.java, ...). */
 typedef enum {
     TGO_DT_BYTE = 1, TGO_DT_SHORT = 2, TGO_DT_INTEGER = 3, TGO_DT_LONG = 4,
-    TGO_DT_FLOAT = 5, TGO_DT_DOUBLE = 6, TGO_DT_BOOLEAN = 7
+    TGO_DT_FLOAT = 5, TGO_DT_DOUBLE = 6, TGO_DT_BOOLEAN = 7,
+    TGO_DT_DATE = 8,       /* DateSerializer: the Long form of getTime()                    */
+    TGO_DT_CHARACTER = 9,  /* CharacterSerializer: 2 bytes                                  */
+    TGO_DT_STRING = 10     /* StringSerializer: ASCII / full UTF / compressed (skipped only) */
 } tgo_datatype;
+
+/* RelationType sort order (EdgeSerializer.java:137,311-313): DESC inverts the sort-key bytes. */
+typedef enum { TGO_ORDER_ASC = 0, TGO_ORDER_DESC = 1 } tgo_sort_order;
 
 typedef struct {
     int32_t abi_version;       /* must be TGO_ABI_VERSION                                  */
@@ -111,6 +117,7 @@ typedef struct {
     int32_t n_sort_key;           /* sort-key property keys (only for MULTI; KEY inline)       */
     const int64_t* sort_key_ids;
     int32_t n_signature;          /* signature property keys, in definition order             */
+    int32_t sort_order;           /* tgo_sort_order of the label's sort key (0 = ASC)         */
     const int64_t* signature_ids;
 } tgo_edge_type;
 
@@ -133,7 +140,14 @@ typedef struct {
     int32_t apply_cap;            /* 1 = reproduce the reference's cap (parity mode), 0 = not   */
     int32_t n_labels;             /* 0 = untyped scope (all user edge labels)                  */
     const int64_t* label_ids;     /* typed scope: __.inE("label")... — fitted, no cap          */
-    int64_t weight_key;           /* Integer edge property read as weight; 0 = none            */
+    int64_t weight_key;           /* Integer edge property read as weight; 0 = none.  It may sit
+                                     in a MULTI label's sort key (ASC or DESC), its signature or
+                                     its remaining properties; a non-Integer key fails with
+                                     TGO_E_UNSUPPORTED (ShortestDistanceVertexProgram.java:53
+                                     casts edge.<Integer>value).  TTL / timestamp metadata is not
+                                     part of the entry bytes (EdgeSerializer.java:154-161 only
+                                     copies it into the relation); expired cells never reach the
+                                     scan.                                                     */
 } tgo_load_opts;
 
 /* Decoded adjacency given directly (bench / already-decoded callers).  Dense vertex ids
@@ -231,6 +245,23 @@ int  tgo_load_rows(tgo_ctx* ctx, const tgo_rows* rows, const tgo_schema* schema,
 int  tgo_finish_load(tgo_ctx* ctx);
 /* Load an already-decoded edge list (finishes the load). */
 int  tgo_load_edges(tgo_ctx* ctx, const tgo_edges* edges, const tgo_load_opts* opts);
+
+/* One edge entry through the product decoder (EdgeSerializer.parseRelation, :73-166, restricted
+ * to what the traversal reads), on the host, without a ctx or a device: the per-entry half of
+ * tgo_load_rows, for callers that decode single entries and for codec tests.
+ * Returns TGO_OK, TGO_E_CODEC (malformed), TGO_E_UNSUPPORTED (an inline property of a key
+ * missing from the schema; a non-Integer weight key).  selected = 0: the label is outside the
+ * typed scope (the entry is not preloaded). */
+typedef struct {
+    int64_t type_id;
+    int64_t other_id;             /* other vertex Titan id                                    */
+    int32_t dir;                  /* 0 OUT, 1 IN                                              */
+    int32_t selected;
+    int32_t has_weight;
+    int32_t weight;
+} tgo_edge_entry;
+int  tgo_decode_edge_entry(const tgo_schema* schema, const tgo_load_opts* opts, const uint8_t* entry,
+                           int64_t len, int64_t value_pos, tgo_edge_entry* out);
 
 int64_t tgo_num_vertices(const tgo_ctx* ctx);
 /* Titan vertex id of every dense index, in row order (n entries). */

@@ -38,16 +38,16 @@ JNIEXPORT jstring JNICALL JFN(lastError)(JNIEnv* env, jclass cls, jlong h) {
     return (*env)->NewStringUTF(env, h ? tgo_last_error(CTX(h)) : "tgo_create failed: no usable gfx950 device");
 }
 
-/* Flattened edge labels: {typeId, multiplicity, nSortKey, sortKeyIds..., nSignature, signatureIds...}*. */
+/* Flattened edge labels: {typeId, multiplicity, sortOrder, nSortKey, sortKeyIds..., nSignature, signatureIds...}*. */
 static int unpack_schema(const jlong* et, jsize net, const jlong* pk, jsize npk, tgo_schema* s,
                          tgo_edge_type** types_out, tgo_property_key** keys_out) {
     int n = 0;
     for (jsize i = 0; i < net;) {
-        if (i + 3 > net) return TGO_E_INVALID;
-        jsize nsk = (jsize)et[i + 2];
-        if (i + 3 + nsk + 1 > net) return TGO_E_INVALID;
-        jsize nsig = (jsize)et[i + 3 + nsk];
-        i += 3 + nsk + 1 + nsig;
+        if (i + 4 > net) return TGO_E_INVALID;
+        jsize nsk = (jsize)et[i + 3];
+        if (i + 4 + nsk + 1 > net) return TGO_E_INVALID;
+        jsize nsig = (jsize)et[i + 4 + nsk];
+        i += 4 + nsk + 1 + nsig;
         if (i > net) return TGO_E_INVALID;
         n++;
     }
@@ -58,9 +58,10 @@ static int unpack_schema(const jlong* et, jsize net, const jlong* pk, jsize npk,
     for (jsize i = 0; i < net; j++) {
         t[j].type_id = et[i];
         t[j].multiplicity = (int32_t)et[i + 1];
-        t[j].n_sort_key = (int32_t)et[i + 2];
-        t[j].sort_key_ids = (const int64_t*)&et[i + 3];
-        jsize sig = i + 3 + t[j].n_sort_key;
+        t[j].sort_order = (int32_t)et[i + 2];
+        t[j].n_sort_key = (int32_t)et[i + 3];
+        t[j].sort_key_ids = (const int64_t*)&et[i + 4];
+        jsize sig = i + 4 + t[j].n_sort_key;
         t[j].n_signature = (int32_t)et[sig];
         t[j].signature_ids = (const int64_t*)&et[sig + 1];
         i = sig + 1 + t[j].n_signature;

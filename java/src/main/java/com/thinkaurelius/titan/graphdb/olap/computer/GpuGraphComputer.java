@@ -188,6 +188,7 @@ public class GpuGraphComputer implements TitanGraphComputer {
                             (com.thinkaurelius.titan.graphdb.internal.InternalRelationType) l;
                     out.add(t.longId());
                     out.add((long) t.multiplicity().ordinal());
+                    out.add(t.getSortOrder() == com.thinkaurelius.titan.graphdb.internal.Order.DESC ? 1L : 0L);
                     long[] sk = t.getSortKey();
                     out.add((long) sk.length);
                     for (long k : sk) out.add(k);
@@ -223,6 +224,9 @@ public class GpuGraphComputer implements TitanGraphComputer {
             if (c == Float.class) return TgoNative.DT_FLOAT;
             if (c == Double.class) return TgoNative.DT_DOUBLE;
             if (c == Boolean.class) return TgoNative.DT_BOOLEAN;
+            if (c == java.util.Date.class) return TgoNative.DT_DATE;
+            if (c == Character.class) return TgoNative.DT_CHARACTER;
+            if (c == String.class) return TgoNative.DT_STRING;
             return 0;   // unknown: the decoder fails loudly if such a property must be skipped
         }
     }

@@ -30,7 +30,7 @@ public final class TgoNative {
     public static final int MULTI = 0, SIMPLE = 1, MANY2ONE = 2, ONE2MANY = 3, ONE2ONE = 4;
     /* tgo_datatype */
     public static final int DT_BYTE = 1, DT_SHORT = 2, DT_INTEGER = 3, DT_LONG = 4, DT_FLOAT = 5, DT_DOUBLE = 6,
-            DT_BOOLEAN = 7;
+            DT_BOOLEAN = 7, DT_DATE = 8, DT_CHARACTER = 9, DT_STRING = 10;
     /** TGO_DIST_ABSENT: no DISTANCE property was set (the vertex was not reached). */
     public static final long DIST_ABSENT = Long.MIN_VALUE;
 
@@ -44,7 +44,8 @@ public final class TgoNative {
     /**
      * tgo_load_rows: one work block of scanned rows in StaticArrayEntryList form
      * (StaticArrayEntryList.java:15-50).  {@code entryBytes} must be a direct buffer.
-     * The schema is flattened: per edge label {typeId, multiplicity, nSortKey, sortKeyIds...,
+     * The schema is flattened: per edge label {typeId, multiplicity, sortOrder (0 ASC, 1 DESC),
+     * nSortKey, sortKeyIds...,
      * nSignature, signatureIds...}; per property key {keyId, datatype}.
      */
     public static native int loadRows(long ctx, long[] rowKeys, long[] rowEntryBegin, long[] rowByteBegin,

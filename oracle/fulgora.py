@@ -31,7 +31,8 @@ class FrRows(C.Structure):
 
 class FrEdgeType(C.Structure):
     _fields_ = [("type_id", C.c_int64), ("multiplicity", C.c_int32), ("n_sort_key", C.c_int32),
-                ("sort_key_ids", _i64p), ("n_signature", C.c_int32), ("signature_ids", _i64p)]
+                ("sort_key_ids", _i64p), ("n_signature", C.c_int32), ("sort_order", C.c_int32),
+                ("signature_ids", _i64p)]
 
 
 class FrPropertyKey(C.Structure):
@@ -101,6 +102,8 @@ def load() -> C.CDLL:
         "fr_encode_edge": (C.c_int, [P(FrBuf), _i32p, P(FrSchema), C.c_int64, C.c_int, C.c_int64,
                                      C.c_int64, P(FrProp), C.c_int]),
         "fr_encode_vertex_exists": (C.c_int, [P(FrBuf), _i32p, C.c_int64]),
+        "fr_write_value": (C.c_int, [P(FrBuf), C.c_int, C.c_int, C.c_int64, C.c_int]),
+        "fr_string_of": (C.c_int, [C.c_int64, P(C.c_uint16)]),
         "fr_encode_property": (C.c_int, [P(FrBuf), _i32p, C.c_int64, C.c_int, C.c_int64, C.c_int64]),
         "fr_decode_edge": (C.c_int, [_u8p, C.c_size_t, C.c_size_t, P(FrSchema), C.c_int64, _i64p,
                                      P(C.c_int), _i64p, _i64p, P(C.c_int), _i64p]),
@@ -147,14 +150,16 @@ class OracleSchema:
     """Holds ctypes arrays alive for an FrSchema built from a python schema description."""
 
     def __init__(self, edge_types, property_keys):
-        # edge_types: list of dicts {type_id, multiplicity, sort_key:[ids], signature:[ids]}
+        # edge_types: list of dicts {type_id, multiplicity, sort_key:[ids], signature:[ids],
+        # order: "ASC" | "DESC"}
         self._keep = []
         et = (FrEdgeType * max(1, len(edge_types)))()
         for i, t in enumerate(edge_types):
             sk = np.asarray(t.get("sort_key", []), dtype=np.int64)
             sg = np.asarray(t.get("signature", []), dtype=np.int64)
             self._keep += [sk, sg]
-            et[i] = FrEdgeType(t["type_id"], t["multiplicity"], len(sk), _p(sk, C.c_int64), len(sg), _p(sg, C.c_int64))
+            et[i] = FrEdgeType(t["type_id"], t["multiplicity"], len(sk), _p(sk, C.c_int64), len(sg),
+                               1 if t.get("order", "ASC") == "DESC" else 0, _p(sg, C.c_int64))
         pk = (FrPropertyKey * max(1, len(property_keys)))()
         for i, (kid, dt) in enumerate(property_keys):
             pk[i] = FrPropertyKey(kid, dt)

@@ -215,48 +215,160 @@ static int is_unique(int mult, int dir) {                                /* Mult
     return mult == FR_MANY2ONE || mult == FR_ONE2ONE;
 }
 static void put_be(fr_buf* b, uint64_t v, int n) { for (int i = n - 1; i >= 0; i--) buf_put(b, (uint8_t)(v >> (8 * i))); }
-static uint64_t get_be(const uint8_t* d, size_t* pos, int n) {
-    uint64_t v = 0; for (int i = 0; i < n; i++) v = (v << 8) | d[(*pos)++]; return v;
+/* fr_prop's String convention (fulgora_ref.h). */
+int fr_string_of(int64_t value, uint16_t* chars) {
+    int n = 0;
+    if (value == 0) return 0;
+    if (value < 0) { chars[n++] = 0x00E9; chars[n++] = 0x2135; }
+    uint64_t a = value < 0 ? (uint64_t)0 - (uint64_t)value : (uint64_t)value;
+    char digits[24]; int nd = 0;
+    while (a) { digits[nd++] = (char)('0' + a % 10); a /= 10; }
+    while (nd) chars[n++] = (uint16_t)digits[--nd];
+    return n;
 }
-/* StandardSerializer.writeObjectInternal :286-301 (null flag) + attribute serializers. */
-static int write_object(fr_buf* b, int dt, int present, int64_t value, int byte_order) {
+static uint32_t float_bits(int64_t v) { float f = (float)v; uint32_t u; memcpy(&u, &f, 4); return u; }
+static uint64_t double_bits(int64_t v) { double f = (double)v; uint64_t u; memcpy(&u, &f, 8); return u; }
+/* StringSerializer.write :142-186 (no compression below 16000 chars; ASCII or full UTF). */
+static void write_string(fr_buf* b, int64_t value) {
+    uint16_t c[32]; int n = fr_string_of(value, c), ascii = 1;
+    for (int i = 0; i < n; i++) ascii &= c[i] <= 127;
+    if (ascii) {
+        fr_vl_write_positive(b, (n == 0 ? 1 : 2) << 4);          /* NO_COMPRESSION_OFFSET = 4 */
+        for (int i = 0; i < n; i++) buf_put(b, (uint8_t)(c[i] | (i + 1 == n ? 0x80 : 0)));
+    } else {
+        fr_vl_write_positive(b, ((int64_t)n << 4) + (1 << 3));    /* full UTF marker */
+        for (int i = 0; i < n; i++) {
+            if (c[i] <= 0x7F) buf_put(b, (uint8_t)c[i]);
+            else if (c[i] > 0x7FF) { buf_put(b, (uint8_t)(0xE0 | (c[i] >> 12 & 0x0F))); buf_put(b, (uint8_t)(0x80 | (c[i] >> 6 & 0x3F))); buf_put(b, (uint8_t)(0x80 | (c[i] & 0x3F))); }
+            else { buf_put(b, (uint8_t)(0xC0 | (c[i] >> 6 & 0x1F))); buf_put(b, (uint8_t)(0x80 | (c[i] & 0x3F))); }
+        }
+    }
+}
+/* StandardSerializer.writeObjectInternal :286-301: a null flag byte (0 / -1) unless the
+ * serializer handles null itself (StringSerializer is a SupportsNullSerializer), then the
+ * attribute serializer's write or, for sort keys, writeByteOrder. */
+int fr_write_value(fr_buf* b, int dt, int present, int64_t value, int byte_order) {
+    if (dt == FR_DT_STRING) {
+        if (byte_order) {                                        /* StringSerializer.writeByteOrder :54-67 */
+            if (!present) { buf_put(b, 0xFF); return FR_OK; }
+            buf_put(b, 0x00);
+            uint16_t c[32]; int n = fr_string_of(value, c);
+            for (int i = 0; i < n; i++) put_be(b, c[i], 2);      /* CharacterSerializer: the char, big-endian */
+            put_be(b, 0, 2);
+        } else if (!present) fr_vl_write_positive(b, 0);
+        else write_string(b, value);
+        return FR_OK;
+    }
     if (!present) { buf_put(b, 0xFF); return FR_OK; }
     buf_put(b, 0x00);
     switch (dt) {
     case FR_DT_BYTE: buf_put(b, (uint8_t)((int8_t)value - (-128))); break;          /* ByteSerializer :17-19 */
-    case FR_DT_SHORT: put_be(b, (uint16_t)((int16_t)value - (-32768)), 2); break;    /* ShortSerializer */
+    case FR_DT_SHORT: put_be(b, (uint16_t)((int16_t)value - (-32768)), 2); break;    /* ShortSerializer :17-19 */
+    case FR_DT_CHARACTER: put_be(b, (uint16_t)value, 2); break;                      /* CharacterSerializer: short(c - 2^15) + 2^15 */
     case FR_DT_INTEGER:
         if (byte_order) put_be(b, (uint32_t)((int32_t)value - INT32_MIN), 4);        /* IntegerSerializer :27-34 */
         else fr_vl_write(b, (int32_t)value);                                         /* :20-23 */
         break;
-    case FR_DT_LONG: put_be(b, (uint64_t)value - (uint64_t)INT64_MIN, 8); break;     /* LongSerializer :20-22 */
+    case FR_DT_LONG: case FR_DT_DATE:                                                /* LongSerializer :20-22, DateSerializer */
+        put_be(b, (uint64_t)value - (uint64_t)INT64_MIN, 8); break;
+    case FR_DT_FLOAT: {                                                              /* FloatSerializer :33-46 */
+        uint32_t u = float_bits(value);
+        if (byte_order) { int32_t si = (int32_t)u; si ^= (si >> 31) & 0x7fffffff; u = (uint32_t)si ^ 0x80000000u; }
+        put_be(b, u, 4); break;                                  /* NumericUtils.floatToSortableInt */
+    }
+    case FR_DT_DOUBLE: {                                                             /* DoubleSerializer :33-46 */
+        uint64_t u = double_bits(value);
+        if (byte_order) { int64_t sl = (int64_t)u; sl ^= (sl >> 63) & 0x7fffffffffffffffLL; u = (uint64_t)sl ^ 0x8000000000000000ULL; }
+        put_be(b, u, 8); break;
+    }
     case FR_DT_BOOLEAN: buf_put(b, value ? 1 : 0); break;
     default: return FR_E_UNSUPPORTED;
     }
     return FR_OK;
 }
-/* StandardSerializer.readObjectInternal :220-233.  Returns size-consumed; *present=0 on null. */
-static int read_object(const uint8_t* d, size_t len, size_t* pos, int dt, int byte_order,
-                       int* present, int64_t* ival) {
+static int write_object(fr_buf* b, int dt, int present, int64_t value, int byte_order) {
+    return fr_write_value(b, dt, present, value, byte_order);
+}
+/* StandardSerializer.readObjectInternal :220-233 + the attribute serializers' read /
+ * readByteOrder.  d is read through `x` (0xFF inverts: a DESC sort key, EdgeSerializer.java:137).
+ * *ival is the value of integral types (Byte..Long, Boolean, Date, Character); other types
+ * are skipped (*ival = 0).  *present = 0 on a serialized null. */
+static int read_object_x(const uint8_t* d, size_t len, size_t* pos, int dt, int byte_order, uint8_t x,
+                         int* present, int64_t* ival) {
+#define RD() ((*pos) < len ? (uint8_t)(d[(*pos)++] ^ x) : (uint8_t)((*pos)++, 0))
+    *ival = 0;
+    if (dt == FR_DT_STRING) {
+        if (byte_order) {                                        /* StringSerializer.readByteOrder :40-51 */
+            if (*pos >= len) return FR_E_CODEC;
+            uint8_t p = RD();
+            if (p == 0xFF) { *present = 0; return FR_OK; }
+            if (p != 0) return FR_E_CODEC;
+            *present = 1;
+            for (;;) {
+                if (*pos + 2 > len) return FR_E_CODEC;
+                uint8_t h = RD(), l = RD();
+                if (h == 0 && l == 0) break;
+            }
+            return FR_OK;
+        }
+        /* StringSerializer.read :84-135 */
+        uint64_t L = 0; uint8_t bb;
+        do { if (*pos >= len) return FR_E_CODEC; bb = RD(); L = (L << 7) | (bb & 0x7F); } while (!(bb & 0x80));
+        if (L == 0) { *present = 0; return FR_OK; }
+        *present = 1;
+        uint64_t cid = L & 7; L >>= 3;
+        if (cid != 0) { *pos += L; return *pos <= len ? FR_OK : FR_E_CODEC; }   /* compressed: L bytes */
+        if ((L & 1) == 0) {
+            L >>= 1;
+            if (L == 1) return FR_OK;                            /* "" */
+            if (L != 2) return FR_E_CODEC;
+            do { if (*pos >= len) return FR_E_CODEC; bb = RD(); } while (!(bb & 0x80));
+            return FR_OK;
+        }
+        L >>= 1;
+        for (uint64_t i = 0; i < L; i++) {
+            if (*pos >= len) return FR_E_CODEC;
+            uint8_t c = RD();
+            switch (c >> 4) {
+            case 12: case 13: RD(); break;
+            case 14: RD(); RD(); break;
+            default: break;
+            }
+        }
+        return *pos <= len ? FR_OK : FR_E_CODEC;
+    }
     if (*pos >= len) return FR_E_CODEC;
-    int8_t flag = (int8_t)d[(*pos)++];
+    int8_t flag = (int8_t)RD();
     if (flag == -1) { *present = 0; return FR_OK; }
     if (flag != 0) return FR_E_CODEC;
     *present = 1;
+    uint64_t u = 0;
     switch (dt) {
-    case FR_DT_BYTE: *ival = (int8_t)(d[(*pos)++] + (-128)); break;
-    case FR_DT_SHORT: *ival = (int16_t)(get_be(d, pos, 2) + (-32768)); break;
+    case FR_DT_BYTE: *ival = (int8_t)(RD() + (-128)); break;
+    case FR_DT_SHORT: u = RD(); u = (u << 8) | RD(); *ival = (int16_t)(u + (-32768)); break;
+    case FR_DT_CHARACTER: u = RD(); u = (u << 8) | RD(); *ival = (int64_t)(uint16_t)u; break;
     case FR_DT_INTEGER:
-        if (byte_order) *ival = (int32_t)(get_be(d, pos, 4) + (uint32_t)INT32_MIN);
-        else { int64_t l = fr_vl_read(d, pos); if (l < INT32_MIN || l > INT32_MAX) return FR_E_CODEC; *ival = l; }
+        if (byte_order) { for (int i = 0; i < 4; i++) u = (u << 8) | RD(); *ival = (int32_t)((uint32_t)u + (uint32_t)INT32_MIN); }
+        else {
+            uint64_t z = 0; uint8_t bb;
+            do { if (*pos >= len) return FR_E_CODEC; bb = RD(); z = (z << 7) | (bb & 0x7F); } while (!(bb & 0x80));
+            int64_t l = (z & 1) ? -(int64_t)(z >> 1) : (int64_t)(z >> 1);   /* VariableLong.read zig-zag */
+            if (l < INT32_MIN || l > INT32_MAX) return FR_E_CODEC;
+            *ival = l;
+        }
         break;
-    case FR_DT_LONG: *ival = (int64_t)(get_be(d, pos, 8) + (uint64_t)INT64_MIN); break;
-    case FR_DT_FLOAT: *pos += 4; *ival = 0; break;
-    case FR_DT_DOUBLE: *pos += 8; *ival = 0; break;
-    case FR_DT_BOOLEAN: *ival = d[(*pos)++]; break;
+    case FR_DT_LONG: case FR_DT_DATE: for (int i = 0; i < 8; i++) u = (u << 8) | RD(); *ival = (int64_t)(u + (uint64_t)INT64_MIN); break;
+    case FR_DT_FLOAT: for (int i = 0; i < 4; i++) RD(); break;
+    case FR_DT_DOUBLE: for (int i = 0; i < 8; i++) RD(); break;
+    case FR_DT_BOOLEAN: *ival = RD(); break;
     default: return FR_E_UNSUPPORTED;
     }
+#undef RD
     return *pos <= len ? FR_OK : FR_E_CODEC;
+}
+static int read_object(const uint8_t* d, size_t len, size_t* pos, int dt, int byte_order,
+                       int* present, int64_t* ival) {
+    return read_object_x(d, len, pos, dt, byte_order, 0, present, ival);
 }
 
 int fr_encode_vertex_exists(fr_buf* out, int32_t* value_pos, int64_t relation_id) {
@@ -289,12 +401,15 @@ int fr_encode_edge(fr_buf* out, int32_t* value_pos, const fr_schema* schema, int
     fr_write_relation_type(out, type_id, 1, dir, 0);
     int mult = t->multiplicity;
     if (mult == FR_MULTI) {
+        const size_t key_start = out->len;
         for (int k = 0; k < t->n_sort_key; k++) {                        /* writeInlineTypes KEY */
             int present = 0; int64_t v = 0;
             for (int j = 0; j < nprops; j++) if (props[j].key_id == t->sort_key_ids[k]) { present = 1; v = props[j].value; }
             int rc = write_object(out, key_datatype(schema, t->sort_key_ids[k]), present, v, 1);
             if (rc) return rc;
         }
+        if (t->sort_order == FR_DESC)                                    /* getStaticBufferFlipBytes :311-313 */
+            for (size_t i = key_start; i < out->len; i++) out->p[i] = (uint8_t)~out->p[i];
         fr_vl_write_positive_backward(out, other);
         fr_vl_write_positive_backward(out, relation_id);
         *value_pos = (int32_t)out->len;
@@ -364,8 +479,19 @@ int fr_decode_edge(const uint8_t* d, size_t len, size_t value_pos, const fr_sche
     }
     *has_weight = 0;
     if (weight_key == 0) return FR_OK;
-    if (mult == FR_MULTI) for (int k = 0; k < t->n_sort_key; k++)
-        if (t->sort_key_ids[k] == weight_key) return FR_E_UNSUPPORTED;
+    /* ShortestDistance reads edge.<Integer>value(weight) (ShortestDistanceVertexProgram.java:53):
+     * any other datatype is a ClassCastException in the reference. */
+    if (key_datatype(schema, weight_key) != FR_DT_INTEGER) return FR_E_UNSUPPORTED;
+    if (mult == FR_MULTI) {                                              /* sort key :130-140 */
+        size_t kp = pos;                                                 /* startKeyPos: after the type */
+        const uint8_t x = t->sort_order == FR_DESC ? 0xFF : 0x00;        /* in.subrange(keyLength, true) */
+        for (int k = 0; k < t->n_sort_key; k++) {
+            int present; int64_t v = 0;
+            rc = read_object_x(d, value_pos, &kp, key_datatype(schema, t->sort_key_ids[k]), 1, x, &present, &v);
+            if (rc) return rc;
+            if (t->sort_key_ids[k] == weight_key) { *has_weight = present; *weight = v; return FR_OK; }
+        }
+    }
     pos = props_pos;
     for (int k = 0; k < t->n_signature; k++) {                           /* readInlineTypes SIGNATURE */
         int present; int64_t v = 0;

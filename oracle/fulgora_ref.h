@@ -35,7 +35,9 @@ enum { FR_OK = 0, FR_E_INVALID = -1, FR_E_CODEC = -4, FR_E_PROGRAM = -6, FR_E_UN
 enum { FR_SCOPE_OUT_E = 0, FR_SCOPE_IN_E = 1, FR_SCOPE_BOTH_E = 2 };
 enum { FR_MULTI = 0, FR_SIMPLE = 1, FR_MANY2ONE = 2, FR_ONE2MANY = 3, FR_ONE2ONE = 4 };
 enum { FR_DT_BYTE = 1, FR_DT_SHORT = 2, FR_DT_INTEGER = 3, FR_DT_LONG = 4,
-       FR_DT_FLOAT = 5, FR_DT_DOUBLE = 6, FR_DT_BOOLEAN = 7 };
+       FR_DT_FLOAT = 5, FR_DT_DOUBLE = 6, FR_DT_BOOLEAN = 7,
+       FR_DT_DATE = 8, FR_DT_CHARACTER = 9, FR_DT_STRING = 10 };
+enum { FR_ASC = 0, FR_DESC = 1 };   /* RelationType sort order (EdgeSerializer.java:137,311-313) */
 
 #define FR_ABSENT INT64_MIN   /* "no distance property" */
 
@@ -80,7 +82,8 @@ typedef struct {
 typedef struct {
     int64_t type_id; int32_t multiplicity;
     int32_t n_sort_key; const int64_t* sort_key_ids;
-    int32_t n_signature; const int64_t* signature_ids;
+    int32_t n_signature; int32_t sort_order;   /* FR_ASC / FR_DESC */
+    const int64_t* signature_ids;
 } fr_edge_type;
 typedef struct { int64_t key_id; int32_t datatype; } fr_property_key;
 typedef struct {
@@ -89,7 +92,16 @@ typedef struct {
 } fr_schema;
 
 /* ---- encoder: one edge entry (EdgeSerializer.writeRelation, :222-315) ---- */
-typedef struct { int64_t key_id; int64_t value; } fr_prop;   /* integral-valued inline property */
+/* Inline property value, carried as an int64 `value` whose meaning follows the key's
+ * datatype: integral types and Date (ms) as is, Float/Double = (float)/(double)value,
+ * Character = (uint16_t)value, String = fr_string_of(value) (decimal digits of |value|,
+ * prefixed by U+00E9 U+2135 when value < 0 so both multi-byte UTF forms occur; "" for 0). */
+typedef struct { int64_t key_id; int64_t value; } fr_prop;
+/* UTF-16 code units of fr_prop's String for `value`; returns the length (<= 24). */
+int fr_string_of(int64_t value, uint16_t* chars);
+/* One value through StandardSerializer (byte_order: the sort-key form, writeByteOrder).
+ * Exposed for the codec known-answer tests. */
+int fr_write_value(fr_buf* out, int datatype, int present, int64_t value, int byte_order);
 int fr_encode_edge(fr_buf* out, int32_t* value_pos, const fr_schema* schema, int64_t type_id,
                    int dir, int64_t other_vertex_id, int64_t relation_id,
                    const fr_prop* props, int nprops);

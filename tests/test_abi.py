@@ -43,6 +43,10 @@ def test_struct_layouts_match_header():
     assert C.sizeof(L.BfsArgs) == 24
     assert C.sizeof(L.SsspArgs) == 40
     assert C.sizeof(L.PrArgs) == 24
+    assert C.sizeof(L.EdgeEntry) == 32
+    # tgo_edge_type: sort_order fills the slot after n_signature (no size change)
+    assert C.sizeof(L.EdgeType) == 40
+    assert L.EdgeType.sort_order.offset == 28 and L.EdgeType.signature_ids.offset == 32
 
 
 def test_default_options():

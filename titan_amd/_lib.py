@@ -51,7 +51,8 @@ class Rows(C.Structure):
 
 class EdgeType(C.Structure):
     _fields_ = [("type_id", C.c_int64), ("multiplicity", C.c_int32), ("n_sort_key", C.c_int32),
-                ("sort_key_ids", _i64p), ("n_signature", C.c_int32), ("signature_ids", _i64p)]
+                ("sort_key_ids", _i64p), ("n_signature", C.c_int32), ("sort_order", C.c_int32),
+                ("signature_ids", _i64p)]
 
 
 class PropertyKey(C.Structure):
@@ -66,6 +67,11 @@ class Schema(C.Structure):
 class LoadOpts(C.Structure):
     _fields_ = [("scope", C.c_int32), ("apply_cap", C.c_int32), ("n_labels", C.c_int32),
                 ("label_ids", _i64p), ("weight_key", C.c_int64)]
+
+
+class EdgeEntry(C.Structure):
+    _fields_ = [("type_id", C.c_int64), ("other_id", C.c_int64), ("dir", C.c_int32), ("selected", C.c_int32),
+                ("has_weight", C.c_int32), ("weight", C.c_int32)]
 
 
 class Edges(C.Structure):
@@ -108,7 +114,7 @@ EXPORTS = [
     "tgo_finish_load", "tgo_load_edges", "tgo_num_vertices", "tgo_vertex_ids", "tgo_bfs",
     "tgo_sssp", "tgo_copy_distances", "tgo_pagerank", "tgo_walkcount", "tgo_stats_get", "tgo_sync",
     "tgo_bfs_multi", "tgo_copy_multi_distances", "tgo_multi_stats",
-    "tgo_gather", "tgo_combine_global", "tgo_dense_ids",
+    "tgo_gather", "tgo_combine_global", "tgo_dense_ids", "tgo_decode_edge_entry",
     "tgo_rmat_edges", "tgo_pick_roots", "tgo_synth_rows",
     # titan_gpu_olap_part.h (1-D vertex-partitioned multi-GPU)
     "tgo_load_partition", "tgo_part_layout", "tgo_load_partition_layout", "tgo_part_bfs_begin", "tgo_part_bfs_td", "tgo_part_bfs_claim", "tgo_part_bfs_bu",
@@ -147,6 +153,7 @@ def load() -> C.CDLL:
         "tgo_last_error": (C.c_char_p, [vp]),
         "tgo_load_rows": (C.c_int, [vp, P(Rows), P(Schema), P(LoadOpts)]),
         "tgo_finish_load": (C.c_int, [vp]),
+        "tgo_decode_edge_entry": (C.c_int, [P(Schema), P(LoadOpts), _u8p, C.c_int64, C.c_int64, P(EdgeEntry)]),
         "tgo_load_edges": (C.c_int, [vp, P(Edges), P(LoadOpts)]),
         "tgo_num_vertices": (C.c_int64, [vp]),
         "tgo_vertex_ids": (C.c_int, [vp, _i64p]),

@@ -675,6 +675,13 @@ void tgo_destroy(tgo_ctx* ctx) {
 
 const char* tgo_last_error(const tgo_ctx* ctx) { return ctx ? ctx->err.c_str() : "null ctx"; }
 
+int tgo_decode_edge_entry(const tgo_schema* schema, const tgo_load_opts* opts, const uint8_t* entry,
+                          int64_t len, int64_t value_pos, tgo_edge_entry* out) {
+    if (!schema || !opts || !out) return TGO_E_INVALID;
+    std::string err;
+    return decode_one_entry(schema, opts, entry, len, value_pos, out, err);
+}
+
 int tgo_load_rows(tgo_ctx* ctx, const tgo_rows* rows, const tgo_schema* schema, const tgo_load_opts* opts) {
     if (!ctx) return TGO_E_INVALID;
     if (!rows || !schema || !opts) return fail(ctx, TGO_E_INVALID, "null argument");

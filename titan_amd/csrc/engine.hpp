@@ -63,6 +63,20 @@ struct RowStaging {
 // reference throw inside execute() (edge.value() on a missing key), i.e. TGO_E_PROGRAM.
 constexpr int32_t kMissingWeight = INT32_MIN;
 
+// Owner of a codec PlanView (codec.hpp) built from tgo_schema + tgo_load_opts.
+struct HostPlan {
+    std::vector<uint8_t> label_bytes;   // LabelPlan records (opaque here; codec.hpp defines them)
+    std::vector<int64_t> key_ids;
+    std::vector<int8_t> key_dts;
+    std::vector<int8_t> dts;
+    int32_t n_labels = 0;
+    int64_t weight_key = 0;
+};
+int build_plan(const tgo_schema* schema, const tgo_load_opts* opts, HostPlan& hp, std::string& err);
+// tgo_decode_edge_entry body (graph_build.cpp).
+int decode_one_entry(const tgo_schema* schema, const tgo_load_opts* opts, const uint8_t* entry,
+                     int64_t len, int64_t value_pos, tgo_edge_entry* out, std::string& err);
+
 int decode_rows(RowStaging& st, const tgo_rows* rows, const tgo_schema* schema,
                 const tgo_load_opts* opts, int pb, int64_t hard_limit, int threads,
                 std::string& err);

@@ -45,30 +45,102 @@ static void parallel_dynamic(int64_t n, int threads, int64_t chunk, F&& fn) {
 }
 
 // ------------------------------------------------------------------ rows -> staging
+// Decode plan: labels sorted by type id, property keys sorted by id (binary-searched by the
+// codec on the host and on the device).  The weight is an Integer property
+// (ShortestDistanceVertexProgram.java:53 reads edge.<Integer>value(weight): another datatype
+// is a ClassCastException in the reference).
+int build_plan(const tgo_schema* schema, const tgo_load_opts* opts, HostPlan& hp, std::string& err) {
+    hp = HostPlan();
+    hp.weight_key = opts->weight_key;
+    std::vector<std::pair<int64_t, int8_t>> keys;
+    for (int k = 0; k < schema->n_property_keys; ++k)
+        keys.emplace_back(schema->property_keys[k].key_id, static_cast<int8_t>(schema->property_keys[k].datatype));
+    std::sort(keys.begin(), keys.end());
+    for (const auto& kt : keys) { hp.key_ids.push_back(kt.first); hp.key_dts.push_back(kt.second); }
+    auto dt_of = [&](int64_t key) -> int8_t {
+        auto it = std::lower_bound(hp.key_ids.begin(), hp.key_ids.end(), key);
+        return it != hp.key_ids.end() && *it == key ? hp.key_dts[it - hp.key_ids.begin()] : 0;
+    };
+    if (opts->weight_key != 0 && dt_of(opts->weight_key) != TGO_DT_INTEGER) {
+        err = "weight property must be an Integer key (edge.<Integer>value in ShortestDistanceVertexProgram)";
+        return TGO_E_UNSUPPORTED;
+    }
+    std::vector<LabelPlan> labels;
+    for (int t = 0; t < schema->n_edge_types; ++t) {
+        const tgo_edge_type& et = schema->edge_types[t];
+        LabelPlan lp{};
+        lp.type_id = et.type_id;
+        lp.multiplicity = et.multiplicity;
+        lp.desc = et.sort_order == TGO_ORDER_DESC;
+        lp.selected = 1;
+        if (opts->n_labels > 0) {
+            lp.selected = 0;
+            for (int j = 0; j < opts->n_labels; ++j) lp.selected |= opts->label_ids[j] == et.type_id;
+        }
+        const bool multi = et.multiplicity == TGO_MULTI;
+        lp.n_sort = multi ? et.n_sort_key : 0;     // constrained labels carry no sort key (:235)
+        lp.n_sig = et.n_signature;
+        lp.sort_dt_off = static_cast<int32_t>(hp.dts.size());
+        for (int k = 0; k < lp.n_sort; ++k) hp.dts.push_back(dt_of(et.sort_key_ids[k]));
+        lp.sig_dt_off = static_cast<int32_t>(hp.dts.size());
+        for (int k = 0; k < lp.n_sig; ++k) hp.dts.push_back(dt_of(et.signature_ids[k]));
+        lp.weight_where = opts->weight_key == 0 ? kWeightNone : kWeightRemaining;
+        for (int k = 0; k < lp.n_sort && opts->weight_key != 0; ++k)
+            if (et.sort_key_ids[k] == opts->weight_key) { lp.weight_where = kWeightSortKey; lp.weight_index = k; break; }
+        for (int k = 0; k < lp.n_sig && lp.weight_where == kWeightRemaining; ++k)
+            if (et.signature_ids[k] == opts->weight_key) { lp.weight_where = kWeightSignature; lp.weight_index = k; break; }
+        labels.push_back(lp);
+    }
+    std::sort(labels.begin(), labels.end(), [](const LabelPlan& a, const LabelPlan& b) { return a.type_id < b.type_id; });
+    for (size_t i = 1; i < labels.size(); ++i)
+        if (labels[i].type_id == labels[i - 1].type_id) { err = "duplicate edge type in schema"; return TGO_E_INVALID; }
+    hp.n_labels = static_cast<int32_t>(labels.size());
+    hp.label_bytes.resize(labels.size() * sizeof(LabelPlan));
+    if (!labels.empty()) std::memcpy(hp.label_bytes.data(), labels.data(), hp.label_bytes.size());
+    return TGO_OK;
+}
+
+PlanView plan_view(const HostPlan& hp) {
+    PlanView v{};
+    v.labels = reinterpret_cast<const LabelPlan*>(hp.label_bytes.data());
+    v.n_labels = hp.n_labels;
+    v.n_keys = static_cast<int32_t>(hp.key_ids.size());
+    v.key_ids = hp.key_ids.data();
+    v.key_dts = hp.key_dts.data();
+    v.dts = hp.dts.data();
+    v.weight_key = hp.weight_key;
+    return v;
+}
+
+int decode_one_entry(const tgo_schema* schema, const tgo_load_opts* opts, const uint8_t* entry,
+                     int64_t len, int64_t value_pos, tgo_edge_entry* out, std::string& err) {
+    HostPlan hp;
+    if (int rc = build_plan(schema, opts, hp, err)) return rc;
+    if (len < 0 || value_pos < 0 || (len > 0 && !entry)) { err = "invalid entry"; return TGO_E_INVALID; }
+    DecodedEdge de{};
+    const DecodeResult dr = decode_edge(entry, static_cast<size_t>(len), static_cast<size_t>(value_pos),
+                                        plan_view(hp), de);
+    *out = tgo_edge_entry{};
+    if (dr == DecodeResult::kError) { err = "malformed edge entry"; return TGO_E_CODEC; }
+    if (dr == DecodeResult::kUnsupported) { err = "inline property of a key missing from the schema"; return TGO_E_UNSUPPORTED; }
+    if (dr == DecodeResult::kSkip) return TGO_OK;
+    out->type_id = de.type_id;
+    out->other_id = de.other;
+    out->dir = de.dir;
+    out->selected = 1;
+    out->has_weight = de.has_weight ? 1 : 0;
+    out->weight = de.weight;
+    return TGO_OK;
+}
+
+
+// ------------------------------------------------------------------ rows -> staging
 int decode_rows(RowStaging& st, const tgo_rows* rows, const tgo_schema* schema,
                 const tgo_load_opts* opts, int pb, int64_t hard_limit, int threads,
                 std::string& err) {
-    DecodePlan plan;
-    plan.weight_key = opts->weight_key;
-    for (int k = 0; k < schema->n_property_keys; ++k)
-        plan.key_types.emplace_back(schema->property_keys[k].key_id, schema->property_keys[k].datatype);
-    for (int t = 0; t < schema->n_edge_types; ++t) {
-        const tgo_edge_type& et = schema->edge_types[t];
-        LabelPlan lp;
-        lp.type_id = et.type_id;
-        lp.multiplicity = et.multiplicity;
-        if (opts->n_labels > 0) {
-            lp.selected = false;
-            for (int j = 0; j < opts->n_labels; ++j) lp.selected |= opts->label_ids[j] == et.type_id;
-        }
-        for (int k = 0; k < et.n_signature; ++k) {
-            lp.sig_types.push_back(plan.datatype(et.signature_ids[k]));
-            if (et.signature_ids[k] == opts->weight_key && lp.weight_sig_index < 0) lp.weight_sig_index = k;
-        }
-        if (et.multiplicity == TGO_MULTI)
-            for (int k = 0; k < et.n_sort_key; ++k) lp.weight_in_sortkey |= et.sort_key_ids[k] == opts->weight_key;
-        plan.labels.push_back(lp);
-    }
+    HostPlan hp;
+    if (int rc = build_plan(schema, opts, hp, err)) return rc;
+    const PlanView plan = plan_view(hp);
     // Untyped single-direction scopes are not "fitted" and get the hard limit; BOTH and
     // typed scopes keep NO_LIMIT (BasicVertexCentricQueryBuilder.java:418-431,469-474;
     // QueryContainer.java:122).
@@ -129,14 +201,14 @@ int decode_rows(RowStaging& st, const tgo_rows* rows, const tgo_schema* schema,
                 if (dr == DecodeResult::kSkip) continue;
                 if (dr != DecodeResult::kOk) {
                     L.rc = dr == DecodeResult::kUnsupported ? TGO_E_UNSUPPORTED : TGO_E_CODEC;
-                    L.msg = dr == DecodeResult::kUnsupported ? "weight property datatype/placement not supported"
+                    L.msg = dr == DecodeResult::kUnsupported ? "inline property of a key missing from the schema"
                                                              : "malformed edge entry";
                     break;
                 }
                 // messages are looked up by canonical id (VertexMemoryHandler.java:89)
                 L.other.push_back(is_partitioned_vertex(de.other, pb) ? canonical_vertex_id(de.other, pb) : de.other);
                 L.dir.push_back(static_cast<uint8_t>(de.dir));
-                L.w.push_back(plan.weight_key == 0 ? 1 : (de.has_weight ? de.weight : kMissingWeight));
+                L.w.push_back(opts->weight_key == 0 ? 1 : (de.has_weight ? de.weight : kMissingWeight));
                 ++kept;
             }
             if (L.rc != TGO_OK) break;

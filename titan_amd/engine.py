@@ -33,7 +33,7 @@ class Schema:
             sg = np.ascontiguousarray(t.get("signature", []), dtype=np.int64)
             self._keep += [sk, sg]
             et[i] = L.EdgeType(t["type_id"], t["multiplicity"], len(sk), L.ptr(sk, C.c_int64),
-                               len(sg), L.ptr(sg, C.c_int64))
+                               len(sg), 1 if t.get("order", "ASC") == "DESC" else 0, L.ptr(sg, C.c_int64))
         pk = (L.PropertyKey * max(1, len(property_keys)))()
         for i, (kid, dt) in enumerate(property_keys):
             pk[i] = L.PropertyKey(kid, dt)
