@@ -326,6 +326,43 @@ int  tgo_combine_global(tgo_ctx* ctx, int32_t value_type, int32_t combiner, int6
  * 111-115); -1 for an id that is not an executed vertex (its messages are never read). */
 int  tgo_dense_ids(tgo_ctx* ctx, const int64_t* titan_ids, int64_t count, int64_t* dense_out);
 
+/* ---- Result write-back ----------------------------------------------
+ * ResultMode PERSIST / LOCALTX: FulgoraGraphComputer writes every vertex's compute-key
+ * properties back with v.property(Cardinality.single, key, value) in batched transactions
+ * (FulgoraGraphComputer.java:248-305, VertexPropertyWriter :314-342).  tgo_result_rows encodes,
+ * on the device, the edgestore entries those writes produce for the LAST finished program of
+ * `kind` — one row per vertex holding the property, in the API's row order, each entry a
+ * SINGLE-cardinality property entry (EdgeSerializer.writeRelation :261-283): column = the key's
+ * relation-type header, value = null flag + serialized value + relation id.  The caller hands
+ * the rows to the store as mutations (column overwrite = the single-cardinality replace).
+ *   DISTANCE  ShortestDistance DISTANCE (Long) on reached vertices (tgo_bfs / tgo_sssp)
+ *   PAGERANK  PAGE_RANK and OUTGOING_EDGE_COUNT (Double) on every executed vertex once
+ *             iterations >= 1 (PageRankVertexProgram.java:79-88)
+ *   DEGREE    OLAPTest.DegreeCounter DEGREE (Integer) on every executed vertex
+ * Compute keys must be typed property keys of those datatypes (a key left to
+ * getOrCreatePropertyKey's generic Object type is TGO_E_UNSUPPORTED).  Relation ids are
+ * relation_id_base + the entry's running index (a block the caller reserved).
+ * out == NULL: only *size is filled; otherwise out's buffers (sized from a first call) get
+ * nrows keys, nrows+1 entry / byte offsets, nbytes bytes and nentries limit|valuePos words
+ * (the tgo_rows layout, so the rows can be scanned again). */
+typedef enum { TGO_RESULT_DISTANCE = 0, TGO_RESULT_PAGERANK = 1, TGO_RESULT_DEGREE = 2 } tgo_result_kind;
+typedef struct {
+    int32_t kind;                 /* tgo_result_kind                                          */
+    int32_t reserved;
+    int64_t key_ids[2];           /* [0] DISTANCE / PAGE_RANK / DEGREE key; [1] OUTGOING_EDGE_COUNT */
+    int32_t datatypes[2];         /* tgo_datatype of each key                                  */
+    int64_t relation_id_base;
+} tgo_result_args;
+typedef struct { int64_t nrows, nentries, nbytes; } tgo_result_size;
+typedef struct {
+    int64_t* row_keys;
+    int64_t* row_entry_begin;
+    int64_t* row_byte_begin;
+    uint8_t* entry_bytes;
+    int64_t* entry_limit_valpos;
+} tgo_rows_buf;
+int  tgo_result_rows(tgo_ctx* ctx, const tgo_result_args* args, tgo_result_size* size, const tgo_rows_buf* out);
+
 int  tgo_stats_get(tgo_ctx* ctx, tgo_stats* out);
 /* Block until all work queued on the ctx stream has finished. */
 int  tgo_sync(tgo_ctx* ctx);

@@ -103,6 +103,7 @@ def load() -> C.CDLL:
                                      C.c_int64, P(FrProp), C.c_int]),
         "fr_encode_vertex_exists": (C.c_int, [P(FrBuf), _i32p, C.c_int64]),
         "fr_write_value": (C.c_int, [P(FrBuf), C.c_int, C.c_int, C.c_int64, C.c_int]),
+        "fr_encode_property_f64": (C.c_int, [P(FrBuf), _i32p, C.c_int64, C.c_double, C.c_int64]),
         "fr_string_of": (C.c_int, [C.c_int64, P(C.c_uint16)]),
         "fr_encode_property": (C.c_int, [P(FrBuf), _i32p, C.c_int64, C.c_int, C.c_int64, C.c_int64]),
         "fr_decode_edge": (C.c_int, [_u8p, C.c_size_t, C.c_size_t, P(FrSchema), C.c_int64, _i64p,
@@ -188,6 +189,16 @@ def encode_property(key_id, datatype, value, relation_id):
     rc = lib.fr_encode_property(C.byref(b), C.byref(vp), key_id, datatype, value, relation_id)
     if rc:
         raise ValueError(f"fr_encode_property rc={rc}")
+    out = C.string_at(b.p, b.len)
+    lib.fr_buf_free(C.byref(b))
+    return out, vp.value
+
+
+def encode_property_f64(key_id, value, relation_id):
+    lib = load()
+    b = FrBuf()
+    vp = C.c_int32(0)
+    lib.fr_encode_property_f64(C.byref(b), C.byref(vp), key_id, float(value), relation_id)
     out = C.string_at(b.p, b.len)
     lib.fr_buf_free(C.byref(b))
     return out, vp.value

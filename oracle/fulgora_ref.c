@@ -393,6 +393,16 @@ int fr_encode_property(fr_buf* out, int32_t* value_pos, int64_t key_id, int data
     return FR_OK;
 }
 
+int fr_encode_property_f64(fr_buf* out, int32_t* value_pos, int64_t key_id, double value, int64_t relation_id) {
+    fr_write_relation_type(out, key_id, 0, 0, 0);                       /* EdgeSerializer.java:270-281 */
+    *value_pos = (int32_t)out->len;
+    buf_put(out, 0x00);                                                 /* StandardSerializer null flag */
+    uint64_t u; memcpy(&u, &value, 8);
+    put_be(out, u, 8);
+    fr_vl_write_positive(out, relation_id);
+    return FR_OK;
+}
+
 int fr_encode_edge(fr_buf* out, int32_t* value_pos, const fr_schema* schema, int64_t type_id,
                    int dir, int64_t other, int64_t relation_id, const fr_prop* props, int nprops) {
     /* EdgeSerializer.writeRelation :222-315 (edge branch :255-266) */

@@ -108,6 +108,8 @@ int fr_encode_edge(fr_buf* out, int32_t* value_pos, const fr_schema* schema, int
 /* A SINGLE-cardinality user property entry (prefix 0x40-0x5F, outside the edge slice). */
 int fr_encode_property(fr_buf* out, int32_t* value_pos, int64_t key_id, int datatype,
                        int64_t value, int64_t relation_id);
+/* The same for a Double-valued key (DoubleSerializer.write: the raw IEEE bits, :33-36). */
+int fr_encode_property_f64(fr_buf* out, int32_t* value_pos, int64_t key_id, double value, int64_t relation_id);
 /* VertexExists system property entry (BaseKey.java:27-28), the first entry of every live row. */
 int fr_encode_vertex_exists(fr_buf* out, int32_t* value_pos, int64_t relation_id);
 /* Decode one edge entry.  weight_key==0: no weight.  Returns FR_OK / FR_E_CODEC. */

@@ -565,3 +565,38 @@ def test_typed_scope_is_fitted_and_sees_only_its_label(scope):
         fin = np.isfinite(opr)
         assert np.array_equal(np.isfinite(pr), fin)
         assert np.abs(pr[fin] - opr[fin]).sum() <= PR_L1_TOL
+
+
+def test_rows_with_sort_key_weights_and_string_properties():
+    """Codec breadth through the device load: a MULTI label whose sort key is
+    (String, Float, weight) in DESC order, a String + Double signature and String / Date /
+    Character remaining properties; SSSP distances bit-exact against the oracle in every scope,
+    cap on (EdgeSerializer.java:130-152,311-313; StringSerializer, FloatSerializer, ...)."""
+    import random
+    import edgestore as es
+    lib = fr.load()
+    knows = es.user_edge_label(1)
+    w, ks, kf, kd, kdt, kc = (lib.fr_schema_id(0, c) for c in (1, 2, 3, 4, 5, 6))
+    pkeys = [(w, 3), (ks, 10), (kf, 5), (kd, 6), (kdt, 8), (kc, 9)]
+    sd = {"edge_types": [{"type_id": knows, "multiplicity": 0, "sort_key": [ks, kf, w], "signature": [ks, kd],
+                          "order": "DESC"}],
+          "property_keys": [list(p) for p in pkeys]}
+    osch = fr.OracleSchema(sd["edge_types"], pkeys)
+    scale = 9
+    src, dst, _ = rmat_edges(scale, 8, seed=5)
+    n = 1 << scale
+    rnd = random.Random(11)
+    edges = []
+    for a, b in zip(src, dst):
+        props = [(w, rnd.randint(1, 40)), (ks, rnd.choice([0, 7, -31, 123456])), (kf, rnd.randint(-9, 9)),
+                 (kd, rnd.randint(-5, 5)), (kdt, rnd.randint(0, 1 << 40)), (kc, rnd.randint(1, 0xFFFF))]
+        edges.append((int(a), int(b), knows, [p for p in props if rnd.random() > 0.05 or p[0] == w]))
+    rows, vids = es.build_rows(es.GraphSpec(n=n, edges=edges), osch)
+    for scope in (IN, OUT, BOTH):
+        o = fr.OracleGraph.from_rows(rows, osch, scope, hard_limit=40, weight_key=w)
+        eng = Engine(hard_query_limit=40).load_rows(rows, Schema.from_dict(sd), scope, weight_key=w, batch_rows=100)
+        assert eng.stats()["truncated_results"] == o.stats.truncated_results
+        for r in vids[:3]:
+            assert np.array_equal(eng.sssp(int(r), 5, scope), o.shortest_distance(int(r), 5, scope, weighted=True)[0])
+            assert np.array_equal(eng.sssp(int(r), n, scope, mode=L.SSSP_DELTA),
+                                  o.shortest_distance(int(r), n, scope, weighted=True)[0])

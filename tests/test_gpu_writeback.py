@@ -1,0 +1,162 @@
+"""GPU: result write-back.  tgo_result_rows encodes the last program's compute
+keys on the device; the rows must equal, byte for byte, the entries the oracle's
+EdgeSerializer restatement writes for v.property(single, key, value) on the same vertices with
+the same relation ids (FulgoraGraphComputer.java:248-305; EdgeSerializer.java:261-283), and
+PERSIST / LOCALTX must leave the store / the local transaction holding those values."""
+import numpy as np
+import pytest
+
+import fulgora as fr
+from conftest import load_fixture
+from titan_amd import (DegreeCounter, Engine, GpuGraph, PageRankVertexProgram, Schema, ShortestDistanceVertexProgram,
+                       TitanException, TitanGraphComputer, rmat_edges)
+from titan_amd import _lib as L
+
+pytestmark = pytest.mark.gpu
+OUT, IN, BOTH = L.SCOPE_OUT_E, L.SCOPE_IN_E, L.SCOPE_BOTH_E
+DIST, PR, EC, DEG = ((c << 6) | 5 for c in (900, 901, 902, 903))
+BASE = 1 << 40
+
+
+def expected_rows(ids, entries_of):
+    """Rows of the oracle's entries for every vertex (API row order) that holds a value."""
+    keys, eb, bb, data, lv = [], [0], [0], bytearray(), []
+    rel = BASE
+    lib = fr.load()
+    for i, vid in enumerate(ids):
+        ents = entries_of(i, rel)
+        if not ents:
+            continue
+        rel += len(ents)
+        start = len(data)
+        for b, vp in sorted(ents, key=lambda e: e[0][:e[1]]):
+            data += b
+            lv.append(((len(data) - start) << 32) | vp)
+        keys.append(lib.fr_key_of(int(vid), 5))
+        eb.append(len(lv))
+        bb.append(len(data))
+    return keys, eb, bb, bytes(data), lv
+
+
+def assert_rows_equal(got, want):
+    keys, eb, bb, data, lv = want
+    assert list(got.keys) == keys
+    assert list(got.entry_begin) == eb and list(got.byte_begin) == bb
+    assert bytes(got.data) == data
+    assert list(got.limit_valpos) == lv
+
+
+@pytest.fixture(scope="module")
+def rmat_rows():
+    import edgestore as es
+    scale = 9
+    src, dst, w = rmat_edges(scale, 8, seed=77, weights=True)
+    n = 1 << scale
+    knows = es.user_edge_label(1)
+    wkey = (1 << 6) | 5
+    sd = {"edge_types": [{"type_id": knows, "multiplicity": 0, "signature": [wkey]}], "property_keys": [[wkey, 3]]}
+    osch = fr.OracleSchema(sd["edge_types"], [(wkey, 3)])
+    spec = es.GraphSpec(n=n, edges=[(int(a), int(b), knows, [(wkey, int(x))]) for a, b, x in zip(src, dst, w)])
+    rows, vids = es.build_rows(spec, osch)
+    return rows, vids, sd, wkey, n
+
+
+def test_distance_rows_match_oracle_encoder(rmat_rows):
+    rows, vids, sd, wkey, n = rmat_rows
+    eng = Engine(hard_query_limit=40).load_rows(rows, Schema.from_dict(sd), IN, weight_key=wkey)
+    ids = eng.vertex_ids()
+    for depth, mode in ((3, L.SSSP_HOP_BOUNDED), (n, L.SSSP_DELTA)):
+        d = eng.sssp(int(vids[1]), depth, IN, mode=mode)
+        got = eng.result_rows(L.RESULT_DISTANCE, [DIST], [L.DT_LONG], BASE)
+        want = expected_rows(ids, lambda i, rel: [] if d[i] == L.DIST_ABSENT else
+                             [fr.encode_property(DIST, L.DT_LONG, int(d[i]), rel)])
+        assert_rows_equal(got, want)
+    d = eng.bfs(int(vids[2]), n, IN)
+    got = eng.result_rows(L.RESULT_DISTANCE, [DIST], [L.DT_LONG], BASE)
+    assert_rows_equal(got, expected_rows(ids, lambda i, rel: [] if d[i] == L.DIST_ABSENT else
+                                         [fr.encode_property(DIST, L.DT_LONG, int(d[i]), rel)]))
+
+
+@pytest.mark.parametrize("keys", [(PR, EC), (EC + (5 << 6), PR)])
+def test_pagerank_rows_match_oracle_encoder(rmat_rows, keys):
+    rows, vids, sd, wkey, n = rmat_rows
+    eng = Engine(hard_query_limit=40).load_rows(rows, Schema.from_dict(sd), IN)
+    ids = eng.vertex_ids()
+    pr = eng.pagerank(0.85, n, 6)
+    outdeg = np.zeros(len(ids))
+    o = fr.OracleGraph.from_rows(rows, fr.OracleSchema(sd["edge_types"], [(wkey, 3)]), IN, hard_limit=40)
+    assert np.array_equal(o.vertex_ids(), ids)
+    off, mid, adj, _ = o.export()
+    outdeg = (mid - off[:-1]).astype(np.float64)          # OUT entries kept per vertex = edgeCount
+    got = eng.result_rows(L.RESULT_PAGERANK, list(keys), [L.DT_DOUBLE, L.DT_DOUBLE], BASE)
+    def col(kv):
+        return fr.buf_bytes("fr_write_relation_type", kv[0], 0, 0, 0)
+
+    def entries(i, rel):
+        kvs = sorted([(keys[0], pr[i]), (keys[1], outdeg[i])], key=col)
+        return [fr.encode_property_f64(k, v, rel + j) for j, (k, v) in enumerate(kvs)]
+
+    want = expected_rows(ids, entries)
+    assert_rows_equal(got, want)
+    # iterations(0): no PAGE_RANK property is ever set
+    eng.pagerank(0.85, n, 0)
+    assert eng.result_rows(L.RESULT_PAGERANK, list(keys), [L.DT_DOUBLE, L.DT_DOUBLE], BASE).nrows == 0
+
+
+def test_degree_rows_and_errors(rmat_rows):
+    rows, vids, sd, wkey, n = rmat_rows
+    eng = Engine(hard_query_limit=40).load_rows(rows, Schema.from_dict(sd), IN)
+    ids = eng.vertex_ids()
+    deg = eng.walkcount(6)                                  # wraps like Java int at k = 6
+    got = eng.result_rows(L.RESULT_DEGREE, [DEG], [L.DT_INTEGER], BASE)
+    assert_rows_equal(got, expected_rows(ids, lambda i, rel: [fr.encode_property(DEG, L.DT_INTEGER, int(deg[i]), rel)]))
+    with pytest.raises(TitanException):                     # last program is DegreeCounter
+        eng.result_rows(L.RESULT_DISTANCE, [DIST], [L.DT_LONG], BASE)
+    with pytest.raises(TitanException):                     # DEGREE is an Integer key
+        eng.result_rows(L.RESULT_DEGREE, [DEG], [L.DT_LONG], BASE)
+
+
+def test_persist_and_localtx_through_computer():
+    rows, vids, sd, npz = load_fixture("gotg")
+    keys = {ShortestDistanceVertexProgram.DISTANCE: (DIST, L.DT_LONG),
+            PageRankVertexProgram.PAGE_RANK: (PR, L.DT_DOUBLE),
+            PageRankVertexProgram.OUTGOING_EDGE_COUNT: (EC, L.DT_DOUBLE),
+            DegreeCounter.DEGREE: (DEG, L.DT_INTEGER)}
+    graph = GpuGraph(rows, sd, property_keys=keys)
+    seed = int(vids[list(npz["names"]).index("saturn")])
+    # LOCALTX: the store is unchanged, the result graph sees the values
+    c = graph.compute()
+    c.resultMode(TitanGraphComputer.ResultMode.LOCALTX)
+    c.program(ShortestDistanceVertexProgram(seed, 5, scope="inE", weighted=False))
+    res = c.submit().get()
+    ids, dist = res.vertex_properties[ShortestDistanceVertexProgram.DISTANCE]
+    assert graph.read_property(seed, DIST, L.DT_LONG) is None
+    for vid, d in zip(ids, dist):
+        want = None if d == L.DIST_ABSENT else int(d)
+        assert res.graph().read_property(int(vid), DIST, L.DT_LONG) == want
+    # PERSIST: the store holds them, and a fresh scan of the new rows traverses identically
+    c = graph.compute()
+    c.resultMode(TitanGraphComputer.ResultMode.PERSIST)
+    c.program(DegreeCounter(1))
+    res = c.submit().get()
+    ids, deg = res.vertex_properties[DegreeCounter.DEGREE]
+    assert res.graph() is graph
+    assert [graph.read_property(int(v), DEG, L.DT_INTEGER) for v in ids] == [int(x) for x in deg]
+    assert sorted(int(x) for x in deg) == sorted(int(x) for x in npz["degree1"])
+    eng_before = Engine().load_rows(rows, Schema.from_dict(sd), BOTH)
+    eng_after = Engine().load_rows(graph.rows, Schema.from_dict(sd), BOTH)
+    assert np.array_equal(eng_before.vertex_ids(), eng_after.vertex_ids())
+    assert eng_after.stats()["ghost_vertices"] == eng_before.stats()["ghost_vertices"]
+    for v in vids[:4]:
+        assert np.array_equal(eng_before.bfs(int(v), 12, BOTH), eng_after.bfs(int(v), 12, BOTH))
+    # PageRank: both compute keys land on every vertex, equal to the program's result
+    c = graph.compute()
+    c.resultMode(TitanGraphComputer.ResultMode.PERSIST)
+    c.program(PageRankVertexProgram(0.85, 3, 12))
+    res = c.submit().get()
+    ids, pr = res.vertex_properties[PageRankVertexProgram.PAGE_RANK]
+    for vid, x in zip(ids, pr):
+        assert graph.read_property(int(vid), PR, L.DT_DOUBLE) == x
+        assert graph.read_property(int(vid), EC, L.DT_DOUBLE) is not None
+    # DegreeCounter values survive the later PageRank write (different keys, same rows)
+    assert [graph.read_property(int(v), DEG, L.DT_INTEGER) for v in ids] == [int(x) for x in deg]

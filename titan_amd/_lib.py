@@ -26,6 +26,9 @@ TGO_E_COMM = -8
 SCOPE_OUT_E, SCOPE_IN_E, SCOPE_BOTH_E = 0, 1, 2
 MULTI, SIMPLE, MANY2ONE, ONE2MANY, ONE2ONE = 0, 1, 2, 3, 4
 DT_BYTE, DT_SHORT, DT_INTEGER, DT_LONG, DT_FLOAT, DT_DOUBLE, DT_BOOLEAN = 1, 2, 3, 4, 5, 6, 7
+DT_DATE, DT_CHARACTER, DT_STRING = 8, 9, 10
+ORDER_ASC, ORDER_DESC = 0, 1
+RESULT_DISTANCE, RESULT_PAGERANK, RESULT_DEGREE = 0, 1, 2
 SSSP_HOP_BOUNDED, SSSP_DELTA = 0, 1
 FLAG_STATS = 1
 DIST_ABSENT = -(1 << 63)
@@ -74,6 +77,20 @@ class EdgeEntry(C.Structure):
                 ("has_weight", C.c_int32), ("weight", C.c_int32)]
 
 
+class ResultArgs(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("reserved", C.c_int32), ("key_ids", C.c_int64 * 2), ("datatypes", C.c_int32 * 2),
+                ("relation_id_base", C.c_int64)]
+
+
+class ResultSize(C.Structure):
+    _fields_ = [("nrows", C.c_int64), ("nentries", C.c_int64), ("nbytes", C.c_int64)]
+
+
+class RowsBuf(C.Structure):
+    _fields_ = [("row_keys", _i64p), ("row_entry_begin", _i64p), ("row_byte_begin", _i64p),
+                ("entry_bytes", _u8p), ("entry_limit_valpos", _i64p)]
+
+
 class Edges(C.Structure):
     _fields_ = [("n", C.c_int64), ("m", C.c_int64), ("src", _i32p), ("dst", _i32p),
                 ("weight", _i32p), ("titan_ids", _i64p)]
@@ -114,7 +131,7 @@ EXPORTS = [
     "tgo_finish_load", "tgo_load_edges", "tgo_num_vertices", "tgo_vertex_ids", "tgo_bfs",
     "tgo_sssp", "tgo_copy_distances", "tgo_pagerank", "tgo_walkcount", "tgo_stats_get", "tgo_sync",
     "tgo_bfs_multi", "tgo_copy_multi_distances", "tgo_multi_stats",
-    "tgo_gather", "tgo_combine_global", "tgo_dense_ids", "tgo_decode_edge_entry",
+    "tgo_gather", "tgo_combine_global", "tgo_dense_ids", "tgo_decode_edge_entry", "tgo_result_rows",
     "tgo_rmat_edges", "tgo_pick_roots", "tgo_synth_rows",
     # titan_gpu_olap_part.h (1-D vertex-partitioned multi-GPU)
     "tgo_load_partition", "tgo_part_layout", "tgo_load_partition_layout", "tgo_part_bfs_begin", "tgo_part_bfs_td", "tgo_part_bfs_claim", "tgo_part_bfs_bu",
@@ -153,6 +170,7 @@ def load() -> C.CDLL:
         "tgo_last_error": (C.c_char_p, [vp]),
         "tgo_load_rows": (C.c_int, [vp, P(Rows), P(Schema), P(LoadOpts)]),
         "tgo_finish_load": (C.c_int, [vp]),
+        "tgo_result_rows": (C.c_int, [vp, P(ResultArgs), P(ResultSize), P(RowsBuf)]),
         "tgo_decode_edge_entry": (C.c_int, [P(Schema), P(LoadOpts), _u8p, C.c_int64, C.c_int64, P(EdgeEntry)]),
         "tgo_load_edges": (C.c_int, [vp, P(Edges), P(LoadOpts)]),
         "tgo_num_vertices": (C.c_int64, [vp]),

@@ -93,6 +93,116 @@ class Memory:
         return set(self._values)
 
 
+# ----------------------------------------------------------------------------- write-back
+def _relation_type_header(key_id: int) -> bytes:
+    """IDHandler.writeRelationType(keyId, PROPERTY_DIR) for a user property key (:88-94): prefix
+    0b010, then VariableLong.writePositiveWithPrefix(count << 1) (VariableLong.java:139-164)."""
+    v = (key_id >> 6) << 1
+    delta = 5
+    first = 2 << delta
+    vl = max(1, v.bit_length())
+    mod = vl % 7
+    if mod <= delta - 1:
+        off = vl - mod
+        first |= v >> off
+        v &= (1 << off) - 1
+        vl -= mod
+    else:
+        vl += 7 - mod
+    if vl > 0:
+        first |= 1 << (delta - 1)
+    out = [first]
+    while vl > 0:
+        vl -= 7
+        out.append(((v >> vl) & 0x7F) | (0x80 if vl == 0 else 0))
+    return bytes(out)
+
+
+def _row_key(vid: int, pb: int) -> int:
+    """IDManager.getKey (IDManager.java:461-473), as a signed 64-bit long."""
+    part = (vid >> 3) & ((1 << pb) - 1) if pb else 0
+    key = ((part << (64 - pb)) if pb else 0) | ((vid >> (3 + pb)) << 3) | (vid & 7)
+    return key - (1 << 64) if key >= (1 << 63) else key
+
+
+def _row_entries(rows, r):
+    base = int(rows.byte_begin[r])
+    out, start = [], 0
+    for e in range(int(rows.entry_begin[r]), int(rows.entry_begin[r + 1])):
+        lv = int(rows.limit_valpos[e])
+        end, vpos = lv >> 32, lv & 0x7FFFFFFF
+        out.append((bytes(rows.data[base + start:base + end]), vpos))
+        start = end
+    return out
+
+
+def merge_rows(store, mutations):
+    """Apply result rows to a row store the way the backend applies mutations: per row key the
+    entries are merged in column byte order and an entry whose column equals an existing one
+    replaces it (single cardinality: the column is the property key alone)."""
+    from .engine import Rows
+    rows = {int(k): _row_entries(store, r) for r, k in enumerate(store.keys)}
+    for r, k in enumerate(mutations.keys):
+        cur = {e[0][:e[1]]: e for e in rows.get(int(k), [])}
+        for e in _row_entries(mutations, r):
+            cur[e[0][:e[1]]] = e
+        rows[int(k)] = sorted(cur.values(), key=lambda e: e[0][:e[1]])
+    keys = sorted(rows, key=lambda k: k & ((1 << 64) - 1))       # unsigned key order
+    data, lv, eb, bb = bytearray(), [], [0], [0]
+    for k in keys:
+        start = len(data)
+        for b, vpos in rows[k]:
+            data += b
+            lv.append(((len(data) - start) << 32) | vpos)
+        eb.append(len(lv))
+        bb.append(len(data))
+    return Rows(np.asarray(keys, np.int64), np.asarray(eb, np.int64), np.asarray(bb, np.int64),
+                np.frombuffer(bytes(data) or b"\0", np.uint8).copy(), np.asarray(lv or [0], np.int64))
+
+
+def read_property(rows, vid: int, key_id: int, datatype: int, pb: int = 5):
+    """The value of a SINGLE-cardinality property on a vertex's row (EdgeSerializer.parseRelation
+    property branch :112-126), or None."""
+    key = _row_key(vid, pb)
+    idx = np.nonzero(rows.keys == key)[0]
+    if len(idx) == 0:
+        return None
+    hdr = _relation_type_header(key_id)
+    for b, vpos in _row_entries(rows, int(idx[0])):
+        if b[:vpos] != hdr:
+            continue
+        if b[vpos] == 0xFF:
+            return None
+        v = b[vpos + 1:]
+        if datatype == L.DT_LONG:
+            return int.from_bytes(v[:8], "big") - (1 << 63)
+        if datatype == L.DT_DOUBLE:
+            return float(np.frombuffer(v[:8][::-1], np.float64)[0])
+        if datatype == L.DT_INTEGER:
+            u, i = 0, 0
+            while True:
+                u = (u << 7) | (v[i] & 0x7F)
+                if v[i] & 0x80:
+                    break
+                i += 1
+            return -(u >> 1) if u & 1 else u >> 1
+        raise TitanException(L.TGO_E_UNSUPPORTED, f"datatype {datatype}")
+    return None
+
+
+class LocalTxGraph:
+    """ResultMode LOCALTX: the graph seen through a new, uncommitted transaction that holds the
+    computed properties (FulgoraGraphComputer.java:296-305, ResultGraph.NEW)."""
+
+    def __init__(self, graph, mutations):
+        self.graph = graph
+        self.mutations = mutations
+
+    def read_property(self, vid, key_id, datatype):
+        v = read_property(self.mutations, vid, key_id, datatype, self.graph.partition_bits)
+        return v if v is not None else self.graph.read_property(vid, key_id, datatype)
+
+
 class ComputerResult:
     def __init__(self, graph, memory: Memory, vertex_properties):
         self._graph = graph
@@ -300,8 +410,11 @@ class GpuGraph:
     the slice each message scope needs, once, and keeps it resident on the device."""
 
     def __init__(self, rows=None, schema=None, edges=None, device=0, partition_bits=5, hard_query_limit=100000,
-                 apply_cap=True):
+                 apply_cap=True, property_keys=None, relation_id_base=1 << 40):
         self.rows = rows
+        # compute-key name -> (PropertyKey schema id, tgo datatype): the typed keys write-back uses
+        self.property_keys = dict(property_keys or {})
+        self._next_relation_id = relation_id_base     # the IDAuthority block result writes draw from
         self.schema = schema if (schema is None or isinstance(schema, Schema)) else Schema.from_dict(schema)
         self.edges = edges       # (n, src, dst, weight) decoded-adjacency input
         self.device = device
@@ -313,6 +426,22 @@ class GpuGraph:
 
     def compute(self):
         return GpuGraphComputer(self)
+
+    def reserve_relation_ids(self, count):
+        with self._lock:
+            base = self._next_relation_id
+            self._next_relation_id += max(1, count)
+            return base
+
+    def persist(self, mutations):
+        """Commit result rows to the store (VertexPropertyWriter's batched transactions)."""
+        if self.rows is None:
+            raise TitanException(L.TGO_E_UNSUPPORTED, "write-back needs an edgestore-backed graph")
+        with self._lock:
+            self.rows = merge_rows(self.rows, mutations)
+
+    def read_property(self, vid, key_id, datatype):
+        return None if self.rows is None else read_property(self.rows, vid, key_id, datatype, self.partition_bits)
 
     def engine_for(self, scope: int, weight_key: int = 0) -> Engine:
         key = (scope, weight_key)
@@ -357,14 +486,39 @@ class GpuGraphComputer(TitanGraphComputer):
         return self
 
     def resultMode(self, mode):  # noqa: N802
-        """ResultMode NONE only: PERSIST / LOCALTX write compute keys back through batched
-        transactions in the reference (FulgoraGraphComputer.java:248-305), which this
-        path does not do — rejected instead of silently ignored."""
-        if mode != TitanGraphComputer.ResultMode.NONE:
-            raise TitanException(L.TGO_E_UNSUPPORTED, f"result mode {mode.name} (property write-back) is not supported; "
-                                                      "results are returned through memory and MapReduce")
-        self._mode = mode
+        """core/TitanGraphComputer.java:10-37.  NONE: results only in memory / MapReduce.
+        PERSIST: the compute keys are written back to the graph (FulgoraGraphComputer.java:
+        248-295, ResultGraph.ORIGINAL + Persist.VERTEX_PROPERTIES).  LOCALTX: they are held by a
+        new uncommitted transaction returned as the result graph (:296-305)."""
+        self._mode = TitanGraphComputer.ResultMode(mode)
         return self
+
+    # compute key name -> (tgo result kind, slot) for the natively run programs
+    _RESULT_KEYS = {ShortestDistanceVertexProgram: (L.RESULT_DISTANCE, (ShortestDistanceVertexProgram.DISTANCE,)),
+                    PageRankVertexProgram: (L.RESULT_PAGERANK, (PageRankVertexProgram.PAGE_RANK,
+                                                                PageRankVertexProgram.OUTGOING_EDGE_COUNT)),
+                    DegreeCounter: (L.RESULT_DEGREE, (DegreeCounter.DEGREE,))}
+
+    def _write_back(self, eng):
+        """Encode the last program's compute keys on the device (tgo_result_rows) and persist
+        them (PERSIST) or hand them to a local transaction (LOCALTX)."""
+        if self._mode == TitanGraphComputer.ResultMode.NONE:
+            return self.graph
+        spec = self._RESULT_KEYS.get(type(self._program))
+        if spec is None:
+            raise TitanException(L.TGO_E_UNSUPPORTED, f"write-back of {type(self._program).__name__} compute keys")
+        kind, names = spec
+        missing = [k for k in names if k not in self.graph.property_keys]
+        if missing:
+            raise TitanException(L.TGO_E_UNSUPPORTED, f"compute keys {missing} have no typed PropertyKey "
+                                                      "(getOrCreatePropertyKey would make them generic Object keys)")
+        keys = [self.graph.property_keys[k] for k in names]
+        base = self.graph.reserve_relation_ids(eng.n * len(keys))
+        rows = eng.result_rows(kind, [k for k, _ in keys], [d for _, d in keys], base)
+        if self._mode == TitanGraphComputer.ResultMode.PERSIST:
+            self.graph.persist(rows)
+            return self.graph
+        return LocalTxGraph(self.graph, rows)
 
     def program(self, program: VertexProgram):
         if self._program is not None:
@@ -422,9 +576,10 @@ class GpuGraphComputer(TitanGraphComputer):
         values = {}
         for mr in self._map_reduces:
             values[mr.memory_key] = mr.emit(ids, props)
+        result_graph = self._write_back(eng)
         rt = (time.perf_counter() - t0) * 1000.0
         vprops = {k: (ids, v) for k, v in props.items()}
-        return ComputerResult(self.graph, Memory(iteration, rt, values), vprops)
+        return ComputerResult(result_graph, Memory(iteration, rt, values), vprops)
 
     def _run_generic(self, p, t0):
         """Vectorised program: Fulgora's superstep loop on the host, messages combined on the
@@ -438,6 +593,8 @@ class GpuGraphComputer(TitanGraphComputer):
                 raise TitanException(L.TGO_E_INVALID, f"weight property '{p.weight_property}' has no key id")
         eng = self.graph.engine_for(scope, wk)
         memory = FulgoraMemory(tuple(p.memory_compute_keys) + tuple(mr.memory_key for mr in self._map_reduces))
+        if self._mode != TitanGraphComputer.ResultMode.NONE:
+            raise TitanException(L.TGO_E_UNSUPPORTED, "write-back of a generic program's compute keys")
         verts = run_generic(eng, p, memory)
         memory.setRuntime((time.perf_counter() - t0) * 1000.0)
         memory.complete()

@@ -52,6 +52,10 @@ struct tgo_ctx {
     int64_t part_relaxed = 0;   // partitioned SSSP: entries relaxed, phases
     int32_t part_phases = 0;
     int64_t pv_max_out = 0, pv_max_in = 0;   // largest OUT / IN list of a vertex cut
+    // last finished program whose compute keys tgo_result_rows can encode (-1 = none)
+    int res_kind = -1;
+    bool res_empty = false;                  // it set no property (PageRank iterations(0))
+    ResultSource res_src;
     int num_cus = 256;          // compute units of the device (persistent launches)
 };
 
@@ -261,8 +265,14 @@ int upload_graph(tgo_ctx* ctx, HostGraph& h, bool allow_segments = true) {
     HIP_TRY(dev_alloc(ctx, s.cnt, 1));
     if (!s.hcnt) {
         void* hp = nullptr;
-        HIP_TRY(hipHostMalloc(&hp, sizeof(Counters), hipHostMallocDefault));
+        // fine-grained: the publish kernel's system-scope stores reach the spinning host
+        HIP_TRY(hipHostMalloc(&hp, sizeof(Counters) + 64, hipHostMallocMapped | hipHostMallocCoherent));
+        std::memset(hp, 0, sizeof(Counters) + 64);
         s.hcnt = static_cast<Counters*>(hp);
+        void* dp = nullptr;
+        HIP_TRY(hipHostGetDevicePointer(&dp, hp, 0));
+        s.hcnt_dev = static_cast<unsigned long long*>(dp);
+        s.pub_seq = 0;
     }
     HIP_TRY(hipDeviceSynchronize());
     ctx->titan_id = h.titan_id;
@@ -327,9 +337,25 @@ int check_program(tgo_ctx* ctx, int scope) {
     return TGO_OK;
 }
 
+// Counters of the work queued so far, without a copy + stream synchronisation: the publish
+// kernel stores them and then a sequence number into host-mapped memory; the host spins on
+// the sequence number (the level loops read a few words per level, so the wake-up latency of
+// a blocking synchronisation dominated short levels).  A stream error ends the spin.
 int read_counters(tgo_ctx* ctx) {
-    HIP_TRY(hipMemcpyAsync(ctx->sc.hcnt, ctx->sc.cnt, sizeof(Counters), hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    Scratch& s = ctx->sc;
+    const unsigned long long seq = ++s.pub_seq;
+    HIP_TRY(k_publish_counters(s.cnt, s.hcnt_dev, seq, ctx->stream));
+    const volatile unsigned long long* flag = reinterpret_cast<volatile unsigned long long*>(s.hcnt) + kCounterWords;
+    for (uint64_t it = 1;; ++it) {
+        if (*flag == seq) break;
+        if ((it & 0x3FFF) == 0) {
+            const hipError_t q = hipStreamQuery(ctx->stream);
+            if (q != hipSuccess && q != hipErrorNotReady) return fail(ctx, TGO_E_HIP, hipGetErrorString(q));
+            if (q == hipSuccess && *flag != seq) return fail(ctx, TGO_E_HIP, "counter publish not visible after the stream drained");
+        }
+        __builtin_ia32_pause();
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
     return TGO_OK;
 }
 
@@ -378,18 +404,17 @@ int run_bfs(tgo_ctx* ctx, int64_t seed, int max_depth, int scope) {
             if (!bottom_up && static_cast<double>(mf) > static_cast<double>(mu) / alpha) bottom_up = true;
             else if (bottom_up && static_cast<double>(qlen) < static_cast<double>(n) / beta) bottom_up = false;
             if (!bottom_up && !queued) {    // after bottom-up levels: queue the frontier bitmap
-                HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
+                HIP_TRY(k_level_prep(s.cnt, nullptr, 0, nullptr, st));
                 HIP_TRY(k_bfs_queue(push, g.n_active, s.fb, s.q[cur], s.qdeg, s.cnt, st));
             }
             queued = !bottom_up;
-            HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
-            HIP_TRY(hipMemsetAsync(s.nb, 0, words * 8, st));
             if (bottom_up) {
+                HIP_TRY(k_level_prep(s.cnt, s.nb, words, nullptr, st));
                 // words past n_active hold only entry-less vertices: nothing to find there
                 HIP_TRY(k_bu_step(pull, push, g.n_active, s.fb, s.vb, s.nb, s.level, s.cnt, L + 1, st));
             } else {
-                int rc = scan_frontier(ctx, qlen);
-                if (rc) return rc;
+                HIP_TRY(k_level_prep(s.cnt, s.nb, words, s.qdeg + qlen, st));
+                HIP_TRY(scan_exclusive_i64(s.cub_tmp, s.cub_bytes, s.qdeg, s.qpre, qlen + 1, st));
                 // qdeg is reused for the next queue's degrees after the scan consumed it
                 HIP_TRY(k_td_expand(push, s.q[cur], s.qpre, qlen, s.level, s.vb, s.nb, s.q[cur ^ 1], s.qdeg, s.cnt, L + 1, st));
             }
@@ -425,10 +450,10 @@ int run_sssp(tgo_ctx* ctx, int64_t seed, int max_depth, int scope, bool weighted
         int64_t qlen = 1;
         int cur = 0;
         for (int L = 0; L < max_depth && qlen > 0; ++L) {
-            HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
-            HIP_TRY(hipMemsetAsync(s.vb, 0, words * 8, st));       // "improved this level" marks
-            int rc = scan_frontier(ctx, qlen);
-            if (rc) return rc;
+            // counters, "improved this level" marks, scan tail
+            HIP_TRY(k_level_prep(s.cnt, s.vb, words, s.qdeg + qlen, st));
+            HIP_TRY(scan_exclusive_i64(s.cub_tmp, s.cub_bytes, s.qdeg, s.qpre, qlen + 1, st));
+            int rc;
             HIP_TRY(k_sssp_relax(push, s.q[cur], s.qpre, qlen, s.msg, s.dist, s.vb, s.q[cur ^ 1], s.qdeg, s.cnt, weighted ? 1 : 0, st));
             rc = read_counters(ctx);
             if (rc) return rc;
@@ -684,6 +709,7 @@ int tgo_decode_edge_entry(const tgo_schema* schema, const tgo_load_opts* opts, c
 
 int tgo_load_rows(tgo_ctx* ctx, const tgo_rows* rows, const tgo_schema* schema, const tgo_load_opts* opts) {
     if (!ctx) return TGO_E_INVALID;
+    ctx->res_kind = -1;
     if (!rows || !schema || !opts) return fail(ctx, TGO_E_INVALID, "null argument");
     if (rows->nrows < 0 || (rows->nrows > 0 && (!rows->row_keys || !rows->row_entry_begin ||
         !rows->row_byte_begin || !rows->entry_bytes || !rows->entry_limit_valpos)))
@@ -717,6 +743,7 @@ int tgo_finish_load(tgo_ctx* ctx) {
 
 int tgo_load_edges(tgo_ctx* ctx, const tgo_edges* edges, const tgo_load_opts* opts) {
     if (!ctx) return TGO_E_INVALID;
+    ctx->res_kind = -1;
     if (!edges || !opts || (edges->m > 0 && (!edges->src || !edges->dst)))
         return fail(ctx, TGO_E_INVALID, "null argument");
     if (opts->scope < 0 || opts->scope > 2) return fail(ctx, TGO_E_INVALID, "invalid scope");
@@ -744,6 +771,7 @@ int tgo_vertex_ids(tgo_ctx* ctx, int64_t* out) {
 
 int tgo_bfs(tgo_ctx* ctx, const tgo_bfs_args* a, int64_t* dist_out) {
     if (!ctx) return TGO_E_INVALID;
+    ctx->res_kind = -1;
     if (!a) return fail(ctx, TGO_E_INVALID, "null args");
     int rc = check_program(ctx, a->scope);
     if (rc) return rc;
@@ -753,11 +781,16 @@ int tgo_bfs(tgo_ctx* ctx, const tgo_bfs_args* a, int64_t* dist_out) {
     if ((rc = resolve_seed(ctx, a->seed, a->seed_is_dense, seed))) return rc;
     HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
     if ((rc = run_bfs(ctx, seed, a->max_depth, a->scope))) return rc;
-    return finish_distance_program(ctx, a->scope, a->flags, dist_out);
+    if ((rc = finish_distance_program(ctx, a->scope, a->flags, dist_out))) return rc;
+    ctx->res_kind = TGO_RESULT_DISTANCE;
+    ctx->res_empty = false;
+    ctx->res_src = ResultSource{ctx->sc.dist, nullptr};
+    return TGO_OK;
 }
 
 int tgo_sssp(tgo_ctx* ctx, const tgo_sssp_args* a, int64_t* dist_out) {
     if (!ctx) return TGO_E_INVALID;
+    ctx->res_kind = -1;
     if (!a) return fail(ctx, TGO_E_INVALID, "null args");
     int rc = check_program(ctx, a->scope);
     if (rc) return rc;
@@ -778,7 +811,11 @@ int tgo_sssp(tgo_ctx* ctx, const tgo_sssp_args* a, int64_t* dist_out) {
     } else {
         if ((rc = run_sssp(ctx, seed, a->max_depth, a->scope, ctx->g.has_weight))) return rc;
     }
-    return finish_distance_program(ctx, a->scope, a->flags, dist_out);
+    if ((rc = finish_distance_program(ctx, a->scope, a->flags, dist_out))) return rc;
+    ctx->res_kind = TGO_RESULT_DISTANCE;
+    ctx->res_empty = false;
+    ctx->res_src = ResultSource{ctx->sc.dist, nullptr};
+    return TGO_OK;
 }
 
 // ------------------------------------------------------------------ multi-source BFS
@@ -813,6 +850,7 @@ static int ms_alloc(tgo_ctx* ctx) {
 
 int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_bfs_args* a, int64_t* dist_out) {
     if (!ctx) return TGO_E_INVALID;
+    ctx->res_kind = -1;
     if (!a || !seeds) return fail(ctx, TGO_E_INVALID, "null args");
     if (nseeds < 1 || nseeds > TGO_MAX_SOURCES) return fail(ctx, TGO_E_INVALID, "nseeds must be in [1, 64]");
     int rc = check_program(ctx, a->scope);
@@ -947,6 +985,7 @@ int tgo_copy_distances(tgo_ctx* ctx, int64_t* dist_out) {
 
 int tgo_pagerank(tgo_ctx* ctx, const tgo_pr_args* a, double* pr_out) {
     if (!ctx) return TGO_E_INVALID;
+    ctx->res_kind = -1;
     if (!a) return fail(ctx, TGO_E_INVALID, "null args");
     if (!ctx->loaded) return fail(ctx, TGO_E_STATE, "no graph loaded");
     if (ctx->g.scope == TGO_SCOPE_BOTH_E)
@@ -1001,11 +1040,15 @@ int tgo_pagerank(tgo_ctx* ctx, const tgo_pr_args* a, double* pr_out) {
         HIP_TRY(hipMemcpyAsync(pr_out, s.msg, n * sizeof(double), hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
     }
+    ctx->res_kind = TGO_RESULT_PAGERANK;
+    ctx->res_empty = a->max_iterations == 0;        // PAGE_RANK / OUTGOING_EDGE_COUNT set at iteration 1
+    ctx->res_src = ResultSource{pr, edge_count};
     return TGO_OK;
 }
 
 int tgo_walkcount(tgo_ctx* ctx, int32_t k, int32_t* out) {
     if (!ctx) return TGO_E_INVALID;
+    ctx->res_kind = -1;
     if (!ctx->loaded) return fail(ctx, TGO_E_STATE, "no graph loaded");
     if (k <= 0) return fail(ctx, TGO_E_INVALID, "DegreeCounter length must be > 0");   // OLAPTest.java:347
     if (ctx->g.scope != TGO_SCOPE_IN_E)
@@ -1034,6 +1077,65 @@ int tgo_walkcount(tgo_ctx* ctx, int32_t k, int32_t* out) {
         HIP_TRY(hipMemcpyAsync(out, s.level, n * sizeof(int32_t), hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
     }
+    ctx->res_kind = TGO_RESULT_DEGREE;
+    ctx->res_empty = false;
+    ctx->res_src = ResultSource{a, nullptr};
+    return TGO_OK;
+}
+
+int tgo_result_rows(tgo_ctx* ctx, const tgo_result_args* a, tgo_result_size* size, const tgo_rows_buf* out) {
+    if (!ctx) return TGO_E_INVALID;
+    if (!a || !size) return fail(ctx, TGO_E_INVALID, "null args");
+    if (a->kind < TGO_RESULT_DISTANCE || a->kind > TGO_RESULT_DEGREE) return fail(ctx, TGO_E_INVALID, "invalid result kind");
+    if (ctx->res_kind != a->kind)
+        return fail(ctx, TGO_E_STATE, "no finished program of that kind is the last one run on this ctx");
+    if (out && (!out->row_keys || !out->row_entry_begin || !out->row_byte_begin || !out->entry_bytes ||
+                !out->entry_limit_valpos))
+        return fail(ctx, TGO_E_INVALID, "incomplete tgo_rows_buf");
+    (void)hipSetDevice(ctx->opts.device);
+    const int64_t n = ctx->g.n;
+    const tgo_result_size want = *size;
+    if (ctx->res_empty) {
+        *size = tgo_result_size{0, 0, 0};
+        if (out) out->row_entry_begin[0] = out->row_byte_begin[0] = 0;
+        return TGO_OK;
+    }
+    int64_t* scratch[4] = {nullptr, nullptr, nullptr, nullptr};
+    auto release = [&] { for (auto* p : scratch) if (p) (void)hipFree(p); };
+    for (auto*& p : scratch)
+        if (hipMalloc(&p, (n + 1) * sizeof(int64_t)) != hipSuccess) { release(); return fail(ctx, TGO_E_OOM, "result scratch"); }
+    ResultRows rr;
+    std::vector<int64_t> row_src;
+    std::string err;
+    int rc = encode_results(ctx->res_src, a, ctx->g.perm, n, scratch, ctx->sc.cub_tmp, ctx->sc.cub_bytes, &rr,
+                            ctx->stream, err);
+    if (!rc && out) {
+        if (want.nrows < rr.nrows || want.nentries < rr.nentries || want.nbytes < rr.nbytes) {
+            release();
+            *size = tgo_result_size{rr.nrows, rr.nentries, rr.nbytes};
+            return fail(ctx, TGO_E_INVALID, "result buffers smaller than the sizes of the first call");
+        }
+        row_src.resize(static_cast<size_t>(std::max<int64_t>(1, rr.nrows)));
+        rr.write = true;
+        rr.row_src = row_src.data();
+        rr.row_entry_begin = out->row_entry_begin;
+        rr.row_byte_begin = out->row_byte_begin;
+        rr.entry_bytes = out->entry_bytes;
+        rr.entry_limit_valpos = out->entry_limit_valpos;
+        rc = encode_results(ctx->res_src, a, ctx->g.perm, n, scratch, ctx->sc.cub_tmp, ctx->sc.cub_bytes, &rr,
+                            ctx->stream, err);
+        // row keys: IDManager.getKey of each vertex id (IDManager.java:461-473)
+        const int pb = ctx->opts.partition_bits;
+        for (int64_t i = 0; !rc && i < rr.nrows; ++i) {
+            const uint64_t vid = static_cast<uint64_t>(ctx->titan_id[static_cast<size_t>(row_src[i])]);
+            const uint64_t part = pb ? (vid >> 3) & ((1ULL << pb) - 1) : 0;
+            const uint64_t count = vid >> (3 + pb);
+            out->row_keys[i] = static_cast<int64_t>((pb ? part << (64 - pb) : 0) | (count << 3) | (vid & 7));
+        }
+    }
+    release();
+    if (rc) return fail(ctx, rc, err);
+    *size = tgo_result_size{rr.nrows, rr.nentries, rr.nbytes};
     return TGO_OK;
 }
 
@@ -1802,6 +1904,7 @@ static int generic_alloc(tgo_ctx* ctx) {
 int tgo_gather(tgo_ctx* ctx, const tgo_gather_args* a, const void* msg, const uint8_t* has, void* out,
                uint8_t* out_has) {
     if (!ctx) return TGO_E_INVALID;
+    ctx->res_kind = -1;
     if (!a || !msg || !out || !out_has) return fail(ctx, TGO_E_INVALID, "null argument");
     if (!ctx->loaded) return fail(ctx, TGO_E_STATE, "no graph loaded");
     if (ctx->g.partitioned) return fail(ctx, TGO_E_UNSUPPORTED, "generic gathers run on a one-GPU load");
@@ -1841,6 +1944,7 @@ int tgo_gather(tgo_ctx* ctx, const tgo_gather_args* a, const void* msg, const ui
 int tgo_combine_global(tgo_ctx* ctx, int32_t value_type, int32_t combiner, int64_t nmsgs, const int64_t* targets,
                        const void* values, void* out, uint8_t* out_has) {
     if (!ctx) return TGO_E_INVALID;
+    ctx->res_kind = -1;
     if (nmsgs < 0 || (nmsgs > 0 && (!targets || !values)) || !out || !out_has) return fail(ctx, TGO_E_INVALID, "null argument");
     if (!ctx->loaded) return fail(ctx, TGO_E_STATE, "no graph loaded");
     if (value_type < 0 || value_type > 1 || combiner < 0 || combiner > 2)

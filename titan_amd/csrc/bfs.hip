@@ -339,6 +339,31 @@ hipError_t k_bfs_queue(const View& push, int64_t n, const uint64_t* fb, int32_t*
     bfs_queue<<<extract_grid((n + 63) / 64), kBlock, 0, s>>>(push, n, fb, qn, qdeg, cnt);
     return hipGetLastError();
 }
+__global__ void publish_counters(const Counters* c, unsigned long long* host, unsigned long long seq) {
+    const int i = threadIdx.x;
+    const unsigned long long* w = reinterpret_cast<const unsigned long long*>(c);
+    if (i < kCounterWords) {
+        __hip_atomic_store(&host[i], w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __threadfence_system();
+    }
+    __syncthreads();
+    if (i == 0) __hip_atomic_store(&host[kCounterWords], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__global__ void level_prep(Counters* cnt, uint64_t* nb, int64_t words, int64_t* tail) {
+    const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i < words) nb[i] = 0;
+    if (cnt && i < kCounterWords) reinterpret_cast<unsigned long long*>(cnt)[i] = 0;
+    if (tail && i == 0) *tail = 0;
+}
+hipError_t k_publish_counters(const Counters* c, unsigned long long* host, unsigned long long seq, hipStream_t s) {
+    publish_counters<<<1, 64, 0, s>>>(c, host, seq);
+    return hipGetLastError();
+}
+hipError_t k_level_prep(Counters* cnt, uint64_t* nb, int64_t words, int64_t* tail, hipStream_t s) {
+    const int64_t n = std::max<int64_t>(words, kCounterWords);
+    level_prep<<<grid_for(n), kBlock, 0, s>>>(cnt, nb, words, tail);
+    return hipGetLastError();
+}
 hipError_t k_publish_counts(const Counters* c, int64_t* out, int64_t* slot, hipStream_t s) {
     publish_counts<<<1, 64, 0, s>>>(c, out, slot);
     return hipGetLastError();

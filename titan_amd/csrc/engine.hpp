@@ -59,6 +59,21 @@ struct RowStaging {
     std::vector<int64_t> labels;
 };
 
+// Result write-back (results.hip): device arrays of the last finished program.
+struct ResultSource { const void* v0 = nullptr; const void* v1 = nullptr; };
+struct ResultRows {
+    int64_t nrows = 0, nentries = 0, nbytes = 0;
+    bool write = false;
+    int64_t* row_src = nullptr;              // API row index of every output row
+    int64_t* row_entry_begin = nullptr;
+    int64_t* row_byte_begin = nullptr;
+    uint8_t* entry_bytes = nullptr;
+    int64_t* entry_limit_valpos = nullptr;
+};
+int encode_results(const ResultSource& src, const tgo_result_args* a, const int32_t* perm, int64_t n,
+                   int64_t* const scratch[4], void*& cub_tmp, size_t& cub_bytes, ResultRows* out, hipStream_t st,
+                   std::string& err);
+
 // Weight value marking an edge whose weight property is absent: traversing it makes the
 // reference throw inside execute() (edge.value() on a missing key), i.e. TGO_E_PROGRAM.
 constexpr int32_t kMissingWeight = INT32_MIN;
@@ -229,7 +244,9 @@ struct Scratch {
     void* cub_tmp = nullptr;
     size_t cub_bytes = 0;
     Counters* cnt = nullptr;        // device
-    Counters* hcnt = nullptr;       // pinned host mirror
+    Counters* hcnt = nullptr;       // host mirror: fine-grained (coherent) pinned memory, mapped
+    unsigned long long* hcnt_dev = nullptr;   // its device address; word kCounterWords = seq
+    unsigned long long pub_seq = 0; // last published sequence number
     // multi-source BFS (allocated on first use)
     uint64_t* ms_vis = nullptr;     // n: reached-by mask
     uint64_t* ms_fr = nullptr;      // n: frontier mask
@@ -273,6 +290,13 @@ hipError_t k_bfs_queue(const View& push, int64_t n, const uint64_t* fb, int32_t*
                        hipStream_t s);
 hipError_t k_level_to_dist(const int32_t* level, int64_t* dist, int64_t n, hipStream_t s);
 hipError_t k_publish_counts(const Counters* c, int64_t* out, int64_t* slot, hipStream_t s);
+// Level control without a copy + stream synchronisation: one wave stores the counters into the
+// host-mapped mirror, then the sequence number after them (system scope); the host spins on it.
+constexpr int kCounterWords = static_cast<int>(sizeof(Counters) / 8);
+hipError_t k_publish_counters(const Counters* c, unsigned long long* host, unsigned long long seq, hipStream_t s);
+// One launch instead of per-level memsets: zero the counters (cnt may be null), the next
+// frontier bitmap (words, may be 0) and the scan tail slot (may be null).
+hipError_t k_level_prep(Counters* cnt, uint64_t* nb, int64_t words, int64_t* tail, hipStream_t s);
 hipError_t k_reach_stats(const View& both_or_pull, const int64_t* dist, int64_t n,
                          unsigned long long* out2, hipStream_t s);
 hipError_t k_degree_i64(const View& v, const int32_t* q, int64_t qlen, int64_t* qdeg, hipStream_t s);

@@ -195,6 +195,24 @@ class Engine:
         _check(self.lib, self.ctx, self.lib.tgo_walkcount(self.ctx, int(k), L.ptr(out, C.c_int32)))
         return out
 
+    def result_rows(self, kind, key_ids, datatypes, relation_id_base):
+        """Edgestore entries of the last program's compute keys (tgo_result_rows): the rows
+        ResultMode PERSIST writes back (FulgoraGraphComputer.java:248-305)."""
+        k = list(key_ids) + [0] * (2 - len(key_ids))
+        d = list(datatypes) + [0] * (2 - len(datatypes))
+        a = L.ResultArgs(kind, 0, (C.c_int64 * 2)(*k), (C.c_int32 * 2)(*d), int(relation_id_base))
+        sz = L.ResultSize()
+        _check(self.lib, self.ctx, self.lib.tgo_result_rows(self.ctx, C.byref(a), C.byref(sz), None))
+        keys = np.empty(max(sz.nrows, 1), np.int64)
+        eb = np.empty(sz.nrows + 1, np.int64)
+        bb = np.empty(sz.nrows + 1, np.int64)
+        data = np.empty(max(sz.nbytes, 1), np.uint8)
+        lv = np.empty(max(sz.nentries, 1), np.int64)
+        buf = L.RowsBuf(L.ptr(keys, C.c_int64), L.ptr(eb, C.c_int64), L.ptr(bb, C.c_int64), L.ptr(data, C.c_uint8),
+                        L.ptr(lv, C.c_int64))
+        _check(self.lib, self.ctx, self.lib.tgo_result_rows(self.ctx, C.byref(a), C.byref(sz), C.byref(buf)))
+        return Rows(keys[:sz.nrows], eb, bb, data[:sz.nbytes], lv[:sz.nentries])
+
     # ------------------------------------------------------------------ generic vertex programs
     @staticmethod
     def _vals(values, value_type):
