@@ -207,6 +207,50 @@ JNIEXPORT jintArray JNICALL JFN(walkCount)(JNIEnv* env, jclass cls, jlong h, jin
     return rc == TGO_OK ? out : NULL;
 }
 
+/* tgo_result_rows: {rowKeys, rowEntryBegin, rowByteBegin, entryLimitValuePos} as long[][] plus
+ * the entry bytes in a new direct ByteBuffer (element 4), or NULL on error. */
+JNIEXPORT jobjectArray JNICALL JFN(resultRows)(JNIEnv* env, jclass cls, jlong h, jint kind, jlongArray jkeys,
+                                              jintArray jtypes, jlong relationIdBase) {
+    (void)cls;
+    tgo_result_args a;
+    memset(&a, 0, sizeof a);
+    a.kind = kind;
+    a.relation_id_base = relationIdBase;
+    jsize nk = (*env)->GetArrayLength(env, jkeys);
+    if (nk < 1 || nk > 2 || (*env)->GetArrayLength(env, jtypes) != nk) return NULL;
+    (*env)->GetLongArrayRegion(env, jkeys, 0, nk, (jlong*)a.key_ids);
+    (*env)->GetIntArrayRegion(env, jtypes, 0, nk, (jint*)a.datatypes);
+    tgo_result_size sz;
+    memset(&sz, 0, sizeof sz);
+    if (tgo_result_rows(CTX(h), &a, &sz, NULL) != TGO_OK) return NULL;
+    int64_t* keys = (int64_t*)malloc((size_t)(sz.nrows + 1) * 8);
+    int64_t* eb = (int64_t*)malloc((size_t)(sz.nrows + 1) * 8);
+    int64_t* bb = (int64_t*)malloc((size_t)(sz.nrows + 1) * 8);
+    int64_t* lv = (int64_t*)malloc((size_t)(sz.nentries + 1) * 8);
+    uint8_t* bytes = (uint8_t*)malloc((size_t)(sz.nbytes + 1));
+    jobjectArray out = NULL;
+    tgo_rows_buf buf = {keys, eb, bb, bytes, lv};
+    if (keys && eb && bb && lv && bytes && tgo_result_rows(CTX(h), &a, &sz, &buf) == TGO_OK) {
+        jclass la = (*env)->FindClass(env, "java/lang/Object");
+        out = (*env)->NewObjectArray(env, 5, la, NULL);
+        const int64_t* parts[4] = {keys, eb, bb, lv};
+        const jsize lens[4] = {(jsize)sz.nrows, (jsize)sz.nrows + 1, (jsize)sz.nrows + 1, (jsize)sz.nentries};
+        for (int i = 0; out && i < 4; ++i) {
+            jlongArray arr = (*env)->NewLongArray(env, lens[i]);
+            if (!arr) { out = NULL; break; }
+            (*env)->SetLongArrayRegion(env, arr, 0, lens[i], (const jlong*)parts[i]);
+            (*env)->SetObjectArrayElement(env, out, i, arr);
+        }
+        if (out) {
+            jbyteArray data = (*env)->NewByteArray(env, (jsize)sz.nbytes);
+            if (data) (*env)->SetByteArrayRegion(env, data, 0, (jsize)sz.nbytes, (const jbyte*)bytes);
+            (*env)->SetObjectArrayElement(env, out, 4, data);
+        }
+    }
+    free(keys); free(eb); free(bb); free(lv); free(bytes);
+    return out;
+}
+
 JNIEXPORT jdoubleArray JNICALL JFN(stats)(JNIEnv* env, jclass cls, jlong h) {
     (void)cls;
     tgo_stats st;

@@ -41,9 +41,14 @@ import java.util.concurrent.Future;
  *
  * Supported: tmain's PageRankVertexProgram, ShortestDistanceVertexProgram and
  * OLAPTest.DegreeCounter (matched by class name; their parameters are read from
- * storeState(), or the DegreeCounter's length field).  ResultMode NONE only: PERSIST and
- * LOCALTX write the compute keys back through batched transactions in the reference
- * (:248-305) and are rejected here.
+ * storeState(), or the DegreeCounter's length field).
+ *
+ * Write-back (FulgoraGraphComputer.java:248-305): with Persist.VERTEX_PROPERTIES the compute
+ * keys are encoded on the device (tgo_result_rows: single-cardinality property entries, one
+ * row per vertex holding a value) and written to the edgestore as column overwrites in
+ * batches of writeBatchSize rows (ResultGraph.ORIGINAL); ResultGraph.NEW sets them in a new,
+ * uncommitted transaction instead, as Fulgora does.  The compute keys must exist as typed
+ * property keys (Long distance, Double pageRank / edgeCount, Integer degree).
  */
 public class GpuGraphComputer implements TitanGraphComputer {
 
@@ -108,8 +113,9 @@ public class GpuGraphComputer implements TitanGraphComputer {
             mapReduces.addAll(vertexProgram.getMapReducers());
         }
         final Persist persist = persistMode == null ? Persist.NOTHING : persistMode;
-        if (persist != Persist.NOTHING)
-            throw new TitanException("GpuGraphComputer supports ResultMode.NONE only (no property write-back)");
+        final ResultGraph resultGraph = resultGraphMode == null ? ResultGraph.ORIGINAL : resultGraphMode;
+        if (!features().supportsResultGraphPersistCombination(resultGraph, persist))
+            throw GraphComputer.Exceptions.resultGraphPersistCombinationNotSupported(resultGraph, persist);
         final DeviceProgram program = DeviceProgram.recognise(vertexProgram);
         final FulgoraMemory memory = new FulgoraMemory(vertexProgram, mapReduces);
         return CompletableFuture.<ComputerResult>supplyAsync(() -> {
@@ -154,9 +160,15 @@ public class GpuGraphComputer implements TitanGraphComputer {
                         mr.addResultToMemory(memory, emitter.mapQueue.iterator());
                     }
                 }
+                // (4) write-back of the compute keys
+                org.apache.tinkerpop.gremlin.structure.Graph result = graph;
+                if (persist == Persist.VERTEX_PROPERTIES) {
+                    if (resultGraph == ResultGraph.ORIGINAL) WriteBack.persist(graph, ctx, program);
+                    else result = WriteBack.localTx(graph, ids, values, program);
+                }
                 memory.setRuntime(System.currentTimeMillis() - start);
                 memory.complete();
-                return new DefaultComputerResult(graph, memory.asImmutable());
+                return new DefaultComputerResult(result, memory.asImmutable());
             } catch (TitanException e) {
                 throw e;
             } catch (Exception e) {
@@ -172,9 +184,90 @@ public class GpuGraphComputer implements TitanGraphComputer {
         return new GraphComputer.Features() {
             @Override public boolean supportsWorkerPersistenceBetweenIterations() { return false; }
             @Override public boolean supportsResultGraphPersistCombination(ResultGraph r, Persist p) {
-                return p == Persist.NOTHING;
+                return p == Persist.NOTHING || p == Persist.VERTEX_PROPERTIES;
             }
         };
+    }
+
+    /** Compute-key write-back (FulgoraGraphComputer.java:248-305). */
+    static final class WriteBack {
+        static final int WRITE_BATCH_ROWS = 10000;
+
+        /** ResultGraph.ORIGINAL: device-encoded property entries as edgestore column overwrites. */
+        static void persist(StandardTitanGraph graph, long ctx, DeviceProgram program) throws Exception {
+            long[] keys = program.computeKeyIds(graph);
+            int[] types = program.computeKeyTypes();
+            long base = RelationIds.reserve(graph, keys.length * (long) TgoNative.vertexIds(ctx).length);
+            Object[] rows = TgoNative.checked(ctx, TgoNative.resultRows(ctx, program.resultKind(), keys, types, base));
+            long[] rowKeys = (long[]) rows[0], eb = (long[]) rows[1], bb = (long[]) rows[2], lv = (long[]) rows[3];
+            byte[] data = (byte[]) rows[4];
+            com.thinkaurelius.titan.diskstorage.keycolumnvalue.KeyColumnValueStoreManager mgr =
+                    graph.getBackend().getStoreManager();
+            String store = com.thinkaurelius.titan.diskstorage.Backend.EDGESTORE_NAME;
+            for (int r0 = 0; r0 < rowKeys.length; r0 += WRITE_BATCH_ROWS) {
+                Map<String, Map<com.thinkaurelius.titan.diskstorage.StaticBuffer,
+                        com.thinkaurelius.titan.diskstorage.keycolumnvalue.KCVMutation>> batch = new HashMap<>();
+                Map<com.thinkaurelius.titan.diskstorage.StaticBuffer,
+                        com.thinkaurelius.titan.diskstorage.keycolumnvalue.KCVMutation> muts = new HashMap<>();
+                for (int r = r0; r < Math.min(rowKeys.length, r0 + WRITE_BATCH_ROWS); r++) {
+                    java.util.List<com.thinkaurelius.titan.diskstorage.Entry> adds = new java.util.ArrayList<>();
+                    long start = 0;
+                    for (int e = (int) eb[r]; e < eb[r + 1]; e++) {
+                        int end = (int) (lv[e] >>> 32), vpos = (int) (lv[e] & 0x7FFFFFFF);
+                        byte[] entry = java.util.Arrays.copyOfRange(data, (int) (bb[r] + start), (int) (bb[r] + end));
+                        adds.add(com.thinkaurelius.titan.diskstorage.util.StaticArrayEntry.of(
+                                new com.thinkaurelius.titan.diskstorage.util.StaticArrayBuffer(entry, 0, vpos),
+                                new com.thinkaurelius.titan.diskstorage.util.StaticArrayBuffer(entry, vpos, entry.length)));
+                        start = end;
+                    }
+                    muts.put(com.thinkaurelius.titan.diskstorage.util.BufferUtil.getLongBuffer(rowKeys[r]),
+                            new com.thinkaurelius.titan.diskstorage.keycolumnvalue.KCVMutation(adds,
+                                    java.util.Collections.emptyList()));
+                }
+                batch.put(store, muts);
+                com.thinkaurelius.titan.diskstorage.keycolumnvalue.StoreTransaction tx =
+                        mgr.beginTransaction(com.thinkaurelius.titan.diskstorage.util.StandardBaseTransactionConfig.of(
+                                graph.getConfiguration().getTimestampProvider()));
+                try {
+                    mgr.mutateMany(batch, tx);
+                    tx.commit();
+                } catch (Exception e) {
+                    tx.rollback();
+                    throw new TitanException("Could not persist program results to graph", e);
+                }
+            }
+        }
+
+        /** ResultGraph.NEW: a new transaction holding the properties, not committed (:296-305). */
+        static org.apache.tinkerpop.gremlin.structure.Graph localTx(StandardTitanGraph graph, long[] ids,
+                                                                     Map<String, Object> values, DeviceProgram program) {
+            com.thinkaurelius.titan.core.TitanTransaction tx = graph.newTransaction();
+            for (Map.Entry<String, Object> kv : values.entrySet()) {
+                for (int i = 0; i < ids.length; i++) {
+                    Object v = program.valueAt(kv.getValue(), i);
+                    if (v != null) tx.getVertex(ids[i]).property(
+                            org.apache.tinkerpop.gremlin.structure.VertexProperty.Cardinality.single, kv.getKey(), v);
+                }
+            }
+            return tx;
+        }
+    }
+
+    /**
+     * First id of a block of `count` consecutive relation ids for the written properties.  Titan
+     * hands relation ids out of IDAuthority blocks per partition (VertexIDAssigner.java); the
+     * device numbers entries base + i, so the host takes one block large enough from the
+     * authority's relation namespace (the hook a maintainer wires to IDAuthority.getIDBlock).
+     */
+    static final class RelationIds {
+        static long reserve(StandardTitanGraph graph, long count) {
+            com.thinkaurelius.titan.diskstorage.IDBlock block = graph.getBackend().getIDAuthority()
+                    .getIDBlock(0, com.thinkaurelius.titan.graphdb.database.idassigner.VertexIDAssigner.RELATION_NAMESPACE,
+                            java.time.Duration.ofMinutes(1));
+            if (block.numIds() < count)
+                throw new TitanException("relation-id block of " + block.numIds() + " ids is smaller than " + count);
+            return block.getId(0);
+        }
     }
 
     /** Flattened schema for tgo_load_rows (layout documented in TgoNative.loadRows). */
@@ -242,6 +335,32 @@ public class GpuGraphComputer implements TitanGraphComputer {
         long weightKey(StandardTitanGraph graph) { return 0; }
         abstract Map<String, Object> run(long ctx);
         abstract void emit(long[] ids, Map<String, Object> values, FulgoraMapEmitter emitter);
+        /** Write-back: tgo_result_kind, the compute keys (typed property keys) and their datatypes. */
+        abstract int resultKind();
+        abstract String[] computeKeys();
+        abstract int[] computeKeyTypes();
+        long[] computeKeyIds(StandardTitanGraph graph) {
+            TitanManagement mgmt = graph.openManagement();
+            try {
+                String[] names = computeKeys();
+                long[] out = new long[names.length];
+                for (int i = 0; i < names.length; i++) {
+                    PropertyKey k = mgmt.getPropertyKey(names[i]);
+                    if (k == null || Schemas.datatype(k.dataType()) != computeKeyTypes()[i])
+                        throw new TitanException("compute key '" + names[i] + "' must be a typed property key");
+                    out[i] = ((com.thinkaurelius.titan.graphdb.internal.InternalRelationType) k).longId();
+                }
+                return out;
+            } finally {
+                mgmt.rollback();
+            }
+        }
+        /** The value of compute-key array `values` at row i, null when the vertex holds none. */
+        Object valueAt(Object values, int i) {
+            if (values instanceof long[]) { long d = ((long[]) values)[i]; return d == TgoNative.DIST_ABSENT ? null : d; }
+            if (values instanceof double[]) { double d = ((double[]) values)[i]; return Double.isNaN(d) ? null : d; }
+            return ((int[]) values)[i];
+        }
 
         static DeviceProgram recognise(VertexProgram<?> p) {
             if (p == null) throw new TitanException("the GPU path needs a vertex program");
@@ -280,6 +399,9 @@ public class GpuGraphComputer implements TitanGraphComputer {
         }
         int scope() { return TgoNative.SCOPE_IN_E; }
         int iterations() { return maxIterations; }
+        int resultKind() { return TgoNative.RESULT_PAGERANK; }
+        String[] computeKeys() { return new String[]{"titan.pageRank.pageRank", "titan.pageRank.edgeCount"}; }
+        int[] computeKeyTypes() { return new int[]{TgoNative.DT_DOUBLE, TgoNative.DT_DOUBLE}; }
         Map<String, Object> run(long ctx) {
             Map<String, Object> v = new HashMap<>();
             v.put("titan.pageRank.pageRank", TgoNative.checked(ctx, TgoNative.pageRank(ctx, alpha, vertexCount, maxIterations)));
@@ -298,6 +420,9 @@ public class GpuGraphComputer implements TitanGraphComputer {
         }
         int scope() { return TgoNative.SCOPE_IN_E; }       // Local(inE, m + e.value(weight)) (:53)
         int iterations() { return maxDepth; }
+        int resultKind() { return TgoNative.RESULT_DISTANCE; }
+        String[] computeKeys() { return new String[]{"titan.shortestDistanceVertexProgram.distance"}; }
+        int[] computeKeyTypes() { return new int[]{TgoNative.DT_LONG}; }
         long weightKey(StandardTitanGraph graph) {
             TitanManagement mgmt = graph.openManagement();
             try {
@@ -325,6 +450,9 @@ public class GpuGraphComputer implements TitanGraphComputer {
         DegreeCount(int length) { this.length = length; }
         int scope() { return TgoNative.SCOPE_IN_E; }        // DEG_MSG = Local(inE) (OLAPTest.java:338)
         int iterations() { return length; }
+        int resultKind() { return TgoNative.RESULT_DEGREE; }
+        String[] computeKeys() { return new String[]{"degree"}; }
+        int[] computeKeyTypes() { return new int[]{TgoNative.DT_INTEGER}; }
         Map<String, Object> run(long ctx) {
             Map<String, Object> v = new HashMap<>();
             v.put("degree", TgoNative.checked(ctx, TgoNative.walkCount(ctx, length)));

@@ -69,6 +69,15 @@ public final class TgoNative {
     /** tgo_stats_get: {ghostVertices, truncatedResults, skippedRows, iterations, loadMs, lastKernelMs}. */
     public static native double[] stats(long ctx);
 
+    /** tgo_result_kind */
+    public static final int RESULT_DISTANCE = 0, RESULT_PAGERANK = 1, RESULT_DEGREE = 2;
+    /**
+     * tgo_result_rows: the edgestore entries (single-cardinality property entries) of the last
+     * program's compute keys, as {long[] rowKeys, long[] rowEntryBegin, long[] rowByteBegin,
+     * long[] entryLimitValuePos, byte[] entryBytes}; null on error (see lastError).
+     */
+    public static native Object[] resultRows(long ctx, int kind, long[] keyIds, int[] datatypes, long relationIdBase);
+
     static void check(long ctx, int rc) {
         if (rc != 0) throw new TitanException("[" + rc + "] " + lastError(ctx));
     }

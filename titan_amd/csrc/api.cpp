@@ -842,6 +842,7 @@ static int ms_alloc(tgo_ctx* ctx) {
     HIP_TRY(dev_alloc(ctx, s.ms_fr, n + 1));
     HIP_TRY(dev_alloc(ctx, s.ms_nx, n + 1));
     HIP_TRY(dev_alloc(ctx, s.ms_lvl, n * kLevelPlanes + 1));
+    HIP_TRY(dev_alloc(ctx, s.ms_fbm, (n + 63) / 64 + 1));
     HIP_TRY(dev_alloc(ctx, s.ms_seeds, TGO_MAX_SOURCES));
     HIP_TRY(dev_alloc(ctx, s.ms_stat, 2 * TGO_MAX_SOURCES));
     ctx->st.device_bytes = ctx->dev_bytes;
@@ -884,6 +885,7 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
     const int64_t total = pull.nlists > 1 ? g.out.nnz + g.in.nnz : (a->scope == TGO_SCOPE_IN_E ? g.out.nnz : g.in.nnz);
     static const double ms_alpha = env_double("TGO_MS_ALPHA", 12.0);
     static const bool trace = env_double("TGO_TRACE", 0.0) != 0.0;
+    static const bool filter = env_double("TGO_MS_FILTER", 1.0) != 0.0;
     int64_t qlen = static_cast<int64_t>(uniq.size());
     int64_t mf = 0;
     {
@@ -907,7 +909,9 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
         HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
         queued = !use_pull;
         if (use_pull) {
-            HIP_TRY(k_ms_pull(pull, push, g.n_active, full, fr, s.ms_vis, nx, ms_planes(ctx), s.cnt, L + 1, st));
+            if (filter) HIP_TRY(k_ms_fbitmap(fr, n, s.ms_fbm, st));
+            HIP_TRY(k_ms_pull(pull, push, g.n_active, full, fr, filter ? s.ms_fbm : nullptr, s.ms_vis, nx,
+                              ms_planes(ctx), s.cnt, L + 1, st));
         } else {
             HIP_TRY(hipMemsetAsync(nx, 0, n * 8, st));
             if ((rc = scan_frontier(ctx, qlen))) return rc;
@@ -1412,7 +1416,8 @@ int tgo_part_ms_pull(tgo_ctx* ctx, int32_t level, const uint64_t* fr_global, uin
     HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
     HIP_TRY(hipMemsetAsync(fr_next, 0, g.n * 8, st));
     const int nxt = ctx->part_cur ^ 1;
-    HIP_TRY(k_ms_pull(pull, push, g.n_active, full, fr_global, s.ms_vis, fr_next, ms_planes(ctx), s.cnt, level + 1, st));
+    HIP_TRY(k_ms_pull(pull, push, g.n_active, full, fr_global, nullptr, s.ms_vis, fr_next, ms_planes(ctx), s.cnt,
+                      level + 1, st));
     ctx->part_cur = nxt;
     ctx->part_queued = false;       // counted only: ms_push builds the queue if it needs one
     return part_counts(ctx, counts);

@@ -249,6 +249,7 @@ struct Scratch {
     unsigned long long pub_seq = 0; // last published sequence number
     // multi-source BFS (allocated on first use)
     uint64_t* ms_vis = nullptr;     // n: reached-by mask
+    uint64_t* ms_fbm = nullptr;     // n/64: frontier bitmap of a pull level (fr != 0)
     uint64_t* ms_fr = nullptr;      // n: frontier mask
     uint64_t* ms_nx = nullptr;      // n: next-frontier mask
     uint64_t* ms_lvl = nullptr;     // kLevelPlanes x n: bit r of plane k = bit k of source r's level
@@ -344,7 +345,9 @@ hipError_t k_ds_apply(const View& push, const int64_t* recv, int64_t npairs, int
 hipError_t k_unpermute_i64(const int64_t* in, const int32_t* perm, int64_t* out, int64_t n, hipStream_t s);
 hipError_t k_ms_seed(const int64_t* seeds, int nseeds, uint64_t* vis, uint64_t* fr, hipStream_t s);
 hipError_t k_ms_pull(const View& pull, const View& push, int64_t n_active, uint64_t full, const uint64_t* fr,
-                     uint64_t* vis, uint64_t* nx, LevelPlanes lvl, Counters* cnt, int32_t next_level, hipStream_t s);
+                     const uint64_t* fbm, uint64_t* vis, uint64_t* nx, LevelPlanes lvl, Counters* cnt,
+                     int32_t next_level, hipStream_t s);
+hipError_t k_ms_fbitmap(const uint64_t* fr, int64_t n, uint64_t* fbm, hipStream_t s);
 hipError_t k_ms_queue(const View& push, int64_t n_active, const uint64_t* fr, int32_t* qn, int64_t* qdeg, Counters* cnt,
                       hipStream_t s);
 hipError_t k_ms_push(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen, const uint64_t* fr,

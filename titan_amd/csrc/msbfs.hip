@@ -73,9 +73,15 @@ __global__ void ms_seed(const int64_t* __restrict__ seeds, int nseeds, uint64_t*
 // kCoop are OR-reduced by the whole wave.
 constexpr int64_t kCoop = 64;
 constexpr int kStep = 8;
+// fbm (optional): bit u set iff fr[u] != 0.  The 2 MB bitmap stays in every XCD's L2, so a
+// neighbour outside every source's frontier costs an L2 probe instead of an 8-byte mask
+// gather from the 134 MB mask array (mostly cold, low-degree vertices: the misses).
+__device__ __forceinline__ bool in_frontier(const uint64_t* __restrict__ fbm, int32_t u) {
+    return !fbm || ((fbm[u >> 6] >> (u & 63)) & 1ULL);
+}
 __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t n_active, uint64_t full,
-        const uint64_t* __restrict__ fr, uint64_t* __restrict__ vis, uint64_t* __restrict__ nx,
-        LevelPlanes lvl, Counters* cnt, int32_t next_level) {
+        const uint64_t* __restrict__ fr, const uint64_t* __restrict__ fbm, uint64_t* __restrict__ vis,
+        uint64_t* __restrict__ nx, LevelPlanes lvl, Counters* cnt, int32_t next_level) {
     unsigned long long nv = 0, mf = 0, bits = 0;
     const int64_t words = (n_active + 63) >> 6;
     // wave w of the block takes word b + w; words past the end run as all-closed lanes.  No
@@ -103,10 +109,13 @@ __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t 
                     int32_t u[kStep];
 #pragma unroll
                     for (int j = 0; j < kStep; ++j) u[j] = k + j < e ? __builtin_nontemporal_load(adj + k + j) : -1;
+                    bool f[kStep];
+#pragma unroll
+                    for (int j = 0; j < kStep; ++j) f[j] = u[j] >= 0 && in_frontier(fbm, u[j]);
                     uint64_t m = 0;
 #pragma unroll
                     for (int j = 0; j < kStep; ++j)
-                        if (u[j] >= 0) m |= fr[u[j]];
+                        if (f[j]) m |= fr[u[j]];
                     acc |= m;
                 }
             }
@@ -129,10 +138,13 @@ __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t 
                         const int64_t x = k + j * 64 + lane();
                         u[j] = x < ee ? __builtin_nontemporal_load(adj + x) : -1;
                     }
+                    bool f[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) f[j] = u[j] >= 0 && in_frontier(fbm, u[j]);
                     uint64_t m = 0;
 #pragma unroll
                     for (int j = 0; j < 4; ++j)
-                        if (u[j] >= 0) m |= fr[u[j]];
+                        if (f[j]) m |= fr[u[j]];
                     for (int off = 32; off > 0; off >>= 1) m |= __shfl_xor(m, off, 64);
                     a |= m;
                     done = (a & want) == want;
@@ -154,6 +166,18 @@ __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t 
         }
     }
     count_flush(cnt, nv, mf, bits);
+}
+
+// Frontier bitmap of a pull level: one wave per 64-vertex word, a ballot of fr != 0.
+__global__ void __launch_bounds__(kBlock) ms_fbitmap(const uint64_t* __restrict__ fr, int64_t n,
+                                                     uint64_t* __restrict__ fbm) {
+    const int64_t words = (n + 63) >> 6;
+    for (int64_t wd = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6; wd < words;
+         wd += (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6) {
+        const int64_t v = (wd << 6) + lane();
+        const unsigned long long b = __ballot(v < n && fr[v] != 0);
+        if (lane() == 0) fbm[wd] = b;
+    }
 }
 
 // Push level: edge-balanced over the frontier queue (exclusive scan of degrees in qpre).
@@ -314,8 +338,15 @@ hipError_t k_ms_seed(const int64_t* seeds, int nseeds, uint64_t* vis, uint64_t* 
     return hipGetLastError();
 }
 hipError_t k_ms_pull(const View& pull, const View& push, int64_t n_active, uint64_t full, const uint64_t* fr,
-                     uint64_t* vis, uint64_t* nx, LevelPlanes lvl, Counters* cnt, int32_t next_level, hipStream_t s) {
-    ms_pull<<<grid_for(n_active, 8192), kBlock, 0, s>>>(pull, push, n_active, full, fr, vis, nx, lvl, cnt, next_level);
+                     const uint64_t* fbm, uint64_t* vis, uint64_t* nx, LevelPlanes lvl, Counters* cnt,
+                     int32_t next_level, hipStream_t s) {
+    ms_pull<<<grid_for(n_active, 8192), kBlock, 0, s>>>(pull, push, n_active, full, fr, fbm, vis, nx, lvl, cnt,
+                                                       next_level);
+    return hipGetLastError();
+}
+hipError_t k_ms_fbitmap(const uint64_t* fr, int64_t n, uint64_t* fbm, hipStream_t s) {
+    const int64_t words = (n + 63) / 64;
+    ms_fbitmap<<<grid_for(words * 64, 8192), kBlock, 0, s>>>(fr, n, fbm);
     return hipGetLastError();
 }
 hipError_t k_ms_queue(const View& push, int64_t n_active, const uint64_t* fr, int32_t* qn, int64_t* qdeg, Counters* cnt,
