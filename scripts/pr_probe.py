@@ -59,3 +59,5 @@ for v in variants:
            "bitwise_equal_default": bool(np.array_equal(pr, base)), "l1_vs_default": float(np.abs(pr - base).sum())}
     out.append(rec)
     print(json.dumps(rec), flush=True)
+if os.environ.get("PR_PROBE_SAVE"):
+    np.save(os.environ["PR_PROBE_SAVE"], base)

@@ -885,7 +885,10 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
     const int64_t total = pull.nlists > 1 ? g.out.nnz + g.in.nnz : (a->scope == TGO_SCOPE_IN_E ? g.out.nnz : g.in.nnz);
     static const double ms_alpha = env_double("TGO_MS_ALPHA", 12.0);
     static const bool trace = env_double("TGO_TRACE", 0.0) != 0.0;
-    static const bool filter = env_double("TGO_MS_FILTER", 1.0) != 0.0;
+    // frontier-bitmap filter of pull levels: measured slower (every pull level: 3.07 -> 3.99 ms,
+    // 0.95 -> 1.25, 0.18 -> 0.19; MS-BFS 3146 -> 2471 GTEPS, profiles/r02ad_*): the mask gathers
+    // mostly hit L2 / the Infinity Cache already and the probe adds a dependent load.  Opt-in.
+    static const bool filter = env_double("TGO_MS_FILTER", 0.0) != 0.0;
     int64_t qlen = static_cast<int64_t>(uniq.size());
     int64_t mf = 0;
     {

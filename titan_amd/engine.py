@@ -108,6 +108,24 @@ class Engine:
         self.n = self.lib.tgo_num_vertices(self.ctx)
         return self
 
+    def append_rows(self, rows, schema: Schema, scope, apply_cap=True, labels=(), weight_key=0):
+        """One work block of scanned rows (tgo_load_rows without finishing the load)."""
+        opts, keep = self._opts(scope, apply_cap, labels, weight_key)
+        keys = np.ascontiguousarray(rows.keys, dtype=np.int64)
+        eb = np.ascontiguousarray(rows.entry_begin, dtype=np.int64)
+        bb = np.ascontiguousarray(rows.byte_begin, dtype=np.int64)
+        data = np.ascontiguousarray(rows.data, dtype=np.uint8)
+        lv = np.ascontiguousarray(rows.limit_valpos, dtype=np.int64)
+        cr = L.Rows(rows.nrows, L.ptr(keys, C.c_int64), L.ptr(eb, C.c_int64), L.ptr(bb, C.c_int64),
+                    L.ptr(data, C.c_uint8), L.ptr(lv, C.c_int64))
+        _check(self.lib, self.ctx, self.lib.tgo_load_rows(self.ctx, C.byref(cr), C.byref(schema.c), C.byref(opts)))
+        return self
+
+    def finish_rows(self):
+        _check(self.lib, self.ctx, self.lib.tgo_finish_load(self.ctx))
+        self.n = self.lib.tgo_num_vertices(self.ctx)
+        return self
+
     def load_edges(self, n, src, dst, scope, weight=None, titan_ids=None, apply_cap=True, weight_key=0):
         src = np.ascontiguousarray(src, dtype=np.int32)
         dst = np.ascontiguousarray(dst, dtype=np.int32)
