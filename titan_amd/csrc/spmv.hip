@@ -376,8 +376,10 @@ int resident_groups(K kernel) {
     cached = ((per_cu * cus + 7) / 8) * 8;
     return cached;
 }
+// Measured slower than one workgroup per tile (RMAT-24: 1.547 vs 1.388 ms/update, bitwise
+// equal; profiles/r02ae_pr_pipe.log): opt-in only.
 inline bool pr_pipelined() {
-    static const int on = [] { const char* e = std::getenv("TGO_PR_PIPE"); return e ? std::atoi(e) : 1; }();
+    static const int on = [] { const char* e = std::getenv("TGO_PR_PIPE"); return e ? std::atoi(e) : 0; }();
     return on != 0;
 }
 
