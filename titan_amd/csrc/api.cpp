@@ -54,6 +54,7 @@ struct tgo_ctx {
     int64_t pv_max_out = 0, pv_max_in = 0;   // largest OUT / IN list of a vertex cut
     // last finished program whose compute keys tgo_result_rows can encode (-1 = none)
     int res_kind = -1;
+    DecodeScratch dec;                       // device row decoder buffers (decode.hip)
     bool res_empty = false;                  // it set no property (PageRank iterations(0))
     ResultSource res_src;
     int num_cus = 256;          // compute units of the device (persistent launches)
@@ -691,6 +692,7 @@ void tgo_destroy(tgo_ctx* ctx) {
     (void)hipSetDevice(ctx->opts.device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     free_graph(ctx);
+    ctx->dec.release();
     if (ctx->sc.hcnt) (void)hipHostFree(ctx->sc.hcnt);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
@@ -719,8 +721,13 @@ int tgo_load_rows(tgo_ctx* ctx, const tgo_rows* rows, const tgo_schema* schema, 
     (void)hipSetDevice(ctx->opts.device);
     const auto t0 = std::chrono::steady_clock::now();
     std::string err;
-    int rc = decode_rows(ctx->staging, rows, schema, opts, ctx->opts.partition_bits,
-                         ctx->opts.hard_query_limit, threads_of(ctx), err);
+    // device decode (decode.hip) unless TGO_HOST_DECODE=1 picks the multi-threaded host decoder
+    const char* host = std::getenv("TGO_HOST_DECODE");
+    int rc = (host && std::atoi(host) != 0)
+                 ? decode_rows(ctx->staging, rows, schema, opts, ctx->opts.partition_bits, ctx->opts.hard_query_limit,
+                               threads_of(ctx), err)
+                 : decode_rows_device(ctx->staging, rows, schema, opts, ctx->opts.partition_bits,
+                                      ctx->opts.hard_query_limit, ctx->dec, ctx->stream, err);
     ctx->st.load_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     if (rc) { ctx->staging = RowStaging(); return fail(ctx, rc, err); }
     return TGO_OK;
@@ -733,6 +740,7 @@ int tgo_finish_load(tgo_ctx* ctx) {
     const auto t0 = std::chrono::steady_clock::now();
     HostGraph h;
     std::string err;
+    ctx->dec.release();                      // the decoder's batch buffers are done
     int rc = assemble_from_rows(ctx->staging, h, threads_of(ctx), err);
     if (rc) return fail(ctx, rc, err);
     free_graph(ctx);

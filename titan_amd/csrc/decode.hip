@@ -1,0 +1,225 @@
+// decode.hip — device decode of scanned edgestore rows: the per-row rules of
+// VertexJobConverter.process (key filter, ghost check, user-edge slice, QueryContainer limit;
+// VertexJobConverter.java:109-171) and EdgeSerializer.parseRelation for every kept entry
+// (EdgeSerializer.java:73-166), on the GPU, with the same codec as the host path (codec.hpp,
+// compiled here as __host__ __device__).
+//
+// Per batch: the StaticArrayEntryList arrays are uploaded; `dec_rows` (one thread per row)
+// classifies the row and finds its user-edge slice [0x60, 0x80) by binary search over the
+// column-sorted entries' first bytes; an exclusive scan of the kept counts gives every kept
+// entry an output slot; `dec_entries` (one thread per kept entry, its row found by binary
+// search over the scan) decodes it.  The staging arrays come back to the host, which keeps
+// the same RowStaging as the host decoder: parity is checked by running both paths.
+// Byte work over HBM: the batch's row bytes are read once, 13 bytes per kept entry written.
+#define TGO_HD __host__ __device__
+#include <cstring>
+#include <hip/hip_runtime.h>
+#include "codec.hpp"
+#include "engine.hpp"
+
+namespace tgo {
+namespace {
+
+constexpr int kBlock = 256;
+inline unsigned grid_for(int64_t n) {
+    int64_t g = (n + kBlock - 1) / kBlock;
+    return static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(g, 65536)));
+}
+
+enum : int32_t { kRowLive = 0, kRowSkipped = 1, kRowGhost = 2, kRowBadId = -1, kRowEmpty = -2, kRowBadFirst = -3 };
+
+__device__ __forceinline__ int64_t ent_start(const int64_t* lv, int64_t e0, int64_t k) {
+    return k == e0 ? 0 : static_cast<int64_t>(static_cast<uint64_t>(lv[k - 1]) >> 32);
+}
+
+__global__ void __launch_bounds__(kBlock) dec_rows(const int64_t* __restrict__ keys, const int64_t* __restrict__ eb,
+        const int64_t* __restrict__ bb, const uint8_t* __restrict__ bytes, const int64_t* __restrict__ lv,
+        int64_t nrows, int pb, int64_t limit, int64_t* __restrict__ vid_out, int64_t* __restrict__ first_out,
+        int64_t* __restrict__ keep_out, int32_t* __restrict__ status, uint8_t* __restrict__ rep_out,
+        unsigned long long* __restrict__ truncated) {
+    for (int64_t r = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; r <= nrows;
+         r += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        if (r == nrows) { keep_out[nrows] = 0; continue; }
+        keep_out[r] = 0;
+        first_out[r] = 0;
+        rep_out[r] = 0;
+        const int64_t vid = key_to_vertex_id(keys[r], pb);
+        vid_out[r] = vid;
+        if (vid & 1) { status[r] = kRowSkipped; continue; }          // key filter: Invisible (:156-162)
+        const int64_t sfx = vid & 7;
+        if (sfx != 0 && sfx != 2 && sfx != 4) { status[r] = kRowBadId; continue; }
+        const bool is_rep = sfx == 2 && vid != canonical_vertex_id(vid, pb);
+        const int64_t e0 = eb[r], e1 = eb[r + 1];
+        if (e1 <= e0) { status[r] = kRowEmpty; continue; }
+        const uint8_t* base = bytes + bb[r];
+        if (!is_rep) {                                               // ghost check (:131-137)
+            Cursor c{base, static_cast<size_t>(static_cast<uint64_t>(lv[e0]) >> 32), 0};
+            RelType rt;
+            if (!read_relation_type(c, rt)) { status[r] = kRowBadFirst; continue; }
+            if (rt.is_edge || rt.type_id != kVertexExistsId) { status[r] = kRowGhost; continue; }
+        }
+        // user-edge slice [0x60, 0x80): entries are column-sorted, so two lower bounds
+        int64_t lo = e0, hi = e1;
+        while (lo < hi) { const int64_t m = (lo + hi) >> 1; if (base[ent_start(lv, e0, m)] < 0x60) lo = m + 1; else hi = m; }
+        const int64_t first = lo;
+        hi = e1;
+        while (lo < hi) { const int64_t m = (lo + hi) >> 1; if (base[ent_start(lv, e0, m)] < 0x80) lo = m + 1; else hi = m; }
+        const int64_t cnt = lo - first;
+        if (cnt >= limit) atomicAdd(truncated, 1ULL);                // TRUNCATED_ENTRY_LISTS (:125)
+        status[r] = kRowLive;
+        rep_out[r] = is_rep ? 1 : 0;
+        vid_out[r] = is_rep ? canonical_vertex_id(vid, pb) : vid;
+        first_out[r] = first;
+        keep_out[r] = cnt < limit ? cnt : limit;
+    }
+}
+
+__global__ void __launch_bounds__(kBlock) dec_entries(const int64_t* __restrict__ bb, const uint8_t* __restrict__ bytes,
+        const int64_t* __restrict__ eb, const int64_t* __restrict__ lv, const int64_t* __restrict__ first,
+        const int64_t* __restrict__ koff, int64_t nrows, int64_t total, PlanView plan, int pb, int weighted,
+        int64_t* __restrict__ other, uint8_t* __restrict__ dir, int32_t* __restrict__ w, uint8_t* __restrict__ sel,
+        int32_t* __restrict__ err) {
+    for (int64_t p = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; p < total;
+         p += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        int64_t lo = 0, hi = nrows;                                  // row r: koff[r] <= p < koff[r+1]
+        while (lo < hi) { const int64_t m = (lo + hi + 1) >> 1; if (koff[m] <= p) lo = m; else hi = m - 1; }
+        const int64_t r = lo;
+        const int64_t e0 = eb[r];
+        const int64_t k = first[r] + (p - koff[r]);
+        const int64_t s = ent_start(lv, e0, k);
+        const int64_t e = static_cast<int64_t>(static_cast<uint64_t>(lv[k]) >> 32);
+        const int64_t vp = lv[k] & 0x7FFFFFFF;
+        DecodedEdge de{};
+        const DecodeResult dr = e >= s ? decode_edge(bytes + bb[r] + s, static_cast<size_t>(e - s),
+                                                     static_cast<size_t>(vp), plan, de)
+                                       : DecodeResult::kError;
+        if (dr == DecodeResult::kSkip) { sel[p] = 0; continue; }
+        if (dr != DecodeResult::kOk) {
+            atomicOr(err, dr == DecodeResult::kUnsupported ? 2 : 1);
+            sel[p] = 0;
+            continue;
+        }
+        sel[p] = 1;
+        other[p] = is_partitioned_vertex(de.other, pb) ? canonical_vertex_id(de.other, pb) : de.other;  // :89
+        dir[p] = static_cast<uint8_t>(de.dir);
+        w[p] = weighted ? (de.has_weight ? de.weight : kMissingWeight) : 1;
+    }
+}
+
+}  // namespace
+
+void DecodeScratch::release() {
+    keys.release(); eb.release(); bb.release(); bytes.release(); lv.release(); vid.release(); first.release();
+    keep.release(); koff.release(); status.release(); rep.release(); other.release(); dir.release(); w.release();
+    sel.release(); err.release(); trunc.release(); plan_labels.release(); plan_keys.release(); plan_kdts.release();
+    plan_dts.release();
+    if (cub_tmp) (void)hipFree(cub_tmp);
+    cub_tmp = nullptr;
+    cub_bytes = 0;
+}
+
+int decode_rows_device(RowStaging& st, const tgo_rows* rows, const tgo_schema* schema, const tgo_load_opts* opts,
+                       int pb, int64_t hard_limit, DecodeScratch& ds, hipStream_t stream, std::string& err) {
+    HostPlan hp;
+    if (int rc = build_plan(schema, opts, hp, err)) return rc;
+    const bool typed = opts->n_labels > 0;
+    const int64_t limit = (opts->apply_cap && !typed && opts->scope != TGO_SCOPE_BOTH_E) ? hard_limit : INT64_MAX;
+    const int64_t nrows = rows->nrows;
+    if (int rc = staging_begin(st, opts, err)) return rc;
+    if (nrows == 0) return TGO_OK;
+    const int64_t nent = rows->row_entry_begin[nrows], nbytes = rows->row_byte_begin[nrows];
+    hipError_t e = hipSuccess;
+#define DEC_TRY(x) do { e = (x); if (e != hipSuccess) { err = hipGetErrorString(e); return e == hipErrorOutOfMemory ? TGO_E_OOM : TGO_E_HIP; } } while (0)
+    for (DBuf<int64_t>* b : {&ds.keys, &ds.eb, &ds.bb, &ds.vid, &ds.first, &ds.keep, &ds.koff}) DEC_TRY(b->grow(nrows + 1));
+    DEC_TRY(ds.status.grow(nrows + 1));
+    DEC_TRY(ds.rep.grow(nrows + 1));
+    DEC_TRY(ds.bytes.grow(nbytes + 1));
+    DEC_TRY(ds.lv.grow(nent + 1));
+    DEC_TRY(ds.err.grow(1));
+    DEC_TRY(ds.trunc.grow(1));
+    DEC_TRY(ds.plan_labels.grow(static_cast<int64_t>(hp.label_bytes.size()) + 1));
+    DEC_TRY(ds.plan_keys.grow(static_cast<int64_t>(hp.key_ids.size()) + 1));
+    DEC_TRY(ds.plan_kdts.grow(static_cast<int64_t>(hp.key_dts.size()) + 1));
+    DEC_TRY(ds.plan_dts.grow(static_cast<int64_t>(hp.dts.size()) + 1));
+    auto h2d = [&](void* d, const void* h, size_t n) { return n ? hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, stream) : hipSuccess; };
+    DEC_TRY(h2d(ds.keys.p, rows->row_keys, nrows * 8));
+    DEC_TRY(h2d(ds.eb.p, rows->row_entry_begin, (nrows + 1) * 8));
+    DEC_TRY(h2d(ds.bb.p, rows->row_byte_begin, (nrows + 1) * 8));
+    DEC_TRY(h2d(ds.bytes.p, rows->entry_bytes, nbytes));
+    DEC_TRY(h2d(ds.lv.p, rows->entry_limit_valpos, nent * 8));
+    DEC_TRY(h2d(ds.plan_labels.p, hp.label_bytes.data(), hp.label_bytes.size()));
+    DEC_TRY(h2d(ds.plan_keys.p, hp.key_ids.data(), hp.key_ids.size() * 8));
+    DEC_TRY(h2d(ds.plan_kdts.p, hp.key_dts.data(), hp.key_dts.size()));
+    DEC_TRY(h2d(ds.plan_dts.p, hp.dts.data(), hp.dts.size()));
+    DEC_TRY(hipMemsetAsync(ds.err.p, 0, sizeof(int32_t), stream));
+    DEC_TRY(hipMemsetAsync(ds.trunc.p, 0, sizeof(unsigned long long), stream));
+    dec_rows<<<grid_for(nrows + 1), kBlock, 0, stream>>>(ds.keys.p, ds.eb.p, ds.bb.p, ds.bytes.p, ds.lv.p, nrows, pb, limit, ds.vid.p,
+                                                         ds.first.p, ds.keep.p, ds.status.p, ds.rep.p, ds.trunc.p);
+    DEC_TRY(hipGetLastError());
+    DEC_TRY(scan_exclusive_i64(ds.cub_tmp, ds.cub_bytes, ds.keep.p, ds.koff.p, nrows + 1, stream));
+    std::vector<int64_t> vid(nrows), koff(nrows + 1);
+    std::vector<int32_t> status(nrows);
+    std::vector<uint8_t> rep(nrows);
+    unsigned long long trunc = 0;
+    DEC_TRY(hipMemcpyAsync(koff.data(), ds.koff.p, (nrows + 1) * 8, hipMemcpyDeviceToHost, stream));
+    DEC_TRY(hipMemcpyAsync(vid.data(), ds.vid.p, nrows * 8, hipMemcpyDeviceToHost, stream));
+    DEC_TRY(hipMemcpyAsync(status.data(), ds.status.p, nrows * 4, hipMemcpyDeviceToHost, stream));
+    DEC_TRY(hipMemcpyAsync(rep.data(), ds.rep.p, nrows, hipMemcpyDeviceToHost, stream));
+    DEC_TRY(hipMemcpyAsync(&trunc, ds.trunc.p, sizeof(trunc), hipMemcpyDeviceToHost, stream));
+    DEC_TRY(hipStreamSynchronize(stream));
+    for (int64_t r = 0; r < nrows; ++r) {
+        if (status[r] >= 0) continue;
+        err = status[r] == kRowBadId ? "row key has an unrecognized vertex id type"
+            : status[r] == kRowEmpty ? "row without entries" : "malformed first column";
+        return TGO_E_CODEC;
+    }
+    const int64_t total = koff[nrows];
+    DEC_TRY(ds.other.grow(total + 1));
+    DEC_TRY(ds.w.grow(total + 1));
+    DEC_TRY(ds.dir.grow(total + 1));
+    DEC_TRY(ds.sel.grow(total + 1));
+    const PlanView plan{reinterpret_cast<const LabelPlan*>(ds.plan_labels.p), hp.n_labels,
+                        static_cast<int32_t>(hp.key_ids.size()), ds.plan_keys.p, ds.plan_kdts.p, ds.plan_dts.p, hp.weight_key};
+    if (total > 0) {
+        dec_entries<<<grid_for(total), kBlock, 0, stream>>>(ds.bb.p, ds.bytes.p, ds.eb.p, ds.lv.p, ds.first.p, ds.koff.p, nrows, total,
+                                                             plan, pb, opts->weight_key != 0 ? 1 : 0, ds.other.p, ds.dir.p,
+                                                             ds.w.p, ds.sel.p, ds.err.p);
+        DEC_TRY(hipGetLastError());
+    }
+    std::vector<int64_t> other(total);
+    std::vector<uint8_t> dir(total), sel(total);
+    std::vector<int32_t> w(total);
+    int32_t eflag = 0;
+    DEC_TRY(hipMemcpyAsync(&eflag, ds.err.p, 4, hipMemcpyDeviceToHost, stream));
+    if (total) {
+        DEC_TRY(hipMemcpyAsync(other.data(), ds.other.p, total * 8, hipMemcpyDeviceToHost, stream));
+        DEC_TRY(hipMemcpyAsync(dir.data(), ds.dir.p, total, hipMemcpyDeviceToHost, stream));
+        DEC_TRY(hipMemcpyAsync(sel.data(), ds.sel.p, total, hipMemcpyDeviceToHost, stream));
+        DEC_TRY(hipMemcpyAsync(w.data(), ds.w.p, total * 4, hipMemcpyDeviceToHost, stream));
+    }
+    DEC_TRY(hipStreamSynchronize(stream));
+#undef DEC_TRY
+    if (eflag) {
+        err = (eflag & 1) ? "malformed edge entry" : "inline property of a key missing from the schema";
+        return (eflag & 1) ? TGO_E_CODEC : TGO_E_UNSUPPORTED;
+    }
+    // append in row order, exactly as the host decoder stages them
+    st.truncated += static_cast<int64_t>(trunc);
+    for (int64_t r = 0; r < nrows; ++r) {
+        if (status[r] == kRowSkipped) { ++st.skipped; continue; }
+        if (status[r] == kRowGhost) { ++st.ghost; continue; }
+        st.vid.push_back(vid[r]);
+        st.rep.push_back(rep[r]);
+        st.n_rep += rep[r];
+        for (int64_t p = koff[r]; p < koff[r + 1]; ++p) {
+            if (!sel[p]) continue;
+            st.other.push_back(other[p]);
+            st.dir.push_back(dir[p]);
+            st.w.push_back(w[p]);
+        }
+        st.row_begin.push_back(static_cast<int64_t>(st.other.size()));
+    }
+    return TGO_OK;
+}
+
+}  // namespace tgo

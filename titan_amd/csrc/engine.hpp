@@ -12,6 +12,7 @@
 // are no longer transposes of each other, and the push list is an explicit transpose
 // of the pull list (t-CSR).
 #pragma once
+#include <algorithm>
 #include <cstdint>
 #include <string>
 #include <vector>
@@ -92,6 +93,40 @@ int build_plan(const tgo_schema* schema, const tgo_load_opts* opts, HostPlan& hp
 int decode_one_entry(const tgo_schema* schema, const tgo_load_opts* opts, const uint8_t* entry,
                      int64_t len, int64_t value_pos, tgo_edge_entry* out, std::string& err);
 
+int staging_begin(RowStaging& st, const tgo_load_opts* opts, std::string& err);
+// Grow-only device buffer (the device decoder reuses its buffers across row batches).
+template <class T>
+struct DBuf {
+    T* p = nullptr;
+    int64_t cap = 0;
+    hipError_t grow(int64_t need) {
+        if (need <= cap) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        const int64_t c = std::max<int64_t>(need, 1) + need / 4;
+        const hipError_t e = hipMalloc(&p, static_cast<size_t>(c) * sizeof(T));
+        if (e == hipSuccess) cap = c;
+        return e;
+    }
+    void release() { if (p) (void)hipFree(p); p = nullptr; cap = 0; }
+};
+struct DecodeScratch {
+    DBuf<int64_t> keys, eb, bb, lv, vid, first, keep, koff, other, plan_keys;
+    DBuf<uint8_t> bytes, rep, dir, sel, plan_labels;
+    DBuf<int8_t> plan_kdts, plan_dts;
+    DBuf<int32_t> status, w, err;
+    DBuf<unsigned long long> trunc;
+    void* cub_tmp = nullptr;
+    size_t cub_bytes = 0;
+    void release();
+};
+// The same decode as decode_rows, on the device (decode.hip): the batch is uploaded, one
+// kernel classifies rows (key filter, ghost check, user-edge slice, cap) and one decodes
+// every kept entry; the staging arrays come back to the host.
+int decode_rows_device(RowStaging& st, const tgo_rows* rows, const tgo_schema* schema,
+                       const tgo_load_opts* opts, int pb, int64_t hard_limit, DecodeScratch& ds,
+                       hipStream_t stream, std::string& err);
 int decode_rows(RowStaging& st, const tgo_rows* rows, const tgo_schema* schema,
                 const tgo_load_opts* opts, int pb, int64_t hard_limit, int threads,
                 std::string& err);

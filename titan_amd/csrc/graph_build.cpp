@@ -135,6 +135,23 @@ int decode_one_entry(const tgo_schema* schema, const tgo_load_opts* opts, const 
 
 
 // ------------------------------------------------------------------ rows -> staging
+// First batch: remember the load options; later batches must repeat them.
+int staging_begin(RowStaging& st, const tgo_load_opts* opts, std::string& err) {
+    if (!st.active) {
+        st = RowStaging();
+        st.active = true;
+        st.opts = *opts;
+        st.labels.assign(opts->label_ids, opts->label_ids + opts->n_labels);
+        st.opts.label_ids = nullptr;
+        st.row_begin.push_back(0);
+    } else if (st.opts.scope != opts->scope || st.opts.weight_key != opts->weight_key ||
+               st.opts.apply_cap != opts->apply_cap) {
+        err = "tgo_load_opts differ between row batches";
+        return TGO_E_INVALID;
+    }
+    return TGO_OK;
+}
+
 int decode_rows(RowStaging& st, const tgo_rows* rows, const tgo_schema* schema,
                 const tgo_load_opts* opts, int pb, int64_t hard_limit, int threads,
                 std::string& err) {
@@ -218,18 +235,7 @@ int decode_rows(RowStaging& st, const tgo_rows* rows, const tgo_schema* schema,
         }
     });
     for (auto& L : loc) if (L.rc != TGO_OK) { err = L.msg; return L.rc; }
-    if (!st.active) {
-        st = RowStaging();
-        st.active = true;
-        st.opts = *opts;
-        st.labels.assign(opts->label_ids, opts->label_ids + opts->n_labels);
-        st.opts.label_ids = nullptr;
-        st.row_begin.push_back(0);
-    } else if (st.opts.scope != opts->scope || st.opts.weight_key != opts->weight_key ||
-               st.opts.apply_cap != opts->apply_cap) {
-        err = "tgo_load_opts differ between row batches";
-        return TGO_E_INVALID;
-    }
+    if (int rc = staging_begin(st, opts, err)) return rc;
     for (auto& L : loc) {
         st.ghost += L.ghost; st.truncated += L.truncated; st.skipped += L.skipped;
         for (size_t i = 0; i < L.vid.size(); ++i) {

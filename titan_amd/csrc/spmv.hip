@@ -195,7 +195,7 @@ __device__ __forceinline__ void load_packed_idx(const int32_t* __restrict__ padj
     }
 }
 template <class Fin>
-__global__ void __launch_bounds__(kBlock) gather_packed_pipe(const int64_t* __restrict__ off,
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5, 8))) gather_packed_pipe(const int64_t* __restrict__ off,
         const int32_t* __restrict__ padj, const int64_t* __restrict__ blk, int64_t nblocks,
         const double* __restrict__ msg, Fin fin) {
     __shared__ double s_val[kTile];
@@ -207,9 +207,8 @@ __global__ void __launch_bounds__(kBlock) gather_packed_pipe(const int64_t* __re
     int32_t v[kPer];
     load_packed_idx(padj, s0, nnz, v);
     for (;;) {
-        double val[kPer];
-#pragma unroll
-        for (int j = 0; j < kPer; ++j) val[j] = v[j] >= 0 ? msg[v[j] >> kPackShift] : 0.0;
+        // the next tile's index loads go out first, then this tile's gathers: one wait covers
+        // both, so a tile costs max(index latency, gather latency) instead of their sum
         const int64_t nb = b + gridDim.x;
         int64_t nr0 = 0, nr1 = 0, ns0 = 0, nnnz = 0;
         if (nb < nblocks) {
@@ -218,7 +217,10 @@ __global__ void __launch_bounds__(kBlock) gather_packed_pipe(const int64_t* __re
             nnnz = off[nr1] - ns0;
         }
         int32_t nv[kPer];
-        load_packed_idx(padj, ns0, nnnz, nv);       // in flight during this tile's scatter + reduce
+        load_packed_idx(padj, ns0, nnnz, nv);
+        double val[kPer];
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) val[j] = v[j] >= 0 ? msg[v[j] >> kPackShift] : 0.0;
         if (nnz <= kTile) {
 #pragma unroll
             for (int j = 0; j < kPer; ++j)
@@ -320,7 +322,7 @@ __global__ void __launch_bounds__(kBlock) cold_gather(const int64_t* __restrict_
 // that XCD's blocks j = b[x] + g/8, + G/8, ... in segment order, prefetching the next tile's
 // indices during the current tile's scatter and reduce.  Same per-tile arithmetic as
 // cold_gather<true>.
-__global__ void __launch_bounds__(kBlock) cold_gather_pipe(const int64_t* __restrict__ poff,
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5, 8))) cold_gather_pipe(const int64_t* __restrict__ poff,
         const int32_t* __restrict__ cadj, const int64_t* __restrict__ bbeg, const int64_t* __restrict__ bend,
         const int32_t* __restrict__ xblk, const int32_t* __restrict__ bsrc, XcdBase xb, const double* __restrict__ msg,
         double* __restrict__ partial) {
@@ -338,9 +340,6 @@ __global__ void __launch_bounds__(kBlock) cold_gather_pipe(const int64_t* __rest
     load_packed_idx(cadj, s0, nnz, v);
     for (;;) {
         const double* seg_msg = msg + bsrc[blkid];
-        double val[kPer];
-#pragma unroll
-        for (int q = 0; q < kPer; ++q) val[q] = v[q] >= 0 ? seg_msg[v[q] >> kPackShift] : 0.0;
         const int64_t nj = j + stride;
         int64_t nblk = 0, np0 = 0, np1 = 0, ns0 = 0, nnnz = 0;
         if (nj < jend) {
@@ -350,7 +349,10 @@ __global__ void __launch_bounds__(kBlock) cold_gather_pipe(const int64_t* __rest
             nnnz = poff[np1] - ns0;
         }
         int32_t nv[kPer];
-        load_packed_idx(cadj, ns0, nnnz, nv);
+        load_packed_idx(cadj, ns0, nnnz, nv);       // next tile's indices, then this tile's gathers
+        double val[kPer];
+#pragma unroll
+        for (int q = 0; q < kPer; ++q) val[q] = v[q] >= 0 ? seg_msg[v[q] >> kPackShift] : 0.0;
 #pragma unroll
         for (int q = 0; q < kPer; ++q)
             if (v[q] >= 0) s_val[v[q] & ((1 << kPackShift) - 1)] = val[q];
