@@ -59,4 +59,5 @@ def test_scan_gotg_ghost_and_typed_scope():
                          work_block_size=3)
         d = eng.bfs(int(vids[names.index(seed)]), 12, scope)
         got = by_id(eng.vertex_ids(), d)
-        assert [got[int(v)] for v in vids] == [int(x) for x in npz[key]]
+        assert [-1 if got[int(v)] == L.DIST_ABSENT else got[int(v)] for v in vids] == [int(x) for x in npz[key]]
+        assert eng.stats()["ghost_vertices"] == 1 and eng.stats()["skipped_rows"] == 1

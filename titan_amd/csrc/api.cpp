@@ -1425,7 +1425,8 @@ int tgo_part_ms_pull(tgo_ctx* ctx, int32_t level, const uint64_t* fr_global, uin
     if (level + 1 >= (1 << kLevelPlanes)) return fail(ctx, TGO_E_UNSUPPORTED, "multi-source BFS levels are < 65536");
     if ((rc = ms_planes_for(ctx, level + 1))) return rc;
     HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
-    HIP_TRY(hipMemsetAsync(fr_next, 0, g.n * 8, st));
+    // the pull writes every active row's mask; only the entry-less tail needs clearing
+    if (g.n > g.n_active) HIP_TRY(hipMemsetAsync(fr_next + g.n_active, 0, (g.n - g.n_active) * 8, st));
     const int nxt = ctx->part_cur ^ 1;
     HIP_TRY(k_ms_pull(pull, push, g.n_active, full, fr_global, nullptr, s.ms_vis, fr_next, ms_planes(ctx), s.cnt,
                       level + 1, st));

@@ -13,6 +13,7 @@
 // sources `fresh` of v at level L ORs `fresh` into plane k of v for every set bit k of L —
 // at most log2(L)+1 coalesced 8-byte writes per vertex and level, and planes are zeroed
 // only when the sweep first reaches level 2^k.
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 #include "frontier.hpp"
 
@@ -72,13 +73,13 @@ __global__ void ms_seed(const int64_t* __restrict__ seeds, int nseeds, uint64_t*
 // every still-unreached source of v is covered.  One vertex per lane; lists longer than
 // kCoop are OR-reduced by the whole wave.
 constexpr int64_t kCoop = 64;
-constexpr int kStep = 8;
 // fbm (optional): bit u set iff fr[u] != 0.  The 2 MB bitmap stays in every XCD's L2, so a
 // neighbour outside every source's frontier costs an L2 probe instead of an 8-byte mask
 // gather from the 134 MB mask array (mostly cold, low-degree vertices: the misses).
 __device__ __forceinline__ bool in_frontier(const uint64_t* __restrict__ fbm, int32_t u) {
     return !fbm || ((fbm[u >> 6] >> (u & 63)) & 1ULL);
 }
+template <int kStep>       // entries per dependent round trip of a lane's own list
 __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t n_active, uint64_t full,
         const uint64_t* __restrict__ fr, const uint64_t* __restrict__ fbm, uint64_t* __restrict__ vis,
         uint64_t* __restrict__ nx, LevelPlanes lvl, Counters* cnt, int32_t next_level) {
@@ -340,8 +341,17 @@ hipError_t k_ms_seed(const int64_t* seeds, int nseeds, uint64_t* vis, uint64_t* 
 hipError_t k_ms_pull(const View& pull, const View& push, int64_t n_active, uint64_t full, const uint64_t* fr,
                      const uint64_t* fbm, uint64_t* vis, uint64_t* nx, LevelPlanes lvl, Counters* cnt,
                      int32_t next_level, hipStream_t s) {
-    ms_pull<<<grid_for(n_active, 8192), kBlock, 0, s>>>(pull, push, n_active, full, fr, fbm, vis, nx, lvl, cnt,
-                                                       next_level);
+    // TGO_MS_STEP: entries a lane loads per round trip of its own list (8 default; 16 probe)
+    static const int step = [] { const char* e = std::getenv("TGO_MS_STEP"); return e ? std::atoi(e) : 8; }();
+    if (step == 16)
+        ms_pull<16><<<grid_for(n_active, 8192), kBlock, 0, s>>>(pull, push, n_active, full, fr, fbm, vis, nx, lvl, cnt,
+                                                               next_level);
+    else if (step == 4)
+        ms_pull<4><<<grid_for(n_active, 8192), kBlock, 0, s>>>(pull, push, n_active, full, fr, fbm, vis, nx, lvl, cnt,
+                                                              next_level);
+    else
+        ms_pull<8><<<grid_for(n_active, 8192), kBlock, 0, s>>>(pull, push, n_active, full, fr, fbm, vis, nx, lvl, cnt,
+                                                              next_level);
     return hipGetLastError();
 }
 hipError_t k_ms_fbitmap(const uint64_t* fr, int64_t n, uint64_t* fbm, hipStream_t s) {

@@ -19,7 +19,6 @@
 // their per-(row, segment) sums land in partial[], and the hot pass adds them to each row.
 // Every sum has a fixed order: results are bitwise reproducible run to run.
 #include <algorithm>
-#include <cstdlib>
 #include <hip/hip_runtime.h>
 #include "engine.hpp"
 
@@ -181,61 +180,6 @@ __global__ void __launch_bounds__(kBlock) gather_short_packed(const int64_t* __r
     __syncthreads();
     reduce_runs<PrOp>(off, r0, r1, s0, s_val, fin);
 }
-// Persistent, software-pipelined form of gather_short_packed: workgroup g takes tiles
-// g, g + G, g + 2G, ... and issues the NEXT tile's index loads right after the current
-// tile's gathers, so the HBM latency of the index stream overlaps the gathers, the LDS scatter
-// and the row reduce instead of starting every tile cold.  The per-tile arithmetic (slots,
-// reduce order) is the one of gather_short_packed: results are bitwise identical.
-__device__ __forceinline__ void load_packed_idx(const int32_t* __restrict__ padj, int64_t s0, int64_t nnz,
-                                                int32_t (&v)[kPer]) {
-#pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-        const int64_t k = threadIdx.x + static_cast<int64_t>(j) * kBlock;
-        v[j] = (nnz <= kTile && k < nnz) ? stream_idx(padj + s0 + k) : -1;
-    }
-}
-template <class Fin>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5, 8))) gather_packed_pipe(const int64_t* __restrict__ off,
-        const int32_t* __restrict__ padj, const int64_t* __restrict__ blk, int64_t nblocks,
-        const double* __restrict__ msg, Fin fin) {
-    __shared__ double s_val[kTile];
-    int64_t b = blockIdx.x;
-    if (b >= nblocks) return;
-    int64_t r0 = blk[b], r1 = blk[b + 1];
-    int64_t s0 = off[r0];
-    int64_t nnz = off[r1] - s0;                      // > kTile: a long row (chunks handle it)
-    int32_t v[kPer];
-    load_packed_idx(padj, s0, nnz, v);
-    for (;;) {
-        // the next tile's index loads go out first, then this tile's gathers: one wait covers
-        // both, so a tile costs max(index latency, gather latency) instead of their sum
-        const int64_t nb = b + gridDim.x;
-        int64_t nr0 = 0, nr1 = 0, ns0 = 0, nnnz = 0;
-        if (nb < nblocks) {
-            nr0 = blk[nb]; nr1 = blk[nb + 1];
-            ns0 = off[nr0];
-            nnnz = off[nr1] - ns0;
-        }
-        int32_t nv[kPer];
-        load_packed_idx(padj, ns0, nnnz, nv);
-        double val[kPer];
-#pragma unroll
-        for (int j = 0; j < kPer; ++j) val[j] = v[j] >= 0 ? msg[v[j] >> kPackShift] : 0.0;
-        if (nnz <= kTile) {
-#pragma unroll
-            for (int j = 0; j < kPer; ++j)
-                if (v[j] >= 0) s_val[v[j] & ((1 << kPackShift) - 1)] = val[j];
-            __syncthreads();
-            reduce_runs<PrOp>(off, r0, r1, s0, s_val, fin);
-        }
-        if (nb >= nblocks) break;
-        __syncthreads();                             // s_val is rewritten by the next tile
-        b = nb; r0 = nr0; r1 = nr1; s0 = ns0; nnz = nnnz;
-#pragma unroll
-        for (int j = 0; j < kPer; ++j) v[j] = nv[j];
-    }
-}
-
 // A long row's chunk of packed entries: the chunk sum (source order, fixed).
 struct PackedOp {
     using T = double;
@@ -318,73 +262,6 @@ __global__ void __launch_bounds__(kBlock) cold_gather(const int64_t* __restrict_
     reduce_runs<PrOp>(poff, p0, p1, s0, s_val, [&](int64_t p, double sum) { partial[p] = sum; });
 }
 
-// Persistent, pipelined cold pass (packed tiles): workgroup g stays on XCD g % 8 and walks
-// that XCD's blocks j = b[x] + g/8, + G/8, ... in segment order, prefetching the next tile's
-// indices during the current tile's scatter and reduce.  Same per-tile arithmetic as
-// cold_gather<true>.
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5, 8))) cold_gather_pipe(const int64_t* __restrict__ poff,
-        const int32_t* __restrict__ cadj, const int64_t* __restrict__ bbeg, const int64_t* __restrict__ bend,
-        const int32_t* __restrict__ xblk, const int32_t* __restrict__ bsrc, XcdBase xb, const double* __restrict__ msg,
-        double* __restrict__ partial) {
-    __shared__ double s_val[kTile];
-    const int x = static_cast<int>(blockIdx.x & 7);
-    const int64_t stride = gridDim.x >> 3;
-    int64_t j = xb.b[x] + (blockIdx.x >> 3);
-    const int64_t jend = xb.b[x + 1];
-    if (j >= jend) return;
-    int64_t blkid = xblk[j];
-    int64_t p0 = bbeg[blkid], p1 = bend[blkid];
-    int64_t s0 = poff[p0];
-    int64_t nnz = poff[p1] - s0;
-    int32_t v[kPer];
-    load_packed_idx(cadj, s0, nnz, v);
-    for (;;) {
-        const double* seg_msg = msg + bsrc[blkid];
-        const int64_t nj = j + stride;
-        int64_t nblk = 0, np0 = 0, np1 = 0, ns0 = 0, nnnz = 0;
-        if (nj < jend) {
-            nblk = xblk[nj];
-            np0 = bbeg[nblk]; np1 = bend[nblk];
-            ns0 = poff[np0];
-            nnnz = poff[np1] - ns0;
-        }
-        int32_t nv[kPer];
-        load_packed_idx(cadj, ns0, nnnz, nv);       // next tile's indices, then this tile's gathers
-        double val[kPer];
-#pragma unroll
-        for (int q = 0; q < kPer; ++q) val[q] = v[q] >= 0 ? seg_msg[v[q] >> kPackShift] : 0.0;
-#pragma unroll
-        for (int q = 0; q < kPer; ++q)
-            if (v[q] >= 0) s_val[v[q] & ((1 << kPackShift) - 1)] = val[q];
-        __syncthreads();
-        reduce_runs<PrOp>(poff, p0, p1, s0, s_val, [&](int64_t p, double sum) { partial[p] = sum; });
-        if (nj >= jend) break;
-        __syncthreads();
-        j = nj; blkid = nblk; p0 = np0; p1 = np1; s0 = ns0; nnz = nnnz;
-#pragma unroll
-        for (int q = 0; q < kPer; ++q) v[q] = nv[q];
-    }
-}
-
-// Workgroups of a persistent kernel that fit the chip at once (LDS-limited: 32 KB each).
-template <class K>
-int resident_groups(K kernel) {
-    static int cached = 0;
-    if (cached) return cached;
-    int per_cu = 0, dev = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, 0) != hipSuccess || per_cu <= 0) per_cu = 4;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-    cached = ((per_cu * cus + 7) / 8) * 8;
-    return cached;
-}
-// Measured slower than one workgroup per tile (RMAT-24: 1.547 vs 1.388 ms/update, bitwise
-// equal; profiles/r02ae_pr_pipe.log): opt-in only.
-inline bool pr_pipelined() {
-    static const int on = [] { const char* e = std::getenv("TGO_PR_PIPE"); return e ? std::atoi(e) : 0; }();
-    return on != 0;
-}
-
 // Per-row cold sums of the rows that own pieces: the pieces added in segment order.
 __global__ void cold_fold(const int32_t* __restrict__ crow, int64_t ncrows, const uint32_t* __restrict__ cptr,
                           const int32_t* __restrict__ cpid, const double* __restrict__ partial, double* __restrict__ csum) {
@@ -454,11 +331,7 @@ hipError_t k_pr_iter(const DevCsr& in, const RowBlocks& rb, const double* contri
 // Cold phase: the cold segments' partial sums, folded per row into csum (reads only the cold
 // sources [hot, n_src) of `contrib`).
 hipError_t k_pr_cold_phase(const ColdBlocks& cb, const double* contrib, hipStream_t s) {
-    if (cb.max_xcd_blocks > 0 && cb.cpacked && pr_pipelined()) {
-        const int64_t g = std::min<int64_t>(cb.max_xcd_blocks * 8, resident_groups(cold_gather_pipe));
-        cold_gather_pipe<<<static_cast<unsigned>(g), kBlock, 0, s>>>(cb.poff, cb.cadj, cb.bbeg, cb.bend, cb.xblk, cb.bsrc,
-                                                                   cb.xbase, contrib, cb.partial);
-    } else if (cb.max_xcd_blocks > 0) {
+    if (cb.max_xcd_blocks > 0) {
         const unsigned g = static_cast<unsigned>(cb.max_xcd_blocks * 8);
         if (cb.cpacked)
             cold_gather<true><<<g, kBlock, 0, s>>>(cb.poff, cb.cadj, cb.bbeg, cb.bend, cb.xblk, cb.bsrc, cb.xbase, contrib,
@@ -479,11 +352,7 @@ hipError_t k_pr_hot_phase(const ColdBlocks& cb, const double* contrib, const dou
     const PrColdFinal fin{PrFinal{edge_count, pr, contrib_next, alpha, base}, cb.csum};
     if (!cb.packed) return run_gather(cb.hcsr, cb.rb_hot, PrOp{contrib}, fin, partial_long, s);
     const RowBlocks& rb = cb.rb_hot;
-    if (rb.nblocks > 0 && pr_pipelined()) {
-        const int64_t g = std::min<int64_t>(rb.nblocks, resident_groups(gather_packed_pipe<PrColdFinal>));
-        gather_packed_pipe<PrColdFinal><<<static_cast<unsigned>(g), kBlock, 0, s>>>(cb.hcsr.off, cb.hcsr.adj, rb.blk,
-                                                                                   rb.nblocks, contrib, fin);
-    } else if (rb.nblocks > 0) {
+    if (rb.nblocks > 0) {
         gather_short_packed<PrColdFinal><<<static_cast<unsigned>(rb.nblocks), kBlock, 0, s>>>(cb.hcsr.off, cb.hcsr.adj,
                                                                                              rb.blk, contrib, fin);
     }
