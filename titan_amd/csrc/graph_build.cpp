@@ -5,6 +5,9 @@
 // VertexJobConverter.java:109-129, rebuilds a PreloadedVertex per row per superstep).
 // Here the rows are decoded once into an out-CSR and an in-CSR of dense vertex ids.
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <atomic>
 #include <cmath>
 #include <cstring>
@@ -282,29 +285,64 @@ struct IdMap {
     }
 };
 
-// Transpose of the union of `lists` (each an n-row CSR): t[w] gets v for every w in L(v).
+// Transpose of the union of `lists` (each an n-row CSR): t[w] gets v for every w in L(v), each
+// transposed row sorted by source id.  Threads own contiguous source ranges of equal entry
+// counts; per-thread histograms give every thread its slots in every row, so the scatter is
+// stable (source order) without atomics.
 static void transpose_lists(int64_t n, const std::vector<const HostCsr*>& lists, bool weighted,
                             HostCsr& t, int threads) {
-    std::vector<std::atomic<int64_t>> cnt(n + 1);
-    for (auto& c : cnt) c.store(0, std::memory_order_relaxed);
-    for (const HostCsr* L : lists)
-        parallel_for(static_cast<int64_t>(L->adj.size()), threads, [&](int64_t lo, int64_t hi, int) {
-            for (int64_t k = lo; k < hi; ++k) cnt[L->adj[k]].fetch_add(1, std::memory_order_relaxed);
-        });
+    int64_t E = 0;
+    for (const HostCsr* L : lists) E += static_cast<int64_t>(L->adj.size());
+    const int T = std::max(1, std::min<int>(threads, static_cast<int>(std::max<int64_t>(1, E / 65536))));
+    // source ranges [vb[i], vb[i+1]) with ~E/T entries each
+    std::vector<int64_t> vb(T + 1, n);
+    vb[0] = 0;
+    {
+        int64_t acc = 0, next = 1;
+        for (int64_t v = 0; v < n && next < T; ++v) {
+            for (const HostCsr* L : lists) acc += L->off[v + 1] - L->off[v];
+            while (next < T && acc >= E * next / T) vb[next++] = v + 1;
+        }
+    }
+    std::vector<std::vector<int64_t>> pos(T, std::vector<int64_t>(static_cast<size_t>(n), 0));
+    auto run = [&](auto&& body) {
+        std::vector<std::thread> th;
+        for (int i = 0; i < T; ++i) th.emplace_back([&, i] { body(i); });
+        for (auto& x : th) x.join();
+    };
+    run([&](int i) {
+        int64_t* c = pos[i].data();
+        for (int64_t v = vb[i]; v < vb[i + 1]; ++v)
+            for (const HostCsr* L : lists)
+                for (int64_t k = L->off[v]; k < L->off[v + 1]; ++k) ++c[L->adj[k]];
+    });
     t.off.assign(n + 1, 0);
-    for (int64_t v = 0; v < n; ++v) t.off[v + 1] = t.off[v] + cnt[v].load(std::memory_order_relaxed);
-    const int64_t E = t.off[n];
-    t.adj.assign(E, 0);
-    if (weighted) t.w.assign(E, 0);
-    // Sequential fill in source order keeps each transposed row sorted by source id.
-    std::vector<int64_t> pos(t.off.begin(), t.off.end() - 1);
-    for (int64_t v = 0; v < n; ++v)
-        for (const HostCsr* L : lists)
-            for (int64_t k = L->off[v]; k < L->off[v + 1]; ++k) {
-                const int64_t p = pos[L->adj[k]]++;
-                t.adj[p] = static_cast<int32_t>(v);
-                if (weighted) t.w[p] = L->w[k];
-            }
+    parallel_for(n, threads, [&](int64_t a, int64_t b, int) {
+        for (int64_t w = a; w < b; ++w) {
+            int64_t s = 0;
+            for (int i = 0; i < T; ++i) s += pos[i][w];
+            t.off[w + 1] = s;
+        }
+    });
+    for (int64_t w = 0; w < n; ++w) t.off[w + 1] += t.off[w];
+    parallel_for(n, threads, [&](int64_t a, int64_t b, int) {
+        for (int64_t w = a; w < b; ++w) {
+            int64_t p = t.off[w];
+            for (int i = 0; i < T; ++i) { const int64_t c = pos[i][w]; pos[i][w] = p; p += c; }
+        }
+    });
+    t.adj.assign(static_cast<size_t>(E), 0);
+    if (weighted) t.w.assign(static_cast<size_t>(E), 0);
+    run([&](int i) {
+        int64_t* p = pos[i].data();
+        for (int64_t v = vb[i]; v < vb[i + 1]; ++v)
+            for (const HostCsr* L : lists)
+                for (int64_t k = L->off[v]; k < L->off[v + 1]; ++k) {
+                    const int64_t q = p[L->adj[k]]++;
+                    t.adj[q] = static_cast<int32_t>(v);
+                    if (weighted) t.w[q] = L->w[k];
+                }
+    });
 }
 
 // Degree-grouped relabel (DBG, Faldu et al., IISWC'19): vertices are grouped by
@@ -346,17 +384,37 @@ static void permute_graph(HostGraph& g, Nbr nbr, int threads) {
         r.adj.resize(c.adj.size());
         const bool w = !c.w.empty();
         if (w) r.w.resize(c.w.size());
-        parallel_dynamic(n, threads, 2048, [&](int64_t lo, int64_t hi) {
+        // neighbour ids first, in one streaming parallel pass
+        parallel_for(static_cast<int64_t>(c.adj.size()), threads, [&](int64_t lo, int64_t hi, int) {
+            for (int64_t k = lo; k < hi; ++k) c.adj[k] = static_cast<int32_t>(nbr(c.adj[k]));
+        });
+        // small chunks: rows are hottest-first, so the first rows are the hubs
+        parallel_dynamic(n, threads, 64, [&](int64_t lo, int64_t hi) {
             std::vector<uint64_t> key;
             for (int64_t u = lo; u < hi; ++u) {
                 const int64_t b = c.off[inv[u]], len = c.off[inv[u] + 1] - b;
+                int32_t* dst = r.adj.data() + r.off[u];
+                if (!w) {                           // equal neighbours are indistinguishable: sort ids
+                    std::memcpy(dst, c.adj.data() + b, static_cast<size_t>(len) * sizeof(int32_t));
+                    if (len <= 32) {
+                        for (int64_t i = 1; i < len; ++i) {
+                            const int32_t x = dst[i];
+                            int64_t j = i - 1;
+                            while (j >= 0 && dst[j] > x) { dst[j + 1] = dst[j]; --j; }
+                            dst[j + 1] = x;
+                        }
+                    } else {
+                        std::sort(dst, dst + len);
+                    }
+                    continue;
+                }
                 key.resize(len);
-                for (int64_t j = 0; j < len; ++j)   // (new neighbour, original position)
-                    key[j] = (static_cast<uint64_t>(static_cast<uint32_t>(nbr(c.adj[b + j]))) << 32) | static_cast<uint64_t>(j);
+                for (int64_t j = 0; j < len; ++j)   // (new neighbour, original position): stable
+                    key[j] = (static_cast<uint64_t>(static_cast<uint32_t>(c.adj[b + j])) << 32) | static_cast<uint64_t>(j);
                 std::sort(key.begin(), key.end());
                 for (int64_t j = 0; j < len; ++j) {
-                    r.adj[r.off[u] + j] = static_cast<int32_t>(key[j] >> 32);
-                    if (w) r.w[r.off[u] + j] = c.w[b + static_cast<int64_t>(key[j] & 0xFFFFFFFFULL)];
+                    dst[j] = static_cast<int32_t>(key[j] >> 32);
+                    r.w[r.off[u] + j] = c.w[b + static_cast<int64_t>(key[j] & 0xFFFFFFFFULL)];
                 }
             }
         });
@@ -373,11 +431,17 @@ static void permute_graph(HostGraph& g, Nbr nbr, int threads) {
 // BFS hit the XCD L2 / Infinity Cache instead of HBM.  Purely a device layout: the API
 // keeps row-order dense ids (perm maps them) and every result is mapped back.
 static void relabel_by_degree(HostGraph& g, int threads) {
+    auto t0 = std::chrono::steady_clock::now();
     degree_group_order(g.n, [&](int64_t v) {
         return (g.out.off[v + 1] - g.out.off[v]) + (g.in.off[v + 1] - g.in.off[v]);
     }, g.perm);
+    auto t1 = std::chrono::steady_clock::now();
     const int32_t* p = g.perm.data();
     permute_graph(g, [p](int32_t u) { return p[u]; }, threads);
+    if (std::getenv("TGO_TRACE") && std::atoi(std::getenv("TGO_TRACE")))
+        std::fprintf(stderr, "[tgo] relabel: order %.1f ms, permute %.1f ms\n",
+                     std::chrono::duration<double, std::milli>(t1 - t0).count(),
+                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count());
 }
 
 // Multi-GPU layout (tgo_part_layout): the degree-grouped order of the owned range, as
@@ -479,7 +543,21 @@ static void fold_representatives(RowStaging& st, HostGraph& g) {
 }
 
 // ------------------------------------------------------------------ staging -> CSR
+// TGO_TRACE=1: per-phase host assembly times on stderr.
+struct PhaseClock {
+    bool on;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    PhaseClock() : on(std::getenv("TGO_TRACE") && std::atoi(std::getenv("TGO_TRACE")) != 0) {}
+    void lap(const char* what) {
+        if (!on) return;
+        const auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[tgo] assemble %-12s %8.1f ms\n", what, std::chrono::duration<double, std::milli>(now - t).count());
+        t = now;
+    }
+};
+
 int assemble_from_rows(RowStaging& st, HostGraph& g, int threads, std::string& err) {
+    PhaseClock clk;
     g = HostGraph();
     if (st.n_rep > 0 || std::any_of(st.vid.begin(), st.vid.end(), [](int64_t v) { return (v & 7) == 2; }))
         fold_representatives(st, g);
@@ -489,8 +567,10 @@ int assemble_from_rows(RowStaging& st, HostGraph& g, int threads, std::string& e
     g.scope = st.opts.scope;
     g.has_weight = st.opts.weight_key != 0;
     g.ghost = st.ghost; g.truncated = st.truncated; g.skipped = st.skipped;
+    clk.lap("folds");
     IdMap map;
     map.build(st.vid);
+    clk.lap("id map");
     const int64_t n = g.n;
     // Map Titan ids to dense ids; entries to non-executed vertices can never carry a
     // message (EMPTY_STATE => null, VertexState.java:103-137) and are dropped.
@@ -498,6 +578,7 @@ int assemble_from_rows(RowStaging& st, HostGraph& g, int threads, std::string& e
     parallel_for(static_cast<int64_t>(st.other.size()), threads, [&](int64_t lo, int64_t hi, int) {
         for (int64_t k = lo; k < hi; ++k) dense[k] = map.find(st.other[k]);
     });
+    clk.lap("lookups");
     std::vector<int64_t> co(n + 1, 0), ci(n + 1, 0);
     parallel_for(n, threads, [&](int64_t lo, int64_t hi, int) {
         for (int64_t v = lo; v < hi; ++v) {
@@ -525,10 +606,82 @@ int assemble_from_rows(RowStaging& st, HostGraph& g, int threads, std::string& e
             }
         }
     });
+    clk.lap("csr");
     relabel_by_degree(g, threads);
+    clk.lap("relabel");
     finish_views(g, threads);
+    clk.lap("views");
     st = RowStaging();
     return TGO_OK;
+}
+
+// Rows of the owners in [lo, hi) from an edge list: for every edge k with own[k] in range an
+// entry (nbr[k] << 32 | k) in row own[k] - lo, each row sorted by (neighbour, edge index).
+// Counting sort with per-thread histograms over contiguous edge chunks (no atomics: hub rows
+// made a shared-counter scatter contention-bound), then the short per-row sorts.
+static void rows_by_owner(int64_t m, const int32_t* own, const int32_t* nbr, int64_t lo, int64_t hi, int threads,
+                          std::vector<int64_t>& off, std::vector<uint64_t>& keys) {
+    const int64_t n = hi - lo;
+    const int T = std::max(1, std::min<int>(threads, static_cast<int>(std::max<int64_t>(1, m / 65536))));
+    std::vector<std::vector<int64_t>> pos(T, std::vector<int64_t>(static_cast<size_t>(n), 0));
+    auto chunk = [&](int t) { return std::make_pair(m * t / T, m * (t + 1) / T); };
+    {
+        std::vector<std::thread> th;
+        for (int t = 0; t < T; ++t)
+            th.emplace_back([&, t] {
+                const auto [a, b] = chunk(t);
+                int64_t* c = pos[t].data();
+                for (int64_t k = a; k < b; ++k)
+                    if (own[k] >= lo && own[k] < hi) ++c[own[k] - lo];
+            });
+        for (auto& x : th) x.join();
+    }
+    off.assign(n + 1, 0);
+    parallel_for(n, threads, [&](int64_t a, int64_t b, int) {
+        for (int64_t v = a; v < b; ++v) {
+            int64_t s = 0;
+            for (int t = 0; t < T; ++t) s += pos[t][v];
+            off[v + 1] = s;
+        }
+    });
+    for (int64_t v = 0; v < n; ++v) off[v + 1] += off[v];
+    parallel_for(n, threads, [&](int64_t a, int64_t b, int) {      // counts -> each thread's first slot
+        for (int64_t v = a; v < b; ++v) {
+            int64_t p = off[v];
+            for (int t = 0; t < T; ++t) { const int64_t c = pos[t][v]; pos[t][v] = p; p += c; }
+        }
+    });
+    keys.resize(static_cast<size_t>(off[n]));
+    {
+        std::vector<std::thread> th;
+        for (int t = 0; t < T; ++t)
+            th.emplace_back([&, t] {
+                const auto [a, b] = chunk(t);
+                int64_t* p = pos[t].data();
+                for (int64_t k = a; k < b; ++k)
+                    if (own[k] >= lo && own[k] < hi)
+                        keys[p[own[k] - lo]++] = (static_cast<uint64_t>(static_cast<uint32_t>(nbr[k])) << 32) |
+                                                  static_cast<uint64_t>(k);
+            });
+        for (auto& x : th) x.join();
+    }
+    std::vector<std::vector<int64_t>>().swap(pos);
+    parallel_dynamic(n, threads, 256, [&](int64_t a, int64_t b) {   // edge order inside a row: sort by neighbour
+        for (int64_t v = a; v < b; ++v) {
+            uint64_t* r = keys.data() + off[v];
+            const int64_t len = off[v + 1] - off[v];
+            if (len <= 32) {
+                for (int64_t i = 1; i < len; ++i) {
+                    const uint64_t x = r[i];
+                    int64_t j = i - 1;
+                    while (j >= 0 && r[j] > x) { r[j + 1] = r[j]; --j; }
+                    r[j + 1] = x;
+                }
+            } else {
+                std::sort(r, r + len);
+            }
+        }
+    });
 }
 
 // ------------------------------------------------------------------ edges -> CSR
@@ -541,6 +694,7 @@ int assemble_from_rows(RowStaging& st, HostGraph& g, int threads, std::string& e
 // edge index.  Titan ids, when not given, are assigned monotonically in dense order.
 int assemble_from_edges(const tgo_edges* e, const tgo_load_opts* opts, int64_t hard_limit,
                         HostGraph& g, int threads, std::string& err) {
+    PhaseClock clk;
     g = HostGraph();
     const int64_t n = e->n, m = e->m;
     if (n <= 0 || n >= INT32_MAX) { err = "vertex count out of range"; return TGO_E_INVALID; }
@@ -565,32 +719,16 @@ int assemble_from_edges(const tgo_edges* e, const tgo_load_opts* opts, int64_t h
 
     // Full (uncapped) sorted rows for one direction: keys = neighbor << 32 | edge index.
     auto build_dir = [&](bool out_dir, std::vector<int64_t>& off, std::vector<uint64_t>& keys) {
-        const int32_t* own = out_dir ? e->src : e->dst;
-        const int32_t* nbr = out_dir ? e->dst : e->src;
-        std::vector<std::atomic<int64_t>> cnt(n + 1);
-        for (auto& c : cnt) c.store(0, std::memory_order_relaxed);
-        parallel_for(m, threads, [&](int64_t lo, int64_t hi, int) {
-            for (int64_t k = lo; k < hi; ++k) cnt[own[k]].fetch_add(1, std::memory_order_relaxed);
-        });
-        off.assign(n + 1, 0);
-        for (int64_t v = 0; v < n; ++v) off[v + 1] = off[v] + cnt[v].load(std::memory_order_relaxed);
-        for (int64_t v = 0; v < n; ++v) cnt[v].store(off[v], std::memory_order_relaxed);
-        keys.resize(m);
-        parallel_for(m, threads, [&](int64_t lo, int64_t hi, int) {
-            for (int64_t k = lo; k < hi; ++k) {
-                const int64_t p = cnt[own[k]].fetch_add(1, std::memory_order_relaxed);
-                keys[p] = (static_cast<uint64_t>(static_cast<uint32_t>(nbr[k])) << 32) | static_cast<uint64_t>(k);
-            }
-        });
-        parallel_dynamic(n, threads, 4096, [&](int64_t lo, int64_t hi) {
-            for (int64_t v = lo; v < hi; ++v) std::sort(keys.begin() + off[v], keys.begin() + off[v + 1]);
-        });
+        rows_by_owner(m, out_dir ? e->src : e->dst, out_dir ? e->dst : e->src, 0, n, threads, off, keys);
     };
     if (m >= (int64_t(1) << 32)) { err = "more than 2^32 edges per load"; return TGO_E_UNSUPPORTED; }
     std::vector<int64_t> off_o, off_i;
     std::vector<uint64_t> keys_o, keys_i;
+    clk.lap("checks");
     build_dir(true, off_o, keys_o);
+    clk.lap("out rows");
     build_dir(false, off_i, keys_i);
+    clk.lap("in rows");
     // Cap: keep the first `limit` entries of [OUT... | IN...] per row.
     std::vector<int64_t> ko(n + 1, 0), ki(n + 1, 0);
     int64_t truncated = 0;
@@ -622,8 +760,11 @@ int assemble_from_edges(const tgo_edges* e, const tgo_load_opts* opts, int64_t h
     fill(off_o, keys_o, ko, g.out);
     std::vector<uint64_t>().swap(keys_o);
     fill(off_i, keys_i, ki, g.in);
+    clk.lap("fill");
     relabel_by_degree(g, threads);
+    clk.lap("relabel");
     finish_views(g, threads);
+    clk.lap("views");
     return TGO_OK;
 }
 
@@ -654,28 +795,7 @@ int assemble_partition(const tgo_edges* e, int64_t n_global, int64_t lo, int64_t
     const bool cap = opts->apply_cap && opts->n_labels == 0 && opts->scope != TGO_SCOPE_BOTH_E;
     const int64_t limit = cap ? hard_limit : INT64_MAX;
     auto build_dir = [&](bool out_dir, std::vector<int64_t>& off, std::vector<uint64_t>& keys) {
-        const int32_t* own = out_dir ? e->src : e->dst;
-        const int32_t* nbr = out_dir ? e->dst : e->src;
-        std::vector<std::atomic<int64_t>> cnt(n + 1);
-        for (auto& c : cnt) c.store(0, std::memory_order_relaxed);
-        parallel_for(m, threads, [&](int64_t a, int64_t b, int) {
-            for (int64_t k = a; k < b; ++k)
-                if (own[k] >= lo && own[k] < hi) cnt[own[k] - lo].fetch_add(1, std::memory_order_relaxed);
-        });
-        off.assign(n + 1, 0);
-        for (int64_t v = 0; v < n; ++v) off[v + 1] = off[v] + cnt[v].load(std::memory_order_relaxed);
-        for (int64_t v = 0; v < n; ++v) cnt[v].store(off[v], std::memory_order_relaxed);
-        keys.resize(off[n]);
-        parallel_for(m, threads, [&](int64_t a, int64_t b, int) {
-            for (int64_t k = a; k < b; ++k) {
-                if (own[k] < lo || own[k] >= hi) continue;
-                const int64_t p = cnt[own[k] - lo].fetch_add(1, std::memory_order_relaxed);
-                keys[p] = (static_cast<uint64_t>(static_cast<uint32_t>(nbr[k])) << 32) | static_cast<uint64_t>(k);
-            }
-        });
-        parallel_dynamic(n, threads, 4096, [&](int64_t a, int64_t b) {
-            for (int64_t v = a; v < b; ++v) std::sort(keys.begin() + off[v], keys.begin() + off[v + 1]);
-        });
+        rows_by_owner(m, out_dir ? e->src : e->dst, out_dir ? e->dst : e->src, lo, hi, threads, off, keys);
     };
     if (m >= (int64_t(1) << 32)) { err = "more than 2^32 edges per load"; return TGO_E_UNSUPPORTED; }
     std::vector<int64_t> off_o, off_i;
