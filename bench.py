@@ -259,6 +259,12 @@ def config2_rows_leg(args, cores):
     vid = ((roots >> 5) + 1) << 5
     vid = (vid + (roots & 31)) << 3             # IDManager.constructId(i/32 + 1, i%32), pb = 5
     schema = Schema([{"type_id": label, "multiplicity": 0}], [])
+    # the host decoder once, for comparison (same rows, same work blocks; untimed for GTEPS)
+    os.environ["TGO_HOST_DECODE"] = "1"
+    t0 = time.perf_counter()
+    Engine(device=0, host_threads=cores).load_rows(rows, schema, L.SCOPE_BOTH_E, batch_rows=10 * 1024)
+    host_load_s = time.perf_counter() - t0
+    os.environ.pop("TGO_HOST_DECODE")
     t0 = time.perf_counter()
     eng = Engine(device=0, host_threads=cores).load_rows(rows, schema, L.SCOPE_BOTH_E, batch_rows=10 * 1024)
     load_s = time.perf_counter() - t0
@@ -278,6 +284,8 @@ def config2_rows_leg(args, cores):
             "rows": int(st["num_vertices"]), "entries": nent, "row_bytes": nbytes,
             "rows_encode_s": round(encode_s, 3),
             "load_rows_ms": round(load_s * 1e3, 1), "engine_load_ms": round(st["load_ms"], 1),
+            "decode": "device (decode.hip), work blocks of 10240 rows",
+            "load_rows_ms_host_decode": round(host_load_s * 1e3, 1),
             "decode_entries_per_s": round(nent / load_s, 1),
             "gteps_hmean": round(len(t_all) / float(np.sum(t_all / mR)) / 1e9, 4),
             "ms_per_root": round(float(t_all.mean()) * 1e3, 3)}

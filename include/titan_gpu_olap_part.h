@@ -126,11 +126,15 @@ int tgo_part_pr_step(tgo_ctx* ctx, const double* contrib_global, double* contrib
 int tgo_part_pr_end(tgo_ctx* ctx, double* pr_local);
 
 /* Device-resident level counts for the BFS / multi-source BFS steps: with dev_counts (a
- * device int64[2]) set, the steps that return counts {next queue length, its push entries}
- * write them there stream-ordered instead of synchronising into the host `counts` (which
- * may then be NULL); the caller all-reduces the device buffer and reads it once per level.
- * NULL restores host counts.  The SSSP steps always return host counts. */
+ * device int64[3]) set, the steps that return counts write {next queue length, its push
+ * entries} into [0..1] and this rank's own queue length into [2], stream-ordered, instead of
+ * synchronising into the host `counts` (which may then be NULL).  The caller all-reduces
+ * [0..1], reads the three values once per level and hands [2] back with
+ * tgo_part_set_local_qlen, so the next step needs no read of its own.  NULL restores host
+ * counts.  The SSSP steps always return host counts. */
 int tgo_part_device_counts(tgo_ctx* ctx, int64_t* dev_counts);
+/* The local queue length the caller read from dev_counts[2] after the last counting step. */
+int tgo_part_set_local_qlen(tgo_ctx* ctx, int64_t qlen);
 
 /* Rows of this rank holding any entry (the degree-grouped layout puts the others last). */
 int tgo_part_active_rows(tgo_ctx* ctx, int64_t* n_active);

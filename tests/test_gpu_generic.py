@@ -177,12 +177,20 @@ def test_components_over_vertex_cuts():
     assert np.array_equal(reorder(ids, cc, verts.ids), verts.property("cc")[0])
 
 
-def test_result_modes_other_than_none_are_rejected():
+def test_generic_program_write_back_is_rejected():
+    """PERSIST / LOCALTX write back the natively run programs' compute keys
+    (tests/test_gpu_writeback.py); a generic program's keys are not encoded: the job fails
+    (ExecutionException from get(), as a failing Fulgora job does)."""
     rows, vids, sd, npz = load_fixture("gotg")
     computer = GpuGraph(rows, sd).compute()
-    with pytest.raises(TitanException):
-        computer.resultMode(TitanGraphComputer.ResultMode.PERSIST)
+    computer.resultMode(TitanGraphComputer.ResultMode.PERSIST)
+    computer.program(ConnectedComponents())
+    with pytest.raises(ExecutionException):
+        computer.submit().get()
+    computer = GpuGraph(rows, sd).compute()
     computer.resultMode(TitanGraphComputer.ResultMode.NONE)
+    computer.program(ConnectedComponents())
+    computer.submit().get()
 
 
 def test_generic_program_failure_surfaces_as_execution_exception():

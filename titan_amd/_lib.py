@@ -136,7 +136,7 @@ EXPORTS = [
     # titan_gpu_olap_part.h (1-D vertex-partitioned multi-GPU)
     "tgo_load_partition", "tgo_part_layout", "tgo_load_partition_layout", "tgo_part_bfs_begin", "tgo_part_bfs_td", "tgo_part_bfs_claim", "tgo_part_bfs_bu",
     "tgo_part_bfs_end", "tgo_part_pr_begin", "tgo_part_pr_step", "tgo_part_pr_end", "tgo_rmat_partition",
-    "tgo_part_active_rows", "tgo_part_pr_blocked", "tgo_part_device_counts", "tgo_part_ms_pack_dev", "tgo_part_pr_step_cold", "tgo_part_pr_step_hot",
+    "tgo_part_active_rows", "tgo_part_pr_blocked", "tgo_part_device_counts", "tgo_part_set_local_qlen", "tgo_part_ms_pack_dev", "tgo_part_pr_step_cold", "tgo_part_pr_step_hot",
     "tgo_part_ms_begin", "tgo_part_ms_pull", "tgo_part_ms_push", "tgo_part_ms_settle", "tgo_part_ms_end",
     "tgo_part_ms_pack", "tgo_part_ms_settle_pairs",
     "tgo_part_ms_levels", "tgo_part_sssp_begin", "tgo_part_sssp_relax", "tgo_part_sssp_apply",
@@ -220,6 +220,7 @@ def load() -> C.CDLL:
         "tgo_part_pr_end": (C.c_int, [vp, C.POINTER(C.c_double)]),
         "tgo_part_active_rows": (C.c_int, [vp, _i64p]),
         "tgo_part_device_counts": (C.c_int, [vp, vp]),
+        "tgo_part_set_local_qlen": (C.c_int, [vp, C.c_int64]),
         "tgo_part_ms_pack_dev": (C.c_int, [vp, vp, C.c_int32, vp, vp]),
         "tgo_part_pr_blocked": (C.c_int, [vp, C.c_int32, C.c_int64, _i64p]),
         "tgo_part_pr_step_cold": (C.c_int, [vp, vp]),

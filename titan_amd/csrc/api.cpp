@@ -1242,12 +1242,22 @@ static int part_qlen_now(tgo_ctx* ctx, int64_t& q) {
 int tgo_part_device_counts(tgo_ctx* ctx, int64_t* dev_counts) {
     int rc = part_check(ctx);
     if (rc) return rc;
-    if (dev_counts && !ctx->part_qlen_dev) HIP_TRY(dev_alloc(ctx, ctx->part_qlen_dev, 1));
+    if (dev_counts) ctx->part_qlen_dev = dev_counts + 2;        // [2]: this rank's queue length
     if (!dev_counts && ctx->part_qlen_stale) {
         int64_t q;
         if ((rc = part_qlen_now(ctx, q))) return rc;
     }
     ctx->part_dcounts = dev_counts;
+    return TGO_OK;
+}
+
+int tgo_part_set_local_qlen(tgo_ctx* ctx, int64_t qlen) {
+    int rc = part_check(ctx);
+    if (rc) return rc;
+    if (!ctx->part_qlen_stale) return TGO_OK;               // nothing pending
+    if (qlen < 0 || qlen > ctx->g.n) return fail(ctx, TGO_E_INVALID, "local queue length out of range");
+    ctx->part_qlen = qlen;
+    ctx->part_qlen_stale = false;
     return TGO_OK;
 }
 

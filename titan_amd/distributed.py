@@ -144,8 +144,10 @@ class HipPartBackend:
         # place by the driver, read once per level) instead of a host array per call
         self.dc = None
         if device_counts:
-            self.dc = torch.zeros(2, dtype=torch.int64, device=self.device)
+            # [0..1] all-reduced counts, [2] this rank's queue length: one host read per level
+            self.dc = torch.zeros(3, dtype=torch.int64, device=self.device)
             engine.part_call("tgo_part_device_counts", self._vp(self.dc))
+            self.dc._tgo_backend = self
 
     def tensor(self, n, dtype):
         return torch.zeros(n, dtype=dtype, device=self.device)
@@ -292,7 +294,14 @@ def _scratch(backend, name, n, dtype):
 
 def _allreduce_counts(c, device, group):
     """Global sums of per-rank counters (frontier size / entries, reached, ...) over `group`.
-    A device tensor (HipPartBackend device_counts) is reduced in place: one read per level."""
+    A device tensor (HipPartBackend device_counts) is reduced in place and read once per level
+    together with the rank's own queue length, which goes back to the engine."""
+    be = getattr(c, "_tgo_backend", None)
+    if be is not None:
+        dist.all_reduce(c[:2], group=group)
+        v = c.cpu().numpy()
+        be.e.part_call("tgo_part_set_local_qlen", C.c_int64(int(v[2])))
+        return v[:2]
     t = c if isinstance(c, torch.Tensor) else torch.tensor(c, dtype=torch.int64, device=device)
     dist.all_reduce(t, group=group)
     return t.cpu().numpy()
