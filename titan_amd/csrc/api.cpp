@@ -54,6 +54,7 @@ struct tgo_ctx {
     int64_t pv_max_out = 0, pv_max_in = 0;   // largest OUT / IN list of a vertex cut
     // last finished program whose compute keys tgo_result_rows can encode (-1 = none)
     int res_kind = -1;
+    bool host_decode = false;                // TGO_HOST_DECODE latched for the load in progress
     DecodeScratch dec;                       // device row decoder buffers (decode.hip)
     bool res_empty = false;                  // it set no property (PageRank iterations(0))
     ResultSource res_src;
@@ -722,12 +723,14 @@ int tgo_load_rows(tgo_ctx* ctx, const tgo_rows* rows, const tgo_schema* schema, 
     const auto t0 = std::chrono::steady_clock::now();
     std::string err;
     // device decode (decode.hip) unless TGO_HOST_DECODE=1 picks the multi-threaded host decoder
-    const char* host = std::getenv("TGO_HOST_DECODE");
-    int rc = (host && std::atoi(host) != 0)
-                 ? decode_rows(ctx->staging, rows, schema, opts, ctx->opts.partition_bits, ctx->opts.hard_query_limit,
-                               threads_of(ctx), err)
-                 : decode_rows_device(ctx->staging, rows, schema, opts, ctx->opts.partition_bits,
-                                      ctx->opts.hard_query_limit, ctx->dec, ctx->stream, err);
+    // (latched at the first batch of a load, so one load never mixes the two)
+    if (!ctx->staging.active) {
+        const char* host = std::getenv("TGO_HOST_DECODE");
+        ctx->host_decode = host && std::atoi(host) != 0;
+    }
+    int rc = ctx->host_decode ? decode_rows(ctx->staging, rows, schema, opts, ctx->opts.partition_bits,
+                                       ctx->opts.hard_query_limit, threads_of(ctx), err)
+                         : stage_rows_raw(ctx->staging, rows, schema, opts, err);
     ctx->st.load_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     if (rc) { ctx->staging = RowStaging(); return fail(ctx, rc, err); }
     return TGO_OK;
@@ -740,8 +743,12 @@ int tgo_finish_load(tgo_ctx* ctx) {
     const auto t0 = std::chrono::steady_clock::now();
     HostGraph h;
     std::string err;
-    ctx->dec.release();                      // the decoder's batch buffers are done
-    int rc = assemble_from_rows(ctx->staging, h, threads_of(ctx), err);
+    // the staged work blocks, decoded in one device pass (decode.hip)
+    int rc = decode_staged_raw(ctx->staging, ctx->opts.partition_bits, ctx->opts.hard_query_limit, ctx->dec,
+                               ctx->stream, err);
+    ctx->dec.release();
+    if (rc) { ctx->staging = RowStaging(); return fail(ctx, rc, err); }
+    rc = assemble_from_rows(ctx->staging, h, threads_of(ctx), err);
     if (rc) return fail(ctx, rc, err);
     free_graph(ctx);
     rc = upload_graph(ctx, h);

@@ -118,15 +118,56 @@ void DecodeScratch::release() {
     cub_bytes = 0;
 }
 
-int decode_rows_device(RowStaging& st, const tgo_rows* rows, const tgo_schema* schema, const tgo_load_opts* opts,
-                       int pb, int64_t hard_limit, DecodeScratch& ds, hipStream_t stream, std::string& err) {
+// One work block of scanned rows: validated, then concatenated onto the raw staging (the
+// device decodes every block in one pass at tgo_finish_load — one upload and one launch
+// sequence instead of a round trip per block).
+int stage_rows_raw(RowStaging& st, const tgo_rows* rows, const tgo_schema* schema, const tgo_load_opts* opts,
+                   std::string& err) {
     HostPlan hp;
     if (int rc = build_plan(schema, opts, hp, err)) return rc;
-    const bool typed = opts->n_labels > 0;
-    const int64_t limit = (opts->apply_cap && !typed && opts->scope != TGO_SCOPE_BOTH_E) ? hard_limit : INT64_MAX;
-    const int64_t nrows = rows->nrows;
+    std::vector<uint8_t> pb;                              // the plan's bytes: batches must agree
+    auto put = [&](const void* p, size_t n) { pb.insert(pb.end(), static_cast<const uint8_t*>(p), static_cast<const uint8_t*>(p) + n); };
+    put(hp.label_bytes.data(), hp.label_bytes.size());
+    put(hp.key_ids.data(), hp.key_ids.size() * 8);
+    put(hp.key_dts.data(), hp.key_dts.size());
+    put(hp.dts.data(), hp.dts.size());
+    const bool first = !st.active;
     if (int rc = staging_begin(st, opts, err)) return rc;
+    if (first) { st.plan = hp; st.plan_bytes = pb; }
+    else if (pb != st.plan_bytes) { err = "tgo_schema differs between row batches"; return TGO_E_INVALID; }
+    const int64_t nrows = rows->nrows;
     if (nrows == 0) return TGO_OK;
+    const int64_t e0 = static_cast<int64_t>(st.raw_lv.size()), b0 = static_cast<int64_t>(st.raw_bytes.size());
+    const int64_t nent = rows->row_entry_begin[nrows] - rows->row_entry_begin[0];
+    const int64_t nbytes = rows->row_byte_begin[nrows] - rows->row_byte_begin[0];
+    if (nent < 0 || nbytes < 0) { err = "row offsets decrease"; return TGO_E_INVALID; }
+    st.raw_keys.insert(st.raw_keys.end(), rows->row_keys, rows->row_keys + nrows);
+    for (int64_t r = 1; r <= nrows; ++r) {
+        const int64_t de = rows->row_entry_begin[r] - rows->row_entry_begin[r - 1];
+        const int64_t db = rows->row_byte_begin[r] - rows->row_byte_begin[r - 1];
+        if (de < 0 || db < 0) { err = "row offsets decrease"; return TGO_E_INVALID; }
+        st.raw_eb.push_back(st.raw_eb.back() + de);
+        st.raw_bb.push_back(st.raw_bb.back() + db);
+    }
+    st.raw_lv.insert(st.raw_lv.end(), rows->entry_limit_valpos + rows->row_entry_begin[0],
+                     rows->entry_limit_valpos + rows->row_entry_begin[0] + nent);
+    st.raw_bytes.insert(st.raw_bytes.end(), rows->entry_bytes + rows->row_byte_begin[0],
+                        rows->entry_bytes + rows->row_byte_begin[0] + nbytes);
+    (void)e0; (void)b0;
+    return TGO_OK;
+}
+
+int decode_staged_raw(RowStaging& st, int pb, int64_t hard_limit, DecodeScratch& ds, hipStream_t stream,
+                      std::string& err) {
+    const HostPlan& hp = st.plan;
+    const tgo_load_opts* opts = &st.opts;
+    const bool typed = !st.labels.empty();
+    const int64_t limit = (opts->apply_cap && !typed && opts->scope != TGO_SCOPE_BOTH_E) ? hard_limit : INT64_MAX;
+    const int64_t nrows = static_cast<int64_t>(st.raw_keys.size());
+    if (nrows == 0) return TGO_OK;
+    const tgo_rows staged{nrows, st.raw_keys.data(), st.raw_eb.data(), st.raw_bb.data(), st.raw_bytes.data(),
+                          st.raw_lv.data()};
+    const tgo_rows* rows = &staged;
     const int64_t nent = rows->row_entry_begin[nrows], nbytes = rows->row_byte_begin[nrows];
     hipError_t e = hipSuccess;
 #define DEC_TRY(x) do { e = (x); if (e != hipSuccess) { err = hipGetErrorString(e); return e == hipErrorOutOfMemory ? TGO_E_OOM : TGO_E_HIP; } } while (0)
@@ -204,7 +245,19 @@ int decode_rows_device(RowStaging& st, const tgo_rows* rows, const tgo_schema* s
         return (eflag & 1) ? TGO_E_CODEC : TGO_E_UNSUPPORTED;
     }
     // append in row order, exactly as the host decoder stages them
+    std::vector<int64_t>().swap(st.raw_keys);
+    std::vector<int64_t>().swap(st.raw_lv);
+    std::vector<uint8_t>().swap(st.raw_bytes);
+    st.raw_eb.assign(1, 0);
+    st.raw_bb.assign(1, 0);
     st.truncated += static_cast<int64_t>(trunc);
+    int64_t kept = 0;
+    for (int64_t p = 0; p < total; ++p) kept += sel[p];
+    const size_t e0 = st.other.size();
+    st.other.resize(e0 + static_cast<size_t>(kept));
+    st.dir.resize(e0 + static_cast<size_t>(kept));
+    st.w.resize(e0 + static_cast<size_t>(kept));
+    size_t q = e0;
     for (int64_t r = 0; r < nrows; ++r) {
         if (status[r] == kRowSkipped) { ++st.skipped; continue; }
         if (status[r] == kRowGhost) { ++st.ghost; continue; }
@@ -213,11 +266,12 @@ int decode_rows_device(RowStaging& st, const tgo_rows* rows, const tgo_schema* s
         st.n_rep += rep[r];
         for (int64_t p = koff[r]; p < koff[r + 1]; ++p) {
             if (!sel[p]) continue;
-            st.other.push_back(other[p]);
-            st.dir.push_back(dir[p]);
-            st.w.push_back(w[p]);
+            st.other[q] = other[p];
+            st.dir[q] = dir[p];
+            st.w[q] = w[p];
+            ++q;
         }
-        st.row_begin.push_back(static_cast<int64_t>(st.other.size()));
+        st.row_begin.push_back(static_cast<int64_t>(q));
     }
     return TGO_OK;
 }

@@ -45,6 +45,15 @@ struct HostGraph {
     std::vector<uint8_t> pv_flags;   // row-order dense id -> is a vertex cut (empty if none)
 };
 
+// Owner of a codec PlanView (codec.hpp) built from tgo_schema + tgo_load_opts.
+struct HostPlan {
+    std::vector<uint8_t> label_bytes;   // LabelPlan records (opaque here; codec.hpp defines them)
+    std::vector<int64_t> key_ids;
+    std::vector<int8_t> key_dts;
+    std::vector<int8_t> dts;
+    int32_t n_labels = 0;
+    int64_t weight_key = 0;
+};
 // Staging of decoded rows between tgo_load_rows batches (decoded on arrival).
 struct RowStaging {
     std::vector<int64_t> vid;        // live vertices in row order
@@ -58,6 +67,12 @@ struct RowStaging {
     bool active = false;
     tgo_load_opts opts{};
     std::vector<int64_t> labels;
+    // device decode: the scan's work blocks are concatenated here (offsets rebased) and
+    // decoded in one device pass at tgo_finish_load
+    std::vector<int64_t> raw_keys, raw_eb{0}, raw_bb{0}, raw_lv;
+    std::vector<uint8_t> raw_bytes;
+    std::vector<uint8_t> plan_bytes;  // HostPlan of the first raw batch, serialised for comparison
+    HostPlan plan;
 };
 
 // Result write-back (results.hip): device arrays of the last finished program.
@@ -79,15 +94,6 @@ int encode_results(const ResultSource& src, const tgo_result_args* a, const int3
 // reference throw inside execute() (edge.value() on a missing key), i.e. TGO_E_PROGRAM.
 constexpr int32_t kMissingWeight = INT32_MIN;
 
-// Owner of a codec PlanView (codec.hpp) built from tgo_schema + tgo_load_opts.
-struct HostPlan {
-    std::vector<uint8_t> label_bytes;   // LabelPlan records (opaque here; codec.hpp defines them)
-    std::vector<int64_t> key_ids;
-    std::vector<int8_t> key_dts;
-    std::vector<int8_t> dts;
-    int32_t n_labels = 0;
-    int64_t weight_key = 0;
-};
 int build_plan(const tgo_schema* schema, const tgo_load_opts* opts, HostPlan& hp, std::string& err);
 // tgo_decode_edge_entry body (graph_build.cpp).
 int decode_one_entry(const tgo_schema* schema, const tgo_load_opts* opts, const uint8_t* entry,
@@ -124,9 +130,10 @@ struct DecodeScratch {
 // The same decode as decode_rows, on the device (decode.hip): the batch is uploaded, one
 // kernel classifies rows (key filter, ghost check, user-edge slice, cap) and one decodes
 // every kept entry; the staging arrays come back to the host.
-int decode_rows_device(RowStaging& st, const tgo_rows* rows, const tgo_schema* schema,
-                       const tgo_load_opts* opts, int pb, int64_t hard_limit, DecodeScratch& ds,
-                       hipStream_t stream, std::string& err);
+int stage_rows_raw(RowStaging& st, const tgo_rows* rows, const tgo_schema* schema, const tgo_load_opts* opts,
+                   std::string& err);
+int decode_staged_raw(RowStaging& st, int pb, int64_t hard_limit, DecodeScratch& ds, hipStream_t stream,
+                      std::string& err);
 int decode_rows(RowStaging& st, const tgo_rows* rows, const tgo_schema* schema,
                 const tgo_load_opts* opts, int pb, int64_t hard_limit, int threads,
                 std::string& err);
