@@ -894,7 +894,7 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
     HIP_TRY(hipMemsetAsync(s.ms_vis, 0, n * 8, st));
     HIP_TRY(hipMemsetAsync(s.ms_fr, 0, n * 8, st));
     s.ms_nplanes = 0;
-    HIP_TRY(k_ms_seed(s.ms_seeds, nseeds, s.ms_vis, s.ms_fr, st));
+    HIP_TRY(k_ms_seed(s.ms_seeds, nseeds, s.ms_vis, s.ms_fr, INT64_MAX, st));
     HIP_TRY(k_degree_i64(push, s.q[0], static_cast<int64_t>(uniq.size()), s.qdeg, st));
     const uint64_t full = nseeds == 64 ? ~0ULL : ((1ULL << nseeds) - 1ULL);
     const int64_t total = pull.nlists > 1 ? g.out.nnz + g.in.nnz : (a->scope == TGO_SCOPE_IN_E ? g.out.nnz : g.in.nnz);
@@ -1412,7 +1412,9 @@ int tgo_part_ms_begin(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, uint64
     s.ms_nplanes = 0;
     // seeds owned elsewhere stay -1 (skipped by the seed kernel; their bit is set by the owner)
     HIP_TRY(hipMemcpyAsync(s.ms_seeds, local.data(), nseeds * sizeof(int64_t), hipMemcpyHostToDevice, st));
-    HIP_TRY(k_ms_seed(s.ms_seeds, nseeds, s.ms_vis, fr_local, st));
+    // entry-less seeds stay out of the masks: the pull levels never write the masks' tail
+    // [n_active, n), which therefore stays zero in both alternating buffers
+    HIP_TRY(k_ms_seed(s.ms_seeds, nseeds, s.ms_vis, fr_local, g.n_active, st));
     ctx->part_cur = 0;
     ctx->part_queued = true;
     ctx->part_qlen = static_cast<int64_t>(uniq.size());
@@ -1442,8 +1444,8 @@ int tgo_part_ms_pull(tgo_ctx* ctx, int32_t level, const uint64_t* fr_global, uin
     if (level + 1 >= (1 << kLevelPlanes)) return fail(ctx, TGO_E_UNSUPPORTED, "multi-source BFS levels are < 65536");
     if ((rc = ms_planes_for(ctx, level + 1))) return rc;
     HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
-    // the pull writes every active row's mask; only the entry-less tail needs clearing
-    if (g.n > g.n_active) HIP_TRY(hipMemsetAsync(fr_next + g.n_active, 0, (g.n - g.n_active) * 8, st));
+    // the pull writes every active row's mask; the entry-less tail is zero already (no
+    // entry-less seed enters a mask, tgo_part_ms_begin)
     const int nxt = ctx->part_cur ^ 1;
     HIP_TRY(k_ms_pull(pull, push, g.n_active, full, fr_global, nullptr, s.ms_vis, fr_next, ms_planes(ctx), s.cnt,
                       level + 1, st));

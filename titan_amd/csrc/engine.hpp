@@ -385,7 +385,7 @@ hipError_t k_ds_mark_pack(uint64_t* rmark, int64_t words, int64_t wpr, int64_t n
 hipError_t k_ds_apply(const View& push, const int64_t* recv, int64_t npairs, int64_t* dist, uint64_t* pend, int32_t* qn,
                       int64_t* qdeg_n, Counters* cnt, int64_t thr, hipStream_t s);
 hipError_t k_unpermute_i64(const int64_t* in, const int32_t* perm, int64_t* out, int64_t n, hipStream_t s);
-hipError_t k_ms_seed(const int64_t* seeds, int nseeds, uint64_t* vis, uint64_t* fr, hipStream_t s);
+hipError_t k_ms_seed(const int64_t* seeds, int nseeds, uint64_t* vis, uint64_t* fr, int64_t fr_rows, hipStream_t s);
 hipError_t k_ms_pull(const View& pull, const View& push, int64_t n_active, uint64_t full, const uint64_t* fr,
                      const uint64_t* fbm, uint64_t* vis, uint64_t* nx, LevelPlanes lvl, Counters* cnt,
                      int32_t next_level, hipStream_t s);

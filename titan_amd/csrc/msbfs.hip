@@ -58,13 +58,16 @@ __device__ __forceinline__ void count_flush(Counters* cnt, unsigned long long nv
     }
 }
 
-__global__ void ms_seed(const int64_t* __restrict__ seeds, int nseeds, uint64_t* vis, uint64_t* fr) {
+// fr_rows: seeds at rows >= fr_rows (entry-less rows of a partitioned layout) are reached
+// but left out of the frontier mask — they have no entries to push or be pulled through,
+// and keeping them out leaves the masks' entry-less tail zero for the whole sweep.
+__global__ void ms_seed(const int64_t* __restrict__ seeds, int nseeds, uint64_t* vis, uint64_t* fr, int64_t fr_rows) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         for (int r = 0; r < nseeds; ++r) {
             const int64_t s = seeds[r];
             if (s < 0) continue;                 // partitioned: seed owned by another rank
             vis[s] |= 1ULL << r;
-            fr[s] |= 1ULL << r;
+            if (s < fr_rows) fr[s] |= 1ULL << r;
         }
     }
 }
@@ -334,8 +337,8 @@ inline int grid_for(int64_t work, int cap) {
 
 }  // namespace
 
-hipError_t k_ms_seed(const int64_t* seeds, int nseeds, uint64_t* vis, uint64_t* fr, hipStream_t s) {
-    ms_seed<<<1, 64, 0, s>>>(seeds, nseeds, vis, fr);
+hipError_t k_ms_seed(const int64_t* seeds, int nseeds, uint64_t* vis, uint64_t* fr, int64_t fr_rows, hipStream_t s) {
+    ms_seed<<<1, 64, 0, s>>>(seeds, nseeds, vis, fr, fr_rows);
     return hipGetLastError();
 }
 hipError_t k_ms_pull(const View& pull, const View& push, int64_t n_active, uint64_t full, const uint64_t* fr,

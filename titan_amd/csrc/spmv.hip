@@ -19,6 +19,7 @@
 // their per-(row, segment) sums land in partial[], and the hot pass adds them to each row.
 // Every sum has a fixed order: results are bitwise reproducible run to run.
 #include <algorithm>
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 #include "engine.hpp"
 
@@ -85,6 +86,14 @@ __device__ __forceinline__ int32_t stream_idx(const int32_t* p) { return __built
 
 constexpr int kPer = static_cast<int>(kTile / kBlock);   // entries per thread per tile (16)
 
+// LDS slot of tile entry k.  Thread-per-row reduces read s_val[row_start + j] across a wave;
+// with degree-grouped rows of a common length L those addresses stride by L doubles, which
+// for L a multiple of 16 lands every lane of a half-wave on the same few banks.  kPad inserts
+// one double after every 32, so the stride becomes L + L/32 (odd multiples spread the banks).
+template <bool kPad>
+__device__ __forceinline__ int lds_slot(int64_t k) { return kPad ? static_cast<int>(k + (k >> 5)) : static_cast<int>(k); }
+constexpr int kLdsPadded = static_cast<int>(kTile + kTile / 32);
+
 // Gather up to kTile messages of the entries [s0, s0+nnz) into registers: all kPer index
 // loads are issued first, then all kPer message loads, so every thread keeps kPer
 // independent gathers in flight (a dependent load per loop trip leaves the wave waiting
@@ -118,7 +127,7 @@ __device__ __forceinline__ void stage_tile(const int32_t* __restrict__ adj, int6
 
 // Reduce the runs [off[i], off[i+1]) of items i in [i0, i1) from the staged tile (base s0):
 // thread-per-run for many runs, wave-per-run with a fixed shuffle tree for few.
-template <class Op, class Emit>
+template <class Op, bool kPad = false, class Emit>
 __device__ __forceinline__ void reduce_runs(const int64_t* __restrict__ off, int64_t i0, int64_t i1, int64_t s0,
                                             const typename Op::T* s_val, const Emit& emit) {
     using T = typename Op::T;
@@ -126,7 +135,7 @@ __device__ __forceinline__ void reduce_runs(const int64_t* __restrict__ off, int
         for (int64_t i = i0 + threadIdx.x; i < i1; i += kBlock) {
             T sum = Op::zero();
             const int64_t e = off[i + 1] - s0;
-            for (int64_t k = off[i] - s0; k < e; ++k) sum = Op::add(sum, s_val[k]);
+            for (int64_t k = off[i] - s0; k < e; ++k) sum = Op::add(sum, s_val[lds_slot<kPad>(k)]);
             emit(i, sum);
         }
     } else {
@@ -134,7 +143,7 @@ __device__ __forceinline__ void reduce_runs(const int64_t* __restrict__ off, int
         for (int64_t i = i0 + wave; i < i1; i += kBlock / 64) {
             T sum = Op::zero();
             const int64_t e = off[i + 1] - s0;
-            for (int64_t k = off[i] - s0 + lane(); k < e; k += 64) sum = Op::add(sum, s_val[k]);
+            for (int64_t k = off[i] - s0 + lane(); k < e; k += 64) sum = Op::add(sum, s_val[lds_slot<kPad>(k)]);
             sum = wave_sum(sum);
             if (lane() == 0) emit(i, sum);
         }
@@ -155,10 +164,10 @@ __global__ void __launch_bounds__(kBlock) gather_short(const int64_t* __restrict
 
 // Packed, source-sorted tiles (pack_tiles): entry = source << kPackShift | slot.  The
 // gathered message goes back to its slot, so the row reduce is unchanged.
-template <class Fin>
+template <class Fin, bool kPad>
 __global__ void __launch_bounds__(kBlock) gather_short_packed(const int64_t* __restrict__ off,
         const int32_t* __restrict__ padj, const int64_t* __restrict__ blk, const double* __restrict__ msg, Fin fin) {
-    __shared__ double s_val[kTile];
+    __shared__ double s_val[kPad ? kLdsPadded : kTile];
     const int64_t r0 = blk[blockIdx.x], r1 = blk[blockIdx.x + 1];
     const int64_t s0 = off[r0];
     const int64_t nnz = off[r1] - s0;
@@ -175,10 +184,10 @@ __global__ void __launch_bounds__(kBlock) gather_short_packed(const int64_t* __r
         for (int j = 0; j < kPer; ++j) val[j] = v[j] >= 0 ? msg[v[j] >> kPackShift] : 0.0;
 #pragma unroll
         for (int j = 0; j < kPer; ++j)
-            if (v[j] >= 0) s_val[v[j] & ((1 << kPackShift) - 1)] = val[j];
+            if (v[j] >= 0) s_val[lds_slot<kPad>(v[j] & ((1 << kPackShift) - 1))] = val[j];
     }
     __syncthreads();
-    reduce_runs<PrOp>(off, r0, r1, s0, s_val, fin);
+    reduce_runs<PrOp, kPad>(off, r0, r1, s0, s_val, fin);
 }
 // A long row's chunk of packed entries: the chunk sum (source order, fixed).
 struct PackedOp {
@@ -228,12 +237,12 @@ __global__ void finalize_long(const int64_t* __restrict__ long_row, const int64_
 // dispatcher deals workgroups round-robin over the 8 XCDs) and takes that XCD's (b / 8)-th
 // cold block, so each XCD walks its own segments in order and its L2 holds the 2 MB slice of
 // messages the block gathers from.  Workgroups past the XCD's block count exit at once.
-template <bool kPacked>
+template <bool kPacked, bool kPad>
 __global__ void __launch_bounds__(kBlock) cold_gather(const int64_t* __restrict__ poff,
         const int32_t* __restrict__ cadj, const int64_t* __restrict__ bbeg, const int64_t* __restrict__ bend,
         const int32_t* __restrict__ xblk, const int32_t* __restrict__ bsrc, XcdBase xb, const double* __restrict__ msg,
         double* __restrict__ partial) {
-    __shared__ double s_val[kTile];
+    __shared__ double s_val[kPad ? kLdsPadded : kTile];
     const int x = static_cast<int>(blockIdx.x & 7);
     const int64_t j = xb.b[x] + (blockIdx.x >> 3);
     if (j >= xb.b[x + 1]) return;
@@ -254,12 +263,13 @@ __global__ void __launch_bounds__(kBlock) cold_gather(const int64_t* __restrict_
         for (int q = 0; q < kPer; ++q) val[q] = v[q] >= 0 ? seg_msg[v[q] >> kPackShift] : 0.0;
 #pragma unroll
         for (int q = 0; q < kPer; ++q)
-            if (v[q] >= 0) s_val[v[q] & ((1 << kPackShift) - 1)] = val[q];
+            if (v[q] >= 0) s_val[lds_slot<kPad>(v[q] & ((1 << kPackShift) - 1))] = val[q];
         __syncthreads();
+        reduce_runs<PrOp, kPad>(poff, p0, p1, s0, s_val, [&](int64_t p, double sum) { partial[p] = sum; });
     } else {
         stage_tile(cadj, s0, nnz, PrOp{msg}, s_val);
+        reduce_runs<PrOp>(poff, p0, p1, s0, s_val, [&](int64_t p, double sum) { partial[p] = sum; });
     }
-    reduce_runs<PrOp>(poff, p0, p1, s0, s_val, [&](int64_t p, double sum) { partial[p] = sum; });
 }
 
 // Per-row cold sums of the rows that own pieces: the pieces added in segment order.
@@ -330,15 +340,23 @@ hipError_t k_pr_iter(const DevCsr& in, const RowBlocks& rb, const double* contri
 }
 // Cold phase: the cold segments' partial sums, folded per row into csum (reads only the cold
 // sources [hot, n_src) of `contrib`).
+static bool lds_pad() {
+    static const bool on = [] { const char* e = std::getenv("TGO_PR_LDSPAD"); return !e || std::atoi(e) != 0; }();
+    return on;
+}
+
 hipError_t k_pr_cold_phase(const ColdBlocks& cb, const double* contrib, hipStream_t s) {
     if (cb.max_xcd_blocks > 0) {
         const unsigned g = static_cast<unsigned>(cb.max_xcd_blocks * 8);
-        if (cb.cpacked)
-            cold_gather<true><<<g, kBlock, 0, s>>>(cb.poff, cb.cadj, cb.bbeg, cb.bend, cb.xblk, cb.bsrc, cb.xbase, contrib,
-                                                   cb.partial);
+        if (cb.cpacked && lds_pad())
+            cold_gather<true, true><<<g, kBlock, 0, s>>>(cb.poff, cb.cadj, cb.bbeg, cb.bend, cb.xblk, cb.bsrc, cb.xbase,
+                                                         contrib, cb.partial);
+        else if (cb.cpacked)
+            cold_gather<true, false><<<g, kBlock, 0, s>>>(cb.poff, cb.cadj, cb.bbeg, cb.bend, cb.xblk, cb.bsrc, cb.xbase,
+                                                          contrib, cb.partial);
         else
-            cold_gather<false><<<g, kBlock, 0, s>>>(cb.poff, cb.cadj, cb.bbeg, cb.bend, cb.xblk, cb.bsrc, cb.xbase, contrib,
-                                                    cb.partial);
+            cold_gather<false, false><<<g, kBlock, 0, s>>>(cb.poff, cb.cadj, cb.bbeg, cb.bend, cb.xblk, cb.bsrc, cb.xbase,
+                                                           contrib, cb.partial);
     }
     int64_t g = (cb.n_crows + kBlock - 1) / kBlock;
     g = std::max<int64_t>(1, std::min<int64_t>(g, 65536));
@@ -353,8 +371,12 @@ hipError_t k_pr_hot_phase(const ColdBlocks& cb, const double* contrib, const dou
     if (!cb.packed) return run_gather(cb.hcsr, cb.rb_hot, PrOp{contrib}, fin, partial_long, s);
     const RowBlocks& rb = cb.rb_hot;
     if (rb.nblocks > 0) {
-        gather_short_packed<PrColdFinal><<<static_cast<unsigned>(rb.nblocks), kBlock, 0, s>>>(cb.hcsr.off, cb.hcsr.adj,
-                                                                                             rb.blk, contrib, fin);
+        if (lds_pad())
+            gather_short_packed<PrColdFinal, true><<<static_cast<unsigned>(rb.nblocks), kBlock, 0, s>>>(
+                cb.hcsr.off, cb.hcsr.adj, rb.blk, contrib, fin);
+        else
+            gather_short_packed<PrColdFinal, false><<<static_cast<unsigned>(rb.nblocks), kBlock, 0, s>>>(
+                cb.hcsr.off, cb.hcsr.adj, rb.blk, contrib, fin);
     }
     if (rb.nchunks > 0) {
         gather_chunks<PackedOp><<<static_cast<unsigned>(rb.nchunks), kBlock, 0, s>>>(cb.hcsr.adj, rb.chunk_beg,

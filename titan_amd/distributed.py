@@ -390,10 +390,14 @@ def distributed_msbfs(backend, seeds, max_depth: int, ms_alpha: float = 12.0, st
     world = dist.get_world_size(group)
     nseeds = len(seeds)
     dev = backend.device
-    fr = _scratch(backend, "ms_fr", backend.n_local, torch.int64)
-    frn = _scratch(backend, "ms_frn", backend.n_local, torch.int64)
-    frn.zero_()                  # rows without entries are never rewritten by the pull levels
-    fr_global = _scratch(backend, "ms_fr_global", backend.n_global, torch.int64)
+    # the owned masks are the rank's slice of a global buffer (two, alternating by level), so
+    # a dense level's all-gather is in place: no copy of the rank's own slice
+    lo, nl = backend.lo, backend.n_local
+    glob = [_scratch(backend, "ms_fr_global", backend.n_global, torch.int64),
+            _scratch(backend, "ms_frn_global", backend.n_global, torch.int64)]
+    fr, frn = glob[0][lo:lo + nl], glob[1][lo:lo + nl]
+    # no clearing: every level rewrites the active rows of the next mask, and the entry-less
+    # tail stays zero (tgo_part_ms_begin leaves entry-less seeds out of the masks)
     cand = _scratch(backend, "ms_cand", backend.n_global, torch.int64)     # all-zero between sparse levels
     send = recv = None
     total = _allreduce_counts([backend.total_entries, 0], dev, group)[0]
@@ -403,8 +407,8 @@ def distributed_msbfs(backend, seeds, max_depth: int, ms_alpha: float = 12.0, st
         if nf == 0:
             break
         if mf * ms_alpha > total:
-            dist.all_gather_into_tensor(fr_global, fr, group=group)
-            c = backend.ms_pull(level, fr_global, frn)
+            dist.all_gather_into_tensor(glob[0], fr, group=group)
+            c = backend.ms_pull(level, glob[0], frn)
         elif sparse_exchange:
             send = _scratch(backend, "pairs_send", 2 * backend.n_global, torch.int64)
             recv = _scratch(backend, "pairs_recv", 2 * backend.n_global, torch.int64)
@@ -424,6 +428,7 @@ def distributed_msbfs(backend, seeds, max_depth: int, ms_alpha: float = 12.0, st
             cand.zero_()
             c = backend.ms_settle(level, recv, world, frn)
         fr, frn = frn, fr
+        glob.reverse()
         nf, mf = _allreduce_counts(c, dev, group)
         levels += 1
     r, e = backend.ms_end(nseeds, stats)
