@@ -730,7 +730,7 @@ int tgo_load_rows(tgo_ctx* ctx, const tgo_rows* rows, const tgo_schema* schema, 
     }
     int rc = ctx->host_decode ? decode_rows(ctx->staging, rows, schema, opts, ctx->opts.partition_bits,
                                        ctx->opts.hard_query_limit, threads_of(ctx), err)
-                         : stage_rows_raw(ctx->staging, rows, schema, opts, err);
+                         : stage_rows_raw(ctx->staging, rows, schema, opts, ctx->dec, ctx->stream, err);
     ctx->st.load_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     if (rc) { ctx->staging = RowStaging(); return fail(ctx, rc, err); }
     return TGO_OK;

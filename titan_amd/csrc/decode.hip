@@ -106,23 +106,48 @@ __global__ void __launch_bounds__(kBlock) dec_entries(const int64_t* __restrict_
     }
 }
 
+// Compaction of the kept entries (sel) into staging order: the exclusive scan ks of sel
+// places entry p at ks[p]; a row's kept entries start at ks[koff[r]].
+__global__ void sel_to_i64(const uint8_t* __restrict__ sel, int64_t total, int64_t* __restrict__ out) {
+    for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p <= total; p += (int64_t)gridDim.x * blockDim.x)
+        out[p] = p < total ? sel[p] : 0;
+}
+__global__ void compact_entries(const uint8_t* __restrict__ sel, const int64_t* __restrict__ ks, int64_t total,
+                                const int64_t* __restrict__ other, const uint8_t* __restrict__ dir,
+                                const int32_t* __restrict__ w, int64_t* __restrict__ c_other,
+                                uint8_t* __restrict__ c_dir, int32_t* __restrict__ c_w) {
+    for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < total; p += (int64_t)gridDim.x * blockDim.x) {
+        if (!sel[p]) continue;
+        const int64_t q = ks[p];
+        c_other[q] = other[p];
+        c_dir[q] = dir[p];
+        c_w[q] = w[p];
+    }
+}
+__global__ void row_kept_begin(const int64_t* __restrict__ koff, const int64_t* __restrict__ ks, int64_t nrows,
+                               int64_t* __restrict__ out) {
+    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r <= nrows; r += (int64_t)gridDim.x * blockDim.x)
+        out[r] = ks[koff[r]];
+}
+
 }  // namespace
 
 void DecodeScratch::release() {
     keys.release(); eb.release(); bb.release(); bytes.release(); lv.release(); vid.release(); first.release();
     keep.release(); koff.release(); status.release(); rep.release(); other.release(); dir.release(); w.release();
     sel.release(); err.release(); trunc.release(); plan_labels.release(); plan_keys.release(); plan_kdts.release();
-    plan_dts.release();
+    plan_dts.release(); ks.release(); c_other.release(); c_dir.release(); c_w.release();
+    bytes_used = lv_used = 0;
     if (cub_tmp) (void)hipFree(cub_tmp);
     cub_tmp = nullptr;
     cub_bytes = 0;
 }
 
-// One work block of scanned rows: validated, then concatenated onto the raw staging (the
-// device decodes every block in one pass at tgo_finish_load — one upload and one launch
-// sequence instead of a round trip per block).
+// One work block of scanned rows: validated, its entry bytes and limit/valuePos words
+// appended to device buffers (no host copy), its keys and rebased row offsets to the host
+// staging; the device decodes every block in one pass at tgo_finish_load.
 int stage_rows_raw(RowStaging& st, const tgo_rows* rows, const tgo_schema* schema, const tgo_load_opts* opts,
-                   std::string& err) {
+                   DecodeScratch& ds, hipStream_t stream, std::string& err) {
     HostPlan hp;
     if (int rc = build_plan(schema, opts, hp, err)) return rc;
     std::vector<uint8_t> pb;                              // the plan's bytes: batches must agree
@@ -137,7 +162,7 @@ int stage_rows_raw(RowStaging& st, const tgo_rows* rows, const tgo_schema* schem
     else if (pb != st.plan_bytes) { err = "tgo_schema differs between row batches"; return TGO_E_INVALID; }
     const int64_t nrows = rows->nrows;
     if (nrows == 0) return TGO_OK;
-    const int64_t e0 = static_cast<int64_t>(st.raw_lv.size()), b0 = static_cast<int64_t>(st.raw_bytes.size());
+    if (first) ds.bytes_used = ds.lv_used = 0;
     const int64_t nent = rows->row_entry_begin[nrows] - rows->row_entry_begin[0];
     const int64_t nbytes = rows->row_byte_begin[nrows] - rows->row_byte_begin[0];
     if (nent < 0 || nbytes < 0) { err = "row offsets decrease"; return TGO_E_INVALID; }
@@ -149,11 +174,12 @@ int stage_rows_raw(RowStaging& st, const tgo_rows* rows, const tgo_schema* schem
         st.raw_eb.push_back(st.raw_eb.back() + de);
         st.raw_bb.push_back(st.raw_bb.back() + db);
     }
-    st.raw_lv.insert(st.raw_lv.end(), rows->entry_limit_valpos + rows->row_entry_begin[0],
-                     rows->entry_limit_valpos + rows->row_entry_begin[0] + nent);
-    st.raw_bytes.insert(st.raw_bytes.end(), rows->entry_bytes + rows->row_byte_begin[0],
-                        rows->entry_bytes + rows->row_byte_begin[0] + nbytes);
-    (void)e0; (void)b0;
+    hipError_t e = ds.lv.append(rows->entry_limit_valpos + rows->row_entry_begin[0], nent, ds.lv_used, stream);
+    if (e == hipSuccess) e = ds.bytes.append(rows->entry_bytes + rows->row_byte_begin[0], nbytes, ds.bytes_used, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);    // the caller may reuse its buffers on return
+    if (e != hipSuccess) { err = hipGetErrorString(e); return e == hipErrorOutOfMemory ? TGO_E_OOM : TGO_E_HIP; }
+    ds.lv_used += nent;
+    ds.bytes_used += nbytes;
     return TGO_OK;
 }
 
@@ -165,17 +191,15 @@ int decode_staged_raw(RowStaging& st, int pb, int64_t hard_limit, DecodeScratch&
     const int64_t limit = (opts->apply_cap && !typed && opts->scope != TGO_SCOPE_BOTH_E) ? hard_limit : INT64_MAX;
     const int64_t nrows = static_cast<int64_t>(st.raw_keys.size());
     if (nrows == 0) return TGO_OK;
-    const tgo_rows staged{nrows, st.raw_keys.data(), st.raw_eb.data(), st.raw_bb.data(), st.raw_bytes.data(),
-                          st.raw_lv.data()};
+    const tgo_rows staged{nrows, st.raw_keys.data(), st.raw_eb.data(), st.raw_bb.data(), nullptr, nullptr};
     const tgo_rows* rows = &staged;
     const int64_t nent = rows->row_entry_begin[nrows], nbytes = rows->row_byte_begin[nrows];
+    if (nent != ds.lv_used || nbytes != ds.bytes_used) { err = "raw staging out of step"; return TGO_E_STATE; }
     hipError_t e = hipSuccess;
 #define DEC_TRY(x) do { e = (x); if (e != hipSuccess) { err = hipGetErrorString(e); return e == hipErrorOutOfMemory ? TGO_E_OOM : TGO_E_HIP; } } while (0)
     for (DBuf<int64_t>* b : {&ds.keys, &ds.eb, &ds.bb, &ds.vid, &ds.first, &ds.keep, &ds.koff}) DEC_TRY(b->grow(nrows + 1));
     DEC_TRY(ds.status.grow(nrows + 1));
     DEC_TRY(ds.rep.grow(nrows + 1));
-    DEC_TRY(ds.bytes.grow(nbytes + 1));
-    DEC_TRY(ds.lv.grow(nent + 1));
     DEC_TRY(ds.err.grow(1));
     DEC_TRY(ds.trunc.grow(1));
     DEC_TRY(ds.plan_labels.grow(static_cast<int64_t>(hp.label_bytes.size()) + 1));
@@ -186,8 +210,6 @@ int decode_staged_raw(RowStaging& st, int pb, int64_t hard_limit, DecodeScratch&
     DEC_TRY(h2d(ds.keys.p, rows->row_keys, nrows * 8));
     DEC_TRY(h2d(ds.eb.p, rows->row_entry_begin, (nrows + 1) * 8));
     DEC_TRY(h2d(ds.bb.p, rows->row_byte_begin, (nrows + 1) * 8));
-    DEC_TRY(h2d(ds.bytes.p, rows->entry_bytes, nbytes));
-    DEC_TRY(h2d(ds.lv.p, rows->entry_limit_valpos, nent * 8));
     DEC_TRY(h2d(ds.plan_labels.p, hp.label_bytes.data(), hp.label_bytes.size()));
     DEC_TRY(h2d(ds.plan_keys.p, hp.key_ids.data(), hp.key_ids.size() * 8));
     DEC_TRY(h2d(ds.plan_kdts.p, hp.key_dts.data(), hp.key_dts.size()));
@@ -227,51 +249,55 @@ int decode_staged_raw(RowStaging& st, int pb, int64_t hard_limit, DecodeScratch&
                                                              ds.w.p, ds.sel.p, ds.err.p);
         DEC_TRY(hipGetLastError());
     }
-    std::vector<int64_t> other(total);
-    std::vector<uint8_t> dir(total), sel(total);
-    std::vector<int32_t> w(total);
+    // kept entries compacted on the device, in staging order
+    DEC_TRY(ds.ks.grow(total + 1));
+    DEC_TRY(ds.c_other.grow(total + 1));
+    DEC_TRY(ds.c_dir.grow(total + 1));
+    DEC_TRY(ds.c_w.grow(total + 1));
+    DEC_TRY(ds.keep.grow(std::max(nrows, total) + 1));
+    sel_to_i64<<<grid_for(total + 1), kBlock, 0, stream>>>(ds.sel.p, total, ds.keep.p);
+    DEC_TRY(hipGetLastError());
+    DEC_TRY(scan_exclusive_i64(ds.cub_tmp, ds.cub_bytes, ds.keep.p, ds.ks.p, total + 1, stream));
+    if (total > 0) {
+        compact_entries<<<grid_for(total), kBlock, 0, stream>>>(ds.sel.p, ds.ks.p, total, ds.other.p, ds.dir.p, ds.w.p,
+                                                                ds.c_other.p, ds.c_dir.p, ds.c_w.p);
+        DEC_TRY(hipGetLastError());
+    }
+    row_kept_begin<<<grid_for(nrows + 1), kBlock, 0, stream>>>(ds.koff.p, ds.ks.p, nrows, ds.keep.p);
+    DEC_TRY(hipGetLastError());
+    std::vector<int64_t> rk(nrows + 1);
     int32_t eflag = 0;
     DEC_TRY(hipMemcpyAsync(&eflag, ds.err.p, 4, hipMemcpyDeviceToHost, stream));
-    if (total) {
-        DEC_TRY(hipMemcpyAsync(other.data(), ds.other.p, total * 8, hipMemcpyDeviceToHost, stream));
-        DEC_TRY(hipMemcpyAsync(dir.data(), ds.dir.p, total, hipMemcpyDeviceToHost, stream));
-        DEC_TRY(hipMemcpyAsync(sel.data(), ds.sel.p, total, hipMemcpyDeviceToHost, stream));
-        DEC_TRY(hipMemcpyAsync(w.data(), ds.w.p, total * 4, hipMemcpyDeviceToHost, stream));
-    }
+    DEC_TRY(hipMemcpyAsync(rk.data(), ds.keep.p, (nrows + 1) * 8, hipMemcpyDeviceToHost, stream));
     DEC_TRY(hipStreamSynchronize(stream));
-#undef DEC_TRY
     if (eflag) {
         err = (eflag & 1) ? "malformed edge entry" : "inline property of a key missing from the schema";
         return (eflag & 1) ? TGO_E_CODEC : TGO_E_UNSUPPORTED;
     }
-    // append in row order, exactly as the host decoder stages them
-    std::vector<int64_t>().swap(st.raw_keys);
-    std::vector<int64_t>().swap(st.raw_lv);
-    std::vector<uint8_t>().swap(st.raw_bytes);
-    st.raw_eb.assign(1, 0);
-    st.raw_bb.assign(1, 0);
-    st.truncated += static_cast<int64_t>(trunc);
-    int64_t kept = 0;
-    for (int64_t p = 0; p < total; ++p) kept += sel[p];
+    const int64_t kept = rk[nrows];
     const size_t e0 = st.other.size();
     st.other.resize(e0 + static_cast<size_t>(kept));
     st.dir.resize(e0 + static_cast<size_t>(kept));
     st.w.resize(e0 + static_cast<size_t>(kept));
-    size_t q = e0;
+    if (kept > 0) {
+        DEC_TRY(hipMemcpyAsync(st.other.data() + e0, ds.c_other.p, kept * 8, hipMemcpyDeviceToHost, stream));
+        DEC_TRY(hipMemcpyAsync(st.dir.data() + e0, ds.c_dir.p, kept, hipMemcpyDeviceToHost, stream));
+        DEC_TRY(hipMemcpyAsync(st.w.data() + e0, ds.c_w.p, kept * 4, hipMemcpyDeviceToHost, stream));
+        DEC_TRY(hipStreamSynchronize(stream));
+    }
+#undef DEC_TRY
+    std::vector<int64_t>().swap(st.raw_keys);
+    st.raw_eb.assign(1, 0);
+    st.raw_bb.assign(1, 0);
+    st.truncated += static_cast<int64_t>(trunc);
+    // rows in order, exactly as the host decoder stages them
     for (int64_t r = 0; r < nrows; ++r) {
         if (status[r] == kRowSkipped) { ++st.skipped; continue; }
         if (status[r] == kRowGhost) { ++st.ghost; continue; }
         st.vid.push_back(vid[r]);
         st.rep.push_back(rep[r]);
         st.n_rep += rep[r];
-        for (int64_t p = koff[r]; p < koff[r + 1]; ++p) {
-            if (!sel[p]) continue;
-            st.other[q] = other[p];
-            st.dir[q] = dir[p];
-            st.w[q] = w[p];
-            ++q;
-        }
-        st.row_begin.push_back(static_cast<int64_t>(q));
+        st.row_begin.push_back(static_cast<int64_t>(e0) + rk[r + 1]);
     }
     return TGO_OK;
 }

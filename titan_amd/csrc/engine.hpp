@@ -69,8 +69,8 @@ struct RowStaging {
     std::vector<int64_t> labels;
     // device decode: the scan's work blocks are concatenated here (offsets rebased) and
     // decoded in one device pass at tgo_finish_load
-    std::vector<int64_t> raw_keys, raw_eb{0}, raw_bb{0}, raw_lv;
-    std::vector<uint8_t> raw_bytes;
+    // (entry bytes and limit/valuePos words go straight to the device: DecodeScratch)
+    std::vector<int64_t> raw_keys, raw_eb{0}, raw_bb{0};
     std::vector<uint8_t> plan_bytes;  // HostPlan of the first raw batch, serialised for comparison
     HostPlan plan;
 };
@@ -116,12 +116,30 @@ struct DBuf {
         return e;
     }
     void release() { if (p) (void)hipFree(p); p = nullptr; cap = 0; }
+    // host -> device append after the first `used` elements (a grow keeps them)
+    hipError_t append(const T* h, int64_t n, int64_t used, hipStream_t s) {
+        if (n <= 0) return hipSuccess;
+        if (used + n > cap) {
+            T* np = nullptr;
+            const int64_t c = std::max<int64_t>(2 * cap, used + n);
+            hipError_t e = hipMalloc(&np, static_cast<size_t>(c) * sizeof(T));
+            if (e != hipSuccess) return e;
+            if (used > 0) e = hipMemcpyAsync(np, p, static_cast<size_t>(used) * sizeof(T), hipMemcpyDeviceToDevice, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e != hipSuccess) { (void)hipFree(np); return e; }
+            if (p) (void)hipFree(p);
+            p = np;
+            cap = c;
+        }
+        return hipMemcpyAsync(p + used, h, static_cast<size_t>(n) * sizeof(T), hipMemcpyHostToDevice, s);
+    }
 };
 struct DecodeScratch {
-    DBuf<int64_t> keys, eb, bb, lv, vid, first, keep, koff, other, plan_keys;
-    DBuf<uint8_t> bytes, rep, dir, sel, plan_labels;
+    DBuf<int64_t> keys, eb, bb, lv, vid, first, keep, koff, other, plan_keys, ks, c_other;
+    DBuf<uint8_t> bytes, rep, dir, sel, plan_labels, c_dir;
     DBuf<int8_t> plan_kdts, plan_dts;
-    DBuf<int32_t> status, w, err;
+    DBuf<int32_t> status, w, err, c_w;
+    int64_t bytes_used = 0, lv_used = 0;   // raw work blocks staged on the device so far
     DBuf<unsigned long long> trunc;
     void* cub_tmp = nullptr;
     size_t cub_bytes = 0;
@@ -131,7 +149,7 @@ struct DecodeScratch {
 // kernel classifies rows (key filter, ghost check, user-edge slice, cap) and one decodes
 // every kept entry; the staging arrays come back to the host.
 int stage_rows_raw(RowStaging& st, const tgo_rows* rows, const tgo_schema* schema, const tgo_load_opts* opts,
-                   std::string& err);
+                   DecodeScratch& ds, hipStream_t stream, std::string& err);
 int decode_staged_raw(RowStaging& st, int pb, int64_t hard_limit, DecodeScratch& ds, hipStream_t stream,
                       std::string& err);
 int decode_rows(RowStaging& st, const tgo_rows* rows, const tgo_schema* schema,

@@ -189,6 +189,80 @@ __global__ void __launch_bounds__(kBlock) gather_short_packed(const int64_t* __r
     __syncthreads();
     reduce_runs<PrOp, kPad>(off, r0, r1, s0, s_val, fin);
 }
+// gather_short_packed with the row data prefetched.  A tile's chain of dependent memory
+// trips is blk -> off -> indices -> messages -> (barrier) -> row offsets -> csum/edge_count
+// -> stores; here every thread issues its first row's offsets, cold sum and edge count
+// together with the index loads, so the reduce starts from registers instead of waiting one
+// more memory latency after the barrier.  Thread-per-row tiles prefetch row r0 + tid;
+// wave-per-row tiles (<= 64 rows) prefetch row r0 + wave + 4 * lane, handed to the row's
+// wave by a shuffle.  Same sums in the same order as gather_short_packed: bitwise equal.
+template <bool kPad>
+__global__ void __launch_bounds__(kBlock) gather_hot_pf(const int64_t* __restrict__ off,
+        const int32_t* __restrict__ padj, const int64_t* __restrict__ blk, const double* __restrict__ msg,
+        PrColdFinal fin) {
+    __shared__ double s_val[kPad ? kLdsPadded : kTile];
+    const int64_t r0 = blk[blockIdx.x], r1 = blk[blockIdx.x + 1];
+    const bool tpr = r1 - r0 > 64;
+    const int wave = threadIdx.x >> 6;
+    const int64_t pr = tpr ? r0 + threadIdx.x : r0 + wave + 4 * lane();
+    int64_t pb = 0, pe = 0;
+    double pcs = 0.0, pec = 1.0;
+    if (pr < r1) {
+        pb = off[pr];
+        pe = off[pr + 1];
+        pcs = fin.csum[pr];
+        pec = __builtin_nontemporal_load(fin.f.edge_count + pr);
+    }
+    const int64_t s0 = off[r0];
+    const int64_t nnz = off[r1] - s0;
+    if (nnz > kTile) return;                          // long row: handled by chunks
+    {
+        int32_t v[kPer];
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+            const int64_t k = threadIdx.x + static_cast<int64_t>(j) * kBlock;
+            v[j] = k < nnz ? stream_idx(padj + s0 + k) : -1;
+        }
+        double val[kPer];
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) val[j] = v[j] >= 0 ? msg[v[j] >> kPackShift] : 0.0;
+#pragma unroll
+        for (int j = 0; j < kPer; ++j)
+            if (v[j] >= 0) s_val[lds_slot<kPad>(v[j] & ((1 << kPackShift) - 1))] = val[j];
+    }
+    __syncthreads();
+    const PrFinal& f = fin.f;
+    auto emit = [&](int64_t r, double sum, double cs, double ec) {
+        const double p = (f.alpha * (sum + cs)) + f.base;   // PrColdFinal: f(r, sum + csum[r])
+        if (f.pr) f.pr[r] = p;
+        f.contrib_next[r] = p / ec;
+    };
+    if (tpr) {
+        bool first = true;
+        for (int64_t i = r0 + threadIdx.x; i < r1; i += kBlock) {
+            int64_t b = pb, e = pe;
+            double cs = pcs, ec = pec;
+            if (!first) {
+                b = off[i]; e = off[i + 1]; cs = fin.csum[i]; ec = __builtin_nontemporal_load(f.edge_count + i);
+            }
+            first = false;
+            double sum = 0.0;
+            for (int64_t k = b - s0; k < e - s0; ++k) sum = sum + s_val[lds_slot<kPad>(k)];
+            emit(i, sum, cs, ec);
+        }
+    } else {
+        for (int t = 0; r0 + wave + 4 * t < r1; ++t) {
+            const int64_t i = r0 + wave + 4 * t;
+            const int64_t b = __shfl(pb, t, 64), e = __shfl(pe, t, 64);
+            const double cs = __shfl(pcs, t, 64), ec = __shfl(pec, t, 64);
+            double sum = 0.0;
+            for (int64_t k = b - s0 + lane(); k < e - s0; k += 64) sum = sum + s_val[lds_slot<kPad>(k)];
+            sum = wave_sum(sum);
+            if (lane() == 0) emit(i, sum, cs, ec);
+        }
+    }
+}
+
 // A long row's chunk of packed entries: the chunk sum (source order, fixed).
 struct PackedOp {
     using T = double;
@@ -237,7 +311,7 @@ __global__ void finalize_long(const int64_t* __restrict__ long_row, const int64_
 // dispatcher deals workgroups round-robin over the 8 XCDs) and takes that XCD's (b / 8)-th
 // cold block, so each XCD walks its own segments in order and its L2 holds the 2 MB slice of
 // messages the block gathers from.  Workgroups past the XCD's block count exit at once.
-template <bool kPacked, bool kPad>
+template <bool kPacked, bool kPad, bool kPf = false>
 __global__ void __launch_bounds__(kBlock) cold_gather(const int64_t* __restrict__ poff,
         const int32_t* __restrict__ cadj, const int64_t* __restrict__ bbeg, const int64_t* __restrict__ bend,
         const int32_t* __restrict__ xblk, const int32_t* __restrict__ bsrc, XcdBase xb, const double* __restrict__ msg,
@@ -248,6 +322,15 @@ __global__ void __launch_bounds__(kBlock) cold_gather(const int64_t* __restrict_
     if (j >= xb.b[x + 1]) return;
     const int64_t blk = xblk[j];
     const int64_t p0 = bbeg[blk], p1 = bend[blk];
+    // kPf: the first piece bounds of this thread (thread-per-piece) or of its wave's pieces
+    // (wave-per-piece, one per lane) load with the indices, as in gather_hot_pf
+    const bool tpr = p1 - p0 > 64;
+    const int wave = threadIdx.x >> 6;
+    int64_t pb = 0, pe = 0;
+    if (kPf) {
+        const int64_t pp = tpr ? p0 + threadIdx.x : p0 + wave + 4 * lane();
+        if (pp < p1) { pb = poff[pp]; pe = poff[pp + 1]; }
+    }
     const int64_t s0 = poff[p0];
     const int64_t nnz = poff[p1] - s0;                 // <= kTile by construction
     if (kPacked) {                                     // source-sorted tile: values go back to their slot
@@ -265,7 +348,28 @@ __global__ void __launch_bounds__(kBlock) cold_gather(const int64_t* __restrict_
         for (int q = 0; q < kPer; ++q)
             if (v[q] >= 0) s_val[lds_slot<kPad>(v[q] & ((1 << kPackShift) - 1))] = val[q];
         __syncthreads();
-        reduce_runs<PrOp, kPad>(poff, p0, p1, s0, s_val, [&](int64_t p, double sum) { partial[p] = sum; });
+        if (kPf && tpr) {
+            bool first = true;
+            for (int64_t i = p0 + threadIdx.x; i < p1; i += kBlock) {
+                int64_t b = pb, e = pe;
+                if (!first) { b = poff[i]; e = poff[i + 1]; }
+                first = false;
+                double sum = 0.0;
+                for (int64_t k = b - s0; k < e - s0; ++k) sum = sum + s_val[lds_slot<kPad>(k)];
+                partial[i] = sum;
+            }
+        } else if (kPf) {
+            for (int t = 0; p0 + wave + 4 * t < p1; ++t) {
+                const int64_t i = p0 + wave + 4 * t;
+                const int64_t b = __shfl(pb, t, 64), e = __shfl(pe, t, 64);
+                double sum = 0.0;
+                for (int64_t k = b - s0 + lane(); k < e - s0; k += 64) sum = sum + s_val[lds_slot<kPad>(k)];
+                sum = wave_sum(sum);
+                if (lane() == 0) partial[i] = sum;
+            }
+        } else {
+            reduce_runs<PrOp, kPad>(poff, p0, p1, s0, s_val, [&](int64_t p, double sum) { partial[p] = sum; });
+        }
     } else {
         stage_tile(cadj, s0, nnz, PrOp{msg}, s_val);
         reduce_runs<PrOp>(poff, p0, p1, s0, s_val, [&](int64_t p, double sum) { partial[p] = sum; });
@@ -345,10 +449,21 @@ static bool lds_pad() {
     return on;
 }
 
+static bool row_prefetch() {
+    static const bool on = [] { const char* e = std::getenv("TGO_PR_PF"); return !e || std::atoi(e) != 0; }();
+    return on;
+}
+
 hipError_t k_pr_cold_phase(const ColdBlocks& cb, const double* contrib, hipStream_t s) {
     if (cb.max_xcd_blocks > 0) {
         const unsigned g = static_cast<unsigned>(cb.max_xcd_blocks * 8);
-        if (cb.cpacked && lds_pad())
+        if (cb.cpacked && row_prefetch() && lds_pad())
+            cold_gather<true, true, true><<<g, kBlock, 0, s>>>(cb.poff, cb.cadj, cb.bbeg, cb.bend, cb.xblk, cb.bsrc,
+                                                               cb.xbase, contrib, cb.partial);
+        else if (cb.cpacked && row_prefetch())
+            cold_gather<true, false, true><<<g, kBlock, 0, s>>>(cb.poff, cb.cadj, cb.bbeg, cb.bend, cb.xblk, cb.bsrc,
+                                                                cb.xbase, contrib, cb.partial);
+        else if (cb.cpacked && lds_pad())
             cold_gather<true, true><<<g, kBlock, 0, s>>>(cb.poff, cb.cadj, cb.bbeg, cb.bend, cb.xblk, cb.bsrc, cb.xbase,
                                                          contrib, cb.partial);
         else if (cb.cpacked)
@@ -371,7 +486,13 @@ hipError_t k_pr_hot_phase(const ColdBlocks& cb, const double* contrib, const dou
     if (!cb.packed) return run_gather(cb.hcsr, cb.rb_hot, PrOp{contrib}, fin, partial_long, s);
     const RowBlocks& rb = cb.rb_hot;
     if (rb.nblocks > 0) {
-        if (lds_pad())
+        if (row_prefetch() && lds_pad())
+            gather_hot_pf<true><<<static_cast<unsigned>(rb.nblocks), kBlock, 0, s>>>(cb.hcsr.off, cb.hcsr.adj, rb.blk,
+                                                                                  contrib, fin);
+        else if (row_prefetch())
+            gather_hot_pf<false><<<static_cast<unsigned>(rb.nblocks), kBlock, 0, s>>>(cb.hcsr.off, cb.hcsr.adj, rb.blk,
+                                                                                   contrib, fin);
+        else if (lds_pad())
             gather_short_packed<PrColdFinal, true><<<static_cast<unsigned>(rb.nblocks), kBlock, 0, s>>>(
                 cb.hcsr.off, cb.hcsr.adj, rb.blk, contrib, fin);
         else
