@@ -75,6 +75,18 @@ struct PrColdFinal {
     PrFinal f; const double* csum;
     __device__ __forceinline__ void operator()(int64_t r, double sum) const { f(r, sum + csum[r]); }
 };
+// Fused fold: the row's cold pieces summed here, in segment order from 0.0 exactly as
+// cold_fold does (so the result is bitwise the same), instead of a separate pass + csum.
+struct PrFoldFinal {
+    PrFinal f; const uint32_t* cptr; const int32_t* cpid; const double* partial;
+    __device__ __forceinline__ double cold(int64_t r) const {
+        double s = 0.0;
+        const uint32_t e = cptr[r + 1];
+        for (uint32_t k = cptr[r]; k < e; ++k) s += partial[cpid[k]];
+        return s;
+    }
+    __device__ __forceinline__ void operator()(int64_t r, double sum) const { f(r, sum + cold(r)); }
+};
 struct WalkFinal {
     int32_t* next;
     __device__ __forceinline__ void operator()(int64_t r, uint32_t sum) const { next[r] = static_cast<int32_t>(sum); }
@@ -196,10 +208,12 @@ __global__ void __launch_bounds__(kBlock) gather_short_packed(const int64_t* __r
 // more memory latency after the barrier.  Thread-per-row tiles prefetch row r0 + tid;
 // wave-per-row tiles (<= 64 rows) prefetch row r0 + wave + 4 * lane, handed to the row's
 // wave by a shuffle.  Same sums in the same order as gather_short_packed: bitwise equal.
-template <bool kPad>
+// kFold: the cold sums come from the pieces (PrFoldFinal) — each thread folds its first
+// row's pieces in the prologue, overlapping the tile's index and message loads.
+template <bool kPad, bool kFold = false>
 __global__ void __launch_bounds__(kBlock) gather_hot_pf(const int64_t* __restrict__ off,
         const int32_t* __restrict__ padj, const int64_t* __restrict__ blk, const double* __restrict__ msg,
-        PrColdFinal fin) {
+        PrColdFinal fin, PrFoldFinal fold) {
     __shared__ double s_val[kPad ? kLdsPadded : kTile];
     const int64_t r0 = blk[blockIdx.x], r1 = blk[blockIdx.x + 1];
     const bool tpr = r1 - r0 > 64;
@@ -210,7 +224,7 @@ __global__ void __launch_bounds__(kBlock) gather_hot_pf(const int64_t* __restric
     if (pr < r1) {
         pb = off[pr];
         pe = off[pr + 1];
-        pcs = fin.csum[pr];
+        pcs = kFold ? fold.cold(pr) : fin.csum[pr];
         pec = __builtin_nontemporal_load(fin.f.edge_count + pr);
     }
     const int64_t s0 = off[r0];
@@ -243,7 +257,8 @@ __global__ void __launch_bounds__(kBlock) gather_hot_pf(const int64_t* __restric
             int64_t b = pb, e = pe;
             double cs = pcs, ec = pec;
             if (!first) {
-                b = off[i]; e = off[i + 1]; cs = fin.csum[i]; ec = __builtin_nontemporal_load(f.edge_count + i);
+                b = off[i]; e = off[i + 1]; cs = kFold ? fold.cold(i) : fin.csum[i];
+                ec = __builtin_nontemporal_load(f.edge_count + i);
             }
             first = false;
             double sum = 0.0;
@@ -453,6 +468,12 @@ static bool row_prefetch() {
     static const bool on = [] { const char* e = std::getenv("TGO_PR_PF"); return !e || std::atoi(e) != 0; }();
     return on;
 }
+// TGO_PR_FOLD: the hot pass folds the cold pieces itself (no cold_fold pass, no csum);
+// requires the prefetching hot kernel and packed hot tiles
+static bool fused_fold(const ColdBlocks& cb) {
+    static const bool on = [] { const char* e = std::getenv("TGO_PR_FOLD"); return e && std::atoi(e) != 0; }();
+    return on && row_prefetch() && cb.packed;
+}
 
 hipError_t k_pr_cold_phase(const ColdBlocks& cb, const double* contrib, hipStream_t s) {
     if (cb.max_xcd_blocks > 0) {
@@ -473,6 +494,7 @@ hipError_t k_pr_cold_phase(const ColdBlocks& cb, const double* contrib, hipStrea
             cold_gather<false, false><<<g, kBlock, 0, s>>>(cb.poff, cb.cadj, cb.bbeg, cb.bend, cb.xblk, cb.bsrc, cb.xbase,
                                                            contrib, cb.partial);
     }
+    if (fused_fold(cb)) return hipGetLastError();
     int64_t g = (cb.n_crows + kBlock - 1) / kBlock;
     g = std::max<int64_t>(1, std::min<int64_t>(g, 65536));
     cold_fold<<<static_cast<unsigned>(g), kBlock, 0, s>>>(cb.crow, cb.n_crows, cb.cptr, cb.cpid, cb.partial, cb.csum);
@@ -483,15 +505,19 @@ hipError_t k_pr_cold_phase(const ColdBlocks& cb, const double* contrib, hipStrea
 hipError_t k_pr_hot_phase(const ColdBlocks& cb, const double* contrib, const double* edge_count, double* pr,
                           double* contrib_next, double* partial_long, double alpha, double base, hipStream_t s) {
     const PrColdFinal fin{PrFinal{edge_count, pr, contrib_next, alpha, base}, cb.csum};
+    const PrFoldFinal fold{fin.f, cb.cptr, cb.cpid, cb.partial};
     if (!cb.packed) return run_gather(cb.hcsr, cb.rb_hot, PrOp{contrib}, fin, partial_long, s);
     const RowBlocks& rb = cb.rb_hot;
     if (rb.nblocks > 0) {
-        if (row_prefetch() && lds_pad())
+        if (fused_fold(cb))
+            gather_hot_pf<false, true><<<static_cast<unsigned>(rb.nblocks), kBlock, 0, s>>>(cb.hcsr.off, cb.hcsr.adj,
+                                                                                         rb.blk, contrib, fin, fold);
+        else if (row_prefetch() && lds_pad())
             gather_hot_pf<true><<<static_cast<unsigned>(rb.nblocks), kBlock, 0, s>>>(cb.hcsr.off, cb.hcsr.adj, rb.blk,
-                                                                                  contrib, fin);
+                                                                                  contrib, fin, fold);
         else if (row_prefetch())
             gather_hot_pf<false><<<static_cast<unsigned>(rb.nblocks), kBlock, 0, s>>>(cb.hcsr.off, cb.hcsr.adj, rb.blk,
-                                                                                   contrib, fin);
+                                                                                   contrib, fin, fold);
         else if (lds_pad())
             gather_short_packed<PrColdFinal, true><<<static_cast<unsigned>(rb.nblocks), kBlock, 0, s>>>(
                 cb.hcsr.off, cb.hcsr.adj, rb.blk, contrib, fin);
@@ -503,8 +529,12 @@ hipError_t k_pr_hot_phase(const ColdBlocks& cb, const double* contrib, const dou
         gather_chunks<PackedOp><<<static_cast<unsigned>(rb.nchunks), kBlock, 0, s>>>(cb.hcsr.adj, rb.chunk_beg,
                                                                                     rb.chunk_end, PackedOp{contrib},
                                                                                     partial_long);
-        finalize_long<PackedOp, PrColdFinal><<<grid_for(rb.nlong), kBlock, 0, s>>>(rb.long_row, rb.long_chunk, rb.nlong,
-                                                                                   partial_long, fin);
+        if (fused_fold(cb))
+            finalize_long<PackedOp, PrFoldFinal><<<grid_for(rb.nlong), kBlock, 0, s>>>(rb.long_row, rb.long_chunk,
+                                                                                       rb.nlong, partial_long, fold);
+        else
+            finalize_long<PackedOp, PrColdFinal><<<grid_for(rb.nlong), kBlock, 0, s>>>(rb.long_row, rb.long_chunk,
+                                                                                       rb.nlong, partial_long, fin);
     }
     return hipGetLastError();
 }
