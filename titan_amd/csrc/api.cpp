@@ -156,6 +156,9 @@ hipError_t upload_row_blocks(tgo_ctx* ctx, const std::vector<int64_t>& off, RowB
     if ((e = upload(ctx, rb.chunk_end, cend)) != hipSuccess) return e;
     if ((e = upload(ctx, rb.long_row, lrow)) != hipSuccess) return e;
     if ((e = upload(ctx, rb.long_chunk, lch)) != hipSuccess) return e;
+    std::vector<int64_t> desc(2 * blk.size());
+    for (size_t b = 0; b < blk.size(); ++b) { desc[2 * b] = blk[b]; desc[2 * b + 1] = off[blk[b]]; }
+    if ((e = upload(ctx, rb.bdesc, desc)) != hipSuccess) return e;
     return hipSuccess;
 }
 
@@ -189,6 +192,17 @@ int upload_cold_blocks(tgo_ctx* ctx, const std::vector<int64_t>& off, const std:
     HIP_TRY(upload(ctx, cb.bend, hc.bend));
     HIP_TRY(upload(ctx, cb.xblk, hc.xblk));
     HIP_TRY(upload(ctx, cb.bsrc, hc.bsrc));
+    {
+        std::vector<int64_t> desc(4 * hc.xblk.size());
+        for (size_t j = 0; j < hc.xblk.size(); ++j) {
+            const int32_t b = hc.xblk[j];
+            const int64_t p0 = hc.bbeg[b], p1 = hc.bend[b], s0 = hc.poff[p0], nnz = hc.poff[p1] - s0;
+            const int64_t src = hc.bsrc.empty() ? 0 : hc.bsrc[b];
+            if (nnz > kTile || src < 0) return fail(ctx, TGO_E_STATE, "cold block descriptor out of range");
+            desc[4 * j] = p0; desc[4 * j + 1] = p1; desc[4 * j + 2] = s0; desc[4 * j + 3] = (src << 16) | nnz;
+        }
+        HIP_TRY(upload(ctx, cb.cdesc, desc));
+    }
     cb.cpacked = hc.cpacked;
     HIP_TRY(dev_alloc(ctx, cb.partial, cb.npieces));
     HIP_TRY(dev_alloc(ctx, cb.csum, std::max<int64_t>(cb.n_rows, 1)));

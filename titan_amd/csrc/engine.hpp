@@ -190,6 +190,8 @@ struct RowBlocks {
     int64_t nlong = 0;          // long rows
     int64_t* long_row = nullptr;    // per long row: row id
     int64_t* long_chunk = nullptr;  // nlong+1: chunk index range
+    int64_t* bdesc = nullptr;   // 2*(nblocks+1): {first row, first entry} of every block — one
+                                // load per bound instead of blk -> off (gather_hot_pf)
     std::vector<int64_t> h_blk;
 };
 
@@ -221,6 +223,9 @@ struct ColdBlocks {
     int64_t* bend = nullptr;    // per cold block: end piece
     int32_t* xblk = nullptr;    // cold blocks in XCD-major launch order
     int32_t* bsrc = nullptr;    // per cold block: first source of its segment (packed tiles)
+    int64_t* cdesc = nullptr;   // 4 per launch slot j (xblk order): {first piece, end piece,
+                                // first entry, bsrc << 16 | entries} — one load for the chain
+                                // xblk -> bbeg/bend -> poff (cold_gather, prefetching form)
     bool cpacked = false;       // cold tiles source-sorted and packed relative to bsrc
     double* partial = nullptr;  // npieces, in piece order (streaming writes)
     double* csum = nullptr;     // n_rows: per-row cold sums (cold_fold; 0 for rows without pieces)

@@ -75,18 +75,6 @@ struct PrColdFinal {
     PrFinal f; const double* csum;
     __device__ __forceinline__ void operator()(int64_t r, double sum) const { f(r, sum + csum[r]); }
 };
-// Fused fold: the row's cold pieces summed here, in segment order from 0.0 exactly as
-// cold_fold does (so the result is bitwise the same), instead of a separate pass + csum.
-struct PrFoldFinal {
-    PrFinal f; const uint32_t* cptr; const int32_t* cpid; const double* partial;
-    __device__ __forceinline__ double cold(int64_t r) const {
-        double s = 0.0;
-        const uint32_t e = cptr[r + 1];
-        for (uint32_t k = cptr[r]; k < e; ++k) s += partial[cpid[k]];
-        return s;
-    }
-    __device__ __forceinline__ void operator()(int64_t r, double sum) const { f(r, sum + cold(r)); }
-};
 struct WalkFinal {
     int32_t* next;
     __device__ __forceinline__ void operator()(int64_t r, uint32_t sum) const { next[r] = static_cast<int32_t>(sum); }
@@ -98,13 +86,7 @@ __device__ __forceinline__ int32_t stream_idx(const int32_t* p) { return __built
 
 constexpr int kPer = static_cast<int>(kTile / kBlock);   // entries per thread per tile (16)
 
-// LDS slot of tile entry k.  Thread-per-row reduces read s_val[row_start + j] across a wave;
-// with degree-grouped rows of a common length L those addresses stride by L doubles, which
-// for L a multiple of 16 lands every lane of a half-wave on the same few banks.  kPad inserts
-// one double after every 32, so the stride becomes L + L/32 (odd multiples spread the banks).
-template <bool kPad>
-__device__ __forceinline__ int lds_slot(int64_t k) { return kPad ? static_cast<int>(k + (k >> 5)) : static_cast<int>(k); }
-constexpr int kLdsPadded = static_cast<int>(kTile + kTile / 32);
+
 
 // Gather up to kTile messages of the entries [s0, s0+nnz) into registers: all kPer index
 // loads are issued first, then all kPer message loads, so every thread keeps kPer
@@ -139,7 +121,7 @@ __device__ __forceinline__ void stage_tile(const int32_t* __restrict__ adj, int6
 
 // Reduce the runs [off[i], off[i+1]) of items i in [i0, i1) from the staged tile (base s0):
 // thread-per-run for many runs, wave-per-run with a fixed shuffle tree for few.
-template <class Op, bool kPad = false, class Emit>
+template <class Op, class Emit>
 __device__ __forceinline__ void reduce_runs(const int64_t* __restrict__ off, int64_t i0, int64_t i1, int64_t s0,
                                             const typename Op::T* s_val, const Emit& emit) {
     using T = typename Op::T;
@@ -147,7 +129,7 @@ __device__ __forceinline__ void reduce_runs(const int64_t* __restrict__ off, int
         for (int64_t i = i0 + threadIdx.x; i < i1; i += kBlock) {
             T sum = Op::zero();
             const int64_t e = off[i + 1] - s0;
-            for (int64_t k = off[i] - s0; k < e; ++k) sum = Op::add(sum, s_val[lds_slot<kPad>(k)]);
+            for (int64_t k = off[i] - s0; k < e; ++k) sum = Op::add(sum, s_val[k]);
             emit(i, sum);
         }
     } else {
@@ -155,7 +137,7 @@ __device__ __forceinline__ void reduce_runs(const int64_t* __restrict__ off, int
         for (int64_t i = i0 + wave; i < i1; i += kBlock / 64) {
             T sum = Op::zero();
             const int64_t e = off[i + 1] - s0;
-            for (int64_t k = off[i] - s0 + lane(); k < e; k += 64) sum = Op::add(sum, s_val[lds_slot<kPad>(k)]);
+            for (int64_t k = off[i] - s0 + lane(); k < e; k += 64) sum = Op::add(sum, s_val[k]);
             sum = wave_sum(sum);
             if (lane() == 0) emit(i, sum);
         }
@@ -176,10 +158,10 @@ __global__ void __launch_bounds__(kBlock) gather_short(const int64_t* __restrict
 
 // Packed, source-sorted tiles (pack_tiles): entry = source << kPackShift | slot.  The
 // gathered message goes back to its slot, so the row reduce is unchanged.
-template <class Fin, bool kPad>
+template <class Fin>
 __global__ void __launch_bounds__(kBlock) gather_short_packed(const int64_t* __restrict__ off,
         const int32_t* __restrict__ padj, const int64_t* __restrict__ blk, const double* __restrict__ msg, Fin fin) {
-    __shared__ double s_val[kPad ? kLdsPadded : kTile];
+    __shared__ double s_val[kTile];
     const int64_t r0 = blk[blockIdx.x], r1 = blk[blockIdx.x + 1];
     const int64_t s0 = off[r0];
     const int64_t nnz = off[r1] - s0;
@@ -196,10 +178,10 @@ __global__ void __launch_bounds__(kBlock) gather_short_packed(const int64_t* __r
         for (int j = 0; j < kPer; ++j) val[j] = v[j] >= 0 ? msg[v[j] >> kPackShift] : 0.0;
 #pragma unroll
         for (int j = 0; j < kPer; ++j)
-            if (v[j] >= 0) s_val[lds_slot<kPad>(v[j] & ((1 << kPackShift) - 1))] = val[j];
+            if (v[j] >= 0) s_val[v[j] & ((1 << kPackShift) - 1)] = val[j];
     }
     __syncthreads();
-    reduce_runs<PrOp, kPad>(off, r0, r1, s0, s_val, fin);
+    reduce_runs<PrOp>(off, r0, r1, s0, s_val, fin);
 }
 // gather_short_packed with the row data prefetched.  A tile's chain of dependent memory
 // trips is blk -> off -> indices -> messages -> (barrier) -> row offsets -> csum/edge_count
@@ -208,14 +190,13 @@ __global__ void __launch_bounds__(kBlock) gather_short_packed(const int64_t* __r
 // more memory latency after the barrier.  Thread-per-row tiles prefetch row r0 + tid;
 // wave-per-row tiles (<= 64 rows) prefetch row r0 + wave + 4 * lane, handed to the row's
 // wave by a shuffle.  Same sums in the same order as gather_short_packed: bitwise equal.
-// kFold: the cold sums come from the pieces (PrFoldFinal) — each thread folds its first
-// row's pieces in the prologue, overlapping the tile's index and message loads.
-template <bool kPad, bool kFold = false>
 __global__ void __launch_bounds__(kBlock) gather_hot_pf(const int64_t* __restrict__ off,
-        const int32_t* __restrict__ padj, const int64_t* __restrict__ blk, const double* __restrict__ msg,
-        PrColdFinal fin, PrFoldFinal fold) {
-    __shared__ double s_val[kPad ? kLdsPadded : kTile];
-    const int64_t r0 = blk[blockIdx.x], r1 = blk[blockIdx.x + 1];
+        const int32_t* __restrict__ padj, const int64_t* __restrict__ bdesc, const double* __restrict__ msg,
+        PrColdFinal fin) {
+    __shared__ double s_val[kTile];
+    // block bounds and first entries in one descriptor pair (RowBlocks::bdesc)
+    const int64_t r0 = bdesc[2 * blockIdx.x], s0 = bdesc[2 * blockIdx.x + 1];
+    const int64_t r1 = bdesc[2 * blockIdx.x + 2], nnz = bdesc[2 * blockIdx.x + 3] - s0;
     const bool tpr = r1 - r0 > 64;
     const int wave = threadIdx.x >> 6;
     const int64_t pr = tpr ? r0 + threadIdx.x : r0 + wave + 4 * lane();
@@ -224,11 +205,9 @@ __global__ void __launch_bounds__(kBlock) gather_hot_pf(const int64_t* __restric
     if (pr < r1) {
         pb = off[pr];
         pe = off[pr + 1];
-        pcs = kFold ? fold.cold(pr) : fin.csum[pr];
+        pcs = fin.csum[pr];
         pec = __builtin_nontemporal_load(fin.f.edge_count + pr);
     }
-    const int64_t s0 = off[r0];
-    const int64_t nnz = off[r1] - s0;
     if (nnz > kTile) return;                          // long row: handled by chunks
     {
         int32_t v[kPer];
@@ -242,7 +221,7 @@ __global__ void __launch_bounds__(kBlock) gather_hot_pf(const int64_t* __restric
         for (int j = 0; j < kPer; ++j) val[j] = v[j] >= 0 ? msg[v[j] >> kPackShift] : 0.0;
 #pragma unroll
         for (int j = 0; j < kPer; ++j)
-            if (v[j] >= 0) s_val[lds_slot<kPad>(v[j] & ((1 << kPackShift) - 1))] = val[j];
+            if (v[j] >= 0) s_val[v[j] & ((1 << kPackShift) - 1)] = val[j];
     }
     __syncthreads();
     const PrFinal& f = fin.f;
@@ -257,12 +236,12 @@ __global__ void __launch_bounds__(kBlock) gather_hot_pf(const int64_t* __restric
             int64_t b = pb, e = pe;
             double cs = pcs, ec = pec;
             if (!first) {
-                b = off[i]; e = off[i + 1]; cs = kFold ? fold.cold(i) : fin.csum[i];
+                b = off[i]; e = off[i + 1]; cs = fin.csum[i];
                 ec = __builtin_nontemporal_load(f.edge_count + i);
             }
             first = false;
             double sum = 0.0;
-            for (int64_t k = b - s0; k < e - s0; ++k) sum = sum + s_val[lds_slot<kPad>(k)];
+            for (int64_t k = b - s0; k < e - s0; ++k) sum = sum + s_val[k];
             emit(i, sum, cs, ec);
         }
     } else {
@@ -271,7 +250,7 @@ __global__ void __launch_bounds__(kBlock) gather_hot_pf(const int64_t* __restric
             const int64_t b = __shfl(pb, t, 64), e = __shfl(pe, t, 64);
             const double cs = __shfl(pcs, t, 64), ec = __shfl(pec, t, 64);
             double sum = 0.0;
-            for (int64_t k = b - s0 + lane(); k < e - s0; k += 64) sum = sum + s_val[lds_slot<kPad>(k)];
+            for (int64_t k = b - s0 + lane(); k < e - s0; k += 64) sum = sum + s_val[k];
             sum = wave_sum(sum);
             if (lane() == 0) emit(i, sum, cs, ec);
         }
@@ -326,17 +305,28 @@ __global__ void finalize_long(const int64_t* __restrict__ long_row, const int64_
 // dispatcher deals workgroups round-robin over the 8 XCDs) and takes that XCD's (b / 8)-th
 // cold block, so each XCD walks its own segments in order and its L2 holds the 2 MB slice of
 // messages the block gathers from.  Workgroups past the XCD's block count exit at once.
-template <bool kPacked, bool kPad, bool kPf = false>
+template <bool kPacked, bool kPf = false>
 __global__ void __launch_bounds__(kBlock) cold_gather(const int64_t* __restrict__ poff,
         const int32_t* __restrict__ cadj, const int64_t* __restrict__ bbeg, const int64_t* __restrict__ bend,
-        const int32_t* __restrict__ xblk, const int32_t* __restrict__ bsrc, XcdBase xb, const double* __restrict__ msg,
-        double* __restrict__ partial) {
-    __shared__ double s_val[kPad ? kLdsPadded : kTile];
+        const int32_t* __restrict__ xblk, const int32_t* __restrict__ bsrc, const int64_t* __restrict__ cdesc,
+        XcdBase xb, const double* __restrict__ msg, double* __restrict__ partial) {
+    __shared__ double s_val[kTile];
     const int x = static_cast<int>(blockIdx.x & 7);
     const int64_t j = xb.b[x] + (blockIdx.x >> 3);
     if (j >= xb.b[x + 1]) return;
-    const int64_t blk = xblk[j];
-    const int64_t p0 = bbeg[blk], p1 = bend[blk];
+    int64_t p0, p1, s0, nnz, src = 0;
+    if (kPf) {                                         // one descriptor (ColdBlocks::cdesc)
+        p0 = cdesc[4 * j]; p1 = cdesc[4 * j + 1]; s0 = cdesc[4 * j + 2];
+        const int64_t w = cdesc[4 * j + 3];
+        src = w >> 16;
+        nnz = w & 0xFFFF;
+    } else {
+        const int64_t blk = xblk[j];
+        p0 = bbeg[blk]; p1 = bend[blk];
+        s0 = poff[p0];
+        nnz = poff[p1] - s0;                           // <= kTile by construction
+        if (kPacked) src = bsrc[blk];
+    }
     // kPf: the first piece bounds of this thread (thread-per-piece) or of its wave's pieces
     // (wave-per-piece, one per lane) load with the indices, as in gather_hot_pf
     const bool tpr = p1 - p0 > 64;
@@ -346,10 +336,8 @@ __global__ void __launch_bounds__(kBlock) cold_gather(const int64_t* __restrict_
         const int64_t pp = tpr ? p0 + threadIdx.x : p0 + wave + 4 * lane();
         if (pp < p1) { pb = poff[pp]; pe = poff[pp + 1]; }
     }
-    const int64_t s0 = poff[p0];
-    const int64_t nnz = poff[p1] - s0;                 // <= kTile by construction
     if (kPacked) {                                     // source-sorted tile: values go back to their slot
-        const double* seg_msg = msg + bsrc[blk];
+        const double* seg_msg = msg + src;
         int32_t v[kPer];
 #pragma unroll
         for (int q = 0; q < kPer; ++q) {
@@ -361,7 +349,7 @@ __global__ void __launch_bounds__(kBlock) cold_gather(const int64_t* __restrict_
         for (int q = 0; q < kPer; ++q) val[q] = v[q] >= 0 ? seg_msg[v[q] >> kPackShift] : 0.0;
 #pragma unroll
         for (int q = 0; q < kPer; ++q)
-            if (v[q] >= 0) s_val[lds_slot<kPad>(v[q] & ((1 << kPackShift) - 1))] = val[q];
+            if (v[q] >= 0) s_val[v[q] & ((1 << kPackShift) - 1)] = val[q];
         __syncthreads();
         if (kPf && tpr) {
             bool first = true;
@@ -370,7 +358,7 @@ __global__ void __launch_bounds__(kBlock) cold_gather(const int64_t* __restrict_
                 if (!first) { b = poff[i]; e = poff[i + 1]; }
                 first = false;
                 double sum = 0.0;
-                for (int64_t k = b - s0; k < e - s0; ++k) sum = sum + s_val[lds_slot<kPad>(k)];
+                for (int64_t k = b - s0; k < e - s0; ++k) sum = sum + s_val[k];
                 partial[i] = sum;
             }
         } else if (kPf) {
@@ -378,12 +366,12 @@ __global__ void __launch_bounds__(kBlock) cold_gather(const int64_t* __restrict_
                 const int64_t i = p0 + wave + 4 * t;
                 const int64_t b = __shfl(pb, t, 64), e = __shfl(pe, t, 64);
                 double sum = 0.0;
-                for (int64_t k = b - s0 + lane(); k < e - s0; k += 64) sum = sum + s_val[lds_slot<kPad>(k)];
+                for (int64_t k = b - s0 + lane(); k < e - s0; k += 64) sum = sum + s_val[k];
                 sum = wave_sum(sum);
                 if (lane() == 0) partial[i] = sum;
             }
         } else {
-            reduce_runs<PrOp, kPad>(poff, p0, p1, s0, s_val, [&](int64_t p, double sum) { partial[p] = sum; });
+            reduce_runs<PrOp>(poff, p0, p1, s0, s_val, [&](int64_t p, double sum) { partial[p] = sum; });
         }
     } else {
         stage_tile(cadj, s0, nnz, PrOp{msg}, s_val);
@@ -459,42 +447,23 @@ hipError_t k_pr_iter(const DevCsr& in, const RowBlocks& rb, const double* contri
 }
 // Cold phase: the cold segments' partial sums, folded per row into csum (reads only the cold
 // sources [hot, n_src) of `contrib`).
-static bool lds_pad() {
-    static const bool on = [] { const char* e = std::getenv("TGO_PR_LDSPAD"); return !e || std::atoi(e) != 0; }();
-    return on;
-}
-
 static bool row_prefetch() {
     static const bool on = [] { const char* e = std::getenv("TGO_PR_PF"); return !e || std::atoi(e) != 0; }();
     return on;
 }
-// TGO_PR_FOLD: the hot pass folds the cold pieces itself (no cold_fold pass, no csum);
-// requires the prefetching hot kernel and packed hot tiles
-static bool fused_fold(const ColdBlocks& cb) {
-    static const bool on = [] { const char* e = std::getenv("TGO_PR_FOLD"); return e && std::atoi(e) != 0; }();
-    return on && row_prefetch() && cb.packed;
-}
-
 hipError_t k_pr_cold_phase(const ColdBlocks& cb, const double* contrib, hipStream_t s) {
     if (cb.max_xcd_blocks > 0) {
         const unsigned g = static_cast<unsigned>(cb.max_xcd_blocks * 8);
-        if (cb.cpacked && row_prefetch() && lds_pad())
-            cold_gather<true, true, true><<<g, kBlock, 0, s>>>(cb.poff, cb.cadj, cb.bbeg, cb.bend, cb.xblk, cb.bsrc,
-                                                               cb.xbase, contrib, cb.partial);
-        else if (cb.cpacked && row_prefetch())
-            cold_gather<true, false, true><<<g, kBlock, 0, s>>>(cb.poff, cb.cadj, cb.bbeg, cb.bend, cb.xblk, cb.bsrc,
-                                                                cb.xbase, contrib, cb.partial);
-        else if (cb.cpacked && lds_pad())
-            cold_gather<true, true><<<g, kBlock, 0, s>>>(cb.poff, cb.cadj, cb.bbeg, cb.bend, cb.xblk, cb.bsrc, cb.xbase,
+        if (cb.cpacked && row_prefetch())
+            cold_gather<true, true><<<g, kBlock, 0, s>>>(cb.poff, cb.cadj, cb.bbeg, cb.bend, cb.xblk, cb.bsrc, cb.cdesc, cb.xbase,
                                                          contrib, cb.partial);
         else if (cb.cpacked)
-            cold_gather<true, false><<<g, kBlock, 0, s>>>(cb.poff, cb.cadj, cb.bbeg, cb.bend, cb.xblk, cb.bsrc, cb.xbase,
+            cold_gather<true, false><<<g, kBlock, 0, s>>>(cb.poff, cb.cadj, cb.bbeg, cb.bend, cb.xblk, cb.bsrc, cb.cdesc, cb.xbase,
                                                           contrib, cb.partial);
         else
-            cold_gather<false, false><<<g, kBlock, 0, s>>>(cb.poff, cb.cadj, cb.bbeg, cb.bend, cb.xblk, cb.bsrc, cb.xbase,
+            cold_gather<false><<<g, kBlock, 0, s>>>(cb.poff, cb.cadj, cb.bbeg, cb.bend, cb.xblk, cb.bsrc, cb.cdesc, cb.xbase,
                                                            contrib, cb.partial);
     }
-    if (fused_fold(cb)) return hipGetLastError();
     int64_t g = (cb.n_crows + kBlock - 1) / kBlock;
     g = std::max<int64_t>(1, std::min<int64_t>(g, 65536));
     cold_fold<<<static_cast<unsigned>(g), kBlock, 0, s>>>(cb.crow, cb.n_crows, cb.cptr, cb.cpid, cb.partial, cb.csum);
@@ -505,35 +474,21 @@ hipError_t k_pr_cold_phase(const ColdBlocks& cb, const double* contrib, hipStrea
 hipError_t k_pr_hot_phase(const ColdBlocks& cb, const double* contrib, const double* edge_count, double* pr,
                           double* contrib_next, double* partial_long, double alpha, double base, hipStream_t s) {
     const PrColdFinal fin{PrFinal{edge_count, pr, contrib_next, alpha, base}, cb.csum};
-    const PrFoldFinal fold{fin.f, cb.cptr, cb.cpid, cb.partial};
     if (!cb.packed) return run_gather(cb.hcsr, cb.rb_hot, PrOp{contrib}, fin, partial_long, s);
     const RowBlocks& rb = cb.rb_hot;
     if (rb.nblocks > 0) {
-        if (fused_fold(cb))
-            gather_hot_pf<false, true><<<static_cast<unsigned>(rb.nblocks), kBlock, 0, s>>>(cb.hcsr.off, cb.hcsr.adj,
-                                                                                         rb.blk, contrib, fin, fold);
-        else if (row_prefetch() && lds_pad())
-            gather_hot_pf<true><<<static_cast<unsigned>(rb.nblocks), kBlock, 0, s>>>(cb.hcsr.off, cb.hcsr.adj, rb.blk,
-                                                                                  contrib, fin, fold);
-        else if (row_prefetch())
-            gather_hot_pf<false><<<static_cast<unsigned>(rb.nblocks), kBlock, 0, s>>>(cb.hcsr.off, cb.hcsr.adj, rb.blk,
-                                                                                   contrib, fin, fold);
-        else if (lds_pad())
-            gather_short_packed<PrColdFinal, true><<<static_cast<unsigned>(rb.nblocks), kBlock, 0, s>>>(
-                cb.hcsr.off, cb.hcsr.adj, rb.blk, contrib, fin);
+        if (row_prefetch())
+            gather_hot_pf<<<static_cast<unsigned>(rb.nblocks), kBlock, 0, s>>>(cb.hcsr.off, cb.hcsr.adj, rb.bdesc,
+                                                                             contrib, fin);
         else
-            gather_short_packed<PrColdFinal, false><<<static_cast<unsigned>(rb.nblocks), kBlock, 0, s>>>(
-                cb.hcsr.off, cb.hcsr.adj, rb.blk, contrib, fin);
+            gather_short_packed<PrColdFinal><<<static_cast<unsigned>(rb.nblocks), kBlock, 0, s>>>(cb.hcsr.off, cb.hcsr.adj,
+                                                                                             rb.blk, contrib, fin);
     }
     if (rb.nchunks > 0) {
         gather_chunks<PackedOp><<<static_cast<unsigned>(rb.nchunks), kBlock, 0, s>>>(cb.hcsr.adj, rb.chunk_beg,
                                                                                     rb.chunk_end, PackedOp{contrib},
                                                                                     partial_long);
-        if (fused_fold(cb))
-            finalize_long<PackedOp, PrFoldFinal><<<grid_for(rb.nlong), kBlock, 0, s>>>(rb.long_row, rb.long_chunk,
-                                                                                       rb.nlong, partial_long, fold);
-        else
-            finalize_long<PackedOp, PrColdFinal><<<grid_for(rb.nlong), kBlock, 0, s>>>(rb.long_row, rb.long_chunk,
+        finalize_long<PackedOp, PrColdFinal><<<grid_for(rb.nlong), kBlock, 0, s>>>(rb.long_row, rb.long_chunk,
                                                                                        rb.nlong, partial_long, fin);
     }
     return hipGetLastError();
