@@ -190,9 +190,6 @@ __global__ void __launch_bounds__(kBlock) gather_short_packed(const int64_t* __r
 // more memory latency after the barrier.  Thread-per-row tiles prefetch row r0 + tid;
 // wave-per-row tiles (<= 64 rows) prefetch row r0 + wave + 4 * lane, handed to the row's
 // wave by a shuffle.  Same sums in the same order as gather_short_packed: bitwise equal.
-// kNT: the per-row streams (offsets, cold sums, contributions out) bypass the caches with
-// non-temporal loads/stores, so they do not evict the L2-resident hot message head.
-template <bool kNT>
 __global__ void __launch_bounds__(kBlock) gather_hot_pf(const int64_t* __restrict__ off,
         const int32_t* __restrict__ padj, const int64_t* __restrict__ bdesc, const double* __restrict__ msg,
         PrColdFinal fin) {
@@ -206,9 +203,9 @@ __global__ void __launch_bounds__(kBlock) gather_hot_pf(const int64_t* __restric
     int64_t pb = 0, pe = 0;
     double pcs = 0.0, pec = 1.0;
     if (pr < r1) {
-        pb = kNT ? __builtin_nontemporal_load(off + pr) : off[pr];
-        pe = kNT ? __builtin_nontemporal_load(off + pr + 1) : off[pr + 1];
-        pcs = kNT ? __builtin_nontemporal_load(fin.csum + pr) : fin.csum[pr];
+        pb = off[pr];
+        pe = off[pr + 1];
+        pcs = fin.csum[pr];
         pec = __builtin_nontemporal_load(fin.f.edge_count + pr);
     }
     if (nnz > kTile) return;                          // long row: handled by chunks
@@ -231,8 +228,7 @@ __global__ void __launch_bounds__(kBlock) gather_hot_pf(const int64_t* __restric
     auto emit = [&](int64_t r, double sum, double cs, double ec) {
         const double p = (f.alpha * (sum + cs)) + f.base;   // PrColdFinal: f(r, sum + csum[r])
         if (f.pr) f.pr[r] = p;
-        if (kNT) __builtin_nontemporal_store(p / ec, f.contrib_next + r);
-        else f.contrib_next[r] = p / ec;
+        f.contrib_next[r] = p / ec;
     };
     if (tpr) {
         bool first = true;
@@ -313,7 +309,7 @@ template <bool kPacked, bool kPf = false>
 __global__ void __launch_bounds__(kBlock) cold_gather(const int64_t* __restrict__ poff,
         const int32_t* __restrict__ cadj, const int64_t* __restrict__ bbeg, const int64_t* __restrict__ bend,
         const int32_t* __restrict__ xblk, const int32_t* __restrict__ bsrc, const int64_t* __restrict__ cdesc,
-        XcdBase xb, const double* __restrict__ msg, double* __restrict__ partial, bool nt = false) {
+        XcdBase xb, const double* __restrict__ msg, double* __restrict__ partial) {
     __shared__ double s_val[kTile];
     const int x = static_cast<int>(blockIdx.x & 7);
     const int64_t j = xb.b[x] + (blockIdx.x >> 3);
@@ -363,8 +359,7 @@ __global__ void __launch_bounds__(kBlock) cold_gather(const int64_t* __restrict_
                 first = false;
                 double sum = 0.0;
                 for (int64_t k = b - s0; k < e - s0; ++k) sum = sum + s_val[k];
-                if (nt) __builtin_nontemporal_store(sum, partial + i);
-                else partial[i] = sum;
+                partial[i] = sum;
             }
         } else if (kPf) {
             for (int t = 0; p0 + wave + 4 * t < p1; ++t) {
@@ -373,10 +368,7 @@ __global__ void __launch_bounds__(kBlock) cold_gather(const int64_t* __restrict_
                 double sum = 0.0;
                 for (int64_t k = b - s0 + lane(); k < e - s0; k += 64) sum = sum + s_val[k];
                 sum = wave_sum(sum);
-                if (lane() == 0) {
-                    if (nt) __builtin_nontemporal_store(sum, partial + i);
-                    else partial[i] = sum;
-                }
+                if (lane() == 0) partial[i] = sum;
             }
         } else {
             reduce_runs<PrOp>(poff, p0, p1, s0, s_val, [&](int64_t p, double sum) { partial[p] = sum; });
@@ -455,10 +447,6 @@ hipError_t k_pr_iter(const DevCsr& in, const RowBlocks& rb, const double* contri
 }
 // Cold phase: the cold segments' partial sums, folded per row into csum (reads only the cold
 // sources [hot, n_src) of `contrib`).
-static bool nt_streams() {
-    static const bool on = [] { const char* e = std::getenv("TGO_PR_NT"); return !e || std::atoi(e) != 0; }();
-    return on;
-}
 static bool row_prefetch() {
     static const bool on = [] { const char* e = std::getenv("TGO_PR_PF"); return !e || std::atoi(e) != 0; }();
     return on;
@@ -468,7 +456,7 @@ hipError_t k_pr_cold_phase(const ColdBlocks& cb, const double* contrib, hipStrea
         const unsigned g = static_cast<unsigned>(cb.max_xcd_blocks * 8);
         if (cb.cpacked && row_prefetch())
             cold_gather<true, true><<<g, kBlock, 0, s>>>(cb.poff, cb.cadj, cb.bbeg, cb.bend, cb.xblk, cb.bsrc, cb.cdesc, cb.xbase,
-                                                         contrib, cb.partial, nt_streams());
+                                                         contrib, cb.partial);
         else if (cb.cpacked)
             cold_gather<true, false><<<g, kBlock, 0, s>>>(cb.poff, cb.cadj, cb.bbeg, cb.bend, cb.xblk, cb.bsrc, cb.cdesc, cb.xbase,
                                                           contrib, cb.partial);
@@ -489,11 +477,8 @@ hipError_t k_pr_hot_phase(const ColdBlocks& cb, const double* contrib, const dou
     if (!cb.packed) return run_gather(cb.hcsr, cb.rb_hot, PrOp{contrib}, fin, partial_long, s);
     const RowBlocks& rb = cb.rb_hot;
     if (rb.nblocks > 0) {
-        if (row_prefetch() && nt_streams())
-            gather_hot_pf<true><<<static_cast<unsigned>(rb.nblocks), kBlock, 0, s>>>(cb.hcsr.off, cb.hcsr.adj, rb.bdesc,
-                                                                                   contrib, fin);
-        else if (row_prefetch())
-            gather_hot_pf<false><<<static_cast<unsigned>(rb.nblocks), kBlock, 0, s>>>(cb.hcsr.off, cb.hcsr.adj, rb.bdesc,
+        if (row_prefetch())
+            gather_hot_pf<<<static_cast<unsigned>(rb.nblocks), kBlock, 0, s>>>(cb.hcsr.off, cb.hcsr.adj, rb.bdesc,
                                                                                     contrib, fin);
         else
             gather_short_packed<PrColdFinal><<<static_cast<unsigned>(rb.nblocks), kBlock, 0, s>>>(cb.hcsr.off, cb.hcsr.adj,
