@@ -89,6 +89,17 @@ int tgo_part_ms_pack(tgo_ctx* ctx, uint64_t* cand_global, int32_t nranks, int64_
 int tgo_part_ms_pack_dev(tgo_ctx* ctx, uint64_t* cand_global, int32_t nranks, int64_t* send, int64_t* send_elems_dev);
 int tgo_part_ms_settle_pairs(tgo_ctx* ctx, int32_t level, const int64_t* recv, const int64_t* recv_counts,
                              int32_t nslices, uint64_t* fr_next, int64_t* counts);
+/* Fixed-capacity form of the sparse exchange, for levels whose frontier is small: owner r's
+ * slot of `send` is 2 * (cap + 1) int64 — a header pair (count, 0) then up to cap (owner-
+ * local id, mask) pairs — so the caller's all-to-all has equal splits of 2 * (cap + 1)
+ * elements known before the level (no all-to-all of split sizes, no host read of them).
+ * cap must bound every owner's pair count: the level's global frontier entries (each pair
+ * needs a pushed entry of this rank) capped at n_local.  A count over cap fails the sweep
+ * at tgo_part_ms_end with TGO_E_STATE.  tgo_part_ms_settle_fixed ORs the received slots
+ * (nslices of them, same cap) into fr_next and settles like tgo_part_ms_settle_pairs. */
+int tgo_part_ms_pack_fixed(tgo_ctx* ctx, uint64_t* cand_global, int32_t nranks, int64_t cap, int64_t* send);
+int tgo_part_ms_settle_fixed(tgo_ctx* ctx, int32_t level, const int64_t* recv, int32_t nslices, int64_t cap,
+                             uint64_t* fr_next, int64_t* counts);
 /* reached / entries: per seed, over this rank's vertices (NULL to skip). */
 int tgo_part_ms_end(tgo_ctx* ctx, int64_t* reached, int64_t* entries);
 /* Source `source`'s distances of the owned vertices (TGO_DIST_ABSENT = unreached). */

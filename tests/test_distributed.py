@@ -255,6 +255,34 @@ class NumpyPartBackend:
             p += len(nz)
         return counts
 
+    def ms_pack_fixed(self, cand, send, nranks, cap):
+        """tgo_part_ms_pack_fixed: owner r's slot = header (count, 0) + up to cap pairs."""
+        self.n_fixed = getattr(self, "n_fixed", 0) + 1
+        counts = self.ms_pack(cand, self._fixed_tmp(send), nranks)
+        tmp = self._fixed_tmp(send).numpy()
+        s = send.numpy()
+        p = 0
+        for r in range(nranks):
+            assert counts[r] <= cap                  # the driver's bound: pairs <= frontier entries
+            base = 2 * r * (cap + 1)
+            s[base], s[base + 1] = counts[r], 0
+            s[base + 2:base + 2 + 2 * counts[r]] = tmp[2 * p:2 * (p + counts[r])]
+            p += counts[r]
+
+    def _fixed_tmp(self, like):
+        if getattr(self, "_ftmp", None) is None or self._ftmp.numel() < like.numel():
+            self._ftmp = torch.zeros(like.numel(), dtype=torch.int64)
+        return self._ftmp
+
+    def ms_settle_fixed(self, level, recv, nslices, cap, fr_next):
+        r = recv.numpy()
+        acc = np.zeros(self.n_local, np.uint64)
+        for s in range(nslices):
+            base = 2 * s * (cap + 1)
+            k = int(r[base])
+            np.bitwise_or.at(acc, r[base + 2:base + 2 + 2 * k:2], r[base + 3:base + 3 + 2 * k:2].view(np.uint64))
+        return self._ms_fresh(level, acc, fr_next)
+
     def ms_settle_pairs(self, level, recv, recv_counts, fr_next):
         r = recv.numpy()
         k = int(np.sum(recv_counts))
@@ -341,9 +369,11 @@ def _worker(rank, world, port, scale, roots, out_q, alpha):
         res["bfs"].append(torch.cat(full).numpy())
         res["reached"].append(reached)
     from titan_amd.distributed import distributed_msbfs
-    # mixed, always push (packed pairs and dense slices), always pull
-    for ms_alpha, sparse in ((12.0, True), (1e9, True), (1e9, False), (1e-9, True)):
-        r, e, _ = distributed_msbfs(be, roots, n, ms_alpha=ms_alpha, sparse_exchange=sparse)
+    # mixed, always push (fixed-capacity pairs, sized pairs, dense slices), always pull
+    for ms_alpha, sparse, fixed in ((12.0, True, None), (1e9, True, None), (1e9, True, 0), (1e9, False, None),
+                                    (1e-9, True, None)):
+        r, e, _ = distributed_msbfs(be, roots, n, ms_alpha=ms_alpha, sparse_exchange=sparse,
+                                    fixed_exchange_bytes=fixed)
         lv = []
         for i in range(len(roots)):
             loc = np.where(be.mslvl[:, i] >= 0, be.mslvl[:, i], ABSENT)
@@ -351,6 +381,7 @@ def _worker(rank, world, port, scale, roots, out_q, alpha):
             dist.all_gather(full, torch.from_numpy(loc.astype(np.int64)))
             lv.append(torch.cat(full).numpy())
         res.setdefault("ms", []).append((lv, r))
+    res["n_fixed"] = getattr(be, "n_fixed", 0)
     for hot in (0, 16):             # plain rank-major all-gather; blocked hot-first layout
         be.pr_hot = hot
         pr = distributed_pagerank(be, 0.85, n, 10)
@@ -387,6 +418,7 @@ def test_distributed_bfs_and_pagerank_match_oracle(world, alpha):
         od, _ = og.shortest_distance(int(ids[r]), n, 2)
         assert np.array_equal(d, od)
         assert reached[0] == int((od != ABSENT).sum())
+    assert res["n_fixed"] > 0                    # the fixed-capacity exchange ran
     for lv, reached in res["ms"]:
         for i, r in enumerate(roots):
             od, _ = og.shortest_distance(int(ids[r]), n, 2)

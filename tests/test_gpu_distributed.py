@@ -76,8 +76,8 @@ def run_msbfs(backends, seeds, max_depth, ms_alpha=12.0, sparse=False):
     frn = [b.tensor(nl, torch.int64) for b in backends]
     fg = [b.tensor(n, torch.int64) for b in backends]
     cand = [b.tensor(n, torch.int64) for b in backends]
-    recv = [b.tensor(2 * n if sparse else n, torch.int64) for b in backends]
-    send = [b.tensor(2 * n, torch.int64) for b in backends] if sparse else None
+    recv = [b.tensor(2 * n + 2 * world if sparse else n, torch.int64) for b in backends]
+    send = [b.tensor(2 * n + 2 * world, torch.int64) for b in backends] if sparse else None
     total = sum(b.total_entries for b in backends)
     nf, mf = sum(b.ms_begin(seeds, fr_[i]) for i, b in enumerate(backends))
     for level in range(max_depth):
@@ -92,6 +92,19 @@ def run_msbfs(backends, seeds, max_depth, ms_alpha=12.0, sparse=False):
             torch.cuda.synchronize()
             for i, b in enumerate(backends):
                 cs.append(b.ms_pull(level, fg[i], frn[i]))
+        elif sparse == "fixed":         # tgo_part_ms_pack_fixed / ms_settle_fixed, equal splits
+            cap = int(min(mf, nl))
+            slot = 2 * (cap + 1)
+            for i, b in enumerate(backends):
+                b.ms_push(level, fr_[i], cand[i])
+                b.ms_pack_fixed(cand[i], send[i], world, cap)
+                assert int(torch.count_nonzero(cand[i])) == 0
+            torch.cuda.synchronize()
+            for r in range(world):      # all_to_all with equal splits: sender s's slot for rank r
+                recv[r][:world * slot].copy_(torch.cat([send[s][r * slot:(r + 1) * slot] for s in range(world)]))
+            torch.cuda.synchronize()
+            for i, b in enumerate(backends):
+                cs.append(b.ms_settle_fixed(level, recv[i], world, cap, frn[i]))
         elif sparse:
             counts = []
             for i, b in enumerate(backends):
@@ -207,7 +220,8 @@ def test_partitioned_multi_source_bfs(world, layout):
     rng = np.random.default_rng(5)
     seeds = [int(s) for s in rng.choice(n, 40, replace=False)] + [int(src[0])]
     expect = [og.shortest_distance(int(ids[s]), n, 2)[0] for s in seeds]
-    for ms_alpha, sparse in ((12.0, False), (12.0, True), (1e9, False), (1e9, True), (1e-9, False)):
+    for ms_alpha, sparse in ((12.0, False), (12.0, True), (12.0, "fixed"), (1e9, False), (1e9, True), (1e9, "fixed"),
+                             (1e-9, False)):
         levels, reached = run_msbfs(backends, seeds, n, ms_alpha, sparse)
         for i, od in enumerate(expect):
             assert np.array_equal(levels[i], od), (ms_alpha, i)
@@ -340,11 +354,13 @@ def test_drivers_on_a_real_world1_group(monkeypatch):
             d, reached, _ = distributed_bfs(bfs_be, seed, n)
             assert np.array_equal(d, od)
             assert reached[0] == int((od != ABSENT).sum())
-        r, _, _ = distributed_msbfs(bfs_be, seeds, n)
-        for i, seed in enumerate(seeds):
-            od, _ = og.shortest_distance(int(ids[seed]), n, 2)
-            assert np.array_equal(bfs_be.ms_levels(i), od)
-            assert r[i] == int((od != ABSENT).sum())
+        # default (fixed-capacity exchange on small sparse levels), sized pairs only, push only
+        for alpha, fixed in ((12.0, None), (12.0, 0), (1e9, None), (1e9, 0)):
+            r, _, _ = distributed_msbfs(bfs_be, seeds, n, ms_alpha=alpha, fixed_exchange_bytes=fixed)
+            for i, seed in enumerate(seeds):
+                od, _ = og.shortest_distance(int(ids[seed]), n, 2)
+                assert np.array_equal(bfs_be.ms_levels(i), od)
+                assert r[i] == int((od != ABSENT).sum())
         pr_be = HipPartBackend(Engine(stream=st).load_partition(n, 0, n, src, dst, L.SCOPE_IN_E, apply_cap=False,
                                                                  layout=lay), n, 0, n)
         hot, span = pagerank_layout(pr_be)

@@ -1389,7 +1389,10 @@ int tgo_part_bfs_end(tgo_ctx* ctx, int64_t* dist_local, int64_t* reached) {
         HIP_TRY(k_unpermute_i64(s.dist, g.perm, s.msg, g.n, st));
         HIP_TRY(hipMemcpyAsync(dist_local, s.msg, g.n * sizeof(int64_t), hipMemcpyDeviceToHost, st));
     }
+    int ovf = 0;
+    if (s.pk_ovf) HIP_TRY(hipMemcpyAsync(&ovf, s.pk_ovf, sizeof(int), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
+    if (ovf) return fail(ctx, TGO_E_STATE, "ms_pack_fixed: an owner's pairs exceeded the capacity (cap below the level's frontier entries)");
     float ms = 0;
     HIP_TRY(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
     ctx->st.last_kernel_ms = ms;
@@ -1423,6 +1426,8 @@ int tgo_part_ms_begin(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, uint64
     HIP_TRY(hipEventRecord(ctx->ev0, st));
     HIP_TRY(hipMemsetAsync(s.ms_vis, 0, n * 8, st));
     HIP_TRY(hipMemsetAsync(fr_local, 0, n * 8, st));
+    if (!s.pk_ovf) HIP_TRY(dev_alloc(ctx, s.pk_ovf, 1));
+    HIP_TRY(hipMemsetAsync(s.pk_ovf, 0, sizeof(int), st));
     s.ms_nplanes = 0;
     // seeds owned elsewhere stay -1 (skipped by the seed kernel; their bit is set by the owner)
     HIP_TRY(hipMemcpyAsync(s.ms_seeds, local.data(), nseeds * sizeof(int64_t), hipMemcpyHostToDevice, st));
@@ -1558,6 +1563,53 @@ int tgo_part_ms_pack_dev(tgo_ctx* ctx, uint64_t* cand_global, int32_t nranks, in
     HIP_TRY(k_slice_elems(s.pk_off, cps, nranks, send_elems_dev, st));
     HIP_TRY(k_ms_pack(true, cand_global, g.n, cps, nchunks, s.pk_cnt, s.pk_off, send, st));
     return part_done(ctx);
+}
+
+// Fixed-capacity sparse exchange (msbfs.hip ms_pack_fixed): owner r's slot of `send` is
+// 2 * (cap + 1) int64 (header + pairs), so the caller's all-to-all has equal splits.
+int tgo_part_ms_pack_fixed(tgo_ctx* ctx, uint64_t* cand_global, int32_t nranks, int64_t cap, int64_t* send) {
+    int rc = part_check(ctx);
+    if (rc) return rc;
+    DevGraph& g = ctx->g;
+    Scratch& s = ctx->sc;
+    if (!cand_global || !send || nranks < 1 || nranks > kMaxRanks || cap < 1 || cap > g.n ||
+        static_cast<int64_t>(nranks) * g.n != g.n_global)
+        return fail(ctx, TGO_E_INVALID, "ms_pack_fixed: bad arguments (1 <= cap <= n_local, nranks * n_local == n_global)");
+    if (!s.pk_ovf) return fail(ctx, TGO_E_STATE, "ms_pack_fixed before ms_begin");
+    hipStream_t st = ctx->stream;
+    const int64_t cps = (g.n + kPackChunk - 1) / kPackChunk;
+    const int64_t nchunks = cps * nranks;
+    if (!s.pk_cnt) {
+        HIP_TRY(dev_alloc(ctx, s.pk_cnt, g.n_global / kPackChunk + kMaxRanks + 1));
+        HIP_TRY(dev_alloc(ctx, s.pk_off, g.n_global / kPackChunk + kMaxRanks + 1));
+    }
+    HIP_TRY(hipMemsetAsync(s.pk_cnt + nchunks, 0, sizeof(int64_t), st));
+    HIP_TRY(k_ms_pack(false, cand_global, g.n, cps, nchunks, s.pk_cnt, s.pk_off, send, st));
+    HIP_TRY(scan_exclusive_i64(s.cub_tmp, s.cub_bytes, s.pk_cnt, s.pk_off, nchunks + 1, st));
+    HIP_TRY(k_ms_pack_fixed(cand_global, g.n, cps, nchunks, s.pk_off, nranks, cap, send, s.pk_ovf, st));
+    return part_done(ctx);
+}
+
+int tgo_part_ms_settle_fixed(tgo_ctx* ctx, int32_t level, const int64_t* recv, int32_t nslices, int64_t cap,
+                             uint64_t* fr_next, int64_t* counts) {
+    int rc = part_check(ctx);
+    if (rc) return rc;
+    DevGraph& g = ctx->g;
+    Scratch& s = ctx->sc;
+    hipStream_t st = ctx->stream;
+    if (!recv || !fr_next || nslices < 1 || nslices > kMaxRanks || cap < 1 || cap > g.n)
+        return fail(ctx, TGO_E_INVALID, "ms_settle_fixed: bad arguments");
+    if (level + 1 >= (1 << kLevelPlanes)) return fail(ctx, TGO_E_UNSUPPORTED, "multi-source BFS levels are < 65536");
+    if ((rc = ms_planes_for(ctx, level + 1))) return rc;
+    HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
+    HIP_TRY(hipMemsetAsync(fr_next, 0, g.n * 8, st));
+    HIP_TRY(k_ms_or_fixed(recv, nslices, cap, fr_next, st));
+    const int nxt = ctx->part_cur ^ 1;
+    HIP_TRY(k_ms_settle(push_view(g, TGO_SCOPE_BOTH_E), g.n, s.ms_vis, fr_next, ms_planes(ctx), s.q[nxt], s.qdeg, s.cnt,
+                        level + 1, st));
+    ctx->part_cur = nxt;
+    ctx->part_queued = true;
+    return part_counts(ctx, counts);
 }
 
 int tgo_part_ms_settle_pairs(tgo_ctx* ctx, int32_t level, const int64_t* recv, const int64_t* recv_counts,

@@ -322,6 +322,7 @@ struct Scratch {
     int64_t* ms_seeds = nullptr;    // 64
     unsigned long long* ms_stat = nullptr;   // 128: reached[64], entries[64]
     int32_t ms_nsrc = 0;
+    int* pk_ovf = nullptr;          // fixed-capacity exchange overflow flag (checked at ms_end)
     int64_t* pk_cnt = nullptr;      // partitioned sparse exchange: per-chunk pair counts
     int64_t* pk_off = nullptr;      // and their exclusive scan (n_global / kPackChunk + 1 each)
     // light/heavy delta-stepping (allocated on first use)
@@ -429,6 +430,9 @@ hipError_t k_ms_pack(bool write, uint64_t* cand, int64_t n_local, int64_t cps, i
                      const int64_t* offs, int64_t* send, hipStream_t s);
 hipError_t k_slice_elems(const int64_t* off, int64_t cps, int nranks, int64_t* out, hipStream_t s);
 hipError_t k_ms_or_pairs(const int64_t* pairs, int64_t npairs, uint64_t* nx, hipStream_t s);
+hipError_t k_ms_pack_fixed(uint64_t* cand, int64_t n_local, int64_t cps, int64_t nchunks, const int64_t* offs,
+                           int nranks, int64_t cap, int64_t* send, int* ovf, hipStream_t s);
+hipError_t k_ms_or_fixed(const int64_t* recv, int nslices, int64_t cap, uint64_t* nx, hipStream_t s);
 hipError_t k_part_td_mark(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen,
                           uint64_t* disc, const uint64_t* vb_local, int64_t lo, int64_t n_local, hipStream_t s);
 hipError_t k_part_claim(const View& push, const uint64_t* recv, int nslices, int64_t words, int64_t n_local,

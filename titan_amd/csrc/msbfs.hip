@@ -282,6 +282,56 @@ __global__ void slice_elems(const int64_t* __restrict__ off, int64_t cps, int nr
     const int r = threadIdx.x;
     if (blockIdx.x == 0 && r < nranks) out[r] = 2 * (off[(r + 1) * cps] - off[r * cps]);
 }
+// Fixed-capacity form of the exchange (tgo_part_ms_pack_fixed): destination r's slot holds
+// a header pair (count, 0) and up to `cap` pairs, so the all-to-all has equal splits known
+// on the host before the level — no all-to-all of split sizes, no host read of them.  The
+// caller's cap bounds the count (a rank's pairs for one owner <= its pushed entries <= the
+// level's frontier entries); a count over cap is recorded in *ovf and fails the sweep.
+__global__ void __launch_bounds__(kBlock) ms_pack_fixed(uint64_t* __restrict__ cand, int64_t n_local, int64_t cps,
+        int64_t nchunks, const int64_t* __restrict__ offs, int64_t cap, int64_t* __restrict__ send, int* ovf) {
+    const int64_t c = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    if (c >= nchunks) return;
+    const int64_t r = c / cps, j = c - r * cps;
+    const int64_t w0 = r * n_local + j * kPackChunk;
+    const int64_t w1 = r * n_local + min(n_local, (j + 1) * kPackChunk);
+    int64_t base = offs[c] - offs[r * cps];                 // pair index within owner r's slot
+    int64_t* slot = send + 2 * r * (cap + 1) + 2;
+    for (int64_t g = w0; g < w1; g += 64) {
+        const int64_t i = g + lane();
+        const uint64_t m = cand[i];
+        const uint64_t bal = __ballot(m != 0);
+        if (m) {
+            const int64_t p = base + __popcll(bal & ((1ULL << lane()) - 1ULL));
+            if (p < cap) {
+                slot[2 * p] = i - r * n_local;
+                slot[2 * p + 1] = static_cast<int64_t>(m);
+            } else {
+                atomicOr(ovf, 1);
+            }
+            cand[i] = 0;
+        }
+        base += __popcll(bal);
+    }
+}
+__global__ void fixed_headers(const int64_t* __restrict__ off, int64_t cps, int nranks, int64_t cap,
+                              int64_t* __restrict__ send) {
+    const int r = threadIdx.x;
+    if (blockIdx.x == 0 && r < nranks) {
+        send[2 * r * (cap + 1)] = min(cap, off[(r + 1) * cps] - off[r * cps]);
+        send[2 * r * (cap + 1) + 1] = 0;
+    }
+}
+// Receiver side: slot s of recv came from sender s; OR its pairs into the owned words.
+__global__ void ms_or_fixed(const int64_t* __restrict__ recv, int nslices, int64_t cap, uint64_t* __restrict__ nx) {
+    const int64_t total = static_cast<int64_t>(nslices) * cap;
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < total; k += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t s = k / cap, i = k - s * cap;
+        const int64_t* slot = recv + 2 * s * (cap + 1);
+        if (i >= slot[0]) continue;
+        atomicOr(reinterpret_cast<unsigned long long*>(nx + slot[2 + 2 * i]), static_cast<unsigned long long>(slot[3 + 2 * i]));
+    }
+}
+
 // Received pairs of one sender: OR the masks into the owned candidate words (several
 // senders may name one vertex).
 __global__ void ms_or_pairs(const int64_t* __restrict__ pairs, int64_t npairs, uint64_t* __restrict__ nx) {
@@ -392,6 +442,21 @@ hipError_t k_ms_pack(bool write, uint64_t* cand, int64_t n_local, int64_t cps, i
 }
 hipError_t k_slice_elems(const int64_t* off, int64_t cps, int nranks, int64_t* out, hipStream_t s) {
     slice_elems<<<1, kBlock, 0, s>>>(off, cps, nranks, out);
+    return hipGetLastError();
+}
+hipError_t k_ms_pack_fixed(uint64_t* cand, int64_t n_local, int64_t cps, int64_t nchunks, const int64_t* offs,
+                           int nranks, int64_t cap, int64_t* send, int* ovf, hipStream_t s) {
+    const int64_t threads = nchunks * 64;
+    ms_pack_fixed<<<static_cast<unsigned>((threads + kBlock - 1) / kBlock), kBlock, 0, s>>>(cand, n_local, cps, nchunks, offs,
+                                                                                           cap, send, ovf);
+    fixed_headers<<<1, 64, 0, s>>>(offs, cps, nranks, cap, send);
+    return hipGetLastError();
+}
+hipError_t k_ms_or_fixed(const int64_t* recv, int nslices, int64_t cap, uint64_t* nx, hipStream_t s) {
+    const int64_t total = static_cast<int64_t>(nslices) * cap;
+    int64_t g = (total + kBlock - 1) / kBlock;
+    g = std::max<int64_t>(1, std::min<int64_t>(g, 65536));
+    ms_or_fixed<<<static_cast<unsigned>(g), kBlock, 0, s>>>(recv, nslices, cap, nx);
     return hipGetLastError();
 }
 hipError_t k_ms_or_pairs(const int64_t* pairs, int64_t npairs, uint64_t* nx, hipStream_t s) {

@@ -26,6 +26,8 @@ from __future__ import annotations
 
 import ctypes as C
 
+import os
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -129,7 +131,7 @@ class HipPartBackend:
 
     # steps whose level counts can stay on the device (tgo_part_device_counts)
     DEVICE_COUNT_STEPS = frozenset({"tgo_part_bfs_claim", "tgo_part_bfs_bu", "tgo_part_ms_pull", "tgo_part_ms_settle",
-                                    "tgo_part_ms_settle_pairs"})
+                                    "tgo_part_ms_settle_pairs", "tgo_part_ms_settle_fixed"})
 
     def __init__(self, engine, n_global, lo, hi, device_counts=False):
         if engine.stream == 0 or engine.stream != torch.cuda.current_stream().cuda_stream:
@@ -203,6 +205,12 @@ class HipPartBackend:
         sc = np.zeros(nranks, np.int64)
         self.e.part_call("tgo_part_ms_pack", self._vp(cand), nranks, self._vp(send), L.ptr(sc, C.c_int64))
         return sc
+
+    def ms_pack_fixed(self, cand, send, nranks, cap):
+        self.e.part_call("tgo_part_ms_pack_fixed", self._vp(cand), nranks, C.c_int64(cap), self._vp(send))
+
+    def ms_settle_fixed(self, level, recv, nslices, cap, fr_next):
+        return self._counts("tgo_part_ms_settle_fixed", level, self._vp(recv), nslices, C.c_int64(cap), self._vp(fr_next))
 
     def ms_settle_pairs(self, level, recv, recv_counts, fr_next):
         rc = np.ascontiguousarray(recv_counts, np.int64)
@@ -378,8 +386,13 @@ def _exchange_pairs_dev(send, sct, recv, group):
     return np.asarray(outs, np.int64) // 2
 
 
+# sparse multi-source levels whose per-rank send fits this many bytes use the fixed-capacity
+# exchange (equal splits bounded by the frontier entries, no all-to-all of split sizes)
+FIXED_EXCHANGE_BYTES = int(os.environ.get("TGO_MS_FIXED_BYTES", 64 << 20))
+
+
 def distributed_msbfs(backend, seeds, max_depth: int, ms_alpha: float = 12.0, stats: bool = True, group=None,
-                      sparse_exchange: bool = True):
+                      sparse_exchange: bool = True, fixed_exchange_bytes: int = None):
     """Up to 64 ShortestDistance programs with unit weights over bothE, run together with
     bit-parallel frontier masks on a vertex-partitioned graph.
       dense level : all_gather of owned frontier masks (8 bytes per vertex) -> local pull
@@ -390,6 +403,8 @@ def distributed_msbfs(backend, seeds, max_depth: int, ms_alpha: float = 12.0, st
     world = dist.get_world_size(group)
     nseeds = len(seeds)
     dev = backend.device
+    if fixed_exchange_bytes is None:
+        fixed_exchange_bytes = FIXED_EXCHANGE_BYTES
     # the owned masks are the rank's slice of a global buffer (two, alternating by level), so
     # a dense level's all-gather is in place: no copy of the rank's own slice
     lo, nl = backend.lo, backend.n_local
@@ -410,16 +425,24 @@ def distributed_msbfs(backend, seeds, max_depth: int, ms_alpha: float = 12.0, st
             dist.all_gather_into_tensor(glob[0], fr, group=group)
             c = backend.ms_pull(level, glob[0], frn)
         elif sparse_exchange:
-            send = _scratch(backend, "pairs_send", 2 * backend.n_global, torch.int64)
-            recv = _scratch(backend, "pairs_recv", 2 * backend.n_global, torch.int64)
+            send = _scratch(backend, "pairs_send", 2 * backend.n_global + 2 * world, torch.int64)
+            recv = _scratch(backend, "pairs_recv", 2 * backend.n_global + 2 * world, torch.int64)
             backend.ms_push(level, fr, cand)           # cand is all-zero here: the pack clears it
-            if hasattr(backend, "ms_pack_dev"):
+            # small frontier: equal splits bounded by the frontier entries, no size exchange
+            cap = int(min(mf, backend.n_local))
+            if hasattr(backend, "ms_pack_fixed") and cap > 0 and world * (cap + 1) * 16 <= fixed_exchange_bytes:
+                ne = 2 * world * (cap + 1)
+                backend.ms_pack_fixed(cand, send, world, cap)
+                dist.all_to_all_single(recv[:ne], send[:ne], group=group)
+                c = backend.ms_settle_fixed(level, recv, world, cap, frn)
+            elif hasattr(backend, "ms_pack_dev"):
                 sct = _scratch(backend, "pairs_sct", world, torch.int64)
                 backend.ms_pack_dev(cand, send, world, sct)
                 rcounts = _exchange_pairs_dev(send, sct, recv, group)
+                c = backend.ms_settle_pairs(level, recv, rcounts, frn)
             else:
                 rcounts = _exchange_pairs(send, backend.ms_pack(cand, send, world), recv, dev, group)
-            c = backend.ms_settle_pairs(level, recv, rcounts, frn)
+                c = backend.ms_settle_pairs(level, recv, rcounts, frn)
         else:
             recv = _scratch(backend, "slices_recv", backend.n_global, torch.int64)
             cand.zero_()
