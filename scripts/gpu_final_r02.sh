@@ -11,3 +11,4 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
     python3 bench.py > gpurun_out/$T/bench_prof.json 2> gpurun_out/$T/bench_prof.err
 rc=$?; echo "prof bench exit $rc"; rm -f gpurun_out/$T/run_kernel_trace.csv; [ $rc -eq 0 ] || exit $rc
 bash scripts/gpu_pmc.sh ${T}_pmc --rows-scale 0 --sssp-roots 0
+bash scripts/gpu_part_prof.sh
