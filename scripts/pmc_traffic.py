@@ -28,11 +28,14 @@ from collections import defaultdict
 
 GROUPS = {
     # one rank update of the cache-blocked gather (spmv.hip): cold pass, fold, hot pass, long rows
-    "pagerank_update": ("cold_gather<", "cold_fold(", "gather_short_packed<", "gather_chunks<tgo::(anonymous namespace)::PackedOp",
+    # (gather_hot_pf: the prefetching hot pass; gather_short_packed: its TGO_PR_PF=0 form)
+    "pagerank_update": ("cold_gather<", "cold_fold(", "gather_hot_pf(", "gather_short_packed<",
+                        "gather_chunks<tgo::(anonymous namespace)::PackedOp",
                         "finalize_long<tgo::(anonymous namespace)::PackedOp"),
-    "msbfs_sweep": ("ms_seed(", "ms_pull(", "ms_push(", "ms_settle("),
+    # ms_pull is templated on its round-trip width (ms_pull<8>)
+    "msbfs_sweep": ("ms_seed(", "ms_pull(", "ms_pull<", "ms_push(", "ms_settle(", "ms_queue(", "ms_fbitmap("),
 }
-UNIT_KERNEL = {"pagerank_update": "gather_short_packed<", "msbfs_sweep": "ms_seed("}
+UNIT_KERNEL = {"pagerank_update": ("gather_hot_pf(", "gather_short_packed<"), "msbfs_sweep": ("ms_seed(",)}
 
 
 def load(d):
@@ -63,7 +66,7 @@ def per_unit(passes, counter):
             if g is None or counter not in cs:
                 continue
             tot[g] += cs[counter]
-            if UNIT_KERNEL[g] in name:
+            if any(k in name for k in UNIT_KERNEL[g]):
                 units[g] += 1
     return {g: tot[g] / units[g] for g in tot if units[g]}
 
