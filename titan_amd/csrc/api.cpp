@@ -1428,6 +1428,9 @@ int tgo_part_ms_begin(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, uint64
     HIP_TRY(hipMemsetAsync(fr_local, 0, n * 8, st));
     if (!s.pk_ovf) HIP_TRY(dev_alloc(ctx, s.pk_ovf, 1));
     HIP_TRY(hipMemsetAsync(s.pk_ovf, 0, sizeof(int), st));
+    const int64_t touch_n = g.n_global / kPackChunk + kMaxRanks + 1;
+    if (!s.pk_touch) HIP_TRY(dev_alloc(ctx, s.pk_touch, touch_n));
+    HIP_TRY(hipMemsetAsync(s.pk_touch, 0, touch_n, st));
     s.ms_nplanes = 0;
     // seeds owned elsewhere stay -1 (skipped by the seed kernel; their bit is set by the owner)
     HIP_TRY(hipMemcpyAsync(s.ms_seeds, local.data(), nseeds * sizeof(int64_t), hipMemcpyHostToDevice, st));
@@ -1488,8 +1491,9 @@ int tgo_part_ms_push(tgo_ctx* ctx, int32_t level, const uint64_t* fr_local, uint
     }
     if (qlen > 0) {
         if ((rc = scan_frontier(ctx, ctx->part_qlen))) return rc;
+        const PackTouch touch{s.pk_touch, g.n, (g.n + kPackChunk - 1) / kPackChunk};
         HIP_TRY(k_ms_push(push_view(g, TGO_SCOPE_BOTH_E), s.q[ctx->part_cur], s.qpre, ctx->part_qlen, fr_local,
-                          nullptr, cand_global, ctx->stream));
+                          nullptr, cand_global, ctx->stream, touch));
     }
     return part_done(ctx);
 }
@@ -1529,14 +1533,14 @@ int tgo_part_ms_pack(tgo_ctx* ctx, uint64_t* cand_global, int32_t nranks, int64_
         HIP_TRY(dev_alloc(ctx, s.pk_off, g.n_global / kPackChunk + kMaxRanks + 1));
     }
     HIP_TRY(hipMemsetAsync(s.pk_cnt + nchunks, 0, sizeof(int64_t), st));
-    HIP_TRY(k_ms_pack(false, cand_global, g.n, cps, nchunks, s.pk_cnt, s.pk_off, send, st));
+    HIP_TRY(k_ms_pack(false, cand_global, g.n, cps, nchunks, s.pk_cnt, s.pk_off, send, st, s.pk_touch));
     HIP_TRY(scan_exclusive_i64(s.cub_tmp, s.cub_bytes, s.pk_cnt, s.pk_off, nchunks + 1, st));
     std::vector<int64_t> off(nranks + 1);
     for (int r = 0; r <= nranks; ++r)     // offsets at the slice boundaries (pk_cnt[nchunks] is 0)
         HIP_TRY(hipMemcpyAsync(&off[r], s.pk_off + r * cps, sizeof(int64_t), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     for (int r = 0; r < nranks; ++r) send_counts[r] = off[r + 1] - off[r];
-    if (off[nranks] > 0) HIP_TRY(k_ms_pack(true, cand_global, g.n, cps, nchunks, s.pk_cnt, s.pk_off, send, st));
+    if (off[nranks] > 0) HIP_TRY(k_ms_pack(true, cand_global, g.n, cps, nchunks, s.pk_cnt, s.pk_off, send, st, s.pk_touch));
     return part_done(ctx);
 }
 
@@ -1558,10 +1562,10 @@ int tgo_part_ms_pack_dev(tgo_ctx* ctx, uint64_t* cand_global, int32_t nranks, in
         HIP_TRY(dev_alloc(ctx, s.pk_off, g.n_global / kPackChunk + kMaxRanks + 1));
     }
     HIP_TRY(hipMemsetAsync(s.pk_cnt + nchunks, 0, sizeof(int64_t), st));
-    HIP_TRY(k_ms_pack(false, cand_global, g.n, cps, nchunks, s.pk_cnt, s.pk_off, send, st));
+    HIP_TRY(k_ms_pack(false, cand_global, g.n, cps, nchunks, s.pk_cnt, s.pk_off, send, st, s.pk_touch));
     HIP_TRY(scan_exclusive_i64(s.cub_tmp, s.cub_bytes, s.pk_cnt, s.pk_off, nchunks + 1, st));
     HIP_TRY(k_slice_elems(s.pk_off, cps, nranks, send_elems_dev, st));
-    HIP_TRY(k_ms_pack(true, cand_global, g.n, cps, nchunks, s.pk_cnt, s.pk_off, send, st));
+    HIP_TRY(k_ms_pack(true, cand_global, g.n, cps, nchunks, s.pk_cnt, s.pk_off, send, st, s.pk_touch));
     return part_done(ctx);
 }
 
@@ -1584,9 +1588,9 @@ int tgo_part_ms_pack_fixed(tgo_ctx* ctx, uint64_t* cand_global, int32_t nranks, 
         HIP_TRY(dev_alloc(ctx, s.pk_off, g.n_global / kPackChunk + kMaxRanks + 1));
     }
     HIP_TRY(hipMemsetAsync(s.pk_cnt + nchunks, 0, sizeof(int64_t), st));
-    HIP_TRY(k_ms_pack(false, cand_global, g.n, cps, nchunks, s.pk_cnt, s.pk_off, send, st));
+    HIP_TRY(k_ms_pack(false, cand_global, g.n, cps, nchunks, s.pk_cnt, s.pk_off, send, st, s.pk_touch));
     HIP_TRY(scan_exclusive_i64(s.cub_tmp, s.cub_bytes, s.pk_cnt, s.pk_off, nchunks + 1, st));
-    HIP_TRY(k_ms_pack_fixed(cand_global, g.n, cps, nchunks, s.pk_off, nranks, cap, send, s.pk_ovf, st));
+    HIP_TRY(k_ms_pack_fixed(cand_global, g.n, cps, nchunks, s.pk_off, nranks, cap, send, s.pk_ovf, s.pk_touch, st));
     return part_done(ctx);
 }
 

@@ -323,6 +323,7 @@ struct Scratch {
     unsigned long long* ms_stat = nullptr;   // 128: reached[64], entries[64]
     int32_t ms_nsrc = 0;
     int* pk_ovf = nullptr;          // fixed-capacity exchange overflow flag (checked at ms_end)
+    uint8_t* pk_touch = nullptr;    // per pack chunk: written by this level's push (PackTouch)
     int64_t* pk_cnt = nullptr;      // partitioned sparse exchange: per-chunk pair counts
     int64_t* pk_off = nullptr;      // and their exclusive scan (n_global / kPackChunk + 1 each)
     // light/heavy delta-stepping (allocated on first use)
@@ -416,8 +417,11 @@ hipError_t k_ms_pull(const View& pull, const View& push, int64_t n_active, uint6
 hipError_t k_ms_fbitmap(const uint64_t* fr, int64_t n, uint64_t* fbm, hipStream_t s);
 hipError_t k_ms_queue(const View& push, int64_t n_active, const uint64_t* fr, int32_t* qn, int64_t* qdeg, Counters* cnt,
                       hipStream_t s);
+// Partitioned push: per-pack-chunk "written" flags (chunk of global word v: owner v / n_local,
+// chunk (v % n_local) / kPackChunk of the owner's cps) so the pack skips untouched chunks.
+struct PackTouch { uint8_t* flag = nullptr; int64_t n_local = 1; int64_t cps = 1; };
 hipError_t k_ms_push(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen, const uint64_t* fr,
-                     const uint64_t* vis, uint64_t* nx, hipStream_t s);
+                     const uint64_t* vis, uint64_t* nx, hipStream_t s, PackTouch touch = {});
 hipError_t k_ms_settle(const View& push, int64_t n_active, uint64_t* vis, uint64_t* nx, LevelPlanes lvl, int32_t* qn,
                        int64_t* qdeg, Counters* cnt, int32_t next_level, hipStream_t s);
 hipError_t k_ms_reach(const View& v, const uint64_t* vis, int64_t n_active, int nsrc, unsigned long long* reached,
@@ -427,11 +431,11 @@ hipError_t k_ms_extract(LevelPlanes lvl, int nplanes, const uint64_t* vis, const
 hipError_t k_or_slices(const uint64_t* recv, int nslices, int64_t n_local, uint64_t* out, hipStream_t s);
 constexpr int64_t kPackChunk = 2048;   // candidate words per wave in the sparse-exchange pack
 hipError_t k_ms_pack(bool write, uint64_t* cand, int64_t n_local, int64_t cps, int64_t nchunks, int64_t* cnt,
-                     const int64_t* offs, int64_t* send, hipStream_t s);
+                     const int64_t* offs, int64_t* send, hipStream_t s, uint8_t* touched = nullptr);
 hipError_t k_slice_elems(const int64_t* off, int64_t cps, int nranks, int64_t* out, hipStream_t s);
 hipError_t k_ms_or_pairs(const int64_t* pairs, int64_t npairs, uint64_t* nx, hipStream_t s);
 hipError_t k_ms_pack_fixed(uint64_t* cand, int64_t n_local, int64_t cps, int64_t nchunks, const int64_t* offs,
-                           int nranks, int64_t cap, int64_t* send, int* ovf, hipStream_t s);
+                           int nranks, int64_t cap, int64_t* send, int* ovf, uint8_t* touched, hipStream_t s);
 hipError_t k_ms_or_fixed(const int64_t* recv, int nslices, int64_t cap, uint64_t* nx, hipStream_t s);
 hipError_t k_part_td_mark(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen,
                           uint64_t* disc, const uint64_t* vb_local, int64_t lo, int64_t n_local, hipStream_t s);

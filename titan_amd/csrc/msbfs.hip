@@ -187,13 +187,16 @@ __global__ void __launch_bounds__(kBlock) ms_fbitmap(const uint64_t* __restrict_
 // Push level: edge-balanced over the frontier queue (exclusive scan of degrees in qpre).
 __global__ void __launch_bounds__(kBlock) ms_push(View push, const int32_t* __restrict__ q,
         const int64_t* __restrict__ qpre, int64_t qlen, const uint64_t* __restrict__ fr,
-        const uint64_t* __restrict__ vis, uint64_t* __restrict__ nx) {
+        const uint64_t* __restrict__ vis, uint64_t* __restrict__ nx, PackTouch touch) {
     for_each_queue_edge(q, qpre, qlen, [&](bool valid, int32_t u, int64_t o) {
         if (!valid) return;
         const int32_t v = view_entry(push, u, o);
         // partitioned graphs pass vis = nullptr: remote vertices' masks are not local
         const uint64_t m = vis ? (fr[u] & ~vis[v]) : fr[u];
-        if (m && (nx[v] & m) != m) atomicOr(reinterpret_cast<unsigned long long*>(&nx[v]), m);
+        if (m && (nx[v] & m) != m) {
+            atomicOr(reinterpret_cast<unsigned long long*>(&nx[v]), m);
+            if (touch.flag) touch.flag[(v / touch.n_local) * touch.cps + (v % touch.n_local) / kPackChunk] = 1;
+        }
     });
 }
 
@@ -253,11 +256,18 @@ __global__ void or_slices(const uint64_t* __restrict__ recv, int nslices, int64_
 // counts the chunk's nonzero words (cnt[c]); an exclusive scan gives each chunk its first
 // pair; pass 1 writes the pairs in word order and clears the words (the candidate array is
 // zero again for the next level).  No atomics: the pair order is deterministic.
+// touched (optional): per-chunk flags set by ms_push — a chunk no push wrote is all zero and
+// is skipped without reading its words; the write pass clears the flags it consumed.
 template <bool kWrite>
 __global__ void __launch_bounds__(kBlock) ms_pack(uint64_t* __restrict__ cand, int64_t n_local, int64_t cps,
-        int64_t nchunks, int64_t* __restrict__ cnt, const int64_t* __restrict__ offs, int64_t* __restrict__ send) {
+        int64_t nchunks, int64_t* __restrict__ cnt, const int64_t* __restrict__ offs, int64_t* __restrict__ send,
+        uint8_t* __restrict__ touched) {
     const int64_t c = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
     if (c >= nchunks) return;
+    if (touched && !touched[c]) {
+        if (!kWrite && lane() == 0) cnt[c] = 0;
+        return;
+    }
     const int64_t r = c / cps, j = c - r * cps;
     const int64_t w0 = r * n_local + j * kPackChunk;
     const int64_t w1 = r * n_local + min(n_local, (j + 1) * kPackChunk);
@@ -275,6 +285,7 @@ __global__ void __launch_bounds__(kBlock) ms_pack(uint64_t* __restrict__ cand, i
         base += __popcll(bal);
     }
     if (!kWrite && lane() == 0) cnt[c] = base;
+    if (kWrite && touched && lane() == 0) touched[c] = 0;
 }
 // Per-destination element counts of the packed pairs (2 int64 per pair) from the chunk
 // offsets, for a device-side all-to-all of the split sizes.
@@ -288,9 +299,11 @@ __global__ void slice_elems(const int64_t* __restrict__ off, int64_t cps, int nr
 // caller's cap bounds the count (a rank's pairs for one owner <= its pushed entries <= the
 // level's frontier entries); a count over cap is recorded in *ovf and fails the sweep.
 __global__ void __launch_bounds__(kBlock) ms_pack_fixed(uint64_t* __restrict__ cand, int64_t n_local, int64_t cps,
-        int64_t nchunks, const int64_t* __restrict__ offs, int64_t cap, int64_t* __restrict__ send, int* ovf) {
+        int64_t nchunks, const int64_t* __restrict__ offs, int64_t cap, int64_t* __restrict__ send, int* ovf,
+        uint8_t* __restrict__ touched) {
     const int64_t c = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
     if (c >= nchunks) return;
+    if (touched && !touched[c]) return;
     const int64_t r = c / cps, j = c - r * cps;
     const int64_t w0 = r * n_local + j * kPackChunk;
     const int64_t w1 = r * n_local + min(n_local, (j + 1) * kPackChunk);
@@ -312,6 +325,7 @@ __global__ void __launch_bounds__(kBlock) ms_pack_fixed(uint64_t* __restrict__ c
         }
         base += __popcll(bal);
     }
+    if (touched && lane() == 0) touched[c] = 0;
 }
 __global__ void fixed_headers(const int64_t* __restrict__ off, int64_t cps, int nranks, int64_t cap,
                               int64_t* __restrict__ send) {
@@ -418,8 +432,8 @@ hipError_t k_ms_queue(const View& push, int64_t n_active, const uint64_t* fr, in
     return hipGetLastError();
 }
 hipError_t k_ms_push(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen, const uint64_t* fr,
-                     const uint64_t* vis, uint64_t* nx, hipStream_t s) {
-    ms_push<<<256 * 8, kBlock, 0, s>>>(push, q, qpre, qlen, fr, vis, nx);
+                     const uint64_t* vis, uint64_t* nx, hipStream_t s, PackTouch touch) {
+    ms_push<<<256 * 8, kBlock, 0, s>>>(push, q, qpre, qlen, fr, vis, nx, touch);
     return hipGetLastError();
 }
 hipError_t k_ms_settle(const View& push, int64_t n_active, uint64_t* vis, uint64_t* nx, LevelPlanes lvl, int32_t* qn,
@@ -434,10 +448,10 @@ hipError_t k_ms_reach(const View& v, const uint64_t* vis, int64_t n_active, int 
     return hipGetLastError();
 }
 hipError_t k_ms_pack(bool write, uint64_t* cand, int64_t n_local, int64_t cps, int64_t nchunks, int64_t* cnt,
-                     const int64_t* offs, int64_t* send, hipStream_t s) {
+                     const int64_t* offs, int64_t* send, hipStream_t s, uint8_t* touched) {
     const unsigned blocks = static_cast<unsigned>((nchunks * 64 + kBlock - 1) / kBlock);
-    if (write) ms_pack<true><<<blocks, kBlock, 0, s>>>(cand, n_local, cps, nchunks, cnt, offs, send);
-    else ms_pack<false><<<blocks, kBlock, 0, s>>>(cand, n_local, cps, nchunks, cnt, offs, send);
+    if (write) ms_pack<true><<<blocks, kBlock, 0, s>>>(cand, n_local, cps, nchunks, cnt, offs, send, touched);
+    else ms_pack<false><<<blocks, kBlock, 0, s>>>(cand, n_local, cps, nchunks, cnt, offs, send, touched);
     return hipGetLastError();
 }
 hipError_t k_slice_elems(const int64_t* off, int64_t cps, int nranks, int64_t* out, hipStream_t s) {
@@ -445,10 +459,10 @@ hipError_t k_slice_elems(const int64_t* off, int64_t cps, int nranks, int64_t* o
     return hipGetLastError();
 }
 hipError_t k_ms_pack_fixed(uint64_t* cand, int64_t n_local, int64_t cps, int64_t nchunks, const int64_t* offs,
-                           int nranks, int64_t cap, int64_t* send, int* ovf, hipStream_t s) {
+                           int nranks, int64_t cap, int64_t* send, int* ovf, uint8_t* touched, hipStream_t s) {
     const int64_t threads = nchunks * 64;
     ms_pack_fixed<<<static_cast<unsigned>((threads + kBlock - 1) / kBlock), kBlock, 0, s>>>(cand, n_local, cps, nchunks, offs,
-                                                                                           cap, send, ovf);
+                                                                                           cap, send, ovf, touched);
     fixed_headers<<<1, 64, 0, s>>>(offs, cps, nranks, cap, send);
     return hipGetLastError();
 }
