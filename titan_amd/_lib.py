@@ -10,7 +10,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libtitan_gpu_olap.so")
+# TGO_LIB_PATH: a probe build of the same sources (e.g. another tile size, scripts/gpu_ktile.sh)
+LIB_PATH = os.environ.get("TGO_LIB_PATH") or os.path.join(_HERE, "libtitan_gpu_olap.so")
 
 # status codes (tgo_status)
 TGO_OK = 0

@@ -489,7 +489,12 @@ void build_row_blocks(const std::vector<int64_t>& off, int64_t tile, int64_t max
                       std::vector<int64_t>& blk, std::vector<int64_t>& chunk_row,
                       std::vector<int64_t>& chunk_beg, std::vector<int64_t>& chunk_end,
                       std::vector<int64_t>& long_row, std::vector<int64_t>& long_chunk);
-constexpr int64_t kTile = 4096;      // entries per CSR-adaptive block (32 KB of fp64 in LDS; 2048: 1.84, 8192: 1.87 ms/update)
+#ifndef TGO_KTILE
+#define TGO_KTILE 4096
+#endif
+// entries per CSR-adaptive block (32 KB of fp64 in LDS; round 1: 2048 1.84, 8192 1.87 ms/update;
+// TGO_KTILE builds a probe library with another size, scripts/gpu_ktile.sh)
+constexpr int64_t kTile = TGO_KTILE;
 constexpr int64_t kMaxRows = 1024;   // rows per CSR-adaptive block
 
 }  // namespace tgo
