@@ -34,6 +34,8 @@ variants = [
 RELOAD = ("TGO_PR_BLOCKED", "TGO_PR_HOT", "TGO_PR_SEG", "TGO_PR_PACK", "TGO_PR_CPACK")   # read at load time
 if os.environ.get("PR_PROBE_DEFAULT_ONLY"):
     variants = [{}]
+if os.environ.get("PR_PROBE_VARIANTS"):        # a JSON list of env dicts, e.g. '[{}, {"TGO_PR_SEG": "393216"}]'
+    variants = json.loads(os.environ["PR_PROBE_VARIANTS"])
 base = None
 out = []
 for v in variants:
