@@ -126,7 +126,7 @@ int64_t env_i64(const char* name, int64_t dflt) {
     const char* v = std::getenv(name);
     return v ? std::atoll(v) : dflt;
 }
-constexpr int64_t kPrHotDefault = 524288, kPrSegDefault = 524288;
+constexpr int64_t kPrHotDefault = 393216, kPrSegDefault = 393216;   // 3 MB each (profiles/r02an_pr_hot_seg_probe*.log)
 
 // PageRank diagnostics (engine.hpp PrTuning): TGO_PR_DIAG=lo:hi gathers only sources in
 // [lo, hi) — a timing attribution tool, its ranks are wrong (scripts/pr_probe.py).
