@@ -120,8 +120,9 @@ int threads_of(const tgo_ctx* ctx) {
 
 // Cache-blocked PageRank in-lists (ColdBlocks, engine.hpp) for one-GPU PageRank.
 // TGO_PR_BLOCKED=0 turns it off; TGO_PR_HOT / TGO_PR_SEG set the hot threshold and the cold
-// segment size in sources (defaults: 4 MB of fp64 messages each, one XCD's L2; swept on
-// RMAT-24 in profiles/r02m_pr_probe.log: 512K/512K fastest of 128K..1M).
+// segment size in sources (defaults: 384 K sources = 3 MB of fp64 messages each, under one
+// XCD's 4 MB L2 so the row streams do not evict the head; swept on RMAT-24 in
+// profiles/r02m_pr_probe.log and profiles/r02an_pr_hot_seg_probe*.log).
 int64_t env_i64(const char* name, int64_t dflt) {
     const char* v = std::getenv(name);
     return v ? std::atoll(v) : dflt;
