@@ -76,7 +76,10 @@ typedef enum {
     TGO_DT_FLOAT = 5, TGO_DT_DOUBLE = 6, TGO_DT_BOOLEAN = 7,
     TGO_DT_DATE = 8,       /* DateSerializer: the Long form of getTime()                    */
     TGO_DT_CHARACTER = 9,  /* CharacterSerializer: 2 bytes                                  */
-    TGO_DT_STRING = 10     /* StringSerializer: ASCII / full UTF / compressed (skipped only) */
+    TGO_DT_STRING = 10,    /* StringSerializer: ASCII / full UTF / compressed (skipped only) */
+    TGO_DT_OBJECT = 11     /* generic key (DefaultSchemaMaker: dataType(Object.class)): the value
+                            * class's registration number, then its serializer without a null flag
+                            * (StandardSerializer.writeClassAndObject :316-322) — result write-back only */
 } tgo_datatype;
 
 /* RelationType sort order (EdgeSerializer.java:137,311-313): DESC inverts the sort-key bytes. */
@@ -339,8 +342,9 @@ int  tgo_dense_ids(tgo_ctx* ctx, const int64_t* titan_ids, int64_t count, int64_
  *   PAGERANK  PAGE_RANK and OUTGOING_EDGE_COUNT (Double) on every executed vertex once
  *             iterations >= 1 (PageRankVertexProgram.java:79-88)
  *   DEGREE    OLAPTest.DegreeCounter DEGREE (Integer) on every executed vertex
- * Compute keys must be typed property keys of those datatypes (a key left to
- * getOrCreatePropertyKey's generic Object type is TGO_E_UNSUPPORTED).  Relation ids are
+ * Compute keys are typed property keys of those datatypes, or generic keys (TGO_DT_OBJECT: what
+ * getOrCreatePropertyKey makes for a key the program sets without a schema, DefaultSchemaMaker
+ * .java:46-48), whose values carry their class (Long 13, Double 20, Integer 12).  Relation ids are
  * relation_id_base + the entry's running index (a block the caller reserved).
  * out == NULL: only *size is filled; otherwise out's buffers (sized from a first call) get
  * nrows keys, nrows+1 entry / byte offsets, nbytes bytes and nentries limit|valuePos words

@@ -16,6 +16,15 @@
 #define JFN(name) Java_com_thinkaurelius_titan_graphdb_olap_gpu_TgoNative_##name
 #define CTX(h) ((tgo_ctx*)(intptr_t)(h))
 
+/* Java arrays are indexed by jsize (int32): a result larger than that cannot be handed back
+ * as one array.  Raise IllegalStateException (pending on return) instead of truncating. */
+static int fits_jsize(JNIEnv* env, int64_t n, const char* what) {
+    if (n >= 0 && n <= INT32_MAX) return 1;
+    jclass ex = (*env)->FindClass(env, "java/lang/IllegalStateException");
+    if (ex) (*env)->ThrowNew(env, ex, what);
+    return 0;
+}
+
 JNIEXPORT jlong JNICALL JFN(create)(JNIEnv* env, jclass cls, jint device, jint pb, jint threads, jlong limit) {
     (void)env; (void)cls;
     tgo_options o;
@@ -135,6 +144,7 @@ JNIEXPORT jint JNICALL JFN(finishLoad)(JNIEnv* env, jclass cls, jlong h) {
 
 JNIEXPORT jlongArray JNICALL JFN(vertexIds)(JNIEnv* env, jclass cls, jlong h) {
     (void)cls;
+    if (!fits_jsize(env, tgo_num_vertices(CTX(h)), "more vertices than a Java array holds")) return NULL;
     jsize n = (jsize)tgo_num_vertices(CTX(h));
     jlongArray out = (*env)->NewLongArray(env, n);
     if (!out) return NULL;
@@ -145,6 +155,7 @@ JNIEXPORT jlongArray JNICALL JFN(vertexIds)(JNIEnv* env, jclass cls, jlong h) {
 }
 
 static jlongArray distances(JNIEnv* env, jlong h, int (*run)(tgo_ctx*, const void*, int64_t*), const void* args) {
+    if (!fits_jsize(env, tgo_num_vertices(CTX(h)), "more vertices than a Java array holds")) return NULL;
     jsize n = (jsize)tgo_num_vertices(CTX(h));
     jlongArray out = (*env)->NewLongArray(env, n);
     if (!out) return NULL;
@@ -182,6 +193,7 @@ JNIEXPORT jlongArray JNICALL JFN(sssp)(JNIEnv* env, jclass cls, jlong h, jlong s
 JNIEXPORT jdoubleArray JNICALL JFN(pageRank)(JNIEnv* env, jclass cls, jlong h, jdouble alpha, jlong vertex_count,
                                              jint iterations) {
     (void)cls;
+    if (!fits_jsize(env, tgo_num_vertices(CTX(h)), "more vertices than a Java array holds")) return NULL;
     jsize n = (jsize)tgo_num_vertices(CTX(h));
     jdoubleArray out = (*env)->NewDoubleArray(env, n);
     if (!out) return NULL;
@@ -198,6 +210,7 @@ JNIEXPORT jdoubleArray JNICALL JFN(pageRank)(JNIEnv* env, jclass cls, jlong h, j
 
 JNIEXPORT jintArray JNICALL JFN(walkCount)(JNIEnv* env, jclass cls, jlong h, jint length) {
     (void)cls;
+    if (!fits_jsize(env, tgo_num_vertices(CTX(h)), "more vertices than a Java array holds")) return NULL;
     jsize n = (jsize)tgo_num_vertices(CTX(h));
     jintArray out = (*env)->NewIntArray(env, n);
     if (!out) return NULL;
@@ -207,8 +220,9 @@ JNIEXPORT jintArray JNICALL JFN(walkCount)(JNIEnv* env, jclass cls, jlong h, jin
     return rc == TGO_OK ? out : NULL;
 }
 
-/* tgo_result_rows: {rowKeys, rowEntryBegin, rowByteBegin, entryLimitValuePos} as long[][] plus
- * the entry bytes in a new direct ByteBuffer (element 4), or NULL on error. */
+/* tgo_result_rows: Object[5] = {long[] rowKeys, long[] rowEntryBegin, long[] rowByteBegin,
+ * long[] entryLimitValuePos, byte[] entryBytes}, or NULL on error (status: lastError; a result
+ * beyond the int32 index range of a Java array: IllegalStateException). */
 JNIEXPORT jobjectArray JNICALL JFN(resultRows)(JNIEnv* env, jclass cls, jlong h, jint kind, jlongArray jkeys,
                                               jintArray jtypes, jlong relationIdBase) {
     (void)cls;
@@ -223,6 +237,10 @@ JNIEXPORT jobjectArray JNICALL JFN(resultRows)(JNIEnv* env, jclass cls, jlong h,
     tgo_result_size sz;
     memset(&sz, 0, sizeof sz);
     if (tgo_result_rows(CTX(h), &a, &sz, NULL) != TGO_OK) return NULL;
+    if (!fits_jsize(env, sz.nrows + 1, "result rows exceed a Java array") ||
+        !fits_jsize(env, sz.nentries, "result entries exceed a Java array") ||
+        !fits_jsize(env, sz.nbytes, "result bytes exceed a Java array (write back in smaller batches)"))
+        return NULL;
     int64_t* keys = (int64_t*)malloc((size_t)(sz.nrows + 1) * 8);
     int64_t* eb = (int64_t*)malloc((size_t)(sz.nrows + 1) * 8);
     int64_t* bb = (int64_t*)malloc((size_t)(sz.nrows + 1) * 8);
@@ -243,8 +261,12 @@ JNIEXPORT jobjectArray JNICALL JFN(resultRows)(JNIEnv* env, jclass cls, jlong h,
         }
         if (out) {
             jbyteArray data = (*env)->NewByteArray(env, (jsize)sz.nbytes);
-            if (data) (*env)->SetByteArrayRegion(env, data, 0, (jsize)sz.nbytes, (const jbyte*)bytes);
-            (*env)->SetObjectArrayElement(env, out, 4, data);
+            if (!data) {
+                out = NULL;                                  /* OutOfMemoryError is pending */
+            } else {
+                (*env)->SetByteArrayRegion(env, data, 0, (jsize)sz.nbytes, (const jbyte*)bytes);
+                (*env)->SetObjectArrayElement(env, out, 4, data);
+            }
         }
     }
     free(keys); free(eb); free(bb); free(lv); free(bytes);

@@ -24,6 +24,7 @@ import java.util.HashSet;
 import java.util.Map;
 import java.util.HashMap;
 import java.util.Set;
+import java.util.Optional;
 import java.util.concurrent.CompletableFuture;
 import java.util.concurrent.Future;
 
@@ -112,8 +113,12 @@ public class GpuGraphComputer implements TitanGraphComputer {
             GraphComputerHelper.validateProgramOnComputer(this, vertexProgram);
             mapReduces.addAll(vertexProgram.getMapReducers());
         }
-        final Persist persist = persistMode == null ? Persist.NOTHING : persistMode;
-        final ResultGraph resultGraph = resultGraphMode == null ? ResultGraph.ORIGINAL : resultGraphMode;
+        // unset modes come from the program's preference (FulgoraGraphComputer.java:133-135):
+        // PageRank / ShortestDistance persist into the original graph, DegreeCounter into NEW
+        final Persist persist = GraphComputerHelper.getPersistState(Optional.ofNullable(vertexProgram),
+                Optional.ofNullable(persistMode));
+        final ResultGraph resultGraph = GraphComputerHelper.getResultGraphState(Optional.ofNullable(vertexProgram),
+                Optional.ofNullable(resultGraphMode));
         if (!features().supportsResultGraphPersistCombination(resultGraph, persist))
             throw GraphComputer.Exceptions.resultGraphPersistCombinationNotSupported(resultGraph, persist);
         final DeviceProgram program = DeviceProgram.recognise(vertexProgram);
@@ -136,11 +141,18 @@ public class GpuGraphComputer implements TitanGraphComputer {
                 ScanMetrics m = scan.execute().get();
                 if (m.get(ScanMetrics.Metric.FAILURE) > 0)
                     throw new TitanException("Failed to process [" + m.get(ScanMetrics.Metric.FAILURE) + "] rows");
+                // a block whose flush failed in workerIterationEnd is only logged by the scanner
+                // (StandardScannerExecutor.java:278-282): the handle keeps that failure
+                handle.rethrowFailure();
                 TgoNative.check(ctx, TgoNative.finishLoad(ctx));
-                // (2) the program on the device; memory reports its iteration (FulgoraMemory.java:73-76)
+                // (2) the program on the device.  Fulgora runs supersteps 0..T (T = the first
+                // iteration whose terminate() holds: maxIterations, maxDepth, length) and
+                // increments the iteration after each of them, the terminating one included
+                // (FulgoraGraphComputer.java:181-188); complete() then steps back once
+                // (FulgoraMemory.java:73-76), so getIteration() reports T (OLAPTest.java:219,255)
                 long[] ids = TgoNative.vertexIds(ctx);
                 Map<String, Object> values = program.run(ctx);
-                for (int i = 0; i < program.iterations(); i++) memory.incrIteration();
+                for (int i = 0; i <= program.iterations(); i++) memory.incrIteration();
                 // (3) map / reduce / addResultToMemory as Fulgora's map phase
                 for (MapReduce mr : mapReduces) {
                     FulgoraMapEmitter emitter = new FulgoraMapEmitter<>(mr.doStage(MapReduce.Stage.REDUCE));
@@ -163,8 +175,9 @@ public class GpuGraphComputer implements TitanGraphComputer {
                 // (4) write-back of the compute keys
                 org.apache.tinkerpop.gremlin.structure.Graph result = graph;
                 if (persist == Persist.VERTEX_PROPERTIES) {
-                    if (resultGraph == ResultGraph.ORIGINAL) WriteBack.persist(graph, ctx, program);
-                    else result = WriteBack.localTx(graph, ids, values, program);
+                    if (resultGraph == ResultGraph.NEW) result = WriteBack.localTx(graph, ids, values, program);
+                    else if (WriteBack.directWriteSafe(graph, program)) WriteBack.persist(graph, ctx, program);
+                    else WriteBack.transactional(graph, ids, values, program, numThreads);
                 }
                 memory.setRuntime(System.currentTimeMillis() - start);
                 memory.complete();
@@ -192,6 +205,58 @@ public class GpuGraphComputer implements TitanGraphComputer {
     /** Compute-key write-back (FulgoraGraphComputer.java:248-305). */
     static final class WriteBack {
         static final int WRITE_BATCH_ROWS = 10000;
+
+        /**
+         * The device-encoded entries may go straight to the store only when nothing above the
+         * store keeps a copy of the properties: no graph index over a compute key (the
+         * transaction path maintains indexes) and no edgestore cache (cache.db-cache), which
+         * would keep serving the old values.  Otherwise {@link #transactional} writes them.
+         */
+        static boolean directWriteSafe(StandardTitanGraph graph, DeviceProgram program) {
+            if (graph.getConfiguration().getConfiguration()
+                    .get(com.thinkaurelius.titan.graphdb.configuration.GraphDatabaseConfiguration.DB_CACHE))
+                return false;
+            Set<String> keys = new HashSet<>(java.util.Arrays.asList(program.computeKeys()));
+            TitanManagement mgmt = graph.openManagement();
+            try {
+                for (com.thinkaurelius.titan.core.schema.TitanGraphIndex idx :
+                        mgmt.getGraphIndexes(org.apache.tinkerpop.gremlin.structure.Vertex.class))
+                    for (PropertyKey k : idx.getFieldKeys())
+                        if (keys.contains(k.name())) return false;
+                return true;
+            } finally {
+                mgmt.rollback();
+            }
+        }
+
+        /**
+         * Fulgora's own write path (VertexPropertyWriter, FulgoraGraphComputer.java:314-342):
+         * batched transactions of v.property(single, key, value), committed, so indexes and
+         * caches are maintained; a failed batch fails the job (:285-292).
+         */
+        static void transactional(StandardTitanGraph graph, long[] ids, Map<String, Object> values,
+                                  DeviceProgram program, int threads) {
+            for (int r0 = 0; r0 < ids.length; r0 += WRITE_BATCH_ROWS) {
+                com.thinkaurelius.titan.core.TitanTransaction tx = graph.buildTransaction().enableBatchLoading().start();
+                try {
+                    for (int i = r0; i < Math.min(ids.length, r0 + WRITE_BATCH_ROWS); i++) {
+                        org.apache.tinkerpop.gremlin.structure.Vertex v = null;
+                        for (Map.Entry<String, Object> kv : values.entrySet()) {
+                            Object x = program.valueAt(kv.getValue(), i);
+                            if (x == null) continue;
+                            if (v == null) v = tx.getVertex(ids[i]);
+                            v.property(org.apache.tinkerpop.gremlin.structure.VertexProperty.Cardinality.single,
+                                    kv.getKey(), x);
+                        }
+                    }
+                    tx.commit();
+                } catch (Exception e) {
+                    throw new TitanException("Could not persist program results to graph", e);
+                } finally {
+                    if (tx.isOpen()) tx.rollback();
+                }
+            }
+        }
 
         /** ResultGraph.ORIGINAL: device-encoded property entries as edgestore column overwrites. */
         static void persist(StandardTitanGraph graph, long ctx, DeviceProgram program) throws Exception {

@@ -62,6 +62,16 @@ public class CsrCollectingScanJob implements ScanJob {
         final int scope;
         final boolean applyCap;
         final long weightKey;
+        // the first failed flush: a TitanException thrown from workerIterationEnd escapes a
+        // processor's finally, where StandardScannerExecutor only logs it (:278-282) and counts
+        // no FAILURE, so the submitting thread must check it before tgo_finish_load
+        private volatile Throwable failure;
+
+        /** Throws the first flush failure of any clone (sticky). */
+        public void rethrowFailure() {
+            Throwable f = failure;
+            if (f != null) throw new com.thinkaurelius.titan.core.TitanException("a work block failed to load", f);
+        }
 
         public Handle(long ctx, IDManager idManager, long[] edgeTypes, long[] propertyKeys, int scope,
                       boolean applyCap, long[] labelIds, long weightKey) {
@@ -162,10 +172,17 @@ public class CsrCollectingScanJob implements ScanJob {
         long[] bb = java.util.Arrays.copyOf(byteBegin, rows + 1);
         long[] lv = java.util.Arrays.copyOf(limitValuePos, Math.max(entries, 1));
         synchronized (handle) {
-            TgoNative.check(handle.ctx, TgoNative.loadRows(handle.ctx, k, eb, bb, bytes, lv, handle.edgeTypes,
-                    handle.propertyKeys, handle.scope, handle.applyCap, handle.labelIds, handle.weightKey));
+            try {
+                if (handle.failure != null) return;       // the load is lost already: stop feeding it
+                TgoNative.check(handle.ctx, TgoNative.loadRows(handle.ctx, k, eb, bb, bytes, lv, handle.edgeTypes,
+                        handle.propertyKeys, handle.scope, handle.applyCap, handle.labelIds, handle.weightKey));
+            } catch (RuntimeException e) {
+                if (handle.failure == null) handle.failure = e;
+                throw e;
+            } finally {
+                reset();
+            }
         }
-        reset();
     }
 
     @Override

@@ -78,11 +78,13 @@ public final class TgoNative {
      */
     public static native Object[] resultRows(long ctx, int kind, long[] keyIds, int[] datatypes, long relationIdBase);
 
-    static void check(long ctx, int rc) {
+    /** A non-zero status of a C-ABI call as a TitanException carrying tgo_last_error(). */
+    public static void check(long ctx, int rc) {
         if (rc != 0) throw new TitanException("[" + rc + "] " + lastError(ctx));
     }
 
-    static <T> T checked(long ctx, T result) {
+    /** A null result of a C-ABI call (its status was non-zero) as a TitanException. */
+    public static <T> T checked(long ctx, T result) {
         if (result == null) throw new TitanException(lastError(ctx));
         return result;
     }

@@ -106,6 +106,7 @@ def load() -> C.CDLL:
         "fr_encode_property_f64": (C.c_int, [P(FrBuf), _i32p, C.c_int64, C.c_double, C.c_int64]),
         "fr_string_of": (C.c_int, [C.c_int64, P(C.c_uint16)]),
         "fr_encode_property": (C.c_int, [P(FrBuf), _i32p, C.c_int64, C.c_int, C.c_int64, C.c_int64]),
+        "fr_encode_property_generic": (C.c_int, [P(FrBuf), _i32p, C.c_int64, C.c_int, C.c_int64, C.c_int64]),
         "fr_decode_edge": (C.c_int, [_u8p, C.c_size_t, C.c_size_t, P(FrSchema), C.c_int64, _i64p,
                                      P(C.c_int), _i64p, _i64p, P(C.c_int), _i64p]),
         "fr_load_rows": (C.c_int, [P(FrRows), P(FrSchema), P(FrLoadOpts), P(vp), P(FrLoadStats)]),
@@ -189,6 +190,22 @@ def encode_property(key_id, datatype, value, relation_id):
     rc = lib.fr_encode_property(C.byref(b), C.byref(vp), key_id, datatype, value, relation_id)
     if rc:
         raise ValueError(f"fr_encode_property rc={rc}")
+    out = C.string_at(b.p, b.len)
+    lib.fr_buf_free(C.byref(b))
+    return out, vp.value
+
+
+def encode_property_generic(key_id, value_dt, value, relation_id):
+    """A generic (Object) key's entry; value_dt = the value's class (DT_INTEGER / LONG / DOUBLE)."""
+    import struct
+    lib = load()
+    b = FrBuf()
+    vp = C.c_int32(0)
+    if value_dt == 6:
+        value = struct.unpack("<q", struct.pack("<d", float(value)))[0]
+    rc = lib.fr_encode_property_generic(C.byref(b), C.byref(vp), key_id, value_dt, int(value), relation_id)
+    if rc:
+        raise ValueError(f"fr_encode_property_generic rc={rc}")
     out = C.string_at(b.p, b.len)
     lib.fr_buf_free(C.byref(b))
     return out, vp.value

@@ -403,6 +403,37 @@ int fr_encode_property_f64(fr_buf* out, int32_t* value_pos, int64_t key_id, doub
     return FR_OK;
 }
 
+/* A generic (Object-typed) property key — what DefaultSchemaMaker.makePropertyKey creates for a
+ * key the program sets without a schema (dataType(Object.class), DefaultSchemaMaker.java:46-48).
+ * AttributeUtil.hasGenericDataType(key) => EdgeSerializer.writePropertyValue :353-356 calls
+ * StandardSerializer.writeClassAndObject (:316-322): VariableLong.writePositive of the value
+ * class's registration number (registerClassInternal :66-82: Integer 12, Long 13, Double 20),
+ * then writeObjectNotNullInternal (:303-314): the class's serializer with NO null flag.
+ * value_dt is the value's class; a Double value is passed as its IEEE bits. */
+int fr_encode_property_generic(fr_buf* out, int32_t* value_pos, int64_t key_id, int value_dt,
+                               int64_t value, int64_t relation_id) {
+    int reg;
+    switch (value_dt) {
+    case FR_DT_INTEGER: reg = 12; break;
+    case FR_DT_LONG: reg = 13; break;
+    case FR_DT_DOUBLE: reg = 20; break;
+    default: return FR_E_UNSUPPORTED;
+    }
+    fr_write_relation_type(out, key_id, 0, 0, 0);                       /* EdgeSerializer.java:270-281 */
+    *value_pos = (int32_t)out->len;
+    fr_vl_write_positive(out, (uint64_t)reg);
+    if (value_dt == FR_DT_DOUBLE) put_be(out, (uint64_t)value, 8);      /* DoubleSerializer.write: raw bits */
+    else {
+        const size_t mark = out->len;
+        int rc = write_object(out, value_dt, 1, value, 0);
+        if (rc) return rc;
+        memmove(out->p + mark, out->p + mark + 1, out->len - mark - 1); /* no null flag */
+        out->len--;
+    }
+    fr_vl_write_positive(out, relation_id);
+    return FR_OK;
+}
+
 int fr_encode_edge(fr_buf* out, int32_t* value_pos, const fr_schema* schema, int64_t type_id,
                    int dir, int64_t other, int64_t relation_id, const fr_prop* props, int nprops) {
     /* EdgeSerializer.writeRelation :222-315 (edge branch :255-266) */

@@ -110,6 +110,11 @@ int fr_encode_property(fr_buf* out, int32_t* value_pos, int64_t key_id, int data
                        int64_t value, int64_t relation_id);
 /* The same for a Double-valued key (DoubleSerializer.write: the raw IEEE bits, :33-36). */
 int fr_encode_property_f64(fr_buf* out, int32_t* value_pos, int64_t key_id, double value, int64_t relation_id);
+/* The same for a generic (Object-typed) key: writeClassAndObject — the value class's
+ * registration number, then its serializer without a null flag (value_dt: INTEGER, LONG or
+ * DOUBLE, a Double passed as its IEEE bits). */
+int fr_encode_property_generic(fr_buf* out, int32_t* value_pos, int64_t key_id, int value_dt,
+                               int64_t value, int64_t relation_id);
 /* VertexExists system property entry (BaseKey.java:27-28), the first entry of every live row. */
 int fr_encode_vertex_exists(fr_buf* out, int32_t* value_pos, int64_t relation_id);
 /* Decode one edge entry.  weight_key==0: no weight.  Returns FR_OK / FR_E_CODEC. */

@@ -606,3 +606,58 @@ def test_distributed_drivers_on_subgroups():
         assert np.abs(np.concatenate([p["pr"] for p in parts]) - opr).sum() <= 1e-6
         osd, _ = og.shortest_distance(int(ids[roots[gid]]), n, 1, weighted=True)
         assert np.array_equal(np.concatenate([p["sssp"] for p in parts]), osd)
+
+
+def test_in_process_group_runs_the_real_drivers():
+    """InProcessGroup (one thread per rank, the drivers' collectives as thread rendezvous):
+    the same drivers over the numpy local steps give the oracle's results at world 2 and 4 —
+    the communicator the one-GPU GPU tests drive the HIP local steps with."""
+    import fulgora as fr
+    from titan_amd import rmat_edges
+    from titan_amd.distributed import (InProcessGroup, distributed_bfs, distributed_msbfs, distributed_pagerank,
+                                       distributed_sssp, partition_range)
+    scale = 8
+    n = 1 << scale
+    src, dst, w = rmat_edges(scale, 8, seed=29, weights=True)
+    og = fr.OracleGraph.from_edges(n, src, dst, w)
+    ids = (np.arange(n, dtype=np.int64) + 1) << 3
+    roots = [int(src[0]), int(dst[11])]
+    for world in (2, 4):
+        bes = [NumpyPartBackend(n, *partition_range(n, world, r), src, dst) for r in range(world)]
+        wbes = [NumpyPartBackend(n, *partition_range(n, world, r), src, dst, w=w, scope=1) for r in range(world)]
+
+        def body(rank, comm):
+            be = bes[rank]
+            d, reached, _ = distributed_bfs(be, roots[0], n, comm=comm)
+            r, _, _ = distributed_msbfs(be, roots, n, comm=comm)
+            lv = [np.where(be.mslvl[:, i] >= 0, be.mslvl[:, i], ABSENT) for i in range(len(roots))]
+            pr = distributed_pagerank(be, 0.85, n, 8, comm=comm)
+            sd, sreached, _ = distributed_sssp(wbes[rank], roots[1], 0, comm=comm)
+            return d, reached, r, lv, pr, sd, sreached
+
+        res = InProcessGroup(world).run(body)
+        od, _ = og.shortest_distance(int(ids[roots[0]]), n, 2)
+        assert np.array_equal(np.concatenate([x[0] for x in res]), od)
+        assert all(x[1][0] == int((od != ABSENT).sum()) for x in res)
+        for i, root in enumerate(roots):
+            o, _ = og.shortest_distance(int(ids[root]), n, 2)
+            assert np.array_equal(np.concatenate([x[3][i] for x in res]), o)
+            assert res[0][2][i] == int((o != ABSENT).sum())
+        opr, _ = og.pagerank(0.85, n, 8)
+        assert np.abs(np.concatenate([x[4] for x in res]) - opr).sum() <= 1e-6
+        osd, _ = og.shortest_distance(int(ids[roots[1]]), n, 1, weighted=True)
+        assert np.array_equal(np.concatenate([x[5] for x in res]), osd)
+
+
+def test_in_process_group_propagates_a_rank_failure():
+    from titan_amd.distributed import InProcessGroup
+
+    def body(rank, comm):
+        t = torch.ones(4)
+        if rank == 1:
+            raise ValueError("rank 1 fails")
+        comm.all_reduce(t)            # rank 0 would wait forever without the abort
+        return t
+
+    with pytest.raises(ValueError, match="rank 1 fails"):
+        InProcessGroup(2, timeout=30).run(body)

@@ -1,8 +1,10 @@
-"""GPU: the partitioned (multi-GPU) local steps of the HIP engine, driven by the same
-exchange driver as the real multi-GPU run.  The 1-GPU box has one device, so the ranks
-are simulated in ONE process: every "rank" is an Engine holding its partition, and a
-tiny in-process communicator performs the all-to-all / all-gather / all-reduce with
-torch ops on the device.  Results must equal the oracle bit-for-bit (BFS) / 1e-6 L1 (PR).
+"""GPU: the partitioned (multi-GPU) path — the REAL drivers of titan_amd/distributed.py
+(distributed_bfs / distributed_msbfs / distributed_sssp / distributed_pagerank) over the HIP
+local steps (HipPartBackend, titan_gpu_olap_part.h).  The 1-GPU box has one device, so the
+ranks run in ONE process: every rank is a thread with its own Engine (ctx, partition, HIP
+stream), and titan_amd.distributed.InProcessGroup performs the drivers' all-to-all /
+all-gather / all-reduce as thread rendezvous with torch ops on the device.  Results must equal
+the oracle bit-for-bit (BFS / SSSP levels and distances) or within 1e-6 L1 (PageRank).
 """
 import numpy as np
 import pytest
@@ -11,184 +13,40 @@ import torch
 import fulgora as fr
 from titan_amd import Engine, rmat_edges
 from titan_amd import _lib as L
-from titan_amd.distributed import HipPartBackend, exchange_stream, local_layout, partition_range
+from titan_amd.distributed import (HipPartBackend, InProcessGroup, distributed_bfs, distributed_msbfs,
+                                   distributed_pagerank, distributed_sssp, exchange_stream, local_layout,
+                                   pagerank_layout, partition_range)
+from titan_amd.engine import TitanException
 
 pytestmark = pytest.mark.gpu
 ABSENT = L.DIST_ABSENT
 
 
-def run_bfs(backends, seed, max_depth, alpha=15.0, beta=18.0):
-    """The distributed_bfs protocol with the collectives done in-process."""
-    world = len(backends)
-    n = backends[0].n_global
-    nwl = backends[0].n_local // 64
-    dev = backends[0].device
-    fb = [b.tensor(n // 64, torch.int64) for b in backends]
-    nb = [b.tensor(nwl, torch.int64) for b in backends]
-    disc = [b.tensor(n // 64, torch.int64) for b in backends]
-    recv = [b.tensor(n // 64, torch.int64) for b in backends]
+class Ranks:
+    """One Engine + HipPartBackend + HIP stream per simulated rank; run() drives a function
+    on every rank's thread with that rank's communicator."""
 
-    def allgather():
-        g = torch.cat(nb)
-        for t in fb:
-            t.copy_(g)
+    def __init__(self, world, n, src, dst, scope, weight=None, layout=False, apply_cap=False, hard_limit=100000,
+                 device_counts=False):
+        lay = None
+        if layout:
+            lay = np.concatenate([local_layout(src, dst, n, *partition_range(n, world, r)) for r in range(world)])
+            assert np.array_equal(np.sort(lay), np.arange(n))
+        self.world, self.streams, self.backends = world, [], []
+        for r in range(world):
+            lo, hi = partition_range(n, world, r)
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                eng = Engine(stream=s.cuda_stream, hard_query_limit=hard_limit).load_partition(
+                    n, lo, hi, src, dst, scope, weight=weight, apply_cap=apply_cap, layout=lay)
+                self.backends.append(HipPartBackend(eng, n, lo, hi, device_counts=device_counts))
+            self.streams.append(s)
 
-    total = sum(b.total_entries for b in backends)
-    c = sum(b.bfs_begin(seed, nb[i]) for i, b in enumerate(backends))
-    allgather()
-    nf, mf = c
-    mu = total - mf
-    bottom_up = False
-    for level in range(max_depth):
-        if nf == 0:
-            break
-        if not bottom_up and mf > mu / alpha:
-            bottom_up = True
-        elif bottom_up and nf < n / beta:
-            bottom_up = False
-        cs = []
-        if bottom_up:
-            for i, b in enumerate(backends):
-                cs.append(b.bfs_bu(level, fb[i], nb[i]))
-        else:
-            for i, b in enumerate(backends):
-                disc[i].zero_()
-                b.bfs_td(level, disc[i])
-            torch.cuda.synchronize()
-            for r in range(world):          # all_to_all_single: slice r of every sender -> rank r
-                recv[r].copy_(torch.cat([disc[s][r * nwl:(r + 1) * nwl] for s in range(world)]))
-            for i, b in enumerate(backends):
-                cs.append(b.bfs_claim(level, recv[i], world, nb[i]))
-        allgather()
-        nf, mf = sum(cs)
-        mu -= mf
-    outs = [b.bfs_end(True) for b in backends]
-    return np.concatenate([o[0] for o in outs]), sum(o[1] for o in outs)
-
-
-def run_msbfs(backends, seeds, max_depth, ms_alpha=12.0, sparse=False):
-    """The distributed_msbfs protocol with the collectives done in-process (sparse: the
-    packed-pair exchange of the sparse levels, tgo_part_ms_pack / ms_settle_pairs)."""
-    world = len(backends)
-    n = backends[0].n_global
-    nl = backends[0].n_local
-    fr_ = [b.tensor(nl, torch.int64) for b in backends]
-    frn = [b.tensor(nl, torch.int64) for b in backends]
-    fg = [b.tensor(n, torch.int64) for b in backends]
-    cand = [b.tensor(n, torch.int64) for b in backends]
-    recv = [b.tensor(2 * n + 2 * world if sparse else n, torch.int64) for b in backends]
-    send = [b.tensor(2 * n + 2 * world, torch.int64) for b in backends] if sparse else None
-    total = sum(b.total_entries for b in backends)
-    nf, mf = sum(b.ms_begin(seeds, fr_[i]) for i, b in enumerate(backends))
-    for level in range(max_depth):
-        if nf == 0:
-            break
-        cs = []
-        if mf * ms_alpha > total:
-            torch.cuda.synchronize()
-            g = torch.cat(fr_)
-            for t in fg:
-                t.copy_(g)
-            torch.cuda.synchronize()
-            for i, b in enumerate(backends):
-                cs.append(b.ms_pull(level, fg[i], frn[i]))
-        elif sparse == "fixed":         # tgo_part_ms_pack_fixed / ms_settle_fixed, equal splits
-            cap = int(min(mf, nl))
-            slot = 2 * (cap + 1)
-            for i, b in enumerate(backends):
-                b.ms_push(level, fr_[i], cand[i])
-                b.ms_pack_fixed(cand[i], send[i], world, cap)
-                assert int(torch.count_nonzero(cand[i])) == 0
-            torch.cuda.synchronize()
-            for r in range(world):      # all_to_all with equal splits: sender s's slot for rank r
-                recv[r][:world * slot].copy_(torch.cat([send[s][r * slot:(r + 1) * slot] for s in range(world)]))
-            torch.cuda.synchronize()
-            for i, b in enumerate(backends):
-                cs.append(b.ms_settle_fixed(level, recv[i], world, cap, frn[i]))
-        elif sparse:
-            counts = []
-            for i, b in enumerate(backends):
-                b.ms_push(level, fr_[i], cand[i])
-                counts.append(b.ms_pack(cand[i], send[i], world))
-                assert int(torch.count_nonzero(cand[i])) == 0        # pack clears what it packs
-            torch.cuda.synchronize()
-            offs = [np.concatenate([[0], np.cumsum(c)]) for c in counts]
-            for r in range(world):      # all_to_all with split sizes: sender s's run for rank r
-                parts = [send[s][2 * offs[s][r]:2 * offs[s][r + 1]] for s in range(world)]
-                got = torch.cat(parts)
-                recv[r][:got.numel()].copy_(got)
-            torch.cuda.synchronize()
-            for i, b in enumerate(backends):
-                cs.append(b.ms_settle_pairs(level, recv[i], [counts[s][i] for s in range(world)], frn[i]))
-        else:
-            for i, b in enumerate(backends):
-                cand[i].zero_()
-                b.ms_push(level, fr_[i], cand[i])
-            torch.cuda.synchronize()
-            for r in range(world):
-                recv[r].copy_(torch.cat([cand[s][r * nl:(r + 1) * nl] for s in range(world)]))
-            torch.cuda.synchronize()
-            for i, b in enumerate(backends):
-                cs.append(b.ms_settle(level, recv[i], world, frn[i]))
-        fr_, frn = frn, fr_
-        nf, mf = sum(cs)
-    ends = [b.ms_end(len(seeds)) for b in backends]
-    reached = sum(e[0] for e in ends)
-    levels = [np.concatenate([b.ms_levels(s) for b in backends]) for s in range(len(seeds))]
-    return levels, reached
-
-
-INT64_MAX = (1 << 63) - 1
-
-
-def run_sssp(backends, seed, delta):
-    """The distributed_sssp protocol with the collectives done in-process."""
-    world = len(backends)
-    n = backends[0].n_global
-    send = [b.tensor(2 * n, torch.int64) for b in backends]
-    recv = [b.tensor(2 * n, torch.int64) for b in backends]
-    st = [b.sssp_begin(seed, delta) for b in backends]
-    if delta <= 0:
-        delta = max(int(s[1]) for s in st)
-    q = [int(s[0]) for s in st]
-    thr = delta
-    while True:
-        if sum(q) == 0:
-            mn = min(int(b.sssp_pending_min()[0]) for b in backends)
-            if mn == INT64_MAX:
-                break
-            if mn >= thr:
-                thr = (mn // delta + 1) * delta
-            q = [int(b.sssp_extract(thr)[0]) for b in backends]
-            continue
-        sc = [b.sssp_relax(thr, send[i], world) for i, b in enumerate(backends)]
-        torch.cuda.synchronize()
-        npairs = []
-        for r in range(world):            # all_to_all_single: rank s's block r -> rank r
-            parts = [send[s][2 * int(sc[s][:r].sum()): 2 * int(sc[s][:r + 1].sum())] for s in range(world)]
-            cat = torch.cat(parts)
-            recv[r][:cat.numel()].copy_(cat)
-            npairs.append(cat.numel() // 2)
-        torch.cuda.synchronize()
-        q = [int(b.sssp_apply(thr, recv[r], npairs[r])[0]) for r, b in enumerate(backends)]
-    outs = [b.sssp_end(True) for b in backends]
-    return np.concatenate([o[0] for o in outs]), sum(o[1] for o in outs)
-
-
-def make_backends(world, n, src, dst, scope, weight=None, layout=False):
-    """One Engine per simulated rank; layout=True loads every rank with the all-gathered
-    degree-grouped layout (tgo_part_layout), as bench.py does."""
-    lay = None
-    if layout:
-        lay = np.concatenate([local_layout(src, dst, n, *partition_range(n, world, r)) for r in range(world)])
-        assert np.array_equal(np.sort(lay), np.arange(n))
-    backends = []
-    for r in range(world):
-        lo, hi = partition_range(n, world, r)
-        eng = Engine(stream=exchange_stream()).load_partition(
-            n, lo, hi, src, dst, scope, weight=weight, apply_cap=False, layout=lay)
-        backends.append(HipPartBackend(eng, n, lo, hi))
-    return backends
+    def run(self, fn):
+        def body(rank, comm):
+            torch.cuda.set_stream(self.streams[rank])
+            return fn(self.backends[rank], comm)
+        return InProcessGroup(self.world).run(body)
 
 
 @pytest.mark.parametrize("layout", [False, True])
@@ -197,139 +55,190 @@ def test_partitioned_delta_stepping(world, scope, layout):
     scale = 12
     n = 1 << scale
     src, dst, w = rmat_edges(scale, 16, seed=35, weights=True)
-    backends = make_backends(world, n, src, dst, scope, weight=w, layout=layout)
+    ranks = Ranks(world, n, src, dst, scope, weight=w, layout=layout)
     og = fr.OracleGraph.from_edges(n, src, dst, w)
     ids = (np.arange(n, dtype=np.int64) + 1) << 3
     for seed in (int(src[0]), int(dst[9])):
         od, _ = og.shortest_distance(int(ids[seed]), n, scope, weighted=True)
         for delta in (0, 1, 1 << 40):
-            d, reached = run_sssp(backends, seed, delta)
+            res = ranks.run(lambda be, comm: distributed_sssp(be, seed, delta, comm=comm))
+            d = np.concatenate([x[0] for x in res])
             assert np.array_equal(d, od), (seed, delta)
-            assert reached[0] == int((od != ABSENT).sum())
+            assert all(x[1][0] == int((od != ABSENT).sum()) for x in res)
+            assert len({x[2] for x in res}) == 1                  # every rank ran the same phases
 
 
+@pytest.mark.parametrize("device_counts", [False, True])
 @pytest.mark.parametrize("layout", [False, True])
 @pytest.mark.parametrize("world", [2, 4])
-def test_partitioned_multi_source_bfs(world, layout):
+def test_partitioned_multi_source_bfs(world, layout, device_counts):
     scale = 12
     n = 1 << scale
     src, dst, _ = rmat_edges(scale, 16, seed=33)
-    backends = make_backends(world, n, src, dst, L.SCOPE_BOTH_E, layout=layout)
+    ranks = Ranks(world, n, src, dst, L.SCOPE_BOTH_E, layout=layout, device_counts=device_counts)
+    nfixed = [0] * world
+    for r, be in enumerate(ranks.backends):                   # count the fixed-capacity exchanges
+        def counted(*a, _f=be.ms_pack_fixed, _r=r):
+            nfixed[_r] += 1
+            return _f(*a)
+        be.ms_pack_fixed = counted
     og = fr.OracleGraph.from_edges(n, src, dst)
     ids = (np.arange(n, dtype=np.int64) + 1) << 3
     rng = np.random.default_rng(5)
     seeds = [int(s) for s in rng.choice(n, 40, replace=False)] + [int(src[0])]
     expect = [og.shortest_distance(int(ids[s]), n, 2)[0] for s in seeds]
-    for ms_alpha, sparse in ((12.0, False), (12.0, True), (12.0, "fixed"), (1e9, False), (1e9, True), (1e9, "fixed"),
-                             (1e-9, False)):
-        levels, reached = run_msbfs(backends, seeds, n, ms_alpha, sparse)
+    # mixed levels with the default sparse exchange (fixed capacity), sized pairs (fixed=0),
+    # whole-slice all-to-all; always push in each form; always pull
+    for ms_alpha, sparse, fixed in ((12.0, True, None), (12.0, True, 0), (12.0, False, None), (1e9, True, None),
+                                    (1e9, True, 0), (1e9, False, None), (1e-9, True, None)):
+        def body(be, comm):
+            r, e, lv = distributed_msbfs(be, seeds, n, ms_alpha=ms_alpha, sparse_exchange=sparse,
+                                         fixed_exchange_bytes=fixed, comm=comm)
+            return r, [be.ms_levels(i) for i in range(len(seeds))]
+        res = ranks.run(body)
         for i, od in enumerate(expect):
-            assert np.array_equal(levels[i], od), (ms_alpha, i)
-            assert reached[i] == int((od != ABSENT).sum())
+            assert np.array_equal(np.concatenate([x[1][i] for x in res]), od), (ms_alpha, sparse, fixed, i)
+            assert all(x[0][i] == int((od != ABSENT).sum()) for x in res)
+    assert min(nfixed) > 0                                     # the fixed-capacity exchange ran on every rank
 
 
 @pytest.mark.parametrize("layout", [False, True])
 @pytest.mark.parametrize("world", [2, 4])
-def test_partitioned_bfs_and_pagerank(world, layout):
+def test_partitioned_bfs_and_plain_pagerank(world, layout):
     scale = 12
     n = 1 << scale
     src, dst, _ = rmat_edges(scale, 16, seed=31)
-    backends = make_backends(world, n, src, dst, L.SCOPE_BOTH_E, layout=layout)
+    ranks = Ranks(world, n, src, dst, L.SCOPE_BOTH_E, layout=layout)
     og = fr.OracleGraph.from_edges(n, src, dst)
     ids = (np.arange(n, dtype=np.int64) + 1) << 3
     for seed in (int(src[0]), int(dst[9]), int(src[100])):
+        od, _ = og.shortest_distance(int(ids[seed]), n, 2)
         for alpha in (15.0, 1e9):
-            d, reached = run_bfs(backends, seed, n, alpha=alpha)
-            od, _ = og.shortest_distance(int(ids[seed]), n, 2)
-            assert np.array_equal(d, od)
-            assert reached[0] == int((od != ABSENT).sum())
-    # PageRank: in-process all-gather of the contributions
+            res = ranks.run(lambda be, comm: distributed_bfs(be, seed, n, alpha=alpha, comm=comm))
+            assert np.array_equal(np.concatenate([x[0] for x in res]), od)
+            assert all(x[1][0] == int((od != ABSENT).sum()) for x in res)
+    # PageRank on the same partitions (the in-lists of a bothE load) with the plain
+    # rank-major all-gather: a bothE load is never cache-blocked (tgo_part_pr_blocked)
     iters = 10
-    cl = [b.tensor(b.n_local, torch.float64) for b in backends]
-    cg = [b.tensor(n, torch.float64) for b in backends]
-    for b, c in zip(backends, cl):
-        b.pr_begin(0.85, n, iters, c)
-    for _ in range(2, iters + 1):
-        torch.cuda.synchronize()
-        g = torch.cat(cl)
-        for t in cg:
-            t.copy_(g)
-        torch.cuda.synchronize()
-        for b, c, gg in zip(backends, cl, cg):
-            b.pr_step(gg, c)
-    pr = np.concatenate([b.pr_end(True) for b in backends])
+    assert set(ranks.run(lambda be, comm: pagerank_layout(be, comm=comm))) == {(0, n // world)}
+    res = ranks.run(lambda be, comm: distributed_pagerank(be, 0.85, n, iters, comm=comm))
+    pr = np.concatenate(res)
     opr, _ = og.pagerank(0.85, n, iters)
     fin = np.isfinite(opr)
     assert np.array_equal(np.isfinite(pr), fin)
     assert np.abs(pr[fin] - opr[fin]).sum() <= 1e-6
 
 
-def run_pagerank_blocked(backends, n, iters):
-    """distributed_pagerank's blocked protocol in-process: agree on the active span, build
-    the hot-first gathered layout, cold slices gathered before step_cold, hot slices before
-    step_hot."""
-    world = len(backends)
-    span = max(b.active_rows() for b in backends)
-    hots = {b.pr_layout(world, span) for b in backends}
-    assert len(hots) == 1
-    hot = hots.pop()
-    cl = [b.tensor(b.n_local, torch.float64) for b in backends]
-    cg = [b.tensor(world * span, torch.float64) for b in backends]
-    for b, c in zip(backends, cl):
-        b.pr_begin(0.85, n, iters, c)
-    for _ in range(2, iters + 1):
-        torch.cuda.synchronize()
-        cold = torch.cat([c[hot:span] for c in cl])
-        for t in cg:
-            t[world * hot:].copy_(cold)
-            t[:world * hot].fill_(float("nan"))          # the hot gather is still in flight
-        torch.cuda.synchronize()
-        for b, gg in zip(backends, cg):
-            b.pr_step_cold(gg)
-        torch.cuda.synchronize()
-        hotv = torch.cat([c[:hot] for c in cl])
-        for t in cg:
-            t[:world * hot].copy_(hotv)
-        torch.cuda.synchronize()
-        for b, c, gg in zip(backends, cl, cg):
-            b.pr_step_hot(gg, c)
-    return hot, span, np.concatenate([b.pr_end(True) for b in backends])
-
-
+@pytest.mark.parametrize("overlap", [True, False])
 @pytest.mark.parametrize("layout", [False, True])
 @pytest.mark.parametrize("world", [1, 2, 4])
-def test_partitioned_pagerank_cache_blocked(world, layout, monkeypatch):
-    """tgo_part_pr_blocked: the owned in-lists re-expressed in the hot-first gathered index
-    space and cache-blocked (small hot set / segments so every rank has hot rows, cold
-    pieces in several segments and entry-less rows past the span)."""
+def test_partitioned_pagerank(world, layout, overlap, monkeypatch):
+    """distributed_pagerank over inE lists: the plain all-gather and the cache-blocked
+    hot-first gathered layout (tgo_part_pr_blocked; small hot set / segments so every rank
+    has hot rows, cold pieces in several segments and entry-less rows past the span)."""
     monkeypatch.setenv("TGO_PR_HOT", "512")
     monkeypatch.setenv("TGO_PR_SEG", "256")
     scale = 12
     n = 1 << scale
     src, dst, _ = rmat_edges(scale, 16, seed=37)
-    backends = make_backends(world, n, src, dst, L.SCOPE_IN_E, layout=layout)
+    ranks = Ranks(world, n, src, dst, L.SCOPE_IN_E, layout=layout)
     og = fr.OracleGraph.from_edges(n, src, dst)
+    lays = ranks.run(lambda be, comm: pagerank_layout(be, comm=comm))
+    assert len(set(lays)) == 1
+    hot, span = lays[0]
+    assert hot == max(64, 512 // world // 64 * 64)
+    if layout:
+        assert span < n // world                               # entry-less rows are not exchanged
     for iters in (2, 10):
-        hot, span, pr = run_pagerank_blocked(backends, n, iters)
-        assert hot == max(64, 512 // world // 64 * 64)
-        if layout:
-            assert span < n // world                    # entry-less rows are not exchanged
+        opr, _ = og.pagerank(0.85, n, iters)
+        fin = np.isfinite(opr)
+        res = ranks.run(lambda be, comm: distributed_pagerank(be, 0.85, n, iters, layout=(hot, span), overlap=overlap,
+                                                              comm=comm))
+        pr = np.concatenate(res)
+        assert np.array_equal(np.isfinite(pr), fin)
+        assert np.abs(pr[fin] - opr[fin]).sum() <= 1e-6
+    be = ranks.backends[0]
+    with pytest.raises(TitanException):                        # rank property only after the last step
+        be.pr_begin(0.85, n, 5, be.tensor(be.n_local, torch.float64))
+        be.pr_end(True)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_partitioned_pagerank_capped(world, monkeypatch):
+    """The bench loads partitioned PageRank with the preload cap on: rows cut at the hard
+    limit in column order (QueryContainer.java:28,122), the same cut as one GPU and the oracle."""
+    monkeypatch.setenv("TGO_PR_HOT", "512")
+    monkeypatch.setenv("TGO_PR_SEG", "256")
+    scale = 12
+    n = 1 << scale
+    limit = 40
+    src, dst, _ = rmat_edges(scale, 16, seed=43)
+    ranks = Ranks(world, n, src, dst, L.SCOPE_IN_E, layout=True, apply_cap=True, hard_limit=limit)
+    og = fr.OracleGraph.from_edges(n, src, dst, hard_limit=limit)
+    trunc = sum(be.e.stats()["truncated_results"] for be in ranks.backends)
+    assert trunc == og.stats.truncated_results > 0
+    for iters in (3, 20):
+        res = ranks.run(lambda be, comm: distributed_pagerank(be, 0.85, n, iters, comm=comm))
+        pr = np.concatenate(res)
         opr, _ = og.pagerank(0.85, n, iters)
         fin = np.isfinite(opr)
         assert np.array_equal(np.isfinite(pr), fin)
         assert np.abs(pr[fin] - opr[fin]).sum() <= 1e-6
-    with pytest.raises(Exception):                      # rank property only after the last step
-        backends[0].pr_begin(0.85, n, 5, backends[0].tensor(backends[0].n_local, torch.float64))
-        backends[0].pr_end(True)
+    one = Engine(hard_query_limit=limit).load_edges(n, src, dst, L.SCOPE_IN_E, apply_cap=True)
+    assert one.stats()["truncated_results"] == trunc
+
+
+def test_fixed_exchange_overflow_fails_the_sweep():
+    """A fixed-capacity pack whose owner receives more pairs than `cap` fails tgo_part_ms_end
+    (the dropped pairs would give wrong levels); the flag does not leak into the next sweep."""
+    scale = 10
+    n = 1 << scale
+    src, dst, _ = rmat_edges(scale, 16, seed=47)
+    st = exchange_stream()
+    be = HipPartBackend(Engine(stream=st).load_partition(n, 0, n, src, dst, L.SCOPE_BOTH_E, apply_cap=False),
+                        n, 0, n)
+    deg = np.bincount(src, minlength=n) + np.bincount(dst, minlength=n)
+    seed = int(np.argmax(deg))
+    fr_ = be.tensor(n, torch.int64)
+    cand = be.tensor(n, torch.int64)
+    send = be.tensor(2 * n + 2, torch.int64)
+    be.ms_begin([seed], fr_)
+    be.ms_push(0, fr_, cand)
+    be.ms_pack_fixed(cand, send, 1, 1)                   # the hub's neighbours do not fit one pair
+    with pytest.raises(TitanException, match="capacity"):
+        be.ms_end(1)
+    og = fr.OracleGraph.from_edges(n, src, dst)
+    r, _, _ = distributed_msbfs_world1(be, [seed], n)
+    od, _ = og.shortest_distance(int((seed + 1) << 3), n, 2)
+    assert np.array_equal(be.ms_levels(0), od)
+    assert r[0] == int((od != ABSENT).sum())
+
+
+def distributed_msbfs_world1(be, seeds, n):
+    return InProcessGroup(1).run(lambda rank, comm: distributed_msbfs(be, seeds, n, comm=comm))[0]
+
+
+def test_partition_load_drops_the_last_programs_results():
+    """a partition load frees the scratch a finished program's results live in,
+    so tgo_result_rows must refuse afterwards instead of reading freed device memory."""
+    scale = 10
+    n = 1 << scale
+    src, dst, _ = rmat_edges(scale, 16, seed=53)
+    eng = Engine(stream=exchange_stream()).load_edges(n, src, dst, L.SCOPE_IN_E)
+    eng.bfs(int(src[0]), n, L.SCOPE_IN_E, seed_is_dense=True)
+    assert eng.result_rows(L.RESULT_DISTANCE, [(900 << 6) | 5], [L.DT_LONG], 1 << 20).nrows > 0
+    eng.load_partition(n, 0, n, src, dst, L.SCOPE_BOTH_E, apply_cap=False)
+    with pytest.raises(TitanException) as ei:
+        eng.result_rows(L.RESULT_DISTANCE, [(900 << 6) | 5], [L.DT_LONG], 1 << 20)
+    assert ei.value.code == L.TGO_E_STATE
 
 
 def test_drivers_on_a_real_world1_group(monkeypatch):
-    """The real drivers (titan_amd.distributed) on a one-rank RCCL group: device-resident
-    level counts (tgo_part_device_counts) for BFS / multi-source BFS, and the cache-blocked
-    PageRank exchange with the hot all-gather overlapping the cold phase."""
+    """The real drivers on a one-rank RCCL group (TorchComm over backend "nccl"): device-
+    resident level counts (tgo_part_device_counts) for BFS / multi-source BFS, and the
+    cache-blocked PageRank exchange with the hot all-gather overlapping the cold phase."""
     import socket
     import torch.distributed as dist
-    from titan_amd.distributed import (distributed_bfs, distributed_msbfs, distributed_pagerank, pagerank_layout)
     monkeypatch.setenv("TGO_PR_HOT", "512")
     monkeypatch.setenv("TGO_PR_SEG", "256")
     sock = socket.socket()

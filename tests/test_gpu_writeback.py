@@ -160,3 +160,60 @@ def test_persist_and_localtx_through_computer():
         assert graph.read_property(int(vid), EC, L.DT_DOUBLE) is not None
     # DegreeCounter values survive the later PageRank write (different keys, same rows)
     assert [graph.read_property(int(v), DEG, L.DT_INTEGER) for v in ids] == [int(x) for x in deg]
+
+
+def test_generic_key_rows_match_oracle_encoder(rmat_rows):
+    """Generic (Object) compute keys — what the default schema maker creates for a program's
+    keys: each value carries its class registration (StandardSerializer.writeClassAndObject)."""
+    rows, vids, sd, wkey, n = rmat_rows
+    eng = Engine(hard_query_limit=40).load_rows(rows, Schema.from_dict(sd), IN, weight_key=wkey)
+    ids = eng.vertex_ids()
+    d = eng.sssp(int(vids[1]), 4, IN)
+    got = eng.result_rows(L.RESULT_DISTANCE, [DIST], [L.DT_OBJECT], BASE)
+    assert_rows_equal(got, expected_rows(ids, lambda i, rel: [] if d[i] == L.DIST_ABSENT else
+                                         [fr.encode_property_generic(DIST, L.DT_LONG, int(d[i]), rel)]))
+    deg = eng.walkcount(3)
+    got = eng.result_rows(L.RESULT_DEGREE, [DEG], [L.DT_OBJECT], BASE)
+    assert_rows_equal(got, expected_rows(ids, lambda i, rel: [fr.encode_property_generic(DEG, L.DT_INTEGER,
+                                                                                         int(deg[i]), rel)]))
+    pr = eng.pagerank(0.85, n, 4)
+    o = fr.OracleGraph.from_rows(rows, fr.OracleSchema(sd["edge_types"], [(wkey, 3)]), IN, hard_limit=40)
+    off, mid, adj, _ = o.export()
+    outdeg = (mid - off[:-1]).astype(np.float64)
+    got = eng.result_rows(L.RESULT_PAGERANK, [PR, EC], [L.DT_DOUBLE, L.DT_OBJECT], BASE)   # one typed, one generic
+
+    def entries(i, rel):
+        kvs = sorted([(PR, pr[i]), (EC, outdeg[i])], key=lambda kv: fr.buf_bytes("fr_write_relation_type", kv[0], 0, 0, 0))
+        return [fr.encode_property_f64(k, v, rel + j) if k == PR else fr.encode_property_generic(k, L.DT_DOUBLE, v, rel + j)
+                for j, (k, v) in enumerate(kvs)]
+    assert_rows_equal(got, expected_rows(ids, entries))
+
+
+def test_unset_result_mode_follows_the_program_preference():
+    """No resultMode: ShortestDistance / PageRank persist their keys into the store (created
+    as generic keys: the graph has no schema for them), DegreeCounter holds them in a new
+    transaction (LOCALTX) and leaves the store unchanged; getIteration() reports T."""
+    rows, vids, sd, npz = load_fixture("gotg")
+    graph = GpuGraph(rows, sd)
+    seed = int(vids[list(npz["names"]).index("saturn")])
+    c = graph.compute()
+    c.program(ShortestDistanceVertexProgram(seed, 5, scope="inE", weighted=False))
+    res = c.submit().get()
+    assert res.memory().getIteration() == 5
+    key, dt = graph.property_key(ShortestDistanceVertexProgram.DISTANCE)
+    assert dt == L.DT_OBJECT
+    ids, dist = res.vertex_properties[ShortestDistanceVertexProgram.DISTANCE]
+    assert res.graph() is graph
+    for vid, d in zip(ids, dist):
+        assert graph.read_property(int(vid), key, L.DT_OBJECT) == (None if d == L.DIST_ABSENT else int(d))
+    before = graph.rows
+    for k in (1, 2):
+        c = graph.compute()
+        c.program(DegreeCounter(k))
+        res = c.submit().get()
+        assert res.memory().getIteration() == k                    # OLAPTest.java:219 (k = 1)
+        assert graph.rows is before                                 # LOCALTX: the store is unchanged
+        dkey, _ = graph.property_key(DegreeCounter.DEGREE)
+        ids, deg = res.vertex_properties[DegreeCounter.DEGREE]
+        assert [res.graph().read_property(int(v), dkey, L.DT_OBJECT) for v in ids] == [int(x) for x in deg]
+        assert graph.read_property(int(ids[0]), dkey, L.DT_OBJECT) is None

@@ -1,0 +1,69 @@
+"""CPU: the Java host layer's native boundary where no JDK exists.
+
+* java/jni/titan_gpu_olap_jni.c is compiled with gcc -fsyntax-only against the REAL C-ABI
+  header (include/titan_gpu_olap.h) and a minimal JNI declaration file (tests/jni_stub/jni.h,
+  the JNI specification's signatures), so a drift between the shim and the C-ABI fails here.
+* Every `native` method of TgoNative.java has exactly one JNI entry point in the shim, and
+  the Java side calls the natives and helpers it relies on with the visibility it needs.
+"""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SHIM = os.path.join(ROOT, "java", "jni", "titan_gpu_olap_jni.c")
+JAVA = os.path.join(ROOT, "java", "src", "main", "java", "com", "thinkaurelius", "titan", "graphdb", "olap")
+NATIVE = os.path.join(JAVA, "gpu", "TgoNative.java")
+COMPUTER = os.path.join(JAVA, "computer", "GpuGraphComputer.java")
+SCANJOB = os.path.join(JAVA, "gpu", "CsrCollectingScanJob.java")
+
+
+def _read(p):
+    with open(p) as f:
+        return f.read()
+
+
+@pytest.mark.skipif(shutil.which("gcc") is None, reason="needs gcc")
+def test_shim_type_checks_against_the_c_abi():
+    r = subprocess.run(["gcc", "-fsyntax-only", "-std=c11", "-Wall", "-Wextra", "-Werror", "-Wno-unused-parameter",
+                        "-I", os.path.join(ROOT, "tests", "jni_stub"), "-I", os.path.join(ROOT, "include"), SHIM],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+
+
+def test_every_native_method_has_one_entry_point():
+    java = _read(NATIVE)
+    natives = re.findall(r"\bnative\s+[\w\[\]<>]+\s+(\w+)\s*\(", java)
+    shim = re.findall(r"JNIEXPORT\s+\w+\s+JNICALL\s+JFN\((\w+)\)", _read(SHIM))
+    assert natives and sorted(natives) == sorted(shim)
+    assert len(set(shim)) == len(shim)
+
+
+def test_helpers_called_across_packages_are_public():
+    """GpuGraphComputer (package ...olap.computer) calls TgoNative.check / checked (package
+    ...olap.gpu): package-private helpers would not compile."""
+    java = _read(NATIVE)
+    for name in ("check", "checked"):
+        assert re.search(r"public\s+static\s+[\w<> ]*\b" + name + r"\s*\(", java), name
+    comp = _read(COMPUTER)
+    assert "TgoNative.check(" in comp and "TgoNative.checked(" in comp
+
+
+def test_computer_follows_fulgora_iteration_and_result_modes():
+    """Fulgora increments the iteration after every superstep 0..T (FulgoraGraphComputer.java:
+    181-188) and complete() steps back once (FulgoraMemory.java:73-76): T + 1 increments.  Unset
+    modes come from the program (GraphComputerHelper.getPersistState / getResultGraphState)."""
+    comp = _read(COMPUTER)
+    assert re.search(r"for \(int i = 0; i <= program\.iterations\(\); i\+\+\) memory\.incrIteration\(\);", comp)
+    assert "GraphComputerHelper.getPersistState(Optional.ofNullable(vertexProgram)" in comp
+    assert "GraphComputerHelper.getResultGraphState(Optional.ofNullable(vertexProgram)" in comp
+    assert "handle.rethrowFailure();" in comp.split("TgoNative.finishLoad(ctx)")[0]
+
+
+def test_scan_job_failures_are_sticky():
+    job = _read(SCANJOB)
+    assert "public void rethrowFailure()" in job
+    assert re.search(r"if \(handle\.failure == null\) handle\.failure = e;", job)

@@ -78,3 +78,56 @@ def test_read_property_integer_values():
     for val in (0, 1, -1, 2 ** 31 - 1, -2 ** 31):
         r = rows_of({v: [fr.encode_vertex_exists(1), fr.encode_property(deg, L.DT_INTEGER, val, 3)]})
         assert read_property(r, v, deg, L.DT_INTEGER) == val
+
+
+def test_generic_key_known_answer():
+    """A generic (Object) key's value: writeClassAndObject = VariableLong.writePositive of the
+    class registration (Long 13, Double 20, Integer 12; StandardSerializer.java:71-81) and the
+    serializer's bytes WITHOUT the null flag (:303-322) — hand-derived, then read back."""
+    key = uprop(900)
+    hdr = _relation_type_header(key)
+    b, vp = fr.encode_property_generic(key, L.DT_LONG, 5, 3)
+    assert vp == len(hdr) and b[:vp] == hdr
+    assert b[vp:] == bytes([0x80 | 13]) + (5 + (1 << 63)).to_bytes(8, "big") + bytes([0x83])
+    b, vp = fr.encode_property_generic(key, L.DT_INTEGER, -3, 3)
+    assert b[vp:] == bytes([0x80 | 12, 0x80 | 7, 0x83])     # convert2Unsigned(-3) = |-3| << 1 | 1 = 7 (VariableLong.java:112-115)
+    b, vp = fr.encode_property_generic(key, L.DT_DOUBLE, 0.5, 3)
+    assert b[vp:] == bytes([0x80 | 20]) + bytes.fromhex("3fe0000000000000") + bytes([0x83])
+    v = lib.fr_vertex_id(5, 0, 5)
+    for dt, val in ((L.DT_LONG, -(1 << 40)), (L.DT_INTEGER, 2 ** 31 - 1), (L.DT_DOUBLE, 1.0 / 3)):
+        r = rows_of({v: [fr.encode_vertex_exists(1), fr.encode_property_generic(key, dt, val, 7)]})
+        assert read_property(r, v, key, L.DT_OBJECT) == val
+
+
+def test_result_mode_defaults_follow_the_program():
+    """An unset resultMode takes the program's getPreferredResultGraph / getPreferredPersist
+    (FulgoraGraphComputer.java:133-135): PageRank / ShortestDistance persist into the original
+    graph (PageRankVertexProgram.java:103-110, ShortestDistanceVertexProgram.java:81-88),
+    DegreeCounter into a new one (OLAPTest.java:391-398); an explicit mode wins."""
+    from titan_amd import DegreeCounter, GpuGraph, PageRankVertexProgram, ShortestDistanceVertexProgram
+    from titan_amd.computer import TitanGraphComputer as TGC
+    from titan_amd.generic import GenericVertexProgram
+    g = GpuGraph(edges=(64, np.zeros(1, np.int32), np.ones(1, np.int32), None))
+    for prog, mode in ((PageRankVertexProgram(), TGC.ResultMode.PERSIST),
+                       (ShortestDistanceVertexProgram(8, 3), TGC.ResultMode.PERSIST),
+                       (DegreeCounter(2), TGC.ResultMode.LOCALTX),
+                       (GenericVertexProgram(), TGC.ResultMode.NONE)):
+        c = g.compute().program(prog)
+        assert c._result_mode() == (False, mode)
+        c.resultMode(TGC.ResultMode.NONE)
+        assert c._result_mode() == (True, TGC.ResultMode.NONE)
+    assert g.compute()._result_mode() == (False, TGC.ResultMode.NONE)
+
+
+def test_missing_compute_keys_become_generic_keys():
+    """getOrCreatePropertyKey with the default schema maker: an unknown compute key is created
+    generic (dataType(Object.class), DefaultSchemaMaker.java:46-48) with the next schema id."""
+    from titan_amd import GpuGraph
+    sd = {"edge_types": [{"type_id": lib.fr_schema_id(7, 1), "multiplicity": 0}], "property_keys": [[uprop(40), 3]]}
+    g = GpuGraph(edges=(64, np.zeros(1, np.int32), np.ones(1, np.int32), None), schema=sd,
+                 property_keys={"typed": (uprop(900), L.DT_LONG)})
+    assert g.property_key("typed") == (uprop(900), L.DT_LONG)
+    k1 = g.property_key("a")
+    k2 = g.property_key("b")
+    assert k1 == (uprop(901), L.DT_OBJECT) and k2 == (uprop(902), L.DT_OBJECT)
+    assert g.property_key("a") == k1                                   # created once

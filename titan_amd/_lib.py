@@ -27,6 +27,7 @@ TGO_E_COMM = -8
 SCOPE_OUT_E, SCOPE_IN_E, SCOPE_BOTH_E = 0, 1, 2
 MULTI, SIMPLE, MANY2ONE, ONE2MANY, ONE2ONE = 0, 1, 2, 3, 4
 DT_BYTE, DT_SHORT, DT_INTEGER, DT_LONG, DT_FLOAT, DT_DOUBLE, DT_BOOLEAN = 1, 2, 3, 4, 5, 6, 7
+DT_OBJECT = 11      # generic key (DefaultSchemaMaker: dataType(Object.class)); result write-back only
 DT_DATE, DT_CHARACTER, DT_STRING = 8, 9, 10
 ORDER_ASC, ORDER_DESC = 0, 1
 RESULT_DISTANCE, RESULT_PAGERANK, RESULT_DEGREE = 0, 1, 2

@@ -171,7 +171,16 @@ def read_property(rows, vid: int, key_id: int, datatype: int, pb: int = 5):
     for b, vpos in _row_entries(rows, int(idx[0])):
         if b[:vpos] != hdr:
             continue
-        if b[vpos] == 0xFF:
+        if datatype == L.DT_OBJECT:
+            # generic key: the value's class registration, then its serializer, no null flag
+            # (StandardSerializer.readClassAndObject :247-252; Long 13, Double 20, Integer 12)
+            cls = b[vpos] & 0x7F
+            if b[vpos] == 0x80:
+                return None
+            datatype = {13: L.DT_LONG, 20: L.DT_DOUBLE, 12: L.DT_INTEGER}.get(cls)
+            if datatype is None or not b[vpos] & 0x80:
+                raise TitanException(L.TGO_E_UNSUPPORTED, f"generic value class {b[vpos]}")
+        elif b[vpos] == 0xFF:
             return None
         v = b[vpos + 1:]
         if datatype == L.DT_LONG:
@@ -217,9 +226,24 @@ class ComputerResult:
 
 
 # ----------------------------------------------------------------------------- programs
+class ResultGraph(enum.Enum):          # GraphComputer.ResultGraph
+    ORIGINAL = 0
+    NEW = 1
+
+
+class Persist(enum.Enum):              # GraphComputer.Persist
+    NOTHING = 0
+    VERTEX_PROPERTIES = 1
+    EDGES = 2
+
+
 class VertexProgram:
     scope_name = "bothE"
     compute_keys: tuple = ()
+    # getPreferredResultGraph / getPreferredPersist: what submit() uses when resultMode was
+    # not set (FulgoraGraphComputer.java:133-135, GraphComputerHelper.getPersistState)
+    preferred_result_graph = ResultGraph.ORIGINAL
+    preferred_persist = Persist.VERTEX_PROPERTIES
 
 
 class ShortestDistanceVertexProgram(VertexProgram):
@@ -326,6 +350,7 @@ class DegreeCounter(VertexProgram):
     DEGREE = "degree"
     compute_keys = (DEGREE,)
     scope_name = "inE"
+    preferred_result_graph = ResultGraph.NEW          # OLAPTest.java:391-398
 
     def __init__(self, length=1):
         if length <= 0:
@@ -415,6 +440,7 @@ class GpuGraph:
         # compute-key name -> (PropertyKey schema id, tgo datatype): the typed keys write-back uses
         self.property_keys = dict(property_keys or {})
         self._next_relation_id = relation_id_base     # the IDAuthority block result writes draw from
+        self._schema_dict = schema if isinstance(schema, dict) else None
         self.schema = schema if (schema is None or isinstance(schema, Schema)) else Schema.from_dict(schema)
         self.edges = edges       # (n, src, dst, weight) decoded-adjacency input
         self.device = device
@@ -426,6 +452,22 @@ class GpuGraph:
 
     def compute(self):
         return GpuGraphComputer(self)
+
+    def property_key(self, name):
+        """(schema id, tgo datatype) of a compute key; a key the graph has no schema for is
+        created the way getOrCreatePropertyKey does with the default schema maker: a generic
+        key, dataType(Object.class) (DefaultSchemaMaker.java:46-48), whose values carry their
+        class.  Ids continue after the largest schema id in use."""
+        with self._lock:
+            k = self.property_keys.get(name)
+            if k is None:
+                used = [int(i) >> 6 for i, _ in self.property_keys.values()]
+                if self._schema_dict is not None:
+                    used += [int(t["type_id"]) >> 6 for t in self._schema_dict.get("edge_types", [])]
+                    used += [int(p[0]) >> 6 for p in self._schema_dict.get("property_keys", [])]
+                k = (((max(used, default=0) + 1) << 6) | 5, L.DT_OBJECT)     # IDManager: UserPropertyKey
+                self.property_keys[name] = k
+            return k
 
     def reserve_relation_ids(self, count):
         with self._lock:
@@ -475,7 +517,7 @@ class GpuGraphComputer(TitanGraphComputer):
         self._program = None
         self._map_reduces = []
         self._workers = 1
-        self._mode = TitanGraphComputer.ResultMode.NONE
+        self._mode = None                # unset: the program's preference (see _result_mode)
         self._executed = False
         self.weight_keys = {}            # weight property name -> key id (schema lookup)
 
@@ -499,23 +541,38 @@ class GpuGraphComputer(TitanGraphComputer):
                                                                 PageRankVertexProgram.OUTGOING_EDGE_COUNT)),
                     DegreeCounter: (L.RESULT_DEGREE, (DegreeCounter.DEGREE,))}
 
+    def _result_mode(self):
+        """resultMode if set, else the program's preferred (ResultGraph, Persist) as Fulgora
+        takes them (FulgoraGraphComputer.java:133-135): PageRank and ShortestDistance persist
+        into the original graph, DegreeCounter into a new one (LOCALTX); no program: NONE.
+        (whether the mode was explicit, the mode)"""
+        if self._mode is not None:
+            return True, self._mode
+        p = self._program
+        if p is None or getattr(p, "preferred_persist", None) in (None, Persist.NOTHING):
+            return False, TitanGraphComputer.ResultMode.NONE
+        if getattr(p, "preferred_result_graph", ResultGraph.ORIGINAL) == ResultGraph.NEW:
+            return False, TitanGraphComputer.ResultMode.LOCALTX
+        return False, TitanGraphComputer.ResultMode.PERSIST
+
     def _write_back(self, eng):
         """Encode the last program's compute keys on the device (tgo_result_rows) and persist
         them (PERSIST) or hand them to a local transaction (LOCALTX)."""
-        if self._mode == TitanGraphComputer.ResultMode.NONE:
+        explicit, mode = self._result_mode()
+        if mode == TitanGraphComputer.ResultMode.NONE:
+            return self.graph
+        if self.graph.rows is None and not explicit:
+            # a graph given as an already-decoded adjacency has no store to write into: the
+            # program's preference cannot apply (an explicit PERSIST / LOCALTX still fails)
             return self.graph
         spec = self._RESULT_KEYS.get(type(self._program))
         if spec is None:
             raise TitanException(L.TGO_E_UNSUPPORTED, f"write-back of {type(self._program).__name__} compute keys")
         kind, names = spec
-        missing = [k for k in names if k not in self.graph.property_keys]
-        if missing:
-            raise TitanException(L.TGO_E_UNSUPPORTED, f"compute keys {missing} have no typed PropertyKey "
-                                                      "(getOrCreatePropertyKey would make them generic Object keys)")
-        keys = [self.graph.property_keys[k] for k in names]
+        keys = [self.graph.property_key(k) for k in names]
         base = self.graph.reserve_relation_ids(eng.n * len(keys))
         rows = eng.result_rows(kind, [k for k, _ in keys], [d for _, d in keys], base)
-        if self._mode == TitanGraphComputer.ResultMode.PERSIST:
+        if mode == TitanGraphComputer.ResultMode.PERSIST:
             self.graph.persist(rows)
             return self.graph
         return LocalTxGraph(self.graph, rows)
@@ -593,7 +650,7 @@ class GpuGraphComputer(TitanGraphComputer):
                 raise TitanException(L.TGO_E_INVALID, f"weight property '{p.weight_property}' has no key id")
         eng = self.graph.engine_for(scope, wk)
         memory = FulgoraMemory(tuple(p.memory_compute_keys) + tuple(mr.memory_key for mr in self._map_reduces))
-        if self._mode != TitanGraphComputer.ResultMode.NONE:
+        if self._result_mode()[1] != TitanGraphComputer.ResultMode.NONE:
             raise TitanException(L.TGO_E_UNSUPPORTED, "write-back of a generic program's compute keys")
         verts = run_generic(eng, p, memory)
         memory.setRuntime((time.perf_counter() - t0) * 1000.0)

@@ -110,6 +110,7 @@ void free_graph(tgo_ctx* ctx) {
     ctx->g = DevGraph();
     ctx->sc = Scratch();
     ctx->loaded = false;
+    ctx->res_kind = -1;         // the last program's results lived in the freed scratch
 }
 
 int threads_of(const tgo_ctx* ctx) {
@@ -1390,10 +1391,7 @@ int tgo_part_bfs_end(tgo_ctx* ctx, int64_t* dist_local, int64_t* reached) {
         HIP_TRY(k_unpermute_i64(s.dist, g.perm, s.msg, g.n, st));
         HIP_TRY(hipMemcpyAsync(dist_local, s.msg, g.n * sizeof(int64_t), hipMemcpyDeviceToHost, st));
     }
-    int ovf = 0;
-    if (s.pk_ovf) HIP_TRY(hipMemcpyAsync(&ovf, s.pk_ovf, sizeof(int), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
-    if (ovf) return fail(ctx, TGO_E_STATE, "ms_pack_fixed: an owner's pairs exceeded the capacity (cap below the level's frontier entries)");
     float ms = 0;
     HIP_TRY(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
     ctx->st.last_kernel_ms = ms;
@@ -1662,7 +1660,12 @@ int tgo_part_ms_end(tgo_ctx* ctx, int64_t* reached, int64_t* entries) {
             if (entries) entries[r] = static_cast<int64_t>(h[TGO_MAX_SOURCES + r]);
         }
     }
+    // the fixed-capacity exchange (tgo_part_ms_pack_fixed) drops the pairs past an owner's
+    // capacity: a sweep that overflowed has wrong levels and fails here
+    int ovf = 0;
+    if (s.pk_ovf) HIP_TRY(hipMemcpyAsync(&ovf, s.pk_ovf, sizeof(int), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
+    if (ovf) return fail(ctx, TGO_E_STATE, "ms_pack_fixed: an owner's pairs exceeded the capacity (cap below the level's frontier entries)");
     float ms = 0;
     HIP_TRY(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
     ctx->st.last_kernel_ms = ms;

@@ -160,9 +160,11 @@ int stage_rows_raw(RowStaging& st, const tgo_rows* rows, const tgo_schema* schem
     if (int rc = staging_begin(st, opts, err)) return rc;
     if (first) { st.plan = hp; st.plan_bytes = pb; }
     else if (pb != st.plan_bytes) { err = "tgo_schema differs between row batches"; return TGO_E_INVALID; }
+    // a new load starts from empty device buffers even when its first block has no rows (an
+    // earlier load aborted mid-batch may have left the counters behind)
+    if (first) ds.bytes_used = ds.lv_used = 0;
     const int64_t nrows = rows->nrows;
     if (nrows == 0) return TGO_OK;
-    if (first) ds.bytes_used = ds.lv_used = 0;
     const int64_t nent = rows->row_entry_begin[nrows] - rows->row_entry_begin[0];
     const int64_t nbytes = rows->row_byte_begin[nrows] - rows->row_byte_begin[0];
     if (nent < 0 || nbytes < 0) { err = "row offsets decrease"; return TGO_E_INVALID; }

@@ -46,6 +46,8 @@ struct ResArgs {
     uint8_t hdr[2][12];     // column bytes of each key, in column order
     int hlen[2];
     int slot[2];            // value slot of the key in that column position (0 = primary value, 1 = edge count)
+    uint8_t lead[2];        // first value byte: 0x00 = the null flag of a typed key; a generic key's
+                            // class registration (writePositive(13 / 20 / 12) = 0x8D / 0x94 / 0x8C)
     int64_t rel_base;
 };
 
@@ -116,7 +118,7 @@ __global__ void res_write(ResArgs a, const int32_t* perm, const void* v0, const 
         uint8_t* const ent = p;
         for (int i = 0; i < a.hlen[j]; ++i) *p++ = a.hdr[j][i];
         const int64_t vpos = p - ent;
-        *p++ = 0x00;                                   // StandardSerializer: not null
+        *p++ = a.lead[j];                              // null flag (typed key) or value class (generic key)
         if (a.kind == TGO_RESULT_DEGREE) {
             p = put_pos(p, zigzag(static_cast<int64_t>(bits)));
         } else {
@@ -166,10 +168,17 @@ int encode_results(const ResultSource& src, const tgo_result_args* a, const int3
     ra.nkeys = a->kind == TGO_RESULT_PAGERANK ? 2 : 1;
     ra.rel_base = a->relation_id_base;
     static const int want[3][2] = {{TGO_DT_LONG, 0}, {TGO_DT_DOUBLE, TGO_DT_DOUBLE}, {TGO_DT_INTEGER, 0}};
+    // StandardSerializer registration numbers of the value classes (:71-81): Long 13, Double 20, Integer 12
+    static const uint8_t reg[3] = {0x80 | 13, 0x80 | 20, 0x80 | 12};
+    if (a->kind < TGO_RESULT_DISTANCE || a->kind > TGO_RESULT_DEGREE) { err = "unknown result kind"; return TGO_E_INVALID; }
+    uint8_t lead[2] = {0, 0};
     for (int k = 0; k < ra.nkeys; ++k) {
         if ((a->key_ids[k] & 63) != 5 || (a->key_ids[k] >> 6) <= 0) { err = "compute key is not a user property key id"; return TGO_E_INVALID; }
-        if (a->datatypes[k] != want[a->kind][k]) {
-            err = "compute key datatype must be Long (distance), Double (pageRank, edgeCount) or Integer (degree)";
+        if (a->datatypes[k] == TGO_DT_OBJECT) {
+            lead[k] = reg[a->kind];                     // generic key: writeClassAndObject
+        } else if (a->datatypes[k] != want[a->kind][k]) {
+            err = "compute key datatype must be Long (distance), Double (pageRank, edgeCount), Integer (degree) "
+                  "or generic (Object)";
             return TGO_E_UNSUPPORTED;
         }
     }
@@ -188,6 +197,7 @@ int encode_results(const ResultSource& src, const tgo_result_args* a, const int3
         std::memcpy(ra.hdr[j], h[order[j]], 12);
         ra.hlen[j] = hl[order[j]];
         ra.slot[j] = order[j];
+        ra.lead[j] = lead[order[j]];
     }
     // scratch: A = row flags, B = their scan (output row index), C = entries per row then
     // byte sizes, D = entry scan; byte scan into A (free once B holds the row scan)

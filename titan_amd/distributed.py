@@ -35,6 +35,137 @@ import torch.distributed as dist
 from . import _lib as L
 
 
+class TorchComm:
+    """The collectives the drivers issue, over a torch.distributed group: backend "nccl"
+    (RCCL over xGMI) on MI355X, "gloo" in the CPU tests.  All on torch's current stream."""
+
+    _OPS = {"sum": dist.ReduceOp.SUM, "min": dist.ReduceOp.MIN, "max": dist.ReduceOp.MAX}
+
+    def __init__(self, group=None):
+        self.group = group
+
+    @property
+    def world(self) -> int:
+        return dist.get_world_size(self.group)
+
+    @property
+    def rank(self) -> int:
+        return dist.get_rank(self.group)
+
+    def all_gather_into_tensor(self, out, inp, async_op=False):
+        return dist.all_gather_into_tensor(out, inp, group=self.group, async_op=async_op)
+
+    def all_to_all_single(self, out, inp, output_split_sizes=None, input_split_sizes=None):
+        dist.all_to_all_single(out, inp, output_split_sizes=output_split_sizes, input_split_sizes=input_split_sizes,
+                               group=self.group)
+
+    def all_reduce(self, t, op="sum"):
+        dist.all_reduce(t, op=self._OPS[op], group=self.group)
+
+
+class _Done:
+    def wait(self):
+        return None
+
+
+class InProcessGroup:
+    """`world` ranks in ONE process, one Python thread each (InProcessGroup.run): every rank
+    runs the real driver over its own backend (its own ctx and HIP stream), and the
+    collectives are rendezvous of the threads that copy / reduce with torch ops.  What the
+    one-GPU box can run of the partitioned path: the drivers' exchange protocol against the
+    HIP local steps (tests/test_gpu_distributed.py)."""
+
+    def __init__(self, world: int, timeout: float = 300.0):
+        import threading
+        self.world = world
+        self._bar = threading.Barrier(world, timeout=timeout)
+        self._slots = [None] * world
+
+    def comm(self, rank: int) -> "InProcessComm":
+        return InProcessComm(self, rank)
+
+    def run(self, fn):
+        """fn(rank, comm) on every rank's thread; returns the results in rank order and
+        re-raises the first failure (the rendezvous is aborted so no rank waits forever)."""
+        import threading
+        res, errs = [None] * self.world, [None] * self.world
+
+        def body(r):
+            try:
+                res[r] = fn(r, self.comm(r))
+            except BaseException as e:          # noqa: BLE001 — re-raised in the caller
+                errs[r] = e
+                self._bar.abort()
+
+        th = [threading.Thread(target=body, args=(r,), daemon=True) for r in range(self.world)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        first = next((e for e in errs if e is not None and not isinstance(e, threading.BrokenBarrierError)), None)
+        if first is None:
+            first = next((e for e in errs if e is not None), None)
+        if first is not None:
+            raise first
+        return res
+
+
+class InProcessComm:
+    """One rank's view of an InProcessGroup (the TorchComm interface)."""
+
+    def __init__(self, grp: InProcessGroup, rank: int):
+        self.g, self.rank, self.world = grp, rank, grp.world
+
+    @staticmethod
+    def _sync(t):
+        if t.is_cuda:
+            torch.cuda.current_stream(t.device).synchronize()
+
+    def _rendezvous(self, t, item, compute):
+        """Publish `item` (after this rank's stream has produced t), compute this rank's
+        result from every rank's item, and wait until every rank has finished reading."""
+        self._sync(t)
+        self.g._slots[self.rank] = item
+        self.g._bar.wait()
+        compute(list(self.g._slots))
+        self._sync(t)
+        self.g._bar.wait()
+
+    def all_gather_into_tensor(self, out, inp, async_op=False):
+        def compute(items):
+            out.copy_(torch.cat([x.to(out.device) for x in items]))
+        self._rendezvous(out, inp, compute)
+        return _Done() if async_op else None
+
+    def all_to_all_single(self, out, inp, output_split_sizes=None, input_split_sizes=None):
+        w = self.world
+        ins = list(input_split_sizes) if input_split_sizes is not None else [inp.numel() // w] * w
+
+        def compute(items):
+            parts = []
+            for x, splits in items:
+                off = int(sum(splits[:self.rank]))
+                parts.append(x[off:off + int(splits[self.rank])].to(out.device))
+            got = torch.cat(parts)
+            if output_split_sizes is not None and got.numel() != int(sum(output_split_sizes)):
+                raise RuntimeError("all_to_all_single: output split sizes do not match the senders'")
+            if got.numel() > out.numel():
+                raise RuntimeError("all_to_all_single: output too small")
+            out[:got.numel()].copy_(got)
+        self._rendezvous(out, (inp, ins), compute)
+
+    def all_reduce(self, t, op="sum"):
+        def compute(items):
+            st = torch.stack([x.to(t.device) for x in items])
+            r = st.sum(0) if op == "sum" else (st.min(0).values if op == "min" else st.max(0).values)
+            t.copy_(r)
+        self._rendezvous(t, t.clone(), compute)
+
+
+def _comm(comm, group):
+    return comm if comm is not None else TorchComm(group)
+
+
 def partition_range(n_global: int, world: int, rank: int):
     """Contiguous owned range; every slice is a whole number of 64-bit bitmap words."""
     if n_global % (64 * world):
@@ -57,12 +188,12 @@ def local_layout(src, dst, n_global: int, lo: int, hi: int, threads: int = 16):
     return out
 
 
-def all_gather_layout(src, dst, n_global: int, lo: int, hi: int, device, group=None, threads: int = 16):
+def all_gather_layout(src, dst, n_global: int, lo: int, hi: int, device, group=None, threads: int = 16, comm=None):
     """Every rank's local_layout slice, all-gathered into the global layout (host int32,
     n_global) that every rank passes to Engine.load_partition(layout=...)."""
     loc = torch.from_numpy(local_layout(src, dst, n_global, lo, hi, threads)).to(device)
     out = torch.empty(n_global, dtype=torch.int32, device=device)
-    dist.all_gather_into_tensor(out, loc, group=group)
+    _comm(comm, group).all_gather_into_tensor(out, loc)
     return out.cpu().numpy()
 
 
@@ -76,7 +207,8 @@ def _splitmix64(x: int) -> int:
     return x ^ (x >> 31)
 
 
-def pick_roots_partitioned(n_global: int, src, dst, lo: int, hi: int, nroots: int, seed: int, device, group=None):
+def pick_roots_partitioned(n_global: int, src, dst, lo: int, hi: int, nroots: int, seed: int, device, group=None,
+                           comm=None):
     """The roots tgo_pick_roots draws on the whole edge list (synth.cpp), from a rank's
     partition edges: owned "has an entry" flags are all-gathered (n bytes), then every rank
     walks the same splitmix64 candidate sequence — the partitioned bench runs the same
@@ -87,7 +219,7 @@ def pick_roots_partitioned(n_global: int, src, dst, lo: int, hi: int, nroots: in
         has[x[(x >= lo) & (x < hi)] - lo] = 1
     loc = torch.from_numpy(has).to(device)
     out = torch.empty(n_global, dtype=torch.uint8, device=device)
-    dist.all_gather_into_tensor(out, loc, group=group)
+    _comm(comm, group).all_gather_into_tensor(out, loc)
     has = out.cpu().numpy()
     if int(has.sum()) < nroots:
         raise ValueError("fewer vertices with entries than roots")
@@ -102,12 +234,13 @@ def pick_roots_partitioned(n_global: int, src, dst, lo: int, hi: int, nroots: in
     return roots
 
 
-def entry_imbalance(entries_local: int, device, group=None):
+def entry_imbalance(entries_local: int, device, group=None, comm=None):
     """Per-rank owned entries, all-gathered: (list, max / mean) — the load imbalance of the
     1-D partition."""
+    cm = _comm(comm, group)
     t = torch.tensor([int(entries_local)], dtype=torch.int64, device=device)
-    out = torch.empty(dist.get_world_size(group), dtype=torch.int64, device=device)
-    dist.all_gather_into_tensor(out, t, group=group)
+    out = torch.empty(cm.world, dtype=torch.int64, device=device)
+    cm.all_gather_into_tensor(out, t)
     e = [int(x) for x in out.cpu()]
     mean = sum(e) / len(e)
     return e, (max(e) / mean if mean else 1.0)
@@ -300,26 +433,27 @@ def _scratch(backend, name, n, dtype):
     return t[:n]
 
 
-def _allreduce_counts(c, device, group):
-    """Global sums of per-rank counters (frontier size / entries, reached, ...) over `group`.
+def _allreduce_counts(c, device, comm):
+    """Global sums of per-rank counters (frontier size / entries, reached, ...) over `comm`.
     A device tensor (HipPartBackend device_counts) is reduced in place and read once per level
     together with the rank's own queue length, which goes back to the engine."""
     be = getattr(c, "_tgo_backend", None)
     if be is not None:
-        dist.all_reduce(c[:2], group=group)
+        comm.all_reduce(c[:2])
         v = c.cpu().numpy()
         be.e.part_call("tgo_part_set_local_qlen", C.c_int64(int(v[2])))
         return v[:2]
     t = c if isinstance(c, torch.Tensor) else torch.tensor(c, dtype=torch.int64, device=device)
-    dist.all_reduce(t, group=group)
+    comm.all_reduce(t)
     return t.cpu().numpy()
 
 
 def distributed_bfs(backend, seed: int, max_depth: int, alpha: float = 15.0, beta: float = 18.0,
-                    fetch: bool = True, stats: bool = True, group=None):
+                    fetch: bool = True, stats: bool = True, group=None, comm=None):
     """ShortestDistance with unit weights over bothE on a vertex-partitioned graph.
     Returns (local distances or None, global reached [vertices, entries] or None, levels)."""
-    world = dist.get_world_size(group)
+    cm = _comm(comm, group)
+    world = cm.world
     nwl = backend.n_local // 64
     nwg = backend.n_global // 64
     dev = backend.device
@@ -327,10 +461,10 @@ def distributed_bfs(backend, seed: int, max_depth: int, alpha: float = 15.0, bet
     nb_local = _scratch(backend, "bfs_nb", nwl, torch.int64)
     disc = _scratch(backend, "bfs_disc", nwg, torch.int64)
     recv = _scratch(backend, "bfs_recv", nwg, torch.int64)
-    total = _allreduce_counts([backend.total_entries, 0], dev, group)[0]
+    total = _allreduce_counts([backend.total_entries, 0], dev, cm)[0]
     c = backend.bfs_begin(seed, nb_local)
-    dist.all_gather_into_tensor(fb_global, nb_local, group=group)
-    nf, mf = _allreduce_counts(c, dev, group)
+    cm.all_gather_into_tensor(fb_global, nb_local)
+    nf, mf = _allreduce_counts(c, dev, cm)
     mu = total - mf
     bottom_up = False
     levels = 0
@@ -347,42 +481,40 @@ def distributed_bfs(backend, seed: int, max_depth: int, alpha: float = 15.0, bet
         else:
             disc.zero_()
             backend.bfs_td(level, disc)
-            dist.all_to_all_single(recv, disc, group=group)
+            cm.all_to_all_single(recv, disc)
             c = backend.bfs_claim(level, recv, world, nb_local)
-        dist.all_gather_into_tensor(fb_global, nb_local, group=group)
-        nf, mf = _allreduce_counts(c, dev, group)
+        cm.all_gather_into_tensor(fb_global, nb_local)
+        nf, mf = _allreduce_counts(c, dev, cm)
         mu -= mf
         levels += 1
     out, reached = backend.bfs_end(fetch, stats)
     if stats:
-        reached = _allreduce_counts(reached, dev, group)
+        reached = _allreduce_counts(reached, dev, cm)
     return out, reached, levels
 
 
-def _exchange_pairs(send, counts, recv, dev, group):
+def _exchange_pairs(send, counts, recv, dev, comm):
     """all_to_all of the per-rank pair counts, then of the (id, value) int64 pairs with
     split sizes; returns the received count per sender."""
     sct = torch.from_numpy(2 * np.asarray(counts, np.int64)).to(dev)
     rct = torch.empty_like(sct)
-    dist.all_to_all_single(rct, sct, group=group)
+    comm.all_to_all_single(rct, sct)
     ins = [int(x) for x in sct.cpu()]
     outs = [int(x) for x in rct.cpu()]
-    dist.all_to_all_single(recv[:sum(outs)], send[:sum(ins)], output_split_sizes=outs, input_split_sizes=ins,
-                           group=group)
+    comm.all_to_all_single(recv[:sum(outs)], send[:sum(ins)], output_split_sizes=outs, input_split_sizes=ins)
     return np.asarray(outs, np.int64) // 2
 
 
-def _exchange_pairs_dev(send, sct, recv, group):
+def _exchange_pairs_dev(send, sct, recv, comm):
     """As _exchange_pairs with the split sizes already on the device (sct, int64 elements per
     destination): one all_to_all of the sizes, ONE host read of both size vectors."""
     rct = torch.empty_like(sct)
-    dist.all_to_all_single(rct, sct, group=group)
+    comm.all_to_all_single(rct, sct)
     both = torch.cat([sct, rct]).cpu().numpy()
     w = len(sct)
     ins = [int(x) for x in both[:w]]
     outs = [int(x) for x in both[w:]]
-    dist.all_to_all_single(recv[:sum(outs)], send[:sum(ins)], output_split_sizes=outs, input_split_sizes=ins,
-                           group=group)
+    comm.all_to_all_single(recv[:sum(outs)], send[:sum(ins)], output_split_sizes=outs, input_split_sizes=ins)
     return np.asarray(outs, np.int64) // 2
 
 
@@ -392,7 +524,7 @@ FIXED_EXCHANGE_BYTES = int(os.environ.get("TGO_MS_FIXED_BYTES", 64 << 20))
 
 
 def distributed_msbfs(backend, seeds, max_depth: int, ms_alpha: float = 12.0, stats: bool = True, group=None,
-                      sparse_exchange: bool = True, fixed_exchange_bytes: int = None):
+                      sparse_exchange: bool = True, fixed_exchange_bytes: int = None, comm=None):
     """Up to 64 ShortestDistance programs with unit weights over bothE, run together with
     bit-parallel frontier masks on a vertex-partitioned graph.
       dense level : all_gather of owned frontier masks (8 bytes per vertex) -> local pull
@@ -400,7 +532,8 @@ def distributed_msbfs(backend, seeds, max_depth: int, ms_alpha: float = 12.0, st
                     (owner-local id, mask) pairs -> all_to_all with split sizes -> settle
                     (sparse_exchange=False: all_to_all of the whole n_global-word slices)
     Returns (per-seed global reached vertices, per-seed reached entries, levels)."""
-    world = dist.get_world_size(group)
+    cm = _comm(comm, group)
+    world = cm.world
     nseeds = len(seeds)
     dev = backend.device
     if fixed_exchange_bytes is None:
@@ -415,14 +548,14 @@ def distributed_msbfs(backend, seeds, max_depth: int, ms_alpha: float = 12.0, st
     # tail stays zero (tgo_part_ms_begin leaves entry-less seeds out of the masks)
     cand = _scratch(backend, "ms_cand", backend.n_global, torch.int64)     # all-zero between sparse levels
     send = recv = None
-    total = _allreduce_counts([backend.total_entries, 0], dev, group)[0]
-    nf, mf = _allreduce_counts(backend.ms_begin(seeds, fr), dev, group)
+    total = _allreduce_counts([backend.total_entries, 0], dev, cm)[0]
+    nf, mf = _allreduce_counts(backend.ms_begin(seeds, fr), dev, cm)
     levels = 0
     for level in range(max_depth):
         if nf == 0:
             break
         if mf * ms_alpha > total:
-            dist.all_gather_into_tensor(glob[0], fr, group=group)
+            cm.all_gather_into_tensor(glob[0], fr)
             c = backend.ms_pull(level, glob[0], frn)
         elif sparse_exchange:
             send = _scratch(backend, "pairs_send", 2 * backend.n_global + 2 * world, torch.int64)
@@ -433,31 +566,31 @@ def distributed_msbfs(backend, seeds, max_depth: int, ms_alpha: float = 12.0, st
             if hasattr(backend, "ms_pack_fixed") and cap > 0 and world * (cap + 1) * 16 <= fixed_exchange_bytes:
                 ne = 2 * world * (cap + 1)
                 backend.ms_pack_fixed(cand, send, world, cap)
-                dist.all_to_all_single(recv[:ne], send[:ne], group=group)
+                cm.all_to_all_single(recv[:ne], send[:ne])
                 c = backend.ms_settle_fixed(level, recv, world, cap, frn)
             elif hasattr(backend, "ms_pack_dev"):
                 sct = _scratch(backend, "pairs_sct", world, torch.int64)
                 backend.ms_pack_dev(cand, send, world, sct)
-                rcounts = _exchange_pairs_dev(send, sct, recv, group)
+                rcounts = _exchange_pairs_dev(send, sct, recv, cm)
                 c = backend.ms_settle_pairs(level, recv, rcounts, frn)
             else:
-                rcounts = _exchange_pairs(send, backend.ms_pack(cand, send, world), recv, dev, group)
+                rcounts = _exchange_pairs(send, backend.ms_pack(cand, send, world), recv, dev, cm)
                 c = backend.ms_settle_pairs(level, recv, rcounts, frn)
         else:
             recv = _scratch(backend, "slices_recv", backend.n_global, torch.int64)
             cand.zero_()
             backend.ms_push(level, fr, cand)
-            dist.all_to_all_single(recv, cand, group=group)
+            cm.all_to_all_single(recv, cand)
             cand.zero_()
             c = backend.ms_settle(level, recv, world, frn)
         fr, frn = frn, fr
         glob.reverse()
-        nf, mf = _allreduce_counts(c, dev, group)
+        nf, mf = _allreduce_counts(c, dev, cm)
         levels += 1
     r, e = backend.ms_end(nseeds, stats)
     if stats:
         t = torch.tensor(np.concatenate([r, e]), dtype=torch.int64, device=dev)
-        dist.all_reduce(t, group=group)
+        cm.all_reduce(t)
         t = t.cpu().numpy()
         r, e = t[:nseeds], t[nseeds:]
     return r, e, levels
@@ -466,7 +599,8 @@ def distributed_msbfs(backend, seeds, max_depth: int, ms_alpha: float = 12.0, st
 INT64_MAX = (1 << 63) - 1
 
 
-def distributed_sssp(backend, seed: int, delta: int = 0, fetch: bool = True, stats: bool = True, group=None):
+def distributed_sssp(backend, seed: int, delta: int = 0, fetch: bool = True, stats: bool = True, group=None,
+                     comm=None):
     """Delta-stepping ShortestDistance (converged distances) on a vertex-partitioned graph.
       phase  : local relax of the owned near queue; improvements of remote vertices are
                packed per owner -> all_to_all of the pair counts, all_to_all_single of the
@@ -475,7 +609,8 @@ def distributed_sssp(backend, seed: int, delta: int = 0, fetch: bool = True, sta
       bucket : when every near queue is empty, all_reduce(MIN) of the pending distances
                moves the threshold to the end of the next non-empty bucket
     Returns (local distances or None, global [reached vertices, entries] or None, phases)."""
-    world = dist.get_world_size(group)
+    cm = _comm(comm, group)
+    world = cm.world
     dev = backend.device
     n = backend.n_global
     send = _scratch(backend, "pairs_send", 2 * n, torch.int64)
@@ -483,13 +618,13 @@ def distributed_sssp(backend, seed: int, delta: int = 0, fetch: bool = True, sta
     qlen, dflt = (int(x) for x in backend.sssp_begin(seed, delta))
     if delta <= 0:      # ranks' default widths differ with their local mean weight: agree on one
         t = torch.tensor([dflt], dtype=torch.int64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        cm.all_reduce(t, op="max")
         delta = int(t.item())
     thr, phases = delta, 0
     while True:
-        if int(_allreduce_counts([qlen, 0], dev, group)[0]) == 0:
+        if int(_allreduce_counts([qlen, 0], dev, cm)[0]) == 0:
             mn = torch.tensor([int(backend.sssp_pending_min()[0])], dtype=torch.int64, device=dev)
-            dist.all_reduce(mn, op=dist.ReduceOp.MIN, group=group)
+            cm.all_reduce(mn, op="min")
             mn = int(mn.item())
             if mn == INT64_MAX:
                 break
@@ -500,16 +635,15 @@ def distributed_sssp(backend, seed: int, delta: int = 0, fetch: bool = True, sta
         sc = backend.sssp_relax(thr, send, world)
         sct = torch.from_numpy(2 * sc).to(dev)
         rct = torch.empty_like(sct)
-        dist.all_to_all_single(rct, sct, group=group)
+        cm.all_to_all_single(rct, sct)
         ins = [int(x) for x in 2 * sc]
         outs = [int(x) for x in rct.cpu()]
-        dist.all_to_all_single(recv[:sum(outs)], send[:sum(ins)], output_split_sizes=outs, input_split_sizes=ins,
-                               group=group)
+        cm.all_to_all_single(recv[:sum(outs)], send[:sum(ins)], output_split_sizes=outs, input_split_sizes=ins)
         qlen = int(backend.sssp_apply(thr, recv, sum(outs) // 2)[0])
         phases += 1
     out, reached = backend.sssp_end(fetch, stats)
     if stats:
-        reached = _allreduce_counts(reached, dev, group)
+        reached = _allreduce_counts(reached, dev, cm)
     return out, reached, phases
 
 
@@ -522,19 +656,20 @@ def gathered_index(u, n_local: int, world: int, hot: int, span: int):
     return np.where(o < hot, r * hot + o, world * hot + r * (span - hot) + (o - hot))
 
 
-def pagerank_layout(backend, group=None):
+def pagerank_layout(backend, group=None, comm=None):
     """(hot rows per rank H, active span A) agreed by every rank: A = max active rows
     (all-reduce MAX), H from the backend (0 = plain rank-major layout, A = n_local)."""
-    world = dist.get_world_size(group)
+    cm = _comm(comm, group)
+    world = cm.world
     t = torch.tensor([backend.active_rows()], dtype=torch.int64, device=backend.device)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    cm.all_reduce(t, op="max")
     span = int(t.item())
     hot = backend.pr_layout(world, span)
     return (hot, span) if hot > 0 else (0, backend.n_local)
 
 
 def distributed_pagerank(backend, alpha: float, vertex_count: int, iterations: int, fetch: bool = True,
-                         group=None, layout=None, overlap: bool = True):
+                         group=None, layout=None, overlap: bool = True, comm=None):
     """PageRankVertexProgram on a vertex-partitioned graph; returns local ranks.
       plain   : all_gather of the owned contributions (8 n_local B per rank) -> local update
       blocked : (pagerank_layout) cold slices [H, A) all-gathered first; the hot slices
@@ -543,23 +678,23 @@ def distributed_pagerank(backend, alpha: float, vertex_count: int, iterations: i
                 past A hold no entries anywhere and are not exchanged."""
     if iterations == 0:
         return np.full(backend.n_local, np.nan) if fetch else None
-    world = dist.get_world_size(group)
-    hot, span = layout if layout is not None else pagerank_layout(backend, group)
+    cm = _comm(comm, group)
+    world = cm.world
+    hot, span = layout if layout is not None else pagerank_layout(backend, comm=cm)
     contrib_local = _scratch(backend, "pr_local", backend.n_local, torch.float64)
     contrib_global = _scratch(backend, "pr_global", world * span, torch.float64)
     backend.pr_begin(alpha, vertex_count, iterations, contrib_local)
     for _ in range(2, iterations + 1):
         if hot == 0:
-            dist.all_gather_into_tensor(contrib_global, contrib_local, group=group)
+            cm.all_gather_into_tensor(contrib_global, contrib_local)
             backend.pr_step(contrib_global, contrib_local)
             continue
-        dist.all_gather_into_tensor(contrib_global[world * hot:], contrib_local[hot:span], group=group)
+        cm.all_gather_into_tensor(contrib_global[world * hot:], contrib_local[hot:span])
         if not overlap:
-            dist.all_gather_into_tensor(contrib_global[:world * hot], contrib_local[:hot], group=group)
+            cm.all_gather_into_tensor(contrib_global[:world * hot], contrib_local[:hot])
             backend.pr_step(contrib_global, contrib_local)
             continue
-        work = dist.all_gather_into_tensor(contrib_global[:world * hot], contrib_local[:hot], group=group,
-                                           async_op=True)
+        work = cm.all_gather_into_tensor(contrib_global[:world * hot], contrib_local[:hot], async_op=True)
         backend.pr_step_cold(contrib_global)
         work.wait()
         backend.pr_step_hot(contrib_global, contrib_local)

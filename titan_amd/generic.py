@@ -240,6 +240,9 @@ class GenericVertexProgram:
     compute_keys: tuple = ()
     memory_compute_keys: tuple = ()
     weight_property = None              # property read by add_weight / mul_weight edge functions
+    # getPreferredPersist: the mode submit() uses when resultMode is not set; NOTHING keeps
+    # the results in memory / MapReduce (subclasses may prefer VERTEX_PROPERTIES)
+    preferred_persist = None            # None = Persist.NOTHING
 
     def setup(self, memory):
         pass
