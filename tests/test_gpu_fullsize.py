@@ -12,6 +12,8 @@ CPU oracle on the very graphs bench.py measures:
 * configs[2] — RMAT scale 24: the 64-source multi-source BFS sweep against 64 single-source
   runs and against the oracle for two seeds; PageRank(20) on the capped inE graph within
   1e-6 L1 of the oracle, with the same truncated-row count on both sides.
+* configs[4] on one GPU — the bench's weighted RMAT-24 inE graph: delta-stepping SSSP from two
+  of the bench's roots and hop-bounded maxDepth 3, bit-exact against the oracle.
 
 Sized so each test finishes in well under two minutes on the GPU box (oracle threads = 16,
 the box's CPU share).
@@ -74,14 +76,22 @@ def test_config2_rmat20_rows_bfs_bit_exact(rmat20_rows, scope):
 def rmat24():
     scale = 24
     n = 1 << scale
-    src, dst, _ = rmat_edges(scale, 16, seed=0x54495441)
+    src, dst, w = rmat_edges(scale, 16, seed=0x54495441, weights=True)     # bench.py's graph and weights
     roots = pick_roots(n, src, dst, 64, seed=7)
-    return n, src, dst, roots
+    return n, src, dst, roots, w
+
+
+@pytest.fixture(scope="module")
+def oracle24_in_capped(rmat24):
+    """The oracle's inE graph at the real 100 000-entry cap, with the bench's weights (PageRank
+    ignores them): shared by the PageRank and SSSP tests."""
+    n, src, dst, roots, w = rmat24
+    return fr.OracleGraph.from_edges(n, src, dst, w, hard_limit=100000).resolve(THREADS)
 
 
 def test_config3_rmat24_msbfs_sweep(rmat24):
     """All 64 seeds of the bench's sweep equal their single-source runs; two equal the oracle."""
-    n, src, dst, roots = rmat24
+    n, src, dst, roots, _ = rmat24
     eng = Engine(host_threads=THREADS).load_edges(n, src, dst, BOTH, apply_cap=False)
     eng.bfs_multi(roots, n, BOTH, seed_is_dense=True, stats=True, fetch=False)
     reached, entries = eng.multi_stats(len(roots))
@@ -101,16 +111,16 @@ def test_config3_rmat24_msbfs_sweep(rmat24):
         assert np.array_equal(d, od), r
 
 
-def test_config3_rmat24_pagerank_capped(rmat24):
+def test_config3_rmat24_pagerank_capped(rmat24, oracle24_in_capped):
     """PageRank(20) on the capped inE graph (25 rows cut at 100 000 entries)."""
-    n, src, dst, roots = rmat24
+    n, src, dst, roots, _ = rmat24
     eng = Engine(host_threads=THREADS).load_edges(n, src, dst, IN, apply_cap=True)
     pr = eng.pagerank(0.85, n, 20)
     assert np.array_equal(pr, eng.pagerank(0.85, n, 20))             # fixed reduction order
     st = eng.stats()
     d_in = eng.bfs(int(roots[1]), n, IN, seed_is_dense=True)
     del eng
-    o = fr.OracleGraph.from_edges(n, src, dst, hard_limit=100000).resolve(THREADS)
+    o = oracle24_in_capped
     assert st["truncated_results"] == o.stats.truncated_results > 0
     opr, it = o.pagerank(0.85, n, 20, threads=THREADS)
     assert it == 20
@@ -119,3 +129,38 @@ def test_config3_rmat24_pagerank_capped(rmat24):
     assert np.abs(pr[fin] - opr[fin]).sum() <= PR_L1_TOL
     od, _ = o.shortest_distance(int((int(roots[1]) + 1) << 3), n, IN, threads=THREADS)
     assert np.array_equal(d_in, od)
+
+
+def test_config5_rmat24_weighted_sssp(rmat24, oracle24_in_capped):
+    """configs[4] at the size bench.py measures it: weighted inE ShortestDistance (int32 weights
+    1 + splitmix64 mod 255, the 100 000 cap on) from the first two of the bench's SSSP roots
+    (roots whose reach is the giant component).  Delta-stepping gives the converged distances,
+    bit-exact against the oracle's Jacobi supersteps run to their fixpoint
+    (ShortestDistanceVertexProgram.java:96-130); hop-bounded maxDepth 3 gives the reference's
+    3-superstep distances exactly.  Reached counts equal; relaxed/reached stays near 1."""
+    n, src, dst, roots, w = rmat24
+    eng = Engine(host_threads=THREADS).load_edges(n, src, dst, IN, weight=w, apply_cap=True)
+    picked = []
+    for r in roots:
+        d = eng.sssp(int(r), n, IN, mode=L.SSSP_DELTA, seed_is_dense=True, stats=True)
+        st = eng.stats()
+        if st["reached"] * 4 < n:                 # bench.py sssp_leg: the giant component only
+            continue
+        assert st["relaxed_entries"] <= 1.5 * st["reached_entries"]
+        picked.append((int(r), d, st["reached"]))
+        if len(picked) == 2:
+            break
+    assert len(picked) == 2
+    hop3 = eng.sssp(picked[0][0], 3, IN, mode=L.SSSP_HOP_BOUNDED, seed_is_dense=True, stats=True)
+    hop3_reached = eng.stats()["reached"]
+    del eng
+    o = oracle24_in_capped
+    for r, d, reached in picked:
+        od, it = o.shortest_distance((r + 1) << 3, n, IN, weighted=True, threads=THREADS)
+        assert it == n
+        assert np.array_equal(d, od), r
+        assert reached == int((od != L.DIST_ABSENT).sum())
+    od3, it = o.shortest_distance((picked[0][0] + 1) << 3, 3, IN, weighted=True, threads=THREADS)
+    assert it == 3
+    assert np.array_equal(hop3, od3)
+    assert hop3_reached == int((od3 != L.DIST_ABSENT).sum())

@@ -441,16 +441,19 @@ def test_partitioned_hubs_match_oracle():
                 o.pagerank(0.85, n, 4)
 
 
+@pytest.mark.parametrize("tile", ["4096", "8192", "16384"])
 @pytest.mark.parametrize("iters", [2, 20])
 @pytest.mark.parametrize("hot,seg", [(64, 256), (1000, 100), (4096, 512)])
-def test_rmat_pagerank_cache_blocked(rmat12, iters, hot, seg, monkeypatch):
+def test_rmat_pagerank_cache_blocked(rmat12, iters, hot, seg, tile, monkeypatch):
     """The cache-blocked PageRank gather (hot CSR + XCD-pinned cold segments, engine.hpp
     ColdBlocks) forced onto a small graph with tiny hot sets / segments (many segments, so
-    every XCD has several): oracle bar, bitwise reproducible, within rounding of the plain
-    CSR-adaptive gather.  hot >= n means nothing is cold (plain path)."""
+    every XCD has several), with each hot tile size (gather_hot_pf / gather_hot_big): oracle
+    bar, bitwise reproducible, within rounding of the plain CSR-adaptive gather.  hot >= n
+    means nothing is cold (plain path)."""
     n, src, dst, w, ids, oracle, roots = rmat12
     monkeypatch.setenv("TGO_PR_HOT", str(hot))
     monkeypatch.setenv("TGO_PR_SEG", str(seg))
+    monkeypatch.setenv("TGO_PR_HOT_TILE", tile)
     eng = Engine().load_edges(n, src, dst, IN)
     pr = eng.pagerank(0.85, n, iters)
     opr, _ = oracle.pagerank(0.85, n, iters)
@@ -472,13 +475,15 @@ def hub_graph(n, hub, k_in, k_out, seed=11):
 KTILE = 4096     # CSR-adaptive tile (engine.hpp kTile): rows longer than this are split in chunks
 
 
-@pytest.mark.parametrize("blocked", ["0", "1"])
-def test_pagerank_long_rows(monkeypatch, blocked):
+@pytest.mark.parametrize("blocked,tile", [("0", "4096"), ("1", "4096"), ("1", "8192"), ("1", "16384")])
+def test_pagerank_long_rows(monkeypatch, blocked, tile):
     """A hub whose in-list spans many tiles: 80 000 entries = ~20 chunks of kTile through
     gather_chunks + finalize_long; cache-blocked with 1024 hot sources and 4096-source cold
-    segments, its cold run per segment (~10 000 entries) is cut into several kTile pieces.
-    Both within 1e-6 L1 of the oracle and bitwise reproducible."""
+    segments, its cold run per segment (~10 000 entries) is cut into several kTile pieces;
+    the larger hot tiles cut the hub's hot run into 8192 / 16384-entry chunks (packed words
+    with the top bit set).  All within 1e-6 L1 of the oracle and bitwise reproducible."""
     monkeypatch.setenv("TGO_PR_BLOCKED", blocked)
+    monkeypatch.setenv("TGO_PR_HOT_TILE", tile)
     monkeypatch.setenv("TGO_PR_HOT", "1024")
     monkeypatch.setenv("TGO_PR_SEG", "4096")
     n = 1 << 15

@@ -144,10 +144,11 @@ PrTuning pr_tuning() {
 // CSR-adaptive row blocks of one CSR; `pack` (optional) source-sorts and packs the CSR's
 // tiles first (spmv.hip gather_short_packed).
 hipError_t upload_row_blocks(tgo_ctx* ctx, const std::vector<int64_t>& off, RowBlocks& rb,
-                             std::vector<int32_t>* pack = nullptr, bool* packed = nullptr) {
+                             std::vector<int32_t>* pack = nullptr, bool* packed = nullptr, int64_t tile = kTile,
+                             int shift = kPackShift) {
     std::vector<int64_t> blk, crow, cbeg, cend, lrow, lch;
-    build_row_blocks(off, kTile, kMaxRows, blk, crow, cbeg, cend, lrow, lch);
-    if (pack) *packed = pack_tiles(off, *pack, blk, cbeg, cend, kTile, threads_of(ctx));
+    build_row_blocks(off, tile, kMaxRows, blk, crow, cbeg, cend, lrow, lch);
+    if (pack) *packed = pack_tiles(off, *pack, blk, cbeg, cend, tile, threads_of(ctx), shift);
     rb.nblocks = static_cast<int64_t>(blk.size()) - 1;
     rb.nchunks = static_cast<int64_t>(crow.size());
     rb.nlong = static_cast<int64_t>(lrow.size());
@@ -182,7 +183,22 @@ int upload_cold_blocks(tgo_ctx* ctx, const std::vector<int64_t>& off, const std:
     cb.xbase = hc.xbase;
     cb.n_rows = n_rows;
     const std::vector<int64_t> hoff_act(hc.hoff.begin(), hc.hoff.begin() + n_rows + 1);
-    HIP_TRY(upload_row_blocks(ctx, hoff_act, cb.rb_hot, env_i64("TGO_PR_PACK", 1) ? &hc.hadj : nullptr, &cb.packed));
+    // hot tiles: 4096 entries (256 threads, 32 KB of LDS), 8192 (512 threads, 64 KB) or 16384
+    // (1024 threads, 128 KB): a larger tile shares more 128-byte lines between the lanes of one
+    // gather instruction (fewer L2 requests per entry) at fewer workgroups per CU
+    const int64_t ht = env_i64("TGO_PR_HOT_TILE", 4096);
+    cb.hot_tile = ht == 16384 ? 16384 : ht == 8192 ? 8192 : 4096;
+    cb.hot_shift = cb.hot_tile == 16384 ? 14 : cb.hot_tile == 8192 ? 13 : kPackShift;
+    const bool pack = env_i64("TGO_PR_PACK", 1) != 0;
+    if (!pack) cb.hot_tile = static_cast<int>(kTile), cb.hot_shift = kPackShift;
+    HIP_TRY(upload_row_blocks(ctx, hoff_act, cb.rb_hot, pack ? &hc.hadj : nullptr, &cb.packed, cb.hot_tile,
+                              cb.hot_shift));
+    if (!cb.packed && cb.hot_tile != kTile) {      // sources too wide for the slot space: the 4096 form
+        cb.hot_tile = static_cast<int>(kTile);
+        cb.hot_shift = kPackShift;
+        cb.rb_hot = RowBlocks();
+        HIP_TRY(upload_row_blocks(ctx, hoff_act, cb.rb_hot, pack ? &hc.hadj : nullptr, &cb.packed));
+    }
     HIP_TRY(upload(ctx, cb.hcsr.off, hc.hoff));
     HIP_TRY(upload(ctx, cb.hcsr.adj, hc.hadj));
     cb.hcsr.nnz = static_cast<int64_t>(hc.hadj.size());

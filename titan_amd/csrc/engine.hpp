@@ -235,6 +235,8 @@ struct ColdBlocks {
     XcdBase xbase{};
     RowBlocks rb_hot;           // CSR-adaptive blocks of the hot CSR
     bool packed = false;        // hot CSR tiles source-sorted and packed (pack_tiles)
+    int hot_tile = 4096;        // entries per hot tile (TGO_PR_HOT_TILE: 4096, 8192 or 16384)
+    int hot_shift = 12;         // packed hot entry = source << hot_shift | slot (log2 hot_tile)
 };
 struct HostColdBlocks {
     int64_t hot = 0, seg = 0;
@@ -482,8 +484,11 @@ hipError_t scan_exclusive_i64(void*& tmp, size_t& tmp_bytes, const int64_t* in, 
 // Push entries of the loaded scope in one list per vertex sorted by (weight, target).
 void weight_sorted_push(const HostGraph& g, HostCsr& ws, int threads);
 // Source-sorted, packed tiles of a CSR (see graph_build.cpp); false if sources need > 19 bits.
+// shift = log2 of the slot space (tile <= 1 << shift); sources must fit 32 - shift bits (the
+// packed word is read as uint32 by kernels whose shift exceeds 12).
 bool pack_tiles(const std::vector<int64_t>& off, std::vector<int32_t>& adj, const std::vector<int64_t>& blk,
-                const std::vector<int64_t>& cbeg, const std::vector<int64_t>& cend, int64_t tile, int threads);
+                const std::vector<int64_t>& cbeg, const std::vector<int64_t>& cend, int64_t tile, int threads,
+                int shift = kPackShift);
 // Row-block construction (host) for a CSR.
 void build_row_blocks(const std::vector<int64_t>& off, int64_t tile, int64_t max_rows,
                       std::vector<int64_t>& blk, std::vector<int64_t>& chunk_row,

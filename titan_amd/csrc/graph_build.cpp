@@ -891,15 +891,19 @@ void build_row_blocks(const std::vector<int64_t>& off, int64_t tile, int64_t max
 // sources — shared 128-byte lines are fetched once — and the gathered values are written
 // back to their slot, so the row sums keep the tile's row order.
 bool pack_tiles(const std::vector<int64_t>& off, std::vector<int32_t>& adj, const std::vector<int64_t>& blk,
-                const std::vector<int64_t>& cbeg, const std::vector<int64_t>& cend, int64_t tile, int threads) {
-    if (tile > (int64_t(1) << kPackShift)) return false;
+                const std::vector<int64_t>& cbeg, const std::vector<int64_t>& cend, int64_t tile, int threads,
+                int shift) {
+    if (shift < 1 || shift > 20 || tile > (int64_t(1) << shift)) return false;
+    // shift 12: the word stays a non-negative int32 (kernels read it signed); wider slot spaces
+    // use all 32 bits (their kernels read it as uint32)
+    const int64_t src_limit = shift == kPackShift ? (int64_t(1) << (31 - shift)) : (int64_t(1) << (32 - shift));
     for (int32_t u : adj)
-        if (u < 0 || u >= (int32_t(1) << (31 - kPackShift))) return false;
+        if (u < 0 || u >= src_limit) return false;
     const int64_t nblk = static_cast<int64_t>(blk.size()) - 1, nch = static_cast<int64_t>(cbeg.size());
     auto pack_range = [&](int64_t b, int64_t e, std::vector<uint32_t>& tmp) {
         tmp.resize(static_cast<size_t>(e - b));
         for (int64_t k = b; k < e; ++k)
-            tmp[k - b] = (static_cast<uint32_t>(adj[k]) << kPackShift) | static_cast<uint32_t>(k - b);
+            tmp[k - b] = (static_cast<uint32_t>(adj[k]) << shift) | static_cast<uint32_t>(k - b);
         std::sort(tmp.begin(), tmp.end());
         for (int64_t k = b; k < e; ++k) adj[k] = static_cast<int32_t>(tmp[k - b]);
     };

@@ -99,10 +99,12 @@ __device__ __forceinline__ void gather_tile(const int32_t* __restrict__ adj, int
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
         const int64_t k = threadIdx.x + static_cast<int64_t>(j) * kBlock;
-        idx[j] = k < nnz ? stream_idx(adj + s0 + k) : -1;
+        idx[j] = k < nnz ? stream_idx(adj + s0 + k) : 0;
     }
+    // validity by position: a packed word of a wide slot space may have its top bit set
 #pragma unroll
-    for (int j = 0; j < kPer; ++j) val[j] = idx[j] >= 0 ? op.load(idx[j]) : Op::zero();
+    for (int j = 0; j < kPer; ++j)
+        val[j] = threadIdx.x + static_cast<int64_t>(j) * kBlock < nnz ? op.load(idx[j]) : Op::zero();
 }
 
 // Stage a tile's gathered messages in LDS.
@@ -257,11 +259,93 @@ __global__ void __launch_bounds__(kBlock) gather_hot_pf(const int64_t* __restric
     }
 }
 
+// gather_hot_pf with larger tiles: kT entries (kT / kThreads = 16 per thread) staged in kT * 8
+// bytes of LDS, entries packed as uint32 source << kShift | slot.  A larger tile holds more
+// entries of the same 128-byte lines, and a tile is source-sorted, so more lanes of one gather
+// instruction share a line: at RMAT-24, 0.70 line requests per hot entry at 4096 entries,
+// 0.60 at 8192 and 0.48 at 16384 (host count over the bench graph).  Same sums in the same
+// order as the 4096 form's reduce for the same tile boundaries (fixed association).
+template <int kT, int kThreads, int kShift>
+__global__ void __launch_bounds__(kThreads) gather_hot_big(const int64_t* __restrict__ off,
+        const uint32_t* __restrict__ padj, const int64_t* __restrict__ bdesc, const double* __restrict__ msg,
+        PrColdFinal fin) {
+    constexpr int kP = kT / kThreads;
+    constexpr int kWaves = kThreads / 64;
+    static_assert(kP * kThreads == kT && (1 << kShift) == kT, "tile shape");
+    __shared__ double s_val[kT];
+    const int64_t r0 = bdesc[2 * blockIdx.x], s0 = bdesc[2 * blockIdx.x + 1];
+    const int64_t r1 = bdesc[2 * blockIdx.x + 2], nnz = bdesc[2 * blockIdx.x + 3] - s0;
+    const bool tpr = r1 - r0 > 64;
+    const int wave = threadIdx.x >> 6;
+    const int64_t pr = tpr ? r0 + threadIdx.x : r0 + wave + kWaves * lane();
+    int64_t pb = 0, pe = 0;
+    double pcs = 0.0, pec = 1.0;
+    if (pr < r1) {
+        pb = off[pr];
+        pe = off[pr + 1];
+        pcs = fin.csum[pr];
+        pec = __builtin_nontemporal_load(fin.f.edge_count + pr);
+    }
+    if (nnz > kT) return;                             // long row: handled by chunks
+    {
+        uint32_t v[kP];
+#pragma unroll
+        for (int j = 0; j < kP; ++j) {
+            const int64_t k = threadIdx.x + static_cast<int64_t>(j) * kThreads;
+            v[j] = k < nnz ? __builtin_nontemporal_load(padj + s0 + k) : 0u;
+        }
+        double val[kP];
+#pragma unroll
+        for (int j = 0; j < kP; ++j) {
+            const int64_t k = threadIdx.x + static_cast<int64_t>(j) * kThreads;
+            val[j] = k < nnz ? msg[v[j] >> kShift] : 0.0;
+        }
+#pragma unroll
+        for (int j = 0; j < kP; ++j) {
+            const int64_t k = threadIdx.x + static_cast<int64_t>(j) * kThreads;
+            if (k < nnz) s_val[v[j] & (kT - 1)] = val[j];
+        }
+    }
+    __syncthreads();
+    const PrFinal& f = fin.f;
+    auto emit = [&](int64_t r, double sum, double cs, double ec) {
+        const double p = (f.alpha * (sum + cs)) + f.base;   // PrColdFinal: f(r, sum + csum[r])
+        if (f.pr) f.pr[r] = p;
+        f.contrib_next[r] = p / ec;
+    };
+    if (tpr) {
+        bool first = true;
+        for (int64_t i = r0 + threadIdx.x; i < r1; i += kThreads) {
+            int64_t b = pb, e = pe;
+            double cs = pcs, ec = pec;
+            if (!first) {
+                b = off[i]; e = off[i + 1]; cs = fin.csum[i];
+                ec = __builtin_nontemporal_load(f.edge_count + i);
+            }
+            first = false;
+            double sum = 0.0;
+            for (int64_t k = b - s0; k < e - s0; ++k) sum = sum + s_val[k];
+            emit(i, sum, cs, ec);
+        }
+    } else {
+        for (int t = 0; r0 + wave + kWaves * t < r1; ++t) {
+            const int64_t i = r0 + wave + kWaves * t;
+            const int64_t b = __shfl(pb, t, 64), e = __shfl(pe, t, 64);
+            const double cs = __shfl(pcs, t, 64), ec = __shfl(pec, t, 64);
+            double sum = 0.0;
+            for (int64_t k = b - s0 + lane(); k < e - s0; k += 64) sum = sum + s_val[k];
+            sum = wave_sum(sum);
+            if (lane() == 0) emit(i, sum, cs, ec);
+        }
+    }
+}
+
 // A long row's chunk of packed entries: the chunk sum (source order, fixed).
 struct PackedOp {
     using T = double;
     const double* msg;
-    __device__ __forceinline__ double load(int32_t v) const { return msg[v >> kPackShift]; }
+    int shift = kPackShift;
+    __device__ __forceinline__ double load(int32_t v) const { return msg[static_cast<uint32_t>(v) >> shift]; }
     __device__ __forceinline__ static double add(double a, double b) { return a + b; }
     __device__ __forceinline__ static double zero() { return 0.0; }
 };
@@ -476,7 +560,14 @@ hipError_t k_pr_hot_phase(const ColdBlocks& cb, const double* contrib, const dou
     const PrColdFinal fin{PrFinal{edge_count, pr, contrib_next, alpha, base}, cb.csum};
     if (!cb.packed) return run_gather(cb.hcsr, cb.rb_hot, PrOp{contrib}, fin, partial_long, s);
     const RowBlocks& rb = cb.rb_hot;
-    if (rb.nblocks > 0) {
+    if (rb.nblocks > 0 && cb.hot_tile != kTile) {
+        const unsigned g = static_cast<unsigned>(rb.nblocks);
+        const uint32_t* padj = reinterpret_cast<const uint32_t*>(cb.hcsr.adj);
+        if (cb.hot_tile == 8192)
+            gather_hot_big<8192, 512, 13><<<g, 512, 0, s>>>(cb.hcsr.off, padj, rb.bdesc, contrib, fin);
+        else
+            gather_hot_big<16384, 1024, 14><<<g, 1024, 0, s>>>(cb.hcsr.off, padj, rb.bdesc, contrib, fin);
+    } else if (rb.nblocks > 0) {
         if (row_prefetch())
             gather_hot_pf<<<static_cast<unsigned>(rb.nblocks), kBlock, 0, s>>>(cb.hcsr.off, cb.hcsr.adj, rb.bdesc,
                                                                                     contrib, fin);
@@ -486,7 +577,8 @@ hipError_t k_pr_hot_phase(const ColdBlocks& cb, const double* contrib, const dou
     }
     if (rb.nchunks > 0) {
         gather_chunks<PackedOp><<<static_cast<unsigned>(rb.nchunks), kBlock, 0, s>>>(cb.hcsr.adj, rb.chunk_beg,
-                                                                                    rb.chunk_end, PackedOp{contrib},
+                                                                                    rb.chunk_end,
+                                                                                    PackedOp{contrib, cb.hot_shift},
                                                                                     partial_long);
         finalize_long<PackedOp, PrColdFinal><<<grid_for(rb.nlong), kBlock, 0, s>>>(rb.long_row, rb.long_chunk,
                                                                                        rb.nlong, partial_long, fin);
