@@ -63,6 +63,11 @@ typedef enum {
  * reversed incident step (FulgoraUtil.java:49-62, reversal at :57). */
 typedef enum { TGO_SCOPE_OUT_E = 0, TGO_SCOPE_IN_E = 1, TGO_SCOPE_BOTH_E = 2 } tgo_scope;
 
+/* tgo_load_opts.flags: TGO_LOAD_COLUMN_ORDER keeps every entry's position in its Titan row
+ * (4 more bytes per entry) so tgo_gather_lists can hand a vertex its messages in the order
+ * the reference's receive stream yields them. */
+enum { TGO_LOAD_COLUMN_ORDER = 1 };
+
 /* Multiplicity of an edge label (core/Multiplicity.java:21-75). Decides where the
  * other vertex id sits inside an edge entry (EdgeSerializer.java:90-110). */
 typedef enum {
@@ -142,12 +147,17 @@ typedef struct {
                                      QueryContainer.java:110-134)                              */
     int32_t apply_cap;            /* 1 = reproduce the reference's cap (parity mode), 0 = not   */
     int32_t n_labels;             /* 0 = untyped scope (all user edge labels)                  */
+    int32_t flags;                /* TGO_LOAD_* bits (0 = none); fills what was padding        */
     const int64_t* label_ids;     /* typed scope: __.inE("label")... — fitted, no cap          */
-    int64_t weight_key;           /* Integer edge property read as weight; 0 = none.  It may sit
-                                     in a MULTI label's sort key (ASC or DESC), its signature or
-                                     its remaining properties; a non-Integer key fails with
-                                     TGO_E_UNSUPPORTED (ShortestDistanceVertexProgram.java:53
-                                     casts edge.<Integer>value).  TTL / timestamp metadata is not
+    int64_t weight_key;           /* edge property read as weight; 0 = none.  It may sit in a
+                                     MULTI label's sort key (ASC or DESC), its signature or its
+                                     remaining properties.  Byte, Short, Integer, Character and
+                                     Boolean keys are read as integers, Float keys as their IEEE
+                                     bits (-0.0 reads as +0.0); other datatypes fail with
+                                     TGO_E_UNSUPPORTED.  tgo_sssp / tgo_bfs need an Integer key
+                                     (ShortestDistanceVertexProgram.java:53 casts edge.<Integer>
+                                     value; another datatype is a ClassCastException there);
+                                     generic edge functions take any of them.  TTL / timestamp metadata is not
                                      part of the entry bytes (EdgeSerializer.java:154-161 only
                                      copies it into the relation); expired cells never reach the
                                      scan.                                                     */
@@ -308,11 +318,19 @@ int  tgo_walkcount(tgo_ctx* ctx, int32_t k, int32_t* out);
  * weight property fails with TGO_E_PROGRAM (edge.value() throws in the reference). */
 typedef enum { TGO_COMBINE_SUM = 0, TGO_COMBINE_MIN = 1, TGO_COMBINE_MAX = 2 } tgo_combiner;
 typedef enum { TGO_VAL_INT64 = 0, TGO_VAL_FP64 = 1 } tgo_value_type;
+/* Edge functions: (message, edge) -> message, the BiFunction of MessageScope.Local
+ * (VertexMemoryHandler.java:85,90) as "message op w", w = e.value(weight) of the load's
+ * weight key.  int64 arithmetic wraps like Java long; int64 / 0 and a Float weight with
+ * int64 messages fail with TGO_E_PROGRAM / TGO_E_INVALID. */
 typedef enum {
     TGO_EDGE_IDENTITY = 0,    /* (m, e) -> m                    */
     TGO_EDGE_ADD_ONE = 1,     /* (m, e) -> m + 1                */
-    TGO_EDGE_ADD_WEIGHT = 2,  /* (m, e) -> m + e.value(weight)  */
-    TGO_EDGE_MUL_WEIGHT = 3   /* (m, e) -> m * e.value(weight)  */
+    TGO_EDGE_ADD_WEIGHT = 2,  /* (m, e) -> m + w                */
+    TGO_EDGE_MUL_WEIGHT = 3,  /* (m, e) -> m * w                */
+    TGO_EDGE_SUB_WEIGHT = 4,  /* (m, e) -> m - w                */
+    TGO_EDGE_MIN_WEIGHT = 5,  /* (m, e) -> min(m, w)            */
+    TGO_EDGE_MAX_WEIGHT = 6,  /* (m, e) -> max(m, w)            */
+    TGO_EDGE_DIV_WEIGHT = 7   /* (m, e) -> m / w (Java / : int64 truncates, / 0 throws) */
 } tgo_edge_fn;
 typedef struct {
     int32_t scope;            /* tgo_scope of the Local message scope                     */
@@ -322,6 +340,15 @@ typedef struct {
 } tgo_gather_args;
 int  tgo_gather(tgo_ctx* ctx, const tgo_gather_args* args, const void* msg, const uint8_t* has,
                 void* out, uint8_t* out_has);
+/* The same receive WITHOUT a combiner: every vertex's message stream materialised —
+ * edgeFct(msg[u], e) for each entry of its reversed incident traversal whose sender holds a
+ * message, in the row's column order (the order the reference's stream yields them,
+ * VertexMemoryHandler.java:83-92) when the graph was loaded with TGO_LOAD_COLUMN_ORDER, else
+ * in (direction, neighbour) order.  row_offsets: n+1 (row order); values: NULL for a sizing
+ * call, else row_offsets[n] values.  args->combiner is ignored.  A vertex cut receiving 2 or
+ * more messages fails with TGO_E_PROGRAM (FulgoraUtil's ThrowingCombiner, :80-91). */
+int  tgo_gather_lists(tgo_ctx* ctx, const tgo_gather_args* args, const void* msg, const uint8_t* has,
+                      int64_t* row_offsets, void* values);
 /* targets: dense row ids (tgo_dense_ids); values: nmsgs int64 or fp64. */
 int  tgo_combine_global(tgo_ctx* ctx, int32_t value_type, int32_t combiner, int64_t nmsgs,
                         const int64_t* targets, const void* values, void* out, uint8_t* out_has);
@@ -349,10 +376,11 @@ int  tgo_dense_ids(tgo_ctx* ctx, const int64_t* titan_ids, int64_t count, int64_
  * out == NULL: only *size is filled; otherwise out's buffers (sized from a first call) get
  * nrows keys, nrows+1 entry / byte offsets, nbytes bytes and nentries limit|valuePos words
  * (the tgo_rows layout, so the rows can be scanned again). */
-typedef enum { TGO_RESULT_DISTANCE = 0, TGO_RESULT_PAGERANK = 1, TGO_RESULT_DEGREE = 2 } tgo_result_kind;
+typedef enum { TGO_RESULT_DISTANCE = 0, TGO_RESULT_PAGERANK = 1, TGO_RESULT_DEGREE = 2,
+               TGO_RESULT_VALUES = 3 } tgo_result_kind;
 typedef struct {
     int32_t kind;                 /* tgo_result_kind                                          */
-    int32_t reserved;
+    int32_t reserved;             /* TGO_RESULT_VALUES: tgo_value_type of the values           */
     int64_t key_ids[2];           /* [0] DISTANCE / PAGE_RANK / DEGREE key; [1] OUTGOING_EDGE_COUNT */
     int32_t datatypes[2];         /* tgo_datatype of each key                                  */
     int64_t relation_id_base;
@@ -366,6 +394,14 @@ typedef struct {
     int64_t* entry_limit_valpos;
 } tgo_rows_buf;
 int  tgo_result_rows(tgo_ctx* ctx, const tgo_result_args* args, tgo_result_size* size, const tgo_rows_buf* out);
+/* A generic program's compute key (kind TGO_RESULT_VALUES, key_ids[0], datatypes[0], value
+ * type in args->reserved): values / present in the API's row order, the host vectors the
+ * program's execute() left (int64: a Long, Integer or generic key — an Integer key needs
+ * every present value in int range, else TGO_E_INVALID; fp64: a Double or generic key).
+ * Entries exactly as for the native programs (one SINGLE-cardinality property entry per
+ * present vertex, FulgoraGraphComputer.java:248-305). */
+int  tgo_result_rows_values(tgo_ctx* ctx, const tgo_result_args* args, const void* values, const uint8_t* present,
+                            tgo_result_size* size, const tgo_rows_buf* out);
 
 int  tgo_stats_get(tgo_ctx* ctx, tgo_stats* out);
 /* Block until all work queued on the ctx stream has finished. */

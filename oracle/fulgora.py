@@ -124,6 +124,7 @@ def load() -> C.CDLL:
         "fr_pagerank": (C.c_int, [vp, C.c_double, C.c_int64, C.c_int, C.c_int, C.POINTER(C.c_double), P(C.c_int)]),
         "fr_degree_counter": (C.c_int, [vp, C.c_int, C.c_int, _i32p, P(C.c_int)]),
         "fr_gather": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, _u8p, vp, _u8p]),
+        "fr_gather_lists": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, vp, _u8p, _i64p, vp]),
         "fr_combine_global": (C.c_int, [C.c_int64, C.c_int, C.c_int, C.c_int64, _i64p, vp, vp, _u8p]),
     }
     for name, (res, args) in sig.items():
@@ -356,6 +357,25 @@ class OracleGraph:
         if rc:
             raise RuntimeError(f"fr_gather rc={rc}")
         return out, oh.astype(bool)
+
+    def gather_lists(self, scope, value_type, edge_fn, msg, has):
+        """Local-scope receive without a combiner (fr_gather_lists): (offsets n+1, values), every
+        vertex's messages in its row's column order."""
+        dt = np.int64 if value_type == 0 else np.float64
+        m = np.ascontiguousarray(msg, dt)
+        h = np.ascontiguousarray(has, np.uint8)
+        off = np.zeros(self.n + 1, np.int64)
+        lib = load()
+        rc = lib.fr_gather_lists(self.h, scope, value_type, edge_fn, m.ctypes.data_as(C.c_void_p), _p(h, C.c_uint8),
+                                 _p(off, C.c_int64), None)
+        if rc:
+            raise RuntimeError(f"fr_gather_lists rc={rc}")
+        vals = np.zeros(max(int(off[-1]), 1), dt)
+        rc = lib.fr_gather_lists(self.h, scope, value_type, edge_fn, m.ctypes.data_as(C.c_void_p), _p(h, C.c_uint8),
+                                 _p(off, C.c_int64), vals.ctypes.data_as(C.c_void_p))
+        if rc:
+            raise RuntimeError(f"fr_gather_lists rc={rc}")
+        return off, vals[:int(off[-1])]
 
     def degree_counter(self, length, threads=1):
         out = np.zeros(self.n, dtype=np.int32)

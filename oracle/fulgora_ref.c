@@ -358,7 +358,19 @@ static int read_object_x(const uint8_t* d, size_t len, size_t* pos, int dt, int 
         }
         break;
     case FR_DT_LONG: case FR_DT_DATE: for (int i = 0; i < 8; i++) u = (u << 8) | RD(); *ival = (int64_t)(u + (uint64_t)INT64_MIN); break;
-    case FR_DT_FLOAT: for (int i = 0; i < 4; i++) RD(); break;
+    case FR_DT_FLOAT: {                                  /* FloatSerializer.read / readByteOrder :33-46 */
+        uint32_t u = 0;
+        for (int i = 0; i < 4; i++) u = (u << 8) | RD();
+        if (byte_order) {                                /* NumericUtils.sortableIntToFloat */
+            u ^= 0x80000000u;
+            int32_t si = (int32_t)u;
+            si ^= (si >> 31) & 0x7fffffff;
+            u = (uint32_t)si;
+        }
+        if (u == 0x80000000u) u = 0;                     /* -0.0f as +0.0f (the product's weight sentinel) */
+        *ival = (int32_t)u;                              /* the IEEE bits */
+        break;
+    }
     case FR_DT_DOUBLE: for (int i = 0; i < 8; i++) RD(); break;
     case FR_DT_BOOLEAN: *ival = RD(); break;
     default: return FR_E_UNSUPPORTED;
@@ -488,6 +500,11 @@ int fr_encode_edge(fr_buf* out, int32_t* value_pos, const fr_schema* schema, int
     return FR_OK;
 }
 
+int fr_weight_datatype_ok(int dt) {
+    return dt == FR_DT_INTEGER || dt == FR_DT_BYTE || dt == FR_DT_SHORT || dt == FR_DT_CHARACTER ||
+           dt == FR_DT_BOOLEAN || dt == FR_DT_FLOAT;
+}
+
 int fr_decode_edge(const uint8_t* d, size_t len, size_t value_pos, const fr_schema* schema,
                    int64_t weight_key, int64_t* type_id, int* dir, int64_t* other_id,
                    int64_t* relation_id, int* has_weight, int64_t* weight) {
@@ -520,9 +537,10 @@ int fr_decode_edge(const uint8_t* d, size_t len, size_t value_pos, const fr_sche
     }
     *has_weight = 0;
     if (weight_key == 0) return FR_OK;
-    /* ShortestDistance reads edge.<Integer>value(weight) (ShortestDistanceVertexProgram.java:53):
-     * any other datatype is a ClassCastException in the reference. */
-    if (key_datatype(schema, weight_key) != FR_DT_INTEGER) return FR_E_UNSUPPORTED;
+    /* The weight: an integral key that fits 32 bits, or a Float (its IEEE bits).
+     * ShortestDistance itself casts to Integer (ShortestDistanceVertexProgram.java:53):
+     * fr_shortest_distance rejects the others (a ClassCastException in the reference). */
+    if (!fr_weight_datatype_ok(key_datatype(schema, weight_key))) return FR_E_UNSUPPORTED;
     if (mult == FR_MULTI) {                                              /* sort key :130-140 */
         size_t kp = pos;                                                 /* startKeyPos: after the type */
         const uint8_t x = t->sort_order == FR_DESC ? 0xFF : 0x00;        /* in.subrange(keyLength, true) */
@@ -571,6 +589,7 @@ struct fr_graph {
      * on the full-size parity tests.  NULL = probe the hash map per entry, as the reference. */
     int64_t* oidx;
     int64_t nent;             /* entries stored in other/edir/has_w/w                */
+    int32_t wdt;              /* datatype of the weight key (0: Integer / none)       */
 };
 
 static uint64_t mix64(uint64_t x) {
@@ -752,6 +771,7 @@ int fr_load_rows(const fr_rows* rows, const fr_schema* schema, const fr_load_opt
     free(kind); free(rid);
     st.num_entries = e;
     g->nent = e;
+    g->wdt = opts->weight_key ? key_datatype(schema, opts->weight_key) : 0;
     *out = g;
     if (stats) *stats = st;
     return FR_OK;
@@ -991,6 +1011,9 @@ static void sd_exec(void* p, const fr_graph* g, int64_t lo, int64_t hi) {
 }
 int fr_shortest_distance(const fr_graph* g, int64_t seed, int max_depth, int scope, int weighted,
                          int threads, int64_t* dist_out, int* iterations_out) {
+    /* edge.<Integer>value(weight) (ShortestDistanceVertexProgram.java:53): another weight
+     * datatype is a ClassCastException in the reference */
+    if (weighted && g->wdt != 0 && g->wdt != FR_DT_INTEGER) return FR_E_UNSUPPORTED;
     sd_t s; memset(&s, 0, sizeof s);
     s.scope = scope; s.weighted = weighted; s.seed = seed;
     s.dist = dist_out;
@@ -1179,11 +1202,61 @@ static inline double g_combine_d(int comb, double acc, double m) {
     if (comb == 2) return m > acc ? m : acc;
     return m + acc;
 }
+/* The edge functions "m op w" (w = e.value(weight)) in Java arithmetic: long + - * wrap,
+ * long / truncates (MIN_VALUE / -1 = MIN_VALUE, / 0 throws ArithmeticException), double ops
+ * are IEEE; a Float weight is widened to double (and refused with long messages).
+ * Returns 0, or FR_E_PROGRAM for a division by zero. */
+static int edge_fn_i(int fn, int64_t m, int64_t w, int64_t* out) {
+    uint64_t u = (uint64_t)m;
+    switch (fn) {
+    case 0: *out = m; return 0;
+    case 1: *out = (int64_t)(u + 1u); return 0;
+    case 2: *out = (int64_t)(u + (uint64_t)w); return 0;
+    case 3: *out = (int64_t)(u * (uint64_t)w); return 0;
+    case 4: *out = (int64_t)(u - (uint64_t)w); return 0;
+    case 5: *out = w < m ? w : m; return 0;
+    case 6: *out = w > m ? w : m; return 0;
+    default:
+        if (w == 0) return FR_E_PROGRAM;
+        *out = w == -1 ? (int64_t)(0u - u) : m / w;
+        return 0;
+    }
+}
+static double edge_fn_d(int fn, double m, double x) {
+    switch (fn) {
+    case 0: return m;
+    case 1: return m + 1.0;
+    case 2: return m + x;
+    case 3: return m * x;
+    case 4: return m - x;
+    case 5: return x < m ? x : m;
+    case 6: return x > m ? x : m;
+    default: return m / x;
+    }
+}
+static double weight_as_double(const fr_graph* g, int32_t w) {
+    if (g->wdt == FR_DT_FLOAT) { float f; memcpy(&f, &w, 4); return (double)f; }
+    return (double)w;
+}
+/* One message edgeFct(msg[o], e) of entry k (VertexMemoryHandler.java:83-92); 1 = present,
+ * 0 = filtered (no message), <0 = the program fails. */
+static int entry_message(const fr_graph* g, int64_t k, int64_t o, int value_type, int edge_fn, const void* msg,
+                         int64_t* mi_out, double* md_out) {
+    int64_t w = 0;
+    if (edge_fn >= 2) {
+        if (!g->has_w[k]) return FR_E_PROGRAM;                                 /* e.value(key) throws */
+        w = g->w[k];
+    }
+    if (value_type == 0) {
+        if (edge_fn >= 2 && g->wdt == FR_DT_FLOAT) return FR_E_INVALID;
+        return edge_fn_i(edge_fn, ((const int64_t*)msg)[o], w, mi_out) ? FR_E_PROGRAM : 1;
+    }
+    *md_out = edge_fn_d(edge_fn, ((const double*)msg)[o], edge_fn >= 2 ? weight_as_double(g, (int32_t)w) : 0.0);
+    return 1;
+}
 int fr_gather(const fr_graph* g, int scope, int value_type, int combiner, int edge_fn, const void* msg,
               const uint8_t* has, void* out, uint8_t* out_has) {
-    const int64_t* mi = (const int64_t*)msg; const double* md = (const double*)msg;
     int64_t* oi = (int64_t*)out; double* od = (double*)out;
-    int needs_w = edge_fn == 2 || edge_fn == 3;
     for (int64_t v = 0; v < g->n; v++) {
         int any = 0; int64_t ai = 0; double ad = 0.0;
         for (int64_t i = 0; i < nrows_of(g, v); i++) {
@@ -1192,29 +1265,45 @@ int fr_gather(const fr_graph* g, int scope, int value_type, int combiner, int ed
                 if (!take(scope, g->edir[k])) continue;
                 int64_t o = entry_vertex(g, k);
                 if (o < 0 || !has[o]) continue;                                /* filter(m != null) */
-                int64_t w = 0;
-                if (needs_w) {
-                    if (!g->has_w[k]) return FR_E_PROGRAM;                     /* e.value(key) throws */
-                    w = g->w[k];
-                }
-                if (value_type == 0) {
-                    uint64_t m = (uint64_t)mi[o];
-                    if (edge_fn == 1) m += 1u;
-                    else if (edge_fn == 2) m += (uint64_t)w;
-                    else if (edge_fn == 3) m *= (uint64_t)w;
-                    ai = any ? g_combine_i(combiner, ai, (int64_t)m) : (int64_t)m;
-                } else {
-                    double m = md[o];
-                    if (edge_fn == 1) m += 1.0;
-                    else if (edge_fn == 2) m += (double)w;
-                    else if (edge_fn == 3) m *= (double)w;
-                    ad = any ? g_combine_d(combiner, ad, m) : m;
-                }
+                int64_t mi = 0; double md = 0.0;
+                int rc = entry_message(g, k, o, value_type, edge_fn, msg, &mi, &md);
+                if (rc < 0) return rc;
+                if (value_type == 0) ai = any ? g_combine_i(combiner, ai, mi) : mi;
+                else ad = any ? g_combine_d(combiner, ad, md) : md;
                 any = 1;
             }
         }
         if (value_type == 0) oi[v] = ai; else od[v] = ad;
         out_has[v] = (uint8_t)any;
+    }
+    return FR_OK;
+}
+/* Local receive WITHOUT a combiner: the stream itself, per vertex in the order the
+ * reference's receiveMessages yields it — its row's entries in column order (VertexMemoryHandler
+ * .java:83-92).  off: n+1; vals: NULL for a sizing call.  A vertex cut that receives two or
+ * more messages meets FulgoraUtil's ThrowingCombiner (:80-91): FR_E_PROGRAM. */
+int fr_gather_lists(const fr_graph* g, int scope, int value_type, int edge_fn, const void* msg, const uint8_t* has,
+                    int64_t* off, void* vals) {
+    int64_t* vi = (int64_t*)vals; double* vd = (double*)vals;
+    int64_t p = 0;
+    off[0] = 0;
+    for (int64_t v = 0; v < g->n; v++) {
+        int64_t c = 0;
+        for (int64_t i = 0; i < nrows_of(g, v); i++) {
+            int64_t kb, ke; row_range(g, v, i, &kb, &ke);
+            for (int64_t k = kb; k < ke; k++) {
+                if (!take(scope, g->edir[k])) continue;
+                int64_t o = entry_vertex(g, k);
+                if (o < 0 || !has[o]) continue;
+                int64_t mi = 0; double md = 0.0;
+                int rc = entry_message(g, k, o, value_type, edge_fn, msg, &mi, &md);
+                if (rc < 0) return rc;
+                if (vals) { if (value_type == 0) vi[p] = mi; else vd[p] = md; }
+                p++; c++;
+            }
+        }
+        if (g->pv && g->pv[v] && c >= 2) return FR_E_PROGRAM;
+        off[v + 1] = p;
     }
     return FR_OK;
 }

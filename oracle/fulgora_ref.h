@@ -165,6 +165,9 @@ int fr_pagerank(const fr_graph* g, double alpha, int64_t vertex_count, int max_i
                 int threads, double* pr_out, int* iterations_out);
 /* Generic message passing (value_type 0 = int64, 1 = fp64; combiner 0 SUM, 1 MIN, 2 MAX;
  * edge_fn 0 identity, 1 +1, 2 +weight, 3 *weight).  Vectors in oracle vertex order. */
+int fr_weight_datatype_ok(int datatype);
+int fr_gather_lists(const fr_graph* g, int scope, int value_type, int edge_fn, const void* msg, const uint8_t* has,
+                    int64_t* off, void* vals);
 int fr_gather(const fr_graph* g, int scope, int value_type, int combiner, int edge_fn, const void* msg,
               const uint8_t* has, void* out, uint8_t* out_has);
 int fr_combine_global(int64_t n, int value_type, int combiner, int64_t nmsgs, const int64_t* targets,

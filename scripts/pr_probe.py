@@ -20,7 +20,7 @@ n = 1 << scale
 src, dst, _ = rmat_edges(scale, 16, seed=0x54495441)
 eng = None
 loaded_with = None
-KEYS = ("TGO_PR_BLOCKED", "TGO_PR_HOT", "TGO_PR_SEG", "TGO_PR_DIAG", "TGO_PR_PACK", "TGO_PR_CPACK", "TGO_PR_HOT_TILE")
+KEYS = ("TGO_PR_BLOCKED", "TGO_PR_HOT", "TGO_PR_SEG", "TGO_PR_DIAG", "TGO_PR_PACK", "TGO_PR_CPACK", "TGO_PR_HOT_TILE", "TGO_PR_HOT_PIPE")
 variants = [
     {},
     {"TGO_PR_BLOCKED": "0"},
@@ -31,7 +31,7 @@ variants = [
     {"TGO_PR_DIAG": "-2:-1"},                 # no gathers at all: index stream + finalize
     {},
 ]
-RELOAD = ("TGO_PR_BLOCKED", "TGO_PR_HOT", "TGO_PR_SEG", "TGO_PR_PACK", "TGO_PR_CPACK", "TGO_PR_HOT_TILE")   # read at load time
+RELOAD = ("TGO_PR_BLOCKED", "TGO_PR_HOT", "TGO_PR_SEG", "TGO_PR_PACK", "TGO_PR_CPACK", "TGO_PR_HOT_TILE", "TGO_PR_HOT_PIPE")   # read at load time
 if os.environ.get("PR_PROBE_DEFAULT_ONLY"):       # one variant: the TGO_PR_* settings of the caller's environment
     variants = [{k: os.environ[k] for k in KEYS if k in os.environ}]
 if os.environ.get("PR_PROBE_VARIANTS"):        # a JSON list of env dicts, e.g. '[{}, {"TGO_PR_SEG": "393216"}]'

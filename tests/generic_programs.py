@@ -28,6 +28,10 @@ class OracleEngine:
         h = np.ones(self.n, bool) if has is None else has
         return self.o.gather(scope, value_type, combiner, edge_fn, msg, h)
 
+    def gather_lists(self, scope, value_type, edge_fn, msg, has):
+        h = np.ones(self.n, bool) if has is None else has
+        return self.o.gather_lists(scope, value_type, edge_fn, msg, h)
+
     def combine_global(self, value_type, combiner, targets, values):
         return fr.combine_global(self.n, value_type, combiner, targets, values)
 
@@ -150,3 +154,63 @@ class GlobalDegreeSum(GenericVertexProgram):
 
     def terminate(self, memory):
         return memory.getIteration() >= 2
+
+
+class FirstLastCount(GenericVertexProgram):
+    """No combiner: iteration 0 every vertex sends (its Titan id mod 1000) on inE with the edge
+    function sub_weight; iteration 1 each vertex keeps the first and the last message of its
+    stream and their count (order-sensitive: the stream order is the reference's)."""
+    value_type = L.VAL_INT64
+    combiner = None
+    compute_keys = ("first", "last", "count")
+    weight_property = "w"
+    SCOPE = MessageScope.Local("inE", "sub_weight")
+
+    def getMessageScopes(self, memory):  # noqa: N802
+        return [self.SCOPE] if memory.getIteration() == 0 else []
+
+    def execute(self, v, messenger, memory):
+        if memory.getIteration() == 0:
+            messenger.send(self.SCOPE, np.asarray(v.ids, np.int64) % 1000)
+            return
+        lists = messenger.receive(self.SCOPE)
+        cnt = lists.counts()
+        has = cnt > 0
+        first = np.zeros(v.n, np.int64)
+        last = np.zeros(v.n, np.int64)
+        first[has] = lists.values[lists.offsets[:-1][has]]
+        last[has] = lists.values[lists.offsets[1:][has] - 1]
+        v.set_property("first", first, has)
+        v.set_property("last", last, has)
+        v.set_property("count", cnt.astype(np.int64))
+
+    def terminate(self, memory):
+        return memory.getIteration() >= 1
+
+
+class GlobalNoCombiner(GenericVertexProgram):
+    """No combiner, a Global scope: every vertex sends 3 x its index to one target (a
+    permutation when unique, else two senders share each target -> the job fails)."""
+    value_type = L.VAL_INT64
+    combiner = None
+    compute_keys = ("inbox",)
+    SCOPE = MessageScope.Global()
+
+    def __init__(self, ids, unique=True):
+        self.ids = np.asarray(ids, np.int64)
+        self.unique = unique
+
+    def getMessageScopes(self, memory):  # noqa: N802
+        return [self.SCOPE] if memory.getIteration() == 0 else []
+
+    def execute(self, v, messenger, memory):
+        n = v.n
+        if memory.getIteration() == 0:
+            tgt = self.ids[::-1] if self.unique else self.ids[np.arange(n) // 2]
+            messenger.send_global(self.SCOPE, tgt, 3 * np.arange(n, dtype=np.int64))
+            return
+        inbox, has = messenger.receive(self.SCOPE)
+        v.set_property("inbox", inbox, has)
+
+    def terminate(self, memory):
+        return memory.getIteration() >= 1

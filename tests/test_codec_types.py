@@ -123,7 +123,8 @@ def _oracle_decode(s, b, vp, weight_key):
 def _product_decode(sd, b, vp, weight_key, labels=()):
     sch = Schema.from_dict(sd)
     lab = np.asarray(labels, np.int64)
-    opts = L.LoadOpts(0, 1, len(lab), L.ptr(lab, C.c_int64) if len(lab) else None, weight_key)
+    opts = L.LoadOpts(scope=0, apply_cap=1, n_labels=len(lab), label_ids=L.ptr(lab, C.c_int64) if len(lab) else None,
+                      weight_key=weight_key)
     arr = (C.c_uint8 * max(1, len(b))).from_buffer_copy(b or b"\0")
     e = L.EdgeEntry()
     rc = L.load().tgo_decode_edge_entry(C.byref(sch.c), C.byref(opts), C.cast(arr, C.POINTER(C.c_uint8)),
@@ -203,6 +204,29 @@ def test_non_integer_weight_key_is_rejected():
     E_UNSUPPORTED = -7                     # TGO_E_UNSUPPORTED / FR_E_UNSUPPORTED
     assert _oracle_decode(s, b, vp, K[LONG])[0] == E_UNSUPPORTED
     assert _product_decode(sd, b, vp, K[LONG])[0] == E_UNSUPPORTED
+
+
+@pytest.mark.parametrize("dt", [BYTE, SHORT, CHARACTER, BOOLEAN, FLOAT])
+@pytest.mark.parametrize("where", ["sort_key", "signature", "remaining"])
+def test_32_bit_weight_datatypes_decode_alike(dt, where):
+    """A weight of any datatype that fits 32 bits (generic programs' edge functions read it):
+    integral values as integers, a Float as its IEEE bits (-0.0 as +0.0), in the sort key (ASC /
+    DESC byte-ordered form), the signature or the remaining properties; oracle == product."""
+    import struct
+    vals = {BYTE: [-128, -1, 0, 5, 127], SHORT: [-32768, -3, 0, 7, 32767], CHARACTER: [0, 65, 65535],
+            BOOLEAN: [0, 1], FLOAT: [-7, -1, 0, 3, 1000]}[dt]
+    for order in ("ASC", "DESC"):
+        sd = schema_dict(0, [K[dt]] if where == "sort_key" else [], [K[dt]] if where == "signature" else [], order)
+        s = osch(sd)
+        for i, x in enumerate(vals):
+            b, vp = fr.encode_edge(s, KNOWS, i % 2, 8 + 8 * i, 100 + i, [(K[dt], x)])
+            orc, o = _oracle_decode(s, b, vp, K[dt])
+            prc, e = _product_decode(sd, b, vp, K[dt])
+            assert orc == 0 and prc == 0 and e.has_weight == 1 == o[4]
+            want = struct.unpack("<i", struct.pack("<f", float(x)))[0] if dt == FLOAT else x
+            if dt == FLOAT and x == 0:
+                want = 0
+            assert e.weight == o[5] == want, (dt, where, order, x)
 
 
 def test_compressed_string_is_skipped():

@@ -60,12 +60,21 @@ def python_gather(off, mid, adj, w, scope, vt, comb, fn, msg, has):
                 if not has[u]:
                     continue
                 m = msg[u]
+                x = w[k] if fn >= 2 else 0
                 if fn == 1:
                     m = m + 1
                 elif fn == 2:
-                    m = m + w[k]
+                    m = m + x
                 elif fn == 3:
-                    m = m * w[k]
+                    m = m * x
+                elif fn == 4:
+                    m = m - x
+                elif fn == 5:
+                    m = min(m, x)
+                elif fn == 6:
+                    m = max(m, x)
+                elif fn == 7:                      # Java: long / truncates toward zero
+                    m = (abs(int(m)) // abs(int(x))) * (1 if (m < 0) == (x < 0) else -1) if vt == 0 else m / x
                 if vt == 0:
                     m = np.int64(m)
                 if not any_:
@@ -82,7 +91,9 @@ def python_gather(off, mid, adj, w, scope, vt, comb, fn, msg, has):
 
 
 @pytest.mark.parametrize("scope", [IN, OUT, BOTH])
-@pytest.mark.parametrize("vt,comb,fn", [(0, 0, 0), (0, 1, 2), (0, 2, 1), (1, 0, 3), (1, 1, 0), (1, 0, 2)])
+@pytest.mark.parametrize("vt,comb,fn", [(0, 0, 0), (0, 1, 2), (0, 2, 1), (1, 0, 3), (1, 1, 0), (1, 0, 2),
+                                        (0, 0, 4), (0, 1, 5), (0, 2, 6), (0, 0, 7), (1, 0, 4), (1, 1, 5),
+                                        (1, 2, 6), (1, 0, 7)])
 def test_oracle_gather_matches_plain_restatement(scope, vt, comb, fn):
     scale = 7
     n = 1 << scale
@@ -178,3 +189,98 @@ def test_global_scope_program_through_the_oracle_loop():
     for h, s in exp.items():
         assert inbox[pos[h]] == s
     assert mem.get("total") == int(wdeg.sum()) and mem.get("best") == max(exp.values())
+
+
+def python_lists(off, mid, adj, w, scope, vt, fn, msg, has):
+    """Per-vertex message streams on the exported adjacency (OUT entries first, in stored
+    order = column order for an edge-list graph of one label)."""
+    n = len(off) - 1
+    o2 = np.zeros(n + 1, np.int64)
+    vals = []
+    for v in range(n):
+        rr = {IN: [(off[v], mid[v])], OUT: [(mid[v], off[v + 1])], BOTH: [(off[v], off[v + 1])]}[scope]
+        for b, e in rr:
+            for k in range(b, e):
+                u = adj[k]
+                if has[u]:
+                    m = python_gather(np.array([0, 1]), np.array([1]), np.array([0]), np.array([w[k]]), IN, vt, 0, fn,
+                                      np.array([msg[u]]), np.array([True]))[0][0]
+                    vals.append(m)
+        o2[v + 1] = len(vals)
+    return o2, np.array(vals, np.int64 if vt == 0 else np.float64)
+
+
+@pytest.mark.parametrize("scope", [IN, OUT, BOTH])
+@pytest.mark.parametrize("vt,fn", [(0, 0), (0, 4), (1, 2), (1, 7)])
+def test_oracle_gather_lists_are_the_streams_in_column_order(scope, vt, fn):
+    """fr_gather_lists: no combiner — each vertex's stream as VertexMemoryHandler.receiveMessages
+    yields it (VertexMemoryHandler.java:83-92): the row's entries in column order, null
+    messages filtered, edgeFct applied."""
+    scale = 6
+    n = 1 << scale
+    src, dst, w = rmat_edges(scale, 4, seed=14, weights=True)
+    o = fr.OracleGraph.from_edges(n, src, dst, w)
+    off, mid, adj, ww = o.export(weighted=True)
+    rng = np.random.default_rng(5)
+    msg = rng.integers(-1000, 1000, n) if vt == 0 else rng.standard_normal(n)
+    has = rng.random(n) < 0.7
+    got_off, got = o.gather_lists(scope, vt, fn, msg, has)
+    exp_off, exp = python_lists(off, mid, adj, ww, scope, vt, fn, msg, has)
+    assert np.array_equal(got_off, exp_off)
+    if vt == 0:
+        assert np.array_equal(got, exp)
+    else:
+        np.testing.assert_allclose(got, exp, rtol=1e-15)
+    # folded with SUM the streams give the combined receive
+    comb, ch = o.gather(scope, vt, 0, fn, msg, has)
+    from titan_amd.generic import MessageLists
+    red, rh = MessageLists(got_off, got).reduce(np.add)
+    assert np.array_equal(rh, ch)
+    assert np.allclose(red, comb, rtol=1e-12)
+
+
+def test_oracle_integer_division_by_zero_fails():
+    n = 4
+    src, dst, w = np.array([0, 1], np.int32), np.array([1, 2], np.int32), np.array([3, 0], np.int32)
+    o = fr.OracleGraph.from_edges(n, src, dst, w)
+    with pytest.raises(RuntimeError):
+        o.gather(IN, 0, 0, 7, np.ones(n, np.int64), np.ones(n, bool))
+    out, has = o.gather(IN, 1, 0, 7, np.ones(n), np.ones(n, bool))          # double: IEEE infinity
+    assert has[1] and np.isinf(out[1])
+
+
+def test_combiner_less_program_through_the_oracle_loop():
+    """A program without a combiner reads message streams (MessageLists): the first and the
+    last message of each vertex and their count — order-sensitive, so the stream order matters."""
+    from generic_programs import FirstLastCount
+    scale = 7
+    n = 1 << scale
+    src, dst, w = rmat_edges(scale, 4, seed=22, weights=True)
+    o = fr.OracleGraph.from_edges(n, src, dst, w)
+    mem = FulgoraMemory()
+    verts = run_generic(OracleEngine(o), FirstLastCount(), mem)
+    first, fp = verts.property("first")
+    cnt, _ = verts.property("count")
+    off, mid, adj, ww = o.export(weighted=True)
+    ids = o.vertex_ids()
+    for v in range(n):
+        ins = [int(ids[adj[k]] % 1000) - int(ww[k]) for k in range(off[v], mid[v])]    # inE: walk OUT entries, sub_weight
+        assert cnt[v] == len(ins)
+        assert fp[v] == bool(ins)
+        if ins:
+            assert first[v] == ins[0] and verts.property("last")[0][v] == ins[-1]
+
+
+def test_global_scope_without_combiner_delivers_single_messages_only():
+    from generic_programs import GlobalNoCombiner
+    scale = 6
+    n = 1 << scale
+    src, dst, _ = rmat_edges(scale, 4, seed=23)
+    o = fr.OracleGraph.from_edges(n, src, dst)
+    ids = o.vertex_ids()
+    verts = run_generic(OracleEngine(o), GlobalNoCombiner(ids, unique=True), FulgoraMemory())
+    inbox, has = verts.property("inbox")
+    assert has.sum() == n and np.array_equal(inbox, np.arange(n)[::-1] * 3)
+    from titan_amd import TitanException
+    with pytest.raises(TitanException):               # two messages meet at one target: ThrowingCombiner
+        run_generic(OracleEngine(o), GlobalNoCombiner(ids, unique=False), FulgoraMemory())

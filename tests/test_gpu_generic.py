@@ -12,7 +12,8 @@ import pytest
 
 import fulgora as fr
 from conftest import load_fixture
-from generic_programs import ConnectedComponents, GenericPageRank, GlobalDegreeSum, OracleEngine
+from generic_programs import (ConnectedComponents, FirstLastCount, GenericPageRank, GlobalDegreeSum, GlobalNoCombiner,
+                              OracleEngine)
 from titan_amd import (ComputeKeyMapReduce, Engine, ExecutionException, GpuGraph, Schema, TitanException,
                        TitanGraphComputer, rmat_edges)
 from titan_amd import _lib as L
@@ -47,7 +48,8 @@ def test_local_gather_matches_oracle(weighted_rmat, load_scope, scope):
         msg = rng.integers(-(1 << 40), 1 << 40, n) if vt == L.VAL_INT64 else rng.standard_normal(n)
         has = rng.random(n) < 0.6
         for comb in (L.COMBINE_SUM, L.COMBINE_MIN, L.COMBINE_MAX):
-            for fn in (L.EDGE_IDENTITY, L.EDGE_ADD_ONE, L.EDGE_ADD_WEIGHT, L.EDGE_MUL_WEIGHT):
+            for fn in (L.EDGE_IDENTITY, L.EDGE_ADD_ONE, L.EDGE_ADD_WEIGHT, L.EDGE_MUL_WEIGHT, L.EDGE_SUB_WEIGHT,
+                       L.EDGE_MIN_WEIGHT, L.EDGE_MAX_WEIGHT, L.EDGE_DIV_WEIGHT):
                 got, gh = eng.gather(scope, vt, comb, fn, msg, has)
                 exp, eh = o.gather(scope, vt, comb, fn, msg, has)
                 assert np.array_equal(gh, eh), (vt, comb, fn)
@@ -177,20 +179,155 @@ def test_components_over_vertex_cuts():
     assert np.array_equal(reorder(ids, cc, verts.ids), verts.property("cc")[0])
 
 
-def test_generic_program_write_back_is_rejected():
-    """PERSIST / LOCALTX write back the natively run programs' compute keys
-    (tests/test_gpu_writeback.py); a generic program's keys are not encoded: the job fails
-    (ExecutionException from get(), as a failing Fulgora job does)."""
+def test_generic_program_write_back():
+    """PERSIST / LOCALTX of a generic program's element compute keys (FulgoraGraphComputer.java:
+    248-305): one SINGLE-cardinality entry per vertex holding a value, byte-exact against the
+    oracle's EdgeSerializer restatement — a typed Long key and a generic (Object) key, read
+    back through the store (PERSIST) or the local transaction (LOCALTX)."""
     rows, vids, sd, npz = load_fixture("gotg")
-    computer = GpuGraph(rows, sd).compute()
+    cc_key = (7000 << 6) | 5
+    graph = GpuGraph(rows, sd, property_keys={"cc": (cc_key, L.DT_LONG)})
+    computer = graph.compute()
     computer.resultMode(TitanGraphComputer.ResultMode.PERSIST)
     computer.program(ConnectedComponents())
+    res = computer.submit().get()
+    ids, (cc, present) = res.vertex_properties["cc"]
+    assert res.graph() is graph and present.all()
+    for vid, c in zip(ids, cc):
+        assert graph.read_property(int(vid), cc_key, L.DT_LONG) == int(c)
+    # the device rows equal the oracle's encoder, relation ids base + running index
+    eng = Engine().load_rows(rows, Schema.from_dict(sd), BOTH)
+    base = 1 << 30
+    got = eng.result_rows_values(cc_key, L.DT_LONG, L.VAL_INT64, reorder(ids, cc, eng.vertex_ids()),
+                                 np.ones(eng.n, bool), base)
+    lib = fr.load()
+    want = [fr.encode_property(cc_key, L.DT_LONG, int(c), base + i)
+            for i, c in enumerate(reorder(ids, cc, eng.vertex_ids()))]
+    for r in range(got.nrows):
+        b = bytes(got.data[got.byte_begin[r]:got.byte_begin[r + 1]])
+        lv = int(got.limit_valpos[r])
+        assert (b, lv & 0x7FFFFFFF) == want[r] and got.keys[r] == lib.fr_key_of(int(eng.vertex_ids()[r]), 5)
+    # generic key (no schema): LOCALTX leaves the store alone; fp64 values
+    g2 = GpuGraph(rows, sd)
+    c2 = g2.compute()
+    c2.resultMode(TitanGraphComputer.ResultMode.LOCALTX)
+    c2.program(GenericPageRank(0.85, eng.n, 4))
+    res = c2.submit().get()
+    key, dt = g2.property_key("pr")
+    assert dt == L.DT_OBJECT
+    ids, (pr, _) = res.vertex_properties["pr"]
+    assert g2.read_property(int(ids[0]), key, L.DT_OBJECT) is None
+    assert [res.graph().read_property(int(v), key, L.DT_OBJECT) for v in ids] == [float(x) for x in pr]
+    got = eng.result_rows_values(key, L.DT_OBJECT, L.VAL_FP64, np.full(eng.n, 0.25), np.arange(eng.n) % 2 == 0, 9)
+    assert got.nrows == (eng.n + 1) // 2
+    assert bytes(got.data[:got.byte_begin[1]]) == fr.encode_property_generic(key, L.DT_DOUBLE, 0.25, 9)[0]
+    with pytest.raises(TitanException):                     # an Integer key holds int values only
+        eng.result_rows_values(cc_key, L.DT_INTEGER, L.VAL_INT64, np.full(eng.n, 1 << 40), np.ones(eng.n, bool), 9)
+
+
+def float_weight_rows():
+    """A weighted power-law graph whose weight is a Float property (values -3..250)."""
+    import edgestore as es
+    scale = 9
+    n = 1 << scale
+    src, dst, w = rmat_edges(scale, 8, seed=91, weights=True)
+    knows = es.user_edge_label(1)
+    fkey = es.user_property_key(3)
+    sd = {"edge_types": [{"type_id": knows, "multiplicity": 0}], "property_keys": [[fkey, 5]]}
+    osch = fr.OracleSchema(sd["edge_types"], [(fkey, 5)])
+    spec = es.GraphSpec(n=n, edges=[(int(a), int(b), knows, [(fkey, int(x) - 4)]) for a, b, x in zip(src, dst, w)])
+    rows, vids = es.build_rows(spec, osch)
+    return rows, vids, sd, osch, fkey, n
+
+
+def test_float_weights_in_generic_edge_functions():
+    """A Float weight (FloatSerializer bits): generic fp64 edge functions read it widened to
+    double, int64 messages are refused, and ShortestDistance (edge.<Integer>value) fails as
+    its ClassCastException does."""
+    rows, vids, sd, osch, fkey, n = float_weight_rows()
+    eng = Engine().load_rows(rows, Schema.from_dict(sd), IN, weight_key=fkey)
+    o = fr.OracleGraph.from_rows(rows, osch, IN, weight_key=fkey)
+    rng = np.random.default_rng(2)
+    msg = rng.standard_normal(eng.n)
+    has = rng.random(eng.n) < 0.8
+    for fn in (L.EDGE_ADD_WEIGHT, L.EDGE_MUL_WEIGHT, L.EDGE_SUB_WEIGHT, L.EDGE_MIN_WEIGHT, L.EDGE_MAX_WEIGHT,
+               L.EDGE_DIV_WEIGHT):
+        got, gh = eng.gather(IN, L.VAL_FP64, L.COMBINE_MAX, fn, msg, has)
+        exp, eh = o.gather(IN, 1, 2, fn, msg, has)
+        assert np.array_equal(gh, eh) and np.array_equal(got[gh], exp[eh]), fn
+    with pytest.raises(TitanException) as e:
+        eng.gather(IN, L.VAL_INT64, L.COMBINE_SUM, L.EDGE_ADD_WEIGHT, np.zeros(eng.n, np.int64))
+    assert e.value.code == L.TGO_E_INVALID
+    with pytest.raises(TitanException) as e:
+        eng.sssp(int(vids[0]), 5, IN)
+    assert e.value.code == L.TGO_E_UNSUPPORTED
+    with pytest.raises(RuntimeError):
+        o.shortest_distance(int(vids[0]), 5, IN, weighted=True)
+
+
+def test_integer_division_by_zero_fails_the_program():
+    n = 64
+    src, dst, w = np.array([0, 1, 2], np.int32), np.array([1, 2, 3], np.int32), np.array([3, 0, 5], np.int32)
+    eng = Engine().load_edges(n, src, dst, IN, weight=w)
+    with pytest.raises(TitanException) as e:
+        eng.gather(IN, L.VAL_INT64, L.COMBINE_SUM, L.EDGE_DIV_WEIGHT, np.ones(n, np.int64))
+    assert e.value.code == L.TGO_E_PROGRAM
+    out, has = eng.gather(IN, L.VAL_FP64, L.COMBINE_SUM, L.EDGE_DIV_WEIGHT, np.ones(n))
+    assert has[1] and np.isinf(out[1]) and out[0] == 1.0 / 3
+
+
+@pytest.mark.parametrize("column_order", [False, True])
+@pytest.mark.parametrize("load_scope,scope", [(IN, IN), (OUT, OUT), (BOTH, BOTH), (BOTH, IN)])
+def test_gather_lists_match_oracle_streams(weighted_rmat, load_scope, scope, column_order):
+    """Combiner-less receive (tgo_gather_lists) over an edge list: every vertex's stream equal
+    to the oracle's (fr_gather_lists), element by element.  For an edge list the (direction,
+    neighbour) order IS the column order, so both loads must match."""
+    n, src, dst, w = weighted_rmat
+    eng = Engine().load_edges(n, src, dst, load_scope, weight=w, apply_cap=False, column_order=column_order)
+    o = fr.OracleGraph.from_edges(n, src, dst, w)
+    rng = np.random.default_rng(17)
+    for vt, fn in ((L.VAL_INT64, L.EDGE_IDENTITY), (L.VAL_INT64, L.EDGE_SUB_WEIGHT), (L.VAL_FP64, L.EDGE_MUL_WEIGHT)):
+        msg = rng.integers(-(1 << 40), 1 << 40, n) if vt == L.VAL_INT64 else rng.standard_normal(n)
+        has = rng.random(n) < 0.6
+        off, vals = eng.gather_lists(scope, vt, fn, msg, has)
+        ooff, ovals = o.gather_lists(scope, vt, fn, msg, has)
+        assert np.array_equal(off, ooff)
+        assert np.array_equal(vals, ovals), (vt, fn)
+
+
+def test_gather_lists_in_column_order_on_edgestore_rows():
+    """GraphOfTheGods rows (several labels: the column order interleaves labels and
+    directions): with TGO_LOAD_COLUMN_ORDER every stream is in the reference's order."""
+    rows, vids, sd, npz = load_fixture("gotg")
+    osch = fr.OracleSchema(sd["edge_types"], [tuple(x) for x in sd["property_keys"]])
+    o = fr.OracleGraph.from_rows(rows, osch, BOTH)
+    eng = Engine().load_rows(rows, Schema.from_dict(sd), BOTH, column_order=True)
+    assert np.array_equal(eng.vertex_ids(), o.vertex_ids())
+    msg = np.arange(eng.n, dtype=np.int64) * 10
+    for scope in (IN, OUT, BOTH):
+        off, vals = eng.gather_lists(scope, L.VAL_INT64, L.EDGE_ADD_ONE, msg, np.ones(eng.n, bool))
+        ooff, ovals = o.gather_lists(scope, 0, 1, msg, np.ones(eng.n, bool))
+        assert np.array_equal(off, ooff) and np.array_equal(vals, ovals), scope
+
+
+def test_combiner_less_programs(weighted_rmat):
+    n, src, dst, w = weighted_rmat
+    o = fr.OracleGraph.from_edges(n, src, dst, w)
+    result, verts, mem = run_both({"edges": (n, src, dst, w)}, FirstLastCount, o, weight_keys={"w": 1})
+    for key in ("first", "last", "count"):
+        ids, (vals, present) = result.vertex_properties[key]
+        assert np.array_equal(reorder(ids, present, verts.ids), verts.property(key)[1]), key
+        ok = verts.property(key)[1]
+        assert np.array_equal(reorder(ids, vals, verts.ids)[ok], verts.property(key)[0][ok]), key
+    ids = o.vertex_ids()
+    result, verts, mem = run_both({"edges": (n, src, dst, None)}, lambda: GlobalNoCombiner(ids, True), o)
+    gids, (inbox, has) = result.vertex_properties["inbox"]
+    assert has.all() and np.array_equal(reorder(gids, inbox, verts.ids), verts.property("inbox")[0])
+    graph = GpuGraph(edges=(n, src, dst, None))
+    c = graph.compute()
+    c.program(GlobalNoCombiner(ids, False))
     with pytest.raises(ExecutionException):
-        computer.submit().get()
-    computer = GpuGraph(rows, sd).compute()
-    computer.resultMode(TitanGraphComputer.ResultMode.NONE)
-    computer.program(ConnectedComponents())
-    computer.submit().get()
+        c.submit().get()
 
 
 def test_generic_program_failure_surfaces_as_execution_exception():

@@ -459,6 +459,11 @@ def test_rmat_pagerank_cache_blocked(rmat12, iters, hot, seg, tile, monkeypatch)
     opr, _ = oracle.pagerank(0.85, n, iters)
     assert np.abs(pr - opr).sum() <= PR_L1_TOL
     assert np.array_equal(pr, eng.pagerank(0.85, n, iters))
+    # the persistent software-pipelined hot pass (gather_hot_pipe) sums the same tiles in the
+    # same order: bitwise equal
+    monkeypatch.setenv("TGO_PR_HOT_PIPE", "1")
+    assert np.array_equal(pr, Engine().load_edges(n, src, dst, IN).pagerank(0.85, n, iters))
+    monkeypatch.delenv("TGO_PR_HOT_PIPE")
     monkeypatch.setenv("TGO_PR_BLOCKED", "0")
     plain = Engine().load_edges(n, src, dst, IN).pagerank(0.85, n, iters)
     assert np.abs(pr - plain).sum() <= 1e-12
@@ -475,8 +480,9 @@ def hub_graph(n, hub, k_in, k_out, seed=11):
 KTILE = 4096     # CSR-adaptive tile (engine.hpp kTile): rows longer than this are split in chunks
 
 
-@pytest.mark.parametrize("blocked,tile", [("0", "4096"), ("1", "4096"), ("1", "8192"), ("1", "16384")])
-def test_pagerank_long_rows(monkeypatch, blocked, tile):
+@pytest.mark.parametrize("blocked,tile,pipe", [("0", "4096", "0"), ("1", "4096", "0"), ("1", "8192", "0"),
+                                               ("1", "16384", "0"), ("1", "4096", "1"), ("1", "16384", "1")])
+def test_pagerank_long_rows(monkeypatch, blocked, tile, pipe):
     """A hub whose in-list spans many tiles: 80 000 entries = ~20 chunks of kTile through
     gather_chunks + finalize_long; cache-blocked with 1024 hot sources and 4096-source cold
     segments, its cold run per segment (~10 000 entries) is cut into several kTile pieces;
@@ -484,6 +490,7 @@ def test_pagerank_long_rows(monkeypatch, blocked, tile):
     with the top bit set).  All within 1e-6 L1 of the oracle and bitwise reproducible."""
     monkeypatch.setenv("TGO_PR_BLOCKED", blocked)
     monkeypatch.setenv("TGO_PR_HOT_TILE", tile)
+    monkeypatch.setenv("TGO_PR_HOT_PIPE", pipe)
     monkeypatch.setenv("TGO_PR_HOT", "1024")
     monkeypatch.setenv("TGO_PR_SEG", "4096")
     n = 1 << 15

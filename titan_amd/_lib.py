@@ -30,7 +30,7 @@ DT_BYTE, DT_SHORT, DT_INTEGER, DT_LONG, DT_FLOAT, DT_DOUBLE, DT_BOOLEAN = 1, 2, 
 DT_OBJECT = 11      # generic key (DefaultSchemaMaker: dataType(Object.class)); result write-back only
 DT_DATE, DT_CHARACTER, DT_STRING = 8, 9, 10
 ORDER_ASC, ORDER_DESC = 0, 1
-RESULT_DISTANCE, RESULT_PAGERANK, RESULT_DEGREE = 0, 1, 2
+RESULT_DISTANCE, RESULT_PAGERANK, RESULT_DEGREE, RESULT_VALUES = 0, 1, 2, 3
 SSSP_HOP_BOUNDED, SSSP_DELTA = 0, 1
 FLAG_STATS = 1
 DIST_ABSENT = -(1 << 63)
@@ -38,6 +38,7 @@ ABI_VERSION = 2
 COMBINE_SUM, COMBINE_MIN, COMBINE_MAX = 0, 1, 2
 VAL_INT64, VAL_FP64 = 0, 1
 EDGE_IDENTITY, EDGE_ADD_ONE, EDGE_ADD_WEIGHT, EDGE_MUL_WEIGHT = 0, 1, 2, 3
+EDGE_SUB_WEIGHT, EDGE_MIN_WEIGHT, EDGE_MAX_WEIGHT, EDGE_DIV_WEIGHT = 4, 5, 6, 7
 
 _i64p = C.POINTER(C.c_int64)
 _i32p = C.POINTER(C.c_int32)
@@ -70,8 +71,12 @@ class Schema(C.Structure):
 
 
 class LoadOpts(C.Structure):
-    _fields_ = [("scope", C.c_int32), ("apply_cap", C.c_int32), ("n_labels", C.c_int32),
+    # flags sits in what was the padding after n_labels: same size and offsets as before
+    _fields_ = [("scope", C.c_int32), ("apply_cap", C.c_int32), ("n_labels", C.c_int32), ("flags", C.c_int32),
                 ("label_ids", _i64p), ("weight_key", C.c_int64)]
+
+
+LOAD_COLUMN_ORDER = 1       # tgo_load_opts.flags: keep column positions (tgo_gather_lists order)
 
 
 class EdgeEntry(C.Structure):
@@ -134,6 +139,7 @@ EXPORTS = [
     "tgo_sssp", "tgo_copy_distances", "tgo_pagerank", "tgo_walkcount", "tgo_stats_get", "tgo_sync",
     "tgo_bfs_multi", "tgo_copy_multi_distances", "tgo_multi_stats",
     "tgo_gather", "tgo_combine_global", "tgo_dense_ids", "tgo_decode_edge_entry", "tgo_result_rows",
+    "tgo_gather_lists", "tgo_result_rows_values",
     "tgo_rmat_edges", "tgo_pick_roots", "tgo_synth_rows",
     # titan_gpu_olap_part.h (1-D vertex-partitioned multi-GPU)
     "tgo_load_partition", "tgo_part_layout", "tgo_load_partition_layout", "tgo_part_bfs_begin", "tgo_part_bfs_td", "tgo_part_bfs_claim", "tgo_part_bfs_bu",
@@ -188,6 +194,8 @@ def load() -> C.CDLL:
         "tgo_copy_multi_distances": (C.c_int, [vp, C.c_int32, _i64p]),
         "tgo_multi_stats": (C.c_int, [vp, _i64p, _i64p]),
         "tgo_gather": (C.c_int, [vp, P(GatherArgs), vp, P(C.c_uint8), vp, P(C.c_uint8)]),
+        "tgo_gather_lists": (C.c_int, [vp, P(GatherArgs), vp, P(C.c_uint8), _i64p, vp]),
+        "tgo_result_rows_values": (C.c_int, [vp, P(ResultArgs), vp, P(C.c_uint8), P(ResultSize), P(RowsBuf)]),
         "tgo_combine_global": (C.c_int, [vp, C.c_int32, C.c_int32, C.c_int64, _i64p, vp, vp, P(C.c_uint8)]),
         "tgo_dense_ids": (C.c_int, [vp, _i64p, C.c_int64, _i64p]),
         "tgo_rmat_edges": (C.c_int, [C.c_int32, C.c_int32, C.c_uint64, C.c_int64, C.c_int64,

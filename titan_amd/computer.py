@@ -485,16 +485,18 @@ class GpuGraph:
     def read_property(self, vid, key_id, datatype):
         return None if self.rows is None else read_property(self.rows, vid, key_id, datatype, self.partition_bits)
 
-    def engine_for(self, scope: int, weight_key: int = 0) -> Engine:
-        key = (scope, weight_key)
+    def engine_for(self, scope: int, weight_key: int = 0, column_order: bool = False) -> Engine:
+        key = (scope, weight_key, column_order)
         with self._lock:
             if key not in self._engines:
                 eng = Engine(self.device, self.partition_bits, hard_query_limit=self.hard_query_limit)
                 if self.rows is not None:
-                    eng.load_rows(self.rows, self.schema, scope, apply_cap=self.apply_cap, weight_key=weight_key)
+                    eng.load_rows(self.rows, self.schema, scope, apply_cap=self.apply_cap, weight_key=weight_key,
+                                  column_order=column_order)
                 else:
                     n, src, dst, w = self.edges
-                    eng.load_edges(n, src, dst, scope, weight=w if weight_key else None, apply_cap=self.apply_cap)
+                    eng.load_edges(n, src, dst, scope, weight=w if weight_key else None, apply_cap=self.apply_cap,
+                                   column_order=column_order)
                 self._engines[key] = eng
             return self._engines[key]
 
@@ -648,10 +650,9 @@ class GpuGraphComputer(TitanGraphComputer):
             wk = self.weight_keys.get(p.weight_property, 0)
             if wk == 0:
                 raise TitanException(L.TGO_E_INVALID, f"weight property '{p.weight_property}' has no key id")
-        eng = self.graph.engine_for(scope, wk)
+        # a combiner-less program reads message streams: keep the column order for them
+        eng = self.graph.engine_for(scope, wk, column_order=p.combiner is None)
         memory = FulgoraMemory(tuple(p.memory_compute_keys) + tuple(mr.memory_key for mr in self._map_reduces))
-        if self._result_mode()[1] != TitanGraphComputer.ResultMode.NONE:
-            raise TitanException(L.TGO_E_UNSUPPORTED, "write-back of a generic program's compute keys")
         verts = run_generic(eng, p, memory)
         memory.setRuntime((time.perf_counter() - t0) * 1000.0)
         memory.complete()
@@ -659,4 +660,41 @@ class GpuGraphComputer(TitanGraphComputer):
         for mr in self._map_reduces:
             values[mr.memory_key] = mr.emit_generic(verts)
         vprops = {k: (verts.ids, v) for k, v in verts._props.items() if v is not None}
-        return ComputerResult(self.graph, Memory(memory.getIteration(), memory.getRuntime(), values), vprops)
+        result_graph = self._write_back_generic(eng, verts)
+        return ComputerResult(result_graph, Memory(memory.getIteration(), memory.getRuntime(), values), vprops)
+
+    def _write_back_generic(self, eng, verts):
+        """A generic program's element compute keys written back like Fulgora writes every
+        vertex's mutable properties (FulgoraGraphComputer.java:248-305): one SINGLE-cardinality
+        entry per vertex holding the key, encoded on the device (tgo_result_rows_values).
+        int64 values go to a Long / Integer key, fp64 values to a Double key; a key without a
+        schema becomes a generic key (getOrCreatePropertyKey)."""
+        explicit, mode = self._result_mode()
+        if mode == TitanGraphComputer.ResultMode.NONE or (self.graph.rows is None and not explicit):
+            return self.graph
+        merged = None
+        for name in self._program.compute_keys:
+            prop = verts.property(name)
+            if prop is None:
+                continue
+            vals, present = prop
+            vals = np.asarray(vals)
+            if vals.dtype.kind in "iu":
+                vt, ok = L.VAL_INT64, (L.DT_LONG, L.DT_INTEGER, L.DT_OBJECT)
+            elif vals.dtype.kind == "f":
+                vt, ok = L.VAL_FP64, (L.DT_DOUBLE, L.DT_OBJECT)
+            else:
+                raise TitanException(L.TGO_E_UNSUPPORTED, f"compute key {name}: values of dtype {vals.dtype}")
+            key, dt = self.graph.property_key(name)
+            if dt not in ok:
+                raise TitanException(L.TGO_E_INVALID, f"compute key {name}: its PropertyKey datatype {dt} does not "
+                                                      f"hold {vals.dtype} values")
+            base = self.graph.reserve_relation_ids(int(np.count_nonzero(present)))
+            rows = eng.result_rows_values(key, dt, vt, vals, present, base)
+            merged = rows if merged is None else merge_rows(merged, rows)
+        if merged is None:
+            return self.graph
+        if mode == TitanGraphComputer.ResultMode.PERSIST:
+            self.graph.persist(merged)
+            return self.graph
+        return LocalTxGraph(self.graph, merged)

@@ -52,6 +52,7 @@ struct tgo_ctx {
     int64_t part_relaxed = 0;   // partitioned SSSP: entries relaxed, phases
     int32_t part_phases = 0;
     int64_t pv_max_out = 0, pv_max_in = 0;   // largest OUT / IN list of a vertex cut
+    std::vector<int64_t> pv_rows;            // row ids of the vertex cuts
     // last finished program whose compute keys tgo_result_rows can encode (-1 = none)
     int res_kind = -1;
     bool host_decode = false;                // TGO_HOST_DECODE latched for the load in progress
@@ -189,6 +190,8 @@ int upload_cold_blocks(tgo_ctx* ctx, const std::vector<int64_t>& off, const std:
     const int64_t ht = env_i64("TGO_PR_HOT_TILE", 4096);
     cb.hot_tile = ht == 16384 ? 16384 : ht == 8192 ? 8192 : 4096;
     cb.hot_shift = cb.hot_tile == 16384 ? 14 : cb.hot_tile == 8192 ? 13 : kPackShift;
+    cb.hot_pipe = static_cast<int>(env_i64("TGO_PR_HOT_PIPE", 0));
+    cb.num_cus = ctx->num_cus;
     const bool pack = env_i64("TGO_PR_PACK", 1) != 0;
     if (!pack) cb.hot_tile = static_cast<int>(kTile), cb.hot_shift = kPackShift;
     HIP_TRY(upload_row_blocks(ctx, hoff_act, cb.rb_hot, pack ? &hc.hadj : nullptr, &cb.packed, cb.hot_tile,
@@ -236,6 +239,8 @@ int upload_graph(tgo_ctx* ctx, HostGraph& h, bool allow_segments = true) {
     g.n = h.n;
     g.scope = h.scope;
     g.has_weight = h.has_weight;
+    g.weight_dt = h.weight_dt;
+    g.has_col = !h.out.col.empty() || !h.in.col.empty();
     g.has_transpose = h.has_transpose;
     g.n_active = 0;
     for (int64_t v = h.n - 1; v >= 0; --v)
@@ -252,6 +257,7 @@ int upload_graph(tgo_ctx* ctx, HostGraph& h, bool allow_segments = true) {
         if ((e = upload(ctx, dst.off, src.off)) != hipSuccess) return e;
         if ((e = upload(ctx, dst.adj, src.adj)) != hipSuccess) return e;
         if (h.has_weight && (e = upload(ctx, dst.w, src.w)) != hipSuccess) return e;
+        if (!src.col.empty() && (e = upload(ctx, dst.col, src.col)) != hipSuccess) return e;
         dst.nnz = static_cast<int64_t>(src.adj.size());
         return hipSuccess;
     };
@@ -327,6 +333,9 @@ int upload_graph(tgo_ctx* ctx, HostGraph& h, bool allow_segments = true) {
     ctx->st.ghost_partition_rows = h.ghost_partition_rows;
     ctx->pv_max_out = h.pv_max_out;
     ctx->pv_max_in = h.pv_max_in;
+    ctx->pv_rows.clear();
+    for (size_t r = 0; r < h.pv_flags.size(); ++r)
+        if (h.pv_flags[r]) ctx->pv_rows.push_back(static_cast<int64_t>(r));
     ctx->st.device_bytes = ctx->dev_bytes;
     ctx->loaded = true;
     return TGO_OK;
@@ -843,6 +852,9 @@ int tgo_sssp(tgo_ctx* ctx, const tgo_sssp_args* a, int64_t* dist_out) {
     if (rc) return rc;
     if (a->max_depth < 0) return fail(ctx, TGO_E_INVALID, "max_depth < 0");
     if (a->mode != TGO_SSSP_HOP_BOUNDED && a->mode != TGO_SSSP_DELTA) return fail(ctx, TGO_E_INVALID, "invalid mode");
+    if (ctx->g.has_weight && ctx->g.weight_dt != TGO_DT_INTEGER)
+        return fail(ctx, TGO_E_UNSUPPORTED, "ShortestDistanceVertexProgram reads edge.<Integer>value(weight): the weight "
+                                            "property is not an Integer key (ClassCastException in the reference)");
     (void)hipSetDevice(ctx->opts.device);
     int64_t seed;
     if ((rc = resolve_seed(ctx, a->seed, a->seed_is_dense, seed))) return rc;
@@ -1137,19 +1149,15 @@ int tgo_walkcount(tgo_ctx* ctx, int32_t k, int32_t* out) {
     return TGO_OK;
 }
 
-int tgo_result_rows(tgo_ctx* ctx, const tgo_result_args* a, tgo_result_size* size, const tgo_rows_buf* out) {
-    if (!ctx) return TGO_E_INVALID;
-    if (!a || !size) return fail(ctx, TGO_E_INVALID, "null args");
-    if (a->kind < TGO_RESULT_DISTANCE || a->kind > TGO_RESULT_DEGREE) return fail(ctx, TGO_E_INVALID, "invalid result kind");
-    if (ctx->res_kind != a->kind)
-        return fail(ctx, TGO_E_STATE, "no finished program of that kind is the last one run on this ctx");
+static int result_rows_impl(tgo_ctx* ctx, const tgo_result_args* a, const ResultSource& src, bool empty,
+                            tgo_result_size* size, const tgo_rows_buf* out) {
     if (out && (!out->row_keys || !out->row_entry_begin || !out->row_byte_begin || !out->entry_bytes ||
                 !out->entry_limit_valpos))
         return fail(ctx, TGO_E_INVALID, "incomplete tgo_rows_buf");
     (void)hipSetDevice(ctx->opts.device);
     const int64_t n = ctx->g.n;
     const tgo_result_size want = *size;
-    if (ctx->res_empty) {
+    if (empty) {
         *size = tgo_result_size{0, 0, 0};
         if (out) out->row_entry_begin[0] = out->row_byte_begin[0] = 0;
         return TGO_OK;
@@ -1161,7 +1169,7 @@ int tgo_result_rows(tgo_ctx* ctx, const tgo_result_args* a, tgo_result_size* siz
     ResultRows rr;
     std::vector<int64_t> row_src;
     std::string err;
-    int rc = encode_results(ctx->res_src, a, ctx->g.perm, n, scratch, ctx->sc.cub_tmp, ctx->sc.cub_bytes, &rr,
+    int rc = encode_results(src, a, ctx->g.perm, n, scratch, ctx->sc.cub_tmp, ctx->sc.cub_bytes, &rr,
                             ctx->stream, err);
     if (!rc && out) {
         if (want.nrows < rr.nrows || want.nentries < rr.nentries || want.nbytes < rr.nbytes) {
@@ -1176,7 +1184,7 @@ int tgo_result_rows(tgo_ctx* ctx, const tgo_result_args* a, tgo_result_size* siz
         rr.row_byte_begin = out->row_byte_begin;
         rr.entry_bytes = out->entry_bytes;
         rr.entry_limit_valpos = out->entry_limit_valpos;
-        rc = encode_results(ctx->res_src, a, ctx->g.perm, n, scratch, ctx->sc.cub_tmp, ctx->sc.cub_bytes, &rr,
+        rc = encode_results(src, a, ctx->g.perm, n, scratch, ctx->sc.cub_tmp, ctx->sc.cub_bytes, &rr,
                             ctx->stream, err);
         // row keys: IDManager.getKey of each vertex id (IDManager.java:461-473)
         const int pb = ctx->opts.partition_bits;
@@ -1191,6 +1199,43 @@ int tgo_result_rows(tgo_ctx* ctx, const tgo_result_args* a, tgo_result_size* siz
     if (rc) return fail(ctx, rc, err);
     *size = tgo_result_size{rr.nrows, rr.nentries, rr.nbytes};
     return TGO_OK;
+}
+
+int tgo_result_rows(tgo_ctx* ctx, const tgo_result_args* a, tgo_result_size* size, const tgo_rows_buf* out) {
+    if (!ctx) return TGO_E_INVALID;
+    if (!a || !size) return fail(ctx, TGO_E_INVALID, "null args");
+    if (a->kind < TGO_RESULT_DISTANCE || a->kind > TGO_RESULT_DEGREE) return fail(ctx, TGO_E_INVALID, "invalid result kind");
+    if (ctx->res_kind != a->kind)
+        return fail(ctx, TGO_E_STATE, "no finished program of that kind is the last one run on this ctx");
+    return result_rows_impl(ctx, a, ctx->res_src, ctx->res_empty, size, out);
+}
+
+static int generic_alloc(tgo_ctx* ctx);
+
+int tgo_result_rows_values(tgo_ctx* ctx, const tgo_result_args* a, const void* values, const uint8_t* present,
+                           tgo_result_size* size, const tgo_rows_buf* out) {
+    if (!ctx) return TGO_E_INVALID;
+    if (!a || !size || !values || !present) return fail(ctx, TGO_E_INVALID, "null args");
+    if (!ctx->loaded) return fail(ctx, TGO_E_STATE, "no graph loaded");
+    if (a->kind != TGO_RESULT_VALUES) return fail(ctx, TGO_E_INVALID, "tgo_result_rows_values takes kind TGO_RESULT_VALUES");
+    if (ctx->g.partitioned) return fail(ctx, TGO_E_UNSUPPORTED, "generic programs run on a one-GPU load");
+    const int64_t n = ctx->g.n;
+    if (a->reserved == TGO_VAL_INT64 && a->datatypes[0] == TGO_DT_INTEGER) {
+        const int64_t* v = static_cast<const int64_t*>(values);
+        for (int64_t i = 0; i < n; ++i)
+            if (present[i] && (v[i] < INT32_MIN || v[i] > INT32_MAX))
+                return fail(ctx, TGO_E_INVALID, "a value of an Integer compute key is out of int range");
+    }
+    (void)hipSetDevice(ctx->opts.device);
+    int rc = generic_alloc(ctx);
+    if (rc) return rc;
+    Scratch& s = ctx->sc;
+    hipStream_t st = ctx->stream;
+    HIP_TRY(hipMemcpyAsync(s.gv[0], values, n * 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(s.gh[0], present, n, hipMemcpyHostToDevice, st));
+    HIP_TRY(k_to_internal(s.gv[0], s.gh[0], ctx->g.perm, s.gv[1], s.gh[1], n, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return result_rows_impl(ctx, a, ResultSource{s.gv[1], s.gh[1]}, false, size, out);
 }
 
 // ------------------------------------------------------------------ 1-D partitioned (multi-GPU)
@@ -2027,23 +2072,40 @@ static int generic_alloc(tgo_ctx* ctx) {
     return TGO_OK;
 }
 
-int tgo_gather(tgo_ctx* ctx, const tgo_gather_args* a, const void* msg, const uint8_t* has, void* out,
-               uint8_t* out_has) {
-    if (!ctx) return TGO_E_INVALID;
-    ctx->res_kind = -1;
-    if (!a || !msg || !out || !out_has) return fail(ctx, TGO_E_INVALID, "null argument");
+static bool weight_edge_fn(int fn) { return fn >= TGO_EDGE_ADD_WEIGHT && fn <= TGO_EDGE_DIV_WEIGHT; }
+
+// Scope, value type, combiner (when used) and edge function of a Local receive.
+static int check_gather_args(tgo_ctx* ctx, const tgo_gather_args* a, bool combiner) {
     if (!ctx->loaded) return fail(ctx, TGO_E_STATE, "no graph loaded");
     if (ctx->g.partitioned) return fail(ctx, TGO_E_UNSUPPORTED, "generic gathers run on a one-GPU load");
     if (a->scope < 0 || a->scope > 2) return fail(ctx, TGO_E_INVALID, "invalid scope");
     if (a->scope != ctx->g.scope && ctx->g.scope != TGO_SCOPE_BOTH_E)
         return fail(ctx, TGO_E_INVALID, "message scope differs from the scope the graph was loaded (preloaded) for");
-    if (a->value_type < 0 || a->value_type > 1 || a->combiner < 0 || a->combiner > 2 || a->edge_fn < 0 || a->edge_fn > 3)
+    if (a->value_type < 0 || a->value_type > 1 || (combiner && (a->combiner < 0 || a->combiner > 2)) ||
+        a->edge_fn < TGO_EDGE_IDENTITY || a->edge_fn > TGO_EDGE_DIV_WEIGHT)
         return fail(ctx, TGO_E_INVALID, "invalid value type, combiner or edge function");
-    if ((a->edge_fn == TGO_EDGE_ADD_WEIGHT || a->edge_fn == TGO_EDGE_MUL_WEIGHT) && !ctx->g.has_weight)
+    if (weight_edge_fn(a->edge_fn) && !ctx->g.has_weight)
         return fail(ctx, TGO_E_INVALID, "weight edge function on a graph loaded without a weight property");
+    if (weight_edge_fn(a->edge_fn) && ctx->g.weight_dt == TGO_DT_FLOAT && a->value_type == TGO_VAL_INT64)
+        return fail(ctx, TGO_E_INVALID, "a Float weight needs fp64 messages (long op float is a float in Java)");
+    return TGO_OK;
+}
+
+static int gather_error(tgo_ctx* ctx, unsigned long long err) {
+    if (err & 2) return fail(ctx, TGO_E_PROGRAM, "vertex program failed: integer division by zero in an edge function");
+    if (err) return fail(ctx, TGO_E_PROGRAM, "vertex program failed: a traversed edge has no value for the weight property");
+    return TGO_OK;
+}
+
+int tgo_gather(tgo_ctx* ctx, const tgo_gather_args* a, const void* msg, const uint8_t* has, void* out,
+               uint8_t* out_has) {
+    if (!ctx) return TGO_E_INVALID;
+    ctx->res_kind = -1;
+    if (!a || !msg || !out || !out_has) return fail(ctx, TGO_E_INVALID, "null argument");
+    int rc;
+    if ((rc = check_gather_args(ctx, a, true))) return rc;
     (void)hipSetDevice(ctx->opts.device);
-    int rc = generic_alloc(ctx);
-    if (rc) return rc;
+    if ((rc = generic_alloc(ctx))) return rc;
     Scratch& s = ctx->sc;
     hipStream_t st = ctx->stream;
     const int64_t n = ctx->g.n;
@@ -2054,7 +2116,7 @@ int tgo_gather(tgo_ctx* ctx, const tgo_gather_args* a, const void* msg, const ui
     HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
     HIP_TRY(k_to_internal(s.gv[0], s.gh[0], ctx->g.perm, s.gv[1], s.gh[1], n, st));
     HIP_TRY(k_local_gather(pull_view(ctx->g, a->scope), n, a->value_type, s.gv[1], s.gh[1], a->combiner, a->edge_fn,
-                           s.gv[2], s.gh[2], &s.cnt->err, st));
+                           ctx->g.weight_dt == TGO_DT_FLOAT, s.gv[2], s.gh[2], &s.cnt->err, st));
     HIP_TRY(k_to_rows(s.gv[2], s.gh[2], ctx->g.perm, s.gv[0], s.gh[0], n, st));
     HIP_TRY(hipEventRecord(ctx->ev1, st));
     HIP_TRY(hipMemcpyAsync(out, s.gv[0], n * 8, hipMemcpyDeviceToHost, st));
@@ -2063,8 +2125,66 @@ int tgo_gather(tgo_ctx* ctx, const tgo_gather_args* a, const void* msg, const ui
     float ms = 0;
     HIP_TRY(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
     ctx->st.last_kernel_ms = ms;
-    if (s.hcnt->err) return fail(ctx, TGO_E_PROGRAM, "vertex program failed: a traversed edge has no value for the weight property");
-    return TGO_OK;
+    return gather_error(ctx, s.hcnt->err);
+}
+
+int tgo_gather_lists(tgo_ctx* ctx, const tgo_gather_args* a, const void* msg, const uint8_t* has, int64_t* row_offsets,
+                     void* values) {
+    if (!ctx) return TGO_E_INVALID;
+    ctx->res_kind = -1;
+    if (!a || !msg || !row_offsets) return fail(ctx, TGO_E_INVALID, "null argument");
+    int rc;
+    if ((rc = check_gather_args(ctx, a, false))) return rc;
+    (void)hipSetDevice(ctx->opts.device);
+    if ((rc = generic_alloc(ctx))) return rc;
+    Scratch& s = ctx->sc;
+    hipStream_t st = ctx->stream;
+    const DevGraph& g = ctx->g;
+    const int64_t n = g.n;
+    const View pull = pull_view(g, a->scope);
+    const bool wfloat = g.weight_dt == TGO_DT_FLOAT;
+    HIP_TRY(hipMemcpyAsync(s.gv[0], msg, n * 8, hipMemcpyHostToDevice, st));
+    if (has) HIP_TRY(hipMemcpyAsync(s.gh[0], has, n, hipMemcpyHostToDevice, st));
+    else HIP_TRY(hipMemsetAsync(s.gh[0], 1, n, st));
+    HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
+    HIP_TRY(k_to_internal(s.gv[0], s.gh[0], g.perm, s.gv[1], s.gh[1], n, st));
+    // offsets: counts per row (s.gv[2] as int64 n+1), scanned into s.gv[0]
+    int64_t* cnt = reinterpret_cast<int64_t*>(s.gv[2]);
+    int64_t* off = reinterpret_cast<int64_t*>(s.gv[0]);
+    HIP_TRY(k_list_count(pull, g.perm, n, s.gh[1], a->edge_fn, cnt, &s.cnt->err, st));
+    HIP_TRY(scan_exclusive_i64(s.cub_tmp, s.cub_bytes, cnt, off, n + 1, st));
+    HIP_TRY(hipMemcpyAsync(row_offsets, off, (n + 1) * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    if ((rc = read_counters(ctx))) return rc;
+    if ((rc = gather_error(ctx, s.hcnt->err))) return rc;
+    // a vertex cut that receives two messages meets FulgoraUtil's ThrowingCombiner (:80-91)
+    for (int64_t r : ctx->pv_rows)
+        if (row_offsets[r + 1] - row_offsets[r] >= 2)
+            return fail(ctx, TGO_E_PROGRAM, "The VertexProgram needs to define a message combiner in order to preserve "
+                                            "memory and handle partitioned vertices");
+    const int64_t total = row_offsets[n];
+    if (!values || total == 0) return TGO_OK;
+    if (total >= (int64_t(1) << 31)) return fail(ctx, TGO_E_UNSUPPORTED, "more than 2^31 messages in one receive");
+    // keys in/out (4 B each) + values in/out (8 B each) + the internal -> row map
+    char* buf = nullptr;
+    const size_t bytes = static_cast<size_t>(total) * 24 + static_cast<size_t>(n) * 4 + 64;
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&buf), bytes));
+    uint64_t* val_in = reinterpret_cast<uint64_t*>(buf);
+    uint64_t* val_out = val_in + total;
+    uint32_t* key_in = reinterpret_cast<uint32_t*>(val_out + total);
+    uint32_t* key_out = key_in + total;
+    int32_t* inv = reinterpret_cast<int32_t*>(key_out + total);
+    // column positions of the pull lists (pull_view: inE walks OUT entries, outE IN, bothE both)
+    const uint32_t* col0 = !g.has_col ? nullptr : a->scope == TGO_SCOPE_OUT_E ? g.in.col : g.out.col;
+    const uint32_t* col1 = !g.has_col || a->scope != TGO_SCOPE_BOTH_E ? nullptr : g.in.col;
+    hipError_t e = k_list_fill_sort(pull, col0, col1, g.perm, inv, n,
+                                    a->value_type, s.gv[1], s.gh[1], a->edge_fn, wfloat, off, total, key_in, key_out,
+                                    val_in, val_out, s.sort_tmp, s.sort_bytes, &s.cnt->err, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(values, val_out, total * 8, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    (void)hipFree(buf);
+    HIP_TRY(e);
+    if ((rc = read_counters(ctx))) return rc;
+    return gather_error(ctx, s.hcnt->err);
 }
 
 int tgo_combine_global(tgo_ctx* ctx, int32_t value_type, int32_t combiner, int64_t nmsgs, const int64_t* targets,

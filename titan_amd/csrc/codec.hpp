@@ -146,7 +146,8 @@ TGO_HD inline bool unique_in(int mult, int dir) {  // Multiplicity.isUnique
 // Reads (or skips) one inline value through StandardSerializer (readObjectInternal :220-233):
 // a null flag byte unless the serializer handles null itself (StringSerializer), then the
 // attribute serializer's read, or readByteOrder for a sort key (byte_order).  Integral values
-// (Byte..Long, Boolean, Date, Character) are returned in v; Float/Double/String are skipped.
+// (Byte..Long, Boolean, Date, Character) are returned in v, a Float as its IEEE bits (int32);
+// Double/String are skipped.
 // Returns false on a codec error; present=false for a serialized null.
 TGO_HD inline bool read_value(Cursor& c, int dt, bool byte_order, bool& present, int64_t& v) {
     v = 0;
@@ -203,7 +204,19 @@ TGO_HD inline bool read_value(Cursor& c, int dt, bool byte_order, bool& present,
             break;
         case TGO_DT_LONG:
         case TGO_DT_DATE: v = static_cast<int64_t>(c.be(8) + 0x8000000000000000ULL); break;
-        case TGO_DT_FLOAT: c.skip(4); break;
+        case TGO_DT_FLOAT: {                       // FloatSerializer :33-46: the IEEE bits, or
+            uint32_t u = static_cast<uint32_t>(c.be(4));    // NumericUtils.floatToSortableInt ^ sign
+            if (byte_order) {
+                u ^= 0x80000000u;
+                int32_t si = static_cast<int32_t>(u);
+                si ^= (si >> 31) & 0x7fffffff;
+                u = static_cast<uint32_t>(si);
+            }
+            if (u == 0x80000000u) u = 0;           // -0.0f reads as +0.0f (the bits of -0.0f are the
+                                                   // missing-weight sentinel INT32_MIN)
+            v = static_cast<int32_t>(u);
+            break;
+        }
         case TGO_DT_DOUBLE: c.skip(8); break;
         case TGO_DT_BOOLEAN: v = c.get(); break;
         default: return false;

@@ -26,6 +26,8 @@ struct HostCsr {
     std::vector<int64_t> off;   // n+1
     std::vector<int32_t> adj;
     std::vector<int32_t> w;     // empty when unweighted
+    std::vector<uint32_t> col;  // TGO_LOAD_COLUMN_ORDER: each entry's position in its Titan row
+                                // (column order across both directions); empty otherwise
 };
 
 struct HostGraph {
@@ -36,6 +38,7 @@ struct HostGraph {
     HostCsr push_t;             // explicit transpose of the pull view (cap / asymmetric rows)
     bool has_transpose = false;
     bool has_weight = false;
+    int32_t weight_dt = TGO_DT_INTEGER;   // datatype of the weight property (int32 bits; Float: IEEE bits)
     int32_t scope = TGO_SCOPE_BOTH_E;
     int64_t ghost = 0, truncated = 0, skipped = 0;
     int64_t partitioned = 0, partition_rows = 0, ghost_partition_rows = 0;
@@ -53,6 +56,7 @@ struct HostPlan {
     std::vector<int8_t> dts;
     int32_t n_labels = 0;
     int64_t weight_key = 0;
+    int32_t weight_dt = 0;               // datatype of weight_key (0: no weight)
 };
 // Staging of decoded rows between tgo_load_rows batches (decoded on arrival).
 struct RowStaging {
@@ -169,6 +173,7 @@ struct DevCsr {
     int64_t* off = nullptr;
     int32_t* adj = nullptr;
     int32_t* w = nullptr;
+    uint32_t* col = nullptr;    // column position of every entry (TGO_LOAD_COLUMN_ORDER loads)
     int64_t nnz = 0;
 };
 
@@ -237,6 +242,9 @@ struct ColdBlocks {
     bool packed = false;        // hot CSR tiles source-sorted and packed (pack_tiles)
     int hot_tile = 4096;        // entries per hot tile (TGO_PR_HOT_TILE: 4096, 8192 or 16384)
     int hot_shift = 12;         // packed hot entry = source << hot_shift | slot (log2 hot_tile)
+    int hot_pipe = 0;           // hot pass as persistent workgroups that gather tile t+1 while
+                                // reducing tile t (TGO_PR_HOT_PIPE; gather_hot_pipe)
+    int num_cus = 256;          // persistent grid: workgroups per CU x CUs
 };
 struct HostColdBlocks {
     int64_t hot = 0, seg = 0;
@@ -260,6 +268,8 @@ struct DevGraph {
     DevCsr out, in, push_t;
     bool has_transpose = false;
     bool has_weight = false;
+    int32_t weight_dt = TGO_DT_INTEGER;
+    bool has_col = false;       // out.col / in.col hold column positions
     int32_t min_weight = 0;
     double mean_weight = 1.0;   // over present weights (delta-stepping's default bucket width)
     int32_t scope = TGO_SCOPE_BOTH_E;
@@ -469,7 +479,15 @@ hipError_t k_walk_iter(const DevCsr& out, const RowBlocks& rb, const int32_t* pr
 
 // Generic vertex programs (generic.hip)
 hipError_t k_local_gather(const View& pull, int64_t n, int value_type, const void* msg_int, const uint8_t* has_int,
-                          int comb, int fn, void* out_int, uint8_t* out_has_int, unsigned long long* err, hipStream_t s);
+                          int comb, int fn, bool wfloat, void* out_int, uint8_t* out_has_int, unsigned long long* err,
+                          hipStream_t s);
+hipError_t k_list_count(const View& pull, const int32_t* perm, int64_t n, const uint8_t* has_int, int fn,
+                        int64_t* cnt, unsigned long long* err, hipStream_t s);
+hipError_t k_list_fill_sort(const View& pull, const uint32_t* col0, const uint32_t* col1, const int32_t* perm,
+                            int32_t* inv, int64_t n, int value_type, const void* msg_int, const uint8_t* has_int,
+                            int fn, bool wfloat, const int64_t* off_out, int64_t total, uint32_t* key_in,
+                            uint32_t* key_out, void* val_in, void* val_out, void*& tmp, size_t& tmp_bytes,
+                            unsigned long long* err, hipStream_t s);
 hipError_t k_to_internal(const void* row8, const uint8_t* row1, const int32_t* perm, void* int8, uint8_t* int1,
                          int64_t n, hipStream_t s);
 hipError_t k_to_rows(const void* int8, const uint8_t* int1, const int32_t* perm, void* row8, uint8_t* row1, int64_t n,

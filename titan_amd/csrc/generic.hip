@@ -42,28 +42,58 @@ __device__ __forceinline__ int64_t combine<int64_t>(int comb, int64_t acc, int64
     return static_cast<int64_t>(static_cast<uint64_t>(acc) + static_cast<uint64_t>(m));
 }
 
-// edgeFct(m, e): identity, m + 1, m + e.value(weight), m * e.value(weight)
-template <typename T>
-__device__ __forceinline__ T edge_apply(int fn, T m, int32_t w) {
-    if (fn == TGO_EDGE_ADD_ONE) return m + T(1);
-    if (fn == TGO_EDGE_ADD_WEIGHT) return m + static_cast<T>(w);
-    if (fn == TGO_EDGE_MUL_WEIGHT) return m * static_cast<T>(w);
-    return m;
+// edgeFct(m, e) = "m op w", w = e.value(weight): the weight column holds 32-bit integers, or
+// a Float's IEEE bits (wfloat).  Error bits: 1 = an edge without the weight property
+// (e.value() throws), 2 = int64 division by zero (Java ArithmeticException).
+constexpr unsigned long long kErrNoWeight = 1, kErrDivZero = 2;
+__host__ __device__ __forceinline__ bool weight_fn(int fn) { return fn >= TGO_EDGE_ADD_WEIGHT && fn <= TGO_EDGE_DIV_WEIGHT; }
+
+__device__ __forceinline__ double edge_apply_f(int fn, double m, int32_t w, bool wfloat) {
+    if (fn == TGO_EDGE_IDENTITY) return m;
+    if (fn == TGO_EDGE_ADD_ONE) return m + 1.0;
+    const double x = wfloat ? static_cast<double>(__int_as_float(w)) : static_cast<double>(w);
+    switch (fn) {
+        case TGO_EDGE_ADD_WEIGHT: return m + x;
+        case TGO_EDGE_MUL_WEIGHT: return m * x;
+        case TGO_EDGE_SUB_WEIGHT: return m - x;
+        case TGO_EDGE_MIN_WEIGHT: return x < m ? x : m;
+        case TGO_EDGE_MAX_WEIGHT: return x > m ? x : m;
+        default: return m / x;                               // IEEE: x = 0 gives +-inf / NaN as in Java
+    }
 }
-template <>
-__device__ __forceinline__ int64_t edge_apply<int64_t>(int fn, int64_t m, int32_t w) {
+// Java long arithmetic: + - * wrap, / truncates toward zero, MIN_VALUE / -1 = MIN_VALUE
+__device__ __forceinline__ int64_t edge_apply_i(int fn, int64_t m, int32_t w, unsigned long long* err) {
     const uint64_t u = static_cast<uint64_t>(m);
+    if (fn == TGO_EDGE_IDENTITY) return m;
     if (fn == TGO_EDGE_ADD_ONE) return static_cast<int64_t>(u + 1u);
-    if (fn == TGO_EDGE_ADD_WEIGHT) return static_cast<int64_t>(u + static_cast<uint64_t>(static_cast<int64_t>(w)));
-    if (fn == TGO_EDGE_MUL_WEIGHT) return static_cast<int64_t>(u * static_cast<uint64_t>(static_cast<int64_t>(w)));
-    return m;
+    const int64_t x = static_cast<int64_t>(w);
+    switch (fn) {
+        case TGO_EDGE_ADD_WEIGHT: return static_cast<int64_t>(u + static_cast<uint64_t>(x));
+        case TGO_EDGE_MUL_WEIGHT: return static_cast<int64_t>(u * static_cast<uint64_t>(x));
+        case TGO_EDGE_SUB_WEIGHT: return static_cast<int64_t>(u - static_cast<uint64_t>(x));
+        case TGO_EDGE_MIN_WEIGHT: return x < m ? x : m;
+        case TGO_EDGE_MAX_WEIGHT: return x > m ? x : m;
+        default:
+            if (x == 0) { atomicOr(err, kErrDivZero); return 0; }
+            if (x == -1) return static_cast<int64_t>(0ULL - u);
+            return m / x;
+    }
+}
+template <typename T> __device__ __forceinline__ T edge_apply(int fn, T m, int32_t w, bool wfloat, unsigned long long* err);
+template <> __device__ __forceinline__ double edge_apply<double>(int fn, double m, int32_t w, bool wfloat,
+                                                               unsigned long long*) {
+    return edge_apply_f(fn, m, w, wfloat);
+}
+template <> __device__ __forceinline__ int64_t edge_apply<int64_t>(int fn, int64_t m, int32_t w, bool,
+                                                                 unsigned long long* err) {
+    return edge_apply_i(fn, m, w, err);
 }
 
 template <typename T>
 __global__ void local_gather(View pull, int64_t n, const T* __restrict__ msg, const uint8_t* __restrict__ has,
-                             int comb, int fn, T* __restrict__ out, uint8_t* __restrict__ out_has,
+                             int comb, int fn, bool wfloat, T* __restrict__ out, uint8_t* __restrict__ out_has,
                              unsigned long long* err) {
-    const bool needs_w = fn == TGO_EDGE_ADD_WEIGHT || fn == TGO_EDGE_MUL_WEIGHT;
+    const bool needs_w = weight_fn(fn);
     for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x) {
         T acc = T(0);
         bool any = false;
@@ -77,9 +107,9 @@ __global__ void local_gather(View pull, int64_t n, const T* __restrict__ msg, co
                 int32_t wt = 0;
                 if (needs_w) {
                     wt = w ? w[k] : kMissingWeight;
-                    if (wt == kMissingWeight) { atomicOr(err, 1ull); continue; }   // e.value(key) throws
+                    if (wt == kMissingWeight) { atomicOr(err, kErrNoWeight); continue; }   // e.value(key) throws
                 }
-                const T m = edge_apply<T>(fn, msg[u], wt);
+                const T m = edge_apply<T>(fn, msg[u], wt, wfloat, err);
                 acc = any ? combine<T>(comb, acc, m) : m;
                 any = true;
             }
@@ -87,6 +117,65 @@ __global__ void local_gather(View pull, int64_t n, const T* __restrict__ msg, co
         out[v] = acc;
         out_has[v] = any ? 1 : 0;
     }
+}
+
+// ---- combiner-less receive (tgo_gather_lists): every row's message stream, materialised.
+// Pass 1 counts a row's messages (entries whose sender holds one); after the scan, pass 2
+// writes (order key, edgeFct(msg[u], e)) at the row's offsets; a segmented radix sort by key
+// then puts each row's messages in column order (key = the entry's column position, kept by
+// TGO_LOAD_COLUMN_ORDER loads) or (direction, neighbour row) order (key = list << 31 | row).
+__global__ void list_count(View pull, const int32_t* __restrict__ perm, int64_t n, const uint8_t* __restrict__ has,
+                           bool needs_w, int64_t* __restrict__ cnt, unsigned long long* err) {
+    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t v = perm[r];
+        int64_t c = 0;
+        for (int l = 0; l < pull.nlists; ++l) {
+            const int64_t* off = l == 0 ? pull.off0 : pull.off1;
+            const int32_t* adj = l == 0 ? pull.adj0 : pull.adj1;
+            const int32_t* w = l == 0 ? pull.w0 : pull.w1;
+            for (int64_t k = off[v]; k < off[v + 1]; ++k) {
+                if (!has[adj[k]]) continue;
+                if (needs_w && (!w || w[k] == kMissingWeight)) { atomicOr(err, kErrNoWeight); continue; }
+                ++c;
+            }
+        }
+        cnt[r] = c;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) cnt[n] = 0;
+}
+template <typename T>
+__global__ void list_fill(View pull, const uint32_t* __restrict__ col0, const uint32_t* __restrict__ col1,
+                          const int32_t* __restrict__ perm, const int32_t* __restrict__ inv, int64_t n,
+                          const T* __restrict__ msg, const uint8_t* __restrict__ has, int fn, bool wfloat,
+                          const int64_t* __restrict__ off_out, uint32_t* __restrict__ key, T* __restrict__ val,
+                          unsigned long long* err) {
+    const bool needs_w = weight_fn(fn);
+    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t v = perm[r];
+        int64_t p = off_out[r];
+        for (int l = 0; l < pull.nlists; ++l) {
+            const int64_t* off = l == 0 ? pull.off0 : pull.off1;
+            const int32_t* adj = l == 0 ? pull.adj0 : pull.adj1;
+            const int32_t* w = l == 0 ? pull.w0 : pull.w1;
+            const uint32_t* col = l == 0 ? col0 : col1;
+            for (int64_t k = off[v]; k < off[v + 1]; ++k) {
+                const int32_t u = adj[k];
+                if (!has[u]) continue;
+                int32_t wt = 0;
+                if (needs_w) {
+                    wt = w ? w[k] : kMissingWeight;
+                    if (wt == kMissingWeight) continue;
+                }
+                key[p] = col ? col[k] : ((static_cast<uint32_t>(l) << 31) | static_cast<uint32_t>(inv[u]));
+                val[p] = edge_apply<T>(fn, msg[u], wt, wfloat, err);
+                ++p;
+            }
+        }
+    }
+}
+__global__ void invert_perm(const int32_t* __restrict__ perm, int32_t* __restrict__ inv, int64_t n) {
+    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x)
+        inv[perm[r]] = static_cast<int32_t>(r);
 }
 
 // internal[perm[r]] = row[r]
@@ -125,14 +214,56 @@ __global__ void iota_i64(int64_t* p, int64_t n) {
 }  // namespace
 
 hipError_t k_local_gather(const View& pull, int64_t n, int value_type, const void* msg_int, const uint8_t* has_int,
-                          int comb, int fn, void* out_int, uint8_t* out_has_int, unsigned long long* err, hipStream_t s) {
+                          int comb, int fn, bool wfloat, void* out_int, uint8_t* out_has_int, unsigned long long* err,
+                          hipStream_t s) {
     if (value_type == TGO_VAL_INT64)
         local_gather<int64_t><<<grid_for(n), kBlock, 0, s>>>(pull, n, static_cast<const int64_t*>(msg_int), has_int, comb,
-                                                            fn, static_cast<int64_t*>(out_int), out_has_int, err);
+                                                            fn, wfloat, static_cast<int64_t*>(out_int), out_has_int, err);
     else
         local_gather<double><<<grid_for(n), kBlock, 0, s>>>(pull, n, static_cast<const double*>(msg_int), has_int, comb,
-                                                           fn, static_cast<double*>(out_int), out_has_int, err);
+                                                           fn, wfloat, static_cast<double*>(out_int), out_has_int, err);
     return hipGetLastError();
+}
+
+// Combiner-less receive: counts per row (row order) into cnt[0..n], cnt[n] = 0.
+hipError_t k_list_count(const View& pull, const int32_t* perm, int64_t n, const uint8_t* has_int, int fn,
+                        int64_t* cnt, unsigned long long* err, hipStream_t s) {
+    list_count<<<grid_for(n), kBlock, 0, s>>>(pull, perm, n, has_int, weight_fn(fn), cnt, err);
+    return hipGetLastError();
+}
+// ... then the (key, value) pairs of every row at off_out[r], and a segmented sort of each
+// row by key into key_out / val_out.  inv: n int32 scratch (internal -> row).
+hipError_t k_list_fill_sort(const View& pull, const uint32_t* col0, const uint32_t* col1, const int32_t* perm,
+                            int32_t* inv, int64_t n, int value_type, const void* msg_int, const uint8_t* has_int,
+                            int fn, bool wfloat, const int64_t* off_out, int64_t total, uint32_t* key_in,
+                            uint32_t* key_out, void* val_in, void* val_out, void*& tmp, size_t& tmp_bytes,
+                            unsigned long long* err, hipStream_t s) {
+    if (!col0) invert_perm<<<grid_for(n), kBlock, 0, s>>>(perm, inv, n);
+    if (value_type == TGO_VAL_INT64)
+        list_fill<int64_t><<<grid_for(n), kBlock, 0, s>>>(pull, col0, col1, perm, inv, n,
+                                                         static_cast<const int64_t*>(msg_int), has_int, fn, wfloat, off_out,
+                                                         key_in, static_cast<int64_t*>(val_in), err);
+    else
+        list_fill<double><<<grid_for(n), kBlock, 0, s>>>(pull, col0, col1, perm, inv, n,
+                                                        static_cast<const double*>(msg_int), has_int, fn, wfloat, off_out,
+                                                        key_in, static_cast<double*>(val_in), err);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || total == 0) return e;
+    const uint64_t* vi = static_cast<const uint64_t*>(val_in);
+    uint64_t* vo = static_cast<uint64_t*>(val_out);
+    size_t need = 0;
+    e = hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, need, key_in, key_out, vi, vo, static_cast<int>(total),
+                                                    static_cast<int>(n), off_out, off_out + 1, 0, 32, s);
+    if (e != hipSuccess) return e;
+    if (need > tmp_bytes) {
+        if (tmp) (void)hipFree(tmp);
+        tmp = nullptr;
+        tmp_bytes = 0;
+        if ((e = hipMalloc(&tmp, need)) != hipSuccess) return e;
+        tmp_bytes = need;
+    }
+    return hipcub::DeviceSegmentedRadixSort::SortPairs(tmp, tmp_bytes, key_in, key_out, vi, vo, static_cast<int>(total),
+                                                       static_cast<int>(n), off_out, off_out + 1, 0, 32, s);
 }
 
 hipError_t k_to_internal(const void* row8, const uint8_t* row1, const int32_t* perm, void* int8, uint8_t* int1,

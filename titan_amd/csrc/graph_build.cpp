@@ -64,9 +64,19 @@ int build_plan(const tgo_schema* schema, const tgo_load_opts* opts, HostPlan& hp
         auto it = std::lower_bound(hp.key_ids.begin(), hp.key_ids.end(), key);
         return it != hp.key_ids.end() && *it == key ? hp.key_dts[it - hp.key_ids.begin()] : 0;
     };
-    if (opts->weight_key != 0 && dt_of(opts->weight_key) != TGO_DT_INTEGER) {
-        err = "weight property must be an Integer key (edge.<Integer>value in ShortestDistanceVertexProgram)";
-        return TGO_E_UNSUPPORTED;
+    // The weight is read into 32 bits: the integral datatypes that fit (Byte, Short, Integer,
+    // Character, Boolean) as integers, Float as its IEEE bits.  Long / Double / Date / String
+    // weights are not supported.  ShortestDistanceVertexProgram itself casts to Integer
+    // (edge.<Integer>value, :53): its entry points reject any other weight datatype, as the
+    // reference fails with a ClassCastException; generic programs' edge functions take them all.
+    if (opts->weight_key != 0) {
+        const int dt = dt_of(opts->weight_key);
+        if (dt != TGO_DT_INTEGER && dt != TGO_DT_BYTE && dt != TGO_DT_SHORT && dt != TGO_DT_CHARACTER &&
+            dt != TGO_DT_BOOLEAN && dt != TGO_DT_FLOAT) {
+            err = "weight property must be a Byte, Short, Integer, Character, Boolean or Float key";
+            return TGO_E_UNSUPPORTED;
+        }
+        hp.weight_dt = dt;
     }
     std::vector<LabelPlan> labels;
     for (int t = 0; t < schema->n_edge_types; ++t) {
@@ -382,8 +392,10 @@ static void permute_graph(HostGraph& g, Nbr nbr, int threads) {
         r.off.assign(n + 1, 0);
         for (int64_t u = 0; u < n; ++u) r.off[u + 1] = r.off[u] + (c.off[inv[u] + 1] - c.off[inv[u]]);
         r.adj.resize(c.adj.size());
-        const bool w = !c.w.empty();
-        if (w) r.w.resize(c.w.size());
+        const bool hw = !c.w.empty(), hc = !c.col.empty();
+        const bool w = hw || hc;                    // payloads follow their entries (stable)
+        if (hw) r.w.resize(c.w.size());
+        if (hc) r.col.resize(c.col.size());
         // neighbour ids first, in one streaming parallel pass
         parallel_for(static_cast<int64_t>(c.adj.size()), threads, [&](int64_t lo, int64_t hi, int) {
             for (int64_t k = lo; k < hi; ++k) c.adj[k] = static_cast<int32_t>(nbr(c.adj[k]));
@@ -414,7 +426,9 @@ static void permute_graph(HostGraph& g, Nbr nbr, int threads) {
                 std::sort(key.begin(), key.end());
                 for (int64_t j = 0; j < len; ++j) {
                     dst[j] = static_cast<int32_t>(key[j] >> 32);
-                    r.w[r.off[u] + j] = c.w[b + static_cast<int64_t>(key[j] & 0xFFFFFFFFULL)];
+                    const int64_t src = b + static_cast<int64_t>(key[j] & 0xFFFFFFFFULL);
+                    if (hw) r.w[r.off[u] + j] = c.w[src];
+                    if (hc) r.col[r.off[u] + j] = c.col[src];
                 }
             }
         });
@@ -566,6 +580,8 @@ int assemble_from_rows(RowStaging& st, HostGraph& g, int threads, std::string& e
     g.titan_id = st.vid;
     g.scope = st.opts.scope;
     g.has_weight = st.opts.weight_key != 0;
+    g.weight_dt = st.plan.weight_dt ? st.plan.weight_dt : TGO_DT_INTEGER;
+    const bool keep_col = (st.opts.flags & TGO_LOAD_COLUMN_ORDER) != 0;
     g.ghost = st.ghost; g.truncated = st.truncated; g.skipped = st.skipped;
     clk.lap("folds");
     IdMap map;
@@ -596,13 +612,25 @@ int assemble_from_rows(RowStaging& st, HostGraph& g, int threads, std::string& e
     g.out.off = co; g.in.off = ci;
     g.out.adj.resize(co[n]); g.in.adj.resize(ci[n]);
     if (g.has_weight) { g.out.w.resize(co[n]); g.in.w.resize(ci[n]); }
+    if (keep_col) { g.out.col.resize(co[n]); g.in.col.resize(ci[n]); }
     parallel_for(n, threads, [&](int64_t lo, int64_t hi, int) {
         for (int64_t v = lo; v < hi; ++v) {
             int64_t a = co[v], b = ci[v];
             for (int64_t k = st.row_begin[v]; k < st.row_begin[v + 1]; ++k) {
                 if (dense[k] < 0) continue;
-                if (st.dir[k] == 0) { g.out.adj[a] = dense[k]; if (g.has_weight) g.out.w[a] = st.w[k]; ++a; }
-                else { g.in.adj[b] = dense[k]; if (g.has_weight) g.in.w[b] = st.w[k]; ++b; }
+                // staged entries of a row are in the scan's column order
+                const uint32_t col = static_cast<uint32_t>(k - st.row_begin[v]);
+                if (st.dir[k] == 0) {
+                    g.out.adj[a] = dense[k];
+                    if (g.has_weight) g.out.w[a] = st.w[k];
+                    if (keep_col) g.out.col[a] = col;
+                    ++a;
+                } else {
+                    g.in.adj[b] = dense[k];
+                    if (g.has_weight) g.in.w[b] = st.w[k];
+                    if (keep_col) g.in.col[b] = col;
+                    ++b;
+                }
             }
         }
     });
@@ -701,6 +729,8 @@ int assemble_from_edges(const tgo_edges* e, const tgo_load_opts* opts, int64_t h
     g.n = n;
     g.scope = opts->scope;
     g.has_weight = opts->weight_key != 0 && e->weight != nullptr;
+    g.weight_dt = TGO_DT_INTEGER;
+    const bool keep_col = (opts->flags & TGO_LOAD_COLUMN_ORDER) != 0;
     g.titan_id.resize(n);
     for (int64_t v = 0; v < n; ++v)
         g.titan_id[v] = e->titan_ids ? e->titan_ids[v] : ((v + 1) << 3);  // NormalVertex, 0 partition bits
@@ -741,25 +771,30 @@ int assemble_from_edges(const tgo_edges* e, const tgo_load_opts* opts, int64_t h
         ki[v + 1] = ki[v] + kb;
     }
     g.truncated = truncated;
+    // col_base: column position of the list's first entry in the row (OUT entries, direction
+    // id 2, precede IN entries, id 3: IDHandler.DirectionID)
     auto fill = [&](const std::vector<int64_t>& off, const std::vector<uint64_t>& keys,
-                    const std::vector<int64_t>& koff, HostCsr& c) {
+                    const std::vector<int64_t>& koff, HostCsr& c, const std::vector<int64_t>* col_base) {
         c.off = koff;
         c.adj.resize(koff[n]);
         if (g.has_weight) c.w.resize(koff[n]);
+        if (keep_col) c.col.resize(koff[n]);
         parallel_for(n, threads, [&](int64_t lo, int64_t hi, int) {
             for (int64_t v = lo; v < hi; ++v) {
                 const int64_t len = koff[v + 1] - koff[v];
+                const int64_t cb = col_base ? (*col_base)[v + 1] - (*col_base)[v] : 0;
                 for (int64_t j = 0; j < len; ++j) {
                     const uint64_t key = keys[off[v] + j];
                     c.adj[koff[v] + j] = static_cast<int32_t>(key >> 32);
                     if (g.has_weight) c.w[koff[v] + j] = e->weight[key & 0xFFFFFFFFULL];
+                    if (keep_col) c.col[koff[v] + j] = static_cast<uint32_t>(cb + j);
                 }
             }
         });
     };
-    fill(off_o, keys_o, ko, g.out);
+    fill(off_o, keys_o, ko, g.out, nullptr);
     std::vector<uint64_t>().swap(keys_o);
-    fill(off_i, keys_i, ki, g.in);
+    fill(off_i, keys_i, ki, g.in, &ko);
     clk.lap("fill");
     relabel_by_degree(g, threads);
     clk.lap("relabel");

@@ -42,6 +42,8 @@ __device__ inline uint64_t zigzag(int64_t v) {   // VariableLong.convert2Unsigne
 
 struct ResArgs {
     int kind;
+    int vtype;              // TGO_RESULT_VALUES: TGO_VAL_INT64 / TGO_VAL_FP64
+    int vdt;                // TGO_RESULT_VALUES: the value's encoding (TGO_DT_LONG / INTEGER / DOUBLE)
     int nkeys;
     uint8_t hdr[2][12];     // column bytes of each key, in column order
     int hlen[2];
@@ -63,12 +65,20 @@ __device__ inline bool value_of(const ResArgs& a, const void* v0, const void* v1
         bits = static_cast<uint64_t>(__double_as_longlong(x));
         return true;
     }
+    if (a.kind == TGO_RESULT_VALUES) {          // v0: 8-byte values, v1: present flags
+        bits = static_cast<const uint64_t*>(v0)[v];
+        return static_cast<const uint8_t*>(v1)[v] != 0;
+    }
     bits = static_cast<uint64_t>(static_cast<int64_t>(static_cast<const int32_t*>(v0)[v]));
     return true;
 }
 
+// Integer encodings: DEGREE, or a generic program's Integer key
+__device__ inline bool varint_value(const ResArgs& a) {
+    return a.kind == TGO_RESULT_DEGREE || (a.kind == TGO_RESULT_VALUES && a.vdt == TGO_DT_INTEGER);
+}
 __device__ inline int value_len(const ResArgs& a, uint64_t bits) {
-    if (a.kind == TGO_RESULT_DEGREE) return 1 + pos_len(zigzag(static_cast<int64_t>(bits)));
+    if (varint_value(a)) return 1 + pos_len(zigzag(static_cast<int64_t>(bits)));
     return 9;
 }
 
@@ -119,10 +129,11 @@ __global__ void res_write(ResArgs a, const int32_t* perm, const void* v0, const 
         for (int i = 0; i < a.hlen[j]; ++i) *p++ = a.hdr[j][i];
         const int64_t vpos = p - ent;
         *p++ = a.lead[j];                              // null flag (typed key) or value class (generic key)
-        if (a.kind == TGO_RESULT_DEGREE) {
+        if (varint_value(a)) {
             p = put_pos(p, zigzag(static_cast<int64_t>(bits)));
         } else {
-            const uint64_t be = a.kind == TGO_RESULT_DISTANCE ? (bits ^ 0x8000000000000000ULL) : bits;
+            const bool long_bits = a.kind == TGO_RESULT_DISTANCE || (a.kind == TGO_RESULT_VALUES && a.vdt == TGO_DT_LONG);
+            const uint64_t be = long_bits ? (bits ^ 0x8000000000000000ULL) : bits;
             for (int i = 7; i >= 0; --i) *p++ = static_cast<uint8_t>(be >> (8 * i));
         }
         p = put_pos(p, static_cast<uint64_t>(a.rel_base + e0 + j));
@@ -167,10 +178,27 @@ int encode_results(const ResultSource& src, const tgo_result_args* a, const int3
     ra.kind = a->kind;
     ra.nkeys = a->kind == TGO_RESULT_PAGERANK ? 2 : 1;
     ra.rel_base = a->relation_id_base;
-    static const int want[3][2] = {{TGO_DT_LONG, 0}, {TGO_DT_DOUBLE, TGO_DT_DOUBLE}, {TGO_DT_INTEGER, 0}};
+    if (a->kind < TGO_RESULT_DISTANCE || a->kind > TGO_RESULT_VALUES) { err = "unknown result kind"; return TGO_E_INVALID; }
+    int want[4][2] = {{TGO_DT_LONG, 0}, {TGO_DT_DOUBLE, TGO_DT_DOUBLE}, {TGO_DT_INTEGER, 0}, {0, 0}};
     // StandardSerializer registration numbers of the value classes (:71-81): Long 13, Double 20, Integer 12
-    static const uint8_t reg[3] = {0x80 | 13, 0x80 | 20, 0x80 | 12};
-    if (a->kind < TGO_RESULT_DISTANCE || a->kind > TGO_RESULT_DEGREE) { err = "unknown result kind"; return TGO_E_INVALID; }
+    uint8_t reg[4] = {0x80 | 13, 0x80 | 20, 0x80 | 12, 0};
+    if (a->kind == TGO_RESULT_VALUES) {
+        // a generic program's key: int64 values as a Long or Integer key (generic: Long),
+        // fp64 values as a Double key (generic: Double)
+        ra.vtype = a->reserved;
+        if (ra.vtype == TGO_VAL_INT64) {
+            ra.vdt = a->datatypes[0] == TGO_DT_INTEGER ? TGO_DT_INTEGER : TGO_DT_LONG;
+            want[3][0] = a->datatypes[0] == TGO_DT_INTEGER ? TGO_DT_INTEGER : TGO_DT_LONG;
+            reg[3] = 0x80 | 13;
+        } else if (ra.vtype == TGO_VAL_FP64) {
+            ra.vdt = TGO_DT_DOUBLE;
+            want[3][0] = TGO_DT_DOUBLE;
+            reg[3] = 0x80 | 20;
+        } else {
+            err = "TGO_RESULT_VALUES needs a value type (args.reserved)";
+            return TGO_E_INVALID;
+        }
+    }
     uint8_t lead[2] = {0, 0};
     for (int k = 0; k < ra.nkeys; ++k) {
         if ((a->key_ids[k] & 63) != 5 || (a->key_ids[k] >> 6) <= 0) { err = "compute key is not a user property key id"; return TGO_E_INVALID; }

@@ -340,6 +340,129 @@ __global__ void __launch_bounds__(kThreads) gather_hot_big(const int64_t* __rest
     }
 }
 
+// gather_hot_big as persistent workgroups (grid = CUs x workgroups per CU) that walk the
+// tiles t = blockIdx.x, + gridDim.x, ... and software-pipeline them: tile t+1's gathers and
+// tile t+2's index loads are in flight while tile t is reduced from LDS.  A large tile leaves
+// one (16384) or two (8192) workgroups per CU, too few for the hardware to hide a tile's
+// load -> gather -> barrier -> reduce chain by switching workgroups; here each workgroup
+// overlaps it itself.  Issue order keeps the counted waits short: a tile's row data is
+// loaded before the next tile's gathers, so the reduce waits only for loads older than them.
+// Same sums in the same order as gather_hot_big (bitwise equal for the same tiles).
+template <int kT, int kThreads, int kShift>
+__global__ void __launch_bounds__(kThreads, 4) gather_hot_pipe(const int64_t* __restrict__ off,
+        const uint32_t* __restrict__ padj, const int64_t* __restrict__ bdesc, int64_t nblocks,
+        const double* __restrict__ msg, PrColdFinal fin) {
+    constexpr int kP = kT / kThreads;
+    constexpr int kWaves = kThreads / 64;
+    static_assert(kP * kThreads == kT && (1 << kShift) == kT && kP % 2 == 0, "tile shape");
+    __shared__ double s_val[kT + 1];                     // [kT]: the sink of lanes past the tile's entries
+    const int wave = threadIdx.x >> 6;
+    const PrFinal& f = fin.f;
+    struct Desc { int64_t r0, s0, r1; int nnz; };
+    auto desc = [&](int64_t t) {
+        Desc d{0, 0, 0, 0};
+        if (t < nblocks) {
+            d.r0 = bdesc[2 * t]; d.s0 = bdesc[2 * t + 1];
+            d.r1 = bdesc[2 * t + 2];
+            const int64_t nnz = bdesc[2 * t + 3] - d.s0;
+            d.nnz = nnz > kT ? -1 : static_cast<int>(nnz);   // -1: a long row, handled by chunks
+        }
+        return d;
+    };
+    typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+    uint32_t idx[kP];
+    uint32_t slot2[kP / 2];                              // two 16-bit LDS slots per register
+    double val[kP];
+    // buffer loads: 32-bit per-lane offsets against wave-uniform descriptors, and their range
+    // check instead of branches — a lane past the tile's entries reads index 0 (records end
+    // at the tile) and gathers from an offset past the vector's records, i.e. reads 0.0
+    // without touching memory; its value goes to the sink slot kT
+    const __amdgpu_buffer_rsrc_t rmsg = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(msg), (short)0,
+                                                                          0x7FFFFFF0, 0x00020000);
+    auto load_idx = [&](const Desc& d) {
+        const __amdgpu_buffer_rsrc_t ri = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint32_t*>(padj + d.s0), (short)0, d.nnz > 0 ? d.nnz * 4 : 0, 0x00020000);
+#pragma unroll
+        for (int j = 0; j < kP; ++j)
+            idx[j] = __builtin_amdgcn_raw_buffer_load_b32(ri, (threadIdx.x + j * kThreads) * 4, 0, 2);  // aux 2: nt
+    };
+    auto gather = [&](const Desc& d) {
+#pragma unroll
+        for (int j = 0; j < kP; ++j) {
+            const bool ok = static_cast<int>(threadIdx.x + j * kThreads) < d.nnz;
+            const v2u x = __builtin_amdgcn_raw_buffer_load_b64(rmsg, ok ? (idx[j] >> kShift) * 8u : 0x7FFFFFF8u, 0, 0);
+            val[j] = __longlong_as_double(static_cast<long long>((static_cast<unsigned long long>(x.y) << 32) | x.x));
+        }
+#pragma unroll
+        for (int j = 0; j < kP; j += 2) {
+            const int k = threadIdx.x + j * kThreads;
+            const uint32_t a = k < d.nnz ? (idx[j] & (kT - 1)) : kT;
+            const uint32_t b = k + kThreads < d.nnz ? (idx[j + 1] & (kT - 1)) : kT;
+            slot2[j / 2] = a | (b << 16);
+        }
+    };
+    int64_t t = blockIdx.x;
+    Desc cur = desc(t), nxt = desc(t + gridDim.x);
+    load_idx(cur);
+    gather(cur);
+    load_idx(nxt);
+    for (; t < nblocks; t += gridDim.x) {
+        const Desc nx2 = desc(t + 2 * static_cast<int64_t>(gridDim.x));
+        // row data of this tile first (older than the next tile's loads)
+        const bool tpr = cur.r1 - cur.r0 > 64;
+        const int64_t pr = tpr ? cur.r0 + threadIdx.x : cur.r0 + wave + kWaves * lane();
+        int64_t pb = 0, pe = 0;
+        double pcs = 0.0, pec = 1.0;
+        if (cur.nnz >= 0 && pr < cur.r1) {
+            pb = off[pr];
+            pe = off[pr + 1];
+            pcs = fin.csum[pr];
+            pec = __builtin_nontemporal_load(f.edge_count + pr);
+        }
+#pragma unroll
+        for (int j = 0; j < kP; ++j) s_val[(slot2[j / 2] >> (16 * (j & 1))) & 0xFFFFu] = val[j];
+        __syncthreads();
+        gather(nxt);                                     // tile t+1 in flight during the reduce
+        load_idx(nx2);                                   // tile t+2's indices behind it
+        if (cur.nnz >= 0) {
+            auto emit = [&](int64_t r, double sum, double cs, double ec) {
+                const double p = (f.alpha * (sum + cs)) + f.base;
+                if (f.pr) f.pr[r] = p;
+                f.contrib_next[r] = p / ec;
+            };
+            const int64_t s0 = cur.s0;
+            if (tpr) {
+                bool first = true;
+                for (int64_t i = cur.r0 + threadIdx.x; i < cur.r1; i += kThreads) {
+                    int64_t b = pb, e = pe;
+                    double cs = pcs, ec = pec;
+                    if (!first) {
+                        b = off[i]; e = off[i + 1]; cs = fin.csum[i];
+                        ec = __builtin_nontemporal_load(f.edge_count + i);
+                    }
+                    first = false;
+                    double sum = 0.0;
+                    for (int k = static_cast<int>(b - s0); k < static_cast<int>(e - s0); ++k) sum = sum + s_val[k];
+                    emit(i, sum, cs, ec);
+                }
+            } else {
+                for (int q = 0; cur.r0 + wave + kWaves * q < cur.r1; ++q) {
+                    const int64_t i = cur.r0 + wave + kWaves * q;
+                    const int b = static_cast<int>(__shfl(pb, q, 64) - s0), e = static_cast<int>(__shfl(pe, q, 64) - s0);
+                    const double cs = __shfl(pcs, q, 64), ec = __shfl(pec, q, 64);
+                    double sum = 0.0;
+                    for (int k = b + lane(); k < e; k += 64) sum = sum + s_val[k];
+                    sum = wave_sum(sum);
+                    if (lane() == 0) emit(i, sum, cs, ec);
+                }
+            }
+        }
+        __syncthreads();                                 // every read of s_val done before the next store
+        cur = nxt;
+        nxt = nx2;
+    }
+}
+
 // A long row's chunk of packed entries: the chunk sum (source order, fixed).
 struct PackedOp {
     using T = double;
@@ -560,7 +683,17 @@ hipError_t k_pr_hot_phase(const ColdBlocks& cb, const double* contrib, const dou
     const PrColdFinal fin{PrFinal{edge_count, pr, contrib_next, alpha, base}, cb.csum};
     if (!cb.packed) return run_gather(cb.hcsr, cb.rb_hot, PrOp{contrib}, fin, partial_long, s);
     const RowBlocks& rb = cb.rb_hot;
-    if (rb.nblocks > 0 && cb.hot_tile != kTile) {
+    if (rb.nblocks > 0 && cb.hot_pipe) {
+        const uint32_t* padj = reinterpret_cast<const uint32_t*>(cb.hcsr.adj);
+        const int per_cu = cb.hot_tile == 16384 ? 1 : cb.hot_tile == 8192 ? 2 : 4;
+        const unsigned g = static_cast<unsigned>(std::min<int64_t>(rb.nblocks, int64_t(cb.num_cus) * per_cu));
+        if (cb.hot_tile == 16384)
+            gather_hot_pipe<16384, 1024, 14><<<g, 1024, 0, s>>>(cb.hcsr.off, padj, rb.bdesc, rb.nblocks, contrib, fin);
+        else if (cb.hot_tile == 8192)
+            gather_hot_pipe<8192, 512, 13><<<g, 512, 0, s>>>(cb.hcsr.off, padj, rb.bdesc, rb.nblocks, contrib, fin);
+        else
+            gather_hot_pipe<4096, 256, 12><<<g, 256, 0, s>>>(cb.hcsr.off, padj, rb.bdesc, rb.nblocks, contrib, fin);
+    } else if (rb.nblocks > 0 && cb.hot_tile != kTile) {
         const unsigned g = static_cast<unsigned>(rb.nblocks);
         const uint32_t* padj = reinterpret_cast<const uint32_t*>(cb.hcsr.adj);
         if (cb.hot_tile == 8192)

@@ -81,15 +81,17 @@ class Engine:
 
     # ------------------------------------------------------------------ loads
     @staticmethod
-    def _opts(scope, apply_cap, labels, weight_key):
+    def _opts(scope, apply_cap, labels, weight_key, flags=0):
         lab = np.ascontiguousarray(labels, dtype=np.int64)
-        o = L.LoadOpts(scope, 1 if apply_cap else 0, len(lab), L.ptr(lab, C.c_int64) if len(lab) else None,
-                       weight_key)
+        o = L.LoadOpts(scope=scope, apply_cap=1 if apply_cap else 0, n_labels=len(lab), flags=flags,
+                       label_ids=L.ptr(lab, C.c_int64) if len(lab) else None, weight_key=weight_key)
         return o, lab
 
-    def load_rows(self, rows, schema: Schema, scope, apply_cap=True, labels=(), weight_key=0, batch_rows=None):
-        """Feed scanned rows (optionally in work blocks) and finish the load."""
-        opts, keep = self._opts(scope, apply_cap, labels, weight_key)
+    def load_rows(self, rows, schema: Schema, scope, apply_cap=True, labels=(), weight_key=0, batch_rows=None,
+                  column_order=False):
+        """Feed scanned rows (optionally in work blocks) and finish the load.  column_order:
+        keep each entry's column position (gather_lists hands messages over in column order)."""
+        opts, keep = self._opts(scope, apply_cap, labels, weight_key, L.LOAD_COLUMN_ORDER if column_order else 0)
         nrows = rows.nrows
         step = batch_rows or max(nrows, 1)
         for r0 in range(0, max(nrows, 1), step):
@@ -126,14 +128,15 @@ class Engine:
         self.n = self.lib.tgo_num_vertices(self.ctx)
         return self
 
-    def load_edges(self, n, src, dst, scope, weight=None, titan_ids=None, apply_cap=True, weight_key=0):
+    def load_edges(self, n, src, dst, scope, weight=None, titan_ids=None, apply_cap=True, weight_key=0,
+                   column_order=False):
         src = np.ascontiguousarray(src, dtype=np.int32)
         dst = np.ascontiguousarray(dst, dtype=np.int32)
         w = None if weight is None else np.ascontiguousarray(weight, dtype=np.int32)
         t = None if titan_ids is None else np.ascontiguousarray(titan_ids, dtype=np.int64)
         e = L.Edges(n, len(src), L.ptr(src, C.c_int32), L.ptr(dst, C.c_int32), L.ptr(w, C.c_int32),
                     L.ptr(t, C.c_int64))
-        opts, keep = self._opts(scope, apply_cap, (), weight_key)
+        opts, keep = self._opts(scope, apply_cap, (), weight_key, L.LOAD_COLUMN_ORDER if column_order else 0)
         if w is not None and weight_key == 0:
             opts.weight_key = 1      # any non-zero key: the edge list carries the weights
         _check(self.lib, self.ctx, self.lib.tgo_load_edges(self.ctx, C.byref(e), C.byref(opts)))
@@ -248,6 +251,43 @@ class Engine:
                                                        L.ptr(h, C.c_uint8), out.ctypes.data_as(C.c_void_p),
                                                        L.ptr(out_has, C.c_uint8)))
         return out, out_has.astype(bool)
+
+    def gather_lists(self, scope, value_type, edge_fn, msg, has=None):
+        """MessageScope.Local receive WITHOUT a combiner (tgo_gather_lists): every vertex's
+        message stream as (row offsets n+1, values) in the API's row order."""
+        m = self._vals(msg, value_type)
+        h = None if has is None else np.ascontiguousarray(has, dtype=np.uint8)
+        off = np.zeros(self.n + 1, dtype=np.int64)
+        a = L.GatherArgs(scope, value_type, 0, edge_fn)
+        _check(self.lib, self.ctx, self.lib.tgo_gather_lists(self.ctx, C.byref(a), m.ctypes.data_as(C.c_void_p),
+                                                             L.ptr(h, C.c_uint8), L.ptr(off, C.c_int64), None))
+        vals = np.zeros(max(int(off[-1]), 1), dtype=m.dtype)
+        if off[-1] > 0:
+            _check(self.lib, self.ctx, self.lib.tgo_gather_lists(self.ctx, C.byref(a), m.ctypes.data_as(C.c_void_p),
+                                                                 L.ptr(h, C.c_uint8), L.ptr(off, C.c_int64),
+                                                                 vals.ctypes.data_as(C.c_void_p)))
+        return off, vals[:int(off[-1])]
+
+    def result_rows_values(self, key_id, datatype, value_type, values, present, relation_id_base):
+        """Edgestore entries of a generic program's compute key (tgo_result_rows_values)."""
+        v = self._vals(values, value_type)
+        p = np.ascontiguousarray(present, dtype=np.uint8)
+        a = L.ResultArgs(L.RESULT_VALUES, int(value_type), (C.c_int64 * 2)(int(key_id), 0), (C.c_int32 * 2)(int(datatype), 0),
+                         int(relation_id_base))
+        sz = L.ResultSize()
+        vp = v.ctypes.data_as(C.c_void_p)
+        _check(self.lib, self.ctx, self.lib.tgo_result_rows_values(self.ctx, C.byref(a), vp, L.ptr(p, C.c_uint8),
+                                                                   C.byref(sz), None))
+        keys = np.empty(max(sz.nrows, 1), np.int64)
+        eb = np.empty(sz.nrows + 1, np.int64)
+        bb = np.empty(sz.nrows + 1, np.int64)
+        data = np.empty(max(sz.nbytes, 1), np.uint8)
+        lv = np.empty(max(sz.nentries, 1), np.int64)
+        buf = L.RowsBuf(L.ptr(keys, C.c_int64), L.ptr(eb, C.c_int64), L.ptr(bb, C.c_int64), L.ptr(data, C.c_uint8),
+                        L.ptr(lv, C.c_int64))
+        _check(self.lib, self.ctx, self.lib.tgo_result_rows_values(self.ctx, C.byref(a), vp, L.ptr(p, C.c_uint8),
+                                                                   C.byref(sz), C.byref(buf)))
+        return Rows(keys[:sz.nrows], eb, bb, data[:sz.nbytes], lv[:sz.nentries])
 
     def combine_global(self, value_type, combiner, targets, values):
         """MessageScope.Global: messages to dense row ids combined per target in send order."""

@@ -17,8 +17,18 @@ message traffic — what Fulgora spends its supersteps on — is combined on the
 Messages are double-buffered exactly as VertexState does (sent in iteration i, read in i+1;
 VertexState.java:55-89), and the scopes a vertex may receive on are the ones the program
 declared for the previous iteration (FulgoraVertexMemory.nextIteration/completeIteration).
-A combiner is required: the vectorised receive returns the combined message (the reference's
-programs reduce the stream with theirs, and a vertex cut needs one anyway, FulgoraUtil.java:80-91).
+With a combiner the receive returns the combined message per vertex.  Without one
+(``combiner = None``) a Local receive returns every vertex's message stream itself
+(``MessageLists``, ``tgo_gather_lists``) in the order the reference's stream yields it, the
+row's column order, for the program to reduce however it likes; a Global scope then delivers
+at most one message per target, and two messages meeting at a target (or at a vertex cut)
+fail the job as FulgoraUtil's ThrowingCombiner does (FulgoraUtil.java:80-91).
+
+Edge functions are "message op w" over the load's weight property (any 32-bit numeric key:
+Byte, Short, Integer, Character, Boolean, Float): identity, +1, + - * / min max of w.
+TinkerPop's own TraversalVertexProgram (Gremlin OLAP traversals, BOTH preload at
+VertexProgramScanJob.java:101-107) is not restated: its tests live in the absent gremlin-test
+jar, so its results would be parity-unpinned.
 """
 from __future__ import annotations
 
@@ -27,7 +37,8 @@ import numpy as np
 from . import _lib as L
 
 EDGE_FNS = {"identity": L.EDGE_IDENTITY, "add_one": L.EDGE_ADD_ONE, "add_weight": L.EDGE_ADD_WEIGHT,
-            "mul_weight": L.EDGE_MUL_WEIGHT}
+            "mul_weight": L.EDGE_MUL_WEIGHT, "sub_weight": L.EDGE_SUB_WEIGHT, "min_weight": L.EDGE_MIN_WEIGHT,
+            "max_weight": L.EDGE_MAX_WEIGHT, "div_weight": L.EDGE_DIV_WEIGHT}
 INCIDENT = {"outE": L.SCOPE_OUT_E, "inE": L.SCOPE_IN_E, "bothE": L.SCOPE_BOTH_E}
 
 
@@ -169,6 +180,38 @@ class Vertices:
             self._props[key] = (nv, op | present)
 
 
+class MessageLists:
+    """A combiner-less Local receive: every vertex's message stream (row order), the values
+    of vertex i in ``values[offsets[i]:offsets[i+1]]`` in the order the reference's
+    receiveMessages stream yields them (VertexMemoryHandler.java:83-92)."""
+
+    def __init__(self, offsets, values):
+        self.offsets = np.asarray(offsets, np.int64)
+        self.values = np.asarray(values)
+
+    def __len__(self):
+        return len(self.offsets) - 1
+
+    def of(self, i):
+        return self.values[self.offsets[i]:self.offsets[i + 1]]
+
+    def counts(self):
+        return np.diff(self.offsets)
+
+    def has(self):
+        return self.counts() > 0
+
+    def reduce(self, ufunc):
+        """ufunc folded over each vertex's stream in stream order -> (values, has)."""
+        n = len(self)
+        cnt = self.counts()
+        out = np.zeros(n, self.values.dtype)
+        nz = cnt > 0
+        if nz.any():
+            out[nz] = ufunc.reduceat(self.values, self.offsets[:-1][nz])
+        return out, nz
+
+
 class Messenger:
     """Messenger of one superstep: receive() combines the previous superstep's messages of a
     scope on the device; send() records this superstep's messages."""
@@ -189,6 +232,9 @@ class Messenger:
         vals, has = self._prev[scope]
         if isinstance(scope, MessageScope.Global):
             return vals, has
+        if self._p.combiner is None:
+            return MessageLists(*self._e.gather_lists(INCIDENT[scope.incident], self._p.value_type,
+                                                      EDGE_FNS[scope.edge_fn], vals, has))
         return self._e.gather(INCIDENT[scope.incident], self._p.value_type, self._p.combiner, EDGE_FNS[scope.edge_fn],
                               vals, has)
 
@@ -226,7 +272,17 @@ class Messenger:
                 val = np.concatenate([x for _, x in v]) if v else np.zeros(0)
                 dense = self._e.dense_ids(tid)
                 keep = dense >= 0
-                out[scope] = self._e.combine_global(self._p.value_type, self._p.combiner, dense[keep], val[keep])
+                comb = self._p.combiner
+                if comb is None:
+                    # no combiner: VertexState.addMessage combines a second message to one
+                    # target with FulgoraUtil's ThrowingCombiner (:80-91)
+                    t = dense[keep]
+                    if len(t) != len(np.unique(t)):
+                        from .engine import TitanException
+                        raise TitanException(L.TGO_E_PROGRAM, "The VertexProgram needs to define a message combiner "
+                                                              "in order to preserve memory and handle partitioned vertices")
+                    comb = L.COMBINE_SUM
+                out[scope] = self._e.combine_global(self._p.value_type, comb, dense[keep], val[keep])
             else:
                 out[scope] = v
         return out
@@ -236,7 +292,7 @@ class GenericVertexProgram:
     """Base of vectorised vertex programs (TinkerPop VertexProgram, one call per superstep
     over all vertices).  Subclasses set value_type / combiner and override the hooks."""
     value_type = L.VAL_INT64
-    combiner = L.COMBINE_SUM
+    combiner = L.COMBINE_SUM            # None: receive() hands Local streams over as MessageLists
     compute_keys: tuple = ()
     memory_compute_keys: tuple = ()
     weight_property = None              # property read by add_weight / mul_weight edge functions
