@@ -70,6 +70,8 @@ def parse():
                    help="partitioned path: degree-grouped device layout (tgo_part_layout); 0 = global ids as given")
     p.add_argument("--partitioned", action="store_true",
                    help="use the vertex-partitioned multi-GPU path even at N=1 (for testing it on one GPU)")
+    p.add_argument("--balanced", type=int, default=1,
+                   help="partitioned path: edge-balanced ranges (entries + vertices, SlotPartition); 0 = equal ranges")
     return p.parse_args()
 
 
@@ -331,63 +333,88 @@ def run_partitioned(args, world, rank, local_rank):
     import torch.distributed as dist
     from titan_amd import Engine
     from titan_amd import _lib as L
-    from titan_amd.distributed import (HipPartBackend, all_gather_layout, distributed_bfs, distributed_msbfs,
-                                       distributed_pagerank, entry_imbalance, exchange_stream, pagerank_layout,
-                                       partition_range, pick_roots_partitioned)
+    from titan_amd.distributed import (HipPartBackend, SlotPartition, all_gather_layout, balanced_partition,
+                                       distributed_bfs, distributed_msbfs, distributed_pagerank, entry_imbalance,
+                                       exchange_stream, pagerank_layout, partition_range, pick_roots_partitioned,
+                                       word_weights)
     torch.cuda.set_device(local_rank)
     dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
     scale = args.scale + int(round(math.log2(world)))
     n = 1 << scale
     m = args.edge_factor << scale
-    lo, hi = partition_range(n, world, rank)
     lib = L.load()
-    t0 = time.perf_counter()
-    cap = int(2.3 * m / world) + (1 << 22)
-    src = np.empty(cap, np.int32)
-    dst = np.empty(cap, np.int32)
-    wgt = np.empty(cap, np.int32) if args.sssp_roots > 0 else None
-    cnt = C.c_int64()
-    rc = lib.tgo_rmat_partition(scale, args.edge_factor, 0x54495441, lo, hi, L.ptr(src, C.c_int32),
-                                L.ptr(dst, C.c_int32), L.ptr(wgt, C.c_int32), cap, C.byref(cnt), 16)
-    if rc:
-        raise RuntimeError(f"tgo_rmat_partition rc={rc} count={cnt.value} cap={cap}")
-    src, dst = src[:cnt.value], dst[:cnt.value]
-    wgt = wgt[:cnt.value] if wgt is not None else None
-    log(f"rmat scale {scale} partition [{lo},{hi}) of {world}: {cnt.value} edges in {time.perf_counter() - t0:.1f}s")
+
+    def edges_of(lo, hi):
+        """The RMAT stream's edges with an endpoint in [lo, hi) (tgo_rmat_partition)."""
+        t0 = time.perf_counter()
+        cap = int(2.3 * m * (hi - lo) / n) + (1 << 22)
+        src = np.empty(cap, np.int32)
+        dst = np.empty(cap, np.int32)
+        wgt = np.empty(cap, np.int32) if args.sssp_roots > 0 else None
+        cnt = C.c_int64()
+        rc = lib.tgo_rmat_partition(scale, args.edge_factor, 0x54495441, lo, hi, L.ptr(src, C.c_int32),
+                                    L.ptr(dst, C.c_int32), L.ptr(wgt, C.c_int32), cap, C.byref(cnt), 16)
+        if rc:
+            raise RuntimeError(f"tgo_rmat_partition rc={rc} count={cnt.value} cap={cap}")
+        log(f"rmat scale {scale} partition [{lo},{hi}) of {world}: {cnt.value} edges in "
+            f"{time.perf_counter() - t0:.1f}s")
+        return src[:cnt.value], dst[:cnt.value], (wgt[:cnt.value] if wgt is not None else None)
+
+    # Edge-balanced ranges (SURVEY §8e): the words of the equal ranges are weighed (entries +
+    # vertices) and all-gathered, every rank cuts the same balanced bounds, then takes the
+    # edges of its own range.  The exchanges run over equal slots (SlotPartition): the edges
+    # are handed to the engine in slot ids, results and roots map back to caller ids.
+    elo, ehi = partition_range(n, world, rank)
+    src, dst, wgt = edges_of(elo, ehi)
+    if args.balanced:
+        part, ww = balanced_partition(src, dst, n, elo, ehi, dev)
+    else:
+        part = SlotPartition.equal(n, world)
+        loc = torch.from_numpy(word_weights(src, dst, elo, ehi)).to(dev)
+        wg = torch.empty(n // 64, dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(wg, loc)
+        ww = wg.cpu().numpy()
+    lo, hi = part.range(rank)
+    if (lo, hi) != (elo, ehi):
+        del src, dst, wgt
+        src, dst, wgt = edges_of(lo, hi)
+    # the one-GPU bench's roots (tgo_pick_roots over the whole edge list), from partition edges
+    roots = pick_roots_partitioned(n, src, dst, lo, hi, args.roots, 7, dev, part=part)
+    ns, (slo, shi) = part.n_slots, part.slot_range(rank)
+    src, dst = part.to_slots(src), part.to_slots(dst)
+    roots_s = [int(x) for x in part.to_slots(np.asarray(roots, np.int64))]
     stream = exchange_stream()     # kernels and RCCL collectives ordered on one (non-default) stream
     t0 = time.perf_counter()
-    lay = all_gather_layout(src, dst, n, lo, hi, torch.device("cuda", local_rank)) if args.layout else None
+    lay = all_gather_layout(src, dst, ns, slo, shi, dev) if args.layout else None
     bfs_be = HipPartBackend(Engine(device=local_rank, host_threads=16, stream=stream)
-                            .load_partition(n, lo, hi, src, dst, L.SCOPE_BOTH_E, apply_cap=False, layout=lay),
-                            n, lo, hi, device_counts=True)
-    pr_eng = Engine(device=local_rank, host_threads=16, stream=stream).load_partition(n, lo, hi, src, dst,
+                            .load_partition(ns, slo, shi, src, dst, L.SCOPE_BOTH_E, apply_cap=False, layout=lay),
+                            ns, slo, shi, device_counts=True)
+    pr_eng = Engine(device=local_rank, host_threads=16, stream=stream).load_partition(ns, slo, shi, src, dst,
                                                                                     L.SCOPE_IN_E, apply_cap=True,
                                                                                     layout=lay)
-    pr_be = HipPartBackend(pr_eng, n, lo, hi)
+    pr_be = HipPartBackend(pr_eng, ns, slo, shi)
     pr_layout = pagerank_layout(pr_be)       # cache-blocked hot-first exchange (tgo_part_pr_blocked)
     log(f"partition graphs loaded in {time.perf_counter() - t0:.1f}s")
-    # the one-GPU bench's roots (tgo_pick_roots over the whole edge list), from partition edges
-    roots = pick_roots_partitioned(n, src, dst, lo, hi, args.roots, 7, torch.device("cuda", local_rank))
     # per-rank owned entries of the bothE graph: the partition's load imbalance (max / mean)
     ent = bfs_be.e.stats()
-    rank_entries, imbalance = entry_imbalance(int(ent["out_entries"] + ent["in_entries"]),
-                                              torch.device("cuda", local_rank))
+    rank_entries, imbalance = entry_imbalance(int(ent["out_entries"] + ent["in_entries"]), dev)
     # per-root reached entries (untimed) for GTEPS
-    _, mR, depth_ms = distributed_msbfs(bfs_be, roots, n, stats=True)
+    _, mR, depth_ms = distributed_msbfs(bfs_be, roots_s, ns, stats=True)
     # single-source side measurement (untimed, every root, Graph500 style harmonic mean)
     ss_t = []
-    distributed_bfs(bfs_be, roots[0], n, fetch=False, stats=False)
-    for r in roots:
+    distributed_bfs(bfs_be, roots_s[0], ns, fetch=False, stats=False)
+    for r in roots_s:
         torch.cuda.synchronize()
         t = time.perf_counter()
-        distributed_bfs(bfs_be, r, n, fetch=False, stats=False)
+        distributed_bfs(bfs_be, r, ns, fetch=False, stats=False)
         torch.cuda.synchronize()
         ss_t.append(time.perf_counter() - t)
     hmean = len(ss_t) / float(np.sum(np.array(ss_t) / (mR[:len(ss_t)] / 2.0)))
 
     def step():
         t = time.perf_counter()
-        distributed_msbfs(bfs_be, roots, n, stats=False)
+        distributed_msbfs(bfs_be, roots_s, ns, stats=False)
         torch.cuda.synchronize()
         bt = time.perf_counter() - t
         t = time.perf_counter()
@@ -416,7 +443,8 @@ def run_partitioned(args, world, rank, local_rank):
     del pr_be, pr_eng
     sssp = None
     if wgt is not None:
-        sssp = sssp_leg_partitioned(args, world, rank, local_rank, n, lo, hi, src, dst, wgt, roots, stream, lay)
+        sssp = sssp_leg_partitioned(args, world, rank, local_rank, ns, slo, shi, src, dst, wgt, roots_s, stream, lay,
+                                    n)
     if rank == 0:
         edges_in = mR / 2.0
         teps = float(edges_in.sum()) * args.steps / bfs_wall
@@ -434,18 +462,23 @@ def run_partitioned(args, world, rank, local_rank):
         line["config"]["device_layout"] = "degree-grouped per rank" if args.layout else "global ids"
         line["pagerank_exchange"] = {"hot_rows_per_rank": pr_layout[0], "active_span": pr_layout[1],
                                      "bytes_per_rank_per_update": 8 * pr_layout[1]}
-        line["partition"] = {"ranges": "equal 64-aligned vertex ranges of the seeded relabel",
-                             "rank_entries": rank_entries, "entry_imbalance_max_over_mean": round(imbalance, 4)}
+        wr = part.weights(ww)
+        line["partition"] = {"ranges": ("edge-balanced 64-aligned ranges (entries + vertices) in equal exchange slots"
+                                        if args.balanced else "equal 64-aligned vertex ranges of the seeded relabel"),
+                             "bounds": [int(x) for x in part.bounds], "slot": part.slot,
+                             "rank_entries": rank_entries, "entry_imbalance_max_over_mean": round(imbalance, 4),
+                             "weight_imbalance_max_over_mean": round(max(wr) / (sum(wr) / len(wr)), 4)}
         line["sssp"] = sssp
         print(json.dumps(line), file=JSON_OUT, flush=True)
     dist.barrier()
     dist.destroy_process_group()
 
 
-def sssp_leg_partitioned(args, world, rank, local_rank, n, lo, hi, src, dst, wgt, roots, stream, lay):
+def sssp_leg_partitioned(args, world, rank, local_rank, n, lo, hi, src, dst, wgt, roots, stream, lay, n_real):
     """configs[4] over N GPUs: delta-stepping SSSP on the vertex-partitioned weighted graph
     (inE scope, no preload cap), per-owner relaxation exchange over RCCL
-    (titan_amd/distributed.distributed_sssp); roots whose reach is the giant component."""
+    (titan_amd/distributed.distributed_sssp); roots whose reach is the giant component.
+    n, lo, hi, src, dst, roots: slot ids (SlotPartition); n_real: the graph's vertices."""
     import torch
     import torch.distributed as dist
     from titan_amd import Engine
@@ -460,7 +493,7 @@ def sssp_leg_partitioned(args, world, rank, local_rank, n, lo, hi, src, dst, wgt
         if len(res) == args.sssp_roots:
             break
         _, reached, _ = distributed_sssp(be, int(r), args.delta, fetch=False, stats=True)
-        if reached[0] * 4 < n:
+        if reached[0] * 4 < n_real:
             continue
         torch.cuda.synchronize()
         dist.barrier()
@@ -474,7 +507,7 @@ def sssp_leg_partitioned(args, world, rank, local_rank, n, lo, hi, src, dst, wgt
         return None
     mR = np.array([x[0] for x in res], np.float64)
     wall = np.array([x[1] for x in res])
-    return {"workload": f"rmat{int(math.log2(n))}-weighted-inE-delta-sssp-partitioned", "roots": len(res),
+    return {"workload": f"rmat{int(math.log2(n_real))}-weighted-inE-delta-sssp-partitioned", "roots": len(res),
             "gteps_hmean": round(len(res) / float(np.sum(wall / mR)) / 1e9, 4),
             "ms_per_root": round(float(wall.mean()) * 1e3, 3), "reached_entries": int(mR.mean()),
             "phases": int(np.mean([x[2] for x in res]))}

@@ -649,6 +649,91 @@ def test_in_process_group_runs_the_real_drivers():
         assert np.array_equal(np.concatenate([x[5] for x in res]), osd)
 
 
+def test_slot_partition_balances_entries_and_round_trips():
+    """SlotPartition.balanced: 64-aligned ranges of near-equal entries + vertices, equal
+    exchange slots, caller <-> slot ids round trip; a skewed weight vector is cut at the
+    boundary closest to the even share."""
+    from titan_amd import rmat_edges
+    from titan_amd.distributed import SlotPartition, word_weights
+    p = SlotPartition.balanced(np.array([10, 1, 1, 1, 50, 1, 1, 1, 1, 1]), 3)
+    assert list(p.bounds) == [0, 256, 320, 640] and p.slot == 320 and p.n_slots == 960
+    scale = 14
+    n = 1 << scale
+    src, dst, _ = rmat_edges(scale, 16, seed=5)
+    ww = word_weights(src, dst, 0, n)
+    assert int(ww.sum()) == 2 * len(src) + n
+    for world in (2, 4, 8):
+        bal, eq = SlotPartition.balanced(ww, world), SlotPartition.equal(n, world)
+        wb, we = bal.weights(ww), eq.weights(ww)
+        assert sum(wb) == sum(we) == int(ww.sum())
+        assert max(wb) / np.mean(wb) <= max(we) / np.mean(we)
+        assert max(wb) / np.mean(wb) < 1.1           # word granularity: hub words are coarse at scale 14
+        assert bal.slot % 64 == 0 and bal.slot >= n // world
+        v = np.arange(n, dtype=np.int32)
+        s = bal.to_slots(v)
+        assert s.dtype == np.int32 and len(np.unique(s)) == n and s.max() < bal.n_slots
+        assert np.array_equal(bal.from_slots(s), v)
+        for r in range(world):
+            lo, hi = bal.range(r)
+            assert np.array_equal(s[lo:hi], np.arange(r * bal.slot, r * bal.slot + hi - lo))
+    with pytest.raises(ValueError):
+        SlotPartition([0, 100, 256], 256)
+
+
+def test_balanced_partition_runs_the_real_drivers():
+    """The edge-balanced partition end to end over InProcessGroup: weights all-gathered from
+    equal ranges, the same bounds on every rank, the roots of the one-GPU bench, and the real
+    drivers over slot ids (numpy local steps) — results mapped back equal the oracle's."""
+    import fulgora as fr
+    from titan_amd import pick_roots, rmat_edges
+    from titan_amd.distributed import (InProcessGroup, balanced_partition, distributed_bfs, distributed_msbfs,
+                                       distributed_pagerank, distributed_sssp, partition_range,
+                                       pick_roots_partitioned)
+    scale = 9
+    n = 1 << scale
+    src, dst, w = rmat_edges(scale, 8, seed=41, weights=True)
+    og = fr.OracleGraph.from_edges(n, src, dst, w)
+    ids = (np.arange(n, dtype=np.int64) + 1) << 3
+    for world in (2, 4):
+        def body(rank, comm):
+            elo, ehi = partition_range(n, world, rank)
+            mine = ((src >= elo) & (src < ehi)) | ((dst >= elo) & (dst < ehi))
+            part, ww = balanced_partition(src[mine], dst[mine], n, elo, ehi, torch.device("cpu"), comm=comm)
+            lo, hi = part.range(rank)
+            mine = ((src >= lo) & (src < hi)) | ((dst >= lo) & (dst < hi))
+            roots = pick_roots_partitioned(n, src[mine], dst[mine], lo, hi, 3, 7, torch.device("cpu"), comm=comm,
+                                           part=part)
+            s, d, wt = part.to_slots(src[mine]), part.to_slots(dst[mine]), w[mine]
+            ns, (slo, shi) = part.n_slots, part.slot_range(rank)
+            be = NumpyPartBackend(ns, slo, shi, s, d)
+            rs = [int(x) for x in part.to_slots(np.asarray(roots))]
+            bd, _, _ = distributed_bfs(be, rs[0], ns, comm=comm)
+            distributed_msbfs(be, rs, ns, comm=comm)
+            lv = [part.slot_results(rank, np.where(be.mslvl[:, i] >= 0, be.mslvl[:, i], ABSENT))
+                  for i in range(len(rs))]
+            pr = distributed_pagerank(be, 0.85, n, 8, comm=comm)
+            wbe = NumpyPartBackend(ns, slo, shi, s, d, w=wt, scope=1)
+            sd, _, _ = distributed_sssp(wbe, rs[1], 0, comm=comm)
+            return (list(part.bounds), roots, part.slot_results(rank, bd), lv, part.slot_results(rank, pr),
+                    part.slot_results(rank, sd))
+
+        res = InProcessGroup(world).run(body)
+        assert all(x[0] == res[0][0] for x in res) and all(x[1] == res[0][1] for x in res)
+        assert res[0][1] == [int(x) for x in pick_roots(n, src, dst, 3, seed=7)]
+        roots = res[0][1]
+        od, _ = og.shortest_distance(int(ids[roots[0]]), n, 2)
+        assert np.array_equal(np.concatenate([x[2] for x in res]), od)
+        for i, root in enumerate(roots):
+            o, _ = og.shortest_distance(int(ids[root]), n, 2)
+            assert np.array_equal(np.concatenate([x[3][i] for x in res]), o)
+        opr, _ = og.pagerank(0.85, n, 8)
+        got = np.concatenate([x[4] for x in res])
+        fin = np.isfinite(opr)
+        assert np.array_equal(np.isfinite(got), fin) and np.abs(got[fin] - opr[fin]).sum() <= 1e-6
+        osd, _ = og.shortest_distance(int(ids[roots[1]]), n, 1, weighted=True)
+        assert np.array_equal(np.concatenate([x[5] for x in res]), osd)
+
+
 def test_in_process_group_propagates_a_rank_failure():
     from titan_amd.distributed import InProcessGroup
 

@@ -13,9 +13,9 @@ import torch
 import fulgora as fr
 from titan_amd import Engine, rmat_edges
 from titan_amd import _lib as L
-from titan_amd.distributed import (HipPartBackend, InProcessGroup, distributed_bfs, distributed_msbfs,
-                                   distributed_pagerank, distributed_sssp, exchange_stream, local_layout,
-                                   pagerank_layout, partition_range)
+from titan_amd.distributed import (HipPartBackend, InProcessGroup, SlotPartition, distributed_bfs,
+                                   distributed_msbfs, distributed_pagerank, distributed_sssp, exchange_stream,
+                                   local_layout, pagerank_layout, partition_range, word_weights)
 from titan_amd.engine import TitanException
 
 pytestmark = pytest.mark.gpu
@@ -27,14 +27,18 @@ class Ranks:
     on every rank's thread with that rank's communicator."""
 
     def __init__(self, world, n, src, dst, scope, weight=None, layout=False, apply_cap=False, hard_limit=100000,
-                 device_counts=False):
+                 device_counts=False, part=None):
+        # part (SlotPartition): edge-balanced ranges — the engines see slot ids over n_slots
+        if part is not None:
+            src, dst, n = part.to_slots(src), part.to_slots(dst), part.n_slots
+        rng = (lambda r: part.slot_range(r)) if part is not None else (lambda r: partition_range(n, world, r))
         lay = None
         if layout:
-            lay = np.concatenate([local_layout(src, dst, n, *partition_range(n, world, r)) for r in range(world)])
+            lay = np.concatenate([local_layout(src, dst, n, *rng(r)) for r in range(world)])
             assert np.array_equal(np.sort(lay), np.arange(n))
         self.world, self.streams, self.backends = world, [], []
         for r in range(world):
-            lo, hi = partition_range(n, world, r)
+            lo, hi = rng(r)
             s = torch.cuda.Stream()
             with torch.cuda.stream(s):
                 eng = Engine(stream=s.cuda_stream, hard_query_limit=hard_limit).load_partition(
@@ -281,3 +285,53 @@ def test_drivers_on_a_real_world1_group(monkeypatch):
         assert np.abs(pr[fin] - opr[fin]).sum() <= 1e-6
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_edge_balanced_partition_drivers(world, monkeypatch):
+    """Edge-balanced ranges (SlotPartition, what bench.py's partitioned path runs): unequal
+    64-aligned caller ranges in equal exchange slots, the real drivers over the HIP local
+    steps — BFS / multi-source BFS / delta SSSP bit-exact and capped cache-blocked PageRank
+    within 1e-6 L1 of the oracle, results mapped back to caller ids."""
+    scale = 12
+    n = 1 << scale
+    src, dst, w = rmat_edges(scale, 16, seed=43, weights=True)
+    part = SlotPartition.balanced(word_weights(src, dst, 0, n), world)
+    assert part.n_slots > n                                   # unequal ranges: padded slots
+    og = fr.OracleGraph.from_edges(n, src, dst, w)
+    ids = (np.arange(n, dtype=np.int64) + 1) << 3
+    roots = [int(src[0]), int(dst[9]), int(src[100])]
+    rs = [int(x) for x in part.to_slots(np.asarray(roots))]
+    ns = part.n_slots
+    cut = lambda res, k: np.concatenate([part.slot_results(r, x[k]) for r, x in enumerate(res)])  # noqa: E731
+    ranks = Ranks(world, n, src, dst, L.SCOPE_BOTH_E, layout=True, device_counts=True, part=part)
+    res = ranks.run(lambda be, comm: distributed_bfs(be, rs[0], ns, comm=comm))
+    od, _ = og.shortest_distance(int(ids[roots[0]]), n, 2)
+    assert np.array_equal(cut(res, 0), od)
+
+    def ms(be, comm):
+        r, _, _ = distributed_msbfs(be, rs, ns, comm=comm)
+        return [be.ms_levels(i) for i in range(len(rs))], r
+    res = ranks.run(ms)
+    for i, root in enumerate(roots):
+        o, _ = og.shortest_distance(int(ids[root]), n, 2)
+        assert np.array_equal(np.concatenate([part.slot_results(r, x[0][i]) for r, x in enumerate(res)]), o)
+        assert res[0][1][i] == int((o != ABSENT).sum())
+    hard = 40
+    monkeypatch.setenv("TGO_PR_HOT", "512")
+    monkeypatch.setenv("TGO_PR_SEG", "256")
+    pr_ranks = Ranks(world, n, src, dst, L.SCOPE_IN_E, layout=True, apply_cap=True, hard_limit=hard, part=part)
+
+    def pr(be, comm):
+        lay = pagerank_layout(be, comm=comm)
+        return (distributed_pagerank(be, 0.85, n, 12, layout=lay, comm=comm), lay)
+    res = pr_ranks.run(pr)
+    assert res[0][1][0] > 0                                   # the blocked hot-first layout ran
+    opr, _ = fr.OracleGraph.from_edges(n, src, dst, hard_limit=hard).pagerank(0.85, n, 12)
+    got = cut(res, 0)
+    fin = np.isfinite(opr)
+    assert np.array_equal(np.isfinite(got), fin) and np.abs(got[fin] - opr[fin]).sum() <= 1e-6
+    w_ranks = Ranks(world, n, src, dst, L.SCOPE_IN_E, weight=w, layout=True, part=part)
+    res = w_ranks.run(lambda be, comm: distributed_sssp(be, rs[1], 0, comm=comm))
+    osd, _ = og.shortest_distance(int(ids[roots[1]]), n, L.SCOPE_IN_E, weighted=True)
+    assert np.array_equal(cut(res, 0), osd)

@@ -174,6 +174,106 @@ def partition_range(n_global: int, world: int, rank: int):
     return rank * per, (rank + 1) * per
 
 
+class SlotPartition:
+    """Edge-balanced 1-D partition (contiguous ranges balanced by entries +
+    vertices).  Rank r owns the caller's vertices [bounds[r], bounds[r+1]) — 64-aligned, of
+    unequal sizes — and every exchange runs in a SLOT space of `world` equal slots of `slot`
+    ids (the largest range, rounded up to a word): caller id v of rank r is slot id
+    r * slot + (v - bounds[r]).  The C-ABI's partitioned path (titan_gpu_olap_part.h) keeps
+    its equal-slice exchanges (all-gathers need equal slices; owner = id // n_local) over
+    n_slots = world * slot ids; a slot past the end of its rank's range is an entry-less
+    vertex that no program reaches and no result reports (slot_results drops it)."""
+
+    def __init__(self, bounds, n: int):
+        b = np.asarray(bounds, np.int64)
+        if b[0] != 0 or b[-1] != n or np.any(np.diff(b) <= 0) or np.any(b % 64):
+            raise ValueError("bounds must be increasing, 64-aligned and cover [0, n)")
+        self.bounds, self.n, self.world = b, int(n), len(b) - 1
+        self.slot = int(np.diff(b).max())
+        self.n_slots = self.world * self.slot
+
+    @classmethod
+    def equal(cls, n: int, world: int):
+        return cls([partition_range(n, world, r)[0] for r in range(world)] + [n], n)
+
+    @classmethod
+    def balanced(cls, word_weight, world: int):
+        """Ranges of near-equal total weight over 64-vertex words (word_weight[i] = the list
+        entries of vertices [64 i, 64 i + 64) plus their count): boundary r is the word
+        boundary whose running weight is closest to r/world of the total; every range keeps
+        >= 1 word."""
+        w = np.asarray(word_weight, np.int64)
+        nw = len(w)
+        if nw < world:
+            raise ValueError("fewer 64-vertex words than ranks")
+        c = np.concatenate([[0], np.cumsum(w)])          # c[k] = weight of words [0, k)
+        tot = int(c[-1])
+        cut = [0]
+        for r in range(1, world):
+            t = tot * r / world
+            k = int(np.searchsorted(c, t, side="left"))  # first boundary with c[k] >= t
+            if k > 0 and t - c[k - 1] < c[k] - t:
+                k -= 1
+            k = max(k, cut[-1] + 1)
+            k = min(k, nw - (world - r))
+            cut.append(k)
+        cut.append(nw)
+        return cls(np.asarray(cut, np.int64) * 64, nw * 64)
+
+    def range(self, rank: int):
+        return int(self.bounds[rank]), int(self.bounds[rank + 1])
+
+    def slot_range(self, rank: int):
+        return rank * self.slot, (rank + 1) * self.slot
+
+    def to_slots(self, v):
+        """Caller ids -> slot ids (vectorised; int32 arrays stay int32 when the slots fit)."""
+        v = np.asarray(v)
+        r = np.searchsorted(self.bounds, v, side="right") - 1
+        s = r.astype(np.int64) * self.slot + (v.astype(np.int64) - self.bounds[r])
+        return s.astype(np.int32) if v.dtype == np.int32 and self.n_slots < 2**31 else s
+
+    def from_slots(self, s):
+        s = np.asarray(s, np.int64)
+        r, o = s // self.slot, s % self.slot
+        if np.any(o >= self.bounds[r + 1] - self.bounds[r]):
+            raise ValueError("slot id past its rank's range")
+        return self.bounds[r] + o
+
+    def slot_results(self, rank: int, local):
+        """A rank's slot-local results (n_local = slot values) cut to its owned caller range."""
+        lo, hi = self.range(rank)
+        return np.asarray(local)[:hi - lo]
+
+    def weights(self, word_weight):
+        """Per-rank total weight (the imbalance this partition leaves)."""
+        c = np.concatenate([[0], np.cumsum(np.asarray(word_weight, np.int64))])
+        return [int(c[self.bounds[r + 1] // 64] - c[self.bounds[r] // 64]) for r in range(self.world)]
+
+
+def word_weights(src, dst, lo: int, hi: int):
+    """Entries + vertices of the owned rows per 64-vertex word of [lo, hi): each edge gives
+    an OUT entry to its source row and an IN entry to its target row."""
+    w = np.zeros((hi - lo) // 64, np.int64)
+    for x in (np.asarray(src), np.asarray(dst)):
+        x = x[(x >= lo) & (x < hi)].astype(np.int64)
+        w += np.bincount((x - lo) >> 6, minlength=len(w))
+    return w + 64
+
+
+def balanced_partition(src, dst, n: int, lo: int, hi: int, device, group=None, comm=None):
+    """The edge-balanced SlotPartition every rank agrees on: each rank weighs the words of
+    its equal range [lo, hi) from its partition edges (word_weights), the weights are
+    all-gathered (n / 64 int64) and SlotPartition.balanced cuts them — same bounds on every
+    rank.  The caller then takes the edges of its new range and maps them to slot ids."""
+    cm = _comm(comm, group)
+    loc = torch.from_numpy(word_weights(src, dst, lo, hi)).to(device)
+    out = torch.empty(n // 64, dtype=torch.int64, device=device)
+    cm.all_gather_into_tensor(out, loc)
+    w = out.cpu().numpy()
+    return SlotPartition.balanced(w, cm.world), w
+
+
 def local_layout(src, dst, n_global: int, lo: int, hi: int, threads: int = 16):
     """tgo_part_layout: internal global ids of the owned vertices [lo, hi) (degree-grouped,
     hottest first, kept inside the owned range).  Host code only (no device needed)."""
@@ -208,19 +308,24 @@ def _splitmix64(x: int) -> int:
 
 
 def pick_roots_partitioned(n_global: int, src, dst, lo: int, hi: int, nroots: int, seed: int, device, group=None,
-                           comm=None):
+                           comm=None, part: "SlotPartition" = None):
     """The roots tgo_pick_roots draws on the whole edge list (synth.cpp), from a rank's
     partition edges: owned "has an entry" flags are all-gathered (n bytes), then every rank
     walks the same splitmix64 candidate sequence — the partitioned bench runs the same
-    sources as the one-GPU bench."""
-    has = np.zeros(hi - lo, np.uint8)
+    sources as the one-GPU bench.  Caller ids throughout; with a SlotPartition the flags
+    travel in its equal slots (lo, hi = the rank's caller range)."""
+    width = part.slot if part is not None else hi - lo
+    has = np.zeros(width, np.uint8)
     for x in (src, dst):
         x = np.asarray(x)
         has[x[(x >= lo) & (x < hi)] - lo] = 1
     loc = torch.from_numpy(has).to(device)
-    out = torch.empty(n_global, dtype=torch.uint8, device=device)
+    out = torch.empty(width * _comm(comm, group).world, dtype=torch.uint8, device=device)
     _comm(comm, group).all_gather_into_tensor(out, loc)
     has = out.cpu().numpy()
+    if part is not None:
+        has = np.concatenate([has[r * part.slot:r * part.slot + (part.bounds[r + 1] - part.bounds[r])]
+                              for r in range(part.world)])
     if int(has.sum()) < nroots:
         raise ValueError("fewer vertices with entries than roots")
     roots, used, i = [], set(), 0
