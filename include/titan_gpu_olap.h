@@ -280,6 +280,15 @@ int64_t tgo_num_vertices(const tgo_ctx* ctx);
 /* Titan vertex id of every dense index, in row order (n entries). */
 int  tgo_vertex_ids(tgo_ctx* ctx, int64_t* titan_ids_out);
 
+/* Inspection of the assembled device graph (tests: device vs host assembly, array for
+ * array).  which: 0 = OUT lists, 1 = IN lists, 2 = the push transpose (absent: *nnz = -1).
+ * Internal (degree-grouped) ids.  *nnz = entries; off (n+1), adj, w, col (nnz each) are
+ * filled when non-NULL (w / col only if the load kept them).  tgo_graph_perm: row-order
+ * dense id -> internal id (n).  A load assembles on the device unless TGO_HOST_ASSEMBLY=1
+ * (edge lists; rows keep the host assembly), latched per load. */
+int  tgo_graph_csr(tgo_ctx* ctx, int32_t which, int64_t* nnz, int64_t* off, int32_t* adj, int32_t* w, uint32_t* col);
+int  tgo_graph_perm(tgo_ctx* ctx, int32_t* perm);
+
 /* BFS / k-hop: ShortestDistance with unit edge function.  dist_out may be NULL: the
  * result then stays on the device (tgo_copy_distances fetches it). */
 int  tgo_bfs(tgo_ctx* ctx, const tgo_bfs_args* args, int64_t* dist_out);

@@ -807,7 +807,10 @@ int tgo_load_edges(tgo_ctx* ctx, const tgo_edges* edges, const tgo_load_opts* op
     const auto t0 = std::chrono::steady_clock::now();
     HostGraph h;
     std::string err;
-    int rc = assemble_from_edges(edges, opts, ctx->opts.hard_query_limit, h, threads_of(ctx), err);
+    // device assembly (assemble.hip) unless TGO_HOST_ASSEMBLY=1; the host path for > 2^31 edges
+    const bool on_dev = env_i64("TGO_HOST_ASSEMBLY", 0) == 0 && edges->m < (int64_t(1) << 31);
+    int rc = on_dev ? assemble_edges_device(edges, opts, ctx->opts.hard_query_limit, h, ctx->stream, err)
+                    : assemble_from_edges(edges, opts, ctx->opts.hard_query_limit, h, threads_of(ctx), err);
     if (rc) return fail(ctx, rc, err);
     free_graph(ctx);
     ctx->staging = RowStaging();
@@ -822,6 +825,29 @@ int tgo_vertex_ids(tgo_ctx* ctx, int64_t* out) {
     if (!ctx || !out) return TGO_E_INVALID;
     if (!ctx->loaded) return fail(ctx, TGO_E_STATE, "no graph loaded");
     std::memcpy(out, ctx->titan_id.data(), ctx->titan_id.size() * sizeof(int64_t));
+    return TGO_OK;
+}
+
+int tgo_graph_csr(tgo_ctx* ctx, int32_t which, int64_t* nnz, int64_t* off, int32_t* adj, int32_t* w, uint32_t* col) {
+    if (!ctx || !nnz || which < 0 || which > 2) return TGO_E_INVALID;
+    if (!ctx->loaded) return fail(ctx, TGO_E_STATE, "no graph loaded");
+    const DevGraph& g = ctx->g;
+    if (which == 2 && !g.has_transpose) { *nnz = -1; return TGO_OK; }
+    const DevCsr& c = which == 0 ? g.out : which == 1 ? g.in : g.push_t;
+    *nnz = c.nnz;
+    (void)hipSetDevice(ctx->opts.device);
+    if (off) HIP_TRY(hipMemcpy(off, c.off, (g.n + 1) * sizeof(int64_t), hipMemcpyDeviceToHost));
+    if (adj && c.nnz) HIP_TRY(hipMemcpy(adj, c.adj, c.nnz * sizeof(int32_t), hipMemcpyDeviceToHost));
+    if (w && c.w && c.nnz) HIP_TRY(hipMemcpy(w, c.w, c.nnz * sizeof(int32_t), hipMemcpyDeviceToHost));
+    if (col && c.col && c.nnz) HIP_TRY(hipMemcpy(col, c.col, c.nnz * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    return TGO_OK;
+}
+
+int tgo_graph_perm(tgo_ctx* ctx, int32_t* perm) {
+    if (!ctx || !perm) return TGO_E_INVALID;
+    if (!ctx->loaded) return fail(ctx, TGO_E_STATE, "no graph loaded");
+    (void)hipSetDevice(ctx->opts.device);
+    HIP_TRY(hipMemcpy(perm, ctx->g.perm, ctx->g.n * sizeof(int32_t), hipMemcpyDeviceToHost));
     return TGO_OK;
 }
 

@@ -1,0 +1,454 @@
+// assemble.hip — CSR assembly of an edge-list load on the device (tgo_load_edges).
+//
+// The same graph as the host path (graph_build.cpp assemble_from_edges), array for array:
+// every directed edge u->v is an OUT entry of row u and an IN entry of row v
+// (StandardTitanGraph.java:564-591); a row's entries are in column order (direction, other
+// Titan id, relation id — IDHandler / EdgeSerializer.java:255-259), which for dense ids in
+// row order is (neighbour, edge index); the untyped single-direction scopes cut each row at
+// the QueryContainer limit in that order (QueryContainer.java:28,122 and
+// BasicVertexCentricQueryBuilder.java:418-431); then the degree-grouped relabel (DBG) and,
+// when the cut made the lists asymmetric, the explicit push transpose.  Each of those steps
+// is one stable LSD radix sort over 64-bit (row << b | neighbour) keys, which keeps the edge
+// order among equal keys — exactly the host path's (neighbour, edge index) tie order:
+//   [cap or column order]  sort 1 by (row, neighbour) from edge order; row offsets by
+//                          binary search; keep flags + scan = the cut; column positions
+//   relabel                degrees -> half-octave buckets -> order (sort of n keys)
+//   final lists            sort 2 by (perm[row], perm[neighbour]) from the sort-1 order
+//                          (or edge order): = the host's stable per-row re-sort by the new ids
+//   transpose              sort by (target, source) from row order
+// Weights / column positions ride along as a 32-bit payload (an index into the previous
+// order) and are gathered once at the end.
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include <hip/hip_runtime.h>
+#include <rocprim/rocprim.hpp>
+
+#include "engine.hpp"
+
+namespace tgo {
+namespace {
+
+constexpr int kB = 256;
+
+inline unsigned grid(int64_t work) {
+    int64_t g = (work + kB - 1) / kB;
+    return static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(g, 65536)));
+}
+
+template <class T>
+struct ScopedBuf {                      // scoped device buffer
+    T* p = nullptr;
+    size_t n = 0;
+    hipError_t alloc(size_t count) {
+        release();
+        n = count;
+        return hipMalloc(&p, std::max<size_t>(count, 1) * sizeof(T));
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    ~ScopedBuf() { release(); }
+};
+
+#define AS_TRY(x)                                            \
+    do {                                                     \
+        hipError_t e_ = (x);                                 \
+        if (e_ != hipSuccess) {                              \
+            err = std::string("device assembly: ") + hipGetErrorString(e_); \
+            return TGO_E_HIP;                                \
+        }                                                    \
+    } while (0)
+
+__global__ void range_check(const int32_t* __restrict__ src, const int32_t* __restrict__ dst, int64_t m, int64_t n,
+                            int* bad) {
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x)
+        if (src[k] < 0 || src[k] >= n || dst[k] < 0 || dst[k] >= n) atomicOr(bad, 1);
+}
+
+// key = own << b | nbr (or through perm), val = edge index
+__global__ void edge_keys(const int32_t* __restrict__ own, const int32_t* __restrict__ nbr, int64_t m, int b,
+                          const int32_t* __restrict__ perm, uint64_t* __restrict__ key, uint32_t* __restrict__ val) {
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x) {
+        uint64_t o = static_cast<uint32_t>(own[k]), x = static_cast<uint32_t>(nbr[k]);
+        if (perm) { o = static_cast<uint32_t>(perm[o]); x = static_cast<uint32_t>(perm[x]); }
+        key[k] = (o << b) | x;
+        if (val) val[k] = static_cast<uint32_t>(k);
+    }
+}
+
+// off[v] = first position of row v in keys sorted by row (binary search), v in [0, n]
+__global__ void row_offsets(const uint64_t* __restrict__ key, int64_t m, int b, int64_t n, int64_t* __restrict__ off) {
+    for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v <= n; v += (int64_t)gridDim.x * blockDim.x) {
+        int64_t lo = 0, hi = m;
+        const uint64_t t = static_cast<uint64_t>(v) << b;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (key[mid] < t) lo = mid + 1; else hi = mid;
+        }
+        off[v] = lo;
+    }
+}
+
+// Degrees of an uncut load: one atomic per entry end (hub contention is bounded by degree).
+__global__ void degree_count(const int32_t* __restrict__ src, const int32_t* __restrict__ dst, int64_t m,
+                             uint32_t* __restrict__ deg) {
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x) {
+        atomicAdd(&deg[src[k]], 1u);
+        atomicAdd(&deg[dst[k]], 1u);
+    }
+}
+
+// Per row: kept OUT / IN counts under the limit (the first `limit` entries of [OUT... | IN...]),
+// truncated rows counted (a + b >= limit: the slice came back full, VertexJobConverter.java:125).
+__global__ void cap_rows(const int64_t* __restrict__ oo, const int64_t* __restrict__ oi, int64_t n, int64_t limit,
+                         int64_t* __restrict__ ko, int64_t* __restrict__ ki, uint32_t* __restrict__ deg,
+                         unsigned long long* __restrict__ truncated) {
+    unsigned long long t = 0;
+    for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t a = oo[v + 1] - oo[v], b = oi[v + 1] - oi[v];
+        if (a + b >= limit) ++t;
+        const int64_t ka = min(a, limit);
+        const int64_t kb = min(b, limit - ka);
+        ko[v] = ka;
+        ki[v] = kb;
+        deg[v] = static_cast<uint32_t>(ka + kb);
+    }
+    if (t) atomicAdd(truncated, t);
+}
+
+// Keep flag of every sorted entry (position j < kept count of its row) and its column
+// position in the Titan row (OUT entries first: col = j; IN entries: col = kept OUT + j).
+__global__ void keep_flags(const uint64_t* __restrict__ key, int64_t m, int b, const int64_t* __restrict__ off,
+                           const int64_t* __restrict__ kept, const int64_t* __restrict__ col_base,
+                           uint32_t* __restrict__ flag, uint32_t* __restrict__ col) {
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t v = static_cast<int64_t>(key[k] >> b);
+        const int64_t j = k - off[v];
+        flag[k] = j < kept[v] ? 1u : 0u;
+        if (col) col[k] = static_cast<uint32_t>((col_base ? col_base[v] : 0) + j);
+    }
+}
+
+// Compact the kept entries: key through perm, payload = kept index's sort-1 position.
+__global__ void compact_kept(const uint64_t* __restrict__ key, const uint32_t* __restrict__ flag,
+                             const uint64_t* __restrict__ pos, int64_t m, int b, const int32_t* __restrict__ perm,
+                             uint64_t* __restrict__ okey, uint32_t* __restrict__ oval) {
+    const uint64_t mask = (uint64_t(1) << b) - 1;
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x) {
+        if (!flag[k]) continue;
+        const uint64_t p = pos[k];
+        uint64_t o = key[k] >> b, x = key[k] & mask;
+        if (perm) { o = static_cast<uint32_t>(perm[o]); x = static_cast<uint32_t>(perm[x]); }
+        okey[p] = (o << b) | x;
+        oval[p] = static_cast<uint32_t>(k);
+    }
+}
+
+// Re-key through perm (sort 2 input), payload = the entry's index.
+__global__ void rekey(const uint64_t* __restrict__ key, int64_t m, int b, const int32_t* __restrict__ perm,
+                      uint64_t* __restrict__ okey, uint32_t* __restrict__ oval) {
+    const uint64_t mask = (uint64_t(1) << b) - 1;
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t o = static_cast<uint32_t>(perm[key[k] >> b]), x = static_cast<uint32_t>(perm[key[k] & mask]);
+        okey[k] = (o << b) | x;
+        if (oval) oval[k] = static_cast<uint32_t>(k);
+    }
+}
+
+// Half-octave bucket of a degree (graph_build.cpp degree_group_order: 1 + floor(2 log2 d),
+// 0 for d = 0) in integer arithmetic: floor(log2(d^2)).  Sort key: hottest bucket first,
+// row order inside a bucket.
+__global__ void bucket_keys(const uint32_t* __restrict__ deg, int64_t n, uint64_t* __restrict__ key) {
+    for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t d = deg[v];
+        const int bk = d == 0 ? 0 : 1 + (63 - __clzll(static_cast<long long>(d * d)));
+        key[v] = (static_cast<uint64_t>(127 - bk) << 32) | static_cast<uint64_t>(v);
+    }
+}
+__global__ void order_to_perm(const uint64_t* __restrict__ sorted, int64_t n, int32_t* __restrict__ perm) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        perm[static_cast<uint32_t>(sorted[i])] = static_cast<int32_t>(i);
+}
+
+// Final list: neighbour ids, weights / column positions gathered through the payload chain.
+__global__ void emit_list(const uint64_t* __restrict__ key, const uint32_t* __restrict__ val, int64_t m, int b,
+                          const uint32_t* __restrict__ edge_of, const int32_t* __restrict__ weight,
+                          const uint32_t* __restrict__ col_in, int32_t* __restrict__ adj, int32_t* __restrict__ w,
+                          uint32_t* __restrict__ col) {
+    const uint64_t mask = (uint64_t(1) << b) - 1;
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x) {
+        adj[k] = static_cast<int32_t>(key[k] & mask);
+        if (val) {
+            const uint32_t p = val[k];
+            if (w) w[k] = weight[edge_of ? edge_of[p] : p];
+            if (col) col[k] = col_in[p];
+        }
+    }
+}
+
+// Transpose keys: entry k of row v (key = v << b | t) -> t << b | v, payload k.
+__global__ void transpose_keys(const uint64_t* __restrict__ key, int64_t m, int b, uint64_t* __restrict__ tkey,
+                               uint32_t* __restrict__ tval) {
+    const uint64_t mask = (uint64_t(1) << b) - 1;
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x) {
+        tkey[k] = ((key[k] & mask) << b) | (key[k] >> b);
+        if (tval) tval[k] = static_cast<uint32_t>(k);
+    }
+}
+__global__ void gather_i32(const uint32_t* __restrict__ idx, const int32_t* __restrict__ in, int64_t m,
+                           int32_t* __restrict__ out) {
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x)
+        out[k] = in[idx[k]];
+}
+
+struct Sorter {
+    ScopedBuf<uint8_t> tmp;
+    hipStream_t s;
+    hipError_t pairs(const uint64_t* ki, uint64_t* ko, const uint32_t* vi, uint32_t* vo, int64_t m, int bits) {
+        size_t need = 0;
+        hipError_t e = rocprim::radix_sort_pairs(nullptr, need, ki, ko, vi, vo, static_cast<size_t>(m), 0, bits, s);
+        if (e != hipSuccess) return e;
+        if (need > tmp.n && (e = tmp.alloc(need)) != hipSuccess) return e;
+        return rocprim::radix_sort_pairs(tmp.p, need, ki, ko, vi, vo, static_cast<size_t>(m), 0, bits, s);
+    }
+    hipError_t keys(const uint64_t* ki, uint64_t* ko, int64_t m, int bits) {
+        size_t need = 0;
+        hipError_t e = rocprim::radix_sort_keys(nullptr, need, ki, ko, static_cast<size_t>(m), 0, bits, s);
+        if (e != hipSuccess) return e;
+        if (need > tmp.n && (e = tmp.alloc(need)) != hipSuccess) return e;
+        return rocprim::radix_sort_keys(tmp.p, need, ki, ko, static_cast<size_t>(m), 0, bits, s);
+    }
+    hipError_t excl_scan(const uint32_t* in, uint64_t* out, int64_t m) {
+        size_t need = 0;
+        hipError_t e = rocprim::exclusive_scan(nullptr, need, in, out, uint64_t(0), static_cast<size_t>(m),
+                                               rocprim::plus<uint64_t>(), s);
+        if (e != hipSuccess) return e;
+        if (need > tmp.n && (e = tmp.alloc(need)) != hipSuccess) return e;
+        return rocprim::exclusive_scan(tmp.p, need, in, out, uint64_t(0), static_cast<size_t>(m),
+                                       rocprim::plus<uint64_t>(), s);
+    }
+};
+
+template <class T>
+hipError_t download(std::vector<T>& h, const T* d, int64_t count, hipStream_t s) {
+    h.resize(static_cast<size_t>(count));
+    if (count == 0) return hipSuccess;
+    return hipMemcpyAsync(h.data(), d, static_cast<size_t>(count) * sizeof(T), hipMemcpyDeviceToHost, s);
+}
+
+}  // namespace
+
+int assemble_edges_device(const tgo_edges* e, const tgo_load_opts* opts, int64_t hard_limit, HostGraph& g,
+                          hipStream_t s, std::string& err) {
+    g = HostGraph();
+    const int64_t n = e->n, m = e->m;
+    if (n <= 0 || n >= INT32_MAX) { err = "vertex count out of range"; return TGO_E_INVALID; }
+    if (m >= (int64_t(1) << 32)) { err = "more than 2^32 edges per load"; return TGO_E_UNSUPPORTED; }
+    g.n = n;
+    g.scope = opts->scope;
+    g.has_weight = opts->weight_key != 0 && e->weight != nullptr;
+    g.weight_dt = TGO_DT_INTEGER;
+    const bool keep_col = (opts->flags & TGO_LOAD_COLUMN_ORDER) != 0;
+    g.titan_id.resize(n);
+    for (int64_t v = 0; v < n; ++v) g.titan_id[v] = e->titan_ids ? e->titan_ids[v] : ((v + 1) << 3);
+    for (int64_t v = 1; e->titan_ids && v < n; ++v)
+        if (e->titan_ids[v] <= e->titan_ids[v - 1]) { err = "titan_ids must be strictly increasing"; return TGO_E_INVALID; }
+    const bool cap = opts->apply_cap && opts->n_labels == 0 && opts->scope != TGO_SCOPE_BOTH_E;
+    const int64_t limit = cap ? hard_limit : INT64_MAX;
+    const bool sort1 = cap || keep_col;          // the cut / column positions need column order first
+    int b = 1;
+    while ((int64_t(1) << b) < n) ++b;
+    const int bits = 2 * b;
+
+    ScopedBuf<int32_t> d_src, d_dst, d_w;
+    AS_TRY(d_src.alloc(m));
+    AS_TRY(d_dst.alloc(m));
+    if (m) {
+        AS_TRY(hipMemcpyAsync(d_src.p, e->src, m * sizeof(int32_t), hipMemcpyHostToDevice, s));
+        AS_TRY(hipMemcpyAsync(d_dst.p, e->dst, m * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    }
+    if (g.has_weight) {
+        AS_TRY(d_w.alloc(m));
+        if (m) AS_TRY(hipMemcpyAsync(d_w.p, e->weight, m * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    }
+    {
+        ScopedBuf<int> bad;
+        AS_TRY(bad.alloc(1));
+        AS_TRY(hipMemsetAsync(bad.p, 0, sizeof(int), s));
+        if (m) range_check<<<grid(m), kB, 0, s>>>(d_src.p, d_dst.p, m, n, bad.p);
+        int hb = 0;
+        AS_TRY(hipMemcpyAsync(&hb, bad.p, sizeof(int), hipMemcpyDeviceToHost, s));
+        AS_TRY(hipStreamSynchronize(s));
+        if (hb) { err = "edge endpoint out of range"; return TGO_E_INVALID; }
+    }
+    Sorter so{{}, s};
+    ScopedBuf<uint32_t> deg;
+    AS_TRY(deg.alloc(n));
+    // ---- sort 1 (column order) + cut, per direction: kept entries' sort-1 keys and payloads
+    struct Dir { ScopedBuf<uint64_t> key; ScopedBuf<uint32_t> edge, col; int64_t count = 0; };
+    Dir dir[2];                 // [0] OUT (rows = src), [1] IN (rows = dst)
+    unsigned long long truncated = 0;
+    if (sort1) {
+        ScopedBuf<uint64_t> k1[2];
+        ScopedBuf<uint32_t> v1[2];
+        ScopedBuf<int64_t> off[2], kept[2];
+        for (int d = 0; d < 2; ++d) {
+            ScopedBuf<uint64_t> kt;
+            ScopedBuf<uint32_t> vt;
+            AS_TRY(kt.alloc(m));
+            AS_TRY(vt.alloc(m));
+            AS_TRY(k1[d].alloc(m));
+            AS_TRY(v1[d].alloc(m));
+            if (m) edge_keys<<<grid(m), kB, 0, s>>>(d == 0 ? d_src.p : d_dst.p, d == 0 ? d_dst.p : d_src.p, m, b, nullptr,
+                                                    kt.p, vt.p);
+            if (m) AS_TRY(so.pairs(kt.p, k1[d].p, vt.p, v1[d].p, m, bits));
+            AS_TRY(off[d].alloc(n + 1));
+            row_offsets<<<grid(n + 1), kB, 0, s>>>(k1[d].p, m, b, n, off[d].p);
+            AS_TRY(kept[d].alloc(n));
+        }
+        ScopedBuf<unsigned long long> tr;
+        AS_TRY(tr.alloc(1));
+        AS_TRY(hipMemsetAsync(tr.p, 0, sizeof(unsigned long long), s));
+        cap_rows<<<grid(n), kB, 0, s>>>(off[0].p, off[1].p, n, limit, kept[0].p, kept[1].p, deg.p, tr.p);
+        AS_TRY(hipMemcpyAsync(&truncated, tr.p, sizeof(truncated), hipMemcpyDeviceToHost, s));
+        for (int d = 0; d < 2; ++d) {
+            ScopedBuf<uint32_t> flag, colfull;
+            ScopedBuf<uint64_t> pos;
+            AS_TRY(flag.alloc(m));
+            AS_TRY(pos.alloc(m + 1));
+            if (keep_col) AS_TRY(colfull.alloc(m));
+            if (m) keep_flags<<<grid(m), kB, 0, s>>>(k1[d].p, m, b, off[d].p, kept[d].p, d == 1 ? kept[0].p : nullptr,
+                                                     flag.p, keep_col ? colfull.p : nullptr);
+            AS_TRY(so.excl_scan(flag.p, pos.p, m));
+            uint64_t cnt = 0;
+            uint32_t lastf = 0;
+            if (m) {
+                AS_TRY(hipMemcpyAsync(&cnt, pos.p + m - 1, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+                AS_TRY(hipMemcpyAsync(&lastf, flag.p + m - 1, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+            }
+            AS_TRY(hipStreamSynchronize(s));
+            const int64_t kc = static_cast<int64_t>(cnt + lastf);
+            dir[d].count = kc;
+            // kept entries: sort-1 keys (original ids), edge index, column position
+            AS_TRY(dir[d].key.alloc(kc));
+            AS_TRY(dir[d].edge.alloc(kc));
+            if (keep_col) AS_TRY(dir[d].col.alloc(kc));
+            ScopedBuf<uint32_t> sel;                           // sort-1 position of each kept entry
+            AS_TRY(sel.alloc(kc));
+            if (m) compact_kept<<<grid(m), kB, 0, s>>>(k1[d].p, flag.p, pos.p, m, b, nullptr, dir[d].key.p, sel.p);
+            if (kc) {
+                gather_i32<<<grid(kc), kB, 0, s>>>(sel.p, reinterpret_cast<const int32_t*>(v1[d].p), kc,
+                                                   reinterpret_cast<int32_t*>(dir[d].edge.p));
+                if (keep_col)
+                    gather_i32<<<grid(kc), kB, 0, s>>>(sel.p, reinterpret_cast<const int32_t*>(colfull.p), kc,
+                                                       reinterpret_cast<int32_t*>(dir[d].col.p));
+            }
+            AS_TRY(hipStreamSynchronize(s));             // the scoped buffers are freed next
+        }
+    } else {
+        AS_TRY(hipMemsetAsync(deg.p, 0, n * sizeof(uint32_t), s));
+        if (m) degree_count<<<grid(m), kB, 0, s>>>(d_src.p, d_dst.p, m, deg.p);
+        for (int d = 0; d < 2; ++d) dir[d].count = m;
+    }
+    g.truncated = static_cast<int64_t>(truncated);
+    // ---- degree-grouped relabel: perm[v] = position of v (hottest half-octave first)
+    ScopedBuf<int32_t> perm;
+    AS_TRY(perm.alloc(n));
+    {
+        ScopedBuf<uint64_t> bk, bs;
+        AS_TRY(bk.alloc(n));
+        AS_TRY(bs.alloc(n));
+        bucket_keys<<<grid(n), kB, 0, s>>>(deg.p, n, bk.p);
+        AS_TRY(so.keys(bk.p, bs.p, n, 32 + 7));
+        order_to_perm<<<grid(n), kB, 0, s>>>(bs.p, n, perm.p);
+    }
+    deg.release();
+    // ---- sort 2: final lists in (perm[row], perm[neighbour]) order
+    HostCsr* outc[2] = {&g.out, &g.in};
+    ScopedBuf<uint64_t> fkey[2];                    // final keys (kept for the transpose)
+    ScopedBuf<int32_t> fadj[2], fw[2];
+    for (int d = 0; d < 2; ++d) {
+        const int64_t c = dir[d].count;
+        ScopedBuf<uint64_t> kt;
+        ScopedBuf<uint32_t> vt, vs;
+        AS_TRY(kt.alloc(c));
+        AS_TRY(fkey[d].alloc(c));
+        const bool payload = g.has_weight || keep_col;
+        if (sort1) {
+            // re-key the kept sort-1 entries through perm, payload = their kept index
+            AS_TRY(vt.alloc(payload ? c : 0));
+            if (c) rekey<<<grid(c), kB, 0, s>>>(dir[d].key.p, c, b, perm.p, kt.p, payload ? vt.p : nullptr);
+            dir[d].key.release();
+        } else {
+            AS_TRY(vt.alloc(payload ? c : 0));
+            if (c) edge_keys<<<grid(c), kB, 0, s>>>(d == 0 ? d_src.p : d_dst.p, d == 0 ? d_dst.p : d_src.p, c, b, perm.p,
+                                                    kt.p, payload ? vt.p : nullptr);
+        }
+        if (payload) {
+            AS_TRY(vs.alloc(c));
+            if (c) AS_TRY(so.pairs(kt.p, fkey[d].p, vt.p, vs.p, c, bits));
+        } else if (c) {
+            AS_TRY(so.keys(kt.p, fkey[d].p, c, bits));
+        }
+        kt.release();
+        HostCsr& hc = *outc[d];
+        ScopedBuf<int64_t> off;
+        AS_TRY(off.alloc(n + 1));
+        row_offsets<<<grid(n + 1), kB, 0, s>>>(fkey[d].p, c, b, n, off.p);
+        AS_TRY(fadj[d].alloc(c));
+        ScopedBuf<uint32_t> col;
+        if (g.has_weight) AS_TRY(fw[d].alloc(c));
+        if (keep_col) AS_TRY(col.alloc(c));
+        if (c)
+            emit_list<<<grid(c), kB, 0, s>>>(fkey[d].p, payload ? vs.p : nullptr, c, b,
+                                             sort1 ? dir[d].edge.p : nullptr, d_w.p, sort1 ? dir[d].col.p : nullptr,
+                                             fadj[d].p, g.has_weight ? fw[d].p : nullptr, keep_col ? col.p : nullptr);
+        AS_TRY(download(hc.off, off.p, n + 1, s));
+        AS_TRY(download(hc.adj, fadj[d].p, c, s));
+        if (g.has_weight) AS_TRY(download(hc.w, fw[d].p, c, s));
+        if (keep_col) AS_TRY(download(hc.col, col.p, c, s));
+        AS_TRY(hipStreamSynchronize(s));
+        dir[d].edge.release();
+        dir[d].col.release();
+    }
+    AS_TRY(download(g.perm, perm.p, n, s));
+    // ---- push view: equal to the stored opposite list unless the cut made rows asymmetric
+    g.has_transpose = g.truncated != 0;
+    if (g.has_transpose && g.scope != TGO_SCOPE_BOTH_E) {
+        const int d = g.scope == TGO_SCOPE_IN_E ? 0 : 1;      // pull list of inE = OUT rows, outE = IN rows
+        const int64_t c = static_cast<int64_t>(g.scope == TGO_SCOPE_IN_E ? g.out.adj.size() : g.in.adj.size());
+        ScopedBuf<uint64_t> tk, ts;
+        ScopedBuf<uint32_t> tv, tvs;
+        AS_TRY(tk.alloc(c));
+        AS_TRY(ts.alloc(c));
+        AS_TRY(tv.alloc(g.has_weight ? c : 0));
+        if (c) transpose_keys<<<grid(c), kB, 0, s>>>(fkey[d].p, c, b, tk.p, g.has_weight ? tv.p : nullptr);
+        if (g.has_weight) {
+            AS_TRY(tvs.alloc(c));
+            if (c) AS_TRY(so.pairs(tk.p, ts.p, tv.p, tvs.p, c, bits));
+        } else if (c) {
+            AS_TRY(so.keys(tk.p, ts.p, c, bits));
+        }
+        ScopedBuf<int64_t> off;
+        AS_TRY(off.alloc(n + 1));
+        row_offsets<<<grid(n + 1), kB, 0, s>>>(ts.p, c, b, n, off.p);
+        ScopedBuf<int32_t> adj, w;
+        AS_TRY(adj.alloc(c));
+        if (g.has_weight) AS_TRY(w.alloc(c));
+        if (c) emit_list<<<grid(c), kB, 0, s>>>(ts.p, g.has_weight ? tvs.p : nullptr, c, b, nullptr, fw[d].p, nullptr,
+                                                adj.p, g.has_weight ? w.p : nullptr, nullptr);
+        AS_TRY(download(g.push_t.off, off.p, n + 1, s));
+        AS_TRY(download(g.push_t.adj, adj.p, c, s));
+        if (g.has_weight) AS_TRY(download(g.push_t.w, w.p, c, s));
+    }
+    AS_TRY(hipStreamSynchronize(s));
+    return TGO_OK;
+}
+
+}  // namespace tgo

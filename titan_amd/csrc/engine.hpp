@@ -162,6 +162,10 @@ int decode_rows(RowStaging& st, const tgo_rows* rows, const tgo_schema* schema,
 int assemble_from_rows(RowStaging& st, HostGraph& g, int threads, std::string& err);
 int assemble_from_edges(const tgo_edges* e, const tgo_load_opts* opts, int64_t hard_limit,
                         HostGraph& g, int threads, std::string& err);
+// The same graph assembled on the device (assemble.hip): radix sorts instead of the host
+// counting sorts; m < 2^31.
+int assemble_edges_device(const tgo_edges* e, const tgo_load_opts* opts, int64_t hard_limit, HostGraph& g,
+                          hipStream_t s, std::string& err);
 int partition_layout(const tgo_edges* e, int64_t n_global, int64_t lo, int64_t hi, int threads,
                      int32_t* layout_local, std::string& err);
 int assemble_partition(const tgo_edges* e, int64_t n_global, int64_t lo, int64_t hi,

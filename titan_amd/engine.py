@@ -172,6 +172,27 @@ class Engine:
         _check(self.lib, self.ctx, self.lib.tgo_vertex_ids(self.ctx, L.ptr(out, C.c_int64)))
         return out
 
+    def graph_csr(self, which):
+        """The assembled device lists (which: 0 OUT, 1 IN, 2 push transpose) in internal ids:
+        dict(off, adj, w, col) with w / col None when the load has none; None if absent."""
+        nnz = C.c_int64()
+        _check(self.lib, self.ctx, self.lib.tgo_graph_csr(self.ctx, which, C.byref(nnz), None, None, None, None))
+        if nnz.value < 0:
+            return None
+        off = np.zeros(self.n + 1, np.int64)
+        adj = np.zeros(nnz.value, np.int32)
+        w = np.full(nnz.value, -7, np.int32)
+        col = np.full(nnz.value, 0xFFFFFFFF, np.uint32)
+        _check(self.lib, self.ctx, self.lib.tgo_graph_csr(self.ctx, which, C.byref(nnz), L.ptr(off, C.c_int64),
+                                                          L.ptr(adj, C.c_int32), L.ptr(w, C.c_int32),
+                                                          L.ptr(col, C.c_uint32)))
+        return {"off": off, "adj": adj, "w": w, "col": col}
+
+    def graph_perm(self):
+        out = np.zeros(self.n, np.int32)
+        _check(self.lib, self.ctx, self.lib.tgo_graph_perm(self.ctx, L.ptr(out, C.c_int32)))
+        return out
+
     # ------------------------------------------------------------------ programs
     def bfs(self, seed, max_depth, scope, seed_is_dense=False, stats=False, fetch=True):
         a = L.BfsArgs(int(seed), 1 if seed_is_dense else 0, int(max_depth), scope, L.FLAG_STATS if stats else 0)
