@@ -70,6 +70,9 @@ def parse():
                    help="partitioned path: degree-grouped device layout (tgo_part_layout); 0 = global ids as given")
     p.add_argument("--partitioned", action="store_true",
                    help="use the vertex-partitioned multi-GPU path even at N=1 (for testing it on one GPU)")
+    p.add_argument("--native", type=int, default=1,
+                   help="partitioned path: the multi-source sweep as one native call over RCCL (tgo_part_msbfs_run); "
+                        "0 = the Python level driver")
     p.add_argument("--balanced", type=int, default=1,
                    help="partitioned path: edge-balanced ranges (entries + vertices, SlotPartition); 0 = equal ranges")
     return p.parse_args()
@@ -333,8 +336,9 @@ def run_partitioned(args, world, rank, local_rank):
     import torch.distributed as dist
     from titan_amd import Engine
     from titan_amd import _lib as L
-    from titan_amd.distributed import (HipPartBackend, SlotPartition, all_gather_layout, balanced_partition,
-                                       distributed_bfs, distributed_msbfs, distributed_pagerank, entry_imbalance,
+    from titan_amd.distributed import (HipPartBackend, NativeExchange, SlotPartition, all_gather_layout,
+                                       balanced_partition, distributed_bfs, distributed_msbfs,
+                                       distributed_msbfs_native, distributed_pagerank, entry_imbalance,
                                        exchange_stream, pagerank_layout, partition_range, pick_roots_partitioned,
                                        word_weights)
     torch.cuda.set_device(local_rank)
@@ -399,8 +403,16 @@ def run_partitioned(args, world, rank, local_rank):
     # per-rank owned entries of the bothE graph: the partition's load imbalance (max / mean)
     ent = bfs_be.e.stats()
     rank_entries, imbalance = entry_imbalance(int(ent["out_entries"] + ent["in_entries"]), dev)
+    # the sweep: one native call whose level loop issues RCCL collectives on the engine stream
+    # (tgo_part_msbfs_run), or the Python level driver
+    xchg = NativeExchange.rccl(local_rank) if args.native else None
+
+    def sweep(stats):
+        if xchg is not None:
+            return distributed_msbfs_native(bfs_be, roots_s, ns, xchg)
+        return distributed_msbfs(bfs_be, roots_s, ns, stats=stats)
     # per-root reached entries (untimed) for GTEPS
-    _, mR, depth_ms = distributed_msbfs(bfs_be, roots_s, ns, stats=True)
+    _, mR, depth_ms = sweep(True)
     # single-source side measurement (untimed, every root, Graph500 style harmonic mean)
     ss_t = []
     distributed_bfs(bfs_be, roots_s[0], ns, fetch=False, stats=False)
@@ -414,7 +426,7 @@ def run_partitioned(args, world, rank, local_rank):
 
     def step():
         t = time.perf_counter()
-        distributed_msbfs(bfs_be, roots_s, ns, stats=False)
+        sweep(False)
         torch.cuda.synchronize()
         bt = time.perf_counter() - t
         t = time.perf_counter()
@@ -460,6 +472,8 @@ def run_partitioned(args, world, rank, local_rank):
         line = result_line(args, world, scale, n, m, roots, elapsed, teps, hmean, pr_wall / upd, e_in,
                            roof_bfs, roof_pr, bfs_share, None, f"vertex-partition{world}")
         line["config"]["device_layout"] = "degree-grouped per rank" if args.layout else "global ids"
+        line["config"]["msbfs_driver"] = ("native level loop, RCCL on the engine stream (tgo_part_msbfs_run)"
+                                          if args.native else "Python level driver (titan_amd/distributed.py)")
         line["pagerank_exchange"] = {"hot_rows_per_rank": pr_layout[0], "active_span": pr_layout[1],
                                      "bytes_per_rank_per_update": 8 * pr_layout[1]}
         wr = part.weights(ww)
@@ -470,6 +484,8 @@ def run_partitioned(args, world, rank, local_rank):
                              "weight_imbalance_max_over_mean": round(max(wr) / (sum(wr) / len(wr)), 4)}
         line["sssp"] = sssp
         print(json.dumps(line), file=JSON_OUT, flush=True)
+    torch.cuda.synchronize()
+    del xchg                        # the native driver's RCCL communicator, before torch's group
     dist.barrier()
     dist.destroy_process_group()
 
@@ -566,6 +582,13 @@ def cpu_baseline(args, n, src, dst, roots, mR, depth, threads, pr_s_iter_gpu=Non
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.partitioned and "RANK" not in os.environ:     # one rank without a launcher
+        import socket
+        sk = socket.socket()
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+        sk.close()
+        os.environ.update(RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     if world > 1 or args.partitioned:
         # RCCL prints its version banner on fd 1: route native stdout to stderr and keep the
         # real stdout for the single JSON result line.

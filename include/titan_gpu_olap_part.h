@@ -164,6 +164,31 @@ int tgo_part_pr_blocked(tgo_ctx* ctx, int32_t world, int64_t active_span, int64_
 int tgo_part_pr_step_cold(tgo_ctx* ctx, const double* gathered);
 int tgo_part_pr_step_hot(tgo_ctx* ctx, const double* gathered, double* contrib_local);
 
+/* The partitioned multi-source BFS sweep as ONE native call (part_driver.cpp): the protocol
+ * of titan_amd/distributed.distributed_msbfs (dense level: in-place all-gather of the owned
+ * frontier masks + tgo_part_ms_pull; sparse level: tgo_part_ms_push, then the fixed-capacity
+ * pair exchange while world * (cap + 1) * 16 <= fixed_bytes (cap = the level's global frontier
+ * entries, at most n_local), else sized pairs (one all-to-all of the split sizes, one of the
+ * pairs); level counts all-reduced on the device) run as a C++ loop whose collectives go
+ * through an exchange object on the ctx stream, without a Python step per level.
+ *   tgo_exchange_rccl_id / _create : RCCL over xGMI (one process per GPU; rank 0 makes the
+ *                                    128-byte id, the caller broadcasts it, every rank creates)
+ *   tgo_exchange_local_group       : `world` ranks as threads of ONE process (tests on one
+ *                                    device): collectives are device copies at a barrier; a
+ *                                    rank that fails releases the others (60 s barrier limit)
+ * The exchange's world / rank must match the partition (world * n_local == n_global, lo ==
+ * rank * n_local).  reached / entries: per seed, global (NULL to skip); *levels = levels run.
+ * The per-source levels are read with tgo_part_ms_levels afterwards, as after the Python
+ * driver.  The ctx's device-counts setting (tgo_part_device_counts) is restored on return. */
+typedef struct tgo_exchange tgo_exchange;
+int  tgo_exchange_rccl_id(uint8_t* id_out /* 128 bytes */);
+int  tgo_exchange_rccl_create(int32_t world, int32_t rank, const uint8_t* id, int32_t device, tgo_exchange** out);
+int  tgo_exchange_local_group(int32_t world, tgo_exchange** ranks_out /* world handles */);
+void tgo_exchange_destroy(tgo_exchange* x);
+const char* tgo_exchange_last_error(const tgo_exchange* x);
+int  tgo_part_msbfs_run(tgo_ctx* ctx, tgo_exchange* x, const int64_t* seeds, int32_t nseeds, int32_t max_depth,
+                        double ms_alpha, int64_t fixed_bytes, int64_t* reached, int64_t* entries, int32_t* levels);
+
 /* Bench / test input: the edges of an RMAT stream (tgo_synth.h) with an endpoint in
  * [lo, hi).  *count = edges written; if capacity is too small, nothing is written,
  * *count = required capacity and TGO_E_INVALID is returned. */

@@ -95,3 +95,66 @@ def test_device_assembly_rejects_bad_input(monkeypatch):
     g = e.graph_csr(1)
     assert len(g["adj"]) == 0 and np.all(g["off"] == 0)
     assert np.array_equal(np.sort(e.graph_perm()), np.arange(70))
+
+
+# ---------------------------------------------------------------- row loads (tgo_load_rows)
+def _rows_both(monkeypatch, rows, sd, scope, limit, **kw):
+    from titan_amd import Schema
+    out = []
+    for host in ("1", "0"):
+        monkeypatch.setenv("TGO_HOST_ASSEMBLY", host)
+        out.append(_snapshot(Engine(hard_query_limit=limit).load_rows(rows, Schema.from_dict(sd), scope, **kw)))
+    monkeypatch.delenv("TGO_HOST_ASSEMBLY")
+    return out
+
+
+@pytest.mark.parametrize("scope", [L.SCOPE_IN_E, L.SCOPE_OUT_E, L.SCOPE_BOTH_E])
+@pytest.mark.parametrize("cols", [False, True])
+def test_device_row_assembly_equals_host(monkeypatch, scope, cols):
+    """Edgestore rows (ghost rows, schema rows, a small cap so hub rows are cut, weights in
+    the signature): device row assembly == host assemble_from_rows, array for array."""
+    import sys
+    import os
+    sys.path.insert(0, os.path.dirname(__file__))
+    from test_gpu_decode import rmat_rows
+    rows, vids, sd, wkey, n = rmat_rows(with_w=True)
+    h, d = _rows_both(monkeypatch, rows, sd, scope, 25, weight_key=wkey, batch_rows=77, column_order=cols)
+    _same(h, d)
+    if scope != L.SCOPE_BOTH_E:
+        assert h["counters"][3] > 0
+
+
+def test_device_row_assembly_typed_scopes(monkeypatch):
+    """Typed scopes over DESC sort keys and SIMPLE labels (uncapped), weights: device == host."""
+    import random
+    import edgestore as es
+    import fulgora as fr
+    lib = fr.load()
+    knows, likes = es.user_edge_label(1), es.user_edge_label(2)
+    w, ks = lib.fr_schema_id(0, 1), lib.fr_schema_id(0, 2)
+    pkeys = [(w, 3), (ks, 10)]
+    sd = {"edge_types": [{"type_id": knows, "multiplicity": 0, "sort_key": [ks, w], "order": "DESC"},
+                         {"type_id": likes, "multiplicity": 1, "signature": [ks, w]}],
+          "property_keys": [list(p) for p in pkeys]}
+    osch = fr.OracleSchema(sd["edge_types"], pkeys)
+    rnd = random.Random(5)
+    n = 300
+    edges = [(rnd.randrange(n), rnd.randrange(n), rnd.choice([knows, likes]),
+              [(w, rnd.randint(1, 30)), (ks, rnd.choice([0, 5, -8, 1234]))]) for _ in range(4000)]
+    rows, vids = es.build_rows(es.GraphSpec(n=n, edges=edges), osch)
+    for scope in (L.SCOPE_IN_E, L.SCOPE_OUT_E):
+        for labels in ((), (knows,), (likes,)):
+            h, d = _rows_both(monkeypatch, rows, sd, scope, 20, labels=labels, weight_key=w)
+            _same(h, d)
+
+
+def test_vertex_cut_rows_keep_the_host_assembly(monkeypatch):
+    """Representative rows of vertex cuts fold on the host (graph_build.cpp): the device
+    switch must not change that load (same arrays either way)."""
+    import sys
+    import os
+    sys.path.insert(0, os.path.dirname(__file__))
+    from conftest import load_fixture
+    rows, vids, sd, npz = load_fixture("partition_groups")
+    h, d = _rows_both(monkeypatch, rows, sd, L.SCOPE_BOTH_E, 100000, batch_rows=5)
+    _same(h, d)

@@ -335,3 +335,74 @@ def test_edge_balanced_partition_drivers(world, monkeypatch):
     res = w_ranks.run(lambda be, comm: distributed_sssp(be, rs[1], 0, comm=comm))
     osd, _ = og.shortest_distance(int(ids[roots[1]]), n, L.SCOPE_IN_E, weighted=True)
     assert np.array_equal(cut(res, 0), osd)
+
+
+@pytest.mark.parametrize("world,fixed", [(1, None), (2, None), (2, 0), (4, None), (4, 0)])
+def test_native_msbfs_driver(world, fixed):
+    """tgo_part_msbfs_run: the partitioned multi-source sweep as ONE native call (C++ level
+    loop, collectives through an in-process exchange group of thread ranks on this device):
+    every seed's levels equal the oracle's, reached counts global, and the result equals the
+    Python driver's.  fixed=0 forces the sized-pairs exchange on every sparse level."""
+    from titan_amd.distributed import NativeExchange, distributed_msbfs_native
+    scale = 12
+    n = 1 << scale
+    src, dst, _ = rmat_edges(scale, 16, seed=33)
+    ranks = Ranks(world, n, src, dst, L.SCOPE_BOTH_E, layout=True, device_counts=True)
+    og = fr.OracleGraph.from_edges(n, src, dst)
+    ids = (np.arange(n, dtype=np.int64) + 1) << 3
+    rng = np.random.default_rng(9)
+    seeds = [int(s) for s in rng.choice(n, 63, replace=False)] + [int(src[0])]
+    xs = NativeExchange.local_group(world)
+
+    def body(be, comm):
+        r, e, lv = distributed_msbfs_native(be, seeds, n, xs[comm.rank], fixed_exchange_bytes=fixed)
+        return r, e, lv, [be.ms_levels(i) for i in range(len(seeds))]
+    res = ranks.run(body)
+    for i, s in enumerate(seeds):
+        od, _ = og.shortest_distance(int(ids[s]), n, 2)
+        assert np.array_equal(np.concatenate([x[3][i] for x in res]), od), i
+        assert all(x[0][i] == int((od != ABSENT).sum()) for x in res)
+    assert len({x[2] for x in res}) == 1
+    # the Python driver on the same partitions gives the same counts and levels
+    py = ranks.run(lambda be, comm: distributed_msbfs(be, seeds, n, comm=comm, fixed_exchange_bytes=fixed))
+    assert all(np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) for a, b in zip(res, py))
+    # device counts of the Python driver's backends were restored by the native call
+    res2 = ranks.run(body)
+    assert all(np.array_equal(a[0], b[0]) for a, b in zip(res, res2))
+
+
+def test_native_msbfs_rccl_world1():
+    """The RCCL exchange (one rank): unique id shared over the driver's communicator, the
+    sweep through ncclAllGather / ncclAllToAll paths, equal to the oracle."""
+    from titan_amd.distributed import NativeExchange, distributed_msbfs_native
+    scale = 11
+    n = 1 << scale
+    src, dst, _ = rmat_edges(scale, 16, seed=35)
+    st = torch.cuda.Stream()
+    with torch.cuda.stream(st):
+        be = HipPartBackend(Engine(stream=st.cuda_stream).load_partition(n, 0, n, src, dst, L.SCOPE_BOTH_E,
+                                                                         apply_cap=False), n, 0, n)
+        x = NativeExchange.rccl(0, comm=InProcessGroup(1).comm(0))
+        seeds = [int(src[0]), int(dst[1]), int(src[7])]
+        r, e, lv = distributed_msbfs_native(be, seeds, n, x)
+        og = fr.OracleGraph.from_edges(n, src, dst)
+        ids = (np.arange(n, dtype=np.int64) + 1) << 3
+        for i, s in enumerate(seeds):
+            od, _ = og.shortest_distance(int(ids[s]), n, 2)
+            assert np.array_equal(be.ms_levels(i), od)
+            assert r[i] == int((od != ABSENT).sum())
+        del x
+
+
+def test_native_msbfs_rejects_a_mismatched_exchange():
+    from titan_amd.distributed import NativeExchange, distributed_msbfs_native
+    scale = 10
+    n = 1 << scale
+    src, dst, _ = rmat_edges(scale, 16, seed=3)
+    st = torch.cuda.Stream()
+    with torch.cuda.stream(st):
+        be = HipPartBackend(Engine(stream=st.cuda_stream).load_partition(n, 0, n, src, dst, L.SCOPE_BOTH_E,
+                                                                         apply_cap=False), n, 0, n)
+        xs = NativeExchange.local_group(2)          # world 2 against a one-rank partition
+        with pytest.raises(TitanException):
+            distributed_msbfs_native(be, [int(src[0])], n, xs[0])

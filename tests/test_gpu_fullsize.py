@@ -164,3 +164,26 @@ def test_config5_rmat24_weighted_sssp(rmat24, oracle24_in_capped):
     assert it == 3
     assert np.array_equal(hop3, od3)
     assert hop3_reached == int((od3 != L.DIST_ABSENT).sum())
+
+
+def test_wide_bitmap_single_source_bfs():
+    """More vertices than one launch grid has threads (2^26 vertices = 1 M bitmap words,
+    the capped grids cover 524 288): every per-level bitmap clear must reach the whole array.
+    At RMAT-27 the one-thread-per-word level_prep left the next-frontier tail stale and 24 of
+    the 64 single-source runs differed from the sweep (profiles/r03d_scale27_one_gpu.json).
+    Single-source direction-optimizing BFS == multi-source sweep == hop-bounded Jacobi."""
+    scale = 26
+    n = 1 << scale
+    src, dst, _ = rmat_edges(scale, 2, seed=0x54495441)
+    roots = [int(r) for r in pick_roots(n, src, dst, 4, seed=7)]
+    eng = Engine(host_threads=16).load_edges(n, src, dst, L.SCOPE_BOTH_E, apply_cap=False)
+    del src, dst
+    eng.bfs_multi(roots, n, L.SCOPE_BOTH_E, seed_is_dense=True, fetch=False)
+    ms = np.empty(n, np.int64)
+    for i, r in enumerate(roots):
+        eng.lib.tgo_copy_multi_distances(eng.ctx, i, L.ptr(ms, C.c_int64))
+        bf = eng.bfs(r, n, L.SCOPE_BOTH_E, seed_is_dense=True)
+        assert np.array_equal(ms, bf), (i, int(np.sum(ms != bf)))
+        if i == 0:
+            hb = eng.sssp(r, 64, L.SCOPE_BOTH_E, mode=L.SSSP_HOP_BOUNDED, seed_is_dense=True)
+            assert np.array_equal(hb, bf)

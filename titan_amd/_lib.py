@@ -150,6 +150,8 @@ EXPORTS = [
     "tgo_part_ms_pack", "tgo_part_ms_settle_pairs", "tgo_part_ms_pack_fixed", "tgo_part_ms_settle_fixed",
     "tgo_part_ms_levels", "tgo_part_sssp_begin", "tgo_part_sssp_relax", "tgo_part_sssp_apply",
     "tgo_part_sssp_pending_min", "tgo_part_sssp_extract", "tgo_part_sssp_end",
+    "tgo_exchange_rccl_id", "tgo_exchange_rccl_create", "tgo_exchange_local_group", "tgo_exchange_destroy",
+    "tgo_exchange_last_error", "tgo_part_msbfs_run",
 ]
 
 _lib = None
@@ -242,6 +244,13 @@ def load() -> C.CDLL:
         "tgo_part_pr_step_hot": (C.c_int, [vp, vp, vp]),
         "tgo_rmat_partition": (C.c_int, [C.c_int32, C.c_int32, C.c_uint64, C.c_int64, C.c_int64, _i32p, _i32p,
                                          _i32p, C.c_int64, _i64p, C.c_int32]),
+        "tgo_exchange_rccl_id": (C.c_int, [_u8p]),
+        "tgo_exchange_rccl_create": (C.c_int, [C.c_int32, C.c_int32, _u8p, C.c_int32, P(vp)]),
+        "tgo_exchange_local_group": (C.c_int, [C.c_int32, P(vp)]),
+        "tgo_exchange_destroy": (None, [vp]),
+        "tgo_exchange_last_error": (C.c_char_p, [vp]),
+        "tgo_part_msbfs_run": (C.c_int, [vp, vp, _i64p, C.c_int32, C.c_int32, C.c_double, C.c_int64, _i64p, _i64p,
+                                         P(C.c_int32)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

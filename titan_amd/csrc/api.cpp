@@ -31,7 +31,11 @@ struct tgo_ctx {
     bool loaded = false;
     std::vector<int64_t> titan_id;
     std::vector<int32_t> perm;                       // row-order dense -> internal
-    std::unordered_map<int64_t, int64_t> id_index;   // Titan id -> dense (seed lookup)
+    // Titan id -> dense (seed lookups, tgo_dense_ids): binary search over titan_id when it is
+    // strictly increasing (edge loads; row loads of an ordered scan usually), else over a
+    // sorted copy built on the first lookup — no per-load hash map (16.8 M inserts at RMAT-24)
+    bool id_sorted = false;
+    std::vector<std::pair<int64_t, int32_t>> id_index;
     Scratch sc;
     tgo_stats st{};
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -98,7 +102,7 @@ template <class T>
 hipError_t upload(tgo_ctx* ctx, T*& p, const std::vector<T>& h) {
     hipError_t e = dev_alloc(ctx, p, static_cast<int64_t>(h.size()));
     if (e != hipSuccess || h.empty()) return e;
-    return hipMemcpy(p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice);
+    return copy_chunked(p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice);
 }
 
 void free_graph(tgo_ctx* ctx) {
@@ -236,6 +240,15 @@ int upload_cold_blocks(tgo_ctx* ctx, const std::vector<int64_t>& off, const std:
 
 int upload_graph(tgo_ctx* ctx, HostGraph& h, bool allow_segments = true) {
     DevGraph& g = ctx->g;
+    // TGO_TRACE=1: per-phase load times on stderr
+    static const bool trace = env_i64("TGO_TRACE", 0) != 0;
+    auto t_last = std::chrono::steady_clock::now();
+    auto lap = [&](const char* what) {
+        if (!trace) return;
+        const auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[tgo] upload %-14s %8.1f ms\n", what, std::chrono::duration<double, std::milli>(now - t_last).count());
+        t_last = now;
+    };
     g.n = h.n;
     g.scope = h.scope;
     g.has_weight = h.has_weight;
@@ -264,10 +277,12 @@ int upload_graph(tgo_ctx* ctx, HostGraph& h, bool allow_segments = true) {
     HIP_TRY(up(h.out, g.out));
     HIP_TRY(up(h.in, g.in));
     if (h.has_transpose) HIP_TRY(up(h.push_t, g.push_t));
+    lap("csr");
     // CSR-adaptive blocks for the two pull gathers (walk counts: out; PageRank: in).
     HIP_TRY(upload_row_blocks(ctx, h.out.off, g.rb_out));
     HIP_TRY(upload_row_blocks(ctx, h.in.off, g.rb_in));
     g.rb_out_ready = g.rb_in_ready = true;
+    lap("row blocks");
     g.push_ws = DevCsr();
     g.push_ws_ready = false;
     if (allow_segments && h.has_weight && env_i64("TGO_DS_SPLIT", 1) != 0) {
@@ -275,6 +290,7 @@ int upload_graph(tgo_ctx* ctx, HostGraph& h, bool allow_segments = true) {
         weight_sorted_push(h, ws, threads_of(ctx));
         HIP_TRY(up(ws, g.push_ws));
         g.push_ws_ready = true;
+        lap("weight-sorted");
     }
     g.cold_in = ColdBlocks();
     g.cold_in_ready = false;
@@ -284,6 +300,7 @@ int upload_graph(tgo_ctx* ctx, HostGraph& h, bool allow_segments = true) {
         if (int rc = upload_cold_blocks(ctx, h.in.off, h.in.adj, h.n, env_i64("TGO_PR_HOT", kPrHotDefault), g.n_active,
                                         g.cold_in, g.cold_in_ready))
             return rc;
+        lap("cold blocks");
     }
     // scratch
     Scratch& s = ctx->sc;
@@ -320,8 +337,8 @@ int upload_graph(tgo_ctx* ctx, HostGraph& h, bool allow_segments = true) {
     if (ctx->perm.empty()) { ctx->perm.resize(n); for (int64_t v = 0; v < n; ++v) ctx->perm[v] = static_cast<int32_t>(v); }
     HIP_TRY(upload(ctx, g.perm, ctx->perm));
     ctx->id_index.clear();
-    ctx->id_index.reserve(static_cast<size_t>(n) * 2);
-    for (int64_t v = 0; v < n; ++v) ctx->id_index.emplace(h.titan_id[v], v);
+    ctx->id_sorted = true;
+    for (int64_t v = 1; v < n && ctx->id_sorted; ++v) ctx->id_sorted = h.titan_id[v] > h.titan_id[v - 1];
     ctx->st.num_vertices = n;
     ctx->st.out_entries = static_cast<int64_t>(h.out.adj.size());
     ctx->st.in_entries = static_cast<int64_t>(h.in.adj.size());
@@ -338,6 +355,7 @@ int upload_graph(tgo_ctx* ctx, HostGraph& h, bool allow_segments = true) {
         if (h.pv_flags[r]) ctx->pv_rows.push_back(static_cast<int64_t>(r));
     ctx->st.device_bytes = ctx->dev_bytes;
     ctx->loaded = true;
+    lap("scratch, ids");
     return TGO_OK;
 }
 
@@ -361,14 +379,30 @@ View push_view(const DevGraph& g, int scope) {
     return make_view(&g.out, &g.in);
 }
 
+// Row-order dense index of a Titan id, -1 when no executed vertex has it.
+int64_t dense_of(tgo_ctx* ctx, int64_t id) {
+    const std::vector<int64_t>& t = ctx->titan_id;
+    if (ctx->id_sorted) {
+        const auto it = std::lower_bound(t.begin(), t.end(), id);
+        return it != t.end() && *it == id ? static_cast<int64_t>(it - t.begin()) : -1;
+    }
+    if (ctx->id_index.size() != t.size()) {
+        ctx->id_index.resize(t.size());
+        for (size_t v = 0; v < t.size(); ++v) ctx->id_index[v] = {t[v], static_cast<int32_t>(v)};
+        std::sort(ctx->id_index.begin(), ctx->id_index.end());
+    }
+    const auto it = std::lower_bound(ctx->id_index.begin(), ctx->id_index.end(), std::make_pair(id, INT32_MIN));
+    return it != ctx->id_index.end() && it->first == id ? it->second : -1;
+}
+
 int resolve_seed(tgo_ctx* ctx, int64_t seed, int is_dense, int64_t& out) {
     if (is_dense) {
         if (seed < 0 || seed >= ctx->g.n) return fail(ctx, TGO_E_INVALID, "dense seed out of range");
         out = ctx->perm[seed];
         return TGO_OK;
     }
-    auto it = ctx->id_index.find(seed);
-    out = it == ctx->id_index.end() ? -1 : ctx->perm[it->second];   // unknown seed: nobody gets a distance
+    const int64_t d = dense_of(ctx, seed);
+    out = d < 0 ? -1 : ctx->perm[d];                                 // unknown seed: nobody gets a distance
     return TGO_OK;
 }
 
@@ -686,6 +720,7 @@ int finish_distance_program(tgo_ctx* ctx, int scope, int flags, int64_t* dist_ou
 }  // namespace
 
 // ============================================================================ C-ABI
+
 extern "C" {
 
 void tgo_default_options(tgo_options* o) {
@@ -789,8 +824,17 @@ int tgo_finish_load(tgo_ctx* ctx) {
                                ctx->stream, err);
     ctx->dec.release();
     if (rc) { ctx->staging = RowStaging(); return fail(ctx, rc, err); }
-    rc = assemble_from_rows(ctx->staging, h, threads_of(ctx), err);
-    if (rc) return fail(ctx, rc, err);
+    // CSR assembly on the device (assemble.hip) unless TGO_HOST_ASSEMBLY=1 or the scan holds
+    // vertex cuts (their representative rows fold on the host, graph_build.cpp)
+    const RowStaging& stg = ctx->staging;
+    const bool cuts = stg.n_rep > 0 || std::any_of(stg.vid.begin(), stg.vid.end(), [](int64_t v) { return (v & 7) == 2; });
+    const bool on_dev = env_i64("TGO_HOST_ASSEMBLY", 0) == 0 && !cuts;
+    rc = on_dev ? assemble_rows_device(ctx->staging, h, ctx->stream, err)
+                : assemble_from_rows(ctx->staging, h, threads_of(ctx), err);
+    if (rc) { ctx->staging = RowStaging(); return fail(ctx, rc, err); }
+    if (env_i64("TGO_TRACE", 0))
+        std::fprintf(stderr, "[tgo] finish_load decode + assembly (%s) %8.1f ms\n", on_dev ? "device" : "host",
+                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
     free_graph(ctx);
     rc = upload_graph(ctx, h);
     ctx->st.load_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -807,11 +851,14 @@ int tgo_load_edges(tgo_ctx* ctx, const tgo_edges* edges, const tgo_load_opts* op
     const auto t0 = std::chrono::steady_clock::now();
     HostGraph h;
     std::string err;
-    // device assembly (assemble.hip) unless TGO_HOST_ASSEMBLY=1; the host path for > 2^31 edges
-    const bool on_dev = env_i64("TGO_HOST_ASSEMBLY", 0) == 0 && edges->m < (int64_t(1) << 31);
+    // device assembly (assemble.hip) unless TGO_HOST_ASSEMBLY=1
+    const bool on_dev = env_i64("TGO_HOST_ASSEMBLY", 0) == 0;
     int rc = on_dev ? assemble_edges_device(edges, opts, ctx->opts.hard_query_limit, h, ctx->stream, err)
                     : assemble_from_edges(edges, opts, ctx->opts.hard_query_limit, h, threads_of(ctx), err);
     if (rc) return fail(ctx, rc, err);
+    if (env_i64("TGO_TRACE", 0))
+        std::fprintf(stderr, "[tgo] load_edges assembly (%s) %8.1f ms\n", on_dev ? "device" : "host",
+                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
     free_graph(ctx);
     ctx->staging = RowStaging();
     rc = upload_graph(ctx, h);
@@ -836,10 +883,10 @@ int tgo_graph_csr(tgo_ctx* ctx, int32_t which, int64_t* nnz, int64_t* off, int32
     const DevCsr& c = which == 0 ? g.out : which == 1 ? g.in : g.push_t;
     *nnz = c.nnz;
     (void)hipSetDevice(ctx->opts.device);
-    if (off) HIP_TRY(hipMemcpy(off, c.off, (g.n + 1) * sizeof(int64_t), hipMemcpyDeviceToHost));
-    if (adj && c.nnz) HIP_TRY(hipMemcpy(adj, c.adj, c.nnz * sizeof(int32_t), hipMemcpyDeviceToHost));
-    if (w && c.w && c.nnz) HIP_TRY(hipMemcpy(w, c.w, c.nnz * sizeof(int32_t), hipMemcpyDeviceToHost));
-    if (col && c.col && c.nnz) HIP_TRY(hipMemcpy(col, c.col, c.nnz * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    if (off) HIP_TRY(copy_chunked(off, c.off, (g.n + 1) * sizeof(int64_t), hipMemcpyDeviceToHost));
+    if (adj && c.nnz) HIP_TRY(copy_chunked(adj, c.adj, c.nnz * sizeof(int32_t), hipMemcpyDeviceToHost));
+    if (w && c.w && c.nnz) HIP_TRY(copy_chunked(w, c.w, c.nnz * sizeof(int32_t), hipMemcpyDeviceToHost));
+    if (col && c.col && c.nnz) HIP_TRY(copy_chunked(col, c.col, c.nnz * sizeof(uint32_t), hipMemcpyDeviceToHost));
     return TGO_OK;
 }
 
@@ -1011,6 +1058,13 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
         mf = static_cast<int64_t>(s.hcnt->mf);
         if (trace) std::fprintf(stderr, "[tgo] ms level %d %s -> %lld vertices, %lld entries, %llu source-bits\n", L,
                                 use_pull ? "pull" : "push", (long long)qlen, (long long)mf, s.hcnt->red[0]);
+        static const bool diag = env_double("TGO_MS_DIAG", 0.0) != 0.0;
+        if (trace && diag && use_pull) {
+            unsigned long long d[5] = {};
+            HIP_TRY(k_ms_diag_take(d, st));
+            std::fprintf(stderr, "[tgo]   pull: %llu entries examined, %llu hot / %llu cold mask gathers, %llu open vertices, "
+                         "%llu stopped early\n", d[0], d[1], d[2], d[3], d[4]);
+        }
         std::swap(fr, nx);
         cur ^= 1;
         ++levels;
@@ -1302,6 +1356,9 @@ int tgo_load_partition_layout(tgo_ctx* ctx, int64_t n_global, int64_t lo, int64_
     ctx->st.load_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return TGO_OK;
 }
+
+static int part_check(tgo_ctx* ctx);
+
 
 static int part_check(tgo_ctx* ctx) {
     if (!ctx) return TGO_E_INVALID;
@@ -2258,8 +2315,7 @@ int tgo_dense_ids(tgo_ctx* ctx, const int64_t* titan_ids, int64_t count, int64_t
     for (int64_t i = 0; i < count; ++i) {
         int64_t id = titan_ids[i];
         if (is_partitioned_vertex(id, pb)) id = canonical_vertex_id(id, pb);    // getCanonicalId
-        auto it = ctx->id_index.find(id);
-        dense_out[i] = it == ctx->id_index.end() ? -1 : it->second;
+        dense_out[i] = dense_of(ctx, id);
     }
     return TGO_OK;
 }
@@ -2277,3 +2333,30 @@ int tgo_sync(tgo_ctx* ctx) {
 }
 
 }  // extern "C"
+
+// accessors for the C++ partitioned driver (part_driver.cpp)
+namespace tgo {
+hipStream_t part_stream(tgo_ctx* ctx) { return ctx->stream; }
+int part_fail(tgo_ctx* ctx, int code, const std::string& msg) { return fail(ctx, code, msg); }
+int64_t* part_dcounts_of(tgo_ctx* ctx) { return ctx->part_dcounts; }
+int part_dims(tgo_ctx* ctx, int64_t* n_local, int64_t* lo, int64_t* n_global, int64_t* entries) {
+    if (int rc = part_check(ctx)) return rc;
+    *n_local = ctx->g.n;
+    *lo = ctx->g.lo;
+    *n_global = ctx->g.n_global;
+    *entries = ctx->g.out.nnz + ctx->g.in.nnz;
+    return TGO_OK;
+}
+int part_scratch(tgo_ctx* ctx, void** p, int64_t bytes, int slot) {
+    Scratch& s = ctx->sc;
+    if (slot < 0 || slot >= 8) return fail(ctx, TGO_E_INVALID, "driver scratch slot");
+    if (s.drv_bytes[slot] < bytes) {
+        uint8_t* q = nullptr;
+        HIP_TRY(dev_alloc(ctx, q, bytes));
+        s.drv[slot] = q;
+        s.drv_bytes[slot] = bytes;
+    }
+    *p = s.drv[slot];
+    return TGO_OK;
+}
+}  // namespace tgo

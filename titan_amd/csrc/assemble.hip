@@ -201,10 +201,73 @@ __global__ void transpose_keys(const uint64_t* __restrict__ key, int64_t m, int 
         if (tval) tval[k] = static_cast<uint32_t>(k);
     }
 }
+__global__ void shift_u32(uint32_t* __restrict__ v, int64_t m, uint32_t by) {
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x) v[k] += by;
+}
 __global__ void gather_i32(const uint32_t* __restrict__ idx, const int32_t* __restrict__ in, int64_t m,
                            int32_t* __restrict__ out) {
     for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x)
         out[k] = in[idx[k]];
+}
+
+
+// ---- rows (tgo_load_rows after the decode): Titan ids -> dense ids by binary search over the
+// sorted vertex ids; the staged entries are already grouped by row in column order
+__global__ void id_keys(const int64_t* __restrict__ vid, int64_t n, uint64_t* __restrict__ key, uint32_t* __restrict__ val) {
+    for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x) {
+        key[v] = static_cast<uint64_t>(vid[v]) ^ 0x8000000000000000ULL;     // signed order
+        val[v] = static_cast<uint32_t>(v);
+    }
+}
+// Per staged entry: its row (binary search over row_begin), its neighbour's dense id (-1: the
+// neighbour never executes -> dropped, VertexState.java:103-137) and the direction flags.
+__global__ void entry_dense(const int64_t* __restrict__ other, const uint8_t* __restrict__ dir, int64_t E,
+                            const int64_t* __restrict__ row_begin, int64_t n, const uint64_t* __restrict__ skey,
+                            const uint32_t* __restrict__ sval, int32_t* __restrict__ row, int32_t* __restrict__ dense,
+                            uint32_t* __restrict__ fout, uint32_t* __restrict__ fin) {
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < E; k += (int64_t)gridDim.x * blockDim.x) {
+        int64_t lo = 0, hi = n;                          // last row with row_begin <= k
+        while (hi - lo > 1) { const int64_t mid = (lo + hi) >> 1; if (row_begin[mid] <= k) lo = mid; else hi = mid; }
+        const uint64_t t = static_cast<uint64_t>(other[k]) ^ 0x8000000000000000ULL;
+        int64_t a = 0, b = n;
+        while (a < b) { const int64_t mid = (a + b) >> 1; if (skey[mid] < t) a = mid + 1; else b = mid; }
+        const int32_t d = (a < n && skey[a] == t) ? static_cast<int32_t>(sval[a]) : -1;
+        row[k] = static_cast<int32_t>(lo);
+        dense[k] = d;
+        fout[k] = (d >= 0 && dir[k] == 0) ? 1u : 0u;
+        fin[k] = (d >= 0 && dir[k] != 0) ? 1u : 0u;
+    }
+}
+// Compact one direction's entries (staged order) into keys row << b | dense, payload = the
+// staged entry index (weights, column positions gathered at the end).
+__global__ void compact_dir(const uint32_t* __restrict__ flag, const uint64_t* __restrict__ pos, int64_t E, int b,
+                            const int32_t* __restrict__ row, const int32_t* __restrict__ dense,
+                            uint64_t* __restrict__ okey, uint32_t* __restrict__ oval) {
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < E; k += (int64_t)gridDim.x * blockDim.x) {
+        if (!flag[k]) continue;
+        const uint64_t p = pos[k];
+        okey[p] = (static_cast<uint64_t>(static_cast<uint32_t>(row[k])) << b) | static_cast<uint32_t>(dense[k]);
+        oval[p] = static_cast<uint32_t>(k);
+    }
+}
+__global__ void col_of(const int32_t* __restrict__ row, const int64_t* __restrict__ row_begin, int64_t E,
+                       uint32_t* __restrict__ col) {
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < E; k += (int64_t)gridDim.x * blockDim.x)
+        col[k] = static_cast<uint32_t>(k - row_begin[row[k]]);
+}
+__global__ void degree_rows(const int64_t* __restrict__ oo, const int64_t* __restrict__ oi, int64_t n,
+                            uint32_t* __restrict__ deg) {
+    for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x)
+        deg[v] = static_cast<uint32_t>((oo[v + 1] - oo[v]) + (oi[v + 1] - oi[v]));
+}
+// Views check (graph_build.cpp finish_views): every OUT entry u->v has an IN entry at v.
+__global__ void count_targets(const int32_t* __restrict__ adj, int64_t m, uint32_t* __restrict__ cnt) {
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x)
+        atomicAdd(&cnt[adj[k]], 1u);
+}
+__global__ void count_mismatch(const uint32_t* __restrict__ cnt, const int64_t* __restrict__ off, int64_t n, int* bad) {
+    for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x)
+        if (static_cast<int64_t>(cnt[v]) != off[v + 1] - off[v]) atomicOr(bad, 1);
 }
 
 struct Sorter {
@@ -239,7 +302,9 @@ template <class T>
 hipError_t download(std::vector<T>& h, const T* d, int64_t count, hipStream_t s) {
     h.resize(static_cast<size_t>(count));
     if (count == 0) return hipSuccess;
-    return hipMemcpyAsync(h.data(), d, static_cast<size_t>(count) * sizeof(T), hipMemcpyDeviceToHost, s);
+    const hipError_t e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return e;
+    return copy_chunked(h.data(), d, static_cast<size_t>(count) * sizeof(T), hipMemcpyDeviceToHost);
 }
 
 }  // namespace
@@ -270,12 +335,12 @@ int assemble_edges_device(const tgo_edges* e, const tgo_load_opts* opts, int64_t
     AS_TRY(d_src.alloc(m));
     AS_TRY(d_dst.alloc(m));
     if (m) {
-        AS_TRY(hipMemcpyAsync(d_src.p, e->src, m * sizeof(int32_t), hipMemcpyHostToDevice, s));
-        AS_TRY(hipMemcpyAsync(d_dst.p, e->dst, m * sizeof(int32_t), hipMemcpyHostToDevice, s));
+        AS_TRY(copy_chunked(d_src.p, e->src, m * sizeof(int32_t), hipMemcpyHostToDevice));
+        AS_TRY(copy_chunked(d_dst.p, e->dst, m * sizeof(int32_t), hipMemcpyHostToDevice));
     }
     if (g.has_weight) {
         AS_TRY(d_w.alloc(m));
-        if (m) AS_TRY(hipMemcpyAsync(d_w.p, e->weight, m * sizeof(int32_t), hipMemcpyHostToDevice, s));
+        if (m) AS_TRY(copy_chunked(d_w.p, e->weight, m * sizeof(int32_t), hipMemcpyHostToDevice));
     }
     {
         ScopedBuf<int> bad;
@@ -448,6 +513,199 @@ int assemble_edges_device(const tgo_edges* e, const tgo_load_opts* opts, int64_t
         if (g.has_weight) AS_TRY(download(g.push_t.w, w.p, c, s));
     }
     AS_TRY(hipStreamSynchronize(s));
+    return TGO_OK;
+}
+
+
+// Row loads (tgo_load_rows + tgo_finish_load): the host assemble_from_rows, on the device.
+// Vertex cuts (representative rows, PartitionedVertex ids) keep the host path (the caller
+// checks); the staging is the decoder's, in row order with each row in column order.
+int assemble_rows_device(RowStaging& st, HostGraph& g, hipStream_t s, std::string& err) {
+    g = HostGraph();
+    const int64_t n = static_cast<int64_t>(st.vid.size());
+    if (n >= INT32_MAX) { err = "more than 2^31-1 vertices per device"; return TGO_E_UNSUPPORTED; }
+    const int64_t E = static_cast<int64_t>(st.other.size());
+    if (E >= (int64_t(1) << 32)) { err = "more than 2^32 staged entries"; return TGO_E_UNSUPPORTED; }
+    g.n = n;
+    g.titan_id = st.vid;
+    g.scope = st.opts.scope;
+    g.has_weight = st.opts.weight_key != 0;
+    g.weight_dt = st.plan.weight_dt ? st.plan.weight_dt : TGO_DT_INTEGER;
+    g.ghost = st.ghost; g.truncated = st.truncated; g.skipped = st.skipped;
+    const bool keep_col = (st.opts.flags & TGO_LOAD_COLUMN_ORDER) != 0;
+    const bool weighted = g.has_weight && static_cast<int64_t>(st.w.size()) == E;
+    if (g.has_weight && !weighted) { err = "staged weights out of step"; return TGO_E_STATE; }
+    if (n == 0) {
+        g.out.off.assign(1, 0); g.in.off.assign(1, 0);
+        st = RowStaging();
+        return TGO_OK;
+    }
+    int b = 1;
+    while ((int64_t(1) << b) < n) ++b;
+    const int bits = 2 * b;
+    Sorter so{{}, s};
+    ScopedBuf<int64_t> d_vid, d_other, d_rb;
+    ScopedBuf<uint8_t> d_dir;
+    ScopedBuf<int32_t> d_w;
+    AS_TRY(d_vid.alloc(n));
+    AS_TRY(d_rb.alloc(n + 1));
+    AS_TRY(d_other.alloc(E));
+    AS_TRY(d_dir.alloc(E));
+    AS_TRY(copy_chunked(d_vid.p, st.vid.data(), n * 8, hipMemcpyHostToDevice));
+    AS_TRY(copy_chunked(d_rb.p, st.row_begin.data(), (n + 1) * 8, hipMemcpyHostToDevice));
+    if (E) {
+        AS_TRY(copy_chunked(d_other.p, st.other.data(), E * 8, hipMemcpyHostToDevice));
+        AS_TRY(copy_chunked(d_dir.p, st.dir.data(), E, hipMemcpyHostToDevice));
+    }
+    if (weighted) {
+        AS_TRY(d_w.alloc(E));
+        if (E) AS_TRY(copy_chunked(d_w.p, st.w.data(), E * 4, hipMemcpyHostToDevice));
+    }
+    // id map: vertex ids sorted (signed order), their dense index alongside
+    ScopedBuf<uint64_t> ik, sk;
+    ScopedBuf<uint32_t> iv, sv;
+    AS_TRY(ik.alloc(n)); AS_TRY(sk.alloc(n)); AS_TRY(iv.alloc(n)); AS_TRY(sv.alloc(n));
+    id_keys<<<grid(n), kB, 0, s>>>(d_vid.p, n, ik.p, iv.p);
+    AS_TRY(so.pairs(ik.p, sk.p, iv.p, sv.p, n, 64));
+    ik.release(); iv.release();
+    ScopedBuf<int32_t> row, dense;
+    ScopedBuf<uint32_t> fl[2], col;
+    AS_TRY(row.alloc(E)); AS_TRY(dense.alloc(E)); AS_TRY(fl[0].alloc(E)); AS_TRY(fl[1].alloc(E));
+    if (E) entry_dense<<<grid(E), kB, 0, s>>>(d_other.p, d_dir.p, E, d_rb.p, n, sk.p, sv.p, row.p, dense.p, fl[0].p, fl[1].p);
+    if (keep_col) {
+        AS_TRY(col.alloc(E));
+        if (E) col_of<<<grid(E), kB, 0, s>>>(row.p, d_rb.p, E, col.p);
+    }
+    d_other.release(); d_dir.release(); sk.release(); sv.release();
+    // per direction: kept entries in staged order, keys row << b | dense
+    ScopedBuf<uint64_t> k1[2];
+    ScopedBuf<uint32_t> v1[2];
+    ScopedBuf<int64_t> off1[2];
+    int64_t cnt[2] = {0, 0};
+    for (int d = 0; d < 2; ++d) {
+        ScopedBuf<uint64_t> pos;
+        AS_TRY(pos.alloc(E + 1));
+        AS_TRY(so.excl_scan(fl[d].p, pos.p, E + 0));
+        uint64_t last = 0;
+        uint32_t lf = 0;
+        if (E) {
+            AS_TRY(hipMemcpyAsync(&last, pos.p + E - 1, 8, hipMemcpyDeviceToHost, s));
+            AS_TRY(hipMemcpyAsync(&lf, fl[d].p + E - 1, 4, hipMemcpyDeviceToHost, s));
+        }
+        AS_TRY(hipStreamSynchronize(s));
+        cnt[d] = static_cast<int64_t>(last + lf);
+        AS_TRY(k1[d].alloc(cnt[d])); AS_TRY(v1[d].alloc(cnt[d])); AS_TRY(off1[d].alloc(n + 1));
+        if (E) compact_dir<<<grid(E), kB, 0, s>>>(fl[d].p, pos.p, E, b, row.p, dense.p, k1[d].p, v1[d].p);
+        row_offsets<<<grid(n + 1), kB, 0, s>>>(k1[d].p, cnt[d], b, n, off1[d].p);
+        AS_TRY(hipStreamSynchronize(s));
+    }
+    row.release(); dense.release(); fl[0].release(); fl[1].release();
+    // degree-grouped relabel over the kept lists
+    ScopedBuf<int32_t> perm;
+    AS_TRY(perm.alloc(n));
+    {
+        ScopedBuf<uint32_t> deg;
+        ScopedBuf<uint64_t> bk, bs;
+        AS_TRY(deg.alloc(n)); AS_TRY(bk.alloc(n)); AS_TRY(bs.alloc(n));
+        degree_rows<<<grid(n), kB, 0, s>>>(off1[0].p, off1[1].p, n, deg.p);
+        bucket_keys<<<grid(n), kB, 0, s>>>(deg.p, n, bk.p);
+        AS_TRY(so.keys(bk.p, bs.p, n, 32 + 7));
+        order_to_perm<<<grid(n), kB, 0, s>>>(bs.p, n, perm.p);
+        AS_TRY(hipStreamSynchronize(s));
+    }
+    // final lists: stable sort by (perm[row], perm[neighbour]) from the staged order
+    HostCsr* outc[2] = {&g.out, &g.in};
+    ScopedBuf<uint64_t> fkey[2];
+    ScopedBuf<int32_t> fadj[2], fw[2];
+    ScopedBuf<int64_t> foff[2];
+    for (int d = 0; d < 2; ++d) {
+        const int64_t c = cnt[d];
+        ScopedBuf<uint64_t> kt;
+        ScopedBuf<uint32_t> vt, vs;
+        AS_TRY(kt.alloc(c)); AS_TRY(vt.alloc(c)); AS_TRY(vs.alloc(c)); AS_TRY(fkey[d].alloc(c));
+        if (c) rekey<<<grid(c), kB, 0, s>>>(k1[d].p, c, b, perm.p, kt.p, vt.p);
+        if (c) AS_TRY(so.pairs(kt.p, fkey[d].p, vt.p, vs.p, c, bits));
+        k1[d].release();
+        AS_TRY(foff[d].alloc(n + 1));
+        row_offsets<<<grid(n + 1), kB, 0, s>>>(fkey[d].p, c, b, n, foff[d].p);
+        AS_TRY(fadj[d].alloc(c));
+        ScopedBuf<uint32_t> fcol;
+        if (weighted) AS_TRY(fw[d].alloc(c));
+        if (keep_col) AS_TRY(fcol.alloc(c));
+        // payload chain: sorted position -> kept index (vs) -> staged entry (v1)
+        if (c)
+            emit_list<<<grid(c), kB, 0, s>>>(fkey[d].p, vs.p, c, b, v1[d].p, d_w.p, nullptr, fadj[d].p,
+                                             weighted ? fw[d].p : nullptr, nullptr);
+        if (keep_col && c) {
+            ScopedBuf<uint32_t> staged;              // staged entry of every final entry
+            AS_TRY(staged.alloc(c));
+            gather_i32<<<grid(c), kB, 0, s>>>(vs.p, reinterpret_cast<const int32_t*>(v1[d].p), c,
+                                              reinterpret_cast<int32_t*>(staged.p));
+            gather_i32<<<grid(c), kB, 0, s>>>(staged.p, reinterpret_cast<const int32_t*>(col.p), c,
+                                              reinterpret_cast<int32_t*>(fcol.p));
+            AS_TRY(hipStreamSynchronize(s));
+        }
+        HostCsr& hc = *outc[d];
+        AS_TRY(download(hc.off, foff[d].p, n + 1, s));
+        AS_TRY(download(hc.adj, fadj[d].p, c, s));
+        if (weighted) AS_TRY(download(hc.w, fw[d].p, c, s));
+        if (keep_col) AS_TRY(download(hc.col, fcol.p, c, s));
+        v1[d].release();
+    }
+    AS_TRY(download(g.perm, perm.p, n, s));
+    // views: the push lists equal the stored opposite lists unless rows were cut or a
+    // neighbour's opposite entry is missing (count check, graph_build.cpp finish_views)
+    bool consistent = g.truncated == 0;
+    if (consistent) {
+        ScopedBuf<uint32_t> tc;
+        ScopedBuf<int> bad;
+        AS_TRY(tc.alloc(n)); AS_TRY(bad.alloc(1));
+        AS_TRY(hipMemsetAsync(tc.p, 0, n * 4, s));
+        AS_TRY(hipMemsetAsync(bad.p, 0, sizeof(int), s));
+        if (cnt[0]) count_targets<<<grid(cnt[0]), kB, 0, s>>>(fadj[0].p, cnt[0], tc.p);
+        count_mismatch<<<grid(n), kB, 0, s>>>(tc.p, foff[1].p, n, bad.p);
+        int hb = 0;
+        AS_TRY(hipMemcpyAsync(&hb, bad.p, sizeof(int), hipMemcpyDeviceToHost, s));
+        AS_TRY(hipStreamSynchronize(s));
+        consistent = hb == 0;
+    }
+    g.has_transpose = !consistent;
+    if (!consistent) {
+        // pull lists of the scope: inE = OUT rows, outE = IN rows, bothE = both (source order,
+        // OUT before IN for one source: the host transpose_lists order)
+        std::vector<int> lists = g.scope == TGO_SCOPE_IN_E ? std::vector<int>{0}
+                               : g.scope == TGO_SCOPE_OUT_E ? std::vector<int>{1} : std::vector<int>{0, 1};
+        int64_t c = 0;
+        for (int d : lists) c += cnt[d];
+        ScopedBuf<uint64_t> tk, ts;
+        ScopedBuf<uint32_t> tv, tvs;
+        ScopedBuf<int32_t> tw;
+        AS_TRY(tk.alloc(c)); AS_TRY(ts.alloc(c)); AS_TRY(tv.alloc(c)); AS_TRY(tvs.alloc(c));
+        if (weighted) AS_TRY(tw.alloc(c));
+        int64_t at = 0;
+        for (int d : lists) {
+            if (cnt[d]) transpose_keys<<<grid(cnt[d]), kB, 0, s>>>(fkey[d].p, cnt[d], b, tk.p + at, tv.p + at);
+            if (weighted && cnt[d])
+                AS_TRY(hipMemcpyAsync(tw.p + at, fw[d].p, cnt[d] * 4, hipMemcpyDeviceToDevice, s));
+            at += cnt[d];
+        }
+        if (lists.size() == 2 && cnt[0] && cnt[1])      // the second list's payloads index the concatenation
+            shift_u32<<<grid(cnt[1]), kB, 0, s>>>(tv.p + cnt[0], cnt[1], static_cast<uint32_t>(cnt[0]));
+        if (c) AS_TRY(so.pairs(tk.p, ts.p, tv.p, tvs.p, c, bits));
+        ScopedBuf<int64_t> off;
+        AS_TRY(off.alloc(n + 1));
+        row_offsets<<<grid(n + 1), kB, 0, s>>>(ts.p, c, b, n, off.p);
+        ScopedBuf<int32_t> adj, w;
+        AS_TRY(adj.alloc(c));
+        if (weighted) AS_TRY(w.alloc(c));
+        if (c) emit_list<<<grid(c), kB, 0, s>>>(ts.p, tvs.p, c, b, nullptr, tw.p, nullptr, adj.p,
+                                                weighted ? w.p : nullptr, nullptr);
+        AS_TRY(download(g.push_t.off, off.p, n + 1, s));
+        AS_TRY(download(g.push_t.adj, adj.p, c, s));
+        if (weighted) AS_TRY(download(g.push_t.w, w.p, c, s));
+    }
+    AS_TRY(hipStreamSynchronize(s));
+    st = RowStaging();
     return TGO_OK;
 }
 

@@ -349,11 +349,13 @@ __global__ void publish_counters(const Counters* c, unsigned long long* host, un
     __syncthreads();
     if (i == 0) __hip_atomic_store(&host[kCounterWords], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// Grid-stride: the launch grid is capped (grid_for: 2048 blocks = 524 288 threads), and RMAT-27
+// has 2.1 M bitmap words — a one-thread-per-word form left the tail of nb uncleared there.
 __global__ void level_prep(Counters* cnt, uint64_t* nb, int64_t words, int64_t* tail) {
-    const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (i < words) nb[i] = 0;
-    if (cnt && i < kCounterWords) reinterpret_cast<unsigned long long*>(cnt)[i] = 0;
-    if (tail && i == 0) *tail = 0;
+    const int64_t i0 = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    for (int64_t i = i0; i < words; i += static_cast<int64_t>(gridDim.x) * blockDim.x) nb[i] = 0;
+    if (cnt && i0 < kCounterWords) reinterpret_cast<unsigned long long*>(cnt)[i0] = 0;
+    if (tail && i0 == 0) *tail = 0;
 }
 hipError_t k_publish_counters(const Counters* c, unsigned long long* host, unsigned long long seq, hipStream_t s) {
     publish_counters<<<1, 64, 0, s>>>(c, host, seq);

@@ -237,16 +237,28 @@ __global__ void __launch_bounds__(kBlock) ds_extract_ws(const int64_t* __restric
 // Pending minimum / count (red[0], red[1]) and the settled bucket's members left (red2).
 __global__ void __launch_bounds__(kBlock) ds_pending_min_ws(const uint64_t* __restrict__ pend,
         const uint64_t* __restrict__ member, int64_t words, const int64_t* __restrict__ dist, Counters* cnt) {
+    // one wave per 64-vertex word, lane = vertex: the pending vertices' distances load
+    // coalesced and in parallel (a thread per word walked its set bits one dependent load at
+    // a time); 4 words per trip keep their loads in flight together
     unsigned long long mn = ~0ULL >> 1, count = 0, mem = 0;
-    for (int64_t wd = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; wd < words; wd += (int64_t)gridDim.x * blockDim.x) {
-        uint64_t b = pend[wd];
-        count += __popcll(b);
-        mem += __popcll(member[wd]);
-        while (b) {
-            const int r = __ffsll(static_cast<long long>(b)) - 1;
-            b &= b - 1;
-            const unsigned long long d = static_cast<unsigned long long>(dist[(wd << 6) + r]);
-            mn = d < mn ? d : mn;
+    const int64_t nw = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
+    const int64_t w0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    for (int64_t wd = w0; wd < words; wd += 4 * nw) {
+        uint64_t b[4], m[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t w = wd + u * nw;
+            b[u] = w < words ? pend[w] : 0;
+            m[u] = w < words ? member[w] : 0;
+        }
+        unsigned long long d[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            d[u] = ((b[u] >> lane()) & 1ULL) ? static_cast<unsigned long long>(dist[((wd + u * nw) << 6) + lane()]) : ~0ULL >> 1;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            mn = d[u] < mn ? d[u] : mn;
+            if (lane() == 0) { count += __popcll(b[u]); mem += __popcll(m[u]); }
         }
     }
     for (int off = 32; off > 0; off >>= 1) {
@@ -433,7 +445,7 @@ hipError_t k_ds_extract_ws(const DevCsr& ws, const int64_t* light, uint64_t* pen
 }
 hipError_t k_ds_pending_min_ws(const uint64_t* pend, const uint64_t* member, int64_t words, const int64_t* dist,
                                Counters* cnt, hipStream_t s) {
-    ds_pending_min_ws<<<grid_for(words, 1024), kBlock, 0, s>>>(pend, member, words, dist, cnt);
+    ds_pending_min_ws<<<grid_for(words * 8, 2048), kBlock, 0, s>>>(pend, member, words, dist, cnt);
     return hipGetLastError();
 }
 hipError_t k_ds_pending_min(const uint64_t* pend, int64_t words, const int64_t* dist, Counters* cnt, hipStream_t s) {

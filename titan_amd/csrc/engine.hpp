@@ -162,10 +162,23 @@ int decode_rows(RowStaging& st, const tgo_rows* rows, const tgo_schema* schema,
 int assemble_from_rows(RowStaging& st, HostGraph& g, int threads, std::string& err);
 int assemble_from_edges(const tgo_edges* e, const tgo_load_opts* opts, int64_t hard_limit,
                         HostGraph& g, int threads, std::string& err);
+// hipMemcpy in pieces of at most 256 MiB: single pageable copies of several GiB (RMAT-27
+// lists are 8.6 GB each) are split so no one staging transfer spans more than 2^32 bytes.
+inline hipError_t copy_chunked(void* dst, const void* src, size_t bytes, hipMemcpyKind kind) {
+    constexpr size_t kPiece = size_t(256) << 20;
+    for (size_t o = 0; o < bytes; o += kPiece) {
+        const hipError_t e = hipMemcpy(static_cast<char*>(dst) + o, static_cast<const char*>(src) + o,
+                                       std::min(kPiece, bytes - o), kind);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
 // The same graph assembled on the device (assemble.hip): radix sorts instead of the host
-// counting sorts; m < 2^31.
+// counting sorts; m < 2^32.
 int assemble_edges_device(const tgo_edges* e, const tgo_load_opts* opts, int64_t hard_limit, HostGraph& g,
                           hipStream_t s, std::string& err);
+// assemble_from_rows on the device (no vertex cuts: the caller keeps those on the host path)
+int assemble_rows_device(RowStaging& st, HostGraph& g, hipStream_t s, std::string& err);
 int partition_layout(const tgo_edges* e, int64_t n_global, int64_t lo, int64_t hi, int threads,
                      int32_t* layout_local, std::string& err);
 int assemble_partition(const tgo_edges* e, int64_t n_global, int64_t lo, int64_t hi,
@@ -309,6 +322,8 @@ struct Counters {               // device-side level counters (one cache line ea
 };
 
 struct Scratch {
+    void* drv[8] = {};          // partitioned C++ driver buffers (part_driver.cpp), by slot
+    int64_t drv_bytes[8] = {};
     int64_t n = 0;
     int32_t* level = nullptr;       // n
     int32_t* q[2] = {nullptr, nullptr};   // frontier queues
@@ -427,6 +442,7 @@ hipError_t k_ds_apply(const View& push, const int64_t* recv, int64_t npairs, int
                       int64_t* qdeg_n, Counters* cnt, int64_t thr, hipStream_t s);
 hipError_t k_unpermute_i64(const int64_t* in, const int32_t* perm, int64_t* out, int64_t n, hipStream_t s);
 hipError_t k_ms_seed(const int64_t* seeds, int nseeds, uint64_t* vis, uint64_t* fr, int64_t fr_rows, hipStream_t s);
+hipError_t k_ms_diag_take(unsigned long long* out5, hipStream_t s);
 hipError_t k_ms_pull(const View& pull, const View& push, int64_t n_active, uint64_t full, const uint64_t* fr,
                      const uint64_t* fbm, uint64_t* vis, uint64_t* nx, LevelPlanes lvl, Counters* cnt,
                      int32_t next_level, hipStream_t s);

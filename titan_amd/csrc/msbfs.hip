@@ -82,11 +82,17 @@ constexpr int64_t kCoop = 64;
 __device__ __forceinline__ bool in_frontier(const uint64_t* __restrict__ fbm, int32_t u) {
     return !fbm || ((fbm[u >> 6] >> (u & 63)) & 1ULL);
 }
-template <int kStep>       // entries per dependent round trip of a lane's own list
+// Diagnostic tallies of a pull level (TGO_MS_DIAG=1 with TGO_TRACE=1; off in the product):
+// [0] list entries examined, [1] mask gathers of hot neighbours (u < kDiagHot), [2] of cold
+// ones, [3] open vertices, [4] open vertices whose walk stopped early (every open source covered)
+constexpr int32_t kDiagHot = 393216;
+__device__ unsigned long long g_ms_diag[8];
+template <int kStep, bool kDiag = false>       // entries per dependent round trip of a lane's own list
 __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t n_active, uint64_t full,
         const uint64_t* __restrict__ fr, const uint64_t* __restrict__ fbm, uint64_t* __restrict__ vis,
         uint64_t* __restrict__ nx, LevelPlanes lvl, Counters* cnt, int32_t next_level) {
     unsigned long long nv = 0, mf = 0, bits = 0;
+    unsigned long long dg[5] = {0, 0, 0, 0, 0};
     const int64_t words = (n_active + 63) >> 6;
     // wave w of the block takes word b + w; words past the end run as all-closed lanes.  No
     // block barrier inside: the next frontier is only counted here (ms_queue builds its queue
@@ -121,8 +127,12 @@ __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t 
                     for (int j = 0; j < kStep; ++j)
                         if (f[j]) m |= fr[u[j]];
                     acc |= m;
+                    if (kDiag)
+                        for (int j = 0; j < kStep; ++j)
+                            if (u[j] >= 0) { ++dg[0]; ++dg[u[j] < kDiagHot ? 1 : 2]; }
                 }
             }
+            if (kDiag) { ++dg[3]; if ((acc & open) == open) ++dg[4]; }
         }
         unsigned long long big = __ballot(open != 0 && deg > kCoop);
         while (big) {
@@ -167,6 +177,13 @@ __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t 
             ++nv;
             mf += static_cast<unsigned long long>(push_degree(push, v));
             bits += static_cast<unsigned long long>(__popcll(fresh));
+        }
+    }
+    if (kDiag) {
+        for (int i = 0; i < 5; ++i) {
+            unsigned long long x = dg[i];
+            for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+            if (lane() == 0 && x) atomicAdd(&g_ms_diag[i], x);
         }
     }
     count_flush(cnt, nv, mf, bits);
@@ -410,7 +427,11 @@ hipError_t k_ms_pull(const View& pull, const View& push, int64_t n_active, uint6
                      int32_t next_level, hipStream_t s) {
     // TGO_MS_STEP: entries a lane loads per round trip of its own list (8 default; 16 probe)
     static const int step = [] { const char* e = std::getenv("TGO_MS_STEP"); return e ? std::atoi(e) : 8; }();
-    if (step == 16)
+    static const bool diag = [] { const char* e = std::getenv("TGO_MS_DIAG"); return e && std::atoi(e) != 0; }();
+    if (diag)
+        ms_pull<8, true><<<grid_for(n_active, 8192), kBlock, 0, s>>>(pull, push, n_active, full, fr, fbm, vis, nx, lvl, cnt,
+                                                                   next_level);
+    else if (step == 16)
         ms_pull<16><<<grid_for(n_active, 8192), kBlock, 0, s>>>(pull, push, n_active, full, fr, fbm, vis, nx, lvl, cnt,
                                                                next_level);
     else if (step == 4)
@@ -420,6 +441,16 @@ hipError_t k_ms_pull(const View& pull, const View& push, int64_t n_active, uint6
         ms_pull<8><<<grid_for(n_active, 8192), kBlock, 0, s>>>(pull, push, n_active, full, fr, fbm, vis, nx, lvl, cnt,
                                                               next_level);
     return hipGetLastError();
+}
+// The pull diagnostics since the last call (zeroed after the read).
+hipError_t k_ms_diag_take(unsigned long long* out5, hipStream_t s) {
+    hipError_t e = hipMemcpyFromSymbolAsync(out5, HIP_SYMBOL(g_ms_diag), 5 * sizeof(unsigned long long), 0,
+                                            hipMemcpyDeviceToHost, s);
+    if (e != hipSuccess) return e;
+    static const unsigned long long zero[8] = {};
+    e = hipMemcpyToSymbolAsync(HIP_SYMBOL(g_ms_diag), zero, sizeof(zero), 0, hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return e;
+    return hipStreamSynchronize(s);
 }
 hipError_t k_ms_fbitmap(const uint64_t* fr, int64_t n, uint64_t* fbm, hipStream_t s) {
     const int64_t words = (n + 63) / 64;

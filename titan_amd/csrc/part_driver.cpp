@@ -1,0 +1,402 @@
+// part_driver.cpp — the partitioned multi-source BFS sweep driven from C++.
+//
+// titan_amd/distributed.py drives the partitioned (multi-GPU) programs from Python: every
+// level is a local step through the C-ABI plus an RCCL collective through torch.distributed,
+// and each level pays Python dispatch and several host round trips.  tgo_part_msbfs_run runs
+// the same protocol (dense level: in-place all-gather of the owned frontier masks + pull;
+// sparse level: push into candidate masks, packed (owner-local id, mask) pairs in a fixed-
+// capacity or sized all-to-all, settle; level counts all-reduced on the device) as one C++
+// loop over an exchange object:
+//   * tgo_exchange_rccl_*  : RCCL over xGMI on the ctx stream (production, one process per GPU);
+//   * tgo_exchange_local_group : ranks as threads of one process on one device (tests: the
+//     same loop at world 2 / 4 on a one-GPU box), collectives as device-to-device copies
+//     between the ranks' buffers at a barrier.
+// The reference has no multi-process OLAP executor (FulgoraGraphComputer.java:117-311 is one
+// JVM); this is the multi-GPU form of ShortestDistanceVertexProgram with unit weights
+// (ShortestDistanceVertexProgram.java:96-130) over bothE.
+#include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include "engine.hpp"
+#include "../../include/titan_gpu_olap_part.h"
+
+// Exchange: the four collectives the sweep needs, all on device buffers, ordered on `s`.
+struct tgo_exchange {
+    int world = 1, rank = 0;
+    virtual ~tgo_exchange() = default;
+    // buf holds `world` slices of `bytes` (this rank's at rank * bytes); every rank's slice
+    // ends up in every buffer
+    virtual int all_gather(void* buf, size_t bytes, hipStream_t s) = 0;
+    // send / recv hold `world` blocks of `bytes`: block r of send goes to rank r, block p of
+    // recv comes from rank p
+    virtual int all_to_all(const void* send, void* recv, size_t bytes, hipStream_t s) = 0;
+    // per-peer byte counts and offsets (host arrays of `world`)
+    virtual int all_to_allv(const void* send, const size_t* sb, const size_t* so, void* recv, const size_t* rb,
+                            const size_t* ro, hipStream_t s) = 0;
+    virtual int all_reduce_sum(int64_t* buf, size_t count, hipStream_t s) = 0;
+    // a rank leaving the protocol early releases the peers waiting on it (in-process group)
+    virtual void abort() {}
+    std::string err;
+};
+
+namespace {
+
+using tgo::copy_chunked;
+
+// ------------------------------------------------------------------ RCCL (production)
+struct RcclExchange : tgo_exchange {
+    ncclComm_t comm = nullptr;
+    ~RcclExchange() override {
+        if (comm) (void)ncclCommDestroy(comm);
+    }
+    int check(ncclResult_t r, const char* what) {
+        if (r == ncclSuccess) return TGO_OK;
+        err = std::string(what) + ": " + ncclGetErrorString(r);
+        return TGO_E_HIP;
+    }
+    int all_gather(void* buf, size_t bytes, hipStream_t s) override {
+        if (world == 1) return TGO_OK;
+        char* b = static_cast<char*>(buf);
+        return check(ncclAllGather(b + rank * bytes, b, bytes, ncclChar, comm, s), "ncclAllGather");
+    }
+    int all_to_all(const void* send, void* recv, size_t bytes, hipStream_t s) override {
+        if (world == 1) return copy_on(send, recv, bytes, s);
+        return check(ncclAllToAll(send, recv, bytes, ncclChar, comm, s), "ncclAllToAll");
+    }
+    int all_to_allv(const void* send, const size_t* sb, const size_t* so, void* recv, const size_t* rb,
+                    const size_t* ro, hipStream_t s) override {
+        if (world == 1) return copy_on(static_cast<const char*>(send) + so[0], static_cast<char*>(recv) + ro[0], sb[0], s);
+        int rc = check(ncclGroupStart(), "ncclGroupStart");
+        for (int p = 0; !rc && p < world; ++p) {
+            if (sb[p]) rc = check(ncclSend(static_cast<const char*>(send) + so[p], sb[p], ncclChar, p, comm, s), "ncclSend");
+            if (!rc && rb[p]) rc = check(ncclRecv(static_cast<char*>(recv) + ro[p], rb[p], ncclChar, p, comm, s), "ncclRecv");
+        }
+        const int rc2 = check(ncclGroupEnd(), "ncclGroupEnd");
+        return rc ? rc : rc2;
+    }
+    int all_reduce_sum(int64_t* buf, size_t count, hipStream_t s) override {
+        if (world == 1) return TGO_OK;
+        return check(ncclAllReduce(buf, buf, count, ncclInt64, ncclSum, comm, s), "ncclAllReduce");
+    }
+    int copy_on(const void* src, void* dst, size_t bytes, hipStream_t s) {
+        if (!bytes || src == dst) return TGO_OK;
+        const hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s);
+        if (e == hipSuccess) return TGO_OK;
+        err = hipGetErrorString(e);
+        return TGO_E_HIP;
+    }
+};
+
+// ------------------------------------------------------------------ in-process group (tests)
+// Ranks are threads of one process; a collective is: finish the own stream, publish the
+// buffer pointers, barrier, copy what this rank needs from the peers' buffers (device to
+// device, own stream), finish, barrier (the peers' buffers may be reused afterwards).
+struct LocalGroup {
+    int world;
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    long generation = 0;
+    bool broken = false;
+    struct Slot { const void* send; void* recv; const size_t* sb; const size_t* so; std::vector<int64_t> red; };
+    std::vector<Slot> slot;
+    explicit LocalGroup(int w) : world(w), slot(w) {}
+    bool barrier() {
+        std::unique_lock<std::mutex> lk(mu);
+        if (broken) return false;
+        const long gen = generation;
+        if (++arrived == world) {
+            arrived = 0;
+            ++generation;
+            cv.notify_all();
+            return true;
+        }
+        const bool ok = cv.wait_for(lk, std::chrono::seconds(60), [&] { return generation != gen || broken; });
+        if (!ok || broken) { broken = true; cv.notify_all(); return false; }
+        return true;
+    }
+};
+
+struct LocalExchange : tgo_exchange {
+    std::shared_ptr<LocalGroup> g;
+    void abort() override {
+        std::lock_guard<std::mutex> lk(g->mu);
+        g->broken = true;
+        g->cv.notify_all();
+    }
+    int fail_msg(const char* m) { err = m; return TGO_E_STATE; }
+    int sync(hipStream_t s) {
+        const hipError_t e = hipStreamSynchronize(s);
+        if (e == hipSuccess) return TGO_OK;
+        err = hipGetErrorString(e);
+        return TGO_E_HIP;
+    }
+    int copy(void* dst, const void* src, size_t bytes, hipStream_t s) {
+        if (!bytes || dst == src) return TGO_OK;
+        const hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s);
+        if (e == hipSuccess) return TGO_OK;
+        err = hipGetErrorString(e);
+        return TGO_E_HIP;
+    }
+    template <class F>
+    int collective(hipStream_t s, const LocalGroup::Slot& mine, F&& body) {
+        int rc = sync(s);
+        g->slot[rank] = mine;
+        if (!g->barrier()) return fail_msg("local exchange: a rank failed or timed out");
+        if (!rc) rc = body();
+        if (!rc) rc = sync(s);
+        if (!g->barrier()) return fail_msg("local exchange: a rank failed or timed out");
+        return rc;
+    }
+    int all_gather(void* buf, size_t bytes, hipStream_t s) override {
+        return collective(s, {buf, buf, nullptr, nullptr, {}}, [&]() -> int {
+            for (int p = 0; p < world; ++p)
+                if (p != rank) {
+                    const char* src = static_cast<const char*>(g->slot[p].recv) + p * bytes;
+                    if (int rc = copy(static_cast<char*>(buf) + p * bytes, src, bytes, s)) return rc;
+                }
+            return TGO_OK;
+        });
+    }
+    int all_to_all(const void* send, void* recv, size_t bytes, hipStream_t s) override {
+        return collective(s, {send, recv, nullptr, nullptr, {}}, [&]() -> int {
+            for (int p = 0; p < world; ++p) {
+                const char* src = static_cast<const char*>(g->slot[p].send) + rank * bytes;
+                if (int rc = copy(static_cast<char*>(recv) + p * bytes, src, bytes, s)) return rc;
+            }
+            return TGO_OK;
+        });
+    }
+    int all_to_allv(const void* send, const size_t* sb, const size_t* so, void* recv, const size_t* rb,
+                    const size_t* ro, hipStream_t s) override {
+        return collective(s, {send, recv, sb, so, {}}, [&]() -> int {
+            for (int p = 0; p < world; ++p) {
+                const LocalGroup::Slot& q = g->slot[p];
+                if (q.sb[rank] != rb[p]) return fail_msg("local exchange: all_to_allv sizes do not match");
+                const char* src = static_cast<const char*>(q.send) + q.so[rank];
+                if (int rc = copy(static_cast<char*>(recv) + ro[p], src, rb[p], s)) return rc;
+            }
+            return TGO_OK;
+        });
+    }
+    int all_reduce_sum(int64_t* buf, size_t count, hipStream_t s) override {
+        std::vector<int64_t> mine(count);
+        int rc = sync(s);
+        if (!rc) {
+            const hipError_t e = hipMemcpy(mine.data(), buf, count * sizeof(int64_t), hipMemcpyDeviceToHost);
+            if (e != hipSuccess) { err = hipGetErrorString(e); rc = TGO_E_HIP; }
+        }
+        g->slot[rank] = {nullptr, nullptr, nullptr, nullptr, mine};
+        if (!g->barrier()) return fail_msg("local exchange: a rank failed or timed out");
+        std::vector<int64_t> sum(count, 0);
+        for (int p = 0; p < world; ++p)
+            for (size_t i = 0; i < count && i < g->slot[p].red.size(); ++i) sum[i] += g->slot[p].red[i];
+        if (!g->barrier()) return fail_msg("local exchange: a rank failed or timed out");
+        if (rc) return rc;
+        const hipError_t e = hipMemcpyAsync(buf, sum.data(), count * sizeof(int64_t), hipMemcpyHostToDevice, s);
+        if (e != hipSuccess) { err = hipGetErrorString(e); return TGO_E_HIP; }
+        return sync(s);          // sum is a local: the copy must finish before it goes away
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+int tgo_exchange_rccl_id(uint8_t* id_out) {
+    if (!id_out) return TGO_E_INVALID;
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return TGO_E_HIP;
+    std::memcpy(id_out, &id, sizeof(id));
+    return TGO_OK;
+}
+
+int tgo_exchange_rccl_create(int32_t world, int32_t rank, const uint8_t* id, int32_t device, tgo_exchange** out) {
+    if (!id || !out || world < 1 || rank < 0 || rank >= world) return TGO_E_INVALID;
+    *out = nullptr;
+    if (hipSetDevice(device) != hipSuccess) return TGO_E_HIP;
+    auto x = std::make_unique<RcclExchange>();
+    x->world = world;
+    x->rank = rank;
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof(uid));
+    if (ncclCommInitRank(&x->comm, world, uid, rank) != ncclSuccess) return TGO_E_HIP;
+    *out = x.release();
+    return TGO_OK;
+}
+
+int tgo_exchange_local_group(int32_t world, tgo_exchange** ranks_out) {
+    if (!ranks_out || world < 1 || world > 64) return TGO_E_INVALID;
+    auto g = std::make_shared<LocalGroup>(world);
+    for (int r = 0; r < world; ++r) {
+        auto* x = new LocalExchange();
+        x->world = world;
+        x->rank = r;
+        x->g = g;
+        ranks_out[r] = x;
+    }
+    return TGO_OK;
+}
+
+void tgo_exchange_destroy(tgo_exchange* x) { delete x; }
+
+const char* tgo_exchange_last_error(const tgo_exchange* x) { return x ? x->err.c_str() : "null exchange"; }
+
+}  // extern "C"
+
+namespace tgo {
+
+// ctx accessors (api.cpp): the ctx stream, partition dimensions, error text
+hipStream_t part_stream(tgo_ctx* ctx);
+int part_dims(tgo_ctx* ctx, int64_t* n_local, int64_t* lo, int64_t* n_global, int64_t* entries);
+int part_fail(tgo_ctx* ctx, int code, const std::string& msg);
+int part_scratch(tgo_ctx* ctx, void** p, int64_t bytes, int slot);
+int64_t* part_dcounts_of(tgo_ctx* ctx);
+template <class T>
+int scratch(tgo_ctx* ctx, T*& p, int64_t count, int slot) {
+    void* q = nullptr;
+    const int rc = part_scratch(ctx, &q, count * static_cast<int64_t>(sizeof(T)), slot);
+    p = static_cast<T*>(q);
+    return rc;
+}
+
+}  // namespace tgo
+
+using namespace tgo;
+
+extern "C" int tgo_part_msbfs_run(tgo_ctx* ctx, tgo_exchange* x, const int64_t* seeds, int32_t nseeds, int32_t max_depth,
+                                  double ms_alpha, int64_t fixed_bytes, int64_t* reached, int64_t* entries,
+                                  int32_t* levels_out) {
+    if (!ctx) return TGO_E_INVALID;
+    if (!x || !seeds || nseeds < 1 || nseeds > TGO_MAX_SOURCES || max_depth < 0)
+        return part_fail(ctx, TGO_E_INVALID, "tgo_part_msbfs_run: bad arguments");
+    int64_t nl = 0, lo = 0, ng = 0, ent = 0;
+    int rc = part_dims(ctx, &nl, &lo, &ng, &ent);
+    if (rc) return rc;
+    const int W = x->world;
+    if (static_cast<int64_t>(W) * nl != ng || lo != static_cast<int64_t>(x->rank) * nl)
+        return part_fail(ctx, TGO_E_INVALID, "tgo_part_msbfs_run: the exchange's world / rank do not match the partition");
+    hipStream_t st = part_stream(ctx);
+    auto xfail = [&](int code) { return part_fail(ctx, code, "exchange: " + x->err); };
+    // scratch (ctx-owned, reused): two alternating global mask buffers, the candidate masks,
+    // the pair buffers, the device counts and the split sizes
+    uint64_t *g0 = nullptr, *g1 = nullptr, *cand = nullptr;
+    int64_t *send = nullptr, *recv = nullptr, *dc = nullptr, *sizes = nullptr;
+    const int64_t pairs_cap = 2 * ng + 2 * W;
+    if ((rc = scratch(ctx, g0, ng, 0)) || (rc = scratch(ctx, g1, ng, 1)) || (rc = scratch(ctx, cand, ng, 2)) ||
+        (rc = scratch(ctx, send, pairs_cap, 3)) || (rc = scratch(ctx, recv, pairs_cap, 4)) ||
+        (rc = scratch(ctx, dc, 3 + 2 * TGO_MAX_SOURCES, 5)) || (rc = scratch(ctx, sizes, 2 * W, 6)))
+        return rc;
+    int64_t* const caller_dc = part_dcounts_of(ctx);       // restored at the end
+    uint64_t* glob[2] = {g0, g1};
+    // entry-less tail of both mask buffers and the candidate masks start zero (the steps keep
+    // them so); only this rank's slices are written by the local steps
+    if (hipMemsetAsync(g0, 0, ng * 8, st) != hipSuccess || hipMemsetAsync(g1, 0, ng * 8, st) != hipSuccess ||
+        hipMemsetAsync(cand, 0, ng * 8, st) != hipSuccess)
+        return part_fail(ctx, TGO_E_HIP, "tgo_part_msbfs_run: memset");
+    int64_t* hc = nullptr;                                  // pinned host view of the counts
+    if (hipHostMalloc(reinterpret_cast<void**>(&hc), 4 * sizeof(int64_t), hipHostMallocDefault) != hipSuccess)
+        return part_fail(ctx, TGO_E_HIP, "tgo_part_msbfs_run: pinned counts");
+    struct Pinned { int64_t* p; ~Pinned() { if (p) (void)hipHostFree(p); } } pin{hc};
+    // global counts: write local {a, b} to dc, all-reduce, read back (one sync)
+    auto global2 = [&](int64_t a, int64_t b, int64_t* out) -> int {
+        hc[0] = a; hc[1] = b;
+        if (hipMemcpyAsync(dc, hc, 2 * sizeof(int64_t), hipMemcpyHostToDevice, st) != hipSuccess)
+            return part_fail(ctx, TGO_E_HIP, "counts upload");
+        if (int r = x->all_reduce_sum(dc, 2, st)) return xfail(r);
+        if (hipMemcpyAsync(hc, dc, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            return part_fail(ctx, TGO_E_HIP, "counts read");
+        out[0] = hc[0]; out[1] = hc[1];
+        return TGO_OK;
+    };
+    int64_t tot[2];
+    if ((rc = global2(ent, 0, tot))) return rc;
+    const int64_t total = tot[0];
+    uint64_t* fr = glob[0] + lo;
+    uint64_t* frn = glob[1] + lo;
+    int64_t c[2];
+    if ((rc = tgo_part_ms_begin(ctx, seeds, nseeds, fr, c))) return rc;
+    int64_t g[2];
+    if ((rc = global2(c[0], c[1], g))) return rc;
+    int64_t nf = g[0], mf = g[1];
+    // level counts stay on the device: the steps publish {next queue, its entries, own queue}
+    if ((rc = tgo_part_device_counts(ctx, dc))) return rc;
+    int levels = 0;
+    for (int level = 0; level < max_depth && nf > 0; ++level) {
+        if (static_cast<double>(mf) * ms_alpha > static_cast<double>(total)) {
+            if (int r = x->all_gather(glob[0], static_cast<size_t>(nl) * 8, st)) { rc = xfail(r); break; }
+            if ((rc = tgo_part_ms_pull(ctx, level, glob[0], frn, nullptr))) break;
+        } else {
+            if ((rc = tgo_part_ms_push(ctx, level, fr, cand))) break;
+            const int64_t cap = std::min<int64_t>(mf, nl);
+            if (cap > 0 && static_cast<int64_t>(W) * (cap + 1) * 16 <= fixed_bytes) {
+                if ((rc = tgo_part_ms_pack_fixed(ctx, cand, W, cap, send))) break;
+                if (int r = x->all_to_all(send, recv, static_cast<size_t>(cap + 1) * 16, st)) { rc = xfail(r); break; }
+                if ((rc = tgo_part_ms_settle_fixed(ctx, level, recv, W, cap, frn, nullptr))) break;
+            } else {
+                // sized pairs: split sizes on the device, one all-to-all of them, one host read
+                if ((rc = tgo_part_ms_pack_dev(ctx, cand, W, send, sizes))) break;
+                if (int r = x->all_to_all(sizes, sizes + W, 8, st)) { rc = xfail(r); break; }
+                std::vector<int64_t> both(2 * W);
+                if (hipMemcpyAsync(both.data(), sizes, 2 * W * sizeof(int64_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                    hipStreamSynchronize(st) != hipSuccess) { rc = part_fail(ctx, TGO_E_HIP, "split sizes read"); break; }
+                std::vector<size_t> sb(W), so(W), rb(W), ro(W);
+                std::vector<int64_t> rpairs(W);
+                size_t a = 0, b = 0;
+                for (int p = 0; p < W; ++p) {
+                    sb[p] = static_cast<size_t>(both[p]) * 8; so[p] = a; a += sb[p];
+                    rb[p] = static_cast<size_t>(both[W + p]) * 8; ro[p] = b; b += rb[p];
+                    rpairs[p] = both[W + p] / 2;
+                }
+                if (int r = x->all_to_allv(send, sb.data(), so.data(), recv, rb.data(), ro.data(), st)) { rc = xfail(r); break; }
+                if ((rc = tgo_part_ms_settle_pairs(ctx, level, recv, rpairs.data(), W, frn, nullptr))) break;
+            }
+        }
+        std::swap(fr, frn);
+        std::swap(glob[0], glob[1]);
+        // global {next frontier, its entries}; this rank's queue length back to the engine
+        if (int r = x->all_reduce_sum(dc, 2, st)) { rc = xfail(r); break; }
+        if (hipMemcpyAsync(hc, dc, 3 * sizeof(int64_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess) { rc = part_fail(ctx, TGO_E_HIP, "counts read"); break; }
+        nf = hc[0];
+        mf = hc[1];
+        if ((rc = tgo_part_set_local_qlen(ctx, hc[2]))) break;
+        ++levels;
+    }
+    const int rc_off = tgo_part_device_counts(ctx, caller_dc);
+    if (rc) {
+        x->abort();
+        return rc;
+    }
+    if (rc_off) return rc_off;
+    std::vector<int64_t> r(nseeds), e(nseeds);
+    if ((rc = tgo_part_ms_end(ctx, r.data(), e.data()))) return rc;
+    if (reached || entries) {
+        std::vector<int64_t> both(2 * nseeds);
+        std::copy(r.begin(), r.end(), both.begin());
+        std::copy(e.begin(), e.end(), both.begin() + nseeds);
+        int64_t* d = dc + 3;
+        if (hipMemcpyAsync(d, both.data(), both.size() * 8, hipMemcpyHostToDevice, st) != hipSuccess)
+            return part_fail(ctx, TGO_E_HIP, "stats upload");
+        if (int q = x->all_reduce_sum(d, both.size(), st)) return xfail(q);
+        if (hipMemcpyAsync(both.data(), d, both.size() * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            return part_fail(ctx, TGO_E_HIP, "stats read");
+        for (int i = 0; i < nseeds; ++i) {
+            if (reached) reached[i] = both[i];
+            if (entries) entries[i] = both[nseeds + i];
+        }
+    }
+    if (levels_out) *levels_out = levels;
+    return TGO_OK;
+}

@@ -701,6 +701,68 @@ def distributed_msbfs(backend, seeds, max_depth: int, ms_alpha: float = 12.0, st
     return r, e, levels
 
 
+class NativeExchange:
+    """An exchange object of the native partitioned driver (titan_gpu_olap_part.h
+    tgo_exchange_*): RCCL over xGMI (rccl(), one process per GPU) or an in-process group of
+    thread ranks on one device (local_group(), tests).  Destroyed with the wrapper."""
+
+    def __init__(self, handle):
+        self.h = C.c_void_p(handle)
+
+    @classmethod
+    def rccl(cls, device: int, group=None, comm=None):
+        """Rank 0 makes the RCCL unique id, every rank receives it over `comm` (an all-gather
+        of 128 bytes per rank, rank 0's slice taken) and joins the communicator."""
+        lib = L.load()
+        cm = _comm(comm, group)
+        uid = np.zeros(128, np.uint8)
+        if cm.rank == 0 and lib.tgo_exchange_rccl_id(L.ptr(uid, C.c_uint8)):
+            raise RuntimeError("tgo_exchange_rccl_id failed")
+        dev = torch.device("cuda", device) if torch.cuda.is_available() else torch.device("cpu")
+        out = torch.empty(128 * cm.world, dtype=torch.uint8, device=dev)
+        cm.all_gather_into_tensor(out, torch.from_numpy(uid).to(dev))
+        uid = np.ascontiguousarray(out[:128].cpu().numpy())
+        h = C.c_void_p()
+        rc = lib.tgo_exchange_rccl_create(cm.world, cm.rank, L.ptr(uid, C.c_uint8), device, C.byref(h))
+        if rc:
+            raise RuntimeError(f"tgo_exchange_rccl_create rc={rc}")
+        return cls(h.value)
+
+    @classmethod
+    def local_group(cls, world: int):
+        lib = L.load()
+        hs = (C.c_void_p * world)()
+        if lib.tgo_exchange_local_group(world, hs):
+            raise RuntimeError("tgo_exchange_local_group failed")
+        return [cls(h) for h in hs]
+
+    def __del__(self):
+        if getattr(self, "h", None) is not None and self.h.value:
+            L.load().tgo_exchange_destroy(self.h)
+            self.h = None
+
+
+def distributed_msbfs_native(backend, seeds, max_depth: int, exchange: NativeExchange, ms_alpha: float = 12.0,
+                             fixed_exchange_bytes: int = None):
+    """distributed_msbfs as ONE native call (tgo_part_msbfs_run): the same protocol, the level
+    loop and its collectives in C++ on the engine's stream.  Returns (per-seed global reached
+    vertices, per-seed reached entries, levels)."""
+    if fixed_exchange_bytes is None:
+        fixed_exchange_bytes = FIXED_EXCHANGE_BYTES
+    sd = np.ascontiguousarray(seeds, np.int64)
+    r = np.zeros(len(sd), np.int64)
+    e = np.zeros(len(sd), np.int64)
+    lv = C.c_int32()
+    lib = backend.e.lib
+    rc = lib.tgo_part_msbfs_run(backend.e.ctx, exchange.h, L.ptr(sd, C.c_int64), len(sd), int(max_depth),
+                                float(ms_alpha), int(fixed_exchange_bytes), L.ptr(r, C.c_int64), L.ptr(e, C.c_int64),
+                                C.byref(lv))
+    if rc:
+        from .engine import TitanException
+        raise TitanException(rc, (lib.tgo_last_error(backend.e.ctx) or b"").decode())
+    return r, e, lv.value
+
+
 INT64_MAX = (1 << 63) - 1
 
 
