@@ -409,7 +409,7 @@ def run_partitioned(args, world, rank, local_rank):
 
     def sweep(stats):
         if xchg is not None:
-            return distributed_msbfs_native(bfs_be, roots_s, ns, xchg)
+            return distributed_msbfs_native(bfs_be, roots_s, ns, xchg, stats=stats)
         return distributed_msbfs(bfs_be, roots_s, ns, stats=stats)
     # per-root reached entries (untimed) for GTEPS
     _, mR, depth_ms = sweep(True)

@@ -158,3 +158,30 @@ def test_vertex_cut_rows_keep_the_host_assembly(monkeypatch):
     rows, vids, sd, npz = load_fixture("partition_groups")
     h, d = _rows_both(monkeypatch, rows, sd, L.SCOPE_BOTH_E, 100000, batch_rows=5)
     _same(h, d)
+
+
+# ---------------------------------------------------------------- PageRank layout (pr_layout.hip)
+@pytest.mark.parametrize("scale,hot,seg,tile", [(14, "1024", "512", None), (14, "600", "333", "8192"), (20, None, None, None)])
+def test_device_pagerank_layout_bitwise(monkeypatch, scale, hot, seg, tile):
+    """The cache-blocked PageRank layout built on the device (hot CSR, cold pieces, blocks,
+    source-sorted packing of hot tiles and cold blocks) equals the host build: every sum runs
+    in the same fixed order, so the ranks are bitwise identical (and match the oracle)."""
+    import fulgora as fr
+    for k, v in (("TGO_PR_HOT", hot), ("TGO_PR_SEG", seg), ("TGO_PR_HOT_TILE", tile)):
+        if v is None:
+            monkeypatch.delenv(k, raising=False)
+        else:
+            monkeypatch.setenv(k, v)
+    n = 1 << scale
+    src, dst, _ = rmat_edges(scale, 16, seed=71)
+    res = []
+    for host in ("1", "0"):
+        monkeypatch.setenv("TGO_HOST_ASSEMBLY", host)
+        eng = Engine(hard_query_limit=300).load_edges(n, src, dst, L.SCOPE_IN_E, apply_cap=True)
+        res.append(eng.pagerank(0.85, n, 12))
+    monkeypatch.delenv("TGO_HOST_ASSEMBLY")
+    assert np.array_equal(res[0], res[1])
+    if scale <= 14:
+        opr, _ = fr.OracleGraph.from_edges(n, src, dst, hard_limit=300).pagerank(0.85, n, 12)
+        fin = np.isfinite(opr)
+        assert np.abs(res[1][fin] - opr[fin]).sum() <= 1e-6

@@ -170,16 +170,79 @@ hipError_t upload_row_blocks(tgo_ctx* ctx, const std::vector<int64_t>& off, RowB
     return hipSuccess;
 }
 
+// upload_row_blocks with the tiles packed on the device, in place in d_adj (pr_layout.hip):
+// the same blocks (built on the host from the offsets) and the same packed words.  *packed =
+// false (d_adj untouched) when a source is too wide for the slot space (pack_tiles' rule).
+int upload_row_blocks_dev(tgo_ctx* ctx, const std::vector<int64_t>& off, RowBlocks& rb, int32_t* d_adj,
+                          int32_t max_src, bool* packed, int64_t tile, int shift) {
+    std::vector<int64_t> blk, crow, cbeg, cend, lrow, lch;
+    build_row_blocks(off, tile, kMaxRows, blk, crow, cbeg, cend, lrow, lch);
+    *packed = false;
+    const int64_t src_limit = shift == kPackShift ? (int64_t(1) << (31 - shift)) : (int64_t(1) << (32 - shift));
+    if (d_adj && shift >= 1 && shift <= 20 && tile <= (int64_t(1) << shift) && max_src < src_limit) {
+        // tiles in entry order: short blocks, and the chunks of each long row (they cover it)
+        std::vector<std::pair<int64_t, int64_t>> t;
+        for (size_t b = 0; b + 1 < blk.size(); ++b) {
+            const int64_t s0 = off[blk[b]], s1 = off[blk[b + 1]];
+            if (s1 - s0 <= tile) t.emplace_back(s0, s1);
+        }
+        for (size_t c = 0; c < cbeg.size(); ++c) t.emplace_back(cbeg[c], cend[c]);
+        std::sort(t.begin(), t.end());
+        std::vector<int64_t> ts(t.size());
+        for (size_t i = 0; i < t.size(); ++i) ts[i] = t[i].first;
+        std::string err;
+        if (int rc = pack_tiles_device(d_adj, off.back(), ts, nullptr, shift, ctx->stream, err)) return fail(ctx, rc, err);
+        *packed = true;
+    }
+    rb.nblocks = static_cast<int64_t>(blk.size()) - 1;
+    rb.nchunks = static_cast<int64_t>(crow.size());
+    rb.nlong = static_cast<int64_t>(lrow.size());
+    HIP_TRY(upload(ctx, rb.blk, blk));
+    HIP_TRY(upload(ctx, rb.chunk_row, crow));
+    HIP_TRY(upload(ctx, rb.chunk_beg, cbeg));
+    HIP_TRY(upload(ctx, rb.chunk_end, cend));
+    HIP_TRY(upload(ctx, rb.long_row, lrow));
+    HIP_TRY(upload(ctx, rb.long_chunk, lch));
+    std::vector<int64_t> desc(2 * blk.size());
+    for (size_t b = 0; b < blk.size(); ++b) { desc[2 * b] = blk[b]; desc[2 * b + 1] = off[blk[b]]; }
+    HIP_TRY(upload(ctx, rb.bdesc, desc));
+    return TGO_OK;
+}
+
 // Cache-blocked PageRank in-lists of the rows [0, n_rows) (rows past n_rows have no entries)
-// over sources [0, n_src): build on the host, upload into cb.
+// over sources [0, n_src): built on the device from the uploaded in-lists (d_off / d_adj,
+// pr_layout.hip) unless TGO_HOST_ASSEMBLY=1 (or a row is not sorted by source), then on the
+// host; uploaded into cb.
 int upload_cold_blocks(tgo_ctx* ctx, const std::vector<int64_t>& off, const std::vector<int32_t>& adj,
-                       int64_t n_src, int64_t hot, int64_t n_rows, ColdBlocks& cb, bool& ready) {
+                       int64_t n_src, int64_t hot, int64_t n_rows, ColdBlocks& cb, bool& ready,
+                       const int64_t* d_off = nullptr, const int32_t* d_adj = nullptr) {
     cb = ColdBlocks();
     ready = false;
     HostColdBlocks hc;
-    if (!build_cold_blocks(off, adj, n_src, hot, env_i64("TGO_PR_SEG", kPrSegDefault), kTile, kMaxRows,
-                           threads_of(ctx), env_i64("TGO_PR_CPACK", 1) != 0, hc))
-        return TGO_OK;                                    // too small to block: plain gather
+    static const bool trace = env_i64("TGO_TRACE", 0) != 0;
+    auto t_last = std::chrono::steady_clock::now();
+    auto lap = [&](const char* what) {
+        if (!trace) return;
+        const auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[tgo]   cold %-18s %8.1f ms\n", what, std::chrono::duration<double, std::milli>(now - t_last).count());
+        t_last = now;
+    };
+    bool on_dev = false;
+    if (d_off && d_adj && env_i64("TGO_HOST_ASSEMBLY", 0) == 0) {
+        std::string err;
+        if (int rc = build_cold_blocks_device(d_off, d_adj, static_cast<int64_t>(off.size()) - 1,
+                                              static_cast<int64_t>(adj.size()), n_src, hot,
+                                              env_i64("TGO_PR_SEG", kPrSegDefault), kTile, kMaxRows,
+                                              env_i64("TGO_PR_CPACK", 1) != 0, hc, on_dev, ctx->stream, err))
+            return fail(ctx, rc, err);
+        if (on_dev) lap("build (device)");
+    }
+    if (!on_dev) {
+        if (!build_cold_blocks(off, adj, n_src, hot, env_i64("TGO_PR_SEG", kPrSegDefault), kTile, kMaxRows,
+                               threads_of(ctx), env_i64("TGO_PR_CPACK", 1) != 0, hc))
+            return TGO_OK;                                // too small to block: plain gather
+        lap("build (host)");
+    }
     cb.hot = hc.hot;
     cb.seg = hc.seg;
     cb.npieces = static_cast<int64_t>(hc.cpid.size());
@@ -198,16 +261,33 @@ int upload_cold_blocks(tgo_ctx* ctx, const std::vector<int64_t>& off, const std:
     cb.num_cus = ctx->num_cus;
     const bool pack = env_i64("TGO_PR_PACK", 1) != 0;
     if (!pack) cb.hot_tile = static_cast<int>(kTile), cb.hot_shift = kPackShift;
-    HIP_TRY(upload_row_blocks(ctx, hoff_act, cb.rb_hot, pack ? &hc.hadj : nullptr, &cb.packed, cb.hot_tile,
-                              cb.hot_shift));
-    if (!cb.packed && cb.hot_tile != kTile) {      // sources too wide for the slot space: the 4096 form
-        cb.hot_tile = static_cast<int>(kTile);
-        cb.hot_shift = kPackShift;
-        cb.rb_hot = RowBlocks();
-        HIP_TRY(upload_row_blocks(ctx, hoff_act, cb.rb_hot, pack ? &hc.hadj : nullptr, &cb.packed));
+    if (on_dev) {                                   // hot tiles packed on the device
+        HIP_TRY(upload(ctx, cb.hcsr.adj, hc.hadj));
+        const int32_t max_src = static_cast<int32_t>(std::min<int64_t>(hot, n_src) - 1);
+        if (int rc = upload_row_blocks_dev(ctx, hoff_act, cb.rb_hot, pack ? cb.hcsr.adj : nullptr, max_src, &cb.packed,
+                                           cb.hot_tile, cb.hot_shift))
+            return rc;
+        if (pack && !cb.packed && cb.hot_tile != kTile) {
+            cb.hot_tile = static_cast<int>(kTile);
+            cb.hot_shift = kPackShift;
+            cb.rb_hot = RowBlocks();
+            if (int rc = upload_row_blocks_dev(ctx, hoff_act, cb.rb_hot, cb.hcsr.adj, max_src, &cb.packed, kTile,
+                                               kPackShift))
+                return rc;
+        }
+    } else {
+        HIP_TRY(upload_row_blocks(ctx, hoff_act, cb.rb_hot, pack ? &hc.hadj : nullptr, &cb.packed, cb.hot_tile,
+                                  cb.hot_shift));
+        if (!cb.packed && cb.hot_tile != kTile) {  // sources too wide for the slot space: the 4096 form
+            cb.hot_tile = static_cast<int>(kTile);
+            cb.hot_shift = kPackShift;
+            cb.rb_hot = RowBlocks();
+            HIP_TRY(upload_row_blocks(ctx, hoff_act, cb.rb_hot, pack ? &hc.hadj : nullptr, &cb.packed));
+        }
+        HIP_TRY(upload(ctx, cb.hcsr.adj, hc.hadj));
     }
+    lap("hot row blocks+pack");
     HIP_TRY(upload(ctx, cb.hcsr.off, hc.hoff));
-    HIP_TRY(upload(ctx, cb.hcsr.adj, hc.hadj));
     cb.hcsr.nnz = static_cast<int64_t>(hc.hadj.size());
     HIP_TRY(upload(ctx, cb.poff, hc.poff));
     HIP_TRY(upload(ctx, cb.cadj, hc.cadj));
@@ -234,6 +314,7 @@ int upload_cold_blocks(tgo_ctx* ctx, const std::vector<int64_t>& off, const std:
     HIP_TRY(hipMemset(cb.csum, 0, std::max<int64_t>(cb.n_rows, 1) * sizeof(double)));
     cb.n_crows = static_cast<int64_t>(hc.crow.size());
     HIP_TRY(upload(ctx, cb.crow, hc.crow));
+    lap("uploads");
     ready = true;
     return TGO_OK;
 }
@@ -298,7 +379,7 @@ int upload_graph(tgo_ctx* ctx, HostGraph& h, bool allow_segments = true) {
         // rows >= n_active have no entries at all: the hot pass skips them (their rank
         // after any update is (1-a)/N, written once at the end of the program)
         if (int rc = upload_cold_blocks(ctx, h.in.off, h.in.adj, h.n, env_i64("TGO_PR_HOT", kPrHotDefault), g.n_active,
-                                        g.cold_in, g.cold_in_ready))
+                                        g.cold_in, g.cold_in_ready, g.in.off, g.in.adj))
             return rc;
         lap("cold blocks");
     }
@@ -1060,10 +1141,11 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
                                 use_pull ? "pull" : "push", (long long)qlen, (long long)mf, s.hcnt->red[0]);
         static const bool diag = env_double("TGO_MS_DIAG", 0.0) != 0.0;
         if (trace && diag && use_pull) {
-            unsigned long long d[5] = {};
+            unsigned long long d[8] = {};
             HIP_TRY(k_ms_diag_take(d, st));
             std::fprintf(stderr, "[tgo]   pull: %llu entries examined, %llu hot / %llu cold mask gathers, %llu open vertices, "
-                         "%llu stopped early\n", d[0], d[1], d[2], d[3], d[4]);
+                         "%llu stopped early; long lists: %llu, %llu entries examined, %llu stopped early\n",
+                         d[0], d[1], d[2], d[3], d[4], d[6], d[5], d[7]);
         }
         std::swap(fr, nx);
         cur ^= 1;

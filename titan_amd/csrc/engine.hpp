@@ -277,6 +277,12 @@ struct HostColdBlocks {
 bool build_cold_blocks(const std::vector<int64_t>& off, const std::vector<int32_t>& adj, int64_t n_src,
                        int64_t hot, int64_t seg, int64_t tile, int64_t max_pieces, int threads, bool pack,
                        HostColdBlocks& hc);
+// pr_layout.hip: build_cold_blocks / pack_tiles on the device (same arrays)
+int build_cold_blocks_device(const int64_t* d_off, const int32_t* d_adj, int64_t n, int64_t nnz, int64_t n_src,
+                             int64_t hot, int64_t seg, int64_t tile, int64_t max_pieces, bool pack, HostColdBlocks& hc,
+                             bool& built, hipStream_t s, std::string& err);
+int pack_tiles_device(int32_t* d_adj, int64_t m, const std::vector<int64_t>& tstart, const std::vector<int32_t>* tbase,
+                      int shift, hipStream_t s, std::string& err);
 
 struct DevGraph {
     int64_t n = 0;
@@ -442,7 +448,7 @@ hipError_t k_ds_apply(const View& push, const int64_t* recv, int64_t npairs, int
                       int64_t* qdeg_n, Counters* cnt, int64_t thr, hipStream_t s);
 hipError_t k_unpermute_i64(const int64_t* in, const int32_t* perm, int64_t* out, int64_t n, hipStream_t s);
 hipError_t k_ms_seed(const int64_t* seeds, int nseeds, uint64_t* vis, uint64_t* fr, int64_t fr_rows, hipStream_t s);
-hipError_t k_ms_diag_take(unsigned long long* out5, hipStream_t s);
+hipError_t k_ms_diag_take(unsigned long long* out8, hipStream_t s);
 hipError_t k_ms_pull(const View& pull, const View& push, int64_t n_active, uint64_t full, const uint64_t* fr,
                      const uint64_t* fbm, uint64_t* vis, uint64_t* nx, LevelPlanes lvl, Counters* cnt,
                      int32_t next_level, hipStream_t s);

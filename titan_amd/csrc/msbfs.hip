@@ -84,7 +84,8 @@ __device__ __forceinline__ bool in_frontier(const uint64_t* __restrict__ fbm, in
 }
 // Diagnostic tallies of a pull level (TGO_MS_DIAG=1 with TGO_TRACE=1; off in the product):
 // [0] list entries examined, [1] mask gathers of hot neighbours (u < kDiagHot), [2] of cold
-// ones, [3] open vertices, [4] open vertices whose walk stopped early (every open source covered)
+// ones, [3] open vertices, [4] open vertices whose walk stopped early (every open source covered);
+// long lists (wave-cooperative): [5] entries examined, [6] lists, [7] lists that stopped early
 constexpr int32_t kDiagHot = 393216;
 __device__ unsigned long long g_ms_diag[8];
 template <int kStep, bool kDiag = false>       // entries per dependent round trip of a lane's own list
@@ -92,7 +93,7 @@ __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t 
         const uint64_t* __restrict__ fr, const uint64_t* __restrict__ fbm, uint64_t* __restrict__ vis,
         uint64_t* __restrict__ nx, LevelPlanes lvl, Counters* cnt, int32_t next_level) {
     unsigned long long nv = 0, mf = 0, bits = 0;
-    unsigned long long dg[5] = {0, 0, 0, 0, 0};
+    unsigned long long dg[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const int64_t words = (n_active + 63) >> 6;
     // wave w of the block takes word b + w; words past the end run as all-closed lanes.  No
     // block barrier inside: the next frontier is only counted here (ms_queue builds its queue
@@ -162,10 +163,15 @@ __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t 
                     for (int off = 32; off > 0; off >>= 1) m |= __shfl_xor(m, off, 64);
                     a |= m;
                     done = (a & want) == want;
+                    if (kDiag && lane() == src)
+                        for (int j = 0; j < 4; ++j) dg[5] += k + j * 64 < ee ? min<int64_t>(64, ee - k - j * 64) : 0;
                 }
                 if ((a & want) == want) break;
             }
-            if (lane() == src) acc = a;
+            if (lane() == src) {
+                acc = a;
+                if (kDiag) { ++dg[6]; if ((a & want) == want) ++dg[7]; }
+            }
         }
         const uint64_t fresh = acc & open;
         if (v < n_active) {
@@ -180,7 +186,7 @@ __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t 
         }
     }
     if (kDiag) {
-        for (int i = 0; i < 5; ++i) {
+        for (int i = 0; i < 8; ++i) {
             unsigned long long x = dg[i];
             for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
             if (lane() == 0 && x) atomicAdd(&g_ms_diag[i], x);
@@ -443,8 +449,8 @@ hipError_t k_ms_pull(const View& pull, const View& push, int64_t n_active, uint6
     return hipGetLastError();
 }
 // The pull diagnostics since the last call (zeroed after the read).
-hipError_t k_ms_diag_take(unsigned long long* out5, hipStream_t s) {
-    hipError_t e = hipMemcpyFromSymbolAsync(out5, HIP_SYMBOL(g_ms_diag), 5 * sizeof(unsigned long long), 0,
+hipError_t k_ms_diag_take(unsigned long long* out5, hipStream_t s) {  // 8 words
+    hipError_t e = hipMemcpyFromSymbolAsync(out5, HIP_SYMBOL(g_ms_diag), 8 * sizeof(unsigned long long), 0,
                                             hipMemcpyDeviceToHost, s);
     if (e != hipSuccess) return e;
     static const unsigned long long zero[8] = {};

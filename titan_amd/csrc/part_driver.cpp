@@ -46,6 +46,16 @@ struct tgo_exchange {
     // a rank leaving the protocol early releases the peers waiting on it (in-process group)
     virtual void abort() {}
     std::string err;
+    int64_t* pinned = nullptr;      // host counts of the driver (pinned once per exchange)
+    int64_t* host_counts() {
+        if (!pinned && hipHostMalloc(reinterpret_cast<void**>(&pinned), 8 * sizeof(int64_t), hipHostMallocDefault) != hipSuccess)
+            pinned = nullptr;
+        return pinned;
+    }
+    void release_pinned() {
+        if (pinned) (void)hipHostFree(pinned);
+        pinned = nullptr;
+    }
 };
 
 namespace {
@@ -57,6 +67,7 @@ struct RcclExchange : tgo_exchange {
     ncclComm_t comm = nullptr;
     ~RcclExchange() override {
         if (comm) (void)ncclCommDestroy(comm);
+        release_pinned();
     }
     int check(ncclResult_t r, const char* what) {
         if (r == ncclSuccess) return TGO_OK;
@@ -128,6 +139,7 @@ struct LocalGroup {
 
 struct LocalExchange : tgo_exchange {
     std::shared_ptr<LocalGroup> g;
+    ~LocalExchange() override { release_pinned(); }
     void abort() override {
         std::lock_guard<std::mutex> lk(g->mu);
         g->broken = true;
@@ -303,10 +315,8 @@ extern "C" int tgo_part_msbfs_run(tgo_ctx* ctx, tgo_exchange* x, const int64_t* 
     if (hipMemsetAsync(g0, 0, ng * 8, st) != hipSuccess || hipMemsetAsync(g1, 0, ng * 8, st) != hipSuccess ||
         hipMemsetAsync(cand, 0, ng * 8, st) != hipSuccess)
         return part_fail(ctx, TGO_E_HIP, "tgo_part_msbfs_run: memset");
-    int64_t* hc = nullptr;                                  // pinned host view of the counts
-    if (hipHostMalloc(reinterpret_cast<void**>(&hc), 4 * sizeof(int64_t), hipHostMallocDefault) != hipSuccess)
-        return part_fail(ctx, TGO_E_HIP, "tgo_part_msbfs_run: pinned counts");
-    struct Pinned { int64_t* p; ~Pinned() { if (p) (void)hipHostFree(p); } } pin{hc};
+    int64_t* hc = x->host_counts();                         // pinned host view of the counts (kept)
+    if (!hc) return part_fail(ctx, TGO_E_HIP, "tgo_part_msbfs_run: pinned counts");
     // global counts: write local {a, b} to dc, all-reduce, read back (one sync)
     auto global2 = [&](int64_t a, int64_t b, int64_t* out) -> int {
         hc[0] = a; hc[1] = b;
@@ -380,8 +390,9 @@ extern "C" int tgo_part_msbfs_run(tgo_ctx* ctx, tgo_exchange* x, const int64_t* 
     }
     if (rc_off) return rc_off;
     std::vector<int64_t> r(nseeds), e(nseeds);
-    if ((rc = tgo_part_ms_end(ctx, r.data(), e.data()))) return rc;
-    if (reached || entries) {
+    const bool stats = reached || entries;           // the per-seed counts cost a pass over the masks
+    if ((rc = tgo_part_ms_end(ctx, stats ? r.data() : nullptr, stats ? e.data() : nullptr))) return rc;
+    if (stats) {
         std::vector<int64_t> both(2 * nseeds);
         std::copy(r.begin(), r.end(), both.begin());
         std::copy(e.begin(), e.end(), both.begin() + nseeds);

@@ -510,7 +510,7 @@ __global__ void finalize_long(const int64_t* __restrict__ long_row, const int64_
 
 // Cold pass of the cache-blocked PageRank gather.  Workgroup b runs on XCD b % 8 (the
 // dispatcher deals workgroups round-robin over the 8 XCDs) and takes that XCD's (b / 8)-th
-// cold block, so each XCD walks its own segments in order and its L2 holds the 2 MB slice of
+// cold block, so each XCD walks its own segments in order and its L2 holds the segment slice (384 K sources = 3 MB) of
 // messages the block gathers from.  Workgroups past the XCD's block count exit at once.
 template <bool kPacked, bool kPf = false>
 __global__ void __launch_bounds__(kBlock) cold_gather(const int64_t* __restrict__ poff,

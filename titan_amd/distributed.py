@@ -743,15 +743,15 @@ class NativeExchange:
 
 
 def distributed_msbfs_native(backend, seeds, max_depth: int, exchange: NativeExchange, ms_alpha: float = 12.0,
-                             fixed_exchange_bytes: int = None):
+                             fixed_exchange_bytes: int = None, stats: bool = True):
     """distributed_msbfs as ONE native call (tgo_part_msbfs_run): the same protocol, the level
     loop and its collectives in C++ on the engine's stream.  Returns (per-seed global reached
-    vertices, per-seed reached entries, levels)."""
+    vertices, per-seed reached entries, levels); without stats the counts are None."""
     if fixed_exchange_bytes is None:
         fixed_exchange_bytes = FIXED_EXCHANGE_BYTES
     sd = np.ascontiguousarray(seeds, np.int64)
-    r = np.zeros(len(sd), np.int64)
-    e = np.zeros(len(sd), np.int64)
+    r = np.zeros(len(sd), np.int64) if stats else None
+    e = np.zeros(len(sd), np.int64) if stats else None
     lv = C.c_int32()
     lib = backend.e.lib
     rc = lib.tgo_part_msbfs_run(backend.e.ctx, exchange.h, L.ptr(sd, C.c_int64), len(sd), int(max_depth),
