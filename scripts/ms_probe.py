@@ -21,7 +21,7 @@ roots = [int(r) for r in pick_roots(n, src, dst, 64, seed=7)]
 eng = Engine(host_threads=16).load_edges(n, src, dst, L.SCOPE_BOTH_E, apply_cap=False)
 del src, dst
 eng.bfs_multi(roots, n, L.SCOPE_BOTH_E, seed_is_dense=True, stats=True, fetch=False)
-_, e = eng.multi_stats(len(roots))
+r, e = eng.multi_stats(len(roots))
 edges = float(np.sum(e)) / 2.0
 best = 1e9
 for _ in range(sweeps):
@@ -30,5 +30,5 @@ for _ in range(sweeps):
     best = min(best, eng.stats()["last_kernel_ms"])
     wall = time.perf_counter() - t
 print(f"msbfs scale {scale}: device {best:.3f} ms/sweep (wall {wall * 1e3:.3f}), levels {eng.stats()['levels']}, "
-      f"GTEPS {edges / best / 1e6:.1f}  env={ {k: v for k, v in os.environ.items() if k.startswith('TGO_')} }",
+      f"GTEPS {edges / best / 1e6:.1f} reached {int(np.sum(r))} entries {int(np.sum(e))}  env={ {k: v for k, v in os.environ.items() if k.startswith('TGO_')} }",
       flush=True)

@@ -98,6 +98,18 @@ hipError_t dev_alloc(tgo_ctx* ctx, T*& p, int64_t count) {
     return hipSuccess;
 }
 
+// Adopt a device array built on the device (DevArray): no copy, freed with the graph.
+template <class T>
+void adopt(tgo_ctx* ctx, T*& p, DevArray<T>& a) {
+    p = a.p;
+    if (a.p) {
+        ctx->allocs.push_back(a.p);
+        ctx->dev_bytes += static_cast<int64_t>(std::max<int64_t>(a.n, 1) * sizeof(T));
+    }
+    a.p = nullptr;
+    a.n = -1;
+}
+
 template <class T>
 hipError_t upload(tgo_ctx* ctx, T*& p, const std::vector<T>& h) {
     hipError_t e = dev_alloc(ctx, p, static_cast<int64_t>(h.size()));
@@ -215,7 +227,7 @@ int upload_row_blocks_dev(tgo_ctx* ctx, const std::vector<int64_t>& off, RowBloc
 // host; uploaded into cb.
 int upload_cold_blocks(tgo_ctx* ctx, const std::vector<int64_t>& off, const std::vector<int32_t>& adj,
                        int64_t n_src, int64_t hot, int64_t n_rows, ColdBlocks& cb, bool& ready,
-                       const int64_t* d_off = nullptr, const int32_t* d_adj = nullptr) {
+                       const int64_t* d_off = nullptr, const int32_t* d_adj = nullptr, int64_t d_nnz = 0) {
     cb = ColdBlocks();
     ready = false;
     HostColdBlocks hc;
@@ -230,15 +242,19 @@ int upload_cold_blocks(tgo_ctx* ctx, const std::vector<int64_t>& off, const std:
     bool on_dev = false;
     if (d_off && d_adj && env_i64("TGO_HOST_ASSEMBLY", 0) == 0) {
         std::string err;
-        if (int rc = build_cold_blocks_device(d_off, d_adj, static_cast<int64_t>(off.size()) - 1,
-                                              static_cast<int64_t>(adj.size()), n_src, hot,
+        if (int rc = build_cold_blocks_device(d_off, d_adj, static_cast<int64_t>(off.size()) - 1, d_nnz, n_src, hot,
                                               env_i64("TGO_PR_SEG", kPrSegDefault), kTile, kMaxRows,
                                               env_i64("TGO_PR_CPACK", 1) != 0, hc, on_dev, ctx->stream, err))
             return fail(ctx, rc, err);
         if (on_dev) lap("build (device)");
     }
+    std::vector<int32_t> adj_dl;        // host copy of a device-resident list, for the host build
+    if (!on_dev && d_adj && static_cast<int64_t>(adj.size()) != d_nnz) {
+        adj_dl.resize(static_cast<size_t>(d_nnz));
+        HIP_TRY(copy_chunked(adj_dl.data(), d_adj, static_cast<size_t>(d_nnz) * sizeof(int32_t), hipMemcpyDeviceToHost));
+    }
     if (!on_dev) {
-        if (!build_cold_blocks(off, adj, n_src, hot, env_i64("TGO_PR_SEG", kPrSegDefault), kTile, kMaxRows,
+        if (!build_cold_blocks(off, adj_dl.empty() ? adj : adj_dl, n_src, hot, env_i64("TGO_PR_SEG", kPrSegDefault), kTile, kMaxRows,
                                threads_of(ctx), env_i64("TGO_PR_CPACK", 1) != 0, hc))
             return TGO_OK;                                // too small to block: plain gather
         lap("build (host)");
@@ -262,7 +278,8 @@ int upload_cold_blocks(tgo_ctx* ctx, const std::vector<int64_t>& off, const std:
     const bool pack = env_i64("TGO_PR_PACK", 1) != 0;
     if (!pack) cb.hot_tile = static_cast<int>(kTile), cb.hot_shift = kPackShift;
     if (on_dev) {                                   // hot tiles packed on the device
-        HIP_TRY(upload(ctx, cb.hcsr.adj, hc.hadj));
+        cb.hcsr.nnz = hc.d_hadj.n;
+        adopt(ctx, cb.hcsr.adj, hc.d_hadj);
         const int32_t max_src = static_cast<int32_t>(std::min<int64_t>(hot, n_src) - 1);
         if (int rc = upload_row_blocks_dev(ctx, hoff_act, cb.rb_hot, pack ? cb.hcsr.adj : nullptr, max_src, &cb.packed,
                                            cb.hot_tile, cb.hot_shift))
@@ -285,12 +302,13 @@ int upload_cold_blocks(tgo_ctx* ctx, const std::vector<int64_t>& off, const std:
             HIP_TRY(upload_row_blocks(ctx, hoff_act, cb.rb_hot, pack ? &hc.hadj : nullptr, &cb.packed));
         }
         HIP_TRY(upload(ctx, cb.hcsr.adj, hc.hadj));
+        cb.hcsr.nnz = static_cast<int64_t>(hc.hadj.size());
     }
     lap("hot row blocks+pack");
     HIP_TRY(upload(ctx, cb.hcsr.off, hc.hoff));
-    cb.hcsr.nnz = static_cast<int64_t>(hc.hadj.size());
     HIP_TRY(upload(ctx, cb.poff, hc.poff));
-    HIP_TRY(upload(ctx, cb.cadj, hc.cadj));
+    if (hc.d_cadj.present()) adopt(ctx, cb.cadj, hc.d_cadj);
+    else HIP_TRY(upload(ctx, cb.cadj, hc.cadj));
     HIP_TRY(upload(ctx, cb.cptr, hc.cptr));
     HIP_TRY(upload(ctx, cb.cpid, hc.cpid));
     HIP_TRY(upload(ctx, cb.bbeg, hc.bbeg));
@@ -334,7 +352,7 @@ int upload_graph(tgo_ctx* ctx, HostGraph& h, bool allow_segments = true) {
     g.scope = h.scope;
     g.has_weight = h.has_weight;
     g.weight_dt = h.weight_dt;
-    g.has_col = !h.out.col.empty() || !h.in.col.empty();
+    g.has_col = h.out.has_col() || h.in.has_col();
     g.has_transpose = h.has_transpose;
     g.n_active = 0;
     for (int64_t v = h.n - 1; v >= 0; --v)
@@ -348,11 +366,17 @@ int upload_graph(tgo_ctx* ctx, HostGraph& h, bool allow_segments = true) {
     g.mean_weight = wcnt ? wsum / static_cast<double>(wcnt) : 1.0;
     auto up = [&](HostCsr& src, DevCsr& dst) -> hipError_t {
         hipError_t e;
+        dst.nnz = src.nnz();
         if ((e = upload(ctx, dst.off, src.off)) != hipSuccess) return e;
-        if ((e = upload(ctx, dst.adj, src.adj)) != hipSuccess) return e;
-        if (h.has_weight && (e = upload(ctx, dst.w, src.w)) != hipSuccess) return e;
-        if (!src.col.empty() && (e = upload(ctx, dst.col, src.col)) != hipSuccess) return e;
-        dst.nnz = static_cast<int64_t>(src.adj.size());
+        // lists assembled on the device stay there (adopted); host-assembled ones are copied
+        if (src.dadj.present()) adopt(ctx, dst.adj, src.dadj);
+        else if ((e = upload(ctx, dst.adj, src.adj)) != hipSuccess) return e;
+        if (h.has_weight) {
+            if (src.dw.present()) adopt(ctx, dst.w, src.dw);
+            else if ((e = upload(ctx, dst.w, src.w)) != hipSuccess) return e;
+        }
+        if (src.dcol.present()) adopt(ctx, dst.col, src.dcol);
+        else if (!src.col.empty() && (e = upload(ctx, dst.col, src.col)) != hipSuccess) return e;
         return hipSuccess;
     };
     HIP_TRY(up(h.out, g.out));
@@ -379,7 +403,7 @@ int upload_graph(tgo_ctx* ctx, HostGraph& h, bool allow_segments = true) {
         // rows >= n_active have no entries at all: the hot pass skips them (their rank
         // after any update is (1-a)/N, written once at the end of the program)
         if (int rc = upload_cold_blocks(ctx, h.in.off, h.in.adj, h.n, env_i64("TGO_PR_HOT", kPrHotDefault), g.n_active,
-                                        g.cold_in, g.cold_in_ready, g.in.off, g.in.adj))
+                                        g.cold_in, g.cold_in_ready, g.in.off, g.in.adj, g.in.nnz))
             return rc;
         lap("cold blocks");
     }
@@ -421,8 +445,8 @@ int upload_graph(tgo_ctx* ctx, HostGraph& h, bool allow_segments = true) {
     ctx->id_sorted = true;
     for (int64_t v = 1; v < n && ctx->id_sorted; ++v) ctx->id_sorted = h.titan_id[v] > h.titan_id[v - 1];
     ctx->st.num_vertices = n;
-    ctx->st.out_entries = static_cast<int64_t>(h.out.adj.size());
-    ctx->st.in_entries = static_cast<int64_t>(h.in.adj.size());
+    ctx->st.out_entries = g.out.nnz;       // (the device lists were adopted: h's are empty)
+    ctx->st.in_entries = g.in.nnz;
     ctx->st.ghost_vertices = h.ghost;
     ctx->st.truncated_results = h.truncated;
     ctx->st.skipped_rows = h.skipped;
@@ -1101,7 +1125,14 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
     // frontier-bitmap filter of pull levels: measured slower (every pull level: 3.07 -> 3.99 ms,
     // 0.95 -> 1.25, 0.18 -> 0.19; MS-BFS 3146 -> 2471 GTEPS, profiles/r02ad_*): the mask gathers
     // mostly hit L2 / the Infinity Cache already and the probe adds a dependent load.  Opt-in.
-    static const bool filter = env_double("TGO_MS_FILTER", 0.0) != 0.0;
+    // TGO_MS_FILTER_FROM=H probes the bitmap only for neighbours >= H (the cold ids whose
+    // gathers miss L2); TGO_MS_FILTER=1 is H=0, the filter for every neighbour.  Measured on
+    // RMAT-24 (profiles/r03h_ms_filter.log): off 5.59 ms/sweep; H = 0 7.05, 128K 6.32, 256K 6.10,
+    // 384K 5.93, 1M 5.62 — monotone towards no filter, so the probe's dependent load costs more
+    // than the cold gathers it saves.  Off by default.
+    static const int32_t filter_from = env_double("TGO_MS_FILTER", 0.0) != 0.0
+        ? 0 : static_cast<int32_t>(env_double("TGO_MS_FILTER_FROM", -1.0));
+    const bool filter = filter_from >= 0 && filter_from < n;
     int64_t qlen = static_cast<int64_t>(uniq.size());
     int64_t mf = 0;
     {
@@ -1127,7 +1158,7 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
         if (use_pull) {
             if (filter) HIP_TRY(k_ms_fbitmap(fr, n, s.ms_fbm, st));
             HIP_TRY(k_ms_pull(pull, push, g.n_active, full, fr, filter ? s.ms_fbm : nullptr, s.ms_vis, nx,
-                              ms_planes(ctx), s.cnt, L + 1, st));
+                              ms_planes(ctx), s.cnt, L + 1, st, filter ? filter_from : 0));
         } else {
             HIP_TRY(hipMemsetAsync(nx, 0, n * 8, st));
             if ((rc = scan_frontier(ctx, qlen))) return rc;
@@ -1695,7 +1726,7 @@ int tgo_part_ms_pull(tgo_ctx* ctx, int32_t level, const uint64_t* fr_global, uin
     // entry-less seed enters a mask, tgo_part_ms_begin)
     const int nxt = ctx->part_cur ^ 1;
     HIP_TRY(k_ms_pull(pull, push, g.n_active, full, fr_global, nullptr, s.ms_vis, fr_next, ms_planes(ctx), s.cnt,
-                      level + 1, st));
+                      level + 1, st, 0));
     ctx->part_cur = nxt;
     ctx->part_queued = false;       // counted only: ms_push builds the queue if it needs one
     return part_counts(ctx, counts);

@@ -19,7 +19,10 @@
 // Weights / column positions ride along as a 32-bit payload (an index into the previous
 // order) and are gathered once at the end.
 #include <algorithm>
+#include <chrono>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -52,6 +55,12 @@ struct ScopedBuf {                      // scoped device buffer
         if (p) (void)hipFree(p);
         p = nullptr;
         n = 0;
+    }
+    T* take() {                         // hand the allocation over (DevArray::own)
+        T* q = p;
+        p = nullptr;
+        n = 0;
+        return q;
     }
     ~ScopedBuf() { release(); }
 };
@@ -331,6 +340,16 @@ int assemble_edges_device(const tgo_edges* e, const tgo_load_opts* opts, int64_t
     while ((int64_t(1) << b) < n) ++b;
     const int bits = 2 * b;
 
+    // TGO_TRACE=1: per-phase times on stderr (synchronising the stream at each phase end)
+    static const bool trace = std::getenv("TGO_TRACE") && std::atoi(std::getenv("TGO_TRACE")) != 0;
+    auto t_last = std::chrono::steady_clock::now();
+    auto lap = [&](const char* what) {
+        if (!trace) return;
+        (void)hipStreamSynchronize(s);
+        const auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[tgo]   assemble %-16s %8.1f ms\n", what, std::chrono::duration<double, std::milli>(now - t_last).count());
+        t_last = now;
+    };
     ScopedBuf<int32_t> d_src, d_dst, d_w;
     AS_TRY(d_src.alloc(m));
     AS_TRY(d_dst.alloc(m));
@@ -352,6 +371,7 @@ int assemble_edges_device(const tgo_edges* e, const tgo_load_opts* opts, int64_t
         AS_TRY(hipStreamSynchronize(s));
         if (hb) { err = "edge endpoint out of range"; return TGO_E_INVALID; }
     }
+    lap("upload + check");
     Sorter so{{}, s};
     ScopedBuf<uint32_t> deg;
     AS_TRY(deg.alloc(n));
@@ -422,6 +442,7 @@ int assemble_edges_device(const tgo_edges* e, const tgo_load_opts* opts, int64_t
         for (int d = 0; d < 2; ++d) dir[d].count = m;
     }
     g.truncated = static_cast<int64_t>(truncated);
+    lap(sort1 ? "sort 1 + cut" : "degrees");
     // ---- degree-grouped relabel: perm[v] = position of v (hottest half-octave first)
     ScopedBuf<int32_t> perm;
     AS_TRY(perm.alloc(n));
@@ -475,19 +496,22 @@ int assemble_edges_device(const tgo_edges* e, const tgo_load_opts* opts, int64_t
                                              sort1 ? dir[d].edge.p : nullptr, d_w.p, sort1 ? dir[d].col.p : nullptr,
                                              fadj[d].p, g.has_weight ? fw[d].p : nullptr, keep_col ? col.p : nullptr);
         AS_TRY(download(hc.off, off.p, n + 1, s));
-        AS_TRY(download(hc.adj, fadj[d].p, c, s));
-        if (g.has_weight) AS_TRY(download(hc.w, fw[d].p, c, s));
-        if (keep_col) AS_TRY(download(hc.col, col.p, c, s));
+        if (g.has_weight) {                          // weight_sorted_push reads the host lists
+            AS_TRY(download(hc.adj, fadj[d].p, c, s));
+            AS_TRY(download(hc.w, fw[d].p, c, s));
+        }
         AS_TRY(hipStreamSynchronize(s));
+        if (keep_col) hc.dcol.own(col.take(), c);
         dir[d].edge.release();
         dir[d].col.release();
+        lap(d == 0 ? "relabel + OUT" : "IN");
     }
     AS_TRY(download(g.perm, perm.p, n, s));
     // ---- push view: equal to the stored opposite list unless the cut made rows asymmetric
     g.has_transpose = g.truncated != 0;
     if (g.has_transpose && g.scope != TGO_SCOPE_BOTH_E) {
         const int d = g.scope == TGO_SCOPE_IN_E ? 0 : 1;      // pull list of inE = OUT rows, outE = IN rows
-        const int64_t c = static_cast<int64_t>(g.scope == TGO_SCOPE_IN_E ? g.out.adj.size() : g.in.adj.size());
+        const int64_t c = dir[d].count;
         ScopedBuf<uint64_t> tk, ts;
         ScopedBuf<uint32_t> tv, tvs;
         AS_TRY(tk.alloc(c));
@@ -509,10 +533,21 @@ int assemble_edges_device(const tgo_edges* e, const tgo_load_opts* opts, int64_t
         if (c) emit_list<<<grid(c), kB, 0, s>>>(ts.p, g.has_weight ? tvs.p : nullptr, c, b, nullptr, fw[d].p, nullptr,
                                                 adj.p, g.has_weight ? w.p : nullptr, nullptr);
         AS_TRY(download(g.push_t.off, off.p, n + 1, s));
-        AS_TRY(download(g.push_t.adj, adj.p, c, s));
-        if (g.has_weight) AS_TRY(download(g.push_t.w, w.p, c, s));
+        if (g.has_weight) {
+            AS_TRY(download(g.push_t.adj, adj.p, c, s));
+            AS_TRY(download(g.push_t.w, w.p, c, s));
+        }
+        AS_TRY(hipStreamSynchronize(s));
+        g.push_t.dadj.own(adj.take(), c);
+        if (g.has_weight) g.push_t.dw.own(w.take(), c);
+        lap("transpose");
     }
     AS_TRY(hipStreamSynchronize(s));
+    // the final lists stay on the device: upload_graph adopts them
+    for (int d = 0; d < 2; ++d) {
+        outc[d]->dadj.own(fadj[d].take(), dir[d].count);
+        if (g.has_weight) outc[d]->dw.own(fw[d].take(), dir[d].count);
+    }
     return TGO_OK;
 }
 
@@ -618,6 +653,7 @@ int assemble_rows_device(RowStaging& st, HostGraph& g, hipStream_t s, std::strin
     ScopedBuf<uint64_t> fkey[2];
     ScopedBuf<int32_t> fadj[2], fw[2];
     ScopedBuf<int64_t> foff[2];
+    ScopedBuf<uint32_t> fcol[2];
     for (int d = 0; d < 2; ++d) {
         const int64_t c = cnt[d];
         ScopedBuf<uint64_t> kt;
@@ -629,9 +665,8 @@ int assemble_rows_device(RowStaging& st, HostGraph& g, hipStream_t s, std::strin
         AS_TRY(foff[d].alloc(n + 1));
         row_offsets<<<grid(n + 1), kB, 0, s>>>(fkey[d].p, c, b, n, foff[d].p);
         AS_TRY(fadj[d].alloc(c));
-        ScopedBuf<uint32_t> fcol;
         if (weighted) AS_TRY(fw[d].alloc(c));
-        if (keep_col) AS_TRY(fcol.alloc(c));
+        if (keep_col) AS_TRY(fcol[d].alloc(c));
         // payload chain: sorted position -> kept index (vs) -> staged entry (v1)
         if (c)
             emit_list<<<grid(c), kB, 0, s>>>(fkey[d].p, vs.p, c, b, v1[d].p, d_w.p, nullptr, fadj[d].p,
@@ -642,14 +677,15 @@ int assemble_rows_device(RowStaging& st, HostGraph& g, hipStream_t s, std::strin
             gather_i32<<<grid(c), kB, 0, s>>>(vs.p, reinterpret_cast<const int32_t*>(v1[d].p), c,
                                               reinterpret_cast<int32_t*>(staged.p));
             gather_i32<<<grid(c), kB, 0, s>>>(staged.p, reinterpret_cast<const int32_t*>(col.p), c,
-                                              reinterpret_cast<int32_t*>(fcol.p));
+                                              reinterpret_cast<int32_t*>(fcol[d].p));
             AS_TRY(hipStreamSynchronize(s));
         }
         HostCsr& hc = *outc[d];
         AS_TRY(download(hc.off, foff[d].p, n + 1, s));
-        AS_TRY(download(hc.adj, fadj[d].p, c, s));
-        if (weighted) AS_TRY(download(hc.w, fw[d].p, c, s));
-        if (keep_col) AS_TRY(download(hc.col, fcol.p, c, s));
+        if (weighted) {                              // weight_sorted_push reads the host lists
+            AS_TRY(download(hc.adj, fadj[d].p, c, s));
+            AS_TRY(download(hc.w, fw[d].p, c, s));
+        }
         v1[d].release();
     }
     AS_TRY(download(g.perm, perm.p, n, s));
@@ -701,10 +737,20 @@ int assemble_rows_device(RowStaging& st, HostGraph& g, hipStream_t s, std::strin
         if (c) emit_list<<<grid(c), kB, 0, s>>>(ts.p, tvs.p, c, b, nullptr, tw.p, nullptr, adj.p,
                                                 weighted ? w.p : nullptr, nullptr);
         AS_TRY(download(g.push_t.off, off.p, n + 1, s));
-        AS_TRY(download(g.push_t.adj, adj.p, c, s));
-        if (weighted) AS_TRY(download(g.push_t.w, w.p, c, s));
+        if (weighted) {
+            AS_TRY(download(g.push_t.adj, adj.p, c, s));
+            AS_TRY(download(g.push_t.w, w.p, c, s));
+        }
+        AS_TRY(hipStreamSynchronize(s));
+        g.push_t.dadj.own(adj.take(), c);
+        if (weighted) g.push_t.dw.own(w.take(), c);
     }
     AS_TRY(hipStreamSynchronize(s));
+    for (int d = 0; d < 2; ++d) {                    // adopted by upload_graph
+        outc[d]->dadj.own(fadj[d].take(), cnt[d]);
+        if (weighted) outc[d]->dw.own(fw[d].take(), cnt[d]);
+        if (keep_col) outc[d]->dcol.own(fcol[d].take(), cnt[d]);
+    }
     st = RowStaging();
     return TGO_OK;
 }

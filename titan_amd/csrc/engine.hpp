@@ -22,12 +22,38 @@
 namespace tgo {
 
 // ---------------------------------------------------------------- host graph
+// A device array built on the device (assemble.hip, pr_layout.hip) and handed to the upload,
+// which adopts it instead of a host round trip.  Move-only; frees itself if never adopted.
+template <class T>
+struct DevArray {
+    T* p = nullptr;
+    int64_t n = -1;             // element count; < 0: no device array
+    DevArray() = default;
+    DevArray(const DevArray&) = delete;
+    DevArray& operator=(const DevArray&) = delete;
+    DevArray(DevArray&& o) noexcept : p(o.p), n(o.n) { o.p = nullptr; o.n = -1; }
+    DevArray& operator=(DevArray&& o) noexcept {
+        if (this != &o) { reset(); p = o.p; n = o.n; o.p = nullptr; o.n = -1; }
+        return *this;
+    }
+    ~DevArray() { reset(); }
+    void reset() { if (p) (void)hipFree(p); p = nullptr; n = -1; }
+    void own(T* q, int64_t count) { reset(); p = q; n = count; }
+    bool present() const { return n >= 0; }
+};
+
 struct HostCsr {
     std::vector<int64_t> off;   // n+1
     std::vector<int32_t> adj;
     std::vector<int32_t> w;     // empty when unweighted
     std::vector<uint32_t> col;  // TGO_LOAD_COLUMN_ORDER: each entry's position in its Titan row
                                 // (column order across both directions); empty otherwise
+    // device-resident lists of a device assembly; the host vectors above are then filled only
+    // where a host consumer needs them (weights: weight_sorted_push)
+    DevArray<int32_t> dadj, dw;
+    DevArray<uint32_t> dcol;
+    int64_t nnz() const { return dadj.present() ? dadj.n : static_cast<int64_t>(adj.size()); }
+    bool has_col() const { return dcol.present() || !col.empty(); }
 };
 
 struct HostGraph {
@@ -267,6 +293,7 @@ struct HostColdBlocks {
     int64_t hot = 0, seg = 0;
     std::vector<int64_t> hoff, poff, bbeg, bend;
     std::vector<int32_t> hadj, cadj, cpid, xblk, crow, bsrc;
+    DevArray<int32_t> d_hadj, d_cadj;   // the device build keeps hadj / cadj on the device
     bool cpacked = false;
     std::vector<uint32_t> cptr;
     XcdBase xbase{};
@@ -451,7 +478,7 @@ hipError_t k_ms_seed(const int64_t* seeds, int nseeds, uint64_t* vis, uint64_t* 
 hipError_t k_ms_diag_take(unsigned long long* out8, hipStream_t s);
 hipError_t k_ms_pull(const View& pull, const View& push, int64_t n_active, uint64_t full, const uint64_t* fr,
                      const uint64_t* fbm, uint64_t* vis, uint64_t* nx, LevelPlanes lvl, Counters* cnt,
-                     int32_t next_level, hipStream_t s);
+                     int32_t next_level, hipStream_t s, int32_t filter_from);
 hipError_t k_ms_fbitmap(const uint64_t* fr, int64_t n, uint64_t* fbm, hipStream_t s);
 hipError_t k_ms_queue(const View& push, int64_t n_active, const uint64_t* fr, int32_t* qn, int64_t* qdeg, Counters* cnt,
                       hipStream_t s);

@@ -82,6 +82,13 @@ constexpr int64_t kCoop = 64;
 __device__ __forceinline__ bool in_frontier(const uint64_t* __restrict__ fbm, int32_t u) {
     return !fbm || ((fbm[u >> 6] >> (u & 63)) & 1ULL);
 }
+// The filter only for neighbours u >= from (the cold ids): hot neighbours' masks sit in L2 and
+// are mostly frontier members at the dense levels, so probing the bitmap first only adds a
+// dependent load there; a cold neighbour outside every frontier costs an L2 probe instead of
+// an Infinity-Cache / HBM gather (at RMAT-24's first pull level ~88 % of them).
+__device__ __forceinline__ bool maybe_frontier(const uint64_t* __restrict__ fbm, int32_t u, int32_t from) {
+    return u < from || in_frontier(fbm, u);
+}
 // Diagnostic tallies of a pull level (TGO_MS_DIAG=1 with TGO_TRACE=1; off in the product):
 // [0] list entries examined, [1] mask gathers of hot neighbours (u < kDiagHot), [2] of cold
 // ones, [3] open vertices, [4] open vertices whose walk stopped early (every open source covered);
@@ -91,7 +98,7 @@ __device__ unsigned long long g_ms_diag[8];
 template <int kStep, bool kDiag = false>       // entries per dependent round trip of a lane's own list
 __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t n_active, uint64_t full,
         const uint64_t* __restrict__ fr, const uint64_t* __restrict__ fbm, uint64_t* __restrict__ vis,
-        uint64_t* __restrict__ nx, LevelPlanes lvl, Counters* cnt, int32_t next_level) {
+        uint64_t* __restrict__ nx, LevelPlanes lvl, Counters* cnt, int32_t next_level, int32_t filter_from) {
     unsigned long long nv = 0, mf = 0, bits = 0;
     unsigned long long dg[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const int64_t words = (n_active + 63) >> 6;
@@ -122,7 +129,7 @@ __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t 
                     for (int j = 0; j < kStep; ++j) u[j] = k + j < e ? __builtin_nontemporal_load(adj + k + j) : -1;
                     bool f[kStep];
 #pragma unroll
-                    for (int j = 0; j < kStep; ++j) f[j] = u[j] >= 0 && in_frontier(fbm, u[j]);
+                    for (int j = 0; j < kStep; ++j) f[j] = u[j] >= 0 && maybe_frontier(fbm, u[j], filter_from);
                     uint64_t m = 0;
 #pragma unroll
                     for (int j = 0; j < kStep; ++j)
@@ -155,7 +162,7 @@ __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t 
                     }
                     bool f[4];
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) f[j] = u[j] >= 0 && in_frontier(fbm, u[j]);
+                    for (int j = 0; j < 4; ++j) f[j] = u[j] >= 0 && maybe_frontier(fbm, u[j], filter_from);
                     uint64_t m = 0;
 #pragma unroll
                     for (int j = 0; j < 4; ++j)
@@ -430,22 +437,22 @@ hipError_t k_ms_seed(const int64_t* seeds, int nseeds, uint64_t* vis, uint64_t* 
 }
 hipError_t k_ms_pull(const View& pull, const View& push, int64_t n_active, uint64_t full, const uint64_t* fr,
                      const uint64_t* fbm, uint64_t* vis, uint64_t* nx, LevelPlanes lvl, Counters* cnt,
-                     int32_t next_level, hipStream_t s) {
+                     int32_t next_level, hipStream_t s, int32_t filter_from) {
     // TGO_MS_STEP: entries a lane loads per round trip of its own list (8 default; 16 probe)
     static const int step = [] { const char* e = std::getenv("TGO_MS_STEP"); return e ? std::atoi(e) : 8; }();
     static const bool diag = [] { const char* e = std::getenv("TGO_MS_DIAG"); return e && std::atoi(e) != 0; }();
     if (diag)
         ms_pull<8, true><<<grid_for(n_active, 8192), kBlock, 0, s>>>(pull, push, n_active, full, fr, fbm, vis, nx, lvl, cnt,
-                                                                   next_level);
+                                                                   next_level, filter_from);
     else if (step == 16)
         ms_pull<16><<<grid_for(n_active, 8192), kBlock, 0, s>>>(pull, push, n_active, full, fr, fbm, vis, nx, lvl, cnt,
-                                                               next_level);
+                                                               next_level, filter_from);
     else if (step == 4)
         ms_pull<4><<<grid_for(n_active, 8192), kBlock, 0, s>>>(pull, push, n_active, full, fr, fbm, vis, nx, lvl, cnt,
-                                                              next_level);
+                                                              next_level, filter_from);
     else
         ms_pull<8><<<grid_for(n_active, 8192), kBlock, 0, s>>>(pull, push, n_active, full, fr, fbm, vis, nx, lvl, cnt,
-                                                              next_level);
+                                                              next_level, filter_from);
     return hipGetLastError();
 }
 // The pull diagnostics since the last call (zeroed after the read).

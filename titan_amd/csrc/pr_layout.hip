@@ -40,6 +40,7 @@ struct Buf {
         return hipMalloc(&p, static_cast<size_t>(std::max<int64_t>(count, 1)) * sizeof(T));
     }
     void release() { if (p) (void)hipFree(p); p = nullptr; }
+    T* take() { T* q = p; p = nullptr; return q; }     // hand over (DevArray::own)
     ~Buf() { release(); }
 };
 
@@ -333,8 +334,9 @@ int build_cold_blocks_device(const int64_t* d_off, const int32_t* d_adj, int64_t
             if (int rc = pack_tiles_device(cadj.p, C, tstart, &hc.bsrc, kPackShift, s, err)) return rc;
         hc.cpacked = true;
     }
-    PL_TRY(fetch(hc.cadj, cadj.p, C, s));
-    PL_TRY(fetch(hc.hadj, hadj.p, nhot, s));
+    PL_TRY(hipStreamSynchronize(s));
+    hc.d_cadj.own(cadj.take(), C);                   // both stay on the device (upload_cold_blocks)
+    hc.d_hadj.own(hadj.take(), nhot);
     hc.xblk.resize(nb);
     for (int64_t b = 0; b < nb; ++b) hc.xblk[b] = static_cast<int32_t>(b);
     const int64_t total = hc.poff[np];
