@@ -125,7 +125,11 @@ void free_graph(tgo_ctx* ctx) {
     ctx->allocs.clear();
     ctx->dev_bytes = 0;
     ctx->g = DevGraph();
-    ctx->sc = Scratch();
+    Scratch keep;                   // the mapped host counters outlive the graph (tgo_destroy frees them)
+    keep.hcnt = ctx->sc.hcnt;
+    keep.hcnt_dev = ctx->sc.hcnt_dev;
+    keep.pub_seq = ctx->sc.pub_seq;
+    ctx->sc = keep;
     ctx->loaded = false;
     ctx->res_kind = -1;         // the last program's results lived in the freed scratch
 }
@@ -663,6 +667,51 @@ int64_t default_delta(const DevGraph& g, bool weighted) {
     return std::max<int64_t>(1, static_cast<int64_t>(weighted ? 0.25 * g.mean_weight : 1.0));
 }
 
+// The light/heavy loop driven from the device (delta_loop.hip): the host enqueues steps in
+// batches and reads the loop state once per batch (dist, pending and member bitmaps are
+// initialised by the caller).
+int run_delta_device(tgo_ctx* ctx, int64_t seed, int64_t delta) {
+    DevGraph& g = ctx->g;
+    Scratch& s = ctx->sc;
+    hipStream_t st = ctx->stream;
+    const int64_t n = g.n;
+    static const bool trace = env_double("TGO_TRACE", 0.0) != 0.0;
+    static const int batch = static_cast<int>(std::max(1.0, env_double("TGO_DS_BATCH", 8.0)));
+    if (!s.ds_loop) {
+        for (int b = 0; b < 2; ++b) {
+            HIP_TRY(dev_alloc(ctx, s.ds_q[b], 2 * n + 2));
+            HIP_TRY(dev_alloc(ctx, s.ds_qp[b], 2 * n + 2));
+        }
+        HIP_TRY(dev_alloc(ctx, s.ds_loop, 1));
+        ctx->st.device_bytes = ctx->dev_bytes;
+    }
+    HIP_TRY(k_ds_loop_seed(g.push_ws, s.ds_light, s.dist, s.ds_q[0], s.ds_qp[0], s.ds_loop, seed, delta, st));
+    DsLoop h{};
+    int cur = 0;
+    // every step either relaxes a non-empty queue or extracts (at most one extraction in a row
+    // takes nothing); a run needs far fewer than 4n + 64 steps — the bound only stops a bug
+    const int64_t max_steps = 4 * n + 64;
+    for (int64_t steps = 0;;) {
+        for (int k = 0; k < batch; ++k) {
+            HIP_TRY(k_ds_loop_step(g.push_ws, s.ds_light, s.vb, s.ds_member, n, s.dist, s.msg, s.ds_q, s.ds_qp,
+                                   s.ds_loop, cur, delta, st));
+            cur ^= 1;
+        }
+        steps += batch;
+        HIP_TRY(hipMemcpyAsync(&h, s.ds_loop, sizeof(DsLoop), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        if (h.err) return fail(ctx, TGO_E_PROGRAM, "vertex program failed: a traversed edge has no value for the weight property");
+        if (h.done) break;
+        if (steps > max_steps) return fail(ctx, TGO_E_HIP, "delta-stepping: the device loop did not converge");
+    }
+    HIP_TRY(k_dist_finalize(s.dist, n, st));
+    if (trace) std::fprintf(stderr, "[tgo] delta %lld (device loop): %llu phases, %llu buckets, %llu extractions, %llu entries relaxed\n",
+                            (long long)delta, h.phases, h.buckets, h.extractions, h.relaxed);
+    ctx->st.levels = static_cast<int32_t>(h.phases);
+    ctx->st.relaxed_entries = static_cast<int64_t>(h.relaxed);
+    return TGO_OK;
+}
+
 // Light/heavy delta-stepping (delta.hip, weighted one-GPU loads): a bucket's phases relax
 // light entries only; when its near queue runs dry the bucket's members relax their heavy
 // entries once; then the threshold moves to the next non-empty bucket.
@@ -684,8 +733,16 @@ int run_delta_split(tgo_ctx* ctx, int64_t seed, int64_t delta) {
     HIP_TRY(k_fill_i64(s.dist, INT64_MAX, n, st));
     HIP_TRY(hipMemsetAsync(s.vb, 0, words * 8, st));        // pending bitmap
     HIP_TRY(hipMemsetAsync(s.ds_member, 0, words * 8, st));
+    // device-driven steps (delta_loop.hip) unless TGO_DS_HOSTLOOP=1 or the packed queue
+    // counters could overflow (count < 2^28, entries < 2^36)
+    static const bool host_loop = env_double("TGO_DS_HOSTLOOP", 0.0) != 0.0;
+    if (!host_loop && seed >= 0 && n < (int64_t(1) << 28) && g.push_ws.nnz < (int64_t(1) << kDsCountShift))
+        return run_delta_device(ctx, seed, delta);
     int phases = 0, buckets = 0;
     int64_t relaxed = 0;
+    // TGO_DS_TRACE=1: one line per phase (queue, entries, wall time since the previous phase)
+    static const bool phase_trace = env_double("TGO_DS_TRACE", 0.0) != 0.0;
+    auto t_phase = std::chrono::steady_clock::now();
     if (seed >= 0) {
         HIP_TRY(k_ds_seed_ws(g.push_ws, s.ds_light, s.dist, s.q[0], s.qdeg, seed, st));
         int64_t qlen = 1, thr = delta;
@@ -725,6 +782,13 @@ int run_delta_split(tgo_ctx* ctx, int64_t seed, int64_t delta) {
             if (s.hcnt->err) return fail(ctx, TGO_E_PROGRAM,
                 "vertex program failed: a traversed edge has no value for the weight property");
             relaxed += static_cast<int64_t>(s.hcnt->red[1]);
+            if (phase_trace) {
+                const auto now = std::chrono::steady_clock::now();
+                std::fprintf(stderr, "[tgo] ds phase %d thr %lld: queue %lld, entries %llu, next %llu, %.1f us\n", phases,
+                             (long long)thr, (long long)qlen, s.hcnt->red[1], s.hcnt->qlen,
+                             std::chrono::duration<double, std::micro>(now - t_phase).count());
+                t_phase = now;
+            }
             qlen = static_cast<int64_t>(s.hcnt->qlen);
             cur ^= 1;
             ++phases;
@@ -1742,7 +1806,8 @@ int tgo_part_ms_push(tgo_ctx* ctx, int32_t level, const uint64_t* fr_local, uint
     if ((rc = part_qlen_now(ctx, qlen))) return rc;
     if (qlen > 0 && !ctx->part_queued) {
         HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), ctx->stream));
-        HIP_TRY(k_ms_queue(push_view(g, TGO_SCOPE_BOTH_E), g.n, fr_local, s.q[ctx->part_cur], s.qdeg, s.cnt, ctx->stream));
+        HIP_TRY(k_ms_queue(push_view(g, TGO_SCOPE_BOTH_E), g.n_active, fr_local, s.q[ctx->part_cur], s.qdeg, s.cnt,
+                           ctx->stream));
         ctx->part_queued = true;
     }
     if (qlen > 0) {
@@ -1766,8 +1831,8 @@ int tgo_part_ms_settle(tgo_ctx* ctx, int32_t level, const uint64_t* recv, int32_
     HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
     HIP_TRY(k_or_slices(recv, nslices, g.n, fr_next, st));
     const int nxt = ctx->part_cur ^ 1;
-    HIP_TRY(k_ms_settle(push_view(g, TGO_SCOPE_BOTH_E), g.n, s.ms_vis, fr_next, ms_planes(ctx), s.q[nxt], s.qdeg, s.cnt,
-                        level + 1, st));
+    HIP_TRY(k_ms_settle(push_view(g, TGO_SCOPE_BOTH_E), g.n_active, s.ms_vis, fr_next, ms_planes(ctx), s.q[nxt], s.qdeg,
+                        s.cnt, level + 1, st));
     ctx->part_cur = nxt;
     ctx->part_queued = true;
     return part_counts(ctx, counts);
@@ -1862,11 +1927,11 @@ int tgo_part_ms_settle_fixed(tgo_ctx* ctx, int32_t level, const int64_t* recv, i
     if (level + 1 >= (1 << kLevelPlanes)) return fail(ctx, TGO_E_UNSUPPORTED, "multi-source BFS levels are < 65536");
     if ((rc = ms_planes_for(ctx, level + 1))) return rc;
     HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
-    HIP_TRY(hipMemsetAsync(fr_next, 0, g.n * 8, st));
+    HIP_TRY(hipMemsetAsync(fr_next, 0, g.n_active * 8, st));     // the tail [n_active, n) stays zero
     HIP_TRY(k_ms_or_fixed(recv, nslices, cap, fr_next, st));
     const int nxt = ctx->part_cur ^ 1;
-    HIP_TRY(k_ms_settle(push_view(g, TGO_SCOPE_BOTH_E), g.n, s.ms_vis, fr_next, ms_planes(ctx), s.q[nxt], s.qdeg, s.cnt,
-                        level + 1, st));
+    HIP_TRY(k_ms_settle(push_view(g, TGO_SCOPE_BOTH_E), g.n_active, s.ms_vis, fr_next, ms_planes(ctx), s.q[nxt], s.qdeg,
+                        s.cnt, level + 1, st));
     ctx->part_cur = nxt;
     ctx->part_queued = true;
     return part_counts(ctx, counts);
@@ -1884,7 +1949,7 @@ int tgo_part_ms_settle_pairs(tgo_ctx* ctx, int32_t level, const int64_t* recv, c
     if (level + 1 >= (1 << kLevelPlanes)) return fail(ctx, TGO_E_UNSUPPORTED, "multi-source BFS levels are < 65536");
     if ((rc = ms_planes_for(ctx, level + 1))) return rc;
     HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
-    HIP_TRY(hipMemsetAsync(fr_next, 0, g.n * 8, st));
+    HIP_TRY(hipMemsetAsync(fr_next, 0, g.n_active * 8, st));     // the tail [n_active, n) stays zero
     int64_t npairs = 0;
     for (int r = 0; r < nslices; ++r) {
         if (recv_counts[r] < 0 || recv_counts[r] > g.n) return fail(ctx, TGO_E_INVALID, "ms_settle_pairs: bad count");
@@ -1892,8 +1957,8 @@ int tgo_part_ms_settle_pairs(tgo_ctx* ctx, int32_t level, const int64_t* recv, c
     }
     HIP_TRY(k_ms_or_pairs(recv, npairs, fr_next, st));
     const int nxt = ctx->part_cur ^ 1;
-    HIP_TRY(k_ms_settle(push_view(g, TGO_SCOPE_BOTH_E), g.n, s.ms_vis, fr_next, ms_planes(ctx), s.q[nxt], s.qdeg, s.cnt,
-                        level + 1, st));
+    HIP_TRY(k_ms_settle(push_view(g, TGO_SCOPE_BOTH_E), g.n_active, s.ms_vis, fr_next, ms_planes(ctx), s.q[nxt], s.qdeg,
+                        s.cnt, level + 1, st));
     ctx->part_cur = nxt;
     ctx->part_queued = true;
     return part_counts(ctx, counts);
@@ -2463,9 +2528,10 @@ int part_dims(tgo_ctx* ctx, int64_t* n_local, int64_t* lo, int64_t* n_global, in
 int part_scratch(tgo_ctx* ctx, void** p, int64_t bytes, int slot) {
     Scratch& s = ctx->sc;
     if (slot < 0 || slot >= 8) return fail(ctx, TGO_E_INVALID, "driver scratch slot");
-    if (s.drv_bytes[slot] < bytes) {
+    if (s.drv_bytes[slot] < bytes) {                // fresh buffers start zero
         uint8_t* q = nullptr;
         HIP_TRY(dev_alloc(ctx, q, bytes));
+        HIP_TRY(hipMemsetAsync(q, 0, static_cast<size_t>(bytes), ctx->stream));
         s.drv[slot] = q;
         s.drv_bytes[slot] = bytes;
     }

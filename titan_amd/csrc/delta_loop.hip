@@ -1,0 +1,391 @@
+// delta_loop.hip — the light/heavy delta-stepping loop of one GPU (delta.hip's
+// run_delta_split protocol) driven from the device: no host round trip per phase.
+//
+// The host-driven loop pays, per phase, a scan launch sized on the host and a host read of
+// the next queue's length, and per bucket a pending-minimum pass plus a second read; on
+// RMAT-24 that is ~170 host round trips and ~45 full bitmap passes per source, a third of
+// the run.  Here every launch reads its sizes from device memory (DsLoop), so the host
+// enqueues steps in batches and reads the state once per batch:
+//   step = decide (1 thread: is the near queue empty? then the next threshold, or done)
+//        + extract (only if decided: next near queue + the settled members' heavy entries)
+//        + commit  (snapshot the queue's distances, clear their pending bits, mark members)
+//        + relax   (the queue's entries, edge-balanced; appends the next near queue)
+// Two changes make this possible:
+//   * queue counters are packed (count << 36 | entries), so ONE atomicAdd per block reserves
+//     both the queue slots and the entry range: the appender writes the exclusive prefix of
+//     the entries directly (qpre), and no scan pass is needed before the next relax;
+//   * the minimum pending distance is never scanned for: it is min(tm, lo), where tm is the
+//     smallest improvement since the last extraction that queued nothing (block-reduced in
+//     the relax) and lo the smallest distance the last extraction left pending.  tm can be
+//     stale-low (its vertex may have been queued since); then the extraction takes nothing,
+//     lo becomes exact and the next step's decision is exact — one extra step, same result.
+// The converged distances are unique (ShortestDistanceVertexProgram.java:96-130 is a
+// Jacobi Bellman-Ford with a min combiner), so this order of the same relaxations reaches
+// the same bit-exact result as the host loop and the oracle.
+#include <hip/hip_runtime.h>
+#include "frontier.hpp"
+
+namespace tgo {
+namespace {
+
+constexpr unsigned long long kEntryMask = (1ULL << kDsCountShift) - 1ULL;
+constexpr long long kInf = 0x7FFFFFFFFFFFFFFFLL;
+constexpr uint32_t kHeavy = 0x80000000u;
+
+__device__ __forceinline__ int64_t qcount(unsigned long long c) { return static_cast<int64_t>(c >> kDsCountShift); }
+__device__ __forceinline__ int64_t qentries(unsigned long long c) { return static_cast<int64_t>(c & kEntryMask); }
+__device__ __forceinline__ int64_t light_deg(const int64_t* off, const int64_t* light, int64_t u) { return light[u] - off[u]; }
+
+__device__ __forceinline__ int64_t wave_incl_scan(int64_t x) {
+    for (int o = 1; o < 64; o <<= 1) {
+        const int64_t y = __shfl_up(x, o, 64);
+        if (lane() >= o) x += y;
+    }
+    return x;
+}
+
+__device__ __forceinline__ long long block_min(long long x) {
+    __shared__ long long s_min[kWavesPerBlock];
+    for (int o = 32; o > 0; o >>= 1) {
+        const long long y = __shfl_xor(x, o, 64);
+        x = y < x ? y : x;
+    }
+    if (lane() == 0) s_min[threadIdx.x >> 6] = x;
+    __syncthreads();
+    long long m = s_min[0];
+    for (int w = 1; w < kWavesPerBlock; ++w) m = s_min[w] < m ? s_min[w] : m;
+    return m;
+}
+
+// Reserve `cnt` queue slots and `deg` entries with one packed atomic; every thread of the
+// block calls it with its own (cnt, deg) and gets its first slot and entry offset, in thread
+// order.  `qc` is the queue's packed counter.
+__device__ __forceinline__ void block_reserve(unsigned long long* qc, int64_t cnt, int64_t deg, int64_t& slot,
+                                              int64_t& doff) {
+    __shared__ int64_t s_c[kWavesPerBlock], s_d[kWavesPerBlock];
+    __shared__ unsigned long long s_base;
+    const int wave = threadIdx.x >> 6;
+    const int64_t ic = wave_incl_scan(cnt), id = wave_incl_scan(deg);
+    if (lane() == 63) { s_c[wave] = ic; s_d[wave] = id; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int64_t tc = 0, td = 0;
+        for (int w = 0; w < kWavesPerBlock; ++w) {
+            const int64_t c = s_c[w], d = s_d[w];
+            s_c[w] = tc; s_d[w] = td;
+            tc += c; td += d;
+        }
+        s_base = tc ? atomicAdd(qc, (static_cast<unsigned long long>(tc) << kDsCountShift) |
+                                        static_cast<unsigned long long>(td))
+                    : 0ULL;
+    }
+    __syncthreads();
+    slot = qcount(s_base) + s_c[wave] + ic - cnt;
+    doff = qentries(s_base) + s_d[wave] + id - deg;
+}
+
+// ---------------------------------------------------------------- seed / decide
+__global__ void ds_loop_seed(const int64_t* off, const int64_t* light, int64_t* dist, int32_t* q, int64_t* qpre,
+                             DsLoop* L, int64_t seed, int64_t delta) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    dist[seed] = 0;
+    q[0] = static_cast<int32_t>(seed);
+    qpre[0] = 0;
+    L->qc[0] = (1ULL << kDsCountShift) | static_cast<unsigned long long>(light_deg(off, light, seed));
+    L->qc[1] = 0;
+    L->tm = kInf;
+    L->lo = kInf;
+    L->thr = delta;
+    L->extract = 0;
+    L->members = 0;
+    L->done = 0;
+    L->err = 0;
+    L->phases = 0;
+    L->relaxed = 0;
+    L->buckets = 0;
+    L->extractions = 0;
+}
+
+// The near queue ran dry: next threshold from min(tm, lo) (the host loop's pending minimum),
+// or done when nothing is pending and no settled member has heavy entries left to relax.
+__global__ void ds_decide(DsLoop* L, int cur, int64_t delta) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    L->extract = 0;
+    if (L->done || qcount(L->qc[cur]) != 0) return;
+    const long long mn = L->tm < L->lo ? L->tm : L->lo;
+    if (mn == kInf && !L->members) { L->done = 1; return; }
+    if (mn != kInf) {
+        if (mn >= L->thr) L->thr = (mn / delta + 1) * delta;
+        L->buckets += 1;
+    }
+    L->tm = kInf;
+    L->lo = kInf;
+    L->members = 0;
+    L->extract = 1;
+    L->extractions += 1;
+}
+
+// ---------------------------------------------------------------- extract
+// chunk_extract (frontier.hpp) with the packed counter: pass 1 counts (slots and entries),
+// one packed atomic per block, pass 2 writes the queue and its entry offsets.
+template <int kStreams, class Probe>
+__device__ __forceinline__ void chunk_extract_packed(int64_t words, const Probe& probe, int32_t* __restrict__ qn,
+                                                     int64_t* __restrict__ qpre, unsigned long long* qc) {
+    const int64_t per = ((words + gridDim.x - 1) / gridDim.x + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock;
+    const int64_t w0 = static_cast<int64_t>(blockIdx.x) * per;
+    const int64_t w1 = min(words, w0 + per);
+    const int wave = threadIdx.x >> 6;
+    const unsigned long long below = (1ULL << lane()) - 1ULL;
+    int64_t count = 0, dsum = 0;             // this lane's takes (count per lane, not per wave)
+    bool touch = false;
+    constexpr int kUnroll = 4;
+    int64_t wd = w0 + wave;
+    for (; wd + (kUnroll - 1) * kWavesPerBlock < w1; wd += kUnroll * kWavesPerBlock) {
+        Take t[kUnroll][kStreams];
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) touch |= probe(wd + u * kWavesPerBlock, t[u], false);
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u)
+            for (int k = 0; k < kStreams; ++k)
+                if (t[u][k].take) { ++count; dsum += t[u][k].deg; }
+    }
+    for (; wd < w1; wd += kWavesPerBlock) {
+        Take t[kStreams];
+        touch |= probe(wd, t, false);
+        for (int k = 0; k < kStreams; ++k)
+            if (t[k].take) { ++count; dsum += t[k].deg; }
+    }
+    // per-wave totals, wave-major: the pass-2 order is word by word inside a wave, so only the
+    // wave's first slot / offset come from the reservation
+    const int64_t wc = wave_incl_scan(count), wdg = wave_incl_scan(dsum);
+    int64_t slot0, doff0;
+    block_reserve(qc, lane() == 63 ? wc : 0, lane() == 63 ? wdg : 0, slot0, doff0);
+    int64_t cursor = __shfl(slot0, 63, 64), dcur = __shfl(doff0, 63, 64);
+    if (!touch) return;                                      // wave-uniform
+    for (int64_t w = w0 + wave; w < w1; w += kWavesPerBlock) {
+        Take t[kStreams];
+        probe(w, t, true);
+        for (int k = 0; k < kStreams; ++k) {
+            const unsigned long long mask = __ballot(t[k].take);
+            if (!mask) continue;
+            const int64_t d = t[k].take ? t[k].deg : 0;
+            const int64_t id = wave_incl_scan(d);
+            if (t[k].take) {
+                const int64_t slot = cursor + __popcll(mask & below);
+                qn[slot] = t[k].entry;
+                qpre[slot] = dcur + id - d;
+            }
+            cursor += __popcll(mask);
+            dcur += __shfl(id, 63, 64);
+        }
+    }
+}
+
+__global__ void __launch_bounds__(kBlock) ds_extract_dev(const int64_t* __restrict__ off,
+        const int64_t* __restrict__ light, uint64_t* __restrict__ pend, uint64_t* __restrict__ member, int64_t n,
+        const int64_t* __restrict__ dist, DsLoop* L, int cur, int32_t* __restrict__ qn, int64_t* __restrict__ qpre) {
+    if (!L->extract) return;                                 // grid-uniform
+    const int64_t thr = L->thr;
+    const int64_t words = (n + 63) >> 6;
+    long long left = kInf;                                   // smallest distance left pending
+    auto probe = [&](int64_t wd, Take* t, bool commit) -> bool {
+        const uint64_t pb = pend[wd];                        // uniform across the wave
+        const uint64_t mb = member[wd];
+        const int64_t v = (wd << 6) + lane();
+        const bool p = pb && ((pb >> lane()) & 1ULL);
+        const long long d = p ? static_cast<long long>(dist[v]) : kInf;
+        const bool lt = p && d < thr;
+        if (!commit && p && !lt && d < left) left = d;
+        const bool mine = mb && ((mb >> lane()) & 1ULL);
+        const int64_t hdeg = mine ? off[v + 1] - light[v] : 0;
+        const unsigned long long tm = __ballot(lt);
+        if (commit && lane() == 0) {
+            if (tm) pend[wd] = pb & ~tm;
+            if (mb) member[wd] = 0;
+        }
+        t[0] = {lt, static_cast<int32_t>(v), lt ? light_deg(off, light, v) : 0};
+        t[1] = {hdeg > 0, static_cast<int32_t>(static_cast<uint32_t>(v) | kHeavy), hdeg};
+        return tm || mb;
+    };
+    chunk_extract_packed<2>(words, probe, qn, qpre, &L->qc[cur]);
+    const long long m = block_min(left);
+    if (threadIdx.x == 0 && m != kInf) atomicMin(&L->lo, m);
+}
+
+// ---------------------------------------------------------------- commit
+__global__ void __launch_bounds__(kBlock) ds_commit_dev(const int32_t* __restrict__ q, const int64_t* __restrict__ dist,
+        int64_t* __restrict__ msg, uint64_t* __restrict__ pend, uint64_t* __restrict__ member, DsLoop* L, int cur) {
+    const int64_t qlen = qcount(L->qc[cur]);
+    if (blockIdx.x == 0 && threadIdx.x == 0) L->qc[cur ^ 1] = 0;     // the relax appends there next
+    bool marked = false;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < qlen; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t e = static_cast<uint32_t>(q[i]);
+        if (e & kHeavy) continue;
+        const int32_t v = static_cast<int32_t>(e);
+        msg[v] = dist[v];
+        const uint64_t bit = 1ULL << (v & 63);
+        if (pend[v >> 6] & bit) atomicAnd(reinterpret_cast<unsigned long long*>(&pend[v >> 6]), ~bit);
+        if (!(member[v >> 6] & bit)) {
+            atomicOr(reinterpret_cast<unsigned long long*>(&member[v >> 6]), bit);
+            marked = true;
+        }
+    }
+    if (__ballot(marked) && lane() == 0) L->members = 1;
+}
+
+// ---------------------------------------------------------------- relax
+// ds_relax_ws over the packed queue: the load-balanced search of frontier.hpp
+// (for_each_queue_edge) with the total from the counter, and the takes of a whole tile
+// appended with one packed reservation (the per-trip block_append cost 8 reservations and
+// 16 barriers per tile).
+__global__ void __launch_bounds__(kBlock) ds_relax_dev(const int64_t* __restrict__ off, const int32_t* __restrict__ adj,
+        const int32_t* __restrict__ wt, const int64_t* __restrict__ light, const int32_t* __restrict__ q,
+        const int64_t* __restrict__ qpre, const int64_t* __restrict__ msg, int64_t* __restrict__ dist,
+        uint64_t* __restrict__ pend, int32_t* __restrict__ qn, int64_t* __restrict__ qpre_n, DsLoop* L, int cur) {
+    const unsigned long long c = L->qc[cur];
+    const int64_t qlen = qcount(c), total = qentries(c);
+    if (qlen == 0) return;                                   // grid-uniform
+    const int64_t thr = L->thr;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        L->phases += 1;
+        L->relaxed += static_cast<unsigned long long>(total);
+    }
+    __shared__ int64_t s_pre[kLdsEntries];
+    __shared__ int32_t s_q[kLdsEntries];
+    __shared__ int64_t s_lo, s_hi;
+    long long tmin = kInf;                                   // improvements that queued nothing
+    bool bad = false;
+    const int64_t ntiles = (total + kTileEdges - 1) / kTileEdges;
+    auto pre = [&](int64_t i) -> int64_t { return i < qlen ? qpre[i] : total; };
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t t0 = tile * kTileEdges;
+        const int64_t t1 = min(total, t0 + kTileEdges);
+        if (threadIdx.x == 0) {             // lo = last i with pre(i) <= t0; hi = last i with pre(i) <= t1-1
+            int64_t a = 0, b = qlen;
+            while (b - a > 1) { const int64_t m = (a + b) >> 1; if (qpre[m] <= t0) a = m; else b = m; }
+            s_lo = a;
+            int64_t a2 = a, b2 = qlen;
+            while (b2 - a2 > 1) { const int64_t m = (a2 + b2) >> 1; if (qpre[m] <= t1 - 1) a2 = m; else b2 = m; }
+            s_hi = a2;
+        }
+        __syncthreads();
+        const int64_t lo = s_lo, hi = s_hi;
+        const int64_t span = hi - lo + 1;
+        const bool in_lds = span + 1 <= kLdsEntries;
+        if (in_lds) {
+            for (int64_t i = threadIdx.x; i <= span; i += kBlock) {
+                s_pre[i] = pre(lo + i);
+                if (i < span) s_q[i] = q[lo + i];
+            }
+        }
+        __syncthreads();
+        // the tile's kEdgesPerThread entries per thread in stages, so each stage's loads are
+        // independent and in flight together (one entry at a time left every thread waiting
+        // out the whole search -> list -> distance -> atomic chain once per entry)
+        int64_t u[kEdgesPerThread], e[kEdgesPerThread];
+#pragma unroll
+        for (int k = 0; k < kEdgesPerThread; ++k) {           // 1: owning queue entry (LDS search)
+            const int64_t j = t0 + k * kBlock + threadIdx.x;
+            u[k] = -1;
+            e[k] = 0;
+            if (j >= t1) continue;
+            int32_t qe;
+            int64_t start;
+            if (in_lds) {
+                int64_t a = 0, b = span;
+                while (b - a > 1) { const int64_t m = (a + b) >> 1; if (s_pre[m] <= j) a = m; else b = m; }
+                qe = s_q[a]; start = s_pre[a];
+            } else {
+                int64_t a = lo, b = hi + 1;
+                while (b - a > 1) { const int64_t m = (a + b) >> 1; if (qpre[m] <= j) a = m; else b = m; }
+                qe = q[a]; start = qpre[a];
+            }
+            const uint32_t ue = static_cast<uint32_t>(qe);
+            u[k] = static_cast<int64_t>(ue & ~kHeavy);
+            e[k] = ((ue & kHeavy) ? light[u[k]] : off[u[k]]) + (j - start);
+        }
+        int32_t t[kEdgesPerThread], w[kEdgesPerThread];
+        int64_t mu[kEdgesPerThread], du[kEdgesPerThread];
+#pragma unroll
+        for (int k = 0; k < kEdgesPerThread; ++k) {           // 2: entry, the source's snapshot
+            if (u[k] < 0) continue;
+            t[k] = adj[e[k]];
+            w[k] = wt[e[k]];
+            mu[k] = msg[u[k]];
+            du[k] = dist[u[k]];
+        }
+        int64_t cand[kEdgesPerThread], dt[kEdgesPerThread];
+#pragma unroll
+        for (int k = 0; k < kEdgesPerThread; ++k) {           // 3: the targets' distances
+            cand[k] = -1;
+            if (u[k] < 0) continue;
+            if (w[k] == kMissingWeight) { bad = true; continue; }     // edge.value(weight) on a missing key
+            if (du[k] < mu[k]) continue;     // u improved during this phase: pending again, relaxes later
+            cand[k] = mu[k] + static_cast<int64_t>(w[k]);
+            dt[k] = dist[t[k]];
+        }
+        int32_t tv[kEdgesPerThread];
+        int64_t td[kEdgesPerThread];
+        int ntake = 0;
+        int64_t dtake = 0;
+#pragma unroll
+        for (int k = 0; k < kEdgesPerThread; ++k) {           // 4: min, pending bit, take
+            tv[k] = -1;
+            td[k] = 0;
+            if (cand[k] < 0 || cand[k] >= dt[k]) continue;    // a stale (larger) read only costs an atomic
+            const int32_t tk = t[k];
+            const long long old = atomicMin(reinterpret_cast<long long*>(&dist[tk]), static_cast<long long>(cand[k]));
+            if (cand[k] >= old) continue;
+            const uint64_t bit = 1ULL << (tk & 63);
+            const unsigned long long ob = atomicOr(reinterpret_cast<unsigned long long*>(&pend[tk >> 6]), bit);
+            if (!(ob & bit) && cand[k] < thr) {
+                tv[k] = tk;
+                td[k] = light_deg(off, light, tk);
+                ++ntake;
+                dtake += td[k];
+            } else if (cand[k] < tmin) {
+                tmin = cand[k];
+            }
+        }
+        // the tile's takes: one packed reservation (block-uniform call)
+        int64_t slot, doff;
+        block_reserve(&L->qc[cur ^ 1], ntake, dtake, slot, doff);
+        if (ntake) {
+#pragma unroll
+            for (int k = 0; k < kEdgesPerThread; ++k)
+                if (tv[k] >= 0) {
+                    qn[slot] = tv[k];
+                    qpre_n[slot] = doff;
+                    ++slot;
+                    doff += td[k];
+                }
+        }
+        __syncthreads();
+    }
+    if (__ballot(bad) && lane() == 0) L->err = 1;
+    const long long m = block_min(tmin);
+    if (threadIdx.x == 0 && m != kInf) atomicMin(&L->tm, m);
+}
+
+}  // namespace
+
+hipError_t k_ds_loop_seed(const DevCsr& ws, const int64_t* light, int64_t* dist, int32_t* q, int64_t* qpre, DsLoop* L,
+                          int64_t seed, int64_t delta, hipStream_t s) {
+    ds_loop_seed<<<1, 64, 0, s>>>(ws.off, light, dist, q, qpre, L, seed, delta);
+    return hipGetLastError();
+}
+
+// One step (decide, extract, commit, relax) of the device-driven loop, queue buffer `cur` in.
+hipError_t k_ds_loop_step(const DevCsr& ws, const int64_t* light, uint64_t* pend, uint64_t* member, int64_t n,
+                          int64_t* dist, int64_t* msg, int32_t* const q[2], int64_t* const qpre[2], DsLoop* L, int cur,
+                          int64_t delta, hipStream_t s) {
+    ds_decide<<<1, 64, 0, s>>>(L, cur, delta);
+    const int64_t words = (n + 63) / 64;
+    ds_extract_dev<<<extract_grid(words), kBlock, 0, s>>>(ws.off, light, pend, member, n, dist, L, cur, q[cur], qpre[cur]);
+    ds_commit_dev<<<1024, kBlock, 0, s>>>(q[cur], dist, msg, pend, member, L, cur);
+    ds_relax_dev<<<256 * 8, kBlock, 0, s>>>(ws.off, ws.adj, ws.w, light, q[cur], qpre[cur], msg, dist, pend, q[cur ^ 1],
+                                            qpre[cur ^ 1], L, cur);
+    return hipGetLastError();
+}
+
+}  // namespace tgo

@@ -354,6 +354,20 @@ struct Counters {               // device-side level counters (one cache line ea
     unsigned long long pad3[5];
 };
 
+// State of the device-driven delta-stepping loop (delta_loop.hip), in device memory.
+constexpr int kDsCountShift = 36;   // queue counters: count << 36 | entries (one atomic reserves both)
+struct DsLoop {
+    unsigned long long qc[2];   // per queue buffer
+    long long tm;               // smallest improvement since the last extraction that queued nothing
+    long long lo;               // smallest distance the last extraction left pending
+    long long thr;              // bucket threshold
+    unsigned long long extract; // ds_decide -> extraction this step
+    unsigned long long members; // a bucket member was marked since the last extraction
+    unsigned long long done, err;
+    unsigned long long phases, relaxed, buckets, extractions;
+    unsigned long long pad[3];
+};
+
 struct Scratch {
     void* drv[8] = {};          // partitioned C++ driver buffers (part_driver.cpp), by slot
     int64_t drv_bytes[8] = {};
@@ -394,6 +408,9 @@ struct Scratch {
     int64_t* ds_light = nullptr;    // n: end of each vertex's light entries in push_ws
     int64_t ds_light_delta = -1;    // bucket width ds_light was computed for
     uint64_t* ds_member = nullptr;  // words: vertices relaxed in the current bucket
+    int32_t* ds_q[2] = {nullptr, nullptr};    // device-driven loop: queues (2n + 2: light + heavy)
+    int64_t* ds_qp[2] = {nullptr, nullptr};   // and their entry offsets
+    DsLoop* ds_loop = nullptr;
     // generic vertex programs (allocated on first use): row-order staging + internal-order vectors
     int64_t* gv[3] = {nullptr, nullptr, nullptr};
     uint8_t* gh[3] = {nullptr, nullptr, nullptr};
@@ -462,6 +479,12 @@ hipError_t k_ds_extract_ws(const DevCsr& ws, const int64_t* light, uint64_t* pen
                            const int64_t* dist, int64_t thr, int32_t* qn, int64_t* qdeg, Counters* cnt, hipStream_t s);
 hipError_t k_ds_pending_min_ws(const uint64_t* pend, const uint64_t* member, int64_t words, const int64_t* dist,
                                Counters* cnt, hipStream_t s);
+// device-driven light/heavy loop (delta_loop.hip)
+hipError_t k_ds_loop_seed(const DevCsr& ws, const int64_t* light, int64_t* dist, int32_t* q, int64_t* qpre, DsLoop* L,
+                          int64_t seed, int64_t delta, hipStream_t s);
+hipError_t k_ds_loop_step(const DevCsr& ws, const int64_t* light, uint64_t* pend, uint64_t* member, int64_t n,
+                          int64_t* dist, int64_t* msg, int32_t* const q[2], int64_t* const qpre[2], DsLoop* L, int cur,
+                          int64_t delta, hipStream_t s);
 hipError_t k_ds_pending_min(const uint64_t* pend, int64_t words, const int64_t* dist, Counters* cnt, hipStream_t s);
 hipError_t k_ds_extract(const View& push, uint64_t* pend, int64_t n, const int64_t* dist, int64_t thr, int32_t* qn,
                         int64_t* qdeg, Counters* cnt, hipStream_t s);

@@ -310,11 +310,15 @@ extern "C" int tgo_part_msbfs_run(tgo_ctx* ctx, tgo_exchange* x, const int64_t* 
         return rc;
     int64_t* const caller_dc = part_dcounts_of(ctx);       // restored at the end
     uint64_t* glob[2] = {g0, g1};
-    // entry-less tail of both mask buffers and the candidate masks start zero (the steps keep
-    // them so); only this rank's slices are written by the local steps
-    if (hipMemsetAsync(g0, 0, ng * 8, st) != hipSuccess || hipMemsetAsync(g1, 0, ng * 8, st) != hipSuccess ||
-        hipMemsetAsync(cand, 0, ng * 8, st) != hipSuccess)
-        return part_fail(ctx, TGO_E_HIP, "tgo_part_msbfs_run: memset");
+    // no clearing per sweep (as the Python driver): the buffers start zero (part_scratch), a
+    // level rewrites the active rows of the next mask and the entry-less tail stays zero, the
+    // pack clears the candidate masks it reads, and a dense level's all-gather overwrites the
+    // peers' slices before the pull reads them.  A failed sweep re-zeroes all three.
+    auto rezero = [&]() {
+        (void)hipMemsetAsync(g0, 0, ng * 8, st);
+        (void)hipMemsetAsync(g1, 0, ng * 8, st);
+        (void)hipMemsetAsync(cand, 0, ng * 8, st);
+    };
     int64_t* hc = x->host_counts();                         // pinned host view of the counts (kept)
     if (!hc) return part_fail(ctx, TGO_E_HIP, "tgo_part_msbfs_run: pinned counts");
     // global counts: write local {a, b} to dc, all-reduce, read back (one sync)
@@ -386,6 +390,7 @@ extern "C" int tgo_part_msbfs_run(tgo_ctx* ctx, tgo_exchange* x, const int64_t* 
     const int rc_off = tgo_part_device_counts(ctx, caller_dc);
     if (rc) {
         x->abort();
+        rezero();
         return rc;
     }
     if (rc_off) return rc_off;
