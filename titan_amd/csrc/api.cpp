@@ -988,18 +988,25 @@ int tgo_finish_load(tgo_ctx* ctx) {
     const auto t0 = std::chrono::steady_clock::now();
     HostGraph h;
     std::string err;
-    // the staged work blocks, decoded in one device pass (decode.hip)
+    // the staged work blocks, decoded in one device pass (decode.hip); the kept entries stay
+    // on the device for the device assembly
+    const bool dev_asm = env_i64("TGO_HOST_ASSEMBLY", 0) == 0;
     int rc = decode_staged_raw(ctx->staging, ctx->opts.partition_bits, ctx->opts.hard_query_limit, ctx->dec,
-                               ctx->stream, err);
+                               ctx->stream, err, dev_asm);
     ctx->dec.release();
     if (rc) { ctx->staging = RowStaging(); return fail(ctx, rc, err); }
+    if (env_i64("TGO_TRACE", 0))
+        std::fprintf(stderr, "[tgo] finish_load decode %8.1f ms\n",
+                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
     // CSR assembly on the device (assemble.hip) unless TGO_HOST_ASSEMBLY=1 or the scan holds
     // vertex cuts (their representative rows fold on the host, graph_build.cpp)
     const RowStaging& stg = ctx->staging;
     const bool cuts = stg.n_rep > 0 || std::any_of(stg.vid.begin(), stg.vid.end(), [](int64_t v) { return (v & 7) == 2; });
-    const bool on_dev = env_i64("TGO_HOST_ASSEMBLY", 0) == 0 && !cuts;
-    rc = on_dev ? assemble_rows_device(ctx->staging, h, ctx->stream, err)
-                : assemble_from_rows(ctx->staging, h, threads_of(ctx), err);
+    const bool on_dev = dev_asm && !cuts;
+    if (!on_dev) rc = staging_entries_to_host(ctx->staging, ctx->stream, err);
+    if (!rc)
+        rc = on_dev ? assemble_rows_device(ctx->staging, h, ctx->stream, err)
+                    : assemble_from_rows(ctx->staging, h, threads_of(ctx), err);
     if (rc) { ctx->staging = RowStaging(); return fail(ctx, rc, err); }
     if (env_i64("TGO_TRACE", 0))
         std::fprintf(stderr, "[tgo] finish_load decode + assembly (%s) %8.1f ms\n", on_dev ? "device" : "host",

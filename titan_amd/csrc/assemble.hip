@@ -559,7 +559,7 @@ int assemble_rows_device(RowStaging& st, HostGraph& g, hipStream_t s, std::strin
     g = HostGraph();
     const int64_t n = static_cast<int64_t>(st.vid.size());
     if (n >= INT32_MAX) { err = "more than 2^31-1 vertices per device"; return TGO_E_UNSUPPORTED; }
-    const int64_t E = static_cast<int64_t>(st.other.size());
+    const int64_t E = st.entries();
     if (E >= (int64_t(1) << 32)) { err = "more than 2^32 staged entries"; return TGO_E_UNSUPPORTED; }
     g.n = n;
     g.titan_id = st.vid;
@@ -568,7 +568,7 @@ int assemble_rows_device(RowStaging& st, HostGraph& g, hipStream_t s, std::strin
     g.weight_dt = st.plan.weight_dt ? st.plan.weight_dt : TGO_DT_INTEGER;
     g.ghost = st.ghost; g.truncated = st.truncated; g.skipped = st.skipped;
     const bool keep_col = (st.opts.flags & TGO_LOAD_COLUMN_ORDER) != 0;
-    const bool weighted = g.has_weight && static_cast<int64_t>(st.w.size()) == E;
+    const bool weighted = g.has_weight && (st.d_other.present() ? st.d_w.n == E : static_cast<int64_t>(st.w.size()) == E);
     if (g.has_weight && !weighted) { err = "staged weights out of step"; return TGO_E_STATE; }
     if (n == 0) {
         g.out.off.assign(1, 0); g.in.off.assign(1, 0);
@@ -584,18 +584,29 @@ int assemble_rows_device(RowStaging& st, HostGraph& g, hipStream_t s, std::strin
     ScopedBuf<int32_t> d_w;
     AS_TRY(d_vid.alloc(n));
     AS_TRY(d_rb.alloc(n + 1));
-    AS_TRY(d_other.alloc(E));
-    AS_TRY(d_dir.alloc(E));
     AS_TRY(copy_chunked(d_vid.p, st.vid.data(), n * 8, hipMemcpyHostToDevice));
     AS_TRY(copy_chunked(d_rb.p, st.row_begin.data(), (n + 1) * 8, hipMemcpyHostToDevice));
-    if (E) {
-        AS_TRY(copy_chunked(d_other.p, st.other.data(), E * 8, hipMemcpyHostToDevice));
-        AS_TRY(copy_chunked(d_dir.p, st.dir.data(), E, hipMemcpyHostToDevice));
+    // staged entries: in place when the device decoder left them on the device
+    const bool dev_staged = st.d_other.present();
+    const int64_t* p_other = st.d_other.p;
+    const uint8_t* p_dir = st.d_dir.p;
+    const int32_t* p_w = st.d_w.p;
+    if (!dev_staged) {
+        AS_TRY(d_other.alloc(E));
+        AS_TRY(d_dir.alloc(E));
+        if (E) {
+            AS_TRY(copy_chunked(d_other.p, st.other.data(), E * 8, hipMemcpyHostToDevice));
+            AS_TRY(copy_chunked(d_dir.p, st.dir.data(), E, hipMemcpyHostToDevice));
+        }
+        if (weighted) {
+            AS_TRY(d_w.alloc(E));
+            if (E) AS_TRY(copy_chunked(d_w.p, st.w.data(), E * 4, hipMemcpyHostToDevice));
+        }
+        p_other = d_other.p;
+        p_dir = d_dir.p;
+        p_w = d_w.p;
     }
-    if (weighted) {
-        AS_TRY(d_w.alloc(E));
-        if (E) AS_TRY(copy_chunked(d_w.p, st.w.data(), E * 4, hipMemcpyHostToDevice));
-    }
+    if (!weighted) p_w = nullptr;
     // id map: vertex ids sorted (signed order), their dense index alongside
     ScopedBuf<uint64_t> ik, sk;
     ScopedBuf<uint32_t> iv, sv;
@@ -606,12 +617,14 @@ int assemble_rows_device(RowStaging& st, HostGraph& g, hipStream_t s, std::strin
     ScopedBuf<int32_t> row, dense;
     ScopedBuf<uint32_t> fl[2], col;
     AS_TRY(row.alloc(E)); AS_TRY(dense.alloc(E)); AS_TRY(fl[0].alloc(E)); AS_TRY(fl[1].alloc(E));
-    if (E) entry_dense<<<grid(E), kB, 0, s>>>(d_other.p, d_dir.p, E, d_rb.p, n, sk.p, sv.p, row.p, dense.p, fl[0].p, fl[1].p);
+    if (E) entry_dense<<<grid(E), kB, 0, s>>>(p_other, p_dir, E, d_rb.p, n, sk.p, sv.p, row.p, dense.p, fl[0].p, fl[1].p);
     if (keep_col) {
         AS_TRY(col.alloc(E));
         if (E) col_of<<<grid(E), kB, 0, s>>>(row.p, d_rb.p, E, col.p);
     }
+    AS_TRY(hipStreamSynchronize(s));
     d_other.release(); d_dir.release(); sk.release(); sv.release();
+    st.d_other.reset(); st.d_dir.reset();
     // per direction: kept entries in staged order, keys row << b | dense
     ScopedBuf<uint64_t> k1[2];
     ScopedBuf<uint32_t> v1[2];
@@ -669,7 +682,7 @@ int assemble_rows_device(RowStaging& st, HostGraph& g, hipStream_t s, std::strin
         if (keep_col) AS_TRY(fcol[d].alloc(c));
         // payload chain: sorted position -> kept index (vs) -> staged entry (v1)
         if (c)
-            emit_list<<<grid(c), kB, 0, s>>>(fkey[d].p, vs.p, c, b, v1[d].p, d_w.p, nullptr, fadj[d].p,
+            emit_list<<<grid(c), kB, 0, s>>>(fkey[d].p, vs.p, c, b, v1[d].p, p_w, nullptr, fadj[d].p,
                                              weighted ? fw[d].p : nullptr, nullptr);
         if (keep_col && c) {
             ScopedBuf<uint32_t> staged;              // staged entry of every final entry

@@ -186,7 +186,7 @@ int stage_rows_raw(RowStaging& st, const tgo_rows* rows, const tgo_schema* schem
 }
 
 int decode_staged_raw(RowStaging& st, int pb, int64_t hard_limit, DecodeScratch& ds, hipStream_t stream,
-                      std::string& err) {
+                      std::string& err, bool device_entries) {
     const HostPlan& hp = st.plan;
     const tgo_load_opts* opts = &st.opts;
     const bool typed = !st.labels.empty();
@@ -278,16 +278,22 @@ int decode_staged_raw(RowStaging& st, int pb, int64_t hard_limit, DecodeScratch&
     }
     const int64_t kept = rk[nrows];
     const size_t e0 = st.other.size();
-    st.other.resize(e0 + static_cast<size_t>(kept));
-    st.dir.resize(e0 + static_cast<size_t>(kept));
-    st.w.resize(e0 + static_cast<size_t>(kept));
-    if (kept > 0) {
+    if (device_entries && e0 == 0 && !st.d_other.present()) {
+        // the compacted entries stay where they are: the device assembly reads them in place
+        st.d_other.own(ds.c_other.p, kept); ds.c_other.p = nullptr; ds.c_other.cap = 0;
+        st.d_dir.own(ds.c_dir.p, kept); ds.c_dir.p = nullptr; ds.c_dir.cap = 0;
+        st.d_w.own(ds.c_w.p, kept); ds.c_w.p = nullptr; ds.c_w.cap = 0;
+    } else if (kept > 0) {
+        st.other.resize(e0 + static_cast<size_t>(kept));
+        st.dir.resize(e0 + static_cast<size_t>(kept));
+        st.w.resize(e0 + static_cast<size_t>(kept));
         DEC_TRY(hipMemcpyAsync(st.other.data() + e0, ds.c_other.p, kept * 8, hipMemcpyDeviceToHost, stream));
         DEC_TRY(hipMemcpyAsync(st.dir.data() + e0, ds.c_dir.p, kept, hipMemcpyDeviceToHost, stream));
         DEC_TRY(hipMemcpyAsync(st.w.data() + e0, ds.c_w.p, kept * 4, hipMemcpyDeviceToHost, stream));
         DEC_TRY(hipStreamSynchronize(stream));
     }
 #undef DEC_TRY
+    if (st.d_other.present() && st.d_other.n != kept) { err = "staged entries out of step"; return TGO_E_STATE; }
     std::vector<int64_t>().swap(st.raw_keys);
     st.raw_eb.assign(1, 0);
     st.raw_bb.assign(1, 0);
@@ -301,6 +307,23 @@ int decode_staged_raw(RowStaging& st, int pb, int64_t hard_limit, DecodeScratch&
         st.n_rep += rep[r];
         st.row_begin.push_back(static_cast<int64_t>(e0) + rk[r + 1]);
     }
+    return TGO_OK;
+}
+
+int staging_entries_to_host(RowStaging& st, hipStream_t stream, std::string& err) {
+    if (!st.d_other.present()) return TGO_OK;
+    const int64_t E = st.d_other.n;
+    hipError_t e = hipStreamSynchronize(stream);
+    st.other.resize(static_cast<size_t>(E));
+    st.dir.resize(static_cast<size_t>(E));
+    st.w.resize(static_cast<size_t>(E));
+    if (E > 0 && e == hipSuccess) e = copy_chunked(st.other.data(), st.d_other.p, E * 8, hipMemcpyDeviceToHost);
+    if (E > 0 && e == hipSuccess) e = copy_chunked(st.dir.data(), st.d_dir.p, E, hipMemcpyDeviceToHost);
+    if (E > 0 && e == hipSuccess) e = copy_chunked(st.w.data(), st.d_w.p, E * 4, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) { err = hipGetErrorString(e); return TGO_E_HIP; }
+    st.d_other.reset();
+    st.d_dir.reset();
+    st.d_w.reset();
     return TGO_OK;
 }
 

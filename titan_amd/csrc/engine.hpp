@@ -91,6 +91,12 @@ struct RowStaging {
     std::vector<int64_t> other;      // other vertex Titan id per kept entry
     std::vector<uint8_t> dir;        // 0 OUT, 1 IN
     std::vector<int32_t> w;          // weight (INT32_MIN = property missing)
+    // the device decoder's kept entries stay on the device for the device assembly (the
+    // host vectors other / dir / w are then empty; staging_entries_to_host fetches them)
+    DevArray<int64_t> d_other;
+    DevArray<uint8_t> d_dir;
+    DevArray<int32_t> d_w;
+    int64_t entries() const { return d_other.present() ? d_other.n : static_cast<int64_t>(other.size()); }
     std::vector<uint8_t> rep;        // per row: 1 = non-canonical representative of a vertex cut
     int64_t ghost = 0, truncated = 0, skipped = 0;
     int64_t n_rep = 0;               // representative rows staged
@@ -181,7 +187,10 @@ struct DecodeScratch {
 int stage_rows_raw(RowStaging& st, const tgo_rows* rows, const tgo_schema* schema, const tgo_load_opts* opts,
                    DecodeScratch& ds, hipStream_t stream, std::string& err);
 int decode_staged_raw(RowStaging& st, int pb, int64_t hard_limit, DecodeScratch& ds, hipStream_t stream,
-                      std::string& err);
+                      std::string& err,
+                      bool device_entries = false);
+// Device-resident staged entries (decode_staged_raw with device_entries) to the host vectors.
+int staging_entries_to_host(RowStaging& st, hipStream_t stream, std::string& err);
 int decode_rows(RowStaging& st, const tgo_rows* rows, const tgo_schema* schema,
                 const tgo_load_opts* opts, int pb, int64_t hard_limit, int threads,
                 std::string& err);
