@@ -1,12 +1,10 @@
 #!/bin/bash
-# Round-3 call m: rows load with device-resident decoded entries (tests + probe); SSSP delta sweep
-# under the device loop.
+# Round-3 call o: unrolled / mask-skipping extraction (every frontier kernel): parity tests and probes.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
-OUT=gpurun_out/r03m; mkdir -p $OUT
+OUT=gpurun_out/r03o; mkdir -p $OUT
 T="python -u -m pytest -x -q --timeout 300 --timeout-method thread"
-timeout -k 10 600 $T tests/test_gpu_assembly.py tests/test_gpu_decode.py tests/test_gpu_scan.py > $OUT/gpu_tests.log 2>&1
+timeout -k 10 700 $T tests/test_gpu_parity.py tests/test_gpu_fullsize.py tests/test_gpu_distributed.py > $OUT/gpu_tests.log 2>&1
 rc=$?; tail -3 $OUT/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
-TGO_TRACE=1 timeout -k 10 300 python3 scripts/rows_probe.py 20 > $OUT/rows.log 2>&1
-rc=$?; grep -E "finish|load [0-9]" $OUT/rows.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 400 python3 scripts/sssp_probe.py 24 12,16,24,31,48,64 > $OUT/sssp_delta.log 2>&1
-rc=$?; grep -E "^delta" $OUT/sssp_delta.log; exit $rc
+timeout -k 10 200 python3 scripts/ms_probe.py 24 5 > $OUT/ms.log 2>&1; rc=$?; grep msbfs $OUT/ms.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python3 scripts/sssp_probe.py 24 0 > $OUT/sssp.log 2>&1; rc=$?; grep "^delta" $OUT/sssp.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python3 scripts/bfs_probe.py > $OUT/bfs.log 2>&1; rc=$?; tail -3 $OUT/bfs.log; exit $rc

@@ -152,7 +152,7 @@ __global__ void __launch_bounds__(kBlock) bfs_queue(View push, int64_t n, const 
         const int64_t v = (wd << 6) + lane();
         const bool take = v < n && ((fb[wd] >> lane()) & 1ULL);
         t[0] = {take, static_cast<int32_t>(v), take ? push_degree(push, v) : 0};
-        return true;
+        return __ballot(take) != 0;
     };
     chunk_extract<1>(words, probe, qn, qdeg, cnt);
 }

@@ -136,49 +136,32 @@ __device__ __forceinline__ void chunk_extract_packed(int64_t words, const Probe&
     const int64_t w1 = min(words, w0 + per);
     const int wave = threadIdx.x >> 6;
     const unsigned long long below = (1ULL << lane()) - 1ULL;
-    int64_t count = 0, dsum = 0;             // this lane's takes (count per lane, not per wave)
+    int64_t count = 0, dsum = 0;             // this lane's takes
+    unsigned long long mask = 0;
     bool touch = false;
-    constexpr int kUnroll = 4;
-    int64_t wd = w0 + wave;
-    for (; wd + (kUnroll - 1) * kWavesPerBlock < w1; wd += kUnroll * kWavesPerBlock) {
-        Take t[kUnroll][kStreams];
-#pragma unroll
-        for (int u = 0; u < kUnroll; ++u) touch |= probe(wd + u * kWavesPerBlock, t[u], false);
-#pragma unroll
-        for (int u = 0; u < kUnroll; ++u)
-            for (int k = 0; k < kStreams; ++k)
-                if (t[u][k].take) { ++count; dsum += t[u][k].deg; }
-    }
-    for (; wd < w1; wd += kWavesPerBlock) {
-        Take t[kStreams];
-        touch |= probe(wd, t, false);
-        for (int k = 0; k < kStreams; ++k)
-            if (t[k].take) { ++count; dsum += t[k].deg; }
-    }
-    // per-wave totals, wave-major: the pass-2 order is word by word inside a wave, so only the
-    // wave's first slot / offset come from the reservation
+    extract_count<kStreams>(w0 + wave, w1, probe, count, dsum, mask, touch);
+    // per-wave totals: the pass-2 order is word by word inside a wave, so only the wave's
+    // first slot / offset come from the reservation
     const int64_t wc = wave_incl_scan(count), wdg = wave_incl_scan(dsum);
     int64_t slot0, doff0;
     block_reserve(qc, lane() == 63 ? wc : 0, lane() == 63 ? wdg : 0, slot0, doff0);
     int64_t cursor = __shfl(slot0, 63, 64), dcur = __shfl(doff0, 63, 64);
     if (!touch) return;                                      // wave-uniform
-    for (int64_t w = w0 + wave; w < w1; w += kWavesPerBlock) {
-        Take t[kStreams];
-        probe(w, t, true);
+    extract_write<kStreams>(w0 + wave, w1, mask, probe, [&](const Take* t) {
         for (int k = 0; k < kStreams; ++k) {
-            const unsigned long long mask = __ballot(t[k].take);
-            if (!mask) continue;
+            const unsigned long long bm = __ballot(t[k].take);
+            if (!bm) continue;
             const int64_t d = t[k].take ? t[k].deg : 0;
             const int64_t id = wave_incl_scan(d);
             if (t[k].take) {
-                const int64_t slot = cursor + __popcll(mask & below);
+                const int64_t slot = cursor + __popcll(bm & below);
                 qn[slot] = t[k].entry;
                 qpre[slot] = dcur + id - d;
             }
-            cursor += __popcll(mask);
+            cursor += __popcll(bm);
             dcur += __shfl(id, 63, 64);
         }
-    }
+    });
 }
 
 __global__ void __launch_bounds__(kBlock) ds_extract_dev(const int64_t* __restrict__ off,

@@ -160,9 +160,73 @@ __device__ __forceinline__ void count_flush(Counters* cnt, unsigned long long nv
 // reserves its slots, pass 2 re-reads (L2-warm) and writes.  No per-trip block barriers or
 // counter atomics, which dominated the one-pass form (~200 us per extraction at 16M
 // vertices).  probe(wd, takes, commit) fills up to kStreams (take, entry, degree) per lane and
-// returns whether the word needs a write; with commit it also applies its writes (one writer
-// per word) — pass 1 never writes, so both passes see the same state.
+// returns whether the word needs pass 2 (it takes something or, with commit, writes
+// something); with commit it also applies its writes (one writer per word) — pass 1 never
+// writes, so both passes see the same state.  Both passes keep kUnroll words in flight per
+// wave (one word per trip left each wave waiting a memory latency per word), and pass 2
+// visits only the words pass 1 flagged (a wave's first 64 words by a bit mask; a longer
+// chunk visits all).
 struct Take { bool take; int32_t entry; int64_t deg; };
+constexpr int kExtractUnroll = 4;
+// Pass 1 of a wave's words [first, end) step kWavesPerBlock: per-lane take counts and degree
+// sums, the flagged-word mask (bit i = i-th word of the wave), and whether any word was flagged.
+template <int kStreams, class Probe>
+__device__ __forceinline__ void extract_count(int64_t first, int64_t end, const Probe& probe, int64_t& count,
+                                              int64_t& dsum, unsigned long long& mask, bool& touch) {
+    int64_t wd = first;
+    int idx = 0;
+    for (; wd + (kExtractUnroll - 1) * kWavesPerBlock < end; wd += kExtractUnroll * kWavesPerBlock, idx += kExtractUnroll) {
+        Take t[kExtractUnroll][kStreams];
+        bool r[kExtractUnroll];
+#pragma unroll
+        for (int u = 0; u < kExtractUnroll; ++u) r[u] = probe(wd + u * kWavesPerBlock, t[u], false);
+#pragma unroll
+        for (int u = 0; u < kExtractUnroll; ++u) {
+            if (r[u]) { touch = true; if (idx + u < 64) mask |= 1ULL << (idx + u); }
+            for (int k = 0; k < kStreams; ++k)
+                if (t[u][k].take) { ++count; dsum += t[u][k].deg; }
+        }
+    }
+    for (; wd < end; wd += kWavesPerBlock, ++idx) {
+        Take t[kStreams];
+        if (probe(wd, t, false)) { touch = true; if (idx < 64) mask |= 1ULL << idx; }
+        for (int k = 0; k < kStreams; ++k)
+            if (t[k].take) { ++count; dsum += t[k].deg; }
+    }
+}
+// Pass 2: the flagged words in order (all words when the wave has more than 64), kUnroll
+// probes in flight, then emit(takes) per word in order.
+template <int kStreams, class Probe, class Emit>
+__device__ __forceinline__ void extract_write(int64_t first, int64_t end, unsigned long long mask, const Probe& probe,
+                                              const Emit& emit) {
+    const int64_t nwords = end > first ? (end - first + kWavesPerBlock - 1) / kWavesPerBlock : 0;
+    const bool all = nwords > 64;
+    int64_t next = 0;                        // (all) next word index to visit
+    for (;;) {
+        int64_t wl[kExtractUnroll];
+        bool any = false;
+#pragma unroll
+        for (int u = 0; u < kExtractUnroll; ++u) {
+            wl[u] = -1;
+            if (all) {
+                if (next < nwords) wl[u] = first + (next++) * kWavesPerBlock;
+            } else if (mask) {
+                const int b = __ffsll(static_cast<long long>(mask)) - 1;
+                mask &= mask - 1;
+                wl[u] = first + static_cast<int64_t>(b) * kWavesPerBlock;
+            }
+            any |= wl[u] >= 0;
+        }
+        if (!any) break;                      // wave-uniform
+        Take t[kExtractUnroll][kStreams];
+#pragma unroll
+        for (int u = 0; u < kExtractUnroll; ++u)
+            if (wl[u] >= 0) probe(wl[u], t[u], true);
+#pragma unroll
+        for (int u = 0; u < kExtractUnroll; ++u)
+            if (wl[u] >= 0) emit(t[u]);
+    }
+}
 template <int kStreams, class Probe>
 __device__ __forceinline__ void chunk_extract(int64_t words, const Probe& probe, int32_t* __restrict__ qn,
                                               int64_t* __restrict__ qdeg, Counters* cnt) {
@@ -172,57 +236,34 @@ __device__ __forceinline__ void chunk_extract(int64_t words, const Probe& probe,
     const int64_t w1 = min(words, w0 + per);
     const int wave = threadIdx.x >> 6;
     const unsigned long long below = (1ULL << lane()) - 1ULL;
-    unsigned long long count = 0, dsum = 0;
+    int64_t count = 0, dsum = 0;
+    unsigned long long mask = 0;
     bool touch = false;
-    // pass 1 reads only: kUnroll words per trip, so their loads are in flight together (one
-    // word per trip left each wave waiting a memory latency per word, ~60 us per extraction
-    // at 16M vertices)
-    constexpr int kUnroll = 4;
-    int64_t wd = w0 + wave;
-    for (; wd + (kUnroll - 1) * kWavesPerBlock < w1; wd += kUnroll * kWavesPerBlock) {
-        Take t[kUnroll][kStreams];
-#pragma unroll
-        for (int u = 0; u < kUnroll; ++u) touch |= probe(wd + u * kWavesPerBlock, t[u], false);
-#pragma unroll
-        for (int u = 0; u < kUnroll; ++u)
-            for (int k = 0; k < kStreams; ++k) {
-                count += __popcll(__ballot(t[u][k].take));
-                if (t[u][k].take) dsum += static_cast<unsigned long long>(t[u][k].deg);
-            }
-    }
-    for (; wd < w1; wd += kWavesPerBlock) {
-        Take t[kStreams];
-        touch |= probe(wd, t, false);
-        for (int k = 0; k < kStreams; ++k) {
-            count += __popcll(__ballot(t[k].take));
-            if (t[k].take) dsum += static_cast<unsigned long long>(t[k].deg);
-        }
-    }
-    for (int o = 32; o > 0; o >>= 1) dsum += __shfl_xor(dsum, o, 64);
-    if (lane() == 0) { s_cnt[wave] = count; s_mf[wave] = dsum; }
+    extract_count<kStreams>(w0 + wave, w1, probe, count, dsum, mask, touch);
+    unsigned long long c = static_cast<unsigned long long>(count), m = static_cast<unsigned long long>(dsum);
+    for (int o = 32; o > 0; o >>= 1) { c += __shfl_xor(c, o, 64); m += __shfl_xor(m, o, 64); }
+    if (lane() == 0) { s_cnt[wave] = c; s_mf[wave] = m; }
     __syncthreads();
     if (threadIdx.x == 0) {
-        unsigned long long t = 0, m = 0;
-        for (int w = 0; w < kWavesPerBlock; ++w) { const unsigned long long c = s_cnt[w]; s_cnt[w] = t; t += c; m += s_mf[w]; }
+        unsigned long long t = 0, mm = 0;
+        for (int w = 0; w < kWavesPerBlock; ++w) { const unsigned long long x = s_cnt[w]; s_cnt[w] = t; t += x; mm += s_mf[w]; }
         s_base = t ? atomicAdd(&cnt->qlen, t) : 0ULL;
-        if (m) atomicAdd(&cnt->mf, m);
+        if (mm) atomicAdd(&cnt->mf, mm);
     }
     __syncthreads();
     if (!touch) return;                                      // wave-uniform
     unsigned long long cursor = s_base + s_cnt[wave];
-    for (int64_t wd = w0 + wave; wd < w1; wd += kWavesPerBlock) {
-        Take t[kStreams];
-        probe(wd, t, true);
+    extract_write<kStreams>(w0 + wave, w1, mask, probe, [&](const Take* t) {
         for (int k = 0; k < kStreams; ++k) {
-            const unsigned long long mask = __ballot(t[k].take);
+            const unsigned long long bm = __ballot(t[k].take);
             if (t[k].take) {
-                const unsigned long long slot = cursor + __popcll(mask & below);
+                const unsigned long long slot = cursor + __popcll(bm & below);
                 qn[slot] = t[k].entry;
                 qdeg[slot] = t[k].deg;
             }
-            cursor += __popcll(mask);
+            cursor += __popcll(bm);
         }
-    }
+    });
 }
 
 // Grid for chunk_extract: >= 64 words per block, at most 2048 blocks.

@@ -238,9 +238,9 @@ __global__ void __launch_bounds__(kBlock) ms_settle(View push, int64_t n_active,
     const int64_t words = (n_active + 63) >> 6;
     auto probe = [&](int64_t wd, Take* t, bool commit) -> bool {
         const int64_t v = (wd << 6) + lane();
-        uint64_t fresh = 0;
+        uint64_t fresh = 0, c = 0;
         if (v < n_active) {
-            const uint64_t c = nx[v];
+            c = nx[v];
             if (c) {
                 const uint64_t seen = vis[v];
                 fresh = c & ~seen;
@@ -251,7 +251,7 @@ __global__ void __launch_bounds__(kBlock) ms_settle(View push, int64_t n_active,
             }
         }
         t[0] = {fresh != 0, static_cast<int32_t>(v), fresh ? push_degree(push, v) : 0};
-        return true;
+        return __ballot(c != 0) != 0;                           // words with candidates are rewritten
     };
     chunk_extract<1>(words, probe, qn, qdeg, cnt);
 }
@@ -265,7 +265,7 @@ __global__ void __launch_bounds__(kBlock) ms_queue(View push, int64_t n_active, 
         const int64_t v = (wd << 6) + lane();
         const bool take = v < n_active && fr[v] != 0;
         t[0] = {take, static_cast<int32_t>(v), take ? push_degree(push, v) : 0};
-        return true;
+        return __ballot(take) != 0;
     };
     chunk_extract<1>(words, probe, qn, qdeg, cnt);
 }
