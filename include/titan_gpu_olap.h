@@ -258,6 +258,22 @@ int  tgo_load_rows(tgo_ctx* ctx, const tgo_rows* rows, const tgo_schema* schema,
 int  tgo_finish_load(tgo_ctx* ctx);
 /* Load an already-decoded edge list (finishes the load). */
 int  tgo_load_edges(tgo_ctx* ctx, const tgo_edges* edges, const tgo_load_opts* opts);
+/* Load a caller-assembled adjacency (SURVEY §8(b) tgo_load_csr; finishes the load): the
+ * rows as a CSR-collecting scan job holds them after VertexJobConverter
+ * (VertexJobConverter.java:109-129) — row v (dense index 0..n-1 in row order, Titan id
+ * titan_ids[v], strictly increasing; NULL = synthesised) has the OUT entries
+ * [out_off[v], out_off[v+1]) and the IN entries [in_off[v], in_off[v+1]) of out_idx / in_idx
+ * (dense neighbour indices), weights out_w / in_w (NULL when opts->weight_key == 0).
+ * The rows are taken as preloaded: a cut the scan applied stays (opts->apply_cap is not
+ * applied again) and the OUT and IN lists need not be transposes of each other (the push view
+ * is then an explicit transpose).  A row's OUT entries and then its IN entries, in the given
+ * order, are its column order (TGO_LOAD_COLUMN_ORDER positions).  opts->scope picks the
+ * views as for every load; label_ids must be empty.
+ * Returns TGO_E_INVALID for decreasing offsets, an index outside [0, n), non-increasing
+ * titan_ids or a missing weight array. */
+int  tgo_load_csr(tgo_ctx* ctx, int64_t n, const int64_t* titan_ids, const int64_t* out_off,
+                  const int32_t* out_idx, const int32_t* out_w, const int64_t* in_off,
+                  const int32_t* in_idx, const int32_t* in_w, const tgo_load_opts* opts);
 
 /* One edge entry through the product decoder (EdgeSerializer.parseRelation, :73-166, restricted
  * to what the traversal reads), on the host, without a ctx or a device: the per-entry half of

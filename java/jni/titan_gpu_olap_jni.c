@@ -142,6 +142,42 @@ JNIEXPORT jint JNICALL JFN(finishLoad)(JNIEnv* env, jclass cls, jlong h) {
     return tgo_finish_load(CTX(h));
 }
 
+/* tgo_load_csr: the rows a Java CSR collector already holds (dense neighbour indices); the
+ * weight arrays may be null when weightKey == 0. */
+JNIEXPORT jint JNICALL JFN(loadCsr)(JNIEnv* env, jclass cls, jlong h, jlongArray ids, jlongArray out_off,
+                                    jintArray out_idx, jintArray out_w, jlongArray in_off, jintArray in_idx,
+                                    jintArray in_w, jint scope, jlong weight_key, jboolean column_order) {
+    (void)cls;
+    const jsize n1 = (*env)->GetArrayLength(env, out_off);
+    if (n1 < 1 || (*env)->GetArrayLength(env, in_off) != n1 || (*env)->GetArrayLength(env, ids) != n1 - 1)
+        return TGO_E_INVALID;
+    jlong* t = (*env)->GetLongArrayElements(env, ids, NULL);
+    jlong* oo = (*env)->GetLongArrayElements(env, out_off, NULL);
+    jlong* io = (*env)->GetLongArrayElements(env, in_off, NULL);
+    jint* oi = (*env)->GetIntArrayElements(env, out_idx, NULL);
+    jint* ii = (*env)->GetIntArrayElements(env, in_idx, NULL);
+    jint* ow = out_w ? (*env)->GetIntArrayElements(env, out_w, NULL) : NULL;
+    jint* iw = in_w ? (*env)->GetIntArrayElements(env, in_w, NULL) : NULL;
+    int rc = TGO_E_OOM;
+    if (t && oo && io && oi && ii && (!out_w || ow) && (!in_w || iw)) {
+        tgo_load_opts o;
+        memset(&o, 0, sizeof o);
+        o.scope = scope;
+        o.weight_key = weight_key;
+        o.flags = column_order ? TGO_LOAD_COLUMN_ORDER : 0;
+        rc = tgo_load_csr(CTX(h), (int64_t)(n1 - 1), (const int64_t*)t, (const int64_t*)oo, (const int32_t*)oi,
+                          (const int32_t*)ow, (const int64_t*)io, (const int32_t*)ii, (const int32_t*)iw, &o);
+    }
+    if (t) (*env)->ReleaseLongArrayElements(env, ids, t, JNI_ABORT);
+    if (oo) (*env)->ReleaseLongArrayElements(env, out_off, oo, JNI_ABORT);
+    if (io) (*env)->ReleaseLongArrayElements(env, in_off, io, JNI_ABORT);
+    if (oi) (*env)->ReleaseIntArrayElements(env, out_idx, oi, JNI_ABORT);
+    if (ii) (*env)->ReleaseIntArrayElements(env, in_idx, ii, JNI_ABORT);
+    if (ow) (*env)->ReleaseIntArrayElements(env, out_w, ow, JNI_ABORT);
+    if (iw) (*env)->ReleaseIntArrayElements(env, in_w, iw, JNI_ABORT);
+    return rc;
+}
+
 JNIEXPORT jlongArray JNICALL JFN(vertexIds)(JNIEnv* env, jclass cls, jlong h) {
     (void)cls;
     if (!fits_jsize(env, tgo_num_vertices(CTX(h)), "more vertices than a Java array holds")) return NULL;

@@ -55,6 +55,15 @@ public final class TgoNative {
 
     public static native int finishLoad(long ctx);
 
+    /**
+     * tgo_load_csr: rows already collected as CSR (row v = titanIds[v]; OUT entries
+     * outIdx[outOff[v]..outOff[v+1]), IN entries inIdx[inOff[v]..inOff[v+1]) as dense indices;
+     * weights null when weightKey == 0).  The rows as preloaded: no cap is applied again.
+     */
+    public static native int loadCsr(long ctx, long[] titanIds, long[] outOff, int[] outIdx, int[] outWeight,
+                                     long[] inOff, int[] inIdx, int[] inWeight, int scope, long weightKey,
+                                     boolean columnOrder);
+
     public static native long[] vertexIds(long ctx);
 
     /** tgo_bfs with the unit edge function; null on failure (see lastError). */

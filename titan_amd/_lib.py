@@ -135,7 +135,7 @@ class Stats(C.Structure):
 # Every symbol include/*.h declares (checked by tests/test_abi.py).
 EXPORTS = [
     "tgo_default_options", "tgo_create", "tgo_destroy", "tgo_last_error", "tgo_load_rows",
-    "tgo_finish_load", "tgo_load_edges", "tgo_num_vertices", "tgo_vertex_ids", "tgo_graph_csr", "tgo_graph_perm",
+    "tgo_finish_load", "tgo_load_edges", "tgo_load_csr", "tgo_num_vertices", "tgo_vertex_ids", "tgo_graph_csr", "tgo_graph_perm",
     "tgo_bfs",
     "tgo_sssp", "tgo_copy_distances", "tgo_pagerank", "tgo_walkcount", "tgo_stats_get", "tgo_sync",
     "tgo_bfs_multi", "tgo_copy_multi_distances", "tgo_multi_stats",
@@ -184,6 +184,8 @@ def load() -> C.CDLL:
         "tgo_result_rows": (C.c_int, [vp, P(ResultArgs), P(ResultSize), P(RowsBuf)]),
         "tgo_decode_edge_entry": (C.c_int, [P(Schema), P(LoadOpts), _u8p, C.c_int64, C.c_int64, P(EdgeEntry)]),
         "tgo_load_edges": (C.c_int, [vp, P(Edges), P(LoadOpts)]),
+        "tgo_load_csr": (C.c_int, [vp, C.c_int64, P(C.c_int64), P(C.c_int64), P(C.c_int32), P(C.c_int32),
+                                   P(C.c_int64), P(C.c_int32), P(C.c_int32), P(LoadOpts)]),
         "tgo_num_vertices": (C.c_int64, [vp]),
         "tgo_vertex_ids": (C.c_int, [vp, _i64p]),
         "tgo_graph_csr": (C.c_int, [vp, C.c_int32, _i64p, _i64p, P(C.c_int32), P(C.c_int32), P(C.c_uint32)]),

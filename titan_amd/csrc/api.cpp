@@ -1042,6 +1042,39 @@ int tgo_load_edges(tgo_ctx* ctx, const tgo_edges* edges, const tgo_load_opts* op
     return rc;
 }
 
+int tgo_load_csr(tgo_ctx* ctx, int64_t n, const int64_t* titan_ids, const int64_t* out_off, const int32_t* out_idx,
+                 const int32_t* out_w, const int64_t* in_off, const int32_t* in_idx, const int32_t* in_w,
+                 const tgo_load_opts* opts) {
+    if (!ctx) return TGO_E_INVALID;
+    ctx->res_kind = -1;
+    if (!opts || !out_off || !in_off) return fail(ctx, TGO_E_INVALID, "null argument");
+    if (opts->scope < 0 || opts->scope > 2) return fail(ctx, TGO_E_INVALID, "invalid scope");
+    if (opts->n_labels != 0) return fail(ctx, TGO_E_INVALID, "tgo_load_csr takes no label_ids (the rows are already sliced)");
+    (void)hipSetDevice(ctx->opts.device);
+    const auto t0 = std::chrono::steady_clock::now();
+    // the rows as a staging of decoded rows (each row's OUT entries, then its IN entries), on
+    // the device; then the row assembly of tgo_finish_load
+    RowStaging st;
+    st.active = true;
+    st.opts = *opts;
+    st.opts.label_ids = nullptr;
+    const bool weighted = opts->weight_key != 0;
+    const CsrInput in{n, titan_ids, {out_off, in_off}, {out_idx, in_idx}, {out_w, in_w}};
+    std::string err;
+    int rc = stage_csr_device(in, weighted, st, ctx->stream, err);
+    if (rc) return fail(ctx, rc, err);
+    HostGraph h;
+    const bool on_dev = env_i64("TGO_HOST_ASSEMBLY", 0) == 0;
+    if (!on_dev) rc = staging_entries_to_host(st, ctx->stream, err);
+    if (!rc) rc = on_dev ? assemble_rows_device(st, h, ctx->stream, err) : assemble_from_rows(st, h, threads_of(ctx), err);
+    if (rc) return fail(ctx, rc, err);
+    free_graph(ctx);
+    ctx->staging = RowStaging();
+    rc = upload_graph(ctx, h);
+    ctx->st.load_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return rc;
+}
+
 int64_t tgo_num_vertices(const tgo_ctx* ctx) { return ctx && ctx->loaded ? ctx->g.n : 0; }
 
 int tgo_vertex_ids(tgo_ctx* ctx, int64_t* out) {
@@ -1231,7 +1264,8 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
             HIP_TRY(k_ms_pull(pull, push, g.n_active, full, fr, filter ? s.ms_fbm : nullptr, s.ms_vis, nx,
                               ms_planes(ctx), s.cnt, L + 1, st, filter ? filter_from : 0));
         } else {
-            HIP_TRY(hipMemsetAsync(nx, 0, n * 8, st));
+            // candidates only land on rows with entries (< n_active); the tail is never read
+            HIP_TRY(hipMemsetAsync(nx, 0, g.n_active * 8, st));
             if ((rc = scan_frontier(ctx, qlen))) return rc;
             HIP_TRY(k_ms_push(push, s.q[cur], s.qpre, qlen, fr, s.ms_vis, nx, st));
             HIP_TRY(k_ms_settle(push, g.n_active, s.ms_vis, nx, ms_planes(ctx), s.q[cur ^ 1], s.qdeg, s.cnt, L + 1, st));

@@ -307,6 +307,26 @@ struct Sorter {
     }
 };
 
+// tgo_load_csr staging: entry k of direction d's list (row v by binary search over off)
+// goes to its row's slot rb[v] + (OUT: k - off[v]; IN: out degree + k - off[v]); the other
+// endpoint as its Titan id, bad indices flagged.
+__global__ void csr_stage(const int64_t* __restrict__ off, const int32_t* __restrict__ idx,
+                          const int32_t* __restrict__ w, const int64_t* __restrict__ other_off, int dir, int64_t n,
+                          int64_t m, const int64_t* __restrict__ rb, const int64_t* __restrict__ tid,
+                          int64_t* __restrict__ other, uint8_t* __restrict__ odir, int32_t* __restrict__ ow, int* bad) {
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x) {
+        int64_t a = 0, b = n;                          // last v with off[v] <= k
+        while (b - a > 1) { const int64_t c = (a + b) >> 1; if (off[c] <= k) a = c; else b = c; }
+        const int64_t base = dir == 0 ? 0 : other_off[a + 1] - other_off[a];   // IN entries after OUT
+        const int64_t pos = rb[a] + base + (k - off[a]);
+        const int32_t u = idx[k];
+        if (u < 0 || u >= n) { *bad = 1; continue; }
+        other[pos] = tid[u];
+        odir[pos] = static_cast<uint8_t>(dir);
+        if (ow) ow[pos] = w[k];
+    }
+}
+
 template <class T>
 hipError_t download(std::vector<T>& h, const T* d, int64_t count, hipStream_t s) {
     h.resize(static_cast<size_t>(count));
@@ -551,6 +571,71 @@ int assemble_edges_device(const tgo_edges* e, const tgo_load_opts* opts, int64_t
     return TGO_OK;
 }
 
+
+int stage_csr_device(const CsrInput& in, bool weighted, RowStaging& st, hipStream_t s, std::string& err) {
+    const int64_t n = in.n;
+    if (n < 0 || n >= INT32_MAX) { err = "vertex count out of range"; return TGO_E_INVALID; }
+    int64_t m[2];
+    for (int d = 0; d < 2; ++d) {
+        if (!in.off[d] || (n > 0 && in.off[d][0] != 0)) { err = "offsets must start at 0"; return TGO_E_INVALID; }
+        for (int64_t v = 0; v < n; ++v)
+            if (in.off[d][v + 1] < in.off[d][v]) { err = "row offsets decrease"; return TGO_E_INVALID; }
+        m[d] = n > 0 ? in.off[d][n] : 0;
+        if (m[d] > 0 && !in.idx[d]) { err = "null index array"; return TGO_E_INVALID; }
+        if (weighted && m[d] > 0 && !in.w[d]) { err = "a weight array is missing"; return TGO_E_INVALID; }
+    }
+    const int64_t E = m[0] + m[1];
+    if (E >= (int64_t(1) << 32)) { err = "more than 2^32 entries per load"; return TGO_E_UNSUPPORTED; }
+    st.vid.resize(n);
+    for (int64_t v = 0; v < n; ++v) st.vid[v] = in.titan_ids ? in.titan_ids[v] : ((v + 1) << 3);
+    for (int64_t v = 1; in.titan_ids && v < n; ++v)
+        if (in.titan_ids[v] <= in.titan_ids[v - 1]) { err = "titan_ids must be strictly increasing"; return TGO_E_INVALID; }
+    st.rep.assign(n, 0);
+    st.row_begin.resize(n + 1);
+    st.row_begin[0] = 0;
+    for (int64_t v = 0; v < n; ++v)
+        st.row_begin[v + 1] = st.row_begin[v] + (in.off[0][v + 1] - in.off[0][v]) + (in.off[1][v + 1] - in.off[1][v]);
+    int64_t* d_other = nullptr;
+    uint8_t* d_dir = nullptr;
+    int32_t* d_w = nullptr;
+    AS_TRY(hipMalloc(&d_other, std::max<int64_t>(E, 1) * 8));
+    st.d_other.own(d_other, E);
+    AS_TRY(hipMalloc(&d_dir, std::max<int64_t>(E, 1)));
+    st.d_dir.own(d_dir, E);
+    if (weighted) {
+        AS_TRY(hipMalloc(&d_w, std::max<int64_t>(E, 1) * 4));
+        st.d_w.own(d_w, E);
+    }
+    if (n == 0 || E == 0) return TGO_OK;
+    ScopedBuf<int64_t> tid, rb, off[2];
+    ScopedBuf<int32_t> idx, w;
+    ScopedBuf<int> bad;
+    AS_TRY(tid.alloc(n)); AS_TRY(rb.alloc(n + 1)); AS_TRY(bad.alloc(1));
+    AS_TRY(copy_chunked(tid.p, st.vid.data(), n * 8, hipMemcpyHostToDevice));
+    AS_TRY(copy_chunked(rb.p, st.row_begin.data(), (n + 1) * 8, hipMemcpyHostToDevice));
+    for (int d = 0; d < 2; ++d) {
+        AS_TRY(off[d].alloc(n + 1));
+        AS_TRY(copy_chunked(off[d].p, in.off[d], (n + 1) * 8, hipMemcpyHostToDevice));
+    }
+    AS_TRY(hipMemsetAsync(bad.p, 0, sizeof(int), s));
+    for (int d = 0; d < 2; ++d) {
+        if (m[d] == 0) continue;
+        AS_TRY(idx.alloc(m[d]));
+        AS_TRY(copy_chunked(idx.p, in.idx[d], m[d] * 4, hipMemcpyHostToDevice));
+        if (weighted) {
+            AS_TRY(w.alloc(m[d]));
+            AS_TRY(copy_chunked(w.p, in.w[d], m[d] * 4, hipMemcpyHostToDevice));
+        }
+        csr_stage<<<grid(m[d]), kB, 0, s>>>(off[d].p, idx.p, weighted ? w.p : nullptr, off[0].p, d, n, m[d], rb.p, tid.p,
+                                            d_other, d_dir, weighted ? d_w : nullptr, bad.p);
+        AS_TRY(hipStreamSynchronize(s));                 // idx / w are reused by the next direction
+    }
+    int hb = 0;
+    AS_TRY(hipMemcpyAsync(&hb, bad.p, sizeof(int), hipMemcpyDeviceToHost, s));
+    AS_TRY(hipStreamSynchronize(s));
+    if (hb) { err = "neighbour index out of range"; return TGO_E_INVALID; }
+    return TGO_OK;
+}
 
 // Row loads (tgo_load_rows + tgo_finish_load): the host assemble_from_rows, on the device.
 // Vertex cuts (representative rows, PartitionedVertex ids) keep the host path (the caller

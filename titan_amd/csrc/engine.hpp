@@ -214,6 +214,16 @@ int assemble_edges_device(const tgo_edges* e, const tgo_load_opts* opts, int64_t
                           hipStream_t s, std::string& err);
 // assemble_from_rows on the device (no vertex cuts: the caller keeps those on the host path)
 int assemble_rows_device(RowStaging& st, HostGraph& g, hipStream_t s, std::string& err);
+// tgo_load_csr: the caller's rows as device-resident staging (each row's OUT entries then its
+// IN entries, neighbour Titan ids), for assemble_rows_device / assemble_from_rows.
+struct CsrInput {
+    int64_t n;
+    const int64_t* titan_ids;
+    const int64_t* off[2];
+    const int32_t* idx[2];
+    const int32_t* w[2];
+};
+int stage_csr_device(const CsrInput& in, bool weighted, RowStaging& st, hipStream_t s, std::string& err);
 int partition_layout(const tgo_edges* e, int64_t n_global, int64_t lo, int64_t hi, int threads,
                      int32_t* layout_local, std::string& err);
 int assemble_partition(const tgo_edges* e, int64_t n_global, int64_t lo, int64_t hi,

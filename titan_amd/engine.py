@@ -143,6 +143,30 @@ class Engine:
         self.n = self.lib.tgo_num_vertices(self.ctx)
         return self
 
+    def load_csr(self, n, out_off, out_idx, in_off, in_idx, scope, out_w=None, in_w=None, titan_ids=None,
+                 weight_key=0, column_order=False):
+        """A caller-assembled adjacency (tgo_load_csr): row v's OUT entries out_idx[out_off[v]:
+        out_off[v+1]] and IN entries in_idx[in_off[v]:in_off[v+1]] (dense neighbour indices), the
+        rows as preloaded (no cap applied again)."""
+        oo = np.ascontiguousarray(out_off, dtype=np.int64)
+        io = np.ascontiguousarray(in_off, dtype=np.int64)
+        oi = np.ascontiguousarray(out_idx, dtype=np.int32)
+        ii = np.ascontiguousarray(in_idx, dtype=np.int32)
+        ow = None if out_w is None else np.ascontiguousarray(out_w, dtype=np.int32)
+        iw = None if in_w is None else np.ascontiguousarray(in_w, dtype=np.int32)
+        t = None if titan_ids is None else np.ascontiguousarray(titan_ids, dtype=np.int64)
+        if len(oo) != n + 1 or len(io) != n + 1:
+            raise ValueError("offsets must hold n + 1 entries")
+        opts, keep = self._opts(scope, False, (), weight_key, L.LOAD_COLUMN_ORDER if column_order else 0)
+        if (ow is not None or iw is not None) and weight_key == 0:
+            opts.weight_key = 1      # any non-zero key: the lists carry the weights
+        rc = self.lib.tgo_load_csr(self.ctx, n, L.ptr(t, C.c_int64), L.ptr(oo, C.c_int64), L.ptr(oi, C.c_int32),
+                                   L.ptr(ow, C.c_int32), L.ptr(io, C.c_int64), L.ptr(ii, C.c_int32),
+                                   L.ptr(iw, C.c_int32), C.byref(opts))
+        _check(self.lib, self.ctx, rc)
+        self.n = self.lib.tgo_num_vertices(self.ctx)
+        return self
+
     # ------------------------------------------------------------------ 1-D partition (multi-GPU)
     def load_partition(self, n_global, lo, hi, src, dst, scope, weight=None, apply_cap=True, layout=None):
         """Rows of global vertices [lo, hi) (titan_gpu_olap_part.h); `layout` = the
