@@ -1,11 +1,14 @@
 #!/bin/bash
-# Round-3 call q: tgo_load_csr tests; staged push kernels (ms_push, td_expand) with tile appends: parity + probes.
+# Round-3 call r: source split with per-source frontier counts (parity + budget A/B), SSSP
+# with the separate decide kernel again.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
-OUT=gpurun_out/r03q; mkdir -p $OUT
+OUT=gpurun_out/r03r; mkdir -p $OUT
 T="python -u -m pytest -x -q --timeout 300 --timeout-method thread"
-timeout -k 10 800 $T tests/test_gpu_load_csr.py tests/test_gpu_parity.py tests/test_gpu_fullsize.py tests/test_gpu_distributed.py > $OUT/gpu_tests.log 2>&1
+timeout -k 10 800 $T tests/test_gpu_parity.py tests/test_gpu_fullsize.py::test_config3_rmat24_msbfs_sweep tests/test_gpu_fullsize.py::test_config5_rmat24_weighted_sssp tests/test_gpu_distributed.py > $OUT/gpu_tests.log 2>&1
 rc=$?; tail -3 $OUT/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 200 python3 scripts/ms_probe.py 24 5 > $OUT/ms.log 2>&1; rc=$?; grep msbfs $OUT/ms.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python3 scripts/bfs_probe.py 24 8 > $OUT/bfs.log 2>&1; rc=$?; tail -8 $OUT/bfs.log; [ $rc -eq 0 ] || exit $rc
+for f in 0 0.002 0.005 0.01 0.02; do TGO_MS_SPLIT=$f timeout -k 10 200 python3 scripts/ms_probe.py 24 5 > $OUT/ms_split_$f.log 2>&1 || exit 1; grep msbfs $OUT/ms_split_$f.log; done
+TGO_TRACE=1 TGO_MS_DIAG=1 timeout -k 10 200 python3 scripts/ms_probe.py 24 1 > $OUT/ms_diag.log 2>&1 || exit 1
+grep split $OUT/ms_diag.log | head -4
+timeout -k 10 300 python3 scripts/sssp_probe.py 24 0 > $OUT/sssp.log 2>&1; rc=$?; grep "^delta" $OUT/sssp.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/ms -o run -- python3 scripts/ms_probe.py 24 3 > $OUT/ms_prof.log 2>&1
 rc=$?; rm -f $OUT/ms/run_kernel_trace.csv; exit $rc

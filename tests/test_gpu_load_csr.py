@@ -101,7 +101,8 @@ def test_csr_load_cut_rows_match_the_oracle(monkeypatch):
     opr, _ = oracle.pagerank(0.85, n, 10)
     fin = np.isfinite(opr)
     assert np.array_equal(np.isfinite(pr), fin)
-    assert np.abs(pr[fin] - opr[fin]).sum() <= 1e-9
+    # the cut OUT lists make edgeCount small, so the ranks grow far beyond 1: relative L1
+    assert np.abs(pr[fin] - opr[fin]).sum() <= 1e-12 * np.abs(opr[fin]).sum()
 
 
 def test_csr_load_rejects_bad_input():

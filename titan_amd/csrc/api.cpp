@@ -1186,6 +1186,7 @@ static int ms_alloc(tgo_ctx* ctx) {
     HIP_TRY(dev_alloc(ctx, s.ms_fbm, (n + 63) / 64 + 1));
     HIP_TRY(dev_alloc(ctx, s.ms_seeds, TGO_MAX_SOURCES));
     HIP_TRY(dev_alloc(ctx, s.ms_stat, 2 * TGO_MAX_SOURCES));
+    HIP_TRY(dev_alloc(ctx, s.ms_srcent, TGO_MAX_SOURCES));
     ctx->st.device_bytes = ctx->dev_bytes;
     return TGO_OK;
 }
@@ -1237,6 +1238,9 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
     static const int32_t filter_from = env_double("TGO_MS_FILTER", 0.0) != 0.0
         ? 0 : static_cast<int32_t>(env_double("TGO_MS_FILTER_FROM", -1.0));
     const bool filter = filter_from >= 0 && filter_from < n;
+    // TGO_MS_SPLIT: push budget of the pull levels' sparse sources, as a fraction of the
+    // list entries (0 = every source pulled)
+    static const double split_frac = env_double("TGO_MS_SPLIT", 0.002);
     int64_t qlen = static_cast<int64_t>(uniq.size());
     int64_t mf = 0;
     {
@@ -1260,9 +1264,56 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
         HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
         queued = !use_pull;
         if (use_pull) {
+            // Split the sources: the pull's walk of a vertex stops once every open source is
+            // covered, and one source whose frontier never reaches the vertex (a source far
+            // from it, or one whose sweep is over) makes every walk scan its whole list.  The
+            // sources with the smallest frontiers (their push entries estimated as frontier
+            // size x the frontier's mean degree, within a budget of split_frac of the list
+            // entries, plus every source with an empty frontier) are pushed into candidate
+            // masks instead, and the pull covers only the rest.
+            uint64_t sparse = 0;
+            if (split_frac > 0.0) {
+                HIP_TRY(k_ms_source_counts(fr, g.n_active, s.ms_srcent, st));
+                unsigned long long se[TGO_MAX_SOURCES];
+                HIP_TRY(hipMemcpyAsync(se, s.ms_srcent, sizeof(se), hipMemcpyDeviceToHost, st));
+                HIP_TRY(hipStreamSynchronize(st));
+                int order[TGO_MAX_SOURCES];
+                for (int r = 0; r < nseeds; ++r) order[r] = r;
+                std::sort(order, order + nseeds, [&](int a, int b) { return se[a] < se[b]; });
+                const double budget = split_frac * static_cast<double>(total);
+                const double mean_deg = qlen > 0 ? static_cast<double>(mf) / static_cast<double>(qlen) : 0.0;
+                double used = 0.0;
+                for (int i = 0; i < nseeds; ++i) {
+                    const int r = order[i];
+                    const double cost = static_cast<double>(se[r]) * mean_deg;
+                    if (se[r] > 0 && used + cost > budget) break;
+                    used += cost;
+                    sparse |= 1ULL << r;
+                }
+                if (sparse == full) sparse = 0;            // nothing left to pull: plain pull
+                if (sparse) {
+                    bool any = false;
+                    for (int r = 0; r < nseeds; ++r) any |= ((sparse >> r) & 1ULL) && se[r] > 0;
+                    HIP_TRY(hipMemsetAsync(nx, 0, g.n_active * 8, st));
+                    if (any) {                           // push the sparse sources' frontiers
+                        HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
+                        HIP_TRY(k_ms_queue(push, g.n_active, fr, s.q[cur ^ 1], s.qdeg, s.cnt, st, sparse));
+                        if ((rc = read_counters(ctx))) return rc;
+                        const int64_t sq = static_cast<int64_t>(s.hcnt->qlen);
+                        HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
+                        if (sq > 0) {
+                            if ((rc = scan_frontier(ctx, sq))) return rc;
+                            HIP_TRY(k_ms_push(push, s.q[cur ^ 1], s.qpre, sq, fr, s.ms_vis, nx, st, PackTouch{}, sparse));
+                        }
+                    }
+                    if (trace) std::fprintf(stderr, "[tgo] ms level %d split: %d sparse sources, ~%.0f push entries\n", L,
+                                            __builtin_popcountll(sparse), used);
+                }
+            }
             if (filter) HIP_TRY(k_ms_fbitmap(fr, n, s.ms_fbm, st));
             HIP_TRY(k_ms_pull(pull, push, g.n_active, full, fr, filter ? s.ms_fbm : nullptr, s.ms_vis, nx,
-                              ms_planes(ctx), s.cnt, L + 1, st, filter ? filter_from : 0));
+                              ms_planes(ctx), s.cnt, L + 1, st, filter ? filter_from : 0, full & ~sparse,
+                              sparse ? nx : nullptr));
         } else {
             // candidates only land on rows with entries (< n_active); the tail is never read
             HIP_TRY(hipMemsetAsync(nx, 0, g.n_active * 8, st));

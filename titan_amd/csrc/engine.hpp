@@ -412,6 +412,7 @@ struct Scratch {
     // multi-source BFS (allocated on first use)
     uint64_t* ms_vis = nullptr;     // n: reached-by mask
     uint64_t* ms_fbm = nullptr;     // n/64: frontier bitmap of a pull level (fr != 0)
+    unsigned long long* ms_srcent = nullptr;   // 64: per-source frontier sizes of a pull level
     uint64_t* ms_fr = nullptr;      // n: frontier mask
     uint64_t* ms_nx = nullptr;      // n: next-frontier mask
     uint64_t* ms_lvl = nullptr;     // kLevelPlanes x n: bit r of plane k = bit k of source r's level
@@ -520,15 +521,18 @@ hipError_t k_ms_seed(const int64_t* seeds, int nseeds, uint64_t* vis, uint64_t* 
 hipError_t k_ms_diag_take(unsigned long long* out8, hipStream_t s);
 hipError_t k_ms_pull(const View& pull, const View& push, int64_t n_active, uint64_t full, const uint64_t* fr,
                      const uint64_t* fbm, uint64_t* vis, uint64_t* nx, LevelPlanes lvl, Counters* cnt,
-                     int32_t next_level, hipStream_t s, int32_t filter_from);
+                     int32_t next_level, hipStream_t s, int32_t filter_from, uint64_t dense = ~0ULL,
+                     const uint64_t* cand = nullptr);
+// per-source frontier sizes of fr (out64[s], zeroed first) — the pull level's split
+hipError_t k_ms_source_counts(const uint64_t* fr, int64_t n_active, unsigned long long* out64, hipStream_t s);
 hipError_t k_ms_fbitmap(const uint64_t* fr, int64_t n, uint64_t* fbm, hipStream_t s);
 hipError_t k_ms_queue(const View& push, int64_t n_active, const uint64_t* fr, int32_t* qn, int64_t* qdeg, Counters* cnt,
-                      hipStream_t s);
+                      hipStream_t s, uint64_t mask = ~0ULL);
 // Partitioned push: per-pack-chunk "written" flags (chunk of global word v: owner v / n_local,
 // chunk (v % n_local) / kPackChunk of the owner's cps) so the pack skips untouched chunks.
 struct PackTouch { uint8_t* flag = nullptr; int64_t n_local = 1; int64_t cps = 1; };
 hipError_t k_ms_push(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen, const uint64_t* fr,
-                     const uint64_t* vis, uint64_t* nx, hipStream_t s, PackTouch touch = {});
+                     const uint64_t* vis, uint64_t* nx, hipStream_t s, PackTouch touch = {}, uint64_t mask = ~0ULL);
 hipError_t k_ms_settle(const View& push, int64_t n_active, uint64_t* vis, uint64_t* nx, LevelPlanes lvl, int32_t* qn,
                        int64_t* qdeg, Counters* cnt, int32_t next_level, hipStream_t s);
 hipError_t k_ms_reach(const View& v, const uint64_t* vis, int64_t n_active, int nsrc, unsigned long long* reached,

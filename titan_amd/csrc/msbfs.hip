@@ -95,10 +95,13 @@ __device__ __forceinline__ bool maybe_frontier(const uint64_t* __restrict__ fbm,
 // long lists (wave-cooperative): [5] entries examined, [6] lists, [7] lists that stopped early
 constexpr int32_t kDiagHot = 393216;
 __device__ unsigned long long g_ms_diag[8];
-template <int kStep, bool kDiag = false>       // entries per dependent round trip of a lane's own list
+// kStep: entries per dependent round trip of a lane's own list; kLong: entries per lane per
+// trip of a wave-cooperative long list (kLong * 64 per trip)
+template <int kStep, bool kDiag = false, int kLong = 4>
 __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t n_active, uint64_t full,
         const uint64_t* __restrict__ fr, const uint64_t* __restrict__ fbm, uint64_t* __restrict__ vis,
-        uint64_t* __restrict__ nx, LevelPlanes lvl, Counters* cnt, int32_t next_level, int32_t filter_from) {
+        uint64_t* __restrict__ nx, LevelPlanes lvl, Counters* cnt, int32_t next_level, int32_t filter_from,
+        uint64_t dense, const uint64_t* __restrict__ cand) {
     unsigned long long nv = 0, mf = 0, bits = 0;
     unsigned long long dg[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const int64_t words = (n_active + 63) >> 6;
@@ -110,6 +113,9 @@ __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t 
         const int64_t v = (wd << 6) + lane();
         const uint64_t seen = v < n_active ? vis[v] : full;
         const uint64_t open = full & ~seen;
+        // the walk only has to cover the dense sources; the sparse ones come from the push
+        // candidates (cand, exact over every entry of their frontiers)
+        const uint64_t want = open & dense;
         int64_t b0 = 0, e0 = 0, b1 = 0, e1 = 0;
         if (open) {
             b0 = pull.off0[v]; e0 = pull.off0[v + 1];
@@ -117,13 +123,13 @@ __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t 
         }
         const int64_t deg = (e0 - b0) + (e1 - b1);
         uint64_t acc = 0;
-        if (open && deg <= kCoop) {
-            for (int l = 0; l < 2 && (acc & open) != open; ++l) {
+        if (want && deg <= kCoop) {
+            for (int l = 0; l < 2 && (acc & want) != want; ++l) {
                 const int32_t* adj = l == 0 ? pull.adj0 : pull.adj1;
                 const int64_t e = l == 0 ? e0 : e1;
                 // kStep entries per dependent round trip: their index loads issue together,
                 // then their mask gathers (lists rarely cover every open source early)
-                for (int64_t k = l == 0 ? b0 : b1; k < e && (acc & open) != open; k += kStep) {
+                for (int64_t k = l == 0 ? b0 : b1; k < e && (acc & want) != want; k += kStep) {
                     int32_t u[kStep];
 #pragma unroll
                     for (int j = 0; j < kStep; ++j) u[j] = k + j < e ? __builtin_nontemporal_load(adj + k + j) : -1;
@@ -140,46 +146,47 @@ __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t 
                             if (u[j] >= 0) { ++dg[0]; ++dg[u[j] < kDiagHot ? 1 : 2]; }
                 }
             }
-            if (kDiag) { ++dg[3]; if ((acc & open) == open) ++dg[4]; }
+            if (kDiag) { ++dg[3]; if ((acc & want) == want) ++dg[4]; }
         }
-        unsigned long long big = __ballot(open != 0 && deg > kCoop);
+        unsigned long long big = __ballot(want != 0 && deg > kCoop);
         while (big) {
             const int src = __ffsll(static_cast<long long>(big)) - 1;
             big &= big - 1;
-            const uint64_t want = __shfl(open, src, 64);
+            const uint64_t wsrc = __shfl(want, src, 64);
             uint64_t a = 0;
             for (int l = 0; l < 2; ++l) {
                 const int64_t bb = __shfl(l == 0 ? b0 : b1, src, 64);
                 const int64_t ee = __shfl(l == 0 ? e0 : e1, src, 64);
                 const int32_t* adj = l == 0 ? pull.adj0 : pull.adj1;
                 bool done = false;
-                for (int64_t k = bb; k < ee && !done; k += 4 * 64) {
-                    int32_t u[4];
+                for (int64_t k = bb; k < ee && !done; k += kLong * 64) {
+                    int32_t u[kLong];
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) {
+                    for (int j = 0; j < kLong; ++j) {
                         const int64_t x = k + j * 64 + lane();
                         u[j] = x < ee ? __builtin_nontemporal_load(adj + x) : -1;
                     }
-                    bool f[4];
+                    bool f[kLong];
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) f[j] = u[j] >= 0 && maybe_frontier(fbm, u[j], filter_from);
+                    for (int j = 0; j < kLong; ++j) f[j] = u[j] >= 0 && maybe_frontier(fbm, u[j], filter_from);
                     uint64_t m = 0;
 #pragma unroll
-                    for (int j = 0; j < 4; ++j)
+                    for (int j = 0; j < kLong; ++j)
                         if (f[j]) m |= fr[u[j]];
                     for (int off = 32; off > 0; off >>= 1) m |= __shfl_xor(m, off, 64);
                     a |= m;
-                    done = (a & want) == want;
+                    done = (a & wsrc) == wsrc;
                     if (kDiag && lane() == src)
-                        for (int j = 0; j < 4; ++j) dg[5] += k + j * 64 < ee ? min<int64_t>(64, ee - k - j * 64) : 0;
+                        for (int j = 0; j < kLong; ++j) dg[5] += k + j * 64 < ee ? min<int64_t>(64, ee - k - j * 64) : 0;
                 }
-                if ((a & want) == want) break;
+                if ((a & wsrc) == wsrc) break;
             }
             if (lane() == src) {
                 acc = a;
-                if (kDiag) { ++dg[6]; if ((a & want) == want) ++dg[7]; }
+                if (kDiag) { ++dg[6]; if ((a & wsrc) == wsrc) ++dg[7]; }
             }
         }
+        if (cand && open && v < n_active) acc |= cand[v];
         const uint64_t fresh = acc & open;
         if (v < n_active) {
             nx[v] = fresh;
@@ -202,6 +209,34 @@ __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t 
     count_flush(cnt, nv, mf, bits);
 }
 
+// Per-source frontier sizes of a pull level (vertices whose mask holds the source's bit):
+// one wave per 64-vertex word, one coalesced mask load, then 64 ballots — lane b keeps the
+// count of bit b.  Pure ALU after the load; one atomicAdd per lane and block.
+__global__ void __launch_bounds__(kBlock) ms_source_counts(const uint64_t* __restrict__ fr, int64_t n_active,
+                                                           unsigned long long* __restrict__ out) {
+    __shared__ unsigned long long s_sum[kWavesPerBlock][64];
+    const int64_t words = (n_active + 63) >> 6;
+    unsigned long long sum = 0;
+    for (int64_t wd = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6; wd < words;
+         wd += (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6) {
+        const int64_t v = (wd << 6) + lane();
+        const uint64_t mine = v < n_active ? fr[v] : 0;
+        if (!__ballot(mine != 0)) continue;                      // wave-uniform
+#pragma unroll 8
+        for (int b = 0; b < 64; ++b) {
+            const unsigned long long c = __popcll(__ballot((mine >> b) & 1ULL));
+            if (lane() == b) sum += c;
+        }
+    }
+    s_sum[threadIdx.x >> 6][lane()] = sum;
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        unsigned long long t = 0;
+        for (int w = 0; w < kWavesPerBlock; ++w) t += s_sum[w][threadIdx.x];
+        if (t) atomicAdd(&out[threadIdx.x], t);
+    }
+}
+
 // Frontier bitmap of a pull level: one wave per 64-vertex word, a ballot of fr != 0.
 __global__ void __launch_bounds__(kBlock) ms_fbitmap(const uint64_t* __restrict__ fr, int64_t n,
                                                      uint64_t* __restrict__ fbm) {
@@ -217,7 +252,7 @@ __global__ void __launch_bounds__(kBlock) ms_fbitmap(const uint64_t* __restrict_
 // Push level: edge-balanced over the frontier queue (exclusive scan of degrees in qpre).
 __global__ void __launch_bounds__(kBlock) ms_push(View push, const int32_t* __restrict__ q,
         const int64_t* __restrict__ qpre, int64_t qlen, const uint64_t* __restrict__ fr,
-        const uint64_t* __restrict__ vis, uint64_t* __restrict__ nx, PackTouch touch) {
+        const uint64_t* __restrict__ vis, uint64_t* __restrict__ nx, PackTouch touch, uint64_t mask) {
     // staged (for_each_queue_tile): all of a thread's list reads, then all target reads, then
     // the atomics — each stage's loads in flight together
     for_each_queue_tile(q, qpre, qlen, [&](const int32_t* u, const int64_t* o, const bool* valid) {
@@ -229,7 +264,7 @@ __global__ void __launch_bounds__(kBlock) ms_push(View push, const int32_t* __re
             m[k] = 0;
             if (!valid[k]) continue;
             v[k] = view_entry(push, u[k], o[k]);
-            m[k] = fr[u[k]];
+            m[k] = fr[u[k]] & mask;
         }
         uint64_t seen[kEdgesPerThread], have[kEdgesPerThread];
 #pragma unroll
@@ -281,11 +316,11 @@ __global__ void __launch_bounds__(kBlock) ms_settle(View push, int64_t n_active,
 // The queue of a frontier produced by a pull level (which only counts): every active v with
 // fr[v] != 0, push degrees for the scan.  Built only when the next level pushes.
 __global__ void __launch_bounds__(kBlock) ms_queue(View push, int64_t n_active, const uint64_t* __restrict__ fr,
-        int32_t* __restrict__ qn, int64_t* __restrict__ qdeg, Counters* cnt) {
+        int32_t* __restrict__ qn, int64_t* __restrict__ qdeg, Counters* cnt, uint64_t mask) {
     const int64_t words = (n_active + 63) >> 6;
     auto probe = [&](int64_t wd, Take* t, bool) -> bool {
         const int64_t v = (wd << 6) + lane();
-        const bool take = v < n_active && fr[v] != 0;
+        const bool take = v < n_active && (fr[v] & mask) != 0;
         t[0] = {take, static_cast<int32_t>(v), take ? push_degree(push, v) : 0};
         return __ballot(take) != 0;
     };
@@ -459,22 +494,27 @@ hipError_t k_ms_seed(const int64_t* seeds, int nseeds, uint64_t* vis, uint64_t* 
 }
 hipError_t k_ms_pull(const View& pull, const View& push, int64_t n_active, uint64_t full, const uint64_t* fr,
                      const uint64_t* fbm, uint64_t* vis, uint64_t* nx, LevelPlanes lvl, Counters* cnt,
-                     int32_t next_level, hipStream_t s, int32_t filter_from) {
+                     int32_t next_level, hipStream_t s, int32_t filter_from, uint64_t dense, const uint64_t* cand) {
     // TGO_MS_STEP: entries a lane loads per round trip of its own list (8 default; 16 probe)
     static const int step = [] { const char* e = std::getenv("TGO_MS_STEP"); return e ? std::atoi(e) : 8; }();
     static const bool diag = [] { const char* e = std::getenv("TGO_MS_DIAG"); return e && std::atoi(e) != 0; }();
-    if (diag)
+    // TGO_MS_LONG: entries per lane per trip of a long list (4 default; 8 probe)
+    static const int lng = [] { const char* e = std::getenv("TGO_MS_LONG"); return e ? std::atoi(e) : 4; }();
+    if (!diag && step == 8 && lng == 8)
+        ms_pull<8, false, 8><<<grid_for(n_active, 8192), kBlock, 0, s>>>(pull, push, n_active, full, fr, fbm, vis, nx, lvl,
+                                                                         cnt, next_level, filter_from, dense, cand);
+    else if (diag)
         ms_pull<8, true><<<grid_for(n_active, 8192), kBlock, 0, s>>>(pull, push, n_active, full, fr, fbm, vis, nx, lvl, cnt,
-                                                                   next_level, filter_from);
+                                                                   next_level, filter_from, dense, cand);
     else if (step == 16)
         ms_pull<16><<<grid_for(n_active, 8192), kBlock, 0, s>>>(pull, push, n_active, full, fr, fbm, vis, nx, lvl, cnt,
-                                                               next_level, filter_from);
+                                                               next_level, filter_from, dense, cand);
     else if (step == 4)
         ms_pull<4><<<grid_for(n_active, 8192), kBlock, 0, s>>>(pull, push, n_active, full, fr, fbm, vis, nx, lvl, cnt,
-                                                              next_level, filter_from);
+                                                              next_level, filter_from, dense, cand);
     else
         ms_pull<8><<<grid_for(n_active, 8192), kBlock, 0, s>>>(pull, push, n_active, full, fr, fbm, vis, nx, lvl, cnt,
-                                                              next_level, filter_from);
+                                                              next_level, filter_from, dense, cand);
     return hipGetLastError();
 }
 // The pull diagnostics since the last call (zeroed after the read).
@@ -487,19 +527,25 @@ hipError_t k_ms_diag_take(unsigned long long* out5, hipStream_t s) {  // 8 words
     if (e != hipSuccess) return e;
     return hipStreamSynchronize(s);
 }
+hipError_t k_ms_source_counts(const uint64_t* fr, int64_t n_active, unsigned long long* out64, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(out64, 0, 64 * sizeof(unsigned long long), s);
+    if (e != hipSuccess) return e;
+    ms_source_counts<<<grid_for(n_active, 4096), kBlock, 0, s>>>(fr, n_active, out64);
+    return hipGetLastError();
+}
 hipError_t k_ms_fbitmap(const uint64_t* fr, int64_t n, uint64_t* fbm, hipStream_t s) {
     const int64_t words = (n + 63) / 64;
     ms_fbitmap<<<grid_for(words * 64, 8192), kBlock, 0, s>>>(fr, n, fbm);
     return hipGetLastError();
 }
 hipError_t k_ms_queue(const View& push, int64_t n_active, const uint64_t* fr, int32_t* qn, int64_t* qdeg, Counters* cnt,
-                      hipStream_t s) {
-    ms_queue<<<extract_grid((n_active + 63) / 64), kBlock, 0, s>>>(push, n_active, fr, qn, qdeg, cnt);
+                      hipStream_t s, uint64_t mask) {
+    ms_queue<<<extract_grid((n_active + 63) / 64), kBlock, 0, s>>>(push, n_active, fr, qn, qdeg, cnt, mask);
     return hipGetLastError();
 }
 hipError_t k_ms_push(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen, const uint64_t* fr,
-                     const uint64_t* vis, uint64_t* nx, hipStream_t s, PackTouch touch) {
-    ms_push<<<256 * 8, kBlock, 0, s>>>(push, q, qpre, qlen, fr, vis, nx, touch);
+                     const uint64_t* vis, uint64_t* nx, hipStream_t s, PackTouch touch, uint64_t mask) {
+    ms_push<<<256 * 8, kBlock, 0, s>>>(push, q, qpre, qlen, fr, vis, nx, touch, mask);
     return hipGetLastError();
 }
 hipError_t k_ms_settle(const View& push, int64_t n_active, uint64_t* vis, uint64_t* nx, LevelPlanes lvl, int32_t* qn,
