@@ -5,6 +5,7 @@
 // each iteration is one or two kernel launches over the device-resident adjacency, and
 // only the frontier is touched for BFS/SSSP.
 #include <algorithm>
+#include <numeric>
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -1240,7 +1241,7 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
     const bool filter = filter_from >= 0 && filter_from < n;
     // TGO_MS_SPLIT: push budget of the pull levels' sparse sources, as a fraction of the
     // list entries (0 = every source pulled)
-    static const double split_frac = env_double("TGO_MS_SPLIT", 0.002);
+    static const double split_frac = env_double("TGO_MS_SPLIT", 0.005);
     int64_t qlen = static_cast<int64_t>(uniq.size());
     int64_t mf = 0;
     {
@@ -1267,10 +1268,10 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
             // Split the sources: the pull's walk of a vertex stops once every open source is
             // covered, and one source whose frontier never reaches the vertex (a source far
             // from it, or one whose sweep is over) makes every walk scan its whole list.  The
-            // sources with the smallest frontiers (their push entries estimated as frontier
-            // size x the frontier's mean degree, within a budget of split_frac of the list
-            // entries, plus every source with an empty frontier) are pushed into candidate
-            // masks instead, and the pull covers only the rest.
+            // sources with the smallest frontiers (frontier sizes by ballots, then the exact
+            // push entries of the few smallest, within a budget of split_frac of the list
+            // entries; every source with an empty frontier) are pushed into candidate masks
+            // instead, and the pull covers only the rest.
             uint64_t sparse = 0;
             if (split_frac > 0.0) {
                 HIP_TRY(k_ms_source_counts(fr, g.n_active, s.ms_srcent, st));
@@ -1280,15 +1281,32 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
                 int order[TGO_MAX_SOURCES];
                 for (int r = 0; r < nseeds; ++r) order[r] = r;
                 std::sort(order, order + nseeds, [&](int a, int b) { return se[a] < se[b]; });
-                const double budget = split_frac * static_cast<double>(total);
-                const double mean_deg = qlen > 0 ? static_cast<double>(mf) / static_cast<double>(qlen) : 0.0;
-                double used = 0.0;
-                for (int i = 0; i < nseeds; ++i) {
+                // candidates: the sources with the smallest frontiers (at most 16, each under
+                // 1/16 of the mean frontier); empty frontiers are free
+                const double mean_cnt = static_cast<double>(std::accumulate(se, se + nseeds, 0ULL)) / nseeds;
+                uint64_t cand = 0;
+                for (int i = 0, k = 0; i < nseeds && k < 16; ++i) {
                     const int r = order[i];
-                    const double cost = static_cast<double>(se[r]) * mean_deg;
-                    if (se[r] > 0 && used + cost > budget) break;
-                    used += cost;
-                    sparse |= 1ULL << r;
+                    if (se[r] == 0) { sparse |= 1ULL << r; continue; }
+                    if (static_cast<double>(se[r]) * 16.0 > mean_cnt) break;
+                    cand |= 1ULL << r;
+                    ++k;
+                }
+                double used = 0.0;
+                if (cand) {                              // their exact push entries, then the budget
+                    HIP_TRY(k_ms_source_entries(push, fr, g.n_active, cand, s.ms_srcent, st));
+                    HIP_TRY(hipMemcpyAsync(se, s.ms_srcent, sizeof(se), hipMemcpyDeviceToHost, st));
+                    HIP_TRY(hipStreamSynchronize(st));
+                    const double budget = split_frac * static_cast<double>(total);
+                    int co[TGO_MAX_SOURCES], nc = 0;
+                    for (int r = 0; r < nseeds; ++r)
+                        if ((cand >> r) & 1ULL) co[nc++] = r;
+                    std::sort(co, co + nc, [&](int a, int b) { return se[a] < se[b]; });
+                    for (int i = 0; i < nc; ++i) {
+                        if (used + static_cast<double>(se[co[i]]) > budget) break;
+                        used += static_cast<double>(se[co[i]]);
+                        sparse |= 1ULL << co[i];
+                    }
                 }
                 if (sparse == full) sparse = 0;            // nothing left to pull: plain pull
                 if (sparse) {
@@ -1306,7 +1324,7 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
                             HIP_TRY(k_ms_push(push, s.q[cur ^ 1], s.qpre, sq, fr, s.ms_vis, nx, st, PackTouch{}, sparse));
                         }
                     }
-                    if (trace) std::fprintf(stderr, "[tgo] ms level %d split: %d sparse sources, ~%.0f push entries\n", L,
+                    if (trace) std::fprintf(stderr, "[tgo] ms level %d split: %d sparse sources, %.0f push entries\n", L,
                                             __builtin_popcountll(sparse), used);
                 }
             }

@@ -525,6 +525,9 @@ hipError_t k_ms_pull(const View& pull, const View& push, int64_t n_active, uint6
                      const uint64_t* cand = nullptr);
 // per-source frontier sizes of fr (out64[s], zeroed first) — the pull level's split
 hipError_t k_ms_source_counts(const uint64_t* fr, int64_t n_active, unsigned long long* out64, hipStream_t s);
+// exact push entries of the frontiers of the sources in `cand` (out64[s], zeroed first)
+hipError_t k_ms_source_entries(const View& push, const uint64_t* fr, int64_t n_active, uint64_t cand,
+                               unsigned long long* out64, hipStream_t s);
 hipError_t k_ms_fbitmap(const uint64_t* fr, int64_t n, uint64_t* fbm, hipStream_t s);
 hipError_t k_ms_queue(const View& push, int64_t n_active, const uint64_t* fr, int32_t* qn, int64_t* qdeg, Counters* cnt,
                       hipStream_t s, uint64_t mask = ~0ULL);

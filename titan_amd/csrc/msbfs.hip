@@ -210,22 +210,68 @@ __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t 
 }
 
 // Per-source frontier sizes of a pull level (vertices whose mask holds the source's bit):
-// one wave per 64-vertex word, one coalesced mask load, then 64 ballots — lane b keeps the
-// count of bit b.  Pure ALU after the load; one atomicAdd per lane and block.
+// one wave per 64-vertex word, one coalesced mask load, then a 64 x 64 bit transpose across
+// the lanes (6 shuffle stages swapping off-diagonal blocks) so lane b holds source b's column
+// and adds its popcount.  One atomicAdd per lane and block.
 __global__ void __launch_bounds__(kBlock) ms_source_counts(const uint64_t* __restrict__ fr, int64_t n_active,
                                                            unsigned long long* __restrict__ out) {
+    __shared__ unsigned long long s_sum[kWavesPerBlock][64];
+    const int64_t words = (n_active + 63) >> 6;
+    unsigned long long sum = 0;
+    const int64_t nw = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
+    for (int64_t w0 = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6; w0 < words; w0 += 4 * nw) {
+      uint64_t mw[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {                              // four words' loads in flight
+          const int64_t v = ((w0 + u * nw) << 6) + lane();
+          mw[u] = (w0 + u * nw < words && v < n_active) ? fr[v] : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint64_t mine = mw[u];
+        if (!__ballot(mine != 0)) continue;                      // wave-uniform
+        uint64_t x = mine;
+        constexpr uint64_t kLow[6] = {0x00000000FFFFFFFFULL, 0x0000FFFF0000FFFFULL, 0x00FF00FF00FF00FFULL,
+                                      0x0F0F0F0F0F0F0F0FULL, 0x3333333333333333ULL, 0x5555555555555555ULL};
+#pragma unroll
+        for (int st = 0; st < 6; ++st) {
+            const int j = 32 >> st;
+            const uint64_t m = kLow[st];
+            const uint64_t y = __shfl_xor(x, j, 64);
+            x = (lane() & j) ? (((y & ~m) >> j) | (x & ~m)) : ((x & m) | ((y & m) << j));
+        }
+        sum += static_cast<unsigned long long>(__popcll(x));
+      }
+    }
+    s_sum[threadIdx.x >> 6][lane()] = sum;
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        unsigned long long t = 0;
+        for (int w = 0; w < kWavesPerBlock; ++w) t += s_sum[w][threadIdx.x];
+        if (t) atomicAdd(&out[threadIdx.x], t);
+    }
+}
+
+// Exact push entries of the candidate sources `cand` (their frontiers are small): only words
+// holding a candidate bit load degrees; lane b keeps the entries of source b.
+__global__ void __launch_bounds__(kBlock) ms_source_entries(View push, const uint64_t* __restrict__ fr,
+        int64_t n_active, uint64_t cand, unsigned long long* __restrict__ out) {
     __shared__ unsigned long long s_sum[kWavesPerBlock][64];
     const int64_t words = (n_active + 63) >> 6;
     unsigned long long sum = 0;
     for (int64_t wd = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6; wd < words;
          wd += (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6) {
         const int64_t v = (wd << 6) + lane();
-        const uint64_t mine = v < n_active ? fr[v] : 0;
+        const uint64_t mine = v < n_active ? (fr[v] & cand) : 0;
         if (!__ballot(mine != 0)) continue;                      // wave-uniform
-#pragma unroll 8
-        for (int b = 0; b < 64; ++b) {
-            const unsigned long long c = __popcll(__ballot((mine >> b) & 1ULL));
-            if (lane() == b) sum += c;
+        const unsigned long long deg = mine ? static_cast<unsigned long long>(push_degree(push, v)) : 0ULL;
+        uint64_t bits = cand;
+        while (bits) {
+            const int b = __ffsll(static_cast<long long>(bits)) - 1;
+            bits &= bits - 1;
+            unsigned long long t = ((mine >> b) & 1ULL) ? deg : 0ULL;
+            for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+            if (lane() == b) sum += t;
         }
     }
     s_sum[threadIdx.x >> 6][lane()] = sum;
@@ -530,7 +576,16 @@ hipError_t k_ms_diag_take(unsigned long long* out5, hipStream_t s) {  // 8 words
 hipError_t k_ms_source_counts(const uint64_t* fr, int64_t n_active, unsigned long long* out64, hipStream_t s) {
     hipError_t e = hipMemsetAsync(out64, 0, 64 * sizeof(unsigned long long), s);
     if (e != hipSuccess) return e;
-    ms_source_counts<<<grid_for(n_active, 4096), kBlock, 0, s>>>(fr, n_active, out64);
+    // few blocks: each block ends in 64 atomics on the same 64 words (4096 blocks spent
+    // ~50 us queueing on them)
+    ms_source_counts<<<grid_for(n_active, 512), kBlock, 0, s>>>(fr, n_active, out64);
+    return hipGetLastError();
+}
+hipError_t k_ms_source_entries(const View& push, const uint64_t* fr, int64_t n_active, uint64_t cand,
+                               unsigned long long* out64, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(out64, 0, 64 * sizeof(unsigned long long), s);
+    if (e != hipSuccess) return e;
+    ms_source_entries<<<grid_for(n_active, 512), kBlock, 0, s>>>(push, fr, n_active, cand, out64);
     return hipGetLastError();
 }
 hipError_t k_ms_fbitmap(const uint64_t* fr, int64_t n, uint64_t* fbm, hipStream_t s) {
