@@ -1255,6 +1255,7 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
     uint64_t* nx = s.ms_nx;
     int cur = 0, levels = 0;
     bool queued = true;         // q[cur] holds the frontier (pull levels only count it)
+    bool pulled = false;        // the previous level pulled
     for (int L = 0; L < depth && qlen > 0; ++L) {
         const bool use_pull = static_cast<double>(mf) * ms_alpha > static_cast<double>(total);
         if ((rc = ms_planes_for(ctx, L + 1))) return rc;
@@ -1264,6 +1265,8 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
         }
         HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
         queued = !use_pull;
+        const bool prev_pull = pulled;
+        pulled = use_pull;
         if (use_pull) {
             // Split the sources: the pull's walk of a vertex stops once every open source is
             // covered, and one source whose frontier never reaches the vertex (a source far
@@ -1272,8 +1275,10 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
             // push entries of the few smallest, within a budget of split_frac of the list
             // entries; every source with an empty frontier) are pushed into candidate masks
             // instead, and the pull covers only the rest.
+            // (tried at the first pull level of a run of pull levels, where the frontiers
+            // are most unequal; later pull levels found nothing to split on RMAT-24)
             uint64_t sparse = 0;
-            if (split_frac > 0.0) {
+            if (split_frac > 0.0 && !prev_pull) {
                 HIP_TRY(k_ms_source_counts(fr, g.n_active, s.ms_srcent, st));
                 unsigned long long se[TGO_MAX_SOURCES];
                 HIP_TRY(hipMemcpyAsync(se, s.ms_srcent, sizeof(se), hipMemcpyDeviceToHost, st));
