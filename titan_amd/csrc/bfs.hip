@@ -47,38 +47,25 @@ __global__ void __launch_bounds__(kBlock) td_expand(View push, const int32_t* __
         int64_t* __restrict__ qdeg_n, Counters* cnt, int32_t next_level) {
     __shared__ AppendLds sh;
     unsigned long long mf = 0;
-    // staged (for_each_queue_tile): list reads, visited words, claims, one append per tile
-    for_each_queue_tile(q, qpre, qlen, [&](const int32_t* u, const int64_t* o, const bool* valid) {
-        int32_t v[kEdgesPerThread];
-#pragma unroll
-        for (int k = 0; k < kEdgesPerThread; ++k) {
-            v[k] = -1;
-            if (!valid[k]) continue;
+    for_each_queue_edge(q, qpre, qlen, [&](bool valid, int32_t u, int64_t o) {
+        bool take = false;
+        int32_t v = 0;
+        int64_t vdeg = 0;
+        if (valid) {
             int32_t w;
-            entry_at(push, u[k], o[k], v[k], w);
+            entry_at(push, u, o, v, w);
+            const uint64_t bit = 1ULL << (v & 63);
+            if (!(vb[v >> 6] & bit)) {
+                const unsigned long long old = atomicOr(reinterpret_cast<unsigned long long*>(&vb[v >> 6]), bit);
+                if (!(old & bit)) {
+                    take = true;
+                    level[v] = next_level;
+                    atomicOr(reinterpret_cast<unsigned long long*>(&nb[v >> 6]), bit);
+                    vdeg = push_degree(push, v);
+                }
+            }
         }
-        uint64_t word[kEdgesPerThread];
-#pragma unroll
-        for (int k = 0; k < kEdgesPerThread; ++k) word[k] = v[k] >= 0 ? vb[v[k] >> 6] : ~0ULL;
-        int32_t tv[kEdgesPerThread];
-        int64_t td[kEdgesPerThread];
-#pragma unroll
-        for (int k = 0; k < kEdgesPerThread; ++k) {
-            tv[k] = -1;
-            td[k] = 0;
-            if (v[k] < 0) continue;
-            const uint64_t bit = 1ULL << (v[k] & 63);
-            if (word[k] & bit) continue;
-            const unsigned long long old = atomicOr(reinterpret_cast<unsigned long long*>(&vb[v[k] >> 6]), bit);
-            if (old & bit) continue;
-            tv[k] = v[k];
-            level[v[k]] = next_level;
-            atomicOr(reinterpret_cast<unsigned long long*>(&nb[v[k] >> 6]), bit);
-        }
-#pragma unroll
-        for (int k = 0; k < kEdgesPerThread; ++k)
-            if (tv[k] >= 0) td[k] = push_degree(push, tv[k]);
-        tile_append(tv, td, qn, qdeg_n, cnt, mf);
+        block_append(take, v, vdeg, qn, qdeg_n, cnt, sh, mf);
     });
     block_flush(cnt, sh, mf);
 }

@@ -98,102 +98,6 @@ __device__ __forceinline__ void for_each_queue_edge(const int32_t* __restrict__ 
     }
 }
 
-// Tile form of for_each_queue_edge: body(entry, offset, valid) once per tile with this
-// thread's kEdgesPerThread edges (edge j = t0 + k * kBlock + threadIdx.x), so the body can
-// issue each stage's loads (lists, then targets, then atomics) for all of them together
-// instead of one dependent chain per edge.  Block-uniform calls (the body may synchronise).
-template <class Body>
-__device__ __forceinline__ void for_each_queue_tile(const int32_t* __restrict__ q, const int64_t* __restrict__ qpre,
-                                                    int64_t qlen, Body&& body) {
-    __shared__ int64_t s_pre[kLdsEntries];
-    __shared__ int32_t s_q[kLdsEntries];
-    __shared__ int64_t s_lo, s_hi;
-    const int64_t total = qpre[qlen];
-    const int64_t ntiles = (total + kTileEdges - 1) / kTileEdges;
-    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const int64_t t0 = tile * kTileEdges;
-        const int64_t t1 = min(total, t0 + kTileEdges);
-        if (threadIdx.x == 0) {
-            int64_t a = 0, b = qlen;
-            while (b - a > 1) { const int64_t c = (a + b) >> 1; if (qpre[c] <= t0) a = c; else b = c; }
-            s_lo = a;
-            int64_t a2 = a, b2 = qlen;
-            while (b2 - a2 > 1) { const int64_t c = (a2 + b2) >> 1; if (qpre[c] <= t1 - 1) a2 = c; else b2 = c; }
-            s_hi = a2;
-        }
-        __syncthreads();
-        const int64_t lo = s_lo, hi = s_hi;
-        const int64_t span = hi - lo + 1;
-        const bool in_lds = span + 1 <= kLdsEntries;
-        if (in_lds) {
-            for (int64_t i = threadIdx.x; i <= span; i += kBlock) {
-                s_pre[i] = qpre[lo + i];
-                if (i < span) s_q[i] = q[lo + i];
-            }
-        }
-        __syncthreads();
-        int32_t entry[kEdgesPerThread];
-        int64_t off[kEdgesPerThread];
-        bool valid[kEdgesPerThread];
-#pragma unroll
-        for (int k = 0; k < kEdgesPerThread; ++k) {
-            const int64_t j = t0 + k * kBlock + threadIdx.x;
-            valid[k] = j < t1;
-            entry[k] = 0;
-            off[k] = 0;
-            if (!valid[k]) continue;
-            int64_t start;
-            if (in_lds) {
-                int64_t a = 0, b = span;
-                while (b - a > 1) { const int64_t c = (a + b) >> 1; if (s_pre[c] <= j) a = c; else b = c; }
-                entry[k] = s_q[a]; start = s_pre[a];
-            } else {
-                int64_t a = lo, b = hi + 1;
-                while (b - a > 1) { const int64_t c = (a + b) >> 1; if (qpre[c] <= j) a = c; else b = c; }
-                entry[k] = q[a]; start = qpre[a];
-            }
-            off[k] = j - start;
-        }
-        body(entry, off, valid);
-        __syncthreads();
-    }
-}
-
-// Tile-aggregated append: every thread's takes of a tile (tv[k] >= 0, degree td[k]) with
-// one atomicAdd per block on cnt->qlen; the degrees stay in mf until block_flush.
-// Block-uniform call.
-__device__ __forceinline__ void tile_append(const int32_t* tv, const int64_t* td, int32_t* qn, int64_t* qdeg,
-                                            Counters* cnt, unsigned long long& mf) {
-    __shared__ unsigned long long s_off[kWavesPerBlock], s_base;
-    int mine = 0;
-    int64_t dsum = 0;
-#pragma unroll
-    for (int k = 0; k < kEdgesPerThread; ++k)
-        if (tv[k] >= 0) { ++mine; dsum += td[k]; }
-    int incl = mine;                                   // inclusive scan over the wave
-    for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(incl, o, 64);
-        if (lane() >= o) incl += y;
-    }
-    for (int o = 32; o > 0; o >>= 1) dsum += __shfl_xor(dsum, o, 64);
-    mf += static_cast<unsigned long long>(dsum);
-    const int wave = threadIdx.x >> 6;
-    if (lane() == 63) s_off[wave] = static_cast<unsigned long long>(incl);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long t = 0;
-        for (int w = 0; w < kWavesPerBlock; ++w) { const unsigned long long c = s_off[w]; s_off[w] = t; t += c; }
-        s_base = t ? atomicAdd(&cnt->qlen, t) : 0ULL;
-    }
-    __syncthreads();
-    if (mine) {
-        unsigned long long slot = s_base + s_off[wave] + static_cast<unsigned long long>(incl - mine);
-#pragma unroll
-        for (int k = 0; k < kEdgesPerThread; ++k)
-            if (tv[k] >= 0) { qn[slot] = tv[k]; qdeg[slot] = td[k]; ++slot; }
-    }
-}
-
 // Block-aggregated append (all threads of the block call it in the same trip): the block
 // reserves its queue slots with ONE atomicAdd on cnt->qlen; the appended degrees stay in
 // registers (mf) until block_flush.  A single contended counter word serves ~88 atomics/us

@@ -299,36 +299,14 @@ __global__ void __launch_bounds__(kBlock) ms_fbitmap(const uint64_t* __restrict_
 __global__ void __launch_bounds__(kBlock) ms_push(View push, const int32_t* __restrict__ q,
         const int64_t* __restrict__ qpre, int64_t qlen, const uint64_t* __restrict__ fr,
         const uint64_t* __restrict__ vis, uint64_t* __restrict__ nx, PackTouch touch, uint64_t mask) {
-    // staged (for_each_queue_tile): all of a thread's list reads, then all target reads, then
-    // the atomics — each stage's loads in flight together
-    for_each_queue_tile(q, qpre, qlen, [&](const int32_t* u, const int64_t* o, const bool* valid) {
-        int32_t v[kEdgesPerThread];
-        uint64_t m[kEdgesPerThread];
-#pragma unroll
-        for (int k = 0; k < kEdgesPerThread; ++k) {
-            v[k] = 0;
-            m[k] = 0;
-            if (!valid[k]) continue;
-            v[k] = view_entry(push, u[k], o[k]);
-            m[k] = fr[u[k]] & mask;
-        }
-        uint64_t seen[kEdgesPerThread], have[kEdgesPerThread];
-#pragma unroll
-        for (int k = 0; k < kEdgesPerThread; ++k) {
-            seen[k] = 0;
-            have[k] = 0;
-            if (!m[k]) continue;
-            // partitioned graphs pass vis = nullptr: remote vertices' masks are not local
-            if (vis) seen[k] = vis[v[k]];
-            have[k] = nx[v[k]];
-        }
-#pragma unroll
-        for (int k = 0; k < kEdgesPerThread; ++k) {
-            const uint64_t mk = m[k] & ~seen[k];
-            if (mk && (have[k] & mk) != mk) {
-                atomicOr(reinterpret_cast<unsigned long long*>(&nx[v[k]]), mk);
-                if (touch.flag) touch.flag[(v[k] / touch.n_local) * touch.cps + (v[k] % touch.n_local) / kPackChunk] = 1;
-            }
+    for_each_queue_edge(q, qpre, qlen, [&](bool valid, int32_t u, int64_t o) {
+        if (!valid) return;
+        const int32_t v = view_entry(push, u, o);
+        // partitioned graphs pass vis = nullptr: remote vertices' masks are not local
+        const uint64_t m = (vis ? (fr[u] & ~vis[v]) : fr[u]) & mask;
+        if (m && (nx[v] & m) != m) {
+            atomicOr(reinterpret_cast<unsigned long long*>(&nx[v]), m);
+            if (touch.flag) touch.flag[(v / touch.n_local) * touch.cps + (v % touch.n_local) / kPackChunk] = 1;
         }
     });
 }
