@@ -100,6 +100,26 @@ int tgo_part_ms_settle_pairs(tgo_ctx* ctx, int32_t level, const int64_t* recv, c
 int tgo_part_ms_pack_fixed(tgo_ctx* ctx, uint64_t* cand_global, int32_t nranks, int64_t cap, int64_t* send);
 int tgo_part_ms_settle_fixed(tgo_ctx* ctx, int32_t level, const int64_t* recv, int32_t nslices, int64_t cap,
                              uint64_t* fr_next, int64_t* counts);
+/* Source split of a dense level (tgo_bfs_multi's split, partitioned; tgo_part_msbfs_run does
+ * it at the first dense level of a run of dense levels): a pull walk stops once every open
+ * source is covered, and a source whose frontier barely reaches the vertex makes every walk
+ * scan its whole list, so the sources with the smallest frontiers are pushed instead.
+ *   tgo_part_ms_source_counts / _entries: this rank's per-source frontier sizes / exact push
+ *     entries of the candidate sources `cand` into DEVICE int64[64] (the caller all-reduces);
+ *   tgo_part_ms_push_masked: the `mask` sources' frontiers into cand_global (then the caller's
+ *     pack + exchange, as at a sparse level, with cap = their global push entries);
+ *   tgo_part_ms_or_fixed / _or_pairs: the received pairs OR-ed into fr_next (zeroed first),
+ *     without settling;
+ *   tgo_part_ms_pull_split: the pull for the sources outside `sparse`, OR-ing in the
+ *     candidates already in fr_next when cand_in_next != 0.  Same traversal as the plain pull. */
+int tgo_part_ms_source_counts(tgo_ctx* ctx, const uint64_t* fr_local, int64_t* counts_dev);
+int tgo_part_ms_source_entries(tgo_ctx* ctx, const uint64_t* fr_local, uint64_t cand, int64_t* entries_dev);
+int tgo_part_ms_push_masked(tgo_ctx* ctx, const uint64_t* fr_local, uint64_t* cand_global, uint64_t mask);
+int tgo_part_ms_or_fixed(tgo_ctx* ctx, const int64_t* recv, int32_t nslices, int64_t cap, uint64_t* fr_next);
+int tgo_part_ms_or_pairs(tgo_ctx* ctx, const int64_t* recv, const int64_t* recv_counts, int32_t nslices,
+                         uint64_t* fr_next);
+int tgo_part_ms_pull_split(tgo_ctx* ctx, int32_t level, const uint64_t* fr_global, uint64_t* fr_next, uint64_t sparse,
+                           int32_t cand_in_next, int64_t* counts);
 /* reached / entries: per seed, over this rank's vertices (NULL to skip). */
 int tgo_part_ms_end(tgo_ctx* ctx, int64_t* reached, int64_t* entries);
 /* Source `source`'s distances of the owned vertices (TGO_DIST_ABSENT = unreached). */

@@ -148,6 +148,8 @@ EXPORTS = [
     "tgo_part_active_rows", "tgo_part_pr_blocked", "tgo_part_device_counts", "tgo_part_set_local_qlen", "tgo_part_ms_pack_dev", "tgo_part_pr_step_cold", "tgo_part_pr_step_hot",
     "tgo_part_ms_begin", "tgo_part_ms_pull", "tgo_part_ms_push", "tgo_part_ms_settle", "tgo_part_ms_end",
     "tgo_part_ms_pack", "tgo_part_ms_settle_pairs", "tgo_part_ms_pack_fixed", "tgo_part_ms_settle_fixed",
+    "tgo_part_ms_source_counts", "tgo_part_ms_source_entries", "tgo_part_ms_push_masked", "tgo_part_ms_or_fixed",
+    "tgo_part_ms_or_pairs", "tgo_part_ms_pull_split",
     "tgo_part_ms_levels", "tgo_part_sssp_begin", "tgo_part_sssp_relax", "tgo_part_sssp_apply",
     "tgo_part_sssp_pending_min", "tgo_part_sssp_extract", "tgo_part_sssp_end",
     "tgo_exchange_rccl_id", "tgo_exchange_rccl_create", "tgo_exchange_local_group", "tgo_exchange_destroy",
@@ -241,6 +243,12 @@ def load() -> C.CDLL:
         "tgo_part_ms_pack_dev": (C.c_int, [vp, vp, C.c_int32, vp, vp]),
         "tgo_part_ms_pack_fixed": (C.c_int, [vp, vp, C.c_int32, C.c_int64, vp]),
         "tgo_part_ms_settle_fixed": (C.c_int, [vp, C.c_int32, vp, C.c_int32, C.c_int64, vp, _i64p]),
+        "tgo_part_ms_source_counts": (C.c_int, [vp, vp, vp]),
+        "tgo_part_ms_source_entries": (C.c_int, [vp, vp, C.c_uint64, vp]),
+        "tgo_part_ms_push_masked": (C.c_int, [vp, vp, vp, C.c_uint64]),
+        "tgo_part_ms_or_fixed": (C.c_int, [vp, vp, C.c_int32, C.c_int64, vp]),
+        "tgo_part_ms_or_pairs": (C.c_int, [vp, vp, _i64p, C.c_int32, vp]),
+        "tgo_part_ms_pull_split": (C.c_int, [vp, C.c_int32, vp, vp, C.c_uint64, C.c_int32, _i64p]),
         "tgo_part_pr_blocked": (C.c_int, [vp, C.c_int32, C.c_int64, _i64p]),
         "tgo_part_pr_step_cold": (C.c_int, [vp, vp]),
         "tgo_part_pr_step_hot": (C.c_int, [vp, vp, vp]),

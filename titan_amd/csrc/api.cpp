@@ -1890,6 +1890,95 @@ int tgo_part_ms_begin(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, uint64
     return TGO_OK;
 }
 
+// ---- source split of a dense level (tgo_bfs_multi's split, partitioned; titan_gpu_olap_part.h)
+int tgo_part_ms_source_counts(tgo_ctx* ctx, const uint64_t* fr_local, int64_t* counts_dev) {
+    int rc = part_check(ctx);
+    if (rc) return rc;
+    if (!fr_local || !counts_dev) return fail(ctx, TGO_E_INVALID, "null argument");
+    HIP_TRY(k_ms_source_counts(fr_local, ctx->g.n_active, reinterpret_cast<unsigned long long*>(counts_dev), ctx->stream));
+    return part_done(ctx);
+}
+
+int tgo_part_ms_source_entries(tgo_ctx* ctx, const uint64_t* fr_local, uint64_t cand, int64_t* entries_dev) {
+    int rc = part_check(ctx);
+    if (rc) return rc;
+    if (!fr_local || !entries_dev) return fail(ctx, TGO_E_INVALID, "null argument");
+    HIP_TRY(k_ms_source_entries(push_view(ctx->g, TGO_SCOPE_BOTH_E), fr_local, ctx->g.n_active, cand,
+                                reinterpret_cast<unsigned long long*>(entries_dev), ctx->stream));
+    return part_done(ctx);
+}
+
+// The sparse sources' frontiers pushed into cand_global: a masked queue of this rank's
+// frontier in the idle queue buffer (a dense level builds no queue), the pack's touch flags.
+int tgo_part_ms_push_masked(tgo_ctx* ctx, const uint64_t* fr_local, uint64_t* cand_global, uint64_t mask) {
+    int rc = part_check(ctx);
+    if (rc) return rc;
+    if (!fr_local || !cand_global) return fail(ctx, TGO_E_INVALID, "null argument");
+    DevGraph& g = ctx->g;
+    Scratch& s = ctx->sc;
+    hipStream_t st = ctx->stream;
+    const View push = push_view(g, TGO_SCOPE_BOTH_E);
+    int32_t* q = s.q[ctx->part_cur ^ 1];
+    HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
+    HIP_TRY(k_ms_queue(push, g.n_active, fr_local, q, s.qdeg, s.cnt, st, mask));
+    if ((rc = read_counters(ctx))) return rc;
+    const int64_t qlen = static_cast<int64_t>(s.hcnt->qlen);
+    if (qlen > 0) {
+        if ((rc = scan_frontier(ctx, qlen))) return rc;
+        const PackTouch touch{s.pk_touch, g.n, (g.n + kPackChunk - 1) / kPackChunk};
+        HIP_TRY(k_ms_push(push, q, s.qpre, qlen, fr_local, nullptr, cand_global, st, touch, mask));
+    }
+    return part_done(ctx);
+}
+
+// The received candidate pairs OR-ed into fr_next (zeroed first), no settle: the pull of the
+// same level reads them (tgo_part_ms_pull_split).
+int tgo_part_ms_or_fixed(tgo_ctx* ctx, const int64_t* recv, int32_t nslices, int64_t cap, uint64_t* fr_next) {
+    int rc = part_check(ctx);
+    if (rc) return rc;
+    if (!recv || !fr_next || nslices < 1 || nslices > kMaxRanks || cap < 1 || cap > ctx->g.n)
+        return fail(ctx, TGO_E_INVALID, "ms_or_fixed: bad arguments");
+    HIP_TRY(hipMemsetAsync(fr_next, 0, ctx->g.n_active * 8, ctx->stream));
+    HIP_TRY(k_ms_or_fixed(recv, nslices, cap, fr_next, ctx->stream));
+    return part_done(ctx);
+}
+
+int tgo_part_ms_or_pairs(tgo_ctx* ctx, const int64_t* recv, const int64_t* recv_counts, int32_t nslices,
+                         uint64_t* fr_next) {
+    int rc = part_check(ctx);
+    if (rc) return rc;
+    if (!recv || !recv_counts || !fr_next || nslices < 1 || nslices > kMaxRanks)
+        return fail(ctx, TGO_E_INVALID, "ms_or_pairs: bad arguments");
+    int64_t npairs = 0;
+    for (int r = 0; r < nslices; ++r) {
+        if (recv_counts[r] < 0 || recv_counts[r] > ctx->g.n) return fail(ctx, TGO_E_INVALID, "ms_or_pairs: bad count");
+        npairs += recv_counts[r];
+    }
+    HIP_TRY(hipMemsetAsync(fr_next, 0, ctx->g.n_active * 8, ctx->stream));
+    HIP_TRY(k_ms_or_pairs(recv, npairs, fr_next, ctx->stream));
+    return part_done(ctx);
+}
+
+int tgo_part_ms_pull_split(tgo_ctx* ctx, int32_t level, const uint64_t* fr_global, uint64_t* fr_next, uint64_t sparse,
+                           int32_t cand_in_next, int64_t* counts) {
+    int rc = part_check(ctx);
+    if (rc) return rc;
+    DevGraph& g = ctx->g;
+    Scratch& s = ctx->sc;
+    hipStream_t st = ctx->stream;
+    const View pull = pull_view(g, TGO_SCOPE_BOTH_E), push = push_view(g, TGO_SCOPE_BOTH_E);
+    const uint64_t full = s.ms_nsrc == 64 ? ~0ULL : ((1ULL << s.ms_nsrc) - 1ULL);
+    if (level + 1 >= (1 << kLevelPlanes)) return fail(ctx, TGO_E_UNSUPPORTED, "multi-source BFS levels are < 65536");
+    if ((rc = ms_planes_for(ctx, level + 1))) return rc;
+    HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
+    const int nxt = ctx->part_cur ^ 1;
+    HIP_TRY(k_ms_pull(pull, push, g.n_active, full, fr_global, nullptr, s.ms_vis, fr_next, ms_planes(ctx), s.cnt,
+                      level + 1, st, 0, full & ~sparse, cand_in_next ? fr_next : nullptr));
+    ctx->part_cur = nxt;
+    ctx->part_queued = false;
+    return part_counts(ctx, counts);
+}
+
 int tgo_part_ms_pull(tgo_ctx* ctx, int32_t level, const uint64_t* fr_global, uint64_t* fr_next, int64_t* counts) {
     int rc = part_check(ctx);
     if (rc) return rc;

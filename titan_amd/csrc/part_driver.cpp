@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -346,35 +347,99 @@ extern "C" int tgo_part_msbfs_run(tgo_ctx* ctx, tgo_exchange* x, const int64_t* 
     // level counts stay on the device: the steps publish {next queue, its entries, own queue}
     if ((rc = tgo_part_device_counts(ctx, dc))) return rc;
     int levels = 0;
+    // source split of the first dense level of a run (tgo_bfs_multi's rule; TGO_MS_SPLIT)
+    static const double split_frac = [] { const char* e = std::getenv("TGO_MS_SPLIT"); return e ? std::atof(e) : 0.005; }();
+    const uint64_t full = nseeds == 64 ? ~0ULL : ((1ULL << nseeds) - 1ULL);
+    int64_t* sc64 = dc + 3;                                 // 64 per-source sums (free during the sweep)
+    auto read64 = [&](int64_t* host) -> int {
+        if (int r = x->all_reduce_sum(sc64, 64, st)) return xfail(r);
+        if (hipMemcpyAsync(host, sc64, 64 * sizeof(int64_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            return part_fail(ctx, TGO_E_HIP, "per-source sums read");
+        return TGO_OK;
+    };
+    // pack + exchange the candidate masks of a push (fixed slots when cap bounds them), then
+    // hand the received pairs to `fixed_fn` / `pairs_fn`
+    auto exchange = [&](int64_t entries, auto&& fixed_fn, auto&& pairs_fn) -> int {
+        const int64_t cap = std::min<int64_t>(entries, nl);
+        if (cap > 0 && static_cast<int64_t>(W) * (cap + 1) * 16 <= fixed_bytes) {
+            if (int r = tgo_part_ms_pack_fixed(ctx, cand, W, cap, send)) return r;
+            if (int r = x->all_to_all(send, recv, static_cast<size_t>(cap + 1) * 16, st)) return xfail(r);
+            return fixed_fn(cap);
+        }
+        // sized pairs: split sizes on the device, one all-to-all of them, one host read
+        if (int r = tgo_part_ms_pack_dev(ctx, cand, W, send, sizes)) return r;
+        if (int r = x->all_to_all(sizes, sizes + W, 8, st)) return xfail(r);
+        std::vector<int64_t> both(2 * W);
+        if (hipMemcpyAsync(both.data(), sizes, 2 * W * sizeof(int64_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess) return part_fail(ctx, TGO_E_HIP, "split sizes read");
+        std::vector<size_t> sb(W), so(W), rb(W), ro(W);
+        std::vector<int64_t> rpairs(W);
+        size_t a = 0, b = 0;
+        for (int p = 0; p < W; ++p) {
+            sb[p] = static_cast<size_t>(both[p]) * 8; so[p] = a; a += sb[p];
+            rb[p] = static_cast<size_t>(both[W + p]) * 8; ro[p] = b; b += rb[p];
+            rpairs[p] = both[W + p] / 2;
+        }
+        if (int r = x->all_to_allv(send, sb.data(), so.data(), recv, rb.data(), ro.data(), st)) return xfail(r);
+        return pairs_fn(rpairs.data());
+    };
+    bool prev_dense = false;
     for (int level = 0; level < max_depth && nf > 0; ++level) {
-        if (static_cast<double>(mf) * ms_alpha > static_cast<double>(total)) {
+        const bool dense = static_cast<double>(mf) * ms_alpha > static_cast<double>(total);
+        const bool first_dense = dense && !prev_dense;
+        prev_dense = dense;
+        if (dense) {
+            uint64_t sparse = 0;
+            int32_t with_cand = 0;
+            if (first_dense && split_frac > 0.0) {
+                int64_t se[64];
+                if ((rc = tgo_part_ms_source_counts(ctx, fr, sc64)) || (rc = read64(se))) break;
+                int order[64];
+                for (int r = 0; r < nseeds; ++r) order[r] = r;
+                std::sort(order, order + nseeds, [&](int a, int b) { return se[a] < se[b]; });
+                double mean = 0.0;
+                for (int r = 0; r < nseeds; ++r) mean += static_cast<double>(se[r]);
+                mean /= nseeds;
+                uint64_t candm = 0;
+                for (int i = 0, k = 0; i < nseeds && k < 16; ++i) {
+                    const int r = order[i];
+                    if (se[r] == 0) { sparse |= 1ULL << r; continue; }
+                    if (static_cast<double>(se[r]) * 16.0 > mean) break;
+                    candm |= 1ULL << r;
+                    ++k;
+                }
+                int64_t used = 0;
+                if (candm) {
+                    if ((rc = tgo_part_ms_source_entries(ctx, fr, candm, sc64)) || (rc = read64(se))) break;
+                    int co[64], nc = 0;
+                    for (int r = 0; r < nseeds; ++r)
+                        if ((candm >> r) & 1ULL) co[nc++] = r;
+                    std::sort(co, co + nc, [&](int a, int b) { return se[a] < se[b]; });
+                    for (int i = 0; i < nc; ++i) {
+                        if (static_cast<double>(used + se[co[i]]) > split_frac * static_cast<double>(total)) break;
+                        used += se[co[i]];
+                        sparse |= 1ULL << co[i];
+                    }
+                }
+                if (sparse == full) sparse = 0;
+                if (sparse && used > 0) {               // push the sparse sources' frontiers
+                    if ((rc = tgo_part_ms_push_masked(ctx, fr, cand, sparse))) break;
+                    rc = exchange(used,
+                                  [&](int64_t cap) { return tgo_part_ms_or_fixed(ctx, recv, W, cap, frn); },
+                                  [&](const int64_t* rp) { return tgo_part_ms_or_pairs(ctx, recv, rp, W, frn); });
+                    if (rc) break;
+                    with_cand = 1;
+                }
+            }
             if (int r = x->all_gather(glob[0], static_cast<size_t>(nl) * 8, st)) { rc = xfail(r); break; }
-            if ((rc = tgo_part_ms_pull(ctx, level, glob[0], frn, nullptr))) break;
+            if ((rc = tgo_part_ms_pull_split(ctx, level, glob[0], frn, sparse, with_cand, nullptr))) break;
         } else {
             if ((rc = tgo_part_ms_push(ctx, level, fr, cand))) break;
-            const int64_t cap = std::min<int64_t>(mf, nl);
-            if (cap > 0 && static_cast<int64_t>(W) * (cap + 1) * 16 <= fixed_bytes) {
-                if ((rc = tgo_part_ms_pack_fixed(ctx, cand, W, cap, send))) break;
-                if (int r = x->all_to_all(send, recv, static_cast<size_t>(cap + 1) * 16, st)) { rc = xfail(r); break; }
-                if ((rc = tgo_part_ms_settle_fixed(ctx, level, recv, W, cap, frn, nullptr))) break;
-            } else {
-                // sized pairs: split sizes on the device, one all-to-all of them, one host read
-                if ((rc = tgo_part_ms_pack_dev(ctx, cand, W, send, sizes))) break;
-                if (int r = x->all_to_all(sizes, sizes + W, 8, st)) { rc = xfail(r); break; }
-                std::vector<int64_t> both(2 * W);
-                if (hipMemcpyAsync(both.data(), sizes, 2 * W * sizeof(int64_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
-                    hipStreamSynchronize(st) != hipSuccess) { rc = part_fail(ctx, TGO_E_HIP, "split sizes read"); break; }
-                std::vector<size_t> sb(W), so(W), rb(W), ro(W);
-                std::vector<int64_t> rpairs(W);
-                size_t a = 0, b = 0;
-                for (int p = 0; p < W; ++p) {
-                    sb[p] = static_cast<size_t>(both[p]) * 8; so[p] = a; a += sb[p];
-                    rb[p] = static_cast<size_t>(both[W + p]) * 8; ro[p] = b; b += rb[p];
-                    rpairs[p] = both[W + p] / 2;
-                }
-                if (int r = x->all_to_allv(send, sb.data(), so.data(), recv, rb.data(), ro.data(), st)) { rc = xfail(r); break; }
-                if ((rc = tgo_part_ms_settle_pairs(ctx, level, recv, rpairs.data(), W, frn, nullptr))) break;
-            }
+            rc = exchange(mf,
+                          [&](int64_t cap) { return tgo_part_ms_settle_fixed(ctx, level, recv, W, cap, frn, nullptr); },
+                          [&](const int64_t* rp) { return tgo_part_ms_settle_pairs(ctx, level, recv, rp, W, frn, nullptr); });
+            if (rc) break;
         }
         std::swap(fr, frn);
         std::swap(glob[0], glob[1]);
