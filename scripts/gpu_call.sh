@@ -1,15 +1,7 @@
 #!/bin/bash
-# Round-3 call v: per-edge td_expand / ms_push back; source split in the native partitioned
-# driver (parity at the default and a forced large split budget), probes, partitioned bench.
+# Round-3 call w: the scale-27 one-GPU line with the round-3 code (device assembly + handoff,
+# source split), full-size property checks.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
-OUT=gpurun_out/r03v; mkdir -p $OUT
-T="python -u -m pytest -x -q --timeout 300 --timeout-method thread"
-timeout -k 10 700 $T tests/test_gpu_parity.py tests/test_gpu_fullsize.py::test_config3_rmat24_msbfs_sweep tests/test_gpu_distributed.py > $OUT/gpu_tests.log 2>&1
-rc=$?; tail -2 $OUT/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
-TGO_MS_SPLIT=0.3 timeout -k 10 600 $T tests/test_gpu_parity.py -k multi_source tests/test_gpu_distributed.py -k "msbfs or multi_source" > $OUT/gpu_tests_split.log 2>&1
-rc=$?; tail -2 $OUT/gpu_tests_split.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 200 python3 scripts/ms_probe.py 24 5 > $OUT/ms.log 2>&1; rc=$?; grep msbfs $OUT/ms.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python3 scripts/bfs_probe.py 24 8 > $OUT/bfs.log 2>&1; rc=$?; tail -3 $OUT/bfs.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 400 python3 bench.py --partitioned --cpu-baseline 0 --sssp-roots 0 --rows-scale 0 > $OUT/bench_part.json 2> $OUT/bench_part.err
-rc=$?; [ $rc -eq 0 ] || { tail -5 $OUT/bench_part.err; exit 1; }
-python3 -c "import json; d=json.load(open('$OUT/bench_part.json')); print('native partitioned', d['value'], d['ms_per_step'])"
+OUT=gpurun_out/r03w; mkdir -p $OUT
+TGO_TRACE=1 timeout -k 10 1000 python3 -u scripts/scale27_check.py 27 64 > $OUT/scale27.json 2> $OUT/scale27.log
+rc=$?; tail -3 $OUT/scale27.log; cat $OUT/scale27.json; exit $rc
