@@ -1271,47 +1271,28 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
             // Split the sources: the pull's walk of a vertex stops once every open source is
             // covered, and one source whose frontier never reaches the vertex (a source far
             // from it, or one whose sweep is over) makes every walk scan its whole list.  The
-            // sources with the smallest frontiers (frontier sizes by ballots, then the exact
-            // push entries of the few smallest, within a budget of split_frac of the list
-            // entries; every source with an empty frontier) are pushed into candidate masks
-            // instead, and the pull covers only the rest.
+            // sources with the smallest frontiers (exact push entries per source, within a
+            // budget of split_frac of the list entries; every source with an empty frontier)
+            // are pushed into candidate masks instead, and the pull covers only the rest.
             // (tried at the first pull level of a run of pull levels, where the frontiers
             // are most unequal; later pull levels found nothing to split on RMAT-24)
             uint64_t sparse = 0;
             if (split_frac > 0.0 && !prev_pull) {
-                HIP_TRY(k_ms_source_counts(fr, g.n_active, s.ms_srcent, st));
+                // every source's exact push entries in one pass, then the smallest within the budget
+                HIP_TRY(k_ms_source_entries(push, fr, g.n_active, full, s.ms_srcent, st));
                 unsigned long long se[TGO_MAX_SOURCES];
                 HIP_TRY(hipMemcpyAsync(se, s.ms_srcent, sizeof(se), hipMemcpyDeviceToHost, st));
                 HIP_TRY(hipStreamSynchronize(st));
                 int order[TGO_MAX_SOURCES];
                 for (int r = 0; r < nseeds; ++r) order[r] = r;
                 std::sort(order, order + nseeds, [&](int a, int b) { return se[a] < se[b]; });
-                // candidates: the sources with the smallest frontiers (at most 16, each under
-                // 1/16 of the mean frontier); empty frontiers are free
-                const double mean_cnt = static_cast<double>(std::accumulate(se, se + nseeds, 0ULL)) / nseeds;
-                uint64_t cand = 0;
-                for (int i = 0, k = 0; i < nseeds && k < 16; ++i) {
-                    const int r = order[i];
-                    if (se[r] == 0) { sparse |= 1ULL << r; continue; }
-                    if (static_cast<double>(se[r]) * 16.0 > mean_cnt) break;
-                    cand |= 1ULL << r;
-                    ++k;
-                }
+                const double budget = split_frac * static_cast<double>(total);
                 double used = 0.0;
-                if (cand) {                              // their exact push entries, then the budget
-                    HIP_TRY(k_ms_source_entries(push, fr, g.n_active, cand, s.ms_srcent, st));
-                    HIP_TRY(hipMemcpyAsync(se, s.ms_srcent, sizeof(se), hipMemcpyDeviceToHost, st));
-                    HIP_TRY(hipStreamSynchronize(st));
-                    const double budget = split_frac * static_cast<double>(total);
-                    int co[TGO_MAX_SOURCES], nc = 0;
-                    for (int r = 0; r < nseeds; ++r)
-                        if ((cand >> r) & 1ULL) co[nc++] = r;
-                    std::sort(co, co + nc, [&](int a, int b) { return se[a] < se[b]; });
-                    for (int i = 0; i < nc; ++i) {
-                        if (used + static_cast<double>(se[co[i]]) > budget) break;
-                        used += static_cast<double>(se[co[i]]);
-                        sparse |= 1ULL << co[i];
-                    }
+                for (int i = 0; i < nseeds; ++i) {
+                    const int r = order[i];
+                    if (used + static_cast<double>(se[r]) > budget) break;
+                    used += static_cast<double>(se[r]);
+                    sparse |= 1ULL << r;
                 }
                 if (sparse == full) sparse = 0;            // nothing left to pull: plain pull
                 if (sparse) {

@@ -252,26 +252,36 @@ __global__ void __launch_bounds__(kBlock) ms_source_counts(const uint64_t* __res
     }
 }
 
-// Exact push entries of the candidate sources `cand` (their frontiers are small): only words
-// holding a candidate bit load degrees; lane b keeps the entries of source b.
+// Exact push entries per source of the frontier, for the sources in `cand`: one wave per
+// 64-vertex word; the lanes load their vertex's mask (and push degree when it is in the
+// frontier), the masks are transposed across the wave (as in ms_source_counts) so lane b holds
+// source b's column, and lane b adds the degrees of the column's set bits, fetched from their
+// lanes (one permute per set bit; a wave does max-column-popcount trips).
 __global__ void __launch_bounds__(kBlock) ms_source_entries(View push, const uint64_t* __restrict__ fr,
         int64_t n_active, uint64_t cand, unsigned long long* __restrict__ out) {
     __shared__ unsigned long long s_sum[kWavesPerBlock][64];
     const int64_t words = (n_active + 63) >> 6;
     unsigned long long sum = 0;
-    for (int64_t wd = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6; wd < words;
-         wd += (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6) {
+    const int64_t nw = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
+    for (int64_t wd = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6; wd < words; wd += nw) {
         const int64_t v = (wd << 6) + lane();
         const uint64_t mine = v < n_active ? (fr[v] & cand) : 0;
         if (!__ballot(mine != 0)) continue;                      // wave-uniform
         const unsigned long long deg = mine ? static_cast<unsigned long long>(push_degree(push, v)) : 0ULL;
-        uint64_t bits = cand;
-        while (bits) {
-            const int b = __ffsll(static_cast<long long>(bits)) - 1;
-            bits &= bits - 1;
-            unsigned long long t = ((mine >> b) & 1ULL) ? deg : 0ULL;
-            for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
-            if (lane() == b) sum += t;
+        uint64_t x = mine;
+        constexpr uint64_t kLow[6] = {0x00000000FFFFFFFFULL, 0x0000FFFF0000FFFFULL, 0x00FF00FF00FF00FFULL,
+                                      0x0F0F0F0F0F0F0F0FULL, 0x3333333333333333ULL, 0x5555555555555555ULL};
+#pragma unroll
+        for (int st = 0; st < 6; ++st) {
+            const int j = 32 >> st;
+            const uint64_t m = kLow[st];
+            const uint64_t y = __shfl_xor(x, j, 64);
+            x = (lane() & j) ? (((y & ~m) >> j) | (x & ~m)) : ((x & m) | ((y & m) << j));
+        }
+        while (__ballot(x != 0)) {                               // x: the vertices holding my source
+            const int src = x ? __ffsll(static_cast<long long>(x)) - 1 : lane();
+            const unsigned long long d = __shfl(deg, src, 64);
+            if (x) { sum += d; x &= x - 1; }
         }
     }
     s_sum[threadIdx.x >> 6][lane()] = sum;

@@ -393,34 +393,18 @@ extern "C" int tgo_part_msbfs_run(tgo_ctx* ctx, tgo_exchange* x, const int64_t* 
             uint64_t sparse = 0;
             int32_t with_cand = 0;
             if (first_dense && split_frac > 0.0) {
+                // every source's exact push entries (all-reduced), the smallest within the budget
                 int64_t se[64];
-                if ((rc = tgo_part_ms_source_counts(ctx, fr, sc64)) || (rc = read64(se))) break;
+                if ((rc = tgo_part_ms_source_entries(ctx, fr, full, sc64)) || (rc = read64(se))) break;
                 int order[64];
                 for (int r = 0; r < nseeds; ++r) order[r] = r;
                 std::sort(order, order + nseeds, [&](int a, int b) { return se[a] < se[b]; });
-                double mean = 0.0;
-                for (int r = 0; r < nseeds; ++r) mean += static_cast<double>(se[r]);
-                mean /= nseeds;
-                uint64_t candm = 0;
-                for (int i = 0, k = 0; i < nseeds && k < 16; ++i) {
-                    const int r = order[i];
-                    if (se[r] == 0) { sparse |= 1ULL << r; continue; }
-                    if (static_cast<double>(se[r]) * 16.0 > mean) break;
-                    candm |= 1ULL << r;
-                    ++k;
-                }
                 int64_t used = 0;
-                if (candm) {
-                    if ((rc = tgo_part_ms_source_entries(ctx, fr, candm, sc64)) || (rc = read64(se))) break;
-                    int co[64], nc = 0;
-                    for (int r = 0; r < nseeds; ++r)
-                        if ((candm >> r) & 1ULL) co[nc++] = r;
-                    std::sort(co, co + nc, [&](int a, int b) { return se[a] < se[b]; });
-                    for (int i = 0; i < nc; ++i) {
-                        if (static_cast<double>(used + se[co[i]]) > split_frac * static_cast<double>(total)) break;
-                        used += se[co[i]];
-                        sparse |= 1ULL << co[i];
-                    }
+                for (int i = 0; i < nseeds; ++i) {
+                    const int r = order[i];
+                    if (static_cast<double>(used + se[r]) > split_frac * static_cast<double>(total)) break;
+                    used += se[r];
+                    sparse |= 1ULL << r;
                 }
                 if (sparse == full) sparse = 0;
                 if (sparse && used > 0) {               // push the sparse sources' frontiers
