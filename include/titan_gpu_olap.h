@@ -270,7 +270,8 @@ int  tgo_load_edges(tgo_ctx* ctx, const tgo_edges* edges, const tgo_load_opts* o
  * order, are its column order (TGO_LOAD_COLUMN_ORDER positions).  opts->scope picks the
  * views as for every load; label_ids must be empty.
  * Returns TGO_E_INVALID for decreasing offsets, an index outside [0, n), non-increasing
- * titan_ids or a missing weight array. */
+ * titan_ids or a missing weight array; TGO_E_STATE while a tgo_load_rows scan is in progress
+ * (its staged rows are kept: tgo_finish_load still completes it). */
 int  tgo_load_csr(tgo_ctx* ctx, int64_t n, const int64_t* titan_ids, const int64_t* out_off,
                   const int32_t* out_idx, const int32_t* out_w, const int64_t* in_off,
                   const int32_t* in_idx, const int32_t* in_w, const tgo_load_opts* opts);
@@ -318,6 +319,12 @@ int  tgo_sssp(tgo_ctx* ctx, const tgo_sssp_args* args, int64_t* dist_out);
 int  tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_bfs_args* args,
                    int64_t* dist_out);
 int  tgo_copy_multi_distances(tgo_ctx* ctx, int32_t source, int64_t* dist_out);
+/* Per-ctx tuning of a traversal policy (never of a result: every value gives the same
+ * distances / ranks).  TGO_TUNE_MS_SPLIT: push budget of the sparse sources at the first pull
+ * level of a multi-source sweep (tgo_bfs_multi, tgo_part_msbfs_run), a fraction of the list
+ * entries; 0 = every source pulled; < 0 = the default (TGO_MS_SPLIT or 0.005). */
+enum { TGO_TUNE_MS_SPLIT = 1 };
+int  tgo_set_tuning(tgo_ctx* ctx, int32_t key, double value);
 /* After tgo_bfs_multi with TGO_FLAG_STATS: per seed, reached vertices and their entries. */
 int  tgo_multi_stats(tgo_ctx* ctx, int64_t* reached, int64_t* reached_entries);
 int  tgo_copy_distances(tgo_ctx* ctx, int64_t* dist_out);

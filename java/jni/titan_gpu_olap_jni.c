@@ -148,9 +148,25 @@ JNIEXPORT jint JNICALL JFN(loadCsr)(JNIEnv* env, jclass cls, jlong h, jlongArray
                                     jintArray out_idx, jintArray out_w, jlongArray in_off, jintArray in_idx,
                                     jintArray in_w, jint scope, jlong weight_key, jboolean column_order) {
     (void)cls;
+    if (!ids || !out_off || !in_off || !out_idx || !in_idx) return TGO_E_INVALID;
     const jsize n1 = (*env)->GetArrayLength(env, out_off);
     if (n1 < 1 || (*env)->GetArrayLength(env, in_off) != n1 || (*env)->GetArrayLength(env, ids) != n1 - 1)
         return TGO_E_INVALID;
+    /* tgo_load_csr stages out_off[n] / in_off[n] entries from the pinned index (and weight)
+     * arrays: arrays shorter than the offsets say would be read past their end */
+    jlong ends[4];
+    (*env)->GetLongArrayRegion(env, out_off, 0, 1, &ends[0]);
+    (*env)->GetLongArrayRegion(env, out_off, n1 - 1, 1, &ends[1]);
+    (*env)->GetLongArrayRegion(env, in_off, 0, 1, &ends[2]);
+    (*env)->GetLongArrayRegion(env, in_off, n1 - 1, 1, &ends[3]);
+    if (ends[0] != 0 || ends[2] != 0 || ends[1] < 0 || ends[3] < 0 ||
+        ends[1] > (jlong)(*env)->GetArrayLength(env, out_idx) || ends[3] > (jlong)(*env)->GetArrayLength(env, in_idx))
+        return TGO_E_INVALID;
+    if (weight_key != 0 &&
+        (!out_w || !in_w || ends[1] > (jlong)(*env)->GetArrayLength(env, out_w) ||
+         ends[3] > (jlong)(*env)->GetArrayLength(env, in_w)))
+        return TGO_E_INVALID;
+    if (weight_key == 0) { out_w = NULL; in_w = NULL; }
     jlong* t = (*env)->GetLongArrayElements(env, ids, NULL);
     jlong* oo = (*env)->GetLongArrayElements(env, out_off, NULL);
     jlong* io = (*env)->GetLongArrayElements(env, in_off, NULL);

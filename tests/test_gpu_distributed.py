@@ -337,17 +337,22 @@ def test_edge_balanced_partition_drivers(world, monkeypatch):
     assert np.array_equal(cut(res, 0), osd)
 
 
-@pytest.mark.parametrize("world,fixed", [(1, None), (2, None), (2, 0), (4, None), (4, 0)])
-def test_native_msbfs_driver(world, fixed):
+@pytest.mark.parametrize("world,fixed,split", [(1, None, -1.0), (2, None, -1.0), (2, 0, -1.0), (4, None, -1.0),
+                                               (4, 0, -1.0), (1, None, 0.0), (2, None, 0.3), (4, 0, 0.3),
+                                               (4, None, 0.0)])
+def test_native_msbfs_driver(world, fixed, split):
     """tgo_part_msbfs_run: the partitioned multi-source sweep as ONE native call (C++ level
     loop, collectives through an in-process exchange group of thread ranks on this device):
     every seed's levels equal the oracle's, reached counts global, and the result equals the
-    Python driver's.  fixed=0 forces the sized-pairs exchange on every sparse level."""
+    Python driver's.  fixed=0 forces the sized-pairs exchange on every sparse level; split sets
+    the source-split budget (tgo_set_tuning; -1 the default, 0 no split, 0.3 a forced split)."""
     from titan_amd.distributed import NativeExchange, distributed_msbfs_native
     scale = 12
     n = 1 << scale
     src, dst, _ = rmat_edges(scale, 16, seed=33)
     ranks = Ranks(world, n, src, dst, L.SCOPE_BOTH_E, layout=True, device_counts=True)
+    for be in ranks.backends:
+        be.e.set_tuning(L.TUNE_MS_SPLIT, split)
     og = fr.OracleGraph.from_edges(n, src, dst)
     ids = (np.arange(n, dtype=np.int64) + 1) << 3
     rng = np.random.default_rng(9)

@@ -214,6 +214,26 @@ def test_rmat_multi_source_bfs_bit_exact(rmat12, scope, nseeds):
         assert np.array_equal(d2[i], oracle.shortest_distance(int(ids[s]), 2, scope)[0])
 
 
+@pytest.mark.parametrize("split", [0.0, -1.0, 0.3, 1.0])
+def test_multi_source_split_budget_is_policy_only(rmat12, split):
+    """the source split's push budget (tgo_set_tuning TGO_TUNE_MS_SPLIT; 0 = pull
+    every source, -1 = the default 0.5 %, 0.3 / 1.0 = most or all sources pushed at the first
+    pull level) changes the traversal plan, never a level: every seed equals the oracle."""
+    n, src, dst, w, ids, oracle, roots = rmat12
+    eng = Engine().load_edges(n, src, dst, BOTH).set_tuning(L.TUNE_MS_SPLIT, split)
+    seeds = pick_roots(n, src, dst, 64, seed=17)
+    d = eng.bfs_multi(seeds, n, BOTH, seed_is_dense=True, stats=True)
+    r, _ = eng.multi_stats(64)
+    for i, s in enumerate(seeds):
+        od, _ = oracle.shortest_distance(int(ids[s]), n, BOTH)
+        assert np.array_equal(d[i], od), (split, i)
+        assert r[i] == int((od != ABSENT).sum())
+    with pytest.raises(TitanException):
+        eng.set_tuning(L.TUNE_MS_SPLIT, 1.5)
+    with pytest.raises(TitanException):
+        eng.set_tuning(99, 0.0)
+
+
 def test_multi_source_duplicate_and_gotg_seeds():
     eng, rows, vids, sd, npz = engine_from_fixture("gotg", BOTH)
     names = list(npz["names"])

@@ -67,3 +67,23 @@ def test_scan_job_failures_are_sticky():
     job = _read(SCANJOB)
     assert "public void rethrowFailure()" in job
     assert re.search(r"if \(handle\.failure == null\) handle\.failure = e;", job)
+
+
+@pytest.mark.skipif(shutil.which("gcc") is None, reason="needs gcc")
+def test_load_csr_validates_array_lengths_before_pinning(tmp_path):
+    """loadCsr hands tgo_load_csr the pinned Java arrays, which stages out_off[n] /
+    in_off[n] entries from them — short or null index / weight arrays must fail with
+    TGO_E_INVALID before the C-ABI is reached (tests/jni_harness.c: a fake JNIEnv, the shim
+    linked against the harness's recording tgo_load_csr and the real library for the rest)."""
+    lib = os.path.join(ROOT, "titan_amd")
+    if not os.path.exists(os.path.join(lib, "libtitan_gpu_olap.so")):
+        pytest.skip("libtitan_gpu_olap.so not built")
+    exe = str(tmp_path / "jni_harness")
+    r = subprocess.run(["gcc", "-std=c11", "-Wall", "-Wextra", "-Werror", "-Wno-unused-parameter",
+                        "-I", os.path.join(ROOT, "tests", "jni_stub"), "-I", os.path.join(ROOT, "include"),
+                        os.path.join(ROOT, "tests", "jni_harness.c"), SHIM, "-o", exe,
+                        "-L", lib, "-ltitan_gpu_olap", "-Wl,-rpath," + lib], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    run = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert run.returncode == 0, run.stdout + run.stderr
+    assert run.stdout.count("ok  ") == 12, run.stdout

@@ -33,6 +33,7 @@ ORDER_ASC, ORDER_DESC = 0, 1
 RESULT_DISTANCE, RESULT_PAGERANK, RESULT_DEGREE, RESULT_VALUES = 0, 1, 2, 3
 SSSP_HOP_BOUNDED, SSSP_DELTA = 0, 1
 FLAG_STATS = 1
+TUNE_MS_SPLIT = 1          # tgo_set_tuning keys
 DIST_ABSENT = -(1 << 63)
 ABI_VERSION = 2
 COMBINE_SUM, COMBINE_MIN, COMBINE_MAX = 0, 1, 2
@@ -138,7 +139,7 @@ EXPORTS = [
     "tgo_finish_load", "tgo_load_edges", "tgo_load_csr", "tgo_num_vertices", "tgo_vertex_ids", "tgo_graph_csr", "tgo_graph_perm",
     "tgo_bfs",
     "tgo_sssp", "tgo_copy_distances", "tgo_pagerank", "tgo_walkcount", "tgo_stats_get", "tgo_sync",
-    "tgo_bfs_multi", "tgo_copy_multi_distances", "tgo_multi_stats",
+    "tgo_bfs_multi", "tgo_copy_multi_distances", "tgo_multi_stats", "tgo_set_tuning",
     "tgo_gather", "tgo_combine_global", "tgo_dense_ids", "tgo_decode_edge_entry", "tgo_result_rows",
     "tgo_gather_lists", "tgo_result_rows_values",
     "tgo_rmat_edges", "tgo_pick_roots", "tgo_synth_rows",
@@ -202,6 +203,7 @@ def load() -> C.CDLL:
         "tgo_bfs_multi": (C.c_int, [vp, _i64p, C.c_int32, P(BfsArgs), _i64p]),
         "tgo_copy_multi_distances": (C.c_int, [vp, C.c_int32, _i64p]),
         "tgo_multi_stats": (C.c_int, [vp, _i64p, _i64p]),
+        "tgo_set_tuning": (C.c_int, [vp, C.c_int32, C.c_double]),
         "tgo_gather": (C.c_int, [vp, P(GatherArgs), vp, P(C.c_uint8), vp, P(C.c_uint8)]),
         "tgo_gather_lists": (C.c_int, [vp, P(GatherArgs), vp, P(C.c_uint8), _i64p, vp]),
         "tgo_result_rows_values": (C.c_int, [vp, P(ResultArgs), vp, P(C.c_uint8), P(ResultSize), P(RowsBuf)]),

@@ -65,6 +65,7 @@ struct tgo_ctx {
     bool res_empty = false;                  // it set no property (PageRank iterations(0))
     ResultSource res_src;
     int num_cus = 256;          // compute units of the device (persistent launches)
+    double ms_split = -1.0;     // tgo_set_tuning(TGO_TUNE_MS_SPLIT); < 0: TGO_MS_SPLIT / the default
 };
 
 namespace {
@@ -735,9 +736,13 @@ int run_delta_split(tgo_ctx* ctx, int64_t seed, int64_t delta) {
     HIP_TRY(hipMemsetAsync(s.vb, 0, words * 8, st));        // pending bitmap
     HIP_TRY(hipMemsetAsync(s.ds_member, 0, words * 8, st));
     // device-driven steps (delta_loop.hip) unless TGO_DS_HOSTLOOP=1 or the packed queue
-    // counters could overflow (count < 2^28, entries < 2^36)
+    // counters could overflow: a queue holds up to 2n + 2 takes (a light and a heavy take per
+    // vertex, ds_q / ds_qp are sized for that) in the count field above kDsCountShift, and up
+    // to nnz entries below it
     static const bool host_loop = env_double("TGO_DS_HOSTLOOP", 0.0) != 0.0;
-    if (!host_loop && seed >= 0 && n < (int64_t(1) << 28) && g.push_ws.nnz < (int64_t(1) << kDsCountShift))
+    constexpr int64_t kDsMaxCount = int64_t(1) << (64 - kDsCountShift);
+    static_assert(kDsCountShift > 32 && kDsCountShift < 64, "queue counter layout");
+    if (!host_loop && seed >= 0 && 2 * n + 2 < kDsMaxCount && g.push_ws.nnz < (int64_t(1) << kDsCountShift))
         return run_delta_device(ctx, seed, delta);
     int phases = 0, buckets = 0;
     int64_t relaxed = 0;
@@ -891,6 +896,8 @@ int finish_distance_program(tgo_ctx* ctx, int scope, int flags, int64_t* dist_ou
 
 // ============================================================================ C-ABI
 
+namespace tgo { double ms_split_of(const tgo_ctx* ctx); }
+
 extern "C" {
 
 void tgo_default_options(tgo_options* o) {
@@ -901,6 +908,18 @@ void tgo_default_options(tgo_options* o) {
     o->host_threads = 0;
     o->hard_query_limit = 100000;
     o->stream = nullptr;
+}
+
+int tgo_set_tuning(tgo_ctx* ctx, int32_t key, double value) {
+    if (!ctx) return TGO_E_INVALID;
+    switch (key) {
+    case TGO_TUNE_MS_SPLIT:
+        if (!(value <= 1.0)) return fail(ctx, TGO_E_INVALID, "TGO_TUNE_MS_SPLIT: a fraction <= 1 (< 0: the default)");
+        ctx->ms_split = value < 0.0 ? -1.0 : value;
+        return TGO_OK;
+    default:
+        return fail(ctx, TGO_E_INVALID, "tgo_set_tuning: unknown key");
+    }
 }
 
 int tgo_create(const tgo_options* opts, tgo_ctx** out) {
@@ -1051,6 +1070,8 @@ int tgo_load_csr(tgo_ctx* ctx, int64_t n, const int64_t* titan_ids, const int64_
     if (!opts || !out_off || !in_off) return fail(ctx, TGO_E_INVALID, "null argument");
     if (opts->scope < 0 || opts->scope > 2) return fail(ctx, TGO_E_INVALID, "invalid scope");
     if (opts->n_labels != 0) return fail(ctx, TGO_E_INVALID, "tgo_load_csr takes no label_ids (the rows are already sliced)");
+    if (ctx->staging.active)            // a tgo_load_rows scan is in progress: finish (or destroy) it first
+        return fail(ctx, TGO_E_STATE, "tgo_load_csr during a row load (tgo_load_rows without tgo_finish_load)");
     (void)hipSetDevice(ctx->opts.device);
     const auto t0 = std::chrono::steady_clock::now();
     // the rows as a staging of decoded rows (each row's OUT entries, then its IN entries), on
@@ -1241,7 +1262,7 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
     const bool filter = filter_from >= 0 && filter_from < n;
     // TGO_MS_SPLIT: push budget of the pull levels' sparse sources, as a fraction of the
     // list entries (0 = every source pulled)
-    static const double split_frac = env_double("TGO_MS_SPLIT", 0.005);
+    const double split_frac = tgo::ms_split_of(ctx);
     int64_t qlen = static_cast<int64_t>(uniq.size());
     int64_t mf = 0;
     {
@@ -2723,4 +2744,11 @@ int part_scratch(tgo_ctx* ctx, void** p, int64_t bytes, int slot) {
     *p = s.drv[slot];
     return TGO_OK;
 }
+// Push budget of the multi-source pull levels' sparse sources (the source split), as a
+// fraction of the list entries: the ctx's tgo_set_tuning value, else TGO_MS_SPLIT, else 0.5 %.
+double ms_split_of(const tgo_ctx* ctx) {
+    static const double env = env_double("TGO_MS_SPLIT", 0.005);
+    return ctx->ms_split >= 0.0 ? ctx->ms_split : env;
+}
+
 }  // namespace tgo

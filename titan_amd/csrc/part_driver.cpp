@@ -66,26 +66,43 @@ using tgo::copy_chunked;
 // ------------------------------------------------------------------ RCCL (production)
 struct RcclExchange : tgo_exchange {
     ncclComm_t comm = nullptr;
+    bool aborted = false;
     ~RcclExchange() override {
         if (comm) (void)ncclCommDestroy(comm);
         release_pinned();
+    }
+    // A rank that fails between collectives (a local step's error, a HIP error) would leave
+    // its peers blocked in the next collective forever: abort the communicator, which makes
+    // their pending and later RCCL calls return an error, and refuse further use here.
+    void abort() override {
+        if (comm) (void)ncclCommAbort(comm);
+        comm = nullptr;
+        aborted = true;
     }
     int check(ncclResult_t r, const char* what) {
         if (r == ncclSuccess) return TGO_OK;
         err = std::string(what) + ": " + ncclGetErrorString(r);
         return TGO_E_HIP;
     }
+    bool usable() {
+        if (!aborted) return true;
+        err = "RCCL exchange aborted by an earlier failure";
+        return false;
+    }
     int all_gather(void* buf, size_t bytes, hipStream_t s) override {
+        if (!usable()) return TGO_E_COMM;
         if (world == 1) return TGO_OK;
         char* b = static_cast<char*>(buf);
         return check(ncclAllGather(b + rank * bytes, b, bytes, ncclChar, comm, s), "ncclAllGather");
     }
     int all_to_all(const void* send, void* recv, size_t bytes, hipStream_t s) override {
+        if (!usable()) return TGO_E_COMM;
         if (world == 1) return copy_on(send, recv, bytes, s);
         return check(ncclAllToAll(send, recv, bytes, ncclChar, comm, s), "ncclAllToAll");
     }
     int all_to_allv(const void* send, const size_t* sb, const size_t* so, void* recv, const size_t* rb,
                     const size_t* ro, hipStream_t s) override {
+        if (!usable()) return TGO_E_COMM;
         if (world == 1) return copy_on(static_cast<const char*>(send) + so[0], static_cast<char*>(recv) + ro[0], sb[0], s);
         int rc = check(ncclGroupStart(), "ncclGroupStart");
         for (int p = 0; !rc && p < world; ++p) {
@@ -96,6 +113,7 @@ struct RcclExchange : tgo_exchange {
         return rc ? rc : rc2;
     }
     int all_reduce_sum(int64_t* buf, size_t count, hipStream_t s) override {
+        if (!usable()) return TGO_E_COMM;
         if (world == 1) return TGO_OK;
         return check(ncclAllReduce(buf, buf, count, ncclInt64, ncclSum, comm, s), "ncclAllReduce");
     }
@@ -274,6 +292,7 @@ int part_dims(tgo_ctx* ctx, int64_t* n_local, int64_t* lo, int64_t* n_global, in
 int part_fail(tgo_ctx* ctx, int code, const std::string& msg);
 int part_scratch(tgo_ctx* ctx, void** p, int64_t bytes, int slot);
 int64_t* part_dcounts_of(tgo_ctx* ctx);
+double ms_split_of(const tgo_ctx* ctx);
 template <class T>
 int scratch(tgo_ctx* ctx, T*& p, int64_t count, int slot) {
     void* q = nullptr;
@@ -347,8 +366,8 @@ extern "C" int tgo_part_msbfs_run(tgo_ctx* ctx, tgo_exchange* x, const int64_t* 
     // level counts stay on the device: the steps publish {next queue, its entries, own queue}
     if ((rc = tgo_part_device_counts(ctx, dc))) return rc;
     int levels = 0;
-    // source split of the first dense level of a run (tgo_bfs_multi's rule; TGO_MS_SPLIT)
-    static const double split_frac = [] { const char* e = std::getenv("TGO_MS_SPLIT"); return e ? std::atof(e) : 0.005; }();
+    // source split of the first dense level of a run (tgo_bfs_multi's rule and budget)
+    const double split_frac = ms_split_of(ctx);
     const uint64_t full = nseeds == 64 ? ~0ULL : ((1ULL << nseeds) - 1ULL);
     int64_t* sc64 = dc + 3;                                 // 64 per-source sums (free during the sweep)
     auto read64 = [&](int64_t* host) -> int {

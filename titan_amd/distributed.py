@@ -715,13 +715,18 @@ class NativeExchange:
         of 128 bytes per rank, rank 0's slice taken) and joins the communicator."""
         lib = L.load()
         cm = _comm(comm, group)
-        uid = np.zeros(128, np.uint8)
+        # 128 id bytes + a status byte per rank: rank 0's failure to make the id travels with
+        # the all-gather, so every rank raises instead of the peers waiting for an id forever
+        uid = np.zeros(136, np.uint8)
         if cm.rank == 0 and lib.tgo_exchange_rccl_id(L.ptr(uid, C.c_uint8)):
-            raise RuntimeError("tgo_exchange_rccl_id failed")
+            uid[128] = 1
         dev = torch.device("cuda", device) if torch.cuda.is_available() else torch.device("cpu")
-        out = torch.empty(128 * cm.world, dtype=torch.uint8, device=dev)
+        out = torch.empty(136 * cm.world, dtype=torch.uint8, device=dev)
         cm.all_gather_into_tensor(out, torch.from_numpy(uid).to(dev))
-        uid = np.ascontiguousarray(out[:128].cpu().numpy())
+        got = out[:136].cpu().numpy()
+        if got[128]:
+            raise RuntimeError("tgo_exchange_rccl_id failed on rank 0")
+        uid = np.ascontiguousarray(got[:128])
         h = C.c_void_p()
         rc = lib.tgo_exchange_rccl_create(cm.world, cm.rank, L.ptr(uid, C.c_uint8), device, C.byref(h))
         if rc:

@@ -233,6 +233,12 @@ class Engine:
                                                           L.ptr(out, C.c_int64)))
         return out
 
+    def set_tuning(self, key, value):
+        """tgo_set_tuning: a traversal policy of this ctx (L.TUNE_MS_SPLIT: the multi-source
+        source-split budget; < 0 restores the default).  Never changes a result."""
+        _check(self.lib, self.ctx, self.lib.tgo_set_tuning(self.ctx, int(key), float(value)))
+        return self
+
     def multi_stats(self, nseeds):
         r = np.zeros(nseeds, np.int64)
         e = np.zeros(nseeds, np.int64)
