@@ -19,6 +19,12 @@ extern "C" {
 int tgo_rmat_edges(int32_t scale, int32_t edge_factor, uint64_t seed, int64_t edge_begin,
                    int64_t count, int32_t* src, int32_t* dst, int32_t* weight, int32_t threads);
 
+/* tgo_rmat_edges computed on GPU `device` (the same stream, bit for bit): the edges are
+ * generated there chunk by chunk and copied into the host arrays.  TGO_E_HIP without a usable
+ * device. */
+int tgo_rmat_edges_device(int32_t scale, int32_t edge_factor, uint64_t seed, int64_t edge_begin,
+                          int64_t count, int32_t* src, int32_t* dst, int32_t* weight, int32_t device);
+
 /* Undirected degree (out + in) histogram helper and seeded root selection among vertices
  * of degree > 0 (Graph500 style): writes `nroots` distinct dense ids. */
 int tgo_pick_roots(int64_t n, int64_t m, const int32_t* src, const int32_t* dst, uint64_t seed,

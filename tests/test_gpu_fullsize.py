@@ -187,3 +187,30 @@ def test_wide_bitmap_single_source_bfs():
         if i == 0:
             hb = eng.sssp(r, 64, L.SCOPE_BOTH_E, mode=L.SSSP_HOP_BOUNDED, seed_is_dense=True)
             assert np.array_equal(hb, bf)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_config5_rmat24_weighted_sssp_partitioned(rmat24, world):
+    """configs[4] partitioned: the bench's weighted, capped RMAT-24 inE graph over `world`
+    ranks (equal ranges, degree-grouped global layout, one device, ranks as threads with the
+    drivers' collectives in-process) — delta-stepping distances equal the one-GPU engine's bit
+    for bit (that engine is oracle-pinned in test_config5_rmat24_weighted_sssp), reached
+    counts global, every rank through the same phases."""
+    from test_gpu_distributed import Ranks
+    from titan_amd.distributed import distributed_sssp
+    n, src, dst, roots, w = rmat24
+    one = Engine(host_threads=THREADS).load_edges(n, src, dst, IN, weight=w, apply_cap=True)
+    picked = []
+    for r in roots:
+        d = one.sssp(int(r), n, IN, mode=L.SSSP_DELTA, seed_is_dense=True, stats=True)
+        if one.stats()["reached"] * 4 >= n:                  # the giant component, as bench.py
+            picked.append((int(r), d, one.stats()["reached"]))
+        if len(picked) == 2:
+            break
+    del one
+    ranks = Ranks(world, n, src, dst, IN, weight=w, layout=True, apply_cap=True)
+    for r, d, reached in picked:
+        res = ranks.run(lambda be, comm: distributed_sssp(be, r, 0, comm=comm))
+        assert np.array_equal(np.concatenate([x[0] for x in res]), d), r
+        assert all(x[1][0] == reached for x in res)
+        assert len({x[2] for x in res}) == 1

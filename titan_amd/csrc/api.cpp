@@ -1634,8 +1634,15 @@ int tgo_load_partition_layout(tgo_ctx* ctx, int64_t n_global, int64_t lo, int64_
     const auto t0 = std::chrono::steady_clock::now();
     HostGraph h;
     std::string err;
-    int rc = assemble_partition(edges, n_global, lo, hi, opts, ctx->opts.hard_query_limit, layout_global, h,
-                                threads_of(ctx), err);
+    // device assembly (assemble.hip) unless TGO_HOST_ASSEMBLY=1
+    const bool on_dev = env_i64("TGO_HOST_ASSEMBLY", 0) == 0;
+    int rc = on_dev ? assemble_partition_device(edges, n_global, lo, hi, opts, ctx->opts.hard_query_limit, layout_global,
+                                                h, ctx->stream, err)
+                    : assemble_partition(edges, n_global, lo, hi, opts, ctx->opts.hard_query_limit, layout_global, h,
+                                         threads_of(ctx), err);
+    if (rc == TGO_OK && env_i64("TGO_TRACE", 0))
+        std::fprintf(stderr, "[tgo] load_partition assembly (%s) %8.1f ms\n", on_dev ? "device" : "host",
+                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
     if (rc) return fail(ctx, rc, err);
     free_graph(ctx);
     ctx->staging = RowStaging();
@@ -2246,25 +2253,27 @@ int tgo_part_pr_blocked(tgo_ctx* ctx, int32_t world, int64_t active_span, int64_
     }
     const int64_t A = active_span, W = world;
     std::vector<int64_t> off(nl + 1);
-    std::vector<int32_t> adj(static_cast<size_t>(g.in.nnz));
     HIP_TRY(hipMemcpy(off.data(), g.in.off, (nl + 1) * sizeof(int64_t), hipMemcpyDeviceToHost));
-    if (g.in.nnz) HIP_TRY(hipMemcpy(adj.data(), g.in.adj, g.in.nnz * sizeof(int32_t), hipMemcpyDeviceToHost));
-    std::atomic<bool> bad{false};
-    const int threads = threads_of(ctx);
-    std::vector<std::thread> th;
-    for (int t = 0; t < threads; ++t)
-        th.emplace_back([&, t] {
-            const size_t m = adj.size(), a = m * t / threads, b = m * (t + 1) / threads;
-            for (size_t k = a; k < b; ++k) {
-                const int64_t u = adj[k], r = u / nl, o = u % nl;
-                if (o >= A) { bad = true; continue; }
-                adj[k] = static_cast<int32_t>(o < H ? r * H + o : W * H + r * (A - H) + (o - H));
-            }
-        });
-    for (auto& x : th) x.join();
-    if (bad) return fail(ctx, TGO_E_INVALID, "tgo_part_pr_blocked: a source row lies beyond active_span");
+    // the in-lists' sources as positions in the blocked gathered vector, mapped on the device;
+    // the cold layout is built from that device copy (pr_layout.hip), as on one GPU
+    const int64_t nnz = g.in.nnz;
+    int32_t* gidx = nullptr;
+    int* bad = nullptr;
+    HIP_TRY(hipMalloc(&gidx, std::max<int64_t>(nnz, 1) * sizeof(int32_t)));
+    struct Free { void* p; ~Free() { if (p) (void)hipFree(p); } } free_gidx{gidx};
+    HIP_TRY(hipMalloc(&bad, sizeof(int)));
+    Free free_bad{bad};
+    HIP_TRY(hipMemsetAsync(bad, 0, sizeof(int), ctx->stream));
+    HIP_TRY(k_part_gathered_index(g.in.adj, nnz, nl, A, H, W, gidx, bad, ctx->stream));
+    int hbad = 0;
+    HIP_TRY(hipMemcpyAsync(&hbad, bad, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    if (hbad) return fail(ctx, TGO_E_INVALID, "tgo_part_pr_blocked: a source row lies beyond active_span");
     bool ready = false;
-    if ((rc = upload_cold_blocks(ctx, off, adj, W * A, W * H, g.n_active, g.cold_in, ready))) return rc;
+    const std::vector<int32_t> no_host_adj;
+    if ((rc = upload_cold_blocks(ctx, off, no_host_adj, W * A, W * H, g.n_active, g.cold_in, ready, g.in.off, gidx, nnz)))
+        return rc;
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
     g.cold_in_ready = ready;
     if (!ready) { ctx->part_pr_world = 0; return TGO_OK; }
     Scratch& s = ctx->sc;

@@ -279,6 +279,35 @@ __global__ void count_mismatch(const uint32_t* __restrict__ cnt, const int64_t* 
         if (static_cast<int64_t>(cnt[v]) != off[v + 1] - off[v]) atomicOr(bad, 1);
 }
 
+// ---- partitions (tgo_load_partition): the rows of the owned range [lo, lo + n) only
+// Entries of direction d whose row (own) is owned: flag for the compaction scan.
+__global__ void owned_flags(const int32_t* __restrict__ own, int64_t m, int64_t lo, int64_t hi, uint32_t* __restrict__ flag) {
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x)
+        flag[k] = (own[k] >= lo && own[k] < hi) ? 1u : 0u;
+}
+// Owned entries compacted in edge order: key = (own - lo) << b | nbr (global id), payload = edge index.
+__global__ void owned_keys(const int32_t* __restrict__ own, const int32_t* __restrict__ nbr, const uint32_t* __restrict__ flag,
+                           const uint64_t* __restrict__ pos, int64_t m, int64_t lo, int b, uint64_t* __restrict__ key,
+                           uint32_t* __restrict__ val) {
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x) {
+        if (!flag[k]) continue;
+        const uint64_t p = pos[k];
+        key[p] = (static_cast<uint64_t>(own[k] - lo) << b) | static_cast<uint32_t>(nbr[k]);
+        val[p] = static_cast<uint32_t>(k);
+    }
+}
+// Re-key through the global layout: row -> layout[lo + row] - lo, neighbour -> layout[nbr].
+__global__ void part_rekey(const uint64_t* __restrict__ key, int64_t m, int b, const int32_t* __restrict__ layout,
+                           int64_t lo, uint64_t* __restrict__ okey, uint32_t* __restrict__ oval) {
+    const uint64_t mask = (uint64_t(1) << b) - 1;
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = static_cast<int64_t>(key[k] >> b);
+        const uint64_t o = static_cast<uint64_t>(layout[lo + r] - lo), x = static_cast<uint32_t>(layout[key[k] & mask]);
+        okey[k] = (o << b) | x;
+        if (oval) oval[k] = static_cast<uint32_t>(k);
+    }
+}
+
 struct Sorter {
     ScopedBuf<uint8_t> tmp;
     hipStream_t s;
@@ -571,6 +600,217 @@ int assemble_edges_device(const tgo_edges* e, const tgo_load_opts* opts, int64_t
     return TGO_OK;
 }
 
+
+// tgo_load_partition on the device: the rows of the owned range [lo, hi) of a global edge
+// list (graph_build.cpp assemble_partition, array for array).  Row v (local) has the OUT
+// entries of the edges with src = lo + v and the IN entries of those with dst = lo + v, each
+// in column order (global neighbour, edge index) — the owned entries compacted in edge order,
+// then one stable sort by (row, neighbour); the untyped single-direction scopes cut each row
+// at the limit (OUT first); with a layout, rows and neighbours move to their layout ids and a
+// second stable sort restores (row, neighbour) order, equal entries keeping the cut order.
+int assemble_partition_device(const tgo_edges* e, int64_t n_global, int64_t lo, int64_t hi, const tgo_load_opts* opts,
+                              int64_t hard_limit, const int32_t* layout, HostGraph& g, hipStream_t s, std::string& err) {
+    g = HostGraph();
+    const int64_t n = hi - lo, m = e->m;
+    if (lo < 0 || hi > n_global || n <= 0 || n_global >= INT32_MAX) { err = "invalid partition range"; return TGO_E_INVALID; }
+    if (m >= (int64_t(1) << 32)) { err = "more than 2^32 edges per load"; return TGO_E_UNSUPPORTED; }
+    g.n = n;
+    g.scope = opts->scope;
+    g.has_weight = opts->weight_key != 0 && e->weight != nullptr;
+    g.weight_dt = TGO_DT_INTEGER;
+    g.titan_id.resize(n);
+    for (int64_t v = 0; v < n; ++v) g.titan_id[v] = (lo + v + 1) << 3;
+    if (layout) {                 // owned rows move inside [lo, hi); neighbours take their owners' layout
+        g.perm.resize(n);
+        std::vector<uint8_t> seen(n, 0);
+        for (int64_t v = 0; v < n; ++v) {
+            const int64_t p = static_cast<int64_t>(layout[lo + v]) - lo;
+            if (p < 0 || p >= n || seen[p]) { err = "layout is not a permutation of the owned range"; return TGO_E_INVALID; }
+            seen[p] = 1;
+            g.perm[v] = static_cast<int32_t>(p);
+        }
+    }
+    const bool cap = opts->apply_cap && opts->n_labels == 0 && opts->scope != TGO_SCOPE_BOTH_E;
+    const int64_t limit = cap ? hard_limit : INT64_MAX;
+    int b = 1;                    // neighbour bits (global ids)
+    while ((int64_t(1) << b) < n_global) ++b;
+    int br = 1;                   // row bits (local ids)
+    while ((int64_t(1) << br) < n) ++br;
+    const int bits = b + br;
+    static const bool trace = std::getenv("TGO_TRACE") && std::atoi(std::getenv("TGO_TRACE")) != 0;
+    auto t_last = std::chrono::steady_clock::now();
+    auto lap = [&](const char* what) {
+        if (!trace) return;
+        (void)hipStreamSynchronize(s);
+        const auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[tgo]   partition %-14s %8.1f ms\n", what, std::chrono::duration<double, std::milli>(now - t_last).count());
+        t_last = now;
+    };
+    ScopedBuf<int32_t> d_src, d_dst, d_w, d_lay;
+    AS_TRY(d_src.alloc(m));
+    AS_TRY(d_dst.alloc(m));
+    if (m) {
+        AS_TRY(copy_chunked(d_src.p, e->src, m * sizeof(int32_t), hipMemcpyHostToDevice));
+        AS_TRY(copy_chunked(d_dst.p, e->dst, m * sizeof(int32_t), hipMemcpyHostToDevice));
+    }
+    if (g.has_weight) {
+        AS_TRY(d_w.alloc(m));
+        if (m) AS_TRY(copy_chunked(d_w.p, e->weight, m * sizeof(int32_t), hipMemcpyHostToDevice));
+    }
+    if (layout) {
+        AS_TRY(d_lay.alloc(n_global));
+        AS_TRY(copy_chunked(d_lay.p, layout, n_global * sizeof(int32_t), hipMemcpyHostToDevice));
+    }
+    {
+        ScopedBuf<int> bad;
+        AS_TRY(bad.alloc(1));
+        AS_TRY(hipMemsetAsync(bad.p, 0, sizeof(int), s));
+        if (m) range_check<<<grid(m), kB, 0, s>>>(d_src.p, d_dst.p, m, n_global, bad.p);
+        int hb = 0;
+        AS_TRY(hipMemcpyAsync(&hb, bad.p, sizeof(int), hipMemcpyDeviceToHost, s));
+        AS_TRY(hipStreamSynchronize(s));
+        if (hb) { err = "edge endpoint out of range"; return TGO_E_INVALID; }
+    }
+    lap("upload + check");
+    Sorter so{{}, s};
+    auto count_of = [&](const uint32_t* flag, const uint64_t* pos, int64_t len, int64_t& out) -> hipError_t {
+        uint64_t cnt = 0;
+        uint32_t lastf = 0;
+        out = 0;
+        if (!len) return hipSuccess;
+        hipError_t x = hipMemcpyAsync(&cnt, pos + len - 1, sizeof(uint64_t), hipMemcpyDeviceToHost, s);
+        if (x == hipSuccess) x = hipMemcpyAsync(&lastf, flag + len - 1, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+        if (x == hipSuccess) x = hipStreamSynchronize(s);
+        out = static_cast<int64_t>(cnt + lastf);
+        return x;
+    };
+    // ---- owned entries of each direction, sorted by (row, neighbour) from edge order
+    ScopedBuf<uint64_t> k1[2];
+    ScopedBuf<uint32_t> v1[2];
+    ScopedBuf<int64_t> off[2], kept[2];
+    int64_t cnt[2] = {0, 0};
+    for (int d = 0; d < 2; ++d) {
+        const int32_t* own = d == 0 ? d_src.p : d_dst.p;
+        const int32_t* nbr = d == 0 ? d_dst.p : d_src.p;
+        ScopedBuf<uint32_t> flag;
+        ScopedBuf<uint64_t> pos;
+        AS_TRY(flag.alloc(m));
+        AS_TRY(pos.alloc(m + 1));
+        if (m) owned_flags<<<grid(m), kB, 0, s>>>(own, m, lo, hi, flag.p);
+        AS_TRY(so.excl_scan(flag.p, pos.p, m));
+        AS_TRY(count_of(flag.p, pos.p, m, cnt[d]));
+        ScopedBuf<uint64_t> kt;
+        ScopedBuf<uint32_t> vt;
+        AS_TRY(kt.alloc(cnt[d]));
+        AS_TRY(vt.alloc(cnt[d]));
+        if (m) owned_keys<<<grid(m), kB, 0, s>>>(own, nbr, flag.p, pos.p, m, lo, b, kt.p, vt.p);
+        AS_TRY(k1[d].alloc(cnt[d]));
+        AS_TRY(v1[d].alloc(cnt[d]));
+        if (cnt[d]) AS_TRY(so.pairs(kt.p, k1[d].p, vt.p, v1[d].p, cnt[d], bits));
+        AS_TRY(off[d].alloc(n + 1));
+        row_offsets<<<grid(n + 1), kB, 0, s>>>(k1[d].p, cnt[d], b, n, off[d].p);
+        AS_TRY(kept[d].alloc(n));
+        AS_TRY(hipStreamSynchronize(s));            // the scoped buffers are freed next
+    }
+    d_src.release();
+    d_dst.release();
+    lap("owned + sort 1");
+    // ---- the cut (OUT entries first, then IN, up to the limit per row)
+    unsigned long long truncated = 0;
+    {
+        ScopedBuf<unsigned long long> tr;
+        ScopedBuf<uint32_t> deg;
+        AS_TRY(tr.alloc(1));
+        AS_TRY(deg.alloc(n));
+        AS_TRY(hipMemsetAsync(tr.p, 0, sizeof(unsigned long long), s));
+        cap_rows<<<grid(n), kB, 0, s>>>(off[0].p, off[1].p, n, limit, kept[0].p, kept[1].p, deg.p, tr.p);
+        AS_TRY(hipMemcpyAsync(&truncated, tr.p, sizeof(truncated), hipMemcpyDeviceToHost, s));
+        AS_TRY(hipStreamSynchronize(s));
+    }
+    g.truncated = static_cast<int64_t>(truncated);
+    HostCsr* outc[2] = {&g.out, &g.in};
+    ScopedBuf<int32_t> fadj[2], fw[2];
+    int64_t fc[2] = {0, 0};
+    for (int d = 0; d < 2; ++d) {
+        // kept entries: keys in cut order, payload = edge index
+        ScopedBuf<uint64_t> kk;
+        ScopedBuf<uint32_t> ke;
+        if (truncated) {
+            ScopedBuf<uint32_t> flag, sel;
+            ScopedBuf<uint64_t> pos;
+            AS_TRY(flag.alloc(cnt[d]));
+            AS_TRY(pos.alloc(cnt[d] + 1));
+            if (cnt[d]) keep_flags<<<grid(cnt[d]), kB, 0, s>>>(k1[d].p, cnt[d], b, off[d].p, kept[d].p, nullptr, flag.p, nullptr);
+            AS_TRY(so.excl_scan(flag.p, pos.p, cnt[d]));
+            AS_TRY(count_of(flag.p, pos.p, cnt[d], fc[d]));
+            AS_TRY(kk.alloc(fc[d]));
+            AS_TRY(ke.alloc(fc[d]));
+            AS_TRY(sel.alloc(fc[d]));
+            if (cnt[d]) compact_kept<<<grid(cnt[d]), kB, 0, s>>>(k1[d].p, flag.p, pos.p, cnt[d], b, nullptr, kk.p, sel.p);
+            if (fc[d]) gather_i32<<<grid(fc[d]), kB, 0, s>>>(sel.p, reinterpret_cast<const int32_t*>(v1[d].p), fc[d],
+                                                          reinterpret_cast<int32_t*>(ke.p));
+            AS_TRY(hipStreamSynchronize(s));
+            k1[d].release();
+            v1[d].release();
+        } else {
+            fc[d] = cnt[d];
+            kk.p = k1[d].take();
+            kk.n = static_cast<size_t>(cnt[d]);
+            ke.p = v1[d].take();
+            ke.n = static_cast<size_t>(cnt[d]);
+        }
+        const int64_t c = fc[d];
+        // ---- layout: (layout row, layout neighbour), stable from the cut order
+        ScopedBuf<uint64_t> fkey;
+        ScopedBuf<uint32_t> fval;                    // payload: index into the cut order
+        if (layout) {
+            ScopedBuf<uint64_t> kt;
+            ScopedBuf<uint32_t> vt;
+            AS_TRY(kt.alloc(c));
+            AS_TRY(vt.alloc(c));
+            if (c) part_rekey<<<grid(c), kB, 0, s>>>(kk.p, c, b, d_lay.p, lo, kt.p, vt.p);
+            AS_TRY(fkey.alloc(c));
+            AS_TRY(fval.alloc(c));
+            if (c) AS_TRY(so.pairs(kt.p, fkey.p, vt.p, fval.p, c, bits));
+            AS_TRY(hipStreamSynchronize(s));
+            kk.release();
+        } else {
+            fkey.p = kk.take();
+            fkey.n = static_cast<size_t>(c);
+        }
+        ScopedBuf<int64_t> foff;
+        AS_TRY(foff.alloc(n + 1));
+        row_offsets<<<grid(n + 1), kB, 0, s>>>(fkey.p, c, b, n, foff.p);
+        AS_TRY(fadj[d].alloc(c));
+        if (g.has_weight) AS_TRY(fw[d].alloc(c));
+        if (c)
+            emit_list<<<grid(c), kB, 0, s>>>(fkey.p, layout ? fval.p : nullptr, c, b, layout ? ke.p : nullptr, d_w.p,
+                                             nullptr, fadj[d].p, nullptr, nullptr);
+        if (c && g.has_weight) {
+            // weights through the payload chain: entry -> cut index (fval, with a layout) -> edge index
+            ScopedBuf<uint32_t> eidx;
+            AS_TRY(eidx.alloc(c));
+            if (layout) gather_i32<<<grid(c), kB, 0, s>>>(fval.p, reinterpret_cast<const int32_t*>(ke.p), c,
+                                                          reinterpret_cast<int32_t*>(eidx.p));
+            gather_i32<<<grid(c), kB, 0, s>>>(layout ? eidx.p : ke.p, d_w.p, c, fw[d].p);
+            AS_TRY(hipStreamSynchronize(s));
+        }
+        HostCsr& hc = *outc[d];
+        AS_TRY(download(hc.off, foff.p, n + 1, s));
+        if (g.has_weight) {                          // weight_sorted_push reads the host lists
+            AS_TRY(download(hc.adj, fadj[d].p, c, s));
+            AS_TRY(download(hc.w, fw[d].p, c, s));
+        }
+        AS_TRY(hipStreamSynchronize(s));
+        lap(d == 0 ? "OUT" : "IN");
+    }
+    g.has_transpose = false;
+    for (int d = 0; d < 2; ++d) {
+        outc[d]->dadj.own(fadj[d].take(), fc[d]);
+        if (g.has_weight) outc[d]->dw.own(fw[d].take(), fc[d]);
+    }
+    return TGO_OK;
+}
 
 int stage_csr_device(const CsrInput& in, bool weighted, RowStaging& st, hipStream_t s, std::string& err) {
     const int64_t n = in.n;

@@ -229,6 +229,9 @@ int partition_layout(const tgo_edges* e, int64_t n_global, int64_t lo, int64_t h
 int assemble_partition(const tgo_edges* e, int64_t n_global, int64_t lo, int64_t hi,
                        const tgo_load_opts* opts, int64_t hard_limit, const int32_t* layout, HostGraph& g,
                        int threads, std::string& err);
+// assemble_partition on the device (assemble.hip), array for array; m < 2^32.
+int assemble_partition_device(const tgo_edges* e, int64_t n_global, int64_t lo, int64_t hi, const tgo_load_opts* opts,
+                              int64_t hard_limit, const int32_t* layout, HostGraph& g, hipStream_t s, std::string& err);
 
 // ---------------------------------------------------------------- device graph
 struct DevCsr {
@@ -329,6 +332,8 @@ int build_cold_blocks_device(const int64_t* d_off, const int32_t* d_adj, int64_t
                              bool& built, hipStream_t s, std::string& err);
 int pack_tiles_device(int32_t* d_adj, int64_t m, const std::vector<int64_t>& tstart, const std::vector<int32_t>* tbase,
                       int shift, hipStream_t s, std::string& err);
+hipError_t k_part_gathered_index(const int32_t* in, int64_t m, int64_t nl, int64_t A, int64_t H, int64_t W, int32_t* out,
+                                 int* bad, hipStream_t s);
 
 struct DevGraph {
     int64_t n = 0;

@@ -353,4 +353,24 @@ int build_cold_blocks_device(const int64_t* d_off, const int32_t* d_adj, int64_t
     return TGO_OK;
 }
 
+// Partitioned PageRank (tgo_part_pr_blocked): every in-list source u (global slot id, rank
+// r = u / nl, offset o = u % nl) to its position in the blocked gathered vector — rank-major
+// hot slices [0, H) first, then the cold slices [H, A); a source past A sets *bad.
+__global__ void part_gathered_index(const int32_t* __restrict__ in, int64_t m, int64_t nl, int64_t A, int64_t H,
+                                    int64_t W, int32_t* __restrict__ out, int* __restrict__ bad) {
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t u = in[k], r = u / nl, o = u % nl;
+        if (o >= A) { *bad = 1; out[k] = 0; continue; }
+        out[k] = static_cast<int32_t>(o < H ? r * H + o : W * H + r * (A - H) + (o - H));
+    }
+}
+hipError_t k_part_gathered_index(const int32_t* in, int64_t m, int64_t nl, int64_t A, int64_t H, int64_t W, int32_t* out,
+                                 int* bad, hipStream_t s) {
+    if (m > 0) {
+        const unsigned g = static_cast<unsigned>(std::min<int64_t>((m + 255) / 256, 65536));
+        part_gathered_index<<<g, 256, 0, s>>>(in, m, nl, A, H, W, out, bad);
+    }
+    return hipGetLastError();
+}
+
 }  // namespace tgo

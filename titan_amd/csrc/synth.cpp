@@ -16,8 +16,11 @@ inline uint64_t splitmix64(uint64_t x) {
     return x ^ (x >> 31);
 }
 
-// Seeded permutation of [0, n) (Fisher-Yates driven by splitmix64).
-std::vector<int32_t> relabel(int64_t n, uint64_t seed) {
+}  // namespace
+
+namespace tgo {
+// Seeded permutation of [0, n) (Fisher-Yates driven by splitmix64); rmat_dev.hip uses it too.
+std::vector<int32_t> rmat_relabel(int64_t n, uint64_t seed) {
     std::vector<int32_t> p(n);
     for (int64_t i = 0; i < n; ++i) p[i] = static_cast<int32_t>(i);
     for (int64_t i = n - 1; i > 0; --i) {
@@ -27,8 +30,8 @@ std::vector<int32_t> relabel(int64_t n, uint64_t seed) {
     }
     return p;
 }
-
-}  // namespace
+}  // namespace tgo
+using tgo::rmat_relabel;
 
 static void rmat_range(int32_t scale, uint64_t seed, int64_t edge_begin, int64_t count,
                        const std::vector<int32_t>& perm, int32_t* src, int32_t* dst, int32_t* weight,
@@ -72,7 +75,7 @@ static int clamp_threads(int threads) {
 extern "C" int tgo_rmat_edges(int32_t scale, int32_t edge_factor, uint64_t seed, int64_t edge_begin,
                               int64_t count, int32_t* src, int32_t* dst, int32_t* weight, int32_t threads) {
     if (scale < 1 || scale > 30 || edge_factor < 1 || count < 0 || !src || !dst) return TGO_E_INVALID;
-    const std::vector<int32_t> perm = relabel(int64_t(1) << scale, seed ^ 0x5EED5EEDULL);
+    const std::vector<int32_t> perm = rmat_relabel(int64_t(1) << scale, seed ^ 0x5EED5EEDULL);
     rmat_range(scale, seed, edge_begin, count, perm, src, dst, weight, clamp_threads(threads));
     return TGO_OK;
 }
@@ -82,7 +85,7 @@ extern "C" int tgo_rmat_partition(int32_t scale, int32_t edge_factor, uint64_t s
                                   int64_t* count, int32_t threads) {
     if (scale < 1 || scale > 30 || edge_factor < 1 || !count || lo < 0 || hi <= lo) return TGO_E_INVALID;
     threads = clamp_threads(threads);
-    const std::vector<int32_t> perm = relabel(int64_t(1) << scale, seed ^ 0x5EED5EEDULL);
+    const std::vector<int32_t> perm = rmat_relabel(int64_t(1) << scale, seed ^ 0x5EED5EEDULL);
     const int64_t m = static_cast<int64_t>(edge_factor) << scale;
     const int64_t chunk = int64_t(1) << 24;
     std::vector<int32_t> s(chunk), d(chunk), w(weight ? chunk : 0);

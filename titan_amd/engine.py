@@ -366,15 +366,20 @@ class Engine:
         _check(self.lib, self.ctx, self.lib.tgo_sync(self.ctx))
 
 
-def rmat_edges(scale, edge_factor=16, seed=0x54495441, weights=False, threads=0):
-    """Synthetic RMAT edge list (include/tgo_synth.h)."""
+def rmat_edges(scale, edge_factor=16, seed=0x54495441, weights=False, threads=0, device=None):
+    """Synthetic RMAT edge list (include/tgo_synth.h); device=k generates the same stream on
+    GPU k (tgo_rmat_edges_device)."""
     lib = L.load()
     m = edge_factor << scale
     src = np.empty(m, dtype=np.int32)
     dst = np.empty(m, dtype=np.int32)
     w = np.empty(m, dtype=np.int32) if weights else None
-    rc = lib.tgo_rmat_edges(scale, edge_factor, seed, 0, m, L.ptr(src, C.c_int32), L.ptr(dst, C.c_int32),
-                            L.ptr(w, C.c_int32), threads)
+    if device is not None:
+        rc = lib.tgo_rmat_edges_device(scale, edge_factor, seed, 0, m, L.ptr(src, C.c_int32), L.ptr(dst, C.c_int32),
+                                       L.ptr(w, C.c_int32), int(device))
+    else:
+        rc = lib.tgo_rmat_edges(scale, edge_factor, seed, 0, m, L.ptr(src, C.c_int32), L.ptr(dst, C.c_int32),
+                                L.ptr(w, C.c_int32), threads)
     if rc:
         raise TitanException(rc, "tgo_rmat_edges failed")
     return src, dst, w
