@@ -72,6 +72,33 @@ def test_partitioned_delta_stepping(world, scope, layout):
             assert len({x[2] for x in res}) == 1                  # every rank ran the same phases
 
 
+@pytest.mark.parametrize("layout", [False, True])
+@pytest.mark.parametrize("world,scope", [(2, L.SCOPE_IN_E), (4, L.SCOPE_IN_E), (3, L.SCOPE_OUT_E)])
+def test_partitioned_delta_stepping_capped(world, scope, layout):
+    """Capped single-direction scopes (QueryContainer.java:28,122 at a small limit): a vertex
+    pushes to v only if it survived in v's cut pull list, and v may live on another rank — the
+    partition load builds its push rows from the global cut (the one-GPU load's explicit
+    transpose).  Weighted delta-stepping equals the oracle's converged distances bit for bit.
+    (Found at RMAT-24 with the real 100 000 cap: a hub's own IN list, cut after its OUT
+    entries, missed pushes its receivers' uncut OUT lists hold.)"""
+    scale = 12
+    n = 1 << scale
+    limit = 40
+    src, dst, w = rmat_edges(scale, 16, seed=39, weights=True)
+    if world == 3:
+        n = 3 * 1408                                  # 64-aligned equal thirds past the RMAT range
+    ranks = Ranks(world, n, src, dst, scope, weight=w, layout=layout, apply_cap=True, hard_limit=limit)
+    og = fr.OracleGraph.from_edges(n, src, dst, w, hard_limit=limit)
+    assert sum(be.e.stats()["truncated_results"] for be in ranks.backends) == og.stats.truncated_results > 0
+    ids = (np.arange(n, dtype=np.int64) + 1) << 3
+    deg = np.bincount(src, minlength=n) + np.bincount(dst, minlength=n)
+    for seed in (int(np.argmax(deg)), int(src[3]), int(dst[11])):
+        od, _ = og.shortest_distance(int(ids[seed]), n, scope, weighted=True)
+        res = ranks.run(lambda be, comm: distributed_sssp(be, seed, 0, comm=comm))
+        assert np.array_equal(np.concatenate([x[0] for x in res]), od), seed
+        assert all(x[1][0] == int((od != ABSENT).sum()) for x in res)
+
+
 @pytest.mark.parametrize("device_counts", [False, True])
 @pytest.mark.parametrize("layout", [False, True])
 @pytest.mark.parametrize("world", [2, 4])

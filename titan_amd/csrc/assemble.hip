@@ -308,6 +308,71 @@ __global__ void part_rekey(const uint64_t* __restrict__ key, int64_t m, int b, c
     }
 }
 
+// Global degrees of a partition load's edge list (every row, owned or not).
+__global__ void degree_both(const int32_t* __restrict__ src, const int32_t* __restrict__ dst, int64_t m,
+                            uint32_t* __restrict__ dout, uint32_t* __restrict__ din) {
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x) {
+        atomicAdd(&dout[src[k]], 1u);
+        atomicAdd(&din[dst[k]], 1u);
+    }
+}
+// Kept entries of every global pull row under the cut (OUT entries first, QueryContainer
+// limit): pull = OUT (inE scope) keeps min(out, limit); pull = IN (outE) keeps
+// min(in, limit - min(out, limit)).  drops[0] = 1 when some row loses entries.
+__global__ void pull_kept(const uint32_t* __restrict__ dout, const uint32_t* __restrict__ din, int64_t n, int64_t limit,
+                          int pull_out, uint32_t* __restrict__ kept, int* __restrict__ drops) {
+    for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t a = dout[v], b = din[v];
+        if (a + b > limit) *drops = 1;
+        const int64_t ka = a < limit ? a : limit;
+        const int64_t kb = b < limit - ka ? b : limit - ka;
+        kept[v] = static_cast<uint32_t>(pull_out ? ka : kb);
+    }
+}
+// Edges of the pull rows that lose entries (kept < row length): flag for the compaction.
+__global__ void cut_row_flags(const int32_t* __restrict__ prow, int64_t m, const uint32_t* __restrict__ kept,
+                              const uint32_t* __restrict__ dlen, uint32_t* __restrict__ flag) {
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t v = prow[k];
+        flag[k] = kept[v] < dlen[v] ? 1u : 0u;
+    }
+}
+// Sorted (pull row, neighbour) entries of the cut rows: entry j of row v is dropped when
+// j >= kept[v]; mark its edge.
+__global__ void mark_dropped(const uint64_t* __restrict__ key, const uint32_t* __restrict__ eidx, int64_t c, int b,
+                             const uint32_t* __restrict__ kept, uint8_t* __restrict__ dropped) {
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < c; k += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t v = key[k] >> b;
+        // first entry of the row: binary search for the first key >= v << b
+        int64_t lo = 0, hi = k;
+        const uint64_t t = v << b;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (key[mid] < t) lo = mid + 1; else hi = mid;
+        }
+        if (k - lo >= static_cast<int64_t>(kept[v])) dropped[eidx[k]] = 1;
+    }
+}
+// Push entries of the owned push rows (the pull neighbour in [lo, hi)), kept edges only.
+__global__ void push_flags(const int32_t* __restrict__ pn, int64_t m, int64_t lo, int64_t hi,
+                           const uint8_t* __restrict__ dropped, uint32_t* __restrict__ flag) {
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x)
+        flag[k] = (pn[k] >= lo && pn[k] < hi && !dropped[k]) ? 1u : 0u;
+}
+// key = (push row, through the layout) << b | (pull row, through the layout), payload = edge.
+__global__ void push_keys(const int32_t* __restrict__ pn, const int32_t* __restrict__ pr, const uint32_t* __restrict__ flag,
+                          const uint64_t* __restrict__ pos, int64_t m, int64_t lo, int b, const int32_t* __restrict__ layout,
+                          uint64_t* __restrict__ key, uint32_t* __restrict__ val) {
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x) {
+        if (!flag[k]) continue;
+        const uint64_t p = pos[k];
+        const int64_t row = layout ? static_cast<int64_t>(layout[pn[k]]) - lo : static_cast<int64_t>(pn[k]) - lo;
+        const uint32_t t = static_cast<uint32_t>(layout ? layout[pr[k]] : pr[k]);
+        key[p] = (static_cast<uint64_t>(row) << b) | t;
+        val[p] = static_cast<uint32_t>(k);
+    }
+}
+
 struct Sorter {
     ScopedBuf<uint8_t> tmp;
     hipStream_t s;
@@ -712,8 +777,6 @@ int assemble_partition_device(const tgo_edges* e, int64_t n_global, int64_t lo, 
         AS_TRY(kept[d].alloc(n));
         AS_TRY(hipStreamSynchronize(s));            // the scoped buffers are freed next
     }
-    d_src.release();
-    d_dst.release();
     lap("owned + sort 1");
     // ---- the cut (OUT entries first, then IN, up to the limit per row)
     unsigned long long truncated = 0;
@@ -805,6 +868,85 @@ int assemble_partition_device(const tgo_edges* e, int64_t n_global, int64_t lo, 
         lap(d == 0 ? "OUT" : "IN");
     }
     g.has_transpose = false;
+    // ---- push view of a cut single-direction scope: the pull lists of EVERY rank decide which
+    // entries a vertex pushes along (u pushes to v iff u survived in v's cut pull list), so the
+    // owned push rows come from the global cut, not from the owned rows' own cut opposite lists
+    // (the one-GPU load's explicit transpose, partitioned)
+    if (cap && m) {
+        const bool pull_out = opts->scope == TGO_SCOPE_IN_E;        // inE pulls over OUT entries
+        const int32_t* prow = pull_out ? d_src.p : d_dst.p;          // pull row (receiver)
+        const int32_t* pnbr = pull_out ? d_dst.p : d_src.p;          // pull neighbour (pusher)
+        ScopedBuf<uint32_t> dout, din, kept_g;
+        ScopedBuf<int> drops;
+        AS_TRY(dout.alloc(n_global));
+        AS_TRY(din.alloc(n_global));
+        AS_TRY(kept_g.alloc(n_global));
+        AS_TRY(drops.alloc(1));
+        AS_TRY(hipMemsetAsync(dout.p, 0, n_global * 4, s));
+        AS_TRY(hipMemsetAsync(din.p, 0, n_global * 4, s));
+        AS_TRY(hipMemsetAsync(drops.p, 0, sizeof(int), s));
+        degree_both<<<grid(m), kB, 0, s>>>(d_src.p, d_dst.p, m, dout.p, din.p);
+        pull_kept<<<grid(n_global), kB, 0, s>>>(dout.p, din.p, n_global, limit, pull_out ? 1 : 0, kept_g.p, drops.p);
+        int any = 0;
+        AS_TRY(hipMemcpyAsync(&any, drops.p, sizeof(int), hipMemcpyDeviceToHost, s));
+        AS_TRY(hipStreamSynchronize(s));
+        if (any) {
+            ScopedBuf<uint8_t> dropped;
+            AS_TRY(dropped.alloc(m));
+            AS_TRY(hipMemsetAsync(dropped.p, 0, m, s));
+            {   // rank of every entry of the cut rows in its row's column order (neighbour, edge)
+                ScopedBuf<uint32_t> flag;
+                ScopedBuf<uint64_t> pos;
+                AS_TRY(flag.alloc(m));
+                AS_TRY(pos.alloc(m + 1));
+                cut_row_flags<<<grid(m), kB, 0, s>>>(prow, m, kept_g.p, pull_out ? dout.p : din.p, flag.p);
+                AS_TRY(so.excl_scan(flag.p, pos.p, m));
+                int64_t c = 0;
+                AS_TRY(count_of(flag.p, pos.p, m, c));
+                ScopedBuf<uint64_t> kt, ks;
+                ScopedBuf<uint32_t> vt, vs;
+                AS_TRY(kt.alloc(c)); AS_TRY(vt.alloc(c)); AS_TRY(ks.alloc(c)); AS_TRY(vs.alloc(c));
+                // the cut rows' entries: key = row << b | neighbour (the owned_keys layout, lo = 0)
+                owned_keys<<<grid(m), kB, 0, s>>>(prow, pnbr, flag.p, pos.p, m, 0, b, kt.p, vt.p);
+                int bg = 1;
+                while ((int64_t(1) << bg) < n_global) ++bg;
+                if (c) AS_TRY(so.pairs(kt.p, ks.p, vt.p, vs.p, c, b + bg));
+                if (c) mark_dropped<<<grid(c), kB, 0, s>>>(ks.p, vs.p, c, b, kept_g.p, dropped.p);
+                AS_TRY(hipStreamSynchronize(s));
+            }
+            ScopedBuf<uint32_t> flag;
+            ScopedBuf<uint64_t> pos;
+            AS_TRY(flag.alloc(m));
+            AS_TRY(pos.alloc(m + 1));
+            push_flags<<<grid(m), kB, 0, s>>>(pnbr, m, lo, hi, dropped.p, flag.p);
+            AS_TRY(so.excl_scan(flag.p, pos.p, m));
+            int64_t c = 0;
+            AS_TRY(count_of(flag.p, pos.p, m, c));
+            ScopedBuf<uint64_t> kt, ks;
+            ScopedBuf<uint32_t> vt, vs;
+            AS_TRY(kt.alloc(c)); AS_TRY(vt.alloc(c)); AS_TRY(ks.alloc(c)); AS_TRY(vs.alloc(c));
+            push_keys<<<grid(m), kB, 0, s>>>(pnbr, prow, flag.p, pos.p, m, lo, b, layout ? d_lay.p : nullptr, kt.p, vt.p);
+            if (c) AS_TRY(so.pairs(kt.p, ks.p, vt.p, vs.p, c, bits));
+            ScopedBuf<int64_t> poff;
+            AS_TRY(poff.alloc(n + 1));
+            row_offsets<<<grid(n + 1), kB, 0, s>>>(ks.p, c, b, n, poff.p);
+            ScopedBuf<int32_t> padj, pw;
+            AS_TRY(padj.alloc(c));
+            if (g.has_weight) AS_TRY(pw.alloc(c));
+            if (c) emit_list<<<grid(c), kB, 0, s>>>(ks.p, vs.p, c, b, nullptr, d_w.p, nullptr, padj.p,
+                                                    g.has_weight ? pw.p : nullptr, nullptr);
+            AS_TRY(download(g.push_t.off, poff.p, n + 1, s));
+            if (g.has_weight) {
+                AS_TRY(download(g.push_t.adj, padj.p, c, s));
+                AS_TRY(download(g.push_t.w, pw.p, c, s));
+            }
+            AS_TRY(hipStreamSynchronize(s));
+            g.push_t.dadj.own(padj.take(), c);
+            if (g.has_weight) g.push_t.dw.own(pw.take(), c);
+            g.has_transpose = true;
+            lap("push transpose");
+        }
+    }
     for (int d = 0; d < 2; ++d) {
         outc[d]->dadj.own(fadj[d].take(), fc[d]);
         if (g.has_weight) outc[d]->dw.own(fw[d].take(), fc[d]);

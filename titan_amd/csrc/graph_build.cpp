@@ -5,6 +5,7 @@
 // VertexJobConverter.java:109-129, rebuilds a PreloadedVertex per row per superstep).
 // Here the rows are decoded once into an out-CSR and an in-CSR of dense vertex ids.
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -875,6 +876,51 @@ int assemble_partition(const tgo_edges* e, int64_t n_global, int64_t lo, int64_t
             g.perm[v] = static_cast<int32_t>(p);
         }
         permute_graph(g, [layout](int32_t u) { return layout[u]; }, threads);
+    }
+    // push view of a cut single-direction scope (assemble_partition_device): u pushes to v iff
+    // u survived in v's cut pull list, whichever rank owns v
+    if (cap && m) {
+        const bool pull_out = opts->scope == TGO_SCOPE_IN_E;
+        const int32_t* prow = pull_out ? e->src : e->dst;
+        const int32_t* pnbr = pull_out ? e->dst : e->src;
+        std::vector<int64_t> dout(n_global, 0), din(n_global, 0);
+        for (int64_t k = 0; k < m; ++k) { ++dout[e->src[k]]; ++din[e->dst[k]]; }
+        std::vector<int64_t> kept(n_global);
+        bool any = false;
+        for (int64_t v = 0; v < n_global; ++v) {
+            const int64_t a = dout[v], b = din[v];
+            any = any || a + b > limit;
+            const int64_t ka = std::min(a, limit);
+            kept[v] = pull_out ? ka : std::min(b, limit - ka);
+        }
+        if (any) {
+            const std::vector<int64_t>& len = pull_out ? dout : din;
+            std::vector<uint8_t> dropped(m, 0);
+            std::vector<std::array<int64_t, 3>> cut;       // (pull row, neighbour, edge) of the cut rows
+            for (int64_t k = 0; k < m; ++k)
+                if (kept[prow[k]] < len[prow[k]]) cut.push_back({prow[k], pnbr[k], k});
+            std::sort(cut.begin(), cut.end());
+            for (size_t i = 0, j = 0; i < cut.size(); ++i) {
+                j = (i > 0 && cut[i][0] == cut[i - 1][0]) ? j + 1 : 0;
+                if (static_cast<int64_t>(j) >= kept[cut[i][0]]) dropped[cut[i][2]] = 1;
+            }
+            std::vector<std::array<int64_t, 3>> push;      // (push row, target, edge), layout ids
+            for (int64_t k = 0; k < m; ++k)
+                if (pnbr[k] >= lo && pnbr[k] < hi && !dropped[k])
+                    push.push_back({layout ? layout[pnbr[k]] - lo : pnbr[k] - lo, layout ? layout[prow[k]] : prow[k], k});
+            std::sort(push.begin(), push.end());
+            HostCsr& pt = g.push_t;
+            pt.off.assign(n + 1, 0);
+            pt.adj.resize(push.size());
+            if (g.has_weight) pt.w.resize(push.size());
+            for (size_t i = 0; i < push.size(); ++i) {
+                ++pt.off[push[i][0] + 1];
+                pt.adj[i] = static_cast<int32_t>(push[i][1]);
+                if (g.has_weight) pt.w[i] = e->weight[push[i][2]];
+            }
+            for (int64_t v = 0; v < n; ++v) pt.off[v + 1] += pt.off[v];
+            g.has_transpose = true;
+        }
     }
     return TGO_OK;
 }
