@@ -209,6 +209,34 @@ const char* tgo_exchange_last_error(const tgo_exchange* x);
 int  tgo_part_msbfs_run(tgo_ctx* ctx, tgo_exchange* x, const int64_t* seeds, int32_t nseeds, int32_t max_depth,
                         double ms_alpha, int64_t fixed_bytes, int64_t* reached, int64_t* entries, int32_t* levels);
 
+/* The other partitioned programs as ONE native call each (part_driver.cpp), same exchange
+ * objects and preconditions as tgo_part_msbfs_run; outputs are host arrays, results equal the
+ * Python drivers' (titan_amd/distributed.py) and the one-GPU programs':
+ *   tgo_part_bfs_run      ShortestDistance with unit weights over bothE from global seed
+ *                         (distributed_bfs): direction-optimizing levels (alpha / beta as
+ *                         tgo_bfs), top-down = discovered-bitmap all-to-all + claim, bottom-up
+ *                         = owned frontier slices all-gathered; dist_local = the owned
+ *                         distances in row order (NULL to skip), reached = global {vertices,
+ *                         entries} (NULL to skip), *levels = levels run.
+ *   tgo_part_sssp_run     delta-stepping ShortestDistance (distributed_sssp): per phase a
+ *                         relax, an all-to-all of the pair counts and an all-to-allv of the
+ *                         (owner-local id, distance) pairs; an all-reduce(MIN) of the pending
+ *                         minimum moves the bucket.  delta <= 0: the maximum of the ranks'
+ *                         default widths.  *phases = relax phases run.
+ *   tgo_part_pagerank_run PageRankVertexProgram (distributed_pagerank): layout agreed with an
+ *                         all-reduce(MAX) of the active rows, tgo_part_pr_blocked, then per
+ *                         update the gathered vector refreshed by exchange_mode 0 = all-gather
+ *                         of every rank's slices, 1 = ghost exchange: only the contributions
+ *                         this rank's in-lists read (lists built once per layout and kept with
+ *                         the graph; pack -> all-to-allv -> unpack).  pr_local = owned ranks in
+ *                         row order; *exchanged_bytes = bytes this rank received over the run. */
+int  tgo_part_bfs_run(tgo_ctx* ctx, tgo_exchange* x, int64_t seed_global, int32_t max_depth, double alpha, double beta,
+                      int64_t* dist_local, int64_t* reached, int32_t* levels);
+int  tgo_part_sssp_run(tgo_ctx* ctx, tgo_exchange* x, int64_t seed_global, int64_t delta, int64_t* dist_local,
+                       int64_t* reached, int32_t* phases);
+int  tgo_part_pagerank_run(tgo_ctx* ctx, tgo_exchange* x, const tgo_pr_args* args, int32_t exchange_mode,
+                           double* pr_local, int64_t* exchanged_bytes);
+
 /* Bench / test input: the edges of an RMAT stream (tgo_synth.h) with an endpoint in
  * [lo, hi).  *count = edges written; if capacity is too small, nothing is written,
  * *count = required capacity and TGO_E_INVALID is returned. */

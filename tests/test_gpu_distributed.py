@@ -438,3 +438,86 @@ def test_native_msbfs_rejects_a_mismatched_exchange():
         xs = NativeExchange.local_group(2)          # world 2 against a one-rank partition
         with pytest.raises(TitanException):
             distributed_msbfs_native(be, [int(src[0])], n, xs[0])
+
+
+@pytest.mark.parametrize("world", [1, 2, 4])
+def test_native_bfs_sssp_pagerank_drivers(world, monkeypatch):
+    """tgo_part_bfs_run / tgo_part_sssp_run / tgo_part_pagerank_run: each partitioned program
+    as ONE native call over an in-process exchange group — BFS and capped weighted SSSP
+    bit-exact against the oracle and equal to the Python drivers, capped cache-blocked
+    PageRank within 1e-6 L1 of the oracle and bitwise equal across the all-gather and the
+    ghost exchange (which moves fewer bytes whenever there is more than one rank)."""
+    from titan_amd.distributed import (NativeExchange, PR_EXCHANGE_ALLGATHER, PR_EXCHANGE_GHOST, distributed_bfs_native,
+                                       distributed_pagerank_native, distributed_sssp_native)
+    monkeypatch.setenv("TGO_PR_HOT", "512")
+    monkeypatch.setenv("TGO_PR_SEG", "256")
+    scale = 12
+    n = 1 << scale
+    src, dst, w = rmat_edges(scale, 16, seed=57, weights=True)
+    ids = (np.arange(n, dtype=np.int64) + 1) << 3
+    og = fr.OracleGraph.from_edges(n, src, dst)
+    seeds = [int(src[0]), int(dst[5]), int(src[900])]
+    bfs = Ranks(world, n, src, dst, L.SCOPE_BOTH_E, layout=True, device_counts=True)
+    xs = NativeExchange.local_group(world)
+    for seed in seeds:
+        od, _ = og.shortest_distance(int(ids[seed]), n, 2)
+        for alpha in (15.0, 1e9):
+            res = bfs.run(lambda be, comm: distributed_bfs_native(be, seed, n, xs[comm.rank], alpha=alpha))
+            assert np.array_equal(np.concatenate([x[0] for x in res]), od), (seed, alpha)
+            assert all(x[1][0] == int((od != ABSENT).sum()) for x in res)
+            py = bfs.run(lambda be, comm: distributed_bfs(be, seed, n, alpha=alpha, comm=comm))
+            assert res[0][2] == py[0][2]                      # same levels
+    limit = 40
+    sp = Ranks(world, n, src, dst, L.SCOPE_IN_E, weight=w, layout=True, apply_cap=True, hard_limit=limit)
+    ogc = fr.OracleGraph.from_edges(n, src, dst, w, hard_limit=limit)
+    for seed in seeds:
+        od, _ = ogc.shortest_distance(int(ids[seed]), n, L.SCOPE_IN_E, weighted=True)
+        res = sp.run(lambda be, comm: distributed_sssp_native(be, seed, xs[comm.rank]))
+        assert np.array_equal(np.concatenate([x[0] for x in res]), od), seed
+        assert all(x[1][0] == int((od != ABSENT).sum()) for x in res)
+        py = sp.run(lambda be, comm: distributed_sssp(be, seed, 0, comm=comm))
+        assert res[0][2] == py[0][2]                          # same phases
+    pr = Ranks(world, n, src, dst, L.SCOPE_IN_E, layout=True, apply_cap=True, hard_limit=limit)
+    opr, _ = fr.OracleGraph.from_edges(n, src, dst, hard_limit=limit).pagerank(0.85, n, 15)
+    fin = np.isfinite(opr)
+    got = {}
+    for mode in (PR_EXCHANGE_ALLGATHER, PR_EXCHANGE_GHOST):
+        res = pr.run(lambda be, comm: distributed_pagerank_native(be, 0.85, n, 15, xs[comm.rank], mode=mode))
+        got[mode] = (np.concatenate([x[0] for x in res]), sum(x[1] for x in res))
+        assert np.array_equal(np.isfinite(got[mode][0]), fin)
+        assert np.abs(got[mode][0][fin] - opr[fin]).sum() <= 1e-6
+    assert np.array_equal(got[0][0], got[1][0])
+    if world > 1:
+        assert 0 < got[PR_EXCHANGE_GHOST][1] < got[PR_EXCHANGE_ALLGATHER][1]
+    py = pr.run(lambda be, comm: distributed_pagerank(be, 0.85, n, 15, comm=comm))
+    assert np.array_equal(np.concatenate(py), got[0][0])
+
+
+def test_native_drivers_rccl_world1():
+    """The three native loops over the RCCL exchange (one rank)."""
+    from titan_amd.distributed import (NativeExchange, distributed_bfs_native, distributed_pagerank_native,
+                                       distributed_sssp_native)
+    scale = 11
+    n = 1 << scale
+    src, dst, w = rmat_edges(scale, 16, seed=59, weights=True)
+    ids = (np.arange(n, dtype=np.int64) + 1) << 3
+    st = torch.cuda.Stream()
+    with torch.cuda.stream(st):
+        x = NativeExchange.rccl(0, comm=InProcessGroup(1).comm(0))
+        be = HipPartBackend(Engine(stream=st.cuda_stream).load_partition(n, 0, n, src, dst, L.SCOPE_BOTH_E,
+                                                                         apply_cap=False), n, 0, n)
+        og = fr.OracleGraph.from_edges(n, src, dst, w)
+        seed = int(src[0])
+        d, r, _ = distributed_bfs_native(be, seed, n, x)
+        od, _ = og.shortest_distance(int(ids[seed]), n, 2)
+        assert np.array_equal(d, od) and r[0] == int((od != ABSENT).sum())
+        wb = HipPartBackend(Engine(stream=st.cuda_stream).load_partition(n, 0, n, src, dst, L.SCOPE_IN_E, weight=w,
+                                                                         apply_cap=False), n, 0, n)
+        d, r, _ = distributed_sssp_native(wb, seed, x)
+        od, _ = og.shortest_distance(int(ids[seed]), n, L.SCOPE_IN_E, weighted=True)
+        assert np.array_equal(d, od)
+        p, _ = distributed_pagerank_native(wb, 0.85, n, 10, x)
+        opr, _ = og.pagerank(0.85, n, 10)
+        fin = np.isfinite(opr)
+        assert np.abs(p[fin] - opr[fin]).sum() <= 1e-6
+        del x

@@ -154,7 +154,7 @@ EXPORTS = [
     "tgo_part_ms_levels", "tgo_part_sssp_begin", "tgo_part_sssp_relax", "tgo_part_sssp_apply",
     "tgo_part_sssp_pending_min", "tgo_part_sssp_extract", "tgo_part_sssp_end",
     "tgo_exchange_rccl_id", "tgo_exchange_rccl_create", "tgo_exchange_local_group", "tgo_exchange_destroy",
-    "tgo_exchange_last_error", "tgo_part_msbfs_run",
+    "tgo_exchange_last_error", "tgo_part_msbfs_run", "tgo_part_bfs_run", "tgo_part_sssp_run", "tgo_part_pagerank_run",
 ]
 
 _lib = None
@@ -265,6 +265,10 @@ def load() -> C.CDLL:
         "tgo_exchange_last_error": (C.c_char_p, [vp]),
         "tgo_part_msbfs_run": (C.c_int, [vp, vp, _i64p, C.c_int32, C.c_int32, C.c_double, C.c_int64, _i64p, _i64p,
                                          P(C.c_int32)]),
+        "tgo_part_bfs_run": (C.c_int, [vp, vp, C.c_int64, C.c_int32, C.c_double, C.c_double, _i64p, _i64p,
+                                       P(C.c_int32)]),
+        "tgo_part_sssp_run": (C.c_int, [vp, vp, C.c_int64, C.c_int64, _i64p, _i64p, P(C.c_int32)]),
+        "tgo_part_pagerank_run": (C.c_int, [vp, vp, P(PrArgs), C.c_int32, C.POINTER(C.c_double), _i64p]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

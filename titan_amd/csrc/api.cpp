@@ -5,6 +5,7 @@
 // each iteration is one or two kernel launches over the device-resident adjacency, and
 // only the frontier is touched for BFS/SSSP.
 #include <algorithm>
+#include <memory>
 #include <numeric>
 #include <atomic>
 #include <chrono>
@@ -66,6 +67,9 @@ struct tgo_ctx {
     ResultSource res_src;
     int num_cus = 256;          // compute units of the device (persistent launches)
     double ms_split = -1.0;     // tgo_set_tuning(TGO_TUNE_MS_SPLIT); < 0: TGO_MS_SPLIT / the default
+    // state a native partitioned driver keeps between runs on this graph (part_driver.cpp:
+    // the PageRank ghost lists); dropped with the graph
+    std::shared_ptr<void> part_state;
 };
 
 namespace {
@@ -134,6 +138,7 @@ void free_graph(tgo_ctx* ctx) {
     ctx->sc = keep;
     ctx->loaded = false;
     ctx->res_kind = -1;         // the last program's results lived in the freed scratch
+    ctx->part_state.reset();
 }
 
 int threads_of(const tgo_ctx* ctx) {
@@ -2732,6 +2737,22 @@ namespace tgo {
 hipStream_t part_stream(tgo_ctx* ctx) { return ctx->stream; }
 int part_fail(tgo_ctx* ctx, int code, const std::string& msg) { return fail(ctx, code, msg); }
 int64_t* part_dcounts_of(tgo_ctx* ctx) { return ctx->part_dcounts; }
+std::shared_ptr<void>& part_state_of(tgo_ctx* ctx) { return ctx->part_state; }
+int part_in_list(tgo_ctx* ctx, const int32_t** adj, int64_t* nnz) {
+    if (int rc = part_check(ctx)) return rc;
+    *adj = ctx->g.in.adj;
+    *nnz = ctx->g.in.nnz;
+    return TGO_OK;
+}
+// the blocked gathered layout of the last tgo_part_pr_blocked (world 0: plain layout)
+int part_pr_layout_of(tgo_ctx* ctx, int32_t* world, int64_t* hot, int64_t* span) {
+    if (int rc = part_check(ctx)) return rc;
+    const bool blocked = ctx->part_pr_world > 0 && ctx->g.cold_in_ready;
+    *world = blocked ? ctx->part_pr_world : 0;
+    *hot = blocked ? ctx->part_pr_hot : 0;
+    *span = blocked ? ctx->part_pr_span : ctx->g.n;
+    return TGO_OK;
+}
 int part_dims(tgo_ctx* ctx, int64_t* n_local, int64_t* lo, int64_t* n_global, int64_t* entries) {
     if (int rc = part_check(ctx)) return rc;
     *n_local = ctx->g.n;
@@ -2742,7 +2763,7 @@ int part_dims(tgo_ctx* ctx, int64_t* n_local, int64_t* lo, int64_t* n_global, in
 }
 int part_scratch(tgo_ctx* ctx, void** p, int64_t bytes, int slot) {
     Scratch& s = ctx->sc;
-    if (slot < 0 || slot >= 8) return fail(ctx, TGO_E_INVALID, "driver scratch slot");
+    if (slot < 0 || slot >= Scratch::kDrvSlots) return fail(ctx, TGO_E_INVALID, "driver scratch slot");
     if (s.drv_bytes[slot] < bytes) {                // fresh buffers start zero
         uint8_t* q = nullptr;
         HIP_TRY(dev_alloc(ctx, q, bytes));

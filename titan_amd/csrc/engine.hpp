@@ -332,6 +332,14 @@ int build_cold_blocks_device(const int64_t* d_off, const int32_t* d_adj, int64_t
                              bool& built, hipStream_t s, std::string& err);
 int pack_tiles_device(int32_t* d_adj, int64_t m, const std::vector<int64_t>& tstart, const std::vector<int32_t>* tbase,
                       int shift, hipStream_t s, std::string& err);
+// part_ghost.hip: the partitioned PageRank ghost exchange
+int pr_ghost_needs(const int32_t* d_adj, int64_t nnz, int64_t nl, int rank, int world, int32_t** need,
+                   std::vector<int64_t>& need_count, hipStream_t s, std::string& err);
+hipError_t k_gathered_pos(const int32_t* u, int64_t m, int64_t nl, int64_t A, int64_t H, int64_t W, int32_t* pos,
+                          hipStream_t s);
+hipError_t k_sub_i32(int32_t* v, int64_t m, int32_t by, hipStream_t s);
+hipError_t k_pack_f64(const double* src, const int32_t* row, int64_t m, double* out, hipStream_t s);
+hipError_t k_unpack_f64(const double* in, const int32_t* pos, int64_t m, double* g, hipStream_t s);
 hipError_t k_part_gathered_index(const int32_t* in, int64_t m, int64_t nl, int64_t A, int64_t H, int64_t W, int32_t* out,
                                  int* bad, hipStream_t s);
 
@@ -393,8 +401,9 @@ struct DsLoop {
 };
 
 struct Scratch {
-    void* drv[8] = {};          // partitioned C++ driver buffers (part_driver.cpp), by slot
-    int64_t drv_bytes[8] = {};
+    static constexpr int kDrvSlots = 24;
+    void* drv[kDrvSlots] = {};  // partitioned C++ driver buffers (part_driver.cpp), by slot:
+    int64_t drv_bytes[kDrvSlots] = {};   // 0-7 multi-source sweep, 8-12 BFS, 13-17 SSSP, 18-23 PageRank
     int64_t n = 0;
     int32_t* level = nullptr;       // n
     int32_t* q[2] = {nullptr, nullptr};   // frontier queues

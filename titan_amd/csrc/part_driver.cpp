@@ -43,7 +43,10 @@ struct tgo_exchange {
     // per-peer byte counts and offsets (host arrays of `world`)
     virtual int all_to_allv(const void* send, const size_t* sb, const size_t* so, void* recv, const size_t* rb,
                             const size_t* ro, hipStream_t s) = 0;
-    virtual int all_reduce_sum(int64_t* buf, size_t count, hipStream_t s) = 0;
+    // element-wise reduction over the ranks, in place (op: kRedSum / kRedMin / kRedMax)
+    enum { kRedSum = 0, kRedMin = 1, kRedMax = 2 };
+    virtual int all_reduce(int64_t* buf, size_t count, int op, hipStream_t s) = 0;
+    int all_reduce_sum(int64_t* buf, size_t count, hipStream_t s) { return all_reduce(buf, count, kRedSum, s); }
     // a rank leaving the protocol early releases the peers waiting on it (in-process group)
     virtual void abort() {}
     std::string err;
@@ -112,10 +115,11 @@ struct RcclExchange : tgo_exchange {
         const int rc2 = check(ncclGroupEnd(), "ncclGroupEnd");
         return rc ? rc : rc2;
     }
-    int all_reduce_sum(int64_t* buf, size_t count, hipStream_t s) override {
+    int all_reduce(int64_t* buf, size_t count, int op, hipStream_t s) override {
         if (!usable()) return TGO_E_COMM;
         if (world == 1) return TGO_OK;
-        return check(ncclAllReduce(buf, buf, count, ncclInt64, ncclSum, comm, s), "ncclAllReduce");
+        const ncclRedOp_t o = op == kRedMin ? ncclMin : op == kRedMax ? ncclMax : ncclSum;
+        return check(ncclAllReduce(buf, buf, count, ncclInt64, o, comm, s), "ncclAllReduce");
     }
     int copy_on(const void* src, void* dst, size_t bytes, hipStream_t s) {
         if (!bytes || src == dst) return TGO_OK;
@@ -219,7 +223,7 @@ struct LocalExchange : tgo_exchange {
             return TGO_OK;
         });
     }
-    int all_reduce_sum(int64_t* buf, size_t count, hipStream_t s) override {
+    int all_reduce(int64_t* buf, size_t count, int op, hipStream_t s) override {
         std::vector<int64_t> mine(count);
         int rc = sync(s);
         if (!rc) {
@@ -228,9 +232,14 @@ struct LocalExchange : tgo_exchange {
         }
         g->slot[rank] = {nullptr, nullptr, nullptr, nullptr, mine};
         if (!g->barrier()) return fail_msg("local exchange: a rank failed or timed out");
-        std::vector<int64_t> sum(count, 0);
-        for (int p = 0; p < world; ++p)
-            for (size_t i = 0; i < count && i < g->slot[p].red.size(); ++i) sum[i] += g->slot[p].red[i];
+        std::vector<int64_t> sum(mine);
+        for (int p = 0; p < world; ++p) {
+            if (p == rank) continue;
+            for (size_t i = 0; i < count && i < g->slot[p].red.size(); ++i) {
+                const int64_t v = g->slot[p].red[i];
+                sum[i] = op == kRedMin ? std::min(sum[i], v) : op == kRedMax ? std::max(sum[i], v) : sum[i] + v;
+            }
+        }
         if (!g->barrier()) return fail_msg("local exchange: a rank failed or timed out");
         if (rc) return rc;
         const hipError_t e = hipMemcpyAsync(buf, sum.data(), count * sizeof(int64_t), hipMemcpyHostToDevice, s);
@@ -293,6 +302,9 @@ int part_fail(tgo_ctx* ctx, int code, const std::string& msg);
 int part_scratch(tgo_ctx* ctx, void** p, int64_t bytes, int slot);
 int64_t* part_dcounts_of(tgo_ctx* ctx);
 double ms_split_of(const tgo_ctx* ctx);
+std::shared_ptr<void>& part_state_of(tgo_ctx* ctx);
+int part_in_list(tgo_ctx* ctx, const int32_t** adj, int64_t* nnz);
+int part_pr_layout_of(tgo_ctx* ctx, int32_t* world, int64_t* hot, int64_t* span);
 template <class T>
 int scratch(tgo_ctx* ctx, T*& p, int64_t count, int slot) {
     void* q = nullptr;
@@ -482,5 +494,326 @@ extern "C" int tgo_part_msbfs_run(tgo_ctx* ctx, tgo_exchange* x, const int64_t* 
         }
     }
     if (levels_out) *levels_out = levels;
+    return TGO_OK;
+}
+
+// ======================================================================================
+// Native loops of the other partitioned programs: single-source BFS, delta-stepping SSSP and
+// PageRank, each ONE C-ABI call whose C++ loop issues its collectives through the exchange on
+// the ctx stream (the protocols of titan_amd/distributed.py distributed_bfs / _sssp /
+// _pagerank, which stay as the Python reference drivers).  They replace the per-superstep
+// Python round trips of FulgoraGraphComputer's superstep loop (FulgoraGraphComputer.java:
+// 151-189) in its multi-GPU form.
+
+namespace {
+
+// Host-side helpers shared by the loops: small global reductions through a device buffer.
+struct Driver {
+    tgo_ctx* ctx;
+    tgo_exchange* x;
+    hipStream_t st;
+    int64_t* dbuf = nullptr;        // device scalars (8)
+    int64_t* hc = nullptr;          // pinned host view
+    int xfail(int code) { return part_fail(ctx, code, "exchange: " + x->err); }
+    int hip(const char* what) { return part_fail(ctx, TGO_E_HIP, what); }
+    // out[i] = op over the ranks of vals[i], i < k <= 8 (one round trip)
+    int reduce(const int64_t* vals, int k, int op, int64_t* out) {
+        for (int i = 0; i < k; ++i) hc[i] = vals[i];
+        if (hipMemcpyAsync(dbuf, hc, k * sizeof(int64_t), hipMemcpyHostToDevice, st) != hipSuccess) return hip("reduce upload");
+        if (int r = x->all_reduce(dbuf, static_cast<size_t>(k), op, st)) return xfail(r);
+        if (hipMemcpyAsync(hc, dbuf, k * sizeof(int64_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            return hip("reduce read");
+        for (int i = 0; i < k; ++i) out[i] = hc[i];
+        return TGO_OK;
+    }
+};
+
+int driver_open(tgo_ctx* ctx, tgo_exchange* x, const char* name, int slot, Driver& d, int64_t& nl, int64_t& lo,
+                int64_t& ng, int64_t& ent) {
+    int rc = part_dims(ctx, &nl, &lo, &ng, &ent);
+    if (rc) return rc;
+    if (static_cast<int64_t>(x->world) * nl != ng || lo != static_cast<int64_t>(x->rank) * nl)
+        return part_fail(ctx, TGO_E_INVALID, std::string(name) + ": the exchange's world / rank do not match the partition");
+    d.ctx = ctx;
+    d.x = x;
+    d.st = part_stream(ctx);
+    if ((rc = scratch(ctx, d.dbuf, 8, slot))) return rc;
+    d.hc = x->host_counts();
+    if (!d.hc) return part_fail(ctx, TGO_E_HIP, std::string(name) + ": pinned counts");
+    return TGO_OK;
+}
+
+}  // namespace
+
+extern "C" int tgo_part_bfs_run(tgo_ctx* ctx, tgo_exchange* x, int64_t seed_global, int32_t max_depth, double alpha,
+                                double beta, int64_t* dist_local, int64_t* reached, int32_t* levels_out) {
+    if (!ctx) return TGO_E_INVALID;
+    if (!x || max_depth < 0 || !(alpha > 0.0) || !(beta > 0.0))
+        return part_fail(ctx, TGO_E_INVALID, "tgo_part_bfs_run: bad arguments");
+    Driver d{};
+    int64_t nl = 0, lo = 0, ng = 0, ent = 0;
+    int rc = driver_open(ctx, x, "tgo_part_bfs_run", 12, d, nl, lo, ng, ent);
+    if (rc) return rc;
+    const int W = x->world;
+    const int64_t nwl = nl / 64, nwg = ng / 64;
+    hipStream_t st = d.st;
+    // two alternating global frontier bitmaps (the owned next frontier is the rank's slice of
+    // the other one, so the all-gather is in place), the discovered bitmap and its received
+    // slices, the device level counts
+    uint64_t *f0 = nullptr, *f1 = nullptr, *disc = nullptr, *recv = nullptr;
+    int64_t* dc = nullptr;
+    if ((rc = scratch(ctx, f0, nwg, 8)) || (rc = scratch(ctx, f1, nwg, 9)) || (rc = scratch(ctx, disc, nwg, 10)) ||
+        (rc = scratch(ctx, recv, nwg, 11)) || (rc = scratch(ctx, dc, 4, 13)))
+        return rc;
+    int64_t* const caller_dc = part_dcounts_of(ctx);
+    uint64_t* glob[2] = {f0, f1};
+    int64_t tot = 0;
+    if ((rc = d.reduce(&ent, 1, tgo_exchange::kRedSum, &tot))) return rc;
+    int64_t c[2] = {0, 0};
+    if ((rc = tgo_part_bfs_begin(ctx, seed_global, glob[0] + x->rank * nwl, c))) return rc;
+    if (int r = x->all_gather(glob[0], static_cast<size_t>(nwl) * 8, st)) return d.xfail(r);
+    int64_t g[2] = {0, 0};
+    if ((rc = d.reduce(c, 2, tgo_exchange::kRedSum, g))) return rc;
+    int64_t nf = g[0], mf = g[1], mu = tot - mf;
+    if ((rc = tgo_part_device_counts(ctx, dc))) return rc;
+    bool bottom_up = false;
+    int levels = 0;
+    for (int level = 0; level < max_depth && nf > 0; ++level) {
+        // direction-optimizing switch (Beamer et al.; the one-GPU rule, tgo_bfs)
+        if (!bottom_up && static_cast<double>(mf) > static_cast<double>(mu) / alpha) bottom_up = true;
+        else if (bottom_up && static_cast<double>(nf) < static_cast<double>(ng) / beta) bottom_up = false;
+        uint64_t* nb = glob[1] + x->rank * nwl;
+        if (bottom_up) {
+            if ((rc = tgo_part_bfs_bu(ctx, level, glob[0], nb, nullptr))) break;
+        } else {
+            if (hipMemsetAsync(disc, 0, nwg * 8, st) != hipSuccess) { rc = d.hip("disc clear"); break; }
+            if ((rc = tgo_part_bfs_td(ctx, level, disc))) break;
+            if (int r = x->all_to_all(disc, recv, static_cast<size_t>(nwl) * 8, st)) { rc = d.xfail(r); break; }
+            if ((rc = tgo_part_bfs_claim(ctx, level, recv, W, nb, nullptr))) break;
+        }
+        if (int r = x->all_gather(glob[1], static_cast<size_t>(nwl) * 8, st)) { rc = d.xfail(r); break; }
+        std::swap(glob[0], glob[1]);
+        if (int r = x->all_reduce_sum(dc, 2, st)) { rc = d.xfail(r); break; }
+        if (hipMemcpyAsync(d.hc, dc, 3 * sizeof(int64_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess) { rc = d.hip("counts read"); break; }
+        nf = d.hc[0];
+        mf = d.hc[1];
+        mu -= mf;
+        if ((rc = tgo_part_set_local_qlen(ctx, d.hc[2]))) break;
+        ++levels;
+    }
+    const int rc_off = tgo_part_device_counts(ctx, caller_dc);
+    if (rc) { x->abort(); return rc; }
+    if (rc_off) return rc_off;
+    int64_t rl[2] = {0, 0};
+    if ((rc = tgo_part_bfs_end(ctx, dist_local, rl))) return rc;
+    if (reached && (rc = d.reduce(rl, 2, tgo_exchange::kRedSum, reached))) return rc;
+    if (levels_out) *levels_out = levels;
+    return TGO_OK;
+}
+
+extern "C" int tgo_part_sssp_run(tgo_ctx* ctx, tgo_exchange* x, int64_t seed_global, int64_t delta, int64_t* dist_local,
+                                 int64_t* reached, int32_t* phases_out) {
+    if (!ctx) return TGO_E_INVALID;
+    if (!x) return part_fail(ctx, TGO_E_INVALID, "tgo_part_sssp_run: bad arguments");
+    Driver d{};
+    int64_t nl = 0, lo = 0, ng = 0, ent = 0;
+    int rc = driver_open(ctx, x, "tgo_part_sssp_run", 17, d, nl, lo, ng, ent);
+    if (rc) return rc;
+    const int W = x->world;
+    hipStream_t st = d.st;
+    int64_t *send = nullptr, *recv = nullptr, *sizes = nullptr;
+    if ((rc = scratch(ctx, send, 2 * ng + 2, 14)) || (rc = scratch(ctx, recv, 2 * ng + 2, 15)) ||
+        (rc = scratch(ctx, sizes, 2 * W, 16)))
+        return rc;
+    int64_t out[2] = {0, 0};
+    if ((rc = tgo_part_sssp_begin(ctx, seed_global, delta, out))) return rc;
+    int64_t qlen = out[0];
+    if (delta <= 0) {           // the ranks' default widths follow their local mean weight: agree on one
+        if ((rc = d.reduce(&out[1], 1, tgo_exchange::kRedMax, &delta))) return rc;
+    }
+    if (delta <= 0) return part_fail(ctx, TGO_E_INVALID, "tgo_part_sssp_run: bucket width");
+    int64_t thr = delta;
+    int phases = 0;
+    std::vector<int64_t> sc(W), both(2 * W);
+    std::vector<size_t> sb(W), so(W), rb(W), ro(W);
+    for (;;) {
+        int64_t gq = 0;
+        if ((rc = d.reduce(&qlen, 1, tgo_exchange::kRedSum, &gq))) break;
+        if (gq == 0) {          // every near queue is empty: the next non-empty bucket
+            int64_t pm[2] = {0, 0}, mn = 0;
+            if ((rc = tgo_part_sssp_pending_min(ctx, pm))) break;
+            if ((rc = d.reduce(&pm[0], 1, tgo_exchange::kRedMin, &mn))) break;
+            if (mn == INT64_MAX) break;
+            if (mn >= thr) thr = (mn / delta + 1) * delta;
+            int64_t c[2] = {0, 0};
+            if ((rc = tgo_part_sssp_extract(ctx, thr, c))) break;
+            qlen = c[0];
+            continue;
+        }
+        if ((rc = tgo_part_sssp_relax(ctx, thr, W, send, sc.data()))) break;
+        for (int p = 0; p < W; ++p) both[p] = 2 * sc[p];
+        if (hipMemcpyAsync(sizes, both.data(), W * sizeof(int64_t), hipMemcpyHostToDevice, st) != hipSuccess) {
+            rc = d.hip("sizes upload");
+            break;
+        }
+        if (int r = x->all_to_all(sizes, sizes + W, 8, st)) { rc = d.xfail(r); break; }
+        if (hipMemcpyAsync(both.data(), sizes, 2 * W * sizeof(int64_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess) { rc = d.hip("sizes read"); break; }
+        size_t a = 0, b = 0;
+        for (int p = 0; p < W; ++p) {
+            sb[p] = static_cast<size_t>(both[p]) * 8; so[p] = a; a += sb[p];
+            rb[p] = static_cast<size_t>(both[W + p]) * 8; ro[p] = b; b += rb[p];
+        }
+        if (int r = x->all_to_allv(send, sb.data(), so.data(), recv, rb.data(), ro.data(), st)) { rc = d.xfail(r); break; }
+        int64_t c[2] = {0, 0};
+        if ((rc = tgo_part_sssp_apply(ctx, thr, recv, static_cast<int64_t>(b / 16), c))) break;
+        qlen = c[0];
+        ++phases;
+    }
+    if (rc) { x->abort(); return rc; }
+    int64_t rl[2] = {0, 0};
+    if ((rc = tgo_part_sssp_end(ctx, dist_local, rl))) return rc;
+    if (reached && (rc = d.reduce(rl, 2, tgo_exchange::kRedSum, reached))) return rc;
+    if (phases_out) *phases_out = phases;
+    return TGO_OK;
+}
+
+namespace {
+
+// The ghost lists of a partitioned PageRank layout (part_ghost.hip), kept with the graph.
+struct PrGhost {
+    int world = 0, rank = -1;
+    int64_t nl = 0, hot = 0, span = 0;
+    int32_t* send_row = nullptr;    // local rows this rank sends, peer-major
+    int32_t* recv_pos = nullptr;    // gathered-vector position of every received value
+    double* sbuf = nullptr;
+    double* rbuf = nullptr;
+    int64_t nsend = 0, nrecv = 0;
+    std::vector<size_t> sb, so, rb, ro;   // byte counts / offsets per peer (doubles)
+    ~PrGhost() {
+        for (void* p : {static_cast<void*>(send_row), static_cast<void*>(recv_pos), static_cast<void*>(sbuf),
+                        static_cast<void*>(rbuf)})
+            if (p) (void)hipFree(p);
+    }
+};
+
+int build_pr_ghost(tgo_ctx* ctx, tgo_exchange* x, Driver& d, int64_t nl, int64_t hot, int64_t span, PrGhost& gh) {
+    const int W = x->world, R = x->rank;
+    hipStream_t st = d.st;
+    const int32_t* adj = nullptr;
+    int64_t nnz = 0;
+    int rc = part_in_list(ctx, &adj, &nnz);
+    if (rc) return rc;
+    std::string err;
+    int32_t* need = nullptr;
+    std::vector<int64_t> need_count;
+    if ((rc = pr_ghost_needs(adj, nnz, nl, R, W, &need, need_count, st, err))) return part_fail(ctx, rc, err);
+    struct Free { void* p; ~Free() { if (p) (void)hipFree(p); } } free_need{need};
+    int64_t nneed = 0;
+    for (int64_t c : need_count) nneed += c;
+    // counts to the owners, then the ids (as int32 bytes)
+    int64_t* sizes = nullptr;
+    if ((rc = scratch(ctx, sizes, 2 * W, 21))) return rc;
+    if (hipMemcpyAsync(sizes, need_count.data(), W * sizeof(int64_t), hipMemcpyHostToDevice, st) != hipSuccess)
+        return d.hip("ghost counts upload");
+    if (int r = x->all_to_all(sizes, sizes + W, 8, st)) return d.xfail(r);
+    std::vector<int64_t> gives(W);
+    if (hipMemcpyAsync(gives.data(), sizes + W, W * sizeof(int64_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return d.hip("ghost counts read");
+    int64_t ngive = 0;
+    for (int64_t c : gives) ngive += c;
+    gh.world = W; gh.rank = R; gh.nl = nl; gh.hot = hot; gh.span = span;
+    gh.nsend = ngive;
+    gh.nrecv = nneed;
+    if (hipMalloc(&gh.send_row, std::max<int64_t>(ngive, 1) * 4) != hipSuccess ||
+        hipMalloc(&gh.recv_pos, std::max<int64_t>(nneed, 1) * 4) != hipSuccess ||
+        hipMalloc(&gh.sbuf, std::max<int64_t>(ngive, 1) * 8) != hipSuccess ||
+        hipMalloc(&gh.rbuf, std::max<int64_t>(nneed, 1) * 8) != hipSuccess)
+        return part_fail(ctx, TGO_E_OOM, "ghost buffers");
+    std::vector<size_t> ib(W), io(W), gb(W), go(W);
+    gh.sb.assign(W, 0); gh.so.assign(W, 0); gh.rb.assign(W, 0); gh.ro.assign(W, 0);
+    size_t a = 0, b = 0;
+    for (int p = 0; p < W; ++p) {
+        ib[p] = static_cast<size_t>(need_count[p]) * 4; io[p] = a; a += ib[p];       // my needs, to owner p
+        gb[p] = static_cast<size_t>(gives[p]) * 4; go[p] = b; b += gb[p];            // p's needs of my rows
+        gh.rb[p] = static_cast<size_t>(need_count[p]) * 8; gh.ro[p] = io[p] * 2;      // values received from p
+        gh.sb[p] = static_cast<size_t>(gives[p]) * 8; gh.so[p] = go[p] * 2;           // values sent to p
+    }
+    if (int r = x->all_to_allv(need, ib.data(), io.data(), gh.send_row, gb.data(), go.data(), st)) return d.xfail(r);
+    if (hipError_t e = k_sub_i32(gh.send_row, ngive, static_cast<int32_t>(static_cast<int64_t>(R) * nl), st))
+        return part_fail(ctx, TGO_E_HIP, hipGetErrorString(e));
+    if (hipError_t e = k_gathered_pos(need, nneed, nl, span, hot, W, gh.recv_pos, st))
+        return part_fail(ctx, TGO_E_HIP, hipGetErrorString(e));
+    if (hipStreamSynchronize(st) != hipSuccess) return d.hip("ghost lists");
+    return TGO_OK;
+}
+
+}  // namespace
+
+extern "C" int tgo_part_pagerank_run(tgo_ctx* ctx, tgo_exchange* x, const tgo_pr_args* args, int32_t exchange_mode,
+                                     double* pr_local, int64_t* exchanged_bytes) {
+    if (!ctx) return TGO_E_INVALID;
+    if (!x || !args || args->max_iterations < 1 || exchange_mode < 0 || exchange_mode > 1)
+        return part_fail(ctx, TGO_E_INVALID, "tgo_part_pagerank_run: bad arguments");
+    Driver d{};
+    int64_t nl = 0, lo = 0, ng = 0, ent = 0;
+    int rc = driver_open(ctx, x, "tgo_part_pagerank_run", 22, d, nl, lo, ng, ent);
+    if (rc) return rc;
+    const int W = x->world, R = x->rank;
+    hipStream_t st = d.st;
+    // layout: active span A = max active rows (every rank), the blocked hot-first layout
+    int64_t act = 0, span = 0, hot = 0;
+    if ((rc = tgo_part_active_rows(ctx, &act))) return rc;
+    if ((rc = d.reduce(&act, 1, tgo_exchange::kRedMax, &span))) return rc;
+    if ((rc = tgo_part_pr_blocked(ctx, W, span, &hot))) return rc;
+    if (hot == 0) span = nl;                     // plain layout: rank-major n_local slices
+    double *contrib = nullptr, *gath = nullptr;
+    if ((rc = scratch(ctx, contrib, nl, 18)) || (rc = scratch(ctx, gath, static_cast<int64_t>(W) * span, 19))) return rc;
+    PrGhost* gh = nullptr;
+    if (exchange_mode == 1 && W > 1) {
+        std::shared_ptr<void>& state = part_state_of(ctx);
+        gh = static_cast<PrGhost*>(state.get());
+        if (!gh || gh->world != W || gh->rank != R || gh->hot != hot || gh->span != span || gh->nl != nl) {
+            auto fresh = std::make_shared<PrGhost>();
+            if ((rc = build_pr_ghost(ctx, x, d, nl, hot, span, *fresh))) { x->abort(); return rc; }
+            state = fresh;
+            gh = fresh.get();
+        }
+    }
+    int64_t moved = 0;
+    if ((rc = tgo_part_pr_begin(ctx, args, contrib))) return rc;
+    for (int it = 2; it <= args->max_iterations; ++it) {
+        // the rank's own slice into the gathered vector
+        hipError_t e = hot == 0
+            ? hipMemcpyAsync(gath + static_cast<int64_t>(R) * nl, contrib, nl * 8, hipMemcpyDeviceToDevice, st)
+            : hipMemcpyAsync(gath + static_cast<int64_t>(R) * hot, contrib, hot * 8, hipMemcpyDeviceToDevice, st);
+        if (e == hipSuccess && hot > 0 && span > hot)
+            e = hipMemcpyAsync(gath + static_cast<int64_t>(W) * hot + static_cast<int64_t>(R) * (span - hot), contrib + hot,
+                               (span - hot) * 8, hipMemcpyDeviceToDevice, st);
+        if (e != hipSuccess) { rc = d.hip("own slice"); break; }
+        if (W > 1 && gh) {                       // ghosts: exactly the remote values this rank reads
+            if ((e = k_pack_f64(contrib, gh->send_row, gh->nsend, gh->sbuf, st)) != hipSuccess) { rc = d.hip("pack"); break; }
+            if (int r = x->all_to_allv(gh->sbuf, gh->sb.data(), gh->so.data(), gh->rbuf, gh->rb.data(), gh->ro.data(), st)) {
+                rc = d.xfail(r);
+                break;
+            }
+            if ((e = k_unpack_f64(gh->rbuf, gh->recv_pos, gh->nrecv, gath, st)) != hipSuccess) { rc = d.hip("unpack"); break; }
+            moved += gh->nrecv * 8;
+        } else if (W > 1) {                      // all-gather of every rank's slices (in place)
+            int r = hot == 0 ? x->all_gather(gath, static_cast<size_t>(nl) * 8, st)
+                             : x->all_gather(gath, static_cast<size_t>(hot) * 8, st);
+            if (!r && hot > 0 && span > hot)
+                r = x->all_gather(gath + static_cast<int64_t>(W) * hot, static_cast<size_t>(span - hot) * 8, st);
+            if (r) { rc = d.xfail(r); break; }
+            moved += static_cast<int64_t>(W - 1) * (hot == 0 ? nl : span) * 8;
+        }
+        if ((rc = tgo_part_pr_step(ctx, gath, contrib))) break;
+    }
+    if (rc) { x->abort(); return rc; }
+    if ((rc = tgo_part_pr_end(ctx, pr_local))) return rc;
+    if (exchanged_bytes) *exchanged_bytes = moved;
     return TGO_OK;
 }

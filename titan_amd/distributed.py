@@ -768,6 +768,57 @@ def distributed_msbfs_native(backend, seeds, max_depth: int, exchange: NativeExc
     return r, e, lv.value
 
 
+def _native_check(backend, rc):
+    if rc:
+        from .engine import TitanException
+        raise TitanException(rc, (backend.e.lib.tgo_last_error(backend.e.ctx) or b"").decode())
+
+
+def distributed_bfs_native(backend, seed: int, max_depth: int, exchange: NativeExchange, alpha: float = 15.0,
+                           beta: float = 18.0, fetch: bool = True, stats: bool = True):
+    """distributed_bfs as ONE native call (tgo_part_bfs_run).  Returns (local distances or
+    None, global [reached vertices, entries] or None, levels)."""
+    out = np.zeros(backend.n_local, np.int64) if fetch else None
+    reached = np.zeros(2, np.int64) if stats else None
+    lv = C.c_int32()
+    _native_check(backend, backend.e.lib.tgo_part_bfs_run(backend.e.ctx, exchange.h, int(seed), int(max_depth),
+                                                          float(alpha), float(beta), L.ptr(out, C.c_int64),
+                                                          L.ptr(reached, C.c_int64), C.byref(lv)))
+    return out, reached, lv.value
+
+
+def distributed_sssp_native(backend, seed: int, exchange: NativeExchange, delta: int = 0, fetch: bool = True,
+                            stats: bool = True):
+    """distributed_sssp as ONE native call (tgo_part_sssp_run).  Returns (local distances or
+    None, global [reached vertices, entries] or None, phases)."""
+    out = np.zeros(backend.n_local, np.int64) if fetch else None
+    reached = np.zeros(2, np.int64) if stats else None
+    ph = C.c_int32()
+    _native_check(backend, backend.e.lib.tgo_part_sssp_run(backend.e.ctx, exchange.h, int(seed), int(delta),
+                                                           L.ptr(out, C.c_int64), L.ptr(reached, C.c_int64),
+                                                           C.byref(ph)))
+    return out, reached, ph.value
+
+
+PR_EXCHANGE_ALLGATHER, PR_EXCHANGE_GHOST = 0, 1
+
+
+def distributed_pagerank_native(backend, alpha: float, vertex_count: int, iterations: int, exchange: NativeExchange,
+                                mode: int = PR_EXCHANGE_GHOST, fetch: bool = True):
+    """distributed_pagerank as ONE native call (tgo_part_pagerank_run): the layout agreed
+    inside, then every update refreshes the gathered vector by an all-gather (mode 0) or the
+    ghost exchange (mode 1, only the contributions this rank reads).  Returns (local ranks or
+    None, bytes this rank received)."""
+    if iterations == 0:
+        return (np.full(backend.n_local, np.nan) if fetch else None), 0
+    out = np.zeros(backend.n_local, np.float64) if fetch else None
+    moved = C.c_int64()
+    a = L.PrArgs(float(alpha), int(vertex_count), int(iterations), 0)
+    _native_check(backend, backend.e.lib.tgo_part_pagerank_run(backend.e.ctx, exchange.h, C.byref(a), int(mode),
+                                                               L.ptr(out, C.c_double), C.byref(moved)))
+    return out, moved.value
+
+
 INT64_MAX = (1 << 63) - 1
 
 
