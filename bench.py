@@ -71,8 +71,10 @@ def parse():
     p.add_argument("--partitioned", action="store_true",
                    help="use the vertex-partitioned multi-GPU path even at N=1 (for testing it on one GPU)")
     p.add_argument("--native", type=int, default=1,
-                   help="partitioned path: the multi-source sweep as one native call over RCCL (tgo_part_msbfs_run); "
-                        "0 = the Python level driver")
+                   help="partitioned path: every program as one native call over RCCL (tgo_part_msbfs_run / "
+                        "_bfs_run / _pagerank_run / _sssp_run); 0 = the Python level drivers")
+    p.add_argument("--pr-exchange", choices=["ghost", "allgather"], default="ghost",
+                   help="partitioned PageRank: ghost exchange (only the contributions a rank reads) or all-gather")
     p.add_argument("--balanced", type=int, default=1,
                    help="partitioned path: edge-balanced ranges (entries + vertices, SlotPartition); 0 = equal ranges")
     return p.parse_args()
@@ -336,9 +338,10 @@ def run_partitioned(args, world, rank, local_rank):
     import torch.distributed as dist
     from titan_amd import Engine
     from titan_amd import _lib as L
-    from titan_amd.distributed import (HipPartBackend, NativeExchange, SlotPartition, all_gather_layout,
-                                       balanced_partition, distributed_bfs, distributed_msbfs,
-                                       distributed_msbfs_native, distributed_pagerank, entry_imbalance,
+    from titan_amd.distributed import (PR_EXCHANGE_ALLGATHER, PR_EXCHANGE_GHOST, HipPartBackend, NativeExchange,
+                                       SlotPartition, all_gather_layout, balanced_partition, distributed_bfs,
+                                       distributed_bfs_native, distributed_msbfs, distributed_msbfs_native,
+                                       distributed_pagerank, distributed_pagerank_native, entry_imbalance,
                                        exchange_stream, pagerank_layout, partition_range, pick_roots_partitioned,
                                        word_weights)
     torch.cuda.set_device(local_rank)
@@ -350,15 +353,16 @@ def run_partitioned(args, world, rank, local_rank):
     lib = L.load()
 
     def edges_of(lo, hi):
-        """The RMAT stream's edges with an endpoint in [lo, hi) (tgo_rmat_partition)."""
+        """The RMAT stream's edges with an endpoint in [lo, hi), generated and selected on this
+        rank's GPU (tgo_rmat_partition_device; the host stream of tgo_rmat_partition)."""
         t0 = time.perf_counter()
         cap = int(2.3 * m * (hi - lo) / n) + (1 << 22)
         src = np.empty(cap, np.int32)
         dst = np.empty(cap, np.int32)
         wgt = np.empty(cap, np.int32) if args.sssp_roots > 0 else None
         cnt = C.c_int64()
-        rc = lib.tgo_rmat_partition(scale, args.edge_factor, 0x54495441, lo, hi, L.ptr(src, C.c_int32),
-                                    L.ptr(dst, C.c_int32), L.ptr(wgt, C.c_int32), cap, C.byref(cnt), 16)
+        rc = lib.tgo_rmat_partition_device(scale, args.edge_factor, 0x54495441, lo, hi, L.ptr(src, C.c_int32),
+                                           L.ptr(dst, C.c_int32), L.ptr(wgt, C.c_int32), cap, C.byref(cnt), local_rank)
         if rc:
             raise RuntimeError(f"tgo_rmat_partition rc={rc} count={cnt.value} cap={cap}")
         log(f"rmat scale {scale} partition [{lo},{hi}) of {world}: {cnt.value} edges in "
@@ -415,13 +419,26 @@ def run_partitioned(args, world, rank, local_rank):
     _, mR, depth_ms = sweep(True)
     # single-source side measurement (untimed, every root, Graph500 style harmonic mean)
     ss_t = []
-    distributed_bfs(bfs_be, roots_s[0], ns, fetch=False, stats=False)
+
+    def single(r):
+        if xchg is not None:
+            return distributed_bfs_native(bfs_be, r, ns, xchg, fetch=False, stats=False)
+        return distributed_bfs(bfs_be, r, ns, fetch=False, stats=False)
+    single(roots_s[0])
     for r in roots_s:
         torch.cuda.synchronize()
         t = time.perf_counter()
-        distributed_bfs(bfs_be, r, ns, fetch=False, stats=False)
+        single(r)
         torch.cuda.synchronize()
         ss_t.append(time.perf_counter() - t)
+    pr_mode = PR_EXCHANGE_GHOST if args.pr_exchange == "ghost" else PR_EXCHANGE_ALLGATHER
+    pr_moved = [0]
+
+    def pagerank():
+        if xchg is not None:
+            _, pr_moved[0] = distributed_pagerank_native(pr_be, 0.85, n, args.pr_iters, xchg, mode=pr_mode, fetch=False)
+        else:
+            distributed_pagerank(pr_be, 0.85, n, args.pr_iters, fetch=False, layout=pr_layout)
     hmean = len(ss_t) / float(np.sum(np.array(ss_t) / (mR[:len(ss_t)] / 2.0)))
 
     def step():
@@ -430,7 +447,7 @@ def run_partitioned(args, world, rank, local_rank):
         torch.cuda.synchronize()
         bt = time.perf_counter() - t
         t = time.perf_counter()
-        distributed_pagerank(pr_be, 0.85, n, args.pr_iters, fetch=False, layout=pr_layout)
+        pagerank()
         torch.cuda.synchronize()
         return bt, time.perf_counter() - t
 
@@ -456,7 +473,7 @@ def run_partitioned(args, world, rank, local_rank):
     sssp = None
     if wgt is not None:
         sssp = sssp_leg_partitioned(args, world, rank, local_rank, ns, slo, shi, src, dst, wgt, roots_s, stream, lay,
-                                    n)
+                                    n, xchg)
     if rank == 0:
         edges_in = mR / 2.0
         teps = float(edges_in.sum()) * args.steps / bfs_wall
@@ -472,10 +489,14 @@ def run_partitioned(args, world, rank, local_rank):
         line = result_line(args, world, scale, n, m, roots, elapsed, teps, hmean, pr_wall / upd, e_in,
                            roof_bfs, roof_pr, bfs_share, None, f"vertex-partition{world}")
         line["config"]["device_layout"] = "degree-grouped per rank" if args.layout else "global ids"
-        line["config"]["msbfs_driver"] = ("native level loop, RCCL on the engine stream (tgo_part_msbfs_run)"
-                                          if args.native else "Python level driver (titan_amd/distributed.py)")
+        line["config"]["msbfs_driver"] = ("native level loops, RCCL on the engine stream (tgo_part_msbfs_run / "
+                                          "_bfs_run / _pagerank_run / _sssp_run)"
+                                          if args.native else "Python level drivers (titan_amd/distributed.py)")
         line["pagerank_exchange"] = {"hot_rows_per_rank": pr_layout[0], "active_span": pr_layout[1],
-                                     "bytes_per_rank_per_update": 8 * pr_layout[1]}
+                                     "mode": args.pr_exchange if args.native else "allgather (Python driver)",
+                                     "allgather_bytes_per_rank_per_update": 8 * pr_layout[1] * (world - 1),
+                                     "received_bytes_rank0_per_update": (pr_moved[0] // upd if args.native
+                                                                         else 8 * pr_layout[1] * (world - 1))}
         wr = part.weights(ww)
         line["partition"] = {"ranges": ("edge-balanced 64-aligned ranges (entries + vertices) in equal exchange slots"
                                         if args.balanced else "equal 64-aligned vertex ranges of the seeded relabel"),
@@ -490,7 +511,7 @@ def run_partitioned(args, world, rank, local_rank):
     dist.destroy_process_group()
 
 
-def sssp_leg_partitioned(args, world, rank, local_rank, n, lo, hi, src, dst, wgt, roots, stream, lay, n_real):
+def sssp_leg_partitioned(args, world, rank, local_rank, n, lo, hi, src, dst, wgt, roots, stream, lay, n_real, xchg=None):
     """configs[4] over N GPUs: delta-stepping SSSP on the vertex-partitioned weighted graph
     (inE scope, no preload cap), per-owner relaxation exchange over RCCL
     (titan_amd/distributed.distributed_sssp); roots whose reach is the giant component.
@@ -499,7 +520,12 @@ def sssp_leg_partitioned(args, world, rank, local_rank, n, lo, hi, src, dst, wgt
     import torch.distributed as dist
     from titan_amd import Engine
     from titan_amd import _lib as L
-    from titan_amd.distributed import HipPartBackend, distributed_sssp
+    from titan_amd.distributed import HipPartBackend, distributed_sssp, distributed_sssp_native
+
+    def run(r, stats):
+        if xchg is not None:
+            return distributed_sssp_native(be, r, xchg, args.delta, fetch=False, stats=stats)
+        return distributed_sssp(be, r, args.delta, fetch=False, stats=stats)
     eng = Engine(device=local_rank, host_threads=16, stream=stream).load_partition(n, lo, hi, src, dst, L.SCOPE_IN_E,
                                                                                  weight=wgt, apply_cap=False,
                                                                                  layout=lay)
@@ -508,13 +534,13 @@ def sssp_leg_partitioned(args, world, rank, local_rank, n, lo, hi, src, dst, wgt
     for r in roots:
         if len(res) == args.sssp_roots:
             break
-        _, reached, _ = distributed_sssp(be, int(r), args.delta, fetch=False, stats=True)
+        _, reached, _ = run(int(r), True)
         if reached[0] * 4 < n_real:
             continue
         torch.cuda.synchronize()
         dist.barrier()
         t = time.perf_counter()
-        _, _, phases = distributed_sssp(be, int(r), args.delta, fetch=False, stats=False)
+        _, _, phases = run(int(r), False)
         torch.cuda.synchronize()
         wall = torch.tensor([time.perf_counter() - t], dtype=torch.float64, device="cuda")
         dist.all_reduce(wall, op=dist.ReduceOp.MAX)

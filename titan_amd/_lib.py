@@ -142,7 +142,7 @@ EXPORTS = [
     "tgo_bfs_multi", "tgo_copy_multi_distances", "tgo_multi_stats", "tgo_set_tuning",
     "tgo_gather", "tgo_combine_global", "tgo_dense_ids", "tgo_decode_edge_entry", "tgo_result_rows",
     "tgo_gather_lists", "tgo_result_rows_values",
-    "tgo_rmat_edges", "tgo_rmat_edges_device", "tgo_pick_roots", "tgo_synth_rows",
+    "tgo_rmat_edges", "tgo_rmat_edges_device", "tgo_rmat_partition_device", "tgo_pick_roots", "tgo_synth_rows",
     # titan_gpu_olap_part.h (1-D vertex-partitioned multi-GPU)
     "tgo_load_partition", "tgo_part_layout", "tgo_load_partition_layout", "tgo_part_bfs_begin", "tgo_part_bfs_td", "tgo_part_bfs_claim", "tgo_part_bfs_bu",
     "tgo_part_bfs_end", "tgo_part_pr_begin", "tgo_part_pr_step", "tgo_part_pr_end", "tgo_rmat_partition",
@@ -213,6 +213,8 @@ def load() -> C.CDLL:
                                      _i32p, _i32p, _i32p, C.c_int32]),
         "tgo_rmat_edges_device": (C.c_int, [C.c_int32, C.c_int32, C.c_uint64, C.c_int64, C.c_int64,
                                             _i32p, _i32p, _i32p, C.c_int32]),
+        "tgo_rmat_partition_device": (C.c_int, [C.c_int32, C.c_int32, C.c_uint64, C.c_int64, C.c_int64, _i32p, _i32p,
+                                                _i32p, C.c_int64, _i64p, C.c_int32]),
         "tgo_pick_roots": (C.c_int, [C.c_int64, C.c_int64, _i32p, _i32p, C.c_uint64, C.c_int32, _i64p]),
         "tgo_synth_rows": (C.c_int, [C.c_int64, C.c_int64, _i32p, _i32p, _i32p, C.c_int64, C.c_int32, C.c_int32,
                                      _i64p, _i64p, _i64p, _i64p, P(C.c_uint8), _i64p]),
