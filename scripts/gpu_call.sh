@@ -1,12 +1,10 @@
 #!/bin/bash
-# Round-4 call c: native partitioned BFS / SSSP / PageRank loops (ghost exchange), device RMAT partition.
+# Round-4 call d: counter names on gfx950; PageRank time attributable to the top sources of
+# the hot pass (TGO_PR_SKIP_BELOW diagnostic: those gathers skipped).
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
-mkdir -p gpurun_out/r04c
-timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
-    tests/test_gpu_distributed.py > gpurun_out/r04c/gpu_tests.log 2>&1
-rc=$?; grep -E "PASSED|FAILED|Error|error" gpurun_out/r04c/gpu_tests.log | tail -6; tail -40 gpurun_out/r04c/gpu_tests.log | grep -v PASSED
-[ $rc -eq 0 ] || exit $rc
-export RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=29533
-timeout -k 10 600 python3 bench.py --partitioned --steps 3 --warmup 1 --cpu-baseline 0 --rows-scale 0 --sssp-roots 2 \
-    > gpurun_out/r04c/bench_part.json 2> gpurun_out/r04c/bench_part.err
-rc=$?; tail -3 gpurun_out/r04c/bench_part.err; cat gpurun_out/r04c/bench_part.json | head -c 3000; exit $rc
+mkdir -p gpurun_out/r04d
+timeout -k 10 120 rocprofv3 -L > gpurun_out/r04d/counters.txt 2>&1; echo "rocprofv3 -L exit $?"
+bash scripts/gpu_pr_ab.sh r04d_skip "TGO_PR_SKIP_BELOW=0" "TGO_PR_SKIP_BELOW=1024" "TGO_PR_SKIP_BELOW=4096" \
+    "TGO_PR_SKIP_BELOW=16384" "TGO_PR_SKIP_BELOW=65536" "TGO_PR_SKIP_BELOW=131072" "TGO_PR_SKIP_BELOW=393216" \
+    > gpurun_out/r04d/skip.log 2>&1
+rc=$?; cat gpurun_out/r04d/skip.log; exit $rc

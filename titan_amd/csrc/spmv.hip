@@ -192,9 +192,10 @@ __global__ void __launch_bounds__(kBlock) gather_short_packed(const int64_t* __r
 // more memory latency after the barrier.  Thread-per-row tiles prefetch row r0 + tid;
 // wave-per-row tiles (<= 64 rows) prefetch row r0 + wave + 4 * lane, handed to the row's
 // wave by a shuffle.  Same sums in the same order as gather_short_packed: bitwise equal.
+template <bool kSkip = false>
 __global__ void __launch_bounds__(kBlock) gather_hot_pf(const int64_t* __restrict__ off,
         const int32_t* __restrict__ padj, const int64_t* __restrict__ bdesc, const double* __restrict__ msg,
-        PrColdFinal fin) {
+        PrColdFinal fin, int32_t skip_below = 0) {
     __shared__ double s_val[kTile];
     // block bounds and first entries in one descriptor pair (RowBlocks::bdesc)
     const int64_t r0 = bdesc[2 * blockIdx.x], s0 = bdesc[2 * blockIdx.x + 1];
@@ -219,8 +220,11 @@ __global__ void __launch_bounds__(kBlock) gather_hot_pf(const int64_t* __restric
             v[j] = k < nnz ? stream_idx(padj + s0 + k) : -1;
         }
         double val[kPer];
+        // kSkip (diagnostic, TGO_PR_SKIP_BELOW): sources below skip_below read as 0 without a
+        // load — the time the top sources' gathers cost in this pass; results are wrong
 #pragma unroll
-        for (int j = 0; j < kPer; ++j) val[j] = v[j] >= 0 ? msg[v[j] >> kPackShift] : 0.0;
+        for (int j = 0; j < kPer; ++j)
+            val[j] = v[j] >= 0 && (!kSkip || (v[j] >> kPackShift) >= skip_below) ? msg[v[j] >> kPackShift] : 0.0;
 #pragma unroll
         for (int j = 0; j < kPer; ++j)
             if (v[j] >= 0) s_val[v[j] & ((1 << kPackShift) - 1)] = val[j];
@@ -701,7 +705,11 @@ hipError_t k_pr_hot_phase(const ColdBlocks& cb, const double* contrib, const dou
         else
             gather_hot_big<16384, 1024, 14><<<g, 1024, 0, s>>>(cb.hcsr.off, padj, rb.bdesc, contrib, fin);
     } else if (rb.nblocks > 0) {
-        if (row_prefetch())
+        static const int32_t skip_below = static_cast<int32_t>(std::atol(std::getenv("TGO_PR_SKIP_BELOW") ? std::getenv("TGO_PR_SKIP_BELOW") : "0"));
+        if (skip_below > 0)
+            gather_hot_pf<true><<<static_cast<unsigned>(rb.nblocks), kBlock, 0, s>>>(cb.hcsr.off, cb.hcsr.adj, rb.bdesc,
+                                                                                      contrib, fin, skip_below);
+        else if (row_prefetch())
             gather_hot_pf<<<static_cast<unsigned>(rb.nblocks), kBlock, 0, s>>>(cb.hcsr.off, cb.hcsr.adj, rb.bdesc,
                                                                                     contrib, fin);
         else
