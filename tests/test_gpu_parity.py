@@ -461,18 +461,21 @@ def test_partitioned_hubs_match_oracle():
                 o.pagerank(0.85, n, 4)
 
 
+@pytest.mark.parametrize("win", [0, 2])
 @pytest.mark.parametrize("tile", ["4096", "8192", "16384"])
 @pytest.mark.parametrize("iters", [2, 20])
 @pytest.mark.parametrize("hot,seg", [(64, 256), (1000, 100), (4096, 512)])
-def test_rmat_pagerank_cache_blocked(rmat12, iters, hot, seg, tile, monkeypatch):
+def test_rmat_pagerank_cache_blocked(rmat12, iters, hot, seg, tile, win, monkeypatch):
     """The cache-blocked PageRank gather (hot CSR + XCD-pinned cold segments, engine.hpp
     ColdBlocks) forced onto a small graph with tiny hot sets / segments (many segments, so
-    every XCD has several), with each hot tile size (gather_hot_pf / gather_hot_big): oracle
-    bar, bitwise reproducible, within rounding of the plain CSR-adaptive gather.  hot >= n
-    means nothing is cold (plain path)."""
+    every XCD has several), with each hot tile size (gather_hot_pf / gather_hot_big), without
+    and with the LDS window pass over the hottest hot / win sources (lds_window): oracle bar,
+    bitwise reproducible, within rounding of the plain CSR-adaptive gather.  hot >= n means
+    nothing is cold (plain path)."""
     n, src, dst, w, ids, oracle, roots = rmat12
     monkeypatch.setenv("TGO_PR_HOT", str(hot))
     monkeypatch.setenv("TGO_PR_SEG", str(seg))
+    monkeypatch.setenv("TGO_PR_WIN", str(hot // win if win else 0))
     monkeypatch.setenv("TGO_PR_HOT_TILE", tile)
     eng = Engine().load_edges(n, src, dst, IN)
     pr = eng.pagerank(0.85, n, iters)
@@ -500,19 +503,23 @@ def hub_graph(n, hub, k_in, k_out, seed=11):
 KTILE = 4096     # CSR-adaptive tile (engine.hpp kTile): rows longer than this are split in chunks
 
 
-@pytest.mark.parametrize("blocked,tile,pipe", [("0", "4096", "0"), ("1", "4096", "0"), ("1", "8192", "0"),
-                                               ("1", "16384", "0"), ("1", "4096", "1"), ("1", "16384", "1")])
-def test_pagerank_long_rows(monkeypatch, blocked, tile, pipe):
+@pytest.mark.parametrize("blocked,tile,pipe,win", [("0", "4096", "0", 0), ("1", "4096", "0", 0), ("1", "8192", "0", 0),
+                                                   ("1", "16384", "0", 0), ("1", "4096", "1", 0), ("1", "16384", "1", 0),
+                                                   ("1", "4096", "0", 8192), ("1", "8192", "0", 512)])
+def test_pagerank_long_rows(monkeypatch, blocked, tile, pipe, win):
     """A hub whose in-list spans many tiles: 80 000 entries = ~20 chunks of kTile through
     gather_chunks + finalize_long; cache-blocked with 1024 hot sources and 4096-source cold
     segments, its cold run per segment (~10 000 entries) is cut into several kTile pieces;
     the larger hot tiles cut the hub's hot run into 8192 / 16384-entry chunks (packed words
-    with the top bit set).  All within 1e-6 L1 of the oracle and bitwise reproducible."""
+    with the top bit set).  With an LDS window of 8192 sources (16 384 hot) the hub's ~20 000
+    window entries are one long window row, summed by a whole workgroup.  All within 1e-6 L1
+    of the oracle and bitwise reproducible."""
     monkeypatch.setenv("TGO_PR_BLOCKED", blocked)
     monkeypatch.setenv("TGO_PR_HOT_TILE", tile)
     monkeypatch.setenv("TGO_PR_HOT_PIPE", pipe)
-    monkeypatch.setenv("TGO_PR_HOT", "1024")
+    monkeypatch.setenv("TGO_PR_HOT", "16384" if win > 1024 else "1024")
     monkeypatch.setenv("TGO_PR_SEG", "4096")
+    monkeypatch.setenv("TGO_PR_WIN", str(win))
     n = 1 << 15
     src, dst = hub_graph(n, 7, 80000, 0)
     assert (dst == 7).sum() > 2 * 8 * KTILE

@@ -157,6 +157,9 @@ int64_t env_i64(const char* name, int64_t dflt) {
     return v ? std::atoll(v) : dflt;
 }
 constexpr int64_t kPrHotDefault = 393216, kPrSegDefault = 393216;   // 3 MB each (profiles/r02an_pr_hot_seg_probe*.log)
+// LDS window of the hottest sources (lds_window, spmv.hip): 15872 doubles = 124 KB of a CU's
+// 160 KB LDS beside the 32 KB tile; 0 = off
+constexpr int64_t kPrWinDefault = 15872;
 
 // PageRank diagnostics (engine.hpp PrTuning): TGO_PR_DIAG=lo:hi gathers only sources in
 // [lo, hi) — a timing attribution tool, its ranks are wrong (scripts/pr_probe.py).
@@ -238,7 +241,8 @@ int upload_row_blocks_dev(tgo_ctx* ctx, const std::vector<int64_t>& off, RowBloc
 // host; uploaded into cb.
 int upload_cold_blocks(tgo_ctx* ctx, const std::vector<int64_t>& off, const std::vector<int32_t>& adj,
                        int64_t n_src, int64_t hot, int64_t n_rows, ColdBlocks& cb, bool& ready,
-                       const int64_t* d_off = nullptr, const int32_t* d_adj = nullptr, int64_t d_nnz = 0) {
+                       const int64_t* d_off = nullptr, const int32_t* d_adj = nullptr, int64_t d_nnz = 0,
+                       int64_t win = 0) {
     cb = ColdBlocks();
     ready = false;
     HostColdBlocks hc;
@@ -255,7 +259,7 @@ int upload_cold_blocks(tgo_ctx* ctx, const std::vector<int64_t>& off, const std:
         std::string err;
         if (int rc = build_cold_blocks_device(d_off, d_adj, static_cast<int64_t>(off.size()) - 1, d_nnz, n_src, hot,
                                               env_i64("TGO_PR_SEG", kPrSegDefault), kTile, kMaxRows,
-                                              env_i64("TGO_PR_CPACK", 1) != 0, hc, on_dev, ctx->stream, err))
+                                              env_i64("TGO_PR_CPACK", 1) != 0, hc, on_dev, ctx->stream, err, win))
             return fail(ctx, rc, err);
         if (on_dev) lap("build (device)");
     }
@@ -266,7 +270,7 @@ int upload_cold_blocks(tgo_ctx* ctx, const std::vector<int64_t>& off, const std:
     }
     if (!on_dev) {
         if (!build_cold_blocks(off, adj_dl.empty() ? adj : adj_dl, n_src, hot, env_i64("TGO_PR_SEG", kPrSegDefault), kTile, kMaxRows,
-                               threads_of(ctx), env_i64("TGO_PR_CPACK", 1) != 0, hc))
+                               threads_of(ctx), env_i64("TGO_PR_CPACK", 1) != 0, hc, win))
             return TGO_OK;                                // too small to block: plain gather
         lap("build (host)");
     }
@@ -316,6 +320,15 @@ int upload_cold_blocks(tgo_ctx* ctx, const std::vector<int64_t>& off, const std:
         cb.hcsr.nnz = static_cast<int64_t>(hc.hadj.size());
     }
     lap("hot row blocks+pack");
+    if (hc.win > 0) {                               // LDS window CSR: blocks over the active rows
+        const std::vector<int64_t> woff_act(hc.woff.begin(), hc.woff.begin() + n_rows + 1);
+        bool unused = false;
+        if (int rc = upload_row_blocks_dev(ctx, woff_act, cb.rb_win, nullptr, 0, &unused, kTile, kPackShift)) return rc;
+        HIP_TRY(upload(ctx, cb.woff, woff_act));
+        if (hc.d_widx.present()) adopt(ctx, cb.widx, hc.d_widx);
+        else HIP_TRY(upload(ctx, cb.widx, hc.widx));
+        cb.win = hc.win;
+    }
     HIP_TRY(upload(ctx, cb.hcsr.off, hc.hoff));
     HIP_TRY(upload(ctx, cb.poff, hc.poff));
     if (hc.d_cadj.present()) adopt(ctx, cb.cadj, hc.d_cadj);
@@ -414,7 +427,8 @@ int upload_graph(tgo_ctx* ctx, HostGraph& h, bool allow_segments = true) {
         // rows >= n_active have no entries at all: the hot pass skips them (their rank
         // after any update is (1-a)/N, written once at the end of the program)
         if (int rc = upload_cold_blocks(ctx, h.in.off, h.in.adj, h.n, env_i64("TGO_PR_HOT", kPrHotDefault), g.n_active,
-                                        g.cold_in, g.cold_in_ready, g.in.off, g.in.adj, g.in.nnz))
+                                        g.cold_in, g.cold_in_ready, g.in.off, g.in.adj, g.in.nnz,
+                                        env_i64("TGO_PR_WIN", kPrWinDefault)))
             return rc;
         lap("cold blocks");
     }

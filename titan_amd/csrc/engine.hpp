@@ -310,9 +310,22 @@ struct ColdBlocks {
     int hot_pipe = 0;           // hot pass as persistent workgroups that gather tile t+1 while
                                 // reducing tile t (TGO_PR_HOT_PIPE; gather_hot_pipe)
     int num_cus = 256;          // persistent grid: workgroups per CU x CUs
+    // LDS window pass (lds_window, spmv.hip): the rows' entries with source < win come from a
+    // copy of contrib[0, win) in LDS instead of L2 gathers; the pass writes every row's window
+    // sum into csum, which cold_fold then accumulates onto (win = 0: no window)
+    int64_t win = 0;
+    int64_t* woff = nullptr;    // n_rows+1
+    uint16_t* widx = nullptr;   // window entries (source ids < win), row-major
+    RowBlocks rb_win;           // CSR-adaptive blocks of the window CSR (bdesc used)
 };
 struct HostColdBlocks {
     int64_t hot = 0, seg = 0;
+    // LDS window (device build only): sources [0, win) of every row, as uint16, row-major —
+    // woff (n+1) and the entries; the hot CSR then holds sources [win, hot)
+    int64_t win = 0;
+    std::vector<int64_t> woff;
+    std::vector<uint16_t> widx;         // host build
+    DevArray<uint16_t> d_widx;          // device build
     std::vector<int64_t> hoff, poff, bbeg, bend;
     std::vector<int32_t> hadj, cadj, cpid, xblk, crow, bsrc;
     DevArray<int32_t> d_hadj, d_cadj;   // the device build keeps hadj / cadj on the device
@@ -325,11 +338,11 @@ struct HostColdBlocks {
 // false when nothing is cold (n <= hot) or the piece count overflows 32-bit indices.
 bool build_cold_blocks(const std::vector<int64_t>& off, const std::vector<int32_t>& adj, int64_t n_src,
                        int64_t hot, int64_t seg, int64_t tile, int64_t max_pieces, int threads, bool pack,
-                       HostColdBlocks& hc);
+                       HostColdBlocks& hc, int64_t win = 0);
 // pr_layout.hip: build_cold_blocks / pack_tiles on the device (same arrays)
 int build_cold_blocks_device(const int64_t* d_off, const int32_t* d_adj, int64_t n, int64_t nnz, int64_t n_src,
                              int64_t hot, int64_t seg, int64_t tile, int64_t max_pieces, bool pack, HostColdBlocks& hc,
-                             bool& built, hipStream_t s, std::string& err);
+                             bool& built, hipStream_t s, std::string& err, int64_t win = 0);
 int pack_tiles_device(int32_t* d_adj, int64_t m, const std::vector<int64_t>& tstart, const std::vector<int32_t>* tbase,
                       int shift, hipStream_t s, std::string& err);
 // part_ghost.hip: the partitioned PageRank ghost exchange

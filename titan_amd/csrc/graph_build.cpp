@@ -1048,14 +1048,15 @@ void weight_sorted_push(const HostGraph& g, HostCsr& ws, int threads) {
 // (a thread's rows follow the previous thread's rows in every segment).
 bool build_cold_blocks(const std::vector<int64_t>& off, const std::vector<int32_t>& adj, int64_t n_src,
                        int64_t hot, int64_t seg, int64_t tile, int64_t max_pieces, int threads, bool pack,
-                       HostColdBlocks& hc) {
+                       HostColdBlocks& hc, int64_t win) {
     const int64_t n = static_cast<int64_t>(off.size()) - 1;
     if (hot <= 0 || seg <= 0 || n_src <= hot || n <= 0) return false;
+    if (win < 0 || win > 65536 || win > hot) win = 0;       // the device build's rule (pr_layout.hip)
     const int64_t nseg = (n_src - hot + seg - 1) / seg;
     threads = std::max(1, std::min<int>(threads, static_cast<int>(std::max<int64_t>(1, n / 4096))));
     hc.hot = hot;
     hc.seg = seg;
-    std::vector<int64_t> hcount(n), npc(n);
+    std::vector<int64_t> hcount(n), npc(n), wcount(n, 0);
     std::vector<std::vector<int64_t>> tpieces(threads, std::vector<int64_t>(nseg, 0)),
         tentries(threads, std::vector<int64_t>(nseg, 0));
     // A row's cold entries grouped by segment (stable: list order inside a segment).  Lists
@@ -1083,9 +1084,13 @@ bool build_cold_blocks(const std::vector<int64_t>& off, const std::vector<int32_
                 std::vector<std::pair<int64_t, int32_t>> buf;
                 const auto [lo, hi] = range(t);
                 for (int64_t r = lo; r < hi; ++r) {
-                    int64_t h = 0;
-                    for (int64_t k = off[r]; k < off[r + 1]; ++k) h += adj[k] < hot;
+                    int64_t h = 0, wc = 0;
+                    for (int64_t k = off[r]; k < off[r + 1]; ++k) {
+                        h += adj[k] < hot && adj[k] >= win;
+                        wc += adj[k] < win;
+                    }
                     hcount[r] = h;
+                    wcount[r] = wc;
                     cold_runs(r, buf);
                     int64_t pcs = 0;
                     for (size_t i = 0; i < buf.size();) {
@@ -1107,6 +1112,12 @@ bool build_cold_blocks(const std::vector<int64_t>& off, const std::vector<int32_
     hc.cptr.assign(n + 1, 0);
     int64_t acc = 0;
     for (int64_t r = 0; r < n; ++r) { hc.hoff[r + 1] = hc.hoff[r] + hcount[r]; acc += npc[r]; }
+    hc.win = win;
+    if (win > 0) {
+        hc.woff.assign(n + 1, 0);
+        for (int64_t r = 0; r < n; ++r) hc.woff[r + 1] = hc.woff[r] + wcount[r];
+        hc.widx.assign(static_cast<size_t>(hc.woff[n]), 0);
+    }
     if (acc >= (int64_t(1) << 31)) return false;
     hc.crow.clear();
     for (int64_t r = 0; r < n; ++r) {
@@ -1142,9 +1153,11 @@ bool build_cold_blocks(const std::vector<int64_t>& off, const std::vector<int32_
                 std::vector<int64_t> pc = pbase[t], ec = ebase[t];
                 const auto [lo, hi] = range(t);
                 for (int64_t r = lo; r < hi; ++r) {
-                    int64_t h = hc.hoff[r];
-                    for (int64_t k = off[r]; k < off[r + 1]; ++k)
-                        if (adj[k] < hot) hc.hadj[h++] = adj[k];
+                    int64_t h = hc.hoff[r], wq = win > 0 ? hc.woff[r] : 0;
+                    for (int64_t k = off[r]; k < off[r + 1]; ++k) {
+                        if (adj[k] < win) hc.widx[wq++] = static_cast<uint16_t>(adj[k]);
+                        else if (adj[k] < hot) hc.hadj[h++] = adj[k];
+                    }
                     cold_runs(r, buf);
                     int64_t slot = hc.cptr[r];
                     for (size_t i = 0; i < buf.size();) {

@@ -70,23 +70,33 @@ __global__ void hot_counts(const int64_t* __restrict__ off, const int32_t* __res
         hcount[r] = lo - off[r];
     }
 }
-// hot prefix -> hadj; cold entry -> (segment << 32 | row, source) at its cold position
+// window prefix (sources < win) -> widx; the rest of the hot prefix -> hadj; cold entry ->
+// (segment << 32 | row, source) at its cold position.  wcount == nullptr: no window.
 __global__ void split_entries(const int64_t* __restrict__ off, const int32_t* __restrict__ adj, int64_t n, int64_t nnz,
                               const int64_t* __restrict__ hcount, const int64_t* __restrict__ hoff, int32_t hot,
                               int64_t seg, int32_t* __restrict__ hadj, uint64_t* __restrict__ ckey,
-                              int32_t* __restrict__ cval) {
+                              int32_t* __restrict__ cval, const int64_t* __restrict__ wcount,
+                              const int64_t* __restrict__ woff, uint16_t* __restrict__ widx) {
     for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < nnz; k += (int64_t)gridDim.x * blockDim.x) {
         const int64_t r = row_of(off, n, k);
         const int64_t j = k - off[r];
         const int32_t u = adj[k];
-        if (j < hcount[r]) {
-            hadj[hoff[r] + j] = u;
+        const int64_t wc = wcount ? wcount[r] : 0;
+        if (j < wc) {
+            widx[woff[r] + j] = static_cast<uint16_t>(u);
+        } else if (j < hcount[r]) {
+            hadj[hoff[r] + (j - wc)] = u;
         } else {
-            const int64_t c = (off[r] - hoff[r]) + (j - hcount[r]);      // cold entries before this one
+            // cold entries before this one: the row's earlier entries minus the hot and window ones
+            const int64_t c = (off[r] - hoff[r] - (wcount ? woff[r] : 0)) + (j - hcount[r]);
             ckey[c] = (static_cast<uint64_t>((u - hot) / seg) << 32) | static_cast<uint64_t>(r);
             cval[c] = u;
         }
     }
+}
+__global__ void sub_counts(const int64_t* __restrict__ a, const int64_t* __restrict__ b, int64_t m, int64_t* __restrict__ out) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = a[i] - b[i];
 }
 // run starts (a new (segment, row)) and piece starts (a run start or every tile-th entry of a run)
 __global__ void run_marks(const uint64_t* __restrict__ key, int64_t m, int64_t* __restrict__ rs) {
@@ -224,10 +234,11 @@ int pack_tiles_device(int32_t* d_adj, int64_t m, const std::vector<int64_t>& tst
 // a row is not sorted by source (then the caller keeps the host build).
 int build_cold_blocks_device(const int64_t* d_off, const int32_t* d_adj, int64_t n, int64_t nnz, int64_t n_src,
                              int64_t hot, int64_t seg, int64_t tile, int64_t max_pieces, bool pack, HostColdBlocks& hc,
-                             bool& built, hipStream_t s, std::string& err) {
+                             bool& built, hipStream_t s, std::string& err, int64_t win) {
     built = false;
     hc = HostColdBlocks();
     if (hot <= 0 || seg <= 0 || n_src <= hot || n <= 0 || hot >= INT32_MAX) return TGO_OK;
+    if (win < 0 || win > 65536 || win > hot) win = 0;       // uint16 window entries inside the hot range
     const int64_t nseg = (n_src - hot + seg - 1) / seg;
     Sort so{{}, 0, s};
     {
@@ -253,6 +264,27 @@ int build_cold_blocks_device(const int64_t* d_off, const int32_t* d_adj, int64_t
     PL_TRY(hipMemcpyAsync(&nhot, hoff.p + n, 8, hipMemcpyDeviceToHost, s));
     PL_TRY(hipStreamSynchronize(s));
     const int64_t C = nnz - nhot;
+    // LDS window: each row's sources < win leave the hot CSR for the window CSR
+    Buf<int64_t> wcount, woff;
+    Buf<uint16_t> widx;
+    int64_t nwin = 0;
+    if (win > 0) {
+        PL_TRY(wcount.alloc(n + 1));
+        PL_TRY(woff.alloc(n + 1));
+        hot_counts<<<grid(n), kB, 0, s>>>(d_off, d_adj, n, static_cast<int32_t>(win), wcount.p);
+        PL_TRY(hipMemsetAsync(wcount.p + n, 0, sizeof(int64_t), s));
+        PL_TRY(so.excl(wcount.p, woff.p, n + 1));
+        PL_TRY(hipMemcpyAsync(&nwin, woff.p + n, 8, hipMemcpyDeviceToHost, s));
+        PL_TRY(hipStreamSynchronize(s));
+        // the hot CSR keeps [wcount, hcount) of every row
+        Buf<int64_t> hc2;
+        PL_TRY(hc2.alloc(n + 1));
+        sub_counts<<<grid(n + 1), kB, 0, s>>>(hcount.p, wcount.p, n + 1, hc2.p);
+        PL_TRY(so.excl(hc2.p, hoff.p, n + 1));
+        PL_TRY(hipStreamSynchronize(s));
+        nhot -= nwin;
+        PL_TRY(widx.alloc(nwin));
+    }
     Buf<int32_t> hadj, cval, cadj;
     Buf<uint64_t> ckey, skey;
     PL_TRY(hadj.alloc(nhot));
@@ -261,7 +293,13 @@ int build_cold_blocks_device(const int64_t* d_off, const int32_t* d_adj, int64_t
     PL_TRY(ckey.alloc(C));
     PL_TRY(skey.alloc(C));
     if (nnz) split_entries<<<grid(nnz), kB, 0, s>>>(d_off, d_adj, n, nnz, hcount.p, hoff.p, static_cast<int32_t>(hot), seg,
-                                                   hadj.p, ckey.p, cval.p);
+                                                   hadj.p, ckey.p, cval.p, win > 0 ? wcount.p : nullptr, woff.p, widx.p);
+    if (win > 0) {
+        PL_TRY(fetch(hc.woff, woff.p, n + 1, s));
+        hc.win = win;
+        PL_TRY(hipStreamSynchronize(s));
+        hc.d_widx.own(widx.take(), nwin);
+    }
     if (C) PL_TRY(so.pairs(ckey.p, skey.p, cval.p, cadj.p, C, 32 + bits_for(nseg)));
     ckey.release();
     cval.release();

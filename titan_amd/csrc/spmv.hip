@@ -590,12 +590,88 @@ __global__ void __launch_bounds__(kBlock) cold_gather(const int64_t* __restrict_
     }
 }
 
-// Per-row cold sums of the rows that own pieces: the pieces added in segment order.
+// LDS window pass of the cache-blocked PageRank gather.  The hottest `win` sources of the
+// degree-grouped order (about 30 % of RMAT-24's entries for 15.9 K sources) are read from a copy
+// of contrib[0, win) in LDS — no L2 request per entry, where the other passes pay one per
+// distinct line (the update is bound by the L2 request rate: profiles/r04e_pmc/).  Persistent
+// workgroups, one per CU (the window takes 124 KB of the CU's 160 KB LDS), load the window once
+// per update and walk the CSR-adaptive tiles of the window CSR (2-byte source ids, row-major):
+// a tile's entries are staged in LDS in row order with coalesced index loads, then reduced
+// thread-per-row (many short rows) or wave-per-row (<= 64 rows, fixed shuffle tree); a row with
+// more window entries than a tile (a hub) is summed by the whole workgroup, strided per thread
+// and reduced in wave order.  Every row of [0, n_rows) gets its window sum in csum, which
+// cold_fold then accumulates the cold pieces onto: a fixed association, bitwise reproducible.
+constexpr int kWinThreads = 512;
+constexpr int kWinPer = static_cast<int>(kTile / kWinThreads);      // 8 entries per thread per tile
+__global__ void __launch_bounds__(kWinThreads) lds_window(const int64_t* __restrict__ woff,
+        const uint16_t* __restrict__ widx, const int64_t* __restrict__ bdesc, int64_t nblocks, int32_t win,
+        const double* __restrict__ msg, double* __restrict__ csum) {
+    extern __shared__ double lds[];
+    double* s_win = lds;
+    double* s_val = lds + win;
+    constexpr int kWaves = kWinThreads / 64;
+    const int wave = threadIdx.x >> 6;
+    for (int i = threadIdx.x; i < win; i += kWinThreads) s_win[i] = msg[i];
+    __syncthreads();
+    for (int64_t t = blockIdx.x; t < nblocks; t += gridDim.x) {
+        const int64_t r0 = bdesc[2 * t], s0 = bdesc[2 * t + 1];
+        const int64_t r1 = bdesc[2 * t + 2], nnz = bdesc[2 * t + 3] - s0;
+        if (nnz > kTile) {                            // one long row (build_row_blocks marks it alone)
+            double acc = 0.0;
+            for (int64_t k = threadIdx.x; k < nnz; k += kWinThreads) acc = acc + s_win[widx[s0 + k]];
+            acc = wave_sum(acc);
+            if (lane() == 0) s_val[wave] = acc;
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                double tot = 0.0;
+                for (int w = 0; w < kWaves; ++w) tot = tot + s_val[w];
+                csum[r0] = tot;
+            }
+            __syncthreads();
+            continue;
+        }
+        {
+            uint16_t v[kWinPer];
+#pragma unroll
+            for (int j = 0; j < kWinPer; ++j) {
+                const int64_t k = threadIdx.x + static_cast<int64_t>(j) * kWinThreads;
+                v[j] = k < nnz ? widx[s0 + k] : 0;
+            }
+#pragma unroll
+            for (int j = 0; j < kWinPer; ++j) {
+                const int k = threadIdx.x + j * kWinThreads;
+                if (k < nnz) s_val[k] = s_win[v[j]];
+            }
+        }
+        __syncthreads();
+        if (r1 - r0 > 64) {
+            for (int64_t i = r0 + threadIdx.x; i < r1; i += kWinThreads) {
+                double sum = 0.0;
+                const int64_t e = woff[i + 1] - s0;
+                for (int64_t k = woff[i] - s0; k < e; ++k) sum = sum + s_val[k];
+                csum[i] = sum;
+            }
+        } else {
+            for (int64_t i = r0 + wave; i < r1; i += kWaves) {
+                double sum = 0.0;
+                const int64_t e = woff[i + 1] - s0;
+                for (int64_t k = woff[i] - s0 + lane(); k < e; k += 64) sum = sum + s_val[k];
+                sum = wave_sum(sum);
+                if (lane() == 0) csum[i] = sum;
+            }
+        }
+        __syncthreads();                              // s_val is rewritten by the next tile
+    }
+}
+
+// Per-row cold sums of the rows that own pieces: the pieces added in segment order (onto the
+// row's LDS window sum when the window pass ran: acc).
 __global__ void cold_fold(const int32_t* __restrict__ crow, int64_t ncrows, const uint32_t* __restrict__ cptr,
-                          const int32_t* __restrict__ cpid, const double* __restrict__ partial, double* __restrict__ csum) {
+                          const int32_t* __restrict__ cpid, const double* __restrict__ partial, double* __restrict__ csum,
+                          bool acc) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < ncrows; i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t r = crow[i];
-        double s = 0.0;
+        double s = acc ? csum[r] : 0.0;
         const uint32_t e = cptr[r + 1];
         for (uint32_t k = cptr[r]; k < e; ++k) s += partial[cpid[k]];
         csum[r] = s;
@@ -663,6 +739,20 @@ static bool row_prefetch() {
     return on;
 }
 hipError_t k_pr_cold_phase(const ColdBlocks& cb, const double* contrib, hipStream_t s) {
+    const bool window = cb.win > 0 && cb.rb_win.nblocks > 0;
+    if (window) {
+        const size_t lds = static_cast<size_t>(cb.win + kTile) * sizeof(double);
+        static size_t lds_set = 0;                    // the >64 KB dynamic LDS limit, raised once
+        if (lds > lds_set) {
+            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&lds_window),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+            if (e != hipSuccess) return e;
+            lds_set = lds;
+        }
+        const unsigned g = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(cb.rb_win.nblocks, cb.num_cus)));
+        lds_window<<<g, kWinThreads, lds, s>>>(cb.woff, cb.widx, cb.rb_win.bdesc, cb.rb_win.nblocks,
+                                                static_cast<int32_t>(cb.win), contrib, cb.csum);
+    }
     if (cb.max_xcd_blocks > 0) {
         const unsigned g = static_cast<unsigned>(cb.max_xcd_blocks * 8);
         if (cb.cpacked && row_prefetch())
@@ -677,7 +767,7 @@ hipError_t k_pr_cold_phase(const ColdBlocks& cb, const double* contrib, hipStrea
     }
     int64_t g = (cb.n_crows + kBlock - 1) / kBlock;
     g = std::max<int64_t>(1, std::min<int64_t>(g, 65536));
-    cold_fold<<<static_cast<unsigned>(g), kBlock, 0, s>>>(cb.crow, cb.n_crows, cb.cptr, cb.cpid, cb.partial, cb.csum);
+    cold_fold<<<static_cast<unsigned>(g), kBlock, 0, s>>>(cb.crow, cb.n_crows, cb.cptr, cb.cpid, cb.partial, cb.csum, window);
     return hipGetLastError();
 }
 
