@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-4 call f: the LDS window pass of PageRank: parity tests, then A/B of window sizes.
+# Round-4 call f2: the LDS window pass (wave items, prefetch): parity tests, then A/B of window sizes.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out/r04f
 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
@@ -9,6 +9,6 @@ timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method threa
     tests/test_gpu_assembly.py -k "pagerank" "tests/test_gpu_fullsize.py::test_config3_rmat24_pagerank_capped" \
     > gpurun_out/r04f/gpu_tests2.log 2>&1
 rc=$?; tail -5 gpurun_out/r04f/gpu_tests2.log; [ $rc -eq 0 ] || exit $rc
-bash scripts/gpu_pr_ab.sh r04f_win "TGO_PR_WIN=0" "TGO_PR_WIN=15872" "TGO_PR_WIN=8192" "TGO_PR_WIN=12288" "TGO_PR_WIN=4096" \
+bash scripts/gpu_pr_ab.sh r04f_win "TGO_PR_WIN=0" "TGO_PR_WIN=15872" "TGO_PR_WIN=8192" "TGO_PR_WIN=4096" "TGO_PR_WIN=15872 TGO_PR_SKIP_BELOW=393216" \
     > gpurun_out/r04f/ab.log 2>&1
 rc=$?; cat gpurun_out/r04f/ab.log; exit $rc

@@ -157,7 +157,7 @@ int64_t env_i64(const char* name, int64_t dflt) {
     return v ? std::atoll(v) : dflt;
 }
 constexpr int64_t kPrHotDefault = 393216, kPrSegDefault = 393216;   // 3 MB each (profiles/r02an_pr_hot_seg_probe*.log)
-// LDS window of the hottest sources (lds_window, spmv.hip): 15872 doubles = 124 KB of a CU's
+// LDS window of the hottest sources (lds_window, spmv.hip): 15872 doubles = 124 KB of a CUs
 // 160 KB LDS beside the 32 KB tile; 0 = off
 constexpr int64_t kPrWinDefault = 15872;
 
@@ -200,9 +200,9 @@ hipError_t upload_row_blocks(tgo_ctx* ctx, const std::vector<int64_t>& off, RowB
 // the same blocks (built on the host from the offsets) and the same packed words.  *packed =
 // false (d_adj untouched) when a source is too wide for the slot space (pack_tiles' rule).
 int upload_row_blocks_dev(tgo_ctx* ctx, const std::vector<int64_t>& off, RowBlocks& rb, int32_t* d_adj,
-                          int32_t max_src, bool* packed, int64_t tile, int shift) {
+                          int32_t max_src, bool* packed, int64_t tile, int shift, int64_t max_rows = kMaxRows) {
     std::vector<int64_t> blk, crow, cbeg, cend, lrow, lch;
-    build_row_blocks(off, tile, kMaxRows, blk, crow, cbeg, cend, lrow, lch);
+    build_row_blocks(off, tile, max_rows, blk, crow, cbeg, cend, lrow, lch);
     *packed = false;
     const int64_t src_limit = shift == kPackShift ? (int64_t(1) << (31 - shift)) : (int64_t(1) << (32 - shift));
     if (d_adj && shift >= 1 && shift <= 20 && tile <= (int64_t(1) << shift) && max_src < src_limit) {
@@ -323,7 +323,8 @@ int upload_cold_blocks(tgo_ctx* ctx, const std::vector<int64_t>& off, const std:
     if (hc.win > 0) {                               // LDS window CSR: blocks over the active rows
         const std::vector<int64_t> woff_act(hc.woff.begin(), hc.woff.begin() + n_rows + 1);
         bool unused = false;
-        if (int rc = upload_row_blocks_dev(ctx, woff_act, cb.rb_win, nullptr, 0, &unused, kTile, kPackShift)) return rc;
+        // wave items of the window pass (lds_window): <= 256 entries, <= 64 rows
+        if (int rc = upload_row_blocks_dev(ctx, woff_act, cb.rb_win, nullptr, 0, &unused, 256, kPackShift, 64)) return rc;
         HIP_TRY(upload(ctx, cb.woff, woff_act));
         if (hc.d_widx.present()) adopt(ctx, cb.widx, hc.d_widx);
         else HIP_TRY(upload(ctx, cb.widx, hc.widx));

@@ -601,66 +601,72 @@ __global__ void __launch_bounds__(kBlock) cold_gather(const int64_t* __restrict_
 // more window entries than a tile (a hub) is summed by the whole workgroup, strided per thread
 // and reduced in wave order.  Every row of [0, n_rows) gets its window sum in csum, which
 // cold_fold then accumulates the cold pieces onto: a fixed association, bitwise reproducible.
-constexpr int kWinThreads = 512;
-constexpr int kWinPer = static_cast<int>(kTile / kWinThreads);      // 8 entries per thread per tile
+constexpr int kWinThreads = 1024;                    // 16 independent waves per CU
+constexpr int kWinWaveTile = 256;                    // entries per wave item (4 per lane); <= 64 rows
+
+__device__ __forceinline__ void wave_sync() {          // a wave's LDS writes visible to its own later reads
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Every wave works alone on items t = global wave, + all waves, ...: an item is <= 64 rows with
+// <= 256 window entries (build_row_blocks(tile 256, 64 rows)), or one longer row.  The wave
+// loads the next item's descriptor, indices and row bounds before it reduces the current one
+// from LDS, so each wave keeps its global loads in flight; no workgroup barrier after the
+// window is loaded.
 __global__ void __launch_bounds__(kWinThreads) lds_window(const int64_t* __restrict__ woff,
-        const uint16_t* __restrict__ widx, const int64_t* __restrict__ bdesc, int64_t nblocks, int32_t win,
+        const uint16_t* __restrict__ widx, const int64_t* __restrict__ bdesc, int64_t nitems, int32_t win,
         const double* __restrict__ msg, double* __restrict__ csum) {
     extern __shared__ double lds[];
     double* s_win = lds;
-    double* s_val = lds + win;
-    constexpr int kWaves = kWinThreads / 64;
     const int wave = threadIdx.x >> 6;
+    double* s_val = lds + win + wave * kWinWaveTile;
     for (int i = threadIdx.x; i < win; i += kWinThreads) s_win[i] = msg[i];
     __syncthreads();
-    for (int64_t t = blockIdx.x; t < nblocks; t += gridDim.x) {
-        const int64_t r0 = bdesc[2 * t], s0 = bdesc[2 * t + 1];
-        const int64_t r1 = bdesc[2 * t + 2], nnz = bdesc[2 * t + 3] - s0;
-        if (nnz > kTile) {                            // one long row (build_row_blocks marks it alone)
+    constexpr int kPerLane = kWinWaveTile / 64;
+    const int64_t nwaves = static_cast<int64_t>(gridDim.x) * (kWinThreads / 64);
+    struct Item { int64_t r0, s0, r1, nnz; uint16_t v[kPerLane]; int64_t rb, re; };
+    auto fetch = [&](int64_t t, Item& it) {
+        it.r0 = it.s0 = it.r1 = 0; it.nnz = 0; it.rb = it.re = 0;
+        if (t >= nitems) return;
+        it.r0 = bdesc[2 * t]; it.s0 = bdesc[2 * t + 1];
+        it.r1 = bdesc[2 * t + 2]; it.nnz = bdesc[2 * t + 3] - it.s0;
+        if (it.nnz > kWinWaveTile) return;            // a long row: streamed when processed
+#pragma unroll
+        for (int j = 0; j < kPerLane; ++j) {
+            const int k = lane() + 64 * j;
+            it.v[j] = k < it.nnz ? widx[it.s0 + k] : 0;
+        }
+        const int64_t i = it.r0 + lane();
+        if (i < it.r1) { it.rb = woff[i]; it.re = woff[i + 1]; }
+    };
+    Item cur, nxt;
+    int64_t t = blockIdx.x * static_cast<int64_t>(kWinThreads / 64) + wave;
+    fetch(t, cur);
+    for (; t < nitems; t += nwaves) {
+        fetch(t + nwaves, nxt);                       // next item's loads in flight
+        if (cur.nnz > kWinWaveTile) {                 // one long row: lanes stride its entries
             double acc = 0.0;
-            for (int64_t k = threadIdx.x; k < nnz; k += kWinThreads) acc = acc + s_win[widx[s0 + k]];
+            for (int64_t k = lane(); k < cur.nnz; k += 64) acc = acc + s_win[widx[cur.s0 + k]];
             acc = wave_sum(acc);
-            if (lane() == 0) s_val[wave] = acc;
-            __syncthreads();
-            if (threadIdx.x == 0) {
-                double tot = 0.0;
-                for (int w = 0; w < kWaves; ++w) tot = tot + s_val[w];
-                csum[r0] = tot;
-            }
-            __syncthreads();
-            continue;
-        }
-        {
-            uint16_t v[kWinPer];
+            if (lane() == 0) csum[cur.r0] = acc;
+        } else {
 #pragma unroll
-            for (int j = 0; j < kWinPer; ++j) {
-                const int64_t k = threadIdx.x + static_cast<int64_t>(j) * kWinThreads;
-                v[j] = k < nnz ? widx[s0 + k] : 0;
+            for (int j = 0; j < kPerLane; ++j) {
+                const int k = lane() + 64 * j;
+                if (k < cur.nnz) s_val[k] = s_win[cur.v[j]];
             }
-#pragma unroll
-            for (int j = 0; j < kWinPer; ++j) {
-                const int k = threadIdx.x + j * kWinThreads;
-                if (k < nnz) s_val[k] = s_win[v[j]];
-            }
-        }
-        __syncthreads();
-        if (r1 - r0 > 64) {
-            for (int64_t i = r0 + threadIdx.x; i < r1; i += kWinThreads) {
+            wave_sync();
+            const int64_t i = cur.r0 + lane();
+            if (i < cur.r1) {
                 double sum = 0.0;
-                const int64_t e = woff[i + 1] - s0;
-                for (int64_t k = woff[i] - s0; k < e; ++k) sum = sum + s_val[k];
+                for (int64_t k = cur.rb - cur.s0; k < cur.re - cur.s0; ++k) sum = sum + s_val[k];
                 csum[i] = sum;
             }
-        } else {
-            for (int64_t i = r0 + wave; i < r1; i += kWaves) {
-                double sum = 0.0;
-                const int64_t e = woff[i + 1] - s0;
-                for (int64_t k = woff[i] - s0 + lane(); k < e; k += 64) sum = sum + s_val[k];
-                sum = wave_sum(sum);
-                if (lane() == 0) csum[i] = sum;
-            }
+            wave_sync();                              // s_val is rewritten by the next item
         }
-        __syncthreads();                              // s_val is rewritten by the next tile
+        cur = nxt;
     }
 }
 
@@ -741,7 +747,7 @@ static bool row_prefetch() {
 hipError_t k_pr_cold_phase(const ColdBlocks& cb, const double* contrib, hipStream_t s) {
     const bool window = cb.win > 0 && cb.rb_win.nblocks > 0;
     if (window) {
-        const size_t lds = static_cast<size_t>(cb.win + kTile) * sizeof(double);
+        const size_t lds = static_cast<size_t>(cb.win + (kWinThreads / 64) * kWinWaveTile) * sizeof(double);
         static size_t lds_set = 0;                    // the >64 KB dynamic LDS limit, raised once
         if (lds > lds_set) {
             const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&lds_window),
