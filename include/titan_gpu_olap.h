@@ -325,6 +325,21 @@ int  tgo_copy_multi_distances(tgo_ctx* ctx, int32_t source, int64_t* dist_out);
  * entries; 0 = every source pulled; < 0 = the default (TGO_MS_SPLIT or 0.005). */
 enum { TGO_TUNE_MS_SPLIT = 1 };
 int  tgo_set_tuning(tgo_ctx* ctx, int32_t key, double value);
+
+/* ---- Tracing (the reference's only hook is FulgoraGraphComputer.java:143,307
+ * memory.setRuntime).  Every program marks its supersteps / levels / phases as spans:
+ * TGO_TRACE_ROCTX: roctx ranges (rocprofv3 --marker-trace shows them beside the kernels);
+ * TGO_TRACE_JSON: Chrome-trace events ("traceEvents", ph "X"; cat "device" spans carry GPU
+ * times from HIP events on the engine stream, cat "host" spans host times; args = the level,
+ * iteration, frontier size ...), written by tgo_trace_flush (json_path NULL = the path given
+ * to tgo_trace_enable or TGO_TRACE_JSON; TGO_TRACE_JSON also flushes at exit).  Process-wide.
+ * tgo_trace_range_push / _pop: the caller's own ranges (per thread, nested). */
+enum { TGO_TRACE_JSON = 1, TGO_TRACE_ROCTX = 2 };
+int  tgo_trace_enable(const char* json_path, int32_t flags);   /* flags 0 = off */
+int  tgo_trace_flush(const char* json_path);
+int  tgo_trace_clear(void);
+int  tgo_trace_range_push(const char* name);
+int  tgo_trace_range_pop(void);
 /* After tgo_bfs_multi with TGO_FLAG_STATS: per seed, reached vertices and their entries. */
 int  tgo_multi_stats(tgo_ctx* ctx, int64_t* reached, int64_t* reached_entries);
 int  tgo_copy_distances(tgo_ctx* ctx, int64_t* dist_out);

@@ -3,7 +3,7 @@
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out/r04f
 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
-    tests/test_gpu_parity.py -k "pagerank" > gpurun_out/r04f/gpu_tests.log 2>&1
+    tests/test_gpu_parity.py -k "pagerank" tests/test_gpu_trace.py > gpurun_out/r04f/gpu_tests.log 2>&1
 rc=$?; tail -5 gpurun_out/r04f/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
     tests/test_gpu_assembly.py -k "pagerank" "tests/test_gpu_fullsize.py::test_config3_rmat24_pagerank_capped" \

@@ -34,6 +34,7 @@ RESULT_DISTANCE, RESULT_PAGERANK, RESULT_DEGREE, RESULT_VALUES = 0, 1, 2, 3
 SSSP_HOP_BOUNDED, SSSP_DELTA = 0, 1
 FLAG_STATS = 1
 TUNE_MS_SPLIT = 1          # tgo_set_tuning keys
+TRACE_JSON, TRACE_ROCTX = 1, 2   # tgo_trace_enable flags
 DIST_ABSENT = -(1 << 63)
 ABI_VERSION = 2
 COMBINE_SUM, COMBINE_MIN, COMBINE_MAX = 0, 1, 2
@@ -140,6 +141,7 @@ EXPORTS = [
     "tgo_bfs",
     "tgo_sssp", "tgo_copy_distances", "tgo_pagerank", "tgo_walkcount", "tgo_stats_get", "tgo_sync",
     "tgo_bfs_multi", "tgo_copy_multi_distances", "tgo_multi_stats", "tgo_set_tuning",
+    "tgo_trace_enable", "tgo_trace_flush", "tgo_trace_clear", "tgo_trace_range_push", "tgo_trace_range_pop",
     "tgo_gather", "tgo_combine_global", "tgo_dense_ids", "tgo_decode_edge_entry", "tgo_result_rows",
     "tgo_gather_lists", "tgo_result_rows_values",
     "tgo_rmat_edges", "tgo_rmat_edges_device", "tgo_rmat_partition_device", "tgo_pick_roots", "tgo_synth_rows",
@@ -204,6 +206,11 @@ def load() -> C.CDLL:
         "tgo_copy_multi_distances": (C.c_int, [vp, C.c_int32, _i64p]),
         "tgo_multi_stats": (C.c_int, [vp, _i64p, _i64p]),
         "tgo_set_tuning": (C.c_int, [vp, C.c_int32, C.c_double]),
+        "tgo_trace_enable": (C.c_int, [C.c_char_p, C.c_int32]),
+        "tgo_trace_flush": (C.c_int, [C.c_char_p]),
+        "tgo_trace_clear": (C.c_int, []),
+        "tgo_trace_range_push": (C.c_int, [C.c_char_p]),
+        "tgo_trace_range_pop": (C.c_int, []),
         "tgo_gather": (C.c_int, [vp, P(GatherArgs), vp, P(C.c_uint8), vp, P(C.c_uint8)]),
         "tgo_gather_lists": (C.c_int, [vp, P(GatherArgs), vp, P(C.c_uint8), _i64p, vp]),
         "tgo_result_rows_values": (C.c_int, [vp, P(ResultArgs), vp, P(C.c_uint8), P(ResultSize), P(RowsBuf)]),

@@ -19,6 +19,7 @@
 #include <hip/hip_runtime_api.h>
 #include "codec.hpp"
 #include "engine.hpp"
+#include "trace.hpp"
 #include "../../include/titan_gpu_olap_part.h"
 
 using namespace tgo;
@@ -249,9 +250,11 @@ int upload_cold_blocks(tgo_ctx* ctx, const std::vector<int64_t>& off, const std:
     static const bool trace = env_i64("TGO_TRACE", 0) != 0;
     auto t_last = std::chrono::steady_clock::now();
     auto lap = [&](const char* what) {
-        if (!trace) return;
+        if (!trace && !tracing()) return;
         const auto now = std::chrono::steady_clock::now();
-        std::fprintf(stderr, "[tgo]   cold %-18s %8.1f ms\n", what, std::chrono::duration<double, std::milli>(now - t_last).count());
+        const double ms = std::chrono::duration<double, std::milli>(now - t_last).count();
+        if (trace) std::fprintf(stderr, "[tgo]   cold %-18s %8.1f ms\n", what, ms);
+        trace_complete(std::string("pagerank_layout.") + what, ms * 1e3);
         t_last = now;
     };
     bool on_dev = false;
@@ -368,9 +371,11 @@ int upload_graph(tgo_ctx* ctx, HostGraph& h, bool allow_segments = true) {
     static const bool trace = env_i64("TGO_TRACE", 0) != 0;
     auto t_last = std::chrono::steady_clock::now();
     auto lap = [&](const char* what) {
-        if (!trace) return;
+        if (!trace && !tracing()) return;
         const auto now = std::chrono::steady_clock::now();
-        std::fprintf(stderr, "[tgo] upload %-14s %8.1f ms\n", what, std::chrono::duration<double, std::milli>(now - t_last).count());
+        const double ms = std::chrono::duration<double, std::milli>(now - t_last).count();
+        if (trace) std::fprintf(stderr, "[tgo] upload %-14s %8.1f ms\n", what, ms);
+        trace_complete(std::string("upload.") + what, ms * 1e3);
         t_last = now;
     };
     g.n = h.n;
@@ -616,6 +621,7 @@ int run_bfs(tgo_ctx* ctx, int64_t seed, int max_depth, int scope) {
                 HIP_TRY(k_bfs_queue(push, g.n_active, s.fb, s.q[cur], s.qdeg, s.cnt, st));
             }
             queued = !bottom_up;
+            DevSpan span(st, "bfs.level", {"level", L}, {"bottom_up", bottom_up ? 1 : 0});
             if (bottom_up) {
                 HIP_TRY(k_level_prep(s.cnt, s.nb, words, nullptr, st));
                 // words past n_active hold only entry-less vertices: nothing to find there
@@ -626,6 +632,7 @@ int run_bfs(tgo_ctx* ctx, int64_t seed, int max_depth, int scope) {
                 // qdeg is reused for the next queue's degrees after the scan consumed it
                 HIP_TRY(k_td_expand(push, s.q[cur], s.qpre, qlen, s.level, s.vb, s.nb, s.q[cur ^ 1], s.qdeg, s.cnt, L + 1, st));
             }
+            span.end();
             int rc = read_counters(ctx);
             if (rc) return rc;
             qlen = static_cast<int64_t>(s.hcnt->qlen);
@@ -639,6 +646,7 @@ int run_bfs(tgo_ctx* ctx, int64_t seed, int max_depth, int scope) {
         }
     }
     HIP_TRY(k_level_to_dist(s.level, s.dist, n, st));
+    trace_resolve(st);
     ctx->st.levels = levels;
     ctx->st.iterations = max_depth;   // the reference always runs iterations 0..maxDepth
     return TGO_OK;
@@ -659,10 +667,12 @@ int run_sssp(tgo_ctx* ctx, int64_t seed, int max_depth, int scope, bool weighted
         int cur = 0;
         for (int L = 0; L < max_depth && qlen > 0; ++L) {
             // counters, "improved this level" marks, scan tail
+            DevSpan span(st, "sssp.superstep", {"superstep", L}, {"queue", qlen});
             HIP_TRY(k_level_prep(s.cnt, s.vb, words, s.qdeg + qlen, st));
             HIP_TRY(scan_exclusive_i64(s.cub_tmp, s.cub_bytes, s.qdeg, s.qpre, qlen + 1, st));
             int rc;
             HIP_TRY(k_sssp_relax(push, s.q[cur], s.qpre, qlen, s.msg, s.dist, s.vb, s.q[cur ^ 1], s.qdeg, s.cnt, weighted ? 1 : 0, st));
+            span.end();
             rc = read_counters(ctx);
             if (rc) return rc;
             if (s.hcnt->err) return fail(ctx, TGO_E_PROGRAM,
@@ -675,6 +685,7 @@ int run_sssp(tgo_ctx* ctx, int64_t seed, int max_depth, int scope, bool weighted
         }
     }
     HIP_TRY(k_dist_finalize(s.dist, n, st));
+    trace_resolve(st);
     ctx->st.levels = levels;
     ctx->st.iterations = max_depth;
     return TGO_OK;
@@ -714,12 +725,14 @@ int run_delta_device(tgo_ctx* ctx, int64_t seed, int64_t delta) {
     // takes nothing); a run needs far fewer than 4n + 64 steps — the bound only stops a bug
     const int64_t max_steps = 4 * n + 64;
     for (int64_t steps = 0;;) {
+        DevSpan span(st, "sssp.delta_steps", {"first_step", steps}, {"steps", batch});
         for (int k = 0; k < batch; ++k) {
             HIP_TRY(k_ds_loop_step(g.push_ws, s.ds_light, s.vb, s.ds_member, n, s.dist, s.msg, s.ds_q, s.ds_qp,
                                    s.ds_loop, cur, delta, st));
             cur ^= 1;
         }
         steps += batch;
+        span.end();
         HIP_TRY(hipMemcpyAsync(&h, s.ds_loop, sizeof(DsLoop), hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
         if (h.err) return fail(ctx, TGO_E_PROGRAM, "vertex program failed: a traversed edge has no value for the weight property");
@@ -727,6 +740,7 @@ int run_delta_device(tgo_ctx* ctx, int64_t seed, int64_t delta) {
         if (steps > max_steps) return fail(ctx, TGO_E_HIP, "delta-stepping: the device loop did not converge");
     }
     HIP_TRY(k_dist_finalize(s.dist, n, st));
+    trace_resolve(st);
     if (trace) std::fprintf(stderr, "[tgo] delta %lld (device loop): %llu phases, %llu buckets, %llu extractions, %llu entries relaxed\n",
                             (long long)delta, h.phases, h.buckets, h.extractions, h.relaxed);
     ctx->st.levels = static_cast<int32_t>(h.phases);
@@ -1022,6 +1036,7 @@ int tgo_load_rows(tgo_ctx* ctx, const tgo_rows* rows, const tgo_schema* schema, 
 }
 
 int tgo_finish_load(tgo_ctx* ctx) {
+    Span load_span("load.finish_rows");
     if (!ctx) return TGO_E_INVALID;
     if (!ctx->staging.active) return fail(ctx, TGO_E_STATE, "tgo_finish_load without tgo_load_rows");
     (void)hipSetDevice(ctx->opts.device);
@@ -1058,6 +1073,7 @@ int tgo_finish_load(tgo_ctx* ctx) {
 }
 
 int tgo_load_edges(tgo_ctx* ctx, const tgo_edges* edges, const tgo_load_opts* opts) {
+    Span load_span("load.edges");
     if (!ctx) return TGO_E_INVALID;
     ctx->res_kind = -1;
     if (!edges || !opts || (edges->m > 0 && (!edges->src || !edges->dst)))
@@ -1086,6 +1102,7 @@ int tgo_load_csr(tgo_ctx* ctx, int64_t n, const int64_t* titan_ids, const int64_
                  const int32_t* out_w, const int64_t* in_off, const int32_t* in_idx, const int32_t* in_w,
                  const tgo_load_opts* opts) {
     if (!ctx) return TGO_E_INVALID;
+    Span load_span("load.csr");
     ctx->res_kind = -1;
     if (!opts || !out_off || !in_off) return fail(ctx, TGO_E_INVALID, "null argument");
     if (opts->scope < 0 || opts->scope > 2) return fail(ctx, TGO_E_INVALID, "invalid scope");
@@ -1299,6 +1316,7 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
     bool pulled = false;        // the previous level pulled
     for (int L = 0; L < depth && qlen > 0; ++L) {
         const bool use_pull = static_cast<double>(mf) * ms_alpha > static_cast<double>(total);
+        DevSpan span(st, "msbfs.level", {"level", L}, {"pull", use_pull ? 1 : 0});
         if ((rc = ms_planes_for(ctx, L + 1))) return rc;
         if (!use_pull && !queued) {     // the frontier's queue, for the push level's scan
             HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
@@ -1387,6 +1405,7 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
         return fail(ctx, TGO_E_UNSUPPORTED, "multi-source BFS stores levels as uint16: depth > 65534");
     HIP_TRY(hipEventRecord(ctx->ev1, st));
     HIP_TRY(hipEventSynchronize(ctx->ev1));
+    trace_resolve(st);
     float ms = 0;
     HIP_TRY(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
     ctx->st.last_kernel_ms = ms;
@@ -1478,10 +1497,16 @@ int tgo_pagerank(tgo_ctx* ctx, const tgo_pr_args* a, double* pr_out) {
         for (int it = 2; it <= a->max_iterations; ++it) {
             // the PAGE_RANK property is only read after the last superstep: write it there
             double* pr_it = it == a->max_iterations ? pr : nullptr;
-            if (blocked)
-                HIP_TRY(k_pr_iter_cold(g.cold_in, contrib, edge_count, pr_it, contrib_next, s.partial, a->alpha, base,
+            DevSpan span(st, "pagerank.update", {"iteration", it});
+            if (blocked) {
+                {
+                    DevSpan ph(st, "pagerank.window_cold_phase", {"iteration", it});
+                    HIP_TRY(k_pr_cold_phase(g.cold_in, contrib, st));
+                }
+                DevSpan ph(st, "pagerank.hot_phase", {"iteration", it});
+                HIP_TRY(k_pr_hot_phase(g.cold_in, contrib, edge_count, pr_it, contrib_next, s.partial, a->alpha, base,
                                        st));
-            else
+            } else
                 HIP_TRY(k_pr_iter(g.in, g.rb_in, contrib, edge_count, pr_it, contrib_next, s.partial, a->alpha, base,
                                   n, tune, st));
             std::swap(contrib, contrib_next);
@@ -1491,6 +1516,7 @@ int tgo_pagerank(tgo_ctx* ctx, const tgo_pr_args* a, double* pr_out) {
     }
     HIP_TRY(hipEventRecord(ctx->ev1, st));
     HIP_TRY(hipEventSynchronize(ctx->ev1));
+    trace_resolve(st);
     float ms = 0;
     HIP_TRY(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
     ctx->st.last_kernel_ms = ms;
@@ -1523,11 +1549,13 @@ int tgo_walkcount(tgo_ctx* ctx, int32_t k, int32_t* out) {
     int32_t* b = reinterpret_cast<int32_t*>(s.vec[1]);
     HIP_TRY(k_fill_i32(a, 1, n, st));                  // iteration 0: every vertex sends 1
     for (int it = 1; it <= k; ++it) {
+        DevSpan span(st, "degree_counter.superstep", {"iteration", it});
         HIP_TRY(k_walk_iter(g.out, g.rb_out, a, b, reinterpret_cast<int32_t*>(s.partial), n, st));
         std::swap(a, b);
     }
     HIP_TRY(hipEventRecord(ctx->ev1, st));
     HIP_TRY(hipEventSynchronize(ctx->ev1));
+    trace_resolve(st);
     float ms = 0;
     HIP_TRY(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
     ctx->st.last_kernel_ms = ms;
@@ -1648,6 +1676,7 @@ int tgo_load_partition(tgo_ctx* ctx, int64_t n_global, int64_t lo, int64_t hi, c
 int tgo_load_partition_layout(tgo_ctx* ctx, int64_t n_global, int64_t lo, int64_t hi, const tgo_edges* edges,
                               const tgo_load_opts* opts, const int32_t* layout_global) {
     if (!ctx) return TGO_E_INVALID;
+    Span load_span("load.partition");
     if (!edges || !opts || (edges->m > 0 && (!edges->src || !edges->dst))) return fail(ctx, TGO_E_INVALID, "null argument");
     if ((hi - lo) % 64 != 0) return fail(ctx, TGO_E_INVALID, "partition size must be a multiple of 64");
     (void)hipSetDevice(ctx->opts.device);

@@ -31,6 +31,7 @@
 #include <rocprim/rocprim.hpp>
 
 #include "engine.hpp"
+#include "trace.hpp"
 
 namespace tgo {
 namespace {
@@ -458,10 +459,12 @@ int assemble_edges_device(const tgo_edges* e, const tgo_load_opts* opts, int64_t
     static const bool trace = std::getenv("TGO_TRACE") && std::atoi(std::getenv("TGO_TRACE")) != 0;
     auto t_last = std::chrono::steady_clock::now();
     auto lap = [&](const char* what) {
-        if (!trace) return;
+        if (!trace && !tracing()) return;
         (void)hipStreamSynchronize(s);
         const auto now = std::chrono::steady_clock::now();
-        std::fprintf(stderr, "[tgo]   assemble %-16s %8.1f ms\n", what, std::chrono::duration<double, std::milli>(now - t_last).count());
+        const double ms = std::chrono::duration<double, std::milli>(now - t_last).count();
+        if (trace) std::fprintf(stderr, "[tgo]   assemble %-16s %8.1f ms\n", what, ms);
+        trace_complete(std::string("assemble.") + what, ms * 1e3);
         t_last = now;
     };
     ScopedBuf<int32_t> d_src, d_dst, d_w;
@@ -705,10 +708,12 @@ int assemble_partition_device(const tgo_edges* e, int64_t n_global, int64_t lo, 
     static const bool trace = std::getenv("TGO_TRACE") && std::atoi(std::getenv("TGO_TRACE")) != 0;
     auto t_last = std::chrono::steady_clock::now();
     auto lap = [&](const char* what) {
-        if (!trace) return;
+        if (!trace && !tracing()) return;
         (void)hipStreamSynchronize(s);
         const auto now = std::chrono::steady_clock::now();
-        std::fprintf(stderr, "[tgo]   partition %-14s %8.1f ms\n", what, std::chrono::duration<double, std::milli>(now - t_last).count());
+        const double ms = std::chrono::duration<double, std::milli>(now - t_last).count();
+        if (trace) std::fprintf(stderr, "[tgo]   partition %-14s %8.1f ms\n", what, ms);
+        trace_complete(std::string("partition.") + what, ms * 1e3);
         t_last = now;
     };
     ScopedBuf<int32_t> d_src, d_dst, d_w, d_lay;

@@ -28,6 +28,7 @@
 #include <rccl/rccl.h>
 
 #include "engine.hpp"
+#include "trace.hpp"
 #include "../../include/titan_gpu_olap_part.h"
 
 // Exchange: the four collectives the sweep needs, all on device buffers, ordered on `s`.
@@ -418,6 +419,7 @@ extern "C" int tgo_part_msbfs_run(tgo_ctx* ctx, tgo_exchange* x, const int64_t* 
     bool prev_dense = false;
     for (int level = 0; level < max_depth && nf > 0; ++level) {
         const bool dense = static_cast<double>(mf) * ms_alpha > static_cast<double>(total);
+        DevSpan span(st, "part.msbfs.level", {"level", level}, {"dense", dense ? 1 : 0});
         const bool first_dense = dense && !prev_dense;
         prev_dense = dense;
         if (dense) {
@@ -468,6 +470,7 @@ extern "C" int tgo_part_msbfs_run(tgo_ctx* ctx, tgo_exchange* x, const int64_t* 
         ++levels;
     }
     const int rc_off = tgo_part_device_counts(ctx, caller_dc);
+    trace_resolve(st);
     if (rc) {
         x->abort();
         rezero();
@@ -584,6 +587,7 @@ extern "C" int tgo_part_bfs_run(tgo_ctx* ctx, tgo_exchange* x, int64_t seed_glob
         if (!bottom_up && static_cast<double>(mf) > static_cast<double>(mu) / alpha) bottom_up = true;
         else if (bottom_up && static_cast<double>(nf) < static_cast<double>(ng) / beta) bottom_up = false;
         uint64_t* nb = glob[1] + x->rank * nwl;
+        DevSpan span(st, "part.bfs.level", {"level", level}, {"bottom_up", bottom_up ? 1 : 0});
         if (bottom_up) {
             if ((rc = tgo_part_bfs_bu(ctx, level, glob[0], nb, nullptr))) break;
         } else {
@@ -604,6 +608,7 @@ extern "C" int tgo_part_bfs_run(tgo_ctx* ctx, tgo_exchange* x, int64_t seed_glob
         ++levels;
     }
     const int rc_off = tgo_part_device_counts(ctx, caller_dc);
+    trace_resolve(st);
     if (rc) { x->abort(); return rc; }
     if (rc_off) return rc_off;
     int64_t rl[2] = {0, 0};
@@ -652,6 +657,7 @@ extern "C" int tgo_part_sssp_run(tgo_ctx* ctx, tgo_exchange* x, int64_t seed_glo
             qlen = c[0];
             continue;
         }
+        DevSpan span(st, "part.sssp.phase", {"phase", phases}, {"threshold", thr});
         if ((rc = tgo_part_sssp_relax(ctx, thr, W, send, sc.data()))) break;
         for (int p = 0; p < W; ++p) both[p] = 2 * sc[p];
         if (hipMemcpyAsync(sizes, both.data(), W * sizeof(int64_t), hipMemcpyHostToDevice, st) != hipSuccess) {
@@ -672,6 +678,7 @@ extern "C" int tgo_part_sssp_run(tgo_ctx* ctx, tgo_exchange* x, int64_t seed_glo
         qlen = c[0];
         ++phases;
     }
+    trace_resolve(st);
     if (rc) { x->abort(); return rc; }
     int64_t rl[2] = {0, 0};
     if ((rc = tgo_part_sssp_end(ctx, dist_local, rl))) return rc;
@@ -786,6 +793,7 @@ extern "C" int tgo_part_pagerank_run(tgo_ctx* ctx, tgo_exchange* x, const tgo_pr
     int64_t moved = 0;
     if ((rc = tgo_part_pr_begin(ctx, args, contrib))) return rc;
     for (int it = 2; it <= args->max_iterations; ++it) {
+        DevSpan upd(st, "part.pagerank.update", {"iteration", it}, {"ghost", gh ? 1 : 0});
         // the rank's own slice into the gathered vector
         hipError_t e = hot == 0
             ? hipMemcpyAsync(gath + static_cast<int64_t>(R) * nl, contrib, nl * 8, hipMemcpyDeviceToDevice, st)
@@ -812,6 +820,7 @@ extern "C" int tgo_part_pagerank_run(tgo_ctx* ctx, tgo_exchange* x, const tgo_pr
         }
         if ((rc = tgo_part_pr_step(ctx, gath, contrib))) break;
     }
+    trace_resolve(st);
     if (rc) { x->abort(); return rc; }
     if ((rc = tgo_part_pr_end(ctx, pr_local))) return rc;
     if (exchanged_bytes) *exchanged_bytes = moved;
