@@ -323,7 +323,10 @@ int  tgo_copy_multi_distances(tgo_ctx* ctx, int32_t source, int64_t* dist_out);
  * distances / ranks).  TGO_TUNE_MS_SPLIT: push budget of the sparse sources at the first pull
  * level of a multi-source sweep (tgo_bfs_multi, tgo_part_msbfs_run), a fraction of the list
  * entries; 0 = every source pulled; < 0 = the default (TGO_MS_SPLIT or 0.005). */
-enum { TGO_TUNE_MS_SPLIT = 1 };
+/* TGO_TUNE_MS_GHOST (partitioned tgo_part_msbfs_run): 1 (default) = a dense level refreshes
+ * only the frontier masks this rank's lists read (ghost exchange: all-to-allv of precomputed
+ * lists), 0 = all-gather of every rank's masks. */
+enum { TGO_TUNE_MS_SPLIT = 1, TGO_TUNE_MS_GHOST = 2 };
 int  tgo_set_tuning(tgo_ctx* ctx, int32_t key, double value);
 
 /* ---- Tracing (the reference's only hook is FulgoraGraphComputer.java:143,307

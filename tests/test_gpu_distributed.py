@@ -401,6 +401,15 @@ def test_native_msbfs_driver(world, fixed, split):
     # device counts of the Python driver's backends were restored by the native call
     res2 = ranks.run(body)
     assert all(np.array_equal(a[0], b[0]) for a, b in zip(res, res2))
+    # dense levels refresh only the ghost masks by default (TGO_TUNE_MS_GHOST); the all-gather
+    # of every rank's masks gives the same sweep
+    for be in ranks.backends:
+        be.e.set_tuning(L.TUNE_MS_GHOST, 0)
+    res3 = ranks.run(body)
+    assert all(np.array_equal(a[0], b[0]) and all(np.array_equal(p, q) for p, q in zip(a[3], b[3]))
+               for a, b in zip(res, res3))
+    for be in ranks.backends:
+        be.e.set_tuning(L.TUNE_MS_GHOST, 1)
 
 
 def test_native_msbfs_rccl_world1():

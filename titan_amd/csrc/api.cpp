@@ -68,6 +68,7 @@ struct tgo_ctx {
     ResultSource res_src;
     int num_cus = 256;          // compute units of the device (persistent launches)
     double ms_split = -1.0;     // tgo_set_tuning(TGO_TUNE_MS_SPLIT); < 0: TGO_MS_SPLIT / the default
+    int ms_ghost = 1;           // tgo_set_tuning(TGO_TUNE_MS_GHOST): dense partitioned levels exchange ghosts
     // state a native partitioned driver keeps between runs on this graph (part_driver.cpp:
     // the PageRank ghost lists); dropped with the graph
     std::shared_ptr<void> part_state;
@@ -950,6 +951,10 @@ int tgo_set_tuning(tgo_ctx* ctx, int32_t key, double value) {
     case TGO_TUNE_MS_SPLIT:
         if (!(value <= 1.0)) return fail(ctx, TGO_E_INVALID, "TGO_TUNE_MS_SPLIT: a fraction <= 1 (< 0: the default)");
         ctx->ms_split = value < 0.0 ? -1.0 : value;
+        return TGO_OK;
+    case TGO_TUNE_MS_GHOST:
+        if (value != 0.0 && value != 1.0) return fail(ctx, TGO_E_INVALID, "TGO_TUNE_MS_GHOST: 0 or 1");
+        ctx->ms_ghost = value != 0.0 ? 1 : 0;
         return TGO_OK;
     default:
         return fail(ctx, TGO_E_INVALID, "tgo_set_tuning: unknown key");
@@ -2788,6 +2793,14 @@ int part_in_list(tgo_ctx* ctx, const int32_t** adj, int64_t* nnz) {
     *nnz = ctx->g.in.nnz;
     return TGO_OK;
 }
+int part_out_list(tgo_ctx* ctx, const int32_t** adj, int64_t* nnz) {
+    if (int rc = part_check(ctx)) return rc;
+    *adj = ctx->g.out.adj;
+    *nnz = ctx->g.out.nnz;
+    return TGO_OK;
+}
+// ghost exchange of the dense multi-source levels (tgo_set_tuning TGO_TUNE_MS_GHOST; default on)
+bool ms_ghost_of(const tgo_ctx* ctx) { return ctx->ms_ghost != 0; }
 // the blocked gathered layout of the last tgo_part_pr_blocked (world 0: plain layout)
 int part_pr_layout_of(tgo_ctx* ctx, int32_t* world, int64_t* hot, int64_t* span) {
     if (int rc = part_check(ctx)) return rc;

@@ -346,8 +346,10 @@ int build_cold_blocks_device(const int64_t* d_off, const int32_t* d_adj, int64_t
 int pack_tiles_device(int32_t* d_adj, int64_t m, const std::vector<int64_t>& tstart, const std::vector<int32_t>* tbase,
                       int shift, hipStream_t s, std::string& err);
 // part_ghost.hip: the partitioned PageRank ghost exchange
-int pr_ghost_needs(const int32_t* d_adj, int64_t nnz, int64_t nl, int rank, int world, int32_t** need,
-                   std::vector<int64_t>& need_count, hipStream_t s, std::string& err);
+int ghost_needs(const int32_t* d_adj, int64_t nnz, const int32_t* d_adj2, int64_t nnz2, int64_t nl, int rank, int world,
+                int32_t** need, std::vector<int64_t>& need_count, hipStream_t s, std::string& err);
+hipError_t k_pack_u64(const uint64_t* src, const int32_t* row, int64_t m, uint64_t* out, hipStream_t s);
+hipError_t k_unpack_u64(const uint64_t* in, const int32_t* pos, int64_t m, uint64_t* g, hipStream_t s);
 hipError_t k_gathered_pos(const int32_t* u, int64_t m, int64_t nl, int64_t A, int64_t H, int64_t W, int32_t* pos,
                           hipStream_t s);
 hipError_t k_sub_i32(int32_t* v, int64_t m, int32_t by, hipStream_t s);

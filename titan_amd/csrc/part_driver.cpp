@@ -305,6 +305,8 @@ int64_t* part_dcounts_of(tgo_ctx* ctx);
 double ms_split_of(const tgo_ctx* ctx);
 std::shared_ptr<void>& part_state_of(tgo_ctx* ctx);
 int part_in_list(tgo_ctx* ctx, const int32_t** adj, int64_t* nnz);
+int part_out_list(tgo_ctx* ctx, const int32_t** adj, int64_t* nnz);
+bool ms_ghost_of(const tgo_ctx* ctx);
 int part_pr_layout_of(tgo_ctx* ctx, int32_t* world, int64_t* hot, int64_t* span);
 template <class T>
 int scratch(tgo_ctx* ctx, T*& p, int64_t count, int slot) {
@@ -317,6 +319,135 @@ int scratch(tgo_ctx* ctx, T*& p, int64_t count, int slot) {
 }  // namespace tgo
 
 using namespace tgo;
+
+namespace {
+
+// Host-side helpers shared by the loops: small global reductions through a device buffer.
+struct Driver {
+    tgo_ctx* ctx;
+    tgo_exchange* x;
+    hipStream_t st;
+    int64_t* dbuf = nullptr;        // device scalars (8)
+    int64_t* hc = nullptr;          // pinned host view
+    int xfail(int code) { return part_fail(ctx, code, "exchange: " + x->err); }
+    int hip(const char* what) { return part_fail(ctx, TGO_E_HIP, what); }
+    // out[i] = op over the ranks of vals[i], i < k <= 8 (one round trip)
+    int reduce(const int64_t* vals, int k, int op, int64_t* out) {
+        for (int i = 0; i < k; ++i) hc[i] = vals[i];
+        if (hipMemcpyAsync(dbuf, hc, k * sizeof(int64_t), hipMemcpyHostToDevice, st) != hipSuccess) return hip("reduce upload");
+        if (int r = x->all_reduce(dbuf, static_cast<size_t>(k), op, st)) return xfail(r);
+        if (hipMemcpyAsync(hc, dbuf, k * sizeof(int64_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            return hip("reduce read");
+        for (int i = 0; i < k; ++i) out[i] = hc[i];
+        return TGO_OK;
+    }
+};
+
+int driver_open(tgo_ctx* ctx, tgo_exchange* x, const char* name, int slot, Driver& d, int64_t& nl, int64_t& lo,
+                int64_t& ng, int64_t& ent) {
+    int rc = part_dims(ctx, &nl, &lo, &ng, &ent);
+    if (rc) return rc;
+    if (static_cast<int64_t>(x->world) * nl != ng || lo != static_cast<int64_t>(x->rank) * nl)
+        return part_fail(ctx, TGO_E_INVALID, std::string(name) + ": the exchange's world / rank do not match the partition");
+    d.ctx = ctx;
+    d.x = x;
+    d.st = part_stream(ctx);
+    if ((rc = scratch(ctx, d.dbuf, 8, slot))) return rc;
+    d.hc = x->host_counts();
+    if (!d.hc) return part_fail(ctx, TGO_E_HIP, std::string(name) + ": pinned counts");
+    return TGO_OK;
+}
+
+}  // namespace
+
+namespace {
+
+// Ghost lists (part_ghost.hip), kept with the graph: which of this rank's rows every peer
+// reads (send_row) and where each value received from a peer goes (recv_pos).  PageRank reads
+// over its in-lists into the blocked gathered vector; the multi-source sweep over both lists
+// into the global mask vector (position = global id).
+struct PrGhost {
+    int world = 0, rank = -1;
+    int64_t nl = 0, hot = 0, span = 0;
+    int32_t* send_row = nullptr;    // local rows this rank sends, peer-major
+    int32_t* recv_pos = nullptr;    // gathered-vector position of every received value
+    double* sbuf = nullptr;
+    double* rbuf = nullptr;
+    int64_t nsend = 0, nrecv = 0;
+    std::vector<size_t> sb, so, rb, ro;   // byte counts / offsets per peer (doubles)
+    ~PrGhost() {
+        for (void* p : {static_cast<void*>(send_row), static_cast<void*>(recv_pos), static_cast<void*>(sbuf),
+                        static_cast<void*>(rbuf)})
+            if (p) (void)hipFree(p);
+    }
+};
+
+int build_ghost(tgo_ctx* ctx, tgo_exchange* x, Driver& d, int64_t nl, int64_t hot, int64_t span, bool both_lists,
+                PrGhost& gh) {
+    const int W = x->world, R = x->rank;
+    hipStream_t st = d.st;
+    const int32_t *adj = nullptr, *adj2 = nullptr;
+    int64_t nnz = 0, nnz2 = 0;
+    int rc = part_in_list(ctx, &adj, &nnz);
+    if (!rc && both_lists) rc = part_out_list(ctx, &adj2, &nnz2);
+    if (rc) return rc;
+    std::string err;
+    int32_t* need = nullptr;
+    std::vector<int64_t> need_count;
+    if ((rc = ghost_needs(adj, nnz, adj2, nnz2, nl, R, W, &need, need_count, st, err))) return part_fail(ctx, rc, err);
+    struct Free { void* p; ~Free() { if (p) (void)hipFree(p); } } free_need{need};
+    int64_t nneed = 0;
+    for (int64_t c : need_count) nneed += c;
+    // counts to the owners, then the ids (as int32 bytes)
+    int64_t* sizes = nullptr;
+    if ((rc = scratch(ctx, sizes, 2 * W, both_lists ? 7 : 21))) return rc;
+    if (hipMemcpyAsync(sizes, need_count.data(), W * sizeof(int64_t), hipMemcpyHostToDevice, st) != hipSuccess)
+        return d.hip("ghost counts upload");
+    if (int r = x->all_to_all(sizes, sizes + W, 8, st)) return d.xfail(r);
+    std::vector<int64_t> gives(W);
+    if (hipMemcpyAsync(gives.data(), sizes + W, W * sizeof(int64_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return d.hip("ghost counts read");
+    int64_t ngive = 0;
+    for (int64_t c : gives) ngive += c;
+    gh.world = W; gh.rank = R; gh.nl = nl; gh.hot = hot; gh.span = span;
+    gh.nsend = ngive;
+    gh.nrecv = nneed;
+    if (hipMalloc(&gh.send_row, std::max<int64_t>(ngive, 1) * 4) != hipSuccess ||
+        hipMalloc(&gh.recv_pos, std::max<int64_t>(nneed, 1) * 4) != hipSuccess ||
+        hipMalloc(&gh.sbuf, std::max<int64_t>(ngive, 1) * 8) != hipSuccess ||
+        hipMalloc(&gh.rbuf, std::max<int64_t>(nneed, 1) * 8) != hipSuccess)
+        return part_fail(ctx, TGO_E_OOM, "ghost buffers");
+    std::vector<size_t> ib(W), io(W), gb(W), go(W);
+    gh.sb.assign(W, 0); gh.so.assign(W, 0); gh.rb.assign(W, 0); gh.ro.assign(W, 0);
+    size_t a = 0, b = 0;
+    for (int p = 0; p < W; ++p) {
+        ib[p] = static_cast<size_t>(need_count[p]) * 4; io[p] = a; a += ib[p];       // my needs, to owner p
+        gb[p] = static_cast<size_t>(gives[p]) * 4; go[p] = b; b += gb[p];            // p's needs of my rows
+        gh.rb[p] = static_cast<size_t>(need_count[p]) * 8; gh.ro[p] = io[p] * 2;      // values received from p
+        gh.sb[p] = static_cast<size_t>(gives[p]) * 8; gh.so[p] = go[p] * 2;           // values sent to p
+    }
+    if (int r = x->all_to_allv(need, ib.data(), io.data(), gh.send_row, gb.data(), go.data(), st)) return d.xfail(r);
+    if (hipError_t e = k_sub_i32(gh.send_row, ngive, static_cast<int32_t>(static_cast<int64_t>(R) * nl), st))
+        return part_fail(ctx, TGO_E_HIP, hipGetErrorString(e));
+    if (hipError_t e = k_gathered_pos(need, nneed, nl, span, hot, W, gh.recv_pos, st))
+        return part_fail(ctx, TGO_E_HIP, hipGetErrorString(e));
+    if (hipStreamSynchronize(st) != hipSuccess) return d.hip("ghost lists");
+    return TGO_OK;
+}
+
+// the ghost lists a driver keeps with the graph (part_state_of): PageRank's and the sweep's
+struct GhostCache {
+    std::shared_ptr<PrGhost> pr, ms;
+};
+GhostCache& ghost_cache(tgo_ctx* ctx) {
+    std::shared_ptr<void>& st = part_state_of(ctx);
+    if (!st) st = std::make_shared<GhostCache>();
+    return *static_cast<GhostCache*>(st.get());
+}
+
+}  // namespace
 
 extern "C" int tgo_part_msbfs_run(tgo_ctx* ctx, tgo_exchange* x, const int64_t* seeds, int32_t nseeds, int32_t max_depth,
                                   double ms_alpha, int64_t fixed_bytes, int64_t* reached, int64_t* entries,
@@ -354,6 +485,20 @@ extern "C" int tgo_part_msbfs_run(tgo_ctx* ctx, tgo_exchange* x, const int64_t* 
     };
     int64_t* hc = x->host_counts();                         // pinned host view of the counts (kept)
     if (!hc) return part_fail(ctx, TGO_E_HIP, "tgo_part_msbfs_run: pinned counts");
+    // dense levels: the ghost exchange (only the masks this rank's lists read, lists built once
+    // per graph) unless TGO_TUNE_MS_GHOST = 0 or a single rank
+    PrGhost* gh = nullptr;
+    if (W > 1 && ms_ghost_of(ctx)) {
+        Driver d{ctx, x, st, dc, hc};
+        std::shared_ptr<PrGhost>& cached = ghost_cache(ctx).ms;
+        gh = cached.get();
+        if (!gh || gh->world != W || gh->rank != x->rank || gh->nl != nl) {
+            auto fresh = std::make_shared<PrGhost>();
+            if ((rc = build_ghost(ctx, x, d, nl, 0, nl, true, *fresh))) { x->abort(); return rc; }
+            cached = fresh;
+            gh = fresh.get();
+        }
+    }
     // global counts: write local {a, b} to dc, all-reduce, read back (one sync)
     auto global2 = [&](int64_t a, int64_t b, int64_t* out) -> int {
         hc[0] = a; hc[1] = b;
@@ -449,7 +594,25 @@ extern "C" int tgo_part_msbfs_run(tgo_ctx* ctx, tgo_exchange* x, const int64_t* 
                     with_cand = 1;
                 }
             }
-            if (int r = x->all_gather(glob[0], static_cast<size_t>(nl) * 8, st)) { rc = xfail(r); break; }
+            if (gh) {                                   // ghosts: pack -> all-to-allv -> unpack into glob[0]
+                const uint64_t* own = glob[0] + lo;
+                if (k_pack_u64(own, gh->send_row, gh->nsend, reinterpret_cast<uint64_t*>(gh->sbuf), st) != hipSuccess) {
+                    rc = part_fail(ctx, TGO_E_HIP, "ghost pack");
+                    break;
+                }
+                if (int r = x->all_to_allv(gh->sbuf, gh->sb.data(), gh->so.data(), gh->rbuf, gh->rb.data(), gh->ro.data(), st)) {
+                    rc = xfail(r);
+                    break;
+                }
+                if (k_unpack_u64(reinterpret_cast<const uint64_t*>(gh->rbuf), gh->recv_pos, gh->nrecv, glob[0], st) !=
+                    hipSuccess) {
+                    rc = part_fail(ctx, TGO_E_HIP, "ghost unpack");
+                    break;
+                }
+            } else if (int r = x->all_gather(glob[0], static_cast<size_t>(nl) * 8, st)) {
+                rc = xfail(r);
+                break;
+            }
             if ((rc = tgo_part_ms_pull_split(ctx, level, glob[0], frn, sparse, with_cand, nullptr))) break;
         } else {
             if ((rc = tgo_part_ms_push(ctx, level, fr, cand))) break;
@@ -508,46 +671,6 @@ extern "C" int tgo_part_msbfs_run(tgo_ctx* ctx, tgo_exchange* x, const int64_t* 
 // Python round trips of FulgoraGraphComputer's superstep loop (FulgoraGraphComputer.java:
 // 151-189) in its multi-GPU form.
 
-namespace {
-
-// Host-side helpers shared by the loops: small global reductions through a device buffer.
-struct Driver {
-    tgo_ctx* ctx;
-    tgo_exchange* x;
-    hipStream_t st;
-    int64_t* dbuf = nullptr;        // device scalars (8)
-    int64_t* hc = nullptr;          // pinned host view
-    int xfail(int code) { return part_fail(ctx, code, "exchange: " + x->err); }
-    int hip(const char* what) { return part_fail(ctx, TGO_E_HIP, what); }
-    // out[i] = op over the ranks of vals[i], i < k <= 8 (one round trip)
-    int reduce(const int64_t* vals, int k, int op, int64_t* out) {
-        for (int i = 0; i < k; ++i) hc[i] = vals[i];
-        if (hipMemcpyAsync(dbuf, hc, k * sizeof(int64_t), hipMemcpyHostToDevice, st) != hipSuccess) return hip("reduce upload");
-        if (int r = x->all_reduce(dbuf, static_cast<size_t>(k), op, st)) return xfail(r);
-        if (hipMemcpyAsync(hc, dbuf, k * sizeof(int64_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
-            hipStreamSynchronize(st) != hipSuccess)
-            return hip("reduce read");
-        for (int i = 0; i < k; ++i) out[i] = hc[i];
-        return TGO_OK;
-    }
-};
-
-int driver_open(tgo_ctx* ctx, tgo_exchange* x, const char* name, int slot, Driver& d, int64_t& nl, int64_t& lo,
-                int64_t& ng, int64_t& ent) {
-    int rc = part_dims(ctx, &nl, &lo, &ng, &ent);
-    if (rc) return rc;
-    if (static_cast<int64_t>(x->world) * nl != ng || lo != static_cast<int64_t>(x->rank) * nl)
-        return part_fail(ctx, TGO_E_INVALID, std::string(name) + ": the exchange's world / rank do not match the partition");
-    d.ctx = ctx;
-    d.x = x;
-    d.st = part_stream(ctx);
-    if ((rc = scratch(ctx, d.dbuf, 8, slot))) return rc;
-    d.hc = x->host_counts();
-    if (!d.hc) return part_fail(ctx, TGO_E_HIP, std::string(name) + ": pinned counts");
-    return TGO_OK;
-}
-
-}  // namespace
 
 extern "C" int tgo_part_bfs_run(tgo_ctx* ctx, tgo_exchange* x, int64_t seed_global, int32_t max_depth, double alpha,
                                 double beta, int64_t* dist_local, int64_t* reached, int32_t* levels_out) {
@@ -687,78 +810,6 @@ extern "C" int tgo_part_sssp_run(tgo_ctx* ctx, tgo_exchange* x, int64_t seed_glo
     return TGO_OK;
 }
 
-namespace {
-
-// The ghost lists of a partitioned PageRank layout (part_ghost.hip), kept with the graph.
-struct PrGhost {
-    int world = 0, rank = -1;
-    int64_t nl = 0, hot = 0, span = 0;
-    int32_t* send_row = nullptr;    // local rows this rank sends, peer-major
-    int32_t* recv_pos = nullptr;    // gathered-vector position of every received value
-    double* sbuf = nullptr;
-    double* rbuf = nullptr;
-    int64_t nsend = 0, nrecv = 0;
-    std::vector<size_t> sb, so, rb, ro;   // byte counts / offsets per peer (doubles)
-    ~PrGhost() {
-        for (void* p : {static_cast<void*>(send_row), static_cast<void*>(recv_pos), static_cast<void*>(sbuf),
-                        static_cast<void*>(rbuf)})
-            if (p) (void)hipFree(p);
-    }
-};
-
-int build_pr_ghost(tgo_ctx* ctx, tgo_exchange* x, Driver& d, int64_t nl, int64_t hot, int64_t span, PrGhost& gh) {
-    const int W = x->world, R = x->rank;
-    hipStream_t st = d.st;
-    const int32_t* adj = nullptr;
-    int64_t nnz = 0;
-    int rc = part_in_list(ctx, &adj, &nnz);
-    if (rc) return rc;
-    std::string err;
-    int32_t* need = nullptr;
-    std::vector<int64_t> need_count;
-    if ((rc = pr_ghost_needs(adj, nnz, nl, R, W, &need, need_count, st, err))) return part_fail(ctx, rc, err);
-    struct Free { void* p; ~Free() { if (p) (void)hipFree(p); } } free_need{need};
-    int64_t nneed = 0;
-    for (int64_t c : need_count) nneed += c;
-    // counts to the owners, then the ids (as int32 bytes)
-    int64_t* sizes = nullptr;
-    if ((rc = scratch(ctx, sizes, 2 * W, 21))) return rc;
-    if (hipMemcpyAsync(sizes, need_count.data(), W * sizeof(int64_t), hipMemcpyHostToDevice, st) != hipSuccess)
-        return d.hip("ghost counts upload");
-    if (int r = x->all_to_all(sizes, sizes + W, 8, st)) return d.xfail(r);
-    std::vector<int64_t> gives(W);
-    if (hipMemcpyAsync(gives.data(), sizes + W, W * sizeof(int64_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess)
-        return d.hip("ghost counts read");
-    int64_t ngive = 0;
-    for (int64_t c : gives) ngive += c;
-    gh.world = W; gh.rank = R; gh.nl = nl; gh.hot = hot; gh.span = span;
-    gh.nsend = ngive;
-    gh.nrecv = nneed;
-    if (hipMalloc(&gh.send_row, std::max<int64_t>(ngive, 1) * 4) != hipSuccess ||
-        hipMalloc(&gh.recv_pos, std::max<int64_t>(nneed, 1) * 4) != hipSuccess ||
-        hipMalloc(&gh.sbuf, std::max<int64_t>(ngive, 1) * 8) != hipSuccess ||
-        hipMalloc(&gh.rbuf, std::max<int64_t>(nneed, 1) * 8) != hipSuccess)
-        return part_fail(ctx, TGO_E_OOM, "ghost buffers");
-    std::vector<size_t> ib(W), io(W), gb(W), go(W);
-    gh.sb.assign(W, 0); gh.so.assign(W, 0); gh.rb.assign(W, 0); gh.ro.assign(W, 0);
-    size_t a = 0, b = 0;
-    for (int p = 0; p < W; ++p) {
-        ib[p] = static_cast<size_t>(need_count[p]) * 4; io[p] = a; a += ib[p];       // my needs, to owner p
-        gb[p] = static_cast<size_t>(gives[p]) * 4; go[p] = b; b += gb[p];            // p's needs of my rows
-        gh.rb[p] = static_cast<size_t>(need_count[p]) * 8; gh.ro[p] = io[p] * 2;      // values received from p
-        gh.sb[p] = static_cast<size_t>(gives[p]) * 8; gh.so[p] = go[p] * 2;           // values sent to p
-    }
-    if (int r = x->all_to_allv(need, ib.data(), io.data(), gh.send_row, gb.data(), go.data(), st)) return d.xfail(r);
-    if (hipError_t e = k_sub_i32(gh.send_row, ngive, static_cast<int32_t>(static_cast<int64_t>(R) * nl), st))
-        return part_fail(ctx, TGO_E_HIP, hipGetErrorString(e));
-    if (hipError_t e = k_gathered_pos(need, nneed, nl, span, hot, W, gh.recv_pos, st))
-        return part_fail(ctx, TGO_E_HIP, hipGetErrorString(e));
-    if (hipStreamSynchronize(st) != hipSuccess) return d.hip("ghost lists");
-    return TGO_OK;
-}
-
-}  // namespace
 
 extern "C" int tgo_part_pagerank_run(tgo_ctx* ctx, tgo_exchange* x, const tgo_pr_args* args, int32_t exchange_mode,
                                      double* pr_local, int64_t* exchanged_bytes) {
@@ -781,12 +832,12 @@ extern "C" int tgo_part_pagerank_run(tgo_ctx* ctx, tgo_exchange* x, const tgo_pr
     if ((rc = scratch(ctx, contrib, nl, 18)) || (rc = scratch(ctx, gath, static_cast<int64_t>(W) * span, 19))) return rc;
     PrGhost* gh = nullptr;
     if (exchange_mode == 1 && W > 1) {
-        std::shared_ptr<void>& state = part_state_of(ctx);
-        gh = static_cast<PrGhost*>(state.get());
+        std::shared_ptr<PrGhost>& cached = ghost_cache(ctx).pr;
+        gh = cached.get();
         if (!gh || gh->world != W || gh->rank != R || gh->hot != hot || gh->span != span || gh->nl != nl) {
             auto fresh = std::make_shared<PrGhost>();
-            if ((rc = build_pr_ghost(ctx, x, d, nl, hot, span, *fresh))) { x->abort(); return rc; }
-            state = fresh;
+            if ((rc = build_ghost(ctx, x, d, nl, hot, span, false, *fresh))) { x->abort(); return rc; }
+            cached = fresh;
             gh = fresh.get();
         }
     }

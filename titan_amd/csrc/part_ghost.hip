@@ -77,10 +77,10 @@ __global__ void unpack_f64(const double* __restrict__ in, const int32_t* __restr
 
 }  // namespace
 
-// Sorted unique remote sources of the in-list (global internal ids), grouped by owner:
+// Sorted unique remote neighbours of one or two lists (global internal ids), grouped by owner:
 // need (device, owned by the caller via hipFree), need_count[q] per owner q (host).
-int pr_ghost_needs(const int32_t* d_adj, int64_t nnz, int64_t nl, int rank, int world, int32_t** need,
-                   std::vector<int64_t>& need_count, hipStream_t s, std::string& err) {
+int ghost_needs(const int32_t* d_adj, int64_t nnz, const int32_t* d_adj2, int64_t nnz2, int64_t nl, int rank, int world,
+                int32_t** need, std::vector<int64_t>& need_count, hipStream_t s, std::string& err) {
     *need = nullptr;
     need_count.assign(world, 0);
     const int64_t lo = static_cast<int64_t>(rank) * nl, hi = lo + nl;
@@ -109,31 +109,44 @@ int pr_ghost_needs(const int32_t* d_adj, int64_t nnz, int64_t nl, int rank, int 
         return hipMalloc(&tmp, b);
     };
     hipError_t e;
-    const size_t m1 = static_cast<size_t>(std::max<int64_t>(nnz, 1));
+    const size_t m1 = static_cast<size_t>(std::max<int64_t>(std::max(nnz, nnz2), 1));
     if ((e = hipMalloc(&f, m1 * 4)) || (e = hipMalloc(&pos, (m1 + 1) * 8)) || (e = hipMalloc(&nuniq, 8)) ||
         (e = hipMalloc(&bounds, (world + 1) * 8)))
         return fail(e);
-    int64_t c = 0;
-    if (nnz > 0) {
-        remote_flags<<<grid(nnz), kB, 0, s>>>(d_adj, nnz, lo, hi, f);
+    // remote entries of each list, counted then compacted into rem (list 1, then list 2)
+    auto count_remote = [&](const int32_t* adj, int64_t m, int64_t& c) -> hipError_t {
+        c = 0;
+        if (m <= 0) return hipSuccess;
+        remote_flags<<<grid(m), kB, 0, s>>>(adj, m, lo, hi, f);
         size_t b = 0;
-        if ((e = rocprim::exclusive_scan(nullptr, b, f, pos, uint64_t(0), static_cast<size_t>(nnz) + 0,
-                                         rocprim::plus<uint64_t>(), s)) ||
-            (e = need_tmp(b)) ||
-            (e = rocprim::exclusive_scan(tmp, b, f, pos, uint64_t(0), static_cast<size_t>(nnz), rocprim::plus<uint64_t>(), s)))
-            return fail(e);
+        hipError_t x;
+        if ((x = rocprim::exclusive_scan(nullptr, b, f, pos, uint64_t(0), static_cast<size_t>(m), rocprim::plus<uint64_t>(), s)) ||
+            (x = need_tmp(b)) ||
+            (x = rocprim::exclusive_scan(tmp, b, f, pos, uint64_t(0), static_cast<size_t>(m), rocprim::plus<uint64_t>(), s)))
+            return x;
         uint64_t last = 0;
         uint32_t lastf = 0;
-        if ((e = hipMemcpyAsync(&last, pos + nnz - 1, 8, hipMemcpyDeviceToHost, s)) ||
-            (e = hipMemcpyAsync(&lastf, f + nnz - 1, 4, hipMemcpyDeviceToHost, s)) || (e = hipStreamSynchronize(s)))
-            return fail(e);
+        if ((x = hipMemcpyAsync(&last, pos + m - 1, 8, hipMemcpyDeviceToHost, s)) ||
+            (x = hipMemcpyAsync(&lastf, f + m - 1, 4, hipMemcpyDeviceToHost, s)) || (x = hipStreamSynchronize(s)))
+            return x;
         c = static_cast<int64_t>(last + lastf);
-    }
+        return hipSuccess;
+    };
+    int64_t c1n = 0, c2n = 0;
+    if ((e = count_remote(d_adj, nnz, c1n))) return fail(e);
+    if ((e = count_remote(d_adj2, nnz2, c2n))) return fail(e);
+    const int64_t c = c1n + c2n;
     const size_t c1 = static_cast<size_t>(std::max<int64_t>(c, 1));
     if ((e = hipMalloc(&rem, c1 * 4)) || (e = hipMalloc(&srt, c1 * 4)) || (e = hipMalloc(&uq, c1 * 4))) return fail(e);
     int64_t u = 0;
     if (c > 0) {
-        compact_i32<<<grid(nnz), kB, 0, s>>>(d_adj, f, pos, nnz, rem);
+        // the flags / positions of list 2 are still in f / pos: compact it first, behind list 1's
+        if (c2n > 0) compact_i32<<<grid(nnz2), kB, 0, s>>>(d_adj2, f, pos, nnz2, rem + c1n);
+        if (c1n > 0) {
+            int64_t again = 0;
+            if ((e = count_remote(d_adj, nnz, again))) return fail(e);
+            compact_i32<<<grid(nnz), kB, 0, s>>>(d_adj, f, pos, nnz, rem);
+        }
         int bits = 1;
         while ((int64_t(1) << bits) < static_cast<int64_t>(world) * nl) ++bits;
         size_t b = 0;
@@ -169,6 +182,14 @@ hipError_t k_sub_i32(int32_t* v, int64_t m, int32_t by, hipStream_t s) {
 hipError_t k_pack_f64(const double* src, const int32_t* row, int64_t m, double* out, hipStream_t s) {
     if (m > 0) pack_f64<<<grid(m), kB, 0, s>>>(src, row, m, out);
     return hipGetLastError();
+}
+// 8-byte words moved as integers (multi-source frontier masks; doubles use the same kernels
+// through their bits)
+hipError_t k_pack_u64(const uint64_t* src, const int32_t* row, int64_t m, uint64_t* out, hipStream_t s) {
+    return k_pack_f64(reinterpret_cast<const double*>(src), row, m, reinterpret_cast<double*>(out), s);
+}
+hipError_t k_unpack_u64(const uint64_t* in, const int32_t* pos, int64_t m, uint64_t* g, hipStream_t s) {
+    return k_unpack_f64(reinterpret_cast<const double*>(in), pos, m, reinterpret_cast<double*>(g), s);
 }
 hipError_t k_unpack_f64(const double* in, const int32_t* pos, int64_t m, double* g, hipStream_t s) {
     if (m > 0) unpack_f64<<<grid(m), kB, 0, s>>>(in, pos, m, g);
