@@ -11,4 +11,7 @@ timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method threa
 rc=$?; tail -5 gpurun_out/r04f/gpu_tests2.log; [ $rc -eq 0 ] || exit $rc
 bash scripts/gpu_pr_ab.sh r04f_win "TGO_PR_WIN=0" "TGO_PR_WIN=15872" "TGO_PR_WIN=8192" "TGO_PR_WIN=4096" "TGO_PR_WIN=15872 TGO_PR_SKIP_BELOW=393216" \
     > gpurun_out/r04f/ab.log 2>&1
-rc=$?; cat gpurun_out/r04f/ab.log; exit $rc
+rc=$?; cat gpurun_out/r04f/ab.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
+    tests/test_gpu_distributed.py -k "native" > gpurun_out/r04f/gpu_tests3.log 2>&1
+rc=$?; tail -5 gpurun_out/r04f/gpu_tests3.log; exit $rc

@@ -572,6 +572,7 @@ int assemble_edges_device(const tgo_edges* e, const tgo_load_opts* opts, int64_t
         order_to_perm<<<grid(n), kB, 0, s>>>(bs.p, n, perm.p);
     }
     deg.release();
+    lap("relabel");
     // ---- sort 2: final lists in (perm[row], perm[neighbour]) order
     HostCsr* outc[2] = {&g.out, &g.in};
     ScopedBuf<uint64_t> fkey[2];                    // final keys (kept for the transpose)
@@ -587,7 +588,9 @@ int assemble_edges_device(const tgo_edges* e, const tgo_load_opts* opts, int64_t
             // re-key the kept sort-1 entries through perm, payload = their kept index
             AS_TRY(vt.alloc(payload ? c : 0));
             if (c) rekey<<<grid(c), kB, 0, s>>>(dir[d].key.p, c, b, perm.p, kt.p, payload ? vt.p : nullptr);
+            lap(d == 0 ? "OUT rekey" : "IN rekey");
             dir[d].key.release();
+            lap(d == 0 ? "OUT free sort-1 keys" : "IN free sort-1 keys");
         } else {
             AS_TRY(vt.alloc(payload ? c : 0));
             if (c) edge_keys<<<grid(c), kB, 0, s>>>(d == 0 ? d_src.p : d_dst.p, d == 0 ? d_dst.p : d_src.p, c, b, perm.p,
@@ -599,6 +602,7 @@ int assemble_edges_device(const tgo_edges* e, const tgo_load_opts* opts, int64_t
         } else if (c) {
             AS_TRY(so.keys(kt.p, fkey[d].p, c, bits));
         }
+        lap(d == 0 ? "OUT sort 2" : "IN sort 2");
         kt.release();
         HostCsr& hc = *outc[d];
         ScopedBuf<int64_t> off;
@@ -612,16 +616,18 @@ int assemble_edges_device(const tgo_edges* e, const tgo_load_opts* opts, int64_t
             emit_list<<<grid(c), kB, 0, s>>>(fkey[d].p, payload ? vs.p : nullptr, c, b,
                                              sort1 ? dir[d].edge.p : nullptr, d_w.p, sort1 ? dir[d].col.p : nullptr,
                                              fadj[d].p, g.has_weight ? fw[d].p : nullptr, keep_col ? col.p : nullptr);
+        lap(d == 0 ? "OUT offsets + emit" : "IN offsets + emit");
         AS_TRY(download(hc.off, off.p, n + 1, s));
         if (g.has_weight) {                          // weight_sorted_push reads the host lists
             AS_TRY(download(hc.adj, fadj[d].p, c, s));
             AS_TRY(download(hc.w, fw[d].p, c, s));
         }
         AS_TRY(hipStreamSynchronize(s));
+        lap(d == 0 ? "OUT download" : "IN download");
         if (keep_col) hc.dcol.own(col.take(), c);
         dir[d].edge.release();
         dir[d].col.release();
-        lap(d == 0 ? "relabel + OUT" : "IN");
+        lap(d == 0 ? "OUT frees" : "IN frees");
     }
     AS_TRY(download(g.perm, perm.p, n, s));
     // ---- push view: equal to the stored opposite list unless the cut made rows asymmetric
