@@ -13,6 +13,9 @@
 //                 (source << 12 | slot) — one radix sort over (tile << 32 | packed) keys.
 // The reference's update this layout feeds: PageRankVertexProgram.java:84-89.
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstdint>
 #include <cstring>
 #include <string>
@@ -22,6 +25,7 @@
 #include <rocprim/rocprim.hpp>
 
 #include "engine.hpp"
+#include "trace.hpp"
 
 namespace tgo {
 namespace {
@@ -241,6 +245,17 @@ int build_cold_blocks_device(const int64_t* d_off, const int32_t* d_adj, int64_t
     if (win < 0 || win > 65536 || win > hot) win = 0;       // uint16 window entries inside the hot range
     const int64_t nseg = (n_src - hot + seg - 1) / seg;
     Sort so{{}, 0, s};
+    static const bool trace = std::getenv("TGO_TRACE") && std::atoi(std::getenv("TGO_TRACE")) != 0;
+    auto t_last = std::chrono::steady_clock::now();
+    auto lap = [&](const char* what) {
+        if (!trace && !tracing()) return;
+        (void)hipStreamSynchronize(s);
+        const auto now = std::chrono::steady_clock::now();
+        const double ms = std::chrono::duration<double, std::milli>(now - t_last).count();
+        if (trace) std::fprintf(stderr, "[tgo]     cold build %-18s %8.1f ms\n", what, ms);
+        trace_complete(std::string("pagerank_layout.build.") + what, ms * 1e3);
+        t_last = now;
+    };
     {
         Buf<int> bad;
         PL_TRY(bad.alloc(1));
@@ -300,7 +315,9 @@ int build_cold_blocks_device(const int64_t* d_off, const int32_t* d_adj, int64_t
         PL_TRY(hipStreamSynchronize(s));
         hc.d_widx.own(widx.take(), nwin);
     }
+    lap("split");
     if (C) PL_TRY(so.pairs(ckey.p, skey.p, cval.p, cadj.p, C, 32 + bits_for(nseg)));
+    lap("cold sort");
     ckey.release();
     cval.release();
     // pieces
@@ -335,6 +352,7 @@ int build_cold_blocks_device(const int64_t* d_off, const int32_t* d_adj, int64_t
     start.release();
     pid.release();
     skey.release();
+    lap("pieces");
     // to the host: the piece structure, the hot CSR and the cold entries
     std::vector<uint32_t> h_pseg;
     PL_TRY(fetch(hc.poff, poff.p, np + 1, s));
@@ -349,6 +367,7 @@ int build_cold_blocks_device(const int64_t* d_off, const int32_t* d_adj, int64_t
     hc.crow.clear();
     for (int64_t r = 0; r < n; ++r)
         if (hc.cptr[r + 1] > hc.cptr[r]) hc.crow.push_back(static_cast<int32_t>(r));
+    lap("fetch");
     // blocks: greedy per segment (<= tile entries, <= max_pieces pieces), segment-major
     std::vector<int64_t> seg_pbase(nseg + 1, np);
     for (int64_t p = np - 1; p >= 0; --p) seg_pbase[h_pseg[p]] = p;
@@ -365,6 +384,7 @@ int build_cold_blocks_device(const int64_t* d_off, const int32_t* d_adj, int64_t
         }
     }
     const int64_t nb = static_cast<int64_t>(hc.bbeg.size());
+    lap("blocks (host)");
     if (pack && seg <= (int64_t(1) << (31 - kPackShift)) && tile <= (int64_t(1) << kPackShift)) {
         std::vector<int64_t> tstart(nb);
         for (int64_t b = 0; b < nb; ++b) tstart[b] = hc.poff[hc.bbeg[b]];
