@@ -159,9 +159,9 @@ int64_t env_i64(const char* name, int64_t dflt) {
     return v ? std::atoll(v) : dflt;
 }
 constexpr int64_t kPrHotDefault = 393216, kPrSegDefault = 393216;   // 3 MB each (profiles/r02an_pr_hot_seg_probe*.log)
-// LDS window of the hottest sources (lds_window, spmv.hip): 15872 doubles = 124 KB of a CUs
-// 160 KB LDS beside the 32 KB tile; 0 = off
-constexpr int64_t kPrWinDefault = 15872;
+// LDS window of the hottest sources (lds_window, spmv.hip): 12032 doubles = 94 KB of a CU's
+// 160 KB LDS beside the 16 waves' 4 KB item buffers; 0 = off
+constexpr int64_t kPrWinDefault = 12032, kPrWinMax = 12288;
 
 // PageRank diagnostics (engine.hpp PrTuning): TGO_PR_DIAG=lo:hi gathers only sources in
 // [lo, hi) — a timing attribution tool, its ranks are wrong (scripts/pr_probe.py).
@@ -259,6 +259,7 @@ int upload_cold_blocks(tgo_ctx* ctx, const std::vector<int64_t>& off, const std:
         t_last = now;
     };
     bool on_dev = false;
+    win = std::min<int64_t>(win, kPrWinMax);        // the window and the waves' item buffers share 160 KB of LDS
     if (d_off && d_adj && env_i64("TGO_HOST_ASSEMBLY", 0) == 0) {
         std::string err;
         if (int rc = build_cold_blocks_device(d_off, d_adj, static_cast<int64_t>(off.size()) - 1, d_nnz, n_src, hot,
@@ -327,8 +328,8 @@ int upload_cold_blocks(tgo_ctx* ctx, const std::vector<int64_t>& off, const std:
     if (hc.win > 0) {                               // LDS window CSR: blocks over the active rows
         const std::vector<int64_t> woff_act(hc.woff.begin(), hc.woff.begin() + n_rows + 1);
         bool unused = false;
-        // wave items of the window pass (lds_window): <= 256 entries, <= 64 rows
-        if (int rc = upload_row_blocks_dev(ctx, woff_act, cb.rb_win, nullptr, 0, &unused, 256, kPackShift, 64)) return rc;
+        // wave items of the window pass (lds_window): <= 512 entries, <= 64 rows
+        if (int rc = upload_row_blocks_dev(ctx, woff_act, cb.rb_win, nullptr, 0, &unused, 512, kPackShift, 64)) return rc;
         HIP_TRY(upload(ctx, cb.woff, woff_act));
         if (hc.d_widx.present()) adopt(ctx, cb.widx, hc.d_widx);
         else HIP_TRY(upload(ctx, cb.widx, hc.widx));

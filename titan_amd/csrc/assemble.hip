@@ -507,13 +507,17 @@ int assemble_edges_device(const tgo_edges* e, const tgo_load_opts* opts, int64_t
             AS_TRY(vt.alloc(m));
             AS_TRY(k1[d].alloc(m));
             AS_TRY(v1[d].alloc(m));
+            lap(d == 0 ? "sort 1 OUT allocs" : "sort 1 IN allocs");
             if (m) edge_keys<<<grid(m), kB, 0, s>>>(d == 0 ? d_src.p : d_dst.p, d == 0 ? d_dst.p : d_src.p, m, b, nullptr,
                                                     kt.p, vt.p);
+            lap(d == 0 ? "sort 1 OUT keys" : "sort 1 IN keys");
             if (m) AS_TRY(so.pairs(kt.p, k1[d].p, vt.p, v1[d].p, m, bits));
+            lap(d == 0 ? "sort 1 OUT sort" : "sort 1 IN sort");
             AS_TRY(off[d].alloc(n + 1));
             row_offsets<<<grid(n + 1), kB, 0, s>>>(k1[d].p, m, b, n, off[d].p);
             AS_TRY(kept[d].alloc(n));
         }
+        lap("sort 1 scoped frees");
         ScopedBuf<unsigned long long> tr;
         AS_TRY(tr.alloc(1));
         AS_TRY(hipMemsetAsync(tr.p, 0, sizeof(unsigned long long), s));
@@ -552,6 +556,7 @@ int assemble_edges_device(const tgo_edges* e, const tgo_load_opts* opts, int64_t
                                                        reinterpret_cast<int32_t*>(dir[d].col.p));
             }
             AS_TRY(hipStreamSynchronize(s));             // the scoped buffers are freed next
+            lap(d == 0 ? "cut OUT" : "cut IN");
         }
     } else {
         AS_TRY(hipMemsetAsync(deg.p, 0, n * sizeof(uint32_t), s));
@@ -640,13 +645,16 @@ int assemble_edges_device(const tgo_edges* e, const tgo_load_opts* opts, int64_t
         AS_TRY(tk.alloc(c));
         AS_TRY(ts.alloc(c));
         AS_TRY(tv.alloc(g.has_weight ? c : 0));
+        lap("transpose allocs");
         if (c) transpose_keys<<<grid(c), kB, 0, s>>>(fkey[d].p, c, b, tk.p, g.has_weight ? tv.p : nullptr);
+        lap("transpose keys");
         if (g.has_weight) {
             AS_TRY(tvs.alloc(c));
             if (c) AS_TRY(so.pairs(tk.p, ts.p, tv.p, tvs.p, c, bits));
         } else if (c) {
             AS_TRY(so.keys(tk.p, ts.p, c, bits));
         }
+        lap("transpose sort");
         ScopedBuf<int64_t> off;
         AS_TRY(off.alloc(n + 1));
         row_offsets<<<grid(n + 1), kB, 0, s>>>(ts.p, c, b, n, off.p);

@@ -602,7 +602,7 @@ __global__ void __launch_bounds__(kBlock) cold_gather(const int64_t* __restrict_
 // and reduced in wave order.  Every row of [0, n_rows) gets its window sum in csum, which
 // cold_fold then accumulates the cold pieces onto: a fixed association, bitwise reproducible.
 constexpr int kWinThreads = 1024;                    // 16 independent waves per CU
-constexpr int kWinWaveTile = 256;                    // entries per wave item (4 per lane); <= 64 rows
+constexpr int kWinWaveTile = 512;                    // entries per wave item (8 per lane); <= 64 rows
 
 __device__ __forceinline__ void wave_sync() {          // a wave's LDS writes visible to its own later reads
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -611,10 +611,10 @@ __device__ __forceinline__ void wave_sync() {          // a wave's LDS writes vi
 }
 
 // Every wave works alone on items t = global wave, + all waves, ...: an item is <= 64 rows with
-// <= 256 window entries (build_row_blocks(tile 256, 64 rows)), or one longer row.  The wave
-// loads the next item's descriptor, indices and row bounds before it reduces the current one
-// from LDS, so each wave keeps its global loads in flight; no workgroup barrier after the
-// window is loaded.
+// <= 512 window entries (build_row_blocks(tile 512, 64 rows)), or one longer row.  Loads are
+// software-pipelined two deep so no wave waits on a chain of dependent loads: while item t is
+// reduced from LDS, item t+1's indices and row bounds (its descriptor arrived one trip ago)
+// and item t+2's descriptor are in flight.  No workgroup barrier after the window is loaded.
 __global__ void __launch_bounds__(kWinThreads) lds_window(const int64_t* __restrict__ woff,
         const uint16_t* __restrict__ widx, const int64_t* __restrict__ bdesc, int64_t nitems, int32_t win,
         const double* __restrict__ msg, double* __restrict__ csum) {
@@ -626,47 +626,58 @@ __global__ void __launch_bounds__(kWinThreads) lds_window(const int64_t* __restr
     __syncthreads();
     constexpr int kPerLane = kWinWaveTile / 64;
     const int64_t nwaves = static_cast<int64_t>(gridDim.x) * (kWinThreads / 64);
-    struct Item { int64_t r0, s0, r1, nnz; uint16_t v[kPerLane]; int64_t rb, re; };
-    auto fetch = [&](int64_t t, Item& it) {
-        it.r0 = it.s0 = it.r1 = 0; it.nnz = 0; it.rb = it.re = 0;
-        if (t >= nitems) return;
-        it.r0 = bdesc[2 * t]; it.s0 = bdesc[2 * t + 1];
-        it.r1 = bdesc[2 * t + 2]; it.nnz = bdesc[2 * t + 3] - it.s0;
-        if (it.nnz > kWinWaveTile) return;            // a long row: streamed when processed
+    struct Desc { int64_t r0, s0, r1, nnz; };
+    struct Data { uint16_t v[kPerLane]; int64_t rb, re; };
+    auto desc = [&](int64_t t) {
+        Desc d{0, 0, 0, 0};
+        if (t < nitems) {
+            d.r0 = bdesc[2 * t]; d.s0 = bdesc[2 * t + 1];
+            d.r1 = bdesc[2 * t + 2]; d.nnz = bdesc[2 * t + 3] - d.s0;
+        }
+        return d;
+    };
+    auto data = [&](const Desc& d) {
+        Data x;
+        x.rb = x.re = 0;
+        const bool small = d.nnz <= kWinWaveTile;     // a long row streams its entries when processed
 #pragma unroll
         for (int j = 0; j < kPerLane; ++j) {
             const int k = lane() + 64 * j;
-            it.v[j] = k < it.nnz ? widx[it.s0 + k] : 0;
+            x.v[j] = small && k < d.nnz ? widx[d.s0 + k] : 0;
         }
-        const int64_t i = it.r0 + lane();
-        if (i < it.r1) { it.rb = woff[i]; it.re = woff[i + 1]; }
+        const int64_t i = d.r0 + lane();
+        if (small && i < d.r1) { x.rb = woff[i]; x.re = woff[i + 1]; }
+        return x;
     };
-    Item cur, nxt;
     int64_t t = blockIdx.x * static_cast<int64_t>(kWinThreads / 64) + wave;
-    fetch(t, cur);
+    Desc dc = desc(t), dn = desc(t + nwaves);
+    Data xc = data(dc);
     for (; t < nitems; t += nwaves) {
-        fetch(t + nwaves, nxt);                       // next item's loads in flight
-        if (cur.nnz > kWinWaveTile) {                 // one long row: lanes stride its entries
+        const Desc dn2 = desc(t + 2 * nwaves);         // two items ahead: the descriptor
+        const Data xn = data(dn);                      // one item ahead: indices and row bounds
+        if (dc.nnz > kWinWaveTile) {                   // one long row: lanes stride its entries
             double acc = 0.0;
-            for (int64_t k = lane(); k < cur.nnz; k += 64) acc = acc + s_win[widx[cur.s0 + k]];
+            for (int64_t k = lane(); k < dc.nnz; k += 64) acc = acc + s_win[widx[dc.s0 + k]];
             acc = wave_sum(acc);
-            if (lane() == 0) csum[cur.r0] = acc;
+            if (lane() == 0) csum[dc.r0] = acc;
         } else {
 #pragma unroll
             for (int j = 0; j < kPerLane; ++j) {
                 const int k = lane() + 64 * j;
-                if (k < cur.nnz) s_val[k] = s_win[cur.v[j]];
+                if (k < dc.nnz) s_val[k] = s_win[xc.v[j]];
             }
             wave_sync();
-            const int64_t i = cur.r0 + lane();
-            if (i < cur.r1) {
+            const int64_t i = dc.r0 + lane();
+            if (i < dc.r1) {
                 double sum = 0.0;
-                for (int64_t k = cur.rb - cur.s0; k < cur.re - cur.s0; ++k) sum = sum + s_val[k];
+                for (int64_t k = xc.rb - dc.s0; k < xc.re - dc.s0; ++k) sum = sum + s_val[k];
                 csum[i] = sum;
             }
-            wave_sync();                              // s_val is rewritten by the next item
+            wave_sync();                               // s_val is rewritten by the next item
         }
-        cur = nxt;
+        dc = dn;
+        dn = dn2;
+        xc = xn;
     }
 }
 
