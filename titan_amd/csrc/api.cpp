@@ -2324,6 +2324,11 @@ int tgo_part_pr_blocked(tgo_ctx* ctx, int32_t world, int64_t active_span, int64_
     HIP_TRY(hipMemcpyAsync(&hbad, bad, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     if (hbad) return fail(ctx, TGO_E_INVALID, "tgo_part_pr_blocked: a source row lies beyond active_span");
+    // the mapping is not monotone in the global id: re-sort each row so the device build applies
+    if (env_i64("TGO_HOST_ASSEMBLY", 0) == 0) {
+        std::string err;
+        if (int r = sort_rows_device(g.in.off, nl, gidx, nnz, ctx->stream, err)) return fail(ctx, r, err);
+    }
     bool ready = false;
     const std::vector<int32_t> no_host_adj;
     if ((rc = upload_cold_blocks(ctx, off, no_host_adj, W * A, W * H, g.n_active, g.cold_in, ready, g.in.off, gidx, nnz)))

@@ -355,6 +355,7 @@ hipError_t k_gathered_pos(const int32_t* u, int64_t m, int64_t nl, int64_t A, in
 hipError_t k_sub_i32(int32_t* v, int64_t m, int32_t by, hipStream_t s);
 hipError_t k_pack_f64(const double* src, const int32_t* row, int64_t m, double* out, hipStream_t s);
 hipError_t k_unpack_f64(const double* in, const int32_t* pos, int64_t m, double* g, hipStream_t s);
+int sort_rows_device(const int64_t* d_off, int64_t n, int32_t* d_vals, int64_t m, hipStream_t s, std::string& err);
 hipError_t k_part_gathered_index(const int32_t* in, int64_t m, int64_t nl, int64_t A, int64_t H, int64_t W, int32_t* out,
                                  int* bad, hipStream_t s);
 

@@ -1024,21 +1024,19 @@ void weight_sorted_push(const HostGraph& g, HostCsr& ws, int threads) {
     }
     ws.adj.assign(static_cast<size_t>(ws.off[n]), 0);
     ws.w.assign(static_cast<size_t>(ws.off[n]), 0);
-    threads = std::max(1, threads);
-    std::vector<std::thread> th;
-    for (int t = 0; t < threads; ++t)
-        th.emplace_back([&, t] {
-            std::vector<std::pair<int32_t, int32_t>> buf;
-            for (int64_t v = n * t / threads; v < n * (t + 1) / threads; ++v) {
-                buf.clear();
-                for (const HostCsr* c : lists)
-                    for (int64_t k = c->off[v]; k < c->off[v + 1]; ++k) buf.emplace_back(c->w[k], c->adj[k]);
-                std::sort(buf.begin(), buf.end());
-                int64_t o = ws.off[v];
-                for (const auto& e : buf) { ws.w[o] = e.first; ws.adj[o] = e.second; ++o; }
-            }
-        });
-    for (auto& x : th) x.join();
+    // rows in small dynamic chunks: the degree-grouped order puts the hubs first, and a static
+    // split left one thread sorting all of them (8.2 s for the capped RMAT-24 graph)
+    parallel_dynamic(n, std::max(1, threads), 256, [&](int64_t lo, int64_t hi) {
+        std::vector<std::pair<int32_t, int32_t>> buf;
+        for (int64_t v = lo; v < hi; ++v) {
+            buf.clear();
+            for (const HostCsr* c : lists)
+                for (int64_t k = c->off[v]; k < c->off[v + 1]; ++k) buf.emplace_back(c->w[k], c->adj[k]);
+            std::sort(buf.begin(), buf.end());
+            int64_t o = ws.off[v];
+            for (const auto& e : buf) { ws.w[o] = e.first; ws.adj[o] = e.second; ++o; }
+        }
+    });
 }
 
 // ------------------------------------------------------------------ cache-blocked gather

@@ -431,4 +431,32 @@ hipError_t k_part_gathered_index(const int32_t* in, int64_t m, int64_t nl, int64
     return hipGetLastError();
 }
 
+namespace {
+__global__ void row_value_keys(const int64_t* __restrict__ off, int64_t n, const int32_t* __restrict__ v, int64_t m,
+                               uint64_t* __restrict__ key) {
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x)
+        key[k] = (static_cast<uint64_t>(row_of(off, n, k)) << 32) | static_cast<uint32_t>(v[k]);
+}
+__global__ void low_words(const uint64_t* __restrict__ key, int64_t m, int32_t* __restrict__ v) {
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x)
+        v[k] = static_cast<int32_t>(static_cast<uint32_t>(key[k]));
+}
+}  // namespace
+
+// Sort every row's (non-negative) values ascending in place: one radix sort of (row, value)
+// keys.  The partitioned PageRank maps its sources into the blocked gathered vector, which is
+// not monotone in the global id, so the rows are re-sorted before the device cold build.
+int sort_rows_device(const int64_t* d_off, int64_t n, int32_t* d_vals, int64_t m, hipStream_t s, std::string& err) {
+    if (m <= 1) return TGO_OK;
+    Buf<uint64_t> k0, k1;
+    PL_TRY(k0.alloc(m));
+    PL_TRY(k1.alloc(m));
+    row_value_keys<<<grid(m), kB, 0, s>>>(d_off, n, d_vals, m, k0.p);
+    Sort so{{}, 0, s};
+    PL_TRY(so.keys(k0.p, k1.p, m, 32 + bits_for(n)));
+    low_words<<<grid(m), kB, 0, s>>>(k1.p, m, d_vals);
+    PL_TRY(hipStreamSynchronize(s));
+    return TGO_OK;
+}
+
 }  // namespace tgo
