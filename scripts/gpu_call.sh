@@ -13,7 +13,7 @@ bash scripts/gpu_pr_ab.sh r04f_win "TGO_PR_WIN=0" "TGO_PR_WIN=12032" "TGO_PR_WIN
     > gpurun_out/r04f/ab.log 2>&1
 rc=$?; cat gpurun_out/r04f/ab.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
-    tests/test_gpu_distributed.py -k "native_msbfs_driver and 4" > gpurun_out/r04f/gpu_tests3.log 2>&1
+    tests/test_gpu_distributed.py -k "native or pagerank" > gpurun_out/r04f/gpu_tests3.log 2>&1
 rc=$?; tail -5 gpurun_out/r04f/gpu_tests3.log; [ $rc -eq 0 ] || exit $rc
 TGO_TRACE=1 timeout -k 10 300 python3 scripts/load27_trace.py 27 gpurun_out/r04f/load27_trace.json > gpurun_out/r04f/load27.log 2>&1
 rc=$?; grep -v "level" gpurun_out/r04f/load27.log | tail -40; exit $rc

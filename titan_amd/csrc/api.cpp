@@ -2512,8 +2512,7 @@ int tgo_part_sssp_relax(tgo_ctx* ctx, int64_t thr, int32_t nranks, int64_t* send
     }
     HIP_TRY(hipMemcpyAsync(offs, ho, nranks * sizeof(unsigned long long), hipMemcpyHostToDevice, st));
     HIP_TRY(k_ds_mark_pack(s.ds_rmark, words, wpr, g.n, s.ds_rbest, offs, cursor, send, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    return TGO_OK;
+    return part_done(ctx);          // the caller's exchange follows on the same stream
 }
 
 int tgo_part_sssp_apply(tgo_ctx* ctx, int64_t thr, const int64_t* recv, int64_t npairs, int64_t* counts) {

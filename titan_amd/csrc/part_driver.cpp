@@ -753,7 +753,7 @@ extern "C" int tgo_part_sssp_run(tgo_ctx* ctx, tgo_exchange* x, int64_t seed_glo
     hipStream_t st = d.st;
     int64_t *send = nullptr, *recv = nullptr, *sizes = nullptr;
     if ((rc = scratch(ctx, send, 2 * ng + 2, 14)) || (rc = scratch(ctx, recv, 2 * ng + 2, 15)) ||
-        (rc = scratch(ctx, sizes, 2 * W, 16)))
+        (rc = scratch(ctx, sizes, 4 * W, 16)))
         return rc;
     int64_t out[2] = {0, 0};
     if ((rc = tgo_part_sssp_begin(ctx, seed_global, delta, out))) return rc;
@@ -764,12 +764,26 @@ extern "C" int tgo_part_sssp_run(tgo_ctx* ctx, tgo_exchange* x, int64_t seed_glo
     if (delta <= 0) return part_fail(ctx, TGO_E_INVALID, "tgo_part_sssp_run: bucket width");
     int64_t thr = delta;
     int phases = 0;
-    std::vector<int64_t> sc(W), both(2 * W);
+    std::vector<int64_t> sc(W), both(4 * W);
     std::vector<size_t> sb(W), so(W), rb(W), ro(W);
     for (;;) {
+        // relax (a no-op on an empty near queue), then ONE all-to-all carrying, per peer, the
+        // pair elements sent to it and this rank's queue length: the sizes of the pair exchange
+        // and the global queue length arrive together (one host read per phase for both)
+        DevSpan span(st, "part.sssp.phase", {"phase", phases}, {"threshold", thr});
+        if ((rc = tgo_part_sssp_relax(ctx, thr, W, send, sc.data()))) break;
+        for (int p = 0; p < W; ++p) { both[2 * p] = 2 * sc[p]; both[2 * p + 1] = qlen; }
+        if (hipMemcpyAsync(sizes, both.data(), 2 * W * sizeof(int64_t), hipMemcpyHostToDevice, st) != hipSuccess) {
+            rc = d.hip("sizes upload");
+            break;
+        }
+        if (int r = x->all_to_all(sizes, sizes + 2 * W, 16, st)) { rc = d.xfail(r); break; }
+        if (hipMemcpyAsync(both.data(), sizes, 4 * W * sizeof(int64_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess) { rc = d.hip("sizes read"); break; }
         int64_t gq = 0;
-        if ((rc = d.reduce(&qlen, 1, tgo_exchange::kRedSum, &gq))) break;
-        if (gq == 0) {          // every near queue is empty: the next non-empty bucket
+        for (int p = 0; p < W; ++p) gq += both[2 * W + 2 * p + 1];
+        if (gq == 0) {          // every near queue was empty (nothing was relaxed): the next non-empty bucket
+            span.end();
             int64_t pm[2] = {0, 0}, mn = 0;
             if ((rc = tgo_part_sssp_pending_min(ctx, pm))) break;
             if ((rc = d.reduce(&pm[0], 1, tgo_exchange::kRedMin, &mn))) break;
@@ -780,20 +794,10 @@ extern "C" int tgo_part_sssp_run(tgo_ctx* ctx, tgo_exchange* x, int64_t seed_glo
             qlen = c[0];
             continue;
         }
-        DevSpan span(st, "part.sssp.phase", {"phase", phases}, {"threshold", thr});
-        if ((rc = tgo_part_sssp_relax(ctx, thr, W, send, sc.data()))) break;
-        for (int p = 0; p < W; ++p) both[p] = 2 * sc[p];
-        if (hipMemcpyAsync(sizes, both.data(), W * sizeof(int64_t), hipMemcpyHostToDevice, st) != hipSuccess) {
-            rc = d.hip("sizes upload");
-            break;
-        }
-        if (int r = x->all_to_all(sizes, sizes + W, 8, st)) { rc = d.xfail(r); break; }
-        if (hipMemcpyAsync(both.data(), sizes, 2 * W * sizeof(int64_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
-            hipStreamSynchronize(st) != hipSuccess) { rc = d.hip("sizes read"); break; }
         size_t a = 0, b = 0;
         for (int p = 0; p < W; ++p) {
-            sb[p] = static_cast<size_t>(both[p]) * 8; so[p] = a; a += sb[p];
-            rb[p] = static_cast<size_t>(both[W + p]) * 8; ro[p] = b; b += rb[p];
+            sb[p] = static_cast<size_t>(both[2 * p]) * 8; so[p] = a; a += sb[p];
+            rb[p] = static_cast<size_t>(both[2 * W + 2 * p]) * 8; ro[p] = b; b += rb[p];
         }
         if (int r = x->all_to_allv(send, sb.data(), so.data(), recv, rb.data(), ro.data(), st)) { rc = d.xfail(r); break; }
         int64_t c[2] = {0, 0};
