@@ -1,19 +1,18 @@
 #!/bin/bash
-# Round-4 call f2: the LDS window pass (wave items, prefetch): parity tests, then A/B of window sizes.
+# Round-4 call g: full GPU suite (logged), scale-27 load trace with the temporaries cache, the
+# one-GPU bench line and the partitioned world-1 bench line.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
-mkdir -p gpurun_out/r04f
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
-    tests/test_gpu_parity.py -k "pagerank" tests/test_gpu_trace.py > gpurun_out/r04f/gpu_tests.log 2>&1
-rc=$?; tail -5 gpurun_out/r04f/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
-    tests/test_gpu_assembly.py -k "pagerank" "tests/test_gpu_fullsize.py::test_config3_rmat24_pagerank_capped" \
-    > gpurun_out/r04f/gpu_tests2.log 2>&1
-rc=$?; tail -5 gpurun_out/r04f/gpu_tests2.log; [ $rc -eq 0 ] || exit $rc
-bash scripts/gpu_pr_ab.sh r04f_win "TGO_PR_WIN=0" "TGO_PR_WIN=12032" "TGO_PR_WIN=8192" "TGO_PR_WIN=4096" "TGO_PR_WIN=12032 TGO_PR_SKIP_BELOW=393216" \
-    > gpurun_out/r04f/ab.log 2>&1
-rc=$?; cat gpurun_out/r04f/ab.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
-    tests/test_gpu_distributed.py -k "native or pagerank" > gpurun_out/r04f/gpu_tests3.log 2>&1
-rc=$?; tail -5 gpurun_out/r04f/gpu_tests3.log; [ $rc -eq 0 ] || exit $rc
-TGO_TRACE=1 timeout -k 10 300 python3 scripts/load27_trace.py 27 gpurun_out/r04f/load27_trace.json > gpurun_out/r04f/load27.log 2>&1
-rc=$?; grep -v "level" gpurun_out/r04f/load27.log | tail -40; exit $rc
+mkdir -p gpurun_out/r04g
+timeout -k 10 1000 python -u -m pytest -x -v --timeout 600 --timeout-method thread -m gpu tests \
+    > gpurun_out/r04g/gpu_tests.log 2>&1
+rc=$?; grep -E "passed|failed|FAILED|Error" gpurun_out/r04g/gpu_tests.log | tail -8; [ $rc -eq 0 ] || exit $rc
+TGO_TRACE=1 timeout -k 10 300 python3 scripts/load27_trace.py 27 gpurun_out/r04g/load27_trace.json > gpurun_out/r04g/load27.log 2>&1
+rc=$?; grep -v "level" gpurun_out/r04g/load27.log | tail -45; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python3 bench.py > gpurun_out/r04g/bench.json 2> gpurun_out/r04g/bench.err
+rc=$?; tail -2 gpurun_out/r04g/bench.err; head -c 1500 gpurun_out/r04g/bench.json; echo; [ $rc -eq 0 ] || exit $rc
+export RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=29533
+timeout -k 10 600 python3 bench.py --partitioned --steps 3 --warmup 1 --cpu-baseline 0 --rows-scale 0 --sssp-roots 2 \
+    > gpurun_out/r04g/bench_part.json 2> gpurun_out/r04g/bench_part.err
+rc=$?; tail -2 gpurun_out/r04g/bench_part.err; python3 -c "
+import json; d=json.load(open('gpurun_out/r04g/bench_part.json')); print('GTEPS', d['value'], 'PR', d['pagerank_s_per_iter'], 'ss', d['single_source_gteps_hmean'], 'sssp', d['sssp'])"
+exit $rc

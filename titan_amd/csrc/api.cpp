@@ -159,9 +159,10 @@ int64_t env_i64(const char* name, int64_t dflt) {
     return v ? std::atoll(v) : dflt;
 }
 constexpr int64_t kPrHotDefault = 393216, kPrSegDefault = 393216;   // 3 MB each (profiles/r02an_pr_hot_seg_probe*.log)
-// LDS window of the hottest sources (lds_window, spmv.hip): 12032 doubles = 94 KB of a CU's
-// 160 KB LDS beside the 16 waves' 4 KB item buffers; 0 = off
-constexpr int64_t kPrWinDefault = 12032, kPrWinMax = 12288;
+// LDS window of the hottest sources (lds_window, spmv.hip; TGO_PR_WIN, at most 12288 doubles =
+// 96 KB beside the 16 waves' 4 KB item buffers).  Off by default: measured slower at every
+// window size (negative result 13: 1.252 -> 1.385-1.476 ms/update at RMAT-24)
+constexpr int64_t kPrWinDefault = 0, kPrWinMax = 12288;
 
 // PageRank diagnostics (engine.hpp PrTuning): TGO_PR_DIAG=lo:hi gathers only sources in
 // [lo, hi) — a timing attribution tool, its ranks are wrong (scripts/pr_probe.py).
@@ -934,6 +935,12 @@ int finish_distance_program(tgo_ctx* ctx, int scope, int flags, int64_t* dist_ou
 
 namespace tgo { double ms_split_of(const tgo_ctx* ctx); }
 
+namespace {
+struct TrimTemps {                  // tmp_cache.cpp: nothing stays reserved between loads
+    ~TrimTemps() { tgo::tmp_trim(); }
+};
+}  // namespace
+
 extern "C" {
 
 void tgo_default_options(tgo_options* o) {
@@ -1043,6 +1050,7 @@ int tgo_load_rows(tgo_ctx* ctx, const tgo_rows* rows, const tgo_schema* schema, 
 
 int tgo_finish_load(tgo_ctx* ctx) {
     Span load_span("load.finish_rows");
+    TrimTemps trim_temps;   // the build temporaries are released when the load returns
     if (!ctx) return TGO_E_INVALID;
     if (!ctx->staging.active) return fail(ctx, TGO_E_STATE, "tgo_finish_load without tgo_load_rows");
     (void)hipSetDevice(ctx->opts.device);
@@ -1080,6 +1088,7 @@ int tgo_finish_load(tgo_ctx* ctx) {
 
 int tgo_load_edges(tgo_ctx* ctx, const tgo_edges* edges, const tgo_load_opts* opts) {
     Span load_span("load.edges");
+    TrimTemps trim_temps;   // the build temporaries are released when the load returns
     if (!ctx) return TGO_E_INVALID;
     ctx->res_kind = -1;
     if (!edges || !opts || (edges->m > 0 && (!edges->src || !edges->dst)))
@@ -1109,6 +1118,7 @@ int tgo_load_csr(tgo_ctx* ctx, int64_t n, const int64_t* titan_ids, const int64_
                  const tgo_load_opts* opts) {
     if (!ctx) return TGO_E_INVALID;
     Span load_span("load.csr");
+    TrimTemps trim_temps;   // the build temporaries are released when the load returns
     ctx->res_kind = -1;
     if (!opts || !out_off || !in_off) return fail(ctx, TGO_E_INVALID, "null argument");
     if (opts->scope < 0 || opts->scope > 2) return fail(ctx, TGO_E_INVALID, "invalid scope");
@@ -1683,6 +1693,7 @@ int tgo_load_partition_layout(tgo_ctx* ctx, int64_t n_global, int64_t lo, int64_
                               const tgo_load_opts* opts, const int32_t* layout_global) {
     if (!ctx) return TGO_E_INVALID;
     Span load_span("load.partition");
+    TrimTemps trim_temps;   // the build temporaries are released when the load returns
     if (!edges || !opts || (edges->m > 0 && (!edges->src || !edges->dst))) return fail(ctx, TGO_E_INVALID, "null argument");
     if ((hi - lo) % 64 != 0) return fail(ctx, TGO_E_INVALID, "partition size must be a multiple of 64");
     (void)hipSetDevice(ctx->opts.device);
@@ -2306,6 +2317,7 @@ int tgo_part_pr_blocked(tgo_ctx* ctx, int32_t world, int64_t active_span, int64_
         *hot_per_rank = H;
         return TGO_OK;                                  // already built for this layout
     }
+    TrimTemps trim_temps;
     const int64_t A = active_span, W = world;
     std::vector<int64_t> off(nl + 1);
     HIP_TRY(hipMemcpy(off.data(), g.in.off, (nl + 1) * sizeof(int64_t), hipMemcpyDeviceToHost));

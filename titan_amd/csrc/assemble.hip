@@ -44,16 +44,19 @@ inline unsigned grid(int64_t work) {
 }
 
 template <class T>
-struct ScopedBuf {                      // scoped device buffer
+struct ScopedBuf {                      // scoped device buffer (large ones recycled: tmp_cache.cpp)
     T* p = nullptr;
     size_t n = 0;
     hipError_t alloc(size_t count) {
         release();
         n = count;
-        return hipMalloc(&p, std::max<size_t>(count, 1) * sizeof(T));
+        void* q = nullptr;
+        const hipError_t e = tmp_alloc(&q, std::max<size_t>(count, 1) * sizeof(T));
+        p = static_cast<T*>(q);
+        return e;
     }
     void release() {
-        if (p) (void)hipFree(p);
+        if (p) tmp_free(p, std::max<size_t>(n, 1) * sizeof(T));
         p = nullptr;
         n = 0;
     }

@@ -208,6 +208,11 @@ inline hipError_t copy_chunked(void* dst, const void* src, size_t bytes, hipMemc
     }
     return hipSuccess;
 }
+// Large temporaries of the load-time device builds (tmp_cache.cpp): freed blocks >= 64 MB are
+// reused by the next request they fit; tmp_trim releases them (every load entry point).
+hipError_t tmp_alloc(void** p, size_t bytes);
+void tmp_free(void* p, size_t bytes);
+void tmp_trim();
 // The same graph assembled on the device (assemble.hip): radix sorts instead of the host
 // counting sorts; m < 2^32.
 int assemble_edges_device(const tgo_edges* e, const tgo_load_opts* opts, int64_t hard_limit, HostGraph& g,

@@ -37,13 +37,18 @@ inline unsigned grid(int64_t work) {
 }
 
 template <class T>
-struct Buf {
+struct Buf {                            // large ones recycled (tmp_cache.cpp)
     T* p = nullptr;
+    size_t bytes = 0;
     hipError_t alloc(int64_t count) {
         release();
-        return hipMalloc(&p, static_cast<size_t>(std::max<int64_t>(count, 1)) * sizeof(T));
+        bytes = static_cast<size_t>(std::max<int64_t>(count, 1)) * sizeof(T);
+        void* q = nullptr;
+        const hipError_t e = tmp_alloc(&q, bytes);
+        p = static_cast<T*>(q);
+        return e;
     }
-    void release() { if (p) (void)hipFree(p); p = nullptr; }
+    void release() { if (p) tmp_free(p, bytes); p = nullptr; }
     T* take() { T* q = p; p = nullptr; return q; }     // hand over (DevArray::own)
     ~Buf() { release(); }
 };
