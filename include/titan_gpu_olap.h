@@ -326,7 +326,11 @@ int  tgo_copy_multi_distances(tgo_ctx* ctx, int32_t source, int64_t* dist_out);
 /* TGO_TUNE_MS_GHOST (partitioned tgo_part_msbfs_run): 1 (default) = a dense level refreshes
  * only the frontier masks this rank's lists read (ghost exchange: all-to-allv of precomputed
  * lists), 0 = all-gather of every rank's masks. */
-enum { TGO_TUNE_MS_SPLIT = 1, TGO_TUNE_MS_GHOST = 2 };
+/* TGO_TUNE_DS_BINS (one-GPU delta SSSP, tgo_sssp DELTA on a weighted load): 1 (default, or
+ * TGO_DS_BINS) = the next bucket is extracted from a pile of the vertices improved into it,
+ * 0 = by a scan of the whole pending bitmap.  TGO_TUNE_DS_PILE_CAP: entries a pile holds per
+ * bucket before that bucket falls back to the scan (0 = the vertex count; tests use small caps). */
+enum { TGO_TUNE_MS_SPLIT = 1, TGO_TUNE_MS_GHOST = 2, TGO_TUNE_DS_BINS = 3, TGO_TUNE_DS_PILE_CAP = 4 };
 int  tgo_set_tuning(tgo_ctx* ctx, int32_t key, double value);
 
 /* ---- Tracing (the reference's only hook is FulgoraGraphComputer.java:143,307

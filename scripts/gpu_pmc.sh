@@ -16,6 +16,9 @@ run_pass() {   # $1 = dir name, rest = counters
     return $rc
 }
 BENCH_ARGS="$*"
+# req: the request-rate set of DESIGN §4 (L2 requests, L2 channel / TA busy cycles) — the
+# bound of the PageRank and multi-source gathers is the L2 request rate, not HBM bytes
 run_pass fetch FETCH_SIZE && run_pass write WRITE_SIZE && run_pass hit TCC_HIT_sum TCC_MISS_sum && \
-    run_pass ea TCC_EA0_RDREQ_sum || exit 1
-python3 scripts/pmc_traffic.py $OUT/pmc_traffic.json $OUT/fetch $OUT/write $OUT/hit $OUT/ea
+    run_pass ea TCC_EA0_RDREQ_sum && \
+    run_pass req TCC_REQ_sum TCC_BUSY_sum TCP_TCC_READ_REQ_sum TA_TA_BUSY_sum GRBM_GUI_ACTIVE || exit 1
+python3 scripts/pmc_traffic.py $OUT/pmc_traffic.json $OUT/fetch $OUT/write $OUT/hit $OUT/ea $OUT/req

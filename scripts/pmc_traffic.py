@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 --pmc passes into per-launch HBM traffic for bench.py's roofline.
 
-usage: pmc_traffic.py OUT.json FETCH_DIR WRITE_DIR [HIT_DIR]
+usage: pmc_traffic.py OUT.json FETCH_DIR WRITE_DIR [HIT_DIR [EA_DIR [REQ_DIR]]]
 
 Each *_DIR holds one rocprofv3 `--pmc` pass (`--output-format csv`) of the same bench
 command: FETCH_SIZE, WRITE_SIZE and (optionally) TCC_HIT_sum + TCC_MISS_sum.  Kernels are
@@ -79,6 +79,13 @@ def main():
     rdreq = per_unit(passes, "TCC_EA0_RDREQ_sum")
     hit = per_unit(passes, "TCC_HIT_sum")
     miss = per_unit(passes, "TCC_MISS_sum")
+    # request-rate set: L2 requests, and busy cycles over all 128 L2 channels /
+    # 256 TAs against the XCD cycles (GRBM_GUI_ACTIVE is summed over the 8 XCDs)
+    req = per_unit(passes, "TCC_REQ_sum")
+    l1req = per_unit(passes, "TCP_TCC_READ_REQ_sum")
+    busy = per_unit(passes, "TCC_BUSY_sum")
+    ta = per_unit(passes, "TA_TA_BUSY_sum")
+    gui = per_unit(passes, "GRBM_GUI_ACTIVE")
     res = {}
     for g in GROUPS:
         if g not in fetch or g not in write:
@@ -92,6 +99,16 @@ def main():
             ent["ea_read_requests"] = rdreq[g]
         if g in hit and g in miss and hit[g] + miss[g] > 0:
             ent["l2_hit_rate"] = hit[g] / (hit[g] + miss[g])
+        if g in req:
+            ent["l2_requests"] = req[g]
+        if g in l1req:
+            ent["l1_to_l2_read_requests"] = l1req[g]
+        if g in gui and gui[g] > 0:
+            cyc = gui[g] / 8.0
+            if g in busy:
+                ent["l2_channel_busy"] = busy[g] / (128.0 * cyc)
+            if g in ta:
+                ent["ta_busy"] = ta[g] / (256.0 * cyc)
         res[g] = ent
     with open(out, "w") as f:
         json.dump(res, f, indent=1)

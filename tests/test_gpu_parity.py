@@ -278,6 +278,23 @@ def test_rmat_sssp_delta_equals_converged(rmat12, scope, delta):
         assert (st["relaxed_entries"] > 0) == (st["reached"] > 1)   # a seed with no push entries reaches nobody
 
 
+@pytest.mark.parametrize("scope", [OUT, IN])
+@pytest.mark.parametrize("delta", [0, 9, 37, 200])
+@pytest.mark.parametrize("bins,cap", [(1, 0), (1, 16), (1, 1024), (0, 0)])
+def test_rmat_sssp_delta_piles(rmat12, scope, delta, bins, cap):
+    """The binned loop (next bucket extracted from its pile of improved vertices), the same loop
+    with piles so small that buckets overflow into the bitmap scan, and the bitmap-scan loop all
+    give the oracle's converged distances bit for bit."""
+    n, src, dst, w, ids, oracle, roots = rmat12
+    eng = Engine().load_edges(n, src, dst, scope, weight=w)
+    eng.set_tuning(L.TUNE_DS_BINS, bins).set_tuning(L.TUNE_DS_PILE_CAP, cap)
+    for r in roots[:3]:
+        d = eng.sssp(int(r), n, scope, mode=L.SSSP_DELTA, seed_is_dense=True, stats=True, delta=delta)
+        od, _ = oracle.shortest_distance(int(ids[r]), n, scope, weighted=True)
+        assert np.array_equal(d, od)
+        assert eng.stats()["reached"] == int((od != ABSENT).sum())
+
+
 def test_rmat_sssp_delta_zero_weights(rmat12):
     """Zero-weight edges (ties inside a bucket, re-relaxation at equal distance)."""
     n, src, dst, w, ids, _, roots = rmat12

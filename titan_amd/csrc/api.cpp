@@ -69,6 +69,8 @@ struct tgo_ctx {
     int num_cus = 256;          // compute units of the device (persistent launches)
     double ms_split = -1.0;     // tgo_set_tuning(TGO_TUNE_MS_SPLIT); < 0: TGO_MS_SPLIT / the default
     int ms_ghost = 1;           // tgo_set_tuning(TGO_TUNE_MS_GHOST): dense partitioned levels exchange ghosts
+    int ds_bins = -1;           // tgo_set_tuning(TGO_TUNE_DS_BINS): 1 / 0; < 0: TGO_DS_BINS / on
+    int64_t ds_pile_cap = 0;    // tgo_set_tuning(TGO_TUNE_DS_PILE_CAP): entries per pile; 0 = n
     // state a native partitioned driver keeps between runs on this graph (part_driver.cpp:
     // the PageRank ghost lists); dropped with the graph
     std::shared_ptr<void> part_state;
@@ -104,6 +106,21 @@ hipError_t dev_alloc(tgo_ctx* ctx, T*& p, int64_t count) {
     ctx->dev_bytes += static_cast<int64_t>(bytes);
     p = static_cast<T*>(q);
     return hipSuccess;
+}
+
+// Release one dev_alloc array of `count` elements before the graph goes (the stream is
+// synchronised first: queued kernels may still use it).
+template <class T>
+void dev_free(tgo_ctx* ctx, T*& p, int64_t count) {
+    if (!p) return;
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    auto it = std::find(ctx->allocs.begin(), ctx->allocs.end(), static_cast<void*>(p));
+    if (it != ctx->allocs.end()) {
+        ctx->allocs.erase(it);
+        ctx->dev_bytes -= static_cast<int64_t>(std::max<int64_t>(count, 1) * sizeof(T));
+        (void)hipFree(p);
+    }
+    p = nullptr;
 }
 
 // Adopt a device array built on the device (DevArray): no copy, freed with the graph.
@@ -391,11 +408,17 @@ int upload_graph(tgo_ctx* ctx, HostGraph& h, bool allow_segments = true) {
     for (int64_t v = h.n - 1; v >= 0; --v)
         if (h.out.off[v + 1] > h.out.off[v] || h.in.off[v + 1] > h.in.off[v]) { g.n_active = v + 1; break; }
     g.min_weight = 0;
+    g.max_weight = 0;
     double wsum = 0.0;
     int64_t wcnt = 0;
     for (const HostCsr* c : {&h.out, &h.in})
         for (int32_t x : c->w)
-            if (x != kMissingWeight) { g.min_weight = std::min(g.min_weight, x); wsum += x; ++wcnt; }
+            if (x != kMissingWeight) {
+                g.min_weight = std::min(g.min_weight, x);
+                g.max_weight = std::max(g.max_weight, x);
+                wsum += x;
+                ++wcnt;
+            }
     g.mean_weight = wcnt ? wsum / static_cast<double>(wcnt) : 1.0;
     auto up = [&](HostCsr& src, DevCsr& dst) -> hipError_t {
         hipError_t e;
@@ -706,13 +729,20 @@ int64_t default_delta(const DevGraph& g, bool weighted) {
 // The light/heavy loop driven from the device (delta_loop.hip): the host enqueues steps in
 // batches and reads the loop state once per batch (dist, pending and member bitmaps are
 // initialised by the caller).
-int run_delta_device(tgo_ctx* ctx, int64_t seed, int64_t delta) {
+int run_delta_device(tgo_ctx* ctx, int64_t seed, int64_t delta, bool force_scan) {
     DevGraph& g = ctx->g;
     Scratch& s = ctx->sc;
     hipStream_t st = ctx->stream;
     const int64_t n = g.n;
     static const bool trace = env_double("TGO_TRACE", 0.0) != 0.0;
     static const int batch = static_cast<int>(std::max(1.0, env_double("TGO_DS_BATCH", 8.0)));
+    // Piles (binned loop, TGO_DS_BINS=0 turns them off): a relaxation from bucket k reaches at
+    // most bucket k + 1 + (max_weight - 1) / delta, so that many + 1 piles in a ring hold every
+    // pending vertex; wider weight ranges keep the bitmap-scan loop.
+    static const bool bins_env = env_double("TGO_DS_BINS", 1.0) != 0.0;
+    const bool bins_on = ctx->ds_bins < 0 ? bins_env : ctx->ds_bins != 0;
+    const int64_t reach = 2 + (std::max<int64_t>(g.max_weight, 1) - 1) / delta;
+    const int nbins = (bins_on && !force_scan && reach <= kDsMaxBins) ? static_cast<int>(reach) : 0;
     if (!s.ds_loop) {
         for (int b = 0; b < 2; ++b) {
             HIP_TRY(dev_alloc(ctx, s.ds_q[b], 2 * n + 2));
@@ -721,6 +751,20 @@ int run_delta_device(tgo_ctx* ctx, int64_t seed, int64_t delta) {
         HIP_TRY(dev_alloc(ctx, s.ds_loop, 1));
         ctx->st.device_bytes = ctx->dev_bytes;
     }
+    const int64_t cap = ctx->ds_pile_cap > 0 ? ctx->ds_pile_cap : std::max<int64_t>(n, 1024);
+    if (nbins && s.ds_pile && s.ds_pile_cap != cap) {
+        dev_free(ctx, s.ds_pile, kDsMaxBins * s.ds_pile_cap);
+        s.ds_pile_cap = 0;
+    }
+    if (nbins && !s.ds_pile) {
+        // a pile holds up to n appends per bucket (more drop to the bitmap scan of that bucket)
+        s.ds_pile_cap = cap;
+        HIP_TRY(dev_alloc(ctx, s.ds_pile, kDsMaxBins * s.ds_pile_cap));
+        if (!s.ds_mlist) HIP_TRY(dev_alloc(ctx, s.ds_mlist, n + 1));
+        if (!s.ds_done) HIP_TRY(dev_alloc(ctx, s.ds_done, (n + 63) / 64 + 1));
+        ctx->st.device_bytes = ctx->dev_bytes;
+    }
+    if (nbins) HIP_TRY(hipMemsetAsync(s.ds_done, 0, ((n + 63) / 64 + 1) * 8, st));
     HIP_TRY(k_ds_loop_seed(g.push_ws, s.ds_light, s.dist, s.ds_q[0], s.ds_qp[0], s.ds_loop, seed, delta, st));
     DsLoop h{};
     int cur = 0;
@@ -730,8 +774,13 @@ int run_delta_device(tgo_ctx* ctx, int64_t seed, int64_t delta) {
     for (int64_t steps = 0;;) {
         DevSpan span(st, "sssp.delta_steps", {"first_step", steps}, {"steps", batch});
         for (int k = 0; k < batch; ++k) {
-            HIP_TRY(k_ds_loop_step(g.push_ws, s.ds_light, s.vb, s.ds_member, n, s.dist, s.msg, s.ds_q, s.ds_qp,
-                                   s.ds_loop, cur, delta, st));
+            if (nbins)
+                HIP_TRY(k_ds_loop_step_bins(g.push_ws, s.ds_light, s.vb, s.ds_member, n, s.dist, s.msg, s.ds_q, s.ds_qp,
+                                            s.ds_loop, cur, delta, nbins, s.ds_pile, s.ds_pile_cap, s.ds_mlist,
+                                            s.ds_done, st));
+            else
+                HIP_TRY(k_ds_loop_step(g.push_ws, s.ds_light, s.vb, s.ds_member, n, s.dist, s.msg, s.ds_q, s.ds_qp,
+                                       s.ds_loop, cur, delta, st));
             cur ^= 1;
         }
         steps += batch;
@@ -739,13 +788,22 @@ int run_delta_device(tgo_ctx* ctx, int64_t seed, int64_t delta) {
         HIP_TRY(hipMemcpyAsync(&h, s.ds_loop, sizeof(DsLoop), hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
         if (h.err) return fail(ctx, TGO_E_PROGRAM, "vertex program failed: a traversed edge has no value for the weight property");
+        if (h.spill) break;
         if (h.done) break;
         if (steps > max_steps) return fail(ctx, TGO_E_HIP, "delta-stepping: the device loop did not converge");
     }
+    if (h.spill) {
+        // a relaxation reached past the piles (the weight bound was wrong): start again with
+        // the bitmap-scan loop (dist, pending and member state re-initialised by the caller)
+        trace_resolve(st);
+        return TGO_E_STATE;
+    }
     HIP_TRY(k_dist_finalize(s.dist, n, st));
     trace_resolve(st);
-    if (trace) std::fprintf(stderr, "[tgo] delta %lld (device loop): %llu phases, %llu buckets, %llu extractions, %llu entries relaxed\n",
-                            (long long)delta, h.phases, h.buckets, h.extractions, h.relaxed);
+    if (trace)
+        std::fprintf(stderr, "[tgo] delta %lld (device loop, %d piles): %llu phases, %llu buckets, %llu extractions "
+                     "(%llu bitmap scans), %llu entries relaxed\n", (long long)delta, nbins, h.phases, h.buckets,
+                     h.extractions, h.full_scans, h.relaxed);
     ctx->st.levels = static_cast<int32_t>(h.phases);
     ctx->st.relaxed_entries = static_cast<int64_t>(h.relaxed);
     return TGO_OK;
@@ -779,8 +837,14 @@ int run_delta_split(tgo_ctx* ctx, int64_t seed, int64_t delta) {
     static const bool host_loop = env_double("TGO_DS_HOSTLOOP", 0.0) != 0.0;
     constexpr int64_t kDsMaxCount = int64_t(1) << (64 - kDsCountShift);
     static_assert(kDsCountShift > 32 && kDsCountShift < 64, "queue counter layout");
-    if (!host_loop && seed >= 0 && 2 * n + 2 < kDsMaxCount && g.push_ws.nnz < (int64_t(1) << kDsCountShift))
-        return run_delta_device(ctx, seed, delta);
+    if (!host_loop && seed >= 0 && 2 * n + 2 < kDsMaxCount && g.push_ws.nnz < (int64_t(1) << kDsCountShift)) {
+        const int rc = run_delta_device(ctx, seed, delta, false);
+        if (rc != TGO_E_STATE) return rc;
+        HIP_TRY(k_fill_i64(s.dist, INT64_MAX, n, st));
+        HIP_TRY(hipMemsetAsync(s.vb, 0, words * 8, st));
+        HIP_TRY(hipMemsetAsync(s.ds_member, 0, words * 8, st));
+        return run_delta_device(ctx, seed, delta, true);
+    }
     int phases = 0, buckets = 0;
     int64_t relaxed = 0;
     // TGO_DS_TRACE=1: one line per phase (queue, entries, wall time since the previous phase)
@@ -963,6 +1027,14 @@ int tgo_set_tuning(tgo_ctx* ctx, int32_t key, double value) {
     case TGO_TUNE_MS_GHOST:
         if (value != 0.0 && value != 1.0) return fail(ctx, TGO_E_INVALID, "TGO_TUNE_MS_GHOST: 0 or 1");
         ctx->ms_ghost = value != 0.0 ? 1 : 0;
+        return TGO_OK;
+    case TGO_TUNE_DS_BINS:
+        if (value != 0.0 && value != 1.0 && value != -1.0) return fail(ctx, TGO_E_INVALID, "TGO_TUNE_DS_BINS: 0, 1 or -1");
+        ctx->ds_bins = static_cast<int>(value);
+        return TGO_OK;
+    case TGO_TUNE_DS_PILE_CAP:
+        if (!(value >= 0.0) || value > 9.0e15) return fail(ctx, TGO_E_INVALID, "TGO_TUNE_DS_PILE_CAP: entries >= 0");
+        ctx->ds_pile_cap = static_cast<int64_t>(value);
         return TGO_OK;
     default:
         return fail(ctx, TGO_E_INVALID, "tgo_set_tuning: unknown key");

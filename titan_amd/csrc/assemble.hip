@@ -532,6 +532,7 @@ int assemble_edges_device(const tgo_edges* e, const tgo_load_opts* opts, int64_t
             AS_TRY(flag.alloc(m));
             AS_TRY(pos.alloc(m + 1));
             if (keep_col) AS_TRY(colfull.alloc(m));
+            lap(d == 0 ? "cut OUT allocs" : "cut IN allocs");
             if (m) keep_flags<<<grid(m), kB, 0, s>>>(k1[d].p, m, b, off[d].p, kept[d].p, d == 1 ? kept[0].p : nullptr,
                                                      flag.p, keep_col ? colfull.p : nullptr);
             AS_TRY(so.excl_scan(flag.p, pos.p, m));
@@ -542,6 +543,7 @@ int assemble_edges_device(const tgo_edges* e, const tgo_load_opts* opts, int64_t
                 AS_TRY(hipMemcpyAsync(&lastf, flag.p + m - 1, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
             }
             AS_TRY(hipStreamSynchronize(s));
+            lap(d == 0 ? "cut OUT flags + scan" : "cut IN flags + scan");
             const int64_t kc = static_cast<int64_t>(cnt + lastf);
             dir[d].count = kc;
             // kept entries: sort-1 keys (original ids), edge index, column position
@@ -550,6 +552,7 @@ int assemble_edges_device(const tgo_edges* e, const tgo_load_opts* opts, int64_t
             if (keep_col) AS_TRY(dir[d].col.alloc(kc));
             ScopedBuf<uint32_t> sel;                           // sort-1 position of each kept entry
             AS_TRY(sel.alloc(kc));
+            lap(d == 0 ? "cut OUT kept allocs" : "cut IN kept allocs");
             if (m) compact_kept<<<grid(m), kB, 0, s>>>(k1[d].p, flag.p, pos.p, m, b, nullptr, dir[d].key.p, sel.p);
             if (kc) {
                 gather_i32<<<grid(kc), kB, 0, s>>>(sel.p, reinterpret_cast<const int32_t*>(v1[d].p), kc,

@@ -87,7 +87,9 @@ __device__ __forceinline__ void block_reserve(unsigned long long* qc, int64_t cn
 // ---------------------------------------------------------------- seed / decide
 __global__ void ds_loop_seed(const int64_t* off, const int64_t* light, int64_t* dist, int32_t* q, int64_t* qpre,
                              DsLoop* L, int64_t seed, int64_t delta) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    if (blockIdx.x != 0) return;
+    if (threadIdx.x < kDsMaxBins) L->bc[threadIdx.x] = 0;
+    if (threadIdx.x != 0) return;
     dist[seed] = 0;
     q[0] = static_cast<int32_t>(seed);
     qpre[0] = 0;
@@ -104,6 +106,14 @@ __global__ void ds_loop_seed(const int64_t* off, const int64_t* light, int64_t* 
     L->relaxed = 0;
     L->buckets = 0;
     L->extractions = 0;
+    L->bucket = 0;
+    L->xbin = -1;
+    L->xcount = 0;
+    L->xm = 0;
+    L->mcount = 0;
+    L->overflow = 0;
+    L->spill = 0;
+    L->full_scans = 0;
 }
 
 __device__ __forceinline__ unsigned long long load_agent(const unsigned long long* p) {
@@ -133,6 +143,55 @@ __device__ void decide_next(DsLoop* L, int cur, int64_t delta) {
     L->extractions += 1;
 }
 
+// The binned decision: when the near queue ran dry, the current bucket's pile if it holds
+// entries (improvements into the current bucket of vertices that were already pending).
+// Otherwise the bucket is finished: its members' distances are final, so their heavy entries
+// are taken now, once (a heavy entry cannot reach back into its own bucket), and the members
+// become `done`; the threshold moves to the nearest later bucket whose pile holds entries and
+// that pile is extracted in the same step; with no such pile only the heavy entries, and with
+// no members either the run is done.  A pile that dropped entries is extracted by the bitmap
+// scan instead (extract = 1: it takes every member from the member bitmap, none becomes done).
+__device__ void decide_bins(DsLoop* L, int cur, int64_t delta, int nbins, int64_t cap) {
+    L->extract = 0;
+    if (L->done || qcount(load_agent(&L->qc[cur])) != 0) return;
+    long long k = L->bucket;
+    int b = static_cast<int>(k % nbins);
+    unsigned long long c = load_agent(&L->bc[b]);
+    const bool finished = c == 0;
+    if (finished) {
+        int j = 1;
+        while (j < nbins && load_agent(&L->bc[(k + j) % nbins]) == 0) ++j;
+        if (j < nbins) {
+            k += j;
+            L->bucket = k;
+            L->thr = (k + 1) * delta;
+            L->buckets += 1;
+            b = static_cast<int>(k % nbins);
+            c = load_agent(&L->bc[b]);
+        } else if (L->mcount == 0) {
+            L->done = 1;
+            return;
+        } else {
+            b = -1;
+        }
+    }
+    L->extractions += 1;
+    L->xbin = b;
+    L->xcount = b >= 0 ? (c < static_cast<unsigned long long>(cap) ? c : static_cast<unsigned long long>(cap)) : 0;
+    L->xm = finished ? L->mcount : 0;
+    if (finished) L->mcount = 0;
+    L->extract = 2;
+    if (b >= 0) {
+        L->bc[b] = 0;
+        if ((L->overflow >> b) & 1ULL) {
+            L->overflow &= ~(1ULL << b);
+            L->extract = 1;
+            L->xm = 0;
+            L->mcount = 0;                   // the scan clears the member bitmap
+            L->full_scans += 1;
+        }
+    }
+}
 
 // ---------------------------------------------------------------- extract
 // chunk_extract (frontier.hpp) with the packed counter: pass 1 counts (slots and entries),
@@ -173,10 +232,9 @@ __device__ __forceinline__ void chunk_extract_packed(int64_t words, const Probe&
     });
 }
 
-__global__ void __launch_bounds__(kBlock) ds_extract_dev(const int64_t* __restrict__ off,
-        const int64_t* __restrict__ light, uint64_t* __restrict__ pend, uint64_t* __restrict__ member, int64_t n,
-        const int64_t* __restrict__ dist, DsLoop* L, int cur, int32_t* __restrict__ qn, int64_t* __restrict__ qpre) {
-    if (!L->extract) return;                                 // grid-uniform
+__device__ __forceinline__ void extract_scan(const int64_t* __restrict__ off, const int64_t* __restrict__ light,
+        uint64_t* __restrict__ pend, uint64_t* __restrict__ member, int64_t n, const int64_t* __restrict__ dist,
+        DsLoop* L, int cur, int32_t* __restrict__ qn, int64_t* __restrict__ qpre) {
     const int64_t thr = L->thr;
     const int64_t words = (n + 63) >> 6;
     long long left = kInf;                                   // smallest distance left pending
@@ -204,22 +262,107 @@ __global__ void __launch_bounds__(kBlock) ds_extract_dev(const int64_t* __restri
     if (threadIdx.x == 0 && m != kInf) atomicMin(&L->lo, m);
 }
 
+__global__ void __launch_bounds__(kBlock) ds_extract_dev(const int64_t* __restrict__ off,
+        const int64_t* __restrict__ light, uint64_t* __restrict__ pend, uint64_t* __restrict__ member, int64_t n,
+        const int64_t* __restrict__ dist, DsLoop* L, int cur, int32_t* __restrict__ qn, int64_t* __restrict__ qpre) {
+    if (L->extract != 1) return;                             // grid-uniform
+    extract_scan(off, light, pend, member, n, dist, L, cur, qn, qpre);
+}
+
+// The binned extraction (extract == 2): the decided pile's entries — a vertex is taken when it
+// is still pending and below the threshold, the pending bit cleared by the taking atomic, so a
+// vertex appended several times is taken once — then, when a bucket finished, its member
+// list's heavy entries (member words reset: every set bit of the member bitmap is on the list;
+// the members marked done).  Work proportional to the pile, not to n.
+__global__ void __launch_bounds__(kBlock) ds_extract_bins(const int64_t* __restrict__ off,
+        const int64_t* __restrict__ light, uint64_t* __restrict__ pend, uint64_t* __restrict__ member,
+        const int64_t* __restrict__ dist, DsLoop* L, int cur, const int32_t* __restrict__ pile, int64_t cap,
+        const int32_t* __restrict__ mlist, uint64_t* __restrict__ done, int32_t* __restrict__ qn,
+        int64_t* __restrict__ qpre, int64_t n) {
+    const unsigned long long mode = L->extract;             // grid-uniform
+    if (mode == 1) {                                         // an overflowed pile: the bitmap scan
+        extract_scan(off, light, pend, member, n, dist, L, cur, qn, qpre);
+        return;
+    }
+    if (mode != 2) return;
+    const int64_t thr = L->thr;
+    const int64_t xc = static_cast<int64_t>(L->xcount), total = xc + static_cast<int64_t>(L->xm);
+    const int32_t* __restrict__ pl = pile + (L->xbin >= 0 ? L->xbin : 0) * cap;
+    for (int64_t base = static_cast<int64_t>(blockIdx.x) * kBlock; base < total;
+         base += static_cast<int64_t>(gridDim.x) * kBlock) {                 // block-uniform trips
+        const int64_t i = base + threadIdx.x;
+        bool take = false;
+        int32_t entry = 0;
+        int64_t deg = 0;
+        if (i < xc) {
+            const int32_t v = pl[i];
+            const uint64_t bit = 1ULL << (v & 63);
+            if ((pend[v >> 6] & bit) && dist[v] < thr) {
+                const unsigned long long old = atomicAnd(reinterpret_cast<unsigned long long*>(&pend[v >> 6]), ~bit);
+                if (old & bit) {
+                    take = true;
+                    entry = v;
+                    deg = light_deg(off, light, v);
+                }
+            }
+        } else if (i < total) {                               // a finished bucket's member: final
+            const int32_t v = mlist[i - xc];
+            member[v >> 6] = 0;
+            atomicOr(reinterpret_cast<unsigned long long*>(&done[v >> 6]), 1ULL << (v & 63));
+            const int64_t hdeg = off[v + 1] - light[v];
+            if (hdeg > 0) {
+                take = true;
+                entry = static_cast<int32_t>(static_cast<uint32_t>(v) | kHeavy);
+                deg = hdeg;
+            }
+        }
+        int64_t slot, doff;
+        block_reserve(&L->qc[cur], take ? 1 : 0, deg, slot, doff);
+        if (take) {
+            qn[slot] = entry;
+            qpre[slot] = doff;
+        }
+    }
+}
+
 // ---------------------------------------------------------------- commit
+// kList (binned loop): a newly marked member is also appended to the member list (one
+// reservation per wave), so the extraction visits the members without scanning the bitmap.
+template <bool kList>
 __global__ void __launch_bounds__(kBlock) ds_commit_dev(const int32_t* __restrict__ q, const int64_t* __restrict__ dist,
-        int64_t* __restrict__ msg, uint64_t* __restrict__ pend, uint64_t* __restrict__ member, DsLoop* L, int cur) {
+        int64_t* __restrict__ msg, uint64_t* __restrict__ pend, uint64_t* __restrict__ member, DsLoop* L, int cur,
+        int32_t* __restrict__ mlist) {
     const int64_t qlen = qcount(L->qc[cur]);
     if (blockIdx.x == 0 && threadIdx.x == 0) L->qc[cur ^ 1] = 0;     // the relax appends there next
     bool marked = false;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < qlen; i += (int64_t)gridDim.x * blockDim.x) {
-        const uint32_t e = static_cast<uint32_t>(q[i]);
-        if (e & kHeavy) continue;
-        const int32_t v = static_cast<int32_t>(e);
-        msg[v] = dist[v];
-        const uint64_t bit = 1ULL << (v & 63);
-        if (pend[v >> 6] & bit) atomicAnd(reinterpret_cast<unsigned long long*>(&pend[v >> 6]), ~bit);
-        if (!(member[v >> 6] & bit)) {
-            atomicOr(reinterpret_cast<unsigned long long*>(&member[v >> 6]), bit);
-            marked = true;
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+    for (int64_t base = static_cast<int64_t>(blockIdx.x) * blockDim.x + (threadIdx.x & ~63u);
+         base < qlen; base += stride) {                      // wave-uniform trips
+        const int64_t i = base + lane();
+        bool nm = false;
+        int32_t v = -1;
+        if (i < qlen) {
+            const uint32_t e = static_cast<uint32_t>(q[i]);
+            if (!(e & kHeavy)) {
+                v = static_cast<int32_t>(e);
+                msg[v] = dist[v];
+                const uint64_t bit = 1ULL << (v & 63);
+                if (pend[v >> 6] & bit) atomicAnd(reinterpret_cast<unsigned long long*>(&pend[v >> 6]), ~bit);
+                if (!(member[v >> 6] & bit)) {
+                    const unsigned long long ob = atomicOr(reinterpret_cast<unsigned long long*>(&member[v >> 6]), bit);
+                    nm = !(ob & bit);
+                    marked = true;
+                }
+            }
+        }
+        if (kList) {
+            const unsigned long long bm = __ballot(nm);
+            if (bm) {
+                unsigned long long b0 = 0;
+                if (lane() == 0) b0 = atomicAdd(&L->mcount, static_cast<unsigned long long>(__popcll(bm)));
+                b0 = __shfl(b0, 0, 64);
+                if (nm) mlist[b0 + __popcll(bm & ((1ULL << lane()) - 1ULL))] = v;
+            }
         }
     }
     if (__ballot(marked) && lane() == 0) L->members = 1;
@@ -230,14 +373,24 @@ __global__ void __launch_bounds__(kBlock) ds_commit_dev(const int32_t* __restric
 // (for_each_queue_edge) with the total from the counter, and the takes of a whole tile
 // appended with one packed reservation (the per-trip block_append cost 8 reservations and
 // 16 barriers per tile).
+// kBins (binned loop): an improvement that is not taken into the near queue — a later bucket,
+// or the current bucket for a vertex already pending — is appended to its bucket's pile
+// (bucket / nbins ring), the appends of a tile aggregated per pile in LDS (one atomic per
+// pile and tile).
+template <bool kBins>
 __global__ void __launch_bounds__(kBlock) ds_relax_dev(const int64_t* __restrict__ off, const int32_t* __restrict__ adj,
         const int32_t* __restrict__ wt, const int64_t* __restrict__ light, const int32_t* __restrict__ q,
         const int64_t* __restrict__ qpre, const int64_t* __restrict__ msg, int64_t* __restrict__ dist,
-        uint64_t* __restrict__ pend, int32_t* __restrict__ qn, int64_t* __restrict__ qpre_n, DsLoop* L, int cur) {
+        uint64_t* __restrict__ pend, int32_t* __restrict__ qn, int64_t* __restrict__ qpre_n, DsLoop* L, int cur,
+        int64_t delta, int nbins, int32_t* __restrict__ pile, int64_t cap, const uint64_t* __restrict__ done) {
     const unsigned long long c = L->qc[cur];
     const int64_t qlen = qcount(c), total = qentries(c);
     if (qlen == 0) return;                                   // grid-uniform
     const int64_t thr = L->thr;
+    const int64_t bucket = kBins ? L->bucket : 0;
+    __shared__ unsigned int s_bn[kDsMaxBins];
+    __shared__ unsigned long long s_bb[kDsMaxBins];
+    bool spill = false;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         L->phases += 1;
         L->relaxed += static_cast<unsigned long long>(total);
@@ -252,6 +405,7 @@ __global__ void __launch_bounds__(kBlock) ds_relax_dev(const int64_t* __restrict
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int64_t t0 = tile * kTileEdges;
         const int64_t t1 = min(total, t0 + kTileEdges);
+        if (kBins && threadIdx.x < kDsMaxBins) s_bn[threadIdx.x] = 0;
         if (threadIdx.x == 0) {             // lo = last i with pre(i) <= t0; hi = last i with pre(i) <= t1-1
             int64_t a = 0, b = qlen;
             while (b - a > 1) { const int64_t m = (a + b) >> 1; if (qpre[m] <= t0) a = m; else b = m; }
@@ -307,23 +461,34 @@ __global__ void __launch_bounds__(kBlock) ds_relax_dev(const int64_t* __restrict
             du[k] = dist[u[k]];
         }
         int64_t cand[kEdgesPerThread], dt[kEdgesPerThread];
+        uint64_t dw[kEdgesPerThread];
+        if (kBins) {
+#pragma unroll
+            for (int k = 0; k < kEdgesPerThread; ++k)         // 3a: done words (L2-resident bitmap)
+                dw[k] = u[k] >= 0 ? done[t[k] >> 6] : 0ULL;
+        }
 #pragma unroll
         for (int k = 0; k < kEdgesPerThread; ++k) {           // 3: the targets' distances
             cand[k] = -1;
             if (u[k] < 0) continue;
             if (w[k] == kMissingWeight) { bad = true; continue; }     // edge.value(weight) on a missing key
             if (du[k] < mu[k]) continue;     // u improved during this phase: pending again, relaxes later
+            // a done target's distance is below every candidate of a later bucket: no read
+            if (kBins && ((dw[k] >> (t[k] & 63)) & 1ULL)) continue;
             cand[k] = mu[k] + static_cast<int64_t>(w[k]);
             dt[k] = dist[t[k]];
         }
         int32_t tv[kEdgesPerThread];
         int64_t td[kEdgesPerThread];
+        int32_t fb[kEdgesPerThread];                          // kBins: pile of a far append, or -1
+        unsigned int fl[kEdgesPerThread];                     // and its slot among the tile's appends
         int ntake = 0;
         int64_t dtake = 0;
 #pragma unroll
         for (int k = 0; k < kEdgesPerThread; ++k) {           // 4: min, pending bit, take
             tv[k] = -1;
             td[k] = 0;
+            fb[k] = -1;
             if (cand[k] < 0 || cand[k] >= dt[k]) continue;    // a stale (larger) read only costs an atomic
             const int32_t tk = t[k];
             const long long old = atomicMin(reinterpret_cast<long long*>(&dist[tk]), static_cast<long long>(cand[k]));
@@ -335,9 +500,33 @@ __global__ void __launch_bounds__(kBlock) ds_relax_dev(const int64_t* __restrict
                 td[k] = light_deg(off, light, tk);
                 ++ntake;
                 dtake += td[k];
+            } else if (kBins) {
+                const int64_t ahead = cand[k] / delta - bucket;
+                if (ahead >= nbins) {
+                    spill = true;
+                } else {
+                    fb[k] = static_cast<int32_t>((bucket + ahead) % nbins);
+                    fl[k] = atomicAdd(&s_bn[fb[k]], 1u);
+                }
             } else if (cand[k] < tmin) {
                 tmin = cand[k];
             }
+        }
+        if (kBins) {                                          // the tile's far appends, per pile
+            __syncthreads();
+            if (threadIdx.x < nbins) {
+                const unsigned int cnt = s_bn[threadIdx.x];
+                s_bb[threadIdx.x] = cnt ? atomicAdd(&L->bc[threadIdx.x], static_cast<unsigned long long>(cnt)) : 0ULL;
+                if (cnt && s_bb[threadIdx.x] + cnt > static_cast<unsigned long long>(cap))
+                    atomicOr(&L->overflow, 1ULL << threadIdx.x);
+            }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < kEdgesPerThread; ++k)
+                if (fb[k] >= 0) {
+                    const unsigned long long slot = s_bb[fb[k]] + fl[k];
+                    if (slot < static_cast<unsigned long long>(cap)) pile[fb[k] * cap + static_cast<int64_t>(slot)] = t[k];
+                }
         }
         // the tile's takes: one packed reservation (block-uniform call)
         int64_t slot, doff;
@@ -355,6 +544,10 @@ __global__ void __launch_bounds__(kBlock) ds_relax_dev(const int64_t* __restrict
         __syncthreads();
     }
     if (__ballot(bad) && lane() == 0) L->err = 1;
+    if (kBins) {
+        if (__ballot(spill) && lane() == 0) L->spill = 1;
+        return;
+    }
     const long long m = block_min(tmin);
     if (threadIdx.x == 0 && m != kInf) atomicMin(&L->tm, m);
 }
@@ -364,6 +557,9 @@ __global__ void __launch_bounds__(kBlock) ds_relax_dev(const int64_t* __restrict
 // the agent-scope fence every block issues before taking its ticket.)
 __global__ void ds_decide(DsLoop* L, int cur, int64_t delta) {
     if (threadIdx.x == 0 && blockIdx.x == 0) decide_next(L, cur, delta);
+}
+__global__ void ds_decide_bins(DsLoop* L, int cur, int64_t delta, int nbins, int64_t cap) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) decide_bins(L, cur, delta, nbins, cap);
 }
 
 }  // namespace
@@ -382,9 +578,26 @@ hipError_t k_ds_loop_step(const DevCsr& ws, const int64_t* light, uint64_t* pend
     ds_decide<<<1, 64, 0, s>>>(L, cur, delta);
     const int64_t words = (n + 63) / 64;
     ds_extract_dev<<<extract_grid(words), kBlock, 0, s>>>(ws.off, light, pend, member, n, dist, L, cur, q[cur], qpre[cur]);
-    ds_commit_dev<<<1024, kBlock, 0, s>>>(q[cur], dist, msg, pend, member, L, cur);
-    ds_relax_dev<<<256 * 8, kBlock, 0, s>>>(ws.off, ws.adj, ws.w, light, q[cur], qpre[cur], msg, dist, pend, q[cur ^ 1],
-                                            qpre[cur ^ 1], L, cur);
+    ds_commit_dev<false><<<1024, kBlock, 0, s>>>(q[cur], dist, msg, pend, member, L, cur, nullptr);
+    ds_relax_dev<false><<<256 * 8, kBlock, 0, s>>>(ws.off, ws.adj, ws.w, light, q[cur], qpre[cur], msg, dist, pend,
+                                                   q[cur ^ 1], qpre[cur ^ 1], L, cur, delta, 0, nullptr, 0, nullptr);
+    return hipGetLastError();
+}
+
+// One step of the binned loop: decide, extract (piles, or the bitmap scan for a pile that
+// overflowed — each kernel returns at once unless its mode was decided), commit, relax.
+hipError_t k_ds_loop_step_bins(const DevCsr& ws, const int64_t* light, uint64_t* pend, uint64_t* member, int64_t n,
+                               int64_t* dist, int64_t* msg, int32_t* const q[2], int64_t* const qpre[2], DsLoop* L,
+                               int cur, int64_t delta, int nbins, int32_t* pile, int64_t cap, int32_t* mlist,
+                               uint64_t* done, hipStream_t s) {
+    if (nbins < 2 || nbins > kDsMaxBins || nbins > kBlock || cap < 1) return hipErrorInvalidValue;
+    ds_decide_bins<<<1, 64, 0, s>>>(L, cur, delta, nbins, cap);
+    const int64_t words = (n + 63) / 64;
+    ds_extract_bins<<<extract_grid(words), kBlock, 0, s>>>(ws.off, light, pend, member, dist, L, cur, pile, cap, mlist,
+                                                           done, q[cur], qpre[cur], n);
+    ds_commit_dev<true><<<1024, kBlock, 0, s>>>(q[cur], dist, msg, pend, member, L, cur, mlist);
+    ds_relax_dev<true><<<256 * 8, kBlock, 0, s>>>(ws.off, ws.adj, ws.w, light, q[cur], qpre[cur], msg, dist, pend,
+                                                  q[cur ^ 1], qpre[cur ^ 1], L, cur, delta, nbins, pile, cap, done);
     return hipGetLastError();
 }
 

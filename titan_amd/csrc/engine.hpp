@@ -373,7 +373,7 @@ struct DevGraph {
     bool has_weight = false;
     int32_t weight_dt = TGO_DT_INTEGER;
     bool has_col = false;       // out.col / in.col hold column positions
-    int32_t min_weight = 0;
+    int32_t min_weight = 0, max_weight = 0;
     double mean_weight = 1.0;   // over present weights (delta-stepping's default bucket width)
     int32_t scope = TGO_SCOPE_BOTH_E;
     bool partitioned = false;   // 1-D vertex partition: rows [lo, lo+n) of an n_global graph
@@ -409,16 +409,30 @@ struct Counters {               // device-side level counters (one cache line ea
 
 // State of the device-driven delta-stepping loop (delta_loop.hip), in device memory.
 constexpr int kDsCountShift = 36;   // queue counters: count << 36 | entries (one atomic reserves both)
+// Binned form (kDsMaxBins piles): a relaxation that improves a vertex to a distance of a later
+// bucket appends it to that bucket's pile; the next bucket is extracted from its pile, not by
+// a scan of the whole pending bitmap (delta_loop.hip).
+constexpr int kDsMaxBins = 32;
 struct DsLoop {
     unsigned long long qc[2];   // per queue buffer
     long long tm;               // smallest improvement since the last extraction that queued nothing
     long long lo;               // smallest distance the last extraction left pending
     long long thr;              // bucket threshold
-    unsigned long long extract; // ds_decide -> extraction this step
+    unsigned long long extract; // ds_decide -> extraction this step: 0 none, 1 bitmap scan, 2 piles
     unsigned long long members; // a bucket member was marked since the last extraction
     unsigned long long done, err;
     unsigned long long phases, relaxed, buckets, extractions;
-    unsigned long long pad[3];
+    // binned loop
+    long long bucket;           // current bucket: thr = (bucket + 1) * delta
+    long long xbin;             // pile of the decided extraction (-1: members only)
+    unsigned long long xcount;  // its entries
+    unsigned long long xm;      // member-list entries of the decided extraction
+    unsigned long long mcount;  // member list length
+    unsigned long long overflow;          // bit b: pile b dropped entries (its bucket is scanned)
+    unsigned long long spill;   // a candidate beyond the piles' reach (cannot happen when the
+                                // piles cover the largest weight; the host then reruns unbinned)
+    unsigned long long full_scans;        // extractions that fell back to the bitmap scan
+    unsigned long long bc[kDsMaxBins];    // pile counts
 };
 
 struct Scratch {
@@ -466,6 +480,10 @@ struct Scratch {
     int32_t* ds_q[2] = {nullptr, nullptr};    // device-driven loop: queues (2n + 2: light + heavy)
     int64_t* ds_qp[2] = {nullptr, nullptr};   // and their entry offsets
     DsLoop* ds_loop = nullptr;
+    int32_t* ds_pile = nullptr;     // binned loop: kDsMaxBins piles of ds_pile_cap vertices
+    int64_t ds_pile_cap = 0;
+    int32_t* ds_mlist = nullptr;    // n: members of the current bucket
+    uint64_t* ds_done = nullptr;    // words: members of finished buckets (final distances)
     // generic vertex programs (allocated on first use): row-order staging + internal-order vectors
     int64_t* gv[3] = {nullptr, nullptr, nullptr};
     uint8_t* gh[3] = {nullptr, nullptr, nullptr};
@@ -540,6 +558,12 @@ hipError_t k_ds_loop_seed(const DevCsr& ws, const int64_t* light, int64_t* dist,
 hipError_t k_ds_loop_step(const DevCsr& ws, const int64_t* light, uint64_t* pend, uint64_t* member, int64_t n,
                           int64_t* dist, int64_t* msg, int32_t* const q[2], int64_t* const qpre[2], DsLoop* L, int cur,
                           int64_t delta, hipStream_t s);
+// the binned form: nbins piles of cap entries (pile), member list mlist (n), done bitmap (words,
+// zeroed by the caller: members of finished buckets)
+hipError_t k_ds_loop_step_bins(const DevCsr& ws, const int64_t* light, uint64_t* pend, uint64_t* member, int64_t n,
+                               int64_t* dist, int64_t* msg, int32_t* const q[2], int64_t* const qpre[2], DsLoop* L,
+                               int cur, int64_t delta, int nbins, int32_t* pile, int64_t cap, int32_t* mlist,
+                               uint64_t* done, hipStream_t s);
 hipError_t k_ds_pending_min(const uint64_t* pend, int64_t words, const int64_t* dist, Counters* cnt, hipStream_t s);
 hipError_t k_ds_extract(const View& push, uint64_t* pend, int64_t n, const int64_t* dist, int64_t thr, int32_t* qn,
                         int64_t* qdeg, Counters* cnt, hipStream_t s);

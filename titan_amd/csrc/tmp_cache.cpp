@@ -8,7 +8,10 @@
 // handed to the next request it fits (best fit within 2x), and every load entry point trims
 // the cache when it ends (tgo::tmp_trim), so nothing stays reserved between loads.
 #include <algorithm>
+#include <chrono>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <mutex>
 #include <vector>
 
@@ -20,6 +23,19 @@ constexpr size_t kCacheMin = size_t(64) << 20;
 struct Block { void* p; size_t bytes; };
 std::mutex g_mu;
 std::vector<Block> g_free;
+
+// TGO_TRACE=1: a driver call of >= 50 ms on stderr (the load laps show which phase stalls,
+// this shows whether an allocation or a device synchronisation is the stall)
+template <class F>
+hipError_t timed(const char* what, size_t bytes, F&& f) {
+    static const bool trace = std::getenv("TGO_TRACE") && std::atoi(std::getenv("TGO_TRACE")) != 0;
+    if (!trace) return f();
+    const auto t0 = std::chrono::steady_clock::now();
+    const hipError_t e = f();
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (ms >= 50.0) std::fprintf(stderr, "[tgo]     tmp %s %.2f GB: %.1f ms\n", what, bytes / 1e9, ms);
+    return e;
+}
 }  // namespace
 
 hipError_t tmp_alloc(void** p, size_t bytes) {
@@ -36,10 +52,10 @@ hipError_t tmp_alloc(void** p, size_t bytes) {
             g_free.erase(g_free.begin() + static_cast<long>(best));
             // its previous user's work may still be queued (on any stream, host copies included):
             // hand it out only once the device is idle
-            return hipDeviceSynchronize();
+            return timed("reuse sync", bytes, [] { return hipDeviceSynchronize(); });
         }
     }
-    hipError_t e = hipMalloc(p, bytes);
+    hipError_t e = timed("hipMalloc", bytes, [&] { return hipMalloc(p, bytes); });
     if (e == hipErrorOutOfMemory) {             // give the cached blocks back and retry once
         {
             std::lock_guard<std::mutex> lk(g_mu);
