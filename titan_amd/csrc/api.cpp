@@ -743,6 +743,11 @@ int run_delta_device(tgo_ctx* ctx, int64_t seed, int64_t delta, bool force_scan)
     const bool bins_on = ctx->ds_bins < 0 ? bins_env : ctx->ds_bins != 0;
     const int64_t reach = 2 + (std::max<int64_t>(g.max_weight, 1) - 1) / delta;
     const int nbins = (bins_on && !force_scan && reach <= kDsMaxBins) ? static_cast<int>(reach) : 0;
+    // TGO_DS_DONE=0: no done-target filter in the relax; TGO_DS_PILE_SCAN: piles above this
+    // fraction of n are extracted by the bitmap scan
+    static const bool done_filter = env_double("TGO_DS_DONE", 1.0) != 0.0;
+    static const double pile_scan = env_double("TGO_DS_PILE_SCAN", 1.0 / 16.0);
+    const int64_t scan_above = static_cast<int64_t>(pile_scan * static_cast<double>(n));
     if (!s.ds_loop) {
         for (int b = 0; b < 2; ++b) {
             HIP_TRY(dev_alloc(ctx, s.ds_q[b], 2 * n + 2));
@@ -777,7 +782,7 @@ int run_delta_device(tgo_ctx* ctx, int64_t seed, int64_t delta, bool force_scan)
             if (nbins)
                 HIP_TRY(k_ds_loop_step_bins(g.push_ws, s.ds_light, s.vb, s.ds_member, n, s.dist, s.msg, s.ds_q, s.ds_qp,
                                             s.ds_loop, cur, delta, nbins, s.ds_pile, s.ds_pile_cap, s.ds_mlist,
-                                            s.ds_done, st));
+                                            s.ds_done, done_filter, scan_above, st));
             else
                 HIP_TRY(k_ds_loop_step(g.push_ws, s.ds_light, s.vb, s.ds_member, n, s.dist, s.msg, s.ds_q, s.ds_qp,
                                        s.ds_loop, cur, delta, st));

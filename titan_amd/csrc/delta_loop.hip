@@ -114,6 +114,7 @@ __global__ void ds_loop_seed(const int64_t* off, const int64_t* light, int64_t* 
     L->overflow = 0;
     L->spill = 0;
     L->full_scans = 0;
+    L->xfin = 0;
 }
 
 __device__ __forceinline__ unsigned long long load_agent(const unsigned long long* p) {
@@ -151,7 +152,7 @@ __device__ void decide_next(DsLoop* L, int cur, int64_t delta) {
 // that pile is extracted in the same step; with no such pile only the heavy entries, and with
 // no members either the run is done.  A pile that dropped entries is extracted by the bitmap
 // scan instead (extract = 1: it takes every member from the member bitmap, none becomes done).
-__device__ void decide_bins(DsLoop* L, int cur, int64_t delta, int nbins, int64_t cap) {
+__device__ void decide_bins(DsLoop* L, int cur, int64_t delta, int nbins, int64_t cap, int64_t scan_above) {
     L->extract = 0;
     if (L->done || qcount(load_agent(&L->qc[cur])) != 0) return;
     long long k = L->bucket;
@@ -180,14 +181,18 @@ __device__ void decide_bins(DsLoop* L, int cur, int64_t delta, int nbins, int64_
     L->xcount = b >= 0 ? (c < static_cast<unsigned long long>(cap) ? c : static_cast<unsigned long long>(cap)) : 0;
     L->xm = finished ? L->mcount : 0;
     if (finished) L->mcount = 0;
+    L->xfin = finished ? 1 : 0;
     L->extract = 2;
     if (b >= 0) {
         L->bc[b] = 0;
-        if ((L->overflow >> b) & 1ULL) {
-            L->overflow &= ~(1ULL << b);
+        const bool over = (L->overflow >> b) & 1ULL;
+        L->overflow &= ~(1ULL << b);
+        // a pile past scan_above entries (random reads per entry) costs more than the scan's
+        // sequential pass over the bitmaps
+        if (over || c > static_cast<unsigned long long>(scan_above)) {
             L->extract = 1;
             L->xm = 0;
-            L->mcount = 0;                   // the scan clears the member bitmap
+            L->mcount = 0;                   // the scan takes every member from the bitmap
             L->full_scans += 1;
         }
     }
@@ -232,10 +237,13 @@ __device__ __forceinline__ void chunk_extract_packed(int64_t words, const Probe&
     });
 }
 
+// done (binned loop, may be null): when the decision found the bucket finished (L->xfin), the
+// members taken here are final and become done.
 __device__ __forceinline__ void extract_scan(const int64_t* __restrict__ off, const int64_t* __restrict__ light,
         uint64_t* __restrict__ pend, uint64_t* __restrict__ member, int64_t n, const int64_t* __restrict__ dist,
-        DsLoop* L, int cur, int32_t* __restrict__ qn, int64_t* __restrict__ qpre) {
+        DsLoop* L, int cur, int32_t* __restrict__ qn, int64_t* __restrict__ qpre, uint64_t* __restrict__ done) {
     const int64_t thr = L->thr;
+    uint64_t* const fin = (done && L->xfin) ? done : nullptr;
     const int64_t words = (n + 63) >> 6;
     long long left = kInf;                                   // smallest distance left pending
     auto probe = [&](int64_t wd, Take* t, bool commit) -> bool {
@@ -251,7 +259,10 @@ __device__ __forceinline__ void extract_scan(const int64_t* __restrict__ off, co
         const unsigned long long tm = __ballot(lt);
         if (commit && lane() == 0) {
             if (tm) pend[wd] = pb & ~tm;
-            if (mb) member[wd] = 0;
+            if (mb) {
+                member[wd] = 0;
+                if (fin) fin[wd] |= mb;
+            }
         }
         t[0] = {lt, static_cast<int32_t>(v), lt ? light_deg(off, light, v) : 0};
         t[1] = {hdeg > 0, static_cast<int32_t>(static_cast<uint32_t>(v) | kHeavy), hdeg};
@@ -266,7 +277,7 @@ __global__ void __launch_bounds__(kBlock) ds_extract_dev(const int64_t* __restri
         const int64_t* __restrict__ light, uint64_t* __restrict__ pend, uint64_t* __restrict__ member, int64_t n,
         const int64_t* __restrict__ dist, DsLoop* L, int cur, int32_t* __restrict__ qn, int64_t* __restrict__ qpre) {
     if (L->extract != 1) return;                             // grid-uniform
-    extract_scan(off, light, pend, member, n, dist, L, cur, qn, qpre);
+    extract_scan(off, light, pend, member, n, dist, L, cur, qn, qpre, nullptr);
 }
 
 // The binned extraction (extract == 2): the decided pile's entries — a vertex is taken when it
@@ -280,8 +291,8 @@ __global__ void __launch_bounds__(kBlock) ds_extract_bins(const int64_t* __restr
         const int32_t* __restrict__ mlist, uint64_t* __restrict__ done, int32_t* __restrict__ qn,
         int64_t* __restrict__ qpre, int64_t n) {
     const unsigned long long mode = L->extract;             // grid-uniform
-    if (mode == 1) {                                         // an overflowed pile: the bitmap scan
-        extract_scan(off, light, pend, member, n, dist, L, cur, qn, qpre);
+    if (mode == 1) {                                         // a large or overflowed pile: the bitmap scan
+        extract_scan(off, light, pend, member, n, dist, L, cur, qn, qpre, done);
         return;
     }
     if (mode != 2) return;
@@ -335,10 +346,11 @@ __global__ void __launch_bounds__(kBlock) ds_commit_dev(const int32_t* __restric
     const int64_t qlen = qcount(L->qc[cur]);
     if (blockIdx.x == 0 && threadIdx.x == 0) L->qc[cur ^ 1] = 0;     // the relax appends there next
     bool marked = false;
+    __shared__ unsigned int s_wc[kWavesPerBlock];
+    __shared__ unsigned long long s_mb;
     const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
-    for (int64_t base = static_cast<int64_t>(blockIdx.x) * blockDim.x + (threadIdx.x & ~63u);
-         base < qlen; base += stride) {                      // wave-uniform trips
-        const int64_t i = base + lane();
+    for (int64_t base = static_cast<int64_t>(blockIdx.x) * blockDim.x; base < qlen; base += stride) {   // block-uniform
+        const int64_t i = base + threadIdx.x;
         bool nm = false;
         int32_t v = -1;
         if (i < qlen) {
@@ -355,14 +367,19 @@ __global__ void __launch_bounds__(kBlock) ds_commit_dev(const int32_t* __restric
                 }
             }
         }
-        if (kList) {
+        if (kList) {                                          // one reservation per block and trip
             const unsigned long long bm = __ballot(nm);
-            if (bm) {
-                unsigned long long b0 = 0;
-                if (lane() == 0) b0 = atomicAdd(&L->mcount, static_cast<unsigned long long>(__popcll(bm)));
-                b0 = __shfl(b0, 0, 64);
-                if (nm) mlist[b0 + __popcll(bm & ((1ULL << lane()) - 1ULL))] = v;
+            const int wave = threadIdx.x >> 6;
+            if (lane() == 0) s_wc[wave] = static_cast<unsigned int>(__popcll(bm));
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                unsigned int tot = 0;
+                for (int w = 0; w < kWavesPerBlock; ++w) { const unsigned int x = s_wc[w]; s_wc[w] = tot; tot += x; }
+                s_mb = tot ? atomicAdd(&L->mcount, static_cast<unsigned long long>(tot)) : 0ULL;
             }
+            __syncthreads();
+            if (nm) mlist[s_mb + s_wc[wave] + __popcll(bm & ((1ULL << lane()) - 1ULL))] = v;
+            __syncthreads();
         }
     }
     if (__ballot(marked) && lane() == 0) L->members = 1;
@@ -465,7 +482,7 @@ __global__ void __launch_bounds__(kBlock) ds_relax_dev(const int64_t* __restrict
         if (kBins) {
 #pragma unroll
             for (int k = 0; k < kEdgesPerThread; ++k)         // 3a: done words (L2-resident bitmap)
-                dw[k] = u[k] >= 0 ? done[t[k] >> 6] : 0ULL;
+                dw[k] = (done && u[k] >= 0) ? done[t[k] >> 6] : 0ULL;
         }
 #pragma unroll
         for (int k = 0; k < kEdgesPerThread; ++k) {           // 3: the targets' distances
@@ -558,8 +575,8 @@ __global__ void __launch_bounds__(kBlock) ds_relax_dev(const int64_t* __restrict
 __global__ void ds_decide(DsLoop* L, int cur, int64_t delta) {
     if (threadIdx.x == 0 && blockIdx.x == 0) decide_next(L, cur, delta);
 }
-__global__ void ds_decide_bins(DsLoop* L, int cur, int64_t delta, int nbins, int64_t cap) {
-    if (threadIdx.x == 0 && blockIdx.x == 0) decide_bins(L, cur, delta, nbins, cap);
+__global__ void ds_decide_bins(DsLoop* L, int cur, int64_t delta, int nbins, int64_t cap, int64_t scan_above) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) decide_bins(L, cur, delta, nbins, cap, scan_above);
 }
 
 }  // namespace
@@ -589,15 +606,16 @@ hipError_t k_ds_loop_step(const DevCsr& ws, const int64_t* light, uint64_t* pend
 hipError_t k_ds_loop_step_bins(const DevCsr& ws, const int64_t* light, uint64_t* pend, uint64_t* member, int64_t n,
                                int64_t* dist, int64_t* msg, int32_t* const q[2], int64_t* const qpre[2], DsLoop* L,
                                int cur, int64_t delta, int nbins, int32_t* pile, int64_t cap, int32_t* mlist,
-                               uint64_t* done, hipStream_t s) {
+                               uint64_t* done, bool done_filter, int64_t scan_above, hipStream_t s) {
     if (nbins < 2 || nbins > kDsMaxBins || nbins > kBlock || cap < 1) return hipErrorInvalidValue;
-    ds_decide_bins<<<1, 64, 0, s>>>(L, cur, delta, nbins, cap);
+    ds_decide_bins<<<1, 64, 0, s>>>(L, cur, delta, nbins, cap, scan_above);
     const int64_t words = (n + 63) / 64;
     ds_extract_bins<<<extract_grid(words), kBlock, 0, s>>>(ws.off, light, pend, member, dist, L, cur, pile, cap, mlist,
                                                            done, q[cur], qpre[cur], n);
     ds_commit_dev<true><<<1024, kBlock, 0, s>>>(q[cur], dist, msg, pend, member, L, cur, mlist);
     ds_relax_dev<true><<<256 * 8, kBlock, 0, s>>>(ws.off, ws.adj, ws.w, light, q[cur], qpre[cur], msg, dist, pend,
-                                                  q[cur ^ 1], qpre[cur ^ 1], L, cur, delta, nbins, pile, cap, done);
+                                                  q[cur ^ 1], qpre[cur ^ 1], L, cur, delta, nbins, pile, cap,
+                                                  done_filter ? done : nullptr);
     return hipGetLastError();
 }
 

@@ -431,7 +431,8 @@ struct DsLoop {
     unsigned long long overflow;          // bit b: pile b dropped entries (its bucket is scanned)
     unsigned long long spill;   // a candidate beyond the piles' reach (cannot happen when the
                                 // piles cover the largest weight; the host then reruns unbinned)
-    unsigned long long full_scans;        // extractions that fell back to the bitmap scan
+    unsigned long long full_scans;        // extractions by the bitmap scan (large or overflowed piles)
+    unsigned long long xfin;    // the decided extraction follows a finished bucket (members final)
     unsigned long long bc[kDsMaxBins];    // pile counts
 };
 
@@ -563,7 +564,7 @@ hipError_t k_ds_loop_step(const DevCsr& ws, const int64_t* light, uint64_t* pend
 hipError_t k_ds_loop_step_bins(const DevCsr& ws, const int64_t* light, uint64_t* pend, uint64_t* member, int64_t n,
                                int64_t* dist, int64_t* msg, int32_t* const q[2], int64_t* const qpre[2], DsLoop* L,
                                int cur, int64_t delta, int nbins, int32_t* pile, int64_t cap, int32_t* mlist,
-                               uint64_t* done, hipStream_t s);
+                               uint64_t* done, bool done_filter, int64_t scan_above, hipStream_t s);
 hipError_t k_ds_pending_min(const uint64_t* pend, int64_t words, const int64_t* dist, Counters* cnt, hipStream_t s);
 hipError_t k_ds_extract(const View& push, uint64_t* pend, int64_t n, const int64_t* dist, int64_t thr, int32_t* qn,
                         int64_t* qdeg, Counters* cnt, hipStream_t s);
