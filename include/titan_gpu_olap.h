@@ -330,7 +330,10 @@ int  tgo_copy_multi_distances(tgo_ctx* ctx, int32_t source, int64_t* dist_out);
  * TGO_DS_BINS) = the next bucket is extracted from a pile of the vertices improved into it,
  * 0 = by a scan of the whole pending bitmap.  TGO_TUNE_DS_PILE_CAP: entries a pile holds per
  * bucket before that bucket falls back to the scan (0 = the vertex count; tests use small caps). */
-enum { TGO_TUNE_MS_SPLIT = 1, TGO_TUNE_MS_GHOST = 2, TGO_TUNE_DS_BINS = 3, TGO_TUNE_DS_PILE_CAP = 4 };
+/* TGO_TUNE_DS_DONE: 1 = the binned loop's relax skips the distance read of targets whose bucket
+ * finished (0, default: reads every target). */
+enum { TGO_TUNE_MS_SPLIT = 1, TGO_TUNE_MS_GHOST = 2, TGO_TUNE_DS_BINS = 3, TGO_TUNE_DS_PILE_CAP = 4,
+       TGO_TUNE_DS_DONE = 5 };
 int  tgo_set_tuning(tgo_ctx* ctx, int32_t key, double value);
 
 /* ---- Tracing (the reference's only hook is FulgoraGraphComputer.java:143,307

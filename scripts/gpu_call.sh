@@ -1,18 +1,13 @@
 #!/bin/bash
-# Round-4 call i: binned delta-stepping variants (pile-scan threshold, done filter) A/B with a
-# kernel trace, parity first.
+# Round-4 call j: load path changes (pinned-bounce downloads, huge-page host vectors, threaded
+# id fill, moved host vectors) against the assembly / full-size tests and the scale-27 trace;
+# delta SSSP parity with the tuning keys.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
-mkdir -p gpurun_out/r04i
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu \
-    tests/test_gpu_parity.py -k "sssp or delta" tests/test_gpu_fullsize.py::test_config5_rmat24_weighted_sssp \
-    > gpurun_out/r04i/tests.log 2>&1
-rc=$?; tail -3 gpurun_out/r04i/tests.log; [ $rc -eq 0 ] || exit $rc
-i=0
-for V in "TGO_DS_BINS=0" "TGO_DS_BINS=1" "TGO_DS_DONE=0" "TGO_DS_PILE_SCAN=0.25" "TGO_DS_PILE_SCAN=0.01" "TGO_DS_PILE_SCAN=0.01 TGO_DS_DONE=0"; do
-  env $V SSSP_BINS=-1 TGO_TRACE=1 timeout -k 10 300 python3 scripts/sssp_once.py 24 3 > gpurun_out/r04i/v$i.log 2>&1
-  rc=$?; echo "== $V"; grep -E "root" gpurun_out/r04i/v$i.log; [ $rc -eq 0 ] || exit $rc
-  i=$((i+1))
-done
-TGO_TRACE=1 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/r04i/sssp_kt -o run -- \
-    python3 scripts/sssp_once.py 24 2 > gpurun_out/r04i/sssp_once.log 2>&1
-rc=$?; grep -E "delta" gpurun_out/r04i/sssp_once.log | tail -4; exit $rc
+mkdir -p gpurun_out/r04j
+cat /sys/kernel/mm/transparent_hugepage/enabled /sys/kernel/mm/transparent_hugepage/defrag 2>&1 | head -2
+timeout -k 10 900 python -u -m pytest -x -q --timeout 400 --timeout-method thread -m gpu \
+    tests/test_gpu_parity.py -k "sssp or delta" tests/test_gpu_assembly.py tests/test_gpu_fullsize.py \
+    > gpurun_out/r04j/tests.log 2>&1
+rc=$?; tail -3 gpurun_out/r04j/tests.log; [ $rc -eq 0 ] || exit $rc
+TGO_TRACE=1 timeout -k 10 300 python3 scripts/load27_trace.py 27 gpurun_out/r04j/load27_trace.json > gpurun_out/r04j/load27.log 2>&1
+rc=$?; grep -v "level" gpurun_out/r04j/load27.log | tail -60; exit $rc

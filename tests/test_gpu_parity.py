@@ -280,14 +280,15 @@ def test_rmat_sssp_delta_equals_converged(rmat12, scope, delta):
 
 @pytest.mark.parametrize("scope", [OUT, IN])
 @pytest.mark.parametrize("delta", [0, 9, 37, 200])
-@pytest.mark.parametrize("bins,cap", [(1, 0), (1, 16), (1, 1024), (0, 0)])
-def test_rmat_sssp_delta_piles(rmat12, scope, delta, bins, cap):
-    """The binned loop (next bucket extracted from its pile of improved vertices), the same loop
-    with piles so small that buckets overflow into the bitmap scan, and the bitmap-scan loop all
-    give the oracle's converged distances bit for bit."""
+@pytest.mark.parametrize("bins,cap,done", [(1, 0, 0), (1, 0, 1), (1, 16, 1), (1, 1024, 0), (0, 0, 0)])
+def test_rmat_sssp_delta_piles(rmat12, scope, delta, bins, cap, done):
+    """The binned loop (next bucket extracted from its pile of improved vertices; with and
+    without the done-target filter), the same loop with piles so small that buckets overflow
+    into the bitmap scan, and the bitmap-scan loop all give the oracle's converged distances
+    bit for bit."""
     n, src, dst, w, ids, oracle, roots = rmat12
     eng = Engine().load_edges(n, src, dst, scope, weight=w)
-    eng.set_tuning(L.TUNE_DS_BINS, bins).set_tuning(L.TUNE_DS_PILE_CAP, cap)
+    eng.set_tuning(L.TUNE_DS_BINS, bins).set_tuning(L.TUNE_DS_PILE_CAP, cap).set_tuning(L.TUNE_DS_DONE, done)
     for r in roots[:3]:
         d = eng.sssp(int(r), n, scope, mode=L.SSSP_DELTA, seed_is_dense=True, stats=True, delta=delta)
         od, _ = oracle.shortest_distance(int(ids[r]), n, scope, weighted=True)

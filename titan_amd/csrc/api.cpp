@@ -71,6 +71,7 @@ struct tgo_ctx {
     int ms_ghost = 1;           // tgo_set_tuning(TGO_TUNE_MS_GHOST): dense partitioned levels exchange ghosts
     int ds_bins = -1;           // tgo_set_tuning(TGO_TUNE_DS_BINS): 1 / 0; < 0: TGO_DS_BINS / on
     int64_t ds_pile_cap = 0;    // tgo_set_tuning(TGO_TUNE_DS_PILE_CAP): entries per pile; 0 = n
+    int ds_done = -1;           // tgo_set_tuning(TGO_TUNE_DS_DONE): 1 / 0; < 0: TGO_DS_DONE / off
     // state a native partitioned driver keeps between runs on this graph (part_driver.cpp:
     // the PageRank ghost lists); dropped with the graph
     std::shared_ptr<void> part_state;
@@ -494,13 +495,15 @@ int upload_graph(tgo_ctx* ctx, HostGraph& h, bool allow_segments = true) {
         s.pub_seq = 0;
     }
     HIP_TRY(hipDeviceSynchronize());
-    ctx->titan_id = h.titan_id;
-    ctx->perm = h.perm;
+    // the host graph is dropped after the upload: its id and perm vectors move (1.5 GB at 2^27)
+    ctx->titan_id = std::move(h.titan_id);
+    ctx->perm = std::move(h.perm);
     if (ctx->perm.empty()) { ctx->perm.resize(n); for (int64_t v = 0; v < n; ++v) ctx->perm[v] = static_cast<int32_t>(v); }
     HIP_TRY(upload(ctx, g.perm, ctx->perm));
     ctx->id_index.clear();
     ctx->id_sorted = true;
-    for (int64_t v = 1; v < n && ctx->id_sorted; ++v) ctx->id_sorted = h.titan_id[v] > h.titan_id[v - 1];
+    if (!h.ids_sorted)
+        for (int64_t v = 1; v < n && ctx->id_sorted; ++v) ctx->id_sorted = ctx->titan_id[v] > ctx->titan_id[v - 1];
     ctx->st.num_vertices = n;
     ctx->st.out_entries = g.out.nnz;       // (the device lists were adopted: h's are empty)
     ctx->st.in_entries = g.in.nnz;
@@ -743,9 +746,11 @@ int run_delta_device(tgo_ctx* ctx, int64_t seed, int64_t delta, bool force_scan)
     const bool bins_on = ctx->ds_bins < 0 ? bins_env : ctx->ds_bins != 0;
     const int64_t reach = 2 + (std::max<int64_t>(g.max_weight, 1) - 1) / delta;
     const int nbins = (bins_on && !force_scan && reach <= kDsMaxBins) ? static_cast<int>(reach) : 0;
-    // TGO_DS_DONE=0: no done-target filter in the relax; TGO_DS_PILE_SCAN: piles above this
-    // fraction of n are extracted by the bitmap scan
-    static const bool done_filter = env_double("TGO_DS_DONE", 1.0) != 0.0;
+    // TGO_DS_DONE=1: the relax skips the distance read of done targets (measured neutral at
+    // RMAT-24: the largest phases come before most vertices are done); TGO_DS_PILE_SCAN: piles
+    // above this fraction of n are extracted by the bitmap scan
+    static const bool done_env = env_double("TGO_DS_DONE", 0.0) != 0.0;
+    const bool done_filter = ctx->ds_done < 0 ? done_env : ctx->ds_done != 0;
     static const double pile_scan = env_double("TGO_DS_PILE_SCAN", 1.0 / 16.0);
     const int64_t scan_above = static_cast<int64_t>(pile_scan * static_cast<double>(n));
     if (!s.ds_loop) {
@@ -1036,6 +1041,10 @@ int tgo_set_tuning(tgo_ctx* ctx, int32_t key, double value) {
     case TGO_TUNE_DS_BINS:
         if (value != 0.0 && value != 1.0 && value != -1.0) return fail(ctx, TGO_E_INVALID, "TGO_TUNE_DS_BINS: 0, 1 or -1");
         ctx->ds_bins = static_cast<int>(value);
+        return TGO_OK;
+    case TGO_TUNE_DS_DONE:
+        if (value != 0.0 && value != 1.0 && value != -1.0) return fail(ctx, TGO_E_INVALID, "TGO_TUNE_DS_DONE: 0, 1 or -1");
+        ctx->ds_done = static_cast<int>(value);
         return TGO_OK;
     case TGO_TUNE_DS_PILE_CAP:
         if (!(value >= 0.0) || value > 9.0e15) return fail(ctx, TGO_E_INVALID, "TGO_TUNE_DS_PILE_CAP: entries >= 0");

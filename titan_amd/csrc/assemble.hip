@@ -27,6 +27,8 @@
 #include <string>
 #include <vector>
 
+#include <thread>
+
 #include <hip/hip_runtime.h>
 #include <rocprim/rocprim.hpp>
 
@@ -427,11 +429,11 @@ __global__ void csr_stage(const int64_t* __restrict__ off, const int32_t* __rest
 
 template <class T>
 hipError_t download(std::vector<T>& h, const T* d, int64_t count, hipStream_t s) {
-    h.resize(static_cast<size_t>(count));
+    host_resize(h, static_cast<size_t>(count));
     if (count == 0) return hipSuccess;
     const hipError_t e = hipStreamSynchronize(s);
     if (e != hipSuccess) return e;
-    return copy_chunked(h.data(), d, static_cast<size_t>(count) * sizeof(T), hipMemcpyDeviceToHost);
+    return copy_d2h(h.data(), d, static_cast<size_t>(count) * sizeof(T));
 }
 
 }  // namespace
@@ -447,10 +449,27 @@ int assemble_edges_device(const tgo_edges* e, const tgo_load_opts* opts, int64_t
     g.has_weight = opts->weight_key != 0 && e->weight != nullptr;
     g.weight_dt = TGO_DT_INTEGER;
     const bool keep_col = (opts->flags & TGO_LOAD_COLUMN_ORDER) != 0;
-    g.titan_id.resize(n);
-    for (int64_t v = 0; v < n; ++v) g.titan_id[v] = e->titan_ids ? e->titan_ids[v] : ((v + 1) << 3);
-    for (int64_t v = 1; e->titan_ids && v < n; ++v)
-        if (e->titan_ids[v] <= e->titan_ids[v - 1]) { err = "titan_ids must be strictly increasing"; return TGO_E_INVALID; }
+    // ids: copied or synthesised by 8 host threads into huge-page-advised memory (n = 2^27 is
+    // 1 GB), strictly increasing (checked for caller ids)
+    host_resize(g.titan_id, static_cast<size_t>(n));
+    {
+        constexpr int kT = 8;
+        bool bad[kT] = {};
+        std::thread th[kT];
+        const int64_t per = (n + kT - 1) / kT;
+        for (int t = 0; t < kT; ++t)
+            th[t] = std::thread([&, t] {
+                const int64_t a = std::min(n, t * per), b = std::min(n, a + per);
+                for (int64_t v = a; v < b; ++v) {
+                    g.titan_id[v] = e->titan_ids ? e->titan_ids[v] : ((v + 1) << 3);
+                    if (e->titan_ids && v > 0 && e->titan_ids[v] <= e->titan_ids[v - 1]) bad[t] = true;
+                }
+            });
+        for (auto& x : th) x.join();
+        for (bool x : bad)
+            if (x) { err = "titan_ids must be strictly increasing"; return TGO_E_INVALID; }
+    }
+    g.ids_sorted = true;
     const bool cap = opts->apply_cap && opts->n_labels == 0 && opts->scope != TGO_SCOPE_BOTH_E;
     const int64_t limit = cap ? hard_limit : INT64_MAX;
     const bool sort1 = cap || keep_col;          // the cut / column positions need column order first

@@ -59,6 +59,7 @@ struct HostCsr {
 struct HostGraph {
     int64_t n = 0;
     std::vector<int64_t> titan_id;   // row order (the API's dense ids)
+    bool ids_sorted = false;         // titan_id known strictly increasing (no check needed)
     std::vector<int32_t> perm;       // row-order dense id -> internal id (degree-grouped)
     HostCsr out, in;
     HostCsr push_t;             // explicit transpose of the pull view (cap / asymmetric rows)
@@ -207,6 +208,23 @@ inline hipError_t copy_chunked(void* dst, const void* src, size_t bytes, hipMemc
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
+}
+// Large device -> host copies (tmp_cache.cpp): through two pinned 64 MB buffers, each piece
+// copied out by several host threads (a pageable hipMemcpy of GBs runs at a few GB/s); the
+// device data must be complete (the producing stream synchronised).
+hipError_t copy_d2h(void* dst, const void* src, size_t bytes);
+// madvise(MADV_HUGEPAGE) over a large host buffer before its first touch (fewer page faults).
+void advise_huge(void* p, size_t bytes);
+// Resize a host vector for a large download: capacity reserved untouched, advised huge, then
+// value-initialised (the zero fill faults 2 MB pages where the kernel allows them).
+template <class T>
+void host_resize(std::vector<T>& h, size_t count) {
+    if (count * sizeof(T) >= (size_t(64) << 20) && h.capacity() < count) {
+        std::vector<T>().swap(h);
+        h.reserve(count);
+        advise_huge(h.data(), count * sizeof(T));
+    }
+    h.resize(count);
 }
 // Large temporaries of the load-time device builds (tmp_cache.cpp): freed blocks >= 64 MB are
 // reused by the next request they fit; tmp_trim releases them (every load entry point).

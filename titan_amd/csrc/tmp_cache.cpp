@@ -12,8 +12,12 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <mutex>
+#include <thread>
 #include <vector>
+
+#include <sys/mman.h>
 
 #include <hip/hip_runtime.h>
 
@@ -78,6 +82,67 @@ void tmp_free(void* p, size_t bytes) {
         return;
     }
     (void)hipFree(p);
+}
+
+void advise_huge(void* p, size_t bytes) {
+    constexpr uintptr_t kHuge = uintptr_t(2) << 20;
+    const uintptr_t a = (reinterpret_cast<uintptr_t>(p) + kHuge - 1) & ~(kHuge - 1);
+    const uintptr_t b = (reinterpret_cast<uintptr_t>(p) + bytes) & ~(kHuge - 1);
+    if (b > a) (void)madvise(reinterpret_cast<void*>(a), b - a, MADV_HUGEPAGE);
+}
+
+hipError_t copy_d2h(void* dst, const void* src, size_t bytes) {
+    constexpr size_t kPiece = size_t(64) << 20;
+    constexpr int kThreads = 8;
+    auto plain = [&] {
+        for (size_t o = 0; o < bytes; o += 4 * kPiece) {
+            const hipError_t e = hipMemcpy(static_cast<char*>(dst) + o, static_cast<const char*>(src) + o,
+                                           std::min(4 * kPiece, bytes - o), hipMemcpyDeviceToHost);
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
+    };
+    if (bytes < 4 * kPiece) return plain();
+    static std::mutex mu;
+    static void* pin[2] = {nullptr, nullptr};
+    static hipStream_t st = nullptr;
+    static hipEvent_t ev[2] = {nullptr, nullptr};
+    static bool ready = false, failed = false;
+    std::lock_guard<std::mutex> lk(mu);
+    if (!ready && !failed) {
+        failed = hipHostMalloc(&pin[0], kPiece, hipHostMallocDefault) != hipSuccess ||
+                 hipHostMalloc(&pin[1], kPiece, hipHostMallocDefault) != hipSuccess ||
+                 hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess ||
+                 hipEventCreateWithFlags(&ev[0], hipEventDisableTiming) != hipSuccess ||
+                 hipEventCreateWithFlags(&ev[1], hipEventDisableTiming) != hipSuccess;
+        ready = !failed;
+        (void)hipGetLastError();
+    }
+    if (!ready) return plain();
+    const size_t np = (bytes + kPiece - 1) / kPiece;
+    auto issue = [&](size_t i) -> hipError_t {
+        const size_t o = i * kPiece, len = std::min(kPiece, bytes - o);
+        hipError_t e = hipMemcpyAsync(pin[i & 1], static_cast<const char*>(src) + o, len, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipEventRecord(ev[i & 1], st);
+        return e;
+    };
+    hipError_t e = issue(0);
+    for (size_t i = 0; i < np && e == hipSuccess; ++i) {
+        if (i + 1 < np && (e = issue(i + 1)) != hipSuccess) break;
+        if ((e = hipEventSynchronize(ev[i & 1])) != hipSuccess) break;
+        const size_t o = i * kPiece, len = std::min(kPiece, bytes - o);
+        const size_t per = (len + kThreads - 1) / kThreads;
+        std::thread th[kThreads];
+        for (int t = 0; t < kThreads; ++t) {
+            const size_t a = std::min(len, t * per), b = std::min(len, a + per);
+            th[t] = std::thread([=] {
+                if (b > a) std::memcpy(static_cast<char*>(dst) + o + a, static_cast<const char*>(pin[i & 1]) + a, b - a);
+            });
+        }
+        for (auto& x : th) x.join();
+    }
+    if (e != hipSuccess) (void)hipStreamSynchronize(st);
+    return e;
 }
 
 void tmp_trim() {
