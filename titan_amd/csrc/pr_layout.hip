@@ -196,13 +196,16 @@ struct Sort {
     }
 };
 
-template <class T>
-hipError_t fetch(std::vector<T>& h, const T* d, int64_t count, hipStream_t s) {
-    h.resize(static_cast<size_t>(count));
+// device -> host vector (pinned double-buffered copy, huge-page-advised vector); D may differ
+// from T in signedness only (same size)
+template <class T, class D>
+hipError_t fetch(std::vector<T>& h, const D* d, int64_t count, hipStream_t s) {
+    static_assert(sizeof(T) == sizeof(D), "fetch: element sizes differ");
+    host_resize(h, static_cast<size_t>(count));
     if (count <= 0) return hipSuccess;
     hipError_t e = hipStreamSynchronize(s);
     if (e != hipSuccess) return e;
-    return copy_chunked(h.data(), d, static_cast<size_t>(count) * sizeof(T), hipMemcpyDeviceToHost);
+    return copy_d2h(h.data(), d, static_cast<size_t>(count) * sizeof(T));
 }
 
 int bits_for(int64_t x) {
@@ -363,11 +366,7 @@ int build_cold_blocks_device(const int64_t* d_off, const int32_t* d_adj, int64_t
     PL_TRY(fetch(hc.poff, poff.p, np + 1, s));
     PL_TRY(fetch(h_pseg, pseg.p, np, s));
     PL_TRY(fetch(hc.cptr, cptr.p, n + 1, s));
-    {
-        std::vector<uint32_t> t;
-        PL_TRY(fetch(t, pix_s.p, np, s));
-        hc.cpid.assign(t.begin(), t.end());
-    }
+    PL_TRY(fetch(hc.cpid, pix_s.p, np, s));             // piece ids < 2^31 (checked above)
     PL_TRY(fetch(hc.hoff, hoff.p, n + 1, s));
     hc.crow.clear();
     for (int64_t r = 0; r < n; ++r)
