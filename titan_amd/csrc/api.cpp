@@ -47,6 +47,10 @@ struct tgo_ctx {
     int part_cur = 0;           // partitioned BFS: queue buffer holding the frontier
     int64_t part_qlen = 0;      // its length
     bool part_queued = true;    // q[part_cur] holds the frontier (pull / bottom-up levels only count it)
+    // native multi-source sweep (part_driver.cpp): this rank's slice of the candidate words is
+    // not packed but ORed in directly (tgo::part_ms_bypass); -1 = every slice packed
+    int part_ms_self = -1;
+    uint64_t* part_ms_cand = nullptr;
     const uint64_t* part_frontier = nullptr;   // after bottom-up: the caller's nb_local (queued lazily)
     int64_t* part_dcounts = nullptr;    // caller's device counts (tgo_part_device_counts)
     int64_t* part_qlen_dev = nullptr;   // device copy of the queue length (lazy host read)
@@ -2094,6 +2098,15 @@ int tgo_part_ms_push_masked(tgo_ctx* ctx, const uint64_t* fr_local, uint64_t* ca
 
 // The received candidate pairs OR-ed into fr_next (zeroed first), no settle: the pull of the
 // same level reads them (tgo_part_ms_pull_split).
+// With the own-slice bypass on: this rank's candidate words into the owned next masks.
+static hipError_t ms_or_own(tgo_ctx* ctx, uint64_t* fr_next) {
+    if (ctx->part_ms_self < 0 || !ctx->part_ms_cand) return hipSuccess;
+    const int64_t nl = ctx->g.n, cps = (nl + kPackChunk - 1) / kPackChunk;
+    uint8_t* touched = ctx->sc.pk_touch ? ctx->sc.pk_touch + static_cast<int64_t>(ctx->part_ms_self) * cps : nullptr;
+    return k_ms_or_local(ctx->part_ms_cand + static_cast<int64_t>(ctx->part_ms_self) * nl, nl, cps, touched, fr_next,
+                         ctx->stream);
+}
+
 int tgo_part_ms_or_fixed(tgo_ctx* ctx, const int64_t* recv, int32_t nslices, int64_t cap, uint64_t* fr_next) {
     int rc = part_check(ctx);
     if (rc) return rc;
@@ -2101,6 +2114,7 @@ int tgo_part_ms_or_fixed(tgo_ctx* ctx, const int64_t* recv, int32_t nslices, int
         return fail(ctx, TGO_E_INVALID, "ms_or_fixed: bad arguments");
     HIP_TRY(hipMemsetAsync(fr_next, 0, ctx->g.n_active * 8, ctx->stream));
     HIP_TRY(k_ms_or_fixed(recv, nslices, cap, fr_next, ctx->stream));
+    HIP_TRY(ms_or_own(ctx, fr_next));
     return part_done(ctx);
 }
 
@@ -2117,6 +2131,7 @@ int tgo_part_ms_or_pairs(tgo_ctx* ctx, const int64_t* recv, const int64_t* recv_
     }
     HIP_TRY(hipMemsetAsync(fr_next, 0, ctx->g.n_active * 8, ctx->stream));
     HIP_TRY(k_ms_or_pairs(recv, npairs, fr_next, ctx->stream));
+    HIP_TRY(ms_or_own(ctx, fr_next));
     return part_done(ctx);
 }
 
@@ -2247,11 +2262,12 @@ int tgo_part_ms_pack_dev(tgo_ctx* ctx, uint64_t* cand_global, int32_t nranks, in
         HIP_TRY(dev_alloc(ctx, s.pk_cnt, g.n_global / kPackChunk + kMaxRanks + 1));
         HIP_TRY(dev_alloc(ctx, s.pk_off, g.n_global / kPackChunk + kMaxRanks + 1));
     }
+    const int self = cand_global == ctx->part_ms_cand ? ctx->part_ms_self : -1;
     HIP_TRY(hipMemsetAsync(s.pk_cnt + nchunks, 0, sizeof(int64_t), st));
-    HIP_TRY(k_ms_pack(false, cand_global, g.n, cps, nchunks, s.pk_cnt, s.pk_off, send, st, s.pk_touch));
+    HIP_TRY(k_ms_pack(false, cand_global, g.n, cps, nchunks, s.pk_cnt, s.pk_off, send, st, s.pk_touch, self));
     HIP_TRY(scan_exclusive_i64(s.cub_tmp, s.cub_bytes, s.pk_cnt, s.pk_off, nchunks + 1, st));
     HIP_TRY(k_slice_elems(s.pk_off, cps, nranks, send_elems_dev, st));
-    HIP_TRY(k_ms_pack(true, cand_global, g.n, cps, nchunks, s.pk_cnt, s.pk_off, send, st, s.pk_touch));
+    HIP_TRY(k_ms_pack(true, cand_global, g.n, cps, nchunks, s.pk_cnt, s.pk_off, send, st, s.pk_touch, self));
     return part_done(ctx);
 }
 
@@ -2273,10 +2289,12 @@ int tgo_part_ms_pack_fixed(tgo_ctx* ctx, uint64_t* cand_global, int32_t nranks, 
         HIP_TRY(dev_alloc(ctx, s.pk_cnt, g.n_global / kPackChunk + kMaxRanks + 1));
         HIP_TRY(dev_alloc(ctx, s.pk_off, g.n_global / kPackChunk + kMaxRanks + 1));
     }
+    const int self = cand_global == ctx->part_ms_cand ? ctx->part_ms_self : -1;
     HIP_TRY(hipMemsetAsync(s.pk_cnt + nchunks, 0, sizeof(int64_t), st));
-    HIP_TRY(k_ms_pack(false, cand_global, g.n, cps, nchunks, s.pk_cnt, s.pk_off, send, st, s.pk_touch));
+    HIP_TRY(k_ms_pack(false, cand_global, g.n, cps, nchunks, s.pk_cnt, s.pk_off, send, st, s.pk_touch, self));
     HIP_TRY(scan_exclusive_i64(s.cub_tmp, s.cub_bytes, s.pk_cnt, s.pk_off, nchunks + 1, st));
-    HIP_TRY(k_ms_pack_fixed(cand_global, g.n, cps, nchunks, s.pk_off, nranks, cap, send, s.pk_ovf, s.pk_touch, st));
+    HIP_TRY(k_ms_pack_fixed(cand_global, g.n, cps, nchunks, s.pk_off, nranks, cap, send, s.pk_ovf, s.pk_touch, st,
+                            self));
     return part_done(ctx);
 }
 
@@ -2294,6 +2312,7 @@ int tgo_part_ms_settle_fixed(tgo_ctx* ctx, int32_t level, const int64_t* recv, i
     HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
     HIP_TRY(hipMemsetAsync(fr_next, 0, g.n_active * 8, st));     // the tail [n_active, n) stays zero
     HIP_TRY(k_ms_or_fixed(recv, nslices, cap, fr_next, st));
+    HIP_TRY(ms_or_own(ctx, fr_next));
     const int nxt = ctx->part_cur ^ 1;
     HIP_TRY(k_ms_settle(push_view(g, TGO_SCOPE_BOTH_E), g.n_active, s.ms_vis, fr_next, ms_planes(ctx), s.q[nxt], s.qdeg,
                         s.cnt, level + 1, st));
@@ -2321,6 +2340,7 @@ int tgo_part_ms_settle_pairs(tgo_ctx* ctx, int32_t level, const int64_t* recv, c
         npairs += recv_counts[r];
     }
     HIP_TRY(k_ms_or_pairs(recv, npairs, fr_next, st));
+    HIP_TRY(ms_or_own(ctx, fr_next));
     const int nxt = ctx->part_cur ^ 1;
     HIP_TRY(k_ms_settle(push_view(g, TGO_SCOPE_BOTH_E), g.n_active, s.ms_vis, fr_next, ms_planes(ctx), s.q[nxt], s.qdeg,
                         s.cnt, level + 1, st));
@@ -2889,6 +2909,10 @@ namespace tgo {
 hipStream_t part_stream(tgo_ctx* ctx) { return ctx->stream; }
 int part_fail(tgo_ctx* ctx, int code, const std::string& msg) { return fail(ctx, code, msg); }
 int64_t* part_dcounts_of(tgo_ctx* ctx) { return ctx->part_dcounts; }
+void part_ms_bypass(tgo_ctx* ctx, uint64_t* cand_global, int self) {
+    ctx->part_ms_cand = cand_global;
+    ctx->part_ms_self = cand_global ? self : -1;
+}
 std::shared_ptr<void>& part_state_of(tgo_ctx* ctx) { return ctx->part_state; }
 int part_in_list(tgo_ctx* ctx, const int32_t** adj, int64_t* nnz) {
     if (int rc = part_check(ctx)) return rc;

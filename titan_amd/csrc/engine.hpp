@@ -623,11 +623,15 @@ hipError_t k_ms_extract(LevelPlanes lvl, int nplanes, const uint64_t* vis, const
 hipError_t k_or_slices(const uint64_t* recv, int nslices, int64_t n_local, uint64_t* out, hipStream_t s);
 constexpr int64_t kPackChunk = 2048;   // candidate words per wave in the sparse-exchange pack
 hipError_t k_ms_pack(bool write, uint64_t* cand, int64_t n_local, int64_t cps, int64_t nchunks, int64_t* cnt,
-                     const int64_t* offs, int64_t* send, hipStream_t s, uint8_t* touched = nullptr);
+                     const int64_t* offs, int64_t* send, hipStream_t s, uint8_t* touched = nullptr, int self = -1);
+// the own slice left by a pack with self: OR into nx, cleared (touched chunks only)
+hipError_t k_ms_or_local(uint64_t* cand_own, int64_t n_local, int64_t cps, uint8_t* touched_own, uint64_t* nx,
+                         hipStream_t s);
 hipError_t k_slice_elems(const int64_t* off, int64_t cps, int nranks, int64_t* out, hipStream_t s);
 hipError_t k_ms_or_pairs(const int64_t* pairs, int64_t npairs, uint64_t* nx, hipStream_t s);
 hipError_t k_ms_pack_fixed(uint64_t* cand, int64_t n_local, int64_t cps, int64_t nchunks, const int64_t* offs,
-                           int nranks, int64_t cap, int64_t* send, int* ovf, uint8_t* touched, hipStream_t s);
+                           int nranks, int64_t cap, int64_t* send, int* ovf, uint8_t* touched, hipStream_t s,
+                           int self = -1);
 hipError_t k_ms_or_fixed(const int64_t* recv, int nslices, int64_t cap, uint64_t* nx, hipStream_t s);
 hipError_t k_part_td_mark(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen,
                           uint64_t* disc, const uint64_t* vb_local, int64_t lo, int64_t n_local, hipStream_t s);

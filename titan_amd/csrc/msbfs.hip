@@ -379,17 +379,19 @@ __global__ void or_slices(const uint64_t* __restrict__ recv, int nslices, int64_
 // zero again for the next level).  No atomics: the pair order is deterministic.
 // touched (optional): per-chunk flags set by ms_push — a chunk no push wrote is all zero and
 // is skipped without reading its words; the write pass clears the flags it consumed.
+// self >= 0: the chunks of that slice (the packing rank's own vertices) are not packed; their
+// words stay for ms_or_local (no pairs to or from oneself).
 template <bool kWrite>
 __global__ void __launch_bounds__(kBlock) ms_pack(uint64_t* __restrict__ cand, int64_t n_local, int64_t cps,
         int64_t nchunks, int64_t* __restrict__ cnt, const int64_t* __restrict__ offs, int64_t* __restrict__ send,
-        uint8_t* __restrict__ touched) {
+        uint8_t* __restrict__ touched, int self) {
     const int64_t c = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
     if (c >= nchunks) return;
-    if (touched && !touched[c]) {
+    const int64_t r = c / cps, j = c - r * cps;
+    if ((touched && !touched[c]) || r == self) {
         if (!kWrite && lane() == 0) cnt[c] = 0;
         return;
     }
-    const int64_t r = c / cps, j = c - r * cps;
     const int64_t w0 = r * n_local + j * kPackChunk;
     const int64_t w1 = r * n_local + min(n_local, (j + 1) * kPackChunk);
     int64_t base = kWrite ? offs[c] : 0;
@@ -421,11 +423,11 @@ __global__ void slice_elems(const int64_t* __restrict__ off, int64_t cps, int nr
 // level's frontier entries); a count over cap is recorded in *ovf and fails the sweep.
 __global__ void __launch_bounds__(kBlock) ms_pack_fixed(uint64_t* __restrict__ cand, int64_t n_local, int64_t cps,
         int64_t nchunks, const int64_t* __restrict__ offs, int64_t cap, int64_t* __restrict__ send, int* ovf,
-        uint8_t* __restrict__ touched) {
+        uint8_t* __restrict__ touched, int self) {
     const int64_t c = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
     if (c >= nchunks) return;
-    if (touched && !touched[c]) return;
     const int64_t r = c / cps, j = c - r * cps;
+    if ((touched && !touched[c]) || r == self) return;
     const int64_t w0 = r * n_local + j * kPackChunk;
     const int64_t w1 = r * n_local + min(n_local, (j + 1) * kPackChunk);
     int64_t base = offs[c] - offs[r * cps];                 // pair index within owner r's slot
@@ -472,6 +474,24 @@ __global__ void ms_or_fixed(const int64_t* __restrict__ recv, int nslices, int64
 __global__ void ms_or_pairs(const int64_t* __restrict__ pairs, int64_t npairs, uint64_t* __restrict__ nx) {
     for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < npairs; k += (int64_t)gridDim.x * blockDim.x)
         atomicOr(reinterpret_cast<unsigned long long*>(nx + pairs[2 * k]), static_cast<unsigned long long>(pairs[2 * k + 1]));
+}
+
+// The packing rank's own slice of the candidate words (left by ms_pack with self): OR into
+// the owned next masks and clear, chunk by chunk (only chunks a push touched), flags reset.
+__global__ void __launch_bounds__(kBlock) ms_or_local(uint64_t* __restrict__ cand_own, int64_t n_local, int64_t cps,
+        uint8_t* __restrict__ touched_own, uint64_t* __restrict__ nx) {
+    const int64_t j = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    if (j >= cps) return;
+    if (touched_own && !touched_own[j]) return;
+    const int64_t w1 = min(n_local, (j + 1) * kPackChunk);
+    for (int64_t i = j * kPackChunk + lane(); i < w1; i += 64) {
+        const uint64_t m = cand_own[i];
+        if (m) {
+            nx[i] |= m;
+            cand_own[i] = 0;
+        }
+    }
+    if (touched_own && lane() == 0) touched_own[j] = 0;
 }
 
 // Per-source reached vertices / entries (stats, untimed): 64 counters per block in LDS.
@@ -603,10 +623,16 @@ hipError_t k_ms_reach(const View& v, const uint64_t* vis, int64_t n_active, int 
     return hipGetLastError();
 }
 hipError_t k_ms_pack(bool write, uint64_t* cand, int64_t n_local, int64_t cps, int64_t nchunks, int64_t* cnt,
-                     const int64_t* offs, int64_t* send, hipStream_t s, uint8_t* touched) {
+                     const int64_t* offs, int64_t* send, hipStream_t s, uint8_t* touched, int self) {
     const unsigned blocks = static_cast<unsigned>((nchunks * 64 + kBlock - 1) / kBlock);
-    if (write) ms_pack<true><<<blocks, kBlock, 0, s>>>(cand, n_local, cps, nchunks, cnt, offs, send, touched);
-    else ms_pack<false><<<blocks, kBlock, 0, s>>>(cand, n_local, cps, nchunks, cnt, offs, send, touched);
+    if (write) ms_pack<true><<<blocks, kBlock, 0, s>>>(cand, n_local, cps, nchunks, cnt, offs, send, touched, self);
+    else ms_pack<false><<<blocks, kBlock, 0, s>>>(cand, n_local, cps, nchunks, cnt, offs, send, touched, self);
+    return hipGetLastError();
+}
+hipError_t k_ms_or_local(uint64_t* cand_own, int64_t n_local, int64_t cps, uint8_t* touched_own, uint64_t* nx,
+                         hipStream_t s) {
+    ms_or_local<<<static_cast<unsigned>((cps * 64 + kBlock - 1) / kBlock), kBlock, 0, s>>>(cand_own, n_local, cps,
+                                                                                           touched_own, nx);
     return hipGetLastError();
 }
 hipError_t k_slice_elems(const int64_t* off, int64_t cps, int nranks, int64_t* out, hipStream_t s) {
@@ -614,10 +640,10 @@ hipError_t k_slice_elems(const int64_t* off, int64_t cps, int nranks, int64_t* o
     return hipGetLastError();
 }
 hipError_t k_ms_pack_fixed(uint64_t* cand, int64_t n_local, int64_t cps, int64_t nchunks, const int64_t* offs,
-                           int nranks, int64_t cap, int64_t* send, int* ovf, uint8_t* touched, hipStream_t s) {
+                           int nranks, int64_t cap, int64_t* send, int* ovf, uint8_t* touched, hipStream_t s, int self) {
     const int64_t threads = nchunks * 64;
     ms_pack_fixed<<<static_cast<unsigned>((threads + kBlock - 1) / kBlock), kBlock, 0, s>>>(cand, n_local, cps, nchunks, offs,
-                                                                                           cap, send, ovf, touched);
+                                                                                           cap, send, ovf, touched, self);
     fixed_headers<<<1, 64, 0, s>>>(offs, cps, nranks, cap, send);
     return hipGetLastError();
 }

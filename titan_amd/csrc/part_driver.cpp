@@ -302,6 +302,9 @@ int part_dims(tgo_ctx* ctx, int64_t* n_local, int64_t* lo, int64_t* n_global, in
 int part_fail(tgo_ctx* ctx, int code, const std::string& msg);
 int part_scratch(tgo_ctx* ctx, void** p, int64_t bytes, int slot);
 int64_t* part_dcounts_of(tgo_ctx* ctx);
+// this rank's slice of the candidate words bypasses the pack / exchange (ORed in directly by the
+// settle); (nullptr, -1) turns it off
+void part_ms_bypass(tgo_ctx* ctx, uint64_t* cand_global, int self);
 double ms_split_of(const tgo_ctx* ctx);
 std::shared_ptr<void>& part_state_of(tgo_ctx* ctx);
 int part_in_list(tgo_ctx* ctx, const int32_t** adj, int64_t* nnz);
@@ -473,6 +476,13 @@ extern "C" int tgo_part_msbfs_run(tgo_ctx* ctx, tgo_exchange* x, const int64_t* 
         (rc = scratch(ctx, dc, 3 + 2 * TGO_MAX_SOURCES, 5)) || (rc = scratch(ctx, sizes, 2 * W, 6)))
         return rc;
     int64_t* const caller_dc = part_dcounts_of(ctx);       // restored at the end
+    // the rank's own candidate words never travel: the packs skip its slice and the settles OR
+    // it in (the Python reference driver keeps packing every slice)
+    struct Bypass {
+        tgo_ctx* c;
+        ~Bypass() { part_ms_bypass(c, nullptr, -1); }
+    } bypass{ctx};
+    part_ms_bypass(ctx, cand, x->rank);
     uint64_t* glob[2] = {g0, g1};
     // no clearing per sweep (as the Python driver): the buffers start zero (part_scratch), a
     // level rewrites the active rows of the next mask and the entry-less tail stays zero, the
@@ -537,11 +547,25 @@ extern "C" int tgo_part_msbfs_run(tgo_ctx* ctx, tgo_exchange* x, const int64_t* 
     };
     // pack + exchange the candidate masks of a push (fixed slots when cap bounds them), then
     // hand the received pairs to `fixed_fn` / `pairs_fn`
+    // The own slice never travels (part_ms_bypass): its slot / split is empty, the settle ORs
+    // it in; with one rank nothing is exchanged at all.
     auto exchange = [&](int64_t entries, auto&& fixed_fn, auto&& pairs_fn) -> int {
         const int64_t cap = std::min<int64_t>(entries, nl);
+        if (W == 1) {
+            const int64_t none = 0;
+            return pairs_fn(&none);
+        }
         if (cap > 0 && static_cast<int64_t>(W) * (cap + 1) * 16 <= fixed_bytes) {
             if (int r = tgo_part_ms_pack_fixed(ctx, cand, W, cap, send)) return r;
-            if (int r = x->all_to_all(send, recv, static_cast<size_t>(cap + 1) * 16, st)) return xfail(r);
+            // equal slots known on the host; the own slot is neither sent nor received (its
+            // header in recv zeroed so the settle reads no pairs from it)
+            const size_t slot = static_cast<size_t>(cap + 1) * 16;
+            std::vector<size_t> sb(W, slot), so(W);
+            for (int p = 0; p < W; ++p) so[p] = static_cast<size_t>(p) * slot;
+            sb[x->rank] = 0;
+            if (hipMemsetAsync(reinterpret_cast<char*>(recv) + so[x->rank], 0, 16, st) != hipSuccess)
+                return part_fail(ctx, TGO_E_HIP, "own slot header");
+            if (int r = x->all_to_allv(send, sb.data(), so.data(), recv, sb.data(), so.data(), st)) return xfail(r);
             return fixed_fn(cap);
         }
         // sized pairs: split sizes on the device, one all-to-all of them, one host read
