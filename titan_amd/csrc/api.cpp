@@ -1497,11 +1497,11 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
                                 use_pull ? "pull" : "push", (long long)qlen, (long long)mf, s.hcnt->red[0]);
         static const bool diag = env_double("TGO_MS_DIAG", 0.0) != 0.0;
         if (trace && diag && use_pull) {
-            unsigned long long d[8] = {};
+            unsigned long long d[10] = {};
             HIP_TRY(k_ms_diag_take(d, st));
             std::fprintf(stderr, "[tgo]   pull: %llu entries examined, %llu hot / %llu cold mask gathers, %llu open vertices, "
-                         "%llu stopped early; long lists: %llu, %llu entries examined, %llu stopped early\n",
-                         d[0], d[1], d[2], d[3], d[4], d[6], d[5], d[7]);
+                         "%llu stopped early; long lists: %llu, %llu entries examined (%llu hot / %llu cold gathers), "
+                         "%llu stopped early\n", d[0], d[1], d[2], d[3], d[4], d[6], d[5], d[8], d[9], d[7]);
         }
         std::swap(fr, nx);
         cur ^= 1;

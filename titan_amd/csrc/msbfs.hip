@@ -92,9 +92,11 @@ __device__ __forceinline__ bool maybe_frontier(const uint64_t* __restrict__ fbm,
 // Diagnostic tallies of a pull level (TGO_MS_DIAG=1 with TGO_TRACE=1; off in the product):
 // [0] list entries examined, [1] mask gathers of hot neighbours (u < kDiagHot), [2] of cold
 // ones, [3] open vertices, [4] open vertices whose walk stopped early (every open source covered);
-// long lists (wave-cooperative): [5] entries examined, [6] lists, [7] lists that stopped early
+// long lists (wave-cooperative): [5] entries examined, [6] lists, [7] lists that stopped early,
+// [8] / [9] their hot / cold mask gathers
 constexpr int32_t kDiagHot = 393216;
-__device__ unsigned long long g_ms_diag[8];
+constexpr int kDiagWords = 10;
+__device__ unsigned long long g_ms_diag[kDiagWords];
 // kStep: entries per dependent round trip of a lane's own list; kLong: entries per lane per
 // trip of a wave-cooperative long list (kLong * 64 per trip)
 template <int kStep, bool kDiag = false, int kLong = 4>
@@ -103,7 +105,7 @@ __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t 
         uint64_t* __restrict__ nx, LevelPlanes lvl, Counters* cnt, int32_t next_level, int32_t filter_from,
         uint64_t dense, const uint64_t* __restrict__ cand) {
     unsigned long long nv = 0, mf = 0, bits = 0;
-    unsigned long long dg[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long dg[kDiagWords] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     const int64_t words = (n_active + 63) >> 6;
     // wave w of the block takes word b + w; words past the end run as all-closed lanes.  No
     // block barrier inside: the next frontier is only counted here (ms_queue builds its queue
@@ -174,6 +176,9 @@ __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t 
                     for (int j = 0; j < kLong; ++j)
                         if (f[j]) m |= fr[u[j]];
                     for (int off = 32; off > 0; off >>= 1) m |= __shfl_xor(m, off, 64);
+                    if (kDiag)
+                        for (int j = 0; j < kLong; ++j)
+                            if (u[j] >= 0) ++dg[u[j] < kDiagHot ? 8 : 9];
                     a |= m;
                     done = (a & wsrc) == wsrc;
                     if (kDiag && lane() == src)
@@ -200,7 +205,7 @@ __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t 
         }
     }
     if (kDiag) {
-        for (int i = 0; i < 8; ++i) {
+        for (int i = 0; i < kDiagWords; ++i) {
             unsigned long long x = dg[i];
             for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
             if (lane() == 0 && x) atomicAdd(&g_ms_diag[i], x);
@@ -572,11 +577,11 @@ hipError_t k_ms_pull(const View& pull, const View& push, int64_t n_active, uint6
     return hipGetLastError();
 }
 // The pull diagnostics since the last call (zeroed after the read).
-hipError_t k_ms_diag_take(unsigned long long* out5, hipStream_t s) {  // 8 words
-    hipError_t e = hipMemcpyFromSymbolAsync(out5, HIP_SYMBOL(g_ms_diag), 8 * sizeof(unsigned long long), 0,
+hipError_t k_ms_diag_take(unsigned long long* out, hipStream_t s) {  // kDiagWords (10) words
+    hipError_t e = hipMemcpyFromSymbolAsync(out, HIP_SYMBOL(g_ms_diag), kDiagWords * sizeof(unsigned long long), 0,
                                             hipMemcpyDeviceToHost, s);
     if (e != hipSuccess) return e;
-    static const unsigned long long zero[8] = {};
+    static const unsigned long long zero[kDiagWords] = {};
     e = hipMemcpyToSymbolAsync(HIP_SYMBOL(g_ms_diag), zero, sizeof(zero), 0, hipMemcpyHostToDevice, s);
     if (e != hipSuccess) return e;
     return hipStreamSynchronize(s);
