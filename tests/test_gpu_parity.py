@@ -234,6 +234,29 @@ def test_multi_source_split_budget_is_policy_only(rmat12, split):
         eng.set_tuning(99, 0.0)
 
 
+@pytest.mark.parametrize("scope", [BOTH, IN, OUT])
+@pytest.mark.parametrize("cold,split", [(0, -1.0), (1, -1.0), (300, -1.0), (300, 0.0), (1000, 0.3), (64, 1.0)])
+def test_multi_source_cold_split_level(rmat12, scope, cold, split):
+    """The first pull level split at a hot head (TGO_TUNE_MS_COLD: hot walk + blocked cold pass +
+    finish; values > 1 set the head and segment size so RMAT-12 has cold entries) with the source
+    split on / off / forced: every seed equals the oracle and the plain sweep."""
+    n, src, dst, w, ids, oracle, roots = rmat12
+    eng = Engine().load_edges(n, src, dst, scope).set_tuning(L.TUNE_MS_SPLIT, split)
+    seeds = pick_roots(n, src, dst, 64, seed=23)
+    plain = eng.set_tuning(L.TUNE_MS_COLD, 0).bfs_multi(seeds, n, scope, seed_is_dense=True)
+    d = eng.set_tuning(L.TUNE_MS_COLD, cold).bfs_multi(seeds, n, scope, seed_is_dense=True, stats=True)
+    r, _ = eng.multi_stats(64)
+    assert np.array_equal(d, plain)
+    for i, s in enumerate(seeds):
+        od, _ = oracle.shortest_distance(int(ids[s]), n, scope)
+        assert np.array_equal(d[i], od), (cold, i)
+        assert r[i] == int((od != ABSENT).sum())
+    # the layout is rebuilt for another head and reused; a repeated sweep is identical
+    assert np.array_equal(eng.bfs_multi(seeds, n, scope, seed_is_dense=True), d)
+    with pytest.raises(TitanException):
+        eng.set_tuning(L.TUNE_MS_COLD, 2.5)
+
+
 def test_multi_source_duplicate_and_gotg_seeds():
     eng, rows, vids, sd, npz = engine_from_fixture("gotg", BOTH)
     names = list(npz["names"])

@@ -76,6 +76,8 @@ struct tgo_ctx {
     int ds_bins = -1;           // tgo_set_tuning(TGO_TUNE_DS_BINS): 1 / 0; < 0: TGO_DS_BINS / on
     int64_t ds_pile_cap = 0;    // tgo_set_tuning(TGO_TUNE_DS_PILE_CAP): entries per pile; 0 = n
     int ds_done = -1;           // tgo_set_tuning(TGO_TUNE_DS_DONE): 1 / 0; < 0: TGO_DS_DONE / off
+    int64_t ms_cold = -1;       // tgo_set_tuning(TGO_TUNE_MS_COLD): 0 off, 1 on, > 1 on with that
+                                // hot head (and segment); < 0: TGO_MS_COLD / on
     // state a native partitioned driver keeps between runs on this graph (part_driver.cpp:
     // the PageRank ghost lists); dropped with the graph
     std::shared_ptr<void> part_state;
@@ -1050,6 +1052,11 @@ int tgo_set_tuning(tgo_ctx* ctx, int32_t key, double value) {
         if (value != 0.0 && value != 1.0 && value != -1.0) return fail(ctx, TGO_E_INVALID, "TGO_TUNE_DS_DONE: 0, 1 or -1");
         ctx->ds_done = static_cast<int>(value);
         return TGO_OK;
+    case TGO_TUNE_MS_COLD:
+        if (!(value >= -1.0) || value >= 2147483647.0 || value != static_cast<double>(static_cast<int64_t>(value)))
+            return fail(ctx, TGO_E_INVALID, "TGO_TUNE_MS_COLD: -1, 0, 1 or a hot-head size > 1");
+        ctx->ms_cold = static_cast<int64_t>(value);
+        return TGO_OK;
     case TGO_TUNE_DS_PILE_CAP:
         if (!(value >= 0.0) || value > 9.0e15) return fail(ctx, TGO_E_INVALID, "TGO_TUNE_DS_PILE_CAP: entries >= 0");
         ctx->ds_pile_cap = static_cast<int64_t>(value);
@@ -1356,6 +1363,40 @@ static int ms_alloc(tgo_ctx* ctx) {
     return TGO_OK;
 }
 
+// The cold layout of the scope's pull view for the split first pull level (built once per
+// graph and scope, on first use): neighbours >= hot (TGO_MS_COLD_HOT, 384 K = 3 MB of masks,
+// the hot head every XCD's L2 keeps) in segments of TGO_MS_COLD_SEG (384 K) neighbours.
+static int ms_cold_layout(tgo_ctx* ctx, int32_t scope, const View& pull, int64_t hot_req) {
+    DevGraph& g = ctx->g;
+    Scratch& s = ctx->sc;
+    static const int64_t hot_env = static_cast<int64_t>(env_double("TGO_MS_COLD_HOT", 393216.0));
+    static const int64_t seg_env = static_cast<int64_t>(env_double("TGO_MS_COLD_SEG", 393216.0));
+    const int64_t hot = hot_req > 1 ? hot_req : hot_env, seg = hot_req > 1 ? hot_req : seg_env;
+    if (g.msc_scope == scope && g.msc_req == hot) return TGO_OK;
+    g.msc_scope = scope;
+    g.msc_req = hot;
+    g.msc_C = 0;
+    if (hot <= 0 || hot >= INT32_MAX || seg <= 0) return TGO_OK;
+    Span span("msbfs.cold_layout");
+    DevArray<int32_t> cadj, crow;
+    int64_t C = 0;
+    std::string err;
+    if (int rc = build_ms_cold(pull, g.n, static_cast<int32_t>(hot), seg, cadj, crow, C, ctx->stream, err))
+        return fail(ctx, rc, err);
+    if (C == 0) return TGO_OK;
+    adopt(ctx, g.msc_adj, cadj);
+    adopt(ctx, g.msc_row, crow);
+    if (!s.ms_cacc) {
+        HIP_TRY(dev_alloc(ctx, s.ms_cacc, g.n + 1));
+        HIP_TRY(dev_alloc(ctx, s.ms_need, g.n + 1));
+        HIP_TRY(hipMemsetAsync(s.ms_need, 0, g.n + 1, ctx->stream));
+    }
+    g.msc_C = C;
+    g.msc_hot = static_cast<int32_t>(hot);
+    ctx->st.device_bytes = ctx->dev_bytes;
+    return TGO_OK;
+}
+
 int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_bfs_args* a, int64_t* dist_out) {
     if (!ctx) return TGO_E_INVALID;
     ctx->res_kind = -1;
@@ -1480,9 +1521,30 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
                 }
             }
             if (filter) HIP_TRY(k_ms_fbitmap(fr, n, s.ms_fbm, st));
+            // The first pull level of a run walks long lists to their end (its frontiers are the
+            // most unequal: few walks are covered early), so most of its mask gathers are cold
+            // neighbours missing L2.  Split it: the walk covers the hot head only, a blocked pass
+            // over the cold entries in (segment, row) order ORs the open rows' cold masks from
+            // L2, ms_finish settles those rows.  Same masks, same result (TGO_TUNE_MS_COLD).
+            MsColdSplit cs;
+            static const bool cold_env = env_double("TGO_MS_COLD", 1.0) != 0.0;
+            const bool cold_on = ctx->ms_cold < 0 ? cold_env : ctx->ms_cold != 0;
+            if (cold_on && !prev_pull && !filter) {
+                if ((rc = ms_cold_layout(ctx, a->scope, pull, ctx->ms_cold))) return rc;
+                if (g.msc_C > 0) {
+                    cs.hot_lim = g.msc_hot;
+                    cs.acc = s.ms_cacc;
+                    cs.need = s.ms_need;
+                }
+            }
             HIP_TRY(k_ms_pull(pull, push, g.n_active, full, fr, filter ? s.ms_fbm : nullptr, s.ms_vis, nx,
                               ms_planes(ctx), s.cnt, L + 1, st, filter ? filter_from : 0, full & ~sparse,
-                              sparse ? nx : nullptr));
+                              sparse ? nx : nullptr, cs));
+            if (cs.acc) {
+                HIP_TRY(k_ms_cold(g.msc_adj, g.msc_row, g.msc_C, fr, s.ms_need, s.ms_cacc, st));
+                HIP_TRY(k_ms_finish(push, g.n_active, full, s.ms_vis, nx, sparse ? nx : nullptr, ms_planes(ctx), s.cnt,
+                                    L + 1, s.ms_need, s.ms_cacc, st));
+            }
         } else {
             // candidates only land on rows with entries (< n_active); the tail is never read
             HIP_TRY(hipMemsetAsync(nx, 0, g.n_active * 8, st));

@@ -272,6 +272,14 @@ struct View {
     int nlists;
 };
 
+// A multi-source pull level split at a neighbour id (msbfs.hip): the walk reads neighbours
+// < hot_lim only; rows it leaves open get acc / need for the blocked cold pass (ms_cold).
+struct MsColdSplit {
+    int32_t hot_lim = 0x7FFFFFFF;   // INT32_MAX: no split
+    uint64_t* acc = nullptr;        // n: the open rows' partial masks
+    uint8_t* need = nullptr;        // n: 1 = the row waits for the cold pass (ms_finish resets)
+};
+
 // Row blocks for the CSR-adaptive gather (PageRank / walk counts), built on the host.
 struct RowBlocks {
     int64_t nblocks = 0;        // short-row blocks
@@ -402,6 +410,13 @@ struct DevGraph {
     bool push_ws_ready = false;
     ColdBlocks cold_in;         // cache-blocked in-lists (one-GPU PageRank)
     bool cold_in_ready = false;
+    // split first pull level of the multi-source sweep (built on its first use, per scope)
+    int32_t* msc_adj = nullptr;     // cold entries' neighbours, (segment, row) order
+    int32_t* msc_row = nullptr;     // and rows
+    int64_t msc_C = 0;
+    int32_t msc_hot = 0;
+    int32_t msc_scope = -1;         // scope the layout was built for (-1: none yet)
+    int64_t msc_req = 0;            // and its hot head
 };
 
 // Multi-source BFS levels as bit planes: the level of (v, source r) is
@@ -499,6 +514,8 @@ struct Scratch {
     int32_t* ds_q[2] = {nullptr, nullptr};    // device-driven loop: queues (2n + 2: light + heavy)
     int64_t* ds_qp[2] = {nullptr, nullptr};   // and their entry offsets
     DsLoop* ds_loop = nullptr;
+    uint64_t* ms_cacc = nullptr;    // split pull: partial masks of the rows left to the cold pass
+    uint8_t* ms_need = nullptr;     // and their flags (n, zero between levels)
     int32_t* ds_pile = nullptr;     // binned loop: kDsMaxBins piles of ds_pile_cap vertices
     int64_t ds_pile_cap = 0;
     int32_t* ds_mlist = nullptr;    // n: members of the current bucket
@@ -600,7 +617,22 @@ hipError_t k_ms_diag_take(unsigned long long* out10, hipStream_t s);   // 10 dia
 hipError_t k_ms_pull(const View& pull, const View& push, int64_t n_active, uint64_t full, const uint64_t* fr,
                      const uint64_t* fbm, uint64_t* vis, uint64_t* nx, LevelPlanes lvl, Counters* cnt,
                      int32_t next_level, hipStream_t s, int32_t filter_from, uint64_t dense = ~0ULL,
-                     const uint64_t* cand = nullptr);
+                     const uint64_t* cand = nullptr, MsColdSplit cs = MsColdSplit());
+// the blocked cold pass and the settle of the rows it completed (msbfs.hip)
+hipError_t k_ms_cold(const int32_t* cadj, const int32_t* crow, int64_t C, const uint64_t* fr, const uint8_t* need,
+                     uint64_t* acc, hipStream_t s);
+hipError_t k_ms_finish(const View& push, int64_t n_active, uint64_t full, uint64_t* vis, uint64_t* nx,
+                       const uint64_t* cand, LevelPlanes lvl, Counters* cnt, int32_t next_level, uint8_t* need,
+                       const uint64_t* acc, hipStream_t s);
+hipError_t k_cold_flags(const int32_t* adj, int64_t m, int32_t hot, uint32_t* flag, hipStream_t s);
+hipError_t k_cold_emit(const int64_t* off, int64_t n, const int32_t* adj, int64_t m, const uint32_t* flag,
+                       const uint64_t* pos, int64_t base, int32_t hot, int64_t seg, uint64_t* key, int32_t* val,
+                       hipStream_t s);
+hipError_t k_low_rows(const uint64_t* key, int64_t m, int32_t* row, hipStream_t s);
+// pr_layout.hip: the cold layout of a split pull (entries >= hot of both lists of v, sorted by
+// (segment, row)); C = 0 when nothing is cold
+int build_ms_cold(const View& v, int64_t n, int32_t hot, int64_t seg, DevArray<int32_t>& cadj, DevArray<int32_t>& crow,
+                  int64_t& C, hipStream_t s, std::string& err);
 // per-source frontier sizes of fr (out64[s], zeroed first) — the pull level's split
 hipError_t k_ms_source_counts(const uint64_t* fr, int64_t n_active, unsigned long long* out64, hipStream_t s);
 // exact push entries of the frontiers of the sources in `cand` (out64[s], zeroed first)

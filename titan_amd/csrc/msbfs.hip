@@ -99,11 +99,16 @@ constexpr int kDiagWords = 10;
 __device__ unsigned long long g_ms_diag[kDiagWords];
 // kStep: entries per dependent round trip of a lane's own list; kLong: entries per lane per
 // trip of a wave-cooperative long list (kLong * 64 per trip)
+// cs (MsColdSplit, hot_lim < INT32_MAX): the walk reads only neighbours < hot_lim (lists are
+// sorted, so it stops at the first cold one); a row it does not cover whose lists go on past
+// hot_lim is left to the blocked cold pass: its partial mask to cs.acc, cs.need set, nothing
+// written (ms_cold ORs its cold neighbours in, ms_finish settles it).
 template <int kStep, bool kDiag = false, int kLong = 4>
 __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t n_active, uint64_t full,
         const uint64_t* __restrict__ fr, const uint64_t* __restrict__ fbm, uint64_t* __restrict__ vis,
         uint64_t* __restrict__ nx, LevelPlanes lvl, Counters* cnt, int32_t next_level, int32_t filter_from,
-        uint64_t dense, const uint64_t* __restrict__ cand) {
+        uint64_t dense, const uint64_t* __restrict__ cand, MsColdSplit cs) {
+    const int32_t hot_lim = cs.hot_lim;
     unsigned long long nv = 0, mf = 0, bits = 0;
     unsigned long long dg[kDiagWords] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     const int64_t words = (n_active + 63) >> 6;
@@ -125,16 +130,21 @@ __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t 
         }
         const int64_t deg = (e0 - b0) + (e1 - b1);
         uint64_t acc = 0;
+        bool cut = false;                                     // a list went on past hot_lim
         if (want && deg <= kCoop) {
             for (int l = 0; l < 2 && (acc & want) != want; ++l) {
                 const int32_t* adj = l == 0 ? pull.adj0 : pull.adj1;
                 const int64_t e = l == 0 ? e0 : e1;
+                bool cutl = false;
                 // kStep entries per dependent round trip: their index loads issue together,
                 // then their mask gathers (lists rarely cover every open source early)
-                for (int64_t k = l == 0 ? b0 : b1; k < e && (acc & want) != want; k += kStep) {
+                for (int64_t k = l == 0 ? b0 : b1; k < e && (acc & want) != want && !cutl; k += kStep) {
                     int32_t u[kStep];
 #pragma unroll
-                    for (int j = 0; j < kStep; ++j) u[j] = k + j < e ? __builtin_nontemporal_load(adj + k + j) : -1;
+                    for (int j = 0; j < kStep; ++j) {
+                        u[j] = k + j < e ? __builtin_nontemporal_load(adj + k + j) : -1;
+                        if (u[j] >= hot_lim) { u[j] = -1; cutl = true; }
+                    }
                     bool f[kStep];
 #pragma unroll
                     for (int j = 0; j < kStep; ++j) f[j] = u[j] >= 0 && maybe_frontier(fbm, u[j], filter_from);
@@ -147,6 +157,7 @@ __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t 
                         for (int j = 0; j < kStep; ++j)
                             if (u[j] >= 0) { ++dg[0]; ++dg[u[j] < kDiagHot ? 1 : 2]; }
                 }
+                cut |= cutl;
             }
             if (kDiag) { ++dg[3]; if ((acc & want) == want) ++dg[4]; }
         }
@@ -156,6 +167,7 @@ __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t 
             big &= big - 1;
             const uint64_t wsrc = __shfl(want, src, 64);
             uint64_t a = 0;
+            bool wcut = false;                                // wave-uniform
             for (int l = 0; l < 2; ++l) {
                 const int64_t bb = __shfl(l == 0 ? b0 : b1, src, 64);
                 const int64_t ee = __shfl(l == 0 ? e0 : e1, src, 64);
@@ -163,11 +175,14 @@ __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t 
                 bool done = false;
                 for (int64_t k = bb; k < ee && !done; k += kLong * 64) {
                     int32_t u[kLong];
+                    bool hc = false;
 #pragma unroll
                     for (int j = 0; j < kLong; ++j) {
                         const int64_t x = k + j * 64 + lane();
                         u[j] = x < ee ? __builtin_nontemporal_load(adj + x) : -1;
+                        if (u[j] >= hot_lim) { u[j] = -1; hc = true; }
                     }
+                    if (__ballot(hc)) { done = true; wcut = true; }   // the rest of the list is cold
                     bool f[kLong];
 #pragma unroll
                     for (int j = 0; j < kLong; ++j) f[j] = u[j] >= 0 && maybe_frontier(fbm, u[j], filter_from);
@@ -180,7 +195,7 @@ __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t 
                         for (int j = 0; j < kLong; ++j)
                             if (u[j] >= 0) ++dg[u[j] < kDiagHot ? 8 : 9];
                     a |= m;
-                    done = (a & wsrc) == wsrc;
+                    done = done || (a & wsrc) == wsrc;
                     if (kDiag && lane() == src)
                         for (int j = 0; j < kLong; ++j) dg[5] += k + j * 64 < ee ? min<int64_t>(64, ee - k - j * 64) : 0;
                 }
@@ -188,8 +203,14 @@ __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t 
             }
             if (lane() == src) {
                 acc = a;
+                cut = wcut;
                 if (kDiag) { ++dg[6]; if ((a & wsrc) == wsrc) ++dg[7]; }
             }
+        }
+        if (cut && (acc & want) != want && v < n_active) {   // left to the cold pass
+            cs.acc[v] = acc;
+            cs.need[v] = 1;
+            continue;
         }
         if (cand && open && v < n_active) acc |= cand[v];
         const uint64_t fresh = acc & open;
@@ -212,6 +233,87 @@ __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t 
         }
     }
     count_flush(cnt, nv, mf, bits);
+}
+
+// Blocked cold pass of a split pull level: the cold entries (neighbour >= hot_lim) of every row,
+// sorted by (segment of the neighbour, row), the XCD-major way: XCD x walks the x-th eighth of
+// the entries in order with its blocks as one grid-stride window, so the segment of masks it
+// reads (3 MB) stays in its L2.  A row the hot walk left open ORs its cold neighbours' masks:
+// a wave reduces each run of one row (the entries are row-contiguous inside a segment) and the
+// run's first lane ORs the result into cs.acc.
+__global__ void __launch_bounds__(kBlock) ms_cold(const int32_t* __restrict__ cadj, const int32_t* __restrict__ crow,
+        int64_t C, const uint64_t* __restrict__ fr, const uint8_t* __restrict__ need, uint64_t* __restrict__ acc) {
+    const int x = static_cast<int>(blockIdx.x & 7u);
+    const int64_t per = gridDim.x >> 3;                      // blocks per XCD (grid is a multiple of 8)
+    const int64_t lo = C * x / 8, hi = C * (x + 1) / 8;
+    const int64_t span = (hi - lo + 63) & ~int64_t(63);
+    for (int64_t e0 = lo + static_cast<int64_t>(blockIdx.x >> 3) * kBlock; e0 < lo + span; e0 += per * kBlock) {
+        const int64_t e = e0 + threadIdx.x;                   // wave-uniform trips (kBlock = 4 waves)
+        int32_t v = -1;
+        uint64_t m = 0;
+        if (e < hi) {
+            v = crow[e];
+            if (need[v]) m = fr[cadj[e]];
+        }
+        // OR of the run of v from this lane on (rows are contiguous, so lane + o shares v only
+        // if every lane between does)
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint64_t y = __shfl_down(m, o, 64);
+            const int32_t w = __shfl_down(v, o, 64);
+            if (lane() + o < 64 && w == v) m |= y;
+        }
+        const int32_t prev = __shfl_up(v, 1, 64);
+        if (v >= 0 && m && (lane() == 0 || prev != v)) atomicOr(reinterpret_cast<unsigned long long*>(&acc[v]), m);
+    }
+}
+
+// The rows the cold pass completed: their mask (hot walk | cold pass | the split's push
+// candidates) settled like the pull's own rows, counted into the same counters.
+__global__ void __launch_bounds__(kBlock) ms_finish(View push, int64_t n_active, uint64_t full,
+        uint64_t* __restrict__ vis, uint64_t* __restrict__ nx, const uint64_t* __restrict__ cand, LevelPlanes lvl,
+        Counters* cnt, int32_t next_level, uint8_t* __restrict__ need, const uint64_t* __restrict__ acc) {
+    unsigned long long nv = 0, mf = 0, bits = 0;
+    for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n_active; v += (int64_t)gridDim.x * blockDim.x) {
+        if (!need[v]) continue;
+        need[v] = 0;
+        const uint64_t seen = vis[v];
+        uint64_t a = acc[v];
+        if (cand) a |= cand[v];
+        const uint64_t fresh = a & full & ~seen;
+        nx[v] = fresh;
+        if (fresh) {
+            vis[v] = seen | fresh;
+            record_level(v, fresh, next_level, lvl);
+            ++nv;
+            mf += static_cast<unsigned long long>(push_degree(push, v));
+            bits += static_cast<unsigned long long>(__popcll(fresh));
+        }
+    }
+    count_flush(cnt, nv, mf, bits);
+}
+
+// Cold layout build: flags / positions of the entries >= hot of one list, then the (segment,
+// row) keys and neighbour payloads at their compacted positions.
+__global__ void cold_flags(const int32_t* __restrict__ adj, int64_t m, int32_t hot, uint32_t* __restrict__ flag) {
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x)
+        flag[k] = adj[k] >= hot ? 1u : 0u;
+}
+__global__ void cold_emit(const int64_t* __restrict__ off, int64_t n, const int32_t* __restrict__ adj, int64_t m,
+                          const uint32_t* __restrict__ flag, const uint64_t* __restrict__ pos, int64_t base, int32_t hot,
+                          int64_t seg, uint64_t* __restrict__ key, int32_t* __restrict__ val) {
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x) {
+        if (!flag[k]) continue;
+        int64_t a = 0, b = n;                                 // row: last r with off[r] <= k
+        while (b - a > 1) { const int64_t c = (a + b) >> 1; if (off[c] <= k) a = c; else b = c; }
+        const int64_t p = base + static_cast<int64_t>(pos[k]);
+        const uint64_t sg = static_cast<uint64_t>((adj[k] - hot) / seg);
+        key[p] = (sg << 32) | static_cast<uint64_t>(a);
+        val[p] = adj[k];
+    }
+}
+__global__ void low_rows(const uint64_t* __restrict__ key, int64_t m, int32_t* __restrict__ row) {
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x)
+        row[k] = static_cast<int32_t>(static_cast<uint32_t>(key[k]));
 }
 
 // Per-source frontier sizes of a pull level (vertices whose mask holds the source's bit):
@@ -553,7 +655,8 @@ hipError_t k_ms_seed(const int64_t* seeds, int nseeds, uint64_t* vis, uint64_t* 
 }
 hipError_t k_ms_pull(const View& pull, const View& push, int64_t n_active, uint64_t full, const uint64_t* fr,
                      const uint64_t* fbm, uint64_t* vis, uint64_t* nx, LevelPlanes lvl, Counters* cnt,
-                     int32_t next_level, hipStream_t s, int32_t filter_from, uint64_t dense, const uint64_t* cand) {
+                     int32_t next_level, hipStream_t s, int32_t filter_from, uint64_t dense, const uint64_t* cand,
+                     MsColdSplit cs) {
     // TGO_MS_STEP: entries a lane loads per round trip of its own list (8 default; 16 probe)
     static const int step = [] { const char* e = std::getenv("TGO_MS_STEP"); return e ? std::atoi(e) : 8; }();
     static const bool diag = [] { const char* e = std::getenv("TGO_MS_DIAG"); return e && std::atoi(e) != 0; }();
@@ -561,19 +664,45 @@ hipError_t k_ms_pull(const View& pull, const View& push, int64_t n_active, uint6
     static const int lng = [] { const char* e = std::getenv("TGO_MS_LONG"); return e ? std::atoi(e) : 4; }();
     if (!diag && step == 8 && lng == 8)
         ms_pull<8, false, 8><<<grid_for(n_active, 8192), kBlock, 0, s>>>(pull, push, n_active, full, fr, fbm, vis, nx, lvl,
-                                                                         cnt, next_level, filter_from, dense, cand);
+                                                                         cnt, next_level, filter_from, dense, cand, cs);
     else if (diag)
         ms_pull<8, true><<<grid_for(n_active, 8192), kBlock, 0, s>>>(pull, push, n_active, full, fr, fbm, vis, nx, lvl, cnt,
-                                                                   next_level, filter_from, dense, cand);
+                                                                   next_level, filter_from, dense, cand, cs);
     else if (step == 16)
         ms_pull<16><<<grid_for(n_active, 8192), kBlock, 0, s>>>(pull, push, n_active, full, fr, fbm, vis, nx, lvl, cnt,
-                                                               next_level, filter_from, dense, cand);
+                                                               next_level, filter_from, dense, cand, cs);
     else if (step == 4)
         ms_pull<4><<<grid_for(n_active, 8192), kBlock, 0, s>>>(pull, push, n_active, full, fr, fbm, vis, nx, lvl, cnt,
-                                                              next_level, filter_from, dense, cand);
+                                                              next_level, filter_from, dense, cand, cs);
     else
         ms_pull<8><<<grid_for(n_active, 8192), kBlock, 0, s>>>(pull, push, n_active, full, fr, fbm, vis, nx, lvl, cnt,
-                                                              next_level, filter_from, dense, cand);
+                                                              next_level, filter_from, dense, cand, cs);
+    return hipGetLastError();
+}
+hipError_t k_ms_cold(const int32_t* cadj, const int32_t* crow, int64_t C, const uint64_t* fr, const uint8_t* need,
+                     uint64_t* acc, hipStream_t s) {
+    if (C > 0) ms_cold<<<8 * 1024, kBlock, 0, s>>>(cadj, crow, C, fr, need, acc);
+    return hipGetLastError();
+}
+hipError_t k_ms_finish(const View& push, int64_t n_active, uint64_t full, uint64_t* vis, uint64_t* nx,
+                       const uint64_t* cand, LevelPlanes lvl, Counters* cnt, int32_t next_level, uint8_t* need,
+                       const uint64_t* acc, hipStream_t s) {
+    ms_finish<<<grid_for(n_active, 4096), kBlock, 0, s>>>(push, n_active, full, vis, nx, cand, lvl, cnt, next_level, need,
+                                                         acc);
+    return hipGetLastError();
+}
+hipError_t k_cold_flags(const int32_t* adj, int64_t m, int32_t hot, uint32_t* flag, hipStream_t s) {
+    if (m > 0) cold_flags<<<grid_for(m, 65536), kBlock, 0, s>>>(adj, m, hot, flag);
+    return hipGetLastError();
+}
+hipError_t k_cold_emit(const int64_t* off, int64_t n, const int32_t* adj, int64_t m, const uint32_t* flag,
+                       const uint64_t* pos, int64_t base, int32_t hot, int64_t seg, uint64_t* key, int32_t* val,
+                       hipStream_t s) {
+    if (m > 0) cold_emit<<<grid_for(m, 65536), kBlock, 0, s>>>(off, n, adj, m, flag, pos, base, hot, seg, key, val);
+    return hipGetLastError();
+}
+hipError_t k_low_rows(const uint64_t* key, int64_t m, int32_t* row, hipStream_t s) {
+    if (m > 0) low_rows<<<grid_for(m, 65536), kBlock, 0, s>>>(key, m, row);
     return hipGetLastError();
 }
 // The pull diagnostics since the last call (zeroed after the read).

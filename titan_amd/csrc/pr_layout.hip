@@ -447,6 +447,51 @@ __global__ void low_words(const uint64_t* __restrict__ key, int64_t m, int32_t* 
 }
 }  // namespace
 
+// The cold layout of a split multi-source pull (msbfs.hip ms_cold): every pull-list entry whose
+// neighbour is >= hot, from both lists of the view, sorted by (segment of the neighbour, row) —
+// crow / cadj per entry.  C = 0 when nothing is cold.
+int build_ms_cold(const View& v, int64_t n, int32_t hot, int64_t seg, DevArray<int32_t>& cadj, DevArray<int32_t>& crow,
+                  int64_t& C, hipStream_t s, std::string& err) {
+    C = 0;
+    if (n <= hot || seg <= 0) return TGO_OK;
+    const int64_t* off[2] = {v.off0, v.off1};
+    const int32_t* adj[2] = {v.adj0, v.adj1};
+    int64_t m[2] = {0, 0}, cnt[2] = {0, 0};
+    Sort so{{}, 0, s};
+    Buf<uint32_t> flag[2];
+    Buf<uint64_t> pos[2];
+    for (int l = 0; l < v.nlists; ++l) {
+        PL_TRY(hipMemcpyAsync(&m[l], off[l] + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        PL_TRY(hipStreamSynchronize(s));
+        PL_TRY(flag[l].alloc(m[l] + 1));
+        PL_TRY(pos[l].alloc(m[l] + 1));
+        PL_TRY(k_cold_flags(adj[l], m[l], hot, flag[l].p, s));
+        PL_TRY(hipMemsetAsync(flag[l].p + m[l], 0, sizeof(uint32_t), s));
+        PL_TRY(so.excl(flag[l].p, pos[l].p, m[l] + 1));
+        PL_TRY(hipMemcpyAsync(&cnt[l], pos[l].p + m[l], sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        PL_TRY(hipStreamSynchronize(s));
+    }
+    const int64_t total = cnt[0] + cnt[1];
+    if (total == 0) return TGO_OK;
+    Buf<uint64_t> k0, k1;
+    Buf<int32_t> v0, v1, rows;
+    PL_TRY(k0.alloc(total));
+    PL_TRY(k1.alloc(total));
+    PL_TRY(v0.alloc(total));
+    PL_TRY(v1.alloc(total));
+    for (int l = 0; l < v.nlists; ++l)
+        PL_TRY(k_cold_emit(off[l], n, adj[l], m[l], flag[l].p, pos[l].p, l == 0 ? 0 : cnt[0], hot, seg, k0.p, v0.p, s));
+    const int64_t nseg = (n - hot + seg - 1) / seg;
+    PL_TRY(so.pairs(k0.p, k1.p, v0.p, v1.p, total, 32 + bits_for(nseg)));
+    PL_TRY(rows.alloc(total));
+    PL_TRY(k_low_rows(k1.p, total, rows.p, s));
+    PL_TRY(hipStreamSynchronize(s));
+    cadj.own(v1.take(), total);
+    crow.own(rows.take(), total);
+    C = total;
+    return TGO_OK;
+}
+
 // Sort every row's (non-negative) values ascending in place: one radix sort of (row, value)
 // keys.  The partitioned PageRank maps its sources into the blocked gathered vector, which is
 // not monotone in the global id, so the rows are re-sorted before the device cold build.
