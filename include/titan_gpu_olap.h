@@ -331,10 +331,10 @@ int  tgo_copy_multi_distances(tgo_ctx* ctx, int32_t source, int64_t* dist_out);
  * 0 = by a scan of the whole pending bitmap.  TGO_TUNE_DS_PILE_CAP: entries a pile holds per
  * bucket before that bucket falls back to the scan (0 = the vertex count; tests use small caps). */
 /* TGO_TUNE_DS_DONE: 1 = the binned loop's relax skips the distance read of targets whose bucket
- * finished (0, default: reads every target).  TGO_TUNE_MS_COLD (tgo_bfs_multi): 1 (default, or
- * TGO_MS_COLD) = the first pull level of a run walks only the hot neighbours and a blocked pass
- * over the cold entries completes the open rows; 0 = the plain walk; a value > 1 = on, with that
- * many hot neighbours and cold segments of that size (tests). */
+ * finished (0, default: reads every target).  TGO_TUNE_MS_COLD (tgo_bfs_multi): 1 = the first
+ * pull level of a run walks only the hot neighbours and a blocked pass over the cold entries
+ * completes the open rows; 0 (default, or TGO_MS_COLD) = the plain walk; a value > 1 = on, with
+ * that many hot neighbours and cold segments of that size (tests). */
 enum { TGO_TUNE_MS_SPLIT = 1, TGO_TUNE_MS_GHOST = 2, TGO_TUNE_DS_BINS = 3, TGO_TUNE_DS_PILE_CAP = 4,
        TGO_TUNE_DS_DONE = 5, TGO_TUNE_MS_COLD = 6 };
 int  tgo_set_tuning(tgo_ctx* ctx, int32_t key, double value);

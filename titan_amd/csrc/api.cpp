@@ -1522,12 +1522,15 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
             }
             if (filter) HIP_TRY(k_ms_fbitmap(fr, n, s.ms_fbm, st));
             // The first pull level of a run walks long lists to their end (its frontiers are the
-            // most unequal: few walks are covered early), so most of its mask gathers are cold
-            // neighbours missing L2.  Split it: the walk covers the hot head only, a blocked pass
-            // over the cold entries in (segment, row) order ORs the open rows' cold masks from
-            // L2, ms_finish settles those rows.  Same masks, same result (TGO_TUNE_MS_COLD).
+            // most unequal: few walks are covered early).  Opt-in split (TGO_TUNE_MS_COLD /
+            // TGO_MS_COLD=1): the walk covers the hot head only, a blocked pass over the cold
+            // entries in (segment, row) order ORs the open rows' cold masks from L2, ms_finish
+            // settles those rows — same masks, same result.  Measured slower at RMAT-24 (level 2
+            // 2.01 -> 2.69 ms, sweep 4.54 -> 5.22 ms, gpurun_out/r04m): of the level's 227 M
+            // gathers only 44 M are cold (profiles/r04l_ms_diag.log), and the pass streams every
+            // cold entry of every row to reach them.
             MsColdSplit cs;
-            static const bool cold_env = env_double("TGO_MS_COLD", 1.0) != 0.0;
+            static const bool cold_env = env_double("TGO_MS_COLD", 0.0) != 0.0;
             const bool cold_on = ctx->ms_cold < 0 ? cold_env : ctx->ms_cold != 0;
             if (cold_on && !prev_pull && !filter) {
                 if ((rc = ms_cold_layout(ctx, a->scope, pull, ctx->ms_cold))) return rc;
