@@ -589,10 +589,18 @@ int check_program(tgo_ctx* ctx, int scope) {
 // kernel stores them and then a sequence number into host-mapped memory; the host spins on
 // the sequence number (the level loops read a few words per level, so the wake-up latency of
 // a blocking synchronisation dominated short levels).  A stream error ends the spin.
+int wait_publish(tgo_ctx* ctx, unsigned long long seq);
+
 int read_counters(tgo_ctx* ctx) {
     Scratch& s = ctx->sc;
     const unsigned long long seq = ++s.pub_seq;
     HIP_TRY(k_publish_counters(s.cnt, s.hcnt_dev, seq, ctx->stream));
+    return wait_publish(ctx, seq);
+}
+
+// Spin on the publish sequence number (a periodic stream query ends the spin on a failure).
+int wait_publish(tgo_ctx* ctx, unsigned long long seq) {
+    Scratch& s = ctx->sc;
     const volatile unsigned long long* flag = reinterpret_cast<volatile unsigned long long*>(s.hcnt) + kCounterWords;
     for (uint64_t it = 1;; ++it) {
         if (*flag == seq) break;
@@ -2974,6 +2982,18 @@ namespace tgo {
 hipStream_t part_stream(tgo_ctx* ctx) { return ctx->stream; }
 int part_fail(tgo_ctx* ctx, int code, const std::string& msg) { return fail(ctx, code, msg); }
 int64_t* part_dcounts_of(tgo_ctx* ctx) { return ctx->part_dcounts; }
+// `count` device words (on the ctx stream, after the work queued so far) to out, through the
+// host-mapped counter page: one tiny kernel and a spin instead of a copy and a stream wait.
+int part_read_words(tgo_ctx* ctx, const int64_t* dev, int count, int64_t* out) {
+    Scratch& s = ctx->sc;
+    if (!s.hcnt || count < 0 || count > kCounterWords) return fail(ctx, TGO_E_STATE, "part_read_words");
+    const unsigned long long seq = ++s.pub_seq;
+    HIP_TRY(k_publish_words(dev, count, s.hcnt_dev, seq, ctx->stream));
+    if (int rc = wait_publish(ctx, seq)) return rc;
+    const volatile unsigned long long* w = reinterpret_cast<volatile unsigned long long*>(s.hcnt);
+    for (int i = 0; i < count; ++i) out[i] = static_cast<int64_t>(w[i]);
+    return TGO_OK;
+}
 void part_ms_bypass(tgo_ctx* ctx, uint64_t* cand_global, int self) {
     ctx->part_ms_cand = cand_global;
     ctx->part_ms_self = cand_global ? self : -1;

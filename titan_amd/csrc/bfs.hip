@@ -349,6 +349,16 @@ __global__ void publish_counters(const Counters* c, unsigned long long* host, un
     __syncthreads();
     if (i == 0) __hip_atomic_store(&host[kCounterWords], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// publish_counters for `count` arbitrary device words (the partitioned drivers' counts).
+__global__ void publish_words(const unsigned long long* src, int count, unsigned long long* host, unsigned long long seq) {
+    const int i = threadIdx.x;
+    if (i < count) {
+        __hip_atomic_store(&host[i], src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __threadfence_system();
+    }
+    __syncthreads();
+    if (i == 0) __hip_atomic_store(&host[kCounterWords], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 // Grid-stride: the launch grid is capped (grid_for: 2048 blocks = 524 288 threads), and RMAT-27
 // has 2.1 M bitmap words — a one-thread-per-word form left the tail of nb uncleared there.
 __global__ void level_prep(Counters* cnt, uint64_t* nb, int64_t words, int64_t* tail) {
@@ -359,6 +369,11 @@ __global__ void level_prep(Counters* cnt, uint64_t* nb, int64_t words, int64_t* 
 }
 hipError_t k_publish_counters(const Counters* c, unsigned long long* host, unsigned long long seq, hipStream_t s) {
     publish_counters<<<1, 64, 0, s>>>(c, host, seq);
+    return hipGetLastError();
+}
+hipError_t k_publish_words(const int64_t* src, int count, unsigned long long* host, unsigned long long seq, hipStream_t s) {
+    if (count < 0 || count > kCounterWords) return hipErrorInvalidValue;
+    publish_words<<<1, 64, 0, s>>>(reinterpret_cast<const unsigned long long*>(src), count, host, seq);
     return hipGetLastError();
 }
 hipError_t k_level_prep(Counters* cnt, uint64_t* nb, int64_t words, int64_t* tail, hipStream_t s) {

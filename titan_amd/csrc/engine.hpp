@@ -552,6 +552,8 @@ hipError_t k_publish_counts(const Counters* c, int64_t* out, int64_t* slot, hipS
 // host-mapped mirror, then the sequence number after them (system scope); the host spins on it.
 constexpr int kCounterWords = static_cast<int>(sizeof(Counters) / 8);
 hipError_t k_publish_counters(const Counters* c, unsigned long long* host, unsigned long long seq, hipStream_t s);
+// `count` (<= kCounterWords) device words published like the counters (partitioned drivers)
+hipError_t k_publish_words(const int64_t* src, int count, unsigned long long* host, unsigned long long seq, hipStream_t s);
 // One launch instead of per-level memsets: zero the counters (cnt may be null), the next
 // frontier bitmap (words, may be 0) and the scan tail slot (may be null).
 hipError_t k_level_prep(Counters* cnt, uint64_t* nb, int64_t words, int64_t* tail, hipStream_t s);

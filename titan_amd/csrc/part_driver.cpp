@@ -305,6 +305,8 @@ int64_t* part_dcounts_of(tgo_ctx* ctx);
 // this rank's slice of the candidate words bypasses the pack / exchange (ORed in directly by the
 // settle); (nullptr, -1) turns it off
 void part_ms_bypass(tgo_ctx* ctx, uint64_t* cand_global, int self);
+// device words to the host through the mapped counter page (no stream synchronisation)
+int part_read_words(tgo_ctx* ctx, const int64_t* dev, int count, int64_t* out);
 double ms_split_of(const tgo_ctx* ctx);
 std::shared_ptr<void>& part_state_of(tgo_ctx* ctx);
 int part_in_list(tgo_ctx* ctx, const int32_t** adj, int64_t* nnz);
@@ -339,11 +341,7 @@ struct Driver {
         for (int i = 0; i < k; ++i) hc[i] = vals[i];
         if (hipMemcpyAsync(dbuf, hc, k * sizeof(int64_t), hipMemcpyHostToDevice, st) != hipSuccess) return hip("reduce upload");
         if (int r = x->all_reduce(dbuf, static_cast<size_t>(k), op, st)) return xfail(r);
-        if (hipMemcpyAsync(hc, dbuf, k * sizeof(int64_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
-            hipStreamSynchronize(st) != hipSuccess)
-            return hip("reduce read");
-        for (int i = 0; i < k; ++i) out[i] = hc[i];
-        return TGO_OK;
+        return part_read_words(ctx, dbuf, k, out);
     }
 };
 
@@ -649,8 +647,7 @@ extern "C" int tgo_part_msbfs_run(tgo_ctx* ctx, tgo_exchange* x, const int64_t* 
         std::swap(glob[0], glob[1]);
         // global {next frontier, its entries}; this rank's queue length back to the engine
         if (int r = x->all_reduce_sum(dc, 2, st)) { rc = xfail(r); break; }
-        if (hipMemcpyAsync(hc, dc, 3 * sizeof(int64_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
-            hipStreamSynchronize(st) != hipSuccess) { rc = part_fail(ctx, TGO_E_HIP, "counts read"); break; }
+        if ((rc = part_read_words(ctx, dc, 3, hc))) break;
         nf = hc[0];
         mf = hc[1];
         if ((rc = tgo_part_set_local_qlen(ctx, hc[2]))) break;
@@ -746,8 +743,7 @@ extern "C" int tgo_part_bfs_run(tgo_ctx* ctx, tgo_exchange* x, int64_t seed_glob
         if (int r = x->all_gather(glob[1], static_cast<size_t>(nwl) * 8, st)) { rc = d.xfail(r); break; }
         std::swap(glob[0], glob[1]);
         if (int r = x->all_reduce_sum(dc, 2, st)) { rc = d.xfail(r); break; }
-        if (hipMemcpyAsync(d.hc, dc, 3 * sizeof(int64_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
-            hipStreamSynchronize(st) != hipSuccess) { rc = d.hip("counts read"); break; }
+        if ((rc = part_read_words(ctx, dc, 3, d.hc))) break;
         nf = d.hc[0];
         mf = d.hc[1];
         mu -= mf;
@@ -802,8 +798,10 @@ extern "C" int tgo_part_sssp_run(tgo_ctx* ctx, tgo_exchange* x, int64_t seed_glo
             break;
         }
         if (int r = x->all_to_all(sizes, sizes + 2 * W, 16, st)) { rc = d.xfail(r); break; }
-        if (hipMemcpyAsync(both.data(), sizes, 4 * W * sizeof(int64_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
-            hipStreamSynchronize(st) != hipSuccess) { rc = d.hip("sizes read"); break; }
+        if (4 * W <= 32) {                 // through the mapped counter page (up to 8 ranks)
+            if ((rc = part_read_words(ctx, sizes, 4 * W, both.data()))) break;
+        } else if (hipMemcpyAsync(both.data(), sizes, 4 * W * sizeof(int64_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                   hipStreamSynchronize(st) != hipSuccess) { rc = d.hip("sizes read"); break; }
         int64_t gq = 0;
         for (int p = 0; p < W; ++p) gq += both[2 * W + 2 * p + 1];
         if (gq == 0) {          // every near queue was empty (nothing was relaxed): the next non-empty bucket
