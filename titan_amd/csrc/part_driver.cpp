@@ -194,6 +194,7 @@ struct LocalExchange : tgo_exchange {
         return rc;
     }
     int all_gather(void* buf, size_t bytes, hipStream_t s) override {
+        if (world == 1) return TGO_OK;                      // one rank: nothing to exchange (as RCCL)
         return collective(s, {buf, buf, nullptr, nullptr, {}}, [&]() -> int {
             for (int p = 0; p < world; ++p)
                 if (p != rank) {
@@ -204,6 +205,7 @@ struct LocalExchange : tgo_exchange {
         });
     }
     int all_to_all(const void* send, void* recv, size_t bytes, hipStream_t s) override {
+        if (world == 1) return copy(recv, send, bytes, s);
         return collective(s, {send, recv, nullptr, nullptr, {}}, [&]() -> int {
             for (int p = 0; p < world; ++p) {
                 const char* src = static_cast<const char*>(g->slot[p].send) + rank * bytes;
@@ -214,6 +216,10 @@ struct LocalExchange : tgo_exchange {
     }
     int all_to_allv(const void* send, const size_t* sb, const size_t* so, void* recv, const size_t* rb,
                     const size_t* ro, hipStream_t s) override {
+        if (world == 1) {
+            if (sb[0] != rb[0]) return fail_msg("local exchange: all_to_allv sizes do not match");
+            return copy(static_cast<char*>(recv) + ro[0], static_cast<const char*>(send) + so[0], rb[0], s);
+        }
         return collective(s, {send, recv, sb, so, {}}, [&]() -> int {
             for (int p = 0; p < world; ++p) {
                 const LocalGroup::Slot& q = g->slot[p];
@@ -225,6 +231,7 @@ struct LocalExchange : tgo_exchange {
         });
     }
     int all_reduce(int64_t* buf, size_t count, int op, hipStream_t s) override {
+        if (world == 1) return TGO_OK;
         std::vector<int64_t> mine(count);
         int rc = sync(s);
         if (!rc) {
