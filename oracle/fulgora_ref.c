@@ -371,7 +371,16 @@ static int read_object_x(const uint8_t* d, size_t len, size_t* pos, int dt, int 
         *ival = (int32_t)u;                              /* the IEEE bits */
         break;
     }
-    case FR_DT_DOUBLE: for (int i = 0; i < 8; i++) RD(); break;
+    case FR_DT_DOUBLE: {                                 /* DoubleSerializer.read / readByteOrder :25-41 */
+        for (int i = 0; i < 8; i++) u = (u << 8) | RD();
+        if (byte_order) {                                /* LongSerializer.readByteOrder + sortableLongToDouble */
+            int64_t sl = (int64_t)(u ^ 0x8000000000000000ULL);
+            sl ^= (sl >> 63) & 0x7fffffffffffffffLL;
+            u = (uint64_t)sl;
+        }
+        *ival = (int64_t)u;                              /* the IEEE bits */
+        break;
+    }
     case FR_DT_BOOLEAN: *ival = RD(); break;
     default: return FR_E_UNSUPPORTED;
     }
@@ -502,7 +511,7 @@ int fr_encode_edge(fr_buf* out, int32_t* value_pos, const fr_schema* schema, int
 
 int fr_weight_datatype_ok(int dt) {
     return dt == FR_DT_INTEGER || dt == FR_DT_BYTE || dt == FR_DT_SHORT || dt == FR_DT_CHARACTER ||
-           dt == FR_DT_BOOLEAN || dt == FR_DT_FLOAT;
+           dt == FR_DT_BOOLEAN || dt == FR_DT_FLOAT || dt == FR_DT_LONG || dt == FR_DT_DOUBLE;
 }
 
 int fr_decode_edge(const uint8_t* d, size_t len, size_t value_pos, const fr_schema* schema,
@@ -576,7 +585,7 @@ struct fr_graph {
     int64_t* other;           /* E: other vertex Titan id                         */
     uint8_t* edir;            /* E: 0 OUT, 1 IN                                   */
     uint8_t* has_w;           /* E                                                */
-    int32_t* w;               /* E                                                */
+    int64_t* w;               /* E (Long / Double keys: the value / its IEEE bits) */
     /* FulgoraVertexMemory's NonBlockingHashMapLong<VertexState>: Titan id -> index */
     int64_t* hkeys; int64_t* hvals; uint64_t hmask;
     /* Vertex cuts: pv[v] = 1 for a canonical partitioned vertex.  Its canonical row's
@@ -677,7 +686,7 @@ static int decode_row_entries(const fr_rows* rows, int64_t r, const fr_schema* s
         }
         /* messages are looked up by canonical id (VertexMemoryHandler.java:89) */
         if (fr_is_partitioned(oid, pb)) oid = fr_canonical_vertex_id(oid, pb);
-        g->other[*e] = oid; g->edir[*e] = (uint8_t)dr; g->has_w[*e] = (uint8_t)hw; g->w[*e] = (int32_t)wv;
+        g->other[*e] = oid; g->edir[*e] = (uint8_t)dr; g->has_w[*e] = (uint8_t)hw; g->w[*e] = wv;
         (*e)++;
     }
     return FR_OK;
@@ -702,7 +711,7 @@ int fr_load_rows(const fr_rows* rows, const fr_schema* schema, const fr_load_opt
     g->other = (int64_t*)malloc((total + 1) * sizeof(int64_t));
     g->edir = (uint8_t*)malloc(total + 1);
     g->has_w = (uint8_t*)malloc(total + 1);
-    g->w = (int32_t*)malloc((total + 1) * sizeof(int32_t));
+    g->w = (int64_t*)malloc((total + 1) * sizeof(int64_t));
     int typed = opts->n_labels > 0;
     int64_t limit = (opts->apply_cap && !typed && opts->scope != FR_SCOPE_BOTH_E) ? opts->hard_query_limit : INT64_MAX;
     /* pass 1: which rows execute (0 = filtered, 1 = vertex row, 2 = representative row) */
@@ -788,7 +797,7 @@ int fr_load_adjacency(int64_t n, const int64_t* titan_ids, const int64_t* off, c
     g->other = (int64_t*)malloc((E + 1) * sizeof(int64_t));
     g->edir = (uint8_t*)malloc(E + 1);
     g->has_w = (uint8_t*)malloc(E + 1);
-    g->w = (int32_t*)malloc((E + 1) * sizeof(int32_t));
+    g->w = (int64_t*)malloc((E + 1) * sizeof(int64_t));
     memcpy(g->titan_id, titan_ids, n * sizeof(int64_t));
     memcpy(g->eoff, off, (n + 1) * sizeof(int64_t));
     for (int64_t v = 0; v < n; v++)
@@ -822,7 +831,7 @@ int fr_load_edges_capped(int64_t n, int64_t m, const int32_t* src, const int32_t
     g->other = (int64_t*)malloc((E + 1) * sizeof(int64_t));
     g->edir = (uint8_t*)malloc(E + 1);
     g->has_w = (uint8_t*)malloc(E + 1);
-    g->w = (int32_t*)malloc((E + 1) * sizeof(int32_t));
+    g->w = (int64_t*)malloc((E + 1) * sizeof(int64_t));
     for (int64_t v = 0; v < n; v++) g->titan_id[v] = titan_ids[v];
     int64_t* outc = (int64_t*)calloc(n + 1, sizeof(int64_t));
     for (int64_t k = 0; k < m; k++) { outc[src[k]]++; g->eoff[src[k] + 1]++; g->eoff[dst[k] + 1]++; }
@@ -915,7 +924,7 @@ int64_t fr_export(const fr_graph* g, int64_t* off, int64_t* mid, int32_t* adj, i
                     int64_t o = entry_vertex(g, k);
                     if (o < 0) continue;
                     adj[e] = (int32_t)o;
-                    if (w) w[e] = g->has_w[k] ? g->w[k] : INT32_MIN;
+                    if (w) w[e] = g->has_w[k] ? (int32_t)g->w[k] : INT32_MIN;
                     e++;
                 }
             }
@@ -1234,8 +1243,10 @@ static double edge_fn_d(int fn, double m, double x) {
     default: return m / x;
     }
 }
-static double weight_as_double(const fr_graph* g, int32_t w) {
-    if (g->wdt == FR_DT_FLOAT) { float f; memcpy(&f, &w, 4); return (double)f; }
+/* e.value(key) widened to double: a Float's / Double's IEEE bits, an integral value as is */
+static double weight_as_double(const fr_graph* g, int64_t w) {
+    if (g->wdt == FR_DT_FLOAT) { int32_t b = (int32_t)w; float f; memcpy(&f, &b, 4); return (double)f; }
+    if (g->wdt == FR_DT_DOUBLE) { double d; memcpy(&d, &w, 8); return d; }
     return (double)w;
 }
 /* One message edgeFct(msg[o], e) of entry k (VertexMemoryHandler.java:83-92); 1 = present,
@@ -1248,10 +1259,10 @@ static int entry_message(const fr_graph* g, int64_t k, int64_t o, int value_type
         w = g->w[k];
     }
     if (value_type == 0) {
-        if (edge_fn >= 2 && g->wdt == FR_DT_FLOAT) return FR_E_INVALID;
+        if (edge_fn >= 2 && (g->wdt == FR_DT_FLOAT || g->wdt == FR_DT_DOUBLE)) return FR_E_INVALID;
         return edge_fn_i(edge_fn, ((const int64_t*)msg)[o], w, mi_out) ? FR_E_PROGRAM : 1;
     }
-    *md_out = edge_fn_d(edge_fn, ((const double*)msg)[o], edge_fn >= 2 ? weight_as_double(g, (int32_t)w) : 0.0);
+    *md_out = edge_fn_d(edge_fn, ((const double*)msg)[o], edge_fn >= 2 ? weight_as_double(g, w) : 0.0);
     return 1;
 }
 int fr_gather(const fr_graph* g, int scope, int value_type, int combiner, int edge_fn, const void* msg,
