@@ -153,8 +153,10 @@ typedef struct {
                                      MULTI label's sort key (ASC or DESC), its signature or its
                                      remaining properties.  Byte, Short, Integer, Character and
                                      Boolean keys are read as integers, Float keys as their IEEE
-                                     bits (-0.0 reads as +0.0); other datatypes fail with
-                                     TGO_E_UNSUPPORTED.  tgo_sssp / tgo_bfs need an Integer key
+                                     bits (-0.0 reads as +0.0), Long and Double keys into a
+                                     64-bit value table (row loads; generic edge functions only);
+                                     other datatypes fail with TGO_E_UNSUPPORTED.
+                                     tgo_sssp / tgo_bfs need an Integer key
                                      (ShortestDistanceVertexProgram.java:53 casts edge.<Integer>
                                      value; another datatype is a ClassCastException there);
                                      generic edge functions take any of them.  TTL / timestamp metadata is not
@@ -290,6 +292,7 @@ typedef struct {
     int32_t has_weight;
     int32_t weight;
 } tgo_edge_entry;
+/* (A Long / Double weight key fails here with TGO_E_UNSUPPORTED: the weight field is 32 bits.) */
 int  tgo_decode_edge_entry(const tgo_schema* schema, const tgo_load_opts* opts, const uint8_t* entry,
                            int64_t len, int64_t value_pos, tgo_edge_entry* out);
 
@@ -380,8 +383,9 @@ typedef enum { TGO_COMBINE_SUM = 0, TGO_COMBINE_MIN = 1, TGO_COMBINE_MAX = 2 } t
 typedef enum { TGO_VAL_INT64 = 0, TGO_VAL_FP64 = 1 } tgo_value_type;
 /* Edge functions: (message, edge) -> message, the BiFunction of MessageScope.Local
  * (VertexMemoryHandler.java:85,90) as "message op w", w = e.value(weight) of the load's
- * weight key.  int64 arithmetic wraps like Java long; int64 / 0 and a Float weight with
- * int64 messages fail with TGO_E_PROGRAM / TGO_E_INVALID. */
+ * weight key (an integral key, Float, Long or Double).  int64 arithmetic wraps like Java
+ * long; int64 / 0 fails with TGO_E_PROGRAM; a Float or Double weight with int64 messages
+ * with TGO_E_INVALID (long op double is a double in Java). */
 typedef enum {
     TGO_EDGE_IDENTITY = 0,    /* (m, e) -> m                    */
     TGO_EDGE_ADD_ONE = 1,     /* (m, e) -> m + 1                */

@@ -195,15 +195,38 @@ def test_product_decoder_matches_oracle(layout):
         assert prc == 0 and (e0.other_id, e0.has_weight) == (other, 0)
 
 
-def test_non_integer_weight_key_is_rejected():
-    # ShortestDistanceVertexProgram.java:53 casts edge.<Integer>value: any other datatype would
-    # be a ClassCastException in the reference
-    sd = schema_dict(0, [K[LONG]], [])
+@pytest.mark.parametrize("dt", [DATE, STRING])
+def test_unsupported_weight_key_is_rejected(dt):
+    # Date and String weights have no edge function here (and ShortestDistanceVertexProgram.java:53
+    # casts edge.<Integer>value: a ClassCastException in the reference)
+    sd = schema_dict(0, [K[dt]], [])
     s = osch(sd)
-    b, vp = fr.encode_edge(s, KNOWS, 0, 8, 1, [(K[LONG], 3)])
+    b, vp = fr.encode_edge(s, KNOWS, 0, 8, 1, [(K[dt], 3)])
     E_UNSUPPORTED = -7                     # TGO_E_UNSUPPORTED / FR_E_UNSUPPORTED
-    assert _oracle_decode(s, b, vp, K[LONG])[0] == E_UNSUPPORTED
-    assert _product_decode(sd, b, vp, K[LONG])[0] == E_UNSUPPORTED
+    assert _oracle_decode(s, b, vp, K[dt])[0] == E_UNSUPPORTED
+    assert _product_decode(sd, b, vp, K[dt])[0] == E_UNSUPPORTED
+
+
+@pytest.mark.parametrize("dt", [LONG, DOUBLE])
+@pytest.mark.parametrize("where", ["sort_key", "signature", "remaining"])
+def test_wide_weight_keys_decode_to_64_bits(dt, where):
+    """Long and Double weight keys (generic edge functions): the oracle reads
+    the 64-bit value — the Long, or the Double's IEEE bits (DoubleSerializer.java:25-41: putDouble,
+    byte order doubleToSortableLong then the Long flip) — in every position and sort order; the
+    product's single-entry call rejects them (its weight field is 32 bits), the row loads carry
+    them in a value table (tests/test_gpu_generic.py)."""
+    import struct
+    vals = [-(1 << 40) - 3, -1, 0, 7, 5_000_000_000] if dt == LONG else [-1099511627779, -2, 0, 3, 1 << 53]
+    for order in ("ASC", "DESC"):
+        sd = schema_dict(0, [K[dt]] if where == "sort_key" else [], [K[dt]] if where == "signature" else [], order)
+        s = osch(sd)
+        for i, x in enumerate(vals):
+            b, vp = fr.encode_edge(s, KNOWS, i % 2, 8 + 8 * i, 100 + i, [(K[dt], x)])
+            orc, o = _oracle_decode(s, b, vp, K[dt])
+            assert orc == 0 and o[4] == 1
+            want = x if dt == LONG else struct.unpack("<q", struct.pack("<d", float(x)))[0]
+            assert o[5] == want, (dt, where, order, x)
+            assert _product_decode(sd, b, vp, K[dt])[0] == -7
 
 
 @pytest.mark.parametrize("dt", [BYTE, SHORT, CHARACTER, BOOLEAN, FLOAT])

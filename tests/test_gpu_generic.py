@@ -265,6 +265,78 @@ def test_float_weights_in_generic_edge_functions():
         o.shortest_distance(int(vids[0]), 5, IN, weighted=True)
 
 
+def wide_weight_rows(dt, where, order="ASC"):
+    """A power-law graph whose weight is a Long (4) or Double (6) property, in the remaining
+    properties or a MULTI label's sort key (ASC / DESC), with values past 32 bits (Long: about
+    +-4e11; Double: integral values up to 2^41, not representable as a Float)."""
+    import edgestore as es
+    scale = 9
+    n = 1 << scale
+    src, dst, w = rmat_edges(scale, 8, seed=93, weights=True)
+    knows = es.user_edge_label(1)
+    key = es.user_property_key(3)
+    et = {"type_id": knows, "multiplicity": 0}
+    if where == "sort_key":
+        et.update({"sort_key": [key], "order": order})
+    sd = {"edge_types": [et], "property_keys": [[key, dt]]}
+    osch = fr.OracleSchema(sd["edge_types"], [(key, dt)])
+    vals = (w.astype(np.int64) - 100) * 3_000_000_007 + 11
+    spec = es.GraphSpec(n=n, edges=[(int(a), int(b), knows, [(key, int(x))]) for a, b, x in zip(src, dst, vals)])
+    rows, vids = es.build_rows(spec, osch)
+    return rows, vids, sd, osch, key
+
+
+@pytest.mark.parametrize("dt", [4, 6])
+@pytest.mark.parametrize("where,order", [("remaining", "ASC"), ("sort_key", "ASC"), ("sort_key", "DESC")])
+@pytest.mark.parametrize("host_decode", [False, True])
+def test_long_double_weights_in_generic_edge_functions(dt, where, order, host_decode, monkeypatch):
+    """Long and Double weight keys (row loads; the weight column holds each
+    entry's staged position into a 64-bit value table).  fp64 messages with every weight edge
+    function and int64 messages with a Long weight (Java long arithmetic) equal the oracle's
+    gathers (exact combiners) and streams; a Double weight refuses int64 messages, and
+    ShortestDistance (edge.<Integer>value) fails as its ClassCastException does — through the
+    device decoder and the host decoder (TGO_HOST_DECODE=1) alike."""
+    if host_decode:
+        monkeypatch.setenv("TGO_HOST_DECODE", "1")
+    rows, vids, sd, osch, key = wide_weight_rows(dt, where, order)
+    eng = Engine().load_rows(rows, Schema.from_dict(sd), IN, weight_key=key)
+    o = fr.OracleGraph.from_rows(rows, osch, IN, weight_key=key)
+    ids = o.vertex_ids()
+    assert np.array_equal(np.sort(eng.vertex_ids()), np.sort(ids))
+    rng = np.random.default_rng(5)
+    msg = rng.standard_normal(eng.n) * 1e3
+    has = rng.random(eng.n) < 0.8
+    fns = (L.EDGE_ADD_WEIGHT, L.EDGE_MUL_WEIGHT, L.EDGE_SUB_WEIGHT, L.EDGE_MIN_WEIGHT, L.EDGE_MAX_WEIGHT,
+           L.EDGE_DIV_WEIGHT)
+    for fn in fns:
+        for comb in (L.COMBINE_MIN, L.COMBINE_MAX):
+            got, gh = eng.gather(IN, L.VAL_FP64, comb, fn, reorder(ids, msg, eng.vertex_ids()),
+                                 reorder(ids, has, eng.vertex_ids()))
+            exp, eh = o.gather(IN, 1, comb, fn, msg, has)
+            got, gh = reorder(eng.vertex_ids(), got, ids), reorder(eng.vertex_ids(), gh, ids)
+            assert np.array_equal(gh, eh) and np.array_equal(got[gh], exp[eh]), (fn, comb)
+    off, vals = eng.gather_lists(IN, L.VAL_FP64, L.EDGE_ADD_WEIGHT, reorder(ids, msg, eng.vertex_ids()),
+                                 reorder(ids, has, eng.vertex_ids()))
+    ooff, ovals = o.gather_lists(IN, 1, L.EDGE_ADD_WEIGHT, msg, has)
+    assert off[-1] == ooff[-1] and np.array_equal(np.sort(vals), np.sort(ovals))
+    imsg = rng.integers(-(1 << 40), 1 << 40, eng.n)
+    if dt == 4:
+        for fn in fns[:-1]:
+            for comb in (L.COMBINE_SUM, L.COMBINE_MIN):
+                got, gh = eng.gather(IN, L.VAL_INT64, comb, fn, reorder(ids, imsg, eng.vertex_ids()),
+                                     reorder(ids, has, eng.vertex_ids()))
+                exp, eh = o.gather(IN, 0, comb, fn, imsg, has)
+                got, gh = reorder(eng.vertex_ids(), got, ids), reorder(eng.vertex_ids(), gh, ids)
+                assert np.array_equal(gh, eh) and np.array_equal(got[gh], exp[eh]), (fn, comb)
+    else:
+        with pytest.raises(TitanException) as e:
+            eng.gather(IN, L.VAL_INT64, L.COMBINE_SUM, L.EDGE_ADD_WEIGHT, np.zeros(eng.n, np.int64))
+        assert e.value.code == L.TGO_E_INVALID
+    with pytest.raises(TitanException) as e:
+        eng.sssp(int(vids[0]), 5, IN)
+    assert e.value.code == L.TGO_E_UNSUPPORTED
+
+
 def test_integer_division_by_zero_fails_the_program():
     n = 64
     src, dst, w = np.array([0, 1, 2], np.int32), np.array([1, 2, 3], np.int32), np.array([3, 0, 5], np.int32)

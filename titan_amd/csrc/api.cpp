@@ -418,9 +418,10 @@ int upload_graph(tgo_ctx* ctx, HostGraph& h, bool allow_segments = true) {
     g.max_weight = 0;
     double wsum = 0.0;
     int64_t wcnt = 0;
+    const bool wide = h.has_weight && wide_weight_dt(h.weight_dt);   // the column holds value-table indices
     for (const HostCsr* c : {&h.out, &h.in})
         for (int32_t x : c->w)
-            if (x != kMissingWeight) {
+            if (x != kMissingWeight && !wide) {
                 g.min_weight = std::min(g.min_weight, x);
                 g.max_weight = std::max(g.max_weight, x);
                 wsum += x;
@@ -445,6 +446,11 @@ int upload_graph(tgo_ctx* ctx, HostGraph& h, bool allow_segments = true) {
     HIP_TRY(up(h.out, g.out));
     HIP_TRY(up(h.in, g.in));
     if (h.has_transpose) HIP_TRY(up(h.push_t, g.push_t));
+    g.wval = nullptr;
+    if (wide) {
+        if (h.d_wval.present()) adopt(ctx, g.wval, h.d_wval);
+        else HIP_TRY(upload(ctx, g.wval, h.wval));
+    }
     lap("csr");
     // CSR-adaptive blocks for the two pull gathers (walk counts: out; PageRank: in).
     HIP_TRY(upload_row_blocks(ctx, h.out.off, g.rb_out));
@@ -453,7 +459,7 @@ int upload_graph(tgo_ctx* ctx, HostGraph& h, bool allow_segments = true) {
     lap("row blocks");
     g.push_ws = DevCsr();
     g.push_ws_ready = false;
-    if (allow_segments && h.has_weight && env_i64("TGO_DS_SPLIT", 1) != 0) {
+    if (allow_segments && h.has_weight && !wide && env_i64("TGO_DS_SPLIT", 1) != 0) {
         HostCsr ws;                      // light/heavy delta-stepping: push entries sorted by weight
         weight_sorted_push(h, ws, threads_of(ctx));
         HIP_TRY(up(ws, g.push_ws));
@@ -1182,6 +1188,9 @@ int tgo_finish_load(tgo_ctx* ctx) {
         rc = on_dev ? assemble_rows_device(ctx->staging, h, ctx->stream, err)
                     : assemble_from_rows(ctx->staging, h, threads_of(ctx), err);
     if (rc) { ctx->staging = RowStaging(); return fail(ctx, rc, err); }
+    // a wide (Long / Double) weight key: the staged values become the graph's value table
+    h.wval = std::move(ctx->staging.wv);
+    h.d_wval = std::move(ctx->staging.d_wv);
     if (env_i64("TGO_TRACE", 0))
         std::fprintf(stderr, "[tgo] finish_load decode + assembly (%s) %8.1f ms\n", on_dev ? "device" : "host",
                      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
@@ -2812,9 +2821,17 @@ static int check_gather_args(tgo_ctx* ctx, const tgo_gather_args* a, bool combin
         return fail(ctx, TGO_E_INVALID, "invalid value type, combiner or edge function");
     if (weight_edge_fn(a->edge_fn) && !ctx->g.has_weight)
         return fail(ctx, TGO_E_INVALID, "weight edge function on a graph loaded without a weight property");
-    if (weight_edge_fn(a->edge_fn) && ctx->g.weight_dt == TGO_DT_FLOAT && a->value_type == TGO_VAL_INT64)
-        return fail(ctx, TGO_E_INVALID, "a Float weight needs fp64 messages (long op float is a float in Java)");
+    if (weight_edge_fn(a->edge_fn) && (ctx->g.weight_dt == TGO_DT_FLOAT || ctx->g.weight_dt == TGO_DT_DOUBLE) &&
+        a->value_type == TGO_VAL_INT64)
+        return fail(ctx, TGO_E_INVALID, "a Float / Double weight needs fp64 messages (long op double is a double in Java)");
     return TGO_OK;
+}
+
+static WeightCol weight_col(const DevGraph& g) {
+    WeightCol wc;
+    wc.kind = g.weight_dt == TGO_DT_FLOAT ? 1 : g.weight_dt == TGO_DT_LONG ? 2 : g.weight_dt == TGO_DT_DOUBLE ? 3 : 0;
+    wc.wide = g.wval;
+    return wc;
 }
 
 static int gather_error(tgo_ctx* ctx, unsigned long long err) {
@@ -2842,7 +2859,7 @@ int tgo_gather(tgo_ctx* ctx, const tgo_gather_args* a, const void* msg, const ui
     HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
     HIP_TRY(k_to_internal(s.gv[0], s.gh[0], ctx->g.perm, s.gv[1], s.gh[1], n, st));
     HIP_TRY(k_local_gather(pull_view(ctx->g, a->scope), n, a->value_type, s.gv[1], s.gh[1], a->combiner, a->edge_fn,
-                           ctx->g.weight_dt == TGO_DT_FLOAT, s.gv[2], s.gh[2], &s.cnt->err, st));
+                           weight_col(ctx->g), s.gv[2], s.gh[2], &s.cnt->err, st));
     HIP_TRY(k_to_rows(s.gv[2], s.gh[2], ctx->g.perm, s.gv[0], s.gh[0], n, st));
     HIP_TRY(hipEventRecord(ctx->ev1, st));
     HIP_TRY(hipMemcpyAsync(out, s.gv[0], n * 8, hipMemcpyDeviceToHost, st));
@@ -2868,7 +2885,7 @@ int tgo_gather_lists(tgo_ctx* ctx, const tgo_gather_args* a, const void* msg, co
     const DevGraph& g = ctx->g;
     const int64_t n = g.n;
     const View pull = pull_view(g, a->scope);
-    const bool wfloat = g.weight_dt == TGO_DT_FLOAT;
+    const WeightCol wc = weight_col(g);
     HIP_TRY(hipMemcpyAsync(s.gv[0], msg, n * 8, hipMemcpyHostToDevice, st));
     if (has) HIP_TRY(hipMemcpyAsync(s.gh[0], has, n, hipMemcpyHostToDevice, st));
     else HIP_TRY(hipMemsetAsync(s.gh[0], 1, n, st));
@@ -2903,7 +2920,7 @@ int tgo_gather_lists(tgo_ctx* ctx, const tgo_gather_args* a, const void* msg, co
     const uint32_t* col0 = !g.has_col ? nullptr : a->scope == TGO_SCOPE_OUT_E ? g.in.col : g.out.col;
     const uint32_t* col1 = !g.has_col || a->scope != TGO_SCOPE_BOTH_E ? nullptr : g.in.col;
     hipError_t e = k_list_fill_sort(pull, col0, col1, g.perm, inv, n,
-                                    a->value_type, s.gv[1], s.gh[1], a->edge_fn, wfloat, off, total, key_in, key_out,
+                                    a->value_type, s.gv[1], s.gh[1], a->edge_fn, wc, off, total, key_in, key_out,
                                     val_in, val_out, s.sort_tmp, s.sort_bytes, &s.cnt->err, st);
     if (e == hipSuccess) e = hipMemcpyAsync(values, val_out, total * 8, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);

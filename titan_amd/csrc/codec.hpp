@@ -147,7 +147,7 @@ TGO_HD inline bool unique_in(int mult, int dir) {  // Multiplicity.isUnique
 // a null flag byte unless the serializer handles null itself (StringSerializer), then the
 // attribute serializer's read, or readByteOrder for a sort key (byte_order).  Integral values
 // (Byte..Long, Boolean, Date, Character) are returned in v, a Float as its IEEE bits (int32);
-// Double/String are skipped.
+// String is skipped; Double gives its IEEE bits.
 // Returns false on a codec error; present=false for a serialized null.
 TGO_HD inline bool read_value(Cursor& c, int dt, bool byte_order, bool& present, int64_t& v) {
     v = 0;
@@ -217,7 +217,16 @@ TGO_HD inline bool read_value(Cursor& c, int dt, bool byte_order, bool& present,
             v = static_cast<int32_t>(u);
             break;
         }
-        case TGO_DT_DOUBLE: c.skip(8); break;
+        case TGO_DT_DOUBLE: {                      // DoubleSerializer :25-41: the IEEE bits, or
+            uint64_t u = c.be(8);                  // NumericUtils.doubleToSortableLong ^ sign
+            if (byte_order) {
+                int64_t sl = static_cast<int64_t>(u ^ 0x8000000000000000ULL);
+                sl ^= (sl >> 63) & 0x7fffffffffffffffLL;
+                u = static_cast<uint64_t>(sl);
+            }
+            v = static_cast<int64_t>(u);
+            break;
+        }
         case TGO_DT_BOOLEAN: v = c.get(); break;
         default: return false;
     }
@@ -269,7 +278,8 @@ struct DecodedEdge {
     int dir;
     int64_t other;
     bool has_weight;
-    int32_t weight;
+    int32_t weight;          // 32-bit weight keys (Float: the IEEE bits)
+    int64_t weight64;        // the same value in 64 bits (Long: the value, Double: the IEEE bits)
 };
 
 enum class DecodeResult { kOk, kSkip, kError, kUnsupported };
@@ -311,6 +321,7 @@ TGO_HD inline DecodeResult decode_edge(const uint8_t* d, size_t len, size_t valu
     if (c.bad) return DecodeResult::kError;
     out.has_weight = false;
     out.weight = 0;
+    out.weight64 = 0;
     if (plan.weight_key == 0 || lp->weight_where == kWeightNone) return DecodeResult::kOk;
     bool present; int64_t v = 0;
     if (lp->weight_where == kWeightSortKey) {
@@ -320,6 +331,7 @@ TGO_HD inline DecodeResult decode_edge(const uint8_t* d, size_t len, size_t valu
             if (!read_value(k, plan.dts[lp->sort_dt_off + i], true, present, v)) return DecodeResult::kError;
         out.has_weight = present;
         out.weight = static_cast<int32_t>(v);
+        out.weight64 = v;
         return DecodeResult::kOk;
     }
     c.pos = props;
@@ -328,6 +340,7 @@ TGO_HD inline DecodeResult decode_edge(const uint8_t* d, size_t len, size_t valu
         if (k == lp->weight_index && lp->weight_where == kWeightSignature) {
             out.has_weight = present;
             out.weight = static_cast<int32_t>(v);
+            out.weight64 = v;
             return DecodeResult::kOk;
         }
     }
@@ -339,6 +352,7 @@ TGO_HD inline DecodeResult decode_edge(const uint8_t* d, size_t len, size_t valu
         if (kid == plan.weight_key) {
             out.has_weight = present;
             out.weight = static_cast<int32_t>(v);
+            out.weight64 = v;
             return DecodeResult::kOk;
         }
     }

@@ -78,7 +78,7 @@ __global__ void __launch_bounds__(kBlock) dec_entries(const int64_t* __restrict_
         const int64_t* __restrict__ eb, const int64_t* __restrict__ lv, const int64_t* __restrict__ first,
         const int64_t* __restrict__ koff, int64_t nrows, int64_t total, PlanView plan, int pb, int weighted,
         int64_t* __restrict__ other, uint8_t* __restrict__ dir, int32_t* __restrict__ w, uint8_t* __restrict__ sel,
-        int32_t* __restrict__ err) {
+        int32_t* __restrict__ err, int64_t* __restrict__ wv) {
     for (int64_t p = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; p < total;
          p += static_cast<int64_t>(gridDim.x) * blockDim.x) {
         int64_t lo = 0, hi = nrows;                                  // row r: koff[r] <= p < koff[r+1]
@@ -103,6 +103,7 @@ __global__ void __launch_bounds__(kBlock) dec_entries(const int64_t* __restrict_
         other[p] = is_partitioned_vertex(de.other, pb) ? canonical_vertex_id(de.other, pb) : de.other;  // :89
         dir[p] = static_cast<uint8_t>(de.dir);
         w[p] = weighted ? (de.has_weight ? de.weight : kMissingWeight) : 1;
+        if (wv) wv[p] = de.has_weight ? de.weight64 : 0;          // wide keys (Long / Double)
     }
 }
 
@@ -112,16 +113,20 @@ __global__ void sel_to_i64(const uint8_t* __restrict__ sel, int64_t total, int64
     for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p <= total; p += (int64_t)gridDim.x * blockDim.x)
         out[p] = p < total ? sel[p] : 0;
 }
+// wv (wide weight keys): the values follow their entries, and the weight column becomes the
+// entry's staged position (base + q) — the index into the graph's value table.
 __global__ void compact_entries(const uint8_t* __restrict__ sel, const int64_t* __restrict__ ks, int64_t total,
                                 const int64_t* __restrict__ other, const uint8_t* __restrict__ dir,
                                 const int32_t* __restrict__ w, int64_t* __restrict__ c_other,
-                                uint8_t* __restrict__ c_dir, int32_t* __restrict__ c_w) {
+                                uint8_t* __restrict__ c_dir, int32_t* __restrict__ c_w,
+                                const int64_t* __restrict__ wv, int64_t* __restrict__ c_wv, int64_t base) {
     for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < total; p += (int64_t)gridDim.x * blockDim.x) {
         if (!sel[p]) continue;
         const int64_t q = ks[p];
         c_other[q] = other[p];
         c_dir[q] = dir[p];
-        c_w[q] = w[p];
+        c_w[q] = (wv && w[p] != kMissingWeight) ? static_cast<int32_t>(base + q) : w[p];
+        if (wv) c_wv[q] = wv[p];
     }
 }
 __global__ void row_kept_begin(const int64_t* __restrict__ koff, const int64_t* __restrict__ ks, int64_t nrows,
@@ -136,7 +141,7 @@ void DecodeScratch::release() {
     keys.release(); eb.release(); bb.release(); bytes.release(); lv.release(); vid.release(); first.release();
     keep.release(); koff.release(); status.release(); rep.release(); other.release(); dir.release(); w.release();
     sel.release(); err.release(); trunc.release(); plan_labels.release(); plan_keys.release(); plan_kdts.release();
-    plan_dts.release(); ks.release(); c_other.release(); c_dir.release(); c_w.release();
+    plan_dts.release(); ks.release(); c_other.release(); c_dir.release(); c_w.release(); wv.release(); c_wv.release();
     bytes_used = lv_used = 0;
     if (cub_tmp) (void)hipFree(cub_tmp);
     cub_tmp = nullptr;
@@ -245,10 +250,12 @@ int decode_staged_raw(RowStaging& st, int pb, int64_t hard_limit, DecodeScratch&
     DEC_TRY(ds.sel.grow(total + 1));
     const PlanView plan{reinterpret_cast<const LabelPlan*>(ds.plan_labels.p), hp.n_labels,
                         static_cast<int32_t>(hp.key_ids.size()), ds.plan_keys.p, ds.plan_kdts.p, ds.plan_dts.p, hp.weight_key};
+    const bool wide = opts->weight_key != 0 && wide_weight_dt(hp.weight_dt);
+    if (wide) DEC_TRY(ds.wv.grow(total + 1));
     if (total > 0) {
         dec_entries<<<grid_for(total), kBlock, 0, stream>>>(ds.bb.p, ds.bytes.p, ds.eb.p, ds.lv.p, ds.first.p, ds.koff.p, nrows, total,
                                                              plan, pb, opts->weight_key != 0 ? 1 : 0, ds.other.p, ds.dir.p,
-                                                             ds.w.p, ds.sel.p, ds.err.p);
+                                                             ds.w.p, ds.sel.p, ds.err.p, wide ? ds.wv.p : nullptr);
         DEC_TRY(hipGetLastError());
     }
     // kept entries compacted on the device, in staging order
@@ -256,13 +263,17 @@ int decode_staged_raw(RowStaging& st, int pb, int64_t hard_limit, DecodeScratch&
     DEC_TRY(ds.c_other.grow(total + 1));
     DEC_TRY(ds.c_dir.grow(total + 1));
     DEC_TRY(ds.c_w.grow(total + 1));
+    if (wide) DEC_TRY(ds.c_wv.grow(total + 1));
     DEC_TRY(ds.keep.grow(std::max(nrows, total) + 1));
+    const int64_t e_base = static_cast<int64_t>(st.other.size());     // staged position of the first kept entry
+    if (wide && e_base + total >= INT32_MAX) { err = "wide weights: more than 2^31 - 1 staged entries"; return TGO_E_UNSUPPORTED; }
     sel_to_i64<<<grid_for(total + 1), kBlock, 0, stream>>>(ds.sel.p, total, ds.keep.p);
     DEC_TRY(hipGetLastError());
     DEC_TRY(scan_exclusive_i64(ds.cub_tmp, ds.cub_bytes, ds.keep.p, ds.ks.p, total + 1, stream));
     if (total > 0) {
         compact_entries<<<grid_for(total), kBlock, 0, stream>>>(ds.sel.p, ds.ks.p, total, ds.other.p, ds.dir.p, ds.w.p,
-                                                                ds.c_other.p, ds.c_dir.p, ds.c_w.p);
+                                                                ds.c_other.p, ds.c_dir.p, ds.c_w.p, wide ? ds.wv.p : nullptr,
+                                                                wide ? ds.c_wv.p : nullptr, e_base);
         DEC_TRY(hipGetLastError());
     }
     row_kept_begin<<<grid_for(nrows + 1), kBlock, 0, stream>>>(ds.koff.p, ds.ks.p, nrows, ds.keep.p);
@@ -283,6 +294,7 @@ int decode_staged_raw(RowStaging& st, int pb, int64_t hard_limit, DecodeScratch&
         st.d_other.own(ds.c_other.p, kept); ds.c_other.p = nullptr; ds.c_other.cap = 0;
         st.d_dir.own(ds.c_dir.p, kept); ds.c_dir.p = nullptr; ds.c_dir.cap = 0;
         st.d_w.own(ds.c_w.p, kept); ds.c_w.p = nullptr; ds.c_w.cap = 0;
+        if (wide) { st.d_wv.own(ds.c_wv.p, kept); ds.c_wv.p = nullptr; ds.c_wv.cap = 0; }
     } else if (kept > 0) {
         st.other.resize(e0 + static_cast<size_t>(kept));
         st.dir.resize(e0 + static_cast<size_t>(kept));
@@ -290,6 +302,10 @@ int decode_staged_raw(RowStaging& st, int pb, int64_t hard_limit, DecodeScratch&
         DEC_TRY(hipMemcpyAsync(st.other.data() + e0, ds.c_other.p, kept * 8, hipMemcpyDeviceToHost, stream));
         DEC_TRY(hipMemcpyAsync(st.dir.data() + e0, ds.c_dir.p, kept, hipMemcpyDeviceToHost, stream));
         DEC_TRY(hipMemcpyAsync(st.w.data() + e0, ds.c_w.p, kept * 4, hipMemcpyDeviceToHost, stream));
+        if (wide) {
+            st.wv.resize(e0 + static_cast<size_t>(kept));
+            DEC_TRY(hipMemcpyAsync(st.wv.data() + e0, ds.c_wv.p, kept * 8, hipMemcpyDeviceToHost, stream));
+        }
         DEC_TRY(hipStreamSynchronize(stream));
     }
 #undef DEC_TRY
@@ -320,10 +336,15 @@ int staging_entries_to_host(RowStaging& st, hipStream_t stream, std::string& err
     if (E > 0 && e == hipSuccess) e = copy_chunked(st.other.data(), st.d_other.p, E * 8, hipMemcpyDeviceToHost);
     if (E > 0 && e == hipSuccess) e = copy_chunked(st.dir.data(), st.d_dir.p, E, hipMemcpyDeviceToHost);
     if (E > 0 && e == hipSuccess) e = copy_chunked(st.w.data(), st.d_w.p, E * 4, hipMemcpyDeviceToHost);
+    if (st.d_wv.present()) {
+        st.wv.resize(static_cast<size_t>(E));
+        if (E > 0 && e == hipSuccess) e = copy_chunked(st.wv.data(), st.d_wv.p, E * 8, hipMemcpyDeviceToHost);
+    }
     if (e != hipSuccess) { err = hipGetErrorString(e); return TGO_E_HIP; }
     st.d_other.reset();
     st.d_dir.reset();
     st.d_w.reset();
+    st.d_wv.reset();
     return TGO_OK;
 }
 

@@ -58,6 +58,9 @@ struct HostCsr {
 
 struct HostGraph {
     int64_t n = 0;
+    // Long / Double weight keys: the value table the lists' weight column indexes (host or device)
+    std::vector<int64_t> wval;
+    DevArray<int64_t> d_wval;
     std::vector<int64_t> titan_id;   // row order (the API's dense ids)
     bool ids_sorted = false;         // titan_id known strictly increasing (no check needed)
     std::vector<int32_t> perm;       // row-order dense id -> internal id (degree-grouped)
@@ -76,6 +79,9 @@ struct HostGraph {
 };
 
 // Owner of a codec PlanView (codec.hpp) built from tgo_schema + tgo_load_opts.
+// Long / Double weight keys: the weight column holds staged positions into a 64-bit value table
+inline bool wide_weight_dt(int dt) { return dt == TGO_DT_LONG || dt == TGO_DT_DOUBLE; }
+
 struct HostPlan {
     std::vector<uint8_t> label_bytes;   // LabelPlan records (opaque here; codec.hpp defines them)
     std::vector<int64_t> key_ids;
@@ -97,6 +103,8 @@ struct RowStaging {
     DevArray<int64_t> d_other;
     DevArray<uint8_t> d_dir;
     DevArray<int32_t> d_w;
+    std::vector<int64_t> wv;         // wide weight keys: entry k's 64-bit value (w[k] = k)
+    DevArray<int64_t> d_wv;
     int64_t entries() const { return d_other.present() ? d_other.n : static_cast<int64_t>(other.size()); }
     std::vector<uint8_t> rep;        // per row: 1 = non-canonical representative of a vertex cut
     int64_t ghost = 0, truncated = 0, skipped = 0;
@@ -172,7 +180,7 @@ struct DBuf {
     }
 };
 struct DecodeScratch {
-    DBuf<int64_t> keys, eb, bb, lv, vid, first, keep, koff, other, plan_keys, ks, c_other;
+    DBuf<int64_t> keys, eb, bb, lv, vid, first, keep, koff, other, plan_keys, ks, c_other, wv, c_wv;
     DBuf<uint8_t> bytes, rep, dir, sel, plan_labels, c_dir;
     DBuf<int8_t> plan_kdts, plan_dts;
     DBuf<int32_t> status, w, err, c_w;
@@ -401,6 +409,7 @@ struct DevGraph {
     bool has_col = false;       // out.col / in.col hold column positions
     int32_t min_weight = 0, max_weight = 0;
     double mean_weight = 1.0;   // over present weights (delta-stepping's default bucket width)
+    int64_t* wval = nullptr;    // Long / Double weight keys: the value table the weight column indexes
     int32_t scope = TGO_SCOPE_BOTH_E;
     bool partitioned = false;   // 1-D vertex partition: rows [lo, lo+n) of an n_global graph
     int64_t lo = 0, n_global = 0;
@@ -696,14 +705,20 @@ hipError_t k_walk_iter(const DevCsr& out, const RowBlocks& rb, const int32_t* pr
                        int32_t* partial, int64_t n, hipStream_t s);
 
 // Generic vertex programs (generic.hip)
+// The weight column of a generic edge function: 32-bit integers (kind 0), a Float's IEEE bits
+// (1), or indices into the Long (2) / Double (3, IEEE bits) value table `wide`.
+struct WeightCol {
+    int kind = 0;
+    const int64_t* wide = nullptr;
+};
 hipError_t k_local_gather(const View& pull, int64_t n, int value_type, const void* msg_int, const uint8_t* has_int,
-                          int comb, int fn, bool wfloat, void* out_int, uint8_t* out_has_int, unsigned long long* err,
+                          int comb, int fn, WeightCol wc, void* out_int, uint8_t* out_has_int, unsigned long long* err,
                           hipStream_t s);
 hipError_t k_list_count(const View& pull, const int32_t* perm, int64_t n, const uint8_t* has_int, int fn,
                         int64_t* cnt, unsigned long long* err, hipStream_t s);
 hipError_t k_list_fill_sort(const View& pull, const uint32_t* col0, const uint32_t* col1, const int32_t* perm,
                             int32_t* inv, int64_t n, int value_type, const void* msg_int, const uint8_t* has_int,
-                            int fn, bool wfloat, const int64_t* off_out, int64_t total, uint32_t* key_in,
+                            int fn, WeightCol wc, const int64_t* off_out, int64_t total, uint32_t* key_in,
                             uint32_t* key_out, void* val_in, void* val_out, void*& tmp, size_t& tmp_bytes,
                             unsigned long long* err, hipStream_t s);
 hipError_t k_to_internal(const void* row8, const uint8_t* row1, const int32_t* perm, void* int8, uint8_t* int1,

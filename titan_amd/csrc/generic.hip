@@ -42,16 +42,26 @@ __device__ __forceinline__ int64_t combine<int64_t>(int comb, int64_t acc, int64
     return static_cast<int64_t>(static_cast<uint64_t>(acc) + static_cast<uint64_t>(m));
 }
 
-// edgeFct(m, e) = "m op w", w = e.value(weight): the weight column holds 32-bit integers, or
-// a Float's IEEE bits (wfloat).  Error bits: 1 = an edge without the weight property
-// (e.value() throws), 2 = int64 division by zero (Java ArithmeticException).
+// edgeFct(m, e) = "m op w", w = e.value(weight): the weight column holds 32-bit integers, a
+// Float's IEEE bits, or an index into the Long / Double value table (WeightCol).  Error bits:
+// 1 = an edge without the weight property (e.value() throws), 2 = int64 division by zero (Java
+// ArithmeticException).
 constexpr unsigned long long kErrNoWeight = 1, kErrDivZero = 2;
 __host__ __device__ __forceinline__ bool weight_fn(int fn) { return fn >= TGO_EDGE_ADD_WEIGHT && fn <= TGO_EDGE_DIV_WEIGHT; }
 
-__device__ __forceinline__ double edge_apply_f(int fn, double m, int32_t w, bool wfloat) {
+// e.value(weight) widened to double (double message): the value by the column's kind
+__device__ __forceinline__ double weight_f(int32_t w, const WeightCol& wc) {
+    switch (wc.kind) {
+        case 1: return static_cast<double>(__int_as_float(w));
+        case 2: return static_cast<double>(wc.wide[w]);
+        case 3: return __longlong_as_double(static_cast<long long>(wc.wide[w]));
+        default: return static_cast<double>(w);
+    }
+}
+__device__ __forceinline__ double edge_apply_f(int fn, double m, int32_t w, const WeightCol& wc) {
     if (fn == TGO_EDGE_IDENTITY) return m;
     if (fn == TGO_EDGE_ADD_ONE) return m + 1.0;
-    const double x = wfloat ? static_cast<double>(__int_as_float(w)) : static_cast<double>(w);
+    const double x = weight_f(w, wc);
     switch (fn) {
         case TGO_EDGE_ADD_WEIGHT: return m + x;
         case TGO_EDGE_MUL_WEIGHT: return m * x;
@@ -62,11 +72,13 @@ __device__ __forceinline__ double edge_apply_f(int fn, double m, int32_t w, bool
     }
 }
 // Java long arithmetic: + - * wrap, / truncates toward zero, MIN_VALUE / -1 = MIN_VALUE
-__device__ __forceinline__ int64_t edge_apply_i(int fn, int64_t m, int32_t w, unsigned long long* err) {
+// (long message: the host admits integral columns only — an int or a Long)
+__device__ __forceinline__ int64_t edge_apply_i(int fn, int64_t m, int32_t w, const WeightCol& wc,
+                                                unsigned long long* err) {
     const uint64_t u = static_cast<uint64_t>(m);
     if (fn == TGO_EDGE_IDENTITY) return m;
     if (fn == TGO_EDGE_ADD_ONE) return static_cast<int64_t>(u + 1u);
-    const int64_t x = static_cast<int64_t>(w);
+    const int64_t x = wc.kind == 2 ? wc.wide[w] : static_cast<int64_t>(w);
     switch (fn) {
         case TGO_EDGE_ADD_WEIGHT: return static_cast<int64_t>(u + static_cast<uint64_t>(x));
         case TGO_EDGE_MUL_WEIGHT: return static_cast<int64_t>(u * static_cast<uint64_t>(x));
@@ -79,19 +91,20 @@ __device__ __forceinline__ int64_t edge_apply_i(int fn, int64_t m, int32_t w, un
             return m / x;
     }
 }
-template <typename T> __device__ __forceinline__ T edge_apply(int fn, T m, int32_t w, bool wfloat, unsigned long long* err);
-template <> __device__ __forceinline__ double edge_apply<double>(int fn, double m, int32_t w, bool wfloat,
+template <typename T> __device__ __forceinline__ T edge_apply(int fn, T m, int32_t w, const WeightCol& wc,
+                                                             unsigned long long* err);
+template <> __device__ __forceinline__ double edge_apply<double>(int fn, double m, int32_t w, const WeightCol& wc,
                                                                unsigned long long*) {
-    return edge_apply_f(fn, m, w, wfloat);
+    return edge_apply_f(fn, m, w, wc);
 }
-template <> __device__ __forceinline__ int64_t edge_apply<int64_t>(int fn, int64_t m, int32_t w, bool,
+template <> __device__ __forceinline__ int64_t edge_apply<int64_t>(int fn, int64_t m, int32_t w, const WeightCol& wc,
                                                                  unsigned long long* err) {
-    return edge_apply_i(fn, m, w, err);
+    return edge_apply_i(fn, m, w, wc, err);
 }
 
 template <typename T>
 __global__ void local_gather(View pull, int64_t n, const T* __restrict__ msg, const uint8_t* __restrict__ has,
-                             int comb, int fn, bool wfloat, T* __restrict__ out, uint8_t* __restrict__ out_has,
+                             int comb, int fn, WeightCol wc, T* __restrict__ out, uint8_t* __restrict__ out_has,
                              unsigned long long* err) {
     const bool needs_w = weight_fn(fn);
     for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x) {
@@ -109,7 +122,7 @@ __global__ void local_gather(View pull, int64_t n, const T* __restrict__ msg, co
                     wt = w ? w[k] : kMissingWeight;
                     if (wt == kMissingWeight) { atomicOr(err, kErrNoWeight); continue; }   // e.value(key) throws
                 }
-                const T m = edge_apply<T>(fn, msg[u], wt, wfloat, err);
+                const T m = edge_apply<T>(fn, msg[u], wt, wc, err);
                 acc = any ? combine<T>(comb, acc, m) : m;
                 any = true;
             }
@@ -146,7 +159,7 @@ __global__ void list_count(View pull, const int32_t* __restrict__ perm, int64_t 
 template <typename T>
 __global__ void list_fill(View pull, const uint32_t* __restrict__ col0, const uint32_t* __restrict__ col1,
                           const int32_t* __restrict__ perm, const int32_t* __restrict__ inv, int64_t n,
-                          const T* __restrict__ msg, const uint8_t* __restrict__ has, int fn, bool wfloat,
+                          const T* __restrict__ msg, const uint8_t* __restrict__ has, int fn, WeightCol wc,
                           const int64_t* __restrict__ off_out, uint32_t* __restrict__ key, T* __restrict__ val,
                           unsigned long long* err) {
     const bool needs_w = weight_fn(fn);
@@ -167,7 +180,7 @@ __global__ void list_fill(View pull, const uint32_t* __restrict__ col0, const ui
                     if (wt == kMissingWeight) continue;
                 }
                 key[p] = col ? col[k] : ((static_cast<uint32_t>(l) << 31) | static_cast<uint32_t>(inv[u]));
-                val[p] = edge_apply<T>(fn, msg[u], wt, wfloat, err);
+                val[p] = edge_apply<T>(fn, msg[u], wt, wc, err);
                 ++p;
             }
         }
@@ -214,14 +227,14 @@ __global__ void iota_i64(int64_t* p, int64_t n) {
 }  // namespace
 
 hipError_t k_local_gather(const View& pull, int64_t n, int value_type, const void* msg_int, const uint8_t* has_int,
-                          int comb, int fn, bool wfloat, void* out_int, uint8_t* out_has_int, unsigned long long* err,
+                          int comb, int fn, WeightCol wc, void* out_int, uint8_t* out_has_int, unsigned long long* err,
                           hipStream_t s) {
     if (value_type == TGO_VAL_INT64)
         local_gather<int64_t><<<grid_for(n), kBlock, 0, s>>>(pull, n, static_cast<const int64_t*>(msg_int), has_int, comb,
-                                                            fn, wfloat, static_cast<int64_t*>(out_int), out_has_int, err);
+                                                            fn, wc, static_cast<int64_t*>(out_int), out_has_int, err);
     else
         local_gather<double><<<grid_for(n), kBlock, 0, s>>>(pull, n, static_cast<const double*>(msg_int), has_int, comb,
-                                                           fn, wfloat, static_cast<double*>(out_int), out_has_int, err);
+                                                           fn, wc, static_cast<double*>(out_int), out_has_int, err);
     return hipGetLastError();
 }
 
@@ -235,17 +248,17 @@ hipError_t k_list_count(const View& pull, const int32_t* perm, int64_t n, const 
 // row by key into key_out / val_out.  inv: n int32 scratch (internal -> row).
 hipError_t k_list_fill_sort(const View& pull, const uint32_t* col0, const uint32_t* col1, const int32_t* perm,
                             int32_t* inv, int64_t n, int value_type, const void* msg_int, const uint8_t* has_int,
-                            int fn, bool wfloat, const int64_t* off_out, int64_t total, uint32_t* key_in,
+                            int fn, WeightCol wc, const int64_t* off_out, int64_t total, uint32_t* key_in,
                             uint32_t* key_out, void* val_in, void* val_out, void*& tmp, size_t& tmp_bytes,
                             unsigned long long* err, hipStream_t s) {
     if (!col0) invert_perm<<<grid_for(n), kBlock, 0, s>>>(perm, inv, n);
     if (value_type == TGO_VAL_INT64)
         list_fill<int64_t><<<grid_for(n), kBlock, 0, s>>>(pull, col0, col1, perm, inv, n,
-                                                         static_cast<const int64_t*>(msg_int), has_int, fn, wfloat, off_out,
+                                                         static_cast<const int64_t*>(msg_int), has_int, fn, wc, off_out,
                                                          key_in, static_cast<int64_t*>(val_in), err);
     else
         list_fill<double><<<grid_for(n), kBlock, 0, s>>>(pull, col0, col1, perm, inv, n,
-                                                        static_cast<const double*>(msg_int), has_int, fn, wfloat, off_out,
+                                                        static_cast<const double*>(msg_int), has_int, fn, wc, off_out,
                                                         key_in, static_cast<double*>(val_in), err);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || total == 0) return e;

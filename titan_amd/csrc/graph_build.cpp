@@ -65,16 +65,19 @@ int build_plan(const tgo_schema* schema, const tgo_load_opts* opts, HostPlan& hp
         auto it = std::lower_bound(hp.key_ids.begin(), hp.key_ids.end(), key);
         return it != hp.key_ids.end() && *it == key ? hp.key_dts[it - hp.key_ids.begin()] : 0;
     };
-    // The weight is read into 32 bits: the integral datatypes that fit (Byte, Short, Integer,
-    // Character, Boolean) as integers, Float as its IEEE bits.  Long / Double / Date / String
-    // weights are not supported.  ShortestDistanceVertexProgram itself casts to Integer
-    // (edge.<Integer>value, :53): its entry points reject any other weight datatype, as the
-    // reference fails with a ClassCastException; generic programs' edge functions take them all.
+    // The weight column is 32 bits: the integral datatypes that fit (Byte, Short, Integer,
+    // Character, Boolean) as integers, Float as its IEEE bits.  Long and Double keys are wide:
+    // the column then holds each entry's staged position and the 64-bit values (the Long, the
+    // Double's IEEE bits) ride in a parallel staged array (RowStaging::wv) that becomes the
+    // graph's value table (DevGraph::wval).  Date / String weights are not supported.
+    // ShortestDistanceVertexProgram itself casts to Integer (edge.<Integer>value, :53): its entry
+    // points reject any other weight datatype, as the reference fails with a ClassCastException;
+    // generic programs' edge functions take them all.
     if (opts->weight_key != 0) {
         const int dt = dt_of(opts->weight_key);
         if (dt != TGO_DT_INTEGER && dt != TGO_DT_BYTE && dt != TGO_DT_SHORT && dt != TGO_DT_CHARACTER &&
-            dt != TGO_DT_BOOLEAN && dt != TGO_DT_FLOAT) {
-            err = "weight property must be a Byte, Short, Integer, Character, Boolean or Float key";
+            dt != TGO_DT_BOOLEAN && dt != TGO_DT_FLOAT && !wide_weight_dt(dt)) {
+            err = "weight property must be a Byte, Short, Integer, Character, Boolean, Float, Long or Double key";
             return TGO_E_UNSUPPORTED;
         }
         hp.weight_dt = dt;
@@ -130,6 +133,10 @@ int decode_one_entry(const tgo_schema* schema, const tgo_load_opts* opts, const 
                      int64_t len, int64_t value_pos, tgo_edge_entry* out, std::string& err) {
     HostPlan hp;
     if (int rc = build_plan(schema, opts, hp, err)) return rc;
+    if (opts->weight_key != 0 && wide_weight_dt(hp.weight_dt)) {      // tgo_edge_entry.weight is 32 bits
+        err = "tgo_decode_edge_entry: a Long / Double weight key does not fit the 32-bit weight field";
+        return TGO_E_UNSUPPORTED;
+    }
     if (len < 0 || value_pos < 0 || (len > 0 && !entry)) { err = "invalid entry"; return TGO_E_INVALID; }
     DecodedEdge de{};
     const DecodeResult dr = decode_edge(entry, static_cast<size_t>(len), static_cast<size_t>(value_pos),
@@ -183,10 +190,12 @@ int decode_rows(RowStaging& st, const tgo_rows* rows, const tgo_schema* schema,
         std::vector<int64_t> vid, cnt, other;
         std::vector<uint8_t> dir, rep;
         std::vector<int32_t> w;
+        std::vector<int64_t> wv;         // wide weight keys: the 64-bit values
         int64_t ghost = 0, truncated = 0, skipped = 0;
         int rc = TGO_OK;
         std::string msg;
     };
+    const bool wide = opts->weight_key != 0 && wide_weight_dt(hp.weight_dt);
     const int64_t nrows = rows->nrows;
     const int nth = std::max(1, std::min<int>(threads, static_cast<int>((nrows + 1023) / 1024)));
     std::vector<Local> loc(nth);
@@ -240,6 +249,7 @@ int decode_rows(RowStaging& st, const tgo_rows* rows, const tgo_schema* schema,
                 L.other.push_back(is_partitioned_vertex(de.other, pb) ? canonical_vertex_id(de.other, pb) : de.other);
                 L.dir.push_back(static_cast<uint8_t>(de.dir));
                 L.w.push_back(opts->weight_key == 0 ? 1 : (de.has_weight ? de.weight : kMissingWeight));
+                if (wide) L.wv.push_back(de.has_weight ? de.weight64 : 0);
                 ++kept;
             }
             if (L.rc != TGO_OK) break;
@@ -260,7 +270,14 @@ int decode_rows(RowStaging& st, const tgo_rows* rows, const tgo_schema* schema,
         }
         st.other.insert(st.other.end(), L.other.begin(), L.other.end());
         st.dir.insert(st.dir.end(), L.dir.begin(), L.dir.end());
+        const size_t base = st.w.size();
         st.w.insert(st.w.end(), L.w.begin(), L.w.end());
+        if (wide) {                      // the column of a wide key: each entry's staged position
+            if (st.w.size() >= static_cast<size_t>(INT32_MAX)) { err = "wide weights: more than 2^31 - 1 staged entries"; return TGO_E_UNSUPPORTED; }
+            for (size_t i = base; i < st.w.size(); ++i)
+                if (st.w[i] != kMissingWeight) st.w[i] = static_cast<int32_t>(i);
+            st.wv.insert(st.wv.end(), L.wv.begin(), L.wv.end());
+        }
     }
     return TGO_OK;
 }
