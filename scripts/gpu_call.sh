@@ -1,11 +1,8 @@
 #!/bin/bash
-# Round-4 close, part A: the full GPU suite, smoke(), the one-GPU bench line.
+# Round-4 call o: Long / Double weight keys (generic tests), codec / rows / write-back tests.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
-T=r04z
-mkdir -p gpurun_out/$T
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 400 --timeout-method thread > gpurun_out/$T/gpu_tests.log 2>&1
-rc=$?; tail -2 gpurun_out/$T/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/$T/smoke.log 2>&1
-rc=$?; tail -2 gpurun_out/$T/smoke.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 500 python3 bench.py > gpurun_out/$T/bench.json 2> gpurun_out/$T/bench.err
-rc=$?; echo "bench exit $rc"; tail -2 gpurun_out/$T/bench.err; head -c 700 gpurun_out/$T/bench.json; echo; exit $rc
+mkdir -p gpurun_out/r04o
+timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu \
+    tests/test_gpu_generic.py tests/test_gpu_parity.py tests/test_gpu_rows.py tests/test_gpu_writeback.py \
+    > gpurun_out/r04o/tests.log 2>&1
+rc=$?; grep -E "passed|failed|FAILED|Error" gpurun_out/r04o/tests.log | tail -12; exit $rc
