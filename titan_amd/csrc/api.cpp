@@ -448,6 +448,8 @@ int upload_graph(tgo_ctx* ctx, HostGraph& h, bool allow_segments = true) {
     if (h.has_transpose) HIP_TRY(up(h.push_t, g.push_t));
     g.wval = nullptr;
     if (wide) {
+        const int64_t nv = h.d_wval.present() ? h.d_wval.n : static_cast<int64_t>(h.wval.size());
+        if (nv == 0 && (g.out.nnz > 0 || g.in.nnz > 0)) return fail(ctx, TGO_E_STATE, "wide weights: the value table is missing");
         if (h.d_wval.present()) adopt(ctx, g.wval, h.d_wval);
         else HIP_TRY(upload(ctx, g.wval, h.wval));
     }
@@ -1184,13 +1186,16 @@ int tgo_finish_load(tgo_ctx* ctx) {
     const bool cuts = stg.n_rep > 0 || std::any_of(stg.vid.begin(), stg.vid.end(), [](int64_t v) { return (v & 7) == 2; });
     const bool on_dev = dev_asm && !cuts;
     if (!on_dev) rc = staging_entries_to_host(ctx->staging, ctx->stream, err);
+    // a wide (Long / Double) weight key: the staged values become the graph's value table (taken
+    // before the assembly, which consumes the staging)
+    std::vector<int64_t> wval = std::move(ctx->staging.wv);
+    DevArray<int64_t> d_wval = std::move(ctx->staging.d_wv);
     if (!rc)
         rc = on_dev ? assemble_rows_device(ctx->staging, h, ctx->stream, err)
                     : assemble_from_rows(ctx->staging, h, threads_of(ctx), err);
     if (rc) { ctx->staging = RowStaging(); return fail(ctx, rc, err); }
-    // a wide (Long / Double) weight key: the staged values become the graph's value table
-    h.wval = std::move(ctx->staging.wv);
-    h.d_wval = std::move(ctx->staging.d_wv);
+    h.wval = std::move(wval);
+    h.d_wval = std::move(d_wval);
     if (env_i64("TGO_TRACE", 0))
         std::fprintf(stderr, "[tgo] finish_load decode + assembly (%s) %8.1f ms\n", on_dev ? "device" : "host",
                      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
