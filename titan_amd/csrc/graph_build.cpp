@@ -260,6 +260,7 @@ int decode_rows(RowStaging& st, const tgo_rows* rows, const tgo_schema* schema,
     });
     for (auto& L : loc) if (L.rc != TGO_OK) { err = L.msg; return L.rc; }
     if (int rc = staging_begin(st, opts, err)) return rc;
+    st.plan.weight_dt = hp.weight_dt;     // the assembly types the weight column from it (Float / Long / Double)
     for (auto& L : loc) {
         st.ghost += L.ghost; st.truncated += L.truncated; st.skipped += L.skipped;
         for (size_t i = 0; i < L.vid.size(); ++i) {
