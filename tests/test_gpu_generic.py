@@ -240,10 +240,14 @@ def float_weight_rows():
     return rows, vids, sd, osch, fkey, n
 
 
-def test_float_weights_in_generic_edge_functions():
+@pytest.mark.parametrize("host_decode", [False, True])
+def test_float_weights_in_generic_edge_functions(host_decode, monkeypatch):
     """A Float weight (FloatSerializer bits): generic fp64 edge functions read it widened to
     double, int64 messages are refused, and ShortestDistance (edge.<Integer>value) fails as
-    its ClassCastException does."""
+    its ClassCastException does — through the device and the host decoder (the host decoder
+    once left the column typed Integer)."""
+    if host_decode:
+        monkeypatch.setenv("TGO_HOST_DECODE", "1")
     rows, vids, sd, osch, fkey, n = float_weight_rows()
     eng = Engine().load_rows(rows, Schema.from_dict(sd), IN, weight_key=fkey)
     o = fr.OracleGraph.from_rows(rows, osch, IN, weight_key=fkey)
