@@ -29,13 +29,13 @@ from collections import defaultdict
 GROUPS = {
     # one rank update of the cache-blocked gather (spmv.hip): cold pass, fold, hot pass, long rows
     # (gather_hot_pf: the prefetching hot pass; gather_short_packed: its TGO_PR_PF=0 form)
-    "pagerank_update": ("cold_gather<", "cold_fold(", "gather_hot_pf(", "gather_short_packed<",
+    "pagerank_update": ("cold_gather<", "cold_fold(", "gather_hot_pf<", "gather_hot_pf(", "gather_short_packed<",
                         "gather_chunks<tgo::(anonymous namespace)::PackedOp",
                         "finalize_long<tgo::(anonymous namespace)::PackedOp"),
     # ms_pull is templated on its round-trip width (ms_pull<8>)
     "msbfs_sweep": ("ms_seed(", "ms_pull(", "ms_pull<", "ms_push(", "ms_settle(", "ms_queue(", "ms_fbitmap("),
 }
-UNIT_KERNEL = {"pagerank_update": ("gather_hot_pf(", "gather_short_packed<"), "msbfs_sweep": ("ms_seed(",)}
+UNIT_KERNEL = {"pagerank_update": ("gather_hot_pf<", "gather_hot_pf(", "gather_short_packed<"), "msbfs_sweep": ("ms_seed(",)}
 
 
 def load(d):

@@ -475,6 +475,12 @@ struct DsLoop {
                                 // piles cover the largest weight; the host then reruns unbinned)
     unsigned long long full_scans;        // extractions by the bitmap scan (large or overflowed piles)
     unsigned long long xfin;    // the decided extraction follows a finished bucket (members final)
+    // pull form of a large finished bucket's heavy entries (ds_pull_heavy)
+    unsigned long long xpull;   // this step pulls instead of queueing the members' heavy entries
+    unsigned long long pulls;   // pulls so far (pull j uses bitmap / list j & 1)
+    long long pbucket;          // the finished bucket of the current pull
+    unsigned long long pcount[2];         // members recorded per list
+    unsigned long long xprev;   // entries of the previous pull's list the extraction clears
     unsigned long long bc[kDsMaxBins];    // pile counts
 };
 
@@ -529,6 +535,8 @@ struct Scratch {
     int64_t ds_pile_cap = 0;
     int32_t* ds_mlist = nullptr;    // n: members of the current bucket
     uint64_t* ds_done = nullptr;    // words: members of finished buckets (final distances)
+    uint64_t* ds_pm[2] = {nullptr, nullptr};   // pull form: member bitmaps (words) and lists (n)
+    int32_t* ds_pl[2] = {nullptr, nullptr};
     // generic vertex programs (allocated on first use): row-order staging + internal-order vectors
     int64_t* gv[3] = {nullptr, nullptr, nullptr};
     uint8_t* gh[3] = {nullptr, nullptr, nullptr};
@@ -605,12 +613,23 @@ hipError_t k_ds_loop_seed(const DevCsr& ws, const int64_t* light, int64_t* dist,
 hipError_t k_ds_loop_step(const DevCsr& ws, const int64_t* light, uint64_t* pend, uint64_t* member, int64_t n,
                           int64_t* dist, int64_t* msg, int32_t* const q[2], int64_t* const qpre[2], DsLoop* L, int cur,
                           int64_t delta, hipStream_t s);
+// Pull form of the heavy entries of a finished bucket with >= min_members members: every
+// vertex that can still improve reads its pull list (view) for heavy entries from those members
+// (bitmap pm[j & 1], list pl[j & 1]) instead of the members pushing them.  min_members <= 0: off.
+struct DsPull {
+    View view{};
+    int64_t n_active = 0;
+    int64_t min_members = 0;
+    uint64_t* pm[2] = {nullptr, nullptr};
+    int32_t* pl[2] = {nullptr, nullptr};
+};
 // the binned form: nbins piles of cap entries (pile), member list mlist (n), done bitmap (words,
 // zeroed by the caller: members of finished buckets)
 hipError_t k_ds_loop_step_bins(const DevCsr& ws, const int64_t* light, uint64_t* pend, uint64_t* member, int64_t n,
                                int64_t* dist, int64_t* msg, int32_t* const q[2], int64_t* const qpre[2], DsLoop* L,
                                int cur, int64_t delta, int nbins, int32_t* pile, int64_t cap, int32_t* mlist,
-                               uint64_t* done, bool done_filter, int64_t scan_above, hipStream_t s);
+                               uint64_t* done, bool done_filter, int64_t scan_above, const DsPull& pull,
+                               hipStream_t s);
 hipError_t k_ds_pending_min(const uint64_t* pend, int64_t words, const int64_t* dist, Counters* cnt, hipStream_t s);
 hipError_t k_ds_extract(const View& push, uint64_t* pend, int64_t n, const int64_t* dist, int64_t thr, int32_t* qn,
                         int64_t* qdeg, Counters* cnt, hipStream_t s);
