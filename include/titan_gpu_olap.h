@@ -338,8 +338,11 @@ int  tgo_copy_multi_distances(tgo_ctx* ctx, int32_t source, int64_t* dist_out);
  * pull level of a run walks only the hot neighbours and a blocked pass over the cold entries
  * completes the open rows; 0 (default, or TGO_MS_COLD) = the plain walk; a value > 1 = on, with
  * that many hot neighbours and cold segments of that size (tests). */
+/* TGO_TUNE_DS_PULL (binned delta SSSP): a fraction f in (0, 1] = a finished bucket with at least
+ * f * n members has its heavy entries pulled by the vertices that can still improve instead of
+ * pushed; 0 = always pushed; -1 = TGO_DS_PULL (default 0).  Same distances either way. */
 enum { TGO_TUNE_MS_SPLIT = 1, TGO_TUNE_MS_GHOST = 2, TGO_TUNE_DS_BINS = 3, TGO_TUNE_DS_PILE_CAP = 4,
-       TGO_TUNE_DS_DONE = 5, TGO_TUNE_MS_COLD = 6 };
+       TGO_TUNE_DS_DONE = 5, TGO_TUNE_MS_COLD = 6, TGO_TUNE_DS_PULL = 7 };
 int  tgo_set_tuning(tgo_ctx* ctx, int32_t key, double value);
 
 /* ---- Tracing (the reference's only hook is FulgoraGraphComputer.java:143,307

@@ -2,7 +2,8 @@
 """Dev probe: RMAT-24 weighted inE delta SSSP (bench.py's configs[4] leg) on `nroots` roots that
 reach a quarter of the graph, one run each after a warm-up run, printing the loop counters
 (TGO_TRACE=1 adds the device loop's phase / bucket / extraction counts); SSSP_BINS=1,0 runs
-the binned and the bitmap-scan loop (TGO_TUNE_DS_BINS) and compares their distances.  Run it under
+the binned and the bitmap-scan loop (TGO_TUNE_DS_BINS), SSSP_PULL=0,0.01 the push and pull form
+of finished buckets' heavy entries (TGO_TUNE_DS_PULL), and compares their distances.  Run it under
 rocprofv3 --kernel-trace to split the time per kernel (scripts/ktrace.py).
 usage: sssp_once.py [scale] [nroots]"""
 import os
@@ -27,10 +28,12 @@ for r in roots:
         good.append(int(r))
     if len(good) == nroots:
         break
-modes = [int(x) for x in os.environ.get("SSSP_BINS", "1").split(",")]   # TGO_TUNE_DS_BINS values to run
+# TGO_TUNE_DS_BINS values to run, each with the TGO_TUNE_DS_PULL fractions of SSSP_PULL
+modes = [(int(x), float(p)) for x in os.environ.get("SSSP_BINS", "1").split(",")
+         for p in os.environ.get("SSSP_PULL", "0").split(",")]
 first = {}
-for b in modes:
-    eng.set_tuning(L.TUNE_DS_BINS, b)
+for b, p in modes:
+    eng.set_tuning(L.TUNE_DS_BINS, b).set_tuning(L.TUNE_DS_PULL, p)
     for r in good:
         eng.sssp(r, n, L.SCOPE_IN_E, mode=L.SSSP_DELTA, seed_is_dense=True, fetch=False)
         t0 = time.perf_counter()
@@ -38,7 +41,7 @@ for b in modes:
         ms = (time.perf_counter() - t0) * 1e3
         st = eng.stats()
         same = first.setdefault(r, d) is d or (first[r] == d).all()
-        print(f"bins={b} root {r}: {ms:.2f} ms (incl. fetch), kernel {st['last_kernel_ms']:.2f} ms, phases {st['levels']}, "
+        print(f"bins={b} pull={p} root {r}: {ms:.2f} ms (incl. fetch), kernel {st['last_kernel_ms']:.2f} ms, phases {st['levels']}, "
               f"relaxed {st['relaxed_entries']}, reached_entries {st['reached_entries']}, "
               f"GTEPS(kernel) {st['reached_entries'] / st['last_kernel_ms'] / 1e6:.2f}, equal_first_mode={bool(same)}",
               flush=True)

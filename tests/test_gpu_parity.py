@@ -303,15 +303,17 @@ def test_rmat_sssp_delta_equals_converged(rmat12, scope, delta):
 
 @pytest.mark.parametrize("scope", [OUT, IN])
 @pytest.mark.parametrize("delta", [0, 9, 37, 200])
-@pytest.mark.parametrize("bins,cap,done", [(1, 0, 0), (1, 0, 1), (1, 16, 1), (1, 1024, 0), (0, 0, 0)])
-def test_rmat_sssp_delta_piles(rmat12, scope, delta, bins, cap, done):
+@pytest.mark.parametrize("bins,cap,done,pull", [(1, 0, 0, 0), (1, 0, 1, 0), (1, 16, 1, 0), (1, 1024, 0, 0), (0, 0, 0, 0),
+                                                (1, 0, 0, 0.001), (1, 16, 1, 0.001), (1, 0, 1, 0.02)])
+def test_rmat_sssp_delta_piles(rmat12, scope, delta, bins, cap, done, pull):
     """The binned loop (next bucket extracted from its pile of improved vertices; with and
-    without the done-target filter), the same loop with piles so small that buckets overflow
-    into the bitmap scan, and the bitmap-scan loop all give the oracle's converged distances
-    bit for bit."""
+    without the done-target filter; finished buckets' heavy entries pushed or pulled), the same
+    loop with piles so small that buckets overflow into the bitmap scan, and the bitmap-scan
+    loop all give the oracle's converged distances bit for bit."""
     n, src, dst, w, ids, oracle, roots = rmat12
     eng = Engine().load_edges(n, src, dst, scope, weight=w)
     eng.set_tuning(L.TUNE_DS_BINS, bins).set_tuning(L.TUNE_DS_PILE_CAP, cap).set_tuning(L.TUNE_DS_DONE, done)
+    eng.set_tuning(L.TUNE_DS_PULL, pull)
     for r in roots[:3]:
         d = eng.sssp(int(r), n, scope, mode=L.SSSP_DELTA, seed_is_dense=True, stats=True, delta=delta)
         od, _ = oracle.shortest_distance(int(ids[r]), n, scope, weighted=True)
@@ -326,9 +328,11 @@ def test_rmat_sssp_delta_zero_weights(rmat12):
     off, mid, adj, ww = numpy_adjacency(n, src, dst, w0)
     oracle = fr.OracleGraph.from_adjacency(ids, off, mid, adj, ww)
     eng = Engine().load_edges(n, src, dst, OUT, weight=w0)
-    for r in roots[:2]:
-        d = eng.sssp(int(r), n, OUT, mode=L.SSSP_DELTA, seed_is_dense=True, delta=2)
-        assert np.array_equal(d, oracle.shortest_distance(int(ids[r]), n, OUT, weighted=True)[0])
+    for pull in (0, 0.001):
+        eng.set_tuning(L.TUNE_DS_PULL, pull)
+        for r in roots[:2]:
+            d = eng.sssp(int(r), n, OUT, mode=L.SSSP_DELTA, seed_is_dense=True, delta=2)
+            assert np.array_equal(d, oracle.shortest_distance(int(ids[r]), n, OUT, weighted=True)[0])
 
 
 def test_sssp_tree_delta():

@@ -76,6 +76,7 @@ struct tgo_ctx {
     int ds_bins = -1;           // tgo_set_tuning(TGO_TUNE_DS_BINS): 1 / 0; < 0: TGO_DS_BINS / on
     int64_t ds_pile_cap = 0;    // tgo_set_tuning(TGO_TUNE_DS_PILE_CAP): entries per pile; 0 = n
     int ds_done = -1;           // tgo_set_tuning(TGO_TUNE_DS_DONE): 1 / 0; < 0: TGO_DS_DONE / off
+    double ds_pull = -1;        // tgo_set_tuning(TGO_TUNE_DS_PULL): member fraction; < 0: TGO_DS_PULL / off
     int64_t ms_cold = -1;       // tgo_set_tuning(TGO_TUNE_MS_COLD): 0 off, 1 on, > 1 on with that
                                 // hot head (and segment); < 0: TGO_MS_COLD / on
     // state a native partitioned driver keeps between runs on this graph (part_driver.cpp:
@@ -797,6 +798,26 @@ int run_delta_device(tgo_ctx* ctx, int64_t seed, int64_t delta, bool force_scan)
         ctx->st.device_bytes = ctx->dev_bytes;
     }
     if (nbins) HIP_TRY(hipMemsetAsync(s.ds_done, 0, ((n + 63) / 64 + 1) * 8, st));
+    // Pull form (TGO_DS_PULL = members as a fraction of n, 0 = off): a finished bucket with at
+    // least that many members has its heavy entries pulled by the vertices that can still
+    // improve (delta_loop.hip ds_pull_heavy) instead of pushed entry by entry.
+    static const double pull_env = env_double("TGO_DS_PULL", 0.0);
+    const double pull_frac = ctx->ds_pull >= 0 ? ctx->ds_pull : pull_env;
+    DsPull pull{};
+    if (nbins && pull_frac > 0) {
+        const int64_t words = (n + 63) / 64 + 1;
+        for (int b = 0; b < 2; ++b) {
+            if (!s.ds_pm[b]) HIP_TRY(dev_alloc(ctx, s.ds_pm[b], words));
+            if (!s.ds_pl[b]) HIP_TRY(dev_alloc(ctx, s.ds_pl[b], n + 1));
+            HIP_TRY(hipMemsetAsync(s.ds_pm[b], 0, words * 8, st));
+            pull.pm[b] = s.ds_pm[b];
+            pull.pl[b] = s.ds_pl[b];
+        }
+        ctx->st.device_bytes = ctx->dev_bytes;
+        pull.view = pull_view(g, g.scope);
+        pull.n_active = g.n_active > 0 ? std::min<int64_t>(g.n_active, n) : n;
+        pull.min_members = std::max<int64_t>(1, static_cast<int64_t>(pull_frac * static_cast<double>(n)));
+    }
     HIP_TRY(k_ds_loop_seed(g.push_ws, s.ds_light, s.dist, s.ds_q[0], s.ds_qp[0], s.ds_loop, seed, delta, st));
     DsLoop h{};
     int cur = 0;
@@ -809,7 +830,7 @@ int run_delta_device(tgo_ctx* ctx, int64_t seed, int64_t delta, bool force_scan)
             if (nbins)
                 HIP_TRY(k_ds_loop_step_bins(g.push_ws, s.ds_light, s.vb, s.ds_member, n, s.dist, s.msg, s.ds_q, s.ds_qp,
                                             s.ds_loop, cur, delta, nbins, s.ds_pile, s.ds_pile_cap, s.ds_mlist,
-                                            s.ds_done, done_filter, scan_above, st));
+                                            s.ds_done, done_filter, scan_above, pull, st));
             else
                 HIP_TRY(k_ds_loop_step(g.push_ws, s.ds_light, s.vb, s.ds_member, n, s.dist, s.msg, s.ds_q, s.ds_qp,
                                        s.ds_loop, cur, delta, st));
@@ -1067,6 +1088,10 @@ int tgo_set_tuning(tgo_ctx* ctx, int32_t key, double value) {
     case TGO_TUNE_DS_DONE:
         if (value != 0.0 && value != 1.0 && value != -1.0) return fail(ctx, TGO_E_INVALID, "TGO_TUNE_DS_DONE: 0, 1 or -1");
         ctx->ds_done = static_cast<int>(value);
+        return TGO_OK;
+    case TGO_TUNE_DS_PULL:
+        if (!(value >= -1.0) || value > 1.0) return fail(ctx, TGO_E_INVALID, "TGO_TUNE_DS_PULL: a fraction in [0, 1] or -1");
+        ctx->ds_pull = value;
         return TGO_OK;
     case TGO_TUNE_MS_COLD:
         if (!(value >= -1.0) || value >= 2147483647.0 || value != static_cast<double>(static_cast<int64_t>(value)))

@@ -115,6 +115,11 @@ __global__ void ds_loop_seed(const int64_t* off, const int64_t* light, int64_t* 
     L->spill = 0;
     L->full_scans = 0;
     L->xfin = 0;
+    L->xpull = 0;
+    L->pulls = 0;
+    L->pbucket = 0;
+    L->pcount[0] = L->pcount[1] = 0;
+    L->xprev = 0;
 }
 
 __device__ __forceinline__ unsigned long long load_agent(const unsigned long long* p) {
@@ -152,10 +157,13 @@ __device__ void decide_next(DsLoop* L, int cur, int64_t delta) {
 // that pile is extracted in the same step; with no such pile only the heavy entries, and with
 // no members either the run is done.  A pile that dropped entries is extracted by the bitmap
 // scan instead (extract = 1: it takes every member from the member bitmap, none becomes done).
-__device__ void decide_bins(DsLoop* L, int cur, int64_t delta, int nbins, int64_t cap, int64_t scan_above) {
+__device__ void decide_bins(DsLoop* L, int cur, int64_t delta, int nbins, int64_t cap, int64_t scan_above,
+                            int64_t pull_min) {
     L->extract = 0;
+    L->xpull = 0;
     if (L->done || qcount(load_agent(&L->qc[cur])) != 0) return;
     long long k = L->bucket;
+    const long long kfin = k;
     int b = static_cast<int>(k % nbins);
     unsigned long long c = load_agent(&L->bc[b]);
     const bool finished = c == 0;
@@ -195,6 +203,16 @@ __device__ void decide_bins(DsLoop* L, int cur, int64_t delta, int nbins, int64_
             L->mcount = 0;                   // the scan takes every member from the bitmap
             L->full_scans += 1;
         }
+    }
+    // A large finished bucket pulls its heavy entries (ds_pull_heavy) instead of pushing them;
+    // its members go to pull list j & 1 and the previous pull's list is cleared on the way.
+    if (L->extract == 2 && pull_min > 0 && L->xm >= static_cast<unsigned long long>(pull_min)) {
+        const unsigned long long j = L->pulls;
+        L->xpull = 1;
+        L->pbucket = kfin;
+        L->xprev = L->pcount[(j + 1) & 1];
+        L->pcount[(j + 1) & 1] = 0;
+        L->pcount[j & 1] = L->xm;
     }
 }
 
@@ -289,7 +307,7 @@ __global__ void __launch_bounds__(kBlock) ds_extract_bins(const int64_t* __restr
         const int64_t* __restrict__ light, uint64_t* __restrict__ pend, uint64_t* __restrict__ member,
         const int64_t* __restrict__ dist, DsLoop* L, int cur, const int32_t* __restrict__ pile, int64_t cap,
         const int32_t* __restrict__ mlist, uint64_t* __restrict__ done, int32_t* __restrict__ qn,
-        int64_t* __restrict__ qpre, int64_t n) {
+        int64_t* __restrict__ qpre, int64_t n, DsPull pull) {
     const unsigned long long mode = L->extract;             // grid-uniform
     if (mode == 1) {                                         // a large or overflowed pile: the bitmap scan
         extract_scan(off, light, pend, member, n, dist, L, cur, qn, qpre, done);
@@ -297,7 +315,14 @@ __global__ void __launch_bounds__(kBlock) ds_extract_bins(const int64_t* __restr
     }
     if (mode != 2) return;
     const int64_t thr = L->thr;
-    const int64_t xc = static_cast<int64_t>(L->xcount), total = xc + static_cast<int64_t>(L->xm);
+    const bool xpull = L->xpull != 0;
+    const unsigned long long j = L->pulls;
+    uint64_t* __restrict__ pm = pull.pm[j & 1];
+    int32_t* __restrict__ pl_now = pull.pl[j & 1];
+    uint64_t* __restrict__ pm_prev = pull.pm[(j + 1) & 1];
+    const int32_t* __restrict__ pl_prev = pull.pl[(j + 1) & 1];
+    const int64_t xc = static_cast<int64_t>(L->xcount), xme = xc + static_cast<int64_t>(L->xm);
+    const int64_t total = xme + (xpull ? static_cast<int64_t>(L->xprev) : 0);
     const int32_t* __restrict__ pl = pile + (L->xbin >= 0 ? L->xbin : 0) * cap;
     for (int64_t base = static_cast<int64_t>(blockIdx.x) * kBlock; base < total;
          base += static_cast<int64_t>(gridDim.x) * kBlock) {                 // block-uniform trips
@@ -316,16 +341,23 @@ __global__ void __launch_bounds__(kBlock) ds_extract_bins(const int64_t* __restr
                     deg = light_deg(off, light, v);
                 }
             }
-        } else if (i < total) {                               // a finished bucket's member: final
+        } else if (i < xme) {                                 // a finished bucket's member: final
             const int32_t v = mlist[i - xc];
             member[v >> 6] = 0;
             atomicOr(reinterpret_cast<unsigned long long*>(&done[v >> 6]), 1ULL << (v & 63));
-            const int64_t hdeg = off[v + 1] - light[v];
-            if (hdeg > 0) {
-                take = true;
-                entry = static_cast<int32_t>(static_cast<uint32_t>(v) | kHeavy);
-                deg = hdeg;
+            if (xpull) {                                      // its heavy entries are pulled
+                atomicOr(reinterpret_cast<unsigned long long*>(&pm[v >> 6]), 1ULL << (v & 63));
+                pl_now[i - xc] = v;
+            } else {
+                const int64_t hdeg = off[v + 1] - light[v];
+                if (hdeg > 0) {
+                    take = true;
+                    entry = static_cast<int32_t>(static_cast<uint32_t>(v) | kHeavy);
+                    deg = hdeg;
+                }
             }
+        } else if (i < total) {                               // the previous pull's bitmap words
+            pm_prev[pl_prev[i - xme] >> 6] = 0;
         }
         int64_t slot, doff;
         block_reserve(&L->qc[cur], take ? 1 : 0, deg, slot, doff);
@@ -569,14 +601,120 @@ __global__ void __launch_bounds__(kBlock) ds_relax_dev(const int64_t* __restrict
     if (threadIdx.x == 0 && m != kInf) atomicMin(&L->tm, m);
 }
 
+// The pull form of a large finished bucket's heavy entries: a vertex that can still improve
+// (dist > (finished bucket + 1) * delta: every heavy candidate is at least that) reads its pull
+// list for heavy entries (w >= delta) from the bucket's members (bitmap pm) and takes the
+// minimum over msg[u] + w; an improvement is settled as the relax settles one (near queue below
+// the threshold when newly pending, else the pile of its bucket).  Same relaxations as the
+// members' push, so the same converged distances.
+__global__ void __launch_bounds__(kBlock) ds_pull_heavy(const int64_t* __restrict__ ws_off,
+        const int64_t* __restrict__ light, const int64_t* __restrict__ msg, int64_t* __restrict__ dist,
+        uint64_t* __restrict__ pend, int32_t* __restrict__ qn, int64_t* __restrict__ qpre_n, DsLoop* L, int cur,
+        int64_t delta, int nbins, int32_t* __restrict__ pile, int64_t cap, DsPull pull) {
+    if (!L->xpull) return;                                   // grid-uniform
+    const uint64_t* __restrict__ pm = pull.pm[L->pulls & 1];
+    const int64_t thr = L->thr, bucket = L->bucket;
+    const int64_t floor_c = (L->pbucket + 1) * delta;        // no heavy candidate is below this
+    const View& pv = pull.view;
+    __shared__ unsigned int s_bn[kDsMaxBins];
+    __shared__ unsigned long long s_bb[kDsMaxBins];
+    bool bad = false, spill = false;
+    for (int64_t base = static_cast<int64_t>(blockIdx.x) * kBlock; base < pull.n_active;
+         base += static_cast<int64_t>(gridDim.x) * kBlock) {                 // block-uniform trips
+        if (threadIdx.x < kDsMaxBins) s_bn[threadIdx.x] = 0;
+        __syncthreads();
+        const int64_t v = base + threadIdx.x;
+        long long best = kInf;
+        long long dv = kInf;
+        if (v < pull.n_active) {
+            dv = static_cast<long long>(dist[v]);
+            if (dv > floor_c) {
+                for (int l = 0; l < pv.nlists; ++l) {
+                    const int64_t* off = l == 0 ? pv.off0 : pv.off1;
+                    const int32_t* adj = l == 0 ? pv.adj0 : pv.adj1;
+                    const int32_t* wt = l == 0 ? pv.w0 : pv.w1;
+                    const int64_t e1 = off[v + 1];
+                    for (int64_t e = off[v]; e < e1; e += 4) {
+                        int32_t u[4], w[4];
+                        uint64_t mw[4];
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            u[q] = e + q < e1 ? adj[e + q] : -1;
+                            w[q] = e + q < e1 ? wt[e + q] : 0;
+                        }
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) mw[q] = u[q] >= 0 ? pm[u[q] >> 6] : 0ULL;
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            if (u[q] < 0 || !((mw[q] >> (u[q] & 63)) & 1ULL)) continue;
+                            if (w[q] == kMissingWeight) { bad = true; continue; }
+                            if (w[q] < delta) continue;               // light: relaxed in its bucket
+                            const long long c = static_cast<long long>(msg[u[q]] + static_cast<int64_t>(w[q]));
+                            best = c < best ? c : best;
+                        }
+                    }
+                }
+            }
+        }
+        int take = 0, fb = -1;
+        unsigned int fl = 0;
+        int64_t td = 0;
+        if (best < dv) {
+            const long long old = atomicMin(reinterpret_cast<long long*>(&dist[v]), best);
+            if (best < old) {
+                const uint64_t bit = 1ULL << (v & 63);
+                const unsigned long long ob = atomicOr(reinterpret_cast<unsigned long long*>(&pend[v >> 6]), bit);
+                if (!(ob & bit) && best < thr) {
+                    take = 1;
+                    td = light_deg(ws_off, light, v);
+                } else {
+                    const int64_t ahead = best / delta - bucket;
+                    if (ahead >= nbins || ahead < 0) {
+                        spill = true;
+                    } else {
+                        fb = static_cast<int>((bucket + ahead) % nbins);
+                        fl = atomicAdd(&s_bn[fb], 1u);
+                    }
+                }
+            }
+        }
+        int64_t slot, doff;
+        block_reserve(&L->qc[cur ^ 1], take, td, slot, doff);
+        if (take) {
+            qn[slot] = static_cast<int32_t>(v);
+            qpre_n[slot] = doff;
+        }
+        __syncthreads();
+        if (threadIdx.x < nbins) {
+            const unsigned int cnt = s_bn[threadIdx.x];
+            s_bb[threadIdx.x] = cnt ? atomicAdd(&L->bc[threadIdx.x], static_cast<unsigned long long>(cnt)) : 0ULL;
+            if (cnt && s_bb[threadIdx.x] + cnt > static_cast<unsigned long long>(cap))
+                atomicOr(&L->overflow, 1ULL << threadIdx.x);
+        }
+        __syncthreads();
+        if (fb >= 0) {
+            const unsigned long long sl = s_bb[fb] + fl;
+            if (sl < static_cast<unsigned long long>(cap)) pile[fb * cap + static_cast<int64_t>(sl)] = static_cast<int32_t>(v);
+        }
+        __syncthreads();
+    }
+    if (__ballot(bad) && lane() == 0) L->err = 1;
+    if (__ballot(spill) && lane() == 0) L->spill = 1;
+}
+
 // One thread, at the start of a step: the decision of decide_next.  (Folding it into the
 // relax's last block — a ticket counter — measured 13.3 -> 24.8 ms per source, most likely
 // the agent-scope fence every block issues before taking its ticket.)
 __global__ void ds_decide(DsLoop* L, int cur, int64_t delta) {
     if (threadIdx.x == 0 && blockIdx.x == 0) decide_next(L, cur, delta);
 }
-__global__ void ds_decide_bins(DsLoop* L, int cur, int64_t delta, int nbins, int64_t cap, int64_t scan_above) {
-    if (threadIdx.x == 0 && blockIdx.x == 0) decide_bins(L, cur, delta, nbins, cap, scan_above);
+__global__ void ds_decide_bins(DsLoop* L, int cur, int64_t delta, int nbins, int64_t cap, int64_t scan_above,
+                               int64_t pull_min) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) decide_bins(L, cur, delta, nbins, cap, scan_above, pull_min);
+}
+// After a pull step: the next pull uses the other bitmap / list.
+__global__ void ds_pull_flip(DsLoop* L) {
+    if (threadIdx.x == 0 && blockIdx.x == 0 && L->xpull) L->pulls += 1;
 }
 
 }  // namespace
@@ -606,13 +744,21 @@ hipError_t k_ds_loop_step(const DevCsr& ws, const int64_t* light, uint64_t* pend
 hipError_t k_ds_loop_step_bins(const DevCsr& ws, const int64_t* light, uint64_t* pend, uint64_t* member, int64_t n,
                                int64_t* dist, int64_t* msg, int32_t* const q[2], int64_t* const qpre[2], DsLoop* L,
                                int cur, int64_t delta, int nbins, int32_t* pile, int64_t cap, int32_t* mlist,
-                               uint64_t* done, bool done_filter, int64_t scan_above, hipStream_t s) {
+                               uint64_t* done, bool done_filter, int64_t scan_above, const DsPull& pull,
+                               hipStream_t s) {
     if (nbins < 2 || nbins > kDsMaxBins || nbins > kBlock || cap < 1) return hipErrorInvalidValue;
-    ds_decide_bins<<<1, 64, 0, s>>>(L, cur, delta, nbins, cap, scan_above);
+    const bool pulls = pull.min_members > 0 && pull.pm[0] && pull.pm[1] && pull.pl[0] && pull.pl[1];
+    if (pulls && pull.n_active > n) return hipErrorInvalidValue;
+    ds_decide_bins<<<1, 64, 0, s>>>(L, cur, delta, nbins, cap, scan_above, pulls ? pull.min_members : 0);
     const int64_t words = (n + 63) / 64;
     ds_extract_bins<<<extract_grid(words), kBlock, 0, s>>>(ws.off, light, pend, member, dist, L, cur, pile, cap, mlist,
-                                                           done, q[cur], qpre[cur], n);
+                                                           done, q[cur], qpre[cur], n, pull);
     ds_commit_dev<true><<<1024, kBlock, 0, s>>>(q[cur], dist, msg, pend, member, L, cur, mlist);
+    if (pulls) {
+        ds_pull_heavy<<<256 * 8, kBlock, 0, s>>>(ws.off, light, msg, dist, pend, q[cur ^ 1], qpre[cur ^ 1], L, cur, delta,
+                                                 nbins, pile, cap, pull);
+        ds_pull_flip<<<1, 64, 0, s>>>(L);
+    }
     ds_relax_dev<true><<<256 * 8, kBlock, 0, s>>>(ws.off, ws.adj, ws.w, light, q[cur], qpre[cur], msg, dist, pend,
                                                   q[cur ^ 1], qpre[cur ^ 1], L, cur, delta, nbins, pile, cap,
                                                   done_filter ? done : nullptr);
