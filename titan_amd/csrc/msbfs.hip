@@ -61,15 +61,14 @@ __device__ __forceinline__ void count_flush(Counters* cnt, unsigned long long nv
 // fr_rows: seeds at rows >= fr_rows (entry-less rows of a partitioned layout) are reached
 // but left out of the frontier mask — they have no entries to push or be pulled through,
 // and keeping them out leaves the masks' entry-less tail zero for the whole sweep.
+// One lane per seed (a single thread's 64 dependent read-modify-writes took 37 us).
 __global__ void ms_seed(const int64_t* __restrict__ seeds, int nseeds, uint64_t* vis, uint64_t* fr, int64_t fr_rows) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        for (int r = 0; r < nseeds; ++r) {
-            const int64_t s = seeds[r];
-            if (s < 0) continue;                 // partitioned: seed owned by another rank
-            vis[s] |= 1ULL << r;
-            if (s < fr_rows) fr[s] |= 1ULL << r;
-        }
-    }
+    const int r = static_cast<int>(threadIdx.x);
+    if (blockIdx.x != 0 || r >= nseeds) return;
+    const int64_t s = seeds[r];
+    if (s < 0) return;                           // partitioned: seed owned by another rank
+    atomicOr(reinterpret_cast<unsigned long long*>(&vis[s]), 1ULL << r);
+    if (s < fr_rows) atomicOr(reinterpret_cast<unsigned long long*>(&fr[s]), 1ULL << r);
 }
 
 // Pull level over the active vertices: OR the neighbours' frontier masks, stop as soon as
@@ -362,8 +361,10 @@ __global__ void __launch_bounds__(kBlock) ms_source_counts(const uint64_t* __res
 // Exact push entries per source of the frontier, for the sources in `cand`: one wave per
 // 64-vertex word; the lanes load their vertex's mask (and push degree when it is in the
 // frontier), the masks are transposed across the wave (as in ms_source_counts) so lane b holds
-// source b's column, and lane b adds the degrees of the column's set bits, fetched from their
-// lanes (one permute per set bit; a wave does max-column-popcount trips).
+// source b's column, and lane b adds the degrees of the column's set bits bit-sliced: with D_k
+// the ballot of bit k of the lanes' degrees, the column's sum is sum_k 2^k popcount(x & D_k) —
+// one ballot per degree bit instead of one permute per set bit (a word of hubs, each in every
+// source's frontier, took 64 permute trips: 158 us at RMAT-24's first pull level).
 __global__ void __launch_bounds__(kBlock) ms_source_entries(View push, const uint64_t* __restrict__ fr,
         int64_t n_active, uint64_t cand, unsigned long long* __restrict__ out) {
     __shared__ unsigned long long s_sum[kWavesPerBlock][64];
@@ -385,10 +386,12 @@ __global__ void __launch_bounds__(kBlock) ms_source_entries(View push, const uin
             const uint64_t y = __shfl_xor(x, j, 64);
             x = (lane() & j) ? (((y & ~m) >> j) | (x & ~m)) : ((x & m) | ((y & m) << j));
         }
-        while (__ballot(x != 0)) {                               // x: the vertices holding my source
-            const int src = x ? __ffsll(static_cast<long long>(x)) - 1 : lane();
-            const unsigned long long d = __shfl(deg, src, 64);
-            if (x) { sum += d; x &= x - 1; }
+        unsigned long long dor = deg;                             // the wave's highest degree bit
+        for (int off = 32; off > 0; off >>= 1) dor |= __shfl_xor(dor, off, 64);
+        const int kb = dor ? 64 - __clzll(static_cast<long long>(dor)) : 0;
+        for (int k = 0; k < kb; ++k) {                           // x: the vertices holding my source
+            const uint64_t dk = __ballot((deg >> k) & 1ULL);
+            sum += static_cast<unsigned long long>(__popcll(x & dk)) << k;
         }
     }
     s_sum[threadIdx.x >> 6][lane()] = sum;
@@ -412,20 +415,115 @@ __global__ void __launch_bounds__(kBlock) ms_fbitmap(const uint64_t* __restrict_
     }
 }
 
-// Push level: edge-balanced over the frontier queue (exclusive scan of degrees in qpre).
+// Push level: edge-balanced over the frontier queue (exclusive scan of degrees in qpre).  A
+// tile's queue slice (entry, scan offset, list bounds, mask) is staged in LDS once, and each
+// thread's kEdgesPerThread edges go through the dependent chain in stages — owning entry,
+// neighbour index, the neighbour's masks, the atomic — so every stage's loads are in flight
+// together (one edge at a time left each thread waiting out index -> masks -> atomic per edge:
+// 463 us for the 12.7 M entries of RMAT-24's second level).  The staged slice holds 512
+// entries (18 KB of LDS, eight blocks a CU); a tile touching more (low-degree frontiers)
+// searches the global scan instead.
+constexpr int kPushLds = 514;
 __global__ void __launch_bounds__(kBlock) ms_push(View push, const int32_t* __restrict__ q,
         const int64_t* __restrict__ qpre, int64_t qlen, const uint64_t* __restrict__ fr,
         const uint64_t* __restrict__ vis, uint64_t* __restrict__ nx, PackTouch touch, uint64_t mask) {
-    for_each_queue_edge(q, qpre, qlen, [&](bool valid, int32_t u, int64_t o) {
-        if (!valid) return;
-        const int32_t v = view_entry(push, u, o);
-        // partitioned graphs pass vis = nullptr: remote vertices' masks are not local
-        const uint64_t m = (vis ? (fr[u] & ~vis[v]) : fr[u]) & mask;
-        if (m && (nx[v] & m) != m) {
-            atomicOr(reinterpret_cast<unsigned long long*>(&nx[v]), m);
-            if (touch.flag) touch.flag[(v / touch.n_local) * touch.cps + (v % touch.n_local) / kPackChunk] = 1;
+    __shared__ int64_t s_pre[kPushLds];
+    __shared__ int64_t s_b0[kPushLds];     // list 0 begin
+    __shared__ int64_t s_b1[kPushLds];     // list 1 begin minus list 0's length (o >= d0 reads adj1[s_b1 + o])
+    __shared__ int32_t s_d0[kPushLds];     // list 0 length
+    __shared__ uint64_t s_m[kPushLds];
+    __shared__ int64_t s_lo, s_hi;
+    const int64_t total = qpre[qlen];
+    const int64_t ntiles = (total + kTileEdges - 1) / kTileEdges;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t t0 = tile * kTileEdges;
+        const int64_t t1 = min(total, t0 + kTileEdges);
+        if (threadIdx.x == 0) {
+            int64_t a = 0, b = qlen;
+            while (b - a > 1) { const int64_t c = (a + b) >> 1; if (qpre[c] <= t0) a = c; else b = c; }
+            s_lo = a;
+            int64_t a2 = a, b2 = qlen;
+            while (b2 - a2 > 1) { const int64_t c = (a2 + b2) >> 1; if (qpre[c] <= t1 - 1) a2 = c; else b2 = c; }
+            s_hi = a2;
         }
-    });
+        __syncthreads();
+        const int64_t lo = s_lo, hi = s_hi;
+        const int64_t span = hi - lo + 1;
+        const bool in_lds = span + 1 <= kPushLds;             // block-uniform
+        if (in_lds) {
+            for (int64_t i = threadIdx.x; i <= span; i += kBlock) {
+                s_pre[i] = qpre[lo + i];
+                if (i < span) {
+                    const int32_t u = q[lo + i];
+                    const int64_t b0 = push.off0[u];
+                    const int64_t d0 = push.off0[u + 1] - b0;
+                    s_b0[i] = b0;
+                    s_d0[i] = static_cast<int32_t>(min<int64_t>(d0, INT32_MAX));
+                    s_b1[i] = push.nlists > 1 ? push.off1[u] - d0 : 0;
+                    s_m[i] = fr[u] & mask;
+                }
+            }
+        }
+        __syncthreads();
+        int32_t v[kEdgesPerThread];
+        uint64_t m[kEdgesPerThread];
+        if (in_lds) {
+            int64_t ia[kEdgesPerThread], o[kEdgesPerThread];
+#pragma unroll
+            for (int k = 0; k < kEdgesPerThread; ++k) {       // 1: owning entry (LDS search)
+                const int64_t j = t0 + k * kBlock + threadIdx.x;
+                ia[k] = -1;
+                o[k] = 0;
+                if (j >= t1) continue;
+                int64_t a = 0, b = span;
+                while (b - a > 1) { const int64_t c = (a + b) >> 1; if (s_pre[c] <= j) a = c; else b = c; }
+                ia[k] = a;
+                o[k] = j - s_pre[a];
+            }
+#pragma unroll
+            for (int k = 0; k < kEdgesPerThread; ++k) {       // 2: neighbour index
+                v[k] = -1;
+                m[k] = 0;
+                if (ia[k] < 0) continue;
+                m[k] = s_m[ia[k]];
+                if (!m[k]) continue;
+                v[k] = o[k] < s_d0[ia[k]] ? push.adj0[s_b0[ia[k]] + o[k]] : push.adj1[s_b1[ia[k]] + o[k]];
+            }
+        } else {                                              // a huge slice: global search
+#pragma unroll
+            for (int k = 0; k < kEdgesPerThread; ++k) {
+                const int64_t j = t0 + k * kBlock + threadIdx.x;
+                v[k] = -1;
+                m[k] = 0;
+                if (j >= t1) continue;
+                int64_t a = lo, b = hi + 1;
+                while (b - a > 1) { const int64_t c = (a + b) >> 1; if (qpre[c] <= j) a = c; else b = c; }
+                const int32_t u = q[a];
+                m[k] = fr[u] & mask;
+                if (m[k]) v[k] = view_entry(push, u, j - qpre[a]);
+            }
+        }
+        uint64_t cv[kEdgesPerThread], cn[kEdgesPerThread];
+#pragma unroll
+        for (int k = 0; k < kEdgesPerThread; ++k) {           // 3: the neighbour's masks
+            cv[k] = 0;
+            cn[k] = 0;
+            if (v[k] < 0) continue;
+            // partitioned graphs pass vis = nullptr: remote vertices' masks are not local
+            if (vis) cv[k] = vis[v[k]];
+            cn[k] = nx[v[k]];
+        }
+#pragma unroll
+        for (int k = 0; k < kEdgesPerThread; ++k) {           // 4: the atomic
+            if (v[k] < 0) continue;
+            const uint64_t mk = m[k] & ~cv[k];
+            if (mk && (cn[k] & mk) != mk) {
+                atomicOr(reinterpret_cast<unsigned long long*>(&nx[v[k]]), mk);
+                if (touch.flag) touch.flag[(v[k] / touch.n_local) * touch.cps + (v[k] % touch.n_local) / kPackChunk] = 1;
+            }
+        }
+        __syncthreads();
+    }
 }
 
 // After a push level: settle the candidates (nx & ~vis), record levels, build the queue
