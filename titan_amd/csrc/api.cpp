@@ -1496,6 +1496,9 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
     const double split_frac = tgo::ms_split_of(ctx);
     int64_t qlen = static_cast<int64_t>(uniq.size());
     int64_t mf = 0;
+    int64_t reached = qlen;     // vertices reached by any source so far
+    static const double push_light = env_double("TGO_MS_PUSH_LIGHT", 1.0 / 16.0);
+    static const bool push_probe = env_double("TGO_MS_PUSH_PROBE", 1.0) != 0.0;
     {
         std::vector<int64_t> d(qlen);
         HIP_TRY(hipMemcpyAsync(d.data(), s.qdeg, qlen * sizeof(int64_t), hipMemcpyDeviceToHost, st));
@@ -1599,12 +1602,19 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
             // candidates only land on rows with entries (< n_active); the tail is never read
             HIP_TRY(hipMemsetAsync(nx, 0, g.n_active * 8, st));
             if ((rc = scan_frontier(ctx, qlen))) return rc;
-            HIP_TRY(k_ms_push(push, s.q[cur], s.qpre, qlen, fr, s.ms_vis, nx, st));
+            // While few vertices are reached the push skips the reached-mask read of its
+            // targets (ms_settle drops the reached bits anyway): one random 8-byte read less
+            // per entry at the second level's 12.7 M entries (RMAT-24).  TGO_MS_PUSH_PROBE=0
+            // also drops the read of the candidate mask before the atomic there.
+            const bool light = static_cast<double>(reached) < push_light * static_cast<double>(n);
+            HIP_TRY(k_ms_push(push, s.q[cur], s.qpre, qlen, fr, light ? nullptr : s.ms_vis, nx, st, PackTouch{}, ~0ULL,
+                              light ? push_probe : true));
             HIP_TRY(k_ms_settle(push, g.n_active, s.ms_vis, nx, ms_planes(ctx), s.q[cur ^ 1], s.qdeg, s.cnt, L + 1, st));
         }
         if ((rc = read_counters(ctx))) return rc;
         qlen = static_cast<int64_t>(s.hcnt->qlen);
         mf = static_cast<int64_t>(s.hcnt->mf);
+        reached += qlen;
         if (trace) std::fprintf(stderr, "[tgo] ms level %d %s -> %lld vertices, %lld entries, %llu source-bits\n", L,
                                 use_pull ? "pull" : "push", (long long)qlen, (long long)mf, s.hcnt->red[0]);
         static const bool diag = env_double("TGO_MS_DIAG", 0.0) != 0.0;

@@ -675,7 +675,8 @@ hipError_t k_ms_queue(const View& push, int64_t n_active, const uint64_t* fr, in
 // chunk (v % n_local) / kPackChunk of the owner's cps) so the pack skips untouched chunks.
 struct PackTouch { uint8_t* flag = nullptr; int64_t n_local = 1; int64_t cps = 1; };
 hipError_t k_ms_push(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen, const uint64_t* fr,
-                     const uint64_t* vis, uint64_t* nx, hipStream_t s, PackTouch touch = {}, uint64_t mask = ~0ULL);
+                     const uint64_t* vis, uint64_t* nx, hipStream_t s, PackTouch touch = {}, uint64_t mask = ~0ULL,
+                     bool probe = true);
 hipError_t k_ms_settle(const View& push, int64_t n_active, uint64_t* vis, uint64_t* nx, LevelPlanes lvl, int32_t* qn,
                        int64_t* qdeg, Counters* cnt, int32_t next_level, hipStream_t s);
 hipError_t k_ms_reach(const View& v, const uint64_t* vis, int64_t n_active, int nsrc, unsigned long long* reached,

@@ -371,11 +371,24 @@ __global__ void __launch_bounds__(kBlock) ms_source_entries(View push, const uin
     const int64_t words = (n_active + 63) >> 6;
     unsigned long long sum = 0;
     const int64_t nw = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
-    for (int64_t wd = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6; wd < words; wd += nw) {
-        const int64_t v = (wd << 6) + lane();
-        const uint64_t mine = v < n_active ? (fr[v] & cand) : 0;
+    for (int64_t w0 = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6; w0 < words; w0 += 4 * nw) {
+      uint64_t mw[4];
+      unsigned long long dw[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {                              // four words' loads in flight
+          const int64_t v = ((w0 + u * nw) << 6) + lane();
+          mw[u] = (w0 + u * nw < words && v < n_active) ? (fr[v] & cand) : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+          const int64_t v = ((w0 + u * nw) << 6) + lane();
+          dw[u] = mw[u] ? static_cast<unsigned long long>(push_degree(push, v)) : 0ULL;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint64_t mine = mw[u];
         if (!__ballot(mine != 0)) continue;                      // wave-uniform
-        const unsigned long long deg = mine ? static_cast<unsigned long long>(push_degree(push, v)) : 0ULL;
+        const unsigned long long deg = dw[u];
         uint64_t x = mine;
         constexpr uint64_t kLow[6] = {0x00000000FFFFFFFFULL, 0x0000FFFF0000FFFFULL, 0x00FF00FF00FF00FFULL,
                                       0x0F0F0F0F0F0F0F0FULL, 0x3333333333333333ULL, 0x5555555555555555ULL};
@@ -393,6 +406,7 @@ __global__ void __launch_bounds__(kBlock) ms_source_entries(View push, const uin
             const uint64_t dk = __ballot((deg >> k) & 1ULL);
             sum += static_cast<unsigned long long>(__popcll(x & dk)) << k;
         }
+      }
     }
     s_sum[threadIdx.x >> 6][lane()] = sum;
     __syncthreads();
@@ -426,7 +440,7 @@ __global__ void __launch_bounds__(kBlock) ms_fbitmap(const uint64_t* __restrict_
 constexpr int kPushLds = 514;
 __global__ void __launch_bounds__(kBlock) ms_push(View push, const int32_t* __restrict__ q,
         const int64_t* __restrict__ qpre, int64_t qlen, const uint64_t* __restrict__ fr,
-        const uint64_t* __restrict__ vis, uint64_t* __restrict__ nx, PackTouch touch, uint64_t mask) {
+        const uint64_t* __restrict__ vis, uint64_t* __restrict__ nx, PackTouch touch, uint64_t mask, bool probe) {
     __shared__ int64_t s_pre[kPushLds];
     __shared__ int64_t s_b0[kPushLds];     // list 0 begin
     __shared__ int64_t s_b1[kPushLds];     // list 1 begin minus list 0's length (o >= d0 reads adj1[s_b1 + o])
@@ -511,7 +525,7 @@ __global__ void __launch_bounds__(kBlock) ms_push(View push, const int32_t* __re
             if (v[k] < 0) continue;
             // partitioned graphs pass vis = nullptr: remote vertices' masks are not local
             if (vis) cv[k] = vis[v[k]];
-            cn[k] = nx[v[k]];
+            if (probe) cn[k] = nx[v[k]];
         }
 #pragma unroll
         for (int k = 0; k < kEdgesPerThread; ++k) {           // 4: the atomic
@@ -839,8 +853,8 @@ hipError_t k_ms_queue(const View& push, int64_t n_active, const uint64_t* fr, in
     return hipGetLastError();
 }
 hipError_t k_ms_push(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen, const uint64_t* fr,
-                     const uint64_t* vis, uint64_t* nx, hipStream_t s, PackTouch touch, uint64_t mask) {
-    ms_push<<<256 * 8, kBlock, 0, s>>>(push, q, qpre, qlen, fr, vis, nx, touch, mask);
+                     const uint64_t* vis, uint64_t* nx, hipStream_t s, PackTouch touch, uint64_t mask, bool probe) {
+    ms_push<<<256 * 8, kBlock, 0, s>>>(push, q, qpre, qlen, fr, vis, nx, touch, mask, probe);
     return hipGetLastError();
 }
 hipError_t k_ms_settle(const View& push, int64_t n_active, uint64_t* vis, uint64_t* nx, LevelPlanes lvl, int32_t* qn,
