@@ -234,6 +234,39 @@ def test_multi_source_split_budget_is_policy_only(rmat12, split):
         eng.set_tuning(99, 0.0)
 
 
+_SRCENT_CHECK = """
+import sys
+from titan_amd import Engine, pick_roots, rmat_edges
+from titan_amd import _lib as L
+n = 1 << 14
+src, dst, _ = rmat_edges(14, 16, seed=5)
+for scope in (L.SCOPE_BOTH_E, L.SCOPE_IN_E, L.SCOPE_OUT_E):
+    eng = Engine().load_edges(n, src, dst, scope, apply_cap=False)
+    for split in (-1.0, 0.3, 1.0):
+        eng.set_tuning(L.TUNE_MS_SPLIT, split)
+        for seed in (3, 4):
+            eng.bfs_multi(pick_roots(n, src, dst, 64, seed=seed), n, scope, seed_is_dense=True, fetch=False)
+print("ok")
+"""
+
+
+def test_multi_source_settle_source_entries_match():
+    """The source split after a push level reads the per-source push entries that level's
+    settle summed (bit-sliced over the fresh masks); TGO_MS_SRCENT_CHECK=1 recomputes them with
+    ms_source_entries at every such split and fails the sweep on any difference.  (The split only
+    picks the plan, so the parity tests alone would not see wrong sums.)"""
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ, TGO_MS_SRCENT_CHECK="1", TGO_TRACE="1")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, "-c", _SRCENT_CHECK], cwd=root, env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert p.stdout.strip().endswith("ok")
+    assert "settle per-source entries checked" in p.stderr
+
+
 @pytest.mark.parametrize("scope", [BOTH, IN, OUT])
 @pytest.mark.parametrize("cold,split", [(0, -1.0), (1, -1.0), (300, -1.0), (300, 0.0), (1000, 0.3), (64, 1.0)])
 def test_multi_source_cold_split_level(rmat12, scope, cold, split):

@@ -1497,6 +1497,7 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
     int64_t qlen = static_cast<int64_t>(uniq.size());
     int64_t mf = 0;
     int64_t reached = qlen;     // vertices reached by any source so far
+    bool srcent_ready = false;  // ms_srcent holds the current frontier's push entries per source
     static const double push_light = env_double("TGO_MS_PUSH_LIGHT", 1.0 / 16.0);
     static const bool push_probe = env_double("TGO_MS_PUSH_PROBE", 1.0) != 0.0;
     {
@@ -1535,7 +1536,19 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
             uint64_t sparse = 0;
             if (split_frac > 0.0 && !prev_pull) {
                 // every source's exact push entries in one pass, then the smallest within the budget
-                HIP_TRY(k_ms_source_entries(push, fr, g.n_active, full, s.ms_srcent, st));
+                // after a push level its settle summed them already (srcent_ready)
+                if (!srcent_ready) HIP_TRY(k_ms_source_entries(push, fr, g.n_active, full, s.ms_srcent, st));
+                static const bool srcent_check = env_double("TGO_MS_SRCENT_CHECK", 0.0) != 0.0;
+                if (srcent_ready && srcent_check) {     // dev check: the settle's sums = a pass of their own
+                    HIP_TRY(k_ms_source_entries(push, fr, g.n_active, full, s.ms_stat, st));
+                    unsigned long long x[2][TGO_MAX_SOURCES];
+                    HIP_TRY(hipMemcpyAsync(x[0], s.ms_srcent, sizeof(x[0]), hipMemcpyDeviceToHost, st));
+                    HIP_TRY(hipMemcpyAsync(x[1], s.ms_stat, sizeof(x[1]), hipMemcpyDeviceToHost, st));
+                    HIP_TRY(hipStreamSynchronize(st));
+                    if (std::memcmp(x[0], x[1], sizeof(x[0])) != 0)
+                        return fail(ctx, TGO_E_HIP, "multi-source BFS: settle per-source entries differ from ms_source_entries");
+                    if (trace) std::fprintf(stderr, "[tgo] ms level %d: settle per-source entries checked\n", L);
+                }
                 unsigned long long se[TGO_MAX_SOURCES];
                 HIP_TRY(hipMemcpyAsync(se, s.ms_srcent, sizeof(se), hipMemcpyDeviceToHost, st));
                 HIP_TRY(hipStreamSynchronize(st));
@@ -1609,8 +1622,12 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
             const bool light = static_cast<double>(reached) < push_light * static_cast<double>(n);
             HIP_TRY(k_ms_push(push, s.q[cur], s.qpre, qlen, fr, light ? nullptr : s.ms_vis, nx, st, PackTouch{}, ~0ULL,
                               light ? push_probe : true));
-            HIP_TRY(k_ms_settle(push, g.n_active, s.ms_vis, nx, ms_planes(ctx), s.q[cur ^ 1], s.qdeg, s.cnt, L + 1, st));
+            // the new frontier's push entries per source, for the next level's split
+            if (split_frac > 0.0) HIP_TRY(hipMemsetAsync(s.ms_srcent, 0, 64 * sizeof(unsigned long long), st));
+            HIP_TRY(k_ms_settle(push, g.n_active, s.ms_vis, nx, ms_planes(ctx), s.q[cur ^ 1], s.qdeg, s.cnt, L + 1, st,
+                                split_frac > 0.0 ? s.ms_srcent : nullptr));
         }
+        srcent_ready = !use_pull && split_frac > 0.0;
         if ((rc = read_counters(ctx))) return rc;
         qlen = static_cast<int64_t>(s.hcnt->qlen);
         mf = static_cast<int64_t>(s.hcnt->mf);

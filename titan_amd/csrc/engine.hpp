@@ -678,7 +678,8 @@ hipError_t k_ms_push(const View& push, const int32_t* q, const int64_t* qpre, in
                      const uint64_t* vis, uint64_t* nx, hipStream_t s, PackTouch touch = {}, uint64_t mask = ~0ULL,
                      bool probe = true);
 hipError_t k_ms_settle(const View& push, int64_t n_active, uint64_t* vis, uint64_t* nx, LevelPlanes lvl, int32_t* qn,
-                       int64_t* qdeg, Counters* cnt, int32_t next_level, hipStream_t s);
+                       int64_t* qdeg, Counters* cnt, int32_t next_level, hipStream_t s,
+                       unsigned long long* srcent = nullptr);
 hipError_t k_ms_reach(const View& v, const uint64_t* vis, int64_t n_active, int nsrc, unsigned long long* reached,
                       unsigned long long* entries, hipStream_t s);
 hipError_t k_ms_extract(LevelPlanes lvl, int nplanes, const uint64_t* vis, const int32_t* perm, int r, int64_t* dist,

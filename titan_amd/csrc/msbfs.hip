@@ -358,6 +358,41 @@ __global__ void __launch_bounds__(kBlock) ms_source_counts(const uint64_t* __res
     }
 }
 
+// Wave-wide (all lanes call it): lane b adds the degrees of the lanes whose mask holds bit b.
+// The masks are transposed across the wave (as in ms_source_counts) so lane b holds source b's
+// column x, and with D_k the ballot of bit k of the lanes' degrees the column's sum is
+// sum_k 2^k popcount(x & D_k).
+__device__ __forceinline__ void source_columns_add(uint64_t mine, unsigned long long deg, unsigned long long& sum) {
+    uint64_t x = mine;
+    constexpr uint64_t kLow[6] = {0x00000000FFFFFFFFULL, 0x0000FFFF0000FFFFULL, 0x00FF00FF00FF00FFULL,
+                                  0x0F0F0F0F0F0F0F0FULL, 0x3333333333333333ULL, 0x5555555555555555ULL};
+#pragma unroll
+    for (int st = 0; st < 6; ++st) {
+        const int j = 32 >> st;
+        const uint64_t m = kLow[st];
+        const uint64_t y = __shfl_xor(x, j, 64);
+        x = (lane() & j) ? (((y & ~m) >> j) | (x & ~m)) : ((x & m) | ((y & m) << j));
+    }
+    unsigned long long dor = deg;                                // the wave's highest degree bit
+    for (int off = 32; off > 0; off >>= 1) dor |= __shfl_xor(dor, off, 64);
+    const int kb = dor ? 64 - __clzll(static_cast<long long>(dor)) : 0;
+    for (int k = 0; k < kb; ++k) {
+        const uint64_t dk = __ballot((deg >> k) & 1ULL);
+        sum += static_cast<unsigned long long>(__popcll(x & dk)) << k;
+    }
+}
+// Block end of a per-source sum: the block's lanes b added into out[b] with one atomic each.
+__device__ __forceinline__ void source_sums_flush(unsigned long long sum, unsigned long long* __restrict__ out) {
+    __shared__ unsigned long long s_sum[kWavesPerBlock][64];
+    s_sum[threadIdx.x >> 6][lane()] = sum;
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        unsigned long long t = 0;
+        for (int w = 0; w < kWavesPerBlock; ++w) t += s_sum[w][threadIdx.x];
+        if (t) atomicAdd(&out[threadIdx.x], t);
+    }
+}
+
 // Exact push entries per source of the frontier, for the sources in `cand`: one wave per
 // 64-vertex word; the lanes load their vertex's mask (and push degree when it is in the
 // frontier), the masks are transposed across the wave (as in ms_source_counts) so lane b holds
@@ -367,7 +402,6 @@ __global__ void __launch_bounds__(kBlock) ms_source_counts(const uint64_t* __res
 // source's frontier, took 64 permute trips: 158 us at RMAT-24's first pull level).
 __global__ void __launch_bounds__(kBlock) ms_source_entries(View push, const uint64_t* __restrict__ fr,
         int64_t n_active, uint64_t cand, unsigned long long* __restrict__ out) {
-    __shared__ unsigned long long s_sum[kWavesPerBlock][64];
     const int64_t words = (n_active + 63) >> 6;
     unsigned long long sum = 0;
     const int64_t nw = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
@@ -388,33 +422,10 @@ __global__ void __launch_bounds__(kBlock) ms_source_entries(View push, const uin
       for (int u = 0; u < 4; ++u) {
         const uint64_t mine = mw[u];
         if (!__ballot(mine != 0)) continue;                      // wave-uniform
-        const unsigned long long deg = dw[u];
-        uint64_t x = mine;
-        constexpr uint64_t kLow[6] = {0x00000000FFFFFFFFULL, 0x0000FFFF0000FFFFULL, 0x00FF00FF00FF00FFULL,
-                                      0x0F0F0F0F0F0F0F0FULL, 0x3333333333333333ULL, 0x5555555555555555ULL};
-#pragma unroll
-        for (int st = 0; st < 6; ++st) {
-            const int j = 32 >> st;
-            const uint64_t m = kLow[st];
-            const uint64_t y = __shfl_xor(x, j, 64);
-            x = (lane() & j) ? (((y & ~m) >> j) | (x & ~m)) : ((x & m) | ((y & m) << j));
-        }
-        unsigned long long dor = deg;                             // the wave's highest degree bit
-        for (int off = 32; off > 0; off >>= 1) dor |= __shfl_xor(dor, off, 64);
-        const int kb = dor ? 64 - __clzll(static_cast<long long>(dor)) : 0;
-        for (int k = 0; k < kb; ++k) {                           // x: the vertices holding my source
-            const uint64_t dk = __ballot((deg >> k) & 1ULL);
-            sum += static_cast<unsigned long long>(__popcll(x & dk)) << k;
-        }
+        source_columns_add(mine, dw[u], sum);
       }
     }
-    s_sum[threadIdx.x >> 6][lane()] = sum;
-    __syncthreads();
-    if (threadIdx.x < 64) {
-        unsigned long long t = 0;
-        for (int w = 0; w < kWavesPerBlock; ++w) t += s_sum[w][threadIdx.x];
-        if (t) atomicAdd(&out[threadIdx.x], t);
-    }
+    source_sums_flush(sum, out);
 }
 
 // Frontier bitmap of a pull level: one wave per 64-vertex word, a ballot of fr != 0.
@@ -542,10 +553,13 @@ __global__ void __launch_bounds__(kBlock) ms_push(View push, const int32_t* __re
 
 // After a push level: settle the candidates (nx & ~vis), record levels, build the queue
 // (two-pass chunked extraction, frontier.hpp).
+// srcent (optional): the new frontier's push entries per source added in (the next level's
+// source split reads them instead of a pass of its own, ms_source_entries).
 __global__ void __launch_bounds__(kBlock) ms_settle(View push, int64_t n_active, uint64_t* __restrict__ vis,
         uint64_t* __restrict__ nx, LevelPlanes lvl, int32_t* __restrict__ qn,
-        int64_t* __restrict__ qdeg, Counters* cnt, int32_t next_level) {
+        int64_t* __restrict__ qdeg, Counters* cnt, int32_t next_level, unsigned long long* __restrict__ srcent) {
     const int64_t words = (n_active + 63) >> 6;
+    unsigned long long ssum = 0;
     auto probe = [&](int64_t wd, Take* t, bool commit) -> bool {
         const int64_t v = (wd << 6) + lane();
         uint64_t fresh = 0, c = 0;
@@ -561,9 +575,12 @@ __global__ void __launch_bounds__(kBlock) ms_settle(View push, int64_t n_active,
             }
         }
         t[0] = {fresh != 0, static_cast<int32_t>(v), fresh ? push_degree(push, v) : 0};
+        // the probe runs wave-uniformly; the commit pass visits each word once
+        if (commit && srcent && __ballot(fresh != 0)) source_columns_add(fresh, static_cast<unsigned long long>(t[0].deg), ssum);
         return __ballot(c != 0) != 0;                           // words with candidates are rewritten
     };
     chunk_extract<1>(words, probe, qn, qdeg, cnt);
+    if (srcent) source_sums_flush(ssum, srcent);                 // grid-uniform
 }
 
 // The queue of a frontier produced by a pull level (which only counts): every active v with
@@ -858,9 +875,9 @@ hipError_t k_ms_push(const View& push, const int32_t* q, const int64_t* qpre, in
     return hipGetLastError();
 }
 hipError_t k_ms_settle(const View& push, int64_t n_active, uint64_t* vis, uint64_t* nx, LevelPlanes lvl, int32_t* qn,
-                       int64_t* qdeg, Counters* cnt, int32_t next_level, hipStream_t s) {
+                       int64_t* qdeg, Counters* cnt, int32_t next_level, hipStream_t s, unsigned long long* srcent) {
     ms_settle<<<extract_grid((n_active + 63) / 64), kBlock, 0, s>>>(push, n_active, vis, nx, lvl, qn, qdeg, cnt,
-                                                                    next_level);
+                                                                    next_level, srcent);
     return hipGetLastError();
 }
 hipError_t k_ms_reach(const View& v, const uint64_t* vis, int64_t n_active, int nsrc, unsigned long long* reached,
