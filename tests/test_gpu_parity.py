@@ -234,37 +234,47 @@ def test_multi_source_split_budget_is_policy_only(rmat12, split):
         eng.set_tuning(99, 0.0)
 
 
-_SRCENT_CHECK = """
-import sys
+_MS_SWEEPS = """
+import hashlib
 from titan_amd import Engine, pick_roots, rmat_edges
 from titan_amd import _lib as L
 n = 1 << 14
 src, dst, _ = rmat_edges(14, 16, seed=5)
+h = hashlib.sha256()
 for scope in (L.SCOPE_BOTH_E, L.SCOPE_IN_E, L.SCOPE_OUT_E):
     eng = Engine().load_edges(n, src, dst, scope, apply_cap=False)
     for split in (-1.0, 0.3, 1.0):
         eng.set_tuning(L.TUNE_MS_SPLIT, split)
         for seed in (3, 4):
-            eng.bfs_multi(pick_roots(n, src, dst, 64, seed=seed), n, scope, seed_is_dense=True, fetch=False)
-print("ok")
+            d = eng.bfs_multi(pick_roots(n, src, dst, 64, seed=seed), n, scope, seed_is_dense=True)
+            h.update(d.tobytes())
+print(h.hexdigest())
 """
 
 
-def test_multi_source_settle_source_entries_match():
-    """The source split after a push level reads the per-source push entries that level's
-    settle summed (bit-sliced over the fresh masks); TGO_MS_SRCENT_CHECK=1 recomputes them with
-    ms_source_entries at every such split and fails the sweep on any difference.  (The split only
-    picks the plan, so the parity tests alone would not see wrong sums.)"""
+def _ms_sweeps(**env):
     import os
     import subprocess
     import sys
-    env = dict(os.environ, TGO_MS_SRCENT_CHECK="1", TGO_TRACE="1")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    p = subprocess.run([sys.executable, "-c", _SRCENT_CHECK], cwd=root, env=env, capture_output=True, text=True,
-                       timeout=240)
+    p = subprocess.run([sys.executable, "-c", _MS_SWEEPS], cwd=root, env=dict(os.environ, TGO_TRACE="1", **env),
+                       capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, p.stderr[-2000:]
-    assert p.stdout.strip().endswith("ok")
-    assert "settle per-source entries checked" in p.stderr
+    return p.stdout.strip().splitlines()[-1], p.stderr
+
+
+def test_multi_source_settle_sums_and_ranged_push():
+    """Two sweep-plan paths the parity tests alone would not pin, in fresh processes (their
+    switches are read once per process): (1) the source split after a push level reads the
+    per-source push entries that level's settle summed (bit-sliced over the fresh masks);
+    TGO_MS_SRCENT_CHECK=1 recomputes them with ms_source_entries at every such split and fails the
+    sweep on any difference; (2) the target-ranged push (TGO_MS_PUSH_RANGE = log2 of the range,
+    here 256-vertex ranges for every push level) gives the same levels as the queue-order push."""
+    plain, _ = _ms_sweeps(TGO_MS_PUSH_RANGE="0")
+    checked, err = _ms_sweeps(TGO_MS_PUSH_RANGE="0", TGO_MS_SRCENT_CHECK="1")
+    assert "settle per-source entries checked" in err
+    ranged, _ = _ms_sweeps(TGO_MS_PUSH_RANGE="8", TGO_MS_PUSH_RANGE_MIN="1", TGO_MS_SRCENT_CHECK="1")
+    assert plain == checked == ranged
 
 
 @pytest.mark.parametrize("scope", [BOTH, IN, OUT])

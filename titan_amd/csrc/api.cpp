@@ -1500,6 +1500,8 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
     bool srcent_ready = false;  // ms_srcent holds the current frontier's push entries per source
     static const double push_light = env_double("TGO_MS_PUSH_LIGHT", 1.0 / 16.0);
     static const bool push_probe = env_double("TGO_MS_PUSH_PROBE", 1.0) != 0.0;
+    static const int push_range_log2 = static_cast<int>(env_double("TGO_MS_PUSH_RANGE", 18.0));
+    static const int64_t push_range_min = static_cast<int64_t>(env_double("TGO_MS_PUSH_RANGE_MIN", 1048576.0));
     {
         std::vector<int64_t> d(qlen);
         HIP_TRY(hipMemcpyAsync(d.data(), s.qdeg, qlen * sizeof(int64_t), hipMemcpyDeviceToHost, st));
@@ -1614,6 +1616,20 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
         } else {
             // candidates only land on rows with entries (< n_active); the tail is never read
             HIP_TRY(hipMemsetAsync(nx, 0, g.n_active * 8, st));
+            // A small frontier of long lists pushes target-ranged (k_ms_push_ranged: XCD x on
+            // the x-th eighth of the (target range, entry) enumeration, its ranges' masks in
+            // its L2); TGO_MS_PUSH_RANGE = log2 of the range (0 = off).
+            const int64_t rng = static_cast<int64_t>(1) << std::min(40, std::max(0, push_range_log2));
+            const int64_t nr = (g.n_active + rng - 1) / rng;
+            const bool ranged = push_range_log2 > 0 && mf >= push_range_min && nr > 1 &&
+                                (nr + 1) * qlen <= kMsRangePairs && nr * qlen + 1 <= n + 2;
+            if (ranged) {
+                for (int b = 0; b < 2; ++b)
+                    if (!s.ms_rp[b]) HIP_TRY(dev_alloc(ctx, s.ms_rp[b], kMsRangePairs));
+                const bool light = static_cast<double>(reached) < push_light * static_cast<double>(n);
+                HIP_TRY(k_ms_push_ranged(push, s.q[cur], qlen, g.n_active, rng, s.ms_rp[0], s.ms_rp[1], s.qdeg, s.qpre,
+                                         s.cub_tmp, s.cub_bytes, fr, light ? nullptr : s.ms_vis, nx, st));
+            } else {
             if ((rc = scan_frontier(ctx, qlen))) return rc;
             // While few vertices are reached the push skips the reached-mask read of its
             // targets (ms_settle drops the reached bits anyway): one random 8-byte read less
@@ -1622,6 +1638,7 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
             const bool light = static_cast<double>(reached) < push_light * static_cast<double>(n);
             HIP_TRY(k_ms_push(push, s.q[cur], s.qpre, qlen, fr, light ? nullptr : s.ms_vis, nx, st, PackTouch{}, ~0ULL,
                               light ? push_probe : true));
+            }
             // the new frontier's push entries per source, for the next level's split
             if (split_frac > 0.0) HIP_TRY(hipMemsetAsync(s.ms_srcent, 0, 64 * sizeof(unsigned long long), st));
             HIP_TRY(k_ms_settle(push, g.n_active, s.ms_vis, nx, ms_planes(ctx), s.q[cur ^ 1], s.qdeg, s.cnt, L + 1, st,

@@ -511,6 +511,7 @@ struct Scratch {
     uint64_t* ms_vis = nullptr;     // n: reached-by mask
     uint64_t* ms_fbm = nullptr;     // n/64: frontier bitmap of a pull level (fr != 0)
     unsigned long long* ms_srcent = nullptr;   // 64: per-source frontier sizes of a pull level
+    int64_t* ms_rp[2] = {nullptr, nullptr};    // ranged push: list bounds per (entry, range), kMsRangePairs each
     uint64_t* ms_fr = nullptr;      // n: frontier mask
     uint64_t* ms_nx = nullptr;      // n: next-frontier mask
     uint64_t* ms_lvl = nullptr;     // kLevelPlanes x n: bit r of plane k = bit k of source r's level
@@ -677,6 +678,12 @@ struct PackTouch { uint8_t* flag = nullptr; int64_t n_local = 1; int64_t cps = 1
 hipError_t k_ms_push(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen, const uint64_t* fr,
                      const uint64_t* vis, uint64_t* nx, hipStream_t s, PackTouch touch = {}, uint64_t mask = ~0ULL,
                      bool probe = true);
+constexpr int64_t kMsRangePairs = int64_t(1) << 22;   // ranged push: (entry, range) bounds per list
+// Target-ranged push of a small frontier (msbfs.hip): pairs (range of S targets, entry) in
+// range-major order, XCD x on the x-th eighth; P0 / P1 hold qlen * (R + 1), cnt / pre R * qlen + 1.
+hipError_t k_ms_push_ranged(const View& push, const int32_t* q, int64_t qlen, int64_t n_active, int64_t S,
+                            int64_t* P0, int64_t* P1, int64_t* cnt, int64_t* pre, void*& tmp, size_t& tmp_bytes,
+                            const uint64_t* fr, const uint64_t* vis, uint64_t* nx, hipStream_t s, uint64_t mask = ~0ULL);
 hipError_t k_ms_settle(const View& push, int64_t n_active, uint64_t* vis, uint64_t* nx, LevelPlanes lvl, int32_t* qn,
                        int64_t* qdeg, Counters* cnt, int32_t next_level, hipStream_t s,
                        unsigned long long* srcent = nullptr);

@@ -551,6 +551,132 @@ __global__ void __launch_bounds__(kBlock) ms_push(View push, const int32_t* __re
     }
 }
 
+// Target-ranged push (a small frontier of long lists, e.g. RMAT-24's second level: 1355
+// vertices, 12.7 M entries): the targets are cut into ranges of S vertices, and the edges are
+// enumerated range-major — (range r, frontier entry i) pairs, each the run of entry i's sorted
+// lists that lands in range r.  XCD x walks the x-th eighth of that enumeration in order with
+// its blocks as one window, so the candidate / reached masks of the ranges it is on stay in its
+// L2 and the atomics hit there (in queue order every XCD touched the whole 134 MB mask array).
+// P0 / P1 [i * (R + 1) + r]: the first position of entry i's list 0 / 1 with target >= r * S.
+__global__ void ms_range_bounds(View push, const int32_t* __restrict__ q, int64_t qlen, int64_t R, int64_t S,
+                                int64_t* __restrict__ P0, int64_t* __restrict__ P1) {
+    const int64_t R1 = R + 1;
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < qlen * R1; t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = t / R1, r = t - i * R1;
+        const int32_t u = q[i];
+        const int64_t key = r * S;
+#pragma unroll
+        for (int l = 0; l < 2; ++l) {
+            if (l == 1 && push.nlists < 2) { P1[t] = 0; break; }
+            const int64_t* off = l == 0 ? push.off0 : push.off1;
+            const int32_t* adj = l == 0 ? push.adj0 : push.adj1;
+            int64_t a = off[u], b = off[u + 1];             // first position with adj >= key
+            if (r == R) a = b;
+            while (a < b) { const int64_t c = (a + b) >> 1; if (static_cast<int64_t>(adj[c]) < key) a = c + 1; else b = c; }
+            (l == 0 ? P0 : P1)[t] = a;
+        }
+    }
+}
+// cnt[r * qlen + i] = entries of pair (r, i); cnt[R * qlen] = 0 (for the exclusive scan)
+__global__ void ms_range_counts(View push, int64_t qlen, int64_t R, const int64_t* __restrict__ P0,
+                                const int64_t* __restrict__ P1, int64_t* __restrict__ cnt) {
+    const int64_t R1 = R + 1;
+    for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p <= R * qlen; p += (int64_t)gridDim.x * blockDim.x) {
+        if (p == R * qlen) { cnt[p] = 0; continue; }
+        const int64_t r = p / qlen, i = p - r * qlen;
+        const int64_t t = i * R1 + r;
+        int64_t c = P0[t + 1] - P0[t];
+        if (push.nlists > 1) c += P1[t + 1] - P1[t];
+        cnt[p] = c;
+    }
+}
+__global__ void __launch_bounds__(kBlock) ms_push_ranged(View push, const int32_t* __restrict__ q, int64_t qlen,
+        int64_t R, const int64_t* __restrict__ P0, const int64_t* __restrict__ P1, const int64_t* __restrict__ pre,
+        const uint64_t* __restrict__ fr, const uint64_t* __restrict__ vis, uint64_t* __restrict__ nx, uint64_t mask) {
+    __shared__ int64_t s_pre[kPushLds];
+    __shared__ int64_t s_b0[kPushLds];
+    __shared__ int64_t s_b1[kPushLds];
+    __shared__ int32_t s_d0[kPushLds];
+    __shared__ uint64_t s_m[kPushLds];
+    __shared__ int64_t s_lo, s_hi;
+    const int64_t npairs = R * qlen, R1 = R + 1;
+    const int64_t total = pre[npairs];
+    const int64_t ntiles = (total + kTileEdges - 1) / kTileEdges;
+    const int64_t x = blockIdx.x & 7, per = gridDim.x >> 3;       // grid: a multiple of 8
+    const int64_t tlo = ntiles * x / 8, thi = ntiles * (x + 1) / 8;
+    // the pair's list bounds and mask (pair p = r * qlen + i)
+    auto pair_info = [&](int64_t p, int64_t& b0, int32_t& d0, int64_t& b1, uint64_t& m) {
+        const int64_t r = p / qlen, i = p - r * qlen;
+        const int64_t t = i * R1 + r;
+        b0 = P0[t];
+        const int64_t c0 = P0[t + 1] - b0;
+        d0 = static_cast<int32_t>(c0);
+        b1 = push.nlists > 1 ? P1[t] - c0 : 0;
+        m = fr[q[i]] & mask;
+    };
+    for (int64_t tile = tlo + (blockIdx.x >> 3); tile < thi; tile += per) {   // block-uniform trips
+        const int64_t t0 = tile * kTileEdges;
+        const int64_t t1 = min(total, t0 + kTileEdges);
+        if (threadIdx.x == 0) {
+            int64_t a = 0, b = npairs;
+            while (b - a > 1) { const int64_t c = (a + b) >> 1; if (pre[c] <= t0) a = c; else b = c; }
+            s_lo = a;
+            int64_t a2 = a, b2 = npairs;
+            while (b2 - a2 > 1) { const int64_t c = (a2 + b2) >> 1; if (pre[c] <= t1 - 1) a2 = c; else b2 = c; }
+            s_hi = a2;
+        }
+        __syncthreads();
+        const int64_t lo = s_lo, hi = s_hi;
+        const int64_t span = hi - lo + 1;
+        const bool in_lds = span + 1 <= kPushLds;              // block-uniform
+        if (in_lds)
+            for (int64_t i = threadIdx.x; i <= span; i += kBlock) {
+                s_pre[i] = pre[lo + i];
+                if (i < span) pair_info(lo + i, s_b0[i], s_d0[i], s_b1[i], s_m[i]);
+            }
+        __syncthreads();
+        int32_t v[kEdgesPerThread];
+        uint64_t m[kEdgesPerThread];
+#pragma unroll
+        for (int k = 0; k < kEdgesPerThread; ++k) {            // owning pair, neighbour index
+            const int64_t j = t0 + k * kBlock + threadIdx.x;
+            v[k] = -1;
+            m[k] = 0;
+            if (j >= t1) continue;
+            int64_t b0, b1, o;
+            int32_t d0;
+            if (in_lds) {
+                int64_t a = 0, b = span;
+                while (b - a > 1) { const int64_t c = (a + b) >> 1; if (s_pre[c] <= j) a = c; else b = c; }
+                b0 = s_b0[a]; d0 = s_d0[a]; b1 = s_b1[a]; m[k] = s_m[a];
+                o = j - s_pre[a];
+            } else {
+                int64_t a = lo, b = hi + 1;
+                while (b - a > 1) { const int64_t c = (a + b) >> 1; if (pre[c] <= j) a = c; else b = c; }
+                pair_info(a, b0, d0, b1, m[k]);
+                o = j - pre[a];
+            }
+            if (m[k]) v[k] = o < d0 ? push.adj0[b0 + o] : push.adj1[b1 + o];
+        }
+        uint64_t cv[kEdgesPerThread], cn[kEdgesPerThread];
+#pragma unroll
+        for (int k = 0; k < kEdgesPerThread; ++k) {            // the neighbour's masks
+            cv[k] = 0;
+            cn[k] = 0;
+            if (v[k] < 0) continue;
+            if (vis) cv[k] = vis[v[k]];
+            cn[k] = nx[v[k]];
+        }
+#pragma unroll
+        for (int k = 0; k < kEdgesPerThread; ++k) {            // the atomic
+            if (v[k] < 0) continue;
+            const uint64_t mk = m[k] & ~cv[k];
+            if (mk && (cn[k] & mk) != mk) atomicOr(reinterpret_cast<unsigned long long*>(&nx[v[k]]), mk);
+        }
+        __syncthreads();
+    }
+}
+
 // After a push level: settle the candidates (nx & ~vis), record levels, build the queue
 // (two-pass chunked extraction, frontier.hpp).
 // srcent (optional): the new frontier's push entries per source added in (the next level's
@@ -872,6 +998,19 @@ hipError_t k_ms_queue(const View& push, int64_t n_active, const uint64_t* fr, in
 hipError_t k_ms_push(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen, const uint64_t* fr,
                      const uint64_t* vis, uint64_t* nx, hipStream_t s, PackTouch touch, uint64_t mask, bool probe) {
     ms_push<<<256 * 8, kBlock, 0, s>>>(push, q, qpre, qlen, fr, vis, nx, touch, mask, probe);
+    return hipGetLastError();
+}
+hipError_t k_ms_push_ranged(const View& push, const int32_t* q, int64_t qlen, int64_t n_active, int64_t S,
+                            int64_t* P0, int64_t* P1, int64_t* cnt, int64_t* pre, void*& tmp, size_t& tmp_bytes,
+                            const uint64_t* fr, const uint64_t* vis, uint64_t* nx, hipStream_t s, uint64_t mask) {
+    if (S < 1 || qlen < 1) return hipErrorInvalidValue;
+    const int64_t R = (n_active + S - 1) / S;
+    if (R < 1) return hipErrorInvalidValue;
+    ms_range_bounds<<<grid_for(qlen * (R + 1), 2048), kBlock, 0, s>>>(push, q, qlen, R, S, P0, P1);
+    ms_range_counts<<<grid_for(R * qlen + 1, 2048), kBlock, 0, s>>>(push, qlen, R, P0, P1, cnt);
+    hipError_t e = scan_exclusive_i64(tmp, tmp_bytes, cnt, pre, R * qlen + 1, s);
+    if (e != hipSuccess) return e;
+    ms_push_ranged<<<256 * 8, kBlock, 0, s>>>(push, q, qlen, R, P0, P1, pre, fr, vis, nx, mask);
     return hipGetLastError();
 }
 hipError_t k_ms_settle(const View& push, int64_t n_active, uint64_t* vis, uint64_t* nx, LevelPlanes lvl, int32_t* qn,
