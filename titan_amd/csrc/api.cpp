@@ -1500,7 +1500,8 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
     bool srcent_ready = false;  // ms_srcent holds the current frontier's push entries per source
     static const double push_light = env_double("TGO_MS_PUSH_LIGHT", 1.0 / 16.0);
     static const bool push_probe = env_double("TGO_MS_PUSH_PROBE", 1.0) != 0.0;
-    static const int push_range_log2 = static_cast<int>(env_double("TGO_MS_PUSH_RANGE", 18.0));
+    // measured slower at RMAT-24 (second level 446 -> 561 us, profiles/r04t_ms_push_ab.log): off
+    static const int push_range_log2 = static_cast<int>(env_double("TGO_MS_PUSH_RANGE", 0.0));
     static const int64_t push_range_min = static_cast<int64_t>(env_double("TGO_MS_PUSH_RANGE_MIN", 1048576.0));
     {
         std::vector<int64_t> d(qlen);
@@ -1526,6 +1527,7 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
         queued = !use_pull;
         const bool prev_pull = pulled;
         pulled = use_pull;
+        bool sums = false;          // this push level's settle sums the per-source entries
         if (use_pull) {
             // Split the sources: the pull's walk of a vertex stops once every open source is
             // covered, and one source whose frontier never reaches the vertex (a source far
@@ -1639,12 +1641,15 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
             HIP_TRY(k_ms_push(push, s.q[cur], s.qpre, qlen, fr, light ? nullptr : s.ms_vis, nx, st, PackTouch{}, ~0ULL,
                               light ? push_probe : true));
             }
-            // the new frontier's push entries per source, for the next level's split
-            if (split_frac > 0.0) HIP_TRY(hipMemsetAsync(s.ms_srcent, 0, 64 * sizeof(unsigned long long), st));
+            // the new frontier's push entries per source, for the next level's split — when that
+            // level may pull (this frontier's entries within 64x of the pull threshold; a
+            // frontier grows at most ~40x a level on RMAT-24), else the split computes them
+            sums = split_frac > 0.0 && static_cast<double>(mf) * ms_alpha * 64.0 > static_cast<double>(total);
+            if (sums) HIP_TRY(hipMemsetAsync(s.ms_srcent, 0, 64 * sizeof(unsigned long long), st));
             HIP_TRY(k_ms_settle(push, g.n_active, s.ms_vis, nx, ms_planes(ctx), s.q[cur ^ 1], s.qdeg, s.cnt, L + 1, st,
-                                split_frac > 0.0 ? s.ms_srcent : nullptr));
+                                sums ? s.ms_srcent : nullptr));
         }
-        srcent_ready = !use_pull && split_frac > 0.0;
+        srcent_ready = !use_pull && sums;
         if ((rc = read_counters(ctx))) return rc;
         qlen = static_cast<int64_t>(s.hcnt->qlen);
         mf = static_cast<int64_t>(s.hcnt->mf);
