@@ -1523,12 +1523,12 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
             HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
             HIP_TRY(k_ms_queue(push, g.n_active, fr, s.q[cur], s.qdeg, s.cnt, st));
         }
-        HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
         queued = !use_pull;
         const bool prev_pull = pulled;
         pulled = use_pull;
         bool sums = false;          // this push level's settle sums the per-source entries
         if (use_pull) {
+            HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
             // Split the sources: the pull's walk of a vertex stops once every open source is
             // covered, and one source whose frontier never reaches the vertex (a source far
             // from it, or one whose sweep is over) makes every walk scan its whole list.  The
@@ -1617,7 +1617,9 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
             }
         } else {
             // candidates only land on rows with entries (< n_active); the tail is never read
-            HIP_TRY(hipMemsetAsync(nx, 0, g.n_active * 8, st));
+            // one kernel zeroes the counters, the candidate masks and the scan's tail entry
+            // (three fills of ~5 us launch each before)
+            HIP_TRY(k_level_prep(s.cnt, nx, g.n_active, s.qdeg + qlen, st));
             // A small frontier of long lists pushes target-ranged (k_ms_push_ranged: XCD x on
             // the x-th eighth of the (target range, entry) enumeration, its ranges' masks in
             // its L2); TGO_MS_PUSH_RANGE = log2 of the range (0 = off).
@@ -1632,7 +1634,7 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
                 HIP_TRY(k_ms_push_ranged(push, s.q[cur], qlen, g.n_active, rng, s.ms_rp[0], s.ms_rp[1], s.qdeg, s.qpre,
                                          s.cub_tmp, s.cub_bytes, fr, light ? nullptr : s.ms_vis, nx, st));
             } else {
-            if ((rc = scan_frontier(ctx, qlen))) return rc;
+            HIP_TRY(scan_exclusive_i64(s.cub_tmp, s.cub_bytes, s.qdeg, s.qpre, qlen + 1, st));   // tail zeroed above
             // While few vertices are reached the push skips the reached-mask read of its
             // targets (ms_settle drops the reached bits anyway): one random 8-byte read less
             // per entry at the second level's 12.7 M entries (RMAT-24).  TGO_MS_PUSH_PROBE=0
