@@ -1,15 +1,17 @@
 #!/bin/bash
-# Settle sums only ahead of a possible pull level, ranged push off: parity of the sweep paths,
-# the sweep A/B, and the bench line.
+# Fused push-level prep (sweep A/B), and one delta-SSSP run kernel by kernel.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
-T=r04u
+T=r04v
 mkdir -p gpurun_out/$T
 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_parity.py \
-    tests/test_gpu_distributed.py tests/test_gpu_fullsize.py -k "multi or msbfs or config3" > gpurun_out/$T/parity.log 2>&1
-rc=$?; tail -3 gpurun_out/$T/parity.log; [ $rc -eq 0 ] || exit $rc
+    -k "multi" > gpurun_out/$T/parity.log 2>&1
+rc=$?; tail -2 gpurun_out/$T/parity.log; [ $rc -eq 0 ] || exit $rc
 for i in 1 2; do
     timeout -k 10 300 python3 scripts/ms_probe.py 24 5 > gpurun_out/$T/ab.tmp 2>&1
     rc=$?; tail -1 gpurun_out/$T/ab.tmp | tee -a gpurun_out/$T/ab.log; [ $rc -eq 0 ] || exit $rc
 done
-timeout -k 10 600 python3 bench.py > gpurun_out/$T/bench.json 2> gpurun_out/$T/bench.err
-rc=$?; cat gpurun_out/$T/bench.json; exit $rc
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/$T/kt -o ss -- \
+    python3 scripts/sssp_once.py 24 1 > gpurun_out/$T/sssp.log 2>&1
+rc=$?; tail -2 gpurun_out/$T/sssp.log; [ $rc -eq 0 ] || exit $rc
+python3 scripts/ktimeline.py gpurun_out/$T/kt ds_loop_seed > gpurun_out/$T/sssp_timeline.txt
+rc=$?; rm -rf gpurun_out/$T/kt; tail -14 gpurun_out/$T/sssp_timeline.txt; exit $rc
