@@ -624,6 +624,24 @@ int wait_publish(tgo_ctx* ctx, unsigned long long seq) {
     return TGO_OK;
 }
 
+// wait_publish for a publish that later ones may have overwritten: spin until the sequence
+// word reaches seq (the words then hold that publish or a later one).
+int wait_publish_at_least(tgo_ctx* ctx, unsigned long long seq) {
+    Scratch& s = ctx->sc;
+    const volatile unsigned long long* flag = reinterpret_cast<volatile unsigned long long*>(s.hcnt) + kCounterWords;
+    for (uint64_t it = 1;; ++it) {
+        if (*flag >= seq) break;
+        if ((it & 0x3FFF) == 0) {
+            const hipError_t q = hipStreamQuery(ctx->stream);
+            if (q != hipSuccess && q != hipErrorNotReady) return fail(ctx, TGO_E_HIP, hipGetErrorString(q));
+            if (q == hipSuccess && *flag < seq) return fail(ctx, TGO_E_HIP, "loop state publish not visible after the stream drained");
+        }
+        __builtin_ia32_pause();
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    return TGO_OK;
+}
+
 // Exclusive scan of qdeg[0..qlen) into qpre[0..qlen] (qpre[qlen] = total).
 int scan_frontier(tgo_ctx* ctx, int64_t qlen) {
     Scratch& s = ctx->sc;
@@ -824,7 +842,44 @@ int run_delta_device(tgo_ctx* ctx, int64_t seed, int64_t delta, bool force_scan)
     // every step either relaxes a non-empty queue or extracts (at most one extraction in a row
     // takes nothing); a run needs far fewer than 4n + 64 steps — the bound only stops a bug
     const int64_t max_steps = 4 * n + 64;
-    for (int64_t steps = 0;;) {
+    // Pipelined stop checks (TGO_DS_PIPE, default on): each batch ends with a publish of the
+    // stop flags to host-mapped words, and the host checks batch k while batch k + 1 runs (a
+    // batch after the stop only runs steps that find nothing to do).  The stream no longer
+    // drains at every check: one SSSP run had ~12 drains of ~60 us (profiles/r04v_sssp_timeline.txt).
+    static const bool pipe = env_double("TGO_DS_PIPE", 1.0) != 0.0;
+    if (pipe) {
+        unsigned long long pending = 0;                       // publish to check next (0: none)
+        bool stop = false;
+        for (int64_t steps = 0; !stop;) {
+            DevSpan span(st, "sssp.delta_steps", {"first_step", steps}, {"steps", batch});
+            for (int k = 0; k < batch; ++k) {
+                if (nbins)
+                    HIP_TRY(k_ds_loop_step_bins(g.push_ws, s.ds_light, s.vb, s.ds_member, n, s.dist, s.msg, s.ds_q,
+                                                s.ds_qp, s.ds_loop, cur, delta, nbins, s.ds_pile, s.ds_pile_cap,
+                                                s.ds_mlist, s.ds_done, done_filter, scan_above, pull, st));
+                else
+                    HIP_TRY(k_ds_loop_step(g.push_ws, s.ds_light, s.vb, s.ds_member, n, s.dist, s.msg, s.ds_q, s.ds_qp,
+                                           s.ds_loop, cur, delta, st));
+                cur ^= 1;
+            }
+            steps += batch;
+            span.end();
+            const unsigned long long seq = ++s.pub_seq;
+            HIP_TRY(k_ds_publish(s.ds_loop, s.hcnt_dev, seq, st));
+            if (pending) {
+                if (int rc = wait_publish_at_least(ctx, pending)) return rc;
+                const volatile unsigned long long* hw = reinterpret_cast<volatile unsigned long long*>(s.hcnt);
+                if (hw[1]) return fail(ctx, TGO_E_PROGRAM, "vertex program failed: a traversed edge has no value for the weight property");
+                stop = hw[0] != 0 || hw[2] != 0;
+            }
+            pending = seq;
+            if (!stop && steps > max_steps) return fail(ctx, TGO_E_HIP, "delta-stepping: the device loop did not converge");
+        }
+        HIP_TRY(hipMemcpyAsync(&h, s.ds_loop, sizeof(DsLoop), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        if (h.err) return fail(ctx, TGO_E_PROGRAM, "vertex program failed: a traversed edge has no value for the weight property");
+    }
+    for (int64_t steps = 0; !pipe;) {
         DevSpan span(st, "sssp.delta_steps", {"first_step", steps}, {"steps", batch});
         for (int k = 0; k < batch; ++k) {
             if (nbins)

@@ -712,6 +712,16 @@ __global__ void ds_decide_bins(DsLoop* L, int cur, int64_t delta, int nbins, int
                                int64_t pull_min) {
     if (threadIdx.x == 0 && blockIdx.x == 0) decide_bins(L, cur, delta, nbins, cap, scan_above, pull_min);
 }
+// The loop's stop flags (done, err, spill) to host-mapped words, then the sequence number
+// (publish_counters' protocol): the host checks a batch while the next one runs.
+__global__ void ds_publish(const DsLoop* L, unsigned long long* host, unsigned long long seq) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    __hip_atomic_store(&host[0], L->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&host[1], L->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&host[2], L->spill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __threadfence_system();
+    __hip_atomic_store(&host[kCounterWords], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 // After a pull step: the next pull uses the other bitmap / list.
 __global__ void ds_pull_flip(DsLoop* L) {
     if (threadIdx.x == 0 && blockIdx.x == 0 && L->xpull) L->pulls += 1;
@@ -741,6 +751,10 @@ hipError_t k_ds_loop_step(const DevCsr& ws, const int64_t* light, uint64_t* pend
 
 // One step of the binned loop: decide, extract (piles, or the bitmap scan for a pile that
 // overflowed — each kernel returns at once unless its mode was decided), commit, relax.
+hipError_t k_ds_publish(const DsLoop* L, unsigned long long* host, unsigned long long seq, hipStream_t s) {
+    ds_publish<<<1, 64, 0, s>>>(L, host, seq);
+    return hipGetLastError();
+}
 hipError_t k_ds_loop_step_bins(const DevCsr& ws, const int64_t* light, uint64_t* pend, uint64_t* member, int64_t n,
                                int64_t* dist, int64_t* msg, int32_t* const q[2], int64_t* const qpre[2], DsLoop* L,
                                int cur, int64_t delta, int nbins, int32_t* pile, int64_t cap, int32_t* mlist,

@@ -571,6 +571,8 @@ hipError_t k_publish_counts(const Counters* c, int64_t* out, int64_t* slot, hipS
 constexpr int kCounterWords = static_cast<int>(sizeof(Counters) / 8);
 hipError_t k_publish_counters(const Counters* c, unsigned long long* host, unsigned long long seq, hipStream_t s);
 // `count` (<= kCounterWords) device words published like the counters (partitioned drivers)
+// The delta loop's done / err / spill flags to host-mapped words 0..2 and the sequence number.
+hipError_t k_ds_publish(const DsLoop* L, unsigned long long* host, unsigned long long seq, hipStream_t s);
 hipError_t k_publish_words(const int64_t* src, int count, unsigned long long* host, unsigned long long seq, hipStream_t s);
 // One launch instead of per-level memsets: zero the counters (cnt may be null), the next
 // frontier bitmap (words, may be 0) and the scan tail slot (may be null).
