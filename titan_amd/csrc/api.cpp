@@ -77,6 +77,7 @@ struct tgo_ctx {
     int64_t ds_pile_cap = 0;    // tgo_set_tuning(TGO_TUNE_DS_PILE_CAP): entries per pile; 0 = n
     int ds_done = -1;           // tgo_set_tuning(TGO_TUNE_DS_DONE): 1 / 0; < 0: TGO_DS_DONE / off
     double ds_pull = -1;        // tgo_set_tuning(TGO_TUNE_DS_PULL): member fraction; < 0: TGO_DS_PULL / off
+    unsigned long long* part_srcent = nullptr;   // next settle's per-source sums (part_ms_settle_sums)
     int64_t ms_cold = -1;       // tgo_set_tuning(TGO_TUNE_MS_COLD): 0 off, 1 on, > 1 on with that
                                 // hot head (and segment); < 0: TGO_MS_COLD / on
     // state a native partitioned driver keeps between runs on this graph (part_driver.cpp:
@@ -2430,7 +2431,8 @@ int tgo_part_ms_settle(tgo_ctx* ctx, int32_t level, const uint64_t* recv, int32_
     HIP_TRY(k_or_slices(recv, nslices, g.n, fr_next, st));
     const int nxt = ctx->part_cur ^ 1;
     HIP_TRY(k_ms_settle(push_view(g, TGO_SCOPE_BOTH_E), g.n_active, s.ms_vis, fr_next, ms_planes(ctx), s.q[nxt], s.qdeg,
-                        s.cnt, level + 1, st));
+                        s.cnt, level + 1, st, ctx->part_srcent));
+    ctx->part_srcent = nullptr;
     ctx->part_cur = nxt;
     ctx->part_queued = true;
     return part_counts(ctx, counts);
@@ -2527,13 +2529,13 @@ int tgo_part_ms_settle_fixed(tgo_ctx* ctx, int32_t level, const int64_t* recv, i
         return fail(ctx, TGO_E_INVALID, "ms_settle_fixed: bad arguments");
     if (level + 1 >= (1 << kLevelPlanes)) return fail(ctx, TGO_E_UNSUPPORTED, "multi-source BFS levels are < 65536");
     if ((rc = ms_planes_for(ctx, level + 1))) return rc;
-    HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
-    HIP_TRY(hipMemsetAsync(fr_next, 0, g.n_active * 8, st));     // the tail [n_active, n) stays zero
+    HIP_TRY(k_level_prep(s.cnt, fr_next, g.n_active, nullptr, st));   // the tail [n_active, n) stays zero
     HIP_TRY(k_ms_or_fixed(recv, nslices, cap, fr_next, st));
     HIP_TRY(ms_or_own(ctx, fr_next));
     const int nxt = ctx->part_cur ^ 1;
     HIP_TRY(k_ms_settle(push_view(g, TGO_SCOPE_BOTH_E), g.n_active, s.ms_vis, fr_next, ms_planes(ctx), s.q[nxt], s.qdeg,
-                        s.cnt, level + 1, st));
+                        s.cnt, level + 1, st, ctx->part_srcent));
+    ctx->part_srcent = nullptr;
     ctx->part_cur = nxt;
     ctx->part_queued = true;
     return part_counts(ctx, counts);
@@ -2550,8 +2552,7 @@ int tgo_part_ms_settle_pairs(tgo_ctx* ctx, int32_t level, const int64_t* recv, c
         return fail(ctx, TGO_E_INVALID, "ms_settle_pairs: bad arguments");
     if (level + 1 >= (1 << kLevelPlanes)) return fail(ctx, TGO_E_UNSUPPORTED, "multi-source BFS levels are < 65536");
     if ((rc = ms_planes_for(ctx, level + 1))) return rc;
-    HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
-    HIP_TRY(hipMemsetAsync(fr_next, 0, g.n_active * 8, st));     // the tail [n_active, n) stays zero
+    HIP_TRY(k_level_prep(s.cnt, fr_next, g.n_active, nullptr, st));   // the tail [n_active, n) stays zero
     int64_t npairs = 0;
     for (int r = 0; r < nslices; ++r) {
         if (recv_counts[r] < 0 || recv_counts[r] > g.n) return fail(ctx, TGO_E_INVALID, "ms_settle_pairs: bad count");
@@ -2561,7 +2562,8 @@ int tgo_part_ms_settle_pairs(tgo_ctx* ctx, int32_t level, const int64_t* recv, c
     HIP_TRY(ms_or_own(ctx, fr_next));
     const int nxt = ctx->part_cur ^ 1;
     HIP_TRY(k_ms_settle(push_view(g, TGO_SCOPE_BOTH_E), g.n_active, s.ms_vis, fr_next, ms_planes(ctx), s.q[nxt], s.qdeg,
-                        s.cnt, level + 1, st));
+                        s.cnt, level + 1, st, ctx->part_srcent));
+    ctx->part_srcent = nullptr;
     ctx->part_cur = nxt;
     ctx->part_queued = true;
     return part_counts(ctx, counts);
@@ -3145,6 +3147,16 @@ int part_read_words(tgo_ctx* ctx, const int64_t* dev, int count, int64_t* out) {
     if (int rc = wait_publish(ctx, seq)) return rc;
     const volatile unsigned long long* w = reinterpret_cast<volatile unsigned long long*>(s.hcnt);
     for (int i = 0; i < count; ++i) out[i] = static_cast<int64_t>(w[i]);
+    return TGO_OK;
+}
+// The next multi-source settle also sums the new frontier's push entries per source into
+// out (64 words, zeroed here on the ctx stream): the native driver's split after that level
+// reads them instead of a tgo_part_ms_source_entries pass.  One-shot; nullptr cancels.
+int part_ms_settle_sums(tgo_ctx* ctx, int64_t* out) {
+    ctx->part_srcent = nullptr;                                  // out == nullptr: cancel
+    if (!out) return TGO_OK;
+    HIP_TRY(hipMemsetAsync(out, 0, 64 * sizeof(int64_t), ctx->stream));
+    ctx->part_srcent = reinterpret_cast<unsigned long long*>(out);
     return TGO_OK;
 }
 void part_ms_bypass(tgo_ctx* ctx, uint64_t* cand_global, int self) {

@@ -312,6 +312,8 @@ int64_t* part_dcounts_of(tgo_ctx* ctx);
 // this rank's slice of the candidate words bypasses the pack / exchange (ORed in directly by the
 // settle); (nullptr, -1) turns it off
 void part_ms_bypass(tgo_ctx* ctx, uint64_t* cand_global, int self);
+// the next settle sums its new frontier's push entries per source into out (one-shot)
+int part_ms_settle_sums(tgo_ctx* ctx, int64_t* out);
 // device words to the host through the mapped counter page (no stream synchronisation)
 int part_read_words(tgo_ctx* ctx, const int64_t* dev, int count, int64_t* out);
 double ms_split_of(const tgo_ctx* ctx);
@@ -591,18 +593,23 @@ extern "C" int tgo_part_msbfs_run(tgo_ctx* ctx, tgo_exchange* x, const int64_t* 
         return pairs_fn(rpairs.data());
     };
     bool prev_dense = false;
+    bool sums = false;
     for (int level = 0; level < max_depth && nf > 0; ++level) {
         const bool dense = static_cast<double>(mf) * ms_alpha > static_cast<double>(total);
         DevSpan span(st, "part.msbfs.level", {"level", level}, {"dense", dense ? 1 : 0});
         const bool first_dense = dense && !prev_dense;
         prev_dense = dense;
+        const bool sums_ready = sums;   // the previous level's settle summed the per-source entries
+        sums = false;
         if (dense) {
             uint64_t sparse = 0;
             int32_t with_cand = 0;
             if (first_dense && split_frac > 0.0) {
                 // every source's exact push entries (all-reduced), the smallest within the budget
+                // after a push level its settle summed them (part_ms_settle_sums)
                 int64_t se[64];
-                if ((rc = tgo_part_ms_source_entries(ctx, fr, full, sc64)) || (rc = read64(se))) break;
+                if (!sums_ready && (rc = tgo_part_ms_source_entries(ctx, fr, full, sc64))) break;
+                if ((rc = read64(se))) break;
                 int order[64];
                 for (int r = 0; r < nseeds; ++r) order[r] = r;
                 std::sort(order, order + nseeds, [&](int a, int b) { return se[a] < se[b]; });
@@ -645,6 +652,10 @@ extern "C" int tgo_part_msbfs_run(tgo_ctx* ctx, tgo_exchange* x, const int64_t* 
             if ((rc = tgo_part_ms_pull_split(ctx, level, glob[0], frn, sparse, with_cand, nullptr))) break;
         } else {
             if ((rc = tgo_part_ms_push(ctx, level, fr, cand))) break;
+            // the settle sums the per-source entries when the next level may pull (this
+            // frontier's entries within 64x of the pull threshold), as the one-GPU sweep
+            sums = split_frac > 0.0 && static_cast<double>(mf) * ms_alpha * 64.0 > static_cast<double>(total);
+            if (sums && (rc = part_ms_settle_sums(ctx, sc64))) break;
             rc = exchange(mf,
                           [&](int64_t cap) { return tgo_part_ms_settle_fixed(ctx, level, recv, W, cap, frn, nullptr); },
                           [&](const int64_t* rp) { return tgo_part_ms_settle_pairs(ctx, level, recv, rp, W, frn, nullptr); });
@@ -662,6 +673,7 @@ extern "C" int tgo_part_msbfs_run(tgo_ctx* ctx, tgo_exchange* x, const int64_t* 
     }
     const int rc_off = tgo_part_device_counts(ctx, caller_dc);
     trace_resolve(st);
+    (void)part_ms_settle_sums(ctx, nullptr);          // a failed level may have left it armed
     if (rc) {
         x->abort();
         rezero();
