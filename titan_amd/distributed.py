@@ -708,6 +708,8 @@ class NativeExchange:
 
     def __init__(self, handle):
         self.h = C.c_void_p(handle)
+        # bound now: at interpreter exit the module globals (L) may be gone before __del__ runs
+        self._destroy = L.load().tgo_exchange_destroy
 
     @classmethod
     def rccl(cls, device: int, group=None, comm=None):
@@ -742,8 +744,9 @@ class NativeExchange:
         return [cls(h) for h in hs]
 
     def __del__(self):
-        if getattr(self, "h", None) is not None and self.h.value:
-            L.load().tgo_exchange_destroy(self.h)
+        destroy = getattr(self, "_destroy", None)
+        if destroy is not None and getattr(self, "h", None) is not None and self.h.value:
+            destroy(self.h)
             self.h = None
 
 
