@@ -1551,7 +1551,8 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
     // list entries (0 = every source pulled)
     const double split_frac = tgo::ms_split_of(ctx);
     int64_t qlen = static_cast<int64_t>(uniq.size());
-    int64_t mf = 0;
+    int64_t mf = 0;             // the seeds' entries are not read back: level 0 always pushes (a
+                                // direction is policy only; the read cost a stream drain, ~45 us)
     int64_t reached = qlen;     // vertices reached by any source so far
     bool srcent_ready = false;  // ms_srcent holds the current frontier's push entries per source
     static const double push_light = env_double("TGO_MS_PUSH_LIGHT", 1.0 / 16.0);
@@ -1559,12 +1560,6 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
     // measured slower at RMAT-24 (second level 446 -> 561 us, profiles/r04t_ms_push_ab.log): off
     static const int push_range_log2 = static_cast<int>(env_double("TGO_MS_PUSH_RANGE", 0.0));
     static const int64_t push_range_min = static_cast<int64_t>(env_double("TGO_MS_PUSH_RANGE_MIN", 1048576.0));
-    {
-        std::vector<int64_t> d(qlen);
-        HIP_TRY(hipMemcpyAsync(d.data(), s.qdeg, qlen * sizeof(int64_t), hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipStreamSynchronize(st));
-        for (int64_t x : d) mf += x;
-    }
     const int depth = std::min(a->max_depth, 65534);
     uint64_t* fr = s.ms_fr;
     uint64_t* nx = s.ms_nx;
@@ -1704,8 +1699,17 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
             // frontier grows at most ~40x a level on RMAT-24), else the split computes them
             sums = split_frac > 0.0 && static_cast<double>(mf) * ms_alpha * 64.0 > static_cast<double>(total);
             if (sums) HIP_TRY(hipMemsetAsync(s.ms_srcent, 0, 64 * sizeof(unsigned long long), st));
-            HIP_TRY(k_ms_settle(push, g.n_active, s.ms_vis, nx, ms_planes(ctx), s.q[cur ^ 1], s.qdeg, s.cnt, L + 1, st,
-                                sums ? s.ms_srcent : nullptr));
+            // a frontier within 8x of the pull threshold: the next level will likely pull and
+            // needs no queue — settle and count only (ms_queue builds it if the level pushes)
+            const bool next_pull = static_cast<double>(mf) * ms_alpha * 8.0 > static_cast<double>(total);
+            if (next_pull) {
+                HIP_TRY(k_ms_settle_count(push, g.n_active, s.ms_vis, nx, ms_planes(ctx), s.cnt, L + 1, st,
+                                          sums ? s.ms_srcent : nullptr));
+                queued = false;
+            } else {
+                HIP_TRY(k_ms_settle(push, g.n_active, s.ms_vis, nx, ms_planes(ctx), s.q[cur ^ 1], s.qdeg, s.cnt, L + 1,
+                                    st, sums ? s.ms_srcent : nullptr));
+            }
         }
         srcent_ready = !use_pull && sums;
         if ((rc = read_counters(ctx))) return rc;

@@ -686,6 +686,9 @@ constexpr int64_t kMsRangePairs = int64_t(1) << 22;   // ranged push: (entry, ra
 hipError_t k_ms_push_ranged(const View& push, const int32_t* q, int64_t qlen, int64_t n_active, int64_t S,
                             int64_t* P0, int64_t* P1, int64_t* cnt, int64_t* pre, void*& tmp, size_t& tmp_bytes,
                             const uint64_t* fr, const uint64_t* vis, uint64_t* nx, hipStream_t s, uint64_t mask = ~0ULL);
+// ms_settle without the queue (the next level pulls; counts only)
+hipError_t k_ms_settle_count(const View& push, int64_t n_active, uint64_t* vis, uint64_t* nx, LevelPlanes lvl,
+                            Counters* cnt, int32_t next_level, hipStream_t s, unsigned long long* srcent = nullptr);
 hipError_t k_ms_settle(const View& push, int64_t n_active, uint64_t* vis, uint64_t* nx, LevelPlanes lvl, int32_t* qn,
                        int64_t* qdeg, Counters* cnt, int32_t next_level, hipStream_t s,
                        unsigned long long* srcent = nullptr);

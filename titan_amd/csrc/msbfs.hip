@@ -709,6 +709,49 @@ __global__ void __launch_bounds__(kBlock) ms_settle(View push, int64_t n_active,
     if (srcent) source_sums_flush(ssum, srcent);                 // grid-uniform
 }
 
+// The settle of a push level whose next level will likely pull: the same masks, levels and
+// counts as ms_settle without the frontier queue (a pull needs none; ms_queue builds it if the
+// next level pushes after all) — one pass instead of the extraction's two, four words in
+// flight per wave.  srcent as in ms_settle.
+__global__ void __launch_bounds__(kBlock) ms_settle_count(View push, int64_t n_active, uint64_t* __restrict__ vis,
+        uint64_t* __restrict__ nx, LevelPlanes lvl, Counters* cnt, int32_t next_level,
+        unsigned long long* __restrict__ srcent) {
+    unsigned long long nv = 0, mf = 0, bits = 0, ssum = 0;
+    const int64_t words = (n_active + 63) >> 6;
+    const int64_t nw = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
+    for (int64_t w0 = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6; w0 < words; w0 += 4 * nw) {
+        uint64_t c[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t v = ((w0 + u * nw) << 6) + lane();
+            c[u] = (w0 + u * nw < words && v < n_active) ? nx[v] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (!__ballot(c[u] != 0)) continue;                  // wave-uniform
+            const int64_t v = ((w0 + u * nw) << 6) + lane();
+            uint64_t fresh = 0;
+            int64_t deg = 0;
+            if (c[u]) {
+                const uint64_t seen = vis[v];
+                fresh = c[u] & ~seen;
+                nx[v] = fresh;
+                if (fresh) {
+                    vis[v] = seen | fresh;
+                    record_level(v, fresh, next_level, lvl);
+                    deg = push_degree(push, v);
+                    ++nv;
+                    mf += static_cast<unsigned long long>(deg);
+                    bits += static_cast<unsigned long long>(__popcll(fresh));
+                }
+            }
+            if (srcent && __ballot(fresh != 0)) source_columns_add(fresh, static_cast<unsigned long long>(deg), ssum);
+        }
+    }
+    count_flush(cnt, nv, mf, bits);
+    if (srcent) source_sums_flush(ssum, srcent);                 // grid-uniform
+}
+
 // The queue of a frontier produced by a pull level (which only counts): every active v with
 // fr[v] != 0, push degrees for the scan.  Built only when the next level pushes.
 __global__ void __launch_bounds__(kBlock) ms_queue(View push, int64_t n_active, const uint64_t* __restrict__ fr,
@@ -1011,6 +1054,11 @@ hipError_t k_ms_push_ranged(const View& push, const int32_t* q, int64_t qlen, in
     hipError_t e = scan_exclusive_i64(tmp, tmp_bytes, cnt, pre, R * qlen + 1, s);
     if (e != hipSuccess) return e;
     ms_push_ranged<<<256 * 8, kBlock, 0, s>>>(push, q, qlen, R, P0, P1, pre, fr, vis, nx, mask);
+    return hipGetLastError();
+}
+hipError_t k_ms_settle_count(const View& push, int64_t n_active, uint64_t* vis, uint64_t* nx, LevelPlanes lvl,
+                            Counters* cnt, int32_t next_level, hipStream_t s, unsigned long long* srcent) {
+    ms_settle_count<<<grid_for(n_active, 2048), kBlock, 0, s>>>(push, n_active, vis, nx, lvl, cnt, next_level, srcent);
     return hipGetLastError();
 }
 hipError_t k_ms_settle(const View& push, int64_t n_active, uint64_t* vis, uint64_t* nx, LevelPlanes lvl, int32_t* qn,
