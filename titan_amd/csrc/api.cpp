@@ -1697,7 +1697,8 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
             // the new frontier's push entries per source, for the next level's split — when that
             // level may pull (this frontier's entries within 64x of the pull threshold; a
             // frontier grows at most ~40x a level on RMAT-24), else the split computes them
-            sums = split_frac > 0.0 && static_cast<double>(mf) * ms_alpha * 64.0 > static_cast<double>(total);
+            // (level 0: the seeds' entries are not known, so always)
+            sums = split_frac > 0.0 && (L == 0 || static_cast<double>(mf) * ms_alpha * 64.0 > static_cast<double>(total));
             if (sums) HIP_TRY(hipMemsetAsync(s.ms_srcent, 0, 64 * sizeof(unsigned long long), st));
             // a frontier within 8x of the pull threshold: the next level will likely pull and
             // needs no queue — settle and count only (ms_queue builds it if the level pushes)
