@@ -2,7 +2,7 @@
 # Sweep: no seed-degree readback, queue-less settle ahead of a pull level — parity, the sweep
 # time, its kernel timeline.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
-T=r04z2
+T=r04z3
 mkdir -p gpurun_out/$T
 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_parity.py \
     tests/test_gpu_distributed.py tests/test_gpu_fullsize.py -k "multi or msbfs or config3" > gpurun_out/$T/parity.log 2>&1

@@ -1566,10 +1566,12 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
     int cur = 0, levels = 0;
     bool queued = true;         // q[cur] holds the frontier (pull levels only count it)
     bool pulled = false;        // the previous level pulled
+    bool cnt_zero = false;      // the counters were zeroed after the last publish
     for (int L = 0; L < depth && qlen > 0; ++L) {
         const bool use_pull = static_cast<double>(mf) * ms_alpha > static_cast<double>(total);
         DevSpan span(st, "msbfs.level", {"level", L}, {"pull", use_pull ? 1 : 0});
         if ((rc = ms_planes_for(ctx, L + 1))) return rc;
+        const bool queued_before = queued;
         if (!use_pull && !queued) {     // the frontier's queue, for the push level's scan
             HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
             HIP_TRY(k_ms_queue(push, g.n_active, fr, s.q[cur], s.qdeg, s.cnt, st));
@@ -1578,8 +1580,9 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
         const bool prev_pull = pulled;
         pulled = use_pull;
         bool sums = false;          // this push level's settle sums the per-source entries
+        if (!use_pull && !queued_before) cnt_zero = false;      // ms_queue counted into them
         if (use_pull) {
-            HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
+            if (!cnt_zero) HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
             // Split the sources: the pull's walk of a vertex stops once every open source is
             // covered, and one source whose frontier never reaches the vertex (a source far
             // from it, or one whose sweep is over) makes every walk scan its whole list.  The
@@ -1713,7 +1716,19 @@ int tgo_bfs_multi(tgo_ctx* ctx, const int64_t* seeds, int32_t nseeds, const tgo_
             }
         }
         srcent_ready = !use_pull && sums;
-        if ((rc = read_counters(ctx))) return rc;
+        {
+            // publish the counts, then queue the next level's direction-independent prefix (its
+            // level planes, zeroed counters) before the host waits: the GPU runs it during the
+            // host's round trip (≈ 10–25 us a level)
+            const unsigned long long seq = ++s.pub_seq;
+            HIP_TRY(k_publish_counters(s.cnt, s.hcnt_dev, seq, st));
+            if (L + 1 < depth) {
+                if ((rc = ms_planes_for(ctx, L + 2))) return rc;
+                HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
+                cnt_zero = true;
+            }
+            if ((rc = wait_publish(ctx, seq))) return rc;
+        }
         qlen = static_cast<int64_t>(s.hcnt->qlen);
         mf = static_cast<int64_t>(s.hcnt->mf);
         reached += qlen;
