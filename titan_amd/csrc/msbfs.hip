@@ -102,7 +102,9 @@ __device__ unsigned long long g_ms_diag[kDiagWords];
 // sorted, so it stops at the first cold one); a row it does not cover whose lists go on past
 // hot_lim is left to the blocked cold pass: its partial mask to cs.acc, cs.need set, nothing
 // written (ms_cold ORs its cold neighbours in, ms_finish settles it).
-template <int kStep, bool kDiag = false, int kLong = 4>
+// kRamp: a long list's first trip reads 64 entries only (its head of hubs often covers every
+// open source), the later ones kLong * 64.
+template <int kStep, bool kDiag = false, int kLong = 4, bool kRamp = false>
 __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t n_active, uint64_t full,
         const uint64_t* __restrict__ fr, const uint64_t* __restrict__ fbm, uint64_t* __restrict__ vis,
         uint64_t* __restrict__ nx, LevelPlanes lvl, Counters* cnt, int32_t next_level, int32_t filter_from,
@@ -172,15 +174,19 @@ __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t 
                 const int64_t ee = __shfl(l == 0 ? e0 : e1, src, 64);
                 const int32_t* adj = l == 0 ? pull.adj0 : pull.adj1;
                 bool done = false;
-                for (int64_t k = bb; k < ee && !done; k += kLong * 64) {
+                bool first = kRamp && l == 0;
+                for (int64_t k = bb; k < ee && !done;) {
+                    const int jl = first ? 1 : kLong;                 // wave-uniform
                     int32_t u[kLong];
                     bool hc = false;
 #pragma unroll
                     for (int j = 0; j < kLong; ++j) {
                         const int64_t x = k + j * 64 + lane();
-                        u[j] = x < ee ? __builtin_nontemporal_load(adj + x) : -1;
+                        u[j] = (j < jl && x < ee) ? __builtin_nontemporal_load(adj + x) : -1;
                         if (u[j] >= hot_lim) { u[j] = -1; hc = true; }
                     }
+                    k += static_cast<int64_t>(jl) * 64;
+                    first = false;
                     if (__ballot(hc)) { done = true; wcut = true; }   // the rest of the list is cold
                     bool f[kLong];
 #pragma unroll
@@ -196,7 +202,7 @@ __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t 
                     a |= m;
                     done = done || (a & wsrc) == wsrc;
                     if (kDiag && lane() == src)
-                        for (int j = 0; j < kLong; ++j) dg[5] += k + j * 64 < ee ? min<int64_t>(64, ee - k - j * 64) : 0;
+                        for (int j = 0; j < kLong; ++j) dg[5] += u[j] >= 0 ? 1 : 0;
                 }
                 if ((a & wsrc) == wsrc) break;
             }
@@ -960,7 +966,18 @@ hipError_t k_ms_pull(const View& pull, const View& push, int64_t n_active, uint6
     static const bool diag = [] { const char* e = std::getenv("TGO_MS_DIAG"); return e && std::atoi(e) != 0; }();
     // TGO_MS_LONG: entries per lane per trip of a long list (4 default; 8 probe)
     static const int lng = [] { const char* e = std::getenv("TGO_MS_LONG"); return e ? std::atoi(e) : 4; }();
-    if (!diag && step == 8 && lng == 8)
+    // TGO_MS_RAMP=1: a long list's first trip reads 64 entries
+    static const bool ramp = [] { const char* e = std::getenv("TGO_MS_RAMP"); return e && std::atoi(e) != 0; }();
+    if (!diag && step == 8 && ramp)
+        ms_pull<8, false, 4, true><<<grid_for(n_active, 8192), kBlock, 0, s>>>(pull, push, n_active, full, fr, fbm, vis, nx,
+                                                                               lvl, cnt, next_level, filter_from, dense, cand, cs);
+    else if (!diag && step == 8 && lng == 1)
+        ms_pull<8, false, 1><<<grid_for(n_active, 8192), kBlock, 0, s>>>(pull, push, n_active, full, fr, fbm, vis, nx, lvl,
+                                                                         cnt, next_level, filter_from, dense, cand, cs);
+    else if (!diag && step == 8 && lng == 2)
+        ms_pull<8, false, 2><<<grid_for(n_active, 8192), kBlock, 0, s>>>(pull, push, n_active, full, fr, fbm, vis, nx, lvl,
+                                                                         cnt, next_level, filter_from, dense, cand, cs);
+    else if (!diag && step == 8 && lng == 8)
         ms_pull<8, false, 8><<<grid_for(n_active, 8192), kBlock, 0, s>>>(pull, push, n_active, full, fr, fbm, vis, nx, lvl,
                                                                          cnt, next_level, filter_from, dense, cand, cs);
     else if (diag)
