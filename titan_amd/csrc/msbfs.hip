@@ -961,37 +961,29 @@ hipError_t k_ms_pull(const View& pull, const View& push, int64_t n_active, uint6
                      const uint64_t* fbm, uint64_t* vis, uint64_t* nx, LevelPlanes lvl, Counters* cnt,
                      int32_t next_level, hipStream_t s, int32_t filter_from, uint64_t dense, const uint64_t* cand,
                      MsColdSplit cs) {
-    // TGO_MS_STEP: entries a lane loads per round trip of its own list (8 default; 16 probe)
+    // TGO_MS_STEP: entries a lane loads per round trip of its own list (8 default; 4 / 16 probes)
     static const int step = [] { const char* e = std::getenv("TGO_MS_STEP"); return e ? std::atoi(e) : 8; }();
     static const bool diag = [] { const char* e = std::getenv("TGO_MS_DIAG"); return e && std::atoi(e) != 0; }();
-    // TGO_MS_LONG: entries per lane per trip of a long list (4 default; 8 probe)
-    static const int lng = [] { const char* e = std::getenv("TGO_MS_LONG"); return e ? std::atoi(e) : 4; }();
-    // TGO_MS_RAMP=1: a long list's first trip reads 64 entries
+    // TGO_MS_LONG: entries per lane per trip of a long list.  1 (default, round 4): with the
+    // source split most long walks stop early, and a 64-entry trip stops them soonest — sweep
+    // 4.27 -> 3.69-3.74 ms against 4 (2: 4.00, 8: 4.60; profiles/r04z4_ms_pull_ab.log)
+    static const int lng = [] { const char* e = std::getenv("TGO_MS_LONG"); return e ? std::atoi(e) : 1; }();
+    // TGO_MS_RAMP=1 (with TGO_MS_LONG=4): a long list's first trip reads 64 entries
     static const bool ramp = [] { const char* e = std::getenv("TGO_MS_RAMP"); return e && std::atoi(e) != 0; }();
-    if (!diag && step == 8 && ramp)
-        ms_pull<8, false, 4, true><<<grid_for(n_active, 8192), kBlock, 0, s>>>(pull, push, n_active, full, fr, fbm, vis, nx,
-                                                                               lvl, cnt, next_level, filter_from, dense, cand, cs);
-    else if (!diag && step == 8 && lng == 1)
-        ms_pull<8, false, 1><<<grid_for(n_active, 8192), kBlock, 0, s>>>(pull, push, n_active, full, fr, fbm, vis, nx, lvl,
-                                                                         cnt, next_level, filter_from, dense, cand, cs);
-    else if (!diag && step == 8 && lng == 2)
-        ms_pull<8, false, 2><<<grid_for(n_active, 8192), kBlock, 0, s>>>(pull, push, n_active, full, fr, fbm, vis, nx, lvl,
-                                                                         cnt, next_level, filter_from, dense, cand, cs);
-    else if (!diag && step == 8 && lng == 8)
-        ms_pull<8, false, 8><<<grid_for(n_active, 8192), kBlock, 0, s>>>(pull, push, n_active, full, fr, fbm, vis, nx, lvl,
-                                                                         cnt, next_level, filter_from, dense, cand, cs);
-    else if (diag)
-        ms_pull<8, true><<<grid_for(n_active, 8192), kBlock, 0, s>>>(pull, push, n_active, full, fr, fbm, vis, nx, lvl, cnt,
-                                                                   next_level, filter_from, dense, cand, cs);
-    else if (step == 16)
-        ms_pull<16><<<grid_for(n_active, 8192), kBlock, 0, s>>>(pull, push, n_active, full, fr, fbm, vis, nx, lvl, cnt,
-                                                               next_level, filter_from, dense, cand, cs);
-    else if (step == 4)
-        ms_pull<4><<<grid_for(n_active, 8192), kBlock, 0, s>>>(pull, push, n_active, full, fr, fbm, vis, nx, lvl, cnt,
-                                                              next_level, filter_from, dense, cand, cs);
-    else
-        ms_pull<8><<<grid_for(n_active, 8192), kBlock, 0, s>>>(pull, push, n_active, full, fr, fbm, vis, nx, lvl, cnt,
-                                                              next_level, filter_from, dense, cand, cs);
+    const dim3 grid(grid_for(n_active, 8192));
+#define TGO_MS_PULL(S, D, LG, R) ms_pull<S, D, LG, R><<<grid, kBlock, 0, s>>>(pull, push, n_active, full, fr, fbm, vis, \
+        nx, lvl, cnt, next_level, filter_from, dense, cand, cs)
+    if (diag) TGO_MS_PULL(8, true, 1, false);
+    else if (ramp) TGO_MS_PULL(8, false, 4, true);
+    else if (step == 4 && lng == 1) TGO_MS_PULL(4, false, 1, false);
+    else if (step == 16 && lng == 1) TGO_MS_PULL(16, false, 1, false);
+    else if (lng == 1) TGO_MS_PULL(8, false, 1, false);
+    else if (lng == 2) TGO_MS_PULL(8, false, 2, false);
+    else if (lng == 8) TGO_MS_PULL(8, false, 8, false);
+    else if (step == 4) TGO_MS_PULL(4, false, 4, false);
+    else if (step == 16) TGO_MS_PULL(16, false, 4, false);
+    else TGO_MS_PULL(8, false, 4, false);
+#undef TGO_MS_PULL
     return hipGetLastError();
 }
 hipError_t k_ms_cold(const int32_t* cadj, const int32_t* crow, int64_t C, const uint64_t* fr, const uint8_t* need,
