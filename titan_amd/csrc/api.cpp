@@ -78,6 +78,7 @@ struct tgo_ctx {
     int ds_done = -1;           // tgo_set_tuning(TGO_TUNE_DS_DONE): 1 / 0; < 0: TGO_DS_DONE / off
     double ds_pull = -1;        // tgo_set_tuning(TGO_TUNE_DS_PULL): member fraction; < 0: TGO_DS_PULL / off
     unsigned long long* part_srcent = nullptr;   // next settle's per-source sums (part_ms_settle_sums)
+    bool part_count_only = false;               // next settle: no queue (part_ms_settle_sums)
     int64_t ms_cold = -1;       // tgo_set_tuning(TGO_TUNE_MS_COLD): 0 off, 1 on, > 1 on with that
                                 // hot head (and segment); < 0: TGO_MS_COLD / on
     // state a native partitioned driver keeps between runs on this graph (part_driver.cpp:
@@ -2450,11 +2451,17 @@ int tgo_part_ms_settle(tgo_ctx* ctx, int32_t level, const uint64_t* recv, int32_
     HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
     HIP_TRY(k_or_slices(recv, nslices, g.n, fr_next, st));
     const int nxt = ctx->part_cur ^ 1;
-    HIP_TRY(k_ms_settle(push_view(g, TGO_SCOPE_BOTH_E), g.n_active, s.ms_vis, fr_next, ms_planes(ctx), s.q[nxt], s.qdeg,
-                        s.cnt, level + 1, st, ctx->part_srcent));
+    if (ctx->part_count_only) {
+        HIP_TRY(k_ms_settle_count(push_view(g, TGO_SCOPE_BOTH_E), g.n_active, s.ms_vis, fr_next, ms_planes(ctx), s.cnt,
+                                  level + 1, st, ctx->part_srcent));
+    } else {
+        HIP_TRY(k_ms_settle(push_view(g, TGO_SCOPE_BOTH_E), g.n_active, s.ms_vis, fr_next, ms_planes(ctx), s.q[nxt], s.qdeg,
+                            s.cnt, level + 1, st, ctx->part_srcent));
+    }
+    ctx->part_queued = !ctx->part_count_only;
     ctx->part_srcent = nullptr;
+    ctx->part_count_only = false;
     ctx->part_cur = nxt;
-    ctx->part_queued = true;
     return part_counts(ctx, counts);
 }
 
@@ -2553,11 +2560,17 @@ int tgo_part_ms_settle_fixed(tgo_ctx* ctx, int32_t level, const int64_t* recv, i
     HIP_TRY(k_ms_or_fixed(recv, nslices, cap, fr_next, st));
     HIP_TRY(ms_or_own(ctx, fr_next));
     const int nxt = ctx->part_cur ^ 1;
-    HIP_TRY(k_ms_settle(push_view(g, TGO_SCOPE_BOTH_E), g.n_active, s.ms_vis, fr_next, ms_planes(ctx), s.q[nxt], s.qdeg,
-                        s.cnt, level + 1, st, ctx->part_srcent));
+    if (ctx->part_count_only) {
+        HIP_TRY(k_ms_settle_count(push_view(g, TGO_SCOPE_BOTH_E), g.n_active, s.ms_vis, fr_next, ms_planes(ctx), s.cnt,
+                                  level + 1, st, ctx->part_srcent));
+    } else {
+        HIP_TRY(k_ms_settle(push_view(g, TGO_SCOPE_BOTH_E), g.n_active, s.ms_vis, fr_next, ms_planes(ctx), s.q[nxt], s.qdeg,
+                            s.cnt, level + 1, st, ctx->part_srcent));
+    }
+    ctx->part_queued = !ctx->part_count_only;
     ctx->part_srcent = nullptr;
+    ctx->part_count_only = false;
     ctx->part_cur = nxt;
-    ctx->part_queued = true;
     return part_counts(ctx, counts);
 }
 
@@ -2581,11 +2594,17 @@ int tgo_part_ms_settle_pairs(tgo_ctx* ctx, int32_t level, const int64_t* recv, c
     HIP_TRY(k_ms_or_pairs(recv, npairs, fr_next, st));
     HIP_TRY(ms_or_own(ctx, fr_next));
     const int nxt = ctx->part_cur ^ 1;
-    HIP_TRY(k_ms_settle(push_view(g, TGO_SCOPE_BOTH_E), g.n_active, s.ms_vis, fr_next, ms_planes(ctx), s.q[nxt], s.qdeg,
-                        s.cnt, level + 1, st, ctx->part_srcent));
+    if (ctx->part_count_only) {
+        HIP_TRY(k_ms_settle_count(push_view(g, TGO_SCOPE_BOTH_E), g.n_active, s.ms_vis, fr_next, ms_planes(ctx), s.cnt,
+                                  level + 1, st, ctx->part_srcent));
+    } else {
+        HIP_TRY(k_ms_settle(push_view(g, TGO_SCOPE_BOTH_E), g.n_active, s.ms_vis, fr_next, ms_planes(ctx), s.q[nxt], s.qdeg,
+                            s.cnt, level + 1, st, ctx->part_srcent));
+    }
+    ctx->part_queued = !ctx->part_count_only;
     ctx->part_srcent = nullptr;
+    ctx->part_count_only = false;
     ctx->part_cur = nxt;
-    ctx->part_queued = true;
     return part_counts(ctx, counts);
 }
 
@@ -3172,8 +3191,11 @@ int part_read_words(tgo_ctx* ctx, const int64_t* dev, int count, int64_t* out) {
 // The next multi-source settle also sums the new frontier's push entries per source into
 // out (64 words, zeroed here on the ctx stream): the native driver's split after that level
 // reads them instead of a tgo_part_ms_source_entries pass.  One-shot; nullptr cancels.
-int part_ms_settle_sums(tgo_ctx* ctx, int64_t* out) {
+// count_only: that settle builds no frontier queue (the next level will likely pull;
+// tgo_part_ms_push builds the queue if it runs after all).
+int part_ms_settle_sums(tgo_ctx* ctx, int64_t* out, bool count_only) {
     ctx->part_srcent = nullptr;                                  // out == nullptr: cancel
+    ctx->part_count_only = count_only;
     if (!out) return TGO_OK;
     HIP_TRY(hipMemsetAsync(out, 0, 64 * sizeof(int64_t), ctx->stream));
     ctx->part_srcent = reinterpret_cast<unsigned long long*>(out);

@@ -313,7 +313,7 @@ int64_t* part_dcounts_of(tgo_ctx* ctx);
 // settle); (nullptr, -1) turns it off
 void part_ms_bypass(tgo_ctx* ctx, uint64_t* cand_global, int self);
 // the next settle sums its new frontier's push entries per source into out (one-shot)
-int part_ms_settle_sums(tgo_ctx* ctx, int64_t* out);
+int part_ms_settle_sums(tgo_ctx* ctx, int64_t* out, bool count_only = false);
 // device words to the host through the mapped counter page (no stream synchronisation)
 int part_read_words(tgo_ctx* ctx, const int64_t* dev, int count, int64_t* out);
 double ms_split_of(const tgo_ctx* ctx);
@@ -655,7 +655,9 @@ extern "C" int tgo_part_msbfs_run(tgo_ctx* ctx, tgo_exchange* x, const int64_t* 
             // the settle sums the per-source entries when the next level may pull (this
             // frontier's entries within 64x of the pull threshold), as the one-GPU sweep
             sums = split_frac > 0.0 && static_cast<double>(mf) * ms_alpha * 64.0 > static_cast<double>(total);
-            if (sums && (rc = part_ms_settle_sums(ctx, sc64))) break;
+            // and builds no queue when the next level will likely pull (within 8x of the threshold)
+            const bool next_pull = static_cast<double>(mf) * ms_alpha * 8.0 > static_cast<double>(total);
+            if ((sums || next_pull) && (rc = part_ms_settle_sums(ctx, sums ? sc64 : nullptr, next_pull))) break;
             rc = exchange(mf,
                           [&](int64_t cap) { return tgo_part_ms_settle_fixed(ctx, level, recv, W, cap, frn, nullptr); },
                           [&](const int64_t* rp) { return tgo_part_ms_settle_pairs(ctx, level, recv, rp, W, frn, nullptr); });
