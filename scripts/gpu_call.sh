@@ -1,14 +1,9 @@
 #!/bin/bash
-# Partitioned sweep: queue-less settle ahead of a likely pull level — distributed parity and
-# the world-1 partitioned bench.
+# Multi-source pull: the wave-cooperative list threshold (TGO_MS_COOP) A/B on the sweep.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
-T=r04z6
+T=r04z7
 mkdir -p gpurun_out/$T
-timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_distributed.py \
-    tests/test_gpu_fullsize.py -k "msbfs or multi or partitioned" > gpurun_out/$T/parity.log 2>&1
-rc=$?; tail -3 gpurun_out/$T/parity.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 600 python3 bench.py --partitioned --cpu-baseline 0 --rows-scale 0 --sssp-roots 0 \
-    > gpurun_out/$T/bench_part.json 2> gpurun_out/$T/bench_part.err
-rc=$?; cut -c1-300 gpurun_out/$T/bench_part.json; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python3 scripts/ms_levels.py 24 3 > gpurun_out/$T/ms_levels.log 2>&1
-rc=$?; head -14 gpurun_out/$T/ms_levels.log; exit $rc
+for v in 64 16 32 128 256 64 16 32 128 256; do
+    TGO_MS_COOP=$v timeout -k 10 300 python3 scripts/ms_probe.py 24 5 > gpurun_out/$T/ab.tmp 2>&1
+    rc=$?; echo "coop $v: $(tail -1 gpurun_out/$T/ab.tmp)" | cut -c1-110 | tee -a gpurun_out/$T/ab.log; [ $rc -eq 0 ] || exit $rc
+done

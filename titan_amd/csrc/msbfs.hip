@@ -108,7 +108,7 @@ template <int kStep, bool kDiag = false, int kLong = 4, bool kRamp = false>
 __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t n_active, uint64_t full,
         const uint64_t* __restrict__ fr, const uint64_t* __restrict__ fbm, uint64_t* __restrict__ vis,
         uint64_t* __restrict__ nx, LevelPlanes lvl, Counters* cnt, int32_t next_level, int32_t filter_from,
-        uint64_t dense, const uint64_t* __restrict__ cand, MsColdSplit cs) {
+        uint64_t dense, const uint64_t* __restrict__ cand, MsColdSplit cs, int64_t coop) {
     const int32_t hot_lim = cs.hot_lim;
     unsigned long long nv = 0, mf = 0, bits = 0;
     unsigned long long dg[kDiagWords] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -132,7 +132,7 @@ __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t 
         const int64_t deg = (e0 - b0) + (e1 - b1);
         uint64_t acc = 0;
         bool cut = false;                                     // a list went on past hot_lim
-        if (want && deg <= kCoop) {
+        if (want && deg <= coop) {
             for (int l = 0; l < 2 && (acc & want) != want; ++l) {
                 const int32_t* adj = l == 0 ? pull.adj0 : pull.adj1;
                 const int64_t e = l == 0 ? e0 : e1;
@@ -162,7 +162,7 @@ __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t 
             }
             if (kDiag) { ++dg[3]; if ((acc & want) == want) ++dg[4]; }
         }
-        unsigned long long big = __ballot(want != 0 && deg > kCoop);
+        unsigned long long big = __ballot(want != 0 && deg > coop);
         while (big) {
             const int src = __ffsll(static_cast<long long>(big)) - 1;
             big &= big - 1;
@@ -970,9 +970,11 @@ hipError_t k_ms_pull(const View& pull, const View& push, int64_t n_active, uint6
     static const int lng = [] { const char* e = std::getenv("TGO_MS_LONG"); return e ? std::atoi(e) : 1; }();
     // TGO_MS_RAMP=1 (with TGO_MS_LONG=4): a long list's first trip reads 64 entries
     static const bool ramp = [] { const char* e = std::getenv("TGO_MS_RAMP"); return e && std::atoi(e) != 0; }();
+    // TGO_MS_COOP: lists longer than this are walked by the whole wave (64 default)
+    static const int64_t coop = [] { const char* e = std::getenv("TGO_MS_COOP"); return e ? std::atoll(e) : kCoop; }();
     const dim3 grid(grid_for(n_active, 8192));
 #define TGO_MS_PULL(S, D, LG, R) ms_pull<S, D, LG, R><<<grid, kBlock, 0, s>>>(pull, push, n_active, full, fr, fbm, vis, \
-        nx, lvl, cnt, next_level, filter_from, dense, cand, cs)
+        nx, lvl, cnt, next_level, filter_from, dense, cand, cs, coop)
     if (diag) TGO_MS_PULL(8, true, 1, false);
     else if (ramp) TGO_MS_PULL(8, false, 4, true);
     else if (step == 4 && lng == 1) TGO_MS_PULL(4, false, 1, false);
