@@ -1,9 +1,11 @@
 #!/bin/bash
-# Multi-source pull: the wave-cooperative list threshold (TGO_MS_COOP) A/B on the sweep.
+# Round-4 close, part A: the full GPU suite, smoke(), the bench line.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
-T=r04z7
+T=r04f
 mkdir -p gpurun_out/$T
-for v in 64 16 32 128 256 64 16 32 128 256; do
-    TGO_MS_COOP=$v timeout -k 10 300 python3 scripts/ms_probe.py 24 5 > gpurun_out/$T/ab.tmp 2>&1
-    rc=$?; echo "coop $v: $(tail -1 gpurun_out/$T/ab.tmp)" | cut -c1-110 | tee -a gpurun_out/$T/ab.log; [ $rc -eq 0 ] || exit $rc
-done
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/$T/gpu_tests.log 2>&1
+rc=$?; tail -3 gpurun_out/$T/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/$T/smoke.log 2>&1
+rc=$?; tail -2 gpurun_out/$T/smoke.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 500 python3 bench.py > gpurun_out/$T/bench.json 2> gpurun_out/$T/bench.err
+rc=$?; cut -c1-300 gpurun_out/$T/bench.json; exit $rc
