@@ -79,6 +79,8 @@ struct tgo_ctx {
     double ds_pull = -1;        // tgo_set_tuning(TGO_TUNE_DS_PULL): member fraction; < 0: TGO_DS_PULL / off
     unsigned long long* part_srcent = nullptr;   // next settle's per-source sums (part_ms_settle_sums)
     bool part_count_only = false;               // next settle: no queue (part_ms_settle_sums)
+    uint64_t* part_own_next = nullptr;          // next push: owned targets straight into these masks
+    uint64_t* part_own_direct = nullptr;        // the last push did so (its settle skips the own OR)
     int64_t ms_cold = -1;       // tgo_set_tuning(TGO_TUNE_MS_COLD): 0 off, 1 on, > 1 on with that
                                 // hot head (and segment); < 0: TGO_MS_COLD / on
     // state a native partitioned driver keeps between runs on this graph (part_driver.cpp:
@@ -2430,11 +2432,22 @@ int tgo_part_ms_push(tgo_ctx* ctx, int32_t level, const uint64_t* fr_local, uint
                            ctx->stream));
         ctx->part_queued = true;
     }
+    // bypass on and the next masks named (part_ms_own_next): the owned targets' candidates go
+    // straight into them (zeroed here), so the settle neither zeroes them nor ORs the own slice
+    uint64_t* own = nullptr;
+    int64_t own_lo = 0;
+    if (ctx->part_own_next && ctx->part_ms_self >= 0 && cand_global == ctx->part_ms_cand) {
+        own = ctx->part_own_next;
+        own_lo = static_cast<int64_t>(ctx->part_ms_self) * g.n;
+        HIP_TRY(k_level_prep(nullptr, own, g.n_active, nullptr, ctx->stream));   // the tail stays zero
+    }
+    ctx->part_own_next = nullptr;
+    ctx->part_own_direct = own;
     if (qlen > 0) {
         if ((rc = scan_frontier(ctx, ctx->part_qlen))) return rc;
         const PackTouch touch{s.pk_touch, g.n, (g.n + kPackChunk - 1) / kPackChunk};
         HIP_TRY(k_ms_push(push_view(g, TGO_SCOPE_BOTH_E), s.q[ctx->part_cur], s.qpre, ctx->part_qlen, fr_local,
-                          nullptr, cand_global, ctx->stream, touch));
+                          nullptr, cand_global, ctx->stream, touch, ~0ULL, true, own, own_lo));
     }
     return part_done(ctx);
 }
@@ -2556,9 +2569,11 @@ int tgo_part_ms_settle_fixed(tgo_ctx* ctx, int32_t level, const int64_t* recv, i
         return fail(ctx, TGO_E_INVALID, "ms_settle_fixed: bad arguments");
     if (level + 1 >= (1 << kLevelPlanes)) return fail(ctx, TGO_E_UNSUPPORTED, "multi-source BFS levels are < 65536");
     if ((rc = ms_planes_for(ctx, level + 1))) return rc;
-    HIP_TRY(k_level_prep(s.cnt, fr_next, g.n_active, nullptr, st));   // the tail [n_active, n) stays zero
+    const bool direct = ctx->part_own_direct == fr_next;     // the push wrote the owned targets here
+    ctx->part_own_direct = nullptr;
+    HIP_TRY(k_level_prep(s.cnt, direct ? nullptr : fr_next, direct ? 0 : g.n_active, nullptr, st));   // tail stays zero
     HIP_TRY(k_ms_or_fixed(recv, nslices, cap, fr_next, st));
-    HIP_TRY(ms_or_own(ctx, fr_next));
+    if (!direct) HIP_TRY(ms_or_own(ctx, fr_next));
     const int nxt = ctx->part_cur ^ 1;
     if (ctx->part_count_only) {
         HIP_TRY(k_ms_settle_count(push_view(g, TGO_SCOPE_BOTH_E), g.n_active, s.ms_vis, fr_next, ms_planes(ctx), s.cnt,
@@ -2585,14 +2600,16 @@ int tgo_part_ms_settle_pairs(tgo_ctx* ctx, int32_t level, const int64_t* recv, c
         return fail(ctx, TGO_E_INVALID, "ms_settle_pairs: bad arguments");
     if (level + 1 >= (1 << kLevelPlanes)) return fail(ctx, TGO_E_UNSUPPORTED, "multi-source BFS levels are < 65536");
     if ((rc = ms_planes_for(ctx, level + 1))) return rc;
-    HIP_TRY(k_level_prep(s.cnt, fr_next, g.n_active, nullptr, st));   // the tail [n_active, n) stays zero
+    const bool direct = ctx->part_own_direct == fr_next;     // the push wrote the owned targets here
+    ctx->part_own_direct = nullptr;
+    HIP_TRY(k_level_prep(s.cnt, direct ? nullptr : fr_next, direct ? 0 : g.n_active, nullptr, st));   // tail stays zero
     int64_t npairs = 0;
     for (int r = 0; r < nslices; ++r) {
         if (recv_counts[r] < 0 || recv_counts[r] > g.n) return fail(ctx, TGO_E_INVALID, "ms_settle_pairs: bad count");
         npairs += recv_counts[r];
     }
     HIP_TRY(k_ms_or_pairs(recv, npairs, fr_next, st));
-    HIP_TRY(ms_or_own(ctx, fr_next));
+    if (!direct) HIP_TRY(ms_or_own(ctx, fr_next));
     const int nxt = ctx->part_cur ^ 1;
     if (ctx->part_count_only) {
         HIP_TRY(k_ms_settle_count(push_view(g, TGO_SCOPE_BOTH_E), g.n_active, s.ms_vis, fr_next, ms_planes(ctx), s.cnt,
@@ -3200,6 +3217,12 @@ int part_ms_settle_sums(tgo_ctx* ctx, int64_t* out, bool count_only) {
     HIP_TRY(hipMemsetAsync(out, 0, 64 * sizeof(int64_t), ctx->stream));
     ctx->part_srcent = reinterpret_cast<unsigned long long*>(out);
     return TGO_OK;
+}
+// The next tgo_part_ms_push writes its owned targets' candidates straight into next (with the
+// bypass on); nullptr cancels.
+void part_ms_own_next(tgo_ctx* ctx, uint64_t* next) {
+    ctx->part_own_next = next;
+    if (!next) ctx->part_own_direct = nullptr;
 }
 void part_ms_bypass(tgo_ctx* ctx, uint64_t* cand_global, int self) {
     ctx->part_ms_cand = cand_global;

@@ -679,7 +679,7 @@ hipError_t k_ms_queue(const View& push, int64_t n_active, const uint64_t* fr, in
 struct PackTouch { uint8_t* flag = nullptr; int64_t n_local = 1; int64_t cps = 1; };
 hipError_t k_ms_push(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen, const uint64_t* fr,
                      const uint64_t* vis, uint64_t* nx, hipStream_t s, PackTouch touch = {}, uint64_t mask = ~0ULL,
-                     bool probe = true);
+                     bool probe = true, uint64_t* own_nx = nullptr, int64_t own_lo = 0);
 constexpr int64_t kMsRangePairs = int64_t(1) << 22;   // ranged push: (entry, range) bounds per list
 // Target-ranged push of a small frontier (msbfs.hip): pairs (range of S targets, entry) in
 // range-major order, XCD x on the x-th eighth; P0 / P1 hold qlen * (R + 1), cnt / pre R * qlen + 1.

@@ -457,7 +457,8 @@ __global__ void __launch_bounds__(kBlock) ms_fbitmap(const uint64_t* __restrict_
 constexpr int kPushLds = 514;
 __global__ void __launch_bounds__(kBlock) ms_push(View push, const int32_t* __restrict__ q,
         const int64_t* __restrict__ qpre, int64_t qlen, const uint64_t* __restrict__ fr,
-        const uint64_t* __restrict__ vis, uint64_t* __restrict__ nx, PackTouch touch, uint64_t mask, bool probe) {
+        const uint64_t* __restrict__ vis, uint64_t* __restrict__ nx, PackTouch touch, uint64_t mask, bool probe,
+        uint64_t* __restrict__ own_nx, int64_t own_lo) {
     __shared__ int64_t s_pre[kPushLds];
     __shared__ int64_t s_b0[kPushLds];     // list 0 begin
     __shared__ int64_t s_b1[kPushLds];     // list 1 begin minus list 0's length (o >= d0 reads adj1[s_b1 + o])
@@ -535,22 +536,28 @@ __global__ void __launch_bounds__(kBlock) ms_push(View push, const int32_t* __re
             }
         }
         uint64_t cv[kEdgesPerThread], cn[kEdgesPerThread];
+        uint64_t* tgt[kEdgesPerThread];
 #pragma unroll
         for (int k = 0; k < kEdgesPerThread; ++k) {           // 3: the neighbour's masks
             cv[k] = 0;
             cn[k] = 0;
+            tgt[k] = nullptr;
             if (v[k] < 0) continue;
-            // partitioned graphs pass vis = nullptr: remote vertices' masks are not local
+            // partitioned graphs pass vis = nullptr: remote vertices' masks are not local; with
+            // own_nx the owned range [own_lo, own_lo + n_local) goes straight to the next masks
+            const int64_t ov = static_cast<int64_t>(v[k]) - own_lo;
+            tgt[k] = (own_nx && ov >= 0 && ov < touch.n_local) ? own_nx + ov : nx + v[k];
             if (vis) cv[k] = vis[v[k]];
-            if (probe) cn[k] = nx[v[k]];
+            if (probe) cn[k] = *tgt[k];
         }
 #pragma unroll
         for (int k = 0; k < kEdgesPerThread; ++k) {           // 4: the atomic
             if (v[k] < 0) continue;
             const uint64_t mk = m[k] & ~cv[k];
             if (mk && (cn[k] & mk) != mk) {
-                atomicOr(reinterpret_cast<unsigned long long*>(&nx[v[k]]), mk);
-                if (touch.flag) touch.flag[(v[k] / touch.n_local) * touch.cps + (v[k] % touch.n_local) / kPackChunk] = 1;
+                atomicOr(reinterpret_cast<unsigned long long*>(tgt[k]), mk);
+                if (touch.flag && tgt[k] == nx + v[k])
+                    touch.flag[(v[k] / touch.n_local) * touch.cps + (v[k] % touch.n_local) / kPackChunk] = 1;
             }
         }
         __syncthreads();
@@ -1050,8 +1057,9 @@ hipError_t k_ms_queue(const View& push, int64_t n_active, const uint64_t* fr, in
     return hipGetLastError();
 }
 hipError_t k_ms_push(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen, const uint64_t* fr,
-                     const uint64_t* vis, uint64_t* nx, hipStream_t s, PackTouch touch, uint64_t mask, bool probe) {
-    ms_push<<<256 * 8, kBlock, 0, s>>>(push, q, qpre, qlen, fr, vis, nx, touch, mask, probe);
+                     const uint64_t* vis, uint64_t* nx, hipStream_t s, PackTouch touch, uint64_t mask, bool probe,
+                     uint64_t* own_nx, int64_t own_lo) {
+    ms_push<<<256 * 8, kBlock, 0, s>>>(push, q, qpre, qlen, fr, vis, nx, touch, mask, probe, own_nx, own_lo);
     return hipGetLastError();
 }
 hipError_t k_ms_push_ranged(const View& push, const int32_t* q, int64_t qlen, int64_t n_active, int64_t S,

@@ -314,6 +314,8 @@ int64_t* part_dcounts_of(tgo_ctx* ctx);
 void part_ms_bypass(tgo_ctx* ctx, uint64_t* cand_global, int self);
 // the next settle sums its new frontier's push entries per source into out (one-shot)
 int part_ms_settle_sums(tgo_ctx* ctx, int64_t* out, bool count_only = false);
+// the next push writes its owned targets straight into next (bypass on); nullptr cancels
+void part_ms_own_next(tgo_ctx* ctx, uint64_t* next);
 // device words to the host through the mapped counter page (no stream synchronisation)
 int part_read_words(tgo_ctx* ctx, const int64_t* dev, int count, int64_t* out);
 double ms_split_of(const tgo_ctx* ctx);
@@ -651,6 +653,7 @@ extern "C" int tgo_part_msbfs_run(tgo_ctx* ctx, tgo_exchange* x, const int64_t* 
             }
             if ((rc = tgo_part_ms_pull_split(ctx, level, glob[0], frn, sparse, with_cand, nullptr))) break;
         } else {
+            part_ms_own_next(ctx, frn);                 // owned candidates straight into frn
             if ((rc = tgo_part_ms_push(ctx, level, fr, cand))) break;
             // the settle sums the per-source entries when the next level may pull (this
             // frontier's entries within 64x of the pull threshold), as the one-GPU sweep
@@ -676,6 +679,7 @@ extern "C" int tgo_part_msbfs_run(tgo_ctx* ctx, tgo_exchange* x, const int64_t* 
     const int rc_off = tgo_part_device_counts(ctx, caller_dc);
     trace_resolve(st);
     (void)part_ms_settle_sums(ctx, nullptr);          // a failed level may have left it armed
+    part_ms_own_next(ctx, nullptr);
     if (rc) {
         x->abort();
         rezero();
