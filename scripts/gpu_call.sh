@@ -1,14 +1,16 @@
 #!/bin/bash
-# Partitioned push straight into the next masks for owned targets: distributed parity (world
-# 1/2/4 in-process, scale 27 world 2) and the world-1 partitioned bench.
+# Pull-shape sweeps equal (new test), then split budget / direction switch A/B with the
+# 64-entry long-list trips.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
-T=r04z8
+T=r04z9
 mkdir -p gpurun_out/$T
-timeout -k 10 800 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_distributed.py \
-    tests/test_gpu_fullsize.py tests/test_gpu_scale27.py -k "msbfs or multi or partitioned or world" > gpurun_out/$T/parity.log 2>&1
+timeout -k 10 800 python -u -m pytest -x -v --timeout 600 --timeout-method thread tests/test_gpu_parity.py \
+    -k "pull_shapes or settle_sums" > gpurun_out/$T/parity.log 2>&1
 rc=$?; tail -3 gpurun_out/$T/parity.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 600 python3 bench.py --partitioned --cpu-baseline 0 --rows-scale 0 --sssp-roots 0 \
-    > gpurun_out/$T/bench_part.json 2> gpurun_out/$T/bench_part.err
-rc=$?; cut -c1-300 gpurun_out/$T/bench_part.json; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python3 scripts/ms_levels.py 24 3 > gpurun_out/$T/ms_levels.log 2>&1
-rc=$?; head -14 gpurun_out/$T/ms_levels.log; exit $rc
+for v in "TGO_MS_SPLIT=0.005" "TGO_MS_SPLIT=0" "TGO_MS_SPLIT=0.002" "TGO_MS_SPLIT=0.01" "TGO_MS_SPLIT=0.02" \
+         "TGO_MS_ALPHA=8" "TGO_MS_ALPHA=16" "TGO_MS_ALPHA=24" \
+         "TGO_MS_SPLIT=0.005" "TGO_MS_SPLIT=0" "TGO_MS_SPLIT=0.002" "TGO_MS_SPLIT=0.01" "TGO_MS_SPLIT=0.02" \
+         "TGO_MS_ALPHA=8" "TGO_MS_ALPHA=16" "TGO_MS_ALPHA=24"; do
+    env $v timeout -k 10 300 python3 scripts/ms_probe.py 24 5 > gpurun_out/$T/ab.tmp 2>&1
+    rc=$?; echo "$v: $(tail -1 gpurun_out/$T/ab.tmp)" | cut -c1-110 | tee -a gpurun_out/$T/ab.log; [ $rc -eq 0 ] || exit $rc
+done

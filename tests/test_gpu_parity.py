@@ -277,6 +277,24 @@ def test_multi_source_settle_sums_and_ranged_push():
     assert plain == checked == ranged
 
 
+@pytest.mark.parametrize("env", [{"TGO_MS_LONG": "4"}, {"TGO_MS_LONG": "2"}, {"TGO_MS_LONG": "8"},
+                                 {"TGO_MS_RAMP": "1"}, {"TGO_MS_STEP": "4"}, {"TGO_MS_STEP": "16", "TGO_MS_LONG": "4"},
+                                 {"TGO_MS_COOP": "8"}, {"TGO_MS_COOP": "1000"}, {"TGO_MS_PUSH_PROBE": "0"},
+                                 {"TGO_MS_PUSH_LIGHT": "0"}])
+def test_multi_source_pull_shapes_give_the_same_levels(env):
+    """The pull's walk shapes (long-list trip 64 / 128 / 256 / 512 entries, a 64-entry first trip,
+    4 / 8 / 16 entries per short-list round trip, the wave-cooperative threshold) and the push's
+    probe / reached-mask read only change how much is read before a walk stops: every sweep
+    equals the default's, level for level (fresh processes: the switches are read once)."""
+    if "base" not in _MS_BASE:
+        _MS_BASE["base"] = _ms_sweeps()[0]
+    other, _ = _ms_sweeps(**env)
+    assert other == _MS_BASE["base"], env
+
+
+_MS_BASE = {}
+
+
 @pytest.mark.parametrize("scope", [BOTH, IN, OUT])
 @pytest.mark.parametrize("cold,split", [(0, -1.0), (1, -1.0), (300, -1.0), (300, 0.0), (1000, 0.3), (64, 1.0)])
 def test_multi_source_cold_split_level(rmat12, scope, cold, split):
