@@ -543,36 +543,22 @@ __global__ void __launch_bounds__(kBlock) ds_relax_dev(const int64_t* __restrict
             const long long old = atomicMin(reinterpret_cast<long long*>(&dist[tk]), static_cast<long long>(cand[k]));
             if (cand[k] >= old) continue;
             const uint64_t bit = 1ULL << (tk & 63);
-            // the old pending word matters only for a take into the near queue (cand < thr): a
-            // far improvement sets its bit with a non-returning atomic after its pile slot (so
-            // the two atomics are not merged into one returning form), no wait on the result
-            auto far = [&]() {
-                if (kBins) {
-                    const int64_t ahead = cand[k] / delta - bucket;
-                    if (ahead >= nbins) {
-                        spill = true;
-                    } else {
-                        fb[k] = static_cast<int32_t>((bucket + ahead) % nbins);
-                        fl[k] = atomicAdd(&s_bn[fb[k]], 1u);
-                    }
-                } else if (cand[k] < tmin) {
-                    tmin = cand[k];
-                }
-            };
-            if (cand[k] < thr) {
-                const unsigned long long ob = atomicOr(reinterpret_cast<unsigned long long*>(&pend[tk >> 6]), bit);
-                if (!(ob & bit)) {
-                    tv[k] = tk;
-                    td[k] = light_deg(off, light, tk);
-                    ++ntake;
-                    dtake += td[k];
+            const unsigned long long ob = atomicOr(reinterpret_cast<unsigned long long*>(&pend[tk >> 6]), bit);
+            if (!(ob & bit) && cand[k] < thr) {
+                tv[k] = tk;
+                td[k] = light_deg(off, light, tk);
+                ++ntake;
+                dtake += td[k];
+            } else if (kBins) {
+                const int64_t ahead = cand[k] / delta - bucket;
+                if (ahead >= nbins) {
+                    spill = true;
                 } else {
-                    far();
+                    fb[k] = static_cast<int32_t>((bucket + ahead) % nbins);
+                    fl[k] = atomicAdd(&s_bn[fb[k]], 1u);
                 }
-            } else {
-                far();
-                __hip_atomic_fetch_or(reinterpret_cast<unsigned long long*>(&pend[tk >> 6]), bit, __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_AGENT);
+            } else if (cand[k] < tmin) {
+                tmin = cand[k];
             }
         }
         if (kBins) {                                          // the tile's far appends, per pile
