@@ -13,6 +13,7 @@
 //               neighbour in the frontier bitmap (one wave per 64-vertex bitmap word,
 //               so visited/next bitmap words are written without atomics).
 // Wave = 64 lanes; ballots are 64-bit.
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 #include "frontier.hpp"
@@ -75,7 +76,7 @@ __global__ void __launch_bounds__(kBlock) td_expand(View push, const int32_t* __
 // top-down.  No block barrier inside, so waves with long lists do not hold up the block.
 __global__ void __launch_bounds__(kBlock) bu_step(View pull, View push, int64_t n,
         const uint64_t* __restrict__ fb, uint64_t* __restrict__ vb, uint64_t* __restrict__ nb,
-        int32_t* __restrict__ level, Counters* cnt, int32_t next_level) {
+        int32_t* __restrict__ level, Counters* cnt, int32_t next_level, int64_t serial) {
     unsigned long long nv = 0, mf = 0;
     const int64_t words = (n + 63) >> 6;
     for (int64_t b = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock; b < words;
@@ -92,7 +93,7 @@ __global__ void __launch_bounds__(kBlock) bu_step(View pull, View push, int64_t 
         }
         const int64_t deg = (e0 - b0) + (e1 - b1);
         // short lists: the lane scans its own list and stops at the first frontier hit
-        if (open && deg <= kSerialScan) {
+        if (open && deg <= serial) {
             // 4 entries per step: their index loads and bitmap probes issue together, so a
             // lane pays one dependent round trip per 4 entries instead of per entry.
             for (int l = 0; l < 2 && !found; ++l) {
@@ -110,7 +111,7 @@ __global__ void __launch_bounds__(kBlock) bu_step(View pull, View push, int64_t 
             }
         }
         // long lists: the whole wave scans one list 64 entries at a time (ballot exit)
-        unsigned long long big = __ballot(open && deg > kSerialScan);
+        unsigned long long big = __ballot(open && deg > serial);
         while (big) {
             const int src = __ffsll(static_cast<long long>(big)) - 1;
             big &= big - 1;
@@ -331,7 +332,10 @@ hipError_t k_bu_step(const View& pull, const View& push, int64_t n, const uint64
     // one wave per bitmap word, all launched at once: the dispatcher keeps every CU full
     // and a wave's dependent probe chain overlaps with hundreds of others.
     const int64_t words = (n + 63) / 64;
-    bu_step<<<grid_for(words * 64, kBlock, 8192), kBlock, 0, s>>>(pull, push, n, fb, vb, nb, level, cnt, next_level);
+    // TGO_BFS_SERIAL: lists up to this many entries are scanned by their own lane (32 default)
+    static const int64_t serial = [] { const char* e = std::getenv("TGO_BFS_SERIAL"); return e ? std::atoll(e) : kSerialScan; }();
+    bu_step<<<grid_for(words * 64, kBlock, 8192), kBlock, 0, s>>>(pull, push, n, fb, vb, nb, level, cnt, next_level,
+                                                                  serial);
     return hipGetLastError();
 }
 hipError_t k_bfs_queue(const View& push, int64_t n, const uint64_t* fb, int32_t* qn, int64_t* qdeg, Counters* cnt,
