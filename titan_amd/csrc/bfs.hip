@@ -22,7 +22,10 @@ namespace tgo {
 
 namespace {
 
-constexpr int64_t kSerialScan = 32;    // bottom-up: longer lists are scanned by the whole wave
+// bottom-up: longer lists are scanned by the whole wave.  128 (round 4; 32 before): single-
+// source hmean over 8 RMAT-24 roots 277-280 GTEPS at 32, 240-245 at 16, 273-276 at 64, 310-314 at
+// 128 (profiles/r04za_bfs_serial_ab.log)
+constexpr int64_t kSerialScan = 128;
 
 __global__ void fill_i32(int32_t* p, int32_t v, int64_t n) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = v;
@@ -332,7 +335,7 @@ hipError_t k_bu_step(const View& pull, const View& push, int64_t n, const uint64
     // one wave per bitmap word, all launched at once: the dispatcher keeps every CU full
     // and a wave's dependent probe chain overlaps with hundreds of others.
     const int64_t words = (n + 63) / 64;
-    // TGO_BFS_SERIAL: lists up to this many entries are scanned by their own lane (32 default)
+    // TGO_BFS_SERIAL: lists up to this many entries are scanned by their own lane (kSerialScan default)
     static const int64_t serial = [] { const char* e = std::getenv("TGO_BFS_SERIAL"); return e ? std::atoll(e) : kSerialScan; }();
     bu_step<<<grid_for(words * 64, kBlock, 8192), kBlock, 0, s>>>(pull, push, n, fb, vb, nb, level, cnt, next_level,
                                                                   serial);
