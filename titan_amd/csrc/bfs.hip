@@ -22,10 +22,11 @@ namespace tgo {
 
 namespace {
 
-// bottom-up: longer lists are scanned by the whole wave.  128 (round 4; 32 before): single-
-// source hmean over 8 RMAT-24 roots 277-280 GTEPS at 32, 240-245 at 16, 273-276 at 64, 310-314 at
-// 128 (profiles/r04za_bfs_serial_ab.log)
-constexpr int64_t kSerialScan = 128;
+// bottom-up: longer lists are scanned by the whole wave.  256 (round 4; 32 before): single-
+// source hmean over 8 RMAT-24 roots 277-280 GTEPS at 32, 240-245 at 16, 273-276 at 64, 300-314 at
+// 128, 322-329 at 256, 316-320 at 512, 318-324 at 1024 (profiles/r04za_bfs_serial_ab.log) — a
+// lane's own walk stops at its first frontier hit, the wave's walk pays a round trip per 64
+constexpr int64_t kSerialScan = 256;
 
 __global__ void fill_i32(int32_t* p, int32_t v, int64_t n) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = v;
