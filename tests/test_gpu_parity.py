@@ -396,6 +396,32 @@ def test_rmat_sssp_delta_zero_weights(rmat12):
             assert np.array_equal(d, oracle.shortest_distance(int(ids[r]), n, OUT, weighted=True)[0])
 
 
+@pytest.mark.parametrize("scope", [OUT, IN])
+@pytest.mark.parametrize("done,pull", [(0, 0), (1, 0), (0, 0.001), (1, 0.001), (1, 1.0)])
+def test_sssp_delta_bucket_merge(scope, done, pull):
+    """A bucket merge in the binned loop (delta 10): s -10-> a, s -35-> z, a -10-> y, z -4-> c,
+    y -10-> c.  When bucket 1 (a) finishes, pile 2 is empty and pile 3 holds z, so the loop
+    jumps to bucket 3 while a's heavy entry puts y (20) into the near queue: buckets 2..3 merge.
+    z's light entry gives c 39; y's heavy entry, relaxed at the merged range's finish, must
+    still lower c to 30 — with the done filter and the pull form, whose members are final only
+    after a single bucket (the merged range once marked c done)."""
+    n = 5
+    src = np.array([0, 0, 1, 2, 3], np.int64)
+    dst = np.array([1, 2, 3, 4, 4], np.int64)
+    w = np.array([10, 35, 10, 4, 10], np.int32)
+    if scope == IN:                        # an inE scope's messages travel against the edges
+        src, dst = dst, src
+    ids = (np.arange(n, dtype=np.int64) + 1) << 3
+    off, mid, adj, ww = numpy_adjacency(n, src, dst, w)
+    oracle = fr.OracleGraph.from_adjacency(ids, off, mid, adj, ww)
+    od = oracle.shortest_distance(int(ids[0]), n, scope, weighted=True)[0]
+    assert list(od) == [0, 10, 35, 20, 30]
+    eng = Engine().load_edges(n, src, dst, scope, weight=w)
+    eng.set_tuning(L.TUNE_DS_BINS, 1).set_tuning(L.TUNE_DS_DONE, done).set_tuning(L.TUNE_DS_PULL, pull)
+    d = eng.sssp(0, n, scope, mode=L.SSSP_DELTA, seed_is_dense=True, delta=10)
+    assert np.array_equal(d, od), (d, od)
+
+
 def test_sssp_tree_delta():
     rows, vids, sd, npz = load_fixture("sssp_tree")
     wk = int(npz["weight_key"])

@@ -11,7 +11,7 @@
 //        + commit  (snapshot the queue's distances, clear their pending bits, mark members)
 //        + relax   (the queue's entries, edge-balanced; appends the next near queue)
 // Two changes make this possible:
-//   * queue counters are packed (count << 36 | entries), so ONE atomicAdd per block reserves
+//   * queue counters are packed (count << kDsCountShift | entries), so ONE atomicAdd per block reserves
 //     both the queue slots and the entry range: the appender writes the exclusive prefix of
 //     the entries directly (qpre), and no scan pass is needed before the next relax;
 //   * the minimum pending distance is never scanned for: it is min(tm, lo), where tm is the
@@ -115,6 +115,7 @@ __global__ void ds_loop_seed(const int64_t* off, const int64_t* light, int64_t* 
     L->spill = 0;
     L->full_scans = 0;
     L->xfin = 0;
+    L->mlo = 0;
     L->xpull = 0;
     L->pulls = 0;
     L->pbucket = 0;
@@ -167,11 +168,16 @@ __device__ void decide_bins(DsLoop* L, int cur, int64_t delta, int nbins, int64_
     int b = static_cast<int>(k % nbins);
     unsigned long long c = load_agent(&L->bc[b]);
     const bool finished = c == 0;
+    // the finished range [mlo, kfin] is one bucket: its members are final (done, pull floor)
+    const bool single = finished && L->mlo == kfin;
     if (finished) {
         int j = 1;
         while (j < nbins && load_agent(&L->bc[(k + j) % nbins]) == 0) ++j;
         if (j < nbins) {
             k += j;
+            // the members' heavy entries pushed in this step reach buckets >= kfin + 1 and are
+            // taken into the near queue below the new threshold: buckets kfin+1 .. k merge
+            L->mlo = L->mcount > 0 ? kfin + 1 : k;
             L->bucket = k;
             L->thr = (k + 1) * delta;
             L->buckets += 1;
@@ -189,7 +195,7 @@ __device__ void decide_bins(DsLoop* L, int cur, int64_t delta, int nbins, int64_
     L->xcount = b >= 0 ? (c < static_cast<unsigned long long>(cap) ? c : static_cast<unsigned long long>(cap)) : 0;
     L->xm = finished ? L->mcount : 0;
     if (finished) L->mcount = 0;
-    L->xfin = finished ? 1 : 0;
+    L->xfin = single ? 1 : 0;
     L->extract = 2;
     if (b >= 0) {
         L->bc[b] = 0;
@@ -206,7 +212,7 @@ __device__ void decide_bins(DsLoop* L, int cur, int64_t delta, int nbins, int64_
     }
     // A large finished bucket pulls its heavy entries (ds_pull_heavy) instead of pushing them;
     // its members go to pull list j & 1 and the previous pull's list is cleared on the way.
-    if (L->extract == 2 && pull_min > 0 && L->xm >= static_cast<unsigned long long>(pull_min)) {
+    if (L->extract == 2 && single && pull_min > 0 && L->xm >= static_cast<unsigned long long>(pull_min)) {
         const unsigned long long j = L->pulls;
         L->xpull = 1;
         L->pbucket = kfin;
@@ -316,6 +322,7 @@ __global__ void __launch_bounds__(kBlock) ds_extract_bins(const int64_t* __restr
     if (mode != 2) return;
     const int64_t thr = L->thr;
     const bool xpull = L->xpull != 0;
+    const bool xfin = L->xfin != 0;
     const unsigned long long j = L->pulls;
     uint64_t* __restrict__ pm = pull.pm[j & 1];
     int32_t* __restrict__ pl_now = pull.pl[j & 1];
@@ -341,10 +348,11 @@ __global__ void __launch_bounds__(kBlock) ds_extract_bins(const int64_t* __restr
                     deg = light_deg(off, light, v);
                 }
             }
-        } else if (i < xme) {                                 // a finished bucket's member: final
+        } else if (i < xme) {                                 // a finished bucket's member
             const int32_t v = mlist[i - xc];
             member[v >> 6] = 0;
-            atomicOr(reinterpret_cast<unsigned long long*>(&done[v >> 6]), 1ULL << (v & 63));
+            if (xfin)                                         // final only after a single bucket
+                atomicOr(reinterpret_cast<unsigned long long*>(&done[v >> 6]), 1ULL << (v & 63));
             if (xpull) {                                      // its heavy entries are pulled
                 atomicOr(reinterpret_cast<unsigned long long*>(&pm[v >> 6]), 1ULL << (v & 63));
                 pl_now[i - xc] = v;

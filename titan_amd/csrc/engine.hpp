@@ -450,7 +450,11 @@ struct Counters {               // device-side level counters (one cache line ea
 };
 
 // State of the device-driven delta-stepping loop (delta_loop.hip), in device memory.
-constexpr int kDsCountShift = 36;   // queue counters: count << 36 | entries (one atomic reserves both)
+constexpr int kDsCountShift = 35;   // queue counters: count << 35 | entries (one atomic reserves both):
+                                    // counts < 2^29 (a queue holds <= 2n + 2 takes: n <= 2^28 - 1),
+                                    // entries < 2^35 (RMAT-27 bothE: 2^32)
+static_assert((int64_t(1) << (64 - kDsCountShift)) > 2 * (int64_t(1) << 27) + 2,
+              "the device delta loop must hold a scale-27 queue (api.cpp run_delta_split guard)");
 // Binned form (kDsMaxBins piles): a relaxation that improves a vertex to a distance of a later
 // bucket appends it to that bucket's pile; the next bucket is extracted from its pile, not by
 // a scan of the whole pending bitmap (delta_loop.hip).
@@ -474,7 +478,11 @@ struct DsLoop {
     unsigned long long spill;   // a candidate beyond the piles' reach (cannot happen when the
                                 // piles cover the largest weight; the host then reruns unbinned)
     unsigned long long full_scans;        // extractions by the bitmap scan (large or overflowed piles)
-    unsigned long long xfin;    // the decided extraction follows a finished bucket (members final)
+    unsigned long long xfin;    // the decided extraction follows a finished single bucket (members final)
+    long long mlo;              // lowest bucket of the current range: a jump over empty piles
+                                // while the finished bucket's heavy entries are pushed lets
+                                // them land in the skipped buckets, which merge into the range
+                                // [mlo, bucket]; only a single-bucket range has final members
     // pull form of a large finished bucket's heavy entries (ds_pull_heavy)
     unsigned long long xpull;   // this step pulls instead of queueing the members' heavy entries
     unsigned long long pulls;   // pulls so far (pull j uses bitmap / list j & 1)

@@ -75,9 +75,12 @@ struct RcclExchange : tgo_exchange {
         if (comm) (void)ncclCommDestroy(comm);
         release_pinned();
     }
-    // A rank that fails between collectives (a local step's error, a HIP error) would leave
-    // its peers blocked in the next collective forever: abort the communicator, which makes
-    // their pending and later RCCL calls return an error, and refuse further use here.
+    // A rank that fails between collectives (a local step's error, a HIP error) aborts its own
+    // communicator and refuses further use here, so it returns the error at once instead of
+    // entering another collective.  ncclCommAbort does NOT notify the peers: a peer already
+    // in, or about to enter, a collective with this rank waits until its launcher ends it.
+    // One process per GPU under torch.distributed.run provides that: the failed rank exits
+    // with an error and the launcher terminates the rest of the group.
     void abort() override {
         if (comm) (void)ncclCommAbort(comm);
         comm = nullptr;

@@ -6,7 +6,8 @@
 // load, ~4.5 s, in a different phase each time: profiles/r04f_load27.log), while reusing
 // memory the process already touched is fast.  So a freed temporary of >= 64 MB is kept and
 // handed to the next request it fits (best fit within 2x), and every load entry point trims
-// the cache when it ends (tgo::tmp_trim), so nothing stays reserved between loads.
+// the cache when it ends (tgo::tmp_trim), so nothing stays reserved between loads.  Cached
+// blocks and the copy-out staging are per device: contexts on different GPUs may load at once.
 #include <algorithm>
 #include <chrono>
 #include <cstdint>
@@ -15,6 +16,7 @@
 #include <cstring>
 #include <mutex>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include <sys/mman.h>
@@ -24,9 +26,18 @@
 namespace tgo {
 namespace {
 constexpr size_t kCacheMin = size_t(64) << 20;
-struct Block { void* p; size_t bytes; };
+struct Block { void* p; size_t bytes; int dev; };
 std::mutex g_mu;
 std::vector<Block> g_free;
+// real sizes of the cached blocks handed out (a reuse may be up to 2x the request; the caller
+// frees with its request, and the block goes back to the cache with its real size)
+std::unordered_map<void*, size_t> g_real;
+
+int current_device() {
+    int d = 0;
+    if (hipGetDevice(&d) != hipSuccess) { (void)hipGetLastError(); d = 0; }
+    return d;
+}
 
 // TGO_TRACE=1: a driver call of >= 50 ms on stderr (the load laps show which phase stalls,
 // this shows whether an allocation or a device synchronisation is the stall)
@@ -45,17 +56,19 @@ hipError_t timed(const char* what, size_t bytes, F&& f) {
 hipError_t tmp_alloc(void** p, size_t bytes) {
     *p = nullptr;
     if (bytes >= kCacheMin) {
+        const int dev = current_device();
         std::lock_guard<std::mutex> lk(g_mu);
         size_t best = g_free.size();
         for (size_t i = 0; i < g_free.size(); ++i)
-            if (g_free[i].bytes >= bytes && g_free[i].bytes <= 2 * bytes &&
+            if (g_free[i].dev == dev && g_free[i].bytes >= bytes && g_free[i].bytes <= 2 * bytes &&
                 (best == g_free.size() || g_free[i].bytes < g_free[best].bytes))
                 best = i;
         if (best < g_free.size()) {
             *p = g_free[best].p;
+            g_real[*p] = g_free[best].bytes;
             g_free.erase(g_free.begin() + static_cast<long>(best));
-            // its previous user's work may still be queued (on any stream, host copies included):
-            // hand it out only once the device is idle
+            // its previous user's work may still be queued (on any stream of this device, host
+            // copies included): hand it out only once the device is idle
             return timed("reuse sync", bytes, [] { return hipDeviceSynchronize(); });
         }
     }
@@ -72,13 +85,20 @@ hipError_t tmp_alloc(void** p, size_t bytes) {
     return e;
 }
 
-// the block's size must be the one it was allocated with (the caller's request, or more when
-// it came from the cache: callers pass their request; a cached block's real size is kept here)
+// callers pass their request size; a block that came from the cache goes back with its real
+// size (g_real), and every block is cached under the device current at its free — the one it
+// was allocated on, as every caller allocates and frees under the same context
 void tmp_free(void* p, size_t bytes) {
     if (!p) return;
     if (bytes >= kCacheMin) {
+        const int dev = current_device();
         std::lock_guard<std::mutex> lk(g_mu);
-        g_free.push_back({p, bytes});
+        const auto it = g_real.find(p);
+        if (it != g_real.end()) {
+            bytes = std::max(bytes, it->second);
+            g_real.erase(it);
+        }
+        g_free.push_back({p, bytes, dev});
         return;
     }
     (void)hipFree(p);
@@ -103,12 +123,26 @@ hipError_t copy_d2h(void* dst, const void* src, size_t bytes) {
         return hipSuccess;
     };
     if (bytes < 4 * kPiece) return plain();
-    static std::mutex mu;
-    static void* pin[2] = {nullptr, nullptr};
-    static hipStream_t st = nullptr;
-    static hipEvent_t ev[2] = {nullptr, nullptr};
-    static bool ready = false, failed = false;
-    std::lock_guard<std::mutex> lk(mu);
+    // the staging stream, events and pinned buffers of the current device (a stream belongs to
+    // the device it was created on: another device's copies must not go through it)
+    struct Staging {
+        std::mutex mu;
+        void* pin[2] = {nullptr, nullptr};
+        hipStream_t st = nullptr;
+        hipEvent_t ev[2] = {nullptr, nullptr};
+        bool ready = false, failed = false;
+    };
+    constexpr int kMaxDevices = 64;
+    static Staging per_dev[kMaxDevices];
+    const int dev = current_device();
+    if (dev < 0 || dev >= kMaxDevices) return plain();
+    Staging& S = per_dev[dev];
+    std::lock_guard<std::mutex> lk(S.mu);
+    void** const pin = S.pin;
+    hipEvent_t* const ev = S.ev;
+    hipStream_t& st = S.st;
+    bool& ready = S.ready;
+    bool& failed = S.failed;
     if (!ready && !failed) {
         failed = hipHostMalloc(&pin[0], kPiece, hipHostMallocDefault) != hipSuccess ||
                  hipHostMalloc(&pin[1], kPiece, hipHostMallocDefault) != hipSuccess ||
