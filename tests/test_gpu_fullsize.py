@@ -193,11 +193,12 @@ def test_wide_bitmap_single_source_bfs():
 def test_config5_rmat24_weighted_sssp_partitioned(rmat24, world):
     """configs[4] partitioned: the bench's weighted, capped RMAT-24 inE graph over `world`
     ranks (equal ranges, degree-grouped global layout, one device, ranks as threads with the
-    drivers' collectives in-process) — delta-stepping distances equal the one-GPU engine's bit
-    for bit (that engine is oracle-pinned in test_config5_rmat24_weighted_sssp), reached
-    counts global, every rank through the same phases."""
+    drivers' collectives in-process) — the native loop bench.py times at N > 1
+    (tgo_part_sssp_run) gives delta-stepping distances equal to the one-GPU engine's bit for bit
+    (that engine is oracle-pinned in test_config5_rmat24_weighted_sssp) for both roots, reached
+    counts global, every rank through the same phases; the Python driver agrees on one root."""
     from test_gpu_distributed import Ranks
-    from titan_amd.distributed import distributed_sssp
+    from titan_amd.distributed import NativeExchange, distributed_sssp, distributed_sssp_native
     n, src, dst, roots, w = rmat24
     one = Engine(host_threads=THREADS).load_edges(n, src, dst, IN, weight=w, apply_cap=True)
     picked = []
@@ -209,8 +210,13 @@ def test_config5_rmat24_weighted_sssp_partitioned(rmat24, world):
             break
     del one
     ranks = Ranks(world, n, src, dst, IN, weight=w, layout=True, apply_cap=True)
+    xs = NativeExchange.local_group(world)
     for r, d, reached in picked:
-        res = ranks.run(lambda be, comm: distributed_sssp(be, r, 0, comm=comm))
+        res = ranks.run(lambda be, comm: distributed_sssp_native(be, r, xs[comm.rank]))
         assert np.array_equal(np.concatenate([x[0] for x in res]), d), r
         assert all(x[1][0] == reached for x in res)
         assert len({x[2] for x in res}) == 1
+    r, d, reached = picked[0]
+    res = ranks.run(lambda be, comm: distributed_sssp(be, r, 0, comm=comm))
+    assert np.array_equal(np.concatenate([x[0] for x in res]), d), r
+    assert all(x[1][0] == reached for x in res)

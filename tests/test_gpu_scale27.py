@@ -11,9 +11,11 @@ frontier exchange".  A 288 GB MI355X holds the whole graph, so the one-GPU box r
   capped inE graph is bitwise reproducible (PageRankVertexProgram.java:75-95);
 * the PARTITIONED path at scale 27, world 2, in one process (two engines, two streams, the
   ranks as threads; collectives through tgo_exchange_local_group / InProcessGroup, the same
-  protocol RCCL carries between processes): the native multi-source sweep (tgo_part_msbfs_run)
-  and the Python single-source driver equal the one-GPU results bit for bit, and the capped,
-  cache-blocked partitioned PageRank(20) is within 1e-6 L1 of the one-GPU ranks.
+  protocol RCCL carries between processes) — the exact native loops `bench.py --gpus N` times:
+  the multi-source sweep (tgo_part_msbfs_run) and the single-source BFS (tgo_part_bfs_run, two
+  seeds) equal the one-GPU results bit for bit, and the capped, cache-blocked PageRank(20)
+  (tgo_part_pagerank_run) is bitwise equal between the ghost exchange and the all-gather and
+  within 1e-6 L1 of the one-GPU ranks; the Python reference drivers agree with them.
 
 The one-GPU path itself is pinned to the oracle at scale 24 (test_gpu_fullsize.py); scale 27 is
 too large for the oracle within a test's time, so parity here is against that pinned path.
@@ -27,8 +29,9 @@ import torch
 
 from titan_amd import Engine, pick_roots, rmat_edges
 from titan_amd import _lib as L
-from titan_amd.distributed import (NativeExchange, distributed_bfs, distributed_msbfs_native, distributed_pagerank,
-                                   pagerank_layout)
+from titan_amd.distributed import (PR_EXCHANGE_ALLGATHER, PR_EXCHANGE_GHOST, NativeExchange, distributed_bfs,
+                                   distributed_bfs_native, distributed_msbfs_native, distributed_pagerank,
+                                   distributed_pagerank_native, pagerank_layout)
 from test_gpu_distributed import Ranks
 
 pytestmark = pytest.mark.gpu
@@ -119,8 +122,9 @@ def test_config3_rmat27_one_gpu(rmat27, one_gpu27):
 
 def test_config3_rmat27_partitioned_world2(rmat27, one_gpu27, monkeypatch):
     """Two ranks of the scale-27 graph (equal vertex ranges, degree-grouped global layout) on
-    one device: the native multi-source sweep and the single-source driver against the one-GPU
-    sweep, then the capped cache-blocked partitioned PageRank(20) against the one-GPU ranks."""
+    one device, through the native loops bench.py runs at N > 1: the multi-source sweep and the
+    single-source BFS against the one-GPU sweep, then the capped cache-blocked PageRank(20) in
+    both exchange modes against the one-GPU ranks (and the Python drivers beside them)."""
     n, src, dst, roots = rmat27
     o = one_gpu27
     world = 2
@@ -137,14 +141,28 @@ def test_config3_rmat27_partitioned_world2(rmat27, one_gpu27, monkeypatch):
         assert np.array_equal(np.concatenate([x[3][i] for x in res]), o["levels"][i]), i
     del res
     for i in (0, 38):
-        got = ranks.run(lambda be, comm: distributed_bfs(be, roots[i], n, comm=comm))
+        got = ranks.run(lambda be, comm: distributed_bfs_native(be, roots[i], n, xs[comm.rank]))
         assert np.array_equal(np.concatenate([x[0] for x in got]), o["levels"][i]), i
-        assert got[0][1][0] == o["reached"][i]
-    del ranks, xs
+        assert got[0][1][0] == o["reached"][i] and got[1][1][0] == o["reached"][i]
+        assert got[0][2] == got[1][2]                                # every rank ran the same levels
+    got = ranks.run(lambda be, comm: distributed_bfs(be, roots[0], n, comm=comm))
+    assert np.array_equal(np.concatenate([x[0] for x in got]), o["levels"][0])
+    del ranks, got
     torch.cuda.empty_cache()
     pr_ranks = Ranks(world, n, src, dst, IN, layout=True, apply_cap=True)
     trunc = sum(be.e.stats()["truncated_results"] for be in pr_ranks.backends)
     assert trunc == o["truncated"]
+    ref = o["pr"]
+    fin = np.isfinite(ref)
+    native = {}
+    for mode in (PR_EXCHANGE_GHOST, PR_EXCHANGE_ALLGATHER):
+        res = pr_ranks.run(lambda be, comm: distributed_pagerank_native(be, 0.85, n, 20, xs[comm.rank], mode=mode))
+        native[mode] = (np.concatenate([x[0] for x in res]), sum(x[1] for x in res))
+        got = native[mode][0]
+        assert np.array_equal(np.isfinite(got), fin), mode
+        assert np.abs(got[fin] - ref[fin]).sum() <= PR_L1_TOL, mode
+    assert np.array_equal(native[PR_EXCHANGE_GHOST][0], native[PR_EXCHANGE_ALLGATHER][0])
+    assert 0 < native[PR_EXCHANGE_GHOST][1] < native[PR_EXCHANGE_ALLGATHER][1]   # the ghost exchange moves less
 
     def pr(be, comm):
         lay = pagerank_layout(be, comm=comm)
@@ -152,7 +170,5 @@ def test_config3_rmat27_partitioned_world2(rmat27, one_gpu27, monkeypatch):
     res = pr_ranks.run(pr)
     assert res[0][1][0] > 0                                    # the blocked hot-first layout ran
     got = np.concatenate([x[0] for x in res])
-    ref = o["pr"]
-    fin = np.isfinite(ref)
     assert np.array_equal(np.isfinite(got), fin)
     assert np.abs(got[fin] - ref[fin]).sum() <= PR_L1_TOL
