@@ -20,7 +20,8 @@ n = 1 << scale
 src, dst, _ = rmat_edges(scale, 16, seed=0x54495441)
 eng = None
 loaded_with = None
-KEYS = ("TGO_PR_BLOCKED", "TGO_PR_HOT", "TGO_PR_SEG", "TGO_PR_DIAG", "TGO_PR_PACK", "TGO_PR_CPACK", "TGO_PR_HOT_TILE", "TGO_PR_HOT_PIPE")
+KEYS = ("TGO_PR_BLOCKED", "TGO_PR_HOT", "TGO_PR_SEG", "TGO_PR_DIAG", "TGO_PR_PACK", "TGO_PR_CPACK", "TGO_PR_HOT_TILE", "TGO_PR_HOT_PIPE",
+        "TGO_PR_FX", "TGO_PR_FX_E", "TGO_PR_FX_COLD", "TGO_PR_FX_CE", "TGO_PR_FX_CP")
 variants = [
     {},
     {"TGO_PR_BLOCKED": "0"},
@@ -31,7 +32,8 @@ variants = [
     {"TGO_PR_DIAG": "-2:-1"},                 # no gathers at all: index stream + finalize
     {},
 ]
-RELOAD = ("TGO_PR_BLOCKED", "TGO_PR_HOT", "TGO_PR_SEG", "TGO_PR_PACK", "TGO_PR_CPACK", "TGO_PR_HOT_TILE", "TGO_PR_HOT_PIPE")   # read at load time
+RELOAD = ("TGO_PR_BLOCKED", "TGO_PR_HOT", "TGO_PR_SEG", "TGO_PR_PACK", "TGO_PR_CPACK", "TGO_PR_HOT_TILE", "TGO_PR_HOT_PIPE",
+          "TGO_PR_FX", "TGO_PR_FX_E", "TGO_PR_FX_COLD", "TGO_PR_FX_CE", "TGO_PR_FX_CP")   # read at load time
 if os.environ.get("PR_PROBE_DEFAULT_ONLY"):       # one variant: the TGO_PR_* settings of the caller's environment
     variants = [{k: os.environ[k] for k in KEYS if k in os.environ}]
 if os.environ.get("PR_PROBE_VARIANTS"):        # a JSON list of env dicts, e.g. '[{}, {"TGO_PR_SEG": "393216"}]'
@@ -55,10 +57,13 @@ for v in variants:
         eng.pagerank(0.85, n, iters, fetch=False)
         times.append(eng.stats()["last_kernel_ms"] / (iters - 1))
     pr = eng.pagerank(0.85, n, iters)
+    again = eng.pagerank(0.85, n, iters)
     if base is None:
         base = pr
+    fin = np.isfinite(base)
     rec = {"variant": v or "default", "ms_per_update": round(min(times), 4), "ms_all": [round(t, 4) for t in times],
-           "bitwise_equal_default": bool(np.array_equal(pr, base)), "l1_vs_default": float(np.abs(pr - base).sum())}
+           "reproducible": bool(np.array_equal(pr, again)),
+           "bitwise_equal_default": bool(np.array_equal(pr, base)), "l1_vs_default": float(np.abs(pr[fin] - base[fin]).sum())}
     out.append(rec)
     print(json.dumps(rec), flush=True)
 if os.environ.get("PR_PROBE_SAVE"):           # a digest of the ranks' bytes (bitwise comparison across runs)

@@ -290,11 +290,17 @@ int upload_cold_blocks(tgo_ctx* ctx, const std::vector<int64_t>& off, const std:
     };
     bool on_dev = false;
     win = std::min<int64_t>(win, kPrWinMax);        // the window and the waves' item buffers share 160 KB of LDS
+    // TGO_PR_FX_COLD (default on): fixed-point cold blocks (spmv.hip cold_fx) of up to 4096
+    // pieces and TGO_PR_FX_CE entries
+    const bool cold_fx = env_i64("TGO_PR_FX", 1) != 0 && env_i64("TGO_PR_FX_COLD", 1) != 0 && win == 0;
     if (d_off && d_adj && env_i64("TGO_HOST_ASSEMBLY", 0) == 0) {
         std::string err;
         if (int rc = build_cold_blocks_device(d_off, d_adj, static_cast<int64_t>(off.size()) - 1, d_nnz, n_src, hot,
-                                              env_i64("TGO_PR_SEG", kPrSegDefault), kTile, kMaxRows,
-                                              env_i64("TGO_PR_CPACK", 1) != 0, hc, on_dev, ctx->stream, err, win))
+                                              env_i64("TGO_PR_SEG", kPrSegDefault),
+                                              cold_fx ? env_i64("TGO_PR_FX_CE", 65536) : kTile,
+                                              cold_fx ? std::min<int64_t>(env_i64("TGO_PR_FX_CP", 4096), int64_t(1) << kPackShift)
+                                                      : kMaxRows,
+                                              env_i64("TGO_PR_CPACK", 1) != 0, hc, on_dev, ctx->stream, err, win, cold_fx))
             return fail(ctx, rc, err);
         if (on_dev) lap("build (device)");
     }
@@ -327,7 +333,43 @@ int upload_cold_blocks(tgo_ctx* ctx, const std::vector<int64_t>& off, const std:
     cb.num_cus = ctx->num_cus;
     const bool pack = env_i64("TGO_PR_PACK", 1) != 0;
     if (!pack) cb.hot_tile = static_cast<int>(kTile), cb.hot_shift = kPackShift;
-    if (on_dev) {                                   // hot tiles packed on the device
+    // Fixed-point hot pass (TGO_PR_FX, default on; spmv.hip gather_hot_fx): super-tiles of
+    // TGO_PR_FX_E entries, built on the device from the hot CSR (its sources must leave at least
+    // 6 bits of the packed word for the row)
+    if (on_dev && pack && env_i64("TGO_PR_FX", 1) != 0) {
+        const int64_t hmax = std::min<int64_t>(hot, n_src);
+        int sb = 1;
+        while ((int64_t(1) << sb) < hmax) ++sb;         // sources < 2^sb
+        const int rbits = std::min(12, 32 - sb);
+        if (rbits >= 6) {
+            cb.hcsr.nnz = hc.d_hadj.n;
+            adopt(ctx, cb.hcsr.adj, hc.d_hadj);
+            HIP_TRY(upload(ctx, cb.hcsr.off, hc.hoff));
+            std::vector<int64_t> tdesc, long_len;
+            std::vector<int32_t> long_rows;
+            std::string err;
+            // entries per super-tile: larger tiles share more lines, but keep >= 512 tiles for the
+            // 256 CUs (RMAT-24 A/B: 256 K 0.964, 512 K 0.951, 1 M 1.203 ms/update — 97 tiles idle
+            // most CUs; profiles/r05e_pr_fx_probe.log)
+            const int64_t fx_e = env_i64("TGO_PR_FX_E", std::min<int64_t>(int64_t(1) << 19,
+                                                                          std::max<int64_t>(int64_t(1) << 16, hc.hoff[n_rows] / 512)));
+            if (int rc = pack_supertiles_device(cb.hcsr.adj, cb.hcsr.off, hc.hoff, n_rows, fx_e,
+                                                rbits, tdesc, long_rows, long_len, ctx->stream, err))
+                return fail(ctx, rc, err);
+            cb.fx = true;
+            cb.fx_rbits = rbits;
+            cb.fx_ntiles = static_cast<int64_t>(tdesc.size() / 4);
+            cb.fx_nlong = static_cast<int64_t>(long_rows.size());
+            HIP_TRY(upload(ctx, cb.fx_desc, tdesc));
+            HIP_TRY(upload(ctx, cb.fx_long_row, long_rows));
+            HIP_TRY(dev_alloc(ctx, cb.fx_long_acc, 2 * std::max<int64_t>(cb.fx_nlong, 1)));
+            HIP_TRY(hipMemset(cb.fx_long_acc, 0, 2 * std::max<int64_t>(cb.fx_nlong, 1) * sizeof(unsigned long long)));
+            lap("hot super-tiles");
+        }
+    }
+    if (cb.fx) {
+        // hot CSR adopted and packed above
+    } else if (on_dev) {                            // hot tiles packed on the device
         cb.hcsr.nnz = hc.d_hadj.n;
         adopt(ctx, cb.hcsr.adj, hc.d_hadj);
         const int32_t max_src = static_cast<int32_t>(std::min<int64_t>(hot, n_src) - 1);
@@ -365,7 +407,7 @@ int upload_cold_blocks(tgo_ctx* ctx, const std::vector<int64_t>& off, const std:
         else HIP_TRY(upload(ctx, cb.widx, hc.widx));
         cb.win = hc.win;
     }
-    HIP_TRY(upload(ctx, cb.hcsr.off, hc.hoff));
+    if (!cb.fx) HIP_TRY(upload(ctx, cb.hcsr.off, hc.hoff));
     HIP_TRY(upload(ctx, cb.poff, hc.poff));
     if (hc.d_cadj.present()) adopt(ctx, cb.cadj, hc.d_cadj);
     else HIP_TRY(upload(ctx, cb.cadj, hc.cadj));
@@ -375,7 +417,19 @@ int upload_cold_blocks(tgo_ctx* ctx, const std::vector<int64_t>& off, const std:
     HIP_TRY(upload(ctx, cb.bend, hc.bend));
     HIP_TRY(upload(ctx, cb.xblk, hc.xblk));
     HIP_TRY(upload(ctx, cb.bsrc, hc.bsrc));
-    {
+    if (hc.cfx) {                                   // cold_fx descriptors, launch-slot order
+        std::vector<int64_t> desc(4 * hc.xblk.size());
+        for (size_t j = 0; j < hc.xblk.size(); ++j) {
+            const int32_t b = hc.xblk[j];
+            const int64_t p0 = hc.bbeg[b], p1 = hc.bend[b];
+            const int64_t src = hc.bsrc[b];
+            if (p1 - p0 > (int64_t(1) << kPackShift) || src < 0) return fail(ctx, TGO_E_STATE, "cold block descriptor out of range");
+            desc[4 * j] = hc.poff[p0]; desc[4 * j + 1] = hc.poff[p1]; desc[4 * j + 2] = p0;
+            desc[4 * j + 3] = (src << 16) | (p1 - p0);
+        }
+        HIP_TRY(upload(ctx, cb.cfx_desc, desc));
+        cb.cfx = true;
+    } else {
         std::vector<int64_t> desc(4 * hc.xblk.size());
         for (size_t j = 0; j < hc.xblk.size(); ++j) {
             const int32_t b = hc.xblk[j];

@@ -336,6 +336,9 @@ struct ColdBlocks {
                                 // first entry, bsrc << 16 | entries} — one load for the chain
                                 // xblk -> bbeg/bend -> poff (cold_gather, prefetching form)
     bool cpacked = false;       // cold tiles source-sorted and packed relative to bsrc
+    bool cfx = false;           // cold tiles for cold_fx (fixed-point piece sums, cfx_desc): up to
+                                // 4096 pieces and TGO_PR_FX_CE entries, packed (source - bsrc) << 12 | piece - first
+    int64_t* cfx_desc = nullptr;   // 4 per launch slot j (xblk order): first entry, end entry, first piece, bsrc << 16 | pieces
     double* partial = nullptr;  // npieces, in piece order (streaming writes)
     double* csum = nullptr;     // n_rows: per-row cold sums (cold_fold; 0 for rows without pieces)
     int32_t* crow = nullptr;    // rows that own cold pieces (ascending)
@@ -356,6 +359,17 @@ struct ColdBlocks {
     int64_t* woff = nullptr;    // n_rows+1
     uint16_t* widx = nullptr;   // window entries (source ids < win), row-major
     RowBlocks rb_win;           // CSR-adaptive blocks of the window CSR (bdesc used)
+    // Fixed-point hot pass (gather_hot_fx, spmv.hip): super-tiles of <= 2^fx_rbits rows and <=
+    // TGO_PR_FX_E entries (pack_supertiles_device), entries source-sorted and packed as
+    // source << fx_rbits | row - first row; sums are 128-bit fixed-point integers (exact,
+    // order-free), so a tile needs one LDS accumulator per row instead of one slot per entry
+    bool fx = false;
+    int fx_rbits = 12;
+    int64_t fx_ntiles = 0;
+    int64_t* fx_desc = nullptr;         // 4 per tile: first entry, end entry, first row, rows or -(long + 1)
+    int64_t fx_nlong = 0;
+    int32_t* fx_long_row = nullptr;     // rows longer than a tile
+    unsigned long long* fx_long_acc = nullptr;   // 2 per long row (low, high word), zero between updates
 };
 struct HostColdBlocks {
     int64_t hot = 0, seg = 0;
@@ -372,6 +386,7 @@ struct HostColdBlocks {
     std::vector<uint32_t> cptr;
     XcdBase xbase{};
     int64_t max_xcd_blocks = 0;
+    bool cfx = false;                   // cold tiles packed for cold_fx: (source - base) << 12 | piece - first piece
 };
 // Builds the split of a CSR (entries = source ids) at hot / seg (see ColdBlocks); returns
 // false when nothing is cold (n <= hot) or the piece count overflows 32-bit indices.
@@ -379,9 +394,12 @@ bool build_cold_blocks(const std::vector<int64_t>& off, const std::vector<int32_
                        int64_t hot, int64_t seg, int64_t tile, int64_t max_pieces, int threads, bool pack,
                        HostColdBlocks& hc, int64_t win = 0);
 // pr_layout.hip: build_cold_blocks / pack_tiles on the device (same arrays)
+int pack_supertiles_device(int32_t* d_adj, const int64_t* d_off, const std::vector<int64_t>& off, int64_t n_rows,
+                           int64_t max_e, int rbits, std::vector<int64_t>& tdesc, std::vector<int32_t>& long_rows,
+                           std::vector<int64_t>& long_len, hipStream_t s, std::string& err);
 int build_cold_blocks_device(const int64_t* d_off, const int32_t* d_adj, int64_t n, int64_t nnz, int64_t n_src,
                              int64_t hot, int64_t seg, int64_t tile, int64_t max_pieces, bool pack, HostColdBlocks& hc,
-                             bool& built, hipStream_t s, std::string& err, int64_t win = 0);
+                             bool& built, hipStream_t s, std::string& err, int64_t win = 0, bool fx = false);
 int pack_tiles_device(int32_t* d_adj, int64_t m, const std::vector<int64_t>& tstart, const std::vector<int32_t>* tbase,
                       int shift, hipStream_t s, std::string& err);
 // part_ghost.hip: the partitioned PageRank ghost exchange

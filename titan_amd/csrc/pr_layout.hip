@@ -148,6 +148,26 @@ __global__ void pack_keys(const int32_t* __restrict__ adj, int64_t m, const int6
         key[k] = (static_cast<uint64_t>(lo) << 32) | packed;
     }
 }
+// super-tile packing (gather_hot_fx / cold_fx): entry k of tile t (desc: first entry, end, first
+// row, rows or a long row's -(index + 1); rows = pieces and off = piece offsets for cold tiles)
+// -> t << 32 | (source - tbase[t]) << rbits | row - first row
+__global__ void pack_rowlocal_keys(const int32_t* __restrict__ adj, int64_t m, const int64_t* __restrict__ td,
+                                   int64_t ntiles, const int64_t* __restrict__ off, int rbits, uint64_t* __restrict__ key,
+                                   const int32_t* __restrict__ tbase = nullptr) {
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x) {
+        int64_t lo = 0, hi = ntiles;                 // last tile whose first entry is <= k (empty tiles skipped by ties)
+        while (hi - lo > 1) { const int64_t mid = (lo + hi) >> 1; if (td[4 * mid] <= k) lo = mid; else hi = mid; }
+        const int64_t r0 = td[4 * lo + 2], nr = td[4 * lo + 3];
+        int64_t rl = 0;
+        if (nr > 1) {                                // the row of entry k: last r in [r0, r0 + nr) with off[r] <= k
+            int64_t a = r0, b = r0 + nr;
+            while (b - a > 1) { const int64_t mid = (a + b) >> 1; if (off[mid] <= k) a = mid; else b = mid; }
+            rl = a - r0;
+        }
+        const uint32_t src = static_cast<uint32_t>(adj[k] - (tbase ? tbase[lo] : 0));
+        key[k] = (static_cast<uint64_t>(lo) << 32) | (static_cast<uint64_t>(src << rbits) | static_cast<uint64_t>(rl));
+    }
+}
 __global__ void unpack_keys(const uint64_t* __restrict__ key, int64_t m, int32_t* __restrict__ adj) {
     for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x)
         adj[k] = static_cast<int32_t>(static_cast<uint32_t>(key[k]));
@@ -241,12 +261,60 @@ int pack_tiles_device(int32_t* d_adj, int64_t m, const std::vector<int64_t>& tst
     return TGO_OK;
 }
 
+// Super-tiles of the hot CSR (rows [0, n_rows), entries [0, off[n_rows]) on the device, sources
+// < 2^(32 - rbits)) for the fixed-point hot pass (gather_hot_fx, spmv.hip): greedy row ranges of
+// at most 2^rbits rows and max_e entries; a row with more than max_e entries forms tiles of its
+// own (max_e-entry chunks, rows field -(long index + 1), long_rows[index] = the row).  Every
+// tile's entries are then sorted by source and packed in place as source << rbits | row - r0.
+// tdesc: 4 per tile {first entry, end entry, first row, rows or -(long index + 1)}.
+int pack_supertiles_device(int32_t* d_adj, const int64_t* d_off, const std::vector<int64_t>& off, int64_t n_rows,
+                           int64_t max_e, int rbits, std::vector<int64_t>& tdesc, std::vector<int32_t>& long_rows,
+                           std::vector<int64_t>& long_len, hipStream_t s, std::string& err) {
+    tdesc.clear();
+    long_rows.clear();
+    long_len.clear();
+    const int64_t R = int64_t(1) << rbits;
+    if (max_e < 1 || static_cast<int64_t>(off.size()) < n_rows + 1) { err = "pr layout: super-tile arguments"; return TGO_E_INVALID; }
+    for (int64_t r = 0; r < n_rows;) {
+        const int64_t e0 = off[r];
+        if (off[r + 1] - e0 > max_e) {               // a long row: chunks of its own
+            const int64_t li = static_cast<int64_t>(long_rows.size());
+            long_rows.push_back(static_cast<int32_t>(r));
+            long_len.push_back(off[r + 1] - e0);
+            for (int64_t c = e0; c < off[r + 1]; c += max_e)
+                tdesc.insert(tdesc.end(), {c, std::min(c + max_e, off[r + 1]), r, -(li + 1)});
+            ++r;
+            continue;
+        }
+        const int64_t rmax = std::min(n_rows, r + R);
+        // the last r2 in (r, rmax] with off[r2] - e0 <= max_e
+        int64_t r2 = std::upper_bound(off.begin() + r + 1, off.begin() + rmax + 1, e0 + max_e) - off.begin() - 1;
+        r2 = std::max(r2, r + 1);
+        tdesc.insert(tdesc.end(), {e0, off[r2], r, r2 - r});
+        r = r2;
+    }
+    const int64_t nt = static_cast<int64_t>(tdesc.size() / 4), m = off[n_rows];
+    if (m == 0 || nt == 0) return TGO_OK;
+    Buf<int64_t> td;
+    Buf<uint64_t> k0, k1;
+    PL_TRY(td.alloc(4 * nt));
+    PL_TRY(copy_chunked(td.p, tdesc.data(), 4 * nt * 8, hipMemcpyHostToDevice));
+    PL_TRY(k0.alloc(m));
+    PL_TRY(k1.alloc(m));
+    pack_rowlocal_keys<<<grid(m), kB, 0, s>>>(d_adj, m, td.p, nt, d_off, rbits, k0.p);
+    Sort so{{}, 0, s};
+    PL_TRY(so.keys(k0.p, k1.p, m, 32 + bits_for(nt)));
+    unpack_keys<<<grid(m), kB, 0, s>>>(k1.p, m, d_adj);
+    PL_TRY(hipStreamSynchronize(s));
+    return TGO_OK;
+}
+
 // The ColdBlocks host structure (graph_build.cpp build_cold_blocks, same arrays) from device
 // in-lists.  built = false when the layout does not apply (nothing cold, too many pieces) or
 // a row is not sorted by source (then the caller keeps the host build).
 int build_cold_blocks_device(const int64_t* d_off, const int32_t* d_adj, int64_t n, int64_t nnz, int64_t n_src,
                              int64_t hot, int64_t seg, int64_t tile, int64_t max_pieces, bool pack, HostColdBlocks& hc,
-                             bool& built, hipStream_t s, std::string& err, int64_t win) {
+                             bool& built, hipStream_t s, std::string& err, int64_t win, bool fx) {
     built = false;
     hc = HostColdBlocks();
     if (hot <= 0 || seg <= 0 || n_src <= hot || n <= 0 || hot >= INT32_MAX) return TGO_OK;
@@ -389,7 +457,32 @@ int build_cold_blocks_device(const int64_t* d_off, const int32_t* d_adj, int64_t
     }
     const int64_t nb = static_cast<int64_t>(hc.bbeg.size());
     lap("blocks (host)");
-    if (pack && seg <= (int64_t(1) << (31 - kPackShift)) && tile <= (int64_t(1) << kPackShift)) {
+    if (fx && pack && max_pieces <= (int64_t(1) << kPackShift) && seg <= (int64_t(1) << (32 - kPackShift))) {
+        // fixed-point cold tiles (cold_fx): (source - segment base) << 12 | piece - first piece
+        std::vector<int64_t> td(4 * nb);
+        for (int64_t b = 0; b < nb; ++b) {
+            td[4 * b] = hc.poff[hc.bbeg[b]];
+            td[4 * b + 1] = hc.poff[hc.bend[b]];
+            td[4 * b + 2] = hc.bbeg[b];
+            td[4 * b + 3] = hc.bend[b] - hc.bbeg[b];
+        }
+        if (nb > 0 && C > 0) {
+            Buf<int64_t> dtd;
+            Buf<int32_t> dtb;
+            Buf<uint64_t> k0, k1;
+            PL_TRY(dtd.alloc(4 * nb));
+            PL_TRY(copy_chunked(dtd.p, td.data(), 4 * nb * 8, hipMemcpyHostToDevice));
+            PL_TRY(dtb.alloc(nb));
+            PL_TRY(copy_chunked(dtb.p, hc.bsrc.data(), nb * 4, hipMemcpyHostToDevice));
+            PL_TRY(k0.alloc(C));
+            PL_TRY(k1.alloc(C));
+            pack_rowlocal_keys<<<grid(C), kB, 0, s>>>(cadj.p, C, dtd.p, nb, poff.p, kPackShift, k0.p, dtb.p);
+            PL_TRY(so.keys(k0.p, k1.p, C, 32 + bits_for(nb)));
+            unpack_keys<<<grid(C), kB, 0, s>>>(k1.p, C, cadj.p);
+        }
+        hc.cpacked = true;
+        hc.cfx = true;
+    } else if (pack && seg <= (int64_t(1) << (31 - kPackShift)) && tile <= (int64_t(1) << kPackShift)) {
         std::vector<int64_t> tstart(nb);
         for (int64_t b = 0; b < nb; ++b) tstart[b] = hc.poff[hc.bbeg[b]];
         if (nb > 0)

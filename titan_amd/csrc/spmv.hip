@@ -467,6 +467,177 @@ __global__ void __launch_bounds__(kThreads, 4) gather_hot_pipe(const int64_t* __
     }
 }
 
+// ---------------------------------------------------------------- fixed-point hot pass
+// The slot form above stages one double per entry in LDS so that every row can add its
+// entries in a fixed order; LDS then caps a tile at 4096 - 16384 entries, and a tile's sorted
+// sources share few 128-byte lines (0.70 L2 requests per hot entry at 4096 at RMAT-24, the
+// request rate being the hot pass's bound — DESIGN.md §4.1).  Here a row's sum is an exact
+// 128-bit fixed-point integer (binary point at bit kFxPoint: resolution 2^-80, range 2^47), so
+// the entries of a tile may be added in ANY order and the result is still bit-for-bit the same:
+// a tile needs one LDS accumulator per row, not one slot per entry, and grows to 64 K entries
+// (super-tiles, pack_supertiles_device) — its source-sorted entries then share lines: 0.29 L2
+// requests per hot entry at RMAT-24 (host count over the bench graph, 64 K entries / 4096 rows).
+// The conversion of the exact sum back to a double rounds once; the reference's fp64 sum
+// (PageRankVertexProgram.java:84-89, VertexMemoryHandler.java:97-102) rounds once per entry.
+constexpr int kFxPoint = 80;
+constexpr int kFxThreads = 1024;
+constexpr int kFxSlots = 4096;         // LDS accumulators of a tile: rows x copies
+constexpr int kFxUnroll = 8;
+
+// v * 2^kFxPoint as a two's complement 128-bit integer (truncated below 2^-80; |v| < 2^47)
+__device__ __forceinline__ void fx_of(double v, unsigned long long& lo, unsigned long long& hi) {
+    const unsigned long long b = static_cast<unsigned long long>(__double_as_longlong(v));
+    const int e = static_cast<int>((b >> 52) & 0x7FF);
+    lo = 0;
+    hi = 0;
+    if (e == 0) return;                                   // zero (or subnormal: below the resolution)
+    const unsigned long long m = (b & 0xFFFFFFFFFFFFFull) | (1ull << 52);
+    const int sh = e - 1075 + kFxPoint;                   // v * 2^P = m * 2^sh
+    if (sh > 74) {
+        hi = 1ull << 62;                                  // out of range (inf / nan / >= 2^47): loudly huge
+    } else if (sh >= 64) {
+        hi = m << (sh - 64);
+    } else if (sh >= 0) {
+        lo = m << sh;
+        hi = sh > 11 ? m >> (64 - sh) : 0ull;
+    } else if (sh > -53) {
+        lo = m >> (-sh);
+    }
+    if (b >> 63) {                                        // negative: two's complement
+        const unsigned long long c = lo == 0 ? 1ull : 0ull;
+        lo = ~lo + 1ull;
+        hi = ~hi + c;
+    }
+}
+__device__ __forceinline__ double fx_to_double(unsigned long long lo, unsigned long long hi) {
+    return static_cast<double>(static_cast<long long>(hi)) * 0x1p-16 + static_cast<double>(lo) * 0x1p-80;
+}
+__device__ __forceinline__ void fx_add(unsigned long long* plo, unsigned long long* phi, unsigned long long lo,
+                                       unsigned long long hi) {
+    const unsigned long long old = atomicAdd(plo, lo);
+    const unsigned long long c = hi + (old + lo < old ? 1ull : 0ull);
+    if (c) atomicAdd(phi, c);
+}
+
+// A tile's entries (packed source << rbits | accumulator) into the LDS accumulators: all index
+// loads, then all gathers, then the conversions and LDS atomics, kFxUnroll entries per thread
+// in flight.  lc: log2 of the copies per accumulator (the lane picks the copy).
+__device__ __forceinline__ void fx_accumulate(const uint32_t* __restrict__ p, int64_t ne, const double* __restrict__ msg,
+                                              int rbits, int lc, unsigned long long* s_lo, unsigned long long* s_hi) {
+    const uint32_t rmask = (1u << rbits) - 1u;
+    const uint32_t cl = threadIdx.x & ((1u << lc) - 1u);
+    for (int64_t b = 0; b < ne; b += static_cast<int64_t>(kFxThreads) * kFxUnroll) {
+        uint32_t w[kFxUnroll];
+#pragma unroll
+        for (int j = 0; j < kFxUnroll; ++j) {
+            const int64_t k = b + j * kFxThreads + threadIdx.x;
+            w[j] = k < ne ? __builtin_nontemporal_load(p + k) : 0u;
+        }
+        double v[kFxUnroll];
+#pragma unroll
+        for (int j = 0; j < kFxUnroll; ++j) {
+            const int64_t k = b + j * kFxThreads + threadIdx.x;
+            v[j] = k < ne ? msg[w[j] >> rbits] : 0.0;
+        }
+#pragma unroll
+        for (int j = 0; j < kFxUnroll; ++j) {
+            unsigned long long lo, hi;
+            fx_of(v[j], lo, hi);
+            if (lo | hi) {
+                const uint32_t slot = ((w[j] & rmask) << lc) | cl;
+                fx_add(&s_lo[slot], &s_hi[slot], lo, hi);
+            }
+        }
+    }
+}
+__device__ __forceinline__ int fx_copies_log2(int rows) {
+    int lc = 6;
+    while (lc > 0 && (rows << lc) > kFxSlots) --lc;
+    return lc;
+}
+// The 128-bit total of accumulator i's copies.
+__device__ __forceinline__ void fx_total(const unsigned long long* s_lo, const unsigned long long* s_hi, int i, int lc,
+                                         unsigned long long& lo, unsigned long long& hi) {
+    lo = 0;
+    hi = 0;
+    for (int c = 0; c < (1 << lc); ++c) {
+        const unsigned long long nl = lo + s_lo[(i << lc) + c];
+        hi += s_hi[(i << lc) + c] + (nl < lo ? 1ull : 0ull);
+        lo = nl;
+    }
+}
+
+// One super-tile per workgroup: desc {first entry, end entry, first row, rows | -(long + 1)}.
+// Each row has 2^lc copies of its accumulator (rows * copies <= kFxSlots), the copy chosen by
+// the lane, so a tile of few rows does not serialise its lanes on one LDS address.
+__global__ void __launch_bounds__(kFxThreads) gather_hot_fx(const uint32_t* __restrict__ padj,
+        const int64_t* __restrict__ desc, int rbits, const double* __restrict__ msg, PrColdFinal fin,
+        unsigned long long* __restrict__ long_acc) {
+    __shared__ unsigned long long s_lo[kFxSlots], s_hi[kFxSlots];
+    const int64_t t = blockIdx.x;
+    const int64_t e0 = desc[4 * t], e1 = desc[4 * t + 1], r0 = desc[4 * t + 2], nr = desc[4 * t + 3];
+    const int rows = nr > 0 ? static_cast<int>(nr) : 1;
+    const int lc = fx_copies_log2(rows);
+    const int nslots = rows << lc;
+    for (int i = threadIdx.x; i < nslots; i += kFxThreads) { s_lo[i] = 0; s_hi[i] = 0; }
+    __syncthreads();
+    fx_accumulate(padj + e0, e1 - e0, msg, rbits, lc, s_lo, s_hi);
+    __syncthreads();
+    if (nr > 0) {
+        for (int i = threadIdx.x; i < rows; i += kFxThreads) {
+            unsigned long long lo, hi;
+            fx_total(s_lo, s_hi, i, lc, lo, hi);
+            fin(r0 + i, fx_to_double(lo, hi));            // + the row's cold sum, then the update
+        }
+    } else if (threadIdx.x == 0) {                        // a long row's chunk: into the row's accumulator
+        unsigned long long lo = 0, hi = 0;
+        for (int c = 0; c < nslots; ++c) {
+            const unsigned long long nl = lo + s_lo[c];
+            hi += s_hi[c] + (nl < lo ? 1ull : 0ull);
+            lo = nl;
+        }
+        fx_add(&long_acc[2 * (-nr - 1)], &long_acc[2 * (-nr - 1) + 1], lo, hi);
+    }
+}
+// Cold pass in fixed point: the cold_gather protocol (workgroup b on XCD b % 8 takes that XCD's
+// (b / 8)-th block, so each XCD walks its segments in order with the segment's messages in its
+// L2), but a block is a run of up to 4096 pieces and TGO_PR_FX_CE entries, packed
+// (source - segment base) << 12 | piece - first piece, summed into per-piece accumulators in
+// any order — a larger block shares more lines between the lanes of a gather (0.52 L2 requests
+// per cold entry against 0.91 for the 4096-entry slot tiles, host count at RMAT-24).  Each
+// piece's exact sum goes to partial[] as a double, where cold_fold adds a row's pieces in
+// segment order as before.
+__global__ void __launch_bounds__(kFxThreads) cold_fx(const uint32_t* __restrict__ cadj,
+        const int64_t* __restrict__ cfd, XcdBase xb, const double* __restrict__ msg, double* __restrict__ partial) {
+    __shared__ unsigned long long s_lo[kFxSlots], s_hi[kFxSlots];
+    const int x = static_cast<int>(blockIdx.x & 7);
+    const int64_t j = xb.b[x] + (blockIdx.x >> 3);
+    if (j >= xb.b[x + 1]) return;
+    const int64_t e0 = cfd[4 * j], e1 = cfd[4 * j + 1], p0 = cfd[4 * j + 2], w = cfd[4 * j + 3];
+    const int np = static_cast<int>(w & 0xFFFF);
+    const int lc = fx_copies_log2(np);
+    for (int i = threadIdx.x; i < (np << lc); i += kFxThreads) { s_lo[i] = 0; s_hi[i] = 0; }
+    __syncthreads();
+    fx_accumulate(cadj + e0, e1 - e0, msg + (w >> 16), kPackShift, lc, s_lo, s_hi);
+    __syncthreads();
+    for (int i = threadIdx.x; i < np; i += kFxThreads) {
+        unsigned long long lo, hi;
+        fx_total(s_lo, s_hi, i, lc, lo, hi);
+        partial[p0 + i] = fx_to_double(lo, hi);
+    }
+}
+
+// The long rows after every chunk has landed: the update, and the accumulator back to zero.
+__global__ void finalize_long_fx(const int32_t* __restrict__ long_row, int64_t nlong,
+                                 unsigned long long* __restrict__ long_acc, PrColdFinal fin) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nlong; i += (int64_t)gridDim.x * blockDim.x) {
+        const unsigned long long lo = long_acc[2 * i], hi = long_acc[2 * i + 1];
+        long_acc[2 * i] = 0;
+        long_acc[2 * i + 1] = 0;
+        fin(long_row[i], fx_to_double(lo, hi));
+    }
+}
+
 // A long row's chunk of packed entries: the chunk sum (source order, fixed).
 struct PackedOp {
     using T = double;
@@ -772,7 +943,10 @@ hipError_t k_pr_cold_phase(const ColdBlocks& cb, const double* contrib, hipStrea
     }
     if (cb.max_xcd_blocks > 0) {
         const unsigned g = static_cast<unsigned>(cb.max_xcd_blocks * 8);
-        if (cb.cpacked && row_prefetch())
+        if (cb.cfx)
+            cold_fx<<<g, kFxThreads, 0, s>>>(reinterpret_cast<const uint32_t*>(cb.cadj), cb.cfx_desc, cb.xbase, contrib,
+                                             cb.partial);
+        else if (cb.cpacked && row_prefetch())
             cold_gather<true, true><<<g, kBlock, 0, s>>>(cb.poff, cb.cadj, cb.bbeg, cb.bend, cb.xblk, cb.bsrc, cb.cdesc, cb.xbase,
                                                          contrib, cb.partial);
         else if (cb.cpacked)
@@ -792,6 +966,14 @@ hipError_t k_pr_cold_phase(const ColdBlocks& cb, const double* contrib, hipStrea
 hipError_t k_pr_hot_phase(const ColdBlocks& cb, const double* contrib, const double* edge_count, double* pr,
                           double* contrib_next, double* partial_long, double alpha, double base, hipStream_t s) {
     const PrColdFinal fin{PrFinal{edge_count, pr, contrib_next, alpha, base}, cb.csum};
+    if (cb.fx) {
+        if (cb.fx_ntiles > 0)
+            gather_hot_fx<<<static_cast<unsigned>(cb.fx_ntiles), kFxThreads, 0, s>>>(
+                reinterpret_cast<const uint32_t*>(cb.hcsr.adj), cb.fx_desc, cb.fx_rbits, contrib, fin, cb.fx_long_acc);
+        if (cb.fx_nlong > 0)
+            finalize_long_fx<<<grid_for(cb.fx_nlong), kBlock, 0, s>>>(cb.fx_long_row, cb.fx_nlong, cb.fx_long_acc, fin);
+        return hipGetLastError();
+    }
     if (!cb.packed) return run_gather(cb.hcsr, cb.rb_hot, PrOp{contrib}, fin, partial_long, s);
     const RowBlocks& rb = cb.rb_hot;
     if (rb.nblocks > 0 && cb.hot_pipe) {
