@@ -226,7 +226,7 @@ def run_single(args):
     upd = max(args.pr_iters - 1, 1)
     e_in = int(pst["in_entries"])
     pr_bytes = 4.0 * e_in + 8.0 * (n + 1) + 24.0 * n
-    roof_pr = roofline("pagerank_update (cache-blocked: cold_gather + cold_fold + gather_short_packed + long-row chunks)",
+    roof_pr = roofline("pagerank_update (cache-blocked, fixed-point tile sums: cold_fx + cold_fold + gather_hot_fx + long rows)",
                        pr_bytes / (pks.mean() / upd) / 1e9,
                        "4*m + 8*(n+1) + 24*n per update", "pagerank_update", pr_bytes)
     bfs_share = float(bts.sum()) / (float(bts.sum()) + float(pts.sum()))

@@ -9,6 +9,7 @@ grouped the way bench.py prices them:
 
   pagerank_update : gather_short + gather_chunks + finalize_long (one group = one rank update)
   msbfs_sweep     : ms_seed + ms_pull + ms_push + ms_settle (one group = one 64-source sweep)
+  sssp_source     : the delta-stepping device loop's kernels (one group = one source)
 
 Corrections (MI355X_MICROARCH.md §HBM, calibrated for these access shapes by
 scripts/pmc_calib.hip, profiles/r02f_pmc_calibration.txt): FETCH_SIZE and WRITE_SIZE are in
@@ -29,13 +30,19 @@ from collections import defaultdict
 GROUPS = {
     # one rank update of the cache-blocked gather (spmv.hip): cold pass, fold, hot pass, long rows
     # (gather_hot_pf: the prefetching hot pass; gather_short_packed: its TGO_PR_PF=0 form)
+    # (round 5 default: cold_fx + cold_fold + gather_hot_fx + finalize_long_fx, fixed-point tile sums)
     "pagerank_update": ("cold_gather<", "cold_fold(", "gather_hot_pf<", "gather_hot_pf(", "gather_short_packed<",
                         "gather_chunks<tgo::(anonymous namespace)::PackedOp",
-                        "finalize_long<tgo::(anonymous namespace)::PackedOp"),
+                        "finalize_long<tgo::(anonymous namespace)::PackedOp",
+                        "cold_fx(", "gather_hot_fx(", "finalize_long_fx("),
     # ms_pull is templated on its round-trip width (ms_pull<8>)
     "msbfs_sweep": ("ms_seed(", "ms_pull(", "ms_pull<", "ms_push(", "ms_settle(", "ms_queue(", "ms_fbitmap("),
+    # one delta-stepping source of the device-driven loop (delta_loop.hip): every step's kernels
+    "sssp_source": ("ds_loop_seed(", "ds_decide(", "ds_decide_bins(", "ds_extract_dev(", "ds_extract_bins(",
+                    "ds_commit_dev<", "ds_relax_dev<", "ds_pull_heavy(", "ds_publish(", "ds_pull_flip("),
 }
-UNIT_KERNEL = {"pagerank_update": ("gather_hot_pf<", "gather_hot_pf(", "gather_short_packed<"), "msbfs_sweep": ("ms_seed(",)}
+UNIT_KERNEL = {"pagerank_update": ("gather_hot_pf<", "gather_hot_pf(", "gather_short_packed<", "gather_hot_fx("),
+               "msbfs_sweep": ("ms_seed(",), "sssp_source": ("ds_loop_seed(",)}
 
 
 def load(d):
