@@ -187,7 +187,12 @@ int64_t env_i64(const char* name, int64_t dflt) {
     const char* v = std::getenv(name);
     return v ? std::atoll(v) : dflt;
 }
-constexpr int64_t kPrHotDefault = 393216, kPrSegDefault = 393216;   // 3 MB each (profiles/r02an_pr_hot_seg_probe*.log)
+constexpr int64_t kPrSegDefault = 393216;   // 3 MB (profiles/r02an_pr_hot_seg_probe*.log)
+// hot head: 3 MB for the slot tiles; 6 MB for the fixed-point super-tiles, whose source-sorted
+// 380 K-entry tiles reuse lines enough that a head past one XCD's L2 still pays (RMAT-24
+// ms/update: 384 K 0.852, 512 K 0.827, 768 K 0.814-0.818, 1 M 0.830, 1.5 M 0.913;
+// profiles/r05j_pr_fx_hot_ab.log, r05k_pr_fx_hot_ab.log)
+int64_t pr_hot_default() { return env_i64("TGO_PR_FX", 1) != 0 ? 786432 : 393216; }
 // LDS window of the hottest sources (lds_window, spmv.hip; TGO_PR_WIN, at most 12288 doubles =
 // 96 KB beside the 16 waves' 4 KB item buffers).  Off by default: measured slower at every
 // window size (negative result 13: 1.252 -> 1.385-1.476 ms/update at RMAT-24)
@@ -298,7 +303,7 @@ int upload_cold_blocks(tgo_ctx* ctx, const std::vector<int64_t>& off, const std:
         if (int rc = build_cold_blocks_device(d_off, d_adj, static_cast<int64_t>(off.size()) - 1, d_nnz, n_src, hot,
                                               env_i64("TGO_PR_SEG", kPrSegDefault),
                                               cold_fx ? env_i64("TGO_PR_FX_CE", 65536) : kTile,
-                                              cold_fx ? std::min<int64_t>(env_i64("TGO_PR_FX_CP", 4096), int64_t(1) << kPackShift)
+                                              cold_fx ? std::min<int64_t>(env_i64("TGO_PR_FX_CP", 4096), int64_t(1) << (kPackShift + 1))
                                                       : kMaxRows,
                                               env_i64("TGO_PR_CPACK", 1) != 0, hc, on_dev, ctx->stream, err, win, cold_fx))
             return fail(ctx, rc, err);
@@ -423,12 +428,13 @@ int upload_cold_blocks(tgo_ctx* ctx, const std::vector<int64_t>& off, const std:
             const int32_t b = hc.xblk[j];
             const int64_t p0 = hc.bbeg[b], p1 = hc.bend[b];
             const int64_t src = hc.bsrc[b];
-            if (p1 - p0 > (int64_t(1) << kPackShift) || src < 0) return fail(ctx, TGO_E_STATE, "cold block descriptor out of range");
+            if (p1 - p0 > (int64_t(1) << hc.cfx_shift) || src < 0) return fail(ctx, TGO_E_STATE, "cold block descriptor out of range");
             desc[4 * j] = hc.poff[p0]; desc[4 * j + 1] = hc.poff[p1]; desc[4 * j + 2] = p0;
             desc[4 * j + 3] = (src << 16) | (p1 - p0);
         }
         HIP_TRY(upload(ctx, cb.cfx_desc, desc));
         cb.cfx = true;
+        cb.cfx_shift = hc.cfx_shift;
     } else {
         std::vector<int64_t> desc(4 * hc.xblk.size());
         for (size_t j = 0; j < hc.xblk.size(); ++j) {
@@ -532,7 +538,7 @@ int upload_graph(tgo_ctx* ctx, HostGraph& h, bool allow_segments = true) {
     if (allow_segments && h.scope != TGO_SCOPE_BOTH_E && env_i64("TGO_PR_BLOCKED", 1) != 0) {
         // rows >= n_active have no entries at all: the hot pass skips them (their rank
         // after any update is (1-a)/N, written once at the end of the program)
-        if (int rc = upload_cold_blocks(ctx, h.in.off, h.in.adj, h.n, env_i64("TGO_PR_HOT", kPrHotDefault), g.n_active,
+        if (int rc = upload_cold_blocks(ctx, h.in.off, h.in.adj, h.n, env_i64("TGO_PR_HOT", pr_hot_default()), g.n_active,
                                         g.cold_in, g.cold_in_ready, g.in.off, g.in.adj, g.in.nnz,
                                         env_i64("TGO_PR_WIN", kPrWinDefault)))
             return rc;
@@ -2747,7 +2753,7 @@ int tgo_part_pr_blocked(tgo_ctx* ctx, int32_t world, int64_t active_span, int64_
         ctx->part_pr_world = 0;
         return TGO_OK;                                  // plain layout: one rank-major all-gather
     }
-    int64_t H = env_i64("TGO_PR_HOT", kPrHotDefault) / world;
+    int64_t H = env_i64("TGO_PR_HOT", pr_hot_default()) / world;
     H = std::min(active_span, std::max<int64_t>(64, H / 64 * 64));
     if (ctx->part_pr_world == world && ctx->part_pr_hot == H && ctx->part_pr_span == active_span) {
         *hot_per_rank = H;

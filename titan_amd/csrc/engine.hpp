@@ -339,6 +339,7 @@ struct ColdBlocks {
     bool cfx = false;           // cold tiles for cold_fx (fixed-point piece sums, cfx_desc): up to
                                 // 4096 pieces and TGO_PR_FX_CE entries, packed (source - bsrc) << 12 | piece - first
     int64_t* cfx_desc = nullptr;   // 4 per launch slot j (xblk order): first entry, end entry, first piece, bsrc << 16 | pieces
+    int cfx_shift = 12;            // piece-id bits of a packed cold entry (13 for 8192-piece tiles)
     double* partial = nullptr;  // npieces, in piece order (streaming writes)
     double* csum = nullptr;     // n_rows: per-row cold sums (cold_fold; 0 for rows without pieces)
     int32_t* crow = nullptr;    // rows that own cold pieces (ascending)
@@ -386,7 +387,8 @@ struct HostColdBlocks {
     std::vector<uint32_t> cptr;
     XcdBase xbase{};
     int64_t max_xcd_blocks = 0;
-    bool cfx = false;                   // cold tiles packed for cold_fx: (source - base) << 12 | piece - first piece
+    bool cfx = false;                   // cold tiles packed for cold_fx: (source - base) << cfx_shift | piece - first piece
+    int cfx_shift = 12;
 };
 // Builds the split of a CSR (entries = source ids) at hot / seg (see ColdBlocks); returns
 // false when nothing is cold (n <= hot) or the piece count overflows 32-bit indices.

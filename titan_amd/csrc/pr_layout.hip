@@ -457,8 +457,9 @@ int build_cold_blocks_device(const int64_t* d_off, const int32_t* d_adj, int64_t
     }
     const int64_t nb = static_cast<int64_t>(hc.bbeg.size());
     lap("blocks (host)");
-    if (fx && pack && max_pieces <= (int64_t(1) << kPackShift) && seg <= (int64_t(1) << (32 - kPackShift))) {
-        // fixed-point cold tiles (cold_fx): (source - segment base) << 12 | piece - first piece
+    const int cshift = max_pieces > (int64_t(1) << kPackShift) ? kPackShift + 1 : kPackShift;
+    if (fx && pack && max_pieces <= (int64_t(1) << cshift) && seg <= (int64_t(1) << (32 - cshift))) {
+        // fixed-point cold tiles (cold_fx): (source - segment base) << cshift | piece - first piece
         std::vector<int64_t> td(4 * nb);
         for (int64_t b = 0; b < nb; ++b) {
             td[4 * b] = hc.poff[hc.bbeg[b]];
@@ -476,12 +477,13 @@ int build_cold_blocks_device(const int64_t* d_off, const int32_t* d_adj, int64_t
             PL_TRY(copy_chunked(dtb.p, hc.bsrc.data(), nb * 4, hipMemcpyHostToDevice));
             PL_TRY(k0.alloc(C));
             PL_TRY(k1.alloc(C));
-            pack_rowlocal_keys<<<grid(C), kB, 0, s>>>(cadj.p, C, dtd.p, nb, poff.p, kPackShift, k0.p, dtb.p);
+            pack_rowlocal_keys<<<grid(C), kB, 0, s>>>(cadj.p, C, dtd.p, nb, poff.p, cshift, k0.p, dtb.p);
             PL_TRY(so.keys(k0.p, k1.p, C, 32 + bits_for(nb)));
             unpack_keys<<<grid(C), kB, 0, s>>>(k1.p, C, cadj.p);
         }
         hc.cpacked = true;
         hc.cfx = true;
+        hc.cfx_shift = cshift;
     } else if (pack && seg <= (int64_t(1) << (31 - kPackShift)) && tile <= (int64_t(1) << kPackShift)) {
         std::vector<int64_t> tstart(nb);
         for (int64_t b = 0; b < nb; ++b) tstart[b] = hc.poff[hc.bbeg[b]];

@@ -550,9 +550,9 @@ __device__ __forceinline__ void fx_accumulate(const uint32_t* __restrict__ p, in
         }
     }
 }
-__device__ __forceinline__ int fx_copies_log2(int rows) {
+__device__ __forceinline__ int fx_copies_log2(int rows, int slots = kFxSlots) {
     int lc = 6;
-    while (lc > 0 && (rows << lc) > kFxSlots) --lc;
+    while (lc > 0 && (rows << lc) > slots) --lc;
     return lc;
 }
 // The 128-bit total of accumulator i's copies.
@@ -607,18 +607,23 @@ __global__ void __launch_bounds__(kFxThreads) gather_hot_fx(const uint32_t* __re
 // per cold entry against 0.91 for the 4096-entry slot tiles, host count at RMAT-24).  Each
 // piece's exact sum goes to partial[] as a double, where cold_fold adds a row's pieces in
 // segment order as before.
+// kSlots = 8192 (TGO_PR_FX_CP): 13-bit piece ids, 128 KB of dynamic LDS, one workgroup a CU.
+template <int kSlots>
 __global__ void __launch_bounds__(kFxThreads) cold_fx(const uint32_t* __restrict__ cadj,
-        const int64_t* __restrict__ cfd, XcdBase xb, const double* __restrict__ msg, double* __restrict__ partial) {
-    __shared__ unsigned long long s_lo[kFxSlots], s_hi[kFxSlots];
+        const int64_t* __restrict__ cfd, XcdBase xb, const double* __restrict__ msg, double* __restrict__ partial,
+        int shift) {
+    extern __shared__ unsigned long long fx_lds[];
+    unsigned long long* s_lo = fx_lds;
+    unsigned long long* s_hi = fx_lds + kSlots;
     const int x = static_cast<int>(blockIdx.x & 7);
     const int64_t j = xb.b[x] + (blockIdx.x >> 3);
     if (j >= xb.b[x + 1]) return;
     const int64_t e0 = cfd[4 * j], e1 = cfd[4 * j + 1], p0 = cfd[4 * j + 2], w = cfd[4 * j + 3];
     const int np = static_cast<int>(w & 0xFFFF);
-    const int lc = fx_copies_log2(np);
+    const int lc = fx_copies_log2(np, kSlots);
     for (int i = threadIdx.x; i < (np << lc); i += kFxThreads) { s_lo[i] = 0; s_hi[i] = 0; }
     __syncthreads();
-    fx_accumulate(cadj + e0, e1 - e0, msg + (w >> 16), kPackShift, lc, s_lo, s_hi);
+    fx_accumulate(cadj + e0, e1 - e0, msg + (w >> 16), shift, lc, s_lo, s_hi);
     __syncthreads();
     for (int i = threadIdx.x; i < np; i += kFxThreads) {
         unsigned long long lo, hi;
@@ -943,9 +948,20 @@ hipError_t k_pr_cold_phase(const ColdBlocks& cb, const double* contrib, hipStrea
     }
     if (cb.max_xcd_blocks > 0) {
         const unsigned g = static_cast<unsigned>(cb.max_xcd_blocks * 8);
-        if (cb.cfx)
-            cold_fx<<<g, kFxThreads, 0, s>>>(reinterpret_cast<const uint32_t*>(cb.cadj), cb.cfx_desc, cb.xbase, contrib,
-                                             cb.partial);
+        if (cb.cfx && cb.cfx_shift > kPackShift) {
+            constexpr size_t lds = 2 * 8192 * sizeof(unsigned long long);
+            static bool lds_set = false;              // the > 64 KB dynamic LDS limit, raised once
+            if (!lds_set) {
+                const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&cold_fx<8192>),
+                                                         hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+                if (e != hipSuccess) return e;
+                lds_set = true;
+            }
+            cold_fx<8192><<<g, kFxThreads, lds, s>>>(reinterpret_cast<const uint32_t*>(cb.cadj), cb.cfx_desc, cb.xbase,
+                                                     contrib, cb.partial, cb.cfx_shift);
+        } else if (cb.cfx)
+            cold_fx<kFxSlots><<<g, kFxThreads, 2 * kFxSlots * sizeof(unsigned long long), s>>>(
+                reinterpret_cast<const uint32_t*>(cb.cadj), cb.cfx_desc, cb.xbase, contrib, cb.partial, cb.cfx_shift);
         else if (cb.cpacked && row_prefetch())
             cold_gather<true, true><<<g, kBlock, 0, s>>>(cb.poff, cb.cadj, cb.bbeg, cb.bend, cb.xblk, cb.bsrc, cb.cdesc, cb.xbase,
                                                          contrib, cb.partial);
