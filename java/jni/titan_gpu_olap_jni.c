@@ -12,6 +12,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include "titan_gpu_olap.h"
+#include "titan_gpu_olap_part.h"
 
 #define JFN(name) Java_com_thinkaurelius_titan_graphdb_olap_gpu_TgoNative_##name
 #define CTX(h) ((tgo_ctx*)(intptr_t)(h))
@@ -334,4 +335,205 @@ JNIEXPORT jdoubleArray JNICALL JFN(stats)(JNIEnv* env, jclass cls, jlong h) {
     jdoubleArray out = (*env)->NewDoubleArray(env, 6);
     if (out) (*env)->SetDoubleArrayRegion(env, out, 0, 6, v);
     return out;
+}
+
+/* ---- multi-GPU (include/titan_gpu_olap_part.h): one ctx + one exchange per GPU worker ----
+ * GpuGraphComputer.devices(...) runs one worker thread per device in the JVM; every worker
+ * loads its 1-D vertex range [lo, hi) of the global dense ids from an edge list that holds
+ * every edge with an endpoint in the range, and the program runs as ONE native call per
+ * worker whose collectives go over its RCCL communicator (tgo_exchange_rccl_*). */
+#define XCH(h) ((tgo_exchange*)(intptr_t)(h))
+
+/* edge arrays: src / dst (and weight, may be null) of equal length m */
+static int edge_lengths(JNIEnv* env, jintArray src, jintArray dst, jintArray w, jsize* m) {
+    if (!src || !dst) return TGO_E_INVALID;
+    *m = (*env)->GetArrayLength(env, src);
+    if ((*env)->GetArrayLength(env, dst) != *m) return TGO_E_INVALID;
+    if (w && (*env)->GetArrayLength(env, w) != *m) return TGO_E_INVALID;
+    return TGO_OK;
+}
+
+/* tgo_part_layout: the degree-grouped ids of the owned vertices [lo, hi) (int[hi - lo]) or
+ * null on failure; every worker's slice goes into one layoutGlobal array (n_global). */
+JNIEXPORT jintArray JNICALL JFN(partLayout)(JNIEnv* env, jclass cls, jintArray src, jintArray dst, jlong n_global,
+                                            jlong lo, jlong hi, jint threads) {
+    (void)cls;
+    jsize m = 0;
+    if (edge_lengths(env, src, dst, NULL, &m) != TGO_OK || lo < 0 || hi <= lo || hi > n_global) return NULL;
+    if (!fits_jsize(env, hi - lo, "a partition larger than a Java array holds")) return NULL;
+    jintArray out = (*env)->NewIntArray(env, (jsize)(hi - lo));
+    if (!out) return NULL;
+    jint* s = (*env)->GetIntArrayElements(env, src, NULL);
+    jint* d = (*env)->GetIntArrayElements(env, dst, NULL);
+    jint* o = (*env)->GetIntArrayElements(env, out, NULL);
+    int rc = TGO_E_OOM;
+    if (s && d && o) {
+        tgo_edges e;
+        memset(&e, 0, sizeof e);
+        e.n = n_global;
+        e.m = m;
+        e.src = (const int32_t*)s;
+        e.dst = (const int32_t*)d;
+        rc = tgo_part_layout(&e, n_global, lo, hi, threads, (int32_t*)o);
+    }
+    if (s) (*env)->ReleaseIntArrayElements(env, src, s, JNI_ABORT);
+    if (d) (*env)->ReleaseIntArrayElements(env, dst, d, JNI_ABORT);
+    if (o) (*env)->ReleaseIntArrayElements(env, out, o, 0);
+    return rc == TGO_OK ? out : NULL;
+}
+
+/* tgo_load_partition(_layout): weight may be null (unweighted); layoutGlobal null = the
+ * caller's ids as they are, else int[n_global] (every worker the same array). */
+JNIEXPORT jint JNICALL JFN(loadPartition)(JNIEnv* env, jclass cls, jlong h, jlong n_global, jlong lo, jlong hi,
+                                          jintArray src, jintArray dst, jintArray weight, jint scope, jboolean apply_cap,
+                                          jintArray layout_global) {
+    (void)cls;
+    jsize m = 0;
+    if (edge_lengths(env, src, dst, weight, &m) != TGO_OK || lo < 0 || hi <= lo || hi > n_global) return TGO_E_INVALID;
+    if (layout_global && (jlong)(*env)->GetArrayLength(env, layout_global) != n_global) return TGO_E_INVALID;
+    jint* s = (*env)->GetIntArrayElements(env, src, NULL);
+    jint* d = (*env)->GetIntArrayElements(env, dst, NULL);
+    jint* w = weight ? (*env)->GetIntArrayElements(env, weight, NULL) : NULL;
+    jint* lg = layout_global ? (*env)->GetIntArrayElements(env, layout_global, NULL) : NULL;
+    int rc = TGO_E_OOM;
+    if (s && d && (!weight || w) && (!layout_global || lg)) {
+        tgo_edges e;
+        memset(&e, 0, sizeof e);
+        e.n = n_global;
+        e.m = m;
+        e.src = (const int32_t*)s;
+        e.dst = (const int32_t*)d;
+        e.weight = (const int32_t*)w;
+        tgo_load_opts o;
+        memset(&o, 0, sizeof o);
+        o.scope = scope;
+        o.apply_cap = apply_cap ? 1 : 0;
+        rc = tgo_load_partition_layout(CTX(h), n_global, lo, hi, &e, &o, (const int32_t*)lg);
+    }
+    if (s) (*env)->ReleaseIntArrayElements(env, src, s, JNI_ABORT);
+    if (d) (*env)->ReleaseIntArrayElements(env, dst, d, JNI_ABORT);
+    if (w) (*env)->ReleaseIntArrayElements(env, weight, w, JNI_ABORT);
+    if (lg) (*env)->ReleaseIntArrayElements(env, layout_global, lg, JNI_ABORT);
+    return rc;
+}
+
+/* tgo_exchange_rccl_id: the 128-byte RCCL unique id (worker 0 makes it, every worker of the
+ * JVM creates its communicator from the same bytes), null on failure. */
+JNIEXPORT jbyteArray JNICALL JFN(exchangeRcclId)(JNIEnv* env, jclass cls) {
+    (void)cls;
+    uint8_t id[128];
+    if (tgo_exchange_rccl_id(id) != TGO_OK) return NULL;
+    jbyteArray out = (*env)->NewByteArray(env, 128);
+    if (out) (*env)->SetByteArrayRegion(env, out, 0, 128, (const jbyte*)id);
+    return out;
+}
+
+/* tgo_exchange_rccl_create: 0 on failure.  Every rank of `world` must call it concurrently
+ * (one thread per device): RCCL's communicator set-up is collective. */
+JNIEXPORT jlong JNICALL JFN(exchangeRcclCreate)(JNIEnv* env, jclass cls, jint world, jint rank, jbyteArray id,
+                                                jint device) {
+    (void)cls;
+    if (!id || (*env)->GetArrayLength(env, id) != 128 || world < 1 || rank < 0 || rank >= world) return 0;
+    uint8_t b[128];
+    (*env)->GetByteArrayRegion(env, id, 0, 128, (jbyte*)b);
+    tgo_exchange* x = NULL;
+    return tgo_exchange_rccl_create(world, rank, b, device, &x) == TGO_OK ? (jlong)(intptr_t)x : 0;
+}
+
+JNIEXPORT void JNICALL JFN(exchangeDestroy)(JNIEnv* env, jclass cls, jlong x) {
+    (void)env; (void)cls;
+    if (x) tgo_exchange_destroy(XCH(x));
+}
+
+JNIEXPORT jstring JNICALL JFN(exchangeLastError)(JNIEnv* env, jclass cls, jlong x) {
+    (void)cls;
+    return (*env)->NewStringUTF(env, x ? tgo_exchange_last_error(XCH(x)) : "no exchange");
+}
+
+/* The partitioned programs as one call each; outputs are the owned vertices in row order
+ * (n_local = tgo_num_vertices of the partition ctx), null on failure (see lastError). */
+static jsize owned(JNIEnv* env, jlong h) {
+    const int64_t n = tgo_num_vertices(CTX(h));
+    return fits_jsize(env, n, "a partition larger than a Java array holds") ? (jsize)n : -1;
+}
+
+JNIEXPORT jlongArray JNICALL JFN(partBfsRun)(JNIEnv* env, jclass cls, jlong h, jlong x, jlong seed, jint max_depth,
+                                             jdouble alpha, jdouble beta) {
+    (void)cls;
+    const jsize n = owned(env, h);
+    if (n < 0 || !x) return NULL;
+    jlongArray out = (*env)->NewLongArray(env, n);
+    if (!out) return NULL;
+    jlong* p = (*env)->GetLongArrayElements(env, out, NULL);
+    int32_t levels = 0;
+    const int rc = p ? tgo_part_bfs_run(CTX(h), XCH(x), seed, max_depth, alpha, beta, (int64_t*)p, NULL, &levels) : TGO_E_OOM;
+    if (p) (*env)->ReleaseLongArrayElements(env, out, p, 0);
+    return rc == TGO_OK ? out : NULL;
+}
+
+JNIEXPORT jlongArray JNICALL JFN(partSsspRun)(JNIEnv* env, jclass cls, jlong h, jlong x, jlong seed, jlong delta) {
+    (void)cls;
+    const jsize n = owned(env, h);
+    if (n < 0 || !x) return NULL;
+    jlongArray out = (*env)->NewLongArray(env, n);
+    if (!out) return NULL;
+    jlong* p = (*env)->GetLongArrayElements(env, out, NULL);
+    int32_t phases = 0;
+    const int rc = p ? tgo_part_sssp_run(CTX(h), XCH(x), seed, delta, (int64_t*)p, NULL, &phases) : TGO_E_OOM;
+    if (p) (*env)->ReleaseLongArrayElements(env, out, p, 0);
+    return rc == TGO_OK ? out : NULL;
+}
+
+JNIEXPORT jdoubleArray JNICALL JFN(partPageRankRun)(JNIEnv* env, jclass cls, jlong h, jlong x, jdouble alpha,
+                                                    jlong vertex_count, jint iterations, jint exchange_mode) {
+    (void)cls;
+    const jsize n = owned(env, h);
+    if (n < 0 || !x) return NULL;
+    jdoubleArray out = (*env)->NewDoubleArray(env, n);
+    if (!out) return NULL;
+    jdouble* p = (*env)->GetDoubleArrayElements(env, out, NULL);
+    tgo_pr_args a;
+    memset(&a, 0, sizeof a);
+    a.alpha = alpha;
+    a.vertex_count = vertex_count;
+    a.max_iterations = iterations;
+    int64_t moved = 0;
+    const int rc = p ? tgo_part_pagerank_run(CTX(h), XCH(x), &a, exchange_mode, (double*)p, &moved) : TGO_E_OOM;
+    if (p) (*env)->ReleaseDoubleArrayElements(env, out, p, 0);
+    return rc == TGO_OK ? out : NULL;
+}
+
+/* tgo_part_msbfs_run: long[1 + 2 * nseeds] = {levels, reached per seed..., entries per seed...}
+ * (global counts), null on failure; the owned levels of source i then come from partMsLevels. */
+JNIEXPORT jlongArray JNICALL JFN(partMsbfsRun)(JNIEnv* env, jclass cls, jlong h, jlong x, jlongArray seeds,
+                                               jint max_depth, jdouble ms_alpha, jlong fixed_bytes) {
+    (void)cls;
+    if (!seeds || !x) return NULL;
+    const jsize ns = (*env)->GetArrayLength(env, seeds);
+    if (ns < 1 || ns > 64) return NULL;
+    jlong sd[64], re[64], en[64];
+    (*env)->GetLongArrayRegion(env, seeds, 0, ns, sd);
+    int32_t levels = 0;
+    if (tgo_part_msbfs_run(CTX(h), XCH(x), (const int64_t*)sd, ns, max_depth, ms_alpha, fixed_bytes, (int64_t*)re,
+                           (int64_t*)en, &levels) != TGO_OK)
+        return NULL;
+    jlongArray out = (*env)->NewLongArray(env, 1 + 2 * ns);
+    if (!out) return NULL;
+    const jlong lv = levels;
+    (*env)->SetLongArrayRegion(env, out, 0, 1, &lv);
+    (*env)->SetLongArrayRegion(env, out, 1, ns, re);
+    (*env)->SetLongArrayRegion(env, out, 1 + ns, ns, en);
+    return out;
+}
+
+JNIEXPORT jlongArray JNICALL JFN(partMsLevels)(JNIEnv* env, jclass cls, jlong h, jint source) {
+    (void)cls;
+    const jsize n = owned(env, h);
+    if (n < 0) return NULL;
+    jlongArray out = (*env)->NewLongArray(env, n);
+    if (!out) return NULL;
+    jlong* p = (*env)->GetLongArrayElements(env, out, NULL);
+    const int rc = p ? tgo_part_ms_levels(CTX(h), source, (int64_t*)p) : TGO_E_OOM;
+    if (p) (*env)->ReleaseLongArrayElements(env, out, p, 0);
+    return rc == TGO_OK ? out : NULL;
 }

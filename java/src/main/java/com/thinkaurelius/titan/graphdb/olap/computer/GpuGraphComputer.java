@@ -58,6 +58,7 @@ public class GpuGraphComputer implements TitanGraphComputer {
     private final Set<MapReduce> mapReduces = new HashSet<>();
     private int numThreads = 1;
     private int device = 0;
+    private int[] devices = null;       // > 1: the multi-GPU path (PartitionedRun)
     private ResultGraph resultGraphMode = null;
     private Persist persistMode = null;
     private boolean executed = false;
@@ -68,6 +69,20 @@ public class GpuGraphComputer implements TitanGraphComputer {
 
     public GpuGraphComputer device(int ordinal) {
         this.device = ordinal;
+        this.devices = null;
+        return this;
+    }
+
+    /**
+     * Several GPUs of this node: programs that partition (PageRank, and ShortestDistance when its
+     * depth bound cannot cut a path — the converged distances) run 1-D vertex-partitioned, one
+     * worker thread per device with an RCCL communicator each ({@link PartitionedRun}); the
+     * others run on the first device alone.
+     */
+    public GpuGraphComputer devices(int... ordinals) {
+        Preconditions.checkArgument(ordinals != null && ordinals.length > 0, "no devices");
+        this.device = ordinals[0];
+        this.devices = ordinals.length > 1 ? ordinals.clone() : null;
         return this;
     }
 
@@ -123,6 +138,9 @@ public class GpuGraphComputer implements TitanGraphComputer {
             throw GraphComputer.Exceptions.resultGraphPersistCombinationNotSupported(resultGraph, persist);
         final DeviceProgram program = DeviceProgram.recognise(vertexProgram);
         final FulgoraMemory memory = new FulgoraMemory(vertexProgram, mapReduces);
+        if (devices != null && program.partitioned(Long.MAX_VALUE) != null)
+            return CompletableFuture.<ComputerResult>supplyAsync(() -> submitPartitioned(program, memory, persist,
+                    resultGraph));
         return CompletableFuture.<ComputerResult>supplyAsync(() -> {
             final long start = System.currentTimeMillis();
             long ctx = TgoNative.create(device, graph.getIDManager().getPartitionBits(), numThreads,
@@ -190,6 +208,66 @@ public class GpuGraphComputer implements TitanGraphComputer {
                 TgoNative.destroy(ctx);
             }
         });
+    }
+
+    /**
+     * The multi-GPU path: one decoding scan (PartitionedRun.EdgeCollectingScanJob), then one
+     * worker per device; the map phase and the write-back are the single-GPU path's, on the
+     * gathered results (row order = the sorted live vertex ids).  The device-encoded write-back
+     * needs one ctx holding every vertex, so results persist through the transactional path.
+     */
+    private ComputerResult submitPartitioned(DeviceProgram program, FulgoraMemory memory, Persist persist,
+                                             ResultGraph resultGraph) {
+        final long start = System.currentTimeMillis();
+        try {
+            PartitionedRun.Collected collected = new PartitionedRun.Collected(program.weightKey(graph) != 0);
+            StandardScanner.Builder scan = graph.getBackend().buildEdgeScanJob();
+            scan.setJobId("gpu-olap#partitioned-load");
+            scan.setNumProcessingThreads(numThreads);
+            scan.setWorkBlockSize(CsrCollectingScanJob.DEFAULT_BLOCK_ROWS);
+            scan.setJob(new PartitionedRun.EdgeCollectingScanJob(graph, program.weightKey(graph), collected));
+            ScanMetrics m = scan.execute().get();
+            if (m.get(ScanMetrics.Metric.FAILURE) > 0)
+                throw new TitanException("Failed to process [" + m.get(ScanMetrics.Metric.FAILURE) + "] rows");
+            PartitionedRun.Program p = program.partitioned(collected.vertices.size);
+            if (p == null) throw new TitanException("the program cannot run partitioned on this graph");
+            Object[] out = PartitionedRun.run(collected, p, devices, graph.getIDManager().getPartitionBits(), numThreads,
+                    QueryContainer.DEFAULT_HARD_QUERY_LIMIT);
+            long[] ids = (long[]) out[0];
+            Map<String, Object> values = new HashMap<>();
+            values.put(program.computeKeys()[0], out[1]);
+            for (int i = 0; i <= program.iterations(); i++) memory.incrIteration();
+            for (MapReduce mr : mapReduces) {
+                FulgoraMapEmitter emitter = new FulgoraMapEmitter<>(mr.doStage(MapReduce.Stage.REDUCE));
+                program.emit(ids, values, emitter);
+                emitter.complete(mr);
+                if (mr.doStage(MapReduce.Stage.REDUCE)) {
+                    FulgoraReduceEmitter reduce = new FulgoraReduceEmitter<>();
+                    mr.workerStart(MapReduce.Stage.REDUCE);
+                    for (Object e : emitter.reduceMap.entrySet()) {
+                        Map.Entry entry = (Map.Entry) e;
+                        mr.reduce(entry.getKey(), ((Iterable) entry.getValue()).iterator(), reduce);
+                    }
+                    mr.workerEnd(MapReduce.Stage.REDUCE);
+                    reduce.complete(mr);
+                    mr.addResultToMemory(memory, reduce.reduceQueue.iterator());
+                } else {
+                    mr.addResultToMemory(memory, emitter.mapQueue.iterator());
+                }
+            }
+            org.apache.tinkerpop.gremlin.structure.Graph result = graph;
+            if (persist == Persist.VERTEX_PROPERTIES) {
+                if (resultGraph == ResultGraph.NEW) result = WriteBack.localTx(graph, ids, values, program);
+                else WriteBack.transactional(graph, ids, values, program, numThreads);
+            }
+            memory.setRuntime(System.currentTimeMillis() - start);
+            memory.complete();
+            return new DefaultComputerResult(result, memory.asImmutable());
+        } catch (TitanException e) {
+            throw e;
+        } catch (Exception e) {
+            throw new TitanException(e);
+        }
     }
 
     @Override
@@ -420,6 +498,11 @@ public class GpuGraphComputer implements TitanGraphComputer {
                 mgmt.rollback();
             }
         }
+        /**
+         * The multi-GPU form of the program over n live vertices, or null when it has none
+         * (then the program runs on one device).
+         */
+        PartitionedRun.Program partitioned(long n) { return null; }
         /** The value of compute-key array `values` at row i, null when the vertex holds none. */
         Object valueAt(Object values, int i) {
             if (values instanceof long[]) { long d = ((long[]) values)[i]; return d == TgoNative.DIST_ABSENT ? null : d; }
@@ -472,6 +555,17 @@ public class GpuGraphComputer implements TitanGraphComputer {
             v.put("titan.pageRank.pageRank", TgoNative.checked(ctx, TgoNative.pageRank(ctx, alpha, vertexCount, maxIterations)));
             return v;
         }
+        PartitionedRun.Program partitioned(long n) {
+            return new PartitionedRun.Program() {
+                public int scope() { return TgoNative.SCOPE_IN_E; }
+                public boolean applyCap() { return true; }
+                public Object run(long ctx, long x, long[] live) {
+                    return TgoNative.partPageRankRun(ctx, x, alpha, vertexCount, maxIterations,
+                            PartitionedRun.PR_EXCHANGE_GHOST);
+                }
+                public Object newResult(int count) { return new double[count]; }
+            };
+        }
         void emit(long[] ids, Map<String, Object> values, FulgoraMapEmitter emitter) {
             double[] pr = (double[]) values.get("titan.pageRank.pageRank");
             for (int i = 0; i < ids.length; i++) if (!Double.isNaN(pr[i])) emitter.emit(ids[i], pr[i]);
@@ -503,6 +597,26 @@ public class GpuGraphComputer implements TitanGraphComputer {
             v.put("titan.shortestDistanceVertexProgram.distance", TgoNative.checked(ctx,
                     TgoNative.sssp(ctx, seed, maxDepth, scope(), TgoNative.SSSP_HOP_BOUNDED, 0)));
             return v;
+        }
+        /**
+         * Partitioned: delta-stepping's converged distances, which equal the hop-bounded result
+         * only when no shortest path can exceed maxDepth hops — maxDepth >= n - 1 (a shortest
+         * path visits each vertex once).  n is unknown before the scan (Long.MAX_VALUE asks
+         * whether a partitioned form may exist at all).
+         */
+        PartitionedRun.Program partitioned(long n) {
+            if (n != Long.MAX_VALUE && maxDepth < n - 1) return null;
+            return new PartitionedRun.Program() {
+                public int scope() { return TgoNative.SCOPE_IN_E; }
+                public boolean applyCap() { return true; }
+                public Object run(long ctx, long x, long[] live) {
+                    // every worker runs the same phases (collectives), so a seed that is no live
+                    // vertex still runs: -1 reaches nobody (every distance TGO_DIST_ABSENT)
+                    int s = java.util.Arrays.binarySearch(live, seed);
+                    return TgoNative.partSsspRun(ctx, x, s >= 0 ? s : -1, 0);
+                }
+                public Object newResult(int count) { return new long[count]; }
+            };
         }
         void emit(long[] ids, Map<String, Object> values, FulgoraMapEmitter emitter) {
             long[] d = (long[]) values.get("titan.shortestDistanceVertexProgram.distance");

@@ -87,6 +87,48 @@ public final class TgoNative {
      */
     public static native Object[] resultRows(long ctx, int kind, long[] keyIds, int[] datatypes, long relationIdBase);
 
+    /* ---- multi-GPU (include/titan_gpu_olap_part.h; PartitionedRun): one ctx + one exchange per
+     * GPU worker thread, the ranks' vertex ranges [lo, hi) of the global dense ids. ---- */
+
+    /** tgo_part_layout: the degree-grouped ids of the owned vertices (int[hi - lo]); null on failure. */
+    public static native int[] partLayout(int[] src, int[] dst, long nGlobal, long lo, long hi, int threads);
+
+    /**
+     * tgo_load_partition_layout: edges (dense global ids) holding every edge with an endpoint in
+     * [lo, hi); weight null when unweighted; layoutGlobal null = ids as given, else every
+     * worker's partLayout slice gathered (int[nGlobal]).
+     */
+    public static native int loadPartition(long ctx, long nGlobal, long lo, long hi, int[] src, int[] dst, int[] weight,
+                                           int scope, boolean applyCap, int[] layoutGlobal);
+
+    /** tgo_exchange_rccl_id: the 128-byte RCCL unique id (made once, shared by every worker). */
+    public static native byte[] exchangeRcclId();
+
+    /** tgo_exchange_rccl_create (collective: every rank calls it concurrently); 0 on failure. */
+    public static native long exchangeRcclCreate(int world, int rank, byte[] id, int device);
+
+    public static native void exchangeDestroy(long exchange);
+
+    public static native String exchangeLastError(long exchange);
+
+    /** tgo_part_bfs_run: the owned distances in row order; null on failure (see lastError). */
+    public static native long[] partBfsRun(long ctx, long exchange, long seedGlobal, int maxDepth, double alpha,
+                                           double beta);
+
+    /** tgo_part_sssp_run (delta-stepping, converged distances): owned distances; null on failure. */
+    public static native long[] partSsspRun(long ctx, long exchange, long seedGlobal, long delta);
+
+    /** tgo_part_pagerank_run: owned ranks; null on failure.  exchangeMode 0 all-gather, 1 ghost. */
+    public static native double[] partPageRankRun(long ctx, long exchange, double alpha, long vertexCount,
+                                                  int maxIterations, int exchangeMode);
+
+    /** tgo_part_msbfs_run: {levels, reached per seed..., entries per seed...} (global); null on failure. */
+    public static native long[] partMsbfsRun(long ctx, long exchange, long[] seedsGlobal, int maxDepth, double msAlpha,
+                                             long fixedExchangeBytes);
+
+    /** tgo_part_ms_levels: source i's owned distances after partMsbfsRun; null on failure. */
+    public static native long[] partMsLevels(long ctx, int source);
+
     /** A non-zero status of a C-ABI call as a TitanException carrying tgo_last_error(). */
     public static void check(long ctx, int rc) {
         if (rc != 0) throw new TitanException("[" + rc + "] " + lastError(ctx));

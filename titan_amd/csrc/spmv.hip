@@ -522,10 +522,14 @@ __device__ __forceinline__ void fx_add(unsigned long long* plo, unsigned long lo
 // A tile's entries (packed source << rbits | accumulator) into the LDS accumulators: all index
 // loads, then all gathers, then the conversions and LDS atomics, kFxUnroll entries per thread
 // in flight.  lc: log2 of the copies per accumulator (the lane picks the copy).
+// diag (TGO_PR_FX_DIAG, results wrong by design; attribution only): 1 = no LDS atomics (the
+// values are folded into one register), 2 = no gathers (the index word stands in for the value)
+template <int diag = 0>
 __device__ __forceinline__ void fx_accumulate(const uint32_t* __restrict__ p, int64_t ne, const double* __restrict__ msg,
                                               int rbits, int lc, unsigned long long* s_lo, unsigned long long* s_hi) {
     const uint32_t rmask = (1u << rbits) - 1u;
     const uint32_t cl = threadIdx.x & ((1u << lc) - 1u);
+    unsigned long long sink = 0;
     for (int64_t b = 0; b < ne; b += static_cast<int64_t>(kFxThreads) * kFxUnroll) {
         uint32_t w[kFxUnroll];
 #pragma unroll
@@ -537,18 +541,21 @@ __device__ __forceinline__ void fx_accumulate(const uint32_t* __restrict__ p, in
 #pragma unroll
         for (int j = 0; j < kFxUnroll; ++j) {
             const int64_t k = b + j * kFxThreads + threadIdx.x;
-            v[j] = k < ne ? msg[w[j] >> rbits] : 0.0;
+            v[j] = k < ne ? (diag == 2 ? static_cast<double>(w[j]) * 0x1p-40 : msg[w[j] >> rbits]) : 0.0;
         }
 #pragma unroll
         for (int j = 0; j < kFxUnroll; ++j) {
             unsigned long long lo, hi;
             fx_of(v[j], lo, hi);
-            if (lo | hi) {
+            if (diag == 1) {
+                sink += lo ^ hi ^ (w[j] & rmask);
+            } else if (lo | hi) {
                 const uint32_t slot = ((w[j] & rmask) << lc) | cl;
                 fx_add(&s_lo[slot], &s_hi[slot], lo, hi);
             }
         }
     }
+    if (diag == 1 && sink == 0x5a5a5a5a5a5a5a5aull) s_lo[0] = sink;      // keep the loads alive
 }
 __device__ __forceinline__ int fx_copies_log2(int rows, int slots = kFxSlots) {
     int lc = 6;
@@ -570,6 +577,7 @@ __device__ __forceinline__ void fx_total(const unsigned long long* s_lo, const u
 // One super-tile per workgroup: desc {first entry, end entry, first row, rows | -(long + 1)}.
 // Each row has 2^lc copies of its accumulator (rows * copies <= kFxSlots), the copy chosen by
 // the lane, so a tile of few rows does not serialise its lanes on one LDS address.
+template <int diag>
 __global__ void __launch_bounds__(kFxThreads) gather_hot_fx(const uint32_t* __restrict__ padj,
         const int64_t* __restrict__ desc, int rbits, const double* __restrict__ msg, PrColdFinal fin,
         unsigned long long* __restrict__ long_acc) {
@@ -581,7 +589,7 @@ __global__ void __launch_bounds__(kFxThreads) gather_hot_fx(const uint32_t* __re
     const int nslots = rows << lc;
     for (int i = threadIdx.x; i < nslots; i += kFxThreads) { s_lo[i] = 0; s_hi[i] = 0; }
     __syncthreads();
-    fx_accumulate(padj + e0, e1 - e0, msg, rbits, lc, s_lo, s_hi);
+    fx_accumulate<diag>(padj + e0, e1 - e0, msg, rbits, lc, s_lo, s_hi);
     __syncthreads();
     if (nr > 0) {
         for (int i = threadIdx.x; i < rows; i += kFxThreads) {
@@ -608,7 +616,7 @@ __global__ void __launch_bounds__(kFxThreads) gather_hot_fx(const uint32_t* __re
 // piece's exact sum goes to partial[] as a double, where cold_fold adds a row's pieces in
 // segment order as before.
 // kSlots = 8192 (TGO_PR_FX_CP): 13-bit piece ids, 128 KB of dynamic LDS, one workgroup a CU.
-template <int kSlots>
+template <int kSlots, int diag>
 __global__ void __launch_bounds__(kFxThreads) cold_fx(const uint32_t* __restrict__ cadj,
         const int64_t* __restrict__ cfd, XcdBase xb, const double* __restrict__ msg, double* __restrict__ partial,
         int shift) {
@@ -623,7 +631,7 @@ __global__ void __launch_bounds__(kFxThreads) cold_fx(const uint32_t* __restrict
     const int lc = fx_copies_log2(np, kSlots);
     for (int i = threadIdx.x; i < (np << lc); i += kFxThreads) { s_lo[i] = 0; s_hi[i] = 0; }
     __syncthreads();
-    fx_accumulate(cadj + e0, e1 - e0, msg + (w >> 16), shift, lc, s_lo, s_hi);
+    fx_accumulate<diag>(cadj + e0, e1 - e0, msg + (w >> 16), shift, lc, s_lo, s_hi);
     __syncthreads();
     for (int i = threadIdx.x; i < np; i += kFxThreads) {
         unsigned long long lo, hi;
@@ -927,6 +935,10 @@ hipError_t k_pr_iter(const DevCsr& in, const RowBlocks& rb, const double* contri
 }
 // Cold phase: the cold segments' partial sums, folded per row into csum (reads only the cold
 // sources [hot, n_src) of `contrib`).
+static int fx_diag() {                                // read per launch: an A/B flips it between runs
+    const char* e = std::getenv("TGO_PR_FX_DIAG");
+    return e ? std::atoi(e) : 0;
+}
 static bool row_prefetch() {
     static const bool on = [] { const char* e = std::getenv("TGO_PR_PF"); return !e || std::atoi(e) != 0; }();
     return on;
@@ -952,16 +964,24 @@ hipError_t k_pr_cold_phase(const ColdBlocks& cb, const double* contrib, hipStrea
             constexpr size_t lds = 2 * 8192 * sizeof(unsigned long long);
             static bool lds_set = false;              // the > 64 KB dynamic LDS limit, raised once
             if (!lds_set) {
-                const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&cold_fx<8192>),
+                const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&cold_fx<8192, 0>),
                                                          hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
                 if (e != hipSuccess) return e;
                 lds_set = true;
             }
-            cold_fx<8192><<<g, kFxThreads, lds, s>>>(reinterpret_cast<const uint32_t*>(cb.cadj), cb.cfx_desc, cb.xbase,
-                                                     contrib, cb.partial, cb.cfx_shift);
-        } else if (cb.cfx)
-            cold_fx<kFxSlots><<<g, kFxThreads, 2 * kFxSlots * sizeof(unsigned long long), s>>>(
-                reinterpret_cast<const uint32_t*>(cb.cadj), cb.cfx_desc, cb.xbase, contrib, cb.partial, cb.cfx_shift);
+            cold_fx<8192, 0><<<g, kFxThreads, lds, s>>>(reinterpret_cast<const uint32_t*>(cb.cadj), cb.cfx_desc, cb.xbase,
+                                                        contrib, cb.partial, cb.cfx_shift);
+        } else if (cb.cfx) {
+            const size_t lds = 2 * kFxSlots * sizeof(unsigned long long);
+            const uint32_t* cadj = reinterpret_cast<const uint32_t*>(cb.cadj);
+            const int d = fx_diag();
+            if (d == 1)
+                cold_fx<kFxSlots, 1><<<g, kFxThreads, lds, s>>>(cadj, cb.cfx_desc, cb.xbase, contrib, cb.partial, cb.cfx_shift);
+            else if (d == 2)
+                cold_fx<kFxSlots, 2><<<g, kFxThreads, lds, s>>>(cadj, cb.cfx_desc, cb.xbase, contrib, cb.partial, cb.cfx_shift);
+            else
+                cold_fx<kFxSlots, 0><<<g, kFxThreads, lds, s>>>(cadj, cb.cfx_desc, cb.xbase, contrib, cb.partial, cb.cfx_shift);
+        }
         else if (cb.cpacked && row_prefetch())
             cold_gather<true, true><<<g, kBlock, 0, s>>>(cb.poff, cb.cadj, cb.bbeg, cb.bend, cb.xblk, cb.bsrc, cb.cdesc, cb.xbase,
                                                          contrib, cb.partial);
@@ -983,9 +1003,17 @@ hipError_t k_pr_hot_phase(const ColdBlocks& cb, const double* contrib, const dou
                           double* contrib_next, double* partial_long, double alpha, double base, hipStream_t s) {
     const PrColdFinal fin{PrFinal{edge_count, pr, contrib_next, alpha, base}, cb.csum};
     if (cb.fx) {
-        if (cb.fx_ntiles > 0)
-            gather_hot_fx<<<static_cast<unsigned>(cb.fx_ntiles), kFxThreads, 0, s>>>(
-                reinterpret_cast<const uint32_t*>(cb.hcsr.adj), cb.fx_desc, cb.fx_rbits, contrib, fin, cb.fx_long_acc);
+        if (cb.fx_ntiles > 0) {
+            const unsigned g = static_cast<unsigned>(cb.fx_ntiles);
+            const uint32_t* padj = reinterpret_cast<const uint32_t*>(cb.hcsr.adj);
+            const int d = fx_diag();
+            if (d == 1)
+                gather_hot_fx<1><<<g, kFxThreads, 0, s>>>(padj, cb.fx_desc, cb.fx_rbits, contrib, fin, cb.fx_long_acc);
+            else if (d == 2)
+                gather_hot_fx<2><<<g, kFxThreads, 0, s>>>(padj, cb.fx_desc, cb.fx_rbits, contrib, fin, cb.fx_long_acc);
+            else
+                gather_hot_fx<0><<<g, kFxThreads, 0, s>>>(padj, cb.fx_desc, cb.fx_rbits, contrib, fin, cb.fx_long_acc);
+        }
         if (cb.fx_nlong > 0)
             finalize_long_fx<<<grid_for(cb.fx_nlong), kBlock, 0, s>>>(cb.fx_long_row, cb.fx_nlong, cb.fx_long_acc, fin);
         return hipGetLastError();
