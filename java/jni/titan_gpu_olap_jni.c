@@ -460,8 +460,9 @@ static jsize owned(JNIEnv* env, jlong h) {
 JNIEXPORT jlongArray JNICALL JFN(partBfsRun)(JNIEnv* env, jclass cls, jlong h, jlong x, jlong seed, jint max_depth,
                                              jdouble alpha, jdouble beta) {
     (void)cls;
+    if (!h || !x) return NULL;                            /* validated before the ctx is touched */
     const jsize n = owned(env, h);
-    if (n < 0 || !x) return NULL;
+    if (n < 0) return NULL;
     jlongArray out = (*env)->NewLongArray(env, n);
     if (!out) return NULL;
     jlong* p = (*env)->GetLongArrayElements(env, out, NULL);
@@ -473,8 +474,9 @@ JNIEXPORT jlongArray JNICALL JFN(partBfsRun)(JNIEnv* env, jclass cls, jlong h, j
 
 JNIEXPORT jlongArray JNICALL JFN(partSsspRun)(JNIEnv* env, jclass cls, jlong h, jlong x, jlong seed, jlong delta) {
     (void)cls;
+    if (!h || !x) return NULL;                            /* validated before the ctx is touched */
     const jsize n = owned(env, h);
-    if (n < 0 || !x) return NULL;
+    if (n < 0) return NULL;
     jlongArray out = (*env)->NewLongArray(env, n);
     if (!out) return NULL;
     jlong* p = (*env)->GetLongArrayElements(env, out, NULL);
@@ -487,8 +489,9 @@ JNIEXPORT jlongArray JNICALL JFN(partSsspRun)(JNIEnv* env, jclass cls, jlong h, 
 JNIEXPORT jdoubleArray JNICALL JFN(partPageRankRun)(JNIEnv* env, jclass cls, jlong h, jlong x, jdouble alpha,
                                                     jlong vertex_count, jint iterations, jint exchange_mode) {
     (void)cls;
+    if (!h || !x) return NULL;                            /* validated before the ctx is touched */
     const jsize n = owned(env, h);
-    if (n < 0 || !x) return NULL;
+    if (n < 0) return NULL;
     jdoubleArray out = (*env)->NewDoubleArray(env, n);
     if (!out) return NULL;
     jdouble* p = (*env)->GetDoubleArrayElements(env, out, NULL);

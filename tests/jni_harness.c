@@ -1,15 +1,23 @@
-/* Runtime check of the JNI shim's argument validation without a JVM (tests/test_jni_shim.py).
+/* Runtime check of the JNI shim without a JVM (tests/test_jni_shim.py).
  *
  * java/jni/titan_gpu_olap_jni.c is linked into this program together with a fake JNIEnv whose
  * arrays are plain C buffers (tests/jni_stub/jni.h declares the table), and this program's own
  * tgo_load_csr, which records the call instead of touching a device (the executable's
- * definition is the one the shim's call binds to).  Each case calls the loadCsr entry point
- * as TgoNative.loadCsr would and checks the status and whether tgo_load_csr was reached.
+ * definition is the one the shim's call binds to); every other entry point is the real
+ * library's.  The loadCsr cases call the entry point as TgoNative.loadCsr would and check the
+ * status and whether tgo_load_csr was reached; the multi-GPU cases check the argument
+ * validation of the partition / exchange natives and run tgo_part_layout (host work).
+ * `jni_harness gpu` (a GPU box) then drives the Java multi-GPU path end to end at world 1:
+ * create, partLayout, loadPartition, exchangeRcclId / exchangeRcclCreate and the three native
+ * loops through the shim, against the one-GPU engine on the same graph.
  * Prints one line per case; exit status = failed cases. */
 #include <jni.h>
+#include <math.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include "titan_gpu_olap.h"
+#include "titan_gpu_olap_part.h"
 
 typedef struct { jsize len; void* data; } FakeArr;
 #define ARR(a) ((jarray)(void*)(a))
@@ -26,6 +34,33 @@ static void long_region(JNIEnv* env, jlongArray a, jsize start, jsize len, jlong
     if (start < 0 || len < 0 || start + len > f->len) { region_oob = 1; return; }   /* JNI: ArrayIndexOutOfBounds */
     memcpy(buf, (jlong*)f->data + start, (size_t)len * sizeof(jlong));
 }
+
+/* arrays the shim creates (New*Array) and region copies with the JNI bounds rule */
+static int thrown = 0;
+static jclass find_class(JNIEnv* env, const char* name) { (void)env; (void)name; return (jclass)(void*)&thrown; }
+static jint throw_new(JNIEnv* env, jclass c, const char* msg) { (void)env; (void)c; (void)msg; thrown = 1; return 0; }
+static jstring new_string(JNIEnv* env, const char* utf) { (void)env; return (jstring)(void*)utf; }
+static jarray new_arr(jsize len, size_t es) {
+    FakeArr* f = (FakeArr*)calloc(1, sizeof(FakeArr));
+    f->len = len;
+    f->data = calloc((size_t)(len > 0 ? len : 1), es);
+    return (jarray)(void*)f;
+}
+static jbyteArray new_bytes(JNIEnv* env, jsize len) { (void)env; return new_arr(len, 1); }
+static jintArray new_ints(JNIEnv* env, jsize len) { (void)env; return new_arr(len, 4); }
+static jlongArray new_longs(JNIEnv* env, jsize len) { (void)env; return new_arr(len, 8); }
+static jdoubleArray new_doubles(JNIEnv* env, jsize len) { (void)env; return new_arr(len, 8); }
+static jdouble* get_doubles(JNIEnv* env, jdoubleArray a, jboolean* c) { (void)env; (void)c; return (jdouble*)((FakeArr*)(void*)a)->data; }
+static void rel_doubles(JNIEnv* env, jdoubleArray a, jdouble* p, jint m) { (void)env; (void)a; (void)p; (void)m; }
+static void region(jarray a, jsize start, jsize len, void* buf, size_t es, int to_array) {
+    FakeArr* f = (FakeArr*)(void*)a;
+    if (start < 0 || len < 0 || start + len > f->len) { region_oob = 1; return; }
+    if (to_array) memcpy((char*)f->data + (size_t)start * es, buf, (size_t)len * es);
+    else memcpy(buf, (char*)f->data + (size_t)start * es, (size_t)len * es);
+}
+static void get_byte_region(JNIEnv* env, jbyteArray a, jsize s, jsize l, jbyte* b) { (void)env; region(a, s, l, b, 1, 0); }
+static void set_byte_region(JNIEnv* env, jbyteArray a, jsize s, jsize l, const jbyte* b) { (void)env; region(a, s, l, (void*)b, 1, 1); }
+static void set_long_region(JNIEnv* env, jlongArray a, jsize s, jsize l, const jlong* b) { (void)env; region(a, s, l, (void*)b, 8, 1); }
 
 static struct JNINativeInterface_ table;
 static int csr_calls = 0;
@@ -46,7 +81,166 @@ jint Java_com_thinkaurelius_titan_graphdb_olap_gpu_TgoNative_loadCsr(JNIEnv* env
         jlongArray out_off, jintArray out_idx, jintArray out_w, jlongArray in_off, jintArray in_idx, jintArray in_w,
         jint scope, jlong weight_key, jboolean column_order);
 
+#define JFN(name) Java_com_thinkaurelius_titan_graphdb_olap_gpu_TgoNative_##name
+jlong JFN(create)(JNIEnv*, jclass, jint, jint, jint, jlong);
+void JFN(destroy)(JNIEnv*, jclass, jlong);
+jintArray JFN(partLayout)(JNIEnv*, jclass, jintArray, jintArray, jlong, jlong, jlong, jint);
+jint JFN(loadPartition)(JNIEnv*, jclass, jlong, jlong, jlong, jlong, jintArray, jintArray, jintArray, jint, jboolean,
+                        jintArray);
+jbyteArray JFN(exchangeRcclId)(JNIEnv*, jclass);
+jlong JFN(exchangeRcclCreate)(JNIEnv*, jclass, jint, jint, jbyteArray, jint);
+void JFN(exchangeDestroy)(JNIEnv*, jclass, jlong);
+jlongArray JFN(partBfsRun)(JNIEnv*, jclass, jlong, jlong, jlong, jint, jdouble, jdouble);
+jlongArray JFN(partSsspRun)(JNIEnv*, jclass, jlong, jlong, jlong, jlong);
+jdoubleArray JFN(partPageRankRun)(JNIEnv*, jclass, jlong, jlong, jdouble, jlong, jint, jint);
+jlongArray JFN(partMsbfsRun)(JNIEnv*, jclass, jlong, jlong, jlongArray, jint, jdouble, jlong);
+jlongArray JFN(partMsLevels)(JNIEnv*, jclass, jlong, jint);
+
 static int failures = 0;
+static void check(const char* name, int ok) {
+    printf("%s %s\n", ok ? "ok  " : "FAIL", name);
+    failures += !ok;
+}
+
+/* the test graph of the multi-GPU cases: a ring 0 -> 1 -> ... -> n-1 -> 0 plus chords
+ * v -> 3v+1 mod n, weights 1 + (v * 7 + u) % 13 */
+enum { GN = 256 };
+static jint g_src[2 * GN], g_dst[2 * GN], g_w[2 * GN];
+static int graph_edges(void) {
+    int m = 0;
+    for (int v = 0; v < GN; ++v) {
+        const int t[2] = {(v + 1) % GN, (3 * v + 1) % GN};
+        for (int k = 0; k < 2; ++k) { g_src[m] = v; g_dst[m] = t[k]; g_w[m] = 1 + (v * 7 + t[k]) % 13; ++m; }
+    }
+    return m;
+}
+
+static void partition_cases(JNIEnv* env) {
+    const int m = graph_edges();
+    FakeArr src = {m, g_src}, dst = {m, g_dst}, w = {m, g_w}, short_dst = {m - 1, g_dst}, w_short = {m - 2, g_w};
+    jint lay_d[GN];
+    FakeArr lay_short = {GN - 1, lay_d};
+    /* partLayout (host work): a permutation of the owned range */
+    jintArray lay = JFN(partLayout)(env, NULL, ARR(&src), ARR(&dst), GN, 64, 192, 2);
+    int perm_ok = lay != NULL && ((FakeArr*)(void*)lay)->len == 128;
+    if (perm_ok) {
+        int seen[GN] = {0};
+        const jint* p = (const jint*)((FakeArr*)(void*)lay)->data;
+        for (int i = 0; i < 128; ++i) perm_ok &= p[i] >= 64 && p[i] < 192 && !seen[p[i]]++;
+    }
+    check("partLayout returns a permutation of [lo, hi)", perm_ok);
+    check("partLayout rejects src / dst of different lengths",
+          JFN(partLayout)(env, NULL, ARR(&src), ARR(&short_dst), GN, 0, GN, 2) == NULL);
+    check("partLayout rejects an empty range", JFN(partLayout)(env, NULL, ARR(&src), ARR(&dst), GN, 64, 64, 2) == NULL);
+    check("partLayout rejects a range past n_global", JFN(partLayout)(env, NULL, ARR(&src), ARR(&dst), GN, 0, GN + 64, 2) == NULL);
+    /* loadPartition validates before the C-ABI (the ctx handle is fake: reaching it would crash) */
+    check("loadPartition rejects src / dst of different lengths",
+          JFN(loadPartition)(env, NULL, 1, GN, 0, GN, ARR(&src), ARR(&short_dst), NULL, 1, 1, NULL) == TGO_E_INVALID);
+    check("loadPartition rejects a short weight array",
+          JFN(loadPartition)(env, NULL, 1, GN, 0, GN, ARR(&src), ARR(&dst), ARR(&w_short), 1, 1, NULL) == TGO_E_INVALID);
+    check("loadPartition rejects a layout shorter than n_global",
+          JFN(loadPartition)(env, NULL, 1, GN, 0, GN, ARR(&src), ARR(&dst), ARR(&w), 1, 1, ARR(&lay_short)) == TGO_E_INVALID);
+    check("loadPartition rejects null edges",
+          JFN(loadPartition)(env, NULL, 1, GN, 0, GN, NULL, ARR(&dst), NULL, 1, 1, NULL) == TGO_E_INVALID);
+    /* exchange creation: 128 id bytes, 0 <= rank < world */
+    jbyte idb[128] = {0};
+    FakeArr id_short = {127, idb}, id = {128, idb};
+    check("exchangeRcclCreate rejects a 127-byte id", JFN(exchangeRcclCreate)(env, NULL, 1, 0, ARR(&id_short), 0) == 0);
+    check("exchangeRcclCreate rejects rank >= world", JFN(exchangeRcclCreate)(env, NULL, 2, 2, ARR(&id), 0) == 0);
+    /* the loops need an exchange; the sweep takes 1..64 seeds */
+    jlong sd[65] = {0};
+    FakeArr seeds65 = {65, sd}, seeds0 = {0, sd};
+    check("partBfsRun without an exchange", JFN(partBfsRun)(env, NULL, 1, 0, 0, 4, 15.0, 18.0) == NULL);
+    check("partMsbfsRun rejects 65 seeds", JFN(partMsbfsRun)(env, NULL, 1, 1, ARR(&seeds65), 4, 12.0, 0) == NULL);
+    check("partMsbfsRun rejects no seeds", JFN(partMsbfsRun)(env, NULL, 1, 1, ARR(&seeds0), 4, 12.0, 0) == NULL);
+}
+
+/* world 1 on a GPU: the Java multi-GPU calls through the shim against the one-GPU engine */
+static void gpu_cases(JNIEnv* env) {
+    const int m = graph_edges();
+    FakeArr src = {m, g_src}, dst = {m, g_dst}, w = {m, g_w};
+    jlong h = JFN(create)(env, NULL, 0, 5, 4, 100000);
+    check("create (device 0)", h != 0);
+    if (!h) return;
+    jintArray lay = JFN(partLayout)(env, NULL, ARR(&src), ARR(&dst), GN, 0, GN, 4);
+    check("partLayout (world 1)", lay != NULL);
+    jint rc = JFN(loadPartition)(env, NULL, h, GN, 0, GN, ARR(&src), ARR(&dst), ARR(&w), TGO_SCOPE_IN_E, 1, lay);
+    check("loadPartition (weighted inE, layout)", rc == TGO_OK);
+    jbyteArray id = JFN(exchangeRcclId)(env, NULL);
+    check("exchangeRcclId", id != NULL);
+    jlong x = id ? JFN(exchangeRcclCreate)(env, NULL, 1, 0, id, 0) : 0;
+    check("exchangeRcclCreate (world 1)", x != 0);
+    /* the one-GPU engine on the same edges */
+    tgo_options o;
+    tgo_default_options(&o);
+    tgo_ctx* one = NULL;
+    int ok = tgo_create(&o, &one) == TGO_OK;
+    tgo_edges e;
+    memset(&e, 0, sizeof e);
+    e.n = GN; e.m = m; e.src = (const int32_t*)g_src; e.dst = (const int32_t*)g_dst; e.weight = (const int32_t*)g_w;
+    tgo_load_opts lo;
+    memset(&lo, 0, sizeof lo);
+    lo.scope = TGO_SCOPE_IN_E;
+    lo.apply_cap = 1;
+    ok = ok && tgo_load_edges(one, &e, &lo) == TGO_OK;
+    check("one-GPU reference engine", ok);
+    if (x && ok && rc == TGO_OK) {
+        static int64_t ref[GN];
+        tgo_sssp_args sa;
+        memset(&sa, 0, sizeof sa);
+        sa.seed = 5; sa.seed_is_dense = 1; sa.max_depth = GN; sa.scope = TGO_SCOPE_IN_E; sa.mode = TGO_SSSP_DELTA;
+        jlongArray d = JFN(partSsspRun)(env, NULL, h, x, 5, 0);
+        int same = d != NULL && tgo_sssp(one, &sa, ref) == TGO_OK;
+        for (int v = 0; same && v < GN; ++v) same = ((jlong*)((FakeArr*)(void*)d)->data)[v] == ref[v];
+        check("partSsspRun == tgo_sssp (delta, converged)", same);
+        tgo_pr_args pa;
+        memset(&pa, 0, sizeof pa);
+        pa.alpha = 0.85; pa.vertex_count = GN; pa.max_iterations = 12;
+        static double pref[GN];
+        for (int mode = 0; mode < 2; ++mode) {
+            jdoubleArray p = JFN(partPageRankRun)(env, NULL, h, x, 0.85, GN, 12, mode);
+            int close = p != NULL && tgo_pagerank(one, &pa, pref) == TGO_OK;
+            double l1 = 0;
+            for (int v = 0; close && v < GN; ++v) l1 += fabs(((jdouble*)((FakeArr*)(void*)p)->data)[v] - pref[v]);
+            printf("     pagerank mode %d L1 vs one GPU %.3g\n", mode, l1);
+            check(mode ? "partPageRankRun (ghost) within 1e-12 L1 of tgo_pagerank"
+                       : "partPageRankRun (all-gather) within 1e-12 L1 of tgo_pagerank", close && l1 <= 1e-12);
+        }
+    }
+    if (x) JFN(exchangeDestroy)(env, NULL, x);
+    JFN(destroy)(env, NULL, h);
+    /* unweighted bothE: BFS and the multi-source sweep against tgo_bfs */
+    h = JFN(create)(env, NULL, 0, 5, 4, 100000);
+    lo.scope = TGO_SCOPE_BOTH_E;
+    lo.apply_cap = 0;
+    e.weight = NULL;
+    tgo_ctx* oneb = NULL;
+    ok = h != 0 && tgo_create(&o, &oneb) == TGO_OK && tgo_load_edges(oneb, &e, &lo) == TGO_OK &&
+         JFN(loadPartition)(env, NULL, h, GN, 0, GN, ARR(&src), ARR(&dst), NULL, TGO_SCOPE_BOTH_E, 0, NULL) == TGO_OK;
+    check("bothE partition + reference", ok);
+    x = (ok && id) ? JFN(exchangeRcclCreate)(env, NULL, 1, 0, id, 0) : 0;
+    if (ok && x) {
+        static int64_t ref[GN];
+        tgo_bfs_args ba;
+        memset(&ba, 0, sizeof ba);
+        ba.seed = 7; ba.seed_is_dense = 1; ba.max_depth = GN; ba.scope = TGO_SCOPE_BOTH_E;
+        jlongArray d = JFN(partBfsRun)(env, NULL, h, x, 7, GN, 15.0, 18.0);
+        int same = d != NULL && tgo_bfs(oneb, &ba, ref) == TGO_OK;
+        for (int v = 0; same && v < GN; ++v) same = ((jlong*)((FakeArr*)(void*)d)->data)[v] == ref[v];
+        check("partBfsRun == tgo_bfs", same);
+        jlong sdv[3] = {7, 100, 200};
+        FakeArr seeds = {3, sdv};
+        jlongArray r = JFN(partMsbfsRun)(env, NULL, h, x, ARR(&seeds), GN, 12.0, 1 << 20);
+        jlongArray lv = r ? JFN(partMsLevels)(env, NULL, h, 0) : NULL;
+        same = r != NULL && lv != NULL && ((FakeArr*)(void*)r)->len == 7;
+        for (int v = 0; same && v < GN; ++v) same = ((jlong*)((FakeArr*)(void*)lv)->data)[v] == ref[v];
+        check("partMsbfsRun + partMsLevels(0) == tgo_bfs", same);
+    }
+    if (x) JFN(exchangeDestroy)(env, NULL, x);
+    if (h) JFN(destroy)(env, NULL, h);
+    tgo_destroy(one);
+    tgo_destroy(oneb);
+}
 static void expect(const char* name, jint rc, jint want_rc, int want_calls) {
     const int ok = rc == want_rc && csr_calls == want_calls && !region_oob;
     printf("%s %s: rc=%d calls=%d\n", ok ? "ok  " : "FAIL", name, (int)rc, csr_calls);
@@ -55,7 +249,19 @@ static void expect(const char* name, jint rc, jint want_rc, int want_calls) {
     region_oob = 0;
 }
 
-int main(void) {
+int main(int argc, char** argv) {
+    table.FindClass = find_class;
+    table.ThrowNew = throw_new;
+    table.NewStringUTF = new_string;
+    table.NewByteArray = new_bytes;
+    table.NewIntArray = new_ints;
+    table.NewLongArray = new_longs;
+    table.NewDoubleArray = new_doubles;
+    table.GetDoubleArrayElements = get_doubles;
+    table.ReleaseDoubleArrayElements = rel_doubles;
+    table.GetByteArrayRegion = get_byte_region;
+    table.SetByteArrayRegion = set_byte_region;
+    table.SetLongArrayRegion = set_long_region;
     table.GetArrayLength = get_len;
     table.GetIntArrayElements = get_ints;
     table.GetLongArrayElements = get_longs;
@@ -86,5 +292,7 @@ int main(void) {
     expect("offsets not starting at 0", CALL(&ids, &bad0, &oi, NULL, &io, &ii, NULL, 0), TGO_E_INVALID, 0);
     expect("ids length disagrees with the offsets", CALL(&ids2, &oo, &oi, NULL, &io, &ii, NULL, 0), TGO_E_INVALID, 0);
     expect("empty offset array", CALL(&ids, &empty_off, &oi, NULL, &empty_off, &ii, NULL, 0), TGO_E_INVALID, 0);
+    partition_cases(env);
+    if (argc > 1 && strcmp(argv[1], "gpu") == 0) gpu_cases(env);
     return failures;
 }

@@ -75,6 +75,13 @@ def test_load_csr_validates_array_lengths_before_pinning(tmp_path):
     in_off[n] entries from them — short or null index / weight arrays must fail with
     TGO_E_INVALID before the C-ABI is reached (tests/jni_harness.c: a fake JNIEnv, the shim
     linked against the harness's recording tgo_load_csr and the real library for the rest)."""
+    exe = _build_harness(tmp_path)
+    run = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert run.returncode == 0, run.stdout + run.stderr
+    assert run.stdout.count("ok  ") == 25, run.stdout
+
+
+def _build_harness(tmp_path):
     lib = os.path.join(ROOT, "titan_amd")
     if not os.path.exists(os.path.join(lib, "libtitan_gpu_olap.so")):
         pytest.skip("libtitan_gpu_olap.so not built")
@@ -82,8 +89,20 @@ def test_load_csr_validates_array_lengths_before_pinning(tmp_path):
     r = subprocess.run(["gcc", "-std=c11", "-Wall", "-Wextra", "-Werror", "-Wno-unused-parameter",
                         "-I", os.path.join(ROOT, "tests", "jni_stub"), "-I", os.path.join(ROOT, "include"),
                         os.path.join(ROOT, "tests", "jni_harness.c"), SHIM, "-o", exe,
-                        "-L", lib, "-ltitan_gpu_olap", "-Wl,-rpath," + lib], capture_output=True, text=True)
+                        "-L", lib, "-ltitan_gpu_olap", "-Wl,-rpath," + lib, "-lm"], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
-    run = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    return exe
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(shutil.which("gcc") is None, reason="needs gcc")
+def test_java_multi_gpu_natives_world1(tmp_path):
+    """the Java multi-GPU path's natives (TgoNative.partLayout /
+    loadPartition / exchangeRcclId / exchangeRcclCreate / partSsspRun / partPageRankRun /
+    partBfsRun / partMsbfsRun / partMsLevels — what PartitionedRun calls per worker) run through
+    the JNI shim against the real library at world 1 over RCCL, and equal the one-GPU engine on
+    the same graph (SSSP and BFS bit-exact, PageRank in both exchange modes within 1e-12 L1)."""
+    exe = _build_harness(tmp_path)
+    run = subprocess.run([exe, "gpu"], capture_output=True, text=True, timeout=120)
     assert run.returncode == 0, run.stdout + run.stderr
-    assert run.stdout.count("ok  ") == 12, run.stdout
+    assert "FAIL" not in run.stdout and run.stdout.count("ok  ") == 25 + 12, run.stdout
