@@ -218,7 +218,9 @@ static void gpu_cases(JNIEnv* env) {
     ok = h != 0 && tgo_create(&o, &oneb) == TGO_OK && tgo_load_edges(oneb, &e, &lo) == TGO_OK &&
          JFN(loadPartition)(env, NULL, h, GN, 0, GN, ARR(&src), ARR(&dst), NULL, TGO_SCOPE_BOTH_E, 0, NULL) == TGO_OK;
     check("bothE partition + reference", ok);
+    id = JFN(exchangeRcclId)(env, NULL);                   /* one unique id per communicator */
     x = (ok && id) ? JFN(exchangeRcclCreate)(env, NULL, 1, 0, id, 0) : 0;
+    check("second exchange (a fresh id)", x != 0);
     if (ok && x) {
         static int64_t ref[GN];
         tgo_bfs_args ba;

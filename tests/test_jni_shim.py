@@ -105,4 +105,4 @@ def test_java_multi_gpu_natives_world1(tmp_path):
     exe = _build_harness(tmp_path)
     run = subprocess.run([exe, "gpu"], capture_output=True, text=True, timeout=120)
     assert run.returncode == 0, run.stdout + run.stderr
-    assert "FAIL" not in run.stdout and run.stdout.count("ok  ") == 25 + 12, run.stdout
+    assert "FAIL" not in run.stdout and run.stdout.count("ok  ") == 25 + 13, run.stdout
