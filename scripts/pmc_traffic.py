@@ -34,14 +34,14 @@ GROUPS = {
     "pagerank_update": ("cold_gather<", "cold_fold(", "gather_hot_pf<", "gather_hot_pf(", "gather_short_packed<",
                         "gather_chunks<tgo::(anonymous namespace)::PackedOp",
                         "finalize_long<tgo::(anonymous namespace)::PackedOp",
-                        "cold_fx(", "gather_hot_fx(", "finalize_long_fx("),
+                        "cold_fx<", "gather_hot_fx<", "finalize_long_fx("),
     # ms_pull is templated on its round-trip width (ms_pull<8>)
     "msbfs_sweep": ("ms_seed(", "ms_pull(", "ms_pull<", "ms_push(", "ms_settle(", "ms_queue(", "ms_fbitmap("),
     # one delta-stepping source of the device-driven loop (delta_loop.hip): every step's kernels
     "sssp_source": ("ds_loop_seed(", "ds_decide(", "ds_decide_bins(", "ds_extract_dev(", "ds_extract_bins(",
                     "ds_commit_dev<", "ds_relax_dev<", "ds_pull_heavy(", "ds_publish(", "ds_pull_flip("),
 }
-UNIT_KERNEL = {"pagerank_update": ("gather_hot_pf<", "gather_hot_pf(", "gather_short_packed<", "gather_hot_fx("),
+UNIT_KERNEL = {"pagerank_update": ("gather_hot_pf<", "gather_hot_pf(", "gather_short_packed<", "gather_hot_fx<"),
                "msbfs_sweep": ("ms_seed(",), "sssp_source": ("ds_loop_seed(",)}
 
 
