@@ -2258,6 +2258,54 @@ int tgo_part_bfs_claim(tgo_ctx* ctx, int32_t level, const uint64_t* recv, int32_
     return part_counts(ctx, counts);
 }
 
+}  // extern "C" (the fused level helpers below are C++, used by part_driver.cpp)
+namespace tgo {
+// tgo_part_bfs_run's top-down level, fused: the current queue (built from the frontier bitmap
+// when the last level was bottom-up), then ONE expansion that claims owned targets in place —
+// the one-GPU td_expand — and marks only remote ones in disc; nb_local is zeroed first.  With
+// world 1 nothing is remote, and the level needs no exchange and no claim pass over the whole
+// bitmap (the C-ABI's td / all-to-all / claim protocol makes two passes over every word).
+int part_bfs_td_fused(tgo_ctx* ctx, int32_t level, uint64_t* disc, uint64_t* nb_local) {
+    int rc = part_check(ctx);
+    if (rc) return rc;
+    DevGraph& g = ctx->g;
+    Scratch& s = ctx->sc;
+    hipStream_t st = ctx->stream;
+    const View push = push_view(g, TGO_SCOPE_BOTH_E);
+    int64_t qlen = 0;
+    if ((rc = part_qlen_now(ctx, qlen))) return rc;
+    if (qlen > 0 && !ctx->part_queued) {
+        HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
+        HIP_TRY(k_bfs_queue(push, g.n_active, ctx->part_frontier, s.q[ctx->part_cur], s.qdeg, s.cnt, st));
+        ctx->part_queued = true;
+    }
+    if (qlen > 0 && (rc = scan_frontier(ctx, qlen))) return rc;
+    HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
+    HIP_TRY(hipMemsetAsync(nb_local, 0, (g.n / 64) * 8, st));
+    const int nxt = ctx->part_cur ^ 1;
+    if (qlen > 0)
+        HIP_TRY(k_part_td_claim(push, s.q[ctx->part_cur], s.qpre, qlen, disc, s.vb, nb_local, s.level, s.q[nxt], s.qdeg,
+                                s.cnt, level + 1, g.lo, g.n, st));
+    ctx->part_cur = nxt;
+    ctx->part_queued = true;
+    return part_done(ctx);
+}
+// The remote discoveries (received slices) into the queue part_bfs_td_fused started.
+int part_bfs_claim_remote(tgo_ctx* ctx, int32_t level, const uint64_t* recv, int32_t nslices, uint64_t* nb_local) {
+    int rc = part_check(ctx);
+    if (rc) return rc;
+    DevGraph& g = ctx->g;
+    Scratch& s = ctx->sc;
+    const View push = push_view(g, TGO_SCOPE_BOTH_E);
+    HIP_TRY(k_part_claim(push, recv, nslices, g.n / 64, g.n, s.vb, nb_local, s.level, s.q[ctx->part_cur], s.qdeg, s.cnt,
+                         level + 1, ctx->stream, true));
+    return part_done(ctx);
+}
+// The level's counts (device counts when set, as tgo_part_bfs_claim).
+int part_bfs_level_done(tgo_ctx* ctx) { return part_counts(ctx, nullptr); }
+}  // namespace tgo
+extern "C" {
+
 int tgo_part_bfs_bu(tgo_ctx* ctx, int32_t level, const uint64_t* fb_global, uint64_t* nb_local, int64_t* counts) {
     int rc = part_check(ctx);
     if (rc) return rc;

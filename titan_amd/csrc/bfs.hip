@@ -268,8 +268,51 @@ __global__ void __launch_bounds__(kBlock) part_td_mark(View push, const int32_t*
     });
 }
 
+// Top-down on a partition with the owned targets claimed in place (tgo_part_bfs_run): an owned
+// neighbour joins the next frontier here, as in td_expand (visited bit, level, next-frontier bit,
+// queue slot); only remote neighbours are marked in the discovered bitmap for their owners'
+// part_claim<true>.  nb (the owned next-frontier slice) is zeroed by the caller.
+__global__ void __launch_bounds__(kBlock) part_td_claim(View push, const int32_t* __restrict__ q,
+        const int64_t* __restrict__ qpre, int64_t qlen, uint64_t* __restrict__ disc, uint64_t* __restrict__ vb,
+        uint64_t* __restrict__ nb, int32_t* __restrict__ level, int32_t* __restrict__ qn, int64_t* __restrict__ qdeg_n,
+        Counters* cnt, int32_t next_level, int64_t lo, int64_t n_local) {
+    __shared__ AppendLds sh;
+    unsigned long long mf = 0;
+    for_each_queue_edge(q, qpre, qlen, [&](bool valid, int32_t u, int64_t o) {
+        bool take = false;
+        int32_t vt = 0;
+        int64_t vdeg = 0;
+        if (valid) {
+            int32_t v, w;
+            entry_at(push, u, o, v, w);
+            const int64_t vl = static_cast<int64_t>(v) - lo;
+            if (vl >= 0 && vl < n_local) {
+                const uint64_t bit = 1ULL << (vl & 63);
+                if (!(vb[vl >> 6] & bit)) {
+                    const unsigned long long old = atomicOr(reinterpret_cast<unsigned long long*>(&vb[vl >> 6]), bit);
+                    if (!(old & bit)) {
+                        take = true;
+                        vt = static_cast<int32_t>(vl);
+                        level[vl] = next_level;
+                        atomicOr(reinterpret_cast<unsigned long long*>(&nb[vl >> 6]), bit);
+                        vdeg = push_degree(push, vt);
+                    }
+                }
+            } else {
+                const uint64_t bit = 1ULL << (v & 63);
+                if (!(disc[v >> 6] & bit)) atomicOr(reinterpret_cast<unsigned long long*>(&disc[v >> 6]), bit);
+            }
+        }
+        block_append(take, vt, vdeg, qn, qdeg_n, cnt, sh, mf);
+    });
+    block_flush(cnt, sh, mf);
+}
+
 // Owner side: OR the received slices, claim the unvisited bits (one wave per word; two-pass
-// chunked extraction, frontier.hpp).
+// chunked extraction, frontier.hpp).  kOr (after part_td_claim): nb already holds the owned
+// claims, so only words that take something are visited in pass 2 and OR-ed into nb;
+// otherwise nb is written for every word.
+template <bool kOr>
 __global__ void __launch_bounds__(kBlock) part_claim(View push, const uint64_t* __restrict__ recv,
         int nslices, int64_t words, int64_t n_local, uint64_t* __restrict__ vb, uint64_t* __restrict__ nb,
         int32_t* __restrict__ level, int32_t* __restrict__ qn, int64_t* __restrict__ qdeg_n, Counters* cnt,
@@ -284,13 +327,17 @@ __global__ void __launch_bounds__(kBlock) part_claim(View push, const uint64_t* 
         const unsigned long long tm = __ballot(take);
         if (commit) {
             if (lane() == 0) {
-                nb[wd] = tm;
+                if (kOr) {
+                    if (tm) nb[wd] |= tm;
+                } else {
+                    nb[wd] = tm;
+                }
                 if (tm) vb[wd] = vis | tm;
             }
             if (take) level[v] = next_level;
         }
         t[0] = {take, static_cast<int32_t>(v), take ? push_degree(push, v) : 0};
-        return true;                            // nb[wd] is written for every word
+        return kOr ? tm != 0 : true;            // (!kOr) nb[wd] is written for every word
     };
     chunk_extract<1>(words, probe, qn, qdeg_n, cnt);
 }
@@ -429,9 +476,20 @@ hipError_t k_part_td_mark(const View& push, const int32_t* q, const int64_t* qpr
 }
 hipError_t k_part_claim(const View& push, const uint64_t* recv, int nslices, int64_t words, int64_t n_local,
                         uint64_t* vb, uint64_t* nb, int32_t* level, int32_t* qn, int64_t* qdeg_n,
-                        Counters* cnt, int32_t next_level, hipStream_t s) {
-    part_claim<<<extract_grid(words), kBlock, 0, s>>>(push, recv, nslices, words, n_local, vb, nb, level, qn, qdeg_n, cnt,
-                                                       next_level);
+                        Counters* cnt, int32_t next_level, hipStream_t s, bool or_into_nb) {
+    if (or_into_nb)
+        part_claim<true><<<extract_grid(words), kBlock, 0, s>>>(push, recv, nslices, words, n_local, vb, nb, level, qn,
+                                                                qdeg_n, cnt, next_level);
+    else
+        part_claim<false><<<extract_grid(words), kBlock, 0, s>>>(push, recv, nslices, words, n_local, vb, nb, level, qn,
+                                                                 qdeg_n, cnt, next_level);
+    return hipGetLastError();
+}
+hipError_t k_part_td_claim(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen, uint64_t* disc,
+                           uint64_t* vb, uint64_t* nb, int32_t* level, int32_t* qn, int64_t* qdeg_n, Counters* cnt,
+                           int32_t next_level, int64_t lo, int64_t n_local, hipStream_t s) {
+    part_td_claim<<<256 * 8, kBlock, 0, s>>>(push, q, qpre, qlen, disc, vb, nb, level, qn, qdeg_n, cnt, next_level, lo,
+                                             n_local);
     return hipGetLastError();
 }
 hipError_t k_unpermute_i64(const int64_t* in, const int32_t* perm, int64_t* out, int64_t n, hipStream_t s) {

@@ -741,7 +741,15 @@ hipError_t k_part_td_mark(const View& push, const int32_t* q, const int64_t* qpr
                           uint64_t* disc, const uint64_t* vb_local, int64_t lo, int64_t n_local, hipStream_t s);
 hipError_t k_part_claim(const View& push, const uint64_t* recv, int nslices, int64_t words, int64_t n_local,
                         uint64_t* vb, uint64_t* nb, int32_t* level, int32_t* qn, int64_t* qdeg_n,
-                        Counters* cnt, int32_t next_level, hipStream_t s);
+                        Counters* cnt, int32_t next_level, hipStream_t s, bool or_into_nb = false);
+hipError_t k_part_td_claim(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen, uint64_t* disc,
+                           uint64_t* vb, uint64_t* nb, int32_t* level, int32_t* qn, int64_t* qdeg_n, Counters* cnt,
+                           int32_t next_level, int64_t lo, int64_t n_local, hipStream_t s);
+// tgo_part_bfs_run's top-down level (api.cpp): owned targets claimed during the expansion, remote
+// ones marked in disc (world > 1) and claimed from the received slices into the same queue.
+int part_bfs_td_fused(tgo_ctx* ctx, int32_t level, uint64_t* disc, uint64_t* nb_local);
+int part_bfs_claim_remote(tgo_ctx* ctx, int32_t level, const uint64_t* recv, int32_t nslices, uint64_t* nb_local);
+int part_bfs_level_done(tgo_ctx* ctx);
 hipError_t k_unpermute_i32(const int32_t* in, const int32_t* perm, int32_t* out, int64_t n, hipStream_t s);
 
 // PageRank gather diagnostics: [diag_lo, diag_hi) = only sources in this range are gathered

@@ -743,14 +743,13 @@ extern "C" int tgo_part_bfs_run(tgo_ctx* ctx, tgo_exchange* x, int64_t seed_glob
         return rc;
     int64_t* const caller_dc = part_dcounts_of(ctx);
     uint64_t* glob[2] = {f0, f1};
-    int64_t tot = 0;
-    if ((rc = d.reduce(&ent, 1, tgo_exchange::kRedSum, &tot))) return rc;
     int64_t c[2] = {0, 0};
     if ((rc = tgo_part_bfs_begin(ctx, seed_global, glob[0] + x->rank * nwl, c))) return rc;
     if (int r = x->all_gather(glob[0], static_cast<size_t>(nwl) * 8, st)) return d.xfail(r);
-    int64_t g[2] = {0, 0};
-    if ((rc = d.reduce(c, 2, tgo_exchange::kRedSum, g))) return rc;
-    int64_t nf = g[0], mf = g[1], mu = tot - mf;
+    // the seed level's counts and the graph's total entries in one reduction (one host round trip)
+    int64_t v3[3] = {c[0], c[1], ent}, g[3] = {0, 0, 0};
+    if ((rc = d.reduce(v3, 3, tgo_exchange::kRedSum, g))) return rc;
+    int64_t nf = g[0], mf = g[1], mu = g[2] - mf;
     if ((rc = tgo_part_device_counts(ctx, dc))) return rc;
     bool bottom_up = false;
     int levels = 0;
@@ -763,10 +762,15 @@ extern "C" int tgo_part_bfs_run(tgo_ctx* ctx, tgo_exchange* x, int64_t seed_glob
         if (bottom_up) {
             if ((rc = tgo_part_bfs_bu(ctx, level, glob[0], nb, nullptr))) break;
         } else {
-            if (hipMemsetAsync(disc, 0, nwg * 8, st) != hipSuccess) { rc = d.hip("disc clear"); break; }
-            if ((rc = tgo_part_bfs_td(ctx, level, disc))) break;
-            if (int r = x->all_to_all(disc, recv, static_cast<size_t>(nwl) * 8, st)) { rc = d.xfail(r); break; }
-            if ((rc = tgo_part_bfs_claim(ctx, level, recv, W, nb, nullptr))) break;
+            // owned targets claimed during the expansion (tgo::part_bfs_td_fused); the remote
+            // ones travel as discovered-bitmap slices and are claimed by their owners
+            if (W > 1 && hipMemsetAsync(disc, 0, nwg * 8, st) != hipSuccess) { rc = d.hip("disc clear"); break; }
+            if ((rc = tgo::part_bfs_td_fused(ctx, level, disc, nb))) break;
+            if (W > 1) {
+                if (int r = x->all_to_all(disc, recv, static_cast<size_t>(nwl) * 8, st)) { rc = d.xfail(r); break; }
+                if ((rc = tgo::part_bfs_claim_remote(ctx, level, recv, W, nb))) break;
+            }
+            if ((rc = tgo::part_bfs_level_done(ctx))) break;
         }
         if (int r = x->all_gather(glob[1], static_cast<size_t>(nwl) * 8, st)) { rc = d.xfail(r); break; }
         std::swap(glob[0], glob[1]);
@@ -783,7 +787,8 @@ extern "C" int tgo_part_bfs_run(tgo_ctx* ctx, tgo_exchange* x, int64_t seed_glob
     if (rc) { x->abort(); return rc; }
     if (rc_off) return rc_off;
     int64_t rl[2] = {0, 0};
-    if ((rc = tgo_part_bfs_end(ctx, dist_local, rl))) return rc;
+    // the reach statistics (a pass over every list) only when asked for
+    if ((rc = tgo_part_bfs_end(ctx, dist_local, reached ? rl : nullptr))) return rc;
     if (reached && (rc = d.reduce(rl, 2, tgo_exchange::kRedSum, reached))) return rc;
     if (levels_out) *levels_out = levels;
     return TGO_OK;
