@@ -21,7 +21,7 @@ src, dst, _ = rmat_edges(scale, 16, seed=0x54495441)
 eng = None
 loaded_with = None
 KEYS = ("TGO_PR_BLOCKED", "TGO_PR_HOT", "TGO_PR_SEG", "TGO_PR_DIAG", "TGO_PR_PACK", "TGO_PR_CPACK", "TGO_PR_HOT_TILE", "TGO_PR_HOT_PIPE",
-        "TGO_PR_FX", "TGO_PR_FX_E", "TGO_PR_FX_COLD", "TGO_PR_FX_CE", "TGO_PR_FX_CP", "TGO_PR_FX_DIAG")
+        "TGO_PR_FX", "TGO_PR_FX_E", "TGO_PR_FX_COLD", "TGO_PR_FX_CE", "TGO_PR_FX_CP", "TGO_PR_FX_DIAG", "TGO_PR_FX_FOLD")
 variants = [
     {},
     {"TGO_PR_BLOCKED": "0"},

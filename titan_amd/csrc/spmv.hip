@@ -574,13 +574,32 @@ __device__ __forceinline__ void fx_total(const unsigned long long* s_lo, const u
     }
 }
 
+// The cold sum of row r at emission (TGO_PR_FX_FOLD): its pieces added in segment order, as
+// cold_fold adds them — the same association, so the ranks are bitwise those of the separate
+// fold — read here instead of from csum, so the fold kernel and csum's write + read go away.
+struct FoldSrc {
+    const uint32_t* cptr = nullptr;      // null: csum holds the cold sums (cold_fold ran)
+    const int32_t* cpid = nullptr;
+    const double* partial = nullptr;
+    __device__ __forceinline__ double cold(int64_t r) const {
+        double c = 0.0;
+        const uint32_t e = cptr[r + 1];
+        for (uint32_t k = cptr[r]; k < e; ++k) c += partial[cpid[k]];
+        return c;
+    }
+};
+__device__ __forceinline__ void fx_emit(const PrColdFinal& fin, const FoldSrc& fold, int64_t r, double hot) {
+    if (fold.cptr) fin.f(r, hot + fold.cold(r));
+    else fin(r, hot);
+}
+
 // One super-tile per workgroup: desc {first entry, end entry, first row, rows | -(long + 1)}.
 // Each row has 2^lc copies of its accumulator (rows * copies <= kFxSlots), the copy chosen by
 // the lane, so a tile of few rows does not serialise its lanes on one LDS address.
 template <int diag>
 __global__ void __launch_bounds__(kFxThreads) gather_hot_fx(const uint32_t* __restrict__ padj,
         const int64_t* __restrict__ desc, int rbits, const double* __restrict__ msg, PrColdFinal fin,
-        unsigned long long* __restrict__ long_acc) {
+        unsigned long long* __restrict__ long_acc, FoldSrc fold) {
     __shared__ unsigned long long s_lo[kFxSlots], s_hi[kFxSlots];
     const int64_t t = blockIdx.x;
     const int64_t e0 = desc[4 * t], e1 = desc[4 * t + 1], r0 = desc[4 * t + 2], nr = desc[4 * t + 3];
@@ -595,7 +614,7 @@ __global__ void __launch_bounds__(kFxThreads) gather_hot_fx(const uint32_t* __re
         for (int i = threadIdx.x; i < rows; i += kFxThreads) {
             unsigned long long lo, hi;
             fx_total(s_lo, s_hi, i, lc, lo, hi);
-            fin(r0 + i, fx_to_double(lo, hi));            // + the row's cold sum, then the update
+            fx_emit(fin, fold, r0 + i, fx_to_double(lo, hi));   // + the row's cold sum, then the update
         }
     } else if (threadIdx.x == 0) {                        // a long row's chunk: into the row's accumulator
         unsigned long long lo = 0, hi = 0;
@@ -642,12 +661,12 @@ __global__ void __launch_bounds__(kFxThreads) cold_fx(const uint32_t* __restrict
 
 // The long rows after every chunk has landed: the update, and the accumulator back to zero.
 __global__ void finalize_long_fx(const int32_t* __restrict__ long_row, int64_t nlong,
-                                 unsigned long long* __restrict__ long_acc, PrColdFinal fin) {
+                                 unsigned long long* __restrict__ long_acc, PrColdFinal fin, FoldSrc fold) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nlong; i += (int64_t)gridDim.x * blockDim.x) {
         const unsigned long long lo = long_acc[2 * i], hi = long_acc[2 * i + 1];
         long_acc[2 * i] = 0;
         long_acc[2 * i + 1] = 0;
-        fin(long_row[i], fx_to_double(lo, hi));
+        fx_emit(fin, fold, long_row[i], fx_to_double(lo, hi));
     }
 }
 
@@ -935,6 +954,10 @@ hipError_t k_pr_iter(const DevCsr& in, const RowBlocks& rb, const double* contri
 }
 // Cold phase: the cold segments' partial sums, folded per row into csum (reads only the cold
 // sources [hot, n_src) of `contrib`).
+static bool fx_fold_in_hot() {                       // TGO_PR_FX_FOLD (read per launch, A/B)
+    const char* e = std::getenv("TGO_PR_FX_FOLD");
+    return e ? std::atoi(e) != 0 : true;
+}
 static int fx_diag() {                                // read per launch: an A/B flips it between runs
     const char* e = std::getenv("TGO_PR_FX_DIAG");
     return e ? std::atoi(e) : 0;
@@ -994,7 +1017,9 @@ hipError_t k_pr_cold_phase(const ColdBlocks& cb, const double* contrib, hipStrea
     }
     int64_t g = (cb.n_crows + kBlock - 1) / kBlock;
     g = std::max<int64_t>(1, std::min<int64_t>(g, 65536));
-    cold_fold<<<static_cast<unsigned>(g), kBlock, 0, s>>>(cb.crow, cb.n_crows, cb.cptr, cb.cpid, cb.partial, cb.csum, window);
+    if (!(cb.fx && fx_fold_in_hot() && !window))
+        cold_fold<<<static_cast<unsigned>(g), kBlock, 0, s>>>(cb.crow, cb.n_crows, cb.cptr, cb.cpid, cb.partial, cb.csum,
+                                                              window);
     return hipGetLastError();
 }
 
@@ -1003,19 +1028,22 @@ hipError_t k_pr_hot_phase(const ColdBlocks& cb, const double* contrib, const dou
                           double* contrib_next, double* partial_long, double alpha, double base, hipStream_t s) {
     const PrColdFinal fin{PrFinal{edge_count, pr, contrib_next, alpha, base}, cb.csum};
     if (cb.fx) {
+        FoldSrc fold;
+        if (fx_fold_in_hot() && cb.win == 0) { fold.cptr = cb.cptr; fold.cpid = cb.cpid; fold.partial = cb.partial; }
         if (cb.fx_ntiles > 0) {
             const unsigned g = static_cast<unsigned>(cb.fx_ntiles);
             const uint32_t* padj = reinterpret_cast<const uint32_t*>(cb.hcsr.adj);
             const int d = fx_diag();
             if (d == 1)
-                gather_hot_fx<1><<<g, kFxThreads, 0, s>>>(padj, cb.fx_desc, cb.fx_rbits, contrib, fin, cb.fx_long_acc);
+                gather_hot_fx<1><<<g, kFxThreads, 0, s>>>(padj, cb.fx_desc, cb.fx_rbits, contrib, fin, cb.fx_long_acc, fold);
             else if (d == 2)
-                gather_hot_fx<2><<<g, kFxThreads, 0, s>>>(padj, cb.fx_desc, cb.fx_rbits, contrib, fin, cb.fx_long_acc);
+                gather_hot_fx<2><<<g, kFxThreads, 0, s>>>(padj, cb.fx_desc, cb.fx_rbits, contrib, fin, cb.fx_long_acc, fold);
             else
-                gather_hot_fx<0><<<g, kFxThreads, 0, s>>>(padj, cb.fx_desc, cb.fx_rbits, contrib, fin, cb.fx_long_acc);
+                gather_hot_fx<0><<<g, kFxThreads, 0, s>>>(padj, cb.fx_desc, cb.fx_rbits, contrib, fin, cb.fx_long_acc, fold);
         }
         if (cb.fx_nlong > 0)
-            finalize_long_fx<<<grid_for(cb.fx_nlong), kBlock, 0, s>>>(cb.fx_long_row, cb.fx_nlong, cb.fx_long_acc, fin);
+            finalize_long_fx<<<grid_for(cb.fx_nlong), kBlock, 0, s>>>(cb.fx_long_row, cb.fx_nlong, cb.fx_long_acc, fin,
+                                                                      fold);
         return hipGetLastError();
     }
     if (!cb.packed) return run_gather(cb.hcsr, cb.rb_hot, PrOp{contrib}, fin, partial_long, s);
