@@ -22,6 +22,8 @@
 // The converged distances are unique (ShortestDistanceVertexProgram.java:96-130 is a
 // Jacobi Bellman-Ford with a min combiner), so this order of the same relaxations reaches
 // the same bit-exact result as the host loop and the oracle.
+#include <algorithm>
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 #include "frontier.hpp"
 
@@ -737,6 +739,11 @@ __global__ void ds_pull_flip(DsLoop* L) {
 
 }  // namespace
 
+static long long env_i64_dl(const char* name, long long dflt) {
+    const char* e = std::getenv(name);
+    return e ? std::atoll(e) : dflt;
+}
+
 hipError_t k_ds_loop_seed(const DevCsr& ws, const int64_t* light, int64_t* dist, int32_t* q, int64_t* qpre, DsLoop* L,
                           int64_t seed, int64_t delta, hipStream_t s) {
     ds_loop_seed<<<1, 64, 0, s>>>(ws.off, light, dist, q, qpre, L, seed, delta);
@@ -773,15 +780,21 @@ hipError_t k_ds_loop_step_bins(const DevCsr& ws, const int64_t* light, uint64_t*
     if (pulls && pull.n_active > n) return hipErrorInvalidValue;
     ds_decide_bins<<<1, 64, 0, s>>>(L, cur, delta, nbins, cap, scan_above, pulls ? pull.min_members : 0);
     const int64_t words = (n + 63) / 64;
-    ds_extract_bins<<<extract_grid(words), kBlock, 0, s>>>(ws.off, light, pend, member, dist, L, cur, pile, cap, mlist,
+    // grids (TGO_DS_XGRID / _CGRID / _RGRID, A/B): most of a run's ~100 steps have tiny queues
+    // and no extraction, and a launch of thousands of blocks that exit at once still costs
+    // ~10-15 us; the grid-stride loops take any grid
+    static const int xg = static_cast<int>(env_i64_dl("TGO_DS_XGRID", 0));
+    static const int cg = static_cast<int>(env_i64_dl("TGO_DS_CGRID", 1024));
+    static const int rg = static_cast<int>(env_i64_dl("TGO_DS_RGRID", 256 * 8));
+    ds_extract_bins<<<xg > 0 ? std::min(xg, extract_grid(words)) : extract_grid(words), kBlock, 0, s>>>(ws.off, light, pend, member, dist, L, cur, pile, cap, mlist,
                                                            done, q[cur], qpre[cur], n, pull);
-    ds_commit_dev<true><<<1024, kBlock, 0, s>>>(q[cur], dist, msg, pend, member, L, cur, mlist);
+    ds_commit_dev<true><<<cg, kBlock, 0, s>>>(q[cur], dist, msg, pend, member, L, cur, mlist);
     if (pulls) {
         ds_pull_heavy<<<256 * 8, kBlock, 0, s>>>(ws.off, light, msg, dist, pend, q[cur ^ 1], qpre[cur ^ 1], L, cur, delta,
                                                  nbins, pile, cap, pull);
         ds_pull_flip<<<1, 64, 0, s>>>(L);
     }
-    ds_relax_dev<true><<<256 * 8, kBlock, 0, s>>>(ws.off, ws.adj, ws.w, light, q[cur], qpre[cur], msg, dist, pend,
+    ds_relax_dev<true><<<rg, kBlock, 0, s>>>(ws.off, ws.adj, ws.w, light, q[cur], qpre[cur], msg, dist, pend,
                                                   q[cur ^ 1], qpre[cur ^ 1], L, cur, delta, nbins, pile, cap,
                                                   done_filter ? done : nullptr);
     return hipGetLastError();
