@@ -62,6 +62,8 @@ struct tgo_ctx {
     int64_t part_pr_hot = 0, part_pr_span = 0;
     int64_t part_relaxed = 0;   // partitioned SSSP: entries relaxed, phases
     int32_t part_phases = 0;
+    int64_t part_seed = -1;     // partitioned SSSP: the seed's internal id when owned here
+    bool part_split = false;    // partitioned SSSP run on the light/heavy split (part_sssp_split)
     int64_t pv_max_out = 0, pv_max_in = 0;   // largest OUT / IN list of a vertex cut
     std::vector<int64_t> pv_rows;            // row ids of the vertex cuts
     // last finished program whose compute keys tgo_result_rows can encode (-1 = none)
@@ -2941,9 +2943,11 @@ static int ds_part_alloc(tgo_ctx* ctx) {
     if (s.ds_rbest) return TGO_OK;
     HIP_TRY(dev_alloc(ctx, s.ds_rbest, ctx->g.n_global));
     HIP_TRY(dev_alloc(ctx, s.ds_rmark, ctx->g.n_global / 64 + 1));
-    HIP_TRY(dev_alloc(ctx, s.ds_pack, 3 * kMaxRanks));
+    HIP_TRY(dev_alloc(ctx, s.ds_pack, 3 * kMaxRanks + 2));
     return TGO_OK;
 }
+// the loop state words after the pack counters (delta.hip ds_track_reset)
+static long long* ds_track(Scratch& s) { return reinterpret_cast<long long*>(s.ds_pack + 3 * kMaxRanks); }
 
 int tgo_part_sssp_begin(tgo_ctx* ctx, int64_t seed_global, int64_t delta, int64_t* out) {
     int rc = part_check(ctx);
@@ -2960,16 +2964,21 @@ int tgo_part_sssp_begin(tgo_ctx* ctx, int64_t seed_global, int64_t delta, int64_
     HIP_TRY(hipMemsetAsync(s.vb, 0, ((n + 63) / 64 + 1) * 8, st));
     HIP_TRY(k_fill_i64(s.ds_rbest, INT64_MAX, g.n_global, st));
     HIP_TRY(hipMemsetAsync(s.ds_rmark, 0, (g.n_global / 64 + 1) * 8, st));
+    HIP_TRY(hipMemsetAsync(s.ds_pack, 0, 3 * kMaxRanks * sizeof(unsigned long long), st));
+    HIP_TRY(k_ds_track_reset(ds_track(s), st));
     ctx->part_cur = 0;
     ctx->part_qlen = 0;
     ctx->part_qlen_stale = false;
     ctx->part_relaxed = 0;
     ctx->part_phases = 0;
+    ctx->part_seed = -1;
+    ctx->part_split = false;
     int64_t seed = seed_global - g.lo;
     if (seed >= 0 && seed < n) {
         seed = ctx->perm[seed];
         HIP_TRY(k_ds_seed(push, s.dist, s.q[0], s.qdeg, seed, st));
         ctx->part_qlen = 1;
+        ctx->part_seed = seed;
     }
     HIP_TRY(hipStreamSynchronize(st));
     if (out) {
@@ -2979,30 +2988,52 @@ int tgo_part_sssp_begin(tgo_ctx* ctx, int64_t seed_global, int64_t delta, int64_
     return TGO_OK;
 }
 
-int tgo_part_sssp_relax(tgo_ctx* ctx, int64_t thr, int32_t nranks, int64_t* send, int64_t* send_counts) {
+// The relax half of a phase.  send_counts (host) set: the pair counts come back to the host
+// (one stream synchronisation); sizes (device) set instead: the exchange header is written on
+// the device (ds_mark_sizes) and nothing waits.
+static int part_sssp_relax_impl(tgo_ctx* ctx, int64_t thr, int32_t nranks, int64_t* send, int64_t* send_counts,
+                                int64_t* sizes) {
     int rc = part_check(ctx);
     if (rc) return rc;
     DevGraph& g = ctx->g;
     Scratch& s = ctx->sc;
     if (!s.ds_rbest) return fail(ctx, TGO_E_STATE, "tgo_part_sssp_begin has not run");
-    if (nranks < 1 || nranks > kMaxRanks || g.n * nranks != g.n_global || !send || !send_counts)
+    if (nranks < 1 || nranks > kMaxRanks || g.n * nranks != g.n_global || !send || (!send_counts && !sizes))
         return fail(ctx, TGO_E_INVALID, "nranks * n_local must equal n_global (equal partitions, <= 64 ranks)");
     hipStream_t st = ctx->stream;
     const View push = push_view(g, g.scope);
-    HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
     const int cur = ctx->part_cur;
-    if (ctx->part_qlen > 0) {
+    if (ctx->part_split && ctx->part_qlen > 0) {      // commit_ws zeroes the counters and the scan's tail
+        const int64_t ql = ctx->part_qlen;
+        HIP_TRY(k_ds_commit_ws(s.q[cur], ql, s.dist, s.msg, s.vb, s.ds_member, s.qdeg, s.cnt, st, ds_track(s)));
+        HIP_TRY(scan_exclusive_i64(s.cub_tmp, s.cub_bytes, s.qdeg, s.qpre, ql + 1, st));
+        HIP_TRY(k_ds_relax_ws_part(s.ds_pws, s.ds_light, s.q[cur], s.qpre, ql, s.msg, s.dist, s.vb, s.q[cur ^ 1], s.qdeg,
+                                   s.cnt, thr, g.lo, g.n, s.ds_rbest, s.ds_rmark, ds_track(s), st));
+    } else {
+        HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
+    }
+    if (!ctx->part_split && ctx->part_qlen > 0) {
         HIP_TRY(k_ds_commit(s.q[cur], ctx->part_qlen, s.dist, s.msg, s.vb, st));
         if ((rc = scan_frontier(ctx, ctx->part_qlen))) return rc;
         HIP_TRY(k_ds_relax_part(push, s.q[cur], s.qpre, ctx->part_qlen, s.msg, s.dist, s.vb, s.q[cur ^ 1], s.qdeg,
-                                s.cnt, g.has_weight ? 1 : 0, thr, g.lo, g.n, s.ds_rbest, s.ds_rmark, st));
+                                s.cnt, g.has_weight ? 1 : 0, thr, g.lo, g.n, s.ds_rbest, s.ds_rmark, ds_track(s), st));
     }
     unsigned long long* counts = s.ds_pack;
     unsigned long long* offs = counts + kMaxRanks;
     unsigned long long* cursor = offs + kMaxRanks;
-    HIP_TRY(hipMemsetAsync(counts, 0, 3 * kMaxRanks * sizeof(unsigned long long), st));
+    // device header: the counts / cursors are zero here (begin, then every ds_mark_sizes)
+    if (send_counts) HIP_TRY(hipMemsetAsync(counts, 0, 3 * kMaxRanks * sizeof(unsigned long long), st));
     const int64_t words = g.n_global / 64, wpr = g.n / 64;
+    if (!send_counts && nranks == 1) {      // one rank owns every target: nothing is ever marked
+        HIP_TRY(k_ds_mark_sizes(counts, nranks, ctx->part_qlen, offs, cursor, ds_track(s), sizes, st));
+        return part_done(ctx);
+    }
     HIP_TRY(k_ds_mark_count(s.ds_rmark, words, wpr, counts, st));
+    if (!send_counts) {
+        HIP_TRY(k_ds_mark_sizes(counts, nranks, ctx->part_qlen, offs, cursor, ds_track(s), sizes, st));
+        HIP_TRY(k_ds_mark_pack(s.ds_rmark, words, wpr, g.n, s.ds_rbest, offs, cursor, send, st));
+        return part_done(ctx);
+    }
     unsigned long long h[kMaxRanks], ho[kMaxRanks];
     HIP_TRY(hipMemcpyAsync(h, counts, nranks * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
@@ -3017,6 +3048,11 @@ int tgo_part_sssp_relax(tgo_ctx* ctx, int64_t thr, int32_t nranks, int64_t* send
     return part_done(ctx);          // the caller's exchange follows on the same stream
 }
 
+int tgo_part_sssp_relax(tgo_ctx* ctx, int64_t thr, int32_t nranks, int64_t* send, int64_t* send_counts) {
+    if (ctx && !send_counts) return fail(ctx, TGO_E_INVALID, "null send_counts");
+    return part_sssp_relax_impl(ctx, thr, nranks, send, send_counts, nullptr);
+}
+
 int tgo_part_sssp_apply(tgo_ctx* ctx, int64_t thr, const int64_t* recv, int64_t npairs, int64_t* counts) {
     int rc = part_check(ctx);
     if (rc) return rc;
@@ -3027,7 +3063,8 @@ int tgo_part_sssp_apply(tgo_ctx* ctx, int64_t thr, const int64_t* recv, int64_t 
     hipStream_t st = ctx->stream;
     if (npairs > 0)
         HIP_TRY(k_ds_apply(push_view(g, g.scope), recv, npairs, s.dist, s.vb, s.q[ctx->part_cur ^ 1], s.qdeg, s.cnt,
-                           thr, st));
+                           thr, ctx->part_split ? s.ds_pws.off : nullptr, ctx->part_split ? s.ds_light : nullptr,
+                           ds_track(s), st));
     if ((rc = read_counters(ctx))) return rc;
     if (s.hcnt->err) return fail(ctx, TGO_E_PROGRAM,
         "vertex program failed: a traversed edge has no value for the weight property");
@@ -3065,7 +3102,14 @@ int tgo_part_sssp_extract(tgo_ctx* ctx, int64_t thr, int64_t* counts) {
     Scratch& s = ctx->sc;
     hipStream_t st = ctx->stream;
     HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
-    HIP_TRY(k_ds_extract(push_view(g, g.scope), s.vb, g.n, s.dist, thr, s.q[ctx->part_cur], s.qdeg, s.cnt, st));
+    if (!s.ds_rbest) return fail(ctx, TGO_E_STATE, "tgo_part_sssp_begin has not run");
+    HIP_TRY(k_ds_track_reset(ds_track(s), st));     // the extraction sets the pending minimum afresh
+    if (ctx->part_split)            // the new near queue (light) and the settled members' heavy entries
+        HIP_TRY(k_ds_extract_ws(s.ds_pws, s.ds_light, s.vb, s.ds_member, g.n, s.dist, thr, s.q[ctx->part_cur], s.qdeg,
+                                s.cnt, st, ds_track(s)));
+    else
+        HIP_TRY(k_ds_extract(push_view(g, g.scope), s.vb, g.n, s.dist, thr, s.q[ctx->part_cur], s.qdeg, s.cnt, st,
+                             ds_track(s)));
     return part_counts(ctx, counts, false);   // the SSSP driver reads counts on the host
 }
 
@@ -3301,6 +3345,55 @@ namespace tgo {
 hipStream_t part_stream(tgo_ctx* ctx) { return ctx->stream; }
 int part_fail(tgo_ctx* ctx, int code, const std::string& msg) { return fail(ctx, code, msg); }
 int64_t* part_dcounts_of(tgo_ctx* ctx) { return ctx->part_dcounts; }
+// tgo_part_sssp_relax with the exchange header (sizes, 2 * nranks words) written on the device
+int part_sssp_relax_dev(tgo_ctx* ctx, int64_t thr, int32_t nranks, int64_t* send, int64_t* sizes) {
+    if (!sizes) return fail(ctx, TGO_E_INVALID, "null sizes");
+    return part_sssp_relax_impl(ctx, thr, nranks, send, nullptr, sizes);
+}
+// The header fold after the driver's header all-to-all (delta.hip ds_header_fold).
+int part_sssp_header_fold(tgo_ctx* ctx, const int64_t* own, const int64_t* recv, int nranks, int64_t* out) {
+    HIP_TRY(k_ds_header_fold(own, recv, nranks, out, ctx->stream));
+    return TGO_OK;
+}
+// Switch the run tgo_part_sssp_begin started onto the light/heavy split at bucket width delta
+// (weighted loads; TGO_DS_SPLIT=0 keeps the plain form): the push view is split on the device
+// (once per width), and the seed re-queued with its light degree.  Returns whether it did.
+int part_sssp_split(tgo_ctx* ctx, int64_t delta, bool* on) {
+    int rc = part_check(ctx);
+    if (rc) return rc;
+    DevGraph& g = ctx->g;
+    Scratch& s = ctx->sc;
+    *on = false;
+    static const bool enabled = env_i64("TGO_DS_SPLIT", 1) != 0;
+    if (!enabled || !g.has_weight || delta <= 0 || !s.ds_rbest) return TGO_OK;
+    hipStream_t st = ctx->stream;
+    const View push = push_view(g, g.scope);
+    const int64_t n = g.n, words = (n + 63) / 64 + 1;
+    if (!s.ds_light) {
+        HIP_TRY(dev_alloc(ctx, s.ds_light, n + 1));
+        HIP_TRY(dev_alloc(ctx, s.ds_member, words));
+    }
+    if (!s.ds_pws.off) {
+        const int64_t nnz = (g.has_transpose ? g.push_t.nnz
+                             : g.scope == TGO_SCOPE_IN_E ? g.in.nnz
+                             : g.scope == TGO_SCOPE_OUT_E ? g.out.nnz : g.in.nnz + g.out.nnz);
+        HIP_TRY(dev_alloc(ctx, s.ds_pws.off, n + 1));
+        HIP_TRY(dev_alloc(ctx, s.ds_pws.adj, std::max<int64_t>(nnz, 1)));
+        HIP_TRY(dev_alloc(ctx, s.ds_pws.w, std::max<int64_t>(nnz, 1)));
+        s.ds_pws.nnz = nnz;
+        s.ds_light_delta = -1;
+        ctx->st.device_bytes = ctx->dev_bytes;
+    }
+    if (s.ds_light_delta != delta) {
+        HIP_TRY(k_ds_split_rows(push, n, delta, s.ds_pws, s.ds_light, st));
+        s.ds_light_delta = delta;
+    }
+    HIP_TRY(hipMemsetAsync(s.ds_member, 0, words * 8, st));
+    if (ctx->part_seed >= 0) HIP_TRY(k_ds_seed_ws(s.ds_pws, s.ds_light, s.dist, s.q[0], s.qdeg, ctx->part_seed, st));
+    ctx->part_split = true;
+    *on = true;
+    return part_done(ctx);
+}
 // `count` device words (on the ctx stream, after the work queued so far) to out, through the
 // host-mapped counter page: one tiny kernel and a spin instead of a copy and a stream wait.
 int part_read_words(tgo_ctx* ctx, const int64_t* dev, int count, int64_t* out) {

@@ -29,20 +29,44 @@
 // id, distance) pairs, the caller's all-to-all moves them, and the owner mins them into its
 // dist with the same pending / near-queue rule (ds_apply).  rbest lives for the whole run:
 // a target is re-sent only when this rank improves on what it sent before.
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 #include "frontier.hpp"
 
 namespace tgo {
 namespace {
 
-// min(cand) into dist[v] of an owned vertex; true when v has to join the near queue.
-__device__ __forceinline__ bool relax_owned(int64_t* dist, uint64_t* pend, int64_t v, int64_t cand, int64_t thr) {
+constexpr long long kInfLL = 0x7FFFFFFFFFFFFFFFLL;
+
+// min(cand) into dist[v] of an owned vertex; true when v has to join the near queue.  An
+// improvement that leaves v pending outside the queue folds cand into tmin (the partitioned
+// loop's running pending minimum, see ds_track_reset).
+__device__ __forceinline__ bool relax_owned(int64_t* dist, uint64_t* pend, int64_t v, int64_t cand, int64_t thr,
+                                            long long& tmin) {
     if (cand >= dist[v]) return false;                  // a stale (larger) read only costs an atomic
     const long long old = atomicMin(reinterpret_cast<long long*>(&dist[v]), static_cast<long long>(cand));
     if (cand >= old) return false;
     const uint64_t bit = 1ULL << (v & 63);
     const unsigned long long ob = atomicOr(reinterpret_cast<unsigned long long*>(&pend[v >> 6]), bit);
-    return !(ob & bit) && cand < thr;
+    const bool take = !(ob & bit) && cand < thr;
+    if (!take && cand < tmin) tmin = cand;
+    return take;
+}
+
+// Block minimum of x into *dst, one atomicMin per block (every thread of the block calls it).
+__device__ __forceinline__ void block_fold_min(long long x, long long* dst) {
+    __shared__ long long s_m[kWavesPerBlock];
+    for (int o = 32; o > 0; o >>= 1) {
+        const long long y = __shfl_xor(x, o, 64);
+        x = y < x ? y : x;
+    }
+    __syncthreads();
+    if (lane() == 0) s_m[threadIdx.x >> 6] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kWavesPerBlock; ++w) x = s_m[w] < x ? s_m[w] : x;
+        if (x != kInfLL) atomicMin(dst, x);
+    }
 }
 
 __global__ void ds_seed(View push, int64_t* dist, int32_t* q, int64_t* qdeg, int64_t seed) {
@@ -72,9 +96,10 @@ __global__ void __launch_bounds__(kBlock) ds_relax(View push, const int32_t* __r
         const int64_t* __restrict__ qpre, int64_t qlen, const int64_t* __restrict__ msg,
         int64_t* __restrict__ dist, uint64_t* __restrict__ pend, int32_t* __restrict__ qn,
         int64_t* __restrict__ qdeg_n, Counters* cnt, int weighted, int64_t thr, int64_t lo, int64_t n_local,
-        int64_t* __restrict__ rbest, uint64_t* __restrict__ rmark) {
+        int64_t* __restrict__ rbest, uint64_t* __restrict__ rmark, long long* __restrict__ track) {
     __shared__ AppendLds sh;
     unsigned long long mf = 0;
+    long long tmin = kInfLL;
     if (blockIdx.x == 0 && threadIdx.x == 0) cnt->red[1] = static_cast<unsigned long long>(qpre[qlen]);   // work done
     for_each_queue_edge(q, qpre, qlen, [&](bool valid, int32_t u, int64_t o) {
         bool take = false;
@@ -94,7 +119,7 @@ __global__ void __launch_bounds__(kBlock) ds_relax(View push, const int32_t* __r
                 const int64_t cand = mu + static_cast<int64_t>(w);
                 const int64_t tl = kPart ? static_cast<int64_t>(t) - lo : static_cast<int64_t>(t);
                 if (!kPart || (tl >= 0 && tl < n_local)) {
-                    if (relax_owned(dist, pend, tl, cand, thr)) {
+                    if (relax_owned(dist, pend, tl, cand, thr, tmin)) {
                         take = true;
                         v = static_cast<int32_t>(tl);
                         vdeg = push_degree(push, tl);
@@ -111,6 +136,7 @@ __global__ void __launch_bounds__(kBlock) ds_relax(View push, const int32_t* __r
         block_append(take, v, vdeg, qn, qdeg_n, cnt, sh, mf);
     });
     block_flush(cnt, sh, mf);
+    if (track) block_fold_min(tmin, track);
 }
 
 // ---- light/heavy split (one GPU, weighted): the push entries of every vertex sorted by
@@ -153,9 +179,10 @@ __global__ void ds_seed_ws(const int64_t* off, const int64_t* light, int64_t* di
 // Light entries: snapshot, clear pending, mark the bucket member.  Heavy entries: the member's
 // distance is final and msg already holds it.  Also zeroes the counters and the scan's tail
 // degree for the phase (saves two memset launches per phase).
+// track (partitioned): track[1] = 1 once a member is marked (members wait for their heavy pass).
 __global__ void ds_commit_ws(const int32_t* __restrict__ q, int64_t qlen, const int64_t* __restrict__ dist,
                              int64_t* __restrict__ msg, uint64_t* __restrict__ pend, uint64_t* __restrict__ member,
-                             int64_t* __restrict__ qdeg, Counters* cnt) {
+                             int64_t* __restrict__ qdeg, Counters* cnt, long long* __restrict__ track) {
     if (blockIdx.x == 0) {
         constexpr int kWords = sizeof(Counters) / sizeof(unsigned long long);
         static_assert(kWords <= kBlock, "one thread per counter word");
@@ -169,18 +196,26 @@ __global__ void ds_commit_ws(const int32_t* __restrict__ q, int64_t qlen, const 
         msg[v] = dist[v];
         const uint64_t bit = 1ULL << (v & 63);
         if (pend[v >> 6] & bit) atomicAnd(reinterpret_cast<unsigned long long*>(&pend[v >> 6]), ~bit);
-        if (!(member[v >> 6] & bit)) atomicOr(reinterpret_cast<unsigned long long*>(&member[v >> 6]), bit);
+        if (!(member[v >> 6] & bit)) {
+            atomicOr(reinterpret_cast<unsigned long long*>(&member[v >> 6]), bit);
+            if (track) track[1] = 1;
+        }
     }
 }
 
 // ds_relax over one weight-sorted list: queue entry u relaxes [off[u], light[u]) or, flagged
 // heavy, [light[u], off[u+1]); load-balanced as in ds_relax.
+// kPart: targets outside [lo, lo + n_local) go to rbest / rmark as in ds_relax.
+template <bool kPart>
 __global__ void __launch_bounds__(kBlock) ds_relax_ws(const int64_t* __restrict__ off, const int32_t* __restrict__ adj,
         const int32_t* __restrict__ wt, const int64_t* __restrict__ light, const int32_t* __restrict__ q,
         const int64_t* __restrict__ qpre, int64_t qlen, const int64_t* __restrict__ msg, int64_t* __restrict__ dist,
-        uint64_t* __restrict__ pend, int32_t* __restrict__ qn, int64_t* __restrict__ qdeg_n, Counters* cnt, int64_t thr) {
+        uint64_t* __restrict__ pend, int32_t* __restrict__ qn, int64_t* __restrict__ qdeg_n, Counters* cnt, int64_t thr,
+        int64_t lo, int64_t n_local, int64_t* __restrict__ rbest, uint64_t* __restrict__ rmark,
+        long long* __restrict__ track) {
     __shared__ AppendLds sh;
     unsigned long long mf = 0;
+    long long tmin = kInfLL;
     if (blockIdx.x == 0 && threadIdx.x == 0) cnt->red[1] = static_cast<unsigned long long>(qpre[qlen]);   // work done
     for_each_queue_edge(q, qpre, qlen, [&](bool valid, int32_t qentry, int64_t o) {
         bool take = false;
@@ -196,15 +231,185 @@ __global__ void __launch_bounds__(kBlock) ds_relax_ws(const int64_t* __restrict_
                 atomicOr(&cnt->err, 1ULL);              // edge.value(weight) on a missing key
             } else if (dist[u] < mu) {
                 // improved during this phase: pending again, relaxes with the better distance
-            } else if (relax_owned(dist, pend, t, mu + static_cast<int64_t>(w), thr)) {
-                take = true;
-                v = t;
-                vdeg = light_degree(off, light, t);
+            } else {
+                const int64_t cand = mu + static_cast<int64_t>(w);
+                const int64_t tl = kPart ? static_cast<int64_t>(t) - lo : static_cast<int64_t>(t);
+                if (!kPart || (tl >= 0 && tl < n_local)) {
+                    if (relax_owned(dist, pend, tl, cand, thr, tmin)) {
+                        take = true;
+                        v = static_cast<int32_t>(tl);
+                        vdeg = light_degree(off, light, tl);
+                    }
+                } else if (cand < rbest[t]) {
+                    const long long old = atomicMin(reinterpret_cast<long long*>(&rbest[t]), static_cast<long long>(cand));
+                    if (cand < old) {
+                        const uint64_t bit = 1ULL << (t & 63);
+                        if (!(rmark[t >> 6] & bit)) atomicOr(reinterpret_cast<unsigned long long*>(&rmark[t >> 6]), bit);
+                    }
+                }
             }
         }
         block_append(take, v, vdeg, qn, qdeg_n, cnt, sh, mf);
     });
     block_flush(cnt, sh, mf);
+    if (track) block_fold_min(tmin, track);
+}
+
+// ds_relax_ws<true> in stages (the structure of delta_loop.hip's ds_relax_dev): each thread's
+// kEdgesPerThread entries go through the queue search, the list / snapshot loads, the target
+// loads and the atomics stage by stage, so that each stage's loads are in flight together
+// (one entry at a time left every thread waiting out the search -> list -> distance -> atomic
+// chain once per entry).  The tile's takes are appended with one reservation per block; an
+// owned target's improvement that stays pending outside the queue is folded into track[0],
+// a remote target's goes to rbest / rmark.
+__device__ __forceinline__ int64_t wave_incl_scan(int64_t x) {
+    for (int o = 1; o < 64; o <<= 1) {
+        const int64_t y = __shfl_up(x, o, 64);
+        if (lane() >= o) x += y;
+    }
+    return x;
+}
+
+__global__ void __launch_bounds__(kBlock) ds_relax_ws_staged(const int64_t* __restrict__ off,
+        const int32_t* __restrict__ adj, const int32_t* __restrict__ wt, const int64_t* __restrict__ light,
+        const int32_t* __restrict__ q, const int64_t* __restrict__ qpre, int64_t qlen, const int64_t* __restrict__ msg,
+        int64_t* __restrict__ dist, uint64_t* __restrict__ pend, int32_t* __restrict__ qn, int64_t* __restrict__ qdeg_n,
+        Counters* cnt, int64_t thr, int64_t lo, int64_t n_local, int64_t* __restrict__ rbest,
+        uint64_t* __restrict__ rmark, long long* __restrict__ track) {
+    __shared__ int64_t s_pre[kLdsEntries];
+    __shared__ int32_t s_q[kLdsEntries];
+    __shared__ int64_t s_lo, s_hi;
+    __shared__ int64_t s_c[kWavesPerBlock];
+    __shared__ unsigned long long s_base;
+    const int64_t total = qpre[qlen];
+    if (blockIdx.x == 0 && threadIdx.x == 0) cnt->red[1] = static_cast<unsigned long long>(total);   // work done
+    long long tmin = kInfLL;
+    bool bad = false;
+    unsigned long long mf = 0;
+    const int wave = threadIdx.x >> 6;
+    const int64_t ntiles = (total + kTileEdges - 1) / kTileEdges;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t t0 = tile * kTileEdges;
+        const int64_t t1 = min(total, t0 + kTileEdges);
+        if (threadIdx.x == 0) {             // lo = last i with qpre[i] <= t0; hi = last i with qpre[i] <= t1-1
+            int64_t a = 0, b = qlen;
+            while (b - a > 1) { const int64_t m = (a + b) >> 1; if (qpre[m] <= t0) a = m; else b = m; }
+            s_lo = a;
+            int64_t a2 = a, b2 = qlen;
+            while (b2 - a2 > 1) { const int64_t m = (a2 + b2) >> 1; if (qpre[m] <= t1 - 1) a2 = m; else b2 = m; }
+            s_hi = a2;
+        }
+        __syncthreads();
+        const int64_t qlo = s_lo, qhi = s_hi;
+        const int64_t span = qhi - qlo + 1;
+        const bool in_lds = span + 1 <= kLdsEntries;
+        if (in_lds) {
+            for (int64_t i = threadIdx.x; i <= span; i += kBlock) {
+                s_pre[i] = qpre[qlo + i];
+                if (i < span) s_q[i] = q[qlo + i];
+            }
+        }
+        __syncthreads();
+        int64_t u[kEdgesPerThread], e[kEdgesPerThread];
+#pragma unroll
+        for (int k = 0; k < kEdgesPerThread; ++k) {           // 1: owning queue entry
+            const int64_t j = t0 + k * kBlock + threadIdx.x;
+            u[k] = -1;
+            e[k] = 0;
+            if (j >= t1) continue;
+            int32_t qe;
+            int64_t start;
+            if (in_lds) {
+                int64_t a = 0, b = span;
+                while (b - a > 1) { const int64_t m = (a + b) >> 1; if (s_pre[m] <= j) a = m; else b = m; }
+                qe = s_q[a]; start = s_pre[a];
+            } else {
+                int64_t a = qlo, b = qhi + 1;
+                while (b - a > 1) { const int64_t m = (a + b) >> 1; if (qpre[m] <= j) a = m; else b = m; }
+                qe = q[a]; start = qpre[a];
+            }
+            const uint32_t ue = static_cast<uint32_t>(qe);
+            u[k] = static_cast<int64_t>(ue & ~kHeavyFlag);
+            e[k] = ((ue & kHeavyFlag) ? light[u[k]] : off[u[k]]) + (j - start);
+        }
+        int32_t t[kEdgesPerThread], w[kEdgesPerThread];
+        int64_t mu[kEdgesPerThread], du[kEdgesPerThread];
+#pragma unroll
+        for (int k = 0; k < kEdgesPerThread; ++k) {           // 2: entry, the source's snapshot
+            if (u[k] < 0) continue;
+            t[k] = adj[e[k]];
+            w[k] = wt[e[k]];
+            mu[k] = msg[u[k]];
+            du[k] = dist[u[k]];
+        }
+        int64_t cand[kEdgesPerThread], dt[kEdgesPerThread], tl[kEdgesPerThread];
+#pragma unroll
+        for (int k = 0; k < kEdgesPerThread; ++k) {           // 3: the targets' current bests
+            cand[k] = -1;
+            if (u[k] < 0) continue;
+            if (w[k] == kMissingWeight) { bad = true; continue; }     // edge.value(weight) on a missing key
+            if (du[k] < mu[k]) continue;     // u improved during this phase: pending again, relaxes later
+            cand[k] = mu[k] + static_cast<int64_t>(w[k]);
+            tl[k] = static_cast<int64_t>(t[k]) - lo;
+            dt[k] = (tl[k] >= 0 && tl[k] < n_local) ? dist[tl[k]] : rbest[t[k]];
+        }
+        int32_t tv[kEdgesPerThread];
+        int64_t td[kEdgesPerThread];
+        int64_t ntake = 0, dtake = 0;
+#pragma unroll
+        for (int k = 0; k < kEdgesPerThread; ++k) {           // 4: min, pending bit, take
+            tv[k] = -1;
+            td[k] = 0;
+            if (cand[k] < 0 || cand[k] >= dt[k]) continue;    // a stale (larger) read only costs an atomic
+            if (tl[k] >= 0 && tl[k] < n_local) {
+                const int64_t v = tl[k];
+                const long long old = atomicMin(reinterpret_cast<long long*>(&dist[v]), static_cast<long long>(cand[k]));
+                if (cand[k] >= old) continue;
+                const uint64_t bit = 1ULL << (v & 63);
+                const unsigned long long ob = atomicOr(reinterpret_cast<unsigned long long*>(&pend[v >> 6]), bit);
+                if (!(ob & bit) && cand[k] < thr) {
+                    tv[k] = static_cast<int32_t>(v);
+                    td[k] = light_degree(off, light, v);
+                    ++ntake;
+                    dtake += td[k];
+                } else if (cand[k] < tmin) {
+                    tmin = cand[k];
+                }
+            } else {
+                const int64_t g = t[k];
+                const long long old = atomicMin(reinterpret_cast<long long*>(&rbest[g]), static_cast<long long>(cand[k]));
+                if (cand[k] < old) {
+                    const uint64_t bit = 1ULL << (g & 63);
+                    if (!(rmark[g >> 6] & bit)) atomicOr(reinterpret_cast<unsigned long long*>(&rmark[g >> 6]), bit);
+                }
+            }
+        }
+        // the tile's takes: one reservation per block (block-uniform)
+        const int64_t inc = wave_incl_scan(ntake);
+        if (lane() == 63) s_c[wave] = inc;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int64_t tc = 0;
+            for (int x = 0; x < kWavesPerBlock; ++x) { const int64_t c = s_c[x]; s_c[x] = tc; tc += c; }
+            s_base = tc ? atomicAdd(&cnt->qlen, static_cast<unsigned long long>(tc)) : 0ULL;
+        }
+        __syncthreads();
+        if (ntake) {
+            unsigned long long slot = s_base + static_cast<unsigned long long>(s_c[wave] + inc - ntake);
+#pragma unroll
+            for (int k = 0; k < kEdgesPerThread; ++k)
+                if (tv[k] >= 0) {
+                    qn[slot] = tv[k];
+                    qdeg_n[slot] = td[k];
+                    ++slot;
+                }
+            mf += static_cast<unsigned long long>(dtake);
+        }
+        __syncthreads();
+    }
+    if (__ballot(bad) && lane() == 0) atomicOr(&cnt->err, 1ULL);
+    count_flush(cnt, 0ULL, mf);
+    if (track) block_fold_min(tmin, track);
 }
 
 // Next queue from the bitmaps (one wave per 64-vertex word), clearing what it takes: pending
@@ -213,13 +418,22 @@ __global__ void __launch_bounds__(kBlock) ds_relax_ws(const int64_t* __restrict_
 __global__ void __launch_bounds__(kBlock) ds_extract_ws(const int64_t* __restrict__ off,
         const int64_t* __restrict__ light, uint64_t* __restrict__ pend, uint64_t* __restrict__ member, int64_t n,
         const int64_t* __restrict__ dist, int64_t thr, int32_t* __restrict__ qn, int64_t* __restrict__ qdeg,
-        Counters* cnt) {
+        Counters* cnt, long long* __restrict__ track) {
     const int64_t words = (n + 63) >> 6;
+    long long rest = kInfLL;                    // smallest distance left pending (>= thr)
     auto probe = [&](int64_t wd, Take* t, bool commit) -> bool {
         const uint64_t pb = pend[wd];                            // uniform across the wave
         const uint64_t mb = member[wd];
         const int64_t v = (wd << 6) + lane();
-        const bool lt = pb && ((pb >> lane()) & 1ULL) && dist[v] < thr;
+        if (!(pb | mb)) {                                        // uniform: no loads for an empty word
+            t[0] = {false, 0, 0};
+            t[1] = {false, 0, 0};
+            return false;
+        }
+        const bool pbit = (pb >> lane()) & 1ULL;
+        const long long dv = pbit ? static_cast<long long>(dist[v]) : kInfLL;
+        const bool lt = pbit && dv < thr;
+        if (pbit && !lt && dv < rest) rest = dv;
         const bool mine = mb && ((mb >> lane()) & 1ULL);
         const int64_t hdeg = mine ? off[v + 1] - light[v] : 0;
         const unsigned long long tm = __ballot(lt);
@@ -232,6 +446,50 @@ __global__ void __launch_bounds__(kBlock) ds_extract_ws(const int64_t* __restric
         return tm || mb;
     };
     chunk_extract<2>(words, probe, qn, qdeg, cnt);
+    if (track) block_fold_min(rest, track);
+}
+
+// ---- light/heavy split of a partitioned load (device-assembled: no host lists to sort).
+// The split only needs every row's light entries (w < delta) first, so instead of the one-GPU
+// load's full weight sort, each row is stably partitioned at delta on the device, once per
+// bucket width: off = the concatenated push lists' offsets, light[v] = end of v's light run.
+__global__ void ds_ws_off(View push, int64_t n, int64_t* __restrict__ off) {
+    for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v <= n; v += (int64_t)gridDim.x * blockDim.x)
+        off[v] = push.off0[v] + (push.nlists > 1 ? push.off1[v] : 0);
+}
+
+// One wave per row: a counting pass (ballots) for the light total, then a writing pass with
+// each entry's rank among its kind from the ballots (stable: list order kept on both sides).
+__global__ void __launch_bounds__(kBlock) ds_split_rows(View push, const int64_t* __restrict__ off, int64_t n,
+        int64_t delta, int32_t* __restrict__ adj, int32_t* __restrict__ wt, int64_t* __restrict__ light) {
+    const int64_t waves = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
+    const unsigned long long below = (1ULL << lane()) - 1ULL;
+    for (int64_t v = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; v < n; v += waves) {
+        const int64_t deg = push_degree(push, v);
+        int64_t nl = 0;
+        for (int64_t c = 0; c < deg; c += 64) {
+            int32_t t = 0, w = 0;
+            if (c + lane() < deg) entry_at(push, v, c + lane(), t, w);
+            nl += __popcll(__ballot(c + lane() < deg && static_cast<int64_t>(w) < delta));
+        }
+        const int64_t base = off[v];
+        int64_t li = 0, hi = 0;
+        for (int64_t c = 0; c < deg; c += 64) {
+            const bool in = c + lane() < deg;
+            int32_t t = 0, w = 0;
+            if (in) entry_at(push, v, c + lane(), t, w);
+            const bool lt = in && static_cast<int64_t>(w) < delta;
+            const unsigned long long bl = __ballot(lt), bh = __ballot(in && !lt);
+            if (in) {
+                const int64_t p = lt ? base + li + __popcll(bl & below) : base + nl + hi + __popcll(bh & below);
+                adj[p] = t;
+                wt[p] = w;
+            }
+            li += __popcll(bl);
+            hi += __popcll(bh);
+        }
+        if (lane() == 0) light[v] = base + nl;
+    }
 }
 
 // Pending minimum / count (red[0], red[1]) and the settled bucket's members left (red2).
@@ -253,8 +511,12 @@ __global__ void __launch_bounds__(kBlock) ds_pending_min_ws(const uint64_t* __re
         }
         unsigned long long d[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-            d[u] = ((b[u] >> lane()) & 1ULL) ? static_cast<unsigned long long>(dist[((wd + u * nw) << 6) + lane()]) : ~0ULL >> 1;
+        for (int u = 0; u < 4; ++u) {
+            // b[u] is wave-uniform: an empty word issues no load at all (without the branch the
+            // compiler may load dist for every lane of every word, a full pass over dist)
+            d[u] = ~0ULL >> 1;
+            if (b[u] != 0 && ((b[u] >> lane()) & 1ULL)) d[u] = static_cast<unsigned long long>(dist[((wd + u * nw) << 6) + lane()]);
+        }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             mn = d[u] < mn ? d[u] : mn;
@@ -313,20 +575,30 @@ __global__ void __launch_bounds__(kBlock) ds_pending_min(const uint64_t* __restr
 }
 
 // Next near queue: pending vertices with dist < thr (one wave per 64-vertex word).
+// track (partitioned): the smallest distance left pending is folded into track[0].
 __global__ void __launch_bounds__(kBlock) ds_extract(View push, uint64_t* __restrict__ pend, int64_t n,
         const int64_t* __restrict__ dist, int64_t thr, int32_t* __restrict__ qn, int64_t* __restrict__ qdeg,
-        Counters* cnt) {
+        Counters* cnt, long long* __restrict__ track) {
     const int64_t words = (n + 63) >> 6;
+    long long rest = kInfLL;
     auto probe = [&](int64_t wd, Take* t, bool commit) -> bool {
         const uint64_t b = pend[wd];                             // uniform across the wave
         const int64_t v = (wd << 6) + lane();
-        const bool take = b && ((b >> lane()) & 1ULL) && dist[v] < thr;
+        if (!b) {                                                // uniform: no loads for an empty word
+            t[0] = {false, 0, 0};
+            return false;
+        }
+        const bool pbit = (b >> lane()) & 1ULL;
+        const long long dv = pbit ? static_cast<long long>(dist[v]) : kInfLL;
+        const bool take = pbit && dv < thr;
+        if (pbit && !take && dv < rest) rest = dv;
         const unsigned long long tm = __ballot(take);
         if (commit && lane() == 0 && tm) pend[wd] = b & ~tm;
         t[0] = {take, static_cast<int32_t>(v), take ? push_degree(push, v) : 0};
         return tm != 0;
     };
     chunk_extract<1>(words, probe, qn, qdeg, cnt);
+    if (track) block_fold_min(rest, track);
 }
 
 // Partitioned: marked remote targets per owner rank (rank r owns words [r*wpr, (r+1)*wpr)).
@@ -359,13 +631,71 @@ __global__ void ds_mark_pack(uint64_t* __restrict__ rmark, int64_t words, int64_
     }
 }
 
+// Partitioned loop state without a bitmap scan (the idea of delta_loop.hip's decision):
+//   track[0] <= the smallest distance of a pending vertex outside the near queue.  An
+//            extraction sets it to the smallest distance it leaves pending; every later
+//            improvement that leaves its vertex pending outside the queue mins its distance in.
+//            It can be stale-low (that vertex was queued and committed since): then the next
+//            extraction takes nothing, track[0] is exact again, and the loop goes on, one
+//            extra exchange later, to the same converged distances.
+//   track[1] = 1 once a bucket member was marked since the last extraction (light/heavy).
+// Reset right before every extraction.
+__global__ void ds_track_reset(long long* __restrict__ track) {
+    if (threadIdx.x == 0) { track[0] = kInfLL; track[1] = 0; }
+}
+
+// After the header all-to-all: own[4r..4r+4) = this rank's header to r, recv[4r..) = r's
+// header to this rank {pair elements, near-queue length, track[0], track[1]}.  out (2W + 3
+// words, read by the host in one go): pair elements sent to / received from each rank, then
+// the global near-queue length, pending minimum and -(ranks with members).
+__global__ void ds_header_fold(const int64_t* __restrict__ own, const int64_t* __restrict__ recv, int nranks,
+                               int64_t* __restrict__ out) {
+    if (threadIdx.x != 0) return;
+    int64_t gq = 0, pm = INT64_MAX, mem = 0;
+    for (int r = 0; r < nranks; ++r) {
+        out[r] = own[4 * r];
+        out[nranks + r] = recv[4 * r];
+        gq += recv[4 * r + 1];
+        pm = recv[4 * r + 2] < pm ? recv[4 * r + 2] : pm;
+        mem -= recv[4 * r + 3];
+    }
+    out[2 * nranks] = gq;
+    out[2 * nranks + 1] = pm;
+    out[2 * nranks + 2] = mem;
+}
+
+// The exchange header on the device (no host round trip): offs[r] = the pack offset of rank r's
+// pairs; header to r = {pair elements sent to r, this rank's near-queue length, track[0],
+// track[1]} (sizes[4r..4r+4)).
+__global__ void ds_mark_sizes(unsigned long long* __restrict__ counts, int nranks, int64_t qlen,
+                              unsigned long long* __restrict__ offs, unsigned long long* __restrict__ cursor,
+                              const long long* __restrict__ track, int64_t* __restrict__ sizes) {
+    if (threadIdx.x != 0) return;
+    unsigned long long acc = 0;
+    const int64_t pm = track[0], mem = track[1];
+    for (int r = 0; r < nranks; ++r) {
+        const unsigned long long c = counts[r];
+        offs[r] = acc;
+        acc += c;
+        sizes[4 * r] = 2 * static_cast<int64_t>(c);
+        sizes[4 * r + 1] = qlen;
+        sizes[4 * r + 2] = pm;
+        sizes[4 * r + 3] = mem;
+        counts[r] = 0;              // ready for the next phase's count; the pack's cursors start at 0
+        cursor[r] = 0;
+    }
+}
+
 // Owner side of the exchange: min the received (local id, distance) pairs into dist with
 // the pending / near-queue rule of ds_relax.
+// ws_off / light set (light/heavy split): a queued vertex carries its light degree.
 __global__ void __launch_bounds__(kBlock) ds_apply(View push, const int64_t* __restrict__ recv, int64_t npairs,
         int64_t* __restrict__ dist, uint64_t* __restrict__ pend, int32_t* __restrict__ qn,
-        int64_t* __restrict__ qdeg_n, Counters* cnt, int64_t thr) {
+        int64_t* __restrict__ qdeg_n, Counters* cnt, int64_t thr, const int64_t* __restrict__ ws_off,
+        const int64_t* __restrict__ light, long long* __restrict__ track) {
     __shared__ AppendLds sh;
     unsigned long long mf = 0;
+    long long tmin = kInfLL;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < npairs; base += stride) {   // block-uniform trips
         const int64_t i = base + threadIdx.x;
@@ -374,15 +704,16 @@ __global__ void __launch_bounds__(kBlock) ds_apply(View push, const int64_t* __r
         int64_t vdeg = 0;
         if (i < npairs) {
             const int64_t vl = recv[2 * i];
-            if (relax_owned(dist, pend, vl, recv[2 * i + 1], thr)) {
+            if (relax_owned(dist, pend, vl, recv[2 * i + 1], thr, tmin)) {
                 take = true;
                 v = static_cast<int32_t>(vl);
-                vdeg = push_degree(push, vl);
+                vdeg = light ? light_degree(ws_off, light, vl) : push_degree(push, vl);
             }
         }
         block_append(take, v, vdeg, qn, qdeg_n, cnt, sh, mf);
     }
     block_flush(cnt, sh, mf);
+    if (track) block_fold_min(tmin, track);
 }
 
 inline int grid_for(int64_t work, int cap) {
@@ -393,6 +724,11 @@ inline int grid_for(int64_t work, int cap) {
 }
 
 }  // namespace
+
+static long long env_i64_d(const char* name, long long dflt) {
+    const char* e = std::getenv(name);
+    return e ? std::atoll(e) : dflt;
+}
 
 hipError_t k_ds_seed(const View& push, int64_t* dist, int32_t* q, int64_t* qdeg, int64_t seed, hipStream_t s) {
     ds_seed<<<1, 64, 0, s>>>(push, dist, q, qdeg, seed);
@@ -406,14 +742,15 @@ hipError_t k_ds_relax(const View& push, const int32_t* q, const int64_t* qpre, i
                       int64_t* dist, uint64_t* pend, int32_t* qn, int64_t* qdeg_n, Counters* cnt, int weighted,
                       int64_t thr, hipStream_t s) {
     ds_relax<false><<<256 * 8, kBlock, 0, s>>>(push, q, qpre, qlen, msg, dist, pend, qn, qdeg_n, cnt, weighted, thr,
-                                              0, 0, nullptr, nullptr);
+                                              0, 0, nullptr, nullptr, nullptr);
     return hipGetLastError();
 }
 hipError_t k_ds_relax_part(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen, const int64_t* msg,
                            int64_t* dist, uint64_t* pend, int32_t* qn, int64_t* qdeg_n, Counters* cnt, int weighted,
-                           int64_t thr, int64_t lo, int64_t n_local, int64_t* rbest, uint64_t* rmark, hipStream_t s) {
+                           int64_t thr, int64_t lo, int64_t n_local, int64_t* rbest, uint64_t* rmark, long long* track,
+                           hipStream_t s) {
     ds_relax<true><<<256 * 8, kBlock, 0, s>>>(push, q, qpre, qlen, msg, dist, pend, qn, qdeg_n, cnt, weighted, thr,
-                                             lo, n_local, rbest, rmark);
+                                             lo, n_local, rbest, rmark, track);
     return hipGetLastError();
 }
 hipError_t k_ds_light_end(const DevCsr& ws, int64_t delta, int64_t n, int64_t* light, hipStream_t s) {
@@ -426,21 +763,40 @@ hipError_t k_ds_seed_ws(const DevCsr& ws, const int64_t* light, int64_t* dist, i
     return hipGetLastError();
 }
 hipError_t k_ds_commit_ws(const int32_t* q, int64_t qlen, const int64_t* dist, int64_t* msg, uint64_t* pend,
-                          uint64_t* member, int64_t* qdeg, Counters* cnt, hipStream_t s) {
-    ds_commit_ws<<<grid_for(qlen, 2048), kBlock, 0, s>>>(q, qlen, dist, msg, pend, member, qdeg, cnt);
+                          uint64_t* member, int64_t* qdeg, Counters* cnt, hipStream_t s, long long* track) {
+    ds_commit_ws<<<grid_for(qlen, 2048), kBlock, 0, s>>>(q, qlen, dist, msg, pend, member, qdeg, cnt, track);
     return hipGetLastError();
 }
 hipError_t k_ds_relax_ws(const DevCsr& ws, const int64_t* light, const int32_t* q, const int64_t* qpre, int64_t qlen,
                          const int64_t* msg, int64_t* dist, uint64_t* pend, int32_t* qn, int64_t* qdeg_n, Counters* cnt,
                          int64_t thr, hipStream_t s) {
-    ds_relax_ws<<<256 * 8, kBlock, 0, s>>>(ws.off, ws.adj, ws.w, light, q, qpre, qlen, msg, dist, pend, qn, qdeg_n, cnt,
-                                           thr);
+    ds_relax_ws<false><<<256 * 8, kBlock, 0, s>>>(ws.off, ws.adj, ws.w, light, q, qpre, qlen, msg, dist, pend, qn, qdeg_n,
+                                                  cnt, thr, 0, 0, nullptr, nullptr, nullptr);
+    return hipGetLastError();
+}
+hipError_t k_ds_relax_ws_part(const DevCsr& ws, const int64_t* light, const int32_t* q, const int64_t* qpre, int64_t qlen,
+                              const int64_t* msg, int64_t* dist, uint64_t* pend, int32_t* qn, int64_t* qdeg_n,
+                              Counters* cnt, int64_t thr, int64_t lo, int64_t n_local, int64_t* rbest, uint64_t* rmark,
+                              long long* track, hipStream_t s) {
+    static const bool staged = env_i64_d("TGO_DS_PART_STAGED", 1) != 0;     // A/B: 0 = one entry at a time
+    if (staged)
+        ds_relax_ws_staged<<<256 * 8, kBlock, 0, s>>>(ws.off, ws.adj, ws.w, light, q, qpre, qlen, msg, dist, pend, qn,
+                                                      qdeg_n, cnt, thr, lo, n_local, rbest, rmark, track);
+    else
+        ds_relax_ws<true><<<256 * 8, kBlock, 0, s>>>(ws.off, ws.adj, ws.w, light, q, qpre, qlen, msg, dist, pend, qn,
+                                                     qdeg_n, cnt, thr, lo, n_local, rbest, rmark, track);
+    return hipGetLastError();
+}
+hipError_t k_ds_split_rows(const View& push, int64_t n, int64_t delta, DevCsr& ws, int64_t* light, hipStream_t s) {
+    ds_ws_off<<<grid_for(n + 1, 4096), kBlock, 0, s>>>(push, n, ws.off);
+    ds_split_rows<<<grid_for(n * 64, 8192), kBlock, 0, s>>>(push, ws.off, n, delta, ws.adj, ws.w, light);
     return hipGetLastError();
 }
 hipError_t k_ds_extract_ws(const DevCsr& ws, const int64_t* light, uint64_t* pend, uint64_t* member, int64_t n,
-                           const int64_t* dist, int64_t thr, int32_t* qn, int64_t* qdeg, Counters* cnt, hipStream_t s) {
+                           const int64_t* dist, int64_t thr, int32_t* qn, int64_t* qdeg, Counters* cnt, hipStream_t s,
+                           long long* track) {
     const int64_t words = (n + 63) / 64;
-    ds_extract_ws<<<extract_grid(words), kBlock, 0, s>>>(ws.off, light, pend, member, n, dist, thr, qn, qdeg, cnt);
+    ds_extract_ws<<<extract_grid(words), kBlock, 0, s>>>(ws.off, light, pend, member, n, dist, thr, qn, qdeg, cnt, track);
     return hipGetLastError();
 }
 hipError_t k_ds_pending_min_ws(const uint64_t* pend, const uint64_t* member, int64_t words, const int64_t* dist,
@@ -452,10 +808,18 @@ hipError_t k_ds_pending_min(const uint64_t* pend, int64_t words, const int64_t* 
     ds_pending_min<<<grid_for(words, 1024), kBlock, 0, s>>>(pend, words, dist, cnt);
     return hipGetLastError();
 }
+hipError_t k_ds_track_reset(long long* track, hipStream_t s) {
+    ds_track_reset<<<1, 64, 0, s>>>(track);
+    return hipGetLastError();
+}
+hipError_t k_ds_header_fold(const int64_t* own, const int64_t* recv, int nranks, int64_t* out, hipStream_t s) {
+    ds_header_fold<<<1, 64, 0, s>>>(own, recv, nranks, out);
+    return hipGetLastError();
+}
 hipError_t k_ds_extract(const View& push, uint64_t* pend, int64_t n, const int64_t* dist, int64_t thr, int32_t* qn,
-                        int64_t* qdeg, Counters* cnt, hipStream_t s) {
+                        int64_t* qdeg, Counters* cnt, hipStream_t s, long long* track) {
     const int64_t words = (n + 63) / 64;
-    ds_extract<<<extract_grid(words), kBlock, 0, s>>>(push, pend, n, dist, thr, qn, qdeg, cnt);
+    ds_extract<<<extract_grid(words), kBlock, 0, s>>>(push, pend, n, dist, thr, qn, qdeg, cnt, track);
     return hipGetLastError();
 }
 hipError_t k_ds_mark_count(const uint64_t* rmark, int64_t words, int64_t wpr, unsigned long long* counts, hipStream_t s) {
@@ -467,9 +831,16 @@ hipError_t k_ds_mark_pack(uint64_t* rmark, int64_t words, int64_t wpr, int64_t n
     ds_mark_pack<<<grid_for(words, 4096), kBlock, 0, s>>>(rmark, words, wpr, n_local, rbest, offs, cursor, send);
     return hipGetLastError();
 }
+hipError_t k_ds_mark_sizes(unsigned long long* counts, int nranks, int64_t qlen, unsigned long long* offs,
+                           unsigned long long* cursor, const long long* track, int64_t* sizes, hipStream_t s) {
+    ds_mark_sizes<<<1, 64, 0, s>>>(counts, nranks, qlen, offs, cursor, track, sizes);
+    return hipGetLastError();
+}
 hipError_t k_ds_apply(const View& push, const int64_t* recv, int64_t npairs, int64_t* dist, uint64_t* pend, int32_t* qn,
-                      int64_t* qdeg_n, Counters* cnt, int64_t thr, hipStream_t s) {
-    ds_apply<<<grid_for(npairs, 4096), kBlock, 0, s>>>(push, recv, npairs, dist, pend, qn, qdeg_n, cnt, thr);
+                      int64_t* qdeg_n, Counters* cnt, int64_t thr, const int64_t* ws_off, const int64_t* light,
+                      long long* track, hipStream_t s) {
+    ds_apply<<<grid_for(npairs, 4096), kBlock, 0, s>>>(push, recv, npairs, dist, pend, qn, qdeg_n, cnt, thr, ws_off, light,
+                                                       track);
     return hipGetLastError();
 }
 

@@ -575,6 +575,7 @@ struct Scratch {
     int64_t* ds_rbest = nullptr;    // n_global: best distance sent to each remote vertex
     uint64_t* ds_rmark = nullptr;   // n_global bits: remote vertices improved this phase
     unsigned long long* ds_pack = nullptr;   // 3 x kMaxRanks: counts, offsets, cursors
+    DevCsr ds_pws;                  // the push view split at ds_light_delta (k_ds_split_rows)
 };
 
 constexpr int kMaxRanks = 64;
@@ -629,13 +630,23 @@ hipError_t k_ds_relax(const View& push, const int32_t* q, const int64_t* qpre, i
 hipError_t k_ds_light_end(const DevCsr& ws, int64_t delta, int64_t n, int64_t* light, hipStream_t s);
 hipError_t k_ds_seed_ws(const DevCsr& ws, const int64_t* light, int64_t* dist, int32_t* q, int64_t* qdeg, int64_t seed,
                         hipStream_t s);
+// track (partitioned, see ds_track_reset): pending-minimum / member state, nullptr on one GPU
 hipError_t k_ds_commit_ws(const int32_t* q, int64_t qlen, const int64_t* dist, int64_t* msg, uint64_t* pend,
-                          uint64_t* member, int64_t* qdeg, Counters* cnt, hipStream_t s);
+                          uint64_t* member, int64_t* qdeg, Counters* cnt, hipStream_t s, long long* track = nullptr);
 hipError_t k_ds_relax_ws(const DevCsr& ws, const int64_t* light, const int32_t* q, const int64_t* qpre, int64_t qlen,
                          const int64_t* msg, int64_t* dist, uint64_t* pend, int32_t* qn, int64_t* qdeg_n, Counters* cnt,
                          int64_t thr, hipStream_t s);
+// partitioned: remote targets to rbest / rmark (as k_ds_relax_part)
+hipError_t k_ds_relax_ws_part(const DevCsr& ws, const int64_t* light, const int32_t* q, const int64_t* qpre, int64_t qlen,
+                              const int64_t* msg, int64_t* dist, uint64_t* pend, int32_t* qn, int64_t* qdeg_n,
+                              Counters* cnt, int64_t thr, int64_t lo, int64_t n_local, int64_t* rbest, uint64_t* rmark,
+                              long long* track, hipStream_t s);
+// partitioned loads: ws (off n+1, adj / w push-view nnz) = the push view with every row stably
+// partitioned at delta (light entries first); light[v] = end of v's light run
+hipError_t k_ds_split_rows(const View& push, int64_t n, int64_t delta, DevCsr& ws, int64_t* light, hipStream_t s);
 hipError_t k_ds_extract_ws(const DevCsr& ws, const int64_t* light, uint64_t* pend, uint64_t* member, int64_t n,
-                           const int64_t* dist, int64_t thr, int32_t* qn, int64_t* qdeg, Counters* cnt, hipStream_t s);
+                           const int64_t* dist, int64_t thr, int32_t* qn, int64_t* qdeg, Counters* cnt, hipStream_t s,
+                           long long* track = nullptr);
 hipError_t k_ds_pending_min_ws(const uint64_t* pend, const uint64_t* member, int64_t words, const int64_t* dist,
                                Counters* cnt, hipStream_t s);
 // device-driven light/heavy loop (delta_loop.hip)
@@ -662,16 +673,25 @@ hipError_t k_ds_loop_step_bins(const DevCsr& ws, const int64_t* light, uint64_t*
                                uint64_t* done, bool done_filter, int64_t scan_above, const DsPull& pull,
                                hipStream_t s);
 hipError_t k_ds_pending_min(const uint64_t* pend, int64_t words, const int64_t* dist, Counters* cnt, hipStream_t s);
+// partitioned loop state (delta.hip ds_track_reset): reset before an extraction; the header
+// all-to-all's result folded into {sent W, received W, global queue, pending min, -members}
+hipError_t k_ds_track_reset(long long* track, hipStream_t s);
+hipError_t k_ds_header_fold(const int64_t* own, const int64_t* recv, int nranks, int64_t* out, hipStream_t s);
 hipError_t k_ds_extract(const View& push, uint64_t* pend, int64_t n, const int64_t* dist, int64_t thr, int32_t* qn,
-                        int64_t* qdeg, Counters* cnt, hipStream_t s);
+                        int64_t* qdeg, Counters* cnt, hipStream_t s, long long* track = nullptr);
 hipError_t k_ds_relax_part(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen, const int64_t* msg,
                            int64_t* dist, uint64_t* pend, int32_t* qn, int64_t* qdeg_n, Counters* cnt, int weighted,
-                           int64_t thr, int64_t lo, int64_t n_local, int64_t* rbest, uint64_t* rmark, hipStream_t s);
+                           int64_t thr, int64_t lo, int64_t n_local, int64_t* rbest, uint64_t* rmark, long long* track,
+                           hipStream_t s);
 hipError_t k_ds_mark_count(const uint64_t* rmark, int64_t words, int64_t wpr, unsigned long long* counts, hipStream_t s);
 hipError_t k_ds_mark_pack(uint64_t* rmark, int64_t words, int64_t wpr, int64_t n_local, const int64_t* rbest,
                           const unsigned long long* offs, unsigned long long* cursor, int64_t* send, hipStream_t s);
+// also zeroes counts and cursor (the next phase's count / this phase's pack start from 0)
+hipError_t k_ds_mark_sizes(unsigned long long* counts, int nranks, int64_t qlen, unsigned long long* offs,
+                           unsigned long long* cursor, const long long* track, int64_t* sizes, hipStream_t s);
 hipError_t k_ds_apply(const View& push, const int64_t* recv, int64_t npairs, int64_t* dist, uint64_t* pend, int32_t* qn,
-                      int64_t* qdeg_n, Counters* cnt, int64_t thr, hipStream_t s);
+                      int64_t* qdeg_n, Counters* cnt, int64_t thr, const int64_t* ws_off, const int64_t* light,
+                      long long* track, hipStream_t s);
 hipError_t k_unpermute_i64(const int64_t* in, const int32_t* perm, int64_t* out, int64_t n, hipStream_t s);
 hipError_t k_ms_seed(const int64_t* seeds, int nseeds, uint64_t* vis, uint64_t* fr, int64_t fr_rows, hipStream_t s);
 hipError_t k_ms_diag_take(unsigned long long* out10, hipStream_t s);   // 10 diagnostic words

@@ -321,6 +321,9 @@ int part_ms_settle_sums(tgo_ctx* ctx, int64_t* out, bool count_only = false);
 void part_ms_own_next(tgo_ctx* ctx, uint64_t* next);
 // device words to the host through the mapped counter page (no stream synchronisation)
 int part_read_words(tgo_ctx* ctx, const int64_t* dev, int count, int64_t* out);
+int part_sssp_relax_dev(tgo_ctx* ctx, int64_t thr, int32_t nranks, int64_t* send, int64_t* sizes);
+int part_sssp_header_fold(tgo_ctx* ctx, const int64_t* own, const int64_t* recv, int nranks, int64_t* out);
+int part_sssp_split(tgo_ctx* ctx, int64_t delta, bool* on);
 double ms_split_of(const tgo_ctx* ctx);
 std::shared_ptr<void>& part_state_of(tgo_ctx* ctx);
 int part_in_list(tgo_ctx* ctx, const int32_t** adj, int64_t* nnz);
@@ -806,58 +809,56 @@ extern "C" int tgo_part_sssp_run(tgo_ctx* ctx, tgo_exchange* x, int64_t seed_glo
     hipStream_t st = d.st;
     int64_t *send = nullptr, *recv = nullptr, *sizes = nullptr;
     if ((rc = scratch(ctx, send, 2 * ng + 2, 14)) || (rc = scratch(ctx, recv, 2 * ng + 2, 15)) ||
-        (rc = scratch(ctx, sizes, 4 * W, 16)))
+        (rc = scratch(ctx, sizes, 11 * W + 3, 16)))
         return rc;
     int64_t out[2] = {0, 0};
     if ((rc = tgo_part_sssp_begin(ctx, seed_global, delta, out))) return rc;
-    int64_t qlen = out[0];
     if (delta <= 0) {           // the ranks' default widths follow their local mean weight: agree on one
         if ((rc = d.reduce(&out[1], 1, tgo_exchange::kRedMax, &delta))) return rc;
     }
     if (delta <= 0) return part_fail(ctx, TGO_E_INVALID, "tgo_part_sssp_run: bucket width");
+    // light/heavy split (weighted loads): the same decision on every rank (the load's weights
+    // and the agreed width); the loop below is the same either way
+    bool split = false;
+    if ((rc = part_sssp_split(ctx, delta, &split))) return rc;
+    (void)split;
     int64_t thr = delta;
     int phases = 0;
-    std::vector<int64_t> sc(W), both(4 * W);
+    // per phase, ONE host read: the relax writes a 4-word header per peer on the device
+    // {pair elements for it, near-queue length, pending minimum, members flag}; one all-to-all
+    // moves the headers and a fold (2W + 3 words: sent / received sizes, global queue length,
+    // pending minimum, members) comes back through the mapped counter page.  An empty global
+    // near queue then moves straight to the next bucket: the pending minimum is kept on the
+    // fly (delta.hip ds_track_reset), so no bitmap scan and no second collective.
+    int64_t* hdr_recv = sizes + 4 * W;
+    int64_t* fold = sizes + 8 * W;
+    const int nf = 2 * W + 3;
+    std::vector<int64_t> hf(nf);
     std::vector<size_t> sb(W), so(W), rb(W), ro(W);
     for (;;) {
-        // relax (a no-op on an empty near queue), then ONE all-to-all carrying, per peer, the
-        // pair elements sent to it and this rank's queue length: the sizes of the pair exchange
-        // and the global queue length arrive together (one host read per phase for both)
         DevSpan span(st, "part.sssp.phase", {"phase", phases}, {"threshold", thr});
-        if ((rc = tgo_part_sssp_relax(ctx, thr, W, send, sc.data()))) break;
-        for (int p = 0; p < W; ++p) { both[2 * p] = 2 * sc[p]; both[2 * p + 1] = qlen; }
-        if (hipMemcpyAsync(sizes, both.data(), 2 * W * sizeof(int64_t), hipMemcpyHostToDevice, st) != hipSuccess) {
-            rc = d.hip("sizes upload");
-            break;
-        }
-        if (int r = x->all_to_all(sizes, sizes + 2 * W, 16, st)) { rc = d.xfail(r); break; }
-        if (4 * W <= 32) {                 // through the mapped counter page (up to 8 ranks)
-            if ((rc = part_read_words(ctx, sizes, 4 * W, both.data()))) break;
-        } else if (hipMemcpyAsync(both.data(), sizes, 4 * W * sizeof(int64_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
-                   hipStreamSynchronize(st) != hipSuccess) { rc = d.hip("sizes read"); break; }
-        int64_t gq = 0;
-        for (int p = 0; p < W; ++p) gq += both[2 * W + 2 * p + 1];
-        if (gq == 0) {          // every near queue was empty (nothing was relaxed): the next non-empty bucket
+        if ((rc = part_sssp_relax_dev(ctx, thr, W, send, sizes))) break;
+        if (int r = x->all_to_all(sizes, hdr_recv, 32, st)) { rc = d.xfail(r); break; }
+        if ((rc = part_sssp_header_fold(ctx, sizes, hdr_recv, W, fold))) break;
+        if (nf <= 32) {                    // through the mapped counter page (up to 14 ranks)
+            if ((rc = part_read_words(ctx, fold, nf, hf.data()))) break;
+        } else if (hipMemcpyAsync(hf.data(), fold, nf * sizeof(int64_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                   hipStreamSynchronize(st) != hipSuccess) { rc = d.hip("header read"); break; }
+        if (hf[2 * W] == 0) {   // every near queue was empty (nothing was relaxed): the next non-empty bucket
             span.end();
-            int64_t pm[2] = {0, 0}, mn = 0;
-            if ((rc = tgo_part_sssp_pending_min(ctx, pm))) break;
-            if ((rc = d.reduce(&pm[0], 1, tgo_exchange::kRedMin, &mn))) break;
-            if (mn == INT64_MAX) break;
-            if (mn >= thr) thr = (mn / delta + 1) * delta;
-            int64_t c[2] = {0, 0};
-            if ((rc = tgo_part_sssp_extract(ctx, thr, c))) break;
-            qlen = c[0];
+            const int64_t mn = hf[2 * W + 1];
+            if (mn == INT64_MAX && hf[2 * W + 2] == 0) break;   // converged: nothing pending, no members left
+            if (mn != INT64_MAX && mn >= thr) thr = (mn / delta + 1) * delta;
+            if ((rc = tgo_part_sssp_extract(ctx, thr, nullptr))) break;
             continue;
         }
         size_t a = 0, b = 0;
         for (int p = 0; p < W; ++p) {
-            sb[p] = static_cast<size_t>(both[2 * p]) * 8; so[p] = a; a += sb[p];
-            rb[p] = static_cast<size_t>(both[2 * W + 2 * p]) * 8; ro[p] = b; b += rb[p];
+            sb[p] = static_cast<size_t>(hf[p]) * 8; so[p] = a; a += sb[p];
+            rb[p] = static_cast<size_t>(hf[W + p]) * 8; ro[p] = b; b += rb[p];
         }
         if (int r = x->all_to_allv(send, sb.data(), so.data(), recv, rb.data(), ro.data(), st)) { rc = d.xfail(r); break; }
-        int64_t c[2] = {0, 0};
-        if ((rc = tgo_part_sssp_apply(ctx, thr, recv, static_cast<int64_t>(b / 16), c))) break;
-        qlen = c[0];
+        if ((rc = tgo_part_sssp_apply(ctx, thr, recv, static_cast<int64_t>(b / 16), nullptr))) break;
         ++phases;
     }
     trace_resolve(st);
