@@ -64,6 +64,7 @@ struct tgo_ctx {
     int32_t part_phases = 0;
     int64_t part_seed = -1;     // partitioned SSSP: the seed's internal id when owned here
     bool part_split = false;    // partitioned SSSP run on the light/heavy split (part_sssp_split)
+    bool part_devloop = false;  // ... and on the device-sized loop (delta_loop.hip, part_sssp_dev_*)
     int64_t pv_max_out = 0, pv_max_in = 0;   // largest OUT / IN list of a vertex cut
     std::vector<int64_t> pv_rows;            // row ids of the vertex cuts
     // last finished program whose compute keys tgo_result_rows can encode (-1 = none)
@@ -2973,6 +2974,7 @@ int tgo_part_sssp_begin(tgo_ctx* ctx, int64_t seed_global, int64_t delta, int64_
     ctx->part_phases = 0;
     ctx->part_seed = -1;
     ctx->part_split = false;
+    ctx->part_devloop = false;
     int64_t seed = seed_global - g.lo;
     if (seed >= 0 && seed < n) {
         seed = ctx->perm[seed];
@@ -3119,6 +3121,16 @@ int tgo_part_sssp_end(tgo_ctx* ctx, int64_t* dist_local, int64_t* reached) {
     DevGraph& g = ctx->g;
     Scratch& s = ctx->sc;
     hipStream_t st = ctx->stream;
+    if (ctx->part_devloop) {            // the device loop's counts and failure flag
+        DsLoop h{};
+        HIP_TRY(hipMemcpyAsync(&h, s.ds_loop, sizeof(DsLoop), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        ctx->part_devloop = false;
+        if (h.err) return fail(ctx, TGO_E_PROGRAM,
+            "vertex program failed: a traversed edge has no value for the weight property");
+        ctx->part_relaxed = static_cast<int64_t>(h.relaxed);
+        ctx->part_phases = static_cast<int32_t>(h.phases);
+    }
     HIP_TRY(k_dist_finalize(s.dist, g.n, st));
     HIP_TRY(hipEventRecord(ctx->ev1, st));
     if (reached) {
@@ -3392,7 +3404,61 @@ int part_sssp_split(tgo_ctx* ctx, int64_t delta, bool* on) {
     if (ctx->part_seed >= 0) HIP_TRY(k_ds_seed_ws(s.ds_pws, s.ds_light, s.dist, s.q[0], s.qdeg, ctx->part_seed, st));
     ctx->part_split = true;
     *on = true;
+    // the device-sized loop (TGO_DS_PART_DEVLOOP=0: the host-sized phases above) when the
+    // packed queue counters hold a queue (2n + 2 takes, nnz entries), as on one GPU
+    static const bool devloop = env_i64("TGO_DS_PART_DEVLOOP", 1) != 0;
+    constexpr int64_t kDsMaxCount = int64_t(1) << (64 - kDsCountShift);
+    if (devloop && 2 * n + 2 < kDsMaxCount && s.ds_pws.nnz < (int64_t(1) << kDsCountShift)) {
+        if (!s.ds_loop) {
+            for (int b = 0; b < 2; ++b) {
+                HIP_TRY(dev_alloc(ctx, s.ds_q[b], 2 * n + 2));
+                HIP_TRY(dev_alloc(ctx, s.ds_qp[b], 2 * n + 2));
+            }
+            HIP_TRY(dev_alloc(ctx, s.ds_loop, 1));
+            ctx->st.device_bytes = ctx->dev_bytes;
+        }
+        HIP_TRY(k_ds_loop_seed(s.ds_pws, s.ds_light, s.dist, s.ds_q[0], s.ds_qp[0], s.ds_loop, ctx->part_seed, delta, st));
+        ctx->part_devloop = true;
+        ctx->part_cur = 0;
+    }
     return part_done(ctx);
+}
+bool part_sssp_devloop(const tgo_ctx* ctx) { return ctx->part_devloop; }
+// One phase of the device-sized loop, relax half: commit + relax of the current queue (remote
+// targets marked), then the exchange header (sizes, 4 words per rank) and the pack.
+int part_sssp_dev_relax(tgo_ctx* ctx, int32_t nranks, int64_t* send, int64_t* sizes) {
+    DevGraph& g = ctx->g;
+    Scratch& s = ctx->sc;
+    hipStream_t st = ctx->stream;
+    if (!ctx->part_devloop || nranks < 1 || nranks > kMaxRanks || g.n * nranks != g.n_global)
+        return fail(ctx, TGO_E_STATE, "part_sssp_dev_relax");
+    HIP_TRY(k_ds_part_relax(s.ds_pws, s.ds_light, s.vb, s.ds_member, s.dist, s.msg, s.ds_q, s.ds_qp, s.ds_loop,
+                            ctx->part_cur, s.ds_light_delta, g.lo, g.n, s.ds_rbest, s.ds_rmark, st));
+    unsigned long long* counts = s.ds_pack;
+    unsigned long long* offs = counts + kMaxRanks;
+    unsigned long long* cursor = offs + kMaxRanks;
+    const int64_t words = g.n_global / 64, wpr = g.n / 64;
+    if (nranks > 1) HIP_TRY(k_ds_mark_count(s.ds_rmark, words, wpr, counts, st));   // one rank marks nothing
+    HIP_TRY(k_ds_part_header(counts, nranks, s.ds_loop, ctx->part_cur, offs, cursor, sizes, st));
+    if (nranks > 1) HIP_TRY(k_ds_mark_pack(s.ds_rmark, words, wpr, g.n, s.ds_rbest, offs, cursor, send, st));
+    return TGO_OK;
+}
+// ... apply half: the received pairs into the next queue, which becomes current
+int part_sssp_dev_apply(tgo_ctx* ctx, const int64_t* recv, int64_t npairs) {
+    Scratch& s = ctx->sc;
+    if (!ctx->part_devloop) return fail(ctx, TGO_E_STATE, "part_sssp_dev_apply");
+    HIP_TRY(k_ds_part_apply(recv, npairs, s.ds_pws, s.ds_light, s.dist, s.vb, s.ds_q, s.ds_qp, s.ds_loop, ctx->part_cur,
+                            ctx->stream));
+    ctx->part_cur ^= 1;
+    return TGO_OK;
+}
+// ... after an empty global phase: the next near queue (and the members' heavy entries) below thr
+int part_sssp_dev_extract(tgo_ctx* ctx, int64_t thr) {
+    Scratch& s = ctx->sc;
+    if (!ctx->part_devloop) return fail(ctx, TGO_E_STATE, "part_sssp_dev_extract");
+    HIP_TRY(k_ds_part_extract(s.ds_pws, s.ds_light, s.vb, s.ds_member, ctx->g.n, s.dist, s.ds_q, s.ds_qp, s.ds_loop,
+                              ctx->part_cur, thr, ctx->stream));
+    return TGO_OK;
 }
 // `count` device words (on the ctx stream, after the work queued so far) to out, through the
 // host-mapped counter page: one tiny kernel and a spin instead of a copy and a stream wait.

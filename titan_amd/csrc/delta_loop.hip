@@ -92,10 +92,14 @@ __global__ void ds_loop_seed(const int64_t* off, const int64_t* light, int64_t* 
     if (blockIdx.x != 0) return;
     if (threadIdx.x < kDsMaxBins) L->bc[threadIdx.x] = 0;
     if (threadIdx.x != 0) return;
-    dist[seed] = 0;
-    q[0] = static_cast<int32_t>(seed);
-    qpre[0] = 0;
-    L->qc[0] = (1ULL << kDsCountShift) | static_cast<unsigned long long>(light_deg(off, light, seed));
+    if (seed >= 0) {                        // (a partitioned run's rank without the seed: empty queue)
+        dist[seed] = 0;
+        q[0] = static_cast<int32_t>(seed);
+        qpre[0] = 0;
+        L->qc[0] = (1ULL << kDsCountShift) | static_cast<unsigned long long>(light_deg(off, light, seed));
+    } else {
+        L->qc[0] = 0;
+    }
     L->qc[1] = 0;
     L->tm = kInf;
     L->lo = kInf;
@@ -436,12 +440,17 @@ __global__ void __launch_bounds__(kBlock) ds_commit_dev(const int32_t* __restric
 // or the current bucket for a vertex already pending — is appended to its bucket's pile
 // (bucket / nbins ring), the appends of a tile aggregated per pile in LDS (one atomic per
 // pile and tile).
-template <bool kBins>
+// kPart (1-D partition, not with kBins): the lists hold global ids; a target outside
+// [plo, plo + n_local) is min-reduced into rbest and marked in rmark for the owner (delta.hip).
+template <bool kBins, bool kPart = false>
 __global__ void __launch_bounds__(kBlock) ds_relax_dev(const int64_t* __restrict__ off, const int32_t* __restrict__ adj,
         const int32_t* __restrict__ wt, const int64_t* __restrict__ light, const int32_t* __restrict__ q,
         const int64_t* __restrict__ qpre, const int64_t* __restrict__ msg, int64_t* __restrict__ dist,
         uint64_t* __restrict__ pend, int32_t* __restrict__ qn, int64_t* __restrict__ qpre_n, DsLoop* L, int cur,
-        int64_t delta, int nbins, int32_t* __restrict__ pile, int64_t cap, const uint64_t* __restrict__ done) {
+        int64_t delta, int nbins, int32_t* __restrict__ pile, int64_t cap, const uint64_t* __restrict__ done,
+        int64_t plo = 0, int64_t n_local = 0, int64_t* __restrict__ rbest = nullptr,
+        uint64_t* __restrict__ rmark = nullptr) {
+    static_assert(!(kBins && kPart), "the partitioned loop has no piles");
     const unsigned long long c = L->qc[cur];
     const int64_t qlen = qcount(c), total = qentries(c);
     if (qlen == 0) return;                                   // grid-uniform
@@ -519,7 +528,7 @@ __global__ void __launch_bounds__(kBlock) ds_relax_dev(const int64_t* __restrict
             mu[k] = msg[u[k]];
             du[k] = dist[u[k]];
         }
-        int64_t cand[kEdgesPerThread], dt[kEdgesPerThread];
+        int64_t cand[kEdgesPerThread], dt[kEdgesPerThread], tl[kEdgesPerThread];
         uint64_t dw[kEdgesPerThread];
         if (kBins) {
 #pragma unroll
@@ -535,7 +544,13 @@ __global__ void __launch_bounds__(kBlock) ds_relax_dev(const int64_t* __restrict
             // a done target's distance is below every candidate of a later bucket: no read
             if (kBins && ((dw[k] >> (t[k] & 63)) & 1ULL)) continue;
             cand[k] = mu[k] + static_cast<int64_t>(w[k]);
-            dt[k] = dist[t[k]];
+            if (kPart) {
+                tl[k] = static_cast<int64_t>(t[k]) - plo;
+                dt[k] = (tl[k] >= 0 && tl[k] < n_local) ? dist[tl[k]] : rbest[t[k]];
+            } else {
+                tl[k] = t[k];
+                dt[k] = dist[t[k]];
+            }
         }
         int32_t tv[kEdgesPerThread];
         int64_t td[kEdgesPerThread];
@@ -549,7 +564,16 @@ __global__ void __launch_bounds__(kBlock) ds_relax_dev(const int64_t* __restrict
             td[k] = 0;
             fb[k] = -1;
             if (cand[k] < 0 || cand[k] >= dt[k]) continue;    // a stale (larger) read only costs an atomic
-            const int32_t tk = t[k];
+            if (kPart && !(tl[k] >= 0 && tl[k] < n_local)) {  // a remote target: best sent so far
+                const int64_t g = t[k];
+                const long long rold = atomicMin(reinterpret_cast<long long*>(&rbest[g]), static_cast<long long>(cand[k]));
+                if (cand[k] < rold) {
+                    const uint64_t rbit = 1ULL << (g & 63);
+                    if (!(rmark[g >> 6] & rbit)) atomicOr(reinterpret_cast<unsigned long long*>(&rmark[g >> 6]), rbit);
+                }
+                continue;
+            }
+            const int32_t tk = static_cast<int32_t>(tl[k]);
             const long long old = atomicMin(reinterpret_cast<long long*>(&dist[tk]), static_cast<long long>(cand[k]));
             if (cand[k] >= old) continue;
             const uint64_t bit = 1ULL << (tk & 63);
@@ -609,6 +633,88 @@ __global__ void __launch_bounds__(kBlock) ds_relax_dev(const int64_t* __restrict
     }
     const long long m = block_min(tmin);
     if (threadIdx.x == 0 && m != kInf) atomicMin(&L->tm, m);
+}
+
+// ---------------------------------------------------------------- 1-D partition
+// The partitioned loop (part_driver.cpp tgo_part_sssp_run over api.cpp's part_sssp_dev_*) runs
+// this file's commit / relax / extraction on each rank's rows; the decisions are global, so
+// they come from the host after the per-phase header exchange instead of ds_decide.
+//
+// Owner side of the exchange: min the received (local id, distance) pairs into dist; a newly
+// pending one below the threshold joins the next near queue (packed reservation), any other
+// improvement folds into tm.
+__global__ void __launch_bounds__(kBlock) ds_part_apply(const int64_t* __restrict__ recv, int64_t npairs,
+        const int64_t* __restrict__ off, const int64_t* __restrict__ light, int64_t* __restrict__ dist,
+        uint64_t* __restrict__ pend, int32_t* __restrict__ qn, int64_t* __restrict__ qpre_n, DsLoop* L, int cur) {
+    const int64_t thr = L->thr;
+    long long tmin = kInf;
+    for (int64_t base = static_cast<int64_t>(blockIdx.x) * kBlock; base < npairs;
+         base += static_cast<int64_t>(gridDim.x) * kBlock) {                 // block-uniform trips
+        const int64_t i = base + threadIdx.x;
+        bool take = false;
+        int64_t v = 0, deg = 0;
+        if (i < npairs) {
+            v = recv[2 * i];
+            const long long cand = recv[2 * i + 1];
+            if (cand < dist[v]) {
+                const long long old = atomicMin(reinterpret_cast<long long*>(&dist[v]), cand);
+                if (cand < old) {
+                    const uint64_t bit = 1ULL << (v & 63);
+                    const unsigned long long ob = atomicOr(reinterpret_cast<unsigned long long*>(&pend[v >> 6]), bit);
+                    if (!(ob & bit) && cand < thr) {
+                        take = true;
+                        deg = light_deg(off, light, v);
+                    } else if (cand < tmin) {
+                        tmin = cand;
+                    }
+                }
+            }
+        }
+        int64_t slot, doff;
+        block_reserve(&L->qc[cur ^ 1], take ? 1 : 0, deg, slot, doff);
+        if (take) {
+            qn[slot] = static_cast<int32_t>(v);
+            qpre_n[slot] = doff;
+        }
+    }
+    const long long m = block_min(tmin);
+    if (threadIdx.x == 0 && m != kInf) atomicMin(&L->tm, m);
+}
+
+// The global decision of an empty phase (host: every near queue empty): extract below thr.
+__global__ void ds_part_decide(DsLoop* L, int64_t thr) {
+    if (threadIdx.x != 0) return;
+    if (thr > L->thr) L->buckets += 1;
+    L->thr = thr;
+    L->tm = kInf;
+    L->lo = kInf;
+    L->members = 0;
+    L->extract = 1;
+    L->extractions += 1;
+}
+
+// The exchange header (delta.hip ds_mark_sizes for this loop): offs[r] = the pack offset of
+// rank r's pairs; to r {pair elements, near-queue length, min(tm, lo), members}.  Zeroes the
+// counts for the next phase and the pack's cursors.
+__global__ void ds_part_header(unsigned long long* __restrict__ counts, int nranks, const DsLoop* L, int cur,
+                               unsigned long long* __restrict__ offs, unsigned long long* __restrict__ cursor,
+                               int64_t* __restrict__ sizes) {
+    if (threadIdx.x != 0) return;
+    const int64_t qlen = qcount(L->qc[cur]);
+    const long long pm = L->tm < L->lo ? L->tm : L->lo;
+    const int64_t mem = L->members ? 1 : 0;
+    unsigned long long acc = 0;
+    for (int r = 0; r < nranks; ++r) {
+        const unsigned long long c = counts[r];
+        offs[r] = acc;
+        acc += c;
+        sizes[4 * r] = 2 * static_cast<int64_t>(c);
+        sizes[4 * r + 1] = qlen;
+        sizes[4 * r + 2] = pm;
+        sizes[4 * r + 3] = mem;
+        counts[r] = 0;
+        cursor[r] = 0;
+    }
 }
 
 // The pull form of a large finished bucket's heavy entries: a vertex that can still improve
@@ -761,6 +867,38 @@ hipError_t k_ds_loop_step(const DevCsr& ws, const int64_t* light, uint64_t* pend
     ds_commit_dev<false><<<1024, kBlock, 0, s>>>(q[cur], dist, msg, pend, member, L, cur, nullptr);
     ds_relax_dev<false><<<256 * 8, kBlock, 0, s>>>(ws.off, ws.adj, ws.w, light, q[cur], qpre[cur], msg, dist, pend,
                                                    q[cur ^ 1], qpre[cur ^ 1], L, cur, delta, 0, nullptr, 0, nullptr);
+    return hipGetLastError();
+}
+
+hipError_t k_ds_part_relax(const DevCsr& ws, const int64_t* light, uint64_t* pend, uint64_t* member, int64_t* dist,
+                           int64_t* msg, int32_t* const q[2], int64_t* const qpre[2], DsLoop* L, int cur, int64_t delta,
+                           int64_t lo, int64_t n_local, int64_t* rbest, uint64_t* rmark, hipStream_t s) {
+    static const int cg = static_cast<int>(env_i64_dl("TGO_DS_CGRID", 1024));
+    ds_commit_dev<false><<<cg, kBlock, 0, s>>>(q[cur], dist, msg, pend, member, L, cur, nullptr);
+    ds_relax_dev<false, true><<<256 * 8, kBlock, 0, s>>>(ws.off, ws.adj, ws.w, light, q[cur], qpre[cur], msg, dist, pend,
+                                                         q[cur ^ 1], qpre[cur ^ 1], L, cur, delta, 0, nullptr, 0,
+                                                         nullptr, lo, n_local, rbest, rmark);
+    return hipGetLastError();
+}
+hipError_t k_ds_part_header(unsigned long long* counts, int nranks, const DsLoop* L, int cur, unsigned long long* offs,
+                            unsigned long long* cursor, int64_t* sizes, hipStream_t s) {
+    ds_part_header<<<1, 64, 0, s>>>(counts, nranks, L, cur, offs, cursor, sizes);
+    return hipGetLastError();
+}
+hipError_t k_ds_part_apply(const int64_t* recv, int64_t npairs, const DevCsr& ws, const int64_t* light, int64_t* dist,
+                           uint64_t* pend, int32_t* const q[2], int64_t* const qpre[2], DsLoop* L, int cur, hipStream_t s) {
+    if (npairs <= 0) return hipSuccess;
+    const int64_t g = std::min<int64_t>(4096, (npairs + kBlock - 1) / kBlock);
+    ds_part_apply<<<static_cast<int>(g), kBlock, 0, s>>>(recv, npairs, ws.off, light, dist, pend, q[cur ^ 1],
+                                                         qpre[cur ^ 1], L, cur);
+    return hipGetLastError();
+}
+hipError_t k_ds_part_extract(const DevCsr& ws, const int64_t* light, uint64_t* pend, uint64_t* member, int64_t n,
+                             int64_t* dist, int32_t* const q[2], int64_t* const qpre[2], DsLoop* L, int cur, int64_t thr,
+                             hipStream_t s) {
+    ds_part_decide<<<1, 64, 0, s>>>(L, thr);
+    const int64_t words = (n + 63) / 64;
+    ds_extract_dev<<<extract_grid(words), kBlock, 0, s>>>(ws.off, light, pend, member, n, dist, L, cur, q[cur], qpre[cur]);
     return hipGetLastError();
 }
 

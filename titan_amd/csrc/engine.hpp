@@ -655,6 +655,19 @@ hipError_t k_ds_loop_seed(const DevCsr& ws, const int64_t* light, int64_t* dist,
 hipError_t k_ds_loop_step(const DevCsr& ws, const int64_t* light, uint64_t* pend, uint64_t* member, int64_t n,
                           int64_t* dist, int64_t* msg, int32_t* const q[2], int64_t* const qpre[2], DsLoop* L, int cur,
                           int64_t delta, hipStream_t s);
+// the partitioned device loop (delta_loop.hip, 1-D partition section): commit + relax of queue
+// cur (remote targets to rbest / rmark), the exchange header, the owner-side apply into queue
+// cur ^ 1, and the extraction below thr after an empty global phase
+hipError_t k_ds_part_relax(const DevCsr& ws, const int64_t* light, uint64_t* pend, uint64_t* member, int64_t* dist,
+                           int64_t* msg, int32_t* const q[2], int64_t* const qpre[2], DsLoop* L, int cur, int64_t delta,
+                           int64_t lo, int64_t n_local, int64_t* rbest, uint64_t* rmark, hipStream_t s);
+hipError_t k_ds_part_header(unsigned long long* counts, int nranks, const DsLoop* L, int cur, unsigned long long* offs,
+                            unsigned long long* cursor, int64_t* sizes, hipStream_t s);
+hipError_t k_ds_part_apply(const int64_t* recv, int64_t npairs, const DevCsr& ws, const int64_t* light, int64_t* dist,
+                           uint64_t* pend, int32_t* const q[2], int64_t* const qpre[2], DsLoop* L, int cur, hipStream_t s);
+hipError_t k_ds_part_extract(const DevCsr& ws, const int64_t* light, uint64_t* pend, uint64_t* member, int64_t n,
+                             int64_t* dist, int32_t* const q[2], int64_t* const qpre[2], DsLoop* L, int cur, int64_t thr,
+                             hipStream_t s);
 // Pull form of the heavy entries of a finished bucket with >= min_members members: every
 // vertex that can still improve reads its pull list (view) for heavy entries from those members
 // (bitmap pm[j & 1], list pl[j & 1]) instead of the members pushing them.  min_members <= 0: off.

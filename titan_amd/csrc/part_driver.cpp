@@ -324,6 +324,10 @@ int part_read_words(tgo_ctx* ctx, const int64_t* dev, int count, int64_t* out);
 int part_sssp_relax_dev(tgo_ctx* ctx, int64_t thr, int32_t nranks, int64_t* send, int64_t* sizes);
 int part_sssp_header_fold(tgo_ctx* ctx, const int64_t* own, const int64_t* recv, int nranks, int64_t* out);
 int part_sssp_split(tgo_ctx* ctx, int64_t delta, bool* on);
+bool part_sssp_devloop(const tgo_ctx* ctx);
+int part_sssp_dev_relax(tgo_ctx* ctx, int32_t nranks, int64_t* send, int64_t* sizes);
+int part_sssp_dev_apply(tgo_ctx* ctx, const int64_t* recv, int64_t npairs);
+int part_sssp_dev_extract(tgo_ctx* ctx, int64_t thr);
 double ms_split_of(const tgo_ctx* ctx);
 std::shared_ptr<void>& part_state_of(tgo_ctx* ctx);
 int part_in_list(tgo_ctx* ctx, const int32_t** adj, int64_t* nnz);
@@ -822,6 +826,8 @@ extern "C" int tgo_part_sssp_run(tgo_ctx* ctx, tgo_exchange* x, int64_t seed_glo
     bool split = false;
     if ((rc = part_sssp_split(ctx, delta, &split))) return rc;
     (void)split;
+    // on the device-sized loop (delta_loop.hip) nothing but the header comes to the host
+    const bool dev = part_sssp_devloop(ctx);
     int64_t thr = delta;
     int phases = 0;
     // per phase, ONE host read: the relax writes a 4-word header per peer on the device
@@ -837,7 +843,7 @@ extern "C" int tgo_part_sssp_run(tgo_ctx* ctx, tgo_exchange* x, int64_t seed_glo
     std::vector<size_t> sb(W), so(W), rb(W), ro(W);
     for (;;) {
         DevSpan span(st, "part.sssp.phase", {"phase", phases}, {"threshold", thr});
-        if ((rc = part_sssp_relax_dev(ctx, thr, W, send, sizes))) break;
+        if ((rc = dev ? part_sssp_dev_relax(ctx, W, send, sizes) : part_sssp_relax_dev(ctx, thr, W, send, sizes))) break;
         if (int r = x->all_to_all(sizes, hdr_recv, 32, st)) { rc = d.xfail(r); break; }
         if ((rc = part_sssp_header_fold(ctx, sizes, hdr_recv, W, fold))) break;
         if (nf <= 32) {                    // through the mapped counter page (up to 14 ranks)
@@ -849,7 +855,7 @@ extern "C" int tgo_part_sssp_run(tgo_ctx* ctx, tgo_exchange* x, int64_t seed_glo
             const int64_t mn = hf[2 * W + 1];
             if (mn == INT64_MAX && hf[2 * W + 2] == 0) break;   // converged: nothing pending, no members left
             if (mn != INT64_MAX && mn >= thr) thr = (mn / delta + 1) * delta;
-            if ((rc = tgo_part_sssp_extract(ctx, thr, nullptr))) break;
+            if ((rc = dev ? part_sssp_dev_extract(ctx, thr) : tgo_part_sssp_extract(ctx, thr, nullptr))) break;
             continue;
         }
         size_t a = 0, b = 0;
@@ -858,7 +864,8 @@ extern "C" int tgo_part_sssp_run(tgo_ctx* ctx, tgo_exchange* x, int64_t seed_glo
             rb[p] = static_cast<size_t>(hf[W + p]) * 8; ro[p] = b; b += rb[p];
         }
         if (int r = x->all_to_allv(send, sb.data(), so.data(), recv, rb.data(), ro.data(), st)) { rc = d.xfail(r); break; }
-        if ((rc = tgo_part_sssp_apply(ctx, thr, recv, static_cast<int64_t>(b / 16), nullptr))) break;
+        const int64_t np = static_cast<int64_t>(b / 16);
+        if ((rc = dev ? part_sssp_dev_apply(ctx, recv, np) : tgo_part_sssp_apply(ctx, thr, recv, np, nullptr))) break;
         ++phases;
     }
     trace_resolve(st);
