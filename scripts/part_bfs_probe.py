@@ -1,55 +1,56 @@
 #!/usr/bin/env python3
-"""Dev probe: one-GPU vs partitioned (world size 1, RCCL) BFS on RMAT bothE with the same
-roots — 64-source sweep and single-source per-root wall times, plus the partitioned
-driver's per-level host time split.  usage: MASTER_ADDR=127.0.0.1 MASTER_PORT=29514
-part_bfs_probe.py [scale]"""
+"""Partitioned single-source BFS at world 1 over RCCL (tgo_part_bfs_run, the native loop bench.py
+runs at N > 1) next to the one-GPU tgo_bfs on the same RMAT bothE graph: kernel ms per root,
+levels, and whether the levels agree.  Run under rocprofv3 --kernel-trace for the per-level
+protocol.  usage: part_bfs_probe.py [scale] [roots]"""
 import os
 import sys
 import time
 
 import numpy as np
 import torch
-import torch.distributed as dist
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 from titan_amd import Engine, pick_roots, rmat_edges  # noqa: E402
 from titan_amd import _lib as L  # noqa: E402
-from titan_amd import distributed as D  # noqa: E402
+from titan_amd.distributed import (HipPartBackend, InProcessGroup, NativeExchange,  # noqa: E402
+                                   distributed_bfs_native, local_layout)
 
 scale = int(sys.argv[1]) if len(sys.argv) > 1 else 24
+nroots = int(sys.argv[2]) if len(sys.argv) > 2 else 4
 n = 1 << scale
-torch.cuda.set_device(0)
-dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
-src, dst, _ = rmat_edges(scale, 16, seed=0x54495441)
+src, dst, _ = rmat_edges(scale, 16, seed=0x54495441, device=0)
 roots = [int(r) for r in pick_roots(n, src, dst, 64, seed=7)]
-lay = D.local_layout(src, dst, n, 0, n)
-st = D.exchange_stream()
-be = D.HipPartBackend(Engine(stream=st, host_threads=16).load_partition(n, 0, n, src, dst, L.SCOPE_BOTH_E,
-                                                                       apply_cap=False, layout=lay), n, 0, n,
-                      device_counts=True)
-one = Engine(host_threads=16).load_edges(n, src, dst, L.SCOPE_BOTH_E, apply_cap=False)
-
-
-def timed(fn, reps=3):
-    ts = []
-    for _ in range(reps):
+one = Engine(host_threads=16).load_edges(n, src, dst, L.SCOPE_BOTH_E)
+good, ref, t1 = [], {}, {}
+for r in roots:
+    d = one.bfs(r, n, L.SCOPE_BOTH_E, seed_is_dense=True, stats=True)
+    if one.stats()["reached"] * 4 >= n:
+        good.append(r)
+        one.bfs(r, n, L.SCOPE_BOTH_E, seed_is_dense=True, fetch=False)
+        ref[r] = d
+        t1[r] = one.stats()["last_kernel_ms"]
+        print(f"one-GPU root {r}: kernel {t1[r]:.3f} ms, levels {one.stats()['levels']}", flush=True)
+    if len(good) == nroots:
+        break
+del one
+st = torch.cuda.Stream()
+tp = {}
+with torch.cuda.stream(st):
+    lay = local_layout(src, dst, n, 0, n)
+    eng = Engine(stream=st.cuda_stream, host_threads=16).load_partition(n, 0, n, src, dst, L.SCOPE_BOTH_E, layout=lay)
+    be = HipPartBackend(eng, n, 0, n)
+    x = NativeExchange.rccl(0, comm=InProcessGroup(1).comm(0))
+    for r in good:
+        distributed_bfs_native(be, r, n, x, fetch=False, stats=False)            # warm
         torch.cuda.synchronize()
         t = time.perf_counter()
-        fn()
+        distributed_bfs_native(be, r, n, x, fetch=False, stats=False)
         torch.cuda.synchronize()
-        ts.append(time.perf_counter() - t)
-    return float(np.median(ts)) * 1e3
-
-
-print(f"msbfs sweep  one-GPU {timed(lambda: one.bfs_multi(roots, n, L.SCOPE_BOTH_E, seed_is_dense=True, fetch=False)):8.2f} ms"
-      f"   partitioned {timed(lambda: D.distributed_msbfs(be, roots, n, stats=False)):8.2f} ms", flush=True)
-t1 = np.mean([timed(lambda r=r: one.bfs(r, n, L.SCOPE_BOTH_E, seed_is_dense=True, fetch=False), 2) for r in roots[:16]])
-t2 = np.mean([timed(lambda r=r: D.distributed_bfs(be, r, n, fetch=False, stats=False), 2) for r in roots[:16]])
-print(f"single-source one-GPU {t1:8.3f} ms/root   partitioned {t2:8.3f} ms/root", flush=True)
-one.bfs(roots[0], n, L.SCOPE_BOTH_E, seed_is_dense=True, stats=True, fetch=False)
-print("one-GPU levels", one.stats()["levels"], flush=True)
-_, _, lv = D.distributed_bfs(be, roots[0], n, fetch=False, stats=False)
-print("partitioned levels", lv, flush=True)
-_, _, lv = D.distributed_msbfs(be, roots, n, stats=False)
-print("partitioned ms levels", lv, flush=True)
-dist.destroy_process_group()
+        ms = (time.perf_counter() - t) * 1e3
+        tp[r] = eng.stats()["last_kernel_ms"]
+        d, _, lv = distributed_bfs_native(be, r, n, x, fetch=True, stats=False)
+        print(f"partitioned world 1 root {r}: wall {ms:.3f} ms, kernel {tp[r]:.3f} ms, levels {lv}, "
+              f"equal one-GPU {bool(np.array_equal(d, ref[r]))}", flush=True)
+print(f"sum one-GPU {sum(t1.values()):.3f} ms, partitioned {sum(tp.values()):.3f} ms, "
+      f"ratio {sum(t1.values()) / sum(tp.values()):.3f}", flush=True)
