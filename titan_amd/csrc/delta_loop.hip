@@ -442,7 +442,9 @@ __global__ void __launch_bounds__(kBlock) ds_commit_dev(const int32_t* __restric
 // pile and tile).
 // kPart (1-D partition, not with kBins): the lists hold global ids; a target outside
 // [plo, plo + n_local) is min-reduced into rbest and marked in rmark for the owner (delta.hip).
-template <bool kBins, bool kPart = false>
+// kDone (binned loop with the done filter, TGO_DS_DONE): the done-word stage is compiled only
+// when it runs (its 8 words per thread cost the occupancy of the filter-off kernel).
+template <bool kBins, bool kPart = false, bool kDone = false>
 __global__ void __launch_bounds__(kBlock) ds_relax_dev(const int64_t* __restrict__ off, const int32_t* __restrict__ adj,
         const int32_t* __restrict__ wt, const int64_t* __restrict__ light, const int32_t* __restrict__ q,
         const int64_t* __restrict__ qpre, const int64_t* __restrict__ msg, int64_t* __restrict__ dist,
@@ -530,7 +532,7 @@ __global__ void __launch_bounds__(kBlock) ds_relax_dev(const int64_t* __restrict
         }
         int64_t cand[kEdgesPerThread], dt[kEdgesPerThread], tl[kEdgesPerThread];
         uint64_t dw[kEdgesPerThread];
-        if (kBins) {
+        if (kBins && kDone) {
 #pragma unroll
             for (int k = 0; k < kEdgesPerThread; ++k)         // 3a: done words (L2-resident bitmap)
                 dw[k] = (done && u[k] >= 0) ? done[t[k] >> 6] : 0ULL;
@@ -542,13 +544,12 @@ __global__ void __launch_bounds__(kBlock) ds_relax_dev(const int64_t* __restrict
             if (w[k] == kMissingWeight) { bad = true; continue; }     // edge.value(weight) on a missing key
             if (du[k] < mu[k]) continue;     // u improved during this phase: pending again, relaxes later
             // a done target's distance is below every candidate of a later bucket: no read
-            if (kBins && ((dw[k] >> (t[k] & 63)) & 1ULL)) continue;
+            if (kBins && kDone && ((dw[k] >> (t[k] & 63)) & 1ULL)) continue;
             cand[k] = mu[k] + static_cast<int64_t>(w[k]);
-            if (kPart) {
+            if constexpr (kPart) {
                 tl[k] = static_cast<int64_t>(t[k]) - plo;
                 dt[k] = (tl[k] >= 0 && tl[k] < n_local) ? dist[tl[k]] : rbest[t[k]];
             } else {
-                tl[k] = t[k];
                 dt[k] = dist[t[k]];
             }
         }
@@ -564,16 +565,19 @@ __global__ void __launch_bounds__(kBlock) ds_relax_dev(const int64_t* __restrict
             td[k] = 0;
             fb[k] = -1;
             if (cand[k] < 0 || cand[k] >= dt[k]) continue;    // a stale (larger) read only costs an atomic
-            if (kPart && !(tl[k] >= 0 && tl[k] < n_local)) {  // a remote target: best sent so far
-                const int64_t g = t[k];
-                const long long rold = atomicMin(reinterpret_cast<long long*>(&rbest[g]), static_cast<long long>(cand[k]));
-                if (cand[k] < rold) {
-                    const uint64_t rbit = 1ULL << (g & 63);
-                    if (!(rmark[g >> 6] & rbit)) atomicOr(reinterpret_cast<unsigned long long*>(&rmark[g >> 6]), rbit);
+            if constexpr (kPart) {
+                if (!(tl[k] >= 0 && tl[k] < n_local)) {       // a remote target: best sent so far
+                    const int64_t g = t[k];
+                    const long long rold = atomicMin(reinterpret_cast<long long*>(&rbest[g]), static_cast<long long>(cand[k]));
+                    if (cand[k] < rold) {
+                        const uint64_t rbit = 1ULL << (g & 63);
+                        if (!(rmark[g >> 6] & rbit)) atomicOr(reinterpret_cast<unsigned long long*>(&rmark[g >> 6]), rbit);
+                    }
+                    continue;
                 }
-                continue;
             }
-            const int32_t tk = static_cast<int32_t>(tl[k]);
+            int32_t tk = t[k];
+            if constexpr (kPart) tk = static_cast<int32_t>(tl[k]);
             const long long old = atomicMin(reinterpret_cast<long long*>(&dist[tk]), static_cast<long long>(cand[k]));
             if (cand[k] >= old) continue;
             const uint64_t bit = 1ULL << (tk & 63);
@@ -932,9 +936,13 @@ hipError_t k_ds_loop_step_bins(const DevCsr& ws, const int64_t* light, uint64_t*
                                                  nbins, pile, cap, pull);
         ds_pull_flip<<<1, 64, 0, s>>>(L);
     }
-    ds_relax_dev<true><<<rg, kBlock, 0, s>>>(ws.off, ws.adj, ws.w, light, q[cur], qpre[cur], msg, dist, pend,
-                                                  q[cur ^ 1], qpre[cur ^ 1], L, cur, delta, nbins, pile, cap,
-                                                  done_filter ? done : nullptr);
+    if (done_filter)
+        ds_relax_dev<true, false, true><<<rg, kBlock, 0, s>>>(ws.off, ws.adj, ws.w, light, q[cur], qpre[cur], msg, dist,
+                                                              pend, q[cur ^ 1], qpre[cur ^ 1], L, cur, delta, nbins, pile,
+                                                              cap, done);
+    else
+        ds_relax_dev<true><<<rg, kBlock, 0, s>>>(ws.off, ws.adj, ws.w, light, q[cur], qpre[cur], msg, dist, pend,
+                                                 q[cur ^ 1], qpre[cur ^ 1], L, cur, delta, nbins, pile, cap, nullptr);
     return hipGetLastError();
 }
 
