@@ -397,8 +397,39 @@ typedef enum {
     TGO_EDGE_SUB_WEIGHT = 4,  /* (m, e) -> m - w                */
     TGO_EDGE_MIN_WEIGHT = 5,  /* (m, e) -> min(m, w)            */
     TGO_EDGE_MAX_WEIGHT = 6,  /* (m, e) -> max(m, w)            */
-    TGO_EDGE_DIV_WEIGHT = 7   /* (m, e) -> m / w (Java / : int64 truncates, / 0 throws) */
+    TGO_EDGE_DIV_WEIGHT = 7,  /* (m, e) -> m / w (Java / : int64 truncates, / 0 throws) */
+    TGO_EDGE_PROGRAM = 8      /* (m, e) -> the ctx's edge-function program (below)       */
 } tgo_edge_fn;
+/* Edge-function programs: any composition of Java arithmetic over the message m, the weight
+ * w = e.value(weight) and constants — the BiFunction<M, Edge, M> of MessageScope.Local
+ * (VertexMemoryHandler.java:85,90) beyond the fixed menu, as a postfix program interpreted per
+ * entry on the device.  ops[i] = tgo_edge_op | (constant index << 8); a binary op pops b, then
+ * a, and pushes a op b.  Arithmetic is the message type's (Java long: + - * and negation wrap,
+ * / and % truncate, / 0 and % 0 throw -> TGO_E_PROGRAM, MIN_VALUE / -1 = MIN_VALUE; Java double:
+ * IEEE, % = fmod, min / max / abs as Math.min / max / abs).  The constants come in both types
+ * (iconsts for long messages, fconsts for double ones; NULL: the program cannot run on that
+ * type).  At most TGO_EDGE_PROGRAM_MAX_OPS ops, TGO_EDGE_PROGRAM_MAX_CONSTS constants and a
+ * stack of TGO_EDGE_PROGRAM_MAX_STACK; the program must leave exactly one value.  A program
+ * that pushes w fails on an edge without the weight property like the menu's weight functions,
+ * and with long messages needs an integral weight key. */
+typedef enum {
+    TGO_OP_MSG = 0, TGO_OP_WEIGHT = 1, TGO_OP_CONST = 2,
+    TGO_OP_ADD = 3, TGO_OP_SUB = 4, TGO_OP_MUL = 5, TGO_OP_DIV = 6, TGO_OP_REM = 7,
+    TGO_OP_MIN = 8, TGO_OP_MAX = 9, TGO_OP_NEG = 10, TGO_OP_ABS = 11
+} tgo_edge_op;
+#define TGO_EDGE_PROGRAM_MAX_OPS 32
+#define TGO_EDGE_PROGRAM_MAX_CONSTS 16
+#define TGO_EDGE_PROGRAM_MAX_STACK 8
+typedef struct {
+    int32_t n_ops;
+    const int32_t* ops;
+    int32_t n_consts;
+    const int64_t* iconsts;   /* n_consts long constants, or NULL                          */
+    const double* fconsts;    /* n_consts double constants, or NULL                        */
+} tgo_edge_program;
+/* Validates and stores the program on the ctx (NULL clears it); TGO_E_INVALID names the first
+ * bad op.  Host-only: no device work. */
+int  tgo_set_edge_program(tgo_ctx* ctx, const tgo_edge_program* prog);
 typedef struct {
     int32_t scope;            /* tgo_scope of the Local message scope                     */
     int32_t value_type;       /* tgo_value_type                                          */

@@ -124,6 +124,7 @@ def load() -> C.CDLL:
         "fr_pagerank": (C.c_int, [vp, C.c_double, C.c_int64, C.c_int, C.c_int, C.POINTER(C.c_double), P(C.c_int)]),
         "fr_degree_counter": (C.c_int, [vp, C.c_int, C.c_int, _i32p, P(C.c_int)]),
         "fr_gather": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, _u8p, vp, _u8p]),
+        "fr_set_edge_program": (C.c_int, [_i32p, C.c_int, _i64p, C.POINTER(C.c_double), C.c_int]),
         "fr_gather_lists": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, vp, _u8p, _i64p, vp]),
         "fr_combine_global": (C.c_int, [C.c_int64, C.c_int, C.c_int, C.c_int64, _i64p, vp, vp, _u8p]),
     }
@@ -230,6 +231,17 @@ def encode_vertex_exists(relation_id):
     out = C.string_at(b.p, b.len)
     lib.fr_buf_free(C.byref(b))
     return out, vp.value
+
+
+def set_edge_program(ops, iconsts=None, fconsts=None):
+    """fr_set_edge_program: the postfix edge-function program edge_fn 8 evaluates."""
+    o = np.ascontiguousarray(ops, np.int32)
+    nc = len(iconsts if iconsts is not None else (fconsts if fconsts is not None else []))
+    ic = None if iconsts is None else np.ascontiguousarray(iconsts, np.int64)
+    fc = None if fconsts is None else np.ascontiguousarray(fconsts, np.float64)
+    rc = load().fr_set_edge_program(_p(o, C.c_int32), len(o), _p(ic, C.c_int64), _p(fc, C.c_double), nc)
+    if rc:
+        raise RuntimeError(f"fr_set_edge_program rc={rc}")
 
 
 def combine_global(n, value_type, combiner, targets, values):

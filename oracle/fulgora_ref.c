@@ -1243,6 +1243,83 @@ static double edge_fn_d(int fn, double m, double x) {
     default: return m / x;
     }
 }
+/* Edge-function programs (edge_fn 8): the BiFunction<M, Edge, M> written as a postfix program
+ * over m, w = e.value(weight) and constants (the op codes of include/titan_gpu_olap.h
+ * tgo_edge_op).  Evaluated here in plain Java semantics, one entry at a time: long + - * and
+ * negation wrap, / and % truncate, / 0 and % 0 throw ArithmeticException, Long.MIN_VALUE / -1
+ * wraps to MIN_VALUE and % -1 gives 0, Math.abs(MIN_VALUE) = MIN_VALUE; double ops are IEEE,
+ * % is fmod, Math.min / Math.max / Math.abs with Java's NaN and signed-zero rules.  One program
+ * per process (fr_set_edge_program), set by the test before the gathers it checks. */
+static struct { int n, uses_w; int32_t ops[64]; int64_t ic[64]; double fc[64]; } g_prog;
+int fr_set_edge_program(const int32_t* ops, int n, const int64_t* iconsts, const double* fconsts, int nconsts) {
+    if (n < 1 || n > 64 || nconsts < 0 || nconsts > 64) return FR_E_INVALID;
+    g_prog.n = n; g_prog.uses_w = 0;
+    for (int i = 0; i < n; i++) { g_prog.ops[i] = ops[i]; if ((ops[i] & 0xFF) == 1) g_prog.uses_w = 1; }
+    for (int i = 0; i < nconsts; i++) {
+        g_prog.ic[i] = iconsts ? iconsts[i] : 0;
+        g_prog.fc[i] = fconsts ? fconsts[i] : 0.0;
+    }
+    return FR_OK;
+}
+static double java_min_d(double a, double b) {
+    if (a != a) return a;
+    if (a == 0.0 && b == 0.0 && signbit(b)) return b;
+    return a <= b ? a : b;
+}
+static double java_max_d(double a, double b) {
+    if (a != a) return a;
+    if (a == 0.0 && b == 0.0 && signbit(a)) return b;
+    return a >= b ? a : b;
+}
+/* 0 or FR_E_PROGRAM (an ArithmeticException) */
+static int prog_eval_i(int64_t m, int64_t w, int64_t* out) {
+    int64_t st[64]; int sp = 0;
+    for (int i = 0; i < g_prog.n; i++) {
+        int op = g_prog.ops[i] & 0xFF, arg = g_prog.ops[i] >> 8;
+        if (op == 0) { st[sp++] = m; continue; }
+        if (op == 1) { st[sp++] = w; continue; }
+        if (op == 2) { st[sp++] = g_prog.ic[arg]; continue; }
+        if (op == 10) { st[sp - 1] = (int64_t)(0u - (uint64_t)st[sp - 1]); continue; }
+        if (op == 11) { if (st[sp - 1] < 0) st[sp - 1] = (int64_t)(0u - (uint64_t)st[sp - 1]); continue; }
+        int64_t b = st[--sp], a = st[sp - 1], r;
+        switch (op) {
+        case 3: r = (int64_t)((uint64_t)a + (uint64_t)b); break;
+        case 4: r = (int64_t)((uint64_t)a - (uint64_t)b); break;
+        case 5: r = (int64_t)((uint64_t)a * (uint64_t)b); break;
+        case 6: if (b == 0) return FR_E_PROGRAM; r = b == -1 ? (int64_t)(0u - (uint64_t)a) : a / b; break;
+        case 7: if (b == 0) return FR_E_PROGRAM; r = b == -1 ? 0 : a % b; break;
+        case 8: r = a <= b ? a : b; break;
+        default: r = a >= b ? a : b; break;
+        }
+        st[sp - 1] = r;
+    }
+    *out = st[0];
+    return 0;
+}
+static double prog_eval_d(double m, double w) {
+    double st[64]; int sp = 0;
+    for (int i = 0; i < g_prog.n; i++) {
+        int op = g_prog.ops[i] & 0xFF, arg = g_prog.ops[i] >> 8;
+        if (op == 0) { st[sp++] = m; continue; }
+        if (op == 1) { st[sp++] = w; continue; }
+        if (op == 2) { st[sp++] = g_prog.fc[arg]; continue; }
+        if (op == 10) { st[sp - 1] = -st[sp - 1]; continue; }
+        if (op == 11) { st[sp - 1] = st[sp - 1] <= 0.0 ? 0.0 - st[sp - 1] : st[sp - 1]; continue; }
+        double b = st[--sp], a = st[sp - 1], r;
+        switch (op) {
+        case 3: r = a + b; break;
+        case 4: r = a - b; break;
+        case 5: r = a * b; break;
+        case 6: r = a / b; break;
+        case 7: r = fmod(a, b); break;
+        case 8: r = java_min_d(a, b); break;
+        default: r = java_max_d(a, b); break;
+        }
+        st[sp - 1] = r;
+    }
+    return st[0];
+}
+
 /* e.value(key) widened to double: a Float's / Double's IEEE bits, an integral value as is */
 static double weight_as_double(const fr_graph* g, int64_t w) {
     if (g->wdt == FR_DT_FLOAT) { int32_t b = (int32_t)w; float f; memcpy(&f, &b, 4); return (double)f; }
@@ -1254,13 +1331,19 @@ static double weight_as_double(const fr_graph* g, int64_t w) {
 static int entry_message(const fr_graph* g, int64_t k, int64_t o, int value_type, int edge_fn, const void* msg,
                          int64_t* mi_out, double* md_out) {
     int64_t w = 0;
-    if (edge_fn >= 2) {
+    const int needs_w = edge_fn == 8 ? g_prog.uses_w : edge_fn >= 2;
+    if (needs_w) {
         if (!g->has_w[k]) return FR_E_PROGRAM;                                 /* e.value(key) throws */
         w = g->w[k];
     }
     if (value_type == 0) {
-        if (edge_fn >= 2 && (g->wdt == FR_DT_FLOAT || g->wdt == FR_DT_DOUBLE)) return FR_E_INVALID;
+        if (needs_w && (g->wdt == FR_DT_FLOAT || g->wdt == FR_DT_DOUBLE)) return FR_E_INVALID;
+        if (edge_fn == 8) return prog_eval_i(((const int64_t*)msg)[o], w, mi_out) ? FR_E_PROGRAM : 1;
         return edge_fn_i(edge_fn, ((const int64_t*)msg)[o], w, mi_out) ? FR_E_PROGRAM : 1;
+    }
+    if (edge_fn == 8) {
+        *md_out = prog_eval_d(((const double*)msg)[o], needs_w ? weight_as_double(g, w) : 0.0);
+        return 1;
     }
     *md_out = edge_fn_d(edge_fn, ((const double*)msg)[o], edge_fn >= 2 ? weight_as_double(g, w) : 0.0);
     return 1;

@@ -168,6 +168,8 @@ int fr_pagerank(const fr_graph* g, double alpha, int64_t vertex_count, int max_i
 int fr_weight_datatype_ok(int datatype);
 int fr_gather_lists(const fr_graph* g, int scope, int value_type, int edge_fn, const void* msg, const uint8_t* has,
                     int64_t* off, void* vals);
+/* edge_fn 8: the postfix program set here (op codes of tgo_edge_op; fulgora_ref.c prog_eval_*) */
+int fr_set_edge_program(const int32_t* ops, int n, const int64_t* iconsts, const double* fconsts, int nconsts);
 int fr_gather(const fr_graph* g, int scope, int value_type, int combiner, int edge_fn, const void* msg,
               const uint8_t* has, void* out, uint8_t* out_has);
 int fr_combine_global(int64_t n, int value_type, int combiner, int64_t nmsgs, const int64_t* targets,

@@ -32,6 +32,9 @@ class OracleEngine:
         h = np.ones(self.n, bool) if has is None else has
         return self.o.gather_lists(scope, value_type, edge_fn, msg, h)
 
+    def set_edge_program(self, ops, iconsts=None, fconsts=None):
+        fr.set_edge_program(ops, iconsts, fconsts)
+
     def combine_global(self, value_type, combiner, targets, values):
         return fr.combine_global(self.n, value_type, combiner, targets, values)
 

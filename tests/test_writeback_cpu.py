@@ -123,7 +123,7 @@ def test_missing_compute_keys_become_generic_keys():
     """getOrCreatePropertyKey with the default schema maker: an unknown compute key is created
     generic (dataType(Object.class), DefaultSchemaMaker.java:46-48) with the next schema id."""
     from titan_amd import GpuGraph
-    sd = {"edge_types": [{"type_id": lib.fr_schema_id(7, 1), "multiplicity": 0}], "property_keys": [[uprop(40), 3]]}
+    sd = {"edge_types": [{"type_id": lib.fr_schema_id(2, 7), "multiplicity": 0}], "property_keys": [[uprop(40), 3]]}
     g = GpuGraph(edges=(64, np.zeros(1, np.int32), np.ones(1, np.int32), None), schema=sd,
                  property_keys={"typed": (uprop(900), L.DT_LONG)})
     assert g.property_key("typed") == (uprop(900), L.DT_LONG)

@@ -41,6 +41,10 @@ COMBINE_SUM, COMBINE_MIN, COMBINE_MAX = 0, 1, 2
 VAL_INT64, VAL_FP64 = 0, 1
 EDGE_IDENTITY, EDGE_ADD_ONE, EDGE_ADD_WEIGHT, EDGE_MUL_WEIGHT = 0, 1, 2, 3
 EDGE_SUB_WEIGHT, EDGE_MIN_WEIGHT, EDGE_MAX_WEIGHT, EDGE_DIV_WEIGHT = 4, 5, 6, 7
+EDGE_PROGRAM = 8
+# tgo_edge_op (edge-function programs, titan_amd/generic.py EdgeExpr)
+OP_MSG, OP_WEIGHT, OP_CONST, OP_ADD, OP_SUB, OP_MUL, OP_DIV, OP_REM, OP_MIN, OP_MAX, OP_NEG, OP_ABS = range(12)
+EDGE_PROGRAM_MAX_OPS, EDGE_PROGRAM_MAX_CONSTS, EDGE_PROGRAM_MAX_STACK = 32, 16, 8
 
 _i64p = C.POINTER(C.c_int64)
 _i32p = C.POINTER(C.c_int32)
@@ -125,6 +129,11 @@ class GatherArgs(C.Structure):
     _fields_ = [("scope", C.c_int32), ("value_type", C.c_int32), ("combiner", C.c_int32), ("edge_fn", C.c_int32)]
 
 
+class EdgeProgram(C.Structure):
+    _fields_ = [("n_ops", C.c_int32), ("ops", C.POINTER(C.c_int32)), ("n_consts", C.c_int32),
+                ("iconsts", C.POINTER(C.c_int64)), ("fconsts", C.POINTER(C.c_double))]
+
+
 class Stats(C.Structure):
     _fields_ = [("num_vertices", C.c_int64), ("out_entries", C.c_int64), ("in_entries", C.c_int64), ("ghost_vertices", C.c_int64),
                 ("truncated_results", C.c_int64), ("skipped_rows", C.c_int64), ("iterations", C.c_int32),
@@ -143,7 +152,7 @@ EXPORTS = [
     "tgo_bfs_multi", "tgo_copy_multi_distances", "tgo_multi_stats", "tgo_set_tuning",
     "tgo_trace_enable", "tgo_trace_flush", "tgo_trace_clear", "tgo_trace_range_push", "tgo_trace_range_pop",
     "tgo_gather", "tgo_combine_global", "tgo_dense_ids", "tgo_decode_edge_entry", "tgo_result_rows",
-    "tgo_gather_lists", "tgo_result_rows_values",
+    "tgo_gather_lists", "tgo_result_rows_values", "tgo_set_edge_program",
     "tgo_rmat_edges", "tgo_rmat_edges_device", "tgo_rmat_partition_device", "tgo_pick_roots", "tgo_synth_rows",
     # titan_gpu_olap_part.h (1-D vertex-partitioned multi-GPU)
     "tgo_load_partition", "tgo_part_layout", "tgo_load_partition_layout", "tgo_part_bfs_begin", "tgo_part_bfs_td", "tgo_part_bfs_claim", "tgo_part_bfs_bu",
@@ -213,6 +222,7 @@ def load() -> C.CDLL:
         "tgo_trace_range_pop": (C.c_int, []),
         "tgo_gather": (C.c_int, [vp, P(GatherArgs), vp, P(C.c_uint8), vp, P(C.c_uint8)]),
         "tgo_gather_lists": (C.c_int, [vp, P(GatherArgs), vp, P(C.c_uint8), _i64p, vp]),
+        "tgo_set_edge_program": (C.c_int, [vp, P(EdgeProgram)]),
         "tgo_result_rows_values": (C.c_int, [vp, P(ResultArgs), vp, P(C.c_uint8), P(ResultSize), P(RowsBuf)]),
         "tgo_combine_global": (C.c_int, [vp, C.c_int32, C.c_int32, C.c_int64, _i64p, vp, vp, P(C.c_uint8)]),
         "tgo_dense_ids": (C.c_int, [vp, _i64p, C.c_int64, _i64p]),

@@ -65,6 +65,7 @@ struct tgo_ctx {
     int64_t part_seed = -1;     // partitioned SSSP: the seed's internal id when owned here
     bool part_split = false;    // partitioned SSSP run on the light/heavy split (part_sssp_split)
     bool part_devloop = false;  // ... and on the device-sized loop (delta_loop.hip, part_sssp_dev_*)
+    EdgeProg edge_prog;         // tgo_set_edge_program (TGO_EDGE_PROGRAM gathers)
     int64_t pv_max_out = 0, pv_max_in = 0;   // largest OUT / IN list of a vertex cut
     std::vector<int64_t> pv_rows;            // row ids of the vertex cuts
     // last finished program whose compute keys tgo_result_rows can encode (-1 = none)
@@ -3165,7 +3166,47 @@ static int generic_alloc(tgo_ctx* ctx) {
     return TGO_OK;
 }
 
-static bool weight_edge_fn(int fn) { return fn >= TGO_EDGE_ADD_WEIGHT && fn <= TGO_EDGE_DIV_WEIGHT; }
+// Whether the gather's edge function reads e.value(weight).
+static bool weight_edge_fn(const tgo_ctx* ctx, int fn) {
+    return (fn >= TGO_EDGE_ADD_WEIGHT && fn <= TGO_EDGE_DIV_WEIGHT) || (fn == TGO_EDGE_PROGRAM && ctx->edge_prog.uses_w);
+}
+
+// Validate a postfix edge-function program (stack effects, constant indices, one result).
+int tgo_set_edge_program(tgo_ctx* ctx, const tgo_edge_program* p) {
+    if (!ctx) return TGO_E_INVALID;
+    if (!p) { ctx->edge_prog = EdgeProg(); return TGO_OK; }
+    if (p->n_ops < 1 || p->n_ops > TGO_EDGE_PROGRAM_MAX_OPS || !p->ops)
+        return fail(ctx, TGO_E_INVALID, "edge program: 1 to " + std::to_string(TGO_EDGE_PROGRAM_MAX_OPS) + " ops");
+    if (p->n_consts < 0 || p->n_consts > TGO_EDGE_PROGRAM_MAX_CONSTS || (p->n_consts > 0 && !p->iconsts && !p->fconsts))
+        return fail(ctx, TGO_E_INVALID, "edge program: 0 to " + std::to_string(TGO_EDGE_PROGRAM_MAX_CONSTS) +
+                                        " constants, long and / or double values");
+    EdgeProg pg;
+    int depth = 0;
+    for (int i = 0; i < p->n_ops; ++i) {
+        const int op = p->ops[i] & 0xFF, arg = p->ops[i] >> 8;
+        const std::string at = "edge program op " + std::to_string(i) + ": ";
+        if (op < TGO_OP_MSG || op > TGO_OP_ABS) return fail(ctx, TGO_E_INVALID, at + "unknown op");
+        if (op != TGO_OP_CONST && arg != 0) return fail(ctx, TGO_E_INVALID, at + "only CONST takes an argument");
+        if (op == TGO_OP_CONST && (arg < 0 || arg >= p->n_consts)) return fail(ctx, TGO_E_INVALID, at + "constant index");
+        const int pops = op <= TGO_OP_CONST ? 0 : op >= TGO_OP_NEG ? 1 : 2;
+        if (depth < pops) return fail(ctx, TGO_E_INVALID, at + "stack underflow");
+        depth += (op <= TGO_OP_CONST ? 1 : op >= TGO_OP_NEG ? 0 : -1);
+        if (depth > TGO_EDGE_PROGRAM_MAX_STACK) return fail(ctx, TGO_E_INVALID, at + "stack deeper than " +
+                                                            std::to_string(TGO_EDGE_PROGRAM_MAX_STACK));
+        if (op == TGO_OP_WEIGHT) pg.uses_w = 1;
+        pg.ops[i] = p->ops[i];
+    }
+    if (depth != 1) return fail(ctx, TGO_E_INVALID, "edge program must leave exactly one value");
+    pg.n = p->n_ops;
+    pg.has_i = p->n_consts == 0 || p->iconsts;
+    pg.has_f = p->n_consts == 0 || p->fconsts;
+    for (int i = 0; i < p->n_consts; ++i) {
+        if (p->iconsts) pg.ic[i] = p->iconsts[i];
+        if (p->fconsts) pg.fc[i] = p->fconsts[i];
+    }
+    ctx->edge_prog = pg;
+    return TGO_OK;
+}
 
 // Scope, value type, combiner (when used) and edge function of a Local receive.
 static int check_gather_args(tgo_ctx* ctx, const tgo_gather_args* a, bool combiner) {
@@ -3175,11 +3216,17 @@ static int check_gather_args(tgo_ctx* ctx, const tgo_gather_args* a, bool combin
     if (a->scope != ctx->g.scope && ctx->g.scope != TGO_SCOPE_BOTH_E)
         return fail(ctx, TGO_E_INVALID, "message scope differs from the scope the graph was loaded (preloaded) for");
     if (a->value_type < 0 || a->value_type > 1 || (combiner && (a->combiner < 0 || a->combiner > 2)) ||
-        a->edge_fn < TGO_EDGE_IDENTITY || a->edge_fn > TGO_EDGE_DIV_WEIGHT)
+        a->edge_fn < TGO_EDGE_IDENTITY || a->edge_fn > TGO_EDGE_PROGRAM)
         return fail(ctx, TGO_E_INVALID, "invalid value type, combiner or edge function");
-    if (weight_edge_fn(a->edge_fn) && !ctx->g.has_weight)
+    if (a->edge_fn == TGO_EDGE_PROGRAM) {
+        const EdgeProg& pg = ctx->edge_prog;
+        if (pg.n == 0) return fail(ctx, TGO_E_STATE, "TGO_EDGE_PROGRAM without a program (tgo_set_edge_program)");
+        if (a->value_type == TGO_VAL_INT64 ? !pg.has_i : !pg.has_f)
+            return fail(ctx, TGO_E_INVALID, "the edge program has no constants of the message type");
+    }
+    if (weight_edge_fn(ctx, a->edge_fn) && !ctx->g.has_weight)
         return fail(ctx, TGO_E_INVALID, "weight edge function on a graph loaded without a weight property");
-    if (weight_edge_fn(a->edge_fn) && (ctx->g.weight_dt == TGO_DT_FLOAT || ctx->g.weight_dt == TGO_DT_DOUBLE) &&
+    if (weight_edge_fn(ctx, a->edge_fn) && (ctx->g.weight_dt == TGO_DT_FLOAT || ctx->g.weight_dt == TGO_DT_DOUBLE) &&
         a->value_type == TGO_VAL_INT64)
         return fail(ctx, TGO_E_INVALID, "a Float / Double weight needs fp64 messages (long op double is a double in Java)");
     return TGO_OK;
@@ -3217,7 +3264,7 @@ int tgo_gather(tgo_ctx* ctx, const tgo_gather_args* a, const void* msg, const ui
     HIP_TRY(hipMemsetAsync(s.cnt, 0, sizeof(Counters), st));
     HIP_TRY(k_to_internal(s.gv[0], s.gh[0], ctx->g.perm, s.gv[1], s.gh[1], n, st));
     HIP_TRY(k_local_gather(pull_view(ctx->g, a->scope), n, a->value_type, s.gv[1], s.gh[1], a->combiner, a->edge_fn,
-                           weight_col(ctx->g), s.gv[2], s.gh[2], &s.cnt->err, st));
+                           weight_col(ctx->g), ctx->edge_prog, s.gv[2], s.gh[2], &s.cnt->err, st));
     HIP_TRY(k_to_rows(s.gv[2], s.gh[2], ctx->g.perm, s.gv[0], s.gh[0], n, st));
     HIP_TRY(hipEventRecord(ctx->ev1, st));
     HIP_TRY(hipMemcpyAsync(out, s.gv[0], n * 8, hipMemcpyDeviceToHost, st));
@@ -3252,7 +3299,7 @@ int tgo_gather_lists(tgo_ctx* ctx, const tgo_gather_args* a, const void* msg, co
     // offsets: counts per row (s.gv[2] as int64 n+1), scanned into s.gv[0]
     int64_t* cnt = reinterpret_cast<int64_t*>(s.gv[2]);
     int64_t* off = reinterpret_cast<int64_t*>(s.gv[0]);
-    HIP_TRY(k_list_count(pull, g.perm, n, s.gh[1], a->edge_fn, cnt, &s.cnt->err, st));
+    HIP_TRY(k_list_count(pull, g.perm, n, s.gh[1], weight_edge_fn(ctx, a->edge_fn), cnt, &s.cnt->err, st));
     HIP_TRY(scan_exclusive_i64(s.cub_tmp, s.cub_bytes, cnt, off, n + 1, st));
     HIP_TRY(hipMemcpyAsync(row_offsets, off, (n + 1) * sizeof(int64_t), hipMemcpyDeviceToHost, st));
     if ((rc = read_counters(ctx))) return rc;
@@ -3278,7 +3325,8 @@ int tgo_gather_lists(tgo_ctx* ctx, const tgo_gather_args* a, const void* msg, co
     const uint32_t* col0 = !g.has_col ? nullptr : a->scope == TGO_SCOPE_OUT_E ? g.in.col : g.out.col;
     const uint32_t* col1 = !g.has_col || a->scope != TGO_SCOPE_BOTH_E ? nullptr : g.in.col;
     hipError_t e = k_list_fill_sort(pull, col0, col1, g.perm, inv, n,
-                                    a->value_type, s.gv[1], s.gh[1], a->edge_fn, wc, off, total, key_in, key_out,
+                                    a->value_type, s.gv[1], s.gh[1], a->edge_fn, wc, ctx->edge_prog, off, total,
+                                    key_in, key_out,
                                     val_in, val_out, s.sort_tmp, s.sort_bytes, &s.cnt->err, st);
     if (e == hipSuccess) e = hipMemcpyAsync(values, val_out, total * 8, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);

@@ -813,16 +813,26 @@ struct WeightCol {
     int kind = 0;
     const int64_t* wide = nullptr;
 };
+// An edge-function program (tgo_set_edge_program, validated on the host), handed to the gather
+// kernels by value: uniform across every lane, read through the kernel arguments.
+struct EdgeProg {
+    int32_t n = 0;                  // ops; 0 = none set
+    int32_t uses_w = 0;             // pushes e.value(weight)
+    int32_t has_i = 0, has_f = 0;   // long / double constants given
+    int32_t ops[TGO_EDGE_PROGRAM_MAX_OPS] = {};
+    int64_t ic[TGO_EDGE_PROGRAM_MAX_CONSTS] = {};
+    double fc[TGO_EDGE_PROGRAM_MAX_CONSTS] = {};
+};
 hipError_t k_local_gather(const View& pull, int64_t n, int value_type, const void* msg_int, const uint8_t* has_int,
-                          int comb, int fn, WeightCol wc, void* out_int, uint8_t* out_has_int, unsigned long long* err,
-                          hipStream_t s);
-hipError_t k_list_count(const View& pull, const int32_t* perm, int64_t n, const uint8_t* has_int, int fn,
+                          int comb, int fn, WeightCol wc, const EdgeProg& pg, void* out_int, uint8_t* out_has_int,
+                          unsigned long long* err, hipStream_t s);
+hipError_t k_list_count(const View& pull, const int32_t* perm, int64_t n, const uint8_t* has_int, bool needs_w,
                         int64_t* cnt, unsigned long long* err, hipStream_t s);
 hipError_t k_list_fill_sort(const View& pull, const uint32_t* col0, const uint32_t* col1, const int32_t* perm,
                             int32_t* inv, int64_t n, int value_type, const void* msg_int, const uint8_t* has_int,
-                            int fn, WeightCol wc, const int64_t* off_out, int64_t total, uint32_t* key_in,
-                            uint32_t* key_out, void* val_in, void* val_out, void*& tmp, size_t& tmp_bytes,
-                            unsigned long long* err, hipStream_t s);
+                            int fn, WeightCol wc, const EdgeProg& pg, const int64_t* off_out, int64_t total,
+                            uint32_t* key_in, uint32_t* key_out, void* val_in, void* val_out, void*& tmp,
+                            size_t& tmp_bytes, unsigned long long* err, hipStream_t s);
 hipError_t k_to_internal(const void* row8, const uint8_t* row1, const int32_t* perm, void* int8, uint8_t* int1,
                          int64_t n, hipStream_t s);
 hipError_t k_to_rows(const void* int8, const uint8_t* int1, const int32_t* perm, void* row8, uint8_t* row1, int64_t n,

@@ -47,7 +47,71 @@ __device__ __forceinline__ int64_t combine<int64_t>(int comb, int64_t acc, int64
 // 1 = an edge without the weight property (e.value() throws), 2 = int64 division by zero (Java
 // ArithmeticException).
 constexpr unsigned long long kErrNoWeight = 1, kErrDivZero = 2;
-__host__ __device__ __forceinline__ bool weight_fn(int fn) { return fn >= TGO_EDGE_ADD_WEIGHT && fn <= TGO_EDGE_DIV_WEIGHT; }
+__host__ __device__ __forceinline__ bool weight_fn(int fn, const EdgeProg& pg) {
+    return (fn >= TGO_EDGE_ADD_WEIGHT && fn <= TGO_EDGE_DIV_WEIGHT) || (fn == TGO_EDGE_PROGRAM && pg.uses_w);
+}
+
+// ---- edge-function programs (TGO_EDGE_PROGRAM): the postfix program interpreted per entry.
+// The program is uniform, so every lane takes the same branch at every op; the stack index is
+// uniform too.  Java long: + - * and negation wrap, / and % truncate toward zero (C's), / 0 and
+// % 0 throw (kErrDivZero), MIN_VALUE / -1 = MIN_VALUE, MIN_VALUE % -1 = 0, Math.abs(MIN_VALUE) =
+// MIN_VALUE.  Java double: IEEE; % is fmod; Math.min / max treat NaN and -0.0 as Java does.
+__device__ __forceinline__ int64_t prog_op(int op, int64_t a, int64_t b, unsigned long long* err) {
+    const uint64_t ua = static_cast<uint64_t>(a), ub = static_cast<uint64_t>(b);
+    switch (op) {
+        case TGO_OP_ADD: return static_cast<int64_t>(ua + ub);
+        case TGO_OP_SUB: return static_cast<int64_t>(ua - ub);
+        case TGO_OP_MUL: return static_cast<int64_t>(ua * ub);
+        case TGO_OP_DIV:
+            if (b == 0) { atomicOr(err, kErrDivZero); return 0; }
+            return b == -1 ? static_cast<int64_t>(0ULL - ua) : a / b;
+        case TGO_OP_REM:
+            if (b == 0) { atomicOr(err, kErrDivZero); return 0; }
+            return b == -1 ? 0 : a % b;
+        case TGO_OP_MIN: return b < a ? b : a;
+        default: return b > a ? b : a;                    // TGO_OP_MAX
+    }
+}
+__device__ __forceinline__ double prog_op(int op, double a, double b, unsigned long long*) {
+    switch (op) {
+        case TGO_OP_ADD: return a + b;
+        case TGO_OP_SUB: return a - b;
+        case TGO_OP_MUL: return a * b;
+        case TGO_OP_DIV: return a / b;
+        case TGO_OP_REM: return fmod(a, b);
+        case TGO_OP_MIN:                                   // Math.min(double, double)
+            if (a != a) return a;
+            if (a == 0.0 && b == 0.0 && signbit(b)) return b;
+            return a <= b ? a : b;
+        default:                                           // Math.max(double, double)
+            if (a != a) return a;
+            if (a == 0.0 && b == 0.0 && signbit(a)) return b;
+            return a >= b ? a : b;
+    }
+}
+__device__ __forceinline__ int64_t prog_neg(int64_t a) { return static_cast<int64_t>(0ULL - static_cast<uint64_t>(a)); }
+__device__ __forceinline__ double prog_neg(double a) { return -a; }
+__device__ __forceinline__ int64_t prog_abs(int64_t a) { return a < 0 ? prog_neg(a) : a; }
+__device__ __forceinline__ double prog_abs(double a) { return a <= 0.0 ? 0.0 - a : a; }    // Math.abs(double)
+__device__ __forceinline__ int64_t prog_const(const EdgeProg& pg, int i, int64_t) { return pg.ic[i]; }
+__device__ __forceinline__ double prog_const(const EdgeProg& pg, int i, double) { return pg.fc[i]; }
+template <typename T>
+__device__ __forceinline__ T run_prog(const EdgeProg& pg, T m, T w, unsigned long long* err) {
+    T st[TGO_EDGE_PROGRAM_MAX_STACK];
+    int sp = 0;
+    for (int i = 0; i < pg.n; ++i) {
+        const int op = pg.ops[i] & 0xFF;
+        switch (op) {
+            case TGO_OP_MSG: st[sp++] = m; break;
+            case TGO_OP_WEIGHT: st[sp++] = w; break;
+            case TGO_OP_CONST: st[sp++] = prog_const(pg, pg.ops[i] >> 8, T(0)); break;
+            case TGO_OP_NEG: st[sp - 1] = prog_neg(st[sp - 1]); break;
+            case TGO_OP_ABS: st[sp - 1] = prog_abs(st[sp - 1]); break;
+            default: st[sp - 2] = prog_op(op, st[sp - 2], st[sp - 1], err); --sp; break;
+        }
+    }
+    return st[0];
+}
 
 // e.value(weight) widened to double (double message): the value by the column's kind
 __device__ __forceinline__ double weight_f(int32_t w, const WeightCol& wc) {
@@ -58,8 +122,10 @@ __device__ __forceinline__ double weight_f(int32_t w, const WeightCol& wc) {
         default: return static_cast<double>(w);
     }
 }
-__device__ __forceinline__ double edge_apply_f(int fn, double m, int32_t w, const WeightCol& wc) {
+__device__ __forceinline__ double edge_apply_f(int fn, double m, int32_t w, const WeightCol& wc, const EdgeProg& pg,
+                                               unsigned long long* err) {
     if (fn == TGO_EDGE_IDENTITY) return m;
+    if (fn == TGO_EDGE_PROGRAM) return run_prog<double>(pg, m, pg.uses_w ? weight_f(w, wc) : 0.0, err);
     if (fn == TGO_EDGE_ADD_ONE) return m + 1.0;
     const double x = weight_f(w, wc);
     switch (fn) {
@@ -74,9 +140,11 @@ __device__ __forceinline__ double edge_apply_f(int fn, double m, int32_t w, cons
 // Java long arithmetic: + - * wrap, / truncates toward zero, MIN_VALUE / -1 = MIN_VALUE
 // (long message: the host admits integral columns only — an int or a Long)
 __device__ __forceinline__ int64_t edge_apply_i(int fn, int64_t m, int32_t w, const WeightCol& wc,
-                                                unsigned long long* err) {
+                                                const EdgeProg& pg, unsigned long long* err) {
     const uint64_t u = static_cast<uint64_t>(m);
     if (fn == TGO_EDGE_IDENTITY) return m;
+    if (fn == TGO_EDGE_PROGRAM)
+        return run_prog<int64_t>(pg, m, pg.uses_w ? (wc.kind == 2 ? wc.wide[w] : static_cast<int64_t>(w)) : 0, err);
     if (fn == TGO_EDGE_ADD_ONE) return static_cast<int64_t>(u + 1u);
     const int64_t x = wc.kind == 2 ? wc.wide[w] : static_cast<int64_t>(w);
     switch (fn) {
@@ -92,21 +160,21 @@ __device__ __forceinline__ int64_t edge_apply_i(int fn, int64_t m, int32_t w, co
     }
 }
 template <typename T> __device__ __forceinline__ T edge_apply(int fn, T m, int32_t w, const WeightCol& wc,
-                                                             unsigned long long* err);
+                                                             const EdgeProg& pg, unsigned long long* err);
 template <> __device__ __forceinline__ double edge_apply<double>(int fn, double m, int32_t w, const WeightCol& wc,
-                                                               unsigned long long*) {
-    return edge_apply_f(fn, m, w, wc);
+                                                               const EdgeProg& pg, unsigned long long* err) {
+    return edge_apply_f(fn, m, w, wc, pg, err);
 }
 template <> __device__ __forceinline__ int64_t edge_apply<int64_t>(int fn, int64_t m, int32_t w, const WeightCol& wc,
-                                                                 unsigned long long* err) {
-    return edge_apply_i(fn, m, w, wc, err);
+                                                                 const EdgeProg& pg, unsigned long long* err) {
+    return edge_apply_i(fn, m, w, wc, pg, err);
 }
 
 template <typename T>
 __global__ void local_gather(View pull, int64_t n, const T* __restrict__ msg, const uint8_t* __restrict__ has,
-                             int comb, int fn, WeightCol wc, T* __restrict__ out, uint8_t* __restrict__ out_has,
-                             unsigned long long* err) {
-    const bool needs_w = weight_fn(fn);
+                             int comb, int fn, WeightCol wc, EdgeProg pg, T* __restrict__ out,
+                             uint8_t* __restrict__ out_has, unsigned long long* err) {
+    const bool needs_w = weight_fn(fn, pg);
     for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x) {
         T acc = T(0);
         bool any = false;
@@ -122,7 +190,7 @@ __global__ void local_gather(View pull, int64_t n, const T* __restrict__ msg, co
                     wt = w ? w[k] : kMissingWeight;
                     if (wt == kMissingWeight) { atomicOr(err, kErrNoWeight); continue; }   // e.value(key) throws
                 }
-                const T m = edge_apply<T>(fn, msg[u], wt, wc, err);
+                const T m = edge_apply<T>(fn, msg[u], wt, wc, pg, err);
                 acc = any ? combine<T>(comb, acc, m) : m;
                 any = true;
             }
@@ -160,9 +228,9 @@ template <typename T>
 __global__ void list_fill(View pull, const uint32_t* __restrict__ col0, const uint32_t* __restrict__ col1,
                           const int32_t* __restrict__ perm, const int32_t* __restrict__ inv, int64_t n,
                           const T* __restrict__ msg, const uint8_t* __restrict__ has, int fn, WeightCol wc,
-                          const int64_t* __restrict__ off_out, uint32_t* __restrict__ key, T* __restrict__ val,
-                          unsigned long long* err) {
-    const bool needs_w = weight_fn(fn);
+                          EdgeProg pg, const int64_t* __restrict__ off_out, uint32_t* __restrict__ key,
+                          T* __restrict__ val, unsigned long long* err) {
+    const bool needs_w = weight_fn(fn, pg);
     for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
         const int64_t v = perm[r];
         int64_t p = off_out[r];
@@ -180,7 +248,7 @@ __global__ void list_fill(View pull, const uint32_t* __restrict__ col0, const ui
                     if (wt == kMissingWeight) continue;
                 }
                 key[p] = col ? col[k] : ((static_cast<uint32_t>(l) << 31) | static_cast<uint32_t>(inv[u]));
-                val[p] = edge_apply<T>(fn, msg[u], wt, wc, err);
+                val[p] = edge_apply<T>(fn, msg[u], wt, wc, pg, err);
                 ++p;
             }
         }
@@ -227,39 +295,39 @@ __global__ void iota_i64(int64_t* p, int64_t n) {
 }  // namespace
 
 hipError_t k_local_gather(const View& pull, int64_t n, int value_type, const void* msg_int, const uint8_t* has_int,
-                          int comb, int fn, WeightCol wc, void* out_int, uint8_t* out_has_int, unsigned long long* err,
-                          hipStream_t s) {
+                          int comb, int fn, WeightCol wc, const EdgeProg& pg, void* out_int, uint8_t* out_has_int,
+                          unsigned long long* err, hipStream_t s) {
     if (value_type == TGO_VAL_INT64)
         local_gather<int64_t><<<grid_for(n), kBlock, 0, s>>>(pull, n, static_cast<const int64_t*>(msg_int), has_int, comb,
-                                                            fn, wc, static_cast<int64_t*>(out_int), out_has_int, err);
+                                                            fn, wc, pg, static_cast<int64_t*>(out_int), out_has_int, err);
     else
         local_gather<double><<<grid_for(n), kBlock, 0, s>>>(pull, n, static_cast<const double*>(msg_int), has_int, comb,
-                                                           fn, wc, static_cast<double*>(out_int), out_has_int, err);
+                                                           fn, wc, pg, static_cast<double*>(out_int), out_has_int, err);
     return hipGetLastError();
 }
 
 // Combiner-less receive: counts per row (row order) into cnt[0..n], cnt[n] = 0.
-hipError_t k_list_count(const View& pull, const int32_t* perm, int64_t n, const uint8_t* has_int, int fn,
+hipError_t k_list_count(const View& pull, const int32_t* perm, int64_t n, const uint8_t* has_int, bool needs_w,
                         int64_t* cnt, unsigned long long* err, hipStream_t s) {
-    list_count<<<grid_for(n), kBlock, 0, s>>>(pull, perm, n, has_int, weight_fn(fn), cnt, err);
+    list_count<<<grid_for(n), kBlock, 0, s>>>(pull, perm, n, has_int, needs_w, cnt, err);
     return hipGetLastError();
 }
 // ... then the (key, value) pairs of every row at off_out[r], and a segmented sort of each
 // row by key into key_out / val_out.  inv: n int32 scratch (internal -> row).
 hipError_t k_list_fill_sort(const View& pull, const uint32_t* col0, const uint32_t* col1, const int32_t* perm,
                             int32_t* inv, int64_t n, int value_type, const void* msg_int, const uint8_t* has_int,
-                            int fn, WeightCol wc, const int64_t* off_out, int64_t total, uint32_t* key_in,
-                            uint32_t* key_out, void* val_in, void* val_out, void*& tmp, size_t& tmp_bytes,
-                            unsigned long long* err, hipStream_t s) {
+                            int fn, WeightCol wc, const EdgeProg& pg, const int64_t* off_out, int64_t total,
+                            uint32_t* key_in, uint32_t* key_out, void* val_in, void* val_out, void*& tmp,
+                            size_t& tmp_bytes, unsigned long long* err, hipStream_t s) {
     if (!col0) invert_perm<<<grid_for(n), kBlock, 0, s>>>(perm, inv, n);
     if (value_type == TGO_VAL_INT64)
         list_fill<int64_t><<<grid_for(n), kBlock, 0, s>>>(pull, col0, col1, perm, inv, n,
-                                                         static_cast<const int64_t*>(msg_int), has_int, fn, wc, off_out,
-                                                         key_in, static_cast<int64_t*>(val_in), err);
+                                                         static_cast<const int64_t*>(msg_int), has_int, fn, wc, pg,
+                                                         off_out, key_in, static_cast<int64_t*>(val_in), err);
     else
         list_fill<double><<<grid_for(n), kBlock, 0, s>>>(pull, col0, col1, perm, inv, n,
-                                                        static_cast<const double*>(msg_int), has_int, fn, wc, off_out,
-                                                        key_in, static_cast<double*>(val_in), err);
+                                                        static_cast<const double*>(msg_int), has_int, fn, wc, pg,
+                                                        off_out, key_in, static_cast<double*>(val_in), err);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || total == 0) return e;
     const uint64_t* vi = static_cast<const uint64_t*>(val_in);

@@ -303,6 +303,20 @@ class Engine:
                                                        L.ptr(out_has, C.c_uint8)))
         return out, out_has.astype(bool)
 
+    def set_edge_program(self, ops, iconsts=None, fconsts=None):
+        """tgo_set_edge_program: the postfix program TGO_EDGE_PROGRAM gathers evaluate (None clears
+        it).  ops: tgo_edge_op | const index << 8; iconsts / fconsts: the constants as Java long /
+        double (None: the program does not run on that message type)."""
+        if ops is None:
+            _check(self.lib, self.ctx, self.lib.tgo_set_edge_program(self.ctx, None))
+            return
+        o = np.ascontiguousarray(ops, dtype=np.int32)
+        ic = None if iconsts is None else np.ascontiguousarray(iconsts, dtype=np.int64)
+        fc = None if fconsts is None else np.ascontiguousarray(fconsts, dtype=np.float64)
+        nc = len(ic) if ic is not None else (len(fc) if fc is not None else 0)
+        p = L.EdgeProgram(len(o), L.ptr(o, C.c_int32), nc, L.ptr(ic, C.c_int64), L.ptr(fc, C.c_double))
+        _check(self.lib, self.ctx, self.lib.tgo_set_edge_program(self.ctx, C.byref(p)))
+
     def gather_lists(self, scope, value_type, edge_fn, msg, has=None):
         """MessageScope.Local receive WITHOUT a combiner (tgo_gather_lists): every vertex's
         message stream as (row offsets n+1, values) in the API's row order."""

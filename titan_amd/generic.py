@@ -25,7 +25,10 @@ at most one message per target, and two messages meeting at a target (or at a ve
 fail the job as FulgoraUtil's ThrowingCombiner does (FulgoraUtil.java:80-91).
 
 Edge functions are "message op w" over the load's weight property (any 32-bit numeric key:
-Byte, Short, Integer, Character, Boolean, Float): identity, +1, + - * / min max of w.
+Byte, Short, Integer, Character, Boolean, Float): identity, +1, + - * / min max of w — or any
+arithmetic composition of the message ``M``, the weight ``W`` and constants written as an
+``EdgeExpr`` (``MessageScope.Local("inE", M * 2 + W)``): compiled to a postfix program
+(tgo_set_edge_program) that the device evaluates per entry in Java arithmetic.
 TinkerPop's own TraversalVertexProgram (Gremlin OLAP traversals, BOTH preload at
 VertexProgramScanJob.java:101-107) is not restated: its tests live in the absent gremlin-test
 jar, so its results would be parity-unpinned.
@@ -42,14 +45,111 @@ EDGE_FNS = {"identity": L.EDGE_IDENTITY, "add_one": L.EDGE_ADD_ONE, "add_weight"
 INCIDENT = {"outE": L.SCOPE_OUT_E, "inE": L.SCOPE_IN_E, "bothE": L.SCOPE_BOTH_E}
 
 
+class EdgeExpr:
+    """An edge function (m, e) -> message as an arithmetic expression over the message ``M``,
+    the weight ``W`` = e.value(weight) and constants, in Java semantics for the message type
+    (long: wrapping + - *, truncating / and %, / 0 throws; double: IEEE, Math.min / max / abs).
+    ``compile()`` gives the postfix program of include/titan_gpu_olap.h tgo_edge_program.
+    Python ints and floats mix in: ``M * 2 + W``, ``(M - 1).min(W)``, ``abs(-M)``."""
+
+    def __init__(self, op, args=(), value=None):
+        self.op, self.args, self.value = op, tuple(args), value
+
+    @staticmethod
+    def lift(x):
+        if isinstance(x, EdgeExpr):
+            return x
+        if isinstance(x, bool) or not isinstance(x, (int, float)):
+            raise TypeError(f"edge expression operand must be an EdgeExpr, int or float: {x!r}")
+        return EdgeExpr(L.OP_CONST, value=x)
+
+    def _bin(self, op, other, swap=False):
+        o = EdgeExpr.lift(other)
+        return EdgeExpr(op, (o, self) if swap else (self, o))
+
+    def __add__(self, o): return self._bin(L.OP_ADD, o)
+    def __radd__(self, o): return self._bin(L.OP_ADD, o, True)
+    def __sub__(self, o): return self._bin(L.OP_SUB, o)
+    def __rsub__(self, o): return self._bin(L.OP_SUB, o, True)
+    def __mul__(self, o): return self._bin(L.OP_MUL, o)
+    def __rmul__(self, o): return self._bin(L.OP_MUL, o, True)
+    def __truediv__(self, o): return self._bin(L.OP_DIV, o)        # Java / (long: truncating)
+    def __rtruediv__(self, o): return self._bin(L.OP_DIV, o, True)
+    def __mod__(self, o): return self._bin(L.OP_REM, o)            # Java %
+    def __rmod__(self, o): return self._bin(L.OP_REM, o, True)
+    def __neg__(self): return EdgeExpr(L.OP_NEG, (self,))
+    def __abs__(self): return EdgeExpr(L.OP_ABS, (self,))
+    def min(self, o): return self._bin(L.OP_MIN, o)                # Math.min
+    def max(self, o): return self._bin(L.OP_MAX, o)                # Math.max
+
+    def compile(self):
+        """(ops, long constants, double constants); a constant that is not integral gives no
+        long form (the program then runs on double messages only)."""
+        ops, consts = [], []
+
+        def emit(e):
+            for a in e.args:
+                emit(a)
+            if e.op == L.OP_CONST:
+                v = e.value
+                if isinstance(v, int) and not -(1 << 63) <= v < (1 << 63):
+                    raise ValueError(f"edge expression constant out of long range: {v}")
+                # the same constant: same type and, for floats, the same bits (0.0 is not -0.0)
+                same = (lambda c: c == v) if isinstance(v, int) else (lambda c: float(c).hex() == float(v).hex())
+                i = next((k for k, c in enumerate(consts) if type(c) is type(v) and same(c)), None)
+                if i is None:
+                    consts.append(v)
+                    i = len(consts) - 1
+                ops.append(L.OP_CONST | (i << 8))
+            else:
+                ops.append(e.op)
+        emit(self)
+        if len(ops) > L.EDGE_PROGRAM_MAX_OPS or len(consts) > L.EDGE_PROGRAM_MAX_CONSTS:
+            raise ValueError(f"edge expression too large: {len(ops)} ops, {len(consts)} constants")
+        integral = all(isinstance(c, int) for c in consts)
+        ic = [int(c) for c in consts] if integral else None
+        fc = [float(c) for c in consts]
+        return ops, ic, fc
+
+    def key(self):
+        return (self.op, self.value, tuple(a.key() for a in self.args))
+
+    def __eq__(self, o):
+        return isinstance(o, EdgeExpr) and self.key() == o.key()
+
+    def __hash__(self):
+        return hash(self.key())
+
+    def __repr__(self):
+        names = {L.OP_ADD: "+", L.OP_SUB: "-", L.OP_MUL: "*", L.OP_DIV: "/", L.OP_REM: "%"}
+        if self.op == L.OP_MSG:
+            return "M"
+        if self.op == L.OP_WEIGHT:
+            return "W"
+        if self.op == L.OP_CONST:
+            return repr(self.value)
+        if self.op in names:
+            return f"({self.args[0]!r} {names[self.op]} {self.args[1]!r})"
+        if self.op == L.OP_NEG:
+            return f"-{self.args[0]!r}"
+        if self.op == L.OP_ABS:
+            return f"abs({self.args[0]!r})"
+        return f"{self.args[0]!r}.{'min' if self.op == L.OP_MIN else 'max'}({self.args[1]!r})"
+
+
+M = EdgeExpr(L.OP_MSG)      # the message the sender holds
+W = EdgeExpr(L.OP_WEIGHT)   # e.value(weight) of the traversed edge
+
+
 class MessageScope:
     class Local:
-        """MessageScope.Local.of(__::<incident>, edgeFunction)."""
+        """MessageScope.Local.of(__::<incident>, edgeFunction); edge_fn is a menu name or an
+        EdgeExpr."""
 
         def __init__(self, incident="inE", edge_fn="identity"):
             if incident not in INCIDENT:
                 raise ValueError(f"incident traversal must be outE, inE or bothE: {incident}")
-            if edge_fn not in EDGE_FNS:
+            if not isinstance(edge_fn, EdgeExpr) and edge_fn not in EDGE_FNS:
                 raise ValueError(f"unsupported edge function {edge_fn}")
             self.incident, self.edge_fn = incident, edge_fn
 
@@ -232,11 +332,12 @@ class Messenger:
         vals, has = self._prev[scope]
         if isinstance(scope, MessageScope.Global):
             return vals, has
+        fn = EDGE_FNS.get(scope.edge_fn) if not isinstance(scope.edge_fn, EdgeExpr) else L.EDGE_PROGRAM
+        if fn == L.EDGE_PROGRAM:
+            self._e.set_edge_program(*scope.edge_fn.compile())
         if self._p.combiner is None:
-            return MessageLists(*self._e.gather_lists(INCIDENT[scope.incident], self._p.value_type,
-                                                      EDGE_FNS[scope.edge_fn], vals, has))
-        return self._e.gather(INCIDENT[scope.incident], self._p.value_type, self._p.combiner, EDGE_FNS[scope.edge_fn],
-                              vals, has)
+            return MessageLists(*self._e.gather_lists(INCIDENT[scope.incident], self._p.value_type, fn, vals, has))
+        return self._e.gather(INCIDENT[scope.incident], self._p.value_type, self._p.combiner, fn, vals, has)
 
     def send(self, scope, values, has=None):
         """Local scope: every vertex with has[v] sends values[v] (setMessage on the sender,
