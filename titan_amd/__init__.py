@@ -11,8 +11,9 @@ from .computer import (  # noqa: F401
     ShortestDistanceVertexProgram, TitanGraphComputer,
 )
 from .generic import (  # noqa: F401
-    ComputeKeyMapReduce, FulgoraMemory, GenericVertexProgram, MessageScope, Messenger, Vertices,
+    ComputeKeyMapReduce, EdgeExpr, FulgoraMemory, GenericVertexProgram, MessageScope, Messenger, Vertices,
 )
+from .traversal import TraversalVertexProgram  # noqa: F401
 from . import _lib  # noqa: F401
 
 __all__ = [
@@ -20,5 +21,5 @@ __all__ = [
     "ExecutionException", "GpuGraph", "GpuGraphComputer", "KeyValue", "PageRankMapReduce",
     "PageRankVertexProgram", "ShortestDistanceMapReduce", "ShortestDistanceVertexProgram",
     "TitanGraphComputer", "ComputeKeyMapReduce", "FulgoraMemory", "GenericVertexProgram", "MessageScope",
-    "Messenger", "Vertices",
+    "Messenger", "Vertices", "EdgeExpr", "TraversalVertexProgram",
 ]

@@ -29,9 +29,10 @@ Byte, Short, Integer, Character, Boolean, Float): identity, +1, + - * / min max 
 arithmetic composition of the message ``M``, the weight ``W`` and constants written as an
 ``EdgeExpr`` (``MessageScope.Local("inE", M * 2 + W)``): compiled to a postfix program
 (tgo_set_edge_program) that the device evaluates per entry in Java arithmetic.
-TinkerPop's own TraversalVertexProgram (Gremlin OLAP traversals, BOTH preload at
-VertexProgramScanJob.java:101-107) is not restated: its tests live in the absent gremlin-test
-jar, so its results would be parity-unpinned.
+TinkerPop's TraversalVertexProgram (Gremlin OLAP traversals, BOTH preload at
+VertexProgramScanJob.java:101-107) is restated for vertex-step traversals in
+titan_amd/traversal.py (a program with ``preload = bothE``); its own tests live in the absent
+gremlin-test jar, so it is pinned against walk-count closed forms instead.
 """
 from __future__ import annotations
 
@@ -416,7 +417,11 @@ class GenericVertexProgram:
 
 def preload_scope(program, probe_memory_iterations=1):
     """The single preload a program's Local scopes need: their common direction, or bothE when
-    they differ (VertexProgramScanJob.getQueries adds one slice per scope, :109-119)."""
+    they differ (VertexProgramScanJob.getQueries adds one slice per scope, :109-119).  A program
+    that fixes its preload (``preload``, e.g. TraversalVertexProgram's whole star graph,
+    VertexProgramScanJob.java:101-107) gets that."""
+    if getattr(program, "preload", None) is not None:
+        return program.preload
     dirs = set()
     mem = FulgoraMemory(program.memory_compute_keys)
     for it in range(probe_memory_iterations):
