@@ -349,7 +349,10 @@ int upload_cold_blocks(tgo_ctx* ctx, const std::vector<int64_t>& off, const std:
         const int64_t hmax = std::min<int64_t>(hot, n_src);
         int sb = 1;
         while ((int64_t(1) << sb) < hmax) ++sb;         // sources < 2^sb
-        const int rbits = std::min(12, 32 - sb);
+        // rows per super-tile: 2^12 (64 KB of LDS accumulators), or 2^13 with TGO_PR_FX_HROWS=8192
+        // when the hot sources leave 13 bits of the packed word (hot <= 512 K)
+        const int want_rbits = env_i64("TGO_PR_FX_HROWS", 4096) == 8192 ? 13 : 12;
+        const int rbits = std::min(want_rbits, 32 - sb);
         if (rbits >= 6) {
             cb.hcsr.nnz = hc.d_hadj.n;
             adopt(ctx, cb.hcsr.adj, hc.d_hadj);

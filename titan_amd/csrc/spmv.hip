@@ -594,17 +594,22 @@ __device__ __forceinline__ void fx_emit(const PrColdFinal& fin, const FoldSrc& f
 }
 
 // One super-tile per workgroup: desc {first entry, end entry, first row, rows | -(long + 1)}.
-// Each row has 2^lc copies of its accumulator (rows * copies <= kFxSlots), the copy chosen by
+// Each row has 2^lc copies of its accumulator (rows * copies <= kSlots), the copy chosen by
 // the lane, so a tile of few rows does not serialise its lanes on one LDS address.
-template <int diag>
+// kSlots = 8192 (rbits 13, TGO_PR_FX_HROWS): twice the rows per tile, so a row-limited tile (the
+// low-degree tail) holds twice the entries and its gathers share more lines; 128 KB of dynamic
+// LDS, one workgroup a CU.
+template <int kSlots, int diag>
 __global__ void __launch_bounds__(kFxThreads) gather_hot_fx(const uint32_t* __restrict__ padj,
         const int64_t* __restrict__ desc, int rbits, const double* __restrict__ msg, PrColdFinal fin,
         unsigned long long* __restrict__ long_acc, FoldSrc fold) {
-    __shared__ unsigned long long s_lo[kFxSlots], s_hi[kFxSlots];
+    extern __shared__ unsigned long long fx_hot_lds[];
+    unsigned long long* s_lo = fx_hot_lds;
+    unsigned long long* s_hi = fx_hot_lds + kSlots;
     const int64_t t = blockIdx.x;
     const int64_t e0 = desc[4 * t], e1 = desc[4 * t + 1], r0 = desc[4 * t + 2], nr = desc[4 * t + 3];
     const int rows = nr > 0 ? static_cast<int>(nr) : 1;
-    const int lc = fx_copies_log2(rows);
+    const int lc = fx_copies_log2(rows, kSlots);
     const int nslots = rows << lc;
     for (int i = threadIdx.x; i < nslots; i += kFxThreads) { s_lo[i] = 0; s_hi[i] = 0; }
     __syncthreads();
@@ -1034,12 +1039,30 @@ hipError_t k_pr_hot_phase(const ColdBlocks& cb, const double* contrib, const dou
             const unsigned g = static_cast<unsigned>(cb.fx_ntiles);
             const uint32_t* padj = reinterpret_cast<const uint32_t*>(cb.hcsr.adj);
             const int d = fx_diag();
-            if (d == 1)
-                gather_hot_fx<1><<<g, kFxThreads, 0, s>>>(padj, cb.fx_desc, cb.fx_rbits, contrib, fin, cb.fx_long_acc, fold);
-            else if (d == 2)
-                gather_hot_fx<2><<<g, kFxThreads, 0, s>>>(padj, cb.fx_desc, cb.fx_rbits, contrib, fin, cb.fx_long_acc, fold);
-            else
-                gather_hot_fx<0><<<g, kFxThreads, 0, s>>>(padj, cb.fx_desc, cb.fx_rbits, contrib, fin, cb.fx_long_acc, fold);
+            if (cb.fx_rbits == 13) {
+                const size_t lds = 2 * 8192 * sizeof(unsigned long long);
+                static bool lds_set = false;
+                if (!lds_set) {
+                    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gather_hot_fx<8192, 0>),
+                                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                             static_cast<int>(lds));
+                    if (e != hipSuccess) return e;
+                    lds_set = true;
+                }
+                gather_hot_fx<8192, 0><<<g, kFxThreads, lds, s>>>(padj, cb.fx_desc, cb.fx_rbits, contrib, fin,
+                                                                  cb.fx_long_acc, fold);
+            } else {
+                const size_t lds = 2 * kFxSlots * sizeof(unsigned long long);
+                if (d == 1)
+                    gather_hot_fx<kFxSlots, 1><<<g, kFxThreads, lds, s>>>(padj, cb.fx_desc, cb.fx_rbits, contrib, fin,
+                                                                          cb.fx_long_acc, fold);
+                else if (d == 2)
+                    gather_hot_fx<kFxSlots, 2><<<g, kFxThreads, lds, s>>>(padj, cb.fx_desc, cb.fx_rbits, contrib, fin,
+                                                                          cb.fx_long_acc, fold);
+                else
+                    gather_hot_fx<kFxSlots, 0><<<g, kFxThreads, lds, s>>>(padj, cb.fx_desc, cb.fx_rbits, contrib, fin,
+                                                                          cb.fx_long_acc, fold);
+            }
         }
         if (cb.fx_nlong > 0)
             finalize_long_fx<<<grid_for(cb.fx_nlong), kBlock, 0, s>>>(cb.fx_long_row, cb.fx_nlong, cb.fx_long_acc, fin,
