@@ -444,7 +444,7 @@ __global__ void __launch_bounds__(kBlock) ds_commit_dev(const int32_t* __restric
 // [plo, plo + n_local) is min-reduced into rbest and marked in rmark for the owner (delta.hip).
 // kDone (binned loop with the done filter, TGO_DS_DONE): the done-word stage is compiled only
 // when it runs (its 8 words per thread cost the occupancy of the filter-off kernel).
-template <bool kBins, bool kPart = false, bool kDone = false>
+template <bool kBins, bool kPart = false, bool kDone = false, int kE = kEdgesPerThread>
 __global__ void __launch_bounds__(kBlock) ds_relax_dev(const int64_t* __restrict__ off, const int32_t* __restrict__ adj,
         const int32_t* __restrict__ wt, const int64_t* __restrict__ light, const int32_t* __restrict__ q,
         const int64_t* __restrict__ qpre, const int64_t* __restrict__ msg, int64_t* __restrict__ dist,
@@ -465,16 +465,16 @@ __global__ void __launch_bounds__(kBlock) ds_relax_dev(const int64_t* __restrict
         L->phases += 1;
         L->relaxed += static_cast<unsigned long long>(total);
     }
-    __shared__ int64_t s_pre[kLdsEntries];
-    __shared__ int32_t s_q[kLdsEntries];
+    __shared__ int64_t s_pre[(kBlock * kE + 2)];
+    __shared__ int32_t s_q[(kBlock * kE + 2)];
     __shared__ int64_t s_lo, s_hi;
     long long tmin = kInf;                                   // improvements that queued nothing
     bool bad = false;
-    const int64_t ntiles = (total + kTileEdges - 1) / kTileEdges;
+    const int64_t ntiles = (total + (kBlock * kE) - 1) / (kBlock * kE);
     auto pre = [&](int64_t i) -> int64_t { return i < qlen ? qpre[i] : total; };
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const int64_t t0 = tile * kTileEdges;
-        const int64_t t1 = min(total, t0 + kTileEdges);
+        const int64_t t0 = tile * (kBlock * kE);
+        const int64_t t1 = min(total, t0 + (kBlock * kE));
         if (kBins && threadIdx.x < kDsMaxBins) s_bn[threadIdx.x] = 0;
         if (threadIdx.x == 0) {             // lo = last i with pre(i) <= t0; hi = last i with pre(i) <= t1-1
             int64_t a = 0, b = qlen;
@@ -487,7 +487,7 @@ __global__ void __launch_bounds__(kBlock) ds_relax_dev(const int64_t* __restrict
         __syncthreads();
         const int64_t lo = s_lo, hi = s_hi;
         const int64_t span = hi - lo + 1;
-        const bool in_lds = span + 1 <= kLdsEntries;
+        const bool in_lds = span + 1 <= (kBlock * kE + 2);
         if (in_lds) {
             for (int64_t i = threadIdx.x; i <= span; i += kBlock) {
                 s_pre[i] = pre(lo + i);
@@ -495,12 +495,12 @@ __global__ void __launch_bounds__(kBlock) ds_relax_dev(const int64_t* __restrict
             }
         }
         __syncthreads();
-        // the tile's kEdgesPerThread entries per thread in stages, so each stage's loads are
+        // the tile's kE entries per thread in stages, so each stage's loads are
         // independent and in flight together (one entry at a time left every thread waiting
         // out the whole search -> list -> distance -> atomic chain once per entry)
-        int64_t u[kEdgesPerThread], e[kEdgesPerThread];
+        int64_t u[kE], e[kE];
 #pragma unroll
-        for (int k = 0; k < kEdgesPerThread; ++k) {           // 1: owning queue entry (LDS search)
+        for (int k = 0; k < kE; ++k) {           // 1: owning queue entry (LDS search)
             const int64_t j = t0 + k * kBlock + threadIdx.x;
             u[k] = -1;
             e[k] = 0;
@@ -520,25 +520,25 @@ __global__ void __launch_bounds__(kBlock) ds_relax_dev(const int64_t* __restrict
             u[k] = static_cast<int64_t>(ue & ~kHeavy);
             e[k] = ((ue & kHeavy) ? light[u[k]] : off[u[k]]) + (j - start);
         }
-        int32_t t[kEdgesPerThread], w[kEdgesPerThread];
-        int64_t mu[kEdgesPerThread], du[kEdgesPerThread];
+        int32_t t[kE], w[kE];
+        int64_t mu[kE], du[kE];
 #pragma unroll
-        for (int k = 0; k < kEdgesPerThread; ++k) {           // 2: entry, the source's snapshot
+        for (int k = 0; k < kE; ++k) {           // 2: entry, the source's snapshot
             if (u[k] < 0) continue;
             t[k] = adj[e[k]];
             w[k] = wt[e[k]];
             mu[k] = msg[u[k]];
             du[k] = dist[u[k]];
         }
-        int64_t cand[kEdgesPerThread], dt[kEdgesPerThread], tl[kEdgesPerThread];
-        uint64_t dw[kEdgesPerThread];
+        int64_t cand[kE], dt[kE], tl[kE];
+        uint64_t dw[kE];
         if (kBins && kDone) {
 #pragma unroll
-            for (int k = 0; k < kEdgesPerThread; ++k)         // 3a: done words (L2-resident bitmap)
+            for (int k = 0; k < kE; ++k)         // 3a: done words (L2-resident bitmap)
                 dw[k] = (done && u[k] >= 0) ? done[t[k] >> 6] : 0ULL;
         }
 #pragma unroll
-        for (int k = 0; k < kEdgesPerThread; ++k) {           // 3: the targets' distances
+        for (int k = 0; k < kE; ++k) {           // 3: the targets' distances
             cand[k] = -1;
             if (u[k] < 0) continue;
             if (w[k] == kMissingWeight) { bad = true; continue; }     // edge.value(weight) on a missing key
@@ -553,14 +553,14 @@ __global__ void __launch_bounds__(kBlock) ds_relax_dev(const int64_t* __restrict
                 dt[k] = dist[t[k]];
             }
         }
-        int32_t tv[kEdgesPerThread];
-        int64_t td[kEdgesPerThread];
-        int32_t fb[kEdgesPerThread];                          // kBins: pile of a far append, or -1
-        unsigned int fl[kEdgesPerThread];                     // and its slot among the tile's appends
+        int32_t tv[kE];
+        int64_t td[kE];
+        int32_t fb[kE];                          // kBins: pile of a far append, or -1
+        unsigned int fl[kE];                     // and its slot among the tile's appends
         int ntake = 0;
         int64_t dtake = 0;
 #pragma unroll
-        for (int k = 0; k < kEdgesPerThread; ++k) {           // 4: min, pending bit, take
+        for (int k = 0; k < kE; ++k) {           // 4: min, pending bit, take
             tv[k] = -1;
             td[k] = 0;
             fb[k] = -1;
@@ -609,7 +609,7 @@ __global__ void __launch_bounds__(kBlock) ds_relax_dev(const int64_t* __restrict
             }
             __syncthreads();
 #pragma unroll
-            for (int k = 0; k < kEdgesPerThread; ++k)
+            for (int k = 0; k < kE; ++k)
                 if (fb[k] >= 0) {
                     const unsigned long long slot = s_bb[fb[k]] + fl[k];
                     if (slot < static_cast<unsigned long long>(cap)) pile[fb[k] * cap + static_cast<int64_t>(slot)] = t[k];
@@ -620,7 +620,7 @@ __global__ void __launch_bounds__(kBlock) ds_relax_dev(const int64_t* __restrict
         block_reserve(&L->qc[cur ^ 1], ntake, dtake, slot, doff);
         if (ntake) {
 #pragma unroll
-            for (int k = 0; k < kEdgesPerThread; ++k)
+            for (int k = 0; k < kE; ++k)
                 if (tv[k] >= 0) {
                     qn[slot] = tv[k];
                     qpre_n[slot] = doff;
@@ -936,7 +936,18 @@ hipError_t k_ds_loop_step_bins(const DevCsr& ws, const int64_t* light, uint64_t*
                                                  nbins, pile, cap, pull);
         ds_pull_flip<<<1, 64, 0, s>>>(L);
     }
-    if (done_filter)
+    // TGO_DS_RELAX_E (A/B): entries per thread of the binned relax (8: 160 VGPRs, 3 waves per
+    // SIMD; 6: 136, still 3; 4: fewer in flight per wave, more waves)
+    static const int re = static_cast<int>(env_i64_dl("TGO_DS_RELAX_E", 8));
+    if (!done_filter && re == 6) {
+        ds_relax_dev<true, false, false, 6><<<rg, kBlock, 0, s>>>(ws.off, ws.adj, ws.w, light, q[cur], qpre[cur], msg,
+                                                                  dist, pend, q[cur ^ 1], qpre[cur ^ 1], L, cur, delta,
+                                                                  nbins, pile, cap, nullptr);
+    } else if (!done_filter && re == 4) {
+        ds_relax_dev<true, false, false, 4><<<rg, kBlock, 0, s>>>(ws.off, ws.adj, ws.w, light, q[cur], qpre[cur], msg,
+                                                                  dist, pend, q[cur ^ 1], qpre[cur ^ 1], L, cur, delta,
+                                                                  nbins, pile, cap, nullptr);
+    } else if (done_filter)
         ds_relax_dev<true, false, true><<<rg, kBlock, 0, s>>>(ws.off, ws.adj, ws.w, light, q[cur], qpre[cur], msg, dist,
                                                               pend, q[cur ^ 1], qpre[cur ^ 1], L, cur, delta, nbins, pile,
                                                               cap, done);
