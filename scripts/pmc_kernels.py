@@ -12,7 +12,7 @@ import os
 import sys
 from collections import defaultdict
 
-KEEP = os.environ.get("PMC_KEEP", "gather_hot_pf,cold_gather,cold_fold,gather_chunks,lds_window,ms_pull,gather<").split(",")
+KEEP = os.environ.get("PMC_KEEP", "gather_hot_fx,cold_fx,finalize_long_fx,gather_hot_pf,cold_gather,cold_fold,gather_chunks,lds_window,ms_pull,gather<").split(",")
 
 
 def short(name):
