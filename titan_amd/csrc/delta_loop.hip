@@ -444,7 +444,12 @@ __global__ void __launch_bounds__(kBlock) ds_commit_dev(const int32_t* __restric
 // [plo, plo + n_local) is min-reduced into rbest and marked in rmark for the owner (delta.hip).
 // kDone (binned loop with the done filter, TGO_DS_DONE): the done-word stage is compiled only
 // when it runs (its 8 words per thread cost the occupancy of the filter-off kernel).
-template <bool kBins, bool kPart = false, bool kDone = false, int kE = kEdgesPerThread>
+// kE: entries per thread of a tile (kBlock * kE per tile).  4 (round 5): 101 VGPRs, 4 waves
+// per SIMD — 7 % faster per RMAT-24 source than 8 (160 VGPRs, 3 waves; 6: 136, 3 waves; 3: 89 /
+// 5 waves and 2: 76 / 6 waves slower: too few loads in flight per wave),
+// profiles/r05s2_sssp_relax_e_ab.log.
+constexpr int kDsRelaxE = 4;
+template <bool kBins, bool kPart = false, bool kDone = false, int kE = kDsRelaxE>
 __global__ void __launch_bounds__(kBlock) ds_relax_dev(const int64_t* __restrict__ off, const int32_t* __restrict__ adj,
         const int32_t* __restrict__ wt, const int64_t* __restrict__ light, const int32_t* __restrict__ q,
         const int64_t* __restrict__ qpre, const int64_t* __restrict__ msg, int64_t* __restrict__ dist,
@@ -936,15 +941,10 @@ hipError_t k_ds_loop_step_bins(const DevCsr& ws, const int64_t* light, uint64_t*
                                                  nbins, pile, cap, pull);
         ds_pull_flip<<<1, 64, 0, s>>>(L);
     }
-    // TGO_DS_RELAX_E (A/B): entries per thread of the binned relax (8: 160 VGPRs, 3 waves per
-    // SIMD; 6: 136, still 3; 4: fewer in flight per wave, more waves)
-    static const int re = static_cast<int>(env_i64_dl("TGO_DS_RELAX_E", 8));
-    if (!done_filter && re == 6) {
-        ds_relax_dev<true, false, false, 6><<<rg, kBlock, 0, s>>>(ws.off, ws.adj, ws.w, light, q[cur], qpre[cur], msg,
-                                                                  dist, pend, q[cur ^ 1], qpre[cur ^ 1], L, cur, delta,
-                                                                  nbins, pile, cap, nullptr);
-    } else if (!done_filter && re == 4) {
-        ds_relax_dev<true, false, false, 4><<<rg, kBlock, 0, s>>>(ws.off, ws.adj, ws.w, light, q[cur], qpre[cur], msg,
+    // TGO_DS_RELAX_E (A/B): entries per thread of the binned relax (default kDsRelaxE)
+    static const int re = static_cast<int>(env_i64_dl("TGO_DS_RELAX_E", kDsRelaxE));
+    if (!done_filter && re == 8) {
+        ds_relax_dev<true, false, false, 8><<<rg, kBlock, 0, s>>>(ws.off, ws.adj, ws.w, light, q[cur], qpre[cur], msg,
                                                                   dist, pend, q[cur ^ 1], qpre[cur ^ 1], L, cur, delta,
                                                                   nbins, pile, cap, nullptr);
     } else if (done_filter)
