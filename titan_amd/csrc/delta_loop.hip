@@ -444,11 +444,11 @@ __global__ void __launch_bounds__(kBlock) ds_commit_dev(const int32_t* __restric
 // [plo, plo + n_local) is min-reduced into rbest and marked in rmark for the owner (delta.hip).
 // kDone (binned loop with the done filter, TGO_DS_DONE): the done-word stage is compiled only
 // when it runs (its 8 words per thread cost the occupancy of the filter-off kernel).
-// kE: entries per thread of a tile (kBlock * kE per tile).  4 (round 5): 101 VGPRs, 4 waves
-// per SIMD — 7 % faster per RMAT-24 source than 8 (160 VGPRs, 3 waves; 6: 136, 3 waves; 3: 89 /
-// 5 waves and 2: 76 / 6 waves slower: too few loads in flight per wave),
-// profiles/r05s2_sssp_relax_e_ab.log.
-constexpr int kDsRelaxE = 4;
+// kE: entries per thread of a tile (kBlock * kE per tile).  5 (round 5): 125 VGPRs, 4 waves
+// per SIMD — 8 % faster per RMAT-24 source than 8 (160 VGPRs, 3 waves; 6: 136, 3 waves), 1 %
+// faster than 4 (101 VGPRs, 4 waves); 3 (89 / 5 waves) and 2 (76 / 6 waves) slower: too few
+// loads in flight per wave (profiles/r05s2_sssp_relax_e_ab.log, r05s4_sssp_relax_e45_ab.log).
+constexpr int kDsRelaxE = 5;
 template <bool kBins, bool kPart = false, bool kDone = false, int kE = kDsRelaxE>
 __global__ void __launch_bounds__(kBlock) ds_relax_dev(const int64_t* __restrict__ off, const int32_t* __restrict__ adj,
         const int32_t* __restrict__ wt, const int64_t* __restrict__ light, const int32_t* __restrict__ q,
@@ -945,6 +945,10 @@ hipError_t k_ds_loop_step_bins(const DevCsr& ws, const int64_t* light, uint64_t*
     static const int re = static_cast<int>(env_i64_dl("TGO_DS_RELAX_E", kDsRelaxE));
     if (!done_filter && re == 8) {
         ds_relax_dev<true, false, false, 8><<<rg, kBlock, 0, s>>>(ws.off, ws.adj, ws.w, light, q[cur], qpre[cur], msg,
+                                                                  dist, pend, q[cur ^ 1], qpre[cur ^ 1], L, cur, delta,
+                                                                  nbins, pile, cap, nullptr);
+    } else if (!done_filter && re == 4) {
+        ds_relax_dev<true, false, false, 4><<<rg, kBlock, 0, s>>>(ws.off, ws.adj, ws.w, light, q[cur], qpre[cur], msg,
                                                                   dist, pend, q[cur ^ 1], qpre[cur ^ 1], L, cur, delta,
                                                                   nbins, pile, cap, nullptr);
     } else if (done_filter)

@@ -455,6 +455,10 @@ __global__ void __launch_bounds__(kBlock) ms_fbitmap(const uint64_t* __restrict_
 // entries (18 KB of LDS, eight blocks a CU); a tile touching more (low-degree frontiers)
 // searches the global scan instead.
 constexpr int kPushLds = 514;
+// kE: edges per thread (a tile is kBlock * kE edges).  4 (round 5): 50 VGPRs, 8 waves per SIMD
+// — the RMAT-24 sweep 3.76 -> 3.68 ms against 8 (86 VGPRs, 5 waves;
+// profiles/r05ms1_ms_push_e_ab.log); TGO_MS_PUSH_E=8 for the A/B
+template <int kE = 4>
 __global__ void __launch_bounds__(kBlock) ms_push(View push, const int32_t* __restrict__ q,
         const int64_t* __restrict__ qpre, int64_t qlen, const uint64_t* __restrict__ fr,
         const uint64_t* __restrict__ vis, uint64_t* __restrict__ nx, PackTouch touch, uint64_t mask, bool probe,
@@ -466,10 +470,10 @@ __global__ void __launch_bounds__(kBlock) ms_push(View push, const int32_t* __re
     __shared__ uint64_t s_m[kPushLds];
     __shared__ int64_t s_lo, s_hi;
     const int64_t total = qpre[qlen];
-    const int64_t ntiles = (total + kTileEdges - 1) / kTileEdges;
+    const int64_t ntiles = (total + (kBlock * kE) - 1) / (kBlock * kE);
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const int64_t t0 = tile * kTileEdges;
-        const int64_t t1 = min(total, t0 + kTileEdges);
+        const int64_t t0 = tile * (kBlock * kE);
+        const int64_t t1 = min(total, t0 + (kBlock * kE));
         if (threadIdx.x == 0) {
             int64_t a = 0, b = qlen;
             while (b - a > 1) { const int64_t c = (a + b) >> 1; if (qpre[c] <= t0) a = c; else b = c; }
@@ -497,12 +501,12 @@ __global__ void __launch_bounds__(kBlock) ms_push(View push, const int32_t* __re
             }
         }
         __syncthreads();
-        int32_t v[kEdgesPerThread];
-        uint64_t m[kEdgesPerThread];
+        int32_t v[kE];
+        uint64_t m[kE];
         if (in_lds) {
-            int64_t ia[kEdgesPerThread], o[kEdgesPerThread];
+            int64_t ia[kE], o[kE];
 #pragma unroll
-            for (int k = 0; k < kEdgesPerThread; ++k) {       // 1: owning entry (LDS search)
+            for (int k = 0; k < kE; ++k) {       // 1: owning entry (LDS search)
                 const int64_t j = t0 + k * kBlock + threadIdx.x;
                 ia[k] = -1;
                 o[k] = 0;
@@ -513,7 +517,7 @@ __global__ void __launch_bounds__(kBlock) ms_push(View push, const int32_t* __re
                 o[k] = j - s_pre[a];
             }
 #pragma unroll
-            for (int k = 0; k < kEdgesPerThread; ++k) {       // 2: neighbour index
+            for (int k = 0; k < kE; ++k) {       // 2: neighbour index
                 v[k] = -1;
                 m[k] = 0;
                 if (ia[k] < 0) continue;
@@ -523,7 +527,7 @@ __global__ void __launch_bounds__(kBlock) ms_push(View push, const int32_t* __re
             }
         } else {                                              // a huge slice: global search
 #pragma unroll
-            for (int k = 0; k < kEdgesPerThread; ++k) {
+            for (int k = 0; k < kE; ++k) {
                 const int64_t j = t0 + k * kBlock + threadIdx.x;
                 v[k] = -1;
                 m[k] = 0;
@@ -535,10 +539,10 @@ __global__ void __launch_bounds__(kBlock) ms_push(View push, const int32_t* __re
                 if (m[k]) v[k] = view_entry(push, u, j - qpre[a]);
             }
         }
-        uint64_t cv[kEdgesPerThread], cn[kEdgesPerThread];
-        uint64_t* tgt[kEdgesPerThread];
+        uint64_t cv[kE], cn[kE];
+        uint64_t* tgt[kE];
 #pragma unroll
-        for (int k = 0; k < kEdgesPerThread; ++k) {           // 3: the neighbour's masks
+        for (int k = 0; k < kE; ++k) {           // 3: the neighbour's masks
             cv[k] = 0;
             cn[k] = 0;
             tgt[k] = nullptr;
@@ -551,7 +555,7 @@ __global__ void __launch_bounds__(kBlock) ms_push(View push, const int32_t* __re
             if (probe) cn[k] = *tgt[k];
         }
 #pragma unroll
-        for (int k = 0; k < kEdgesPerThread; ++k) {           // 4: the atomic
+        for (int k = 0; k < kE; ++k) {           // 4: the atomic
             if (v[k] < 0) continue;
             const uint64_t mk = m[k] & ~cv[k];
             if (mk && (cn[k] & mk) != mk) {
@@ -1059,7 +1063,9 @@ hipError_t k_ms_queue(const View& push, int64_t n_active, const uint64_t* fr, in
 hipError_t k_ms_push(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen, const uint64_t* fr,
                      const uint64_t* vis, uint64_t* nx, hipStream_t s, PackTouch touch, uint64_t mask, bool probe,
                      uint64_t* own_nx, int64_t own_lo) {
-    ms_push<<<256 * 8, kBlock, 0, s>>>(push, q, qpre, qlen, fr, vis, nx, touch, mask, probe, own_nx, own_lo);
+    static const bool e8 = [] { const char* e = std::getenv("TGO_MS_PUSH_E"); return e && std::atoi(e) == 8; }();
+    if (e8) ms_push<8><<<256 * 8, kBlock, 0, s>>>(push, q, qpre, qlen, fr, vis, nx, touch, mask, probe, own_nx, own_lo);
+    else ms_push<><<<256 * 8, kBlock, 0, s>>>(push, q, qpre, qlen, fr, vis, nx, touch, mask, probe, own_nx, own_lo);
     return hipGetLastError();
 }
 hipError_t k_ms_push_ranged(const View& push, const int32_t* q, int64_t qlen, int64_t n_active, int64_t S,
