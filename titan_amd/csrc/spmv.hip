@@ -603,9 +603,11 @@ template <int kSlots, int diag>
 __global__ void __launch_bounds__(kFxThreads) gather_hot_fx(const uint32_t* __restrict__ padj,
         const int64_t* __restrict__ desc, int rbits, const double* __restrict__ msg, PrColdFinal fin,
         unsigned long long* __restrict__ long_acc, FoldSrc fold) {
+    // 4096 slots: static LDS as before the 8192 option (the launch then passes no dynamic LDS)
+    __shared__ unsigned long long s_static[kSlots == kFxSlots ? 2 * kFxSlots : 1];
     extern __shared__ unsigned long long fx_hot_lds[];
-    unsigned long long* s_lo = fx_hot_lds;
-    unsigned long long* s_hi = fx_hot_lds + kSlots;
+    unsigned long long* s_lo = kSlots == kFxSlots ? s_static : fx_hot_lds;
+    unsigned long long* s_hi = s_lo + kSlots;
     const int64_t t = blockIdx.x;
     const int64_t e0 = desc[4 * t], e1 = desc[4 * t + 1], r0 = desc[4 * t + 2], nr = desc[4 * t + 3];
     const int rows = nr > 0 ? static_cast<int>(nr) : 1;
@@ -1052,7 +1054,7 @@ hipError_t k_pr_hot_phase(const ColdBlocks& cb, const double* contrib, const dou
                 gather_hot_fx<8192, 0><<<g, kFxThreads, lds, s>>>(padj, cb.fx_desc, cb.fx_rbits, contrib, fin,
                                                                   cb.fx_long_acc, fold);
             } else {
-                const size_t lds = 2 * kFxSlots * sizeof(unsigned long long);
+                const size_t lds = 0;
                 if (d == 1)
                     gather_hot_fx<kFxSlots, 1><<<g, kFxThreads, lds, s>>>(padj, cb.fx_desc, cb.fx_rbits, contrib, fin,
                                                                           cb.fx_long_acc, fold);
