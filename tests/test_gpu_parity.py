@@ -624,6 +624,24 @@ def test_rmat_pagerank_cache_blocked(rmat12, iters, hot, seg, tile, win, monkeyp
     assert np.abs(pr - plain).sum() <= 1e-12
 
 
+@pytest.mark.parametrize("hot", [64, 1000, 3000])
+def test_rmat_pagerank_source_split_bitwise(rmat12, hot, monkeypatch):
+    """The fixed-point hot pass split over S ranges of the hot sources (TGO_PR_FX_SPLIT = S
+    launches, the row sums carried between them): the same exact 128-bit sums, so the ranks are
+    bitwise equal for S = 1, 2, 3 and 5, and within the oracle bar."""
+    n, src, dst, w, ids, oracle, roots = rmat12
+    monkeypatch.setenv("TGO_PR_HOT", str(hot))
+    monkeypatch.setenv("TGO_PR_SEG", "256")
+    ranks = {}
+    for split in (1, 2, 3, 5):
+        monkeypatch.setenv("TGO_PR_FX_SPLIT", str(split))
+        ranks[split] = Engine().load_edges(n, src, dst, IN).pagerank(0.85, n, 20)
+    opr, _ = oracle.pagerank(0.85, n, 20)
+    assert np.abs(ranks[1] - opr).sum() <= PR_L1_TOL
+    for split in (2, 3, 5):
+        assert np.array_equal(ranks[split], ranks[1]), split
+
+
 def hub_graph(n, hub, k_in, k_out, seed=11):
     """A random background plus a hub receiving `k_in` and sending `k_out` edges."""
     rng = np.random.default_rng(seed)

@@ -371,6 +371,11 @@ struct ColdBlocks {
     int64_t fx_nlong = 0;
     int32_t* fx_long_row = nullptr;     // rows longer than a tile
     unsigned long long* fx_long_acc = nullptr;   // 2 per long row (low, high word), zero between updates
+    // source-split hot pass (TGO_PR_FX_SPLIT = S): S launches over S ranges of the hot sources, so
+    // each launch's messages fit an XCD's L2; the row sums carried between them in fx_part
+    int fx_split = 0;
+    int64_t* fx_mid = nullptr;          // (S + 1) per tile: its entry bounds of the source ranges
+    unsigned long long* fx_part = nullptr;       // 2 per hot row (low, high word)
 };
 struct HostColdBlocks {
     int64_t hot = 0, seg = 0;
@@ -799,6 +804,9 @@ hipError_t k_pr_iter(const DevCsr& in, const RowBlocks& rb, const double* contri
                      double alpha, double base, int64_t n, const PrTuning& t, hipStream_t s);
 hipError_t k_fill_f64(double* p, double v, int64_t n, hipStream_t s);
 hipError_t k_pr_cold_phase(const ColdBlocks& cb, const double* contrib, hipStream_t s);
+// per fixed-point hot tile (desc, packed source << rbits | row): the first entry with source >= hs
+hipError_t k_fx_split_points(const uint32_t* padj, const int64_t* desc, int64_t ntiles, int rbits, int64_t hot,
+                             int nsplit, int64_t* bnd, hipStream_t s);
 hipError_t k_pr_hot_phase(const ColdBlocks& cb, const double* contrib, const double* edge_count, double* pr,
                           double* contrib_next, double* partial_long, double alpha, double base, hipStream_t s);
 hipError_t k_pr_iter_cold(const ColdBlocks& cb, const double* contrib, const double* edge_count, double* pr,

@@ -599,21 +599,33 @@ __device__ __forceinline__ void fx_emit(const PrColdFinal& fin, const FoldSrc& f
 // kSlots = 8192 (rbits 13, TGO_PR_FX_HROWS): twice the rows per tile, so a row-limited tile (the
 // low-degree tail) holds twice the entries and its gathers share more lines; 128 KB of dynamic
 // LDS, one workgroup a CU.
-template <int kSlots, int diag>
+// kPass (source split, TGO_PR_FX_SPLIT = S parts): 0 = the whole tile; otherwise launch p of S
+// takes the tile's entries [bnd[t * (S + 1) + p], bnd[t * (S + 1) + p + 1]) (its sources in the
+// p-th range) — 1 = the first (row totals to part), 3 = a middle one (from part, back to part),
+// 2 = the last (from part, emitted).  The same exact sum in every split, so the ranks are
+// bitwise those of kPass 0.
+template <int kSlots, int diag, int kPass = 0>
 __global__ void __launch_bounds__(kFxThreads) gather_hot_fx(const uint32_t* __restrict__ padj,
         const int64_t* __restrict__ desc, int rbits, const double* __restrict__ msg, PrColdFinal fin,
-        unsigned long long* __restrict__ long_acc, FoldSrc fold) {
+        unsigned long long* __restrict__ long_acc, FoldSrc fold, const int64_t* __restrict__ bnd = nullptr,
+        int nsplit = 1, int p = 0, unsigned long long* __restrict__ part = nullptr) {
     // 4096 slots: static LDS as before the 8192 option (the launch then passes no dynamic LDS)
     __shared__ unsigned long long s_static[kSlots == kFxSlots ? 2 * kFxSlots : 1];
     extern __shared__ unsigned long long fx_hot_lds[];
     unsigned long long* s_lo = kSlots == kFxSlots ? s_static : fx_hot_lds;
     unsigned long long* s_hi = s_lo + kSlots;
     const int64_t t = blockIdx.x;
-    const int64_t e0 = desc[4 * t], e1 = desc[4 * t + 1], r0 = desc[4 * t + 2], nr = desc[4 * t + 3];
+    const int64_t r0 = desc[4 * t + 2], nr = desc[4 * t + 3];
+    const int64_t e0 = kPass == 0 ? desc[4 * t] : bnd[t * (nsplit + 1) + p];
+    const int64_t e1 = kPass == 0 ? desc[4 * t + 1] : bnd[t * (nsplit + 1) + p + 1];
     const int rows = nr > 0 ? static_cast<int>(nr) : 1;
     const int lc = fx_copies_log2(rows, kSlots);
     const int nslots = rows << lc;
-    for (int i = threadIdx.x; i < nslots; i += kFxThreads) { s_lo[i] = 0; s_hi[i] = 0; }
+    for (int i = threadIdx.x; i < nslots; i += kFxThreads) {
+        const bool carry = (kPass == 2 || kPass == 3) && nr > 0 && (i & ((1 << lc) - 1)) == 0;   // copy 0: the sum so far
+        s_lo[i] = carry ? part[2 * (r0 + (i >> lc))] : 0;
+        s_hi[i] = carry ? part[2 * (r0 + (i >> lc)) + 1] : 0;
+    }
     __syncthreads();
     fx_accumulate<diag>(padj + e0, e1 - e0, msg, rbits, lc, s_lo, s_hi);
     __syncthreads();
@@ -621,7 +633,12 @@ __global__ void __launch_bounds__(kFxThreads) gather_hot_fx(const uint32_t* __re
         for (int i = threadIdx.x; i < rows; i += kFxThreads) {
             unsigned long long lo, hi;
             fx_total(s_lo, s_hi, i, lc, lo, hi);
-            fx_emit(fin, fold, r0 + i, fx_to_double(lo, hi));   // + the row's cold sum, then the update
+            if (kPass == 1 || kPass == 3) {
+                part[2 * (r0 + i)] = lo;
+                part[2 * (r0 + i) + 1] = hi;
+            } else {
+                fx_emit(fin, fold, r0 + i, fx_to_double(lo, hi));   // + the row's cold sum, then the update
+            }
         }
     } else if (threadIdx.x == 0) {                        // a long row's chunk: into the row's accumulator
         unsigned long long lo = 0, hi = 0;
@@ -1030,6 +1047,31 @@ hipError_t k_pr_cold_phase(const ColdBlocks& cb, const double* contrib, hipStrea
     return hipGetLastError();
 }
 
+// bnd[t * (S + 1) + p] = the first entry of tile t with source >= p * hot / S (entries sorted by source)
+__global__ void fx_split_points(const uint32_t* __restrict__ padj, const int64_t* __restrict__ desc, int64_t ntiles,
+                                int rbits, int64_t hot, int nsplit, int64_t* __restrict__ bnd) {
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < ntiles; t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t e0 = desc[4 * t], e1 = desc[4 * t + 1];
+        bnd[t * (nsplit + 1)] = e0;
+        bnd[t * (nsplit + 1) + nsplit] = e1;
+        for (int p = 1; p < nsplit; ++p) {
+            const int64_t hs = hot * p / nsplit;
+            int64_t a = e0, b = e1;
+            while (a < b) {
+                const int64_t c = (a + b) >> 1;
+                if (static_cast<int64_t>(padj[c] >> rbits) < hs) a = c + 1; else b = c;
+            }
+            bnd[t * (nsplit + 1) + p] = a;
+        }
+    }
+}
+hipError_t k_fx_split_points(const uint32_t* padj, const int64_t* desc, int64_t ntiles, int rbits, int64_t hot,
+                             int nsplit, int64_t* bnd, hipStream_t s) {
+    if (ntiles <= 0) return hipSuccess;
+    fx_split_points<<<grid_for(ntiles), kBlock, 0, s>>>(padj, desc, ntiles, rbits, hot, nsplit, bnd);
+    return hipGetLastError();
+}
+
 // Hot phase: every row's hot entries (sources [0, hot)) + its folded cold sum -> the update.
 hipError_t k_pr_hot_phase(const ColdBlocks& cb, const double* contrib, const double* edge_count, double* pr,
                           double* contrib_next, double* partial_long, double alpha, double base, hipStream_t s) {
@@ -1053,6 +1095,22 @@ hipError_t k_pr_hot_phase(const ColdBlocks& cb, const double* contrib, const dou
                 }
                 gather_hot_fx<8192, 0><<<g, kFxThreads, lds, s>>>(padj, cb.fx_desc, cb.fx_rbits, contrib, fin,
                                                                   cb.fx_long_acc, fold);
+            } else if (cb.fx_split > 1 && d == 0) {  // one launch per source range
+                const int S = cb.fx_split;
+                for (int p = 0; p < S; ++p) {
+                    if (p == 0)
+                        gather_hot_fx<kFxSlots, 0, 1><<<g, kFxThreads, 0, s>>>(padj, cb.fx_desc, cb.fx_rbits, contrib, fin,
+                                                                               cb.fx_long_acc, fold, cb.fx_mid, S, p,
+                                                                               cb.fx_part);
+                    else if (p + 1 < S)
+                        gather_hot_fx<kFxSlots, 0, 3><<<g, kFxThreads, 0, s>>>(padj, cb.fx_desc, cb.fx_rbits, contrib, fin,
+                                                                               cb.fx_long_acc, fold, cb.fx_mid, S, p,
+                                                                               cb.fx_part);
+                    else
+                        gather_hot_fx<kFxSlots, 0, 2><<<g, kFxThreads, 0, s>>>(padj, cb.fx_desc, cb.fx_rbits, contrib, fin,
+                                                                               cb.fx_long_acc, fold, cb.fx_mid, S, p,
+                                                                               cb.fx_part);
+                }
             } else {
                 const size_t lds = 0;
                 if (d == 1)
