@@ -22,7 +22,7 @@ eng = None
 loaded_with = None
 KEYS = ("TGO_PR_BLOCKED", "TGO_PR_HOT", "TGO_PR_SEG", "TGO_PR_DIAG", "TGO_PR_PACK", "TGO_PR_CPACK", "TGO_PR_HOT_TILE", "TGO_PR_HOT_PIPE",
         "TGO_PR_FX", "TGO_PR_FX_E", "TGO_PR_FX_COLD", "TGO_PR_FX_CE", "TGO_PR_FX_CP", "TGO_PR_FX_DIAG", "TGO_PR_FX_FOLD",
-        "TGO_PR_FX_HROWS", "TGO_PR_FX_SPLIT")
+        "TGO_PR_FX_HROWS", "TGO_PR_FX_SPLIT", "TGO_PR_FX_SPLIT_AT")
 variants = [
     {},
     {"TGO_PR_BLOCKED": "0"},
@@ -34,7 +34,7 @@ variants = [
     {},
 ]
 RELOAD = ("TGO_PR_BLOCKED", "TGO_PR_HOT", "TGO_PR_SEG", "TGO_PR_PACK", "TGO_PR_CPACK", "TGO_PR_HOT_TILE", "TGO_PR_HOT_PIPE",
-          "TGO_PR_FX", "TGO_PR_FX_E", "TGO_PR_FX_COLD", "TGO_PR_FX_CE", "TGO_PR_FX_CP", "TGO_PR_FX_HROWS", "TGO_PR_FX_SPLIT")   # read at load time
+          "TGO_PR_FX", "TGO_PR_FX_E", "TGO_PR_FX_COLD", "TGO_PR_FX_CE", "TGO_PR_FX_CP", "TGO_PR_FX_HROWS", "TGO_PR_FX_SPLIT", "TGO_PR_FX_SPLIT_AT")   # read at load time
 if os.environ.get("PR_PROBE_DEFAULT_ONLY"):       # one variant: the TGO_PR_* settings of the caller's environment
     variants = [{k: os.environ[k] for k in KEYS if k in os.environ}]
 if os.environ.get("PR_PROBE_VARIANTS"):        # a JSON list of env dicts, e.g. '[{}, {"TGO_PR_SEG": "393216"}]'

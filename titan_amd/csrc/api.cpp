@@ -388,8 +388,9 @@ int upload_cold_blocks(tgo_ctx* ctx, const std::vector<int64_t>& off, const std:
             if (split > 1 && cb.fx_ntiles > 0) {
                 HIP_TRY(dev_alloc(ctx, cb.fx_mid, cb.fx_ntiles * (split + 1)));
                 HIP_TRY(dev_alloc(ctx, cb.fx_part, 2 * std::max<int64_t>(n_rows, 1)));
+                const int64_t first = std::min<int64_t>(hmax, std::max<int64_t>(0, env_i64("TGO_PR_FX_SPLIT_AT", 0)));
                 HIP_TRY(k_fx_split_points(reinterpret_cast<const uint32_t*>(cb.hcsr.adj), cb.fx_desc, cb.fx_ntiles, rbits,
-                                          hmax, static_cast<int>(split), cb.fx_mid, ctx->stream));
+                                          hmax, static_cast<int>(split), first, cb.fx_mid, ctx->stream));
                 cb.fx_split = static_cast<int>(split);
             }
             lap("hot super-tiles");

@@ -805,8 +805,9 @@ hipError_t k_pr_iter(const DevCsr& in, const RowBlocks& rb, const double* contri
 hipError_t k_fill_f64(double* p, double v, int64_t n, hipStream_t s);
 hipError_t k_pr_cold_phase(const ColdBlocks& cb, const double* contrib, hipStream_t s);
 // per fixed-point hot tile (desc, packed source << rbits | row): the first entry with source >= hs
+// first > 0: the first range is [0, first) (TGO_PR_FX_SPLIT_AT), else S even ranges
 hipError_t k_fx_split_points(const uint32_t* padj, const int64_t* desc, int64_t ntiles, int rbits, int64_t hot,
-                             int nsplit, int64_t* bnd, hipStream_t s);
+                             int nsplit, int64_t first, int64_t* bnd, hipStream_t s);
 hipError_t k_pr_hot_phase(const ColdBlocks& cb, const double* contrib, const double* edge_count, double* pr,
                           double* contrib_next, double* partial_long, double alpha, double base, hipStream_t s);
 hipError_t k_pr_iter_cold(const ColdBlocks& cb, const double* contrib, const double* edge_count, double* pr,

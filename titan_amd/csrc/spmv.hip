@@ -1049,13 +1049,15 @@ hipError_t k_pr_cold_phase(const ColdBlocks& cb, const double* contrib, hipStrea
 
 // bnd[t * (S + 1) + p] = the first entry of tile t with source >= p * hot / S (entries sorted by source)
 __global__ void fx_split_points(const uint32_t* __restrict__ padj, const int64_t* __restrict__ desc, int64_t ntiles,
-                                int rbits, int64_t hot, int nsplit, int64_t* __restrict__ bnd) {
+                                int rbits, int64_t hot, int nsplit, int64_t first, int64_t* __restrict__ bnd) {
     for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < ntiles; t += (int64_t)gridDim.x * blockDim.x) {
         const int64_t e0 = desc[4 * t], e1 = desc[4 * t + 1];
         bnd[t * (nsplit + 1)] = e0;
         bnd[t * (nsplit + 1) + nsplit] = e1;
         for (int p = 1; p < nsplit; ++p) {
-            const int64_t hs = hot * p / nsplit;
+            // the first boundary at `first` sources when given (the hubs hold most entries), the
+            // rest of the range cut evenly
+            const int64_t hs = first > 0 ? first + (hot - first) * (p - 1) / (nsplit - 1) : hot * p / nsplit;
             int64_t a = e0, b = e1;
             while (a < b) {
                 const int64_t c = (a + b) >> 1;
@@ -1066,9 +1068,9 @@ __global__ void fx_split_points(const uint32_t* __restrict__ padj, const int64_t
     }
 }
 hipError_t k_fx_split_points(const uint32_t* padj, const int64_t* desc, int64_t ntiles, int rbits, int64_t hot,
-                             int nsplit, int64_t* bnd, hipStream_t s) {
+                             int nsplit, int64_t first, int64_t* bnd, hipStream_t s) {
     if (ntiles <= 0) return hipSuccess;
-    fx_split_points<<<grid_for(ntiles), kBlock, 0, s>>>(padj, desc, ntiles, rbits, hot, nsplit, bnd);
+    fx_split_points<<<grid_for(ntiles), kBlock, 0, s>>>(padj, desc, ntiles, rbits, hot, nsplit, first, bnd);
     return hipGetLastError();
 }
 
