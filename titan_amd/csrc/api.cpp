@@ -196,12 +196,13 @@ constexpr int64_t kPrSegDefault = 393216;   // 3 MB (profiles/r02an_pr_hot_seg_p
 // 380 K-entry tiles reuse lines enough that a head past one XCD's L2 still pays (RMAT-24
 // ms/update: 384 K 0.852, 512 K 0.827, 768 K 0.814-0.818, 1 M 0.830, 1.5 M 0.913;
 // profiles/r05j_pr_fx_hot_ab.log, r05k_pr_fx_hot_ab.log)
-int64_t pr_hot_default() { return env_i64("TGO_PR_FX", 1) != 0 ? 786432 : 393216; }
-// One GPU with the source-split hot pass (TGO_PR_FX_SPLIT, default 2): a 1 M-source hot head, its
-// two halves' messages (4 MB each) an XCD's L2 — 0.944-0.950 -> 0.891-0.894 ms/update at
-// RMAT-24 against the unsplit 768 K head (profiles/r05sp3_pr_split_ab.log)
-int64_t pr_hot_default_one_gpu() {
-    return env_i64("TGO_PR_FX", 1) != 0 && env_i64("TGO_PR_FX_SPLIT", 2) > 1 ? 1048576 : pr_hot_default();
+// The hot head (sources of the hot pass; the partitioned layout's gathered head, over every
+// rank).  With the source-split hot pass (TGO_PR_FX_SPLIT, default 2): 1 M sources, each half's
+// messages (4 MB) an XCD's L2 — 0.944-0.950 -> 0.891-0.894 ms/update at RMAT-24 against the
+// unsplit 768 K head (profiles/r05sp3_pr_split_ab.log)
+int64_t pr_hot_default() {
+    if (env_i64("TGO_PR_FX", 1) == 0) return 393216;
+    return env_i64("TGO_PR_FX_SPLIT", 2) > 1 ? 1048576 : 786432;
 }
 // LDS window of the hottest sources (lds_window, spmv.hip; TGO_PR_WIN, at most 12288 doubles =
 // 96 KB beside the 16 waves' 4 KB item buffers).  Off by default: measured slower at every
@@ -562,7 +563,7 @@ int upload_graph(tgo_ctx* ctx, HostGraph& h, bool allow_segments = true) {
     if (allow_segments && h.scope != TGO_SCOPE_BOTH_E && env_i64("TGO_PR_BLOCKED", 1) != 0) {
         // rows >= n_active have no entries at all: the hot pass skips them (their rank
         // after any update is (1-a)/N, written once at the end of the program)
-        if (int rc = upload_cold_blocks(ctx, h.in.off, h.in.adj, h.n, env_i64("TGO_PR_HOT", pr_hot_default_one_gpu()), g.n_active,
+        if (int rc = upload_cold_blocks(ctx, h.in.off, h.in.adj, h.n, env_i64("TGO_PR_HOT", pr_hot_default()), g.n_active,
                                         g.cold_in, g.cold_in_ready, g.in.off, g.in.adj, g.in.nnz,
                                         env_i64("TGO_PR_WIN", kPrWinDefault)))
             return rc;
