@@ -341,8 +341,11 @@ int  tgo_copy_multi_distances(tgo_ctx* ctx, int32_t source, int64_t* dist_out);
 /* TGO_TUNE_DS_PULL (binned delta SSSP): a fraction f in (0, 1] = a finished bucket with at least
  * f * n members has its heavy entries pulled by the vertices that can still improve instead of
  * pushed; 0 = always pushed; -1 = TGO_DS_PULL (default 0).  Same distances either way. */
+/* TGO_TUNE_DS_SMALL (binned delta SSSP without the done filter and pulls): 1 = the tiny steps
+ * run in one block inside one launch (ds_small_steps), 0 = four grid launches per step;
+ * -1 = TGO_DS_SMALL (default 0: measured slower).  Same distances either way. */
 enum { TGO_TUNE_MS_SPLIT = 1, TGO_TUNE_MS_GHOST = 2, TGO_TUNE_DS_BINS = 3, TGO_TUNE_DS_PILE_CAP = 4,
-       TGO_TUNE_DS_DONE = 5, TGO_TUNE_MS_COLD = 6, TGO_TUNE_DS_PULL = 7 };
+       TGO_TUNE_DS_DONE = 5, TGO_TUNE_MS_COLD = 6, TGO_TUNE_DS_PULL = 7, TGO_TUNE_DS_SMALL = 8 };
 int  tgo_set_tuning(tgo_ctx* ctx, int32_t key, double value);
 
 /* ---- Tracing (the reference's only hook is FulgoraGraphComputer.java:143,307

@@ -153,6 +153,9 @@ def test_config5_rmat24_weighted_sssp(rmat24, oracle24_in_capped):
     assert len(picked) == 2
     hop3 = eng.sssp(picked[0][0], 3, IN, mode=L.SSSP_HOP_BOUNDED, seed_is_dense=True, stats=True)
     hop3_reached = eng.stats()["reached"]
+    eng.set_tuning(L.TUNE_DS_SMALL, 1)            # tiny steps in one block: the same distances
+    for r, d, _ in picked:
+        assert np.array_equal(eng.sssp(r, n, IN, mode=L.SSSP_DELTA, seed_is_dense=True), d), r
     del eng
     o = oracle24_in_capped
     for r, d, reached in picked:

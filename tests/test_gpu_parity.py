@@ -382,6 +382,24 @@ def test_rmat_sssp_delta_piles(rmat12, scope, delta, bins, cap, done, pull):
         assert eng.stats()["reached"] == int((od != ABSENT).sum())
 
 
+@pytest.mark.parametrize("scope", [OUT, IN])
+@pytest.mark.parametrize("delta", [0, 9, 200])
+@pytest.mark.parametrize("cap", [0, 16])
+def test_rmat_sssp_delta_small_steps(rmat12, scope, delta, cap):
+    """The binned loop with its tiny steps run in one block (TGO_TUNE_DS_SMALL, delta_loop.hip
+    ds_small_steps, queue buffer on the device) and the grid kernels taking over at the first
+    step that is not small — RMAT-12's steps are mostly small; cap 16 overflows piles into the
+    bitmap scan, which always goes to the grid — gives the oracle's distances bit for bit."""
+    n, src, dst, w, ids, oracle, roots = rmat12
+    eng = Engine().load_edges(n, src, dst, scope, weight=w)
+    eng.set_tuning(L.TUNE_DS_BINS, 1).set_tuning(L.TUNE_DS_PILE_CAP, cap).set_tuning(L.TUNE_DS_SMALL, 1)
+    for r in roots[:3]:
+        d = eng.sssp(int(r), n, scope, mode=L.SSSP_DELTA, seed_is_dense=True, stats=True, delta=delta)
+        od, _ = oracle.shortest_distance(int(ids[r]), n, scope, weighted=True)
+        assert np.array_equal(d, od)
+        assert eng.stats()["reached"] == int((od != ABSENT).sum())
+
+
 def test_rmat_sssp_delta_zero_weights(rmat12):
     """Zero-weight edges (ties inside a bucket, re-relaxation at equal distance)."""
     n, src, dst, w, ids, _, roots = rmat12
@@ -397,8 +415,9 @@ def test_rmat_sssp_delta_zero_weights(rmat12):
 
 
 @pytest.mark.parametrize("scope", [OUT, IN])
-@pytest.mark.parametrize("done,pull", [(0, 0), (1, 0), (0, 0.001), (1, 0.001), (1, 1.0)])
-def test_sssp_delta_bucket_merge(scope, done, pull):
+@pytest.mark.parametrize("done,pull,small", [(0, 0, 0), (1, 0, 0), (0, 0.001, 0), (1, 0.001, 0), (1, 1.0, 0),
+                                             (0, 0, 1)])
+def test_sssp_delta_bucket_merge(scope, done, pull, small):
     """A bucket merge in the binned loop (delta 10): s -10-> a, s -35-> z, a -10-> y, z -4-> c,
     y -10-> c.  When bucket 1 (a) finishes, pile 2 is empty and pile 3 holds z, so the loop
     jumps to bucket 3 while a's heavy entry puts y (20) into the near queue: buckets 2..3 merge.
@@ -418,6 +437,7 @@ def test_sssp_delta_bucket_merge(scope, done, pull):
     assert list(od) == [0, 10, 35, 20, 30]
     eng = Engine().load_edges(n, src, dst, scope, weight=w)
     eng.set_tuning(L.TUNE_DS_BINS, 1).set_tuning(L.TUNE_DS_DONE, done).set_tuning(L.TUNE_DS_PULL, pull)
+    eng.set_tuning(L.TUNE_DS_SMALL, small)
     d = eng.sssp(0, n, scope, mode=L.SSSP_DELTA, seed_is_dense=True, delta=10)
     assert np.array_equal(d, od), (d, od)
 

@@ -34,6 +34,7 @@ RESULT_DISTANCE, RESULT_PAGERANK, RESULT_DEGREE, RESULT_VALUES = 0, 1, 2, 3
 SSSP_HOP_BOUNDED, SSSP_DELTA = 0, 1
 FLAG_STATS = 1
 TUNE_MS_SPLIT, TUNE_MS_GHOST, TUNE_DS_BINS, TUNE_DS_PILE_CAP, TUNE_DS_DONE, TUNE_MS_COLD, TUNE_DS_PULL = 1, 2, 3, 4, 5, 6, 7   # tgo_set_tuning keys
+TUNE_DS_SMALL = 8
 TRACE_JSON, TRACE_ROCTX = 1, 2   # tgo_trace_enable flags
 DIST_ABSENT = -(1 << 63)
 ABI_VERSION = 2

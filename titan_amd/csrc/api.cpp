@@ -81,6 +81,7 @@ struct tgo_ctx {
     int64_t ds_pile_cap = 0;    // tgo_set_tuning(TGO_TUNE_DS_PILE_CAP): entries per pile; 0 = n
     int ds_done = -1;           // tgo_set_tuning(TGO_TUNE_DS_DONE): 1 / 0; < 0: TGO_DS_DONE / off
     double ds_pull = -1;        // tgo_set_tuning(TGO_TUNE_DS_PULL): member fraction; < 0: TGO_DS_PULL / off
+    int ds_small = -1;          // tgo_set_tuning(TGO_TUNE_DS_SMALL): 1 / 0; < 0: TGO_DS_SMALL / off
     unsigned long long* part_srcent = nullptr;   // next settle's per-source sums (part_ms_settle_sums)
     bool part_count_only = false;               // next settle: no queue (part_ms_settle_sums)
     uint64_t* part_own_next = nullptr;          // next push: owned targets straight into these masks
@@ -928,6 +929,14 @@ int run_delta_device(tgo_ctx* ctx, int64_t seed, int64_t delta, bool force_scan)
     HIP_TRY(k_ds_loop_seed(g.push_ws, s.ds_light, s.dist, s.ds_q[0], s.ds_qp[0], s.ds_loop, seed, delta, st));
     DsLoop h{};
     int cur = 0;
+    // Small steps (TGO_TUNE_DS_SMALL / TGO_DS_SMALL, default off; delta_loop.hip ds_small_steps):
+    // the tiny steps run in one block inside one launch.  The binned loop without the done
+    // filter or pulls.  Off by default: 12.6 -> 13.8 ms per RMAT-24 source
+    // (profiles/r05ss1_sssp_small_ab.log) — a tiny step is a chain of dependent memory
+    // round trips either way, and one block pays them with fewer loads in flight.
+    static const bool small_env = env_double("TGO_DS_SMALL", 0.0) != 0.0;
+    const bool small_on = ctx->ds_small < 0 ? small_env : ctx->ds_small != 0;
+    const bool small = small_on && nbins && !done_filter && pull.min_members == 0;
     // every step either relaxes a non-empty queue or extracts (at most one extraction in a row
     // takes nothing); a run needs far fewer than 4n + 64 steps — the bound only stops a bug
     const int64_t max_steps = 4 * n + 64;
@@ -942,7 +951,11 @@ int run_delta_device(tgo_ctx* ctx, int64_t seed, int64_t delta, bool force_scan)
         for (int64_t steps = 0; !stop;) {
             DevSpan span(st, "sssp.delta_steps", {"first_step", steps}, {"steps", batch});
             for (int k = 0; k < batch; ++k) {
-                if (nbins)
+                if (small)
+                    HIP_TRY(k_ds_loop_step_small(g.push_ws, s.ds_light, s.vb, s.ds_member, n, s.dist, s.msg, s.ds_q,
+                                                 s.ds_qp, s.ds_loop, delta, nbins, s.ds_pile, s.ds_pile_cap,
+                                                 s.ds_mlist, s.ds_done, scan_above, st));
+                else if (nbins)
                     HIP_TRY(k_ds_loop_step_bins(g.push_ws, s.ds_light, s.vb, s.ds_member, n, s.dist, s.msg, s.ds_q,
                                                 s.ds_qp, s.ds_loop, cur, delta, nbins, s.ds_pile, s.ds_pile_cap,
                                                 s.ds_mlist, s.ds_done, done_filter, scan_above, pull, st));
@@ -971,7 +984,11 @@ int run_delta_device(tgo_ctx* ctx, int64_t seed, int64_t delta, bool force_scan)
     for (int64_t steps = 0; !pipe;) {
         DevSpan span(st, "sssp.delta_steps", {"first_step", steps}, {"steps", batch});
         for (int k = 0; k < batch; ++k) {
-            if (nbins)
+            if (small)
+                HIP_TRY(k_ds_loop_step_small(g.push_ws, s.ds_light, s.vb, s.ds_member, n, s.dist, s.msg, s.ds_q,
+                                             s.ds_qp, s.ds_loop, delta, nbins, s.ds_pile, s.ds_pile_cap, s.ds_mlist,
+                                             s.ds_done, scan_above, st));
+            else if (nbins)
                 HIP_TRY(k_ds_loop_step_bins(g.push_ws, s.ds_light, s.vb, s.ds_member, n, s.dist, s.msg, s.ds_q, s.ds_qp,
                                             s.ds_loop, cur, delta, nbins, s.ds_pile, s.ds_pile_cap, s.ds_mlist,
                                             s.ds_done, done_filter, scan_above, pull, st));
@@ -1232,6 +1249,10 @@ int tgo_set_tuning(tgo_ctx* ctx, int32_t key, double value) {
     case TGO_TUNE_DS_DONE:
         if (value != 0.0 && value != 1.0 && value != -1.0) return fail(ctx, TGO_E_INVALID, "TGO_TUNE_DS_DONE: 0, 1 or -1");
         ctx->ds_done = static_cast<int>(value);
+        return TGO_OK;
+    case TGO_TUNE_DS_SMALL:
+        if (value != 0.0 && value != 1.0 && value != -1.0) return fail(ctx, TGO_E_INVALID, "TGO_TUNE_DS_SMALL: 0, 1 or -1");
+        ctx->ds_small = static_cast<int>(value);
         return TGO_OK;
     case TGO_TUNE_DS_PULL:
         if (!(value >= -1.0) || value > 1.0) return fail(ctx, TGO_E_INVALID, "TGO_TUNE_DS_PULL: a fraction in [0, 1] or -1");

@@ -127,6 +127,9 @@ __global__ void ds_loop_seed(const int64_t* off, const int64_t* light, int64_t* 
     L->pbucket = 0;
     L->pcount[0] = L->pcount[1] = 0;
     L->xprev = 0;
+    L->cur = 0;
+    L->big = 0;
+    L->small_steps = 0;
 }
 
 __device__ __forceinline__ unsigned long long load_agent(const unsigned long long* p) {
@@ -315,17 +318,13 @@ __global__ void __launch_bounds__(kBlock) ds_extract_dev(const int64_t* __restri
 // vertex appended several times is taken once — then, when a bucket finished, its member
 // list's heavy entries (member words reset: every set bit of the member bitmap is on the list;
 // the members marked done).  Work proportional to the pile, not to n.
-__global__ void __launch_bounds__(kBlock) ds_extract_bins(const int64_t* __restrict__ off,
+// Body of the pile extraction (mode 2) for block `bid` of `nb` (ds_small_steps runs it as one
+// block).
+__device__ __forceinline__ void extract_bins_body(int64_t bid, int64_t nb, const int64_t* __restrict__ off,
         const int64_t* __restrict__ light, uint64_t* __restrict__ pend, uint64_t* __restrict__ member,
         const int64_t* __restrict__ dist, DsLoop* L, int cur, const int32_t* __restrict__ pile, int64_t cap,
         const int32_t* __restrict__ mlist, uint64_t* __restrict__ done, int32_t* __restrict__ qn,
-        int64_t* __restrict__ qpre, int64_t n, DsPull pull) {
-    const unsigned long long mode = L->extract;             // grid-uniform
-    if (mode == 1) {                                         // a large or overflowed pile: the bitmap scan
-        extract_scan(off, light, pend, member, n, dist, L, cur, qn, qpre, done);
-        return;
-    }
-    if (mode != 2) return;
+        int64_t* __restrict__ qpre, const DsPull& pull) {
     const int64_t thr = L->thr;
     const bool xpull = L->xpull != 0;
     const bool xfin = L->xfin != 0;
@@ -337,8 +336,7 @@ __global__ void __launch_bounds__(kBlock) ds_extract_bins(const int64_t* __restr
     const int64_t xc = static_cast<int64_t>(L->xcount), xme = xc + static_cast<int64_t>(L->xm);
     const int64_t total = xme + (xpull ? static_cast<int64_t>(L->xprev) : 0);
     const int32_t* __restrict__ pl = pile + (L->xbin >= 0 ? L->xbin : 0) * cap;
-    for (int64_t base = static_cast<int64_t>(blockIdx.x) * kBlock; base < total;
-         base += static_cast<int64_t>(gridDim.x) * kBlock) {                 // block-uniform trips
+    for (int64_t base = bid * kBlock; base < total; base += nb * kBlock) {   // block-uniform trips
         const int64_t i = base + threadIdx.x;
         bool take = false;
         int32_t entry = 0;
@@ -382,20 +380,35 @@ __global__ void __launch_bounds__(kBlock) ds_extract_bins(const int64_t* __restr
     }
 }
 
+__global__ void __launch_bounds__(kBlock) ds_extract_bins(const int64_t* __restrict__ off,
+        const int64_t* __restrict__ light, uint64_t* __restrict__ pend, uint64_t* __restrict__ member,
+        const int64_t* __restrict__ dist, DsLoop* L, int cur, const int32_t* __restrict__ pile, int64_t cap,
+        const int32_t* __restrict__ mlist, uint64_t* __restrict__ done, int32_t* __restrict__ qn,
+        int64_t* __restrict__ qpre, int64_t n, DsPull pull) {
+    const unsigned long long mode = L->extract;             // grid-uniform
+    if (mode == 1) {                                         // a large or overflowed pile: the bitmap scan
+        extract_scan(off, light, pend, member, n, dist, L, cur, qn, qpre, done);
+        return;
+    }
+    if (mode != 2) return;
+    extract_bins_body(blockIdx.x, gridDim.x, off, light, pend, member, dist, L, cur, pile, cap, mlist, done, qn, qpre,
+                      pull);
+}
+
 // ---------------------------------------------------------------- commit
 // kList (binned loop): a newly marked member is also appended to the member list (one
 // reservation per wave), so the extraction visits the members without scanning the bitmap.
 template <bool kList>
-__global__ void __launch_bounds__(kBlock) ds_commit_dev(const int32_t* __restrict__ q, const int64_t* __restrict__ dist,
-        int64_t* __restrict__ msg, uint64_t* __restrict__ pend, uint64_t* __restrict__ member, DsLoop* L, int cur,
-        int32_t* __restrict__ mlist) {
+__device__ __forceinline__ void commit_body(int64_t bid, int64_t nb, const int32_t* __restrict__ q,
+        const int64_t* __restrict__ dist, int64_t* __restrict__ msg, uint64_t* __restrict__ pend,
+        uint64_t* __restrict__ member, DsLoop* L, int cur, int32_t* __restrict__ mlist) {
     const int64_t qlen = qcount(L->qc[cur]);
-    if (blockIdx.x == 0 && threadIdx.x == 0) L->qc[cur ^ 1] = 0;     // the relax appends there next
+    if (bid == 0 && threadIdx.x == 0) L->qc[cur ^ 1] = 0;           // the relax appends there next
     bool marked = false;
     __shared__ unsigned int s_wc[kWavesPerBlock];
     __shared__ unsigned long long s_mb;
-    const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
-    for (int64_t base = static_cast<int64_t>(blockIdx.x) * blockDim.x; base < qlen; base += stride) {   // block-uniform
+    const int64_t stride = nb * kBlock;
+    for (int64_t base = bid * kBlock; base < qlen; base += stride) {                // block-uniform
         const int64_t i = base + threadIdx.x;
         bool nm = false;
         int32_t v = -1;
@@ -430,6 +443,12 @@ __global__ void __launch_bounds__(kBlock) ds_commit_dev(const int32_t* __restric
     }
     if (__ballot(marked) && lane() == 0) L->members = 1;
 }
+template <bool kList>
+__global__ void __launch_bounds__(kBlock) ds_commit_dev(const int32_t* __restrict__ q, const int64_t* __restrict__ dist,
+        int64_t* __restrict__ msg, uint64_t* __restrict__ pend, uint64_t* __restrict__ member, DsLoop* L, int cur,
+        int32_t* __restrict__ mlist) {
+    commit_body<kList>(blockIdx.x, gridDim.x, q, dist, msg, pend, member, L, cur, mlist);
+}
 
 // ---------------------------------------------------------------- relax
 // ds_relax_ws over the packed queue: the load-balanced search of frontier.hpp
@@ -449,14 +468,14 @@ __global__ void __launch_bounds__(kBlock) ds_commit_dev(const int32_t* __restric
 // faster than 4 (101 VGPRs, 4 waves); 3 (89 / 5 waves) and 2 (76 / 6 waves) slower: too few
 // loads in flight per wave (profiles/r05s2_sssp_relax_e_ab.log, r05s4_sssp_relax_e45_ab.log).
 constexpr int kDsRelaxE = 5;
-template <bool kBins, bool kPart = false, bool kDone = false, int kE = kDsRelaxE>
-__global__ void __launch_bounds__(kBlock) ds_relax_dev(const int64_t* __restrict__ off, const int32_t* __restrict__ adj,
-        const int32_t* __restrict__ wt, const int64_t* __restrict__ light, const int32_t* __restrict__ q,
-        const int64_t* __restrict__ qpre, const int64_t* __restrict__ msg, int64_t* __restrict__ dist,
-        uint64_t* __restrict__ pend, int32_t* __restrict__ qn, int64_t* __restrict__ qpre_n, DsLoop* L, int cur,
-        int64_t delta, int nbins, int32_t* __restrict__ pile, int64_t cap, const uint64_t* __restrict__ done,
-        int64_t plo = 0, int64_t n_local = 0, int64_t* __restrict__ rbest = nullptr,
-        uint64_t* __restrict__ rmark = nullptr) {
+template <bool kBins, bool kPart, bool kDone, int kE>
+__device__ __forceinline__ void relax_body(int64_t bid, int64_t nb, const int64_t* __restrict__ off,
+        const int32_t* __restrict__ adj, const int32_t* __restrict__ wt, const int64_t* __restrict__ light,
+        const int32_t* __restrict__ q, const int64_t* __restrict__ qpre, const int64_t* __restrict__ msg,
+        int64_t* __restrict__ dist, uint64_t* __restrict__ pend, int32_t* __restrict__ qn,
+        int64_t* __restrict__ qpre_n, DsLoop* L, int cur, int64_t delta, int nbins, int32_t* __restrict__ pile,
+        int64_t cap, const uint64_t* __restrict__ done, int64_t plo, int64_t n_local, int64_t* __restrict__ rbest,
+        uint64_t* __restrict__ rmark) {
     static_assert(!(kBins && kPart), "the partitioned loop has no piles");
     const unsigned long long c = L->qc[cur];
     const int64_t qlen = qcount(c), total = qentries(c);
@@ -466,7 +485,7 @@ __global__ void __launch_bounds__(kBlock) ds_relax_dev(const int64_t* __restrict
     __shared__ unsigned int s_bn[kDsMaxBins];
     __shared__ unsigned long long s_bb[kDsMaxBins];
     bool spill = false;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (bid == 0 && threadIdx.x == 0) {
         L->phases += 1;
         L->relaxed += static_cast<unsigned long long>(total);
     }
@@ -477,7 +496,7 @@ __global__ void __launch_bounds__(kBlock) ds_relax_dev(const int64_t* __restrict
     bool bad = false;
     const int64_t ntiles = (total + (kBlock * kE) - 1) / (kBlock * kE);
     auto pre = [&](int64_t i) -> int64_t { return i < qlen ? qpre[i] : total; };
-    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    for (int64_t tile = bid; tile < ntiles; tile += nb) {
         const int64_t t0 = tile * (kBlock * kE);
         const int64_t t1 = min(total, t0 + (kBlock * kE));
         if (kBins && threadIdx.x < kDsMaxBins) s_bn[threadIdx.x] = 0;
@@ -642,6 +661,17 @@ __global__ void __launch_bounds__(kBlock) ds_relax_dev(const int64_t* __restrict
     }
     const long long m = block_min(tmin);
     if (threadIdx.x == 0 && m != kInf) atomicMin(&L->tm, m);
+}
+template <bool kBins, bool kPart = false, bool kDone = false, int kE = kDsRelaxE>
+__global__ void __launch_bounds__(kBlock) ds_relax_dev(const int64_t* __restrict__ off, const int32_t* __restrict__ adj,
+        const int32_t* __restrict__ wt, const int64_t* __restrict__ light, const int32_t* __restrict__ q,
+        const int64_t* __restrict__ qpre, const int64_t* __restrict__ msg, int64_t* __restrict__ dist,
+        uint64_t* __restrict__ pend, int32_t* __restrict__ qn, int64_t* __restrict__ qpre_n, DsLoop* L, int cur,
+        int64_t delta, int nbins, int32_t* __restrict__ pile, int64_t cap, const uint64_t* __restrict__ done,
+        int64_t plo = 0, int64_t n_local = 0, int64_t* __restrict__ rbest = nullptr,
+        uint64_t* __restrict__ rmark = nullptr) {
+    relax_body<kBins, kPart, kDone, kE>(blockIdx.x, gridDim.x, off, adj, wt, light, q, qpre, msg, dist, pend, qn,
+                                        qpre_n, L, cur, delta, nbins, pile, cap, done, plo, n_local, rbest, rmark);
 }
 
 // ---------------------------------------------------------------- 1-D partition
@@ -852,6 +882,132 @@ __global__ void ds_pull_flip(DsLoop* L) {
     if (threadIdx.x == 0 && blockIdx.x == 0 && L->xpull) L->pulls += 1;
 }
 
+// ---------------------------------------------------------------- small steps
+// Most of a run's ~90 steps are tiny: the tail of every bucket (a few queue entries, a few
+// hundred edges) and the run's end.  As four launches each, such a step costs ~20-30 us of
+// dispatch and host enqueue (profiles/r05t_sssp_timeline.txt: ~5 us per launch back to back,
+// ~7.5 us when the host is behind), for microseconds of work.  ds_small_steps runs them in ONE
+// block, looping decide -> extract -> commit -> relax with a barrier and an agent-scope acquire
+// (L1 invalidate: the other waves' atomics are performed in L2) between the phases — the same
+// bodies the grid kernels run, with one block.  It stops at the first step that is not small —
+// the queue or the extraction above small_q entries, or the committed queue above small_e
+// edges — leaving that step, already decided (and committed when big == 2), to the grid
+// kernels launched behind it (ds_*_dc: each returns at once unless big says it has work).
+// The queue buffer in use lives in DsLoop::cur, since the host does not know how many steps a
+// launch ran.  Not with the done filter or the pull form (the host keeps the four-launch step).
+struct DsQ {
+    int32_t* q0;
+    int32_t* q1;
+    int64_t* p0;
+    int64_t* p1;
+    // selects, not an indexed array: a runtime index into a kernel argument array is a
+    // private-memory (scratch) copy
+    __device__ int32_t* q(int c) const { return c ? q1 : q0; }
+    __device__ int64_t* qp(int c) const { return c ? p1 : p0; }
+};
+
+__device__ __forceinline__ void acquire_agent() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent"); }
+
+template <int kE>
+__global__ void __launch_bounds__(kBlock) ds_small_steps(const int64_t* __restrict__ off,
+        const int32_t* __restrict__ adj, const int32_t* __restrict__ wt, const int64_t* __restrict__ light,
+        uint64_t* __restrict__ pend, uint64_t* __restrict__ member, int64_t* __restrict__ dist,
+        int64_t* __restrict__ msg, DsQ qs, DsLoop* L, int64_t delta, int nbins, int32_t* __restrict__ pile,
+        int64_t cap, int32_t* __restrict__ mlist, uint64_t* __restrict__ done, int64_t scan_above, int max_steps,
+        int64_t small_q, int64_t small_e, DsPull nopull) {   // nopull: empty (a kernel argument: no scratch copy)
+    __shared__ int s_go, s_cur, s_mode;
+    if (threadIdx.x == 0 && L->big) {        // the grid kernels ran the previous launch's last step
+        L->cur ^= 1ULL;
+        L->big = 0;
+    }
+    for (int step = 0;; ++step) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            acquire_agent();
+            const int cur = static_cast<int>(L->cur);
+            int go = 0;
+            if (step < max_steps) {
+                decide_bins(L, cur, delta, nbins, cap, scan_above, 0);
+                if (!L->done) {
+                    const unsigned long long m = L->extract;
+                    if (m == 0) {
+                        const unsigned long long c = load_agent(&L->qc[cur]);
+                        go = qcount(c) <= small_q && qentries(c) <= small_e;
+                    } else if (m == 2) {
+                        go = static_cast<int64_t>(L->xcount + L->xm) <= small_q;
+                    }
+                    if (!go) L->big = 1;
+                }
+            }
+            s_go = go;
+            s_cur = cur;
+            s_mode = static_cast<int>(L->extract);
+        }
+        __syncthreads();
+        if (!s_go) break;                                    // block-uniform
+        const int cur = s_cur;
+        acquire_agent();
+        if (s_mode == 2)
+            extract_bins_body(0, 1, off, light, pend, member, dist, L, cur, pile, cap, mlist, done, qs.q(cur),
+                              qs.qp(cur), nopull);
+        __syncthreads();
+        acquire_agent();
+        commit_body<true>(0, 1, qs.q(cur), dist, msg, pend, member, L, cur, mlist);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            acquire_agent();
+            s_go = qentries(load_agent(&L->qc[cur])) <= small_e;
+            if (!s_go) L->big = 2;                           // committed: the grid relaxes it
+        }
+        __syncthreads();
+        if (!s_go) break;
+        acquire_agent();
+        relax_body<true, false, false, kE>(0, 1, off, adj, wt, light, qs.q(cur), qs.qp(cur), msg, dist, pend,
+                                           qs.q(cur ^ 1), qs.qp(cur ^ 1), L, cur, delta, nbins, pile, cap, nullptr,
+                                           0, 0, nullptr, nullptr);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            L->cur = static_cast<unsigned long long>(cur ^ 1);
+            L->small_steps += 1;
+        }
+    }
+}
+
+// The grid kernels behind ds_small_steps, on the step it left (buffer from DsLoop::cur).
+__global__ void __launch_bounds__(kBlock) ds_extract_dc(const int64_t* __restrict__ off,
+        const int64_t* __restrict__ light, uint64_t* __restrict__ pend, uint64_t* __restrict__ member,
+        const int64_t* __restrict__ dist, DsLoop* L, const int32_t* __restrict__ pile, int64_t cap,
+        const int32_t* __restrict__ mlist, uint64_t* __restrict__ done, DsQ qs, int64_t n, DsPull nopull) {
+    if (L->big != 1) return;                                 // grid-uniform
+    const int cur = static_cast<int>(L->cur);
+    const unsigned long long mode = L->extract;
+    if (mode == 1) {
+        extract_scan(off, light, pend, member, n, dist, L, cur, qs.q(cur), qs.qp(cur), done);
+        return;
+    }
+    if (mode != 2) return;
+    extract_bins_body(blockIdx.x, gridDim.x, off, light, pend, member, dist, L, cur, pile, cap, mlist, done,
+                      qs.q(cur), qs.qp(cur), nopull);
+}
+__global__ void __launch_bounds__(kBlock) ds_commit_dc(DsQ qs, const int64_t* __restrict__ dist,
+        int64_t* __restrict__ msg, uint64_t* __restrict__ pend, uint64_t* __restrict__ member, DsLoop* L,
+        int32_t* __restrict__ mlist) {
+    if (L->big != 1) return;
+    const int cur = static_cast<int>(L->cur);
+    commit_body<true>(blockIdx.x, gridDim.x, qs.q(cur), dist, msg, pend, member, L, cur, mlist);
+}
+template <int kE>
+__global__ void __launch_bounds__(kBlock) ds_relax_dc(const int64_t* __restrict__ off, const int32_t* __restrict__ adj,
+        const int32_t* __restrict__ wt, const int64_t* __restrict__ light, DsQ qs, const int64_t* __restrict__ msg,
+        int64_t* __restrict__ dist, uint64_t* __restrict__ pend, DsLoop* L, int64_t delta, int nbins,
+        int32_t* __restrict__ pile, int64_t cap) {
+    if (L->big == 0) return;
+    const int cur = static_cast<int>(L->cur);
+    relax_body<true, false, false, kE>(blockIdx.x, gridDim.x, off, adj, wt, light, qs.q(cur), qs.qp(cur), msg, dist,
+                                       pend, qs.q(cur ^ 1), qs.qp(cur ^ 1), L, cur, delta, nbins, pile, cap, nullptr,
+                                       0, 0, nullptr, nullptr);
+}
+
 }  // namespace
 
 static long long env_i64_dl(const char* name, long long dflt) {
@@ -917,6 +1073,30 @@ hipError_t k_ds_publish(const DsLoop* L, unsigned long long* host, unsigned long
     ds_publish<<<1, 64, 0, s>>>(L, host, seq);
     return hipGetLastError();
 }
+// TGO_DS_SMALL_Q / _E / _STEPS: a small step has at most small_q queue (or extraction)
+// entries and small_e edges; one launch runs at most _STEPS steps
+hipError_t k_ds_loop_step_small(const DevCsr& ws, const int64_t* light, uint64_t* pend, uint64_t* member, int64_t n,
+                                int64_t* dist, int64_t* msg, int32_t* const q[2], int64_t* const qpre[2], DsLoop* L,
+                                int64_t delta, int nbins, int32_t* pile, int64_t cap, int32_t* mlist, uint64_t* done,
+                                int64_t scan_above, hipStream_t s) {
+    if (nbins < 2 || nbins > kDsMaxBins || nbins > kBlock || cap < 1) return hipErrorInvalidValue;
+    static const int64_t sq = env_i64_dl("TGO_DS_SMALL_Q", 1024);
+    static const int64_t se = env_i64_dl("TGO_DS_SMALL_E", 4096);
+    static const int ss = static_cast<int>(env_i64_dl("TGO_DS_SMALL_STEPS", 64));
+    static const int cg = static_cast<int>(env_i64_dl("TGO_DS_CGRID", 1024));
+    static const int rg = static_cast<int>(env_i64_dl("TGO_DS_RGRID", 256 * 8));
+    const DsQ qs{q[0], q[1], qpre[0], qpre[1]};
+    ds_small_steps<kDsRelaxE><<<1, kBlock, 0, s>>>(ws.off, ws.adj, ws.w, light, pend, member, dist, msg, qs, L, delta,
+                                                   nbins, pile, cap, mlist, done, scan_above, ss, sq, se, DsPull{});
+    const int64_t words = (n + 63) / 64;
+    ds_extract_dc<<<extract_grid(words), kBlock, 0, s>>>(ws.off, light, pend, member, dist, L, pile, cap, mlist, done,
+                                                         qs, n, DsPull{});
+    ds_commit_dc<<<cg, kBlock, 0, s>>>(qs, dist, msg, pend, member, L, mlist);
+    ds_relax_dc<kDsRelaxE><<<rg, kBlock, 0, s>>>(ws.off, ws.adj, ws.w, light, qs, msg, dist, pend, L, delta, nbins,
+                                                 pile, cap);
+    return hipGetLastError();
+}
+
 hipError_t k_ds_loop_step_bins(const DevCsr& ws, const int64_t* light, uint64_t* pend, uint64_t* member, int64_t n,
                                int64_t* dist, int64_t* msg, int32_t* const q[2], int64_t* const qpre[2], DsLoop* L,
                                int cur, int64_t delta, int nbins, int32_t* pile, int64_t cap, int32_t* mlist,

@@ -515,6 +515,12 @@ struct DsLoop {
     unsigned long long pcount[2];         // members recorded per list
     unsigned long long xprev;   // entries of the previous pull's list the extraction clears
     unsigned long long bc[kDsMaxBins];    // pile counts
+    // small-step mode (ds_small_steps): the queue buffer in use, kept on the device because
+    // one launch runs a varying number of steps, and the step the launch left to the grid
+    // kernels: 0 none, 1 extract + commit + relax, 2 relax only
+    unsigned long long cur;
+    unsigned long long big;
+    unsigned long long small_steps;       // steps the single-block kernel ran
 };
 
 struct Scratch {
@@ -690,6 +696,13 @@ hipError_t k_ds_loop_step_bins(const DevCsr& ws, const int64_t* light, uint64_t*
                                int cur, int64_t delta, int nbins, int32_t* pile, int64_t cap, int32_t* mlist,
                                uint64_t* done, bool done_filter, int64_t scan_above, const DsPull& pull,
                                hipStream_t s);
+// the binned form with small steps (delta_loop.hip ds_small_steps): one launch runs the tiny
+// steps in one block, then the grid kernels the step it stopped at; queue buffer on the device
+// (DsLoop::cur).  Without the done filter and the pull form.
+hipError_t k_ds_loop_step_small(const DevCsr& ws, const int64_t* light, uint64_t* pend, uint64_t* member, int64_t n,
+                                int64_t* dist, int64_t* msg, int32_t* const q[2], int64_t* const qpre[2], DsLoop* L,
+                                int64_t delta, int nbins, int32_t* pile, int64_t cap, int32_t* mlist, uint64_t* done,
+                                int64_t scan_above, hipStream_t s);
 hipError_t k_ds_pending_min(const uint64_t* pend, int64_t words, const int64_t* dist, Counters* cnt, hipStream_t s);
 // partitioned loop state (delta.hip ds_track_reset): reset before an extraction; the header
 // all-to-all's result folded into {sent W, received W, global queue, pending min, -members}
