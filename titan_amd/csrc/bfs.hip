@@ -221,6 +221,7 @@ __global__ void __launch_bounds__(kBlock) td_expand_staged(View push, const int3
 // Bottom-up: one wave per 64-vertex bitmap word.  The next frontier is counted (vertices,
 // push entries), not queued: bfs_queue builds the queue from nb when the next level is
 // top-down.  No block barrier inside, so waves with long lists do not hold up the block.
+template <int kS>
 __global__ void __launch_bounds__(kBlock) bu_step(View pull, View push, int64_t n,
         const uint64_t* __restrict__ fb, uint64_t* __restrict__ vb, uint64_t* __restrict__ nb,
         int32_t* __restrict__ level, Counters* cnt, int32_t next_level, int64_t serial) {
@@ -241,19 +242,19 @@ __global__ void __launch_bounds__(kBlock) bu_step(View pull, View push, int64_t 
         const int64_t deg = (e0 - b0) + (e1 - b1);
         // short lists: the lane scans its own list and stops at the first frontier hit
         if (open && deg <= serial) {
-            // 4 entries per step: their index loads and bitmap probes issue together, so a
-            // lane pays one dependent round trip per 4 entries instead of per entry.
+            // kS entries per step: their index loads and bitmap probes issue together, so a
+            // lane pays one dependent round trip per kS entries instead of per entry.
             for (int l = 0; l < 2 && !found; ++l) {
                 const int32_t* adj = l == 0 ? pull.adj0 : pull.adj1;
                 const int64_t e = l == 0 ? e0 : e1;
-                for (int64_t k = l == 0 ? b0 : b1; k < e && !found; k += 4) {
-                    int32_t u[4];
+                for (int64_t k = l == 0 ? b0 : b1; k < e && !found; k += kS) {
+                    int32_t u[kS];
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) u[j] = k + j < e ? adj[k + j] : -1;
-                    uint64_t f[4];
+                    for (int j = 0; j < kS; ++j) u[j] = k + j < e ? adj[k + j] : -1;
+                    uint64_t f = 0;
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) f[j] = u[j] >= 0 ? fb[u[j] >> 6] >> (u[j] & 63) : 0;
-                    found = ((f[0] | f[1] | f[2] | f[3]) & 1ULL) != 0;
+                    for (int j = 0; j < kS; ++j) f |= u[j] >= 0 ? fb[u[j] >> 6] >> (u[j] & 63) : 0;
+                    found = (f & 1ULL) != 0;
                 }
             }
         }
@@ -541,8 +542,15 @@ hipError_t k_bu_step(const View& pull, const View& push, int64_t n, const uint64
     const int64_t words = (n + 63) / 64;
     // TGO_BFS_SERIAL: lists up to this many entries are scanned by their own lane (kSerialScan default)
     static const int64_t serial = [] { const char* e = std::getenv("TGO_BFS_SERIAL"); return e ? std::atoll(e) : kSerialScan; }();
-    bu_step<<<grid_for(words * 64, kBlock, 8192), kBlock, 0, s>>>(pull, push, n, fb, vb, nb, level, cnt, next_level,
-                                                                  serial);
+    // TGO_BFS_BU_STEP (A/B): entries per dependent round trip of a lane's own list
+    static const int bs = [] { const char* e = std::getenv("TGO_BFS_BU_STEP"); return e ? std::atoi(e) : 4; }();
+    const int g = grid_for(words * 64, kBlock, 8192);
+    if (bs == 8)
+        bu_step<8><<<g, kBlock, 0, s>>>(pull, push, n, fb, vb, nb, level, cnt, next_level, serial);
+    else if (bs == 2)
+        bu_step<2><<<g, kBlock, 0, s>>>(pull, push, n, fb, vb, nb, level, cnt, next_level, serial);
+    else
+        bu_step<4><<<g, kBlock, 0, s>>>(pull, push, n, fb, vb, nb, level, cnt, next_level, serial);
     return hipGetLastError();
 }
 hipError_t k_bfs_queue(const View& push, int64_t n, const uint64_t* fb, int32_t* qn, int64_t* qdeg, Counters* cnt,
