@@ -75,149 +75,6 @@ __global__ void __launch_bounds__(kBlock) td_expand(View push, const int32_t* __
     block_flush(cnt, sh, mf);
 }
 
-// td_expand with the tile's kE edges per thread in stages (delta_loop.hip ds_relax_dev's
-// form): the owners (LDS search), then the list entries, the visited words, the claiming
-// atomics and the new vertices' degrees, each stage's loads in flight together — td_expand
-// runs the whole search -> list -> bitmap -> atomic chain once per edge, 8 times over, with
-// a two-barrier block append after each.  The takes of a tile are appended with one
-// reservation.  Same vertices, levels and queue contents up to order.
-// kPart (part_td_claim's form, 1-D partition): targets outside [lo, lo + n_local) are marked
-// in the global discovered bitmap `disc` for their owners; owned ones are claimed by local id.
-template <int kE, bool kPart>
-__global__ void __launch_bounds__(kBlock) td_expand_staged(View push, const int32_t* __restrict__ q,
-        const int64_t* __restrict__ qpre, int64_t qlen, int32_t* __restrict__ level,
-        uint64_t* __restrict__ vb, uint64_t* __restrict__ nb, int32_t* __restrict__ qn,
-        int64_t* __restrict__ qdeg_n, Counters* cnt, int32_t next_level, uint64_t* __restrict__ disc = nullptr,
-        int64_t lo = 0, int64_t n_local = 0) {
-    constexpr int kT = kBlock * kE;
-    __shared__ int64_t s_pre[kT + 2];
-    __shared__ int32_t s_q[kT + 2];
-    __shared__ int64_t s_lo, s_hi;
-    __shared__ unsigned int s_wc[kWavesPerBlock];
-    __shared__ unsigned long long s_base;
-    __shared__ AppendLds sh;
-    unsigned long long mf = 0;
-    const int64_t total = qpre[qlen];
-    const int64_t ntiles = (total + kT - 1) / kT;
-    const int wave = threadIdx.x >> 6;
-    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const int64_t t0 = tile * kT;
-        const int64_t t1 = min(total, t0 + kT);
-        if (threadIdx.x == 0) {
-            int64_t a = 0, b = qlen;
-            while (b - a > 1) { const int64_t c = (a + b) >> 1; if (qpre[c] <= t0) a = c; else b = c; }
-            s_lo = a;
-            int64_t a2 = a, b2 = qlen;
-            while (b2 - a2 > 1) { const int64_t c = (a2 + b2) >> 1; if (qpre[c] <= t1 - 1) a2 = c; else b2 = c; }
-            s_hi = a2;
-        }
-        __syncthreads();
-        const int64_t qlo = s_lo, qhi = s_hi;
-        const int64_t span = qhi - qlo + 1;
-        const bool in_lds = span + 1 <= kT + 2;
-        if (in_lds) {
-            for (int64_t i = threadIdx.x; i <= span; i += kBlock) {
-                s_pre[i] = qpre[qlo + i];
-                if (i < span) s_q[i] = q[qlo + i];
-            }
-        }
-        __syncthreads();
-        int32_t u[kE];
-        int64_t o[kE];
-#pragma unroll
-        for (int k = 0; k < kE; ++k) {                       // 1: owner and offset
-            const int64_t j = t0 + k * kBlock + threadIdx.x;
-            u[k] = -1;
-            o[k] = 0;
-            if (j >= t1) continue;
-            int64_t start;
-            if (in_lds) {
-                int64_t a = 0, b = span;
-                while (b - a > 1) { const int64_t c = (a + b) >> 1; if (s_pre[c] <= j) a = c; else b = c; }
-                u[k] = s_q[a]; start = s_pre[a];
-            } else {
-                int64_t a = qlo, b = qhi + 1;
-                while (b - a > 1) { const int64_t c = (a + b) >> 1; if (qpre[c] <= j) a = c; else b = c; }
-                u[k] = q[a]; start = qpre[a];
-            }
-            o[k] = j - start;
-        }
-        int64_t v[kE];                                       // the target: local id, or -2 - global id (remote)
-#pragma unroll
-        for (int k = 0; k < kE; ++k) {                       // 2: the list entry
-            v[k] = -1;
-            if (u[k] < 0) continue;
-            int32_t t, w;
-            entry_at(push, u[k], o[k], t, w);
-            v[k] = t;
-            if constexpr (kPart) {
-                const int64_t x = static_cast<int64_t>(t) - lo;
-                v[k] = (x >= 0 && x < n_local) ? x : -2 - static_cast<int64_t>(t);
-            }
-        }
-        uint64_t vw[kE];
-#pragma unroll
-        for (int k = 0; k < kE; ++k)                         // 3: visited (or discovered) words
-            vw[k] = v[k] >= 0 ? vb[v[k] >> 6] : (kPart && v[k] <= -2 ? disc[(-2 - v[k]) >> 6] : ~0ULL);
-        int ntake = 0;
-        int64_t dsum = 0;
-        int64_t vd[kE];
-#pragma unroll
-        for (int k = 0; k < kE; ++k) {                       // 4: claim (or mark for the owner)
-            vd[k] = -1;
-            if (kPart && v[k] <= -2) {
-                const int64_t g = -2 - v[k];
-                const uint64_t bit = 1ULL << (g & 63);
-                if (!(vw[k] & bit)) atomicOr(reinterpret_cast<unsigned long long*>(&disc[g >> 6]), bit);
-                continue;
-            }
-            if (v[k] < 0) continue;
-            const uint64_t bit = 1ULL << (v[k] & 63);
-            if (vw[k] & bit) continue;
-            const unsigned long long old = atomicOr(reinterpret_cast<unsigned long long*>(&vb[v[k] >> 6]), bit);
-            if (old & bit) continue;
-            vd[k] = 0;
-        }
-#pragma unroll
-        for (int k = 0; k < kE; ++k) {                       // 5: the new vertices
-            if (vd[k] < 0) continue;
-            level[v[k]] = next_level;
-            atomicOr(reinterpret_cast<unsigned long long*>(&nb[v[k] >> 6]), 1ULL << (v[k] & 63));
-            vd[k] = push_degree(push, v[k]);
-            ++ntake;
-            dsum += vd[k];
-        }
-        // one reservation for the tile's takes (thread order within the block)
-        int incl = ntake;
-        for (int d = 1; d < 64; d <<= 1) {
-            const int y = __shfl_up(incl, d, 64);
-            if (lane() >= d) incl += y;
-        }
-        if (lane() == 63) s_wc[wave] = static_cast<unsigned int>(incl);
-        mf += static_cast<unsigned long long>(dsum);
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            unsigned int t = 0;
-            for (int w = 0; w < kWavesPerBlock; ++w) { const unsigned int c = s_wc[w]; s_wc[w] = t; t += c; }
-            s_base = t ? atomicAdd(&cnt->qlen, static_cast<unsigned long long>(t)) : 0ULL;
-        }
-        __syncthreads();
-        if (ntake) {
-            unsigned long long slot = s_base + s_wc[wave] + static_cast<unsigned long long>(incl - ntake);
-#pragma unroll
-            for (int k = 0; k < kE; ++k)
-                if (vd[k] >= 0) {
-                    qn[slot] = static_cast<int32_t>(v[k]);
-                    qdeg_n[slot] = vd[k];
-                    ++slot;
-                }
-        }
-        __syncthreads();
-    }
-    for (int d = 32; d > 0; d >>= 1) mf += __shfl_xor(mf, d, 64);     // block_flush takes lane 0's wave total
-    block_flush(cnt, sh, mf);
-}
-
 // Bottom-up: one wave per 64-vertex bitmap word.  The next frontier is counted (vertices,
 // push entries), not queued: bfs_queue builds the queue from nb when the next level is
 // top-down.  No block barrier inside, so waves with long lists do not hold up the block.
@@ -516,23 +373,10 @@ hipError_t k_bfs_seed(const View& push, int32_t* level, uint64_t* vb, uint64_t* 
     bfs_seed<<<1, 64, 0, s>>>(push, level, vb, fb, q, qdeg, seed);
     return hipGetLastError();
 }
-static int td_staged() {
-    const char* e = std::getenv("TGO_BFS_TD_STAGED");
-    return e ? std::atoi(e) : 4;
-}
 hipError_t k_td_expand(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen,
                        int32_t* level, uint64_t* vb, uint64_t* nb, int32_t* qn, int64_t* qdeg_n,
                        Counters* cnt, int32_t next_level, hipStream_t s) {
-    // TGO_BFS_TD_STAGED: edges per thread of the staged form (0 = td_expand).  4 (46 VGPRs,
-    // 12 KB of LDS, 8 waves per SIMD): 316 -> 330 GTEPS single-source hmean over 8 RMAT-24
-    // roots, 8 (68 VGPRs, 24 KB, 6 waves) 323 (profiles/r05td2_bfs_td_staged_ab.log)
-    static const int staged = td_staged();
-    if (staged == 8)
-        td_expand_staged<8, false><<<256 * 8, kBlock, 0, s>>>(push, q, qpre, qlen, level, vb, nb, qn, qdeg_n, cnt, next_level);
-    else if (staged == 4)
-        td_expand_staged<4, false><<<256 * 8, kBlock, 0, s>>>(push, q, qpre, qlen, level, vb, nb, qn, qdeg_n, cnt, next_level);
-    else
-        td_expand<<<256 * 8, kBlock, 0, s>>>(push, q, qpre, qlen, level, vb, nb, qn, qdeg_n, cnt, next_level);
+    td_expand<<<256 * 8, kBlock, 0, s>>>(push, q, qpre, qlen, level, vb, nb, qn, qdeg_n, cnt, next_level);
     return hipGetLastError();
 }
 hipError_t k_bu_step(const View& pull, const View& push, int64_t n, const uint64_t* fb, uint64_t* vb, uint64_t* nb,
@@ -652,12 +496,8 @@ hipError_t k_part_claim(const View& push, const uint64_t* recv, int nslices, int
 hipError_t k_part_td_claim(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen, uint64_t* disc,
                            uint64_t* vb, uint64_t* nb, int32_t* level, int32_t* qn, int64_t* qdeg_n, Counters* cnt,
                            int32_t next_level, int64_t lo, int64_t n_local, hipStream_t s) {
-    if (td_staged() == 4)                   // the staged form (k_td_expand), remote targets to disc
-        td_expand_staged<4, true><<<256 * 8, kBlock, 0, s>>>(push, q, qpre, qlen, level, vb, nb, qn, qdeg_n, cnt,
-                                                             next_level, disc, lo, n_local);
-    else
-        part_td_claim<<<256 * 8, kBlock, 0, s>>>(push, q, qpre, qlen, disc, vb, nb, level, qn, qdeg_n, cnt, next_level,
-                                                 lo, n_local);
+    part_td_claim<<<256 * 8, kBlock, 0, s>>>(push, q, qpre, qlen, disc, vb, nb, level, qn, qdeg_n, cnt, next_level, lo,
+                                             n_local);
     return hipGetLastError();
 }
 hipError_t k_unpermute_i64(const int64_t* in, const int32_t* perm, int64_t* out, int64_t n, hipStream_t s) {
