@@ -17,6 +17,8 @@ from titan_amd.distributed import (HipPartBackend, InProcessGroup, NativeExchang
                                    distributed_bfs_native, local_layout)
 
 scale = int(sys.argv[1]) if len(sys.argv) > 1 else 24
+# PART_ALPHA / PART_BETA: the partitioned loop's direction switch (default: distributed.BFS_ALPHA / _BETA)
+AB = {k: float(os.environ[e]) for k, e in (("alpha", "PART_ALPHA"), ("beta", "PART_BETA")) if e in os.environ}
 nroots = int(sys.argv[2]) if len(sys.argv) > 2 else 4
 n = 1 << scale
 src, dst, _ = rmat_edges(scale, 16, seed=0x54495441, device=0)
@@ -42,14 +44,14 @@ with torch.cuda.stream(st):
     be = HipPartBackend(eng, n, 0, n)
     x = NativeExchange.rccl(0, comm=InProcessGroup(1).comm(0))
     for r in good:
-        distributed_bfs_native(be, r, n, x, fetch=False, stats=False)            # warm
+        distributed_bfs_native(be, r, n, x, fetch=False, stats=False, **AB)            # warm
         torch.cuda.synchronize()
         t = time.perf_counter()
-        distributed_bfs_native(be, r, n, x, fetch=False, stats=False)
+        distributed_bfs_native(be, r, n, x, fetch=False, stats=False, **AB)
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t) * 1e3
         tp[r] = eng.stats()["last_kernel_ms"]
-        d, _, lv = distributed_bfs_native(be, r, n, x, fetch=True, stats=False)
+        d, _, lv = distributed_bfs_native(be, r, n, x, fetch=True, stats=False, **AB)
         print(f"partitioned world 1 root {r}: wall {ms:.3f} ms, kernel {tp[r]:.3f} ms, levels {lv}, "
               f"equal one-GPU {bool(np.array_equal(d, ref[r]))}", flush=True)
 print(f"sum one-GPU {sum(t1.values()):.3f} ms, partitioned {sum(tp.values()):.3f} ms, "

@@ -756,9 +756,15 @@ int run_bfs(tgo_ctx* ctx, int64_t seed, int max_depth, int scope) {
         int64_t qlen = 1;
         int cur = 0;
         bool bottom_up = false;
-        // Beamer's switch thresholds; TGO_BFS_ALPHA / TGO_BFS_BETA override for tuning.
-        static const double alpha = env_double("TGO_BFS_ALPHA", 15.0);
-        static const double beta = env_double("TGO_BFS_BETA", 18.0);
+        // Beamer's switch thresholds; TGO_BFS_ALPHA / TGO_BFS_BETA override for tuning.  Round 5:
+        // alpha 30 (bottom-up once the frontier's entries pass 1/30 of the unexplored ones) and
+        // beta 5000 (top-down again only below n/5000 frontier vertices), against Beamer's 15 / 18:
+        // hmean 301-318 -> 327-338 GTEPS over the 64 bench roots (profiles/r05ab_bfs_switch_ab.log).
+        // The roots that gain have a level-1 frontier of ~2300 hubs with ~18 M entries, just under
+        // mu / 15: top-down spent ~0.68 ms on that level, where the bottom-up finds nearly every
+        // vertex's parent among the hubs within a few entries.
+        static const double alpha = env_double("TGO_BFS_ALPHA", 30.0);
+        static const double beta = env_double("TGO_BFS_BETA", 5000.0);
         static const bool trace = env_double("TGO_TRACE", 0.0) != 0.0;
         // m_u: entries of unexplored vertices (push degrees); m_f: of the frontier.
         const int64_t total_push = push.nlists > 1 ? (g.out.nnz + g.in.nnz)

@@ -553,7 +553,15 @@ def _allreduce_counts(c, device, comm):
     return t.cpu().numpy()
 
 
-def distributed_bfs(backend, seed: int, max_depth: int, alpha: float = 15.0, beta: float = 18.0,
+# Direction switch of the single-source BFS (Beamer): bottom-up once the frontier's entries pass
+# 1/BFS_ALPHA of the unexplored ones, top-down again below n/BFS_BETA frontier vertices — the
+# one-GPU engine's defaults (api.cpp run_bfs, round 5: 30 / 5000 against Beamer's 15 / 18,
+# profiles/r05ab_bfs_switch_ab.log).
+BFS_ALPHA = 30.0
+BFS_BETA = 5000.0
+
+
+def distributed_bfs(backend, seed: int, max_depth: int, alpha: float = BFS_ALPHA, beta: float = BFS_BETA,
                     fetch: bool = True, stats: bool = True, group=None, comm=None):
     """ShortestDistance with unit weights over bothE on a vertex-partitioned graph.
     Returns (local distances or None, global reached [vertices, entries] or None, levels)."""
@@ -777,8 +785,8 @@ def _native_check(backend, rc):
         raise TitanException(rc, (backend.e.lib.tgo_last_error(backend.e.ctx) or b"").decode())
 
 
-def distributed_bfs_native(backend, seed: int, max_depth: int, exchange: NativeExchange, alpha: float = 15.0,
-                           beta: float = 18.0, fetch: bool = True, stats: bool = True):
+def distributed_bfs_native(backend, seed: int, max_depth: int, exchange: NativeExchange, alpha: float = BFS_ALPHA,
+                           beta: float = BFS_BETA, fetch: bool = True, stats: bool = True):
     """distributed_bfs as ONE native call (tgo_part_bfs_run).  Returns (local distances or
     None, global [reached vertices, entries] or None, levels)."""
     out = np.zeros(backend.n_local, np.int64) if fetch else None
