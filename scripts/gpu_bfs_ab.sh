@@ -7,7 +7,7 @@ TAG=$1; shift
 OUT=gpurun_out/$TAG; mkdir -p $OUT
 i=0
 for v in "$@"; do
-  env $v timeout -k 10 200 python3 scripts/bfs_probe.py 24 ${ROOTS:-8} > $OUT/bfs$i.log 2>&1 || { tail -5 $OUT/bfs$i.log; exit 1; }
+  env $v timeout -k 10 200 python3 scripts/bfs_probe.py ${SCALE:-24} ${ROOTS:-8} > $OUT/bfs$i.log 2>&1 || { tail -5 $OUT/bfs$i.log; exit 1; }
   echo "[$v] $(python3 -c "
 import re,sys
 g=[float(x) for x in re.findall(r'GTEPS ([0-9.]+)', open('$OUT/bfs$i.log').read())]
