@@ -381,14 +381,19 @@ hipError_t k_td_expand(const View& push, const int32_t* q, const int64_t* qpre, 
 }
 hipError_t k_bu_step(const View& pull, const View& push, int64_t n, const uint64_t* fb, uint64_t* vb, uint64_t* nb,
                      int32_t* level, Counters* cnt, int32_t next_level, hipStream_t s) {
-    // one wave per bitmap word, all launched at once: the dispatcher keeps every CU full
-    // and a wave's dependent probe chain overlaps with hundreds of others.
+    // one wave per bitmap word in a grid-stride loop: a wave's dependent probe chain overlaps
+    // with thousands of others.
     const int64_t words = (n + 63) / 64;
     // TGO_BFS_SERIAL: lists up to this many entries are scanned by their own lane (kSerialScan default)
     static const int64_t serial = [] { const char* e = std::getenv("TGO_BFS_SERIAL"); return e ? std::atoll(e) : kSerialScan; }();
     // TGO_BFS_BU_STEP (A/B): entries per dependent round trip of a lane's own list
     static const int bs = [] { const char* e = std::getenv("TGO_BFS_BU_STEP"); return e ? std::atoi(e) : 4; }();
-    const int g = grid_for(words * 64, kBlock, 8192);
+    // 2048 blocks (8192 waves: one resident round at 8 waves per SIMD), each wave walking 32
+    // words at RMAT-24: hmean 326-331 -> 368-371 GTEPS over the 64 bench roots against 8192
+    // blocks (4096: 346-360, 1024: 327, 16384: 276-279; profiles/r05bg_bfs_bu_grid_ab.log).
+    // (The multi-source pull, same one-wave-per-word shape at 7 waves per SIMD, is best at 8192:
+    // 3.66-3.68 ms per sweep against 4.14 at 2048 and 4.43-4.53 at its resident 1792.)
+    const int g = grid_for(words * 64, kBlock, 2048);
     if (bs == 8)
         bu_step<8><<<g, kBlock, 0, s>>>(pull, push, n, fb, vb, nb, level, cnt, next_level, serial);
     else if (bs == 2)
