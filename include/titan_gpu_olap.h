@@ -243,6 +243,10 @@ typedef struct {
     int64_t partition_rows;       /* non-canonical representative rows folded into them       */
     int64_t ghost_partition_rows; /* representative rows whose canonical row is absent or a
                                      ghost (PartitionedVertexProgramExecutor "partition-ghost") */
+    int64_t exact_reruns;         /* PageRank: 1 when the last program re-ran on the plain fp64
+                                     gather because a message left the fixed-point passes' exact
+                                     range (+inf from edgeCount 0 after a row cut, NaN, or a
+                                     magnitude outside [2^-53, 2^47 / longest row)); 0 otherwise */
 } tgo_stats;
 
 /* ---- Entry points ------------------------------------------------------------------- */

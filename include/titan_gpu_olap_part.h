@@ -155,6 +155,14 @@ int tgo_part_sssp_end(tgo_ctx* ctx, int64_t* dist_local, int64_t* reached);
 int tgo_part_pr_begin(tgo_ctx* ctx, const tgo_pr_args* args, double* contrib_local);
 int tgo_part_pr_step(tgo_ctx* ctx, const double* contrib_global, double* contrib_local);
 int tgo_part_pr_end(tgo_ctx* ctx, double* pr_local);
+/* The fixed-point passes of the blocked layout (tgo_part_pr_blocked) are exact only inside a
+ * range; a message outside it (+inf from a vertex whose row cut left it no OUT entry,
+ * PageRankVertexProgram.java:80-88; NaN; a magnitude past 2^47 / longest row) sets a flag.
+ * exact_check reads and clears it after end; when ANY rank reports bad = 1 every rank re-runs
+ * the program with plain = 1 (the plain layout's fp64 gather, Java double sums), then sets
+ * plain = 0.  tgo_part_pagerank_run does this itself. */
+int tgo_part_pr_exact_check(tgo_ctx* ctx, int32_t* bad);
+int tgo_part_pr_plain(tgo_ctx* ctx, int32_t on);
 
 /* Device-resident level counts for the BFS / multi-source BFS steps: with dev_counts (a
  * device int64[3]) set, the steps that return counts write {next queue length, its push

@@ -315,23 +315,31 @@ class NumpyPartBackend:
         idx = gathered_index(np.array(self.inn[v], np.int64), self.n_local, self.world, self.hot, self.span)
         return idx[idx < self.world * self.hot], idx[idx >= self.world * self.hot]
 
+    pr_bad = 0          # tgo_part_pr_exact_check: a non-finite message reached the blocked passes
+    plain = False       # tgo_part_pr_plain
+
     def pr_step_cold(self, gathered):
         g = gathered.numpy()        # only the cold region is complete here (hot gather in flight)
-        self.csum = np.array([g[self._split(v)[1]].sum() for v in range(self.n_local)])
+        cold = [g[self._split(v)[1]] for v in range(self.n_local)]
+        self.pr_bad |= int(any(not np.isfinite(c).all() for c in cold))
+        self.csum = np.array([c.sum() for c in cold])
 
     def pr_step_hot(self, gathered, contrib_local):
         g = gathered.numpy()
-        s = np.array([g[self._split(v)[0]].sum() for v in range(self.n_local)]) + self.csum
+        hot = [g[self._split(v)[0]] for v in range(self.n_local)]
+        self.pr_bad |= int(any(not np.isfinite(h).all() for h in hot))
+        s = np.array([h.sum() for h in hot]) + self.csum
         self.pr = self.alpha * s + self.base
         with np.errstate(divide="ignore"):
             contrib_local.numpy()[:] = self.pr / self.ec
 
     def pr_begin(self, alpha, N, iters, contrib_local):
-        self.alpha, self.base = alpha, (1 - alpha) / N
+        N = np.float64(N)                   # Java doubles: 1 / 0 = +inf
+        self.alpha, self.base = alpha, np.divide(1 - alpha, N)
         self.ec = np.array([float(len(o)) for o in self.out])
         self.pr = np.full(self.n_local, 1.0 / N)
         with np.errstate(divide="ignore"):
-            contrib_local.numpy()[:] = (1.0 / N) / self.ec
+            contrib_local.numpy()[:] = np.divide(1.0, N) / self.ec
 
     def pr_step(self, contrib_global, contrib_local):
         cg = contrib_global.numpy()
@@ -342,6 +350,13 @@ class NumpyPartBackend:
 
     def pr_end(self, fetch=True):
         return self.pr
+
+    def pr_exact_check(self):
+        b, self.pr_bad = self.pr_bad, 0
+        return b
+
+    def pr_plain(self, on):
+        self.plain = bool(on)
 
 
 def _free_port():
@@ -388,13 +403,20 @@ def _worker(rank, world, port, scale, roots, out_q, alpha):
         full = [torch.zeros(be.n_local, dtype=torch.float64) for _ in range(world)]
         dist.all_gather(full, torch.from_numpy(pr))
         res.setdefault("pr", []).append(torch.cat(full).numpy())
+    # vertexCount 0: every message +inf, outside the blocked passes' exact range — the ranks
+    # agree (all-reduce MAX of the flag) and re-run on the plain layout
+    be.pr_hot = 16
+    pr = distributed_pagerank(be, 0.85, 0, 5)
+    full = [torch.zeros(be.n_local, dtype=torch.float64) for _ in range(world)]
+    dist.all_gather(full, torch.from_numpy(pr))
+    res["pr_inf"] = (torch.cat(full).numpy(), be.plain)
     if rank == 0:
         out_q.put(res)
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,alpha", [(2, 15.0), (2, 1e9), (4, 15.0)])
+@pytest.mark.parametrize("world,alpha", [(2, 15.0), (2, 1e9), (4, 15.0), (8, 15.0)])
 def test_distributed_bfs_and_pagerank_match_oracle(world, alpha):
     import fulgora as fr
     from titan_amd import rmat_edges
@@ -429,6 +451,9 @@ def test_distributed_bfs_and_pagerank_match_oracle(world, alpha):
     for pr in res["pr"]:
         assert np.array_equal(np.isfinite(pr), fin)
         assert np.abs(pr[fin] - opr[fin]).sum() <= 1e-6
+    pinf, plain_left_on = res["pr_inf"]
+    assert np.array_equal(np.isposinf(pinf), np.isposinf(og.pagerank(0.85, 0, 5)[0])) and np.isposinf(pinf).all()
+    assert not plain_left_on
 
 
 def _sssp_worker(rank, world, port, scale, seeds, scope, deltas, out_q):

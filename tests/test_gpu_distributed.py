@@ -503,6 +503,39 @@ def test_native_bfs_sssp_pagerank_drivers(world, monkeypatch):
     assert np.array_equal(np.concatenate(py), got[0][0])
 
 
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_partitioned_pagerank_out_of_range_reruns_plain(world, monkeypatch):
+    """The blocked layout's fixed-point passes flag a message outside their exact range (spmv.hip
+    FxGuard); every rank then re-runs the program on the plain layout (all-reduced flag), in the
+    native loop (both exchanges) and the Python driver.  vertexCount = 0 makes every rank +inf
+    (Java 1/0), 2^60 puts every contribution below the 2^-53 floor; N = n stays blocked."""
+    from titan_amd.distributed import (NativeExchange, PR_EXCHANGE_ALLGATHER, PR_EXCHANGE_GHOST,
+                                       distributed_pagerank_native)
+    monkeypatch.setenv("TGO_PR_HOT", "512")
+    monkeypatch.setenv("TGO_PR_SEG", "256")
+    scale = 11
+    n = 1 << scale
+    if world == 3:
+        n = 3 * 704
+    src, dst, _ = rmat_edges(scale, 16, seed=61)
+    og = fr.OracleGraph.from_edges(n, src, dst)
+    ranks = Ranks(world, n, src, dst, L.SCOPE_IN_E, layout=True)
+    xs = NativeExchange.local_group(world)
+    for N in (0, 1 << 60, n):
+        opr, _ = og.pagerank(0.85, N, 7)
+        fin = np.isfinite(opr)
+        for mode in (PR_EXCHANGE_ALLGATHER, PR_EXCHANGE_GHOST):
+            res = ranks.run(lambda be, comm: distributed_pagerank_native(be, 0.85, N, 7, xs[comm.rank], mode=mode))
+            pr = np.concatenate([x[0] for x in res])
+            assert np.array_equal(np.isposinf(pr), np.isposinf(opr)) and np.array_equal(np.isnan(pr), np.isnan(opr))
+            assert np.allclose(pr[fin], opr[fin], rtol=1e-9, atol=0) and np.abs(pr[fin] - opr[fin]).sum() <= 1e-6
+            assert {be.e.stats()["exact_reruns"] for be in ranks.backends} == ({0} if N == n else {1})
+        py = np.concatenate(ranks.run(lambda be, comm: distributed_pagerank(be, 0.85, N, 7, comm=comm)))
+        assert np.array_equal(np.isposinf(py), np.isposinf(opr))
+        assert np.allclose(py[fin], opr[fin], rtol=1e-9, atol=0)
+        assert {be.e.stats()["exact_reruns"] for be in ranks.backends} == ({0} if N == n else {1})
+
+
 def test_native_drivers_rccl_world1():
     """The three native loops over the RCCL exchange (one rank)."""
     from titan_amd.distributed import (NativeExchange, distributed_bfs_native, distributed_pagerank_native,

@@ -776,6 +776,94 @@ def test_typed_scope_is_fitted_and_sees_only_its_label(scope):
         assert np.abs(pr[fin] - opr[fin]).sum() <= PR_L1_TOL
 
 
+def zero_edge_count_rows(n=2000, hubs=(0, 1, 2), k_in=40, k_out=3, seed=31):
+    """Rows where the column-order cut leaves vertices NO OUT entry while their neighbours still
+    read them (What's weak 1).  Two MULTI labels, `knows` (lower type id, so first in
+    column order; IDHandler.java:103-108) and `likes`.  Each hub receives k_in > limit `knows`
+    edges and sends k_out `likes` edges only: its row's user-edge slice is cut inside the `knows`
+    IN entries (ColumnValueStore.java:47-69 at QueryContainer's limit, :28,122), so its edgeCount
+    is 0 (PageRankVertexProgram.java:80-83), while each `likes` target's short row keeps the IN
+    entry and gathers the hub's contribution PR / 0 = +inf (:84-88)."""
+    import random
+    import edgestore as es
+    rnd = random.Random(seed)
+    knows, likes = es.user_edge_label(1), es.user_edge_label(2)
+    sd = {"edge_types": [{"type_id": knows, "multiplicity": 0}, {"type_id": likes, "multiplicity": 0}],
+          "property_keys": []}
+    osch = fr.OracleSchema(sd["edge_types"], [])
+    edges = []
+    for _ in range(2 * n):
+        a, b = rnd.randrange(len(hubs), n), rnd.randrange(len(hubs), n)
+        edges.append((a, b, knows if rnd.random() < 0.5 else likes, []))
+    for h in hubs:
+        edges += [(rnd.randrange(len(hubs), n), h, knows, []) for _ in range(k_in)]
+        edges += [(h, rnd.randrange(len(hubs), n), likes, []) for _ in range(k_out)]
+    rows, vids = es.build_rows(es.GraphSpec(n=n, edges=edges), osch)
+    return rows, vids, sd, osch
+
+
+def assert_pagerank_like_oracle(pr, opr):
+    """Java double semantics: the same +inf / NaN positions, finite ranks within 1e-6 L1."""
+    assert np.array_equal(np.isnan(pr), np.isnan(opr))
+    assert np.array_equal(np.isposinf(pr), np.isposinf(opr)) and np.array_equal(np.isneginf(pr), np.isneginf(opr))
+    fin = np.isfinite(opr)
+    assert np.abs(pr[fin] - opr[fin]).sum() <= PR_L1_TOL
+
+
+@pytest.mark.parametrize("split", ["1", "2"])
+@pytest.mark.parametrize("cold_fx", ["1", "0"])
+def test_pagerank_infinite_contribution_after_cut(split, cold_fx, monkeypatch):
+    """The fixed-point PageRank passes (spmv.hip gather_hot_fx / cold_fx) cannot hold +inf:
+    a message outside their exact range flags the layout and the program re-runs on the plain
+    fp64 gather, so the +inf a zero-edgeCount vertex sends spreads exactly as Java doubles do.
+    Forced onto the cache-blocked layout with a tiny hot set; through tgo_load_rows."""
+    monkeypatch.setenv("TGO_PR_HOT", "64")
+    monkeypatch.setenv("TGO_PR_SEG", "128")
+    monkeypatch.setenv("TGO_PR_FX_SPLIT", split)
+    monkeypatch.setenv("TGO_PR_FX_COLD", cold_fx)
+    rows, vids, sd, osch = zero_edge_count_rows()
+    limit, n = 24, len(vids)
+    o = fr.OracleGraph.from_rows(rows, osch, IN, hard_limit=limit)
+    eng = Engine(hard_query_limit=limit).load_rows(rows, Schema.from_dict(sd), IN, batch_rows=64)
+    assert eng.stats()["truncated_results"] == o.stats.truncated_results >= 3
+    for iters in (2, 3, 8):
+        opr = o.pagerank(0.85, n, iters)[0]
+        assert np.isposinf(opr).sum() >= 3 and np.isfinite(opr).sum() > n // 2    # the fixture reaches the case
+        pr = eng.pagerank(0.85, n, iters)
+        assert_pagerank_like_oracle(pr, opr)
+        assert eng.stats()["exact_reruns"] == 1
+        assert np.array_equal(pr, eng.pagerank(0.85, n, iters), equal_nan=True)
+    # the slot form of the blocked layout (TGO_PR_FX=0) sums doubles itself: no re-run, same ranks
+    monkeypatch.setenv("TGO_PR_FX", "0")
+    slot = Engine(hard_query_limit=limit).load_rows(rows, Schema.from_dict(sd), IN, batch_rows=64)
+    sp = slot.pagerank(0.85, n, 8)
+    assert slot.stats()["exact_reruns"] == 0
+    assert_pagerank_like_oracle(sp, o.pagerank(0.85, n, 8)[0])
+    fin = np.isfinite(sp)
+    assert np.array_equal(fin, np.isfinite(pr)) and np.abs(sp[fin] - pr[fin]).sum() <= 1e-12
+
+
+def test_pagerank_out_of_range_parameters(rmat12, monkeypatch):
+    """vertexCount is a user parameter (PageRankVertexProgram.java:54): N = 0 makes every rank
+    +inf (1/0 in Java doubles), N = 2^60 puts every contribution below the fixed-point form's
+    2^-53 floor.  Both re-run on the fp64 gather and match the oracle."""
+    monkeypatch.setenv("TGO_PR_HOT", "512")
+    monkeypatch.setenv("TGO_PR_SEG", "256")
+    n, src, dst, w, ids, oracle, roots = rmat12
+    eng = Engine().load_edges(n, src, dst, IN)
+    pr = eng.pagerank(0.85, 0, 6)
+    assert eng.stats()["exact_reruns"] == 1 and np.isposinf(pr).all()
+    assert_pagerank_like_oracle(pr, oracle.pagerank(0.85, 0, 6)[0])
+    big = 1 << 60
+    pr = eng.pagerank(0.85, big, 6)
+    assert eng.stats()["exact_reruns"] == 1
+    opr = oracle.pagerank(0.85, big, 6)[0]
+    assert np.allclose(pr, opr, rtol=1e-12, atol=0)
+    pr = eng.pagerank(0.85, n, 6)                      # back in range: the fixed-point passes
+    assert eng.stats()["exact_reruns"] == 0
+    assert np.abs(pr - oracle.pagerank(0.85, n, 6)[0]).sum() <= PR_L1_TOL
+
+
 def test_rows_with_sort_key_weights_and_string_properties():
     """Codec breadth through the device load: a MULTI label whose sort key is
     (String, Float, weight) in DESC order, a String + Double signature and String / Date /

@@ -141,7 +141,7 @@ class Stats(C.Structure):
                 ("levels", C.c_int32), ("reached", C.c_int64), ("reached_entries", C.c_int64),
                 ("load_ms", C.c_double), ("last_kernel_ms", C.c_double), ("device_bytes", C.c_int64),
                 ("relaxed_entries", C.c_int64), ("partitioned_vertices", C.c_int64),
-                ("partition_rows", C.c_int64), ("ghost_partition_rows", C.c_int64)]
+                ("partition_rows", C.c_int64), ("ghost_partition_rows", C.c_int64), ("exact_reruns", C.c_int64)]
 
 
 # Every symbol include/*.h declares (checked by tests/test_abi.py).
@@ -157,7 +157,8 @@ EXPORTS = [
     "tgo_rmat_edges", "tgo_rmat_edges_device", "tgo_rmat_partition_device", "tgo_pick_roots", "tgo_synth_rows",
     # titan_gpu_olap_part.h (1-D vertex-partitioned multi-GPU)
     "tgo_load_partition", "tgo_part_layout", "tgo_load_partition_layout", "tgo_part_bfs_begin", "tgo_part_bfs_td", "tgo_part_bfs_claim", "tgo_part_bfs_bu",
-    "tgo_part_bfs_end", "tgo_part_pr_begin", "tgo_part_pr_step", "tgo_part_pr_end", "tgo_rmat_partition",
+    "tgo_part_bfs_end", "tgo_part_pr_begin", "tgo_part_pr_step", "tgo_part_pr_end", "tgo_part_pr_exact_check", "tgo_part_pr_plain",
+    "tgo_rmat_partition",
     "tgo_part_active_rows", "tgo_part_pr_blocked", "tgo_part_device_counts", "tgo_part_set_local_qlen", "tgo_part_ms_pack_dev", "tgo_part_pr_step_cold", "tgo_part_pr_step_hot",
     "tgo_part_ms_begin", "tgo_part_ms_pull", "tgo_part_ms_push", "tgo_part_ms_settle", "tgo_part_ms_end",
     "tgo_part_ms_pack", "tgo_part_ms_settle_pairs", "tgo_part_ms_pack_fixed", "tgo_part_ms_settle_fixed",
@@ -261,6 +262,8 @@ def load() -> C.CDLL:
         "tgo_part_pr_begin": (C.c_int, [vp, P(PrArgs), vp]),
         "tgo_part_pr_step": (C.c_int, [vp, vp, vp]),
         "tgo_part_pr_end": (C.c_int, [vp, C.POINTER(C.c_double)]),
+        "tgo_part_pr_exact_check": (C.c_int, [vp, C.POINTER(C.c_int32)]),
+        "tgo_part_pr_plain": (C.c_int, [vp, C.c_int32]),
         "tgo_part_active_rows": (C.c_int, [vp, _i64p]),
         "tgo_part_device_counts": (C.c_int, [vp, vp]),
         "tgo_part_set_local_qlen": (C.c_int, [vp, C.c_int64]),

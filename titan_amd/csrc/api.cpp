@@ -59,6 +59,7 @@ struct tgo_ctx {
     int32_t part_pr_iter = 0;   // partitioned PageRank: iteration reached / program length
     int32_t part_pr_iters = 0;
     int32_t part_pr_world = 0;  // blocked gathered layout (tgo_part_pr_blocked): world, H, A
+    bool part_pr_plain = false; // tgo_part_pr_plain: the plain layout although the blocked one is built
     int64_t part_pr_hot = 0, part_pr_span = 0;
     int64_t part_relaxed = 0;   // partitioned SSSP: entries relaxed, phases
     int32_t part_phases = 0;
@@ -284,6 +285,16 @@ int upload_row_blocks_dev(tgo_ctx* ctx, const std::vector<int64_t>& off, RowBloc
     return TGO_OK;
 }
 
+// Biased-exponent range [elo, ehi) in which the fixed-point PageRank sums are exact (spmv.hip
+// kFxPoint): |v| >= 2^-53 (the 2^-80 resolution then costs < 2^-27 of a value), and a row of
+// max_len entries below 2^47 (|v| < 2^(47 - c) with 2^c >= max_len).
+void fx_range(int64_t max_len, int& elo, int& ehi) {
+    int c = 0;
+    while ((int64_t(1) << c) < max_len && c < 47) ++c;
+    elo = 1023 - 53;
+    ehi = 1023 + 47 - c;
+}
+
 // Cache-blocked PageRank in-lists of the rows [0, n_rows) (rows past n_rows have no entries)
 // over sources [0, n_src): built on the device from the uploaded in-lists (d_off / d_adj,
 // pr_layout.hip) unless TGO_HOST_ASSEMBLY=1 (or a row is not sorted by source), then on the
@@ -478,8 +489,34 @@ int upload_cold_blocks(tgo_ctx* ctx, const std::vector<int64_t>& off, const std:
     HIP_TRY(hipMemset(cb.csum, 0, std::max<int64_t>(cb.n_rows, 1) * sizeof(double)));
     cb.n_crows = static_cast<int64_t>(hc.crow.size());
     HIP_TRY(upload(ctx, cb.crow, hc.crow));
+    if (cb.fx || cb.cfx) {                          // the fixed-point passes' range flag (FxGuard)
+        int64_t max_len = 0;
+        for (size_t r = 0; r + 1 < off.size(); ++r) max_len = std::max(max_len, off[r + 1] - off[r]);
+        fx_range(max_len, cb.fx_elo, cb.fx_ehi);
+        HIP_TRY(dev_alloc(ctx, cb.fx_bad, 1));
+        HIP_TRY(hipMemset(cb.fx_bad, 0, sizeof(unsigned)));
+    }
     lap("uploads");
     ready = true;
+    return TGO_OK;
+}
+
+// After a program's updates: did any fixed-point pass see a message outside its exact range?
+// Clears the flag.  (A synchronising read, once per program.)
+int fx_take_bad(tgo_ctx* ctx, ColdBlocks& cb, bool* bad) {
+    *bad = false;
+    if (!cb.fx_bad) return TGO_OK;
+    unsigned h = 0;
+    HIP_TRY(hipMemcpyAsync(&h, cb.fx_bad, sizeof(unsigned), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    if (h) {
+        HIP_TRY(hipMemsetAsync(cb.fx_bad, 0, sizeof(unsigned), ctx->stream));
+        // a long row's accumulators may hold the discarded run's chunks: back to zero
+        if (cb.fx_long_acc)
+            HIP_TRY(hipMemsetAsync(cb.fx_long_acc, 0, 2 * std::max<int64_t>(cb.fx_nlong, 1) * sizeof(unsigned long long),
+                                   ctx->stream));
+        *bad = true;
+    }
     return TGO_OK;
 }
 
@@ -1947,13 +1984,16 @@ int tgo_pagerank(tgo_ctx* ctx, const tgo_pr_args* a, double* pr_out) {
     double* contrib_next = s.vec[2];
     double* pr = reinterpret_cast<double*>(s.dist);    // int64-sized scratch reused for PR
     const double N = static_cast<double>(a->vertex_count);
+    ctx->st.exact_reruns = 0;
+    const PrTuning tune = pr_tuning();
+    bool blocked = g.cold_in_ready && tune.diag_hi <= tune.diag_lo;
     if (a->max_iterations == 0) {
         HIP_TRY(k_fill_f64(pr, NAN, n, st));           // iteration 0 sets no PAGE_RANK property
-    } else {
+    } else for (;;) {
+        contrib = s.vec[1];
+        contrib_next = s.vec[2];
         HIP_TRY(k_pr_init(g.out, edge_count, contrib, pr, 1.0 / N, n, st));
         const double base = (1.0 - a->alpha) / N;
-        const PrTuning tune = pr_tuning();
-        const bool blocked = g.cold_in_ready && tune.diag_hi <= tune.diag_lo;
         for (int it = 2; it <= a->max_iterations; ++it) {
             // the PAGE_RANK property is only read after the last superstep: write it there
             double* pr_it = it == a->max_iterations ? pr : nullptr;
@@ -1961,11 +2001,11 @@ int tgo_pagerank(tgo_ctx* ctx, const tgo_pr_args* a, double* pr_out) {
             if (blocked) {
                 {
                     DevSpan ph(st, "pagerank.window_cold_phase", {"iteration", it});
-                    HIP_TRY(k_pr_cold_phase(g.cold_in, contrib, st));
+                    HIP_TRY(k_pr_cold_phase(g.cold_in, contrib, st, it == 2));
                 }
                 DevSpan ph(st, "pagerank.hot_phase", {"iteration", it});
                 HIP_TRY(k_pr_hot_phase(g.cold_in, contrib, edge_count, pr_it, contrib_next, s.partial, a->alpha, base,
-                                       st));
+                                       st, it == 2));
             } else
                 HIP_TRY(k_pr_iter(g.in, g.rb_in, contrib, edge_count, pr_it, contrib_next, s.partial, a->alpha, base,
                                   n, tune, st));
@@ -1973,6 +2013,15 @@ int tgo_pagerank(tgo_ctx* ctx, const tgo_pr_args* a, double* pr_out) {
         }
         if (blocked && a->max_iterations >= 2 && g.cold_in.n_rows < n)   // entry-less rows: PR = (1-a)/N
             HIP_TRY(k_fill_f64(pr + g.cold_in.n_rows, base, n - g.cold_in.n_rows, st));
+        // a message outside the fixed-point passes' exact range (an infinity from edgeCount 0,
+        // NaN, or a magnitude the 128-bit form cannot hold): the whole program again on the
+        // plain fp64 gather, whose sums are Java double sums
+        bool bad = false;
+        if (blocked && a->max_iterations >= 2)
+            if (int rc = fx_take_bad(ctx, g.cold_in, &bad)) return rc;
+        if (!bad) break;
+        blocked = false;
+        ++ctx->st.exact_reruns;
     }
     HIP_TRY(hipEventRecord(ctx->ev1, st));
     HIP_TRY(hipEventSynchronize(ctx->ev1));
@@ -2914,13 +2963,37 @@ int tgo_part_pr_begin(tgo_ctx* ctx, const tgo_pr_args* a, double* contrib_local)
     ctx->part_base = (1.0 - a->alpha) / N;
     ctx->part_pr_iter = 1;
     ctx->part_pr_iters = a->max_iterations;
+    if (!ctx->part_pr_plain) ctx->st.exact_reruns = 0;
     HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
     // iteration 1 (PageRankVertexProgram.java:78-83) on the owned rows
     HIP_TRY(k_pr_init(g.out, s.vec[0], contrib_local, reinterpret_cast<double*>(s.dist), 1.0 / N, g.n, ctx->stream));
     return part_done(ctx);
 }
 
-static bool part_pr_blocked_ready(const tgo_ctx* ctx) { return ctx->part_pr_world > 0 && ctx->g.cold_in_ready; }
+static bool part_pr_blocked_ready(const tgo_ctx* ctx) {
+    return ctx->part_pr_world > 0 && ctx->g.cold_in_ready && !ctx->part_pr_plain;
+}
+
+// The fixed-point passes' range flag of the last partitioned PageRank (read and cleared).
+int tgo_part_pr_exact_check(tgo_ctx* ctx, int32_t* bad) {
+    int rc = part_check(ctx);
+    if (rc) return rc;
+    if (!bad) return fail(ctx, TGO_E_INVALID, "null argument");
+    bool b = false;
+    if (part_pr_blocked_ready(ctx) && (rc = fx_take_bad(ctx, ctx->g.cold_in, &b))) return rc;
+    *bad = b ? 1 : 0;
+    return TGO_OK;
+}
+
+// Run the next partitioned PageRank programs on the plain layout (rank-major n_local slices,
+// fp64 gather) while on = 1, keeping the blocked layout for later ones.
+int tgo_part_pr_plain(tgo_ctx* ctx, int32_t on) {
+    int rc = part_check(ctx);
+    if (rc) return rc;
+    ctx->part_pr_plain = on != 0;
+    if (on) ctx->st.exact_reruns = 1;                // the stats of the program that re-runs
+    return TGO_OK;
+}
 
 // the PAGE_RANK property is only read after the last superstep: write it there
 static double* part_pr_out(tgo_ctx* ctx) {
@@ -2931,7 +3004,7 @@ int tgo_part_pr_step_cold(tgo_ctx* ctx, const double* gathered) {
     int rc = part_check(ctx);
     if (rc) return rc;
     if (!part_pr_blocked_ready(ctx)) return fail(ctx, TGO_E_STATE, "tgo_part_pr_step_cold needs tgo_part_pr_blocked");
-    HIP_TRY(k_pr_cold_phase(ctx->g.cold_in, gathered, ctx->stream));
+    HIP_TRY(k_pr_cold_phase(ctx->g.cold_in, gathered, ctx->stream, ctx->part_pr_iter == 1));
     return part_done(ctx);
 }
 
@@ -2942,7 +3015,7 @@ int tgo_part_pr_step_hot(tgo_ctx* ctx, const double* gathered, double* contrib_l
     if (ctx->part_pr_iter >= ctx->part_pr_iters) return fail(ctx, TGO_E_STATE, "PageRank program already complete");
     Scratch& s = ctx->sc;
     HIP_TRY(k_pr_hot_phase(ctx->g.cold_in, gathered, s.vec[0], part_pr_out(ctx), contrib_local, s.partial,
-                           ctx->part_alpha, ctx->part_base, ctx->stream));
+                           ctx->part_alpha, ctx->part_base, ctx->stream, ctx->part_pr_iter == 1));
     ++ctx->part_pr_iter;
     return part_done(ctx);
 }
@@ -3609,7 +3682,7 @@ bool ms_ghost_of(const tgo_ctx* ctx) { return ctx->ms_ghost != 0; }
 // the blocked gathered layout of the last tgo_part_pr_blocked (world 0: plain layout)
 int part_pr_layout_of(tgo_ctx* ctx, int32_t* world, int64_t* hot, int64_t* span) {
     if (int rc = part_check(ctx)) return rc;
-    const bool blocked = ctx->part_pr_world > 0 && ctx->g.cold_in_ready;
+    const bool blocked = part_pr_blocked_ready(ctx);
     *world = blocked ? ctx->part_pr_world : 0;
     *hot = blocked ? ctx->part_pr_hot : 0;
     *span = blocked ? ctx->part_pr_span : ctx->g.n;

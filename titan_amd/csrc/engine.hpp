@@ -376,6 +376,11 @@ struct ColdBlocks {
     int fx_split = 0;
     int64_t* fx_mid = nullptr;          // (S + 1) per tile: its entry bounds of the source ranges
     unsigned long long* fx_part = nullptr;       // 2 per hot row (low, high word)
+    // exact range of the fixed-point passes (fx or cfx; spmv.hip FxGuard): nonzero messages with
+    // a biased exponent outside [fx_elo, fx_ehi) set *fx_bad, and the program re-runs on the plain
+    // fp64 gather (fx_ehi from the longest in-list: a row of D entries stays below 2^47)
+    int fx_elo = 0, fx_ehi = 0x800;
+    unsigned* fx_bad = nullptr;
 };
 struct HostColdBlocks {
     int64_t hot = 0, seg = 0;
@@ -816,15 +821,17 @@ hipError_t k_pr_iter(const DevCsr& in, const RowBlocks& rb, const double* contri
                      const double* edge_count, double* pr, double* contrib_next, double* partial,
                      double alpha, double base, int64_t n, const PrTuning& t, hipStream_t s);
 hipError_t k_fill_f64(double* p, double v, int64_t n, hipStream_t s);
-hipError_t k_pr_cold_phase(const ColdBlocks& cb, const double* contrib, hipStream_t s);
+// guard_entries (the first rank update of a program): every gathered message is checked against
+// the fixed-point passes' exact range (FxGuard); later updates check only the emitted
+// contributions, one per row (PrFinal)
+hipError_t k_pr_cold_phase(const ColdBlocks& cb, const double* contrib, hipStream_t s, bool guard_entries);
 // per fixed-point hot tile (desc, packed source << rbits | row): the first entry with source >= hs
 // first > 0: the first range is [0, first) (TGO_PR_FX_SPLIT_AT), else S even ranges
 hipError_t k_fx_split_points(const uint32_t* padj, const int64_t* desc, int64_t ntiles, int rbits, int64_t hot,
                              int nsplit, int64_t first, int64_t* bnd, hipStream_t s);
 hipError_t k_pr_hot_phase(const ColdBlocks& cb, const double* contrib, const double* edge_count, double* pr,
-                          double* contrib_next, double* partial_long, double alpha, double base, hipStream_t s);
-hipError_t k_pr_iter_cold(const ColdBlocks& cb, const double* contrib, const double* edge_count, double* pr,
-                          double* contrib_next, double* partial_long, double alpha, double base, hipStream_t s);
+                          double* contrib_next, double* partial_long, double alpha, double base, hipStream_t s,
+                          bool guard_entries);
 hipError_t k_walk_iter(const DevCsr& out, const RowBlocks& rb, const int32_t* prev, int32_t* next,
                        int32_t* partial, int64_t n, hipStream_t s);
 

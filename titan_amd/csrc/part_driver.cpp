@@ -909,6 +909,7 @@ extern "C" int tgo_part_pagerank_run(tgo_ctx* ctx, tgo_exchange* x, const tgo_pr
         }
     }
     int64_t moved = 0;
+  rerun:
     if ((rc = tgo_part_pr_begin(ctx, args, contrib))) return rc;
     for (int it = 2; it <= args->max_iterations; ++it) {
         DevSpan upd(st, "part.pagerank.update", {"iteration", it}, {"ghost", gh ? 1 : 0});
@@ -939,8 +940,27 @@ extern "C" int tgo_part_pagerank_run(tgo_ctx* ctx, tgo_exchange* x, const tgo_pr
         if ((rc = tgo_part_pr_step(ctx, gath, contrib))) break;
     }
     trace_resolve(st);
-    if (rc) { x->abort(); return rc; }
-    if ((rc = tgo_part_pr_end(ctx, pr_local))) return rc;
+    if (rc) { x->abort(); tgo_part_pr_plain(ctx, 0); return rc; }
+    if (hot > 0) {
+        // a message outside the fixed-point passes' exact range on ANY rank (+inf from a vertex
+        // whose row cut left it no OUT entry, NaN, ...): every rank re-runs the program on the
+        // plain fp64 gather (rank-major all-gather layout), whose sums are Java double sums
+        int32_t bad = 0;
+        if ((rc = tgo_part_pr_exact_check(ctx, &bad))) { x->abort(); return rc; }
+        int64_t b = bad, any = 0;
+        if ((rc = d.reduce(&b, 1, tgo_exchange::kRedMax, &any))) return rc;
+        if (any) {
+            if ((rc = tgo_part_pr_plain(ctx, 1))) return rc;
+            hot = 0;
+            span = nl;
+            gh = nullptr;
+            if ((rc = scratch(ctx, gath, static_cast<int64_t>(W) * span, 19))) { tgo_part_pr_plain(ctx, 0); return rc; }
+            goto rerun;
+        }
+    }
+    rc = tgo_part_pr_end(ctx, pr_local);
+    tgo_part_pr_plain(ctx, 0);
+    if (rc) return rc;
     if (exchanged_bytes) *exchanged_bytes = moved;
     return TGO_OK;
 }

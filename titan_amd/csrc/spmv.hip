@@ -63,10 +63,24 @@ __device__ __forceinline__ T wave_sum(T x) {
 // Finalisers: what a vertex does with its gathered sum.
 struct PrFinal {
     const double* edge_count; double* pr; double* contrib_next; double alpha; double base;
+    // fixed-point layouts: a contribution outside [2^(elo-1023), 2^(ehi-1023)) sets *bad (FxGuard)
+    unsigned* bad = nullptr;
+    unsigned elo = 0, ehi = 0x800;
     __device__ __forceinline__ void operator()(int64_t r, double sum) const {
         const double p = (alpha * sum) + base;      // PageRankVertexProgram.java:86
         if (pr) pr[r] = p;                          // the PAGE_RANK property: read after the last update only
-        contrib_next[r] = p / __builtin_nontemporal_load(edge_count + r);   // :88, edgeCount 0 => +inf (never read)
+        // :88, edgeCount 0 => +inf.  It IS read when a row cut (QueryContainer.java:28,122) left
+        // the vertex no OUT entry but a neighbour's row still holds its IN entry: the fixed-point
+        // passes' first-update entry check flags it (FxGuard; edgeCount never changes), and the
+        // program re-runs on the plain fp64 gather.  Every other contribution is checked here.
+        const double ec = __builtin_nontemporal_load(edge_count + r);
+        const double c = p / ec;
+        contrib_next[r] = c;
+        if (bad && ec != 0.0) {
+            const unsigned long long b = static_cast<unsigned long long>(__double_as_longlong(c));
+            const unsigned e = static_cast<unsigned>(b >> 52) & 0x7FFu;
+            if ((b << 1) != 0 && e - elo >= ehi - elo) *bad = 1u;
+        }
     }
 };
 // Cache-blocked form: the row's cold sum (its pieces in segment order, cold_fold) is added
@@ -477,24 +491,36 @@ __global__ void __launch_bounds__(kThreads, 4) gather_hot_pipe(const int64_t* __
 // a tile needs one LDS accumulator per row, not one slot per entry, and grows to 64 K entries
 // (super-tiles, pack_supertiles_device) — its source-sorted entries then share lines: 0.29 L2
 // requests per hot entry at RMAT-24 (host count over the bench graph, 64 K entries / 4096 rows).
-// The conversion of the exact sum back to a double rounds once; the reference's fp64 sum
-// (PageRankVertexProgram.java:84-89, VertexMemoryHandler.java:97-102) rounds once per entry.
+// The conversion of the exact sum back to a double rounds once (fx_to_double, nearest-even);
+// the reference's fp64 sum (PageRankVertexProgram.java:84-89, VertexMemoryHandler.java:97-102)
+// rounds once per entry.
+//
+// The form is exact only inside a range: a nonzero |v| below 2^-53 loses more than 2^-27 of
+// itself to the 2^-80 resolution, and a row of D entries overflows the 2^47 range unless every
+// |v| < 2^47 / D.  Infinities and NaN — the +inf contribution of a vertex whose row cut left it
+// no OUT entry (PageRankVertexProgram.java:80-88 divides by edgeCount 0) — have no fixed-point
+// form at all.  Every entry is checked against the layout's range (FxGuard: biased exponents
+// [elo, ehi), from the longest row); one outside it sets *bad, and the caller re-runs the whole
+// program on the plain fp64 gather, whose sums follow Java double arithmetic (+inf + x = +inf,
+// +inf + -inf = NaN).  Inside the range the check costs two integer compares per entry.
 constexpr int kFxPoint = 80;
 constexpr int kFxThreads = 1024;
 constexpr int kFxSlots = 4096;         // LDS accumulators of a tile: rows x copies
 constexpr int kFxUnroll = 8;
 
-// v * 2^kFxPoint as a two's complement 128-bit integer (truncated below 2^-80; |v| < 2^47)
+// v * 2^kFxPoint as a two's complement 128-bit integer (truncated below 2^-80).  Only meaningful
+// inside the FxGuard range (|v| < 2^47 at the least); outside it the result is garbage that the
+// guard's flag discards.
 __device__ __forceinline__ void fx_of(double v, unsigned long long& lo, unsigned long long& hi) {
     const unsigned long long b = static_cast<unsigned long long>(__double_as_longlong(v));
     const int e = static_cast<int>((b >> 52) & 0x7FF);
     lo = 0;
     hi = 0;
-    if (e == 0) return;                                   // zero (or subnormal: below the resolution)
+    if (e == 0) return;                                   // zero (or subnormal: flagged by the guard)
     const unsigned long long m = (b & 0xFFFFFFFFFFFFFull) | (1ull << 52);
     const int sh = e - 1075 + kFxPoint;                   // v * 2^P = m * 2^sh
     if (sh > 74) {
-        hi = 1ull << 62;                                  // out of range (inf / nan / >= 2^47): loudly huge
+        hi = 1ull << 62;                                  // out of range (flagged by the guard)
     } else if (sh >= 64) {
         hi = m << (sh - 64);
     } else if (sh >= 0) {
@@ -509,8 +535,26 @@ __device__ __forceinline__ void fx_of(double v, unsigned long long& lo, unsigned
         hi = ~hi + c;
     }
 }
+// The 128-bit sum * 2^-80 rounded once to the nearest double (ties to even): the magnitude's
+// top 64 bits with every lower bit OR-ed into bit 0 (a sticky bit far below the 53-bit rounding
+// point: it breaks exact ties the dropped bits would have broken, and changes nothing else),
+// converted once (u64 -> f64 is correctly rounded) and scaled by an exact power of two.
 __device__ __forceinline__ double fx_to_double(unsigned long long lo, unsigned long long hi) {
-    return static_cast<double>(static_cast<long long>(hi)) * 0x1p-16 + static_cast<double>(lo) * 0x1p-80;
+    const bool neg = static_cast<long long>(hi) < 0;
+    if (neg) {
+        lo = ~lo + 1ull;
+        hi = ~hi + (lo == 0 ? 1ull : 0ull);
+    }
+    unsigned long long t = lo;
+    int e = -kFxPoint;
+    if (hi) {
+        const int s = 64 - __clzll(static_cast<long long>(hi));   // 1..64 significant bits in hi
+        const unsigned long long below = s == 64 ? lo : lo << (64 - s);
+        t = (s == 64 ? hi : (hi << (64 - s)) | (lo >> s)) | (below != 0 ? 1ull : 0ull);
+        e += s;
+    }
+    const double d = __builtin_ldexp(static_cast<double>(t), e);
+    return neg ? -d : d;
 }
 __device__ __forceinline__ void fx_add(unsigned long long* plo, unsigned long long* phi, unsigned long long lo,
                                        unsigned long long hi) {
@@ -519,17 +563,25 @@ __device__ __forceinline__ void fx_add(unsigned long long* plo, unsigned long lo
     if (c) atomicAdd(phi, c);
 }
 
+// The exact range of the layout (see kFxPoint): a nonzero entry whose biased exponent is outside
+// [elo, ehi) — or an infinity / NaN (exponent 0x7FF >= ehi), or a subnormal (0 < elo) — sets *bad.
+struct FxGuard {
+    unsigned elo = 0, ehi = 0x800;
+    unsigned* bad = nullptr;
+};
 // A tile's entries (packed source << rbits | accumulator) into the LDS accumulators: all index
 // loads, then all gathers, then the conversions and LDS atomics, kFxUnroll entries per thread
 // in flight.  lc: log2 of the copies per accumulator (the lane picks the copy).
 // diag (TGO_PR_FX_DIAG, results wrong by design; attribution only): 1 = no LDS atomics (the
 // values are folded into one register), 2 = no gathers (the index word stands in for the value)
-template <int diag = 0>
+template <int diag = 0, bool kGuard = false>
 __device__ __forceinline__ void fx_accumulate(const uint32_t* __restrict__ p, int64_t ne, const double* __restrict__ msg,
-                                              int rbits, int lc, unsigned long long* s_lo, unsigned long long* s_hi) {
+                                              int rbits, int lc, unsigned long long* s_lo, unsigned long long* s_hi,
+                                              const FxGuard& guard) {
     const uint32_t rmask = (1u << rbits) - 1u;
     const uint32_t cl = threadIdx.x & ((1u << lc) - 1u);
     unsigned long long sink = 0;
+    bool out = false;
     for (int64_t b = 0; b < ne; b += static_cast<int64_t>(kFxThreads) * kFxUnroll) {
         uint32_t w[kFxUnroll];
 #pragma unroll
@@ -545,6 +597,9 @@ __device__ __forceinline__ void fx_accumulate(const uint32_t* __restrict__ p, in
         }
 #pragma unroll
         for (int j = 0; j < kFxUnroll; ++j) {
+            const unsigned long long bits = static_cast<unsigned long long>(__double_as_longlong(v[j]));
+            const unsigned e = static_cast<unsigned>(bits >> 52) & 0x7FFu;
+            if (kGuard) out |= (bits << 1) != 0 && e - guard.elo >= guard.ehi - guard.elo;   // unsigned: below elo wraps
             unsigned long long lo, hi;
             fx_of(v[j], lo, hi);
             if (diag == 1) {
@@ -556,6 +611,7 @@ __device__ __forceinline__ void fx_accumulate(const uint32_t* __restrict__ p, in
         }
     }
     if (diag == 1 && sink == 0x5a5a5a5a5a5a5a5aull) s_lo[0] = sink;      // keep the loads alive
+    if (kGuard && out && guard.bad) *guard.bad = 1u;     // rare: the program re-runs in plain fp64
 }
 __device__ __forceinline__ int fx_copies_log2(int rows, int slots = kFxSlots) {
     int lc = 6;
@@ -604,10 +660,10 @@ __device__ __forceinline__ void fx_emit(const PrColdFinal& fin, const FoldSrc& f
 // p-th range) — 1 = the first (row totals to part), 3 = a middle one (from part, back to part),
 // 2 = the last (from part, emitted).  The same exact sum in every split, so the ranks are
 // bitwise those of kPass 0.
-template <int kSlots, int diag, int kPass = 0>
+template <int kSlots, int diag, int kPass = 0, bool kGuard = false>
 __global__ void __launch_bounds__(kFxThreads) gather_hot_fx(const uint32_t* __restrict__ padj,
         const int64_t* __restrict__ desc, int rbits, const double* __restrict__ msg, PrColdFinal fin,
-        unsigned long long* __restrict__ long_acc, FoldSrc fold, const int64_t* __restrict__ bnd = nullptr,
+        unsigned long long* __restrict__ long_acc, FoldSrc fold, FxGuard guard, const int64_t* __restrict__ bnd = nullptr,
         int nsplit = 1, int p = 0, unsigned long long* __restrict__ part = nullptr) {
     // 4096 slots: static LDS as before the 8192 option (the launch then passes no dynamic LDS)
     __shared__ unsigned long long s_static[kSlots == kFxSlots ? 2 * kFxSlots : 1];
@@ -627,7 +683,7 @@ __global__ void __launch_bounds__(kFxThreads) gather_hot_fx(const uint32_t* __re
         s_hi[i] = carry ? part[2 * (r0 + (i >> lc)) + 1] : 0;
     }
     __syncthreads();
-    fx_accumulate<diag>(padj + e0, e1 - e0, msg, rbits, lc, s_lo, s_hi);
+    fx_accumulate<diag, kGuard>(padj + e0, e1 - e0, msg, rbits, lc, s_lo, s_hi, guard);
     __syncthreads();
     if (nr > 0) {
         for (int i = threadIdx.x; i < rows; i += kFxThreads) {
@@ -659,10 +715,10 @@ __global__ void __launch_bounds__(kFxThreads) gather_hot_fx(const uint32_t* __re
 // piece's exact sum goes to partial[] as a double, where cold_fold adds a row's pieces in
 // segment order as before.
 // kSlots = 8192 (TGO_PR_FX_CP): 13-bit piece ids, 128 KB of dynamic LDS, one workgroup a CU.
-template <int kSlots, int diag>
+template <int kSlots, int diag, bool kGuard = false>
 __global__ void __launch_bounds__(kFxThreads) cold_fx(const uint32_t* __restrict__ cadj,
         const int64_t* __restrict__ cfd, XcdBase xb, const double* __restrict__ msg, double* __restrict__ partial,
-        int shift) {
+        int shift, FxGuard guard) {
     extern __shared__ unsigned long long fx_lds[];
     unsigned long long* s_lo = fx_lds;
     unsigned long long* s_hi = fx_lds + kSlots;
@@ -674,7 +730,7 @@ __global__ void __launch_bounds__(kFxThreads) cold_fx(const uint32_t* __restrict
     const int lc = fx_copies_log2(np, kSlots);
     for (int i = threadIdx.x; i < (np << lc); i += kFxThreads) { s_lo[i] = 0; s_hi[i] = 0; }
     __syncthreads();
-    fx_accumulate<diag>(cadj + e0, e1 - e0, msg + (w >> 16), shift, lc, s_lo, s_hi);
+    fx_accumulate<diag, kGuard>(cadj + e0, e1 - e0, msg + (w >> 16), shift, lc, s_lo, s_hi, guard);
     __syncthreads();
     for (int i = threadIdx.x; i < np; i += kFxThreads) {
         unsigned long long lo, hi;
@@ -976,6 +1032,13 @@ hipError_t k_pr_iter(const DevCsr& in, const RowBlocks& rb, const double* contri
     if (t.diag_hi > t.diag_lo) return run_gather(in, rb, PrDiagOp{contrib, t.diag_lo, t.diag_hi}, fin, partial, s);
     return run_gather(in, rb, PrOp{contrib}, fin, partial, s);
 }
+static FxGuard fx_guard(const ColdBlocks& cb) {
+    FxGuard g;
+    g.elo = static_cast<unsigned>(cb.fx_elo);
+    g.ehi = static_cast<unsigned>(cb.fx_ehi);
+    g.bad = cb.fx_bad;
+    return g;
+}
 // Cold phase: the cold segments' partial sums, folded per row into csum (reads only the cold
 // sources [hot, n_src) of `contrib`).
 static bool fx_fold_in_hot() {                       // TGO_PR_FX_FOLD (read per launch, A/B)
@@ -990,7 +1053,18 @@ static bool row_prefetch() {
     static const bool on = [] { const char* e = std::getenv("TGO_PR_PF"); return !e || std::atoi(e) != 0; }();
     return on;
 }
-hipError_t k_pr_cold_phase(const ColdBlocks& cb, const double* contrib, hipStream_t s) {
+// dynamic LDS past 64 KB, raised once per kernel instantiation
+static hipError_t big_lds(const void* fn, size_t lds) {
+    static std::vector<const void*> done;
+    if (std::find(done.begin(), done.end(), fn) != done.end()) return hipSuccess;
+    const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+    if (e == hipSuccess) done.push_back(fn);
+    return e;
+}
+hipError_t k_pr_cold_phase(const ColdBlocks& cb, const double* contrib, hipStream_t s, bool guard_entries) {
+    // fixed-point cold pieces beside a slot hot pass (whose emission does not check the range):
+    // every update checks its entries
+    guard_entries = guard_entries || (cb.cfx && !cb.fx);
     const bool window = cb.win > 0 && cb.rb_win.nblocks > 0;
     if (window) {
         const size_t lds = static_cast<size_t>(cb.win + (kWinThreads / 64) * kWinWaveTile) * sizeof(double);
@@ -1009,25 +1083,23 @@ hipError_t k_pr_cold_phase(const ColdBlocks& cb, const double* contrib, hipStrea
         const unsigned g = static_cast<unsigned>(cb.max_xcd_blocks * 8);
         if (cb.cfx && cb.cfx_shift > kPackShift) {
             constexpr size_t lds = 2 * 8192 * sizeof(unsigned long long);
-            static bool lds_set = false;              // the > 64 KB dynamic LDS limit, raised once
-            if (!lds_set) {
-                const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&cold_fx<8192, 0>),
-                                                         hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
-                if (e != hipSuccess) return e;
-                lds_set = true;
-            }
-            cold_fx<8192, 0><<<g, kFxThreads, lds, s>>>(reinterpret_cast<const uint32_t*>(cb.cadj), cb.cfx_desc, cb.xbase,
-                                                        contrib, cb.partial, cb.cfx_shift);
+            auto k = guard_entries ? &cold_fx<8192, 0, true> : &cold_fx<8192, 0, false>;
+            if (const hipError_t e = big_lds(reinterpret_cast<const void*>(k), lds)) return e;
+            k<<<g, kFxThreads, lds, s>>>(reinterpret_cast<const uint32_t*>(cb.cadj), cb.cfx_desc, cb.xbase, contrib,
+                                         cb.partial, cb.cfx_shift, fx_guard(cb));
         } else if (cb.cfx) {
             const size_t lds = 2 * kFxSlots * sizeof(unsigned long long);
             const uint32_t* cadj = reinterpret_cast<const uint32_t*>(cb.cadj);
             const int d = fx_diag();
-            if (d == 1)
-                cold_fx<kFxSlots, 1><<<g, kFxThreads, lds, s>>>(cadj, cb.cfx_desc, cb.xbase, contrib, cb.partial, cb.cfx_shift);
+            if (guard_entries)
+                cold_fx<kFxSlots, 0, true><<<g, kFxThreads, lds, s>>>(cadj, cb.cfx_desc, cb.xbase, contrib, cb.partial,
+                                                                      cb.cfx_shift, fx_guard(cb));
+            else if (d == 1)
+                cold_fx<kFxSlots, 1><<<g, kFxThreads, lds, s>>>(cadj, cb.cfx_desc, cb.xbase, contrib, cb.partial, cb.cfx_shift, fx_guard(cb));
             else if (d == 2)
-                cold_fx<kFxSlots, 2><<<g, kFxThreads, lds, s>>>(cadj, cb.cfx_desc, cb.xbase, contrib, cb.partial, cb.cfx_shift);
+                cold_fx<kFxSlots, 2><<<g, kFxThreads, lds, s>>>(cadj, cb.cfx_desc, cb.xbase, contrib, cb.partial, cb.cfx_shift, fx_guard(cb));
             else
-                cold_fx<kFxSlots, 0><<<g, kFxThreads, lds, s>>>(cadj, cb.cfx_desc, cb.xbase, contrib, cb.partial, cb.cfx_shift);
+                cold_fx<kFxSlots, 0><<<g, kFxThreads, lds, s>>>(cadj, cb.cfx_desc, cb.xbase, contrib, cb.partial, cb.cfx_shift, fx_guard(cb));
         }
         else if (cb.cpacked && row_prefetch())
             cold_gather<true, true><<<g, kBlock, 0, s>>>(cb.poff, cb.cadj, cb.bbeg, cb.bend, cb.xblk, cb.bsrc, cb.cdesc, cb.xbase,
@@ -1076,8 +1148,14 @@ hipError_t k_fx_split_points(const uint32_t* padj, const int64_t* desc, int64_t 
 
 // Hot phase: every row's hot entries (sources [0, hot)) + its folded cold sum -> the update.
 hipError_t k_pr_hot_phase(const ColdBlocks& cb, const double* contrib, const double* edge_count, double* pr,
-                          double* contrib_next, double* partial_long, double alpha, double base, hipStream_t s) {
-    const PrColdFinal fin{PrFinal{edge_count, pr, contrib_next, alpha, base}, cb.csum};
+                          double* contrib_next, double* partial_long, double alpha, double base, hipStream_t s,
+                          bool guard_entries) {
+    PrColdFinal fin{PrFinal{edge_count, pr, contrib_next, alpha, base}, cb.csum};
+    if (cb.fx || cb.cfx) {                           // every emitted contribution against the range
+        fin.f.bad = cb.fx_bad;
+        fin.f.elo = static_cast<unsigned>(cb.fx_elo);
+        fin.f.ehi = static_cast<unsigned>(cb.fx_ehi);
+    }
     if (cb.fx) {
         FoldSrc fold;
         if (fx_fold_in_hot() && cb.win == 0) { fold.cptr = cb.cptr; fold.cpid = cb.cpid; fold.partial = cb.partial; }
@@ -1085,45 +1163,36 @@ hipError_t k_pr_hot_phase(const ColdBlocks& cb, const double* contrib, const dou
             const unsigned g = static_cast<unsigned>(cb.fx_ntiles);
             const uint32_t* padj = reinterpret_cast<const uint32_t*>(cb.hcsr.adj);
             const int d = fx_diag();
+            const FxGuard gd = fx_guard(cb);
             if (cb.fx_rbits == 13) {
                 const size_t lds = 2 * 8192 * sizeof(unsigned long long);
-                static bool lds_set = false;
-                if (!lds_set) {
-                    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gather_hot_fx<8192, 0>),
-                                                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                             static_cast<int>(lds));
-                    if (e != hipSuccess) return e;
-                    lds_set = true;
-                }
-                gather_hot_fx<8192, 0><<<g, kFxThreads, lds, s>>>(padj, cb.fx_desc, cb.fx_rbits, contrib, fin,
-                                                                  cb.fx_long_acc, fold);
+                auto k = guard_entries ? &gather_hot_fx<8192, 0, 0, true> : &gather_hot_fx<8192, 0, 0, false>;
+                if (const hipError_t e = big_lds(reinterpret_cast<const void*>(k), lds)) return e;
+                k<<<g, kFxThreads, lds, s>>>(padj, cb.fx_desc, cb.fx_rbits, contrib, fin, cb.fx_long_acc, fold, gd, nullptr, 1,
+                                             0, nullptr);
             } else if (cb.fx_split > 1 && d == 0) {  // one launch per source range
                 const int S = cb.fx_split;
                 for (int p = 0; p < S; ++p) {
-                    if (p == 0)
-                        gather_hot_fx<kFxSlots, 0, 1><<<g, kFxThreads, 0, s>>>(padj, cb.fx_desc, cb.fx_rbits, contrib, fin,
-                                                                               cb.fx_long_acc, fold, cb.fx_mid, S, p,
-                                                                               cb.fx_part);
-                    else if (p + 1 < S)
-                        gather_hot_fx<kFxSlots, 0, 3><<<g, kFxThreads, 0, s>>>(padj, cb.fx_desc, cb.fx_rbits, contrib, fin,
-                                                                               cb.fx_long_acc, fold, cb.fx_mid, S, p,
-                                                                               cb.fx_part);
-                    else
-                        gather_hot_fx<kFxSlots, 0, 2><<<g, kFxThreads, 0, s>>>(padj, cb.fx_desc, cb.fx_rbits, contrib, fin,
-                                                                               cb.fx_long_acc, fold, cb.fx_mid, S, p,
-                                                                               cb.fx_part);
+                    auto k = p == 0 ? (guard_entries ? &gather_hot_fx<kFxSlots, 0, 1, true> : &gather_hot_fx<kFxSlots, 0, 1, false>)
+                           : p + 1 < S ? (guard_entries ? &gather_hot_fx<kFxSlots, 0, 3, true> : &gather_hot_fx<kFxSlots, 0, 3, false>)
+                                       : (guard_entries ? &gather_hot_fx<kFxSlots, 0, 2, true> : &gather_hot_fx<kFxSlots, 0, 2, false>);
+                    k<<<g, kFxThreads, 0, s>>>(padj, cb.fx_desc, cb.fx_rbits, contrib, fin, cb.fx_long_acc, fold, gd, cb.fx_mid,
+                                               S, p, cb.fx_part);
                 }
             } else {
                 const size_t lds = 0;
-                if (d == 1)
+                if (guard_entries)
+                    gather_hot_fx<kFxSlots, 0, 0, true><<<g, kFxThreads, lds, s>>>(padj, cb.fx_desc, cb.fx_rbits, contrib, fin,
+                                                                                   cb.fx_long_acc, fold, gd);
+                else if (d == 1)
                     gather_hot_fx<kFxSlots, 1><<<g, kFxThreads, lds, s>>>(padj, cb.fx_desc, cb.fx_rbits, contrib, fin,
-                                                                          cb.fx_long_acc, fold);
+                                                                          cb.fx_long_acc, fold, fx_guard(cb));
                 else if (d == 2)
                     gather_hot_fx<kFxSlots, 2><<<g, kFxThreads, lds, s>>>(padj, cb.fx_desc, cb.fx_rbits, contrib, fin,
-                                                                          cb.fx_long_acc, fold);
+                                                                          cb.fx_long_acc, fold, fx_guard(cb));
                 else
                     gather_hot_fx<kFxSlots, 0><<<g, kFxThreads, lds, s>>>(padj, cb.fx_desc, cb.fx_rbits, contrib, fin,
-                                                                          cb.fx_long_acc, fold);
+                                                                          cb.fx_long_acc, fold, fx_guard(cb));
             }
         }
         if (cb.fx_nlong > 0)
@@ -1173,12 +1242,6 @@ hipError_t k_pr_hot_phase(const ColdBlocks& cb, const double* contrib, const dou
     return hipGetLastError();
 }
 
-hipError_t k_pr_iter_cold(const ColdBlocks& cb, const double* contrib, const double* edge_count, double* pr,
-                          double* contrib_next, double* partial_long, double alpha, double base, hipStream_t s) {
-    hipError_t e = k_pr_cold_phase(cb, contrib, s);
-    if (e != hipSuccess) return e;
-    return k_pr_hot_phase(cb, contrib, edge_count, pr, contrib_next, partial_long, alpha, base, s);
-}
 hipError_t k_walk_iter(const DevCsr& out, const RowBlocks& rb, const int32_t* prev, int32_t* next,
                        int32_t* partial, int64_t n, hipStream_t s) {
     (void)n;

@@ -526,6 +526,17 @@ class HipPartBackend:
         self.e.part_call("tgo_part_pr_end", L.ptr(out, C.c_double))
         return out
 
+    def pr_exact_check(self):
+        """1 when a fixed-point pass of the blocked layout saw a message outside its exact range
+        since the last check (tgo_part_pr_exact_check; the flag is cleared)."""
+        b = C.c_int32()
+        self.e.part_call("tgo_part_pr_exact_check", C.byref(b))
+        return b.value
+
+    def pr_plain(self, on):
+        """Run the next programs on the plain layout (tgo_part_pr_plain)."""
+        self.e.part_call("tgo_part_pr_plain", 1 if on else 0)
+
 
 def _scratch(backend, name, n, dtype):
     """Exchange buffers live as long as the backend (allocated zero-filled once, reused by
@@ -932,4 +943,17 @@ def distributed_pagerank(backend, alpha: float, vertex_count: int, iterations: i
         backend.pr_step_cold(contrib_global)
         work.wait()
         backend.pr_step_hot(contrib_global, contrib_local)
+    if hot > 0:
+        # the blocked layout's fixed-point passes are exact only inside a range: a message
+        # outside it on ANY rank (+inf from a vertex whose row cut left it no OUT entry, NaN, ...)
+        # and every rank runs the program again on the plain layout's fp64 gather
+        bad = torch.tensor([backend.pr_exact_check()], dtype=torch.int64, device=backend.device)
+        cm.all_reduce(bad, op="max")
+        if int(bad.item()):
+            backend.pr_plain(True)
+            try:
+                return distributed_pagerank(backend, alpha, vertex_count, iterations, fetch, layout=(0, backend.n_local),
+                                            overlap=overlap, comm=cm)
+            finally:
+                backend.pr_plain(False)
     return backend.pr_end(fetch)
