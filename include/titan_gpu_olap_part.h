@@ -139,6 +139,10 @@ int tgo_part_ms_levels(tgo_ctx* ctx, int32_t source, int64_t* dist_local);
  * (delta, or the default when delta <= 0; ranks should agree on the maximum).
  * counts = {next near-queue length, its push entries}.  Seeds are global ids. */
 int tgo_part_sssp_begin(tgo_ctx* ctx, int64_t seed_global, int64_t delta, int64_t* out);
+/* The smallest weight of this rank's load (0 without weights).  sssp_begin fails on a negative
+ * weight: a driver all-reduces (MIN) this first so that every rank fails together (the native
+ * tgo_part_sssp_run does). */
+int tgo_part_weight_min(tgo_ctx* ctx, int64_t* min_weight);
 int tgo_part_sssp_relax(tgo_ctx* ctx, int64_t thr, int32_t nranks, int64_t* send, int64_t* send_counts);
 int tgo_part_sssp_apply(tgo_ctx* ctx, int64_t thr, const int64_t* recv, int64_t npairs, int64_t* counts);
 int tgo_part_sssp_pending_min(tgo_ctx* ctx, int64_t* out);
@@ -244,6 +248,26 @@ int  tgo_part_sssp_run(tgo_ctx* ctx, tgo_exchange* x, int64_t seed_global, int64
                        int64_t* reached, int32_t* phases);
 int  tgo_part_pagerank_run(tgo_ctx* ctx, tgo_exchange* x, const tgo_pr_args* args, int32_t exchange_mode,
                            double* pr_local, int64_t* exchanged_bytes);
+
+/* The partitioned load from edgestore rows: the multi-GPU form of tgo_load_rows +
+ * tgo_finish_load (one scan, VertexJobConverter.java:109-129).  A Titan row holds a vertex's
+ * OUT and IN entries, so the 1-D vertex partition is a row-range partition of the scan: rank r
+ * of the exchange passes the rows of ITS vertices (any split of the scan's rows over the ranks;
+ * edge-balanced ranges balance the work).  Each rank decodes its rows with the one-GPU rules —
+ * key filter, ghosts, typed scopes, and the hard-limit cut per row in column order
+ * (QueryContainer.java:28,122; ColumnValueStore.java:47-69) — so its lists are exactly the
+ * lists a one-GPU load keeps for those rows.  Collective (every rank calls it with the same
+ * schema / opts / layout): the ranks agree on failure, the slot size S (the largest live row
+ * count rounded up to 64; rank r's i-th live row is global id r * S + i, slots past its count are
+ * entry-less), the global id map (all-gather of the live ids: entries to vertices no rank holds
+ * are dropped, as on one GPU), the degree-grouped layout (layout = 1), and — when a cut single-
+ * direction scope makes the push view no transpose of the stored lists — the push rows (every
+ * rank's pull entries sent to their sources' owners).  part[0] = this rank's live rows (its
+ * results are the first part[0] of the tgo_part_* outputs, in row order; tgo_vertex_ids gives
+ * their ids), part[1] = S; n_global = world * S, lo = rank * S for the tgo_part_* calls.
+ * TGO_E_UNSUPPORTED for vertex cuts (they fold on one GPU) and non-Integer weight keys. */
+int  tgo_load_partition_rows(tgo_ctx* ctx, tgo_exchange* x, const tgo_rows* rows, const tgo_schema* schema,
+                             const tgo_load_opts* opts, int32_t layout, int64_t* part);
 
 /* Bench / test input: the edges of an RMAT stream (tgo_synth.h) with an endpoint in
  * [lo, hi).  *count = edges written; if capacity is too small, nothing is written,

@@ -55,6 +55,12 @@ class Rows:
     def nrows(self):
         return len(self.keys)
 
+    def slice(self, a, b):
+        """Rows [a, b) with their offsets rebased (a work block, or one rank's row range)."""
+        eb, bb = self.entry_begin[a:b + 1], self.byte_begin[a:b + 1]
+        return Rows(self.keys[a:b].copy(), (eb - eb[0]).copy(), (bb - bb[0]).copy(), self.data[bb[0]:bb[-1]].copy(),
+                    self.limit_valpos[eb[0]:eb[-1]].copy())
+
     def save(self, path, **extra):
         np.savez_compressed(path, keys=self.keys, entry_begin=self.entry_begin, byte_begin=self.byte_begin,
                             data=self.data, limit_valpos=self.limit_valpos, **extra)

@@ -49,6 +49,10 @@ class NumpyPartBackend:
         return [(t, x) for adj, ww in lists for t, x in zip(adj[u], ww[u])]
 
     # ---- delta-stepping SSSP local steps (contract: include/titan_gpu_olap_part.h)
+    def weight_min(self):
+        ws = [x for lst in self.out_w + self.inn_w for x in lst]
+        return min(ws) if ws else 0
+
     def sssp_begin(self, seed, delta):
         self.sd = np.full(self.n_local, INF, np.int64)
         self.pend, self.rbest, self.sq, self.snext = set(), {}, [], []
@@ -771,3 +775,46 @@ def test_in_process_group_propagates_a_rank_failure():
 
     with pytest.raises(ValueError, match="rank 1 fails"):
         InProcessGroup(2, timeout=30).run(body)
+
+
+def _negative_weight_worker(rank, world, port, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from titan_amd import rmat_edges
+    from titan_amd.distributed import distributed_sssp, partition_range
+    from titan_amd.engine import TitanException
+    n = 3 * 128                                     # 64-aligned thirds past the RMAT range
+    src, dst, w = rmat_edges(8, 8, seed=23, weights=True)
+    src, dst = src + 128, dst + 128                 # every rank holds edges
+    w = w.astype(np.int64)
+    lo, hi = partition_range(n, world, rank)
+    last = partition_range(n, world, world - 1)
+    i = int(np.nonzero((src >= last[0]) & (dst >= last[0]))[0][0])   # an edge only the last rank holds
+    w[i] = -3
+    be = NumpyPartBackend(n, lo, hi, src, dst, w=w, scope=1)
+    try:
+        distributed_sssp(be, int(src[0]), 0)
+        out_q.put((rank, "ran"))
+    except TitanException as e:
+        out_q.put((rank, e.code))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_negative_weight_fails_every_rank():
+    """a negative weight on ONE rank made that rank fail before the first collective
+    while its peers waited in it.  The ranks now agree on the minimum weight first (all-reduce
+    MIN, tgo_part_weight_min) and all of them raise."""
+    from titan_amd import _lib as L
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_negative_weight_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res == {r: L.TGO_E_INVALID for r in range(world)}

@@ -536,6 +536,33 @@ def test_partitioned_pagerank_out_of_range_reruns_plain(world, monkeypatch):
         assert {be.e.stats()["exact_reruns"] for be in ranks.backends} == ({0} if N == n else {1})
 
 
+def test_sssp_negative_weight_fails_every_rank():
+    """a negative weight held by ONE rank failed only that rank's tgo_part_sssp_begin
+    while its peers waited in the first collective.  The drivers now agree on the global minimum
+    weight first (tgo_part_weight_min, all-reduce MIN): every rank raises, native and Python."""
+    from titan_amd.distributed import NativeExchange, distributed_sssp_native
+    scale = 10
+    n = 1 << scale
+    src, dst, w = rmat_edges(scale, 16, seed=63, weights=True)
+    w = w.copy()
+    i = int(np.nonzero((src >= n // 2) & (dst >= n // 2))[0][0])   # an edge only rank 1 holds
+    w[i] = -2
+    ranks = Ranks(2, n, src, dst, L.SCOPE_IN_E, weight=w)
+    assert ranks.backends[0].weight_min() >= 0 and ranks.backends[1].weight_min() == -2
+    xs = NativeExchange.local_group(2)
+
+    def body(run):
+        def f(be, comm):
+            try:
+                run(be, comm)
+                return "ran"
+            except TitanException as e:
+                return e.code
+        return f
+    assert ranks.run(body(lambda be, comm: distributed_sssp_native(be, int(src[0]), xs[comm.rank]))) == [L.TGO_E_INVALID] * 2
+    assert ranks.run(body(lambda be, comm: distributed_sssp(be, int(src[0]), 0, comm=comm))) == [L.TGO_E_INVALID] * 2
+
+
 def test_native_drivers_rccl_world1():
     """The three native loops over the RCCL exchange (one rank)."""
     from titan_amd.distributed import (NativeExchange, distributed_bfs_native, distributed_pagerank_native,
@@ -564,3 +591,129 @@ def test_native_drivers_rccl_world1():
         fin = np.isfinite(opr)
         assert np.abs(p[fin] - opr[fin]).sum() <= 1e-6
         del x
+
+
+# ----------------------------------------------------------------------------- partition from rows
+class RowRanks:
+    """tgo_load_partition_rows: each thread rank loads ITS contiguous row range of a scan
+    (balanced_row_ranges) over an in-process exchange group; backends over the slot ids."""
+
+    def __init__(self, world, rows, sd, scope, limit, weight_key=0, layout=True, labels=()):
+        from titan_amd import Schema
+        from titan_amd.distributed import NativeExchange, balanced_row_ranges
+        self.world = world
+        self.ranges = balanced_row_ranges(rows.entry_begin, world)
+        self.xs = NativeExchange.local_group(world)
+        self.streams = [torch.cuda.Stream() for _ in range(world)]
+
+        def load(rank, comm):
+            torch.cuda.set_stream(self.streams[rank])
+            eng = Engine(stream=self.streams[rank].cuda_stream, hard_query_limit=limit)
+            live, S = eng.load_partition_rows(self.xs[rank], rows.slice(*self.ranges[rank]), Schema.from_dict(sd), scope,
+                                              weight_key=weight_key, layout=layout, labels=labels)
+            return eng, live, S
+        res = InProcessGroup(world).run(load)
+        self.S = res[0][2]
+        assert all(r[2] == self.S for r in res)
+        self.n_global = world * self.S
+        self.live = [r[1] for r in res]
+        self.engines = [r[0] for r in res]
+        self.backends = []
+        for r, e in enumerate(self.engines):
+            with torch.cuda.stream(self.streams[r]):
+                self.backends.append(HipPartBackend(e, self.n_global, r * self.S, (r + 1) * self.S))
+        self.ids = [e.vertex_ids()[:lv] for e, lv in zip(self.engines, self.live)]
+        self.slot = {int(v): r * self.S + i for r, ids in enumerate(self.ids) for i, v in enumerate(ids)}
+
+    def run(self, fn):
+        def body(rank, comm):
+            torch.cuda.set_stream(self.streams[rank])
+            return fn(self.backends[rank], comm, self.xs[rank])
+        return InProcessGroup(self.world).run(body)
+
+    def gather(self, per_rank, ids_to):
+        """Concatenate the ranks' live results and order them as ids_to."""
+        got = {}
+        for ids, vals, lv in zip(self.ids, per_rank, self.live):
+            got.update(zip((int(v) for v in ids), vals[:lv]))
+        return np.array([got[int(v)] for v in ids_to])
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
+def test_partition_rows_match_one_gpu_rows(world, monkeypatch):
+    """tgo_load_partition_rows on two-label rows whose hubs are cut in column
+    order at a small hard limit: every native partitioned program over the row-range partition
+    equals the one-GPU tgo_load_rows load of the same rows — BFS (bothE), multi-source BFS and
+    weighted delta SSSP (capped inE: the push rows come from every rank's cut pull lists) bit-exact,
+    equal summed truncated_results, both loads equal to the oracle."""
+    from titan_amd import Schema
+    from titan_amd.distributed import distributed_bfs_native, distributed_msbfs_native, distributed_sssp_native
+    from test_gpu_parity import two_label_rows
+    rows, vids, sd, osch, knows, likes, wkey = two_label_rows(n=900)
+    limit, n = 12, len(vids)
+    for scope in (L.SCOPE_BOTH_E, L.SCOPE_IN_E):
+        one = Engine(hard_query_limit=limit).load_rows(rows, Schema.from_dict(sd), scope, weight_key=wkey)
+        o = fr.OracleGraph.from_rows(rows, osch, scope, hard_limit=limit, weight_key=wkey)
+        ids1 = one.vertex_ids()
+        rr = RowRanks(world, rows, sd, scope, limit, weight_key=wkey)
+        assert sum(rr.live) == len(ids1) and sorted(np.concatenate(rr.ids)) == sorted(ids1)
+        assert sum(be.e.stats()["truncated_results"] for be in rr.backends) == one.stats()["truncated_results"] \
+            == o.stats.truncated_results
+        if scope == L.SCOPE_IN_E:
+            assert one.stats()["truncated_results"] > 0
+        seeds = [int(vids[i]) for i in (0, 1, 5, 77)]
+        for s in seeds:
+            if scope == L.SCOPE_BOTH_E:
+                want = one.bfs(s, n, scope)
+                assert np.array_equal(want, o.shortest_distance(s, n, scope)[0])
+                res = rr.run(lambda be, comm, x: distributed_bfs_native(be, rr.slot[s], rr.n_global, x))
+            else:
+                want = one.sssp(s, n, scope, mode=L.SSSP_DELTA)
+                assert np.array_equal(want, o.shortest_distance(s, n, scope, weighted=True)[0])
+                res = rr.run(lambda be, comm, x: distributed_sssp_native(be, rr.slot[s], x))
+            assert np.array_equal(rr.gather([r[0] for r in res], ids1), want), (scope, s)
+        if scope == L.SCOPE_BOTH_E:
+            res = rr.run(lambda be, comm, x: (distributed_msbfs_native(be, [rr.slot[s] for s in seeds], rr.n_global, x),
+                                              [be.ms_levels(i) for i in range(len(seeds))]))
+            for i, s in enumerate(seeds):
+                assert np.array_equal(rr.gather([r[1][i] for r in res], ids1), one.bfs(s, n, scope)), i
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_partition_rows_pagerank_zero_edge_count(world, monkeypatch):
+    """PageRank over the row-range partition of the zero-edgeCount fixture (hubs whose cut rows
+    keep no OUT entry while their targets read them): the blocked layout's fixed-point passes
+    flag the +inf, every rank re-runs on the plain layout, and the ranks equal the one-GPU
+    tgo_load_rows result and the oracle (same +inf positions, finite part within 1e-6 L1), for
+    both exchanges."""
+    from titan_amd import Schema
+    from titan_amd.distributed import PR_EXCHANGE_ALLGATHER, PR_EXCHANGE_GHOST, distributed_pagerank_native
+    from test_gpu_parity import assert_pagerank_like_oracle, zero_edge_count_rows
+    monkeypatch.setenv("TGO_PR_HOT", "128")
+    monkeypatch.setenv("TGO_PR_SEG", "128")
+    rows, vids, sd, osch = zero_edge_count_rows()
+    limit, n = 24, len(vids)
+    one = Engine(hard_query_limit=limit).load_rows(rows, Schema.from_dict(sd), L.SCOPE_IN_E)
+    ids1 = one.vertex_ids()
+    opr = fr.OracleGraph.from_rows(rows, osch, L.SCOPE_IN_E, hard_limit=limit).pagerank(0.85, n, 8)[0]
+    want = one.pagerank(0.85, n, 8)
+    assert_pagerank_like_oracle(want, opr)
+    rr = RowRanks(world, rows, sd, L.SCOPE_IN_E, limit)
+    for mode in (PR_EXCHANGE_ALLGATHER, PR_EXCHANGE_GHOST):
+        res = rr.run(lambda be, comm, x: distributed_pagerank_native(be, 0.85, n, 8, x, mode=mode))
+        got = rr.gather([r[0] for r in res], ids1)
+        assert_pagerank_like_oracle(got, opr)
+        fin = np.isfinite(want)
+        assert np.abs(got[fin] - want[fin]).sum() <= 1e-9
+        assert {be.e.stats()["exact_reruns"] for be in rr.backends} == {1}
+
+
+def test_partition_rows_refuses_vertex_cuts_on_every_rank():
+    """Vertex cuts fold into their canonical vertex on one GPU only: the partitioned rows load
+    fails with TGO_E_UNSUPPORTED on every rank (agreed before any further collective)."""
+    from titan_amd import Schema
+    from conftest import load_fixture
+    rows, vids, sd, npz = load_fixture("partition_groups")
+    with pytest.raises(TitanException) as ei:
+        RowRanks(2, rows, sd, L.SCOPE_IN_E, 100000)
+    assert ei.value.code in (L.TGO_E_UNSUPPORTED, L.TGO_E_INVALID)

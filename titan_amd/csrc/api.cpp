@@ -1254,7 +1254,7 @@ int finish_distance_program(tgo_ctx* ctx, int scope, int flags, int64_t* dist_ou
 
 // ============================================================================ C-ABI
 
-namespace tgo { double ms_split_of(const tgo_ctx* ctx); }
+namespace tgo { double ms_split_of(const tgo_ctx* ctx); int part_upload(tgo_ctx* ctx, HostGraph& h, int64_t n_global, int64_t lo); }
 
 namespace {
 struct TrimTemps {                  // tmp_cache.cpp: nothing stays reserved between loads
@@ -2203,18 +2203,9 @@ int tgo_load_partition_layout(tgo_ctx* ctx, int64_t n_global, int64_t lo, int64_
         std::fprintf(stderr, "[tgo] load_partition assembly (%s) %8.1f ms\n", on_dev ? "device" : "host",
                      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
     if (rc) return fail(ctx, rc, err);
-    free_graph(ctx);
-    ctx->staging = RowStaging();
-    rc = upload_graph(ctx, h, false);     // partitioned PageRank gathers global ids: plain CSR
-    if (rc) return rc;
-    ctx->g.partitioned = true;
-    ctx->part_pr_world = 0;
-    ctx->part_pr_hot = ctx->part_pr_span = 0;
-    ctx->part_pr_iter = ctx->part_pr_iters = 0;
-    ctx->g.lo = lo;
-    ctx->g.n_global = n_global;
+    rc = tgo::part_upload(ctx, h, n_global, lo);
     ctx->st.load_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    return TGO_OK;
+    return rc;
 }
 
 static int part_check(tgo_ctx* ctx);
@@ -3112,6 +3103,17 @@ int tgo_part_sssp_begin(tgo_ctx* ctx, int64_t seed_global, int64_t delta, int64_
     return TGO_OK;
 }
 
+// The smallest weight of the rank's load (0 without weights).  Delta-stepping refuses negative
+// weights; the drivers agree on the global minimum BEFORE the first collective, so every rank
+// fails together instead of one rank failing while its peers wait in an exchange.
+int tgo_part_weight_min(tgo_ctx* ctx, int64_t* min_weight) {
+    int rc = part_check(ctx);
+    if (rc) return rc;
+    if (!min_weight) return fail(ctx, TGO_E_INVALID, "null argument");
+    *min_weight = ctx->g.has_weight ? ctx->g.min_weight : 0;
+    return TGO_OK;
+}
+
 // The relax half of a phase.  send_counts (host) set: the pair counts come back to the host
 // (one stream synchronisation); sizes (device) set instead: the exchange header is written on
 // the device (ds_mark_sizes) and nothing waits.
@@ -3524,6 +3526,50 @@ int tgo_sync(tgo_ctx* ctx) {
 // accessors for the C++ partitioned driver (part_driver.cpp)
 namespace tgo {
 hipStream_t part_stream(tgo_ctx* ctx) { return ctx->stream; }
+// A partition's host graph onto the device (tgo_load_partition_layout, tgo_load_partition_rows).
+int part_upload(tgo_ctx* ctx, HostGraph& h, int64_t n_global, int64_t lo) {
+    free_graph(ctx);
+    ctx->staging = RowStaging();
+    int rc = upload_graph(ctx, h, false);     // partitioned PageRank gathers global ids: plain CSR
+    if (rc) return rc;
+    ctx->g.partitioned = true;
+    ctx->part_pr_world = 0;
+    ctx->part_pr_plain = false;
+    ctx->part_pr_hot = ctx->part_pr_span = 0;
+    ctx->part_pr_iter = ctx->part_pr_iters = 0;
+    ctx->g.lo = lo;
+    ctx->g.n_global = n_global;
+    return TGO_OK;
+}
+// tgo_load_partition_rows: this rank's rows decoded on the host with the one-GPU rules (the cut
+// in column order per row, typed scopes, key filter, ghosts: decode_rows).  Vertex cuts fold on
+// one GPU only; the partitioned programs read Integer weights.
+int part_rows_decode(tgo_ctx* ctx, const tgo_rows* rows, const tgo_schema* schema, const tgo_load_opts* opts,
+                     RowStaging& st, std::string& err) {
+    (void)hipSetDevice(ctx->opts.device);
+    ctx->res_kind = -1;
+    if (rows->nrows < 0 || (rows->nrows > 0 && (!rows->row_keys || !rows->row_entry_begin || !rows->row_byte_begin ||
+                                                !rows->entry_bytes || !rows->entry_limit_valpos))) {
+        err = "incomplete tgo_rows";
+        return TGO_E_INVALID;
+    }
+    if (opts->scope < 0 || opts->scope > 2) { err = "invalid scope"; return TGO_E_INVALID; }
+    st = RowStaging();
+    if (int rc = decode_rows(st, rows, schema, opts, ctx->opts.partition_bits, ctx->opts.hard_query_limit,
+                             threads_of(ctx), err))
+        return rc;
+    if (st.n_rep > 0 || std::any_of(st.vid.begin(), st.vid.end(), [](int64_t v) { return (v & 7) == 2; })) {
+        err = "vertex cuts fold into their canonical vertex on a one-GPU load (VertexProgramScanJob.java:76-92)";
+        return TGO_E_UNSUPPORTED;
+    }
+    if (opts->weight_key != 0 && st.plan.weight_dt != 0 && st.plan.weight_dt != TGO_DT_INTEGER) {
+        err = "the partitioned programs read edge.<Integer>value(weight) (ShortestDistanceVertexProgram.java:53)";
+        return TGO_E_UNSUPPORTED;
+    }
+    return TGO_OK;
+}
+int part_threads(const tgo_ctx* ctx) { return threads_of(ctx); }
+void part_set_live(tgo_ctx* ctx, int64_t live) { ctx->st.num_vertices = live; }
 int part_fail(tgo_ctx* ctx, int code, const std::string& msg) { return fail(ctx, code, msg); }
 int64_t* part_dcounts_of(tgo_ctx* ctx) { return ctx->part_dcounts; }
 // tgo_part_sssp_relax with the exchange header (sizes, 2 * nranks words) written on the device

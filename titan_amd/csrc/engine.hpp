@@ -260,6 +260,15 @@ int partition_layout(const tgo_edges* e, int64_t n_global, int64_t lo, int64_t h
 int assemble_partition(const tgo_edges* e, int64_t n_global, int64_t lo, int64_t hi,
                        const tgo_load_opts* opts, int64_t hard_limit, const int32_t* layout, HostGraph& g,
                        int threads, std::string& err);
+// 1-D partition from edgestore rows (tgo_load_partition_rows; graph_build.cpp): this rank's
+// decoded rows over global slot ids r * S + i, its layout, and the push view's exchange pairs.
+int assemble_partition_rows(RowStaging& st, const std::vector<int64_t>& slot_vid, int64_t S, int rank,
+                            HostGraph& g, int threads, std::string& err);
+void partition_rows_layout(const HostGraph& g, int64_t lo, int32_t* layout_local);
+int apply_partition_layout(HostGraph& g, int64_t lo, const int32_t* layout, int threads, std::string& err);
+void partition_pull_pairs(const HostGraph& g, int64_t lo, int64_t S, int world, std::vector<int64_t>& counts,
+                          std::vector<int64_t>& pairs);
+void partition_push_from_pairs(HostGraph& g, const int64_t* pairs, int64_t npairs);
 // assemble_partition on the device (assemble.hip), array for array; m < 2^32.
 int assemble_partition_device(const tgo_edges* e, int64_t n_global, int64_t lo, int64_t hi, const tgo_load_opts* opts,
                               int64_t hard_limit, const int32_t* layout, HostGraph& g, hipStream_t s, std::string& err);

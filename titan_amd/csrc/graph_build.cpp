@@ -943,6 +943,136 @@ int assemble_partition(const tgo_edges* e, int64_t n_global, int64_t lo, int64_t
     return TGO_OK;
 }
 
+// ------------------------------------------------------------------ 1-D partition from rows
+// The multi-GPU load from the edgestore (tgo_load_partition_rows): rank `rank` holds the rows
+// of its live vertices, decoded with the cut already applied in column order (decode_rows:
+// QueryContainer.java:28,122 over ColumnValueStore.java:47-69 — the one-GPU rule, per row).
+// Global ids are slots: the i-th live row of rank r is r * S + i; slots past a rank's live
+// count are entry-less padding.  slot_vid holds every rank's live Titan ids at their slots
+// (padding: negative).  Entries whose other endpoint is no live vertex anywhere are dropped,
+// as on one GPU (a vertex that never executes sends nothing, VertexState.java:103-137).
+int assemble_partition_rows(RowStaging& st, const std::vector<int64_t>& slot_vid, int64_t S, int rank,
+                            HostGraph& g, int threads, std::string& err) {
+    g = HostGraph();
+    const int64_t count = static_cast<int64_t>(st.vid.size()), lo = static_cast<int64_t>(rank) * S;
+    if (count > S || static_cast<int64_t>(slot_vid.size()) < lo + S || slot_vid.size() >= size_t(INT32_MAX)) {
+        err = "partition slots out of range";
+        return TGO_E_INVALID;
+    }
+    g.n = S;
+    g.scope = st.opts.scope;
+    g.has_weight = st.opts.weight_key != 0;
+    g.weight_dt = TGO_DT_INTEGER;
+    g.ghost = st.ghost; g.truncated = st.truncated; g.skipped = st.skipped;
+    g.titan_id.assign(static_cast<size_t>(S), 0);
+    std::copy(st.vid.begin(), st.vid.end(), g.titan_id.begin());
+    IdMap map;
+    map.build(slot_vid);
+    std::vector<int32_t> dense(st.other.size());
+    parallel_for(static_cast<int64_t>(st.other.size()), threads, [&](int64_t a, int64_t b, int) {
+        for (int64_t k = a; k < b; ++k) dense[k] = st.other[k] < 0 ? -1 : map.find(st.other[k]);
+    });
+    std::vector<int64_t> co(S + 1, 0), ci(S + 1, 0);
+    for (int64_t v = 0; v < count; ++v) {
+        int64_t a = 0, b = 0;
+        for (int64_t k = st.row_begin[v]; k < st.row_begin[v + 1]; ++k) {
+            if (dense[k] < 0) continue;
+            if (st.dir[k] == 0) ++a; else ++b;
+        }
+        co[v + 1] = a; ci[v + 1] = b;
+    }
+    for (int64_t v = 0; v < S; ++v) { co[v + 1] += co[v]; ci[v + 1] += ci[v]; }
+    g.out.off = co; g.in.off = ci;
+    g.out.adj.resize(co[S]); g.in.adj.resize(ci[S]);
+    if (g.has_weight) { g.out.w.resize(co[S]); g.in.w.resize(ci[S]); }
+    parallel_for(count, threads, [&](int64_t a0, int64_t b0, int) {
+        for (int64_t v = a0; v < b0; ++v) {
+            int64_t a = co[v], b = ci[v];
+            for (int64_t k = st.row_begin[v]; k < st.row_begin[v + 1]; ++k) {   // column order kept
+                if (dense[k] < 0) continue;
+                if (st.dir[k] == 0) {
+                    g.out.adj[a] = dense[k];
+                    if (g.has_weight) g.out.w[a] = st.w[k];
+                    ++a;
+                } else {
+                    g.in.adj[b] = dense[k];
+                    if (g.has_weight) g.in.w[b] = st.w[k];
+                    ++b;
+                }
+            }
+        }
+    });
+    (void)lo;
+    st = RowStaging();
+    return TGO_OK;
+}
+
+// tgo_part_layout for a rows partition: the owned slots grouped by half-octave of their kept
+// entries (padding last), as global ids in [lo, lo + n).
+void partition_rows_layout(const HostGraph& g, int64_t lo, int32_t* layout_local) {
+    std::vector<int32_t> order;
+    degree_group_order(g.n, [&](int64_t v) {
+        return (g.out.off[v + 1] - g.out.off[v]) + (g.in.off[v + 1] - g.in.off[v]);
+    }, order);
+    for (int64_t v = 0; v < g.n; ++v) layout_local[v] = static_cast<int32_t>(lo + order[v]);
+}
+
+// Owned rows move inside [lo, lo + n) and neighbours take their owners' layout (the
+// all-gathered layout of every rank), as assemble_partition does for an edge list.
+int apply_partition_layout(HostGraph& g, int64_t lo, const int32_t* layout, int threads, std::string& err) {
+    const int64_t n = g.n;
+    g.perm.resize(n);
+    std::vector<uint8_t> seen(n, 0);
+    for (int64_t v = 0; v < n; ++v) {
+        const int64_t p = static_cast<int64_t>(layout[lo + v]) - lo;
+        if (p < 0 || p >= n || seen[p]) { err = "layout is not a permutation of the owned range"; return TGO_E_INVALID; }
+        seen[p] = 1;
+        g.perm[v] = static_cast<int32_t>(p);
+    }
+    permute_graph(g, [layout](int32_t u) { return layout[u]; }, threads);
+    return TGO_OK;
+}
+
+// The push view of a cut single-direction scope needs the pull lists of EVERY rank: pull entry
+// (v <- u) of owned row v becomes push entry (u -> v) at u's owner.  pairs: owner-major, two
+// int64 per entry {(u - owner * S) << 32 | (lo + v), weight}; counts[p] = entries for rank p.
+void partition_pull_pairs(const HostGraph& g, int64_t lo, int64_t S, int world, std::vector<int64_t>& counts,
+                          std::vector<int64_t>& pairs) {
+    const HostCsr& pull = g.scope == TGO_SCOPE_IN_E ? g.out : g.in;
+    const int64_t n = g.n;
+    counts.assign(world, 0);
+    for (int64_t k = 0; k < static_cast<int64_t>(pull.adj.size()); ++k) ++counts[pull.adj[k] / S];
+    std::vector<int64_t> pos(world + 1, 0);
+    for (int p = 0; p < world; ++p) pos[p + 1] = pos[p] + counts[p];
+    pairs.assign(static_cast<size_t>(2 * pos[world]), 0);
+    for (int64_t v = 0; v < n; ++v)
+        for (int64_t k = pull.off[v]; k < pull.off[v + 1]; ++k) {
+            const int64_t u = pull.adj[k], owner = u / S, at = pos[owner]++;
+            pairs[2 * at] = ((u - owner * S) << 32) | (lo + v);
+            pairs[2 * at + 1] = pull.w.empty() ? 0 : pull.w[k];
+        }
+}
+
+// The push rows of the owned slots from the pairs every rank sent here (partition_pull_pairs),
+// each row ordered by (target, weight).
+void partition_push_from_pairs(HostGraph& g, const int64_t* pairs, int64_t npairs) {
+    std::vector<std::pair<int64_t, int64_t>> e(static_cast<size_t>(npairs));
+    for (int64_t i = 0; i < npairs; ++i) e[i] = {pairs[2 * i], pairs[2 * i + 1]};
+    std::sort(e.begin(), e.end());
+    HostCsr& pt = g.push_t;
+    pt = HostCsr();
+    pt.off.assign(g.n + 1, 0);
+    pt.adj.resize(static_cast<size_t>(npairs));
+    if (g.has_weight) pt.w.resize(static_cast<size_t>(npairs));
+    for (int64_t i = 0; i < npairs; ++i) {
+        ++pt.off[(e[i].first >> 32) + 1];
+        pt.adj[i] = static_cast<int32_t>(e[i].first & 0xFFFFFFFFLL);
+        if (g.has_weight) pt.w[i] = static_cast<int32_t>(e[i].second);
+    }
+    for (int64_t v = 0; v < g.n; ++v) pt.off[v + 1] += pt.off[v];
+    g.has_transpose = true;
+}
+
 // ------------------------------------------------------------------ CSR-adaptive blocks
 // Greedy partition of rows into blocks of <= tile entries and <= max_rows rows
 // (CSR-Adaptive, Greathouse & Daga SC'14); rows longer than `tile` become "long rows"

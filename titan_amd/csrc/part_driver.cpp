@@ -334,6 +334,11 @@ int part_in_list(tgo_ctx* ctx, const int32_t** adj, int64_t* nnz);
 int part_out_list(tgo_ctx* ctx, const int32_t** adj, int64_t* nnz);
 bool ms_ghost_of(const tgo_ctx* ctx);
 int part_pr_layout_of(tgo_ctx* ctx, int32_t* world, int64_t* hot, int64_t* span);
+int part_upload(tgo_ctx* ctx, HostGraph& h, int64_t n_global, int64_t lo);
+int part_rows_decode(tgo_ctx* ctx, const tgo_rows* rows, const tgo_schema* schema, const tgo_load_opts* opts,
+                     RowStaging& st, std::string& err);
+int part_threads(const tgo_ctx* ctx);
+void part_set_live(tgo_ctx* ctx, int64_t live);
 template <class T>
 int scratch(tgo_ctx* ctx, T*& p, int64_t count, int slot) {
     void* q = nullptr;
@@ -815,6 +820,11 @@ extern "C" int tgo_part_sssp_run(tgo_ctx* ctx, tgo_exchange* x, int64_t seed_glo
     if ((rc = scratch(ctx, send, 2 * ng + 2, 14)) || (rc = scratch(ctx, recv, 2 * ng + 2, 15)) ||
         (rc = scratch(ctx, sizes, 11 * W + 3, 16)))
         return rc;
+    // negative weights: every rank fails here, before any collective a peer could wait in
+    int64_t wmin = 0, gmin = 0;
+    if ((rc = tgo_part_weight_min(ctx, &wmin))) return rc;
+    if ((rc = d.reduce(&wmin, 1, tgo_exchange::kRedMin, &gmin))) return rc;
+    if (gmin < 0) return part_fail(ctx, TGO_E_INVALID, "delta-stepping needs non-negative weights (a rank holds a negative weight)");
     int64_t out[2] = {0, 0};
     if ((rc = tgo_part_sssp_begin(ctx, seed_global, delta, out))) return rc;
     if (delta <= 0) {           // the ranks' default widths follow their local mean weight: agree on one
@@ -962,5 +972,134 @@ extern "C" int tgo_part_pagerank_run(tgo_ctx* ctx, tgo_exchange* x, const tgo_pr
     tgo_part_pr_plain(ctx, 0);
     if (rc) return rc;
     if (exchanged_bytes) *exchanged_bytes = moved;
+    return TGO_OK;
+}
+
+// ======================================================================================
+// The partitioned load from edgestore rows.  Rank r hands in the rows of its vertices (a row
+// holds the vertex's OUT and IN entries, so a 1-D vertex partition is a row-range partition of
+// the scan); the decode and the cut are the one-GPU rules per row (VertexJobConverter.java:
+// 109-129, the 100 000 cap in column order: QueryContainer.java:28,122, ColumnValueStore.java:
+// 47-69), so every rank's lists are exactly the lists tgo_load_rows would hold for those rows.
+// Collectives (all on the exchange, every rank in the same order):
+//   1. MAX of {decode failed, live rows}: a failure on any rank fails every rank here;
+//      S = the largest live count rounded up to 64 (slot ids r * S + i, padding entry-less);
+//   2. all-gather of the live Titan ids at their slots: the global id map;
+//   3. (layout) all-gather of the degree-grouped slot layout;
+//   4. SUM of the cut rows; when a single-direction scope cut any row, its push view is no
+//      transpose of the stored opposite lists: the pull entries go to their sources' owners
+//      (all-to-all of the counts, all-to-allv of the pairs) and become the push rows there.
+namespace {
+struct DevTmp {                 // a device temporary of the load (the ctx holds no graph yet)
+    void* p = nullptr;
+    ~DevTmp() { if (p) (void)hipFree(p); }
+    hipError_t alloc(size_t bytes) { return hipMalloc(&p, std::max<size_t>(bytes, 8)); }
+};
+}  // namespace
+
+extern "C" int tgo_load_partition_rows(tgo_ctx* ctx, tgo_exchange* x, const tgo_rows* rows, const tgo_schema* schema,
+                                       const tgo_load_opts* opts, int32_t layout, int64_t* part_out) {
+    if (!ctx) return TGO_E_INVALID;
+    if (!x || !rows || !schema || !opts || !part_out || x->world < 1 || x->rank < 0 || x->rank >= x->world)
+        return part_fail(ctx, TGO_E_INVALID, "tgo_load_partition_rows: bad arguments");
+    const auto t0 = std::chrono::steady_clock::now();
+    const int W = x->world, R = x->rank;
+    hipStream_t st = part_stream(ctx);
+    std::string err;
+    auto xerr = [&](int code) { return part_fail(ctx, code, "exchange: " + x->err); };
+    auto hip = [&](const char* what) { x->abort(); return part_fail(ctx, TGO_E_HIP, std::string("tgo_load_partition_rows: ") + what); };
+    DevTmp red;
+    if (red.alloc(8 * sizeof(int64_t)) != hipSuccess) return hip("scratch");
+    // element-wise reduction of k host words over the ranks
+    auto reduce = [&](int64_t* v, int k, int op) -> int {
+        if (hipMemcpyAsync(red.p, v, k * sizeof(int64_t), hipMemcpyHostToDevice, st) != hipSuccess) return hip("reduce upload");
+        if (int r = x->all_reduce(static_cast<int64_t*>(red.p), static_cast<size_t>(k), op, st)) return xerr(r);
+        if (hipMemcpyAsync(v, red.p, k * sizeof(int64_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            return hip("reduce read");
+        return TGO_OK;
+    };
+    // 1. decode, then agree on failure and on the slot size
+    RowStaging stg;
+    const int drc = part_rows_decode(ctx, rows, schema, opts, stg, err);
+    const int64_t count = drc ? 0 : static_cast<int64_t>(stg.vid.size());
+    int64_t v1[2] = {drc ? 1 : 0, count};
+    if (int rc = reduce(v1, 2, tgo_exchange::kRedMax)) return rc;
+    if (drc) return part_fail(ctx, drc, "tgo_load_partition_rows: " + err);
+    if (v1[0]) return part_fail(ctx, TGO_E_INVALID, "tgo_load_partition_rows: another rank failed to decode its rows");
+    const int64_t S = std::max<int64_t>(64, (v1[1] + 63) / 64 * 64), lo = static_cast<int64_t>(R) * S;
+    const int64_t n_global = static_cast<int64_t>(W) * S;
+    if (n_global >= INT32_MAX) return part_fail(ctx, TGO_E_UNSUPPORTED, "tgo_load_partition_rows: more than 2^31 - 1 slots");
+    // 2. the global id map: every rank's live ids at their slots
+    std::vector<int64_t> slot_vid(static_cast<size_t>(n_global));
+    {
+        DevTmp buf;
+        if (buf.alloc(n_global * sizeof(int64_t)) != hipSuccess) return hip("id buffer");
+        std::vector<int64_t> own(static_cast<size_t>(S));
+        for (int64_t i = 0; i < S; ++i) own[i] = i < count ? stg.vid[i] : -1 - (lo + i);   // padding: never a Titan id
+        int64_t* b = static_cast<int64_t*>(buf.p);
+        if (hipMemcpyAsync(b + lo, own.data(), S * sizeof(int64_t), hipMemcpyHostToDevice, st) != hipSuccess)
+            return hip("id upload");
+        if (int r = x->all_gather(b, static_cast<size_t>(S) * sizeof(int64_t), st)) return xerr(r);
+        if (hipMemcpyAsync(slot_vid.data(), b, n_global * sizeof(int64_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            return hip("id read");
+    }
+    HostGraph h;
+    const int threads = part_threads(ctx);
+    int arc = assemble_partition_rows(stg, slot_vid, S, R, h, threads, err);
+    std::vector<int64_t>().swap(slot_vid);
+    // 3. the degree-grouped layout of every rank's slots
+    if (!arc && layout) {
+        DevTmp buf;
+        if (buf.alloc(n_global * sizeof(int32_t)) != hipSuccess) return hip("layout buffer");
+        std::vector<int32_t> lay(static_cast<size_t>(n_global));
+        partition_rows_layout(h, lo, lay.data() + lo);
+        int32_t* b = static_cast<int32_t*>(buf.p);
+        if (hipMemcpyAsync(b + lo, lay.data() + lo, S * sizeof(int32_t), hipMemcpyHostToDevice, st) != hipSuccess)
+            return hip("layout upload");
+        if (int r = x->all_gather(b, static_cast<size_t>(S) * sizeof(int32_t), st)) return xerr(r);
+        if (hipMemcpyAsync(lay.data(), b, n_global * sizeof(int32_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            return hip("layout read");
+        arc = apply_partition_layout(h, lo, lay.data(), threads, err);
+    }
+    // 4. cut rows anywhere: the push view from every rank's pull entries (and a last agreement
+    //    on failure before the graph replaces the ctx's)
+    int64_t v4[2] = {arc ? 1 : 0, h.truncated};
+    if (int rc = reduce(v4, 2, tgo_exchange::kRedSum)) return rc;
+    if (arc) return part_fail(ctx, arc, "tgo_load_partition_rows: " + err);
+    if (v4[0]) return part_fail(ctx, TGO_E_INVALID, "tgo_load_partition_rows: another rank failed to assemble its rows");
+    if (v4[1] > 0 && opts->scope != TGO_SCOPE_BOTH_E) {
+        std::vector<int64_t> cnt, pairs;
+        partition_pull_pairs(h, lo, S, W, cnt, pairs);
+        DevTmp dc, rc_, sbuf, rbuf;
+        if (dc.alloc(W * sizeof(int64_t)) != hipSuccess || rc_.alloc(W * sizeof(int64_t)) != hipSuccess) return hip("count buffers");
+        std::vector<int64_t> rcnt(W);
+        if (hipMemcpyAsync(dc.p, cnt.data(), W * sizeof(int64_t), hipMemcpyHostToDevice, st) != hipSuccess) return hip("counts");
+        if (int r = x->all_to_all(dc.p, rc_.p, sizeof(int64_t), st)) return xerr(r);
+        if (hipMemcpyAsync(rcnt.data(), rc_.p, W * sizeof(int64_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            return hip("count read");
+        std::vector<size_t> sb(W), so(W), rb(W), ro(W);
+        size_t a = 0, b = 0;
+        for (int p = 0; p < W; ++p) {
+            sb[p] = static_cast<size_t>(cnt[p]) * 16; so[p] = a; a += sb[p];
+            rb[p] = static_cast<size_t>(rcnt[p]) * 16; ro[p] = b; b += rb[p];
+        }
+        if (sbuf.alloc(a) != hipSuccess || rbuf.alloc(b) != hipSuccess) return hip("pair buffers");
+        if (a && hipMemcpyAsync(sbuf.p, pairs.data(), a, hipMemcpyHostToDevice, st) != hipSuccess) return hip("pairs");
+        if (int r = x->all_to_allv(sbuf.p, sb.data(), so.data(), rbuf.p, rb.data(), ro.data(), st)) return xerr(r);
+        std::vector<int64_t> recv(b / 8);
+        if ((b && hipMemcpyAsync(recv.data(), rbuf.p, b, hipMemcpyDeviceToHost, st) != hipSuccess) ||
+            hipStreamSynchronize(st) != hipSuccess)
+            return hip("pair read");
+        partition_push_from_pairs(h, recv.data(), static_cast<int64_t>(b / 16));
+    }
+    if (int rc = part_upload(ctx, h, n_global, lo)) return rc;
+    part_set_live(ctx, count);
+    part_out[0] = count;
+    part_out[1] = S;
+    (void)t0;
     return TGO_OK;
 }

@@ -470,6 +470,12 @@ class HipPartBackend:
         return out
 
     # delta-stepping SSSP local steps
+    def weight_min(self):
+        """The smallest weight of this rank's load, 0 without weights (tgo_part_weight_min)."""
+        w = C.c_int64()
+        self.e.part_call("tgo_part_weight_min", C.byref(w))
+        return w.value
+
     def sssp_begin(self, seed, delta):
         c = np.zeros(2, np.int64)
         self.e.part_call("tgo_part_sssp_begin", C.c_int64(seed), C.c_int64(delta), L.ptr(c, C.c_int64))
@@ -858,6 +864,12 @@ def distributed_sssp(backend, seed: int, delta: int = 0, fetch: bool = True, sta
     world = cm.world
     dev = backend.device
     n = backend.n_global
+    # negative weights fail every rank together, before a peer could wait in an exchange
+    wmin = torch.tensor([int(backend.weight_min())], dtype=torch.int64, device=dev)
+    cm.all_reduce(wmin, op="min")
+    if int(wmin.item()) < 0:
+        from .engine import TitanException
+        raise TitanException(L.TGO_E_INVALID, "delta-stepping needs non-negative weights (a rank holds a negative weight)")
     send = _scratch(backend, "pairs_send", 2 * n, torch.int64)
     recv = _scratch(backend, "pairs_recv", 2 * n, torch.int64)
     qlen, dflt = (int(x) for x in backend.sssp_begin(seed, delta))
@@ -890,6 +902,23 @@ def distributed_sssp(backend, seed: int, delta: int = 0, fetch: bool = True, sta
     if stats:
         reached = _allreduce_counts(reached, dev, cm)
     return out, reached, phases
+
+
+def balanced_row_ranges(entry_begin, world: int):
+    """Contiguous row ranges [(a, b)] of a scan's rows for `world` ranks, balanced by entries +
+    rows (a row holds its vertex's OUT and IN entries, so this is the edge-balanced 1-D vertex
+    partition of tgo_load_partition_rows; java PartitionedRun.rowRanges restates it): range r
+    ends at the first row whose prefix weight reaches (r + 1) / world of the total."""
+    eb = np.asarray(entry_begin, np.int64)
+    nrows = len(eb) - 1
+    prefix = eb + np.arange(nrows + 1, dtype=np.int64)       # entries + rows before row i
+    total = int(prefix[-1])
+    cuts = [0]
+    for r in range(1, world):
+        target = (total * r + world - 1) // world
+        cuts.append(max(cuts[-1], min(nrows, int(np.searchsorted(prefix, target, side="left")))))
+    cuts.append(nrows)
+    return [(cuts[r], cuts[r + 1]) for r in range(world)]
 
 
 def gathered_index(u, n_local: int, world: int, hot: int, span: int):

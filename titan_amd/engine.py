@@ -188,6 +188,28 @@ class Engine:
         self.n = self.lib.tgo_num_vertices(self.ctx)
         return self
 
+    def load_partition_rows(self, exchange, rows, schema: Schema, scope, apply_cap=True, labels=(), weight_key=0,
+                            layout=True):
+        """This rank's rows of a row-range partition of the scan (tgo_load_partition_rows; a
+        collective over `exchange`, a distributed.NativeExchange): the one-GPU decode and cut per
+        row, global slot ids.  Returns (live rows here, slot size S): n_global = world * S,
+        lo = rank * S; results are the first `live` entries of the rank's outputs, whose ids are
+        vertex_ids()[:live]."""
+        opts, keep = self._opts(scope, apply_cap, labels, weight_key)
+        keys = np.ascontiguousarray(rows.keys, dtype=np.int64)
+        eb = np.ascontiguousarray(rows.entry_begin, dtype=np.int64)
+        bb = np.ascontiguousarray(rows.byte_begin, dtype=np.int64)
+        data = np.ascontiguousarray(rows.data if len(rows.data) else np.zeros(1, np.uint8), dtype=np.uint8)
+        lv = np.ascontiguousarray(rows.limit_valpos if len(rows.limit_valpos) else np.zeros(1, np.int64), dtype=np.int64)
+        cr = L.Rows(rows.nrows, L.ptr(keys, C.c_int64), L.ptr(eb, C.c_int64), L.ptr(bb, C.c_int64),
+                    L.ptr(data, C.c_uint8), L.ptr(lv, C.c_int64))
+        part = np.zeros(2, np.int64)
+        _check(self.lib, self.ctx, self.lib.tgo_load_partition_rows(self.ctx, exchange.h, C.byref(cr), C.byref(schema.c),
+                                                                    C.byref(opts), 1 if layout else 0,
+                                                                    L.ptr(part, C.c_int64)))
+        self.n = self.lib.tgo_num_vertices(self.ctx)
+        return int(part[0]), int(part[1])
+
     def part_call(self, name, *args):
         _check(self.lib, self.ctx, getattr(self.lib, name)(self.ctx, *args))
 
