@@ -252,8 +252,10 @@ int  tgo_part_pagerank_run(tgo_ctx* ctx, tgo_exchange* x, const tgo_pr_args* arg
 /* The partitioned load from edgestore rows: the multi-GPU form of tgo_load_rows +
  * tgo_finish_load (one scan, VertexJobConverter.java:109-129).  A Titan row holds a vertex's
  * OUT and IN entries, so the 1-D vertex partition is a row-range partition of the scan: rank r
- * of the exchange passes the rows of ITS vertices (any split of the scan's rows over the ranks;
- * edge-balanced ranges balance the work).  Each rank decodes its rows with the one-GPU rules —
+ * of the exchange stages the rows of ITS vertices with tgo_load_rows (work blocks, local, any
+ * split of the scan's rows over the ranks; edge-balanced ranges balance the work), then every
+ * rank calls tgo_finish_partition_rows instead of tgo_finish_load (tgo_load_partition_rows =
+ * one tgo_load_rows block + the finish; a failed stage still joins the collective).  Each rank decodes its rows with the one-GPU rules —
  * key filter, ghosts, typed scopes, and the hard-limit cut per row in column order
  * (QueryContainer.java:28,122; ColumnValueStore.java:47-69) — so its lists are exactly the
  * lists a one-GPU load keeps for those rows.  Collective (every rank calls it with the same
@@ -264,8 +266,10 @@ int  tgo_part_pagerank_run(tgo_ctx* ctx, tgo_exchange* x, const tgo_pr_args* arg
  * direction scope makes the push view no transpose of the stored lists — the push rows (every
  * rank's pull entries sent to their sources' owners).  part[0] = this rank's live rows (its
  * results are the first part[0] of the tgo_part_* outputs, in row order; tgo_vertex_ids gives
- * their ids), part[1] = S; n_global = world * S, lo = rank * S for the tgo_part_* calls.
+ * their ids), part[1] = S, part[2] = the live rows of every rank (the job's vertex count);
+ * n_global = world * S, lo = rank * S for the tgo_part_* calls.
  * TGO_E_UNSUPPORTED for vertex cuts (they fold on one GPU) and non-Integer weight keys. */
+int  tgo_finish_partition_rows(tgo_ctx* ctx, tgo_exchange* x, int32_t layout, int64_t* part);
 int  tgo_load_partition_rows(tgo_ctx* ctx, tgo_exchange* x, const tgo_rows* rows, const tgo_schema* schema,
                              const tgo_load_opts* opts, int32_t layout, int64_t* part);
 

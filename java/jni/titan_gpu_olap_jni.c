@@ -540,3 +540,32 @@ JNIEXPORT jlongArray JNICALL JFN(partMsLevels)(JNIEnv* env, jclass cls, jlong h,
     if (p) (*env)->ReleaseLongArrayElements(env, out, p, 0);
     return rc == TGO_OK ? out : NULL;
 }
+
+/* tgo_finish_partition_rows after this worker's loadRows blocks (collective over the exchange):
+ * long[4] = {status, live rows here, slot size S, live rows of every worker}; the status is
+ * returned rather than thrown so that the caller can tell TGO_E_UNSUPPORTED (vertex cuts, a
+ * non-Integer weight key: the graph runs on one device) from a failure.  null only without
+ * memory for the array. */
+JNIEXPORT jlongArray JNICALL JFN(finishPartitionRows)(JNIEnv* env, jclass cls, jlong h, jlong x, jboolean layout) {
+    (void)cls;
+    jlong out[4] = {TGO_E_INVALID, 0, 0, 0};
+    if (h && x) {
+        int64_t part[3] = {0, 0, 0};
+        out[0] = tgo_finish_partition_rows(CTX(h), XCH(x), layout ? 1 : 0, part);
+        out[1] = part[0]; out[2] = part[1]; out[3] = part[2];
+    }
+    jlongArray a = (*env)->NewLongArray(env, 4);
+    if (a) (*env)->SetLongArrayRegion(env, a, 0, 4, out);
+    return a;
+}
+
+/* tgo_part_weight_min: long[2] = {status, smallest weight of this worker's load (0 unweighted)}. */
+JNIEXPORT jlongArray JNICALL JFN(partWeightMin)(JNIEnv* env, jclass cls, jlong h) {
+    (void)cls;
+    int64_t w = 0;
+    jlong out[2] = {h ? tgo_part_weight_min(CTX(h), &w) : TGO_E_INVALID, 0};
+    out[1] = w;
+    jlongArray a = (*env)->NewLongArray(env, 2);
+    if (a) (*env)->SetLongArrayRegion(env, a, 0, 2, out);
+    return a;
+}

@@ -10,6 +10,7 @@ import com.thinkaurelius.titan.diskstorage.keycolumnvalue.scan.StandardScanner;
 import com.thinkaurelius.titan.graphdb.database.StandardTitanGraph;
 import com.thinkaurelius.titan.graphdb.olap.QueryContainer;
 import com.thinkaurelius.titan.graphdb.olap.gpu.CsrCollectingScanJob;
+import com.thinkaurelius.titan.graphdb.olap.gpu.PartitionedRun;
 import com.thinkaurelius.titan.graphdb.olap.gpu.TgoNative;
 import org.apache.commons.configuration.BaseConfiguration;
 import org.apache.tinkerpop.gremlin.process.computer.ComputerResult;
@@ -138,7 +139,7 @@ public class GpuGraphComputer implements TitanGraphComputer {
             throw GraphComputer.Exceptions.resultGraphPersistCombinationNotSupported(resultGraph, persist);
         final DeviceProgram program = DeviceProgram.recognise(vertexProgram);
         final FulgoraMemory memory = new FulgoraMemory(vertexProgram, mapReduces);
-        if (devices != null && program.partitioned(Long.MAX_VALUE) != null)
+        if (devices != null && program.partitioned() != null)
             return CompletableFuture.<ComputerResult>supplyAsync(() -> submitPartitioned(program, memory, persist,
                     resultGraph));
         return CompletableFuture.<ComputerResult>supplyAsync(() -> {
@@ -148,58 +149,13 @@ public class GpuGraphComputer implements TitanGraphComputer {
             if (ctx == 0) throw new TitanException("no usable gfx950 device (the GPU engine has no CPU fallback)");
             try {
                 // (1) one scan collects the rows the program's scope preloads
-                CsrCollectingScanJob.Handle handle = new CsrCollectingScanJob.Handle(ctx, graph.getIDManager(),
-                        Schemas.edgeTypes(graph), Schemas.propertyKeys(graph), program.scope(), true, new long[0],
-                        program.weightKey(graph));
-                StandardScanner.Builder scan = graph.getBackend().buildEdgeScanJob();
-                scan.setJobId("gpu-olap#load");
-                scan.setNumProcessingThreads(numThreads);
-                scan.setWorkBlockSize(CsrCollectingScanJob.DEFAULT_BLOCK_ROWS);
-                scan.setJob(new CsrCollectingScanJob(handle));
-                ScanMetrics m = scan.execute().get();
-                if (m.get(ScanMetrics.Metric.FAILURE) > 0)
-                    throw new TitanException("Failed to process [" + m.get(ScanMetrics.Metric.FAILURE) + "] rows");
+                CsrCollectingScanJob.Handle handle = handle(ctx, null, program);
+                scan(handle, "gpu-olap#load");
                 // a block whose flush failed in workerIterationEnd is only logged by the scanner
                 // (StandardScannerExecutor.java:278-282): the handle keeps that failure
                 handle.rethrowFailure();
                 TgoNative.check(ctx, TgoNative.finishLoad(ctx));
-                // (2) the program on the device.  Fulgora runs supersteps 0..T (T = the first
-                // iteration whose terminate() holds: maxIterations, maxDepth, length) and
-                // increments the iteration after each of them, the terminating one included
-                // (FulgoraGraphComputer.java:181-188); complete() then steps back once
-                // (FulgoraMemory.java:73-76), so getIteration() reports T (OLAPTest.java:219,255)
-                long[] ids = TgoNative.vertexIds(ctx);
-                Map<String, Object> values = program.run(ctx);
-                for (int i = 0; i <= program.iterations(); i++) memory.incrIteration();
-                // (3) map / reduce / addResultToMemory as Fulgora's map phase
-                for (MapReduce mr : mapReduces) {
-                    FulgoraMapEmitter emitter = new FulgoraMapEmitter<>(mr.doStage(MapReduce.Stage.REDUCE));
-                    program.emit(ids, values, emitter);
-                    emitter.complete(mr);
-                    if (mr.doStage(MapReduce.Stage.REDUCE)) {
-                        FulgoraReduceEmitter reduce = new FulgoraReduceEmitter<>();
-                        mr.workerStart(MapReduce.Stage.REDUCE);
-                        for (Object e : emitter.reduceMap.entrySet()) {
-                            Map.Entry entry = (Map.Entry) e;
-                            mr.reduce(entry.getKey(), ((Iterable) entry.getValue()).iterator(), reduce);
-                        }
-                        mr.workerEnd(MapReduce.Stage.REDUCE);
-                        reduce.complete(mr);
-                        mr.addResultToMemory(memory, reduce.reduceQueue.iterator());
-                    } else {
-                        mr.addResultToMemory(memory, emitter.mapQueue.iterator());
-                    }
-                }
-                // (4) write-back of the compute keys
-                org.apache.tinkerpop.gremlin.structure.Graph result = graph;
-                if (persist == Persist.VERTEX_PROPERTIES) {
-                    if (resultGraph == ResultGraph.NEW) result = WriteBack.localTx(graph, ids, values, program);
-                    else if (WriteBack.directWriteSafe(graph, program)) WriteBack.persist(graph, ctx, program);
-                    else WriteBack.transactional(graph, ids, values, program, numThreads);
-                }
-                memory.setRuntime(System.currentTimeMillis() - start);
-                memory.complete();
-                return new DefaultComputerResult(result, memory.asImmutable());
+                return runLoaded(ctx, program, memory, persist, resultGraph, start);
             } catch (TitanException e) {
                 throw e;
             } catch (Exception e) {
@@ -210,51 +166,108 @@ public class GpuGraphComputer implements TitanGraphComputer {
         });
     }
 
+    /** The collecting scan's shared handle: rows to tgo_load_rows on ctx, or to sink. */
+    private CsrCollectingScanJob.Handle handle(long ctx, CsrCollectingScanJob.BlockSink sink, DeviceProgram program) {
+        return new CsrCollectingScanJob.Handle(ctx, sink, graph.getIDManager(), Schemas.edgeTypes(graph),
+                Schemas.propertyKeys(graph), program.scope(), true, new long[0], program.weightKey(graph));
+    }
+
+    /** The one edgestore scan (StandardScanner over the edgestore, Backend.buildEdgeScanJob). */
+    private void scan(CsrCollectingScanJob.Handle handle, String jobId) throws Exception {
+        StandardScanner.Builder scan = graph.getBackend().buildEdgeScanJob();
+        scan.setJobId(jobId);
+        scan.setNumProcessingThreads(numThreads);
+        scan.setWorkBlockSize(CsrCollectingScanJob.DEFAULT_BLOCK_ROWS);
+        scan.setJob(new CsrCollectingScanJob(handle));
+        ScanMetrics m = scan.execute().get();
+        if (m.get(ScanMetrics.Metric.FAILURE) > 0)
+            throw new TitanException("Failed to process [" + m.get(ScanMetrics.Metric.FAILURE) + "] rows");
+    }
+
     /**
-     * The multi-GPU path: one decoding scan (PartitionedRun.EdgeCollectingScanJob), then one
-     * worker per device; the map phase and the write-back are the single-GPU path's, on the
-     * gathered results (row order = the sorted live vertex ids).  The device-encoded write-back
-     * needs one ctx holding every vertex, so results persist through the transactional path.
+     * Steps (2)-(4) on a loaded ctx: the program on the device, the map phase, the write-back.
+     * Fulgora runs supersteps 0..T (T = the first iteration whose terminate() holds: maxIterations,
+     * maxDepth, length) and increments the iteration after each of them, the terminating one
+     * included (FulgoraGraphComputer.java:181-188); complete() then steps back once
+     * (FulgoraMemory.java:73-76), so getIteration() reports T (OLAPTest.java:219,255).
+     */
+    private ComputerResult runLoaded(long ctx, DeviceProgram program, FulgoraMemory memory, Persist persist,
+                                     ResultGraph resultGraph, long start) throws Exception {
+        long[] ids = TgoNative.vertexIds(ctx);
+        Map<String, Object> values = program.run(ctx);
+        for (int i = 0; i <= program.iterations(); i++) memory.incrIteration();
+        mapPhase(program, ids, values, memory);
+        org.apache.tinkerpop.gremlin.structure.Graph result = graph;
+        if (persist == Persist.VERTEX_PROPERTIES) {
+            if (resultGraph == ResultGraph.NEW) result = WriteBack.localTx(graph, ids, values, program);
+            else if (WriteBack.directWriteSafe(graph, program)) WriteBack.persist(graph, ctx, program);
+            else WriteBack.transactional(graph, ids, values, program, numThreads);
+        }
+        memory.setRuntime(System.currentTimeMillis() - start);
+        memory.complete();
+        return new DefaultComputerResult(result, memory.asImmutable());
+    }
+
+    /** (3) map / reduce / addResultToMemory as Fulgora's map phase (FulgoraGraphComputer.java:192-246). */
+    private void mapPhase(DeviceProgram program, long[] ids, Map<String, Object> values, FulgoraMemory memory) {
+        for (MapReduce mr : mapReduces) {
+            FulgoraMapEmitter emitter = new FulgoraMapEmitter<>(mr.doStage(MapReduce.Stage.REDUCE));
+            program.emit(ids, values, emitter);
+            emitter.complete(mr);
+            if (mr.doStage(MapReduce.Stage.REDUCE)) {
+                FulgoraReduceEmitter reduce = new FulgoraReduceEmitter<>();
+                mr.workerStart(MapReduce.Stage.REDUCE);
+                for (Object e : emitter.reduceMap.entrySet()) {
+                    Map.Entry entry = (Map.Entry) e;
+                    mr.reduce(entry.getKey(), ((Iterable) entry.getValue()).iterator(), reduce);
+                }
+                mr.workerEnd(MapReduce.Stage.REDUCE);
+                reduce.complete(mr);
+                mr.addResultToMemory(memory, reduce.reduceQueue.iterator());
+            } else {
+                mr.addResultToMemory(memory, emitter.mapQueue.iterator());
+            }
+        }
+    }
+
+    /**
+     * The multi-GPU path: one scan keeps the raw rows in work blocks (PartitionedRun.RowBlocks),
+     * then one worker per device loads its row range and runs the program; the map phase and
+     * the write-back are the single-GPU path's, on the gathered results.  A graph the
+     * partitioned programs do not cover (PartitionedRun.NotPartitionable: vertex cuts, a
+     * non-Integer weight key, a negative weight, a depth bound that can cut a path, no vertex)
+     * runs on the first device from the same rows, without a second scan.  The device-encoded
+     * write-back needs one ctx holding every vertex, so results persist transactionally.
      */
     private ComputerResult submitPartitioned(DeviceProgram program, FulgoraMemory memory, Persist persist,
                                              ResultGraph resultGraph) {
         final long start = System.currentTimeMillis();
         try {
-            PartitionedRun.Collected collected = new PartitionedRun.Collected(program.weightKey(graph) != 0);
-            StandardScanner.Builder scan = graph.getBackend().buildEdgeScanJob();
-            scan.setJobId("gpu-olap#partitioned-load");
-            scan.setNumProcessingThreads(numThreads);
-            scan.setWorkBlockSize(CsrCollectingScanJob.DEFAULT_BLOCK_ROWS);
-            scan.setJob(new PartitionedRun.EdgeCollectingScanJob(graph, program.weightKey(graph), collected));
-            ScanMetrics m = scan.execute().get();
-            if (m.get(ScanMetrics.Metric.FAILURE) > 0)
-                throw new TitanException("Failed to process [" + m.get(ScanMetrics.Metric.FAILURE) + "] rows");
-            PartitionedRun.Program p = program.partitioned(collected.vertices.size);
-            if (p == null) throw new TitanException("the program cannot run partitioned on this graph");
-            Object[] out = PartitionedRun.run(collected, p, devices, graph.getIDManager().getPartitionBits(), numThreads,
-                    QueryContainer.DEFAULT_HARD_QUERY_LIMIT);
+            PartitionedRun.RowBlocks rows = new PartitionedRun.RowBlocks();
+            CsrCollectingScanJob.Handle handle = handle(0, rows, program);
+            scan(handle, "gpu-olap#partitioned-load");
+            handle.rethrowFailure();
+            Object[] out;
+            try {
+                out = PartitionedRun.run(rows, handle, program.partitioned(), devices, graph.getIDManager().getPartitionBits(),
+                        numThreads, QueryContainer.DEFAULT_HARD_QUERY_LIMIT);
+            } catch (PartitionedRun.NotPartitionable e) {
+                long ctx = TgoNative.create(device, graph.getIDManager().getPartitionBits(), numThreads,
+                        QueryContainer.DEFAULT_HARD_QUERY_LIMIT);
+                if (ctx == 0) throw new TitanException("no usable gfx950 device (the GPU engine has no CPU fallback)");
+                try {
+                    rows.loadInto(ctx, handle);
+                    TgoNative.check(ctx, TgoNative.finishLoad(ctx));
+                    return runLoaded(ctx, program, memory, persist, resultGraph, start);
+                } finally {
+                    TgoNative.destroy(ctx);
+                }
+            }
             long[] ids = (long[]) out[0];
             Map<String, Object> values = new HashMap<>();
             values.put(program.computeKeys()[0], out[1]);
             for (int i = 0; i <= program.iterations(); i++) memory.incrIteration();
-            for (MapReduce mr : mapReduces) {
-                FulgoraMapEmitter emitter = new FulgoraMapEmitter<>(mr.doStage(MapReduce.Stage.REDUCE));
-                program.emit(ids, values, emitter);
-                emitter.complete(mr);
-                if (mr.doStage(MapReduce.Stage.REDUCE)) {
-                    FulgoraReduceEmitter reduce = new FulgoraReduceEmitter<>();
-                    mr.workerStart(MapReduce.Stage.REDUCE);
-                    for (Object e : emitter.reduceMap.entrySet()) {
-                        Map.Entry entry = (Map.Entry) e;
-                        mr.reduce(entry.getKey(), ((Iterable) entry.getValue()).iterator(), reduce);
-                    }
-                    mr.workerEnd(MapReduce.Stage.REDUCE);
-                    reduce.complete(mr);
-                    mr.addResultToMemory(memory, reduce.reduceQueue.iterator());
-                } else {
-                    mr.addResultToMemory(memory, emitter.mapQueue.iterator());
-                }
-            }
+            mapPhase(program, ids, values, memory);
             org.apache.tinkerpop.gremlin.structure.Graph result = graph;
             if (persist == Persist.VERTEX_PROPERTIES) {
                 if (resultGraph == ResultGraph.NEW) result = WriteBack.localTx(graph, ids, values, program);
@@ -498,11 +511,8 @@ public class GpuGraphComputer implements TitanGraphComputer {
                 mgmt.rollback();
             }
         }
-        /**
-         * The multi-GPU form of the program over n live vertices, or null when it has none
-         * (then the program runs on one device).
-         */
-        PartitionedRun.Program partitioned(long n) { return null; }
+        /** The multi-GPU form of the program, or null when it has none (then it runs on one device). */
+        PartitionedRun.Program partitioned() { return null; }
         /** The value of compute-key array `values` at row i, null when the vertex holds none. */
         Object valueAt(Object values, int i) {
             if (values instanceof long[]) { long d = ((long[]) values)[i]; return d == TgoNative.DIST_ABSENT ? null : d; }
@@ -555,15 +565,16 @@ public class GpuGraphComputer implements TitanGraphComputer {
             v.put("titan.pageRank.pageRank", TgoNative.checked(ctx, TgoNative.pageRank(ctx, alpha, vertexCount, maxIterations)));
             return v;
         }
-        PartitionedRun.Program partitioned(long n) {
+        PartitionedRun.Program partitioned() {
             return new PartitionedRun.Program() {
                 public int scope() { return TgoNative.SCOPE_IN_E; }
                 public boolean applyCap() { return true; }
-                public Object run(long ctx, long x, long[] live) {
+                public boolean partitions(long n) { return n > 0; }
+                public boolean needsNonNegativeWeights() { return false; }
+                public Object run(long ctx, long x, long[] ownIds, long lo) {
                     return TgoNative.partPageRankRun(ctx, x, alpha, vertexCount, maxIterations,
                             PartitionedRun.PR_EXCHANGE_GHOST);
                 }
-                public Object newResult(int count) { return new double[count]; }
             };
         }
         void emit(long[] ids, Map<String, Object> values, FulgoraMapEmitter emitter) {
@@ -601,21 +612,22 @@ public class GpuGraphComputer implements TitanGraphComputer {
         /**
          * Partitioned: delta-stepping's converged distances, which equal the hop-bounded result
          * only when no shortest path can exceed maxDepth hops — maxDepth >= n - 1 (a shortest
-         * path visits each vertex once).  n is unknown before the scan (Long.MAX_VALUE asks
-         * whether a partitioned form may exist at all).
+         * path visits each vertex once), n = the job's live vertices (known after the load) —
+         * and only for non-negative weights (the reference's hop-bounded Jacobi takes any).
          */
-        PartitionedRun.Program partitioned(long n) {
-            if (n != Long.MAX_VALUE && maxDepth < n - 1) return null;
+        PartitionedRun.Program partitioned() {
             return new PartitionedRun.Program() {
                 public int scope() { return TgoNative.SCOPE_IN_E; }
                 public boolean applyCap() { return true; }
-                public Object run(long ctx, long x, long[] live) {
-                    // every worker runs the same phases (collectives), so a seed that is no live
-                    // vertex still runs: -1 reaches nobody (every distance TGO_DIST_ABSENT)
-                    int s = java.util.Arrays.binarySearch(live, seed);
-                    return TgoNative.partSsspRun(ctx, x, s >= 0 ? s : -1, 0);
+                public boolean partitions(long n) { return n > 0 && maxDepth >= n - 1; }
+                public boolean needsNonNegativeWeights() { return true; }
+                public Object run(long ctx, long x, long[] ownIds, long lo) {
+                    // every worker runs the same phases (collectives); only the seed's owner
+                    // seeds (a seed that is no live vertex reaches nobody: TGO_DIST_ABSENT)
+                    long s = -1;
+                    for (int i = 0; i < ownIds.length && s < 0; i++) if (ownIds[i] == seed) s = lo + i;
+                    return TgoNative.partSsspRun(ctx, x, s, 0);
                 }
-                public Object newResult(int count) { return new long[count]; }
             };
         }
         void emit(long[] ids, Map<String, Object> values, FulgoraMapEmitter emitter) {

@@ -54,9 +54,19 @@ public class CsrCollectingScanJob implements ScanJob {
     private ByteBuffer bytes;
     private int rows, entries;
 
+    /**
+     * Where full blocks go instead of one ctx: the multi-GPU path keeps the scan's blocks and
+     * hands each worker its row range ({@link PartitionedRun.RowBlocks}).  {@code bytes} holds
+     * {@code byteCount} bytes from position 0 and is reused after the call: copy it.
+     */
+    public interface BlockSink {
+        void accept(long[] keys, long[] entryBegin, long[] byteBegin, ByteBuffer bytes, int byteCount, long[] limitValuePos);
+    }
+
     /** Shared by all clones: the native context and what every tgo_load_rows call needs. */
     public static final class Handle {
         final long ctx;
+        final BlockSink sink;           // non-null: blocks go here, not to tgo_load_rows
         final IDManager idManager;
         final long[] edgeTypes, propertyKeys, labelIds;
         final int scope;
@@ -75,7 +85,13 @@ public class CsrCollectingScanJob implements ScanJob {
 
         public Handle(long ctx, IDManager idManager, long[] edgeTypes, long[] propertyKeys, int scope,
                       boolean applyCap, long[] labelIds, long weightKey) {
+            this(ctx, null, idManager, edgeTypes, propertyKeys, scope, applyCap, labelIds, weightKey);
+        }
+
+        public Handle(long ctx, BlockSink sink, IDManager idManager, long[] edgeTypes, long[] propertyKeys, int scope,
+                      boolean applyCap, long[] labelIds, long weightKey) {
             this.ctx = ctx;
+            this.sink = sink;
             this.idManager = idManager;
             this.edgeTypes = edgeTypes;
             this.propertyKeys = propertyKeys;
@@ -174,6 +190,10 @@ public class CsrCollectingScanJob implements ScanJob {
         synchronized (handle) {
             try {
                 if (handle.failure != null) return;       // the load is lost already: stop feeding it
+                if (handle.sink != null) {
+                    handle.sink.accept(k, eb, bb, bytes, (int) byteBegin[rows], lv);
+                    return;
+                }
                 TgoNative.check(handle.ctx, TgoNative.loadRows(handle.ctx, k, eb, bb, bytes, lv, handle.edgeTypes,
                         handle.propertyKeys, handle.scope, handle.applyCap, handle.labelIds, handle.weightKey));
             } catch (RuntimeException e) {

@@ -1,32 +1,17 @@
 package com.thinkaurelius.titan.graphdb.olap.gpu;
 
 import com.thinkaurelius.titan.core.TitanException;
-import com.thinkaurelius.titan.diskstorage.Entry;
-import com.thinkaurelius.titan.diskstorage.EntryList;
-import com.thinkaurelius.titan.diskstorage.StaticBuffer;
-import com.thinkaurelius.titan.diskstorage.configuration.Configuration;
-import com.thinkaurelius.titan.diskstorage.keycolumnvalue.SliceQuery;
-import com.thinkaurelius.titan.diskstorage.keycolumnvalue.scan.ScanJob;
-import com.thinkaurelius.titan.diskstorage.keycolumnvalue.scan.ScanMetrics;
-import com.thinkaurelius.titan.graphdb.database.StandardTitanGraph;
-import com.thinkaurelius.titan.graphdb.database.idhandling.IDHandler;
-import com.thinkaurelius.titan.graphdb.idmanagement.IDManager;
-import com.thinkaurelius.titan.graphdb.internal.RelationCategory;
-import com.thinkaurelius.titan.graphdb.olap.VertexJobConverter;
-import com.thinkaurelius.titan.graphdb.relations.RelationCache;
-import com.thinkaurelius.titan.graphdb.transaction.StandardTitanTx;
-import org.apache.tinkerpop.gremlin.structure.Direction;
 
+import java.nio.ByteBuffer;
+import java.nio.ByteOrder;
 import java.util.ArrayList;
-import java.util.Arrays;
 import java.util.List;
-import java.util.Map;
 import java.util.concurrent.CyclicBarrier;
 import java.util.concurrent.ExecutorService;
 import java.util.concurrent.Executors;
 import java.util.concurrent.Future;
 import java.util.concurrent.TimeUnit;
-import java.util.function.Predicate;
+import java.util.concurrent.atomic.AtomicBoolean;
 
 /**
  * The multi-GPU form of the GPU path ({@code GpuGraphComputer.devices(...)}): the graph is
@@ -36,215 +21,154 @@ import java.util.function.Predicate;
  * the job API in front of it is unchanged (TitanGraphComputer.java:8-43).
  *
  * <ol>
- * <li>ONE edgestore scan ({@link EdgeCollectingScanJob}) decodes every row with the graph's own
- *     EdgeSerializer (EdgeSerializer.java:73-166), as VertexJobConverter.process does per row
- *     (:109-129): ghost rows (no VertexExists entry) are skipped, vertex cuts fold into their
- *     canonical vertex (PartitionedVertexProgramExecutor.java:47-103), and every user edge is
- *     kept once, from its OUT entry.</li>
- * <li>The live vertices' Titan ids, sorted, are the global dense ids; edges to vertices that
- *     never execute are dropped (PreloadedVertex, VertexState.java:103-137).  The dense range
- *     is cut into {@code world} equal 64-aligned slices (padding ids are entry-less).</li>
- * <li>Worker r: tgo_part_layout of its slice (the degree-grouped order, gathered into one
- *     array every worker loads with), tgo_load_partition_layout of the edges with an endpoint
- *     in its slice (the program's scope and QueryContainer cap applied by the load), an RCCL
- *     exchange (worker 0's id, created by all workers together), then the program as ONE
- *     native call (tgo_part_pagerank_run / tgo_part_sssp_run), owned results into the
- *     global result arrays.</li>
+ * <li>ONE edgestore scan: the single-device path's {@link CsrCollectingScanJob} with a
+ *     {@link RowBlocks} sink, so the rows stay raw (StaticArrayEntryList form) and in scan
+ *     order, in work blocks.</li>
+ * <li>A Titan row holds its vertex's OUT and IN entries, so the 1-D vertex partition is a
+ *     row-range partition of the scan: worker r takes a contiguous range of blocks, balanced
+ *     by rows + entries ({@link #blockRanges}; titan_amd/distributed.py balanced_row_ranges is
+ *     the same rule over rows, and tests/test_java_partition.py pins this one).</li>
+ * <li>Worker r stages its blocks with tgo_load_rows (exactly the single-device decode: key
+ *     filter, ghosts, typed scopes, and the QueryContainer cap per row in column order,
+ *     QueryContainer.java:28,122 / ColumnValueStore.java:47-69), joins the RCCL exchange, and
+ *     finishes with tgo_finish_partition_rows (collective: global ids, layout, the push rows of
+ *     a cut scope); then the program as ONE native call (tgo_part_pagerank_run /
+ *     tgo_part_sssp_run); its results are its live rows' values, ids from tgo_vertex_ids.</li>
  * </ol>
- * A worker that fails before the exchange exists breaks the phase barrier, so the others stop
- * too; a failure inside a running program is reported by that worker, and the job's future
- * fails after {@link #RUN_TIMEOUT_MINUTES} if a peer stays blocked in a collective (RCCL does
- * not notify peers of an aborted communicator).
+ * Graphs the partitioned programs do not cover — vertex cuts (they fold into the canonical
+ * vertex on one device, VertexProgramScanJob.java:76-92), a non-Integer weight key, a negative
+ * weight for delta-stepping, a ShortestDistance depth that can cut a path, no vertex at all —
+ * raise {@link NotPartitionable} on every worker together; the caller then runs the single-
+ * device path on the same {@link RowBlocks} (no second scan).  A worker that fails before the
+ * exchange exists breaks the phase barrier, so the others stop too; the native calls after it
+ * agree on failure among themselves; the job's future fails after {@link #RUN_TIMEOUT_MINUTES}
+ * if a peer still stays blocked in a collective (RCCL does not notify peers of an aborted
+ * communicator).
  */
 public final class PartitionedRun {
 
     public static final int RUN_TIMEOUT_MINUTES = 60;
     /** titan_gpu_olap_part.h tgo_part_pagerank_run exchange modes */
     public static final int PR_EXCHANGE_ALLGATHER = 0, PR_EXCHANGE_GHOST = 1;
-    /** TGO_DIST_ABSENT / the Integer weight of an edge without the weight property (kMissingWeight). */
-    static final int MISSING_WEIGHT = Integer.MIN_VALUE;
 
     private PartitionedRun() {}
 
-    /** What a program runs on each worker: the native call, and how its owned results land. */
+    /** What a program runs on each worker: the native call over the loaded partition. */
     public interface Program {
         int scope();
         boolean applyCap();
-        /** The owned results of this worker (long[] or double[] of the slice length); live = the
-         *  sorted live vertex ids (global dense id = index), for seeds given as Titan ids. */
-        Object run(long ctx, long exchange, long[] live);
-        /** The global result array of n live vertices. */
-        Object newResult(int n);
+        /** Whether the program has a partitioned form for a job of n live vertices (ShortestDistance:
+         *  only when its depth cannot cut a path). */
+        boolean partitions(long n);
+        /** Whether it needs non-negative weights (delta-stepping). */
+        boolean needsNonNegativeWeights();
+        /** The worker's results (long[] or double[], at least ownIds.length entries, row order):
+         *  ownIds = this worker's live vertex ids in row order, lo = the global id of the first. */
+        Object run(long ctx, long exchange, long[] ownIds, long lo);
     }
 
-    // ------------------------------------------------------------------ the scanned graph
-    /** Growable int storage past the 2^31 element limit of one Java array. */
-    static final class IntChunks {
-        static final int CHUNK = 1 << 24;
-        final List<int[]> chunks = new ArrayList<>();
-        long size = 0;
-        void add(int v) {
-            if ((size & (CHUNK - 1)) == 0 && size / CHUNK == chunks.size()) chunks.add(new int[CHUNK]);
-            chunks.get((int) (size / CHUNK))[(int) (size & (CHUNK - 1))] = v;
-            size++;
-        }
-        int get(long i) { return chunks.get((int) (i / CHUNK))[(int) (i & (CHUNK - 1))]; }
-        void set(long i, int v) { chunks.get((int) (i / CHUNK))[(int) (i & (CHUNK - 1))] = v; }
-    }
-    static final class LongChunks {
-        static final int CHUNK = 1 << 23;
-        final List<long[]> chunks = new ArrayList<>();
-        long size = 0;
-        void add(long v) {
-            if ((size & (CHUNK - 1)) == 0 && size / CHUNK == chunks.size()) chunks.add(new long[CHUNK]);
-            chunks.get((int) (size / CHUNK))[(int) (size & (CHUNK - 1))] = v;
-            size++;
-        }
-        long get(long i) { return chunks.get((int) (i / CHUNK))[(int) (i & (CHUNK - 1))]; }
+    /** The graph cannot run partitioned; every worker raised it, the caller runs one device. */
+    public static final class NotPartitionable extends TitanException {
+        public NotPartitionable(String why) { super(why); }
     }
 
-    /** Shared by the scan's clones: every clone's rows are appended under its monitor. */
-    public static final class Collected {
-        final LongChunks vertices = new LongChunks();       // live (canonical) vertex ids
-        final LongChunks src = new LongChunks(), dst = new LongChunks();   // Titan ids, OUT entries
-        final IntChunks weight = new IntChunks();
-        final boolean weighted;
-        public Collected(boolean weighted) { this.weighted = weighted; }
+    // ------------------------------------------------------------------ the scanned rows
+    /** One work block of the scan, copied out of the collector. */
+    static final class Block {
+        final long[] keys, entryBegin, byteBegin, limitValuePos;
+        final ByteBuffer bytes;
+        Block(long[] keys, long[] entryBegin, long[] byteBegin, ByteBuffer bytes, long[] limitValuePos) {
+            this.keys = keys; this.entryBegin = entryBegin; this.byteBegin = byteBegin; this.bytes = bytes;
+            this.limitValuePos = limitValuePos;
+        }
+        /** rows + entries: the balance weight of the block */
+        long weight() { return keys.length + entryBegin[keys.length]; }
+    }
+
+    /** The scan's blocks in arrival order (a {@link CsrCollectingScanJob.BlockSink}). */
+    public static final class RowBlocks implements CsrCollectingScanJob.BlockSink {
+        final List<Block> blocks = new ArrayList<>();
+        long rows = 0;
+
+        @Override
+        public synchronized void accept(long[] keys, long[] entryBegin, long[] byteBegin, ByteBuffer bytes, int byteCount,
+                                        long[] limitValuePos) {
+            ByteBuffer b = ByteBuffer.allocateDirect(Math.max(byteCount, 1)).order(ByteOrder.BIG_ENDIAN);
+            ByteBuffer src = bytes.duplicate();
+            src.position(0);
+            src.limit(byteCount);
+            b.put(src);
+            b.flip();
+            blocks.add(new Block(keys, entryBegin, byteBegin, b, limitValuePos));
+            rows += keys.length;
+        }
+
+        public long rows() { return rows; }
+
+        /** Stages blocks [from, to) into one ctx with tgo_load_rows (a worker, or the single-
+         *  device fallback before tgo_finish_load). */
+        public void loadInto(long ctx, CsrCollectingScanJob.Handle h, int from, int to) {
+            for (int i = from; i < to; i++) {
+                Block b = blocks.get(i);
+                TgoNative.check(ctx, TgoNative.loadRows(ctx, b.keys, b.entryBegin, b.byteBegin, b.bytes, b.limitValuePos,
+                        h.edgeTypes, h.propertyKeys, h.scope, h.applyCap, h.labelIds, h.weightKey));
+            }
+        }
+
+        public void loadInto(long ctx, CsrCollectingScanJob.Handle h) { loadInto(ctx, h, 0, blocks.size()); }
     }
 
     /**
-     * The scan: the grounded VertexExists slice, then the user-edge slice [0x60, 0x80) without a
-     * limit (the partition load applies the scope's cap), as CsrCollectingScanJob asks.
+     * Contiguous block ranges for `world` workers balanced by rows + entries: range r ends at the
+     * first block boundary whose prefix weight reaches ceil(total * (r + 1) / world); returns
+     * world + 1 cut points (cut[r] .. cut[r + 1] is worker r's range, possibly empty).
      */
-    public static final class EdgeCollectingScanJob implements ScanJob {
-        private static final SliceQuery EDGE_SLICE = new SliceQuery(
-                IDHandler.getBounds(RelationCategory.EDGE, false)[0],
-                IDHandler.getBounds(RelationCategory.EDGE, false)[1]);
-        private final StandardTitanGraph graph;
-        private final IDManager idManager;
-        private final long weightKey;
-        private final Collected out;
-        private StandardTitanTx tx;
-        private LongChunks v, s, d;
-        private IntChunks w;
-
-        public EdgeCollectingScanJob(StandardTitanGraph graph, long weightKey, Collected out) {
-            this.graph = graph;
-            this.idManager = graph.getIDManager();
-            this.weightKey = weightKey;
-            this.out = out;
-        }
-
-        @Override
-        public List<SliceQuery> getQueries() {
-            List<SliceQuery> q = new ArrayList<>(2);
-            q.add(VertexJobConverter.VERTEX_EXISTS_QUERY);
-            q.add(EDGE_SLICE);
-            return q;
-        }
-
-        @Override
-        public Predicate<StaticBuffer> getKeyFilter() {
-            return buffer -> !IDManager.VertexIDType.Invisible.is(idManager.getKeyID(buffer));
-        }
-
-        @Override
-        public void workerIterationStart(Configuration jobConfiguration, Configuration graphConfiguration,
-                                         ScanMetrics metrics) {
-            tx = VertexJobConverter.startTransaction(graph);
-            v = new LongChunks();
-            s = new LongChunks();
-            d = new LongChunks();
-            w = new IntChunks();
-        }
-
-        @Override
-        public void process(StaticBuffer key, Map<SliceQuery, EntryList> slices, ScanMetrics metrics) {
-            long vid = idManager.getKeyID(key);
-            final boolean cut = idManager.isPartitionedVertex(vid);
-            EntryList exists = slices.get(VertexJobConverter.VERTEX_EXISTS_QUERY);
-            if (!cut && (exists == null || exists.isEmpty())) return;      // a ghost (VertexJobConverter.java:132)
-            if (cut) vid = idManager.getCanonicalVertexId(vid);
-            v.add(vid);
-            EntryList edges = slices.get(EDGE_SLICE);
-            if (edges == null) return;
-            for (Entry e : edges) {
-                RelationCache rc = tx.getEdgeSerializer().parseRelation(e, weightKey == 0, tx);
-                if (rc.direction != Direction.OUT) continue;               // each edge once, from its tail
-                long other = rc.getOtherVertexId();
-                if (idManager.isPartitionedVertex(other)) other = idManager.getCanonicalVertexId(other);
-                s.add(vid);
-                d.add(other);
-                if (weightKey != 0) {
-                    Object x = rc.hasProperties() ? rc.get(weightKey) : null;
-                    // ShortestDistanceVertexProgram.java:53 reads edge.<Integer>value(weight)
-                    w.add(x instanceof Integer ? (Integer) x : MISSING_WEIGHT);
-                }
+    static int[] blockRanges(long[] weights, int world) {
+        final int nb = weights.length;
+        long[] prefix = new long[nb + 1];
+        for (int i = 0; i < nb; i++) prefix[i + 1] = prefix[i] + weights[i];
+        final long total = prefix[nb];
+        int[] cut = new int[world + 1];
+        for (int r = 1; r < world; r++) {
+            final long target = (total * r + world - 1) / world;
+            int lo = 0, hi = nb;                 // the first boundary with prefix >= target
+            while (lo < hi) {
+                int mid = (lo + hi) >>> 1;
+                if (prefix[mid] < target) lo = mid + 1; else hi = mid;
             }
+            cut[r] = Math.max(cut[r - 1], Math.min(nb, lo));
         }
-
-        @Override
-        public void workerIterationEnd(ScanMetrics metrics) {
-            synchronized (out) {
-                for (long i = 0; i < v.size; i++) out.vertices.add(v.get(i));
-                for (long i = 0; i < s.size; i++) {
-                    out.src.add(s.get(i));
-                    out.dst.add(d.get(i));
-                    if (out.weighted) out.weight.add(w.get(i));
-                }
-            }
-            if (tx != null && tx.isOpen()) tx.rollback();
-        }
-
-        @Override
-        public EdgeCollectingScanJob clone() {
-            return new EdgeCollectingScanJob(graph, weightKey, out);
-        }
+        cut[world] = nb;
+        return cut;
     }
 
     // ------------------------------------------------------------------ partition + run
     /**
-     * Runs `program` over the collected graph on `devices` (one worker each).  Returns the live
-     * vertices' Titan ids (row order) and the program's results in that order.
+     * Runs `program` over the scanned rows on `devices` (one worker each).  Returns the live
+     * vertices' Titan ids (worker-major row order) and the program's results in that order.
      */
-    public static Object[] run(Collected c, Program program, int[] devices, int partitionBits, int hostThreads,
-                               long hardQueryLimit) throws Exception {
+    public static Object[] run(RowBlocks rows, CsrCollectingScanJob.Handle schema, Program program, int[] devices,
+                               int partitionBits, int hostThreads, long hardQueryLimit) throws Exception {
         final int world = devices.length;
-        // (2) global dense ids: the sorted live vertex ids
-        if (c.vertices.size > Integer.MAX_VALUE - 64) throw new TitanException("too many vertices for one job");
-        long[] ids = new long[(int) c.vertices.size];
-        for (int i = 0; i < ids.length; i++) ids[i] = c.vertices.get(i);
-        Arrays.sort(ids);
-        int n = 0;
-        for (int i = 0; i < ids.length; i++) if (i == 0 || ids[i] != ids[i - 1]) ids[n++] = ids[i];  // cut rows repeat
-        final long[] live = Arrays.copyOf(ids, n);
-        final long nLocal = ((n + world - 1L) / world + 63) / 64 * 64;
-        final long nGlobal = nLocal * world;
-        // every edge once, in dense ids; bucketed per worker by its endpoints' owners
-        final IntChunks[] bs = new IntChunks[world], bd = new IntChunks[world], bw = new IntChunks[world];
-        for (int r = 0; r < world; r++) { bs[r] = new IntChunks(); bd[r] = new IntChunks(); bw[r] = new IntChunks(); }
-        for (long i = 0; i < c.src.size; i++) {
-            int a = Arrays.binarySearch(live, c.src.get(i)), b = Arrays.binarySearch(live, c.dst.get(i));
-            if (a < 0 || b < 0) continue;                      // an endpoint never executes
-            int ra = (int) (a / nLocal), rb = (int) (b / nLocal);
-            int wt = c.weighted ? c.weight.get(i) : 0;
-            bs[ra].add(a); bd[ra].add(b); if (c.weighted) bw[ra].add(wt);
-            if (rb != ra) { bs[rb].add(a); bd[rb].add(b); if (c.weighted) bw[rb].add(wt); }
-        }
-        final int[] layoutGlobal = new int[(int) nGlobal];
-        final Object result = program.newResult(n);
+        long[] w = new long[rows.blocks.size()];
+        for (int i = 0; i < w.length; i++) w[i] = rows.blocks.get(i).weight();
+        final int[] cut = blockRanges(w, world);
         final byte[] rcclId = TgoNative.exchangeRcclId();
         if (rcclId == null) throw new TitanException("tgo_exchange_rccl_id failed");
         final CyclicBarrier phase = new CyclicBarrier(world);
+        final AtomicBoolean notPartitionable = new AtomicBoolean(false);
+        final String[] why = new String[1];
+        final long[] minWeight = new long[world];
+        final long[][] ownIds = new long[world][];
+        final Object[] owned = new Object[world];
         ExecutorService pool = Executors.newFixedThreadPool(world);
         try {
             List<Future<?>> fs = new ArrayList<>();
             for (int r = 0; r < world; r++) {
                 final int rank = r;
                 fs.add(pool.submit(() -> {
-                    worker(rank, world, devices[rank], nGlobal, nLocal, live, toArray(bs[rank]), toArray(bd[rank]),
-                            c.weighted ? toArray(bw[rank]) : null, layoutGlobal, rcclId, phase, program, result,
-                            partitionBits, hostThreads, hardQueryLimit);
+                    worker(rank, world, devices[rank], rows, cut[rank], cut[rank + 1], schema, rcclId, phase, program,
+                            minWeight, notPartitionable, why, ownIds, owned, partitionBits, hostThreads, hardQueryLimit);
                     return null;
                 }));
             }
@@ -252,36 +176,81 @@ public final class PartitionedRun {
         } finally {
             pool.shutdownNow();
         }
-        return new Object[]{live, result};
+        if (notPartitionable.get()) throw new NotPartitionable(why[0]);
+        long n = 0;
+        for (long[] ids : ownIds) n += ids.length;
+        if (n > Integer.MAX_VALUE - 8) throw new TitanException("more live vertices than one Java array holds");
+        long[] ids = new long[(int) n];
+        Object values = owned[0] instanceof double[] ? new double[(int) n] : new long[(int) n];
+        int at = 0;
+        for (int r = 0; r < world; r++) {
+            System.arraycopy(ownIds[r], 0, ids, at, ownIds[r].length);
+            System.arraycopy(owned[r], 0, values, at, ownIds[r].length);
+            at += ownIds[r].length;
+        }
+        return new Object[]{ids, values};
     }
 
-    static int[] toArray(IntChunks x) {
-        if (x.size > Integer.MAX_VALUE - 8) throw new TitanException("a partition holds more edges than a Java array");
-        int[] out = new int[(int) x.size];
-        for (int i = 0; i < out.length; i++) out[i] = x.get(i);
-        return out;
+    /** A phase barrier that gives up with the job (a peer that died never arrives). */
+    private static void await(CyclicBarrier phase) throws Exception {
+        phase.await(RUN_TIMEOUT_MINUTES, TimeUnit.MINUTES);
     }
 
-    private static void worker(int rank, int world, int device, long nGlobal, long nLocal, long[] live, int[] src, int[] dst,
-                               int[] weight, int[] layoutGlobal, byte[] rcclId, CyclicBarrier phase, Program program,
-                               Object result, int partitionBits, int hostThreads, long hardQueryLimit) throws Exception {
-        final long lo = rank * nLocal, hi = lo + nLocal;
+    private static void worker(int rank, int world, int device, RowBlocks rows, int from, int to,
+                               CsrCollectingScanJob.Handle schema, byte[] rcclId, CyclicBarrier phase, Program program,
+                               long[] minWeight, AtomicBoolean notPartitionable, String[] why, long[][] ownIds,
+                               Object[] owned, int partitionBits, int hostThreads, long hardQueryLimit) throws Exception {
         long ctx = 0, x = 0;
         try {
-            int[] lay = TgoNative.partLayout(src, dst, nGlobal, lo, hi, hostThreads);
-            if (lay == null) throw new TitanException("tgo_part_layout failed on worker " + rank);
-            System.arraycopy(lay, 0, layoutGlobal, (int) lo, lay.length);
-            phase.await();                                     // every slice in layoutGlobal
             ctx = TgoNative.create(device, partitionBits, hostThreads, hardQueryLimit);
             if (ctx == 0) throw new TitanException("no usable gfx950 device " + device);
-            TgoNative.check(ctx, TgoNative.loadPartition(ctx, nGlobal, lo, hi, src, dst, weight, program.scope(),
-                    program.applyCap(), layoutGlobal));
-            phase.await();                                     // every worker loaded: the communicator may form
+            // staging is local; a block that fails to stage is reported by the collective finish
+            RuntimeException staged = null;
+            try {
+                rows.loadInto(ctx, schema, from, to);
+            } catch (RuntimeException e) {
+                staged = e;
+            }
+            await(phase);                                      // every ctx exists: the communicator may form
             x = TgoNative.exchangeRcclCreate(world, rank, rcclId, device);
             if (x == 0) throw new TitanException("tgo_exchange_rccl_create failed on worker " + rank);
-            Object owned = TgoNative.checked(ctx, program.run(ctx, x, live));
-            int count = (int) Math.max(0, Math.min(hi, live.length) - lo);
-            if (count > 0) System.arraycopy(owned, 0, result, (int) lo, count);
+            long[] part = TgoNative.finishPartitionRows(ctx, x, true);
+            if (part == null) throw new TitanException("out of memory on worker " + rank);
+            // the load's status is agreed (every worker failed it, or none did)
+            if (part[0] != 0) {
+                if (part[0] == TgoNative.E_UNSUPPORTED) {        // vertex cuts / a non-Integer weight key
+                    why[0] = TgoNative.lastError(ctx);
+                    notPartitionable.set(true);
+                }
+                await(phase);                                    // every worker's reason is in
+                if (notPartitionable.get()) return;
+                if (staged != null) throw staged;
+                TgoNative.check(ctx, (int) part[0]);
+            }
+            final long live = part[1], slot = part[2], total = part[3];
+            // the program's own conditions, decided from agreed values: every worker alike
+            if (!program.partitions(total)) {
+                notPartitionable.set(true);
+                why[0] = "the program has no partitioned form for " + total + " vertices";
+                return;
+            }
+            if (program.needsNonNegativeWeights()) {
+                long[] wm = TgoNative.partWeightMin(ctx);
+                TgoNative.check(ctx, (int) wm[0]);
+                minWeight[rank] = wm[1];
+                await(phase);                                    // every worker's minimum is in
+                for (long m : minWeight)
+                    if (m < 0) {
+                        notPartitionable.set(true);
+                        why[0] = "a negative weight: delta-stepping needs non-negative weights";
+                        return;
+                    }
+            }
+            long[] allIds = TgoNative.vertexIds(ctx);
+            long[] ids = java.util.Arrays.copyOf(allIds, (int) live);
+            Object res = TgoNative.checked(ctx, program.run(ctx, x, ids, rank * slot));
+            ownIds[rank] = ids;
+            owned[rank] = res;
         } catch (Exception e) {
             phase.reset();                                     // the peers waiting on a phase fail too
             throw e;

@@ -101,6 +101,21 @@ public final class TgoNative {
     public static native int loadPartition(long ctx, long nGlobal, long lo, long hi, int[] src, int[] dst, int[] weight,
                                            int scope, boolean applyCap, int[] layoutGlobal);
 
+    /**
+     * tgo_finish_partition_rows (collective: every worker calls it after staging ITS rows with
+     * {@link #loadRows}): {status, live rows here, slot size S, live rows of every worker}.  The
+     * worker's results are the first "live" entries of the partSsspRun / partPageRankRun outputs,
+     * whose ids are the first "live" of vertexIds; rank r's global ids are r * S + i.
+     * status TGO_E_UNSUPPORTED: the graph has vertex cuts or a non-Integer weight key.
+     */
+    public static native long[] finishPartitionRows(long ctx, long exchange, boolean layout);
+
+    /** tgo_part_weight_min: {status, smallest weight of this worker's load (0 unweighted)}. */
+    public static native long[] partWeightMin(long ctx);
+
+    /** tgo_status values the Java layer branches on. */
+    public static final int E_INVALID = -1, E_UNSUPPORTED = -7;
+
     /** tgo_exchange_rccl_id: the 128-byte RCCL unique id (made once, shared by every worker). */
     public static native byte[] exchangeRcclId();
 

@@ -95,6 +95,12 @@ jlongArray JFN(partSsspRun)(JNIEnv*, jclass, jlong, jlong, jlong, jlong);
 jdoubleArray JFN(partPageRankRun)(JNIEnv*, jclass, jlong, jlong, jdouble, jlong, jint, jint);
 jlongArray JFN(partMsbfsRun)(JNIEnv*, jclass, jlong, jlong, jlongArray, jint, jdouble, jlong);
 jlongArray JFN(partMsLevels)(JNIEnv*, jclass, jlong, jint);
+jint JFN(loadRows)(JNIEnv*, jclass, jlong, jlongArray, jlongArray, jlongArray, jobject, jlongArray, jlongArray, jlongArray,
+                   jint, jboolean, jlongArray, jlong);
+jlongArray JFN(finishPartitionRows)(JNIEnv*, jclass, jlong, jlong, jboolean);
+jlongArray JFN(partWeightMin)(JNIEnv*, jclass, jlong);
+#include "tgo_synth.h"
+static void* direct_address(JNIEnv* env, jobject b) { (void)env; return ((FakeArr*)(void*)b)->data; }
 
 static int failures = 0;
 static void check(const char* name, int ok) {
@@ -153,6 +159,88 @@ static void partition_cases(JNIEnv* env) {
     check("partBfsRun without an exchange", JFN(partBfsRun)(env, NULL, 1, 0, 0, 4, 15.0, 18.0) == NULL);
     check("partMsbfsRun rejects 65 seeds", JFN(partMsbfsRun)(env, NULL, 1, 1, ARR(&seeds65), 4, 12.0, 0) == NULL);
     check("partMsbfsRun rejects no seeds", JFN(partMsbfsRun)(env, NULL, 1, 1, ARR(&seeds0), 4, 12.0, 0) == NULL);
+    /* the rows partition reports its status instead of throwing (E_UNSUPPORTED -> one device) */
+    jlongArray st = JFN(finishPartitionRows)(env, NULL, 0, 0, 1);
+    check("finishPartitionRows without a ctx: {E_INVALID, 0, 0, 0}",
+          st != NULL && ((FakeArr*)(void*)st)->len == 4 && ((jlong*)((FakeArr*)(void*)st)->data)[0] == TGO_E_INVALID);
+    jlongArray wm = JFN(partWeightMin)(env, NULL, 0);
+    check("partWeightMin without a ctx: {E_INVALID, 0}",
+          wm != NULL && ((FakeArr*)(void*)wm)->len == 2 && ((jlong*)((FakeArr*)(void*)wm)->data)[0] == TGO_E_INVALID);
+}
+
+/* world 1 on a GPU, the Java multi-GPU ROW path (PartitionedRun: loadRows blocks + the collective
+ * finishPartitionRows): synthetic edgestore rows of the test graph at a hard limit of 3 (every
+ * row is cut: a vertex has 2 OUT + 2 IN user-edge entries), so the push rows come from the pull
+ * entries sent through the exchange; SSSP (unit weights) and PageRank against tgo_load_rows. */
+static void gpu_rows_case(JNIEnv* env) {
+    const int m = graph_edges();
+    const int64_t label = (1 << 6) | 21;
+    int64_t sz[3];
+    if (tgo_synth_rows(GN, m, (const int32_t*)g_src, (const int32_t*)g_dst, NULL, label, 5, 2, sz, NULL, NULL, NULL, NULL,
+                       NULL) != TGO_OK) { check("synth rows sizes", 0); return; }
+    static jlong keys[GN], eb[GN + 1], bb[GN + 1];
+    jlong* lv = (jlong*)calloc((size_t)sz[1] + 1, 8);
+    uint8_t* bytes = (uint8_t*)calloc((size_t)sz[2] + 1, 1);
+    int ok = tgo_synth_rows(GN, m, (const int32_t*)g_src, (const int32_t*)g_dst, NULL, label, 5, 2, sz, (int64_t*)keys,
+                            (int64_t*)eb, (int64_t*)bb, bytes, (int64_t*)lv) == TGO_OK;
+    check("synth rows", ok);
+    jlong types_d[5] = {label, TGO_MULTI, 0, 0, 0}, none_d[1] = {0};
+    FakeArr fk = {(jsize)sz[0], keys}, feb = {(jsize)sz[0] + 1, eb}, fbb = {(jsize)sz[0] + 1, bb}, fby = {(jsize)sz[2], bytes};
+    FakeArr flv = {(jsize)sz[1], lv}, types = {5, types_d}, none = {0, none_d};
+    jlong h = JFN(create)(env, NULL, 0, 5, 4, 3);
+    jint rc = ok && h ? JFN(loadRows)(env, NULL, h, ARR(&fk), ARR(&feb), ARR(&fbb), (jobject)(void*)&fby, ARR(&flv),
+                                      ARR(&types), ARR(&none), TGO_SCOPE_IN_E, 1, ARR(&none), 0) : TGO_E_INVALID;
+    check("loadRows (a worker's block)", rc == TGO_OK);
+    jbyteArray id = JFN(exchangeRcclId)(env, NULL);
+    jlong x = (rc == TGO_OK && id) ? JFN(exchangeRcclCreate)(env, NULL, 1, 0, id, 0) : 0;
+    jlongArray part = x ? JFN(finishPartitionRows)(env, NULL, h, x, 1) : NULL;
+    const jlong* p = part ? (const jlong*)((FakeArr*)(void*)part)->data : NULL;
+    check("finishPartitionRows (world 1): {0, 256, 256, 256}", p && p[0] == 0 && p[1] == GN && p[2] == GN && p[3] == GN);
+    tgo_options o;
+    tgo_default_options(&o);
+    o.hard_query_limit = 3;
+    tgo_ctx* one = NULL;
+    tgo_rows r = {sz[0], (const int64_t*)keys, (const int64_t*)eb, (const int64_t*)bb, bytes, (const int64_t*)lv};
+    tgo_edge_type et;
+    memset(&et, 0, sizeof et);
+    et.type_id = label;
+    et.multiplicity = TGO_MULTI;
+    tgo_schema sc = {1, &et, 0, NULL};
+    tgo_load_opts lo;
+    memset(&lo, 0, sizeof lo);
+    lo.scope = TGO_SCOPE_IN_E;
+    lo.apply_cap = 1;
+    int ref_ok = tgo_create(&o, &one) == TGO_OK && tgo_load_rows(one, &r, &sc, &lo) == TGO_OK && tgo_finish_load(one) == TGO_OK;
+    tgo_stats s1;
+    ref_ok = ref_ok && tgo_stats_get(one, &s1) == TGO_OK && s1.truncated_results == GN;
+    check("one-GPU tgo_load_rows reference (every row cut)", ref_ok);
+    if (p && p[0] == 0 && ref_ok) {
+        static int64_t ref[GN];
+        tgo_sssp_args sa;
+        memset(&sa, 0, sizeof sa);
+        sa.seed = 5; sa.seed_is_dense = 1; sa.max_depth = GN; sa.scope = TGO_SCOPE_IN_E; sa.mode = TGO_SSSP_DELTA;
+        jlongArray d = JFN(partSsspRun)(env, NULL, h, x, 5, 0);
+        int same = d != NULL && tgo_sssp(one, &sa, ref) == TGO_OK;
+        for (int v = 0; same && v < GN; ++v) same = ((jlong*)((FakeArr*)(void*)d)->data)[v] == ref[v];
+        check("rows partition: partSsspRun == tgo_sssp (cut rows, pushed pull entries)", same);
+        tgo_pr_args pa;
+        memset(&pa, 0, sizeof pa);
+        pa.alpha = 0.85; pa.vertex_count = GN; pa.max_iterations = 9;
+        static double pref[GN];
+        jdoubleArray pp = JFN(partPageRankRun)(env, NULL, h, x, 0.85, GN, 9, 1);
+        int close = pp != NULL && tgo_pagerank(one, &pa, pref) == TGO_OK;
+        double l1 = 0;
+        for (int v = 0; close && v < GN; ++v) l1 += fabs(((jdouble*)((FakeArr*)(void*)pp)->data)[v] - pref[v]);
+        check("rows partition: partPageRankRun within 1e-12 L1 of tgo_pagerank", close && l1 <= 1e-12);
+        jlongArray wm = JFN(partWeightMin)(env, NULL, h);
+        check("partWeightMin (unweighted: {0, 0})", wm && ((jlong*)((FakeArr*)(void*)wm)->data)[0] == 0 &&
+                                                      ((jlong*)((FakeArr*)(void*)wm)->data)[1] == 0);
+    }
+    if (x) JFN(exchangeDestroy)(env, NULL, x);
+    if (h) JFN(destroy)(env, NULL, h);
+    tgo_destroy(one);
+    free(lv);
+    free(bytes);
 }
 
 /* world 1 on a GPU: the Java multi-GPU calls through the shim against the one-GPU engine */
@@ -270,6 +358,7 @@ int main(int argc, char** argv) {
     table.ReleaseIntArrayElements = rel_ints;
     table.ReleaseLongArrayElements = rel_longs;
     table.GetLongArrayRegion = long_region;
+    table.GetDirectBufferAddress = direct_address;
     JNIEnv envp = &table;
     JNIEnv* env = &envp;
     /* 3 rows: 0 -> 1, 1 -> 2 (OUT); the IN lists their transposes */
@@ -295,6 +384,9 @@ int main(int argc, char** argv) {
     expect("ids length disagrees with the offsets", CALL(&ids2, &oo, &oi, NULL, &io, &ii, NULL, 0), TGO_E_INVALID, 0);
     expect("empty offset array", CALL(&ids, &empty_off, &oi, NULL, &empty_off, &ii, NULL, 0), TGO_E_INVALID, 0);
     partition_cases(env);
-    if (argc > 1 && strcmp(argv[1], "gpu") == 0) gpu_cases(env);
+    if (argc > 1 && strcmp(argv[1], "gpu") == 0) {
+        gpu_cases(env);
+        gpu_rows_case(env);
+    }
     return failures;
 }

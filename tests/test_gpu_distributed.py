@@ -598,7 +598,7 @@ class RowRanks:
     """tgo_load_partition_rows: each thread rank loads ITS contiguous row range of a scan
     (balanced_row_ranges) over an in-process exchange group; backends over the slot ids."""
 
-    def __init__(self, world, rows, sd, scope, limit, weight_key=0, layout=True, labels=()):
+    def __init__(self, world, rows, sd, scope, limit, weight_key=0, layout=True, labels=(), batch_rows=None):
         from titan_amd import Schema
         from titan_amd.distributed import NativeExchange, balanced_row_ranges
         self.world = world
@@ -609,14 +609,16 @@ class RowRanks:
         def load(rank, comm):
             torch.cuda.set_stream(self.streams[rank])
             eng = Engine(stream=self.streams[rank].cuda_stream, hard_query_limit=limit)
-            live, S = eng.load_partition_rows(self.xs[rank], rows.slice(*self.ranges[rank]), Schema.from_dict(sd), scope,
-                                              weight_key=weight_key, layout=layout, labels=labels)
-            return eng, live, S
+            live, S, total = eng.load_partition_rows(self.xs[rank], rows.slice(*self.ranges[rank]), Schema.from_dict(sd),
+                                                     scope, weight_key=weight_key, layout=layout, labels=labels,
+                                                     batch_rows=batch_rows)
+            return eng, live, S, total
         res = InProcessGroup(world).run(load)
         self.S = res[0][2]
         assert all(r[2] == self.S for r in res)
         self.n_global = world * self.S
         self.live = [r[1] for r in res]
+        assert all(r[3] == sum(self.live) for r in res)
         self.engines = [r[0] for r in res]
         self.backends = []
         for r, e in enumerate(self.engines):
@@ -655,7 +657,7 @@ def test_partition_rows_match_one_gpu_rows(world, monkeypatch):
         one = Engine(hard_query_limit=limit).load_rows(rows, Schema.from_dict(sd), scope, weight_key=wkey)
         o = fr.OracleGraph.from_rows(rows, osch, scope, hard_limit=limit, weight_key=wkey)
         ids1 = one.vertex_ids()
-        rr = RowRanks(world, rows, sd, scope, limit, weight_key=wkey)
+        rr = RowRanks(world, rows, sd, scope, limit, weight_key=wkey, batch_rows=64 if world % 2 else None)
         assert sum(rr.live) == len(ids1) and sorted(np.concatenate(rr.ids)) == sorted(ids1)
         assert sum(be.e.stats()["truncated_results"] for be in rr.backends) == one.stats()["truncated_results"] \
             == o.stats.truncated_results

@@ -78,7 +78,7 @@ def test_load_csr_validates_array_lengths_before_pinning(tmp_path):
     exe = _build_harness(tmp_path)
     run = subprocess.run([exe], capture_output=True, text=True, timeout=60)
     assert run.returncode == 0, run.stdout + run.stderr
-    assert run.stdout.count("ok  ") == 25, run.stdout
+    assert run.stdout.count("ok  ") == 27, run.stdout
 
 
 def _build_harness(tmp_path):
@@ -101,8 +101,11 @@ def test_java_multi_gpu_natives_world1(tmp_path):
     loadPartition / exchangeRcclId / exchangeRcclCreate / partSsspRun / partPageRankRun /
     partBfsRun / partMsbfsRun / partMsLevels — what PartitionedRun calls per worker) run through
     the JNI shim against the real library at world 1 over RCCL, and equal the one-GPU engine on
-    the same graph (SSSP and BFS bit-exact, PageRank in both exchange modes within 1e-12 L1)."""
+    the same graph (SSSP and BFS bit-exact, PageRank in both exchange modes within 1e-12 L1); and
+    (round 6) the row path PartitionedRun now takes — loadRows blocks, the collective
+    finishPartitionRows, partSsspRun / partPageRankRun / partWeightMin — on synthetic edgestore
+    rows that are ALL cut at a hard limit of 3, against tgo_load_rows on one GPU."""
     exe = _build_harness(tmp_path)
     run = subprocess.run([exe, "gpu"], capture_output=True, text=True, timeout=120)
     assert run.returncode == 0, run.stdout + run.stderr
-    assert "FAIL" not in run.stdout and run.stdout.count("ok  ") == 25 + 13, run.stdout
+    assert "FAIL" not in run.stdout and run.stdout.count("ok  ") == 27 + 13 + 7, run.stdout

@@ -158,7 +158,7 @@ EXPORTS = [
     # titan_gpu_olap_part.h (1-D vertex-partitioned multi-GPU)
     "tgo_load_partition", "tgo_part_layout", "tgo_load_partition_layout", "tgo_part_bfs_begin", "tgo_part_bfs_td", "tgo_part_bfs_claim", "tgo_part_bfs_bu",
     "tgo_part_bfs_end", "tgo_part_pr_begin", "tgo_part_pr_step", "tgo_part_pr_end", "tgo_part_pr_exact_check", "tgo_part_pr_plain",
-    "tgo_part_weight_min", "tgo_load_partition_rows",
+    "tgo_part_weight_min", "tgo_load_partition_rows", "tgo_finish_partition_rows",
     "tgo_rmat_partition",
     "tgo_part_active_rows", "tgo_part_pr_blocked", "tgo_part_device_counts", "tgo_part_set_local_qlen", "tgo_part_ms_pack_dev", "tgo_part_pr_step_cold", "tgo_part_pr_step_hot",
     "tgo_part_ms_begin", "tgo_part_ms_pull", "tgo_part_ms_push", "tgo_part_ms_settle", "tgo_part_ms_end",
@@ -267,6 +267,7 @@ def load() -> C.CDLL:
         "tgo_part_pr_plain": (C.c_int, [vp, C.c_int32]),
         "tgo_part_weight_min": (C.c_int, [vp, _i64p]),
         "tgo_load_partition_rows": (C.c_int, [vp, vp, P(Rows), P(Schema), P(LoadOpts), C.c_int32, _i64p]),
+        "tgo_finish_partition_rows": (C.c_int, [vp, vp, C.c_int32, _i64p]),
         "tgo_part_active_rows": (C.c_int, [vp, _i64p]),
         "tgo_part_device_counts": (C.c_int, [vp, vp]),
         "tgo_part_set_local_qlen": (C.c_int, [vp, C.c_int64]),

@@ -3541,33 +3541,36 @@ int part_upload(tgo_ctx* ctx, HostGraph& h, int64_t n_global, int64_t lo) {
     ctx->g.n_global = n_global;
     return TGO_OK;
 }
-// tgo_load_partition_rows: this rank's rows decoded on the host with the one-GPU rules (the cut
-// in column order per row, typed scopes, key filter, ghosts: decode_rows).  Vertex cuts fold on
-// one GPU only; the partitioned programs read Integer weights.
-int part_rows_decode(tgo_ctx* ctx, const tgo_rows* rows, const tgo_schema* schema, const tgo_load_opts* opts,
-                     RowStaging& st, std::string& err) {
+// tgo_finish_partition_rows: the rows this rank staged with tgo_load_rows, decoded with the
+// one-GPU rules (device decoder, or the host one under TGO_HOST_DECODE: key filter, ghosts,
+// typed scopes, the cut in column order per row) into host vectors.  Vertex cuts fold on one GPU
+// only; the partitioned programs read Integer weights.
+int part_rows_take(tgo_ctx* ctx, RowStaging& st, std::string& err) {
     (void)hipSetDevice(ctx->opts.device);
     ctx->res_kind = -1;
-    if (rows->nrows < 0 || (rows->nrows > 0 && (!rows->row_keys || !rows->row_entry_begin || !rows->row_byte_begin ||
-                                                !rows->entry_bytes || !rows->entry_limit_valpos))) {
-        err = "incomplete tgo_rows";
-        return TGO_E_INVALID;
+    if (!ctx->staging.active) {          // no rows staged here: an empty range (the caller's scope agreed later)
+        st = RowStaging();
+        st.row_begin.push_back(0);
+        return TGO_OK;
     }
-    if (opts->scope < 0 || opts->scope > 2) { err = "invalid scope"; return TGO_E_INVALID; }
-    st = RowStaging();
-    if (int rc = decode_rows(st, rows, schema, opts, ctx->opts.partition_bits, ctx->opts.hard_query_limit,
-                             threads_of(ctx), err))
-        return rc;
+    int rc = decode_staged_raw(ctx->staging, ctx->opts.partition_bits, ctx->opts.hard_query_limit, ctx->dec, ctx->stream,
+                               err, false);
+    ctx->dec.release();
+    if (!rc) rc = staging_entries_to_host(ctx->staging, ctx->stream, err);
+    st = std::move(ctx->staging);
+    ctx->staging = RowStaging();
+    if (rc) return rc;
     if (st.n_rep > 0 || std::any_of(st.vid.begin(), st.vid.end(), [](int64_t v) { return (v & 7) == 2; })) {
         err = "vertex cuts fold into their canonical vertex on a one-GPU load (VertexProgramScanJob.java:76-92)";
         return TGO_E_UNSUPPORTED;
     }
-    if (opts->weight_key != 0 && st.plan.weight_dt != 0 && st.plan.weight_dt != TGO_DT_INTEGER) {
+    if (st.opts.weight_key != 0 && st.plan.weight_dt != 0 && st.plan.weight_dt != TGO_DT_INTEGER) {
         err = "the partitioned programs read edge.<Integer>value(weight) (ShortestDistanceVertexProgram.java:53)";
         return TGO_E_UNSUPPORTED;
     }
     return TGO_OK;
 }
+void part_drop_staging(tgo_ctx* ctx) { ctx->staging = RowStaging(); ctx->dec.release(); }
 int part_threads(const tgo_ctx* ctx) { return threads_of(ctx); }
 void part_set_live(tgo_ctx* ctx, int64_t live) { ctx->st.num_vertices = live; }
 int part_fail(tgo_ctx* ctx, int code, const std::string& msg) { return fail(ctx, code, msg); }

@@ -335,8 +335,8 @@ int part_out_list(tgo_ctx* ctx, const int32_t** adj, int64_t* nnz);
 bool ms_ghost_of(const tgo_ctx* ctx);
 int part_pr_layout_of(tgo_ctx* ctx, int32_t* world, int64_t* hot, int64_t* span);
 int part_upload(tgo_ctx* ctx, HostGraph& h, int64_t n_global, int64_t lo);
-int part_rows_decode(tgo_ctx* ctx, const tgo_rows* rows, const tgo_schema* schema, const tgo_load_opts* opts,
-                     RowStaging& st, std::string& err);
+int part_rows_take(tgo_ctx* ctx, RowStaging& st, std::string& err);
+void part_drop_staging(tgo_ctx* ctx);
 int part_threads(const tgo_ctx* ctx);
 void part_set_live(tgo_ctx* ctx, int64_t live);
 template <class T>
@@ -997,17 +997,15 @@ struct DevTmp {                 // a device temporary of the load (the ctx holds
 };
 }  // namespace
 
-extern "C" int tgo_load_partition_rows(tgo_ctx* ctx, tgo_exchange* x, const tgo_rows* rows, const tgo_schema* schema,
-                                       const tgo_load_opts* opts, int32_t layout, int64_t* part_out) {
-    if (!ctx) return TGO_E_INVALID;
-    if (!x || !rows || !schema || !opts || !part_out || x->world < 1 || x->rank < 0 || x->rank >= x->world)
-        return part_fail(ctx, TGO_E_INVALID, "tgo_load_partition_rows: bad arguments");
-    const auto t0 = std::chrono::steady_clock::now();
+// local_rc: a failure this rank met before the collective part (its staging is dropped); the
+// ranks still agree on it, so every rank returns an error and none waits in an exchange.
+static int finish_partition_rows(tgo_ctx* ctx, tgo_exchange* x, int32_t layout, int64_t* part_out, int local_rc,
+                                 const std::string& local_err) {
     const int W = x->world, R = x->rank;
     hipStream_t st = part_stream(ctx);
-    std::string err;
+    std::string err = local_err;
     auto xerr = [&](int code) { return part_fail(ctx, code, "exchange: " + x->err); };
-    auto hip = [&](const char* what) { x->abort(); return part_fail(ctx, TGO_E_HIP, std::string("tgo_load_partition_rows: ") + what); };
+    auto hip = [&](const char* what) { x->abort(); return part_fail(ctx, TGO_E_HIP, std::string("tgo_finish_partition_rows: ") + what); };
     DevTmp red;
     if (red.alloc(8 * sizeof(int64_t)) != hipSuccess) return hip("scratch");
     // element-wise reduction of k host words over the ranks
@@ -1021,15 +1019,26 @@ extern "C" int tgo_load_partition_rows(tgo_ctx* ctx, tgo_exchange* x, const tgo_
     };
     // 1. decode, then agree on failure and on the slot size
     RowStaging stg;
-    const int drc = part_rows_decode(ctx, rows, schema, opts, stg, err);
+    int drc = local_rc;
+    if (drc) part_drop_staging(ctx);
+    else drc = part_rows_take(ctx, stg, err);
     const int64_t count = drc ? 0 : static_cast<int64_t>(stg.vid.size());
-    int64_t v1[2] = {drc ? 1 : 0, count};
-    if (int rc = reduce(v1, 2, tgo_exchange::kRedMax)) return rc;
-    if (drc) return part_fail(ctx, drc, "tgo_load_partition_rows: " + err);
-    if (v1[0]) return part_fail(ctx, TGO_E_INVALID, "tgo_load_partition_rows: another rank failed to decode its rows");
+    // a rank without staged rows (an empty range) takes the scope / weightedness of the others
+    const bool staged = !drc && stg.active;
+    int64_t v1[4] = {drc ? 1 : 0, count, staged ? stg.opts.scope + 1 : 0, staged && stg.opts.weight_key != 0 ? 1 : 0};
+    const int64_t own_scope = v1[2], own_weighted = v1[3];
+    if (int rc = reduce(v1, 4, tgo_exchange::kRedMax)) return rc;
+    if (drc) return part_fail(ctx, drc, "tgo_finish_partition_rows: " + err);
+    if (v1[0]) return part_fail(ctx, TGO_E_INVALID, "tgo_finish_partition_rows: another rank failed to decode its rows");
+    if (!staged) {
+        stg.opts.scope = static_cast<int32_t>(std::max<int64_t>(0, v1[2] - 1));
+        stg.opts.weight_key = v1[3];
+    }
+    // ranks that disagree on the scope or the weight key fail below (agreed with the assembly)
+    int mismatch = staged && (own_scope != v1[2] || own_weighted != v1[3]);
     const int64_t S = std::max<int64_t>(64, (v1[1] + 63) / 64 * 64), lo = static_cast<int64_t>(R) * S;
     const int64_t n_global = static_cast<int64_t>(W) * S;
-    if (n_global >= INT32_MAX) return part_fail(ctx, TGO_E_UNSUPPORTED, "tgo_load_partition_rows: more than 2^31 - 1 slots");
+    if (n_global >= INT32_MAX) return part_fail(ctx, TGO_E_UNSUPPORTED, "tgo_finish_partition_rows: more than 2^31 - 1 slots");
     // 2. the global id map: every rank's live ids at their slots
     std::vector<int64_t> slot_vid(static_cast<size_t>(n_global));
     {
@@ -1048,13 +1057,19 @@ extern "C" int tgo_load_partition_rows(tgo_ctx* ctx, tgo_exchange* x, const tgo_
     HostGraph h;
     const int threads = part_threads(ctx);
     int arc = assemble_partition_rows(stg, slot_vid, S, R, h, threads, err);
+    if (!arc && mismatch) {
+        err = "the ranks staged rows with different scopes or weight keys";
+        arc = TGO_E_INVALID;
+    }
     std::vector<int64_t>().swap(slot_vid);
-    // 3. the degree-grouped layout of every rank's slots
-    if (!arc && layout) {
+    // 3. the degree-grouped layout of every rank's slots (a rank whose assembly failed still
+    //    takes part in the collective; the failure is agreed in step 4)
+    if (layout) {
         DevTmp buf;
         if (buf.alloc(n_global * sizeof(int32_t)) != hipSuccess) return hip("layout buffer");
         std::vector<int32_t> lay(static_cast<size_t>(n_global));
-        partition_rows_layout(h, lo, lay.data() + lo);
+        if (arc) for (int64_t i = 0; i < S; ++i) lay[lo + i] = static_cast<int32_t>(lo + i);
+        else partition_rows_layout(h, lo, lay.data() + lo);
         int32_t* b = static_cast<int32_t*>(buf.p);
         if (hipMemcpyAsync(b + lo, lay.data() + lo, S * sizeof(int32_t), hipMemcpyHostToDevice, st) != hipSuccess)
             return hip("layout upload");
@@ -1062,15 +1077,15 @@ extern "C" int tgo_load_partition_rows(tgo_ctx* ctx, tgo_exchange* x, const tgo_
         if (hipMemcpyAsync(lay.data(), b, n_global * sizeof(int32_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
             hipStreamSynchronize(st) != hipSuccess)
             return hip("layout read");
-        arc = apply_partition_layout(h, lo, lay.data(), threads, err);
+        if (!arc) arc = apply_partition_layout(h, lo, lay.data(), threads, err);
     }
     // 4. cut rows anywhere: the push view from every rank's pull entries (and a last agreement
     //    on failure before the graph replaces the ctx's)
-    int64_t v4[2] = {arc ? 1 : 0, h.truncated};
-    if (int rc = reduce(v4, 2, tgo_exchange::kRedSum)) return rc;
-    if (arc) return part_fail(ctx, arc, "tgo_load_partition_rows: " + err);
-    if (v4[0]) return part_fail(ctx, TGO_E_INVALID, "tgo_load_partition_rows: another rank failed to assemble its rows");
-    if (v4[1] > 0 && opts->scope != TGO_SCOPE_BOTH_E) {
+    int64_t v4[3] = {arc ? 1 : 0, h.truncated, count};
+    if (int rc = reduce(v4, 3, tgo_exchange::kRedSum)) return rc;
+    if (arc) return part_fail(ctx, arc, "tgo_finish_partition_rows: " + err);
+    if (v4[0]) return part_fail(ctx, TGO_E_INVALID, "tgo_finish_partition_rows: another rank failed to assemble its rows");
+    if (v4[1] > 0 && h.scope != TGO_SCOPE_BOTH_E) {
         std::vector<int64_t> cnt, pairs;
         partition_pull_pairs(h, lo, S, W, cnt, pairs);
         DevTmp dc, rc_, sbuf, rbuf;
@@ -1100,6 +1115,22 @@ extern "C" int tgo_load_partition_rows(tgo_ctx* ctx, tgo_exchange* x, const tgo_
     part_set_live(ctx, count);
     part_out[0] = count;
     part_out[1] = S;
-    (void)t0;
+    part_out[2] = v4[2];
     return TGO_OK;
+}
+
+extern "C" int tgo_finish_partition_rows(tgo_ctx* ctx, tgo_exchange* x, int32_t layout, int64_t* part) {
+    if (!ctx) return TGO_E_INVALID;
+    if (!x || !part || x->world < 1 || x->rank < 0 || x->rank >= x->world)
+        return part_fail(ctx, TGO_E_INVALID, "tgo_finish_partition_rows: bad arguments");
+    return finish_partition_rows(ctx, x, layout, part, TGO_OK, std::string());
+}
+
+extern "C" int tgo_load_partition_rows(tgo_ctx* ctx, tgo_exchange* x, const tgo_rows* rows, const tgo_schema* schema,
+                                       const tgo_load_opts* opts, int32_t layout, int64_t* part) {
+    if (!ctx) return TGO_E_INVALID;
+    if (!x || !part || x->world < 1 || x->rank < 0 || x->rank >= x->world)
+        return part_fail(ctx, TGO_E_INVALID, "tgo_load_partition_rows: bad arguments");
+    const int rc = tgo_load_rows(ctx, rows, schema, opts);
+    return finish_partition_rows(ctx, x, layout, part, rc, rc ? std::string(tgo_last_error(ctx)) : std::string());
 }

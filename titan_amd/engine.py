@@ -110,6 +110,20 @@ class Engine:
         self.n = self.lib.tgo_num_vertices(self.ctx)
         return self
 
+    @staticmethod
+    def _row_block(rows, r0, r1):
+        """Rows [r0, r1) as a tgo_rows (offsets rebased) and the arrays it points into."""
+        eb = rows.entry_begin[r0:r1 + 1]
+        bb = rows.byte_begin[r0:r1 + 1]
+        keys = np.ascontiguousarray(rows.keys[r0:r1], dtype=np.int64)
+        eb0 = np.ascontiguousarray(eb - eb[0], dtype=np.int64)
+        bb0 = np.ascontiguousarray(bb - bb[0], dtype=np.int64)
+        data = np.ascontiguousarray(rows.data[bb[0]:max(bb[-1], bb[0] + 1)], dtype=np.uint8)
+        lv = np.ascontiguousarray(rows.limit_valpos[eb[0]:max(eb[-1], eb[0] + 1)], dtype=np.int64)
+        cr = L.Rows(r1 - r0, L.ptr(keys, C.c_int64), L.ptr(eb0, C.c_int64), L.ptr(bb0, C.c_int64),
+                    L.ptr(data, C.c_uint8), L.ptr(lv, C.c_int64))
+        return cr, (keys, eb0, bb0, data, lv)
+
     def append_rows(self, rows, schema: Schema, scope, apply_cap=True, labels=(), weight_key=0):
         """One work block of scanned rows (tgo_load_rows without finishing the load)."""
         opts, keep = self._opts(scope, apply_cap, labels, weight_key)
@@ -189,12 +203,29 @@ class Engine:
         return self
 
     def load_partition_rows(self, exchange, rows, schema: Schema, scope, apply_cap=True, labels=(), weight_key=0,
-                            layout=True):
+                            layout=True, batch_rows=None):
         """This rank's rows of a row-range partition of the scan (tgo_load_partition_rows; a
         collective over `exchange`, a distributed.NativeExchange): the one-GPU decode and cut per
-        row, global slot ids.  Returns (live rows here, slot size S): n_global = world * S,
-        lo = rank * S; results are the first `live` entries of the rank's outputs, whose ids are
-        vertex_ids()[:live]."""
+        row, global slot ids.  Returns (live rows here, slot size S, live rows of every rank):
+        n_global = world * S, lo = rank * S; results are the first `live` entries of the rank's
+        outputs, whose ids are vertex_ids()[:live].  batch_rows: stage the rows in work blocks
+        (tgo_load_rows each) and finish with tgo_finish_partition_rows, as a scan hands them over."""
+        if batch_rows:
+            opts, keep = self._opts(scope, apply_cap, labels, weight_key)
+            rc = L.TGO_OK
+            for r0 in range(0, rows.nrows, batch_rows):
+                cr, hold = self._row_block(rows, r0, min(rows.nrows, r0 + batch_rows))
+                rc = self.lib.tgo_load_rows(self.ctx, C.byref(cr), C.byref(schema.c), C.byref(opts))
+                if rc != L.TGO_OK:
+                    break
+            if rc != L.TGO_OK:       # the ranks still meet in the collective load: an empty one
+                msg = self.lib.tgo_last_error(self.ctx).decode(errors="replace")
+                cr, hold = self._row_block(rows, 0, 0)
+                part = np.zeros(3, np.int64)
+                self.lib.tgo_load_partition_rows(self.ctx, exchange.h, C.byref(cr), C.byref(schema.c), None, 0,
+                                                 L.ptr(part, C.c_int64))
+                raise TitanException(rc, msg)
+            return self.finish_partition_rows(exchange, layout)
         opts, keep = self._opts(scope, apply_cap, labels, weight_key)
         keys = np.ascontiguousarray(rows.keys, dtype=np.int64)
         eb = np.ascontiguousarray(rows.entry_begin, dtype=np.int64)
@@ -203,12 +234,20 @@ class Engine:
         lv = np.ascontiguousarray(rows.limit_valpos if len(rows.limit_valpos) else np.zeros(1, np.int64), dtype=np.int64)
         cr = L.Rows(rows.nrows, L.ptr(keys, C.c_int64), L.ptr(eb, C.c_int64), L.ptr(bb, C.c_int64),
                     L.ptr(data, C.c_uint8), L.ptr(lv, C.c_int64))
-        part = np.zeros(2, np.int64)
+        part = np.zeros(3, np.int64)
         _check(self.lib, self.ctx, self.lib.tgo_load_partition_rows(self.ctx, exchange.h, C.byref(cr), C.byref(schema.c),
                                                                     C.byref(opts), 1 if layout else 0,
                                                                     L.ptr(part, C.c_int64)))
         self.n = self.lib.tgo_num_vertices(self.ctx)
-        return int(part[0]), int(part[1])
+        return int(part[0]), int(part[1]), int(part[2])
+
+    def finish_partition_rows(self, exchange, layout=True):
+        """The collective finish of a partition from staged rows (tgo_finish_partition_rows)."""
+        part = np.zeros(3, np.int64)
+        _check(self.lib, self.ctx, self.lib.tgo_finish_partition_rows(self.ctx, exchange.h, 1 if layout else 0,
+                                                                      L.ptr(part, C.c_int64)))
+        self.n = self.lib.tgo_num_vertices(self.ctx)
+        return int(part[0]), int(part[1]), int(part[2])
 
     def part_call(self, name, *args):
         _check(self.lib, self.ctx, getattr(self.lib, name)(self.ctx, *args))
