@@ -223,3 +223,75 @@ def test_config5_rmat24_weighted_sssp_partitioned(rmat24, world):
     res = ranks.run(lambda be, comm: distributed_sssp(be, r, 0, comm=comm))
     assert np.array_equal(np.concatenate([x[0] for x in res]), d), r
     assert all(x[1][0] == reached for x in res)
+
+
+@pytest.fixture(scope="module")
+def rmat24_one_gpu(rmat24):
+    """One-GPU results on the bench's RMAT-24 graphs (each pinned to the oracle by the config
+    tests above): bothE BFS / the multi-source sweep, capped inE PageRank(20), weighted capped
+    inE delta-stepping SSSP.  Engines are dropped: only the arrays stay."""
+    n, src, dst, roots, w = rmat24
+    seeds = [int(r) for r in roots[:8]]
+    eb = Engine(host_threads=THREADS).load_edges(n, src, dst, BOTH, apply_cap=False)
+    eb.bfs_multi(seeds, n, BOTH, seed_is_dense=True, fetch=False)
+    ms = []
+    for i in range(len(seeds)):
+        d = np.empty(n, np.int64)
+        eb.lib.tgo_copy_multi_distances(eb.ctx, i, L.ptr(d, C.c_int64))
+        ms.append(d)
+    del eb
+    ep = Engine(host_threads=THREADS).load_edges(n, src, dst, IN, apply_cap=True)
+    pr = ep.pagerank(0.85, n, 20)
+    del ep
+    es = Engine(host_threads=THREADS).load_edges(n, src, dst, IN, weight=w, apply_cap=True)
+    for r in roots:
+        d = es.sssp(int(r), n, IN, mode=L.SSSP_DELTA, seed_is_dense=True, stats=True)
+        if es.stats()["reached"] * 4 >= n:
+            sssp = (int(r), d)
+            break
+    del es
+    return seeds, ms, pr, sssp
+
+
+@pytest.mark.parametrize("world", [8, 6])
+def test_rmat24_every_native_loop_at_world(rmat24, rmat24_one_gpu, world):
+    """world 8 (north_star's node) and a non-power-of-two world 6 (edge-
+    balanced slot ranges, as bench.py partitions) on the bench's RMAT-24 graphs, every native
+    partitioned loop over an in-process exchange group on one device: the 8-source sweep and
+    single-source BFS (bothE), PageRank(20) in both exchanges (capped inE: the hot-first blocked
+    layout, 8 / 6 peers' ghost sets) and weighted delta SSSP (capped inE: the W-slice pair
+    exchange) — BFS / SSSP bit-exact and PageRank within 1e-6 L1 of the one-GPU results."""
+    from test_gpu_distributed import Ranks
+    from titan_amd.distributed import (NativeExchange, PR_EXCHANGE_ALLGATHER, PR_EXCHANGE_GHOST, SlotPartition,
+                                       distributed_bfs_native, distributed_msbfs_native, distributed_pagerank_native,
+                                       distributed_sssp_native, word_weights)
+    n, src, dst, roots, w = rmat24
+    seeds, ms, pr_one, (sroot, sd_one) = rmat24_one_gpu
+    part = None if world == 8 else SlotPartition.balanced(word_weights(src, dst, 0, n), world)
+    ns = n if part is None else part.n_slots
+    slot = (lambda v: int(v)) if part is None else (lambda v: int(part.to_slots(np.asarray([v]))[0]))
+
+    def cut(per_rank):
+        if part is None:
+            return np.concatenate(per_rank)
+        return np.concatenate([part.slot_results(r, x) for r, x in enumerate(per_rank)])
+    xs = NativeExchange.local_group(world)
+    ranks = Ranks(world, n, src, dst, BOTH, layout=True, device_counts=True, part=part)
+    res = ranks.run(lambda be, comm: (distributed_msbfs_native(be, [slot(s) for s in seeds], ns, xs[comm.rank]),
+                                      [be.ms_levels(i) for i in range(len(seeds))]))
+    for i in range(len(seeds)):
+        assert np.array_equal(cut([r[1][i] for r in res]), ms[i]), i
+        assert all(r[0][0][i] == int((ms[i] != L.DIST_ABSENT).sum()) for r in res)
+    res = ranks.run(lambda be, comm: distributed_bfs_native(be, slot(seeds[0]), ns, xs[comm.rank]))
+    assert np.array_equal(cut([r[0] for r in res]), ms[0])
+    del ranks
+    ranks = Ranks(world, n, src, dst, IN, layout=True, apply_cap=True, part=part)
+    for mode in (PR_EXCHANGE_ALLGATHER, PR_EXCHANGE_GHOST):
+        res = ranks.run(lambda be, comm: distributed_pagerank_native(be, 0.85, n, 20, xs[comm.rank], mode=mode))
+        got = cut([r[0] for r in res])
+        assert np.abs(got - pr_one).sum() <= PR_L1_TOL, mode
+    del ranks
+    ranks = Ranks(world, n, src, dst, IN, weight=w, layout=True, apply_cap=True, part=part)
+    res = ranks.run(lambda be, comm: distributed_sssp_native(be, slot(sroot), xs[comm.rank]))
+    assert np.array_equal(cut([r[0] for r in res]), sd_one)
+    assert len({r[2] for r in res}) == 1

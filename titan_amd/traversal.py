@@ -3,9 +3,11 @@
 TinkerPop's TraversalVertexProgram runs a Gremlin traversal on the computer: traversers sit
 at vertices with a bulk (a long count of the identical traversers merged there), and every
 vertex step moves each traverser along the incident edges of its vertex.  Titan's only part
-in it is the preload: the whole star graph of every vertex, BOTH directions, every label,
-under the 100 000-entry query limit (VertexProgramScanJob.getQueries, :101-107;
-QueryContainer.DEFAULT_HARD_QUERY_LIMIT) — because a traverser may take any incident edge.
+in it is the preload: the whole star graph of every vertex, BOTH directions, every label
+(VertexProgramScanJob.getQueries, :101-107) — because a traverser may take any incident edge.
+An untyped BOTH query is "fitted" and keeps NO_LIMIT (QueryContainer.java:122;
+BasicVertexCentricQueryBuilder.java:418-431), so the star preload is uncapped: the 100 000-entry
+hard limit cuts only single-direction untyped scopes.
 
 Restated here for the traversals that are pure vertex steps, ``g.V([seeds]).out().in()
 .both()...`` followed by ``count()`` (the k-hop / path-count queries Gremlin OLAP is run for):
