@@ -64,6 +64,7 @@ struct ScopedBuf {                      // scoped device buffer (large ones recy
     }
     T* take() {                         // hand the allocation over (DevArray::own)
         T* q = p;
+        tmp_disown(q);
         p = nullptr;
         n = 0;
         return q;

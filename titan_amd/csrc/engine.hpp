@@ -238,6 +238,7 @@ void host_resize(std::vector<T>& h, size_t count) {
 // reused by the next request they fit; tmp_trim releases them (every load entry point).
 hipError_t tmp_alloc(void** p, size_t bytes);
 void tmp_free(void* p, size_t bytes);
+void tmp_disown(void* p);          // a tmp_alloc block taken over for good (freed with hipFree)
 void tmp_trim();
 // The same graph assembled on the device (assemble.hip): radix sorts instead of the host
 // counting sorts; m < 2^32.

@@ -49,7 +49,7 @@ struct Buf {                            // large ones recycled (tmp_cache.cpp)
         return e;
     }
     void release() { if (p) tmp_free(p, bytes); p = nullptr; }
-    T* take() { T* q = p; p = nullptr; return q; }     // hand over (DevArray::own)
+    T* take() { T* q = p; tmp_disown(q); p = nullptr; return q; }     // hand over (DevArray::own)
     ~Buf() { release(); }
 };
 

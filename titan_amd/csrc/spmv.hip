@@ -20,6 +20,8 @@
 // Every sum has a fixed order: results are bitwise reproducible run to run.
 #include <algorithm>
 #include <cstdlib>
+#include <mutex>
+#include <vector>
 #include <hip/hip_runtime.h>
 #include "engine.hpp"
 
@@ -1055,7 +1057,9 @@ static bool row_prefetch() {
 }
 // dynamic LDS past 64 KB, raised once per kernel instantiation
 static hipError_t big_lds(const void* fn, size_t lds) {
+    static std::mutex mu;                                // the ranks of an in-process partition launch from threads
     static std::vector<const void*> done;
+    std::lock_guard<std::mutex> lk(mu);
     if (std::find(done.begin(), done.end(), fn) != done.end()) return hipSuccess;
     const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
     if (e == hipSuccess) done.push_back(fn);

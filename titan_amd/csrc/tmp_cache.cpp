@@ -82,7 +82,23 @@ hipError_t tmp_alloc(void** p, size_t bytes) {
         (void)hipGetLastError();
         e = hipMalloc(p, bytes);
     }
+    if (e == hipSuccess && *p) {
+        // a fresh address may be one a reused block had before it left the cache for good (a
+        // take() into a graph array, freed later with hipFree): its recorded real size is stale
+        // and would let the block back into the cache as larger than it is — a later request
+        // handed it would write past its end (the world-6 RMAT-24 fault, gpurun_out/r06g)
+        std::lock_guard<std::mutex> lk(g_mu);
+        g_real.erase(*p);
+    }
     return e;
+}
+
+// A block handed out by tmp_alloc leaves the cache's management (ScopedBuf / Buf take(): it
+// becomes a graph array, freed with hipFree): forget its recorded real size.
+void tmp_disown(void* p) {
+    if (!p) return;
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_real.erase(p);
 }
 
 // callers pass their request size; a block that came from the cache goes back with its real
