@@ -286,13 +286,16 @@ int upload_row_blocks_dev(tgo_ctx* ctx, const std::vector<int64_t>& off, RowBloc
 }
 
 // Biased-exponent range [elo, ehi) in which the fixed-point PageRank sums are exact (spmv.hip
-// kFxPoint): |v| >= 2^-53 (the 2^-80 resolution then costs < 2^-27 of a value), and a row of
-// max_len entries below 2^47 (|v| < 2^(47 - c) with 2^c >= max_len).
+// kFxPoint): |v| >= 2^-53 (the 2^-80 resolution then costs < 2^-27 of a value), a row of
+// max_len entries below 2^47 (|v| < 2^(47 - c) with 2^c >= max_len), and a tile's split H words
+// (X >> 40, summed over at most min(max_len, kFxTileMax) entries of a row) below 2^63:
+// |v| < 2^(23 - min(c, 22)).
+constexpr int64_t kFxTileMax = int64_t(1) << 22;      // entries of a fixed-point tile / cold block
 void fx_range(int64_t max_len, int& elo, int& ehi) {
     int c = 0;
     while ((int64_t(1) << c) < max_len && c < 47) ++c;
     elo = 1023 - 53;
-    ehi = 1023 + 47 - c;
+    ehi = std::min(1023 + 47 - c, 1023 + 23 - std::min(c, 22));
 }
 
 // Cache-blocked PageRank in-lists of the rows [0, n_rows) (rows past n_rows have no entries)
@@ -325,7 +328,7 @@ int upload_cold_blocks(tgo_ctx* ctx, const std::vector<int64_t>& off, const std:
         std::string err;
         if (int rc = build_cold_blocks_device(d_off, d_adj, static_cast<int64_t>(off.size()) - 1, d_nnz, n_src, hot,
                                               env_i64("TGO_PR_SEG", kPrSegDefault),
-                                              cold_fx ? env_i64("TGO_PR_FX_CE", 65536) : kTile,
+                                              cold_fx ? std::min(kFxTileMax, env_i64("TGO_PR_FX_CE", 65536)) : kTile,
                                               cold_fx ? std::min<int64_t>(env_i64("TGO_PR_FX_CP", 4096), int64_t(1) << (kPackShift + 1))
                                                       : kMaxRows,
                                               env_i64("TGO_PR_CPACK", 1) != 0, hc, on_dev, ctx->stream, err, win, cold_fx))
@@ -382,8 +385,8 @@ int upload_cold_blocks(tgo_ctx* ctx, const std::vector<int64_t>& off, const std:
             // entries per super-tile: larger tiles share more lines, but keep >= 512 tiles for the
             // 256 CUs (RMAT-24 A/B: 256 K 0.964, 512 K 0.951, 1 M 1.203 ms/update — 97 tiles idle
             // most CUs; profiles/r05e_pr_fx_probe.log)
-            const int64_t fx_e = env_i64("TGO_PR_FX_E", std::min<int64_t>(int64_t(1) << 19,
-                                                                          std::max<int64_t>(int64_t(1) << 16, hc.hoff[n_rows] / 512)));
+            const int64_t fx_e = std::min(kFxTileMax, env_i64("TGO_PR_FX_E", std::min<int64_t>(int64_t(1) << 19,
+                                                                          std::max<int64_t>(int64_t(1) << 16, hc.hoff[n_rows] / 512))));
             if (int rc = pack_supertiles_device(cb.hcsr.adj, cb.hcsr.off, hc.hoff, n_rows, fx_e,
                                                 rbits, tdesc, long_rows, long_len, ctx->stream, err))
                 return fail(ctx, rc, err);

@@ -499,43 +499,55 @@ __global__ void __launch_bounds__(kThreads, 4) gather_hot_pipe(const int64_t* __
 //
 // The form is exact only inside a range: a nonzero |v| below 2^-53 loses more than 2^-27 of
 // itself to the 2^-80 resolution, and a row of D entries overflows the 2^47 range unless every
-// |v| < 2^47 / D.  Infinities and NaN — the +inf contribution of a vertex whose row cut left it
-// no OUT entry (PageRankVertexProgram.java:80-88 divides by edgeCount 0) — have no fixed-point
-// form at all.  Every entry is checked against the layout's range (FxGuard: biased exponents
-// [elo, ehi), from the longest row); one outside it sets *bad, and the caller re-runs the whole
-// program on the plain fp64 gather, whose sums follow Java double arithmetic (+inf + x = +inf,
-// +inf + -inf = NaN).  Inside the range the check costs two integer compares per entry.
+// |v| < 2^47 / D; the split LDS accumulators (below) narrow that to |v| < 2^23 / min(D, 2^22).
+// Infinities and NaN — the +inf contribution of a vertex whose row cut left it no OUT entry
+// (PageRankVertexProgram.java:80-88 divides by edgeCount 0) — have no fixed-point form at all.
+// Every entry is checked against the layout's range (FxGuard: biased exponents [elo, ehi), from
+// the longest row); one outside it sets *bad, and the caller re-runs the whole program on the
+// plain fp64 gather, whose sums follow Java double arithmetic (+inf + x = +inf, +inf + -inf =
+// NaN).  Inside the range the check costs two integer compares per entry.
+//
+// Split accumulators: an entry X = v * 2^80 goes into LDS as two words, H = X >> 40 (signed)
+// and L = X & (2^40 - 1), each by a NON-returning 64-bit LDS add — no carry to propagate, so a
+// wave issues its kFxUnroll entries' adds back to back and never waits on LDS.  The L words of
+// at most 2^22 entries (a tile's cap, kFxTileMax) sum below 2^62; X = H * 2^40 + L is rebuilt
+// as 128 bits once per accumulator (fx_join).
 constexpr int kFxPoint = 80;
+constexpr int kFxLowBits = 40;
+constexpr unsigned long long kFxLowMask = (1ull << kFxLowBits) - 1ull;
 constexpr int kFxThreads = 1024;
 constexpr int kFxSlots = 4096;         // LDS accumulators of a tile: rows x copies
 constexpr int kFxUnroll = 8;
 
-// v * 2^kFxPoint as a two's complement 128-bit integer (truncated below 2^-80).  Only meaningful
-// inside the FxGuard range (|v| < 2^47 at the least); outside it the result is garbage that the
-// guard's flag discards.
+// v * 2^kFxPoint as a two's complement 128-bit integer (truncated below 2^-80), without
+// branches (selects; every shift amount in [0, 63]).  Only meaningful inside the FxGuard range
+// (|v| < 2^47 at the least); outside it the result is garbage that the guard's flag discards.
 __device__ __forceinline__ void fx_of(double v, unsigned long long& lo, unsigned long long& hi) {
     const unsigned long long b = static_cast<unsigned long long>(__double_as_longlong(v));
     const int e = static_cast<int>((b >> 52) & 0x7FF);
-    lo = 0;
-    hi = 0;
-    if (e == 0) return;                                   // zero (or subnormal: flagged by the guard)
-    const unsigned long long m = (b & 0xFFFFFFFFFFFFFull) | (1ull << 52);
+    // zero (or subnormal: flagged by the guard) -> 0
+    const unsigned long long m = e == 0 ? 0ull : (b & 0xFFFFFFFFFFFFFull) | (1ull << 52);
     const int sh = e - 1075 + kFxPoint;                   // v * 2^P = m * 2^sh
-    if (sh > 74) {
-        hi = 1ull << 62;                                  // out of range (flagged by the guard)
-    } else if (sh >= 64) {
-        hi = m << (sh - 64);
-    } else if (sh >= 0) {
-        lo = m << sh;
-        hi = sh > 11 ? m >> (64 - sh) : 0ull;
-    } else if (sh > -53) {
-        lo = m >> (-sh);
-    }
-    if (b >> 63) {                                        // negative: two's complement
-        const unsigned long long c = lo == 0 ? 1ull : 0ull;
-        lo = ~lo + 1ull;
-        hi = ~hi + c;
-    }
+    const unsigned ls = static_cast<unsigned>(min(max(sh, 0), 127));
+    const unsigned rs = static_cast<unsigned>(min(max(-sh, 0), 63));   // m < 2^53: >> 63 is 0
+    const unsigned long long l = ls < 64 ? (m << (ls & 63)) >> rs : 0ull;
+    const unsigned long long h = ls >= 64 ? m << ((ls - 64) & 63) : (m >> 1) >> ((63 - ls) & 63);
+    const bool neg = static_cast<long long>(b) < 0;       // two's complement
+    lo = neg ? ~l + 1ull : l;
+    hi = neg ? ~h + (l == 0 ? 1ull : 0ull) : h;
+}
+// 128-bit X -> (H, L) = (X >> 40, X & (2^40 - 1)); exact for |X| < 2^103
+__device__ __forceinline__ void fx_split(unsigned long long lo, unsigned long long hi, unsigned long long& H,
+                                         unsigned long long& L) {
+    H = (hi << (64 - kFxLowBits)) | (lo >> kFxLowBits);
+    L = lo & kFxLowMask;
+}
+// H * 2^40 + L (H signed, 0 <= L < 2^63) as a 128-bit two's complement integer
+__device__ __forceinline__ void fx_join(unsigned long long H, unsigned long long L, unsigned long long& lo,
+                                        unsigned long long& hi) {
+    const unsigned long long hl = H << kFxLowBits;
+    lo = hl + L;
+    hi = static_cast<unsigned long long>(static_cast<long long>(H) >> (64 - kFxLowBits)) + (lo < hl ? 1ull : 0ull);
 }
 // The 128-bit sum * 2^-80 rounded once to the nearest double (ties to even): the magnitude's
 // top 64 bits with every lower bit OR-ed into bit 0 (a sticky bit far below the 53-bit rounding
@@ -558,6 +570,7 @@ __device__ __forceinline__ double fx_to_double(unsigned long long lo, unsigned l
     const double d = __builtin_ldexp(static_cast<double>(t), e);
     return neg ? -d : d;
 }
+// 128-bit add into global memory (the long rows' chunk totals): few, one thread a tile
 __device__ __forceinline__ void fx_add(unsigned long long* plo, unsigned long long* phi, unsigned long long lo,
                                        unsigned long long hi) {
     const unsigned long long old = atomicAdd(plo, lo);
@@ -571,9 +584,51 @@ struct FxGuard {
     unsigned elo = 0, ehi = 0x800;
     unsigned* bad = nullptr;
 };
-// A tile's entries (packed source << rbits | accumulator) into the LDS accumulators: all index
-// loads, then all gathers, then the conversions and LDS atomics, kFxUnroll entries per thread
-// in flight.  lc: log2 of the copies per accumulator (the lane picks the copy).
+// kFxUnroll * kFxThreads entries from entry b: all index loads, then all gathers, then the
+// conversions and the split LDS adds, without a branch between them (a conditional load per
+// entry made the compiler wait for every outstanding load before the next gather: one gather
+// in flight per wave).  Index positions past ne are clamped to ne - 1 (a valid entry, re-read)
+// and their values zeroed.  (Loading the next batch's indices before this batch's adds measured
+// 11 % slower: profiles/r06l_pr_branchfree_ab.log.)
+template <int diag, bool kGuard>
+__device__ __forceinline__ void fx_idx(const uint32_t* __restrict__ p, int64_t b, int64_t ne, uint32_t (&w)[kFxUnroll]) {
+#pragma unroll
+    for (int j = 0; j < kFxUnroll; ++j)
+        w[j] = __builtin_nontemporal_load(p + min(b + j * kFxThreads + static_cast<int64_t>(threadIdx.x), ne - 1));
+}
+template <int diag, bool kGuard>
+__device__ __forceinline__ void fx_batch(const uint32_t* __restrict__ p, int64_t b, int64_t ne,
+                                         const double* __restrict__ msg, int rbits, uint32_t rmask, int lc, uint32_t cl,
+                                         unsigned long long* s_lo, unsigned long long* s_hi, const FxGuard& guard,
+                                         bool& out, unsigned long long& sink) {
+    uint32_t w[kFxUnroll];
+    fx_idx<diag, kGuard>(p, b, ne, w);
+    __builtin_amdgcn_sched_barrier(0);                   // every index load issued before the first wait
+    double v[kFxUnroll];
+#pragma unroll
+    for (int j = 0; j < kFxUnroll; ++j)
+        v[j] = diag == 2 ? static_cast<double>(w[j]) * 0x1p-40 : msg[w[j] >> rbits];
+#pragma unroll
+    for (int j = 0; j < kFxUnroll; ++j) {
+        if (b + j * kFxThreads + threadIdx.x >= ne) v[j] = 0.0;
+        const unsigned long long bits = static_cast<unsigned long long>(__double_as_longlong(v[j]));
+        const unsigned e = static_cast<unsigned>(bits >> 52) & 0x7FFu;
+        if (kGuard) out |= (bits << 1) != 0 && e - guard.elo >= guard.ehi - guard.elo;   // unsigned: below elo wraps
+        unsigned long long lo, hi, H, L;
+        fx_of(v[j], lo, hi);
+        fx_split(lo, hi, H, L);
+        if (diag == 1) {
+            sink += H ^ L ^ (w[j] & rmask);
+        } else {
+            const uint32_t slot = ((w[j] & rmask) << lc) | cl;
+            atomicAdd(&s_lo[slot], L);
+            atomicAdd(&s_hi[slot], H);
+        }
+    }
+}
+// A tile's entries (packed source << rbits | accumulator) into the split LDS accumulators
+// (s_lo: L words, s_hi: H words), kFxUnroll entries per thread in flight.  lc: log2 of the
+// copies per accumulator (the lane picks the copy).
 // diag (TGO_PR_FX_DIAG, results wrong by design; attribution only): 1 = no LDS atomics (the
 // values are folded into one register), 2 = no gathers (the index word stands in for the value)
 template <int diag = 0, bool kGuard = false>
@@ -582,36 +637,11 @@ __device__ __forceinline__ void fx_accumulate(const uint32_t* __restrict__ p, in
                                               const FxGuard& guard) {
     const uint32_t rmask = (1u << rbits) - 1u;
     const uint32_t cl = threadIdx.x & ((1u << lc) - 1u);
+    constexpr int64_t kStep = static_cast<int64_t>(kFxThreads) * kFxUnroll;
     unsigned long long sink = 0;
     bool out = false;
-    for (int64_t b = 0; b < ne; b += static_cast<int64_t>(kFxThreads) * kFxUnroll) {
-        uint32_t w[kFxUnroll];
-#pragma unroll
-        for (int j = 0; j < kFxUnroll; ++j) {
-            const int64_t k = b + j * kFxThreads + threadIdx.x;
-            w[j] = k < ne ? __builtin_nontemporal_load(p + k) : 0u;
-        }
-        double v[kFxUnroll];
-#pragma unroll
-        for (int j = 0; j < kFxUnroll; ++j) {
-            const int64_t k = b + j * kFxThreads + threadIdx.x;
-            v[j] = k < ne ? (diag == 2 ? static_cast<double>(w[j]) * 0x1p-40 : msg[w[j] >> rbits]) : 0.0;
-        }
-#pragma unroll
-        for (int j = 0; j < kFxUnroll; ++j) {
-            const unsigned long long bits = static_cast<unsigned long long>(__double_as_longlong(v[j]));
-            const unsigned e = static_cast<unsigned>(bits >> 52) & 0x7FFu;
-            if (kGuard) out |= (bits << 1) != 0 && e - guard.elo >= guard.ehi - guard.elo;   // unsigned: below elo wraps
-            unsigned long long lo, hi;
-            fx_of(v[j], lo, hi);
-            if (diag == 1) {
-                sink += lo ^ hi ^ (w[j] & rmask);
-            } else if (lo | hi) {
-                const uint32_t slot = ((w[j] & rmask) << lc) | cl;
-                fx_add(&s_lo[slot], &s_hi[slot], lo, hi);
-            }
-        }
-    }
+    for (int64_t b = 0; b < ne; b += kStep)
+        fx_batch<diag, kGuard>(p, b, ne, msg, rbits, rmask, lc, cl, s_lo, s_hi, guard, out, sink);
     if (diag == 1 && sink == 0x5a5a5a5a5a5a5a5aull) s_lo[0] = sink;      // keep the loads alive
     if (kGuard && out && guard.bad) *guard.bad = 1u;     // rare: the program re-runs in plain fp64
 }
@@ -623,13 +653,12 @@ __device__ __forceinline__ int fx_copies_log2(int rows, int slots = kFxSlots) {
 // The 128-bit total of accumulator i's copies.
 __device__ __forceinline__ void fx_total(const unsigned long long* s_lo, const unsigned long long* s_hi, int i, int lc,
                                          unsigned long long& lo, unsigned long long& hi) {
-    lo = 0;
-    hi = 0;
+    unsigned long long H = 0, L = 0;
     for (int c = 0; c < (1 << lc); ++c) {
-        const unsigned long long nl = lo + s_lo[(i << lc) + c];
-        hi += s_hi[(i << lc) + c] + (nl < lo ? 1ull : 0ull);
-        lo = nl;
+        H += s_hi[(i << lc) + c];
+        L += s_lo[(i << lc) + c];
     }
+    fx_join(H, L, lo, hi);
 }
 
 // The cold sum of row r at emission (TGO_PR_FX_FOLD): its pieces added in segment order, as
@@ -681,8 +710,10 @@ __global__ void __launch_bounds__(kFxThreads) gather_hot_fx(const uint32_t* __re
     const int nslots = rows << lc;
     for (int i = threadIdx.x; i < nslots; i += kFxThreads) {
         const bool carry = (kPass == 2 || kPass == 3) && nr > 0 && (i & ((1 << lc) - 1)) == 0;   // copy 0: the sum so far
-        s_lo[i] = carry ? part[2 * (r0 + (i >> lc))] : 0;
-        s_hi[i] = carry ? part[2 * (r0 + (i >> lc)) + 1] : 0;
+        unsigned long long H = 0, L = 0;
+        if (carry) fx_split(part[2 * (r0 + (i >> lc))], part[2 * (r0 + (i >> lc)) + 1], H, L);
+        s_lo[i] = L;
+        s_hi[i] = H;
     }
     __syncthreads();
     fx_accumulate<diag, kGuard>(padj + e0, e1 - e0, msg, rbits, lc, s_lo, s_hi, guard);
@@ -699,12 +730,12 @@ __global__ void __launch_bounds__(kFxThreads) gather_hot_fx(const uint32_t* __re
             }
         }
     } else if (threadIdx.x == 0) {                        // a long row's chunk: into the row's accumulator
-        unsigned long long lo = 0, hi = 0;
+        unsigned long long H = 0, L = 0, lo, hi;
         for (int c = 0; c < nslots; ++c) {
-            const unsigned long long nl = lo + s_lo[c];
-            hi += s_hi[c] + (nl < lo ? 1ull : 0ull);
-            lo = nl;
+            H += s_hi[c];
+            L += s_lo[c];
         }
+        fx_join(H, L, lo, hi);
         fx_add(&long_acc[2 * (-nr - 1)], &long_acc[2 * (-nr - 1) + 1], lo, hi);
     }
 }
