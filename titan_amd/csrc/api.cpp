@@ -289,13 +289,13 @@ int upload_row_blocks_dev(tgo_ctx* ctx, const std::vector<int64_t>& off, RowBloc
 // kFxPoint): |v| >= 2^-53 (the 2^-80 resolution then costs < 2^-27 of a value), a row of
 // max_len entries below 2^47 (|v| < 2^(47 - c) with 2^c >= max_len), and a tile's split H words
 // (X >> 40, summed over at most min(max_len, kFxTileMax) entries of a row) below 2^63:
-// |v| < 2^(23 - min(c, 22)).
+// |v| < 2^(23 - min(c, 22)); and |v| < 2^11 for the entry conversion (spmv.hip fx_hl).
 constexpr int64_t kFxTileMax = int64_t(1) << 22;      // entries of a fixed-point tile / cold block
 void fx_range(int64_t max_len, int& elo, int& ehi) {
     int c = 0;
     while ((int64_t(1) << c) < max_len && c < 47) ++c;
     elo = 1023 - 53;
-    ehi = std::min(1023 + 47 - c, 1023 + 23 - std::min(c, 22));
+    ehi = std::min({1023 + 47 - c, 1023 + 23 - std::min(c, 22), 1023 + 11});
 }
 
 // Cache-blocked PageRank in-lists of the rows [0, n_rows) (rows past n_rows have no entries)

@@ -499,7 +499,8 @@ __global__ void __launch_bounds__(kThreads, 4) gather_hot_pipe(const int64_t* __
 //
 // The form is exact only inside a range: a nonzero |v| below 2^-53 loses more than 2^-27 of
 // itself to the 2^-80 resolution, and a row of D entries overflows the 2^47 range unless every
-// |v| < 2^47 / D; the split LDS accumulators (below) narrow that to |v| < 2^23 / min(D, 2^22).
+// |v| < 2^47 / D; the split LDS accumulators (below) narrow that to |v| < 2^23 / min(D, 2^22),
+// and the entry conversion (fx_hl) to |v| < 2^11.
 // Infinities and NaN — the +inf contribution of a vertex whose row cut left it no OUT entry
 // (PageRankVertexProgram.java:80-88 divides by edgeCount 0) — have no fixed-point form at all.
 // Every entry is checked against the layout's range (FxGuard: biased exponents [elo, ehi), from
@@ -507,8 +508,8 @@ __global__ void __launch_bounds__(kThreads, 4) gather_hot_pipe(const int64_t* __
 // plain fp64 gather, whose sums follow Java double arithmetic (+inf + x = +inf, +inf + -inf =
 // NaN).  Inside the range the check costs two integer compares per entry.
 //
-// Split accumulators: an entry X = v * 2^80 goes into LDS as two words, H = X >> 40 (signed)
-// and L = X & (2^40 - 1), each by a NON-returning 64-bit LDS add — no carry to propagate, so a
+// Split accumulators: an entry X = floor(v * 2^80) goes into LDS as two words, H = X >> 40
+// (signed) and L = X & (2^40 - 1) (fx_hl), each by a NON-returning 64-bit LDS add — no carry to propagate, so a
 // wave issues its kFxUnroll entries' adds back to back and never waits on LDS.  The L words of
 // at most 2^22 entries (a tile's cap, kFxTileMax) sum below 2^62; X = H * 2^40 + L is rebuilt
 // as 128 bits once per accumulator (fx_join).
@@ -519,22 +520,18 @@ constexpr int kFxThreads = 1024;
 constexpr int kFxSlots = 4096;         // LDS accumulators of a tile: rows x copies
 constexpr int kFxUnroll = 8;
 
-// v * 2^kFxPoint as a two's complement 128-bit integer (truncated below 2^-80), without
-// branches (selects; every shift amount in [0, 63]).  Only meaningful inside the FxGuard range
-// (|v| < 2^47 at the least); outside it the result is garbage that the guard's flag discards.
-__device__ __forceinline__ void fx_of(double v, unsigned long long& lo, unsigned long long& hi) {
-    const unsigned long long b = static_cast<unsigned long long>(__double_as_longlong(v));
-    const int e = static_cast<int>((b >> 52) & 0x7FF);
-    // zero (or subnormal: flagged by the guard) -> 0
-    const unsigned long long m = e == 0 ? 0ull : (b & 0xFFFFFFFFFFFFFull) | (1ull << 52);
-    const int sh = e - 1075 + kFxPoint;                   // v * 2^P = m * 2^sh
-    const unsigned ls = static_cast<unsigned>(min(max(sh, 0), 127));
-    const unsigned rs = static_cast<unsigned>(min(max(-sh, 0), 63));   // m < 2^53: >> 63 is 0
-    const unsigned long long l = ls < 64 ? (m << (ls & 63)) >> rs : 0ull;
-    const unsigned long long h = ls >= 64 ? m << ((ls - 64) & 63) : (m >> 1) >> ((63 - ls) & 63);
-    const bool neg = static_cast<long long>(b) < 0;       // two's complement
-    lo = neg ? ~l + 1ull : l;
-    hi = neg ? ~h + (l == 0 ? 1ull : 0ull) : h;
+// An entry's split words straight from the double: X = floor(v * 2^80) as H = floor(v * 2^40)
+// and L = floor(frac(v * 2^40) * 2^40), every step exact in fp64 (scalings by powers of two,
+// floor, and t - floor(t) are exact), the integers read off the bit patterns of h + 1.5 * 2^52
+// and l + 2^52 (ulp 1 there).  Exact while |v| < 2^11 (|h| < 2^51): the FxGuard range keeps
+// every entry below that; outside it the words are garbage that the guard's flag discards.
+// Ten fp64 / integer operations an entry (the shift-and-select form before it took ~50).
+__device__ __forceinline__ void fx_hl(double v, unsigned long long& H, unsigned long long& L) {
+    const double t = v * 0x1p40;
+    const double h = __builtin_floor(t);
+    const double l = __builtin_floor((t - h) * 0x1p40);
+    H = static_cast<unsigned long long>(__double_as_longlong(h + 0x1.8p52) - __double_as_longlong(0x1.8p52));
+    L = static_cast<unsigned long long>(__double_as_longlong(l + 0x1p52) - __double_as_longlong(0x1p52));
 }
 // 128-bit X -> (H, L) = (X >> 40, X & (2^40 - 1)); exact for |X| < 2^103
 __device__ __forceinline__ void fx_split(unsigned long long lo, unsigned long long hi, unsigned long long& H,
@@ -614,9 +611,8 @@ __device__ __forceinline__ void fx_batch(const uint32_t* __restrict__ p, int64_t
         const unsigned long long bits = static_cast<unsigned long long>(__double_as_longlong(v[j]));
         const unsigned e = static_cast<unsigned>(bits >> 52) & 0x7FFu;
         if (kGuard) out |= (bits << 1) != 0 && e - guard.elo >= guard.ehi - guard.elo;   // unsigned: below elo wraps
-        unsigned long long lo, hi, H, L;
-        fx_of(v[j], lo, hi);
-        fx_split(lo, hi, H, L);
+        unsigned long long H, L;
+        fx_hl(v[j], H, L);
         if (diag == 1) {
             sink += H ^ L ^ (w[j] & rmask);
         } else {
