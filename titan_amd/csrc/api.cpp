@@ -199,12 +199,15 @@ constexpr int64_t kPrSegDefault = 393216;   // 3 MB (profiles/r02an_pr_hot_seg_p
 // ms/update: 384 K 0.852, 512 K 0.827, 768 K 0.814-0.818, 1 M 0.830, 1.5 M 0.913;
 // profiles/r05j_pr_fx_hot_ab.log, r05k_pr_fx_hot_ab.log)
 // The hot head (sources of the hot pass; the partitioned layout's gathered head, over every
-// rank).  With the source-split hot pass (TGO_PR_FX_SPLIT, default 2): 1 M sources, each half's
-// messages (4 MB) an XCD's L2 — 0.944-0.950 -> 0.891-0.894 ms/update at RMAT-24 against the
-// unsplit 768 K head (profiles/r05sp3_pr_split_ab.log)
+// rank).  Round 5's source-split hot pass (TGO_PR_FX_SPLIT=2, 1 M sources, each half's 4 MB an
+// XCD's L2) won with returning 128-bit LDS atomics; with the split non-returning accumulators
+// the one-launch 768 K head is faster (same box, RMAT-24: split 1 M 0.897-0.902, unsplit 768 K
+// 0.802-0.807, 655 K 0.806, 1 M 0.828 ms/update; profiles/r06r_*, r06s_pr_unsplit_sweep.log),
+// so the split is off by default (TGO_PR_FX_SPLIT=1)
+int64_t pr_fx_split_default() { return env_i64("TGO_PR_FX_SPLIT", 1); }
 int64_t pr_hot_default() {
     if (env_i64("TGO_PR_FX", 1) == 0) return 393216;
-    return env_i64("TGO_PR_FX_SPLIT", 2) > 1 ? 1048576 : 786432;
+    return pr_fx_split_default() > 1 ? 1048576 : 786432;
 }
 // LDS window of the hottest sources (lds_window, spmv.hip; TGO_PR_WIN, at most 12288 doubles =
 // 96 KB beside the 16 waves' 4 KB item buffers).  Off by default: measured slower at every
@@ -382,11 +385,13 @@ int upload_cold_blocks(tgo_ctx* ctx, const std::vector<int64_t>& off, const std:
             std::vector<int64_t> tdesc, long_len;
             std::vector<int32_t> long_rows;
             std::string err;
-            // entries per super-tile: larger tiles share more lines, but keep >= 512 tiles for the
-            // 256 CUs (RMAT-24 A/B: 256 K 0.964, 512 K 0.951, 1 M 1.203 ms/update — 97 tiles idle
-            // most CUs; profiles/r05e_pr_fx_probe.log)
-            const int64_t fx_e = std::min(kFxTileMax, env_i64("TGO_PR_FX_E", std::min<int64_t>(int64_t(1) << 19,
-                                                                          std::max<int64_t>(int64_t(1) << 16, hc.hoff[n_rows] / 512))));
+            // entries per super-tile: larger tiles share more lines; about one tile a CU (hot
+            // entries / 256, at most 1 M) — with the split accumulators and the one-launch head,
+            // RMAT-24 (768 K head): 262 K 0.848, 430 K 0.802, 860 K 0.779, 1 M 0.772-0.786, 1.3 M
+            // 0.832, 2 M 0.97 ms/update (profiles/r06t_pr_tile_entries_sweep.log, r06u_*); round 5
+            // with returning atomics measured 512 K best (r05e_pr_fx_probe.log)
+            const int64_t fx_e = std::min(kFxTileMax, env_i64("TGO_PR_FX_E", std::min<int64_t>(int64_t(1) << 20,
+                                                                          std::max<int64_t>(int64_t(1) << 16, hc.hoff[n_rows] / 256))));
             if (int rc = pack_supertiles_device(cb.hcsr.adj, cb.hcsr.off, hc.hoff, n_rows, fx_e,
                                                 rbits, tdesc, long_rows, long_len, ctx->stream, err))
                 return fail(ctx, rc, err);
@@ -400,7 +405,7 @@ int upload_cold_blocks(tgo_ctx* ctx, const std::vector<int64_t>& off, const std:
             HIP_TRY(hipMemset(cb.fx_long_acc, 0, 2 * std::max<int64_t>(cb.fx_nlong, 1) * sizeof(unsigned long long)));
             // TGO_PR_FX_SPLIT=S > 1: the hot pass in S launches over S ranges of the hot sources
             // (each range's messages fit an XCD's L2: 3 MB a half at 768 K hot sources)
-            const int64_t split = std::min<int64_t>(8, std::max<int64_t>(1, env_i64("TGO_PR_FX_SPLIT", 2)));
+            const int64_t split = std::min<int64_t>(8, std::max<int64_t>(1, pr_fx_split_default()));
             if (split > 1 && cb.fx_ntiles > 0) {
                 HIP_TRY(dev_alloc(ctx, cb.fx_mid, cb.fx_ntiles * (split + 1)));
                 HIP_TRY(dev_alloc(ctx, cb.fx_part, 2 * std::max<int64_t>(n_rows, 1)));
