@@ -41,7 +41,11 @@ GROUPS = {
     "sssp_source": ("ds_loop_seed(", "ds_decide(", "ds_decide_bins(", "ds_extract_dev(", "ds_extract_bins(",
                     "ds_commit_dev<", "ds_relax_dev<", "ds_pull_heavy(", "ds_publish(", "ds_pull_flip("),
 }
-UNIT_KERNEL = {"pagerank_update": ("gather_hot_pf<", "gather_hot_pf(", "gather_short_packed<", "gather_hot_fx<"),
+# one dispatch per unit: the fixed-point hot pass counts only its emitting launch (kPass 0, or
+# kPass 2 = the last of a source split) — counting every gather_hot_fx dispatch halved the
+# round-5 per-update figures (two launches an update with TGO_PR_FX_SPLIT=2)
+UNIT_KERNEL = {"pagerank_update": ("gather_hot_pf<", "gather_hot_pf(", "gather_short_packed<", "gather_hot_fx<4096, 0, 0,",
+                                   "gather_hot_fx<4096, 0, 2,", "gather_hot_fx<8192, 0, 0,"),
                "msbfs_sweep": ("ms_seed(",), "sssp_source": ("ds_loop_seed(",)}
 
 
