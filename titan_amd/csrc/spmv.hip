@@ -518,7 +518,10 @@ constexpr int kFxLowBits = 40;
 constexpr unsigned long long kFxLowMask = (1ull << kFxLowBits) - 1ull;
 constexpr int kFxThreads = 1024;
 constexpr int kFxSlots = 4096;         // LDS accumulators of a tile: rows x copies
-constexpr int kFxUnroll = 8;
+// entries per thread per batch: the gathers in flight per wave.  6 with the one-launch head and
+// ~1 tile a CU (RMAT-24 same box: 2 0.848, 4 0.786, 5 0.753, 6 0.750, 7 0.765, 8 0.786, 12 1.02,
+// 16 1.20 ms/update — more requests in flight thrash the L2; profiles/r06xyz_pr_unroll_ab.log)
+constexpr int kFxUnroll = 6;
 
 // An entry's split words straight from the double: X = floor(v * 2^80) as H = floor(v * 2^40)
 // and L = floor(frac(v * 2^40) * 2^40), every step exact in fp64 (scalings by powers of two,
