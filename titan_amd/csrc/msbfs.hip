@@ -138,25 +138,40 @@ __global__ void __launch_bounds__(kBlock) ms_pull(View pull, View push, int64_t 
                 const int64_t e = l == 0 ? e0 : e1;
                 bool cutl = false;
                 // kStep entries per dependent round trip: their index loads issue together,
-                // then their mask gathers (lists rarely cover every open source early)
+                // then their bitmap probes, then their mask gathers (lists rarely cover every
+                // open source early).  No branch inside a trip: positions past the list re-read
+                // its last entry, a filtered entry gathers mask 0's line (one L1 line for the
+                // wave) and drops it — a conditional load per entry made the compiler wait for
+                // every outstanding load before the next, one load in flight per lane
                 for (int64_t k = l == 0 ? b0 : b1; k < e && (acc & want) != want && !cutl; k += kStep) {
                     int32_t u[kStep];
+                    bool ok[kStep], f[kStep];
 #pragma unroll
                     for (int j = 0; j < kStep; ++j) {
-                        u[j] = k + j < e ? __builtin_nontemporal_load(adj + k + j) : -1;
-                        if (u[j] >= hot_lim) { u[j] = -1; cutl = true; }
+                        u[j] = __builtin_nontemporal_load(adj + min(k + j, e - 1));
+                        const bool in = k + j < e;
+                        cutl |= in && u[j] >= hot_lim;
+                        ok[j] = in && u[j] < hot_lim;
+                        f[j] = ok[j];
                     }
-                    bool f[kStep];
+                    if (fbm) {                                        // kernel-uniform
+                        uint64_t bw[kStep];
 #pragma unroll
-                    for (int j = 0; j < kStep; ++j) f[j] = u[j] >= 0 && maybe_frontier(fbm, u[j], filter_from);
+                        for (int j = 0; j < kStep; ++j) bw[j] = fbm[(f[j] && u[j] >= filter_from ? u[j] : 0) >> 6];
+#pragma unroll
+                        for (int j = 0; j < kStep; ++j)
+                            f[j] = f[j] && (u[j] < filter_from || ((bw[j] >> (u[j] & 63)) & 1ULL));
+                    }
+                    uint64_t mk[kStep];
+#pragma unroll
+                    for (int j = 0; j < kStep; ++j) mk[j] = fr[f[j] ? u[j] : 0];
                     uint64_t m = 0;
 #pragma unroll
-                    for (int j = 0; j < kStep; ++j)
-                        if (f[j]) m |= fr[u[j]];
+                    for (int j = 0; j < kStep; ++j) m |= f[j] ? mk[j] : 0ULL;
                     acc |= m;
                     if (kDiag)
                         for (int j = 0; j < kStep; ++j)
-                            if (u[j] >= 0) { ++dg[0]; ++dg[u[j] < kDiagHot ? 1 : 2]; }
+                            if (ok[j]) { ++dg[0]; ++dg[u[j] < kDiagHot ? 1 : 2]; }
                 }
                 cut |= cutl;
             }
@@ -972,8 +987,10 @@ hipError_t k_ms_pull(const View& pull, const View& push, int64_t n_active, uint6
                      const uint64_t* fbm, uint64_t* vis, uint64_t* nx, LevelPlanes lvl, Counters* cnt,
                      int32_t next_level, hipStream_t s, int32_t filter_from, uint64_t dense, const uint64_t* cand,
                      MsColdSplit cs) {
-    // TGO_MS_STEP: entries a lane loads per round trip of its own list (8 default; 4 / 16 probes)
-    static const int step = [] { const char* e = std::getenv("TGO_MS_STEP"); return e ? std::atoi(e) : 8; }();
+    // TGO_MS_STEP: entries a lane loads per round trip of its own list (4 default since the
+    // trips are branch-free, round 6: sweep 3.623 -> 3.562 ms against 8 with the branchy trips,
+    // profiles/r06ms1_ms_branchfree_ab.log; 8 / 16 probes)
+    static const int step = [] { const char* e = std::getenv("TGO_MS_STEP"); return e ? std::atoi(e) : 4; }();
     static const bool diag = [] { const char* e = std::getenv("TGO_MS_DIAG"); return e && std::atoi(e) != 0; }();
     // TGO_MS_LONG: entries per lane per trip of a long list.  1 (default, round 4): with the
     // source split most long walks stop early, and a 64-entry trip stops them soonest — sweep
