@@ -463,11 +463,12 @@ __global__ void __launch_bounds__(kBlock) ds_commit_dev(const int32_t* __restric
 // [plo, plo + n_local) is min-reduced into rbest and marked in rmark for the owner (delta.hip).
 // kDone (binned loop with the done filter, TGO_DS_DONE): the done-word stage is compiled only
 // when it runs (its 8 words per thread cost the occupancy of the filter-off kernel).
-// kE: entries per thread of a tile (kBlock * kE per tile).  5 (round 5): 125 VGPRs, 4 waves
-// per SIMD — 8 % faster per RMAT-24 source than 8 (160 VGPRs, 3 waves; 6: 136, 3 waves), 1 %
-// faster than 4 (101 VGPRs, 4 waves); 3 (89 / 5 waves) and 2 (76 / 6 waves) slower: too few
-// loads in flight per wave (profiles/r05s2_sssp_relax_e_ab.log, r05s4_sssp_relax_e45_ab.log).
-constexpr int kDsRelaxE = 5;
+// kE: entries per thread of a tile (kBlock * kE per tile).  8 (round 6, with the branch-free
+// stages below): 127 VGPRs, 4 waves per SIMD — the RMAT-24 sum over 4 roots 47.0 ms (round-5
+// code, kE 5) -> 45.7 (kE 5, 97 VGPRs) -> 44.0 (kE 8); 6: 45.2, 12 (174 VGPRs): 55.6, 16: 56.3
+// (profiles/r06ds1_sssp_branchfree_ab.log, r06ds2_sssp_relax_e_ab.log).  Round 5 measured 5 best
+// when every stage's loads were serialised (125 VGPRs then).
+constexpr int kDsRelaxE = 8;
 template <bool kBins, bool kPart, bool kDone, int kE>
 __device__ __forceinline__ void relax_body(int64_t bid, int64_t nb, const int64_t* __restrict__ off,
         const int32_t* __restrict__ adj, const int32_t* __restrict__ wt, const int64_t* __restrict__ light,
@@ -523,11 +524,13 @@ __device__ __forceinline__ void relax_body(int64_t bid, int64_t nb, const int64_
         // independent and in flight together (one entry at a time left every thread waiting
         // out the whole search -> list -> distance -> atomic chain once per entry)
         int64_t u[kE], e[kE];
+        bool hv[kE];
 #pragma unroll
         for (int k = 0; k < kE; ++k) {           // 1: owning queue entry (LDS search)
             const int64_t j = t0 + k * kBlock + threadIdx.x;
             u[k] = -1;
             e[k] = 0;
+            hv[k] = false;
             if (j >= t1) continue;
             int32_t qe;
             int64_t start;
@@ -542,39 +545,52 @@ __device__ __forceinline__ void relax_body(int64_t bid, int64_t nb, const int64_
             }
             const uint32_t ue = static_cast<uint32_t>(qe);
             u[k] = static_cast<int64_t>(ue & ~kHeavy);
-            e[k] = ((ue & kHeavy) ? light[u[k]] : off[u[k]]) + (j - start);
+            e[k] = j - start;
+            hv[k] = (ue & kHeavy) != 0;
         }
+#pragma unroll
+        for (int k = 0; k < kE; ++k) {           // 1b: the list starts, loads issued together
+            const int64_t* base = hv[k] ? light : off;
+            e[k] += base[u[k] >= 0 ? u[k] : 0];
+        }
+        // Stages 2-4 issue each stage's memory operations for all kE entries together, without a
+        // branch around a load: a conditional load per entry made the compiler wait for every
+        // outstanding load before the next (one load, then one atomic, in flight per lane).
+        // Lanes without an entry read entry 0 / vertex 0 (valid: the tile exists, n >= 1) and
+        // drop the values.
         int32_t t[kE], w[kE];
         int64_t mu[kE], du[kE];
 #pragma unroll
         for (int k = 0; k < kE; ++k) {           // 2: entry, the source's snapshot
-            if (u[k] < 0) continue;
-            t[k] = adj[e[k]];
-            w[k] = wt[e[k]];
-            mu[k] = msg[u[k]];
-            du[k] = dist[u[k]];
+            const bool ok = u[k] >= 0;
+            const int64_t ek = ok ? e[k] : 0, uk = ok ? u[k] : 0;
+            t[k] = adj[ek];
+            w[k] = wt[ek];
+            mu[k] = msg[uk];
+            du[k] = dist[uk];
         }
         int64_t cand[kE], dt[kE], tl[kE];
         uint64_t dw[kE];
         if (kBins && kDone) {
 #pragma unroll
             for (int k = 0; k < kE; ++k)         // 3a: done words (L2-resident bitmap)
-                dw[k] = (done && u[k] >= 0) ? done[t[k] >> 6] : 0ULL;
+                dw[k] = done ? done[(u[k] >= 0 ? t[k] : 0) >> 6] : 0ULL;
         }
 #pragma unroll
         for (int k = 0; k < kE; ++k) {           // 3: the targets' distances
-            cand[k] = -1;
-            if (u[k] < 0) continue;
-            if (w[k] == kMissingWeight) { bad = true; continue; }     // edge.value(weight) on a missing key
-            if (du[k] < mu[k]) continue;     // u improved during this phase: pending again, relaxes later
+            const bool ok = u[k] >= 0;
+            bad |= ok && w[k] == kMissingWeight;                   // edge.value(weight) on a missing key
+            // u improved during this phase (du < mu): pending again, relaxes later
+            bool live = ok && w[k] != kMissingWeight && !(du[k] < mu[k]);
             // a done target's distance is below every candidate of a later bucket: no read
-            if (kBins && kDone && ((dw[k] >> (t[k] & 63)) & 1ULL)) continue;
-            cand[k] = mu[k] + static_cast<int64_t>(w[k]);
+            if (kBins && kDone) live = live && !((dw[k] >> (t[k] & 63)) & 1ULL);
+            cand[k] = live ? mu[k] + static_cast<int64_t>(w[k]) : -1;
             if constexpr (kPart) {
                 tl[k] = static_cast<int64_t>(t[k]) - plo;
-                dt[k] = (tl[k] >= 0 && tl[k] < n_local) ? dist[tl[k]] : rbest[t[k]];
+                const bool local = tl[k] >= 0 && tl[k] < n_local;
+                dt[k] = local ? dist[live ? tl[k] : 0] : rbest[live ? t[k] : 0];
             } else {
-                dt[k] = dist[t[k]];
+                dt[k] = dist[live ? t[k] : 0];
             }
         }
         int32_t tv[kE];
@@ -583,32 +599,54 @@ __device__ __forceinline__ void relax_body(int64_t bid, int64_t nb, const int64_
         unsigned int fl[kE];                     // and its slot among the tile's appends
         int ntake = 0;
         int64_t dtake = 0;
+        bool imp[kE];                            // 4: min, pending bit, take
 #pragma unroll
-        for (int k = 0; k < kE; ++k) {           // 4: min, pending bit, take
+        for (int k = 0; k < kE; ++k) imp[k] = cand[k] >= 0 && cand[k] < dt[k];   // a stale (larger) read only costs an atomic
+        if constexpr (kPart) {                   // a remote target: best sent so far
+            long long rold[kE];
+#pragma unroll
+            for (int k = 0; k < kE; ++k) {
+                rold[k] = kInf;
+                if (imp[k] && !(tl[k] >= 0 && tl[k] < n_local))
+                    rold[k] = atomicMin(reinterpret_cast<long long*>(&rbest[t[k]]), static_cast<long long>(cand[k]));
+            }
+#pragma unroll
+            for (int k = 0; k < kE; ++k) {
+                if (!imp[k] || (tl[k] >= 0 && tl[k] < n_local)) continue;
+                imp[k] = false;
+                if (cand[k] < rold[k]) {
+                    const int64_t g = t[k];
+                    const uint64_t rbit = 1ULL << (g & 63);
+                    if (!(rmark[g >> 6] & rbit)) atomicOr(reinterpret_cast<unsigned long long*>(&rmark[g >> 6]), rbit);
+                }
+            }
+        }
+        int32_t tk[kE];
+        long long old[kE];
+#pragma unroll
+        for (int k = 0; k < kE; ++k) {           // 4a: every improving entry's atomicMin in flight together
+            tk[k] = t[k];
+            if constexpr (kPart) tk[k] = static_cast<int32_t>(tl[k]);
+            old[k] = kInf;
+            if (imp[k]) old[k] = atomicMin(reinterpret_cast<long long*>(&dist[tk[k]]), static_cast<long long>(cand[k]));
+        }
+        unsigned long long ob[kE];
+#pragma unroll
+        for (int k = 0; k < kE; ++k) {           // 4b: then every improved entry's pending bit
+            imp[k] = imp[k] && cand[k] < old[k];
+            ob[k] = 0;
+            if (imp[k]) ob[k] = atomicOr(reinterpret_cast<unsigned long long*>(&pend[tk[k] >> 6]), 1ULL << (tk[k] & 63));
+        }
+#pragma unroll
+        for (int k = 0; k < kE; ++k) {           // 4c: take, or a pile / the pending minimum
             tv[k] = -1;
             td[k] = 0;
             fb[k] = -1;
-            if (cand[k] < 0 || cand[k] >= dt[k]) continue;    // a stale (larger) read only costs an atomic
-            if constexpr (kPart) {
-                if (!(tl[k] >= 0 && tl[k] < n_local)) {       // a remote target: best sent so far
-                    const int64_t g = t[k];
-                    const long long rold = atomicMin(reinterpret_cast<long long*>(&rbest[g]), static_cast<long long>(cand[k]));
-                    if (cand[k] < rold) {
-                        const uint64_t rbit = 1ULL << (g & 63);
-                        if (!(rmark[g >> 6] & rbit)) atomicOr(reinterpret_cast<unsigned long long*>(&rmark[g >> 6]), rbit);
-                    }
-                    continue;
-                }
-            }
-            int32_t tk = t[k];
-            if constexpr (kPart) tk = static_cast<int32_t>(tl[k]);
-            const long long old = atomicMin(reinterpret_cast<long long*>(&dist[tk]), static_cast<long long>(cand[k]));
-            if (cand[k] >= old) continue;
-            const uint64_t bit = 1ULL << (tk & 63);
-            const unsigned long long ob = atomicOr(reinterpret_cast<unsigned long long*>(&pend[tk >> 6]), bit);
-            if (!(ob & bit) && cand[k] < thr) {
-                tv[k] = tk;
-                td[k] = light_deg(off, light, tk);
+            if (!imp[k]) continue;
+            const uint64_t bit = 1ULL << (tk[k] & 63);
+            if (!(ob[k] & bit) && cand[k] < thr) {
+                tv[k] = tk[k];
+                td[k] = light_deg(off, light, tk[k]);
                 ++ntake;
                 dtake += td[k];
             } else if (kBins) {
@@ -1121,14 +1159,10 @@ hipError_t k_ds_loop_step_bins(const DevCsr& ws, const int64_t* light, uint64_t*
                                                  nbins, pile, cap, pull);
         ds_pull_flip<<<1, 64, 0, s>>>(L);
     }
-    // TGO_DS_RELAX_E (A/B): entries per thread of the binned relax (default kDsRelaxE)
+    // TGO_DS_RELAX_E=5 (A/B): the round-5 entries per thread of the binned relax (default kDsRelaxE)
     static const int re = static_cast<int>(env_i64_dl("TGO_DS_RELAX_E", kDsRelaxE));
-    if (!done_filter && re == 8) {
-        ds_relax_dev<true, false, false, 8><<<rg, kBlock, 0, s>>>(ws.off, ws.adj, ws.w, light, q[cur], qpre[cur], msg,
-                                                                  dist, pend, q[cur ^ 1], qpre[cur ^ 1], L, cur, delta,
-                                                                  nbins, pile, cap, nullptr);
-    } else if (!done_filter && re == 4) {
-        ds_relax_dev<true, false, false, 4><<<rg, kBlock, 0, s>>>(ws.off, ws.adj, ws.w, light, q[cur], qpre[cur], msg,
+    if (!done_filter && re == 5) {
+        ds_relax_dev<true, false, false, 5><<<rg, kBlock, 0, s>>>(ws.off, ws.adj, ws.w, light, q[cur], qpre[cur], msg,
                                                                   dist, pend, q[cur ^ 1], qpre[cur ^ 1], L, cur, delta,
                                                                   nbins, pile, cap, nullptr);
     } else if (done_filter)
