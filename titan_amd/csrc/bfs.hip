@@ -100,17 +100,22 @@ __global__ void __launch_bounds__(kBlock) bu_step(View pull, View push, int64_t 
         // short lists: the lane scans its own list and stops at the first frontier hit
         if (open && deg <= serial) {
             // kS entries per step: their index loads and bitmap probes issue together, so a
-            // lane pays one dependent round trip per kS entries instead of per entry.
+            // lane pays one dependent round trip per kS entries instead of per entry.  No branch
+            // around a load (positions past the list re-read its last entry and are masked):
+            // a conditional load per entry made the compiler wait for each probe in turn.
             for (int l = 0; l < 2 && !found; ++l) {
                 const int32_t* adj = l == 0 ? pull.adj0 : pull.adj1;
                 const int64_t e = l == 0 ? e0 : e1;
                 for (int64_t k = l == 0 ? b0 : b1; k < e && !found; k += kS) {
                     int32_t u[kS];
 #pragma unroll
-                    for (int j = 0; j < kS; ++j) u[j] = k + j < e ? adj[k + j] : -1;
+                    for (int j = 0; j < kS; ++j) u[j] = adj[min(k + j, e - 1)];
+                    uint64_t wv[kS];
+#pragma unroll
+                    for (int j = 0; j < kS; ++j) wv[j] = fb[u[j] >> 6];
                     uint64_t f = 0;
 #pragma unroll
-                    for (int j = 0; j < kS; ++j) f |= u[j] >= 0 ? fb[u[j] >> 6] >> (u[j] & 63) : 0;
+                    for (int j = 0; j < kS; ++j) f |= k + j < e ? wv[j] >> (u[j] & 63) : 0;
                     found = (f & 1ULL) != 0;
                 }
             }
@@ -386,8 +391,11 @@ hipError_t k_bu_step(const View& pull, const View& push, int64_t n, const uint64
     const int64_t words = (n + 63) / 64;
     // TGO_BFS_SERIAL: lists up to this many entries are scanned by their own lane (kSerialScan default)
     static const int64_t serial = [] { const char* e = std::getenv("TGO_BFS_SERIAL"); return e ? std::atoll(e) : kSerialScan; }();
-    // TGO_BFS_BU_STEP (A/B): entries per dependent round trip of a lane's own list
-    static const int bs = [] { const char* e = std::getenv("TGO_BFS_BU_STEP"); return e ? std::atoi(e) : 4; }();
+    // TGO_BFS_BU_STEP (A/B): entries per dependent round trip of a lane's own list — 2 since the
+    // trips are branch-free (round 6, RMAT-24 16 roots, one box: 4 -> 2 hmean 360 -> 374 GTEPS,
+    // 8: 313; a second box: 2 371, 4 374, 1 363 — 2 and 4 within noise there;
+    // profiles/r06bu_bfs_bu_step_ab.log)
+    static const int bs = [] { const char* e = std::getenv("TGO_BFS_BU_STEP"); return e ? std::atoi(e) : 2; }();
     // 2048 blocks (8192 waves: one resident round at 8 waves per SIMD), each wave walking 32
     // words at RMAT-24: hmean 326-331 -> 368-371 GTEPS over the 64 bench roots against 8192
     // blocks (4096: 346-360, 1024: 327, 16384: 276-279; profiles/r05bg_bfs_bu_grid_ab.log).
@@ -396,10 +404,12 @@ hipError_t k_bu_step(const View& pull, const View& push, int64_t n, const uint64
     const int g = grid_for(words * 64, kBlock, 2048);
     if (bs == 8)
         bu_step<8><<<g, kBlock, 0, s>>>(pull, push, n, fb, vb, nb, level, cnt, next_level, serial);
-    else if (bs == 2)
-        bu_step<2><<<g, kBlock, 0, s>>>(pull, push, n, fb, vb, nb, level, cnt, next_level, serial);
-    else
+    else if (bs == 4)
         bu_step<4><<<g, kBlock, 0, s>>>(pull, push, n, fb, vb, nb, level, cnt, next_level, serial);
+    else if (bs == 1)
+        bu_step<1><<<g, kBlock, 0, s>>>(pull, push, n, fb, vb, nb, level, cnt, next_level, serial);
+    else
+        bu_step<2><<<g, kBlock, 0, s>>>(pull, push, n, fb, vb, nb, level, cnt, next_level, serial);
     return hipGetLastError();
 }
 hipError_t k_bfs_queue(const View& push, int64_t n, const uint64_t* fb, int32_t* qn, int64_t* qdeg, Counters* cnt,
