@@ -629,7 +629,8 @@ __device__ __forceinline__ void fx_batch(const uint32_t* __restrict__ p, int64_t
 // (s_lo: L words, s_hi: H words), kFxUnroll entries per thread in flight.  lc: log2 of the
 // copies per accumulator (the lane picks the copy).
 // diag (TGO_PR_FX_DIAG, results wrong by design; attribution only): 1 = no LDS atomics (the
-// values are folded into one register), 2 = no gathers (the index word stands in for the value)
+// values are folded into one register), 2 = no gathers (the index word stands in for the value),
+// 3 = the hot pass's emission without the cold fold and the update
 template <int diag = 0, bool kGuard = false>
 __device__ __forceinline__ void fx_accumulate(const uint32_t* __restrict__ p, int64_t ne, const double* __restrict__ msg,
                                               int rbits, int lc, unsigned long long* s_lo, unsigned long long* s_hi,
@@ -678,7 +679,6 @@ __device__ __forceinline__ void fx_emit(const PrColdFinal& fin, const FoldSrc& f
     if (fold.cptr) fin.f(r, hot + fold.cold(r));
     else fin(r, hot);
 }
-
 // One super-tile per workgroup: desc {first entry, end entry, first row, rows | -(long + 1)}.
 // Each row has 2^lc copies of its accumulator (rows * copies <= kSlots), the copy chosen by
 // the lane, so a tile of few rows does not serialise its lanes on one LDS address.
@@ -724,6 +724,8 @@ __global__ void __launch_bounds__(kFxThreads) gather_hot_fx(const uint32_t* __re
             if (kPass == 1 || kPass == 3) {
                 part[2 * (r0 + i)] = lo;
                 part[2 * (r0 + i) + 1] = hi;
+            } else if (diag == 3) {                       // attribution: no fold, no update
+                fin.f.contrib_next[r0 + i] = fx_to_double(lo, hi);
             } else {
                 fx_emit(fin, fold, r0 + i, fx_to_double(lo, hi));   // + the row's cold sum, then the update
             }
@@ -1223,6 +1225,9 @@ hipError_t k_pr_hot_phase(const ColdBlocks& cb, const double* contrib, const dou
                                                                           cb.fx_long_acc, fold, fx_guard(cb));
                 else if (d == 2)
                     gather_hot_fx<kFxSlots, 2><<<g, kFxThreads, lds, s>>>(padj, cb.fx_desc, cb.fx_rbits, contrib, fin,
+                                                                          cb.fx_long_acc, fold, fx_guard(cb));
+                else if (d == 3)
+                    gather_hot_fx<kFxSlots, 3><<<g, kFxThreads, lds, s>>>(padj, cb.fx_desc, cb.fx_rbits, contrib, fin,
                                                                           cb.fx_long_acc, fold, fx_guard(cb));
                 else
                     gather_hot_fx<kFxSlots, 0><<<g, kFxThreads, lds, s>>>(padj, cb.fx_desc, cb.fx_rbits, contrib, fin,
