@@ -270,6 +270,79 @@ __device__ __forceinline__ void chunk_extract_packed(int64_t words, const Probe&
     });
 }
 
+// chunk_extract_packed over a staged probe (frontier.hpp extract_count_staged)
+template <int kStreams, class Probe>
+__device__ __forceinline__ void chunk_extract_packed_staged(int64_t words, const Probe& probe, int32_t* __restrict__ qn,
+                                                            int64_t* __restrict__ qpre, unsigned long long* qc) {
+    const int64_t per = ((words + gridDim.x - 1) / gridDim.x + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock;
+    const int64_t w0 = static_cast<int64_t>(blockIdx.x) * per;
+    const int64_t w1 = min(words, w0 + per);
+    const int wave = threadIdx.x >> 6;
+    const unsigned long long below = (1ULL << lane()) - 1ULL;
+    int64_t count = 0, dsum = 0;
+    unsigned long long mask = 0;
+    bool touch = false;
+    if (w0 + wave < w1) extract_count_staged<kStreams>(w0 + wave, w1, probe, count, dsum, mask, touch);
+    const int64_t wc = wave_incl_scan(count), wdg = wave_incl_scan(dsum);
+    int64_t slot0, doff0;
+    block_reserve(qc, lane() == 63 ? wc : 0, lane() == 63 ? wdg : 0, slot0, doff0);
+    int64_t cursor = __shfl(slot0, 63, 64), dcur = __shfl(doff0, 63, 64);
+    if (!touch) return;                                      // wave-uniform
+    extract_write_staged<kStreams>(w0 + wave, w1, mask, probe, [&](const Take* t) {
+        for (int k = 0; k < kStreams; ++k) {
+            const unsigned long long bm = __ballot(t[k].take);
+            if (!bm) continue;
+            const int64_t d = t[k].take ? t[k].deg : 0;
+            const int64_t id = wave_incl_scan(d);
+            if (t[k].take) {
+                const int64_t slot = cursor + __popcll(bm & below);
+                qn[slot] = t[k].entry;
+                qpre[slot] = dcur + id - d;
+            }
+            cursor += __popcll(bm);
+            dcur += __shfl(id, 63, 64);
+        }
+    });
+}
+
+// The bitmap-scan extraction's probe in stages: the pending / member words, then each lane's
+// distance and list bounds (only where its bit is set), then the takes.
+struct ScanProbe {
+    const int64_t* off; const int64_t* light; uint64_t* pend; uint64_t* member; const int64_t* dist;
+    uint64_t* fin; int64_t thr; long long* left;
+    struct State { uint64_t pb, mb; long long d; int64_t o0, o1, lt; };
+    __device__ __forceinline__ void stage1(int64_t wd, State& s) const {
+        s.pb = pend[wd];                                      // uniform across the wave
+        s.mb = member[wd];
+    }
+    __device__ __forceinline__ void stage2(int64_t wd, State& s) const {
+        const int64_t v = (wd << 6) + lane();
+        const bool p = (s.pb >> lane()) & 1ULL, mine = (s.mb >> lane()) & 1ULL;
+        s.d = p ? static_cast<long long>(dist[v]) : kInf;
+        s.o0 = p ? off[v] : 0;
+        s.o1 = mine ? off[v + 1] : 0;
+        s.lt = p || mine ? light[v] : 0;
+    }
+    __device__ __forceinline__ bool finish(int64_t wd, const State& s, Take* t, bool commit) const {
+        const int64_t v = (wd << 6) + lane();
+        const bool p = (s.pb >> lane()) & 1ULL, mine = (s.mb >> lane()) & 1ULL;
+        const bool lt = p && s.d < thr;
+        if (!commit && p && !lt && s.d < *left) *left = s.d;
+        const int64_t hdeg = mine ? s.o1 - s.lt : 0;
+        const unsigned long long tm = __ballot(lt);
+        if (commit && lane() == 0) {
+            if (tm) pend[wd] = s.pb & ~tm;
+            if (s.mb) {
+                member[wd] = 0;
+                if (fin) fin[wd] |= s.mb;
+            }
+        }
+        t[0] = {lt, static_cast<int32_t>(v), lt ? s.lt - s.o0 : 0};
+        t[1] = {hdeg > 0, static_cast<int32_t>(static_cast<uint32_t>(v) | kHeavy), hdeg};
+        return tm || s.mb;
+    }
+};
+
 // done (binned loop, may be null): when the decision found the bucket finished (L->xfin), the
 // members taken here are final and become done.
 __device__ __forceinline__ void extract_scan(const int64_t* __restrict__ off, const int64_t* __restrict__ light,
@@ -279,29 +352,8 @@ __device__ __forceinline__ void extract_scan(const int64_t* __restrict__ off, co
     uint64_t* const fin = (done && L->xfin) ? done : nullptr;
     const int64_t words = (n + 63) >> 6;
     long long left = kInf;                                   // smallest distance left pending
-    auto probe = [&](int64_t wd, Take* t, bool commit) -> bool {
-        const uint64_t pb = pend[wd];                        // uniform across the wave
-        const uint64_t mb = member[wd];
-        const int64_t v = (wd << 6) + lane();
-        const bool p = pb && ((pb >> lane()) & 1ULL);
-        const long long d = p ? static_cast<long long>(dist[v]) : kInf;
-        const bool lt = p && d < thr;
-        if (!commit && p && !lt && d < left) left = d;
-        const bool mine = mb && ((mb >> lane()) & 1ULL);
-        const int64_t hdeg = mine ? off[v + 1] - light[v] : 0;
-        const unsigned long long tm = __ballot(lt);
-        if (commit && lane() == 0) {
-            if (tm) pend[wd] = pb & ~tm;
-            if (mb) {
-                member[wd] = 0;
-                if (fin) fin[wd] |= mb;
-            }
-        }
-        t[0] = {lt, static_cast<int32_t>(v), lt ? light_deg(off, light, v) : 0};
-        t[1] = {hdeg > 0, static_cast<int32_t>(static_cast<uint32_t>(v) | kHeavy), hdeg};
-        return tm || mb;
-    };
-    chunk_extract_packed<2>(words, probe, qn, qpre, &L->qc[cur]);
+    const ScanProbe probe{off, light, pend, member, dist, fin, thr, &left};
+    chunk_extract_packed_staged<2>(words, probe, qn, qpre, &L->qc[cur]);
     const long long m = block_min(left);
     if (threadIdx.x == 0 && m != kInf) atomicMin(&L->lo, m);
 }

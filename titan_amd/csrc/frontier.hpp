@@ -227,6 +227,73 @@ __device__ __forceinline__ void extract_write(int64_t first, int64_t end, unsign
             if (wl[u] >= 0) emit(t[u]);
     }
 }
+// Staged probes (Probe::State, stage1 / stage2 / finish): the kExtractUnroll words' loads
+// issued stage by stage — stage 1 (word loads) for all of them, then stage 2 (per-lane loads
+// that depend on the words, under a per-lane condition) for all of them, then the uses.  A
+// conditional load whose value is used right away made the compiler wait for every load in
+// flight, so the unrolled words of a plain probe ran one dependent chain after the other.
+template <int kStreams, class Probe>
+__device__ __forceinline__ void extract_count_staged(int64_t first, int64_t end, const Probe& probe, int64_t& count,
+                                                     int64_t& dsum, unsigned long long& mask, bool& touch) {
+    int64_t wd = first;
+    int idx = 0;
+    for (; wd < end; wd += kExtractUnroll * kWavesPerBlock, idx += kExtractUnroll) {
+        typename Probe::State st[kExtractUnroll];
+        bool in[kExtractUnroll];
+#pragma unroll
+        for (int u = 0; u < kExtractUnroll; ++u) {
+            in[u] = wd + u * kWavesPerBlock < end;                // wave-uniform
+            probe.stage1(in[u] ? wd + u * kWavesPerBlock : first, st[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < kExtractUnroll; ++u) probe.stage2(in[u] ? wd + u * kWavesPerBlock : first, st[u]);
+#pragma unroll
+        for (int u = 0; u < kExtractUnroll; ++u) {
+            if (!in[u]) continue;
+            Take t[kStreams];
+            if (probe.finish(wd + u * kWavesPerBlock, st[u], t, false)) { touch = true; if (idx + u < 64) mask |= 1ULL << (idx + u); }
+            for (int k = 0; k < kStreams; ++k)
+                if (t[k].take) { ++count; dsum += t[k].deg; }
+        }
+    }
+}
+template <int kStreams, class Probe, class Emit>
+__device__ __forceinline__ void extract_write_staged(int64_t first, int64_t end, unsigned long long mask, const Probe& probe,
+                                                     const Emit& emit) {
+    const int64_t nwords = end > first ? (end - first + kWavesPerBlock - 1) / kWavesPerBlock : 0;
+    const bool all = nwords > 64;
+    int64_t next = 0;
+    for (;;) {
+        int64_t wl[kExtractUnroll];
+        bool any = false;
+#pragma unroll
+        for (int u = 0; u < kExtractUnroll; ++u) {
+            wl[u] = -1;
+            if (all) {
+                if (next < nwords) wl[u] = first + (next++) * kWavesPerBlock;
+            } else if (mask) {
+                const int b = __ffsll(static_cast<long long>(mask)) - 1;
+                mask &= mask - 1;
+                wl[u] = first + static_cast<int64_t>(b) * kWavesPerBlock;
+            }
+            any |= wl[u] >= 0;
+        }
+        if (!any) break;                      // wave-uniform
+        typename Probe::State st[kExtractUnroll];
+#pragma unroll
+        for (int u = 0; u < kExtractUnroll; ++u) probe.stage1(wl[u] >= 0 ? wl[u] : first, st[u]);
+#pragma unroll
+        for (int u = 0; u < kExtractUnroll; ++u) probe.stage2(wl[u] >= 0 ? wl[u] : first, st[u]);
+        Take t[kExtractUnroll][kStreams];
+#pragma unroll
+        for (int u = 0; u < kExtractUnroll; ++u)
+            if (wl[u] >= 0) probe.finish(wl[u], st[u], t[u], true);
+#pragma unroll
+        for (int u = 0; u < kExtractUnroll; ++u)
+            if (wl[u] >= 0) emit(t[u]);
+    }
+}
+
 template <int kStreams, class Probe>
 __device__ __forceinline__ void chunk_extract(int64_t words, const Probe& probe, int32_t* __restrict__ qn,
                                               int64_t* __restrict__ qdeg, Counters* cnt) {
