@@ -291,14 +291,7 @@ __global__ void __launch_bounds__(kBlock) ds_relax_ws_staged(const int64_t* __re
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int64_t t0 = tile * kTileEdges;
         const int64_t t1 = min(total, t0 + kTileEdges);
-        if (threadIdx.x == 0) {             // lo = last i with qpre[i] <= t0; hi = last i with qpre[i] <= t1-1
-            int64_t a = 0, b = qlen;
-            while (b - a > 1) { const int64_t m = (a + b) >> 1; if (qpre[m] <= t0) a = m; else b = m; }
-            s_lo = a;
-            int64_t a2 = a, b2 = qlen;
-            while (b2 - a2 > 1) { const int64_t m = (a2 + b2) >> 1; if (qpre[m] <= t1 - 1) a2 = m; else b2 = m; }
-            s_hi = a2;
-        }
+        tile_bounds(qpre, qlen, t0, t1, s_lo, s_hi);   // lo = last i with qpre[i] <= t0; hi = last with <= t1-1
         __syncthreads();
         const int64_t qlo = s_lo, qhi = s_hi;
         const int64_t span = qhi - qlo + 1;

@@ -553,14 +553,7 @@ __device__ __forceinline__ void relax_body(int64_t bid, int64_t nb, const int64_
         const int64_t t0 = tile * (kBlock * kE);
         const int64_t t1 = min(total, t0 + (kBlock * kE));
         if (kBins && threadIdx.x < kDsMaxBins) s_bn[threadIdx.x] = 0;
-        if (threadIdx.x == 0) {             // lo = last i with pre(i) <= t0; hi = last i with pre(i) <= t1-1
-            int64_t a = 0, b = qlen;
-            while (b - a > 1) { const int64_t m = (a + b) >> 1; if (qpre[m] <= t0) a = m; else b = m; }
-            s_lo = a;
-            int64_t a2 = a, b2 = qlen;
-            while (b2 - a2 > 1) { const int64_t m = (a2 + b2) >> 1; if (qpre[m] <= t1 - 1) a2 = m; else b2 = m; }
-            s_hi = a2;
-        }
+        tile_bounds(qpre, qlen, t0, t1, s_lo, s_hi);   // lo = last i with pre(i) <= t0; hi = last with <= t1-1
         __syncthreads();
         const int64_t lo = s_lo, hi = s_hi;
         const int64_t span = hi - lo + 1;

@@ -38,6 +38,32 @@ __device__ __forceinline__ void entry_at(const View& v, int64_t u, int64_t o, in
     }
 }
 
+// A tile's queue bounds, by one whole wave: the last i in [a, b) with pre[i] <= key, given
+// pre[a] <= key and pre nondecreasing — 64 probes a round (log64 rounds) instead of a lane-0
+// binary search (~20 dependent loads a tile while the block waits at its barrier).  Every lane
+// of the calling wave gets the result.
+__device__ __forceinline__ int64_t wave_last_le(const int64_t* __restrict__ pre, int64_t a, int64_t b, int64_t key) {
+    while (b - a > 1) {                                   // wave-uniform
+        const int64_t step = (b - a + 63) >> 6;
+        const int64_t pos = a + static_cast<int64_t>(threadIdx.x & 63) * step;
+        const bool le = pos < b && pre[pos < b ? pos : a] <= key;
+        const unsigned long long m = __ballot(le);       // a prefix of the lanes; lane 0 always
+        const int k = 63 - __clzll(static_cast<long long>(m));
+        a += static_cast<int64_t>(k) * step;
+        b = min(b, a + step);
+    }
+    return a;
+}
+// lo = last i with pre[i] <= t0, hi = last i with pre[i] <= t1 - 1, by the block's first wave
+__device__ __forceinline__ void tile_bounds(const int64_t* __restrict__ pre, int64_t n, int64_t t0, int64_t t1,
+                                            int64_t& s_lo, int64_t& s_hi) {
+    if (threadIdx.x < 64) {
+        const int64_t lo = wave_last_le(pre, 0, n, t0);
+        const int64_t hi = wave_last_le(pre, lo, n, t1 - 1);
+        if (threadIdx.x == 0) { s_lo = lo; s_hi = hi; }
+    }
+}
+
 // Edge-balanced load-balanced search (Merrill et al., PPoPP'12) over a queue q[0..qlen) whose
 // entries' edge counts have the exclusive scan qpre[0..qlen] (qpre[qlen] = total).  The edge
 // space is cut into kTileEdges tiles; a block stages the scan entries its tile touches in
@@ -57,14 +83,7 @@ __device__ __forceinline__ void for_each_queue_edge(const int32_t* __restrict__ 
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int64_t t0 = tile * kTileEdges;
         const int64_t t1 = min(total, t0 + kTileEdges);
-        if (threadIdx.x == 0) {             // lo = last i with qpre[i] <= t0; hi = last i with qpre[i] <= t1-1
-            int64_t a = 0, b = qlen;
-            while (b - a > 1) { const int64_t c = (a + b) >> 1; if (qpre[c] <= t0) a = c; else b = c; }
-            s_lo = a;
-            int64_t a2 = a, b2 = qlen;
-            while (b2 - a2 > 1) { const int64_t c = (a2 + b2) >> 1; if (qpre[c] <= t1 - 1) a2 = c; else b2 = c; }
-            s_hi = a2;
-        }
+        tile_bounds(qpre, qlen, t0, t1, s_lo, s_hi);   // lo = last i with qpre[i] <= t0; hi = last with <= t1-1
         __syncthreads();
         const int64_t lo = s_lo, hi = s_hi;
         const int64_t span = hi - lo + 1;   // queue entries touching this tile

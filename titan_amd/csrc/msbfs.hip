@@ -489,14 +489,7 @@ __global__ void __launch_bounds__(kBlock) ms_push(View push, const int32_t* __re
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int64_t t0 = tile * (kBlock * kE);
         const int64_t t1 = min(total, t0 + (kBlock * kE));
-        if (threadIdx.x == 0) {
-            int64_t a = 0, b = qlen;
-            while (b - a > 1) { const int64_t c = (a + b) >> 1; if (qpre[c] <= t0) a = c; else b = c; }
-            s_lo = a;
-            int64_t a2 = a, b2 = qlen;
-            while (b2 - a2 > 1) { const int64_t c = (a2 + b2) >> 1; if (qpre[c] <= t1 - 1) a2 = c; else b2 = c; }
-            s_hi = a2;
-        }
+        tile_bounds(qpre, qlen, t0, t1, s_lo, s_hi);
         __syncthreads();
         const int64_t lo = s_lo, hi = s_hi;
         const int64_t span = hi - lo + 1;
@@ -649,14 +642,7 @@ __global__ void __launch_bounds__(kBlock) ms_push_ranged(View push, const int32_
     for (int64_t tile = tlo + (blockIdx.x >> 3); tile < thi; tile += per) {   // block-uniform trips
         const int64_t t0 = tile * kTileEdges;
         const int64_t t1 = min(total, t0 + kTileEdges);
-        if (threadIdx.x == 0) {
-            int64_t a = 0, b = npairs;
-            while (b - a > 1) { const int64_t c = (a + b) >> 1; if (pre[c] <= t0) a = c; else b = c; }
-            s_lo = a;
-            int64_t a2 = a, b2 = npairs;
-            while (b2 - a2 > 1) { const int64_t c = (a2 + b2) >> 1; if (pre[c] <= t1 - 1) a2 = c; else b2 = c; }
-            s_hi = a2;
-        }
+        tile_bounds(pre, npairs, t0, t1, s_lo, s_hi);
         __syncthreads();
         const int64_t lo = s_lo, hi = s_hi;
         const int64_t span = hi - lo + 1;
