@@ -381,7 +381,7 @@ struct ColdBlocks {
     int64_t fx_nlong = 0;
     int32_t* fx_long_row = nullptr;     // rows longer than a tile
     unsigned long long* fx_long_acc = nullptr;   // 2 per long row (low, high word), zero between updates
-    // source-split hot pass (TGO_PR_FX_SPLIT = S): S launches over S ranges of the hot sources, so
+    // source-split hot pass (TGO_PR_FX_SPLIT = S, off by default since round 6): S launches over S ranges of the hot sources, so
     // each launch's messages fit an XCD's L2; the row sums carried between them in fx_part
     int fx_split = 0;
     int64_t* fx_mid = nullptr;          // (S + 1) per tile: its entry bounds of the source ranges
