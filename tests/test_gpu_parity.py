@@ -862,6 +862,13 @@ def test_pagerank_out_of_range_parameters(rmat12, monkeypatch):
     pr = eng.pagerank(0.85, n, 6)                      # back in range: the fixed-point passes
     assert eng.stats()["exact_reruns"] == 0
     assert np.abs(pr - oracle.pagerank(0.85, n, 6)[0]).sum() <= PR_L1_TOL
+    # a damping factor above 1 (the reference takes any alpha, PageRankVertexProgram.java:86)
+    # grows the ranks past the split words' exact range (|v| < 2^11, spmv.hip fx_hl) within the
+    # run: the emission guard flags the first contribution out of range and the program re-runs
+    pr = eng.pagerank(3.0, 1, 16)
+    opr = oracle.pagerank(3.0, 1, 16)[0]
+    assert eng.stats()["exact_reruns"] == 1 and np.abs(opr).max() > 2.0 ** 20
+    assert np.allclose(pr, opr, rtol=1e-12, atol=0)
 
 
 def test_rows_with_sort_key_weights_and_string_properties():
