@@ -3593,6 +3593,20 @@ int part_sssp_header_fold(tgo_ctx* ctx, const int64_t* own, const int64_t* recv,
     HIP_TRY(k_ds_header_fold(own, recv, nranks, out, ctx->stream));
     return TGO_OK;
 }
+// ... and its 2 * nranks + 3 words to the host in the same launch (through the mapped counter
+// page: part_read_words without its own publish kernel).
+int part_sssp_header_read(tgo_ctx* ctx, const int64_t* own, const int64_t* recv, int nranks, int64_t* out,
+                          int64_t* words) {
+    Scratch& s = ctx->sc;
+    const int count = 2 * nranks + 3;
+    if (!s.hcnt || count > kCounterWords) return fail(ctx, TGO_E_STATE, "part_sssp_header_read");
+    const unsigned long long seq = ++s.pub_seq;
+    HIP_TRY(k_ds_header_fold(own, recv, nranks, out, ctx->stream, s.hcnt_dev, seq));
+    if (int rc = wait_publish(ctx, seq)) return rc;
+    const volatile unsigned long long* w = reinterpret_cast<volatile unsigned long long*>(s.hcnt);
+    for (int i = 0; i < count; ++i) words[i] = static_cast<int64_t>(w[i]);
+    return TGO_OK;
+}
 // Switch the run tgo_part_sssp_begin started onto the light/heavy split at bucket width delta
 // (weighted loads; TGO_DS_SPLIT=0 keeps the plain form): the push view is split on the device
 // (once per width), and the seed re-queued with its light degree.  Returns whether it did.
@@ -3652,7 +3666,9 @@ int part_sssp_split(tgo_ctx* ctx, int64_t delta, bool* on) {
 bool part_sssp_devloop(const tgo_ctx* ctx) { return ctx->part_devloop; }
 // One phase of the device-sized loop, relax half: commit + relax of the current queue (remote
 // targets marked), then the exchange header (sizes, 4 words per rank) and the pack.
-int part_sssp_dev_relax(tgo_ctx* ctx, int32_t nranks, int64_t* send, int64_t* sizes) {
+// fold (one rank only, may be null): the header's fold (part_sssp_header_read's 5 words) read
+// here — one rank's header all-to-all is the identity, so the header kernel publishes it.
+int part_sssp_dev_relax(tgo_ctx* ctx, int32_t nranks, int64_t* send, int64_t* sizes, int64_t* fold) {
     DevGraph& g = ctx->g;
     Scratch& s = ctx->sc;
     hipStream_t st = ctx->stream;
@@ -3665,6 +3681,15 @@ int part_sssp_dev_relax(tgo_ctx* ctx, int32_t nranks, int64_t* send, int64_t* si
     unsigned long long* cursor = offs + kMaxRanks;
     const int64_t words = g.n_global / 64, wpr = g.n / 64;
     if (nranks > 1) HIP_TRY(k_ds_mark_count(s.ds_rmark, words, wpr, counts, st));   // one rank marks nothing
+    if (fold) {
+        if (nranks != 1 || !s.hcnt) return fail(ctx, TGO_E_STATE, "part_sssp_dev_relax: fold");
+        const unsigned long long seq = ++s.pub_seq;
+        HIP_TRY(k_ds_part_header(counts, nranks, s.ds_loop, ctx->part_cur, offs, cursor, sizes, st, s.hcnt_dev, seq));
+        if (int rc = wait_publish(ctx, seq)) return rc;
+        const volatile unsigned long long* w = reinterpret_cast<volatile unsigned long long*>(s.hcnt);
+        for (int i = 0; i < 5; ++i) fold[i] = static_cast<int64_t>(w[i]);
+        return TGO_OK;
+    }
     HIP_TRY(k_ds_part_header(counts, nranks, s.ds_loop, ctx->part_cur, offs, cursor, sizes, st));
     if (nranks > 1) HIP_TRY(k_ds_mark_pack(s.ds_rmark, words, wpr, g.n, s.ds_rbest, offs, cursor, send, st));
     return TGO_OK;

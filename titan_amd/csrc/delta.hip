@@ -641,8 +641,10 @@ __global__ void ds_track_reset(long long* __restrict__ track) {
 // header to this rank {pair elements, near-queue length, track[0], track[1]}.  out (2W + 3
 // words, read by the host in one go): pair elements sent to / received from each rank, then
 // the global near-queue length, pending minimum and -(ranks with members).
+// host (may be null): the same words also go to the host-mapped counter page, then the sequence
+// word (publish_words' protocol) — the fold and its publish in one launch.
 __global__ void ds_header_fold(const int64_t* __restrict__ own, const int64_t* __restrict__ recv, int nranks,
-                               int64_t* __restrict__ out) {
+                               int64_t* __restrict__ out, unsigned long long* host, unsigned long long seq) {
     if (threadIdx.x != 0) return;
     int64_t gq = 0, pm = INT64_MAX, mem = 0;
     for (int r = 0; r < nranks; ++r) {
@@ -655,6 +657,17 @@ __global__ void ds_header_fold(const int64_t* __restrict__ own, const int64_t* _
     out[2 * nranks] = gq;
     out[2 * nranks + 1] = pm;
     out[2 * nranks + 2] = mem;
+    if (!host) return;
+    for (int r = 0; r < nranks; ++r) {
+        __hip_atomic_store(&host[r], static_cast<unsigned long long>(own[4 * r]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&host[nranks + r], static_cast<unsigned long long>(recv[4 * r]), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    __hip_atomic_store(&host[2 * nranks], static_cast<unsigned long long>(gq), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&host[2 * nranks + 1], static_cast<unsigned long long>(pm), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&host[2 * nranks + 2], static_cast<unsigned long long>(mem), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __threadfence_system();
+    __hip_atomic_store(&host[kCounterWords], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // The exchange header on the device (no host round trip): offs[r] = the pack offset of rank r's
@@ -805,8 +818,10 @@ hipError_t k_ds_track_reset(long long* track, hipStream_t s) {
     ds_track_reset<<<1, 64, 0, s>>>(track);
     return hipGetLastError();
 }
-hipError_t k_ds_header_fold(const int64_t* own, const int64_t* recv, int nranks, int64_t* out, hipStream_t s) {
-    ds_header_fold<<<1, 64, 0, s>>>(own, recv, nranks, out);
+hipError_t k_ds_header_fold(const int64_t* own, const int64_t* recv, int nranks, int64_t* out, hipStream_t s,
+                            unsigned long long* host, unsigned long long seq) {
+    if (host && 2 * nranks + 3 > kCounterWords) return hipErrorInvalidValue;
+    ds_header_fold<<<1, 64, 0, s>>>(own, recv, nranks, out, host, seq);
     return hipGetLastError();
 }
 hipError_t k_ds_extract(const View& push, uint64_t* pend, int64_t n, const int64_t* dist, int64_t thr, int32_t* qn,

@@ -130,6 +130,8 @@ __global__ void ds_loop_seed(const int64_t* off, const int64_t* light, int64_t* 
     L->cur = 0;
     L->big = 0;
     L->small_steps = 0;
+    L->lo_next = kInf;
+    L->xnew = 0;
 }
 
 __device__ __forceinline__ unsigned long long load_agent(const unsigned long long* p) {
@@ -271,7 +273,7 @@ __device__ __forceinline__ void chunk_extract_packed(int64_t words, const Probe&
 }
 
 // chunk_extract_packed over a staged probe (frontier.hpp extract_count_staged)
-template <int kStreams, class Probe>
+template <int kStreams, class Probe, int kU = kExtractUnroll>
 __device__ __forceinline__ void chunk_extract_packed_staged(int64_t words, const Probe& probe, int32_t* __restrict__ qn,
                                                             int64_t* __restrict__ qpre, unsigned long long* qc) {
     const int64_t per = ((words + gridDim.x - 1) / gridDim.x + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock;
@@ -282,13 +284,13 @@ __device__ __forceinline__ void chunk_extract_packed_staged(int64_t words, const
     int64_t count = 0, dsum = 0;
     unsigned long long mask = 0;
     bool touch = false;
-    if (w0 + wave < w1) extract_count_staged<kStreams>(w0 + wave, w1, probe, count, dsum, mask, touch);
+    if (w0 + wave < w1) extract_count_staged<kStreams, Probe, kU>(w0 + wave, w1, probe, count, dsum, mask, touch);
     const int64_t wc = wave_incl_scan(count), wdg = wave_incl_scan(dsum);
     int64_t slot0, doff0;
     block_reserve(qc, lane() == 63 ? wc : 0, lane() == 63 ? wdg : 0, slot0, doff0);
     int64_t cursor = __shfl(slot0, 63, 64), dcur = __shfl(doff0, 63, 64);
     if (!touch) return;                                      // wave-uniform
-    extract_write_staged<kStreams>(w0 + wave, w1, mask, probe, [&](const Take* t) {
+    const auto emit = [&](const Take* t) {
         for (int k = 0; k < kStreams; ++k) {
             const unsigned long long bm = __ballot(t[k].take);
             if (!bm) continue;
@@ -302,7 +304,8 @@ __device__ __forceinline__ void chunk_extract_packed_staged(int64_t words, const
             cursor += __popcll(bm);
             dcur += __shfl(id, 63, 64);
         }
-    });
+    };
+    extract_write_staged<kStreams, Probe, decltype(emit), kU>(w0 + wave, w1, mask, probe, emit);
 }
 
 // The bitmap-scan extraction's probe in stages: the pending / member words, then each lane's
@@ -344,25 +347,27 @@ struct ScanProbe {
 };
 
 // done (binned loop, may be null): when the decision found the bucket finished (L->xfin), the
-// members taken here are final and become done.
+// members taken here are final and become done.  The smallest distance left pending is
+// min-reduced into *lo (L->lo, or L->lo_next for the partitioned loop).
+template <int kU = kExtractUnroll>
 __device__ __forceinline__ void extract_scan(const int64_t* __restrict__ off, const int64_t* __restrict__ light,
         uint64_t* __restrict__ pend, uint64_t* __restrict__ member, int64_t n, const int64_t* __restrict__ dist,
-        DsLoop* L, int cur, int32_t* __restrict__ qn, int64_t* __restrict__ qpre, uint64_t* __restrict__ done) {
-    const int64_t thr = L->thr;
+        DsLoop* L, int cur, int32_t* __restrict__ qn, int64_t* __restrict__ qpre, uint64_t* __restrict__ done,
+        int64_t thr, long long* lo) {
     uint64_t* const fin = (done && L->xfin) ? done : nullptr;
     const int64_t words = (n + 63) >> 6;
     long long left = kInf;                                   // smallest distance left pending
     const ScanProbe probe{off, light, pend, member, dist, fin, thr, &left};
-    chunk_extract_packed_staged<2>(words, probe, qn, qpre, &L->qc[cur]);
+    chunk_extract_packed_staged<2, ScanProbe, kU>(words, probe, qn, qpre, &L->qc[cur]);
     const long long m = block_min(left);
-    if (threadIdx.x == 0 && m != kInf) atomicMin(&L->lo, m);
+    if (threadIdx.x == 0 && m != kInf) atomicMin(lo, m);
 }
 
 __global__ void __launch_bounds__(kBlock) ds_extract_dev(const int64_t* __restrict__ off,
         const int64_t* __restrict__ light, uint64_t* __restrict__ pend, uint64_t* __restrict__ member, int64_t n,
         const int64_t* __restrict__ dist, DsLoop* L, int cur, int32_t* __restrict__ qn, int64_t* __restrict__ qpre) {
     if (L->extract != 1) return;                             // grid-uniform
-    extract_scan(off, light, pend, member, n, dist, L, cur, qn, qpre, nullptr);
+    extract_scan(off, light, pend, member, n, dist, L, cur, qn, qpre, nullptr, L->thr, &L->lo);
 }
 
 // The binned extraction (extract == 2): the decided pile's entries — a vertex is taken when it
@@ -439,7 +444,7 @@ __global__ void __launch_bounds__(kBlock) ds_extract_bins(const int64_t* __restr
         int64_t* __restrict__ qpre, int64_t n, DsPull pull) {
     const unsigned long long mode = L->extract;             // grid-uniform
     if (mode == 1) {                                         // a large or overflowed pile: the bitmap scan
-        extract_scan(off, light, pend, member, n, dist, L, cur, qn, qpre, done);
+        extract_scan(off, light, pend, member, n, dist, L, cur, qn, qpre, done, L->thr, &L->lo);
         return;
     }
     if (mode != 2) return;
@@ -803,25 +808,44 @@ __global__ void __launch_bounds__(kBlock) ds_part_apply(const int64_t* __restric
     if (threadIdx.x == 0 && m != kInf) atomicMin(&L->tm, m);
 }
 
-// The global decision of an empty phase (host: every near queue empty): extract below thr.
-__global__ void ds_part_decide(DsLoop* L, int64_t thr) {
-    if (threadIdx.x != 0) return;
-    if (thr > L->thr) L->buckets += 1;
-    L->thr = thr;
-    L->tm = kInf;
-    L->lo = kInf;
-    L->members = 0;
-    L->extract = 1;
-    L->extractions += 1;
+// The global decision of an empty phase (host: every near queue empty) and its extraction below
+// thr, in one launch: block 0 books the decision (none of it is read by the extraction, which
+// takes thr as an argument), the blocks min their pending distances into lo_next, and the next
+// header (ds_part_header, after every block has finished) moves it into lo.  (A separate
+// one-thread decision launch cost ~10 us a bucket.)
+template <int kU>
+__global__ void __launch_bounds__(kBlock) ds_part_extract(const int64_t* __restrict__ off,
+        const int64_t* __restrict__ light, uint64_t* __restrict__ pend, uint64_t* __restrict__ member, int64_t n,
+        const int64_t* __restrict__ dist, DsLoop* L, int cur, int32_t* __restrict__ qn, int64_t* __restrict__ qpre,
+        int64_t thr) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (thr > L->thr) L->buckets += 1;
+        L->thr = thr;
+        L->tm = kInf;
+        L->members = 0;
+        L->extract = 1;
+        L->extractions += 1;
+        L->xnew = 1;
+    }
+    extract_scan<kU>(off, light, pend, member, n, dist, L, cur, qn, qpre, nullptr, thr, &L->lo_next);
 }
 
 // The exchange header (delta.hip ds_mark_sizes for this loop): offs[r] = the pack offset of
 // rank r's pairs; to r {pair elements, near-queue length, min(tm, lo), members}.  Zeroes the
 // counts for the next phase and the pack's cursors.
-__global__ void ds_part_header(unsigned long long* __restrict__ counts, int nranks, const DsLoop* L, int cur,
+// host (one rank only, may be null): the header all-to-all of one rank is the identity, so the
+// fold (delta.hip ds_header_fold: sent / received elements, queue length, pending minimum,
+// -members) goes straight to the host-mapped counter page with its sequence word — one launch
+// where the exchange takes three (header, all-to-all copy, fold + publish).
+__global__ void ds_part_header(unsigned long long* __restrict__ counts, int nranks, DsLoop* L, int cur,
                                unsigned long long* __restrict__ offs, unsigned long long* __restrict__ cursor,
-                               int64_t* __restrict__ sizes) {
+                               int64_t* __restrict__ sizes, unsigned long long* host, unsigned long long seq) {
     if (threadIdx.x != 0) return;
+    if (L->xnew) {                       // the pending minimum of the extraction since the last header
+        L->lo = L->lo_next;
+        L->lo_next = kInf;
+        L->xnew = 0;
+    }
     const int64_t qlen = qcount(L->qc[cur]);
     const long long pm = L->tm < L->lo ? L->tm : L->lo;
     const int64_t mem = L->members ? 1 : 0;
@@ -837,6 +861,13 @@ __global__ void ds_part_header(unsigned long long* __restrict__ counts, int nran
         counts[r] = 0;
         cursor[r] = 0;
     }
+    if (!host || nranks != 1) return;
+    const unsigned long long w[5] = {static_cast<unsigned long long>(sizes[0]), static_cast<unsigned long long>(sizes[0]),
+                                     static_cast<unsigned long long>(qlen), static_cast<unsigned long long>(pm),
+                                     static_cast<unsigned long long>(-mem)};
+    for (int i = 0; i < 5; ++i) __hip_atomic_store(&host[i], w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __threadfence_system();
+    __hip_atomic_store(&host[kCounterWords], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // The pull form of a large finished bucket's heavy entries: a vertex that can still improve
@@ -1065,7 +1096,7 @@ __global__ void __launch_bounds__(kBlock) ds_extract_dc(const int64_t* __restric
     const int cur = static_cast<int>(L->cur);
     const unsigned long long mode = L->extract;
     if (mode == 1) {
-        extract_scan(off, light, pend, member, n, dist, L, cur, qs.q(cur), qs.qp(cur), done);
+        extract_scan(off, light, pend, member, n, dist, L, cur, qs.q(cur), qs.qp(cur), done, L->thr, &L->lo);
         return;
     }
     if (mode != 2) return;
@@ -1128,9 +1159,11 @@ hipError_t k_ds_part_relax(const DevCsr& ws, const int64_t* light, uint64_t* pen
                                                          nullptr, lo, n_local, rbest, rmark);
     return hipGetLastError();
 }
-hipError_t k_ds_part_header(unsigned long long* counts, int nranks, const DsLoop* L, int cur, unsigned long long* offs,
-                            unsigned long long* cursor, int64_t* sizes, hipStream_t s) {
-    ds_part_header<<<1, 64, 0, s>>>(counts, nranks, L, cur, offs, cursor, sizes);
+hipError_t k_ds_part_header(unsigned long long* counts, int nranks, DsLoop* L, int cur, unsigned long long* offs,
+                            unsigned long long* cursor, int64_t* sizes, hipStream_t s, unsigned long long* host,
+                            unsigned long long seq) {
+    if (host && nranks != 1) return hipErrorInvalidValue;
+    ds_part_header<<<1, 64, 0, s>>>(counts, nranks, L, cur, offs, cursor, sizes, host, seq);
     return hipGetLastError();
 }
 hipError_t k_ds_part_apply(const int64_t* recv, int64_t npairs, const DevCsr& ws, const int64_t* light, int64_t* dist,
@@ -1144,9 +1177,12 @@ hipError_t k_ds_part_apply(const int64_t* recv, int64_t npairs, const DevCsr& ws
 hipError_t k_ds_part_extract(const DevCsr& ws, const int64_t* light, uint64_t* pend, uint64_t* member, int64_t n,
                              int64_t* dist, int32_t* const q[2], int64_t* const qpre[2], DsLoop* L, int cur, int64_t thr,
                              hipStream_t s) {
-    ds_part_decide<<<1, 64, 0, s>>>(L, thr);
     const int64_t words = (n + 63) / 64;
-    ds_extract_dev<<<extract_grid(words), kBlock, 0, s>>>(ws.off, light, pend, member, n, dist, L, cur, q[cur], qpre[cur]);
+    // two words a wave in flight (profiles/r06pq_part_sssp_scan_ab.log, r06pr_*: summed over 3
+    // roots at world 1, 1 / 2 / 4 / 8 words 35.9 / 34.2-34.5 / 34.8-35.0 / 38.0 ms; grid 1024 / 4096 with 2
+    // words 38.4 / 35.2: extract_grid's 2048 kept)
+    ds_part_extract<2><<<extract_grid(words), kBlock, 0, s>>>(ws.off, light, pend, member, n, dist, L, cur, q[cur],
+                                                              qpre[cur], thr);
     return hipGetLastError();
 }
 

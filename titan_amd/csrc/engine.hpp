@@ -536,6 +536,10 @@ struct DsLoop {
     unsigned long long cur;
     unsigned long long big;
     unsigned long long small_steps;       // steps the single-block kernel ran
+    // partitioned loop (ds_part_extract): the extraction's pending minimum, moved into lo by
+    // the next header (after every block of the extraction has added to it)
+    long long lo_next;
+    unsigned long long xnew;    // an extraction ran since the last header
 };
 
 struct Scratch {
@@ -687,8 +691,9 @@ hipError_t k_ds_loop_step(const DevCsr& ws, const int64_t* light, uint64_t* pend
 hipError_t k_ds_part_relax(const DevCsr& ws, const int64_t* light, uint64_t* pend, uint64_t* member, int64_t* dist,
                            int64_t* msg, int32_t* const q[2], int64_t* const qpre[2], DsLoop* L, int cur, int64_t delta,
                            int64_t lo, int64_t n_local, int64_t* rbest, uint64_t* rmark, hipStream_t s);
-hipError_t k_ds_part_header(unsigned long long* counts, int nranks, const DsLoop* L, int cur, unsigned long long* offs,
-                            unsigned long long* cursor, int64_t* sizes, hipStream_t s);
+hipError_t k_ds_part_header(unsigned long long* counts, int nranks, DsLoop* L, int cur, unsigned long long* offs,
+                            unsigned long long* cursor, int64_t* sizes, hipStream_t s, unsigned long long* host = nullptr,
+                            unsigned long long seq = 0);
 hipError_t k_ds_part_apply(const int64_t* recv, int64_t npairs, const DevCsr& ws, const int64_t* light, int64_t* dist,
                            uint64_t* pend, int32_t* const q[2], int64_t* const qpre[2], DsLoop* L, int cur, hipStream_t s);
 hipError_t k_ds_part_extract(const DevCsr& ws, const int64_t* light, uint64_t* pend, uint64_t* member, int64_t n,
@@ -722,7 +727,8 @@ hipError_t k_ds_pending_min(const uint64_t* pend, int64_t words, const int64_t* 
 // partitioned loop state (delta.hip ds_track_reset): reset before an extraction; the header
 // all-to-all's result folded into {sent W, received W, global queue, pending min, -members}
 hipError_t k_ds_track_reset(long long* track, hipStream_t s);
-hipError_t k_ds_header_fold(const int64_t* own, const int64_t* recv, int nranks, int64_t* out, hipStream_t s);
+hipError_t k_ds_header_fold(const int64_t* own, const int64_t* recv, int nranks, int64_t* out, hipStream_t s,
+                            unsigned long long* host = nullptr, unsigned long long seq = 0);
 hipError_t k_ds_extract(const View& push, uint64_t* pend, int64_t n, const int64_t* dist, int64_t thr, int32_t* qn,
                         int64_t* qdeg, Counters* cnt, hipStream_t s, long long* track = nullptr);
 hipError_t k_ds_relax_part(const View& push, const int32_t* q, const int64_t* qpre, int64_t qlen, const int64_t* msg,

@@ -251,23 +251,23 @@ __device__ __forceinline__ void extract_write(int64_t first, int64_t end, unsign
 // that depend on the words, under a per-lane condition) for all of them, then the uses.  A
 // conditional load whose value is used right away made the compiler wait for every load in
 // flight, so the unrolled words of a plain probe ran one dependent chain after the other.
-template <int kStreams, class Probe>
+template <int kStreams, class Probe, int kU = kExtractUnroll>
 __device__ __forceinline__ void extract_count_staged(int64_t first, int64_t end, const Probe& probe, int64_t& count,
                                                      int64_t& dsum, unsigned long long& mask, bool& touch) {
     int64_t wd = first;
     int idx = 0;
-    for (; wd < end; wd += kExtractUnroll * kWavesPerBlock, idx += kExtractUnroll) {
-        typename Probe::State st[kExtractUnroll];
-        bool in[kExtractUnroll];
+    for (; wd < end; wd += kU * kWavesPerBlock, idx += kU) {
+        typename Probe::State st[kU];
+        bool in[kU];
 #pragma unroll
-        for (int u = 0; u < kExtractUnroll; ++u) {
+        for (int u = 0; u < kU; ++u) {
             in[u] = wd + u * kWavesPerBlock < end;                // wave-uniform
             probe.stage1(in[u] ? wd + u * kWavesPerBlock : first, st[u]);
         }
 #pragma unroll
-        for (int u = 0; u < kExtractUnroll; ++u) probe.stage2(in[u] ? wd + u * kWavesPerBlock : first, st[u]);
+        for (int u = 0; u < kU; ++u) probe.stage2(in[u] ? wd + u * kWavesPerBlock : first, st[u]);
 #pragma unroll
-        for (int u = 0; u < kExtractUnroll; ++u) {
+        for (int u = 0; u < kU; ++u) {
             if (!in[u]) continue;
             Take t[kStreams];
             if (probe.finish(wd + u * kWavesPerBlock, st[u], t, false)) { touch = true; if (idx + u < 64) mask |= 1ULL << (idx + u); }
@@ -276,17 +276,17 @@ __device__ __forceinline__ void extract_count_staged(int64_t first, int64_t end,
         }
     }
 }
-template <int kStreams, class Probe, class Emit>
+template <int kStreams, class Probe, class Emit, int kU = kExtractUnroll>
 __device__ __forceinline__ void extract_write_staged(int64_t first, int64_t end, unsigned long long mask, const Probe& probe,
                                                      const Emit& emit) {
     const int64_t nwords = end > first ? (end - first + kWavesPerBlock - 1) / kWavesPerBlock : 0;
     const bool all = nwords > 64;
     int64_t next = 0;
     for (;;) {
-        int64_t wl[kExtractUnroll];
+        int64_t wl[kU];
         bool any = false;
 #pragma unroll
-        for (int u = 0; u < kExtractUnroll; ++u) {
+        for (int u = 0; u < kU; ++u) {
             wl[u] = -1;
             if (all) {
                 if (next < nwords) wl[u] = first + (next++) * kWavesPerBlock;
@@ -298,17 +298,17 @@ __device__ __forceinline__ void extract_write_staged(int64_t first, int64_t end,
             any |= wl[u] >= 0;
         }
         if (!any) break;                      // wave-uniform
-        typename Probe::State st[kExtractUnroll];
+        typename Probe::State st[kU];
 #pragma unroll
-        for (int u = 0; u < kExtractUnroll; ++u) probe.stage1(wl[u] >= 0 ? wl[u] : first, st[u]);
+        for (int u = 0; u < kU; ++u) probe.stage1(wl[u] >= 0 ? wl[u] : first, st[u]);
 #pragma unroll
-        for (int u = 0; u < kExtractUnroll; ++u) probe.stage2(wl[u] >= 0 ? wl[u] : first, st[u]);
-        Take t[kExtractUnroll][kStreams];
+        for (int u = 0; u < kU; ++u) probe.stage2(wl[u] >= 0 ? wl[u] : first, st[u]);
+        Take t[kU][kStreams];
 #pragma unroll
-        for (int u = 0; u < kExtractUnroll; ++u)
+        for (int u = 0; u < kU; ++u)
             if (wl[u] >= 0) probe.finish(wl[u], st[u], t[u], true);
 #pragma unroll
-        for (int u = 0; u < kExtractUnroll; ++u)
+        for (int u = 0; u < kU; ++u)
             if (wl[u] >= 0) emit(t[u]);
     }
 }

@@ -325,7 +325,9 @@ int part_sssp_relax_dev(tgo_ctx* ctx, int64_t thr, int32_t nranks, int64_t* send
 int part_sssp_header_fold(tgo_ctx* ctx, const int64_t* own, const int64_t* recv, int nranks, int64_t* out);
 int part_sssp_split(tgo_ctx* ctx, int64_t delta, bool* on);
 bool part_sssp_devloop(const tgo_ctx* ctx);
-int part_sssp_dev_relax(tgo_ctx* ctx, int32_t nranks, int64_t* send, int64_t* sizes);
+int part_sssp_dev_relax(tgo_ctx* ctx, int32_t nranks, int64_t* send, int64_t* sizes, int64_t* fold);
+int part_sssp_header_read(tgo_ctx* ctx, const int64_t* own, const int64_t* recv, int nranks, int64_t* out,
+                          int64_t* words);
 int part_sssp_dev_apply(tgo_ctx* ctx, const int64_t* recv, int64_t npairs);
 int part_sssp_dev_extract(tgo_ctx* ctx, int64_t thr);
 double ms_split_of(const tgo_ctx* ctx);
@@ -851,15 +853,24 @@ extern "C" int tgo_part_sssp_run(tgo_ctx* ctx, tgo_exchange* x, int64_t seed_glo
     const int nf = 2 * W + 3;
     std::vector<int64_t> hf(nf);
     std::vector<size_t> sb(W), so(W), rb(W), ro(W);
+    // One rank on the device loop: its header all-to-all is the identity, so the header kernel
+    // folds and publishes it in one launch (3 launches and a copy fewer per phase).  Up to 14
+    // ranks the fold publishes its own words (nf <= 32 counter-page words).
+    const bool solo = dev && W == 1;
     for (;;) {
         DevSpan span(st, "part.sssp.phase", {"phase", phases}, {"threshold", thr});
-        if ((rc = dev ? part_sssp_dev_relax(ctx, W, send, sizes) : part_sssp_relax_dev(ctx, thr, W, send, sizes))) break;
-        if (int r = x->all_to_all(sizes, hdr_recv, 32, st)) { rc = d.xfail(r); break; }
-        if ((rc = part_sssp_header_fold(ctx, sizes, hdr_recv, W, fold))) break;
-        if (nf <= 32) {                    // through the mapped counter page (up to 14 ranks)
-            if ((rc = part_read_words(ctx, fold, nf, hf.data()))) break;
-        } else if (hipMemcpyAsync(hf.data(), fold, nf * sizeof(int64_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
-                   hipStreamSynchronize(st) != hipSuccess) { rc = d.hip("header read"); break; }
+        if (solo) {
+            if ((rc = part_sssp_dev_relax(ctx, W, send, sizes, hf.data()))) break;
+        } else {
+            if ((rc = dev ? part_sssp_dev_relax(ctx, W, send, sizes, nullptr) : part_sssp_relax_dev(ctx, thr, W, send, sizes)))
+                break;
+            if (int r = x->all_to_all(sizes, hdr_recv, 32, st)) { rc = d.xfail(r); break; }
+            if (nf <= 32) {                // through the mapped counter page (up to 14 ranks)
+                if ((rc = part_sssp_header_read(ctx, sizes, hdr_recv, W, fold, hf.data()))) break;
+            } else if ((rc = part_sssp_header_fold(ctx, sizes, hdr_recv, W, fold)) ||
+                       hipMemcpyAsync(hf.data(), fold, nf * sizeof(int64_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                       hipStreamSynchronize(st) != hipSuccess) { if (!rc) rc = d.hip("header read"); break; }
+        }
         if (hf[2 * W] == 0) {   // every near queue was empty (nothing was relaxed): the next non-empty bucket
             span.end();
             const int64_t mn = hf[2 * W + 1];
