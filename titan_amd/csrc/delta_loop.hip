@@ -314,6 +314,8 @@ struct ScanProbe {
     const int64_t* off; const int64_t* light; uint64_t* pend; uint64_t* member; const int64_t* dist;
     uint64_t* fin; int64_t thr; long long* left;
     struct State { uint64_t pb, mb; long long d; int64_t o0, o1, lt; };
+    // a word with no pending and no member bit takes nothing and leaves nothing pending
+    __device__ __forceinline__ bool live(int64_t wd) const { return (pend[wd] | member[wd]) != 0; }
     __device__ __forceinline__ void stage1(int64_t wd, State& s) const {
         s.pb = pend[wd];                                      // uniform across the wave
         s.mb = member[wd];

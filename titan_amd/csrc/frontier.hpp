@@ -251,9 +251,46 @@ __device__ __forceinline__ void extract_write(int64_t first, int64_t end, unsign
 // that depend on the words, under a per-lane condition) for all of them, then the uses.  A
 // conditional load whose value is used right away made the compiler wait for every load in
 // flight, so the unrolled words of a plain probe ran one dependent chain after the other.
+// A wave of at most 64 words first asks which of them can take anything (Probe::live, one word
+// a lane, one load round trip) and runs the stages on those only: a sparse scan (the tail of a
+// run: a few pending vertices in 16 M) then costs one round trip a wave instead of one per kU
+// words.
 template <int kStreams, class Probe, int kU = kExtractUnroll>
 __device__ __forceinline__ void extract_count_staged(int64_t first, int64_t end, const Probe& probe, int64_t& count,
                                                      int64_t& dsum, unsigned long long& mask, bool& touch) {
+    const int64_t nwords = end > first ? (end - first + kWavesPerBlock - 1) / kWavesPerBlock : 0;
+    if (nwords <= 64) {
+        const int64_t mine = first + static_cast<int64_t>(lane()) * kWavesPerBlock;
+        unsigned long long live = __ballot(lane() < nwords && probe.live(lane() < nwords ? mine : first));
+        while (live) {                                            // wave-uniform
+            int64_t wl[kU];
+            int bi[kU];
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                bi[u] = -1;
+                wl[u] = first;
+                if (live) {
+                    bi[u] = __ffsll(static_cast<long long>(live)) - 1;
+                    live &= live - 1;
+                    wl[u] = first + static_cast<int64_t>(bi[u]) * kWavesPerBlock;
+                }
+            }
+            typename Probe::State st[kU];
+#pragma unroll
+            for (int u = 0; u < kU; ++u) probe.stage1(wl[u], st[u]);
+#pragma unroll
+            for (int u = 0; u < kU; ++u) probe.stage2(wl[u], st[u]);
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                if (bi[u] < 0) continue;
+                Take t[kStreams];
+                if (probe.finish(wl[u], st[u], t, false)) { touch = true; mask |= 1ULL << bi[u]; }
+                for (int k = 0; k < kStreams; ++k)
+                    if (t[k].take) { ++count; dsum += t[k].deg; }
+            }
+        }
+        return;
+    }
     int64_t wd = first;
     int idx = 0;
     for (; wd < end; wd += kU * kWavesPerBlock, idx += kU) {
