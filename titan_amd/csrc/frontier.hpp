@@ -251,17 +251,18 @@ __device__ __forceinline__ void extract_write(int64_t first, int64_t end, unsign
 // that depend on the words, under a per-lane condition) for all of them, then the uses.  A
 // conditional load whose value is used right away made the compiler wait for every load in
 // flight, so the unrolled words of a plain probe ran one dependent chain after the other.
-// A wave of at most 64 words first asks which of them can take anything (Probe::live, one word
-// a lane, one load round trip) and runs the stages on those only: a sparse scan (the tail of a
-// run: a few pending vertices in 16 M) then costs one round trip a wave instead of one per kU
-// words.
-template <int kStreams, class Probe, int kU = kExtractUnroll>
-__device__ __forceinline__ void extract_count_staged(int64_t first, int64_t end, const Probe& probe, int64_t& count,
-                                                     int64_t& dsum, unsigned long long& mask, bool& touch) {
-    const int64_t nwords = end > first ? (end - first + kWavesPerBlock - 1) / kWavesPerBlock : 0;
-    if (nwords <= 64) {
-        const int64_t mine = first + static_cast<int64_t>(lane()) * kWavesPerBlock;
-        unsigned long long live = __ballot(lane() < nwords && probe.live(lane() < nwords ? mine : first));
+// The wave's words in windows of 64: one word a lane asks which can take anything
+// (Probe::live, one load round trip a window), and the stages run on those only — a sparse
+// scan (the tail of a run: a few pending vertices in 16 M) costs a round trip a window instead
+// of one per kU words.  live_words calls visit(wl, bi, st) per kU live words (bi: index within
+// the wave's words, -1 for an unused slot, whose wl is `first`).
+template <class Probe, int kU, class Visit>
+__device__ __forceinline__ void live_words(int64_t first, int64_t nwords, const Probe& probe, const Visit& visit) {
+    for (int64_t w0 = 0; w0 < nwords; w0 += 64) {                // wave-uniform
+        const int64_t base = first + w0 * kWavesPerBlock;
+        const int64_t nw = nwords - w0 < 64 ? nwords - w0 : 64;
+        const bool in = lane() < nw;
+        unsigned long long live = __ballot(in && probe.live(in ? base + static_cast<int64_t>(lane()) * kWavesPerBlock : first));
         while (live) {                                            // wave-uniform
             int64_t wl[kU];
             int bi[kU];
@@ -270,9 +271,10 @@ __device__ __forceinline__ void extract_count_staged(int64_t first, int64_t end,
                 bi[u] = -1;
                 wl[u] = first;
                 if (live) {
-                    bi[u] = __ffsll(static_cast<long long>(live)) - 1;
+                    const int b = __ffsll(static_cast<long long>(live)) - 1;
                     live &= live - 1;
-                    wl[u] = first + static_cast<int64_t>(bi[u]) * kWavesPerBlock;
+                    bi[u] = static_cast<int>(w0) + b;
+                    wl[u] = base + static_cast<int64_t>(b) * kWavesPerBlock;
                 }
             }
             typename Probe::State st[kU];
@@ -280,61 +282,55 @@ __device__ __forceinline__ void extract_count_staged(int64_t first, int64_t end,
             for (int u = 0; u < kU; ++u) probe.stage1(wl[u], st[u]);
 #pragma unroll
             for (int u = 0; u < kU; ++u) probe.stage2(wl[u], st[u]);
-#pragma unroll
-            for (int u = 0; u < kU; ++u) {
-                if (bi[u] < 0) continue;
-                Take t[kStreams];
-                if (probe.finish(wl[u], st[u], t, false)) { touch = true; mask |= 1ULL << bi[u]; }
-                for (int k = 0; k < kStreams; ++k)
-                    if (t[k].take) { ++count; dsum += t[k].deg; }
-            }
-        }
-        return;
-    }
-    int64_t wd = first;
-    int idx = 0;
-    for (; wd < end; wd += kU * kWavesPerBlock, idx += kU) {
-        typename Probe::State st[kU];
-        bool in[kU];
-#pragma unroll
-        for (int u = 0; u < kU; ++u) {
-            in[u] = wd + u * kWavesPerBlock < end;                // wave-uniform
-            probe.stage1(in[u] ? wd + u * kWavesPerBlock : first, st[u]);
-        }
-#pragma unroll
-        for (int u = 0; u < kU; ++u) probe.stage2(in[u] ? wd + u * kWavesPerBlock : first, st[u]);
-#pragma unroll
-        for (int u = 0; u < kU; ++u) {
-            if (!in[u]) continue;
-            Take t[kStreams];
-            if (probe.finish(wd + u * kWavesPerBlock, st[u], t, false)) { touch = true; if (idx + u < 64) mask |= 1ULL << (idx + u); }
-            for (int k = 0; k < kStreams; ++k)
-                if (t[k].take) { ++count; dsum += t[k].deg; }
+            visit(wl, bi, st);
         }
     }
 }
+// Pass 1 over the live words: the takes counted, the touched words of a wave of <= 64 words
+// flagged for pass 2.
+template <int kStreams, class Probe, int kU = kExtractUnroll>
+__device__ __forceinline__ void extract_count_staged(int64_t first, int64_t end, const Probe& probe, int64_t& count,
+                                                     int64_t& dsum, unsigned long long& mask, bool& touch) {
+    const int64_t nwords = end > first ? (end - first + kWavesPerBlock - 1) / kWavesPerBlock : 0;
+    live_words<Probe, kU>(first, nwords, probe, [&](const int64_t* wl, const int* bi, const typename Probe::State* st) {
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            if (bi[u] < 0) continue;
+            Take t[kStreams];
+            if (probe.finish(wl[u], st[u], t, false)) { touch = true; if (bi[u] < 64) mask |= 1ULL << bi[u]; }
+            for (int k = 0; k < kStreams; ++k)
+                if (t[k].take) { ++count; dsum += t[k].deg; }
+        }
+    });
+}
+// Pass 2: the flagged words in order (a wave of <= 64 words), else the live words again.
 template <int kStreams, class Probe, class Emit, int kU = kExtractUnroll>
 __device__ __forceinline__ void extract_write_staged(int64_t first, int64_t end, unsigned long long mask, const Probe& probe,
                                                      const Emit& emit) {
     const int64_t nwords = end > first ? (end - first + kWavesPerBlock - 1) / kWavesPerBlock : 0;
-    const bool all = nwords > 64;
-    int64_t next = 0;
-    for (;;) {
+    if (nwords > 64) {
+        live_words<Probe, kU>(first, nwords, probe, [&](const int64_t* wl, const int* bi, const typename Probe::State* st) {
+            Take t[kU][kStreams];
+#pragma unroll
+            for (int u = 0; u < kU; ++u)
+                if (bi[u] >= 0) probe.finish(wl[u], st[u], t[u], true);
+#pragma unroll
+            for (int u = 0; u < kU; ++u)
+                if (bi[u] >= 0) emit(t[u]);
+        });
+        return;
+    }
+    while (mask) {                            // wave-uniform
         int64_t wl[kU];
-        bool any = false;
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
             wl[u] = -1;
-            if (all) {
-                if (next < nwords) wl[u] = first + (next++) * kWavesPerBlock;
-            } else if (mask) {
+            if (mask) {
                 const int b = __ffsll(static_cast<long long>(mask)) - 1;
                 mask &= mask - 1;
                 wl[u] = first + static_cast<int64_t>(b) * kWavesPerBlock;
             }
-            any |= wl[u] >= 0;
         }
-        if (!any) break;                      // wave-uniform
         typename Probe::State st[kU];
 #pragma unroll
         for (int u = 0; u < kU; ++u) probe.stage1(wl[u] >= 0 ? wl[u] : first, st[u]);
