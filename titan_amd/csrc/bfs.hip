@@ -165,7 +165,7 @@ __global__ void __launch_bounds__(kBlock) bfs_queue(View push, int64_t n, const 
         t[0] = {take, static_cast<int32_t>(v), take ? push_degree(push, v) : 0};
         return __ballot(take) != 0;
     };
-    chunk_extract<1>(words, probe, qn, qdeg, cnt);
+    chunk_extract_live<1>(words, [&](int64_t wd) { return fb[wd] != 0; }, probe, qn, qdeg, cnt);
 }
 
 // Partitioned levels with device-resident counts: {qlen, push entries} for the caller's

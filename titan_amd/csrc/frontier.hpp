@@ -385,6 +385,101 @@ __device__ __forceinline__ void chunk_extract(int64_t words, const Probe& probe,
     });
 }
 
+// chunk_extract for a sparse bitmap: live(wd) says whether word wd can take anything (a
+// cheap load), one word a lane per 64-word window, and both passes probe the live words only
+// (the queue after a bottom-up level: the frontier is a few thousand vertices in 16 M, and a
+// wave's 32 words cost 8 dependent round trips a pass at 4 in flight).
+template <int kU, class Live, class Visit>
+__device__ __forceinline__ void live_words_plain(int64_t first, int64_t nwords, const Live& live, const Visit& visit) {
+    for (int64_t w0 = 0; w0 < nwords; w0 += 64) {                // wave-uniform
+        const int64_t base = first + w0 * kWavesPerBlock;
+        const int64_t nw = nwords - w0 < 64 ? nwords - w0 : 64;
+        const bool in = lane() < nw;
+        unsigned long long lv = __ballot(in && live(in ? base + static_cast<int64_t>(lane()) * kWavesPerBlock : first));
+        while (lv) {                                              // wave-uniform
+            int64_t wl[kU];
+            int bi[kU];
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                bi[u] = -1;
+                wl[u] = first;
+                if (lv) {
+                    const int b = __ffsll(static_cast<long long>(lv)) - 1;
+                    lv &= lv - 1;
+                    bi[u] = static_cast<int>(w0) + b;
+                    wl[u] = base + static_cast<int64_t>(b) * kWavesPerBlock;
+                }
+            }
+            visit(wl, bi);
+        }
+    }
+}
+template <int kStreams, class Live, class Probe>
+__device__ __forceinline__ void chunk_extract_live(int64_t words, const Live& live, const Probe& probe,
+                                                   int32_t* __restrict__ qn, int64_t* __restrict__ qdeg, Counters* cnt) {
+    __shared__ unsigned long long s_cnt[kWavesPerBlock], s_mf[kWavesPerBlock], s_base;
+    const int64_t per = ((words + gridDim.x - 1) / gridDim.x + kWavesPerBlock - 1) / kWavesPerBlock * kWavesPerBlock;
+    const int64_t w0 = static_cast<int64_t>(blockIdx.x) * per;
+    const int64_t w1 = min(words, w0 + per);
+    const int wave = threadIdx.x >> 6;
+    const unsigned long long below = (1ULL << lane()) - 1ULL;
+    const int64_t first = w0 + wave;
+    const int64_t nwords = w1 > first ? (w1 - first + kWavesPerBlock - 1) / kWavesPerBlock : 0;
+    int64_t count = 0, dsum = 0;
+    unsigned long long mask = 0;
+    bool touch = false;
+    live_words_plain<kExtractUnroll>(first, nwords, live, [&](const int64_t* wl, const int* bi) {
+        Take t[kExtractUnroll][kStreams];
+        bool r[kExtractUnroll];
+#pragma unroll
+        for (int u = 0; u < kExtractUnroll; ++u) r[u] = bi[u] >= 0 && probe(wl[u], t[u], false);
+#pragma unroll
+        for (int u = 0; u < kExtractUnroll; ++u) {
+            if (bi[u] < 0) continue;
+            if (r[u]) { touch = true; if (bi[u] < 64) mask |= 1ULL << bi[u]; }
+            for (int k = 0; k < kStreams; ++k)
+                if (t[u][k].take) { ++count; dsum += t[u][k].deg; }
+        }
+    });
+    unsigned long long c = static_cast<unsigned long long>(count), m = static_cast<unsigned long long>(dsum);
+    for (int o = 32; o > 0; o >>= 1) { c += __shfl_xor(c, o, 64); m += __shfl_xor(m, o, 64); }
+    if (lane() == 0) { s_cnt[wave] = c; s_mf[wave] = m; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0, mm = 0;
+        for (int w = 0; w < kWavesPerBlock; ++w) { const unsigned long long x = s_cnt[w]; s_cnt[w] = t; t += x; mm += s_mf[w]; }
+        s_base = t ? atomicAdd(&cnt->qlen, t) : 0ULL;
+        if (mm) atomicAdd(&cnt->mf, mm);
+    }
+    __syncthreads();
+    if (!touch) return;                                      // wave-uniform
+    unsigned long long cursor = s_base + s_cnt[wave];
+    const auto emit = [&](const Take* t) {
+        for (int k = 0; k < kStreams; ++k) {
+            const unsigned long long bm = __ballot(t[k].take);
+            if (t[k].take) {
+                const unsigned long long slot = cursor + __popcll(bm & below);
+                qn[slot] = t[k].entry;
+                qdeg[slot] = t[k].deg;
+            }
+            cursor += __popcll(bm);
+        }
+    };
+    if (nwords <= 64) {
+        extract_write<kStreams>(first, w1, mask, probe, emit);
+        return;
+    }
+    live_words_plain<kExtractUnroll>(first, nwords, live, [&](const int64_t* wl, const int* bi) {
+        Take t[kExtractUnroll][kStreams];
+#pragma unroll
+        for (int u = 0; u < kExtractUnroll; ++u)
+            if (bi[u] >= 0) probe(wl[u], t[u], true);
+#pragma unroll
+        for (int u = 0; u < kExtractUnroll; ++u)
+            if (bi[u] >= 0) emit(t[u]);
+    });
+}
+
 // Grid for chunk_extract: >= 64 words per block, at most 2048 blocks.
 inline int extract_grid(int64_t words) {
     const int64_t g = (words + 63) / 64;
