@@ -798,6 +798,7 @@ int run_bfs(tgo_ctx* ctx, int64_t seed, int max_depth, int scope) {
     int levels = 0;
     if (seed >= 0) {
         HIP_TRY(k_bfs_seed(push, s.level, s.vb, s.fb, s.q[0], s.qdeg, seed, st));
+        HIP_TRY(k_level_prep(s.cnt, s.nb, words, s.qdeg + 1, st));   // level 0: counters, nb, scan tail
         int64_t qlen = 1;
         int cur = 0;
         bool bottom_up = false;
@@ -827,24 +828,27 @@ int run_bfs(tgo_ctx* ctx, int64_t seed, int max_depth, int scope) {
             }
             if (!bottom_up && static_cast<double>(mf) > static_cast<double>(mu) / alpha) bottom_up = true;
             else if (bottom_up && static_cast<double>(qlen) < static_cast<double>(n) / beta) bottom_up = false;
+            // every level starts with zero counters, a clear nb and qdeg[qlen] = 0: level_turn
+            // at the end of the previous level (the first: the level_prep before the loop)
             if (!bottom_up && !queued) {    // after bottom-up levels: queue the frontier bitmap
-                HIP_TRY(k_level_prep(s.cnt, nullptr, 0, nullptr, st));
                 HIP_TRY(k_bfs_queue(push, g.n_active, s.fb, s.q[cur], s.qdeg, s.cnt, st));
+                HIP_TRY(k_level_prep(s.cnt, nullptr, 0, nullptr, st));   // the queue's counts out
             }
             queued = !bottom_up;
             DevSpan span(st, "bfs.level", {"level", L}, {"bottom_up", bottom_up ? 1 : 0});
             if (bottom_up) {
-                HIP_TRY(k_level_prep(s.cnt, s.nb, words, nullptr, st));
                 // words past n_active hold only entry-less vertices: nothing to find there
                 HIP_TRY(k_bu_step(pull, push, g.n_active, s.fb, s.vb, s.nb, s.level, s.cnt, L + 1, st));
             } else {
-                HIP_TRY(k_level_prep(s.cnt, s.nb, words, s.qdeg + qlen, st));
                 HIP_TRY(scan_exclusive_i64(s.cub_tmp, s.cub_bytes, s.qdeg, s.qpre, qlen + 1, st));
                 // qdeg is reused for the next queue's degrees after the scan consumed it
                 HIP_TRY(k_td_expand(push, s.q[cur], s.qpre, qlen, s.level, s.vb, s.nb, s.q[cur ^ 1], s.qdeg, s.cnt, L + 1, st));
             }
             span.end();
-            int rc = read_counters(ctx);
+            // the counters to the host, then the next level's prep (fb, consumed, is its nb)
+            const unsigned long long seq = ++s.pub_seq;
+            HIP_TRY(k_level_turn(s.cnt, s.hcnt_dev, seq, s.fb, words, s.qdeg, st));
+            int rc = wait_publish(ctx, seq);
             if (rc) return rc;
             qlen = static_cast<int64_t>(s.hcnt->qlen);
             mf = static_cast<int64_t>(s.hcnt->mf);

@@ -445,6 +445,35 @@ __global__ void level_prep(Counters* cnt, uint64_t* nb, int64_t words, int64_t* 
     if (cnt && i0 < kCounterWords) reinterpret_cast<unsigned long long*>(cnt)[i0] = 0;
     if (tail && i0 == 0) *tail = 0;
 }
+// The end of a one-GPU BFS level in one launch (publish_counters + the next level's
+// level_prep): block 0 publishes the counters to the host-mapped page, then zeroes them and the
+// scan tail qdeg[qlen] at the new queue length; every block clears `clear` (the frontier bitmap
+// the level just consumed, the next level's nb after the swap).  One dispatch fewer per level.
+__global__ void level_turn(Counters* c, unsigned long long* host, unsigned long long seq, uint64_t* __restrict__ clear,
+                           int64_t words, int64_t* __restrict__ qdeg) {
+    const int64_t i0 = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    for (int64_t i = i0; i < words; i += static_cast<int64_t>(gridDim.x) * blockDim.x) clear[i] = 0;
+    if (blockIdx.x != 0) return;
+    const int i = threadIdx.x;
+    unsigned long long* w = reinterpret_cast<unsigned long long*>(c);
+    const unsigned long long qlen = c->qlen;
+    if (i < kCounterWords) {
+        __hip_atomic_store(&host[i], w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __threadfence_system();
+    }
+    __syncthreads();                          // every word read before any is zeroed
+    if (i == 0) {
+        qdeg[qlen] = 0;
+        __hip_atomic_store(&host[kCounterWords], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    if (i < kCounterWords) w[i] = 0;
+}
+hipError_t k_level_turn(Counters* c, unsigned long long* host, unsigned long long seq, uint64_t* clear, int64_t words,
+                        int64_t* qdeg, hipStream_t s) {
+    if (kBlock < kCounterWords) return hipErrorInvalidValue;
+    level_turn<<<grid_for(std::max<int64_t>(words, kCounterWords)), kBlock, 0, s>>>(c, host, seq, clear, words, qdeg);
+    return hipGetLastError();
+}
 hipError_t k_publish_counters(const Counters* c, unsigned long long* host, unsigned long long seq, hipStream_t s) {
     publish_counters<<<1, 64, 0, s>>>(c, host, seq);
     return hipGetLastError();

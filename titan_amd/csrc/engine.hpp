@@ -633,6 +633,8 @@ hipError_t k_publish_counters(const Counters* c, unsigned long long* host, unsig
 // The delta loop's done / err / spill flags to host-mapped words 0..2 and the sequence number.
 hipError_t k_ds_publish(const DsLoop* L, unsigned long long* host, unsigned long long seq, hipStream_t s);
 hipError_t k_publish_words(const int64_t* src, int count, unsigned long long* host, unsigned long long seq, hipStream_t s);
+hipError_t k_level_turn(Counters* c, unsigned long long* host, unsigned long long seq, uint64_t* clear, int64_t words,
+                        int64_t* qdeg, hipStream_t s);
 // One launch instead of per-level memsets: zero the counters (cnt may be null), the next
 // frontier bitmap (words, may be 0) and the scan tail slot (may be null).
 hipError_t k_level_prep(Counters* cnt, uint64_t* nb, int64_t words, int64_t* tail, hipStream_t s);
