@@ -819,10 +819,12 @@ int run_bfs(tgo_ctx* ctx, int64_t seed, int max_depth, int scope) {
         int64_t mf = -1, mu = total_push;
         bool queued = true;         // q[cur] holds the frontier (bottom-up levels only count it)
         for (int L = 0; L < max_depth && qlen > 0; ++L) {
-            if (mf < 0) {   // degree of the seed
-                int64_t d = 0;
-                HIP_TRY(hipMemcpyAsync(&d, s.qdeg, sizeof(int64_t), hipMemcpyDeviceToHost, st));
-                HIP_TRY(hipStreamSynchronize(st));
+            if (mf < 0) {   // degree of the seed, through the mapped counter page (a copy and a
+                            // stream synchronisation cost ~30 us before the first level)
+                const unsigned long long seq = ++s.pub_seq;
+                HIP_TRY(k_publish_words(s.qdeg, 1, s.hcnt_dev, seq, st));
+                if (int rc = wait_publish(ctx, seq)) return rc;
+                const int64_t d = static_cast<int64_t>(reinterpret_cast<volatile unsigned long long*>(s.hcnt)[0]);
                 mf = d;
                 mu -= d;
             }
