@@ -254,37 +254,21 @@ __device__ __forceinline__ void extract_write(int64_t first, int64_t end, unsign
 // The wave's words in windows of 64: one word a lane asks which can take anything
 // (Probe::live, one load round trip a window), and the stages run on those only — a sparse
 // scan (the tail of a run: a few pending vertices in 16 M) costs a round trip a window instead
-// of one per kU words.  live_words calls visit(wl, bi, st) per kU live words (bi: index within
-// the wave's words, -1 for an unused slot, whose wl is `first`).
+// of one per kU words.  live_words calls visit(wl, bi, st) per kU live words with their
+// stages 1 and 2 issued (live_words_plain below: bi = index within the wave's words, -1 for an
+// unused slot, whose wl is `first`).
+template <int kU, class Live, class Visit>
+__device__ __forceinline__ void live_words_plain(int64_t first, int64_t nwords, const Live& live, const Visit& visit);
 template <class Probe, int kU, class Visit>
 __device__ __forceinline__ void live_words(int64_t first, int64_t nwords, const Probe& probe, const Visit& visit) {
-    for (int64_t w0 = 0; w0 < nwords; w0 += 64) {                // wave-uniform
-        const int64_t base = first + w0 * kWavesPerBlock;
-        const int64_t nw = nwords - w0 < 64 ? nwords - w0 : 64;
-        const bool in = lane() < nw;
-        unsigned long long live = __ballot(in && probe.live(in ? base + static_cast<int64_t>(lane()) * kWavesPerBlock : first));
-        while (live) {                                            // wave-uniform
-            int64_t wl[kU];
-            int bi[kU];
+    live_words_plain<kU>(first, nwords, [&](int64_t wd) { return probe.live(wd); }, [&](const int64_t* wl, const int* bi) {
+        typename Probe::State st[kU];
 #pragma unroll
-            for (int u = 0; u < kU; ++u) {
-                bi[u] = -1;
-                wl[u] = first;
-                if (live) {
-                    const int b = __ffsll(static_cast<long long>(live)) - 1;
-                    live &= live - 1;
-                    bi[u] = static_cast<int>(w0) + b;
-                    wl[u] = base + static_cast<int64_t>(b) * kWavesPerBlock;
-                }
-            }
-            typename Probe::State st[kU];
+        for (int u = 0; u < kU; ++u) probe.stage1(wl[u], st[u]);
 #pragma unroll
-            for (int u = 0; u < kU; ++u) probe.stage1(wl[u], st[u]);
-#pragma unroll
-            for (int u = 0; u < kU; ++u) probe.stage2(wl[u], st[u]);
-            visit(wl, bi, st);
-        }
-    }
+        for (int u = 0; u < kU; ++u) probe.stage2(wl[u], st[u]);
+        visit(wl, bi, st);
+    });
 }
 // Pass 1 over the live words: the takes counted, the touched words of a wave of <= 64 words
 // flagged for pass 2.
@@ -385,10 +369,7 @@ __device__ __forceinline__ void chunk_extract(int64_t words, const Probe& probe,
     });
 }
 
-// chunk_extract for a sparse bitmap: live(wd) says whether word wd can take anything (a
-// cheap load), one word a lane per 64-word window, and both passes probe the live words only
-// (the queue after a bottom-up level: the frontier is a few thousand vertices in 16 M, and a
-// wave's 32 words cost 8 dependent round trips a pass at 4 in flight).
+// The live words of a wave, kU at a time (see live_words).
 template <int kU, class Live, class Visit>
 __device__ __forceinline__ void live_words_plain(int64_t first, int64_t nwords, const Live& live, const Visit& visit) {
     for (int64_t w0 = 0; w0 < nwords; w0 += 64) {                // wave-uniform
@@ -414,6 +395,10 @@ __device__ __forceinline__ void live_words_plain(int64_t first, int64_t nwords, 
         }
     }
 }
+// chunk_extract for a sparse bitmap: live(wd) says whether word wd can take anything (a
+// cheap load), one word a lane per 64-word window, and both passes probe the live words only
+// (the queue after a bottom-up level: the frontier is a few thousand vertices in 16 M, and a
+// wave's 32 words cost 8 dependent round trips a pass at 4 in flight).
 template <int kStreams, class Live, class Probe>
 __device__ __forceinline__ void chunk_extract_live(int64_t words, const Live& live, const Probe& probe,
                                                    int32_t* __restrict__ qn, int64_t* __restrict__ qdeg, Counters* cnt) {
